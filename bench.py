@@ -1,0 +1,133 @@
+#!/usr/bin/env python
+"""Headline benchmark: GBM train rows/sec (100 trees, depth 6) on HIGGS-11M-shaped data.
+
+BASELINE.json metric: "GBM train rows/sec (100 trees, depth 6) on HIGGS-11M at 1/2/4/8 MI355X".
+Data: synthetic HIGGS-shaped matrix (11,000,000 rows x 28 float features, binary label, ~53 %
+positives; 21 "low-level" features incl. discrete b-tag-like columns + 7 "high-level" nonlinear
+combinations) generated on device from a fixed seed — no dataset download is possible here.
+
+Model config: H2O GBM, distribution=bernoulli, ntrees=100, max_depth=6, min_rows=10, learn_rate=0.1,
+sample_rate=1, histogram_type=QuantilesGlobal (255 global quantile bins), fp32 compute.
+
+A "step" = one boosting iteration (one full tree: gradients, histograms, splits, partition, leaf
+values, prediction update). The timed region covers exactly K steps between barrier+synchronize.
+``value`` = rows/sec of a 100-tree training = N_total / (100 * ms_per_step / 1000), whole job.
+Multi-GPU (torchrun): rows are sharded over ranks (strong scaling: total rows fixed); per-level
+histograms and leaf sums are all-reduced over RCCL.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+
+def make_higgs_like(n: int, seed: int, device) -> tuple:
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    F = 28
+    X = torch.empty(F, n, device=device, dtype=torch.float32)
+    # 21 low-level kinematic features: momenta (lognormal-ish), angles (uniform), b-tags (discrete)
+    for f in range(21):
+        kind = f % 4
+        if kind == 0:
+            X[f] = torch.exp(0.5 * torch.randn(n, generator=g, device=device))
+        elif kind == 1:
+            X[f] = torch.randn(n, generator=g, device=device)
+        elif kind == 2:
+            X[f] = (torch.rand(n, generator=g, device=device) * 2 - 1) * 3.1416
+        else:
+            X[f] = torch.randint(0, 3, (n,), generator=g, device=device).float() * 1.0865
+    # 7 high-level features: nonlinear combinations (invariant masses)
+    for j in range(7):
+        a, b, c = X[(3 * j) % 21], X[(3 * j + 1) % 21], X[(3 * j + 5) % 21]
+        X[21 + j] = torch.sqrt(torch.abs(a * b + 0.5 * c * c) + 0.1) + 0.05 * torch.randn(n, generator=g, device=device)
+    logit = (0.9 * X[21] - 0.7 * X[22] + 0.5 * X[23] * X[24] - 0.4 * torch.sin(X[2]) * X[1]
+             + 0.3 * X[3] - 0.35 * (X[25] > 1.2).float() + 0.25 * X[0] * X[5] - 0.3)
+    y = (torch.rand(n, generator=g, device=device) < torch.sigmoid(logit)).float()
+    return X, y
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--rows", type=int, default=11_000_000)
+    ap.add_argument("--depth", type=int, default=6)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
+
+    from llama_github_io_amd.models.base import DataInfo
+    from llama_github_io_amd.models.gbm import GBMTrainer
+    from llama_github_io_amd.parallel import collectives as coll
+
+    n_total = args.rows
+    n_local = n_total // world + (1 if rank < n_total % world else 0)
+    X, y = make_higgs_like(n_local, 1234 + 7919 * rank, dev)
+    F = X.shape[0]
+    info = DataInfo([f"x{i}" for i in range(F)], np.zeros(F, np.int32), [None] * F, "y", ["0", "1"])
+    params = dict(ntrees=args.warmup + args.steps, max_depth=args.depth, min_rows=10, learn_rate=0.1, seed=42,
+                  distribution="bernoulli", histogram_type="QuantilesGlobal")
+
+    # the trainer exposes a per-tree hook so the bench can time exactly K steps after W warmup steps
+    times = {}
+
+    class TimedGBM(GBMTrainer):
+        def _prepare(self, t, k):
+            if t == args.warmup and k == 0:
+                coll.barrier()
+                if dev.type == "cuda":
+                    torch.cuda.synchronize()
+                times["t0"] = time.perf_counter()
+            return super()._prepare(t, k)
+
+        def _finish(self, model, built):
+            coll.barrier()
+            if dev.type == "cuda":
+                torch.cuda.synchronize()
+            times["t1"] = time.perf_counter()
+
+    tr = TimedGBM(params)
+    model = tr.fit(X, y, None, None, info)
+    dt = times["t1"] - times["t0"]
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        import torch.distributed as dist
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    ms_per_step = dt * 1000.0 / args.steps
+    rows_per_sec = n_total / (100 * ms_per_step / 1000.0)
+    tm = model.output["training_metrics"]
+    if rank == 0:
+        print(json.dumps({
+            "metric": "GBM train rows/sec (100 trees, depth 6) on HIGGS-11M",
+            "value": round(rows_per_sec, 1), "unit": "rows/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "fp32", "data": "synthetic HIGGS-shaped 11M x 28",
+            "config": {"model": "GBM bernoulli ntrees=100 max_depth=6 min_rows=10 lr=0.1 QuantilesGlobal(255 bins)",
+                       "global_batch": n_total, "seq_len": None, "parallelism": f"dp{world} (row-sharded, hist all-reduce)",
+                       "rows": n_total, "features": F, "train_auc_after_all_trees": tm.get("AUC") if tm else None},
+        }), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

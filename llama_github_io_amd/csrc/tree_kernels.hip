@@ -1,0 +1,973 @@
+// Histogram tree engine for GBM / DRF / XGBoost / IsolationForest on MI355X (gfx950).
+//
+// Reference behaviour (what these kernels replace):
+//   h2o-algos/src/main/java/hex/tree/ScoreBuildHistogram2.java  (per-chunk histogram accumulation)
+//   h2o-algos/src/main/java/hex/tree/DHistogram.java            (w, wY, wYY bins + NA bin)
+//   h2o-algos/src/main/java/hex/tree/DTree.java:984-1487         (findBestSplitPoint)
+//   h2o-algos/src/main/java/hex/tree/gbm/GBM.java               (leaf Newton sums, prediction update)
+//
+// Design (MI355X-first, not a port):
+//   * features are pre-binned once into a row-major uint8 matrix (bin 255 = NA), so a row is Fp bytes.
+//   * rows are PHYSICALLY partitioned by tree node every level (stable two-pass partition: k_count ->
+//     k_plan scan -> k_move), so every histogram pass streams contiguous rows of ONE node and the
+//     per-node histogram lives privately in LDS (32 features x 256 bins x {w, wY} fp32 = 66 KB).
+//   * only the smaller child of each split is histogrammed (fused into the partition kernel); the
+//     sibling comes from parent - child (k_subtract), in fp64.
+//   * split search, child planning, leaf numbering and tile planning all stay on device: a whole
+//     tree is a fixed launch sequence with no host synchronisation.
+//   * rows reaching a leaf write their leaf id in ORIGINAL row order (scatter through ridx) and stop
+//     moving; the prediction update is then a coalesced elementwise op.
+//   * wave64: 8 lanes own one row (one 32-bit word = 4 bins each), a wave covers 8 rows, so lanes of a
+//     wave hit 8 different feature sub-histograms (few same-address LDS atomic collisions).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define NBIN 256
+#define NA_BIN 255
+#define FTILE 32                // features per LDS histogram tile
+#define HSTRIDE (2 * NBIN + 2)  // floats per feature row in LDS (+2 pad: rotates banks per feature)
+#define BLK 512
+#define TILE 2048               // rows per work tile
+#define LPR 8                   // lanes per row
+#define RPI (BLK / LPR)         // rows per iteration (64)
+
+struct Node {      // one active node of a level (rows [start, start+len) of the level's buffer)
+  int start, len, build, parent, sib, pad0, pad1, pad2;
+};
+
+struct Dec {       // split decision (80 B)
+  int feat;        // -1: no split (terminal)
+  int bin;         // numeric: data bins < bin go left
+  int na_left;     // NA rows go left?
+  int is_cat;      // categorical: bitset `bits` over bins -> 1 = left
+  unsigned bits[8];
+  double gain;     // improvement (for variable importance)
+  double wl, wr;   // weighted row counts left/right
+  float predl, predr;
+};
+
+struct Cand {      // best split of one (node, feature)
+  double expl;     // explained "variance" of the split (larger is better)
+  double gain;
+  double wl, wr;
+  float predl, predr;
+  int bin, na_left, valid, is_cat;
+  unsigned bits[8];
+};
+
+struct SplitParams {
+  double min_w;            // min_rows (SE mode) / min_child_weight (Newton mode)
+  double min_split_improvement;
+  double lambda, alpha, gamma;
+  int mode;                // 0 = squared error (GBM/DRF, H2O semantics), 1 = Newton (XGBoost), 2 = random (IsoForest)
+  int random_split;        // extremely randomized / isolation: pick a random threshold
+  unsigned long long seed;
+};
+
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ unsigned long long splitmix64(unsigned long long x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+__device__ __forceinline__ bool dec_go_left(const Dec* d, int b) {
+  // d points to global memory or LDS: the runtime-indexed bitset must not live in registers (scratch)
+  if (b == NA_BIN) return d->na_left != 0;
+  if (d->is_cat) return (d->bits[b >> 5] >> (b & 31)) & 1u;
+  return b < d->bin;
+}
+
+// node index of tile t: largest i with tile_prefix[i] <= t
+__device__ __forceinline__ int find_node(const int* __restrict__ tp, int n, int t) {
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    int mid = (lo + hi + 1) >> 1;
+    if (tp[mid] <= t) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ int wave_sum_i(int v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Block-reduce 4 doubles (BLK threads), result valid in thread 0.
+__device__ void block_sum4(double v[4], double* scratch /* >= 4*(BLK/64) */) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int k = 0; k < 4; ++k) v[k] = wave_sum_d(v[k]);
+  __syncthreads();
+  if (lane == 0) for (int k = 0; k < 4; ++k) scratch[k * 16 + wid] = v[k];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 0; k < 4; ++k) { double s = 0; for (int w = 0; w < nw; ++w) s += scratch[k * 16 + w]; v[k] = s; }
+  }
+  __syncthreads();
+}
+
+// ------------------------------------------------------------------------------------------------
+// LDS histogram helpers. Layout: h[f_local * HSTRIDE + 2*bin + {0: w, 1: wY}], extra[f_local] = NA wYY,
+// extra[FTILE] = node wYY (accumulated separately in registers).
+__device__ __forceinline__ void lds_zero(float* h, int nfloats) {
+  for (int i = threadIdx.x; i < nfloats; i += blockDim.x) h[i] = 0.f;
+}
+
+__device__ void flush_hist(const float* h, const float* nayy, double node_wyy, int ftile, int F,
+                           double* __restrict__ slot, int slot_doubles) {
+  // slot layout: [F][256][2] doubles, then [F] NA-wYY, then [1] node wYY
+  const int f0 = ftile * FTILE;
+  const int nf = min(FTILE, F - f0);
+  for (int i = threadIdx.x; i < nf * 2 * NBIN; i += blockDim.x) {
+    const int fl = i / (2 * NBIN), r = i - fl * 2 * NBIN;
+    const float v = h[fl * HSTRIDE + r];
+    if (v != 0.f) atomicAdd(slot + (size_t)(f0 + fl) * 2 * NBIN + r, (double)v);
+  }
+  for (int i = threadIdx.x; i < nf; i += blockDim.x) {
+    const float v = nayy[i];
+    if (v != 0.f) atomicAdd(slot + (size_t)F * 2 * NBIN + f0 + i, (double)v);
+  }
+  if (threadIdx.x == 0 && ftile == 0 && node_wyy != 0.0)
+    atomicAdd(slot + (size_t)F * 2 * NBIN + F, node_wyy);
+}
+
+// accumulate one row-word (4 bins) into the LDS tile histogram
+__device__ __forceinline__ void hist_word(float* h, float* nayy, unsigned word, int wl /*word index in tile*/,
+                                          int f_abs0, int F, float a, float b, float yy) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int fl = wl * 4 + k;
+    if (f_abs0 + k < F) {
+      const int bin = (word >> (8 * k)) & 0xFF;
+      float* p = h + fl * HSTRIDE + 2 * bin;
+      atomicAdd(p, a);
+      atomicAdd(p + 1, b);
+      if (bin == NA_BIN) atomicAdd(nayy + fl, yy);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_hist_build: histograms of all nodes with build==1 of a level (root, or F>32 path).
+// grid = (G, n_ftiles); each block takes a contiguous range of tiles so it flushes rarely.
+__global__ __launch_bounds__(BLK) void k_hist_build(
+    const uint8_t* __restrict__ bins, int stride /*bytes per row, multiple of 4*/,
+    const float4* __restrict__ aux, const Node* __restrict__ nodes, const int* __restrict__ tile_prefix,
+    const int* __restrict__ meta /*[0]=n_nodes [1]=n_tiles*/, int F, double* __restrict__ hist, int slot_doubles) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* h = smem;                         // FTILE * HSTRIDE
+  float* nayy = smem + FTILE * HSTRIDE;    // FTILE
+  double* red = (double*)(nayy + FTILE);   // 64 doubles scratch
+
+  const int n_nodes = meta[0], n_tiles = meta[1];
+  if (n_nodes <= 0 || n_tiles <= 0) return;
+  const int per = (n_tiles + gridDim.x - 1) / gridDim.x;
+  const int t0 = blockIdx.x * per, t1 = min(n_tiles, t0 + per);
+  if (t0 >= t1) return;
+  const int ftile = blockIdx.y;
+  const int W = stride >> 2;
+  const int g = threadIdx.x / LPR, j = threadIdx.x % LPR;
+  const int wabs = ftile * LPR + j;        // absolute word index of this lane
+  const unsigned* bins32 = (const unsigned*)bins;
+
+  int cur = -1;
+  double wyy = 0.0;
+  for (int t = t0; t < t1; ++t) {
+    const int node = find_node(tile_prefix, n_nodes, t);
+    const Node nd = nodes[node];
+    if (!nd.build) continue;
+    if (node != cur) {
+      if (cur >= 0) {
+        double v[4] = {wyy, 0, 0, 0};
+        block_sum4(v, red);
+        __syncthreads();
+        flush_hist(h, nayy, v[0], ftile, F, hist + (size_t)cur * slot_doubles, slot_doubles);
+        __syncthreads();
+      }
+      lds_zero(smem, FTILE * HSTRIDE + FTILE);
+      wyy = 0.0;
+      cur = node;
+      __syncthreads();
+    }
+    const int r0 = nd.start + (t - tile_prefix[node]) * TILE;
+    const int r1 = min(r0 + TILE, nd.start + nd.len);
+    for (int row = r0 + g; row < r1; row += RPI) {
+      const float4 ax = aux[row];
+      const float yy = ax.x > 0.f ? ax.y * ax.y / ax.x : 0.f;
+      if (j == 0 && ftile == 0) wyy += yy;
+      if (wabs < W) {
+        const unsigned word = bins32[(size_t)row * W + wabs];
+        hist_word(h, nayy, word, j, wabs * 4, F, ax.x, ax.y, yy);
+      }
+    }
+  }
+  if (cur >= 0) {
+    double v[4] = {wyy, 0, 0, 0};
+    block_sum4(v, red);
+    __syncthreads();
+    flush_hist(h, nayy, v[0], ftile, F, hist + (size_t)cur * slot_doubles, slot_doubles);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_split_find: best split point per (node, feature). grid = (C, F), block 256 (thread = bin).
+__global__ __launch_bounds__(256) void k_split_find(
+    const double* __restrict__ hist, int slot_doubles, const int* __restrict__ meta, int F,
+    const int* __restrict__ nbins_f, const int* __restrict__ iscat_f, const int* __restrict__ mono_f,
+    SplitParams p, int level, Cand* __restrict__ cand) {
+  const int node = blockIdx.x, f = blockIdx.y, t = threadIdx.x;
+  if (node >= meta[0]) return;
+  __shared__ double sw[256], swy[256], skey[256];
+  __shared__ int sidx[256];
+  __shared__ double best_e[256];
+  __shared__ int best_i[256];
+
+  const double* slot = hist + (size_t)node * slot_doubles;
+  const double* h = slot + (size_t)f * 2 * NBIN;
+  const int nb = nbins_f[f];
+  const bool cat = iscat_f[f] != 0;
+  const int mono = mono_f ? mono_f[f] : 0;
+  const double wNA = h[2 * NA_BIN], wyNA = h[2 * NA_BIN + 1];
+  const double naYY = slot[(size_t)F * 2 * NBIN + f];
+  const double wYY = slot[(size_t)F * 2 * NBIN + F];
+
+  double w = 0, wy = 0;
+  if (t < nb && t < NA_BIN) { w = h[2 * t]; wy = h[2 * t + 1]; }
+  sidx[t] = t;
+  if (cat) {
+    // sort bins by mean response (empty bins first, out-of-range bins last) — DTree.java:1006
+    skey[t] = (t < nb) ? (w > 0 ? wy / w : -1.0e308) : 1.0e308;
+    sw[t] = w; swy[t] = wy;
+    __syncthreads();
+    for (int k = 2; k <= 256; k <<= 1) {
+      for (int jj = k >> 1; jj > 0; jj >>= 1) {
+        const int ixj = t ^ jj;
+        if (ixj > t) {
+          const bool up = ((t & k) == 0);
+          const double a = skey[t], b = skey[ixj];
+          const int ia = sidx[t], ib = sidx[ixj];
+          const bool gt = (a > b) || (a == b && ia > ib);
+          if (gt == up) { skey[t] = b; skey[ixj] = a; sidx[t] = ib; sidx[ixj] = ia; }
+        }
+        __syncthreads();
+      }
+    }
+    w = sw[sidx[t]]; wy = swy[sidx[t]];
+    __syncthreads();
+  }
+  // inclusive scan of (w, wy) in sorted order
+  sw[t] = w; swy[t] = wy;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {
+    double a = 0, b = 0;
+    if (t >= o) { a = sw[t - o]; b = swy[t - o]; }
+    __syncthreads();
+    sw[t] += a; swy[t] += b;
+    __syncthreads();
+  }
+  const double W = sw[255], WY = swy[255];
+  const double Wall = W + wNA, WYall = WY + wyNA;
+
+  auto E = [&](double ww, double yy) -> double {
+    if (p.mode == 1) {
+      double g = yy;  // stat is -sum(g): T_alpha soft-threshold
+      if (p.alpha > 0) g = (g > p.alpha) ? g - p.alpha : (g < -p.alpha ? g + p.alpha : 0.0);
+      return g * g / (ww + p.lambda);
+    }
+    return ww > 0 ? yy * yy / ww : 0.0;
+  };
+  auto leafv = [&](double ww, double yy) -> double {
+    return p.mode == 1 ? yy / (ww + p.lambda) : (ww > 0 ? yy / ww : 0.0);
+  };
+
+  // candidate of this thread: threshold b = t (left = sorted positions < t)
+  double my_e = -1.0e300;
+  int my_code = -1;  // code = b*2 + na_left (b in 1..nb-1), or 0 for NA-vs-rest
+  const double min_w = p.min_w;
+  const bool random_mode = p.random_split != 0;
+  int rand_b = -1;
+  if (random_mode && nb > 1) {
+    unsigned long long hsh = splitmix64(p.seed ^ ((unsigned long long)level << 48) ^
+                                        ((unsigned long long)node << 20) ^ (unsigned long long)f);
+    rand_b = 1 + (int)(hsh % (unsigned long long)(nb - 1));
+  }
+  if (t >= 1 && t < nb && (!random_mode || t == rand_b)) {
+    const double wb = (t < 256) ? (sw[t] - sw[t - 1]) : 0.0;
+    if (wb != 0.0 || random_mode) {
+      const double wlo = sw[t - 1], wylo = swy[t - 1];
+      const double whi = W - wlo, wyhi = WY - wylo;
+      if (wNA == 0.0) {
+        if (wlo >= min_w && whi >= min_w) {
+          const double e = E(wlo, wylo) + E(whi, wyhi);
+          const bool ok = mono == 0 || (mono * leafv(wlo, wylo) <= mono * leafv(whi, wyhi));
+          if (ok) { my_e = e; my_code = t * 2 + (wlo > whi ? 1 : 0); }
+        }
+      } else {
+        if (wlo + wNA >= min_w && whi >= min_w) {  // NA left
+          const double e = E(wlo + wNA, wylo + wyNA) + E(whi, wyhi);
+          const bool ok = mono == 0 || (mono * leafv(wlo + wNA, wylo + wyNA) <= mono * leafv(whi, wyhi));
+          if (ok && e > my_e) { my_e = e; my_code = t * 2 + 1; }
+        }
+        if (wlo >= min_w && whi + wNA >= min_w) {  // NA right
+          const double e = E(wlo, wylo) + E(whi + wNA, wyhi + wyNA);
+          const bool ok = mono == 0 || (mono * leafv(wlo, wylo) <= mono * leafv(whi + wNA, wyhi + wyNA));
+          if (ok && e > my_e) { my_e = e; my_code = t * 2 + 0; }
+        }
+      }
+    }
+  }
+  // NA vs REST is the incumbent (DTree.java:1140) and wins ties
+  if (t == 0 && wNA >= min_w && W > 0 && !random_mode) {
+    my_e = E(W, WY) + E(wNA, wyNA);
+    my_code = 0;
+  }
+  best_e[t] = my_e; best_i[t] = my_code;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (t < o) {
+      const double e2 = best_e[t + o];
+      const int c2 = best_i[t + o];
+      // larger explained wins; ties -> smaller threshold index (code 0 = NA-vs-rest first)
+      if (c2 >= 0 && (best_i[t] < 0 || e2 > best_e[t] || (e2 == best_e[t] && c2 < best_i[t]))) {
+        best_e[t] = e2; best_i[t] = c2;
+      }
+    }
+    __syncthreads();
+  }
+  const int code = best_i[0];
+  const double be = best_e[0];
+  Cand* c = cand + (size_t)node * F + f;
+  // categorical bitset: left set = sorted positions < b (empty bins follow the NA direction)
+  __shared__ unsigned sbits[8];
+  if (t < 8) sbits[t] = 0u;
+  __syncthreads();
+  int b = 0, nal = 0;
+  if (code > 0) { b = code >> 1; nal = code & 1; }
+  if (cat && code > 0) {
+    if (t < nb) {
+      const int cidx = sidx[t];
+      const bool empty = (sw[t] - (t > 0 ? sw[t - 1] : 0.0)) == 0.0;
+      const bool left = empty ? (nal != 0) : (t < b);
+      if (left) atomicOr(&sbits[cidx >> 5], 1u << (cidx & 31));
+    }
+  }
+  __syncthreads();
+  if (t == 0) {
+    int valid = 0;
+    double wl = 0, wr = 0, yl = 0, yr = 0;
+    if (code == 0) { wl = W; yl = WY; wr = wNA; yr = wyNA; }
+    else if (code > 0) {
+      wl = sw[b - 1]; yl = swy[b - 1]; wr = W - wl; yr = WY - yl;
+      if (nal) { wl += wNA; yl += wyNA; } else { wr += wNA; yr += wyNA; }
+    }
+    const double Epar = E(Wall, WYall);
+    double gain = be - Epar;
+    if (code >= 0 && Wall >= 2.0 * min_w) {
+      if (p.mode == 0) {
+        const double var = wYY * Wall - WYall * WYall;
+        const double seBefore = (wNA >= min_w) ? (wYY - Epar) : ((wYY - naYY) - E(W, WY));
+        const double seAfter = wYY - be;
+        const float pl = (float)(yl / wl), pr = (float)(yr / wr);
+        valid = ((float)var != 0.f) && (seAfter < seBefore * (1.0 - p.min_split_improvement)) &&
+                (pl != pr) && wl >= min_w && wr >= min_w;
+        if (random_mode) valid = wl > 0 && wr > 0;
+      } else if (p.mode == 1) {
+        valid = (0.5 * gain - p.gamma) > 1e-6 && wl >= min_w && wr >= min_w;
+        gain = 0.5 * gain - p.gamma;
+      } else {
+        valid = wl > 0 && wr > 0;
+      }
+    }
+    c->expl = be; c->gain = gain; c->wl = wl; c->wr = wr;
+    c->predl = (float)leafv(wl, yl); c->predr = (float)leafv(wr, yr);
+    c->bin = (code == 0) ? NA_BIN : b;
+    c->na_left = (code == 0) ? 0 : nal;
+    c->valid = valid;
+    c->is_cat = cat ? 1 : 0;
+    for (int k = 0; k < 8; ++k) c->bits[k] = cat ? sbits[k] : 0u;
+    if (cat && code == 0) {  // NA vs REST on a categorical: every level left
+      for (int k = 0; k < 8; ++k) c->bits[k] = 0xFFFFFFFFu;
+    }
+  }
+}
+
+// k_split_reduce: best feature per node (with per-tree feature mask and per-node column sampling).
+__global__ __launch_bounds__(64) void k_split_reduce(
+    const Cand* __restrict__ cand, const int* __restrict__ meta, int F,
+    const int* __restrict__ feat_ok /*[F] per-tree mask, 1 = usable*/, int k_cols,
+    unsigned long long seed, int level, Dec* __restrict__ dec) {
+  const int node = blockIdx.x, lane = threadIdx.x;
+  if (node >= meta[0]) return;
+  const unsigned long long base = splitmix64(seed ^ ((unsigned long long)(level + 1) << 40) ^ (unsigned long long)node);
+  int n_ok = 0;
+  for (int f = lane; f < F; f += 64) n_ok += feat_ok[f] ? 1 : 0;
+  n_ok = wave_sum_i(n_ok);
+  const bool sample = k_cols > 0 && k_cols < n_ok;
+  double be = -1.0e300;
+  int bf = -1;
+  for (int f = lane; f < F; f += 64) {
+    if (!feat_ok[f]) continue;
+    if (sample) {
+      const unsigned long long kf = splitmix64(base + (unsigned long long)f);
+      int rank = 0;
+      for (int g2 = 0; g2 < F; ++g2) {
+        if (!feat_ok[g2]) continue;
+        const unsigned long long kg = splitmix64(base + (unsigned long long)g2);
+        rank += (kg < kf || (kg == kf && g2 < f)) ? 1 : 0;
+      }
+      if (rank >= k_cols) continue;
+    }
+    const Cand& c = cand[(size_t)node * F + f];
+    if (c.valid && (bf < 0 || c.expl > be)) { be = c.expl; bf = f; }
+  }
+  // wave argmax, ties -> smaller feature index
+  for (int o = 32; o > 0; o >>= 1) {
+    const double e2 = __shfl_xor(be, o, 64);
+    const int f2 = __shfl_xor(bf, o, 64);
+    if (f2 >= 0 && (bf < 0 || e2 > be || (e2 == be && f2 < bf))) { be = e2; bf = f2; }
+  }
+  if (lane == 0) {
+    Dec d;
+    d.feat = bf;
+    if (bf >= 0) {
+      const Cand& c = cand[(size_t)node * F + bf];
+      d.bin = c.bin; d.na_left = c.na_left; d.is_cat = c.is_cat;
+      for (int k = 0; k < 8; ++k) d.bits[k] = c.bits[k];
+      d.gain = c.gain; d.wl = c.wl; d.wr = c.wr; d.predl = c.predl; d.predr = c.predr;
+    } else {
+      d.bin = 0; d.na_left = 0; d.is_cat = 0;
+      for (int k = 0; k < 8; ++k) d.bits[k] = 0u;
+      d.gain = 0; d.wl = 0; d.wr = 0; d.predl = 0; d.predr = 0;
+    }
+    dec[node] = d;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_count: rows going left per tile (one tile per block). Terminal nodes: whole tile counts as left.
+__global__ __launch_bounds__(256) void k_count(
+    const uint8_t* __restrict__ bins, int stride, const Node* __restrict__ nodes,
+    const int* __restrict__ tile_prefix, const int* __restrict__ meta, const Dec* __restrict__ dec,
+    int* __restrict__ tile_cnt) {
+  const int t = blockIdx.x;
+  const int n_nodes = meta[0], n_tiles = meta[1];
+  if (t >= n_tiles) return;
+  const int node = find_node(tile_prefix, n_nodes, t);
+  const Node nd = nodes[node];
+  const int r0 = nd.start + (t - tile_prefix[node]) * TILE;
+  const int r1 = min(r0 + TILE, nd.start + nd.len);
+  const Dec* d = dec + node;
+  const int feat = d->feat;
+  int cnt = 0;
+  if (feat < 0) {
+    cnt = (threadIdx.x == 0) ? (r1 - r0) : 0;
+  } else {
+    for (int row = r0 + threadIdx.x; row < r1; row += blockDim.x)
+      cnt += dec_go_left(d, bins[(size_t)row * stride + feat]) ? 1 : 0;
+  }
+  cnt = wave_sum_i(cnt);
+  __shared__ int s[4];
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) tile_cnt[t] = s[0] + s[1] + s[2] + s[3];
+}
+
+// ------------------------------------------------------------------------------------------------
+// Block-wide exclusive scan helper for k_plan (1024 threads, int values). Returns exclusive prefix
+// of `v` for this thread and writes the block total into *total.
+__device__ int block_excl_scan(int v, int* sh /*>=17*/, int* total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  int x = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) sh[wid] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int s = 0;
+    for (int w = 0; w < nw; ++w) { const int tmp = sh[w]; sh[w] = s; s += tmp; }
+    sh[16] = s;
+  }
+  __syncthreads();
+  const int res = x - v + sh[wid];
+  *total = sh[16];
+  __syncthreads();
+  return res;
+}
+
+// k_plan: one block. Turns per-tile left counts into stable partition offsets, numbers the children
+// (compacted, capacity-limited) and the new leaves, chooses which child is histogrammed, and builds
+// the next level's node list + tile prefix. meta: [0]=n_nodes [1]=n_tiles. counters: [0]=n_leaves.
+__global__ __launch_bounds__(1024) void k_plan(
+    const Node* __restrict__ nodes, const int* __restrict__ meta, const int* __restrict__ tile_prefix,
+    const int* __restrict__ tile_cnt, const Dec* __restrict__ dec,
+    int* __restrict__ tile_off, int* __restrict__ node_nl, int* __restrict__ child_l, int* __restrict__ child_r,
+    Node* __restrict__ next, int* __restrict__ next_tile_prefix, int* __restrict__ next_meta,
+    int* __restrict__ counters, int* __restrict__ scratch /* >= 2*cap_cur ints */,
+    int depth, int max_depth, double min_w, int cap_next, int leaf_cap) {
+  __shared__ int sh[17];
+  const int n = meta[0], nt = meta[1];
+  const int T = blockDim.x, tid = threadIdx.x;
+  int total;
+  // 1. global exclusive scan of tile counts
+  {
+    const int per = (nt + T - 1) / T;
+    const int a = min(nt, tid * per), b = min(nt, a + per);
+    int s = 0;
+    for (int i = a; i < b; ++i) s += tile_cnt[i];
+    int off = block_excl_scan(s, sh, &total);
+    for (int i = a; i < b; ++i) { const int c = tile_cnt[i]; tile_off[i] = off; off += c; }
+  }
+  __syncthreads();
+  // 2. per-node left totals and base offsets (scratch[0..n) = base)
+  {
+    for (int i = tid; i < n; i += T) {
+      const int ta = tile_prefix[i], tb = tile_prefix[i + 1];
+      const int base = (ta < nt) ? tile_off[ta] : total;
+      const int end = (tb < nt) ? tile_off[tb] : total;
+      scratch[i] = base;
+      node_nl[i] = end - base;
+    }
+  }
+  __syncthreads();
+  for (int t = tid; t < nt; t += T) {
+    const int node = find_node(tile_prefix, n, t);
+    tile_off[t] -= scratch[node];
+  }
+  __syncthreads();
+  // 3. children: active / leaf classification, compaction with capacity
+  const int perN = (n + T - 1) / T;
+  const int na = min(n, tid * perN), nb2 = min(n, na + perN);
+  int act_cnt = 0;
+  for (int i = na; i < nb2; ++i) {
+    const Dec d = dec[i];
+    int a = 0;
+    if (d.feat >= 0 && depth + 1 < max_depth) {
+      // child activity is decided from GLOBAL (all-reduced) weights so every rank plans alike
+      a += (d.wl >= 2.0 * min_w) ? 1 : 0;
+      a += (d.wr >= 2.0 * min_w) ? 1 : 0;
+    }
+    act_cnt += a;
+  }
+  int act_off = block_excl_scan(act_cnt, sh, &total);
+  // recount leaves given capacity overflow, store flags in scratch[n + i] (bit0 left active, bit1 right active)
+  int leaf_cnt = 0;
+  {
+    int ao = act_off;
+    for (int i = na; i < nb2; ++i) {
+      const Dec d = dec[i];
+      int flags = 0, lv = 0;
+      if (d.feat < 0) { lv = 1; }
+      else {
+        const bool la = depth + 1 < max_depth && d.wl >= 2.0 * min_w;
+        const bool ra = depth + 1 < max_depth && d.wr >= 2.0 * min_w;
+        if (la) { if (ao < cap_next) flags |= 1; ++ao; }
+        if (ra) { if (ao < cap_next) flags |= 2; ++ao; }
+        lv = 2 - ((flags & 1) + ((flags >> 1) & 1));
+      }
+      scratch[n + i] = flags;
+      leaf_cnt += lv;
+    }
+  }
+  const int leaf_base0 = counters[0];
+  __syncthreads();
+  int leaf_off = block_excl_scan(leaf_cnt, sh, &total);
+  const int n_leaves_new = total;
+  int ao = act_off;
+  int lo = leaf_base0 + leaf_off;
+  for (int i = na; i < nb2; ++i) {
+    const Dec d = dec[i];
+    const Node nd = nodes[i];
+    const int flags = scratch[n + i];
+    if (d.feat < 0) {
+      const int lid = min(lo++, leaf_cap - 1);
+      child_l[i] = -1 - lid; child_r[i] = -1 - lid;
+      continue;
+    }
+    const int nl = node_nl[i], nr = nd.len - nl;
+    const bool la = depth + 1 < max_depth && d.wl >= 2.0 * min_w;
+    const bool ra = depth + 1 < max_depth && d.wr >= 2.0 * min_w;
+    int li = -1, ri = -1;
+    if (la) { if (flags & 1) li = ao; ++ao; }
+    if (ra) { if (flags & 2) ri = ao; ++ao; }
+    child_l[i] = (li >= 0) ? li : -1 - min(lo++, leaf_cap - 1);
+    child_r[i] = (ri >= 0) ? ri : -1 - min(lo++, leaf_cap - 1);
+    if (li >= 0 && ri >= 0) {
+      const bool build_left = d.wl <= d.wr;  // global weights: identical choice on every rank
+      Node L = {nd.start, nl, build_left ? 1 : 0, i, build_left ? -1 : ri, 0, 0, 0};
+      Node R = {nd.start + nl, nr, build_left ? 0 : 1, i, build_left ? li : -1, 0, 0, 0};
+      next[li] = L; next[ri] = R;
+    } else if (li >= 0) {
+      Node L = {nd.start, nl, 1, i, -1, 0, 0, 0};
+      next[li] = L;
+    } else if (ri >= 0) {
+      Node R = {nd.start + nl, nr, 1, i, -1, 0, 0, 0};
+      next[ri] = R;
+    }
+  }
+  __syncthreads();
+  const int n_next = min(act_off + act_cnt, cap_next);  // only the last thread's value is the full total
+  __shared__ int s_nnext;
+  if (tid == T - 1) s_nnext = min(act_off + act_cnt, cap_next);
+  __syncthreads();
+  const int nn = s_nnext;
+  (void)n_next;
+  // 4. next-level tile prefix
+  {
+    const int per = (nn + T - 1) / T;
+    const int a = min(nn, tid * per), b = min(nn, a + per);
+    int s = 0;
+    for (int i = a; i < b; ++i) s += (next[i].len + TILE - 1) / TILE;
+    int off = block_excl_scan(s, sh, &total);
+    for (int i = a; i < b; ++i) { next_tile_prefix[i] = off; off += (next[i].len + TILE - 1) / TILE; }
+    if (tid == 0) {
+      next_tile_prefix[nn] = total;
+      next_meta[0] = nn;
+      next_meta[1] = total;
+      counters[0] = min(leaf_base0 + n_leaves_new, leaf_cap);
+    }
+  }
+}
+
+// k_zero_hist: zero the histogram slots of next-level nodes that are built directly.
+__global__ void k_zero_hist(double* __restrict__ hist, const Node* __restrict__ next,
+                            const int* __restrict__ meta, int slot_doubles) {
+  const int node = blockIdx.y;
+  if (node >= meta[0] || !next[node].build) return;
+  double* s = hist + (size_t)node * slot_doubles;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < slot_doubles; i += gridDim.x * blockDim.x) s[i] = 0.0;
+}
+
+// k_subtract: sibling histogram = parent - built child (fp64).
+__global__ void k_subtract(double* __restrict__ hist_next, const double* __restrict__ hist_cur,
+                           const Node* __restrict__ next, const int* __restrict__ meta, int slot_doubles) {
+  const int node = blockIdx.y;
+  if (node >= meta[0]) return;
+  const Node nd = next[node];
+  if (nd.build) return;
+  double* s = hist_next + (size_t)node * slot_doubles;
+  const double* pa = hist_cur + (size_t)nd.parent * slot_doubles;
+  const double* sb = hist_next + (size_t)nd.sib * slot_doubles;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < slot_doubles; i += gridDim.x * blockDim.x)
+    s[i] = pa[i] - sb[i];
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_move: stable partition of one level into the next, fused with (a) the smaller child's histogram
+// (when F <= 32: one LDS tile covers every feature) and (b) leaf bookkeeping for rows that stop here.
+template <bool HIST>
+__global__ __launch_bounds__(BLK) void k_move(
+    const uint8_t* __restrict__ sbins, const float4* __restrict__ saux, const int* __restrict__ sridx /*nullable*/,
+    uint8_t* __restrict__ dbins, float4* __restrict__ daux, int* __restrict__ dridx,
+    int stride, int F, const Node* __restrict__ nodes, const int* __restrict__ tile_prefix,
+    const int* __restrict__ meta, const Dec* __restrict__ dec, const int* __restrict__ tile_off,
+    const int* __restrict__ node_nl, const int* __restrict__ child_l, const int* __restrict__ child_r,
+    const Node* __restrict__ next, double* __restrict__ hist_next, int slot_doubles,
+    int* __restrict__ leaf_of_row, double* __restrict__ leafsum /*[L][2]*/) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* h = smem;
+  float* nayy = smem + FTILE * HSTRIDE;
+  double* red = (double*)(smem + FTILE * HSTRIDE + FTILE);   // 64 doubles
+  int* cnt = (int*)(red + 64);                                // [2 parity][2 side][8 waves]
+  Dec* sdec = (Dec*)(cnt + 64);                               // current node's decision
+
+  const int n_nodes = meta[0], n_tiles = meta[1];
+  if (n_nodes <= 0 || n_tiles <= 0) return;
+  const int per = (n_tiles + gridDim.x - 1) / gridDim.x;
+  const int t0 = blockIdx.x * per, t1 = min(n_tiles, t0 + per);
+  if (t0 >= t1) return;
+  const int W = stride >> 2;
+  const int g = threadIdx.x / LPR, j = threadIdx.x % LPR;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int gl = lane & ~(LPR - 1);  // group leader lane within the wave
+  const unsigned* sb32 = (const unsigned*)sbins;
+  unsigned* db32 = (unsigned*)dbins;
+  const float* sauxf = (const float*)saux;
+  float* dauxf = (float*)daux;
+
+  int cur = -1, build_child = -1, leafL = -1, leafR = -1;
+  double wyy = 0.0, sLn = 0.0, sLd = 0.0, sRn = 0.0, sRd = 0.0;
+  int parity = 0;
+
+  auto finish_node = [&]() {
+    double v[4] = {sLn, sLd, sRn, sRd};
+    block_sum4(v, red);
+    if (threadIdx.x == 0) {
+      if (leafL >= 0 && (v[0] != 0.0 || v[1] != 0.0)) { atomicAdd(leafsum + 2 * leafL, v[0]); atomicAdd(leafsum + 2 * leafL + 1, v[1]); }
+      if (leafR >= 0 && (v[2] != 0.0 || v[3] != 0.0)) { atomicAdd(leafsum + 2 * leafR, v[2]); atomicAdd(leafsum + 2 * leafR + 1, v[3]); }
+    }
+    if (HIST && build_child >= 0) {
+      double u[4] = {wyy, 0, 0, 0};
+      block_sum4(u, red);
+      __syncthreads();
+      flush_hist(h, nayy, u[0], 0, F, hist_next + (size_t)build_child * slot_doubles, slot_doubles);
+    }
+    __syncthreads();
+  };
+
+  for (int t = t0; t < t1; ++t) {
+    const int node = find_node(tile_prefix, n_nodes, t);
+    if (node != cur) {
+      if (cur >= 0) finish_node();
+      cur = node;
+      const int cl = child_l[node], cr = child_r[node];
+      const bool term = dec[node].feat < 0;
+      leafL = cl < 0 ? -1 - cl : -1;
+      leafR = (!term && cr < 0) ? -1 - cr : -1;
+      build_child = -1;
+      if (cl >= 0 && next[cl].build) build_child = cl;
+      if (cr >= 0 && next[cr].build) build_child = cr;
+      sLn = sLd = sRn = sRd = 0.0; wyy = 0.0;
+      if (HIST && build_child >= 0) lds_zero(smem, FTILE * HSTRIDE + FTILE);
+      if (threadIdx.x < (int)(sizeof(Dec) / 4)) ((int*)sdec)[threadIdx.x] = ((const int*)(dec + node))[threadIdx.x];
+      __syncthreads();
+    }
+    const Node nd = nodes[node];
+    const int feat = sdec->feat;
+    const bool term = feat < 0;
+    const int cl = child_l[node], cr = child_r[node];
+    const int nl = node_nl[node];
+    const int tin = t - tile_prefix[node];
+    const int r0 = nd.start + tin * TILE;
+    const int r1 = min(r0 + TILE, nd.start + nd.len);
+    int runL = tile_off[t];                         // left rows before this tile (within node)
+    int runR = tin * TILE - tile_off[t];            // right rows before this tile
+    for (int base = r0; base < r1; base += RPI) {
+      const int row = base + g;
+      const bool valid = row < r1;
+      int bin = 0;
+      if (valid && !term) bin = sbins[(size_t)row * stride + feat];
+      const bool left = valid && (term || dec_go_left(sdec, bin));
+      const bool right = valid && !left;
+      const unsigned long long mL = __ballot(left && j == 0);
+      const unsigned long long mR = __ballot(right && j == 0);
+      const unsigned long long below = (gl == 0) ? 0ull : ((1ull << gl) - 1ull);
+      const int preL = __popcll(mL & below), preR = __popcll(mR & below);
+      int* c = cnt + parity * 32;
+      if (lane == 0) { c[wid] = __popcll(mL); c[16 + wid] = __popcll(mR); }
+      __syncthreads();
+      int offL = 0, offR = 0, totL = 0, totR = 0;
+      for (int w = 0; w < (BLK >> 6); ++w) {
+        const int a = c[w], b = c[16 + w];
+        if (w < wid) { offL += a; offR += b; }
+        totL += a; totR += b;
+      }
+      parity ^= 1;
+      if (valid) {
+        const int child = left ? cl : cr;
+        const float a_ = sauxf[(size_t)row * 4 + 0];
+        const float b_ = sauxf[(size_t)row * 4 + 1];
+        const float myaux = (j < 4) ? sauxf[(size_t)row * 4 + j] : 0.f;
+        const int rid = sridx ? sridx[row] : row;
+        if (child >= 0 && !term) {
+          const int pos = left ? (nd.start + runL + offL + preL) : (nd.start + nl + runR + offR + preR);
+          for (int w = j; w < W; w += LPR) db32[(size_t)pos * W + w] = sb32[(size_t)row * W + w];
+          if (j < 4) dauxf[(size_t)pos * 4 + j] = myaux;
+          if (j == 4) dridx[pos] = rid;
+          if (HIST && child == build_child) {
+            const float yy = a_ > 0.f ? b_ * b_ / a_ : 0.f;
+            if (j == 0) wyy += yy;
+            if (j < W) {
+              const unsigned word = sb32[(size_t)row * W + j];
+              hist_word(h, nayy, word, j, j * 4, F, a_, b_, yy);
+            }
+          }
+        } else if (j == 0) {
+          // row stops here: leaf id in original order + Newton sums
+          const int leaf = term ? (-1 - cl) : (-1 - child);
+          leaf_of_row[rid] = leaf;
+          const float num = sauxf[(size_t)row * 4 + 2], den = sauxf[(size_t)row * 4 + 3];
+          if (left) { sLn += num; sLd += den; } else { sRn += num; sRd += den; }
+        }
+      }
+      runL += totL; runR += totR;
+    }
+  }
+  if (cur >= 0) finish_node();
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_bin_assign: X (column-major fp32 [F][N]) -> row-major uint8 bins [N][stride].
+// Numeric: bin = #edges <= x (edges sorted, per feature `nedges` of them at edges + f*max_edges);
+// categorical (iscat): bin = code (< nb) else NA. NaN -> NA_BIN.
+__global__ void k_bin_assign(const float* __restrict__ X, long long N, int F, int stride,
+                             const float* __restrict__ edges, int max_edges, const int* __restrict__ nedges,
+                             const int* __restrict__ iscat, uint8_t* __restrict__ bins) {
+  const long long row = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= N) return;
+  uint8_t* out = bins + row * stride;
+  for (int f = 0; f < stride; ++f) {
+    if (f >= F) { out[f] = 0; continue; }
+    const float x = X[(long long)f * N + row];
+    int b;
+    if (x != x) b = NA_BIN;
+    else if (iscat[f]) {
+      const int code = (int)x;
+      b = (code >= 0 && code <= nedges[f]) ? code : NA_BIN;
+    } else {
+      const float* e = edges + (size_t)f * max_edges;
+      int lo = 0, hi = nedges[f];
+      while (lo < hi) { const int mid = (lo + hi) >> 1; if (e[mid] <= x) lo = mid + 1; else hi = mid; }
+      b = lo;
+    }
+    out[f] = (uint8_t)b;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_predict: score raw features through a compressed forest.
+//   X: column-major fp32 [F][N]. Forest nodes (SoA): feat (-1 leaf), thr, left, right (absolute node
+//   index), na_left, cat_off (-1 numeric; else word offset into cat_bits), value. tree_root[t], tree_cls[t].
+//   out[N][K] += value of each tree's leaf (class tree_cls[t]).
+__global__ void k_predict(const float* __restrict__ X, long long N, int K,
+                          const int* __restrict__ feat, const float* __restrict__ thr,
+                          const int* __restrict__ left, const int* __restrict__ right,
+                          const int* __restrict__ na_left, const int* __restrict__ cat_off,
+                          const unsigned* __restrict__ cat_bits, const int* __restrict__ cat_nbits,
+                          const float* __restrict__ value, const int* __restrict__ tree_root,
+                          const int* __restrict__ tree_cls, int n_trees, float* __restrict__ out,
+                          int* __restrict__ leaf_out /*nullable [N][n_trees]*/) {
+  const long long row = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= N) return;
+  for (int t = 0; t < n_trees; ++t) {
+    int n = tree_root[t];
+    while (feat[n] >= 0) {
+      const float x = X[(long long)feat[n] * N + row];
+      bool go_left;
+      if (x != x) go_left = na_left[n] != 0;
+      else if (cat_off[n] >= 0) {
+        const int code = (int)x;
+        if (code < 0 || code >= cat_nbits[n]) go_left = na_left[n] != 0;
+        else go_left = (cat_bits[cat_off[n] + (code >> 5)] >> (code & 31)) & 1u;
+      } else go_left = x < thr[n];
+      n = go_left ? left[n] : right[n];
+    }
+    out[row * K + tree_cls[t]] += value[n];
+    if (leaf_out) leaf_out[row * n_trees + t] = n;
+  }
+}
+
+// ================================================================================================
+// C ABI launchers (called through ctypes with raw device pointers and the current HIP stream).
+extern "C" {
+
+int h2o_tree_sizes(int* out) {
+  out[0] = sizeof(Node); out[1] = sizeof(Dec); out[2] = sizeof(Cand); out[3] = TILE; out[4] = FTILE;
+  out[5] = (FTILE * HSTRIDE + FTILE) * 4 + 64 * 8 + 64 * 4 + (int)sizeof(Dec);  // k_move LDS bytes
+  return 0;
+}
+
+int h2o_hist_build(const void* bins, int stride, const void* aux, const void* nodes, const void* tile_prefix,
+                   const void* meta, int F, void* hist, int slot_doubles, int grid, hipStream_t s) {
+  const int nft = (F + FTILE - 1) / FTILE;
+  const size_t lds = (FTILE * HSTRIDE + FTILE) * 4 + 64 * 8;
+  hipLaunchKernelGGL(k_hist_build, dim3(grid, nft), dim3(BLK), lds, s, (const uint8_t*)bins, stride,
+                     (const float4*)aux, (const Node*)nodes, (const int*)tile_prefix, (const int*)meta, F,
+                     (double*)hist, slot_doubles);
+  return (int)hipGetLastError();
+}
+
+int h2o_split_find(const void* hist, int slot_doubles, const void* meta, int cap, int F, const void* nbins_f,
+                   const void* iscat_f, const void* mono_f, double min_w, double msi, double lambda_, double alpha,
+                   double gamma, int mode, int random_split, unsigned long long seed, int level, void* cand,
+                   hipStream_t s) {
+  SplitParams p;
+  p.min_w = min_w; p.min_split_improvement = msi; p.lambda = lambda_; p.alpha = alpha; p.gamma = gamma;
+  p.mode = mode; p.random_split = random_split; p.seed = seed;
+  hipLaunchKernelGGL(k_split_find, dim3(cap, F), dim3(256), 0, s, (const double*)hist, slot_doubles,
+                     (const int*)meta, F, (const int*)nbins_f, (const int*)iscat_f, (const int*)mono_f, p, level,
+                     (Cand*)cand);
+  return (int)hipGetLastError();
+}
+
+int h2o_split_reduce(const void* cand, const void* meta, int cap, int F, const void* feat_ok, int k_cols,
+                     unsigned long long seed, int level, void* dec, hipStream_t s) {
+  hipLaunchKernelGGL(k_split_reduce, dim3(cap), dim3(64), 0, s, (const Cand*)cand, (const int*)meta, F,
+                     (const int*)feat_ok, k_cols, seed, level, (Dec*)dec);
+  return (int)hipGetLastError();
+}
+
+int h2o_count(const void* bins, int stride, const void* nodes, const void* tile_prefix, const void* meta,
+              const void* dec, void* tile_cnt, int tiles_cap, hipStream_t s) {
+  hipLaunchKernelGGL(k_count, dim3(tiles_cap), dim3(256), 0, s, (const uint8_t*)bins, stride, (const Node*)nodes,
+                     (const int*)tile_prefix, (const int*)meta, (const Dec*)dec, (int*)tile_cnt);
+  return (int)hipGetLastError();
+}
+
+int h2o_plan(const void* nodes, const void* meta, const void* tile_prefix, const void* tile_cnt, const void* dec,
+             void* tile_off, void* node_nl, void* child_l, void* child_r, void* next, void* next_tile_prefix,
+             void* next_meta, void* counters, void* scratch, int depth, int max_depth, double min_w, int cap_next,
+             int leaf_cap, hipStream_t s) {
+  hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, s, (const Node*)nodes, (const int*)meta,
+                     (const int*)tile_prefix, (const int*)tile_cnt, (const Dec*)dec, (int*)tile_off, (int*)node_nl,
+                     (int*)child_l, (int*)child_r, (Node*)next, (int*)next_tile_prefix, (int*)next_meta,
+                     (int*)counters, (int*)scratch, depth, max_depth, min_w, cap_next, leaf_cap);
+  return (int)hipGetLastError();
+}
+
+int h2o_zero_hist(void* hist, const void* next, const void* meta, int cap, int slot_doubles, hipStream_t s) {
+  const int gx = (slot_doubles + 1023) / 1024;
+  hipLaunchKernelGGL(k_zero_hist, dim3(gx < 64 ? gx : 64, cap), dim3(256), 0, s, (double*)hist,
+                     (const Node*)next, (const int*)meta, slot_doubles);
+  return (int)hipGetLastError();
+}
+
+int h2o_subtract(void* hist_next, const void* hist_cur, const void* next, const void* meta, int cap,
+                 int slot_doubles, hipStream_t s) {
+  const int gx = (slot_doubles + 1023) / 1024;
+  hipLaunchKernelGGL(k_subtract, dim3(gx < 64 ? gx : 64, cap), dim3(256), 0, s, (double*)hist_next,
+                     (const double*)hist_cur, (const Node*)next, (const int*)meta, slot_doubles);
+  return (int)hipGetLastError();
+}
+
+int h2o_move(const void* sbins, const void* saux, const void* sridx, void* dbins, void* daux, void* dridx,
+             int stride, int F, const void* nodes, const void* tile_prefix, const void* meta, const void* dec,
+             const void* tile_off, const void* node_nl, const void* child_l, const void* child_r, const void* next,
+             void* hist_next, int slot_doubles, void* leaf_of_row, void* leafsum, int fuse_hist, int grid,
+             hipStream_t s) {
+  const size_t lds_h = (FTILE * HSTRIDE + FTILE) * 4 + 64 * 8 + 64 * 4 + sizeof(Dec);
+  if (fuse_hist) {
+    hipLaunchKernelGGL(k_move<true>, dim3(grid), dim3(BLK), lds_h, s, (const uint8_t*)sbins, (const float4*)saux,
+                       (const int*)sridx, (uint8_t*)dbins, (float4*)daux, (int*)dridx, stride, F, (const Node*)nodes,
+                       (const int*)tile_prefix, (const int*)meta, (const Dec*)dec, (const int*)tile_off,
+                       (const int*)node_nl, (const int*)child_l, (const int*)child_r, (const Node*)next,
+                       (double*)hist_next, slot_doubles, (int*)leaf_of_row, (double*)leafsum);
+  } else {
+    hipLaunchKernelGGL(k_move<false>, dim3(grid), dim3(BLK), lds_h, s, (const uint8_t*)sbins, (const float4*)saux,
+                       (const int*)sridx, (uint8_t*)dbins, (float4*)daux, (int*)dridx, stride, F, (const Node*)nodes,
+                       (const int*)tile_prefix, (const int*)meta, (const Dec*)dec, (const int*)tile_off,
+                       (const int*)node_nl, (const int*)child_l, (const int*)child_r, (const Node*)next,
+                       (double*)hist_next, slot_doubles, (int*)leaf_of_row, (double*)leafsum);
+  }
+  return (int)hipGetLastError();
+}
+
+int h2o_bin_assign(const void* X, long long N, int F, int stride, const void* edges, int max_edges,
+                   const void* nedges, const void* iscat, void* bins, hipStream_t s) {
+  const int blk = 256;
+  const long long grid = (N + blk - 1) / blk;
+  hipLaunchKernelGGL(k_bin_assign, dim3((unsigned)grid), dim3(blk), 0, s, (const float*)X, N, F, stride,
+                     (const float*)edges, max_edges, (const int*)nedges, (const int*)iscat, (uint8_t*)bins);
+  return (int)hipGetLastError();
+}
+
+int h2o_predict(const void* X, long long N, int K, const void* feat, const void* thr, const void* left,
+                const void* right, const void* na_left, const void* cat_off, const void* cat_bits,
+                const void* cat_nbits, const void* value, const void* tree_root, const void* tree_cls, int n_trees,
+                void* out, void* leaf_out, hipStream_t s) {
+  const int blk = 256;
+  const long long grid = (N + blk - 1) / blk;
+  hipLaunchKernelGGL(k_predict, dim3((unsigned)grid), dim3(blk), 0, s, (const float*)X, N, K, (const int*)feat,
+                     (const float*)thr, (const int*)left, (const int*)right, (const int*)na_left,
+                     (const int*)cat_off, (const unsigned*)cat_bits, (const int*)cat_nbits, (const float*)value,
+                     (const int*)tree_root, (const int*)tree_cls, n_trees, (float*)out, (int*)leaf_out);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

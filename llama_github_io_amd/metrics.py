@@ -1,0 +1,248 @@
+"""Model metrics (reference: ``hex/ModelMetricsBinomial.java``, ``ModelMetricsMultinomial.java``,
+``ModelMetricsRegression.java``, ``ModelMetricsClustering.java``, ``AUC2.java``, ``GainsLift.java``,
+``ConfusionMatrix.java``).
+
+All metric builders take torch tensors (any device) and reduce on device; the summary is a plain
+python object with H2O's metric names (``auc``, ``aucpr``, ``logloss``, ``mse``, ``rmse``, ``mae``,
+``rmsle``, ``mean_residual_deviance``, ``r2``, ``mean_per_class_error``, ``hit_ratio_table``,
+``thresholds_and_metric_scores``, ``gains_lift_table``, ...).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+THRESHOLD_CRITERIA = ("f1", "f2", "f0point5", "accuracy", "precision", "recall", "specificity",
+                      "absolute_mcc", "min_per_class_accuracy", "mean_per_class_accuracy")
+
+
+class ModelMetrics(dict):
+    """dict with attribute access; ``model_category`` names the family."""
+
+    def __getattr__(self, k):
+        try:
+            return self[k]
+        except KeyError as e:
+            raise AttributeError(k) from e
+
+    # H2O-python style accessors
+    def auc(self): return self.get("AUC")
+    def aucpr(self): return self.get("pr_auc")
+    def logloss(self): return self.get("logloss")
+    def mse(self): return self.get("MSE")
+    def rmse(self): return self.get("RMSE")
+    def mae(self): return self.get("mae")
+    def r2(self): return self.get("r2")
+    def mean_residual_deviance(self): return self.get("mean_residual_deviance")
+    def mean_per_class_error(self): return self.get("mean_per_class_error")
+    def gini(self): return self.get("Gini")
+
+    def __repr__(self):
+        keys = [k for k in ("model_category", "MSE", "RMSE", "mae", "r2", "logloss", "AUC", "pr_auc",
+                            "mean_per_class_error", "mean_residual_deviance", "tot_withinss", "betweenss")
+                if k in self]
+        return "ModelMetrics(" + ", ".join(f"{k}={self[k]}" for k in keys) + ")"
+
+
+def _w(w, n, device):
+    return torch.ones(n, dtype=torch.float64, device=device) if w is None else w.double()
+
+
+def regression_metrics(y, pred, w=None, distribution=None) -> ModelMetrics:
+    y, pred = y.double(), pred.double()
+    w = _w(w, y.numel(), y.device)
+    ok = ~torch.isnan(y) & (w > 0)
+    y, pred, w = y[ok], pred[ok], w[ok]
+    sw = w.sum()
+    err = y - pred
+    mse = (w * err * err).sum() / sw
+    mae = (w * err.abs()).sum() / sw
+    ybar = (w * y).sum() / sw
+    var = (w * (y - ybar) ** 2).sum() / sw
+    r2 = 1 - mse / var if var > 0 else torch.tensor(float("nan"))
+    rmsle = float("nan")
+    if bool((y > -1).all()) and bool((pred > -1).all()):
+        rmsle = math.sqrt(float((w * (torch.log1p(pred) - torch.log1p(y)) ** 2).sum() / sw))
+    mrd = float(mse)
+    if distribution is not None and distribution.name not in ("gaussian",):
+        f = distribution.link_fn(torch.clamp(pred, min=1e-300)) if distribution.link == "log" else pred
+        try:
+            mrd = float(distribution.deviance(w, y, f).sum() / sw)
+        except Exception:  # noqa: BLE001
+            mrd = float(mse)
+    return ModelMetrics(model_category="Regression", MSE=float(mse), RMSE=math.sqrt(float(mse)), mae=float(mae),
+                        rmsle=rmsle, r2=float(r2), mean_residual_deviance=mrd, nobs=int(y.numel()))
+
+
+def _auc_from_sorted(pos, neg):
+    """pos/neg: weights per distinct threshold sorted by descending score. Trapezoid ROC + PR AUC."""
+    tp = torch.cumsum(pos, 0)
+    fp = torch.cumsum(neg, 0)
+    P, Nn = tp[-1], fp[-1]
+    if P <= 0 or Nn <= 0:
+        return float("nan"), float("nan"), tp, fp
+    tpr = torch.cat([torch.zeros(1, dtype=tp.dtype, device=tp.device), tp / P])
+    fpr = torch.cat([torch.zeros(1, dtype=fp.dtype, device=fp.device), fp / Nn])
+    auc = torch.trapz(tpr, fpr)
+    prec = tp / (tp + fp)
+    rec = tp / P
+    rec0 = torch.cat([torch.zeros(1, dtype=rec.dtype, device=rec.device), rec])
+    prec0 = torch.cat([prec[:1], prec])
+    aucpr = torch.trapz(prec0, rec0)
+    return float(auc), float(aucpr), tp, fp
+
+
+def binomial_metrics(y, p1, w=None, domain=("0", "1"), nbins_thresholds: int = 400) -> ModelMetrics:
+    """y in {0,1}; p1 = P(class 1)."""
+    y, p1 = y.double(), p1.double()
+    w = _w(w, y.numel(), y.device)
+    ok = ~torch.isnan(y) & (w > 0)
+    y, p1, w = y[ok], p1[ok], w[ok]
+    sw = w.sum()
+    pc = torch.clamp(p1, 1e-15, 1 - 1e-15)
+    logloss = float(-(w * (y * torch.log(pc) + (1 - y) * torch.log(1 - pc))).sum() / sw)
+    mse = float((w * (y - p1) ** 2).sum() / sw)
+    # exact ROC over distinct scores
+    order = torch.argsort(p1, descending=True)
+    ps, ys, ws = p1[order], y[order], w[order]
+    uniq, inv = torch.unique_consecutive(ps, return_inverse=True)
+    pos = torch.zeros(uniq.numel(), dtype=torch.float64, device=y.device).index_add_(0, inv, ws * ys)
+    neg = torch.zeros(uniq.numel(), dtype=torch.float64, device=y.device).index_add_(0, inv, ws * (1 - ys))
+    auc, aucpr, tp, fp = _auc_from_sorted(pos, neg)
+    # thresholds table (H2O keeps <= 400 bins)
+    thr_tab = _threshold_table(uniq, tp, fp, nbins_thresholds)
+    ybar = float((w * y).sum() / sw)
+    var = ybar * (1 - ybar)
+    r2 = 1 - mse / var if var > 0 else float("nan")
+    mm = ModelMetrics(model_category="Binomial", MSE=mse, RMSE=math.sqrt(mse), logloss=logloss, AUC=auc,
+                      pr_auc=aucpr, Gini=2 * auc - 1 if auc == auc else float("nan"), r2=r2, nobs=int(y.numel()),
+                      domain=list(domain), thresholds_and_metric_scores=thr_tab)
+    if thr_tab:
+        best = max(thr_tab, key=lambda r: r["f1"])
+        mm["max_f1_threshold"] = best["threshold"]
+        mm["cm"] = dict(threshold=best["threshold"], table=[[best["tns"], best["fps"]], [best["fns"], best["tps"]]])
+        mm["mean_per_class_error"] = 1 - best["mean_per_class_accuracy"]
+        mm["max_criteria_and_metric_scores"] = {c: max(thr_tab, key=lambda r: r[c])[c] for c in THRESHOLD_CRITERIA}
+    mm["gains_lift_table"] = gains_lift(y, p1, w)
+    return mm
+
+
+def _threshold_table(uniq, tp, fp, nb):
+    n = uniq.numel()
+    if n == 0:
+        return []
+    P, Nn = float(tp[-1]), float(fp[-1])
+    idx = torch.linspace(0, n - 1, steps=min(n, nb), device=uniq.device).round().long().unique()
+    th = uniq[idx].cpu().numpy()
+    tps = tp[idx].cpu().numpy(); fps = fp[idx].cpu().numpy()
+    rows = []
+    for t, a, b in zip(th, tps, fps):
+        fn, tn = P - a, Nn - b
+        prec = a / (a + b) if a + b > 0 else 1.0
+        rec = a / P if P > 0 else 0.0
+        spec = tn / Nn if Nn > 0 else 0.0
+        f = lambda beta: (1 + beta ** 2) * prec * rec / (beta ** 2 * prec + rec) if (beta ** 2 * prec + rec) > 0 else 0.0
+        den = math.sqrt(max((a + b) * (a + fn) * (tn + b) * (tn + fn), 1e-300))
+        mcc = (a * tn - b * fn) / den
+        rows.append(dict(threshold=float(t), f1=f(1.0), f2=f(2.0), f0point5=f(0.5), accuracy=(a + tn) / (P + Nn),
+                         precision=prec, recall=rec, specificity=spec, absolute_mcc=abs(mcc),
+                         min_per_class_accuracy=min(rec, spec), mean_per_class_accuracy=(rec + spec) / 2,
+                         tns=tn, fns=fn, fps=b, tps=a))
+    return rows
+
+
+def gains_lift(y, p1, w, groups: int = 16):
+    order = torch.argsort(p1, descending=True)
+    ys, ws = y[order], w[order]
+    cw = torch.cumsum(ws, 0)
+    tot = float(cw[-1]) if cw.numel() else 0.0
+    tot_pos = float((ws * ys).sum())
+    if tot <= 0 or tot_pos <= 0:
+        return []
+    out = []
+    cpos = torch.cumsum(ws * ys, 0)
+    for g in range(1, groups + 1):
+        frac = g / groups
+        k = int(torch.searchsorted(cw, torch.tensor(frac * tot, dtype=cw.dtype, device=cw.device)).clamp(max=cw.numel() - 1))
+        cum_rate = float(cpos[k] / cw[k])
+        out.append(dict(group=g, cumulative_data_fraction=float(cw[k] / tot), cumulative_capture_rate=float(cpos[k]) / tot_pos,
+                        cumulative_lift=cum_rate / (tot_pos / tot), cumulative_response_rate=cum_rate))
+    return out
+
+
+def multinomial_metrics(y, probs, w=None, domain=None, hit_k: int = 10) -> ModelMetrics:
+    """y: class index; probs [N, K]."""
+    y = y.long() if not torch.is_floating_point(y) else torch.nan_to_num(y, nan=-1).long()
+    w = _w(w, y.numel(), y.device)
+    ok = (y >= 0) & (w > 0)
+    y, probs, w = y[ok], probs[ok].double(), w[ok]
+    K = probs.shape[1]
+    sw = w.sum()
+    py = torch.clamp(probs.gather(1, y[:, None]).squeeze(1), 1e-15, 1.0)
+    logloss = float(-(w * torch.log(py)).sum() / sw)
+    onehot = torch.nn.functional.one_hot(y, K).double()
+    mse = float((w * ((onehot - probs) ** 2).sum(1)).sum() / sw)
+    pred = probs.argmax(1)
+    cm = torch.zeros(K, K, dtype=torch.float64, device=y.device)
+    cm.index_put_((y, pred), w, accumulate=True)
+    per_class_err = 1 - torch.diag(cm) / cm.sum(1).clamp(min=1e-300)
+    rank = (probs > py[:, None]).sum(1)
+    hits = [float((w * (rank < k).double()).sum() / sw) for k in range(1, min(hit_k, K) + 1)]
+    auc = multinomial_auc(y, probs, w) if K <= 50 else float("nan")
+    return ModelMetrics(model_category="Multinomial", MSE=mse, RMSE=math.sqrt(mse), logloss=logloss,
+                        mean_per_class_error=float(per_class_err.mean()), cm=dict(table=cm.cpu().tolist()),
+                        hit_ratio_table=hits, nobs=int(y.numel()), domain=domain, AUC=auc)
+
+
+def multinomial_auc(y, probs, w):
+    """Macro one-vs-rest AUC (H2O ``MultinomialAucType.MACRO_OVR``)."""
+    K = probs.shape[1]
+    aucs = []
+    for k in range(K):
+        yk = (y == k).double()
+        if yk.sum() == 0 or yk.sum() == yk.numel():
+            continue
+        order = torch.argsort(probs[:, k], descending=True)
+        ps = probs[order, k]
+        uniq, inv = torch.unique_consecutive(ps, return_inverse=True)
+        pos = torch.zeros(uniq.numel(), dtype=torch.float64, device=y.device).index_add_(0, inv, (w * yk)[order])
+        neg = torch.zeros(uniq.numel(), dtype=torch.float64, device=y.device).index_add_(0, inv, (w * (1 - yk))[order])
+        aucs.append(_auc_from_sorted(pos, neg)[0])
+    return float(np.mean(aucs)) if aucs else float("nan")
+
+
+def clustering_metrics(X, centers, assign, w=None) -> ModelMetrics:
+    """X [N, F] (standardised space), centers [K, F], assign [N]."""
+    X = X.double(); C = centers.double()
+    w = _w(w, X.shape[0], X.device)
+    d = ((X - C[assign]) ** 2).sum(1)
+    K = C.shape[0]
+    within = torch.zeros(K, dtype=torch.float64, device=X.device).index_add_(0, assign, w * d)
+    size = torch.zeros(K, dtype=torch.float64, device=X.device).index_add_(0, assign, w)
+    mu = (w[:, None] * X).sum(0) / w.sum()
+    totss = float((w * ((X - mu) ** 2).sum(1)).sum())
+    tw = float(within.sum())
+    return ModelMetrics(model_category="Clustering", tot_withinss=tw, totss=totss, betweenss=totss - tw,
+                        withinss=within.cpu().tolist(), size=size.cpu().tolist(), nobs=int(X.shape[0]))
+
+
+def anomaly_metrics(score, w=None) -> ModelMetrics:
+    s = score.double()
+    return ModelMetrics(model_category="AnomalyDetection", mean_score=float(s.mean()), nobs=int(s.numel()))
+
+
+def autoencoder_metrics(err) -> ModelMetrics:
+    e = err.double()
+    return ModelMetrics(model_category="AutoEncoder", MSE=float(e.mean()), RMSE=math.sqrt(float(e.mean())), nobs=int(e.numel()))
+
+
+def make_metrics(category: str, y, preds, w=None, domain=None, distribution=None) -> ModelMetrics:
+    """preds: regression -> [N] mean; binomial -> [N] p1 or [N,2]; multinomial -> [N,K] probs."""
+    if category == "Binomial":
+        p1 = preds[:, -1] if preds.dim() == 2 else preds
+        return binomial_metrics(y, p1, w, domain or ("0", "1"))
+    if category == "Multinomial":
+        return multinomial_metrics(y, preds, w, domain)
+    return regression_metrics(y, preds.reshape(-1), w, distribution)

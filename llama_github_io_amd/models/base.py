@@ -1,0 +1,237 @@
+"""Model / ModelBuilder base classes (reference: ``hex/ModelBuilder.java``, ``hex/Model.java``,
+``hex/ScoreKeeper.java`` early stopping, ``hex/CVModelBuilder.java`` cross-validation).
+
+A model is trained from an :class:`~llama_github_io_amd.frame.H2OFrame` (or raw tensors), keeps a
+``DataInfo`` describing how to turn any frame into the model's feature tensor (column order, domains,
+categorical level remapping — ``Model.adaptTestForTrain``), and scores on the training device.
+"""
+from __future__ import annotations
+
+import copy
+import math
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from .. import metrics as mm
+
+
+# ------------------------------------------------------------------------------------------------
+@dataclass
+class DataInfo:
+    x: list                         # predictor names (model order)
+    iscat: np.ndarray               # int32 [F]
+    domains: list                   # per predictor: list of levels or None
+    response: str | None = None
+    response_domain: list | None = None
+    weights: str | None = None
+    offset: str | None = None
+    fold: str | None = None
+
+    @property
+    def F(self):
+        return len(self.x)
+
+    @property
+    def nlevels(self):
+        return np.array([len(d) if d is not None else 0 for d in self.domains], dtype=np.int32)
+
+    def to_state(self):
+        return dict(x=self.x, iscat=self.iscat.tolist(), domains=self.domains, response=self.response,
+                    response_domain=self.response_domain, weights=self.weights, offset=self.offset, fold=self.fold)
+
+    @staticmethod
+    def from_state(s):
+        return DataInfo(s["x"], np.asarray(s["iscat"], dtype=np.int32), s["domains"], s.get("response"),
+                        s.get("response_domain"), s.get("weights"), s.get("offset"), s.get("fold"))
+
+
+def default_device():
+    return torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+
+
+def model_category(info: DataInfo, distribution: str | None = None) -> str:
+    if info.response is None:
+        return "Unsupervised"
+    if info.response_domain is not None:
+        return "Binomial" if len(info.response_domain) == 2 else "Multinomial"
+    return "Regression"
+
+
+# ------------------------------------------------------------------------------------------------
+class ScoreKeeper:
+    """Early stopping on a moving average of the stopping metric (``hex/ScoreKeeper.java``)."""
+
+    LARGER_IS_BETTER = {"auc", "aucpr", "lift_top_group", "r2"}
+
+    def __init__(self, stopping_rounds=0, stopping_metric="AUTO", stopping_tolerance=1e-3, category="Regression"):
+        self.k = int(stopping_rounds)
+        m = (stopping_metric or "AUTO").lower()
+        if m == "auto":
+            m = "logloss" if category in ("Binomial", "Multinomial") else "deviance"
+        self.metric = m
+        self.tol = float(stopping_tolerance)
+        self.values = []
+
+    def value_of(self, metrics: mm.ModelMetrics) -> float:
+        m = self.metric
+        key = {"logloss": "logloss", "mse": "MSE", "rmse": "RMSE", "mae": "mae", "rmsle": "rmsle", "auc": "AUC",
+               "aucpr": "pr_auc", "deviance": "mean_residual_deviance", "misclassification": "mean_per_class_error",
+               "mean_per_class_error": "mean_per_class_error", "r2": "r2"}.get(m, m)
+        v = metrics.get(key)
+        if v is None and key == "mean_residual_deviance":
+            v = metrics.get("MSE")
+        if v is None and key == "logloss":
+            v = metrics.get("MSE")
+        return float("nan") if v is None else float(v)
+
+    def add(self, metrics) -> bool:
+        """Record a scoring event; return True if training should stop."""
+        self.values.append(self.value_of(metrics))
+        k = self.k
+        if k <= 0 or len(self.values) < 2 * k:
+            return False
+        v = np.asarray(self.values, dtype=np.float64)
+        if np.isnan(v[-k:]).any():
+            return False
+        larger = self.metric in self.LARGER_IS_BETTER
+        ma = np.convolve(v, np.ones(k) / k, mode="valid")
+        last = ma[-1]
+        ref = ma[:-k].max() if larger else ma[:-k].min()
+        if larger:
+            return not (last > ref * (1 + self.tol) if ref > 0 else last > ref + abs(ref) * self.tol)
+        return not (last < ref * (1 - self.tol) if ref > 0 else last < ref - abs(ref) * self.tol)
+
+
+# ------------------------------------------------------------------------------------------------
+class Model:
+    """Trained model. Subclasses implement ``_predict_tensor(X [F,N] float32) -> [N] or [N,K]``."""
+
+    algo = "model"
+
+    def __init__(self, key: str, params: dict, info: DataInfo):
+        self.key = key
+        self.params = dict(params)
+        self.info = info
+        self.output = {"model_category": model_category(info), "scoring_history": [], "training_metrics": None,
+                       "validation_metrics": None, "cross_validation_metrics": None, "variable_importances": None,
+                       "run_time_ms": 0}
+        self.device = default_device()
+
+    # ---- category helpers
+    @property
+    def model_category(self) -> str:
+        return self.output["model_category"]
+
+    @property
+    def nclasses(self) -> int:
+        return len(self.info.response_domain) if self.info.response_domain else 1
+
+    # ---- scoring
+    def _predict_tensor(self, X: torch.Tensor, offset=None) -> torch.Tensor:
+        raise NotImplementedError
+
+    def score_tensor(self, X: torch.Tensor, offset=None) -> torch.Tensor:
+        """Returns the prediction matrix: regression [N]; classification [N, K] probabilities."""
+        return self._predict_tensor(X.to(self.device), None if offset is None else offset.to(self.device))
+
+    def predict(self, frame):
+        from ..frame import H2OFrame
+        X, offset = frame.model_matrix(self.info, device=self.device)
+        P = self.score_tensor(X, offset)
+        return H2OFrame.from_predictions(P, self.model_category, self.info.response_domain,
+                                         threshold=self.default_threshold())
+
+    def default_threshold(self):
+        tm = self.output.get("training_metrics") or {}
+        vm = self.output.get("validation_metrics") or {}
+        return (vm or tm).get("max_f1_threshold", 0.5) if self.model_category == "Binomial" else None
+
+    def metrics_for(self, X, y, w=None, offset=None):
+        P = self.score_tensor(X, offset)
+        cat = self.model_category
+        if cat in ("Binomial", "Multinomial", "Regression"):
+            return mm.make_metrics(cat, y.to(P.device), P, None if w is None else w.to(P.device),
+                                   self.info.response_domain, getattr(self, "distribution", None))
+        return None
+
+    def model_performance(self, test_data=None, train=False, valid=False, xval=False):
+        if test_data is None:
+            if valid:
+                return self.output.get("validation_metrics")
+            if xval:
+                return self.output.get("cross_validation_metrics")
+            return self.output.get("training_metrics")
+        X, offset = test_data.model_matrix(self.info, device=self.device)
+        y = test_data.response_tensor(self.info, device=self.device)
+        w = test_data.weights_tensor(self.info, device=self.device)
+        return self.metrics_for(X, y, w, offset)
+
+    # ---- H2O-python style accessors
+    def varimp(self, use_pandas=False):
+        vi = self.output.get("variable_importances")
+        if vi is None:
+            return None
+        if use_pandas:
+            import pandas as pd
+            return pd.DataFrame(vi, columns=["variable", "relative_importance", "scaled_importance", "percentage"])
+        return vi
+
+    def scoring_history(self):
+        return self.output.get("scoring_history")
+
+    def _m(self, name, train, valid, xval):
+        src = "validation_metrics" if valid else ("cross_validation_metrics" if xval else "training_metrics")
+        m = self.output.get(src) or {}
+        return m.get(name)
+
+    def auc(self, train=False, valid=False, xval=False): return self._m("AUC", train, valid, xval)
+    def aucpr(self, train=False, valid=False, xval=False): return self._m("pr_auc", train, valid, xval)
+    def logloss(self, train=False, valid=False, xval=False): return self._m("logloss", train, valid, xval)
+    def mse(self, train=False, valid=False, xval=False): return self._m("MSE", train, valid, xval)
+    def rmse(self, train=False, valid=False, xval=False): return self._m("RMSE", train, valid, xval)
+    def mae(self, train=False, valid=False, xval=False): return self._m("mae", train, valid, xval)
+    def r2(self, train=False, valid=False, xval=False): return self._m("r2", train, valid, xval)
+
+    # ---- persistence
+    def to_state(self) -> dict:
+        return dict(algo=self.algo, key=self.key, params=_jsonable(self.params), info=self.info.to_state(),
+                    output=_jsonable(self.output))
+
+    def _restore(self, state):
+        self.output = state["output"]
+
+    def __repr__(self):
+        return f"<{type(self).__name__} key={self.key} category={self.model_category}>"
+
+
+def _jsonable(o):
+    if isinstance(o, dict):
+        return {k: _jsonable(v) for k, v in o.items()}
+    if isinstance(o, (list, tuple)):
+        return [_jsonable(v) for v in o]
+    if isinstance(o, np.ndarray):
+        return o.tolist()
+    if isinstance(o, (np.floating, np.integer)):
+        return o.item()
+    if isinstance(o, torch.Tensor):
+        return o.detach().cpu().tolist()
+    return o
+
+
+def variable_importance(names, gains) -> list:
+    g = np.asarray(gains, dtype=np.float64)
+    order = np.argsort(-g, kind="stable")
+    mx = g.max() if g.size and g.max() > 0 else 1.0
+    tot = g.sum() if g.sum() > 0 else 1.0
+    return [(names[i], float(g[i]), float(g[i] / mx), float(g[i] / tot)) for i in order]
+
+
+_key_counter = [0]
+
+
+def make_key(algo: str) -> str:
+    _key_counter[0] += 1
+    return f"{algo.upper()}_model_{int(time.time() * 1000) % 10_000_000}_{_key_counter[0]}"

@@ -1,0 +1,205 @@
+"""Gradient Boosting Machine (reference: ``hex/tree/gbm/GBM.java``, ``GBMModel.java``).
+
+Per iteration: pseudo-residuals ``z = negHalfGradient(y, f)`` (``DistributionFactory``), one tree per
+class grown by the device histogram engine on (w, w·z), leaf values by the distribution's Newton step
+``gammaNum/gammaDenom`` (``GBM.fitBestConstants``; median/quantile leaves for laplace / quantile /
+huber), scaled by ``learn_rate * learn_rate_annealing^t`` ((K-1)/K for multinomial) and clamped to
+``max_abs_leafnode_pred``; then ``f += leaf value`` per row via the leaf id each row recorded.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from .. import metrics as mm
+from ..parallel import collectives as coll
+from ..ops import tree as T
+from .base import DataInfo
+from .distributions import ORDER_STAT_DISTS, get_distribution
+from .shared_tree import SharedTreeModel, SharedTreeTrainer
+
+GBM_DEFAULTS = dict(ntrees=50, max_depth=5, min_rows=10.0, learn_rate=0.1, learn_rate_annealing=1.0,
+                    sample_rate=1.0, col_sample_rate=1.0, col_sample_rate_change_per_level=1.0,
+                    col_sample_rate_per_tree=1.0, distribution="AUTO", tweedie_power=1.5, quantile_alpha=0.5,
+                    huber_alpha=0.9, max_abs_leafnode_pred=float("inf"), pred_noise_bandwidth=0.0)
+
+
+def resolve_distribution(name, info: DataInfo) -> str:
+    name = (name or "AUTO").lower()
+    if name == "auto":
+        if info.response_domain is None:
+            return "gaussian"
+        return "bernoulli" if len(info.response_domain) == 2 else "multinomial"
+    return name
+
+
+class GBMModel(SharedTreeModel):
+    algo = "gbm"
+
+    def _trees_per_iter(self):
+        return self.forest.K if self.forest is not None else 1
+
+    def _predict_tensor(self, X, offset=None):
+        f = self.forest.predict_raw(X)
+        init = torch.as_tensor(self.init_f, dtype=torch.float32, device=f.device)
+        f = f + init
+        if offset is not None:
+            f = f + offset.float()[:, None]
+        d = self.distribution
+        if d.name == "multinomial":
+            return torch.softmax(f, dim=1)
+        if d.name in ("bernoulli", "quasibinomial", "modified_huber"):
+            p1 = torch.sigmoid(f[:, 0])
+            return torch.stack([1 - p1, p1], 1)
+        return d.linkinv(f[:, 0])
+
+    @property
+    def distribution(self):
+        return get_distribution(self.output["distribution"], tweedie_power=self.params.get("tweedie_power", 1.5),
+                                quantile_alpha=self.params.get("quantile_alpha", 0.5),
+                                huber_alpha=self.params.get("huber_alpha", 0.9))
+
+    def staged_predict_proba(self, X):
+        out = []
+        for n in range(1, self.ntrees_built() + 1):
+            out.append(self._raw(X, ntrees=n))
+        return out
+
+
+class GBMTrainer(SharedTreeTrainer):
+    algo = "gbm"
+    mode = T.MODE_SE
+    model_cls = GBMModel
+
+    def __init__(self, params):
+        p = dict(GBM_DEFAULTS)
+        p.update({k: v for k, v in params.items() if v is not None or k not in p})
+        super().__init__(p)
+
+    def _trees_per_iter(self):
+        return self.K
+
+    def _k_cols(self, F):
+        r = float(self.p.get("col_sample_rate", 1.0))
+        if r >= 1.0:
+            return 0
+        return max(1, int(math.floor(F * r + 0.5)))
+
+    def fit(self, X, y, w, offset, info, valid=None, model_key=None):
+        dname = resolve_distribution(self.p.get("distribution"), info)
+        self.dist = get_distribution(dname, tweedie_power=self.p["tweedie_power"], quantile_alpha=self.p["quantile_alpha"],
+                                     huber_alpha=self.p["huber_alpha"])
+        self.dname = dname
+        self.K = len(info.response_domain) if dname == "multinomial" else 1
+        return super().fit(X, y, w, offset, info, valid, model_key)
+
+    def _init_model(self, model):
+        N, K, dev = self.N, self.K, self.dev
+        model.output["distribution"] = self.dname
+        w = self.w
+        if self.K > 1:
+            self.yk = torch.nn.functional.one_hot(torch.nan_to_num(self.y, nan=0).long(), K).float()
+            init = np.zeros(K)  # H2O multinomial starts from 0
+        else:
+            init = np.array([self.dist.init_f(self.y, w, self.offset, reduce=coll.all_reduce_scalar)])
+            if self.dname in ORDER_STAT_DISTS:
+                yv = self.y
+                if self.dname == "quantile":
+                    init = np.array([float(torch.quantile(yv.double(), self.p["quantile_alpha"]))])
+                else:
+                    init = np.array([float(torch.median(yv.double()))])
+        self.init = init
+        model.init_f = init.tolist()
+        self.f = torch.tensor(init, dtype=torch.float32, device=dev).repeat(N, 1).contiguous()
+        if self.offset is not None:
+            self.f += self.offset[:, None]
+        self.aux = torch.empty(N, 4, dtype=torch.float32, device=dev)
+
+    def _lr(self, t):
+        return float(self.p["learn_rate"]) * float(self.p["learn_rate_annealing"]) ** t
+
+    def _prepare(self, t, k):
+        d = self.dist
+        f = self.f[:, k]
+        if k == 0:
+            self.w_eff = self._row_sample(float(self.p["sample_rate"]), t)
+            if self.K > 1:
+                self.probs = torch.softmax(self.f, dim=1)
+            if self.dname == "huber":
+                r = (self.y - f).abs()
+                self.dist.huber_delta = float(torch.quantile(r.double()[: 1 << 24], self.p["huber_alpha"]))
+        w = self.w_eff
+        if self.K > 1:
+            y = self.yk[:, k]
+            z = y - self.probs[:, k]
+        else:
+            y = self.y
+            z = d.neg_half_gradient(y, f)
+        a = self.aux
+        a[:, 0] = w
+        a[:, 1] = w * z
+        a[:, 2] = d.gamma_num(w, y, z, f)
+        a[:, 3] = d.gamma_denom(w, y, z, f)
+        self._z = z
+        return a
+
+    def _leaf_values(self, ls, t, k):
+        d = self.dist
+        m1 = (self.K - 1) / self.K if self.K > 1 else 1.0
+        if self.dname in ORDER_STAT_DISTS:
+            g = self._order_stat_leaves(ls.shape[0], k)
+        else:
+            g = d.leaf_gamma(ls[:, 0], ls[:, 1])
+        gf = self._lr(t) * m1 * g
+        if self.K > 1:
+            gf = gf.clamp(-1e4, 1e4)
+        gf = torch.nan_to_num(gf, nan=0.0, posinf=1e4, neginf=-1e4)
+        mx = float(self.p.get("max_abs_leafnode_pred", float("inf")))
+        if mx < float("inf"):
+            gf = gf.clamp(-mx, mx)
+        self._vals = gf.float()
+        return self._vals
+
+    def _order_stat_leaves(self, L, k):
+        """Weighted per-leaf median (laplace) / alpha-quantile (quantile) / huber leaf of y - f."""
+        leaf = self.builder.leaf_of_row.long()
+        diff = (self.y - self.f[:, k]).double()
+        w = self.w_eff.double()
+        alpha = self.p["quantile_alpha"] if self.dname == "quantile" else 0.5
+        order = torch.argsort(diff)
+        leaf_s = leaf[order]
+        order2 = torch.argsort(leaf_s, stable=True)
+        idx = order[order2]
+        ls, ds, ws = leaf[idx], diff[idx], w[idx]
+        tot = torch.zeros(L, dtype=torch.float64, device=ds.device).index_add_(0, ls, ws)
+        cw = torch.cumsum(ws, 0)
+        start = torch.cumsum(tot, 0) - tot
+        within = cw - start[ls]
+        target = alpha * tot[ls]
+        hit = (within >= target) & (ws > 0)
+        big = torch.iinfo(torch.long).max
+        pos = torch.where(hit, torch.arange(ls.numel(), device=ds.device), torch.full_like(ls, big))
+        first = torch.full((L,), big, dtype=torch.long, device=ds.device).scatter_reduce_(0, ls, pos, reduce="amin")
+        q = torch.where(first < big, ds[first.clamp(max=ls.numel() - 1)], torch.zeros(L, dtype=torch.float64, device=ds.device))
+        if self.dname == "huber":
+            delta = self.dist.huber_delta
+            r = diff - q[leaf]
+            c = torch.sign(r) * torch.clamp(r.abs(), max=delta)
+            s = torch.zeros(L, dtype=torch.float64, device=ds.device).index_add_(0, leaf, w * c)
+            q = q + s / tot.clamp(min=1e-300)
+        return q
+
+    def _update(self, t, k):
+        leaf = self.builder.leaf_of_row
+        self.f[:, k] += self._vals[leaf.long()]
+
+    def _training_metrics(self, model):
+        f = self.f
+        y, w = self.y, self.w
+        if self.K > 1:
+            return mm.multinomial_metrics(y, torch.softmax(f, 1), w, self.info.response_domain)
+        if self.dname in ("bernoulli", "quasibinomial", "modified_huber"):
+            return mm.binomial_metrics(y, torch.sigmoid(f[:, 0]), w, self.info.response_domain)
+        return mm.regression_metrics(y, self.dist.linkinv(f[:, 0]), w, self.dist)

@@ -1,0 +1,279 @@
+"""Shared driver for histogram-tree algorithms (reference: ``hex/tree/SharedTree.java``,
+``hex/tree/SharedTreeModel.java``).
+
+Responsibilities: bin the training matrix once (``ops.binning``), own the device tree builder
+(``ops.tree``), run the per-tree loop with row/column sampling, keep the forest, score periodically
+(scoring history, ``ScoreKeeper`` early stopping), and build variable importances from split gains.
+Algorithm subclasses provide ``_prepare`` (per-row histogram/leaf statistics), ``_leaf_values`` and
+``_update`` (prediction bookkeeping).
+"""
+from __future__ import annotations
+
+import math
+import time
+
+import numpy as np
+import torch
+
+from .. import metrics as mm
+from ..ops import tree as T
+from ..ops.binning import Binning, apply_binning, fit_binning
+from ..ops.forest import Forest, Tree, levels_to_tree
+from ..parallel import collectives as coll
+from .base import DataInfo, Model, ScoreKeeper, make_key, model_category, variable_importance
+
+SHARED_TREE_DEFAULTS = dict(
+    ntrees=50, max_depth=5, min_rows=10.0, nbins=20, nbins_top_level=1024, nbins_cats=1024,
+    histogram_type="AUTO", seed=-1, sample_rate=1.0, col_sample_rate_per_tree=1.0,
+    min_split_improvement=1e-5, score_each_iteration=False, score_tree_interval=0,
+    stopping_rounds=0, stopping_metric="AUTO", stopping_tolerance=1e-3, max_runtime_secs=0.0,
+    weights_column=None, offset_column=None, fold_column=None, nfolds=0, ignored_columns=None,
+    monotone_constraints=None, checkpoint=None, categorical_encoding="AUTO", max_bins=255,
+    calibrate_model=False, build_tree_one_node=False, check_constant_response=True,
+)
+
+
+def resolve_seed(seed) -> int:
+    if seed is None or int(seed) == -1:
+        return int(np.random.SeedSequence().entropy % (1 << 62))
+    return int(seed)
+
+
+class SharedTreeModel(Model):
+    def __init__(self, key, params, info):
+        super().__init__(key, params, info)
+        self.forest: Forest | None = None
+        self.binning: Binning | None = None
+        self.init_f = 0.0
+
+    def ntrees_built(self):
+        return len(self.forest) // max(1, self._trees_per_iter()) if self.forest else 0
+
+    def _trees_per_iter(self):
+        return 1
+
+    def _raw(self, X, offset=None, ntrees=None):
+        t1 = None if ntrees is None else ntrees * self._trees_per_iter()
+        raw = self.forest.predict_raw(X, 0, t1)
+        return raw
+
+    def predict_leaf_node_assignment(self, X: torch.Tensor) -> torch.Tensor:
+        _, leaves = self.forest.predict_raw(X.to(self.device), return_leaves=True)
+        return leaves
+
+    def to_state(self):
+        s = super().to_state()
+        s["forest"] = dict(trees=[t.to_state() for t in self.forest.trees], tree_class=self.forest.tree_class,
+                           K=self.forest.K)
+        s["binning"] = self.binning.to_state() if self.binning is not None else None
+        s["init_f"] = self.init_f
+        return s
+
+    def _restore(self, s):
+        super()._restore(s)
+        fs = s["forest"]
+        self.forest = Forest([Tree.from_state(t) for t in fs["trees"]], fs["tree_class"], fs["K"])
+        self.binning = Binning.from_state(s["binning"]) if s.get("binning") else None
+        self.init_f = s["init_f"]
+
+
+class SharedTreeTrainer:
+    """Generic per-tree loop. ``X`` is float32 [F, N] column-major on the training device."""
+
+    algo = "sharedtree"
+    mode = T.MODE_SE
+    model_cls = SharedTreeModel
+
+    def __init__(self, params: dict):
+        p = dict(SHARED_TREE_DEFAULTS)
+        p.update({k: v for k, v in params.items() if v is not None or k not in p})
+        self.p = p
+
+    # ---- hooks
+    def _split_params(self) -> T.SplitParams:
+        return T.SplitParams(min_w=float(self.p["min_rows"]), min_split_improvement=float(self.p["min_split_improvement"]),
+                             mode=self.mode)
+
+    def _k_cols(self, F_ok: int) -> int:
+        return 0
+
+    def _trees_per_iter(self) -> int:
+        return 1
+
+    # ---- main
+    def fit(self, X, y, w, offset, info: DataInfo, valid=None, model_key=None) -> SharedTreeModel:
+        t_start = time.time()
+        p = self.p
+        dev = X.device
+        F, N = X.shape
+        self.dev, self.F, self.N, self.info = dev, F, N, info
+        self.seed = resolve_seed(p["seed"])
+        self.category = model_category(info)
+        self.w = torch.ones(N, dtype=torch.float32, device=dev) if w is None else w.float().to(dev)
+        self.offset = None if offset is None else offset.float().to(dev)
+        self.y = y.float().to(dev)
+        self.X = X
+        # ---- binning (QuantilesGlobal on the whole training set, shared by every tree)
+        max_bins = int(min(255, max(int(p.get("max_bins") or 255), 2)))
+        if str(p.get("histogram_type", "AUTO")).lower() in ("uniformadaptive", "random", "roundrobin", "uniformrobust"):
+            max_bins = int(min(255, max(p.get("nbins_top_level", 1024), p.get("nbins", 20))))
+        if coll.is_dist():
+            # every rank must bin identically: fit on the union of per-rank samples
+            per = max(1, (1 << 20) // coll.world())
+            g = torch.Generator(device="cpu").manual_seed((self.seed + coll.rank()) & 0x7FFFFFFF)
+            idx = torch.randperm(N, generator=g)[:per].to(dev)
+            Xs = coll.all_gather_cat(X.index_select(1, idx).contiguous(), dim=1)
+            self.binning = fit_binning(Xs, info.iscat, info.nlevels, max_bins=max_bins, seed=self.seed,
+                                       sample=Xs.shape[1] + 1)
+        else:
+            self.binning = fit_binning(X, info.iscat, info.nlevels, max_bins=max_bins, seed=self.seed)
+        bins = apply_binning(self.binning, X)
+        mono = None
+        if p.get("monotone_constraints"):
+            mono = np.zeros(F, dtype=np.int32)
+            for k, v in dict(p["monotone_constraints"]).items():
+                if k in info.x:
+                    mono[info.x.index(k)] = int(v)
+        max_depth = int(p["max_depth"]) if int(p["max_depth"]) > 0 else 32
+        node_cap = int(p.get("node_cap", 1 << 14))
+        self.builder = T.make_builder(bins, F, self.binning.nbins, self.binning.iscat, mono, max_depth,
+                                      self._split_params(), node_cap=node_cap)
+        model = self.model_cls(model_key or make_key(self.algo), p, info)
+        model.binning = self.binning
+        model.device = dev
+        self.model = model
+        self._init_model(model)
+        K = self._trees_per_iter()
+        forest = Forest(n_classes_out=self._forest_k())
+        model.forest = forest
+        ntrees = int(p["ntrees"])
+        interval = int(p.get("score_tree_interval") or 0)
+        if p.get("score_each_iteration"):
+            interval = 1
+        keeper = ScoreKeeper(p.get("stopping_rounds", 0), p.get("stopping_metric", "AUTO"),
+                             p.get("stopping_tolerance", 1e-3), self.category)
+        need_sync = valid is not None or keeper.k > 0 or interval > 0
+        if keeper.k > 0 and interval == 0:
+            interval = max(1, min(5, ntrees // 10 or 1))
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(self.seed & 0x7FFFFFFFFFFF)
+        self.gen = gen
+        rng = np.random.default_rng(self.seed & 0xFFFFFFFF)
+        handles = []
+        gains = np.zeros(F, dtype=np.float64)
+        history = []
+        max_rt = float(p.get("max_runtime_secs") or 0)
+        self.valid = valid
+        built = 0
+        for t in range(ntrees):
+            feat_ok = self._tree_feature_mask(rng, F)
+            for k in range(K):
+                aux = self._prepare(t, k)
+                h = self.builder.build(aux, feat_ok, self._k_cols(F), seed=(self.seed * 1000003 + t * 97 + k) & ((1 << 63) - 1),
+                                       leaf_fn=lambda ls, t=t, k=k: self._leaf_values(ls, t, k))
+                self._update(t, k)
+                handles.append((h, k))
+            built = t + 1
+            if need_sync:
+                self._drain(handles, forest, gains)
+                handles = []
+                if interval and (built % interval == 0 or built == ntrees):
+                    ev = self._score_event(model, built, t_start)
+                    history.append(ev)
+                    mref = ev.get("_valid") or ev.get("_train")
+                    if mref is not None and keeper.add(mref):
+                        break
+            if max_rt > 0 and time.time() - t_start > max_rt:
+                break
+        self._drain(handles, forest, gains)
+        if need_sync and (not history or history[-1]["number_of_trees"] != built):
+            history.append(self._score_event(model, built, t_start))
+        self._finish(model, built)
+        model.output["scoring_history"] = [{k: v for k, v in e.items() if not k.startswith("_")} for e in history]
+        model.output["variable_importances"] = variable_importance(info.x, gains)
+        model.output["ntrees"] = built
+        model.output["model_summary"] = self._summary(forest, built)
+        model.output["training_metrics"] = self._training_metrics(model)
+        if valid is not None:
+            Xv, yv, wv, ov = valid
+            model.output["validation_metrics"] = model.metrics_for(Xv, yv, wv, ov)
+        model.output["run_time_ms"] = int((time.time() - t_start) * 1000)
+        return model
+
+    def _forest_k(self):
+        return self._trees_per_iter()
+
+    def _tree_feature_mask(self, rng, F):
+        r = float(self.p.get("col_sample_rate_per_tree", 1.0))
+        if r >= 1.0:
+            return None
+        k = max(1, int(math.floor(F * r + 0.5)))
+        ok = np.zeros(F, dtype=np.int32)
+        ok[rng.choice(F, size=k, replace=False)] = 1
+        return torch.from_numpy(ok).to(self.dev)
+
+    def _drain(self, handles, forest, gains):
+        if not handles:
+            return
+        if hasattr(self.builder, "fetch_all") and len(handles) == len(self.builder.history):
+            levels = self.builder.fetch_all()
+        else:
+            levels = [self.builder.fetch(h) for h, _ in handles]
+            if hasattr(self.builder, "history") and isinstance(self.builder.history, list):
+                self.builder.history.clear()
+        for (h, k), tl in zip(handles, levels):
+            tree = levels_to_tree(tl, self.binning)
+            forest.add(tree, k)
+            for d in tl.decs:
+                fe = d["feat"]
+                m = fe >= 0
+                np.add.at(gains, fe[m], np.maximum(d["gain"][m], 0.0))
+
+    def _summary(self, forest: Forest, built):
+        depths = [t.depth() for t in forest.trees] or [0]
+        leaves = [t.n_leaves() for t in forest.trees] or [0]
+        return dict(number_of_trees=built, number_of_internal_trees=len(forest), min_depth=int(min(depths)),
+                    max_depth=int(max(depths)), mean_depth=float(np.mean(depths)), min_leaves=int(min(leaves)),
+                    max_leaves=int(max(leaves)), mean_leaves=float(np.mean(leaves)))
+
+    def _score_event(self, model, built, t_start):
+        ev = dict(timestamp=time.time(), duration=time.time() - t_start, number_of_trees=built)
+        tm = self._training_metrics(model)
+        ev["_train"] = tm
+        if tm is not None:
+            for k in ("RMSE", "logloss", "AUC", "pr_auc", "mean_per_class_error", "mae", "mean_residual_deviance"):
+                if k in tm:
+                    ev["training_" + k.lower()] = tm[k]
+        if self.valid is not None:
+            Xv, yv, wv, ov = self.valid
+            vm = model.metrics_for(Xv, yv, wv, ov)
+            ev["_valid"] = vm
+            for k in ("RMSE", "logloss", "AUC", "pr_auc", "mean_per_class_error", "mae", "mean_residual_deviance"):
+                if vm is not None and k in vm:
+                    ev["validation_" + k.lower()] = vm[k]
+        return ev
+
+    # defaults, overridden
+    def _init_model(self, model):
+        pass
+
+    def _finish(self, model, built):
+        pass
+
+    def _training_metrics(self, model):
+        return None
+
+    def _prepare(self, t, k):
+        raise NotImplementedError
+
+    def _leaf_values(self, leafsum, t, k):
+        raise NotImplementedError
+
+    def _update(self, t, k):
+        pass
+
+    def _row_sample(self, rate: float, t: int):
+        if rate >= 1.0:
+            return self.w
+        m = torch.rand(self.N, generator=self.gen, device=self.dev) < rate
+        return self.w * m.float()

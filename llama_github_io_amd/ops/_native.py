@@ -1,0 +1,97 @@
+"""ctypes bindings to the in-tree native libraries (``lib/libh2o_hip.so`` and ``lib/libh2o_rt.so``).
+
+GPU ops never fall back silently: if a CUDA(HIP) tensor reaches an op and the HIP library cannot be
+loaded, :func:`hip` raises. CPU tensors take the PyTorch reference path of each op (used by the CPU
+test-suite and as the numerics oracle for the kernels).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must be imported first: shares torch's libamdhip64.so.7)
+
+from .. import build_native
+
+_lock = threading.Lock()
+_hip = None
+_rt = None
+
+c_int, c_ll, c_ull, c_double, c_void_p = ctypes.c_int, ctypes.c_longlong, ctypes.c_ulonglong, ctypes.c_double, ctypes.c_void_p
+
+_HIP_SIGS = {
+    "h2o_tree_sizes": [c_void_p],
+    "h2o_hist_build": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p],
+    "h2o_split_find": [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_double, c_double,
+                       c_double, c_double, c_double, c_int, c_int, c_ull, c_int, c_void_p, c_void_p],
+    "h2o_split_reduce": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_ull, c_int, c_void_p, c_void_p],
+    "h2o_count": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p],
+    "h2o_plan": [c_void_p] * 14 + [c_int, c_int, c_double, c_int, c_int, c_void_p],
+    "h2o_zero_hist": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
+    "h2o_subtract": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
+    "h2o_move": [c_void_p] * 6 + [c_int, c_int] + [c_void_p] * 9 + [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p],
+    "h2o_bin_assign": [c_void_p, c_ll, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
+    "h2o_predict": [c_void_p, c_ll, c_int] + [c_void_p] * 11 + [c_int, c_void_p, c_void_p, c_void_p],
+}
+
+
+def _bind(lib, sigs):
+    for name, args in sigs.items():
+        fn = getattr(lib, name, None)
+        if fn is None:
+            continue
+        fn.argtypes = args
+        fn.restype = c_int
+    return lib
+
+
+def register_hip_signatures(sigs: dict) -> None:
+    """Let other op modules declare their launchers' argtypes."""
+    _HIP_SIGS.update(sigs)
+    if _hip is not None:
+        _bind(_hip, sigs)
+
+
+def hip():
+    """Load (building first if needed) the HIP kernel library. Raises if unavailable."""
+    global _hip
+    if _hip is None:
+        with _lock:
+            if _hip is None:
+                path = build_native.HIP_LIB
+                if not os.path.exists(path) or os.environ.get("H2O_AMD_REBUILD"):
+                    build_native.build_hip()
+                _hip = _bind(ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL), _HIP_SIGS)
+    return _hip
+
+
+def rt():
+    """Load (building first if needed) the host runtime library."""
+    global _rt
+    if _rt is None:
+        with _lock:
+            if _rt is None:
+                path = build_native.RT_LIB
+                if not os.path.exists(path):
+                    build_native.build_rt()
+                _rt = ctypes.CDLL(path)
+    return _rt
+
+
+def stream_ptr(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+def check(rc: int, name: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"HIP launch {name} failed with hipError {rc}")
+
+
+def call(name: str, *args) -> None:
+    rc = getattr(hip(), name)(*args)
+    check(rc, name)

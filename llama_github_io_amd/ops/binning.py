@@ -1,0 +1,147 @@
+"""Global feature binning for the histogram tree engine (H2O ``histogram_type = QuantilesGlobal``).
+
+Reference: ``hex/tree/GlobalQuantilesCalc.java`` (global quantile split points) and
+``hex/tree/DHistogram.java`` (bin(), NA bin). Each numeric column gets at most 255 data bins whose
+edges are exact sample values: ``bin(x) = #{edges <= x}``, so a split "bins < b go left" is the
+threshold rule ``x < edges[b-1]`` on raw values. Categorical columns use their level codes as bins
+(levels beyond 254 are folded by frequency into one shared bin). NaN -> NA bin 255.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from . import _native as nat
+from .tree import MAX_DATA_BINS, NA_BIN
+
+
+@dataclass
+class Binning:
+    F: int
+    stride: int
+    edges: list                     # per feature: float32 np.ndarray (numeric) or None (categorical)
+    nbins: np.ndarray               # int32 [F] data bins per feature
+    iscat: np.ndarray               # int32 [F]
+    nlevels: np.ndarray             # int32 [F] categorical cardinality (0 numeric)
+    level_to_bin: list = field(default_factory=list)  # per feature: int array (None = identity)
+
+    def to_state(self):
+        return dict(F=self.F, stride=self.stride, edges=[None if e is None else e.tolist() for e in self.edges],
+                    nbins=self.nbins.tolist(), iscat=self.iscat.tolist(), nlevels=self.nlevels.tolist(),
+                    level_to_bin=[None if m is None else m.tolist() for m in self.level_to_bin])
+
+    @staticmethod
+    def from_state(s):
+        return Binning(s["F"], s["stride"], [None if e is None else np.asarray(e, dtype=np.float32) for e in s["edges"]],
+                       np.asarray(s["nbins"], dtype=np.int32), np.asarray(s["iscat"], dtype=np.int32),
+                       np.asarray(s["nlevels"], dtype=np.int32),
+                       [None if m is None else np.asarray(m, dtype=np.int64) for m in s["level_to_bin"]])
+
+
+def fit_binning(X: torch.Tensor, iscat, nlevels=None, max_bins: int = MAX_DATA_BINS, sample: int = 1 << 20,
+                seed: int = 0, weights: torch.Tensor | None = None) -> Binning:
+    """X: float32 [F, N] (column-major; NaN = missing; categorical columns hold level codes)."""
+    F, N = X.shape
+    max_bins = int(min(max(2, max_bins), MAX_DATA_BINS))
+    iscat = np.asarray(iscat, dtype=np.int32)
+    nlevels = np.zeros(F, dtype=np.int32) if nlevels is None else np.asarray(nlevels, dtype=np.int32)
+    g = torch.Generator(device="cpu").manual_seed(int(seed) & 0x7FFFFFFF)
+    if N > sample:
+        idx = torch.randperm(N, generator=g)[:sample].to(X.device)
+        Xs = X.index_select(1, idx)
+    else:
+        Xs = X
+    edges, nbins, l2b = [], np.zeros(F, dtype=np.int32), []
+    num_cols = [f for f in range(F) if not iscat[f]]
+    if num_cols:
+        Xn = Xs[num_cols].float()
+        Xn = torch.where(torch.isnan(Xn), torch.full_like(Xn, float("inf")), Xn)
+        srt, _ = torch.sort(Xn, dim=1)
+        srt = srt.cpu().numpy()
+    for f in range(F):
+        if iscat[f]:
+            nl = int(nlevels[f]) if nlevels[f] > 0 else int(torch.nan_to_num(X[f], nan=-1).max().item()) + 1
+            nlevels[f] = nl
+            if nl <= NA_BIN:
+                l2b.append(None)
+                nbins[f] = max(nl, 1)
+            else:  # fold rare levels into the last bin
+                codes = X[f][~torch.isnan(X[f])].long()
+                cnt = torch.bincount(codes, minlength=nl).cpu().numpy()
+                order = np.argsort(-cnt, kind="stable")
+                m = np.full(nl, NA_BIN - 1, dtype=np.int64)
+                m[order[: NA_BIN - 1]] = np.arange(NA_BIN - 1)
+                l2b.append(m)
+                nbins[f] = NA_BIN
+            edges.append(None)
+            continue
+        row = srt[num_cols.index(f)]
+        row = row[np.isfinite(row)]
+        l2b.append(None)
+        if row.size == 0:
+            edges.append(np.zeros(0, dtype=np.float32)); nbins[f] = 1
+            continue
+        u = np.unique(row)
+        if u.size <= max_bins:
+            e = u[1:].astype(np.float32)
+        else:
+            q = (np.arange(1, max_bins) * row.size) // max_bins
+            e = np.unique(row[q]).astype(np.float32)
+            e = e[e > row[0]]  # first bin must be non-empty
+        edges.append(e)
+        nbins[f] = e.size + 1
+    stride = (F + 3) // 4 * 4
+    return Binning(F, stride, edges, nbins, iscat, nlevels, l2b)
+
+
+def _edge_table(b: Binning, device):
+    maxe = max([1] + [0 if e is None else e.size for e in b.edges])
+    tab = np.full((b.F, maxe), np.inf, dtype=np.float32)
+    ned = np.zeros(b.F, dtype=np.int32)
+    for f, e in enumerate(b.edges):
+        if e is None:
+            ned[f] = b.nbins[f] - 1
+        else:
+            tab[f, : e.size] = e
+            ned[f] = e.size
+    return torch.from_numpy(tab).to(device), torch.from_numpy(ned).to(device), maxe
+
+
+def apply_binning(b: Binning, X: torch.Tensor) -> torch.Tensor:
+    """X float32 [F, N] -> uint8 bins [N, stride] (row-major) on X's device."""
+    F, N = X.shape
+    assert F == b.F
+    Xc = X
+    if any(m is not None for m in b.level_to_bin):
+        Xc = X.clone()
+        for f, m in enumerate(b.level_to_bin):
+            if m is not None:
+                col = Xc[f]
+                ok = ~torch.isnan(col)
+                mt = torch.as_tensor(m, device=X.device, dtype=torch.float32)
+                codes = col[ok].long().clamp(0, m.size - 1)
+                col[ok] = mt[codes]
+    Xc = Xc.contiguous().float()
+    if X.is_cuda:
+        tab, ned, maxe = _edge_table(b, X.device)
+        iscat = torch.from_numpy(b.iscat.astype(np.int32)).to(X.device)
+        out = torch.empty(N, b.stride, dtype=torch.uint8, device=X.device)
+        nat.call("h2o_bin_assign", Xc.data_ptr(), N, F, b.stride, tab.data_ptr(), maxe, ned.data_ptr(),
+                 iscat.data_ptr(), out.data_ptr(), nat.stream_ptr(X.device))
+        return out
+    out = torch.zeros(N, b.stride, dtype=torch.uint8)
+    for f in range(F):
+        col = Xc[f]
+        nan = torch.isnan(col)
+        if b.iscat[f]:
+            code = torch.nan_to_num(col, nan=-1).long()
+            bad = nan | (code < 0) | (code >= max(int(b.nbins[f]), 1))
+            bf = torch.where(bad, torch.full_like(code, NA_BIN), code)
+        else:
+            e = torch.from_numpy(b.edges[f])
+            bf = torch.bucketize(torch.nan_to_num(col, nan=0.0), e, right=True)
+            bf = torch.where(nan, torch.full_like(bf, NA_BIN), bf)
+        out[:, f] = bf.to(torch.uint8)
+    return out

@@ -1,0 +1,228 @@
+"""Compressed trees and forest scoring (reference: ``hex/tree/CompressedTree.java``,
+``hex/genmodel/algos/tree/SharedTreeMojoModel.java`` scoreTree).
+
+A :class:`Tree` is a flat node table (root = 0): ``feat`` (-1 = leaf), raw-value threshold ``thr``
+(numeric: ``x < thr`` goes left), ``na_left``, categorical level bitsets, children, leaf ``value``,
+``cover`` (weighted rows, used by TreeSHAP) and split ``gain`` (variable importance).
+:class:`Forest` concatenates trees (with their class index) and scores raw features either with the
+HIP kernel ``k_predict`` (CUDA tensors) or a vectorised PyTorch traversal (CPU).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _native as nat
+from .tree import NA_BIN, TreeLevels
+
+
+@dataclass
+class Tree:
+    feat: np.ndarray
+    thr: np.ndarray
+    bin: np.ndarray
+    na_left: np.ndarray
+    is_cat: np.ndarray
+    cat_bits: list          # per node: None or np.uint32 array over LEVELS
+    cat_nbits: np.ndarray
+    left: np.ndarray
+    right: np.ndarray
+    value: np.ndarray
+    cover: np.ndarray
+    gain: np.ndarray
+
+    @property
+    def n_nodes(self):
+        return len(self.feat)
+
+    def depth(self) -> int:
+        d = np.zeros(self.n_nodes, dtype=np.int64)
+        for i in range(self.n_nodes):
+            if self.feat[i] >= 0:
+                d[self.left[i]] = d[i] + 1
+                d[self.right[i]] = d[i] + 1
+        return int(d.max()) if self.n_nodes else 0
+
+    def n_leaves(self) -> int:
+        return int((self.feat < 0).sum())
+
+    def to_state(self):
+        return {k: (v.tolist() if isinstance(v, np.ndarray) else [None if b is None else b.tolist() for b in v])
+                for k, v in self.__dict__.items()}
+
+    @staticmethod
+    def from_state(s):
+        kw = {}
+        for k, v in s.items():
+            if k == "cat_bits":
+                kw[k] = [None if b is None else np.asarray(b, dtype=np.uint32) for b in v]
+            else:
+                kw[k] = np.asarray(v)
+        kw["thr"] = kw["thr"].astype(np.float32)
+        kw["value"] = kw["value"].astype(np.float32)
+        return Tree(**kw)
+
+
+def levels_to_tree(tl: TreeLevels, binning, leaf_values=None) -> Tree:
+    vals = tl.leaf_values if leaf_values is None else leaf_values
+    recs = []  # [feat, thr, bin, na_left, is_cat, bits, nbits, left, right, value, cover, gain]
+
+    def new(cover):
+        recs.append([-1, 0.0, 0, 0, 0, None, 0, -1, -1, 0.0, cover, 0.0])
+        return len(recs) - 1
+
+    ids = [new(tl.root_weight)]
+    for d, decs in enumerate(tl.decs):
+        nxt = {}
+        for i in range(len(decs)):
+            g = ids[i]
+            dd = decs[i]
+            cl, cr = int(tl.child_l[d][i]), int(tl.child_r[d][i])
+            if dd["feat"] < 0:
+                recs[g][9] = float(vals[-1 - cl]) if cl < 0 and -1 - cl < len(vals) else 0.0
+                continue
+            f = int(dd["feat"])
+            r = recs[g]
+            r[0] = f
+            r[2] = int(dd["bin"])
+            r[3] = int(dd["na_left"])
+            r[4] = int(dd["is_cat"])
+            r[11] = float(dd["gain"])
+            if dd["is_cat"]:
+                nl = int(binning.nlevels[f])
+                bits_b = dd["bits"]
+                m = binning.level_to_bin[f] if binning.level_to_bin else None
+                lv = np.arange(nl)
+                bl = lv if m is None else m[lv]
+                inleft = ((bits_b[bl >> 5] >> (bl & 31).astype(np.uint32)) & 1).astype(bool)
+                words = np.zeros((nl + 31) // 32, dtype=np.uint32)
+                for lvl in np.nonzero(inleft)[0]:
+                    words[lvl >> 5] |= np.uint32(1 << (int(lvl) & 31))
+                r[5], r[6], r[1] = words, nl, 0.0
+            else:
+                b = int(dd["bin"])
+                e = binning.edges[f]
+                r[1] = float("inf") if b >= NA_BIN or b - 1 >= len(e) else float(e[b - 1])
+            for side, c, w in ((7, cl, float(dd["wl"])), (8, cr, float(dd["wr"]))):
+                k = new(w)
+                r[side] = k
+                if c >= 0:
+                    nxt[c] = k
+                else:
+                    lid = -1 - c
+                    recs[k][9] = float(vals[lid]) if lid < len(vals) else 0.0
+        ids = [nxt[c] for c in sorted(nxt)]
+    cols = list(zip(*recs))
+    return Tree(feat=np.asarray(cols[0], dtype=np.int32), thr=np.asarray(cols[1], dtype=np.float32),
+                bin=np.asarray(cols[2], dtype=np.int32), na_left=np.asarray(cols[3], dtype=np.int8),
+                is_cat=np.asarray(cols[4], dtype=np.int8), cat_bits=list(cols[5]),
+                cat_nbits=np.asarray(cols[6], dtype=np.int32), left=np.asarray(cols[7], dtype=np.int32),
+                right=np.asarray(cols[8], dtype=np.int32), value=np.asarray(cols[9], dtype=np.float32),
+                cover=np.asarray(cols[10], dtype=np.float64), gain=np.asarray(cols[11], dtype=np.float64))
+
+
+class Forest:
+    """Trees + class assignment, with cached flat device arrays for scoring."""
+
+    def __init__(self, trees=None, tree_class=None, n_classes_out: int = 1):
+        self.trees = list(trees or [])
+        self.tree_class = list(tree_class or [0] * len(self.trees))
+        self.K = n_classes_out
+        self._flat = {}
+
+    def add(self, tree: Tree, cls: int = 0):
+        self.trees.append(tree)
+        self.tree_class.append(cls)
+        self._flat.clear()
+
+    def __len__(self):
+        return len(self.trees)
+
+    def flatten(self, t0=0, t1=None):
+        t1 = len(self.trees) if t1 is None else t1
+        feat, thr, left, right, nal, coff, cnb, val, roots, cls = [], [], [], [], [], [], [], [], [], []
+        bits = []
+        base = 0
+        for ti in range(t0, t1):
+            t = self.trees[ti]
+            n = t.n_nodes
+            feat.append(t.feat); thr.append(t.thr)
+            left.append(np.where(t.left >= 0, t.left + base, -1)); right.append(np.where(t.right >= 0, t.right + base, -1))
+            nal.append(t.na_left.astype(np.int32)); val.append(t.value)
+            co = np.full(n, -1, dtype=np.int32)
+            for i in range(n):
+                if t.feat[i] >= 0 and t.is_cat[i]:
+                    co[i] = sum(len(b) for b in bits)
+                    bits.append(t.cat_bits[i])
+            coff.append(co); cnb.append(t.cat_nbits)
+            roots.append(base); cls.append(self.tree_class[ti])
+            base += n
+        cat = lambda xs, dt: np.concatenate(xs).astype(dt) if xs else np.zeros(0, dt)
+        return dict(feat=cat(feat, np.int32), thr=cat(thr, np.float32), left=cat(left, np.int32),
+                    right=cat(right, np.int32), na_left=cat(nal, np.int32), cat_off=cat(coff, np.int32),
+                    cat_bits=(np.concatenate(bits).astype(np.uint32) if bits else np.zeros(1, np.uint32)),
+                    cat_nbits=cat(cnb, np.int32), value=cat(val, np.float32),
+                    roots=np.asarray(roots, dtype=np.int32), cls=np.asarray(cls, dtype=np.int32))
+
+    def _device_flat(self, device, t0, t1):
+        key = (str(device), t0, t1)
+        if key not in self._flat:
+            fl = self.flatten(t0, t1)
+            self._flat[key] = {k: torch.from_numpy(np.ascontiguousarray(v)).to(device) for k, v in fl.items()}
+        return self._flat[key]
+
+    def predict_raw(self, X: torch.Tensor, t0: int = 0, t1: int | None = None, out: torch.Tensor | None = None,
+                    return_leaves: bool = False):
+        """X: float32 [F, N] column-major. Returns [N, K] sums of leaf values (no link, no init_f)."""
+        t1 = len(self.trees) if t1 is None else t1
+        F, N = X.shape
+        if out is None:
+            out = torch.zeros(N, self.K, dtype=torch.float32, device=X.device)
+        nt = t1 - t0
+        leaves = torch.empty(N, max(nt, 1), dtype=torch.int32, device=X.device) if return_leaves else None
+        if nt <= 0 or N == 0:
+            return (out, leaves) if return_leaves else out
+        fl = self._device_flat(X.device, t0, t1)
+        Xc = X.contiguous().float()
+        if X.is_cuda:
+            nat.call("h2o_predict", Xc.data_ptr(), N, self.K, fl["feat"].data_ptr(), fl["thr"].data_ptr(),
+                     fl["left"].data_ptr(), fl["right"].data_ptr(), fl["na_left"].data_ptr(), fl["cat_off"].data_ptr(),
+                     fl["cat_bits"].data_ptr(), fl["cat_nbits"].data_ptr(), fl["value"].data_ptr(),
+                     fl["roots"].data_ptr(), fl["cls"].data_ptr(), nt, out.data_ptr(),
+                     0 if leaves is None else leaves.data_ptr(), nat.stream_ptr(X.device))
+        else:
+            self._predict_torch(Xc, fl, nt, out, leaves)
+        return (out, leaves) if return_leaves else out
+
+    @staticmethod
+    def _predict_torch(X, fl, nt, out, leaves):
+        N = X.shape[1]
+        ar = torch.arange(N)
+        feat, thr, left, right = fl["feat"].long(), fl["thr"], fl["left"].long(), fl["right"].long()
+        nal, coff, cnb, bits, val = fl["na_left"].bool(), fl["cat_off"].long(), fl["cat_nbits"].long(), fl["cat_bits"].long(), fl["value"]
+        for t in range(nt):
+            node = torch.full((N,), int(fl["roots"][t]), dtype=torch.long)
+            for _ in range(10_000):
+                f = feat[node]
+                act = f >= 0
+                if not bool(act.any()):
+                    break
+                fi = f.clamp(min=0)
+                x = X[fi, ar]
+                isnan = torch.isnan(x)
+                co = coff[node]
+                iscat = co >= 0
+                code = torch.nan_to_num(x, nan=-1).long()
+                inrange = (code >= 0) & (code < cnb[node])
+                word = bits[(co.clamp(min=0) + (code.clamp(min=0) >> 5)).clamp(max=bits.numel() - 1)]
+                catleft = ((word >> (code.clamp(min=0) & 31)) & 1).bool()
+                catgo = torch.where(inrange, catleft, nal[node])
+                numgo = x < thr[node]
+                go = torch.where(isnan, nal[node], torch.where(iscat, catgo, numgo))
+                nxt = torch.where(go, left[node], right[node])
+                node = torch.where(act, nxt, node)
+            out[:, int(fl["cls"][t])] += val[node]
+            if leaves is not None:
+                leaves[:, t] = node.int()

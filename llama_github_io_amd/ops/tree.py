@@ -1,0 +1,529 @@
+"""Histogram tree engine (device side) shared by GBM / DRF / XGBoost / IsolationForest / DT / Uplift.
+
+Two interchangeable builders produce the same :class:`TreeLevels` result:
+
+* :class:`GpuTreeBuilder` drives the HIP kernels of ``csrc/tree_kernels.hip`` (node-partitioned rows,
+  LDS histograms, fused partition + smaller-child histogram, on-device split search and planning).
+  A whole tree is a fixed sequence of launches on the current stream with no host synchronisation.
+* :class:`RefTreeBuilder` is the PyTorch/NumPy reference of exactly the same algorithm (same split
+  rules, same tie breaks, same leaf numbering); it runs on CPU tensors and is the numerics oracle.
+
+Split semantics follow ``hex/tree/DTree.java:984`` (findBestSplitPoint): squared-error reduction on
+(w, wY) histograms, NA bin with NA-left / NA-right / NA-vs-rest options, ``min_rows`` on weighted
+counts, relative ``min_split_improvement`` against the node's squared error, categorical levels
+sorted by mean response. Mode 1 is XGBoost's Newton gain G²/(H+λ) with L1 soft-threshold α and γ.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from . import _native as nat
+from ..parallel import collectives as coll
+
+NBIN = 256
+NA_BIN = 255
+MAX_DATA_BINS = 255
+FTILE = 32
+
+NODE_DT = np.dtype([("start", "<i4"), ("len", "<i4"), ("build", "<i4"), ("parent", "<i4"), ("sib", "<i4"),
+                    ("p0", "<i4"), ("p1", "<i4"), ("p2", "<i4")])
+DEC_DT = np.dtype([("feat", "<i4"), ("bin", "<i4"), ("na_left", "<i4"), ("is_cat", "<i4"), ("bits", "<u4", (8,)),
+                   ("gain", "<f8"), ("wl", "<f8"), ("wr", "<f8"), ("predl", "<f4"), ("predr", "<f4")])
+CAND_BYTES = 88
+MODE_SE, MODE_NEWTON, MODE_RANDOM = 0, 1, 2
+_M64 = (1 << 64) - 1
+
+
+def splitmix64(x: int) -> int:
+    x = (x + 0x9E3779B97F4A7C15) & _M64
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & _M64
+    return x ^ (x >> 31)
+
+
+@dataclass
+class SplitParams:
+    min_w: float = 10.0                  # min_rows (SE) / min_child_weight (Newton)
+    min_split_improvement: float = 1e-5
+    lam: float = 0.0
+    alpha: float = 0.0
+    gamma: float = 0.0
+    mode: int = MODE_SE
+    random_split: bool = False
+
+
+@dataclass
+class TreeLevels:
+    """Host copy of one built tree: per level decision records and child links.
+
+    child >= 0 is the index of the child in the next level; child < 0 encodes leaf id ``-1 - child``.
+    A terminal node (dec.feat < 0) has child_l == child_r == its own leaf.
+    """
+    decs: list
+    child_l: list
+    child_r: list
+    n_leaves: int
+    leaf_values: np.ndarray | None = None
+    root_weight: float = 0.0
+
+
+# ================================================================================================
+# reference split search (NumPy, float64) — mirrors k_split_find / k_split_reduce exactly
+def _E(mode, p: SplitParams, w, y):
+    if mode == MODE_NEWTON:
+        g = y
+        if p.alpha > 0:
+            g = np.where(g > p.alpha, g - p.alpha, np.where(g < -p.alpha, g + p.alpha, 0.0))
+        return g * g / (w + p.lam)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        return np.where(w > 0, y * y / np.where(w > 0, w, 1.0), 0.0)
+
+
+def _leafv(mode, p, w, y):
+    if mode == MODE_NEWTON:
+        return y / (w + p.lam)
+    return y / w if w > 0 else 0.0
+
+
+def split_find_ref(h, nayy, wyy, nbins_f, iscat_f, mono_f, p: SplitParams, level: int, node: int, seed: int):
+    """h: float64 [F, 256, 2]. Returns list of per-feature candidate dicts."""
+    F = h.shape[0]
+    out = []
+    for f in range(F):
+        nb = int(nbins_f[f])
+        cat = bool(iscat_f[f])
+        mono = int(mono_f[f]) if mono_f is not None else 0
+        w = np.zeros(256); wy = np.zeros(256)
+        lim = min(nb, NA_BIN)
+        w[:lim] = h[f, :lim, 0]; wy[:lim] = h[f, :lim, 1]
+        wNA, wyNA = h[f, NA_BIN, 0], h[f, NA_BIN, 1]
+        idx = np.arange(256)
+        if cat:
+            key = np.where(idx < nb, np.where(w > 0, wy / np.where(w > 0, w, 1), -1.0e308), 1.0e308)
+            idx = np.lexsort((idx, key))  # sort by key then index
+            w = w[idx]; wy = wy[idx]
+        sw = np.cumsum(w); swy = np.cumsum(wy)
+        W, WY = sw[255], swy[255]
+        Wall, WYall = W + wNA, WY + wyNA
+        random_mode = p.random_split
+        rand_b = -1
+        if random_mode and nb > 1:
+            hsh = splitmix64((seed ^ (level << 48) ^ (node << 20) ^ f) & _M64)
+            rand_b = 1 + int(hsh % (nb - 1))
+        best_e, best_code = -1.0e300, -1
+        cands = []
+        if wNA >= p.min_w and W > 0 and not random_mode:
+            cands.append((float(_E(p.mode, p, W, WY) + _E(p.mode, p, wNA, wyNA)), 0))
+        for t in range(1, nb):
+            if random_mode and t != rand_b:
+                continue
+            wb = sw[t] - sw[t - 1]
+            if wb == 0.0 and not random_mode:
+                continue
+            wlo, wylo = sw[t - 1], swy[t - 1]
+            whi, wyhi = W - wlo, WY - wylo
+            my_e, my_c = -1.0e300, -1
+            if wNA == 0.0:
+                if wlo >= p.min_w and whi >= p.min_w:
+                    ok = mono == 0 or mono * _leafv(p.mode, p, wlo, wylo) <= mono * _leafv(p.mode, p, whi, wyhi)
+                    if ok:
+                        my_e = float(_E(p.mode, p, wlo, wylo) + _E(p.mode, p, whi, wyhi)); my_c = t * 2 + (1 if wlo > whi else 0)
+            else:
+                if wlo + wNA >= p.min_w and whi >= p.min_w:
+                    e = float(_E(p.mode, p, wlo + wNA, wylo + wyNA) + _E(p.mode, p, whi, wyhi))
+                    ok = mono == 0 or mono * _leafv(p.mode, p, wlo + wNA, wylo + wyNA) <= mono * _leafv(p.mode, p, whi, wyhi)
+                    if ok and e > my_e:
+                        my_e, my_c = e, t * 2 + 1
+                if wlo >= p.min_w and whi + wNA >= p.min_w:
+                    e = float(_E(p.mode, p, wlo, wylo) + _E(p.mode, p, whi + wNA, wyhi + wyNA))
+                    ok = mono == 0 or mono * _leafv(p.mode, p, wlo, wylo) <= mono * _leafv(p.mode, p, whi + wNA, wyhi + wyNA)
+                    if ok and e > my_e:
+                        my_e, my_c = e, t * 2
+            if my_c >= 0:
+                cands.append((my_e, my_c))
+        for e, c in cands:
+            if best_code < 0 or e > best_e or (e == best_e and c < best_code):
+                best_e, best_code = e, c
+        b, nal = (best_code >> 1, best_code & 1) if best_code > 0 else (0, 0)
+        bits = np.zeros(8, dtype=np.uint32)
+        if cat and best_code > 0:
+            for t in range(nb):
+                cidx = idx[t]
+                empty = (sw[t] - (sw[t - 1] if t > 0 else 0.0)) == 0.0
+                left = (nal != 0) if empty else (t < b)
+                if left:
+                    bits[cidx >> 5] |= np.uint32(1 << (cidx & 31))
+        wl = wr = yl = yr = 0.0
+        if best_code == 0:
+            wl, yl, wr, yr = W, WY, wNA, wyNA
+        elif best_code > 0:
+            wl, yl = sw[b - 1], swy[b - 1]
+            wr, yr = W - wl, WY - yl
+            if nal:
+                wl += wNA; yl += wyNA
+            else:
+                wr += wNA; yr += wyNA
+        Epar = float(_E(p.mode, p, Wall, WYall))
+        gain = best_e - Epar
+        valid = False
+        if best_code >= 0 and Wall >= 2.0 * p.min_w:
+            if p.mode == MODE_SE:
+                var = wyy * Wall - WYall * WYall
+                seBefore = (wyy - Epar) if wNA >= p.min_w else ((wyy - nayy[f]) - float(_E(p.mode, p, W, WY)))
+                seAfter = wyy - best_e
+                pl, pr = np.float32(yl / wl) if wl else np.float32(np.nan), np.float32(yr / wr) if wr else np.float32(np.nan)
+                valid = (np.float32(var) != 0) and (seAfter < seBefore * (1.0 - p.min_split_improvement)) and \
+                    (pl != pr) and wl >= p.min_w and wr >= p.min_w
+                if random_mode:
+                    valid = wl > 0 and wr > 0
+            elif p.mode == MODE_NEWTON:
+                valid = (0.5 * gain - p.gamma) > 1e-6 and wl >= p.min_w and wr >= p.min_w
+                gain = 0.5 * gain - p.gamma
+            else:
+                valid = wl > 0 and wr > 0
+        if cat and best_code == 0:
+            bits[:] = 0xFFFFFFFF
+        out.append(dict(expl=best_e, gain=gain, wl=wl, wr=wr, bin=NA_BIN if best_code == 0 else b,
+                        na_left=0 if best_code == 0 else nal, valid=bool(valid), is_cat=int(cat), bits=bits,
+                        predl=_leafv(p.mode, p, wl, yl), predr=_leafv(p.mode, p, wr, yr)))
+    return out
+
+
+def split_reduce_ref(cands, feat_ok, k_cols, seed, level, node):
+    F = len(cands)
+    base = splitmix64((seed ^ ((level + 1) << 40) ^ node) & _M64)
+    ok = [bool(feat_ok[f]) for f in range(F)]
+    n_ok = sum(ok)
+    sample = 0 < k_cols < n_ok
+    allowed = ok[:]
+    if sample:
+        keys = [splitmix64((base + f) & _M64) for f in range(F)]
+        for f in range(F):
+            if not ok[f]:
+                continue
+            rank = sum(1 for g in range(F) if ok[g] and (keys[g] < keys[f] or (keys[g] == keys[f] and g < f)))
+            allowed[f] = rank < k_cols
+    be, bf = -1.0e300, -1
+    for f in range(F):
+        c = cands[f]
+        if allowed[f] and c["valid"] and (bf < 0 or c["expl"] > be):
+            be, bf = c["expl"], f
+    d = np.zeros(1, dtype=DEC_DT)[0]
+    d["feat"] = bf
+    if bf >= 0:
+        c = cands[bf]
+        d["bin"], d["na_left"], d["is_cat"], d["bits"] = c["bin"], c["na_left"], c["is_cat"], c["bits"]
+        d["gain"], d["wl"], d["wr"], d["predl"], d["predr"] = c["gain"], c["wl"], c["wr"], c["predl"], c["predr"]
+    return d
+
+
+def dec_go_left_np(d, b: np.ndarray) -> np.ndarray:
+    if d["feat"] < 0:
+        return np.ones_like(b, dtype=bool)
+    na = b == NA_BIN
+    if d["is_cat"]:
+        bits = d["bits"]
+        gl = ((bits[b >> 5] >> (b & 31).astype(np.uint32)) & 1).astype(bool)
+    else:
+        gl = b < d["bin"]
+    return np.where(na, bool(d["na_left"]), gl)
+
+
+# ================================================================================================
+class RefTreeBuilder:
+    """CPU reference builder (same algorithm, float64 histograms, index lists instead of partitions)."""
+
+    def __init__(self, bins: torch.Tensor, F: int, nbins_f, iscat_f, mono_f, max_depth: int, params: SplitParams,
+                 node_cap: int = 1 << 15):
+        self.bins = bins.cpu().numpy() if isinstance(bins, torch.Tensor) else np.asarray(bins)
+        self.F = F
+        self.nbins_f = np.asarray(nbins_f)
+        self.iscat_f = np.asarray(iscat_f)
+        self.mono_f = None if mono_f is None else np.asarray(mono_f)
+        self.D = max_depth
+        self.p = params
+        self.node_cap = node_cap
+        self.N = self.bins.shape[0]
+
+    def _hist(self, rows, aux):
+        F = self.F
+        h = np.zeros((F, 256, 2))
+        a = aux[rows, 0].astype(np.float64); b = aux[rows, 1].astype(np.float64)
+        a32 = aux[rows, 0]; b32 = aux[rows, 1]
+        yy = np.where(a32 > 0, (b32 * b32 / np.where(a32 > 0, a32, 1)).astype(np.float32), 0).astype(np.float64)
+        nayy = np.zeros(F)
+        for f in range(F):
+            bf = self.bins[rows, f].astype(np.int64)
+            h[f, :, 0] = np.bincount(bf, weights=a, minlength=256)
+            h[f, :, 1] = np.bincount(bf, weights=b, minlength=256)
+            nayy[f] = yy[bf == NA_BIN].sum()
+        return h, nayy, yy.sum()
+
+    def build(self, aux_static: torch.Tensor, feat_ok=None, k_cols: int = 0, seed: int = 0, leaf_fn=None):
+        aux = aux_static.detach().cpu().numpy().astype(np.float32)
+        F, D, p = self.F, self.D, self.p
+        feat_ok = np.ones(F, dtype=np.int32) if feat_ok is None else np.asarray(feat_ok)
+        leaf_of_row = np.full(self.N, -1, dtype=np.int64)
+        leafsum = []
+        level_rows = [np.arange(self.N)]
+        decs, cls, crs = [], [], []
+        n_leaves = 0
+        for d in range(D):
+            cap_next = min(1 << (d + 1), self.node_cap) if d + 1 < D else 1
+            n = len(level_rows)
+            dl = np.zeros(n, dtype=DEC_DT)
+            for i, rows in enumerate(level_rows):
+                h, nayy, wyy = self._hist(rows, aux)
+                cands = split_find_ref(h, nayy, wyy, self.nbins_f, self.iscat_f, self.mono_f, p, d, i, seed)
+                dl[i] = split_reduce_ref(cands, feat_ok, k_cols, seed, d, i)
+            cl = np.zeros(n, dtype=np.int64); cr = np.zeros(n, dtype=np.int64)
+            nxt = []
+            act = 0
+            for i, rows in enumerate(level_rows):
+                dd = dl[i]
+                if dd["feat"] < 0:
+                    lid = n_leaves; n_leaves += 1
+                    cl[i] = cr[i] = -1 - lid
+                    leaf_of_row[rows] = lid
+                    leafsum.append((aux[rows, 2].astype(np.float64).sum(), aux[rows, 3].astype(np.float64).sum()))
+                    continue
+                gl = dec_go_left_np(dd, self.bins[rows, dd["feat"]].astype(np.int64))
+                lrows, rrows = rows[gl], rows[~gl]
+                for side, crow, wside, arr in ((0, lrows, dd["wl"], cl), (1, rrows, dd["wr"], cr)):
+                    active = d + 1 < D and wside >= 2.0 * p.min_w and act < cap_next
+                    if d + 1 < D and wside >= 2.0 * p.min_w:
+                        act += 1
+                    if active:
+                        arr[i] = len(nxt); nxt.append(crow)
+                    else:
+                        lid = n_leaves; n_leaves += 1
+                        arr[i] = -1 - lid
+                        leaf_of_row[crow] = lid
+                        leafsum.append((aux[crow, 2].astype(np.float64).sum(), aux[crow, 3].astype(np.float64).sum()))
+            decs.append(dl); cls.append(cl); crs.append(cr)
+            level_rows = nxt
+            if not nxt:
+                break
+        res = TreeLevels(decs, cls, crs, n_leaves)
+        res.root_weight = float(aux[:, 0].astype(np.float64).sum())
+        self.leafsum = torch.tensor(np.array(leafsum, dtype=np.float64).reshape(-1, 2))
+        self.leaf_of_row = torch.from_numpy(leaf_of_row.astype(np.int32))
+        if leaf_fn is not None:
+            res.leaf_values = leaf_fn(self.leafsum).to(torch.float32).cpu().numpy()
+        if not hasattr(self, "history"):
+            self.history = []
+        self.history.append(res)
+        return len(self.history) - 1
+
+    def fetch(self, handle):
+        return self.history[handle]
+
+    def fetch_all(self):
+        out = list(self.history)
+        self.history.clear()
+        return out
+
+
+# ================================================================================================
+class _Arena:
+    """One device allocation holding every small per-level array (copied to host in one shot)."""
+
+    def __init__(self):
+        self.off = 0
+        self.items = []
+
+    def add(self, name, nbytes):
+        self.items.append((name, self.off, nbytes))
+        self.off += (nbytes + 255) // 256 * 256
+        return name
+
+
+class GpuTreeBuilder:
+    """Drives the HIP tree kernels. ``bins`` is a CUDA uint8 tensor [N, stride] (stride % 4 == 0)."""
+
+    def __init__(self, bins: torch.Tensor, F: int, nbins_f, iscat_f, mono_f, max_depth: int, params: SplitParams,
+                 node_cap: int = 1 << 14, grid: int = 512):
+        assert bins.is_cuda and bins.dtype == torch.uint8 and bins.dim() == 2
+        self.lib = nat.hip()
+        sz = np.zeros(8, dtype=np.int32)
+        self.lib.h2o_tree_sizes(sz.ctypes.data)
+        assert sz[0] == NODE_DT.itemsize and sz[1] == DEC_DT.itemsize and sz[2] == CAND_BYTES, sz
+        self.TILE = int(sz[3])
+        dev = bins.device
+        self.dev = dev
+        self.N, self.stride = bins.shape
+        assert self.stride % 4 == 0
+        self.F = F
+        self.D = D = max(1, int(max_depth))
+        self.p = params
+        self.grid = grid
+        self.master = bins
+        N, T = self.N, self.TILE
+        self.caps = [min(1 << d, node_cap) for d in range(D)] + [1]
+        capmax = max(self.caps)
+        self.slot = F * 2 * NBIN + F + 1
+        self.slot += self.slot & 1
+        self.hist = [torch.empty(capmax * self.slot, dtype=torch.float64, device=dev) for _ in range(2)]
+        self.tiles_cap = [(N + T - 1) // T + c for c in self.caps]
+        tmax = max(self.tiles_cap)
+        self.tile_cnt = torch.empty(tmax, dtype=torch.int32, device=dev)
+        self.tile_off = torch.empty(tmax, dtype=torch.int32, device=dev)
+        self.cand = torch.empty(capmax * F * CAND_BYTES, dtype=torch.uint8, device=dev)
+        self.scratch = torch.empty(2 * capmax + 16, dtype=torch.int32, device=dev)
+        self.leaf_cap = min(N + 1, 2 * sum(self.caps) + 2)
+        self.leafsum = torch.zeros(self.leaf_cap, 2, dtype=torch.float64, device=dev)
+        self.leaf_of_row = torch.empty(N, dtype=torch.int32, device=dev)
+        self.nbins_f = torch.as_tensor(np.asarray(nbins_f, dtype=np.int32), device=dev)
+        self.iscat_f = torch.as_tensor(np.asarray(iscat_f, dtype=np.int32), device=dev)
+        self.mono_f = None if mono_f is None else torch.as_tensor(np.asarray(mono_f, dtype=np.int32), device=dev)
+        self.feat_ok_all = torch.ones(F, dtype=torch.int32, device=dev)
+        # ping-pong row payload buffers
+        self.bufs = [dict(bins=torch.empty(N, self.stride, dtype=torch.uint8, device=dev),
+                          aux=torch.empty(N, 4, dtype=torch.float32, device=dev),
+                          ridx=torch.empty(N, dtype=torch.int32, device=dev)) for _ in range(2)]
+        # small per-level arrays in one arena
+        ar = _Arena()
+        for d in range(D + 1):
+            c = self.caps[d]
+            ar.add(f"nodes{d}", c * NODE_DT.itemsize)
+            ar.add(f"meta{d}", 8)
+            ar.add(f"tp{d}", (c + 1) * 4)
+            ar.add(f"dec{d}", c * DEC_DT.itemsize)
+            ar.add(f"cl{d}", c * 4)
+            ar.add(f"cr{d}", c * 4)
+            ar.add(f"nl{d}", c * 4)
+        ar.add("counters", 16)
+        ar.add("leafval", self.leaf_cap * 4)
+        self.arena = torch.zeros(ar.off, dtype=torch.uint8, device=dev)
+        self.av = {}
+        for name, off, nb in ar.items:
+            self.av[name] = self.arena[off:off + nb]
+        # level-0 constants
+        n_tiles0 = (N + T - 1) // T
+        root = np.zeros(1, dtype=NODE_DT)
+        root[0] = (0, N, 1, -1, -1, 0, 0, 0)
+        self.av["nodes0"].copy_(torch.from_numpy(root.view(np.uint8)))
+        self.av["meta0"].copy_(torch.from_numpy(np.array([1, n_tiles0], dtype=np.int32).view(np.uint8)))
+        self.av["tp0"][:8].copy_(torch.from_numpy(np.array([0, n_tiles0], dtype=np.int32).view(np.uint8)))
+        self.history = []
+
+    def _p(self, name):
+        return self.av[name].data_ptr()
+
+    def build(self, aux_static: torch.Tensor, feat_ok: torch.Tensor | None = None, k_cols: int = 0, seed: int = 0,
+              leaf_fn=None):
+        """Launch one tree. ``leaf_fn(leafsum[L,2] f64) -> leaf values f32`` runs on device before the
+        arena snapshot, so values travel to the host with the structure (no extra sync)."""
+        lib, s = self.lib, nat.stream_ptr(self.dev)
+        F, D, p, T = self.F, self.D, self.p, self.TILE
+        assert aux_static.shape == (self.N, 4) and aux_static.dtype == torch.float32 and aux_static.is_contiguous()
+        fo = self.feat_ok_all if feat_ok is None else feat_ok
+        self.av["counters"].zero_()
+        self.leafsum.zero_()
+        self.hist[0][: self.slot].zero_()
+        slot = self.slot
+        g0 = min(self.tiles_cap[0], self.grid)
+        nat.check(lib.h2o_hist_build(self.master.data_ptr(), self.stride, aux_static.data_ptr(), self._p("nodes0"),
+                                     self._p("tp0"), self._p("meta0"), F, self.hist[0].data_ptr(), slot, g0, s), "hist_build")
+        coll.all_reduce_(self.hist[0][:slot])
+        mono = 0 if self.mono_f is None else self.mono_f.data_ptr()
+        seed = int(seed) & _M64
+        for d in range(D):
+            if d == 0:
+                sb, sa, sr = self.master.data_ptr(), aux_static.data_ptr(), 0
+            else:
+                b = self.bufs[(d - 1) % 2]
+                sb, sa, sr = b["bins"].data_ptr(), b["aux"].data_ptr(), b["ridx"].data_ptr()
+            dst = self.bufs[d % 2]
+            hc, hn = self.hist[d % 2], self.hist[(d + 1) % 2]
+            cap = self.caps[d]
+            nat.check(lib.h2o_split_find(hc.data_ptr(), slot, self._p(f"meta{d}"), cap, F, self.nbins_f.data_ptr(),
+                                         self.iscat_f.data_ptr(), mono, p.min_w, p.min_split_improvement, p.lam,
+                                         p.alpha, p.gamma, p.mode, int(p.random_split), seed, d,
+                                         self.cand.data_ptr(), s), "split_find")
+            nat.check(lib.h2o_split_reduce(self.cand.data_ptr(), self._p(f"meta{d}"), cap, F, fo.data_ptr(), int(k_cols),
+                                           seed, d, self._p(f"dec{d}"), s), "split_reduce")
+            nat.check(lib.h2o_count(sb, self.stride, self._p(f"nodes{d}"), self._p(f"tp{d}"), self._p(f"meta{d}"),
+                                    self._p(f"dec{d}"), self.tile_cnt.data_ptr(), self.tiles_cap[d], s), "count")
+            nat.check(lib.h2o_plan(self._p(f"nodes{d}"), self._p(f"meta{d}"), self._p(f"tp{d}"), self.tile_cnt.data_ptr(),
+                                   self._p(f"dec{d}"), self.tile_off.data_ptr(), self._p(f"nl{d}"), self._p(f"cl{d}"),
+                                   self._p(f"cr{d}"), self._p(f"nodes{d + 1}"), self._p(f"tp{d + 1}"),
+                                   self._p(f"meta{d + 1}"), self._p("counters"), self.scratch.data_ptr(), d, D,
+                                   p.min_w, self.caps[d + 1], self.leaf_cap, s), "plan")
+            last = d + 1 == D
+            if not last:
+                nat.check(lib.h2o_zero_hist(hn.data_ptr(), self._p(f"nodes{d + 1}"), self._p(f"meta{d + 1}"),
+                                            self.caps[d + 1], slot, s), "zero_hist")
+            fuse = (F <= FTILE) and not last
+            g = min(self.tiles_cap[d], self.grid)
+            nat.check(lib.h2o_move(sb, sa, sr, dst["bins"].data_ptr(), dst["aux"].data_ptr(), dst["ridx"].data_ptr(),
+                                   self.stride, F, self._p(f"nodes{d}"), self._p(f"tp{d}"), self._p(f"meta{d}"),
+                                   self._p(f"dec{d}"), self.tile_off.data_ptr(), self._p(f"nl{d}"), self._p(f"cl{d}"),
+                                   self._p(f"cr{d}"), self._p(f"nodes{d + 1}"), hn.data_ptr(), slot,
+                                   self.leaf_of_row.data_ptr(), self.leafsum.data_ptr(), int(fuse), g, s), "move")
+            if not last and F > FTILE:
+                nat.check(lib.h2o_hist_build(dst["bins"].data_ptr(), self.stride, dst["aux"].data_ptr(),
+                                             self._p(f"nodes{d + 1}"), self._p(f"tp{d + 1}"), self._p(f"meta{d + 1}"),
+                                             F, hn.data_ptr(), slot, min(self.tiles_cap[d + 1], self.grid), s), "hist_build")
+            if not last:
+                coll.all_reduce_(hn[: self.caps[d + 1] * slot])
+                nat.check(lib.h2o_subtract(hn.data_ptr(), hc.data_ptr(), self._p(f"nodes{d + 1}"),
+                                           self._p(f"meta{d + 1}"), self.caps[d + 1], slot, s), "subtract")
+        coll.all_reduce_(self.leafsum)
+        if leaf_fn is not None:
+            vals = leaf_fn(self.leafsum)
+            self.av["leafval"].view(torch.float32)[: vals.numel()].copy_(vals.to(torch.float32))
+        snap = self.arena.clone()
+        rw = coll.all_reduce_(aux_static[:, 0].sum(dtype=torch.float64).reshape(1))
+        self.history.append((snap, rw))
+        return len(self.history) - 1
+
+    def fetch(self, handle) -> TreeLevels:
+        snap, rw = self.history[handle]
+        host = snap.cpu().numpy()
+        rwh = float(rw.cpu())
+        return self._decode(host, rwh)
+
+    def fetch_all(self) -> list:
+        if not self.history:
+            return []
+        snaps = torch.stack([h[0] for h in self.history]).cpu().numpy()
+        rws = torch.cat([h[1] for h in self.history]).cpu().numpy()
+        out = [self._decode(snaps[i], float(rws[i])) for i in range(len(self.history))]
+        self.history.clear()
+        return out
+
+    def _decode(self, host: np.ndarray, root_weight: float) -> TreeLevels:
+        off = {}
+        ar_off = 0
+        # recompute offsets in the same order as construction
+        for name, view in self.av.items():
+            o = view.data_ptr() - self.arena.data_ptr()
+            off[name] = (o, view.numel())
+        def arr(name, dt):
+            o, nb = off[name]
+            return host[o:o + nb].view(dt)
+        decs, cls, crs = [], [], []
+        for d in range(self.D):
+            n = int(arr(f"meta{d}", np.int32)[0])
+            if d == 0:
+                n = 1
+            if n <= 0:
+                break
+            decs.append(arr(f"dec{d}", DEC_DT)[:n].copy())
+            cls.append(arr(f"cl{d}", np.int32)[:n].astype(np.int64))
+            crs.append(arr(f"cr{d}", np.int32)[:n].astype(np.int64))
+        n_leaves = int(arr("counters", np.int32)[0])
+        vals = arr("leafval", np.float32)[:n_leaves].copy()
+        return TreeLevels(decs, cls, crs, n_leaves, vals, root_weight)
+
+
+# ================================================================================================
+def make_builder(bins: torch.Tensor, F, nbins_f, iscat_f, mono_f, max_depth, params, node_cap=1 << 14):
+    if bins.is_cuda:
+        return GpuTreeBuilder(bins, F, nbins_f, iscat_f, mono_f, max_depth, params, node_cap=node_cap)
+    return RefTreeBuilder(bins, F, nbins_f, iscat_f, mono_f, max_depth, params, node_cap=node_cap)
