@@ -25,11 +25,12 @@
 #define NBIN 256
 #define NA_BIN 255
 #define FTILE 32                // features per LDS histogram tile
-#define HSTRIDE (2 * NBIN + 2)  // floats per feature row in LDS (+2 pad: rotates banks per feature)
-#define BLK 512
+#define HS64 (2 * NBIN + 2)     // int64 entries per feature row in LDS: w at [0,256), wY at [257, 513)
+#define BLK 1024                // one 16-wave block per CU (the int64 LDS histogram is 128 KiB)
+#define NW (BLK / 64)
 #define TILE 2048               // rows per work tile
 #define LPR 8                   // lanes per row
-#define RPI (BLK / LPR)         // rows per iteration (64)
+#define RPI (BLK / LPR)         // rows per iteration (128)
 
 struct Node {      // one active node of a level (rows [start, start+len) of the level's buffer)
   int start, len, build, parent, sib, pad0, pad1, pad2;
@@ -112,21 +113,31 @@ __device__ void block_sum4(double v[4], double* scratch /* >= 4*(BLK/64) */) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// LDS histogram helpers. Layout: h[f_local * HSTRIDE + 2*bin + {0: w, 1: wY}], extra[f_local] = NA wYY,
-// extra[FTILE] = node wYY (accumulated separately in registers).
-__device__ __forceinline__ void lds_zero(float* h, int nfloats) {
-  for (int i = threadIdx.x; i < nfloats; i += blockDim.x) h[i] = 0.f;
+// LDS histogram. MEASURED on gfx950 (scripts/mb_lds_atomic.hip): ds_add_f32 runs ~12x slower than
+// integer LDS atomics (3.04 ms vs 0.25 ms for 11M x 28 updates), so bins accumulate in FIXED POINT:
+// every row's (w, wY) is scaled by a per-tree 2^40/max|.| and added as int64 (ds_add_u64). The sums
+// are exact and order independent (deterministic histograms); flushes convert to fp64 globally.
+// Layout (int64): hq[f_local * HS64 + bin] = w, hq[f_local * HS64 + 257 + bin] = wY; nayy (fp32, rare).
+#define HIST_LDS_BYTES (FTILE * HS64 * 8 + FTILE * 4)
+
+__device__ __forceinline__ void lds_zero64(long long* h, int n) {
+  for (int i = threadIdx.x; i < n; i += blockDim.x) h[i] = 0ll;
 }
 
-__device__ void flush_hist(const float* h, const float* nayy, double node_wyy, int ftile, int F,
-                           double* __restrict__ slot, int slot_doubles) {
-  // slot layout: [F][256][2] doubles, then [F] NA-wYY, then [1] node wYY
+__device__ __forceinline__ long long q64(float v, float scale) {
+  return (long long)(v * scale);   // |v*scale| <= 2^40: exact conversion of the fp32 product
+}
+
+__device__ void flush_hist(const long long* h, const float* nayy, double node_wyy, int ftile, int F,
+                           double* __restrict__ slot, const double* __restrict__ qs) {
+  // slot layout: [F][256][2] doubles, then [F] NA-wYY, then [1] node wYY.
   const int f0 = ftile * FTILE;
   const int nf = min(FTILE, F - f0);
+  const double inv_a = qs[2], inv_b = qs[3];
   for (int i = threadIdx.x; i < nf * 2 * NBIN; i += blockDim.x) {
     const int fl = i / (2 * NBIN), r = i - fl * 2 * NBIN;
-    const float v = h[fl * HSTRIDE + r];
-    if (v != 0.f) atomicAdd(slot + (size_t)(f0 + fl) * 2 * NBIN + r, (double)v);
+    const long long v = h[fl * HS64 + (r & 1) * 257 + (r >> 1)];
+    if (v != 0) atomicAdd(slot + (size_t)(f0 + fl) * 2 * NBIN + r, (double)v * ((r & 1) ? inv_b : inv_a));
   }
   for (int i = threadIdx.x; i < nf; i += blockDim.x) {
     const float v = nayy[i];
@@ -137,17 +148,51 @@ __device__ void flush_hist(const float* h, const float* nayy, double node_wyy, i
 }
 
 // accumulate one row-word (4 bins) into the LDS tile histogram
-__device__ __forceinline__ void hist_word(float* h, float* nayy, unsigned word, int wl /*word index in tile*/,
-                                          int f_abs0, int F, float a, float b, float yy) {
+__device__ __forceinline__ void hist_word(long long* h, float* nayy, unsigned word, int wl /*word index in tile*/,
+                                          int f_abs0, int F, long long qa, long long qb, float yy) {
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int fl = wl * 4 + k;
     if (f_abs0 + k < F) {
       const int bin = (word >> (8 * k)) & 0xFF;
-      float* p = h + fl * HSTRIDE + 2 * bin;
-      atomicAdd(p, a);
-      atomicAdd(p + 1, b);
+      unsigned long long* p = (unsigned long long*)(h + fl * HS64 + bin);
+      atomicAdd(p, (unsigned long long)qa);
+      atomicAdd(p + 257, (unsigned long long)qb);
       if (bin == NA_BIN) atomicAdd(nayy + fl, yy);
+    }
+  }
+}
+
+#define UNR 8   // hist: rows per lane-group in flight (memory-level parallelism: 8 independent loads per lane)
+#define MUNR 4  // k_move: rows per lane-group per partition step (MUNR*8 <= 64 for the wave-0 scan)
+
+__device__ __forceinline__ float row_yy(float a, float b) {
+  return a > 0.f ? b * b * __builtin_amdgcn_rcpf(a) : 0.f;
+}
+
+// Histogram rows [r0, r1) of one node into LDS. Loads for UNR rows are issued before any atomic.
+__device__ __forceinline__ void hist_rows(long long* h, float* nayy, const unsigned* __restrict__ bins32,
+                                          const float4* __restrict__ aux, int W, int wabs, int F, bool lead,
+                                          int r0, int r1, int g, int j, float& wyy, float sa, float sb) {
+  const float2* aux2 = (const float2*)aux;
+  for (int base = r0; base < r1; base += RPI * UNR) {
+    unsigned wd[UNR];
+    float2 ab[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int row = base + g + u * RPI;
+      const bool v = row < r1;
+      ab[u] = v ? aux2[(size_t)row * 2] : make_float2(0.f, 0.f);
+      wd[u] = (v && wabs < W) ? bins32[(size_t)row * W + wabs] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int row = base + g + u * RPI;
+      if (row < r1) {
+        const float yy = row_yy(ab[u].x, ab[u].y);
+        if (lead) wyy += yy;
+        if (wabs < W) hist_word(h, nayy, wd[u], j, wabs * 4, F, q64(ab[u].x, sa), q64(ab[u].y, sb), yy);
+      }
     }
   }
 }
@@ -158,11 +203,12 @@ __device__ __forceinline__ void hist_word(float* h, float* nayy, unsigned word, 
 __global__ __launch_bounds__(BLK) void k_hist_build(
     const uint8_t* __restrict__ bins, int stride /*bytes per row, multiple of 4*/,
     const float4* __restrict__ aux, const Node* __restrict__ nodes, const int* __restrict__ tile_prefix,
-    const int* __restrict__ meta /*[0]=n_nodes [1]=n_tiles*/, int F, double* __restrict__ hist, int slot_doubles) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* h = smem;                         // FTILE * HSTRIDE
-  float* nayy = smem + FTILE * HSTRIDE;    // FTILE
-  double* red = (double*)(nayy + FTILE);   // 64 doubles scratch
+    const int* __restrict__ meta /*[0]=n_nodes [1]=n_tiles*/, int F, double* __restrict__ hist, int slot_doubles,
+    const double* __restrict__ qs /*[sa, sb, 1/sa, 1/sb]*/) {
+  extern __shared__ __attribute__((aligned(16))) long long smem64[];
+  long long* h = smem64;                                 // FTILE * HS64
+  float* nayy = (float*)(smem64 + FTILE * HS64);         // FTILE
+  double* red = (double*)(nayy + FTILE);                 // 64 doubles scratch
 
   const int n_nodes = meta[0], n_tiles = meta[1];
   if (n_nodes <= 0 || n_tiles <= 0) return;
@@ -174,6 +220,7 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
   const int g = threadIdx.x / LPR, j = threadIdx.x % LPR;
   const int wabs = ftile * LPR + j;        // absolute word index of this lane
   const unsigned* bins32 = (const unsigned*)bins;
+  const float sa = (float)qs[0], sb = (float)qs[1];
 
   int cur = -1;
   double wyy = 0.0;
@@ -186,31 +233,26 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
         double v[4] = {wyy, 0, 0, 0};
         block_sum4(v, red);
         __syncthreads();
-        flush_hist(h, nayy, v[0], ftile, F, hist + (size_t)cur * slot_doubles, slot_doubles);
+        flush_hist(h, nayy, v[0], ftile, F, hist + (size_t)cur * slot_doubles, qs);
         __syncthreads();
       }
-      lds_zero(smem, FTILE * HSTRIDE + FTILE);
+      lds_zero64(h, FTILE * HS64);
+      for (int i = threadIdx.x; i < FTILE; i += blockDim.x) nayy[i] = 0.f;
       wyy = 0.0;
       cur = node;
       __syncthreads();
     }
     const int r0 = nd.start + (t - tile_prefix[node]) * TILE;
     const int r1 = min(r0 + TILE, nd.start + nd.len);
-    for (int row = r0 + g; row < r1; row += RPI) {
-      const float4 ax = aux[row];
-      const float yy = ax.x > 0.f ? ax.y * ax.y / ax.x : 0.f;
-      if (j == 0 && ftile == 0) wyy += yy;
-      if (wabs < W) {
-        const unsigned word = bins32[(size_t)row * W + wabs];
-        hist_word(h, nayy, word, j, wabs * 4, F, ax.x, ax.y, yy);
-      }
-    }
+    float wf = 0.f;
+    hist_rows(h, nayy, bins32, aux, W, wabs, F, j == 0 && ftile == 0, r0, r1, g, j, wf, sa, sb);
+    wyy += (double)wf;
   }
   if (cur >= 0) {
     double v[4] = {wyy, 0, 0, 0};
     block_sum4(v, red);
     __syncthreads();
-    flush_hist(h, nayy, v[0], ftile, F, hist + (size_t)cur * slot_doubles, slot_doubles);
+    flush_hist(h, nayy, v[0], ftile, F, hist + (size_t)cur * slot_doubles, qs);
   }
 }
 
@@ -661,21 +703,24 @@ __global__ void k_subtract(double* __restrict__ hist_next, const double* __restr
 // ------------------------------------------------------------------------------------------------
 // k_move: stable partition of one level into the next, fused with (a) the smaller child's histogram
 // (when F <= 32: one LDS tile covers every feature) and (b) leaf bookkeeping for rows that stop here.
+// Each lane-group (8 lanes) owns UNR rows per step; all their loads are in flight before the single
+// block-wide prefix exchange of the step (one __syncthreads per RPI*UNR = 512 rows).
 template <bool HIST>
-__global__ __launch_bounds__(BLK) void k_move(
+__global__ __launch_bounds__(BLK, 4) void k_move(
     const uint8_t* __restrict__ sbins, const float4* __restrict__ saux, const int* __restrict__ sridx /*nullable*/,
     uint8_t* __restrict__ dbins, float4* __restrict__ daux, int* __restrict__ dridx,
     int stride, int F, const Node* __restrict__ nodes, const int* __restrict__ tile_prefix,
     const int* __restrict__ meta, const Dec* __restrict__ dec, const int* __restrict__ tile_off,
     const int* __restrict__ node_nl, const int* __restrict__ child_l, const int* __restrict__ child_r,
     const Node* __restrict__ next, double* __restrict__ hist_next, int slot_doubles,
-    int* __restrict__ leaf_of_row, double* __restrict__ leafsum /*[L][2]*/) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* h = smem;
-  float* nayy = smem + FTILE * HSTRIDE;
-  double* red = (double*)(smem + FTILE * HSTRIDE + FTILE);   // 64 doubles
-  int* cnt = (int*)(red + 64);                                // [2 parity][2 side][8 waves]
-  Dec* sdec = (Dec*)(cnt + 64);                               // current node's decision
+    int* __restrict__ leaf_of_row, double* __restrict__ leafsum /*[L][2]*/, const double* __restrict__ qs) {
+  extern __shared__ __attribute__((aligned(16))) long long smem64[];
+  long long* h = smem64;
+  float* nayy = (float*)(smem64 + FTILE * HS64);
+  double* red = (double*)(nayy + FTILE);                      // 64 doubles
+  int* cnt = (int*)(red + 64);                                // [2 parity][MUNR][2 side][NW waves] + 130 prefix
+  Dec* sdec = (Dec*)(cnt + 2 * MUNR * 2 * NW + 132);          // current node's decision
+  const float sa = (float)qs[0], sb = (float)qs[1];
 
   const int n_nodes = meta[0], n_tiles = meta[1];
   if (n_nodes <= 0 || n_tiles <= 0) return;
@@ -683,9 +728,11 @@ __global__ __launch_bounds__(BLK) void k_move(
   const int t0 = blockIdx.x * per, t1 = min(n_tiles, t0 + per);
   if (t0 >= t1) return;
   const int W = stride >> 2;
+  const bool small = W <= LPR;       // whole row held by the 8 lanes of a group (one word each)
   const int g = threadIdx.x / LPR, j = threadIdx.x % LPR;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int gl = lane & ~(LPR - 1);  // group leader lane within the wave
+  const unsigned long long below = (gl == 0) ? 0ull : ((1ull << gl) - 1ull);
   const unsigned* sb32 = (const unsigned*)sbins;
   unsigned* db32 = (unsigned*)dbins;
   const float* sauxf = (const float*)saux;
@@ -706,7 +753,7 @@ __global__ __launch_bounds__(BLK) void k_move(
       double u[4] = {wyy, 0, 0, 0};
       block_sum4(u, red);
       __syncthreads();
-      flush_hist(h, nayy, u[0], 0, F, hist_next + (size_t)build_child * slot_doubles, slot_doubles);
+      flush_hist(h, nayy, u[0], 0, F, hist_next + (size_t)build_child * slot_doubles, qs);
     }
     __syncthreads();
   };
@@ -724,7 +771,10 @@ __global__ __launch_bounds__(BLK) void k_move(
       if (cl >= 0 && next[cl].build) build_child = cl;
       if (cr >= 0 && next[cr].build) build_child = cr;
       sLn = sLd = sRn = sRd = 0.0; wyy = 0.0;
-      if (HIST && build_child >= 0) lds_zero(smem, FTILE * HSTRIDE + FTILE);
+      if (HIST && build_child >= 0) {
+        lds_zero64(h, FTILE * HS64);
+        for (int i = threadIdx.x; i < FTILE; i += blockDim.x) nayy[i] = 0.f;
+      }
       if (threadIdx.x < (int)(sizeof(Dec) / 4)) ((int*)sdec)[threadIdx.x] = ((const int*)(dec + node))[threadIdx.x];
       __syncthreads();
     }
@@ -738,56 +788,98 @@ __global__ __launch_bounds__(BLK) void k_move(
     const int r1 = min(r0 + TILE, nd.start + nd.len);
     int runL = tile_off[t];                         // left rows before this tile (within node)
     int runR = tin * TILE - tile_off[t];            // right rows before this tile
-    for (int base = r0; base < r1; base += RPI) {
-      const int row = base + g;
-      const bool valid = row < r1;
-      int bin = 0;
-      if (valid && !term) bin = sbins[(size_t)row * stride + feat];
-      const bool left = valid && (term || dec_go_left(sdec, bin));
-      const bool right = valid && !left;
-      const unsigned long long mL = __ballot(left && j == 0);
-      const unsigned long long mR = __ballot(right && j == 0);
-      const unsigned long long below = (gl == 0) ? 0ull : ((1ull << gl) - 1ull);
-      const int preL = __popcll(mL & below), preR = __popcll(mR & below);
-      int* c = cnt + parity * 32;
-      if (lane == 0) { c[wid] = __popcll(mL); c[16 + wid] = __popcll(mR); }
-      __syncthreads();
-      int offL = 0, offR = 0, totL = 0, totR = 0;
-      for (int w = 0; w < (BLK >> 6); ++w) {
-        const int a = c[w], b = c[16 + w];
-        if (w < wid) { offL += a; offR += b; }
-        totL += a; totR += b;
+    float wyf = 0.f, lLn = 0.f, lLd = 0.f, lRn = 0.f, lRd = 0.f;
+    for (int base = r0; base < r1; base += RPI * MUNR) {
+      unsigned wd[MUNR];
+      float av[MUNR];
+      int rid[MUNR];
+      unsigned lmask = 0u, vmask = 0u;   // bit u: row u goes left / row u valid
+#pragma unroll
+      for (int u = 0; u < MUNR; ++u) {
+        const int row = base + g + u * RPI;
+        const bool v = row < r1;
+        vmask |= v ? (1u << u) : 0u;
+        wd[u] = (v && small && j < W) ? sb32[(size_t)row * W + j] : 0u;
+        av[u] = (v && j < 4) ? sauxf[(size_t)row * 4 + j] : 0.f;
+        rid[u] = (v && j == 4) ? (sridx ? sridx[row] : row) : 0;
       }
+      int* c = cnt + parity * (MUNR * 2 * NW);
+      int pre[MUNR];  // in-wave exclusive prefix of same-side rows (group leaders only)
+#pragma unroll
+      for (int u = 0; u < MUNR; ++u) {
+        const bool v = (vmask >> u) & 1u;
+        int bin = 0;
+        if (small) {
+          const unsigned w2 = __shfl(wd[u], gl + ((term ? 0 : feat) >> 2), 64);
+          bin = (w2 >> (8 * ((term ? 0 : feat) & 3))) & 0xFF;
+        } else if (v && !term) {
+          bin = sbins[(size_t)(base + g + u * RPI) * stride + feat];
+        }
+        const bool lf = v && (term || dec_go_left(sdec, bin));
+        lmask |= lf ? (1u << u) : 0u;
+        const unsigned long long mL = __ballot(lf && j == 0);
+        const unsigned long long mR = __ballot(v && !lf && j == 0);
+        pre[u] = lf ? __popcll(mL & below) : __popcll(mR & below);
+        if (lane == 0) { c[u * 2 * NW + wid] = __popcll(mL); c[u * 2 * NW + NW + wid] = __popcll(mR); }
+      }
+      __syncthreads();
+      // wave 0: exclusive scan over the (u, wave) order -> offsets; lane = u*NW + w (MUNR*NW <= 64)
+      if (wid == 0) {
+        const int u = lane / NW, w = lane % NW;
+        const bool in = u < MUNR;
+        const int vl = in ? c[u * 2 * NW + w] : 0, vr = in ? c[u * 2 * NW + NW + w] : 0;
+        int xl = vl, xr = vr;
+        for (int o = 1; o < 64; o <<= 1) {
+          const int yl = __shfl_up(xl, o, 64), yr = __shfl_up(xr, o, 64);
+          if (lane >= o) { xl += yl; xr += yr; }
+        }
+        int* q = cnt + 2 * MUNR * 2 * NW;           // parity-independent prefix area
+        q[lane] = xl - vl;                          // exclusive left prefix
+        q[64 + lane] = xr - vr;                     // exclusive right prefix
+        if (lane == 63) { q[128] = xl; q[129] = xr; }
+      }
+      __syncthreads();
+      const int* pfx = cnt + 2 * MUNR * 2 * NW;
+      const int totL = pfx[128], totR = pfx[129];
       parity ^= 1;
-      if (valid) {
-        const int child = left ? cl : cr;
-        const float a_ = sauxf[(size_t)row * 4 + 0];
-        const float b_ = sauxf[(size_t)row * 4 + 1];
-        const float myaux = (j < 4) ? sauxf[(size_t)row * 4 + j] : 0.f;
-        const int rid = sridx ? sridx[row] : row;
+#pragma unroll
+      for (int u = 0; u < MUNR; ++u) {
+        const int row = base + g + u * RPI;
+        // group-wide shuffles (executed by every lane)
+        const float a_ = __shfl(av[u], gl + 0, 64);
+        const float b_ = __shfl(av[u], gl + 1, 64);
+        const float num = __shfl(av[u], gl + 2, 64);
+        const float den = __shfl(av[u], gl + 3, 64);
+        const int rr = __shfl(rid[u], gl + 4, 64);
+        const bool lf = (lmask >> u) & 1u;
+        if (!((vmask >> u) & 1u)) continue;
+        const int child = lf ? cl : cr;
         if (child >= 0 && !term) {
-          const int pos = left ? (nd.start + runL + offL + preL) : (nd.start + nl + runR + offR + preR);
-          for (int w = j; w < W; w += LPR) db32[(size_t)pos * W + w] = sb32[(size_t)row * W + w];
-          if (j < 4) dauxf[(size_t)pos * 4 + j] = myaux;
-          if (j == 4) dridx[pos] = rid;
+          const int k = u * NW + wid;
+          const int pos = lf ? (nd.start + runL + pfx[k] + pre[u]) : (nd.start + nl + runR + pfx[64 + k] + pre[u]);
+          if (small) {
+            if (j < W) db32[(size_t)pos * W + j] = wd[u];
+          } else {
+            for (int w = j; w < W; w += LPR) db32[(size_t)pos * W + w] = sb32[(size_t)row * W + w];
+          }
+          if (j < 4) dauxf[(size_t)pos * 4 + j] = av[u];
+          if (j == 4) dridx[pos] = rr;
           if (HIST && child == build_child) {
-            const float yy = a_ > 0.f ? b_ * b_ / a_ : 0.f;
-            if (j == 0) wyy += yy;
-            if (j < W) {
-              const unsigned word = sb32[(size_t)row * W + j];
-              hist_word(h, nayy, word, j, j * 4, F, a_, b_, yy);
-            }
+            const float yy = row_yy(a_, b_);
+            if (j == 0) wyf += yy;
+            if (j < W) hist_word(h, nayy, wd[u], j, j * 4, F, q64(a_, sa), q64(b_, sb), yy);
           }
         } else if (j == 0) {
           // row stops here: leaf id in original order + Newton sums
           const int leaf = term ? (-1 - cl) : (-1 - child);
-          leaf_of_row[rid] = leaf;
-          const float num = sauxf[(size_t)row * 4 + 2], den = sauxf[(size_t)row * 4 + 3];
-          if (left) { sLn += num; sLd += den; } else { sRn += num; sRd += den; }
+          leaf_of_row[rr] = leaf;
+          if (lf) { lLn += num; lLd += den; } else { lRn += num; lRd += den; }
         }
       }
       runL += totL; runR += totR;
     }
+    wyy += (double)wyf;
+    sLn += (double)lLn; sLd += (double)lLd; sRn += (double)lRn; sRd += (double)lRd;
   }
   if (cur >= 0) finish_node();
 }
@@ -859,17 +951,18 @@ extern "C" {
 
 int h2o_tree_sizes(int* out) {
   out[0] = sizeof(Node); out[1] = sizeof(Dec); out[2] = sizeof(Cand); out[3] = TILE; out[4] = FTILE;
-  out[5] = (FTILE * HSTRIDE + FTILE) * 4 + 64 * 8 + 64 * 4 + (int)sizeof(Dec);  // k_move LDS bytes
+  out[5] = HIST_LDS_BYTES + 64 * 8 + (2 * MUNR * 2 * NW + 132) * 4 + (int)sizeof(Dec);  // k_move LDS bytes
+  out[6] = BLK;
   return 0;
 }
 
 int h2o_hist_build(const void* bins, int stride, const void* aux, const void* nodes, const void* tile_prefix,
-                   const void* meta, int F, void* hist, int slot_doubles, int grid, hipStream_t s) {
+                   const void* meta, int F, void* hist, int slot_doubles, const void* qs, int grid, hipStream_t s) {
   const int nft = (F + FTILE - 1) / FTILE;
-  const size_t lds = (FTILE * HSTRIDE + FTILE) * 4 + 64 * 8;
+  const size_t lds = HIST_LDS_BYTES + 64 * 8;
   hipLaunchKernelGGL(k_hist_build, dim3(grid, nft), dim3(BLK), lds, s, (const uint8_t*)bins, stride,
                      (const float4*)aux, (const Node*)nodes, (const int*)tile_prefix, (const int*)meta, F,
-                     (double*)hist, slot_doubles);
+                     (double*)hist, slot_doubles, (const double*)qs);
   return (int)hipGetLastError();
 }
 
@@ -929,21 +1022,21 @@ int h2o_subtract(void* hist_next, const void* hist_cur, const void* next, const 
 int h2o_move(const void* sbins, const void* saux, const void* sridx, void* dbins, void* daux, void* dridx,
              int stride, int F, const void* nodes, const void* tile_prefix, const void* meta, const void* dec,
              const void* tile_off, const void* node_nl, const void* child_l, const void* child_r, const void* next,
-             void* hist_next, int slot_doubles, void* leaf_of_row, void* leafsum, int fuse_hist, int grid,
-             hipStream_t s) {
-  const size_t lds_h = (FTILE * HSTRIDE + FTILE) * 4 + 64 * 8 + 64 * 4 + sizeof(Dec);
+             void* hist_next, int slot_doubles, void* leaf_of_row, void* leafsum, const void* qs, int fuse_hist,
+             int grid, hipStream_t s) {
+  const size_t lds_h = HIST_LDS_BYTES + 64 * 8 + (2 * MUNR * 2 * NW + 132) * 4 + sizeof(Dec);
   if (fuse_hist) {
     hipLaunchKernelGGL(k_move<true>, dim3(grid), dim3(BLK), lds_h, s, (const uint8_t*)sbins, (const float4*)saux,
                        (const int*)sridx, (uint8_t*)dbins, (float4*)daux, (int*)dridx, stride, F, (const Node*)nodes,
                        (const int*)tile_prefix, (const int*)meta, (const Dec*)dec, (const int*)tile_off,
                        (const int*)node_nl, (const int*)child_l, (const int*)child_r, (const Node*)next,
-                       (double*)hist_next, slot_doubles, (int*)leaf_of_row, (double*)leafsum);
+                       (double*)hist_next, slot_doubles, (int*)leaf_of_row, (double*)leafsum, (const double*)qs);
   } else {
     hipLaunchKernelGGL(k_move<false>, dim3(grid), dim3(BLK), lds_h, s, (const uint8_t*)sbins, (const float4*)saux,
                        (const int*)sridx, (uint8_t*)dbins, (float4*)daux, (int*)dridx, stride, F, (const Node*)nodes,
                        (const int*)tile_prefix, (const int*)meta, (const Dec*)dec, (const int*)tile_off,
                        (const int*)node_nl, (const int*)child_l, (const int*)child_r, (const Node*)next,
-                       (double*)hist_next, slot_doubles, (int*)leaf_of_row, (double*)leafsum);
+                       (double*)hist_next, slot_doubles, (int*)leaf_of_row, (double*)leafsum, (const double*)qs);
   }
   return (int)hipGetLastError();
 }

@@ -107,9 +107,7 @@ def binomial_metrics(y, p1, w=None, domain=("0", "1"), nbins_thresholds: int = 4
     # exact ROC over distinct scores
     order = torch.argsort(p1, descending=True)
     ps, ys, ws = p1[order], y[order], w[order]
-    uniq, inv = torch.unique_consecutive(ps, return_inverse=True)
-    pos = torch.zeros(uniq.numel(), dtype=torch.float64, device=y.device).index_add_(0, inv, ws * ys)
-    neg = torch.zeros(uniq.numel(), dtype=torch.float64, device=y.device).index_add_(0, inv, ws * (1 - ys))
+    pos, neg, uniq = _group_sorted(ps, ws * ys, ws * (1 - ys))
     auc, aucpr, tp, fp = _auc_from_sorted(pos, neg)
     # thresholds table (H2O keeps <= 400 bins)
     thr_tab = _threshold_table(uniq, tp, fp, nbins_thresholds)
@@ -127,6 +125,15 @@ def binomial_metrics(y, p1, w=None, domain=("0", "1"), nbins_thresholds: int = 4
         mm["max_criteria_and_metric_scores"] = {c: max(thr_tab, key=lambda r: r[c])[c] for c in THRESHOLD_CRITERIA}
     mm["gains_lift_table"] = gains_lift(y, p1, w)
     return mm
+
+
+def _group_sorted(keys_sorted, a, b):
+    """Per distinct key of an already-sorted key vector: sums of a and b (segmented by cumsum)."""
+    uniq, counts = torch.unique_consecutive(keys_sorted, return_counts=True)
+    ends = torch.cumsum(counts, 0) - 1
+    ca, cb = torch.cumsum(a, 0)[ends], torch.cumsum(b, 0)[ends]
+    za = torch.zeros(1, dtype=ca.dtype, device=ca.device)
+    return torch.diff(ca, prepend=za), torch.diff(cb, prepend=za), uniq
 
 
 def _threshold_table(uniq, tp, fp, nb):
@@ -206,9 +213,7 @@ def multinomial_auc(y, probs, w):
             continue
         order = torch.argsort(probs[:, k], descending=True)
         ps = probs[order, k]
-        uniq, inv = torch.unique_consecutive(ps, return_inverse=True)
-        pos = torch.zeros(uniq.numel(), dtype=torch.float64, device=y.device).index_add_(0, inv, (w * yk)[order])
-        neg = torch.zeros(uniq.numel(), dtype=torch.float64, device=y.device).index_add_(0, inv, (w * (1 - yk))[order])
+        pos, neg, _ = _group_sorted(ps, (w * yk)[order], (w * (1 - yk))[order])
         aucs.append(_auc_from_sorted(pos, neg)[0])
     return float(np.mean(aucs)) if aucs else float("nan")
 

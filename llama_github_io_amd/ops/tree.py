@@ -346,7 +346,7 @@ class GpuTreeBuilder:
     """Drives the HIP tree kernels. ``bins`` is a CUDA uint8 tensor [N, stride] (stride % 4 == 0)."""
 
     def __init__(self, bins: torch.Tensor, F: int, nbins_f, iscat_f, mono_f, max_depth: int, params: SplitParams,
-                 node_cap: int = 1 << 14, grid: int = 512):
+                 node_cap: int = 1 << 14, grid: int = 256):
         assert bins.is_cuda and bins.dtype == torch.uint8 and bins.dim() == 2
         self.lib = nat.hip()
         sz = np.zeros(8, dtype=np.int32)
@@ -381,6 +381,7 @@ class GpuTreeBuilder:
         self.iscat_f = torch.as_tensor(np.asarray(iscat_f, dtype=np.int32), device=dev)
         self.mono_f = None if mono_f is None else torch.as_tensor(np.asarray(mono_f, dtype=np.int32), device=dev)
         self.feat_ok_all = torch.ones(F, dtype=torch.int32, device=dev)
+        self.qs = torch.empty(4, dtype=torch.float64, device=dev)   # fixed-point scales [sa, sb, 1/sa, 1/sb]
         # ping-pong row payload buffers
         self.bufs = [dict(bins=torch.empty(N, self.stride, dtype=torch.uint8, device=dev),
                           aux=torch.empty(N, 4, dtype=torch.float32, device=dev),
@@ -426,9 +427,15 @@ class GpuTreeBuilder:
         self.leafsum.zero_()
         self.hist[0][: self.slot].zero_()
         slot = self.slot
+        # per-tree fixed-point scales for the int64 LDS histograms: |v| * 2^40 / max|v| <= 2^40
+        amax = aux_static[:, :2].abs().amax(0).double()
+        sc = torch.where(amax > 0, (2.0 ** 40) / amax, torch.ones_like(amax))
+        self.qs[:2] = sc
+        self.qs[2:] = 1.0 / sc
+        qs = self.qs.data_ptr()
         g0 = min(self.tiles_cap[0], self.grid)
         nat.check(lib.h2o_hist_build(self.master.data_ptr(), self.stride, aux_static.data_ptr(), self._p("nodes0"),
-                                     self._p("tp0"), self._p("meta0"), F, self.hist[0].data_ptr(), slot, g0, s), "hist_build")
+                                     self._p("tp0"), self._p("meta0"), F, self.hist[0].data_ptr(), slot, qs, g0, s), "hist_build")
         coll.all_reduce_(self.hist[0][:slot])
         mono = 0 if self.mono_f is None else self.mono_f.data_ptr()
         seed = int(seed) & _M64
@@ -464,11 +471,11 @@ class GpuTreeBuilder:
                                    self.stride, F, self._p(f"nodes{d}"), self._p(f"tp{d}"), self._p(f"meta{d}"),
                                    self._p(f"dec{d}"), self.tile_off.data_ptr(), self._p(f"nl{d}"), self._p(f"cl{d}"),
                                    self._p(f"cr{d}"), self._p(f"nodes{d + 1}"), hn.data_ptr(), slot,
-                                   self.leaf_of_row.data_ptr(), self.leafsum.data_ptr(), int(fuse), g, s), "move")
+                                   self.leaf_of_row.data_ptr(), self.leafsum.data_ptr(), qs, int(fuse), g, s), "move")
             if not last and F > FTILE:
                 nat.check(lib.h2o_hist_build(dst["bins"].data_ptr(), self.stride, dst["aux"].data_ptr(),
                                              self._p(f"nodes{d + 1}"), self._p(f"tp{d + 1}"), self._p(f"meta{d + 1}"),
-                                             F, hn.data_ptr(), slot, min(self.tiles_cap[d + 1], self.grid), s), "hist_build")
+                                             F, hn.data_ptr(), slot, qs, min(self.tiles_cap[d + 1], self.grid), s), "hist_build")
             if not last:
                 coll.all_reduce_(hn[: self.caps[d + 1] * slot])
                 nat.check(lib.h2o_subtract(hn.data_ptr(), hc.data_ptr(), self._p(f"nodes{d + 1}"),
