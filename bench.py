@@ -98,6 +98,7 @@ def main():
             return super()._prepare(t, k)
 
         def _finish(self, model, built):
+            super()._finish(model, built)
             coll.barrier()
             if dev.type == "cuda":
                 torch.cuda.synchronize()

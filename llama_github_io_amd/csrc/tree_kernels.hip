@@ -945,6 +945,34 @@ __global__ void k_predict(const float* __restrict__ X, long long N, int K,
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Fixed-point scales of the int64 LDS histograms: max |aux.x|, |aux.y| -> qs = [2^40/max, .., max/2^40, ..]
+__global__ __launch_bounds__(256) void k_amax(const float4* __restrict__ aux, long long N, unsigned* __restrict__ amax_bits) {
+  float ma = 0.f, mb = 0.f;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += (long long)gridDim.x * blockDim.x) {
+    const float2 v = *(const float2*)(aux + i);
+    ma = fmaxf(ma, fabsf(v.x));
+    mb = fmaxf(mb, fabsf(v.y));
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    ma = fmaxf(ma, __shfl_xor(ma, off, 64));
+    mb = fmaxf(mb, __shfl_xor(mb, off, 64));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMax(amax_bits + 0, __float_as_uint(ma));
+    atomicMax(amax_bits + 1, __float_as_uint(mb));
+  }
+}
+
+__global__ void k_qscale(const unsigned* __restrict__ amax_bits, double* __restrict__ qs) {
+  if (threadIdx.x < 2) {
+    const double m = (double)__uint_as_float(amax_bits[threadIdx.x]);
+    const double sc = (m > 0.0 && m == m) ? 1099511627776.0 / m : 1.0;   // 2^40 / max
+    qs[threadIdx.x] = sc;
+    qs[2 + threadIdx.x] = 1.0 / sc;
+  }
+}
+
 // ================================================================================================
 // C ABI launchers (called through ctypes with raw device pointers and the current HIP stream).
 extern "C" {
@@ -1038,6 +1066,19 @@ int h2o_move(const void* sbins, const void* saux, const void* sridx, void* dbins
                        (const int*)node_nl, (const int*)child_l, (const int*)child_r, (const Node*)next,
                        (double*)hist_next, slot_doubles, (int*)leaf_of_row, (double*)leafsum, (const double*)qs);
   }
+  return (int)hipGetLastError();
+}
+
+int h2o_amax(const void* aux, long long N, void* amax_bits, hipStream_t s) {
+  long long grid = (N + 255) / 256;
+  if (grid > 2048) grid = 2048;
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL(k_amax, dim3((unsigned)grid), dim3(256), 0, s, (const float4*)aux, N, (unsigned*)amax_bits);
+  return (int)hipGetLastError();
+}
+
+int h2o_qscale(const void* amax_bits, void* qs, hipStream_t s) {
+  hipLaunchKernelGGL(k_qscale, dim3(1), dim3(64), 0, s, (const unsigned*)amax_bits, (double*)qs);
   return (int)hipGetLastError();
 }
 

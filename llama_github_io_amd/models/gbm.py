@@ -20,6 +20,9 @@ from .base import DataInfo
 from .distributions import ORDER_STAT_DISTS, get_distribution
 from .shared_tree import SharedTreeModel, SharedTreeTrainer
 
+_FUSED_DIST = {"gaussian": 0, "bernoulli": 1, "quasibinomial": 2, "poisson": 3, "gamma": 4, "tweedie": 5,
+               "laplace": 6, "quantile": 7, "huber": 8, "modified_huber": 9}
+
 GBM_DEFAULTS = dict(ntrees=50, max_depth=5, min_rows=10.0, learn_rate=0.1, learn_rate_annealing=1.0,
                     sample_rate=1.0, col_sample_rate=1.0, col_sample_rate_change_per_level=1.0,
                     col_sample_rate_per_tree=1.0, distribution="AUTO", tweedie_power=1.5, quantile_alpha=0.5,
@@ -120,16 +123,38 @@ class GBMTrainer(SharedTreeTrainer):
     def _lr(self, t):
         return float(self.p["learn_rate"]) * float(self.p["learn_rate_annealing"]) ** t
 
+    def _fused(self):
+        return self.dev.type == "cuda" and self.K == 1 and self.dname in _FUSED_DIST
+
     def _prepare(self, t, k):
         d = self.dist
         f = self.f[:, k]
+        if k == 0 and self.dname == "huber":
+            self._flush_pending()
+            r = (self.y - f).abs()
+            self.dist.huber_delta = float(torch.quantile(r.double()[: 1 << 24], self.p["huber_alpha"]))
+        if self._fused():
+            # one HIP pass: previous tree's f update + sampling + residuals + leaf terms + scale maxima
+            from ..ops import _native as nat
+            if not hasattr(self, "_amax"):
+                self._amax = torch.zeros(2, dtype=torch.int32, device=self.dev)
+                self._wbuf = None if self.w is None or bool((self.w == 1).all()) else self.w.contiguous()
+            self._amax.zero_()
+            pv, pl = self._pending if getattr(self, "_pending", None) is not None else (None, None)
+            p1 = {"tweedie": self.p["tweedie_power"], "quantile": self.p["quantile_alpha"],
+                  "huber": getattr(self.dist, "huber_delta", 1.0)}.get(self.dname, 0.0)
+            nat.call("h2o_gbm_step", self.N, _FUSED_DIST[self.dname], self.y.data_ptr(),
+                     0 if self._wbuf is None else self._wbuf.data_ptr(), self.f.data_ptr(),
+                     0 if pv is None else pv.data_ptr(), 0 if pl is None else pl.data_ptr(),
+                     float(self.p["sample_rate"]), (self.seed * 0x9E3779B1 + t * 7919) & ((1 << 64) - 1),
+                     float(p1), self.aux.data_ptr(), self._amax.data_ptr(), nat.stream_ptr(self.dev))
+            self._pending = None
+            self.w_eff = None
+            return self.aux
         if k == 0:
             self.w_eff = self._row_sample(float(self.p["sample_rate"]), t)
             if self.K > 1:
                 self.probs = torch.softmax(self.f, dim=1)
-            if self.dname == "huber":
-                r = (self.y - f).abs()
-                self.dist.huber_delta = float(torch.quantile(r.double()[: 1 << 24], self.p["huber_alpha"]))
         w = self.w_eff
         if self.K > 1:
             y = self.yk[:, k]
@@ -144,6 +169,17 @@ class GBMTrainer(SharedTreeTrainer):
         a[:, 3] = d.gamma_denom(w, y, z, f)
         self._z = z
         return a
+
+    def _amax_for_build(self):
+        return self._amax if self._fused() else None
+
+    def _flush_pending(self):
+        pend = getattr(self, "_pending", None)
+        if pend is not None:
+            from ..ops import _native as nat
+            vals, leaf = pend
+            nat.call("h2o_add_leaf", self.N, self.f.data_ptr(), 1, vals.data_ptr(), leaf.data_ptr(), nat.stream_ptr(self.dev))
+            self._pending = None
 
     def _leaf_values(self, ls, t, k):
         d = self.dist
@@ -164,9 +200,10 @@ class GBMTrainer(SharedTreeTrainer):
 
     def _order_stat_leaves(self, L, k):
         """Weighted per-leaf median (laplace) / alpha-quantile (quantile) / huber leaf of y - f."""
+        self._flush_pending()
         leaf = self.builder.leaf_of_row.long()
         diff = (self.y - self.f[:, k]).double()
-        w = self.w_eff.double()
+        w = (self.aux[:, 0] if self.w_eff is None else self.w_eff).double()
         alpha = self.p["quantile_alpha"] if self.dname == "quantile" else 0.5
         order = torch.argsort(diff)
         leaf_s = leaf[order]
@@ -193,9 +230,16 @@ class GBMTrainer(SharedTreeTrainer):
 
     def _update(self, t, k):
         leaf = self.builder.leaf_of_row
+        if self._fused():
+            self._pending = (self._vals, leaf)   # applied by the next fused step (or _flush_pending)
+            return
         self.f[:, k] += self._vals[leaf.long()]
 
+    def _finish(self, model, built):
+        self._flush_pending()
+
     def _training_metrics(self, model):
+        self._flush_pending()
         f = self.f
         y, w = self.y, self.w
         if self.K > 1:

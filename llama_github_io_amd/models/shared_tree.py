@@ -169,8 +169,12 @@ class SharedTreeTrainer:
             feat_ok = self._tree_feature_mask(rng, F)
             for k in range(K):
                 aux = self._prepare(t, k)
+                kw = {}
+                am = self._amax_for_build()
+                if am is not None:
+                    kw["amax_bits"] = am
                 h = self.builder.build(aux, feat_ok, self._k_cols(F), seed=(self.seed * 1000003 + t * 97 + k) & ((1 << 63) - 1),
-                                       leaf_fn=lambda ls, t=t, k=k: self._leaf_values(ls, t, k))
+                                       leaf_fn=lambda ls, t=t, k=k: self._leaf_values(ls, t, k), **kw)
                 self._update(t, k)
                 handles.append((h, k))
             built = t + 1
@@ -254,6 +258,9 @@ class SharedTreeTrainer:
         return ev
 
     # defaults, overridden
+    def _amax_for_build(self):
+        return None
+
     def _init_model(self, model):
         pass
 

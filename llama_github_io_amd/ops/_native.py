@@ -32,6 +32,11 @@ _HIP_SIGS = {
     "h2o_subtract": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
     "h2o_move": [c_void_p] * 6 + [c_int, c_int] + [c_void_p] * 9 + [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
     "h2o_bin_assign": [c_void_p, c_ll, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
+    "h2o_amax": [c_void_p, c_ll, c_void_p, c_void_p],
+    "h2o_qscale": [c_void_p, c_void_p, c_void_p],
+    "h2o_gbm_step": [c_ll, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_float, c_ull,
+                     ctypes.c_float, c_void_p, c_void_p, c_void_p],
+    "h2o_add_leaf": [c_ll, c_void_p, c_int, c_void_p, c_void_p, c_void_p],
     "h2o_predict": [c_void_p, c_ll, c_int] + [c_void_p] * 11 + [c_int, c_void_p, c_void_p, c_void_p],
 }
 

@@ -382,6 +382,7 @@ class GpuTreeBuilder:
         self.mono_f = None if mono_f is None else torch.as_tensor(np.asarray(mono_f, dtype=np.int32), device=dev)
         self.feat_ok_all = torch.ones(F, dtype=torch.int32, device=dev)
         self.qs = torch.empty(4, dtype=torch.float64, device=dev)   # fixed-point scales [sa, sb, 1/sa, 1/sb]
+        self.amax_bits = torch.zeros(2, dtype=torch.int32, device=dev)
         # ping-pong row payload buffers
         self.bufs = [dict(bins=torch.empty(N, self.stride, dtype=torch.uint8, device=dev),
                           aux=torch.empty(N, 4, dtype=torch.float32, device=dev),
@@ -416,9 +417,11 @@ class GpuTreeBuilder:
         return self.av[name].data_ptr()
 
     def build(self, aux_static: torch.Tensor, feat_ok: torch.Tensor | None = None, k_cols: int = 0, seed: int = 0,
-              leaf_fn=None):
+              leaf_fn=None, amax_bits: torch.Tensor | None = None):
         """Launch one tree. ``leaf_fn(leafsum[L,2] f64) -> leaf values f32`` runs on device before the
-        arena snapshot, so values travel to the host with the structure (no extra sync)."""
+        arena snapshot, so values travel to the host with the structure (no extra sync).
+        ``amax_bits`` (int32[2], max |aux.x|, |aux.y| as float bits) may be produced by a fused prepare
+        kernel; otherwise it is computed here."""
         lib, s = self.lib, nat.stream_ptr(self.dev)
         F, D, p, T = self.F, self.D, self.p, self.TILE
         assert aux_static.shape == (self.N, 4) and aux_static.dtype == torch.float32 and aux_static.is_contiguous()
@@ -428,10 +431,11 @@ class GpuTreeBuilder:
         self.hist[0][: self.slot].zero_()
         slot = self.slot
         # per-tree fixed-point scales for the int64 LDS histograms: |v| * 2^40 / max|v| <= 2^40
-        amax = aux_static[:, :2].abs().amax(0).double()
-        sc = torch.where(amax > 0, (2.0 ** 40) / amax, torch.ones_like(amax))
-        self.qs[:2] = sc
-        self.qs[2:] = 1.0 / sc
+        if amax_bits is None:
+            amax_bits = self.amax_bits
+            amax_bits.zero_()
+            nat.check(lib.h2o_amax(aux_static.data_ptr(), self.N, amax_bits.data_ptr(), s), "amax")
+        nat.check(lib.h2o_qscale(amax_bits.data_ptr(), self.qs.data_ptr(), s), "qscale")
         qs = self.qs.data_ptr()
         g0 = min(self.tiles_cap[0], self.grid)
         nat.check(lib.h2o_hist_build(self.master.data_ptr(), self.stride, aux_static.data_ptr(), self._p("nodes0"),
@@ -454,8 +458,9 @@ class GpuTreeBuilder:
                                          self.cand.data_ptr(), s), "split_find")
             nat.check(lib.h2o_split_reduce(self.cand.data_ptr(), self._p(f"meta{d}"), cap, F, fo.data_ptr(), int(k_cols),
                                            seed, d, self._p(f"dec{d}"), s), "split_reduce")
-            nat.check(lib.h2o_count(sb, self.stride, self._p(f"nodes{d}"), self._p(f"tp{d}"), self._p(f"meta{d}"),
-                                    self._p(f"dec{d}"), self.tile_cnt.data_ptr(), self.tiles_cap[d], s), "count")
+            if d + 1 < D:  # the last level moves no rows: its partition offsets are never used
+                nat.check(lib.h2o_count(sb, self.stride, self._p(f"nodes{d}"), self._p(f"tp{d}"), self._p(f"meta{d}"),
+                                        self._p(f"dec{d}"), self.tile_cnt.data_ptr(), self.tiles_cap[d], s), "count")
             nat.check(lib.h2o_plan(self._p(f"nodes{d}"), self._p(f"meta{d}"), self._p(f"tp{d}"), self.tile_cnt.data_ptr(),
                                    self._p(f"dec{d}"), self.tile_off.data_ptr(), self._p(f"nl{d}"), self._p(f"cl{d}"),
                                    self._p(f"cr{d}"), self._p(f"nodes{d + 1}"), self._p(f"tp{d + 1}"),
