@@ -117,7 +117,7 @@ def main():
     tm = model.output["training_metrics"]
     if rank == 0:
         print(json.dumps({
-            "metric": "GBM train rows/sec (100 trees, depth 6) on HIGGS-11M",
+            "metric": "GBM train rows/sec (100 trees, depth 6) on HIGGS-11M at 1/2/4/8 MI355X",
             "value": round(rows_per_sec, 1), "unit": "rows/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "fp32", "data": "synthetic HIGGS-shaped 11M x 28",
