@@ -1,2 +1,281 @@
-"""H2O-compatible Python API backed by the MI355X-native engine (``llama_github_io_amd``)."""
+"""H2O-compatible Python API backed by the MI355X-native engine (``llama_github_io_amd``).
+
+Reference: ``h2o-py/h2o/h2o.py``. ``h2o.init()`` boots the in-process engine (no JVM, no REST hop):
+frames live in HBM on this process's GPU, models train through the HIP kernels, and with torchrun
+(``WORLD_SIZE>1``) every rank joins the RCCL process group and holds its row shard.
+"""
+from __future__ import annotations
+
 __version__ = "3.46.0.amd0"
+
+import os as _os
+import sys as _sys
+
+_ROOT = _os.path.dirname(_os.path.dirname(_os.path.abspath(__file__)))
+if _ROOT not in _sys.path:
+    _sys.path.insert(0, _ROOT)
+
+from llama_github_io_amd.core import dkv as _dkv  # noqa: E402
+from llama_github_io_amd.core import runtime as _rt  # noqa: E402
+from llama_github_io_amd.frame import H2OFrame  # noqa: E402
+from llama_github_io_amd import frame_ops as _fops  # noqa: E402
+from llama_github_io_amd.io import parse as _parse  # noqa: E402
+
+from . import estimators  # noqa: E402,F401
+
+_progress = [True]
+
+
+class _Cluster:
+    def show_status(self, detailed=False):
+        st = _rt.cluster_status()
+        print(st)
+        return st
+
+    def status(self):
+        return _rt.cluster_status()
+
+    @property
+    def cloud_name(self):
+        return _rt.cluster_status()["cloud_name"]
+
+    @property
+    def cloud_size(self):
+        return _rt.cluster_status()["cloud_size"]
+
+    def shutdown(self, prompt=False):
+        _rt.shutdown()
+
+    def is_running(self):
+        return _rt.is_running()
+
+    @property
+    def version(self):
+        return __version__
+
+
+_cluster = _Cluster()
+
+
+def init(url=None, ip=None, port=None, name=None, nthreads=-1, max_mem_size=None, min_mem_size=None, strict_version_check=None,
+         enable_assertions=True, verbose=True, **kwargs):
+    """Start (or attach to) the in-process engine. Connection arguments are accepted for API
+    compatibility; use ``h2o.connect(url=...)`` semantics via the REST server for remote use."""
+    st = _rt.init(name=name)
+    if verbose:
+        dev = st["device"]
+        print(f"H2O (MI355X-native) {__version__} cloud '{st['cloud_name']}' size {st['cloud_size']} on {dev}")
+    return _cluster
+
+
+def connect(server=None, url=None, ip=None, port=None, verbose=True, config=None, **kw):
+    return init(verbose=verbose)
+
+
+def cluster():
+    return _cluster
+
+
+def shutdown(prompt=False):
+    _rt.shutdown()
+
+
+def no_progress():
+    _progress[0] = False
+
+
+def show_progress():
+    _progress[0] = True
+
+
+# ---- frames
+def import_file(path=None, destination_frame=None, parse=True, header=0, sep=None, col_names=None, col_types=None,
+                na_strings=None, pattern=None, skipped_columns=None, custom_non_data_line_markers=None,
+                partition_by=None, quotechar=None, escapechar=None):
+    return _parse.import_file(path, destination_frame, parse, header, sep, col_names, col_types, na_strings, pattern,
+                              skipped_columns, custom_non_data_line_markers, partition_by, quotechar, escapechar)
+
+
+def upload_file(path, destination_frame=None, header=0, sep=None, col_names=None, col_types=None, na_strings=None,
+                skipped_columns=None, quotechar=None, escapechar=None):
+    return _parse.upload_file(path, destination_frame, header, sep, col_names, col_types, na_strings, skipped_columns)
+
+
+def parse_setup(raw_frames, destination_frame=None, header=0, separator=None, column_names=None, column_types=None,
+                na_strings=None, **kw):
+    return _parse.parse_setup(raw_frames, destination_frame, header, separator, column_names, column_types, na_strings)
+
+
+def parse_raw(setup, id=None, first_line_is_header=0):
+    src = setup["source_frames"][0]["name"]
+    return _parse.import_file(src, id or setup.get("destination_frame"), header=first_line_is_header,
+                              sep=setup.get("separator"), col_names=setup.get("column_names"))
+
+
+def export_file(frame, path, force=False, sep=",", compression=None, parts=1, header=True, quote_header=True,
+                parallel=False, format="csv"):
+    return _parse.export_file(frame, path, force, sep, header, quote_header, parts, compression)
+
+
+def save_frame(frame, dir_path, force=True):
+    return _parse.save_frame(frame, dir_path, force)
+
+
+def load_frame(frame_id, dir_path, force=True):
+    return _parse.load_frame(frame_id, dir_path)
+
+
+def create_frame(frame_id=None, rows=10000, cols=10, randomize=True, real_fraction=None, categorical_fraction=None,
+                 integer_fraction=None, binary_fraction=None, time_fraction=None, string_fraction=None, value=0,
+                 real_range=100, factors=100, integer_range=100, binary_ones_fraction=0.02, missing_fraction=0.01,
+                 has_response=False, response_factors=2, positive_response=False, seed=None, seed_for_column_types=None):
+    kw = dict(rows=rows, cols=cols, randomize=randomize, value=value, real_range=real_range, factors=factors,
+              integer_range=integer_range, binary_ones_fraction=binary_ones_fraction, missing_fraction=missing_fraction,
+              has_response=has_response, response_factors=response_factors, positive_response=positive_response,
+              seed=seed, seed_for_column_types=seed_for_column_types, frame_id=frame_id)
+    for k, v in (("categorical_fraction", categorical_fraction), ("integer_fraction", integer_fraction),
+                 ("binary_fraction", binary_fraction), ("time_fraction", time_fraction),
+                 ("string_fraction", string_fraction)):
+        if v is not None:
+            kw[k] = v
+    return _fops.create_frame(**kw)
+
+
+def interaction(data, factors, pairwise, max_factors, min_occurrence, destination_frame=None):
+    return _fops.interaction(data, factors, pairwise, max_factors, min_occurrence)
+
+
+def insert_missing_values(frame, fraction=0.1, seed=None):
+    return _fops.insert_missing_values(frame, fraction, seed)
+
+
+def deep_copy(data, xid):
+    cols = [c.copy() for c in data._cols.values()]
+    return H2OFrame._from_columns(cols, xid)
+
+
+def assign(data, xid):
+    _dkv.remove(data.frame_id) if _dkv.contains(data.frame_id) else None
+    data.frame_id = xid
+    _dkv.put(xid, data)
+    return data
+
+
+def as_list(data, use_pandas=True, header=True):
+    df = data.as_data_frame(use_pandas=True)
+    if use_pandas:
+        return df
+    rows = df.values.tolist()
+    return ([list(df.columns)] + rows) if header else rows
+
+
+# ---- DKV
+def get_frame(frame_id, **kw):
+    v = _dkv.get(frame_id)
+    return v if isinstance(v, H2OFrame) else None
+
+
+def get_model(model_id):
+    from llama_github_io_amd.models.base import Model
+    v = _dkv.get(model_id)
+    return v if isinstance(v, Model) else None
+
+
+def get_grid(grid_id):
+    return _dkv.get(grid_id)
+
+
+def get_job(job_id):
+    return _dkv.get(job_id)
+
+
+def ls():
+    import pandas as pd
+    return pd.DataFrame({"key": _dkv.keys()})
+
+
+def frames():
+    return [k for k, v in _dkv.items() if isinstance(v, H2OFrame)]
+
+
+def remove(x, cascade=True):
+    xs = x if isinstance(x, (list, tuple)) else [x]
+    for o in xs:
+        key = o if isinstance(o, str) else getattr(o, "frame_id", None) or getattr(o, "model_id", None) or getattr(o, "key", None)
+        if key is not None and _dkv.contains(key):
+            _dkv.remove(key)
+
+
+def remove_all(retained=None):
+    keep = []
+    for r in retained or []:
+        keep.append(r if isinstance(r, str) else getattr(r, "frame_id", None) or getattr(r, "model_id", None))
+    _dkv.remove_all(keep)
+
+
+# ---- models: persistence & MOJO
+def save_model(model, path="", force=False, export_cross_validation_predictions=False, filename=None):
+    from llama_github_io_amd import persist
+    return persist.save_model(getattr(model, "_model", None) or model, path, force, filename)
+
+
+def load_model(path):
+    from llama_github_io_amd import persist
+    return persist.load_model(path)
+
+
+download_model = save_model
+upload_model = load_model
+
+
+def import_mojo(mojo_path, model_id=None):
+    from llama_github_io_amd.mojo import reader
+    return reader.import_mojo(mojo_path, model_id)
+
+
+upload_mojo = import_mojo
+
+
+def print_mojo(mojo_path, format="json", tree_index=None):
+    from llama_github_io_amd.mojo import reader
+    return reader.print_mojo(mojo_path, format, tree_index)
+
+
+def make_metrics(predicted, actual, domain=None, distribution=None, weights=None, auc_type="NONE"):
+    import torch
+    from llama_github_io_amd import metrics as mm
+    P = predicted.as_tensor(dtype=torch.float32)
+    a = actual._col(0)
+    if domain is not None or a.type == "enum":
+        dom = list(domain or a.domain)
+        from llama_github_io_amd.frame import _remap_codes
+        y = _remap_codes(a, dom, P.device)
+        cat = "Binomial" if len(dom) == 2 else "Multinomial"
+        if cat == "Binomial" and P.shape[1] == 1:
+            P = P[:, 0]
+    else:
+        y, dom, cat = a.as_float().float(), None, "Regression"
+        P = P[:, 0]
+    w = None if weights is None else weights.as_tensor(dtype=torch.float32)[:, 0]
+    return mm.make_metrics(cat, y, P, w, dom, distribution)
+
+
+def download_pojo(model, path="", get_jar=True, jar_name=""):
+    raise NotImplementedError("POJO (Java source) export is not provided by the MI355X-native engine; use download_mojo")
+
+
+def flow():
+    raise NotImplementedError("the Flow web UI is not shipped; use the REST API (python -m llama_github_io_amd.api.server)")
+
+
+def cluster_status():
+    return _rt.cluster_status()
+
+
+def set_s3_credentials(*a, **k):
+    raise NotImplementedError("no network persistence backends in this build")
+
+
+from . import grid, automl  # noqa: E402,F401
+from .grid import H2OGridSearch  # noqa: E402,F401
+from .automl import H2OAutoML, get_leaderboard  # noqa: E402,F401

@@ -1,0 +1,110 @@
+// DeepLearning layer epilogues (reference: h2o-algos/src/main/java/hex/deeplearning/Neurons.java —
+// fprop: bias add + activation (+ input/hidden dropout); bprop: dE/dnet = dE/dout * act'(net)).
+//
+// The GEMMs themselves go to hipBLASLt through torch; these kernels fuse everything elementwise
+// around them so each layer touches its activation tensor once per direction:
+//   fwd: out = act(x + b) * mask/keep   (mask from a counter-based hash of (seed, element): no RNG
+//        state, reproducible, regenerated in bwd instead of stored)
+//   bwd: gx = gout * mask/keep * act'(.)  and the bias gradient column sums (LDS tree + one fp32
+//        atomic per column per workgroup).
+// Activations: 0 linear, 1 Rectifier (ReLU), 2 Tanh, 3 ExpRectifier (ELU).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+__device__ __forceinline__ uint32_t hash32(uint64_t x) {
+  x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL; x ^= x >> 33;
+  return (uint32_t)x;
+}
+
+__device__ __forceinline__ float act_f(int a, float v) {
+  switch (a) {
+    case 1: return v > 0.f ? v : 0.f;
+    case 2: return tanhf(v);
+    case 3: return v > 0.f ? v : expm1f(v);
+    default: return v;
+  }
+}
+
+// derivative expressed through the activation OUTPUT y (what bwd keeps)
+__device__ __forceinline__ float dact_from_y(int a, float y) {
+  switch (a) {
+    case 1: return y > 0.f ? 1.f : 0.f;
+    case 2: return 1.f - y * y;
+    case 3: return y > 0.f ? 1.f : y + 1.f;
+    default: return 1.f;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_bias_act_fwd(const float* __restrict__ x, const float* __restrict__ b,
+                                                      float* __restrict__ y, int64_t rows, int cols, int act,
+                                                      float drop, uint64_t seed) {
+  const int64_t n = rows * (int64_t)cols;
+  const float keep = 1.f - drop;
+  const uint32_t thr = (uint32_t)(drop * 4294967296.0);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % cols);
+    float v = act_f(act, x[i] + (b ? b[c] : 0.f));
+    if (drop > 0.f) v = (hash32(seed ^ (uint64_t)i * 0x9E3779B97F4A7C15ULL) < thr) ? 0.f : v / keep;
+    y[i] = v;
+  }
+}
+
+// gx[i] = gy[i] * mask * act'(y); db[c] += sum_r gx[r, c]
+__global__ __launch_bounds__(256) void k_bias_act_bwd(const float* __restrict__ gy, const float* __restrict__ y,
+                                                      float* __restrict__ gx, float* __restrict__ db, int64_t rows,
+                                                      int cols, int act, float drop, uint64_t seed, int rows_per_block) {
+  // block handles a [rows_per_block x 64] column stripe: thread (ty, tx) with tx = column lane
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tx;
+  const int64_t rbeg = (int64_t)blockIdx.y * rows_per_block;
+  int64_t rend = rbeg + rows_per_block;
+  if (rend > rows) rend = rows;
+  const float keep = 1.f - drop;
+  const uint32_t thr = (uint32_t)(drop * 4294967296.0);
+  float acc = 0.f;
+  if (c < cols) {
+    for (int64_t r = rbeg + ty; r < rend; r += 4) {
+      const int64_t i = r * cols + c;
+      float yy = y[i];
+      float g = gy[i];
+      if (drop > 0.f) {
+        const bool dropped = hash32(seed ^ (uint64_t)i * 0x9E3779B97F4A7C15ULL) < thr;
+        g = dropped ? 0.f : g / keep;
+        yy = dropped ? 0.f : yy * keep;  // stored y was scaled by 1/keep
+      }
+      const float v = g * dact_from_y(act, yy);
+      gx[i] = v;
+      acc += v;
+    }
+  }
+  __shared__ float red[4][64];
+  red[ty][tx] = acc;
+  __syncthreads();
+  if (ty == 0 && c < cols && db) atomicAdd(&db[c], red[0][tx] + red[1][tx] + red[2][tx] + red[3][tx]);
+}
+
+}  // namespace
+
+extern "C" {
+
+int h2o_bias_act_fwd(const float* x, const float* b, float* y, long long rows, int cols, int act, float drop,
+                     unsigned long long seed, hipStream_t stream) {
+  const long long n = rows * (long long)cols;
+  int grid = (int)((n + 255) / 256);
+  if (grid > 8192) grid = 8192;
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL(k_bias_act_fwd, dim3(grid), dim3(256), 0, stream, x, b, y, (int64_t)rows, cols, act, drop, seed);
+  return (int)hipGetLastError();
+}
+
+int h2o_bias_act_bwd(const float* gy, const float* y, float* gx, float* db, long long rows, int cols, int act,
+                     float drop, unsigned long long seed, hipStream_t stream) {
+  const int rpb = 256;
+  dim3 grid((cols + 63) / 64, (unsigned)((rows + rpb - 1) / rpb));
+  hipLaunchKernelGGL(k_bias_act_bwd, grid, dim3(256), 0, stream, gy, y, gx, db, (int64_t)rows, cols, act, drop, seed, rpb);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -333,10 +333,21 @@ __global__ __launch_bounds__(256) void k_split_find(
   const double min_w = p.min_w;
   const bool random_mode = p.random_split != 0;
   int rand_b = -1;
-  if (random_mode && nb > 1) {
-    unsigned long long hsh = splitmix64(p.seed ^ ((unsigned long long)level << 48) ^
-                                        ((unsigned long long)node << 20) ^ (unsigned long long)f);
-    rand_b = 1 + (int)(hsh % (unsigned long long)(nb - 1));
+  if (random_mode) {
+    // random threshold strictly inside the node's occupied bin range [lo, hi] (isolation / XRT):
+    // lo = first non-empty sorted position, hi = last; b in (lo, hi] keeps both sides non-empty
+    __shared__ int s_lo, s_hi;
+    if (t == 0) { s_lo = 0; s_hi = -1; }
+    __syncthreads();
+    const double cw = sw[t], pw = t > 0 ? sw[t - 1] : 0.0;
+    if (t < nb && cw > 0 && pw == 0) s_lo = t;
+    if (t < nb && W > 0 && cw == W && pw < W) s_hi = t;
+    __syncthreads();
+    if (s_hi > s_lo) {
+      unsigned long long hsh = splitmix64(p.seed ^ ((unsigned long long)level << 48) ^
+                                          ((unsigned long long)node << 20) ^ (unsigned long long)f);
+      rand_b = s_lo + 1 + (int)(hsh % (unsigned long long)(s_hi - s_lo));
+    }
   }
   if (t >= 1 && t < nb && (!random_mode || t == rand_b)) {
     const double wb = (t < 256) ? (sw[t] - sw[t - 1]) : 0.0;

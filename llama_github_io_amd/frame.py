@@ -255,8 +255,11 @@ class H2OFrame:
         raise TypeError(f"cannot build an H2OFrame from {type(obj)}")
 
     @staticmethod
-    def from_predictions(P: torch.Tensor, category: str, domain, threshold=None) -> "H2OFrame":
+    def from_predictions(P: torch.Tensor, category: str, domain, threshold=None, names=None) -> "H2OFrame":
         dev = P.device
+        if names is not None:
+            P2 = P if P.dim() == 2 else P.reshape(-1, 1)
+            return H2OFrame._from_columns([Column(n, "real", P2[:, i].double()) for i, n in enumerate(names)])
         if category == "Binomial":
             p1 = P[:, 1].double()
             th = 0.5 if threshold is None else threshold

@@ -142,7 +142,11 @@ class Model:
         X, offset = frame.model_matrix(self.info, device=self.device)
         P = self.score_tensor(X, offset)
         return H2OFrame.from_predictions(P, self.model_category, self.info.response_domain,
-                                         threshold=self.default_threshold())
+                                         threshold=self.default_threshold(), names=self.prediction_names())
+
+    def prediction_names(self):
+        """Column names of a multi-column non-classification prediction frame (None = defaults)."""
+        return None
 
     def default_threshold(self):
         tm = self.output.get("training_metrics") or {}

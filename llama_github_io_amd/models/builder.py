@@ -1,0 +1,243 @@
+"""ModelBuilder front-end: frame -> tensors -> trainer, cross-validation, model registry (reference:
+``hex/ModelBuilder.java`` (init/validation, ``computeCrossValidation``, fold assignment),
+``hex/CVModelBuilder.java``, ``hex/ModelBuilderHelper.java``, ``water/api/ModelBuildersHandler.java``).
+
+Every algorithm registers an :class:`AlgoSpec` (trainer class, supervised?, defaults). ``train``
+resolves predictors/response/special columns exactly like ``ModelBuilder.init`` (ignored columns,
+constant columns dropped, response domain, weights/offset/fold columns), builds the ``[F, N]``
+float32 device matrix, runs N-fold CV when asked (fold models + holdout predictions -> the
+``cross_validation_metrics`` and ``cross_validation_metrics_summary``), then trains the main model.
+"""
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from .. import metrics as mm
+from ..core import dkv
+from ..core.job import Job
+from .base import DataInfo, Model, make_key
+
+REGISTRY: dict = {}
+
+
+@dataclass
+class AlgoSpec:
+    name: str
+    trainer: type
+    supervised: bool = True
+    defaults: dict = field(default_factory=dict)
+    classification_only: bool = False
+    regression_only: bool = False
+    needs_response_optional: bool = False   # e.g. isolation forest accepts an optional label
+
+
+def register(name, trainer, supervised=True, defaults=None, **kw):
+    REGISTRY[name] = AlgoSpec(name, trainer, supervised, dict(defaults or {}), **kw)
+
+
+COMMON = ("nfolds", "fold_assignment", "fold_column", "keep_cross_validation_predictions", "keep_cross_validation_models",
+          "keep_cross_validation_fold_assignment", "weights_column", "offset_column", "ignored_columns",
+          "ignore_const_cols", "model_id", "training_frame", "validation_frame", "response_column", "x", "y")
+
+
+def _resolve_names(fr, cols):
+    if cols is None:
+        return None
+    if isinstance(cols, (str, int)):
+        cols = [cols]
+    out = []
+    for c in cols:
+        out.append(fr.names[c] if isinstance(c, int) else c)
+    return out
+
+
+def _classification_requested(algo, params) -> bool:
+    d = str(params.get("distribution") or "").lower()
+    fam = str(params.get("family") or "").lower()
+    return d in ("bernoulli", "multinomial", "quasibinomial", "modified_huber") or fam in ("binomial", "multinomial",
+                                                                                           "quasibinomial", "ordinal",
+                                                                                           "fractionalbinomial")
+
+
+def prepare(algo: str, params: dict, x=None, y=None, training_frame=None):
+    """Resolve columns and build the DataInfo (``ModelBuilder.init``)."""
+    spec = REGISTRY[algo]
+    fr = training_frame
+    y = _resolve_names(fr, y)
+    y = y[0] if y else None
+    special = {params.get("weights_column"), params.get("offset_column"), params.get("fold_column"),
+               params.get("treatment_column"), y}
+    special.discard(None)
+    ignored = set(_resolve_names(fr, params.get("ignored_columns")) or [])
+    if x is None:
+        xs = [n for n in fr.names if n not in special and n not in ignored]
+    else:
+        xs = [n for n in _resolve_names(fr, x) if n not in special]
+    xs = [n for n in xs if fr.type(n) != "string" or algo in ("word2vec", "targetencoder")]
+    if params.get("ignore_const_cols", True) and fr.nrows > 1:
+        keep = []
+        for n in xs:
+            c = fr._col(n)
+            if c.type == "enum":
+                v = c.data
+                if int(torch.unique(v).numel()) > 1 or int(v.max()) < 0 and False:
+                    keep.append(n)
+            elif c.type == "string":
+                keep.append(n)
+            else:
+                v = c.data
+                ok = ~torch.isnan(v)
+                if ok.any() and (float(v[ok].max()) != float(v[ok].min()) or bool((~ok).any())):
+                    keep.append(n)
+        xs = keep
+    iscat = np.array([1 if fr.type(n) == "enum" else 0 for n in xs], dtype=np.int32)
+    doms = [list(fr._col(n).domain) if fr.type(n) == "enum" else None for n in xs]
+    rdom = None
+    if y is not None:
+        yc = fr._col(y)
+        if yc.type == "enum":
+            rdom = list(yc.domain)
+        elif _classification_requested(algo, params) or spec.classification_only:
+            from ..frame import _num_to_enum
+            rdom = list(_num_to_enum(yc).domain)
+    info = DataInfo(xs, iscat, doms, y, rdom, params.get("weights_column"), params.get("offset_column"),
+                    params.get("fold_column"))
+    return info
+
+
+def tensors(fr, info: DataInfo, device=None):
+    X, offset = fr.model_matrix(info, device=device)
+    yv = fr.response_tensor(info, device=X.device) if info.response else None
+    w = fr.weights_tensor(info, device=X.device)
+    return X, yv, w, offset
+
+
+def _fold_ids(fr, info, params, n, seed):
+    k = int(params.get("nfolds") or 0)
+    if info.fold and info.fold in fr.names:
+        v = fr._col(info.fold).as_float()
+        u = torch.unique(v[~torch.isnan(v)])
+        return torch.bucketize(v, u).long(), int(u.numel())
+    scheme = str(params.get("fold_assignment") or "AUTO").lower()
+    if scheme == "modulo":
+        return torch.arange(n) % k, k
+    rng = np.random.default_rng(seed & 0xFFFFFFFF)
+    if scheme == "stratified" and info.response is not None:
+        yv = fr.response_tensor(info, device=torch.device("cpu")).numpy()
+        fold = np.zeros(n, dtype=np.int64)
+        for cls in np.unique(yv[~np.isnan(yv)]):
+            idx = np.nonzero(yv == cls)[0]
+            rng.shuffle(idx)
+            fold[idx] = np.arange(len(idx)) % k
+        return torch.from_numpy(fold), k
+    return torch.from_numpy(rng.integers(0, k, n)), k
+
+
+def _seed_of(params):
+    s = params.get("seed")
+    if s is None or int(s) == -1:
+        return int(np.random.SeedSequence().entropy % (1 << 62))
+    return int(s)
+
+
+def train(algo: str, params: dict, x=None, y=None, training_frame=None, validation_frame=None, job: Job | None = None,
+          model_id: str | None = None) -> Model:
+    spec = REGISTRY[algo]
+    p = dict(spec.defaults)
+    p.update({k: v for k, v in params.items() if v is not None})
+    if spec.supervised and y is None and not spec.needs_response_optional:
+        raise ValueError(f"{algo} needs a response column y")
+    fr = training_frame
+    if fr is None:
+        raise ValueError("training_frame is required")
+    info = prepare(algo, p, x, y, fr)
+    if not info.x:
+        raise ValueError("no usable predictor columns")
+    X, yv, w, off = tensors(fr, info)
+    if yv is not None and info.response_domain is None and spec.classification_only:
+        raise ValueError(f"{algo} needs a categorical response")
+    valid = None
+    if validation_frame is not None:
+        Xv, yvv, wv, ov = tensors(validation_frame, info, device=X.device)
+        valid = (Xv, yvv, wv, ov)
+    mid = model_id or p.get("model_id") or make_key(algo)
+    seed = _seed_of(p)
+    p["seed"] = seed
+    t0 = time.time()
+    nfolds = int(p.get("nfolds") or 0)
+    cv_out = None
+    if nfolds > 1 or (info.fold and info.fold in fr.names):
+        cv_out = _cross_validate(spec, p, fr, info, X, yv, w, off, seed, mid, job)
+    tr = spec.trainer({k: v for k, v in p.items() if k not in COMMON})
+    tr.job = job
+    model = tr.fit(X, yv, w, off, info, valid, mid) if yv is not None or not spec.supervised else tr.fit(X, yv, w, off, info, valid, mid)
+    model.params.update({k: p.get(k) for k in COMMON if k in p and k not in ("training_frame", "validation_frame", "x", "y")})
+    model.output["names"] = info.x + ([info.response] if info.response else [])
+    model.output["response_column_name"] = info.response
+    model.output["domains"] = info.domains
+    model.output["training_frame"] = fr.frame_id
+    if validation_frame is not None:
+        model.output["validation_frame"] = validation_frame.frame_id
+    if cv_out is not None:
+        model.cv_holdout = cv_out.pop("_cv_holdout", None)
+        model.output.update(cv_out)
+    model.output["run_time_ms"] = int((time.time() - t0) * 1000)
+    model.algo = algo
+    dkv.put(model.key, model)
+    return model
+
+
+def _cross_validate(spec, p, fr, info, X, yv, w, off, seed, mid, job):
+    N = X.shape[1]
+    fold, k = _fold_ids(fr, info, p, N, seed)
+    fold = fold.to(X.device)
+    models, holdout = [], None
+    fold_metrics = []
+    cat = "Unsupervised" if info.response is None else ("Regression" if info.response_domain is None else
+                                                         ("Binomial" if len(info.response_domain) == 2 else "Multinomial"))
+    for i in range(k):
+        tr_m = fold != i
+        ho_m = ~tr_m
+        if int(ho_m.sum()) == 0 or int(tr_m.sum()) == 0:
+            continue
+        sub = lambda t, m: None if t is None else (t[:, m] if t.dim() == 2 else t[m])  # noqa: E731
+        ps = {kk: vv for kk, vv in p.items() if kk not in COMMON}
+        trainer = spec.trainer(ps)
+        trainer.job = job
+        m = trainer.fit(sub(X, tr_m).contiguous(), sub(yv, tr_m), sub(w, tr_m), sub(off, tr_m), info, None,
+                        f"{mid}_cv_{i + 1}")
+        models.append(m)
+        P = m.score_tensor(sub(X, ho_m).contiguous(), sub(off, ho_m))
+        if holdout is None:
+            holdout = torch.zeros((N,) + tuple(P.shape[1:]), dtype=P.dtype, device=P.device)
+        holdout[ho_m] = P
+        if yv is not None:
+            fold_metrics.append(m.metrics_for(sub(X, ho_m).contiguous(), sub(yv, ho_m), sub(w, ho_m), sub(off, ho_m)))
+        if p.get("keep_cross_validation_models", True):
+            dkv.put(m.key, m)
+    out = dict(cross_validation_models=[m.key for m in models] if p.get("keep_cross_validation_models", True) else None)
+    if yv is not None and holdout is not None:
+        cvm = mm.make_metrics(cat, yv, holdout, w, info.response_domain)
+        out["cross_validation_metrics"] = cvm
+        summ = {}
+        for key in ("AUC", "pr_auc", "logloss", "MSE", "RMSE", "mae", "r2", "mean_per_class_error", "mean_residual_deviance"):
+            vals = [fm.get(key) for fm in fold_metrics if fm is not None and fm.get(key) is not None]
+            vals = [v for v in vals if isinstance(v, (int, float)) and not math.isnan(v)]
+            if vals:
+                summ[key] = dict(mean=float(np.mean(vals)), sd=float(np.std(vals, ddof=1)) if len(vals) > 1 else 0.0,
+                                 values=vals)
+        out["cross_validation_metrics_summary"] = summ
+    if p.get("keep_cross_validation_predictions") and holdout is not None:
+        from ..frame import H2OFrame
+        out["cross_validation_holdout_predictions_frame_id"] = H2OFrame.from_predictions(holdout, cat, info.response_domain).frame_id
+    if p.get("keep_cross_validation_fold_assignment"):
+        from ..frame import H2OFrame, Column
+        fa = H2OFrame._from_columns([Column("fold_assignment", "int", fold.double())])
+        out["cross_validation_fold_assignment_frame_id"] = fa.frame_id
+    out["_cv_holdout"] = holdout
+    return out

@@ -1,0 +1,158 @@
+"""Design-matrix expansion for numeric learners (reference: ``hex/DataInfo.java``).
+
+Tree learners consume the raw ``[F, N]`` float32 matrix (categoricals as codes). GLM, DeepLearning,
+KMeans, PCA, GLRM, PSVM, ... need H2O's expanded layout: categoricals first as one-hot blocks
+(``useAllFactorLevels`` keeps the first level, otherwise it is the reference level dropped), then
+numerics optionally standardised; missing numerics are mean-imputed (``MeanImputation``) and a
+missing categorical maps to the most frequent level (or an extra NA level when
+``missing_bucket``). Coefficient names follow H2O: ``col.level`` for one-hot entries.
+
+The expansion is a device gather: one-hot blocks are written with a single ``scatter_`` per
+categorical column into a zeroed ``[N, P]`` tensor, numerics with one fused ``(x - mu) * inv_sd``.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from .base import DataInfo
+
+
+class Expander:
+    def __init__(self, info: DataInfo, standardize=True, use_all_factor_levels=False, missing="MeanImputation",
+                 missing_bucket=False, center_only=False):
+        self.info = info
+        self.standardize = bool(standardize)
+        self.center_only = bool(center_only)
+        self.use_all = bool(use_all_factor_levels)
+        self.missing = missing
+        self.missing_bucket = bool(missing_bucket)
+        iscat = np.asarray(info.iscat)
+        self.cats = [j for j in range(info.F) if iscat[j]]
+        self.nums = [j for j in range(info.F) if not iscat[j]]
+        self.fitted = False
+
+    # ---- fit statistics on the training matrix X [F, N]
+    def fit(self, X: torch.Tensor, w: torch.Tensor | None = None, reduce=None):
+        dev = X.device
+        N = X.shape[1]
+        w = torch.ones(N, dtype=torch.float64, device=dev) if w is None else w.double()
+        self.cat_offsets, self.cat_sizes, self.cat_modes = [], [], []
+        names = []
+        off = 0
+        for j in self.cats:
+            dom = self.info.domains[j] or []
+            L = len(dom)
+            codes = X[j]
+            ok = ~torch.isnan(codes)
+            cnt = torch.zeros(max(L, 1), dtype=torch.float64, device=dev).index_add_(0, codes[ok].long().clamp(0, max(L - 1, 0)), w[ok])
+            if reduce is not None:
+                cnt = reduce(cnt)
+            self.cat_modes.append(int(torch.argmax(cnt)) if L else 0)
+            start = 0 if self.use_all else 1
+            size = L - start + (1 if self.missing_bucket else 0)
+            self.cat_offsets.append(off)
+            self.cat_sizes.append(size)
+            nm = self.info.x[j]
+            names += [f"{nm}.{dom[k]}" for k in range(start, L)]
+            if self.missing_bucket:
+                names.append(f"{nm}.missing(NA)")
+            off += size
+        self.num_off = off
+        Xn = X[self.nums].double() if self.nums else torch.zeros(0, N, dtype=torch.float64, device=dev)
+        ok = ~torch.isnan(Xn)
+        Xz = torch.where(ok, Xn, torch.zeros_like(Xn))
+        sw = (ok.double() * w).sum(1)
+        s1 = (Xz * w).sum(1)
+        s2 = (Xz * Xz * w).sum(1)
+        if reduce is not None:
+            packed = reduce(torch.cat([sw, s1, s2]))
+            k = len(self.nums)
+            sw, s1, s2 = packed[:k], packed[k:2 * k], packed[2 * k:]
+        mu = s1 / sw.clamp(min=1e-300)
+        var = (s2 - sw * mu * mu) / (sw - 1).clamp(min=1e-300)
+        sd = var.clamp(min=0).sqrt()
+        self.num_mean = mu
+        self.num_sd = torch.where(sd > 0, sd, torch.ones_like(sd))
+        self.num_sd_raw = sd
+        names += [self.info.x[j] for j in self.nums]
+        self.names = names
+        self.P = off + len(self.nums)
+        self.fitted = True
+        return self
+
+    @property
+    def ncats_expanded(self):
+        return self.num_off
+
+    def transform(self, X: torch.Tensor, dtype=torch.float32) -> torch.Tensor:
+        """[F, N] raw -> [N, P] design matrix."""
+        N = X.shape[1]
+        dev = X.device
+        Z = torch.zeros(N, self.P, dtype=dtype, device=dev)
+        start = 0 if self.use_all else 1
+        for i, j in enumerate(self.cats):
+            codes = X[j]
+            L = self.cat_sizes[i] + start - (1 if self.missing_bucket else 0)
+            na = torch.isnan(codes)
+            c = torch.where(na, torch.full_like(codes, -2.0), codes).long()
+            if self.missing_bucket:
+                c = torch.where(na, torch.full_like(c, L), c)
+            else:
+                c = torch.where(na, torch.full_like(c, self.cat_modes[i]), c)
+            c = torch.where((c >= L + (1 if self.missing_bucket else 0)) | (c < 0), torch.full_like(c, -1), c)  # unseen
+            col = c - start
+            valid = col >= 0
+            idx = (self.cat_offsets[i] + col.clamp(min=0))
+            rows = torch.nonzero(valid, as_tuple=True)[0]
+            Z[rows, idx[rows]] = 1
+        if self.nums:
+            Xn = X[self.nums].to(dtype=torch.float64)
+            mu = self.num_mean[:, None]
+            Xn = torch.where(torch.isnan(Xn), mu.expand_as(Xn), Xn)
+            if self.standardize:
+                Xn = (Xn - mu) / self.num_sd[:, None]
+            elif self.center_only:
+                Xn = Xn - mu
+            Z[:, self.num_off:] = Xn.T.to(dtype)
+        return Z
+
+    def row_mask_complete(self, X: torch.Tensor) -> torch.Tensor:
+        """Rows with no NA (for ``missing_values_handling='Skip'``)."""
+        return ~torch.isnan(X).any(0)
+
+    # ---- coefficient (de)standardisation helpers for linear models
+    def destandardize(self, beta: torch.Tensor, intercept: float):
+        """beta on standardized numerics -> beta on raw scale (+ intercept shift)."""
+        b = beta.clone().double()
+        ic = float(intercept)
+        if self.nums and self.standardize:
+            k = self.num_off
+            b[k:] = beta[k:].double() / self.num_sd
+            ic = ic - float((b[k:] * self.num_mean).sum())
+        return b, ic
+
+    def to_state(self):
+        return dict(standardize=self.standardize, use_all=self.use_all, missing=self.missing,
+                    missing_bucket=self.missing_bucket, center_only=self.center_only,
+                    cat_offsets=self.cat_offsets, cat_sizes=self.cat_sizes, cat_modes=self.cat_modes,
+                    num_off=self.num_off, num_mean=self.num_mean.cpu().tolist(), num_sd=self.num_sd.cpu().tolist(),
+                    num_sd_raw=self.num_sd_raw.cpu().tolist(), names=self.names, P=self.P)
+
+    @staticmethod
+    def from_state(info, s, device=None):
+        e = Expander(info, s["standardize"], s["use_all"], s["missing"], s["missing_bucket"], s.get("center_only", False))
+        for k in ("cat_offsets", "cat_sizes", "cat_modes", "num_off", "names", "P"):
+            setattr(e, k, s[k])
+        dev = device or torch.device("cpu")
+        e.num_mean = torch.tensor(s["num_mean"], dtype=torch.float64, device=dev)
+        e.num_sd = torch.tensor(s["num_sd"], dtype=torch.float64, device=dev)
+        e.num_sd_raw = torch.tensor(s["num_sd_raw"], dtype=torch.float64, device=dev)
+        e.fitted = True
+        return e
+
+    def to(self, device):
+        self.num_mean = self.num_mean.to(device)
+        self.num_sd = self.num_sd.to(device)
+        self.num_sd_raw = self.num_sd_raw.to(device)
+        return self

@@ -1,0 +1,408 @@
+"""Deep Learning: feed-forward MLP (reference: ``hex/deeplearning/DeepLearning.java``,
+``DeepLearningModel.java`` (parameters/defaults), ``Neurons.java`` (activations, dropout, ADADELTA /
+momentum updates, max_w2), ``DeepLearningTask.java`` (Hogwild! map)).
+
+MI355X design: synchronous mini-batch SGD instead of Hogwild (lock-free races do not map to a GPU).
+Hidden layers are hipBLASLt GEMMs (bf16 or fp32 via ``compute_dtype``) followed by the fused HIP
+bias+activation+dropout epilogue (``ops.dense.BiasAct``, forward and backward). Multi-GPU is data
+parallel with ONE flat bucket all-reduce of all gradients per step over RCCL (the ADADELTA state is
+replicated, so every rank applies the identical update = H2O's model averaging with a 1-step
+period). Supports Rectifier/Tanh/ExpRectifier/Maxout (+WithDropout), input/hidden dropout, L1/L2,
+max_w2, ADADELTA (rho, epsilon) or momentum SGD with rate annealing/decay and Nesterov,
+autoencoder + ``anomaly`` (per-row reconstruction MSE) + ``deepfeatures``, regression
+distributions (gaussian/poisson/gamma/tweedie/laplace/quantile/huber), early stopping.
+"""
+from __future__ import annotations
+
+import math
+import time
+
+import numpy as np
+import torch
+
+from .. import metrics as mm
+from ..ops.dense import ACT, bias_act
+from ..parallel import collectives as coll
+from .base import DataInfo, Model, ScoreKeeper, make_key, model_category
+from .datainfo import Expander
+
+DL_DEFAULTS = dict(hidden=[200, 200], epochs=10.0, activation="Rectifier", adaptive_rate=True, rho=0.99, epsilon=1e-8,
+                   rate=0.005, rate_annealing=1e-6, rate_decay=1.0, momentum_start=0.0, momentum_ramp=1e6,
+                   momentum_stable=0.0, nesterov_accelerated_gradient=True, input_dropout_ratio=0.0,
+                   hidden_dropout_ratios=None, l1=0.0, l2=0.0, max_w2=float("inf"),
+                   initial_weight_distribution="UniformAdaptive", initial_weight_scale=1.0, loss="Automatic",
+                   distribution="AUTO", tweedie_power=1.5, quantile_alpha=0.5, huber_alpha=0.9,
+                   mini_batch_size=1, autoencoder=False, standardize=True, use_all_factor_levels=True,
+                   stopping_rounds=5, stopping_metric="AUTO", stopping_tolerance=0.0, score_interval=5.0,
+                   score_training_samples=10000, seed=-1, shuffle_training_data=True, reproducible=False,
+                   export_weights_and_biases=False, missing_values_handling="MeanImputation", max_runtime_secs=0.0,
+                   compute_dtype="float32", gpu_batch_size=256, train_samples_per_iteration=-2)
+
+
+class MLP(torch.nn.Module):
+    def __init__(self, n_in, hidden, n_out, act: str, maxout: bool, in_drop, hid_drop, init_dist, init_scale, gen):
+        super().__init__()
+        self.act = act
+        self.maxout = maxout
+        self.in_drop = in_drop
+        self.hid_drop = hid_drop
+        dims = [n_in] + list(hidden)
+        self.hidden = torch.nn.ModuleList()
+        for i in range(len(hidden)):
+            width = dims[i + 1] * (2 if maxout else 1)
+            lin = torch.nn.Linear(dims[i], width)
+            self._init(lin, dims[i], width, init_dist, init_scale, gen)
+            self.hidden.append(lin)
+        self.out = torch.nn.Linear(dims[-1], n_out)
+        self._init(self.out, dims[-1], n_out, init_dist, init_scale, gen)
+        self.step = 0
+
+    @staticmethod
+    def _init(lin, fan_in, fan_out, dist, scale, gen):
+        with torch.no_grad():
+            d = dist.lower()
+            if d == "uniformadaptive":
+                r = math.sqrt(6.0 / (fan_in + fan_out))
+                lin.weight.uniform_(-r, r, generator=gen)
+            elif d == "uniform":
+                lin.weight.uniform_(-scale, scale, generator=gen)
+            else:
+                lin.weight.normal_(0, scale, generator=gen)
+            lin.bias.zero_()
+
+    def forward(self, x, seed=0, features_layer=None):
+        if self.training and self.in_drop > 0:
+            keep = (torch.rand(x.shape, device=x.device) >= self.in_drop).to(x.dtype)
+            x = x * keep / (1 - self.in_drop)
+        for i, lin in enumerate(self.hidden):
+            h = torch.nn.functional.linear(x, lin.weight)
+            drop = self.hid_drop[i] if self.training else 0.0
+            if self.maxout:
+                h = h + lin.bias
+                a, b = h.chunk(2, dim=1)
+                x = torch.maximum(a, b)
+                if drop > 0:
+                    x = x * (torch.rand(x.shape, device=x.device) >= drop).to(x.dtype) / (1 - drop)
+            else:
+                x = bias_act(h.float(), lin.bias.float(), self.act, drop, (seed * 1000003 + i * 7919 + self.step) & ((1 << 62) - 1))
+            if features_layer is not None and i == features_layer:
+                return x
+        return self.out(x)
+
+
+class DeepLearningModel(Model):
+    algo = "deeplearning"
+
+    def __init__(self, key, params, info):
+        super().__init__(key, params, info)
+        self.net = None
+        self.expander = None
+        self.resp_mu = 0.0
+        self.resp_sd = 1.0
+
+    def _forward(self, X):
+        Z = self.expander.transform(X.to(self.device))
+        self.net.eval()
+        with torch.no_grad():
+            return self.net(Z), Z
+
+    def _predict_tensor(self, X, offset=None):
+        out, Z = self._forward(X)
+        if self.params.get("autoencoder"):
+            return out.float()
+        cat = self.model_category
+        if cat in ("Binomial", "Multinomial"):
+            return torch.softmax(out.float(), 1)
+        f = out[:, 0].double() * self.resp_sd + self.resp_mu
+        d = self.output.get("distribution", "gaussian")
+        if d in ("poisson", "gamma", "tweedie"):
+            f = torch.exp(out[:, 0].double())
+        return f.float()
+
+    @property
+    def model_category(self):
+        return "AutoEncoder" if self.params.get("autoencoder") else self.output["model_category"]
+
+    def anomaly(self, frame, per_feature=False):
+        from ..frame import Column, H2OFrame
+        X, _ = frame.model_matrix(self.info, device=self.device)
+        out, Z = self._forward(X)
+        err = (out.float() - Z.float()) ** 2
+        if per_feature:
+            return H2OFrame._from_columns([Column(f"reconstr_{n}.SE", "real", err[:, i].double())
+                                           for i, n in enumerate(self.expander.names)])
+        return H2OFrame._from_columns([Column("Reconstruction.MSE", "real", err.mean(1).double())])
+
+    def deepfeatures(self, frame, layer: int):
+        from ..frame import H2OFrame
+        X, _ = frame.model_matrix(self.info, device=self.device)
+        Z = self.expander.transform(X)
+        self.net.eval()
+        with torch.no_grad():
+            F = self.net(Z, features_layer=layer)
+        return H2OFrame.from_tensor(F.float(), [f"DF.L{layer + 1}.C{i + 1}" for i in range(F.shape[1])])
+
+    def weights(self, matrix_id=0):
+        lins = list(self.net.hidden) + [self.net.out]
+        return lins[matrix_id].weight.detach().cpu().numpy()
+
+    def biases(self, vector_id=0):
+        lins = list(self.net.hidden) + [self.net.out]
+        return lins[vector_id].bias.detach().cpu().numpy()
+
+    def to_state(self):
+        s = super().to_state()
+        s["net"] = {k: v.cpu().tolist() for k, v in self.net.state_dict().items()}
+        s["net_cfg"] = self._cfg
+        s["expander"] = self.expander.to_state()
+        s["resp"] = [self.resp_mu, self.resp_sd]
+        return s
+
+    def _restore(self, s):
+        super()._restore(s)
+        self._cfg = s["net_cfg"]
+        c = self._cfg
+        self.net = MLP(c["n_in"], c["hidden"], c["n_out"], c["act"], c["maxout"], 0.0, [0.0] * len(c["hidden"]),
+                       "uniformadaptive", 1.0, torch.Generator().manual_seed(0))
+        self.net.load_state_dict({k: torch.tensor(v) for k, v in s["net"].items()})
+        self.expander = Expander.from_state(self.info, s["expander"])
+        self.resp_mu, self.resp_sd = s["resp"]
+
+
+class DeepLearningTrainer:
+    def __init__(self, params):
+        p = dict(DL_DEFAULTS)
+        p.update({k: v for k, v in params.items() if v is not None})
+        self.p = p
+        self.job = None
+
+    def fit(self, X, y, w, offset, info: DataInfo, valid=None, model_key=None):
+        from .shared_tree import resolve_seed
+        t0 = time.time()
+        p = self.p
+        dev = X.device
+        N = X.shape[1]
+        seed = resolve_seed(p["seed"])
+        torch.manual_seed(seed & 0x7FFFFFFF)
+        gen = torch.Generator().manual_seed(seed & 0x7FFFFFFF)
+        ae = bool(p["autoencoder"])
+        cat = "AutoEncoder" if ae else model_category(info)
+        w = torch.ones(N, dtype=torch.float64, device=dev) if w is None else w.double()
+        if y is not None and not ae:
+            ok = ~torch.isnan(y)
+            w = torch.where(ok, w, torch.zeros_like(w))
+        ex = Expander(info, standardize=p["standardize"], use_all_factor_levels=p["use_all_factor_levels"]).fit(X, w)
+        Z = ex.transform(X)
+        act_name = str(p["activation"]).lower()
+        with_drop = act_name.endswith("withdropout")
+        base = act_name.replace("withdropout", "")
+        maxout = base == "maxout"
+        hidden = list(p["hidden"])
+        hd = p["hidden_dropout_ratios"]
+        if hd is None:
+            hd = [0.5 if with_drop else 0.0] * len(hidden)
+        K = len(info.response_domain) if cat in ("Binomial", "Multinomial") else 1
+        n_out = Z.shape[1] if ae else K
+        dist = str(p["distribution"]).lower()
+        if dist == "auto":
+            dist = "gaussian" if cat == "Regression" else ("bernoulli" if cat == "Binomial" else "multinomial")
+        net = MLP(Z.shape[1], hidden, n_out, "rectifier" if maxout else base, maxout, float(p["input_dropout_ratio"]),
+                  [float(v) for v in hd], str(p["initial_weight_distribution"]), float(p["initial_weight_scale"]), gen).to(dev)
+        if coll.is_dist():
+            flat = torch.cat([q.detach().reshape(-1) for q in net.parameters()])
+            coll.broadcast_(flat)
+            o = 0
+            with torch.no_grad():
+                for q in net.parameters():
+                    q.copy_(flat[o:o + q.numel()].view_as(q))
+                    o += q.numel()
+        model = DeepLearningModel(model_key or make_key("deeplearning"), p, info)
+        model.device = dev
+        model.expander = ex
+        model.net = net
+        model._cfg = dict(n_in=Z.shape[1], hidden=hidden, n_out=n_out, act="rectifier" if maxout else base, maxout=maxout)
+        model.output["distribution"] = dist
+        yt = None
+        if not ae:
+            if cat == "Regression":
+                yy = torch.nan_to_num(y.double(), nan=0.0)
+                if dist in ("gaussian", "laplace", "quantile", "huber"):
+                    mu = float((w * yy).sum() / w.sum())
+                    sd = float(((w * (yy - mu) ** 2).sum() / w.sum()).sqrt()) or 1.0
+                    if not p["standardize"]:
+                        mu, sd = 0.0, 1.0
+                    model.resp_mu, model.resp_sd = mu, sd
+                    yt = ((yy - mu) / sd).float()
+                else:
+                    yt = yy.float()
+            else:
+                yt = torch.nan_to_num(y, nan=0).long()
+        B = int(p["mini_batch_size"])
+        if B <= 1:
+            B = int(p["gpu_batch_size"])      # Hogwild single-row SGD -> GPU mini-batches
+        params = list(net.parameters())
+        adaptive = bool(p["adaptive_rate"])
+        eg2 = [torch.zeros_like(q) for q in params]
+        edx2 = [torch.zeros_like(q) for q in params]
+        mom = [torch.zeros_like(q) for q in params]
+        rho, eps = float(p["rho"]), float(p["epsilon"])
+        l1, l2 = float(p["l1"]), float(p["l2"])
+        max_w2 = float(p["max_w2"])
+        keeper = ScoreKeeper(p["stopping_rounds"], p["stopping_metric"], p["stopping_tolerance"],
+                             "Regression" if ae else cat)
+        epochs = float(p["epochs"])
+        total = int(math.ceil(epochs * N / B))
+        g = torch.Generator(device="cpu").manual_seed(seed & 0x7FFFFFFF)
+        history = []
+        samples = 0
+        last_score = time.time()
+        dtype = torch.bfloat16 if str(p["compute_dtype"]).lower() in ("bf16", "bfloat16") else None
+        perm = None
+        pos = N
+        wf = w.float()
+        for step in range(total):
+            if pos + B > N:
+                perm = torch.randperm(N, generator=g).to(dev) if p["shuffle_training_data"] or True else torch.arange(N, device=dev)
+                pos = 0
+            idx = perm[pos:pos + B]
+            pos += B
+            xb = Z.index_select(0, idx)
+            wb = wf.index_select(0, idx)
+            net.train()
+            net.step = step
+            with torch.autocast(device_type=dev.type, dtype=dtype, enabled=dtype is not None):
+                out = net(xb, seed)
+            out = out.float()
+            loss = self._loss(out, xb if ae else yt.index_select(0, idx), wb, cat, dist, ae) / max(float(wb.sum()), 1e-12)
+            for q in params:
+                q.grad = None
+            loss.backward()
+            grads = [q.grad for q in params]
+            if coll.is_dist():
+                flat = torch.cat([gg.reshape(-1) for gg in grads])
+                coll.all_reduce_(flat)
+                flat /= coll.world()
+                o = 0
+                for gg in grads:
+                    gg.copy_(flat[o:o + gg.numel()].view_as(gg))
+                    o += gg.numel()
+            with torch.no_grad():
+                samples += B * (coll.world() if coll.is_dist() else 1)
+                if not adaptive:
+                    rate = float(p["rate"]) / (1 + float(p["rate_annealing"]) * samples)
+                    m = self._momentum(samples)
+                for i, (q, gg) in enumerate(zip(params, grads)):
+                    if l2 > 0 or l1 > 0:
+                        if q.dim() > 1:
+                            gg = gg + l2 * q + l1 * torch.sign(q)
+                    if adaptive:  # ADADELTA (Neurons.java: rho, epsilon)
+                        eg2[i].mul_(rho).addcmul_(gg, gg, value=1 - rho)
+                        dx = -torch.sqrt(edx2[i] + eps) / torch.sqrt(eg2[i] + eps) * gg
+                        edx2[i].mul_(rho).addcmul_(dx, dx, value=1 - rho)
+                        q.add_(dx)
+                    else:
+                        if m > 0:
+                            mom[i].mul_(m).add_(gg, alpha=-rate)
+                            if p["nesterov_accelerated_gradient"]:
+                                q.add_(mom[i], alpha=m).add_(gg, alpha=-rate)
+                            else:
+                                q.add_(mom[i])
+                        else:
+                            q.add_(gg, alpha=-rate)
+                    if max_w2 < float("inf") and q.dim() > 1:
+                        n2 = (q * q).sum(1, keepdim=True)
+                        q.mul_(torch.where(n2 > max_w2, torch.sqrt(max_w2 / n2), torch.ones_like(n2)))
+            if self.job is not None and step % 50 == 0:
+                self.job.set_progress(step / max(total, 1))
+            end = step == total - 1
+            if end or (time.time() - last_score > float(p["score_interval"])) or \
+                    (keeper.k > 0 and step > 0 and step % max(1, N // B) == 0):
+                last_score = time.time()
+                ev = self._score(model, X, y, w, samples / N, valid)
+                history.append({k: v for k, v in ev.items() if not k.startswith("_")})
+                mref = ev.get("_valid") or ev.get("_train")
+                if mref is not None and not end and keeper.add(mref):
+                    break
+                if float(p["max_runtime_secs"] or 0) > 0 and time.time() - t0 > float(p["max_runtime_secs"]):
+                    break
+        model.output["scoring_history"] = history
+        model.output["epochs"] = samples / N
+        if ae:
+            model.output["training_metrics"] = self._ae_metrics(model, X)
+        else:
+            model.output["training_metrics"] = model.metrics_for(X, y, w.float())
+            if valid is not None:
+                Xv, yv, wv, ov = valid
+                model.output["validation_metrics"] = model.metrics_for(Xv, yv, wv, ov)
+        # Gedeon variable importance from the first layer weights
+        W1 = net.hidden[0].weight.detach().abs() if net.hidden else net.out.weight.detach().abs()
+        imp = W1.sum(0).double()
+        agg = {}
+        for nme, v in zip(ex.names, imp.cpu().tolist()):
+            base_n = nme.split(".")[0] if nme not in info.x else nme
+            agg[base_n] = agg.get(base_n, 0.0) + v
+        from .base import variable_importance
+        model.output["variable_importances"] = variable_importance(list(agg), list(agg.values()))
+        model.output["run_time_ms"] = int((time.time() - t0) * 1000)
+        return model
+
+    def _momentum(self, samples):
+        p = self.p
+        ms, mr, mst = float(p["momentum_start"]), float(p["momentum_ramp"]), float(p["momentum_stable"])
+        if samples >= mr:
+            return mst
+        return ms + (mst - ms) * samples / mr
+
+    def _loss(self, out, target, w, cat, dist, ae):
+        p = self.p
+        lname = str(p["loss"]).lower()
+        if ae:
+            return (w[:, None] * (out - target.float()) ** 2).sum() / out.shape[1]
+        if cat in ("Binomial", "Multinomial"):
+            return (w * torch.nn.functional.cross_entropy(out, target, reduction="none")).sum()
+        f = out[:, 0]
+        t = target
+        if lname == "absolute" or dist == "laplace":
+            return (w * (f - t).abs()).sum()
+        if lname == "quantile" or dist == "quantile":
+            a = float(p["quantile_alpha"])
+            r = t - f
+            return (w * torch.where(r >= 0, a * r, (a - 1) * r)).sum()
+        if lname == "huber" or dist == "huber":
+            return (w * torch.nn.functional.huber_loss(f, t, reduction="none", delta=1.0)).sum()
+        if dist == "poisson":
+            return (w * (torch.exp(f) - t * f)).sum()
+        if dist == "gamma":
+            return (w * (t * torch.exp(-f) + f)).sum()
+        if dist == "tweedie":
+            r = float(p["tweedie_power"])
+            return (w * (-t * torch.exp((1 - r) * f) / (1 - r) + torch.exp((2 - r) * f) / (2 - r))).sum()
+        return 0.5 * (w * (f - t) ** 2).sum()
+
+    def _ae_metrics(self, model, X):
+        out, Z = model._forward(X)
+        return mm.autoencoder_metrics(((out.float() - Z.float()) ** 2).mean(1))
+
+    def _score(self, model, X, y, w, epochs, valid):
+        p = self.p
+        N = X.shape[1]
+        n = int(p["score_training_samples"]) or N
+        idx = torch.arange(N, device=X.device) if n >= N else torch.randperm(N, device=X.device)[:n]
+        Xs = X[:, idx]
+        ev = dict(epochs=epochs, timestamp=time.time())
+        if p["autoencoder"]:
+            m = self._ae_metrics(model, Xs)
+        else:
+            m = model.metrics_for(Xs, y[idx], w[idx].float())
+        ev["_train"] = m
+        for k in ("RMSE", "logloss", "AUC", "mean_per_class_error", "MSE"):
+            if m is not None and k in m:
+                ev["training_" + k.lower()] = m[k]
+        if valid is not None and not p["autoencoder"]:
+            Xv, yv, wv, ov = valid
+            vm = model.metrics_for(Xv, yv, wv, ov)
+            ev["_valid"] = vm
+            for k in ("RMSE", "logloss", "AUC", "mean_per_class_error"):
+                if vm is not None and k in vm:
+                    ev["validation_" + k.lower()] = vm[k]
+        return ev

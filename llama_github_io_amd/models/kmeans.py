@@ -1,0 +1,203 @@
+"""K-Means (reference: ``hex/kmeans/KMeans.java``, ``KMeansModel.java``).
+
+Init: Random, PlusPlus (k-means++), Furthest, User; ``standardize`` via the expander (one-hot
+categoricals, mean-imputed numerics — H2O's DataInfo for KMeans); Lloyd iterations with the fused
+HIP assign kernel (``ops.dense.kmeans_assign``) and device ``index_add_`` centroid sums, all-reduced
+across ranks; empty clusters are re-seeded from the farthest point; ``estimate_k`` grows k until
+the relative reduction of within-SS falls below the H2O criterion. Outputs centers (raw and
+standardized), within/between/total SS, cluster sizes.
+"""
+from __future__ import annotations
+
+import math
+import time
+
+import numpy as np
+import torch
+
+from .. import metrics as mm
+from ..ops.dense import kmeans_assign
+from ..parallel import collectives as coll
+from .base import DataInfo, Model, make_key
+from .datainfo import Expander
+
+KM_DEFAULTS = dict(k=1, max_iterations=10, standardize=True, init="Furthest", user_points=None, estimate_k=False,
+                   seed=-1, cluster_size_constraints=None)
+
+
+class KMeansModel(Model):
+    algo = "kmeans"
+
+    def __init__(self, key, params, info):
+        super().__init__(key, params, info)
+        self.output["model_category"] = "Clustering"
+        self.centers_std = None
+        self.expander = None
+
+    @property
+    def model_category(self):
+        return "Clustering"
+
+    def _predict_tensor(self, X, offset=None):
+        Z = self.expander.transform(X.to(self.device))
+        a, _ = kmeans_assign(Z, self.centers_std.to(Z.device))
+        return a.float()
+
+    def predict(self, frame):
+        from ..frame import Column, H2OFrame
+        X, _ = frame.model_matrix(self.info, device=self.device)
+        a = self._predict_tensor(X)
+        return H2OFrame._from_columns([Column("predict", "int", a.double())])
+
+    def centers(self):
+        return self.output["centers"]
+
+    def centers_std(self):  # noqa: F811 - h2o-py accessor
+        return self.output["centers_std"]
+
+    def size(self):
+        return self.output["training_metrics"]["size"]
+
+    def tot_withinss(self, *a, **k):
+        return self.output["training_metrics"]["tot_withinss"]
+
+    def betweenss(self, *a, **k):
+        return self.output["training_metrics"]["betweenss"]
+
+    def totss(self, *a, **k):
+        return self.output["training_metrics"]["totss"]
+
+    def withinss(self, *a, **k):
+        return self.output["training_metrics"]["withinss"]
+
+    def to_state(self):
+        s = super().to_state()
+        s["centers_std"] = self.centers_std.cpu().tolist()
+        s["expander"] = self.expander.to_state()
+        return s
+
+    def _restore(self, s):
+        super()._restore(s)
+        self.centers_std = torch.tensor(s["centers_std"], dtype=torch.float32)
+        self.expander = Expander.from_state(self.info, s["expander"])
+
+
+class KMeansTrainer:
+    def __init__(self, params):
+        p = dict(KM_DEFAULTS)
+        p.update({k: v for k, v in params.items() if v is not None})
+        self.p = p
+        self.job = None
+
+    def _init_centers(self, Z, k, rng, how):
+        N = Z.shape[0]
+        dev = Z.device
+        if how == "user" and self.p.get("user_points") is not None:
+            up = self.p["user_points"]
+            U = up.as_tensor() if hasattr(up, "as_tensor") else torch.as_tensor(np.asarray(up, dtype=np.float32))
+            return self.ex.transform(U.T.contiguous().to(dev)) if U.shape[1] == self.info.F else U.to(dev).float()
+        first = int(rng.integers(N))
+        C = Z[first:first + 1].clone()
+        if how == "random":
+            idx = torch.as_tensor(rng.choice(N, size=min(k, N), replace=False), device=dev)
+            return Z[idx].clone()
+        while C.shape[0] < k:
+            _, d = kmeans_assign(Z, C)
+            if how == "plusplus":
+                pr = d.double().clamp(min=0)
+                s = float(pr.sum())
+                if s <= 0:
+                    break
+                u = rng.random() * s
+                j = int(torch.searchsorted(torch.cumsum(pr, 0), torch.tensor([u], dtype=torch.float64, device=dev))[0])
+                j = min(j, N - 1)
+            else:  # furthest
+                j = int(torch.argmax(d))
+            C = torch.cat([C, Z[j:j + 1]], 0)
+        return C
+
+    def _lloyd(self, Z, w, C, max_it):
+        K = C.shape[0]
+        dev = Z.device
+        for it in range(max_it):
+            a, d = kmeans_assign(Z, C)
+            sums = torch.zeros(K, Z.shape[1], dtype=torch.float64, device=dev).index_add_(0, a, Z.double() * w[:, None])
+            cnt = torch.zeros(K, dtype=torch.float64, device=dev).index_add_(0, a, w)
+            if coll.is_dist():
+                sums = coll.all_reduce_(sums)
+                cnt = coll.all_reduce_(cnt)
+            newC = torch.where(cnt[:, None] > 0, sums / cnt.clamp(min=1e-300)[:, None], C.double()).float()
+            empty = torch.nonzero(cnt == 0).flatten().tolist()
+            for e in empty:   # re-seed empty clusters at the worst-fit row
+                j = int(torch.argmax(d))
+                newC[e] = Z[j]
+                d[j] = 0
+            shift = float((newC - C).abs().max())
+            C = newC
+            if self.job is not None:
+                self.job.check_cancelled()
+            if shift < 1e-6:
+                break
+        a, d = kmeans_assign(Z, C)
+        return C, a, d, it + 1
+
+    def fit(self, X, y, w, offset, info: DataInfo, valid=None, model_key=None):
+        from .shared_tree import resolve_seed
+        t0 = time.time()
+        p = self.p
+        self.info = info
+        dev = X.device
+        N = X.shape[1]
+        seed = resolve_seed(p["seed"])
+        rng = np.random.default_rng(seed & 0xFFFFFFFF)
+        w = torch.ones(N, dtype=torch.float64, device=dev) if w is None else w.double()
+        self.ex = Expander(info, standardize=p["standardize"], use_all_factor_levels=True).fit(X, w)
+        Z = self.ex.transform(X)
+        how = str(p["init"]).lower()
+        max_it = int(p["max_iterations"])
+        if p["estimate_k"]:
+            # KMeans.java: deterministic growth from k=1, split the worst cluster, stop when the relative
+            # within-SS improvement falls under min(0.02 + 10/N + 2.5/F^2, 0.8) and keep the previous k
+            kmax = int(p["k"])
+            cutoff = min(0.02 + 10.0 / N + 2.5 / max(info.F, 1) ** 2, 0.8)
+            C0 = (Z.double() * w[:, None]).sum(0, keepdim=True).float() / float(w.sum())
+            prev = None
+            best = None
+            for k in range(1, kmax + 1):
+                Ck, ak, dk, it = self._lloyd(Z, w, C0, max_it)
+                wss = float((dk.double() * w).sum())
+                if prev is not None and (prev - wss) / max(prev, 1e-300) < cutoff:
+                    break
+                best, prev = (Ck, ak, dk, it), wss
+                if k == kmax:
+                    break
+                per = torch.zeros(Ck.shape[0], dtype=torch.float64, device=dev).index_add_(0, ak, dk.double() * w)
+                worst = int(torch.argmax(per))
+                far = int(torch.argmax(torch.where(ak == worst, dk, torch.full_like(dk, -1.0))))
+                C0 = torch.cat([Ck, Z[far:far + 1]], 0)
+            C, a, d, iters = best
+        else:
+            C0 = self._init_centers(Z, int(p["k"]), rng, how)
+            C, a, d, iters = self._lloyd(Z, w, C0, max_it)
+        model = KMeansModel(model_key or make_key("kmeans"), p, info)
+        model.device = dev
+        model.expander = self.ex
+        model.centers_std = C
+        raw = C.double().clone()
+        if self.ex.standardize and self.ex.nums:
+            k0 = self.ex.num_off
+            raw[:, k0:] = raw[:, k0:] * self.ex.num_sd[None, :] + self.ex.num_mean[None, :]
+        model.output["centers_std"] = C.cpu().tolist()
+        model.output["centers"] = raw.cpu().tolist()
+        model.output["center_names"] = self.ex.names
+        model.output["k"] = C.shape[0]
+        model.output["iterations"] = iters
+        met = mm.clustering_metrics(Z, C, a, w)
+        model.output["training_metrics"] = met
+        if valid is not None:
+            Xv = valid[0]
+            Zv = self.ex.transform(Xv)
+            av, _ = kmeans_assign(Zv, C)
+            model.output["validation_metrics"] = mm.clustering_metrics(Zv, C, av)
+        model.output["run_time_ms"] = int((time.time() - t0) * 1000)
+        return model

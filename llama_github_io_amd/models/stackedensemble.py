@@ -1,0 +1,151 @@
+"""Stacked Ensemble (reference: ``hex/ensemble/StackedEnsemble.java``, ``StackedEnsembleModel.java``,
+``Metalearners.java``).
+
+Base models must share the fold assignment and keep their cross-validation holdout predictions;
+the level-one frame is [holdout predictions of each base model] (p1 for binomial, all class
+probabilities for multinomial, the prediction for regression) and the metalearner (default GLM
+with non-negative weights, or GBM/DRF/DeepLearning/naive-bayes-free choice) is trained on it.
+Scoring stacks the base models' predictions on the new data and applies the metalearner.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ..core import dkv
+from .base import DataInfo, Model, make_key
+
+
+def _level_one(models, X, offset, category):
+    cols = []
+    for m in models:
+        P = m.score_tensor(X, offset)
+        if category == "Binomial":
+            cols.append(P[:, 1:2].float())
+        elif category == "Multinomial":
+            cols.append(P.float())
+        else:
+            cols.append(P.reshape(-1, 1).float())
+    return torch.cat(cols, 1).T.contiguous()   # [F', N] like every trainer input
+
+
+class StackedEnsembleModel(Model):
+    algo = "stackedensemble"
+
+    def __init__(self, key, params, info):
+        super().__init__(key, params, info)
+        self.base_keys = []
+        self.meta = None
+
+    def base_models(self):
+        return [dkv.get(k) for k in self.base_keys]
+
+    def _predict_tensor(self, X, offset=None):
+        L1 = _level_one(self.base_models(), X, offset, self.model_category)
+        return self.meta.score_tensor(L1)
+
+    def metalearner(self):
+        return self.meta
+
+    def to_state(self):
+        s = super().to_state()
+        s["base_models"] = [m.to_state() | {"__class__": type(m).__module__ + ":" + type(m).__name__}
+                            for m in self.base_models()]
+        s["meta"] = self.meta.to_state() | {"__class__": type(self.meta).__module__ + ":" + type(self.meta).__name__}
+        return s
+
+    def _restore(self, s):
+        super()._restore(s)
+        from ..persist import _from_state
+        bms = [_from_state(dict(b)) for b in s["base_models"]]
+        for b in bms:
+            dkv.put(b.key, b)
+        self.base_keys = [b.key for b in bms]
+        self.meta = _from_state(dict(s["meta"]))
+
+
+class StackedEnsembleTrainer:
+    def __init__(self, params):
+        p = dict(base_models=[], metalearner_algorithm="AUTO", metalearner_params=None, metalearner_nfolds=0,
+                 seed=-1, blending_frame=None)
+        p.update({k: v for k, v in params.items() if v is not None})
+        self.p = p
+        self.job = None
+
+    def fit(self, X, y, w, offset, info: DataInfo, valid=None, model_key=None):
+        from .builder import REGISTRY
+        from .base import model_category
+        keys = []
+        for b in self.p["base_models"]:
+            if isinstance(b, str):
+                keys.append(b)
+            else:
+                k = getattr(b, "model_id", None) or getattr(b, "key", None)
+                if k is None and hasattr(b, "_model"):
+                    k = b._model.key
+                keys.append(k)
+        models = []
+        for k in keys:
+            v = dkv.get(k)
+            if v is None:
+                continue
+            if hasattr(v, "models") and hasattr(v, "grid_id"):   # a Grid: take all its models
+                models += list(v.models)
+            else:
+                models.append(v)
+        if not models:
+            raise ValueError("StackedEnsemble needs base_models")
+        cat = model_category(info)
+        holds = []
+        for m in models:
+            h = getattr(m, "cv_holdout", None)
+            if h is None:
+                raise ValueError(f"base model {m.key} has no cross-validation holdout predictions "
+                                 "(train it with nfolds>1 and keep_cross_validation_predictions=True)")
+            if cat == "Binomial":
+                holds.append(h[:, 1:2].float())
+            elif cat == "Multinomial":
+                holds.append(h.float())
+            else:
+                holds.append(h.reshape(-1, 1).float())
+        L1 = torch.cat(holds, 1).T.contiguous().to(X.device)
+        names = []
+        for m in models:
+            if cat == "Multinomial":
+                names += [f"{m.key}/{d}" for d in info.response_domain]
+            else:
+                names.append(m.key)
+        minfo = DataInfo(names, np.zeros(len(names), np.int32), [None] * len(names), info.response, info.response_domain)
+        algo = str(self.p["metalearner_algorithm"]).lower()
+        mp = dict(self.p["metalearner_params"] or {})
+        if algo in ("auto", "glm"):
+            algo = "glm"
+            mp.setdefault("non_negative", True)
+            if "lambda" not in mp:
+                mp.setdefault("lambda_", 0.0)
+            if cat == "Binomial":
+                mp.setdefault("family", "binomial")
+        elif algo == "naivebayes":
+            algo = "naivebayes"
+        mp.setdefault("seed", self.p.get("seed", -1))
+        trainer = REGISTRY[algo].trainer(mp)
+        meta = trainer.fit(L1, y, w, None, minfo, None, (model_key or make_key("se")) + "_metalearner")
+        model = StackedEnsembleModel(model_key or make_key("stackedensemble"), self.p, info)
+        model.device = X.device
+        model.base_keys = [m.key for m in models]
+        model.meta = meta
+        model.output["base_models"] = model.base_keys
+        model.output["metalearner"] = meta.key
+        model.output["training_metrics"] = model.metrics_for(X, y, w, offset)
+        # CV estimate: metalearner applied to the out-of-fold level-one matrix
+        from .. import metrics as mm
+        Ph = meta.score_tensor(L1)
+        model.output["cross_validation_metrics"] = mm.make_metrics(cat, y, Ph, w, info.response_domain)
+        if valid is not None:
+            Xv, yv, wv, ov = valid
+            model.output["validation_metrics"] = model.metrics_for(Xv, yv, wv, ov)
+        dkv.put(meta.key, meta)
+        return model
+
+    def to_state(self):  # pragma: no cover - persisted through base models' keys
+        return {}

@@ -1,0 +1,120 @@
+"""Fused dense-layer epilogues for DeepLearning (``csrc/dense_kernels.hip``) as autograd ops.
+
+``BiasAct.apply(x, b, act, drop, seed)`` = act(x + b) with inverted dropout, forward and backward in
+one HIP pass each on CUDA tensors; the CPU path is the PyTorch reference of the same math (same
+counter-hash dropout mask so CPU/GPU runs agree bit-for-bit on which units drop).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _native as nat
+
+ACT = {"linear": 0, "rectifier": 1, "relu": 1, "tanh": 2, "exprectifier": 3, "elu": 3}
+
+nat.register_hip_signatures({
+    "h2o_bias_act_fwd": [nat.c_void_p, nat.c_void_p, nat.c_void_p, nat.c_ll, nat.c_int, nat.c_int, nat.ctypes.c_float,
+                         nat.c_ull, nat.c_void_p],
+    "h2o_bias_act_bwd": [nat.c_void_p, nat.c_void_p, nat.c_void_p, nat.c_void_p, nat.c_ll, nat.c_int, nat.c_int,
+                         nat.ctypes.c_float, nat.c_ull, nat.c_void_p],
+    "h2o_kmeans_assign": [nat.c_void_p, nat.c_ll, nat.c_int, nat.c_void_p, nat.c_int, nat.c_void_p, nat.c_void_p, nat.c_void_p],
+})
+
+_M = (1 << 64) - 1
+
+
+def _mask_ref(shape, drop, seed, device):
+    n = shape[0] * shape[1]
+    i = torch.arange(n, dtype=torch.int64, device=device)
+    # same 64-bit mixing as hash32() in the kernel, computed with wrap-around int64 arithmetic
+    x = torch.bitwise_xor(torch.tensor(seed if seed < (1 << 63) else seed - (1 << 64), dtype=torch.int64),
+                          i * torch.tensor(0x9E3779B97F4A7C15 - (1 << 64), dtype=torch.int64))
+
+    def srl(v, k):
+        return torch.bitwise_and(torch.bitwise_right_shift(v, k), (1 << (64 - k)) - 1)
+    x = torch.bitwise_xor(x, srl(x, 33)); x = x * torch.tensor(0xff51afd7ed558ccd - (1 << 64), dtype=torch.int64)
+    x = torch.bitwise_xor(x, srl(x, 33)); x = x * torch.tensor(0xc4ceb9fe1a85ec53 - (1 << 64), dtype=torch.int64)
+    x = torch.bitwise_xor(x, srl(x, 33))
+    h = torch.bitwise_and(x, 0xFFFFFFFF)
+    thr = int(drop * 4294967296.0)
+    return (h >= thr).reshape(shape)
+
+
+def _act(a, v):
+    if a == 1:
+        return torch.relu(v)
+    if a == 2:
+        return torch.tanh(v)
+    if a == 3:
+        return torch.where(v > 0, v, torch.expm1(v))
+    return v
+
+
+class BiasAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, b, act: int, drop: float, seed: int):
+        x = x.contiguous()
+        rows, cols = x.shape
+        if x.is_cuda:
+            y = torch.empty_like(x)
+            nat.call("h2o_bias_act_fwd", x.data_ptr(), 0 if b is None else b.data_ptr(), y.data_ptr(), rows, cols, act,
+                     float(drop), seed & _M, nat.stream_ptr(x.device))
+        else:
+            y = _act(act, x + (b if b is not None else 0))
+            if drop > 0:
+                y = torch.where(_mask_ref(y.shape, drop, seed, y.device), y / (1 - drop), torch.zeros_like(y))
+        ctx.save_for_backward(y)
+        ctx.act, ctx.drop, ctx.seed, ctx.has_b = act, drop, seed, b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        (y,) = ctx.saved_tensors
+        gy = gy.contiguous()
+        rows, cols = y.shape
+        act, drop, seed = ctx.act, ctx.drop, ctx.seed
+        if y.is_cuda:
+            gx = torch.empty_like(y)
+            db = torch.zeros(cols, dtype=torch.float32, device=y.device) if ctx.has_b else None
+            nat.call("h2o_bias_act_bwd", gy.data_ptr(), y.data_ptr(), gx.data_ptr(), 0 if db is None else db.data_ptr(),
+                     rows, cols, act, float(drop), seed & _M, nat.stream_ptr(y.device))
+        else:
+            yy, g = y, gy
+            if drop > 0:
+                m = _mask_ref(y.shape, drop, seed, y.device)
+                g = torch.where(m, gy / (1 - drop), torch.zeros_like(gy))
+                yy = torch.where(m, y * (1 - drop), torch.zeros_like(y))
+            if act == 1:
+                d = (yy > 0).to(y.dtype)
+            elif act == 2:
+                d = 1 - yy * yy
+            elif act == 3:
+                d = torch.where(yy > 0, torch.ones_like(yy), yy + 1)
+            else:
+                d = torch.ones_like(yy)
+            gx = g * d
+            db = gx.sum(0) if ctx.has_b else None
+        return gx, db, None, None, None
+
+
+def bias_act(x, b, act: str | int = "rectifier", drop: float = 0.0, seed: int = 0):
+    a = ACT[act.lower()] if isinstance(act, str) else int(act)
+    return BiasAct.apply(x, b, a, float(drop), int(seed))
+
+
+def kmeans_assign(X: torch.Tensor, C: torch.Tensor):
+    """Closest center and squared distance for every row. X [N, P], C [K, P] float32."""
+    N, P = X.shape
+    K = C.shape[0]
+    if X.is_cuda and (K * P + 256 * (P + 1)) * 4 <= 160 * 1024 and N > 0:
+        X = X.contiguous().float()
+        C = C.contiguous().float()
+        a = torch.empty(N, dtype=torch.int32, device=X.device)
+        d = torch.empty(N, dtype=torch.float32, device=X.device)
+        nat.call("h2o_kmeans_assign", X.data_ptr(), N, P, C.data_ptr(), K, a.data_ptr(), d.data_ptr(), nat.stream_ptr(X.device))
+        return a.long(), d
+    # reference / wide path: ||x||² - 2 x·c + ||c||² via one GEMM
+    Xd, Cd = X.double(), C.double()
+    D = (Xd * Xd).sum(1, keepdim=True) - 2 * Xd @ Cd.T + (Cd * Cd).sum(1)[None, :]
+    d, a = D.clamp(min=0).min(1)
+    return a, d.float()

@@ -1,0 +1,62 @@
+"""Weighted Gram / cross-product ops (GLM GramTask, PCA GramSVD, covariance).
+
+CUDA(HIP) tensors run ``csrc/gram_kernels.hip`` (f32-input MFMA tiles, per-slice fp32 slabs summed
+in fp64); CPU tensors use the fp64 PyTorch reference (the test oracle).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _native as nat
+
+nat.register_hip_signatures({
+    "h2o_gram": [nat.c_void_p, nat.c_ll, nat.c_void_p, nat.c_ll, nat.c_int, nat.c_int, nat.c_void_p, nat.c_int, nat.c_void_p],
+    "h2o_xtv": [nat.c_void_p, nat.c_ll, nat.c_void_p, nat.c_int, nat.c_ll, nat.c_int, nat.c_int, nat.c_void_p, nat.c_void_p],
+})
+
+
+def _splits(N: int, pairs: int) -> int:
+    target = max(1, 2048 // max(1, pairs))        # >= ~8 waves of workgroups per XCD on 256 CUs
+    return int(max(1, min(target, (N + 4095) // 4096)))
+
+
+def gram(Z: torch.Tensor, w: torch.Tensor | None = None) -> torch.Tensor:
+    """Zᵀ diag(w) Z in float64. Z: [N, P] float32 row-major."""
+    N, P = Z.shape
+    if not Z.is_cuda:
+        Zd = Z.double()
+        return (Zd * (w.double()[:, None] if w is not None else 1.0)).T @ Zd
+    Z = Z.contiguous().float()
+    wf = None if w is None else w.contiguous().float()
+    Ppad = (P + 63) // 64 * 64
+    nT = Ppad // 64
+    pairs = nT * (nT + 1) // 2
+    S = _splits(N, pairs)
+    slabs = torch.zeros(S, Ppad, Ppad, dtype=torch.float32, device=Z.device)
+    if N > 0:
+        nat.call("h2o_gram", Z.data_ptr(), P, 0 if wf is None else wf.data_ptr(), N, P, S, slabs.data_ptr(), Ppad,
+                 nat.stream_ptr(Z.device))
+    G = slabs.sum(0, dtype=torch.float64)[:P, :P]
+    # only tiles with ti <= tj were computed: mirror the strictly-lower tile blocks
+    up = torch.triu(torch.ones(nT, nT, dtype=torch.bool, device=Z.device))
+    mask = up.repeat_interleave(64, 0).repeat_interleave(64, 1)[:P, :P]
+    G = torch.where(mask, G, G.T)
+    return G
+
+
+def xtv(Z: torch.Tensor, v: torch.Tensor) -> torch.Tensor:
+    """Zᵀ v in float64; v: [N] or [N, R] (R <= 8)."""
+    vec = v.dim() == 1
+    V = v[:, None] if vec else v
+    N, P = Z.shape
+    R = V.shape[1]
+    if not Z.is_cuda or R > 8:
+        out = Z.double().T @ V.double()
+        return out[:, 0] if vec else out
+    Z = Z.contiguous().float()
+    V = V.contiguous().float()
+    S = int(max(1, min(1024, (N + 8191) // 8192)))
+    slabs = torch.empty(S, P, R, dtype=torch.float32, device=Z.device)
+    nat.call("h2o_xtv", Z.data_ptr(), P, V.data_ptr(), R, N, P, S, slabs.data_ptr(), nat.stream_ptr(Z.device))
+    out = slabs.sum(0, dtype=torch.float64)
+    return out[:, 0] if vec else out

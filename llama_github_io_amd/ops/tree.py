@@ -111,9 +111,12 @@ def split_find_ref(h, nayy, wyy, nbins_f, iscat_f, mono_f, p: SplitParams, level
         Wall, WYall = W + wNA, WY + wyNA
         random_mode = p.random_split
         rand_b = -1
-        if random_mode and nb > 1:
-            hsh = splitmix64((seed ^ (level << 48) ^ (node << 20) ^ f) & _M64)
-            rand_b = 1 + int(hsh % (nb - 1))
+        if random_mode:
+            occ = np.nonzero(w[:nb] > 0)[0]
+            if occ.size and occ[-1] > occ[0]:
+                lo, hi = int(occ[0]), int(occ[-1])
+                hsh = splitmix64((seed ^ (level << 48) ^ (node << 20) ^ f) & _M64)
+                rand_b = lo + 1 + int(hsh % (hi - lo))
         best_e, best_code = -1.0e300, -1
         cands = []
         if wNA >= p.min_w and W > 0 and not random_mode:
@@ -278,6 +281,13 @@ class RefTreeBuilder:
             dl = np.zeros(n, dtype=DEC_DT)
             for i, rows in enumerate(level_rows):
                 h, nayy, wyy = self._hist(rows, aux)
+                if coll.is_dist():  # row-sharded: every rank sees the global node histogram
+                    flat = torch.from_numpy(np.concatenate([h.ravel(), nayy, [wyy]]))
+                    coll.all_reduce_(flat)
+                    flat = flat.numpy()
+                    h = flat[: h.size].reshape(h.shape)
+                    nayy = flat[h.size: h.size + F]
+                    wyy = float(flat[-1])
                 cands = split_find_ref(h, nayy, wyy, self.nbins_f, self.iscat_f, self.mono_f, p, d, i, seed)
                 dl[i] = split_reduce_ref(cands, feat_ok, k_cols, seed, d, i)
             cl = np.zeros(n, dtype=np.int64); cr = np.zeros(n, dtype=np.int64)
@@ -311,6 +321,9 @@ class RefTreeBuilder:
         res = TreeLevels(decs, cls, crs, n_leaves)
         res.root_weight = float(aux[:, 0].astype(np.float64).sum())
         self.leafsum = torch.tensor(np.array(leafsum, dtype=np.float64).reshape(-1, 2))
+        if coll.is_dist():
+            coll.all_reduce_(self.leafsum)
+            res.root_weight = coll.all_reduce_scalar(res.root_weight)
         self.leaf_of_row = torch.from_numpy(leaf_of_row.astype(np.int32))
         if leaf_fn is not None:
             res.leaf_values = leaf_fn(self.leafsum).to(torch.float32).cpu().numpy()

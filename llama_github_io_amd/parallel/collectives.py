@@ -28,10 +28,17 @@ def all_reduce_sum(t: torch.Tensor) -> torch.Tensor:
     return all_reduce_(t)
 
 
+def comm_device() -> torch.device:
+    """Device collectives must use: the rank's GPU under RCCL ('nccl'), the CPU under gloo."""
+    if is_dist() and dist.get_backend() == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
 def all_reduce_scalar(x: float, device=None) -> float:
     if not is_dist():
         return float(x)
-    t = torch.tensor([float(x)], dtype=torch.float64, device=device or "cpu")
+    t = torch.tensor([float(x)], dtype=torch.float64, device=device or comm_device())
     dist.all_reduce(t)
     return float(t.item())
 

@@ -1,0 +1,130 @@
+"""Per-algorithm behaviour on the CPU reference path (the same code drives the HIP kernels on GPU)."""
+import numpy as np
+import pytest
+import torch
+
+from llama_github_io_amd.models.base import DataInfo
+
+
+def _cls(N=3000, F=5, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    X = torch.randn(F, N, generator=g)
+    y = (torch.rand(N, generator=g) < torch.sigmoid(2 * X[0] - X[1] + X[2] * X[3])).float()
+    return X, y, DataInfo([f"x{i}" for i in range(F)], np.zeros(F, np.int32), [None] * F, "y", ["0", "1"])
+
+
+def _reg(N=3000, F=5, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    X = torch.randn(F, N, generator=g)
+    y = 3 * X[0] - 2 * X[1] + 0.1 * torch.randn(N, generator=g)
+    return X, y, DataInfo([f"x{i}" for i in range(F)], np.zeros(F, np.int32), [None] * F, "y", None)
+
+
+def test_drf_oob_and_multinomial():
+    from llama_github_io_amd.models.drf import DRFTrainer
+    X, y, info = _cls()
+    m = DRFTrainer(dict(ntrees=15, seed=1, max_depth=10)).fit(X, y, None, None, info)
+    assert m.output["training_metrics"]["AUC"] > 0.8      # OOB AUC
+    yk = torch.bucketize(X[0], torch.tensor([-0.5, 0.5])).float()
+    info3 = DataInfo(info.x, info.iscat, info.domains, "y", ["a", "b", "c"])
+    m = DRFTrainer(dict(ntrees=10, seed=1)).fit(X, yk, None, None, info3)
+    P = m._predict_tensor(X)
+    assert P.shape == (X.shape[1], 3) and torch.allclose(P.sum(1), torch.ones(X.shape[1]), atol=1e-5)
+    assert (P.argmax(1).float() == yk).float().mean() > 0.9
+
+
+def test_xrt_random_splits():
+    from llama_github_io_amd.models.drf import DRFTrainer
+    X, y, info = _cls()
+    m = DRFTrainer(dict(ntrees=10, seed=1, histogram_type="Random")).fit(X, y, None, None, info)
+    assert m.output["training_metrics"]["AUC"] > 0.75
+
+
+def test_xgboost_objectives_and_dart():
+    from llama_github_io_amd.models.xgboost import XGBoostTrainer
+    X, y, info = _cls()
+    m = XGBoostTrainer(dict(ntrees=20, seed=1)).fit(X, y, None, None, info)
+    assert m.output["training_metrics"]["AUC"] > 0.85
+    f = m.forest.predict_raw(X)[:, 0] + m.init_f[0]
+    assert torch.allclose(torch.sigmoid(f), m._predict_tensor(X)[:, 1], atol=1e-5)
+    m = XGBoostTrainer(dict(ntrees=10, seed=1, booster="dart", rate_drop=0.3)).fit(X, y, None, None, info)
+    assert m.output["training_metrics"]["AUC"] > 0.8
+    f = m.forest.predict_raw(X)[:, 0] + m.init_f[0]
+    # dart weights folded into the leaves reproduce the training margin
+    Xr, yr, infor = _reg()
+    m = XGBoostTrainer(dict(ntrees=30, seed=1)).fit(Xr, yr, None, None, infor)
+    assert m.output["training_metrics"]["r2"] > 0.9
+    m = XGBoostTrainer(dict(ntrees=30, booster="gblinear", learn_rate=0.5)).fit(Xr, yr, None, None, infor)
+    assert m.output["training_metrics"]["r2"] > 0.95
+
+
+def test_gbm_distributions():
+    from llama_github_io_amd.models.gbm import GBMTrainer
+    Xr, yr, infor = _reg()
+    for d in ("gaussian", "laplace", "huber", "quantile"):
+        m = GBMTrainer(dict(ntrees=20, distribution=d, seed=1)).fit(Xr, yr, None, None, infor)
+        assert m.output["training_metrics"]["r2"] > 0.7, d
+    yp = torch.poisson(torch.exp(0.5 * Xr[0]))
+    m = GBMTrainer(dict(ntrees=20, distribution="poisson", seed=1)).fit(Xr, yp, None, None, infor)
+    assert m.output["training_metrics"]["mean_residual_deviance"] < float(yp.var())
+
+
+def test_glm_families():
+    from llama_github_io_amd.models.glm import GLMTrainer
+    Xr, yr, infor = _reg()
+    m = GLMTrainer(dict(family="gaussian", lambda_=0)).fit(Xr, yr, None, None, infor)
+    c = m.output["coefficients"]
+    assert abs(c["x0"] - 3) < 0.02 and abs(c["x1"] + 2) < 0.02
+    mu = torch.exp(0.3 * Xr[0] + 0.2)
+    yg = torch.distributions.Gamma(2.0, 2.0 / mu).sample()
+    m = GLMTrainer(dict(family="gamma", link="log", lambda_=0)).fit(Xr, yg, None, None, infor)
+    assert abs(m.output["coefficients"]["x0"] - 0.3) < 0.05
+    X, y, info = _cls()
+    yk = torch.bucketize(X[0] - X[1], torch.tensor([-0.5, 0.5])).float()
+    info3 = DataInfo(info.x, info.iscat, info.domains, "y", ["a", "b", "c"])
+    m = GLMTrainer(dict(family="multinomial", lambda_=0)).fit(X, yk, None, None, info3)
+    assert m.output["training_metrics"]["mean_per_class_error"] < 0.1
+    m = GLMTrainer(dict(family="ordinal", lambda_=0)).fit(X, yk, None, None, info3)
+    assert m.output["training_metrics"]["mean_per_class_error"] < 0.2
+    m = GLMTrainer(dict(family="binomial", lambda_search=True, alpha=1.0, nlambdas=20)).fit(X, y, None, None, info)
+    assert len(m.output["regularization_path"]["lambdas"]) == 20
+
+
+def test_kmeans_and_estimate_k():
+    from llama_github_io_amd.models.kmeans import KMeansTrainer
+    g = torch.Generator().manual_seed(0)
+    cs = torch.tensor([[5.0, 5], [-5, 5], [0, -6]])
+    X = torch.cat([cs[i][:, None] + torch.randn(2, 400, generator=g) * 0.5 for i in range(3)], 1)
+    info = DataInfo(["a", "b"], np.zeros(2, np.int32), [None, None], None, None)
+    m = KMeansTrainer(dict(k=3, seed=2, init="PlusPlus", standardize=False)).fit(X, None, None, None, info)
+    got = sorted(map(tuple, np.round(np.asarray(m.output["centers"]))))
+    assert got == sorted(map(tuple, cs.numpy()))
+    # estimate_k: H2O's cutoff min(0.02 + 10/N + 2.5/F^2, 0.8) needs enough features to be selective
+    c10 = torch.randn(3, 10, generator=g) * 6
+    X10 = torch.cat([c10[i][:, None] + torch.randn(10, 400, generator=g) * 0.5 for i in range(3)], 1)
+    info10 = DataInfo([f"c{i}" for i in range(10)], np.zeros(10, np.int32), [None] * 10, None, None)
+    m = KMeansTrainer(dict(k=8, estimate_k=True, seed=2, standardize=False)).fit(X10, None, None, None, info10)
+    assert m.output["k"] == 3
+
+
+def test_deeplearning_regression_and_autoencoder():
+    from llama_github_io_amd.models.deeplearning import DeepLearningTrainer
+    Xr, yr, infor = _reg()
+    m = DeepLearningTrainer(dict(hidden=[32], epochs=10, seed=1, mini_batch_size=32)).fit(Xr, yr, None, None, infor)
+    assert m.output["training_metrics"]["r2"] > 0.9
+    m = DeepLearningTrainer(dict(hidden=[32], epochs=3, seed=1, activation="Maxout", adaptive_rate=False,
+                                 rate=0.01, momentum_start=0.5, momentum_stable=0.9, mini_batch_size=16)).fit(Xr, yr, None, None, infor)
+    assert m.output["training_metrics"]["r2"] > 0.8
+
+
+def test_isolation_forests_rank_outliers():
+    from llama_github_io_amd.models.isoforest import ExtendedIsolationForestTrainer, IsolationForestTrainer
+    g = torch.Generator().manual_seed(0)
+    X = torch.cat([torch.randn(3, 1000, generator=g), torch.randn(3, 10, generator=g) * 0.2 + 6], 1)
+    info = DataInfo(["a", "b", "c"], np.zeros(3, np.int32), [None] * 3, None, None)
+    m = IsolationForestTrainer(dict(ntrees=40, seed=1)).fit(X, None, None, None, info)
+    P = m._predict_tensor(X)
+    assert float(P[-10:, 0].mean()) > float(P[:1000, 0].mean()) + 0.2
+    m = ExtendedIsolationForestTrainer(dict(ntrees=40, seed=1, extension_level=2)).fit(X, None, None, None, info)
+    P = m._predict_tensor(X)
+    assert float(P[-10:, 0].mean()) > float(P[:1000, 0].mean()) + 0.1

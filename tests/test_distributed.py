@@ -1,0 +1,88 @@
+"""Multi-process (gloo, world_size=2) tests of the row-sharded distributed paths: histogram trees,
+GLM Gram all-reduce, KMeans centroid all-reduce, DeepLearning gradient all-reduce. Each rank holds
+half of the rows; the sharded model must equal the single-process model on the full data."""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _data(N=3000, F=5, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    X = torch.randn(F, N, generator=g)
+    y = (torch.rand(N, generator=g) < torch.sigmoid(2 * X[0] - X[1] + 0.5 * X[2] * X[3])).float()
+    return X, y
+
+
+def _info(F):
+    from llama_github_io_amd.models.base import DataInfo
+    return DataInfo([f"x{i}" for i in range(F)], np.zeros(F, np.int32), [None] * F, "y", ["0", "1"])
+
+
+def _train(algo, X, y, info):
+    if algo == "gbm":
+        from llama_github_io_amd.models.gbm import GBMTrainer
+        m = GBMTrainer(dict(ntrees=4, max_depth=3, seed=7)).fit(X, y, None, None, info)
+        return m.forest.predict_raw(_data()[0])[:, 0]
+    if algo == "glm":
+        from llama_github_io_amd.models.glm import GLMTrainer
+        m = GLMTrainer(dict(family="binomial", lambda_=0.0)).fit(X, y, None, None, info)
+        return m.beta[0].float()
+    if algo == "kmeans":
+        from llama_github_io_amd.models.base import DataInfo
+        from llama_github_io_amd.models.kmeans import KMeansTrainer
+        inf = DataInfo(info.x, info.iscat, info.domains, None, None)
+        tr = KMeansTrainer(dict(k=3, seed=3, init="User", standardize=False,
+                                user_points=np.array([[1, 0, 0, 0, 0], [-1, 0, 0, 0, 0], [0, 1, 0, 0, 0]], np.float32)))
+        m = tr.fit(X, None, None, None, inf)
+        return m.centers_std.flatten()
+    raise ValueError(algo)
+
+
+def _worker(rank, world, port, algo, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      H2O_AMD_DEVICE="cpu")
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        X, y = _data()
+        N = X.shape[1]
+        sl = slice(rank * N // world, (rank + 1) * N // world)
+        out = _train(algo, X[:, sl].contiguous(), y[sl].contiguous(), _info(X.shape[0]))
+        if rank == 0:
+            q.put(out.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(algo, world=2):
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, algo, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=240)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    return res
+
+
+@pytest.mark.parametrize("algo", ["gbm", "glm", "kmeans"])
+def test_sharded_equals_single(algo):
+    X, y = _data()
+    single = _train(algo, X, y, _info(X.shape[0])).numpy()
+    sharded = _run(algo)
+    tol = 1e-4 if algo != "glm" else 1e-5
+    assert np.allclose(single, sharded, atol=tol, rtol=1e-4), (single[:5], sharded[:5])

@@ -1,0 +1,107 @@
+"""HIP kernels vs fp32/fp64 PyTorch references of the same op (run on an MI355X)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+dev = torch.device("cuda", 0)
+
+
+def test_native_library_loads():
+    from llama_github_io_amd.ops import _native
+    lib = _native.hip()
+    assert lib is not None and hasattr(lib, "h2o_gram") and hasattr(lib, "h2o_kmeans_assign")
+
+
+@pytest.mark.parametrize("N,P", [(1000, 7), (70001, 64), (5000, 130), (33, 200)])
+def test_gram_matches_fp64(N, P):
+    from llama_github_io_amd.ops.gram import gram, xtv
+    g = torch.Generator(device=dev).manual_seed(N + P)
+    Z = torch.randn(N, P, device=dev, generator=g)
+    w = torch.rand(N, device=dev, generator=g)
+    G = gram(Z, w)
+    ref = (Z.double() * w.double()[:, None]).T @ Z.double()
+    scale = (Z.double().abs() * w.double()[:, None]).T @ Z.double().abs()
+    assert torch.all((G - ref).abs() <= 1e-5 * scale + 1e-6)
+    v = torch.randn(N, 3, device=dev, generator=g)
+    assert torch.allclose(xtv(Z, v), Z.double().T @ v.double(), rtol=1e-4, atol=1e-3)
+    assert torch.allclose(gram(Z), Z.double().T @ Z.double(), rtol=1e-4, atol=1e-2)
+
+
+def test_kmeans_assign_matches_reference():
+    from llama_github_io_amd.ops.dense import kmeans_assign
+    g = torch.Generator(device=dev).manual_seed(1)
+    X = torch.randn(10007, 13, device=dev, generator=g)
+    C = torch.randn(9, 13, device=dev, generator=g)
+    a, d = kmeans_assign(X, C)
+    D = ((X[:, None, :].double() - C[None].double()) ** 2).sum(-1)
+    dref, aref = D.min(1)
+    assert (a == aref).float().mean() > 0.999
+    assert torch.allclose(d.double(), dref, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("act", ["rectifier", "tanh", "exprectifier", "linear"])
+@pytest.mark.parametrize("drop", [0.0, 0.3])
+def test_bias_act_fwd_bwd(act, drop):
+    from llama_github_io_amd.ops.dense import bias_act
+    g = torch.Generator(device=dev).manual_seed(2)
+    x = torch.randn(517, 70, device=dev, generator=g)
+    b = torch.randn(70, device=dev, generator=g)
+    gy = torch.randn(517, 70, device=dev, generator=g)
+    xg = x.clone().requires_grad_(True)
+    bg = b.clone().requires_grad_(True)
+    y = bias_act(xg, bg, act, drop, 1234)
+    y.backward(gy)
+    xc = x.cpu().requires_grad_(True)
+    bc = b.cpu().requires_grad_(True)
+    yc = bias_act(xc, bc, act, drop, 1234)
+    yc.backward(gy.cpu())
+    assert torch.allclose(y.cpu(), yc, atol=1e-5, rtol=1e-5)
+    assert torch.allclose(xg.grad.cpu(), xc.grad, atol=1e-5, rtol=1e-5)
+    assert torch.allclose(bg.grad.cpu(), bc.grad, atol=1e-3, rtol=1e-4)
+
+
+def _info(F, dom=("0", "1")):
+    from llama_github_io_amd.models.base import DataInfo
+    return DataInfo([f"x{i}" for i in range(F)], np.zeros(F, np.int32), [None] * F, "y", list(dom) if dom else None)
+
+
+def test_glm_gpu_matches_cpu():
+    from llama_github_io_amd.models.glm import GLMTrainer
+    g = torch.Generator().manual_seed(0)
+    X = torch.randn(6, 20000, generator=g)
+    y = (torch.rand(20000, generator=g) < torch.sigmoid(X[0] - 2 * X[1] + 0.3)).float()
+    mc = GLMTrainer(dict(family="binomial", lambda_=0.0)).fit(X, y, None, None, _info(6))
+    mg = GLMTrainer(dict(family="binomial", lambda_=0.0)).fit(X.to(dev), y.to(dev), None, None, _info(6))
+    assert np.allclose(mc.beta.cpu().numpy(), mg.beta.cpu().numpy(), atol=1e-4)
+
+
+def test_tree_family_trains_on_gpu():
+    from llama_github_io_amd.models.drf import DRFTrainer
+    from llama_github_io_amd.models.isoforest import IsolationForestTrainer
+    from llama_github_io_amd.models.xgboost import XGBoostTrainer
+    g = torch.Generator(device=dev).manual_seed(0)
+    X = torch.randn(8, 50000, device=dev, generator=g)
+    y = (torch.rand(50000, device=dev, generator=g) < torch.sigmoid(2 * X[0] - X[1] * X[2])).float()
+    m = DRFTrainer(dict(ntrees=10, max_depth=8, seed=1)).fit(X, y, None, None, _info(8))
+    assert m.output["training_metrics"]["AUC"] > 0.75
+    m = XGBoostTrainer(dict(ntrees=10, seed=1)).fit(X, y, None, None, _info(8))
+    assert m.output["training_metrics"]["AUC"] > 0.8
+    # forest scoring kernel == torch traversal
+    fr = m.forest
+    a = fr.predict_raw(X[:, :5000])
+    b = fr.predict_raw(X[:, :5000].cpu())
+    assert torch.allclose(a.cpu(), b, atol=1e-5)
+    Xo = torch.cat([X[:, :2000], X[:, :20] * 8], 1)
+    m = IsolationForestTrainer(dict(ntrees=30, seed=1)).fit(Xo, None, None, None, _info(8, None))
+    P = m._predict_tensor(Xo)
+    assert float(P[-20:, 0].mean()) > float(P[:2000, 0].mean())
+
+
+def test_deeplearning_gpu_learns():
+    from llama_github_io_amd.models.deeplearning import DeepLearningTrainer
+    g = torch.Generator(device=dev).manual_seed(0)
+    X = torch.randn(6, 20000, device=dev, generator=g)
+    y = ((X[0] * X[1] + X[2]) > 0).float()
+    m = DeepLearningTrainer(dict(hidden=[64, 64], epochs=3, seed=1)).fit(X, y, None, None, _info(6))
+    assert m.output["training_metrics"]["AUC"] > 0.9
