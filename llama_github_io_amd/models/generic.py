@@ -1,0 +1,189 @@
+"""Generic model: a model imported from a MOJO (reference: ``hex/generic/Generic.java``,
+``GenericModel.java`` — scoring through genmodel without the original algorithm)."""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from .base import DataInfo, Model, make_key
+
+
+class GenericModel(Model):
+    algo = "generic"
+
+    @staticmethod
+    def from_mojo(path: str, model_id=None) -> "GenericModel":
+        from ..mojo.reader import _floats, parse_mojo
+        from ..ops.forest import Forest
+        mj = parse_mojo(path)
+        ki = mj["info"]
+        if mj["state"] is not None:                    # framework-native payload
+            from ..persist import _from_state
+            st = mj["state"]
+            inner = _from_state(st)
+            m = GenericModel(model_id or make_key("generic"), dict(path=path), inner.info)
+            m.inner = inner
+            m.output = dict(inner.output)
+            m.mojo_info = ki
+            return m
+        cols = mj["columns"]
+        sup = ki.get("supervised", "false") == "true"
+        nfeat = int(ki["n_features"])
+        xs = cols[:nfeat]
+        doms = [mj["domains"].get(i) for i in range(nfeat)]
+        iscat = np.array([1 if d is not None else 0 for d in doms], dtype=np.int32)
+        resp = cols[nfeat] if sup and len(cols) > nfeat else None
+        rdom = mj["domains"].get(nfeat) if resp else None
+        info = DataInfo(xs, iscat, doms, resp, rdom)
+        m = GenericModel(model_id or make_key("generic"), dict(path=path), info)
+        m.mojo_info = ki
+        m.inner = None
+        algo = ki["algo"]
+        m.output["original_algo"] = algo
+        cat = ki.get("category", "Regression")
+        m.output["model_category"] = cat
+        if algo in ("gbm", "drf", "isolationforest"):
+            K = int(ki.get("n_trees_per_class", 1))
+            n = int(ki["n_trees"])
+            fr = Forest(n_classes_out=K)
+            binom_drf = algo == "drf" and cat == "Binomial" and K == 1
+            vmap = (lambda v: 1.0 - v) if binom_drf else (lambda v: v)
+            from ..mojo.treebytes import bytes_to_tree
+            for it in range(n):
+                for c in range(K):
+                    name = f"trees/t{c:02d}_{it:03d}.bin"
+                    if name in mj["trees"]:
+                        fr.add(bytes_to_tree(mj["trees"][name], vmap), c)
+            m.forest = fr
+            m.ntrees = n
+        elif algo == "glm":
+            m.beta = torch.tensor(_floats(ki["beta"]), dtype=torch.float64)
+            m.cat_offsets = [int(v) for v in _floats(ki["cat_offsets"])]
+            m.use_all = ki.get("use_all_factor_levels") == "true"
+            m.num_means = _floats(ki.get("num_means", "[]"))
+            m.cat_modes = [int(v) for v in _floats(ki.get("cat_modes", "[]"))]
+        elif algo == "kmeans":
+            m.centers = torch.tensor([_floats(ki[f"center_{i}"]) for i in range(int(ki["center_num"]))], dtype=torch.float64)
+            m.std = ki.get("standardize") == "true"
+            if m.std:
+                m.means = _floats(ki["standardize_means"])
+                m.mults = _floats(ki["standardize_mults"])
+                m.modes = [int(v) for v in _floats(ki["standardize_modes"])]
+        else:
+            raise NotImplementedError(f"MOJO algo {algo} not supported by this reader")
+        return m
+
+    @property
+    def model_category(self):
+        return self.output.get("model_category", "Regression")
+
+    def default_threshold(self):
+        if self.inner is not None:
+            return self.inner.default_threshold()
+        if self.model_category != "Binomial":
+            return None
+        return float(self.mojo_info.get("default_threshold", 0.5))
+
+    def prediction_names(self):
+        if self.inner is not None:
+            return self.inner.prediction_names()
+        if self.output.get("original_algo") == "isolationforest":
+            return ["predict", "mean_length"]
+        return None
+
+    def _design(self, X):
+        """GLM/KMeans layout: one-hot categoricals (cats first), then numerics (GlmMojoModel)."""
+        info = self.info
+        cats = [j for j in range(info.F) if info.iscat[j]]
+        nums = [j for j in range(info.F) if not info.iscat[j]]
+        N = X.shape[1]
+        use_all = getattr(self, "use_all", True)
+        ncat_cols = sum(len(info.domains[j]) - (0 if use_all else 1) for j in cats)
+        Z = torch.zeros(N, ncat_cols + len(nums), dtype=torch.float64, device=X.device)
+        off = 0
+        modes = getattr(self, "cat_modes", None) or getattr(self, "modes", None) or [0] * len(cats)
+        for i, j in enumerate(cats):
+            L = len(info.domains[j])
+            c = X[j]
+            c = torch.where(torch.isnan(c), torch.full_like(c, float(modes[i] if i < len(modes) else 0)), c).long()
+            col = c - (0 if use_all else 1)
+            ok = (col >= 0) & (col < L - (0 if use_all else 1))
+            rows = torch.nonzero(ok).flatten()
+            Z[rows, off + col[rows]] = 1
+            off += L - (0 if use_all else 1)
+        for i, j in enumerate(nums):
+            v = X[j].double()
+            mu = (getattr(self, "num_means", None) or getattr(self, "means", None) or [0.0] * len(nums))
+            Z[:, off + i] = torch.where(torch.isnan(v), torch.full_like(v, mu[i] if i < len(mu) else 0.0), v)
+        return Z, off
+
+    def _predict_tensor(self, X, offset=None):
+        if self.inner is not None:
+            return self.inner._predict_tensor(X, offset)
+        ki = self.mojo_info
+        algo = ki["algo"]
+        cat = self.model_category
+        if algo == "gbm":
+            f = self.forest.predict_raw(X) + float(ki.get("init_f", 0.0))
+            if offset is not None:
+                f = f + offset[:, None]
+            d = ki.get("distribution", "gaussian")
+            if d == "multinomial":
+                return torch.softmax(f, 1)
+            if d in ("bernoulli", "quasibinomial", "modified_huber"):
+                p1 = torch.sigmoid(f[:, 0])
+                return torch.stack([1 - p1, p1], 1)
+            if ki.get("link_function") == "log":
+                return torch.exp(f[:, 0])
+            return f[:, 0]
+        if algo == "drf":
+            s = self.forest.predict_raw(X) / max(1, self.ntrees)
+            if cat == "Regression":
+                return s[:, 0]
+            if cat == "Binomial" and s.shape[1] == 1:
+                p1 = s[:, 0].clamp(0, 1)
+                return torch.stack([1 - p1, p1], 1)
+            return s / s.sum(1, keepdim=True).clamp(min=1e-30)
+        if algo == "isolationforest":
+            s = self.forest.predict_raw(X)[:, 0].double()
+            mn, mx = float(ki["min_path_length"]), float(ki["max_path_length"])
+            score = (mx - s) / (mx - mn) if mx > mn else torch.ones_like(s)
+            return torch.stack([score.float(), (s / max(1, self.ntrees)).float()], 1)
+        if algo == "glm":
+            Z, _ = self._design(X)
+            fam, link = ki["family"], ki["link"]
+            nb = Z.shape[1] + 1
+            B = self.beta.to(Z.device).view(-1, nb)
+            eta = Z @ B[:, :-1].T + B[:, -1]
+            if offset is not None:
+                eta = eta + offset.double()[:, None]
+            if fam == "multinomial":
+                return torch.softmax(eta, 1).float()
+            from .glm import Family
+            mu = Family(fam, link, 0.0, float(ki.get("tweedie_link_power", 1.0))).linkinv(eta[:, 0])
+            if fam in ("binomial", "quasibinomial", "fractionalbinomial"):
+                return torch.stack([1 - mu, mu], 1).float()
+            return mu.float()
+        if algo == "kmeans":
+            Z, off = self._design(X)
+            if self.std:
+                mu = torch.tensor(self.means, dtype=torch.float64, device=Z.device)
+                mul = torch.tensor(self.mults, dtype=torch.float64, device=Z.device)
+                Z[:, off:] = (Z[:, off:] - mu) * mul
+            D = ((Z[:, None, :] - self.centers.to(Z.device)[None]) ** 2).sum(-1)
+            return D.argmin(1).float()
+        raise NotImplementedError(algo)
+
+
+class GenericTrainer:
+    """``H2OGenericEstimator(path=...)``: 'training' imports the MOJO."""
+
+    def __init__(self, params):
+        self.p = dict(params)
+        self.job = None
+
+    def fit(self, X=None, y=None, w=None, offset=None, info=None, valid=None, model_key=None):
+        path = self.p.get("path") or self.p.get("model_key")
+        return GenericModel.from_mojo(path, model_key)

@@ -292,6 +292,7 @@ class GLMTrainer:
         p.update({k: v for k, v in params.items() if v is not None})
         self.p = p
         self.job = None
+        self.penalty = None     # optional (P+1)x(P+1) quadratic penalty (GAM)
 
     def _family(self, info):
         fam = str(self.p["family"]).lower()
@@ -411,6 +412,8 @@ class GLMTrainer:
                     r = coll.all_reduce_(r)
                 Gm = Gm * obj_reg
                 r = r * obj_reg
+                if self.penalty is not None:          # GAM smoothness penalty (standardized space)
+                    Gm = Gm + self.penalty.to(Gm.device)
                 if not intercept:
                     Gm[-1, :] = 0
                     Gm[:, -1] = 0

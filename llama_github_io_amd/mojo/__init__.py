@@ -1,1 +1,2 @@
-
+"""MOJO export / import (reference: ``h2o-genmodel`` — ``AbstractMojoWriter``, ``ModelMojoReader``,
+``SharedTreeMojoModel``, ``GlmMojoModel``, ``KMeansMojoModel``, ``IsolationForestMojoModel``)."""
