@@ -70,8 +70,7 @@ def prepare(algo: str, params: dict, x=None, y=None, training_frame=None):
     fr = training_frame
     y = _resolve_names(fr, y)
     y = y[0] if y else None
-    special = {params.get("weights_column"), params.get("offset_column"), params.get("fold_column"),
-               params.get("treatment_column"), y}
+    special = {params.get("weights_column"), params.get("offset_column"), params.get("fold_column"), y}
     special.discard(None)
     ignored = set(_resolve_names(fr, params.get("ignored_columns")) or [])
     if x is None:
@@ -150,6 +149,11 @@ def train(algo: str, params: dict, x=None, y=None, training_frame=None, validati
     spec = REGISTRY[algo]
     p = dict(spec.defaults)
     p.update({k: v for k, v in params.items() if v is not None})
+    if algo == "generic":                       # import a MOJO: no training frame involved
+        m = spec.trainer(p).fit(model_key=model_id or p.get("model_id"))
+        m.algo = "generic"
+        dkv.put(m.key, m)
+        return m
     if spec.supervised and y is None and not spec.needs_response_optional:
         raise ValueError(f"{algo} needs a response column y")
     fr = training_frame
@@ -175,6 +179,8 @@ def train(algo: str, params: dict, x=None, y=None, training_frame=None, validati
         cv_out = _cross_validate(spec, p, fr, info, X, yv, w, off, seed, mid, job)
     tr = spec.trainer({k: v for k, v in p.items() if k not in COMMON})
     tr.job = job
+    if algo == "word2vec":
+        tr.strings = fr._col(info.x[0]).to_numpy()
     model = tr.fit(X, yv, w, off, info, valid, mid) if yv is not None or not spec.supervised else tr.fit(X, yv, w, off, info, valid, mid)
     model.params.update({k: p.get(k) for k in COMMON if k in p and k not in ("training_frame", "validation_frame", "x", "y")})
     model.output["names"] = info.x + ([info.response] if info.response else [])

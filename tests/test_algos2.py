@@ -1,0 +1,122 @@
+"""Remaining algorithms through the h2o facade (CPU reference path)."""
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+import h2o
+from h2o.estimators import (H2OAggregatorEstimator, H2OANOVAGLMEstimator, H2OCoxProportionalHazardsEstimator,
+                            H2ODecisionTreeEstimator, H2OExtendedIsolationForestEstimator, H2OGeneralizedAdditiveEstimator,
+                            H2OGeneralizedLowRankEstimator, H2OGenericEstimator, H2OGradientBoostingEstimator,
+                            H2OInfogram, H2OIsotonicRegressionEstimator, H2OModelSelectionEstimator,
+                            H2ONaiveBayesEstimator, H2OPrincipalComponentAnalysisEstimator, H2ORuleFitEstimator,
+                            H2OSingularValueDecompositionEstimator, H2OSupportVectorMachineEstimator,
+                            H2OTargetEncoderEstimator, H2OUpliftRandomForestEstimator, H2OWord2vecEstimator)
+
+
+@pytest.fixture(scope="module")
+def df():
+    h2o.init(verbose=False)
+    rng = np.random.default_rng(1)
+    n = 1500
+    d = pd.DataFrame({"a": rng.normal(size=n), "b": rng.normal(size=n), "c": rng.choice(list("xyz"), n),
+                      "t": rng.choice(["0", "1"], n)})
+    d["y"] = np.where(d.a - d.b + (d.c == "x") + rng.normal(size=n) * 0.3 > 0, "1", "0")
+    d["r"] = np.sin(d.a) * 2 + d.b + rng.normal(size=n) * 0.1
+    return h2o.H2OFrame(d, column_types={"t": "enum", "y": "enum"})
+
+
+def test_pca_svd_glrm(df):
+    p = H2OPrincipalComponentAnalysisEstimator(k=2, transform="STANDARDIZE")
+    p.train(x=["a", "b", "r"], training_frame=df)
+    assert p.predict(df).names == ["PC1", "PC2"]
+    imp = p._model.output["importance"]["proportion_of_variance"]
+    assert imp[0] >= imp[1] > 0
+    s = H2OSingularValueDecompositionEstimator(nv=2)
+    s.train(x=["a", "b", "r"], training_frame=df)
+    assert len(s._model.output["d"]) == 2
+    g = H2OGeneralizedLowRankEstimator(k=2, init="SVD", max_iterations=100)
+    g.train(x=["a", "b", "r"], training_frame=df)
+    assert g._model.output["objective"] >= 0 and g.predict(df).ncols == 3
+
+
+def test_naivebayes_dt_psvm_rulefit(df):
+    for E, kw in ((H2ONaiveBayesEstimator, {}), (H2ODecisionTreeEstimator, dict(max_depth=5)),
+                  (H2OSupportVectorMachineEstimator, dict(gamma=0.5)),
+                  (H2ORuleFitEstimator, dict(rule_generation_ntrees=6, max_num_rules=5, seed=1))):
+        m = E(**kw)
+        m.train(x=["a", "b", "c"], y="y", training_frame=df)
+        auc = m._model.output["training_metrics"]["AUC"]
+        assert auc > 0.8, (E.__name__, auc)
+
+
+def test_isotonic_gam_anova_modelselection(df):
+    m = H2OIsotonicRegressionEstimator()
+    m.train(x=["a"], y="r", training_frame=df)
+    assert m._model.output["training_metrics"]["r2"] > 0.5
+    g = H2OGeneralizedAdditiveEstimator(gam_columns=["a"], num_knots=[8])
+    g.train(x=["a", "b"], y="r", training_frame=df)
+    assert g._model.output["training_metrics"]["r2"] > 0.95
+    a = H2OANOVAGLMEstimator(highest_interaction_term=2)
+    a.train(x=["a", "b"], y="r", training_frame=df)
+    t = {r["term"]: r["p_value"] for r in a._model.output["anova_table"]}
+    assert t["a"] < 1e-6 and t["b"] < 1e-6
+    s = H2OModelSelectionEstimator(mode="maxr", max_predictor_number=2)
+    s.train(x=["a", "b"], y="r", training_frame=df)
+    assert s._model.get_best_R2_values()[-1] > 0.8
+
+
+def test_coxph(df):
+    rng = np.random.default_rng(0)
+    n = 1000
+    x = rng.normal(size=n)
+    T = rng.exponential(1 / np.exp(0.8 * x))
+    C = rng.exponential(2.0, n)
+    fr = h2o.H2OFrame(pd.DataFrame({"x": x, "time": np.minimum(T, C), "event": (T <= C).astype(int)}))
+    m = H2OCoxProportionalHazardsEstimator(stop_column="time")
+    m.train(x=["x", "time"], y="event", training_frame=fr)
+    assert abs(m._model.output["coefficients"]["x"] - 0.8) < 0.15
+    assert m._model.output["concordance"] > 0.6
+
+
+def test_uplift_te_aggregator_eif(df):
+    u = H2OUpliftRandomForestEstimator(ntrees=5, max_depth=4, treatment_column="t", seed=1)
+    u.train(x=["a", "b", "t"], y="y", training_frame=df)
+    assert u.predict(df).names == ["uplift_predict", "p_y1_with_treatment", "p_y1_without_treatment"]
+    te = H2OTargetEncoderEstimator(blending=True)
+    te.train(x=["c"], y="y", training_frame=df)
+    assert "c_te" in te.transform(df).names
+    ag = H2OAggregatorEstimator(target_num_exemplars=100)
+    ag.train(x=["a", "b"], training_frame=df)
+    out = ag._model.aggregated_frame()
+    assert 50 <= out.nrows <= 150 and abs(out["counts"].sum() - df.nrows) < 1e-9
+    e = H2OExtendedIsolationForestEstimator(ntrees=10, extension_level=1, seed=1)
+    e.train(x=["a", "b"], training_frame=df)
+    assert e.predict(df).names == ["anomaly_score", "mean_length"]
+
+
+def test_word2vec_and_infogram(df):
+    rng = np.random.default_rng(0)
+    words = []
+    for i in range(800):
+        words += list(rng.choice(["cat", "dog", "cow"] if i % 2 else ["one", "two", "six"], 5)) + [None]
+    fr = h2o.H2OFrame(pd.DataFrame({"w": words}), column_types={"w": "string"})
+    w2v = H2OWord2vecEstimator(vec_size=8, min_word_freq=1, epochs=3, seed=1, sent_sample_rate=0)
+    w2v.train(training_frame=fr)
+    syn = w2v._model.find_synonyms("cat", 2)
+    assert set(syn) <= {"dog", "cow", "one", "two", "six"} and len(syn) == 2
+    ig = H2OInfogram(top_n_features=3, seed=1, algorithm_params=dict(ntrees=5))
+    ig.train(x=["a", "b", "c"], y="y", training_frame=df)
+    assert set(ig._model.get_admissible_features()) <= {"a", "b", "c"}
+
+
+def test_mojo_roundtrip_generic(df, tmp_path):
+    m = H2OGradientBoostingEstimator(ntrees=5, seed=1)
+    m.train(x=["a", "b", "c"], y="y", training_frame=df)
+    path = m.download_mojo(str(tmp_path))
+    g = H2OGenericEstimator(path=path)
+    g.train()
+    a = m.predict(df).as_data_frame()
+    b = g.predict(df).as_data_frame()
+    assert np.allclose(a["1"].values, b["1"].values, atol=1e-6)
+    assert (a["predict"] == b["predict"]).all()
