@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#define AMAX_SHARDS 64  // must match tree_kernels.hip
+
 enum Dist { D_GAUSSIAN = 0, D_BERNOULLI = 1, D_QUASIBINOMIAL = 2, D_POISSON = 3, D_GAMMA = 4, D_TWEEDIE = 5,
             D_LAPLACE = 6, D_QUANTILE = 7, D_HUBER = 8, D_MODIFIED_HUBER = 9 };
 
@@ -25,7 +27,7 @@ __global__ __launch_bounds__(256) void k_gbm_step(
     long long N, int dist, const float* __restrict__ y, const float* __restrict__ w, float* __restrict__ f,
     const float* __restrict__ vals, const int* __restrict__ leaf, float sample_rate, unsigned long long seed,
     float p1 /*tweedie power | quantile alpha | huber delta*/, float4* __restrict__ aux,
-    unsigned* __restrict__ amax_bits /*[2], |.| as uint bits, pre-zeroed*/) {
+    unsigned* __restrict__ amax_bits /*[2*AMAX_SHARDS], |.| as uint bits, pre-zeroed*/) {
   float ma = 0.f, mb = 0.f;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += (long long)gridDim.x * blockDim.x) {
     float fi = f[i];
@@ -79,13 +81,21 @@ __global__ __launch_bounds__(256) void k_gbm_step(
     ma = fmaxf(ma, fabsf(o.x));
     mb = fmaxf(mb, fabsf(o.y));
   }
+  // block max -> ONE atomic pair per block into one of AMAX_SHARDS shards (k_qscale folds the shards):
+  // a single hot word would serialize every wave's atomic (~12 ns each at the memory side)
   for (int off = 32; off > 0; off >>= 1) {
     ma = fmaxf(ma, __shfl_xor(ma, off, 64));
     mb = fmaxf(mb, __shfl_xor(mb, off, 64));
   }
-  if ((threadIdx.x & 63) == 0) {
-    atomicMax(amax_bits + 0, __float_as_uint(ma));   // non-negative floats order like their bit patterns
-    atomicMax(amax_bits + 1, __float_as_uint(mb));
+  __shared__ float sm[2][4];
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { sm[0][wv] = ma; sm[1][wv] = mb; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < (int)(blockDim.x >> 6); ++k) { ma = fmaxf(ma, sm[0][k]); mb = fmaxf(mb, sm[1][k]); }
+    unsigned* sh = amax_bits + 2 * (blockIdx.x & (AMAX_SHARDS - 1));
+    atomicMax(sh + 0, __float_as_uint(ma));   // non-negative floats order like their bit patterns
+    atomicMax(sh + 1, __float_as_uint(mb));
   }
 }
 
@@ -101,7 +111,7 @@ int h2o_gbm_step(long long N, int dist, const void* y, const void* w, void* f, c
                  float sample_rate, unsigned long long seed, float p1, void* aux, void* amax_bits, hipStream_t s) {
   const int blk = 256;
   long long grid = (N + blk - 1) / blk;
-  if (grid > 4096) grid = 4096;
+  if (grid > 2048) grid = 2048;
   if (grid < 1) grid = 1;
   hipLaunchKernelGGL(k_gbm_step, dim3((unsigned)grid), dim3(blk), 0, s, N, dist, (const float*)y, (const float*)w,
                      (float*)f, (const float*)vals, (const int*)leaf, sample_rate, seed, p1, (float4*)aux,

@@ -23,6 +23,7 @@
 #include <stdint.h>
 
 #define NBIN 256
+#define AMAX_SHARDS 64  // per-block |aux| maxima shards (k_amax / k_gbm_step -> k_qscale)
 #define NA_BIN 255
 #define FTILE 32                // features per LDS histogram tile
 #define HS64 (2 * NBIN + 2)     // int64 entries per feature row in LDS: w at [0,256), wY at [257, 513)
@@ -969,15 +970,24 @@ __global__ __launch_bounds__(256) void k_amax(const float4* __restrict__ aux, lo
     ma = fmaxf(ma, __shfl_xor(ma, off, 64));
     mb = fmaxf(mb, __shfl_xor(mb, off, 64));
   }
-  if ((threadIdx.x & 63) == 0) {
-    atomicMax(amax_bits + 0, __float_as_uint(ma));
-    atomicMax(amax_bits + 1, __float_as_uint(mb));
+  __shared__ float sm[2][4];
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { sm[0][wv] = ma; sm[1][wv] = mb; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < (int)(blockDim.x >> 6); ++k) { ma = fmaxf(ma, sm[0][k]); mb = fmaxf(mb, sm[1][k]); }
+    unsigned* sh = amax_bits + 2 * (blockIdx.x & (AMAX_SHARDS - 1));
+    atomicMax(sh + 0, __float_as_uint(ma));
+    atomicMax(sh + 1, __float_as_uint(mb));
   }
 }
 
+// folds the AMAX_SHARDS per-shard maxima, then derives the fixed-point scales
 __global__ void k_qscale(const unsigned* __restrict__ amax_bits, double* __restrict__ qs) {
   if (threadIdx.x < 2) {
-    const double m = (double)__uint_as_float(amax_bits[threadIdx.x]);
+    unsigned mbits = 0u;
+    for (int k = 0; k < AMAX_SHARDS; ++k) mbits = max(mbits, amax_bits[2 * k + threadIdx.x]);
+    const double m = (double)__uint_as_float(mbits);
     const double sc = (m > 0.0 && m == m) ? 1099511627776.0 / m : 1.0;   // 2^40 / max
     qs[threadIdx.x] = sc;
     qs[2 + threadIdx.x] = 1.0 / sc;
@@ -989,6 +999,7 @@ __global__ void k_qscale(const unsigned* __restrict__ amax_bits, double* __restr
 extern "C" {
 
 int h2o_tree_sizes(int* out) {
+  out[7] = AMAX_SHARDS;
   out[0] = sizeof(Node); out[1] = sizeof(Dec); out[2] = sizeof(Cand); out[3] = TILE; out[4] = FTILE;
   out[5] = HIST_LDS_BYTES + 64 * 8 + (2 * MUNR * 2 * NW + 132) * 4 + (int)sizeof(Dec);  // k_move LDS bytes
   out[6] = BLK;

@@ -137,7 +137,7 @@ class GBMTrainer(SharedTreeTrainer):
             # one HIP pass: previous tree's f update + sampling + residuals + leaf terms + scale maxima
             from ..ops import _native as nat
             if not hasattr(self, "_amax"):
-                self._amax = torch.zeros(2, dtype=torch.int32, device=self.dev)
+                self._amax = torch.zeros(2 * T.AMAX_SHARDS, dtype=torch.int32, device=self.dev)
                 self._wbuf = None if self.w is None or bool((self.w == 1).all()) else self.w.contiguous()
             self._amax.zero_()
             pv, pl = self._pending if getattr(self, "_pending", None) is not None else (None, None)

@@ -28,6 +28,7 @@ NBIN = 256
 NA_BIN = 255
 MAX_DATA_BINS = 255
 FTILE = 32
+AMAX_SHARDS = 64   # per-block |aux| maxima shards (csrc: AMAX_SHARDS)
 
 NODE_DT = np.dtype([("start", "<i4"), ("len", "<i4"), ("build", "<i4"), ("parent", "<i4"), ("sib", "<i4"),
                     ("p0", "<i4"), ("p1", "<i4"), ("p2", "<i4")])
@@ -365,6 +366,7 @@ class GpuTreeBuilder:
         sz = np.zeros(8, dtype=np.int32)
         self.lib.h2o_tree_sizes(sz.ctypes.data)
         assert sz[0] == NODE_DT.itemsize and sz[1] == DEC_DT.itemsize and sz[2] == CAND_BYTES, sz
+        assert sz[7] == AMAX_SHARDS, sz
         self.TILE = int(sz[3])
         dev = bins.device
         self.dev = dev
@@ -395,7 +397,7 @@ class GpuTreeBuilder:
         self.mono_f = None if mono_f is None else torch.as_tensor(np.asarray(mono_f, dtype=np.int32), device=dev)
         self.feat_ok_all = torch.ones(F, dtype=torch.int32, device=dev)
         self.qs = torch.empty(4, dtype=torch.float64, device=dev)   # fixed-point scales [sa, sb, 1/sa, 1/sb]
-        self.amax_bits = torch.zeros(2, dtype=torch.int32, device=dev)
+        self.amax_bits = torch.zeros(2 * AMAX_SHARDS, dtype=torch.int32, device=dev)
         # ping-pong row payload buffers
         self.bufs = [dict(bins=torch.empty(N, self.stride, dtype=torch.uint8, device=dev),
                           aux=torch.empty(N, 4, dtype=torch.float32, device=dev),
