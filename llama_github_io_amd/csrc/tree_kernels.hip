@@ -129,16 +129,38 @@ __device__ __forceinline__ long long q64(float v, float scale) {
   return (long long)(v * scale);   // |v*scale| <= 2^40: exact conversion of the fp32 product
 }
 
+// PACKED mode (row weights are small integers, e.g. 1 or a 0/1 sample mask): ONE ds_add_u64 per
+// (row, feature) instead of two — count in bits [48, 64), wY in the low 48 bits as signed fixed point
+// scaled to |q| <= 2^31 per row. A flush window holds < 2^15 rows (PACK_MAX), so the signed low
+// part never exceeds 2^46 and the count never carries out: decode with one arithmetic shift.
+#define PACK_SHIFT 48
+#define PACK_MAX 30720   // rows per LDS flush window in packed mode (15 tiles)
+__device__ __forceinline__ long long qpack(float w, float b, float scale_p) {
+  return ((long long)w << PACK_SHIFT) + (long long)(b * scale_p);
+}
+__device__ __forceinline__ void unpack(long long v, long long& cnt, long long& val) {
+  cnt = (v + (1ll << (PACK_SHIFT - 1))) >> PACK_SHIFT;
+  val = v - (cnt << PACK_SHIFT);
+}
+
 __device__ void flush_hist(const long long* h, const float* nayy, double node_wyy, int ftile, int F,
-                           double* __restrict__ slot, const double* __restrict__ qs) {
+                           double* __restrict__ slot, const double* __restrict__ qs, bool packed) {
   // slot layout: [F][256][2] doubles, then [F] NA-wYY, then [1] node wYY.
   const int f0 = ftile * FTILE;
   const int nf = min(FTILE, F - f0);
-  const double inv_a = qs[2], inv_b = qs[3];
+  const double inv_a = qs[2], inv_b = qs[3], inv_p = qs[5];
   for (int i = threadIdx.x; i < nf * 2 * NBIN; i += blockDim.x) {
     const int fl = i / (2 * NBIN), r = i - fl * 2 * NBIN;
-    const long long v = h[fl * HS64 + (r & 1) * 257 + (r >> 1)];
-    if (v != 0) atomicAdd(slot + (size_t)(f0 + fl) * 2 * NBIN + r, (double)v * ((r & 1) ? inv_b : inv_a));
+    double d;
+    if (packed) {
+      long long c, v;
+      unpack(h[fl * HS64 + (r >> 1)], c, v);
+      d = (r & 1) ? (double)v * inv_p : (double)c;
+    } else {
+      const long long v = h[fl * HS64 + (r & 1) * 257 + (r >> 1)];
+      d = (double)v * ((r & 1) ? inv_b : inv_a);
+    }
+    if (d != 0.0) atomicAdd(slot + (size_t)(f0 + fl) * 2 * NBIN + r, d);
   }
   for (int i = threadIdx.x; i < nf; i += blockDim.x) {
     const float v = nayy[i];
@@ -150,15 +172,15 @@ __device__ void flush_hist(const long long* h, const float* nayy, double node_wy
 
 // accumulate one row-word (4 bins) into the LDS tile histogram
 __device__ __forceinline__ void hist_word(long long* h, float* nayy, unsigned word, int wl /*word index in tile*/,
-                                          int f_abs0, int F, long long qa, long long qb, float yy) {
+                                          int f_abs0, int F, long long qa, long long qb, float yy, bool packed) {
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int fl = wl * 4 + k;
     if (f_abs0 + k < F) {
       const int bin = (word >> (8 * k)) & 0xFF;
       unsigned long long* p = (unsigned long long*)(h + fl * HS64 + bin);
-      atomicAdd(p, (unsigned long long)qa);
-      atomicAdd(p + 257, (unsigned long long)qb);
+      atomicAdd(p, (unsigned long long)qa);          // packed: qa = count<<48 | wY
+      if (!packed) atomicAdd(p + 257, (unsigned long long)qb);
       if (bin == NA_BIN) atomicAdd(nayy + fl, yy);
     }
   }
@@ -174,7 +196,8 @@ __device__ __forceinline__ float row_yy(float a, float b) {
 // Histogram rows [r0, r1) of one node into LDS. Loads for UNR rows are issued before any atomic.
 __device__ __forceinline__ void hist_rows(long long* h, float* nayy, const unsigned* __restrict__ bins32,
                                           const float4* __restrict__ aux, int W, int wabs, int F, bool lead,
-                                          int r0, int r1, int g, int j, float& wyy, float sa, float sb) {
+                                          int r0, int r1, int g, int j, float& wyy, float sa, float sb, float sp,
+                                          bool packed) {
   const float2* aux2 = (const float2*)aux;
   for (int base = r0; base < r1; base += RPI * UNR) {
     unsigned wd[UNR];
@@ -192,7 +215,10 @@ __device__ __forceinline__ void hist_rows(long long* h, float* nayy, const unsig
       if (row < r1) {
         const float yy = row_yy(ab[u].x, ab[u].y);
         if (lead) wyy += yy;
-        if (wabs < W) hist_word(h, nayy, wd[u], j, wabs * 4, F, q64(ab[u].x, sa), q64(ab[u].y, sb), yy);
+        if (wabs < W) {
+          const long long qa = packed ? qpack(ab[u].x, ab[u].y, sp) : q64(ab[u].x, sa);
+          hist_word(h, nayy, wd[u], j, wabs * 4, F, qa, q64(ab[u].y, sb), yy, packed);
+        }
       }
     }
   }
@@ -205,7 +231,8 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
     const uint8_t* __restrict__ bins, int stride /*bytes per row, multiple of 4*/,
     const float4* __restrict__ aux, const Node* __restrict__ nodes, const int* __restrict__ tile_prefix,
     const int* __restrict__ meta /*[0]=n_nodes [1]=n_tiles*/, int F, double* __restrict__ hist, int slot_doubles,
-    const double* __restrict__ qs /*[sa, sb, 1/sa, 1/sb]*/) {
+    const double* __restrict__ qs /*[sa, sb, 1/sa, 1/sb, sp, 1/sp]*/, int packed_i) {
+  const bool packed = packed_i != 0;
   extern __shared__ __attribute__((aligned(16))) long long smem64[];
   long long* h = smem64;                                 // FTILE * HS64
   float* nayy = (float*)(smem64 + FTILE * HS64);         // FTILE
@@ -221,39 +248,42 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
   const int g = threadIdx.x / LPR, j = threadIdx.x % LPR;
   const int wabs = ftile * LPR + j;        // absolute word index of this lane
   const unsigned* bins32 = (const unsigned*)bins;
-  const float sa = (float)qs[0], sb = (float)qs[1];
+  const float sa = (float)qs[0], sb = (float)qs[1], sp = (float)qs[4];
 
-  int cur = -1;
+  int cur = -1, since = 0;
   double wyy = 0.0;
   for (int t = t0; t < t1; ++t) {
     const int node = find_node(tile_prefix, n_nodes, t);
     const Node nd = nodes[node];
     if (!nd.build) continue;
-    if (node != cur) {
+    const int r0 = nd.start + (t - tile_prefix[node]) * TILE;
+    const int r1 = min(r0 + TILE, nd.start + nd.len);
+    // new node, or (packed) the flush window is full: flush the LDS tile and restart it
+    if (node != cur || (packed && since + (r1 - r0) > PACK_MAX)) {
       if (cur >= 0) {
         double v[4] = {wyy, 0, 0, 0};
         block_sum4(v, red);
         __syncthreads();
-        flush_hist(h, nayy, v[0], ftile, F, hist + (size_t)cur * slot_doubles, qs);
+        flush_hist(h, nayy, v[0], ftile, F, hist + (size_t)cur * slot_doubles, qs, packed);
         __syncthreads();
       }
       lds_zero64(h, FTILE * HS64);
       for (int i = threadIdx.x; i < FTILE; i += blockDim.x) nayy[i] = 0.f;
       wyy = 0.0;
+      since = 0;
       cur = node;
       __syncthreads();
     }
-    const int r0 = nd.start + (t - tile_prefix[node]) * TILE;
-    const int r1 = min(r0 + TILE, nd.start + nd.len);
+    since += r1 - r0;
     float wf = 0.f;
-    hist_rows(h, nayy, bins32, aux, W, wabs, F, j == 0 && ftile == 0, r0, r1, g, j, wf, sa, sb);
+    hist_rows(h, nayy, bins32, aux, W, wabs, F, j == 0 && ftile == 0, r0, r1, g, j, wf, sa, sb, sp, packed);
     wyy += (double)wf;
   }
   if (cur >= 0) {
     double v[4] = {wyy, 0, 0, 0};
     block_sum4(v, red);
     __syncthreads();
-    flush_hist(h, nayy, v[0], ftile, F, hist + (size_t)cur * slot_doubles, qs);
+    flush_hist(h, nayy, v[0], ftile, F, hist + (size_t)cur * slot_doubles, qs, packed);
   }
 }
 
@@ -725,14 +755,16 @@ __global__ __launch_bounds__(BLK, 4) void k_move(
     const int* __restrict__ meta, const Dec* __restrict__ dec, const int* __restrict__ tile_off,
     const int* __restrict__ node_nl, const int* __restrict__ child_l, const int* __restrict__ child_r,
     const Node* __restrict__ next, double* __restrict__ hist_next, int slot_doubles,
-    int* __restrict__ leaf_of_row, double* __restrict__ leafsum /*[L][2]*/, const double* __restrict__ qs) {
+    int* __restrict__ leaf_of_row, double* __restrict__ leafsum /*[L][2]*/, const double* __restrict__ qs,
+    int packed_i) {
+  const bool packed = packed_i != 0;
   extern __shared__ __attribute__((aligned(16))) long long smem64[];
   long long* h = smem64;
   float* nayy = (float*)(smem64 + FTILE * HS64);
   double* red = (double*)(nayy + FTILE);                      // 64 doubles
   int* cnt = (int*)(red + 64);                                // [2 parity][MUNR][2 side][NW waves] + 130 prefix
   Dec* sdec = (Dec*)(cnt + 2 * MUNR * 2 * NW + 132);          // current node's decision
-  const float sa = (float)qs[0], sb = (float)qs[1];
+  const float sa = (float)qs[0], sb = (float)qs[1], sp = (float)qs[4];
 
   const int n_nodes = meta[0], n_tiles = meta[1];
   if (n_nodes <= 0 || n_tiles <= 0) return;
@@ -750,7 +782,7 @@ __global__ __launch_bounds__(BLK, 4) void k_move(
   const float* sauxf = (const float*)saux;
   float* dauxf = (float*)daux;
 
-  int cur = -1, build_child = -1, leafL = -1, leafR = -1;
+  int cur = -1, build_child = -1, leafL = -1, leafR = -1, hsince = 0;
   double wyy = 0.0, sLn = 0.0, sLd = 0.0, sRn = 0.0, sRd = 0.0;
   int parity = 0;
 
@@ -765,7 +797,7 @@ __global__ __launch_bounds__(BLK, 4) void k_move(
       double u[4] = {wyy, 0, 0, 0};
       block_sum4(u, red);
       __syncthreads();
-      flush_hist(h, nayy, u[0], 0, F, hist_next + (size_t)build_child * slot_doubles, qs);
+      flush_hist(h, nayy, u[0], 0, F, hist_next + (size_t)build_child * slot_doubles, qs, packed);
     }
     __syncthreads();
   };
@@ -782,7 +814,7 @@ __global__ __launch_bounds__(BLK, 4) void k_move(
       build_child = -1;
       if (cl >= 0 && next[cl].build) build_child = cl;
       if (cr >= 0 && next[cr].build) build_child = cr;
-      sLn = sLd = sRn = sRd = 0.0; wyy = 0.0;
+      sLn = sLd = sRn = sRd = 0.0; wyy = 0.0; hsince = 0;
       if (HIST && build_child >= 0) {
         lds_zero64(h, FTILE * HS64);
         for (int i = threadIdx.x; i < FTILE; i += blockDim.x) nayy[i] = 0.f;
@@ -798,6 +830,21 @@ __global__ __launch_bounds__(BLK, 4) void k_move(
     const int tin = t - tile_prefix[node];
     const int r0 = nd.start + tin * TILE;
     const int r1 = min(r0 + TILE, nd.start + nd.len);
+    if (HIST && packed && build_child >= 0) {     // packed flush window full: flush + restart the tile
+      if (hsince + (r1 - r0) > PACK_MAX) {
+        double u[4] = {wyy, 0, 0, 0};
+        block_sum4(u, red);
+        __syncthreads();
+        flush_hist(h, nayy, u[0], 0, F, hist_next + (size_t)build_child * slot_doubles, qs, true);
+        __syncthreads();
+        lds_zero64(h, FTILE * HS64);
+        for (int i = threadIdx.x; i < FTILE; i += blockDim.x) nayy[i] = 0.f;
+        wyy = 0.0;
+        hsince = 0;
+        __syncthreads();
+      }
+      hsince += r1 - r0;
+    }
     int runL = tile_off[t];                         // left rows before this tile (within node)
     int runR = tin * TILE - tile_off[t];            // right rows before this tile
     float wyf = 0.f, lLn = 0.f, lLd = 0.f, lRn = 0.f, lRd = 0.f;
@@ -879,7 +926,8 @@ __global__ __launch_bounds__(BLK, 4) void k_move(
           if (HIST && child == build_child) {
             const float yy = row_yy(a_, b_);
             if (j == 0) wyf += yy;
-            if (j < W) hist_word(h, nayy, wd[u], j, j * 4, F, q64(a_, sa), q64(b_, sb), yy);
+            if (j < W) hist_word(h, nayy, wd[u], j, j * 4, F, packed ? qpack(a_, b_, sp) : q64(a_, sa), q64(b_, sb), yy,
+                                 packed);
           }
         } else if (j == 0) {
           // row stops here: leaf id in original order + Newton sums
@@ -991,6 +1039,11 @@ __global__ void k_qscale(const unsigned* __restrict__ amax_bits, double* __restr
     const double sc = (m > 0.0 && m == m) ? 1099511627776.0 / m : 1.0;   // 2^40 / max
     qs[threadIdx.x] = sc;
     qs[2 + threadIdx.x] = 1.0 / sc;
+    if (threadIdx.x == 1) {                                                // packed wY: 2^31 / max
+      const double sp = (m > 0.0 && m == m) ? 2147483648.0 / m : 1.0;
+      qs[4] = sp;
+      qs[5] = 1.0 / sp;
+    }
   }
 }
 
@@ -1007,12 +1060,13 @@ int h2o_tree_sizes(int* out) {
 }
 
 int h2o_hist_build(const void* bins, int stride, const void* aux, const void* nodes, const void* tile_prefix,
-                   const void* meta, int F, void* hist, int slot_doubles, const void* qs, int grid, hipStream_t s) {
+                   const void* meta, int F, void* hist, int slot_doubles, const void* qs, int grid, int packed,
+                   hipStream_t s) {
   const int nft = (F + FTILE - 1) / FTILE;
   const size_t lds = HIST_LDS_BYTES + 64 * 8;
   hipLaunchKernelGGL(k_hist_build, dim3(grid, nft), dim3(BLK), lds, s, (const uint8_t*)bins, stride,
                      (const float4*)aux, (const Node*)nodes, (const int*)tile_prefix, (const int*)meta, F,
-                     (double*)hist, slot_doubles, (const double*)qs);
+                     (double*)hist, slot_doubles, (const double*)qs, packed);
   return (int)hipGetLastError();
 }
 
@@ -1073,20 +1127,22 @@ int h2o_move(const void* sbins, const void* saux, const void* sridx, void* dbins
              int stride, int F, const void* nodes, const void* tile_prefix, const void* meta, const void* dec,
              const void* tile_off, const void* node_nl, const void* child_l, const void* child_r, const void* next,
              void* hist_next, int slot_doubles, void* leaf_of_row, void* leafsum, const void* qs, int fuse_hist,
-             int grid, hipStream_t s) {
+             int grid, int packed, hipStream_t s) {
   const size_t lds_h = HIST_LDS_BYTES + 64 * 8 + (2 * MUNR * 2 * NW + 132) * 4 + sizeof(Dec);
   if (fuse_hist) {
     hipLaunchKernelGGL(k_move<true>, dim3(grid), dim3(BLK), lds_h, s, (const uint8_t*)sbins, (const float4*)saux,
                        (const int*)sridx, (uint8_t*)dbins, (float4*)daux, (int*)dridx, stride, F, (const Node*)nodes,
                        (const int*)tile_prefix, (const int*)meta, (const Dec*)dec, (const int*)tile_off,
                        (const int*)node_nl, (const int*)child_l, (const int*)child_r, (const Node*)next,
-                       (double*)hist_next, slot_doubles, (int*)leaf_of_row, (double*)leafsum, (const double*)qs);
+                       (double*)hist_next, slot_doubles, (int*)leaf_of_row, (double*)leafsum, (const double*)qs,
+                       packed);
   } else {
     hipLaunchKernelGGL(k_move<false>, dim3(grid), dim3(BLK), lds_h, s, (const uint8_t*)sbins, (const float4*)saux,
                        (const int*)sridx, (uint8_t*)dbins, (float4*)daux, (int*)dridx, stride, F, (const Node*)nodes,
                        (const int*)tile_prefix, (const int*)meta, (const Dec*)dec, (const int*)tile_off,
                        (const int*)node_nl, (const int*)child_l, (const int*)child_r, (const Node*)next,
-                       (double*)hist_next, slot_doubles, (int*)leaf_of_row, (double*)leafsum, (const double*)qs);
+                       (double*)hist_next, slot_doubles, (int*)leaf_of_row, (double*)leafsum, (const double*)qs,
+                       packed);
   }
   return (int)hipGetLastError();
 }

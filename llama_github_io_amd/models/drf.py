@@ -72,6 +72,9 @@ class DRFTrainer(SharedTreeTrainer):
     def _trees_per_iter(self):
         return self.K
 
+    def _hist_packed(self):
+        return self.p.get("weights_column") is None and bool(((self.w == 0) | (self.w == 1)).all())
+
     def _k_cols(self, F):
         m = int(self.p.get("mtries", -1))
         if m == -2:

@@ -173,6 +173,10 @@ class GBMTrainer(SharedTreeTrainer):
     def _amax_for_build(self):
         return self._amax if self._fused() else None
 
+    def _hist_packed(self):
+        # fused path with no user weights: aux.x = 1 or a 0/1 sample mask
+        return self._fused() and getattr(self, "_wbuf", None) is None and self.p.get("weights_column") is None
+
     def _flush_pending(self):
         pend = getattr(self, "_pending", None)
         if pend is not None:

@@ -173,6 +173,8 @@ class SharedTreeTrainer:
                 am = self._amax_for_build()
                 if am is not None:
                     kw["amax_bits"] = am
+                if self.dev.type == "cuda":
+                    kw["packed"] = self._hist_packed()
                 h = self.builder.build(aux, feat_ok, self._k_cols(F), seed=(self.seed * 1000003 + t * 97 + k) & ((1 << 63) - 1),
                                        leaf_fn=lambda ls, t=t, k=k: self._leaf_values(ls, t, k), **kw)
                 self._update(t, k)
@@ -260,6 +262,10 @@ class SharedTreeTrainer:
     # defaults, overridden
     def _amax_for_build(self):
         return None
+
+    def _hist_packed(self) -> bool:
+        """True when every histogram row weight (aux.x) is a 0/1 (or small integer) count."""
+        return False
 
     def _init_model(self, model):
         pass

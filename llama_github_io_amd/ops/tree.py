@@ -396,7 +396,7 @@ class GpuTreeBuilder:
         self.iscat_f = torch.as_tensor(np.asarray(iscat_f, dtype=np.int32), device=dev)
         self.mono_f = None if mono_f is None else torch.as_tensor(np.asarray(mono_f, dtype=np.int32), device=dev)
         self.feat_ok_all = torch.ones(F, dtype=torch.int32, device=dev)
-        self.qs = torch.empty(4, dtype=torch.float64, device=dev)   # fixed-point scales [sa, sb, 1/sa, 1/sb]
+        self.qs = torch.empty(8, dtype=torch.float64, device=dev)   # fixed-point scales [sa, sb, 1/sa, 1/sb, sp, 1/sp]
         self.amax_bits = torch.zeros(2 * AMAX_SHARDS, dtype=torch.int32, device=dev)
         # ping-pong row payload buffers
         self.bufs = [dict(bins=torch.empty(N, self.stride, dtype=torch.uint8, device=dev),
@@ -432,11 +432,13 @@ class GpuTreeBuilder:
         return self.av[name].data_ptr()
 
     def build(self, aux_static: torch.Tensor, feat_ok: torch.Tensor | None = None, k_cols: int = 0, seed: int = 0,
-              leaf_fn=None, amax_bits: torch.Tensor | None = None):
+              leaf_fn=None, amax_bits: torch.Tensor | None = None, packed: bool = False):
         """Launch one tree. ``leaf_fn(leafsum[L,2] f64) -> leaf values f32`` runs on device before the
         arena snapshot, so values travel to the host with the structure (no extra sync).
-        ``amax_bits`` (int32[2], max |aux.x|, |aux.y| as float bits) may be produced by a fused prepare
-        kernel; otherwise it is computed here."""
+        ``amax_bits`` (int32[2*AMAX_SHARDS], max |aux.x|, |aux.y| as float bits) may be produced by a fused
+        prepare kernel; otherwise it is computed here. ``packed`` (caller guarantees aux.x is a 0/1 or small
+        integer row weight) switches the LDS histograms to one packed count|wY atomic per (row, feature)."""
+        pk = int(bool(packed))
         lib, s = self.lib, nat.stream_ptr(self.dev)
         F, D, p, T = self.F, self.D, self.p, self.TILE
         assert aux_static.shape == (self.N, 4) and aux_static.dtype == torch.float32 and aux_static.is_contiguous()
@@ -454,8 +456,10 @@ class GpuTreeBuilder:
         qs = self.qs.data_ptr()
         g0 = min(self.tiles_cap[0], self.grid)
         nat.check(lib.h2o_hist_build(self.master.data_ptr(), self.stride, aux_static.data_ptr(), self._p("nodes0"),
-                                     self._p("tp0"), self._p("meta0"), F, self.hist[0].data_ptr(), slot, qs, g0, s), "hist_build")
+                                     self._p("tp0"), self._p("meta0"), F, self.hist[0].data_ptr(), slot, qs, g0, pk, s),
+                  "hist_build")
         coll.all_reduce_(self.hist[0][:slot])
+        self.root_w = self.hist[0][0:2 * NBIN:2].sum().reshape(1)   # Σw over feature 0's bins = root weight
         mono = 0 if self.mono_f is None else self.mono_f.data_ptr()
         seed = int(seed) & _M64
         for d in range(D):
@@ -491,11 +495,12 @@ class GpuTreeBuilder:
                                    self.stride, F, self._p(f"nodes{d}"), self._p(f"tp{d}"), self._p(f"meta{d}"),
                                    self._p(f"dec{d}"), self.tile_off.data_ptr(), self._p(f"nl{d}"), self._p(f"cl{d}"),
                                    self._p(f"cr{d}"), self._p(f"nodes{d + 1}"), hn.data_ptr(), slot,
-                                   self.leaf_of_row.data_ptr(), self.leafsum.data_ptr(), qs, int(fuse), g, s), "move")
+                                   self.leaf_of_row.data_ptr(), self.leafsum.data_ptr(), qs, int(fuse), g, pk, s), "move")
             if not last and F > FTILE:
                 nat.check(lib.h2o_hist_build(dst["bins"].data_ptr(), self.stride, dst["aux"].data_ptr(),
                                              self._p(f"nodes{d + 1}"), self._p(f"tp{d + 1}"), self._p(f"meta{d + 1}"),
-                                             F, hn.data_ptr(), slot, qs, min(self.tiles_cap[d + 1], self.grid), s), "hist_build")
+                                             F, hn.data_ptr(), slot, qs, min(self.tiles_cap[d + 1], self.grid), pk, s),
+                          "hist_build")
             if not last:
                 coll.all_reduce_(hn[: self.caps[d + 1] * slot])
                 nat.check(lib.h2o_subtract(hn.data_ptr(), hc.data_ptr(), self._p(f"nodes{d + 1}"),
@@ -505,7 +510,7 @@ class GpuTreeBuilder:
             vals = leaf_fn(self.leafsum)
             self.av["leafval"].view(torch.float32)[: vals.numel()].copy_(vals.to(torch.float32))
         snap = self.arena.clone()
-        rw = coll.all_reduce_(aux_static[:, 0].sum(dtype=torch.float64).reshape(1))
+        rw = self.root_w.clone()
         self.history.append((snap, rw))
         return len(self.history) - 1
 

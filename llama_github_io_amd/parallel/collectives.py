@@ -18,9 +18,19 @@ def rank() -> int:
     return dist.get_rank() if is_dist() else 0
 
 
+def _staged(t: torch.Tensor) -> bool:
+    """gloo cannot run every collective on device tensors: stage those through host memory."""
+    return t.is_cuda and dist.get_backend() != "nccl"
+
+
 def all_reduce_(t: torch.Tensor, op=None) -> torch.Tensor:
     if is_dist():
-        dist.all_reduce(t, op=op or dist.ReduceOp.SUM)
+        if _staged(t):
+            h = t.detach().cpu()
+            dist.all_reduce(h, op=op or dist.ReduceOp.SUM)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, op=op or dist.ReduceOp.SUM)
     return t
 
 
@@ -46,6 +56,8 @@ def all_reduce_scalar(x: float, device=None) -> float:
 def all_gather_cat(t: torch.Tensor, dim: int = 0) -> torch.Tensor:
     if not is_dist():
         return t
+    if _staged(t):
+        return all_gather_cat(t.cpu(), dim).to(t.device)
     n = torch.tensor([t.shape[dim]], device=t.device)
     sizes = [torch.zeros_like(n) for _ in range(world())]
     dist.all_gather(sizes, n)
@@ -60,7 +72,12 @@ def all_gather_cat(t: torch.Tensor, dim: int = 0) -> torch.Tensor:
 
 def broadcast_(t: torch.Tensor, src: int = 0) -> torch.Tensor:
     if is_dist():
-        dist.broadcast(t, src)
+        if _staged(t):
+            h = t.detach().cpu()
+            dist.broadcast(h, src)
+            t.copy_(h)
+        else:
+            dist.broadcast(t, src)
     return t
 
 

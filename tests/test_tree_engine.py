@@ -126,3 +126,31 @@ def test_gpu_many_features_path():
     mc = GBMTrainer(dict(ntrees=10, max_depth=4, seed=1)).fit(X, y, None, None, info)
     assert abs(m.output["training_metrics"]["AUC"] - mc.output["training_metrics"]["AUC"]) < 2e-3
     assert m.output["training_metrics"]["AUC"] > 0.9
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("grid", [4, 256])
+def test_gpu_packed_histograms_match_unpacked(grid):
+    # packed (count<<48 | wY) single-atomic LDS histograms == two-atomic int64 histograms; grid=4 makes every
+    # block stream > PACK_MAX rows so the packed flush window is exercised
+    X, y, info = _data(N=200000, cat=True, seed=9)
+    b = fit_binning(X, info.iscat, info.nlevels, max_bins=255)
+    dev = torch.device("cuda", 0)
+    bins = apply_binning(b, X.to(dev))
+    g = torch.Generator().manual_seed(1)
+    w = (torch.rand(X.shape[1], generator=g) < 0.7).float()
+    z = torch.randn(X.shape[1], generator=g) + y
+    aux = torch.stack([w, w * z, w * z, w], 1).contiguous().to(dev)
+    p = T.SplitParams(min_w=10)
+    out = []
+    for packed in (False, True):
+        gb = T.GpuTreeBuilder(bins, X.shape[0], b.nbins, b.iscat, None, 6, p, grid=grid)
+        h = gb.build(aux, leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1].clamp(min=1)).float(), packed=packed)
+        out.append((gb.fetch(h), gb.leaf_of_row.clone()))
+    (ta, la), (tb, lb) = out
+    assert ta.n_leaves == tb.n_leaves
+    for da, db in zip(ta.decs, tb.decs):
+        assert np.array_equal(da["feat"], db["feat"]) and np.array_equal(da["bin"], db["bin"])
+        np.testing.assert_allclose(da["wl"], db["wl"], rtol=0, atol=1e-9)     # counts are exact in both modes
+    np.testing.assert_allclose(ta.leaf_values, tb.leaf_values, rtol=1e-5, atol=1e-6)
+    assert torch.equal(la, lb)
