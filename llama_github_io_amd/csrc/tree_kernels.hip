@@ -188,6 +188,8 @@ __device__ __forceinline__ void hist_word(long long* h, float* nayy, unsigned wo
 
 #define UNR 8   // hist: rows per lane-group in flight (memory-level parallelism: 8 independent loads per lane)
 #define MUNR 4  // k_move: rows per lane-group per partition step (MUNR*8 <= 64 for the wave-0 scan)
+// (measured: a 512-thread / MUNR=8 k_move without register spills ran 1.6x SLOWER than this 16-wave
+//  one that spills 11 VGPRs: occupancy, not spills, hides this kernel's memory latency)
 
 __device__ __forceinline__ float row_yy(float a, float b) {
   return a > 0.f ? b * b * __builtin_amdgcn_rcpf(a) : 0.f;
@@ -755,16 +757,16 @@ __global__ __launch_bounds__(BLK, 4) void k_move(
     const int* __restrict__ meta, const Dec* __restrict__ dec, const int* __restrict__ tile_off,
     const int* __restrict__ node_nl, const int* __restrict__ child_l, const int* __restrict__ child_r,
     const Node* __restrict__ next, double* __restrict__ hist_next, int slot_doubles,
-    int* __restrict__ leaf_of_row, double* __restrict__ leafsum /*[L][2]*/, const double* __restrict__ qs,
-    int packed_i) {
-  const bool packed = packed_i != 0;
+    int* __restrict__ leaf_of_row, double* __restrict__ leafsum /*[L][2]*/, const double* __restrict__ qs) {
+  // NOTE: the packed single-atomic histogram mode is NOT used here: measured on MI355X it made this
+  // (register-capped, 16-wave) kernel slower (590 -> 660 us/level) while it speeds up k_hist_build.
   extern __shared__ __attribute__((aligned(16))) long long smem64[];
   long long* h = smem64;
   float* nayy = (float*)(smem64 + FTILE * HS64);
   double* red = (double*)(nayy + FTILE);                      // 64 doubles
   int* cnt = (int*)(red + 64);                                // [2 parity][MUNR][2 side][NW waves] + 130 prefix
   Dec* sdec = (Dec*)(cnt + 2 * MUNR * 2 * NW + 132);          // current node's decision
-  const float sa = (float)qs[0], sb = (float)qs[1], sp = (float)qs[4];
+  const float sa = (float)qs[0], sb = (float)qs[1];
 
   const int n_nodes = meta[0], n_tiles = meta[1];
   if (n_nodes <= 0 || n_tiles <= 0) return;
@@ -782,7 +784,7 @@ __global__ __launch_bounds__(BLK, 4) void k_move(
   const float* sauxf = (const float*)saux;
   float* dauxf = (float*)daux;
 
-  int cur = -1, build_child = -1, leafL = -1, leafR = -1, hsince = 0;
+  int cur = -1, build_child = -1, leafL = -1, leafR = -1;
   double wyy = 0.0, sLn = 0.0, sLd = 0.0, sRn = 0.0, sRd = 0.0;
   int parity = 0;
 
@@ -797,7 +799,7 @@ __global__ __launch_bounds__(BLK, 4) void k_move(
       double u[4] = {wyy, 0, 0, 0};
       block_sum4(u, red);
       __syncthreads();
-      flush_hist(h, nayy, u[0], 0, F, hist_next + (size_t)build_child * slot_doubles, qs, packed);
+      flush_hist(h, nayy, u[0], 0, F, hist_next + (size_t)build_child * slot_doubles, qs, false);
     }
     __syncthreads();
   };
@@ -814,7 +816,7 @@ __global__ __launch_bounds__(BLK, 4) void k_move(
       build_child = -1;
       if (cl >= 0 && next[cl].build) build_child = cl;
       if (cr >= 0 && next[cr].build) build_child = cr;
-      sLn = sLd = sRn = sRd = 0.0; wyy = 0.0; hsince = 0;
+      sLn = sLd = sRn = sRd = 0.0; wyy = 0.0;
       if (HIST && build_child >= 0) {
         lds_zero64(h, FTILE * HS64);
         for (int i = threadIdx.x; i < FTILE; i += blockDim.x) nayy[i] = 0.f;
@@ -830,21 +832,6 @@ __global__ __launch_bounds__(BLK, 4) void k_move(
     const int tin = t - tile_prefix[node];
     const int r0 = nd.start + tin * TILE;
     const int r1 = min(r0 + TILE, nd.start + nd.len);
-    if (HIST && packed && build_child >= 0) {     // packed flush window full: flush + restart the tile
-      if (hsince + (r1 - r0) > PACK_MAX) {
-        double u[4] = {wyy, 0, 0, 0};
-        block_sum4(u, red);
-        __syncthreads();
-        flush_hist(h, nayy, u[0], 0, F, hist_next + (size_t)build_child * slot_doubles, qs, true);
-        __syncthreads();
-        lds_zero64(h, FTILE * HS64);
-        for (int i = threadIdx.x; i < FTILE; i += blockDim.x) nayy[i] = 0.f;
-        wyy = 0.0;
-        hsince = 0;
-        __syncthreads();
-      }
-      hsince += r1 - r0;
-    }
     int runL = tile_off[t];                         // left rows before this tile (within node)
     int runR = tin * TILE - tile_off[t];            // right rows before this tile
     float wyf = 0.f, lLn = 0.f, lLd = 0.f, lRn = 0.f, lRd = 0.f;
@@ -926,8 +913,7 @@ __global__ __launch_bounds__(BLK, 4) void k_move(
           if (HIST && child == build_child) {
             const float yy = row_yy(a_, b_);
             if (j == 0) wyf += yy;
-            if (j < W) hist_word(h, nayy, wd[u], j, j * 4, F, packed ? qpack(a_, b_, sp) : q64(a_, sa), q64(b_, sb), yy,
-                                 packed);
+            if (j < W) hist_word(h, nayy, wd[u], j, j * 4, F, q64(a_, sa), q64(b_, sb), yy, false);
           }
         } else if (j == 0) {
           // row stops here: leaf id in original order + Newton sums
@@ -1128,21 +1114,20 @@ int h2o_move(const void* sbins, const void* saux, const void* sridx, void* dbins
              const void* tile_off, const void* node_nl, const void* child_l, const void* child_r, const void* next,
              void* hist_next, int slot_doubles, void* leaf_of_row, void* leafsum, const void* qs, int fuse_hist,
              int grid, int packed, hipStream_t s) {
+  (void)packed;  // k_move keeps the two-atomic histogram (see the note in k_move)
   const size_t lds_h = HIST_LDS_BYTES + 64 * 8 + (2 * MUNR * 2 * NW + 132) * 4 + sizeof(Dec);
   if (fuse_hist) {
     hipLaunchKernelGGL(k_move<true>, dim3(grid), dim3(BLK), lds_h, s, (const uint8_t*)sbins, (const float4*)saux,
                        (const int*)sridx, (uint8_t*)dbins, (float4*)daux, (int*)dridx, stride, F, (const Node*)nodes,
                        (const int*)tile_prefix, (const int*)meta, (const Dec*)dec, (const int*)tile_off,
                        (const int*)node_nl, (const int*)child_l, (const int*)child_r, (const Node*)next,
-                       (double*)hist_next, slot_doubles, (int*)leaf_of_row, (double*)leafsum, (const double*)qs,
-                       packed);
+                       (double*)hist_next, slot_doubles, (int*)leaf_of_row, (double*)leafsum, (const double*)qs);
   } else {
     hipLaunchKernelGGL(k_move<false>, dim3(grid), dim3(BLK), lds_h, s, (const uint8_t*)sbins, (const float4*)saux,
                        (const int*)sridx, (uint8_t*)dbins, (float4*)daux, (int*)dridx, stride, F, (const Node*)nodes,
                        (const int*)tile_prefix, (const int*)meta, (const Dec*)dec, (const int*)tile_off,
                        (const int*)node_nl, (const int*)child_l, (const int*)child_r, (const Node*)next,
-                       (double*)hist_next, slot_doubles, (int*)leaf_of_row, (double*)leafsum, (const double*)qs,
-                       packed);
+                       (double*)hist_next, slot_doubles, (int*)leaf_of_row, (double*)leafsum, (const double*)qs);
   }
   return (int)hipGetLastError();
 }
