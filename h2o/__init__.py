@@ -268,6 +268,12 @@ def flow():
     raise NotImplementedError("the Flow web UI is not shipped; use the REST API (python -m llama_github_io_amd.api.server)")
 
 
+def explain(models, frame, columns=None, top_n_features=5, **kw):
+    from llama_github_io_amd import explain as _ex
+    m = models[0] if isinstance(models, (list, tuple)) else models
+    return _ex.explain(getattr(m, "_model", m), frame, columns, top_n_features)
+
+
 def cluster_status():
     return _rt.cluster_status()
 

@@ -186,6 +186,28 @@ class Model:
     def scoring_history(self):
         return self.output.get("scoring_history")
 
+    # ---- explanation (explain.py)
+    def predict_contributions(self, test_data, output_format="Original", top_n=None, bottom_n=None, compare_abs=False):
+        from .. import explain
+        return explain.predict_contributions(self, test_data, output_format, top_n, bottom_n, compare_abs)
+
+    def partial_plot(self, data, cols=None, nbins=20, plot=False, targets=None, include_na=False, user_splits=None,
+                     **kw):
+        from .. import explain
+        return explain.partial_plot(self, data, cols, nbins, targets, include_na, user_splits)
+
+    def h(self, frame, variables):
+        from .. import explain
+        return explain.h(self, frame, variables)
+
+    def feature_interaction(self, max_interaction_depth=100, max_tree_depth=100, max_deepening=-1):
+        from .. import explain
+        return explain.feature_interaction(self, max_interaction_depth, max_tree_depth, max_deepening)
+
+    def explain(self, frame, **kw):
+        from .. import explain
+        return explain.explain(self, frame, **kw)
+
     def _m(self, name, train, valid, xval):
         src = "validation_metrics" if valid else ("cross_validation_metrics" if xval else "training_metrics")
         m = self.output.get(src) or {}
