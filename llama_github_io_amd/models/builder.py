@@ -195,6 +195,9 @@ def train(algo: str, params: dict, x=None, y=None, training_frame=None, validati
     model.output["run_time_ms"] = int((time.time() - t0) * 1000)
     model.algo = algo
     dkv.put(model.key, model)
+    if p.get("export_checkpoints_dir"):          # ModelBuilder export_checkpoints_dir: persist every final model
+        from ..persist import save_model
+        save_model(model, p["export_checkpoints_dir"], force=True)
     return model
 
 

@@ -208,6 +208,19 @@ class DeepLearningTrainer:
             dist = "gaussian" if cat == "Regression" else ("bernoulli" if cat == "Binomial" else "multinomial")
         net = MLP(Z.shape[1], hidden, n_out, "rectifier" if maxout else base, maxout, float(p["input_dropout_ratio"]),
                   [float(v) for v in hd], str(p["initial_weight_distribution"]), float(p["initial_weight_scale"]), gen).to(dev)
+        prev_epochs = 0.0
+        ck = p.get("checkpoint")
+        if ck:   # continue from a previous model (DeepLearning.java checkpoint): same architecture, more epochs
+            from ..core import dkv
+            prev = dkv.get(ck) if isinstance(ck, str) else getattr(ck, "_model", ck)
+            if prev is None or getattr(prev, "net", None) is None:
+                raise ValueError(f"checkpoint {ck} is not a DeepLearning model")
+            if prev._cfg["hidden"] != hidden or prev._cfg["n_in"] != Z.shape[1]:
+                raise ValueError("checkpoint architecture (hidden / inputs) differs")
+            net.load_state_dict({k: v.to(dev) for k, v in prev.net.state_dict().items()})
+            prev_epochs = float(prev.output.get("epochs", 0.0))
+            if float(p["epochs"]) <= prev_epochs:
+                raise ValueError(f"epochs must exceed the checkpoint's {prev_epochs}")
         if coll.is_dist():
             flat = torch.cat([q.detach().reshape(-1) for q in net.parameters()])
             coll.broadcast_(flat)
@@ -250,7 +263,7 @@ class DeepLearningTrainer:
         max_w2 = float(p["max_w2"])
         keeper = ScoreKeeper(p["stopping_rounds"], p["stopping_metric"], p["stopping_tolerance"],
                              "Regression" if ae else cat)
-        epochs = float(p["epochs"])
+        epochs = float(p["epochs"]) - prev_epochs
         total = int(math.ceil(epochs * N / B))
         g = torch.Generator(device="cpu").manual_seed(seed & 0x7FFFFFFF)
         history = []
@@ -326,7 +339,7 @@ class DeepLearningTrainer:
                 if float(p["max_runtime_secs"] or 0) > 0 and time.time() - t0 > float(p["max_runtime_secs"]):
                     break
         model.output["scoring_history"] = history
-        model.output["epochs"] = samples / N
+        model.output["epochs"] = prev_epochs + samples / N
         if ae:
             model.output["training_metrics"] = self._ae_metrics(model, X)
         else:

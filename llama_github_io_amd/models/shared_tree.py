@@ -161,11 +161,12 @@ class SharedTreeTrainer:
         rng = np.random.default_rng(self.seed & 0xFFFFFFFF)
         handles = []
         gains = np.zeros(F, dtype=np.float64)
+        start = self._apply_checkpoint(model, forest, gains)
         history = []
         max_rt = float(p.get("max_runtime_secs") or 0)
         self.valid = valid
-        built = 0
-        for t in range(ntrees):
+        built = start
+        for t in range(start, ntrees):
             feat_ok = self._tree_feature_mask(rng, F)
             for k in range(K):
                 aux = self._prepare(t, k)
@@ -189,6 +190,11 @@ class SharedTreeTrainer:
                     mref = ev.get("_valid") or ev.get("_train")
                     if mref is not None and keeper.add(mref):
                         break
+            ck_dir = p.get("in_training_checkpoints_dir")
+            if ck_dir and built % max(1, int(p.get("in_training_checkpoints_tree_interval") or 1)) == 0:
+                self._drain(handles, forest, gains)       # snapshot of the model so far, resumable via checkpoint=
+                handles = []
+                self._save_in_training(model, built, ck_dir)
             if max_rt > 0 and time.time() - t_start > max_rt:
                 break
         self._drain(handles, forest, gains)
@@ -258,6 +264,49 @@ class SharedTreeTrainer:
                 if vm is not None and k in vm:
                     ev["validation_" + k.lower()] = vm[k]
         return ev
+
+    # ---- checkpoint / resume (hex/tree/SharedTree.java checkpoint handling)
+    def _apply_checkpoint(self, model, forest, gains) -> int:
+        """Continue from ``checkpoint`` (model or key): copy its trees, restore the training margin, return
+        the number of iterations already built. ntrees must exceed the checkpoint's."""
+        ck = self.p.get("checkpoint")
+        if not ck:
+            return 0
+        from ..core import dkv
+        prev = dkv.get(ck) if isinstance(ck, str) else getattr(ck, "_model", ck)
+        if prev is None or getattr(prev, "forest", None) is None:
+            raise ValueError(f"checkpoint {ck} is not a tree model of this kind")
+        if prev.info.x != self.info.x:
+            raise ValueError("checkpoint model was trained on different predictors")
+        K = self._trees_per_iter()
+        for t, c in zip(prev.forest.trees, prev.forest.tree_class):
+            forest.add(t, c)
+            m = t.feat >= 0
+            np.add.at(gains, t.feat[m], np.maximum(t.gain[m], 0.0))
+        done = len(prev.forest.trees) // max(K, 1)
+        if done >= int(self.p["ntrees"]):
+            raise ValueError(f"ntrees ({self.p['ntrees']}) must be larger than the checkpoint's ({done})")
+        self._restore_margin(model, prev)
+        return done
+
+    def _save_in_training(self, model, built, ck_dir):
+        import copy
+        from ..persist import save_model
+        snap = copy.copy(model)
+        snap.key = f"{model.key}.{built}"
+        snap.output = dict(model.output, ntrees=built)
+        self._finish_snapshot(snap)
+        save_model(snap, ck_dir, force=True)
+
+    def _finish_snapshot(self, snap):
+        pass
+
+    def _restore_margin(self, model, prev):
+        if hasattr(self, "f"):
+            raw = prev.forest.predict_raw(self.X)
+            model.init_f = prev.init_f
+            init = torch.as_tensor(prev.init_f, dtype=torch.float32, device=self.dev).reshape(1, -1)
+            self.f.copy_(raw + init + (self.offset[:, None] if self.offset is not None else 0))
 
     # defaults, overridden
     def _amax_for_build(self):
