@@ -170,7 +170,30 @@ def create_app():
 
     @app.get("/3/Timeline")
     def tl():
-        return dict(events=_timeline[-200:])
+        from ..utils import timeline
+        return _clean(dict(events=timeline.events(1000), http=_timeline[-200:]))
+
+    @app.get("/3/Logs")
+    @app.get("/3/Logs/nodes/{node}/files/{name}")
+    def logs(node: str = "self", name: str = "default"):
+        from ..utils import log
+        return dict(log="\n".join(log.recent(2000)))
+
+    @app.get("/3/Profiler")
+    def profiler(depth: int = 10):
+        from ..utils import timeline
+        return dict(nodes=[dict(node_name="self", profile=timeline.stacks())])
+
+    @app.get("/3/WaterMeterMemory")
+    @app.get("/3/MemoryStats")
+    def memstats():
+        from ..utils import memory
+        return _clean(memory.stats())
+
+    @app.post("/3/GarbageCollect")
+    def gc():
+        from ..utils import memory
+        return dict(spilled_bytes=memory.clean())
 
     @app.delete("/3/DKV")
     def dkv_clear():

@@ -31,7 +31,11 @@ def put(key: str, value) -> None:
 
 def get(key: str, default=None):
     with _lock:
-        return _store.get(key, default)
+        v = _store.get(key, default)
+    if v is not None and hasattr(v, "_cols"):
+        from ..utils import memory
+        memory.touch(key)
+    return v
 
 
 def __getitem__(key):  # pragma: no cover - module-level convenience

@@ -71,6 +71,8 @@ class Job:
     def check_cancelled(self) -> None:
         if self._cancel.is_set():
             raise JobCancelled(self.key)
+        from ..parallel import cluster
+        cluster.check()
 
     # ---- execution
     def _execute(self, fn, args, kwargs):

@@ -58,12 +58,19 @@ def init(name: str | None = None, distributed: bool | None = None, backend: str 
         else:
             dist.init_process_group(backend or "gloo")
         _state["dist_inited_here"] = True
+    if distributed:
+        from ..parallel import cluster
+        cluster.start(float(os.environ.get("H2O_HEARTBEAT_S", "1.0")), float(os.environ.get("H2O_HB_TIMEOUT_S", "30")))
     device()
+    from ..utils import log
+    log.configure(os.environ.get("H2O_LOG_LEVEL", "INFO"), os.environ.get("H2O_LOG_DIR"))
     return cluster_status()
 
 
 def shutdown() -> None:
     import torch.distributed as dist
+    from ..parallel import cluster
+    cluster.stop()
     if _state["dist_inited_here"] and dist.is_initialized():
         dist.destroy_process_group()
         _state["dist_inited_here"] = False
@@ -86,8 +93,11 @@ def cluster_status() -> dict:
                           num_cus=props.multi_processor_count, mem_total=total, free_mem=free, healthy=True))
     else:
         nodes.append(dict(h2o=socket.gethostname(), gpu=None, num_cpus=os.cpu_count(), healthy=True))
-    return dict(version=_version(), cloud_name=_state["name"], cloud_size=world, cloud_uptime_millis=
-                int((time.time() - (_state["started"] or time.time())) * 1000), cloud_healthy=True,
+    from ..parallel import cluster
+    from ..utils import memory
+    hb = cluster.status()
+    return dict(version=_version(), cloud_name=_state["name"], cloud_size=world, heartbeat=hb, memory=memory.stats(), cloud_uptime_millis=
+                int((time.time() - (_state["started"] or time.time())) * 1000), cloud_healthy=hb["healthy"],
                 consensus=True, locked=True, nodes=nodes, device=str(d),
                 backend=(dist.get_backend() if dist.is_initialized() else None))
 

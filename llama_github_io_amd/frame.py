@@ -35,14 +35,38 @@ def engine_device():
 
 # ================================================================================================
 class Column:
-    __slots__ = ("name", "type", "data", "domain", "strings")
+    __slots__ = ("name", "type", "_data", "domain", "strings", "_spilled")
 
     def __init__(self, name, type_, data=None, domain=None, strings=None):
         self.name = name
         self.type = type_
-        self.data = data
+        self._data = data
+        self._spilled = None
         self.domain = domain
         self.strings = strings
+
+    # device residency: a column spilled by the memory manager comes back on first access
+    @property
+    def data(self):
+        if self._spilled is not None:
+            from .utils import memory
+            memory.restore_column(self)
+        return self._data
+
+    @data.setter
+    def data(self, v):
+        self._data = v
+        self._spilled = None
+
+    def raw_data(self):
+        return self._data
+
+    def set_raw_data(self, v, spilled_from=None):
+        self._data = v
+        self._spilled = spilled_from
+
+    def spilled_device(self):
+        return self._spilled
 
     @property
     def n(self):

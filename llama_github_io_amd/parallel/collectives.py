@@ -25,6 +25,8 @@ def _staged(t: torch.Tensor) -> bool:
 
 def all_reduce_(t: torch.Tensor, op=None) -> torch.Tensor:
     if is_dist():
+        from ..utils import timeline
+        timeline.record("collective", "all_reduce", bytes=t.numel() * t.element_size())
         if _staged(t):
             h = t.detach().cpu()
             dist.all_reduce(h, op=op or dist.ReduceOp.SUM)

@@ -1,0 +1,92 @@
+"""Memory manager (reference: ``water/MemoryManager.java`` (allocation accounting, out-of-memory
+back-pressure) and ``water/Cleaner.java`` (swap cold values to disk)).
+
+On MI355X the working set lives in 288 GB of HBM. This module accounts device bytes per DKV frame,
+reports HBM usage (``/3/Cloud`` free_mem), and when usage crosses ``high_water`` (fraction of HBM) spills
+the least-recently-used frames' columns to pinned host memory; a spilled column transparently comes
+back to the device on its next access (``Column.data``). That is the Cleaner's swap, with host RAM
+as the backing store instead of ice files.
+"""
+from __future__ import annotations
+
+import threading
+import time
+
+import torch
+
+_lock = threading.RLock()
+_last_use: dict = {}
+_state = dict(high_water=0.90, spilled_bytes=0, spills=0, restores=0)
+
+
+def touch(frame_id: str):
+    _last_use[frame_id] = time.time()
+
+
+def frame_bytes(frame) -> int:
+    total = 0
+    for c in frame._cols.values():
+        d = c.raw_data()
+        if d is not None and d.is_cuda:
+            total += d.numel() * d.element_size()
+    return total
+
+
+def device_usage(device=None) -> dict:
+    if not torch.cuda.is_available():
+        return dict(total=0, free=0, used=0, allocated=0)
+    free, total = torch.cuda.mem_get_info(device)
+    return dict(total=total, free=free, used=total - free, allocated=torch.cuda.memory_allocated(device))
+
+
+def spill(frame) -> int:
+    """Move a frame's device columns to pinned host memory; returns bytes moved."""
+    moved = 0
+    with _lock:
+        for c in frame._cols.values():
+            d = c.raw_data()
+            if d is not None and d.is_cuda:
+                h = torch.empty(d.shape, dtype=d.dtype, pin_memory=True)
+                h.copy_(d)
+                c.set_raw_data(h, spilled_from=d.device)
+                moved += d.numel() * d.element_size()
+        _state["spilled_bytes"] += moved
+        _state["spills"] += 1 if moved else 0
+    return moved
+
+
+def restore_column(col):
+    """Called from ``Column.data`` when a spilled column is touched."""
+    with _lock:
+        d = col.raw_data()
+        dev = col.spilled_device()
+        if dev is not None and d is not None and not d.is_cuda:
+            col.set_raw_data(d.to(dev, non_blocking=True), spilled_from=None)
+            _state["restores"] += 1
+
+
+def clean(target_fraction: float | None = None) -> int:
+    """Spill LRU frames until device usage is under ``target_fraction`` of HBM."""
+    from ..core import dkv
+    from ..frame import H2OFrame
+    if not torch.cuda.is_available():
+        return 0
+    target = target_fraction if target_fraction is not None else _state["high_water"]
+    frames = [(k, v) for k, v in dkv.items() if isinstance(v, H2OFrame) and not dkv.locked(k)]
+    frames.sort(key=lambda kv: _last_use.get(kv[0], 0.0))
+    moved = 0
+    for k, fr in frames:
+        u = device_usage()
+        if u["total"] == 0 or u["used"] / u["total"] <= target:
+            break
+        moved += spill(fr)
+        torch.cuda.empty_cache()
+    return moved
+
+
+def set_high_water(frac: float):
+    _state["high_water"] = float(frac)
+
+
+def stats() -> dict:
+    return dict(_state, **device_usage())

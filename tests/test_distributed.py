@@ -86,3 +86,42 @@ def test_sharded_equals_single(algo):
     sharded = _run(algo)
     tol = 1e-4 if algo != "glm" else 1e-5
     assert np.allclose(single, sharded, atol=tol, rtol=1e-4), (single[:5], sharded[:5])
+
+
+def _hb_worker(rank, world, port, q):
+    import time as _t
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      H2O_AMD_DEVICE="cpu", H2O_HEARTBEAT_S="0.1", H2O_HB_TIMEOUT_S="1.0")
+    sys.path.insert(0, ROOT)
+    from llama_github_io_amd.core import runtime
+    from llama_github_io_amd.parallel import cluster
+    runtime.init()
+    _t.sleep(0.5)
+    ok_before = cluster.healthy()
+    if rank == 1:
+        cluster.stop()          # rank 1 goes silent (simulated node loss)
+        _t.sleep(3)
+        q.put(("r1", True))
+        return
+    _t.sleep(2.5)
+    q.put(("r0", (ok_before, cluster.healthy(), cluster.status()["dead"])))
+
+
+def test_heartbeat_failure_detection():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_hb_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(30)
+        if p.is_alive():
+            p.kill()
+    ok_before, ok_after, dead = res["r0"]
+    assert ok_before and not ok_after and dead == [1]
