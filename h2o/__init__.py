@@ -149,6 +149,12 @@ def insert_missing_values(frame, fraction=0.1, seed=None):
     return _fops.insert_missing_values(frame, fraction, seed)
 
 
+def dct(frame, dimensions, inverse=False, destination_frame=None):
+    """``hex/DCTTransformer``: DCT-II (inverse: DCT-III) of every row laid out as [width, height, depth]."""
+    from llama_github_io_amd.models.dct import dct as _dct
+    return _dct(frame, dimensions, inverse)
+
+
 def deep_copy(data, xid):
     cols = [c.copy() for c in data._cols.values()]
     return H2OFrame._from_columns(cols, xid)

@@ -236,8 +236,8 @@ class H2OFrame:
         if pd is not None and isinstance(obj, pd.DataFrame):
             names = [str(c) for c in obj.columns]
             cols = []
-            for n in names:
-                s = obj[n]
+            for n, orig in zip(names, obj.columns):
+                s = obj[orig]
                 ft = types.get(n) if isinstance(types, dict) else None
                 if str(s.dtype) == "category":
                     ft = ft or "enum"
@@ -640,13 +640,18 @@ class H2OFrame:
         return bool(torch.nan_to_num(self._num(), nan=1).ne(0).all())
 
     def quantile(self, prob=None, combine_method="interpolate", weights_column=None):
+        """Column quantiles (``hex/quantile/Quantile.java``): combine_method interpolate | average | low |
+        high, optional observation weights; computed on device by one sort per column."""
+        from .models.quantile import weighted_quantiles
         prob = prob or [0.001, 0.01, 0.1, 0.25, 0.333, 0.5, 0.667, 0.75, 0.9, 0.99, 0.999]
+        wcol = None
+        if weights_column is not None:
+            wcol = (weights_column if isinstance(weights_column, H2OFrame) else self[weights_column])._col(0).as_float()
         cols = [Column("Probs", "real", torch.tensor(prob, dtype=torch.float64, device=engine_device()))]
         for c in self._cols.values():
-            if c.type not in _NUMERIC:
+            if c.type not in _NUMERIC or (isinstance(weights_column, str) and c.name == weights_column):
                 continue
-            v = c.data[~torch.isnan(c.data)]
-            q = torch.quantile(v, torch.tensor(prob, dtype=torch.float64, device=v.device)) if v.numel() else torch.full((len(prob),), float("nan"), dtype=torch.float64)
+            q = weighted_quantiles(c.data, prob, combine_method, wcol)
             cols.append(Column(c.name + "Quantiles", "real", q.to(engine_device())))
         return H2OFrame._from_columns(cols)
 

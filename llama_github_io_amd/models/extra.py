@@ -26,6 +26,7 @@ _ALGOS = [
     ("upliftdrf", "uplift", "UpliftDRFTrainer", True, dict(classification_only=True)),
     ("dt", "dt", "DTTrainer", True, dict(classification_only=True)),
     ("infogram", "infogram", "InfogramTrainer", True, {}),
+    ("quantile", "quantile", "QuantileTrainer", False, {}),
 ]
 
 for name, mod, cls, sup, kw in _ALGOS:
