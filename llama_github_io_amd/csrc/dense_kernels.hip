@@ -85,9 +85,38 @@ __global__ __launch_bounds__(256) void k_bias_act_bwd(const float* __restrict__ 
   if (ty == 0 && c < cols && db) atomicAdd(&db[c], red[0][tx] + red[1][tx] + red[2][tx] + red[3][tx]);
 }
 
+// ADADELTA (Neurons.java: rho, epsilon) fused over the FLAT parameter buffer of the whole network:
+// one launch updates every weight and bias (the per-tensor torch version is ~36 launches per step).
+// L1/L2 apply to weights only: elements [0, n_decay) are the weight matrices, the rest biases.
+__global__ __launch_bounds__(256) void k_adadelta(float* __restrict__ p, const float* __restrict__ g,
+                                                  float* __restrict__ eg2, float* __restrict__ edx2, int64_t n,
+                                                  int64_t n_decay, float rho, float eps, float l1, float l2) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float pi = p[i];
+    float gi = g[i];
+    if (i < n_decay) gi += l2 * pi + (pi > 0.f ? l1 : (pi < 0.f ? -l1 : 0.f));
+    const float e = rho * eg2[i] + (1.f - rho) * gi * gi;
+    const float d = -sqrtf(edx2[i] + eps) / sqrtf(e + eps) * gi;
+    eg2[i] = e;
+    edx2[i] = rho * edx2[i] + (1.f - rho) * d * d;
+    p[i] = pi + d;
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+int h2o_adadelta(float* p, const float* g, float* eg2, float* edx2, long long n, long long n_decay, float rho, float eps,
+                 float l1, float l2, hipStream_t stream) {
+  long long grid = (n + 255) / 256;
+  if (grid > 4096) grid = 4096;
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL(k_adadelta, dim3((unsigned)grid), dim3(256), 0, stream, p, g, eg2, edx2, (int64_t)n,
+                     (int64_t)n_decay, rho, eps, l1, l2);
+  return (int)hipGetLastError();
+}
+
 
 int h2o_bias_act_fwd(const float* x, const float* b, float* y, long long rows, int cols, int act, float drop,
                      unsigned long long seed, hipStream_t stream) {

@@ -59,15 +59,21 @@ class Expander:
                 names.append(f"{nm}.missing(NA)")
             off += size
         self.num_off = off
-        Xn = X[self.nums].double() if self.nums else torch.zeros(0, N, dtype=torch.float64, device=dev)
-        ok = ~torch.isnan(Xn)
-        Xz = torch.where(ok, Xn, torch.zeros_like(Xn))
-        sw = (ok.double() * w).sum(1)
-        s1 = (Xz * w).sum(1)
-        s2 = (Xz * Xz * w).sum(1)
+        k = len(self.nums)
+        sw = torch.zeros(k, dtype=torch.float64, device=dev)
+        s1 = torch.zeros(k, dtype=torch.float64, device=dev)
+        s2 = torch.zeros(k, dtype=torch.float64, device=dev)
+        CH = 32   # feature chunks keep the fp64 temporaries small on wide frames (e.g. 784 x 10M)
+        for a in range(0, k, CH):
+            Xn = X[self.nums[a:a + CH]].double()
+            ok = ~torch.isnan(Xn)
+            Xz = torch.where(ok, Xn, torch.zeros_like(Xn))
+            sw[a:a + CH] = (ok.double() * w).sum(1)
+            s1[a:a + CH] = (Xz * w).sum(1)
+            s2[a:a + CH] = (Xz * Xz * w).sum(1)
+            del Xn, ok, Xz
         if reduce is not None:
             packed = reduce(torch.cat([sw, s1, s2]))
-            k = len(self.nums)
             sw, s1, s2 = packed[:k], packed[k:2 * k], packed[2 * k:]
         mu = s1 / sw.clamp(min=1e-300)
         var = (s2 - sw * mu * mu) / (sw - 1).clamp(min=1e-300)
@@ -106,15 +112,17 @@ class Expander:
             idx = (self.cat_offsets[i] + col.clamp(min=0))
             rows = torch.nonzero(valid, as_tuple=True)[0]
             Z[rows, idx[rows]] = 1
-        if self.nums:
-            Xn = X[self.nums].to(dtype=torch.float64)
-            mu = self.num_mean[:, None]
+        CH = 32
+        for a in range(0, len(self.nums), CH):
+            Xn = X[self.nums[a:a + CH]].to(dtype=torch.float64)
+            mu = self.num_mean[a:a + CH, None]
             Xn = torch.where(torch.isnan(Xn), mu.expand_as(Xn), Xn)
             if self.standardize:
-                Xn = (Xn - mu) / self.num_sd[:, None]
+                Xn = (Xn - mu) / self.num_sd[a:a + CH, None]
             elif self.center_only:
                 Xn = Xn - mu
-            Z[:, self.num_off:] = Xn.T.to(dtype)
+            Z[:, self.num_off + a:self.num_off + a + Xn.shape[0]] = Xn.T.to(dtype)
+            del Xn
         return Z
 
     def row_mask_complete(self, X: torch.Tensor) -> torch.Tensor:

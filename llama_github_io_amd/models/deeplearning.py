@@ -253,11 +253,11 @@ class DeepLearningTrainer:
         B = int(p["mini_batch_size"])
         if B <= 1:
             B = int(p["gpu_batch_size"])      # Hogwild single-row SGD -> GPU mini-batches
-        params = list(net.parameters())
+        from ..ops.dense import FlatParams
+        fp = FlatParams(net)                 # params/grads as views of two flat buffers
+        params = fp.params
         adaptive = bool(p["adaptive_rate"])
-        eg2 = [torch.zeros_like(q) for q in params]
-        edx2 = [torch.zeros_like(q) for q in params]
-        mom = [torch.zeros_like(q) for q in params]
+        mom = torch.zeros_like(fp.p)
         rho, eps = float(p["rho"]), float(p["epsilon"])
         l1, l2 = float(p["l1"]), float(p["l2"])
         max_w2 = float(p["max_w2"])
@@ -286,45 +286,36 @@ class DeepLearningTrainer:
             with torch.autocast(device_type=dev.type, dtype=dtype, enabled=dtype is not None):
                 out = net(xb, seed)
             out = out.float()
-            loss = self._loss(out, xb if ae else yt.index_select(0, idx), wb, cat, dist, ae) / max(float(wb.sum()), 1e-12)
-            for q in params:
-                q.grad = None
-            loss.backward()
-            grads = [q.grad for q in params]
-            if coll.is_dist():
-                flat = torch.cat([gg.reshape(-1) for gg in grads])
-                coll.all_reduce_(flat)
-                flat /= coll.world()
-                o = 0
-                for gg in grads:
-                    gg.copy_(flat[o:o + gg.numel()].view_as(gg))
-                    o += gg.numel()
+            loss = self._loss(out, xb if ae else yt.index_select(0, idx), wb, cat, dist, ae) / wb.sum().clamp(min=1e-12)
+            fp.zero_grad()
+            loss.backward()                  # accumulates into the flat gradient buffer
+            if coll.is_dist():               # data parallel: ONE all-reduce of every gradient per step
+                coll.all_reduce_(fp.g)
+                fp.g /= coll.world()
             with torch.no_grad():
                 samples += B * (coll.world() if coll.is_dist() else 1)
-                if not adaptive:
+                if adaptive:                 # ADADELTA (Neurons.java: rho, epsilon), one fused HIP launch
+                    fp.adadelta(rho, eps, l1, l2)
+                else:
                     rate = float(p["rate"]) / (1 + float(p["rate_annealing"]) * samples)
                     m = self._momentum(samples)
-                for i, (q, gg) in enumerate(zip(params, grads)):
+                    gg = fp.g.clone()
+                    nd = fp.n_decay
                     if l2 > 0 or l1 > 0:
-                        if q.dim() > 1:
-                            gg = gg + l2 * q + l1 * torch.sign(q)
-                    if adaptive:  # ADADELTA (Neurons.java: rho, epsilon)
-                        eg2[i].mul_(rho).addcmul_(gg, gg, value=1 - rho)
-                        dx = -torch.sqrt(edx2[i] + eps) / torch.sqrt(eg2[i] + eps) * gg
-                        edx2[i].mul_(rho).addcmul_(dx, dx, value=1 - rho)
-                        q.add_(dx)
-                    else:
-                        if m > 0:
-                            mom[i].mul_(m).add_(gg, alpha=-rate)
-                            if p["nesterov_accelerated_gradient"]:
-                                q.add_(mom[i], alpha=m).add_(gg, alpha=-rate)
-                            else:
-                                q.add_(mom[i])
+                        gg[:nd] += l2 * fp.p[:nd] + l1 * torch.sign(fp.p[:nd])
+                    if m > 0:
+                        mom.mul_(m).add_(gg, alpha=-rate)
+                        if p["nesterov_accelerated_gradient"]:
+                            fp.p.add_(mom, alpha=m).add_(gg, alpha=-rate)
                         else:
-                            q.add_(gg, alpha=-rate)
-                    if max_w2 < float("inf") and q.dim() > 1:
-                        n2 = (q * q).sum(1, keepdim=True)
-                        q.mul_(torch.where(n2 > max_w2, torch.sqrt(max_w2 / n2), torch.ones_like(n2)))
+                            fp.p.add_(mom)
+                    else:
+                        fp.p.add_(gg, alpha=-rate)
+                if max_w2 < float("inf"):
+                    for q in params:
+                        if q.dim() > 1:
+                            n2 = (q * q).sum(1, keepdim=True)
+                            q.mul_(torch.where(n2 > max_w2, torch.sqrt(max_w2 / n2), torch.ones_like(n2)))
             if self.job is not None and step % 50 == 0:
                 self.job.set_progress(step / max(total, 1))
             end = step == total - 1

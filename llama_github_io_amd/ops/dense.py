@@ -9,6 +9,7 @@ from __future__ import annotations
 import torch
 
 from . import _native as nat
+from ._native import call, stream_ptr
 
 ACT = {"linear": 0, "rectifier": 1, "relu": 1, "tanh": 2, "exprectifier": 3, "elu": 3}
 
@@ -18,7 +19,51 @@ nat.register_hip_signatures({
     "h2o_bias_act_bwd": [nat.c_void_p, nat.c_void_p, nat.c_void_p, nat.c_void_p, nat.c_ll, nat.c_int, nat.c_int,
                          nat.ctypes.c_float, nat.c_ull, nat.c_void_p],
     "h2o_kmeans_assign": [nat.c_void_p, nat.c_ll, nat.c_int, nat.c_void_p, nat.c_int, nat.c_void_p, nat.c_void_p, nat.c_void_p],
+    "h2o_adadelta": [nat.c_void_p, nat.c_void_p, nat.c_void_p, nat.c_void_p, nat.c_ll, nat.c_ll, nat.ctypes.c_float,
+                     nat.ctypes.c_float, nat.ctypes.c_float, nat.ctypes.c_float, nat.c_void_p],
 })
+
+
+class FlatParams:
+    """All parameters (weights first, then biases) and their gradients as views of two flat fp32
+    buffers: one fused optimizer launch per step and one flat all-reduce for data parallelism."""
+
+    def __init__(self, module: torch.nn.Module):
+        params = list(module.parameters())
+        ws = [q for q in params if q.dim() > 1]
+        bs = [q for q in params if q.dim() <= 1]
+        self.params = ws + bs
+        self.n_decay = sum(q.numel() for q in ws)
+        n = sum(q.numel() for q in self.params)
+        dev = self.params[0].device
+        self.p = torch.empty(n, dtype=torch.float32, device=dev)
+        self.g = torch.zeros(n, dtype=torch.float32, device=dev)
+        o = 0
+        with torch.no_grad():
+            for q in self.params:
+                k = q.numel()
+                self.p[o:o + k].copy_(q.reshape(-1))
+                q.data = self.p[o:o + k].view_as(q)
+                q.grad = self.g[o:o + k].view_as(q)
+                o += k
+        self.eg2 = torch.zeros_like(self.p)
+        self.edx2 = torch.zeros_like(self.p)
+
+    def zero_grad(self):
+        self.g.zero_()
+
+    def adadelta(self, rho, eps, l1=0.0, l2=0.0):
+        if self.p.is_cuda:
+            call("h2o_adadelta", self.p.data_ptr(), self.g.data_ptr(), self.eg2.data_ptr(), self.edx2.data_ptr(),
+                 self.p.numel(), self.n_decay, float(rho), float(eps), float(l1), float(l2), stream_ptr(self.p.device))
+            return
+        g = self.g.clone()
+        w = slice(0, self.n_decay)
+        g[w] += l2 * self.p[w] + l1 * torch.sign(self.p[w])
+        self.eg2.mul_(rho).addcmul_(g, g, value=1 - rho)
+        d = -torch.sqrt(self.edx2 + eps) / torch.sqrt(self.eg2 + eps) * g
+        self.edx2.mul_(rho).addcmul_(d, d, value=1 - rho)
+        self.p.add_(d)
 
 _M = (1 << 64) - 1
 

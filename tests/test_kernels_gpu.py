@@ -105,3 +105,20 @@ def test_deeplearning_gpu_learns():
     y = ((X[0] * X[1] + X[2]) > 0).float()
     m = DeepLearningTrainer(dict(hidden=[64, 64], epochs=3, seed=1)).fit(X, y, None, None, _info(6))
     assert m.output["training_metrics"]["AUC"] > 0.9
+
+
+def test_fused_adadelta_matches_reference():
+    from llama_github_io_amd.ops.dense import FlatParams
+    torch.manual_seed(0)
+    net_c = torch.nn.Sequential(torch.nn.Linear(37, 19), torch.nn.Linear(19, 3))
+    net_g = torch.nn.Sequential(torch.nn.Linear(37, 19), torch.nn.Linear(19, 3)).to(dev)
+    net_g.load_state_dict({k: v.to(dev) for k, v in net_c.state_dict().items()})
+    fc, fg = FlatParams(net_c), FlatParams(net_g)
+    x = torch.randn(64, 37)
+    for _ in range(3):
+        for net, f, xx in ((net_c, fc, x), (net_g, fg, x.to(dev))):
+            f.zero_grad()
+            net(xx).square().mean().backward()
+            f.adadelta(0.99, 1e-8, l1=1e-4, l2=1e-3)
+    assert torch.allclose(fc.p, fg.p.cpu(), atol=1e-6, rtol=1e-5)
+    assert torch.allclose(fc.eg2, fg.eg2.cpu(), atol=1e-9, rtol=1e-4)
