@@ -931,6 +931,117 @@ __global__ __launch_bounds__(BLK, 4) void k_move(
 }
 
 // ------------------------------------------------------------------------------------------------
+// k_move_lean: the stable partition WITHOUT the fused histogram (the smaller child is histogrammed
+// afterwards by k_hist_build over its now-contiguous rows). With no 128 KiB LDS histogram and one
+// row per lane the kernel is light enough for several 8-wave blocks per CU, so many more rows are
+// in flight than in the LDS-histogram-bound fused kernel.
+//   block = one TILE (2048 rows), 8 waves x 256 rows, lane = row (4 rows per lane);
+//   wave-level ballots give in-wave ranks, one LDS exchange gives each wave its offset in the tile,
+//   tile_off (k_plan) gives the tile's offset in its node: positions are stable.
+#define LW 8              // waves per lean-move block
+#define LROWS (TILE / LW) // rows per wave (256)
+#define LU (LROWS / 64)   // rows per lane (4)
+#define LMAXW 16          // max words (64 features) kept in registers per row on the fast path
+
+template <bool MOVE>
+__global__ __launch_bounds__(LW * 64) void k_move_lean(
+    const uint8_t* __restrict__ sbins, const float4* __restrict__ saux, const int* __restrict__ sridx,
+    uint8_t* __restrict__ dbins, float4* __restrict__ daux, int* __restrict__ dridx, int stride,
+    const Node* __restrict__ nodes, const int* __restrict__ tile_prefix, const int* __restrict__ meta,
+    const Dec* __restrict__ dec, const int* __restrict__ tile_off, const int* __restrict__ node_nl,
+    const int* __restrict__ child_l, const int* __restrict__ child_r, int* __restrict__ leaf_of_row,
+    double* __restrict__ leafsum) {
+  const int n_nodes = meta[0], n_tiles = meta[1];
+  const int t = blockIdx.x;
+  if (t >= n_tiles) return;
+  __shared__ int sL[LW], sR[LW];
+  __shared__ double sred[4][LW];
+  __shared__ Dec sd;
+  const int node = find_node(tile_prefix, n_nodes, t);
+  const Node nd = nodes[node];
+  const int tin = t - tile_prefix[node];
+  const int r0 = nd.start + tin * TILE;
+  const int r1 = min(r0 + TILE, nd.start + nd.len);
+  if (threadIdx.x < (int)(sizeof(Dec) / 4)) ((int*)&sd)[threadIdx.x] = ((const int*)(dec + node))[threadIdx.x];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int feat = sd.feat;
+  const bool term = feat < 0;
+  const int cl = child_l[node], cr = child_r[node];
+  const int W = stride >> 2;
+  const int wbase = r0 + wid * LROWS;
+  // 1. decide every row; in-wave ranks
+  bool valid[LU], left[LU];
+  int rank[LU];
+  int cntL = 0, cntR = 0;
+#pragma unroll
+  for (int u = 0; u < LU; ++u) {
+    const int row = wbase + u * 64 + lane;
+    valid[u] = row < r1;
+    bool lf = true;
+    if (valid[u] && !term) lf = dec_go_left(&sd, sbins[(size_t)row * stride + feat]);
+    left[u] = valid[u] && lf;
+    const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const unsigned long long mL = __ballot(left[u]);
+    const unsigned long long mR = __ballot(valid[u] && !lf);
+    rank[u] = left[u] ? cntL + __popcll(mL & below) : cntR + __popcll(mR & below);
+    cntL += __popcll(mL);
+    cntR += __popcll(mR);
+  }
+  if (lane == 0) { sL[wid] = cntL; sR[wid] = cntR; }
+  __syncthreads();
+  int offL = 0, offR = 0;
+  for (int w = 0; w < wid; ++w) { offL += sL[w]; offR += sR[w]; }
+  const int nl = node_nl[node];
+  const int baseL = nd.start + tile_off[t] + offL;
+  const int baseR = nd.start + nl + (tin * TILE - tile_off[t]) + offR;
+  // 2. move rows whose child continues; leaf bookkeeping for rows that stop
+  double lLn = 0, lLd = 0, lRn = 0, lRd = 0;
+  const unsigned* sb32 = (const unsigned*)sbins;
+  unsigned* db32 = (unsigned*)dbins;
+#pragma unroll
+  for (int u = 0; u < LU; ++u) {
+    if (!valid[u]) continue;
+    const int row = wbase + u * 64 + lane;
+    const int child = left[u] ? cl : cr;
+    const float4 a = saux[row];
+    const int rr = sridx ? sridx[row] : row;
+    if (MOVE && child >= 0 && !term) {
+      const int pos = left[u] ? baseL + rank[u] : baseR + rank[u];
+      const unsigned* src = sb32 + (size_t)row * W;
+      unsigned* dst = db32 + (size_t)pos * W;
+      if (W <= LMAXW) {
+        unsigned v[LMAXW];
+#pragma unroll
+        for (int k = 0; k < LMAXW; ++k) if (k < W) v[k] = src[k];
+#pragma unroll
+        for (int k = 0; k < LMAXW; ++k) if (k < W) dst[k] = v[k];
+      } else {
+        for (int k = 0; k < W; ++k) dst[k] = src[k];
+      }
+      daux[pos] = a;
+      dridx[pos] = rr;
+    } else {
+      const int leaf = term ? (-1 - cl) : (-1 - child);
+      leaf_of_row[rr] = leaf;
+      if (left[u]) { lLn += a.z; lLd += a.w; } else { lRn += a.z; lRd += a.w; }
+    }
+  }
+  // 3. leaf sums: wave -> block -> one atomic pair per side
+  lLn = wave_sum_d(lLn); lLd = wave_sum_d(lLd); lRn = wave_sum_d(lRn); lRd = wave_sum_d(lRd);
+  if (lane == 0) { sred[0][wid] = lLn; sred[1][wid] = lLd; sred[2][wid] = lRn; sred[3][wid] = lRd; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double v[4] = {0, 0, 0, 0};
+    for (int k = 0; k < 4; ++k) for (int w = 0; w < LW; ++w) v[k] += sred[k][w];
+    const int leafL = cl < 0 ? -1 - cl : -1;
+    const int leafR = (!term && cr < 0) ? -1 - cr : -1;
+    if (leafL >= 0 && (v[0] != 0.0 || v[1] != 0.0)) { atomicAdd(leafsum + 2 * leafL, v[0]); atomicAdd(leafsum + 2 * leafL + 1, v[1]); }
+    if (leafR >= 0 && (v[2] != 0.0 || v[3] != 0.0)) { atomicAdd(leafsum + 2 * leafR, v[2]); atomicAdd(leafsum + 2 * leafR + 1, v[3]); }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // k_bin_assign: X (column-major fp32 [F][N]) -> row-major uint8 bins [N][stride].
 // Numeric: bin = #edges <= x (edges sorted, per feature `nedges` of them at edges + f*max_edges);
 // categorical (iscat): bin = code (< nb) else NA. NaN -> NA_BIN.
@@ -1128,6 +1239,26 @@ int h2o_move(const void* sbins, const void* saux, const void* sridx, void* dbins
                        (const int*)tile_prefix, (const int*)meta, (const Dec*)dec, (const int*)tile_off,
                        (const int*)node_nl, (const int*)child_l, (const int*)child_r, (const Node*)next,
                        (double*)hist_next, slot_doubles, (int*)leaf_of_row, (double*)leafsum, (const double*)qs);
+  }
+  return (int)hipGetLastError();
+}
+
+int h2o_move_lean(const void* sbins, const void* saux, const void* sridx, void* dbins, void* daux, void* dridx,
+                  int stride, const void* nodes, const void* tile_prefix, const void* meta, const void* dec,
+                  const void* tile_off, const void* node_nl, const void* child_l, const void* child_r,
+                  void* leaf_of_row, void* leafsum, int move, int tiles_cap, hipStream_t s) {
+  if (move) {
+    hipLaunchKernelGGL(k_move_lean<true>, dim3(tiles_cap), dim3(LW * 64), 0, s, (const uint8_t*)sbins,
+                       (const float4*)saux, (const int*)sridx, (uint8_t*)dbins, (float4*)daux, (int*)dridx, stride,
+                       (const Node*)nodes, (const int*)tile_prefix, (const int*)meta, (const Dec*)dec,
+                       (const int*)tile_off, (const int*)node_nl, (const int*)child_l, (const int*)child_r,
+                       (int*)leaf_of_row, (double*)leafsum);
+  } else {
+    hipLaunchKernelGGL(k_move_lean<false>, dim3(tiles_cap), dim3(LW * 64), 0, s, (const uint8_t*)sbins,
+                       (const float4*)saux, (const int*)sridx, (uint8_t*)dbins, (float4*)daux, (int*)dridx, stride,
+                       (const Node*)nodes, (const int*)tile_prefix, (const int*)meta, (const Dec*)dec,
+                       (const int*)tile_off, (const int*)node_nl, (const int*)child_l, (const int*)child_r,
+                       (int*)leaf_of_row, (double*)leafsum);
   }
   return (int)hipGetLastError();
 }

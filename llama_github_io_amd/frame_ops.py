@@ -13,6 +13,7 @@ import numpy as np
 import torch
 
 from .frame import Column, H2OFrame, engine_device
+from .ops.segment import segment_sum
 
 _NA_MODES = ("all", "ignore", "rm")
 
@@ -56,25 +57,25 @@ class GroupBy:
         G, gid = self.G, self.gid
         dev = gid.device
         if op == "nrow":
-            return torch.zeros(G, dtype=torch.float64, device=dev).index_add_(0, gid, torch.ones_like(gid, dtype=torch.float64))
+            return segment_sum(gid, torch.ones_like(gid, dtype=torch.float64), G)
         v = self.fr._col(name).as_float().to(dev)
         nan = torch.isnan(v)
         ok = ~nan
         vz = torch.where(ok, v, torch.zeros_like(v))
-        cnt = torch.zeros(G, dtype=torch.float64, device=dev).index_add_(0, gid, ok.double())
-        anynan = torch.zeros(G, dtype=torch.float64, device=dev).index_add_(0, gid, nan.double()) > 0
+        cnt = segment_sum(gid, ok.double(), G)
+        anynan = segment_sum(gid, nan.double(), G) > 0
         if op == "sum":
-            r = torch.zeros(G, dtype=torch.float64, device=dev).index_add_(0, gid, vz)
+            r = segment_sum(gid, vz, G)
         elif op == "sumSquares":
-            r = torch.zeros(G, dtype=torch.float64, device=dev).index_add_(0, gid, vz * vz)
+            r = segment_sum(gid, vz * vz, G)
         elif op in ("mean", "var", "sdev"):
-            s = torch.zeros(G, dtype=torch.float64, device=dev).index_add_(0, gid, vz)
+            s = segment_sum(gid, vz, G)
             m = s / cnt
             if op == "mean":
                 r = m
             else:
                 d = torch.where(ok, v - m[gid], torch.zeros_like(v))
-                ss = torch.zeros(G, dtype=torch.float64, device=dev).index_add_(0, gid, d * d)
+                ss = segment_sum(gid, d * d, G)
                 r = ss / (cnt - 1)
                 if op == "sdev":
                     r = r.sqrt()

@@ -17,6 +17,7 @@ import torch
 from ..ops.dense import kmeans_assign
 from .base import DataInfo, Model, make_key
 from .datainfo import Expander
+from ..ops.segment import segment_sum
 
 AGG_DEFAULTS = dict(target_num_exemplars=5000, rel_tol_num_exemplars=0.5, transform="NORMALIZE",
                     categorical_encoding="AUTO", save_mapping_frame=False, num_iteration_without_new_exemplar=500,
@@ -110,7 +111,7 @@ class AggregatorTrainer:
                     break
                 r2 *= (n_ex / target) ** (2.0 / dim_eff)
                 ex_rows, assign = _leader(Z, r2)
-        counts = torch.zeros(ex_rows.numel(), dtype=torch.float64, device=dev).index_add_(0, assign, torch.ones(N, dtype=torch.float64, device=dev))
+        counts = segment_sum(assign, torch.ones(N, dtype=torch.float64, device=dev), ex_rows.numel())
         model = AggregatorModel(model_key or make_key("aggregator"), p, info)
         model.device = dev
         model.output["exemplar_rows"] = ex_rows.cpu().tolist()

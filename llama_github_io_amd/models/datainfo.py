@@ -16,6 +16,7 @@ import numpy as np
 import torch
 
 from .base import DataInfo
+from ..ops.segment import segment_sum
 
 
 class Expander:
@@ -45,7 +46,7 @@ class Expander:
             L = len(dom)
             codes = X[j]
             ok = ~torch.isnan(codes)
-            cnt = torch.zeros(max(L, 1), dtype=torch.float64, device=dev).index_add_(0, codes[ok].long().clamp(0, max(L - 1, 0)), w[ok])
+            cnt = segment_sum(codes[ok].long().clamp(0, max(L - 1, 0)), w[ok], max(L, 1))
             if reduce is not None:
                 cnt = reduce(cnt)
             self.cat_modes.append(int(torch.argmax(cnt)) if L else 0)

@@ -19,6 +19,7 @@ from ..ops import tree as T
 from .base import DataInfo
 from .distributions import ORDER_STAT_DISTS, get_distribution
 from .shared_tree import SharedTreeModel, SharedTreeTrainer
+from ..ops.segment import segment_sum
 
 _FUSED_DIST = {"gaussian": 0, "bernoulli": 1, "quasibinomial": 2, "poisson": 3, "gamma": 4, "tweedie": 5,
                "laplace": 6, "quantile": 7, "huber": 8, "modified_huber": 9}
@@ -214,7 +215,7 @@ class GBMTrainer(SharedTreeTrainer):
         order2 = torch.argsort(leaf_s, stable=True)
         idx = order[order2]
         ls, ds, ws = leaf[idx], diff[idx], w[idx]
-        tot = torch.zeros(L, dtype=torch.float64, device=ds.device).index_add_(0, ls, ws)
+        tot = segment_sum(ls, ws, L)
         cw = torch.cumsum(ws, 0)
         start = torch.cumsum(tot, 0) - tot
         within = cw - start[ls]
@@ -228,7 +229,7 @@ class GBMTrainer(SharedTreeTrainer):
             delta = self.dist.huber_delta
             r = diff - q[leaf]
             c = torch.sign(r) * torch.clamp(r.abs(), max=delta)
-            s = torch.zeros(L, dtype=torch.float64, device=ds.device).index_add_(0, leaf, w * c)
+            s = segment_sum(leaf, w * c, L)
             q = q + s / tot.clamp(min=1e-300)
         return q
 

@@ -30,6 +30,7 @@ from ..parallel import collectives as coll
 from ..ops import gram as G
 from .base import DataInfo, Model, make_key
 from .datainfo import Expander
+from ..ops.segment import segment_sum
 
 GLM_DEFAULTS = dict(family="AUTO", link="family_default", solver="AUTO", alpha=None, lambda_=None, lambda_search=False,
                     nlambdas=-1, lambda_min_ratio=-1.0, standardize=True, intercept=True, max_iterations=-1,
@@ -559,7 +560,7 @@ class GLMTrainer:
             probs = P.double()
             yl = y.long().clamp(min=0)
             res_dev = float(-2 * (w * torch.log(probs.gather(1, yl[:, None])[:, 0].clamp(min=1e-15))).sum())
-            freq = torch.zeros(probs.shape[1], dtype=torch.float64, device=w.device).index_add_(0, yl, w)
+            freq = segment_sum(yl, w, probs.shape[1])
             freq = freq / freq.sum()
             null_dev = float(-2 * (w * torch.log(freq[yl].clamp(min=1e-15))).sum())
             rank = int((beta.abs() > 0).sum())

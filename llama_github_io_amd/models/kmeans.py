@@ -16,10 +16,11 @@ import numpy as np
 import torch
 
 from .. import metrics as mm
-from ..ops.dense import kmeans_assign
+from ..ops.dense import kmeans_assign, kmeans_step
 from ..parallel import collectives as coll
 from .base import DataInfo, Model, make_key
 from .datainfo import Expander
+from ..ops.segment import segment_sum
 
 KM_DEFAULTS = dict(k=1, max_iterations=10, standardize=True, init="Furthest", user_points=None, estimate_k=False,
                    seed=-1, cluster_size_constraints=None)
@@ -120,9 +121,7 @@ class KMeansTrainer:
         K = C.shape[0]
         dev = Z.device
         for it in range(max_it):
-            a, d = kmeans_assign(Z, C)
-            sums = torch.zeros(K, Z.shape[1], dtype=torch.float64, device=dev).index_add_(0, a, Z.double() * w[:, None])
-            cnt = torch.zeros(K, dtype=torch.float64, device=dev).index_add_(0, a, w)
+            a, d, sums, cnt = kmeans_step(Z, C, w)
             if coll.is_dist():
                 sums = coll.all_reduce_(sums)
                 cnt = coll.all_reduce_(cnt)
@@ -171,7 +170,7 @@ class KMeansTrainer:
                 best, prev = (Ck, ak, dk, it), wss
                 if k == kmax:
                     break
-                per = torch.zeros(Ck.shape[0], dtype=torch.float64, device=dev).index_add_(0, ak, dk.double() * w)
+                per = segment_sum(ak, dk.double() * w, Ck.shape[0])
                 worst = int(torch.argmax(per))
                 far = int(torch.argmax(torch.where(ak == worst, dk, torch.full_like(dk, -1.0))))
                 C0 = torch.cat([Ck, Z[far:far + 1]], 0)

@@ -16,6 +16,7 @@ import torch
 from .. import metrics as mm
 from ..parallel import collectives as coll
 from .base import DataInfo, Model, make_key
+from ..ops.segment import segment_sum
 
 NB_DEFAULTS = dict(laplace=0.0, min_sdev=0.001, eps_sdev=0.0, min_prob=0.001, eps_prob=0.0, compute_metrics=True, seed=-1)
 
@@ -77,7 +78,7 @@ class NaiveBayesTrainer:
         w = torch.where(ok, w, torch.zeros_like(w))
         yl = torch.nan_to_num(y, nan=0).long()
         red = coll.all_reduce_ if coll.is_dist() else (lambda t: t)
-        cnt = red(torch.zeros(K, dtype=torch.float64, device=dev).index_add_(0, yl, w))
+        cnt = red(segment_sum(yl, w, K))
         lap = float(self.p["laplace"])
         prior = (cnt + lap) / (cnt.sum() + K * lap)
         cond = []
@@ -88,14 +89,14 @@ class NaiveBayesTrainer:
             if info.iscat[j]:
                 L = len(info.domains[j])
                 code = torch.nan_to_num(x, nan=0).long().clamp(0, max(L - 1, 0))
-                tab = red(torch.zeros(K * L, dtype=torch.float64, device=dev).index_add_(0, yl * L + code, wj)).view(K, L)
+                tab = red(segment_sum(yl * L + code, wj, K * L)).view(K, L)
                 tab = (tab + lap) / (tab.sum(1, keepdim=True) + L * lap).clamp(min=1e-300)
                 cond.append(tab.cpu().numpy())
             else:
                 xz = torch.where(na, torch.zeros_like(x), x)
-                s0 = red(torch.zeros(K, dtype=torch.float64, device=dev).index_add_(0, yl, wj))
-                s1 = red(torch.zeros(K, dtype=torch.float64, device=dev).index_add_(0, yl, wj * xz))
-                s2 = red(torch.zeros(K, dtype=torch.float64, device=dev).index_add_(0, yl, wj * xz * xz))
+                s0 = red(segment_sum(yl, wj, K))
+                s1 = red(segment_sum(yl, wj * xz, K))
+                s2 = red(segment_sum(yl, wj * xz * xz, K))
                 mu = s1 / s0.clamp(min=1e-300)
                 var = (s2 - s0 * mu * mu) / (s0 - 1).clamp(min=1e-300)
                 cond.append(np.stack([mu.cpu().numpy(), var.clamp(min=0).sqrt().cpu().numpy()]))

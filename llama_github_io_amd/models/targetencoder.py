@@ -18,6 +18,7 @@ import numpy as np
 import torch
 
 from .base import DataInfo, Model, make_key
+from ..ops.segment import segment_sum
 
 TE_DEFAULTS = dict(blending=False, inflection_point=10.0, smoothing=20.0, data_leakage_handling="none", noise=0.01,
                    seed=-1, columns_to_encode=None, keep_original_categorical_columns=True, fold_column=None)
@@ -168,8 +169,8 @@ class TargetEncoderTrainer:
             code = X[j]
             okc = ~torch.isnan(code) & ok
             c = torch.nan_to_num(code).long().clamp(0, max(L - 1, 0))
-            num = torch.zeros(L, Y.shape[1], dtype=torch.float64, device=dev).index_add_(0, c[okc], Y[okc])
-            den = torch.zeros(L, dtype=torch.float64, device=dev).index_add_(0, c[okc], torch.ones_like(c[okc], dtype=torch.float64))
+            num = segment_sum(c[okc], Y[okc], L)
+            den = segment_sum(c[okc], torch.ones_like(c[okc], dtype=torch.float64), L)
             st = dict(num=num, den=den, prior=prior, domain=list(info.domains[j]))
             if fold is not None:
                 nf = int(fold.max()) + 1

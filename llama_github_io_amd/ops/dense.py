@@ -19,6 +19,8 @@ nat.register_hip_signatures({
     "h2o_bias_act_bwd": [nat.c_void_p, nat.c_void_p, nat.c_void_p, nat.c_void_p, nat.c_ll, nat.c_int, nat.c_int,
                          nat.ctypes.c_float, nat.c_ull, nat.c_void_p],
     "h2o_kmeans_assign": [nat.c_void_p, nat.c_ll, nat.c_int, nat.c_void_p, nat.c_int, nat.c_void_p, nat.c_void_p, nat.c_void_p],
+    "h2o_kmeans_step": [nat.c_void_p, nat.c_ll, nat.c_int, nat.c_void_p, nat.c_int, nat.c_void_p, nat.c_void_p,
+                        nat.c_void_p, nat.c_void_p, nat.c_void_p],
     "h2o_adadelta": [nat.c_void_p, nat.c_void_p, nat.c_void_p, nat.c_void_p, nat.c_ll, nat.c_ll, nat.ctypes.c_float,
                      nat.ctypes.c_float, nat.ctypes.c_float, nat.ctypes.c_float, nat.c_void_p],
 })
@@ -145,6 +147,35 @@ class BiasAct(torch.autograd.Function):
 def bias_act(x, b, act: str | int = "rectifier", drop: float = 0.0, seed: int = 0):
     a = ACT[act.lower()] if isinstance(act, str) else int(act)
     return BiasAct.apply(x, b, a, float(drop), int(seed))
+
+
+def kmeans_step(X: torch.Tensor, C: torch.Tensor, w: torch.Tensor | None = None):
+    """One Lloyd step: (assign [N], min sq. distance [N], per-center weighted sums [K, P] fp64, counts [K])."""
+    N, P = X.shape
+    K = C.shape[0]
+    if X.is_cuda and (K * P + 256 * (P + 1) + 512) * 4 <= 160 * 1024 and N > 0 and K * (P + 1) <= 8192:
+        X = X.contiguous().float()
+        C = C.contiguous().float()
+        wf = None if w is None else w.contiguous().float()
+        a = torch.empty(N, dtype=torch.int32, device=X.device)
+        d = torch.empty(N, dtype=torch.float32, device=X.device)
+        G = (N + 255) // 256
+        slab = torch.empty(G, K, P + 1, dtype=torch.float32, device=X.device)
+        nat.call("h2o_kmeans_step", X.data_ptr(), N, P, C.data_ptr(), K, 0 if wf is None else wf.data_ptr(),
+                 a.data_ptr(), d.data_ptr(), slab.data_ptr(), nat.stream_ptr(X.device))
+        tot = slab.sum(0, dtype=torch.float64)
+        return a.long(), d, tot[:, :P], tot[:, P]
+    a, d = kmeans_assign(X, C)
+    wd = torch.ones(N, dtype=torch.float64, device=X.device) if w is None else w.double()
+    # sort-based segment sums (no contended atomics)
+    order = torch.argsort(a)
+    cnt = torch.bincount(a, weights=wd, minlength=K)
+    nrows = torch.bincount(a, minlength=K)
+    cs = torch.cumsum(X.double()[order] * wd[order, None], 0)
+    cs = torch.cat([torch.zeros(1, P, dtype=torch.float64, device=X.device), cs], 0)
+    ends = torch.cumsum(nrows, 0)
+    sums = cs[ends] - cs[ends - nrows]
+    return a, d, sums, cnt
 
 
 def kmeans_assign(X: torch.Tensor, C: torch.Tensor):

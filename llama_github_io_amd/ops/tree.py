@@ -16,6 +16,7 @@ sorted by mean response. Mode 1 is XGBoost's Newton gain G²/(H+λ) with L1 soft
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -427,6 +428,9 @@ class GpuTreeBuilder:
         self.av["meta0"].copy_(torch.from_numpy(np.array([1, n_tiles0], dtype=np.int32).view(np.uint8)))
         self.av["tp0"][:8].copy_(torch.from_numpy(np.array([0, n_tiles0], dtype=np.int32).view(np.uint8)))
         self.history = []
+        # partition strategy: "lean" (partition-only kernel + separate smaller-child histogram) or
+        # "fused" (partition fused with the LDS histogram, one block per CU)
+        self.lean = os.environ.get("H2O_TREE_MOVE", "lean") == "lean"
 
     def _p(self, name):
         return self.av[name].data_ptr()
@@ -489,14 +493,25 @@ class GpuTreeBuilder:
             if not last:
                 nat.check(lib.h2o_zero_hist(hn.data_ptr(), self._p(f"nodes{d + 1}"), self._p(f"meta{d + 1}"),
                                             self.caps[d + 1], slot, s), "zero_hist")
-            fuse = (F <= FTILE) and not last
+            fuse = (F <= FTILE) and not last and not self.lean
             g = min(self.tiles_cap[d], self.grid)
-            nat.check(lib.h2o_move(sb, sa, sr, dst["bins"].data_ptr(), dst["aux"].data_ptr(), dst["ridx"].data_ptr(),
-                                   self.stride, F, self._p(f"nodes{d}"), self._p(f"tp{d}"), self._p(f"meta{d}"),
-                                   self._p(f"dec{d}"), self.tile_off.data_ptr(), self._p(f"nl{d}"), self._p(f"cl{d}"),
-                                   self._p(f"cr{d}"), self._p(f"nodes{d + 1}"), hn.data_ptr(), slot,
-                                   self.leaf_of_row.data_ptr(), self.leafsum.data_ptr(), qs, int(fuse), g, pk, s), "move")
-            if not last and F > FTILE:
+            if self.lean:
+                # partition-only pass (high occupancy, no LDS histogram); the smaller child is
+                # histogrammed below over its contiguous rows
+                nat.check(lib.h2o_move_lean(sb, sa, sr, dst["bins"].data_ptr(), dst["aux"].data_ptr(),
+                                            dst["ridx"].data_ptr(), self.stride, self._p(f"nodes{d}"), self._p(f"tp{d}"),
+                                            self._p(f"meta{d}"), self._p(f"dec{d}"), self.tile_off.data_ptr(),
+                                            self._p(f"nl{d}"), self._p(f"cl{d}"), self._p(f"cr{d}"),
+                                            self.leaf_of_row.data_ptr(), self.leafsum.data_ptr(), int(not last),
+                                            self.tiles_cap[d], s), "move_lean")
+            else:
+                nat.check(lib.h2o_move(sb, sa, sr, dst["bins"].data_ptr(), dst["aux"].data_ptr(), dst["ridx"].data_ptr(),
+                                       self.stride, F, self._p(f"nodes{d}"), self._p(f"tp{d}"), self._p(f"meta{d}"),
+                                       self._p(f"dec{d}"), self.tile_off.data_ptr(), self._p(f"nl{d}"), self._p(f"cl{d}"),
+                                       self._p(f"cr{d}"), self._p(f"nodes{d + 1}"), hn.data_ptr(), slot,
+                                       self.leaf_of_row.data_ptr(), self.leafsum.data_ptr(), qs, int(fuse), g, pk, s),
+                          "move")
+            if not last and not fuse:
                 nat.check(lib.h2o_hist_build(dst["bins"].data_ptr(), self.stride, dst["aux"].data_ptr(),
                                              self._p(f"nodes{d + 1}"), self._p(f"tp{d + 1}"), self._p(f"meta{d + 1}"),
                                              F, hn.data_ptr(), slot, qs, min(self.tiles_cap[d + 1], self.grid), pk, s),

@@ -122,3 +122,30 @@ def test_fused_adadelta_matches_reference():
             f.adadelta(0.99, 1e-8, l1=1e-4, l2=1e-3)
     assert torch.allclose(fc.p, fg.p.cpu(), atol=1e-6, rtol=1e-5)
     assert torch.allclose(fc.eg2, fg.eg2.cpu(), atol=1e-9, rtol=1e-4)
+
+
+@pytest.mark.parametrize("n,C", [(7, 0), (5000, 0), (9, 13), (3000, 4)])
+def test_segment_sum_paths(n, C):
+    from llama_github_io_amd.ops.segment import segment_sum
+    g = torch.Generator(device=dev).manual_seed(n)
+    N = 200000
+    idx = torch.randint(0, n, (N,), device=dev, generator=g)
+    v = torch.randn((N,) if C == 0 else (N, C), device=dev, generator=g)
+    got = segment_sum(idx, v, n)
+    ref = torch.zeros(got.shape, dtype=torch.float64).index_add_(0, idx.cpu(), v.cpu().double())
+    assert torch.allclose(got.cpu(), ref, atol=1e-6, rtol=1e-6)
+
+
+def test_kmeans_step_kernel():
+    from llama_github_io_amd.ops.dense import kmeans_step
+    g = torch.Generator(device=dev).manual_seed(3)
+    X = torch.randn(100003, 11, device=dev, generator=g)
+    C = torch.randn(6, 11, device=dev, generator=g)
+    w = torch.rand(100003, device=dev, generator=g)
+    a, d, sums, cnt = kmeans_step(X, C, w)
+    D = ((X[:, None, :].double() - C[None].double()) ** 2).sum(-1)
+    aref = D.argmin(1)
+    assert (a == aref).float().mean() > 0.999
+    ref = torch.zeros(6, 11, dtype=torch.float64, device=dev).index_add_(0, a, X.double() * w.double()[:, None])
+    cref = torch.zeros(6, dtype=torch.float64, device=dev).index_add_(0, a, w.double())
+    assert torch.allclose(sums, ref, rtol=1e-4, atol=1e-2) and torch.allclose(cnt, cref, rtol=1e-4, atol=1e-2)
