@@ -192,8 +192,8 @@ def multinomial_metrics(y, probs, w=None, domain=None, hit_k: int = 10) -> Model
     onehot = torch.nn.functional.one_hot(y, K).double()
     mse = float((w * ((onehot - probs) ** 2).sum(1)).sum() / sw)
     pred = probs.argmax(1)
-    cm = torch.zeros(K, K, dtype=torch.float64, device=y.device)
-    cm.index_put_((y, pred), w, accumulate=True)
+    from .ops.segment import segment_sum
+    cm = segment_sum(y * K + pred, w, K * K).view(K, K)
     per_class_err = 1 - torch.diag(cm) / cm.sum(1).clamp(min=1e-300)
     rank = (probs > py[:, None]).sum(1)
     hits = [float((w * (rank < k).double()).sum() / sw) for k in range(1, min(hit_k, K) + 1)]
@@ -224,8 +224,9 @@ def clustering_metrics(X, centers, assign, w=None) -> ModelMetrics:
     w = _w(w, X.shape[0], X.device)
     d = ((X - C[assign]) ** 2).sum(1)
     K = C.shape[0]
-    within = torch.zeros(K, dtype=torch.float64, device=X.device).index_add_(0, assign, w * d)
-    size = torch.zeros(K, dtype=torch.float64, device=X.device).index_add_(0, assign, w)
+    from .ops.segment import segment_sum
+    within = segment_sum(assign, w * d, K)
+    size = segment_sum(assign, w, K)
     mu = (w[:, None] * X).sum(0) / w.sum()
     totss = float((w * ((X - mu) ** 2).sum(1)).sum())
     tw = float(within.sum())

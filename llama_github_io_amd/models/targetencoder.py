@@ -175,8 +175,8 @@ class TargetEncoderTrainer:
             if fold is not None:
                 nf = int(fold.max()) + 1
                 fi = fold[okc] * L + c[okc]
-                st["fold_num"] = torch.zeros(nf * L, Y.shape[1], dtype=torch.float64, device=dev).index_add_(0, fi, Y[okc]).view(nf, L, -1)
-                st["fold_den"] = torch.zeros(nf * L, dtype=torch.float64, device=dev).index_add_(0, fi, torch.ones_like(fi, dtype=torch.float64)).view(nf, L)
+                st["fold_num"] = segment_sum(fi, Y[okc], nf * L).view(nf, L, -1)
+                st["fold_den"] = segment_sum(fi, torch.ones_like(fi, dtype=torch.float64), nf * L).view(nf, L)
             stats[info.x[j]] = st
         model = TargetEncoderModel(model_key or make_key("te"), p, info)
         model.device = dev

@@ -22,6 +22,7 @@ import torch
 from ..ops.binning import apply_binning, fit_binning
 from ..ops.forest import Forest, Tree
 from ..ops.tree import NA_BIN
+from ..ops.segment import segment_sum
 from .base import DataInfo, Model, make_key
 
 UPLIFT_DEFAULTS = dict(ntrees=50, max_depth=20, min_rows=10.0, mtries=-2, sample_rate=0.632, nbins=20,
@@ -138,7 +139,7 @@ class UpliftDRFTrainer:
             act = node >= 0
             rows = torch.nonzero(act).flatten()
             nd = node[rows]
-            tot = torch.zeros(A, 4, dtype=torch.float64, device=dev).index_add_(0, nd, stats[rows])
+            tot = segment_sum(nd, stats[rows], A)
             pt_n = tot[:, 1] / tot[:, 0].clamp(min=1)
             pc_n = tot[:, 3] / tot[:, 2].clamp(min=1)
             for i, gid in enumerate(level):
