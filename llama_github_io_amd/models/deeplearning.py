@@ -15,6 +15,7 @@ distributions (gaussian/poisson/gamma/tweedie/laplace/quantile/huber), early sto
 from __future__ import annotations
 
 import math
+import os
 import time
 
 import numpy as np
@@ -273,49 +274,94 @@ class DeepLearningTrainer:
         perm = None
         pos = N
         wf = w.float()
+        # hipGraph capture of the whole training step (fwd + bwd + fused ADADELTA): the step is a fixed
+        # launch sequence on static buffers, so replaying it removes the per-kernel launch overhead that
+        # dominates small-batch MLP training. Eager path for dropout / momentum / max_w2 / multi-rank.
+        use_graph = (dev.type == "cuda" and adaptive and not coll.is_dist() and float(p["input_dropout_ratio"]) == 0
+                     and all(float(v) == 0 for v in hd) and max_w2 == float("inf") and N >= B
+                     and os.environ.get("H2O_DL_GRAPH", "1") == "1")
+        graph = None
+        if use_graph:
+            sx = torch.empty(B, Z.shape[1], dtype=Z.dtype, device=dev)
+            sw = torch.empty(B, dtype=wf.dtype, device=dev)
+            sy = None if ae else torch.empty((B,) + tuple(yt.shape[1:]), dtype=yt.dtype, device=dev)
+            side = torch.cuda.Stream(dev)
+
+            def graph_step():
+                fp.zero_grad()
+                with torch.autocast(device_type="cuda", dtype=dtype, enabled=dtype is not None):
+                    o = net(sx, seed)
+                ls = self._loss(o.float(), sx if ae else sy, sw, cat, dist, ae) / sw.sum().clamp(min=1e-12)
+                ls.backward()
+                with torch.no_grad():
+                    fp.adadelta(rho, eps, l1, l2)
         for step in range(total):
             if pos + B > N:
                 perm = torch.randperm(N, generator=g).to(dev) if p["shuffle_training_data"] or True else torch.arange(N, device=dev)
                 pos = 0
             idx = perm[pos:pos + B]
             pos += B
-            xb = Z.index_select(0, idx)
-            wb = wf.index_select(0, idx)
             net.train()
             net.step = step
-            with torch.autocast(device_type=dev.type, dtype=dtype, enabled=dtype is not None):
-                out = net(xb, seed)
-            out = out.float()
-            loss = self._loss(out, xb if ae else yt.index_select(0, idx), wb, cat, dist, ae) / wb.sum().clamp(min=1e-12)
-            fp.zero_grad()
-            loss.backward()                  # accumulates into the flat gradient buffer
-            if coll.is_dist():               # data parallel: ONE all-reduce of every gradient per step
-                coll.all_reduce_(fp.g)
-                fp.g /= coll.world()
-            with torch.no_grad():
-                samples += B * (coll.world() if coll.is_dist() else 1)
-                if adaptive:                 # ADADELTA (Neurons.java: rho, epsilon), one fused HIP launch
-                    fp.adadelta(rho, eps, l1, l2)
+            if use_graph:
+                torch.index_select(Z, 0, idx, out=sx)
+                torch.index_select(wf, 0, idx, out=sw)
+                if sy is not None:
+                    torch.index_select(yt, 0, idx, out=sy)
+                if graph is None and step < 3:          # warm-up steps on a side stream before capture
+                    side.wait_stream(torch.cuda.current_stream(dev))
+                    with torch.cuda.stream(side):
+                        graph_step()
+                    torch.cuda.current_stream(dev).wait_stream(side)
                 else:
-                    rate = float(p["rate"]) / (1 + float(p["rate_annealing"]) * samples)
-                    m = self._momentum(samples)
-                    gg = fp.g.clone()
-                    nd = fp.n_decay
-                    if l2 > 0 or l1 > 0:
-                        gg[:nd] += l2 * fp.p[:nd] + l1 * torch.sign(fp.p[:nd])
-                    if m > 0:
-                        mom.mul_(m).add_(gg, alpha=-rate)
-                        if p["nesterov_accelerated_gradient"]:
-                            fp.p.add_(mom, alpha=m).add_(gg, alpha=-rate)
-                        else:
-                            fp.p.add_(mom)
+                    if graph is None:
+                        try:
+                            graph = torch.cuda.CUDAGraph()
+                            with torch.cuda.graph(graph):
+                                graph_step()
+                        except Exception:  # noqa: BLE001 - capture unsupported: fall back to eager replay
+                            graph = False
+                    if graph is False:
+                        graph_step()
                     else:
-                        fp.p.add_(gg, alpha=-rate)
-                if max_w2 < float("inf"):
-                    for q in params:
-                        if q.dim() > 1:
-                            n2 = (q * q).sum(1, keepdim=True)
-                            q.mul_(torch.where(n2 > max_w2, torch.sqrt(max_w2 / n2), torch.ones_like(n2)))
+                        graph.replay()
+                samples += B
+            else:
+                xb = Z.index_select(0, idx)
+                wb = wf.index_select(0, idx)
+                with torch.autocast(device_type=dev.type, dtype=dtype, enabled=dtype is not None):
+                    out = net(xb, seed)
+                out = out.float()
+                loss = self._loss(out, xb if ae else yt.index_select(0, idx), wb, cat, dist, ae) / wb.sum().clamp(min=1e-12)
+                fp.zero_grad()
+                loss.backward()                  # accumulates into the flat gradient buffer
+                if coll.is_dist():               # data parallel: ONE all-reduce of every gradient per step
+                    coll.all_reduce_(fp.g)
+                    fp.g /= coll.world()
+                with torch.no_grad():
+                    samples += B * (coll.world() if coll.is_dist() else 1)
+                    if adaptive:                 # ADADELTA (Neurons.java: rho, epsilon), one fused HIP launch
+                        fp.adadelta(rho, eps, l1, l2)
+                    else:
+                        rate = float(p["rate"]) / (1 + float(p["rate_annealing"]) * samples)
+                        m = self._momentum(samples)
+                        gg = fp.g.clone()
+                        nd = fp.n_decay
+                        if l2 > 0 or l1 > 0:
+                            gg[:nd] += l2 * fp.p[:nd] + l1 * torch.sign(fp.p[:nd])
+                        if m > 0:
+                            mom.mul_(m).add_(gg, alpha=-rate)
+                            if p["nesterov_accelerated_gradient"]:
+                                fp.p.add_(mom, alpha=m).add_(gg, alpha=-rate)
+                            else:
+                                fp.p.add_(mom)
+                        else:
+                            fp.p.add_(gg, alpha=-rate)
+                    if max_w2 < float("inf"):
+                        for q in params:
+                            if q.dim() > 1:
+                                n2 = (q * q).sum(1, keepdim=True)
+                                q.mul_(torch.where(n2 > max_w2, torch.sqrt(max_w2 / n2), torch.ones_like(n2)))
             if self.job is not None and step % 50 == 0:
                 self.job.set_progress(step / max(total, 1))
             end = step == total - 1
