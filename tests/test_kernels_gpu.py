@@ -149,3 +149,17 @@ def test_kmeans_step_kernel():
     ref = torch.zeros(6, 11, dtype=torch.float64, device=dev).index_add_(0, a, X.double() * w.double()[:, None])
     cref = torch.zeros(6, dtype=torch.float64, device=dev).index_add_(0, a, w.double())
     assert torch.allclose(sums, ref, rtol=1e-4, atol=1e-2) and torch.allclose(cnt, cref, rtol=1e-4, atol=1e-2)
+
+
+def test_deeplearning_graph_matches_eager(monkeypatch):
+    from llama_github_io_amd.models.deeplearning import DeepLearningTrainer
+    g = torch.Generator(device=dev).manual_seed(0)
+    X = torch.randn(6, 8192, device=dev, generator=g)
+    y = ((X[0] * X[1] + X[2]) > 0).float()
+    res = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("H2O_DL_GRAPH", flag)
+        m = DeepLearningTrainer(dict(hidden=[32, 32], epochs=2, seed=3, mini_batch_size=512, score_interval=1e9,
+                                     stopping_rounds=0)).fit(X, y, None, None, _info(6))
+        res.append(torch.cat([q.detach().reshape(-1) for q in m.net.parameters()]).cpu())
+    assert torch.allclose(res[0], res[1], atol=1e-5, rtol=1e-4)
