@@ -240,7 +240,9 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
   float* nayy = (float*)(smem64 + FTILE * HS64);         // FTILE
   double* red = (double*)(nayy + FTILE);                 // 64 doubles scratch
 
-  const int n_nodes = meta[0], n_tiles = meta[1];
+  // tile_prefix here is the BUILD-tile prefix (only nodes with build=1 own tiles) and meta[2] the number
+  // of build tiles: blocks split only the rows that are histogrammed (no idle blocks on skipped siblings)
+  const int n_nodes = meta[0], n_tiles = meta[2];
   if (n_nodes <= 0 || n_tiles <= 0) return;
   const int per = (n_tiles + gridDim.x - 1) / gridDim.x;
   const int t0 = blockIdx.x * per, t1 = min(n_tiles, t0 + per);
@@ -595,6 +597,7 @@ __global__ __launch_bounds__(1024) void k_plan(
     const int* __restrict__ tile_cnt, const Dec* __restrict__ dec,
     int* __restrict__ tile_off, int* __restrict__ node_nl, int* __restrict__ child_l, int* __restrict__ child_r,
     Node* __restrict__ next, int* __restrict__ next_tile_prefix, int* __restrict__ next_meta,
+    int* __restrict__ next_build_prefix,
     int* __restrict__ counters, int* __restrict__ scratch /* >= 2*cap_cur ints */,
     int depth, int max_depth, double min_w, int cap_next, int leaf_cap) {
   __shared__ int sh[17];
@@ -708,14 +711,26 @@ __global__ __launch_bounds__(1024) void k_plan(
   {
     const int per = (nn + T - 1) / T;
     const int a = min(nn, tid * per), b = min(nn, a + per);
-    int s = 0;
-    for (int i = a; i < b; ++i) s += (next[i].len + TILE - 1) / TILE;
+    int s = 0, sbt = 0;
+    for (int i = a; i < b; ++i) {
+      const int k = (next[i].len + TILE - 1) / TILE;
+      s += k;
+      sbt += next[i].build ? k : 0;
+    }
     int off = block_excl_scan(s, sh, &total);
-    for (int i = a; i < b; ++i) { next_tile_prefix[i] = off; off += (next[i].len + TILE - 1) / TILE; }
+    int totalb = 0;
+    int offb = block_excl_scan(sbt, sh, &totalb);
+    for (int i = a; i < b; ++i) {
+      const int k = (next[i].len + TILE - 1) / TILE;
+      next_tile_prefix[i] = off; off += k;
+      next_build_prefix[i] = offb; offb += next[i].build ? k : 0;
+    }
     if (tid == 0) {
       next_tile_prefix[nn] = total;
+      next_build_prefix[nn] = totalb;
       next_meta[0] = nn;
       next_meta[1] = total;
+      next_meta[2] = totalb;
       counters[0] = min(leaf_base0 + n_leaves_new, leaf_cap);
     }
   }
@@ -1197,10 +1212,11 @@ int h2o_count(const void* bins, int stride, const void* nodes, const void* tile_
 int h2o_plan(const void* nodes, const void* meta, const void* tile_prefix, const void* tile_cnt, const void* dec,
              void* tile_off, void* node_nl, void* child_l, void* child_r, void* next, void* next_tile_prefix,
              void* next_meta, void* counters, void* scratch, int depth, int max_depth, double min_w, int cap_next,
-             int leaf_cap, hipStream_t s) {
+             int leaf_cap, void* next_build_prefix, hipStream_t s) {
   hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, s, (const Node*)nodes, (const int*)meta,
                      (const int*)tile_prefix, (const int*)tile_cnt, (const Dec*)dec, (int*)tile_off, (int*)node_nl,
                      (int*)child_l, (int*)child_r, (Node*)next, (int*)next_tile_prefix, (int*)next_meta,
+                     (int*)next_build_prefix,
                      (int*)counters, (int*)scratch, depth, max_depth, min_w, cap_next, leaf_cap);
   return (int)hipGetLastError();
 }

@@ -408,8 +408,9 @@ class GpuTreeBuilder:
         for d in range(D + 1):
             c = self.caps[d]
             ar.add(f"nodes{d}", c * NODE_DT.itemsize)
-            ar.add(f"meta{d}", 8)
+            ar.add(f"meta{d}", 16)                 # [n_nodes, n_tiles, n_build_tiles, pad]
             ar.add(f"tp{d}", (c + 1) * 4)
+            ar.add(f"bp{d}", (c + 1) * 4)          # tile prefix over build (histogrammed) nodes only
             ar.add(f"dec{d}", c * DEC_DT.itemsize)
             ar.add(f"cl{d}", c * 4)
             ar.add(f"cr{d}", c * 4)
@@ -425,8 +426,9 @@ class GpuTreeBuilder:
         root = np.zeros(1, dtype=NODE_DT)
         root[0] = (0, N, 1, -1, -1, 0, 0, 0)
         self.av["nodes0"].copy_(torch.from_numpy(root.view(np.uint8)))
-        self.av["meta0"].copy_(torch.from_numpy(np.array([1, n_tiles0], dtype=np.int32).view(np.uint8)))
+        self.av["meta0"].copy_(torch.from_numpy(np.array([1, n_tiles0, n_tiles0, 0], dtype=np.int32).view(np.uint8)))
         self.av["tp0"][:8].copy_(torch.from_numpy(np.array([0, n_tiles0], dtype=np.int32).view(np.uint8)))
+        self.av["bp0"][:8].copy_(torch.from_numpy(np.array([0, n_tiles0], dtype=np.int32).view(np.uint8)))
         self.history = []
         # partition strategy: "lean" (partition-only kernel + separate smaller-child histogram) or
         # "fused" (partition fused with the LDS histogram, one block per CU)
@@ -460,7 +462,7 @@ class GpuTreeBuilder:
         qs = self.qs.data_ptr()
         g0 = min(self.tiles_cap[0], self.grid)
         nat.check(lib.h2o_hist_build(self.master.data_ptr(), self.stride, aux_static.data_ptr(), self._p("nodes0"),
-                                     self._p("tp0"), self._p("meta0"), F, self.hist[0].data_ptr(), slot, qs, g0, pk, s),
+                                     self._p("bp0"), self._p("meta0"), F, self.hist[0].data_ptr(), slot, qs, g0, pk, s),
                   "hist_build")
         coll.all_reduce_(self.hist[0][:slot])
         self.root_w = self.hist[0][0:2 * NBIN:2].sum().reshape(1)   # Σw over feature 0's bins = root weight
@@ -488,7 +490,7 @@ class GpuTreeBuilder:
                                    self._p(f"dec{d}"), self.tile_off.data_ptr(), self._p(f"nl{d}"), self._p(f"cl{d}"),
                                    self._p(f"cr{d}"), self._p(f"nodes{d + 1}"), self._p(f"tp{d + 1}"),
                                    self._p(f"meta{d + 1}"), self._p("counters"), self.scratch.data_ptr(), d, D,
-                                   p.min_w, self.caps[d + 1], self.leaf_cap, s), "plan")
+                                   p.min_w, self.caps[d + 1], self.leaf_cap, self._p(f"bp{d + 1}"), s), "plan")
             last = d + 1 == D
             if not last:
                 nat.check(lib.h2o_zero_hist(hn.data_ptr(), self._p(f"nodes{d + 1}"), self._p(f"meta{d + 1}"),
@@ -513,7 +515,7 @@ class GpuTreeBuilder:
                           "move")
             if not last and not fuse:
                 nat.check(lib.h2o_hist_build(dst["bins"].data_ptr(), self.stride, dst["aux"].data_ptr(),
-                                             self._p(f"nodes{d + 1}"), self._p(f"tp{d + 1}"), self._p(f"meta{d + 1}"),
+                                             self._p(f"nodes{d + 1}"), self._p(f"bp{d + 1}"), self._p(f"meta{d + 1}"),
                                              F, hn.data_ptr(), slot, qs, min(self.tiles_cap[d + 1], self.grid), pk, s),
                           "hist_build")
             if not last:
