@@ -1025,7 +1025,16 @@ __global__ __launch_bounds__(LW * 64) void k_move_lean(
       const int pos = left[u] ? baseL + rank[u] : baseR + rank[u];
       const unsigned* src = sb32 + (size_t)row * W;
       unsigned* dst = db32 + (size_t)pos * W;
-      if (W <= LMAXW) {
+      if ((stride & 15) == 0 && stride <= 64) {      // 16-B aligned rows: vector copy
+        const uint4* s4 = (const uint4*)src;
+        uint4* d4 = (uint4*)dst;
+        const int nv = stride >> 4;
+        uint4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) if (k < nv) v[k] = s4[k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) if (k < nv) d4[k] = v[k];
+      } else if (W <= LMAXW) {
         unsigned v[LMAXW];
 #pragma unroll
         for (int k = 0; k < LMAXW; ++k) if (k < W) v[k] = src[k];

@@ -92,7 +92,9 @@ def fit_binning(X: torch.Tensor, iscat, nlevels=None, max_bins: int = MAX_DATA_B
             e = e[e > row[0]]  # first bin must be non-empty
         edges.append(e)
         nbins[f] = e.size + 1
-    stride = (F + 3) // 4 * 4
+    # rows of more than 12 features are padded to 16 B multiples so the partition kernel moves them
+    # with 16-byte vector loads/stores (2 per 28-feature row instead of 7 dword pairs)
+    stride = (F + 3) // 4 * 4 if F <= 12 else (F + 15) // 16 * 16
     return Binning(F, stride, edges, nbins, iscat, nlevels, l2b)
 
 
