@@ -9,10 +9,12 @@
 // Design (MI355X-first, not a port):
 //   * features are pre-binned once into a row-major uint8 matrix (bin 255 = NA), so a row is Fp bytes.
 //   * rows are PHYSICALLY partitioned by tree node every level (stable two-pass partition: k_count ->
-//     k_plan scan -> k_move), so every histogram pass streams contiguous rows of ONE node and the
-//     per-node histogram lives privately in LDS (32 features x 256 bins x {w, wY} fp32 = 66 KB).
-//   * only the smaller child of each split is histogrammed (fused into the partition kernel); the
-//     sibling comes from parent - child (k_subtract), in fp64.
+//     k_plan scan -> k_move_lean), so every histogram pass streams contiguous rows of ONE node and the
+//     per-node histogram lives privately in LDS (fixed-point int64, see below).
+//   * only the smaller child of each split is histogrammed (k_hist_build over its contiguous rows),
+//     into a COMPACT buffer indexed by the parent (one built child per parent); the sibling comes
+//     from parent - child (k_subtract), in fp64. Row-sharded runs all-reduce only that compact
+//     buffer: half the bytes of reducing every child slot of the level.
 //   * split search, child planning, leaf numbering and tile planning all stay on device: a whole
 //     tree is a fixed launch sequence with no host synchronisation.
 //   * rows reaching a leaf write their leaf id in ORIGINAL row order (scatter through ridx) and stop
@@ -187,9 +189,6 @@ __device__ __forceinline__ void hist_word(long long* h, float* nayy, unsigned wo
 }
 
 #define UNR 8   // hist: rows per lane-group in flight (memory-level parallelism: 8 independent loads per lane)
-#define MUNR 4  // k_move: rows per lane-group per partition step (MUNR*8 <= 64 for the wave-0 scan)
-// (measured: a 512-thread / MUNR=8 k_move without register spills ran 1.6x SLOWER than this 16-wave
-//  one that spills 11 VGPRs: occupancy, not spills, hides this kernel's memory latency)
 
 __device__ __forceinline__ float row_yy(float a, float b) {
   return a > 0.f ? b * b * __builtin_amdgcn_rcpf(a) : 0.f;
@@ -260,10 +259,11 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
     const int node = find_node(tile_prefix, n_nodes, t);
     const Node nd = nodes[node];
     if (!nd.build) continue;
+    const int hslot = nd.parent >= 0 ? nd.parent : 0;   // compact build slot (see header)
     const int r0 = nd.start + (t - tile_prefix[node]) * TILE;
     const int r1 = min(r0 + TILE, nd.start + nd.len);
     // new node, or (packed) the flush window is full: flush the LDS tile and restart it
-    if (node != cur || (packed && since + (r1 - r0) > PACK_MAX)) {
+    if (hslot != cur || (packed && since + (r1 - r0) > PACK_MAX)) {
       if (cur >= 0) {
         double v[4] = {wyy, 0, 0, 0};
         block_sum4(v, red);
@@ -275,7 +275,7 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
       for (int i = threadIdx.x; i < FTILE; i += blockDim.x) nayy[i] = 0.f;
       wyy = 0.0;
       since = 0;
-      cur = node;
+      cur = hslot;
       __syncthreads();
     }
     since += r1 - r0;
@@ -736,220 +736,39 @@ __global__ __launch_bounds__(1024) void k_plan(
   }
 }
 
-// k_zero_hist: zero the histogram slots of next-level nodes that are built directly.
-__global__ void k_zero_hist(double* __restrict__ hist, const Node* __restrict__ next,
+// k_zero_hist: zero the compact build slots (slot = parent) of next-level nodes built directly.
+__global__ void k_zero_hist(double* __restrict__ hbuild, const Node* __restrict__ next,
                             const int* __restrict__ meta, int slot_doubles) {
   const int node = blockIdx.y;
   if (node >= meta[0] || !next[node].build) return;
-  double* s = hist + (size_t)node * slot_doubles;
+  double* s = hbuild + (size_t)next[node].parent * slot_doubles;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < slot_doubles; i += gridDim.x * blockDim.x) s[i] = 0.0;
 }
 
-// k_subtract: sibling histogram = parent - built child (fp64).
+// k_subtract: next-level node histograms from the compact build buffer: the built child copies its
+// slot, the sibling is parent - built child (fp64). Both read hbuild[parent].
 __global__ void k_subtract(double* __restrict__ hist_next, const double* __restrict__ hist_cur,
-                           const Node* __restrict__ next, const int* __restrict__ meta, int slot_doubles) {
+                           const double* __restrict__ hbuild, const Node* __restrict__ next,
+                           const int* __restrict__ meta, int slot_doubles) {
   const int node = blockIdx.y;
   if (node >= meta[0]) return;
   const Node nd = next[node];
-  if (nd.build) return;
   double* s = hist_next + (size_t)node * slot_doubles;
-  const double* pa = hist_cur + (size_t)nd.parent * slot_doubles;
-  const double* sb = hist_next + (size_t)nd.sib * slot_doubles;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < slot_doubles; i += gridDim.x * blockDim.x)
-    s[i] = pa[i] - sb[i];
-}
-
-// ------------------------------------------------------------------------------------------------
-// k_move: stable partition of one level into the next, fused with (a) the smaller child's histogram
-// (when F <= 32: one LDS tile covers every feature) and (b) leaf bookkeeping for rows that stop here.
-// Each lane-group (8 lanes) owns UNR rows per step; all their loads are in flight before the single
-// block-wide prefix exchange of the step (one __syncthreads per RPI*UNR = 512 rows).
-template <bool HIST>
-__global__ __launch_bounds__(BLK, 4) void k_move(
-    const uint8_t* __restrict__ sbins, const float4* __restrict__ saux, const int* __restrict__ sridx /*nullable*/,
-    uint8_t* __restrict__ dbins, float4* __restrict__ daux, int* __restrict__ dridx,
-    int stride, int F, const Node* __restrict__ nodes, const int* __restrict__ tile_prefix,
-    const int* __restrict__ meta, const Dec* __restrict__ dec, const int* __restrict__ tile_off,
-    const int* __restrict__ node_nl, const int* __restrict__ child_l, const int* __restrict__ child_r,
-    const Node* __restrict__ next, double* __restrict__ hist_next, int slot_doubles,
-    int* __restrict__ leaf_of_row, double* __restrict__ leafsum /*[L][2]*/, const double* __restrict__ qs) {
-  // NOTE: the packed single-atomic histogram mode is NOT used here: measured on MI355X it made this
-  // (register-capped, 16-wave) kernel slower (590 -> 660 us/level) while it speeds up k_hist_build.
-  extern __shared__ __attribute__((aligned(16))) long long smem64[];
-  long long* h = smem64;
-  float* nayy = (float*)(smem64 + FTILE * HS64);
-  double* red = (double*)(nayy + FTILE);                      // 64 doubles
-  int* cnt = (int*)(red + 64);                                // [2 parity][MUNR][2 side][NW waves] + 130 prefix
-  Dec* sdec = (Dec*)(cnt + 2 * MUNR * 2 * NW + 132);          // current node's decision
-  const float sa = (float)qs[0], sb = (float)qs[1];
-
-  const int n_nodes = meta[0], n_tiles = meta[1];
-  if (n_nodes <= 0 || n_tiles <= 0) return;
-  const int per = (n_tiles + gridDim.x - 1) / gridDim.x;
-  const int t0 = blockIdx.x * per, t1 = min(n_tiles, t0 + per);
-  if (t0 >= t1) return;
-  const int W = stride >> 2;
-  const bool small = W <= LPR;       // whole row held by the 8 lanes of a group (one word each)
-  const int g = threadIdx.x / LPR, j = threadIdx.x % LPR;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int gl = lane & ~(LPR - 1);  // group leader lane within the wave
-  const unsigned long long below = (gl == 0) ? 0ull : ((1ull << gl) - 1ull);
-  const unsigned* sb32 = (const unsigned*)sbins;
-  unsigned* db32 = (unsigned*)dbins;
-  const float* sauxf = (const float*)saux;
-  float* dauxf = (float*)daux;
-
-  int cur = -1, build_child = -1, leafL = -1, leafR = -1;
-  double wyy = 0.0, sLn = 0.0, sLd = 0.0, sRn = 0.0, sRd = 0.0;
-  int parity = 0;
-
-  auto finish_node = [&]() {
-    double v[4] = {sLn, sLd, sRn, sRd};
-    block_sum4(v, red);
-    if (threadIdx.x == 0) {
-      if (leafL >= 0 && (v[0] != 0.0 || v[1] != 0.0)) { atomicAdd(leafsum + 2 * leafL, v[0]); atomicAdd(leafsum + 2 * leafL + 1, v[1]); }
-      if (leafR >= 0 && (v[2] != 0.0 || v[3] != 0.0)) { atomicAdd(leafsum + 2 * leafR, v[2]); atomicAdd(leafsum + 2 * leafR + 1, v[3]); }
-    }
-    if (HIST && build_child >= 0) {
-      double u[4] = {wyy, 0, 0, 0};
-      block_sum4(u, red);
-      __syncthreads();
-      flush_hist(h, nayy, u[0], 0, F, hist_next + (size_t)build_child * slot_doubles, qs, false);
-    }
-    __syncthreads();
-  };
-
-  for (int t = t0; t < t1; ++t) {
-    const int node = find_node(tile_prefix, n_nodes, t);
-    if (node != cur) {
-      if (cur >= 0) finish_node();
-      cur = node;
-      const int cl = child_l[node], cr = child_r[node];
-      const bool term = dec[node].feat < 0;
-      leafL = cl < 0 ? -1 - cl : -1;
-      leafR = (!term && cr < 0) ? -1 - cr : -1;
-      build_child = -1;
-      if (cl >= 0 && next[cl].build) build_child = cl;
-      if (cr >= 0 && next[cr].build) build_child = cr;
-      sLn = sLd = sRn = sRd = 0.0; wyy = 0.0;
-      if (HIST && build_child >= 0) {
-        lds_zero64(h, FTILE * HS64);
-        for (int i = threadIdx.x; i < FTILE; i += blockDim.x) nayy[i] = 0.f;
-      }
-      if (threadIdx.x < (int)(sizeof(Dec) / 4)) ((int*)sdec)[threadIdx.x] = ((const int*)(dec + node))[threadIdx.x];
-      __syncthreads();
-    }
-    const Node nd = nodes[node];
-    const int feat = sdec->feat;
-    const bool term = feat < 0;
-    const int cl = child_l[node], cr = child_r[node];
-    const int nl = node_nl[node];
-    const int tin = t - tile_prefix[node];
-    const int r0 = nd.start + tin * TILE;
-    const int r1 = min(r0 + TILE, nd.start + nd.len);
-    int runL = tile_off[t];                         // left rows before this tile (within node)
-    int runR = tin * TILE - tile_off[t];            // right rows before this tile
-    float wyf = 0.f, lLn = 0.f, lLd = 0.f, lRn = 0.f, lRd = 0.f;
-    for (int base = r0; base < r1; base += RPI * MUNR) {
-      unsigned wd[MUNR];
-      float av[MUNR];
-      int rid[MUNR];
-      unsigned lmask = 0u, vmask = 0u;   // bit u: row u goes left / row u valid
-#pragma unroll
-      for (int u = 0; u < MUNR; ++u) {
-        const int row = base + g + u * RPI;
-        const bool v = row < r1;
-        vmask |= v ? (1u << u) : 0u;
-        wd[u] = (v && small && j < W) ? sb32[(size_t)row * W + j] : 0u;
-        av[u] = (v && j < 4) ? sauxf[(size_t)row * 4 + j] : 0.f;
-        rid[u] = (v && j == 4) ? (sridx ? sridx[row] : row) : 0;
-      }
-      int* c = cnt + parity * (MUNR * 2 * NW);
-      int pre[MUNR];  // in-wave exclusive prefix of same-side rows (group leaders only)
-#pragma unroll
-      for (int u = 0; u < MUNR; ++u) {
-        const bool v = (vmask >> u) & 1u;
-        int bin = 0;
-        if (small) {
-          const unsigned w2 = __shfl(wd[u], gl + ((term ? 0 : feat) >> 2), 64);
-          bin = (w2 >> (8 * ((term ? 0 : feat) & 3))) & 0xFF;
-        } else if (v && !term) {
-          bin = sbins[(size_t)(base + g + u * RPI) * stride + feat];
-        }
-        const bool lf = v && (term || dec_go_left(sdec, bin));
-        lmask |= lf ? (1u << u) : 0u;
-        const unsigned long long mL = __ballot(lf && j == 0);
-        const unsigned long long mR = __ballot(v && !lf && j == 0);
-        pre[u] = lf ? __popcll(mL & below) : __popcll(mR & below);
-        if (lane == 0) { c[u * 2 * NW + wid] = __popcll(mL); c[u * 2 * NW + NW + wid] = __popcll(mR); }
-      }
-      __syncthreads();
-      // wave 0: exclusive scan over the (u, wave) order -> offsets; lane = u*NW + w (MUNR*NW <= 64)
-      if (wid == 0) {
-        const int u = lane / NW, w = lane % NW;
-        const bool in = u < MUNR;
-        const int vl = in ? c[u * 2 * NW + w] : 0, vr = in ? c[u * 2 * NW + NW + w] : 0;
-        int xl = vl, xr = vr;
-        for (int o = 1; o < 64; o <<= 1) {
-          const int yl = __shfl_up(xl, o, 64), yr = __shfl_up(xr, o, 64);
-          if (lane >= o) { xl += yl; xr += yr; }
-        }
-        int* q = cnt + 2 * MUNR * 2 * NW;           // parity-independent prefix area
-        q[lane] = xl - vl;                          // exclusive left prefix
-        q[64 + lane] = xr - vr;                     // exclusive right prefix
-        if (lane == 63) { q[128] = xl; q[129] = xr; }
-      }
-      __syncthreads();
-      const int* pfx = cnt + 2 * MUNR * 2 * NW;
-      const int totL = pfx[128], totR = pfx[129];
-      parity ^= 1;
-#pragma unroll
-      for (int u = 0; u < MUNR; ++u) {
-        const int row = base + g + u * RPI;
-        // group-wide shuffles (executed by every lane)
-        const float a_ = __shfl(av[u], gl + 0, 64);
-        const float b_ = __shfl(av[u], gl + 1, 64);
-        const float num = __shfl(av[u], gl + 2, 64);
-        const float den = __shfl(av[u], gl + 3, 64);
-        const int rr = __shfl(rid[u], gl + 4, 64);
-        const bool lf = (lmask >> u) & 1u;
-        if (!((vmask >> u) & 1u)) continue;
-        const int child = lf ? cl : cr;
-        if (child >= 0 && !term) {
-          const int k = u * NW + wid;
-          const int pos = lf ? (nd.start + runL + pfx[k] + pre[u]) : (nd.start + nl + runR + pfx[64 + k] + pre[u]);
-          if (small) {
-            if (j < W) db32[(size_t)pos * W + j] = wd[u];
-          } else {
-            for (int w = j; w < W; w += LPR) db32[(size_t)pos * W + w] = sb32[(size_t)row * W + w];
-          }
-          if (j < 4) dauxf[(size_t)pos * 4 + j] = av[u];
-          if (j == 4) dridx[pos] = rr;
-          if (HIST && child == build_child) {
-            const float yy = row_yy(a_, b_);
-            if (j == 0) wyf += yy;
-            if (j < W) hist_word(h, nayy, wd[u], j, j * 4, F, q64(a_, sa), q64(b_, sb), yy, false);
-          }
-        } else if (j == 0) {
-          // row stops here: leaf id in original order + Newton sums
-          const int leaf = term ? (-1 - cl) : (-1 - child);
-          leaf_of_row[rr] = leaf;
-          if (lf) { lLn += num; lLd += den; } else { lRn += num; lRd += den; }
-        }
-      }
-      runL += totL; runR += totR;
-    }
-    wyy += (double)wyf;
-    sLn += (double)lLn; sLd += (double)lLd; sRn += (double)lRn; sRd += (double)lRd;
+  const double* hb = hbuild + (size_t)nd.parent * slot_doubles;
+  if (nd.build) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < slot_doubles; i += gridDim.x * blockDim.x) s[i] = hb[i];
+    return;
   }
-  if (cur >= 0) finish_node();
+  const double* pa = hist_cur + (size_t)nd.parent * slot_doubles;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < slot_doubles; i += gridDim.x * blockDim.x)
+    s[i] = pa[i] - hb[i];
 }
 
 // ------------------------------------------------------------------------------------------------
 // k_move_lean: the stable partition WITHOUT the fused histogram (the smaller child is histogrammed
 // afterwards by k_hist_build over its now-contiguous rows). With no 128 KiB LDS histogram and one
-// row per lane the kernel is light enough for several 8-wave blocks per CU, so many more rows are
-// in flight than in the LDS-histogram-bound fused kernel.
+// row per lane the kernel is light enough for several 8-wave blocks per CU. (Measured: a partition
+// fused with the LDS histogram, one 16-wave block per CU, ran 590 us/level vs 287 + 139 split.)
 //   block = one TILE (2048 rows), 8 waves x 256 rows, lane = row (4 rows per lane);
 //   wave-level ballots give in-wave ranks, one LDS exchange gives each wave its offset in the tile,
 //   tile_off (k_plan) gives the tile's offset in its node: positions are stable.
@@ -1175,7 +994,7 @@ extern "C" {
 int h2o_tree_sizes(int* out) {
   out[7] = AMAX_SHARDS;
   out[0] = sizeof(Node); out[1] = sizeof(Dec); out[2] = sizeof(Cand); out[3] = TILE; out[4] = FTILE;
-  out[5] = HIST_LDS_BYTES + 64 * 8 + (2 * MUNR * 2 * NW + 132) * 4 + (int)sizeof(Dec);  // k_move LDS bytes
+  out[5] = HIST_LDS_BYTES + 64 * 8;  // k_hist_build LDS bytes
   out[6] = BLK;
   return 0;
 }
@@ -1237,34 +1056,12 @@ int h2o_zero_hist(void* hist, const void* next, const void* meta, int cap, int s
   return (int)hipGetLastError();
 }
 
-int h2o_subtract(void* hist_next, const void* hist_cur, const void* next, const void* meta, int cap,
-                 int slot_doubles, hipStream_t s) {
+int h2o_subtract(void* hist_next, const void* hist_cur, const void* hbuild, const void* next, const void* meta,
+                 int cap, int slot_doubles, hipStream_t s) {
   const int gx = (slot_doubles + 1023) / 1024;
   hipLaunchKernelGGL(k_subtract, dim3(gx < 64 ? gx : 64, cap), dim3(256), 0, s, (double*)hist_next,
-                     (const double*)hist_cur, (const Node*)next, (const int*)meta, slot_doubles);
-  return (int)hipGetLastError();
-}
-
-int h2o_move(const void* sbins, const void* saux, const void* sridx, void* dbins, void* daux, void* dridx,
-             int stride, int F, const void* nodes, const void* tile_prefix, const void* meta, const void* dec,
-             const void* tile_off, const void* node_nl, const void* child_l, const void* child_r, const void* next,
-             void* hist_next, int slot_doubles, void* leaf_of_row, void* leafsum, const void* qs, int fuse_hist,
-             int grid, int packed, hipStream_t s) {
-  (void)packed;  // k_move keeps the two-atomic histogram (see the note in k_move)
-  const size_t lds_h = HIST_LDS_BYTES + 64 * 8 + (2 * MUNR * 2 * NW + 132) * 4 + sizeof(Dec);
-  if (fuse_hist) {
-    hipLaunchKernelGGL(k_move<true>, dim3(grid), dim3(BLK), lds_h, s, (const uint8_t*)sbins, (const float4*)saux,
-                       (const int*)sridx, (uint8_t*)dbins, (float4*)daux, (int*)dridx, stride, F, (const Node*)nodes,
-                       (const int*)tile_prefix, (const int*)meta, (const Dec*)dec, (const int*)tile_off,
-                       (const int*)node_nl, (const int*)child_l, (const int*)child_r, (const Node*)next,
-                       (double*)hist_next, slot_doubles, (int*)leaf_of_row, (double*)leafsum, (const double*)qs);
-  } else {
-    hipLaunchKernelGGL(k_move<false>, dim3(grid), dim3(BLK), lds_h, s, (const uint8_t*)sbins, (const float4*)saux,
-                       (const int*)sridx, (uint8_t*)dbins, (float4*)daux, (int*)dridx, stride, F, (const Node*)nodes,
-                       (const int*)tile_prefix, (const int*)meta, (const Dec*)dec, (const int*)tile_off,
-                       (const int*)node_nl, (const int*)child_l, (const int*)child_r, (const Node*)next,
-                       (double*)hist_next, slot_doubles, (int*)leaf_of_row, (double*)leafsum, (const double*)qs);
-  }
+                     (const double*)hist_cur, (const double*)hbuild, (const Node*)next, (const int*)meta,
+                     slot_doubles);
   return (int)hipGetLastError();
 }
 

@@ -30,9 +30,7 @@ _HIP_SIGS = {
     "h2o_count": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p],
     "h2o_plan": [c_void_p] * 14 + [c_int, c_int, c_double, c_int, c_int, c_void_p, c_void_p],
     "h2o_zero_hist": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
-    "h2o_subtract": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
-    "h2o_move": [c_void_p] * 6 + [c_int, c_int] + [c_void_p] * 9 + [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int,
-                                                                     c_int, c_void_p],
+    "h2o_subtract": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
     "h2o_move_lean": [c_void_p] * 6 + [c_int] + [c_void_p] * 10 + [c_int, c_int, c_void_p],
     "h2o_bin_assign": [c_void_p, c_ll, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "h2o_amax": [c_void_p, c_ll, c_void_p, c_void_p],

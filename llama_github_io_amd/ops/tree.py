@@ -16,7 +16,6 @@ sorted by mean response. Mode 1 is XGBoost's Newton gain G²/(H+λ) with L1 soft
 from __future__ import annotations
 
 import math
-import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -384,6 +383,9 @@ class GpuTreeBuilder:
         self.slot = F * 2 * NBIN + F + 1
         self.slot += self.slot & 1
         self.hist = [torch.empty(capmax * self.slot, dtype=torch.float64, device=dev) for _ in range(2)]
+        # compact histograms of the BUILT children of a level, slot = parent index (<= caps[d] slots):
+        # the only histogram bytes a row-sharded run all-reduces per level
+        self.hbuild = torch.empty(max(self.caps[:D]) * self.slot, dtype=torch.float64, device=dev)
         self.tiles_cap = [(N + T - 1) // T + c for c in self.caps]
         tmax = max(self.tiles_cap)
         self.tile_cnt = torch.empty(tmax, dtype=torch.int32, device=dev)
@@ -430,9 +432,6 @@ class GpuTreeBuilder:
         self.av["tp0"][:8].copy_(torch.from_numpy(np.array([0, n_tiles0], dtype=np.int32).view(np.uint8)))
         self.av["bp0"][:8].copy_(torch.from_numpy(np.array([0, n_tiles0], dtype=np.int32).view(np.uint8)))
         self.history = []
-        # partition strategy: "lean" (partition-only kernel + separate smaller-child histogram) or
-        # "fused" (partition fused with the LDS histogram, one block per CU)
-        self.lean = os.environ.get("H2O_TREE_MOVE", "lean") == "lean"
 
     def _p(self, name):
         return self.av[name].data_ptr()
@@ -492,35 +491,26 @@ class GpuTreeBuilder:
                                    self._p(f"meta{d + 1}"), self._p("counters"), self.scratch.data_ptr(), d, D,
                                    p.min_w, self.caps[d + 1], self.leaf_cap, self._p(f"bp{d + 1}"), s), "plan")
             last = d + 1 == D
+            hb = self.hbuild
             if not last:
-                nat.check(lib.h2o_zero_hist(hn.data_ptr(), self._p(f"nodes{d + 1}"), self._p(f"meta{d + 1}"),
+                nat.check(lib.h2o_zero_hist(hb.data_ptr(), self._p(f"nodes{d + 1}"), self._p(f"meta{d + 1}"),
                                             self.caps[d + 1], slot, s), "zero_hist")
-            fuse = (F <= FTILE) and not last and not self.lean
-            g = min(self.tiles_cap[d], self.grid)
-            if self.lean:
-                # partition-only pass (high occupancy, no LDS histogram); the smaller child is
-                # histogrammed below over its contiguous rows
-                nat.check(lib.h2o_move_lean(sb, sa, sr, dst["bins"].data_ptr(), dst["aux"].data_ptr(),
-                                            dst["ridx"].data_ptr(), self.stride, self._p(f"nodes{d}"), self._p(f"tp{d}"),
-                                            self._p(f"meta{d}"), self._p(f"dec{d}"), self.tile_off.data_ptr(),
-                                            self._p(f"nl{d}"), self._p(f"cl{d}"), self._p(f"cr{d}"),
-                                            self.leaf_of_row.data_ptr(), self.leafsum.data_ptr(), int(not last),
-                                            self.tiles_cap[d], s), "move_lean")
-            else:
-                nat.check(lib.h2o_move(sb, sa, sr, dst["bins"].data_ptr(), dst["aux"].data_ptr(), dst["ridx"].data_ptr(),
-                                       self.stride, F, self._p(f"nodes{d}"), self._p(f"tp{d}"), self._p(f"meta{d}"),
-                                       self._p(f"dec{d}"), self.tile_off.data_ptr(), self._p(f"nl{d}"), self._p(f"cl{d}"),
-                                       self._p(f"cr{d}"), self._p(f"nodes{d + 1}"), hn.data_ptr(), slot,
-                                       self.leaf_of_row.data_ptr(), self.leafsum.data_ptr(), qs, int(fuse), g, pk, s),
-                          "move")
-            if not last and not fuse:
+            # partition-only pass (high occupancy, no LDS histogram); the smaller child is
+            # histogrammed below over its contiguous rows
+            nat.check(lib.h2o_move_lean(sb, sa, sr, dst["bins"].data_ptr(), dst["aux"].data_ptr(),
+                                        dst["ridx"].data_ptr(), self.stride, self._p(f"nodes{d}"), self._p(f"tp{d}"),
+                                        self._p(f"meta{d}"), self._p(f"dec{d}"), self.tile_off.data_ptr(),
+                                        self._p(f"nl{d}"), self._p(f"cl{d}"), self._p(f"cr{d}"),
+                                        self.leaf_of_row.data_ptr(), self.leafsum.data_ptr(), int(not last),
+                                        self.tiles_cap[d], s), "move_lean")
+            if not last:
                 nat.check(lib.h2o_hist_build(dst["bins"].data_ptr(), self.stride, dst["aux"].data_ptr(),
                                              self._p(f"nodes{d + 1}"), self._p(f"bp{d + 1}"), self._p(f"meta{d + 1}"),
-                                             F, hn.data_ptr(), slot, qs, min(self.tiles_cap[d + 1], self.grid), pk, s),
+                                             F, hb.data_ptr(), slot, qs, min(self.tiles_cap[d + 1], self.grid), pk, s),
                           "hist_build")
-            if not last:
-                coll.all_reduce_(hn[: self.caps[d + 1] * slot])
-                nat.check(lib.h2o_subtract(hn.data_ptr(), hc.data_ptr(), self._p(f"nodes{d + 1}"),
+                # one built child per parent: the compact buffer holds at most caps[d] slots
+                coll.all_reduce_(hb[: self.caps[d] * slot])
+                nat.check(lib.h2o_subtract(hn.data_ptr(), hc.data_ptr(), hb.data_ptr(), self._p(f"nodes{d + 1}"),
                                            self._p(f"meta{d + 1}"), self.caps[d + 1], slot, s), "subtract")
         coll.all_reduce_(self.leafsum)
         if leaf_fn is not None:
