@@ -36,7 +36,7 @@
 #define RPI (BLK / LPR)         // rows per iteration (128)
 
 struct Node {      // one active node of a level (rows [start, start+len) of the level's buffer)
-  int start, len, build, parent, sib, pad0, pad1, pad2;
+  int start, len, build, parent, sib, dir /*odd levels: 0 left / 1 right child*/, pad1, pad2;
 };
 
 struct Dec {       // split decision (80 B)
@@ -194,26 +194,51 @@ __device__ __forceinline__ float row_yy(float a, float b) {
   return a > 0.f ? b * b * __builtin_amdgcn_rcpf(a) : 0.f;
 }
 
+// Parent-decision filter of an odd-level histogram (k_hist_build<true>): only rows of the parent's
+// range that go to `dir` are accumulated; `count` lanes tally the parent's left-goers.
+struct RowFilter {
+  const Dec* pd;   // parent decision (LDS copy)
+  int feat;        // its split feature
+  int jw;          // lane (within the 8-lane row group) whose word holds `feat`, or -1: load the byte
+  int dir;         // 0: accumulate left-goers, 1: right-goers
+  bool count;
+};
+
 // Histogram rows [r0, r1) of one node into LDS. Loads for UNR rows are issued before any atomic.
+template <bool FILT>
 __device__ __forceinline__ void hist_rows(long long* h, float* nayy, const unsigned* __restrict__ bins32,
                                           const float4* __restrict__ aux, int W, int wabs, int F, bool lead,
                                           int r0, int r1, int g, int j, float& wyy, float sa, float sb, float sp,
-                                          bool packed) {
+                                          bool packed, const RowFilter& flt, int& lcnt) {
   const float2* aux2 = (const float2*)aux;
+  const int lane = threadIdx.x & 63;
   for (int base = r0; base < r1; base += RPI * UNR) {
     unsigned wd[UNR];
     float2 ab[UNR];
+    int sbyte[UNR];
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
       const int row = base + g + u * RPI;
       const bool v = row < r1;
       ab[u] = v ? aux2[(size_t)row * 2] : make_float2(0.f, 0.f);
       wd[u] = (v && wabs < W) ? bins32[(size_t)row * W + wabs] : 0u;
+      if (FILT && flt.jw < 0) sbyte[u] = v ? ((const uint8_t*)bins32)[(size_t)row * W * 4 + flt.feat] : 0;
+    }
+    if (FILT && flt.jw >= 0) {
+      // the split feature's byte is in lane jw's word of the same row group: one cross-lane read
+#pragma unroll
+      for (int u = 0; u < UNR; ++u)
+        sbyte[u] = (__shfl(wd[u], (lane & ~(LPR - 1)) + flt.jw, 64) >> (8 * (flt.feat & 3))) & 0xFF;
     }
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
       const int row = base + g + u * RPI;
       if (row < r1) {
+        if (FILT) {
+          const bool gl = dec_go_left(flt.pd, sbyte[u]);
+          if (flt.count) lcnt += gl ? 1 : 0;
+          if ((gl ? 0 : 1) != flt.dir) continue;
+        }
         const float yy = row_yy(ab[u].x, ab[u].y);
         if (lead) wyy += yy;
         if (wabs < W) {
@@ -226,13 +251,17 @@ __device__ __forceinline__ void hist_rows(long long* h, float* nayy, const unsig
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_hist_build: histograms of all nodes with build==1 of a level (root, or F>32 path).
+// k_hist_build: histograms of all nodes with build==1 of a level into the compact build buffer.
 // grid = (G, n_ftiles); each block takes a contiguous range of tiles so it flushes rarely.
+// FILT (odd levels): a node's tiles cover its PARENT's rows; only rows the parent's decision sends to
+// this child are accumulated, and ftile-0 blocks add the parent's left-going row count to nl_out.
+template <bool FILT>
 __global__ __launch_bounds__(BLK) void k_hist_build(
     const uint8_t* __restrict__ bins, int stride /*bytes per row, multiple of 4*/,
     const float4* __restrict__ aux, const Node* __restrict__ nodes, const int* __restrict__ tile_prefix,
     const int* __restrict__ meta /*[0]=n_nodes [1]=n_tiles*/, int F, double* __restrict__ hist, int slot_doubles,
-    const double* __restrict__ qs /*[sa, sb, 1/sa, 1/sb, sp, 1/sp]*/, int packed_i) {
+    const double* __restrict__ qs /*[sa, sb, 1/sa, 1/sb, sp, 1/sp]*/, int packed_i,
+    const Dec* __restrict__ pdec, int* __restrict__ nl_out) {
   const bool packed = packed_i != 0;
   extern __shared__ __attribute__((aligned(16))) long long smem64[];
   long long* h = smem64;                                 // FTILE * HS64
@@ -253,6 +282,9 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
   const unsigned* bins32 = (const unsigned*)bins;
   const float sa = (float)qs[0], sb = (float)qs[1], sp = (float)qs[4];
 
+  __shared__ Dec spd;
+  RowFilter flt{&spd, 0, -1, 0, false};
+  int lcnt = 0;
   int cur = -1, since = 0;
   double wyy = 0.0;
   for (int t = t0; t < t1; ++t) {
@@ -265,29 +297,42 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
     // new node, or (packed) the flush window is full: flush the LDS tile and restart it
     if (hslot != cur || (packed && since + (r1 - r0) > PACK_MAX)) {
       if (cur >= 0) {
-        double v[4] = {wyy, 0, 0, 0};
+        double v[4] = {wyy, (double)lcnt, 0, 0};
         block_sum4(v, red);
         __syncthreads();
         flush_hist(h, nayy, v[0], ftile, F, hist + (size_t)cur * slot_doubles, qs, packed);
+        if (FILT && threadIdx.x == 0 && v[1] != 0.0) atomicAdd(nl_out + cur, (int)v[1]);
         __syncthreads();
       }
       lds_zero64(h, FTILE * HS64);
       for (int i = threadIdx.x; i < FTILE; i += blockDim.x) nayy[i] = 0.f;
+      if (FILT && threadIdx.x < (int)(sizeof(Dec) / 4))
+        ((int*)&spd)[threadIdx.x] = ((const int*)(pdec + nd.parent))[threadIdx.x];
       wyy = 0.0;
+      lcnt = 0;
       since = 0;
       cur = hslot;
       __syncthreads();
+      if (FILT) {
+        flt.feat = spd.feat;
+        const int jw = (spd.feat >> 2) - ftile * LPR;
+        flt.jw = (jw >= 0 && jw < LPR) ? jw : -1;
+        flt.dir = nd.dir;
+        flt.count = ftile == 0 && j == 0;
+      }
     }
     since += r1 - r0;
     float wf = 0.f;
-    hist_rows(h, nayy, bins32, aux, W, wabs, F, j == 0 && ftile == 0, r0, r1, g, j, wf, sa, sb, sp, packed);
+    hist_rows<FILT>(h, nayy, bins32, aux, W, wabs, F, j == 0 && ftile == 0, r0, r1, g, j, wf, sa, sb, sp, packed,
+                    flt, lcnt);
     wyy += (double)wf;
   }
   if (cur >= 0) {
-    double v[4] = {wyy, 0, 0, 0};
+    double v[4] = {wyy, (double)lcnt, 0, 0};
     block_sum4(v, red);
     __syncthreads();
     flush_hist(h, nayy, v[0], ftile, F, hist + (size_t)cur * slot_doubles, qs, packed);
+    if (FILT && threadIdx.x == 0 && v[1] != 0.0) atomicAdd(nl_out + cur, (int)v[1]);
   }
 }
 
@@ -537,35 +582,6 @@ __global__ __launch_bounds__(64) void k_split_reduce(
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_count: rows going left per tile (one tile per block). Terminal nodes: whole tile counts as left.
-__global__ __launch_bounds__(256) void k_count(
-    const uint8_t* __restrict__ bins, int stride, const Node* __restrict__ nodes,
-    const int* __restrict__ tile_prefix, const int* __restrict__ meta, const Dec* __restrict__ dec,
-    int* __restrict__ tile_cnt) {
-  const int t = blockIdx.x;
-  const int n_nodes = meta[0], n_tiles = meta[1];
-  if (t >= n_tiles) return;
-  const int node = find_node(tile_prefix, n_nodes, t);
-  const Node nd = nodes[node];
-  const int r0 = nd.start + (t - tile_prefix[node]) * TILE;
-  const int r1 = min(r0 + TILE, nd.start + nd.len);
-  const Dec* d = dec + node;
-  const int feat = d->feat;
-  int cnt = 0;
-  if (feat < 0) {
-    cnt = (threadIdx.x == 0) ? (r1 - r0) : 0;
-  } else {
-    for (int row = r0 + threadIdx.x; row < r1; row += blockDim.x)
-      cnt += dec_go_left(d, bins[(size_t)row * stride + feat]) ? 1 : 0;
-  }
-  cnt = wave_sum_i(cnt);
-  __shared__ int s[4];
-  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = cnt;
-  __syncthreads();
-  if (threadIdx.x == 0) tile_cnt[t] = s[0] + s[1] + s[2] + s[3];
-}
-
-// ------------------------------------------------------------------------------------------------
 // Block-wide exclusive scan helper for k_plan (1024 threads, int values). Returns exclusive prefix
 // of `v` for this thread and writes the block total into *total.
 __device__ int block_excl_scan(int v, int* sh /*>=17*/, int* total) {
@@ -589,50 +605,74 @@ __device__ int block_excl_scan(int v, int* sh /*>=17*/, int* total) {
   return res;
 }
 
-// k_plan: one block. Turns per-tile left counts into stable partition offsets, numbers the children
-// (compacted, capacity-limited) and the new leaves, chooses which child is histogrammed, and builds
-// the next level's node list + tile prefix. meta: [0]=n_nodes [1]=n_tiles. counters: [0]=n_leaves.
+// Tile prefix of a level's node list: every node owns ceil(len/TILE) tiles (tp); build nodes also
+// own tiles in the build prefix (bp) that k_hist_build walks. meta: [0]=nodes [1]=tiles [2]=build tiles.
+__device__ void level_tile_prefix(const Node* __restrict__ next, int nn, int* __restrict__ tp,
+                                  int* __restrict__ bp, int* __restrict__ meta, int* sh) {
+  const int T = blockDim.x, tid = threadIdx.x;
+  const int per = (nn + T - 1) / T;
+  const int a = min(nn, tid * per), b = min(nn, a + per);
+  int s = 0, sbt = 0;
+  for (int i = a; i < b; ++i) {
+    const int k = (next[i].len + TILE - 1) / TILE;
+    s += k;
+    sbt += next[i].build ? k : 0;
+  }
+  int total, totalb;
+  int off = block_excl_scan(s, sh, &total);
+  int offb = block_excl_scan(sbt, sh, &totalb);
+  for (int i = a; i < b; ++i) {
+    const int k = (next[i].len + TILE - 1) / TILE;
+    tp[i] = off; off += k;
+    bp[i] = offb; offb += next[i].build ? k : 0;
+  }
+  if (tid == 0) {
+    tp[nn] = total; bp[nn] = totalb;
+    meta[0] = nn; meta[1] = total; meta[2] = totalb;
+  }
+}
+
+// k_plan: one block. Numbers the children of a level (compacted, capacity-limited) and the new
+// leaves, chooses which child is histogrammed (the lighter one by GLOBAL weight, so every rank of a
+// row-sharded run plans alike) and writes the next level's node list.
+// Rows are regrouped only every SECOND level (see k_route), so the node list alternates between
+//   * even levels: nodes own contiguous row ranges [start, start+len) of the level's buffer;
+//   * odd levels: nodes are the two halves of their parent's range (start/len = the parent's, `dir`
+//     = 0 left / 1 right); k_hist_build filters the parent's rows by the parent's decision.
+// Even depth (next level odd): next ranges = parent ranges, tile prefix built here; node_nl is zeroed
+//   for the filtered histogram pass to count left-goers into.
+// Odd depth (next level even): the children's ranges are only known after k_route, which fills each
+//   odd node's region of the next buffer from both ends; this kernel sets up those cursors
+//   (curs[c] = {front, back, region start, region end}, from the parent's left count prev_nl) and
+//   k_ranges turns the final cursors into ranges + tile prefix.
 __global__ __launch_bounds__(1024) void k_plan(
-    const Node* __restrict__ nodes, const int* __restrict__ meta, const int* __restrict__ tile_prefix,
-    const int* __restrict__ tile_cnt, const Dec* __restrict__ dec,
-    int* __restrict__ tile_off, int* __restrict__ node_nl, int* __restrict__ child_l, int* __restrict__ child_r,
+    const Node* __restrict__ nodes, const int* __restrict__ meta, const Dec* __restrict__ dec,
+    int* __restrict__ node_nl, const int* __restrict__ prev_nl, int4* __restrict__ curs,
+    int* __restrict__ child_l, int* __restrict__ child_r,
     Node* __restrict__ next, int* __restrict__ next_tile_prefix, int* __restrict__ next_meta,
     int* __restrict__ next_build_prefix,
-    int* __restrict__ counters, int* __restrict__ scratch /* >= 2*cap_cur ints */,
+    int* __restrict__ counters, int* __restrict__ scratch /* >= cap_cur ints */,
     int depth, int max_depth, double min_w, int cap_next, int leaf_cap) {
   __shared__ int sh[17];
-  const int n = meta[0], nt = meta[1];
+  const int n = meta[0];
   const int T = blockDim.x, tid = threadIdx.x;
+  const bool odd = depth & 1;
   int total;
-  // 1. global exclusive scan of tile counts
-  {
-    const int per = (nt + T - 1) / T;
-    const int a = min(nt, tid * per), b = min(nt, a + per);
-    int s = 0;
-    for (int i = a; i < b; ++i) s += tile_cnt[i];
-    int off = block_excl_scan(s, sh, &total);
-    for (int i = a; i < b; ++i) { const int c = tile_cnt[i]; tile_off[i] = off; off += c; }
-  }
-  __syncthreads();
-  // 2. per-node left totals and base offsets (scratch[0..n) = base)
-  {
-    for (int i = tid; i < n; i += T) {
-      const int ta = tile_prefix[i], tb = tile_prefix[i + 1];
-      const int base = (ta < nt) ? tile_off[ta] : total;
-      const int end = (tb < nt) ? tile_off[tb] : total;
-      scratch[i] = base;
-      node_nl[i] = end - base;
-    }
-  }
-  __syncthreads();
-  for (int t = tid; t < nt; t += T) {
-    const int node = find_node(tile_prefix, n, t);
-    tile_off[t] -= scratch[node];
-  }
-  __syncthreads();
-  // 3. children: active / leaf classification, compaction with capacity
   const int perN = (n + T - 1) / T;
   const int na = min(n, tid * perN), nb2 = min(n, na + perN);
+  // per-node bookkeeping of the CURRENT level
+  for (int i = na; i < nb2; ++i) {
+    const Node nd = nodes[i];
+    if (!odd) {
+      node_nl[i] = 0;
+    } else {
+      const int nl = nd.parent >= 0 ? prev_nl[nd.parent] : 0;
+      const int cs = nd.start + (nd.dir ? nl : 0);
+      const int ce = nd.dir ? nd.start + nd.len : nd.start + nl;
+      curs[i] = make_int4(cs, ce, cs, ce);
+    }
+  }
+  // 1. children: active / leaf classification, compaction with capacity
   int act_cnt = 0;
   for (int i = na; i < nb2; ++i) {
     const Dec d = dec[i];
@@ -645,7 +685,7 @@ __global__ __launch_bounds__(1024) void k_plan(
     act_cnt += a;
   }
   int act_off = block_excl_scan(act_cnt, sh, &total);
-  // recount leaves given capacity overflow, store flags in scratch[n + i] (bit0 left active, bit1 right active)
+  // recount leaves given capacity overflow, store flags in scratch[i] (bit0 left active, bit1 right active)
   int leaf_cnt = 0;
   {
     int ao = act_off;
@@ -660,7 +700,7 @@ __global__ __launch_bounds__(1024) void k_plan(
         if (ra) { if (ao < cap_next) flags |= 2; ++ao; }
         lv = 2 - ((flags & 1) + ((flags >> 1) & 1));
       }
-      scratch[n + i] = flags;
+      scratch[i] = flags;
       leaf_cnt += lv;
     }
   }
@@ -673,13 +713,12 @@ __global__ __launch_bounds__(1024) void k_plan(
   for (int i = na; i < nb2; ++i) {
     const Dec d = dec[i];
     const Node nd = nodes[i];
-    const int flags = scratch[n + i];
+    const int flags = scratch[i];
     if (d.feat < 0) {
       const int lid = min(lo++, leaf_cap - 1);
       child_l[i] = -1 - lid; child_r[i] = -1 - lid;
       continue;
     }
-    const int nl = node_nl[i], nr = nd.len - nl;
     const bool la = depth + 1 < max_depth && d.wl >= 2.0 * min_w;
     const bool ra = depth + 1 < max_depth && d.wr >= 2.0 * min_w;
     int li = -1, ri = -1;
@@ -687,53 +726,45 @@ __global__ __launch_bounds__(1024) void k_plan(
     if (ra) { if (flags & 2) ri = ao; ++ao; }
     child_l[i] = (li >= 0) ? li : -1 - min(lo++, leaf_cap - 1);
     child_r[i] = (ri >= 0) ? ri : -1 - min(lo++, leaf_cap - 1);
+    // children of an even node inherit its range (odd level); children of an odd node get theirs in k_ranges
     if (li >= 0 && ri >= 0) {
       const bool build_left = d.wl <= d.wr;  // global weights: identical choice on every rank
-      Node L = {nd.start, nl, build_left ? 1 : 0, i, build_left ? -1 : ri, 0, 0, 0};
-      Node R = {nd.start + nl, nr, build_left ? 0 : 1, i, build_left ? li : -1, 0, 0, 0};
-      next[li] = L; next[ri] = R;
+      next[li] = Node{nd.start, nd.len, build_left ? 1 : 0, i, build_left ? -1 : ri, 0, 0, 0};
+      next[ri] = Node{nd.start, nd.len, build_left ? 0 : 1, i, build_left ? li : -1, 1, 0, 0};
     } else if (li >= 0) {
-      Node L = {nd.start, nl, 1, i, -1, 0, 0, 0};
-      next[li] = L;
+      next[li] = Node{nd.start, nd.len, 1, i, -1, 0, 0, 0};
     } else if (ri >= 0) {
-      Node R = {nd.start + nl, nr, 1, i, -1, 0, 0, 0};
-      next[ri] = R;
+      next[ri] = Node{nd.start, nd.len, 1, i, -1, 1, 0, 0};
     }
   }
   __syncthreads();
-  const int n_next = min(act_off + act_cnt, cap_next);  // only the last thread's value is the full total
   __shared__ int s_nnext;
-  if (tid == T - 1) s_nnext = min(act_off + act_cnt, cap_next);
+  if (tid == T - 1) s_nnext = min(act_off + act_cnt, cap_next);  // only the last thread holds the total
   __syncthreads();
   const int nn = s_nnext;
-  (void)n_next;
-  // 4. next-level tile prefix
-  {
-    const int per = (nn + T - 1) / T;
-    const int a = min(nn, tid * per), b = min(nn, a + per);
-    int s = 0, sbt = 0;
-    for (int i = a; i < b; ++i) {
-      const int k = (next[i].len + TILE - 1) / TILE;
-      s += k;
-      sbt += next[i].build ? k : 0;
-    }
-    int off = block_excl_scan(s, sh, &total);
-    int totalb = 0;
-    int offb = block_excl_scan(sbt, sh, &totalb);
-    for (int i = a; i < b; ++i) {
-      const int k = (next[i].len + TILE - 1) / TILE;
-      next_tile_prefix[i] = off; off += k;
-      next_build_prefix[i] = offb; offb += next[i].build ? k : 0;
-    }
-    if (tid == 0) {
-      next_tile_prefix[nn] = total;
-      next_build_prefix[nn] = totalb;
-      next_meta[0] = nn;
-      next_meta[1] = total;
-      next_meta[2] = totalb;
-      counters[0] = min(leaf_base0 + n_leaves_new, leaf_cap);
-    }
+  if (tid == 0) counters[0] = min(leaf_base0 + n_leaves_new, leaf_cap);
+  if (!odd) {
+    level_tile_prefix(next, nn, next_tile_prefix, next_build_prefix, next_meta, sh);
+  } else if (tid == 0) {
+    next_meta[0] = nn; next_meta[1] = 0; next_meta[2] = 0;
   }
+}
+
+// k_ranges: after k_route filled the odd level's regions, give each even-level node its range
+// (left child: [region start, front); right child: [back, region end)) and build the tile prefix.
+__global__ __launch_bounds__(1024) void k_ranges(Node* __restrict__ next, const int4* __restrict__ curs,
+                                                 int* __restrict__ tp, int* __restrict__ bp, int* __restrict__ meta) {
+  __shared__ int sh[17];
+  const int nn = meta[0];
+  for (int i = threadIdx.x; i < nn; i += blockDim.x) {
+    Node nd = next[i];
+    const int4 c = curs[nd.parent];
+    if (nd.dir == 0) { nd.start = c.z; nd.len = c.x - c.z; }
+    else { nd.start = c.y; nd.len = c.w - c.y; }
+    next[i] = nd;
+  }
+  __syncthreads();
+  level_tile_prefix(next, nn, tp, bp, meta, sh);
 }
 
 // k_zero_hist: zero the compact build slots (slot = parent) of next-level nodes built directly.
@@ -765,83 +796,131 @@ __global__ void k_subtract(double* __restrict__ hist_next, const double* __restr
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_move_lean: the stable partition WITHOUT the fused histogram (the smaller child is histogrammed
-// afterwards by k_hist_build over its now-contiguous rows). With no 128 KiB LDS histogram and one
-// row per lane the kernel is light enough for several 8-wave blocks per CU. (Measured: a partition
-// fused with the LDS histogram, one 16-wave block per CU, ran 590 us/level vs 287 + 139 split.)
-//   block = one TILE (2048 rows), 8 waves x 256 rows, lane = row (4 rows per lane);
-//   wave-level ballots give in-wave ranks, one LDS exchange gives each wave its offset in the tile,
-//   tile_off (k_plan) gives the tile's offset in its node: positions are stable.
-#define LW 8              // waves per lean-move block
+// k_route: regroups the rows of an EVEN level e two levels down at once (TWO) and does the leaf
+// bookkeeping of every row that stops on the way. Rows are physically moved only every second level:
+// level e+1 is histogrammed by filtering the level-e ranges (k_hist_build<true>), so a depth-6 tree
+// moves its rows twice instead of five times and needs no separate counting pass.
+//   block = one TILE (2048 rows) of a level-e node; 8 waves x 256 rows, lane = row (4 rows per lane).
+//   Each row gets a slot q = 2*dirA + dirB (its grandchild); rows of a continuing grandchild move into
+//   the region of their level-(e+1) node: left grandchildren fill it from the front, right ones from the
+//   back (one atomic per (tile, slot) on curs); rows that reach a leaf write leaf_of_row (original row
+//   order, through ridx) and add their (gamma_num, gamma_den) to the leaf sums.
+// Order inside a region is not preserved: histograms are fixed-point integer sums (order independent)
+// and nothing else depends on the row order within a node.
+// !TWO: route one level only (final pass of a tree whose last level is even). !MOVE: final pass, every
+// row lands on a leaf.
+#define LW 8              // waves per route block
 #define LROWS (TILE / LW) // rows per wave (256)
 #define LU (LROWS / 64)   // rows per lane (4)
 #define LMAXW 16          // max words (64 features) kept in registers per row on the fast path
 
-template <bool MOVE>
-__global__ __launch_bounds__(LW * 64) void k_move_lean(
+template <bool TWO, bool MOVE>
+__global__ __launch_bounds__(LW * 64) void k_route(
     const uint8_t* __restrict__ sbins, const float4* __restrict__ saux, const int* __restrict__ sridx,
     uint8_t* __restrict__ dbins, float4* __restrict__ daux, int* __restrict__ dridx, int stride,
-    const Node* __restrict__ nodes, const int* __restrict__ tile_prefix, const int* __restrict__ meta,
-    const Dec* __restrict__ dec, const int* __restrict__ tile_off, const int* __restrict__ node_nl,
-    const int* __restrict__ child_l, const int* __restrict__ child_r, int* __restrict__ leaf_of_row,
-    double* __restrict__ leafsum) {
-  const int n_nodes = meta[0], n_tiles = meta[1];
+    const Node* __restrict__ nodesA, const int* __restrict__ tpA, const int* __restrict__ metaA,
+    const Dec* __restrict__ decA, const int* __restrict__ clA, const int* __restrict__ crA,
+    const Dec* __restrict__ decB, const int* __restrict__ clB, const int* __restrict__ crB,
+    int4* __restrict__ curs, int* __restrict__ leaf_of_row, double* __restrict__ leafsum) {
+  const int n_nodes = metaA[0], n_tiles = metaA[1];
   const int t = blockIdx.x;
   if (t >= n_tiles) return;
-  __shared__ int sL[LW], sR[LW];
-  __shared__ double sred[4][LW];
-  __shared__ Dec sd;
-  const int node = find_node(tile_prefix, n_nodes, t);
-  const Node nd = nodes[node];
-  const int tin = t - tile_prefix[node];
+  __shared__ Dec sA, sB[2];
+  __shared__ int sC[2], sG[4], sLeaf[4], sBase[4];
+  __shared__ int sCnt[LW][4];
+  __shared__ double sred[8][LW];
+  const int node = find_node(tpA, n_nodes, t);
+  const Node nd = nodesA[node];
+  const int tin = t - tpA[node];
   const int r0 = nd.start + tin * TILE;
   const int r1 = min(r0 + TILE, nd.start + nd.len);
-  if (threadIdx.x < (int)(sizeof(Dec) / 4)) ((int*)&sd)[threadIdx.x] = ((const int*)(dec + node))[threadIdx.x];
+  constexpr int NI = (int)(sizeof(Dec) / 4);
+  if (threadIdx.x < NI) ((int*)&sA)[threadIdx.x] = ((const int*)(decA + node))[threadIdx.x];
+  if (threadIdx.x < 2) sC[threadIdx.x] = threadIdx.x == 0 ? clA[node] : crA[node];
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    // slot q -> grandchild (>= 0 continues) and leaf id (>= 0 when the slot ends in a leaf)
+    const int q = threadIdx.x, c = sC[q >> 1];
+    int g = -1, leaf = -1;
+    if (c < 0) leaf = -1 - c;
+    else if (TWO) { g = (q & 1) ? crB[c] : clB[c]; if (g < 0) leaf = -1 - g; }
+    sG[q] = g; sLeaf[q] = leaf;
+  }
+  if (TWO) {
+    for (int k = 0; k < 2; ++k) {
+      const int c = sC[k];
+      if (c >= 0 && threadIdx.x < NI) ((int*)&sB[k])[threadIdx.x] = ((const int*)(decB + c))[threadIdx.x];
+    }
+  }
   __syncthreads();
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int feat = sd.feat;
-  const bool term = feat < 0;
-  const int cl = child_l[node], cr = child_r[node];
-  const int W = stride >> 2;
+  const int featA = sA.feat;
   const int wbase = r0 + wid * LROWS;
-  // 1. decide every row; in-wave ranks
-  bool valid[LU], left[LU];
-  int rank[LU];
-  int cntL = 0, cntR = 0;
+  const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  // 1. route every row; in-wave ranks per slot
+  int q[LU], rank[LU];
+  bool mv[LU];
+  int cnt[4] = {0, 0, 0, 0};
 #pragma unroll
   for (int u = 0; u < LU; ++u) {
     const int row = wbase + u * 64 + lane;
-    valid[u] = row < r1;
-    bool lf = true;
-    if (valid[u] && !term) lf = dec_go_left(&sd, sbins[(size_t)row * stride + feat]);
-    left[u] = valid[u] && lf;
-    const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    const unsigned long long mL = __ballot(left[u]);
-    const unsigned long long mR = __ballot(valid[u] && !lf);
-    rank[u] = left[u] ? cntL + __popcll(mL & below) : cntR + __popcll(mR & below);
-    cntL += __popcll(mL);
-    cntR += __popcll(mR);
+    const bool valid = row < r1;
+    int dA = 0, dB = 0;
+    if (valid && featA >= 0) dA = dec_go_left(&sA, sbins[(size_t)row * stride + featA]) ? 0 : 1;
+    if (TWO && valid && sC[dA] >= 0) {
+      const Dec* b = &sB[dA];
+      const int fb = b->feat;
+      if (fb >= 0) dB = dec_go_left(b, sbins[(size_t)row * stride + fb]) ? 0 : 1;
+    }
+    q[u] = 2 * dA + dB;
+    mv[u] = MOVE && valid && sG[q[u]] >= 0;
+    rank[u] = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const bool mine = mv[u] && q[u] == k;
+      const unsigned long long bm = __ballot(mine);
+      if (mine) rank[u] = cnt[k] + __popcll(bm & below);
+      cnt[k] += __popcll(bm);
+    }
   }
-  if (lane == 0) { sL[wid] = cntL; sR[wid] = cntR; }
-  __syncthreads();
-  int offL = 0, offR = 0;
-  for (int w = 0; w < wid; ++w) { offL += sL[w]; offR += sR[w]; }
-  const int nl = node_nl[node];
-  const int baseL = nd.start + tile_off[t] + offL;
-  const int baseR = nd.start + nl + (tin * TILE - tile_off[t]) + offR;
-  // 2. move rows whose child continues; leaf bookkeeping for rows that stop
-  double lLn = 0, lLd = 0, lRn = 0, lRd = 0;
+  int off[4] = {0, 0, 0, 0};
+  if (MOVE) {
+    if (lane == 0) for (int k = 0; k < 4; ++k) sCnt[wid][k] = cnt[k];
+    __syncthreads();
+    if (threadIdx.x < 4) {
+      const int k = threadIdx.x;
+      int tot = 0;
+      for (int w = 0; w < LW; ++w) tot += sCnt[w][k];
+      int base = 0;
+      if (tot > 0) {
+        int4* cu = curs + sC[k >> 1];
+        base = (k & 1) ? atomicSub(&cu->y, tot) - tot : atomicAdd(&cu->x, tot);
+      }
+      sBase[k] = base;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      off[k] = sBase[k];
+      for (int w = 0; w < wid; ++w) off[k] += sCnt[w][k];
+    }
+  }
+  // 2. move continuing rows; leaf bookkeeping for rows that stop
+  double ls[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int has_leaf = 0;
+  const int W = stride >> 2;
   const unsigned* sb32 = (const unsigned*)sbins;
   unsigned* db32 = (unsigned*)dbins;
 #pragma unroll
   for (int u = 0; u < LU; ++u) {
-    if (!valid[u]) continue;
     const int row = wbase + u * 64 + lane;
-    const int child = left[u] ? cl : cr;
+    if (row >= r1) continue;
     const float4 a = saux[row];
     const int rr = sridx ? sridx[row] : row;
-    if (MOVE && child >= 0 && !term) {
-      const int pos = left[u] ? baseL + rank[u] : baseR + rank[u];
+    if (mv[u]) {
+      int pos = rank[u];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) if (q[u] == k) pos += off[k];
       const unsigned* src = sb32 + (size_t)row * W;
       unsigned* dst = db32 + (size_t)pos * W;
       if ((stride & 15) == 0 && stride <= 64) {      // 16-B aligned rows: vector copy
@@ -865,22 +944,25 @@ __global__ __launch_bounds__(LW * 64) void k_move_lean(
       daux[pos] = a;
       dridx[pos] = rr;
     } else {
-      const int leaf = term ? (-1 - cl) : (-1 - child);
-      leaf_of_row[rr] = leaf;
-      if (left[u]) { lLn += a.z; lLd += a.w; } else { lRn += a.z; lRd += a.w; }
+      int leaf = -1;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) if (q[u] == k) { leaf = sLeaf[k]; ls[2 * k] += a.z; ls[2 * k + 1] += a.w; }
+      if (leaf >= 0) leaf_of_row[rr] = leaf;
+      has_leaf = 1;
     }
   }
-  // 3. leaf sums: wave -> block -> one atomic pair per side
-  lLn = wave_sum_d(lLn); lLd = wave_sum_d(lLd); lRn = wave_sum_d(lRn); lRd = wave_sum_d(lRd);
-  if (lane == 0) { sred[0][wid] = lLn; sred[1][wid] = lLd; sred[2][wid] = lRn; sred[3][wid] = lRd; }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double v[4] = {0, 0, 0, 0};
-    for (int k = 0; k < 4; ++k) for (int w = 0; w < LW; ++w) v[k] += sred[k][w];
-    const int leafL = cl < 0 ? -1 - cl : -1;
-    const int leafR = (!term && cr < 0) ? -1 - cr : -1;
-    if (leafL >= 0 && (v[0] != 0.0 || v[1] != 0.0)) { atomicAdd(leafsum + 2 * leafL, v[0]); atomicAdd(leafsum + 2 * leafL + 1, v[1]); }
-    if (leafR >= 0 && (v[2] != 0.0 || v[3] != 0.0)) { atomicAdd(leafsum + 2 * leafR, v[2]); atomicAdd(leafsum + 2 * leafR + 1, v[3]); }
+  // 3. leaf sums: wave -> block -> one atomic pair per (tile, leaf)
+  if (__syncthreads_or(has_leaf)) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) ls[k] = wave_sum_d(ls[k]);
+    if (lane == 0) for (int k = 0; k < 8; ++k) sred[k][wid] = ls[k];
+    __syncthreads();
+    if (threadIdx.x < 4) {
+      const int k = threadIdx.x, leaf = sLeaf[k];
+      double vn = 0, vd = 0;
+      for (int w = 0; w < LW; ++w) { vn += sred[2 * k][w]; vd += sred[2 * k + 1][w]; }
+      if (leaf >= 0 && (vn != 0.0 || vd != 0.0)) { atomicAdd(leafsum + 2 * leaf, vn); atomicAdd(leafsum + 2 * leaf + 1, vd); }
+    }
   }
 }
 
@@ -1001,12 +1083,18 @@ int h2o_tree_sizes(int* out) {
 
 int h2o_hist_build(const void* bins, int stride, const void* aux, const void* nodes, const void* tile_prefix,
                    const void* meta, int F, void* hist, int slot_doubles, const void* qs, int grid, int packed,
-                   hipStream_t s) {
+                   const void* pdec, void* nl_out, hipStream_t s) {
   const int nft = (F + FTILE - 1) / FTILE;
   const size_t lds = HIST_LDS_BYTES + 64 * 8;
-  hipLaunchKernelGGL(k_hist_build, dim3(grid, nft), dim3(BLK), lds, s, (const uint8_t*)bins, stride,
-                     (const float4*)aux, (const Node*)nodes, (const int*)tile_prefix, (const int*)meta, F,
-                     (double*)hist, slot_doubles, (const double*)qs, packed);
+  if (pdec) {
+    hipLaunchKernelGGL(k_hist_build<true>, dim3(grid, nft), dim3(BLK), lds, s, (const uint8_t*)bins, stride,
+                       (const float4*)aux, (const Node*)nodes, (const int*)tile_prefix, (const int*)meta, F,
+                       (double*)hist, slot_doubles, (const double*)qs, packed, (const Dec*)pdec, (int*)nl_out);
+  } else {
+    hipLaunchKernelGGL(k_hist_build<false>, dim3(grid, nft), dim3(BLK), lds, s, (const uint8_t*)bins, stride,
+                       (const float4*)aux, (const Node*)nodes, (const int*)tile_prefix, (const int*)meta, F,
+                       (double*)hist, slot_doubles, (const double*)qs, packed, (const Dec*)nullptr, (int*)nullptr);
+  }
   return (int)hipGetLastError();
 }
 
@@ -1030,22 +1118,20 @@ int h2o_split_reduce(const void* cand, const void* meta, int cap, int F, const v
   return (int)hipGetLastError();
 }
 
-int h2o_count(const void* bins, int stride, const void* nodes, const void* tile_prefix, const void* meta,
-              const void* dec, void* tile_cnt, int tiles_cap, hipStream_t s) {
-  hipLaunchKernelGGL(k_count, dim3(tiles_cap), dim3(256), 0, s, (const uint8_t*)bins, stride, (const Node*)nodes,
-                     (const int*)tile_prefix, (const int*)meta, (const Dec*)dec, (int*)tile_cnt);
+int h2o_plan(const void* nodes, const void* meta, const void* dec, void* node_nl, const void* prev_nl, void* curs,
+             void* child_l, void* child_r, void* next, void* next_tile_prefix, void* next_meta, void* next_build_prefix,
+             void* counters, void* scratch, int depth, int max_depth, double min_w, int cap_next, int leaf_cap,
+             hipStream_t s) {
+  hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, s, (const Node*)nodes, (const int*)meta, (const Dec*)dec,
+                     (int*)node_nl, (const int*)prev_nl, (int4*)curs, (int*)child_l, (int*)child_r, (Node*)next,
+                     (int*)next_tile_prefix, (int*)next_meta, (int*)next_build_prefix, (int*)counters, (int*)scratch,
+                     depth, max_depth, min_w, cap_next, leaf_cap);
   return (int)hipGetLastError();
 }
 
-int h2o_plan(const void* nodes, const void* meta, const void* tile_prefix, const void* tile_cnt, const void* dec,
-             void* tile_off, void* node_nl, void* child_l, void* child_r, void* next, void* next_tile_prefix,
-             void* next_meta, void* counters, void* scratch, int depth, int max_depth, double min_w, int cap_next,
-             int leaf_cap, void* next_build_prefix, hipStream_t s) {
-  hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, s, (const Node*)nodes, (const int*)meta,
-                     (const int*)tile_prefix, (const int*)tile_cnt, (const Dec*)dec, (int*)tile_off, (int*)node_nl,
-                     (int*)child_l, (int*)child_r, (Node*)next, (int*)next_tile_prefix, (int*)next_meta,
-                     (int*)next_build_prefix,
-                     (int*)counters, (int*)scratch, depth, max_depth, min_w, cap_next, leaf_cap);
+int h2o_ranges(void* next, const void* curs, void* tp, void* bp, void* meta, hipStream_t s) {
+  hipLaunchKernelGGL(k_ranges, dim3(1), dim3(1024), 0, s, (Node*)next, (const int4*)curs, (int*)tp, (int*)bp,
+                     (int*)meta);
   return (int)hipGetLastError();
 }
 
@@ -1065,23 +1151,20 @@ int h2o_subtract(void* hist_next, const void* hist_cur, const void* hbuild, cons
   return (int)hipGetLastError();
 }
 
-int h2o_move_lean(const void* sbins, const void* saux, const void* sridx, void* dbins, void* daux, void* dridx,
-                  int stride, const void* nodes, const void* tile_prefix, const void* meta, const void* dec,
-                  const void* tile_off, const void* node_nl, const void* child_l, const void* child_r,
-                  void* leaf_of_row, void* leafsum, int move, int tiles_cap, hipStream_t s) {
-  if (move) {
-    hipLaunchKernelGGL(k_move_lean<true>, dim3(tiles_cap), dim3(LW * 64), 0, s, (const uint8_t*)sbins,
-                       (const float4*)saux, (const int*)sridx, (uint8_t*)dbins, (float4*)daux, (int*)dridx, stride,
-                       (const Node*)nodes, (const int*)tile_prefix, (const int*)meta, (const Dec*)dec,
-                       (const int*)tile_off, (const int*)node_nl, (const int*)child_l, (const int*)child_r,
-                       (int*)leaf_of_row, (double*)leafsum);
-  } else {
-    hipLaunchKernelGGL(k_move_lean<false>, dim3(tiles_cap), dim3(LW * 64), 0, s, (const uint8_t*)sbins,
-                       (const float4*)saux, (const int*)sridx, (uint8_t*)dbins, (float4*)daux, (int*)dridx, stride,
-                       (const Node*)nodes, (const int*)tile_prefix, (const int*)meta, (const Dec*)dec,
-                       (const int*)tile_off, (const int*)node_nl, (const int*)child_l, (const int*)child_r,
-                       (int*)leaf_of_row, (double*)leafsum);
-  }
+// two: route two levels (else one); move: regroup continuing rows into the destination buffers
+int h2o_route(const void* sbins, const void* saux, const void* sridx, void* dbins, void* daux, void* dridx,
+              int stride, const void* nodesA, const void* tpA, const void* metaA, const void* decA, const void* clA,
+              const void* crA, const void* decB, const void* clB, const void* crB, void* curs, void* leaf_of_row,
+              void* leafsum, int two, int move, int tiles_cap, hipStream_t s) {
+#define ROUTE_ARGS (const uint8_t*)sbins, (const float4*)saux, (const int*)sridx, (uint8_t*)dbins, (float4*)daux, \
+    (int*)dridx, stride, (const Node*)nodesA, (const int*)tpA, (const int*)metaA, (const Dec*)decA,          \
+    (const int*)clA, (const int*)crA, (const Dec*)decB, (const int*)clB, (const int*)crB, (int4*)curs,       \
+    (int*)leaf_of_row, (double*)leafsum
+  if (two && move) hipLaunchKernelGGL((k_route<true, true>), dim3(tiles_cap), dim3(LW * 64), 0, s, ROUTE_ARGS);
+  else if (two) hipLaunchKernelGGL((k_route<true, false>), dim3(tiles_cap), dim3(LW * 64), 0, s, ROUTE_ARGS);
+  else if (!move) hipLaunchKernelGGL((k_route<false, false>), dim3(tiles_cap), dim3(LW * 64), 0, s, ROUTE_ARGS);
+  else return (int)hipErrorInvalidValue;  // moving after a single level is never needed
+#undef ROUTE_ARGS
   return (int)hipGetLastError();
 }
 

@@ -23,15 +23,15 @@ c_int, c_ll, c_ull, c_double, c_void_p = ctypes.c_int, ctypes.c_longlong, ctypes
 _HIP_SIGS = {
     "h2o_tree_sizes": [c_void_p],
     "h2o_hist_build": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int,
-                       c_int, c_void_p],
+                       c_int, c_void_p, c_void_p, c_void_p],
     "h2o_split_find": [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_double, c_double,
                        c_double, c_double, c_double, c_int, c_int, c_ull, c_int, c_void_p, c_void_p],
     "h2o_split_reduce": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_ull, c_int, c_void_p, c_void_p],
-    "h2o_count": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p],
-    "h2o_plan": [c_void_p] * 14 + [c_int, c_int, c_double, c_int, c_int, c_void_p, c_void_p],
+    "h2o_plan": [c_void_p] * 14 + [c_int, c_int, c_double, c_int, c_int, c_void_p],
+    "h2o_ranges": [c_void_p] * 6,
     "h2o_zero_hist": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
     "h2o_subtract": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
-    "h2o_move_lean": [c_void_p] * 6 + [c_int] + [c_void_p] * 10 + [c_int, c_int, c_void_p],
+    "h2o_route": [c_void_p] * 6 + [c_int] + [c_void_p] * 12 + [c_int, c_int, c_int, c_void_p],
     "h2o_bin_assign": [c_void_p, c_ll, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "h2o_amax": [c_void_p, c_ll, c_void_p, c_void_p],
     "h2o_qscale": [c_void_p, c_void_p, c_void_p],

@@ -31,7 +31,7 @@ FTILE = 32
 AMAX_SHARDS = 64   # per-block |aux| maxima shards (csrc: AMAX_SHARDS)
 
 NODE_DT = np.dtype([("start", "<i4"), ("len", "<i4"), ("build", "<i4"), ("parent", "<i4"), ("sib", "<i4"),
-                    ("p0", "<i4"), ("p1", "<i4"), ("p2", "<i4")])
+                    ("dir", "<i4"), ("p1", "<i4"), ("p2", "<i4")])
 DEC_DT = np.dtype([("feat", "<i4"), ("bin", "<i4"), ("na_left", "<i4"), ("is_cat", "<i4"), ("bits", "<u4", (8,)),
                    ("gain", "<f8"), ("wl", "<f8"), ("wr", "<f8"), ("predl", "<f4"), ("predr", "<f4")])
 CAND_BYTES = 88
@@ -387,9 +387,6 @@ class GpuTreeBuilder:
         # the only histogram bytes a row-sharded run all-reduces per level
         self.hbuild = torch.empty(max(self.caps[:D]) * self.slot, dtype=torch.float64, device=dev)
         self.tiles_cap = [(N + T - 1) // T + c for c in self.caps]
-        tmax = max(self.tiles_cap)
-        self.tile_cnt = torch.empty(tmax, dtype=torch.int32, device=dev)
-        self.tile_off = torch.empty(tmax, dtype=torch.int32, device=dev)
         self.cand = torch.empty(capmax * F * CAND_BYTES, dtype=torch.uint8, device=dev)
         self.scratch = torch.empty(2 * capmax + 16, dtype=torch.int32, device=dev)
         self.leaf_cap = min(N + 1, 2 * sum(self.caps) + 2)
@@ -416,7 +413,8 @@ class GpuTreeBuilder:
             ar.add(f"dec{d}", c * DEC_DT.itemsize)
             ar.add(f"cl{d}", c * 4)
             ar.add(f"cr{d}", c * 4)
-            ar.add(f"nl{d}", c * 4)
+            ar.add(f"nl{d}", c * 4)                # even levels: rows going left (filled by the odd-level histogram)
+            ar.add(f"cur{d}", c * 16)              # odd levels: region cursors {front, back, start, end}
         ar.add("counters", 16)
         ar.add("leafval", self.leaf_cap * 4)
         self.arena = torch.zeros(ar.off, dtype=torch.uint8, device=dev)
@@ -461,57 +459,76 @@ class GpuTreeBuilder:
         qs = self.qs.data_ptr()
         g0 = min(self.tiles_cap[0], self.grid)
         nat.check(lib.h2o_hist_build(self.master.data_ptr(), self.stride, aux_static.data_ptr(), self._p("nodes0"),
-                                     self._p("bp0"), self._p("meta0"), F, self.hist[0].data_ptr(), slot, qs, g0, pk, s),
+                                     self._p("bp0"), self._p("meta0"), F, self.hist[0].data_ptr(), slot, qs, g0, pk,
+                                     0, 0, s),
                   "hist_build")
         coll.all_reduce_(self.hist[0][:slot])
         self.root_w = self.hist[0][0:2 * NBIN:2].sum().reshape(1)   # Σw over feature 0's bins = root weight
         mono = 0 if self.mono_f is None else self.mono_f.data_ptr()
         seed = int(seed) & _M64
+        hb = self.hbuild
+
+        def level_buf(e):
+            # rows are regrouped every second level: level e (even) lives in the master order (e == 0)
+            # or in ping-pong buffer (e/2 - 1) % 2
+            if e == 0:
+                return self.master.data_ptr(), aux_static.data_ptr(), 0
+            b = self.bufs[(e // 2 - 1) % 2]
+            return b["bins"].data_ptr(), b["aux"].data_ptr(), b["ridx"].data_ptr()
+
+        def route(e, two, move):
+            sb, sa, sr = level_buf(e)
+            dst = self.bufs[(e // 2) % 2]
+            b1 = e + 1 if two else e
+            nat.check(lib.h2o_route(sb, sa, sr, dst["bins"].data_ptr(), dst["aux"].data_ptr(), dst["ridx"].data_ptr(),
+                                    self.stride, self._p(f"nodes{e}"), self._p(f"tp{e}"), self._p(f"meta{e}"),
+                                    self._p(f"dec{e}"), self._p(f"cl{e}"), self._p(f"cr{e}"), self._p(f"dec{b1}"),
+                                    self._p(f"cl{b1}"), self._p(f"cr{b1}"), self._p(f"cur{b1}"),
+                                    self.leaf_of_row.data_ptr(), self.leafsum.data_ptr(), int(two), int(move),
+                                    self.tiles_cap[e], s), "route")
+
         for d in range(D):
-            if d == 0:
-                sb, sa, sr = self.master.data_ptr(), aux_static.data_ptr(), 0
-            else:
-                b = self.bufs[(d - 1) % 2]
-                sb, sa, sr = b["bins"].data_ptr(), b["aux"].data_ptr(), b["ridx"].data_ptr()
-            dst = self.bufs[d % 2]
             hc, hn = self.hist[d % 2], self.hist[(d + 1) % 2]
             cap = self.caps[d]
+            odd = d % 2 == 1
             nat.check(lib.h2o_split_find(hc.data_ptr(), slot, self._p(f"meta{d}"), cap, F, self.nbins_f.data_ptr(),
                                          self.iscat_f.data_ptr(), mono, p.min_w, p.min_split_improvement, p.lam,
                                          p.alpha, p.gamma, p.mode, int(p.random_split), seed, d,
                                          self.cand.data_ptr(), s), "split_find")
             nat.check(lib.h2o_split_reduce(self.cand.data_ptr(), self._p(f"meta{d}"), cap, F, fo.data_ptr(), int(k_cols),
                                            seed, d, self._p(f"dec{d}"), s), "split_reduce")
-            if d + 1 < D:  # the last level moves no rows: its partition offsets are never used
-                nat.check(lib.h2o_count(sb, self.stride, self._p(f"nodes{d}"), self._p(f"tp{d}"), self._p(f"meta{d}"),
-                                        self._p(f"dec{d}"), self.tile_cnt.data_ptr(), self.tiles_cap[d], s), "count")
-            nat.check(lib.h2o_plan(self._p(f"nodes{d}"), self._p(f"meta{d}"), self._p(f"tp{d}"), self.tile_cnt.data_ptr(),
-                                   self._p(f"dec{d}"), self.tile_off.data_ptr(), self._p(f"nl{d}"), self._p(f"cl{d}"),
+            nat.check(lib.h2o_plan(self._p(f"nodes{d}"), self._p(f"meta{d}"), self._p(f"dec{d}"), self._p(f"nl{d}"),
+                                   self._p(f"nl{d - 1}") if odd else 0, self._p(f"cur{d}"), self._p(f"cl{d}"),
                                    self._p(f"cr{d}"), self._p(f"nodes{d + 1}"), self._p(f"tp{d + 1}"),
-                                   self._p(f"meta{d + 1}"), self._p("counters"), self.scratch.data_ptr(), d, D,
-                                   p.min_w, self.caps[d + 1], self.leaf_cap, self._p(f"bp{d + 1}"), s), "plan")
-            last = d + 1 == D
-            hb = self.hbuild
-            if not last:
-                nat.check(lib.h2o_zero_hist(hb.data_ptr(), self._p(f"nodes{d + 1}"), self._p(f"meta{d + 1}"),
-                                            self.caps[d + 1], slot, s), "zero_hist")
-            # partition-only pass (high occupancy, no LDS histogram); the smaller child is
-            # histogrammed below over its contiguous rows
-            nat.check(lib.h2o_move_lean(sb, sa, sr, dst["bins"].data_ptr(), dst["aux"].data_ptr(),
-                                        dst["ridx"].data_ptr(), self.stride, self._p(f"nodes{d}"), self._p(f"tp{d}"),
-                                        self._p(f"meta{d}"), self._p(f"dec{d}"), self.tile_off.data_ptr(),
-                                        self._p(f"nl{d}"), self._p(f"cl{d}"), self._p(f"cr{d}"),
-                                        self.leaf_of_row.data_ptr(), self.leafsum.data_ptr(), int(not last),
-                                        self.tiles_cap[d], s), "move_lean")
-            if not last:
-                nat.check(lib.h2o_hist_build(dst["bins"].data_ptr(), self.stride, dst["aux"].data_ptr(),
-                                             self._p(f"nodes{d + 1}"), self._p(f"bp{d + 1}"), self._p(f"meta{d + 1}"),
-                                             F, hb.data_ptr(), slot, qs, min(self.tiles_cap[d + 1], self.grid), pk, s),
-                          "hist_build")
-                # one built child per parent: the compact buffer holds at most caps[d] slots
-                coll.all_reduce_(hb[: self.caps[d] * slot])
-                nat.check(lib.h2o_subtract(hn.data_ptr(), hc.data_ptr(), hb.data_ptr(), self._p(f"nodes{d + 1}"),
-                                           self._p(f"meta{d + 1}"), self.caps[d + 1], slot, s), "subtract")
+                                   self._p(f"meta{d + 1}"), self._p(f"bp{d + 1}"), self._p("counters"),
+                                   self.scratch.data_ptr(), d, D, p.min_w, self.caps[d + 1], self.leaf_cap, s), "plan")
+            if d + 1 == D:
+                # last level: every row lands on a leaf (routed from the last regrouped level)
+                route(d - 1 if odd else d, two=odd, move=False)
+                break
+            nat.check(lib.h2o_zero_hist(hb.data_ptr(), self._p(f"nodes{d + 1}"), self._p(f"meta{d + 1}"),
+                                        self.caps[d + 1], slot, s), "zero_hist")
+            gh = min(self.tiles_cap[d], self.grid)
+            if not odd:
+                # level d+1 (odd) is histogrammed straight from level d's ranges, filtered by level d's
+                # decisions; the pass also counts each parent's left-goers for the next regrouping
+                sb, sa, _ = level_buf(d)
+                nat.check(lib.h2o_hist_build(sb, self.stride, sa, self._p(f"nodes{d + 1}"), self._p(f"bp{d + 1}"),
+                                             self._p(f"meta{d + 1}"), F, hb.data_ptr(), slot, qs, gh, pk,
+                                             self._p(f"dec{d}"), self._p(f"nl{d}"), s), "hist_build")
+            else:
+                # regroup level d-1's rows two levels down, then histogram level d+1 (even) contiguously
+                route(d - 1, two=True, move=True)
+                nat.check(lib.h2o_ranges(self._p(f"nodes{d + 1}"), self._p(f"cur{d}"), self._p(f"tp{d + 1}"),
+                                         self._p(f"bp{d + 1}"), self._p(f"meta{d + 1}"), s), "ranges")
+                sb, sa, _ = level_buf(d + 1)
+                nat.check(lib.h2o_hist_build(sb, self.stride, sa, self._p(f"nodes{d + 1}"), self._p(f"bp{d + 1}"),
+                                             self._p(f"meta{d + 1}"), F, hb.data_ptr(), slot, qs,
+                                             min(self.tiles_cap[d + 1], self.grid), pk, 0, 0, s), "hist_build")
+            # one built child per parent: the compact buffer holds at most caps[d] slots
+            coll.all_reduce_(hb[: self.caps[d] * slot])
+            nat.check(lib.h2o_subtract(hn.data_ptr(), hc.data_ptr(), hb.data_ptr(), self._p(f"nodes{d + 1}"),
+                                       self._p(f"meta{d + 1}"), self.caps[d + 1], slot, s), "subtract")
         coll.all_reduce_(self.leafsum)
         if leaf_fn is not None:
             vals = leaf_fn(self.leafsum)

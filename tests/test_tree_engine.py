@@ -67,26 +67,31 @@ def test_split_ref_numeric_simple():
 
 
 @pytest.mark.gpu
-def test_gpu_tree_matches_reference():
+@pytest.mark.parametrize("depth,min_w,node_cap", [(5, 10, 1 << 14), (1, 10, 1 << 14), (2, 10, 1 << 14),
+                                                  (6, 300, 1 << 14), (7, 40, 1 << 14), (8, 10, 12)])
+def test_gpu_tree_matches_reference(depth, min_w, node_cap):
+    # odd/even last levels, early leaves (large min_rows: terminal nodes and leaf children in the middle of
+    # the two-level regrouping) and node-capacity overflow (children beyond the cap become leaves)
     X, y, info = _data(N=20000, cat=True, seed=5)
     b = fit_binning(X, info.iscat, info.nlevels, max_bins=64)
     bins = apply_binning(b, X)
     aux = torch.stack([torch.ones_like(y), y - y.mean(), y - y.mean(), torch.ones_like(y)], 1).contiguous()
-    p = T.SplitParams(min_w=10)
-    ref = T.RefTreeBuilder(bins, X.shape[0], b.nbins, b.iscat, None, 5, p)
+    p = T.SplitParams(min_w=min_w)
+    ref = T.RefTreeBuilder(bins, X.shape[0], b.nbins, b.iscat, None, depth, p, node_cap=node_cap)
     hr = ref.build(aux, leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1]).float())
     tl_r = ref.fetch(hr)
     dev = torch.device("cuda", 0)
-    gb = T.GpuTreeBuilder(bins.to(dev), X.shape[0], b.nbins, b.iscat, None, 5, p)
-    hg = gb.build(aux.to(dev), leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1]).float())
-    tl_g = gb.fetch(hg)
-    assert tl_g.n_leaves == tl_r.n_leaves
-    for dr, dg in zip(tl_r.decs, tl_g.decs):
-        assert np.array_equal(dr["feat"], dg["feat"])
-        assert np.array_equal(dr["bin"], dg["bin"])
-        np.testing.assert_allclose(dr["wl"], dg["wl"], rtol=1e-6)
-    np.testing.assert_allclose(tl_r.leaf_values, tl_g.leaf_values, rtol=1e-4, atol=1e-6)
-    assert torch.equal(ref.leaf_of_row, gb.leaf_of_row.cpu())
+    gb = T.GpuTreeBuilder(bins.to(dev), X.shape[0], b.nbins, b.iscat, None, depth, p, node_cap=node_cap)
+    for _ in range(2):   # a second tree on the same builder reuses every buffer
+        hg = gb.build(aux.to(dev), leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1]).float())
+        tl_g = gb.fetch(hg)
+        assert tl_g.n_leaves == tl_r.n_leaves
+        for dr, dg in zip(tl_r.decs, tl_g.decs):
+            assert np.array_equal(dr["feat"], dg["feat"])
+            assert np.array_equal(dr["bin"], dg["bin"])
+            np.testing.assert_allclose(dr["wl"], dg["wl"], rtol=1e-6)
+        np.testing.assert_allclose(tl_r.leaf_values, tl_g.leaf_values, rtol=1e-4, atol=1e-6)
+        assert torch.equal(ref.leaf_of_row, gb.leaf_of_row.cpu())
 
 
 @pytest.mark.gpu
