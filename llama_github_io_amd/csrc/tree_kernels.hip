@@ -28,7 +28,6 @@
 #define AMAX_SHARDS 64  // per-block |aux| maxima shards (k_amax / k_gbm_step -> k_qscale)
 #define NA_BIN 255
 #define FTILE 32                // features per LDS histogram tile
-#define HS64 (2 * NBIN + 2)     // int64 entries per feature row in LDS: w at [0,256), wY at [257, 513)
 #define BLK 1024                // one 16-wave block per CU (the int64 LDS histogram is 128 KiB)
 #define NW (BLK / 64)
 #define TILE 2048               // rows per work tile
@@ -120,8 +119,18 @@ __device__ void block_sum4(double v[4], double* scratch /* >= 4*(BLK/64) */) {
 // integer LDS atomics (3.04 ms vs 0.25 ms for 11M x 28 updates), so bins accumulate in FIXED POINT:
 // every row's (w, wY) is scaled by a per-tree 2^40/max|.| and added as int64 (ds_add_u64). The sums
 // are exact and order independent (deterministic histograms); flushes convert to fp64 globally.
-// Layout (int64): hq[f_local * HS64 + bin] = w, hq[f_local * HS64 + 257 + bin] = wY; nayy (fp32, rare).
-#define HIST_LDS_BYTES (FTILE * HS64 * 8 + FTILE * 4)
+//
+// Layout (int64), BANK-CONFLICT FREE for the atomics: entry (feature fl, bin) of plane r (0: w or packed,
+// 1: wY) sits at r * HPLANE + bin * FTILE + fslot(fl). A ds_add_u64 wave-instruction is served in four
+// 16-lane groups (2 rows x 8 words, bank = dword address mod 32); each lane adds feature 4*word + k of its
+// row, with k rotated by the row's parity (hist_rows), and fslot() places features 4j+k and 4(j+4)+k two
+// bank pairs apart, so the 16 lanes of a group always hit 16 distinct bank pairs whatever the bins are.
+// (The former [feature][bin] layout put random bins on random banks: 3-4 way conflicts per group.)
+// Plane 1 is offset by 16 entries so the flush's (r = 0, 1) lane pairs read disjoint banks.
+// nayy (fp32 NA-bin wYY, rare) follows the planes.
+#define HPLANE (NBIN * FTILE + 16)
+#define HIST_LDS_BYTES (2 * HPLANE * 8 + FTILE * 4)
+__device__ __forceinline__ int fslot(int fl) { return (fl & 16) | ((fl + ((fl >> 4) << 1)) & 15); }
 
 __device__ __forceinline__ void lds_zero64(long long* h, int n) {
   for (int i = threadIdx.x; i < n; i += blockDim.x) h[i] = 0ll;
@@ -133,12 +142,12 @@ __device__ __forceinline__ long long q64(float v, float scale) {
 
 // PACKED mode (row weights are small integers, e.g. 1 or a 0/1 sample mask): ONE ds_add_u64 per
 // (row, feature) instead of two — count in bits [48, 64), wY in the low 48 bits as signed fixed point
-// scaled to |q| <= 2^31 per row. A flush window holds < 2^15 rows (PACK_MAX), so the signed low
+// scaled to |q| <= 2^30 per row (one v_cvt_i32_f32 per row). A flush window holds < 2^15 rows (PACK_MAX), so the signed low
 // part never exceeds 2^46 and the count never carries out: decode with one arithmetic shift.
 #define PACK_SHIFT 48
 #define PACK_MAX 30720   // rows per LDS flush window in packed mode (15 tiles)
 __device__ __forceinline__ long long qpack(float w, float b, float scale_p) {
-  return ((long long)w << PACK_SHIFT) + (long long)(b * scale_p);
+  return ((long long)__float2int_rz(w) << PACK_SHIFT) + (long long)__float2int_rz(b * scale_p);
 }
 __device__ __forceinline__ void unpack(long long v, long long& cnt, long long& val) {
   cnt = (v + (1ll << (PACK_SHIFT - 1))) >> PACK_SHIFT;
@@ -147,22 +156,24 @@ __device__ __forceinline__ void unpack(long long v, long long& cnt, long long& v
 
 __device__ void flush_hist(const long long* h, const float* nayy, double node_wyy, int ftile, int F,
                            double* __restrict__ slot, const double* __restrict__ qs, bool packed) {
-  // slot layout: [F][256][2] doubles, then [F] NA-wYY, then [1] node wYY.
+  // slot layout (bin-major): [256 bins][F][2] doubles, then [F] NA-wYY, then [1] node wYY.
+  // Lanes walk (bin, feature, r): consecutive global doubles (coalesced atomics) and, in LDS, distinct
+  // fslot bank pairs per r plus the plane offset (conflict-free reads).
   const int f0 = ftile * FTILE;
   const int nf = min(FTILE, F - f0);
   const double inv_a = qs[2], inv_b = qs[3], inv_p = qs[5];
   for (int i = threadIdx.x; i < nf * 2 * NBIN; i += blockDim.x) {
-    const int fl = i / (2 * NBIN), r = i - fl * 2 * NBIN;
+    const int bin = i / (2 * nf), rem = i - bin * 2 * nf, fl = rem >> 1, r = rem & 1;
+    const int e = bin * FTILE + fslot(fl);
     double d;
     if (packed) {
       long long c, v;
-      unpack(h[fl * HS64 + (r >> 1)], c, v);
-      d = (r & 1) ? (double)v * inv_p : (double)c;
+      unpack(h[e], c, v);
+      d = r ? (double)v * inv_p : (double)c;
     } else {
-      const long long v = h[fl * HS64 + (r & 1) * 257 + (r >> 1)];
-      d = (double)v * ((r & 1) ? inv_b : inv_a);
+      d = (double)h[r * HPLANE + e] * (r ? inv_b : inv_a);
     }
-    if (d != 0.0) atomicAdd(slot + (size_t)(f0 + fl) * 2 * NBIN + r, d);
+    if (d != 0.0) atomicAdd(slot + (size_t)bin * 2 * F + 2 * (f0 + fl) + r, d);
   }
   for (int i = threadIdx.x; i < nf; i += blockDim.x) {
     const float v = nayy[i];
@@ -172,57 +183,67 @@ __device__ void flush_hist(const long long* h, const float* nayy, double node_wy
     atomicAdd(slot + (size_t)F * 2 * NBIN + F, node_wyy);
 }
 
-// accumulate one row-word (4 bins) into the LDS tile histogram
-__device__ __forceinline__ void hist_word(long long* h, float* nayy, unsigned word, int wl /*word index in tile*/,
-                                          int f_abs0, int F, long long qa, long long qb, float yy, bool packed) {
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int fl = wl * 4 + k;
-    if (f_abs0 + k < F) {
-      const int bin = (word >> (8 * k)) & 0xFF;
-      unsigned long long* p = (unsigned long long*)(h + fl * HS64 + bin);
-      atomicAdd(p, (unsigned long long)qa);          // packed: qa = count<<48 | wY
-      if (!packed) atomicAdd(p + 257, (unsigned long long)qb);
-      if (bin == NA_BIN) atomicAdd(nayy + fl, yy);
-    }
-  }
-}
-
-#define UNR 8   // hist: rows per lane-group in flight (memory-level parallelism: 8 independent loads per lane)
-
 __device__ __forceinline__ float row_yy(float a, float b) {
   return a > 0.f ? b * b * __builtin_amdgcn_rcpf(a) : 0.f;
 }
 
 // Parent-decision filter of an odd-level histogram (k_hist_build<true>): only rows of the parent's
-// range that go to `dir` are accumulated; `count` lanes tally the parent's left-goers.
+// range that go to `dir` are accumulated; `count` lanes tally the parent's left-goers. The numeric
+// test runs on registers; only categorical splits read the bitset (LDS copy of the decision).
 struct RowFilter {
   const Dec* pd;   // parent decision (LDS copy)
   int feat;        // its split feature
   int jw;          // lane (within the 8-lane row group) whose word holds `feat`, or -1: load the byte
   int dir;         // 0: accumulate left-goers, 1: right-goers
+  int bin, na_left, is_cat;
   bool count;
+  __device__ __forceinline__ bool left(int b) const {
+    if (b == NA_BIN) return na_left != 0;
+    if (is_cat) return (pd->bits[b >> 5] >> (b & 31)) & 1u;
+    return b < bin;
+  }
 };
 
-// Histogram rows [r0, r1) of one node into LDS. Loads for UNR rows are issued before any atomic.
-template <bool FILT>
+#define UNR 8   // hist: rows per lane group loaded before any atomic (8 independent loads per lane)
+
+// Histogram rows [r0, r1) of one node into LDS: lane group g (8 lanes, one 4-feature row word each)
+// takes rows g, g + RPI, ...; UNR rows per lane group are loaded before any atomic.
+// MEASURED: this loop is VALU-issue bound, not memory bound (prefetching / 4..16 rows in flight all ran
+// within 1.5 %), so everything per-lane is hoisted: the 4 feature slots and byte shifts of the lane's word
+// (rotated by row parity, see the layout note), feature validity, and an all-bytes NA test per word; the
+// common row is then bfe + lshl_add + ds_add_u64 per feature (two atomics when not PACKED).
+template <bool FILT, bool PACKED>
 __device__ __forceinline__ void hist_rows(long long* h, float* nayy, const unsigned* __restrict__ bins32,
                                           const float4* __restrict__ aux, int W, int wabs, int F, bool lead,
                                           int r0, int r1, int g, int j, float& wyy, float sa, float sb, float sp,
-                                          bool packed, const RowFilter& flt, int& lcnt) {
+                                          const RowFilter& flt, int& lcnt) {
   const float2* aux2 = (const float2*)aux;
   const int lane = threadIdx.x & 63;
+  const int rot = g & 1;
+  int off[4], sh[4];
+  unsigned vmask = 0u;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int kk = (k + rot) & 3;
+    off[k] = fslot(j * 4 + kk);
+    sh[k] = 8 * kk;
+    if (wabs < W && wabs * 4 + kk < F) vmask |= 0xFFu << (8 * kk);
+  }
+  const bool full = vmask == 0xFFFFFFFFu;
+  const int wc = min(wabs, W - 1);
+  unsigned long long* H = (unsigned long long*)h;
   for (int base = r0; base < r1; base += RPI * UNR) {
     unsigned wd[UNR];
     float2 ab[UNR];
     int sbyte[UNR];
+    // unconditional loads (rows clamped into the node, words into the row): no exec-mask branches here;
+    // rows past r1 are skipped below, invalid words have vmask == 0
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
-      const int row = base + g + u * RPI;
-      const bool v = row < r1;
-      ab[u] = v ? aux2[(size_t)row * 2] : make_float2(0.f, 0.f);
-      wd[u] = (v && wabs < W) ? bins32[(size_t)row * W + wabs] : 0u;
-      if (FILT && flt.jw < 0) sbyte[u] = v ? ((const uint8_t*)bins32)[(size_t)row * W * 4 + flt.feat] : 0;
+      const size_t row = (size_t)min(base + g + u * RPI, r1 - 1);
+      ab[u] = aux2[row * 2];
+      wd[u] = bins32[row * W + wc];
+      if (FILT && flt.jw < 0) sbyte[u] = ((const uint8_t*)bins32)[row * W * 4 + flt.feat];
     }
     if (FILT && flt.jw >= 0) {
       // the split feature's byte is in lane jw's word of the same row group: one cross-lane read
@@ -233,17 +254,36 @@ __device__ __forceinline__ void hist_rows(long long* h, float* nayy, const unsig
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
       const int row = base + g + u * RPI;
-      if (row < r1) {
-        if (FILT) {
-          const bool gl = dec_go_left(flt.pd, sbyte[u]);
-          if (flt.count) lcnt += gl ? 1 : 0;
-          if ((gl ? 0 : 1) != flt.dir) continue;
+      if (row >= r1) continue;
+      if (FILT) {
+        const bool gl = flt.left(sbyte[u]);
+        if (flt.count) lcnt += gl ? 1 : 0;
+        if ((gl ? 0 : 1) != flt.dir) continue;
+      }
+      if (lead) wyy += row_yy(ab[u].x, ab[u].y);
+      if (vmask == 0u) continue;
+      const long long qa = PACKED ? qpack(ab[u].x, ab[u].y, sp) : q64(ab[u].x, sa);
+      const long long qb = PACKED ? 0ll : q64(ab[u].y, sb);
+      const unsigned w = wd[u];
+      const unsigned x = ~w | ~vmask;                     // a zero byte of x = an NA bin of a valid feature
+      const bool has_na = ((x - 0x01010101u) & ~x & 0x80808080u) != 0u;
+      if (full && !has_na) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          unsigned long long* p = H + (((w >> sh[k]) & 0xFFu) * FTILE + off[k]);
+          atomicAdd(p, (unsigned long long)qa);
+          if (!PACKED) atomicAdd(p + HPLANE, (unsigned long long)qb);
         }
+      } else {
         const float yy = row_yy(ab[u].x, ab[u].y);
-        if (lead) wyy += yy;
-        if (wabs < W) {
-          const long long qa = packed ? qpack(ab[u].x, ab[u].y, sp) : q64(ab[u].x, sa);
-          hist_word(h, nayy, wd[u], j, wabs * 4, F, qa, q64(ab[u].y, sb), yy, packed);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (!((vmask >> sh[k]) & 1u)) continue;
+          const unsigned bin = (w >> sh[k]) & 0xFFu;
+          unsigned long long* p = H + (bin * FTILE + off[k]);
+          atomicAdd(p, (unsigned long long)qa);
+          if (!PACKED) atomicAdd(p + HPLANE, (unsigned long long)qb);
+          if (bin == NA_BIN) atomicAdd(nayy + j * 4 + (sh[k] >> 3), yy);
         }
       }
     }
@@ -255,17 +295,17 @@ __device__ __forceinline__ void hist_rows(long long* h, float* nayy, const unsig
 // grid = (G, n_ftiles); each block takes a contiguous range of tiles so it flushes rarely.
 // FILT (odd levels): a node's tiles cover its PARENT's rows; only rows the parent's decision sends to
 // this child are accumulated, and ftile-0 blocks add the parent's left-going row count to nl_out.
-template <bool FILT>
+template <bool FILT, bool PACKED>
 __global__ __launch_bounds__(BLK) void k_hist_build(
     const uint8_t* __restrict__ bins, int stride /*bytes per row, multiple of 4*/,
     const float4* __restrict__ aux, const Node* __restrict__ nodes, const int* __restrict__ tile_prefix,
     const int* __restrict__ meta /*[0]=n_nodes [1]=n_tiles*/, int F, double* __restrict__ hist, int slot_doubles,
-    const double* __restrict__ qs /*[sa, sb, 1/sa, 1/sb, sp, 1/sp]*/, int packed_i,
+    const double* __restrict__ qs /*[sa, sb, 1/sa, 1/sb, sp, 1/sp]*/,
     const Dec* __restrict__ pdec, int* __restrict__ nl_out) {
-  const bool packed = packed_i != 0;
+  constexpr bool packed = PACKED;
   extern __shared__ __attribute__((aligned(16))) long long smem64[];
-  long long* h = smem64;                                 // FTILE * HS64
-  float* nayy = (float*)(smem64 + FTILE * HS64);         // FTILE
+  long long* h = smem64;                                 // 2 * HPLANE
+  float* nayy = (float*)(smem64 + 2 * HPLANE);           // FTILE
   double* red = (double*)(nayy + FTILE);                 // 64 doubles scratch
 
   // tile_prefix here is the BUILD-tile prefix (only nodes with build=1 own tiles) and meta[2] the number
@@ -283,7 +323,7 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
   const float sa = (float)qs[0], sb = (float)qs[1], sp = (float)qs[4];
 
   __shared__ Dec spd;
-  RowFilter flt{&spd, 0, -1, 0, false};
+  RowFilter flt{&spd, 0, -1, 0, 0, 0, 0, false};
   int lcnt = 0;
   int cur = -1, since = 0;
   double wyy = 0.0;
@@ -304,7 +344,7 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
         if (FILT && threadIdx.x == 0 && v[1] != 0.0) atomicAdd(nl_out + cur, (int)v[1]);
         __syncthreads();
       }
-      lds_zero64(h, FTILE * HS64);
+      lds_zero64(h, packed ? HPLANE : 2 * HPLANE);
       for (int i = threadIdx.x; i < FTILE; i += blockDim.x) nayy[i] = 0.f;
       if (FILT && threadIdx.x < (int)(sizeof(Dec) / 4))
         ((int*)&spd)[threadIdx.x] = ((const int*)(pdec + nd.parent))[threadIdx.x];
@@ -318,13 +358,14 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
         const int jw = (spd.feat >> 2) - ftile * LPR;
         flt.jw = (jw >= 0 && jw < LPR) ? jw : -1;
         flt.dir = nd.dir;
+        flt.bin = spd.bin; flt.na_left = spd.na_left; flt.is_cat = spd.is_cat;
         flt.count = ftile == 0 && j == 0;
       }
     }
     since += r1 - r0;
     float wf = 0.f;
-    hist_rows<FILT>(h, nayy, bins32, aux, W, wabs, F, j == 0 && ftile == 0, r0, r1, g, j, wf, sa, sb, sp, packed,
-                    flt, lcnt);
+    hist_rows<FILT, PACKED>(h, nayy, bins32, aux, W, wabs, F, j == 0 && ftile == 0, r0, r1, g, j, wf, sa, sb, sp,
+                            flt, lcnt);
     wyy += (double)wf;
   }
   if (cur >= 0) {
@@ -350,16 +391,17 @@ __global__ __launch_bounds__(256) void k_split_find(
   __shared__ int best_i[256];
 
   const double* slot = hist + (size_t)node * slot_doubles;
-  const double* h = slot + (size_t)f * 2 * NBIN;
+  const double* h = slot + 2 * f;          // bin-major slot: (bin, f) at bin * 2F + 2f
+  const int hs = 2 * F;
   const int nb = nbins_f[f];
   const bool cat = iscat_f[f] != 0;
   const int mono = mono_f ? mono_f[f] : 0;
-  const double wNA = h[2 * NA_BIN], wyNA = h[2 * NA_BIN + 1];
+  const double wNA = h[NA_BIN * hs], wyNA = h[NA_BIN * hs + 1];
   const double naYY = slot[(size_t)F * 2 * NBIN + f];
   const double wYY = slot[(size_t)F * 2 * NBIN + F];
 
   double w = 0, wy = 0;
-  if (t < nb && t < NA_BIN) { w = h[2 * t]; wy = h[2 * t + 1]; }
+  if (t < nb && t < NA_BIN) { w = h[t * hs]; wy = h[t * hs + 1]; }
   sidx[t] = t;
   if (cat) {
     // sort bins by mean response (empty bins first, out-of-range bins last) — DTree.java:1006
@@ -1061,8 +1103,8 @@ __global__ void k_qscale(const unsigned* __restrict__ amax_bits, double* __restr
     const double sc = (m > 0.0 && m == m) ? 1099511627776.0 / m : 1.0;   // 2^40 / max
     qs[threadIdx.x] = sc;
     qs[2 + threadIdx.x] = 1.0 / sc;
-    if (threadIdx.x == 1) {                                                // packed wY: 2^31 / max
-      const double sp = (m > 0.0 && m == m) ? 2147483648.0 / m : 1.0;
+    if (threadIdx.x == 1) {                                                // packed wY: 2^30 / max
+      const double sp = (m > 0.0 && m == m) ? 1073741824.0 / m : 1.0;
       qs[4] = sp;
       qs[5] = 1.0 / sp;
     }
@@ -1071,6 +1113,20 @@ __global__ void k_qscale(const unsigned* __restrict__ amax_bits, double* __restr
 
 // ================================================================================================
 // C ABI launchers (called through ctypes with raw device pointers and the current HIP stream).
+template <bool PACKED>
+static void launch_hist(dim3 grid, size_t lds, hipStream_t s, const void* bins, int stride, const void* aux,
+                        const void* nodes, const void* tile_prefix, const void* meta, int F, void* hist,
+                        int slot_doubles, const void* qs, const void* pdec, void* nl_out) {
+  if (pdec)
+    hipLaunchKernelGGL((k_hist_build<true, PACKED>), grid, dim3(BLK), lds, s, (const uint8_t*)bins, stride,
+                       (const float4*)aux, (const Node*)nodes, (const int*)tile_prefix, (const int*)meta, F,
+                       (double*)hist, slot_doubles, (const double*)qs, (const Dec*)pdec, (int*)nl_out);
+  else
+    hipLaunchKernelGGL((k_hist_build<false, PACKED>), grid, dim3(BLK), lds, s, (const uint8_t*)bins, stride,
+                       (const float4*)aux, (const Node*)nodes, (const int*)tile_prefix, (const int*)meta, F,
+                       (double*)hist, slot_doubles, (const double*)qs, (const Dec*)nullptr, (int*)nullptr);
+}
+
 extern "C" {
 
 int h2o_tree_sizes(int* out) {
@@ -1086,15 +1142,9 @@ int h2o_hist_build(const void* bins, int stride, const void* aux, const void* no
                    const void* pdec, void* nl_out, hipStream_t s) {
   const int nft = (F + FTILE - 1) / FTILE;
   const size_t lds = HIST_LDS_BYTES + 64 * 8;
-  if (pdec) {
-    hipLaunchKernelGGL(k_hist_build<true>, dim3(grid, nft), dim3(BLK), lds, s, (const uint8_t*)bins, stride,
-                       (const float4*)aux, (const Node*)nodes, (const int*)tile_prefix, (const int*)meta, F,
-                       (double*)hist, slot_doubles, (const double*)qs, packed, (const Dec*)pdec, (int*)nl_out);
-  } else {
-    hipLaunchKernelGGL(k_hist_build<false>, dim3(grid, nft), dim3(BLK), lds, s, (const uint8_t*)bins, stride,
-                       (const float4*)aux, (const Node*)nodes, (const int*)tile_prefix, (const int*)meta, F,
-                       (double*)hist, slot_doubles, (const double*)qs, packed, (const Dec*)nullptr, (int*)nullptr);
-  }
+  const dim3 gr(grid, nft);
+  if (packed) launch_hist<true>(gr, lds, s, bins, stride, aux, nodes, tile_prefix, meta, F, hist, slot_doubles, qs, pdec, nl_out);
+  else launch_hist<false>(gr, lds, s, bins, stride, aux, nodes, tile_prefix, meta, F, hist, slot_doubles, qs, pdec, nl_out);
   return (int)hipGetLastError();
 }
 

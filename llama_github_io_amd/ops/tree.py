@@ -463,7 +463,8 @@ class GpuTreeBuilder:
                                      0, 0, s),
                   "hist_build")
         coll.all_reduce_(self.hist[0][:slot])
-        self.root_w = self.hist[0][0:2 * NBIN:2].sum().reshape(1)   # Σw over feature 0's bins = root weight
+        # Σw over feature 0's bins = root weight (bin-major slot: (bin, f, r) at bin * 2F + 2f + r)
+        self.root_w = self.hist[0][0:2 * NBIN * F:2 * F].sum().reshape(1)
         mono = 0 if self.mono_f is None else self.mono_f.data_ptr()
         seed = int(seed) & _M64
         hb = self.hbuild
