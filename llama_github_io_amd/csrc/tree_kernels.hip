@@ -35,7 +35,8 @@
 #define RPI (BLK / LPR)         // rows per iteration (128)
 
 struct Node {      // one active node of a level (rows [start, start+len) of the level's buffer)
-  int start, len, build, parent, sib, dir /*odd levels: 0 left / 1 right child*/, pad1, pad2;
+  int start, len, build, parent, sib /*other active child of the parent, or -1*/,
+      dir /*odd levels: 0 left / 1 right child*/, pad1, pad2;
 };
 
 struct Dec {       // split decision (80 B)
@@ -154,11 +155,17 @@ __device__ __forceinline__ void unpack(long long v, long long& cnt, long long& v
   val = v - (cnt << PACK_SHIFT);
 }
 
-__device__ void flush_hist(const long long* h, const float* nayy, double node_wyy, int ftile, int F,
-                           double* __restrict__ slot, const double* __restrict__ qs, bool packed) {
-  // slot layout (bin-major): [256 bins][F][2] doubles, then [F] NA-wYY, then [1] node wYY.
-  // Lanes walk (bin, feature, r): consecutive global doubles (coalesced atomics) and, in LDS, distinct
-  // fslot bank pairs per r plus the plane offset (conflict-free reads).
+// Flush of one block's LDS histogram into ITS OWN partial slot (plain stores, no global atomics):
+// partial index = blockIdx.x + node (unique: a block's tiles and nodes both increase, see k_hist_reduce).
+// `acc` (a later packed flush window of the same node) adds into what this same thread stored before.
+// Slot layout (bin-major): [256 bins][F][2] doubles, then [F] NA-wYY, then [1] node wYY. Lanes walk
+// (bin, feature, r): consecutive global doubles and, in LDS, distinct fslot bank pairs per r plus the
+// plane offset (conflict-free reads).
+// MEASURED: the former fp64 atomicAdd flush into one shared slot cost ~30 us per level regardless of
+// row count (256 blocks x 14K same-address atomics serialise in L2) — the fixed cost that dominated
+// small shards (1.375M rows/GPU at 8 GPUs).
+__device__ void flush_partial(const long long* h, const float* nayy, double node_wyy, int ftile, int F,
+                              double* __restrict__ part, const double* __restrict__ qs, bool packed, bool acc) {
   const int f0 = ftile * FTILE;
   const int nf = min(FTILE, F - f0);
   const double inv_a = qs[2], inv_b = qs[3], inv_p = qs[5];
@@ -173,14 +180,17 @@ __device__ void flush_hist(const long long* h, const float* nayy, double node_wy
     } else {
       d = (double)h[r * HPLANE + e] * (r ? inv_b : inv_a);
     }
-    if (d != 0.0) atomicAdd(slot + (size_t)bin * 2 * F + 2 * (f0 + fl) + r, d);
+    double* q = part + (size_t)bin * 2 * F + 2 * (f0 + fl) + r;
+    *q = acc ? *q + d : d;
   }
   for (int i = threadIdx.x; i < nf; i += blockDim.x) {
-    const float v = nayy[i];
-    if (v != 0.f) atomicAdd(slot + (size_t)F * 2 * NBIN + f0 + i, (double)v);
+    double* q = part + (size_t)F * 2 * NBIN + f0 + i;
+    *q = acc ? *q + (double)nayy[i] : (double)nayy[i];
   }
-  if (threadIdx.x == 0 && ftile == 0 && node_wyy != 0.0)
-    atomicAdd(slot + (size_t)F * 2 * NBIN + F, node_wyy);
+  if (threadIdx.x == 0 && ftile == 0) {
+    double* q = part + (size_t)F * 2 * NBIN + F;
+    *q = acc ? *q + node_wyy : node_wyy;
+  }
 }
 
 __device__ __forceinline__ float row_yy(float a, float b) {
@@ -291,16 +301,17 @@ __device__ __forceinline__ void hist_rows(long long* h, float* nayy, const unsig
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_hist_build: histograms of all nodes with build==1 of a level into the compact build buffer.
-// grid = (G, n_ftiles); each block takes a contiguous range of tiles so it flushes rarely.
+// k_hist_build: histograms of all nodes with build==1 of a level, as per-block PARTIAL slots
+// (partials + (blockIdx.x + node) * slot_doubles); k_hist_reduce sums them per node in a fixed order
+// (deterministic, no global atomics). grid = (G, n_ftiles); each block takes a contiguous tile range.
 // FILT (odd levels): a node's tiles cover its PARENT's rows; only rows the parent's decision sends to
 // this child are accumulated, and ftile-0 blocks add the parent's left-going row count to nl_out.
 template <bool FILT, bool PACKED>
 __global__ __launch_bounds__(BLK) void k_hist_build(
     const uint8_t* __restrict__ bins, int stride /*bytes per row, multiple of 4*/,
     const float4* __restrict__ aux, const Node* __restrict__ nodes, const int* __restrict__ tile_prefix,
-    const int* __restrict__ meta /*[0]=n_nodes [1]=n_tiles*/, int F, double* __restrict__ hist, int slot_doubles,
-    const double* __restrict__ qs /*[sa, sb, 1/sa, 1/sb, sp, 1/sp]*/,
+    const int* __restrict__ meta /*[0]=n_nodes [2]=n_build_tiles*/, int F, double* __restrict__ partials,
+    int slot_doubles, const double* __restrict__ qs /*[sa, sb, 1/sa, 1/sb, sp, 1/sp]*/,
     const Dec* __restrict__ pdec, int* __restrict__ nl_out) {
   constexpr bool packed = PACKED;
   extern __shared__ __attribute__((aligned(16))) long long smem64[];
@@ -325,25 +336,27 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
   __shared__ Dec spd;
   RowFilter flt{&spd, 0, -1, 0, 0, 0, 0, false};
   int lcnt = 0;
-  int cur = -1, since = 0;
+  int cur = -1, since = 0, cur_parent = -1;
+  bool acc = false;
   double wyy = 0.0;
+  auto flush = [&]() {
+    double v[4] = {wyy, (double)lcnt, 0, 0};
+    block_sum4(v, red);
+    __syncthreads();
+    flush_partial(h, nayy, v[0], ftile, F, partials + (size_t)(blockIdx.x + cur) * slot_doubles, qs, packed, acc);
+    if (FILT && threadIdx.x == 0 && v[1] != 0.0) atomicAdd(nl_out + cur_parent, (int)v[1]);
+    __syncthreads();
+  };
   for (int t = t0; t < t1; ++t) {
     const int node = find_node(tile_prefix, n_nodes, t);
     const Node nd = nodes[node];
     if (!nd.build) continue;
-    const int hslot = nd.parent >= 0 ? nd.parent : 0;   // compact build slot (see header)
     const int r0 = nd.start + (t - tile_prefix[node]) * TILE;
     const int r1 = min(r0 + TILE, nd.start + nd.len);
     // new node, or (packed) the flush window is full: flush the LDS tile and restart it
-    if (hslot != cur || (packed && since + (r1 - r0) > PACK_MAX)) {
-      if (cur >= 0) {
-        double v[4] = {wyy, (double)lcnt, 0, 0};
-        block_sum4(v, red);
-        __syncthreads();
-        flush_hist(h, nayy, v[0], ftile, F, hist + (size_t)cur * slot_doubles, qs, packed);
-        if (FILT && threadIdx.x == 0 && v[1] != 0.0) atomicAdd(nl_out + cur, (int)v[1]);
-        __syncthreads();
-      }
+    if (node != cur || (packed && since + (r1 - r0) > PACK_MAX)) {
+      if (cur >= 0) flush();
+      acc = node == cur;    // same node, next window: add into the partial stored by the first flush
       lds_zero64(h, packed ? HPLANE : 2 * HPLANE);
       for (int i = threadIdx.x; i < FTILE; i += blockDim.x) nayy[i] = 0.f;
       if (FILT && threadIdx.x < (int)(sizeof(Dec) / 4))
@@ -351,7 +364,8 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
       wyy = 0.0;
       lcnt = 0;
       since = 0;
-      cur = hslot;
+      cur = node;
+      cur_parent = nd.parent;
       __syncthreads();
       if (FILT) {
         flt.feat = spd.feat;
@@ -368,12 +382,36 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
                             flt, lcnt);
     wyy += (double)wf;
   }
-  if (cur >= 0) {
-    double v[4] = {wyy, (double)lcnt, 0, 0};
-    block_sum4(v, red);
-    __syncthreads();
-    flush_hist(h, nayy, v[0], ftile, F, hist + (size_t)cur * slot_doubles, qs, packed);
-    if (FILT && threadIdx.x == 0 && v[1] != 0.0) atomicAdd(nl_out + cur, (int)v[1]);
+  if (cur >= 0) flush();
+}
+
+// k_hist_reduce: per build node, sum its partial slots in block order (deterministic fp64) and write
+// the node histogram to out[slot] (slot = parent: the compact build buffer; 0 for the root).
+// Block b covers tiles [b*per, (b+1)*per), so node n's blocks are b in [bp[n]/per, (bp[n+1]-1)/per] and
+// its partials sit at b + n. With hist_next != nullptr (single process) the sibling subtraction is fused:
+// hist_next[n] = sum and hist_next[sib] = hist_cur[parent] - sum (no compact-buffer round trip).
+__global__ __launch_bounds__(256) void k_hist_reduce(
+    const double* __restrict__ partials, int slot_doubles, int used, const Node* __restrict__ nodes,
+    const int* __restrict__ bp, const int* __restrict__ meta, int G, double* __restrict__ out,
+    double* __restrict__ hist_next, const double* __restrict__ hist_cur) {
+  const int node = blockIdx.y;
+  if (node >= meta[0]) return;
+  const Node nd = nodes[node];
+  if (!nd.build) return;
+  const int n_tiles = meta[2];
+  const int per = n_tiles > 0 ? (n_tiles + G - 1) / G : 1;
+  const int t0 = bp[node], t1 = bp[node + 1];
+  const int b0 = t0 / per, b1 = t1 > t0 ? (t1 - 1) / per : b0 - 1;
+  const int oslot = nd.parent >= 0 ? nd.parent : 0;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < used; i += gridDim.x * blockDim.x) {
+    double acc = 0.0;
+    for (int b = b0; b <= b1; ++b) acc += partials[(size_t)(b + node) * slot_doubles + i];
+    if (out) out[(size_t)oslot * slot_doubles + i] = acc;
+    if (hist_next) {
+      hist_next[(size_t)node * slot_doubles + i] = acc;
+      if (nd.sib >= 0)
+        hist_next[(size_t)nd.sib * slot_doubles + i] = hist_cur[(size_t)nd.parent * slot_doubles + i] - acc;
+    }
   }
 }
 
@@ -382,7 +420,7 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
 __global__ __launch_bounds__(256) void k_split_find(
     const double* __restrict__ hist, int slot_doubles, const int* __restrict__ meta, int F,
     const int* __restrict__ nbins_f, const int* __restrict__ iscat_f, const int* __restrict__ mono_f,
-    SplitParams p, int level, Cand* __restrict__ cand) {
+    SplitParams p, int level, Cand* __restrict__ cand, double* __restrict__ root_w) {
   const int node = blockIdx.x, f = blockIdx.y, t = threadIdx.x;
   if (node >= meta[0]) return;
   __shared__ double sw[256], swy[256], skey[256];
@@ -436,6 +474,7 @@ __global__ __launch_bounds__(256) void k_split_find(
   }
   const double W = sw[255], WY = swy[255];
   const double Wall = W + wNA, WYall = WY + wyNA;
+  if (root_w && node == 0 && f == 0 && t == 0) *root_w = Wall;   // level 0: the tree's total weight
 
   auto E = [&](double ww, double yy) -> double {
     if (p.mode == 1) {
@@ -771,8 +810,8 @@ __global__ __launch_bounds__(1024) void k_plan(
     // children of an even node inherit its range (odd level); children of an odd node get theirs in k_ranges
     if (li >= 0 && ri >= 0) {
       const bool build_left = d.wl <= d.wr;  // global weights: identical choice on every rank
-      next[li] = Node{nd.start, nd.len, build_left ? 1 : 0, i, build_left ? -1 : ri, 0, 0, 0};
-      next[ri] = Node{nd.start, nd.len, build_left ? 0 : 1, i, build_left ? li : -1, 1, 0, 0};
+      next[li] = Node{nd.start, nd.len, build_left ? 1 : 0, i, ri, 0, 0, 0};
+      next[ri] = Node{nd.start, nd.len, build_left ? 0 : 1, i, li, 1, 0, 0};
     } else if (li >= 0) {
       next[li] = Node{nd.start, nd.len, 1, i, -1, 0, 0, 0};
     } else if (ri >= 0) {
@@ -1094,12 +1133,21 @@ __global__ __launch_bounds__(256) void k_amax(const float4* __restrict__ aux, lo
   }
 }
 
-// folds the AMAX_SHARDS per-shard maxima, then derives the fixed-point scales
-__global__ void k_qscale(const unsigned* __restrict__ amax_bits, double* __restrict__ qs) {
+// folds the AMAX_SHARDS per-shard maxima, then derives the fixed-point scales. Also the tree's
+// start-of-build reset (one launch instead of three fills): leaf counters, leaf sums, and the amax
+// shards themselves once read (the next tree's fused step re-fills them).
+__global__ __launch_bounds__(256) void k_qscale(unsigned* __restrict__ amax_bits, double* __restrict__ qs,
+                                                int* __restrict__ counters, double* __restrict__ leafsum,
+                                                int n_leafsum) {
+  __shared__ unsigned sm[2];
   if (threadIdx.x < 2) {
     unsigned mbits = 0u;
     for (int k = 0; k < AMAX_SHARDS; ++k) mbits = max(mbits, amax_bits[2 * k + threadIdx.x]);
-    const double m = (double)__uint_as_float(mbits);
+    sm[threadIdx.x] = mbits;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    const double m = (double)__uint_as_float(sm[threadIdx.x]);
     const double sc = (m > 0.0 && m == m) ? 1099511627776.0 / m : 1.0;   // 2^40 / max
     qs[threadIdx.x] = sc;
     qs[2 + threadIdx.x] = 1.0 / sc;
@@ -1109,22 +1157,43 @@ __global__ void k_qscale(const unsigned* __restrict__ amax_bits, double* __restr
       qs[5] = 1.0 / sp;
     }
   }
+  for (int i = threadIdx.x; i < 2 * AMAX_SHARDS; i += blockDim.x) amax_bits[i] = 0u;
+  if (counters && threadIdx.x < 4) counters[threadIdx.x] = 0;
+  if (leafsum) for (int i = threadIdx.x; i < n_leafsum; i += blockDim.x) leafsum[i] = 0.0;
+}
+
+// Leaf values of the GBM distributions with a closed-form Newton step (GBM.java fitBestConstants):
+// g = num/den (0 where den == 0), log-link families take log(g); scaled by the learning rate, then
+// the multinomial / max_abs_leafnode_pred clamps and nan/inf sanitising of the PyTorch path.
+__global__ void k_leaf_values(const double* __restrict__ leafsum, int n, int log_link, double scale, double kclamp,
+                              double mx, float* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double num = leafsum[2 * i], den = leafsum[2 * i + 1];
+  double g = den == 0.0 ? 0.0 : num / den;
+  if (log_link) g = den == 0.0 ? 0.0 : log(fmax(g, 1e-300));
+  double v = scale * g;
+  if (v != v) v = 0.0;                                      // nan_to_num(nan=0)
+  if (kclamp > 0.0) v = fmin(fmax(v, -kclamp), kclamp);      // multinomial +-1e4
+  if (isinf(v)) v = v > 0 ? 1e4 : -1e4;                      // nan_to_num(posinf/neginf=+-1e4)
+  v = fmin(fmax(v, -mx), mx);                               // max_abs_leafnode_pred (inf: no-op)
+  out[i] = (float)v;
 }
 
 // ================================================================================================
 // C ABI launchers (called through ctypes with raw device pointers and the current HIP stream).
 template <bool PACKED>
 static void launch_hist(dim3 grid, size_t lds, hipStream_t s, const void* bins, int stride, const void* aux,
-                        const void* nodes, const void* tile_prefix, const void* meta, int F, void* hist,
+                        const void* nodes, const void* tile_prefix, const void* meta, int F, void* partials,
                         int slot_doubles, const void* qs, const void* pdec, void* nl_out) {
   if (pdec)
     hipLaunchKernelGGL((k_hist_build<true, PACKED>), grid, dim3(BLK), lds, s, (const uint8_t*)bins, stride,
                        (const float4*)aux, (const Node*)nodes, (const int*)tile_prefix, (const int*)meta, F,
-                       (double*)hist, slot_doubles, (const double*)qs, (const Dec*)pdec, (int*)nl_out);
+                       (double*)partials, slot_doubles, (const double*)qs, (const Dec*)pdec, (int*)nl_out);
   else
     hipLaunchKernelGGL((k_hist_build<false, PACKED>), grid, dim3(BLK), lds, s, (const uint8_t*)bins, stride,
                        (const float4*)aux, (const Node*)nodes, (const int*)tile_prefix, (const int*)meta, F,
-                       (double*)hist, slot_doubles, (const double*)qs, (const Dec*)nullptr, (int*)nullptr);
+                       (double*)partials, slot_doubles, (const double*)qs, (const Dec*)nullptr, (int*)nullptr);
 }
 
 extern "C" {
@@ -1137,27 +1206,47 @@ int h2o_tree_sizes(int* out) {
   return 0;
 }
 
+// partials: >= (grid + max nodes of the level) slots of slot_doubles
 int h2o_hist_build(const void* bins, int stride, const void* aux, const void* nodes, const void* tile_prefix,
-                   const void* meta, int F, void* hist, int slot_doubles, const void* qs, int grid, int packed,
+                   const void* meta, int F, void* partials, int slot_doubles, const void* qs, int grid, int packed,
                    const void* pdec, void* nl_out, hipStream_t s) {
   const int nft = (F + FTILE - 1) / FTILE;
   const size_t lds = HIST_LDS_BYTES + 64 * 8;
   const dim3 gr(grid, nft);
-  if (packed) launch_hist<true>(gr, lds, s, bins, stride, aux, nodes, tile_prefix, meta, F, hist, slot_doubles, qs, pdec, nl_out);
-  else launch_hist<false>(gr, lds, s, bins, stride, aux, nodes, tile_prefix, meta, F, hist, slot_doubles, qs, pdec, nl_out);
+  if (packed) launch_hist<true>(gr, lds, s, bins, stride, aux, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out);
+  else launch_hist<false>(gr, lds, s, bins, stride, aux, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out);
+  return (int)hipGetLastError();
+}
+
+// grid: the G the matching h2o_hist_build ran with; out / hist_next may be null (see k_hist_reduce)
+int h2o_hist_reduce(const void* partials, int slot_doubles, int used, const void* nodes, const void* bp,
+                    const void* meta, int cap, int grid, void* out, void* hist_next, const void* hist_cur,
+                    hipStream_t s) {
+  int gx = (used + 255) / 256;
+  if (gx > 64) gx = 64;
+  hipLaunchKernelGGL(k_hist_reduce, dim3(gx, cap), dim3(256), 0, s, (const double*)partials, slot_doubles, used,
+                     (const Node*)nodes, (const int*)bp, (const int*)meta, grid, (double*)out, (double*)hist_next,
+                     (const double*)hist_cur);
+  return (int)hipGetLastError();
+}
+
+int h2o_leaf_values(const void* leafsum, int n, int log_link, double scale, double kclamp, double mx, void* out,
+                    hipStream_t s) {
+  hipLaunchKernelGGL(k_leaf_values, dim3((n + 255) / 256), dim3(256), 0, s, (const double*)leafsum, n, log_link,
+                     scale, kclamp, mx, (float*)out);
   return (int)hipGetLastError();
 }
 
 int h2o_split_find(const void* hist, int slot_doubles, const void* meta, int cap, int F, const void* nbins_f,
                    const void* iscat_f, const void* mono_f, double min_w, double msi, double lambda_, double alpha,
                    double gamma, int mode, int random_split, unsigned long long seed, int level, void* cand,
-                   hipStream_t s) {
+                   void* root_w, hipStream_t s) {
   SplitParams p;
   p.min_w = min_w; p.min_split_improvement = msi; p.lambda = lambda_; p.alpha = alpha; p.gamma = gamma;
   p.mode = mode; p.random_split = random_split; p.seed = seed;
   hipLaunchKernelGGL(k_split_find, dim3(cap, F), dim3(256), 0, s, (const double*)hist, slot_doubles,
                      (const int*)meta, F, (const int*)nbins_f, (const int*)iscat_f, (const int*)mono_f, p, level,
-                     (Cand*)cand);
+                     (Cand*)cand, (double*)root_w);
   return (int)hipGetLastError();
 }
 
@@ -1226,8 +1315,9 @@ int h2o_amax(const void* aux, long long N, void* amax_bits, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-int h2o_qscale(const void* amax_bits, void* qs, hipStream_t s) {
-  hipLaunchKernelGGL(k_qscale, dim3(1), dim3(64), 0, s, (const unsigned*)amax_bits, (double*)qs);
+int h2o_qscale(void* amax_bits, void* qs, void* counters, void* leafsum, int n_leafsum, hipStream_t s) {
+  hipLaunchKernelGGL(k_qscale, dim3(1), dim3(256), 0, s, (unsigned*)amax_bits, (double*)qs, (int*)counters,
+                     (double*)leafsum, n_leafsum);
   return (int)hipGetLastError();
 }
 

@@ -140,7 +140,6 @@ class GBMTrainer(SharedTreeTrainer):
             if not hasattr(self, "_amax"):
                 self._amax = torch.zeros(2 * T.AMAX_SHARDS, dtype=torch.int32, device=self.dev)
                 self._wbuf = None if self.w is None or bool((self.w == 1).all()) else self.w.contiguous()
-            self._amax.zero_()
             pv, pl = self._pending if getattr(self, "_pending", None) is not None else (None, None)
             p1 = {"tweedie": self.p["tweedie_power"], "quantile": self.p["quantile_alpha"],
                   "huber": getattr(self.dist, "huber_delta", 1.0)}.get(self.dname, 0.0)
@@ -170,6 +169,14 @@ class GBMTrainer(SharedTreeTrainer):
         a[:, 3] = d.gamma_denom(w, y, z, f)
         self._z = z
         return a
+
+    def _leaf_native(self, t, k):
+        """Closed-form Newton leaves in one HIP launch (k_leaf_values) for the fused single-output path."""
+        if not self._fused() or self.dname in ORDER_STAT_DISTS:
+            return None
+        self._vals = self.builder.leaf_values_view()
+        return (int(self.dname in ("poisson", "gamma", "tweedie")), self._lr(t), 0.0,
+                float(self.p.get("max_abs_leafnode_pred", float("inf"))))
 
     def _amax_for_build(self):
         return self._amax if self._fused() else None

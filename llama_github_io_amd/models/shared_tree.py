@@ -176,14 +176,18 @@ class SharedTreeTrainer:
                     kw["amax_bits"] = am
                 if self.dev.type == "cuda":
                     kw["packed"] = self._hist_packed()
+                    ln = self._leaf_native(t, k)
+                    if ln is not None:
+                        kw["leaf_native"] = ln
                 h = self.builder.build(aux, feat_ok, self._k_cols(F), seed=(self.seed * 1000003 + t * 97 + k) & ((1 << 63) - 1),
                                        leaf_fn=lambda ls, t=t, k=k: self._leaf_values(ls, t, k), **kw)
                 self._update(t, k)
                 handles.append((h, k))
             built = t + 1
+            if not need_sync:
+                self._drain(handles, forest, gains, ready_only=True)   # overlap host decode with GPU work
             if need_sync:
                 self._drain(handles, forest, gains)
-                handles = []
                 if interval and (built % interval == 0 or built == ntrees):
                     ev = self._score_event(model, built, t_start)
                     history.append(ev)
@@ -193,7 +197,6 @@ class SharedTreeTrainer:
             ck_dir = p.get("in_training_checkpoints_dir")
             if ck_dir and built % max(1, int(p.get("in_training_checkpoints_tree_interval") or 1)) == 0:
                 self._drain(handles, forest, gains)       # snapshot of the model so far, resumable via checkpoint=
-                handles = []
                 self._save_in_training(model, built, ck_dir)
             if max_rt > 0 and time.time() - t_start > max_rt:
                 break
@@ -224,16 +227,15 @@ class SharedTreeTrainer:
         ok[rng.choice(F, size=k, replace=False)] = 1
         return torch.from_numpy(ok).to(self.dev)
 
-    def _drain(self, handles, forest, gains):
+    def _drain(self, handles, forest, gains, ready_only=False):
+        """Move built trees (in build order) from the builder into the forest; ``handles`` is consumed
+        in place. ``ready_only`` takes only trees whose device->host snapshot has already landed."""
         if not handles:
             return
-        if hasattr(self.builder, "fetch_all") and len(handles) == len(self.builder.history):
-            levels = self.builder.fetch_all()
-        else:
-            levels = [self.builder.fetch(h) for h, _ in handles]
-            if hasattr(self.builder, "history") and isinstance(self.builder.history, list):
-                self.builder.history.clear()
-        for (h, k), tl in zip(handles, levels):
+        levels = self.builder.pop_levels(ready_only=ready_only)
+        done = handles[:len(levels)]
+        del handles[:len(levels)]
+        for (h, k), tl in zip(done, levels):
             tree = levels_to_tree(tl, self.binning)
             forest.add(tree, k)
             for d in tl.decs:
@@ -310,6 +312,10 @@ class SharedTreeTrainer:
 
     # defaults, overridden
     def _amax_for_build(self):
+        return None
+
+    def _leaf_native(self, t, k):
+        """Optional (log_link, scale, kclamp, max_abs) for device-side closed-form leaf values."""
         return None
 
     def _hist_packed(self) -> bool:

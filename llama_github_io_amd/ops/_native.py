@@ -25,7 +25,7 @@ _HIP_SIGS = {
     "h2o_hist_build": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int,
                        c_int, c_void_p, c_void_p, c_void_p],
     "h2o_split_find": [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_double, c_double,
-                       c_double, c_double, c_double, c_int, c_int, c_ull, c_int, c_void_p, c_void_p],
+                       c_double, c_double, c_double, c_int, c_int, c_ull, c_int, c_void_p, c_void_p, c_void_p],
     "h2o_split_reduce": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_ull, c_int, c_void_p, c_void_p],
     "h2o_plan": [c_void_p] * 14 + [c_int, c_int, c_double, c_int, c_int, c_void_p],
     "h2o_ranges": [c_void_p] * 6,
@@ -34,7 +34,10 @@ _HIP_SIGS = {
     "h2o_route": [c_void_p] * 6 + [c_int] + [c_void_p] * 12 + [c_int, c_int, c_int, c_void_p],
     "h2o_bin_assign": [c_void_p, c_ll, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "h2o_amax": [c_void_p, c_ll, c_void_p, c_void_p],
-    "h2o_qscale": [c_void_p, c_void_p, c_void_p],
+    "h2o_qscale": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p],
+    "h2o_hist_reduce": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
+                        c_void_p, c_void_p],
+    "h2o_leaf_values": [c_void_p, c_int, c_int, c_double, c_double, c_double, c_void_p, c_void_p],
     "h2o_gbm_step": [c_ll, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_float, c_ull,
                      ctypes.c_float, c_void_p, c_void_p, c_void_p],
     "h2o_add_leaf": [c_ll, c_void_p, c_int, c_void_p, c_void_p, c_void_p],

@@ -66,61 +66,61 @@ class Tree:
 
 
 def levels_to_tree(tl: TreeLevels, binning, leaf_values=None) -> Tree:
-    vals = tl.leaf_values if leaf_values is None else leaf_values
-    recs = []  # [feat, thr, bin, na_left, is_cat, bits, nbits, left, right, value, cover, gain]
+    """Flatten level-wise decisions into a node array (root 0, children appended in visit order).
+    Hot on the host during training (one call per tree, overlapped with GPU work): per-level columns
+    are pulled out of the structured records once, the node loop touches only Python scalars."""
+    vals = (tl.leaf_values if leaf_values is None else leaf_values)
+    vals = [] if vals is None else np.asarray(vals, dtype=np.float64).tolist()
+    nv = len(vals)
+    feat, thr, bins, nal, iscat, bits, nbits, left, right, value, cover, gain = ([] for _ in range(12))
 
-    def new(cover):
-        recs.append([-1, 0.0, 0, 0, 0, None, 0, -1, -1, 0.0, cover, 0.0])
-        return len(recs) - 1
+    def new(c):
+        feat.append(-1); thr.append(0.0); bins.append(0); nal.append(0); iscat.append(0); bits.append(None)
+        nbits.append(0); left.append(-1); right.append(-1); value.append(0.0); cover.append(c); gain.append(0.0)
+        return len(feat) - 1
 
     ids = [new(tl.root_weight)]
     for d, decs in enumerate(tl.decs):
+        fz, bz, nz, cz = decs["feat"].tolist(), decs["bin"].tolist(), decs["na_left"].tolist(), decs["is_cat"].tolist()
+        gz, wlz, wrz = decs["gain"].tolist(), decs["wl"].tolist(), decs["wr"].tolist()
+        clz, crz = np.asarray(tl.child_l[d]).tolist(), np.asarray(tl.child_r[d]).tolist()
         nxt = {}
-        for i in range(len(decs)):
+        for i in range(len(fz)):
             g = ids[i]
-            dd = decs[i]
-            cl, cr = int(tl.child_l[d][i]), int(tl.child_r[d][i])
-            if dd["feat"] < 0:
-                recs[g][9] = float(vals[-1 - cl]) if cl < 0 and -1 - cl < len(vals) else 0.0
+            f, cl, cr = fz[i], clz[i], crz[i]
+            if f < 0:
+                value[g] = vals[-1 - cl] if cl < 0 and -1 - cl < nv else 0.0
                 continue
-            f = int(dd["feat"])
-            r = recs[g]
-            r[0] = f
-            r[2] = int(dd["bin"])
-            r[3] = int(dd["na_left"])
-            r[4] = int(dd["is_cat"])
-            r[11] = float(dd["gain"])
-            if dd["is_cat"]:
+            feat[g], bins[g], nal[g], iscat[g], gain[g] = f, bz[i], nz[i], cz[i], gz[i]
+            if cz[i]:
                 nl = int(binning.nlevels[f])
-                bits_b = dd["bits"]
+                bits_b = decs["bits"][i]
                 m = binning.level_to_bin[f] if binning.level_to_bin else None
                 lv = np.arange(nl)
                 bl = lv if m is None else m[lv]
                 inleft = ((bits_b[bl >> 5] >> (bl & 31).astype(np.uint32)) & 1).astype(bool)
                 words = np.zeros((nl + 31) // 32, dtype=np.uint32)
-                for lvl in np.nonzero(inleft)[0]:
-                    words[lvl >> 5] |= np.uint32(1 << (int(lvl) & 31))
-                r[5], r[6], r[1] = words, nl, 0.0
+                lvl = np.nonzero(inleft)[0]
+                np.bitwise_or.at(words, lvl >> 5, (np.uint32(1) << (lvl & 31).astype(np.uint32)))
+                bits[g], nbits[g], thr[g] = words, nl, 0.0
             else:
-                b = int(dd["bin"])
+                b = bz[i]
                 e = binning.edges[f]
-                r[1] = float("inf") if b >= NA_BIN or b - 1 >= len(e) else float(e[b - 1])
-            for side, c, w in ((7, cl, float(dd["wl"])), (8, cr, float(dd["wr"]))):
+                thr[g] = float("inf") if b >= NA_BIN or b - 1 >= len(e) else float(e[b - 1])
+            for c, w, arr in ((cl, wlz[i], left), (cr, wrz[i], right)):
                 k = new(w)
-                r[side] = k
+                arr[g] = k
                 if c >= 0:
                     nxt[c] = k
                 else:
-                    lid = -1 - c
-                    recs[k][9] = float(vals[lid]) if lid < len(vals) else 0.0
+                    value[k] = vals[-1 - c] if -1 - c < nv else 0.0
         ids = [nxt[c] for c in sorted(nxt)]
-    cols = list(zip(*recs))
-    return Tree(feat=np.asarray(cols[0], dtype=np.int32), thr=np.asarray(cols[1], dtype=np.float32),
-                bin=np.asarray(cols[2], dtype=np.int32), na_left=np.asarray(cols[3], dtype=np.int8),
-                is_cat=np.asarray(cols[4], dtype=np.int8), cat_bits=list(cols[5]),
-                cat_nbits=np.asarray(cols[6], dtype=np.int32), left=np.asarray(cols[7], dtype=np.int32),
-                right=np.asarray(cols[8], dtype=np.int32), value=np.asarray(cols[9], dtype=np.float32),
-                cover=np.asarray(cols[10], dtype=np.float64), gain=np.asarray(cols[11], dtype=np.float64))
+    return Tree(feat=np.asarray(feat, dtype=np.int32), thr=np.asarray(thr, dtype=np.float32),
+                bin=np.asarray(bins, dtype=np.int32), na_left=np.asarray(nal, dtype=np.int8),
+                is_cat=np.asarray(iscat, dtype=np.int8), cat_bits=bits,
+                cat_nbits=np.asarray(nbits, dtype=np.int32), left=np.asarray(left, dtype=np.int32),
+                right=np.asarray(right, dtype=np.int32), value=np.asarray(value, dtype=np.float32),
+                cover=np.asarray(cover, dtype=np.float64), gain=np.asarray(gain, dtype=np.float64))
 
 
 class Forest:

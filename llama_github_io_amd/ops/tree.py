@@ -333,12 +333,10 @@ class RefTreeBuilder:
         self.history.append(res)
         return len(self.history) - 1
 
-    def fetch(self, handle):
-        return self.history[handle]
-
-    def fetch_all(self):
-        out = list(self.history)
-        self.history.clear()
+    def pop_levels(self, ready_only: bool = False) -> list:
+        """Built trees in build order (the reference builder is synchronous: all are ready)."""
+        out = list(getattr(self, "history", []))
+        self.history = []
         return out
 
 
@@ -380,12 +378,14 @@ class GpuTreeBuilder:
         N, T = self.N, self.TILE
         self.caps = [min(1 << d, node_cap) for d in range(D)] + [1]
         capmax = max(self.caps)
-        self.slot = F * 2 * NBIN + F + 1
-        self.slot += self.slot & 1
+        self.used = F * 2 * NBIN + F + 1      # doubles of a node histogram slot actually written
+        self.slot = self.used + (self.used & 1)
         self.hist = [torch.empty(capmax * self.slot, dtype=torch.float64, device=dev) for _ in range(2)]
         # compact histograms of the BUILT children of a level, slot = parent index (<= caps[d] slots):
         # the only histogram bytes a row-sharded run all-reduces per level
         self.hbuild = torch.empty(max(self.caps[:D]) * self.slot, dtype=torch.float64, device=dev)
+        # per-block partial histograms of one level (k_hist_build -> k_hist_reduce): G + nodes slots
+        self.partials = torch.empty((grid + capmax) * self.slot, dtype=torch.float64, device=dev)
         self.tiles_cap = [(N + T - 1) // T + c for c in self.caps]
         self.cand = torch.empty(capmax * F * CAND_BYTES, dtype=torch.uint8, device=dev)
         self.scratch = torch.empty(2 * capmax + 16, dtype=torch.int32, device=dev)
@@ -416,11 +416,14 @@ class GpuTreeBuilder:
             ar.add(f"nl{d}", c * 4)                # even levels: rows going left (filled by the odd-level histogram)
             ar.add(f"cur{d}", c * 16)              # odd levels: region cursors {front, back, start, end}
         ar.add("counters", 16)
+        ar.add("rootw", 8)
         ar.add("leafval", self.leaf_cap * 4)
         self.arena = torch.zeros(ar.off, dtype=torch.uint8, device=dev)
         self.av = {}
+        self._off = {}
         for name, off, nb in ar.items:
             self.av[name] = self.arena[off:off + nb]
+            self._off[name] = (off, nb)
         # level-0 constants
         n_tiles0 = (N + T - 1) // T
         root = np.zeros(1, dtype=NODE_DT)
@@ -429,42 +432,44 @@ class GpuTreeBuilder:
         self.av["meta0"].copy_(torch.from_numpy(np.array([1, n_tiles0, n_tiles0, 0], dtype=np.int32).view(np.uint8)))
         self.av["tp0"][:8].copy_(torch.from_numpy(np.array([0, n_tiles0], dtype=np.int32).view(np.uint8)))
         self.av["bp0"][:8].copy_(torch.from_numpy(np.array([0, n_tiles0], dtype=np.int32).view(np.uint8)))
-        self.history = []
+        self.history = []       # (pinned host snapshot, copy-done event) per built tree, in build order
+        self._pinned_pool = []
 
     def _p(self, name):
         return self.av[name].data_ptr()
 
     def build(self, aux_static: torch.Tensor, feat_ok: torch.Tensor | None = None, k_cols: int = 0, seed: int = 0,
-              leaf_fn=None, amax_bits: torch.Tensor | None = None, packed: bool = False):
+              leaf_fn=None, amax_bits: torch.Tensor | None = None, packed: bool = False, leaf_native=None):
         """Launch one tree. ``leaf_fn(leafsum[L,2] f64) -> leaf values f32`` runs on device before the
-        arena snapshot, so values travel to the host with the structure (no extra sync).
+        arena snapshot, so values travel to the host with the structure (no extra sync);
+        ``leaf_native = (log_link, scale, kclamp, max_abs)`` instead computes closed-form Newton leaf values
+        in one HIP launch (k_leaf_values).
         ``amax_bits`` (int32[2*AMAX_SHARDS], max |aux.x|, |aux.y| as float bits) may be produced by a fused
-        prepare kernel; otherwise it is computed here. ``packed`` (caller guarantees aux.x is a 0/1 or small
-        integer row weight) switches the LDS histograms to one packed count|wY atomic per (row, feature)."""
+        prepare kernel; otherwise it is computed here (k_qscale re-zeroes it after reading). ``packed``
+        (caller guarantees aux.x is a 0/1 or small integer row weight) switches the LDS histograms to one
+        packed count|wY atomic per (row, feature)."""
         pk = int(bool(packed))
         lib, s = self.lib, nat.stream_ptr(self.dev)
         F, D, p, T = self.F, self.D, self.p, self.TILE
         assert aux_static.shape == (self.N, 4) and aux_static.dtype == torch.float32 and aux_static.is_contiguous()
         fo = self.feat_ok_all if feat_ok is None else feat_ok
-        self.av["counters"].zero_()
-        self.leafsum.zero_()
-        self.hist[0][: self.slot].zero_()
-        slot = self.slot
-        # per-tree fixed-point scales for the int64 LDS histograms: |v| * 2^40 / max|v| <= 2^40
+        slot, used, part = self.slot, self.used, self.partials.data_ptr()
+        dist = coll.is_dist()
+        # per-tree fixed-point scales for the int64 LDS histograms (|v| * 2^40 / max|v| <= 2^40); the same
+        # launch resets the leaf counters, the leaf sums and the amax shards
         if amax_bits is None:
             amax_bits = self.amax_bits
-            amax_bits.zero_()
             nat.check(lib.h2o_amax(aux_static.data_ptr(), self.N, amax_bits.data_ptr(), s), "amax")
-        nat.check(lib.h2o_qscale(amax_bits.data_ptr(), self.qs.data_ptr(), s), "qscale")
+        nat.check(lib.h2o_qscale(amax_bits.data_ptr(), self.qs.data_ptr(), self._p("counters"),
+                                 self.leafsum.data_ptr(), self.leafsum.numel(), s), "qscale")
         qs = self.qs.data_ptr()
         g0 = min(self.tiles_cap[0], self.grid)
         nat.check(lib.h2o_hist_build(self.master.data_ptr(), self.stride, aux_static.data_ptr(), self._p("nodes0"),
-                                     self._p("bp0"), self._p("meta0"), F, self.hist[0].data_ptr(), slot, qs, g0, pk,
-                                     0, 0, s),
+                                     self._p("bp0"), self._p("meta0"), F, part, slot, qs, g0, pk, 0, 0, s),
                   "hist_build")
+        nat.check(lib.h2o_hist_reduce(part, slot, used, self._p("nodes0"), self._p("bp0"), self._p("meta0"), 1, g0,
+                                      self.hist[0].data_ptr(), 0, 0, s), "hist_reduce")
         coll.all_reduce_(self.hist[0][:slot])
-        # Σw over feature 0's bins = root weight (bin-major slot: (bin, f, r) at bin * 2F + 2f + r)
-        self.root_w = self.hist[0][0:2 * NBIN * F:2 * F].sum().reshape(1)
         mono = 0 if self.mono_f is None else self.mono_f.data_ptr()
         seed = int(seed) & _M64
         hb = self.hbuild
@@ -495,7 +500,7 @@ class GpuTreeBuilder:
             nat.check(lib.h2o_split_find(hc.data_ptr(), slot, self._p(f"meta{d}"), cap, F, self.nbins_f.data_ptr(),
                                          self.iscat_f.data_ptr(), mono, p.min_w, p.min_split_improvement, p.lam,
                                          p.alpha, p.gamma, p.mode, int(p.random_split), seed, d,
-                                         self.cand.data_ptr(), s), "split_find")
+                                         self.cand.data_ptr(), self._p("rootw") if d == 0 else 0, s), "split_find")
             nat.check(lib.h2o_split_reduce(self.cand.data_ptr(), self._p(f"meta{d}"), cap, F, fo.data_ptr(), int(k_cols),
                                            seed, d, self._p(f"dec{d}"), s), "split_reduce")
             nat.check(lib.h2o_plan(self._p(f"nodes{d}"), self._p(f"meta{d}"), self._p(f"dec{d}"), self._p(f"nl{d}"),
@@ -507,60 +512,79 @@ class GpuTreeBuilder:
                 # last level: every row lands on a leaf (routed from the last regrouped level)
                 route(d - 1 if odd else d, two=odd, move=False)
                 break
-            nat.check(lib.h2o_zero_hist(hb.data_ptr(), self._p(f"nodes{d + 1}"), self._p(f"meta{d + 1}"),
-                                        self.caps[d + 1], slot, s), "zero_hist")
-            gh = min(self.tiles_cap[d], self.grid)
             if not odd:
                 # level d+1 (odd) is histogrammed straight from level d's ranges, filtered by level d's
                 # decisions; the pass also counts each parent's left-goers for the next regrouping
+                gh = min(self.tiles_cap[d], self.grid)
                 sb, sa, _ = level_buf(d)
                 nat.check(lib.h2o_hist_build(sb, self.stride, sa, self._p(f"nodes{d + 1}"), self._p(f"bp{d + 1}"),
-                                             self._p(f"meta{d + 1}"), F, hb.data_ptr(), slot, qs, gh, pk,
+                                             self._p(f"meta{d + 1}"), F, part, slot, qs, gh, pk,
                                              self._p(f"dec{d}"), self._p(f"nl{d}"), s), "hist_build")
             else:
                 # regroup level d-1's rows two levels down, then histogram level d+1 (even) contiguously
                 route(d - 1, two=True, move=True)
                 nat.check(lib.h2o_ranges(self._p(f"nodes{d + 1}"), self._p(f"cur{d}"), self._p(f"tp{d + 1}"),
                                          self._p(f"bp{d + 1}"), self._p(f"meta{d + 1}"), s), "ranges")
+                gh = min(self.tiles_cap[d + 1], self.grid)
                 sb, sa, _ = level_buf(d + 1)
                 nat.check(lib.h2o_hist_build(sb, self.stride, sa, self._p(f"nodes{d + 1}"), self._p(f"bp{d + 1}"),
-                                             self._p(f"meta{d + 1}"), F, hb.data_ptr(), slot, qs,
-                                             min(self.tiles_cap[d + 1], self.grid), pk, 0, 0, s), "hist_build")
-            # one built child per parent: the compact buffer holds at most caps[d] slots
-            coll.all_reduce_(hb[: self.caps[d] * slot])
-            nat.check(lib.h2o_subtract(hn.data_ptr(), hc.data_ptr(), hb.data_ptr(), self._p(f"nodes{d + 1}"),
-                                       self._p(f"meta{d + 1}"), self.caps[d + 1], slot, s), "subtract")
+                                             self._p(f"meta{d + 1}"), F, part, slot, qs, gh, pk, 0, 0, s),
+                          "hist_build")
+            if not dist:
+                # single process: partial sums + sibling subtraction in one pass, straight into hist_next
+                nat.check(lib.h2o_hist_reduce(part, slot, used, self._p(f"nodes{d + 1}"), self._p(f"bp{d + 1}"),
+                                              self._p(f"meta{d + 1}"), self.caps[d + 1], gh, 0, hn.data_ptr(),
+                                              hc.data_ptr(), s), "hist_reduce")
+            else:
+                # row-sharded: one built child per parent into the compact buffer (<= caps[d] slots), the
+                # only histogram bytes all-reduced per level, then the sibling subtraction
+                nat.check(lib.h2o_hist_reduce(part, slot, used, self._p(f"nodes{d + 1}"), self._p(f"bp{d + 1}"),
+                                              self._p(f"meta{d + 1}"), self.caps[d + 1], gh, hb.data_ptr(), 0, 0,
+                                              s), "hist_reduce")
+                coll.all_reduce_(hb[: self.caps[d] * slot])
+                nat.check(lib.h2o_subtract(hn.data_ptr(), hc.data_ptr(), hb.data_ptr(), self._p(f"nodes{d + 1}"),
+                                           self._p(f"meta{d + 1}"), self.caps[d + 1], slot, s), "subtract")
         coll.all_reduce_(self.leafsum)
-        if leaf_fn is not None:
+        if leaf_native is not None:
+            lg, scale, kclamp, mx = leaf_native
+            nat.check(lib.h2o_leaf_values(self.leafsum.data_ptr(), self.leaf_cap, int(lg), float(scale), float(kclamp),
+                                          float(mx), self._p("leafval"), s), "leaf_values")
+        elif leaf_fn is not None:
             vals = leaf_fn(self.leafsum)
             self.av["leafval"].view(torch.float32)[: vals.numel()].copy_(vals.to(torch.float32))
-        snap = self.arena.clone()
-        rw = self.root_w.clone()
-        self.history.append((snap, rw))
+        # the tree's structure travels to pinned host memory asynchronously: the host decodes finished
+        # trees (pop_levels(ready_only=True)) while the GPU builds the next ones
+        host = self._pinned_pool.pop() if self._pinned_pool else torch.empty(self.arena.numel(), dtype=torch.uint8,
+                                                                               pin_memory=True)
+        host.copy_(self.arena, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.history.append((host, ev))
         return len(self.history) - 1
 
-    def fetch(self, handle) -> TreeLevels:
-        snap, rw = self.history[handle]
-        host = snap.cpu().numpy()
-        rwh = float(rw.cpu())
-        return self._decode(host, rwh)
+    def leaf_values_view(self) -> torch.Tensor:
+        """Device float32 leaf values of the last built tree (valid until the next build writes them)."""
+        return self.av["leafval"].view(torch.float32)
 
-    def fetch_all(self) -> list:
-        if not self.history:
-            return []
-        snaps = torch.stack([h[0] for h in self.history]).cpu().numpy()
-        rws = torch.cat([h[1] for h in self.history]).cpu().numpy()
-        out = [self._decode(snaps[i], float(rws[i])) for i in range(len(self.history))]
-        self.history.clear()
+    def pop_levels(self, ready_only: bool = False) -> list:
+        """Decode built trees in build order: all of them, or (``ready_only``) the prefix whose snapshot
+        copies have completed — never blocks in that mode."""
+        out = []
+        while self.history:
+            host, ev = self.history[0]
+            if ready_only and not ev.query():
+                break
+            ev.synchronize()
+            self.history.pop(0)
+            hn = host.numpy()
+            o = self._off["rootw"][0]
+            out.append(self._decode(hn, float(hn[o:o + 8].view(np.float64)[0])))
+            self._pinned_pool.append(host)
         return out
 
     def _decode(self, host: np.ndarray, root_weight: float) -> TreeLevels:
-        off = {}
-        ar_off = 0
-        # recompute offsets in the same order as construction
-        for name, view in self.av.items():
-            o = view.data_ptr() - self.arena.data_ptr()
-            off[name] = (o, view.numel())
+        off = self._off
+
         def arr(name, dt):
             o, nb = off[name]
             return host[o:o + nb].view(dt)
