@@ -390,7 +390,8 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
 // Block b covers tiles [b*per, (b+1)*per), so node n's blocks are b in [bp[n]/per, (bp[n+1]-1)/per] and
 // its partials sit at b + n. With hist_next != nullptr (single process) the sibling subtraction is fused:
 // hist_next[n] = sum and hist_next[sib] = hist_cur[parent] - sum (no compact-buffer round trip).
-__global__ __launch_bounds__(256) void k_hist_reduce(
+#define RW 8   // waves per k_hist_reduce block: wave w sums partials b0 + w, b0 + w + RW, ... of 64 columns
+__global__ __launch_bounds__(RW * 64) void k_hist_reduce(
     const double* __restrict__ partials, int slot_doubles, int used, const Node* __restrict__ nodes,
     const int* __restrict__ bp, const int* __restrict__ meta, int G, double* __restrict__ out,
     double* __restrict__ hist_next, const double* __restrict__ hist_cur) {
@@ -398,20 +399,36 @@ __global__ __launch_bounds__(256) void k_hist_reduce(
   if (node >= meta[0]) return;
   const Node nd = nodes[node];
   if (!nd.build) return;
+  __shared__ double red[RW][64];
   const int n_tiles = meta[2];
   const int per = n_tiles > 0 ? (n_tiles + G - 1) / G : 1;
   const int t0 = bp[node], t1 = bp[node + 1];
   const int b0 = t0 / per, b1 = t1 > t0 ? (t1 - 1) / per : b0 - 1;
   const int oslot = nd.parent >= 0 ? nd.parent : 0;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < used; i += gridDim.x * blockDim.x) {
-    double acc = 0.0;
-    for (int b = b0; b <= b1; ++b) acc += partials[(size_t)(b + node) * slot_doubles + i];
-    if (out) out[(size_t)oslot * slot_doubles + i] = acc;
-    if (hist_next) {
-      hist_next[(size_t)node * slot_doubles + i] = acc;
-      if (nd.sib >= 0)
-        hist_next[(size_t)nd.sib * slot_doubles + i] = hist_cur[(size_t)nd.parent * slot_doubles + i] - acc;
-    }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + lane;
+  const int ic = min(i, used - 1);
+  // 4 independent loads in flight per lane; fixed summation order -> deterministic result
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  int b = b0 + w;
+  for (; b + 3 * RW <= b1; b += 4 * RW) {
+    a0 += partials[(size_t)(b + node) * slot_doubles + ic];
+    a1 += partials[(size_t)(b + RW + node) * slot_doubles + ic];
+    a2 += partials[(size_t)(b + 2 * RW + node) * slot_doubles + ic];
+    a3 += partials[(size_t)(b + 3 * RW + node) * slot_doubles + ic];
+  }
+  for (; b <= b1; b += RW) a0 += partials[(size_t)(b + node) * slot_doubles + ic];
+  red[w][lane] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (w != 0 || i >= used) return;
+  double acc = red[0][lane];
+#pragma unroll
+  for (int k = 1; k < RW; ++k) acc += red[k][lane];
+  if (out) out[(size_t)oslot * slot_doubles + i] = acc;
+  if (hist_next) {
+    hist_next[(size_t)node * slot_doubles + i] = acc;
+    if (nd.sib >= 0)
+      hist_next[(size_t)nd.sib * slot_doubles + i] = hist_cur[(size_t)nd.parent * slot_doubles + i] - acc;
   }
 }
 
@@ -1222,9 +1239,8 @@ int h2o_hist_build(const void* bins, int stride, const void* aux, const void* no
 int h2o_hist_reduce(const void* partials, int slot_doubles, int used, const void* nodes, const void* bp,
                     const void* meta, int cap, int grid, void* out, void* hist_next, const void* hist_cur,
                     hipStream_t s) {
-  int gx = (used + 255) / 256;
-  if (gx > 64) gx = 64;
-  hipLaunchKernelGGL(k_hist_reduce, dim3(gx, cap), dim3(256), 0, s, (const double*)partials, slot_doubles, used,
+  const int gx = (used + 63) / 64;
+  hipLaunchKernelGGL(k_hist_reduce, dim3(gx, cap), dim3(RW * 64), 0, s, (const double*)partials, slot_doubles, used,
                      (const Node*)nodes, (const int*)bp, (const int*)meta, grid, (double*)out, (double*)hist_next,
                      (const double*)hist_cur);
   return (int)hipGetLastError();
