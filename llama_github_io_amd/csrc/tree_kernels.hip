@@ -315,8 +315,8 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
     const Dec* __restrict__ pdec, int* __restrict__ nl_out) {
   constexpr bool packed = PACKED;
   extern __shared__ __attribute__((aligned(16))) long long smem64[];
-  long long* h = smem64;                                 // 2 * HPLANE
-  float* nayy = (float*)(smem64 + 2 * HPLANE);           // FTILE
+  long long* h = smem64;                                 // 2 planes (PACKED: 1 -> two blocks per CU fit)
+  float* nayy = (float*)(smem64 + (PACKED ? 1 : 2) * HPLANE);   // FTILE
   double* red = (double*)(nayy + FTILE);                 // 64 doubles scratch
 
   // tile_prefix here is the BUILD-tile prefix (only nodes with build=1 own tiles) and meta[2] the number
@@ -1228,7 +1228,8 @@ int h2o_hist_build(const void* bins, int stride, const void* aux, const void* no
                    const void* meta, int F, void* partials, int slot_doubles, const void* qs, int grid, int packed,
                    const void* pdec, void* nl_out, hipStream_t s) {
   const int nft = (F + FTILE - 1) / FTILE;
-  const size_t lds = HIST_LDS_BYTES + 64 * 8;
+  // packed mode needs one int64 plane (66 KB): two 16-wave blocks share a CU (32 waves, 8 per SIMD)
+  const size_t lds = (packed ? HIST_LDS_BYTES - HPLANE * 8 : HIST_LDS_BYTES) + 64 * 8;
   const dim3 gr(grid, nft);
   if (packed) launch_hist<true>(gr, lds, s, bins, stride, aux, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out);
   else launch_hist<false>(gr, lds, s, bins, stride, aux, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out);

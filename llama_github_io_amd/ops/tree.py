@@ -16,6 +16,7 @@ sorted by mean response. Mode 1 is XGBoost's Newton gain G²/(H+λ) with L1 soft
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -385,7 +386,9 @@ class GpuTreeBuilder:
         # the only histogram bytes a row-sharded run all-reduces per level
         self.hbuild = torch.empty(max(self.caps[:D]) * self.slot, dtype=torch.float64, device=dev)
         # per-block partial histograms of one level (k_hist_build -> k_hist_reduce): G + nodes slots
-        self.partials = torch.empty((grid + capmax) * self.slot, dtype=torch.float64, device=dev)
+        # (packed histograms fit two blocks per CU; H2O_HIST_BPC=2 launches hist_bpc * grid blocks)
+        self.hist_bpc = int(os.environ.get("H2O_HIST_BPC", "1"))   # measured: 2 is 3-14 % slower
+        self.partials = torch.empty((self.hist_bpc * grid + capmax) * self.slot, dtype=torch.float64, device=dev)
         self.tiles_cap = [(N + T - 1) // T + c for c in self.caps]
         self.cand = torch.empty(capmax * F * CAND_BYTES, dtype=torch.uint8, device=dev)
         self.scratch = torch.empty(2 * capmax + 16, dtype=torch.int32, device=dev)
@@ -463,7 +466,8 @@ class GpuTreeBuilder:
         nat.check(lib.h2o_qscale(amax_bits.data_ptr(), self.qs.data_ptr(), self._p("counters"),
                                  self.leafsum.data_ptr(), self.leafsum.numel(), s), "qscale")
         qs = self.qs.data_ptr()
-        g0 = min(self.tiles_cap[0], self.grid)
+        hgrid = self.grid * (self.hist_bpc if pk else 1)
+        g0 = min(self.tiles_cap[0], hgrid)
         nat.check(lib.h2o_hist_build(self.master.data_ptr(), self.stride, aux_static.data_ptr(), self._p("nodes0"),
                                      self._p("bp0"), self._p("meta0"), F, part, slot, qs, g0, pk, 0, 0, s),
                   "hist_build")
@@ -515,7 +519,7 @@ class GpuTreeBuilder:
             if not odd:
                 # level d+1 (odd) is histogrammed straight from level d's ranges, filtered by level d's
                 # decisions; the pass also counts each parent's left-goers for the next regrouping
-                gh = min(self.tiles_cap[d], self.grid)
+                gh = min(self.tiles_cap[d], hgrid)
                 sb, sa, _ = level_buf(d)
                 nat.check(lib.h2o_hist_build(sb, self.stride, sa, self._p(f"nodes{d + 1}"), self._p(f"bp{d + 1}"),
                                              self._p(f"meta{d + 1}"), F, part, slot, qs, gh, pk,
@@ -525,7 +529,7 @@ class GpuTreeBuilder:
                 route(d - 1, two=True, move=True)
                 nat.check(lib.h2o_ranges(self._p(f"nodes{d + 1}"), self._p(f"cur{d}"), self._p(f"tp{d + 1}"),
                                          self._p(f"bp{d + 1}"), self._p(f"meta{d + 1}"), s), "ranges")
-                gh = min(self.tiles_cap[d + 1], self.grid)
+                gh = min(self.tiles_cap[d + 1], hgrid)
                 sb, sa, _ = level_buf(d + 1)
                 nat.check(lib.h2o_hist_build(sb, self.stride, sa, self._p(f"nodes{d + 1}"), self._p(f"bp{d + 1}"),
                                              self._p(f"meta{d + 1}"), F, part, slot, qs, gh, pk, 0, 0, s),
