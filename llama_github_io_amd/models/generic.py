@@ -14,10 +14,11 @@ class GenericModel(Model):
     algo = "generic"
 
     @staticmethod
-    def from_mojo(path: str, model_id=None) -> "GenericModel":
+    def from_mojo(path: str, model_id=None, prefix: str = "") -> "GenericModel":
+        from ..mojo import algos as A
         from ..mojo.reader import _floats, parse_mojo
         from ..ops.forest import Forest
-        mj = parse_mojo(path)
+        mj = parse_mojo(path, prefix)
         ki = mj["info"]
         if mj["state"] is not None:                    # framework-native payload
             from ..persist import _from_state
@@ -71,13 +72,53 @@ class GenericModel(Model):
                 m.means = _floats(ki["standardize_means"])
                 m.mults = _floats(ki["standardize_mults"])
                 m.modes = [int(v) for v in _floats(ki["standardize_modes"])]
+        elif algo == "deeplearning":
+            m.dl = A.load_deeplearning(ki)
+        elif algo == "pca":
+            m.pca = A.load_pca(ki, mj["files"]["eigenvectors_raw"])
+            m.output["model_category"] = "DimReduction"
+        elif algo == "word2vec":
+            from .word2vec import Word2VecModel
+            words, V = A.load_word2vec(ki, mj["files"]["vectors"], mj["files"]["vocabulary"].decode())
+            inner = Word2VecModel(m.key + "_w2v", {}, info)
+            inner.words, inner.vectors = words, V
+            inner.vocab = {w: i for i, w in enumerate(words)}
+            m.inner = inner
+            m.output["model_category"] = "WordEmbedding"
+        elif algo == "isotonicregression":
+            from .isotonic import IsotonicModel
+            tx, ty = A.load_isotonic(mj["files"])
+            inner = IsotonicModel(m.key + "_iso", dict(out_of_bounds="clip"), info)
+            inner.thresholds_x, inner.thresholds_y = tx.tolist(), ty.tolist()
+            m.inner = inner
+        elif algo == "stackedensemble":
+            subs = {}
+            for i in range(int(ki.get("submodel_count", 0))):
+                key = ki[f"submodel_key_{i}"]
+                subs[key] = GenericModel.from_mojo(path, key, prefix + ki[f"submodel_dir_{i}"])
+            m.base = [subs[ki[f"base_model{i}"]] for i in range(int(ki["base_models_num"]))
+                      if f"base_model{i}" in ki]
+            m.meta = subs[ki["metalearner"]]
+            m.meta_transform = ki.get("metalearner_transform", "NONE")
         else:
             raise NotImplementedError(f"MOJO algo {algo} not supported by this reader")
         return m
 
+    def __getattr__(self, name):
+        # Word2Vec / isotonic MOJOs delegate their model-specific API (find_synonyms, transform, ...)
+        inner = self.__dict__.get("inner")
+        if inner is not None and not name.startswith("_"):
+            return getattr(inner, name)
+        raise AttributeError(name)
+
     @property
     def model_category(self):
         return self.output.get("model_category", "Regression")
+
+    def _align(self, X, parent_info):
+        """Rows of ``X`` (parent's predictor order) re-ordered into this model's predictor order."""
+        idx = [parent_info.x.index(n) for n in self.info.x]
+        return X[idx]
 
     def default_threshold(self):
         if self.inner is not None:
@@ -166,6 +207,27 @@ class GenericModel(Model):
             if fam in ("binomial", "quasibinomial", "fractionalbinomial"):
                 return torch.stack([1 - mu, mu], 1).float()
             return mu.float()
+        if algo == "deeplearning":
+            from ..mojo import algos as A
+            return A.score_deeplearning(self.dl, X, cat)
+        if algo == "pca":
+            from ..mojo import algos as A
+            return A.score_pca(self.pca, X)
+        if algo == "stackedensemble":
+            cols = []
+            for b in self.base:
+                P = b._predict_tensor(b._align(X, self.info), offset)
+                if cat == "Binomial":
+                    p1 = P[:, 1:2].double()
+                    if self.meta_transform == "Logit":
+                        p1 = torch.logit(p1.clamp(1e-15, 1 - 1e-15))
+                    cols.append(p1)
+                elif cat == "Multinomial":
+                    cols.append(P.double())
+                else:
+                    cols.append(P.reshape(-1, 1).double())
+            L1 = torch.cat(cols, 1).T.contiguous().float()
+            return self.meta._predict_tensor(L1, None)
         if algo == "kmeans":
             Z, off = self._design(X)
             if self.std:

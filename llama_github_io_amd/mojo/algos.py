@@ -1,0 +1,316 @@
+"""Reference-layout MOJO payloads beyond the tree / GLM / KMeans families.
+
+Each ``write_*`` fills ``model.ini`` keys (``kv``) and binary/text entries (``blobs``) exactly as the
+reference writer does, so the zip is readable by h2o-genmodel; each ``score_*`` reproduces the
+reference genmodel scorer on device tensors (``GenericModel`` dispatches to them):
+
+* DeepLearning — ``h2o-algos/.../deeplearning/DeepLearningMojoWriter.java:writeModelData``,
+  ``h2o-genmodel/.../algos/deeplearning/DeeplearningMojoModel.java:score0`` / ``NeuralNetwork.java``
+  (weights ``[out][in]`` row-major, Maxout ``[out][in][k]``; categoricals first, one-hot with an extra
+  NA level per column; numerics ``(x - norm_sub) * norm_mul``, NA -> 0).
+* PCA — ``algos/pca/PCAMojoReader.java`` / ``PCAMojoModel.java:score0`` (``eigenvectors_raw``
+  big-endian doubles, ``permutation`` cats-then-nums).
+* Word2Vec — ``algos/word2vec/Word2VecMojoReader.java`` (``vectors`` big-endian float32 blob,
+  ``vocabulary`` text).
+* Isotonic regression — ``ModelMojoReader.readIsotonicCalibrator`` (``calib/thresholds_x|y``: int32
+  count + big-endian doubles).
+* Stacked ensemble — ``MultiModelMojoReader`` / ``StackedEnsembleMojoReader.java`` (nested MOJOs under
+  ``models/<key>/``, ``base_model<i>`` / ``metalearner`` keys).
+
+Our own trainers differ from H2O in two imputation details that the writers fold into the exported
+parameters so the reference scorer reproduces this framework's predictions: DeepLearning imputes a
+missing categorical with its training mode (exported as an NA level whose first-layer weights are the
+mode level's), and dropout is inverted at training time (exported ratios are 0).
+"""
+from __future__ import annotations
+
+import struct
+
+import numpy as np
+import torch
+
+_ACT = {"rectifier": "Rectifier", "tanh": "Tanh", "exprectifier": "ExpRectifier", "maxout": "Maxout",
+        "linear": "Linear"}
+
+
+def _arr(v):
+    return "[" + ", ".join(repr(float(x)) if isinstance(x, float) else str(x) for x in v) + "]"
+
+
+def _darr(v):
+    return "[" + ", ".join(repr(float(x)) for x in v) + "]"
+
+
+# ================================================================================================ DL
+def dl_columns(model):
+    """DeepLearning MOJOs list categorical predictors first (the reference DataInfo column order)."""
+    info = model.info
+    ex = model.expander
+    order = list(ex.cats) + list(ex.nums)
+    cols = [info.x[j] for j in order] + ([info.response] if info.response else [])
+    doms = [info.domains[j] for j in order] + ([info.response_domain] if info.response else [])
+    return cols, doms
+
+
+def write_deeplearning(model, kv, blobs):
+    ex = model.expander
+    cfg = model._cfg
+    info = model.info
+    start = 0 if ex.use_all else 1
+    # reference one-hot block per categorical: (L - start) levels + 1 NA level
+    ref_off, src_cols = [0], []
+    for i, j in enumerate(ex.cats):
+        L = len(info.domains[j] or [])
+        n = L - start
+        src_cols += [ex.cat_offsets[i] + c for c in range(n)]
+        mode_col = ex.cat_offsets[i] + ex.cat_modes[i] - start if ex.cat_modes[i] - start >= 0 else -1
+        src_cols.append(mode_col)                      # NA level -> the mode level's weights (our imputation)
+        ref_off.append(ref_off[-1] + n + 1)
+    src_cols += [ex.num_off + k for k in range(len(ex.nums))]
+    lins = list(model.net.hidden) + [model.net.out]
+    units = [len(src_cols)] + list(cfg["hidden"]) + [int(cfg["n_out"])]
+    maxout = bool(cfg["maxout"])
+    act = "Maxout" if maxout else _ACT.get(str(cfg["act"]).lower(), "Rectifier")
+    kv["mini_batch_size"] = 1
+    kv["nums"] = len(ex.nums)
+    kv["cats"] = len(ex.cats)
+    kv["cat_offsets"] = _arr(ref_off)
+    if ex.standardize and ex.nums:
+        kv["norm_mul"] = _darr((1.0 / ex.num_sd).cpu().tolist())
+        kv["norm_sub"] = _darr(ex.num_mean.cpu().tolist())
+    else:
+        kv["norm_mul"] = "null"
+        kv["norm_sub"] = "null"
+    dist = model.output.get("distribution", "gaussian")
+    if model.model_category in ("Binomial", "Multinomial"):
+        dist = "bernoulli" if model.model_category == "Binomial" else "multinomial"
+    regress = model.model_category == "Regression"
+    if regress and dist not in ("poisson", "gamma", "tweedie") and (model.resp_sd != 1.0 or model.resp_mu != 0.0):
+        kv["norm_resp_mul"] = _darr([1.0 / model.resp_sd])
+        kv["norm_resp_sub"] = _darr([model.resp_mu])
+    else:
+        kv["norm_resp_mul"] = "null"
+        kv["norm_resp_sub"] = "null"
+    kv["use_all_factor_levels"] = "true" if ex.use_all else "false"
+    kv["activation"] = act
+    kv["distribution"] = dist
+    kv["mean_imputation"] = "true"
+    if ex.cats:
+        kv["cat_modes"] = _arr(ex.cat_modes)
+    kv["neural_network_sizes"] = _arr(units)
+    for li, lin in enumerate(lins):
+        W = lin.weight.detach().double().cpu()
+        b = lin.bias.detach().double().cpu()
+        if li == 0:
+            Wr = torch.zeros(W.shape[0], len(src_cols), dtype=torch.float64)
+            for c, s in enumerate(src_cols):
+                if s >= 0:
+                    Wr[:, c] = W[:, s]
+            W = Wr
+        if maxout and li < len(lins) - 1:
+            H = W.shape[0] // 2
+            # ours: rows [0, H) and [H, 2H) are the two maxout pieces; reference: [out][in][k]
+            W = torch.stack([W[:H], W[H:]], 2)               # [H, in, 2]
+            b = torch.stack([b[:H], b[H:]], 1)               # [H, 2]
+        kv[f"weight_layer{li}"] = _darr(W.reshape(-1).tolist())
+        kv[f"bias_layer{li}"] = _darr(b.reshape(-1).tolist())
+    kv["hidden_dropout_ratios"] = _darr([0.0] * len(lins))
+    kv["_genmodel_encoding"] = "AUTO"
+
+
+def _floats(s):
+    s = (s or "").strip()
+    if s in ("null", ""):
+        return []
+    return [float(x) for x in s.strip("[]").split(",") if x.strip()]
+
+
+def load_deeplearning(ki):
+    units = [int(v) for v in _floats(ki["neural_network_sizes"])]
+    layers = []
+    for li in range(len(units) - 1):
+        layers.append((torch.tensor(_floats(ki[f"weight_layer{li}"]), dtype=torch.float64),
+                       torch.tensor(_floats(ki[f"bias_layer{li}"]), dtype=torch.float64)))
+    return dict(units=units, layers=layers, nums=int(ki["nums"]), cats=int(ki["cats"]),
+                cat_offsets=[int(v) for v in _floats(ki.get("cat_offsets"))], norm_mul=_floats(ki.get("norm_mul")),
+                norm_sub=_floats(ki.get("norm_sub")), resp_mul=_floats(ki.get("norm_resp_mul")),
+                resp_sub=_floats(ki.get("norm_resp_sub")), use_all=ki.get("use_all_factor_levels") == "true",
+                act=ki["activation"], dist=ki.get("distribution", "gaussian"),
+                drop=_floats(ki.get("hidden_dropout_ratios")))
+
+
+def _ref_input(st, X):
+    """GenModel.setInput: [F, N] (MOJO column order) -> [N, P] one-hot + normalised numerics."""
+    N = X.shape[1]
+    dev = X.device
+    off = st["cat_offsets"]
+    ncat = st["cats"]
+    P = (off[ncat] if ncat else 0) + st["nums"]
+    Z = torch.zeros(N, P, dtype=torch.float64, device=dev)
+    for i in range(ncat):
+        c = X[i]
+        na = torch.isnan(c)
+        ci = torch.where(na, torch.zeros_like(c), c).long()
+        idx = ci + off[i] if st["use_all"] else ci - 1 + off[i]
+        valid = st["use_all"] | (ci != 0)
+        idx = torch.where(na | (idx >= off[i + 1]), torch.full_like(idx, off[i + 1] - 1), idx)
+        valid = valid | na
+        rows = torch.nonzero(valid, as_tuple=True)[0]
+        Z[rows, idx[rows]] = 1.0
+    base = off[ncat] if ncat else 0
+    for k in range(st["nums"]):
+        v = X[ncat + k].double()
+        if st["norm_mul"]:
+            v = (v - st["norm_sub"][k]) * st["norm_mul"][k]
+        Z[:, base + k] = torch.nan_to_num(v, nan=0.0)
+    return Z
+
+
+def score_deeplearning(st, X, category):
+    a = _ref_input(st, X)
+    units, act = st["units"], st["act"]
+    nl = len(units) - 1
+    for li in range(nl):
+        W, b = st["layers"][li]
+        W, b = W.to(a.device), b.to(a.device)
+        out_n = units[li + 1]
+        last = li == nl - 1
+        name = act if (not last or category == "AutoEncoder") else ("Softmax" if category in ("Binomial", "Multinomial")
+                                                                    else "Linear")
+        if name.startswith("Maxout"):
+            k = b.numel() // out_n
+            h = torch.einsum("ni,oik->nok", a, W.view(out_n, -1, k)) + b.view(out_n, k)
+            a = h.max(2).values
+        else:
+            h = a @ W.view(out_n, -1).T + b
+            if name.startswith("Rectifier"):
+                a = h.clamp(min=0)
+            elif name.startswith("Tanh"):
+                a = torch.tanh(h)
+            elif name.startswith("ExpRectifier"):
+                a = torch.where(h >= 0, h, torch.expm1(h))
+            elif name == "Softmax":
+                a = torch.softmax(h, 1)
+            else:
+                a = h
+        if "WithDropout" in name and li < len(st["drop"]) and st["drop"][li] > 0:
+            a = a * (1.0 - st["drop"][li])
+    if category in ("Binomial", "Multinomial"):
+        return a.float()
+    if category == "AutoEncoder":
+        if st["norm_mul"]:
+            nn_ = st["nums"]
+            mul = torch.tensor(st["norm_mul"], dtype=torch.float64, device=a.device)
+            sub = torch.tensor(st["norm_sub"], dtype=torch.float64, device=a.device)
+            a[:, -nn_:] = a[:, -nn_:] / mul + sub
+        return a.float()
+    f = a[:, 0]
+    if st["resp_mul"]:
+        f = f / st["resp_mul"][0] + st["resp_sub"][0]
+    if st["dist"] in ("poisson", "gamma", "tweedie", "multinomial"):
+        f = torch.exp(f).clamp(max=1e19)
+    elif st["dist"] in ("bernoulli", "quasibinomial", "modified_huber", "ordinal"):
+        f = torch.sigmoid(f)
+    return f.float()
+
+
+# ================================================================================================ PCA
+def write_pca(model, kv, blobs):
+    ex = model.expander
+    info = model.info
+    start = 0 if ex.use_all else 1
+    offs = list(ex.cat_offsets) + [ex.num_off]
+    kv["use_all_factor_levels"] = "true" if ex.use_all else "false"
+    kv["pca_methods"] = str(model.params.get("pca_method", "GramSVD"))
+    kv["pca_impl"] = str(model.params.get("pca_impl", "MTJ_EVD_SYMMMATRIX"))
+    V = model.V.double().cpu()
+    kv["k"] = V.shape[1]
+    kv["permutation"] = _arr(list(ex.cats) + list(ex.nums))
+    kv["ncats"] = len(ex.cats)
+    kv["nnums"] = len(ex.nums)
+    if ex.nums:
+        mu = ex.num_mean.cpu().double()
+        sd = ex.num_sd.cpu().double()
+        if getattr(ex, "descale_only", False):
+            sub, mul = torch.zeros_like(mu), 1.0 / sd
+        elif ex.standardize:
+            sub, mul = mu, 1.0 / sd
+        elif ex.center_only:
+            sub, mul = mu, torch.ones_like(mu)
+        else:
+            sub, mul = torch.zeros_like(mu), torch.ones_like(mu)
+        kv["normSub"] = _darr(sub.tolist())
+        kv["normMul"] = _darr(mul.tolist())
+    kv["catOffsets"] = _arr(offs)
+    kv["eigenvector_size"] = V.shape[0]
+    blobs["eigenvectors_raw"] = V.numpy().astype(">f8").tobytes()
+    _ = (info, start)
+
+
+def load_pca(ki, raw):
+    k, n = int(ki["k"]), int(ki["eigenvector_size"])
+    V = np.frombuffer(raw, dtype=">f8", count=n * k).reshape(n, k).astype(np.float64)
+    return dict(k=k, V=torch.from_numpy(V.copy()), perm=[int(v) for v in _floats(ki["permutation"])],
+                ncats=int(ki["ncats"]), nnums=int(ki["nnums"]), offs=[int(v) for v in _floats(ki["catOffsets"])],
+                sub=_floats(ki.get("normSub")), mul=_floats(ki.get("normMul")),
+                use_all=ki.get("use_all_factor_levels") == "true")
+
+
+def score_pca(st, X):
+    N = X.shape[1]
+    V = st["V"].to(X.device)
+    out = torch.zeros(N, st["k"], dtype=torch.float64, device=X.device)
+    offs = st["offs"]
+    for j in range(st["ncats"]):
+        c = X[st["perm"][j]]
+        ok = ~torch.isnan(c)
+        lvl = torch.where(ok, c, torch.zeros_like(c)).long() - (0 if st["use_all"] else 1)
+        last = offs[j + 1] - offs[j] - 1
+        ok = ok & (lvl >= 0) & (lvl <= last)
+        rows = torch.nonzero(ok, as_tuple=True)[0]
+        out[rows] += V[offs[j] + lvl[rows]]
+    base = offs[st["ncats"]]
+    for j in range(st["nnums"]):
+        v = (X[st["perm"][st["ncats"] + j]].double() - st["sub"][j]) * st["mul"][j]
+        out += v[:, None] * V[base + j][None, :]
+    return out.float()
+
+
+# ================================================================================================ W2V
+def write_word2vec(model, kv, blobs):
+    V = model.vectors.detach().float().cpu().numpy()
+    kv["vocab_size"] = V.shape[0]
+    kv["vec_size"] = V.shape[1]
+    blobs["vectors"] = V.astype(">f4").tobytes()
+    blobs["vocabulary"] = "".join(str(w).replace("\\", "\\\\").replace("\n", "\\n") + "\n" for w in model.words).encode()
+
+
+def load_word2vec(ki, raw_vectors, vocab_text):
+    from .reader import _unescape
+    n, d = int(ki["vocab_size"]), int(ki["vec_size"])
+    V = np.frombuffer(raw_vectors, dtype=">f4", count=n * d).reshape(n, d).astype(np.float32)
+    words = [_unescape(w) for w in vocab_text.split("\n")[:n]]
+    return words, torch.from_numpy(V.copy())
+
+
+# ================================================================================================ isotonic
+def _blob_doubles(v) -> bytes:
+    v = np.asarray(v, dtype=np.float64)
+    return struct.pack(">i", v.size) + v.astype(">f8").tobytes()
+
+
+def _read_blob_doubles(b: bytes):
+    (n,) = struct.unpack(">i", b[:4])
+    return np.frombuffer(b[4:4 + 8 * n], dtype=">f8").astype(np.float64)
+
+
+def write_isotonic(model, kv, blobs):
+    tx, ty = list(model.thresholds_x), list(model.thresholds_y)
+    kv["calib_min_x"] = repr(float(tx[0]))
+    kv["calib_max_x"] = repr(float(tx[-1]))
+    blobs["calib/thresholds_x"] = _blob_doubles(tx)
+    blobs["calib/thresholds_y"] = _blob_doubles(ty)
+
+
+def load_isotonic(files):
+    return _read_blob_doubles(files["calib/thresholds_x"]), _read_blob_doubles(files["calib/thresholds_y"])

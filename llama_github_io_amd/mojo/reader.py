@@ -28,9 +28,11 @@ def _unescape(s: str) -> str:
     return "".join(out)
 
 
-def parse_mojo(path: str) -> dict:
+def parse_mojo(path: str, prefix: str = "") -> dict:
+    """model.ini sections, domains and every other entry of the MOJO rooted at ``prefix`` (nested
+    sub-models of a multi-model MOJO live under ``models/<key>/``)."""
     with zipfile.ZipFile(path) as z:
-        ini = z.read("model.ini").decode()
+        ini = z.read(prefix + "model.ini").decode()
         section = None
         info, columns, domains = {}, [], {}
         for line in ini.splitlines():
@@ -48,11 +50,17 @@ def parse_mojo(path: str) -> dict:
             elif section == "domains":
                 ci, rest = s.split(":", 1)
                 n, fname = rest.split()
-                lines = z.read(f"domains/{fname}").decode().split("\n")[: int(n)]
+                lines = z.read(f"{prefix}domains/{fname}").decode().split("\n")[: int(n)]
                 domains[int(ci)] = [_unescape(x) for x in lines]
-        trees = {n: z.read(n) for n in z.namelist() if n.startswith("trees/") and n.endswith(".bin") and "_aux" not in n}
-        state = json.loads(z.read("model_state.json")) if "model_state.json" in z.namelist() else None
-    return dict(info=info, columns=columns, domains=domains, trees=trees, state=state)
+        names = [n for n in z.namelist() if n.startswith(prefix)]
+        if not prefix:
+            names = [n for n in names if not n.startswith("models/")]
+        files = {n[len(prefix):]: z.read(n) for n in names
+                 if n != prefix + "model.ini" and not n.startswith(prefix + "domains/")}
+    trees = {n: b for n, b in files.items() if n.startswith("trees/") and n.endswith(".bin") and "_aux" not in n}
+    state = json.loads(files["model_state.json"]) if "model_state.json" in files else None
+    return dict(info=info, columns=columns, domains=domains, trees=trees, state=state, files=files, path=path,
+                prefix=prefix)
 
 
 def _floats(s: str):

@@ -2,9 +2,10 @@
 [domains], ``domains/dNNN.txt``), ``GbmMojoWriter``/``DrfMojoWriter``/``IsolationForestMojoWriter``
 (``trees/tCC_III.bin`` CompressedTree blobs), ``GLMMojoWriter``, ``KMeansMojoWriter``).
 
-Models without a reference MOJO layout here (DeepLearning, PCA, ...) are exported with the same
-zip/ini container plus a ``model_state.json`` + safetensors payload readable by this framework's
-reader (``mojo_version`` suffix ``-amd``).
+DeepLearning, PCA, Word2Vec, IsotonicRegression and StackedEnsemble (nested sub-MOJOs) use the
+reference layouts of ``mojo/algos.py``. Models without a reference MOJO layout here are exported with
+the same zip/ini container plus a ``model_state.json`` payload readable by this framework's reader
+(``mojo_version`` suffix ``-amd``).
 """
 from __future__ import annotations
 
@@ -19,9 +20,13 @@ import numpy as np
 
 from .treebytes import tree_to_bytes
 
-MOJO_VERSIONS = {"gbm": "1.40", "drf": "1.40", "isolationforest": "1.40", "glm": "1.00", "kmeans": "1.00"}
+MOJO_VERSIONS = {"gbm": "1.40", "drf": "1.40", "isolationforest": "1.40", "glm": "1.00", "kmeans": "1.00",
+                 "deeplearning": "1.10", "pca": "1.00", "word2vec": "1.00", "isotonicregression": "1.00",
+                 "stackedensemble": "1.01"}
 ALGO_FULL = {"gbm": "Gradient Boosting Machine", "drf": "Distributed Random Forest", "glm": "Generalized Linear Modeling",
-             "kmeans": "K-means", "isolationforest": "Isolation Forest"}
+             "kmeans": "K-means", "isolationforest": "Isolation Forest", "deeplearning": "Deep Learning",
+             "pca": "Principal Components Analysis", "word2vec": "Word2Vec", "isotonicregression": "Isotonic Regression",
+             "stackedensemble": "StackedEnsemble"}
 
 
 def _escape(s: str) -> str:
@@ -37,11 +42,15 @@ def _category(m):
     return {"AnomalyDetection": "AnomalyDetection", "Clustering": "Clustering"}.get(c, c)
 
 
-def write_mojo(model, path: str) -> str:
+def _mojo_files(model, prefix: str = "") -> dict:
+    """All entries of one model's MOJO (``model.ini``, domains, blobs), names under ``prefix``."""
+    from . import algos as A
     info = model.info
     algo = model.algo
     cols = list(info.x) + ([info.response] if info.response else [])
     doms = list(info.domains) + ([info.response_domain] if info.response else [])
+    if algo == "deeplearning":
+        cols, doms = A.dl_columns(model)
     kv = {}
     kv["h2o_version"] = "3.46.0.amd0"
     kv["mojo_version"] = MOJO_VERSIONS.get(algo, "1.00-amd")
@@ -71,6 +80,16 @@ def write_mojo(model, path: str) -> str:
         _glm(model, kv)
     elif algo == "kmeans":
         _kmeans(model, kv)
+    elif algo == "deeplearning":
+        A.write_deeplearning(model, kv, blobs)
+    elif algo == "pca":
+        A.write_pca(model, kv, blobs)
+    elif algo == "word2vec":
+        A.write_word2vec(model, kv, blobs)
+    elif algo == "isotonicregression":
+        A.write_isotonic(model, kv, blobs)
+    elif algo == "stackedensemble":
+        _stacked(model, kv, blobs)
     else:
         _generic_state(model, kv, blobs)
     buf = io.StringIO()
@@ -82,21 +101,43 @@ def write_mojo(model, path: str) -> str:
         buf.write(c + "\n")
     buf.write("\n[domains]\n")
     di = 0
-    dom_files = {}
+    files = {}
     for ci, d in enumerate(doms):
         if d is None:
             continue
         buf.write(f"{ci}: {len(d)} d{di:03d}.txt\n")
-        dom_files[f"domains/d{di:03d}.txt"] = "".join(_escape(str(s)) + "\n" for s in d)
+        files[prefix + f"domains/d{di:03d}.txt"] = "".join(_escape(str(s)) + "\n" for s in d)
         di += 1
+    files[prefix + "model.ini"] = buf.getvalue()
+    for n, b in blobs.items():
+        files[n if n.startswith("models/") else prefix + n] = b
+    return files
+
+
+def write_mojo(model, path: str) -> str:
+    files = _mojo_files(model)
     os.makedirs(os.path.dirname(os.path.abspath(path)) or ".", exist_ok=True)
     with zipfile.ZipFile(path, "w", zipfile.ZIP_DEFLATED) as z:
-        z.writestr("model.ini", buf.getvalue())
-        for n, s in dom_files.items():
-            z.writestr(n, s)
-        for n, b in blobs.items():
+        z.writestr("model.ini", files.pop("model.ini"))
+        for n, b in files.items():
             z.writestr(n, b)
     return path
+
+
+def _stacked(model, kv, blobs):
+    """MultiModelMojoWriter layout: every base model and the metalearner as a nested MOJO."""
+    subs = [(m.key, m) for m in model.base_models()] + [(model.meta.key, model.meta)]
+    kv["submodel_count"] = len(subs)
+    for i, (key, m) in enumerate(subs):
+        d = f"models/{key}/"
+        kv[f"submodel_key_{i}"] = key
+        kv[f"submodel_dir_{i}"] = d
+        blobs.update(_mojo_files(m, d))
+    kv["base_models_num"] = len(subs) - 1
+    kv["metalearner"] = model.meta.key
+    kv["metalearner_transform"] = str(model.params.get("metalearner_transform", "NONE"))
+    for i, (key, _) in enumerate(subs[:-1]):
+        kv[f"base_model{i}"] = key
 
 
 def _trees(model, kv, blobs):

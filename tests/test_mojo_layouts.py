@@ -1,0 +1,117 @@
+"""Reference-layout MOJOs (DeepLearning, PCA, Word2Vec, Isotonic, StackedEnsemble): the exported zip
+holds the reference keys/blobs and ``h2o.import_mojo`` scores exactly like the original model."""
+import zipfile
+
+import numpy as np
+import pandas as pd
+import pytest
+
+import h2o
+from h2o.estimators import (H2ODeepLearningEstimator, H2OGeneralizedLinearEstimator, H2OGradientBoostingEstimator,
+                            H2OIsotonicRegressionEstimator, H2OPrincipalComponentAnalysisEstimator,
+                            H2OStackedEnsembleEstimator, H2OWord2vecEstimator)
+from llama_github_io_amd.mojo.reader import parse_mojo
+
+
+@pytest.fixture(scope="module")
+def df():
+    h2o.init(verbose=False)
+    rng = np.random.default_rng(3)
+    n = 800
+    a = rng.normal(size=n)
+    a[rng.random(n) < 0.05] = np.nan
+    c = rng.choice(list("pqrs"), n).astype(object)
+    c[rng.random(n) < 0.05] = None
+    d = pd.DataFrame({"a": a, "c": c, "b": rng.normal(size=n), "k": rng.choice(list("uv"), n)})
+    d["y"] = np.where(np.nan_to_num(d.a) - d.b + (d.c == "p") + rng.normal(size=n) * 0.3 > 0, "1", "0")
+    d["m"] = rng.choice(["m0", "m1", "m2"], n)
+    d["r"] = np.sin(np.nan_to_num(d.a)) * 2 + d.b + rng.normal(size=n) * 0.1
+    return h2o.H2OFrame(d, column_types={"y": "enum", "c": "enum", "k": "enum", "m": "enum"})
+
+
+def _roundtrip(est, df, tmp_path):
+    path = est.download_mojo(str(tmp_path))
+    g = h2o.import_mojo(path)
+    return path, est.predict(df).as_data_frame(), g.predict(df).as_data_frame()
+
+
+@pytest.mark.parametrize("kw,y", [
+    (dict(hidden=[8, 6], activation="Rectifier"), "y"),
+    (dict(hidden=[7], activation="Tanh", use_all_factor_levels=False), "m"),
+    (dict(hidden=[5, 4], activation="Maxout"), "y"),
+    (dict(hidden=[6], activation="ExpRectifier"), "r"),
+    (dict(hidden=[6], activation="RectifierWithDropout", hidden_dropout_ratios=[0.2]), "r"),
+])
+def test_deeplearning_mojo_reference_layout(df, tmp_path, kw, y):
+    m = H2ODeepLearningEstimator(epochs=2, seed=1, reproducible=True, **kw)
+    m.train(x=["a", "c", "b", "k"], y=y, training_frame=df)
+    path, a, b = _roundtrip(m, df, tmp_path)
+    mj = parse_mojo(path)
+    ki = mj["info"]
+    # reference keys (DeepLearningMojoWriter.writeModelData), categoricals first in [columns]
+    for key in ("nums", "cats", "cat_offsets", "norm_mul", "norm_sub", "activation", "neural_network_sizes",
+                "weight_layer0", "bias_layer0", "hidden_dropout_ratios", "distribution", "mean_imputation"):
+        assert key in ki, key
+    assert mj["columns"][:2] == ["c", "k"] and int(ki["cats"]) == 2
+    cols = [c for c in a.columns]
+    for c in cols:
+        if c == "predict" and y != "r":
+            assert (a[c].astype(str) == b[c].astype(str)).mean() > 0.99
+        else:
+            np.testing.assert_allclose(a[c].astype(float).values, b[c].astype(float).values, rtol=2e-4, atol=2e-5)
+
+
+@pytest.mark.parametrize("transform", ["NONE", "DEMEAN", "STANDARDIZE"])
+def test_pca_mojo_reference_layout(df, tmp_path, transform):
+    p = H2OPrincipalComponentAnalysisEstimator(k=3, transform=transform, use_all_factor_levels=True)
+    p.train(x=["b", "c", "k"], training_frame=df)
+    path = p.download_mojo(str(tmp_path))
+    with zipfile.ZipFile(path) as z:
+        assert "eigenvectors_raw" in z.namelist()
+    g = h2o.import_mojo(path)
+    ok = ~df.as_data_frame()["c"].isna().values       # NA categoricals: reference skips, training imputes
+    a = p.predict(df).as_data_frame().values[ok]
+    b = g.predict(df).as_data_frame().values[ok]
+    np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-5)
+
+
+def test_word2vec_mojo(tmp_path):
+    h2o.init(verbose=False)
+    rng = np.random.default_rng(0)
+    words = []
+    for i in range(400):
+        words += list(rng.choice(["cat", "dog", "cow"] if i % 2 else ["one", "two", "six"], 5)) + [None]
+    fr = h2o.H2OFrame(pd.DataFrame({"w": words}), column_types={"w": "string"})
+    w2v = H2OWord2vecEstimator(vec_size=6, min_word_freq=1, epochs=2, seed=1, sent_sample_rate=0)
+    w2v.train(training_frame=fr)
+    path = w2v.download_mojo(str(tmp_path))
+    mj = parse_mojo(path)
+    assert int(mj["info"]["vec_size"]) == 6 and len(mj["files"]["vectors"]) == int(mj["info"]["vocab_size"]) * 6 * 4
+    g = h2o.import_mojo(path)
+    assert g.find_synonyms("cat", 2) == pytest.approx(w2v._model.find_synonyms("cat", 2), rel=1e-5)
+
+
+def test_isotonic_mojo(df, tmp_path):
+    m = H2OIsotonicRegressionEstimator(out_of_bounds="clip")
+    m.train(x=["b"], y="r", training_frame=df)
+    path, a, b = _roundtrip(m, df, tmp_path)
+    assert "calib/thresholds_x" in parse_mojo(path)["files"]
+    np.testing.assert_allclose(a.values.astype(float), b.values.astype(float), rtol=1e-6, atol=1e-9)
+
+
+def test_stacked_ensemble_nested_mojo(df, tmp_path):
+    x = ["a", "c", "b", "k"]
+    kw = dict(nfolds=3, fold_assignment="Modulo", keep_cross_validation_predictions=True, seed=1)
+    g1 = H2OGradientBoostingEstimator(ntrees=5, **kw)
+    g1.train(x=x, y="y", training_frame=df)
+    g2 = H2OGeneralizedLinearEstimator(family="binomial", **kw)
+    g2.train(x=x, y="y", training_frame=df)
+    se = H2OStackedEnsembleEstimator(base_models=[g1, g2])
+    se.train(x=x, y="y", training_frame=df)
+    path, a, b = _roundtrip(se, df, tmp_path)
+    ki = parse_mojo(path)["info"]
+    assert int(ki["submodel_count"]) == 3 and int(ki["base_models_num"]) == 2
+    with zipfile.ZipFile(path) as z:
+        assert any(n.startswith("models/") and n.endswith("model.ini") for n in z.namelist())
+    np.testing.assert_allclose(a["1"].values, b["1"].values, rtol=1e-5, atol=1e-6)
+    assert (a["predict"] == b["predict"]).all()
