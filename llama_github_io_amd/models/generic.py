@@ -91,6 +91,9 @@ class GenericModel(Model):
             inner = IsotonicModel(m.key + "_iso", dict(out_of_bounds="clip"), info)
             inner.thresholds_x, inner.thresholds_y = tx.tolist(), ty.tolist()
             m.inner = inner
+        elif algo == "extendedisolationforest":
+            m.eif = A.load_eif(ki, mj["files"])
+            m.output["model_category"] = "AnomalyDetection"
         elif algo == "stackedensemble":
             subs = {}
             for i in range(int(ki.get("submodel_count", 0))):
@@ -132,6 +135,10 @@ class GenericModel(Model):
             return self.inner.prediction_names()
         if self.output.get("original_algo") == "isolationforest":
             return ["predict", "mean_length"]
+        if self.output.get("original_algo") == "extendedisolationforest":
+            return ["anomaly_score", "mean_length"]
+        if self.output.get("original_algo") == "pca":
+            return [f"PC{i + 1}" for i in range(self.pca["k"])]
         return None
 
     def _design(self, X):
@@ -213,6 +220,9 @@ class GenericModel(Model):
         if algo == "pca":
             from ..mojo import algos as A
             return A.score_pca(self.pca, X)
+        if algo == "extendedisolationforest":
+            from ..mojo import algos as A
+            return A.score_eif(self.eif, X)
         if algo == "stackedensemble":
             cols = []
             for b in self.base:

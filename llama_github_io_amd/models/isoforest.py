@@ -218,14 +218,16 @@ class ExtendedIsolationForestTrainer:
 
 def _grow_eif(xs, limit, ext, rng):
     F = xs.shape[1]
-    normal, offset, left, right, value = [], [], [], [], []
+    normal, offset, left, right, value, nrows = [], [], [], [], [], []
 
     def node(rows, depth):
         i = len(normal)
         normal.append(np.zeros(F)); offset.append(0.0); left.append(-1); right.append(-1); value.append(0.0)
+        nrows.append(0)
         n = rows.shape[0]
         if depth >= limit or n <= 1:
             value[i] = depth + float(c_factor(n))
+            nrows[i] = n
             return i
         nv = rng.normal(size=F)
         zero = rng.choice(F, F - ext - 1, replace=False) if F - ext - 1 > 0 else []
@@ -241,4 +243,5 @@ def _grow_eif(xs, limit, ext, rng):
 
     node(xs, 0)
     return dict(normal=np.asarray(normal), offset=np.asarray(offset), left=np.asarray(left, dtype=np.int64),
-                right=np.asarray(right, dtype=np.int64), value=np.asarray(value), depth=limit)
+                right=np.asarray(right, dtype=np.int64), value=np.asarray(value), nrows=np.asarray(nrows, dtype=np.int64),
+                depth=limit)

@@ -16,6 +16,8 @@ reference genmodel scorer on device tensors (``GenericModel`` dispatches to them
   count + big-endian doubles).
 * Stacked ensemble — ``MultiModelMojoReader`` / ``StackedEnsembleMojoReader.java`` (nested MOJOs under
   ``models/<key>/``, ``base_model<i>`` / ``metalearner`` keys).
+* Extended isolation forest — ``algos/isoforextended/ExtendedIsolationForestMojoModel.java:scoreTree0``
+  (heap-numbered 'N'/'L' node records per ``trees/tNN.bin``).
 
 Our own trainers differ from H2O in two imputation details that the writers fold into the exported
 parameters so the reference scorer reproduces this framework's predictions: DeepLearning imputes a
@@ -314,3 +316,100 @@ def write_isotonic(model, kv, blobs):
 
 def load_isotonic(files):
     return _read_blob_doubles(files["calib/thresholds_x"]), _read_blob_doubles(files["calib/thresholds_y"])
+
+
+# ================================================================================================ EIF
+def write_eif(model, kv, blobs):
+    """``trees/tNN.bin`` (ExtendedIsolationForestMojoModel.scoreTree0, native byte order): int F, then
+    per node int number (heap numbering: children 2i+1 / 2i+2), byte 'N' + F doubles normal + F doubles
+    point, or byte 'L' + int row count. The point is the hyperplane's closest point to the origin."""
+    from ..models.isoforest import c_factor
+    kv["ntrees"] = len(model.trees)
+    kv["sample_size"] = int(model.output["sample_size"])
+    for t, tr in enumerate(model.trees):
+        nrm, off = np.asarray(tr["normal"], dtype=np.float64), np.asarray(tr["offset"], dtype=np.float64)
+        left, right = np.asarray(tr["left"]), np.asarray(tr["right"])
+        F = nrm.shape[1]
+        nrows = tr.get("nrows")
+        out = [struct.pack("<i", F)]
+        stack = [(0, 0, 0)]                        # (node, heap number, depth)
+        recs = []
+        while stack:
+            i, h, dep = stack.pop()
+            if left[i] < 0:
+                if nrows is not None:
+                    n = int(nrows[i])
+                else:                              # older models: invert value = depth + c(n)
+                    want = float(tr["value"][i]) - dep
+                    n = min(range(0, int(model.output["sample_size"]) + 1), key=lambda k: abs(float(c_factor(k)) - want))
+                recs.append((h, struct.pack("<ib", h, ord("L")) + struct.pack("<i", n)))
+                continue
+            nn = float(nrm[i] @ nrm[i])
+            pt = nrm[i] * (off[i] / nn) if nn > 0 else np.zeros(F)
+            recs.append((h, struct.pack("<ib", h, ord("N")) + nrm[i].astype("<f8").tobytes() + pt.astype("<f8").tobytes()))
+            stack.append((int(right[i]), 2 * h + 2, dep + 1))
+            stack.append((int(left[i]), 2 * h + 1, dep + 1))
+        recs.sort(key=lambda r: r[0])
+        blobs[f"trees/t{t:02d}.bin"] = b"".join(out + [r[1] for r in recs])
+
+
+def load_eif(ki, files):
+    """Decode every tree into flat arrays (normal, point, left, right, leaf rows) for batched scoring."""
+    trees = []
+    for t in range(int(ki["ntrees"])):
+        b = files[f"trees/t{t:02d}.bin"]
+        (F,) = struct.unpack_from("<i", b, 0)
+        pos = 4
+        nodes = {}
+        while pos < len(b):
+            h, typ = struct.unpack_from("<ib", b, pos)
+            pos += 5
+            if typ == ord("N"):
+                n = np.frombuffer(b, "<f8", F, pos); p = np.frombuffer(b, "<f8", F, pos + 8 * F)
+                nodes[h] = ("N", n, p)
+                pos += 16 * F
+            else:
+                (rows,) = struct.unpack_from("<i", b, pos)
+                nodes[h] = ("L", rows)
+                pos += 4
+        order = sorted(nodes)
+        idx = {h: k for k, h in enumerate(order)}
+        M = len(order)
+        nrm, pt = np.zeros((M, F)), np.zeros((M, F))
+        left, right, rows = -np.ones(M, np.int64), -np.ones(M, np.int64), np.zeros(M, np.int64)
+        for h in order:
+            k = idx[h]
+            if nodes[h][0] == "N":
+                nrm[k], pt[k] = nodes[h][1], nodes[h][2]
+                left[k], right[k] = idx[2 * h + 1], idx[2 * h + 2]
+            else:
+                rows[k] = nodes[h][1]
+        trees.append(dict(normal=torch.from_numpy(nrm), point=torch.from_numpy(pt), left=torch.from_numpy(left),
+                          right=torch.from_numpy(right), rows=torch.from_numpy(rows)))
+    return dict(trees=trees, sample_size=int(ki["sample_size"]))
+
+
+def score_eif(st, X):
+    from ..models.isoforest import c_factor
+    Xr = X.T.double()
+    N = Xr.shape[0]
+    dev = Xr.device
+    tot = torch.zeros(N, dtype=torch.float64, device=dev)
+    for tr in st["trees"]:
+        nrm, pt = tr["normal"].to(dev), tr["point"].to(dev)
+        left, right, rows = tr["left"].to(dev), tr["right"].to(dev), tr["rows"].to(dev)
+        proj = Xr @ nrm.T - (nrm * pt).sum(1)            # (row - p) . n per node
+        node = torch.zeros(N, dtype=torch.long, device=dev)
+        height = torch.zeros(N, dtype=torch.float64, device=dev)
+        for _ in range(64):
+            isleaf = left[node] < 0
+            if bool(isleaf.all()):
+                break
+            go_left = proj.gather(1, node[:, None]).squeeze(1) <= 0     # NaN -> right, as in scoreTree0
+            node = torch.where(isleaf, node, torch.where(go_left, left[node], right[node]))
+            height = height + (~isleaf).double()
+        cf = torch.tensor([float(c_factor(int(r))) for r in tr["rows"].tolist()], dtype=torch.float64, device=dev)
+        tot += height + cf[node]
+    h = tot / max(1, len(st["trees"]))
+    c = float(c_factor(st["sample_size"]))
+    return torch.stack([torch.pow(2.0, -h / c).float(), h.float()], 1)

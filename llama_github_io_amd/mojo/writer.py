@@ -22,11 +22,11 @@ from .treebytes import tree_to_bytes
 
 MOJO_VERSIONS = {"gbm": "1.40", "drf": "1.40", "isolationforest": "1.40", "glm": "1.00", "kmeans": "1.00",
                  "deeplearning": "1.10", "pca": "1.00", "word2vec": "1.00", "isotonicregression": "1.00",
-                 "stackedensemble": "1.01"}
+                 "stackedensemble": "1.01", "extendedisolationforest": "1.00"}
 ALGO_FULL = {"gbm": "Gradient Boosting Machine", "drf": "Distributed Random Forest", "glm": "Generalized Linear Modeling",
              "kmeans": "K-means", "isolationforest": "Isolation Forest", "deeplearning": "Deep Learning",
              "pca": "Principal Components Analysis", "word2vec": "Word2Vec", "isotonicregression": "Isotonic Regression",
-             "stackedensemble": "StackedEnsemble"}
+             "stackedensemble": "StackedEnsemble", "extendedisolationforest": "Extended Isolation Forest"}
 
 
 def _escape(s: str) -> str:
@@ -90,6 +90,8 @@ def _mojo_files(model, prefix: str = "") -> dict:
         A.write_isotonic(model, kv, blobs)
     elif algo == "stackedensemble":
         _stacked(model, kv, blobs)
+    elif algo == "extendedisolationforest":
+        A.write_eif(model, kv, blobs)
     else:
         _generic_state(model, kv, blobs)
     buf = io.StringIO()

@@ -115,3 +115,12 @@ def test_stacked_ensemble_nested_mojo(df, tmp_path):
         assert any(n.startswith("models/") and n.endswith("model.ini") for n in z.namelist())
     np.testing.assert_allclose(a["1"].values, b["1"].values, rtol=1e-5, atol=1e-6)
     assert (a["predict"] == b["predict"]).all()
+
+
+def test_extended_isolation_forest_mojo(df, tmp_path):
+    from h2o.estimators import H2OExtendedIsolationForestEstimator
+    m = H2OExtendedIsolationForestEstimator(ntrees=7, sample_size=64, extension_level=1, seed=3)
+    m.train(x=["b", "r"], training_frame=df)
+    path, a, b = _roundtrip(m, df, tmp_path)
+    assert "trees/t06.bin" in parse_mojo(path)["files"]
+    np.testing.assert_allclose(a.values.astype(float), b.values.astype(float), rtol=1e-6, atol=1e-9)
