@@ -267,7 +267,9 @@ def make_metrics(predicted, actual, domain=None, distribution=None, weights=None
 
 
 def download_pojo(model, path="", get_jar=True, jar_name=""):
-    raise NotImplementedError("POJO (Java source) export is not provided by the MI355X-native engine; use download_mojo")
+    """Java source of a scoring class extending hex.genmodel.GenModel (GBM/DRF/IF/GLM/KMeans)."""
+    from llama_github_io_amd.mojo.pojo import download_pojo as _dp
+    return _dp(getattr(model, "_model", model), path, get_jar, jar_name)
 
 
 def flow():

@@ -103,6 +103,10 @@ class H2OEstimator:
 
     save_mojo = download_mojo
 
+    def download_pojo(self, path="", get_genmodel_jar=False, genmodel_name=""):
+        from llama_github_io_amd.mojo import pojo
+        return pojo.download_pojo(self._m(), path, get_genmodel_jar, genmodel_name)
+
     def download_model(self, path=""):
         from llama_github_io_amd import persist
         return persist.save_model(self._m(), path)

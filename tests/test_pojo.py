@@ -1,0 +1,211 @@
+"""POJO export: the generated Java is evaluated by a small translator of the emitted expression subset
+(nested ternaries, NaN tests, float thresholds, GRPSPLIT bitsets, spilled sub-classes) and must
+reproduce the model's own predictions. No JDK exists in this image, so javac is not exercised."""
+import re
+import shutil
+import subprocess
+
+import numpy as np
+import pandas as pd
+import pytest
+
+import h2o
+from h2o.estimators import (H2OGeneralizedLinearEstimator, H2OGradientBoostingEstimator, H2OKMeansEstimator,
+                            H2ORandomForestEstimator)
+from llama_github_io_amd.mojo import pojo as P
+
+_TOK = re.compile(r"\s*(Double\.isNaN|GenModel\.bitSetContains|Double\.NaN|Float\.POSITIVE_INFINITY|"
+                  r"Float\.NEGATIVE_INFINITY|[A-Za-z_][A-Za-z0-9_]*\.score0|[A-Za-z_][A-Za-z0-9_]*|"
+                  r"-?\d+\.\d*(?:[eE][-+]?\d+)?f?|-?\d+(?:[eE][-+]?\d+)?f?|\|\||&&|>=|<=|[?:()\[\],<>!])")
+
+
+class _Parser:
+    """Java expression subset -> vectorised numpy expression over D[f] (one array per column)."""
+
+    def __init__(self, s):
+        self.t = [m for m in _TOK.findall(s) if m]
+        self.i = 0
+
+    def peek(self):
+        return self.t[self.i] if self.i < len(self.t) else None
+
+    def eat(self, x=None):
+        tok = self.t[self.i]
+        assert x is None or tok == x, (tok, x, self.t[max(0, self.i - 5):self.i + 5])
+        self.i += 1
+        return tok
+
+    def expr(self):
+        c = self.orx()
+        if self.peek() == "?":
+            self.eat("?")
+            a = self.expr()
+            self.eat(":")
+            b = self.expr()
+            return f"np.where({c}, {a}, {b})"
+        return c
+
+    def orx(self):
+        a = self.andx()
+        while self.peek() == "||":
+            self.eat()
+            a = f"({a}) | ({self.andx()})"
+        return a
+
+    def andx(self):
+        a = self.unary()
+        while self.peek() == "&&":
+            self.eat()
+            a = f"({a}) & ({self.unary()})"
+        return a
+
+    def unary(self):
+        if self.peek() == "!":
+            self.eat()
+            return f"~({self.unary()})"
+        a = self.prim()
+        if self.peek() in ("<", ">=", "<=", ">"):
+            op = self.eat()
+            a = f"({a} {op} {self.prim()})"
+        return a
+
+    def prim(self):
+        tok = self.eat()
+        if tok == "(" and self.peek() == "float" and self.t[self.i + 1] == ")":
+            self.eat("float"); self.eat(")")
+            return f"np.float64(np.float32({self.prim()}))"
+        if tok == "(":
+            e = self.expr()
+            self.eat(")")
+            return f"({e})"
+        if tok == "data":
+            self.eat("[")
+            k = self.eat()
+            self.eat("]")
+            return f"D[{k}]"
+        if tok == "Double.isNaN":
+            self.eat("(")
+            e = self.expr()
+            self.eat(")")
+            return f"np.isnan({e})"
+        if tok == "GenModel.bitSetContains":
+            self.eat("(")
+            g = self.eat(); self.eat(","); nb = self.eat(); self.eat(","); off = self.eat(); self.eat(",")
+            e = self.expr()
+            self.eat(")")
+            return f"bsc({g}, {nb}, {off}, {e})"
+        if tok.endswith(".score0"):
+            self.eat("("); self.eat("data"); self.eat(")")
+            return f"SUB['{tok[:-7]}'](D)"
+        if tok in ("true", "false"):
+            return "True" if tok == "true" else "False"
+        if tok == "Double.NaN":
+            return "np.nan"
+        if tok.startswith("Float."):
+            return "np.inf" if "POSITIVE" in tok else "-np.inf"
+        if tok.endswith("f"):
+            return f"np.float64(np.float32({tok[:-1]}))"
+        return f"np.float64({tok})"
+
+
+def _bsc(bits, nb, off, x):
+    idx = np.nan_to_num(x, nan=0).astype(np.int64) - off
+    ok = (idx >= 0) & (idx < nb)
+    i = np.clip(idx, 0, nb - 1)
+    return ok & ((bits[i >> 3].astype(np.int64) & (1 << (i & 7))) != 0)
+
+
+def _tree_functions(src):
+    """Every generated tree class -> python callable D -> per-row score."""
+    classes = re.findall(r"class (\w+) \{\n  static final double score0\(double\[\] data\) \{\n    double pred = "
+                         r"(.*?);\n    return pred;\n  \}\n((?:  [^\n]*\n)*)\}", src, re.S)
+    sub = {}
+    for name, body, grp in classes:
+        env = dict(np=np, SUB=sub)
+        for g, arr in re.findall(r"public static final byte\[\] (GRPSPLIT\d+) = new byte\[\] \{(.*?)\};", grp):
+            env[g] = np.array([int(v) & 0xFF for v in arr.split(",")], dtype=np.uint8)
+        code = _Parser(body).expr()
+        env["bsc"] = _bsc
+        sub[name] = eval(f"lambda D: {code}", env)   # noqa: S307 (our own generated source)
+    return sub
+
+
+@pytest.fixture(scope="module")
+def df():
+    h2o.init(verbose=False)
+    rng = np.random.default_rng(5)
+    n = 600
+    a = rng.normal(size=n)
+    a[rng.random(n) < 0.08] = np.nan
+    d = pd.DataFrame({"a": a, "b": rng.normal(size=n), "c": rng.choice(list("pqrstu"), n)})
+    d["y"] = np.where(np.nan_to_num(d.a) - d.b + d.c.isin(["p", "s"]) + rng.normal(size=n) * 0.3 > 0, "1", "0")
+    d["r"] = np.nan_to_num(d.a) * 2 + d.b + rng.normal(size=n) * 0.1
+    return h2o.H2OFrame(d, column_types={"c": "enum", "y": "enum"})
+
+
+def _cols(df, m):
+    pdf = df.as_data_frame()
+    out = []
+    for n, dom in zip(m.info.x, m.info.domains):
+        v = pdf[n]
+        out.append(v.map({s: i for i, s in enumerate(dom)}).astype(float).values if dom else v.astype(float).values)
+    return out
+
+
+@pytest.mark.parametrize("algo,y", [("gbm", "y"), ("gbm", "r"), ("drf", "y"), ("drf", "r")])
+def test_tree_pojo_reproduces_model(df, tmp_path, algo, y):
+    est = (H2OGradientBoostingEstimator(ntrees=6, max_depth=5, seed=1) if algo == "gbm"
+           else H2ORandomForestEstimator(ntrees=4, max_depth=8, seed=1))
+    est.train(x=["a", "b", "c"], y=y, training_frame=df)
+    path = est.download_pojo(str(tmp_path))
+    src = open(path).read()
+    assert "extends GenModel" in src and "public final double[] score0(double[] data, double[] preds)" in src
+    m = est._model
+    fns = _tree_functions(src)
+    D = _cols(df, m)
+    import torch
+    from llama_github_io_amd.frame import H2OFrame  # noqa: F401
+    X = torch.tensor(np.stack(D), dtype=torch.float32)
+    raw = m.forest.predict_raw(X).double().numpy()
+    tot = np.zeros_like(raw)
+    for idx, c in enumerate(m.forest.tree_class):
+        it = idx // max(m.forest.K, 1)
+        tot[:, c] += fns[f"{P.java_ident(m.key)}_Tree_{it}_class_{c}"](D)
+    np.testing.assert_allclose(tot, raw, rtol=1e-5, atol=1e-5)
+
+
+def test_tree_pojo_spills_large_trees(df, tmp_path, monkeypatch):
+    monkeypatch.setattr(P, "MAX_NODES_PER_CLASS", 3)
+    est = H2OGradientBoostingEstimator(ntrees=2, max_depth=6, seed=2, min_rows=2)
+    est.train(x=["a", "b", "c"], y="r", training_frame=df)
+    src = P.pojo_source(est._model)
+    assert re.search(r"_Tree_0_class_0_\d+\.score0\(data\)", src)
+    fns = _tree_functions(src)
+    D = _cols(df, est._model)
+    import torch
+    raw = est._model.forest.predict_raw(torch.tensor(np.stack(D), dtype=torch.float32)).double().numpy()
+    k = P.java_ident(est._model.key)
+    np.testing.assert_allclose(fns[f"{k}_Tree_0_class_0"](D) + fns[f"{k}_Tree_1_class_0"](D), raw[:, 0], rtol=1e-5,
+                               atol=1e-5)
+
+
+def test_glm_and_kmeans_pojo_constants(df, tmp_path):
+    g = H2OGeneralizedLinearEstimator(family="binomial", lambda_=0)
+    g.train(x=["a", "b", "c"], y="y", training_frame=df)
+    src = P.pojo_source(g._model)
+    beta = [float(v) for v in re.search(r"BETA = new double\[\] \{(.*?)\};", src).group(1).split(",")]
+    coef = g.coef()
+    assert abs(beta[-1] - coef["Intercept"]) < 1e-9
+    k = H2OKMeansEstimator(k=3, seed=1)
+    k.train(x=["a", "b"], training_frame=df)
+    ks = P.pojo_source(k._model)
+    assert ks.count("{") == ks.count("}") and "CENTERS" in ks
+    assert h2o.download_pojo(g, str(tmp_path)).endswith(".java")
+
+
+@pytest.mark.skipif(shutil.which("javac") is None, reason="no JDK in this image")
+def test_pojo_compiles(df, tmp_path):   # pragma: no cover - exercised only where a JDK exists
+    est = H2OGradientBoostingEstimator(ntrees=2, seed=1)
+    est.train(x=["a", "b", "c"], y="y", training_frame=df)
+    path = est.download_pojo(str(tmp_path))
+    subprocess.run(["javac", "-d", str(tmp_path), path], check=True)
