@@ -376,19 +376,17 @@ def import_file(path=None, destination_frame=None, parse=True, header=0, sep=Non
             fr = parse_arff(buf)
         elif ptype == "PARQUET":
             fr = parse_parquet(f)
-        elif ptype in ("XLS", "XLSX"):
-            import pandas as pd
-            fr = H2OFrame(pd.read_excel(io.BytesIO(buf)))
-        elif ptype in ("ORC", "AVRO", "FEATHER"):
-            import pyarrow
+        elif ptype in ("XLS", "XLSX", "AVRO"):
+            from . import formats
+            grid = {"XLS": formats.read_xls, "XLSX": formats.read_xlsx, "AVRO": formats.read_avro}[ptype](buf)
+            fr = formats.to_frame(grid, 1 if ptype == "AVRO" else header, col_types)
+        elif ptype in ("ORC", "FEATHER"):
             if ptype == "FEATHER":
                 import pyarrow.feather as pf
                 fr = H2OFrame(pf.read_table(io.BytesIO(buf)).to_pandas())
-            elif ptype == "ORC":
+            else:
                 import pyarrow.orc as po
                 fr = H2OFrame(po.ORCFile(io.BytesIO(buf)).read().to_pandas())
-            else:
-                raise NotImplementedError("Avro parsing needs fastavro, which is not available")
         else:
             if custom_non_data_line_markers:
                 keep = [ln for ln in buf.split(b"\n") if not any(ln.startswith(m.encode()) for m in custom_non_data_line_markers)]
