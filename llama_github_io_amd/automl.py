@@ -201,3 +201,20 @@ def _metric_of_dict(perf, metric):
     if v is None and key == "mean_residual_deviance" and perf:
         v = perf.get("MSE")
     return float("nan") if v is None else float(v)
+
+
+def leaderboard_frame(models, frame=None, sort_metric="AUTO"):
+    """``makeLeaderboard`` (h2o-automl ``Leaderboard.java``): rank arbitrary models on a frame (or their
+    own training/cross-validation metrics) with the AutoML leaderboard columns."""
+    import numpy as np
+    import torch
+    from .frame import Column, H2OFrame, engine_device
+    lb = AutoML.__new__(AutoML)
+    lb.models = list(models)
+    lb.sort_metric = sort_metric
+    lb.leaderboard_frame = frame
+    rows, cols = lb.leaderboard_rows()
+    out = [Column("model_id", "string", strings=np.array([r["model_id"] for r in rows], dtype=object))]
+    for c in cols[1:]:
+        out.append(Column(c, "real", torch.tensor([r[c] for r in rows], dtype=torch.float64, device=engine_device())))
+    return H2OFrame._from_columns(out)
