@@ -23,6 +23,7 @@
 //     wave hit 8 different feature sub-histograms (few same-address LDS atomic collisions).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #define NBIN 256
 #define AMAX_SHARDS 64  // per-block |aux| maxima shards (k_amax / k_gbm_step -> k_qscale)
@@ -912,7 +913,24 @@ __global__ void k_subtract(double* __restrict__ hist_next, const double* __restr
 #define LU (LROWS / 64)   // rows per lane (4)
 #define LMAXW 16          // max words (64 features) kept in registers per row on the fast path
 
-template <bool TWO, bool MOVE>
+// NV > 0 (rows of NV x 16 B): each row is loaded ONCE into registers up front (with its aux and ridx),
+// split bytes are picked from those registers and the move stores them back — one HBM read per row
+// instead of two dependent byte loads plus the re-read of the row for the move.
+__device__ __forceinline__ unsigned pick_word(uint4 v, int wi) {
+  // wi is block-uniform: a compare/select chain on values (no runtime-indexed register array -> no scratch)
+  unsigned r = v.x;
+  r = wi == 1 ? v.y : r;
+  r = wi == 2 ? v.z : r;
+  r = wi == 3 ? v.w : r;
+  return r;
+}
+__device__ __forceinline__ int row_byte(uint4 v0, uint4 v1, int f) {
+  const int wi = f >> 2;
+  const unsigned w = wi < 4 ? pick_word(v0, wi) : pick_word(v1, wi - 4);
+  return (w >> (8 * (f & 3))) & 0xFF;
+}
+
+template <bool TWO, bool MOVE, int NV>
 __global__ __launch_bounds__(LW * 64) void k_route(
     const uint8_t* __restrict__ sbins, const float4* __restrict__ saux, const int* __restrict__ sridx,
     uint8_t* __restrict__ dbins, float4* __restrict__ daux, int* __restrict__ dridx, int stride,
@@ -959,16 +977,33 @@ __global__ __launch_bounds__(LW * 64) void k_route(
   int q[LU], rank[LU];
   bool mv[LU];
   int cnt[4] = {0, 0, 0, 0};
+  // NV > 0: all of the tile's loads issued before any decision (rows clamped into the node: no divergence).
+  // Plain per-u scalars (not a 2-D array) so everything stays in VGPRs.
+  uint4 rv0[LU], rv1[LU];
+  float4 ra[LU];
+  int rx[LU];
+  if (NV > 0) {
+#pragma unroll
+    for (int u = 0; u < LU; ++u) {
+      const int row = min(wbase + u * 64 + lane, r1 - 1);
+      const uint4* s4 = (const uint4*)(sbins + (size_t)row * stride);
+      rv0[u] = s4[0];
+      rv1[u] = NV > 1 ? s4[1] : make_uint4(0u, 0u, 0u, 0u);
+      ra[u] = saux[row];
+      rx[u] = sridx ? sridx[row] : row;
+    }
+  }
 #pragma unroll
   for (int u = 0; u < LU; ++u) {
     const int row = wbase + u * 64 + lane;
     const bool valid = row < r1;
     int dA = 0, dB = 0;
-    if (valid && featA >= 0) dA = dec_go_left(&sA, sbins[(size_t)row * stride + featA]) ? 0 : 1;
+    if (valid && featA >= 0)
+      dA = dec_go_left(&sA, NV > 0 ? row_byte(rv0[u], rv1[u], featA) : sbins[(size_t)row * stride + featA]) ? 0 : 1;
     if (TWO && valid && sC[dA] >= 0) {
       const Dec* b = &sB[dA];
       const int fb = b->feat;
-      if (fb >= 0) dB = dec_go_left(b, sbins[(size_t)row * stride + fb]) ? 0 : 1;
+      if (fb >= 0) dB = dec_go_left(b, NV > 0 ? row_byte(rv0[u], rv1[u], fb) : sbins[(size_t)row * stride + fb]) ? 0 : 1;
     }
     q[u] = 2 * dA + dB;
     mv[u] = MOVE && valid && sG[q[u]] >= 0;
@@ -1013,15 +1048,19 @@ __global__ __launch_bounds__(LW * 64) void k_route(
   for (int u = 0; u < LU; ++u) {
     const int row = wbase + u * 64 + lane;
     if (row >= r1) continue;
-    const float4 a = saux[row];
-    const int rr = sridx ? sridx[row] : row;
+    const float4 a = NV > 0 ? ra[u] : saux[row];
+    const int rr = NV > 0 ? rx[u] : (sridx ? sridx[row] : row);
     if (mv[u]) {
       int pos = rank[u];
 #pragma unroll
       for (int k = 0; k < 4; ++k) if (q[u] == k) pos += off[k];
       const unsigned* src = sb32 + (size_t)row * W;
       unsigned* dst = db32 + (size_t)pos * W;
-      if ((stride & 15) == 0 && stride <= 64) {      // 16-B aligned rows: vector copy
+      if (NV > 0) {
+        uint4* d4 = (uint4*)dst;
+        d4[0] = rv0[u];
+        if (NV > 1) d4[1] = rv1[u];
+      } else if ((stride & 15) == 0 && stride <= 64) {      // 16-B aligned rows: vector copy
         const uint4* s4 = (const uint4*)src;
         uint4* d4 = (uint4*)dst;
         const int nv = stride >> 4;
@@ -1307,6 +1346,12 @@ int h2o_subtract(void* hist_next, const void* hist_cur, const void* hbuild, cons
   return (int)hipGetLastError();
 }
 
+static bool route_generic() {   // H2O_ROUTE_GENERIC=1: byte-load path (A/B measurements)
+  static int v = -1;
+  if (v < 0) { const char* e = getenv("H2O_ROUTE_GENERIC"); v = (e && e[0] == '1') ? 1 : 0; }
+  return v == 1;
+}
+
 // two: route two levels (else one); move: regroup continuing rows into the destination buffers
 int h2o_route(const void* sbins, const void* saux, const void* sridx, void* dbins, void* daux, void* dridx,
               int stride, const void* nodesA, const void* tpA, const void* metaA, const void* decA, const void* clA,
@@ -1316,10 +1361,15 @@ int h2o_route(const void* sbins, const void* saux, const void* sridx, void* dbin
     (int*)dridx, stride, (const Node*)nodesA, (const int*)tpA, (const int*)metaA, (const Dec*)decA,          \
     (const int*)clA, (const int*)crA, (const Dec*)decB, (const int*)clB, (const int*)crB, (int4*)curs,       \
     (int*)leaf_of_row, (double*)leafsum
-  if (two && move) hipLaunchKernelGGL((k_route<true, true>), dim3(tiles_cap), dim3(LW * 64), 0, s, ROUTE_ARGS);
-  else if (two) hipLaunchKernelGGL((k_route<true, false>), dim3(tiles_cap), dim3(LW * 64), 0, s, ROUTE_ARGS);
-  else if (!move) hipLaunchKernelGGL((k_route<false, false>), dim3(tiles_cap), dim3(LW * 64), 0, s, ROUTE_ARGS);
-  else return (int)hipErrorInvalidValue;  // moving after a single level is never needed
+#define ROUTE_LAUNCH(NV)                                                                                   \
+  if (two && move) hipLaunchKernelGGL((k_route<true, true, NV>), dim3(tiles_cap), dim3(LW * 64), 0, s, ROUTE_ARGS); \
+  else if (two) hipLaunchKernelGGL((k_route<true, false, NV>), dim3(tiles_cap), dim3(LW * 64), 0, s, ROUTE_ARGS); \
+  else if (!move) hipLaunchKernelGGL((k_route<false, false, NV>), dim3(tiles_cap), dim3(LW * 64), 0, s, ROUTE_ARGS); \
+  else return (int)hipErrorInvalidValue;  /* moving after a single level is never needed */
+  if (stride == 32 && !route_generic()) { ROUTE_LAUNCH(2) }
+  else if (stride == 16 && !route_generic()) { ROUTE_LAUNCH(1) }
+  else { ROUTE_LAUNCH(0) }
+#undef ROUTE_LAUNCH
 #undef ROUTE_ARGS
   return (int)hipGetLastError();
 }
