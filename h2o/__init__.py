@@ -266,6 +266,19 @@ def make_metrics(predicted, actual, domain=None, distribution=None, weights=None
     return mm.make_metrics(cat, y, P, w, dom, distribution)
 
 
+def upload_custom_metric(func, func_file="metrics.py", func_name=None, class_name=None, source_provider=None):
+    """Register a CMetricFunc class (map / reduce / metric); returns the ``custom_metric_func`` reference."""
+    from llama_github_io_amd import udf
+    return udf.upload_custom_metric(func, func_file, func_name, class_name, source_provider)
+
+
+def upload_custom_distribution(func, func_file="distributions.py", func_name=None, class_name=None,
+                               source_provider=None):
+    """Register a CDistributionFunc class (link / init / gradient / gamma) for ``distribution="custom"``."""
+    from llama_github_io_amd import udf
+    return udf.upload_custom_distribution(func, func_file, func_name, class_name, source_provider)
+
+
 def download_pojo(model, path="", get_jar=True, jar_name=""):
     """Java source of a scoring class extending hex.genmodel.GenModel (GBM/DRF/IF/GLM/KMeans)."""
     from llama_github_io_amd.mojo.pojo import download_pojo as _dp

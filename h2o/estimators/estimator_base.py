@@ -82,6 +82,23 @@ class H2OEstimator:
         self.model_id = m.key
         return self
 
+    def train_segments(self, x=None, y=None, training_frame=None, offset_column=None, weights_column=None,
+                       validation_frame=None, max_runtime_secs=None, segments=None, segment_models_id=None,
+                       parallelism=1, verbose=False):
+        """One model per segment (``hex/segments/SegmentModelsBuilder.java``); the segment columns come from
+        the ``segment_columns`` parameter. Returns an ``H2OSegmentModels``-like object (``as_frame()``)."""
+        from llama_github_io_amd.segments import train_segments
+        p = dict(self._parms)
+        seg_cols = p.pop("segment_columns", None)
+        if not seg_cols:
+            raise ValueError("set segment_columns on the estimator before train_segments()")
+        for k, v in (("offset_column", offset_column), ("weights_column", weights_column),
+                     ("max_runtime_secs", max_runtime_secs)):
+            if v is not None:
+                p[k] = v
+        return train_segments(self.algo, p, x, y, training_frame, seg_cols, segments, validation_frame, parallelism,
+                              segment_models_id)
+
     def fit(self, X, y=None, **kw):  # scikit-learn style
         return self.train(x=None, y=y, training_frame=X, **kw)
 

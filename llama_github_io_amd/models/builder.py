@@ -42,7 +42,8 @@ def register(name, trainer, supervised=True, defaults=None, **kw):
 
 COMMON = ("nfolds", "fold_assignment", "fold_column", "keep_cross_validation_predictions", "keep_cross_validation_models",
           "keep_cross_validation_fold_assignment", "weights_column", "offset_column", "ignored_columns",
-          "ignore_const_cols", "model_id", "training_frame", "validation_frame", "response_column", "x", "y")
+          "ignore_const_cols", "model_id", "training_frame", "validation_frame", "response_column", "x", "y",
+          "custom_metric_func")
 
 
 def _resolve_names(fr, cols):
@@ -192,6 +193,10 @@ def train(algo: str, params: dict, x=None, y=None, training_frame=None, validati
     if cv_out is not None:
         model.cv_holdout = cv_out.pop("_cv_holdout", None)
         model.output.update(cv_out)
+    if p.get("custom_metric_func") and yv is not None:
+        _custom_metric(model, p["custom_metric_func"], X, yv, w, off, "training_metrics")
+        if valid is not None:
+            _custom_metric(model, p["custom_metric_func"], *valid, "validation_metrics")
     model.output["run_time_ms"] = int((time.time() - t0) * 1000)
     model.algo = algo
     dkv.put(model.key, model)
@@ -199,6 +204,29 @@ def train(algo: str, params: dict, x=None, y=None, training_frame=None, validati
         from ..persist import save_model
         save_model(model, p["export_checkpoints_dir"], force=True)
     return model
+
+
+def _custom_metric(model, ref, X, y, w, off, which):
+    """custom_metric_func (hex/CustomMetric.java): evaluated on the model's predictions in the reference
+    row layout ([label, p0, p1, ...] for classifiers, [value] otherwise) and stored in the metrics."""
+    from .. import udf
+    mets = model.output.get(which)
+    if mets is None:
+        return
+    P = model.score_tensor(X, off).double()
+    if P.dim() == 2:
+        if P.shape[1] == 2 and model.default_threshold() is not None:
+            lab = (P[:, 1] >= float(model.default_threshold())).double()
+        else:
+            lab = P.argmax(1).double()
+        rows = torch.cat([lab[:, None], P], 1)
+    else:
+        rows = P[:, None]
+    name, val = udf.custom_metric_value(ref, rows.cpu().numpy(), y.double().cpu().numpy(),
+                                        None if w is None else w.double().cpu().numpy(),
+                                        None if off is None else off.double().cpu().numpy(), model)
+    mets["custom_metric_name"] = name
+    mets["custom_metric_value"] = val
 
 
 def _cross_validate(spec, p, fr, info, X, yv, w, off, seed, mid, job):

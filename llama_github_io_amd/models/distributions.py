@@ -262,7 +262,61 @@ class Huber(Distribution):
         return torch.where(r <= d, w * r * r, w * (2 * r - d) * d)
 
 
-_DISTS = {c.name: c for c in (Gaussian, Bernoulli, Quasibinomial, ModifiedHuber, Multinomial, Poisson, Gamma, Tweedie,
+class Custom(Distribution):
+    """``distribution="custom"`` with ``custom_distribution_func`` (DistributionFactory.CustomDistribution):
+    gradient / init / gamma terms come from the uploaded CDistributionFunc (``udf.py``); leaves are the
+    plain Newton ratio num/den (GBM.GammaPass.gamma applies no link for custom), the initial value is
+    link(num/den) with the user's link."""
+    name = "custom"
+
+    def __init__(self, custom_distribution_func=None, **kw):
+        super().__init__(**{k: v for k, v in kw.items() if k in ("tweedie_power", "quantile_alpha", "huber_alpha")})
+        from ..udf import CustomDistributionFns
+        if not custom_distribution_func:
+            raise ValueError("distribution='custom' needs custom_distribution_func (h2o.upload_custom_distribution)")
+        self.fns = CustomDistributionFns(custom_distribution_func)
+        self.link = self.fns.link
+
+    @staticmethod
+    def _np(t):
+        return t.detach().double().cpu().numpy()
+
+    def _t(self, a, like):
+        return torch.as_tensor(a, dtype=like.dtype, device=like.device)
+
+    def linkinv(self, f):
+        if self.link == "inverse":
+            return 1.0 / f
+        return super().linkinv(f)
+
+    def neg_half_gradient(self, y, f):
+        return self._t(self.fns.gradient(self._np(y), self._np(f)), f)
+
+    def gamma_num(self, w, y, z, f):
+        num, self._den = self.fns.gamma(self._np(w), self._np(y), self._np(z), self._np(f))
+        return self._t(num, f)
+
+    def gamma_denom(self, w, y, z, f):
+        return self._t(self._den, f)
+
+    def init_f(self, y, w, offset=None, reduce=float):
+        o = torch.zeros_like(y) if offset is None else offset
+        num, den = self.fns.init(self._np(w), self._np(o), self._np(y))
+        g = reduce(float(num.sum())) / max(reduce(float(den.sum())), 1e-300)
+        if self.link == "log":
+            return math.log(max(g, 1e-300))
+        if self.link == "logit":
+            g = min(max(g, 1e-15), 1 - 1e-15)
+            return math.log(g / (1 - g))
+        if self.link == "inverse":
+            return 1.0 / g
+        return g
+
+    def leaf_gamma(self, num, den):
+        return torch.where(den == 0, torch.zeros_like(num), num / torch.where(den == 0, torch.ones_like(den), den))
+
+
+_DISTS = {c.name: c for c in (Custom, Gaussian, Bernoulli, Quasibinomial, ModifiedHuber, Multinomial, Poisson, Gamma, Tweedie,
                               Laplace, Quantile, Huber)}
 # quantile-type leaves (median / alpha-quantile of residuals per leaf)
 ORDER_STAT_DISTS = ("laplace", "quantile", "huber")
@@ -272,4 +326,6 @@ def get_distribution(name: str, **kw) -> Distribution:
     name = name.lower()
     if name not in _DISTS:
         raise ValueError(f"unsupported distribution '{name}'")
+    if name != "custom":
+        kw.pop("custom_distribution_func", None)
     return _DISTS[name](**kw)

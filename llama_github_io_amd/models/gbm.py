@@ -57,13 +57,17 @@ class GBMModel(SharedTreeModel):
         if d.name in ("bernoulli", "quasibinomial", "modified_huber"):
             p1 = torch.sigmoid(f[:, 0])
             return torch.stack([1 - p1, p1], 1)
+        if d.name == "custom" and self.model_category == "Binomial":
+            p1 = d.linkinv(f[:, 0]).clamp(0, 1)
+            return torch.stack([1 - p1, p1], 1)
         return d.linkinv(f[:, 0])
 
     @property
     def distribution(self):
         return get_distribution(self.output["distribution"], tweedie_power=self.params.get("tweedie_power", 1.5),
                                 quantile_alpha=self.params.get("quantile_alpha", 0.5),
-                                huber_alpha=self.params.get("huber_alpha", 0.9))
+                                huber_alpha=self.params.get("huber_alpha", 0.9),
+                                custom_distribution_func=self.params.get("custom_distribution_func"))
 
     def staged_predict_proba(self, X):
         out = []
@@ -94,7 +98,8 @@ class GBMTrainer(SharedTreeTrainer):
     def fit(self, X, y, w, offset, info, valid=None, model_key=None):
         dname = resolve_distribution(self.p.get("distribution"), info)
         self.dist = get_distribution(dname, tweedie_power=self.p["tweedie_power"], quantile_alpha=self.p["quantile_alpha"],
-                                     huber_alpha=self.p["huber_alpha"])
+                                     huber_alpha=self.p["huber_alpha"],
+                                     custom_distribution_func=self.p.get("custom_distribution_func"))
         self.dname = dname
         self.K = len(info.response_domain) if dname == "multinomial" else 1
         return super().fit(X, y, w, offset, info, valid, model_key)

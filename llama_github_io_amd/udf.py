@@ -1,0 +1,102 @@
+"""User-defined functions: custom metrics and custom GBM distributions (reference:
+``h2o-core/src/main/java/water/udf/CFuncRef.java``, ``CMetricFunc.java``, ``CDistributionFunc.java``,
+``hex/CustomMetric.java``, ``hex/DistributionFactory.java:CustomDistribution``; client side
+``h2o-py/h2o/h2o.py:upload_custom_metric`` / ``upload_custom_distribution``).
+
+The reference ships the user's class to the cluster and runs it under Jython, row by row. Here the
+user's class object runs in-process: it is first called with whole NumPy columns (most metric /
+gradient code is plain arithmetic and vectorises as written); a function that only handles scalars
+falls back to a per-row loop with the reference's row-wise semantics. References keep the reference
+string format ``python:<key>=<module>.<Class>Wrapper``. Only class objects are accepted (source
+strings are not compiled here).
+"""
+from __future__ import annotations
+
+import inspect
+
+import numpy as np
+
+_REGISTRY: dict = {}
+
+
+def _register(func, func_file, func_name, kind, methods):
+    module = func_file[:-3] if func_file.endswith(".py") else func_file
+    if not inspect.isclass(func):
+        raise TypeError("pass the custom function as a class (source strings are not supported)")
+    for m in methods:
+        if not callable(getattr(func, m, None)):
+            raise TypeError(f"the {kind} class needs a `{m}` method")
+    key = func_name or f"{kind}_{func.__name__}"
+    _REGISTRY[key] = func()
+    return f"python:{key}={module}.{func.__name__}Wrapper"
+
+
+def upload_custom_metric(func, func_file="metrics.py", func_name=None, class_name=None, source_provider=None):
+    return _register(func, func_file, func_name, "metrics", ("map", "reduce", "metric"))
+
+
+def upload_custom_distribution(func, func_file="distributions.py", func_name=None, class_name=None,
+                               source_provider=None):
+    return _register(func, func_file, func_name, "distributions", ("link", "init", "gradient", "gamma"))
+
+
+def resolve(ref: str):
+    if not isinstance(ref, str) or not ref.startswith("python:"):
+        raise ValueError(f"not a custom function reference: {ref!r}")
+    key = ref[len("python:"):].split("=", 1)[0]
+    if key not in _REGISTRY:
+        raise KeyError(f"custom function {key} was not uploaded")
+    return key, _REGISTRY[key]
+
+
+def custom_metric_value(ref: str, preds: np.ndarray, actual: np.ndarray, w=None, offset=None, model=None):
+    """CMetricFunc over all rows: map(pred_row, act_row, w, o, model) -> state, reduce, metric.
+    ``preds`` [N, P] in the reference's prediction layout ([label, p0, p1, ...] or [value]),
+    ``actual`` [N] (class index for classification)."""
+    name, obj = resolve(ref)
+    n = preds.shape[0]
+    w = np.ones(n) if w is None else np.asarray(w, dtype=np.float64)
+    o = np.zeros(n) if offset is None else np.asarray(offset, dtype=np.float64)
+    try:                                    # vectorised: columns in, per-row state columns out, summed
+        st = obj.map(preds.T, actual[None, :], w, o, model)
+        state = [float(np.sum(s)) for s in st]
+        if not all(np.isfinite(v) for v in state):
+            raise ValueError("non-finite vectorised state")
+    except Exception:                       # noqa: BLE001 - scalar-only user code: row-wise path
+        state = None
+        for i in range(n):
+            s = obj.map(list(preds[i]), [float(actual[i])], float(w[i]), float(o[i]), model)
+            state = s if state is None else obj.reduce(state, s)
+    return name, float(obj.metric(state))
+
+
+class CustomDistributionFns:
+    """Vectorised adapter over a user CDistributionFunc (see module doc)."""
+
+    def __init__(self, ref):
+        self.ref = ref
+        _, self.obj = resolve(ref)
+        self.link = str(self.obj.link())
+
+    def _call(self, fn, *arrays, n_out=1):
+        shape = arrays[-1].shape
+        try:
+            r = fn(*arrays)
+            if n_out == 1:
+                return np.broadcast_to(np.asarray(r, dtype=np.float64), shape).copy()
+            return [np.broadcast_to(np.asarray(v, dtype=np.float64), shape).copy() for v in r]
+        except Exception:                   # noqa: BLE001 - scalar-only user code
+            cols = [a.tolist() for a in arrays]
+            rows = [fn(*[c[i] for c in cols]) for i in range(len(cols[0]))]
+            if n_out == 1:
+                return np.asarray(rows, dtype=np.float64)
+            return [np.asarray([r[k] for r in rows], dtype=np.float64) for k in range(n_out)]
+
+    def gradient(self, y, f):
+        return self._call(self.obj.gradient, y, f)
+
+    def init(self, w, o, y):
+        return self._call(self.obj.init, w, o, y, n_out=2)
+
+    def gamma(self, w, y, z, f):
+        return self._call(self.obj.gamma, w, y, z, f, n_out=2)

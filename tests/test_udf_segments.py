@@ -1,0 +1,86 @@
+"""Custom metrics / custom GBM distribution (water/udf/*) and segment models (hex/segments/*)."""
+import numpy as np
+import pandas as pd
+import pytest
+
+import h2o
+from h2o.estimators import H2OGeneralizedLinearEstimator, H2OGradientBoostingEstimator
+
+
+@pytest.fixture(scope="module")
+def df():
+    h2o.init(verbose=False)
+    rng = np.random.default_rng(7)
+    n = 900
+    d = pd.DataFrame({"a": rng.normal(size=n), "b": rng.normal(size=n), "seg": rng.choice(["s1", "s2", "s3"], n)})
+    d["r"] = 2 * d.a - d.b + (d.seg == "s2") * 3 + rng.normal(size=n) * 0.2
+    d["y"] = np.where(d.a + rng.normal(size=n) * 0.5 > 0, "1", "0")
+    return h2o.H2OFrame(d, column_types={"seg": "enum", "y": "enum"})
+
+
+class CustomMae:
+    def map(self, pred, act, w, o, model):
+        return [w * abs(act[0] - pred[0]), w]
+
+    def reduce(self, l, r):
+        return [l[0] + r[0], l[1] + r[1]]
+
+    def metric(self, l):
+        return l[0] / l[1]
+
+
+class ScalarOnlyMae(CustomMae):
+    def map(self, pred, act, w, o, model):
+        import math
+        return [w * math.fabs(act[0] - pred[0]), w]
+
+
+class CustomGaussian:
+    def link(self):
+        return "identity"
+
+    def init(self, w, o, y):
+        return [w * (y - o), w]
+
+    def gradient(self, y, f):
+        return y - f
+
+    def gamma(self, w, y, z, f):
+        return [w * z, w]
+
+
+@pytest.mark.parametrize("cls", [CustomMae, ScalarOnlyMae])
+def test_custom_metric_matches_mae(df, cls):
+    ref = h2o.upload_custom_metric(cls, func_name=f"mae_{cls.__name__}")
+    assert ref.startswith("python:mae_")
+    m = H2OGradientBoostingEstimator(ntrees=5, seed=1, custom_metric_func=ref)
+    m.train(x=["a", "b", "seg"], y="r", training_frame=df)
+    tm = m._model.output["training_metrics"]
+    assert tm["custom_metric_name"] == f"mae_{cls.__name__}"
+    assert tm["custom_metric_value"] == pytest.approx(tm["mae"], rel=1e-6)
+
+
+def test_custom_distribution_equals_gaussian(df):
+    ref = h2o.upload_custom_distribution(CustomGaussian, func_name="custom_gaussian")
+    kw = dict(ntrees=6, max_depth=3, seed=1)
+    c = H2OGradientBoostingEstimator(distribution="custom", custom_distribution_func=ref, **kw)
+    c.train(x=["a", "b", "seg"], y="r", training_frame=df)
+    g = H2OGradientBoostingEstimator(distribution="gaussian", **kw)
+    g.train(x=["a", "b", "seg"], y="r", training_frame=df)
+    pc = c.predict(df).as_data_frame().values[:, 0]
+    pg = g.predict(df).as_data_frame().values[:, 0]
+    np.testing.assert_allclose(pc, pg, rtol=1e-5, atol=1e-5)
+
+
+def test_segment_models(df):
+    est = H2OGeneralizedLinearEstimator(family="gaussian", segment_columns=["seg"])
+    sm = est.train_segments(x=["a", "b"], y="r", training_frame=df, parallelism=2)
+    tab = sm.as_frame().as_data_frame()
+    assert sorted(tab["seg"].tolist()) == ["s1", "s2", "s3"]
+    assert (tab["status"] == "SUCCEEDED").all()
+    for m, s in zip(sm.models(), tab["seg"]):
+        assert m.coef()["a"] == pytest.approx(2.0, abs=0.1)
+    # a segment that cannot train is reported, not raised
+    bad = H2OGeneralizedLinearEstimator(family="binomial", segment_columns="seg")
+    sm2 = bad.train_segments(x=["a", "b"], y="r", training_frame=df)
+    assert (sm2.as_frame().as_data_frame()["status"] == "FAILED").all()
