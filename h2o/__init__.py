@@ -266,6 +266,12 @@ def make_metrics(predicted, actual, domain=None, distribution=None, weights=None
     return mm.make_metrics(cat, y, P, w, dom, distribution)
 
 
+def resume(recovery_dir=None):
+    """Resume an interrupted grid search from its ``recovery_dir`` snapshot (/3/Recovery/resume)."""
+    from llama_github_io_amd import grid as _g
+    return _g.resume(recovery_dir)
+
+
 def upload_custom_metric(func, func_file="metrics.py", func_name=None, class_name=None, source_provider=None):
     """Register a CMetricFunc class (map / reduce / metric); returns the ``custom_metric_func`` reference."""
     from llama_github_io_amd import udf

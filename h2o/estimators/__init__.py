@@ -42,7 +42,8 @@ def _extra():
             ("H2OModelSelectionEstimator", "modelselection", True),
             ("H2OUpliftRandomForestEstimator", "upliftdrf", True),
             ("H2ODecisionTreeEstimator", "dt", True),
-            ("H2OInfogram", "infogram", True)):
+            ("H2OInfogram", "infogram", True),
+            ("H2OGrepEstimator", "grep", False)):
         if cls_name not in g:
             g[cls_name] = make_estimator(cls_name, algo, sup)
 

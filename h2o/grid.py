@@ -13,6 +13,7 @@ class H2OGridSearch:
         self.grid_id = grid_id
         self.search_criteria = search_criteria
         self.parallelism = parallelism
+        self.recovery_dir = recovery_dir
         self._grid = None
 
     def train(self, x=None, y=None, training_frame=None, offset_column=None, fold_column=None, weights_column=None,
@@ -24,7 +25,8 @@ class H2OGridSearch:
                 base[k] = v
         job = Job(f"grid {self.model.algo}", dest=self.grid_id)
         self._grid = job.run_sync(_grid.grid_search, self.model.algo, self.hyper_params, base, x, y, training_frame,
-                                  validation_frame, self.grid_id, self.search_criteria, self.parallelism, job)
+                                  validation_frame, self.grid_id, self.search_criteria, self.parallelism, job,
+                                  self.recovery_dir)
         self.grid_id = self._grid.grid_id
         return self
 

@@ -422,9 +422,19 @@ def create_app():
         fr = dkv.get(p.pop("training_frame"))
         vf = p.pop("validation_frame", None)
         y = p.pop("response_column", None)
+        rdir = p.pop("recovery_dir", None)
         job = Job(f"grid {algo}", dest=gid)
-        job.run_async(grid_search, algo, hyper, p, None, y, fr, dkv.get(vf) if vf else None, gid, crit, 1, job)
+        job.run_async(grid_search, algo, hyper, p, None, y, fr, dkv.get(vf) if vf else None, gid, crit, 1, job, rdir)
         return dict(job=_clean(job.to_dict()), grid_id=dict(name=gid))
+
+    @app.post("/3/Recovery/resume")
+    async def recovery_resume(request: Request):
+        """hex/faulttolerance/Recovery.java: continue an interrupted grid from its recovery_dir."""
+        from ..grid import resume
+        p = await _params(request)
+        job = Job("recovery resume", dest=None)
+        job.run_async(resume, p["recovery_dir"])
+        return dict(job=_clean(job.to_dict()), recovery_dir=p["recovery_dir"])
 
     @app.get("/99/Grids/{gid}")
     def get_grid(gid: str, sort_by: str | None = None, decreasing: bool | None = None):

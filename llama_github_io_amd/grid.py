@@ -4,7 +4,10 @@ metric), ``hex/grid/Grid.java`` (sorted model table))."""
 from __future__ import annotations
 
 import itertools
+import json
 import math
+import os
+import shutil
 import time
 
 import numpy as np
@@ -70,10 +73,13 @@ def walk(hyper_params: dict, criteria: dict | None, seed=None):
 
 
 def grid_search(algo, hyper_params, base_params, x, y, training_frame, validation_frame=None, grid_id=None,
-                search_criteria=None, parallelism=1, job=None) -> Grid:
+                search_criteria=None, parallelism=1, job=None, recovery_dir=None) -> Grid:
     crit = dict(search_criteria or {})
     grid_id = grid_id or dkv.new_key(f"Grid_{algo.upper()}")
     grid = dkv.get(grid_id) if isinstance(dkv.get(grid_id), Grid) else Grid(grid_id, algo, hyper_params, base_params)
+    rec = _Recovery(recovery_dir) if recovery_dir else None
+    if rec is not None:
+        rec.on_start(grid, x, y, training_frame, validation_frame, crit)
     names, combos = walk(hyper_params, crit, crit.get("seed"))
     max_models = int(crit.get("max_models", 0) or 0)
     max_rt = float(crit.get("max_runtime_secs", 0) or 0)
@@ -100,6 +106,8 @@ def grid_search(algo, hyper_params, base_params, x, y, training_frame, validatio
             continue
         grid.models.append(m)
         grid.hyper_values.append(list(combo))
+        if rec is not None:
+            rec.on_model(grid, m, combo)
         if job is not None:
             job.update(1.0 / max(1, len(combos)))
         if stop_rounds > 0:
@@ -114,4 +122,85 @@ def grid_search(algo, hyper_params, base_params, x, y, training_frame, validatio
                 if imp < stop_tol:
                     break
     dkv.put(grid_id, grid)
+    if rec is not None:
+        rec.on_done()
     return grid
+
+
+# ================================================================================================
+# auto-recovery (reference: hex/faulttolerance/Recovery.java, Recoverable.java, /3/Recovery/resume)
+class _Recovery:
+    """Snapshot of a running grid in ``recovery_dir``: ``recovery.json`` (grid definition, references),
+    the training / validation frames (binary frame save) and every finished model, so an interrupted
+    search resumes with :func:`resume` without retraining finished models. Cleaned up on success."""
+
+    META = "recovery.json"
+
+    def __init__(self, path):
+        self.path = path
+        os.makedirs(path, exist_ok=True)
+
+    def _write(self, meta):
+        tmp = os.path.join(self.path, self.META + ".tmp")
+        with open(tmp, "w") as f:
+            json.dump(meta, f, default=str)
+        os.replace(tmp, os.path.join(self.path, self.META))
+
+    def on_start(self, grid, x, y, training_frame, validation_frame, crit):
+        from .io.parse import save_frame
+        save_frame(training_frame, os.path.join(self.path, "frames", "train"))
+        if validation_frame is not None:
+            save_frame(validation_frame, os.path.join(self.path, "frames", "valid"))
+        self.meta = dict(kind="grid", grid_id=grid.grid_id, algo=grid.algo, hyper_params=grid.hyper_params,
+                         base_params={k: v for k, v in grid.base_params.items() if _jsonable(v)}, x=x, y=y,
+                         search_criteria=crit, training_frame=training_frame.frame_id,
+                         validation_frame=None if validation_frame is None else validation_frame.frame_id,
+                         has_valid=validation_frame is not None, models=[])
+        for m, hv in zip(grid.models, grid.hyper_values):
+            self.on_model(grid, m, hv, write=False)
+        self._write(self.meta)
+
+    def on_model(self, grid, model, combo, write=True):
+        from .persist import save_model
+        path = save_model(model, os.path.join(self.path, "models"), force=True)
+        self.meta["models"].append(dict(key=model.key, path=path, hyper=[_jsonable_value(v) for v in combo]))
+        if write:
+            self._write(self.meta)
+
+    def on_done(self):
+        shutil.rmtree(self.path, ignore_errors=True)
+
+
+def _jsonable(v):
+    try:
+        json.dumps(v)
+        return True
+    except TypeError:
+        return False
+
+
+def _jsonable_value(v):
+    return v if _jsonable(v) else str(v)
+
+
+def resume(recovery_dir: str) -> Grid:
+    """``h2o.resume`` / ``/3/Recovery/resume``: reload the snapshot and continue the interrupted search."""
+    from .io.parse import load_frame
+    from .persist import load_model
+    with open(os.path.join(recovery_dir, _Recovery.META)) as f:
+        meta = json.load(f)
+    train = load_frame(meta["training_frame"], os.path.join(recovery_dir, "frames", "train"))
+    dkv.put(meta["training_frame"], train)
+    valid = None
+    if meta.get("has_valid"):
+        valid = load_frame(meta["validation_frame"], os.path.join(recovery_dir, "frames", "valid"))
+        dkv.put(meta["validation_frame"], valid)
+    grid = Grid(meta["grid_id"], meta["algo"], meta["hyper_params"], meta["base_params"])
+    for rec in meta["models"]:
+        m = load_model(rec["path"])
+        dkv.put(m.key, m)
+        grid.models.append(m)
+        grid.hyper_values.append(rec["hyper"])
+    dkv.put(grid.grid_id, grid)
+    return grid_search(meta["algo"], meta["hyper_params"], meta["base_params"], meta["x"], meta["y"], train, valid,
+                       meta["grid_id"], meta["search_criteria"], recovery_dir=recovery_dir)

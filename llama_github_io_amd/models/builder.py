@@ -150,6 +150,11 @@ def train(algo: str, params: dict, x=None, y=None, training_frame=None, validati
     spec = REGISTRY[algo]
     p = dict(spec.defaults)
     p.update({k: v for k, v in params.items() if v is not None})
+    if algo == "grep":                          # raw-text scan: no DataInfo / device tensors
+        m = spec.trainer(p).fit_text(training_frame, model_id or p.get("model_id"))
+        m.algo = "grep"
+        dkv.put(m.key, m)
+        return m
     if algo == "generic":                       # import a MOJO: no training frame involved
         m = spec.trainer(p).fit(model_key=model_id or p.get("model_id"))
         m.algo = "generic"

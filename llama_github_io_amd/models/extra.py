@@ -27,6 +27,7 @@ _ALGOS = [
     ("dt", "dt", "DTTrainer", True, dict(classification_only=True)),
     ("infogram", "infogram", "InfogramTrainer", True, {}),
     ("quantile", "quantile", "QuantileTrainer", False, {}),
+    ("grep", "grep", "GrepTrainer", False, {}),
 ]
 
 for name, mod, cls, sup, kw in _ALGOS:

@@ -84,3 +84,57 @@ def test_segment_models(df):
     bad = H2OGeneralizedLinearEstimator(family="binomial", segment_columns="seg")
     sm2 = bad.train_segments(x=["a", "b"], y="r", training_frame=df)
     assert (sm2.as_frame().as_data_frame()["status"] == "FAILED").all()
+
+
+def test_grep_model(tmp_path):
+    from h2o.estimators import H2OGrepEstimator
+    from llama_github_io_amd.models import grep as G
+    h2o.init(verbose=False)
+    text = "alpha beta\ngamma alphabet\nalpha"
+    p = tmp_path / "t.txt"
+    p.write_text(text)
+    g = H2OGrepEstimator(regex="alpha[a-z]*", path=str(p))
+    g.train()
+    assert g._model.matches() == ["alpha", "alphabet", "alpha"]
+    assert g._model.offsets() == [m.start() for m in __import__("re").finditer("alpha[a-z]*", text)]
+    # chunk boundaries: a match straddling two chunks is reported exactly once
+    old = G._CHUNK
+    try:
+        G._CHUNK = 7
+        m, o = G.grep_text(text, "alpha[a-z]*")
+        assert m == ["alpha", "alphabet", "alpha"]
+    finally:
+        G._CHUNK = old
+
+
+def test_grid_recovery_resumes_without_retraining(df, tmp_path, monkeypatch):
+    from h2o.grid import H2OGridSearch
+    from llama_github_io_amd import grid as G
+    from llama_github_io_amd.models import builder
+    rdir = str(tmp_path / "rec")
+    calls = []
+    real = builder.train
+
+    def crashing(algo, p, *a, **k):
+        calls.append(p["max_depth"])
+        if len(calls) == 3:
+            raise KeyboardInterrupt("simulated node loss")
+        return real(algo, p, *a, **k)
+    monkeypatch.setattr(G.builder, "train", crashing)
+    gs = H2OGridSearch(H2OGradientBoostingEstimator(ntrees=3, seed=1), {"max_depth": [2, 3, 4, 5]},
+                       grid_id="rec_grid", recovery_dir=rdir)
+    with pytest.raises(KeyboardInterrupt):
+        G.grid_search("gbm", {"max_depth": [2, 3, 4, 5]}, dict(ntrees=3, seed=1), ["a", "b"], "r", df,
+                      grid_id="rec_grid", recovery_dir=rdir)
+    import json, os
+    meta = json.load(open(os.path.join(rdir, "recovery.json")))
+    assert [m["hyper"] for m in meta["models"]] == [[2], [3]]
+    from llama_github_io_amd.core import dkv
+    dkv.remove("rec_grid")
+    monkeypatch.setattr(G.builder, "train", lambda algo, p, *a, **k: (calls.append(p["max_depth"]), real(algo, p, *a, **k))[1])
+    calls.clear()
+    g = h2o.resume(rdir)
+    assert calls == [4, 5]                       # finished models were loaded, not retrained
+    assert sorted(h[0] for h in g.hyper_values) == [2, 3, 4, 5]
+    assert not os.path.exists(rdir)              # cleaned up on success
+    _ = gs
