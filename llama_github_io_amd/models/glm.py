@@ -172,6 +172,9 @@ class GLMModel(Model):
         self.family = None
 
     def _eta(self, X, offset=None):
+        if getattr(self, "hglm", None) is not None:
+            from .hglm import hglm_eta
+            return hglm_eta(self, X, offset)
         Z = self.expander.transform(X.to(self.device))
         b = self.beta.to(Z.device)
         eta = Z.double() @ b[:, :-1].T + b[:, -1]
@@ -223,12 +226,28 @@ class GLMModel(Model):
         s = super().to_state()
         s["beta"] = self.beta.cpu().tolist()
         s["expander"] = self.expander.to_state()
+        hg = getattr(self, "hglm", None)
+        if hg is not None:
+            s["hglm"] = dict(hg, u=hg["u"].cpu().tolist())
         return s
 
     def _restore(self, s):
         super()._restore(s)
         self.beta = torch.tensor(s["beta"], dtype=torch.float64)
-        self.expander = Expander.from_state(self.info, s["expander"])
+        hg = s.get("hglm")
+        if hg is not None:
+            from .base import DataInfo
+            fi = hg["fixed_idx"]
+            finfo = DataInfo([self.info.x[j] for j in fi], np.asarray(self.info.iscat)[fi],
+                             [self.info.domains[j] for j in fi], self.info.response, self.info.response_domain)
+            self.expander = Expander.from_state(finfo, s["expander"])
+            self.hglm = dict(hg, u=torch.tensor(hg["u"], dtype=torch.float64))
+        else:
+            self.expander = Expander.from_state(self.info, s["expander"])
+
+    def coefs_random(self):
+        """Random-effect coefficients of an HGLM model (``ubeta`` by level)."""
+        return self.output.get("random_coefficients")
 
     @staticmethod
     def getGLMRegularizationPath(model):
@@ -311,6 +330,17 @@ class GLMTrainer:
         t0 = time.time()
         p = self.p
         dev = X.device
+        if p.get("HGLM"):
+            from .hglm import fit_hglm
+            model = GLMModel(model_key or make_key("glm"), p, info)
+            model.device = dev
+            fit_hglm(self, X, y, w, offset, info, model, p)
+            model.output["training_metrics"] = model.metrics_for(X, y, w, offset)
+            if valid is not None:
+                Xv, yv, wv, ov = valid
+                model.output["validation_metrics"] = model.metrics_for(Xv, yv, wv, ov)
+            model.output["run_time_ms"] = int((time.time() - t0) * 1000)
+            return model
         fam, link = self._family(info)
         N = X.shape[1]
         w = torch.ones(N, dtype=torch.float64, device=dev) if w is None else w.double()
