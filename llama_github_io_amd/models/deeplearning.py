@@ -193,7 +193,10 @@ class DeepLearningTrainer:
             ok = ~torch.isnan(y)
             w = torch.where(ok, w, torch.zeros_like(w))
         ex = Expander(info, standardize=p["standardize"], use_all_factor_levels=p["use_all_factor_levels"]).fit(X, w)
-        Z = ex.transform(X)
+        # bf16 compute: the design matrix is materialised in bf16 (half the HBM footprint and per-step
+        # gather bytes; GEMM inputs need no per-step cast)
+        bf16 = dev.type == "cuda" and str(p["compute_dtype"]).lower() in ("bf16", "bfloat16") and not bool(p["autoencoder"])
+        Z = ex.transform(X, dtype=torch.bfloat16 if bf16 else torch.float32)
         act_name = str(p["activation"]).lower()
         with_drop = act_name.endswith("withdropout")
         base = act_name.replace("withdropout", "")

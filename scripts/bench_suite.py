@@ -67,6 +67,10 @@ def bench_dl(a, dev, world, rank):
     X = torch.rand(F, n, device=dev, generator=g)
     y = (X[:20].sum(0) > 10).float()
     info = DataInfo([f"p{i}" for i in range(F)], np.zeros(F, np.int32), [None] * F, "y", ["0", "1"])
+    # untimed warmup fit on a slice: library init / kernel autotuning / graph capture code paths
+    DeepLearningTrainer(dict(hidden=[200, 200], epochs=1, compute_dtype="bf16", mini_batch_size=a.batch, seed=1,
+                             stopping_rounds=0, score_interval=1e9, standardize=False)).fit(
+        X[:, :8 * a.batch].contiguous(), y[:8 * a.batch].contiguous(), None, None, info)
     _sync()
     t0 = time.perf_counter()
     m = DeepLearningTrainer(dict(hidden=[200, 200], epochs=a.epochs, compute_dtype="bf16", mini_batch_size=a.batch,
