@@ -9,6 +9,7 @@
 //        atomic per column per workgroup).
 // Activations: 0 linear, 1 Rectifier (ReLU), 2 Tanh, 3 ExpRectifier (ELU).
 #include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
 #include <stdint.h>
 
 namespace {
@@ -37,23 +38,32 @@ __device__ __forceinline__ float dact_from_y(int a, float y) {
   }
 }
 
-__global__ __launch_bounds__(256) void k_bias_act_fwd(const float* __restrict__ x, const float* __restrict__ b,
-                                                      float* __restrict__ y, int64_t rows, int cols, int act,
+// T = float or bf16 activations (bf16: GEMM outputs feed the epilogue and the next GEMM directly, no
+// fp32 round trip); bias, math and the bias gradient stay fp32.
+__device__ __forceinline__ float ld(const float* p, int64_t i) { return p[i]; }
+__device__ __forceinline__ float ld(const __hip_bfloat16* p, int64_t i) { return __bfloat162float(p[i]); }
+__device__ __forceinline__ void st(float* p, int64_t i, float v) { p[i] = v; }
+__device__ __forceinline__ void st(__hip_bfloat16* p, int64_t i, float v) { p[i] = __float2bfloat16(v); }
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_bias_act_fwd(const T* __restrict__ x, const float* __restrict__ b,
+                                                      T* __restrict__ y, int64_t rows, int cols, int act,
                                                       float drop, uint64_t seed) {
   const int64_t n = rows * (int64_t)cols;
   const float keep = 1.f - drop;
   const uint32_t thr = (uint32_t)(drop * 4294967296.0);
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int c = (int)(i % cols);
-    float v = act_f(act, x[i] + (b ? b[c] : 0.f));
+    float v = act_f(act, ld(x, i) + (b ? b[c] : 0.f));
     if (drop > 0.f) v = (hash32(seed ^ (uint64_t)i * 0x9E3779B97F4A7C15ULL) < thr) ? 0.f : v / keep;
-    y[i] = v;
+    st(y, i, v);
   }
 }
 
 // gx[i] = gy[i] * mask * act'(y); db[c] += sum_r gx[r, c]
-__global__ __launch_bounds__(256) void k_bias_act_bwd(const float* __restrict__ gy, const float* __restrict__ y,
-                                                      float* __restrict__ gx, float* __restrict__ db, int64_t rows,
+template <typename T>
+__global__ __launch_bounds__(256) void k_bias_act_bwd(const T* __restrict__ gy, const T* __restrict__ y,
+                                                      T* __restrict__ gx, float* __restrict__ db, int64_t rows,
                                                       int cols, int act, float drop, uint64_t seed, int rows_per_block) {
   // block handles a [rows_per_block x 64] column stripe: thread (ty, tx) with tx = column lane
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
@@ -67,15 +77,15 @@ __global__ __launch_bounds__(256) void k_bias_act_bwd(const float* __restrict__ 
   if (c < cols) {
     for (int64_t r = rbeg + ty; r < rend; r += 4) {
       const int64_t i = r * cols + c;
-      float yy = y[i];
-      float g = gy[i];
+      float yy = ld(y, i);
+      float g = ld(gy, i);
       if (drop > 0.f) {
         const bool dropped = hash32(seed ^ (uint64_t)i * 0x9E3779B97F4A7C15ULL) < thr;
         g = dropped ? 0.f : g / keep;
         yy = dropped ? 0.f : yy * keep;  // stored y was scaled by 1/keep
       }
       const float v = g * dact_from_y(act, yy);
-      gx[i] = v;
+      st(gx, i, v);
       acc += v;
     }
   }
@@ -118,21 +128,33 @@ int h2o_adadelta(float* p, const float* g, float* eg2, float* edx2, long long n,
 }
 
 
-int h2o_bias_act_fwd(const float* x, const float* b, float* y, long long rows, int cols, int act, float drop,
-                     unsigned long long seed, hipStream_t stream) {
+int h2o_bias_act_fwd(const void* x, const float* b, void* y, long long rows, int cols, int act, float drop,
+                     unsigned long long seed, int bf16, hipStream_t stream) {
   const long long n = rows * (long long)cols;
   int grid = (int)((n + 255) / 256);
   if (grid > 8192) grid = 8192;
   if (grid < 1) grid = 1;
-  hipLaunchKernelGGL(k_bias_act_fwd, dim3(grid), dim3(256), 0, stream, x, b, y, (int64_t)rows, cols, act, drop, seed);
+  if (bf16)
+    hipLaunchKernelGGL(k_bias_act_fwd<__hip_bfloat16>, dim3(grid), dim3(256), 0, stream, (const __hip_bfloat16*)x, b,
+                       (__hip_bfloat16*)y, (int64_t)rows, cols, act, drop, seed);
+  else
+    hipLaunchKernelGGL(k_bias_act_fwd<float>, dim3(grid), dim3(256), 0, stream, (const float*)x, b, (float*)y,
+                       (int64_t)rows, cols, act, drop, seed);
   return (int)hipGetLastError();
 }
 
-int h2o_bias_act_bwd(const float* gy, const float* y, float* gx, float* db, long long rows, int cols, int act,
-                     float drop, unsigned long long seed, hipStream_t stream) {
-  const int rpb = 256;
+int h2o_bias_act_bwd(const void* gy, const void* y, void* gx, float* db, long long rows, int cols, int act,
+                     float drop, unsigned long long seed, int bf16, hipStream_t stream) {
+  // enough row stripes to fill the chip: a [4096 x 200] mini-batch was 64 blocks (22.8 us); stripes of
+  // 32 rows give 512 blocks (the per-stripe bias partial is one atomic per column)
+  const int rpb = rows >= (1 << 16) ? 256 : 32;
   dim3 grid((cols + 63) / 64, (unsigned)((rows + rpb - 1) / rpb));
-  hipLaunchKernelGGL(k_bias_act_bwd, grid, dim3(256), 0, stream, gy, y, gx, db, (int64_t)rows, cols, act, drop, seed, rpb);
+  if (bf16)
+    hipLaunchKernelGGL(k_bias_act_bwd<__hip_bfloat16>, grid, dim3(256), 0, stream, (const __hip_bfloat16*)gy,
+                       (const __hip_bfloat16*)y, (__hip_bfloat16*)gx, db, (int64_t)rows, cols, act, drop, seed, rpb);
+  else
+    hipLaunchKernelGGL(k_bias_act_bwd<float>, grid, dim3(256), 0, stream, (const float*)gy, (const float*)y,
+                       (float*)gx, db, (int64_t)rows, cols, act, drop, seed, rpb);
   return (int)hipGetLastError();
 }
 

@@ -85,7 +85,9 @@ class MLP(torch.nn.Module):
                 if drop > 0:
                     x = x * (torch.rand(x.shape, device=x.device) >= drop).to(x.dtype) / (1 - drop)
             else:
-                x = bias_act(h.float(), lin.bias.float(), self.act, drop, (seed * 1000003 + i * 7919 + self.step) & ((1 << 62) - 1))
+                # bf16 GEMM outputs stay bf16 through the fused epilogue into the next GEMM (no fp32 round trip)
+                xin = h if (h.is_cuda and h.dtype == torch.bfloat16) else h.float()
+                x = bias_act(xin, lin.bias, self.act, drop, (seed * 1000003 + i * 7919 + self.step) & ((1 << 62) - 1))
             if features_layer is not None and i == features_layer:
                 return x
         return self.out(x)

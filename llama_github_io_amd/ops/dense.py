@@ -15,9 +15,9 @@ ACT = {"linear": 0, "rectifier": 1, "relu": 1, "tanh": 2, "exprectifier": 3, "el
 
 nat.register_hip_signatures({
     "h2o_bias_act_fwd": [nat.c_void_p, nat.c_void_p, nat.c_void_p, nat.c_ll, nat.c_int, nat.c_int, nat.ctypes.c_float,
-                         nat.c_ull, nat.c_void_p],
+                         nat.c_ull, nat.c_int, nat.c_void_p],
     "h2o_bias_act_bwd": [nat.c_void_p, nat.c_void_p, nat.c_void_p, nat.c_void_p, nat.c_ll, nat.c_int, nat.c_int,
-                         nat.ctypes.c_float, nat.c_ull, nat.c_void_p],
+                         nat.ctypes.c_float, nat.c_ull, nat.c_int, nat.c_void_p],
     "h2o_kmeans_assign": [nat.c_void_p, nat.c_ll, nat.c_int, nat.c_void_p, nat.c_int, nat.c_void_p, nat.c_void_p, nat.c_void_p],
     "h2o_kmeans_step": [nat.c_void_p, nat.c_ll, nat.c_int, nat.c_void_p, nat.c_int, nat.c_void_p, nat.c_void_p,
                         nat.c_void_p, nat.c_void_p, nat.c_void_p],
@@ -103,9 +103,12 @@ class BiasAct(torch.autograd.Function):
         x = x.contiguous()
         rows, cols = x.shape
         if x.is_cuda:
-            y = torch.empty_like(x)
-            nat.call("h2o_bias_act_fwd", x.data_ptr(), 0 if b is None else b.data_ptr(), y.data_ptr(), rows, cols, act,
-                     float(drop), seed & _M, nat.stream_ptr(x.device))
+            if x.dtype not in (torch.float32, torch.bfloat16):
+                x = x.float()
+            y = torch.empty_like(x)          # bf16 in -> bf16 out (fp32 bias and math inside the kernel)
+            bb = None if b is None else b.float().contiguous()
+            nat.call("h2o_bias_act_fwd", x.data_ptr(), 0 if bb is None else bb.data_ptr(), y.data_ptr(), rows, cols,
+                     act, float(drop), seed & _M, int(x.dtype == torch.bfloat16), nat.stream_ptr(x.device))
         else:
             y = _act(act, x + (b if b is not None else 0))
             if drop > 0:
@@ -121,10 +124,11 @@ class BiasAct(torch.autograd.Function):
         rows, cols = y.shape
         act, drop, seed = ctx.act, ctx.drop, ctx.seed
         if y.is_cuda:
+            gy = gy.to(y.dtype).contiguous()
             gx = torch.empty_like(y)
             db = torch.zeros(cols, dtype=torch.float32, device=y.device) if ctx.has_b else None
             nat.call("h2o_bias_act_bwd", gy.data_ptr(), y.data_ptr(), gx.data_ptr(), 0 if db is None else db.data_ptr(),
-                     rows, cols, act, float(drop), seed & _M, nat.stream_ptr(y.device))
+                     rows, cols, act, float(drop), seed & _M, int(y.dtype == torch.bfloat16), nat.stream_ptr(y.device))
         else:
             yy, g = y, gy
             if drop > 0:

@@ -61,6 +61,29 @@ def test_bias_act_fwd_bwd(act, drop):
     assert torch.allclose(bg.grad.cpu(), bc.grad, atol=1e-3, rtol=1e-4)
 
 
+@pytest.mark.parametrize("act", ["rectifier", "tanh"])
+@pytest.mark.parametrize("drop", [0.0, 0.3])
+def test_bias_act_bf16_matches_fp32_reference(act, drop):
+    # bf16 activations in/out (fp32 bias + math): equal to the fp32 PyTorch reference up to bf16 rounding
+    from llama_github_io_amd.ops.dense import bias_act
+    g = torch.Generator(device=dev).manual_seed(3)
+    x = torch.randn(4096, 200, device=dev, generator=g)
+    b = torch.randn(200, device=dev, generator=g)
+    gy = torch.randn(4096, 200, device=dev, generator=g)
+    xb = x.bfloat16().requires_grad_(True)
+    bg = b.clone().requires_grad_(True)
+    y = bias_act(xb, bg, act, drop, 77)
+    assert y.dtype == torch.bfloat16
+    y.backward(gy.bfloat16())
+    xc = xb.detach().float().cpu().requires_grad_(True)
+    bc = b.cpu().requires_grad_(True)
+    yc = bias_act(xc, bc, act, drop, 77)
+    yc.backward(gy.bfloat16().float().cpu())
+    assert torch.allclose(y.float().cpu(), yc, atol=2e-2, rtol=1e-2)
+    assert torch.allclose(xb.grad.float().cpu(), xc.grad, atol=3e-2, rtol=2e-2)
+    assert torch.allclose(bg.grad.cpu(), bc.grad, atol=0.5, rtol=1e-2)
+
+
 def _info(F, dom=("0", "1")):
     from llama_github_io_amd.models.base import DataInfo
     return DataInfo([f"x{i}" for i in range(F)], np.zeros(F, np.int32), [None] * F, "y", list(dom) if dom else None)
