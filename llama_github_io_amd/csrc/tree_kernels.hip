@@ -929,6 +929,10 @@ __device__ __forceinline__ int row_byte(uint4 v0, uint4 v1, int f) {
   const unsigned w = wi < 4 ? pick_word(v0, wi) : pick_word(v1, wi - 4);
   return (w >> (8 * (f & 3))) & 0xFF;
 }
+__device__ __forceinline__ int row_byte4(uint4 v0, uint4 v1, uint4 v2, uint4 v3, int f) {
+  // rows of up to 64 B (NV = 3, 4): f is block-uniform, so the compare chain is uniform too
+  return f < 32 ? row_byte(v0, v1, f) : row_byte(v2, v3, f - 32);
+}
 
 template <bool TWO, bool MOVE, int NV>
 __global__ __launch_bounds__(LW * 64) void k_route(
@@ -979,7 +983,7 @@ __global__ __launch_bounds__(LW * 64) void k_route(
   int cnt[4] = {0, 0, 0, 0};
   // NV > 0: all of the tile's loads issued before any decision (rows clamped into the node: no divergence).
   // Plain per-u scalars (not a 2-D array) so everything stays in VGPRs.
-  uint4 rv0[LU], rv1[LU];
+  uint4 rv0[LU], rv1[LU], rv2[LU], rv3[LU];
   float4 ra[LU];
   int rx[LU];
   if (NV > 0) {
@@ -989,6 +993,8 @@ __global__ __launch_bounds__(LW * 64) void k_route(
       const uint4* s4 = (const uint4*)(sbins + (size_t)row * stride);
       rv0[u] = s4[0];
       rv1[u] = NV > 1 ? s4[1] : make_uint4(0u, 0u, 0u, 0u);
+      rv2[u] = NV > 2 ? s4[2] : make_uint4(0u, 0u, 0u, 0u);
+      rv3[u] = NV > 3 ? s4[3] : make_uint4(0u, 0u, 0u, 0u);
       ra[u] = saux[row];
       rx[u] = sridx ? sridx[row] : row;
     }
@@ -999,11 +1005,14 @@ __global__ __launch_bounds__(LW * 64) void k_route(
     const bool valid = row < r1;
     int dA = 0, dB = 0;
     if (valid && featA >= 0)
-      dA = dec_go_left(&sA, NV > 0 ? row_byte(rv0[u], rv1[u], featA) : sbins[(size_t)row * stride + featA]) ? 0 : 1;
+      dA = dec_go_left(&sA, NV > 2 ? row_byte4(rv0[u], rv1[u], rv2[u], rv3[u], featA)
+                                   : NV > 0 ? row_byte(rv0[u], rv1[u], featA) : sbins[(size_t)row * stride + featA]) ? 0 : 1;
     if (TWO && valid && sC[dA] >= 0) {
       const Dec* b = &sB[dA];
       const int fb = b->feat;
-      if (fb >= 0) dB = dec_go_left(b, NV > 0 ? row_byte(rv0[u], rv1[u], fb) : sbins[(size_t)row * stride + fb]) ? 0 : 1;
+      if (fb >= 0)
+        dB = dec_go_left(b, NV > 2 ? row_byte4(rv0[u], rv1[u], rv2[u], rv3[u], fb)
+                                   : NV > 0 ? row_byte(rv0[u], rv1[u], fb) : sbins[(size_t)row * stride + fb]) ? 0 : 1;
     }
     q[u] = 2 * dA + dB;
     mv[u] = MOVE && valid && sG[q[u]] >= 0;
@@ -1060,6 +1069,8 @@ __global__ __launch_bounds__(LW * 64) void k_route(
         uint4* d4 = (uint4*)dst;
         d4[0] = rv0[u];
         if (NV > 1) d4[1] = rv1[u];
+        if (NV > 2) d4[2] = rv2[u];
+        if (NV > 3) d4[3] = rv3[u];
       } else if ((stride & 15) == 0 && stride <= 64) {      // 16-B aligned rows: vector copy
         const uint4* s4 = (const uint4*)src;
         uint4* d4 = (uint4*)dst;
@@ -1366,7 +1377,9 @@ int h2o_route(const void* sbins, const void* saux, const void* sridx, void* dbin
   else if (two) hipLaunchKernelGGL((k_route<true, false, NV>), dim3(tiles_cap), dim3(LW * 64), 0, s, ROUTE_ARGS); \
   else if (!move) hipLaunchKernelGGL((k_route<false, false, NV>), dim3(tiles_cap), dim3(LW * 64), 0, s, ROUTE_ARGS); \
   else return (int)hipErrorInvalidValue;  /* moving after a single level is never needed */
-  if (stride == 32 && !route_generic()) { ROUTE_LAUNCH(2) }
+  if (stride == 64 && !route_generic()) { ROUTE_LAUNCH(4) }
+  else if (stride == 48 && !route_generic()) { ROUTE_LAUNCH(3) }
+  else if (stride == 32 && !route_generic()) { ROUTE_LAUNCH(2) }
   else if (stride == 16 && !route_generic()) { ROUTE_LAUNCH(1) }
   else { ROUTE_LAUNCH(0) }
 #undef ROUTE_LAUNCH

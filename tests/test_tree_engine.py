@@ -190,3 +190,27 @@ def test_gpu_native_leaf_values_match_torch(log_link, mx):
     assert ta.n_leaves == tb.n_leaves > 1
     np.testing.assert_allclose(ta.leaf_values, tb.leaf_values, rtol=1e-6, atol=1e-7)
     assert abs(ta.root_weight - X.shape[1]) < 1e-6 and ta.root_weight == tb.root_weight
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("F", [10, 20, 40, 50, 70])
+def test_gpu_tree_matches_reference_row_widths(F):
+    # every row stride class of k_route (16 / 32 / 48 / 64 B register paths and the generic byte path)
+    X, y, info = _data(N=30000, F=F, cat=True, seed=F)
+    g = torch.Generator().manual_seed(F)
+    X[F - 1] = X[0] * 0.5 + torch.randn(X.shape[1], generator=g)    # a useful feature in the last word
+    b = fit_binning(X, info.iscat, info.nlevels, max_bins=64)
+    bins = apply_binning(b, X)
+    aux = torch.stack([torch.ones_like(y), y - y.mean(), y - y.mean(), torch.ones_like(y)], 1).contiguous()
+    p = T.SplitParams(min_w=10)
+    ref = T.RefTreeBuilder(bins, F, b.nbins, b.iscat, None, 6, p)
+    ref.build(aux, leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1]).float())
+    tl_r = ref.pop_levels()[0]
+    dev = torch.device("cuda", 0)
+    gb = T.GpuTreeBuilder(bins.to(dev), F, b.nbins, b.iscat, None, 6, p)
+    gb.build(aux.to(dev), leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1]).float())
+    tl_g = gb.pop_levels()[0]
+    assert tl_g.n_leaves == tl_r.n_leaves
+    for dr, dg in zip(tl_r.decs, tl_g.decs):
+        assert np.array_equal(dr["feat"], dg["feat"]) and np.array_equal(dr["bin"], dg["bin"])
+    assert torch.equal(ref.leaf_of_row, gb.leaf_of_row.cpu())
