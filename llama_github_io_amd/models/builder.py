@@ -183,7 +183,10 @@ def train(algo: str, params: dict, x=None, y=None, training_frame=None, validati
     cv_out = None
     if nfolds > 1 or (info.fold and info.fold in fr.names):
         cv_out = _cross_validate(spec, p, fr, info, X, yv, w, off, seed, mid, job)
-    tr = spec.trainer({k: v for k, v in p.items() if k not in COMMON})
+    tp = {k: v for k, v in p.items() if k not in COMMON}
+    if cv_out is not None and float(tp.get("max_runtime_secs") or 0) > 0:
+        tp["max_runtime_secs"] = max(1e-3, float(tp["max_runtime_secs"]) - (time.time() - t0))
+    tr = spec.trainer(tp)
     tr.job = job
     if algo == "word2vec":
         tr.strings = fr._col(info.x[0]).to_numpy()
@@ -249,6 +252,9 @@ def _cross_validate(spec, p, fr, info, X, yv, w, off, seed, mid, job):
             continue
         sub = lambda t, m: None if t is None else (t[:, m] if t.dim() == 2 else t[m])  # noqa: E731
         ps = {kk: vv for kk, vv in p.items() if kk not in COMMON}
+        if float(ps.get("max_runtime_secs") or 0) > 0:
+            # the whole CV procedure (k fold models + the main model) shares the model's time budget
+            ps["max_runtime_secs"] = float(ps["max_runtime_secs"]) / (k + 1)
         trainer = spec.trainer(ps)
         trainer.job = job
         m = trainer.fit(sub(X, tr_m).contiguous(), sub(yv, tr_m), sub(w, tr_m), sub(off, tr_m), info, None,

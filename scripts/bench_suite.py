@@ -5,6 +5,8 @@
   --which dl    : DeepLearning MLP [200,200] on 10M x 784 synthetic, bf16 compute, 1 epoch
   --which glm   : GLM binomial on 10k x 20 synthetic CSV through h2o.init()/import_file (plumbing)
   --which kmeans: KMeans k=10 Lloyd iterations on 10M x 20
+  --which automl: AutoML (GBM/DRF/GLM/DL/XGBoost + StackedEnsembles) on 1M x 100 within --budget seconds,
+                  then the leader's MOJO export -> import_mojo -> prediction parity
 Rows/features can be reduced with --rows/--cols for quick runs (reported in the config).
 Multi-GPU: launch with torchrun; rows are sharded, statistics all-reduced over RCCL.
 """
@@ -82,6 +84,40 @@ def bench_dl(a, dev, world, rank):
                train_auc=m.output["training_metrics"]["AUC"], dtype="bf16", data="synthetic"))
 
 
+def bench_automl(a, dev, world, rank):
+    import tempfile
+    import h2o
+    import pandas as pd
+    from h2o.automl import H2OAutoML
+    h2o.init(verbose=False)
+    n, F = a.rows or 1_000_000, a.cols or 100
+    g = torch.Generator(device=dev).manual_seed(21)
+    X = torch.randn(n, F, device=dev, generator=g)
+    logit = X[:, 0] - 0.8 * X[:, 1] + 0.5 * X[:, 2] * X[:, 3] + 0.4 * torch.sin(3 * X[:, 4]) - 0.3 * (X[:, 5] > 1).float()
+    y = (torch.rand(n, device=dev, generator=g) < torch.sigmoid(logit)).long()
+    df = pd.DataFrame(X.cpu().numpy(), columns=[f"c{i}" for i in range(F)])
+    df["y"] = y.cpu().numpy().astype(str)
+    fr = h2o.H2OFrame(df, column_types={"y": "enum"})
+    _sync()
+    t0 = time.perf_counter()
+    aml = H2OAutoML(max_runtime_secs=a.budget, max_models=a.trees or None, seed=1, nfolds=3)
+    aml.train(y="y", training_frame=fr)
+    _sync()
+    dt = time.perf_counter() - t0
+    lb = aml.leaderboard.as_data_frame()
+    leader = aml.leader
+    path = leader.download_mojo(tempfile.mkdtemp())
+    gm = h2o.import_mojo(path)
+    sub = fr[:100000, :]
+    pa = leader.predict(sub).as_data_frame().iloc[:, -1].values
+    pb = gm.predict(sub).as_data_frame().iloc[:, -1].values
+    _emit(dict(metric="AutoML on 1M x 100: models trained within budget + leader MOJO round trip",
+               value=len(lb), unit="models", n_gpus=world, seconds=dt, budget_secs=a.budget, rows=n, cols=F,
+               leader=str(lb.iloc[0, 0]), leader_auc=float(lb.iloc[0, 1]),
+               mojo_max_abs_diff=float(np.max(np.abs(pa - pb))), algos=sorted({str(m).split("_")[0] for m in lb.iloc[:, 0]}),
+               data="synthetic"))
+
+
 def bench_glm(a, dev, world, rank):
     import tempfile
     import h2o
@@ -124,7 +160,8 @@ def bench_kmeans(a, dev, world, rank):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--which", default="xgb", choices=["xgb", "dl", "glm", "kmeans"])
+    ap.add_argument("--which", default="xgb", choices=["xgb", "dl", "glm", "kmeans", "automl"])
+    ap.add_argument("--budget", type=float, default=240.0, help="AutoML max_runtime_secs")
     ap.add_argument("--rows", type=int, default=0)
     ap.add_argument("--cols", type=int, default=0)
     ap.add_argument("--trees", type=int, default=0)
@@ -139,7 +176,7 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
-    dict(xgb=bench_xgb, dl=bench_dl, glm=bench_glm, kmeans=bench_kmeans)[a.which](a, dev, world, rank)
+    dict(xgb=bench_xgb, dl=bench_dl, glm=bench_glm, kmeans=bench_kmeans, automl=bench_automl)[a.which](a, dev, world, rank)
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
