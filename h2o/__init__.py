@@ -312,3 +312,11 @@ def set_s3_credentials(*a, **k):
 from . import grid, automl  # noqa: E402,F401
 from .grid import H2OGridSearch  # noqa: E402,F401
 from .automl import H2OAutoML, get_leaderboard  # noqa: E402,F401
+
+from ._more import (api, cluster_info, connection, demo, download_all_logs, download_csv,  # noqa: E402,F401
+                    enable_expr_optimizations, estimate_cluster_mem, frame, get_timezone, import_hive_table,
+                    import_sql_select, import_sql_table, is_expr_optimizations_enabled, lazy_import, list_timezones,
+                    load_dataset, load_grid, log_and_echo, models, network_test, parse, rapids, save_grid,
+                    set_timezone, version_check)
+
+import_frame = import_file

@@ -104,7 +104,7 @@ class AutoML:
                 if not (self._allowed("gbm") or self._allowed("xgboost")):
                     break
                 algo = "gbm" if (i % 2 == 0 and self._allowed("gbm")) or not self._allowed("xgboost") else "xgboost"
-                name = f"{algo.upper()}_grid_1_model_{i - len(steps) + 1}"
+                name = f"{dict(gbm='GBM', xgboost='XGBoost')[algo]}_grid_1_model_{i - len(steps) + 1}"
                 p = _random_grid(algo, rng, self.seed)
                 if i > len(steps) + 200:
                     break

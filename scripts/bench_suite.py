@@ -101,7 +101,17 @@ def bench_automl(a, dev, world, rank):
     _sync()
     t0 = time.perf_counter()
     aml = H2OAutoML(max_runtime_secs=a.budget, max_models=a.trees or None, seed=1, nfolds=3)
-    aml.train(y="y", training_frame=fr)
+    import threading
+    stop = threading.Event()
+
+    def beat():   # progress line every 30 s (long AutoML runs must not look silent)
+        while not stop.wait(30):
+            print(f"[automl] {time.perf_counter() - t0:.0f}s", file=sys.stderr, flush=True)
+    threading.Thread(target=beat, daemon=True).start()
+    try:
+        aml.train(y="y", training_frame=fr)
+    finally:
+        stop.set()
     _sync()
     dt = time.perf_counter() - t0
     lb = aml.leaderboard.as_data_frame()
