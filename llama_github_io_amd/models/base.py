@@ -141,8 +141,31 @@ class Model:
         from ..frame import H2OFrame
         X, offset = frame.model_matrix(self.info, device=self.device)
         P = self.score_tensor(X, offset)
-        return H2OFrame.from_predictions(P, self.model_category, self.info.response_domain,
-                                         threshold=self.default_threshold(), names=self.prediction_names())
+        out = H2OFrame.from_predictions(P, self.model_category, self.info.response_domain,
+                                        threshold=self.default_threshold(), names=self.prediction_names())
+        cm = getattr(self, "calibration_model", None)
+        if cm is not None and P.dim() == 2 and P.shape[1] == 2:
+            out = out.cbind(self._calibrated(P))
+        return out
+
+    # ---- calibration (CalibrationHelper.OutputWithCalibration)
+    def set_calibration_model(self, calibration_model):
+        if self.model_category != "Binomial":
+            raise ValueError(f"Models of type {self.algo} don't support calibration.")
+        self.calibration_model = calibration_model
+        self.output["calibration_model"] = getattr(calibration_model, "key", None)
+        return "OK"
+
+    def _calibrated(self, P):
+        from ..frame import Column, H2OFrame
+        cm = self.calibration_model
+        if cm.algo == "isotonicregression":
+            c1 = cm.score_tensor(P[:, 1:2].T.float().contiguous()).double().reshape(-1)
+            c0 = 1 - c1
+        else:
+            C = cm.score_tensor(P[:, 0:1].T.float().contiguous()).double()
+            c0, c1 = C[:, 0], C[:, 1]
+        return H2OFrame._from_columns([Column("cal_p0", "real", c0.contiguous()), Column("cal_p1", "real", c1.contiguous())])
 
     def prediction_names(self):
         """Column names of a multi-column non-classification prediction frame (None = defaults)."""
@@ -204,6 +227,12 @@ class Model:
         from .. import explain
         return explain.feature_interaction(self, max_interaction_depth, max_tree_depth, max_deepening)
 
+    def fairness_metrics(self, frame, protected_columns, reference=None, favorable_class=None):
+        """Per protected-group metrics + adverse impact ratios (h2o-py ``model.fairness_metrics``)."""
+        from ..rapids_more import fairness_metrics
+        fav = favorable_class if favorable_class is not None else self.info.response_domain[-1]
+        return fairness_metrics(self, frame, protected_columns, reference, fav)
+
     def explain(self, frame, **kw):
         from .. import explain
         return explain.explain(self, frame, **kw)
@@ -223,11 +252,20 @@ class Model:
 
     # ---- persistence
     def to_state(self) -> dict:
-        return dict(algo=self.algo, key=self.key, params=_jsonable(self.params), info=self.info.to_state(),
-                    output=_jsonable(self.output))
+        st = dict(algo=self.algo, key=self.key, params=_jsonable(self.params), info=self.info.to_state(),
+                  output=_jsonable(self.output))
+        cm = getattr(self, "calibration_model", None)
+        if cm is not None:
+            cs = cm.to_state()
+            cs["__class__"] = type(cm).__module__ + ":" + type(cm).__name__
+            st["calibration"] = cs
+        return st
 
     def _restore(self, state):
         self.output = state["output"]
+        if state.get("calibration"):
+            from ..persist import _from_state
+            self.calibration_model = _from_state(dict(state["calibration"]))
 
     def __repr__(self):
         return f"<{type(self).__name__} key={self.key} category={self.model_category}>"

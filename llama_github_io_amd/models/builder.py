@@ -43,7 +43,7 @@ def register(name, trainer, supervised=True, defaults=None, **kw):
 COMMON = ("nfolds", "fold_assignment", "fold_column", "keep_cross_validation_predictions", "keep_cross_validation_models",
           "keep_cross_validation_fold_assignment", "weights_column", "offset_column", "ignored_columns",
           "ignore_const_cols", "model_id", "training_frame", "validation_frame", "response_column", "x", "y",
-          "custom_metric_func")
+          "custom_metric_func", "calibrate_model", "calibration_frame", "calibration_method")
 
 
 def _resolve_names(fr, cols):
@@ -191,7 +191,8 @@ def train(algo: str, params: dict, x=None, y=None, training_frame=None, validati
     if algo == "word2vec":
         tr.strings = fr._col(info.x[0]).to_numpy()
     model = tr.fit(X, yv, w, off, info, valid, mid) if yv is not None or not spec.supervised else tr.fit(X, yv, w, off, info, valid, mid)
-    model.params.update({k: p.get(k) for k in COMMON if k in p and k not in ("training_frame", "validation_frame", "x", "y")})
+    model.params.update({k: p.get(k) for k in COMMON if k in p and k not in ("training_frame", "validation_frame", "x", "y",
+                                                                              "calibration_frame")})
     model.output["names"] = info.x + ([info.response] if info.response else [])
     model.output["response_column_name"] = info.response
     model.output["domains"] = info.domains
@@ -205,13 +206,49 @@ def train(algo: str, params: dict, x=None, y=None, training_frame=None, validati
         _custom_metric(model, p["custom_metric_func"], X, yv, w, off, "training_metrics")
         if valid is not None:
             _custom_metric(model, p["custom_metric_func"], *valid, "validation_metrics")
-    model.output["run_time_ms"] = int((time.time() - t0) * 1000)
     model.algo = algo
+    if p.get("calibrate_model") or p.get("calibration_frame") is not None:
+        _calibrate(model, p, job)
+    model.output["run_time_ms"] = int((time.time() - t0) * 1000)
     dkv.put(model.key, model)
     if p.get("export_checkpoints_dir"):          # ModelBuilder export_checkpoints_dir: persist every final model
         from ..persist import save_model
         save_model(model, p["export_checkpoints_dir"], force=True)
     return model
+
+
+def _calibrate(model, p, job):
+    """Post-hoc probability calibration (``hex/tree/CalibrationHelper.java``): Platt scaling = a binomial GLM
+    (lambda 0) on p0 of the calibration frame, isotonic regression = a monotone fit of the response on p1.
+    Predictions then carry ``cal_p0`` / ``cal_p1``."""
+    from ..frame import Column, H2OFrame
+    cf = p.get("calibration_frame")
+    if isinstance(cf, str):
+        cf = dkv.get(cf)
+    if not p.get("calibrate_model"):
+        return                                   # the reference warns: frame given, calibration not requested
+    if model.model_category != "Binomial":
+        raise ValueError("Model calibration is only currently supported for binomial models.")
+    if cf is None:
+        raise ValueError("Calibration frame was not specified.")
+    method = str(p.get("calibration_method") or "AUTO").lower().replace("_", "")
+    iso = method in ("isotonicregression", "isotonic")
+    X, off = cf.model_matrix(model.info, device=model.device)
+    P = model.score_tensor(X, off).double()
+    y = cf.response_tensor(model.info, device=P.device).double()
+    cols = [Column("p", "real", (P[:, 1] if iso else P[:, 0]).contiguous()),
+            Column("response", "real", y) if iso else
+            Column("response", "enum", y.nan_to_num(-1).int(), domain=list(model.info.response_domain))]
+    wname = model.info.weights
+    if wname:
+        cols.append(Column("weights", "real", cf._col(wname).as_float().double()))
+    calib_in = H2OFrame._from_columns(cols)
+    cp = dict(weights_column="weights") if wname else {}
+    if iso:
+        cm = train("isotonicregression", dict(cp, out_of_bounds="clip"), ["p"], "response", calib_in, None, job)
+    else:
+        cm = train("glm", dict(cp, family="binomial", lambda_=0.0), ["p"], "response", calib_in, None, job)
+    model.set_calibration_model(cm)
 
 
 def _custom_metric(model, ref, X, y, w, off, which):

@@ -59,6 +59,11 @@ class GenericModel(Model):
                         fr.add(bytes_to_tree(mj["trees"][name], vmap), c)
             m.forest = fr
             m.ntrees = n
+            if ki.get("calib_method") == "platt":
+                m.calibration_model = ("platt", _floats(ki["calib_glm_beta"]))
+            elif ki.get("calib_method") == "isotonic":
+                tx, ty = A.load_isotonic(mj["files"])
+                m.calibration_model = ("isotonic", float(ki["calib_min_x"]), float(ki["calib_max_x"]), tx, ty)
         elif algo == "glm":
             m.beta = torch.tensor(_floats(ki["beta"]), dtype=torch.float64)
             m.cat_offsets = [int(v) for v in _floats(ki["cat_offsets"])]
@@ -106,6 +111,20 @@ class GenericModel(Model):
         else:
             raise NotImplementedError(f"MOJO algo {algo} not supported by this reader")
         return m
+
+    def _calibrated(self, P):
+        """CalibrationMojoHelper.calibrateClassProbabilities: Platt p = logistic(p0 * b0 + b1), isotonic
+        p = interp(clip(p1)); cal_p0 = 1 - p."""
+        from ..frame import Column, H2OFrame
+        cm = self.calibration_model
+        if cm[0] == "platt":
+            b = cm[1]
+            c1 = torch.sigmoid(P[:, 0].double() * b[0] + b[1])
+        else:
+            _, lo, hi, tx, ty = cm
+            x = P[:, 1].double().clamp(lo, hi).cpu().numpy()
+            c1 = torch.as_tensor(np.interp(x, tx, ty), dtype=torch.float64, device=P.device)
+        return H2OFrame._from_columns([Column("cal_p0", "real", (1 - c1).contiguous()), Column("cal_p1", "real", c1)])
 
     def __getattr__(self, name):
         # Word2Vec / isotonic MOJOs delegate their model-specific API (find_synonyms, transform, ...)

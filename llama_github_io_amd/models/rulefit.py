@@ -88,6 +88,24 @@ class RuleFitModel(Model):
     def rule_importance(self):
         return self.output["rule_importance"]
 
+    def predict_rules(self, frame, rule_ids):
+        """0/1 column per requested rule: does the row satisfy the rule's conditions (RuleFitModel.predictRules)."""
+        from ..frame import Column, H2OFrame
+        X, _ = frame.model_matrix(self.info, device=self.device)
+        where = {}
+        for ti, nodes in self.rule_nodes:
+            for n in nodes:
+                where[f"M{ti}T{ti}N{n}"] = (ti, n)
+        cols, cache = [], {}
+        for rid in rule_ids:
+            if rid not in where:
+                raise ValueError(f"Rule {rid!r} is not part of the model")
+            ti, n = where[rid]
+            if ti not in cache:
+                cache[ti] = _node_masks(self.trees[ti], X)[0]
+            cols.append(Column(rid, "int", cache[ti][n].double()))
+        return H2OFrame._from_columns(cols)
+
 
 class RuleFitTrainer:
     def __init__(self, params):

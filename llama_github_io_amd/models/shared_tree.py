@@ -61,6 +61,31 @@ class SharedTreeModel(Model):
         _, leaves = self.forest.predict_raw(X.to(self.device), return_leaves=True)
         return leaves
 
+    def update_tree_weights(self, frame, weights_column):
+        """Recompute every node's weight (``cover``, used by TreeSHAP and the tree API) from the rows of
+        ``frame`` weighted by ``weights_column`` (Model.UpdateAuxTreeWeights)."""
+        X, _ = frame.model_matrix(self.info, device=self.device)
+        w = frame._col(weights_column).as_float().double().to(self.device)
+        _, leaves = self.forest.predict_raw(X, return_leaves=True)
+        warn = None
+        base = 0
+        for t, tree in enumerate(self.forest.trees):
+            lv = leaves[:, t].long() - base          # flattened node ids -> this tree's ids
+            base += tree.n_nodes
+            cover = torch.zeros(tree.n_nodes, dtype=torch.float64, device=self.device).index_add_(0, lv, w)
+            cover = cover.cpu().numpy()
+            for i in range(tree.n_nodes - 1, -1, -1):     # children are appended after their parent
+                if tree.feat[i] >= 0:
+                    cover[i] = cover[tree.left[i]] + cover[tree.right[i]]
+            if warn is None and (cover == 0).any():
+                warn = (t, self.forest.tree_class[t])
+            tree.cover = cover.astype(tree.cover.dtype if hasattr(tree.cover, "dtype") else np.float64)
+        self.forest._flat = {}
+        if warn is not None:
+            return (f"Some of the updated nodes have zero weights (eg.: tree #{warn[0] + 1}, "
+                    f"class #{warn[1] + 1}).")
+        return "OK"
+
     def to_state(self):
         s = super().to_state()
         s["forest"] = dict(trees=[t.to_state() for t in self.forest.trees], tree_class=self.forest.tree_class,

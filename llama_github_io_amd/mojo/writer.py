@@ -169,6 +169,16 @@ def _trees(model, kv, blobs):
     for idx, (t, c) in enumerate(zip(fr.trees, fr.tree_class)):
         it = idx // max(K, 1)
         blobs[f"trees/t{c:02d}_{it:03d}.bin"] = tree_to_bytes(t, vmap)
+    cm = getattr(model, "calibration_model", None)
+    if cm is not None:                        # SharedTreeMojoWriter: calib_method + GLM beta / isotonic calibrator
+        if cm.algo == "isotonicregression":
+            from .algos import write_isotonic
+            kv["calib_method"] = "isotonic"
+            write_isotonic(cm, kv, blobs)
+        else:
+            co = cm.output["coefficients"]
+            kv["calib_method"] = "platt"
+            kv["calib_glm_beta"] = _arr([co["p"], co["Intercept"]])
 
 
 def _glm(model, kv):

@@ -17,7 +17,7 @@ import torch
 from .core import dkv
 from .frame import Column, H2OFrame, engine_device
 
-_TOKEN = re.compile(r'\s*(\(|\)|\[|\]|"(?:[^"\\]|\\.)*"|\'(?:[^\'\\]|\\.)*\'|[^\s()\[\]]+)')
+_TOKEN = re.compile(r'\s*(\(|\)|\[|\]|\{|\}|"(?:[^"\\]|\\.)*"|\'(?:[^\'\\]|\\.)*\'|[^\s()\[\]{}]+)')
 
 
 def tokenize(s: str):
@@ -50,6 +50,16 @@ def parse(tokens, i=0):
             node, i = parse(tokens, i)
             lst.append(node)
         return ("list", lst), i + 1
+    if t == "{":                       # lambda: { arg1 arg2 . body }
+        params = []
+        i += 1
+        while tokens[i] != ".":
+            params.append(tokens[i])
+            i += 1
+        body, i = parse(tokens, i + 1)
+        if tokens[i] != "}":
+            raise SyntaxError("lambda body must be one expression followed by '}'")
+        return ("fun", (params, body)), i + 1
     if t[0] in "\"'":
         return ("str", bytes(t[1:-1], "utf-8").decode("unicode_escape")), i + 1
     if t in ("TRUE", "FALSE"):
@@ -214,6 +224,9 @@ class Session:
             "comma": lambda *a: a[-1], ",": lambda *a: a[-1],
         }
         self.prims.update(_extended_prims(self))
+        from .rapids_more import more_prims
+        self.prims.update(more_prims(self))
+        self.scopes = []
 
     # ---- special forms
     def _assign(self, name, value):
@@ -272,8 +285,14 @@ class Session:
                 out += r if isinstance(r, list) and x[0] == "span" else [r]
             return out
         if kind == "id":
+            for sc in reversed(self.scopes):
+                if v in sc:
+                    return sc[v]
             val = dkv.get(v)
             return val if val is not None else v
+        if kind == "fun":
+            from .rapids_more import RapidsFunction
+            return RapidsFunction(self, *v)
         op = v[0]
         if op[0] != "id":
             raise SyntaxError("call head must be an operator")
@@ -556,6 +575,11 @@ def _mktime(yr, mo, dy, hr, mi, se, ms):
     return H2OFrame._from_columns([Column("C1", "time", torch.as_tensor(ms_, device=engine_device()))])
 
 
+def _as_fn(sess, f):
+    from .rapids_more import as_function
+    return as_function(sess, f)
+
+
 def _extended_prims(sess):
     fr = _frame
     pi = math.pi
@@ -607,7 +631,7 @@ def _extended_prims(sess):
         "setLevel": lambda a, lvl: _set_level(fr(a), lvl),
         "appendLevels": lambda a, lv, inplace=0: _append_levels(fr(a), lv, inplace),
         "filterNACols": lambda a, frac: _filter_na_cols(fr(a), frac),
-        "apply": lambda a, margin, f: fr(a).apply(f, int(margin) - 1),
+        "apply": lambda a, margin, f: fr(a).apply(_as_fn(sess, f), 0 if int(margin) == 2 else 1),  # R margins
         "t": lambda a: fr(a).transpose(), "topn": lambda a, col, pct, top=1: fr(a).topN(int(col), float(pct), int(top)),
         "hist": lambda a, breaks="sturges": fr(a).hist(breaks if isinstance(breaks, str) else list(breaks)),
         "kfold_column": lambda a, k, seed=-1: fr(a).kfold_column(int(k), int(seed)),
