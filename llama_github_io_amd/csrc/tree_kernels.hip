@@ -165,8 +165,15 @@ __device__ __forceinline__ void unpack(long long v, long long& cnt, long long& v
 // MEASURED: the former fp64 atomicAdd flush into one shared slot cost ~30 us per level regardless of
 // row count (256 blocks x 14K same-address atomics serialise in L2) — the fixed cost that dominated
 // small shards (1.375M rows/GPU at 8 GPUs).
+// f32: the slot holds floats (same slot stride): half the flush / reduce bytes; k_hist_reduce still sums in fp64
+// in a fixed order. Exact per-block counts (< 2^24 rows per block) and ~6e-8 relative wY per partial.
+template <typename P>
+__device__ __forceinline__ void put_partial(P* q, double d, bool acc) {
+  *q = acc ? (P)((double)*q + d) : (P)d;
+}
 __device__ void flush_partial(const long long* h, const float* nayy, double node_wyy, int ftile, int F,
-                              double* __restrict__ part, const double* __restrict__ qs, bool packed, bool acc) {
+                              double* __restrict__ part, const double* __restrict__ qs, bool packed, bool acc,
+                              bool f32) {
   const int f0 = ftile * FTILE;
   const int nf = min(FTILE, F - f0);
   const double inv_a = qs[2], inv_b = qs[3], inv_p = qs[5];
@@ -181,16 +188,19 @@ __device__ void flush_partial(const long long* h, const float* nayy, double node
     } else {
       d = (double)h[r * HPLANE + e] * (r ? inv_b : inv_a);
     }
-    double* q = part + (size_t)bin * 2 * F + 2 * (f0 + fl) + r;
-    *q = acc ? *q + d : d;
+    const size_t e2 = (size_t)bin * 2 * F + 2 * (f0 + fl) + r;
+    if (f32) put_partial((float*)part + e2, d, acc);
+    else put_partial(part + e2, d, acc);
   }
   for (int i = threadIdx.x; i < nf; i += blockDim.x) {
-    double* q = part + (size_t)F * 2 * NBIN + f0 + i;
-    *q = acc ? *q + (double)nayy[i] : (double)nayy[i];
+    const size_t e2 = (size_t)F * 2 * NBIN + f0 + i;
+    if (f32) put_partial((float*)part + e2, (double)nayy[i], acc);
+    else put_partial(part + e2, (double)nayy[i], acc);
   }
   if (threadIdx.x == 0 && ftile == 0) {
-    double* q = part + (size_t)F * 2 * NBIN + F;
-    *q = acc ? *q + node_wyy : node_wyy;
+    const size_t e2 = (size_t)F * 2 * NBIN + F;
+    if (f32) put_partial((float*)part + e2, node_wyy, acc);
+    else put_partial(part + e2, node_wyy, acc);
   }
 }
 
@@ -313,7 +323,7 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
     const float4* __restrict__ aux, const Node* __restrict__ nodes, const int* __restrict__ tile_prefix,
     const int* __restrict__ meta /*[0]=n_nodes [2]=n_build_tiles*/, int F, double* __restrict__ partials,
     int slot_doubles, const double* __restrict__ qs /*[sa, sb, 1/sa, 1/sb, sp, 1/sp]*/,
-    const Dec* __restrict__ pdec, int* __restrict__ nl_out) {
+    const Dec* __restrict__ pdec, int* __restrict__ nl_out, int f32) {
   constexpr bool packed = PACKED;
   extern __shared__ __attribute__((aligned(16))) long long smem64[];
   long long* h = smem64;                                 // 2 planes (PACKED: 1 -> two blocks per CU fit)
@@ -344,7 +354,9 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
     double v[4] = {wyy, (double)lcnt, 0, 0};
     block_sum4(v, red);
     __syncthreads();
-    flush_partial(h, nayy, v[0], ftile, F, partials + (size_t)(blockIdx.x + cur) * slot_doubles, qs, packed, acc);
+    const size_t so = (size_t)(blockIdx.x + cur) * slot_doubles;
+    flush_partial(h, nayy, v[0], ftile, F, f32 ? (double*)((float*)partials + so) : partials + so, qs, packed, acc,
+                  f32 != 0);
     if (FILT && threadIdx.x == 0 && v[1] != 0.0) atomicAdd(nl_out + cur_parent, (int)v[1]);
     __syncthreads();
   };
@@ -392,8 +404,9 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
 // its partials sit at b + n. With hist_next != nullptr (single process) the sibling subtraction is fused:
 // hist_next[n] = sum and hist_next[sib] = hist_cur[parent] - sum (no compact-buffer round trip).
 #define RW 8   // waves per k_hist_reduce block: wave w sums partials b0 + w, b0 + w + RW, ... of 64 columns
+template <typename P>
 __global__ __launch_bounds__(RW * 64) void k_hist_reduce(
-    const double* __restrict__ partials, int slot_doubles, int used, const Node* __restrict__ nodes,
+    const P* __restrict__ partials, int slot_doubles, int used, const Node* __restrict__ nodes,
     const int* __restrict__ bp, const int* __restrict__ meta, int G, double* __restrict__ out,
     double* __restrict__ hist_next, const double* __restrict__ hist_cur) {
   const int node = blockIdx.y;
@@ -413,12 +426,12 @@ __global__ __launch_bounds__(RW * 64) void k_hist_reduce(
   double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
   int b = b0 + w;
   for (; b + 3 * RW <= b1; b += 4 * RW) {
-    a0 += partials[(size_t)(b + node) * slot_doubles + ic];
-    a1 += partials[(size_t)(b + RW + node) * slot_doubles + ic];
-    a2 += partials[(size_t)(b + 2 * RW + node) * slot_doubles + ic];
-    a3 += partials[(size_t)(b + 3 * RW + node) * slot_doubles + ic];
+    a0 += (double)partials[(size_t)(b + node) * slot_doubles + ic];
+    a1 += (double)partials[(size_t)(b + RW + node) * slot_doubles + ic];
+    a2 += (double)partials[(size_t)(b + 2 * RW + node) * slot_doubles + ic];
+    a3 += (double)partials[(size_t)(b + 3 * RW + node) * slot_doubles + ic];
   }
-  for (; b <= b1; b += RW) a0 += partials[(size_t)(b + node) * slot_doubles + ic];
+  for (; b <= b1; b += RW) a0 += (double)partials[(size_t)(b + node) * slot_doubles + ic];
   red[w][lane] = (a0 + a1) + (a2 + a3);
   __syncthreads();
   if (w != 0 || i >= used) return;
@@ -1252,15 +1265,15 @@ __global__ void k_leaf_values(const double* __restrict__ leafsum, int n, int log
 template <bool PACKED>
 static void launch_hist(dim3 grid, size_t lds, hipStream_t s, const void* bins, int stride, const void* aux,
                         const void* nodes, const void* tile_prefix, const void* meta, int F, void* partials,
-                        int slot_doubles, const void* qs, const void* pdec, void* nl_out) {
+                        int slot_doubles, const void* qs, const void* pdec, void* nl_out, int f32) {
   if (pdec)
     hipLaunchKernelGGL((k_hist_build<true, PACKED>), grid, dim3(BLK), lds, s, (const uint8_t*)bins, stride,
                        (const float4*)aux, (const Node*)nodes, (const int*)tile_prefix, (const int*)meta, F,
-                       (double*)partials, slot_doubles, (const double*)qs, (const Dec*)pdec, (int*)nl_out);
+                       (double*)partials, slot_doubles, (const double*)qs, (const Dec*)pdec, (int*)nl_out, f32);
   else
     hipLaunchKernelGGL((k_hist_build<false, PACKED>), grid, dim3(BLK), lds, s, (const uint8_t*)bins, stride,
                        (const float4*)aux, (const Node*)nodes, (const int*)tile_prefix, (const int*)meta, F,
-                       (double*)partials, slot_doubles, (const double*)qs, (const Dec*)nullptr, (int*)nullptr);
+                       (double*)partials, slot_doubles, (const double*)qs, (const Dec*)nullptr, (int*)nullptr, f32);
 }
 
 extern "C" {
@@ -1276,24 +1289,29 @@ int h2o_tree_sizes(int* out) {
 // partials: >= (grid + max nodes of the level) slots of slot_doubles
 int h2o_hist_build(const void* bins, int stride, const void* aux, const void* nodes, const void* tile_prefix,
                    const void* meta, int F, void* partials, int slot_doubles, const void* qs, int grid, int packed,
-                   const void* pdec, void* nl_out, hipStream_t s) {
+                   const void* pdec, void* nl_out, int f32, hipStream_t s) {
   const int nft = (F + FTILE - 1) / FTILE;
   // packed mode needs one int64 plane (66 KB): two 16-wave blocks share a CU (32 waves, 8 per SIMD)
   const size_t lds = (packed ? HIST_LDS_BYTES - HPLANE * 8 : HIST_LDS_BYTES) + 64 * 8;
   const dim3 gr(grid, nft);
-  if (packed) launch_hist<true>(gr, lds, s, bins, stride, aux, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out);
-  else launch_hist<false>(gr, lds, s, bins, stride, aux, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out);
+  if (packed) launch_hist<true>(gr, lds, s, bins, stride, aux, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out, f32);
+  else launch_hist<false>(gr, lds, s, bins, stride, aux, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out, f32);
   return (int)hipGetLastError();
 }
 
 // grid: the G the matching h2o_hist_build ran with; out / hist_next may be null (see k_hist_reduce)
 int h2o_hist_reduce(const void* partials, int slot_doubles, int used, const void* nodes, const void* bp,
                     const void* meta, int cap, int grid, void* out, void* hist_next, const void* hist_cur,
-                    hipStream_t s) {
+                    int f32, hipStream_t s) {
   const int gx = (used + 63) / 64;
-  hipLaunchKernelGGL(k_hist_reduce, dim3(gx, cap), dim3(RW * 64), 0, s, (const double*)partials, slot_doubles, used,
-                     (const Node*)nodes, (const int*)bp, (const int*)meta, grid, (double*)out, (double*)hist_next,
-                     (const double*)hist_cur);
+  if (f32)
+    hipLaunchKernelGGL(k_hist_reduce<float>, dim3(gx, cap), dim3(RW * 64), 0, s, (const float*)partials, slot_doubles,
+                       used, (const Node*)nodes, (const int*)bp, (const int*)meta, grid, (double*)out,
+                       (double*)hist_next, (const double*)hist_cur);
+  else
+    hipLaunchKernelGGL(k_hist_reduce<double>, dim3(gx, cap), dim3(RW * 64), 0, s, (const double*)partials,
+                       slot_doubles, used, (const Node*)nodes, (const int*)bp, (const int*)meta, grid, (double*)out,
+                       (double*)hist_next, (const double*)hist_cur);
   return (int)hipGetLastError();
 }
 

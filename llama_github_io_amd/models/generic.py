@@ -64,6 +64,11 @@ class GenericModel(Model):
             elif ki.get("calib_method") == "isotonic":
                 tx, ty = A.load_isotonic(mj["files"])
                 m.calibration_model = ("isotonic", float(ki["calib_min_x"]), float(ki["calib_max_x"]), tx, ty)
+        elif algo == "xgboost":
+            from ..mojo import xgboost_mojo as XG
+            obj, base, ncls, trees, tinfo = XG.read(mj["files"]["boosterBytes"])
+            m.forest = Forest(trees, tinfo, max(ncls, 1))
+            m.xgb_obj, m.xgb_base = obj, base
         elif algo == "glm":
             m.beta = torch.tensor(_floats(ki["beta"]), dtype=torch.float64)
             m.cat_offsets = [int(v) for v in _floats(ki["cat_offsets"])]
@@ -203,6 +208,19 @@ class GenericModel(Model):
                 p1 = torch.sigmoid(f[:, 0])
                 return torch.stack([1 - p1, p1], 1)
             if ki.get("link_function") == "log":
+                return torch.exp(f[:, 0])
+            return f[:, 0]
+        if algo == "xgboost":
+            f = self.forest.predict_raw(X) + self.xgb_base
+            if offset is not None:
+                f = f + offset[:, None]
+            obj = self.xgb_obj
+            if obj == "binary:logistic":
+                p1 = torch.sigmoid(f[:, 0])
+                return torch.stack([1 - p1, p1], 1)
+            if obj.startswith("multi:"):
+                return torch.softmax(f, 1)
+            if obj in ("count:poisson", "reg:gamma", "reg:tweedie"):
                 return torch.exp(f[:, 0])
             return f[:, 0]
         if algo == "drf":

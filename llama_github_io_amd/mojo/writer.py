@@ -45,6 +45,7 @@ def _category(m):
 def _mojo_files(model, prefix: str = "") -> dict:
     """All entries of one model's MOJO (``model.ini``, domains, blobs), names under ``prefix``."""
     from . import algos as A
+    from . import xgboost_mojo as XG
     info = model.info
     algo = model.algo
     cols = list(info.x) + ([info.response] if info.response else [])
@@ -92,6 +93,8 @@ def _mojo_files(model, prefix: str = "") -> dict:
         _stacked(model, kv, blobs)
     elif algo == "extendedisolationforest":
         A.write_eif(model, kv, blobs)
+    elif algo == "xgboost" and XG.supported(model):
+        XG.write(model, kv, blobs)
     else:
         _generic_state(model, kv, blobs)
     buf = io.StringIO()

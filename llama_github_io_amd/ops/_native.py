@@ -23,7 +23,7 @@ c_int, c_ll, c_ull, c_double, c_void_p = ctypes.c_int, ctypes.c_longlong, ctypes
 _HIP_SIGS = {
     "h2o_tree_sizes": [c_void_p],
     "h2o_hist_build": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int,
-                       c_int, c_void_p, c_void_p, c_void_p],
+                       c_int, c_void_p, c_void_p, c_int, c_void_p],
     "h2o_split_find": [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_double, c_double,
                        c_double, c_double, c_double, c_int, c_int, c_ull, c_int, c_void_p, c_void_p, c_void_p],
     "h2o_split_reduce": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_ull, c_int, c_void_p, c_void_p],
@@ -36,7 +36,7 @@ _HIP_SIGS = {
     "h2o_amax": [c_void_p, c_ll, c_void_p, c_void_p],
     "h2o_qscale": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p],
     "h2o_hist_reduce": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
-                        c_void_p, c_void_p],
+                        c_void_p, c_int, c_void_p],
     "h2o_leaf_values": [c_void_p, c_int, c_int, c_double, c_double, c_double, c_void_p, c_void_p],
     "h2o_gbm_step": [c_ll, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_float, c_ull,
                      ctypes.c_float, c_void_p, c_void_p, c_void_p],

@@ -374,7 +374,10 @@ class GpuTreeBuilder:
         self.F = F
         self.D = D = max(1, int(max_depth))
         self.p = params
-        self.grid = grid
+        self.grid = int(os.environ.get("H2O_HIST_GRID", grid))
+        grid = self.grid
+        # fp32 per-block partial histograms (half the flush + reduce bytes; the reduce sums in fp64)
+        self.pf32 = int(os.environ.get("H2O_PARTIAL_F32", "0"))
         self.master = bins
         N, T = self.N, self.TILE
         self.caps = [min(1 << d, node_cap) for d in range(D)] + [1]
@@ -469,10 +472,10 @@ class GpuTreeBuilder:
         hgrid = self.grid * (self.hist_bpc if pk else 1)
         g0 = min(self.tiles_cap[0], hgrid)
         nat.check(lib.h2o_hist_build(self.master.data_ptr(), self.stride, aux_static.data_ptr(), self._p("nodes0"),
-                                     self._p("bp0"), self._p("meta0"), F, part, slot, qs, g0, pk, 0, 0, s),
+                                     self._p("bp0"), self._p("meta0"), F, part, slot, qs, g0, pk, 0, 0, self.pf32, s),
                   "hist_build")
         nat.check(lib.h2o_hist_reduce(part, slot, used, self._p("nodes0"), self._p("bp0"), self._p("meta0"), 1, g0,
-                                      self.hist[0].data_ptr(), 0, 0, s), "hist_reduce")
+                                      self.hist[0].data_ptr(), 0, 0, self.pf32, s), "hist_reduce")
         coll.all_reduce_(self.hist[0][:slot])
         mono = 0 if self.mono_f is None else self.mono_f.data_ptr()
         seed = int(seed) & _M64
@@ -523,7 +526,7 @@ class GpuTreeBuilder:
                 sb, sa, _ = level_buf(d)
                 nat.check(lib.h2o_hist_build(sb, self.stride, sa, self._p(f"nodes{d + 1}"), self._p(f"bp{d + 1}"),
                                              self._p(f"meta{d + 1}"), F, part, slot, qs, gh, pk,
-                                             self._p(f"dec{d}"), self._p(f"nl{d}"), s), "hist_build")
+                                             self._p(f"dec{d}"), self._p(f"nl{d}"), self.pf32, s), "hist_build")
             else:
                 # regroup level d-1's rows two levels down, then histogram level d+1 (even) contiguously
                 route(d - 1, two=True, move=True)
@@ -532,19 +535,19 @@ class GpuTreeBuilder:
                 gh = min(self.tiles_cap[d + 1], hgrid)
                 sb, sa, _ = level_buf(d + 1)
                 nat.check(lib.h2o_hist_build(sb, self.stride, sa, self._p(f"nodes{d + 1}"), self._p(f"bp{d + 1}"),
-                                             self._p(f"meta{d + 1}"), F, part, slot, qs, gh, pk, 0, 0, s),
+                                             self._p(f"meta{d + 1}"), F, part, slot, qs, gh, pk, 0, 0, self.pf32, s),
                           "hist_build")
             if not dist:
                 # single process: partial sums + sibling subtraction in one pass, straight into hist_next
                 nat.check(lib.h2o_hist_reduce(part, slot, used, self._p(f"nodes{d + 1}"), self._p(f"bp{d + 1}"),
                                               self._p(f"meta{d + 1}"), self.caps[d + 1], gh, 0, hn.data_ptr(),
-                                              hc.data_ptr(), s), "hist_reduce")
+                                              hc.data_ptr(), self.pf32, s), "hist_reduce")
             else:
                 # row-sharded: one built child per parent into the compact buffer (<= caps[d] slots), the
                 # only histogram bytes all-reduced per level, then the sibling subtraction
                 nat.check(lib.h2o_hist_reduce(part, slot, used, self._p(f"nodes{d + 1}"), self._p(f"bp{d + 1}"),
                                               self._p(f"meta{d + 1}"), self.caps[d + 1], gh, hb.data_ptr(), 0, 0,
-                                              s), "hist_reduce")
+                                              self.pf32, s), "hist_reduce")
                 coll.all_reduce_(hb[: self.caps[d] * slot])
                 nat.check(lib.h2o_subtract(hn.data_ptr(), hc.data_ptr(), hb.data_ptr(), self._p(f"nodes{d + 1}"),
                                            self._p(f"meta{d + 1}"), self.caps[d + 1], slot, s), "subtract")

@@ -27,7 +27,7 @@ def run(bins, label, reps=5):
             b.hist[0][: b.slot].zero_()
             ev0.record()
             nat.check(lib.h2o_hist_build(bins.data_ptr(), stride, aux.data_ptr(), b._p("nodes0"), b._p("tp0"),
-                                         b._p("meta0"), F, b.hist[0].data_ptr(), b.slot, b.qs.data_ptr(), grid, 0, 0, 0, s), "hb")
+                                         b._p("meta0"), F, b.hist[0].data_ptr(), b.slot, b.qs.data_ptr(), grid, 0, 0, 0, 0, s), "hb")
             ev1.record()
             torch.cuda.synchronize()
             ts.append(ev0.elapsed_time(ev1))

@@ -124,3 +124,44 @@ def test_extended_isolation_forest_mojo(df, tmp_path):
     path, a, b = _roundtrip(m, df, tmp_path)
     assert "trees/t06.bin" in parse_mojo(path)["files"]
     np.testing.assert_allclose(a.values.astype(float), b.values.astype(float), rtol=1e-6, atol=1e-9)
+
+
+# ------------------------------------------------------------------------------------------------ XGBoost
+@pytest.mark.parametrize("kind", ["binomial", "regression", "multinomial"])
+def test_xgboost_mojo_booster_bytes(tmp_path, kind):
+    import struct
+    import zipfile
+    import h2o
+    import pandas as pd
+    from h2o.estimators import H2OXGBoostEstimator
+    h2o.init(verbose=False)
+    rng = np.random.default_rng(7)
+    n = 1500
+    df = pd.DataFrame(rng.normal(size=(n, 4)), columns=list("abcd"))
+    df.loc[rng.random(n) < 0.05, "b"] = np.nan
+    s = df.a.fillna(0) - 0.5 * df.b.fillna(0) + 0.3 * df.c
+    if kind == "binomial":
+        df["y"] = np.where(s + rng.normal(0, 0.5, n) > 0, "p", "n")
+    elif kind == "multinomial":
+        df["y"] = np.digitize(s, [-0.5, 0.5]).astype(str)
+    else:
+        df["y"] = s + rng.normal(0, 0.1, n)
+    types = {"y": "enum"} if kind != "regression" else None
+    fr = h2o.H2OFrame(df, column_types=types)
+    m = H2OXGBoostEstimator(ntrees=8, max_depth=4, seed=3)
+    m.train(x=list("abcd"), y="y", training_frame=fr)
+    path = m.download_mojo(str(tmp_path))
+    with zipfile.ZipFile(path) as z:
+        ini = z.read("model.ini").decode()
+        bb = z.read("boosterBytes")
+        assert b"0 a q" in z.read("feature_map")
+    assert "algo = xgboost" in ini and "nums = 4" in ini and "use_java_scoring_by_default = true" in ini
+    (bs, nf, ncls) = struct.unpack_from("<fIi", bb, 0)
+    assert nf == 4 and ncls == (3 if kind == "multinomial" else 0)
+    objlen = struct.unpack_from("<Q", bb, 136)[0]
+    assert bb[144:144 + objlen].decode() == {"binomial": "binary:logistic", "regression": "reg:squarederror",
+                                             "multinomial": "multi:softprob"}[kind]
+    g = h2o.import_mojo(path)
+    a = m.predict(fr).as_data_frame().iloc[:, -1].values.astype(float)
+    b = g.predict(fr).as_data_frame().iloc[:, -1].values.astype(float)
+    np.testing.assert_allclose(b, a, rtol=1e-5, atol=1e-5)
