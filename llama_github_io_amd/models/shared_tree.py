@@ -10,6 +10,7 @@ Algorithm subclasses provide ``_prepare`` (per-row histogram/leaf statistics), `
 from __future__ import annotations
 
 import math
+import os
 import time
 
 import numpy as np
@@ -191,10 +192,14 @@ class SharedTreeTrainer:
         max_rt = float(p.get("max_runtime_secs") or 0)
         self.valid = valid
         built = start
+        hprof = os.environ.get("H2O_HOST_PROF") == "1"    # host seconds per phase (launch-bound diagnosis)
+        ht = dict(prepare=0.0, build=0.0, update=0.0, drain=0.0)
         for t in range(start, ntrees):
             feat_ok = self._tree_feature_mask(rng, F)
             for k in range(K):
+                h0 = time.perf_counter()
                 aux = self._prepare(t, k)
+                h1 = time.perf_counter()
                 kw = {}
                 am = self._amax_for_build()
                 if am is not None:
@@ -206,11 +211,20 @@ class SharedTreeTrainer:
                         kw["leaf_native"] = ln
                 h = self.builder.build(aux, feat_ok, self._k_cols(F), seed=(self.seed * 1000003 + t * 97 + k) & ((1 << 63) - 1),
                                        leaf_fn=lambda ls, t=t, k=k: self._leaf_values(ls, t, k), **kw)
+                h2 = time.perf_counter()
                 self._update(t, k)
                 handles.append((h, k))
+                h3 = time.perf_counter()
+                if t >= start + 2:                   # skip first-launch module loads / allocations
+                    ht["prepare"] += h1 - h0
+                    ht["build"] += h2 - h1
+                    ht["update"] += h3 - h2
             built = t + 1
             if not need_sync:
+                h0 = time.perf_counter()
                 self._drain(handles, forest, gains, ready_only=True)   # overlap host decode with GPU work
+                if t >= start + 2:
+                    ht["drain"] += time.perf_counter() - h0
             if need_sync:
                 self._drain(handles, forest, gains)
                 if interval and (built % interval == 0 or built == ntrees):
@@ -226,6 +240,9 @@ class SharedTreeTrainer:
             if max_rt > 0 and time.time() - t_start > max_rt:
                 break
         self._drain(handles, forest, gains)
+        if hprof and built > start + 2:
+            n = (built - start - 2) * K
+            print("[host-prof] us/tree " + " ".join(f"{k}={v / n * 1e6:.1f}" for k, v in ht.items()), flush=True)
         if need_sync and (not history or history[-1]["number_of_trees"] != built):
             history.append(self._score_event(model, built, t_start))
         self._finish(model, built)

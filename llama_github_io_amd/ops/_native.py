@@ -22,6 +22,11 @@ c_int, c_ll, c_ull, c_double, c_void_p = ctypes.c_int, ctypes.c_longlong, ctypes
 
 _HIP_SIGS = {
     "h2o_tree_sizes": [c_void_p],
+    "h2o_tree_plan_size": [],
+    "h2o_tree_root": [c_void_p, c_void_p],
+    "h2o_tree_level": [c_void_p, c_int, c_int, c_void_p],
+    "h2o_tree_subtract": [c_void_p, c_int, c_void_p],
+    "h2o_tree_all": [c_void_p, c_void_p],
     "h2o_hist_build": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int,
                        c_int, c_void_p, c_void_p, c_int, c_void_p],
     "h2o_split_find": [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_double, c_double,

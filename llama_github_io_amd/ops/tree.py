@@ -15,6 +15,7 @@ sorted by mean response. Mode 1 is XGBoost's Newton gain G²/(H+λ) with L1 soft
 """
 from __future__ import annotations
 
+import ctypes
 import math
 import os
 from dataclasses import dataclass, field
@@ -342,6 +343,27 @@ class RefTreeBuilder:
 
 
 # ================================================================================================
+_MAXL = 65
+_vp, _ci, _cd = ctypes.c_void_p, ctypes.c_int, ctypes.c_double
+
+
+class _TreePlan(ctypes.Structure):
+    """Mirror of ``TreePlan`` in ``csrc/tree_kernels.hip`` (native per-tree launch sequence)."""
+    _fields_ = ([("N", ctypes.c_longlong)] +
+                [(n, _ci) for n in ("stride", "F", "D", "slot", "used", "pf32", "grid", "leaf_cap", "mode",
+                                    "random_split", "pad0")] +
+                [(n, _cd) for n in ("min_w", "msi", "lam", "alpha", "gamma")] +
+                [(n, _vp) for n in ("master", "partials", "hist0", "hist1", "hbuild", "cand", "scratch", "nbins_f",
+                                    "iscat_f", "mono_f", "qs", "leafsum", "leaf_of_row", "counters", "rootw",
+                                    "leafval")] +
+                [(n, _vp * 2) for n in ("bb", "ba", "br")] +
+                [(n, _vp * _MAXL) for n in ("nodes", "meta", "tp", "bp", "dec", "cl", "cr", "nl", "cur")] +
+                [("caps", _ci * _MAXL), ("tiles_cap", _ci * _MAXL)] +
+                [(n, _vp) for n in ("aux", "amax_bits", "feat_ok")] +
+                [(n, _ci) for n in ("compute_amax", "k_cols", "packed", "leaf_native", "log_link", "pad1")] +
+                [("seed", ctypes.c_ulonglong)] + [(n, _cd) for n in ("scale", "kclamp", "mx")])
+
+
 class _Arena:
     """One device allocation holding every small per-level array (copied to host in one shot)."""
 
@@ -440,9 +462,41 @@ class GpuTreeBuilder:
         self.av["bp0"][:8].copy_(torch.from_numpy(np.array([0, n_tiles0], dtype=np.int32).view(np.uint8)))
         self.history = []       # (pinned host snapshot, copy-done event) per built tree, in build order
         self._pinned_pool = []
+        self._event_pool = []
+        # raw device pointers resolved once: the per-tree launch sequence is ~45 ctypes calls and at small
+        # shards (1.375M rows/GPU) the host loop, not the GPU, set the pace (82 % busy, rocprofv3 trace)
+        self._pt = {name: t.data_ptr() for name, t in self.av.items()}
+        self._hp = [h.data_ptr() for h in self.hist]
+        self._bp = [dict(bins=b["bins"].data_ptr(), aux=b["aux"].data_ptr(), ridx=b["ridx"].data_ptr())
+                    for b in self.bufs]
 
     def _p(self, name):
-        return self.av[name].data_ptr()
+        return self._pt[name]
+
+    def _make_plan(self):
+        """Static part of the native launch plan (pointers / shapes fixed for the builder's lifetime)."""
+        if self.D >= _MAXL - 1 or os.environ.get("H2O_TREE_PYLAUNCH") == "1":
+            return None
+        assert self.lib.h2o_tree_plan_size() == ctypes.sizeof(_TreePlan), "TreePlan layout mismatch"
+        P = _TreePlan()
+        p = self.p
+        P.N, P.stride, P.F, P.D, P.slot, P.used, P.pf32 = self.N, self.stride, self.F, self.D, self.slot, self.used, self.pf32
+        P.leaf_cap, P.mode, P.random_split = self.leaf_cap, int(p.mode), int(p.random_split)
+        P.min_w, P.msi, P.lam, P.alpha, P.gamma = p.min_w, p.min_split_improvement, p.lam, p.alpha, p.gamma
+        P.master, P.partials = self.master.data_ptr(), self.partials.data_ptr()
+        P.hist0, P.hist1, P.hbuild = self._hp[0], self._hp[1], self.hbuild.data_ptr()
+        P.cand, P.scratch = self.cand.data_ptr(), self.scratch.data_ptr()
+        P.nbins_f, P.iscat_f = self.nbins_f.data_ptr(), self.iscat_f.data_ptr()
+        P.mono_f = 0 if self.mono_f is None else self.mono_f.data_ptr()
+        P.qs, P.leafsum, P.leaf_of_row = self.qs.data_ptr(), self.leafsum.data_ptr(), self.leaf_of_row.data_ptr()
+        P.counters, P.rootw, P.leafval = self._p("counters"), self._p("rootw"), self._p("leafval")
+        for i in range(2):
+            P.bb[i], P.ba[i], P.br[i] = self._bp[i]["bins"], self._bp[i]["aux"], self._bp[i]["ridx"]
+        for d in range(self.D + 1):
+            for n in ("nodes", "meta", "tp", "bp", "dec", "cl", "cr", "nl", "cur"):
+                getattr(P, n)[d] = self._p(f"{n}{d}")
+            P.caps[d], P.tiles_cap[d] = self.caps[d], self.tiles_cap[d]
+        return P
 
     def build(self, aux_static: torch.Tensor, feat_ok: torch.Tensor | None = None, k_cols: int = 0, seed: int = 0,
               leaf_fn=None, amax_bits: torch.Tensor | None = None, packed: bool = False, leaf_native=None):
@@ -456,6 +510,10 @@ class GpuTreeBuilder:
         packed count|wY atomic per (row, feature)."""
         pk = int(bool(packed))
         lib, s = self.lib, nat.stream_ptr(self.dev)
+        if not hasattr(self, "_plan"):
+            self._plan = self._make_plan()
+        if self._plan is not None:
+            return self._build_native(aux_static, feat_ok, k_cols, seed, leaf_fn, amax_bits, pk, leaf_native, s)
         F, D, p, T = self.F, self.D, self.p, self.TILE
         assert aux_static.shape == (self.N, 4) and aux_static.dtype == torch.float32 and aux_static.is_contiguous()
         fo = self.feat_ok_all if feat_ok is None else feat_ok
@@ -481,34 +539,39 @@ class GpuTreeBuilder:
         seed = int(seed) & _M64
         hb = self.hbuild
 
+        master_p, aux_p = self.master.data_ptr(), aux_static.data_ptr()
+
         def level_buf(e):
             # rows are regrouped every second level: level e (even) lives in the master order (e == 0)
             # or in ping-pong buffer (e/2 - 1) % 2
             if e == 0:
-                return self.master.data_ptr(), aux_static.data_ptr(), 0
-            b = self.bufs[(e // 2 - 1) % 2]
-            return b["bins"].data_ptr(), b["aux"].data_ptr(), b["ridx"].data_ptr()
+                return master_p, aux_p, 0
+            b = self._bp[(e // 2 - 1) % 2]
+            return b["bins"], b["aux"], b["ridx"]
 
         def route(e, two, move):
             sb, sa, sr = level_buf(e)
-            dst = self.bufs[(e // 2) % 2]
+            dst = self._bp[(e // 2) % 2]
             b1 = e + 1 if two else e
-            nat.check(lib.h2o_route(sb, sa, sr, dst["bins"].data_ptr(), dst["aux"].data_ptr(), dst["ridx"].data_ptr(),
+            nat.check(lib.h2o_route(sb, sa, sr, dst["bins"], dst["aux"], dst["ridx"],
                                     self.stride, self._p(f"nodes{e}"), self._p(f"tp{e}"), self._p(f"meta{e}"),
                                     self._p(f"dec{e}"), self._p(f"cl{e}"), self._p(f"cr{e}"), self._p(f"dec{b1}"),
                                     self._p(f"cl{b1}"), self._p(f"cr{b1}"), self._p(f"cur{b1}"),
                                     self.leaf_of_row.data_ptr(), self.leafsum.data_ptr(), int(two), int(move),
                                     self.tiles_cap[e], s), "route")
 
+        hc_p = self._hp
+        cand_p, nb_p, ic_p, fo_p = self.cand.data_ptr(), self.nbins_f.data_ptr(), self.iscat_f.data_ptr(), fo.data_ptr()
         for d in range(D):
             hc, hn = self.hist[d % 2], self.hist[(d + 1) % 2]
+            hcp, hnp = hc_p[d % 2], hc_p[(d + 1) % 2]
             cap = self.caps[d]
             odd = d % 2 == 1
-            nat.check(lib.h2o_split_find(hc.data_ptr(), slot, self._p(f"meta{d}"), cap, F, self.nbins_f.data_ptr(),
-                                         self.iscat_f.data_ptr(), mono, p.min_w, p.min_split_improvement, p.lam,
+            nat.check(lib.h2o_split_find(hcp, slot, self._p(f"meta{d}"), cap, F, nb_p,
+                                         ic_p, mono, p.min_w, p.min_split_improvement, p.lam,
                                          p.alpha, p.gamma, p.mode, int(p.random_split), seed, d,
-                                         self.cand.data_ptr(), self._p("rootw") if d == 0 else 0, s), "split_find")
-            nat.check(lib.h2o_split_reduce(self.cand.data_ptr(), self._p(f"meta{d}"), cap, F, fo.data_ptr(), int(k_cols),
+                                         cand_p, self._p("rootw") if d == 0 else 0, s), "split_find")
+            nat.check(lib.h2o_split_reduce(cand_p, self._p(f"meta{d}"), cap, F, fo_p, int(k_cols),
                                            seed, d, self._p(f"dec{d}"), s), "split_reduce")
             nat.check(lib.h2o_plan(self._p(f"nodes{d}"), self._p(f"meta{d}"), self._p(f"dec{d}"), self._p(f"nl{d}"),
                                    self._p(f"nl{d - 1}") if odd else 0, self._p(f"cur{d}"), self._p(f"cl{d}"),
@@ -540,8 +603,8 @@ class GpuTreeBuilder:
             if not dist:
                 # single process: partial sums + sibling subtraction in one pass, straight into hist_next
                 nat.check(lib.h2o_hist_reduce(part, slot, used, self._p(f"nodes{d + 1}"), self._p(f"bp{d + 1}"),
-                                              self._p(f"meta{d + 1}"), self.caps[d + 1], gh, 0, hn.data_ptr(),
-                                              hc.data_ptr(), self.pf32, s), "hist_reduce")
+                                              self._p(f"meta{d + 1}"), self.caps[d + 1], gh, 0, hnp,
+                                              hcp, self.pf32, s), "hist_reduce")
             else:
                 # row-sharded: one built child per parent into the compact buffer (<= caps[d] slots), the
                 # only histogram bytes all-reduced per level, then the sibling subtraction
@@ -564,7 +627,56 @@ class GpuTreeBuilder:
         host = self._pinned_pool.pop() if self._pinned_pool else torch.empty(self.arena.numel(), dtype=torch.uint8,
                                                                                pin_memory=True)
         host.copy_(self.arena, non_blocking=True)
-        ev = torch.cuda.Event()
+        ev = self._event_pool.pop() if self._event_pool else torch.cuda.Event()
+        ev.record()
+        self.history.append((host, ev))
+        return len(self.history) - 1
+
+    def _build_native(self, aux_static, feat_ok, k_cols, seed, leaf_fn, amax_bits, pk, leaf_native, s):
+        """build() through the native launch plan: one host call per tree (single process) or one per
+        collective segment (row-sharded)."""
+        assert aux_static.shape == (self.N, 4) and aux_static.dtype == torch.float32 and aux_static.is_contiguous()
+        lib, P = self.lib, self._plan
+        P.aux = aux_static.data_ptr()
+        P.compute_amax = int(amax_bits is None)
+        P.amax_bits = (self.amax_bits if amax_bits is None else amax_bits).data_ptr()
+        P.feat_ok = (self.feat_ok_all if feat_ok is None else feat_ok).data_ptr()
+        P.k_cols, P.packed, P.seed = int(k_cols), pk, int(seed) & _M64
+        P.grid = self.grid * (self.hist_bpc if pk else 1)
+        P.leaf_native = int(leaf_native is not None)
+        if leaf_native is not None:
+            lg, scale, kclamp, mx = leaf_native
+            P.log_link, P.scale, P.kclamp, P.mx = int(lg), float(scale), float(kclamp), float(mx)
+        ref = ctypes.byref(P)
+        if not coll.is_dist():
+            nat.check(lib.h2o_tree_all(ref, s), "tree_all")
+        else:
+            nat.check(lib.h2o_tree_root(ref, s), "tree_root")
+            coll.all_reduce_(self.hist[0][: self.slot])
+            for d in range(self.D):
+                r = lib.h2o_tree_level(ref, d, 1, s)
+                if r < 0:
+                    nat.check(-r, "tree_level")
+                if r == 1:
+                    break
+                coll.all_reduce_(self.hbuild[: self.caps[d] * self.slot])
+                nat.check(lib.h2o_tree_subtract(ref, d, s), "tree_subtract")
+            coll.all_reduce_(self.leafsum)
+            if leaf_native is not None:
+                nat.check(lib.h2o_leaf_values(self.leafsum.data_ptr(), self.leaf_cap, P.log_link, P.scale, P.kclamp,
+                                              P.mx, self._p("leafval"), s), "leaf_values")
+        if leaf_native is None and leaf_fn is not None:
+            vals = leaf_fn(self.leafsum)
+            self.av["leafval"].view(torch.float32)[: vals.numel()].copy_(vals.to(torch.float32))
+        return self._snapshot()
+
+    def _snapshot(self):
+        # the tree's structure travels to pinned host memory asynchronously: the host decodes finished
+        # trees (pop_levels(ready_only=True)) while the GPU builds the next ones
+        host = self._pinned_pool.pop() if self._pinned_pool else torch.empty(self.arena.numel(), dtype=torch.uint8,
+                                                                               pin_memory=True)
+        host.copy_(self.arena, non_blocking=True)
+        ev = self._event_pool.pop() if self._event_pool else torch.cuda.Event()
         ev.record()
         self.history.append((host, ev))
         return len(self.history) - 1
@@ -587,6 +699,7 @@ class GpuTreeBuilder:
             o = self._off["rootw"][0]
             out.append(self._decode(hn, float(hn[o:o + 8].view(np.float64)[0])))
             self._pinned_pool.append(host)
+            self._event_pool.append(ev)
         return out
 
     def _decode(self, host: np.ndarray, root_weight: float) -> TreeLevels:
