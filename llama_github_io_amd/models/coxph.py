@@ -88,7 +88,9 @@ class CoxPHModel(Model):
         return "CoxPH"
 
     def _predict_tensor(self, X, offset=None):
-        Z = self.expander.transform(X.to(self.device)).double()
+        keep = getattr(self, "keep", None)
+        X = X.to(self.device)
+        Z = self.expander.transform(X if keep is None else X[keep]).double()
         lp = Z @ self.beta.to(Z.device) - float(self.output["lp_mean"])
         if offset is not None:
             lp = lp + offset.double()
@@ -104,12 +106,24 @@ class CoxPHModel(Model):
         s = super().to_state()
         s["beta"] = self.beta.cpu().tolist()
         s["expander"] = self.expander.to_state()
+        s["keep"] = getattr(self, "keep", None)
+        s["strata_idx"] = getattr(self, "strata_idx", [])
+        s["special_idx"] = getattr(self, "special_idx", [])
+        s["strata_values"] = getattr(self, "strata_values", [])
         return s
 
     def _restore(self, s):
         super()._restore(s)
         self.beta = torch.tensor(s["beta"], dtype=torch.float64)
-        self.expander = Expander.from_state(self.info, s["expander"])
+        self.keep = s.get("keep")
+        self.strata_idx = s.get("strata_idx") or []
+        self.special_idx = s.get("special_idx") or []
+        self.strata_values = s.get("strata_values") or []
+        sub = self.info if self.keep is None else DataInfo([self.info.x[j] for j in self.keep],
+                                                          np.asarray(self.info.iscat)[self.keep],
+                                                          [self.info.domains[j] for j in self.keep],
+                                                          self.info.response, self.info.response_domain)
+        self.expander = Expander.from_state(sub, s["expander"])
 
 
 class CoxPHTrainer:
@@ -134,12 +148,14 @@ class CoxPHTrainer:
             special.append(j_start)
             start = X[j_start].double()
         strata = None
+        strata_idx = []
         if p["stratify_by"]:
             sb = p["stratify_by"] if isinstance(p["stratify_by"], (list, tuple)) else [p["stratify_by"]]
             codes = torch.zeros(X.shape[1], dtype=torch.float64, device=X.device)
             for c in sb:
                 j = info.x.index(c)
                 special.append(j)
+                strata_idx.append(j)
                 codes = codes * 1000 + torch.nan_to_num(X[j].double(), nan=-1)
             strata = codes
         keep = [j for j in range(info.F) if j not in special]
@@ -192,8 +208,14 @@ class CoxPHTrainer:
         model.device = dev
         model.expander = ex
         model.beta = beta
+        model.keep, model.strata_idx = keep, strata_idx
+        model.special_idx = [j for j in special if j not in strata_idx]
+        model.strata_values = ([] if not strata_idx else
+                               torch.unique(torch.nan_to_num(X[strata_idx].double(), nan=-1).T, dim=0).cpu().tolist())
         lp = Z @ beta
         model.output["lp_mean"] = float((w * lp).sum() / w.sum())
+        # weighted design means: the MOJO's x_mean_cat / x_mean_num (lp_mean = z_mean . beta)
+        model.output["z_mean"] = ((w[:, None] * Z).sum(0) / w.sum()).cpu().tolist()
         names = ex.names
         model.output["coefficients"] = dict(zip(names, beta.cpu().tolist()))
         model.output["coefficients_table"] = [dict(names=n, coefficients=float(b), exp_coef=math.exp(float(b)),

@@ -104,6 +104,9 @@ class GenericModel(Model):
         elif algo == "extendedisolationforest":
             m.eif = A.load_eif(ki, mj["files"])
             m.output["model_category"] = "AnomalyDetection"
+        elif algo == "coxph":
+            m.cox = A.load_coxph(ki, mj["files"])
+            m.output["model_category"] = "CoxPH"
         elif algo == "stackedensemble":
             subs = {}
             for i in range(int(ki.get("submodel_count", 0))):
@@ -161,6 +164,8 @@ class GenericModel(Model):
             return ["predict", "mean_length"]
         if self.output.get("original_algo") == "extendedisolationforest":
             return ["anomaly_score", "mean_length"]
+        if self.output.get("original_algo") == "coxph":
+            return ["lp"]
         if self.output.get("original_algo") == "pca":
             return [f"PC{i + 1}" for i in range(self.pca["k"])]
         return None
@@ -260,6 +265,9 @@ class GenericModel(Model):
         if algo == "extendedisolationforest":
             from ..mojo import algos as A
             return A.score_eif(self.eif, X)
+        if algo == "coxph":
+            from ..mojo import algos as A
+            return A.score_coxph(self.cox, X)
         if algo == "stackedensemble":
             cols = []
             for b in self.base:

@@ -413,3 +413,96 @@ def score_eif(st, X):
     h = tot / max(1, len(st["trees"]))
     c = float(c_factor(st["sample_size"]))
     return torch.stack([torch.pow(2.0, -h / c).float(), h.float()], 1)
+
+
+# ================================================================================================ CoxPH
+def _blob_rect(rows) -> bytes:
+    """ModelMojoWriter.writeRectangularDoubleArray payload: row-major big-endian doubles, no header."""
+    return np.asarray(rows, dtype=">f8").tobytes()
+
+
+def coxph_columns(model):
+    """CoxPHMojoModel row layout (CoxPHMojoModel.featureValue: strata columns first, then the DataInfo
+    categoricals and numerics); the start/stop columns follow and are not read by the scorer."""
+    info, keep, ex = model.info, model.keep, model.expander
+    order = list(model.strata_idx) + [keep[j] for j in ex.cats] + [keep[j] for j in ex.nums] + list(model.special_idx)
+    cols = [info.x[j] for j in order] + ([info.response] if info.response else [])
+    doms = [info.domains[j] for j in order] + ([info.response_domain] if info.response else [])
+    return cols, doms
+
+
+def write_coxph(model, kv, blobs):
+    """CoxPHMojoWriter.writeModelData layout (h2o-algos/src/main/java/hex/coxph/CoxPHMojoWriter.java):
+    coef, cats / cat_offsets / use_all_factor_levels, num_numerical_columns / num_offsets, x_mean_cat /
+    x_mean_num per stratum (lp base = x_mean . coef) and strata_count / strata_i."""
+    ex = model.expander
+    beta = [float(b) for b in model.beta.cpu().tolist()]
+    zm = model.output.get("z_mean")
+    if zm is None:
+        raise ValueError("CoxPH model has no design means (retrain to export a MOJO)")
+    strata = [list(map(float, s)) for s in getattr(model, "strata_values", [])]
+    S = max(1, len(strata))
+    nc = ex.num_off
+    kv["coef"] = _arr(beta)
+    kv["cats"] = len(ex.cats)
+    kv["cat_offsets"] = _arr(list(ex.cat_offsets) + [nc])
+    kv["use_all_factor_levels"] = "true" if ex.use_all else "false"
+    kv["num_numerical_columns"] = len(ex.nums)
+    kv["num_offsets"] = _arr([nc + i for i in range(len(ex.nums))])
+    for t, part in (("x_mean_cat", zm[:nc]), ("x_mean_num", zm[nc:])):
+        kv[f"{t}_size1"] = S
+        kv[f"{t}_size2"] = len(part)
+        blobs[t] = _blob_rect([part] * S)
+    kv["strata_count"] = len(strata)
+    for i, s in enumerate(strata):
+        kv[f"strata_{i}"] = _arr(s)
+    kv["n_features"] = len(model.info.x)
+
+
+def load_coxph(ki, files):
+    from .reader import _floats
+    coef = np.asarray(_floats(ki["coef"]), dtype=np.float64)
+    ns = int(ki.get("strata_count", 0))
+    strata = [np.asarray(_floats(ki[f"strata_{i}"])) for i in range(ns)]
+
+    def rect(t):
+        a, b = int(ki[f"{t}_size1"]), int(ki[f"{t}_size2"])
+        return np.frombuffer(files.get(t, b""), dtype=">f8", count=a * b).astype(np.float64).reshape(a, b)
+    xc, xn = rect("x_mean_cat"), rect("x_mean_num")
+    nstart = xc.shape[1] if xc.shape[0] >= 1 else 0
+    lp_base = xc @ coef[:xc.shape[1]] + xn @ coef[nstart:nstart + xn.shape[1]]   # CoxPHMojoModel.computeLpBase
+    return dict(coef=coef, cats=int(ki["cats"]), cat_offsets=[int(v) for v in _floats(ki["cat_offsets"])],
+                use_all=ki.get("use_all_factor_levels") == "true", nums=int(ki["num_numerical_columns"]),
+                num_offsets=[int(v) for v in _floats(ki["num_offsets"])], strata=strata,
+                strata_len=len(strata[0]) if strata else 0, lp_base=lp_base)
+
+
+def score_coxph(st, X):
+    """CoxPHMojoModel.score0 on a [F, N] frame: categorical coefficients + numeric terms - lp base of the
+    row's stratum (rows of an unseen stratum score NaN)."""
+    X = X.double()
+    S, coef = st["strata_len"], torch.tensor(st["coef"], dtype=torch.float64, device=X.device)
+    N = X.shape[1]
+    lp = torch.zeros(N, dtype=torch.float64, device=X.device)
+    lo = 0 if st["use_all"] else 1
+    co = st["cat_offsets"]
+    for c in range(st["cats"]):
+        v = X[S + c]
+        lvl = torch.nan_to_num(v, nan=-1).long() - lo
+        x = lvl + co[c]
+        ok = (lvl >= 0) & (x < co[c + 1])
+        lp = lp + torch.where(ok, coef[x.clamp(0, coef.numel() - 1)], torch.zeros_like(lp))
+        lp = torch.where(torch.isnan(v), torch.full_like(lp, float("nan")), lp)
+    for i in range(st["nums"]):
+        if st["num_offsets"][i] >= coef.numel():
+            break
+        lp = lp + coef[st["num_offsets"][i]] * X[S + st["cats"] + i]
+    if not st["strata"]:
+        return (lp - float(st["lp_base"][0])).float()
+    base = torch.full_like(lp, float("nan"))
+    for k, s in enumerate(st["strata"]):
+        m = torch.ones(N, dtype=torch.bool, device=X.device)
+        for j, v in enumerate(s):
+            m &= torch.nan_to_num(X[j], nan=-1).long() == int(v)
+        base = torch.where(m, torch.full_like(base, float(st["lp_base"][k])), base)
+    return (lp - base).float()

@@ -165,3 +165,35 @@ def test_xgboost_mojo_booster_bytes(tmp_path, kind):
     a = m.predict(fr).as_data_frame().iloc[:, -1].values.astype(float)
     b = g.predict(fr).as_data_frame().iloc[:, -1].values.astype(float)
     np.testing.assert_allclose(b, a, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("strata", [False, True])
+def test_coxph_mojo_reference_layout(tmp_path, strata):
+    from h2o.estimators import H2OCoxProportionalHazardsEstimator
+    h2o.init(verbose=False)
+    rng = np.random.default_rng(5)
+    n = 600
+    x = rng.normal(size=n)
+    g = rng.choice(list("abc"), n)
+    s = rng.choice(["s0", "s1"], n)
+    T = rng.exponential(1 / np.exp(0.7 * x + (g == "b") * 0.5))
+    C = rng.exponential(2.0, n)
+    # the stop column first: the scorer must pick the predictors, not the frame's first columns
+    d = pd.DataFrame({"time": np.minimum(T, C), "x": x, "g": g, "s": s, "event": (T <= C).astype(int)})
+    fr = h2o.H2OFrame(d, column_types={"g": "enum", "s": "enum"})
+    kw = dict(stop_column="time")
+    if strata:
+        kw["stratify_by"] = ["s"]
+    m = H2OCoxProportionalHazardsEstimator(**kw)
+    m.train(x=["time", "x", "g", "s"] if strata else ["time", "x", "g"], y="event", training_frame=fr)
+    assert abs(m._model.output["coefficients"]["x"] - 0.7) < 0.2
+    path, a, b = _roundtrip(m, fr, tmp_path)
+    mj = parse_mojo(path)
+    ki = mj["info"]
+    assert ki["algo"] == "coxph" and "coef" in ki and "x_mean_num" in mj["files"]
+    assert int(ki["strata_count"]) == (2 if strata else 0)
+    cols = mj["columns"]
+    assert cols[: (2 if strata else 1)] == (["s", "g"] if strata else ["g"])
+    assert np.allclose(a.values.astype(float), b.values.astype(float), atol=1e-5)
+    # lp is centred: weighted mean of the training linear predictor is 0
+    assert abs(float(a.values.astype(float).mean())) < 1e-6
