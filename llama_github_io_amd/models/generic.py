@@ -104,6 +104,10 @@ class GenericModel(Model):
         elif algo == "extendedisolationforest":
             m.eif = A.load_eif(ki, mj["files"])
             m.output["model_category"] = "AnomalyDetection"
+        elif algo == "targetencoder":
+            m.inner = A.load_targetencoder(ki, mj["files"], info)
+            m.inner.key = m.key + "_te"
+            m.output["model_category"] = "TargetEncoder"
         elif algo == "coxph":
             m.cox = A.load_coxph(ki, mj["files"])
             m.output["model_category"] = "CoxPH"

@@ -506,3 +506,88 @@ def score_coxph(st, X):
             m &= torch.nan_to_num(X[j], nan=-1).long() == int(v)
         base = torch.where(m, torch.full_like(base, float(st["lp_base"][k])), base)
     return (lp - base).float()
+
+
+# ================================================================================================ TargetEncoder
+TE_DIR = "feature_engineering/target_encoding/"
+
+
+def write_targetencoder(model, kv, blobs):
+    """TargetEncoderMojoWriter layout (h2o-extensions/target-encoder/.../TargetEncoderMojoWriter.java):
+    blending parameters in model.ini, ``encoding_map.ini`` ([column] sections of ``level = numerator
+    denominator [targetclass]``), the NA-presence map and the input->encoding / input->output column maps.
+    NA levels are not encoded here (they take the prior), so every column is written with has_NAs = 0."""
+    p, info = model.params, model.info
+    kv["keep_original_categorical_columns"] = "true" if p.get("keep_original_categorical_columns", True) else "false"
+    kv["with_blending"] = "true" if p.get("blending") else "false"
+    if p.get("blending"):
+        kv["inflection_point"] = repr(float(p["inflection_point"]))
+        kv["smoothing"] = repr(float(p["smoothing"]))
+    nonp = [c for c in (info.weights, info.offset, info.fold or p.get("fold_column"), info.response) if c]
+    kv["non_predictors"] = ";".join(nonp)
+    multi = model.K > 1
+    enc, nas, inenc, inout = [], [], [], []
+    for name in model.output["encoded_columns"]:
+        st = model.stats[name]
+        num = np.asarray(st["num"].cpu() if torch.is_tensor(st["num"]) else st["num"], dtype=np.float64)
+        den = np.asarray(st["den"].cpu() if torch.is_tensor(st["den"]) else st["den"], dtype=np.float64)
+        num = num.reshape(den.shape[0], -1)
+        enc.append(f"[{name}]")
+        for lvl in range(den.shape[0]):
+            if den[lvl] <= 0:
+                continue
+            if multi:
+                for k in range(num.shape[1]):
+                    enc.append(f"{lvl} = {float(num[lvl, k])!r} {float(den[lvl])!r} {k + 1}")
+            else:
+                enc.append(f"{lvl} = {float(num[lvl, 0])!r} {float(den[lvl])!r}")
+        nas.append(f"{name} = 0")
+        inenc += ["[from]", name, "[to]", name]
+        outs = ([f"{name}_{info.response_domain[k + 1]}_te" for k in range(model.K)] if multi else [f"{name}_te"])
+        inout += ["[from]", name, "[to]"] + outs
+    for fn, lines in (("encoding_map.ini", enc), ("te_column_name_to_missing_values_presence.ini", nas),
+                      ("input_encoding_columns_map.ini", inenc), ("input_output_columns_map.ini", inout)):
+        blobs[TE_DIR + fn] = "".join(s + "\n" for s in lines)
+
+
+def load_targetencoder(ki, files, info):
+    """Encoding maps -> TargetEncoderModel statistics (prior = Σnumerator / Σdenominator over the map, as
+    TargetEncoderMojoModel computes it)."""
+    from ..models.targetencoder import TargetEncoderModel
+    raw = files[TE_DIR + "encoding_map.ini"]
+    text = raw.decode() if isinstance(raw, bytes) else raw
+    ncls = int(ki.get("n_classes", 1))
+    Kp = ncls - 1 if ncls > 2 else 1
+    maps, cur = {}, None
+    for line in text.splitlines():
+        s = line.strip()
+        if not s:
+            continue
+        if s.startswith("[") and s.endswith("]"):
+            cur = maps.setdefault(s[1:-1], {})
+            continue
+        lvl, _, comp = s.partition("=")
+        parts = comp.split()
+        cls = int(parts[2]) - 1 if len(parts) > 2 else 0
+        e = cur.setdefault(int(lvl), [np.zeros(Kp), 0.0])
+        e[0][cls] = float(parts[0])
+        e[1] = float(parts[1])
+    params = dict(blending=ki.get("with_blending") == "true", inflection_point=float(ki.get("inflection_point", 10)),
+                  smoothing=float(ki.get("smoothing", 20)),
+                  keep_original_categorical_columns=ki.get("keep_original_categorical_columns", "false") == "true",
+                  noise=0.0, data_leakage_handling="none")
+    m = TargetEncoderModel(None, params, info)
+    m.device = torch.device("cpu")
+    m.K = Kp
+    m.stats = {}
+    for name, mp in maps.items():
+        j = info.x.index(name) if name in info.x else None
+        dom = list(info.domains[j]) if j is not None and info.domains[j] is not None else []
+        L = max(len(dom), (max(mp) + 1) if mp else 0)
+        num, den = np.zeros((L, Kp)), np.zeros(L)
+        for lvl, (nv, dv) in mp.items():
+            num[lvl], den[lvl] = nv, dv
+        prior = num.sum(0) / max(den.sum(), 1e-300)
+        m.stats[name] = dict(num=num, den=den, prior=prior, domain=dom)
+    m.output["encoded_columns"] = list(maps)
+    return m

@@ -197,3 +197,23 @@ def test_coxph_mojo_reference_layout(tmp_path, strata):
     assert np.allclose(a.values.astype(float), b.values.astype(float), atol=1e-5)
     # lp is centred: weighted mean of the training linear predictor is 0
     assert abs(float(a.values.astype(float).mean())) < 1e-6
+
+
+@pytest.mark.parametrize("y,blending", [("y", True), ("r", False), ("m", True)])
+def test_target_encoder_mojo_reference_layout(df, tmp_path, y, blending):
+    from h2o.estimators import H2OTargetEncoderEstimator
+    te = H2OTargetEncoderEstimator(blending=blending, inflection_point=5, smoothing=3)
+    te.train(x=["k", "m"] if y != "m" else ["k"], y=y, training_frame=df)
+    path = te.download_mojo(str(tmp_path))
+    mj = parse_mojo(path)
+    f = mj["files"]
+    assert mj["info"]["algo"] == "targetencoder"
+    em = f["feature_engineering/target_encoding/encoding_map.ini"].decode()
+    assert em.startswith("[k]\n0 = ")
+    assert "[from]\nk\n[to]\n" in f["feature_engineering/target_encoding/input_output_columns_map.ini"].decode()
+    g = h2o.import_mojo(path)
+    a = te.transform(df).as_data_frame()
+    b = g.transform(df).as_data_frame()
+    tecols = [c for c in a.columns if c.endswith("_te")]
+    assert tecols and list(b[tecols].columns) == tecols
+    assert np.allclose(a[tecols].values.astype(float), b[tecols].values.astype(float), atol=1e-9)
