@@ -7,8 +7,9 @@ The reference ships the user's class to the cluster and runs it under Jython, ro
 user's class object runs in-process: it is first called with whole NumPy columns (most metric /
 gradient code is plain arithmetic and vectorises as written); a function that only handles scalars
 falls back to a per-row loop with the reference's row-wise semantics. References keep the reference
-string format ``python:<key>=<module>.<Class>Wrapper``. Only class objects are accepted (source
-strings are not compiled here).
+string format ``python:<key>=<module>.<Class>Wrapper``. A class given as a source string (the reference's
+``func`` string form with ``class_name``) is compiled into its own module namespace in-process, where the
+reference would compile it under Jython on the cluster.
 """
 from __future__ import annotations
 
@@ -19,10 +20,25 @@ import numpy as np
 _REGISTRY: dict = {}
 
 
-def _register(func, func_file, func_name, kind, methods):
+def _from_source(src: str, func_file: str, class_name: str | None):
+    """h2o.py:upload_custom_metric string form: ``src`` defines ``class_name`` (required, as in the reference)."""
+    import types
+    if not class_name:
+        raise ValueError("class_name is required when the custom function is given as a source string")
+    mod = types.ModuleType(func_file[:-3] if func_file.endswith(".py") else func_file)
+    exec(compile(src, func_file, "exec"), mod.__dict__)
+    cls = mod.__dict__.get(class_name)
+    if not inspect.isclass(cls):
+        raise ValueError(f"the source does not define a class {class_name!r}")
+    return cls
+
+
+def _register(func, func_file, func_name, kind, methods, class_name=None):
     module = func_file[:-3] if func_file.endswith(".py") else func_file
+    if isinstance(func, str):
+        func = _from_source(func, func_file, class_name)
     if not inspect.isclass(func):
-        raise TypeError("pass the custom function as a class (source strings are not supported)")
+        raise TypeError("pass the custom function as a class or as class source code with class_name")
     for m in methods:
         if not callable(getattr(func, m, None)):
             raise TypeError(f"the {kind} class needs a `{m}` method")
@@ -32,12 +48,12 @@ def _register(func, func_file, func_name, kind, methods):
 
 
 def upload_custom_metric(func, func_file="metrics.py", func_name=None, class_name=None, source_provider=None):
-    return _register(func, func_file, func_name, "metrics", ("map", "reduce", "metric"))
+    return _register(func, func_file, func_name, "metrics", ("map", "reduce", "metric"), class_name)
 
 
 def upload_custom_distribution(func, func_file="distributions.py", func_name=None, class_name=None,
                                source_provider=None):
-    return _register(func, func_file, func_name, "distributions", ("link", "init", "gradient", "gamma"))
+    return _register(func, func_file, func_name, "distributions", ("link", "init", "gradient", "gamma"), class_name)
 
 
 def resolve(ref: str):
@@ -58,7 +74,12 @@ def custom_metric_value(ref: str, preds: np.ndarray, actual: np.ndarray, w=None,
     w = np.ones(n) if w is None else np.asarray(w, dtype=np.float64)
     o = np.zeros(n) if offset is None else np.asarray(offset, dtype=np.float64)
     try:                                    # vectorised: columns in, per-row state columns out, summed
-        st = obj.map(preds.T, actual[None, :], w, o, model)
+        st = [np.broadcast_to(np.asarray(s, dtype=np.float64), (n,)) for s in obj.map(preds.T, actual[None, :], w, o,
+                                                                                          model)]
+        if n >= 2:   # the column sum stands in for reduce only when reduce is element-wise addition
+            a, b = [float(s[0]) for s in st], [float(s[1]) for s in st]
+            if not np.allclose(np.asarray(obj.reduce(a, b), dtype=np.float64), np.add(a, b), rtol=1e-12, atol=0):
+                raise ValueError("non-additive reduce")
         state = [float(np.sum(s)) for s in st]
         if not all(np.isfinite(v) for v in state):
             raise ValueError("non-finite vectorised state")

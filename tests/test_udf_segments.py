@@ -60,6 +60,31 @@ def test_custom_metric_matches_mae(df, cls):
     assert tm["custom_metric_value"] == pytest.approx(tm["mae"], rel=1e-6)
 
 
+MAE_SRC = '''
+class CustomMaeFunc:
+    def map(self, pred, act, w, o, model):
+        return [abs(act[0] - pred[0]), 1]
+
+    def reduce(self, l, r):
+        return [l[0] + r[0], l[1] + r[1]]
+
+    def metric(self, l):
+        return l[0] / l[1]
+'''
+
+
+def test_custom_metric_from_source_string(df):
+    # h2o.py:upload_custom_metric string form: class source + class_name
+    ref = h2o.upload_custom_metric(MAE_SRC, class_name="CustomMaeFunc", func_name="mae_src")
+    assert ref == "python:mae_src=metrics.CustomMaeFuncWrapper"
+    m = H2OGradientBoostingEstimator(ntrees=5, seed=1, custom_metric_func=ref)
+    m.train(x=["a", "b", "seg"], y="r", training_frame=df)
+    tm = m._model.output["training_metrics"]
+    assert tm["custom_metric_value"] == pytest.approx(tm["mae"], rel=1e-6)
+    with pytest.raises(ValueError):
+        h2o.upload_custom_metric(MAE_SRC)
+
+
 def test_custom_distribution_equals_gaussian(df):
     ref = h2o.upload_custom_distribution(CustomGaussian, func_name="custom_gaussian")
     kw = dict(ntrees=6, max_depth=3, seed=1)
