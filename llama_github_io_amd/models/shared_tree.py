@@ -193,8 +193,9 @@ class SharedTreeTrainer:
         self.valid = valid
         built = start
         hprof = os.environ.get("H2O_HOST_PROF") == "1"    # host seconds per phase (launch-bound diagnosis)
-        ht = dict(prepare=0.0, build=0.0, update=0.0, drain=0.0)
+        ht = dict(prepare=0.0, build=0.0, update=0.0, drain=0.0, loop=0.0, build_max=0.0)
         for t in range(start, ntrees):
+            tl0 = time.perf_counter()
             feat_ok = self._tree_feature_mask(rng, F)
             for k in range(K):
                 h0 = time.perf_counter()
@@ -218,6 +219,7 @@ class SharedTreeTrainer:
                 if t >= start + 2:                   # skip first-launch module loads / allocations
                     ht["prepare"] += h1 - h0
                     ht["build"] += h2 - h1
+                    ht["build_max"] = max(ht["build_max"], h2 - h1)
                     ht["update"] += h3 - h2
             built = t + 1
             if not need_sync:
@@ -225,6 +227,8 @@ class SharedTreeTrainer:
                 self._drain(handles, forest, gains, ready_only=True)   # overlap host decode with GPU work
                 if t >= start + 2:
                     ht["drain"] += time.perf_counter() - h0
+            if t >= start + 2:
+                ht["loop"] += time.perf_counter() - tl0
             if need_sync:
                 self._drain(handles, forest, gains)
                 if interval and (built % interval == 0 or built == ntrees):
@@ -242,7 +246,8 @@ class SharedTreeTrainer:
         self._drain(handles, forest, gains)
         if hprof and built > start + 2:
             n = (built - start - 2) * K
-            print("[host-prof] us/tree " + " ".join(f"{k}={v / n * 1e6:.1f}" for k, v in ht.items()), flush=True)
+            print("[host-prof] us/tree " + " ".join(f"{k}={v / (1 if k.endswith('_max') else n) * 1e6:.1f}"
+                                                    for k, v in ht.items()), flush=True)
         if need_sync and (not history or history[-1]["number_of_trees"] != built):
             history.append(self._score_event(model, built, t_start))
         self._finish(model, built)

@@ -622,15 +622,7 @@ class GpuTreeBuilder:
         elif leaf_fn is not None:
             vals = leaf_fn(self.leafsum)
             self.av["leafval"].view(torch.float32)[: vals.numel()].copy_(vals.to(torch.float32))
-        # the tree's structure travels to pinned host memory asynchronously: the host decodes finished
-        # trees (pop_levels(ready_only=True)) while the GPU builds the next ones
-        host = self._pinned_pool.pop() if self._pinned_pool else torch.empty(self.arena.numel(), dtype=torch.uint8,
-                                                                               pin_memory=True)
-        host.copy_(self.arena, non_blocking=True)
-        ev = self._event_pool.pop() if self._event_pool else torch.cuda.Event()
-        ev.record()
-        self.history.append((host, ev))
-        return len(self.history) - 1
+        return self._snapshot()
 
     def _build_native(self, aux_static, feat_ok, k_cols, seed, leaf_fn, amax_bits, pk, leaf_native, s):
         """build() through the native launch plan: one host call per tree (single process) or one per
@@ -672,7 +664,9 @@ class GpuTreeBuilder:
 
     def _snapshot(self):
         # the tree's structure travels to pinned host memory asynchronously: the host decodes finished
-        # trees (pop_levels(ready_only=True)) while the GPU builds the next ones
+        # trees (pop_levels(ready_only=True)) while the GPU builds the next ones. MEASURED: moving the
+        # device-to-host copy to a side stream (device staging ring + stream events) made the host block
+        # in the launches (820 us/tree host, 1.09 vs 0.575 ms/tree at 1.375M rows): kept on the compute stream
         host = self._pinned_pool.pop() if self._pinned_pool else torch.empty(self.arena.numel(), dtype=torch.uint8,
                                                                                pin_memory=True)
         host.copy_(self.arena, non_blocking=True)
