@@ -24,7 +24,7 @@ __device__ __forceinline__ unsigned long long smix(unsigned long long x) {
 __device__ __forceinline__ float expc(float x) { return __expf(fminf(x, 80.f)); }
 
 __global__ __launch_bounds__(256) void k_gbm_step(
-    long long N, int dist, const float* __restrict__ y, const float* __restrict__ w, float* __restrict__ f,
+    long long N, long long row0, int dist, const float* __restrict__ y, const float* __restrict__ w, float* __restrict__ f,
     const float* __restrict__ vals, const int* __restrict__ leaf, float sample_rate, unsigned long long seed,
     float p1 /*tweedie power | quantile alpha | huber delta*/, float4* __restrict__ aux,
     unsigned* __restrict__ amax_bits /*[2*AMAX_SHARDS], |.| as uint bits, pre-zeroed*/) {
@@ -34,7 +34,9 @@ __global__ __launch_bounds__(256) void k_gbm_step(
     if (vals) { fi += vals[leaf[i]]; f[i] = fi; }
     float wi = w ? w[i] : 1.f;
     if (sample_rate < 1.f) {
-      const float u = (float)(smix(seed ^ (unsigned long long)i) >> 40) * (1.0f / 16777216.0f);
+      // keyed by the GLOBAL row index (row0 = this rank's first row): a row-sharded run samples exactly
+      // the rows of the single-GPU run
+      const float u = (float)(smix(seed ^ (unsigned long long)(row0 + i)) >> 40) * (1.0f / 16777216.0f);
       if (u >= sample_rate) wi = 0.f;
     }
     const float yi = y[i];
@@ -107,13 +109,13 @@ __global__ void k_add_leaf(long long N, float* __restrict__ f, int fstride, cons
 }
 
 extern "C" {
-int h2o_gbm_step(long long N, int dist, const void* y, const void* w, void* f, const void* vals, const void* leaf,
+int h2o_gbm_step(long long N, long long row0, int dist, const void* y, const void* w, void* f, const void* vals, const void* leaf,
                  float sample_rate, unsigned long long seed, float p1, void* aux, void* amax_bits, hipStream_t s) {
   const int blk = 256;
   long long grid = (N + blk - 1) / blk;
   if (grid > 2048) grid = 2048;
   if (grid < 1) grid = 1;
-  hipLaunchKernelGGL(k_gbm_step, dim3((unsigned)grid), dim3(blk), 0, s, N, dist, (const float*)y, (const float*)w,
+  hipLaunchKernelGGL(k_gbm_step, dim3((unsigned)grid), dim3(blk), 0, s, N, row0, dist, (const float*)y, (const float*)w,
                      (float*)f, (const float*)vals, (const int*)leaf, sample_rate, seed, p1, (float4*)aux,
                      (unsigned*)amax_bits);
   return (int)hipGetLastError();

@@ -24,6 +24,7 @@ import numpy as np
 import torch
 
 from .core import dkv
+from .parallel import dframe
 
 _NUMERIC = ("real", "int", "time")
 
@@ -204,9 +205,15 @@ class H2OFrame:
     def __init__(self, python_obj=None, destination_frame=None, header=0, separator=",", column_names=None,
                  column_types=None, na_strings=None, skipped_columns=None):
         self._cols: "OrderedDict[str, Column]" = OrderedDict()
+        self._shard = None
         self.frame_id = destination_frame or dkv.new_key("py_frame")
         if python_obj is not None:
             self._from_python(python_obj, column_names, column_types)
+            if dframe.active() and not dframe.in_method() and self._cols and self._nlocal > 1:
+                # a user-built frame under torchrun: every rank was handed the same object (SPMD); keep
+                # this rank's row range (ParseDataset distributes rows the same way)
+                cols, self._shard = dframe.shard_columns(list(self._cols.values()), self._nlocal)
+                self._cols = OrderedDict((c.name, c) for c in cols)
         dkv.put(self.frame_id, self)
 
     # ---- construction
@@ -214,6 +221,7 @@ class H2OFrame:
     def _from_columns(cls, cols, frame_id=None) -> "H2OFrame":
         f = cls.__new__(cls)
         f._cols = OrderedDict()
+        f._shard = dframe.current_ctx()
         for c in cols:
             name = c.name
             k = 0
@@ -323,7 +331,26 @@ class H2OFrame:
 
     @property
     def nrows(self):
+        if self._shard is not None:
+            return self._shard.n_global
+        return self._nlocal
+
+    @property
+    def _nlocal(self):
+        """Rows held by this rank (== nrows unless the frame is row-sharded)."""
         return next(iter(self._cols.values())).n if self._cols else 0
+
+    @property
+    def is_sharded(self):
+        return self._shard is not None
+
+    def gather(self):
+        """Replicated copy of a sharded frame (every rank gets every row); self if not sharded."""
+        return dframe.gather_frame(self)
+
+    def reshard(self):
+        """Sharded copy of a replicated frame under a multi-rank cloud (self otherwise)."""
+        return dframe.shard_frame(self)
 
     nrow = nrows
 
@@ -412,9 +439,12 @@ class H2OFrame:
             return fr._rows(rows)
         if isinstance(item, H2OFrame):  # boolean mask
             return self._rows(item)
-        return H2OFrame._from_columns([self._col(n).copy() if False else self._col(n) for n in self._resolve(item)])
+        with dframe.shard_ctx(self._shard):
+            return H2OFrame._from_columns([self._col(n) for n in self._resolve(item)])
 
     def _rows(self, rows):
+        if self._shard is not None or (isinstance(rows, H2OFrame) and rows._shard is not None):
+            return self._rows_sharded(rows)
         n = self.nrows
         dev = engine_device()
         if isinstance(rows, H2OFrame):
@@ -430,8 +460,56 @@ class H2OFrame:
             idx = torch.as_tensor(np.asarray(rows), device=dev).long()
         return H2OFrame._from_columns([c.take(idx) for c in self._cols.values()])
 
+    def _rows_sharded(self, rows):
+        """Row selection on a sharded frame: masks and ascending global indices / slices stay local
+        (the new shard's offsets come from one all-gather of the kept counts); anything that reorders
+        rows runs on the gathered frame."""
+        me = self
+        if me._shard is None:
+            me = dframe.shard_frame(me) if me.nrows == rows.nrows else me
+        sh = me._shard
+        dev = engine_device()
+        local = None
+        if isinstance(rows, H2OFrame):
+            if rows._shard != sh:
+                if rows._shard is None and rows.nrows == me.nrows:
+                    rows = dframe.shard_frame(rows)
+                else:
+                    return dframe.gather_frame(me)._rows(dframe.gather_frame(rows))
+            m = rows._col(0).as_float()
+            local = torch.nonzero(torch.nan_to_num(m, nan=0.0) != 0).reshape(-1)
+        elif isinstance(rows, torch.Tensor) and rows.dtype == torch.bool and rows.numel() == sh.n_local:
+            local = torch.nonzero(rows).reshape(-1).to(dev)
+        elif isinstance(rows, slice) and (rows.step or 1) > 0:
+            g = range(sh.n_global)[rows]
+            lo, hi = max(g.start, sh.offset), min(g.stop, sh.offset + sh.n_local)
+            st = g.step
+            first = lo + ((g.start - lo) % st) if lo > g.start else g.start
+            local = torch.arange(first - sh.offset, max(hi - sh.offset, first - sh.offset), st, device=dev)
+        elif isinstance(rows, (int, np.integer, list, np.ndarray)) or (isinstance(rows, torch.Tensor) and rows.dtype != torch.bool):
+            idx = np.atleast_1d(rows.cpu().numpy() if isinstance(rows, torch.Tensor) else np.asarray(rows)).astype(np.int64)
+            idx = np.where(idx < 0, idx + sh.n_global, idx)
+            if idx.size > 1 and np.any(np.diff(idx) <= 0):
+                return dframe.gather_frame(me)._rows(idx)
+            sel = idx[(idx >= sh.offset) & (idx < sh.offset + sh.n_local)] - sh.offset
+            local = torch.as_tensor(sel, device=dev)
+        else:
+            return dframe.gather_frame(me)._rows(rows)
+        with dframe.shard_ctx(dframe.make_shard(int(local.numel()))):
+            return H2OFrame._from_columns([c.take(local) for c in me._cols.values()])
+
     def __setitem__(self, key, value):
-        n = self.nrows if self._cols else None
+        n = self._nlocal if self._cols else None
+        if self._shard is not None and isinstance(value, H2OFrame) and value._shard is None and \
+                value.nrows == self.nrows and self.nrows > 1:
+            value = dframe.shard_frame(value)
+        if self._shard is not None and isinstance(key, tuple) and isinstance(key[0], H2OFrame) and \
+                key[0]._shard is None and key[0].nrows == self.nrows:
+            key = (dframe.shard_frame(key[0]), key[1])
+        if self._shard is not None and not isinstance(value, (H2OFrame, int, float, str)) and value is not None \
+                and hasattr(value, "__len__") and len(value) == self.nrows:
+            lo, hi = dframe.bounds(self.nrows)
+            value = value[lo:hi]
         dev = engine_device()
         if isinstance(key, tuple):  # (row mask, col) assignment
             rows, col = key
@@ -468,19 +546,25 @@ class H2OFrame:
 
     def drop(self, index, axis=1):
         if axis == 0:
+            if self._shard is not None:
+                return dframe.gather_frame(self).drop(index, axis)
             keep = torch.ones(self.nrows, dtype=torch.bool, device=engine_device())
             keep[torch.as_tensor(np.atleast_1d(index), device=keep.device).long()] = False
             return self._rows(keep)
         names = set(self._resolve(index))
-        return H2OFrame._from_columns([c for n, c in self._cols.items() if n not in names])
+        with dframe.shard_ctx(self._shard):
+            return H2OFrame._from_columns([c for n, c in self._cols.items() if n not in names])
 
     def pop(self, i):
         n = self._resolve(i)[0]
         c = self._cols.pop(n)
-        return H2OFrame._from_columns([c])
+        with dframe.shard_ctx(self._shard):
+            return H2OFrame._from_columns([c])
 
     # ---- conversion
     def as_data_frame(self, use_pandas=True, header=True, use_multi_thread=False):
+        if self._shard is not None:
+            return dframe.gather_frame(self).as_data_frame(use_pandas, header, use_multi_thread)
         import pandas as pd
         data = OrderedDict()
         for n, c in self._cols.items():
@@ -503,12 +587,18 @@ class H2OFrame:
         return self.as_data_frame().to_csv(index=False)
 
     def head(self, rows=10, cols=200):
-        return self[: min(rows, self.nrows), :][self.names[:cols]]
+        out = self[: min(rows, self.nrows), :][self.names[:cols]]
+        return dframe.gather_frame(out)
 
     def tail(self, rows=10, cols=200):
-        return self[max(0, self.nrows - rows):, :][self.names[:cols]]
+        out = self[max(0, self.nrows - rows):, :][self.names[:cols]]
+        return dframe.gather_frame(out)
 
     def __repr__(self):
+        if self._shard is not None:      # no collectives in repr (a rank may print alone)
+            sh = self._shard
+            return (f"<H2OFrame {self.frame_id} [{sh.n_global} rows x {self.ncols} columns], row-sharded: this rank "
+                    f"holds rows [{sh.offset}, {sh.offset + sh.n_local})>")
         try:
             return repr(self.head().as_data_frame()) + f"\n\n[{self.nrows} rows x {self.ncols} columns]"
         except Exception:  # noqa: BLE001
@@ -520,15 +610,19 @@ class H2OFrame:
     # ---- type conversion
     def asfactor(self):
         cols = []
+        sharded = self._shard is not None
         for c in self._cols.values():
             if c.type == "enum":
                 cols.append(c)
             elif c.type == "string":
-                cols.append(_enum_from_values(c.name, c.strings, engine_device()))
+                e = _enum_from_values(c.name, c.strings, engine_device())
+                if sharded:                      # ParseDataset-style domain unification over the ranks
+                    e.data, e.domain = dframe.unify_domain(e.data, e.domain, _level_key)
+                cols.append(e)
             else:
-                v = c.data.cpu().numpy()
-                cols.append(_enum_from_values(c.name, v.astype(object), engine_device()) if False else _num_to_enum(c))
-        return H2OFrame._from_columns(cols)
+                cols.append(_num_to_enum(c, sharded))
+        with dframe.shard_ctx(self._shard):
+            return H2OFrame._from_columns(cols)
 
     def asnumeric(self):
         cols = []
@@ -584,7 +678,24 @@ class H2OFrame:
     def _num(self, col=0):
         return self._col(col).as_float()
 
+    def _moments(self):
+        """Per-column global moments (one all-gather of per-rank partials when sharded)."""
+        return [dframe.moments(c.as_float(), self._shard is not None) for c in self._cols.values()]
+
     def _reduce(self, fn, na_rm=True, return_frame=False):
+        if self._shard is not None:
+            kind = {torch.sum: "sum", torch.mean: "mean", torch.max: "max", torch.min: "min"}.get(fn)
+            if kind is None:
+                return dframe.gather_frame(self)._reduce(fn, na_rm, return_frame)
+            out = []
+            for m in self._moments():
+                if not na_rm and m["nas"] > 0:
+                    out.append(float("nan"))
+                elif m["n"] == 0:
+                    out.append(float("nan") if kind != "sum" else 0.0)
+                else:
+                    out.append(float(m[kind]))
+            return out if (len(out) > 1 or return_frame) else out[0]
         out = []
         for c in self._cols.values():
             v = c.as_float()
@@ -612,11 +723,18 @@ class H2OFrame:
         return self._reduce(torch.min)
 
     def sd(self, na_rm=True):
+        if self._shard is not None:
+            return [math.sqrt(m["m2"] / (m["n"] - 1)) if m["n"] > 1 else float("nan") for m in self._moments()]
         return self._reduce(lambda v: torch.std(v, unbiased=True), na_rm, True)
 
     std = sd
 
     def var(self, y=None, na_rm=True, use=None):
+        if self._shard is not None and y is None and self.ncols == 1:
+            m = self._moments()[0]
+            return m["m2"] / (m["n"] - 1) if m["n"] > 1 else float("nan")
+        if self._shard is not None or (y is not None and y._shard is not None):
+            return dframe.gather_frame(self).var(dframe.gather_frame(y), na_rm, use)
         if y is None and self.ncols == 1:
             return self._reduce(lambda v: torch.var(v, unbiased=True))
         X = self.as_tensor(dtype=torch.float64)
@@ -628,16 +746,21 @@ class H2OFrame:
         return self._reduce(lambda v: torch.quantile(v, 0.5))
 
     def nacnt(self):
-        return [int(c.isna().sum()) for c in self._cols.values()]
+        cnt = [int(c.isna().sum()) for c in self._cols.values()]
+        if self._shard is not None:
+            cnt = [int(x) for x in coll_all_reduce_np(cnt)]
+        return cnt
 
     def isna(self):
         return H2OFrame._from_columns([Column(f"isNA({c.name})", "int", c.isna().double()) for c in self._cols.values()])
 
     def any(self):
-        return bool(torch.nan_to_num(self._num(), nan=0).ne(0).any())
+        r = bool(torch.nan_to_num(self._num(), nan=0).ne(0).any())
+        return bool(coll_all_reduce_np([r])[0] > 0) if self._shard is not None else r
 
     def all(self):
-        return bool(torch.nan_to_num(self._num(), nan=1).ne(0).all())
+        r = bool(torch.nan_to_num(self._num(), nan=1).ne(0).all())
+        return bool(coll_all_reduce_np([not r])[0] == 0) if self._shard is not None else r
 
     def quantile(self, prob=None, combine_method="interpolate", weights_column=None):
         """Column quantiles (``hex/quantile/Quantile.java``): combine_method interpolate | average | low |
@@ -657,13 +780,16 @@ class H2OFrame:
 
     def summary(self, return_data=False):
         out = {}
+        sharded = self._shard is not None
         for n, c in self._cols.items():
             d = dict(type=c.type, missing=int(c.isna().sum()))
+            if sharded:
+                d["missing"] = int(coll_all_reduce_np([d["missing"]])[0])
             if c.type in _NUMERIC:
-                v = c.data[~torch.isnan(c.data)]
-                if v.numel():
-                    d.update(mean=float(v.mean()), sd=float(v.std()) if v.numel() > 1 else 0.0, min=float(v.min()),
-                             max=float(v.max()), zeros=int((v == 0).sum()))
+                m = dframe.moments(c.data, sharded)
+                if m["n"]:
+                    d.update(mean=m["mean"], sd=math.sqrt(m["m2"] / (m["n"] - 1)) if m["n"] > 1 else 0.0, min=m["min"],
+                             max=m["max"], zeros=int(m["zeros"]))
             elif c.type == "enum":
                 d.update(cardinality=len(c.domain))
             out[n] = d
@@ -824,6 +950,25 @@ class H2OFrame:
     def impute(self, column=-1, method="mean", combine_method="interpolate", by=None, group_by_frame=None, values=None):
         targets = self.names if column in (-1, None) else self._resolve(column)
         res = []
+        if self._shard is not None:
+            # global statistics (collectives), applied to each shard in place
+            for n in targets:
+                c = self._cols[n]
+                if c.type == "enum":
+                    cnt = torch.bincount(c.data[c.data >= 0].long(), minlength=len(c.domain)).double().cpu().numpy()
+                    mode = int(np.argmax(coll_all_reduce_np(cnt)))
+                    c.data = torch.where(c.data < 0, torch.full_like(c.data, mode), c.data)
+                    res.append(mode)
+                elif c.type in _NUMERIC:
+                    if method == "mean":
+                        fill = dframe.moments(c.data, True)["mean"]
+                    else:
+                        g = dframe.gather_tensor(c.data)
+                        gv = g[~torch.isnan(g)]
+                        fill = float(torch.quantile(gv, 0.5)) if method != "mode" else float(torch.mode(gv).values)
+                    c.data = torch.nan_to_num(c.data, nan=fill)
+                    res.append(fill)
+            return res
         for n in targets:
             c = self._cols[n]
             if c.type == "enum":
@@ -840,6 +985,16 @@ class H2OFrame:
 
     def scale(self, center=True, scale=True):
         cols = []
+        if self._shard is not None:
+            for c, m in zip(self._cols.values(), self._moments()):
+                v = c.as_float()
+                if center:
+                    v = v - m["mean"]
+                if scale:
+                    v = v / math.sqrt(m["m2"] / (m["n"] - 1))
+                cols.append(Column(c.name, "real", v))
+            with dframe.shard_ctx(self._shard):
+                return H2OFrame._from_columns(cols)
         for c in self._cols.values():
             v = c.as_float()
             if center:
@@ -940,7 +1095,7 @@ class H2OFrame:
         cols = list(self._cols.values())
         for o in others:
             if isinstance(o, (int, float)):
-                cols.append(Column(f"C{len(cols) + 1}", "real", torch.full((self.nrows,), float(o), dtype=torch.float64, device=engine_device())))
+                cols.append(Column(f"C{len(cols) + 1}", "real", torch.full((self._nlocal,), float(o), dtype=torch.float64, device=engine_device())))
             else:
                 cols += list(o._cols.values())
         return H2OFrame._from_columns([Column(c.name, c.type, c.data, c.domain, c.strings) for c in cols])
@@ -987,10 +1142,17 @@ class H2OFrame:
         from .frame_ops import GroupBy
         return GroupBy(self, by)
 
+    def _row_uniform(self, seed):
+        """Per-row uniforms keyed by the GLOBAL row index: the same draw for a row however the frame is
+        sharded (a SPMD program gets the same split on 1 or N ranks)."""
+        from .parallel import collectives as coll
+        s = int(seed) if seed not in (None, -1) else int(coll.broadcast_object(np.random.randint(1 << 30)))
+        off = self._shard.offset if self._shard is not None else 0
+        return coll.row_uniform(s, 0x5EED, off, self._nlocal, engine_device())
+
     def split_frame(self, ratios=None, destination_frames=None, seed=None):
         ratios = ratios or [0.75]
-        g = torch.Generator().manual_seed(int(seed) if seed not in (None, -1) else np.random.randint(1 << 30))
-        r = torch.rand(self.nrows, generator=g, dtype=torch.float64).to(engine_device())
+        r = self._row_uniform(seed)
         cuts = np.cumsum([0.0] + list(ratios) + [1.0 - sum(ratios)])
         out = []
         for i in range(len(cuts) - 1):
@@ -1003,15 +1165,18 @@ class H2OFrame:
         return out
 
     def runif(self, seed=None):
-        g = torch.Generator().manual_seed(int(seed) if seed not in (None, -1) else np.random.randint(1 << 30))
-        return H2OFrame._from_columns([Column("rnd", "real", torch.rand(self.nrows, generator=g, dtype=torch.float64).to(engine_device()))])
+        with dframe.shard_ctx(self._shard):
+            return H2OFrame._from_columns([Column("rnd", "real", self._row_uniform(seed))])
 
     def kfold_column(self, n_folds=3, seed=-1):
-        g = torch.Generator().manual_seed(int(seed) if seed not in (None, -1) else np.random.randint(1 << 30))
-        return H2OFrame._from_columns([Column("fold", "int", torch.randint(0, n_folds, (self.nrows,), generator=g).double().to(engine_device()))])
+        u = self._row_uniform(seed)
+        with dframe.shard_ctx(self._shard):
+            return H2OFrame._from_columns([Column("fold", "int", torch.floor(u * n_folds).clamp(max=n_folds - 1))])
 
     def modulo_kfold_column(self, n_folds=3):
-        return H2OFrame._from_columns([Column("fold", "int", (torch.arange(self.nrows, device=engine_device()) % n_folds).double())])
+        off = self._shard.offset if self._shard is not None else 0
+        with dframe.shard_ctx(self._shard):
+            return H2OFrame._from_columns([Column("fold", "int", (torch.arange(off, off + self._nlocal, device=engine_device()) % n_folds).double())])
 
     def stratified_kfold_column(self, n_folds=3, seed=-1):
         c = self._col(0)
@@ -1060,7 +1225,7 @@ class H2OFrame:
         return H2OFrame(df.drop_duplicates(subset=self._resolve(columns), keep=keep).reset_index(drop=True))
 
     def na_omit(self):
-        m = torch.ones(self.nrows, dtype=torch.bool, device=engine_device())
+        m = torch.ones(self._nlocal, dtype=torch.bool, device=engine_device())
         for c in self._cols.values():
             m &= ~c.isna().to(m.device)
         return self._rows(m)
@@ -1099,7 +1264,7 @@ class H2OFrame:
     # ---- model adaptation (Model.adaptTestForTrain)
     def model_matrix(self, info, device=None):
         device = device or engine_device()
-        N = self.nrows
+        N = self._nlocal
         X = torch.empty(info.F, N, dtype=torch.float32, device=device)
         for j, n in enumerate(info.x):
             if n not in self._cols:
@@ -1130,16 +1295,24 @@ class H2OFrame:
         return self._cols[info.weights].as_float().to(device=device or engine_device(), dtype=torch.float32)
 
 
+def coll_all_reduce_np(a):
+    from .parallel import collectives as coll
+    if not coll.world_active():
+        return np.asarray(a, dtype=np.float64)
+    with_ = coll.all_gather_object(np.asarray(a, dtype=np.float64))
+    return np.sum(with_, axis=0)
+
+
 def _op_operand(c: Column, other: Column):
     if c.type == "enum" and other.type == "enum" and c.domain != other.domain:
         return c.data.double()
     return c.as_float()
 
 
-def _num_to_enum(c: Column) -> Column:
+def _num_to_enum(c: Column, sharded: bool = False) -> Column:
     v = c.data
     ok = ~torch.isnan(v)
-    u = torch.unique(v[ok])
+    u = dframe.global_unique(v) if sharded else torch.unique(v[ok])
     dom = [_level_str(x) for x in u.cpu().numpy().tolist()]
     codes = torch.full(v.shape, -1, dtype=torch.int32, device=v.device)
     codes[ok] = torch.bucketize(v[ok], u).to(torch.int32)
@@ -1163,3 +1336,7 @@ def _remap_codes(c: Column, domain, device) -> torch.Tensor:
     out = np.array([lut.get(_level_str(v) if v is not None and not (isinstance(v, float) and math.isnan(v)) else None, np.nan)
                     for v in vals], dtype=np.float32)
     return torch.as_tensor(out, device=device)
+
+
+# distribution class of every H2OFrame method (row-local / collective / gathered): parallel/dframe.py
+dframe.install(H2OFrame)

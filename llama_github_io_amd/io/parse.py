@@ -147,7 +147,12 @@ def _sep_byte(sep) -> bytes:
 
 
 def _parse_csv_bytes(buf: bytes, sep, header, column_names, column_types, na_strings, device=None,
-                     skipped_columns=None) -> H2OFrame:
+                     skipped_columns=None, sharded=False, names_from=None) -> H2OFrame:
+    """Parse one CSV buffer. ``sharded``: ``buf`` is this rank's byte range of a file parsed by every rank
+    (``ParseDataset``): column kinds, int-ness and categorical domains are agreed over the ranks with
+    three small all-gathers, and the frame comes back row-sharded. ``names_from``: column names when
+    this chunk carries no header line (ranks > 0)."""
+    from ..parallel import collectives as coll, dframe
     rt = _rt()
     device = device or engine_device()
     if sep is None:
@@ -162,29 +167,39 @@ def _parse_csv_bytes(buf: bytes, sep, header, column_names, column_types, na_str
         for c in range(nc):
             k = rt.h2o_csv_header(h, c, sbuf, 4096) if rt.h2o_csv_has_header(h) else -1
             names.append(sbuf.value.decode("utf-8", "replace").strip().strip('"') if k >= 0 else f"C{c + 1}")
+        if names_from is not None:
+            names = list(names_from) + names[len(names_from):]
         if column_names:
             names = list(column_names) + names[len(column_names):]
+        if sharded:
+            nc = max(int(x) for x in coll.all_gather_object(nc))
+            names = names + [f"C{c + 1}" for c in range(len(names), nc)]
         ctypes_ = _normalize_types(column_types, names)
         na_set = _na_sets(na_strings, names)
         skip = set(skipped_columns or [])
         cols = []
         num = np.empty(n, dtype=np.float64)
         kind = np.empty(n, dtype=np.uint8)
+        counts = np.array([[rt.h2o_csv_count(h, c, 1), rt.h2o_csv_count(h, c, 2)] if c < rt.h2o_csv_ncols(h) else [0, 0]
+                           for c in range(nc)], dtype=np.float64).reshape(nc, 2)
+        if sharded:     # ParseSetup's column-kind vote over the whole file, not one chunk
+            counts = np.sum(coll.all_gather_object(counts), axis=0)
+        want = []
         for c in range(nc):
-            if c in skip or names[c] in skip:
-                continue
             forced = ctypes_.get(names[c])
-            rt.h2o_csv_get(h, c, num.ctypes.data, kind.ctypes.data, None, None)
-            n_num = rt.h2o_csv_count(h, c, 1)
-            n_txt = rt.h2o_csv_count(h, c, 2)
-            nas = na_set.get(names[c])
-            want_text = forced in ("enum", "string") or (forced is None and n_txt > n_num) or bool(nas)
-            if want_text:
-                codes = np.empty(n, dtype=np.int32)
+            want.append(forced in ("enum", "string") or (forced is None and counts[c, 1] > counts[c, 0]) or
+                        bool(na_set.get(names[c])))
+        doms = {}
+        codes_of = {}
+        for c in range(nc):
+            if c in skip or names[c] in skip or not want[c]:
+                continue
+            codes = np.full(n, -1, dtype=np.int32)
+            dom = []
+            if c < rt.h2o_csv_ncols(h) and n > 0:
                 d = rt.h2o_csv_domain(h, buf, c, codes.ctypes.data)
                 try:
                     L = rt.h2o_domain_size(d)
-                    dom = []
                     for k in range(L):
                         ln = rt.h2o_domain_level(d, k, sbuf, 4096)
                         if ln >= 4096:
@@ -195,6 +210,30 @@ def _parse_csv_bytes(buf: bytes, sep, header, column_names, column_types, na_str
                             dom.append(sbuf.value.decode("utf-8", "replace"))
                 finally:
                     rt.h2o_domain_free(d)
+            doms[c], codes_of[c] = dom, codes
+        if sharded:     # categorical domain unification: sorted union of every rank's levels
+            alld = coll.all_gather_object(doms)
+            for c in doms:
+                glob = sorted(set().union(*[set(a.get(c, [])) for a in alld]))
+                if glob != doms[c]:
+                    lut = {v: i for i, v in enumerate(glob)}
+                    m = np.array([lut[v] for v in doms[c]] + [-1], dtype=np.int32)
+                    codes_of[c] = m[np.where(codes_of[c] < 0, len(doms[c]), codes_of[c])]
+                    doms[c] = glob
+        num_int = {}
+        for c in range(nc):
+            if c in skip or names[c] in skip:
+                continue
+            forced = ctypes_.get(names[c])
+            if c < rt.h2o_csv_ncols(h):
+                rt.h2o_csv_get(h, c, num.ctypes.data, kind.ctypes.data, None, None)
+            else:
+                num[:] = np.nan
+            nas = na_set.get(names[c])
+            want_text = want[c]
+            if want_text:
+                codes, dom = codes_of[c], doms[c]
+                L = len(dom)
                 if nas:
                     bad = np.array([s in nas for s in dom] + [True], dtype=bool)
                     codes = np.where(bad[np.where(codes < 0, L, codes)], -1, codes).astype(np.int32)
@@ -215,10 +254,97 @@ def _parse_csv_bytes(buf: bytes, sep, header, column_names, column_types, na_str
                     cols.append(Column(names[c], "time", torch.as_tensor(vals, device=device)))
                 else:
                     t = forced if forced in ("int", "real") else _int_or_real(vals)
+                    num_int[len(cols)] = t == "int"
                     cols.append(Column(names[c], t, torch.as_tensor(vals, device=device)))
+        if sharded:
+            # int vs real is a property of the whole column: real on any rank -> real everywhere
+            agree = coll.all_gather_object(num_int)
+            for i in num_int:
+                if not all(a.get(i, True) for a in agree):
+                    cols[i].type = "real"
+            with dframe.shard_ctx(dframe.make_shard(n)):
+                return H2OFrame._from_columns(cols)
         return H2OFrame._from_columns(cols)
     finally:
         rt.h2o_csv_free(h)
+
+
+def _byte_range(path: str, rank: int, world: int) -> bytes:
+    """This rank's whole lines of an uncompressed file: the lines that START in
+    [rank*S/W, (rank+1)*S/W) (the first line belongs to rank 0), read with two seeks."""
+    size = os.path.getsize(path)
+    lo, hi = rank * size // world, (rank + 1) * size // world
+
+    def line_start(f, pos):
+        if pos == 0:
+            return 0
+        f.seek(pos - 1)
+        while True:
+            chunk = f.read(1 << 16)
+            if not chunk:
+                return size
+            k = chunk.find(b"\n")
+            if k >= 0:
+                return pos - 1 + k + 1
+            pos += len(chunk)
+    with open(path, "rb") as f:
+        a = line_start(f, lo)
+        b = line_start(f, hi) if hi < size else size
+        if b <= a:
+            return b""
+        f.seek(a)
+        return f.read(b - a)
+
+
+def _split_lines(buf: bytes, rank: int, world: int) -> bytes:
+    """In-memory version of :func:`_byte_range` for decompressed buffers."""
+    size = len(buf)
+
+    def line_start(pos):
+        if pos == 0:
+            return 0
+        k = buf.find(b"\n", pos - 1)
+        return size if k < 0 else k + 1
+    a = line_start(rank * size // world)
+    b = line_start((rank + 1) * size // world) if rank + 1 < world else size
+    return buf[a:b] if b > a else b""
+
+
+def _parse_csv_distributed(path, sep, header, column_names, column_types, na_strings, skipped_columns,
+                           markers=None) -> H2OFrame:
+    """``ParseDataset`` over the ranks: every rank guesses the setup from the same file head, parses its
+    own byte range (plain files are read with seeks, never whole), then the ranks agree on the column
+    kinds and domains (:func:`_parse_csv_bytes` with ``sharded=True``)."""
+    from ..parallel import collectives as coll
+    rt = _rt()
+    r, w = coll.rank(), coll.world()
+    plain = not (path.endswith(".gz") or path.endswith(".zip")) and not markers
+    if plain:
+        with open(path, "rb") as f:
+            head = f.read(1 << 16)
+    else:
+        whole = _read_bytes(path)
+        if markers:
+            whole = b"\n".join(ln for ln in whole.split(b"\n") if not any(ln.startswith(m.encode()) for m in markers))
+        head = whole[: 1 << 16]
+    head = head[: head.rfind(b"\n") + 1] or head
+    if sep is None:
+        sep = rt.h2o_csv_guess_sep(head, len(head)).decode("latin-1")
+    hdr = {1: 1, -1: 0, 0: -1}.get(int(header) if header is not None else 0, -1)
+    hh = rt.h2o_csv_parse(head, len(head), _sep_byte(sep), hdr, b'"', 0)
+    try:
+        has_header = bool(rt.h2o_csv_has_header(hh))
+        sbuf = ctypes.create_string_buffer(4096)
+        names = []
+        for c in range(rt.h2o_csv_ncols(hh)):
+            k = rt.h2o_csv_header(hh, c, sbuf, 4096) if has_header else -1
+            names.append(sbuf.value.decode("utf-8", "replace").strip().strip('"') if k >= 0 else f"C{c + 1}")
+    finally:
+        rt.h2o_csv_free(hh)
+    chunk = _byte_range(path, r, w) if plain else _split_lines(whole, r, w)
+    my_header = 1 if (r == 0 and has_header) else -1
+    return _parse_csv_bytes(chunk, sep, my_header, column_names, column_types, na_strings,
+                            skipped_columns=skipped_columns, sharded=True, names_from=names)
 
 
 def _isnum(s: str) -> bool:
@@ -367,9 +493,20 @@ def import_file(path=None, destination_frame=None, parse=True, header=0, sep=Non
     if not files:
         raise FileNotFoundError(f"no files match {path}")
     frames = []
+    from ..parallel import dframe
     for i, f in enumerate(files):
-        buf = _read_bytes(f)
-        ptype = guess_parse_type(f, buf[:4096])
+        dist_parse = dframe.active() and not dframe.in_method()
+        if dist_parse:
+            with open(f, "rb") as fh:
+                head = fh.read(4096)
+            if f.endswith(".gz"):
+                head = _read_bytes(f)[:4096]
+            ptype = guess_parse_type(f, head)
+            if ptype != "CSV":
+                dist_parse = False
+        if not dist_parse or ptype != "CSV":
+            buf = _read_bytes(f)
+            ptype = guess_parse_type(f, buf[:4096])
         if ptype == "SVMLight":
             fr = parse_svmlight(buf)
         elif ptype == "ARFF":
@@ -388,6 +525,13 @@ def import_file(path=None, destination_frame=None, parse=True, header=0, sep=Non
                 import pyarrow.orc as po
                 fr = H2OFrame(po.ORCFile(io.BytesIO(buf)).read().to_pandas())
         else:
+            if dist_parse:
+                fr = _parse_csv_distributed(f, sep, header, col_names, col_types, na_strings, skipped_columns,
+                                            custom_non_data_line_markers)
+                if i > 0 and frames and fr.names != frames[0].names:
+                    fr.names = frames[0].names
+                frames.append(fr)
+                continue
             if custom_non_data_line_markers:
                 keep = [ln for ln in buf.split(b"\n") if not any(ln.startswith(m.encode()) for m in custom_non_data_line_markers)]
                 buf = b"\n".join(keep)
@@ -396,13 +540,42 @@ def import_file(path=None, destination_frame=None, parse=True, header=0, sep=Non
             if i > 0 and frames and fr.names != frames[0].names:
                 fr.names = frames[0].names
         frames.append(fr)
-    out = frames[0] if len(frames) == 1 else frames[0].rbind(frames[1:])
+    if dframe.active() and not dframe.in_method():
+        # non-CSV formats are read whole on every rank: keep this rank's rows
+        frames = [fr if fr._shard is not None else dframe.shard_frame(fr) for fr in frames]
+    out = frames[0] if len(frames) == 1 else _rbind_sharded(frames)
     dest = destination_frame or _dest_name(files[0])
     from ..core import dkv
     dkv.remove(out.frame_id) if out.frame_id != dest and dkv.contains(out.frame_id) else None
     out.frame_id = dest
     dkv.put(dest, out)
     return out
+
+
+def _rbind_sharded(frames):
+    """Row-bind per-file frames. Sharded parts are bound rank-locally (each rank keeps its own rows of
+    every file), so a multi-file import stays sharded; domains are unified over files and ranks."""
+    if all(f._shard is None for f in frames):
+        return frames[0].rbind(frames[1:])
+    from ..parallel import dframe
+    cols = []
+    for n, c in frames[0]._cols.items():
+        parts = [f._col(n) for f in frames]
+        if c.type == "enum":
+            dom = sorted(set().union(*[p.domain for p in parts]))
+            lut = {s: i for i, s in enumerate(dom)}
+            codes = []
+            for p in parts:
+                m = torch.tensor([lut[s] for s in p.domain] + [-1], dtype=torch.int32, device=p.data.device)
+                codes.append(m[torch.where(p.data < 0, torch.full_like(p.data, len(p.domain)), p.data).long()])
+            cols.append(Column(n, "enum", torch.cat(codes), dom))
+        elif c.type == "string":
+            cols.append(Column(n, "string", strings=np.concatenate([p.strings for p in parts])))
+        else:
+            cols.append(Column(n, c.type if all(p.type == c.type for p in parts) else "real",
+                               torch.cat([p.as_float() for p in parts])))
+    with dframe.shard_ctx(dframe.make_shard(cols[0].n if cols else 0)):
+        return H2OFrame._from_columns(cols)
 
 
 def upload_file(path, destination_frame=None, header=0, sep=None, col_names=None, col_types=None, na_strings=None,

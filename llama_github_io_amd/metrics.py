@@ -18,6 +18,36 @@ THRESHOLD_CRITERIA = ("f1", "f2", "f0point5", "accuracy", "precision", "recall",
                       "absolute_mcc", "min_per_class_accuracy", "mean_per_class_accuracy")
 
 
+def _sharded_rows(*row_args):
+    """Metrics of row-sharded predictions: all-gather the per-row arguments named in ``row_args``
+    (rank order) and compute once on the full rows — exact, and bit-identical to the single-process
+    metrics (the reference merges fixed-bin AUC2 histograms instead; the gathered predictions are a
+    few bytes per row, small next to training traffic)."""
+    import functools
+    import inspect
+
+    def deco(fn):
+        sig = inspect.signature(fn)
+
+        @functools.wraps(fn)
+        def w(*args, **kwargs):
+            from .parallel import collectives as coll
+            if not coll.is_dist():
+                return fn(*args, **kwargs)
+            b = sig.bind(*args, **kwargs)
+            b.apply_defaults()
+            for name in row_args:
+                t = b.arguments.get(name)
+                if isinstance(t, torch.Tensor):
+                    dev = t.device
+                    g = coll.all_gather_cat(t.contiguous().cpu() if coll.comm_device().type == "cpu" else t.contiguous(), 0)
+                    b.arguments[name] = g.to(dev)
+            with coll.replicated():
+                return fn(*b.args, **b.kwargs)
+        return w
+    return deco
+
+
 class ModelMetrics(dict):
     """dict with attribute access; ``model_category`` names the family."""
 
@@ -50,6 +80,7 @@ def _w(w, n, device):
     return torch.ones(n, dtype=torch.float64, device=device) if w is None else w.double()
 
 
+@_sharded_rows("y", "pred", "w")
 def regression_metrics(y, pred, w=None, distribution=None) -> ModelMetrics:
     y, pred = y.double(), pred.double()
     w = _w(w, y.numel(), y.device)
@@ -94,6 +125,7 @@ def _auc_from_sorted(pos, neg):
     return float(auc), float(aucpr), tp, fp
 
 
+@_sharded_rows("y", "p1", "w")
 def binomial_metrics(y, p1, w=None, domain=("0", "1"), nbins_thresholds: int = 400) -> ModelMetrics:
     """y in {0,1}; p1 = P(class 1)."""
     y, p1 = y.double(), p1.double()
@@ -179,6 +211,7 @@ def gains_lift(y, p1, w, groups: int = 16):
     return out
 
 
+@_sharded_rows("y", "probs", "w")
 def multinomial_metrics(y, probs, w=None, domain=None, hit_k: int = 10) -> ModelMetrics:
     """y: class index; probs [N, K]."""
     y = y.long() if not torch.is_floating_point(y) else torch.nan_to_num(y, nan=-1).long()
@@ -218,6 +251,7 @@ def multinomial_auc(y, probs, w):
     return float(np.mean(aucs)) if aucs else float("nan")
 
 
+@_sharded_rows("X", "assign", "w")
 def clustering_metrics(X, centers, assign, w=None) -> ModelMetrics:
     """X [N, F] (standardised space), centers [K, F], assign [N]."""
     X = X.double(); C = centers.double()
@@ -234,16 +268,19 @@ def clustering_metrics(X, centers, assign, w=None) -> ModelMetrics:
                         withinss=within.cpu().tolist(), size=size.cpu().tolist(), nobs=int(X.shape[0]))
 
 
+@_sharded_rows("score", "w")
 def anomaly_metrics(score, w=None) -> ModelMetrics:
     s = score.double()
     return ModelMetrics(model_category="AnomalyDetection", mean_score=float(s.mean()), nobs=int(s.numel()))
 
 
+@_sharded_rows("err")
 def autoencoder_metrics(err) -> ModelMetrics:
     e = err.double()
     return ModelMetrics(model_category="AutoEncoder", MSE=float(e.mean()), RMSE=math.sqrt(float(e.mean())), nobs=int(e.numel()))
 
 
+@_sharded_rows("y", "preds", "w")
 def make_metrics(category: str, y, preds, w=None, domain=None, distribution=None) -> ModelMetrics:
     """preds: regression -> [N] mean; binomial -> [N] p1 or [N,2]; multinomial -> [N,K] probs."""
     if category == "Binomial":

@@ -106,10 +106,53 @@ class ScoreKeeper:
 
 
 # ------------------------------------------------------------------------------------------------
+def rows_of(frame):
+    """Context for row-wise work on ``frame``'s tensors: frames built inside carry its shard, and for a
+    replicated frame under a multi-rank cloud nothing is all-reduced / gathered (every rank has all rows)."""
+    import contextlib
+    from ..parallel import collectives as coll, dframe
+    stack = contextlib.ExitStack()
+    sh = getattr(frame, "_shard", None)
+    stack.enter_context(dframe.shard_ctx(sh))
+    if sh is None and coll.world_active():
+        stack.enter_context(coll.replicated())
+    return stack
+
+
+# ------------------------------------------------------------------------------------------------
+_FRAME_METHODS = ("predict", "anomaly", "deepfeatures", "transform", "predict_rules", "reconstruct", "transform_frame",
+                  "predict_leaf_node_assignment_frame", "staged_predict_proba_frame")
+
+
+def _with_rows_of(fn):
+    import functools
+
+    @functools.wraps(fn)
+    def w(self, frame, *a, **k):
+        from ..frame import H2OFrame
+        if not isinstance(frame, H2OFrame):
+            return fn(self, frame, *a, **k)
+        with rows_of(frame):
+            return fn(self, frame, *a, **k)
+    w._rows_of = True
+    return w
+
+
 class Model:
-    """Trained model. Subclasses implement ``_predict_tensor(X [F,N] float32) -> [N] or [N,K]``."""
+    """Trained model. Subclasses implement ``_predict_tensor(X [F,N] float32) -> [N] or [N,K]``.
+
+    Frame-scoring methods (``predict``, ``anomaly``, ``transform``, ...) run under :func:`rows_of` for
+    their input frame in every subclass: scoring is row-local, so a sharded frame is scored on its shard
+    and the result frame is sharded the same way."""
 
     algo = "model"
+
+    def __init_subclass__(cls, **kw):
+        super().__init_subclass__(**kw)
+        for name in _FRAME_METHODS:
+            fn = cls.__dict__.get(name)
+            if fn is not None and callable(fn) and not getattr(fn, "_rows_of", False):
+                setattr(cls, name, _with_rows_of(fn))
 
     def __init__(self, key: str, params: dict, info: DataInfo):
         self.key = key
@@ -139,13 +182,14 @@ class Model:
 
     def predict(self, frame):
         from ..frame import H2OFrame
-        X, offset = frame.model_matrix(self.info, device=self.device)
-        P = self.score_tensor(X, offset)
-        out = H2OFrame.from_predictions(P, self.model_category, self.info.response_domain,
-                                        threshold=self.default_threshold(), names=self.prediction_names())
-        cm = getattr(self, "calibration_model", None)
-        if cm is not None and P.dim() == 2 and P.shape[1] == 2:
-            out = out.cbind(self._calibrated(P))
+        with rows_of(frame):
+            X, offset = frame.model_matrix(self.info, device=self.device)
+            P = self.score_tensor(X, offset)
+            out = H2OFrame.from_predictions(P, self.model_category, self.info.response_domain,
+                                            threshold=self.default_threshold(), names=self.prediction_names())
+            cm = getattr(self, "calibration_model", None)
+            if cm is not None and P.dim() == 2 and P.shape[1] == 2:
+                out = out.cbind(self._calibrated(P))
         return out
 
     # ---- calibration (CalibrationHelper.OutputWithCalibration)
@@ -191,10 +235,11 @@ class Model:
             if xval:
                 return self.output.get("cross_validation_metrics")
             return self.output.get("training_metrics")
-        X, offset = test_data.model_matrix(self.info, device=self.device)
-        y = test_data.response_tensor(self.info, device=self.device)
-        w = test_data.weights_tensor(self.info, device=self.device)
-        return self.metrics_for(X, y, w, offset)
+        with rows_of(test_data):
+            X, offset = test_data.model_matrix(self.info, device=self.device)
+            y = test_data.response_tensor(self.info, device=self.device)
+            w = test_data.weights_tensor(self.info, device=self.device)
+            return self.metrics_for(X, y, w, offset)
 
     # ---- H2O-python style accessors
     def varimp(self, use_pandas=False):

@@ -36,6 +36,13 @@ class AlgoSpec:
     needs_response_optional: bool = False   # e.g. isolation forest accepts an optional label
 
 
+# Trainers that reduce their sufficient statistics over row-sharded tensors (histograms, Gram, centroid
+# sums, gradients, class counts): under a multi-rank cloud they train on the local shard. Every other
+# trainer gets the gathered rows and trains replicated (identical on every rank: the same deterministic
+# program on the same data) — correct everywhere, scaled only where the collectives exist.
+DISTRIBUTED = {"gbm", "drf", "xgboost", "glm", "kmeans", "deeplearning", "naivebayes", "pca"}
+
+
 def register(name, trainer, supervised=True, defaults=None, **kw):
     REGISTRY[name] = AlgoSpec(name, trainer, supervised, dict(defaults or {}), **kw)
 
@@ -81,18 +88,23 @@ def prepare(algo: str, params: dict, x=None, y=None, training_frame=None):
     xs = [n for n in xs if fr.type(n) != "string" or algo in ("word2vec", "targetencoder")]
     if params.get("ignore_const_cols", True) and fr.nrows > 1:
         keep = []
+        sharded = fr._shard is not None
         for n in xs:
             c = fr._col(n)
             if c.type == "enum":
                 v = c.data
-                if int(torch.unique(v).numel()) > 1 or int(v.max()) < 0 and False:
+                u = torch.unique(v)
+                if sharded:                      # distinct codes over every shard
+                    from ..parallel import dframe
+                    u = torch.unique(dframe.gather_tensor(u.cpu()))
+                if int(u.numel()) > 1:
                     keep.append(n)
             elif c.type == "string":
                 keep.append(n)
             else:
-                v = c.data
-                ok = ~torch.isnan(v)
-                if ok.any() and (float(v[ok].max()) != float(v[ok].min()) or bool((~ok).any())):
+                from ..parallel import dframe
+                m = dframe.moments(c.data, sharded)
+                if m["n"] > 0 and (m["max"] != m["min"] or m["nas"] > 0):
                     keep.append(n)
         xs = keep
     iscat = np.array([1 if fr.type(n) == "enum" else 0 for n in xs], dtype=np.int32)
@@ -104,7 +116,7 @@ def prepare(algo: str, params: dict, x=None, y=None, training_frame=None):
             rdom = list(yc.domain)
         elif _classification_requested(algo, params) or spec.classification_only:
             from ..frame import _num_to_enum
-            rdom = list(_num_to_enum(yc).domain)
+            rdom = list(_num_to_enum(yc, fr._shard is not None).domain)
     info = DataInfo(xs, iscat, doms, y, rdom, params.get("weights_column"), params.get("offset_column"),
                     params.get("fold_column"))
     return info
@@ -118,24 +130,30 @@ def tensors(fr, info: DataInfo, device=None):
 
 
 def _fold_ids(fr, info, params, n, seed):
+    """Fold id of every local row (``FoldAssignment``). Assignments are defined on the GLOBAL row index,
+    so a row-sharded training gets exactly the folds of the single-process run."""
+    from ..parallel import dframe
+    sh = fr._shard
+    off, n_glob = (sh.offset, sh.n_global) if sh is not None else (0, n)
     k = int(params.get("nfolds") or 0)
     if info.fold and info.fold in fr.names:
         v = fr._col(info.fold).as_float()
-        u = torch.unique(v[~torch.isnan(v)])
+        u = dframe.global_unique(v) if sh is not None else torch.unique(v[~torch.isnan(v)])
         return torch.bucketize(v, u).long(), int(u.numel())
     scheme = str(params.get("fold_assignment") or "AUTO").lower()
     if scheme == "modulo":
-        return torch.arange(n) % k, k
+        return torch.arange(off, off + n) % k, k
     rng = np.random.default_rng(seed & 0xFFFFFFFF)
     if scheme == "stratified" and info.response is not None:
-        yv = fr.response_tensor(info, device=torch.device("cpu")).numpy()
-        fold = np.zeros(n, dtype=np.int64)
+        yt = fr.response_tensor(info, device=torch.device("cpu"))
+        yv = (dframe.gather_tensor(yt) if sh is not None else yt).numpy()
+        fold = np.zeros(n_glob, dtype=np.int64)
         for cls in np.unique(yv[~np.isnan(yv)]):
             idx = np.nonzero(yv == cls)[0]
             rng.shuffle(idx)
             fold[idx] = np.arange(len(idx)) % k
-        return torch.from_numpy(fold), k
-    return torch.from_numpy(rng.integers(0, k, n)), k
+        return torch.from_numpy(fold[off:off + n]), k
+    return torch.from_numpy(rng.integers(0, k, n_glob)[off:off + n]), k
 
 
 def _seed_of(params):
@@ -165,6 +183,22 @@ def train(algo: str, params: dict, x=None, y=None, training_frame=None, validati
     fr = training_frame
     if fr is None:
         raise ValueError("training_frame is required")
+    from ..parallel import collectives as coll, dframe
+    import contextlib
+    mode = contextlib.ExitStack()
+    if coll.world_active():
+        if algo in DISTRIBUTED and str(p.get("solver", "")).upper() != "L_BFGS_SERIAL":
+            fr = dframe.shard_frame(fr)
+            validation_frame = dframe.shard_frame(validation_frame) if validation_frame is not None else None
+        else:
+            fr = dframe.gather_frame(fr)
+            validation_frame = dframe.gather_frame(validation_frame)
+            mode.enter_context(coll.replicated())
+    with mode:
+        return _train(spec, algo, p, x, y, fr, validation_frame, job, model_id)
+
+
+def _train(spec, algo, p, x, y, fr, validation_frame, job, model_id):
     info = prepare(algo, p, x, y, fr)
     if not info.x:
         raise ValueError("no usable predictor columns")
@@ -267,6 +301,8 @@ def _custom_metric(model, ref, X, y, w, off, which):
         rows = torch.cat([lab[:, None], P], 1)
     else:
         rows = P[:, None]
+    from ..parallel import collectives as coll
+    rows, y, w, off = (coll.gather_rows(t) for t in (rows, y, w, off))
     name, val = udf.custom_metric_value(ref, rows.cpu().numpy(), y.double().cpu().numpy(),
                                         None if w is None else w.double().cpu().numpy(),
                                         None if off is None else off.double().cpu().numpy(), model)
@@ -317,12 +353,16 @@ def _cross_validate(spec, p, fr, info, X, yv, w, off, seed, mid, job):
                 summ[key] = dict(mean=float(np.mean(vals)), sd=float(np.std(vals, ddof=1)) if len(vals) > 1 else 0.0,
                                  values=vals)
         out["cross_validation_metrics_summary"] = summ
+    from ..parallel import collectives as coll, dframe
+    sh = fr._shard if coll.is_dist() else None
     if p.get("keep_cross_validation_predictions") and holdout is not None:
         from ..frame import H2OFrame
-        out["cross_validation_holdout_predictions_frame_id"] = H2OFrame.from_predictions(holdout, cat, info.response_domain).frame_id
+        with dframe.shard_ctx(sh):
+            out["cross_validation_holdout_predictions_frame_id"] = H2OFrame.from_predictions(holdout, cat, info.response_domain).frame_id
     if p.get("keep_cross_validation_fold_assignment"):
         from ..frame import H2OFrame, Column
-        fa = H2OFrame._from_columns([Column("fold_assignment", "int", fold.double())])
+        with dframe.shard_ctx(sh):
+            fa = H2OFrame._from_columns([Column("fold_assignment", "int", fold.double())])
         out["cross_validation_fold_assignment_frame_id"] = fa.frame_id
     out["_cv_holdout"] = holdout
     return out

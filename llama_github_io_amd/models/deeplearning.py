@@ -194,7 +194,11 @@ class DeepLearningTrainer:
         if y is not None and not ae:
             ok = ~torch.isnan(y)
             w = torch.where(ok, w, torch.zeros_like(w))
-        ex = Expander(info, standardize=p["standardize"], use_all_factor_levels=p["use_all_factor_levels"]).fit(X, w)
+        sharded = coll.is_dist()
+        row0, N_glob = coll.exclusive_offset(N) if sharded else (0, N)
+        self._row0, self._N_glob = row0, N_glob
+        ex = Expander(info, standardize=p["standardize"], use_all_factor_levels=p["use_all_factor_levels"]).fit(
+            X, w, reduce=coll.all_reduce_ if sharded else None)
         # bf16 compute: the design matrix is materialised in bf16 (half the HBM footprint and per-step
         # gather bytes; GEMM inputs need no per-step cast)
         bf16 = dev.type == "cuda" and str(p["compute_dtype"]).lower() in ("bf16", "bfloat16") and not bool(p["autoencoder"])
@@ -246,8 +250,9 @@ class DeepLearningTrainer:
             if cat == "Regression":
                 yy = torch.nan_to_num(y.double(), nan=0.0)
                 if dist in ("gaussian", "laplace", "quantile", "huber"):
-                    mu = float((w * yy).sum() / w.sum())
-                    sd = float(((w * (yy - mu) ** 2).sum() / w.sum()).sqrt()) or 1.0
+                    sw_all = coll.all_reduce_scalar(float(w.sum()))
+                    mu = coll.all_reduce_scalar(float((w * yy).sum())) / sw_all
+                    sd = math.sqrt(coll.all_reduce_scalar(float((w * (yy - mu) ** 2).sum())) / sw_all) or 1.0
                     if not p["standardize"]:
                         mu, sd = 0.0, 1.0
                     model.resp_mu, model.resp_sd = mu, sd
@@ -270,19 +275,19 @@ class DeepLearningTrainer:
         keeper = ScoreKeeper(p["stopping_rounds"], p["stopping_metric"], p["stopping_tolerance"],
                              "Regression" if ae else cat)
         epochs = float(p["epochs"]) - prev_epochs
-        total = int(math.ceil(epochs * N / B))
+        total = int(math.ceil(epochs * N_glob / B))
         g = torch.Generator(device="cpu").manual_seed(seed & 0x7FFFFFFF)
         history = []
         samples = 0
         last_score = time.time()
         dtype = torch.bfloat16 if str(p["compute_dtype"]).lower() in ("bf16", "bfloat16") else None
         perm = None
-        pos = N
+        pos = N_glob
         wf = w.float()
         # hipGraph capture of the whole training step (fwd + bwd + fused ADADELTA): the step is a fixed
         # launch sequence on static buffers, so replaying it removes the per-kernel launch overhead that
         # dominates small-batch MLP training. Eager path for dropout / momentum / max_w2 / multi-rank.
-        use_graph = (dev.type == "cuda" and adaptive and not coll.is_dist() and float(p["input_dropout_ratio"]) == 0
+        use_graph = (dev.type == "cuda" and adaptive and not sharded and float(p["input_dropout_ratio"]) == 0
                      and all(float(v) == 0 for v in hd) and max_w2 == float("inf") and N >= B
                      and os.environ.get("H2O_DL_GRAPH", "1") == "1")
         graph = None
@@ -300,12 +305,17 @@ class DeepLearningTrainer:
                 ls.backward()
                 with torch.no_grad():
                     fp.adadelta(rho, eps, l1, l2)
+        gbuf = torch.empty(fp.g.numel() + 1, dtype=fp.g.dtype, device=fp.g.device) if sharded else None
         for step in range(total):
-            if pos + B > N:
-                perm = torch.randperm(N, generator=g).to(dev) if p["shuffle_training_data"] or True else torch.arange(N, device=dev)
+            if pos + B > N_glob:
+                # mini-batches are drawn from the GLOBAL row order: under row sharding each rank takes the
+                # members of the batch it owns, so the summed gradient is the single-process one
+                perm = torch.randperm(N_glob, generator=g).to(dev) if p["shuffle_training_data"] or True else torch.arange(N_glob, device=dev)
                 pos = 0
             idx = perm[pos:pos + B]
             pos += B
+            if sharded:
+                idx = idx[(idx >= row0) & (idx < row0 + N)] - row0
             net.train()
             net.step = step
             if use_graph:
@@ -337,14 +347,20 @@ class DeepLearningTrainer:
                 with torch.autocast(device_type=dev.type, dtype=dtype, enabled=dtype is not None):
                     out = net(xb, seed)
                 out = out.float()
-                loss = self._loss(out, xb if ae else yt.index_select(0, idx), wb, cat, dist, ae) / wb.sum().clamp(min=1e-12)
+                loss = self._loss(out, xb if ae else yt.index_select(0, idx), wb, cat, dist, ae)
                 fp.zero_grad()
-                loss.backward()                  # accumulates into the flat gradient buffer
-                if coll.is_dist():               # data parallel: ONE all-reduce of every gradient per step
-                    coll.all_reduce_(fp.g)
-                    fp.g /= coll.world()
+                if sharded:
+                    # data parallel: ONE all-reduce per step of [sum-gradient, batch weight]; the gradient
+                    # is normalised by the GLOBAL batch weight afterwards
+                    loss.backward()
+                    gbuf[:-1].copy_(fp.g)
+                    gbuf[-1] = wb.sum()
+                    coll.all_reduce_(gbuf)
+                    fp.g.copy_(gbuf[:-1] / gbuf[-1].clamp(min=1e-12))
+                else:
+                    (loss / wb.sum().clamp(min=1e-12)).backward()   # accumulates into the flat gradient buffer
                 with torch.no_grad():
-                    samples += B * (coll.world() if coll.is_dist() else 1)
+                    samples += B
                     if adaptive:                 # ADADELTA (Neurons.java: rho, epsilon), one fused HIP launch
                         fp.adadelta(rho, eps, l1, l2)
                     else:
@@ -370,18 +386,20 @@ class DeepLearningTrainer:
             if self.job is not None and step % 50 == 0:
                 self.job.set_progress(step / max(total, 1))
             end = step == total - 1
-            if end or (time.time() - last_score > float(p["score_interval"])) or \
-                    (keeper.k > 0 and step > 0 and step % max(1, N // B) == 0):
+            timed = time.time() - last_score > float(p["score_interval"])
+            if sharded:                          # every rank must take the same scoring decision
+                timed = coll.agree(timed) if step % 16 == 0 else False
+            if end or timed or (keeper.k > 0 and step > 0 and step % max(1, N_glob // B) == 0):
                 last_score = time.time()
-                ev = self._score(model, X, y, w, samples / N, valid)
+                ev = self._score(model, X, y, w, samples / N_glob, valid)
                 history.append({k: v for k, v in ev.items() if not k.startswith("_")})
                 mref = ev.get("_valid") or ev.get("_train")
                 if mref is not None and not end and keeper.add(mref):
                     break
-                if float(p["max_runtime_secs"] or 0) > 0 and time.time() - t0 > float(p["max_runtime_secs"]):
+                if float(p["max_runtime_secs"] or 0) > 0 and coll.agree(time.time() - t0 > float(p["max_runtime_secs"])):
                     break
         model.output["scoring_history"] = history
-        model.output["epochs"] = prev_epochs + samples / N
+        model.output["epochs"] = prev_epochs + samples / N_glob
         if ae:
             model.output["training_metrics"] = self._ae_metrics(model, X)
         else:
@@ -441,8 +459,14 @@ class DeepLearningTrainer:
     def _score(self, model, X, y, w, epochs, valid):
         p = self.p
         N = X.shape[1]
-        n = int(p["score_training_samples"]) or N
-        idx = torch.arange(N, device=X.device) if n >= N else torch.randperm(N, device=X.device)[:n]
+        Ng, r0 = getattr(self, "_N_glob", N), getattr(self, "_row0", 0)
+        n = int(p["score_training_samples"]) or Ng
+        if n >= Ng:
+            idx = torch.arange(N, device=X.device)
+        else:       # a sample of GLOBAL rows (same rows however the frame is sharded)
+            gi = torch.randperm(Ng, generator=torch.Generator().manual_seed(int(p.get("seed") or 0) & 0x7FFFFFFF))[:n]
+            gi = gi.to(X.device)
+            idx = gi[(gi >= r0) & (gi < r0 + N)] - r0
         Xs = X[:, idx]
         ev = dict(epochs=epochs, timestamp=time.time())
         if p["autoencoder"]:

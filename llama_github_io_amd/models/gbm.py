@@ -114,7 +114,7 @@ class GBMTrainer(SharedTreeTrainer):
         else:
             init = np.array([self.dist.init_f(self.y, w, self.offset, reduce=coll.all_reduce_scalar)])
             if self.dname in ORDER_STAT_DISTS:
-                yv = self.y
+                yv = coll.gather_rows(self.y)          # order statistic of the GLOBAL response
                 if self.dname == "quantile":
                     init = np.array([float(torch.quantile(yv.double(), self.p["quantile_alpha"]))])
                 else:
@@ -137,7 +137,7 @@ class GBMTrainer(SharedTreeTrainer):
         f = self.f[:, k]
         if k == 0 and self.dname == "huber":
             self._flush_pending()
-            r = (self.y - f).abs()
+            r = coll.gather_rows((self.y - f).abs())
             self.dist.huber_delta = float(torch.quantile(r.double()[: 1 << 24], self.p["huber_alpha"]))
         if self._fused():
             # one HIP pass: previous tree's f update + sampling + residuals + leaf terms + scale maxima
@@ -148,7 +148,7 @@ class GBMTrainer(SharedTreeTrainer):
             pv, pl = self._pending if getattr(self, "_pending", None) is not None else (None, None)
             p1 = {"tweedie": self.p["tweedie_power"], "quantile": self.p["quantile_alpha"],
                   "huber": getattr(self.dist, "huber_delta", 1.0)}.get(self.dname, 0.0)
-            nat.call("h2o_gbm_step", self.N, _FUSED_DIST[self.dname], self.y.data_ptr(),
+            nat.call("h2o_gbm_step", self.N, self.row0, _FUSED_DIST[self.dname], self.y.data_ptr(),
                      0 if self._wbuf is None else self._wbuf.data_ptr(), self.f.data_ptr(),
                      0 if pv is None else pv.data_ptr(), 0 if pl is None else pl.data_ptr(),
                      float(self.p["sample_rate"]), (self.seed * 0x9E3779B1 + t * 7919) & ((1 << 64) - 1),
@@ -221,6 +221,11 @@ class GBMTrainer(SharedTreeTrainer):
         leaf = self.builder.leaf_of_row.long()
         diff = (self.y - self.f[:, k]).double()
         w = (self.aux[:, 0] if self.w_eff is None else self.w_eff).double()
+        if coll.is_dist():
+            # per-leaf weighted order statistics need every row of the leaf: gather (leaf, residual, weight)
+            # from the shards (leaf ids are global: every rank built the same tree)
+            full = coll.gather_rows(torch.stack([leaf.double(), diff, w], 1))
+            leaf, diff, w = full[:, 0].long(), full[:, 1], full[:, 2]
         alpha = self.p["quantile_alpha"] if self.dname == "quantile" else 0.5
         order = torch.argsort(diff)
         leaf_s = leaf[order]

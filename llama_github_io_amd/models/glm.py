@@ -151,12 +151,12 @@ class Family:
     def loglik_aic(self, y, mu, w, dev_sum, nobs, rank):
         n = self.name
         if n == "gaussian":
-            W = float(w.sum())
+            W = _gsum(w.sum())
             return float(W * (math.log(2 * math.pi * dev_sum / W) + 1) + 2) + 2 * rank
         if n in ("binomial", "quasibinomial", "fractionalbinomial"):
             return dev_sum + 2 * rank
         if n == "poisson":
-            ll = (w * (y * torch.log(mu.clamp(min=1e-300)) - mu - torch.lgamma(y + 1))).sum()
+            ll = _gsum((w * (y * torch.log(mu.clamp(min=1e-300)) - mu - torch.lgamma(y + 1))).sum())
             return float(-2 * ll) + 2 * rank
         return float("nan")
 
@@ -255,6 +255,17 @@ class GLMModel(Model):
 
 
 # ------------------------------------------------------------------------------------------------
+def _gsum(x) -> float:
+    """Global sum of a per-rank scalar partial (row-sharded training; identity otherwise)."""
+    v = float(x)
+    return coll.all_reduce_scalar(v) if coll.is_dist() else v
+
+
+def _gvec(t: torch.Tensor) -> torch.Tensor:
+    """Global sum of a per-rank vector partial (in place)."""
+    return coll.all_reduce_(t) if coll.is_dist() else t
+
+
 def _soft(x, t):
     return torch.sign(x) * (x.abs() - t).clamp(min=0)
 
@@ -367,7 +378,10 @@ class GLMTrainer:
         model.expander = ex
         model.output.update(family=fam, link=link, alpha=alpha)
         solver = str(p["solver"]).upper()
-        if fam in ("multinomial", "ordinal") or solver == "L_BFGS":
+        if fam == "multinomial" and solver != "L_BFGS":
+            beta, path = self._fit_multinomial_irls(Zi, y, w, off, alpha, obj_reg, intercept, info, nobs)
+            lam_best = path[-1]["lambda"] if path else 0.0
+        elif fam in ("multinomial", "ordinal") or solver == "L_BFGS":
             beta, path = self._fit_lbfgs_or_multi(fam, link, Zi, y, w, off, alpha, obj_reg, intercept, info, ex)
             lam_best = path[-1]["lambda"] if path else 0.0
         else:
@@ -393,7 +407,7 @@ class GLMTrainer:
         p = self.p
         dev = Zi.device
         P1 = Zi.shape[1]
-        ymu = float((w * y).sum() / w.sum())
+        ymu = _gsum((w * y).sum()) / _gsum(w.sum())
         beta = torch.zeros(P1, dtype=torch.float64, device=dev)
         if intercept:
             beta[-1] = float(fam.linkfn(torch.tensor([min(max(ymu, 1e-6), 1 - 1e-6) if fam.name in ("binomial", "quasibinomial", "fractionalbinomial") else ymu], dtype=torch.float64))[0])
@@ -402,7 +416,7 @@ class GLMTrainer:
         mu = fam.linkinv(eta)
         gvec = fam.dlink(mu)
         var = fam.variance(mu)
-        grad = -(G.xtv(Zi, (w * (y - mu) / (var * gvec)).float()) * obj_reg)
+        grad = -(_gvec(G.xtv(Zi, (w * (y - mu) / (var * gvec)).float())) * obj_reg)
         if intercept:
             grad[-1] = 0
         lmax = float(grad.abs().max()) / max(alpha, 1e-2)
@@ -426,7 +440,7 @@ class GLMTrainer:
         beps = float(p["beta_epsilon"])
         path = []
         best = (float("inf"), None, None)
-        null_dev = float((w * fam.deviance(y, torch.full_like(y, ymu))).sum())
+        null_dev = _gsum((w * fam.deviance(y, torch.full_like(y, ymu))).sum())
         for li, lam in enumerate(lambdas):
             l1, l2 = lam * alpha, lam * (1 - alpha)
             for it in range(max(max_it, 1)):
@@ -458,7 +472,7 @@ class GLMTrainer:
                 if diff < beps:
                     break
             mu = fam.linkinv(Zi.double() @ beta + off)
-            dev_tr = float((w * fam.deviance(y, mu)).sum())
+            dev_tr = _gsum((w * fam.deviance(y, mu)).sum())
             entry = dict(lambda_=lam, dev_explained=1 - dev_tr / null_dev if null_dev > 0 else 0.0,
                          coefs=beta.cpu().tolist())
             entry["lambda"] = lam
@@ -471,12 +485,79 @@ class GLMTrainer:
                 muv = fam.linkinv(etav)
                 okv = ~torch.isnan(yv)
                 wvv = torch.ones_like(yv, dtype=torch.float64) if wv is None else wv.double()
-                score = float((wvv[okv] * fam.deviance(yv.double()[okv], muv[okv])).sum())
+                score = _gsum((wvv[okv] * fam.deviance(yv.double()[okv], muv[okv])).sum())
             if valid is not None and len(lambdas) > 1 and score < best[0]:
                 best = (score, beta.clone(), lam)
         if best[1] is not None:
             return best[1], path, best[2]
         return beta, path, lambdas[-1]
+
+    # ---- multinomial IRLSM (GLM.java fitIRLSM_multinomial): one penalized weighted least-squares
+    # solve per class with the other classes' coefficients held fixed, cycled to convergence
+    def _fit_multinomial_irls(self, Zi, y, w, off, alpha, obj_reg, intercept, info, nobs):
+        p = self.p
+        dev = Zi.device
+        P1 = Zi.shape[1]
+        K = len(info.response_domain)
+        yl = torch.nan_to_num(y, nan=0).long().clamp(0, K - 1)
+        Y = torch.nn.functional.one_hot(yl, K).double()
+        B = torch.zeros(K, P1, dtype=torch.float64, device=dev)
+        # null model: class log-frequencies as intercepts
+        freq = _gvec((w[:, None] * Y).sum(0).contiguous())
+        freq = (freq / freq.sum()).clamp(min=1e-10)
+        if intercept:
+            B[:, -1] = torch.log(freq) - torch.log(freq).mean()
+        Zd = Zi.double()
+
+        def probs(B):
+            return torch.softmax(Zd @ B.T + off[:, None], 1)
+        lam_in = p["lambda_"]
+        if lam_in is not None:
+            lambdas = [float(v) for v in (lam_in if isinstance(lam_in, (list, tuple)) else [lam_in])]
+        else:
+            Pm = probs(B)
+            g = _gvec((Zi.double().T @ (w[:, None] * (Y - Pm))).contiguous()) * obj_reg    # [P1, K]
+            if intercept:
+                g[-1] = 0
+            lmax = float(g.abs().max()) / max(alpha, 1e-2)
+            lmr = float(p["lambda_min_ratio"]) if float(p["lambda_min_ratio"]) > 0 else (1e-4 if (nobs >> 4) > P1 else 1e-2)
+            if alpha == 0:
+                lmr *= 1e-2
+            if p["lambda_search"]:
+                nl = int(p["nlambdas"]) if int(p["nlambdas"]) > 0 else (100 if alpha > 0 else 30)
+                dec = lmr ** (1.0 / max(nl - 1, 1))
+                lambdas = [lmax * dec ** i for i in range(nl)]
+            else:
+                lambdas = [10 * lmr * lmax]
+        max_it = int(p["max_iterations"]) if int(p["max_iterations"]) > 0 else 50
+        beps = float(p["beta_epsilon"])
+        path = []
+        for lam in lambdas:
+            l1, l2 = lam * alpha, lam * (1 - alpha)
+            for it in range(max_it):
+                Bold = B.clone()
+                for c in range(K):
+                    Pm = probs(B)
+                    pc = Pm[:, c]
+                    wi = (w * pc * (1 - pc)).clamp(min=1e-10 * float(w.max()) if w.numel() else 0.0)
+                    eta_c = Zd @ B[c]
+                    zi = eta_c + (Y[:, c] - pc) / (pc * (1 - pc)).clamp(min=1e-10)
+                    Gm = _gvec(G.gram(Zi, wi.float())) * obj_reg
+                    r = _gvec(G.xtv(Zi, (wi * zi).float())) * obj_reg
+                    if not intercept:
+                        Gm[-1, :] = 0
+                        Gm[:, -1] = 0
+                        Gm[-1, -1] = 1
+                        r[-1] = 0
+                    B[c] = solve_penalized(Gm, r, l1, l2, intercept, B[c], bool(p["non_negative"]))
+                if self.job is not None:
+                    self.job.check_cancelled()
+                if float((B - Bold).abs().max()) < beps:
+                    break
+            if intercept:                        # softmax is shift-invariant: centre the intercepts
+                B[:, -1] -= B[:, -1].mean()
+            path.append(dict(lambda_=lam, **{"lambda": lam}, coefs=B.cpu().tolist()))
+        return B, path
 
     # ---- multinomial / ordinal / L-BFGS: device autograd objective
     def _fit_lbfgs_or_multi(self, fam, link, Zi, y, w, off, alpha, obj_reg, intercept, info, ex):
@@ -520,12 +601,10 @@ class GLMTrainer:
                 return 0.5 * (w * family.deviance(y, mu)).sum() * obj_reg
             params = [B]
         if lam is None:
-            with torch.no_grad():
-                pass
             Bz = B.detach().clone().requires_grad_(True)
-            g = torch.autograd.grad(nll(Bz), Bz)[0]
+            g = _gvec(torch.autograd.grad(nll(Bz), Bz)[0].contiguous())
             lmax = float((g * pen).abs().max()) / max(alpha, 1e-2)
-            nobs = int((w > 0).sum())
+            nobs = int(_gsum((w > 0).sum()))
             lmr = float(p["lambda_min_ratio"]) if float(p["lambda_min_ratio"]) > 0 else (1e-4 if (nobs >> 4) > P1 else 1e-2)
             if alpha == 0:
                 lmr *= 1e-2
@@ -535,10 +614,18 @@ class GLMTrainer:
                                 tolerance_grad=1e-9, tolerance_change=1e-12, history_size=20, line_search_fn="strong_wolfe")
 
         def closure():
+            # the data term is a sum over rows: its value and gradient are all-reduced over the shards, so
+            # every rank takes the identical L-BFGS step; the penalty is added once, after the reduce
             opt.zero_grad()
-            loss = nll(B) + 0.5 * l2 * ((B * pen) ** 2).sum() + l1 * torch.sqrt((B * pen) ** 2 + 1e-12).sum()
-            loss.backward()
-            return loss
+            data = nll(B)
+            data.backward()
+            if coll.is_dist():
+                for prm in params:
+                    if prm.grad is not None:
+                        coll.all_reduce_(prm.grad)
+            pen_term = 0.5 * l2 * ((B * pen) ** 2).sum() + l1 * torch.sqrt((B * pen) ** 2 + 1e-12).sum()
+            pen_term.backward()
+            return torch.tensor(_gsum(data.detach()) + float(pen_term.detach()), dtype=torch.float64)
         opt.step(closure)
         Bd = B.detach()
         if l1 > 0:
@@ -575,12 +662,12 @@ class GLMTrainer:
         if fam not in ("multinomial", "ordinal"):
             family = Family(fam, link, float(p["tweedie_variance_power"]), float(p["tweedie_link_power"]), float(p["theta"]))
             mu = (P[:, 1] if P.dim() == 2 else P).double()
-            res_dev = float((w * family.deviance(y, mu)).sum())
-            ymu = float((w * y).sum() / w.sum())
+            res_dev = _gsum((w * family.deviance(y, mu)).sum())
+            ymu = _gsum((w * y).sum()) / _gsum(w.sum())
             null_mu = torch.full_like(y, ymu)
             if offset is not None:
                 null_mu = family.linkinv(family.linkfn(null_mu) + off)
-            null_dev = float((w * family.deviance(y, null_mu)).sum())
+            null_dev = _gsum((w * family.deviance(y, null_mu)).sum())
             rank = int((beta[0].abs() > 0).sum())
             out.update(residual_deviance=res_dev, null_deviance=null_dev, null_degrees_of_freedom=nobs - (1 if p["intercept"] else 0),
                        residual_degrees_of_freedom=nobs - rank, aic=family.loglik_aic(y, mu, w, res_dev, nobs, rank))
@@ -589,10 +676,10 @@ class GLMTrainer:
         else:
             probs = P.double()
             yl = y.long().clamp(min=0)
-            res_dev = float(-2 * (w * torch.log(probs.gather(1, yl[:, None])[:, 0].clamp(min=1e-15))).sum())
-            freq = segment_sum(yl, w, probs.shape[1])
+            res_dev = _gsum(-2 * (w * torch.log(probs.gather(1, yl[:, None])[:, 0].clamp(min=1e-15))).sum())
+            freq = _gvec(segment_sum(yl, w, probs.shape[1]))
             freq = freq / freq.sum()
-            null_dev = float(-2 * (w * torch.log(freq[yl].clamp(min=1e-15))).sum())
+            null_dev = _gsum(-2 * (w * torch.log(freq[yl].clamp(min=1e-15))).sum())
             rank = int((beta.abs() > 0).sum())
             out.update(residual_deviance=res_dev, null_deviance=null_dev, aic=res_dev + 2 * rank,
                        null_degrees_of_freedom=nobs - 1, residual_degrees_of_freedom=nobs - rank)
@@ -601,7 +688,7 @@ class GLMTrainer:
             tm.update(null_deviance=out.get("null_deviance"), residual_deviance=out.get("residual_deviance"),
                       AIC=out.get("aic"))
             if cat == "Regression":
-                tm["mean_residual_deviance"] = out["residual_deviance"] / max(float(w.sum()), 1e-300)
+                tm["mean_residual_deviance"] = out["residual_deviance"] / max(_gsum(w.sum()), 1e-300)
         out["training_metrics"] = tm
         imp = [(n[: n.rfind("_")] if K > 1 else n, abs(v)) for n, v in coefs_std.items() if not n.startswith("Intercept")]
         agg = {}
@@ -619,11 +706,11 @@ class GLMTrainer:
         gp = family.dlink(mu)
         var = family.variance(mu)
         wi = w / (var * gp * gp).clamp(min=1e-30)
-        Gm = G.gram(Zi, wi.float())
+        Gm = _gvec(G.gram(Zi, wi.float()))
         if family.name in ("binomial", "poisson", "quasibinomial", "fractionalbinomial"):
             disp = 1.0
         else:
-            disp = float((w * (y - mu) ** 2 / var.clamp(min=1e-30)).sum()) / max(nobs - rank, 1)
+            disp = _gsum((w * (y - mu) ** 2 / var.clamp(min=1e-30)).sum()) / max(nobs - rank, 1)
         cov = torch.linalg.pinv(Gm) * disp
         se_std = cov.diagonal().clamp(min=0).sqrt()
         # raw-scale standard errors: numeric coefficient j scales by 1/sd_j; intercept via the delta method

@@ -90,31 +90,60 @@ class KMeansTrainer:
         self.p = p
         self.job = None
 
+    # ---- global-row helpers: the init / re-seed rules pick rows by GLOBAL index, so a row-sharded run
+    # picks exactly the rows of the single-process run (the owner rank contributes the row)
+    def _row(self, Z, j: int) -> torch.Tensor:
+        """Row ``j`` (global index) of Z on every rank."""
+        if not coll.is_dist():
+            return Z[j:j + 1].clone()
+        r = torch.zeros(1, Z.shape[1], dtype=torch.float64, device=Z.device)
+        if self.row0 <= j < self.row0 + Z.shape[0]:
+            r[0] = Z[j - self.row0].double()
+        return coll.all_reduce_(r).float()
+
+    def _argmax(self, v: torch.Tensor) -> int:
+        """Global index of the first maximum of a row vector."""
+        if not coll.is_dist():
+            return int(torch.argmax(v))
+        j = int(torch.argmax(v)) if v.numel() else 0
+        best = float(v[j]) if v.numel() else float("-inf")
+        parts = coll.all_gather_object((best, self.row0 + j))
+        top = max(p[0] for p in parts)
+        return min(p[1] for p in parts if p[0] == top)
+
     def _init_centers(self, Z, k, rng, how):
-        N = Z.shape[0]
+        N = self.N_glob
         dev = Z.device
         if how == "user" and self.p.get("user_points") is not None:
             up = self.p["user_points"]
             U = up.as_tensor() if hasattr(up, "as_tensor") else torch.as_tensor(np.asarray(up, dtype=np.float32))
             return self.ex.transform(U.T.contiguous().to(dev)) if U.shape[1] == self.info.F else U.to(dev).float()
         first = int(rng.integers(N))
-        C = Z[first:first + 1].clone()
+        C = self._row(Z, first)
         if how == "random":
-            idx = torch.as_tensor(rng.choice(N, size=min(k, N), replace=False), device=dev)
-            return Z[idx].clone()
+            idx = rng.choice(N, size=min(k, N), replace=False)
+            return torch.cat([self._row(Z, int(j)) for j in idx], 0)
         while C.shape[0] < k:
             _, d = kmeans_assign(Z, C)
             if how == "plusplus":
                 pr = d.double().clamp(min=0)
-                s = float(pr.sum())
+                s = coll.all_reduce_scalar(float(pr.sum()))
                 if s <= 0:
                     break
                 u = rng.random() * s
-                j = int(torch.searchsorted(torch.cumsum(pr, 0), torch.tensor([u], dtype=torch.float64, device=dev))[0])
+                before = 0.0
+                if coll.is_dist():      # mass held by lower ranks: exclusive scan of the per-rank sums
+                    sums = coll.all_gather_object(float(pr.sum()))
+                    before = float(sum(sums[:coll.rank()]))
+                cs = torch.cumsum(pr, 0) + before
+                jl = int(torch.searchsorted(cs, torch.tensor([u], dtype=torch.float64, device=dev))[0])
+                mine = jl < pr.numel() and (before < u or coll.rank() == 0)
+                j = self.row0 + jl if mine else N
+                j = int(min(coll.all_gather_object(j))) if coll.is_dist() else j
                 j = min(j, N - 1)
             else:  # furthest
-                j = int(torch.argmax(d))
-            C = torch.cat([C, Z[j:j + 1]], 0)
+                j = self._argmax(d)
+            C = torch.cat([C, self._row(Z, j)], 0)
         return C
 
     def _lloyd(self, Z, w, C, max_it):
@@ -128,9 +157,10 @@ class KMeansTrainer:
             newC = torch.where(cnt[:, None] > 0, sums / cnt.clamp(min=1e-300)[:, None], C.double()).float()
             empty = torch.nonzero(cnt == 0).flatten().tolist()
             for e in empty:   # re-seed empty clusters at the worst-fit row
-                j = int(torch.argmax(d))
-                newC[e] = Z[j]
-                d[j] = 0
+                j = self._argmax(d)
+                newC[e] = self._row(Z, j)[0]
+                if 0 <= j - self.row0 < d.numel():
+                    d[j - self.row0] = 0
             shift = float((newC - C).abs().max())
             C = newC
             if self.job is not None:
@@ -150,7 +180,9 @@ class KMeansTrainer:
         seed = resolve_seed(p["seed"])
         rng = np.random.default_rng(seed & 0xFFFFFFFF)
         w = torch.ones(N, dtype=torch.float64, device=dev) if w is None else w.double()
-        self.ex = Expander(info, standardize=p["standardize"], use_all_factor_levels=True).fit(X, w)
+        self.row0, self.N_glob = (coll.exclusive_offset(N) if coll.is_dist() else (0, N))
+        self.ex = Expander(info, standardize=p["standardize"], use_all_factor_levels=True).fit(
+            X, w, reduce=coll.all_reduce_ if coll.is_dist() else None)
         Z = self.ex.transform(X)
         how = str(p["init"]).lower()
         max_it = int(p["max_iterations"])
@@ -158,22 +190,23 @@ class KMeansTrainer:
             # KMeans.java: deterministic growth from k=1, split the worst cluster, stop when the relative
             # within-SS improvement falls under min(0.02 + 10/N + 2.5/F^2, 0.8) and keep the previous k
             kmax = int(p["k"])
-            cutoff = min(0.02 + 10.0 / N + 2.5 / max(info.F, 1) ** 2, 0.8)
-            C0 = (Z.double() * w[:, None]).sum(0, keepdim=True).float() / float(w.sum())
+            cutoff = min(0.02 + 10.0 / self.N_glob + 2.5 / max(info.F, 1) ** 2, 0.8)
+            sw = coll.all_reduce_scalar(float(w.sum()))
+            C0 = (coll.all_reduce_((Z.double() * w[:, None]).sum(0, keepdim=True)) / sw).float()
             prev = None
             best = None
             for k in range(1, kmax + 1):
                 Ck, ak, dk, it = self._lloyd(Z, w, C0, max_it)
-                wss = float((dk.double() * w).sum())
+                wss = coll.all_reduce_scalar(float((dk.double() * w).sum()))
                 if prev is not None and (prev - wss) / max(prev, 1e-300) < cutoff:
                     break
                 best, prev = (Ck, ak, dk, it), wss
                 if k == kmax:
                     break
-                per = segment_sum(ak, dk.double() * w, Ck.shape[0])
+                per = coll.all_reduce_(segment_sum(ak, dk.double() * w, Ck.shape[0]))
                 worst = int(torch.argmax(per))
-                far = int(torch.argmax(torch.where(ak == worst, dk, torch.full_like(dk, -1.0))))
-                C0 = torch.cat([Ck, Z[far:far + 1]], 0)
+                far = self._argmax(torch.where(ak == worst, dk, torch.full_like(dk, -1.0)))
+                C0 = torch.cat([Ck, self._row(Z, far)], 0)
             C, a, d, iters = best
         else:
             C0 = self._init_centers(Z, int(p["k"]), rng, how)

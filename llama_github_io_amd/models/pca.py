@@ -30,7 +30,7 @@ def _expander(info, transform, use_all, X, w):
     t = str(transform).upper()
     ex = Expander(info, standardize=t in ("STANDARDIZE", "NORMALIZE", "DESCALE"), use_all_factor_levels=use_all,
                   center_only=(t == "DEMEAN"))
-    ex.fit(X, w)
+    ex.fit(X, w, reduce=coll.all_reduce_ if coll.is_dist() else None)
     if t == "DESCALE":          # scale only, no centering
         ex.descale_only = True
     return ex
@@ -51,12 +51,12 @@ def _eig_top(G, k):
 
 
 def _power(Z, k, iters, gen):
-    """Deflated power iteration per component (PCA.java Power method)."""
+    """Deflated power iteration per component (PCA.java Power method) on the (all-reduced) Gram."""
     P = Z.shape[1]
     V = torch.zeros(P, k, dtype=torch.float64, device=Z.device)
     d = torch.zeros(k, dtype=torch.float64, device=Z.device)
     Zd = Z.double()
-    G = Zd.T @ Zd
+    G = coll.all_reduce_(Zd.T @ Zd) if coll.is_dist() else Zd.T @ Zd
     for j in range(k):
         v = torch.randn(P, dtype=torch.float64, generator=gen).to(Z.device)
         v /= v.norm()
@@ -164,13 +164,18 @@ class PCATrainer:
         elif method == "power":
             ev, V = _power(Zw, k, int(p["max_iterations"]), gen)
         else:
-            ev, V = _randomized(Zw, k, int(p["max_iterations"]), gen)
+            # randomized range finder needs a QR over all rows: run it on the gathered rows
+            Zg = coll.gather_rows(Zw)
+            with coll.replicated():
+                ev, V = _randomized(Zg, k, int(p["max_iterations"]), gen)
         # sign convention: largest |loading| positive (stable across methods)
         sgn = torch.sign(V.gather(0, V.abs().argmax(0, keepdim=True)))
         V = V * torch.where(sgn == 0, torch.ones_like(sgn), sgn)
-        W = float(w.sum())
+        W = coll.all_reduce_scalar(float(w.sum()))
         sdev = (ev / max(W - 1, 1)).sqrt()
         G_all = gram(Z, w.float())
+        if coll.is_dist():
+            G_all = coll.all_reduce_(G_all)
         total_var = float(torch.diagonal(G_all).sum()) / max(W - 1, 1)
         prop = (sdev ** 2) / max(total_var, 1e-300)
         model = self.model_cls(model_key or make_key(self.model_cls.algo), p, info)
@@ -219,5 +224,5 @@ class SVDTrainer(PCATrainer):
         if self.p.get("keep_u", True):
             from ..frame import H2OFrame
             U = (Z.double() @ V) / d.clamp(min=1e-300)[None, :]
-            fr = H2OFrame.from_tensor(U.float(), [f"u{i + 1}" for i in range(U.shape[1])])
+            fr = H2OFrame.from_tensor(coll.gather_rows(U.float()), [f"u{i + 1}" for i in range(U.shape[1])])
             model.output["u_key"] = fr.frame_id

@@ -134,6 +134,7 @@ class SharedTreeTrainer:
         F, N = X.shape
         self.dev, self.F, self.N, self.info = dev, F, N, info
         self.seed = resolve_seed(p["seed"])
+        self.row0 = coll.row_offset(N)            # global index of this rank's first row (0 unsharded)
         self.category = model_category(info)
         self.w = torch.ones(N, dtype=torch.float32, device=dev) if w is None else w.float().to(dev)
         self.offset = None if offset is None else offset.float().to(dev)
@@ -144,11 +145,19 @@ class SharedTreeTrainer:
         if str(p.get("histogram_type", "AUTO")).lower() in ("uniformadaptive", "random", "roundrobin", "uniformrobust"):
             max_bins = int(min(255, max(p.get("nbins_top_level", 1024), p.get("nbins", 20))))
         if coll.is_dist():
-            # every rank must bin identically: fit on the union of per-rank samples
-            per = max(1, (1 << 20) // coll.world())
-            g = torch.Generator(device="cpu").manual_seed((self.seed + coll.rank()) & 0x7FFFFFFF)
-            idx = torch.randperm(N, generator=g)[:per].to(dev)
-            Xs = coll.all_gather_cat(X.index_select(1, idx).contiguous(), dim=1)
+            # every rank must bin identically, and exactly like the single-process run: the quantile
+            # sample is drawn on GLOBAL row indices (fit_binning's own rule), each rank contributes the
+            # sampled rows it owns, and the edges come from the gathered sample
+            n_glob = coll.exclusive_offset(N)[1]
+            sample = 1 << 20
+            if n_glob > sample:
+                g = torch.Generator(device="cpu").manual_seed(int(self.seed) & 0x7FFFFFFF)
+                gidx = torch.randperm(n_glob, generator=g)[:sample]
+                mine = gidx[(gidx >= self.row0) & (gidx < self.row0 + N)] - self.row0
+                Xl = X.index_select(1, mine.to(dev))
+            else:
+                Xl = X
+            Xs = coll.all_gather_cat(Xl.contiguous(), dim=1)
             self.binning = fit_binning(Xs, info.iscat, info.nlevels, max_bins=max_bins, seed=self.seed,
                                        sample=Xs.shape[1] + 1)
         else:
@@ -241,7 +250,7 @@ class SharedTreeTrainer:
             if ck_dir and built % max(1, int(p.get("in_training_checkpoints_tree_interval") or 1)) == 0:
                 self._drain(handles, forest, gains)       # snapshot of the model so far, resumable via checkpoint=
                 self._save_in_training(model, built, ck_dir)
-            if max_rt > 0 and time.time() - t_start > max_rt:
+            if max_rt > 0 and coll.agree(time.time() - t_start > max_rt):
                 break
         self._drain(handles, forest, gains)
         if hprof and built > start + 2:
@@ -388,7 +397,9 @@ class SharedTreeTrainer:
         pass
 
     def _row_sample(self, rate: float, t: int):
+        """Bernoulli(rate) row sample keyed by (seed, tree, GLOBAL row index): identical however the
+        rows are sharded."""
         if rate >= 1.0:
             return self.w
-        m = torch.rand(self.N, generator=self.gen, device=self.dev) < rate
+        m = coll.row_uniform(self.seed, 1000 + t, self.row0, self.N, self.dev) < rate
         return self.w * m.float()

@@ -1,0 +1,157 @@
+"""Row-sharded training through the h2o API (gloo, world_size 2 and 4, CPU).
+
+Every rank runs the same script (SPMD, as under torchrun): ``h2o.init()`` joins the process group,
+``h2o.import_file`` parses its own byte range of the CSV (ParseDataset: domains unified over the
+ranks), and each trainer either all-reduces over the shards (GBM/DRF/XGB/GLM/KMeans/DL/NB/PCA) or
+trains replicated on gathered rows. The sharded run must produce the model and training metrics of
+the single-process run (reference: ``water/MRTask.java`` reduce semantics — the cluster size never
+changes the answer).
+"""
+import json
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _write_csv(path, n=1200, seed=0):
+    rng = np.random.default_rng(seed)
+    x = rng.normal(size=(n, 4))
+    # categorical levels that appear only in some row ranges -> every rank sees a different local domain
+    cat = np.array(["a", "b", "c"])[rng.integers(0, 3, n)].astype(object)
+    cat[-n // 5:] = np.where(rng.random(n // 5) < 0.5, "z_late", cat[-n // 5:])
+    logit = 1.5 * x[:, 0] - x[:, 1] + 0.7 * x[:, 2] * x[:, 3] + (cat == "b") * 0.8 - (cat == "z_late") * 0.5
+    yb = np.where(rng.random(n) < 1 / (1 + np.exp(-logit)), "yes", "no")
+    yr = 2 * x[:, 0] + np.sin(3 * x[:, 1]) + 0.3 * rng.standard_t(3, n)
+    y3 = np.array(["k0", "k1", "k2"])[np.clip((logit > -0.5).astype(int) + (logit > 1.0).astype(int), 0, 2)]
+    with open(path, "w") as f:
+        f.write("x0,x1,x2,x3,cat,yb,yr,y3\n")
+        for i in range(n):
+            xs = ",".join("" if (i % 97 == 5 and j == 2) else f"{x[i, j]:.6f}" for j in range(4))
+            f.write(f"{xs},{cat[i]},{yb[i]},{yr[i]:.6f},{y3[i]}\n")
+
+
+CASES = {
+    "gbm_bernoulli": ("gbm", dict(ntrees=4, max_depth=3, seed=11, sample_rate=0.8, col_sample_rate=0.75), "yb"),
+    "gbm_laplace": ("gbm", dict(ntrees=3, max_depth=3, seed=5, distribution="laplace"), "yr"),
+    "gbm_quantile": ("gbm", dict(ntrees=3, max_depth=3, seed=5, distribution="quantile", quantile_alpha=0.8), "yr"),
+    "gbm_huber": ("gbm", dict(ntrees=3, max_depth=3, seed=5, distribution="huber"), "yr"),
+    "gbm_multinomial": ("gbm", dict(ntrees=3, max_depth=3, seed=3), "y3"),
+    "drf": ("drf", dict(ntrees=4, max_depth=4, seed=7), "yb"),
+    "xgboost": ("xgboost", dict(ntrees=4, max_depth=3, seed=2), "yb"),
+    "glm_default_lambda": ("glm", dict(family="binomial"), "yb"),
+    "glm_lambda_search": ("glm", dict(family="binomial", lambda_search=True, nlambdas=8), "yb"),
+    "glm_gaussian_pvalues": ("glm", dict(family="gaussian", lambda_=0.0, compute_p_values=True), "yr"),
+    "glm_multinomial": ("glm", dict(family="multinomial", lambda_=1e-3), "y3"),
+    "kmeans": ("kmeans", dict(k=3, seed=3, init="Furthest"), None),
+    "pca": ("pca", dict(k=2, transform="STANDARDIZE"), None),
+    "naivebayes": ("naivebayes", dict(), "yb"),
+    "gbm_cv": ("gbm", dict(ntrees=3, max_depth=2, seed=4, nfolds=3), "yb"),
+    "deeplearning": ("deeplearning", dict(hidden=[8, 8], epochs=2, seed=1, mini_batch_size=64, score_interval=1e9), "yb"),
+    "deeplearning_reg": ("deeplearning", dict(hidden=[6], epochs=1, seed=2, mini_batch_size=50, activation="Tanh",
+                                              adaptive_rate=False, rate=0.01, momentum_start=0.5, score_interval=1e9), "yr"),
+    "coxph_gathered": ("isotonicregression", dict(), "yr"),     # a trainer without collectives (gathered rows)
+}
+
+METRIC_KEYS = ("AUC", "logloss", "MSE", "RMSE", "mae", "mean_per_class_error", "tot_withinss", "r2")
+
+
+def _run_cases(csv, names, out_path):
+    sys.path.insert(0, ROOT)
+    import h2o
+    from llama_github_io_amd.models import builder
+    h2o.init(verbose=False)
+    res = {"cloud_size": h2o.cluster().cloud_size}
+    fr = h2o.import_file(csv)
+    res["nrows"] = fr.nrows
+    res["types"] = [fr.type(n) for n in fr.names]
+    res["cat_levels"] = fr["cat"].levels()[0]
+    res["mean_x0"] = fr["x0"].mean()
+    res["sd_x1"] = fr["x1"].sd()[0]
+    res["nacnt"] = fr.nacnt()
+    for name in names:
+        algo, params, y = CASES[name]
+        x = ["x0", "x1", "x2", "x3", "cat"] if algo != "isotonicregression" else ["x0"]
+        if algo in ("kmeans", "pca"):
+            x = ["x0", "x1", "x2", "x3"]
+        m = builder.train(algo, dict(params), x=x, y=y, training_frame=fr)
+        P = m.predict(fr).as_data_frame()
+        num = P.select_dtypes(include=[np.number]).to_numpy(dtype=np.float64)
+        tm = m.output.get("training_metrics") or {}
+        cvm = m.output.get("cross_validation_metrics") or {}
+        res[name] = dict(pred=num.tolist(), metrics={k: tm.get(k) for k in METRIC_KEYS if tm.get(k) is not None},
+                         cv={k: cvm.get(k) for k in METRIC_KEYS if cvm.get(k) is not None})
+    import llama_github_io_amd.parallel.collectives as coll
+    if coll.rank() == 0:
+        with open(out_path, "w") as f:
+            json.dump(res, f)
+
+
+def _worker(rank, world, port, csv, names, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), H2O_AMD_DEVICE="cpu", OMP_NUM_THREADS="1")
+    _run_cases(csv, names, out_path)
+    import torch.distributed as dist
+    if dist.is_initialized():
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def _launch(world, csv, names, out_path):
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_worker, args=(r, world, port, csv, names, out_path)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(600)
+        assert p.exitcode == 0, f"rank exited with {p.exitcode}"
+    with open(out_path) as f:
+        return json.load(f)
+
+
+def _compare(single, sharded, world):
+    assert sharded["cloud_size"] == world and single["cloud_size"] == 1
+    assert sharded["nrows"] == single["nrows"]
+    assert sharded["types"] == single["types"]
+    assert sharded["cat_levels"] == single["cat_levels"]
+    assert sharded["nacnt"] == single["nacnt"]
+    assert np.allclose(sharded["mean_x0"], single["mean_x0"], rtol=1e-12, atol=1e-14)
+    assert np.allclose(sharded["sd_x1"], single["sd_x1"], rtol=1e-12, atol=1e-14)
+    for name in CASES:
+        if name not in single:
+            continue
+        a, b = np.asarray(single[name]["pred"]), np.asarray(sharded[name]["pred"])
+        assert a.shape == b.shape, name
+        tol = 1e-4 if name.startswith(("glm_multinomial", "glm_lambda", "glm_default", "deeplearning")) else 2e-5
+        assert np.allclose(a, b, atol=tol, rtol=tol), (name, np.abs(a - b).max())
+        for k, v in single[name]["metrics"].items():
+            assert abs(v - sharded[name]["metrics"][k]) <= tol * max(1.0, abs(v)), (name, k, v, sharded[name]["metrics"][k])
+        for k, v in single[name]["cv"].items():
+            # fold models equal to the last float32 bit of a leaf value; those 1-ulp differences can
+            # re-order tied holdout scores inside AUC, hence the looser bound
+            assert abs(v - sharded[name]["cv"][k]) <= 1e-4 * max(1.0, abs(v)), (name, "cv", k)
+
+
+@pytest.fixture(scope="module")
+def csv_and_single(tmp_path_factory):
+    d = tmp_path_factory.mktemp("dist")
+    csv = str(d / "data.csv")
+    _write_csv(csv)
+    single = _launch(1, csv, list(CASES), str(d / "single.json"))
+    return csv, single, d
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_api_equals_single(csv_and_single, world):
+    csv, single, d = csv_and_single
+    sharded = _launch(world, csv, list(CASES), str(d / f"w{world}.json"))
+    _compare(single, sharded, world)
