@@ -92,8 +92,10 @@ class AutoML:
                       fold_column=fold_column, weights_column=weights_column)
         if self.stopping["stopping_rounds"]:
             common.update(stopping_rounds=self.stopping["stopping_rounds"], stopping_metric=self.stopping["stopping_metric"])
-        budget = lambda: (self.max_runtime_secs <= 0 or time.time() - t0 < self.max_runtime_secs) and \
-            (not self.max_models or len(self.models) < self.max_models)  # noqa: E731
+        from .parallel import collectives as coll
+        # every rank takes rank 0's budget decision (a rank must not start a model the others skip)
+        budget = lambda: coll.agree((self.max_runtime_secs <= 0 or time.time() - t0 < self.max_runtime_secs) and
+                                    (not self.max_models or len(self.models) < self.max_models))  # noqa: E731
         steps = _plan(self.seed)
         rng = np.random.default_rng(self.seed)
         i = 0
@@ -115,7 +117,7 @@ class AutoML:
             if self.per_model:
                 p["max_runtime_secs"] = self.per_model
             elif self.max_runtime_secs > 0:
-                p["max_runtime_secs"] = max(1.0, self.max_runtime_secs - (time.time() - t0))
+                p["max_runtime_secs"] = coll.broadcast_object(max(1.0, self.max_runtime_secs - (time.time() - t0)))
             mid = f"{name}_AutoML_{self.project_name}"
             try:
                 m = builder.train(algo, p, x, y, training_frame, validation_frame, job, mid)
@@ -146,9 +148,13 @@ class AutoML:
                 continue
             mid = f"StackedEnsemble_{name}_1_AutoML_{self.project_name}"
             try:
-                se = builder.train("stackedensemble", dict(base_models=[m.key for m in ms], seed=self.seed), x, y, fr,
-                                   valid, job, mid)
-                se.output["cross_validation_metrics"] = se.output["training_metrics"]
+                # StackedEnsembleStepsProvider.setMetalearnerParameters: the metalearner is cross-validated
+                # with the AutoML nfolds, and its out-of-fold metrics are what the leaderboard ranks
+                sp = dict(base_models=[m.key for m in ms], seed=self.seed, metalearner_nfolds=self.nfolds,
+                          metalearner_fold_assignment="Modulo", keep_levelone_frame=True)
+                if cat in ("Binomial", "Multinomial"):
+                    sp["metalearner_transform"] = "Logit"
+                se = builder.train("stackedensemble", sp, x, y, fr, valid, job, mid)
                 self.models.append(se)
             except Exception as e:  # noqa: BLE001
                 self._log(f"{mid} failed: {e!r}")

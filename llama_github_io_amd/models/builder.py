@@ -186,8 +186,12 @@ def train(algo: str, params: dict, x=None, y=None, training_frame=None, validati
     from ..parallel import collectives as coll, dframe
     import contextlib
     mode = contextlib.ExitStack()
-    if coll.world_active():
-        if algo in DISTRIBUTED and str(p.get("solver", "")).upper() != "L_BFGS_SERIAL":
+    if coll.world_active() and not coll.is_dist():
+        # nested inside a replicated computation (e.g. a metalearner fit inside a gathered trainer)
+        fr = dframe.gather_frame(fr)
+        validation_frame = dframe.gather_frame(validation_frame)
+    elif coll.world_active():
+        if algo in DISTRIBUTED:
             fr = dframe.shard_frame(fr)
             validation_frame = dframe.shard_frame(validation_frame) if validation_frame is not None else None
         else:
@@ -235,6 +239,7 @@ def _train(spec, algo, p, x, y, fr, validation_frame, job, model_id):
         model.output["validation_frame"] = validation_frame.frame_id
     if cv_out is not None:
         model.cv_holdout = cv_out.pop("_cv_holdout", None)
+        model.cv_holdout_sharded = coll_is_dist()       # holdout rows are this rank's shard
         model.output.update(cv_out)
     if p.get("custom_metric_func") and yv is not None:
         _custom_metric(model, p["custom_metric_func"], X, yv, w, off, "training_metrics")
@@ -249,6 +254,11 @@ def _train(spec, algo, p, x, y, fr, validation_frame, job, model_id):
         from ..persist import save_model
         save_model(model, p["export_checkpoints_dir"], force=True)
     return model
+
+
+def coll_is_dist():
+    from ..parallel import collectives as coll
+    return coll.is_dist()
 
 
 def _calibrate(model, p, job):

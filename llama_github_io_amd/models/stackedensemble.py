@@ -16,6 +16,11 @@ from ..core import dkv
 from .base import DataInfo, Model, make_key
 
 
+def builder_train(algo, params, x, y, frame, model_id):
+    from .builder import train
+    return train(algo, params, x, y, frame, None, None, model_id)
+
+
 def _level_one(models, X, offset, category):
     cols = []
     for m in models:
@@ -42,6 +47,8 @@ class StackedEnsembleModel(Model):
 
     def _predict_tensor(self, X, offset=None):
         L1 = _level_one(self.base_models(), X, offset, self.model_category)
+        if self.output.get("metalearner_transform") == "logit":
+            L1 = _logit(L1)
         return self.meta.score_tensor(L1)
 
     def metalearner(self):
@@ -64,10 +71,16 @@ class StackedEnsembleModel(Model):
         self.meta = _from_state(dict(s["meta"]))
 
 
+def _logit(P):
+    p = P.double().clamp(1e-15, 1 - 1e-15)
+    return torch.log(p / (1 - p)).float()
+
+
 class StackedEnsembleTrainer:
     def __init__(self, params):
         p = dict(base_models=[], metalearner_algorithm="AUTO", metalearner_params=None, metalearner_nfolds=0,
-                 seed=-1, blending_frame=None)
+                 metalearner_fold_assignment="AUTO", metalearner_fold_column=None, metalearner_transform="NONE",
+                 keep_levelone_frame=False, seed=-1, blending_frame=None)
         p.update({k: v for k, v in params.items() if v is not None})
         self.p = p
         self.job = None
@@ -96,12 +109,15 @@ class StackedEnsembleTrainer:
         if not models:
             raise ValueError("StackedEnsemble needs base_models")
         cat = model_category(info)
+        from ..parallel import collectives as coll, dframe
         holds = []
         for m in models:
             h = getattr(m, "cv_holdout", None)
             if h is None:
                 raise ValueError(f"base model {m.key} has no cross-validation holdout predictions "
                                  "(train it with nfolds>1 and keep_cross_validation_predictions=True)")
+            if getattr(m, "cv_holdout_sharded", False) and not coll.is_dist():
+                h = dframe.gather_tensor(h.cpu() if coll.comm_device().type == "cpu" else h).to(X.device)
             if cat == "Binomial":
                 holds.append(h[:, 1:2].float())
             elif cat == "Multinomial":
@@ -109,13 +125,17 @@ class StackedEnsembleTrainer:
             else:
                 holds.append(h.reshape(-1, 1).float())
         L1 = torch.cat(holds, 1).T.contiguous().to(X.device)
+        transform = str(self.p.get("metalearner_transform") or "NONE").lower()
+        if transform == "logit":
+            if cat not in ("Binomial", "Multinomial"):
+                raise ValueError("metalearner_transform=Logit needs a categorical response")
+            L1 = _logit(L1)
         names = []
         for m in models:
             if cat == "Multinomial":
                 names += [f"{m.key}/{d}" for d in info.response_domain]
             else:
                 names.append(m.key)
-        minfo = DataInfo(names, np.zeros(len(names), np.int32), [None] * len(names), info.response, info.response_domain)
         algo = str(self.p["metalearner_algorithm"]).lower()
         mp = dict(self.p["metalearner_params"] or {})
         if algo in ("auto", "glm"):
@@ -128,19 +148,47 @@ class StackedEnsembleTrainer:
         elif algo == "naivebayes":
             algo = "naivebayes"
         mp.setdefault("seed", self.p.get("seed", -1))
-        trainer = REGISTRY[algo].trainer(mp)
-        meta = trainer.fit(L1, y, w, None, minfo, None, (model_key or make_key("se")) + "_metalearner")
+        # the metalearner is a regular model trained on the level-one frame (StackedEnsemble.java
+        # buildMetalearner): with metalearner_nfolds it is cross-validated there, so the ensemble's
+        # cross-validation metrics are out-of-fold twice over (base holdouts -> metalearner holdouts)
+        from ..frame import Column, H2OFrame
+        with dframe.shard_ctx(None):
+            cols = [Column(n, "real", L1[i].double()) for i, n in enumerate(names)]
+            if info.response_domain is not None:
+                yc = torch.nan_to_num(y.float(), nan=-1).to(torch.int32)
+                cols.append(Column(info.response, "enum", yc, list(info.response_domain)))
+            else:
+                cols.append(Column(info.response, "real", y.double()))
+            wname = None
+            if w is not None:
+                wname = "__se_weights"
+                cols.append(Column(wname, "real", w.double()))
+            fold_col = self.p.get("metalearner_fold_column")
+            if fold_col:
+                raise ValueError("metalearner_fold_column: pass the fold ids as metalearner_params['fold_column'] "
+                                 "of a column present in the level-one frame")
+            l1_frame = H2OFrame._from_columns(cols)
+        nf = int(self.p.get("metalearner_nfolds") or 0)
+        if nf > 1:
+            fa = str(self.p.get("metalearner_fold_assignment") or "AUTO")
+            mp.update(nfolds=nf, fold_assignment="Random" if fa.upper() == "AUTO" else fa,
+                      keep_cross_validation_predictions=True)
+        if wname:
+            mp["weights_column"] = wname
+        meta = builder_train(algo, mp, names, info.response, l1_frame,
+                             (model_key or make_key("se")) + "_metalearner")
         model = StackedEnsembleModel(model_key or make_key("stackedensemble"), self.p, info)
         model.device = X.device
         model.base_keys = [m.key for m in models]
         model.meta = meta
         model.output["base_models"] = model.base_keys
         model.output["metalearner"] = meta.key
+        model.output["metalearner_transform"] = transform
         model.output["training_metrics"] = model.metrics_for(X, y, w, offset)
-        # CV estimate: metalearner applied to the out-of-fold level-one matrix
-        from .. import metrics as mm
-        Ph = meta.score_tensor(L1)
-        model.output["cross_validation_metrics"] = mm.make_metrics(cat, y, Ph, w, info.response_domain)
+        # out-of-fold estimate only: the metalearner's own cross-validation (never its training fit)
+        model.output["cross_validation_metrics"] = meta.output.get("cross_validation_metrics")
+        if self.p.get("keep_levelone_frame"):
+            model.output["levelone_frame_id"] = l1_frame.frame_id
         if valid is not None:
             Xv, yv, wv, ov = valid
             model.output["validation_metrics"] = model.metrics_for(Xv, yv, wv, ov)
