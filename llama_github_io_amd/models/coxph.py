@@ -91,10 +91,27 @@ class CoxPHModel(Model):
         keep = getattr(self, "keep", None)
         X = X.to(self.device)
         Z = self.expander.transform(X if keep is None else X[keep]).double()
-        lp = Z @ self.beta.to(Z.device) - float(self.output["lp_mean"])
+        lp = Z @ self.beta.to(Z.device) - self._lp_base(X)
         if offset is not None:
             lp = lp + offset.double()
         return lp.float()
+
+    def _lp_base(self, X):
+        """Per-row centring term: the weighted mean linear predictor of the row's stratum
+        (CoxPHModel.java:405 subtracts _lpBase[stratum]); rows of an unseen stratum get NaN."""
+        bases = self.output.get("lp_base")
+        sv = getattr(self, "strata_values", [])
+        if not self.strata_idx or not bases or not sv:
+            return float(self.output["lp_mean"])
+        N = X.shape[1]
+        out = torch.full((N,), float("nan"), dtype=torch.float64, device=X.device)
+        S = X[self.strata_idx].double()
+        for k, vals in enumerate(sv):
+            m = torch.ones(N, dtype=torch.bool, device=X.device)
+            for j, v in enumerate(vals):
+                m &= S[j] == float(v)
+            out = torch.where(m, torch.full_like(out, float(bases[k])), out)
+        return out
 
     def prediction_names(self):
         return ["lp"]
@@ -149,15 +166,20 @@ class CoxPHTrainer:
             start = X[j_start].double()
         strata = None
         strata_idx = []
+        strata_values = []
         if p["stratify_by"]:
             sb = p["stratify_by"] if isinstance(p["stratify_by"], (list, tuple)) else [p["stratify_by"]]
-            codes = torch.zeros(X.shape[1], dtype=torch.float64, device=X.device)
             for c in sb:
                 j = info.x.index(c)
                 special.append(j)
                 strata_idx.append(j)
-                codes = codes * 1000 + torch.nan_to_num(X[j].double(), nan=-1)
-            strata = codes
+            S = X[strata_idx].double()
+            if bool(torch.isnan(S).any()):
+                # genmodel's Strata key casts NaN to 0: an NA stratum could not be looked up by a MOJO scorer
+                raise ValueError("stratify_by columns must not contain missing values")
+            # stratum id = row of the unique (value tuple) table: no positional code collisions
+            uniq, strata = torch.unique(S.T, dim=0, return_inverse=True)
+            strata_values = uniq.cpu().tolist()
         keep = [j for j in range(info.F) if j not in special]
         sub = DataInfo([info.x[j] for j in keep], np.asarray(info.iscat)[keep], [info.domains[j] for j in keep],
                        info.response, info.response_domain)
@@ -210,12 +232,19 @@ class CoxPHTrainer:
         model.beta = beta
         model.keep, model.strata_idx = keep, strata_idx
         model.special_idx = [j for j in special if j not in strata_idx]
-        model.strata_values = ([] if not strata_idx else
-                               torch.unique(torch.nan_to_num(X[strata_idx].double(), nan=-1).T, dim=0).cpu().tolist())
+        model.strata_values = strata_values
         lp = Z @ beta
         model.output["lp_mean"] = float((w * lp).sum() / w.sum())
         # weighted design means: the MOJO's x_mean_cat / x_mean_num (lp_mean = z_mean . beta)
         model.output["z_mean"] = ((w[:, None] * Z).sum(0) / w.sum()).cpu().tolist()
+        if strata is not None:
+            # one mean (and lp base) per stratum, in strata_values order (CoxPH.java:400-408)
+            K = len(strata_values)
+            ws = torch.zeros(K, dtype=torch.float64, device=dev).index_add_(0, strata, w)
+            zs = torch.zeros(K, Z.shape[1], dtype=torch.float64, device=dev).index_add_(0, strata, w[:, None] * Z)
+            zmean_s = zs / ws.clamp(min=1e-300)[:, None]
+            model.output["z_mean_strata"] = zmean_s.cpu().tolist()
+            model.output["lp_base"] = (zmean_s @ beta).cpu().tolist()
         names = ex.names
         model.output["coefficients"] = dict(zip(names, beta.cpu().tolist()))
         model.output["coefficients_table"] = [dict(names=n, coefficients=float(b), exp_coef=math.exp(float(b)),

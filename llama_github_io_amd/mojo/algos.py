@@ -449,10 +449,12 @@ def write_coxph(model, kv, blobs):
     kv["use_all_factor_levels"] = "true" if ex.use_all else "false"
     kv["num_numerical_columns"] = len(ex.nums)
     kv["num_offsets"] = _arr([nc + i for i in range(len(ex.nums))])
-    for t, part in (("x_mean_cat", zm[:nc]), ("x_mean_num", zm[nc:])):
+    zs = model.output.get("z_mean_strata") if strata else None
+    rows = zs if zs is not None else [zm] * S      # one design-mean row per stratum, strata_i order
+    for t, sl in (("x_mean_cat", slice(0, nc)), ("x_mean_num", slice(nc, None))):
         kv[f"{t}_size1"] = S
-        kv[f"{t}_size2"] = len(part)
-        blobs[t] = _blob_rect([part] * S)
+        kv[f"{t}_size2"] = len(zm[sl])
+        blobs[t] = _blob_rect([r[sl] for r in rows])
     kv["strata_count"] = len(strata)
     for i, s in enumerate(strata):
         kv[f"strata_{i}"] = _arr(s)

@@ -74,13 +74,20 @@ def custom_metric_value(ref: str, preds: np.ndarray, actual: np.ndarray, w=None,
     w = np.ones(n) if w is None else np.asarray(w, dtype=np.float64)
     o = np.zeros(n) if offset is None else np.asarray(offset, dtype=np.float64)
     try:                                    # vectorised: columns in, per-row state columns out, summed
-        st = [np.broadcast_to(np.asarray(s, dtype=np.float64), (n,)) for s in obj.map(preds.T, actual[None, :], w, o,
-                                                                                          model)]
-        if n >= 2:   # the column sum stands in for reduce only when reduce is element-wise addition
-            a, b = [float(s[0]) for s in st], [float(s[1]) for s in st]
-            if not np.allclose(np.asarray(obj.reduce(a, b), dtype=np.float64), np.add(a, b), rtol=1e-12, atol=0):
-                raise ValueError("non-additive reduce")
-        state = [float(np.sum(s)) for s in st]
+        st = [np.broadcast_to(np.asarray(s, dtype=np.float64), (n,)).copy() for s in obj.map(preds.T, actual[None, :], w, o,
+                                                                                                 model)]
+        # the user's reduce itself, applied as a pairwise tree fold over the state columns (log2(N)
+        # vectorised calls; MRTask reduces the same way, so reduce must be associative anyway)
+        while st[0].shape[0] > 1:
+            m = st[0].shape[0]
+            h = m // 2
+            left = [s[:2 * h:2] for s in st]
+            right = [s[1:2 * h:2] for s in st]
+            red = [np.broadcast_to(np.asarray(r, dtype=np.float64), (h,)) for r in obj.reduce(left, right)]
+            if len(red) != len(st):
+                raise ValueError("reduce changed the state arity")
+            st = [np.concatenate([r, s[2 * h:]]) for r, s in zip(red, st)]
+        state = [float(s[0]) for s in st]
         if not all(np.isfinite(v) for v in state):
             raise ValueError("non-finite vectorised state")
     except Exception:                       # noqa: BLE001 - scalar-only user code: row-wise path

@@ -195,8 +195,25 @@ def test_coxph_mojo_reference_layout(tmp_path, strata):
     cols = mj["columns"]
     assert cols[: (2 if strata else 1)] == (["s", "g"] if strata else ["g"])
     assert np.allclose(a.values.astype(float), b.values.astype(float), atol=1e-5)
-    # lp is centred: weighted mean of the training linear predictor is 0
-    assert abs(float(a.values.astype(float).mean())) < 1e-6
+    # lp is centred per stratum (CoxPHModel.java:405 _lpBase[stratum]): mean 0 inside every stratum
+    lp = a.values.astype(float).reshape(-1)
+    groups = d["s"].values if strata else np.zeros(n)
+    for gval in np.unique(groups):
+        assert abs(float(lp[groups == gval].mean())) < 1e-6
+    if strata:
+        xm = np.frombuffer(mj["files"]["x_mean_num"], dtype=">f8")
+        assert xm.size == 2 and xm[0] != xm[1]          # a real design-mean row per stratum
+
+
+def test_coxph_rejects_na_strata():
+    from h2o.estimators import H2OCoxProportionalHazardsEstimator
+    h2o.init(verbose=False)
+    d = pd.DataFrame({"time": [1.0, 2, 3, 4, 5, 6], "x": [0.1, 0.5, -0.2, 0.3, 1.0, -1.0],
+                      "s": ["a", None, "b", "a", "b", "a"], "event": [1, 0, 1, 1, 0, 1]})
+    fr = h2o.H2OFrame(d, column_types={"s": "enum"})
+    m = H2OCoxProportionalHazardsEstimator(stop_column="time", stratify_by=["s"])
+    with pytest.raises(Exception, match="missing"):
+        m.train(x=["time", "x", "s"], y="event", training_frame=fr)
 
 
 @pytest.mark.parametrize("y,blending", [("y", True), ("r", False), ("m", True)])

@@ -163,3 +163,27 @@ def test_grid_recovery_resumes_without_retraining(df, tmp_path, monkeypatch):
     assert sorted(h[0] for h in g.hyper_values) == [2, 3, 4, 5]
     assert not os.path.exists(rdir)              # cleaned up on success
     _ = gs
+
+
+class MaxAbsError:
+    """Non-additive reduce (max): the vectorised path must fold with reduce, never sum."""
+    def map(self, pred, act, w, o, model):
+        import numpy as _np
+        return [_np.abs(_np.asarray(act[0]) - _np.asarray(pred[0]))]
+
+    def reduce(self, l, r):
+        import numpy as _np
+        return [_np.maximum(l[0], r[0])]
+
+    def metric(self, l):
+        return l[0]
+
+
+def test_custom_metric_non_additive_reduce(df):
+    ref = h2o.upload_custom_metric(MaxAbsError, func_name="maxerr")
+    m = H2OGradientBoostingEstimator(ntrees=3, seed=1, custom_metric_func=ref)
+    m.train(x=["a", "b", "seg"], y="r", training_frame=df)
+    tm = m._model.output["training_metrics"]
+    p = m.predict(df).as_data_frame().iloc[:, 0].values
+    r = df["r"].as_data_frame().iloc[:, 0].values
+    assert tm["custom_metric_value"] == pytest.approx(float(np.max(np.abs(r - p))), rel=1e-5)
