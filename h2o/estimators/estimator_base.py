@@ -20,8 +20,17 @@ class H2OEstimator:
         object.__setattr__(self, "_model", None)
         object.__setattr__(self, "_job", None)
         object.__setattr__(self, "model_id", model_id)
+        from ._schema import PARAMS
+        known = PARAMS.get(self.algo)
         for k, v in kwargs.items():
-            self._parms[self._param_aliases.get(k, k)] = v
+            kk = self._param_aliases.get(k, k)
+            if known is not None and k not in known and kk not in known and not k.startswith("_") and \
+                    k not in ("segment_columns", "segment_models_id"):
+                # the reference estimators have explicit signatures: an unknown keyword is a TypeError
+                from llama_github_io_amd.models import builder as _b
+                if self.algo not in _b.REGISTRY or kk not in _b.extension_params(self.algo):
+                    raise TypeError(f"{type(self).__name__}.__init__() got an unexpected keyword argument '{k}'")
+            self._parms[kk] = v
 
     # ---- parameter access like h2o-py properties
     def __setattr__(self, k, v):

@@ -1464,6 +1464,8 @@ struct TreePlan {
   int compute_amax, k_cols, packed, leaf_native, log_link, pad1;
   unsigned long long seed;
   double scale, kclamp, mx;
+  int kc_level[TP_MAXL];   // per-level column sample size (col_sample_rate_change_per_level); 0 = k_cols
+  int pad2;
 };
 
 static inline void tp_level_buf(const TreePlan* P, int e, const void*& b, const void*& a, const void*& r) {
@@ -1509,7 +1511,8 @@ int h2o_tree_level(const TreePlan* P, int d, int dist, hipStream_t s) {
                           P->lam, P->alpha, P->gamma, P->mode, P->random_split, P->seed, d, P->cand,
                           d == 0 ? P->rootw : nullptr, s);
   if (rc) return -rc;
-  rc = h2o_split_reduce(P->cand, P->meta[d], cap, P->F, P->feat_ok, P->k_cols, P->seed, d, P->dec[d], s);
+  const int kc = P->kc_level[d] > 0 ? P->kc_level[d] : P->k_cols;
+  rc = h2o_split_reduce(P->cand, P->meta[d], cap, P->F, P->feat_ok, kc, P->seed, d, P->dec[d], s);
   if (rc) return -rc;
   rc = h2o_plan(P->nodes[d], P->meta[d], P->dec[d], P->nl[d], odd ? P->nl[d - 1] : nullptr, P->cur[d], P->cl[d],
                 P->cr[d], P->nodes[d + 1], P->tp[d + 1], P->meta[d + 1], P->bp[d + 1], P->counters, P->scratch, d,

@@ -133,7 +133,7 @@ def _with_rows_of(fn):
         if not isinstance(frame, H2OFrame):
             return fn(self, frame, *a, **k)
         with rows_of(frame):
-            return fn(self, frame, *a, **k)
+            return fn(self, self._adapt(frame), *a, **k)
     w._rows_of = True
     return w
 
@@ -178,10 +178,21 @@ class Model:
 
     def score_tensor(self, X: torch.Tensor, offset=None) -> torch.Tensor:
         """Returns the prediction matrix: regression [N]; classification [N, K] probabilities."""
-        return self._predict_tensor(X.to(self.device), None if offset is None else offset.to(self.device))
+        P = self._predict_tensor(X.to(self.device), None if offset is None else offset.to(self.device))
+        bal = self.output.get("model_class_distrib") if isinstance(self.output, dict) else None
+        if bal and P.dim() == 2 and P.shape[1] == len(bal):
+            from .adapt import correct_probabilities        # balance_classes: back to the prior distribution
+            P = correct_probabilities(P, self.output["prior_class_distrib"], bal)
+        return P
+
+    def _adapt(self, frame):
+        """Replay the training frame's categorical encoding / interaction columns (models/adapt.py)."""
+        ad = getattr(self, "adapter", None)
+        return ad.apply(frame) if ad else frame
 
     def predict(self, frame):
         from ..frame import H2OFrame
+        frame = self._adapt(frame)
         with rows_of(frame):
             X, offset = frame.model_matrix(self.info, device=self.device)
             P = self.score_tensor(X, offset)
@@ -235,6 +246,7 @@ class Model:
             if xval:
                 return self.output.get("cross_validation_metrics")
             return self.output.get("training_metrics")
+        test_data = self._adapt(test_data)
         with rows_of(test_data):
             X, offset = test_data.model_matrix(self.info, device=self.device)
             y = test_data.response_tensor(self.info, device=self.device)
@@ -304,10 +316,16 @@ class Model:
             cs = cm.to_state()
             cs["__class__"] = type(cm).__module__ + ":" + type(cm).__name__
             st["calibration"] = cs
+        ad = getattr(self, "adapter", None)
+        if ad:
+            st["adapter"] = ad.to_state()
         return st
 
     def _restore(self, state):
         self.output = state["output"]
+        if state.get("adapter"):
+            from .adapt import FrameAdapter
+            self.adapter = FrameAdapter.from_state(state["adapter"])
         if state.get("calibration"):
             from ..persist import _from_state
             self.calibration_model = _from_state(dict(state["calibration"]))

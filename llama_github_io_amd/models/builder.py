@@ -166,6 +166,7 @@ def _seed_of(params):
 def train(algo: str, params: dict, x=None, y=None, training_frame=None, validation_frame=None, job: Job | None = None,
           model_id: str | None = None) -> Model:
     spec = REGISTRY[algo]
+    _validate(spec, algo, params)
     p = dict(spec.defaults)
     p.update({k: v for k, v in params.items() if v is not None})
     if algo == "grep":                          # raw-text scan: no DataInfo / device tensors
@@ -202,11 +203,50 @@ def train(algo: str, params: dict, x=None, y=None, training_frame=None, validati
         return _train(spec, algo, p, x, y, fr, validation_frame, job, model_id)
 
 
+_EXTRA = {}
+
+
+def extension_params(algo) -> set:
+    """Parameters a trainer accepts beyond the h2o-py schema (its own defaults: engine extensions such
+    as ``compute_dtype``, ``seed`` where the reference has none, ...)."""
+    if algo not in _EXTRA:
+        spec = REGISTRY[algo]
+        extra = set(COMMON) | set(spec.defaults) | {"model_id", "max_categorical_levels"}
+        try:
+            extra |= set(getattr(spec.trainer({}), "p", {}) or {})
+        except Exception:  # noqa: BLE001 - trainers that need arguments to construct
+            pass
+        _EXTRA[algo] = extra
+    return _EXTRA[algo]
+
+
+def _validate(spec, algo, params):
+    """ModelBuilder.init: unknown / unsupported parameters are errors, never silent no-ops."""
+    from . import params as pv
+    pv.validate(algo, params, extension_params(algo))
+
+
 def _train(spec, algo, p, x, y, fr, validation_frame, job, model_id):
     info = prepare(algo, p, x, y, fr)
     if not info.x:
         raise ValueError("no usable predictor columns")
+    from .adapt import balance_indices, fit_adapter
+    adapter, fr2, x2 = fit_adapter(algo, p, fr, list(info.x), info.response)
+    if adapter:
+        fr = fr2
+        info = prepare(algo, p, x2, y, fr)
+        if validation_frame is not None:
+            validation_frame = adapter.apply(validation_frame)
     X, yv, w, off = tensors(fr, info)
+    balance = None
+    if p.get("balance_classes") and info.response_domain is not None and yv is not None:
+        from ..parallel import collectives as coll
+        idx, prior, mdist = balance_indices(p, yv, len(info.response_domain), coll.row_offset(X.shape[1]))
+        X = X[:, idx].contiguous()
+        yv = yv[idx]
+        w = None if w is None else w[idx]
+        off = None if off is None else off[idx]
+        balance = (prior, mdist)
     if yv is not None and info.response_domain is None and spec.classification_only:
         raise ValueError(f"{algo} needs a categorical response")
     valid = None
@@ -231,6 +271,10 @@ def _train(spec, algo, p, x, y, fr, validation_frame, job, model_id):
     model = tr.fit(X, yv, w, off, info, valid, mid) if yv is not None or not spec.supervised else tr.fit(X, yv, w, off, info, valid, mid)
     model.params.update({k: p.get(k) for k in COMMON if k in p and k not in ("training_frame", "validation_frame", "x", "y",
                                                                               "calibration_frame")})
+    if adapter:
+        model.adapter = adapter
+    if balance is not None:
+        model.output["prior_class_distrib"], model.output["model_class_distrib"] = balance
     model.output["names"] = info.x + ([info.response] if info.response else [])
     model.output["response_column_name"] = info.response
     model.output["domains"] = info.domains

@@ -21,8 +21,9 @@ from ..ops.segment import segment_sum
 
 class Expander:
     def __init__(self, info: DataInfo, standardize=True, use_all_factor_levels=False, missing="MeanImputation",
-                 missing_bucket=False, center_only=False):
+                 missing_bucket=False, center_only=False, plug_values=None):
         self.info = info
+        self.plug_values = plug_values   # missing_values_handling="PlugValues": {column: value or level}
         self.standardize = bool(standardize)
         self.center_only = bool(center_only)
         self.use_all = bool(use_all_factor_levels)
@@ -80,6 +81,23 @@ class Expander:
         var = (s2 - sw * mu * mu) / (sw - 1).clamp(min=1e-300)
         sd = var.clamp(min=0).sqrt()
         self.num_mean = mu
+        self.num_fill = None
+        if str(self.missing).lower() == "plugvalues":
+            pv = self._plug_dict()
+            fill = mu.clone()
+            for i, j in enumerate(self.nums):
+                nm = self.info.x[j]
+                if nm in pv:
+                    fill[i] = float(pv[nm])
+            self.num_fill = fill
+            for i, j in enumerate(self.cats):
+                nm = self.info.x[j]
+                if nm in pv:
+                    dom = list(self.info.domains[j] or [])
+                    v = str(pv[nm])
+                    if v not in dom:
+                        raise ValueError(f"plug_values: level {v!r} is not in the domain of {nm}")
+                    self.cat_modes[i] = dom.index(v)
         self.num_sd = torch.where(sd > 0, sd, torch.ones_like(sd))
         self.num_sd_raw = sd
         names += [self.info.x[j] for j in self.nums]
@@ -114,10 +132,12 @@ class Expander:
             rows = torch.nonzero(valid, as_tuple=True)[0]
             Z[rows, idx[rows]] = 1
         CH = 32
+        fill_all = getattr(self, "num_fill", None)
         for a in range(0, len(self.nums), CH):
             Xn = X[self.nums[a:a + CH]].to(dtype=torch.float64)
             mu = self.num_mean[a:a + CH, None]
-            Xn = torch.where(torch.isnan(Xn), mu.expand_as(Xn), Xn)
+            fill = mu if fill_all is None else fill_all[a:a + CH, None].to(mu.device)
+            Xn = torch.where(torch.isnan(Xn), fill.expand_as(Xn), Xn)
             if self.standardize:
                 Xn = (Xn - mu) / self.num_sd[a:a + CH, None]
             elif self.center_only:
@@ -125,6 +145,16 @@ class Expander:
             Z[:, self.num_off + a:self.num_off + a + Xn.shape[0]] = Xn.T.to(dtype)
             del Xn
         return Z
+
+    def _plug_dict(self):
+        pv = self.plug_values
+        if pv is None:
+            raise ValueError("missing_values_handling='PlugValues' needs plug_values")
+        if hasattr(pv, "as_data_frame"):
+            pv = pv.as_data_frame()
+        if hasattr(pv, "iloc"):
+            return {str(c): pv[c].iloc[0] for c in pv.columns}
+        return dict(pv)
 
     def row_mask_complete(self, X: torch.Tensor) -> torch.Tensor:
         """Rows with no NA (for ``missing_values_handling='Skip'``)."""
@@ -142,8 +172,10 @@ class Expander:
         return b, ic
 
     def to_state(self):
+        nf = getattr(self, "num_fill", None)
         return dict(standardize=self.standardize, use_all=self.use_all, missing=self.missing,
                     missing_bucket=self.missing_bucket, center_only=self.center_only,
+                    num_fill=None if nf is None else nf.cpu().tolist(),
                     cat_offsets=self.cat_offsets, cat_sizes=self.cat_sizes, cat_modes=self.cat_modes,
                     num_off=self.num_off, num_mean=self.num_mean.cpu().tolist(), num_sd=self.num_sd.cpu().tolist(),
                     num_sd_raw=self.num_sd_raw.cpu().tolist(), names=self.names, P=self.P)
@@ -157,6 +189,7 @@ class Expander:
         e.num_mean = torch.tensor(s["num_mean"], dtype=torch.float64, device=dev)
         e.num_sd = torch.tensor(s["num_sd"], dtype=torch.float64, device=dev)
         e.num_sd_raw = torch.tensor(s["num_sd_raw"], dtype=torch.float64, device=dev)
+        e.num_fill = None if s.get("num_fill") is None else torch.tensor(s["num_fill"], dtype=torch.float64, device=dev)
         e.fitted = True
         return e
 
@@ -164,4 +197,6 @@ class Expander:
         self.num_mean = self.num_mean.to(device)
         self.num_sd = self.num_sd.to(device)
         self.num_sd_raw = self.num_sd_raw.to(device)
+        if getattr(self, "num_fill", None) is not None:
+            self.num_fill = self.num_fill.to(device)
         return self

@@ -37,7 +37,8 @@ DL_DEFAULTS = dict(hidden=[200, 200], epochs=10.0, activation="Rectifier", adapt
                    stopping_rounds=5, stopping_metric="AUTO", stopping_tolerance=0.0, score_interval=5.0,
                    score_training_samples=10000, seed=-1, shuffle_training_data=True, reproducible=False,
                    export_weights_and_biases=False, missing_values_handling="MeanImputation", max_runtime_secs=0.0,
-                   compute_dtype="float32", gpu_batch_size=256, train_samples_per_iteration=-2)
+                   compute_dtype="float32", gpu_batch_size=256, train_samples_per_iteration=-2,
+                   overwrite_with_best_model=True)
 
 
 class MLP(torch.nn.Module):
@@ -306,6 +307,10 @@ class DeepLearningTrainer:
                 with torch.no_grad():
                     fp.adadelta(rho, eps, l1, l2)
         gbuf = torch.empty(fp.g.numel() + 1, dtype=fp.g.dtype, device=fp.g.device) if sharded else None
+        # overwrite_with_best_model (default true, off with n-fold CV): the final weights are those of the
+        # scoring event with the lowest Model.loss() (stopping metric; AUTO = logloss / deviance / MSE)
+        owb = bool(p.get("overwrite_with_best_model", True)) and not int(p.get("nfolds") or 0)
+        best_loss, best_p, last_ev = float("inf"), None, {}
         for step in range(total):
             if pos + B > N_glob:
                 # mini-batches are drawn from the GLOBAL row order: under row sharding each rank takes the
@@ -393,11 +398,22 @@ class DeepLearningTrainer:
                 last_score = time.time()
                 ev = self._score(model, X, y, w, samples / N_glob, valid)
                 history.append({k: v for k, v in ev.items() if not k.startswith("_")})
+                last_ev = ev
+                if owb:
+                    lv = self._model_loss(ev.get("_valid") or ev.get("_train"), cat, ae)
+                    if lv < best_loss:     # DeepLearningModel.doScoring: keep the lowest-loss weights
+                        best_loss, best_p = lv, fp.p.detach().clone()
                 mref = ev.get("_valid") or ev.get("_train")
                 if mref is not None and not end and keeper.add(mref):
                     break
                 if float(p["max_runtime_secs"] or 0) > 0 and coll.agree(time.time() - t0 > float(p["max_runtime_secs"])):
                     break
+        if owb and best_p is not None:
+            final = self._model_loss(last_ev.get("_valid") or last_ev.get("_train"), cat, ae)
+            if best_loss < final:
+                with torch.no_grad():
+                    fp.p.copy_(best_p)
+                model.output["best_model_loss"] = best_loss
         model.output["scoring_history"] = history
         model.output["epochs"] = prev_epochs + samples / N_glob
         if ae:
@@ -418,6 +434,26 @@ class DeepLearningTrainer:
         model.output["variable_importances"] = variable_importance(list(agg), list(agg.values()))
         model.output["run_time_ms"] = int((time.time() - t0) * 1000)
         return model
+
+    def _model_loss(self, m, cat, ae) -> float:
+        """hex/Model.java loss(): the stopping metric, or logloss / MSE (autoencoder) / deviance."""
+        if m is None:
+            return float("inf")
+        sm = str(self.p.get("stopping_metric") or "AUTO").lower()
+        key = {"mse": "MSE", "rmse": "RMSE", "mae": "mae", "rmsle": "rmsle", "logloss": "logloss",
+               "deviance": "mean_residual_deviance", "misclassification": "err", "mean_per_class_error": "mean_per_class_error"}.get(sm)
+        if sm in ("auc", "aucpr"):
+            v = m.get("AUC" if sm == "auc" else "pr_auc")
+            return float("inf") if v is None else 1.0 - float(v)
+        if key is None:
+            key = "logloss" if cat in ("Binomial", "Multinomial") else ("MSE" if ae else "mean_residual_deviance")
+        v = m.get(key)
+        if v is None and key == "mean_residual_deviance":
+            v = m.get("MSE")
+        if v is None and key == "err":
+            cm = m.get("mean_per_class_error")
+            v = cm
+        return float("inf") if v is None else float(v)
 
     def _momentum(self, samples):
         p = self.p

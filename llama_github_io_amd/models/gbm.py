@@ -130,7 +130,8 @@ class GBMTrainer(SharedTreeTrainer):
         return float(self.p["learn_rate"]) * float(self.p["learn_rate_annealing"]) ** t
 
     def _fused(self):
-        return self.dev.type == "cuda" and self.K == 1 and self.dname in _FUSED_DIST
+        return (self.dev.type == "cuda" and self.K == 1 and self.dname in _FUSED_DIST
+                and not self.p.get("sample_rate_per_class") and not float(self.p.get("pred_noise_bandwidth") or 0))
 
     def _prepare(self, t, k):
         d = self.dist
@@ -255,7 +256,17 @@ class GBMTrainer(SharedTreeTrainer):
         if self._fused():
             self._pending = (self._vals, leaf)   # applied by the next fused step (or _flush_pending)
             return
-        self.f[:, k] += self._vals[leaf.long()]
+        vals = self._vals
+        bw = float(self.p.get("pred_noise_bandwidth") or 0.0)
+        if bw:
+            # GBM.java pred_noise_bandwidth: the TRAINING margin gets each leaf's value times a factor
+            # 1 + N(0, bw) drawn per (tree, class, leaf); the stored tree keeps the clean values
+            if bw < 0:
+                raise ValueError("pred_noise_bandwidth must be >= 0")
+            g = torch.Generator(device="cpu").manual_seed(((0xDECAF + self.seed) * (0xFAAAAAAB + k * 1000 + t)) & 0x7FFFFFFF)
+            noise = 1.0 + bw * torch.randn(vals.numel(), generator=g, dtype=torch.float64)
+            vals = (vals.double() * noise.to(vals.device)).float()
+        self.f[:, k] += vals[leaf.long()]
 
     def _finish(self, model, built):
         self._flush_pending()

@@ -39,7 +39,8 @@ GLM_DEFAULTS = dict(family="AUTO", link="family_default", solver="AUTO", alpha=N
                     missing_values_handling="MeanImputation", non_negative=False, obj_reg=-1.0, prior=-1.0,
                     max_active_predictors=-1, use_all_factor_levels=False, beta_constraints=None,
                     interactions=None, interaction_pairs=None, early_stopping=True, cold_start=False,
-                    calc_like=False, dispersion_parameter_method="pearson", lambda_min=None, seed=-1)
+                    calc_like=False, dispersion_parameter_method="pearson", lambda_min=None, seed=-1, startval=None,
+                    plug_values=None, build_null_model=False)
 
 DEFAULT_LINK = {"gaussian": "identity", "binomial": "logit", "quasibinomial": "logit", "fractionalbinomial": "logit",
                 "poisson": "log", "gamma": "inverse", "tweedie": "tweedie", "negativebinomial": "log",
@@ -270,13 +271,15 @@ def _soft(x, t):
     return torch.sign(x) * (x.abs() - t).clamp(min=0)
 
 
-def solve_penalized(Gm, r, l1, l2, intercept, beta0=None, non_negative=False, max_iter=500, tol=1e-8):
-    """min ½βᵀGβ - rᵀβ + l2/2‖β₋₀‖² + l1‖β₋₀‖₁ (last coefficient = intercept, unpenalized)."""
+def solve_penalized(Gm, r, l1, l2, intercept, beta0=None, non_negative=False, max_iter=500, tol=1e-8, lb=None, ub=None):
+    """min ½βᵀGβ - rᵀβ + l2/2‖β₋₀‖² + l1‖β₋₀‖₁ (last coefficient = intercept, unpenalized), optionally
+    inside the box ``lb <= β <= ub`` (beta_constraints: projected coordinate descent)."""
     P = Gm.shape[0]
     pen = torch.ones(P, dtype=torch.float64, device=Gm.device)
     if intercept:
         pen[-1] = 0
-    if l1 == 0 and not non_negative:
+    boxed = lb is not None or ub is not None
+    if l1 == 0 and not non_negative and not boxed:
         A = Gm + torch.diag(l2 * pen)
         jitter = 0.0
         for _ in range(6):
@@ -294,6 +297,11 @@ def solve_penalized(Gm, r, l1, l2, intercept, beta0=None, non_negative=False, ma
     diag = np.diag(Gh).copy()
     grad = Gh @ bh
     penh = pen.cpu().numpy()
+    lbh = None if lb is None else lb.cpu().numpy()
+    ubh = None if ub is None else ub.cpu().numpy()
+    if boxed:
+        bh = np.clip(bh, lbh if lbh is not None else -np.inf, ubh if ubh is not None else np.inf)
+        grad = Gh @ bh
     for it in range(max_iter):
         mx = 0.0
         for j in range(P):
@@ -304,6 +312,10 @@ def solve_penalized(Gm, r, l1, l2, intercept, beta0=None, non_negative=False, ma
             nb = rho / denom if penh[j] == 0 else np.sign(rho) * max(abs(rho) - l1, 0.0) / denom
             if non_negative and penh[j] > 0:
                 nb = max(nb, 0.0)
+            if lbh is not None:
+                nb = max(nb, lbh[j])
+            if ubh is not None:
+                nb = min(nb, ubh[j])
             d = nb - bh[j]
             if d != 0.0:
                 grad += Gh[:, j] * d
@@ -363,7 +375,8 @@ class GLMTrainer:
         y = torch.where(ok, y, torch.zeros_like(y))
         off = torch.zeros(N, dtype=torch.float64, device=dev) if offset is None else offset.double()
         ex = Expander(info, standardize=p["standardize"], use_all_factor_levels=p["use_all_factor_levels"] or
-                      fam == "multinomial", missing=p["missing_values_handling"]).fit(X, w, reduce=coll.all_reduce_ if coll.is_dist() else None)
+                      fam == "multinomial", missing=p["missing_values_handling"],
+                      plug_values=p.get("plug_values")).fit(X, w, reduce=coll.all_reduce_ if coll.is_dist() else None)
         Z = ex.transform(X)  # [N, P] f32
         intercept = bool(p["intercept"])
         Zi = torch.cat([Z, torch.ones(N, 1, dtype=Z.dtype, device=dev) if intercept else torch.zeros(N, 1, dtype=Z.dtype, device=dev)], 1)
@@ -396,6 +409,8 @@ class GLMTrainer:
                                                    coefficients=[e.get("coefs") for e in path],
                                                    coefficient_names=ex.names + ["Intercept"])
         self._outputs(model, fam, link, Zi, y, w, off, ex, nobs, X, offset)
+        if getattr(self, "collinear", None) is not None:
+            model.output["removed_collinear_columns"] = list(self.collinear)
         if valid is not None:
             Xv, yv, wv, ov = valid
             model.output["validation_metrics"] = model.metrics_for(Xv, yv, wv, ov)
@@ -411,6 +426,19 @@ class GLMTrainer:
         beta = torch.zeros(P1, dtype=torch.float64, device=dev)
         if intercept:
             beta[-1] = float(fam.linkfn(torch.tensor([min(max(ymu, 1e-6), 1 - 1e-6) if fam.name in ("binomial", "quasibinomial", "fractionalbinomial") else ymu], dtype=torch.float64))[0])
+        lb, ub = self._bounds(ex, P1, dev)
+        fixed = torch.zeros(P1, dtype=torch.bool, device=dev)    # coefficients pinned at 0
+        if p.get("build_null_model"):
+            fixed[:-1] = True                                    # intercept-only model (GLM build_null_model)
+        if p.get("startval") is not None:
+            sv = torch.as_tensor([float(v) for v in p["startval"]], dtype=torch.float64, device=dev)
+            if sv.numel() != P1:
+                raise ValueError(f"startval needs {P1} values (coefficients in order, intercept last)")
+            beta = self._raw_to_std(ex, sv)
+        if p.get("remove_collinear_columns"):
+            fixed |= self._collinear(Zi, w, intercept)
+            self.collinear = [ex.names[j] for j in torch.nonzero(fixed[:-1]).flatten().tolist()]
+        beta = torch.where(fixed, torch.zeros_like(beta), beta)
         # gradient at the null model -> lambda max
         eta = Zi.double() @ beta + off
         mu = fam.linkinv(eta)
@@ -464,7 +492,12 @@ class GLMTrainer:
                     Gm[:, -1] = 0
                     Gm[-1, -1] = 1
                     r[-1] = 0
-                nb = solve_penalized(Gm, r, l1, l2, intercept, beta, bool(p["non_negative"]))
+                if bool(fixed.any()):
+                    Gm[fixed, :] = 0
+                    Gm[:, fixed] = 0
+                    Gm[fixed, fixed] = 1
+                    r[fixed] = 0
+                nb = solve_penalized(Gm, r, l1, l2, intercept, beta, bool(p["non_negative"]), lb=lb, ub=ub)
                 diff = float((nb - beta).abs().max())
                 beta = nb
                 if self.job is not None:
@@ -477,6 +510,12 @@ class GLMTrainer:
                          coefs=beta.cpu().tolist())
             entry["lambda"] = lam
             path.append(entry)
+            mapred = int(p.get("max_active_predictors") or -1)
+            if mapred > 0 and int((beta[:-1].abs() > 0).sum()) > mapred and len(path) > 1:
+                # GLM max_active_predictors: the path stops before the active set exceeds the limit
+                path.pop()
+                beta = torch.tensor(path[-1]["coefs"], dtype=torch.float64, device=dev)
+                break
             score = dev_tr
             if valid is not None and len(lambdas) > 1:
                 Xv, yv, wv, ov = valid
@@ -491,6 +530,68 @@ class GLMTrainer:
         if best[1] is not None:
             return best[1], path, best[2]
         return beta, path, lambdas[-1]
+
+    # ---- coefficient helpers (raw <-> standardized scale, beta_constraints, collinearity)
+    @staticmethod
+    def _raw_to_std(ex, raw):
+        """Raw-scale coefficients (intercept last) -> the standardized space the solver works in."""
+        b = raw.clone()
+        if ex.standardize and ex.nums:
+            k = ex.num_off
+            sd = ex.num_sd.to(raw.device)
+            mu = ex.num_mean.to(raw.device)
+            b[k:-1] = raw[k:-1] * sd
+            b[-1] = raw[-1] + float((raw[k:-1] * mu).sum())
+        return b
+
+    def _bounds(self, ex, P1, dev):
+        """beta_constraints (names, lower_bounds, upper_bounds) on the raw scale -> standardized bounds."""
+        bc = self.p.get("beta_constraints")
+        if bc is None:
+            return None, None
+        if hasattr(bc, "as_data_frame"):
+            bc = bc.as_data_frame()
+        import pandas as pd
+        df = pd.DataFrame(bc)
+        if "names" not in df.columns:
+            raise ValueError("beta_constraints needs a 'names' column")
+        lb = torch.full((P1,), -float("inf"), dtype=torch.float64, device=dev)
+        ub = torch.full((P1,), float("inf"), dtype=torch.float64, device=dev)
+        names = ex.names
+        for _, row in df.iterrows():
+            n = str(row["names"])
+            if n not in names:
+                raise ValueError(f"beta_constraints: unknown coefficient {n!r}")
+            j = names.index(n)
+            sc = float(ex.num_sd[j - ex.num_off]) if (ex.standardize and j >= ex.num_off) else 1.0
+            if "lower_bounds" in df.columns and not pd.isna(row["lower_bounds"]):
+                lb[j] = float(row["lower_bounds"]) * sc
+            if "upper_bounds" in df.columns and not pd.isna(row["upper_bounds"]):
+                ub[j] = float(row["upper_bounds"]) * sc
+        return lb, ub
+
+    def _collinear(self, Zi, w, intercept):
+        """remove_collinear_columns: columns whose Gram pivot (Cholesky of the weighted Gram in column
+        order, intercept first) collapses are dropped (pinned to 0) — GLM.java's collinear-column check."""
+        Gm = _gvec(G.gram(Zi, w.float()))
+        P1 = Gm.shape[0]
+        order = ([P1 - 1] if intercept else []) + list(range(P1 - 1))
+        kept, drop = [], torch.zeros(P1, dtype=torch.bool, device=Gm.device)
+        for j in order:
+            if kept:
+                A = Gm[kept][:, kept]
+                bvec = Gm[kept, j]
+                x = torch.linalg.lstsq(A, bvec[:, None]).solution[:, 0]
+                resid = float(Gm[j, j] - bvec @ x)
+            else:
+                resid = float(Gm[j, j])
+            if resid <= 1e-8 * max(float(Gm[j, j]), 1e-300):
+                drop[j] = True
+            else:
+                kept.append(j)
+        if intercept:
+            drop[-1] = False
+        return drop
 
     # ---- multinomial IRLSM (GLM.java fitIRLSM_multinomial): one penalized weighted least-squares
     # solve per class with the other classes' coefficients held fixed, cycled to convergence

@@ -1,0 +1,102 @@
+"""Parameter validation (reference: ``hex/ModelBuilder.java`` ``init(expensive)`` — every builder
+checks its parameters and refuses bad or unsupported settings with an error message, and the REST /
+h2o-py layer refuses unknown parameter names).
+
+Every algorithm's public parameters come from the h2o-py estimator signatures
+(``h2o/estimators/_schema.py``). Each one is either
+
+* implemented by the trainer (the default),
+* an **execution hint** of the Java cluster that has no meaning on this engine (thread counts,
+  single-node mode, load balancing, DMatrix formats, ...): accepted and ignored, listed in ``HINTS``,
+* or **not supported** yet (``UNSUPPORTED``): any non-default value raises ``ValueError`` instead of
+  silently training a different model.
+
+Names outside the schema (and outside the trainer's own extension defaults) raise too.
+"""
+from __future__ import annotations
+
+import math
+
+# execution hints of the Java backend: no effect on the model
+HINTS = {
+    "nthread", "gpu_id", "backend", "quiet_mode", "build_tree_one_node", "single_node_mode", "force_load_balance",
+    "replicate_training_data", "col_major", "diagnostics", "fast_mode", "score_duty_cycle",
+    "target_ratio_comm_to_comp", "parallelize_cross_validation", "nparallelism", "multinode_mode", "dmatrix_type",
+    "save_matrix_directory", "check_constant_response", "reproducible", "pca_impl", "response_column",
+    "auto_rebalance", "export_weights_and_biases", "verbose", "r2_stopping", "score_eval_metric_only",
+    "max_confusion_matrix_size", "save_transformed_framekeys", "store_knot_locations", "generate_scoring_history",
+    "score_iteration_interval", "classification_stop", "regression_stop", "train_samples_per_iteration",
+    "score_validation_sampling", "u_name", "loading_name", "build_glm_model",
+    "compute_metrics", "num_iteration_without_new_exemplar",
+    "tree_method", "eval_metric", "export_checkpoints_dir",
+}
+
+# parameters not implemented by this engine: a non-default value is refused
+UNSUPPORTED = {
+    "deeplearning": {"average_activation", "elastic_averaging", "elastic_averaging_moving_rate",
+                     "elastic_averaging_regularization", "initial_biases", "initial_weights", "max_categorical_features",
+                     "pretrained_autoencoder", "sparse", "sparsity_beta", "score_validation_samples", "rate_decay",
+                     "huber_alpha", "missing_values_handling"},
+    "gbm": {"interaction_constraints"},
+    "xgboost": {"interaction_constraints", "colsample_bynode", "normalize_type", "sample_type", "grow_policy",
+                "max_leaves"},
+    "glm": {"cold_start", "dispersion_epsilon", "dispersion_learning_rate", "dispersion_parameter_method",
+            "fix_dispersion_parameter", "fix_tweedie_variance_power", "generate_variable_inflation_factors",
+            "influence", "init_dispersion_parameter", "max_iterations_dispersion", "rand_link", "tweedie_epsilon",
+            "calc_like", "checkpoint", "prior", "gradient_epsilon", "early_stopping"},
+    "gam": {"beta_constraints", "bs", "cold_start", "interaction_pairs", "interactions", "knot_ids",
+            "max_active_predictors", "remove_collinear_columns", "scale_tp_penalty_mat", "spline_orders",
+            "splines_non_negative", "standardize_tp_gam_cols", "startval", "prior", "gradient_epsilon",
+            "objective_epsilon", "early_stopping", "plug_values"},
+    "anovaglm": {"early_stopping", "prior", "type", "plug_values"},
+    "modelselection": {"beta_constraints", "cold_start", "influence", "max_active_predictors", "prior",
+                       "remove_collinear_columns", "startval", "p_values_threshold", "gradient_epsilon",
+                       "objective_epsilon", "early_stopping", "plug_values"},
+    "coxph": {"interaction_pairs", "interactions", "interactions_only"},
+    "glrm": {"loss_by_col", "loss_by_col_idx", "multi_loss", "user_x", "svd_method", "expand_user_y",
+             "impute_original", "recover_svd", "max_updates"},
+    "kmeans": {"cluster_size_constraints"},
+    "psvm": {"feasible_threshold", "kernel_type", "mu_factor", "surrogate_gap_threshold"},
+    "word2vec": {"norm_model", "pre_trained", "word_model"},
+    "upliftdrf": {"auuc_nbins", "auuc_type"},
+    "rulefit": {"max_categorical_levels"},
+    "stackedensemble": {"score_training_samples"},
+    "infogram": {"max_iterations", "data_fraction"},
+    "isolationforest": {"validation_response_column"},
+}
+
+# values that count as "left at its default" whatever the schema says
+_NEUTRAL = (None, "AUTO", "auto", "", [], {}, False)
+
+
+def _is_default(v, default) -> bool:
+    if v is None:
+        return True
+    if isinstance(v, float) and isinstance(default, (int, float)) and default is not None and not isinstance(default, bool):
+        return math.isclose(v, float(default)) or (math.isinf(v) and math.isinf(float(default)))
+    if v == default:
+        return True
+    return isinstance(v, (str, list, dict, bool)) and v in _NEUTRAL and default in _NEUTRAL
+
+
+def schema(algo: str) -> dict | None:
+    try:
+        from h2o.estimators._schema import PARAMS
+    except ImportError:    # pragma: no cover - the facade is part of the package tree
+        return None
+    return PARAMS.get(algo)
+
+
+def validate(algo: str, params: dict, extra_allowed=()) -> None:
+    """Raise ``ValueError`` on an unknown parameter name or on a non-default value of a parameter this
+    engine does not implement (ModelBuilder.init's error messages)."""
+    sch = schema(algo)
+    if sch is None:
+        return
+    allowed = set(sch) | set(extra_allowed) | HINTS
+    unknown = sorted(k for k in params if k not in allowed and not k.startswith("_"))
+    if unknown:
+        raise ValueError(f"{algo}: unknown parameter(s) {unknown}")
+    bad = sorted(k for k in UNSUPPORTED.get(algo, ()) if k in params and not _is_default(params[k], sch.get(k)))
+    if bad:
+        raise ValueError(f"{algo}: parameter(s) {bad} are not supported by this engine (leave them at their defaults)")

@@ -123,6 +123,19 @@ class SharedTreeTrainer:
     def _k_cols(self, F_ok: int) -> int:
         return 0
 
+    def _level_k_cols(self, F: int):
+        """k_cols, or its per-level schedule when col_sample_rate_change_per_level != 1
+        (DTree.actual_mtries: min(max(1, int(k * change^depth)), F))."""
+        k = self._k_cols(F)
+        ch = float(self.p.get("col_sample_rate_change_per_level") or 1.0)
+        if not 0.0 < ch <= 2.0:
+            raise ValueError("col_sample_rate_change_per_level must be > 0 and <= 2.0")
+        if ch == 1.0:
+            return k
+        base = k if k > 0 else F
+        D = int(self.p["max_depth"]) if int(self.p["max_depth"]) > 0 else 32
+        return [min(max(1, int(base * ch ** d)), F) for d in range(D + 1)]
+
     def _trees_per_iter(self) -> int:
         return 1
 
@@ -159,9 +172,10 @@ class SharedTreeTrainer:
                 Xl = X
             Xs = coll.all_gather_cat(Xl.contiguous(), dim=1)
             self.binning = fit_binning(Xs, info.iscat, info.nlevels, max_bins=max_bins, seed=self.seed,
-                                       sample=Xs.shape[1] + 1)
+                                       sample=Xs.shape[1] + 1, max_cat_bins=int(p.get("nbins_cats") or 1024))
         else:
-            self.binning = fit_binning(X, info.iscat, info.nlevels, max_bins=max_bins, seed=self.seed)
+            self.binning = fit_binning(X, info.iscat, info.nlevels, max_bins=max_bins, seed=self.seed,
+                                       max_cat_bins=int(p.get("nbins_cats") or 1024))
         bins = apply_binning(self.binning, X)
         mono = None
         if p.get("monotone_constraints"):
@@ -219,7 +233,7 @@ class SharedTreeTrainer:
                     ln = self._leaf_native(t, k)
                     if ln is not None:
                         kw["leaf_native"] = ln
-                h = self.builder.build(aux, feat_ok, self._k_cols(F), seed=(self.seed * 1000003 + t * 97 + k) & ((1 << 63) - 1),
+                h = self.builder.build(aux, feat_ok, self._level_k_cols(F), seed=(self.seed * 1000003 + t * 97 + k) & ((1 << 63) - 1),
                                        leaf_fn=lambda ls, t=t, k=k: self._leaf_values(ls, t, k), **kw)
                 h2 = time.perf_counter()
                 self._update(t, k)
@@ -399,6 +413,15 @@ class SharedTreeTrainer:
     def _row_sample(self, rate: float, t: int):
         """Bernoulli(rate) row sample keyed by (seed, tree, GLOBAL row index): identical however the
         rows are sharded."""
+        spc = self.p.get("sample_rate_per_class")
+        if spc:
+            # sample_rate_per_class: one rate per response class (SharedTree.java sample_rate_per_class)
+            if self.info.response_domain is None or len(spc) != len(self.info.response_domain):
+                raise ValueError("sample_rate_per_class needs one rate per response class")
+            rates = torch.tensor([float(v) for v in spc], dtype=torch.float64, device=self.dev)
+            cls = torch.nan_to_num(self.y, nan=0).long().clamp(0, len(spc) - 1)
+            m = coll.row_uniform(self.seed, 1000 + t, self.row0, self.N, self.dev) < rates[cls]
+            return self.w * m.float()
         if rate >= 1.0:
             return self.w
         m = coll.row_uniform(self.seed, 1000 + t, self.row0, self.N, self.dev) < rate

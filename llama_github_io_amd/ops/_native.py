@@ -39,6 +39,8 @@ _HIP_SIGS = {
     "h2o_route": [c_void_p] * 6 + [c_int] + [c_void_p] * 12 + [c_int, c_int, c_int, c_void_p],
     "h2o_bin_assign": [c_void_p, c_ll, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "h2o_amax": [c_void_p, c_ll, c_void_p, c_void_p],
+    "h2o_kmeans_mfma_shape": [c_int, c_int, c_void_p],
+    "h2o_kmeans_mfma": [c_void_p, c_ll, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p],
     "h2o_qscale": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p],
     "h2o_hist_reduce": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
                         c_void_p, c_int, c_void_p],

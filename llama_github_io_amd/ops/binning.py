@@ -41,8 +41,11 @@ class Binning:
 
 
 def fit_binning(X: torch.Tensor, iscat, nlevels=None, max_bins: int = MAX_DATA_BINS, sample: int = 1 << 20,
-                seed: int = 0, weights: torch.Tensor | None = None) -> Binning:
-    """X: float32 [F, N] (column-major; NaN = missing; categorical columns hold level codes)."""
+                seed: int = 0, weights: torch.Tensor | None = None, max_cat_bins: int = NA_BIN) -> Binning:
+    """X: float32 [F, N] (column-major; NaN = missing; categorical columns hold level codes).
+    ``max_cat_bins`` (nbins_cats, capped at 255): categoricals with more levels keep their most
+    frequent ``max_cat_bins - 1`` levels as bins and fold the rest into one shared bin."""
+    cat_cap = int(min(max(2, max_cat_bins), NA_BIN))
     F, N = X.shape
     max_bins = int(min(max(2, max_bins), MAX_DATA_BINS))
     iscat = np.asarray(iscat, dtype=np.int32)
@@ -64,17 +67,17 @@ def fit_binning(X: torch.Tensor, iscat, nlevels=None, max_bins: int = MAX_DATA_B
         if iscat[f]:
             nl = int(nlevels[f]) if nlevels[f] > 0 else int(torch.nan_to_num(X[f], nan=-1).max().item()) + 1
             nlevels[f] = nl
-            if nl <= NA_BIN:
+            if nl <= cat_cap:
                 l2b.append(None)
                 nbins[f] = max(nl, 1)
             else:  # fold rare levels into the last bin
                 codes = X[f][~torch.isnan(X[f])].long()
                 cnt = torch.bincount(codes, minlength=nl).cpu().numpy()
                 order = np.argsort(-cnt, kind="stable")
-                m = np.full(nl, NA_BIN - 1, dtype=np.int64)
-                m[order[: NA_BIN - 1]] = np.arange(NA_BIN - 1)
+                m = np.full(nl, cat_cap - 1, dtype=np.int64)
+                m[order[: cat_cap - 1]] = np.arange(cat_cap - 1)
                 l2b.append(m)
-                nbins[f] = NA_BIN
+                nbins[f] = cat_cap
             edges.append(None)
             continue
         row = srt[num_cols.index(f)]

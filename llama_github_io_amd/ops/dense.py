@@ -6,6 +6,8 @@ counter-hash dropout mask so CPU/GPU runs agree bit-for-bit on which units drop)
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _native as nat
@@ -153,10 +155,33 @@ def bias_act(x, b, act: str | int = "rectifier", drop: float = 0.0, seed: int = 
     return BiasAct.apply(x, b, a, float(drop), int(seed))
 
 
+def _mfma_shape(K, P):
+    import ctypes
+    out = (ctypes.c_int * 3)()
+    ok = nat.hip().h2o_kmeans_mfma_shape(int(K), int(P), out)
+    return (out[0], out[1], out[2]) if ok else None
+
+
 def kmeans_step(X: torch.Tensor, C: torch.Tensor, w: torch.Tensor | None = None):
-    """One Lloyd step: (assign [N], min sq. distance [N], per-center weighted sums [K, P] fp64, counts [K])."""
+    """One Lloyd step: (assign [N], min sq. distance [N], per-center weighted sums [K, P] fp64, counts [K]).
+    On the GPU: ``csrc/kmeans_mfma.hip`` (distance GEMM + argmin + one-hot centroid GEMM on f32 MFMA,
+    one pass over X) for K, P <= 64; the LDS scalar kernel beyond that."""
     N, P = X.shape
     K = C.shape[0]
+    sh = _mfma_shape(K, P) if X.is_cuda and N > 0 else None
+    if sh is not None and os.environ.get("H2O_KMEANS_MFMA", "1") == "1":
+        KT, PS, PT = sh
+        X = X.contiguous().float()
+        C = C.contiguous().float()
+        wf = None if w is None else w.contiguous().float()
+        a = torch.empty(N, dtype=torch.int32, device=X.device)
+        d = torch.empty(N, dtype=torch.float32, device=X.device)
+        grid = int(max(1, min(1024, (N + 63) // 64)))
+        slab = torch.empty(grid * 4, KT * 16, PT * 16, dtype=torch.float32, device=X.device)
+        nat.call("h2o_kmeans_mfma", X.data_ptr(), N, P, C.data_ptr(), K, 0 if wf is None else wf.data_ptr(),
+                 a.data_ptr(), d.data_ptr(), slab.data_ptr(), grid, nat.stream_ptr(X.device))
+        tot = slab.sum(0, dtype=torch.float64)
+        return a.long(), d, tot[:K, :P].contiguous(), tot[:K, P].contiguous()
     if X.is_cuda and (K * P + 256 * (P + 1) + 512) * 4 <= 160 * 1024 and N > 0 and K * (P + 1) <= 8192:
         X = X.contiguous().float()
         C = C.contiguous().float()

@@ -227,6 +227,14 @@ def split_reduce_ref(cands, feat_ok, k_cols, seed, level, node):
     return d
 
 
+def _level_k(k_cols, d: int) -> int:
+    """Column sample size at depth ``d``: an int for every level, or a per-level list
+    (DTree.actual_mtries with col_sample_rate_change_per_level)."""
+    if isinstance(k_cols, (list, tuple)):
+        return int(k_cols[min(d, len(k_cols) - 1)]) if k_cols else 0
+    return int(k_cols)
+
+
 def dec_go_left_np(d, b: np.ndarray) -> np.ndarray:
     if d["feat"] < 0:
         return np.ones_like(b, dtype=bool)
@@ -292,7 +300,7 @@ class RefTreeBuilder:
                     nayy = flat[h.size: h.size + F]
                     wyy = float(flat[-1])
                 cands = split_find_ref(h, nayy, wyy, self.nbins_f, self.iscat_f, self.mono_f, p, d, i, seed)
-                dl[i] = split_reduce_ref(cands, feat_ok, k_cols, seed, d, i)
+                dl[i] = split_reduce_ref(cands, feat_ok, _level_k(k_cols, d), seed, d, i)
             cl = np.zeros(n, dtype=np.int64); cr = np.zeros(n, dtype=np.int64)
             nxt = []
             act = 0
@@ -361,7 +369,8 @@ class _TreePlan(ctypes.Structure):
                 [("caps", _ci * _MAXL), ("tiles_cap", _ci * _MAXL)] +
                 [(n, _vp) for n in ("aux", "amax_bits", "feat_ok")] +
                 [(n, _ci) for n in ("compute_amax", "k_cols", "packed", "leaf_native", "log_link", "pad1")] +
-                [("seed", ctypes.c_ulonglong)] + [(n, _cd) for n in ("scale", "kclamp", "mx")])
+                [("seed", ctypes.c_ulonglong)] + [(n, _cd) for n in ("scale", "kclamp", "mx")] +
+                [("kc_level", _ci * _MAXL), ("pad2", _ci)])
 
 
 class _Arena:
@@ -571,7 +580,7 @@ class GpuTreeBuilder:
                                          ic_p, mono, p.min_w, p.min_split_improvement, p.lam,
                                          p.alpha, p.gamma, p.mode, int(p.random_split), seed, d,
                                          cand_p, self._p("rootw") if d == 0 else 0, s), "split_find")
-            nat.check(lib.h2o_split_reduce(cand_p, self._p(f"meta{d}"), cap, F, fo_p, int(k_cols),
+            nat.check(lib.h2o_split_reduce(cand_p, self._p(f"meta{d}"), cap, F, fo_p, _level_k(k_cols, d),
                                            seed, d, self._p(f"dec{d}"), s), "split_reduce")
             nat.check(lib.h2o_plan(self._p(f"nodes{d}"), self._p(f"meta{d}"), self._p(f"dec{d}"), self._p(f"nl{d}"),
                                    self._p(f"nl{d - 1}") if odd else 0, self._p(f"cur{d}"), self._p(f"cl{d}"),
@@ -633,7 +642,9 @@ class GpuTreeBuilder:
         P.compute_amax = int(amax_bits is None)
         P.amax_bits = (self.amax_bits if amax_bits is None else amax_bits).data_ptr()
         P.feat_ok = (self.feat_ok_all if feat_ok is None else feat_ok).data_ptr()
-        P.k_cols, P.packed, P.seed = int(k_cols), pk, int(seed) & _M64
+        P.k_cols, P.packed, P.seed = _level_k(k_cols, 0), pk, int(seed) & _M64
+        for d in range(_MAXL):
+            P.kc_level[d] = _level_k(k_cols, d) if isinstance(k_cols, (list, tuple)) else 0
         P.grid = self.grid * (self.hist_bpc if pk else 1)
         P.leaf_native = int(leaf_native is not None)
         if leaf_native is not None:

@@ -174,6 +174,33 @@ def test_kmeans_step_kernel():
     assert torch.allclose(sums, ref, rtol=1e-4, atol=1e-2) and torch.allclose(cnt, cref, rtol=1e-4, atol=1e-2)
 
 
+@pytest.mark.parametrize("N,K,P,weighted", [(100003, 10, 20, True), (4099, 37, 50, False), (20000, 64, 64, True),
+                                             (777, 1, 1, False), (50001, 17, 33, True)])
+def test_kmeans_mfma_lloyd_matches_fp32_reference(N, K, P, weighted, monkeypatch):
+    """csrc/kmeans_mfma.hip (distance + centroid GEMMs on v_mfma_f32_16x16x4_f32) vs a plain PyTorch fp32/fp64
+    reference of the same Lloyd step: argmin, min distance, per-center weighted sums and counts."""
+    from llama_github_io_amd.ops.dense import _mfma_shape, kmeans_step
+    monkeypatch.setenv("H2O_KMEANS_MFMA", "1")
+    assert _mfma_shape(K, P) is not None
+    g = torch.Generator(device=dev).manual_seed(N + K)
+    X = torch.randn(N, P, device=dev, generator=g)
+    C = torch.randn(K, P, device=dev, generator=g)
+    w = torch.rand(N, device=dev, generator=g) if weighted else None
+    a, d, sums, cnt = kmeans_step(X, C, w)
+    D = ((X[:, None, :].double() - C[None].double()) ** 2).sum(-1)
+    dref, aref = D.min(1)
+    # disagreements only on numerical near-ties
+    mism = a != aref
+    if mism.any():
+        gap = (D.gather(1, a[:, None])[:, 0] - dref)[mism]
+        assert float(gap.max()) < 1e-3 * float(dref[mism].abs().max() + 1)
+    assert torch.allclose(d.double(), D.gather(1, a[:, None])[:, 0], rtol=1e-4, atol=1e-3)
+    wd = torch.ones(N, dtype=torch.float64, device=dev) if w is None else w.double()
+    ref = torch.zeros(K, P, dtype=torch.float64, device=dev).index_add_(0, a, X.double() * wd[:, None])
+    cref = torch.zeros(K, dtype=torch.float64, device=dev).index_add_(0, a, wd)
+    assert torch.allclose(sums, ref, rtol=1e-4, atol=1e-2) and torch.allclose(cnt, cref, rtol=1e-5, atol=1e-3)
+
+
 def test_deeplearning_graph_matches_eager(monkeypatch):
     from llama_github_io_amd.models.deeplearning import DeepLearningTrainer
     g = torch.Generator(device=dev).manual_seed(0)

@@ -1,0 +1,153 @@
+"""Parameter surface (ModelBuilder.init): unknown names and unsupported settings raise; every implemented
+parameter changes the model (hex/ModelBuilder.java:1531-1577, hex/Model.java:360, GLMModel.java:413-420,
+DeepLearningModel.java:1329, SharedTreeModel.java:97, GBM.java:1461)."""
+import numpy as np
+import pandas as pd
+import pytest
+
+import h2o
+from llama_github_io_amd.models import builder
+
+
+@pytest.fixture(scope="module")
+def fr():
+    h2o.init(verbose=False)
+    rng = np.random.default_rng(0)
+    n = 800
+    d = pd.DataFrame({"a": rng.normal(size=n), "b": rng.normal(size=n), "c": rng.normal(size=n),
+                      "g": rng.choice(list("pqrstu"), n, p=[.4, .25, .15, .1, .06, .04]),
+                      "h": rng.choice(list("xyz"), n)})
+    logit = 1.2 * d.a - d.b + (d.g == "q") * 1.0 + (d.h == "y") * d.c
+    d["y"] = np.where(rng.random(n) < 1 / (1 + np.exp(-(logit - 1.5))), "1", "0")     # imbalanced
+    d["r"] = 2 * d.a + d.a * d.b + (d.g == "q") * 1.5 - (d.g == "t") * 2.0 + rng.normal(size=n) * 0.3
+    return h2o.H2OFrame(d, column_types={"g": "enum", "h": "enum", "y": "enum"})
+
+
+X = ["a", "b", "c", "g", "h"]
+
+
+def _pred(m, fr):
+    return m.predict(fr).as_data_frame().select_dtypes(include=[np.number]).to_numpy(dtype=float)
+
+
+def test_unknown_parameter_raises(fr):
+    with pytest.raises(ValueError, match="unknown parameter"):
+        builder.train("gbm", dict(ntrees=2, max_dept=3), x=X, y="y", training_frame=fr)
+    with pytest.raises(ValueError, match="unknown parameter"):
+        builder.train("glm", dict(lamda=0.1), x=X, y="y", training_frame=fr)
+
+
+@pytest.mark.parametrize("algo,param,value", [
+    ("gbm", "interaction_constraints", [["a", "b"]]),
+    ("xgboost", "grow_policy", "lossguide"),
+    ("deeplearning", "initial_weights", ["w"]),
+    ("glm", "influence", "dfbetas"),
+])
+def test_unsupported_parameter_raises(fr, algo, param, value):
+    with pytest.raises(ValueError, match="not supported"):
+        builder.train(algo, {param: value, "seed": 1}, x=X, y="y", training_frame=fr)
+
+
+def test_execution_hints_accepted(fr):
+    m = builder.train("gbm", dict(ntrees=2, seed=1, build_tree_one_node=True, nthread=4), x=X, y="y", training_frame=fr)
+    assert m.output["ntrees"] == 2
+
+
+def test_balance_classes_changes_model(fr):
+    base = builder.train("gbm", dict(ntrees=5, max_depth=3, seed=3), x=X, y="y", training_frame=fr)
+    bal = builder.train("gbm", dict(ntrees=5, max_depth=3, seed=3, balance_classes=True), x=X, y="y", training_frame=fr)
+    assert not np.allclose(_pred(base, fr), _pred(bal, fr))
+    prior, md = bal.output["prior_class_distrib"], bal.output["model_class_distrib"]
+    assert abs(md[0] - 0.5) < 1e-9 and prior[0] > 0.6
+    # predictions are corrected back to the prior: mean p1 stays near the observed positive rate
+    p1 = _pred(bal, fr)[:, -1]
+    assert abs(p1.mean() - prior[1]) < 0.1
+    f = builder.train("gbm", dict(ntrees=5, max_depth=3, seed=3, balance_classes=True, class_sampling_factors=[1.0, 3.0],
+                                  max_after_balance_size=2.0), x=X, y="y", training_frame=fr)
+    assert f.output["model_class_distrib"] != md
+
+
+@pytest.mark.parametrize("enc", ["OneHotExplicit", "Binary", "LabelEncoder", "SortByResponse", "EnumLimited", "Eigen"])
+def test_categorical_encodings(fr, enc):
+    base = builder.train("gbm", dict(ntrees=4, max_depth=3, seed=2), x=X, y="r", training_frame=fr)
+    m = builder.train("gbm", dict(ntrees=4, max_depth=3, seed=2, categorical_encoding=enc, max_categorical_levels=3),
+                      x=X, y="r", training_frame=fr)
+    names = m.output["names"]
+    if enc == "OneHotExplicit":
+        assert "g.p" in names and "g.u" in names and "g" not in names   # g.missing(NA) is constant: dropped
+    elif enc == "Binary":
+        assert "g:0" in names and "g:2" in names
+    elif enc == "Eigen":
+        assert "g.Eigen" in names
+    iscat = dict(zip(m.info.x, m.info.iscat))
+    if enc in ("LabelEncoder", "SortByResponse"):
+        assert iscat["g"] == 0                           # the categorical became an ordinal numeric column
+    if enc == "EnumLimited":
+        assert m.info.domains[m.info.x.index("g")] == ["p", "q", "r", "other"]   # top-3 levels + other
+    assert base.info.x != m.info.x or iscat.get("g", 1) == 0 or enc == "EnumLimited"
+    # the encoding is replayed on scoring frames (same predictions on a re-built frame)
+    fr2 = h2o.H2OFrame(fr.as_data_frame(), column_types={"g": "enum", "h": "enum", "y": "enum"})
+    assert np.allclose(_pred(m, fr), _pred(m, fr2))
+
+
+def test_glm_interactions(fr):
+    base = builder.train("glm", dict(family="gaussian", lambda_=0.0), x=["a", "b", "g"], y="r", training_frame=fr)
+    m = builder.train("glm", dict(family="gaussian", lambda_=0.0, interactions=["a", "b"]), x=["a", "b", "g"], y="r",
+                      training_frame=fr)
+    assert abs(m.output["coefficients"]["a:b"] - 1.0) < 0.1
+    assert m.output["training_metrics"]["MSE"] < base.output["training_metrics"]["MSE"] * 0.5
+    m2 = builder.train("glm", dict(family="gaussian", lambda_=0.0, interaction_pairs=[("g", "a")]), x=["a", "b", "g"],
+                       y="r", training_frame=fr)
+    assert "g_p:a" in m2.output["coefficients"]
+
+
+def test_glm_beta_constraints_and_collinear(fr):
+    bc = pd.DataFrame({"names": ["a"], "lower_bounds": [-1.0], "upper_bounds": [0.5]})
+    m = builder.train("glm", dict(family="gaussian", lambda_=0.0, beta_constraints=bc), x=["a", "b"], y="r",
+                      training_frame=fr)
+    assert m.output["coefficients"]["a"] <= 0.5 + 1e-9
+    fr2 = fr.cbind(fr["a"] * 2.0)
+    fr2.set_name(fr2.ncols - 1, "a2")
+    m2 = builder.train("glm", dict(family="gaussian", lambda_=0.0, remove_collinear_columns=True), x=["a", "b", "a2"],
+                       y="r", training_frame=fr2)
+    assert m2.output["removed_collinear_columns"] == ["a2"]
+    m3 = builder.train("glm", dict(family="binomial", lambda_search=True, nlambdas=20, max_active_predictors=3),
+                       x=X, y="y", training_frame=fr)
+    nz = sum(1 for k, v in m3.output["coefficients"].items() if k != "Intercept" and abs(v) > 0)
+    assert nz <= 3
+    m4 = builder.train("glm", dict(family="binomial", build_null_model=True), x=X, y="y", training_frame=fr)
+    assert all(v == 0 for k, v in m4.output["coefficients"].items() if k != "Intercept")
+
+
+def test_glm_plug_values(fr):
+    d = fr.as_data_frame()
+    d.loc[::7, "a"] = np.nan
+    f2 = h2o.H2OFrame(d, column_types={"g": "enum", "h": "enum", "y": "enum"})
+    pv = h2o.H2OFrame(pd.DataFrame({"a": [5.0]}))
+    m1 = builder.train("glm", dict(family="gaussian", lambda_=0.0), x=["a", "b"], y="r", training_frame=f2)
+    m2 = builder.train("glm", dict(family="gaussian", lambda_=0.0, missing_values_handling="PlugValues", plug_values=pv),
+                       x=["a", "b"], y="r", training_frame=f2)
+    assert m1.output["coefficients"]["a"] != m2.output["coefficients"]["a"]
+
+
+def test_tree_level_params_change_model(fr):
+    base = builder.train("gbm", dict(ntrees=5, max_depth=4, seed=9, col_sample_rate=0.8), x=X, y="r", training_frame=fr)
+    for extra in (dict(col_sample_rate_change_per_level=0.5), dict(pred_noise_bandwidth=0.5)):
+        m = builder.train("gbm", dict(ntrees=5, max_depth=4, seed=9, col_sample_rate=0.8, **extra), x=X, y="r",
+                          training_frame=fr)
+        assert not np.allclose(_pred(base, fr), _pred(m, fr)), extra
+    c0 = builder.train("drf", dict(ntrees=5, max_depth=4, seed=9), x=X, y="y", training_frame=fr)
+    c1 = builder.train("drf", dict(ntrees=5, max_depth=4, seed=9, sample_rate_per_class=[0.3, 1.0]), x=X, y="y",
+                       training_frame=fr)
+    assert not np.allclose(_pred(c0, fr), _pred(c1, fr))
+
+
+def test_dl_overwrite_with_best_model(fr):
+    kw = dict(hidden=[16], epochs=8, seed=1, mini_batch_size=32, score_interval=0, score_training_samples=0,
+              rate=0.5, adaptive_rate=False, momentum_start=0.9, momentum_stable=0.99)
+    a = builder.train("deeplearning", dict(kw, overwrite_with_best_model=True), x=X, y="y", training_frame=fr)
+    b = builder.train("deeplearning", dict(kw, overwrite_with_best_model=False), x=X, y="y", training_frame=fr)
+    hist = [e["training_logloss"] for e in b.output["scoring_history"] if "training_logloss" in e]
+    assert len(hist) > 2
+    assert a.output["training_metrics"]["logloss"] <= b.output["training_metrics"]["logloss"] + 1e-9
+    assert a.output["training_metrics"]["logloss"] <= min(hist) + 1e-6
