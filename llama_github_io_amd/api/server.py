@@ -21,6 +21,7 @@ from ..core.job import Job, list_jobs
 from ..frame import H2OFrame
 from ..models import builder
 from ..models.base import Model
+from . import v3
 
 try:
     from fastapi import FastAPI, HTTPException, Request
@@ -52,7 +53,7 @@ def _clean(o):
     return str(o)
 
 
-def _frame_json(fr: H2OFrame, row_offset=0, row_count=10, full=False):
+def _frame_json_legacy(fr: H2OFrame, row_offset=0, row_count=10, full=False):
     cols = []
     for n in fr.names:
         c = fr._col(n)
@@ -77,6 +78,10 @@ def _frame_json(fr: H2OFrame, row_offset=0, row_count=10, full=False):
 
 
 def _model_json(m: Model):
+    return v3.model(m)
+
+
+def _model_json_legacy(m: Model):
     out = dict(model_id=dict(name=m.key, type="Key<Model>"), algo=m.algo, algo_full_name=m.algo,
                response_column_name=m.info.response, parameters=[dict(name=k, actual_value=v) for k, v in m.params.items()],
                output=dict(m.output, model_category=m.model_category, names=m.info.x + ([m.info.response] if m.info.response else []),
@@ -84,16 +89,30 @@ def _model_json(m: Model):
     return _clean(out)
 
 
+def _unquote(v):
+    if isinstance(v, str) and len(v) >= 2 and v[0] == v[-1] == '"':
+        return v[1:-1]
+    if isinstance(v, list):
+        return [_unquote(x) for x in v]
+    return v
+
+
 def _parse_params(raw: dict) -> dict:
     out = {}
     for k, v in raw.items():
         if isinstance(v, str):
             s = v.strip()
+            if s in ("null", "None"):
+                out[k] = None
+                continue
             if s.startswith("[") or s.startswith("{"):
                 try:
-                    v = json.loads(s.replace("'", '"'))
+                    v = _unquote(json.loads(s))
                 except ValueError:
-                    v = [x.strip().strip('"') for x in s.strip("[]").split(",") if x.strip()]
+                    try:
+                        v = _unquote(json.loads(s.replace("'", '"')))
+                    except ValueError:
+                        v = [x.strip().strip('"') for x in s.strip("[]").split(",") if x.strip()]
             elif s.lower() in ("true", "false"):
                 v = s.lower() == "true"
             else:
@@ -121,6 +140,24 @@ async def _params(request: Request) -> dict:
     return _parse_params(q)
 
 
+def _multipart_first_file(body: bytes, boundary: str):
+    """The first file part of a multipart/form-data body (python-multipart is not in the image)."""
+    sep = b"--" + boundary.encode()
+    for part in body.split(sep):
+        if b"\r\n\r\n" not in part:
+            continue
+        head, _, data = part.partition(b"\r\n\r\n")
+        if b"filename=" in head or b"name=" in head:
+            fname = "upload"
+            h = head.decode("latin-1")
+            if 'filename="' in h:
+                fname = h.split('filename="', 1)[1].split('"', 1)[0]
+            if data.endswith(b"\r\n"):
+                data = data[:-2]
+            return data, fname
+    return body, "upload"
+
+
 def create_app():
     if FastAPI is None:
         raise RuntimeError("fastapi is not installed")
@@ -138,14 +175,58 @@ def create_app():
 
     @app.exception_handler(Exception)
     async def errors(request, exc):
-        return JSONResponse(status_code=500 if not isinstance(exc, (ValueError, KeyError)) else 412,
-                            content=dict(__meta=dict(schema_type="H2OError"), msg=str(exc), exception_type=type(exc).__name__,
-                                         http_status=412))
+        status = 404 if isinstance(exc, KeyError) else (412 if isinstance(exc, (ValueError, TypeError)) else 500)
+        return JSONResponse(status_code=status, content=v3.error(str(exc), exc, status))
 
-    # ---- cloud
+    # ---- cloud, sessions, metadata
     @app.get("/3/Cloud")
+    @app.head("/3/Cloud")
     def cloud():
-        return _clean(runtime.cluster_status())
+        return v3.cloud(runtime.cluster_status())
+
+    @app.get("/3/Ping")
+    def ping():
+        st = runtime.cluster_status()
+        return {"__meta": v3.meta("PingV3", "Iced"), "cloud_uptime_millis": st["cloud_uptime_millis"],
+                "cloud_healthy": bool(st["cloud_healthy"]), "nodes": v3.cloud(st)["nodes"]}
+
+    @app.get("/3/Metadata/schemas/{name}")
+    def schema_meta(name: str):
+        if name not in v3.SCHEMA_FIELDS and (name.startswith("AutoML") or name.endswith(("V3", "V4", "V99"))):
+            v3.SCHEMA_FIELDS.setdefault(name, [])
+        r = v3.schema_metadata(name)
+        if r is None:
+            raise KeyError(f"unknown schema {name}")
+        return r
+
+    @app.post("/4/sessions")
+    def new_session():
+        return {"__meta": v3.meta("SessionIdV4", "Iced", 4), "session_key": dkv.new_key("_sid")}
+
+    @app.delete("/4/sessions/{sid}")
+    def end_session(sid: str):
+        return {"__meta": v3.meta("SessionIdV4", "Iced", 4), "session_key": sid}
+
+    @app.get("/3/SessionProperties")
+    @app.post("/3/SessionProperties")
+    async def session_props(request: Request):
+        p = await _params(request)
+        return {"__meta": v3.meta("SessionPropertyV3", "Iced"), "session_key": p.get("session_key"),
+                "key": p.get("key"), "value": p.get("value")}
+
+    @app.get("/3/Capabilities")
+    @app.get("/3/Capabilities/{kind}")
+    def capabilities(kind: str = "All"):
+        caps = [dict(name="GPU", value="MI355X (HIP)"), dict(name="Algos", value=",".join(sorted(builder.REGISTRY)))]
+        return {"__meta": v3.meta("CapabilitiesV3", "Iced"),
+                "capabilities": [{"__meta": v3.meta("CapabilityEntryV3", "Iced"), "name": c["name"]} for c in caps]}
+
+    @app.post("/3/LogAndEcho")
+    async def log_and_echo(request: Request):
+        p = await _params(request)
+        from ..utils import log
+        log.info(str(p.get("message", "")))
+        return {"__meta": v3.meta("LogAndEchoV3", "Iced"), "message": p.get("message", "")}
 
     @app.get("/3/About")
     def about():
@@ -202,7 +283,7 @@ def create_app():
     @app.delete("/3/DKV/{key}")
     def dkv_rm(key: str):
         dkv.remove(key)
-        return dict(key=key)
+        return {"__meta": v3.meta("RemoveV3", "Iced"), "key": v3.key(key)}
 
     # ---- ingest
     @app.post("/3/ImportFiles")
@@ -212,53 +293,148 @@ def create_app():
         p = await _params(request)
         path = p.get("path")
         files = P._expand(path)
-        return dict(path=path, files=files, destination_frames=files, fails=[], dels=[])
+        pat = p.get("pattern")
+        if pat:
+            import re
+            files = [f for f in files if re.search(pat, os.path.basename(f))]
+        return {"__meta": v3.meta("ImportFilesV3", "Iced"), "path": path, "pattern": pat, "files": files,
+                "destination_frames": files, "fails": [], "dels": []}
+
+    @app.post("/3/ImportFilesMulti")
+    async def import_files_multi(request: Request):
+        from ..io import parse as P
+        p = await _params(request)
+        paths = p.get("paths") or []
+        paths = paths if isinstance(paths, list) else [paths]
+        files, fails = [], []
+        pat = p.get("pattern")
+        import re
+        for pth in paths:
+            try:
+                fl = P._expand(pth)
+                files += [f for f in fl if not pat or re.search(pat, os.path.basename(f))]
+            except FileNotFoundError:
+                fails.append(pth)
+        return {"__meta": v3.meta("ImportFilesMultiV3", "Iced"), "paths": paths, "pattern": pat, "files": files,
+                "destination_frames": files, "fails": fails, "dels": []}
 
     @app.post("/3/ParseSetup")
     async def parse_setup(request: Request):
         from ..io import parse as P
         p = await _params(request)
         src = p.get("source_frames")
-        src = src if isinstance(src, list) else [src]
-        return _clean(P.parse_setup(src[0], header=int(p.get("check_header", 0) or 0), separator=p.get("separator")))
+        src = [_unquote(x) for x in (src if isinstance(src, list) else [src])]
+        sep = p.get("separator")
+        sep = chr(sep) if isinstance(sep, int) else sep
+        st = P.parse_setup(src[0], header=int(p.get("check_header", 0) or 0), separator=sep)
+        st = _clean(st)
+        tmap = {"real": "Numeric", "int": "Numeric", "enum": "Enum", "string": "String", "time": "Time"}
+        ctypes_ = [tmap.get(t, t) for t in (st.get("column_types") or [])]
+        sepv = st.get("separator", ",")
+        out = {"__meta": v3.meta("ParseSetupV3", "ParseSetup"),
+               "source_frames": [v3.frame_key(f) for f in src], "parse_type": st.get("parse_type", "CSV"),
+               "separator": ord(sepv) if isinstance(sepv, str) and sepv else 44, "single_quotes": False,
+               "check_header": st.get("check_header", 1), "column_names": st.get("column_names"),
+               "column_types": ctypes_, "na_strings": None, "column_name_filter": None, "column_offset": 0,
+               "column_count": 0, "destination_frame": st.get("destination_frame") or P._dest_name(src[0]),
+               "header_lines": 0, "number_columns": len(st.get("column_names") or []), "data": st.get("data"),
+               "chunk_size": 4194304, "total_filtered_column_count": len(st.get("column_names") or []),
+               "warnings": [], "skipped_columns": None, "custom_non_data_line_markers": None, "partition_by": None,
+               "escapechar": 0, "force_col_types": False, "tz_adjust_to_local": False}
+        return out
 
     @app.post("/3/Parse")
     async def parse(request: Request):
         from ..io import parse as P
         p = await _params(request)
         src = p.get("source_frames")
-        src = src if isinstance(src, list) else [src]
-        dest = p.get("destination_frame")
+        src = [_unquote(x) for x in (src if isinstance(src, list) else [src])]
+        dest = _unquote(p.get("destination_frame")) or P._dest_name(src[0])
         sep = p.get("separator")
         if isinstance(sep, int):
             sep = chr(sep)
+        ct = p.get("column_types")
+        if isinstance(ct, list):
+            tmap = {"numeric": "real", "enum": "enum", "string": "string", "time": "time", "uuid": "string",
+                    "categorical": "enum", "factor": "enum", "real": "real", "int": "int"}
+            ct = [tmap.get(str(t).lower(), None) for t in ct]
         job = Job("Parse", dest=dest)
         job.run_async(P.import_file, src, dest, True, int(p.get("check_header", 0) or 0), sep,
-                      p.get("column_names"), p.get("column_types"), p.get("na_strings"))
-        return dict(job=job.to_dict(), destination_frame=dict(name=dest))
+                      p.get("column_names"), ct, p.get("na_strings"))
+        return {"__meta": v3.meta("ParseV3", "Iced"), "job": v3.job(job), "destination_frame": v3.frame_key(dest),
+                "rows": 0}
 
     # ---- frames
-    @app.get("/3/Frames")
-    def frames():
-        return dict(frames=[dict(frame_id=dict(name=k), rows=v.nrows, columns=v.ncols) for k, v in dkv.items()
-                            if isinstance(v, H2OFrame)])
-
-    @app.get("/3/Frames/{fid}")
-    def frame(fid: str, row_offset: int = 0, row_count: int = 10):
+    def _get_frame(fid):
         fr = dkv.get(fid)
         if not isinstance(fr, H2OFrame):
-            raise KeyError(f"frame {fid} not found")
-        return _clean(dict(frames=[_frame_json(fr, row_offset, row_count)]))
+            raise KeyError(f"Object '{fid}' not found for argument: key")
+        return fr
+
+    @app.get("/3/Frames")
+    def frames():
+        out = []
+        for k, v in dkv.items():
+            if isinstance(v, H2OFrame):
+                out.append({"__meta": v3.meta("FrameBaseV3", "Frame"), "frame_id": v3.frame_key(k), "rows": v.nrows,
+                            "columns": v.ncols, "num_columns": v.ncols, "byte_size": 0, "is_text": False})
+        return v3.frames(out)
+
+    @app.get("/3/Frames/{fid}")
+    def frame(fid: str, row_offset: int = 0, row_count: int = 10, column_offset: int = 0, column_count: int = -1,
+              full_column_count: int = -1):
+        fr = _get_frame(fid)
+        return v3.frames([v3.frame(fr, row_offset, row_count, column_offset, column_count)])
+
+    @app.get("/3/Frames/{fid}/light")
+    def frame_light(fid: str, row_offset: int = 0, row_count: int = 10, column_offset: int = 0, column_count: int = -1):
+        fr = _get_frame(fid)
+        return v3.frames([v3.frame(fr, row_offset, row_count, column_offset, column_count, full=False)])
 
     @app.get("/3/Frames/{fid}/summary")
-    def frame_summary(fid: str):
-        fr = dkv.get(fid)
-        return _clean(dict(frames=[_frame_json(fr, 0, 10, full=True)]))
+    def frame_summary(fid: str, row_offset: int = 0, row_count: int = 10):
+        return v3.frames([v3.frame(_get_frame(fid), row_offset, row_count)])
+
+    @app.get("/3/Frames/{fid}/columns")
+    def frame_columns(fid: str):
+        fr = _get_frame(fid)
+        return v3.frames([v3.frame(fr, 0, 0, full=False)])
+
+    @app.get("/3/Frames/{fid}/columns/{col}")
+    @app.get("/3/Frames/{fid}/columns/{col}/summary")
+    def frame_column(fid: str, col: str, row_offset: int = 0, row_count: int = 10):
+        fr = _get_frame(fid)
+        fj = v3.frame(fr, row_offset, row_count, full=True)
+        fj["columns"] = [c for c in fj["columns"] if c["label"] == col]
+        if not fj["columns"]:
+            raise KeyError(f"column {col} not found")
+        return v3.frames([fj])
+
+    @app.get("/3/Frames/{fid}/columns/{col}/domain")
+    def frame_column_domain(fid: str, col: str):
+        fr = _get_frame(fid)
+        c = fr._col(col)
+        return v3.frames([]) | {"domain": [list(c.domain) if c.type == "enum" else None]}
 
     @app.delete("/3/Frames/{fid}")
     def frame_del(fid: str):
         dkv.remove(fid)
-        return dict(frame_id=fid)
+        return v3.frames([]) | {"frame_id": v3.frame_key(fid)}
+
+    @app.delete("/3/Frames")
+    def frames_del_all():
+        for k, v in list(dkv.items()):
+            if isinstance(v, H2OFrame):
+                dkv.remove(k)
+        return v3.frames([])
+
+    @app.get("/3/DownloadDataset")
+    @app.get("/3/DownloadDataset.bin")
+    def download_dataset(frame_id: str, hex_string: bool = False):
+        from fastapi.responses import Response
+        fr = _get_frame(frame_id)
+        return Response(content=fr.get_frame_data(), media_type="text/csv",
+                        headers={"Content-Disposition": f'attachment; filename="{frame_id}.csv"'})
 
     @app.post("/3/Frames/{fid}/export")
     async def frame_export(fid: str, request: Request):
@@ -290,14 +466,21 @@ def create_app():
     async def rapids_ep(request: Request):
         from ..rapids import rapids
         p = await _params(request)
-        r = rapids(p["ast"])
+        ast = p["ast"]
+        r = rapids(ast if isinstance(ast, str) else json.dumps(ast))
+        base = {"__meta": v3.meta("RapidsSchemaV3", "Iced"), "ast": ast, "session_id": p.get("session_id")}
         if isinstance(r, H2OFrame):
-            return dict(key=dict(name=r.frame_id), num_rows=r.nrows, num_cols=r.ncols)
+            return base | {"__meta": v3.meta("RapidsFrameV3", "Iced"), "key": v3.frame_key(r.frame_id),
+                           "num_rows": r.nrows, "num_cols": r.ncols}
         if isinstance(r, (list, tuple)):
-            return _clean(dict(scalar=None, vals=list(r)))
+            if all(isinstance(x, str) for x in r):
+                return base | {"__meta": v3.meta("RapidsStringsV3", "Iced"), "string": list(r)}
+            return base | {"__meta": v3.meta("RapidsNumbersV3", "Iced"),
+                           "scalar": [None if x is None or (isinstance(x, float) and math.isnan(x)) else float(x)
+                                      for x in r]}
         if isinstance(r, str):
-            return dict(string=r)
-        return _clean(dict(scalar=r))
+            return base | {"__meta": v3.meta("RapidsStringV3", "Iced"), "string": r}
+        return base | {"__meta": v3.meta("RapidsNumberV3", "Iced"), "scalar": _clean(r)}
 
     # ---- model builders
     @app.get("/3/ModelBuilders")
@@ -308,21 +491,51 @@ def create_app():
     @app.get("/3/ModelBuilders/{algo}")
     def model_builder(algo: str):
         s = builder.REGISTRY[algo]
-        return dict(model_builders={algo: dict(algo=algo, supervised=s.supervised)})
+        from ..models.params import schema
+        sch = schema(algo) or {}
+        params = [{"__meta": v3.meta("ModelParameterSchemaV3", "Iced"), "name": k, "label": k, "help": k,
+                   "required": k == "training_frame", "type": v3._param_type(v), "default_value": v3._json_value(v),
+                   "actual_value": v3._json_value(v), "level": "critical", "values": [], "gridable": False,
+                   "is_member_of_frames": [], "is_mutually_exclusive_with": []} for k, v in sch.items()]
+        return {"__meta": v3.meta("ModelBuildersV3", "Iced"),
+                "model_builders": {algo: {"__meta": v3.meta("ModelBuilderV3", "ModelBuilder"), "algo": algo,
+                                          "algo_full_name": v3._FULL.get(algo, algo), "can_build": ["Binomial",
+                                                                                                    "Multinomial",
+                                                                                                    "Regression"],
+                                          "supervised": s.supervised, "parameters": params, "visibility": "Stable"}}}
+
+    _RESERVED = ("training_frame", "validation_frame", "response_column", "model_id")
+
+    def _builder_args(algo, p):
+        fr = dkv.get(_unquote(p.pop("training_frame", None)))
+        if fr is None:
+            raise ValueError("training_frame is required")
+        vf = _unquote(p.pop("validation_frame", None))
+        vf = dkv.get(vf) if vf else None
+        y = _unquote(p.pop("response_column", None))
+        mid = _unquote(p.pop("model_id", None)) or builder.make_key(algo)
+        ig = p.pop("ignored_columns", None)
+        ig = [_unquote(c) for c in (ig if isinstance(ig, list) else ([ig] if ig else []))]
+        special = {p.get("weights_column"), p.get("offset_column"), p.get("fold_column"), y}
+        x = [n for n in fr.names if n not in ig and n not in special] if ig else None
+        for k in ("weights_column", "offset_column", "fold_column"):
+            if k in p:
+                p[k] = _unquote(p[k])
+        if isinstance(p.get("lambda"), list):
+            p["lambda_"] = p.pop("lambda")
+        elif "lambda" in p:
+            p["lambda_"] = p.pop("lambda")
+        return fr, vf, y, mid, x
 
     @app.post("/3/ModelBuilders/{algo}")
     async def build(algo: str, request: Request):
         p = await _params(request)
-        fr = dkv.get(p.pop("training_frame"))
-        vf = p.pop("validation_frame", None)
-        vf = dkv.get(vf) if vf else None
-        y = p.pop("response_column", None)
-        ignored = p.get("ignored_columns")
-        mid = p.pop("model_id", None) or builder.make_key(algo)
-        x = None
+        fr, vf, y, mid, x = _builder_args(algo, p)
+        builder._validate(builder.REGISTRY[algo], algo, p)       # ModelBuilder.init errors before the job starts
         job = Job(f"{algo} build", dest=mid)
         job.run_async(builder.train, algo, p, x, y, fr, vf, job, mid)
-        return dict(job=_clean(job.to_dict()), messages=[], error_count=0)
+        return {"__meta": v3.meta("ModelBuilderV3", "ModelBuilder"), "job": v3.job(job), "messages": [],
+                "error_count": 0, "algo": algo, "parameters": [], "__http_response": {}}
 
     @app.post("/3/ModelBuilders/{algo}/parameters")
     async def validate(algo: str, request: Request):
@@ -335,14 +548,14 @@ def create_app():
     # ---- jobs
     @app.get("/3/Jobs")
     def jobs():
-        return dict(jobs=[_clean(j.to_dict()) for j in list_jobs()])
+        return {"__meta": v3.meta("JobsV3", "Iced"), "job_id": None, "jobs": [v3.job(j) for j in list_jobs()]}
 
     @app.get("/3/Jobs/{key}")
     def job(key: str):
         j = dkv.get(key)
         if not isinstance(j, Job):
             raise KeyError(f"job {key} not found")
-        return dict(jobs=[_clean(j.to_dict())])
+        return {"__meta": v3.meta("JobsV3", "Iced"), "job_id": v3.key(key, "Key<Job>"), "jobs": [v3.job(j)]}
 
     @app.post("/3/Jobs/{key}/cancel")
     def cancel(key: str):
@@ -350,28 +563,50 @@ def create_app():
         return dict(key=key)
 
     # ---- models
+    def _get_model(mid):
+        m = dkv.get(mid)
+        if not isinstance(m, Model):
+            raise KeyError(f"Object '{mid}' not found for argument: key")
+        return m
+
     @app.get("/3/Models")
     def models():
-        return dict(models=[_model_json(v) for k, v in dkv.items() if isinstance(v, Model)])
+        return {"__meta": v3.meta("ModelsV3", "Models"), "model_id": None, "preview": False,
+                "find_compatible_frames": False, "models": [_model_json(v) for k, v in dkv.items() if isinstance(v, Model)]}
 
     @app.get("/3/Models/{mid}")
     def model(mid: str):
-        m = dkv.get(mid)
-        if not isinstance(m, Model):
-            raise KeyError(f"model {mid} not found")
-        return dict(models=[_model_json(m)])
+        return {"__meta": v3.meta("ModelsV3", "Models"), "model_id": v3.model_key(mid), "preview": False,
+                "find_compatible_frames": False, "models": [_model_json(_get_model(mid))]}
 
     @app.delete("/3/Models/{mid}")
     def model_del(mid: str):
         dkv.remove(mid)
-        return dict(model_id=mid)
+        return {"__meta": v3.meta("ModelsV3", "Models"), "model_id": v3.model_key(mid), "models": []}
+
+    @app.delete("/3/Models")
+    def models_del_all():
+        for k, v in list(dkv.items()):
+            if isinstance(v, Model):
+                dkv.remove(k)
+        return {"__meta": v3.meta("ModelsV3", "Models"), "models": []}
+
+    @app.get("/3/Models.java/{mid}")
+    @app.get("/3/Models.java/{mid}/preview")
+    def model_pojo(mid: str):
+        from fastapi.responses import Response
+        from ..mojo.pojo import pojo_source
+        m = _get_model(mid)
+        return Response(content=pojo_source(m), media_type="text/plain",
+                        headers={"Content-Disposition": f'attachment; filename="{mid}.java"'})
 
     @app.get("/3/Models/{mid}/mojo")
     def mojo(mid: str):
+        import tempfile
         from ..mojo.writer import write_mojo
-        path = os.path.join("/tmp", f"{mid}.zip")
-        write_mojo(dkv.get(mid), path)
-        return FileResponse(path, filename=f"{mid}.zip")
+        path = os.path.join(tempfile.gettempdir(), f"{mid}.zip")
+        write_mojo(_get_model(mid), path)
+        return FileResponse(path, filename=f"{mid}.zip", headers={"Content-Disposition": f'attachment; filename="{mid}.zip"'})
 
     @app.get("/99/Models.bin/{mid}")
     def save_bin(mid: str, dir: str = "/tmp", force: bool = True):
@@ -396,20 +631,63 @@ def create_app():
     @app.post("/3/Predictions/models/{mid}/frames/{fid}")
     async def predict(mid: str, fid: str, request: Request):
         p = await _params(request)
-        m, fr = dkv.get(mid), dkv.get(fid)
+        m, fr = _get_model(mid), _get_frame(fid)
         pred = m.predict(fr)
-        dest = p.get("predictions_frame")
+        dest = _unquote(p.get("predictions_frame"))
         if dest:
             dkv.remove(pred.frame_id)
             pred.frame_id = dest
             dkv.put(dest, pred)
-        return dict(predictions_frame=dict(name=pred.frame_id), model_metrics=[])
+        mm = None
+        if m.info.response and m.info.response in fr.names:
+            try:
+                mm = v3.metrics(m.model_performance(fr), m.model_category, mid, fid, m.algo)
+            except Exception:  # noqa: BLE001 - predictions without a usable response column
+                mm = None
+        return {"__meta": v3.meta("ModelMetricsListSchemaV3", "ModelMetricsList"), "model": v3.model_key(mid),
+                "frame": v3.frame_key(fid), "predictions_frame": v3.frame_key(pred.frame_id),
+                "model_metrics": [mm] if mm else [], "deviances_frame": None, "reconstruction_error": False,
+                "leaf_node_assignment": False, "exemplar_index": -1, "deep_features_hidden_layer": -1}
+
+    @app.post("/4/Predictions/models/{mid}/frames/{fid}")
+    async def predict4(mid: str, fid: str, request: Request):
+        p = await _params(request)
+        m, fr = _get_model(mid), _get_frame(fid)
+        dest = _unquote(p.get("predictions_frame")) or f"prediction_{mid}_on_{fid}"
+        job = Job("Predictions", dest=dest)
+
+        def run():
+            pred = m.predict(fr)
+            dkv.remove(pred.frame_id)
+            pred.frame_id = dest
+            dkv.put(dest, pred)
+            return pred
+        job.run_async(run)
+        return {"__meta": v3.meta("JobV4", "Job", 4), "job": v3.job(job), "key": v3.key(job.key, "Key<Job>"),
+                "status": "RUNNING", "dest": v3.frame_key(dest)}
 
     @app.post("/3/ModelMetrics/models/{mid}/frames/{fid}")
     def metrics(mid: str, fid: str):
-        m, fr = dkv.get(mid), dkv.get(fid)
+        m, fr = _get_model(mid), _get_frame(fid)
         mm = m.model_performance(fr)
-        return _clean(dict(model_metrics=[dict(mm or {}, model=dict(name=mid), frame=dict(name=fid))]))
+        return {"__meta": v3.meta("ModelMetricsListSchemaV3", "ModelMetricsList"), "model": v3.model_key(mid),
+                "frame": v3.frame_key(fid), "model_metrics": [v3.metrics(mm, m.model_category, mid, fid, m.algo)]}
+
+    @app.get("/3/ModelMetrics")
+    @app.get("/3/ModelMetrics/models/{mid}")
+    @app.get("/3/ModelMetrics/models/{mid}/frames/{fid}")
+    @app.get("/3/ModelMetrics/frames/{fid}")
+    @app.get("/3/ModelMetrics/frames/{fid}/models/{mid}")
+    def metrics_list(mid: str | None = None, fid: str | None = None):
+        out = []
+        for k, v in dkv.items():
+            if isinstance(v, Model) and (mid is None or k == mid):
+                for which in ("training_metrics", "validation_metrics"):
+                    mm = v.output.get(which)
+                    fk = v.output.get("training_frame" if which == "training_metrics" else "validation_frame")
+                    if mm is not None and (fid is None or fk == fid):
+                        out.append(v3.metrics(mm, v.model_category, k, fk, v.algo))
+        return {"__meta": v3.meta("ModelMetricsListSchemaV3", "ModelMetricsList"), "model_metrics": out}
 
     # ---- grid & automl
     @app.post("/99/Grid/{algo}")
@@ -423,9 +701,15 @@ def create_app():
         vf = p.pop("validation_frame", None)
         y = p.pop("response_column", None)
         rdir = p.pop("recovery_dir", None)
+        y = _unquote(y)
+        ig = p.pop("ignored_columns", None)
+        ig = [_unquote(c) for c in (ig if isinstance(ig, list) else ([ig] if ig else []))]
+        x = [n for n in fr.names if n not in ig and n != y] if ig else None
+        p.pop("parallelism", None)
         job = Job(f"grid {algo}", dest=gid)
-        job.run_async(grid_search, algo, hyper, p, None, y, fr, dkv.get(vf) if vf else None, gid, crit, 1, job, rdir)
-        return dict(job=_clean(job.to_dict()), grid_id=dict(name=gid))
+        job.run_async(grid_search, algo, hyper, p, x, y, fr, dkv.get(_unquote(vf)) if vf else None, gid, crit, 1, job, rdir)
+        return {"__meta": v3.meta("GridSearchSchemaV99", "GridSearch", 99), "job": v3.job(job),
+                "grid_id": v3.key(gid, "Key<Grid>"), "hyper_parameters": hyper, "search_criteria": crit}
 
     @app.post("/3/Recovery/resume")
     async def recovery_resume(request: Request):
@@ -439,34 +723,108 @@ def create_app():
     @app.get("/99/Grids/{gid}")
     def get_grid(gid: str, sort_by: str | None = None, decreasing: bool | None = None):
         g = dkv.get(gid)
+        if g is None:
+            raise KeyError(f"grid {gid} not found")
         rows, key = g.sorted_models(sort_by, decreasing)
-        return _clean(dict(grid_id=dict(name=gid), model_ids=[dict(name=m.key) for m, _, _ in rows],
-                           hyper_names=list(g.hyper_params), failed_params=g.failures,
-                           summary_table=[dict(zip(g.hyper_params, h), model_id=m.key, **{key: v}) for m, h, v in rows]))
+        hn = list(g.hyper_params)
+        table = v3.twodim("Hyper-Parameter Search Summary", [(h, "string", "%s") for h in hn] +
+                          [("model_ids", "string", "%s"), (key, "double", "%.5f")],
+                          [[str(x) for x in h] + [m.key, v] for m, h, v in rows],
+                          f"ordered by {'decreasing' if decreasing else 'increasing'} {key}")
+        fails = g.failures or []
+        return {"__meta": v3.meta("GridSchemaV99", "Grid", 99), "grid_id": v3.key(gid, "Key<Grid>"),
+                "model_ids": [v3.model_key(m.key) for m, _, _ in rows], "hyper_names": hn,
+                "failed_params": [f.get("params") if isinstance(f, dict) else f for f in fails],
+                "failure_details": [str(f.get("error") if isinstance(f, dict) else f) for f in fails],
+                "failure_stack_traces": [str(f.get("error") if isinstance(f, dict) else f) for f in fails],
+                "failed_raw_params": [], "warning_details": [], "summary_table": table, "scoring_history": None,
+                "cross_validation_metrics_summary": None, "training_metrics": [], "validation_metrics": [],
+                "cross_validation_metrics": [], "export_checkpoints_dir": None, "sort_by": sort_by or key,
+                "decreasing": bool(decreasing)}
+
+    @app.get("/99/Models/{mid}")
+    def model99(mid: str):
+        return {"__meta": v3.meta("ModelsV99", "Models", 99), "model_id": v3.model_key(mid),
+                "models": [_model_json(_get_model(mid))]}
+
+    @app.post("/3/PostFile")
+    @app.post("/3/PostFile.bin")
+    async def post_file(request: Request, destination_frame: str | None = None):
+        """Client uploads (multipart/form-data or raw body) land in a server-side temp file whose path
+        is the raw key the following ParseSetup/Parse use (h2o-py H2OFrame(python_obj), upload_file)."""
+        import tempfile
+        body = await request.body()
+        ct = request.headers.get("content-type", "")
+        data, fname = body, "upload"
+        if "multipart/form-data" in ct and "boundary=" in ct:
+            data, fname = _multipart_first_file(body, ct.split("boundary=", 1)[1].strip().strip('"'))
+        ext = os.path.splitext(fname)[1] or ".csv"
+        fd, path = tempfile.mkstemp(prefix="h2o_upload_", suffix=ext)
+        with os.fdopen(fd, "wb") as f:
+            f.write(data)
+        return {"__meta": v3.meta("PostFileV3", "Iced"), "destination_frame": path, "total_bytes": len(data)}
 
     @app.post("/99/AutoMLBuilder")
     async def automl_build(request: Request):
         from ..automl import AutoML
         p = await _params(request)
         spec = p.get("input_spec", p)
-        bs = p.get("build_control", {})
-        bm = p.get("build_models", {})
+        bs = p.get("build_control", {}) or {}
+        bm = p.get("build_models", {}) or {}
         sc = bs.get("stopping_criteria", {}) if isinstance(bs, dict) else {}
+
+        def name_of(v):
+            return v.get("name") if isinstance(v, dict) else _unquote(v)
+        inc = bm.get("include_algos")
+        exc = bm.get("exclude_algos")
         aml = AutoML(project_name=bs.get("project_name"), max_models=sc.get("max_models"),
-                     max_runtime_secs=sc.get("max_runtime_secs"), nfolds=bs.get("nfolds", 5), seed=sc.get("seed"),
-                     include_algos=bm.get("include_algos"), exclude_algos=bm.get("exclude_algos"))
-        fr = dkv.get(spec["training_frame"]) if isinstance(spec.get("training_frame"), str) else dkv.get(spec["training_frame"]["name"])
+                     max_runtime_secs=sc.get("max_runtime_secs") or None, nfolds=bs.get("nfolds", 5),
+                     seed=sc.get("seed"), include_algos=inc, exclude_algos=exc,
+                     sort_metric=spec.get("sort_metric") or "AUTO")
+        fr = dkv.get(name_of(spec["training_frame"]))
+        y = name_of(spec.get("response_column"))
+        ig = spec.get("ignored_columns") or []
+        x = [n for n in fr.names if n not in ig and n != y] if ig else None
+        vf = dkv.get(name_of(spec["validation_frame"])) if spec.get("validation_frame") else None
+        lb = dkv.get(name_of(spec["leaderboard_frame"])) if spec.get("leaderboard_frame") else None
         job = Job("AutoML", dest=aml.project_name)
-        job.run_async(aml.train, None, spec.get("response_column"), fr, None, None, None, None, None, job)
-        return dict(job=_clean(job.to_dict()), automl_id=dict(name=aml.project_name))
+        job.run_async(aml.train, x, y, fr, vf, lb, None, None, None, job)
+        return {"__meta": v3.meta("AutoMLBuilderV99", "AutoMLBuilder", 99), "job": v3.job(job),
+                "build_control": {"project_name": aml.project_name}, "automl_id": v3.key(aml.project_name, "Key<AutoML>")}
+
+    def _leaderboard_table(aml):
+        rows, cols = aml.leaderboard_rows()
+        return rows, v3.twodim("Leaderboard", [("model_id", "string", "%s")] + [(c, "double", "%.6f") for c in cols[1:]],
+                               [[r["model_id"]] + [r[c] for c in cols[1:]] for r in rows],
+                               f"models sorted by {cols[1] if len(cols) > 1 else ''}",
+                               row_headers=[str(i) for i in range(len(rows))])
 
     @app.get("/99/AutoML/{pid}")
-    @app.get("/99/Leaderboards/{pid}")
     def automl_get(pid: str):
         aml = dkv.get(pid)
-        rows, cols = aml.leaderboard_rows()
-        return _clean(dict(project_name=pid, leaderboard_table=dict(columns=cols, data=rows),
-                           leader=dict(name=rows[0]["model_id"]) if rows else None, event_log=aml.event_log))
+        if aml is None:
+            raise KeyError(f"AutoML {pid} not found")
+        rows, table = _leaderboard_table(aml)
+        ev = v3.twodim("Event Log", [("timestamp", "string", "%s"), ("level", "string", "%s"), ("stage", "string", "%s"),
+                                     ("message", "string", "%s"), ("name", "string", "%s"), ("value", "string", "%s")],
+                       [[time.strftime("%H:%M:%S", time.localtime(e["timestamp"])), "Info", "ModelTraining",
+                         e["message"], "", ""] for e in aml.event_log],
+                       row_headers=[str(i) for i in range(len(aml.event_log))])
+        return {"__meta": v3.meta("AutoMLV99", "AutoML", 99), "automl_id": v3.key(pid, "Key<AutoML>"),
+                "project_name": pid, "leaderboard": {"__meta": v3.meta("LeaderboardV99", "Leaderboard", 99),
+                                                     "project_name": pid,
+                                                     "models": [v3.model_key(r["model_id"]) for r in rows]},
+                "leaderboard_table": table, "event_log": {"events": aml.event_log}, "event_log_table": ev,
+                "modeling_steps": [], "leader": v3.model_key(rows[0]["model_id"]) if rows else None}
+
+    @app.get("/99/Leaderboards/{pid}")
+    def leaderboard_get(pid: str):
+        aml = dkv.get(pid)
+        if aml is None:
+            raise KeyError(f"AutoML {pid} not found")
+        rows, table = _leaderboard_table(aml)
+        return {"__meta": v3.meta("LeaderboardV99", "Leaderboard", 99), "project_name": pid,
+                "models": [v3.model_key(r["model_id"]) for r in rows], "table": table}
 
     return app
 

@@ -858,6 +858,14 @@ class H2OFrame:
                     r = fn(a, torch.full_like(a, float(code)))
                     r = torch.where(c.data < 0, torch.full_like(r.double(), float("nan")), r.double())
                     cols.append(Column(c.name, "real", r))
+                elif isinstance(other, str) and (c.type == "string" or bool(torch.isnan(c.as_float()).all())):
+                    # string compare (AstBinOp string ops: a missing string equals ""); ranks in the sorted
+                    # union keep <, > lexicographic
+                    vals = ["" if v is None or (isinstance(v, float) and math.isnan(v)) else str(v)
+                            for v in (c.strings if c.type == "string" else [None] * self._nlocal)]
+                    lut = {s: i for i, s in enumerate(sorted(set(vals) | {other}))}
+                    a = torch.tensor([float(lut[v]) for v in vals], dtype=torch.float64, device=engine_device())
+                    cols.append(Column(c.name, "real", fn(a, torch.full_like(a, float(lut[other]))).double()))
                 else:
                     cols.append(Column(c.name, "real", fn(c.as_float(), torch.as_tensor(float(other), dtype=torch.float64)).double()))
         for c in cols:

@@ -82,7 +82,7 @@ class Expander:
         sd = var.clamp(min=0).sqrt()
         self.num_mean = mu
         self.num_fill = None
-        if str(self.missing).lower() == "plugvalues":
+        if str(self.missing).lower().replace("_", "") == "plugvalues":
             pv = self._plug_dict()
             fill = mu.clone()
             for i, j in enumerate(self.nums):

@@ -24,6 +24,7 @@ import torch
 from .. import metrics as mm
 from ..ops.dense import ACT, bias_act
 from ..parallel import collectives as coll
+from .params import canon
 from .base import DataInfo, Model, ScoreKeeper, make_key, model_category
 from .datainfo import Expander
 
@@ -54,6 +55,9 @@ class MLP(torch.nn.Module):
             width = dims[i + 1] * (2 if maxout else 1)
             lin = torch.nn.Linear(dims[i], width)
             self._init(lin, dims[i], width, init_dist, init_scale, gen)
+            if act == "rectifier" or maxout:     # DeepLearningModelInfo.initializeMembers: 0.5 / 1 (no dead units)
+                with torch.no_grad():
+                    lin.bias.fill_(0.5 if i == 0 else 1.0)
             self.hidden.append(lin)
         self.out = torch.nn.Linear(dims[-1], n_out)
         self._init(self.out, dims[-1], n_out, init_dist, init_scale, gen)
@@ -62,7 +66,7 @@ class MLP(torch.nn.Module):
     @staticmethod
     def _init(lin, fan_in, fan_out, dist, scale, gen):
         with torch.no_grad():
-            d = dist.lower()
+            d = canon(dist)
             if d == "uniformadaptive":
                 r = math.sqrt(6.0 / (fan_in + fan_out))
                 lin.weight.uniform_(-r, r, generator=gen)
@@ -204,7 +208,7 @@ class DeepLearningTrainer:
         # gather bytes; GEMM inputs need no per-step cast)
         bf16 = dev.type == "cuda" and str(p["compute_dtype"]).lower() in ("bf16", "bfloat16") and not bool(p["autoencoder"])
         Z = ex.transform(X, dtype=torch.bfloat16 if bf16 else torch.float32)
-        act_name = str(p["activation"]).lower()
+        act_name = canon(p["activation"])
         with_drop = act_name.endswith("withdropout")
         base = act_name.replace("withdropout", "")
         maxout = base == "maxout"
@@ -264,7 +268,10 @@ class DeepLearningTrainer:
                 yt = torch.nan_to_num(y, nan=0).long()
         B = int(p["mini_batch_size"])
         if B <= 1:
-            B = int(p["gpu_batch_size"])      # Hogwild single-row SGD -> GPU mini-batches
+            # Hogwild single-row SGD -> GPU mini-batches of up to gpu_batch_size rows, but never fewer than
+            # ~1024 updates per epoch: ADADELTA starts from zero step sizes, so a small frame trained in a
+            # handful of large batches would barely move (the reference does one update per row)
+            B = max(1, min(int(p["gpu_batch_size"]), N_glob // 1024))
         from ..ops.dense import FlatParams
         fp = FlatParams(net)                 # params/grads as views of two flat buffers
         params = fp.params

@@ -36,6 +36,12 @@ def resolve_distribution(name, info: DataInfo) -> str:
         if info.response_domain is None:
             return "gaussian"
         return "bernoulli" if len(info.response_domain) == 2 else "multinomial"
+    # GBM.init: a categorical response needs a classification distribution and vice versa
+    classif = name in ("bernoulli", "quasibinomial", "multinomial", "modified_huber", "custom")
+    if info.response_domain is not None and not classif:
+        raise ValueError(f"distribution {name!r} is not allowed for the categorical response {info.response!r}")
+    if info.response_domain is None and classif and name != "custom":
+        raise ValueError(f"distribution {name!r} needs a categorical response; {info.response!r} is numeric")
     return name
 
 

@@ -30,6 +30,7 @@ from ..parallel import collectives as coll
 from ..ops import gram as G
 from .base import DataInfo, Model, make_key
 from .datainfo import Expander
+from .params import canon
 from ..ops.segment import segment_sum
 
 GLM_DEFAULTS = dict(family="AUTO", link="family_default", solver="AUTO", alpha=None, lambda_=None, lambda_search=False,
@@ -338,14 +339,17 @@ class GLMTrainer:
         self.penalty = None     # optional (P+1)x(P+1) quadratic penalty (GAM)
 
     def _family(self, info):
-        fam = str(self.p["family"]).lower()
+        fam = canon(self.p["family"])
         if fam == "auto":
             if info.response_domain is None:
                 fam = "gaussian"
             else:
                 fam = "binomial" if len(info.response_domain) == 2 else "multinomial"
-        link = str(self.p["link"]).lower()
-        if link in ("family_default", "auto", ""):
+        if info.response_domain is not None and fam not in ("binomial", "quasibinomial", "multinomial", "ordinal",
+                                                            "fractionalbinomial"):
+            raise ValueError(f"family {self.p['family']!r} needs a numeric response; {info.response!r} is categorical")
+        link = canon(self.p["link"])
+        if link in ("familydefault", "auto", ""):
             link = DEFAULT_LINK[fam]
         return fam, link
 
@@ -369,7 +373,7 @@ class GLMTrainer:
         w = torch.ones(N, dtype=torch.float64, device=dev) if w is None else w.double()
         y = y.double()
         ok = ~torch.isnan(y)
-        if str(p["missing_values_handling"]).lower() == "skip":
+        if canon(p["missing_values_handling"]) == "skip":
             ok &= ~torch.isnan(X).any(0)
         w = torch.where(ok, w, torch.zeros_like(w))
         y = torch.where(ok, y, torch.zeros_like(y))
@@ -382,7 +386,7 @@ class GLMTrainer:
         Zi = torch.cat([Z, torch.ones(N, 1, dtype=Z.dtype, device=dev) if intercept else torch.zeros(N, 1, dtype=Z.dtype, device=dev)], 1)
         alpha = p["alpha"]
         alpha = float((alpha if isinstance(alpha, (int, float)) else alpha[0]) if alpha is not None else
-                      (0.0 if str(p["solver"]).upper() == "L_BFGS" else 0.5))
+                      (0.0 if canon(p["solver"]) == "lbfgs" else 0.5))
         W = float(coll.all_reduce_scalar(float(w.sum())) if coll.is_dist() else w.sum())
         nobs = int(coll.all_reduce_scalar(float((w > 0).sum()))) if coll.is_dist() else int((w > 0).sum())
         obj_reg = float(p["obj_reg"]) if p["obj_reg"] and p["obj_reg"] > 0 else 1.0 / W
@@ -390,11 +394,11 @@ class GLMTrainer:
         model.device = dev
         model.expander = ex
         model.output.update(family=fam, link=link, alpha=alpha)
-        solver = str(p["solver"]).upper()
-        if fam == "multinomial" and solver != "L_BFGS":
+        solver = canon(p["solver"])
+        if fam == "multinomial" and solver != "lbfgs":
             beta, path = self._fit_multinomial_irls(Zi, y, w, off, alpha, obj_reg, intercept, info, nobs)
             lam_best = path[-1]["lambda"] if path else 0.0
-        elif fam in ("multinomial", "ordinal") or solver == "L_BFGS":
+        elif fam in ("multinomial", "ordinal") or solver == "lbfgs":
             beta, path = self._fit_lbfgs_or_multi(fam, link, Zi, y, w, off, alpha, obj_reg, intercept, info, ex)
             lam_best = path[-1]["lambda"] if path else 0.0
         else:

@@ -28,7 +28,7 @@ GLRM_DEFAULTS = dict(k=1, loss="Quadratic", multi_loss="Categorical", loss_by_co
 
 
 def _loss(name, u, a, period=1):
-    n = name.lower()
+    n = name.lower().replace("_", "")
     if n == "quadratic":
         return (u - a) ** 2
     if n == "absolute":
@@ -48,7 +48,7 @@ def _loss(name, u, a, period=1):
 
 
 def _reg_value(name, M, axis):
-    n = name.lower()
+    n = name.lower().replace("_", "")
     if n == "none":
         return torch.zeros((), dtype=M.dtype, device=M.device)
     if n in ("quadratic", "l2"):
@@ -60,7 +60,7 @@ def _reg_value(name, M, axis):
 
 def _prox(name, M, step_gamma, axis):
     """Proximal operator of the regularizer along rows of X (axis=1) / columns of Y (axis=0)."""
-    n = name.lower()
+    n = name.lower().replace("_", "")
     if n in ("none",):
         return M
     if n == "quadratic":
@@ -183,7 +183,7 @@ class GLRMTrainer:
         A = Zfull
         N, P = A.shape
         k = int(p["k"])
-        init = str(p["init"]).lower()
+        init = str(p["init"]).lower().replace("_", "")
         if init == "user" and p.get("user_y") is not None:
             uy = p["user_y"]
             Y = torch.as_tensor(uy.as_tensor().numpy() if hasattr(uy, "as_tensor") else np.asarray(uy), dtype=torch.float64).to(dev)

@@ -184,7 +184,7 @@ class KMeansTrainer:
         self.ex = Expander(info, standardize=p["standardize"], use_all_factor_levels=True).fit(
             X, w, reduce=coll.all_reduce_ if coll.is_dist() else None)
         Z = self.ex.transform(X)
-        how = str(p["init"]).lower()
+        how = str(p["init"]).lower().replace("_", "")
         max_it = int(p["max_iterations"])
         if p["estimate_k"]:
             # KMeans.java: deterministic growth from k=1, split the worst cluster, stop when the relative

@@ -69,8 +69,16 @@ UNSUPPORTED = {
 _NEUTRAL = (None, "AUTO", "auto", "", [], {}, False)
 
 
+def canon(v) -> str:
+    """Spelling-independent form of an enum value: h2o-py ``uniform_adaptive``, Java
+    ``UniformAdaptive`` and ``UNIFORM_ADAPTIVE`` all become ``uniformadaptive``."""
+    return str(v).lower().replace("_", "").replace(" ", "")
+
+
 def _is_default(v, default) -> bool:
     if v is None:
+        return True
+    if isinstance(v, str) and isinstance(default, str) and canon(v) == canon(default):
         return True
     if isinstance(v, float) and isinstance(default, (int, float)) and default is not None and not isinstance(default, bool):
         return math.isclose(v, float(default)) or (math.isinf(v) and math.isinf(float(default)))

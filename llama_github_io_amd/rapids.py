@@ -66,10 +66,12 @@ def parse(tokens, i=0):
         return ("num", 1.0 if t == "TRUE" else 0.0), i + 1
     if t == "NA":
         return ("num", float("nan")), i + 1
-    m = re.fullmatch(r"(-?\d+):(\d+)", t)
+    # ASTNumList span "start:count[:stride]"; a NaN count is open-ended (h2o-py renders x[1:] this way)
+    m = re.fullmatch(r"(-?\d+):(\d+|nan|NaN)(?::(\d+))?", t)
     if m:
-        a, n = int(m.group(1)), int(m.group(2))
-        return ("span", (a, n)), i + 1
+        a = int(m.group(1))
+        n = None if m.group(2).lower() == "nan" else int(m.group(2))
+        return ("span", (a, n, int(m.group(3) or 1))), i + 1
     try:
         return ("num", float(t)), i + 1
     except ValueError:
@@ -87,10 +89,17 @@ def _frame(v):
 def _idx_list(v, n=None):
     if isinstance(v, (int, float)):
         return [int(v)]
+    if isinstance(v, tuple):
+        v = [v]
     out = []
     for x in v:
         if isinstance(x, tuple):
-            out += list(range(x[0], x[0] + x[1]))
+            a, cnt, st = (tuple(x) + (1,))[:3]
+            if cnt is None:
+                if n is None:
+                    raise ValueError("an open-ended span needs the extent of the indexed axis")
+                cnt = max(0, -(-(n - a) // st))
+            out += list(range(a, a + cnt * st, st))
         else:
             out.append(x if isinstance(x, str) else int(x))
     return out
@@ -149,11 +158,55 @@ def _reduce(name):
     return f
 
 
+def _as_frame(v):
+    """A Rapids value as a frame: list of lists -> one column each (padded with NA; string levels ->
+    enum columns like AstLevels), flat list -> one row, scalar / string -> 1x1."""
+    import numpy as np
+    if isinstance(v, H2OFrame):
+        return v
+    if isinstance(v, (list, tuple)) and v and all(isinstance(x, (list, tuple)) for x in v):
+        L = max((len(x) for x in v), default=0)
+        data = {}
+        for j, col in enumerate(v):
+            vals = list(col) + [None] * (L - len(col))
+            data[f"C{j + 1}"] = vals
+        types = {k: ("enum" if any(isinstance(x, str) for x in c) else None) for k, c in data.items()}
+        return H2OFrame(data, column_types={k: t for k, t in types.items() if t})
+    if isinstance(v, (list, tuple)):
+        return H2OFrame({f"C{j + 1}": [x] for j, x in enumerate(v)})
+    if isinstance(v, str):
+        return H2OFrame({"C1": [v]}, column_types={"C1": "string"})
+    return H2OFrame({"C1": [float("nan") if v is None else float(v)]})
+
+
+def _mean(a, na_rm=1, axis=0, *rest):
+    """AstMean: ``(mean fr na_rm axis)`` -> a 1-row frame of column means (axis 0) or a column of row
+    means (axis 1); a scalar argument passes through."""
+    if not isinstance(a, H2OFrame):
+        return float(a)
+    skip = bool(na_rm) if not isinstance(na_rm, str) else na_rm.upper() == "TRUE"
+    if int(axis or 0) == 1:
+        return a.mean(skipna=skip, axis=1)
+    return a.mean(skipna=skip, return_frame=True)
+
+
+def _reduce_na(name):
+    """sumNA / maxNA / minNA (AstSumNA ...): like sum / max / min but any missing value -> NaN."""
+    base = _reduce(name)
+
+    def f(a, *rest):
+        fr = _frame(a)
+        if any(n > 0 for n in fr.nacnt()):
+            return float("nan")
+        return base(a, *rest)
+    return f
+
+
 def _rows(fr, sel):
     fr = _frame(fr)
     if isinstance(sel, H2OFrame):
         return fr[sel]
-    idx = _idx_list(sel)
+    idx = _idx_list(sel, fr.nrows)
     neg = [i for i in idx if isinstance(i, int) and i < 0]
     if neg and len(neg) == len(idx):
         drop = {-i - 1 for i in neg}
@@ -165,7 +218,7 @@ def _cols(fr, sel):
     fr = _frame(fr)
     if isinstance(sel, (int, float, str)):
         sel = [sel]
-    idx = _idx_list(sel)
+    idx = _idx_list(sel, fr.ncols)
     if idx and all(isinstance(i, int) and i < 0 for i in idx):
         drop = {-i - 1 for i in idx}
         idx = [i for i in range(fr.ncols) if i not in drop]
@@ -187,8 +240,9 @@ class Session:
             **{n: _unary(n) for n in ("log", "exp", "sqrt", "abs", "ceiling", "floor", "trunc", "sign", "sin", "cos",
                                       "tan", "tanh", "log10", "log2", "log1p", "expm1")},
             "ceiling": lambda a: _frame(a).ceil(),
-            **{n: _reduce(n) for n in ("sum", "mean", "min", "max", "sd", "var", "median")},
-            "sumNA": _reduce("sum"), "maxNA": _reduce("max"), "minNA": _reduce("min"),
+            **{n: _reduce(n) for n in ("sum", "min", "max", "sd", "var", "median")},
+            "mean": _mean,
+            "sumNA": _reduce_na("sum"), "maxNA": _reduce_na("max"), "minNA": _reduce_na("min"),
             "nrow": lambda a: float(_frame(a).nrows), "ncol": lambda a: float(_frame(a).ncols),
             "dim": lambda a: [float(_frame(a).nrows), float(_frame(a).ncols)],
             "rows": _rows, "cols": _cols, "cols_py": _cols,
@@ -230,9 +284,15 @@ class Session:
 
     # ---- special forms
     def _assign(self, name, value):
-        if isinstance(value, H2OFrame):
-            dkv.put(name, value)
-            value.frame_id = name
+        """``(tmp= name expr)`` / ``(assign name expr)``: the value becomes a named frame in the DKV (Java
+        Rapids always assigns frames: scalars become 1x1 frames, lists of lists one column per list)."""
+        if not isinstance(value, H2OFrame):
+            value = _as_frame(value)
+        elif value.frame_id != name and dkv.get(value.frame_id) is value:
+            # the source keeps its own key (AstAssign builds a new Frame over the same vecs)
+            value = H2OFrame._from_columns([value._col(n) for n in value.names])
+        dkv.put(name, value)
+        value.frame_id = name
         return value
 
     def _rm(self, name):
@@ -299,6 +359,8 @@ class Session:
         name = op[1]
         if name in ("tmp=", "assign"):
             return self._assign(v[1][1], self.eval_node(v[2]))
+        if name == "rm" and v[1][0] in ("id", "str"):
+            return self._rm(v[1][1])           # by key: the object may also live under another key
         fn = self.prims.get(name)
         if fn is None:
             raise NotImplementedError(f"rapids primitive {name!r}")
@@ -683,7 +745,7 @@ def _model_obj(m):
 
 def _assign_cols(dst, src, cols, rows=None):
     """``(:= dst src cols rows)``: overwrite columns (optionally rows) of dst in place (AstRectangleAssign)."""
-    idx = _idx_list(cols)
+    idx = _idx_list(cols, dst.ncols)
     names = [dst.names[int(i)] if not isinstance(i, str) else i for i in idx]
     for k, n in enumerate(names):
         if isinstance(src, H2OFrame):
@@ -698,7 +760,7 @@ def _assign_cols(dst, src, cols, rows=None):
                 continue
             dst._cols[n] = Column(n, "real", newv.clone())
         else:
-            ridx = torch.as_tensor(_idx_list(rows), dtype=torch.long, device=engine_device())
+            ridx = torch.as_tensor(_idx_list(rows, dst.nrows), dtype=torch.long, device=engine_device())
             cur = dst._col(n).data.double().clone()
             cur[ridx] = newv if newv.numel() == ridx.numel() else newv[0]
             dst._cols[n] = Column(n, "real", cur)
