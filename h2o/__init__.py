@@ -27,21 +27,27 @@ _progress = [True]
 
 
 class _Cluster:
+    def _status(self):
+        from . import _conn
+        if _conn.is_remote():
+            return _conn.current().request("GET /3/Cloud")
+        return _rt.cluster_status()
+
     def show_status(self, detailed=False):
-        st = _rt.cluster_status()
+        st = self._status()
         print(st)
         return st
 
     def status(self):
-        return _rt.cluster_status()
+        return self._status()
 
     @property
     def cloud_name(self):
-        return _rt.cluster_status()["cloud_name"]
+        return self._status()["cloud_name"]
 
     @property
     def cloud_size(self):
-        return _rt.cluster_status()["cloud_size"]
+        return self._status()["cloud_size"]
 
     def shutdown(self, prompt=False):
         _rt.shutdown()
@@ -68,8 +74,27 @@ def init(url=None, ip=None, port=None, name=None, nthreads=-1, max_mem_size=None
     return _cluster
 
 
-def connect(server=None, url=None, ip=None, port=None, verbose=True, config=None, **kw):
-    return init(verbose=verbose)
+def connect(server=None, url=None, ip=None, port=None, https=None, verify_ssl_certificates=None, auth=None,
+            proxy=None, cookies=None, verbose=True, config=None, strict_version_check=False, **kw):
+    """Attach to a running server (``url`` or ``ip``/``port``) over HTTP: ``h2o.api``, ``h2o.ls``,
+    ``h2o.remove``, ``h2o.cluster()`` then talk to it. Without an address this is ``h2o.init()``."""
+    from . import _conn
+    if config:
+        url = url or config.get("url")
+        ip, port = ip or config.get("ip"), port or config.get("port")
+    if server is not None and url is None:
+        url = getattr(server, "url", None) or str(server)
+    if url is None and ip is None and port is None:
+        init(verbose=verbose)
+        return _conn.set_current(_conn.InProcessConnection())
+    if url is None:
+        url = f"{'https' if https else 'http'}://{ip or '127.0.0.1'}:{port or 54321}"
+    c = _conn.set_current(_conn.RemoteConnection(url, verify_ssl_certificates=verify_ssl_certificates is not False,
+                                                 auth=auth))
+    if verbose:
+        cl = c.cloud
+        print(f"Connected to {url}: cloud '{cl.get('cloud_name')}' size {cl.get('cloud_size')} version {cl.get('version')}")
+    return c
 
 
 def cluster():
@@ -177,6 +202,12 @@ def as_list(data, use_pandas=True, header=True):
 
 # ---- DKV
 def get_frame(frame_id, **kw):
+    from . import _conn
+    if _conn.is_remote():            # a local copy of the server's frame (CSV download)
+        import io as _io
+        raw = _conn.current().request("GET /3/DownloadDataset", data={"frame_id": frame_id})
+        import pandas as _pd
+        return H2OFrame(_pd.read_csv(_io.BytesIO(raw if isinstance(raw, bytes) else str(raw).encode())))
     v = _dkv.get(frame_id)
     return v if isinstance(v, H2OFrame) else None
 
@@ -197,6 +228,12 @@ def get_job(job_id):
 
 def ls():
     import pandas as pd
+    from . import _conn
+    if _conn.is_remote():
+        c = _conn.current()
+        keys = [f["frame_id"]["name"] for f in c.request("GET /3/Frames").get("frames", [])]
+        keys += [m["model_id"]["name"] for m in c.request("GET /3/Models").get("models", [])]
+        return pd.DataFrame({"key": keys})
     return pd.DataFrame({"key": _dkv.keys()})
 
 
@@ -205,10 +242,15 @@ def frames():
 
 
 def remove(x, cascade=True):
+    from . import _conn
     xs = x if isinstance(x, (list, tuple)) else [x]
     for o in xs:
         key = o if isinstance(o, str) else getattr(o, "frame_id", None) or getattr(o, "model_id", None) or getattr(o, "key", None)
-        if key is not None and _dkv.contains(key):
+        if key is None:
+            continue
+        if _conn.is_remote():
+            _conn.current().request(f"DELETE /3/DKV/{key}")
+        elif _dkv.contains(key):
             _dkv.remove(key)
 
 

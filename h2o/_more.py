@@ -14,20 +14,11 @@ _STATE = dict(timezone="UTC", expr_optimizations=True)
 
 
 def api(endpoint, data=None, json=None, filename=None, save_to=None):   # noqa: A002 - h2o-py signature
-    """``h2o.api("GET /3/Cloud")``: served in-process by the REST application (``api/server.py``)."""
-    from fastapi.testclient import TestClient
-    from llama_github_io_amd.api.server import create_app
-    method, _, path = endpoint.partition(" ")
-    client = TestClient(create_app())
-    r = client.request(method.upper(), path, params=data if method.upper() == "GET" else None,
-                       data=None if method.upper() == "GET" else data, json=json)
-    r.raise_for_status()
-    if save_to:
-        with open(save_to, "wb") as f:
-            f.write(r.content)
-        return save_to
-    ctype = r.headers.get("content-type", "")
-    return r.json() if "json" in ctype else r.content
+    """``h2o.api("GET /3/Cloud")``: sent to the connected server (``h2o.connect(url=...)``) over HTTP,
+    or served in-process by this process's REST application (one cached client)."""
+    from . import _conn
+    c = _conn.current() or _conn.in_process()
+    return c.request(endpoint, data=data, json=json, filename=filename, save_to=save_to)
 
 
 def cluster_info():
@@ -38,8 +29,8 @@ def cluster_info():
 
 
 def connection():
-    import h2o
-    return h2o.cluster()
+    from . import _conn
+    return _conn.current() or _conn.in_process()
 
 
 def version_check():

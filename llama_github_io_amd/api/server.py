@@ -817,6 +817,9 @@ def create_app():
                 "leaderboard_table": table, "event_log": {"events": aml.event_log}, "event_log_table": ev,
                 "modeling_steps": [], "leader": v3.model_key(rows[0]["model_id"]) if rows else None}
 
+    from .routes_more import register as _register_more
+    _register_more(app, _params, _unquote, _model_json)
+
     @app.get("/99/Leaderboards/{pid}")
     def leaderboard_get(pid: str):
         aml = dkv.get(pid)

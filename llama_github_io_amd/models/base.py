@@ -274,15 +274,23 @@ class Model:
     def partial_plot(self, data, cols=None, nbins=20, plot=False, targets=None, include_na=False, user_splits=None,
                      **kw):
         from .. import explain
-        return explain.partial_plot(self, data, cols, nbins, targets, include_na, user_splits)
+        return explain.partial_plot(self, data, cols, nbins, targets, include_na, user_splits,
+                                    weight_column=kw.get("weight_column"), row_index=kw.get("row_index", -1),
+                                    col_pairs_2dpdp=kw.get("col_pairs_2dpdp"))
 
     def h(self, frame, variables):
         from .. import explain
         return explain.h(self, frame, variables)
 
     def feature_interaction(self, max_interaction_depth=100, max_tree_depth=100, max_deepening=-1):
+        """List of tables as in h2o-py: one per interaction depth, the leaf statistics, then one split-value
+        histogram per single feature (pandas DataFrames)."""
+        import pandas as pd
         from .. import explain
-        return explain.feature_interaction(self, max_interaction_depth, max_tree_depth, max_deepening)
+        r = explain.feature_interaction(self, max_interaction_depth, max_tree_depth, max_deepening)
+        out = [pd.DataFrame(t) for t in r["tables"]] + [pd.DataFrame(r["leaf_statistics"])]
+        out += [pd.DataFrame({"Split Value": list(h), "Count": list(h.values())}) for h in r["split_value_histograms"].values()]
+        return out
 
     def fairness_metrics(self, frame, protected_columns, reference=None, favorable_class=None):
         """Per protected-group metrics + adverse impact ratios (h2o-py ``model.fairness_metrics``)."""

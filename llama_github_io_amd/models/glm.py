@@ -410,7 +410,8 @@ class GLMTrainer:
         model.output["lambda"] = [e["lambda"] for e in path]
         model.output["regularization_path"] = dict(lambdas=[e["lambda"] for e in path], alphas=[alpha] * len(path),
                                                    explained_deviance_train=[e.get("dev_explained") for e in path],
-                                                   coefficients=[e.get("coefs") for e in path],
+                                                   coefficients=[self._path_raw(ex, e.get("coefs")) for e in path],
+                                                   coefficients_std=[e.get("coefs") for e in path],
                                                    coefficient_names=ex.names + ["Intercept"])
         self._outputs(model, fam, link, Zi, y, w, off, ex, nobs, X, offset)
         if getattr(self, "collinear", None) is not None:
@@ -536,6 +537,27 @@ class GLMTrainer:
         return beta, path, lambdas[-1]
 
     # ---- coefficient helpers (raw <-> standardized scale, beta_constraints, collinearity)
+    @staticmethod
+    def _std_to_raw(ex, b):
+        """Inverse of :meth:`_raw_to_std` (intercept last)."""
+        raw = b.clone()
+        if ex.standardize and ex.nums:
+            k = ex.num_off
+            sd = ex.num_sd.to(b.device).double()
+            mu = ex.num_mean.to(b.device).double()
+            raw[k:-1] = b[k:-1] / sd
+            raw[-1] = b[-1] - float((raw[k:-1] * mu).sum())
+        return raw
+
+    def _path_raw(self, ex, coefs):
+        """Regularization-path coefficients on the raw scale (one list, or one per class)."""
+        if coefs is None:
+            return None
+        b = torch.as_tensor(coefs, dtype=torch.float64)
+        if b.dim() == 1:
+            return self._std_to_raw(ex, b).tolist()
+        return [self._std_to_raw(ex, r).tolist() for r in b]
+
     @staticmethod
     def _raw_to_std(ex, raw):
         """Raw-scale coefficients (intercept last) -> the standardized space the solver works in."""

@@ -67,12 +67,12 @@ class TargetEncoderModel(Model):
             dev = self.device
             nz = float(self.params.get("noise", 0.0)) if noise is None else float(noise)
             gen = torch.Generator().manual_seed(int(self.params.get("seed") or 0) & 0x7FFFFFFF)
-            leak = str(self.params.get("data_leakage_handling", "none")).lower()
+            leak = str(self.params.get("data_leakage_handling", "none")).lower().replace("_", "")
             y = None
-            if as_training and leak == "leave_one_out":
+            if as_training and leak == "leaveoneout":
                 y = self._targets(frame, dev)
             fold = None
-            if as_training and leak == "k_fold":
+            if as_training and leak == "kfold":
                 fold = frame._col(self.params["fold_column"]).as_float().to(dev).long()
             cols = [frame._col(n) for n in frame.names if self.params.get("keep_original_categorical_columns", True)
                     or n not in self.output["encoded_columns"]]
@@ -158,7 +158,7 @@ class TargetEncoderTrainer:
         wt = ok.double()
         prior = (Y * wt[:, None]).sum(0) / wt.sum()
         fold = None
-        if str(p["data_leakage_handling"]).lower() == "k_fold":
+        if str(p["data_leakage_handling"]).lower().replace("_", "") == "kfold":
             if not p.get("fold_column") or p["fold_column"] not in info.x:
                 raise ValueError("k_fold leakage handling needs fold_column")
             fold = torch.nan_to_num(X[info.x.index(p["fold_column"])]).long()

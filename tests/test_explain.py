@@ -46,4 +46,10 @@ def test_pdp_and_h(fr):
     hab = m.h(fr, ["a", "b"])
     assert 0 < hab <= 1.5                        # a*b interaction is real
     fi = m.feature_interaction()
-    assert fi and "interaction" in fi[0]
+    assert len(fi) >= 3 and list(fi[0].columns)[:3] == ["Interaction", "Gain", "FScore"]
+    assert set(fi[0]["Interaction"]) <= {"a", "b", "c"} and (fi[1]["Interaction"].str.count("[|]") == 1).all()
+    assert sorted(fi[0]["Gain Rank"]) == list(range(1, len(fi[0]) + 1))
+    p2 = m.partial_plot(fr, [], nbins=4, col_pairs_2dpdp=[["a", "b"]])["a|b"]
+    assert len(p2) == 16 and {"value", "value2", "mean_response"} <= set(p2[0])
+    ice = m.partial_plot(fr, ["a"], nbins=5, row_index=3)["a"]
+    assert len(ice) == 5 and all(r["stddev_response"] == 0 for r in ice)
