@@ -10,6 +10,13 @@ import torch
 from .base import DataInfo, Model, make_key
 
 
+_ALGO_BY_NAME = {"Generalized Linear Modeling": "glm", "Gradient Boosting Machine": "gbm",
+                 "Distributed Random Forest": "drf", "K-means": "kmeans", "Deep Learning": "deeplearning",
+                 "Isolation Forest": "isolationforest", "Word2Vec": "word2vec", "XGBoost": "xgboost",
+                 "Principal Components Analysis": "pca", "Generalized Low Rank Modeling": "glrm",
+                 "Stacked Ensemble": "stackedensemble", "Support Vector Machine (*Spark*)": "svm"}
+
+
 class GenericModel(Model):
     algo = "generic"
 
@@ -35,12 +42,15 @@ class GenericModel(Model):
         xs = cols[:nfeat]
         doms = [mj["domains"].get(i) for i in range(nfeat)]
         iscat = np.array([1 if d is not None else 0 for d in doms], dtype=np.int32)
-        resp = cols[nfeat] if sup and len(cols) > nfeat else None
-        rdom = mj["domains"].get(nfeat) if resp else None
+        # the response is the LAST column (weights / offset / fold columns may sit in between)
+        resp = cols[-1] if sup and len(cols) > nfeat else None
+        rdom = mj["domains"].get(len(cols) - 1) if resp else None
         info = DataInfo(xs, iscat, doms, resp, rdom)
         m = GenericModel(model_id or make_key("generic"), dict(path=path), info)
         m.mojo_info = ki
         m.inner = None
+        if "algo" not in ki:          # MOJO 1.0 files name the algorithm only in full
+            ki["algo"] = _ALGO_BY_NAME.get(ki.get("algorithm", ""), str(ki.get("algorithm", "")).lower())
         algo = ki["algo"]
         m.output["original_algo"] = algo
         cat = ki.get("category", "Regression")
@@ -82,6 +92,13 @@ class GenericModel(Model):
                 m.means = _floats(ki["standardize_means"])
                 m.mults = _floats(ki["standardize_mults"])
                 m.modes = [int(v) for v in _floats(ki["standardize_modes"])]
+        elif algo == "glrm":
+            m.glrm = A.load_glrm(ki, mj["files"])
+            m.output["model_category"] = "DimReduction"
+        elif algo == "svm":
+            m.svm = dict(weights=_floats(ki["weights"]), intercept=float(ki["interceptor"]),
+                         means=_floats(ki.get("means", "[]")), mean_imputation=ki.get("meanImputation") == "true",
+                         threshold=float(ki.get("threshold", 0.0)), default_threshold=float(ki.get("defaultThreshold", 0.0)))
         elif algo == "deeplearning":
             m.dl = A.load_deeplearning(ki)
         elif algo == "pca":
@@ -116,10 +133,13 @@ class GenericModel(Model):
             for i in range(int(ki.get("submodel_count", 0))):
                 key = ki[f"submodel_key_{i}"]
                 subs[key] = GenericModel.from_mojo(path, key, prefix + ki[f"submodel_dir_{i}"])
-            m.base = [subs[ki[f"base_model{i}"]] for i in range(int(ki["base_models_num"]))
-                      if f"base_model{i}" in ki]
+            # a base model the metalearner dropped (zero coefficient) is absent from the zip: keep its
+            # slot so the level-one columns line up with the metalearner's inputs (StackedEnsembleMojoModel)
+            m.base = [subs.get(ki.get(f"base_model{i}")) for i in range(int(ki["base_models_num"]))]
             m.meta = subs[ki["metalearner"]]
             m.meta_transform = ki.get("metalearner_transform", "NONE")
+            if m.info.response_domain is None and m.meta.info.response_domain is not None:
+                m.info.response_domain = list(m.meta.info.response_domain)   # out-of-range domain entry
         else:
             raise NotImplementedError(f"MOJO algo {algo} not supported by this reader")
         return m
@@ -170,6 +190,8 @@ class GenericModel(Model):
             return ["anomaly_score", "mean_length"]
         if self.output.get("original_algo") == "coxph":
             return ["lp"]
+        if self.output.get("original_algo") == "glrm":
+            return [f"Arch{i + 1}" for i in range(self.glrm["ncolX"])]
         if self.output.get("original_algo") == "pca":
             return [f"PC{i + 1}" for i in range(self.pca["k"])]
         return None
@@ -200,6 +222,58 @@ class GenericModel(Model):
             Z[:, off + i] = torch.where(torch.isnan(v), torch.full_like(v, mu[i] if i < len(mu) else 0.0), v)
         return Z, off
 
+    def _xgb_matrix(self, X):
+        """XGBoost MOJO input (h2o XGBoost DataInfo): each categorical one-hot over its levels plus a
+        trailing NA slot at ``cat_offsets``, then the numerics. With ``sparse`` the DMatrix was sparse:
+        absent entries (non-hot levels, numeric zeros) are *missing*, not 0."""
+        ki = self.mojo_info
+        if "cat_offsets" not in ki:
+            return X
+        from ..mojo.reader import _floats
+        off = [int(v) for v in _floats(ki["cat_offsets"])]
+        ncat, nnum = int(ki.get("cats", 0)), int(ki.get("nums", 0))
+        sparse = ki.get("sparse") == "true"
+        N = X.shape[1]
+        P = off[-1] + nnum
+        fill = float("nan") if sparse else 0.0
+        D = torch.full((P, N), fill, dtype=torch.float32, device=X.device)
+        ar = torch.arange(N, device=X.device)
+        for c in range(ncat):
+            v = X[c]
+            L = off[c + 1] - off[c] - 1
+            idx = torch.where(torch.isnan(v), torch.full_like(v, float(L)), v).long().clamp(0, L)
+            D[off[c] + idx, ar] = 1.0
+        nums = X[ncat:ncat + nnum].float()
+        if sparse:
+            nums = torch.where(nums == 0, torch.full_like(nums, float("nan")), nums)
+        D[off[-1]:] = nums
+        return D
+
+    def kmeans_distances(self, X):
+        """KMeansMojoModel.score0: Kmeans_preprocessData (NA -> mean / mode, standardise numerics) then
+        KMeans_distance per center: squared difference for numerics, 0/1 mismatch for categoricals,
+        scaled up by n / (non-NA count)."""
+        info = self.info
+        Xd = X.double().T.clone()                                   # [N, F]
+        F = Xd.shape[1]
+        iscat = torch.tensor([bool(info.iscat[j]) for j in range(F)], device=Xd.device)
+        if self.std:
+            mu = torch.tensor(self.means, dtype=torch.float64, device=Xd.device)
+            mul = torch.tensor(self.mults, dtype=torch.float64, device=Xd.device)
+            mode = torch.tensor([float(v) for v in self.modes], dtype=torch.float64, device=Xd.device)
+            fill = torch.where(iscat, mode, mu)
+            Xd = torch.where(torch.isnan(Xd), fill.expand_as(Xd), Xd)
+            Xd = torch.where(iscat, Xd, (Xd - torch.nan_to_num(mu)) * mul)
+        C = self.centers.to(Xd.device)                              # [K, F]
+        valid = ~torch.isnan(Xd)
+        diff = Xd[:, None, :] - C[None]
+        term = torch.where(iscat, (diff != 0).double(), diff * diff)
+        term = torch.where(valid[:, None, :], term, torch.zeros_like(term))
+        D = term.sum(-1)
+        pts = valid.sum(1, keepdim=True).double()
+        scale = torch.where((pts > 0) & (pts < F), F / pts.clamp(min=1), torch.ones_like(pts))
+        return D * scale
+
     def _predict_tensor(self, X, offset=None):
         if self.inner is not None:
             return self.inner._predict_tensor(X, offset)
@@ -212,6 +286,8 @@ class GenericModel(Model):
                 f = f + offset[:, None]
             d = ki.get("distribution", "gaussian")
             if d == "multinomial":
+                if f.shape[1] == 1 and cat == "Binomial":      # 1-tree binomial optimisation: [f, -f]
+                    f = torch.cat([f, -f], 1)
                 return torch.softmax(f, 1)
             if d in ("bernoulli", "quasibinomial", "modified_huber"):
                 p1 = torch.sigmoid(f[:, 0])
@@ -220,7 +296,7 @@ class GenericModel(Model):
                 return torch.exp(f[:, 0])
             return f[:, 0]
         if algo == "xgboost":
-            f = self.forest.predict_raw(X) + self.xgb_base
+            f = self.forest.predict_raw(self._xgb_matrix(X)) + self.xgb_base
             if offset is not None:
                 f = f + offset[:, None]
             obj = self.xgb_obj
@@ -274,7 +350,11 @@ class GenericModel(Model):
             return A.score_coxph(self.cox, X)
         if algo == "stackedensemble":
             cols = []
+            K = len(self.info.response_domain or []) if cat == "Multinomial" else 1
             for b in self.base:
+                if b is None:
+                    cols.append(torch.zeros(X.shape[1], K, dtype=torch.float64, device=X.device))
+                    continue
                 P = b._predict_tensor(b._align(X, self.info), offset)
                 if cat == "Binomial":
                     p1 = P[:, 1:2].double()
@@ -288,13 +368,26 @@ class GenericModel(Model):
             L1 = torch.cat(cols, 1).T.contiguous().float()
             return self.meta._predict_tensor(L1, None)
         if algo == "kmeans":
-            Z, off = self._design(X)
-            if self.std:
-                mu = torch.tensor(self.means, dtype=torch.float64, device=Z.device)
-                mul = torch.tensor(self.mults, dtype=torch.float64, device=Z.device)
-                Z[:, off:] = (Z[:, off:] - mu) * mul
-            D = ((Z[:, None, :] - self.centers.to(Z.device)[None]) ** 2).sum(-1)
-            return D.argmin(1).float()
+            return self.kmeans_distances(X).argmin(1).float()
+        if algo == "glrm":
+            from ..mojo import algos as A
+            return A.score_glrm(self.glrm, X)
+        if algo == "svm":
+            sv = self.svm
+            Xd = X.double().T
+            w = torch.tensor(sv["weights"], dtype=torch.float64, device=Xd.device)
+            if sv["mean_imputation"] and sv["means"]:
+                mu = torch.tensor(sv["means"][:Xd.shape[1]], dtype=torch.float64, device=Xd.device)
+                Xd = torch.where(torch.isnan(Xd), mu.expand_as(Xd), Xd)
+            pred = Xd @ w + sv["intercept"]
+            if cat != "Binomial":
+                return pred.float()
+            thr, dthr = sv["threshold"], sv["default_threshold"]
+            # SvmMojoModel.score0: preds = [label, p0, p1] built from the margin
+            p1 = torch.where(pred > thr, torch.clamp(pred, min=dthr), torch.where(pred >= dthr, torch.full_like(pred, dthr - 1), pred))
+            p0 = torch.where(pred > thr, p1 - 1, p1 + 1)
+            self._svm_label = (pred > thr)
+            return torch.stack([p0, p1], 1).float()
         raise NotImplementedError(algo)
 
 

@@ -18,7 +18,7 @@ import torch
 
 from .. import metrics as mm
 from ..ops import tree as T
-from ..ops.binning import Binning, apply_binning, fit_binning
+from ..ops.binning import Binning, apply_binning, fit_binning, sample_rows
 from ..ops.forest import Forest, Tree, levels_to_tree
 from ..parallel import collectives as coll
 from .base import DataInfo, Model, ScoreKeeper, make_key, model_category, variable_importance
@@ -162,17 +162,10 @@ class SharedTreeTrainer:
             # sample is drawn on GLOBAL row indices (fit_binning's own rule), each rank contributes the
             # sampled rows it owns, and the edges come from the gathered sample
             n_glob = coll.exclusive_offset(N)[1]
-            sample = 1 << 20
-            if n_glob > sample:
-                g = torch.Generator(device="cpu").manual_seed(int(self.seed) & 0x7FFFFFFF)
-                gidx = torch.randperm(n_glob, generator=g)[:sample]
-                mine = gidx[(gidx >= self.row0) & (gidx < self.row0 + N)] - self.row0
-                Xl = X.index_select(1, mine.to(dev))
-            else:
-                Xl = X
+            Xl = sample_rows(X, 1 << 20, self.seed, self.row0, n_glob)
             Xs = coll.all_gather_cat(Xl.contiguous(), dim=1)
             self.binning = fit_binning(Xs, info.iscat, info.nlevels, max_bins=max_bins, seed=self.seed,
-                                       sample=Xs.shape[1] + 1, max_cat_bins=int(p.get("nbins_cats") or 1024))
+                                       max_cat_bins=int(p.get("nbins_cats") or 1024), presampled=True)
         else:
             self.binning = fit_binning(X, info.iscat, info.nlevels, max_bins=max_bins, seed=self.seed,
                                        max_cat_bins=int(p.get("nbins_cats") or 1024))

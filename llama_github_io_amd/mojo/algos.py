@@ -361,8 +361,10 @@ def load_eif(ki, files):
         (F,) = struct.unpack_from("<i", b, 0)
         pos = 4
         nodes = {}
-        while pos < len(b):
+        while pos + 5 <= len(b):
             h, typ = struct.unpack_from("<ib", b, pos)
+            if typ not in (ord("N"), ord("L")):
+                break                      # zero padding after the last node (fixed-size byte blocks)
             pos += 5
             if typ == ord("N"):
                 n = np.frombuffer(b, "<f8", F, pos); p = np.frombuffer(b, "<f8", F, pos + 8 * F)
@@ -593,3 +595,73 @@ def load_targetencoder(ki, files, info):
         m.stats[name] = dict(num=num, den=den, prior=prior, domain=dom)
     m.output["encoded_columns"] = list(maps)
     return m
+
+
+# ------------------------------------------------------------------------------------------------ GLRM
+def load_glrm(ki, files):
+    """GlrmMojoReader layout: ``archetypes`` (nrowY x ncolY big-endian doubles, Y over the expanded
+    columns: categorical one-hot blocks at ``catOffsets``, then numerics), ``losses`` (one per
+    permuted column), ``cols_permutation`` (cats first), ``num_levels_per_category``,
+    ``norm_sub`` / ``norm_mul`` (numeric standardisation)."""
+    nrow, ncol = int(ki["nrowY"]), int(ki["ncolY"])
+    Y = np.frombuffer(files["archetypes"], ">f8", nrow * ncol).reshape(nrow, ncol).astype(np.float64)
+    losses = [ln.strip() for ln in files["losses"].decode().splitlines() if ln.strip()]
+    ints = lambda k: [int(float(v)) for v in _floats(ki[k])] if ki.get(k) not in (None, "null") else None  # noqa: E731
+    return dict(Y=torch.from_numpy(Y.copy()), losses=losses, perm=ints("cols_permutation"),
+                nlev=ints("num_levels_per_category"), cat_off=ints("catOffsets"), ncats=int(ki["num_categories"]),
+                nnums=int(ki["num_numeric"]), norm_sub=_floats(ki.get("norm_sub", "[]")),
+                norm_mul=_floats(ki.get("norm_mul", "[]")), ncolX=int(ki["ncolX"]),
+                gammax=float(ki.get("gammaX", 0.0)), regx=ki.get("regularizationX", "None"))
+
+
+def glrm_row_data(st, X):
+    """GlrmMojoModel.getRowData: permuted columns, unseen categorical levels -> NaN. X: [F, N]."""
+    A = X.T.double()[:, st["perm"]].clone()
+    for i in range(st["ncats"]):
+        A[:, i] = torch.where(A[:, i] >= st["nlev"][i], torch.full_like(A[:, i], float("nan")), A[:, i])
+    return A
+
+
+def score_glrm(st, X, iters=200):
+    """X factors of each row for the fixed archetypes: minimise the per-column GLRM losses (one-vs-all
+    hinge for categoricals, quadratic for numerics, NAs skipped) + gammaX * regularizer by projected
+    gradient from x = 0 (the reference starts from a seeded Gaussian; the optimum is what we return)."""
+    from ..models.glrm import _prox
+    A = glrm_row_data(st, X)
+    N = A.shape[0]
+    Y = st["Y"].to(A.device)
+    k = Y.shape[0]
+    nc, off = st["ncats"], st["cat_off"] or [0]
+    sub = torch.tensor(st["norm_sub"] or [0.0] * st["nnums"], dtype=torch.float64, device=A.device)
+    mul = torch.tensor(st["norm_mul"] or [1.0] * st["nnums"], dtype=torch.float64, device=A.device)
+    nums = (A[:, nc:] - sub) * mul
+    ncat_cols = off[-1] if nc else 0
+    x = torch.zeros(N, k, dtype=torch.float64, device=A.device, requires_grad=True)
+    opt = torch.optim.LBFGS([x], lr=1.0, max_iter=iters, line_search_fn="strong_wolfe")
+
+    def obj():
+        opt.zero_grad()
+        U = x @ Y
+        L = x.new_zeros(())
+        for i in range(nc):
+            u = U[:, off[i]:off[i + 1]]
+            a = A[:, i]
+            ok = ~torch.isnan(a)
+            if ok.any():
+                ai = a[ok].long()
+                uu = u[ok]
+                hinge = torch.clamp(1 + uu, min=0).sum(1)
+                ua = uu.gather(1, ai[:, None])[:, 0]
+                L = L + (hinge + torch.clamp(1 - ua, min=0) - torch.clamp(1 + ua, min=0)).sum()
+        un = U[:, ncat_cols:ncat_cols + st["nnums"]]
+        okn = ~torch.isnan(nums)
+        L = L + torch.where(okn, (un - torch.nan_to_num(nums)) ** 2, torch.zeros_like(un)).sum()
+        if st["gammax"] > 0 and str(st["regx"]).lower() == "quadratic":
+            L = L + st["gammax"] * (x * x).sum()
+        L.backward()
+        return L
+    opt.step(obj)
+    xd = x.detach()
+    if str(st["regx"]).lower() not in ("none", "quadratic"):
+        xd = _prox(st["regx"], xd, 0.0, 1)
+    return xd.float()

@@ -40,29 +40,49 @@ class Binning:
                        [None if m is None else np.asarray(m, dtype=np.int64) for m in s["level_to_bin"]])
 
 
+def sample_rows(X: torch.Tensor, sample: int, seed: int, row0: int = 0, n_glob: int | None = None) -> torch.Tensor:
+    """Bernoulli row sample for the quantile edges, decided per GLOBAL row index (counter-based hash,
+    ``collectives.row_uniform``): identical on one process and on any row sharding, drawn on the
+    device (no host permutation of N indices). Keeps ~``sample`` rows of ``n_glob``."""
+    from ..parallel import collectives as coll
+    F, N = X.shape
+    n_glob = N if n_glob is None else int(n_glob)
+    if n_glob <= sample:
+        return X
+    u = coll.row_uniform(int(seed), 0xB1A5, row0, N, X.device)
+    return X[:, u < (sample / n_glob)]
+
+
 def fit_binning(X: torch.Tensor, iscat, nlevels=None, max_bins: int = MAX_DATA_BINS, sample: int = 1 << 20,
-                seed: int = 0, weights: torch.Tensor | None = None, max_cat_bins: int = NA_BIN) -> Binning:
+                seed: int = 0, weights: torch.Tensor | None = None, max_cat_bins: int = NA_BIN,
+                presampled: bool = False) -> Binning:
     """X: float32 [F, N] (column-major; NaN = missing; categorical columns hold level codes).
+    Numeric edges are QuantilesGlobal cut points of a ~``sample``-row sample (all distinct values
+    when there are at most ``max_bins``), computed on X's device: one batched sort of the sample,
+    then per-feature distinct / quantile gathers; only the <=255 edges per feature reach the host.
     ``max_cat_bins`` (nbins_cats, capped at 255): categoricals with more levels keep their most
-    frequent ``max_cat_bins - 1`` levels as bins and fold the rest into one shared bin."""
+    frequent ``max_cat_bins - 1`` levels as bins and fold the rest into one shared bin.
+    ``presampled``: X already is the (gathered) sample."""
     cat_cap = int(min(max(2, max_cat_bins), NA_BIN))
     F, N = X.shape
     max_bins = int(min(max(2, max_bins), MAX_DATA_BINS))
     iscat = np.asarray(iscat, dtype=np.int32)
     nlevels = np.zeros(F, dtype=np.int32) if nlevels is None else np.asarray(nlevels, dtype=np.int32)
-    g = torch.Generator(device="cpu").manual_seed(int(seed) & 0x7FFFFFFF)
-    if N > sample:
-        idx = torch.randperm(N, generator=g)[:sample].to(X.device)
-        Xs = X.index_select(1, idx)
-    else:
-        Xs = X
+    Xs = X if presampled else sample_rows(X, sample, seed)
     edges, nbins, l2b = [], np.zeros(F, dtype=np.int32), []
     num_cols = [f for f in range(F) if not iscat[f]]
     if num_cols:
         Xn = Xs[num_cols].float()
         Xn = torch.where(torch.isnan(Xn), torch.full_like(Xn, float("inf")), Xn)
         srt, _ = torch.sort(Xn, dim=1)
-        srt = srt.cpu().numpy()
+        nfin = torch.isfinite(srt).sum(1).cpu().numpy()
+        M = srt.shape[1]
+        # distinct-value counts of every feature in one pass (sorted rows: count value changes)
+        if M > 1:
+            chg = (srt[:, 1:] != srt[:, :-1]) & torch.isfinite(srt[:, 1:])
+            ndist = (chg.sum(1) + torch.isfinite(srt[:, 0]).long()).cpu().numpy()
+        else:
+            ndist = nfin.copy()
     for f in range(F):
         if iscat[f]:
             nl = int(nlevels[f]) if nlevels[f] > 0 else int(torch.nan_to_num(X[f], nan=-1).max().item()) + 1
@@ -71,7 +91,7 @@ def fit_binning(X: torch.Tensor, iscat, nlevels=None, max_bins: int = MAX_DATA_B
                 l2b.append(None)
                 nbins[f] = max(nl, 1)
             else:  # fold rare levels into the last bin
-                codes = X[f][~torch.isnan(X[f])].long()
+                codes = Xs[f][~torch.isnan(Xs[f])].long()      # frequencies of the (global) sample
                 cnt = torch.bincount(codes, minlength=nl).cpu().numpy()
                 order = np.argsort(-cnt, kind="stable")
                 m = np.full(nl, cat_cap - 1, dtype=np.int64)
@@ -80,19 +100,20 @@ def fit_binning(X: torch.Tensor, iscat, nlevels=None, max_bins: int = MAX_DATA_B
                 nbins[f] = cat_cap
             edges.append(None)
             continue
-        row = srt[num_cols.index(f)]
-        row = row[np.isfinite(row)]
+        k = num_cols.index(f)
+        n = int(nfin[k])
         l2b.append(None)
-        if row.size == 0:
+        if n == 0:
             edges.append(np.zeros(0, dtype=np.float32)); nbins[f] = 1
             continue
-        u = np.unique(row)
-        if u.size <= max_bins:
-            e = u[1:].astype(np.float32)
+        row = srt[k, :n]
+        if int(ndist[k]) <= max_bins:
+            e = torch.unique_consecutive(row)[1:]
         else:
-            q = (np.arange(1, max_bins) * row.size) // max_bins
-            e = np.unique(row[q]).astype(np.float32)
+            q = (torch.arange(1, max_bins, device=row.device, dtype=torch.int64) * n) // max_bins
+            e = torch.unique_consecutive(row[q])
             e = e[e > row[0]]  # first bin must be non-empty
+        e = e.float().cpu().numpy()
         edges.append(e)
         nbins[f] = e.size + 1
     # rows of more than 12 features are padded to 16 B multiples so the partition kernel moves them
