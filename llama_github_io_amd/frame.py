@@ -1347,4 +1347,9 @@ def _remap_codes(c: Column, domain, device) -> torch.Tensor:
 
 
 # distribution class of every H2OFrame method (row-local / collective / gathered): parallel/dframe.py
+from . import frame_more as _frame_more  # noqa: E402
+
+_frame_more.install(H2OFrame)
+dframe.LOCAL.update({"acos", "acosh", "asin", "asinh", "atan", "atanh", "cosh", "sinh", "cospi", "sinpi", "tanpi",
+                     "gamma", "lgamma", "digamma", "trigamma", "logical_negation"})
 dframe.install(H2OFrame)

@@ -626,6 +626,10 @@ def _getrow(fr):
     return [float(v) for v in fr.as_tensor(dtype=torch.float64)[0].tolist()]
 
 
+def _minus1(v):
+    return v - 1 if isinstance(v, H2OFrame) else float(v) - 1
+
+
 def _mktime(yr, mo, dy, hr, mi, se, ms):
     import pandas as pd
     parts = [yr, mo, dy, hr, mi, se, ms]
@@ -657,7 +661,9 @@ def _extended_prims(sess):
         "digamma": _elementwise(torch.digamma), "trigamma": _elementwise(lambda v: torch.polygamma(1, v)),
         "round": lambda a, d=0: fr(a).round(int(d)) if isinstance(a, H2OFrame) else float(round(a, int(d))),
         "signif": lambda a, d=6: fr(a).signif(int(d)),
-        "none": lambda a: a, "moment": lambda a, k=2, *r: _moment(fr(a), int(k)),
+        "none": lambda a: a,
+        # AstMoment: a time column from year, month (1-12), day (1-31), hour, minute, second, msec (UTC)
+        "moment": lambda yr, mo, dy, hr, mi, se, ms: _mktime(yr, _minus1(mo), _minus1(dy), hr, mi, se, ms),
         "skewness": lambda a, na_rm=1: _skew(fr(a), na_rm), "kurtosis": lambda a, na_rm=1: _kurt(fr(a), na_rm),
         "h2o.mad": lambda a, combine="interpolate", const=1.4826: _mad(fr(a), combine, float(const)),
         "prod": lambda a: _prod(fr(a)), "prod.na": lambda a: _prod(fr(a), True),
