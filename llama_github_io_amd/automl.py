@@ -1,11 +1,14 @@
 """AutoML (reference: ``h2o-automl/src/main/java/ai/h2o/automl/AutoML.java``, ``ModelingPlans.java``,
 ``Leaderboard.java``, ``modeling/*StepsProvider.java``).
 
-Modeling plan (H2O default order, trimmed by ``include_algos``/``exclude_algos``): XGBoost (3
-presets), GLM, DRF, GBM (5 presets), DeepLearning, XRT, GBM/XGBoost random grids while budget
-remains, then two Stacked Ensembles (best-of-family, all models). Every model gets ``nfolds``
-(default 5, Modulo fold assignment so all share folds) CV with kept holdout predictions. Budgets:
-``max_models``, ``max_runtime_secs`` (default 3600 when neither is set), ``max_runtime_secs_per_model``.
+Modeling plan: the reference default ``ModelingPlans.TEN_LAYERED`` (trimmed by ``include_algos`` /
+``exclude_algos``): priority groups 1..10 of default models (XGBoost def_1..3, GLM, DRF, XRT, GBM
+def_1..5, DeepLearning), random-discrete grids (XGBoost, GBM, DeepLearning 1/2/3 hidden layers),
+exploitation (GBM learning-rate annealing, XGBoost learning-rate search), the completion step (resume
+the two best grids) and Stacked Ensembles closing each group. Every model gets ``nfolds`` (default 5,
+Modulo fold assignment so all share folds) CV with kept holdout predictions; early stopping uses the
+adaptive tolerance of the training frame. Budgets: ``max_models`` (base models), ``max_runtime_secs``
+(default 3600 when neither is set, split over steps by weight), ``max_runtime_secs_per_model``.
 Leaderboard sort: AUC (binomial), mean_per_class_error (multinomial), mean_residual_deviance
 (regression), with the other standard columns.
 """
@@ -25,34 +28,81 @@ _DEFAULT_SORT = {"Binomial": "auc", "Multinomial": "mean_per_class_error", "Regr
 _DESC = {"auc", "aucpr", "r2"}
 
 
-def _plan(seed):
-    s = seed
-    return [
-        ("xgboost", "XGBoost_1", dict(ntrees=100, max_depth=10, min_rows=5, sample_rate=0.6, col_sample_rate=0.8, col_sample_rate_per_tree=0.8, seed=s)),
-        ("xgboost", "XGBoost_2", dict(ntrees=100, max_depth=20, min_rows=10, sample_rate=0.6, col_sample_rate=0.8, col_sample_rate_per_tree=0.8, seed=s)),
-        ("xgboost", "XGBoost_3", dict(ntrees=100, max_depth=5, min_rows=3, sample_rate=0.8, col_sample_rate=0.8, col_sample_rate_per_tree=0.8, seed=s)),
-        ("glm", "GLM_1", dict(lambda_search=True, seed=s)),
-        ("drf", "DRF_1", dict(ntrees=50, seed=s)),
-        ("gbm", "GBM_1", dict(ntrees=100, max_depth=6, min_rows=1, sample_rate=0.8, col_sample_rate=0.8, col_sample_rate_per_tree=0.8, seed=s)),
-        ("gbm", "GBM_2", dict(ntrees=100, max_depth=7, min_rows=10, sample_rate=0.8, col_sample_rate=0.8, col_sample_rate_per_tree=0.8, seed=s)),
-        ("gbm", "GBM_3", dict(ntrees=100, max_depth=8, min_rows=10, sample_rate=0.8, col_sample_rate=0.8, col_sample_rate_per_tree=0.8, seed=s)),
-        ("gbm", "GBM_4", dict(ntrees=100, max_depth=10, min_rows=10, sample_rate=0.8, col_sample_rate=0.8, col_sample_rate_per_tree=0.8, seed=s)),
-        ("gbm", "GBM_5", dict(ntrees=100, max_depth=15, min_rows=100, sample_rate=0.8, col_sample_rate=0.8, col_sample_rate_per_tree=0.8, seed=s)),
-        ("deeplearning", "DeepLearning_1", dict(epochs=10, hidden=[10, 10, 10], seed=s)),
-        ("drf", "XRT_1", dict(ntrees=50, histogram_type="Random", seed=s)),
-    ]
+MODEL_W, GRID_W = 10, 30          # ModelingStep DEFAULT_MODEL_TRAINING_WEIGHT / DEFAULT_GRID_TRAINING_WEIGHT
 
 
-def _random_grid(algo, rng, seed):
+def _plan():
+    """The reference default plan (``ModelingPlans.TEN_LAYERED``): (algo, step id, priority group, weight).
+    Steps run group by group in this definition order; SE steps close each group."""
+    steps = [("xgboost", "def_2", 1, MODEL_W), ("xgboost", "def_1", 2, MODEL_W), ("xgboost", "def_3", 3, MODEL_W),
+             ("xgboost", "grid_1", 4, 3 * GRID_W), ("xgboost", "lr_search", 6, GRID_W),
+             ("glm", "def_1", 1, MODEL_W),
+             ("drf", "def_1", 2, MODEL_W), ("drf", "XRT", 3, MODEL_W),
+             ("gbm", "def_5", 1, MODEL_W), ("gbm", "def_2", 2, MODEL_W), ("gbm", "def_3", 2, MODEL_W),
+             ("gbm", "def_4", 2, MODEL_W), ("gbm", "def_1", 3, MODEL_W), ("gbm", "grid_1", 4, 2 * GRID_W),
+             ("gbm", "lr_annealing", 6, MODEL_W),
+             ("deeplearning", "def_1", 3, MODEL_W), ("deeplearning", "grid_1", 4, GRID_W),
+             ("deeplearning", "grid_2", 5, GRID_W), ("deeplearning", "grid_3", 5, GRID_W),
+             ("completion", "resume_best_grids", 10, 2 * GRID_W)]
+    steps += [("stackedensemble", f"best_of_family_{g}", g, MODEL_W // 2) for g in range(1, 6)]
+    steps += [("stackedensemble", f"all_{g}", g, MODEL_W) for g in range(2, 6)]
+    steps += [("stackedensemble", "best_of_family_gbm", 6, MODEL_W), ("stackedensemble", "all_gbm", 7, MODEL_W),
+              ("stackedensemble", "best_of_family_xglm", 8, MODEL_W), ("stackedensemble", "all_xglm", 8, MODEL_W),
+              ("stackedensemble", "best_of_family", 10, MODEL_W), ("stackedensemble", "best_N", 10, MODEL_W)]
+    order = {id(st): i for i, st in enumerate(steps)}
+    return sorted(steps, key=lambda st: (st[2], order[id(st)]))
+
+
+def _defaults(algo, sid, seed, cat):
+    """Per-step model parameters of the reference steps providers (``modeling/*StepsProvider.java``)."""
+    tree = dict(ntrees=10000, score_tree_interval=5, seed=seed)
+    if algo == "xgboost":
+        base = dict(tree, sample_rate=0.6 if sid != "def_3" else 0.8, col_sample_rate=0.8, col_sample_rate_per_tree=0.8)
+        return dict(base, **{"def_1": dict(max_depth=10, min_rows=5), "def_2": dict(max_depth=15, min_rows=10),
+                             "def_3": dict(max_depth=5, min_rows=3)}[sid])
     if algo == "gbm":
-        return dict(ntrees=int(rng.choice([50, 100, 200])), max_depth=int(rng.choice([3, 5, 7, 9, 11, 13])),
-                    min_rows=float(rng.choice([1, 5, 10, 15, 30, 100])), learn_rate=float(rng.choice([0.01, 0.05, 0.1])),
-                    sample_rate=float(rng.choice([0.5, 0.6, 0.7, 0.8, 0.9, 1.0])),
-                    col_sample_rate=float(rng.choice([0.4, 0.7, 1.0])), seed=seed)
-    return dict(ntrees=int(rng.choice([50, 100, 200])), max_depth=int(rng.choice([5, 10, 15, 20])),
-                min_rows=float(rng.choice([0.01, 0.1, 1, 3, 5, 10])), sample_rate=float(rng.choice([0.6, 0.8, 1.0])),
-                col_sample_rate=float(rng.choice([0.6, 0.8, 1.0])), reg_lambda=float(rng.choice([0.001, 0.01, 0.1, 1, 10])),
-                reg_alpha=float(rng.choice([0.001, 0.01, 0.1, 0.5, 1])), seed=seed)
+        base = dict(tree, sample_rate=0.8, col_sample_rate=0.8, col_sample_rate_per_tree=0.8)
+        return dict(base, **{"def_1": dict(max_depth=6, min_rows=1), "def_2": dict(max_depth=7, min_rows=10),
+                             "def_3": dict(max_depth=8, min_rows=10), "def_4": dict(max_depth=10, min_rows=10),
+                             "def_5": dict(max_depth=15, min_rows=100)}[sid])
+    if algo == "glm":
+        return dict(lambda_search=True, seed=seed, family="binomial" if cat == "Binomial" else
+                    ("multinomial" if cat == "Multinomial" else "gaussian"))
+    if algo == "drf":
+        return dict(ntrees=10000, score_tree_interval=5, seed=seed, **({"histogram_type": "Random"} if sid == "XRT" else {}))
+    if algo == "deeplearning":
+        return dict(hidden=[10, 10, 10], seed=seed)
+    return dict(seed=seed)
+
+
+def _grid_space(algo, sid):
+    """Random-discrete search spaces of the grid steps (GBM/XGBoost/DeepLearning steps providers)."""
+    if algo == "gbm":
+        return dict(max_depth=list(range(3, 18)), min_rows=[1, 5, 10, 15, 30, 100],
+                    sample_rate=[0.5, 0.6, 0.7, 0.8, 0.9, 1.0], col_sample_rate=[0.4, 0.7, 1.0],
+                    col_sample_rate_per_tree=[0.4, 0.7, 1.0], min_split_improvement=[1e-4, 1e-5])
+    if algo == "xgboost":
+        return dict(max_depth=[3, 6, 9, 12, 15], min_rows=[0.01, 0.1, 1.0, 3.0, 5.0, 10.0, 15.0, 20.0],
+                    sample_rate=[0.6, 0.8, 1.0], col_sample_rate=[0.6, 0.8, 1.0],
+                    col_sample_rate_per_tree=[0.7, 0.8, 0.9, 1.0], booster=["gbtree", "dart"],
+                    reg_lambda=[0.001, 0.01, 0.1, 1, 10, 100], reg_alpha=[0.001, 0.01, 0.1, 0.5, 1])
+    layers = {"grid_1": 1, "grid_2": 2, "grid_3": 3}[sid]
+    return dict(hidden=[[u] * layers for u in (20, 50, 100)],
+                hidden_dropout_ratios=[[r] * layers for r in (0.0, 0.1, 0.2, 0.3, 0.4, 0.5)],
+                rho=[0.9, 0.95, 0.99], epsilon=[1e-6, 1e-7, 1e-8, 1e-9], input_dropout_ratio=[0.0, 0.05, 0.1, 0.15, 0.2])
+
+
+def _grid_base(algo, seed):
+    if algo == "gbm":
+        return dict(ntrees=10000, score_tree_interval=5, seed=seed)
+    if algo == "xgboost":
+        return dict(ntrees=10000, score_tree_interval=5, seed=seed)
+    return dict(epochs=10000, adaptive_rate=True, activation="RectifierWithDropout", seed=seed)
+
+
+def default_stopping_tolerance(nrows: int) -> float:
+    """RandomDiscreteValueSearchCriteria.default_stopping_tolerance_for_frame."""
+    return min(0.05, max(0.001, 1.0 / math.sqrt(max(nrows, 1))))
 
 
 class AutoML:
@@ -86,78 +136,218 @@ class AutoML:
 
     def train(self, x=None, y=None, training_frame=None, validation_frame=None, leaderboard_frame=None,
               blending_frame=None, fold_column=None, weights_column=None, job: Job | None = None):
+        """Run the modeling plan group by group. Time budgets follow the steps' weights: a step gets
+        ``remaining_time * weight / remaining_weight`` (ModelingStep weights); ``max_models`` counts
+        base models only (SEs are free). Grid steps draw random-discrete points from their space until
+        their share runs out, exploitation steps retrain the best GBM with learning-rate annealing and
+        search the learning rate of the best XGBoost, the completion step resumes the two best grids,
+        and SE steps (best-of-family / all, per group and for GBM-only and XGBoost+GLM subsets) close
+        each group."""
+        from .parallel import collectives as coll
         t0 = time.time()
+        nrows = training_frame.nrows
+        tol = self.stopping["stopping_tolerance"]
+        tol = default_stopping_tolerance(nrows) if tol in (None, -1, "AUTO") else float(tol)
         common = dict(nfolds=self.nfolds if not fold_column else 0, fold_assignment="Modulo",
                       keep_cross_validation_predictions=True, keep_cross_validation_models=False,
                       fold_column=fold_column, weights_column=weights_column)
         if self.stopping["stopping_rounds"]:
-            common.update(stopping_rounds=self.stopping["stopping_rounds"], stopping_metric=self.stopping["stopping_metric"])
-        from .parallel import collectives as coll
-        # every rank takes rank 0's budget decision (a rank must not start a model the others skip)
-        budget = lambda: coll.agree((self.max_runtime_secs <= 0 or time.time() - t0 < self.max_runtime_secs) and
-                                    (not self.max_models or len(self.models) < self.max_models))  # noqa: E731
-        steps = _plan(self.seed)
+            common.update(stopping_rounds=self.stopping["stopping_rounds"], stopping_metric=self.stopping["stopping_metric"],
+                          stopping_tolerance=tol)
+        self._log(f"stopping tolerance {tol:.6g} (adaptive on {nrows} rows)" if self.stopping["stopping_tolerance"] in
+                  (None, -1, "AUTO") else f"stopping tolerance {tol} (user)")
+        cat = self._category(training_frame, y)
+        steps = [st for st in _plan() if st[0] in ("completion", "stackedensemble") or self._allowed(st[0])]
+        total_w = float(sum(st[3] for st in steps)) or 1.0
+        used_w = 0.0
         rng = np.random.default_rng(self.seed)
-        i = 0
-        while budget():
-            if i < len(steps):
-                algo, name, p = steps[i]
-            else:
-                if not (self._allowed("gbm") or self._allowed("xgboost")):
-                    break
-                algo = "gbm" if (i % 2 == 0 and self._allowed("gbm")) or not self._allowed("xgboost") else "xgboost"
-                name = f"{dict(gbm='GBM', xgboost='XGBoost')[algo]}_grid_1_model_{i - len(steps) + 1}"
-                p = _random_grid(algo, rng, self.seed)
-                if i > len(steps) + 200:
-                    break
-            i += 1
-            if not self._allowed(algo):
-                continue
+        self._grids = {}
+        n_base = lambda: sum(1 for m in self.models if m.algo != "stackedensemble")  # noqa: E731
+
+        def time_left():
+            return self.max_runtime_secs - (time.time() - t0) if self.max_runtime_secs > 0 else float("inf")
+
+        def models_left():
+            return (self.max_models - n_base()) if self.max_models else 1 << 30
+
+        def can_go():
+            return coll.agree(time_left() > 0 and models_left() > 0)
+
+        def run(algo, name, p, share):
+            if algo != "stackedensemble" and not can_go():
+                return None
             p = dict(p, **common)
             if self.per_model:
                 p["max_runtime_secs"] = self.per_model
             elif self.max_runtime_secs > 0:
-                p["max_runtime_secs"] = coll.broadcast_object(max(1.0, self.max_runtime_secs - (time.time() - t0)))
+                p["max_runtime_secs"] = coll.broadcast_object(max(1.0, min(share, time_left())))
             mid = f"{name}_AutoML_{self.project_name}"
             try:
                 m = builder.train(algo, p, x, y, training_frame, validation_frame, job, mid)
                 self.models.append(m)
                 self._log(f"built {mid}")
+                return m
             except Exception as e:  # noqa: BLE001 - AutoML logs and moves on (EventLog)
                 self._log(f"{mid} failed: {e!r}")
-        if self._allowed("stackedensemble") and len(self.models) >= 2 and self.models[0].info.response:
-            self._ensembles(x, y, training_frame, validation_frame, job)
+                return None
+
+        counters = {}
+        last_group = 0
+        for algo, sid, group, w in steps:
+            share = (time_left() * w / max(total_w - used_w, 1e-9)) if self.max_runtime_secs > 0 else float("inf")
+            used_w += w
+            if algo == "stackedensemble":
+                # SEs do not count against the budget: they close every group that trained base models
+                # (and the final group always runs)
+                if (self._allowed("stackedensemble") and len(self.models) >= 2 and self.models[0].info.response
+                        and (group <= last_group or group == 10)):
+                    self._se_step(sid, x, y, training_frame, validation_frame, job)
+                continue
+            if not can_go():
+                continue
+            n_before = len(self.models)
+            fam = dict(gbm="GBM", xgboost="XGBoost", glm="GLM", drf="DRF", deeplearning="DeepLearning").get(algo, algo)
+            if algo == "completion":
+                self._resume_best_grids(run, rng, share)
+                continue
+            if sid.startswith("def_") or sid == "XRT":
+                counters[fam] = counters.get(fam, 0) + 1
+                name = "XRT_1" if sid == "XRT" else f"{fam}_{counters[fam]}"
+                run(algo, name, _defaults(algo, sid, self.seed, cat), share)
+            elif sid.startswith("grid_"):
+                cap = None if not self.max_models else max(1, int(round(models_left() * w / max(total_w - used_w + w, 1e-9))))
+                self._grid_step(algo, fam, sid, run, rng, share, cap)
+            elif sid == "lr_annealing":
+                best = self._best_of(["gbm"])
+                if best is not None:
+                    p = {k: v for k, v in best.params.items() if k in _defaults("gbm", "def_1", self.seed, cat)}
+                    run("gbm", "GBM_lr_annealing_selection_model_1", dict(p, learn_rate_annealing=0.99), share)
+            elif sid == "lr_search":
+                best = self._best_of(["xgboost"])
+                if best is not None:
+                    base = {k: v for k, v in best.params.items() if k in _defaults("xgboost", "def_1", self.seed, cat)}
+                    sti = int(base.get("score_tree_interval") or 5)
+                    for j, lr in enumerate((0.5, 0.2, 0.1, 0.05, 0.02, 0.01, 0.005, 0.002, 0.001, 0.0005)):
+                        if not can_go():
+                            break
+                        run("xgboost", f"XGBoost_lr_search_selection_model_{j + 1}",
+                            dict(base, learn_rate=lr, score_tree_interval=(j + 1) * sti), share / 10)
+            if len(self.models) > n_before:
+                last_group = group
         self.leaderboard_frame = leaderboard_frame
         dkv.put(self.project_name, self)
         return self
 
-    def _ensembles(self, x, y, fr, valid, job):
+    @staticmethod
+    def _category(fr, y):
+        if y is None:
+            return "Regression"
+        if fr.type(y) == "enum":
+            return "Binomial" if len(fr._col(y).domain) == 2 else "Multinomial"
+        return "Regression"
+
+    def _grid_step(self, algo, fam, sid, run, rng, share, cap=None):
+        """Random-discrete grid search (RandomDiscreteValueSearchCriteria) within the step's time share
+        (or, under a model-count budget, its weight share of the remaining models)."""
+        space = _grid_space(algo, sid)
+        g = self._grids.setdefault((algo, sid), dict(n=0, space=space, algo=algo, fam=fam, sid=sid, seen=set()))
+        t_end = time.time() + share
+        tries = 0
+        while time.time() < t_end and tries < 200:
+            tries += 1
+            hp = {k: v[int(rng.integers(len(v)))] for k, v in space.items()}
+            key = repr(sorted(hp.items()))
+            if key in g["seen"]:
+                continue
+            g["seen"].add(key)
+            g["n"] += 1
+            m = run(algo, f"{fam}_{sid}_model_{g['n']}", dict(_grid_base(algo, self.seed), **hp), max(1.0, t_end - time.time()))
+            if m is None and (self.max_models and sum(1 for x in self.models if x.algo != "stackedensemble") >= self.max_models):
+                break
+            if cap is not None and g["n"] >= cap:
+                break
+
+    def _resume_best_grids(self, run, rng, share):
+        """completion step: keep searching the two grids whose best model ranks highest."""
+        if not self._grids:
+            return
+        cat = self.models[0].model_category if self.models else "Regression"
+        metric = self._sort_key(cat)
+
+        def best_of(gk):
+            fam, sid = self._grids[gk]["fam"], self._grids[gk]["sid"]
+            ms = [m for m in self.models if m.key.startswith(f"{fam}_{sid}_model_")]
+            vals = [_metric_of(m, metric) for m in ms]
+            vals = [v for v in vals if not math.isnan(v)]
+            if not vals:
+                return float("nan")
+            return max(vals) if metric in _DESC else min(vals)
+        ranked = sorted(self._grids, key=lambda k: (math.isnan(best_of(k)),
+                                                   -best_of(k) if metric in _DESC else best_of(k)))
+        for gk in ranked[:2]:
+            g = self._grids[gk]
+            self._grid_step(g["algo"], g["fam"], g["sid"], run, rng, share / 2,
+                            None if not self.max_models else g["n"] + 1)
+
+    def _best_of(self, algos):
+        cat = self.models[0].model_category if self.models else "Regression"
+        metric = self._sort_key(cat)
+        best, bv = None, float("nan")
+        for m in self.models:
+            if m.algo in algos:
+                v = _metric_of(m, metric)
+                if best is None or self._better(v, bv, metric):
+                    best, bv = m, v
+        return best
+
+    def _se_step(self, sid, x, y, fr, valid, job):
+        """StackedEnsembleStepsProvider: best_of_family_* (best model of each family) and all_* (every
+        base model so far); ``_gbm`` restricts to GBMs, ``_xglm`` to XGBoost + GLM, ``best_N`` to the top
+        20. A SE is only built when its base set differs from every SE built before."""
         cat = self.models[0].model_category
         metric = self._sort_key(cat)
-        best = {}
-        for m in self.models:
-            if getattr(m, "cv_holdout", None) is None:
-                continue
-            fam = m.algo if not m.key.startswith("XRT") else "xrt"
-            v = _metric_of(m, metric)
-            if fam not in best or self._better(v, best[fam][1], metric):
-                best[fam] = (m, v)
-        for name, ms in (("BestOfFamily", [b[0] for b in best.values()]),
-                         ("AllModels", [m for m in self.models if getattr(m, "cv_holdout", None) is not None])):
-            if len(ms) < 2:
-                continue
-            mid = f"StackedEnsemble_{name}_1_AutoML_{self.project_name}"
-            try:
-                # StackedEnsembleStepsProvider.setMetalearnerParameters: the metalearner is cross-validated
-                # with the AutoML nfolds, and its out-of-fold metrics are what the leaderboard ranks
-                sp = dict(base_models=[m.key for m in ms], seed=self.seed, metalearner_nfolds=self.nfolds,
-                          metalearner_fold_assignment="Modulo", keep_levelone_frame=True)
-                if cat in ("Binomial", "Multinomial"):
-                    sp["metalearner_transform"] = "Logit"
-                se = builder.train("stackedensemble", sp, x, y, fr, valid, job, mid)
-                self.models.append(se)
-            except Exception as e:  # noqa: BLE001
-                self._log(f"{mid} failed: {e!r}")
+        base = [m for m in self.models if m.algo != "stackedensemble" and getattr(m, "cv_holdout", None) is not None]
+        if sid.endswith("_gbm"):
+            base = [m for m in base if m.algo == "gbm"]
+        elif sid.endswith("_xglm"):
+            base = [m for m in base if m.algo in ("xgboost", "glm")]
+        if sid.startswith("best_of_family"):
+            best = {}
+            for m in base:
+                fam = "xrt" if m.key.startswith("XRT") else m.algo
+                v = _metric_of(m, metric)
+                if fam not in best or self._better(v, best[fam][1], metric):
+                    best[fam] = (m, v)
+            ms, kind = [b[0] for b in best.values()], "BestOfFamily"
+        elif sid == "best_N":
+            ranked = sorted(base, key=lambda m: (math.isnan(_metric_of(m, metric)),
+                                                 -_metric_of(m, metric) if metric in _DESC else _metric_of(m, metric)))
+            ms, kind = ranked[:20], "Best20"
+        else:
+            ms, kind = base, "AllModels"
+        if len(ms) < 2:
+            return
+        keyset = frozenset(m.key for m in ms)
+        done = getattr(self, "_se_sets", set())
+        if keyset in done:
+            return
+        done.add(keyset)
+        self._se_sets = done
+        n = sum(1 for m in self.models if m.algo == "stackedensemble" and f"_{kind}_" in m.key) + 1
+        suffix = {"_gbm": "_GBM", "_xglm": "_XGBoost_GLM"}.get(sid[sid.rfind("_"):], "") if not sid[-1].isdigit() else ""
+        mid = f"StackedEnsemble_{kind}{suffix}_{n}_AutoML_{self.project_name}"
+        try:
+            # StackedEnsembleStepsProvider.setMetalearnerParameters: the metalearner is cross-validated
+            # with the AutoML nfolds, and its out-of-fold metrics are what the leaderboard ranks
+            sp = dict(base_models=[m.key for m in ms], seed=self.seed, metalearner_nfolds=self.nfolds,
+                      metalearner_fold_assignment="Modulo", keep_levelone_frame=True)
+            if cat in ("Binomial", "Multinomial"):
+                sp["metalearner_transform"] = "Logit"
+            se = builder.train("stackedensemble", sp, x, y, fr, valid, job, mid)
+            self.models.append(se)
+            self._log(f"built {mid}")
+        except Exception as e:  # noqa: BLE001
+            self._log(f"{mid} failed: {e!r}")
 
     def _sort_key(self, cat):
         s = str(self.sort_metric).lower()

@@ -262,6 +262,18 @@ def _train(spec, algo, p, x, y, fr, validation_frame, job, model_id):
     if nfolds > 1 or (info.fold and info.fold in fr.names):
         cv_out = _cross_validate(spec, p, fr, info, X, yv, w, off, seed, mid, job)
     tp = {k: v for k, v in p.items() if k not in COMMON}
+    if cv_out is not None and int(p.get("stopping_rounds") or 0) > 0:
+        # ModelBuilder.cv_computeAndSetOptimalParameters: the main model trains for the fold models'
+        # average early-stopped length, without early stopping of its own
+        lens = cv_out.pop("_cv_lengths", [])
+        if lens and algo in ("gbm", "drf", "xgboost"):
+            tp["ntrees"] = max(1, int(round(float(np.mean(lens)))))
+            tp["stopping_rounds"] = 0
+        elif lens and algo == "deeplearning":
+            tp["epochs"] = float(np.mean(lens))
+            tp["stopping_rounds"] = 0
+    if cv_out is not None:
+        cv_out.pop("_cv_lengths", None)
     if cv_out is not None and float(tp.get("max_runtime_secs") or 0) > 0:
         tp["max_runtime_secs"] = max(1e-3, float(tp["max_runtime_secs"]) - (time.time() - t0))
     tr = spec.trainer(tp)
@@ -384,7 +396,11 @@ def _cross_validate(spec, p, fr, info, X, yv, w, off, seed, mid, job):
             ps["max_runtime_secs"] = float(ps["max_runtime_secs"]) / (k + 1)
         trainer = spec.trainer(ps)
         trainer.job = job
-        m = trainer.fit(sub(X, tr_m).contiguous(), sub(yv, tr_m), sub(w, tr_m), sub(off, tr_m), info, None,
+        # ModelBuilder.cv_makeFramesAndBuilders: a fold model validates (and early-stops) on its holdout
+        ho_valid = None
+        if int(p.get("stopping_rounds") or 0) > 0 and yv is not None:
+            ho_valid = (sub(X, ho_m).contiguous(), sub(yv, ho_m), sub(w, ho_m), sub(off, ho_m))
+        m = trainer.fit(sub(X, tr_m).contiguous(), sub(yv, tr_m), sub(w, tr_m), sub(off, tr_m), info, ho_valid,
                         f"{mid}_cv_{i + 1}")
         models.append(m)
         P = m.score_tensor(sub(X, ho_m).contiguous(), sub(off, ho_m))
@@ -396,6 +412,8 @@ def _cross_validate(spec, p, fr, info, X, yv, w, off, seed, mid, job):
         if p.get("keep_cross_validation_models", True):
             dkv.put(m.key, m)
     out = dict(cross_validation_models=[m.key for m in models] if p.get("keep_cross_validation_models", True) else None)
+    out["_cv_lengths"] = [float(m.output.get("ntrees") or m.output.get("epochs") or 0) for m in models
+                          if (m.output.get("ntrees") or m.output.get("epochs"))]
     if yv is not None and holdout is not None:
         cvm = mm.make_metrics(cat, yv, holdout, w, info.response_domain)
         out["cross_validation_metrics"] = cvm

@@ -299,8 +299,7 @@ class SharedTreeTrainer:
         done = handles[:len(levels)]
         del handles[:len(levels)]
         for (h, k), tl in zip(done, levels):
-            tree = levels_to_tree(tl, self.binning)
-            forest.add(tree, k)
+            forest.add_levels(tl, self.binning, k)     # flattened lazily (Forest.trees)
             for d in tl.decs:
                 fe = d["feat"]
                 m = fe >= 0

@@ -127,18 +127,41 @@ class Forest:
     """Trees + class assignment, with cached flat device arrays for scoring."""
 
     def __init__(self, trees=None, tree_class=None, n_classes_out: int = 1):
-        self.trees = list(trees or [])
-        self.tree_class = list(tree_class or [0] * len(self.trees))
+        self._trees = list(trees or [])
+        self._pending = []          # (TreeLevels, binning) decoded on first access of ``trees``
+        self.tree_class = list(tree_class or [0] * len(self._trees))
         self.K = n_classes_out
         self._flat = {}
 
+    @property
+    def trees(self):
+        """Node tables of every tree. Trees added with :meth:`add_levels` are decoded from their level
+        records here, on first use (scoring, MOJO, summaries), so the training loop never waits on the
+        host-side flattening of the last trees it built."""
+        if self._pending:
+            pend, self._pending = self._pending, []
+            self._trees.extend(levels_to_tree(tl, b) for tl, b in pend)
+        return self._trees
+
+    @trees.setter
+    def trees(self, v):
+        self._trees = list(v)
+        self._pending = []
+
     def add(self, tree: Tree, cls: int = 0):
-        self.trees.append(tree)
+        if self._pending:
+            self.trees    # keep insertion order
+        self._trees.append(tree)
+        self.tree_class.append(cls)
+        self._flat.clear()
+
+    def add_levels(self, tl, binning, cls: int = 0):
+        self._pending.append((tl, binning))
         self.tree_class.append(cls)
         self._flat.clear()
 
     def __len__(self):
-        return len(self.trees)
+        return len(self._trees) + len(self._pending)
 
     def flatten(self, t0=0, t1=None):
         t1 = len(self.trees) if t1 is None else t1
