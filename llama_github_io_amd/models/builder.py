@@ -184,6 +184,10 @@ def train(algo: str, params: dict, x=None, y=None, training_frame=None, validati
     fr = training_frame
     if fr is None:
         raise ValueError("training_frame is required")
+    if algo == "gam" and p.get("gam_columns") and x is not None:
+        # GAM.java: the smoothed columns are predictors whether or not x lists them
+        gc = [c for g in p["gam_columns"] for c in ([g] if isinstance(g, str) else g)]
+        x = list(x) + [c for c in gc if c not in x]
     from ..parallel import collectives as coll, dframe
     import contextlib
     mode = contextlib.ExitStack()

@@ -337,6 +337,7 @@ class GLMTrainer:
         self.p = p
         self.job = None
         self.penalty = None     # optional (P+1)x(P+1) quadratic penalty (GAM)
+        self.lower_bounds = None  # optional (P+1) coefficient lower bounds (GAM I-splines)
 
     def _family(self, info):
         fam = canon(self.p["family"])
@@ -573,8 +574,11 @@ class GLMTrainer:
     def _bounds(self, ex, P1, dev):
         """beta_constraints (names, lower_bounds, upper_bounds) on the raw scale -> standardized bounds."""
         bc = self.p.get("beta_constraints")
+        extra = getattr(self, "lower_bounds", None)       # set by GAM: non-negative I-spline coefficients
         if bc is None:
-            return None, None
+            if extra is None:
+                return None, None
+            return extra.to(dev), torch.full((P1,), float("inf"), dtype=torch.float64, device=dev)
         if hasattr(bc, "as_data_frame"):
             bc = bc.as_data_frame()
         import pandas as pd

@@ -44,10 +44,9 @@ UNSUPPORTED = {
             "fix_dispersion_parameter", "fix_tweedie_variance_power", "generate_variable_inflation_factors",
             "influence", "init_dispersion_parameter", "max_iterations_dispersion", "rand_link", "tweedie_epsilon",
             "calc_like", "checkpoint", "prior", "gradient_epsilon", "early_stopping"},
-    "gam": {"beta_constraints", "bs", "cold_start", "interaction_pairs", "interactions", "knot_ids",
-            "max_active_predictors", "remove_collinear_columns", "scale_tp_penalty_mat", "spline_orders",
-            "splines_non_negative", "standardize_tp_gam_cols", "startval", "prior", "gradient_epsilon",
-            "objective_epsilon", "early_stopping", "plug_values"},
+    "gam": {"beta_constraints", "cold_start", "interaction_pairs", "interactions",
+            "max_active_predictors", "remove_collinear_columns", "standardize_tp_gam_cols", "startval", "prior",
+            "gradient_epsilon", "objective_epsilon", "early_stopping", "plug_values"},
     "anovaglm": {"early_stopping", "prior", "type", "plug_values"},
     "modelselection": {"beta_constraints", "cold_start", "influence", "max_active_predictors", "prior",
                        "remove_collinear_columns", "startval", "p_values_threshold", "gradient_epsilon",

@@ -1,0 +1,75 @@
+"""GAM smoother families (reference hex/gam/GamSplines/*, MatrixFrameUtils/Gen*GamOneColumn.java):
+cubic regression (bs=0), thin plate (bs=1, several columns), monotone I-splines (bs=2), M-splines
+(bs=3), and categorical linear predictors."""
+import numpy as np
+import pytest
+import torch
+
+
+@pytest.fixture(scope="module")
+def data():
+    import h2o
+    h2o.init(verbose=False)
+    rng = np.random.default_rng(7)
+    n = 800
+    a = rng.uniform(-3, 3, n)
+    b = rng.uniform(-2, 2, n)
+    c = rng.choice(["u", "v", "w"], n)
+    shift = np.select([c == "u", c == "v"], [0.0, 1.0], -1.0)
+    y = np.sin(a) + 0.5 * b ** 2 + shift + rng.normal(size=n) * 0.1
+    ym = np.tanh(a) * 2 + rng.normal(size=n) * 0.2                  # monotone in a
+    fr = h2o.H2OFrame({"a": a.tolist(), "b": b.tolist(), "c": c.tolist(), "y": y.tolist(), "ym": ym.tolist()})
+    fr["c"] = fr["c"].asfactor()
+    return fr, a, b, shift
+
+
+def test_cr_basis_is_cardinal_with_linear_null_space():
+    from llama_github_io_amd.models.gam import _cr_mats, cr_basis
+    knots = torch.tensor([0.0, 0.7, 1.5, 2.0, 3.3, 4.0], dtype=torch.float64)
+    F, S = _cr_mats(knots)
+    X = cr_basis(knots, knots, F)
+    assert torch.allclose(X, torch.eye(6, dtype=torch.float64), atol=1e-12)    # beta = values at the knots
+    assert torch.allclose(S @ torch.ones(6, dtype=torch.float64), torch.zeros(6, dtype=torch.float64), atol=1e-10)
+    assert torch.allclose(S @ knots, torch.zeros(6, dtype=torch.float64), atol=1e-10)   # straight lines unpenalised
+
+
+def test_cr_and_categorical_linear(data):
+    from h2o.estimators import H2OGeneralizedAdditiveEstimator
+    fr, a, b, shift = data
+    m = H2OGeneralizedAdditiveEstimator(gam_columns=["a", "b"], num_knots=[8, 6], bs=[0, 0], family="gaussian")
+    m.train(x=["c"], y="y", training_frame=fr)
+    pred = m.predict(fr).as_data_frame()["predict"].values
+    truth = np.sin(a) + 0.5 * b ** 2 + shift
+    assert np.sqrt(np.mean((pred - truth - np.mean(pred - truth)) ** 2)) < 0.12
+
+
+def test_thin_plate_two_columns(data):
+    from h2o.estimators import H2OGeneralizedAdditiveEstimator
+    fr, a, b, shift = data
+    m = H2OGeneralizedAdditiveEstimator(gam_columns=[["a", "b"]], num_knots=[40], bs=[1], family="gaussian")
+    m.train(x=["c"], y="y", training_frame=fr)
+    pred = m.predict(fr).as_data_frame()["predict"].values
+    truth = np.sin(a) + 0.5 * b ** 2 + shift
+    assert np.corrcoef(pred, truth)[0, 1] > 0.97
+
+
+def test_monotone_ispline(data):
+    from h2o.estimators import H2OGeneralizedAdditiveEstimator
+    import h2o
+    fr, a, b, shift = data
+    m = H2OGeneralizedAdditiveEstimator(gam_columns=["a"], num_knots=[8], bs=[2], spline_orders=[3], family="gaussian")
+    m.train(x=[], y="ym", training_frame=fr)
+    grid = np.linspace(-3, 3, 200)
+    g = h2o.H2OFrame({"a": grid.tolist(), "b": [0.0] * 200, "c": ["u"] * 200}, column_types={"c": "enum"})
+    p = m.predict(g).as_data_frame()["predict"].values
+    assert (np.diff(p) >= -1e-9).all()                                   # non-negative coefficients: monotone
+    assert np.corrcoef(p, np.tanh(grid) * 2)[0, 1] > 0.98
+
+
+def test_mspline(data):
+    from h2o.estimators import H2OGeneralizedAdditiveEstimator
+    fr, a, b, shift = data
+    m = H2OGeneralizedAdditiveEstimator(gam_columns=["a"], num_knots=[8], bs=[3], spline_orders=[3], family="gaussian")
+    m.train(x=["c"], y="y", training_frame=fr)             # b**2 is left out: pred ~ sin(a) + shift + const
+    pred = m.predict(fr).as_data_frame()["predict"].values
+    assert np.corrcoef(pred, np.sin(a) + shift)[0, 1] > 0.95
