@@ -665,3 +665,58 @@ def score_glrm(st, X, iters=200):
     if str(st["regx"]).lower() not in ("none", "quadratic"):
         xd = _prox(st["regx"], xd, 0.0, 1)
     return xd.float()
+
+
+_GLRM_LOSS = {"quadratic": "Quadratic", "absolute": "Absolute", "huber": "Huber", "poisson": "Poisson",
+              "hinge": "Hinge", "logistic": "Logistic", "periodic": "Periodic", "categorical": "Categorical",
+              "ordinal": "Ordinal"}
+_GLRM_REG = {"none": "None", "quadratic": "Quadratic", "l2": "L2", "l1": "L1", "nonnegative": "NonNegative",
+             "onesparse": "OneSparse", "unitonesparse": "UnitOneSparse", "simplex": "Simplex"}
+
+
+def write_glrm(model, kv, blobs):
+    """GlrmMojoWriter layout: the archetypes over the expanded columns (categorical one-hot blocks,
+    then numerics), per-column losses, the cats-first column permutation and the numeric
+    standardisation, so ``GlrmMojoModel`` (and this package's reader) can solve each row's X."""
+    canon = lambda s: str(s).lower().replace("_", "")  # noqa: E731
+    p = model.params
+    ex = model.expander
+    Y = model.Y.double().cpu().numpy()
+    k, P = Y.shape
+    perm = list(ex.cats) + list(ex.nums)
+    nlev = [len(model.info.domains[j] or []) for j in ex.cats]
+    offs = [0]
+    for n in nlev:
+        offs.append(offs[-1] + n)
+    nn = len(ex.nums)
+    if ex.nums and ex.standardize:
+        sub = ex.num_mean.double().cpu().tolist()
+        mul = (1.0 / ex.num_sd.double().clamp(min=1e-300)).cpu().tolist()
+    elif ex.nums and getattr(ex, "center_only", False):
+        sub, mul = ex.num_mean.double().cpu().tolist(), [1.0] * nn
+    else:
+        sub, mul = [0.0] * nn, [1.0] * nn
+    kv["initialization"] = {"plusplus": "PlusPlus", "svd": "SVD", "random": "Random", "user": "User"}.get(
+        canon(p.get("init", "PlusPlus")), "PlusPlus")
+    kv["regularizationX"] = _GLRM_REG.get(canon(p.get("regularization_x", "None")), "None")
+    kv["regularizationY"] = _GLRM_REG.get(canon(p.get("regularization_y", "None")), "None")
+    kv["gammaX"] = float(p.get("gamma_x") or 0.0)
+    kv["gammaY"] = float(p.get("gamma_y") or 0.0)
+    kv["ncolX"] = k
+    kv["seed"] = int(p.get("seed") if p.get("seed") not in (None, -1) else 0)
+    kv["reverse_transform"] = "true" if p.get("impute_original") else "false"
+    kv["cols_permutation"] = "[" + ", ".join(str(int(v)) for v in perm) + "]"
+    kv["num_categories"] = len(ex.cats)
+    kv["num_numeric"] = nn
+    kv["norm_sub"] = "[" + ", ".join(repr(float(v)) for v in sub) + "]"
+    kv["norm_mul"] = "[" + ", ".join(repr(float(v)) for v in mul) + "]"
+    kv["transposed"] = "false"
+    num_loss = _GLRM_LOSS.get(canon(p.get("loss", "Quadratic")), "Quadratic")
+    cat_loss = _GLRM_LOSS.get(canon(p.get("multi_loss", "Categorical")), "Categorical")
+    kv["ncolA"] = len(perm)
+    blobs["losses"] = "".join((cat_loss if i < len(ex.cats) else num_loss) + "\n" for i in range(len(perm)))
+    kv["ncolY"] = P
+    kv["nrowY"] = k
+    kv["num_levels_per_category"] = "[" + ", ".join(str(n) for n in nlev + [-1] * nn) + "]"
+    kv["catOffsets"] = "[" + ", ".join(str(o) for o in offs) + "]"
+    blobs["archetypes"] = Y.astype(">f8").tobytes()

@@ -248,3 +248,34 @@ def test_pipeline_fixtures_load():
         m = getattr(m, "_model", m)
         P = m._predict_tensor(torch.zeros(m.info.F, 2), None)
         assert P.shape[0] == 2
+
+
+def test_glrm_mojo_reference_layout_roundtrip(tmp_path):
+    """Our GLRM written in the GlrmMojoWriter layout reads back through the same reader that scores the
+    reference fixture; the solved X factors reconstruct the (standardised) rows like the trained X."""
+    import h2o
+    from h2o.estimators import H2OGeneralizedLowRankEstimator
+    from llama_github_io_amd.mojo.reader import parse_mojo
+    h2o.init(verbose=False)
+    rng = np.random.default_rng(5)
+    n = 300
+    U = rng.normal(size=(n, 2))
+    V = rng.normal(size=(2, 4))
+    A = U @ V + rng.normal(size=(n, 4)) * 0.01
+    cat = np.where(U[:, 0] > 0, "hi", "lo")
+    fr = h2o.H2OFrame({"x0": A[:, 0].tolist(), "x1": A[:, 1].tolist(), "x2": A[:, 2].tolist(),
+                       "x3": A[:, 3].tolist(), "c": cat.tolist()}, column_types={"c": "enum"})
+    m = H2OGeneralizedLowRankEstimator(k=3, transform="STANDARDIZE", seed=1, max_iterations=200)
+    m.train(training_frame=fr)
+    path = m.download_mojo(str(tmp_path))
+    mj = parse_mojo(path)
+    assert mj["info"]["algo"] == "glrm" and "losses" in mj["files"] and "archetypes" in mj["files"]
+    g = h2o.import_mojo(path)
+    g = getattr(g, "_model", g)
+    X, _ = fr.model_matrix(g.info)
+    x = g._predict_tensor(X, None).double()                  # [n, k] factors
+    st = g.glrm
+    nc = st["cat_off"][-1]
+    rec = (x @ st["Y"])[:, nc:]
+    Z = (torch.tensor(A) - torch.tensor(st["norm_sub"])) * torch.tensor(st["norm_mul"])
+    assert float(((rec - Z) ** 2).mean()) < 0.05
