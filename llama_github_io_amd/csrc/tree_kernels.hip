@@ -451,7 +451,8 @@ __global__ __launch_bounds__(RW * 64) void k_hist_reduce(
 __global__ __launch_bounds__(256) void k_split_find(
     const double* __restrict__ hist, int slot_doubles, const int* __restrict__ meta, int F,
     const int* __restrict__ nbins_f, const int* __restrict__ iscat_f, const int* __restrict__ mono_f,
-    SplitParams p, int level, Cand* __restrict__ cand, double* __restrict__ root_w) {
+    SplitParams p, int level, Cand* __restrict__ cand, double* __restrict__ root_w,
+    const float* __restrict__ edges /*[F][255] global bin edges (inf padded) or null*/, int adapt_nb) {
   const int node = blockIdx.x, f = blockIdx.y, t = threadIdx.x;
   if (node >= meta[0]) return;
   __shared__ double sw[256], swy[256], skey[256];
@@ -541,7 +542,34 @@ __global__ __launch_bounds__(256) void k_split_find(
       rand_b = s_lo + 1 + (int)(hsh % (unsigned long long)(s_hi - s_lo));
     }
   }
-  if (t >= 1 && t < nb && (!random_mode || t == rand_b)) {
+  // UniformAdaptive (DHistogram, the H2O default): a node's numeric split candidates are the
+  // adapt_nb - 1 uniform cut points of its occupied value range; on the global-bin lattice a
+  // threshold t ("bins < t go left" = x < edge[t-1]) is kept iff some cut point falls in
+  // (edge[t-2], edge[t-1]]. adapt_nb = max(nbins, nbins_top_level >> level); 0 = QuantilesGlobal.
+  bool lattice_ok = true;
+  if (adapt_nb > 1 && edges != nullptr && !cat && !random_mode) {
+    __shared__ int a_lo, a_hi;
+    if (t == 0) { a_lo = 0; a_hi = -1; }
+    __syncthreads();
+    const double cw = sw[t], pw = t > 0 ? sw[t - 1] : 0.0;
+    if (t < nb && cw > 0 && pw == 0) a_lo = t;
+    if (t < nb && W > 0 && cw == W && pw < W) a_hi = t;
+    __syncthreads();
+    const float* e = edges + (size_t)f * 255;
+    if (a_hi > a_lo && a_hi - a_lo + 1 > adapt_nb) {
+      const double lo = (double)e[a_lo > 0 ? a_lo - 1 : 0];
+      const double hi = (double)e[a_hi <= nb - 2 ? a_hi : nb - 2];
+      if (hi > lo) {
+        const double sc = (double)adapt_nb / (hi - lo);
+        auto cnt = [&](double x) -> int {
+          double c = floor((x - lo) * sc);
+          return (int)(c < 0 ? 0 : (c > adapt_nb - 1 ? adapt_nb - 1 : c));
+        };
+        lattice_ok = t >= 1 && t < nb && cnt((double)e[t - 1]) > (t >= 2 ? cnt((double)e[t - 2]) : 0);
+      }
+    }
+  }
+  if (t >= 1 && t < nb && lattice_ok && (!random_mode || t == rand_b)) {
     const double wb = (t < 256) ? (sw[t] - sw[t - 1]) : 0.0;
     if (wb != 0.0 || random_mode) {
       const double wlo = sw[t - 1], wylo = swy[t - 1];
@@ -1325,13 +1353,13 @@ int h2o_leaf_values(const void* leafsum, int n, int log_link, double scale, doub
 int h2o_split_find(const void* hist, int slot_doubles, const void* meta, int cap, int F, const void* nbins_f,
                    const void* iscat_f, const void* mono_f, double min_w, double msi, double lambda_, double alpha,
                    double gamma, int mode, int random_split, unsigned long long seed, int level, void* cand,
-                   void* root_w, hipStream_t s) {
+                   void* root_w, const void* edges, int adapt_nb, hipStream_t s) {
   SplitParams p;
   p.min_w = min_w; p.min_split_improvement = msi; p.lambda = lambda_; p.alpha = alpha; p.gamma = gamma;
   p.mode = mode; p.random_split = random_split; p.seed = seed;
   hipLaunchKernelGGL(k_split_find, dim3(cap, F), dim3(256), 0, s, (const double*)hist, slot_doubles,
                      (const int*)meta, F, (const int*)nbins_f, (const int*)iscat_f, (const int*)mono_f, p, level,
-                     (Cand*)cand, (double*)root_w);
+                     (Cand*)cand, (double*)root_w, (const float*)edges, adapt_nb);
   return (int)hipGetLastError();
 }
 
@@ -1466,6 +1494,9 @@ struct TreePlan {
   double scale, kclamp, mx;
   int kc_level[TP_MAXL];   // per-level column sample size (col_sample_rate_change_per_level); 0 = k_cols
   int pad2;
+  void* edges;             // [F][255] global bin edges for UniformAdaptive candidates (null: QuantilesGlobal)
+  int nb_level[TP_MAXL];   // UniformAdaptive bins per level (0 = off)
+  int pad3;
 };
 
 static inline void tp_level_buf(const TreePlan* P, int e, const void*& b, const void*& a, const void*& r) {
@@ -1509,7 +1540,7 @@ int h2o_tree_level(const TreePlan* P, int d, int dist, hipStream_t s) {
   const bool odd = d % 2 == 1;
   int rc = h2o_split_find(hc, P->slot, P->meta[d], cap, P->F, P->nbins_f, P->iscat_f, P->mono_f, P->min_w, P->msi,
                           P->lam, P->alpha, P->gamma, P->mode, P->random_split, P->seed, d, P->cand,
-                          d == 0 ? P->rootw : nullptr, s);
+                          d == 0 ? P->rootw : nullptr, P->edges, P->nb_level[d], s);
   if (rc) return -rc;
   const int kc = P->kc_level[d] > 0 ? P->kc_level[d] : P->k_cols;
   rc = h2o_split_reduce(P->cand, P->meta[d], cap, P->F, P->feat_ok, kc, P->seed, d, P->dec[d], s);

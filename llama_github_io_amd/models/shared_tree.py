@@ -117,8 +117,22 @@ class SharedTreeTrainer:
 
     # ---- hooks
     def _split_params(self) -> T.SplitParams:
-        return T.SplitParams(min_w=float(self.p["min_rows"]), min_split_improvement=float(self.p["min_split_improvement"]),
-                             mode=self.mode)
+        sp = T.SplitParams(min_w=float(self.p["min_rows"]), min_split_improvement=float(self.p["min_split_improvement"]),
+                           mode=self.mode)
+        ht = str(self.p.get("histogram_type", "AUTO")).lower().replace("_", "")
+        if ht in ("auto", "uniformadaptive") and getattr(self, "binning", None) is not None:
+            # DHistogram UniformAdaptive: nbins_top_level bins at the root, halved per level down to nbins
+            sp.adapt_nbins = int(self.p.get("nbins") or 20)
+            sp.adapt_top = int(self.p.get("nbins_top_level") or 1024)
+            sp.edges = self._edge_table()
+        return sp
+
+    def _edge_table(self):
+        tab = np.full((self.binning.F, 255), np.inf, dtype=np.float32)
+        for f, e in enumerate(self.binning.edges):
+            if e is not None and len(e):
+                tab[f, :min(len(e), 255)] = e[:255]
+        return tab
 
     def _k_cols(self, F_ok: int) -> int:
         return 0

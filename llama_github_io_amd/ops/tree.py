@@ -57,6 +57,16 @@ class SplitParams:
     gamma: float = 0.0
     mode: int = MODE_SE
     random_split: bool = False
+    # UniformAdaptive (the H2O default histogram_type): per-level bin counts max(nbins, nbins_top_level >> d)
+    # applied as a candidate lattice over the global bin edges ([F, 255] float32, inf padded)
+    adapt_nbins: int = 0
+    adapt_top: int = 0
+    edges: object = None
+
+    def adapt_nb(self, level: int) -> int:
+        if not self.adapt_nbins or self.edges is None:
+            return 0
+        return max(int(self.adapt_nbins), int(self.adapt_top) >> int(level))
 
 
 @dataclass
@@ -120,12 +130,27 @@ def split_find_ref(h, nayy, wyy, nbins_f, iscat_f, mono_f, p: SplitParams, level
                 lo, hi = int(occ[0]), int(occ[-1])
                 hsh = splitmix64((seed ^ (level << 48) ^ (node << 20) ^ f) & _M64)
                 rand_b = lo + 1 + int(hsh % (hi - lo))
+        allowed = None
+        anb = p.adapt_nb(level)
+        if anb > 1 and not cat and not random_mode:
+            occ = np.nonzero(w[:nb] > 0)[0]
+            if occ.size and occ[-1] > occ[0] and occ[-1] - occ[0] + 1 > anb:
+                a_lo, a_hi = int(occ[0]), int(occ[-1])
+                e = np.asarray(p.edges[f], dtype=np.float32).astype(np.float64)
+                lo = e[a_lo - 1 if a_lo > 0 else 0]
+                hi = e[a_hi if a_hi <= nb - 2 else nb - 2]
+                if hi > lo:
+                    sc = anb / (hi - lo)
+                    cnt = lambda x: int(min(max(math.floor((x - lo) * sc), 0), anb - 1))  # noqa: E731
+                    allowed = {t for t in range(1, nb) if cnt(e[t - 1]) > (cnt(e[t - 2]) if t >= 2 else 0)}
         best_e, best_code = -1.0e300, -1
         cands = []
         if wNA >= p.min_w and W > 0 and not random_mode:
             cands.append((float(_E(p.mode, p, W, WY) + _E(p.mode, p, wNA, wyNA)), 0))
         for t in range(1, nb):
             if random_mode and t != rand_b:
+                continue
+            if allowed is not None and t not in allowed:
                 continue
             wb = sw[t] - sw[t - 1]
             if wb == 0.0 and not random_mode:
@@ -370,7 +395,8 @@ class _TreePlan(ctypes.Structure):
                 [(n, _vp) for n in ("aux", "amax_bits", "feat_ok")] +
                 [(n, _ci) for n in ("compute_amax", "k_cols", "packed", "leaf_native", "log_link", "pad1")] +
                 [("seed", ctypes.c_ulonglong)] + [(n, _cd) for n in ("scale", "kclamp", "mx")] +
-                [("kc_level", _ci * _MAXL), ("pad2", _ci)])
+                [("kc_level", _ci * _MAXL), ("pad2", _ci)] +
+                [("edges", _vp), ("nb_level", _ci * _MAXL), ("pad3", _ci)])
 
 
 class _Arena:
@@ -505,7 +531,17 @@ class GpuTreeBuilder:
             for n in ("nodes", "meta", "tp", "bp", "dec", "cl", "cr", "nl", "cur"):
                 getattr(P, n)[d] = self._p(f"{n}{d}")
             P.caps[d], P.tiles_cap[d] = self.caps[d], self.tiles_cap[d]
+        P.edges = self._edges_ptr()
+        for d in range(_MAXL):
+            P.nb_level[d] = p.adapt_nb(d) if P.edges else 0
         return P
+
+    def _edges_ptr(self):
+        if self.p.edges is None or not self.p.adapt_nbins:
+            return 0
+        if getattr(self, "_edges_dev", None) is None:
+            self._edges_dev = torch.as_tensor(np.asarray(self.p.edges, dtype=np.float32), device=self.master.device).contiguous()
+        return self._edges_dev.data_ptr()
 
     def build(self, aux_static: torch.Tensor, feat_ok: torch.Tensor | None = None, k_cols: int = 0, seed: int = 0,
               leaf_fn=None, amax_bits: torch.Tensor | None = None, packed: bool = False, leaf_native=None):
@@ -579,7 +615,8 @@ class GpuTreeBuilder:
             nat.check(lib.h2o_split_find(hcp, slot, self._p(f"meta{d}"), cap, F, nb_p,
                                          ic_p, mono, p.min_w, p.min_split_improvement, p.lam,
                                          p.alpha, p.gamma, p.mode, int(p.random_split), seed, d,
-                                         cand_p, self._p("rootw") if d == 0 else 0, s), "split_find")
+                                         cand_p, self._p("rootw") if d == 0 else 0, self._edges_ptr(),
+                                         p.adapt_nb(d) if self._edges_ptr() else 0, s), "split_find")
             nat.check(lib.h2o_split_reduce(cand_p, self._p(f"meta{d}"), cap, F, fo_p, _level_k(k_cols, d),
                                            seed, d, self._p(f"dec{d}"), s), "split_reduce")
             nat.check(lib.h2o_plan(self._p(f"nodes{d}"), self._p(f"meta{d}"), self._p(f"dec{d}"), self._p(f"nl{d}"),

@@ -214,3 +214,84 @@ def test_gpu_tree_matches_reference_row_widths(F):
     for dr, dg in zip(tl_r.decs, tl_g.decs):
         assert np.array_equal(dr["feat"], dg["feat"]) and np.array_equal(dr["bin"], dg["bin"])
     assert torch.equal(ref.leaf_of_row, gb.leaf_of_row.cpu())
+
+
+def _edge_tab(b):
+    tab = np.full((b.F, 255), np.inf, dtype=np.float32)
+    for f, e in enumerate(b.edges):
+        if e is not None and len(e):
+            tab[f, :len(e)] = e
+    return tab
+
+
+def test_uniform_adaptive_lattice_restricts_candidates():
+    """UniformAdaptive (DHistogram): at a level with nb adaptive bins, a numeric split lands on one of
+    the <= nb - 1 global edges nearest the uniform cut points of the node's occupied range."""
+    X, y, info = _data(N=6000, seed=2)
+    b = fit_binning(X, info.iscat, info.nlevels, max_bins=255)
+    bins = apply_binning(b, X)
+    aux = torch.stack([torch.ones_like(y), y - y.mean(), y - y.mean(), torch.ones_like(y)], 1).contiguous()
+    tab = _edge_tab(b)
+    p = T.SplitParams(min_w=10, adapt_nbins=4, adapt_top=4, edges=tab)      # 4 bins at every level
+    ref = T.RefTreeBuilder(bins, X.shape[0], b.nbins, b.iscat, None, 3, p)
+    ref.build(aux, leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1]).float())
+    tl = ref.pop_levels()[0]
+    root = tl.decs[0]
+    f, bn = int(root["feat"][0]), int(root["bin"][0])
+    e = tab[f][: b.nbins[f] - 1]
+    lo, hi = e[0], e[b.nbins[f] - 2]
+    cuts = lo + (hi - lo) * np.arange(1, 4) / 4
+    allowed = {int(np.searchsorted(e, c, side="left")) + 1 for c in cuts}
+    assert bn in allowed
+    # the unrestricted (QuantilesGlobal) search can pick any of the 254 thresholds
+    q = T.RefTreeBuilder(bins, X.shape[0], b.nbins, b.iscat, None, 3, T.SplitParams(min_w=10))
+    q.build(aux, leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1]).float())
+    assert int(q.pop_levels()[0].decs[0]["feat"][0]) == f
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["adaptive", "newton", "random", "mono", "kcols", "featok", "multiclass"])
+def test_gpu_tree_modes_match_reference(case):
+    """Every split mode of k_split_find / k_split_reduce pinned against RefTreeBuilder (identical
+    feature / bin / left weight per decision and identical leaf assignment)."""
+    X, y, info = _data(N=20000, cat=True, seed=9)
+    b = fit_binning(X, info.iscat, info.nlevels, max_bins=128)
+    bins = apply_binning(b, X)
+    g = y - y.mean()
+    aux = torch.stack([torch.ones_like(y), g, g, torch.ones_like(y)], 1).contiguous()
+    mono, feat_ok, k_cols, depth = None, None, 0, 5
+    if case == "adaptive":
+        p = T.SplitParams(min_w=10, adapt_nbins=20, adapt_top=128, edges=_edge_tab(b))
+    elif case == "newton":
+        h = torch.full_like(y, 0.25)
+        aux = torch.stack([h, -g, -g, h], 1).contiguous()
+        p = T.SplitParams(min_w=1.0, lam=1.0, alpha=0.1, gamma=0.01, mode=T.MODE_NEWTON)
+    elif case == "random":
+        p = T.SplitParams(min_w=5, mode=T.MODE_RANDOM, random_split=True)
+    elif case == "mono":
+        mono = np.array([1, -1, 0, 0, 0, 0], dtype=np.int32)
+        p = T.SplitParams(min_w=10)
+    elif case == "kcols":
+        k_cols, p = 3, T.SplitParams(min_w=10)
+    elif case == "featok":
+        feat_ok = torch.tensor([1, 0, 1, 1, 0, 1], dtype=torch.int32)
+        p = T.SplitParams(min_w=10)
+    else:                                   # multinomial: K independent class trees on per-class aux
+        y3 = (X[0] > 0.5).float() + (X[1] > 0).float()
+        g = (y3 == 2).float() - (y3 == 2).float().mean()
+        aux = torch.stack([torch.ones_like(y), g, g, torch.ones_like(y)], 1).contiguous()
+        p = T.SplitParams(min_w=10)
+    ref = T.RefTreeBuilder(bins, X.shape[0], b.nbins, b.iscat, mono, depth, p)
+    ref.build(aux, feat_ok, k_cols, seed=77, leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1].clamp(min=1e-12)).float())
+    tl_r = ref.pop_levels()[0]
+    dev = torch.device("cuda", 0)
+    gb = T.GpuTreeBuilder(bins.to(dev), X.shape[0], b.nbins, b.iscat, mono, depth, p)
+    gb.build(aux.to(dev), None if feat_ok is None else feat_ok.to(dev), k_cols, seed=77,
+             leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1].clamp(min=1e-12)).float())
+    tl_g = gb.pop_levels()[0]
+    assert tl_g.n_leaves == tl_r.n_leaves
+    for dr, dg in zip(tl_r.decs, tl_g.decs):
+        assert np.array_equal(dr["feat"], dg["feat"])
+        assert np.array_equal(dr["bin"], dg["bin"])
+        np.testing.assert_allclose(dr["wl"], dg["wl"], rtol=1e-6)
+    assert torch.equal(ref.leaf_of_row, gb.leaf_of_row.cpu())
