@@ -27,6 +27,10 @@ def new_key(prefix: str = "key") -> str:
 def put(key: str, value) -> None:
     with _lock:
         _store[key] = value
+    if hasattr(value, "_cols"):                 # a frame entered the store: LRU stamp + HBM back-pressure
+        from ..utils import memory
+        memory.touch(key)
+        memory.pressure_check()
 
 
 def get(key: str, default=None):

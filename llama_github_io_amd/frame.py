@@ -7,6 +7,7 @@ A :class:`Column` holds one typed vector:
 * ``enum``            -> int32 codes into ``domain`` (sorted level strings), -1 = missing
 * ``string``          -> numpy object array (host), None = missing
 * ``time``            -> float64 ms since epoch, NaN = missing
+* ``uuid``            -> int64 [N, 2] (high, low 64 bits; C16Chunk), both INT64_MIN = missing
 
 Numeric/enum tensors live on the engine device (HBM on MI355X); every reduction and elementwise op
 runs there through torch. :meth:`H2OFrame.model_matrix` adapts any frame to a trained model's
@@ -73,6 +74,8 @@ class Column:
     def n(self):
         if self.type == "string":
             return len(self.strings)
+        if self.type == "uuid":
+            return int(self.data.shape[0])
         return int(self.data.numel())
 
     def copy(self):
@@ -81,6 +84,8 @@ class Column:
                       None if self.strings is None else self.strings.copy())
 
     def isna(self) -> torch.Tensor:
+        if self.type == "uuid":
+            return (self.data[:, 0] == _UUID_NA) & (self.data[:, 1] == _UUID_NA)
         if self.type == "enum":
             return self.data < 0
         if self.type == "string":
@@ -95,6 +100,8 @@ class Column:
         if self.type == "string":
             vals = np.array([_to_float(s) for s in self.strings], dtype=np.float64)
             return torch.from_numpy(vals).to(engine_device())
+        if self.type == "uuid":
+            return torch.full((self.n,), float("nan"), dtype=torch.float64, device=self.data.device)
         return self.data
 
     def take(self, idx: torch.Tensor):
@@ -105,11 +112,47 @@ class Column:
     def to_numpy(self):
         if self.type == "string":
             return self.strings
+        if self.type == "uuid":
+            return uuid_strings(self.data)
         if self.type == "enum":
             codes = self.data.cpu().numpy()
             dom = np.array(self.domain + [None], dtype=object)
             return dom[np.where(codes < 0, len(self.domain), codes)]
         return self.data.cpu().numpy()
+
+
+_UUID_NA = -(1 << 63)
+_UUID_RX = re.compile(r"^[0-9a-fA-F]{8}-[0-9a-fA-F]{4}-[0-9a-fA-F]{4}-[0-9a-fA-F]{4}-[0-9a-fA-F]{12}$")
+
+
+def _signed(v: int) -> int:
+    return v - (1 << 64) if v >= (1 << 63) else v
+
+
+def uuid_column(name, values, device=None) -> "Column":
+    """UUID strings -> a ``uuid`` column (two signed 64-bit halves per row, C16Chunk layout)."""
+    import uuid as _uuid
+    out = np.full((len(values), 2), _UUID_NA, dtype=np.int64)
+    for i, v in enumerate(values):
+        if v is None or (isinstance(v, float) and math.isnan(v)) or str(v).strip() == "":
+            continue
+        u = _uuid.UUID(str(v).strip()).int
+        out[i, 0], out[i, 1] = _signed(u >> 64), _signed(u & ((1 << 64) - 1))
+    return Column(name, "uuid", torch.as_tensor(out, device=device or engine_device()))
+
+
+def uuid_strings(data: torch.Tensor):
+    import uuid as _uuid
+    a = data.cpu().numpy()
+    out = np.empty(a.shape[0], dtype=object)
+    for i, (hi, lo) in enumerate(a.tolist()):
+        out[i] = None if hi == _UUID_NA and lo == _UUID_NA else str(_uuid.UUID(int=((hi % (1 << 64)) << 64) | (lo % (1 << 64))))
+    return out
+
+
+def looks_uuid(values) -> bool:
+    vals = [v for v in values if v is not None and not (isinstance(v, float) and math.isnan(v)) and str(v) != ""]
+    return bool(vals) and all(isinstance(v, str) and _UUID_RX.match(v.strip()) for v in vals)
 
 
 def _to_float(s):
@@ -132,6 +175,8 @@ def _infer_column(name, values, device, force_type=None) -> Column:
         return _enum_from_values(name, arr, device)
     if force_type == "string":
         return Column(name, "string", strings=np.array([None if _isnull(v) else str(v) for v in arr], dtype=object))
+    if force_type == "uuid":
+        return uuid_column(name, list(arr), device)
     if arr.dtype.kind in "biuf":
         t = "int" if arr.dtype.kind in "biu" else "real"
         if force_type == "time":

@@ -26,7 +26,7 @@ from ..frame import Column, H2OFrame, _enum_from_values, engine_device
 
 _TYPE_ALIASES = {"numeric": "real", "real": "real", "float": "real", "double": "real", "int": "int", "integer": "int",
                  "enum": "enum", "factor": "enum", "categorical": "enum", "string": "string", "str": "string",
-                 "time": "time", "date": "time", "uuid": "string"}
+                 "time": "time", "date": "time", "uuid": "uuid"}
 
 
 # ------------------------------------------------------------------------------------------------
@@ -544,12 +544,32 @@ def import_file(path=None, destination_frame=None, parse=True, header=0, sep=Non
         # non-CSV formats are read whole on every rank: keep this rank's rows
         frames = [fr if fr._shard is not None else dframe.shard_frame(fr) for fr in frames]
     out = frames[0] if len(frames) == 1 else _rbind_sharded(frames)
+    _detect_uuid(out, col_types)
     dest = destination_frame or _dest_name(files[0])
     from ..core import dkv
     dkv.remove(out.frame_id) if out.frame_id != dest and dkv.contains(out.frame_id) else None
     out.frame_id = dest
     dkv.put(dest, out)
     return out
+
+
+def _detect_uuid(fr, col_types=None):
+    """ParseSetup's UUID type: a string (or enum) column whose every value is a UUID becomes a ``uuid``
+    column (two int64 halves per row); an explicit ``col_types`` entry "uuid" forces it."""
+    from ..frame import looks_uuid, uuid_column
+    forced = set()
+    if isinstance(col_types, dict):
+        forced = {k for k, v in col_types.items() if str(v).lower() == "uuid"}
+    elif isinstance(col_types, (list, tuple)):
+        forced = {fr.names[i] for i, v in enumerate(col_types) if i < fr.ncols and str(v).lower() == "uuid"}
+    for n in list(fr.names):
+        c = fr._col(n)
+        if c.type not in ("string", "enum"):
+            continue
+        vals = c.to_numpy()
+        if n in forced or looks_uuid(vals[: 1000]) and looks_uuid(vals):
+            dev = c.data.device if c.data is not None else None
+            fr._cols[n] = uuid_column(n, list(vals), dev)
 
 
 def _rbind_sharded(frames):

@@ -203,8 +203,10 @@ def train(algo: str, params: dict, x=None, y=None, training_frame=None, validati
             fr = dframe.gather_frame(fr)
             validation_frame = dframe.gather_frame(validation_frame)
             mode.enter_context(coll.replicated())
+    from ..utils import memory
+    memory.pressure_check()
     with mode:
-        return _train(spec, algo, p, x, y, fr, validation_frame, job, model_id)
+        return memory.with_backpressure(_train, spec, algo, p, x, y, fr, validation_frame, job, model_id)
 
 
 _EXTRA = {}

@@ -84,6 +84,30 @@ def clean(target_fraction: float | None = None) -> int:
     return moved
 
 
+def pressure_check() -> int:
+    """Allocation back-pressure (MemoryManager.set_goals): called when frames enter the DKV and before
+    every model build; spills LRU frames once HBM usage crosses ``high_water``."""
+    if not torch.cuda.is_available():
+        return 0
+    u = device_usage()
+    if u["total"] and u["used"] / u["total"] > _state["high_water"]:
+        return clean()
+    return 0
+
+
+def with_backpressure(fn, *args, **kwargs):
+    """Run ``fn``; on a device out-of-memory error spill cold frames down to half of HBM, release the
+    caching allocator's blocks and retry once (the reference blocks allocations until the Cleaner
+    freed memory; here the retry happens after the spill)."""
+    try:
+        return fn(*args, **kwargs)
+    except torch.cuda.OutOfMemoryError:
+        _state["oom_retries"] = _state.get("oom_retries", 0) + 1
+        clean(0.5)
+        torch.cuda.empty_cache()
+        return fn(*args, **kwargs)
+
+
 def set_high_water(frac: float):
     _state["high_water"] = float(frac)
 

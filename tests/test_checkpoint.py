@@ -49,3 +49,24 @@ def test_deeplearning_checkpoint():
     c = DeepLearningTrainer(dict(hidden=[16], epochs=4, seed=1, checkpoint=a.key, mini_batch_size=32)).fit(X, y, None, None, info)
     assert abs(c.output["epochs"] - 4) < 0.1
     assert c.output["training_metrics"]["AUC"] >= a.output["training_metrics"]["AUC"] - 0.02
+
+
+def test_memory_backpressure_triggers(monkeypatch):
+    """MemoryManager back-pressure: over the high-water mark a DKV put / model build spills LRU frames,
+    and a device OOM inside a build spills then retries once."""
+    import torch
+    from llama_github_io_amd.utils import memory
+    calls = []
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
+    monkeypatch.setattr(memory, "device_usage", lambda device=None: dict(total=100, free=5, used=95, allocated=90))
+    monkeypatch.setattr(memory, "clean", lambda target=None: calls.append(target) or 7)
+    assert memory.pressure_check() == 7 and calls == [None]
+    n = {"i": 0}
+
+    def flaky():
+        n["i"] += 1
+        if n["i"] == 1:
+            raise torch.cuda.OutOfMemoryError("HIP out of memory")
+        return "ok"
+    monkeypatch.setattr(torch.cuda, "empty_cache", lambda: None)
+    assert memory.with_backpressure(flaky) == "ok" and n["i"] == 2 and calls[-1] == 0.5

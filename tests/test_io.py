@@ -39,3 +39,21 @@ def test_multi_file_import(tmp_path):
         (tmp_path / f"p{i}.csv").write_text(f"a,b\n{i},{i * 2}\n{i + 10},{i}\n")
     f = P.import_file(str(tmp_path))
     assert f.nrows == 6 and f.names == ["a", "b"]
+
+
+def test_uuid_columns(tmp_path):
+    """ParseSetup's UUID type (C16Chunk): a column of UUIDs parses to two int64 halves per row, prints
+    back as the same strings, survives row filters and is NA for empty cells."""
+    import uuid
+    import h2o
+    h2o.init(verbose=False)
+    us = [str(uuid.uuid5(uuid.NAMESPACE_DNS, f"row{i}")) for i in range(20)]
+    p = tmp_path / "u.csv"
+    p.write_text("id,x\n" + "\n".join(f"{u},{i}" for i, u in enumerate(us)) + "\n,99\n")
+    fr = h2o.import_file(str(p))
+    assert fr.types["id"] == "uuid"
+    vals = fr.as_data_frame()["id"].tolist()
+    assert vals[:20] == us and vals[20] is None
+    sub = fr[fr["x"] >= 18, :].as_data_frame()["id"].tolist()
+    assert sub == us[18:] + [None]
+    assert fr["id"].isna().as_data_frame().values.ravel().tolist()[-2:] == [0, 1]
