@@ -48,7 +48,8 @@ __device__ __forceinline__ void st(__hip_bfloat16* p, int64_t i, float v) { p[i]
 template <typename T>
 __global__ __launch_bounds__(256) void k_bias_act_fwd(const T* __restrict__ x, const float* __restrict__ b,
                                                       T* __restrict__ y, int64_t rows, int cols, int act,
-                                                      float drop, uint64_t seed) {
+                                                      float drop, uint64_t seed, const uint64_t* __restrict__ seed_dev) {
+  if (seed_dev) seed ^= *seed_dev * 0x9E3779B97F4A7C15ULL;   // per-step offset read on device (graph replays)
   const int64_t n = rows * (int64_t)cols;
   const float keep = 1.f - drop;
   const uint32_t thr = (uint32_t)(drop * 4294967296.0);
@@ -64,7 +65,9 @@ __global__ __launch_bounds__(256) void k_bias_act_fwd(const T* __restrict__ x, c
 template <typename T>
 __global__ __launch_bounds__(256) void k_bias_act_bwd(const T* __restrict__ gy, const T* __restrict__ y,
                                                       T* __restrict__ gx, float* __restrict__ db, int64_t rows,
-                                                      int cols, int act, float drop, uint64_t seed, int rows_per_block) {
+                                                      int cols, int act, float drop, uint64_t seed, int rows_per_block,
+                                                      const uint64_t* __restrict__ seed_dev) {
+  if (seed_dev) seed ^= *seed_dev * 0x9E3779B97F4A7C15ULL;
   // block handles a [rows_per_block x 64] column stripe: thread (ty, tx) with tx = column lane
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + tx;
@@ -129,32 +132,34 @@ int h2o_adadelta(float* p, const float* g, float* eg2, float* edx2, long long n,
 
 
 int h2o_bias_act_fwd(const void* x, const float* b, void* y, long long rows, int cols, int act, float drop,
-                     unsigned long long seed, int bf16, hipStream_t stream) {
+                     unsigned long long seed, const unsigned long long* seed_dev, int bf16, hipStream_t stream) {
   const long long n = rows * (long long)cols;
   int grid = (int)((n + 255) / 256);
   if (grid > 8192) grid = 8192;
   if (grid < 1) grid = 1;
   if (bf16)
     hipLaunchKernelGGL(k_bias_act_fwd<__hip_bfloat16>, dim3(grid), dim3(256), 0, stream, (const __hip_bfloat16*)x, b,
-                       (__hip_bfloat16*)y, (int64_t)rows, cols, act, drop, seed);
+                       (__hip_bfloat16*)y, (int64_t)rows, cols, act, drop, seed, (const uint64_t*)seed_dev);
   else
     hipLaunchKernelGGL(k_bias_act_fwd<float>, dim3(grid), dim3(256), 0, stream, (const float*)x, b, (float*)y,
-                       (int64_t)rows, cols, act, drop, seed);
+                       (int64_t)rows, cols, act, drop, seed, (const uint64_t*)seed_dev);
   return (int)hipGetLastError();
 }
 
 int h2o_bias_act_bwd(const void* gy, const void* y, void* gx, float* db, long long rows, int cols, int act,
-                     float drop, unsigned long long seed, int bf16, hipStream_t stream) {
+                     float drop, unsigned long long seed, const unsigned long long* seed_dev, int bf16,
+                     hipStream_t stream) {
   // enough row stripes to fill the chip: a [4096 x 200] mini-batch was 64 blocks (22.8 us); stripes of
   // 32 rows give 512 blocks (the per-stripe bias partial is one atomic per column)
   const int rpb = rows >= (1 << 16) ? 256 : 32;
   dim3 grid((cols + 63) / 64, (unsigned)((rows + rpb - 1) / rpb));
   if (bf16)
     hipLaunchKernelGGL(k_bias_act_bwd<__hip_bfloat16>, grid, dim3(256), 0, stream, (const __hip_bfloat16*)gy,
-                       (const __hip_bfloat16*)y, (__hip_bfloat16*)gx, db, (int64_t)rows, cols, act, drop, seed, rpb);
+                       (const __hip_bfloat16*)y, (__hip_bfloat16*)gx, db, (int64_t)rows, cols, act, drop, seed, rpb,
+                       (const uint64_t*)seed_dev);
   else
     hipLaunchKernelGGL(k_bias_act_bwd<float>, grid, dim3(256), 0, stream, (const float*)gy, (const float*)y,
-                       (float*)gx, db, (int64_t)rows, cols, act, drop, seed, rpb);
+                       (float*)gx, db, (int64_t)rows, cols, act, drop, seed, rpb, (const uint64_t*)seed_dev);
   return (int)hipGetLastError();
 }
 

@@ -22,7 +22,7 @@ import numpy as np
 import torch
 
 from .. import metrics as mm
-from ..ops.dense import ACT, bias_act
+from ..ops.dense import ACT, bias_act, step_seed
 from ..parallel import collectives as coll
 from .params import canon
 from .base import DataInfo, Model, ScoreKeeper, make_key, model_category
@@ -62,6 +62,7 @@ class MLP(torch.nn.Module):
         self.out = torch.nn.Linear(dims[-1], n_out)
         self._init(self.out, dims[-1], n_out, init_dist, init_scale, gen)
         self.step = 0
+        self.step_dev = None
 
     @staticmethod
     def _init(lin, fan_in, fan_out, dist, scale, gen):
@@ -92,7 +93,11 @@ class MLP(torch.nn.Module):
             else:
                 # bf16 GEMM outputs stay bf16 through the fused epilogue into the next GEMM (no fp32 round trip)
                 xin = h if (h.is_cuda and h.dtype == torch.bfloat16) else h.float()
-                x = bias_act(xin, lin.bias, self.act, drop, (seed * 1000003 + i * 7919 + self.step) & ((1 << 62) - 1))
+                base = (seed * 1000003 + i * 7919) & ((1 << 62) - 1)
+                if self.step_dev is not None:      # captured step: the kernels read the step counter on device
+                    x = bias_act(xin, lin.bias, self.act, drop, base, self.step_dev)
+                else:
+                    x = bias_act(xin, lin.bias, self.act, drop, step_seed(base, self.step))
             if features_layer is not None and i == features_layer:
                 return x
         return self.out(x)
@@ -272,6 +277,7 @@ class DeepLearningTrainer:
             # ~1024 updates per epoch: ADADELTA starts from zero step sizes, so a small frame trained in a
             # handful of large batches would barely move (the reference does one update per row)
             B = max(1, min(int(p["gpu_batch_size"]), N_glob // 1024))
+        B = max(1, min(B, N_glob))
         from ..ops.dense import FlatParams
         fp = FlatParams(net)                 # params/grads as views of two flat buffers
         params = fp.params
@@ -280,6 +286,7 @@ class DeepLearningTrainer:
         rho, eps = float(p["rho"]), float(p["epsilon"])
         l1, l2 = float(p["l1"]), float(p["l2"])
         max_w2 = float(p["max_w2"])
+        nesterov = bool(p["nesterov_accelerated_gradient"])
         keeper = ScoreKeeper(p["stopping_rounds"], p["stopping_metric"], p["stopping_tolerance"],
                              "Regression" if ae else cat)
         epochs = float(p["epochs"]) - prev_epochs
@@ -289,112 +296,162 @@ class DeepLearningTrainer:
         samples = 0
         last_score = time.time()
         dtype = torch.bfloat16 if str(p["compute_dtype"]).lower() in ("bf16", "bfloat16") else None
-        perm = None
-        pos = N_glob
         wf = w.float()
-        # hipGraph capture of the whole training step (fwd + bwd + fused ADADELTA): the step is a fixed
-        # launch sequence on static buffers, so replaying it removes the per-kernel launch overhead that
-        # dominates small-batch MLP training. Eager path for dropout / momentum / max_w2 / multi-rank.
-        use_graph = (dev.type == "cuda" and adaptive and not sharded and float(p["input_dropout_ratio"]) == 0
-                     and all(float(v) == 0 for v in hd) and max_w2 == float("inf") and N >= B
-                     and os.environ.get("H2O_DL_GRAPH", "1") == "1")
-        graph = None
-        if use_graph:
-            sx = torch.empty(B, Z.shape[1], dtype=Z.dtype, device=dev)
-            sw = torch.empty(B, dtype=wf.dtype, device=dev)
-            sy = None if ae else torch.empty((B,) + tuple(yt.shape[1:]), dtype=yt.dtype, device=dev)
-            side = torch.cuda.Stream(dev)
-
-            def graph_step():
-                fp.zero_grad()
-                with torch.autocast(device_type="cuda", dtype=dtype, enabled=dtype is not None):
-                    o = net(sx, seed)
-                ls = self._loss(o.float(), sx if ae else sy, sw, cat, dist, ae) / sw.sum().clamp(min=1e-12)
-                ls.backward()
-                with torch.no_grad():
-                    fp.adadelta(rho, eps, l1, l2)
+        # per-step scalars live on the device so one captured step serves every step
+        step_t = torch.zeros(1, dtype=torch.int64, device=dev)
+        rate_t = torch.zeros((), dtype=torch.float32, device=dev)
+        mom_t = torch.zeros((), dtype=torch.float32, device=dev)
+        on_t = torch.zeros((), dtype=torch.float32, device=dev)
         gbuf = torch.empty(fp.g.numel() + 1, dtype=fp.g.dtype, device=fp.g.device) if sharded else None
-        # overwrite_with_best_model (default true, off with n-fold CV): the final weights are those of the
-        # scoring event with the lowest Model.loss() (stopping metric; AUTO = logloss / deviance / MSE)
+        tdim = tuple(yt.shape[1:]) if yt is not None else ()
+
+        def fwd_bwd(xb, wb, tb):
+            """Forward + backward of one (local) batch into fp.g: the gradient of the weighted loss sum,
+            normalised by the batch weight (single process) or raw + batch weight in gbuf (sharded)."""
+            fp.zero_grad()
+            with torch.autocast(device_type=dev.type, dtype=dtype, enabled=dtype is not None):
+                o = net(xb, seed)
+            ls = self._loss(o.float(), xb if ae else tb, wb, cat, dist, ae)
+            if sharded:
+                ls.backward()
+                gbuf[:-1].copy_(fp.g)
+                gbuf[-1:].copy_(wb.sum().view(1))
+            else:
+                (ls / wb.sum().clamp(min=1e-12)).backward()
+
+        def update():
+            """Optimizer step on the flat buffers (ADADELTA: one fused HIP launch; momentum SGD with rate
+            annealing / Nesterov from the device scalars rate_t, mom_t, on_t), then max_w2 row clipping."""
+            with torch.no_grad():
+                if sharded:       # data parallel: the all-reduced [sum-gradient, batch weight] -> mean gradient
+                    fp.g.copy_(gbuf[:-1] / gbuf[-1].clamp(min=1e-12))
+                if adaptive:      # ADADELTA (Neurons.java: rho, epsilon)
+                    fp.adadelta(rho, eps, l1, l2)
+                else:
+                    gg = fp.g.clone()
+                    nd = fp.n_decay
+                    if l2 > 0 or l1 > 0:
+                        gg[:nd] += l2 * fp.p[:nd] + l1 * torch.sign(fp.p[:nd])
+                    upd = gg * -rate_t
+                    mom.mul_(mom_t).add_(upd * on_t)
+                    if nesterov:
+                        fp.p.add_(mom * mom_t + upd)
+                    else:
+                        fp.p.add_(mom * on_t + upd * (1 - on_t))
+                if max_w2 < float("inf"):
+                    for q in params:
+                        if q.dim() > 1:
+                            n2 = (q * q).sum(1, keepdim=True)
+                            q.mul_(torch.where(n2 > max_w2, torch.sqrt(max_w2 / n2), torch.ones_like(n2)))
+
+        # hipGraph capture of the training step (fwd + bwd (+ update)): a fixed launch sequence on static
+        # batch buffers, replayed per step. Row-sharded runs capture fwd+bwd and the update separately with
+        # the one flat gradient all-reduce between them; their local batch buffer is sized to the largest
+        # per-rank share of a global batch in the epoch (padding rows carry weight 0).
+        use_graph = dev.type == "cuda" and os.environ.get("H2O_DL_GRAPH", "1") == "1"
+        net.step_dev = step_t if use_graph else None
+        gstate = dict(cap=0, g1=None, g2=None, warm=0)
+        sx = sw = sy = None
+        side = torch.cuda.Stream(dev) if use_graph else None
+
+        def alloc(cap):
+            nonlocal sx, sw, sy
+            sx = torch.zeros(cap, Z.shape[1], dtype=Z.dtype, device=dev)
+            sw = torch.zeros(cap, dtype=wf.dtype, device=dev)
+            sy = None if ae else torch.zeros((cap,) + tdim, dtype=yt.dtype, device=dev)
+            gstate.update(cap=cap, g1=None, g2=None, warm=0)
+
+        def run_step():
+            if gstate["warm"] < 2:      # warm-up steps on a side stream before capture (allocator, libraries)
+                side.wait_stream(torch.cuda.current_stream(dev))
+                with torch.cuda.stream(side):
+                    fwd_bwd(sx, sw, sy)
+                    if not sharded:
+                        update()
+                torch.cuda.current_stream(dev).wait_stream(side)
+                gstate["warm"] += 1
+                if sharded:
+                    coll.all_reduce_(gbuf)
+                    update()
+                return
+            if gstate["g1"] is None:
+                try:
+                    g1 = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g1):
+                        fwd_bwd(sx, sw, sy)
+                        if not sharded:
+                            update()
+                    g2 = None
+                    if sharded:
+                        g2 = torch.cuda.CUDAGraph()
+                        with torch.cuda.graph(g2):
+                            update()
+                    gstate.update(g1=g1, g2=g2)
+                except Exception:  # noqa: BLE001 - capture unsupported here: eager steps on the static buffers
+                    gstate.update(g1=False)
+            if gstate["g1"] is False:
+                fwd_bwd(sx, sw, sy)
+                if sharded:
+                    coll.all_reduce_(gbuf)
+                update()
+                return
+            gstate["g1"].replay()
+            if sharded:
+                coll.all_reduce_(gbuf)
+                gstate["g2"].replay()
+
+        # global row order per epoch: mini-batches are consecutive B-slices of a permutation of the GLOBAL
+        # rows; under row sharding each rank takes the members of the batch it owns (one host sync per
+        # epoch for the per-step counts), so the summed gradient is the single-process one
+        S_ep = N_glob // B
+        perm = None
+        sel = offs = None
+        s_in = S_ep
         owb = bool(p.get("overwrite_with_best_model", True)) and not int(p.get("nfolds") or 0)
         best_loss, best_p, last_ev = float("inf"), None, {}
         for step in range(total):
-            if pos + B > N_glob:
-                # mini-batches are drawn from the GLOBAL row order: under row sharding each rank takes the
-                # members of the batch it owns, so the summed gradient is the single-process one
-                perm = torch.randperm(N_glob, generator=g).to(dev) if p["shuffle_training_data"] or True else torch.arange(N_glob, device=dev)
-                pos = 0
-            idx = perm[pos:pos + B]
-            pos += B
+            if s_in >= S_ep:
+                perm = torch.randperm(N_glob, generator=g).to(dev)
+                s_in = 0
+                if sharded:
+                    mine = (perm >= row0) & (perm < row0 + N)
+                    mine[S_ep * B:] = False
+                    sel = torch.nonzero(mine).squeeze(1)
+                    cnt = torch.bincount(sel // B, minlength=S_ep)[:S_ep].cpu()
+                    offs = [0] + np.cumsum(cnt.numpy()).tolist()
+                    cmax = int(cnt.max()) if S_ep > 0 else 0
+                    if use_graph and cmax > gstate["cap"]:
+                        alloc(max(64, (cmax + 63) // 64 * 64))
+                elif use_graph and gstate["cap"] != B:
+                    alloc(B)
             if sharded:
-                idx = idx[(idx >= row0) & (idx < row0 + N)] - row0
+                rows = perm[sel[offs[s_in]:offs[s_in + 1]]] - row0
+            else:
+                rows = perm[s_in * B:(s_in + 1) * B]
+            s_in += 1
             net.train()
             net.step = step
+            samples += B
+            if not adaptive:
+                m = self._momentum(samples)
+                rate_t.fill_(float(p["rate"]) / (1 + float(p["rate_annealing"]) * samples))
+                mom_t.fill_(m)
+                on_t.fill_(1.0 if m > 0 else 0.0)
             if use_graph:
-                torch.index_select(Z, 0, idx, out=sx)
-                torch.index_select(wf, 0, idx, out=sw)
+                c = rows.numel()
+                torch.index_select(Z, 0, rows, out=sx[:c])
+                torch.index_select(wf, 0, rows, out=sw[:c])
+                if c < sw.numel():
+                    sw[c:].zero_()
                 if sy is not None:
-                    torch.index_select(yt, 0, idx, out=sy)
-                if graph is None and step < 3:          # warm-up steps on a side stream before capture
-                    side.wait_stream(torch.cuda.current_stream(dev))
-                    with torch.cuda.stream(side):
-                        graph_step()
-                    torch.cuda.current_stream(dev).wait_stream(side)
-                else:
-                    if graph is None:
-                        try:
-                            graph = torch.cuda.CUDAGraph()
-                            with torch.cuda.graph(graph):
-                                graph_step()
-                        except Exception:  # noqa: BLE001 - capture unsupported: fall back to eager replay
-                            graph = False
-                    if graph is False:
-                        graph_step()
-                    else:
-                        graph.replay()
-                samples += B
+                    torch.index_select(yt, 0, rows, out=sy[:c])
+                step_t.fill_(step)
+                run_step()
             else:
-                xb = Z.index_select(0, idx)
-                wb = wf.index_select(0, idx)
-                with torch.autocast(device_type=dev.type, dtype=dtype, enabled=dtype is not None):
-                    out = net(xb, seed)
-                out = out.float()
-                loss = self._loss(out, xb if ae else yt.index_select(0, idx), wb, cat, dist, ae)
-                fp.zero_grad()
+                fwd_bwd(Z.index_select(0, rows), wf.index_select(0, rows), None if ae else yt.index_select(0, rows))
                 if sharded:
-                    # data parallel: ONE all-reduce per step of [sum-gradient, batch weight]; the gradient
-                    # is normalised by the GLOBAL batch weight afterwards
-                    loss.backward()
-                    gbuf[:-1].copy_(fp.g)
-                    gbuf[-1] = wb.sum()
                     coll.all_reduce_(gbuf)
-                    fp.g.copy_(gbuf[:-1] / gbuf[-1].clamp(min=1e-12))
-                else:
-                    (loss / wb.sum().clamp(min=1e-12)).backward()   # accumulates into the flat gradient buffer
-                with torch.no_grad():
-                    samples += B
-                    if adaptive:                 # ADADELTA (Neurons.java: rho, epsilon), one fused HIP launch
-                        fp.adadelta(rho, eps, l1, l2)
-                    else:
-                        rate = float(p["rate"]) / (1 + float(p["rate_annealing"]) * samples)
-                        m = self._momentum(samples)
-                        gg = fp.g.clone()
-                        nd = fp.n_decay
-                        if l2 > 0 or l1 > 0:
-                            gg[:nd] += l2 * fp.p[:nd] + l1 * torch.sign(fp.p[:nd])
-                        if m > 0:
-                            mom.mul_(m).add_(gg, alpha=-rate)
-                            if p["nesterov_accelerated_gradient"]:
-                                fp.p.add_(mom, alpha=m).add_(gg, alpha=-rate)
-                            else:
-                                fp.p.add_(mom)
-                        else:
-                            fp.p.add_(gg, alpha=-rate)
-                    if max_w2 < float("inf"):
-                        for q in params:
-                            if q.dim() > 1:
-                                n2 = (q * q).sum(1, keepdim=True)
-                                q.mul_(torch.where(n2 > max_w2, torch.sqrt(max_w2 / n2), torch.ones_like(n2)))
+                update()
             if self.job is not None and step % 50 == 0:
                 self.job.set_progress(step / max(total, 1))
             end = step == total - 1
@@ -415,6 +472,7 @@ class DeepLearningTrainer:
                     break
                 if float(p["max_runtime_secs"] or 0) > 0 and coll.agree(time.time() - t0 > float(p["max_runtime_secs"])):
                     break
+        net.step_dev = None
         if owb and best_p is not None:
             final = self._model_loss(last_ev.get("_valid") or last_ev.get("_train"), cat, ae)
             if best_loss < final:

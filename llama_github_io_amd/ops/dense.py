@@ -17,9 +17,9 @@ ACT = {"linear": 0, "rectifier": 1, "relu": 1, "tanh": 2, "exprectifier": 3, "el
 
 nat.register_hip_signatures({
     "h2o_bias_act_fwd": [nat.c_void_p, nat.c_void_p, nat.c_void_p, nat.c_ll, nat.c_int, nat.c_int, nat.ctypes.c_float,
-                         nat.c_ull, nat.c_int, nat.c_void_p],
+                         nat.c_ull, nat.c_void_p, nat.c_int, nat.c_void_p],
     "h2o_bias_act_bwd": [nat.c_void_p, nat.c_void_p, nat.c_void_p, nat.c_void_p, nat.c_ll, nat.c_int, nat.c_int,
-                         nat.ctypes.c_float, nat.c_ull, nat.c_int, nat.c_void_p],
+                         nat.ctypes.c_float, nat.c_ull, nat.c_void_p, nat.c_int, nat.c_void_p],
     "h2o_kmeans_assign": [nat.c_void_p, nat.c_ll, nat.c_int, nat.c_void_p, nat.c_int, nat.c_void_p, nat.c_void_p, nat.c_void_p],
     "h2o_kmeans_step": [nat.c_void_p, nat.c_ll, nat.c_int, nat.c_void_p, nat.c_int, nat.c_void_p, nat.c_void_p,
                         nat.c_void_p, nat.c_void_p, nat.c_void_p],
@@ -70,6 +70,13 @@ class FlatParams:
         self.p.add_(d)
 
 _M = (1 << 64) - 1
+_GOLD = 0x9E3779B97F4A7C15
+
+
+def step_seed(seed: int, step: int) -> int:
+    """Dropout seed of one training step: ``seed ^ step * golden`` (mod 2^64), the same mixing the kernels
+    apply to a device-resident step counter (``seed_dev``) so graph replays draw fresh masks."""
+    return (int(seed) ^ (int(step) * _GOLD)) & _M
 
 
 def _mask_ref(shape, drop, seed, device):
@@ -101,7 +108,7 @@ def _act(a, v):
 
 class BiasAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, b, act: int, drop: float, seed: int):
+    def forward(ctx, x, b, act: int, drop: float, seed: int, seed_dev=None):
         x = x.contiguous()
         rows, cols = x.shape
         if x.is_cuda:
@@ -110,13 +117,16 @@ class BiasAct(torch.autograd.Function):
             y = torch.empty_like(x)          # bf16 in -> bf16 out (fp32 bias and math inside the kernel)
             bb = None if b is None else b.float().contiguous()
             nat.call("h2o_bias_act_fwd", x.data_ptr(), 0 if bb is None else bb.data_ptr(), y.data_ptr(), rows, cols,
-                     act, float(drop), seed & _M, int(x.dtype == torch.bfloat16), nat.stream_ptr(x.device))
+                     act, float(drop), seed & _M, 0 if seed_dev is None else seed_dev.data_ptr(),
+                     int(x.dtype == torch.bfloat16), nat.stream_ptr(x.device))
         else:
+            if seed_dev is not None:
+                seed = step_seed(seed, int(seed_dev.item()))
             y = _act(act, x + (b if b is not None else 0))
             if drop > 0:
                 y = torch.where(_mask_ref(y.shape, drop, seed, y.device), y / (1 - drop), torch.zeros_like(y))
         ctx.save_for_backward(y)
-        ctx.act, ctx.drop, ctx.seed, ctx.has_b = act, drop, seed, b is not None
+        ctx.act, ctx.drop, ctx.seed, ctx.has_b, ctx.seed_dev = act, drop, seed, b is not None, seed_dev
         return y
 
     @staticmethod
@@ -130,7 +140,8 @@ class BiasAct(torch.autograd.Function):
             gx = torch.empty_like(y)
             db = torch.zeros(cols, dtype=torch.float32, device=y.device) if ctx.has_b else None
             nat.call("h2o_bias_act_bwd", gy.data_ptr(), y.data_ptr(), gx.data_ptr(), 0 if db is None else db.data_ptr(),
-                     rows, cols, act, float(drop), seed & _M, int(y.dtype == torch.bfloat16), nat.stream_ptr(y.device))
+                     rows, cols, act, float(drop), seed & _M, 0 if ctx.seed_dev is None else ctx.seed_dev.data_ptr(),
+                     int(y.dtype == torch.bfloat16), nat.stream_ptr(y.device))
         else:
             yy, g = y, gy
             if drop > 0:
@@ -147,12 +158,14 @@ class BiasAct(torch.autograd.Function):
                 d = torch.ones_like(yy)
             gx = g * d
             db = gx.sum(0) if ctx.has_b else None
-        return gx, db, None, None, None
+        return gx, db, None, None, None, None
 
 
-def bias_act(x, b, act: str | int = "rectifier", drop: float = 0.0, seed: int = 0):
+def bias_act(x, b, act: str | int = "rectifier", drop: float = 0.0, seed: int = 0, seed_dev=None):
+    """``seed_dev`` (CUDA int64 [1], optional): per-step counter read by the kernels and mixed into ``seed``
+    (``step_seed``), so a captured hipGraph draws a new dropout mask on every replay."""
     a = ACT[act.lower()] if isinstance(act, str) else int(act)
-    return BiasAct.apply(x, b, a, float(drop), int(seed))
+    return BiasAct.apply(x, b, a, float(drop), int(seed), seed_dev)
 
 
 def _mfma_shape(K, P):

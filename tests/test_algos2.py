@@ -45,9 +45,12 @@ def test_naivebayes_dt_psvm_rulefit(df):
                   (H2OSupportVectorMachineEstimator, dict(gamma=0.5)),
                   (H2ORuleFitEstimator, dict(rule_generation_ntrees=6, max_num_rules=5, seed=1))):
         m = E(**kw)
-        m.train(x=["a", "b", "c"], y="y", training_frame=df)
+        # DT.dtChecks: categorical features are refused, as in the reference
+        m.train(x=["a", "b"] if E is H2ODecisionTreeEstimator else ["a", "b", "c"], y="y", training_frame=df)
         auc = m._model.output["training_metrics"]["AUC"]
         assert auc > 0.8, (E.__name__, auc)
+    with pytest.raises(Exception, match="Categorical features are not supported yet"):
+        H2ODecisionTreeEstimator().train(x=["a", "c"], y="y", training_frame=df)
 
 
 def test_isotonic_gam_anova_modelselection(df):

@@ -201,7 +201,12 @@ def test_kmeans_mfma_lloyd_matches_fp32_reference(N, K, P, weighted, monkeypatch
     assert torch.allclose(sums, ref, rtol=1e-4, atol=1e-2) and torch.allclose(cnt, cref, rtol=1e-5, atol=1e-3)
 
 
-def test_deeplearning_graph_matches_eager(monkeypatch):
+@pytest.mark.parametrize("extra", [{}, dict(activation="RectifierWithDropout", hidden_dropout_ratios=[0.3, 0.2]),
+                                   dict(adaptive_rate=False, rate=0.01, momentum_start=0.5, momentum_stable=0.9,
+                                        momentum_ramp=5000, max_w2=2.0, l2=1e-4)])
+def test_deeplearning_graph_matches_eager(extra, monkeypatch):
+    # the captured step (device step counter for the dropout hash, device rate / momentum scalars) replays
+    # exactly what the eager loop computes step by step
     from llama_github_io_amd.models.deeplearning import DeepLearningTrainer
     g = torch.Generator(device=dev).manual_seed(0)
     X = torch.randn(6, 8192, device=dev, generator=g)
@@ -209,8 +214,8 @@ def test_deeplearning_graph_matches_eager(monkeypatch):
     res = []
     for flag in ("0", "1"):
         monkeypatch.setenv("H2O_DL_GRAPH", flag)
-        m = DeepLearningTrainer(dict(hidden=[32, 32], epochs=2, seed=3, mini_batch_size=512, score_interval=1e9,
-                                     stopping_rounds=0)).fit(X, y, None, None, _info(6))
+        m = DeepLearningTrainer(dict(dict(hidden=[32, 32], epochs=2, seed=3, mini_batch_size=512, score_interval=1e9,
+                                          stopping_rounds=0), **extra)).fit(X, y, None, None, _info(6))
         res.append(torch.cat([q.detach().reshape(-1) for q in m.net.parameters()]).cpu())
     assert torch.allclose(res[0], res[1], atol=1e-5, rtol=1e-4)
 
