@@ -140,6 +140,10 @@ class GenericModel(Model):
             m.meta_transform = ki.get("metalearner_transform", "NONE")
             if m.info.response_domain is None and m.meta.info.response_domain is not None:
                 m.info.response_domain = list(m.meta.info.response_domain)   # out-of-range domain entry
+        elif algo == "rulefit":
+            m.rulefit = A.load_rulefit(ki)
+            m.glm_sub = GenericModel.from_mojo(path, m.rulefit["linear_key"],
+                                               prefix + ki.get("submodel_dir_0", f"models/{m.rulefit['linear_key']}/"))
         else:
             raise NotImplementedError(f"MOJO algo {algo} not supported by this reader")
         return m
@@ -348,6 +352,9 @@ class GenericModel(Model):
         if algo == "coxph":
             from ..mojo import algos as A
             return A.score_coxph(self.cox, X)
+        if algo == "rulefit":
+            from ..mojo import algos as A
+            return A.score_rulefit(self.rulefit, self.glm_sub, X, self.info)
         if algo == "stackedensemble":
             cols = []
             K = len(self.info.response_domain or []) if cat == "Multinomial" else 1

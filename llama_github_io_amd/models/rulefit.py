@@ -1,16 +1,21 @@
-"""RuleFit (reference: ``hex/rulefit/RuleFit.java``, ``RuleFitModel.java``, ``Rule.java``, ``Condition.java``).
+"""RuleFit (reference: ``hex/rulefit/RuleFit.java``, ``RuleFitModel.java``, ``Rule.java``, ``Condition.java``,
+``RuleEnsemble.java``, ``RuleFitUtils.java``; scoring as ``hex/genmodel/algos/rulefit/*``).
 
-1. Rule generation: tree ensembles (DRF by default, or GBM) with depths ``min_rule_length`` ..
-   ``max_rule_length``, ``rule_generation_ntrees`` trees in total.
-2. Every non-root node of every tree is a rule = conjunction of the conditions on its path; rule
-   membership of all rows is computed on device level by level (parent mask & split test).
-3. A Lasso GLM (``lambda`` or lambda search, ``alpha``=1) is fit on the 0/1 rule matrix (plus the
-   standardized linear terms for ``model_type='rules_and_linear'``); non-zero coefficients form the
-   ``rule_importance`` table (rule text, coefficient, support). Duplicate rules are removed.
+1. Rule generation: one tree ensemble per depth ``min_rule_length .. max_rule_length`` (DRF by default, or
+   GBM), each with ``rule_generation_ntrees`` trees, trained on the device tree engine.
+2. Every LEAF of every tree is a rule ``M<model>T<tree>N<node>`` (``_<class>`` per multinomial class tree):
+   the conditions on its root path, one per (feature, operator) — the one closest to the leaf — sorted by
+   feature name (``Rule.extractRulesFromTree`` / ``traversePath``).
+3. The linear model's input has one CATEGORICAL column per tree (``M<i>T<j>``, or ``M<i>T<j>C<k>``) whose
+   level is the last rule of that tree the row satisfies (``RuleEnsemble.createGLMTrainFrame`` + ``Decoder``),
+   plus ``linear.<x>`` copies of the predictors for ``rules_and_linear`` / ``linear``.
+4. A Lasso GLM (alpha 1; ``max_num_rules`` -> ``max_active_predictors``) on that frame; rules with non-zero
+   coefficients form ``rule_importance`` (duplicate conditions merged when ``remove_duplicates``).
+
+Rule membership is evaluated on the device for all rows at once (one boolean tensor per condition).
 """
 from __future__ import annotations
 
-import math
 import time
 
 import numpy as np
@@ -23,88 +28,183 @@ RF_DEFAULTS = dict(algorithm="AUTO", min_rule_length=3, max_rule_length=3, max_n
                    distribution="AUTO", seed=-1)
 
 
-def _node_masks(tree, X):
-    """Row membership for every node: list (node id -> bool [N]) and condition text per node."""
-    N = X.shape[1]
-    masks = {0: torch.ones(N, dtype=torch.bool, device=X.device)}
-    conds = {0: []}
-    order = [0]
-    for i in order:
-        f = int(tree.feat[i])
-        if f < 0:
-            continue
-        x = X[f]
-        na = torch.isnan(x)
-        if tree.is_cat[i]:
-            words = torch.as_tensor(tree.cat_bits[i].astype(np.int64), device=X.device)
-            code = torch.nan_to_num(x, nan=-1).long()
-            inr = (code >= 0) & (code < int(tree.cat_nbits[i]))
-            bit = (words[(code.clamp(min=0) >> 5).clamp(max=words.numel() - 1)] >> (code.clamp(min=0) & 31)) & 1
-            go = torch.where(inr, bit.bool(), torch.full_like(na, bool(tree.na_left[i])))
-            cl = ("in", f, tree.cat_bits[i], int(tree.cat_nbits[i]), bool(tree.na_left[i]))
+class Condition:
+    """One rule condition (``Condition.java``): numeric ``<`` / ``>=`` threshold or categorical ``in`` levels,
+    with ``nas_included`` for missing values."""
+
+    def __init__(self, feat, name, ctype, op, thr=-1.0, levels=None, level_names=None, nas=False):
+        self.feat, self.name, self.ctype, self.op = int(feat), name, ctype, op
+        self.thr = float(thr)
+        self.levels = list(levels or [])
+        self.level_names = list(level_names or [])
+        self.nas = bool(nas)
+
+    def text(self) -> str:
+        """Condition.constructLanguageCondition."""
+        s = f"({self.name}"
+        if self.op == "<":
+            s += f" < {_jfloat(self.thr)}"
+        elif self.op == ">=":
+            s += f" >= {_jfloat(self.thr)}"
         else:
-            go = x < float(tree.thr[i])
-            cl = ("<", f, float(tree.thr[i]), bool(tree.na_left[i]))
-        go = torch.where(na, torch.full_like(go, bool(tree.na_left[i])), go)
-        L, R = int(tree.left[i]), int(tree.right[i])
-        masks[L] = masks[i] & go
-        masks[R] = masks[i] & ~go
-        conds[L] = conds[i] + [(cl, True)]
-        conds[R] = conds[i] + [(cl, False)]
-        order += [L, R]
-    return masks, conds
+            s += " in {" + ", ".join(self.level_names) + "}"
+        if self.nas:
+            s += f" or {self.name} is NA"
+        return s + ")"
+
+    def holds(self, X: torch.Tensor) -> torch.Tensor:
+        """Condition.map over all rows (X [F, N])."""
+        x = X[self.feat].double()
+        na = torch.isnan(x)
+        if self.ctype == "num":
+            ok = (x < self.thr) if self.op == "<" else (x >= self.thr)
+        else:
+            lv = torch.as_tensor(self.levels, dtype=torch.float64, device=x.device)
+            ok = (x[:, None] == lv[None, :]).any(1) if lv.numel() else torch.zeros_like(na)
+        return torch.where(na, torch.full_like(na, self.nas), ok & ~na)
+
+    def to_state(self):
+        return [self.feat, self.name, self.ctype, self.op, self.thr, self.levels, self.level_names, self.nas]
+
+    @staticmethod
+    def from_state(s):
+        return Condition(*s)
 
 
-def _cond_text(c, left, names, domains):
-    kind = c[0]
-    f = c[1]
-    if kind == "<":
-        op = "<" if left else ">="
-        na = " or NA" if c[3] == left else ""
-        return f"({names[f]} {op} {c[2]:.6g}{na})"
-    words, nl = c[2], c[3]
-    levels = [domains[f][lv] if domains[f] and lv < len(domains[f]) else str(lv)
-              for lv in range(nl) if bool((int(words[lv >> 5]) >> (lv & 31)) & 1) == left]
-    return f"({names[f]} in {{{', '.join(levels)}}})"
+def _jfloat(v: float) -> str:
+    """Java ``Double.toString`` (thresholds are float32 split values widened to double)."""
+    v = float(v)
+    if v != v or v in (float("inf"), float("-inf")):
+        return {True: "NaN"}.get(v != v, "Infinity" if v > 0 else "-Infinity")
+    if v == 0 or 1e-3 <= abs(v) < 1e7:
+        r = repr(v)
+        return r if "." in r else r + ".0"
+    mant, exp = np.format_float_scientific(v, unique=True, trim="-").split("e")
+    if "." not in mant:
+        mant += ".0"
+    return f"{mant}E{int(exp)}"
+
+
+class Rule:
+    def __init__(self, conds, pred, var, coef=0.0, support=float("nan")):
+        self.conds, self.pred, self.var = conds, float(pred), var
+        self.coef, self.support = float(coef), float(support)
+
+    def text(self) -> str:
+        """Rule.generateLanguageRule."""
+        return " & ".join(c.text() for c in self.conds)
+
+    def holds(self, X):
+        m = torch.ones(X.shape[1], dtype=torch.bool, device=X.device)
+        for c in self.conds:
+            m &= c.holds(X)
+        return m
+
+    def to_state(self):
+        return [[c.to_state() for c in self.conds], self.pred, self.var, self.coef, self.support]
+
+    @staticmethod
+    def from_state(s):
+        return Rule([Condition.from_state(c) for c in s[0]], s[1], s[2], s[3], s[4])
+
+
+def leaf_rules(tree, mid: int, tj: int, names, domains, cls_suffix: str = ""):
+    """Rules of every leaf of one tree, in node order (Rule.extractRulesFromTree)."""
+    n = tree.n_nodes
+    parent = np.full(n, -1, np.int64)
+    for i in range(n):
+        if tree.feat[i] >= 0:
+            parent[tree.left[i]] = i
+            parent[tree.right[i]] = i
+    rules = []
+    for leaf in range(n):
+        if tree.feat[leaf] >= 0:
+            continue
+        conds, seen = [], set()
+        node = leaf
+        while parent[node] >= 0:                # leaf -> root: the first condition per (feature, op) is kept
+            p = parent[node]
+            f = int(tree.feat[p])
+            is_left = tree.left[p] == node
+            nas = bool(tree.na_left[p]) == bool(is_left)
+            if tree.is_cat[p]:
+                dom = domains[f] or []
+                bits, nb = tree.cat_bits[p], int(tree.cat_nbits[p])
+                lv = [lvl for lvl in range(len(dom))
+                      if ((lvl < nb and bool((int(bits[lvl >> 5]) >> (lvl & 31)) & 1)) or
+                          (lvl >= nb and bool(tree.na_left[p]))) == bool(is_left)]
+                c = Condition(f, names[f], "cat", "in", -1.0, lv, [dom[v] for v in lv], nas)
+            else:
+                c = Condition(f, names[f], "num", "<" if is_left else ">=", float(np.float32(tree.thr[p])), nas=nas)
+            if (f, c.op) not in seen:
+                seen.add((f, c.op))
+                conds.append(c)
+            node = p
+        conds.sort(key=lambda c: c.name)
+        rules.append(Rule(conds, float(tree.value[leaf]), f"M{mid}T{tj}N{leaf}{cls_suffix}"))
+    return rules
 
 
 class RuleFitModel(Model):
     algo = "rulefit"
 
-    def _rule_matrix(self, X):
-        cols = []
-        for ti, nodes in self.rule_nodes:
-            masks, _ = _node_masks(self.trees[ti], X)
-            for n in nodes:
-                cols.append(masks[n].float())
-        R = torch.stack(cols, 0) if cols else torch.zeros(0, X.shape[1], device=X.device)
+    def _groups(self):
+        """[(column name, [rules])] in the GLM frame's column order."""
+        return self.rule_groups
+
+    def _rule_codes(self, X):
+        """One categorical code per tree column: index of the last satisfied rule, NaN when none (Decoder)."""
+        rows = []
+        for _, rules in self._groups():
+            code = torch.full((X.shape[1],), float("nan"), dtype=torch.float32, device=X.device)
+            for r_i, r in enumerate(rules):
+                code = torch.where(r.holds(X), torch.full_like(code, float(r_i)), code)
+            rows.append(code)
+        return rows
+
+    def _glm_matrix(self, X):
+        rows = self._rule_codes(X) if self.params.get("model_type", "rules_and_linear") != "linear" else []
         if self.params.get("model_type", "rules_and_linear") != "rules":
-            R = torch.cat([R, X.float()], 0)
-        return R
+            rows += [X[f].float() for f in range(X.shape[0])]
+        return torch.stack(rows, 0)
 
     def _predict_tensor(self, X, offset=None):
-        return self.glm._predict_tensor(self._rule_matrix(X.to(self.device)), offset)
+        return self.glm._predict_tensor(self._glm_matrix(X.to(self.device)), offset)
 
     def rule_importance(self):
         return self.output["rule_importance"]
+
+    def all_rules(self):
+        return [r for _, rules in self._groups() for r in rules]
 
     def predict_rules(self, frame, rule_ids):
         """0/1 column per requested rule: does the row satisfy the rule's conditions (RuleFitModel.predictRules)."""
         from ..frame import Column, H2OFrame
         X, _ = frame.model_matrix(self.info, device=self.device)
-        where = {}
-        for ti, nodes in self.rule_nodes:
-            for n in nodes:
-                where[f"M{ti}T{ti}N{n}"] = (ti, n)
-        cols, cache = [], {}
+        by = {r.var: r for r in self.all_rules()}
+        cols = []
         for rid in rule_ids:
-            if rid not in where:
+            if rid not in by:
                 raise ValueError(f"Rule {rid!r} is not part of the model")
-            ti, n = where[rid]
-            if ti not in cache:
-                cache[ti] = _node_masks(self.trees[ti], X)[0]
-            cols.append(Column(rid, "int", cache[ti][n].double()))
+            cols.append(Column(rid, "int", by[rid].holds(X).double()))
         return H2OFrame._from_columns(cols)
+
+    def to_state(self):
+        s = super().to_state()
+        s["rule_groups"] = [[n, [r.to_state() for r in rules]] for n, rules in self.rule_groups]
+        s["depth"], s["ntrees"] = self.depth, self.ntrees
+        s["glm"] = self.glm.to_state()
+        s["glm_class"] = type(self.glm).__module__ + ":" + type(self.glm).__name__
+        return s
+
+    def _restore(self, s):
+        from ..persist import _from_state
+        super()._restore(s)
+        self.rule_groups = [(n, [Rule.from_state(r) for r in rules]) for n, rules in s["rule_groups"]]
+        self.depth, self.ntrees = s["depth"], s["ntrees"]
+        gs = dict(s["glm"])
+        gs["__class__"] = s["glm_class"]
+        self.glm = _from_state(gs)
 
 
 class RuleFitTrainer:
@@ -124,65 +224,116 @@ class RuleFitTrainer:
         t0 = time.time()
         p = self.p
         algo = str(p["algorithm"]).upper()
+        mtype = str(p["model_type"]).lower()
         lo, hi = int(p["min_rule_length"]), int(p["max_rule_length"])
         depths = list(range(lo, hi + 1))
-        per = max(1, int(p["rule_generation_ntrees"]) // len(depths))
-        trees = []
-        for d in depths:
-            kw = dict(ntrees=per, max_depth=d, seed=p["seed"], min_rows=1)
-            tr = GBMTrainer(dict(kw, learn_rate=0.1)) if algo == "GBM" else DRFTrainer(kw)
-            m = tr.fit(X, y, w, offset, info)
-            trees += list(m.forest.trees)
-        rule_nodes, seen, rule_text, cols = [], set(), [], []
-        for ti, t in enumerate(trees):
-            masks, conds = _node_masks(t, X)
-            keep = []
-            for n in range(1, t.n_nodes):
-                text = " & ".join(_cond_text(c, left, info.x, info.domains) for c, left in conds[n])
-                if p["remove_duplicates"] and text in seen:
-                    continue
-                seen.add(text)
-                keep.append(n)
-                rule_text.append((f"M{ti}T{ti}N{n}", text))
-                cols.append(masks[n].float())
-            rule_nodes.append((ti, keep))
-        R = torch.stack(cols, 0)
-        names = [r[0] for r in rule_text]
-        iscat = [0] * len(names)
-        doms = [None] * len(names)
-        Xg = R
-        if p["model_type"] != "rules":
-            Xg = torch.cat([R, X.float()], 0)
-            names = names + [f"linear.{n}" for n in info.x]
-            iscat += [0] * info.F
-            doms += [None] * info.F
+        ntrees = int(p["rule_generation_ntrees"])
+        dom = info.response_domain
+        multi = dom is not None and len(dom) > 2
+        groups = []
+        if mtype != "linear":
+            for mid, d in enumerate(depths):
+                kw = dict(ntrees=ntrees, max_depth=d, seed=p["seed"])
+                if str(p.get("distribution", "AUTO")).upper() != "AUTO":
+                    kw["distribution"] = p["distribution"]
+                tr = GBMTrainer(kw) if algo == "GBM" else DRFTrainer(kw)
+                m = tr.fit(X, y, w, offset, info)
+                fr = m.forest
+                K = max(1, fr.K)
+                for t, (tree, c) in enumerate(zip(fr.trees, fr.tree_class)):
+                    tj = t // K
+                    suffix = f"_{dom[c]}" if multi else ""
+                    name = f"M{mid}T{tj}C{c}" if multi else f"M{mid}T{tj}"
+                    groups.append((name, leaf_rules(tree, mid, tj, info.x, info.domains, suffix)))
+                # columns ordered (model, tree, class) as in createGLMTrainFrame
+            groups.sort(key=lambda g: _group_key(g[0]))
+        model = RuleFitModel(model_key or make_key("rulefit"), p, info)
+        model.device = X.device
+        model.rule_groups = groups
+        model.depth, model.ntrees = len(depths), ntrees
+        names, iscat, doms = [], [], []
+        for n, rules in groups:
+            names.append(n)
+            iscat.append(1)
+            doms.append([r.var for r in rules])
+        if mtype != "rules":
+            names += [f"linear.{n}" for n in info.x]
+            iscat += list(np.asarray(info.iscat).tolist())
+            doms += list(info.domains)
         ginfo = DataInfo(names, np.asarray(iscat, np.int32), doms, info.response, info.response_domain)
-        gp = dict(alpha=1.0, standardize=True, seed=p["seed"])
+        Xg = model._glm_matrix(X)
+        # support of every rule (RuleEnsemble.calculateSupport: weighted share of rows satisfying it)
+        wv = None if w is None else w.double()
+        for gi, (_, rules) in enumerate(groups):
+            code = Xg[gi]
+            for r_i, r in enumerate(rules):
+                hit = (code == r_i).double()
+                r.support = float((hit * wv).sum() / wv.sum()) if wv is not None else float(hit.mean())
+        gp = dict(alpha=1.0, seed=p["seed"])
         if p.get("lambda_") is not None:
             gp["lambda_"] = p["lambda_"]
         else:
             gp["lambda_search"] = True
             gp["nlambdas"] = 30
-        if info.response_domain is not None and len(info.response_domain) > 2:
+        if int(p["max_num_rules"]) > 0:
+            gp["max_active_predictors"] = int(p["max_num_rules"]) + 1
+        fam = str(p.get("distribution", "AUTO")).lower()
+        if multi:
             gp["family"] = "multinomial"
-            gp["alpha"] = 0.0
-        glm = GLMTrainer(gp).fit(Xg, y, w, offset, ginfo, valid and (None if valid is None else None))
-        model = RuleFitModel(model_key or make_key("rulefit"), p, info)
-        model.device = X.device
-        model.trees = trees
-        model.rule_nodes = rule_nodes
+        elif fam in ("gaussian", "poisson", "gamma", "tweedie", "bernoulli", "quasibinomial"):
+            gp["family"] = "binomial" if fam == "bernoulli" else fam
+        gvalid = None
+        if valid is not None:
+            Xv, yv, wv2, ov = valid
+            gvalid = (model._glm_matrix(Xv), yv, wv2, ov)
+        glm = GLMTrainer(gp).fit(Xg, y, w, offset, ginfo, gvalid)
         model.glm = glm
+        model.output["linear_names"] = names + [f"linear.{info.response}"]
+        model.output["glm_model_key"] = glm.key
         coefs = glm.output["coefficients"]
-        texts = dict(rule_text)
-        support = {r[0]: float(c.mean()) for r, c in zip(rule_text, cols)}
-        imp = [dict(variable=k, coefficient=v, rule=texts.get(k, k), support=support.get(k, 1.0))
-               for k, v in coefs.items() if k != "Intercept" and v != 0]
+        by = {r.var: r for _, rules in groups for r in rules}
+        imp = []
+        for k, v in coefs.items():
+            if k.startswith("Intercept") or v == 0:
+                continue
+            base, suf = k, ""
+            if multi:
+                for c in dom:
+                    if k.endswith("_" + c):
+                        base, suf = k[: -len(c) - 1], "_" + c
+                        break
+            lvl = base.split(".", 1)[1] if "." in base and not base.startswith("linear.") else None
+            r = by.get(lvl) if lvl is not None else None
+            if r is not None:
+                imp.append(dict(variable=r.var, coefficient=float(v), support=r.support, rule=r.text()))
+            else:
+                imp.append(dict(variable=base + suf, coefficient=float(v), support=float("nan"), rule=""))
+        if p["remove_duplicates"]:
+            merged = {}
+            for row in imp:
+                key = (row["rule"] or row["variable"], row["variable"].split("_")[-1] if multi else "")
+                if key in merged and row["rule"]:
+                    merged[key]["variable"] += ", " + row["variable"]
+                    merged[key]["coefficient"] += row["coefficient"]
+                else:
+                    merged[key] = dict(row)
+            imp = list(merged.values())
         imp.sort(key=lambda r: -abs(r["coefficient"]))
-        mx = int(p["max_num_rules"])
-        model.output["rule_importance"] = imp[:mx] if mx > 0 else imp
+        for r in imp:
+            if r["variable"] in by:
+                by[r["variable"]].coef = r["coefficient"]
+        model.output["rule_importance"] = imp
+        model.output["intercept"] = [v for k, v in coefs.items() if k.startswith("Intercept")]
         model.output["training_metrics"] = model.metrics_for(X, y, w, offset)
         if valid is not None:
-            Xv, yv, wv, ov = valid
-            model.output["validation_metrics"] = model.metrics_for(Xv, yv, wv, ov)
+            Xv, yv, wv2, ov = valid
+            model.output["validation_metrics"] = model.metrics_for(Xv, yv, wv2, ov)
         model.output["run_time_ms"] = int((time.time() - t0) * 1000)
         return model
+
+
+def _group_key(name: str):
+    """(model, tree, class) order of a rule column name ``M<i>T<j>`` / ``M<i>T<j>C<k>``."""
+    m, rest = name[1:].split("T", 1)
+    t, _, c = rest.partition("C")
+    return int(m), int(t), int(c or 0)

@@ -720,3 +720,137 @@ def write_glrm(model, kv, blobs):
     kv["num_levels_per_category"] = "[" + ", ".join(str(n) for n in nlev + [-1] * nn) + "]"
     kv["catOffsets"] = "[" + ", ".join(str(o) for o in offs) + "]"
     blobs["archetypes"] = Y.astype(">f8").tobytes()
+
+
+# ---- RuleFit (RuleFitMojoWriter: MultiModelMojoWriter with the GLM as the one sub-model) ----------------
+def _jbool(b) -> str:
+    return "true" if b else "false"
+
+
+def write_rulefit(model, kv, blobs):
+    from .writer import _mojo_files
+    glm = model.glm
+    key = glm.key
+    kv["submodel_count"] = 1
+    kv["submodel_key_0"] = key
+    kv["submodel_dir_0"] = f"models/{key}/"
+    blobs.update(_mojo_files(glm, f"models/{key}/"))
+    kv["linear_model"] = key
+    mtype = str(model.params.get("model_type", "rules_and_linear")).lower()
+    classes = model.info.response_domain
+    nclasses = len(classes) if classes is not None and len(classes) > 2 else 1
+    if mtype != "linear":
+        groups = dict(model.rule_groups)
+        for i in range(model.depth):
+            for j in range(model.ntrees):
+                rules = []
+                for k in range(nclasses):          # class 0 ... class k, as writeOrderedRuleEnsemble
+                    rules += groups.get(f"M{i}T{j}C{k}" if nclasses > 1 else f"M{i}T{j}", [])
+                kv[f"num_rules_M{i}T{j}"] = len(rules)
+                for r_i, r in enumerate(rules):
+                    rid = f"{i}_{j}_{r_i}"
+                    kv[f"num_conditions_rule_id_{rid}"] = len(r.conds)
+                    for c_i, c in enumerate(r.conds):
+                        cid = f"{c_i}_{rid}"
+                        kv[f"feature_index_{cid}"] = c.feat
+                        if c.ctype == "cat":
+                            kv[f"type_{cid}"] = 0
+                            kv[f"language_cat_treshold_length_{cid}"] = len(c.level_names)
+                            for t, nm in enumerate(c.level_names):
+                                kv[f"language_cat_treshold_{t}_{cid}"] = nm
+                            kv[f"cat_treshold_length_{cid}"] = len(c.levels)
+                            for t, lv in enumerate(c.levels):
+                                kv[f"cat_treshold_length_{t}_{cid}"] = int(lv)
+                        else:
+                            kv[f"type_{cid}"] = 1
+                            kv[f"num_treshold{cid}"] = repr(float(c.thr))
+                        kv[f"operator_{cid}"] = {"<": 0, ">=": 1}.get(c.op, 2)
+                        kv[f"feature_name_{cid}"] = c.name
+                        kv[f"nas_included_{cid}"] = _jbool(c.nas)
+                        kv[f"language_condition{cid}"] = c.text()
+                    kv[f"prediction_value_rule_id_{rid}"] = repr(float(r.pred))
+                    kv[f"language_rule_rule_id_{rid}"] = r.text()
+                    kv[f"coefficient_rule_id_{rid}"] = repr(float(r.coef))
+                    kv[f"var_name_rule_id_{rid}"] = r.var
+                    kv[f"support_rule_id_{rid}"] = repr(float(r.support))
+    kv["model_type"] = {"linear": 0, "rules_and_linear": 1}.get(mtype, 2)
+    kv["type"] = key
+    kv["depth"] = model.depth
+    kv["ntrees"] = model.ntrees
+    codes = model.output["linear_names"]
+    kv["data_from_rules_codes_len"] = len(codes)
+    for i, n in enumerate(codes):
+        kv[f"data_from_rules_codes_{i}"] = n
+    if model.info.weights:
+        kv["weights_column"] = model.info.weights
+    kv["linear_names_len"] = len(codes)
+    for i, n in enumerate(codes):
+        kv[f"linear_names_{i}"] = n
+
+
+def load_rulefit(ki):
+    """RuleFitMojoReader: rule ensemble [depth][ntrees][rules] + model type + linear names."""
+    from ..models.rulefit import Condition, Rule
+    mtype = int(ki["model_type"])
+    depth, ntrees = int(ki["depth"]), int(ki["ntrees"])
+    ordered = []
+    if mtype != 0:
+        for i in range(depth):
+            row = []
+            for j in range(ntrees):
+                rules = []
+                for r_i in range(int(ki[f"num_rules_M{i}T{j}"])):
+                    rid = f"{i}_{j}_{r_i}"
+                    conds = []
+                    for c_i in range(int(ki[f"num_conditions_rule_id_{rid}"])):
+                        cid = f"{c_i}_{rid}"
+                        op = {0: "<", 1: ">="}.get(int(ki[f"operator_{cid}"]), "in")
+                        nas = ki[f"nas_included_{cid}"] == "true"
+                        name = ki[f"feature_name_{cid}"]
+                        if int(ki[f"type_{cid}"]) == 0:
+                            n1 = int(ki[f"language_cat_treshold_length_{cid}"])
+                            n2 = int(ki[f"cat_treshold_length_{cid}"])
+                            conds.append(Condition(int(ki[f"feature_index_{cid}"]), name, "cat", op, -1.0,
+                                                   [int(ki[f"cat_treshold_length_{t}_{cid}"]) for t in range(n2)],
+                                                   [ki[f"language_cat_treshold_{t}_{cid}"] for t in range(n1)], nas))
+                        else:
+                            conds.append(Condition(int(ki[f"feature_index_{cid}"]), name, "num", op,
+                                                   float(ki[f"num_treshold{cid}"]), nas=nas))
+                    sup = ki.get(f"support_rule_id_{rid}")
+                    rules.append(Rule(conds, float(ki[f"prediction_value_rule_id_{rid}"]), ki[f"var_name_rule_id_{rid}"],
+                                      float(ki[f"coefficient_rule_id_{rid}"]), float(sup) if sup else float("nan")))
+                row.append(rules)
+            ordered.append(row)
+    n = int(ki["linear_names_len"])
+    return dict(model_type=mtype, depth=depth, ntrees=ntrees, rules=ordered,
+                linear_names=[ki[f"linear_names_{i}"] for i in range(n)], linear_key=ki["linear_model"])
+
+
+def score_rulefit(st, glm, X, parent_info):
+    """RuleFitMojoModel.score0: rule codes per (depth, tree[, class]) decoded to the GLM's level index,
+    then (rules_and_linear) the raw row, mapped into the GLM's column order by linear_names."""
+    import torch
+    classes = parent_info.response_domain
+    multi = classes is not None and len(classes) > 2
+    test = []
+    if st["model_type"] != 0:
+        gnames = list(glm.info.x)
+        for i in range(st["depth"]):
+            for j in range(st["ntrees"]):
+                rules = st["rules"][i][j]
+                per = [[r for r in rules if r.var.endswith(c)] for c in classes] if multi else [rules]
+                for k, rl in enumerate(per):
+                    col = f"M{i}T{j}" + (f"C{k}" if multi else "")
+                    dom = glm.info.domains[gnames.index(col)] or []
+                    code = torch.full((X.shape[1],), float("nan"), dtype=torch.float32, device=X.device)
+                    for r in rl:
+                        if r.var in dom:
+                            code = torch.where(r.holds(X), torch.full_like(code, float(dom.index(r.var))), code)
+                    test.append(code)
+    if st["model_type"] != 2:
+        test += [X[f].float() for f in range(X.shape[0])]
+    gx = list(glm.info.x)
+    rows = [None] * len(gx)
+    for i, n in enumerate(st["linear_names"][:len(gx)]):
+        rows[gx.index(n)] = test[i]
+    return glm._predict_tensor(torch.stack(rows, 0))

@@ -23,13 +23,13 @@ from .treebytes import tree_to_bytes
 MOJO_VERSIONS = {"gbm": "1.40", "drf": "1.40", "isolationforest": "1.40", "glm": "1.00", "kmeans": "1.00",
                  "deeplearning": "1.10", "pca": "1.00", "word2vec": "1.00", "isotonicregression": "1.00",
                  "stackedensemble": "1.01", "extendedisolationforest": "1.00", "coxph": "1.00", "targetencoder": "1.00",
-                 "glrm": "1.10"}
+                 "glrm": "1.10", "rulefit": "1.00"}
 ALGO_FULL = {"gbm": "Gradient Boosting Machine", "drf": "Distributed Random Forest", "glm": "Generalized Linear Modeling",
              "kmeans": "K-means", "isolationforest": "Isolation Forest", "deeplearning": "Deep Learning",
              "pca": "Principal Components Analysis", "word2vec": "Word2Vec", "isotonicregression": "Isotonic Regression",
              "stackedensemble": "StackedEnsemble", "extendedisolationforest": "Extended Isolation Forest",
              "coxph": "Cox Proportional Hazards", "targetencoder": "TargetEncoder",
-             "glrm": "Generalized Low Rank Modeling"}
+             "glrm": "Generalized Low Rank Modeling", "rulefit": "rulefit"}
 
 
 def _escape(s: str) -> str:
@@ -106,6 +106,8 @@ def _mojo_files(model, prefix: str = "") -> dict:
         A.write_glrm(model, kv, blobs)
     elif algo == "xgboost" and XG.supported(model):
         XG.write(model, kv, blobs)
+    elif algo == "rulefit":
+        A.write_rulefit(model, kv, blobs)
     else:
         _generic_state(model, kv, blobs)
     buf = io.StringIO()
