@@ -137,6 +137,51 @@ __global__ __launch_bounds__(256) void k_xtv(const float* __restrict__ Z, int64_
 
 }  // namespace
 
+// eta = Z @ B (+ off): Z [N, P] fp32 row-major, B [P, R] fp64 (R <= 8), eta [N, R] fp64 — the GLM linear
+// predictor without an fp64 copy of Z (GLMIterationTask's per-row x·beta). 256 rows per block; 32-column
+// tiles staged through LDS with coalesced loads (row stride padded to 33 floats: conflict-free column reads),
+// one row per thread, fp64 accumulation.
+#define ZB_ROWS 256
+#define ZB_COLS 32
+__global__ __launch_bounds__(ZB_ROWS) void k_zbeta(const float* __restrict__ Z, int64_t ldz, const double* __restrict__ B,
+                                                   int R, int64_t N, int P, const double* __restrict__ off,
+                                                   double* __restrict__ eta) {
+  __shared__ float tile[ZB_ROWS * (ZB_COLS + 1)];
+  __shared__ double bt[ZB_COLS * 8];
+  const int t = threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.x * ZB_ROWS;
+  double acc[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) acc[k] = 0.0;
+  for (int c0 = 0; c0 < P; c0 += ZB_COLS) {
+    const int nc = min(ZB_COLS, P - c0);
+    for (int i = t; i < ZB_ROWS * ZB_COLS; i += ZB_ROWS) {
+      const int rr = i / ZB_COLS, cc = i - rr * ZB_COLS;
+      const int64_t row = r0 + rr;
+      tile[rr * (ZB_COLS + 1) + cc] = (row < N && cc < nc) ? Z[row * ldz + c0 + cc] : 0.f;
+    }
+    for (int i = t; i < ZB_COLS * R; i += ZB_ROWS) {
+      const int cc = i / R, k = i - cc * R;
+      bt[cc * 8 + k] = cc < nc ? B[(int64_t)(c0 + cc) * R + k] : 0.0;
+    }
+    __syncthreads();
+    for (int cc = 0; cc < nc; ++cc) {
+      const double z = (double)tile[t * (ZB_COLS + 1) + cc];
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (k < R) acc[k] += z * bt[cc * 8 + k];
+    }
+    __syncthreads();
+  }
+  const int64_t row = r0 + t;
+  if (row < N) {
+    const double o = off ? off[row] : 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (k < R) eta[row * R + k] = acc[k] + o;
+  }
+}
+
 extern "C" {
 
 // slabs: fp32 [S, Ppad, Ppad], Ppad = ceil(P/64)*64 (caller zero-fills nothing: every upper tile is written)
@@ -157,6 +202,15 @@ int h2o_xtv(const float* Z, long long ldz, const float* v, int R, long long N, i
   const long long rps = (N + S - 1) / S;
   dim3 grid((P + 63) / 64, S);
   hipLaunchKernelGGL(k_xtv, grid, dim3(256), 0, stream, Z, (int64_t)ldz, v, R, (int64_t)N, P, (int64_t)rps, slabs);
+  return (int)hipGetLastError();
+}
+
+int h2o_zbeta(const float* Z, long long ldz, const double* B, int R, long long N, int P, const double* off,
+              double* eta, hipStream_t stream) {
+  if (R < 1 || R > 8 || N <= 0) return N <= 0 ? 0 : (int)hipErrorInvalidValue;
+  const long long grid = (N + ZB_ROWS - 1) / ZB_ROWS;
+  hipLaunchKernelGGL(k_zbeta, dim3((unsigned)grid), dim3(ZB_ROWS), 0, stream, Z, (int64_t)ldz, B, R, (int64_t)N, P, off,
+                     eta);
   return (int)hipGetLastError();
 }
 

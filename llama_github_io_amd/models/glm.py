@@ -179,7 +179,7 @@ class GLMModel(Model):
             return hglm_eta(self, X, offset)
         Z = self.expander.transform(X.to(self.device))
         b = self.beta.to(Z.device)
-        eta = Z.double() @ b[:, :-1].T + b[:, -1]
+        eta = G.zbeta(Z, b[:, :-1].T.contiguous()) + b[:, -1]
         if offset is not None:
             eta = eta + offset.double()[:, None]
         return eta
@@ -446,7 +446,7 @@ class GLMTrainer:
             self.collinear = [ex.names[j] for j in torch.nonzero(fixed[:-1]).flatten().tolist()]
         beta = torch.where(fixed, torch.zeros_like(beta), beta)
         # gradient at the null model -> lambda max
-        eta = Zi.double() @ beta + off
+        eta = G.zbeta(Zi, beta, off)
         mu = fam.linkinv(eta)
         gvec = fam.dlink(mu)
         var = fam.variance(mu)
@@ -478,7 +478,7 @@ class GLMTrainer:
         for li, lam in enumerate(lambdas):
             l1, l2 = lam * alpha, lam * (1 - alpha)
             for it in range(max(max_it, 1)):
-                eta = Zi.double() @ beta + off
+                eta = G.zbeta(Zi, beta, off)
                 mu = fam.linkinv(eta)
                 gp = fam.dlink(mu)
                 var = fam.variance(mu)
@@ -510,7 +510,7 @@ class GLMTrainer:
                     self.job.check_cancelled()
                 if diff < beps:
                     break
-            mu = fam.linkinv(Zi.double() @ beta + off)
+            mu = fam.linkinv(G.zbeta(Zi, beta, off))
             dev_tr = _gsum((w * fam.deviance(y, mu)).sum())
             entry = dict(lambda_=lam, dev_explained=1 - dev_tr / null_dev if null_dev > 0 else 0.0,
                          coefs=beta.cpu().tolist())
@@ -526,7 +526,7 @@ class GLMTrainer:
             if valid is not None and len(lambdas) > 1:
                 Xv, yv, wv, ov = valid
                 Zv = ex.transform(Xv)
-                etav = Zv.double() @ beta[:-1] + beta[-1] + (0 if ov is None else ov.double())
+                etav = G.zbeta(Zv, beta[:-1], ov) + beta[-1]
                 muv = fam.linkinv(etav)
                 okv = ~torch.isnan(yv)
                 wvv = torch.ones_like(yv, dtype=torch.float64) if wv is None else wv.double()
@@ -638,16 +638,14 @@ class GLMTrainer:
         freq = (freq / freq.sum()).clamp(min=1e-10)
         if intercept:
             B[:, -1] = torch.log(freq) - torch.log(freq).mean()
-        Zd = Zi.double()
-
-        def probs(B):
-            return torch.softmax(Zd @ B.T + off[:, None], 1)
+        def probs(B):       # fp32 design, fp64 accumulation (no fp64 copy of Z)
+            return torch.softmax(G.zbeta(Zi, B.T.contiguous()) + off[:, None], 1)
         lam_in = p["lambda_"]
         if lam_in is not None:
             lambdas = [float(v) for v in (lam_in if isinstance(lam_in, (list, tuple)) else [lam_in])]
         else:
             Pm = probs(B)
-            g = _gvec((Zi.double().T @ (w[:, None] * (Y - Pm))).contiguous()) * obj_reg    # [P1, K]
+            g = _gvec(G.xtv(Zi, (w[:, None] * (Y - Pm)).contiguous()).contiguous()) * obj_reg    # [P1, K]
             if intercept:
                 g[-1] = 0
             lmax = float(g.abs().max()) / max(alpha, 1e-2)
@@ -671,7 +669,7 @@ class GLMTrainer:
                     Pm = probs(B)
                     pc = Pm[:, c]
                     wi = (w * pc * (1 - pc)).clamp(min=1e-10 * float(w.max()) if w.numel() else 0.0)
-                    eta_c = Zd @ B[c]
+                    eta_c = G.zbeta(Zi, B[c])
                     zi = eta_c + (Y[:, c] - pc) / (pc * (1 - pc)).clamp(min=1e-10)
                     Gm = _gvec(G.gram(Zi, wi.float())) * obj_reg
                     r = _gvec(G.xtv(Zi, (wi * zi).float())) * obj_reg
@@ -832,7 +830,7 @@ class GLMTrainer:
         lam = model.output.get("lambda_best", 0.0)
         if lam and lam > 0:
             model.output["warnings"] = ["p-values are only computed for lambda = 0"]
-        eta = Zi.double() @ beta + off
+        eta = G.zbeta(Zi, beta, off)
         mu = family.linkinv(eta)
         gp = family.dlink(mu)
         var = family.variance(mu)

@@ -12,7 +12,34 @@ from . import _native as nat
 nat.register_hip_signatures({
     "h2o_gram": [nat.c_void_p, nat.c_ll, nat.c_void_p, nat.c_ll, nat.c_int, nat.c_int, nat.c_void_p, nat.c_int, nat.c_void_p],
     "h2o_xtv": [nat.c_void_p, nat.c_ll, nat.c_void_p, nat.c_int, nat.c_ll, nat.c_int, nat.c_int, nat.c_void_p, nat.c_void_p],
+    "h2o_zbeta": [nat.c_void_p, nat.c_ll, nat.c_void_p, nat.c_int, nat.c_ll, nat.c_int, nat.c_void_p, nat.c_void_p,
+                  nat.c_void_p],
 })
+
+
+def zbeta(Z: torch.Tensor, B: torch.Tensor, off=None) -> torch.Tensor:
+    """``Z @ B (+ off)`` in float64 without an fp64 copy of Z. Z: [N, P] float32; B: [P] or [P, R] (R <= 8)."""
+    vec = B.dim() == 1
+    Bm = B[:, None] if vec else B
+    N, P = Z.shape
+    R = Bm.shape[1]
+    if not Z.is_cuda or R > 8:
+        out = Z.double() @ Bm.double()
+        if off is not None:
+            out = out + (off.double()[:, None] if torch.is_tensor(off) and off.dim() == 1 else off)
+        return out[:, 0] if vec else out
+    Z = Z.contiguous().float()
+    Bd = Bm.contiguous().double()
+    od = None
+    if off is not None:
+        od = (off if torch.is_tensor(off) else torch.full((N,), float(off), device=Z.device)).contiguous().double()
+        if od.numel() == 1:
+            od = od.expand(N).contiguous()
+    eta = torch.empty(N, R, dtype=torch.float64, device=Z.device)
+    if N > 0:
+        nat.call("h2o_zbeta", Z.data_ptr(), P, Bd.data_ptr(), R, N, P, 0 if od is None else od.data_ptr(), eta.data_ptr(),
+                 nat.stream_ptr(Z.device))
+    return eta[:, 0] if vec else eta
 
 
 def _splits(N: int, pairs: int) -> int:

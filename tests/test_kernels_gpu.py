@@ -261,3 +261,17 @@ def test_fused_gbm_step_matches_eager_path(dist, monkeypatch):
     np.testing.assert_allclose(f1.score_tensor(X).double().cpu().numpy(), e1.score_tensor(X).double().cpu().numpy(),
                                rtol=2e-4, atol=2e-5)
     _ = (a, b)
+
+
+@pytest.mark.parametrize("N,P,R", [(1000, 7, 1), (70001, 51, 1), (5000, 130, 3), (33, 200, 8)])
+def test_zbeta_matches_fp64(N, P, R):
+    # GLM linear predictor: fp32 design read once, fp64 accumulation (k_zbeta) vs the fp64 matmul
+    from llama_github_io_amd.ops.gram import zbeta
+    g = torch.Generator(device=dev).manual_seed(N + P)
+    Z = torch.randn(N, P, device=dev, generator=g)
+    B = torch.randn(P, R, device=dev, generator=g, dtype=torch.float64)
+    off = torch.randn(N, device=dev, generator=g, dtype=torch.float64)
+    ref = Z.double() @ B + off[:, None]
+    out = zbeta(Z, B, off)
+    assert out.dtype == torch.float64 and torch.allclose(out, ref, rtol=1e-12, atol=1e-10)
+    assert torch.allclose(zbeta(Z, B[:, 0]), Z.double() @ B[:, 0], rtol=1e-12, atol=1e-10)
