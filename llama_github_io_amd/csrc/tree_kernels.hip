@@ -673,23 +673,26 @@ __global__ __launch_bounds__(256) void k_split_find(
 __global__ __launch_bounds__(64) void k_split_reduce(
     const Cand* __restrict__ cand, const int* __restrict__ meta, int F,
     const int* __restrict__ feat_ok /*[F] per-tree mask, 1 = usable*/, int k_cols,
-    unsigned long long seed, int level, Dec* __restrict__ dec) {
+    unsigned long long seed, int level, Dec* __restrict__ dec,
+    const unsigned char* __restrict__ node_ok /*[nodes][F] interaction-constraint mask or null*/) {
   const int node = blockIdx.x, lane = threadIdx.x;
   if (node >= meta[0]) return;
+  const unsigned char* nok = node_ok ? node_ok + (size_t)node * F : nullptr;
+  auto usable = [&](int f) { return feat_ok[f] != 0 && (!nok || nok[f] != 0); };
   const unsigned long long base = splitmix64(seed ^ ((unsigned long long)(level + 1) << 40) ^ (unsigned long long)node);
   int n_ok = 0;
-  for (int f = lane; f < F; f += 64) n_ok += feat_ok[f] ? 1 : 0;
+  for (int f = lane; f < F; f += 64) n_ok += usable(f) ? 1 : 0;
   n_ok = wave_sum_i(n_ok);
   const bool sample = k_cols > 0 && k_cols < n_ok;
   double be = -1.0e300;
   int bf = -1;
   for (int f = lane; f < F; f += 64) {
-    if (!feat_ok[f]) continue;
+    if (!usable(f)) continue;
     if (sample) {
       const unsigned long long kf = splitmix64(base + (unsigned long long)f);
       int rank = 0;
       for (int g2 = 0; g2 < F; ++g2) {
-        if (!feat_ok[g2]) continue;
+        if (!usable(g2)) continue;
         const unsigned long long kg = splitmix64(base + (unsigned long long)g2);
         rank += (kg < kf || (kg == kf && g2 < f)) ? 1 : 0;
       }
@@ -888,6 +891,21 @@ __global__ __launch_bounds__(1024) void k_plan(
   } else if (tid == 0) {
     next_meta[0] = nn; next_meta[1] = 0; next_meta[2] = 0;
   }
+}
+
+// Interaction constraints (GlobalInteractionConstraints / BranchInteractionConstraints): a child may split
+// on the features its parent allowed AND that interact with the parent's split feature:
+// ok[child][f] = ok[parent][f] & map[parent split feature][f]. grid = next-level capacity, block 64.
+__global__ __launch_bounds__(64) void k_ic_next(const Node* __restrict__ next, const int* __restrict__ next_meta,
+                                                const Dec* __restrict__ dec, const unsigned char* __restrict__ ok_cur,
+                                                const unsigned char* __restrict__ ic_map, int F,
+                                                unsigned char* __restrict__ ok_next) {
+  const int c = blockIdx.x;
+  if (c >= next_meta[0]) return;
+  const int par = next[c].parent;
+  const int sf = dec[par].feat;
+  for (int f = threadIdx.x; f < F; f += 64)
+    ok_next[(size_t)c * F + f] = (sf >= 0 && ok_cur[(size_t)par * F + f] && ic_map[(size_t)sf * F + f]) ? 1 : 0;
 }
 
 // k_ranges: after k_route filled the odd level's regions, give each even-level node its range
@@ -1364,9 +1382,18 @@ int h2o_split_find(const void* hist, int slot_doubles, const void* meta, int cap
 }
 
 int h2o_split_reduce(const void* cand, const void* meta, int cap, int F, const void* feat_ok, int k_cols,
-                     unsigned long long seed, int level, void* dec, hipStream_t s) {
+                     unsigned long long seed, int level, void* dec, const void* node_ok, hipStream_t s) {
   hipLaunchKernelGGL(k_split_reduce, dim3(cap), dim3(64), 0, s, (const Cand*)cand, (const int*)meta, F,
-                     (const int*)feat_ok, k_cols, seed, level, (Dec*)dec);
+                     (const int*)feat_ok, k_cols, seed, level, (Dec*)dec, (const unsigned char*)node_ok);
+  return (int)hipGetLastError();
+}
+
+int h2o_ic_next(const void* next, const void* next_meta, const void* dec, const void* ok_cur, const void* ic_map, int F,
+                void* ok_next, int cap_next, hipStream_t s) {
+  if (cap_next <= 0) return 0;
+  hipLaunchKernelGGL(k_ic_next, dim3(cap_next), dim3(64), 0, s, (const Node*)next, (const int*)next_meta,
+                     (const Dec*)dec, (const unsigned char*)ok_cur, (const unsigned char*)ic_map, F,
+                     (unsigned char*)ok_next);
   return (int)hipGetLastError();
 }
 
@@ -1497,6 +1524,8 @@ struct TreePlan {
   void* edges;             // [F][255] global bin edges for UniformAdaptive candidates (null: QuantilesGlobal)
   int nb_level[TP_MAXL];   // UniformAdaptive bins per level (0 = off)
   int pad3;
+  void* ic_map;            // [F][F] interaction-constraint map (null: no constraints)
+  void* ic[TP_MAXL];       // per level [caps][F] allowed-feature masks (ic[0] = the root's)
 };
 
 static inline void tp_level_buf(const TreePlan* P, int e, const void*& b, const void*& a, const void*& r) {
@@ -1543,12 +1572,18 @@ int h2o_tree_level(const TreePlan* P, int d, int dist, hipStream_t s) {
                           d == 0 ? P->rootw : nullptr, P->edges, P->nb_level[d], s);
   if (rc) return -rc;
   const int kc = P->kc_level[d] > 0 ? P->kc_level[d] : P->k_cols;
-  rc = h2o_split_reduce(P->cand, P->meta[d], cap, P->F, P->feat_ok, kc, P->seed, d, P->dec[d], s);
+  rc = h2o_split_reduce(P->cand, P->meta[d], cap, P->F, P->feat_ok, kc, P->seed, d, P->dec[d],
+                        P->ic_map ? P->ic[d] : nullptr, s);
   if (rc) return -rc;
   rc = h2o_plan(P->nodes[d], P->meta[d], P->dec[d], P->nl[d], odd ? P->nl[d - 1] : nullptr, P->cur[d], P->cl[d],
                 P->cr[d], P->nodes[d + 1], P->tp[d + 1], P->meta[d + 1], P->bp[d + 1], P->counters, P->scratch, d,
                 P->D, P->min_w, P->caps[d + 1], P->leaf_cap, s);
   if (rc) return -rc;
+  if (P->ic_map && d + 1 < P->D) {
+    rc = h2o_ic_next(P->nodes[d + 1], P->meta[d + 1], P->dec[d], P->ic[d], P->ic_map, P->F, P->ic[d + 1],
+                     P->caps[d + 1], s);
+    if (rc) return -rc;
+  }
   if (d + 1 == P->D) {
     rc = tp_route(P, odd ? d - 1 : d, odd ? 1 : 0, 0, s);
     return rc ? -rc : 1;

@@ -40,6 +40,23 @@ def resolve_seed(seed) -> int:
     return int(seed)
 
 
+def interaction_map(constraints, names):
+    """GlobalInteractionConstraints: [F, F] map (row f = union of the constraint sets containing f) and the
+    root's allowed features (every column named in some set; unlisted columns are never split on)."""
+    F = len(names)
+    m = np.zeros((F, F), dtype=np.uint8)
+    for group in constraints:
+        group = [group] if isinstance(group, str) else list(group)
+        idx = []
+        for c in group:
+            if c not in names:
+                raise ValueError(f"interaction_constraints: column {c!r} is not a predictor")
+            idx.append(names.index(c))
+        for i in idx:
+            m[i, idx] = 1
+    return m, m.any(1).astype(np.uint8)
+
+
 class SharedTreeModel(Model):
     def __init__(self, key, params, info):
         super().__init__(key, params, info)
@@ -194,6 +211,8 @@ class SharedTreeTrainer:
         node_cap = int(p.get("node_cap", 1 << 14))
         self.builder = T.make_builder(bins, F, self.binning.nbins, self.binning.iscat, mono, max_depth,
                                       self._split_params(), node_cap=node_cap)
+        if p.get("interaction_constraints"):
+            self.builder.set_interaction_constraints(*interaction_map(p["interaction_constraints"], info.x))
         model = self.model_cls(model_key or make_key(self.algo), p, info)
         model.binning = self.binning
         model.device = dev

@@ -224,10 +224,10 @@ def split_find_ref(h, nayy, wyy, nbins_f, iscat_f, mono_f, p: SplitParams, level
     return out
 
 
-def split_reduce_ref(cands, feat_ok, k_cols, seed, level, node):
+def split_reduce_ref(cands, feat_ok, k_cols, seed, level, node, node_ok=None):
     F = len(cands)
     base = splitmix64((seed ^ ((level + 1) << 40) ^ node) & _M64)
-    ok = [bool(feat_ok[f]) for f in range(F)]
+    ok = [bool(feat_ok[f]) and (node_ok is None or bool(node_ok[f])) for f in range(F)]
     n_ok = sum(ok)
     sample = 0 < k_cols < n_ok
     allowed = ok[:]
@@ -287,6 +287,12 @@ class RefTreeBuilder:
         self.p = params
         self.node_cap = node_cap
         self.N = self.bins.shape[0]
+        self.ic_map = None
+
+    def set_interaction_constraints(self, ic_map, root_ok):
+        """``ic_map`` [F, F] (row f: features allowed to interact with f), ``root_ok`` [F]."""
+        self.ic_map = np.asarray(ic_map, dtype=np.uint8)
+        self.ic_root = np.asarray(root_ok, dtype=np.uint8)
 
     def _hist(self, rows, aux):
         F = self.F
@@ -309,6 +315,7 @@ class RefTreeBuilder:
         leaf_of_row = np.full(self.N, -1, dtype=np.int64)
         leafsum = []
         level_rows = [np.arange(self.N)]
+        level_ok = [None if self.ic_map is None else self.ic_root]
         decs, cls, crs = [], [], []
         n_leaves = 0
         for d in range(D):
@@ -325,9 +332,9 @@ class RefTreeBuilder:
                     nayy = flat[h.size: h.size + F]
                     wyy = float(flat[-1])
                 cands = split_find_ref(h, nayy, wyy, self.nbins_f, self.iscat_f, self.mono_f, p, d, i, seed)
-                dl[i] = split_reduce_ref(cands, feat_ok, _level_k(k_cols, d), seed, d, i)
+                dl[i] = split_reduce_ref(cands, feat_ok, _level_k(k_cols, d), seed, d, i, level_ok[i])
             cl = np.zeros(n, dtype=np.int64); cr = np.zeros(n, dtype=np.int64)
-            nxt = []
+            nxt, nxt_ok = [], []
             act = 0
             for i, rows in enumerate(level_rows):
                 dd = dl[i]
@@ -345,6 +352,7 @@ class RefTreeBuilder:
                         act += 1
                     if active:
                         arr[i] = len(nxt); nxt.append(crow)
+                        nxt_ok.append(None if self.ic_map is None else level_ok[i] & self.ic_map[dd["feat"]])
                     else:
                         lid = n_leaves; n_leaves += 1
                         arr[i] = -1 - lid
@@ -352,6 +360,7 @@ class RefTreeBuilder:
                         leafsum.append((aux[crow, 2].astype(np.float64).sum(), aux[crow, 3].astype(np.float64).sum()))
             decs.append(dl); cls.append(cl); crs.append(cr)
             level_rows = nxt
+            level_ok = nxt_ok
             if not nxt:
                 break
         res = TreeLevels(decs, cls, crs, n_leaves)
@@ -396,7 +405,8 @@ class _TreePlan(ctypes.Structure):
                 [(n, _ci) for n in ("compute_amax", "k_cols", "packed", "leaf_native", "log_link", "pad1")] +
                 [("seed", ctypes.c_ulonglong)] + [(n, _cd) for n in ("scale", "kclamp", "mx")] +
                 [("kc_level", _ci * _MAXL), ("pad2", _ci)] +
-                [("edges", _vp), ("nb_level", _ci * _MAXL), ("pad3", _ci)])
+                [("edges", _vp), ("nb_level", _ci * _MAXL), ("pad3", _ci)] +
+                [("ic_map", _vp), ("ic", _vp * _MAXL)])
 
 
 class _Arena:
@@ -501,12 +511,32 @@ class GpuTreeBuilder:
         # raw device pointers resolved once: the per-tree launch sequence is ~45 ctypes calls and at small
         # shards (1.375M rows/GPU) the host loop, not the GPU, set the pace (82 % busy, rocprofv3 trace)
         self._pt = {name: t.data_ptr() for name, t in self.av.items()}
+        self.ic_map = None
         self._hp = [h.data_ptr() for h in self.hist]
         self._bp = [dict(bins=b["bins"].data_ptr(), aux=b["aux"].data_ptr(), ridx=b["ridx"].data_ptr())
                     for b in self.bufs]
 
     def _p(self, name):
         return self._pt[name]
+
+    def set_interaction_constraints(self, ic_map, root_ok):
+        """Per-node allowed features (GlobalInteractionConstraints): ``ic_map`` [F, F] uint8, row f = the
+        features allowed to interact with f; ``root_ok`` [F]. Level masks [caps[d], F] live on the device and
+        are propagated by k_ic_next after each plan."""
+        F, dev = self.F, self.dev
+        self.ic_map = torch.as_tensor(np.asarray(ic_map, dtype=np.uint8), device=dev).contiguous()
+        self.ic_lv = [torch.zeros(self.caps[d] * F, dtype=torch.uint8, device=dev) for d in range(self.D + 1)]
+        self.ic_lv[0][:F].copy_(torch.as_tensor(np.asarray(root_ok, dtype=np.uint8), device=dev))
+        if getattr(self, "_plan", None) is not None:
+            self._set_plan_ic(self._plan)
+
+    def _set_plan_ic(self, P):
+        if self.ic_map is None:
+            P.ic_map = 0
+            return
+        P.ic_map = self.ic_map.data_ptr()
+        for d in range(self.D + 1):
+            P.ic[d] = self.ic_lv[d].data_ptr()
 
     def _make_plan(self):
         """Static part of the native launch plan (pointers / shapes fixed for the builder's lifetime)."""
@@ -534,6 +564,7 @@ class GpuTreeBuilder:
         P.edges = self._edges_ptr()
         for d in range(_MAXL):
             P.nb_level[d] = p.adapt_nb(d) if P.edges else 0
+        self._set_plan_ic(P)
         return P
 
     def _edges_ptr(self):
@@ -617,13 +648,18 @@ class GpuTreeBuilder:
                                          p.alpha, p.gamma, p.mode, int(p.random_split), seed, d,
                                          cand_p, self._p("rootw") if d == 0 else 0, self._edges_ptr(),
                                          p.adapt_nb(d) if self._edges_ptr() else 0, s), "split_find")
+            ic_d = 0 if self.ic_map is None else self.ic_lv[d].data_ptr()
             nat.check(lib.h2o_split_reduce(cand_p, self._p(f"meta{d}"), cap, F, fo_p, _level_k(k_cols, d),
-                                           seed, d, self._p(f"dec{d}"), s), "split_reduce")
+                                           seed, d, self._p(f"dec{d}"), ic_d, s), "split_reduce")
             nat.check(lib.h2o_plan(self._p(f"nodes{d}"), self._p(f"meta{d}"), self._p(f"dec{d}"), self._p(f"nl{d}"),
                                    self._p(f"nl{d - 1}") if odd else 0, self._p(f"cur{d}"), self._p(f"cl{d}"),
                                    self._p(f"cr{d}"), self._p(f"nodes{d + 1}"), self._p(f"tp{d + 1}"),
                                    self._p(f"meta{d + 1}"), self._p(f"bp{d + 1}"), self._p("counters"),
                                    self.scratch.data_ptr(), d, D, p.min_w, self.caps[d + 1], self.leaf_cap, s), "plan")
+            if self.ic_map is not None and d + 1 < D:
+                nat.check(lib.h2o_ic_next(self._p(f"nodes{d + 1}"), self._p(f"meta{d + 1}"), self._p(f"dec{d}"), ic_d,
+                                          self.ic_map.data_ptr(), F, self.ic_lv[d + 1].data_ptr(), self.caps[d + 1], s),
+                          "ic_next")
             if d + 1 == D:
                 # last level: every row lands on a leaf (routed from the last regrouped level)
                 route(d - 1 if odd else d, two=odd, move=False)

@@ -38,7 +38,7 @@ def test_unknown_parameter_raises(fr):
 
 
 @pytest.mark.parametrize("algo,param,value", [
-    ("gbm", "interaction_constraints", [["a", "b"]]),
+    ("kmeans", "cluster_size_constraints", [10, 20]),
     ("xgboost", "grow_policy", "lossguide"),
     ("deeplearning", "initial_weights", ["w"]),
     ("glm", "influence", "dfbetas"),
@@ -151,3 +151,25 @@ def test_dl_overwrite_with_best_model(fr):
     assert len(hist) > 2
     assert a.output["training_metrics"]["logloss"] <= b.output["training_metrics"]["logloss"] + 1e-9
     assert a.output["training_metrics"]["logloss"] <= min(hist) + 1e-6
+
+
+def test_interaction_constraints_gbm_xgboost():
+    """GBM / XGBoost interaction_constraints: every tree path stays inside one constraint set."""
+    import numpy as np
+    import pandas as pd
+    import h2o
+    from h2o.estimators import H2OGradientBoostingEstimator, H2OXGBoostEstimator
+    h2o.init(verbose=False)
+    rng = np.random.default_rng(0)
+    n = 3000
+    d = pd.DataFrame({c: rng.normal(size=n) for c in "abcde"})
+    d["y"] = np.where(d.a * d.b + d.c - d.d + rng.normal(size=n) * 0.2 > 0, "1", "0")
+    fr = h2o.H2OFrame(d, column_types={"y": "enum"})
+    for E in (H2OGradientBoostingEstimator, H2OXGBoostEstimator):
+        m = E(ntrees=5, max_depth=4, seed=1, interaction_constraints=[["a", "b"], ["c", "d"]])
+        m.train(x=list("abcde"), y="y", training_frame=fr)
+        for t in m._model.forest.trees:
+            used = {int(f) for f in t.feat if f >= 0}
+            assert used <= {0, 1} or used <= {2, 3}, used
+        with pytest.raises(Exception, match="not a predictor"):
+            E(ntrees=1, interaction_constraints=[["a", "zz"]]).train(x=list("abcde"), y="y", training_frame=fr)

@@ -3,6 +3,8 @@ import numpy as np
 import pytest
 import torch
 
+from llama_github_io_amd.models.shared_tree import interaction_map
+
 from llama_github_io_amd.models.base import DataInfo
 from llama_github_io_amd.models.gbm import GBMTrainer
 from llama_github_io_amd.ops import tree as T
@@ -224,6 +226,39 @@ def _edge_tab(b):
     return tab
 
 
+def test_interaction_constraints_restrict_paths():
+    """GlobalInteractionConstraints / BranchInteractionConstraints: features on one root-to-leaf path all
+    belong to one constraint set; unlisted features are never used."""
+    X, y, info = _data(N=8000, seed=4)
+    b = fit_binning(X, info.iscat, info.nlevels, max_bins=64)
+    bins = apply_binning(b, X)
+    g = y - y.mean()
+    aux = torch.stack([torch.ones_like(y), g, g, torch.ones_like(y)], 1).contiguous()
+    sets = [["x0", "x2"], ["x1", "x3"]]
+    ref = T.RefTreeBuilder(bins, X.shape[0], b.nbins, b.iscat, None, 5, T.SplitParams(min_w=5))
+    ref.set_interaction_constraints(*interaction_map(sets, info.x))
+    ref.build(aux, leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1]).float())
+    tl = ref.pop_levels()[0]
+    groups = [{info.x.index(c) for c in s_} for s_ in sets]
+    # walk every path (decisions per level, children indices in cls/crs)
+    paths = [(0, 0, set())]
+    used = set()
+    while paths:
+        d, i, feats = paths.pop()
+        if d >= len(tl.decs):
+            continue
+        f = int(tl.decs[d]["feat"][i])
+        if f < 0:
+            continue
+        fs = feats | {f}
+        used.add(f)
+        assert any(fs <= gset for gset in groups), fs
+        for c in (int(tl.child_l[d][i]), int(tl.child_r[d][i])):
+            if c >= 0:
+                paths.append((d + 1, c, fs))
+    assert used and used <= {0, 1, 2, 3}
+
+
 def test_uniform_adaptive_lattice_restricts_candidates():
     """UniformAdaptive (DHistogram): at a level with nb adaptive bins, a numeric split lands on one of
     the <= nb - 1 global edges nearest the uniform cut points of the node's occupied range."""
@@ -250,7 +285,8 @@ def test_uniform_adaptive_lattice_restricts_candidates():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["adaptive", "newton", "random", "mono", "kcols", "featok", "multiclass"])
+@pytest.mark.parametrize("case", ["adaptive", "newton", "random", "mono", "kcols", "featok", "multiclass",
+                                  "interaction"])
 def test_gpu_tree_modes_match_reference(case):
     """Every split mode of k_split_find / k_split_reduce pinned against RefTreeBuilder (identical
     feature / bin / left weight per decision and identical leaf assignment)."""
@@ -276,16 +312,23 @@ def test_gpu_tree_modes_match_reference(case):
     elif case == "featok":
         feat_ok = torch.tensor([1, 0, 1, 1, 0, 1], dtype=torch.int32)
         p = T.SplitParams(min_w=10)
+    elif case == "interaction":
+        p = T.SplitParams(min_w=10)
+        ic = interaction_map([["x0", "x2"], ["x1", "x2", "x3"]], info.x)
     else:                                   # multinomial: K independent class trees on per-class aux
         y3 = (X[0] > 0.5).float() + (X[1] > 0).float()
         g = (y3 == 2).float() - (y3 == 2).float().mean()
         aux = torch.stack([torch.ones_like(y), g, g, torch.ones_like(y)], 1).contiguous()
         p = T.SplitParams(min_w=10)
     ref = T.RefTreeBuilder(bins, X.shape[0], b.nbins, b.iscat, mono, depth, p)
+    if case == "interaction":
+        ref.set_interaction_constraints(*ic)
     ref.build(aux, feat_ok, k_cols, seed=77, leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1].clamp(min=1e-12)).float())
     tl_r = ref.pop_levels()[0]
     dev = torch.device("cuda", 0)
     gb = T.GpuTreeBuilder(bins.to(dev), X.shape[0], b.nbins, b.iscat, mono, depth, p)
+    if case == "interaction":
+        gb.set_interaction_constraints(*ic)
     gb.build(aux.to(dev), None if feat_ok is None else feat_ok.to(dev), k_cols, seed=77,
              leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1].clamp(min=1e-12)).float())
     tl_g = gb.pop_levels()[0]
