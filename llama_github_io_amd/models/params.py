@@ -37,7 +37,7 @@ UNSUPPORTED = {
                      "elastic_averaging_regularization", "initial_biases", "initial_weights", "max_categorical_features",
                      "pretrained_autoencoder", "sparse", "sparsity_beta", "score_validation_samples", "rate_decay",
                      "huber_alpha", "missing_values_handling"},
-    "xgboost": {"colsample_bynode", "normalize_type", "sample_type", "grow_policy",
+    "xgboost": {"grow_policy",
                 "max_leaves"},
     "glm": {"cold_start", "dispersion_epsilon", "dispersion_learning_rate", "dispersion_parameter_method",
             "fix_dispersion_parameter", "fix_tweedie_variance_power", "generate_variable_inflation_factors",

@@ -136,7 +136,9 @@ class XGBoostTrainer(SharedTreeTrainer):
         return self.K
 
     def _k_cols(self, F):
-        r = float(self.p.get("col_sample_rate", 1.0))
+        # colsample_bylevel (H2O col_sample_rate) x colsample_bynode: the engine draws a fresh column sample
+        # for every node (XGBoost samples bynode from the level's sample: the expected size is the product)
+        r = float(self.p.get("col_sample_rate", 1.0)) * float(self.p.get("colsample_bynode") or 1.0)
         return 0 if r >= 1.0 else max(1, int(math.floor(F * r + 0.5)))
 
     def _base_score(self):
@@ -175,9 +177,13 @@ class XGBoostTrainer(SharedTreeTrainer):
         if rng.random() < float(p.get("skip_drop", 0)):
             return
         n_iter = len(self.tree_rows) // self.K
-        drop = np.nonzero(rng.random(n_iter) < float(p["rate_drop"]))[0].tolist()
+        tw = np.asarray(self.tree_w[:n_iter], dtype=np.float64)
+        weighted = str(p.get("sample_type") or "uniform").lower() == "weighted"
+        # gbm::Dart::DropTrees: uniform, or in proportion to the trees' current weights
+        prob = float(p["rate_drop"]) * n_iter * tw / tw.sum() if weighted else float(p["rate_drop"])
+        drop = np.nonzero(rng.random(n_iter) < prob)[0].tolist()
         if not drop and p.get("one_drop"):
-            drop = [int(rng.integers(n_iter))]
+            drop = [int(rng.choice(n_iter, p=tw / tw.sum()))] if weighted else [int(rng.integers(n_iter))]
         self.dropped = drop
         for it in drop:
             for k in range(self.K):
@@ -218,14 +224,23 @@ class XGBoostTrainer(SharedTreeTrainer):
     def _update(self, t, k):
         leaf = self.builder.leaf_of_row
         if self.dart:
+            # gbm::Dart::NormalizeTrees (leaf values already carry eta; lr = eta / trees per iteration):
+            #   tree:   new trees weigh 1 / (k + lr), dropped trees are scaled by k / (k + lr)
+            #   forest: new trees weigh 1 / (1 + lr), dropped trees are scaled by 1 / (1 + lr)
             nd = len(self.dropped)
-            wnew = 1.0 / (nd + 1) if nd else 1.0
+            lr = float(self.p["learn_rate"]) / self.K
+            forest = str(self.p.get("normalize_type") or "tree").lower() == "forest"
+            if not nd:
+                wnew, scale = 1.0, 1.0
+            elif forest:
+                wnew = scale = 1.0 / (1.0 + lr)
+            else:
+                wnew, scale = 1.0 / (nd + lr), nd / (nd + lr)
             self.tree_rows.append((k, self._vals.clone(), leaf.clone()))
             if k == 0:
                 self.tree_w.append(wnew)
             self.f[:, k] += wnew * self._vals[leaf.long()]
             if k == self.K - 1 and nd:
-                scale = nd / (nd + 1.0)
                 for it in self.dropped:
                     for kk in range(self.K):
                         _, vals, lf = self.tree_rows[it * self.K + kk]

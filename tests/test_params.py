@@ -173,3 +173,16 @@ def test_interaction_constraints_gbm_xgboost():
             assert used <= {0, 1} or used <= {2, 3}, used
         with pytest.raises(Exception, match="not a predictor"):
             E(ntrees=1, interaction_constraints=[["a", "zz"]]).train(x=list("abcde"), y="y", training_frame=fr)
+
+
+def test_xgboost_dart_modes_and_bynode(fr):
+    """dart sample_type / normalize_type change the model (gbm::Dart::DropTrees / NormalizeTrees);
+    colsample_bynode samples columns per node."""
+    base = dict(booster="dart", ntrees=8, max_depth=3, seed=1, rate_drop=0.5, one_drop=True)
+    preds = []
+    for extra in ({}, dict(sample_type="weighted"), dict(normalize_type="forest"), dict(colsample_bynode=0.5)):
+        m = builder.train("xgboost", dict(base, **extra), x=X, y="y", training_frame=fr)
+        preds.append(m.predict(fr).as_data_frame().iloc[:, -1].to_numpy())
+    import numpy as np
+    for a in preds[1:]:
+        assert not np.allclose(preds[0], a)
