@@ -204,6 +204,9 @@ class DeepLearningTrainer:
         if y is not None and not ae:
             ok = ~torch.isnan(y)
             w = torch.where(ok, w, torch.zeros_like(w))
+        if canon(p.get("missing_values_handling") or "MeanImputation") == "skip":
+            # DataInfo skipMissing: rows with a missing predictor do not train
+            w = torch.where(torch.isnan(X).any(0), torch.zeros_like(w), w)
         sharded = coll.is_dist()
         row0, N_glob = coll.exclusive_offset(N) if sharded else (0, N)
         self._row0, self._N_glob = row0, N_glob
@@ -241,6 +244,7 @@ class DeepLearningTrainer:
             prev_epochs = float(prev.output.get("epochs", 0.0))
             if float(p["epochs"]) <= prev_epochs:
                 raise ValueError(f"epochs must exceed the checkpoint's {prev_epochs}")
+        self._initial_state(net, p, hidden, Z.shape[1], dev)
         if coll.is_dist():
             flat = torch.cat([q.detach().reshape(-1) for q in net.parameters()])
             coll.broadcast_(flat)
@@ -287,6 +291,16 @@ class DeepLearningTrainer:
         l1, l2 = float(p["l1"]), float(p["l2"])
         max_w2 = float(p["max_w2"])
         nesterov = bool(p["nesterov_accelerated_gradient"])
+        # rate_decay (Neurons.java: layer i learns at rate * rate_decay^i) as a per-element multiplier of the
+        # flat parameter buffer (weights of every layer first, then biases)
+        rdec = float(p.get("rate_decay") or 1.0)
+        rmul = None
+        if not adaptive and rdec != 1.0:
+            lins = list(net.hidden) + [net.out]
+            layer_of = {id(l_.weight): i for i, l_ in enumerate(lins)}
+            layer_of.update({id(l_.bias): i for i, l_ in enumerate(lins)})
+            rmul = torch.cat([torch.full((q.numel(),), rdec ** layer_of[id(q)], dtype=torch.float32, device=dev)
+                              for q in params])
         keeper = ScoreKeeper(p["stopping_rounds"], p["stopping_metric"], p["stopping_tolerance"],
                              "Regression" if ae else cat)
         epochs = float(p["epochs"]) - prev_epochs
@@ -332,7 +346,7 @@ class DeepLearningTrainer:
                     nd = fp.n_decay
                     if l2 > 0 or l1 > 0:
                         gg[:nd] += l2 * fp.p[:nd] + l1 * torch.sign(fp.p[:nd])
-                    upd = gg * -rate_t
+                    upd = gg * -rate_t if rmul is None else gg * rmul * -rate_t
                     mom.mul_(mom_t).add_(upd * on_t)
                     if nesterov:
                         fp.p.add_(mom * mom_t + upd)
@@ -500,6 +514,58 @@ class DeepLearningTrainer:
         model.output["run_time_ms"] = int((time.time() - t0) * 1000)
         return model
 
+    @staticmethod
+    def _initial_state(net, p, hidden, n_in, dev):
+        """``pretrained_autoencoder`` (hidden layers copied from an autoencoder of the same shape,
+        DeepLearning.java pretrained AE), ``initial_weights`` / ``initial_biases`` (one frame per layer:
+        weights [units out x units in], biases [units out x 1])."""
+        from ..core import dkv
+        lins = list(net.hidden) + [net.out]
+
+        def resolve(ref):
+            if ref is None:
+                return None
+            obj = dkv.get(ref) if isinstance(ref, str) else ref
+            return getattr(obj, "_model", obj)
+
+        pa = resolve(p.get("pretrained_autoencoder"))
+        if p.get("pretrained_autoencoder"):
+            if pa is None or getattr(pa, "net", None) is None or not pa.params.get("autoencoder"):
+                raise ValueError(f"pretrained_autoencoder {p['pretrained_autoencoder']} is not a DeepLearning autoencoder")
+            if list(pa._cfg["hidden"]) != list(hidden) or pa._cfg["n_in"] != n_in:
+                raise ValueError("pretrained_autoencoder: hidden layers / input width differ from this model's")
+            with torch.no_grad():
+                for a, b in zip(net.hidden, pa.net.hidden):
+                    a.weight.copy_(b.weight.to(dev))
+                    a.bias.copy_(b.bias.to(dev))
+
+        def mats(key):
+            refs = p.get(key)
+            if not refs:
+                return None
+            if len(refs) != len(lins):
+                raise ValueError(f"{key} needs {len(lins)} frames (one per layer), got {len(refs)}")
+            out = []
+            for r in refs:
+                fr = dkv.get(r) if isinstance(r, str) else r
+                fr = getattr(fr, "_frame", fr)
+                if fr is None:
+                    raise ValueError(f"{key}: frame {r!r} not found")
+                out.append(torch.as_tensor(fr.as_data_frame().to_numpy(dtype=np.float64)))
+            return out
+
+        W, Bs = mats("initial_weights"), mats("initial_biases")
+        with torch.no_grad():
+            for i, lin in enumerate(lins):
+                if W is not None:
+                    if tuple(W[i].shape) != tuple(lin.weight.shape):
+                        raise ValueError(f"initial_weights[{i}] must be {tuple(lin.weight.shape)}, got {tuple(W[i].shape)}")
+                    lin.weight.copy_(W[i].to(lin.weight))
+                if Bs is not None:
+                    if Bs[i].numel() != lin.bias.numel():
+                        raise ValueError(f"initial_biases[{i}] must have {lin.bias.numel()} values")
+                    lin.bias.copy_(Bs[i].reshape(-1).to(lin.bias))
+
     def _model_loss(self, m, cat, ae) -> float:
         """hex/Model.java loss(): the stopping metric, or logloss / MSE (autoencoder) / deviance."""
         if m is None:
@@ -580,6 +646,13 @@ class DeepLearningTrainer:
                 ev["training_" + k.lower()] = m[k]
         if valid is not None and not p["autoencoder"]:
             Xv, yv, wv, ov = valid
+            nv = int(p.get("score_validation_samples") or 0)
+            if 0 < nv < Xv.shape[1]:        # score_validation_samples: a fixed random subset of the validation rows
+                vi = torch.randperm(Xv.shape[1], generator=torch.Generator().manual_seed(
+                    (int(p.get("seed") or 0) + 1) & 0x7FFFFFFF))[:nv].to(Xv.device)
+                Xv, yv = Xv[:, vi], yv[vi]
+                wv = None if wv is None else wv[vi]
+                ov = None if ov is None else ov[vi]
             vm = model.metrics_for(Xv, yv, wv, ov)
             ev["_valid"] = vm
             for k in ("RMSE", "logloss", "AUC", "mean_per_class_error"):

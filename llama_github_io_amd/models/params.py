@@ -29,14 +29,15 @@ HINTS = {
     "score_validation_sampling", "u_name", "loading_name", "build_glm_model",
     "compute_metrics", "num_iteration_without_new_exemplar",
     "tree_method", "eval_metric", "export_checkpoints_dir",
+    # DeepLearning: elastic averaging blends per-node local models into the global one between map/reduce
+    # rounds; with synchronous data parallelism every rank holds the global model after each step, so it
+    # is the identity here. ``sparse`` is a storage hint for sparse input.
+    "elastic_averaging", "elastic_averaging_moving_rate", "elastic_averaging_regularization", "sparse",
 }
 
 # parameters not implemented by this engine: a non-default value is refused
 UNSUPPORTED = {
-    "deeplearning": {"average_activation", "elastic_averaging", "elastic_averaging_moving_rate",
-                     "elastic_averaging_regularization", "initial_biases", "initial_weights", "max_categorical_features",
-                     "pretrained_autoencoder", "sparse", "sparsity_beta", "score_validation_samples", "rate_decay",
-                     "huber_alpha", "missing_values_handling"},
+    "deeplearning": {"average_activation", "max_categorical_features", "sparsity_beta", "huber_alpha"},
     "xgboost": {"grow_policy",
                 "max_leaves"},
     "glm": {"cold_start", "dispersion_epsilon", "dispersion_learning_rate", "dispersion_parameter_method",

@@ -40,7 +40,7 @@ def test_unknown_parameter_raises(fr):
 @pytest.mark.parametrize("algo,param,value", [
     ("kmeans", "cluster_size_constraints", [10, 20]),
     ("xgboost", "grow_policy", "lossguide"),
-    ("deeplearning", "initial_weights", ["w"]),
+    ("deeplearning", "sparsity_beta", 0.5),
     ("glm", "influence", "dfbetas"),
 ])
 def test_unsupported_parameter_raises(fr, algo, param, value):
@@ -186,3 +186,25 @@ def test_xgboost_dart_modes_and_bynode(fr):
     import numpy as np
     for a in preds[1:]:
         assert not np.allclose(preds[0], a)
+
+
+def test_deeplearning_initial_state_and_options(fr):
+    """initial_weights / initial_biases, pretrained_autoencoder, rate_decay, Skip missing values and
+    score_validation_samples are honoured by DeepLearning."""
+    import numpy as np
+    import h2o
+    base = dict(hidden=[4], epochs=0.001, seed=1, mini_batch_size=8, score_interval=1e9, stopping_rounds=0,
+                adaptive_rate=False, rate=0.0)
+    m0 = builder.train("deeplearning", dict(base), x=X, y="y", training_frame=fr)
+    W = [h2o.H2OFrame(np.full(tuple(m0.net.hidden[0].weight.shape), 0.01)),
+         h2o.H2OFrame(np.full(tuple(m0.net.out.weight.shape), -0.02))]
+    B = [h2o.H2OFrame(np.zeros((4, 1))), h2o.H2OFrame(np.zeros((2, 1)))]
+    m1 = builder.train("deeplearning", dict(base, initial_weights=W, initial_biases=B), x=X, y="y", training_frame=fr)
+    # rate 0: the weights stay exactly at their initial values
+    assert np.allclose(m1.weights(0), 0.01) and np.allclose(m1.weights(1), -0.02) and np.allclose(m1.biases(0), 0)
+    ae = builder.train("deeplearning", dict(hidden=[4], epochs=1, seed=2, autoencoder=True, score_interval=1e9),
+                       x=X, training_frame=fr)
+    m2 = builder.train("deeplearning", dict(base, pretrained_autoencoder=ae.key), x=X, y="y", training_frame=fr)
+    assert np.allclose(m2.weights(0), ae.weights(0), atol=1e-6)
+    for extra in (dict(rate_decay=0.5), dict(missing_values_handling="Skip"), dict(score_validation_samples=10)):
+        builder.train("deeplearning", dict(base, epochs=1, rate=0.01, **extra), x=X, y="y", training_frame=fr)
