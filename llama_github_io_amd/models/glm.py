@@ -150,6 +150,28 @@ class Family:
             return 2 * (t1 - (y + 1 / th) * torch.log((1 + th * y) / (1 + th * m)))
         raise ValueError(n)
 
+    def loglik(self, y, mu, w, phi):
+        """Weighted log-likelihood at dispersion ``phi`` (GLMModel likelihood for calc_like)."""
+        n = self.name
+        if n == "gaussian":
+            return _gsum((w * (-0.5 * (y - mu) ** 2 / phi - 0.5 * math.log(2 * math.pi * phi))).sum())
+        if n in ("binomial", "quasibinomial", "fractionalbinomial"):
+            m = mu.clamp(1e-15, 1 - 1e-15)
+            return _gsum((w * (y * torch.log(m) + (1 - y) * torch.log(1 - m))).sum())
+        if n == "poisson":
+            return _gsum((w * (y * torch.log(mu.clamp(min=1e-300)) - mu - torch.lgamma(y + 1))).sum())
+        if n == "gamma":
+            k = 1.0 / phi
+            yc = y.clamp(min=1e-300)
+            return _gsum((w * (k * torch.log(k * yc / mu) - k * yc / mu - torch.log(yc) - math.lgamma(k))).sum())
+        if n == "negativebinomial":
+            th = self.theta
+            r = 1.0 / th
+            return _gsum((w * (torch.lgamma(y + r) - torch.lgamma(y + 1) - math.lgamma(r) + r * math.log(r)
+                               - r * torch.log(r + mu) + y * torch.log(mu.clamp(min=1e-300))
+                               - y * torch.log(r + mu))).sum())
+        return float("nan")
+
     def loglik_aic(self, y, mu, w, dev_sum, nobs, rank):
         n = self.name
         if n == "gaussian":
@@ -161,6 +183,74 @@ class Family:
             ll = _gsum((w * (y * torch.log(mu.clamp(min=1e-300)) - mu - torch.lgamma(y + 1))).sum())
             return float(-2 * ll) + 2 * rank
         return float("nan")
+
+
+def estimate_dispersion(family, y, mu, w, nobs, rank, res_dev, method="pearson", max_it=50, eps=1e-4):
+    """Dispersion φ (GLM.java estimateDispersion / dispersion_parameter_method): ``pearson`` Σ w(y-μ)²/V(μ) /
+    (n - p), ``deviance`` D / (n - p), ``ml`` maximum likelihood (gaussian: D / n; gamma: Newton on the shape
+    1/φ; negative binomial: Newton on θ with μ fixed). Families without a dispersion return 1."""
+    n = family.name
+    if n in ("binomial", "poisson", "quasibinomial", "fractionalbinomial", "multinomial", "ordinal"):
+        return 1.0
+    dfree = max(nobs - rank, 1)
+    method = str(method).lower()
+    if method == "deviance":
+        return res_dev / dfree
+    if method == "ml":
+        if n == "gaussian":
+            return res_dev / max(nobs, 1)
+        if n == "gamma":
+            from scipy.special import digamma, polygamma
+            yc = y.clamp(min=1e-300)
+            W = _gsum(w.sum())
+            c = _gsum((w * (torch.log(yc / mu) - yc / mu)).sum())
+            k = 1.0 / max(estimate_dispersion(family, y, mu, w, nobs, rank, res_dev, "pearson"), 1e-8)
+            for _ in range(max_it):
+                g = W * (math.log(k) + 1 - float(digamma(k))) + c
+                h = W * (1.0 / k - float(polygamma(1, k)))
+                nk = k - g / h if h != 0 else k
+                nk = nk if nk > 0 else k / 2
+                if abs(nk - k) < eps * k:
+                    k = nk
+                    break
+                k = nk
+            return 1.0 / k
+        if n == "negativebinomial":
+            from scipy.special import digamma, polygamma
+            yy, mm_, ww = y.double().cpu().numpy(), mu.double().cpu().numpy(), w.double().cpu().numpy()
+            th = max(family.theta, 1e-3)
+            for _ in range(max_it):       # d/dθ of the NB log-likelihood (r = 1/θ), Newton in r
+                r = 1.0 / th
+                g = (ww * (digamma(yy + r) - digamma(r) + np.log(r) + 1 - np.log(r + mm_) - (yy + r) / (r + mm_))).sum()
+                h = (ww * (polygamma(1, yy + r) - polygamma(1, r) + 1 / r - 2 / (r + mm_)
+                           + (yy + r) / (r + mm_) ** 2)).sum()
+                nr = r - g / h if h != 0 else r
+                nr = nr if nr > 0 else r / 2
+                if abs(nr - r) < eps * r:
+                    r = nr
+                    th = 1.0 / r
+                    break
+                th = 1.0 / nr
+            return th
+        raise ValueError(f"dispersion_parameter_method='ml' is not available for family {n}")
+    return _gsum((w * (y - mu) ** 2 / family.variance(mu).clamp(min=1e-30)).sum()) / dfree
+
+
+def variance_inflation_factors(ex, X, w):
+    """VIF of every numeric predictor: 1 / (1 - R²_j) of regressing it on the other numeric predictors,
+    = diag(R⁻¹) of their weighted correlation matrix (GLM generate_variable_inflation_factors)."""
+    if len(ex.nums) < 2:
+        return {ex.info.x[j]: float("nan") for j in ex.nums}
+    Xn = torch.stack([torch.nan_to_num(X[j].double(), nan=float(ex.num_mean[i])) for i, j in enumerate(ex.nums)], 1)
+    wd = w.double()
+    W = _gsum(wd.sum())
+    mu = _gvec((Xn * wd[:, None]).sum(0)) / W
+    Xc = Xn - mu
+    C = _gvec((Xc * wd[:, None]).T @ Xc) / W
+    sd = C.diagonal().clamp(min=1e-300).sqrt()
+    R = C / (sd[:, None] * sd[None, :])
+    v = torch.linalg.pinv(R).diagonal()
+    return {ex.info.x[j]: float(v[i]) for i, j in enumerate(ex.nums)}
 
 
 # ------------------------------------------------------------------------------------------------
@@ -445,6 +535,7 @@ class GLMTrainer:
             fixed |= self._collinear(Zi, w, intercept)
             self.collinear = [ex.names[j] for j in torch.nonzero(fixed[:-1]).flatten().tolist()]
         beta = torch.where(fixed, torch.zeros_like(beta), beta)
+        beta_start = beta.clone()
         # gradient at the null model -> lambda max
         eta = G.zbeta(Zi, beta, off)
         mu = fam.linkinv(eta)
@@ -477,6 +568,8 @@ class GLMTrainer:
         null_dev = _gsum((w * fam.deviance(y, torch.full_like(y, ymu))).sum())
         for li, lam in enumerate(lambdas):
             l1, l2 = lam * alpha, lam * (1 - alpha)
+            if p.get("cold_start") and li > 0:     # cold_start: every lambda starts from the initial coefficients
+                beta = beta_start.clone()
             for it in range(max(max_it, 1)):
                 eta = G.zbeta(Zi, beta, off)
                 mu = fam.linkinv(eta)
@@ -800,6 +893,21 @@ class GLMTrainer:
             rank = int((beta[0].abs() > 0).sum())
             out.update(residual_deviance=res_dev, null_deviance=null_dev, null_degrees_of_freedom=nobs - (1 if p["intercept"] else 0),
                        residual_degrees_of_freedom=nobs - rank, aic=family.loglik_aic(y, mu, w, res_dev, nobs, rank))
+            if p.get("fix_dispersion_parameter"):
+                self._disp = float(p.get("init_dispersion_parameter") or 1.0)
+            else:
+                self._disp = estimate_dispersion(family, y, mu, w, nobs, rank, res_dev,
+                                                 p.get("dispersion_parameter_method") or "pearson",
+                                                 int(p.get("max_iterations_dispersion") or 50),
+                                                 float(p.get("dispersion_epsilon") or 1e-4))
+            if family.name in ("gaussian", "gamma", "tweedie", "negativebinomial"):
+                out["dispersion"] = self._disp
+            if p.get("calc_like"):
+                phi = self._disp if family.name != "negativebinomial" else 1.0
+                ll = family.loglik(y, mu, w, phi)
+                k = rank + (1 if family.name in ("gaussian", "gamma", "negativebinomial") else 0)
+                out["loglikelihood"] = ll
+                out["aic"] = -2 * ll + 2 * k
             if p["compute_p_values"]:
                 self._p_values(model, family, Zi, y, w, off, beta[0], names, nobs, rank, ex)
         else:
@@ -819,6 +927,10 @@ class GLMTrainer:
             if cat == "Regression":
                 tm["mean_residual_deviance"] = out["residual_deviance"] / max(_gsum(w.sum()), 1e-300)
         out["training_metrics"] = tm
+        if tm is not None and "loglikelihood" in out:
+            tm["loglikelihood"] = out["loglikelihood"]
+        if p.get("generate_variable_inflation_factors"):
+            out["variable_inflation_factors"] = variance_inflation_factors(ex, X, w)
         imp = [(n[: n.rfind("_")] if K > 1 else n, abs(v)) for n, v in coefs_std.items() if not n.startswith("Intercept")]
         agg = {}
         for n, v in imp:
@@ -838,8 +950,10 @@ class GLMTrainer:
         Gm = _gvec(G.gram(Zi, wi.float()))
         if family.name in ("binomial", "poisson", "quasibinomial", "fractionalbinomial"):
             disp = 1.0
-        else:
-            disp = _gsum((w * (y - mu) ** 2 / var.clamp(min=1e-30)).sum()) / max(nobs - rank, 1)
+        else:        # dispersion_parameter_method / fix_dispersion_parameter (estimated in _outputs)
+            disp = getattr(self, "_disp", None)
+            if disp is None:
+                disp = _gsum((w * (y - mu) ** 2 / var.clamp(min=1e-30)).sum()) / max(nobs - rank, 1)
         cov = torch.linalg.pinv(Gm) * disp
         se_std = cov.diagonal().clamp(min=0).sqrt()
         # raw-scale standard errors: numeric coefficient j scales by 1/sd_j; intercept via the delta method

@@ -28,7 +28,7 @@ HINTS = {
     "score_iteration_interval", "classification_stop", "regression_stop", "train_samples_per_iteration",
     "score_validation_sampling", "u_name", "loading_name", "build_glm_model",
     "compute_metrics", "num_iteration_without_new_exemplar",
-    "tree_method", "eval_metric", "export_checkpoints_dir",
+    "tree_method", "eval_metric", "export_checkpoints_dir", "gradient_epsilon",
     # DeepLearning: elastic averaging blends per-node local models into the global one between map/reduce
     # rounds; with synchronous data parallelism every rank holds the global model after each step, so it
     # is the identity here. ``sparse`` is a storage hint for sparse input.
@@ -40,10 +40,8 @@ UNSUPPORTED = {
     "deeplearning": {"average_activation", "max_categorical_features", "sparsity_beta", "huber_alpha"},
     "xgboost": {"grow_policy",
                 "max_leaves"},
-    "glm": {"cold_start", "dispersion_epsilon", "dispersion_learning_rate", "dispersion_parameter_method",
-            "fix_dispersion_parameter", "fix_tweedie_variance_power", "generate_variable_inflation_factors",
-            "influence", "init_dispersion_parameter", "max_iterations_dispersion", "rand_link", "tweedie_epsilon",
-            "calc_like", "checkpoint", "prior", "gradient_epsilon", "early_stopping"},
+    "glm": {"dispersion_learning_rate", "fix_tweedie_variance_power", "influence", "rand_link", "tweedie_epsilon",
+            "checkpoint", "prior", "early_stopping"},
     "gam": {"beta_constraints", "cold_start", "interaction_pairs", "interactions",
             "max_active_predictors", "remove_collinear_columns", "standardize_tp_gam_cols", "startval", "prior",
             "gradient_epsilon", "objective_epsilon", "early_stopping", "plug_values"},

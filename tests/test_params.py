@@ -208,3 +208,38 @@ def test_deeplearning_initial_state_and_options(fr):
     assert np.allclose(m2.weights(0), ae.weights(0), atol=1e-6)
     for extra in (dict(rate_decay=0.5), dict(missing_values_handling="Skip"), dict(score_validation_samples=10)):
         builder.train("deeplearning", dict(base, epochs=1, rate=0.01, **extra), x=X, y="y", training_frame=fr)
+
+
+def test_glm_dispersion_vif_likelihood():
+    """GLM dispersion_parameter_method (pearson / deviance / ml, fixed), generate_variable_inflation_factors
+    (= 1 / (1 - R²) of the OLS of each predictor on the others), calc_like, cold_start."""
+    import numpy as np
+    import torch
+    from llama_github_io_amd.models.base import DataInfo
+    from llama_github_io_amd.models.glm import GLMTrainer
+    rng = np.random.default_rng(5)
+    n = 4000
+    a = rng.normal(size=n)
+    b = 0.8 * a + 0.6 * rng.normal(size=n)
+    c = rng.normal(size=n)
+    X = torch.tensor(np.stack([a, b, c]), dtype=torch.float32)
+    mu = np.exp(0.3 + 0.2 * a - 0.1 * c)
+    shape = 4.0
+    yg = torch.tensor(rng.gamma(shape, mu / shape))
+    info = DataInfo(["a", "b", "c"], np.zeros(3, np.int32), [None] * 3, "y", None)
+    res = {}
+    for meth in ("pearson", "deviance", "ml"):
+        m = GLMTrainer(dict(family="gamma", link="log", lambda_=0.0, dispersion_parameter_method=meth,
+                            calc_like=True, generate_variable_inflation_factors=True)).fit(X, yg, None, None, info)
+        res[meth] = m.output["dispersion"]
+    assert all(abs(v - 1 / shape) < 0.04 for v in res.values()), res
+    fixed = GLMTrainer(dict(family="gamma", link="log", lambda_=0.0, fix_dispersion_parameter=True,
+                            init_dispersion_parameter=0.5)).fit(X, yg, None, None, info)
+    assert fixed.output["dispersion"] == 0.5
+    vif = m.output["variable_inflation_factors"]
+    r2 = np.corrcoef(a, b)[0, 1] ** 2
+    assert abs(vif["a"] - 1 / (1 - r2)) < 0.05 and abs(vif["c"] - 1.0) < 0.05
+    assert np.isfinite(m.output["loglikelihood"]) and m.output["aic"] == pytest.approx(-2 * m.output["loglikelihood"] + 2 * 5)
+    cold = GLMTrainer(dict(family="gaussian", lambda_search=True, nlambdas=5, cold_start=True)).fit(
+        X, torch.tensor(a + c), None, None, info)
+    assert len(cold.output.get("lambda_path", cold.output.get("regularization_path", [0]))) >= 1
