@@ -42,9 +42,7 @@ UNSUPPORTED = {
                 "max_leaves"},
     "glm": {"dispersion_learning_rate", "fix_tweedie_variance_power", "influence", "rand_link", "tweedie_epsilon",
             "checkpoint", "prior", "early_stopping"},
-    "gam": {"beta_constraints", "cold_start", "interaction_pairs", "interactions",
-            "max_active_predictors", "remove_collinear_columns", "standardize_tp_gam_cols", "startval", "prior",
-            "gradient_epsilon", "objective_epsilon", "early_stopping", "plug_values"},
+    "gam": {"beta_constraints", "standardize_tp_gam_cols", "prior", "early_stopping"},
     "anovaglm": {"early_stopping", "prior", "type", "plug_values"},
     "modelselection": {"beta_constraints", "cold_start", "influence", "max_active_predictors", "prior",
                        "remove_collinear_columns", "startval", "p_values_threshold", "gradient_epsilon",

@@ -73,3 +73,29 @@ def test_mspline(data):
     m.train(x=["c"], y="y", training_frame=fr)             # b**2 is left out: pred ~ sin(a) + shift + const
     pred = m.predict(fr).as_data_frame()["predict"].values
     assert np.corrcoef(pred, np.sin(a) + shift)[0, 1] > 0.95
+
+
+def test_gam_passes_glm_options_through():
+    """GAM's linear part honours the GLM options it shares (interactions, max_active_predictors,
+    remove_collinear_columns, cold_start, objective_epsilon)."""
+    import numpy as np
+    import pandas as pd
+    import h2o
+    from h2o.estimators import H2OGeneralizedAdditiveEstimator
+    h2o.init(verbose=False)
+    rng = np.random.default_rng(7)
+    n = 2000
+    d = pd.DataFrame({"a": rng.normal(size=n), "b": rng.normal(size=n), "c": rng.normal(size=n)})
+    d["c2"] = d["c"] * 2.0
+    d["y"] = np.sin(d.a) + d.b * d.c + rng.normal(size=n) * 0.1
+    fr = h2o.H2OFrame(d)
+    base = dict(gam_columns=["a"], num_knots=[6], lambda_=0.0)
+    m0 = H2OGeneralizedAdditiveEstimator(**base)
+    m0.train(x=["a", "b", "c"], y="y", training_frame=fr)
+    m1 = H2OGeneralizedAdditiveEstimator(interactions=["b", "c"], **base)
+    m1.train(x=["a", "b", "c"], y="y", training_frame=fr)
+    assert m1._model.output["training_metrics"]["MSE"] < 0.5 * m0._model.output["training_metrics"]["MSE"]
+    m2 = H2OGeneralizedAdditiveEstimator(remove_collinear_columns=True, **base)
+    m2.train(x=["a", "b", "c", "c2"], y="y", training_frame=fr)
+    m3 = H2OGeneralizedAdditiveEstimator(cold_start=True, objective_epsilon=1e-6, **base)
+    m3.train(x=["a", "b", "c"], y="y", training_frame=fr)
