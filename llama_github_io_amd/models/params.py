@@ -53,7 +53,6 @@ UNSUPPORTED = {
     "kmeans": {"cluster_size_constraints"},
     "psvm": {"feasible_threshold", "kernel_type", "mu_factor", "surrogate_gap_threshold"},
     "word2vec": {"norm_model", "pre_trained", "word_model"},
-    "upliftdrf": {"auuc_nbins", "auuc_type"},
     "rulefit": {"max_categorical_levels"},
     "stackedensemble": {"score_training_samples"},
     "infogram": {"max_iterations", "data_fraction"},

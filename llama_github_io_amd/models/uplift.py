@@ -42,8 +42,10 @@ def _D(kind, pt, pc):
     return _metric(kind, pt, pc) + _metric(kind, 1 - pt, 1 - pc)
 
 
-def auuc(uplift, y, treat, nbins=1000):
-    """Qini / lift / gain AUUC over uplift-sorted rows (AUUC.java)."""
+def auuc(uplift, y, treat, nbins=1000, auuc_type="AUTO"):
+    """Qini / lift / gain AUUC over uplift-sorted rows (AUUC.java); ``AUUC`` is the ``auuc_type`` curve
+    (AUTO = qini) averaged over ``nbins`` thresholds."""
+    nbins = 1000 if nbins is None or int(nbins) <= 0 else int(nbins)
     order = torch.argsort(uplift, descending=True)
     y, t = y[order].double(), treat[order].double()
     nt = torch.cumsum(t, 0)
@@ -56,8 +58,14 @@ def auuc(uplift, y, treat, nbins=1000):
     qini = yt - yc * nt / nc.clamp(min=1)
     lift = yt / nt.clamp(min=1) - yc / nc.clamp(min=1)
     gain = lift * (nt + nc)
-    return dict(qini=float(qini.mean()), lift=float(lift.mean()), gain=float(gain.mean()),
-                AUUC=float(qini.mean()), auuc_table=dict(qini=qini.cpu().tolist()))
+    curves = dict(qini=qini, lift=lift, gain=gain)
+    kind = str(auuc_type or "AUTO").lower()
+    kind = "qini" if kind == "auto" else kind
+    if kind not in curves:
+        raise ValueError(f"auuc_type must be AUTO, qini, lift or gain, got {auuc_type!r}")
+    return dict(qini=float(qini.mean()), lift=float(lift.mean()), gain=float(gain.mean()), auuc_type=kind,
+                auuc_nbins=int(idx.numel()), AUUC=float(curves[kind].mean()),
+                auuc_table={k: v.cpu().tolist() for k, v in curves.items()})
 
 
 class UpliftDRFModel(Model):
@@ -122,7 +130,7 @@ class UpliftDRFTrainer:
         model.f_t, model.f_c = f_t, f_c
         model.output["model_category"] = "BinomialUplift"
         P = model._predict_tensor(Xs)
-        model.output["training_metrics"] = auuc(P[:, 0], yv, treat)
+        model.output["training_metrics"] = auuc(P[:, 0], yv, treat, p.get("auuc_nbins"), p.get("auuc_type"))
         model.output["training_metrics"]["model_category"] = "BinomialUplift"
         model.output["run_time_ms"] = int((time.time() - t0) * 1000)
         return model

@@ -86,6 +86,13 @@ def test_uplift_te_aggregator_eif(df):
     u = H2OUpliftRandomForestEstimator(ntrees=5, max_depth=4, treatment_column="t", seed=1)
     u.train(x=["a", "b", "t"], y="y", training_frame=df)
     assert u.predict(df).names == ["uplift_predict", "p_y1_with_treatment", "p_y1_without_treatment"]
+    tm = u._model.output["training_metrics"]
+    assert tm["auuc_type"] == "qini" and tm["AUUC"] == tm["qini"]
+    u2 = H2OUpliftRandomForestEstimator(ntrees=5, max_depth=4, treatment_column="t", seed=1, auuc_type="gain",
+                                        auuc_nbins=50)
+    u2.train(x=["a", "b", "t"], y="y", training_frame=df)
+    tm2 = u2._model.output["training_metrics"]
+    assert tm2["auuc_nbins"] == 50 and tm2["AUUC"] == tm2["gain"] and len(tm2["auuc_table"]["gain"]) == 50
     te = H2OTargetEncoderEstimator(blending=True)
     te.train(x=["c"], y="y", training_frame=df)
     assert "c_te" in te.transform(df).names
