@@ -205,7 +205,7 @@ def fit_adapter(algo: str, p: dict, fr, x: list, y):
                 steps.append(dict(kind="eigen", col=n, levels=levels, vec=v.tolist()))
                 i = new_x.index(n)
                 new_x[i] = f"{n}.Eigen"
-    if algo in ("glm", "gam") and (p.get("interactions") or p.get("interaction_pairs")):
+    if algo in ("glm", "gam", "coxph") and (p.get("interactions") or p.get("interaction_pairs")):
         pairs = []
         inter = p.get("interactions") or []
         inter = [inter] if isinstance(inter, str) else list(inter)
@@ -238,6 +238,11 @@ def fit_adapter(algo: str, p: dict, fr, x: list, y):
                 seen = [(int(v) // (len(lb) + 1), int(v) % (len(lb) + 1)) for v in u.cpu().tolist()]
                 steps.append(dict(kind="interaction", type="cc", a=a, b=b, la=la, lb=lb, pairs=seen, name=f"{a}_{b}"))
                 new_x.append(f"{a}_{b}")
+        if algo == "coxph" and p.get("interactions_only"):
+            # CoxPH interactions_only: these columns enter the model only through their interaction terms
+            only = p["interactions_only"]
+            only = {only} if isinstance(only, str) else set(only)
+            new_x = [c for c in new_x if c not in only]
     if not steps:
         return None, fr, x
     ad = FrameAdapter(steps)

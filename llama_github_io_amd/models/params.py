@@ -47,7 +47,6 @@ UNSUPPORTED = {
     "modelselection": {"beta_constraints", "cold_start", "influence", "max_active_predictors", "prior",
                        "remove_collinear_columns", "startval", "p_values_threshold", "gradient_epsilon",
                        "objective_epsilon", "early_stopping", "plug_values"},
-    "coxph": {"interaction_pairs", "interactions", "interactions_only"},
     "glrm": {"loss_by_col", "loss_by_col_idx", "multi_loss", "user_x", "svd_method", "expand_user_y",
              "impute_original", "recover_svd", "max_updates"},
     "kmeans": {"cluster_size_constraints"},

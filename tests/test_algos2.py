@@ -130,3 +130,21 @@ def test_mojo_roundtrip_generic(df, tmp_path):
     b = g.predict(df).as_data_frame()
     assert np.allclose(a["1"].values, b["1"].values, atol=1e-6)
     assert (a["predict"] == b["predict"]).all()
+
+
+def test_coxph_interactions():
+    """CoxPH interactions / interactions_only (CoxPH.java): the x1:x2 term is estimated, and with
+    interactions_only the main effects are left out."""
+    rng = np.random.default_rng(1)
+    n = 3000
+    x1, x2 = rng.normal(size=n), rng.normal(size=n)
+    T = rng.exponential(1 / np.exp(0.5 * x1 + 0.7 * x1 * x2))
+    C = rng.exponential(3.0, n)
+    fr = h2o.H2OFrame(pd.DataFrame({"x1": x1, "x2": x2, "time": np.minimum(T, C), "event": (T <= C).astype(int)}))
+    m = H2OCoxProportionalHazardsEstimator(stop_column="time", interactions=["x1", "x2"])
+    m.train(x=["x1", "x2", "time"], y="event", training_frame=fr)
+    co = m._model.output["coefficients"]
+    assert abs(co["x1:x2"] - 0.7) < 0.15 and abs(co["x1"] - 0.5) < 0.15
+    m2 = H2OCoxProportionalHazardsEstimator(stop_column="time", interactions=["x1", "x2"], interactions_only=["x2"])
+    m2.train(x=["x1", "x2", "time"], y="event", training_frame=fr)
+    assert "x2" not in m2._model.output["coefficients"] and "x1:x2" in m2._model.output["coefficients"]
