@@ -258,6 +258,17 @@ def _train(spec, algo, p, x, y, fr, validation_frame, job, model_id):
     valid = None
     if validation_frame is not None:
         Xv, yvv, wv, ov = tensors(validation_frame, info, device=X.device)
+        vrc = p.get("validation_response_column")
+        if vrc and yvv is None:
+            # IsolationForest validation_response_column: labelled anomalies of the validation frame
+            if vrc not in validation_frame.names:
+                raise ValueError(f"validation_response_column {vrc!r} is not in the validation frame")
+            col = validation_frame._col(vrc)
+            if col.domain is None or len(col.domain) != 2:
+                raise ValueError("validation_response_column must be a binary categorical column")
+            yvv = col.data.to(X.device).float()
+            yvv = torch.where(yvv < 0, torch.full_like(yvv, float("nan")), yvv)
+            p["_valid_domain"] = list(col.domain)
         valid = (Xv, yvv, wv, ov)
     mid = model_id or p.get("model_id") or make_key(algo)
     seed = _seed_of(p)

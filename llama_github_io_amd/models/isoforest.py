@@ -88,7 +88,15 @@ class IsolationForestTrainer(SharedTreeTrainer):
         self.label_info = info
         N = X.shape[1]
         yy = torch.zeros(N, device=X.device)
-        return super().fit(X, yy, w, offset, info2, None, model_key)
+        model = super().fit(X, yy, w, offset, info2, None, model_key)
+        if valid is not None and valid[1] is not None:
+            # validation_response_column: binomial metrics of the normalised anomaly score against the labels
+            Xv, yv = valid[0], valid[1]
+            P = model._predict_tensor(Xv)
+            ok = ~torch.isnan(yv)
+            dom = self.p.get("_valid_domain") or ["0", "1"]
+            model.output["validation_metrics"] = mm.binomial_metrics(yv[ok], P[ok, -2], None, dom)
+        return model
 
     def _init_model(self, model):
         model.output["model_category"] = "AnomalyDetection"

@@ -55,7 +55,6 @@ UNSUPPORTED = {
     "rulefit": {"max_categorical_levels"},
     "stackedensemble": {"score_training_samples"},
     "infogram": {"max_iterations", "data_fraction"},
-    "isolationforest": {"validation_response_column"},
 }
 
 # values that count as "left at its default" whatever the schema says

@@ -148,3 +148,19 @@ def test_coxph_interactions():
     m2 = H2OCoxProportionalHazardsEstimator(stop_column="time", interactions=["x1", "x2"], interactions_only=["x2"])
     m2.train(x=["x1", "x2", "time"], y="event", training_frame=fr)
     assert "x2" not in m2._model.output["coefficients"] and "x1:x2" in m2._model.output["coefficients"]
+
+
+def test_isolation_forest_validation_response_column():
+    rng = np.random.default_rng(2)
+    n = 2000
+    a, b = rng.normal(size=n), rng.normal(size=n)
+    lab = np.zeros(n, int)
+    lab[:60] = 1
+    a[:60] += 6
+    fr = h2o.H2OFrame(pd.DataFrame({"a": a, "b": b}))
+    vf = h2o.H2OFrame(pd.DataFrame({"a": a, "b": b, "label": lab.astype(str)}), column_types={"label": "enum"})
+    from h2o.estimators import H2OIsolationForestEstimator
+    m = H2OIsolationForestEstimator(ntrees=30, seed=1, validation_response_column="label")
+    m.train(x=["a", "b"], training_frame=fr, validation_frame=vf)
+    vm = m._model.output["validation_metrics"]
+    assert vm is not None and vm["AUC"] > 0.75
