@@ -179,6 +179,11 @@ def train(algo: str, params: dict, x=None, y=None, training_frame=None, validati
         m.algo = "generic"
         dkv.put(m.key, m)
         return m
+    if algo == "word2vec" and p.get("pre_trained") is not None:
+        # Word2Vec pre_trained: the model is the given [word, v1..vD] frame (no training)
+        m = spec.trainer(p).from_pretrained(p["pre_trained"], model_id or p.get("model_id"))
+        dkv.put(m.key, m)
+        return m
     if spec.supervised and y is None and not spec.needs_response_optional:
         raise ValueError(f"{algo} needs a response column y")
     fr = training_frame

@@ -51,7 +51,7 @@ UNSUPPORTED = {
              "impute_original", "recover_svd", "max_updates"},
     "kmeans": {"cluster_size_constraints"},
     "psvm": {"feasible_threshold", "kernel_type", "mu_factor", "surrogate_gap_threshold"},
-    "word2vec": {"norm_model", "pre_trained", "word_model"},
+    "word2vec": {"word_model"},
     "rulefit": {"max_categorical_levels"},
     "stackedensemble": {"score_training_samples"},
     "infogram": {"max_iterations", "data_fraction"},

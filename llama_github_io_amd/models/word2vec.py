@@ -129,6 +129,30 @@ class Word2VecTrainer:
         self.job = None
         self.strings = None    # the builder passes the raw string column via fit_strings
 
+    def from_pretrained(self, frame, model_key=None):
+        """Word2Vec.java pre-trained mode: a frame of [word (string/enum), v1 .. vD (numeric)] becomes the
+        embedding as is."""
+        from ..core import dkv
+        fr = dkv.get(frame) if isinstance(frame, str) else frame
+        fr = getattr(fr, "_frame", fr)
+        if fr is None or fr.ncols < 2:
+            raise ValueError("pre_trained needs a frame of a word column followed by the vector columns")
+        wc = fr._col(fr.names[0])
+        if fr.type(fr.names[0]) == "enum":
+            words = [wc.domain[int(c)] for c in wc.data.cpu().tolist()]
+        else:
+            words = [str(v) for v in wc.to_numpy()]
+        V = torch.stack([fr._col(n).as_float().double() for n in fr.names[1:]], 1).float()
+        info = DataInfo([fr.names[0]], np.zeros(1, np.int32), [None], None, None)
+        m = Word2VecModel(model_key or make_key("word2vec"), dict(self.p, vec_size=V.shape[1]), info)
+        m.words = words
+        m.vocab = {w_: i for i, w_ in enumerate(words)}
+        m.vectors = V
+        m.output["model_category"] = "WordEmbedding"
+        m.output["vec_size"] = V.shape[1]
+        m.output["vocab_size"] = len(words)
+        return m
+
     def fit(self, X, y, w, offset, info: DataInfo, valid=None, model_key=None):
         if self.strings is None:
             raise ValueError("word2vec trains from a string column (use the estimator API)")

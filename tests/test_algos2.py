@@ -164,3 +164,13 @@ def test_isolation_forest_validation_response_column():
     m.train(x=["a", "b"], training_frame=fr, validation_frame=vf)
     vm = m._model.output["validation_metrics"]
     assert vm is not None and vm["AUC"] > 0.75
+
+
+def test_word2vec_pre_trained():
+    emb = pd.DataFrame({"Word": ["king", "queen", "apple", "pear"], "V1": [1.0, 0.9, -1.0, -0.9],
+                        "V2": [0.1, 0.2, 0.5, 0.4]})
+    fr = h2o.H2OFrame(emb, column_types={"Word": "string"})
+    m = H2OWord2vecEstimator(pre_trained=fr, vec_size=2)
+    m.train()
+    syn = m._model.find_synonyms("king", 1)
+    assert list(syn) == ["queen"]
