@@ -80,6 +80,15 @@ class InfogramTrainer:
     def fit(self, X, y, w, offset, info: DataInfo, valid=None, model_key=None):
         t0 = time.time()
         p = self.p
+        frac = float(p.get("data_fraction") or 1.0)
+        if not 0 < frac <= 1:
+            raise ValueError("data_fraction must be in (0, 1]")
+        if frac < 1.0:      # Infogram data_fraction: the CMI / relevance models see a random row sample
+            from .shared_tree import resolve_seed
+            g = torch.Generator().manual_seed(resolve_seed(p.get("seed", -1)) & 0x7FFFFFFF)
+            keep = (torch.rand(X.shape[1], generator=g) < frac).to(X.device)
+            X, y = X[:, keep], y[keep]
+            w = None if w is None else w[keep]
         prot = [c for c in (p["protected_columns"] or []) if c in info.x]
         prot_idx = [info.x.index(c) for c in prot]
         cand = [j for j in range(info.F) if j not in prot_idx]

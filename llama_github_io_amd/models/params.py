@@ -53,8 +53,7 @@ UNSUPPORTED = {
     "psvm": {"feasible_threshold", "kernel_type", "mu_factor", "surrogate_gap_threshold"},
     "word2vec": {"word_model"},
     "rulefit": {"max_categorical_levels"},
-    "stackedensemble": {"score_training_samples"},
-    "infogram": {"max_iterations", "data_fraction"},
+    "infogram": {"max_iterations"},
 }
 
 # values that count as "left at its default" whatever the schema says

@@ -184,7 +184,15 @@ class StackedEnsembleTrainer:
         model.output["base_models"] = model.base_keys
         model.output["metalearner"] = meta.key
         model.output["metalearner_transform"] = transform
-        model.output["training_metrics"] = model.metrics_for(X, y, w, offset)
+        nst = int(self.p.get("score_training_samples") or 0)
+        if 0 < nst < X.shape[1]:      # score_training_samples: training metrics on a fixed row sample
+            from .shared_tree import resolve_seed
+            g = torch.Generator().manual_seed(resolve_seed(self.p.get("seed", -1)) & 0x7FFFFFFF)
+            si = torch.randperm(X.shape[1], generator=g)[:nst].to(X.device)
+            model.output["training_metrics"] = model.metrics_for(X[:, si], y[si], None if w is None else w[si],
+                                                                 None if offset is None else offset[si])
+        else:
+            model.output["training_metrics"] = model.metrics_for(X, y, w, offset)
         # out-of-fold estimate only: the metalearner's own cross-validation (never its training fit)
         model.output["cross_validation_metrics"] = meta.output.get("cross_validation_metrics")
         if self.p.get("keep_levelone_frame"):
