@@ -338,9 +338,13 @@ def flow():
 
 
 def explain(models, frame, columns=None, top_n_features=5, **kw):
-    from llama_github_io_amd import explain as _ex
-    m = models[0] if isinstance(models, (list, tuple)) else models
-    return _ex.explain(getattr(m, "_model", m), frame, columns, top_n_features)
+    from .explanation import explain as _explain
+    return _explain(models, frame, columns, top_n_features, **kw)
+
+
+def explain_row(models, frame, row_index, columns=None, top_n_features=5, **kw):
+    from .explanation import explain_row as _explain_row
+    return _explain_row(models, frame, row_index, columns, top_n_features, **kw)
 
 
 def cluster_status():
@@ -362,3 +366,7 @@ from ._more import (api, cluster_info, connection, demo, download_all_logs, down
                     set_timezone, version_check)
 
 import_frame = import_file
+
+from .explanation import (model_correlation, model_correlation_heatmap, pareto_front, pd_multi_plot,  # noqa: E402,F401
+                          register_explain_methods, varimp, varimp_heatmap)
+register_explain_methods()
