@@ -158,14 +158,26 @@ def _multipart_first_file(body: bytes, boundary: str):
     return body, "upload"
 
 
-def create_app():
+def create_app(client_disconnect_timeout: float | None = None):
+    """``client_disconnect_timeout`` (seconds; env ``H2O_CLIENT_DISCONNECT_TIMEOUT``) starts the
+    ClientDisconnectCheckThread equivalent (``api/clients.py``)."""
     if FastAPI is None:
         raise RuntimeError("fastapi is not installed")
     runtime.init()
     app = FastAPI(title="H2O (MI355X-native) REST API", version="3.46.0.amd0")
+    from . import clients as _clients
+    cdt = client_disconnect_timeout
+    if cdt is None and os.environ.get("H2O_CLIENT_DISCONNECT_TIMEOUT"):
+        cdt = float(os.environ["H2O_CLIENT_DISCONNECT_TIMEOUT"])
+    if cdt:
+        _clients.start(cdt)
+
+    def _client_id(request):
+        return request.headers.get("X-H2O-Client") or (request.client.host if request.client else "local")
 
     @app.middleware("http")
     async def timeline(request, call_next):
+        _clients.touch(_client_id(request))
         t0 = time.time()
         resp = await call_next(request)
         _timeline.append(dict(time=int(t0 * 1000), method=request.method, url=str(request.url.path),
@@ -200,11 +212,21 @@ def create_app():
         return r
 
     @app.post("/4/sessions")
-    def new_session():
-        return {"__meta": v3.meta("SessionIdV4", "Iced", 4), "session_key": dkv.new_key("_sid")}
+    def new_session(request: Request):
+        sid = dkv.new_key("_sid")
+        _clients.touch(_client_id(request), sid)
+        return {"__meta": v3.meta("SessionIdV4", "Iced", 4), "session_key": sid}
+
+    @app.get("/3/Clients")
+    def list_clients():
+        now = time.time()
+        return {"__meta": v3.meta("ClientsV3", "Iced"), "client_disconnect_timeout": cdt,
+                "clients": [dict(client=k, last_heard_ms_ago=int((now - v["last_heard"]) * 1000), sessions=v["sessions"])
+                            for k, v in _clients.clients().items()]}
 
     @app.delete("/4/sessions/{sid}")
     def end_session(sid: str):
+        _clients.end_session(sid)
         return {"__meta": v3.meta("SessionIdV4", "Iced", 4), "session_key": sid}
 
     @app.get("/3/SessionProperties")
