@@ -47,6 +47,62 @@ def _loss(name, u, a, period=1):
     raise ValueError(f"unknown GLRM loss {name}")
 
 
+def _multi_loss(kind, U, A):
+    """Loss of one categorical column's one-hot block (GlrmLoss Categorical / Ordinal): U [N, L] fitted
+    scores, A [N, L] one-hot target. Categorical: (1 - u_a)_+ + sum_{j != a} (1 + u_j)_+ ; Ordinal: the
+    level index a is reached by the cumulative thresholds, sum_{j < a} (1 - u_j)_+ + sum_{j >= a} (1 + u_j)_+."""
+    k = kind.lower()
+    if k == "categorical":
+        return (torch.relu(1 - U) * A + torch.relu(1 + U) * (1 - A)).sum(1)
+    if k == "ordinal":
+        L = A.shape[1]
+        a = A.argmax(1, keepdim=True)
+        j = torch.arange(L, device=U.device)[None, :]
+        below = (j < a).to(U.dtype)
+        return (torch.relu(1 - U) * below + torch.relu(1 + U) * (1 - below)).sum(1)
+    raise ValueError(f"unknown GLRM multi_loss {kind}")
+
+
+class LossPlan:
+    """Per-column losses of the expanded matrix (loss / loss_by_col / loss_by_col_idx for numeric columns,
+    multi_loss for every categorical block)."""
+
+    def __init__(self, p, ex, info):
+        by = {}
+        lbc, idx = p.get("loss_by_col"), p.get("loss_by_col_idx")
+        if lbc:
+            lbc = [lbc] if isinstance(lbc, str) else list(lbc)
+            if idx is None:
+                raise ValueError("loss_by_col needs loss_by_col_idx")
+            idx = [idx] if isinstance(idx, (int, str)) else list(idx)
+            if len(idx) != len(lbc):
+                raise ValueError("loss_by_col and loss_by_col_idx must have the same length")
+            for c, l in zip(idx, lbc):
+                j = info.x.index(c) if isinstance(c, str) else int(c)
+                by[j] = l
+        self.num = {}
+        for i, j in enumerate(ex.nums):
+            self.num.setdefault(str(by.get(j, p["loss"])), []).append(ex.num_off + i)
+        self.cat = []
+        for i, j in enumerate(ex.cats):
+            lo, hi = ex.cat_offsets[i], ex.cat_offsets[i] + ex.cat_sizes[i]
+            self.cat.append((lo, hi, str(by.get(j, p.get("multi_loss") or "Categorical"))))
+        self.period = p.get("period", 1)
+
+    def total(self, U, A, mask):
+        tot = U.new_zeros(())
+        for l, cols in self.num.items():
+            c = torch.as_tensor(cols, device=U.device)
+            tot = tot + (mask[:, c] * _loss(l, U[:, c], A[:, c], self.period)).sum()
+        for lo, hi, kind in self.cat:
+            m = mask[:, lo]
+            if kind.lower() in ("categorical", "ordinal"):
+                tot = tot + (m * _multi_loss(kind, U[:, lo:hi], torch.nan_to_num(A[:, lo:hi]))).sum()
+            else:
+                tot = tot + (mask[:, lo:hi] * _loss(kind, U[:, lo:hi], A[:, lo:hi], self.period)).sum()
+        return tot
+
+
 def _reg_value(name, M, axis):
     n = name.lower().replace("_", "")
     if n == "none":
@@ -117,7 +173,7 @@ class GLRMModel(Model):
         step = 1.0
         for _ in range(iters):
             Xr = Xr.requires_grad_(True)
-            L = (mask * _loss(p["loss"], Xr @ Y, Z)).sum()
+            L = self.plan.total(Xr @ Y, Z, mask) if getattr(self, "plan", None) else (mask * _loss(p["loss"], Xr @ Y, Z)).sum()
             g, = torch.autograd.grad(L, Xr)
             with torch.no_grad():
                 Xr = _prox(p["regularization_x"], Xr - step * g / max(Z.shape[1], 1), step * float(p["gamma_x"]), 1)
@@ -133,9 +189,23 @@ class GLRMModel(Model):
         if ex.standardize and ex.nums:
             k = ex.num_off
             R[:, k:] = R[:, k:] * ex.num_sd[None, :] + ex.num_mean[None, :]
+        if self.params.get("impute_original"):
+            # impute_original: one column per ORIGINAL column (numerics de-transformed, categoricals = the
+            # level with the highest fitted score of their one-hot block)
+            cols = []
+            for j in range(len(self.info.x)):
+                if j in ex.cats:
+                    i = ex.cats.index(j)
+                    lo = ex.cat_offsets[i]
+                    cols.append(R[:, lo:lo + ex.cat_sizes[i]].argmax(1).to(R.dtype))
+                else:
+                    cols.append(R[:, ex.num_off + ex.nums.index(j)])
+            R = torch.stack(cols, 1)
         return R.float()
 
     def prediction_names(self):
+        if self.params.get("impute_original"):
+            return [f"reconstr_{n}" for n in self.info.x]
         return [f"reconstr_{n}" for n in self.expander.names]
 
     def archetypes(self):
@@ -205,23 +275,33 @@ class GLRMTrainer:
         Xr = torch.randn(N, k, dtype=torch.float64, generator=gen).to(dev) * 0.1
         if init in ("svd", "plusplus"):
             Xr = torch.linalg.lstsq(Y.T, (A * mask).T).solution.T
-        loss, rx, ry = p["loss"], p["regularization_x"], p["regularization_y"]
+        rx, ry = p["regularization_x"], p["regularization_y"]
         gx, gy = float(p["gamma_x"]), float(p["gamma_y"])
+        plan = LossPlan(p, ex, info)
+        if p.get("user_x") is not None:        # init user_x: the initial representation
+            ux = p["user_x"]
+            Xr = torch.as_tensor(ux.as_tensor().numpy() if hasattr(ux, "as_tensor") else np.asarray(ux),
+                                 dtype=torch.float64).to(dev).reshape(N, k)
 
         def objective(Xr, Y):
-            return float((mask * _loss(loss, Xr @ Y, A, p["period"])).sum() + gx * _reg_value(rx, Xr, 1) + gy * _reg_value(ry, Y, 0))
+            return float(plan.total(Xr @ Y, A, mask) + gx * _reg_value(rx, Xr, 1) + gy * _reg_value(ry, Y, 0))
 
         step = float(p["init_step_size"])
         obj = objective(Xr, Y)
         it = 0
         hist = []
+        max_upd = int(p.get("max_updates") or 0)
+        updates = 0
         for it in range(int(p["max_iterations"])):
+            if max_upd > 0 and updates >= max_upd:     # max_updates: cap on accepted + rejected steps
+                break
+            updates += 1
             # X half-step
             Xg = Xr.clone().requires_grad_(True)
-            g, = torch.autograd.grad((mask * _loss(loss, Xg @ Y, A, p["period"])).sum(), Xg)
+            g, = torch.autograd.grad(plan.total(Xg @ Y, A, mask), Xg)
             Xn = _prox(rx, Xr - step * g / max(P, 1), step * gx, 1)
             Yg = Y.clone().requires_grad_(True)
-            g, = torch.autograd.grad((mask * _loss(loss, Xn @ Yg, A, p["period"])).sum(), Yg)
+            g, = torch.autograd.grad(plan.total(Xn @ Yg, A, mask), Yg)
             Yn = _prox(ry, Y - step * g / max(N, 1), step * gy, 0)
             nobj = objective(Xn, Yn)
             if nobj < obj:
@@ -242,6 +322,12 @@ class GLRMTrainer:
         model.device = dev
         model.expander = ex
         model.Y = Y
+        model.plan = plan
+        if p.get("recover_svd"):
+            # GLRM.recoverSVD: SVD of the rank-k product X Y (singular values and right vectors)
+            _, Sv, Vt = torch.linalg.svd(Xr @ Y, full_matrices=False)
+            model.output["singular_vals"] = Sv[:k].cpu().tolist()
+            model.output["eigenvectors"] = Vt[:k].T.cpu().tolist()
         model.output.update(objective=obj, iterations=it + 1, step_size=step, archetypes=Y.cpu().tolist(),
                             names_expanded=ex.names, scoring_history=hist)
         from ..frame import H2OFrame

@@ -28,7 +28,7 @@ HINTS = {
     "score_iteration_interval", "classification_stop", "regression_stop", "train_samples_per_iteration",
     "score_validation_sampling", "u_name", "loading_name", "build_glm_model",
     "compute_metrics", "num_iteration_without_new_exemplar",
-    "tree_method", "eval_metric", "export_checkpoints_dir", "gradient_epsilon",
+    "tree_method", "eval_metric", "export_checkpoints_dir", "gradient_epsilon", "svd_method",
     # DeepLearning: elastic averaging blends per-node local models into the global one between map/reduce
     # rounds; with synchronous data parallelism every rank holds the global model after each step, so it
     # is the identity here. ``sparse`` is a storage hint for sparse input.
@@ -47,8 +47,7 @@ UNSUPPORTED = {
     "modelselection": {"beta_constraints", "cold_start", "influence", "max_active_predictors", "prior",
                        "remove_collinear_columns", "startval", "p_values_threshold", "gradient_epsilon",
                        "objective_epsilon", "early_stopping", "plug_values"},
-    "glrm": {"loss_by_col", "loss_by_col_idx", "multi_loss", "user_x", "svd_method", "expand_user_y",
-             "impute_original", "recover_svd", "max_updates"},
+    "glrm": {"expand_user_y"},
     "kmeans": {"cluster_size_constraints"},
     "psvm": {"feasible_threshold", "kernel_type", "mu_factor", "surrogate_gap_threshold"},
     "word2vec": {"word_model"},

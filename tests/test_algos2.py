@@ -174,3 +174,22 @@ def test_word2vec_pre_trained():
     m.train()
     syn = m._model.find_synonyms("king", 1)
     assert list(syn) == ["queen"]
+
+
+def test_glrm_column_losses_and_outputs(df):
+    from h2o.estimators import H2OGeneralizedLowRankEstimator
+    base = dict(k=2, init="SVD", max_iterations=200, seed=1)
+    g = H2OGeneralizedLowRankEstimator(loss_by_col=["Absolute"], loss_by_col_idx=[1], multi_loss="Categorical",
+                                       impute_original=True, recover_svd=True, **base)
+    g.train(x=["a", "b", "c", "r"], training_frame=df)
+    out = g._model.output
+    assert len(out["singular_vals"]) == 2 and out["singular_vals"][0] >= out["singular_vals"][1]
+    plan = g._model.plan
+    assert "Absolute" in plan.num and plan.cat and plan.cat[0][2] == "Categorical"
+    p = g.predict(df)
+    assert p.names == ["reconstr_a", "reconstr_b", "reconstr_c", "reconstr_r"]
+    lv = p.as_data_frame()["reconstr_c"]
+    assert set(np.unique(lv)) <= {0.0, 1.0, 2.0}
+    g2 = H2OGeneralizedLowRankEstimator(max_updates=3, multi_loss="Ordinal", **base)
+    g2.train(x=["a", "b", "c"], training_frame=df)
+    assert g2._model.output["iterations"] <= 4
