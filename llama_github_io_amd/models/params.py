@@ -49,7 +49,6 @@ UNSUPPORTED = {
                        "objective_epsilon", "early_stopping", "plug_values"},
     "glrm": {"expand_user_y"},
     "kmeans": {"cluster_size_constraints"},
-    "psvm": {"feasible_threshold", "kernel_type", "mu_factor", "surrogate_gap_threshold"},
     "word2vec": {"word_model"},
     "rulefit": {"max_categorical_levels"},
     "infogram": {"max_iterations"},
