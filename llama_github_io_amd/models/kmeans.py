@@ -146,7 +146,53 @@ class KMeansTrainer:
             C = torch.cat([C, self._row(Z, j)], 0)
         return C
 
+    @staticmethod
+    def constrained_assign(D, mins):
+        """Assignment with minimum cluster sizes (KMeans cluster_size_constraints: the reference solves a
+        min-cost flow per iteration): the transportation LP min Σ D_ik x_ik, Σ_k x_ik = 1, Σ_i x_ik >= m_k,
+        whose constraint matrix is totally unimodular, so HiGHS returns an integral assignment."""
+        import scipy.sparse as sp
+        from scipy.optimize import linprog
+        N, K = D.shape
+        Dn = D.double().cpu().numpy()
+        rows = np.repeat(np.arange(N), K)
+        cols = np.arange(N * K)
+        A_eq = sp.csr_matrix((np.ones(N * K), (rows, cols)), shape=(N, N * K))
+        A_ub = sp.csr_matrix((-np.ones(N * K), (np.tile(np.arange(K), N), cols)), shape=(K, N * K))
+        res = linprog(Dn.reshape(-1), A_ub=A_ub, b_ub=-np.asarray(mins, dtype=np.float64), A_eq=A_eq,
+                      b_eq=np.ones(N), bounds=(0, 1), method="highs")
+        if not res.success:
+            raise ValueError(f"cluster_size_constraints cannot be met: {res.message}")
+        return torch.as_tensor(res.x.reshape(N, K).argmax(1), device=D.device)
+
+    def _lloyd_constrained(self, Z, w, C, max_it, mins):
+        K = C.shape[0]
+        if len(mins) != K:
+            raise ValueError(f"cluster_size_constraints needs {K} values")
+        if sum(mins) > Z.shape[0]:
+            raise ValueError("the sum of cluster_size_constraints exceeds the number of rows")
+        if Z.shape[0] * K > 4_000_000:
+            raise ValueError("cluster_size_constraints is available for frames with rows x k <= 4e6")
+        wd = torch.ones(Z.shape[0], dtype=torch.float64, device=Z.device) if w is None else w.double()
+        a_prev = None
+        for it in range(max_it):
+            D = torch.cdist(Z.double(), C.double()) ** 2
+            a = self.constrained_assign(D, mins)
+            oh = torch.nn.functional.one_hot(a, K).double() * wd[:, None]
+            cnt = oh.sum(0)
+            C = torch.where(cnt[:, None] > 0, (oh.T @ Z.double()) / cnt.clamp(min=1e-300)[:, None], C.double()).float()
+            if a_prev is not None and bool((a == a_prev).all()):
+                break
+            a_prev = a
+        d = ((Z.double() - C.double()[a]) ** 2).sum(1).float()
+        return C, a, d, it + 1
+
     def _lloyd(self, Z, w, C, max_it):
+        csc = self.p.get("cluster_size_constraints")
+        if csc:
+            if coll.is_dist():
+                raise ValueError("cluster_size_constraints needs a single-process frame")
+            return self._lloyd_constrained(Z, w, C, max_it, [int(v) for v in csc])
         K = C.shape[0]
         dev = Z.device
         for it in range(max_it):

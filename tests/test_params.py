@@ -38,7 +38,7 @@ def test_unknown_parameter_raises(fr):
 
 
 @pytest.mark.parametrize("algo,param,value", [
-    ("kmeans", "cluster_size_constraints", [10, 20]),
+    ("word2vec", "word_model", "cbow"),
     ("xgboost", "grow_policy", "lossguide"),
     ("deeplearning", "sparsity_beta", 0.5),
     ("glm", "influence", "dfbetas"),
@@ -243,3 +243,18 @@ def test_glm_dispersion_vif_likelihood():
     cold = GLMTrainer(dict(family="gaussian", lambda_search=True, nlambdas=5, cold_start=True)).fit(
         X, torch.tensor(a + c), None, None, info)
     assert len(cold.output.get("lambda_path", cold.output.get("regularization_path", [0]))) >= 1
+
+
+def test_kmeans_cluster_size_constraints():
+    """Every cluster gets at least its constrained number of rows (KMeans cluster_size_constraints)."""
+    import numpy as np
+    import torch
+    from llama_github_io_amd.models.base import DataInfo
+    from llama_github_io_amd.models.kmeans import KMeansTrainer
+    rng = np.random.default_rng(0)
+    X = np.concatenate([rng.normal(0, 0.3, (280, 2)), rng.normal(5, 0.3, (20, 2))]).T
+    info = DataInfo(["a", "b"], np.zeros(2, np.int32), [None, None], None, None)
+    m = KMeansTrainer(dict(k=2, seed=1, standardize=False, cluster_size_constraints=[100, 100])).fit(
+        torch.tensor(X, dtype=torch.float32), None, None, None, info)
+    sizes = m.output["training_metrics"]["size"]
+    assert sizes is not None and min(sizes) >= 100, sizes
