@@ -333,7 +333,7 @@ class DeepLearningTrainer:
             else:
                 (ls / wb.sum().clamp(min=1e-12)).backward()
 
-        def update():
+        def update(rate_t=rate_t, mom_t=mom_t, on_t=on_t):
             """Optimizer step on the flat buffers (ADADELTA: one fused HIP launch; momentum SGD with rate
             annealing / Nesterov from the device scalars rate_t, mom_t, on_t), then max_w2 row clipping."""
             with torch.no_grad():
@@ -401,8 +401,8 @@ class DeepLearningTrainer:
                         with torch.cuda.graph(g2):
                             update()
                     gstate.update(g1=g1, g2=g2)
-                except Exception:  # noqa: BLE001 - capture unsupported here: eager steps on the static buffers
-                    gstate.update(g1=False)
+                except Exception as e:  # noqa: BLE001 - capture unsupported here: eager steps on the static buffers
+                    gstate.update(g1=False, error=f"{type(e).__name__}: {e}")
             if gstate["g1"] is False:
                 fwd_bwd(sx, sw, sy)
                 if sharded:
@@ -414,6 +414,55 @@ class DeepLearningTrainer:
                 coll.all_reduce_(gbuf)
                 gstate["g2"].replay()
 
+        # Single process: CH consecutive steps (gather of the batch rows from the resident design matrix
+        # included) are captured in ONE graph and replayed per chunk — the host issues one index copy, one
+        # arange and one replay per CH steps instead of launching ~40 kernels per step.
+        CH = max(1, int(os.environ.get("H2O_DL_CHUNK", "16"))) if (use_graph and not sharded) else 1
+        chunk = dict(g=None)
+        if CH > 1:
+            ridx = torch.zeros(CH * B, dtype=torch.long, device=dev)
+            step_v = torch.zeros(CH, dtype=torch.int64, device=dev)
+            rate_v = torch.zeros(CH, dtype=torch.float32, device=dev)
+            mom_v = torch.zeros(CH, dtype=torch.float32, device=dev)
+            on_v = torch.zeros(CH, dtype=torch.float32, device=dev)
+
+            def chunk_body():
+                for k in range(CH):
+                    r = ridx[k * B:(k + 1) * B]
+                    torch.index_select(Z, 0, r, out=sx)
+                    torch.index_select(wf, 0, r, out=sw)
+                    if sy is not None:
+                        torch.index_select(yt, 0, r, out=sy)
+                    net.step_dev = step_v[k:k + 1]
+                    fwd_bwd(sx, sw, sy)
+                    update(rate_v[k], mom_v[k], on_v[k])
+                net.step_dev = step_t
+
+            def run_chunk(rows, step0, samples0):
+                ridx.copy_(rows)
+                torch.arange(step0, step0 + CH, out=step_v)
+                if not adaptive:
+                    rs, ms = [], []
+                    for k in range(CH):
+                        smp = samples0 + (k + 1) * B
+                        rs.append(float(p["rate"]) / (1 + float(p["rate_annealing"]) * smp))
+                        ms.append(self._momentum(smp))
+                    rate_v.copy_(torch.tensor(rs, dtype=torch.float32))
+                    mom_v.copy_(torch.tensor(ms, dtype=torch.float32))
+                    on_v.copy_(torch.tensor([1.0 if m_ > 0 else 0.0 for m_ in ms], dtype=torch.float32))
+                if chunk["g"] is None:
+                    try:
+                        gc = torch.cuda.CUDAGraph()
+                        with torch.cuda.graph(gc):
+                            chunk_body()
+                        chunk["g"] = gc
+                    except Exception as e:  # noqa: BLE001 - fall back to per-step replays
+                        chunk.update(g=False, error=f"{type(e).__name__}: {e}")
+                        net.step_dev = step_t
+                        return False
+                chunk["g"].replay()
+                return True
+
         # global row order per epoch: mini-batches are consecutive B-slices of a permutation of the GLOBAL
         # rows; under row sharding each rank takes the members of the batch it owns (one host sync per
         # epoch for the per-step counts), so the summed gradient is the single-process one
@@ -423,7 +472,9 @@ class DeepLearningTrainer:
         s_in = S_ep
         owb = bool(p.get("overwrite_with_best_model", True)) and not int(p.get("nfolds") or 0)
         best_loss, best_p, last_ev = float("inf"), None, {}
-        for step in range(total):
+        step = 0
+        spe = max(1, N_glob // B)
+        while step < total:
             if s_in >= S_ep:
                 perm = torch.randperm(N_glob, generator=g).to(dev)
                 s_in = 0
@@ -438,41 +489,51 @@ class DeepLearningTrainer:
                         alloc(max(64, (cmax + 63) // 64 * 64))
                 elif use_graph and gstate["cap"] != B:
                     alloc(B)
-            if sharded:
-                rows = perm[sel[offs[s_in]:offs[s_in + 1]]] - row0
-            else:
-                rows = perm[s_in * B:(s_in + 1) * B]
-            s_in += 1
             net.train()
-            net.step = step
-            samples += B
-            if not adaptive:
-                m = self._momentum(samples)
-                rate_t.fill_(float(p["rate"]) / (1 + float(p["rate_annealing"]) * samples))
-                mom_t.fill_(m)
-                on_t.fill_(1.0 if m > 0 else 0.0)
-            if use_graph:
-                c = rows.numel()
-                torch.index_select(Z, 0, rows, out=sx[:c])
-                torch.index_select(wf, 0, rows, out=sw[:c])
-                if c < sw.numel():
-                    sw[c:].zero_()
-                if sy is not None:
-                    torch.index_select(yt, 0, rows, out=sy[:c])
-                step_t.fill_(step)
-                run_step()
-            else:
-                fwd_bwd(Z.index_select(0, rows), wf.index_select(0, rows), None if ae else yt.index_select(0, rows))
+            n = 1
+            if (CH > 1 and gstate["warm"] >= 2 and chunk["g"] is not False and s_in + CH <= S_ep
+                    and step + CH <= total):
+                net.step = step
+                if run_chunk(perm[s_in * B:(s_in + CH) * B], step, samples):
+                    n = CH
+            if n == 1:
                 if sharded:
-                    coll.all_reduce_(gbuf)
-                update()
-            if self.job is not None and step % 50 == 0:
-                self.job.set_progress(step / max(total, 1))
-            end = step == total - 1
+                    rows = perm[sel[offs[s_in]:offs[s_in + 1]]] - row0
+                else:
+                    rows = perm[s_in * B:(s_in + 1) * B]
+                net.step = step
+                if not adaptive:
+                    m = self._momentum(samples + B)
+                    rate_t.fill_(float(p["rate"]) / (1 + float(p["rate_annealing"]) * (samples + B)))
+                    mom_t.fill_(m)
+                    on_t.fill_(1.0 if m > 0 else 0.0)
+                if use_graph:
+                    c = rows.numel()
+                    torch.index_select(Z, 0, rows, out=sx[:c])
+                    torch.index_select(wf, 0, rows, out=sw[:c])
+                    if c < sw.numel():
+                        sw[c:].zero_()
+                    if sy is not None:
+                        torch.index_select(yt, 0, rows, out=sy[:c])
+                    step_t.fill_(step)
+                    run_step()
+                else:
+                    fwd_bwd(Z.index_select(0, rows), wf.index_select(0, rows), None if ae else yt.index_select(0, rows))
+                    if sharded:
+                        coll.all_reduce_(gbuf)
+                    update()
+            s_in += n
+            samples += n * B
+            last = step + n - 1
+            if self.job is not None and (step // 50) != ((last + 1) // 50):
+                self.job.set_progress(last / max(total, 1))
+            end = last == total - 1
             timed = time.time() - last_score > float(p["score_interval"])
             if sharded:                          # every rank must take the same scoring decision
                 timed = coll.agree(timed) if step % 16 == 0 else False
-            if end or timed or (keeper.k > 0 and step > 0 and step % max(1, N_glob // B) == 0):
+            epoch_mark = keeper.k > 0 and any(st > 0 and st % spe == 0 for st in range(step, last + 1))
+            step = last + 1
+            if end or timed or epoch_mark:
                 last_score = time.time()
                 ev = self._score(model, X, y, w, samples / N_glob, valid)
                 history.append({k: v for k, v in ev.items() if not k.startswith("_")})
@@ -486,6 +547,10 @@ class DeepLearningTrainer:
                     break
                 if float(p["max_runtime_secs"] or 0) > 0 and coll.agree(time.time() - t0 > float(p["max_runtime_secs"])):
                     break
+        model.output["training_step_mode"] = (
+            "eager" if not use_graph else
+            ("graph_chunk%d" % CH if chunk.get("g") not in (None, False) else
+             ("graph_step" if gstate.get("g1") not in (None, False) else "eager (" + str(gstate.get("error") or chunk.get("error")) + ")")))
         net.step_dev = None
         if owb and best_p is not None:
             final = self._model_loss(last_ev.get("_valid") or last_ev.get("_train"), cat, ae)
