@@ -103,7 +103,8 @@ __global__ __launch_bounds__(256) void k_bias_act_bwd(const T* __restrict__ gy, 
 // L1/L2 apply to weights only: elements [0, n_decay) are the weight matrices, the rest biases.
 __global__ __launch_bounds__(256) void k_adadelta(float* __restrict__ p, const float* __restrict__ g,
                                                   float* __restrict__ eg2, float* __restrict__ edx2, int64_t n,
-                                                  int64_t n_decay, float rho, float eps, float l1, float l2) {
+                                                  int64_t n_decay, float rho, float eps, float l1, float l2,
+                                                  __hip_bfloat16* __restrict__ shadow) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const float pi = p[i];
     float gi = g[i];
@@ -113,6 +114,39 @@ __global__ __launch_bounds__(256) void k_adadelta(float* __restrict__ p, const f
     eg2[i] = e;
     edx2[i] = rho * edx2[i] + (1.f - rho) * d * d;
     p[i] = pi + d;
+    if (shadow && i < n_decay) shadow[i] = __float2bfloat16(pi + d);   // bf16 weights for the next GEMMs
+  }
+}
+
+// Output layer of the explicit MLP step: per row, softmax cross-entropy (K classes) or squared error (K = 1,
+// regression) gradient w.r.t. the logits, dO = (softmax(o) - onehot(y)) * w * inv  |  (o - y) * w * inv,
+// written as T (the dtype of the following GEMMs) and the output-bias gradient Σ_rows dO accumulated
+// with one fp32 atomic per (row, class). inv = 1 / Σw (single process) or 1 (data-parallel sum).
+template <typename T>
+__global__ __launch_bounds__(256) void k_out_grad(const T* __restrict__ logits, const long long* __restrict__ ycls,
+                                                  const float* __restrict__ yreg, const float* __restrict__ w,
+                                                  const float* __restrict__ inv, int64_t rows, int K,
+                                                  T* __restrict__ dO, float* __restrict__ db) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= rows) return;
+  const float s = w[r] * inv[0];
+  const T* o = logits + r * K;
+  if (ycls) {
+    float mx = -INFINITY;
+    for (int k = 0; k < K; ++k) mx = fmaxf(mx, ld(o, k));
+    float z = 0.f;
+    for (int k = 0; k < K; ++k) z += __expf(ld(o, k) - mx);
+    const float iz = 1.f / z;
+    const long long c = ycls[r];
+    for (int k = 0; k < K; ++k) {
+      const float g = (__expf(ld(o, k) - mx) * iz - (k == c ? 1.f : 0.f)) * s;
+      st(dO, r * K + k, g);
+      if (g != 0.f) atomicAdd(db + k, g);
+    }
+  } else {
+    const float g = (ld(o, 0) - yreg[r]) * s;
+    st(dO, r, g);
+    if (g != 0.f) atomicAdd(db, g);
   }
 }
 
@@ -121,12 +155,25 @@ __global__ __launch_bounds__(256) void k_adadelta(float* __restrict__ p, const f
 extern "C" {
 
 int h2o_adadelta(float* p, const float* g, float* eg2, float* edx2, long long n, long long n_decay, float rho, float eps,
-                 float l1, float l2, hipStream_t stream) {
+                 float l1, float l2, void* shadow, hipStream_t stream) {
   long long grid = (n + 255) / 256;
   if (grid > 4096) grid = 4096;
   if (grid < 1) grid = 1;
   hipLaunchKernelGGL(k_adadelta, dim3((unsigned)grid), dim3(256), 0, stream, p, g, eg2, edx2, (int64_t)n,
-                     (int64_t)n_decay, rho, eps, l1, l2);
+                     (int64_t)n_decay, rho, eps, l1, l2, (__hip_bfloat16*)shadow);
+  return (int)hipGetLastError();
+}
+
+int h2o_out_grad(const void* logits, const long long* ycls, const float* yreg, const float* w, const float* inv,
+                 long long rows, int K, void* dO, float* db, int bf16, hipStream_t stream) {
+  if (rows <= 0) return 0;
+  const unsigned grid = (unsigned)((rows + 255) / 256);
+  if (bf16)
+    hipLaunchKernelGGL(k_out_grad<__hip_bfloat16>, dim3(grid), dim3(256), 0, stream, (const __hip_bfloat16*)logits,
+                       ycls, yreg, w, inv, (int64_t)rows, K, (__hip_bfloat16*)dO, db);
+  else
+    hipLaunchKernelGGL(k_out_grad<float>, dim3(grid), dim3(256), 0, stream, (const float*)logits, ycls, yreg, w, inv,
+                       (int64_t)rows, K, (float*)dO, db);
   return (int)hipGetLastError();
 }
 

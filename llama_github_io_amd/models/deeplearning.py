@@ -339,8 +339,8 @@ class DeepLearningTrainer:
             with torch.no_grad():
                 if sharded:       # data parallel: the all-reduced [sum-gradient, batch weight] -> mean gradient
                     fp.g.copy_(gbuf[:-1] / gbuf[-1].clamp(min=1e-12))
-                if adaptive:      # ADADELTA (Neurons.java: rho, epsilon)
-                    fp.adadelta(rho, eps, l1, l2)
+                if adaptive:      # ADADELTA (Neurons.java: rho, epsilon); also refreshes the bf16 weights
+                    fp.adadelta(rho, eps, l1, l2, shadow)
                 else:
                     gg = fp.g.clone()
                     nd = fp.n_decay
@@ -357,6 +357,68 @@ class DeepLearningTrainer:
                         if q.dim() > 1:
                             n2 = (q * q).sum(1, keepdim=True)
                             q.mul_(torch.where(n2 > max_w2, torch.sqrt(max_w2 / n2), torch.ones_like(n2)))
+                if shadow is not None and (not adaptive or max_w2 < float("inf")):
+                    shadow.copy_(fp.p[: fp.n_decay])
+
+        # Explicit training step (no autograd) for the common MLPs: GEMMs on bf16 weight copies kept by the
+        # fused ADADELTA kernel, fused bias/activation/dropout epilogues, one fused softmax-CE / squared-error
+        # output-gradient pass; weight gradients land in the flat buffer, bias gradients are accumulated by
+        # the epilogue kernels straight into it (~20 launches per step instead of ~45).
+        lname = str(p["loss"]).lower()
+        explicit = (os.environ.get("H2O_DL_EXPLICIT", "1") == "1" and not ae and not maxout
+                    and float(p["input_dropout_ratio"]) == 0 and net.act in ACT
+                    and ((cat in ("Binomial", "Multinomial") and dist in ("bernoulli", "multinomial")
+                          and lname in ("automatic", "crossentropy", "cross_entropy"))
+                         or (cat == "Regression" and dist == "gaussian" and lname in ("automatic", "quadratic"))))
+        shadow = None
+        if explicit:
+            lins = list(net.hidden) + [net.out]
+            base_ptr, esz = fp.p.data_ptr(), fp.p.element_size()
+            w_off = [(l_.weight.data_ptr() - base_ptr) // esz for l_ in lins]
+            b_off = [(l_.bias.data_ptr() - base_ptr) // esz for l_ in lins]
+            cdt = torch.bfloat16 if (dtype is not None and dev.type == "cuda") else torch.float32
+            if cdt == torch.bfloat16:
+                shadow = fp.p[: fp.n_decay].to(torch.bfloat16)
+                Wc = [shadow[o:o + l_.weight.numel()].view_as(l_.weight) for o, l_ in zip(w_off, lins)]
+            else:
+                Wc = [l_.weight.data for l_ in lins]
+            gW = [fp.g[o:o + l_.weight.numel()].view_as(l_.weight) for o, l_ in zip(w_off, lins)]
+            gB = [fp.g[o:o + l_.bias.numel()] for o, l_ in zip(b_off, lins)]
+            bO = net.out.bias.data
+            act_code = ACT[net.act]
+            inv_t = torch.ones(1, dtype=torch.float32, device=dev)
+            from ..ops.dense import bias_act_bwd, bias_act_fwd, out_grad
+
+            def fwd_bwd(xb, wb, tb):      # noqa: F811 - the explicit step replaces the autograd one
+                with torch.no_grad():
+                    fp.g[fp.n_decay:].zero_()
+                    if not sharded:
+                        torch.reciprocal(wb.sum().clamp(min=1e-12).view(1), out=inv_t)
+                    hs = [xb if xb.dtype == cdt else xb.to(cdt)]
+                    seeds = []
+                    for i, lin in enumerate(net.hidden):
+                        drop = net.hid_drop[i]
+                        base = (seed * 1000003 + i * 7919) & ((1 << 62) - 1)
+                        sd = (base, net.step_dev) if net.step_dev is not None else (step_seed(base, net.step), None)
+                        seeds.append(sd)
+                        a_ = torch.mm(hs[-1], Wc[i].t())
+                        hs.append(bias_act_fwd(a_, lin.bias.data, act_code, drop, sd[0], sd[1]))
+                    logits = torch.addmm(bO.to(cdt), hs[-1], Wc[-1].t())
+                    wf32 = wb.float()
+                    if cat == "Regression":
+                        dO = out_grad(logits, None, tb.float(), wf32, inv_t, gB[-1])
+                    else:
+                        dO = out_grad(logits, tb.long(), None, wf32, inv_t, gB[-1])
+                    gW[-1].copy_(torch.mm(dO.t(), hs[-1]))
+                    dh = torch.mm(dO, Wc[-1])
+                    for i in range(len(net.hidden) - 1, -1, -1):
+                        dA = bias_act_bwd(dh, hs[i + 1], act_code, net.hid_drop[i], seeds[i][0], seeds[i][1], gB[i])
+                        gW[i].copy_(torch.mm(dA.t(), hs[i]))
+                        if i > 0:
+                            dh = torch.mm(dA, Wc[i])
+                    if sharded:
+                        gbuf[:-1].copy_(fp.g)
+                        gbuf[-1:].copy_(wb.sum().view(1))
 
         # hipGraph capture of the training step (fwd + bwd (+ update)): a fixed launch sequence on static
         # batch buffers, replayed per step. Row-sharded runs capture fwd+bwd and the update separately with
@@ -547,6 +609,7 @@ class DeepLearningTrainer:
                     break
                 if float(p["max_runtime_secs"] or 0) > 0 and coll.agree(time.time() - t0 > float(p["max_runtime_secs"])):
                     break
+        model.output["training_step_explicit"] = bool(explicit)
         model.output["training_step_mode"] = (
             "eager" if not use_graph else
             ("graph_chunk%d" % CH if chunk.get("g") not in (None, False) else

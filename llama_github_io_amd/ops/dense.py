@@ -24,7 +24,9 @@ nat.register_hip_signatures({
     "h2o_kmeans_step": [nat.c_void_p, nat.c_ll, nat.c_int, nat.c_void_p, nat.c_int, nat.c_void_p, nat.c_void_p,
                         nat.c_void_p, nat.c_void_p, nat.c_void_p],
     "h2o_adadelta": [nat.c_void_p, nat.c_void_p, nat.c_void_p, nat.c_void_p, nat.c_ll, nat.c_ll, nat.ctypes.c_float,
-                     nat.ctypes.c_float, nat.ctypes.c_float, nat.ctypes.c_float, nat.c_void_p],
+                     nat.ctypes.c_float, nat.ctypes.c_float, nat.ctypes.c_float, nat.c_void_p, nat.c_void_p],
+    "h2o_out_grad": [nat.c_void_p, nat.c_void_p, nat.c_void_p, nat.c_void_p, nat.c_void_p, nat.c_ll, nat.c_int,
+                     nat.c_void_p, nat.c_void_p, nat.c_int, nat.c_void_p],
 })
 
 
@@ -56,10 +58,13 @@ class FlatParams:
     def zero_grad(self):
         self.g.zero_()
 
-    def adadelta(self, rho, eps, l1=0.0, l2=0.0):
+    def adadelta(self, rho, eps, l1=0.0, l2=0.0, shadow=None):
+        """``shadow`` (bf16 [n_decay], optional): also written with the updated weights (the bf16 copies the
+        explicit MLP step multiplies with)."""
         if self.p.is_cuda:
             call("h2o_adadelta", self.p.data_ptr(), self.g.data_ptr(), self.eg2.data_ptr(), self.edx2.data_ptr(),
-                 self.p.numel(), self.n_decay, float(rho), float(eps), float(l1), float(l2), stream_ptr(self.p.device))
+                 self.p.numel(), self.n_decay, float(rho), float(eps), float(l1), float(l2),
+                 0 if shadow is None else shadow.data_ptr(), stream_ptr(self.p.device))
             return
         g = self.g.clone()
         w = slice(0, self.n_decay)
@@ -68,6 +73,8 @@ class FlatParams:
         d = -torch.sqrt(self.edx2 + eps) / torch.sqrt(self.eg2 + eps) * g
         self.edx2.mul_(rho).addcmul_(d, d, value=1 - rho)
         self.p.add_(d)
+        if shadow is not None:
+            shadow.copy_(self.p[: self.n_decay])
 
 _M = (1 << 64) - 1
 _GOLD = 0x9E3779B97F4A7C15
@@ -106,25 +113,63 @@ def _act(a, v):
     return v
 
 
+def bias_act_fwd(x, b, act: int, drop: float, seed: int, seed_dev=None):
+    """y = act(x + b) with inverted dropout (no autograd). CUDA: one HIP pass, bf16 in -> bf16 out."""
+    x = x.contiguous()
+    rows, cols = x.shape
+    if x.is_cuda:
+        if x.dtype not in (torch.float32, torch.bfloat16):
+            x = x.float()
+        y = torch.empty_like(x)
+        bb = None if b is None else b.float().contiguous()
+        nat.call("h2o_bias_act_fwd", x.data_ptr(), 0 if bb is None else bb.data_ptr(), y.data_ptr(), rows, cols,
+                 act, float(drop), seed & _M, 0 if seed_dev is None else seed_dev.data_ptr(),
+                 int(x.dtype == torch.bfloat16), nat.stream_ptr(x.device))
+        return y
+    if seed_dev is not None:
+        seed = step_seed(seed, int(seed_dev.item()))
+    y = _act(act, x + (b if b is not None else 0))
+    if drop > 0:
+        y = torch.where(_mask_ref(y.shape, drop, seed, y.device), y / (1 - drop), torch.zeros_like(y))
+    return y
+
+
+def bias_act_bwd(gy, y, act: int, drop: float, seed: int, seed_dev=None, db=None):
+    """gx = gy * mask * act'(y); the bias gradient Σ_rows gx is ADDED into ``db`` (fp32) when given."""
+    gy = gy.contiguous()
+    rows, cols = y.shape
+    if y.is_cuda:
+        gy = gy.to(y.dtype).contiguous()
+        gx = torch.empty_like(y)
+        nat.call("h2o_bias_act_bwd", gy.data_ptr(), y.data_ptr(), gx.data_ptr(), 0 if db is None else db.data_ptr(),
+                 rows, cols, act, float(drop), seed & _M, 0 if seed_dev is None else seed_dev.data_ptr(),
+                 int(y.dtype == torch.bfloat16), nat.stream_ptr(y.device))
+        return gx
+    if seed_dev is not None:
+        seed = step_seed(seed, int(seed_dev.item()))
+    yy, g = y, gy
+    if drop > 0:
+        m = _mask_ref(y.shape, drop, seed, y.device)
+        g = torch.where(m, gy / (1 - drop), torch.zeros_like(gy))
+        yy = torch.where(m, y * (1 - drop), torch.zeros_like(y))
+    if act == 1:
+        d = (yy > 0).to(y.dtype)
+    elif act == 2:
+        d = 1 - yy * yy
+    elif act == 3:
+        d = torch.where(yy > 0, torch.ones_like(yy), yy + 1)
+    else:
+        d = torch.ones_like(yy)
+    gx = g * d
+    if db is not None:
+        db += gx.sum(0).to(db.dtype)
+    return gx
+
+
 class BiasAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, b, act: int, drop: float, seed: int, seed_dev=None):
-        x = x.contiguous()
-        rows, cols = x.shape
-        if x.is_cuda:
-            if x.dtype not in (torch.float32, torch.bfloat16):
-                x = x.float()
-            y = torch.empty_like(x)          # bf16 in -> bf16 out (fp32 bias and math inside the kernel)
-            bb = None if b is None else b.float().contiguous()
-            nat.call("h2o_bias_act_fwd", x.data_ptr(), 0 if bb is None else bb.data_ptr(), y.data_ptr(), rows, cols,
-                     act, float(drop), seed & _M, 0 if seed_dev is None else seed_dev.data_ptr(),
-                     int(x.dtype == torch.bfloat16), nat.stream_ptr(x.device))
-        else:
-            if seed_dev is not None:
-                seed = step_seed(seed, int(seed_dev.item()))
-            y = _act(act, x + (b if b is not None else 0))
-            if drop > 0:
-                y = torch.where(_mask_ref(y.shape, drop, seed, y.device), y / (1 - drop), torch.zeros_like(y))
+        y = bias_act_fwd(x, b, act, drop, seed, seed_dev)
         ctx.save_for_backward(y)
         ctx.act, ctx.drop, ctx.seed, ctx.has_b, ctx.seed_dev = act, drop, seed, b is not None, seed_dev
         return y
@@ -132,33 +177,29 @@ class BiasAct(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy):
         (y,) = ctx.saved_tensors
-        gy = gy.contiguous()
-        rows, cols = y.shape
-        act, drop, seed = ctx.act, ctx.drop, ctx.seed
-        if y.is_cuda:
-            gy = gy.to(y.dtype).contiguous()
-            gx = torch.empty_like(y)
-            db = torch.zeros(cols, dtype=torch.float32, device=y.device) if ctx.has_b else None
-            nat.call("h2o_bias_act_bwd", gy.data_ptr(), y.data_ptr(), gx.data_ptr(), 0 if db is None else db.data_ptr(),
-                     rows, cols, act, float(drop), seed & _M, 0 if ctx.seed_dev is None else ctx.seed_dev.data_ptr(),
-                     int(y.dtype == torch.bfloat16), nat.stream_ptr(y.device))
-        else:
-            yy, g = y, gy
-            if drop > 0:
-                m = _mask_ref(y.shape, drop, seed, y.device)
-                g = torch.where(m, gy / (1 - drop), torch.zeros_like(gy))
-                yy = torch.where(m, y * (1 - drop), torch.zeros_like(y))
-            if act == 1:
-                d = (yy > 0).to(y.dtype)
-            elif act == 2:
-                d = 1 - yy * yy
-            elif act == 3:
-                d = torch.where(yy > 0, torch.ones_like(yy), yy + 1)
-            else:
-                d = torch.ones_like(yy)
-            gx = g * d
-            db = gx.sum(0) if ctx.has_b else None
+        db = torch.zeros(y.shape[1], dtype=torch.float32, device=y.device) if ctx.has_b else None
+        gx = bias_act_bwd(gy, y, ctx.act, ctx.drop, ctx.seed, ctx.seed_dev, db)
         return gx, db, None, None, None, None
+
+
+def out_grad(logits, ycls, yreg, w, inv, db):
+    """Logit gradient of the output layer (softmax cross-entropy when ``ycls`` is given, squared error on
+    ``yreg`` otherwise), scaled by ``w * inv``; adds Σ_rows into ``db`` (fp32). One HIP pass on the GPU."""
+    rows, K = logits.shape
+    if logits.is_cuda:
+        dO = torch.empty_like(logits)
+        nat.call("h2o_out_grad", logits.data_ptr(), 0 if ycls is None else ycls.data_ptr(),
+                 0 if yreg is None else yreg.data_ptr(), w.data_ptr(), inv.data_ptr(), rows, K, dO.data_ptr(),
+                 db.data_ptr(), int(logits.dtype == torch.bfloat16), nat.stream_ptr(logits.device))
+        return dO
+    o = logits.float()
+    s = (w.float() * inv.float())[:, None]
+    if ycls is not None:
+        g = (torch.softmax(o, 1) - torch.nn.functional.one_hot(ycls.long(), K).float()) * s
+    else:
+        g = (o - yreg.float()[:, None]) * s
+    db += g.sum(0)
+    return g.to(logits.dtype)
 
 
 def bias_act(x, b, act: str | int = "rectifier", drop: float = 0.0, seed: int = 0, seed_dev=None):

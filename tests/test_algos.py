@@ -128,3 +128,31 @@ def test_isolation_forests_rank_outliers():
     m = ExtendedIsolationForestTrainer(dict(ntrees=40, seed=1, extension_level=2)).fit(X, None, None, None, info)
     P = m._predict_tensor(X)
     assert float(P[-10:, 0].mean()) > float(P[:1000, 0].mean()) + 0.1
+
+
+@pytest.mark.parametrize("extra", [{}, dict(activation="TanhWithDropout", hidden_dropout_ratios=[0.2, 0.1]),
+                                   dict(adaptive_rate=False, rate=0.01, momentum_start=0.5, max_w2=3.0)])
+@pytest.mark.parametrize("kind", ["binomial", "multinomial", "regression"])
+def test_deeplearning_explicit_step_matches_autograd(kind, extra, monkeypatch):
+    """The explicit (autograd-free) MLP step computes the same gradients / updates as autograd."""
+    import numpy as np
+    import torch
+    from llama_github_io_amd.models.base import DataInfo
+    from llama_github_io_amd.models.deeplearning import DeepLearningTrainer
+    g = torch.Generator().manual_seed(0)
+    X = torch.randn(5, 3000, generator=g)
+    if kind == "regression":
+        y, dom = (X[0] * X[1] + X[2]).float(), None
+    elif kind == "binomial":
+        y, dom = ((X[0] * X[1] + X[2]) > 0).float(), ["0", "1"]
+    else:
+        y, dom = (X[0] > 0).float() + (X[1] > 0.5).float(), ["a", "b", "c"]
+    info = DataInfo([f"x{i}" for i in range(5)], np.zeros(5, np.int32), [None] * 5, "y", dom)
+    res = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("H2O_DL_EXPLICIT", flag)
+        m = DeepLearningTrainer(dict(dict(hidden=[16, 8], epochs=1, seed=3, mini_batch_size=100, score_interval=1e9,
+                                          stopping_rounds=0), **extra)).fit(X, y, None, None, info)
+        assert m.output["training_step_explicit"] == (flag == "1")
+        res.append(torch.cat([q.detach().reshape(-1) for q in m.net.parameters()]))
+    assert torch.allclose(res[0], res[1], atol=1e-5, rtol=1e-4)
