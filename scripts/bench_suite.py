@@ -82,7 +82,8 @@ def bench_dl(a, dev, world, rank):
     _emit(dict(metric="DeepLearning MLP [200,200] train samples/sec (10M x 784, bf16, data-parallel)",
                value=N * a.epochs / dt, unit="samples/s", n_gpus=world, seconds=dt, rows=N, cols=F, batch=a.batch,
                train_auc=m.output["training_metrics"]["AUC"], dtype="bf16", data="synthetic",
-               step_mode=m.output.get("training_step_mode")))
+               step_mode=m.output.get("training_step_mode"), explicit=m.output.get("training_step_explicit"),
+               phases=m.output.get("phase_seconds")))
 
 
 def bench_automl(a, dev, world, rank):
