@@ -257,6 +257,13 @@ def variance_inflation_factors(ex, X, w):
 class GLMModel(Model):
     algo = "glm"
 
+    def get_regression_influence_diagnostics(self):
+        """Frame of the DFBETAS columns computed with ``influence='dfbetas'`` (GLMModel RID frame)."""
+        fr = getattr(self, "_rid", None)
+        if fr is None:
+            raise ValueError("train the GLM with influence='dfbetas' first")
+        return fr
+
     def __init__(self, key, params, info):
         super().__init__(key, params, info)
         self.expander: Expander | None = None
@@ -910,6 +917,8 @@ class GLMTrainer:
                 out["aic"] = -2 * ll + 2 * k
             if p["compute_p_values"]:
                 self._p_values(model, family, Zi, y, w, off, beta[0], names, nobs, rank, ex)
+            if p.get("influence"):
+                self._influence(model, family, X, y, w, off, ex, nobs)
         else:
             probs = P.double()
             yl = y.long().clamp(min=0)
@@ -937,6 +946,51 @@ class GLMTrainer:
             agg[n] = agg.get(n, 0.0) + v
         from .base import variable_importance
         out["variable_importances"] = variable_importance(list(agg.keys()), list(agg.values()))
+
+    def _influence(self, model, family, X, y, w, off, ex, nobs):
+        """Regression influence diagnostics (RegressionInfluenceDiagnosticsTasks): DFBETAS of every row and
+        coefficient on the raw scale. Gaussian: (β - β₍ᵢ₎)ⱼ / (s₍ᵢ₎ √(XᵀX)⁻¹ⱼⱼ) with the leave-one-out β₍ᵢ₎ and
+        s₍ᵢ₎ in closed form; binomial: rᵢwᵢ/(1 - hᵢ) · (G⁻¹xᵢ)ⱼ / seⱼ with G = XᵀWX, hᵢ = wᵢμᵢ(1-μᵢ)xᵢᵀG⁻¹xᵢ."""
+        p = self.p
+        if str(p["influence"]).lower() != "dfbetas":
+            raise ValueError("influence must be 'dfbetas'")
+        if family.name not in ("gaussian", "binomial") or float(p.get("lambda_") or 0.0) != 0.0:
+            raise ValueError("influence='dfbetas' needs family gaussian or binomial and lambda = 0")
+        if coll.is_dist():
+            raise ValueError("influence diagnostics need a single-process frame")
+        raw = Expander(ex.info, standardize=False, use_all_factor_levels=ex.use_all).fit(X, w)
+        Xr = raw.transform(X).double()
+        Xr = torch.cat([Xr, torch.ones(Xr.shape[0], 1, dtype=Xr.dtype, device=Xr.device)], 1)
+        braw, ic = ex.destandardize(model.beta[0, :-1], float(model.beta[0, -1]))
+        b = torch.cat([braw.double(), torch.tensor([ic], dtype=torch.float64, device=braw.device)])
+        eta = Xr @ b + off
+        mu = family.linkinv(eta)
+        r = y.double() - mu
+        wd = w.double()
+        if family.name == "gaussian":
+            G = (Xr * wd[:, None]).T @ Xr
+            Gi = torch.linalg.pinv(G)
+            XGi = Xr @ Gi
+            h = wd * (XGi * Xr).sum(1)
+            pdim = Xr.shape[1]
+            s2 = float((wd * r * r).sum()) / max(nobs - pdim, 1)
+            s2i = ((nobs - pdim) * s2 - wd * r * r / (1 - h).clamp(min=1e-12)) / max(nobs - pdim - 1, 1)
+            dbeta = XGi * (wd * r / (1 - h).clamp(min=1e-12))[:, None]          # β - β₍ᵢ₎
+            D = dbeta / (s2i.clamp(min=1e-300).sqrt()[:, None] * Gi.diagonal().clamp(min=1e-300).sqrt()[None, :])
+        else:
+            vw = wd * mu * (1 - mu)
+            G = (Xr * vw[:, None]).T @ Xr
+            Gi = torch.linalg.pinv(G)
+            XGi = Xr @ Gi
+            h = vw * (XGi * Xr).sum(1)
+            se = Gi.diagonal().clamp(min=1e-300).sqrt()
+            D = XGi * (r * wd / (1 - h).clamp(min=1e-12))[:, None] / se[None, :]
+        D = torch.where((wd > 0)[:, None], D, torch.zeros_like(D))
+        from ..frame import H2OFrame
+        names = ["DFBETA_" + n for n in list(raw.names) + ["Intercept"]]
+        fr = H2OFrame.from_tensor(D.float(), names)
+        model.output["regression_influence_diagnostics"] = fr.frame_id
+        model._rid = fr
 
     def _p_values(self, model, family, Zi, y, w, off, beta, names, nobs, rank, ex):
         lam = model.output.get("lambda_best", 0.0)

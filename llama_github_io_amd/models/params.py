@@ -40,7 +40,7 @@ UNSUPPORTED = {
     "deeplearning": {"average_activation", "max_categorical_features", "sparsity_beta", "huber_alpha"},
     "xgboost": {"grow_policy",
                 "max_leaves"},
-    "glm": {"dispersion_learning_rate", "fix_tweedie_variance_power", "influence", "rand_link", "tweedie_epsilon",
+    "glm": {"dispersion_learning_rate", "fix_tweedie_variance_power", "rand_link", "tweedie_epsilon",
             "checkpoint", "prior", "early_stopping"},
     "gam": {"beta_constraints", "standardize_tp_gam_cols", "prior", "early_stopping"},
     "anovaglm": {"early_stopping", "prior", "type", "plug_values"},

@@ -41,7 +41,7 @@ def test_unknown_parameter_raises(fr):
     ("word2vec", "word_model", "cbow"),
     ("xgboost", "grow_policy", "lossguide"),
     ("deeplearning", "sparsity_beta", 0.5),
-    ("glm", "influence", "dfbetas"),
+    ("glm", "rand_link", ["identity"]),
 ])
 def test_unsupported_parameter_raises(fr, algo, param, value):
     with pytest.raises(ValueError, match="not supported"):
@@ -258,3 +258,38 @@ def test_kmeans_cluster_size_constraints():
         torch.tensor(X, dtype=torch.float32), None, None, None, info)
     sizes = m.output["training_metrics"]["size"]
     assert sizes is not None and min(sizes) >= 100, sizes
+
+
+@pytest.mark.parametrize("family", ["gaussian", "binomial"])
+def test_glm_dfbetas_match_leave_one_out(family):
+    """influence='dfbetas': gaussian DFBETAS equal the exact leave-one-out refit; binomial is the
+    one-step approximation of the reference (checked for sign/scale against a refit)."""
+    import numpy as np
+    import torch
+    from llama_github_io_amd.models.base import DataInfo
+    from llama_github_io_amd.models.glm import GLMTrainer
+    rng = np.random.default_rng(2)
+    n = 200
+    X = rng.normal(size=(2, n))
+    if family == "gaussian":
+        y = 1 + X[0] - 0.5 * X[1] + rng.normal(size=n) * 0.5
+        dom = None
+    else:
+        y = (rng.random(n) < 1 / (1 + np.exp(-(X[0] - X[1])))).astype(float)
+        dom = ["0", "1"]
+    info = DataInfo(["a", "b"], np.zeros(2, np.int32), [None, None], "y", dom)
+    Xt, yt = torch.tensor(X, dtype=torch.float32), torch.tensor(y, dtype=torch.float32)
+    m = GLMTrainer(dict(family=family, lambda_=0.0, influence="dfbetas")).fit(Xt, yt, None, None, info)
+    D = m.get_regression_influence_diagnostics().as_data_frame()
+    assert list(D.columns) == ["DFBETA_a", "DFBETA_b", "DFBETA_Intercept"]
+    if family == "gaussian":
+        A = np.column_stack([X.T, np.ones(n)])
+        beta = np.linalg.lstsq(A, y, rcond=None)[0]
+        i = 7
+        keep = np.arange(n) != i
+        b_i = np.linalg.lstsq(A[keep], y[keep], rcond=None)[0]
+        s_i = np.sqrt(((y[keep] - A[keep] @ b_i) ** 2).sum() / (n - 1 - 3))
+        ref = (beta - b_i) / (s_i * np.sqrt(np.diag(np.linalg.inv(A.T @ A))))
+        assert np.allclose(D.iloc[i].to_numpy(), ref, rtol=1e-3, atol=1e-4)
+    else:
+        assert np.isfinite(D.to_numpy()).all() and D.abs().to_numpy().max() < 2
