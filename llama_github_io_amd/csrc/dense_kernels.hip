@@ -150,9 +150,90 @@ __global__ __launch_bounds__(256) void k_out_grad(const T* __restrict__ logits, 
   }
 }
 
+// ---- DataInfo (Expander) numeric columns: feature-major raw X [F, N] fp32 -> row-major design Z [N, P]
+// Per-feature weighted moments in one pass (NaN skipped): out[j] = {Σw, Σw·x, Σw·x²} (fp64). grid (blocks
+// over rows, features); each block reduces its row range in fp64 and adds once per feature.
+__global__ __launch_bounds__(256) void k_num_stats(const float* __restrict__ X, int64_t N, const int* __restrict__ rows,
+                                                   const float* __restrict__ w, double* __restrict__ out) {
+  const int j = blockIdx.y;
+  const float* x = X + (int64_t)rows[j] * N;
+  double a = 0.0, b = 0.0, c = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += (int64_t)gridDim.x * blockDim.x) {
+    const float v = x[i];
+    if (v == v) {
+      const double ww = w ? (double)w[i] : 1.0;
+      a += ww; b += ww * v; c += ww * (double)v * v;
+    }
+  }
+  __shared__ double red[3][8];
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_down(a, o, 64); b += __shfl_down(b, o, 64); c += __shfl_down(c, o, 64);
+  }
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) { red[0][wv] = a; red[1][wv] = b; red[2][wv] = c; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s0 = 0, s1 = 0, s2 = 0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) { s0 += red[0][k]; s1 += red[1][k]; s2 += red[2][k]; }
+    atomicAdd(out + 3 * j, s0); atomicAdd(out + 3 * j + 1, s1); atomicAdd(out + 3 * j + 2, s2);
+  }
+}
+
+// Z[r, col0 + j] = (isnan(x) ? fill_j : x - sub_j) * mul_j for the numeric rows listed in `rows`, through a
+// 64-row x 32-feature LDS tile: reads coalesced along N, writes coalesced along P.
+template <typename T>
+__global__ __launch_bounds__(256) void k_num_transform(const float* __restrict__ X, int64_t N, const int* __restrict__ rows,
+                                                       int nf, const float* __restrict__ fill, const float* __restrict__ sub,
+                                                       const float* __restrict__ mul, T* __restrict__ Z, int ldz, int col0) {
+  __shared__ float tile[32][65];
+  const int64_t r0 = (int64_t)blockIdx.x * 64;
+  const int f0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;   // 64 x 4
+  for (int k = ty; k < 32; k += 4) {
+    const int f = f0 + k;
+    const int64_t r = r0 + tx;
+    float v = 0.f;
+    if (f < nf && r < N) {
+      v = X[(int64_t)rows[f] * N + r];
+      v = (v != v) ? fill[f] : v;
+      v = (v - sub[f]) * mul[f];
+    }
+    tile[k][tx] = v;
+  }
+  __syncthreads();
+  // write: each warp-row of 32 lanes covers the 32 features of one row
+  const int lx = threadIdx.x & 31, ly = threadIdx.x >> 5;   // 32 x 8
+  for (int rr = ly; rr < 64; rr += 8) {
+    const int64_t r = r0 + rr;
+    const int f = f0 + lx;
+    if (r < N && f < nf) st(Z, r * ldz + col0 + f, tile[lx][rr]);
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+int h2o_num_stats(const float* X, long long N, const int* rows, int nf, const float* w, double* out, hipStream_t s) {
+  if (N <= 0 || nf <= 0) return 0;
+  long long g = (N + 255) / 256;
+  if (g > 64) g = 64;
+  hipLaunchKernelGGL(k_num_stats, dim3((unsigned)g, (unsigned)nf), dim3(256), 0, s, X, (int64_t)N, rows, w, out);
+  return (int)hipGetLastError();
+}
+
+int h2o_num_transform(const float* X, long long N, const int* rows, int nf, const float* fill, const float* sub,
+                      const float* mul, void* Z, int ldz, int col0, int bf16, hipStream_t s) {
+  if (N <= 0 || nf <= 0) return 0;
+  dim3 grid((unsigned)((N + 63) / 64), (unsigned)((nf + 31) / 32));
+  if (bf16)
+    hipLaunchKernelGGL(k_num_transform<__hip_bfloat16>, grid, dim3(256), 0, s, X, (int64_t)N, rows, nf, fill, sub, mul,
+                       (__hip_bfloat16*)Z, ldz, col0);
+  else
+    hipLaunchKernelGGL(k_num_transform<float>, grid, dim3(256), 0, s, X, (int64_t)N, rows, nf, fill, sub, mul, (float*)Z,
+                       ldz, col0);
+  return (int)hipGetLastError();
+}
 
 int h2o_adadelta(float* p, const float* g, float* eg2, float* edx2, long long n, long long n_decay, float rho, float eps,
                  float l1, float l2, void* shadow, hipStream_t stream) {

@@ -19,6 +19,19 @@ from .base import DataInfo
 from ..ops.segment import segment_sum
 
 
+def _hip_ok(X) -> bool:
+    """The HIP Expander kernels take a contiguous fp32 [F, N] device matrix."""
+    if not (X.is_cuda and X.dtype == torch.float32 and X.is_contiguous()):
+        return False
+    from ..ops import _native as nat
+    nat.register_hip_signatures({
+        "h2o_num_stats": [nat.c_void_p, nat.c_ll, nat.c_void_p, nat.c_int, nat.c_void_p, nat.c_void_p, nat.c_void_p],
+        "h2o_num_transform": [nat.c_void_p, nat.c_ll, nat.c_void_p, nat.c_int, nat.c_void_p, nat.c_void_p, nat.c_void_p,
+                              nat.c_void_p, nat.c_int, nat.c_int, nat.c_int, nat.c_void_p],
+    })
+    return True
+
+
 class Expander:
     def __init__(self, info: DataInfo, standardize=True, use_all_factor_levels=False, missing="MeanImputation",
                  missing_bucket=False, center_only=False, plug_values=None):
@@ -66,7 +79,17 @@ class Expander:
         s1 = torch.zeros(k, dtype=torch.float64, device=dev)
         s2 = torch.zeros(k, dtype=torch.float64, device=dev)
         CH = 32   # feature chunks keep the fp64 temporaries small on wide frames (e.g. 784 x 10M)
-        for a in range(0, k, CH):
+        if k and _hip_ok(X):
+            # one HIP pass over the numeric rows: fp64 Σw, Σwx, Σwx² per feature (k_num_stats)
+            from ..ops import _native as nat
+            rows = torch.as_tensor(self.nums, dtype=torch.int32, device=dev)
+            st = torch.zeros(k, 3, dtype=torch.float64, device=dev)
+            wf = w.float().contiguous()
+            nat.call("h2o_num_stats", X.data_ptr(), N, rows.data_ptr(), k, wf.data_ptr(), st.data_ptr(),
+                     nat.stream_ptr(dev))
+            sw, s1, s2 = st[:, 0].clone(), st[:, 1].clone(), st[:, 2].clone()
+            CH = 0
+        for a in range(0, k if CH else 0, CH or 1):
             Xn = X[self.nums[a:a + CH]].double()
             ok = ~torch.isnan(Xn)
             Xz = torch.where(ok, Xn, torch.zeros_like(Xn))
@@ -133,6 +156,19 @@ class Expander:
             Z[rows, idx[rows]] = 1
         CH = 32
         fill_all = getattr(self, "num_fill", None)
+        if self.nums and _hip_ok(X) and dtype in (torch.float32, torch.bfloat16):
+            # one tiled HIP pass (k_num_transform): NaN fill, centring / scaling, transpose into Z
+            from ..ops import _native as nat
+            k = len(self.nums)
+            rows = torch.as_tensor(self.nums, dtype=torch.int32, device=dev)
+            mu = self.num_mean.to(dev).float()
+            fill = (mu if fill_all is None else fill_all.to(dev).float()).contiguous()
+            sub = mu if (self.standardize or self.center_only) else torch.zeros_like(mu)
+            mul = (1.0 / self.num_sd.to(dev).float()) if self.standardize else torch.ones_like(mu)
+            nat.call("h2o_num_transform", X.data_ptr(), N, rows.data_ptr(), k, fill.data_ptr(), sub.contiguous().data_ptr(),
+                     mul.contiguous().data_ptr(), Z.data_ptr(), self.P, self.num_off, int(dtype == torch.bfloat16),
+                     nat.stream_ptr(dev))
+            return Z
         for a in range(0, len(self.nums), CH):
             Xn = X[self.nums[a:a + CH]].to(dtype=torch.float64)
             mu = self.num_mean[a:a + CH, None]

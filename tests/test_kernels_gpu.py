@@ -297,3 +297,29 @@ def test_deeplearning_explicit_step_matches_autograd_gpu(dtype, monkeypatch):
         assert torch.allclose(res[0], res[1], atol=1e-4, rtol=1e-3)
     else:   # bf16 GEMMs: the two paths round differently; both must learn equally well
         assert abs(aucs[0] - aucs[1]) < 0.02 and min(aucs) > 0.9
+
+
+@pytest.mark.parametrize("standardize", [True, False])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_expander_hip_matches_cpu(standardize, dtype):
+    # k_num_stats / k_num_transform (NaN fill, centring, scaling, transpose) vs the PyTorch path
+    from llama_github_io_amd.models.base import DataInfo
+    from llama_github_io_amd.models.datainfo import Expander
+    g = torch.Generator().manual_seed(4)
+    F, N = 70, 10001
+    X = torch.randn(F, N, generator=g) * 3 + 1
+    X[2, ::7] = float("nan")
+    X[5] = torch.randint(0, 4, (N,), generator=g).float()
+    X[5, ::11] = float("nan")
+    iscat = np.zeros(F, np.int32)
+    iscat[5] = 1
+    info = DataInfo([f"x{i}" for i in range(F)], iscat, [None] * 5 + [["a", "b", "c", "d"]] + [None] * (F - 6), "y", None)
+    w = torch.rand(N, generator=g).double()
+    ec = Expander(info, standardize=standardize).fit(X, w)
+    eg = Expander(info, standardize=standardize).fit(X.to(dev), w.to(dev))
+    assert torch.allclose(ec.num_mean, eg.num_mean.cpu(), rtol=1e-9, atol=1e-9)
+    assert torch.allclose(ec.num_sd, eg.num_sd.cpu(), rtol=1e-9, atol=1e-9)
+    Zc = ec.transform(X, dtype=torch.float32)
+    Zg = eg.transform(X.to(dev), dtype=dtype).float().cpu()
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    assert torch.allclose(Zc, Zg, rtol=tol, atol=tol)
