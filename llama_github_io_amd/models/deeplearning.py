@@ -766,8 +766,9 @@ class DeepLearningTrainer:
         if n >= Ng:
             idx = torch.arange(N, device=X.device)
         else:       # a sample of GLOBAL rows (same rows however the frame is sharded)
-            gi = torch.randperm(Ng, generator=torch.Generator().manual_seed(int(p.get("seed") or 0) & 0x7FFFFFFF))[:n]
-            gi = gi.to(X.device)
+            # drawn on the device (a host randperm of 10M rows costs ~0.2 s per scoring event)
+            gi = torch.randperm(Ng, device=X.device, generator=torch.Generator(device=X.device).manual_seed(
+                int(p.get("seed") or 0) & 0x7FFFFFFF))[:n]
             idx = gi[(gi >= r0) & (gi < r0 + N)] - r0
         Xs = X[:, idx]
         ev = dict(epochs=epochs, timestamp=time.time())
