@@ -387,40 +387,26 @@ def solve_penalized(Gm, r, l1, l2, intercept, beta0=None, non_negative=False, ma
             except Exception:  # noqa: BLE001 - singular Gram: add ridge jitter (Gram.java addDiag)
                 jitter = 1e-8 if jitter == 0 else jitter * 100
         return torch.linalg.lstsq(A, r[:, None]).solution[:, 0]
-    # cyclic coordinate descent on the Gram (host loop over P, device-resident vectors)
+    # cyclic coordinate descent on the Gram: native C++ (csrc/glm_solver.cpp) on the host copy of G (P x P)
+    import ctypes
+    from ..ops import _native as nat
     b = torch.zeros(P, dtype=torch.float64, device=Gm.device) if beta0 is None else beta0.clone()
-    Gh = Gm.cpu().numpy()
-    rh = r.cpu().numpy()
-    bh = b.cpu().numpy()
-    diag = np.diag(Gh).copy()
-    grad = Gh @ bh
-    penh = pen.cpu().numpy()
-    lbh = None if lb is None else lb.cpu().numpy()
-    ubh = None if ub is None else ub.cpu().numpy()
-    if boxed:
-        bh = np.clip(bh, lbh if lbh is not None else -np.inf, ubh if ubh is not None else np.inf)
-        grad = Gh @ bh
-    for it in range(max_iter):
-        mx = 0.0
-        for j in range(P):
-            denom = diag[j] + l2 * penh[j]
-            if denom <= 0:
-                continue
-            rho = rh[j] - (grad[j] - diag[j] * bh[j])
-            nb = rho / denom if penh[j] == 0 else np.sign(rho) * max(abs(rho) - l1, 0.0) / denom
-            if non_negative and penh[j] > 0:
-                nb = max(nb, 0.0)
-            if lbh is not None:
-                nb = max(nb, lbh[j])
-            if ubh is not None:
-                nb = min(nb, ubh[j])
-            d = nb - bh[j]
-            if d != 0.0:
-                grad += Gh[:, j] * d
-                bh[j] = nb
-                mx = max(mx, abs(d))
-        if mx < tol:
-            break
+    Gh = np.ascontiguousarray(Gm.double().cpu().numpy())
+    rh = np.ascontiguousarray(r.double().cpu().numpy())
+    bh = np.ascontiguousarray(b.double().cpu().numpy())
+    penh = np.ascontiguousarray(pen.cpu().numpy())
+    nan = np.full(P, np.nan)
+    lbh = np.ascontiguousarray(nan if lb is None else np.where(np.isinf(lb.cpu().numpy()), np.nan, lb.cpu().numpy()))
+    ubh = np.ascontiguousarray(nan if ub is None else np.where(np.isinf(ub.cpu().numpy()), np.nan, ub.cpu().numpy()))
+    lib = nat.rt()
+    fn = lib.h2o_gram_cd
+    dp = ctypes.POINTER(ctypes.c_double)
+    fn.argtypes = [dp, dp, ctypes.c_int, ctypes.c_double, ctypes.c_double, dp, ctypes.c_int, dp, dp, dp, ctypes.c_int,
+                   ctypes.c_double]
+    fn.restype = ctypes.c_int
+    ptr = lambda a_: a_.ctypes.data_as(dp)  # noqa: E731
+    fn(ptr(Gh), ptr(rh), P, float(l1), float(l2), ptr(penh), int(bool(non_negative)), ptr(lbh), ptr(ubh), ptr(bh),
+       int(max_iter), float(tol))
     return torch.as_tensor(bh, device=Gm.device)
 
 
