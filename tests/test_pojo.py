@@ -209,3 +209,46 @@ def test_pojo_compiles(df, tmp_path):   # pragma: no cover - exercised only wher
     est.train(x=["a", "b", "c"], y="y", training_frame=df)
     path = est.download_pojo(str(tmp_path))
     subprocess.run(["javac", "-d", str(tmp_path), path], check=True)
+
+
+def _arr(src, name):
+    m = re.search(name + r" = new double\[\]\[\] \{(.*?)\};\n", src, re.S)
+    if m:
+        rows = re.findall(r"\{([^{}]*)\}", m.group(1))
+        return np.array([[float(v) for v in r.split(",")] for r in rows])
+    m = re.search(name + r" = new (?:double|int)\[\] \{(.*?)\};", src)
+    body = m.group(1).strip()
+    return np.array([float(v) for v in body.split(",")]) if body else np.zeros(0)
+
+
+@pytest.mark.parametrize("y", ["y", "r"])
+def test_deeplearning_pojo_reproduces_model(df, y):
+    from h2o.estimators import H2ODeepLearningEstimator
+    m = H2ODeepLearningEstimator(hidden=[6, 5], epochs=2, seed=1, activation="Tanh")
+    m.train(x=["a", "b", "c"], y=y, training_frame=df)
+    mod = m._model
+    src = P.pojo_source(mod)
+    assert src.count("{") == src.count("}") and "static double act(double v) { return Math.tanh(v); }" in src
+    X, _ = df.model_matrix(mod.info)
+    D = X.double().numpy()
+    cats, offs, sizes, modes, nums = (_arr(src, n).astype(int) for n in ("CATS", "CAT_OFFS", "CAT_SIZES", "CAT_MODES", "NUMS"))
+    fill, sub, mul = _arr(src, "NUM_FILL"), _arr(src, "NUM_SUB"), _arr(src, "NUM_MUL")
+    start = 0 if mod.expander.use_all else 1
+    N = D.shape[1]
+    x = np.zeros((N, mod.expander.P))
+    for i, j in enumerate(cats):
+        v = np.where(np.isnan(D[j]), modes[i], D[j]).astype(int) - start
+        ok = (v >= 0) & (v < sizes[i])
+        x[np.nonzero(ok)[0], offs[i] + v[ok]] = 1
+    for i, j in enumerate(nums):
+        x[:, mod.expander.num_off + i] = (np.where(np.isnan(D[j]), fill[i], D[j]) - sub[i]) * mul[i]
+    L = len(mod.net.hidden)
+    for i in range(L):
+        x = np.tanh(x @ _arr(src, f"W{i}").T + _arr(src, f"B{i}"))
+    o = x @ _arr(src, f"W{L}").T + _arr(src, f"B{L}")
+    P_ = mod.score_tensor(X).double().numpy()
+    if y == "y":
+        e = np.exp(o - o.max(1, keepdims=True))
+        assert np.allclose(e / e.sum(1, keepdims=True), P_, atol=1e-4)
+    else:
+        assert np.allclose(o[:, 0] * mod.resp_sd + mod.resp_mu, P_.reshape(-1), atol=1e-3)
