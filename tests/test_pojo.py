@@ -252,3 +252,31 @@ def test_deeplearning_pojo_reproduces_model(df, y):
         assert np.allclose(e / e.sum(1, keepdims=True), P_, atol=1e-4)
     else:
         assert np.allclose(o[:, 0] * mod.resp_sd + mod.resp_mu, P_.reshape(-1), atol=1e-3)
+
+
+def test_naivebayes_pojo_constants_reproduce_model(df):
+    from h2o.estimators import H2ONaiveBayesEstimator
+    m = H2ONaiveBayesEstimator()
+    m.train(x=["a", "b", "c"], y="y", training_frame=df)
+    mod = m._model
+    src = P.pojo_source(mod)
+    assert src.count("{") == src.count("}")
+    prior = _arr(src, "PRIOR")
+    X, _ = df.model_matrix(mod.info)
+    D = X.double().numpy()
+    ll = np.log(prior)[None, :].repeat(D.shape[1], 0)
+    p = mod.params
+    for j in range(mod.info.F):
+        c = _arr(src, f"COND{j}")
+        na = np.isnan(D[j])
+        if mod.info.iscat[j]:
+            code = np.clip(np.nan_to_num(D[j]).astype(int), 0, c.shape[1] - 1)
+            pr = c[:, code].T
+            pr = np.where(pr <= p["eps_prob"], p["min_prob"], pr)
+            ll += np.where(na[:, None], 0, np.log(pr))
+        else:
+            sd = np.where(c[1] <= p["eps_sdev"], p["min_sdev"], c[1])
+            z = (D[j][:, None] - c[0][None, :]) / sd[None, :]
+            ll += np.where(na[:, None], 0, -0.5 * z * z - np.log(sd)[None, :] - 0.5 * np.log(2 * np.pi))
+    e = np.exp(ll - ll.max(1, keepdims=True))
+    assert np.allclose(e / e.sum(1, keepdims=True), mod.score_tensor(X).double().numpy(), atol=1e-5)
