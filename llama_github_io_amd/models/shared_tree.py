@@ -213,6 +213,7 @@ class SharedTreeTrainer:
                                       self._split_params(), node_cap=node_cap)
         if p.get("interaction_constraints"):
             self.builder.set_interaction_constraints(*interaction_map(p["interaction_constraints"], info.x))
+        self.builder = self._wrap_builder(self.builder)
         model = self.model_cls(model_key or make_key(self.algo), p, info)
         model.binning = self.binning
         model.device = dev
@@ -406,6 +407,9 @@ class SharedTreeTrainer:
             self.f.copy_(raw + init + (self.offset[:, None] if self.offset is not None else 0))
 
     # defaults, overridden
+    def _wrap_builder(self, builder):
+        return builder
+
     def _amax_for_build(self):
         return None
 

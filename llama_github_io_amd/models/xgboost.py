@@ -135,6 +135,18 @@ class XGBoostTrainer(SharedTreeTrainer):
     def _trees_per_iter(self):
         return self.K
 
+    def _wrap_builder(self, builder):
+        gp = str(self.p.get("grow_policy") or "depthwise").lower()
+        if gp not in ("depthwise", "lossguide"):
+            raise ValueError(f"grow_policy must be depthwise or lossguide, got {gp!r}")
+        L = int(self.p.get("max_leaves") or 0)
+        if L < 0:
+            raise ValueError("max_leaves must be >= 0")
+        # xgboost's hist driver honours max_leaves under both policies (depthwise: shallowest nodes
+        # first; lossguide: largest loss change first). Without a leaf limit both expand every
+        # positive-gain node up to max_depth, i.e. the level-wise tree itself
+        return T.BestFirstBuilder(builder, L, by_depth=gp == "depthwise") if L > 0 else builder
+
     def _k_cols(self, F):
         # colsample_bylevel (H2O col_sample_rate) x colsample_bynode: the engine draws a fresh column sample
         # for every node (XGBoost samples bynode from the level's sample: the expected size is the product)

@@ -808,3 +808,118 @@ def make_builder(bins: torch.Tensor, F, nbins_f, iscat_f, mono_f, max_depth, par
     if bins.is_cuda:
         return GpuTreeBuilder(bins, F, nbins_f, iscat_f, mono_f, max_depth, params, node_cap=node_cap)
     return RefTreeBuilder(bins, F, nbins_f, iscat_f, mono_f, max_depth, params, node_cap=node_cap)
+
+
+# ================================================================================================
+# best-first ("lossguide") growth
+def best_first_prune(tl: TreeLevels, max_leaves: int, by_depth: bool = False):
+    """Cut a level-wise tree down to the one XGBoost's lossguide policy grows (reference:
+    ``h2o-extensions/xgboost`` ``grow_policy=lossguide`` / ``max_leaves`` -> xgboost ``updater_hist``
+    driven by a loss-change priority queue).
+
+    Best-first growth expands, among the current leaves, the one whose split has the largest loss
+    change, until ``max_leaves`` leaves exist or nothing can split. Every split it considers is the
+    split the level-wise engine already found for that node (the node's rows do not depend on growth
+    order), so the best-first tree is a top part of the level-wise tree of the same depth: expand by
+    recorded gain from the root, stop at ``max_leaves``, and every node left unexpanded becomes a
+    leaf holding the sums of the original leaves below it.
+
+    ``by_depth`` is xgboost's depthwise policy under a leaf limit: nodes expand shallowest first, in
+    creation order within a depth.
+
+    Returns ``(pruned TreeLevels without leaf values, map old leaf id -> new leaf id)``.
+    """
+    import heapq
+    decs, cl, cr = tl.decs, tl.child_l, tl.child_r
+    can = lambda d, i: d < len(decs) and int(decs[d]["feat"][i]) >= 0
+    expanded = set()
+    key = (lambda d, i: float(d)) if by_depth else (lambda d, i: -float(decs[d]["gain"][i]))
+    heap = [(key(0, 0), 0, 0, 0)] if decs and can(0, 0) else []
+    leaves, seq = 1, 1
+    while heap and (max_leaves <= 0 or leaves < max_leaves):
+        _, _, d, i = heapq.heappop(heap)
+        expanded.add((d, i))
+        leaves += 1
+        for c in (int(cl[d][i]), int(cr[d][i])):
+            if c >= 0 and can(d + 1, c):
+                heapq.heappush(heap, (key(d + 1, c), seq, d + 1, c))
+                seq += 1
+    leaf_map = np.zeros(max(int(tl.n_leaves), 1), dtype=np.int64)
+
+    def sub_leaves(d, i):
+        out, stack = [], [(d, i)]
+        while stack:
+            a, b = stack.pop()
+            for c in {int(cl[a][b]), int(cr[a][b])}:
+                if c < 0:
+                    out.append(-1 - c)
+                else:
+                    stack.append((a + 1, c))
+        return out
+
+    ndecs, ncl, ncr = [], [], []
+    n_new = 0
+    level = [0] if decs else []
+    d = 0
+    while level:
+        dd = decs[d][level].copy()
+        lcl = np.zeros(len(level), dtype=np.int64)
+        lcr = np.zeros(len(level), dtype=np.int64)
+        nxt = []
+        for j, i in enumerate(level):
+            if (d, i) in expanded:
+                for c, arr in ((int(cl[d][i]), lcl), (int(cr[d][i]), lcr)):
+                    if c >= 0:
+                        arr[j] = len(nxt)
+                        nxt.append(c)
+                    else:
+                        leaf_map[-1 - c] = n_new
+                        arr[j] = -1 - n_new
+                        n_new += 1
+            else:
+                for lf in sub_leaves(d, i):
+                    leaf_map[lf] = n_new
+                dd["feat"][j] = -1
+                dd["gain"][j] = 0.0
+                lcl[j] = lcr[j] = -1 - n_new
+                n_new += 1
+        ndecs.append(dd)
+        ncl.append(lcl)
+        ncr.append(lcr)
+        level = nxt
+        d += 1
+    return TreeLevels(ndecs, ncl, ncr, max(n_new, 1), None, tl.root_weight), leaf_map
+
+
+class BestFirstBuilder:
+    """Builder wrapper that grows each tree level-wise on the GPU, then prunes it best-first to
+    ``max_leaves`` leaves (:func:`best_first_prune`) and remaps the rows' leaf ids and the leaf sums
+    on the device. The wrapper waits for each tree's structure (one sync per tree)."""
+
+    def __init__(self, inner, max_leaves: int, by_depth: bool = False):
+        self.inner, self.max_leaves, self.by_depth = inner, int(max_leaves), bool(by_depth)
+        self.done = []
+        self.leaf_of_row = None
+        self.leafsum = None
+
+    def __getattr__(self, name):
+        return getattr(self.inner, name)
+
+    def build(self, aux_static, feat_ok=None, k_cols=0, seed=0, leaf_fn=None, **kw):
+        kw.pop("leaf_native", None)
+        self.inner.build(aux_static, feat_ok, k_cols, seed=seed, leaf_fn=None, **kw)
+        tl = self.inner.pop_levels()[-1]
+        pruned, lmap = best_first_prune(tl, self.max_leaves, self.by_depth)
+        dev = self.inner.leaf_of_row.device
+        m = torch.from_numpy(lmap).to(dev)
+        self.leaf_of_row = m[self.inner.leaf_of_row.long()].to(torch.int32)
+        ls = self.inner.leafsum[: tl.n_leaves].to(dev)
+        self.leafsum = torch.zeros(pruned.n_leaves, ls.shape[1], dtype=ls.dtype, device=dev).index_add_(0, m[: ls.shape[0]], ls)
+        if leaf_fn is not None:
+            pruned.leaf_values = leaf_fn(self.leafsum).to(torch.float32).cpu().numpy()
+        self.done.append(pruned)
+        return len(self.done) - 1
+
+    def pop_levels(self, ready_only: bool = False) -> list:
+        out, self.done = self.done, []
+        return out

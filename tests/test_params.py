@@ -39,7 +39,6 @@ def test_unknown_parameter_raises(fr):
 
 @pytest.mark.parametrize("algo,param,value", [
     ("word2vec", "word_model", "cbow"),
-    ("xgboost", "grow_policy", "lossguide"),
     ("deeplearning", "sparsity_beta", 0.5),
     ("glm", "rand_link", ["identity"]),
 ])
@@ -293,3 +292,36 @@ def test_glm_dfbetas_match_leave_one_out(family):
         assert np.allclose(D.iloc[i].to_numpy(), ref, rtol=1e-3, atol=1e-4)
     else:
         assert np.isfinite(D.to_numpy()).all() and D.abs().to_numpy().max() < 2
+
+
+@pytest.mark.parametrize("policy", ["lossguide", "depthwise"])
+def test_xgboost_max_leaves_grow_policy(fr, policy):
+    """grow_policy / max_leaves (xgboost hist driver): the first tree is the full level-wise tree
+    expanded best-first (lossguide: largest gain; depthwise: shallowest) down to max_leaves leaves; the
+    model's predictions agree with the margins the trainer accumulated."""
+    import heapq
+    base = dict(ntrees=4, max_depth=5, seed=3, learn_rate=0.3, min_rows=2)
+    full = builder.train("xgboost", base, x=X, y="r", training_frame=fr)
+    m = builder.train("xgboost", dict(base, grow_policy=policy, max_leaves=6), x=X, y="r", training_frame=fr)
+    for t in m.forest.trees:
+        assert t.n_leaves() <= 6
+    t0 = full.forest.trees[0]
+    depth = {0: 0}
+    heap, seq, leaves, keep = [(0.0, 0, 0)], 1, 1, []
+    while heap and leaves < 6:
+        _, _, n = heapq.heappop(heap)
+        keep.append((int(t0.feat[n]), float(t0.thr[n])))
+        leaves += 1
+        for c in (int(t0.left[n]), int(t0.right[n])):
+            depth[c] = depth[n] + 1
+            if t0.feat[c] >= 0:
+                heapq.heappush(heap, (depth[c] if policy == "depthwise" else -float(t0.gain[c]), seq, c))
+                seq += 1
+    p0 = m.forest.trees[0]
+    got = sorted((int(f), float(th)) for f, th in zip(p0.feat, p0.thr) if f >= 0)
+    assert got == sorted(keep)
+    pred = m.predict(fr).as_data_frame()["predict"].to_numpy()
+    y = fr.as_data_frame()["r"].to_numpy()
+    assert np.mean((pred - y) ** 2) == pytest.approx(m.output["training_metrics"]["MSE"], rel=1e-4)
+    with pytest.raises(Exception, match="grow_policy"):
+        builder.train("xgboost", dict(base, grow_policy="bogus"), x=X, y="r", training_frame=fr)
