@@ -34,6 +34,7 @@ DL_DEFAULTS = dict(hidden=[200, 200], epochs=10.0, activation="Rectifier", adapt
                    hidden_dropout_ratios=None, l1=0.0, l2=0.0, max_w2=float("inf"),
                    initial_weight_distribution="UniformAdaptive", initial_weight_scale=1.0, loss="Automatic",
                    distribution="AUTO", tweedie_power=1.5, quantile_alpha=0.5, huber_alpha=0.9,
+                   average_activation=0.0, sparsity_beta=0.0,
                    mini_batch_size=1, autoencoder=False, standardize=True, use_all_factor_levels=True,
                    stopping_rounds=5, stopping_metric="AUTO", stopping_tolerance=0.0, score_interval=5.0,
                    score_training_samples=10000, seed=-1, shuffle_training_data=True, reproducible=False,
@@ -63,6 +64,7 @@ class MLP(torch.nn.Module):
         self._init(self.out, dims[-1], n_out, init_dist, init_scale, gen)
         self.step = 0
         self.step_dev = None
+        self.track = None       # dict layer -> batch-mean activation (sparse autoencoder)
 
     @staticmethod
     def _init(lin, fan_in, fan_out, dist, scale, gen):
@@ -98,6 +100,8 @@ class MLP(torch.nn.Module):
                     x = bias_act(xin, lin.bias, self.act, drop, base, self.step_dev)
                 else:
                     x = bias_act(xin, lin.bias, self.act, drop, step_seed(base, self.step))
+                if self.track is not None:
+                    self.track[i] = x.detach().float().mean(0)
             if features_layer is not None and i == features_layer:
                 return x
         return self.out(x)
@@ -229,6 +233,11 @@ class DeepLearningTrainer:
         dist = str(p["distribution"]).lower()
         if dist == "auto":
             dist = "gaussian" if cat == "Regression" else ("bernoulli" if cat == "Binomial" else "multinomial")
+        # huber: delta starts at 1 and is re-estimated at every training scoring event as the weighted
+        # huber_alpha quantile of |actual - prediction| (DeepLearningModel.doScoring: setHuberDelta); a
+        # device scalar so captured step graphs see the update
+        self._hdelta = torch.ones((), dtype=torch.float32, device=dev)
+        self._dist = dist
         net = MLP(Z.shape[1], hidden, n_out, "rectifier" if maxout else base, maxout, float(p["input_dropout_ratio"]),
                   [float(v) for v in hd], str(p["initial_weight_distribution"]), float(p["initial_weight_scale"]), gen).to(dev)
         prev_epochs = 0.0
@@ -321,13 +330,28 @@ class DeepLearningTrainer:
         gbuf = torch.empty(fp.g.numel() + 1, dtype=fp.g.dtype, device=fp.g.device) if sharded else None
         tdim = tuple(yt.shape[1:]) if yt is not None else ()
 
+        # sparse autoencoder (Neurons.compute_sparsity / update_bias): a rolling mean activation per neuron
+        # of every hidden layer but the last (decay 0.999 per row) pulls each bias by
+        # sparsity_beta * (mean activation - average_activation): here as that gradient on the bias
+        beta_sp = float(p.get("sparsity_beta") or 0.0)
+        sparse = ae and beta_sp > 0 and len(hidden) > 1 and not maxout
+        avg_a = [torch.zeros(int(hidden[l]), dtype=torch.float32, device=dev) for l in range(len(hidden) - 1)] if sparse else []
+        tgt_a = float(p.get("average_activation") or 0.0)
+
         def fwd_bwd(xb, wb, tb):
             """Forward + backward of one (local) batch into fp.g: the gradient of the weighted loss sum,
             normalised by the batch weight (single process) or raw + batch weight in gbuf (sharded)."""
             fp.zero_grad()
+            net.track = {} if sparse else None
             with torch.autocast(device_type=dev.type, dtype=dtype, enabled=dtype is not None):
                 o = net(xb, seed)
             ls = self._loss(o.float(), xb if ae else tb, wb, cat, dist, ae)
+            if sparse:
+                dec = 0.999 ** xb.shape[0]
+                for l, a in enumerate(avg_a):
+                    a.mul_(dec).add_(net.track[l] * (1.0 - dec))
+                    ls = ls + wb.sum() * beta_sp * ((a - tgt_a) * net.hidden[l].bias.float()).sum()
+                net.track = None
             if sharded:
                 ls.backward()
                 gbuf[:-1].copy_(fp.g)
@@ -744,7 +768,9 @@ class DeepLearningTrainer:
             r = t - f
             return (w * torch.where(r >= 0, a * r, (a - 1) * r)).sum()
         if lname == "huber" or dist == "huber":
-            return (w * torch.nn.functional.huber_loss(f, t, reduction="none", delta=1.0)).sum()
+            d = self._hdelta if hasattr(self, "_hdelta") else torch.ones((), device=f.device)
+            a = (f - t).abs()
+            return (w * torch.where(a <= d, 0.5 * a * a, d * (a - 0.5 * d))).sum()
         if dist == "poisson":
             return (w * (torch.exp(f) - t * f)).sum()
         if dist == "gamma":
@@ -776,6 +802,12 @@ class DeepLearningTrainer:
             m = self._ae_metrics(model, Xs)
         else:
             m = model.metrics_for(Xs, y[idx], w[idx].float())
+            if self._dist == "huber" and hasattr(self, "_hdelta"):
+                from .quantile import weighted_quantiles
+                r = (y[idx].double() - model._predict_tensor(Xs).reshape(-1).double()).abs()
+                dq = float(weighted_quantiles(r, [float(p["huber_alpha"])], w=w[idx])[0])
+                if math.isfinite(dq):
+                    self._hdelta.fill_(dq)
         ev["_train"] = m
         for k in ("RMSE", "logloss", "AUC", "mean_per_class_error", "MSE"):
             if m is not None and k in m:

@@ -39,7 +39,7 @@ def test_unknown_parameter_raises(fr):
 
 @pytest.mark.parametrize("algo,param,value", [
     ("word2vec", "word_model", "cbow"),
-    ("deeplearning", "sparsity_beta", 0.5),
+    ("deeplearning", "max_categorical_features", 10),
     ("glm", "rand_link", ["identity"]),
 ])
 def test_unsupported_parameter_raises(fr, algo, param, value):
@@ -325,3 +325,33 @@ def test_xgboost_max_leaves_grow_policy(fr, policy):
     assert np.mean((pred - y) ** 2) == pytest.approx(m.output["training_metrics"]["MSE"], rel=1e-4)
     with pytest.raises(Exception, match="grow_policy"):
         builder.train("xgboost", dict(base, grow_policy="bogus"), x=X, y="r", training_frame=fr)
+
+
+def test_deeplearning_huber_delta_and_sparsity():
+    """DL huber: delta re-estimated at each training scoring event as the weighted huber_alpha quantile
+    of |actual - prediction| (DeepLearningModel.doScoring); sparse autoencoder: sparsity_beta pulls the
+    hidden layers' mean activation toward average_activation (Neurons.update_bias)."""
+    import torch
+    from llama_github_io_amd.models.deeplearning import DeepLearningTrainer
+    from llama_github_io_amd.models.quantile import weighted_quantiles
+    from llama_github_io_amd.models.datainfo import DataInfo
+    g = torch.Generator().manual_seed(0)
+    X = torch.randn(4, 3000, generator=g)
+    y = X[0] * 2 - X[1] + torch.randn(3000, generator=g) * 0.3
+    info = DataInfo(list("abcd"), np.zeros(4, np.int32), [None] * 4, "y", None)
+    tr = DeepLearningTrainer(dict(hidden=[16], epochs=2, seed=1, distribution="huber", huber_alpha=0.8,
+                                  reproducible=True))
+    m = tr.fit(X, y, None, None, info)
+    r = (y.double() - m._predict_tensor(X).reshape(-1).double()).abs()
+    q = float(weighted_quantiles(r, [0.8], w=torch.ones(3000))[0])
+    assert float(tr._hdelta) == pytest.approx(q, rel=1e-4)
+    assert float(tr._hdelta) != 1.0
+    ia = DataInfo(list("abcd"), np.zeros(4, np.int32), [None] * 4, None, None)
+    means = []
+    for beta in (0.0, 20.0):
+        tr = DeepLearningTrainer(dict(hidden=[12, 6, 12], epochs=3, seed=1, autoencoder=True, activation="Tanh",
+                                      sparsity_beta=beta, average_activation=-0.6, reproducible=True))
+        m = tr.fit(X, None, None, None, ia)
+        Z = m.expander.transform(X)
+        means.append(float(m.net(Z, features_layer=0).mean()))
+    assert abs(means[1] + 0.6) < abs(means[0] + 0.6)
