@@ -489,6 +489,22 @@ class GLMTrainer:
             family = Family(fam, link, float(p["tweedie_variance_power"]), float(p["tweedie_link_power"]), float(p["theta"]))
             beta, path, lam_best = self._fit_irls(family, Zi, y, w, off, alpha, obj_reg, intercept, valid, ex, nobs)
             beta = beta[None, :]
+        pr = float(p.get("prior") if p.get("prior") is not None else -1.0)
+        if pr != -1.0:
+            # GLM.java: prior probability of y == 1 when the training rows were sampled; the intercept moves by
+            # -log(ymu (1 - prior) / (prior (1 - ymu))) once the fit is done
+            if not 0.0 < pr < 1.0:
+                raise ValueError("prior must be in (exclusive) range (0,1)")
+            if fam != "binomial":
+                raise ValueError("prior is only allowed with family = binomial")
+            sw = float(coll.all_reduce_scalar(float((w * y).sum())) if coll.is_dist() else (w * y).sum())
+            ymu = sw / W
+            beta = beta.clone()
+            beta[..., -1] += -math.log(ymu * (1 - pr) / (pr * (1 - ymu)))
+            for e in path:
+                if e.get("coefs") is not None:
+                    e["coefs"] = list(e["coefs"])
+                    e["coefs"][-1] = float(e["coefs"][-1]) - math.log(ymu * (1 - pr) / (pr * (1 - ymu)))
         model.beta = beta
         model.output["lambda_best"] = lam_best
         model.output["lambda"] = [e["lambda"] for e in path]

@@ -39,7 +39,7 @@ HINTS = {
 UNSUPPORTED = {
     "deeplearning": {"max_categorical_features"},
     "glm": {"dispersion_learning_rate", "fix_tweedie_variance_power", "rand_link", "tweedie_epsilon",
-            "checkpoint", "prior", "early_stopping"},
+            "checkpoint", "early_stopping"},
     "gam": {"beta_constraints", "standardize_tp_gam_cols", "prior", "early_stopping"},
     "anovaglm": {"early_stopping", "prior", "type", "plug_values"},
     "modelselection": {"beta_constraints", "cold_start", "influence", "max_active_predictors", "prior",

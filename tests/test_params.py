@@ -355,3 +355,25 @@ def test_deeplearning_huber_delta_and_sparsity():
         Z = m.expander.transform(X)
         means.append(float(m.net(Z, features_layer=0).mean()))
     assert abs(means[1] + 0.6) < abs(means[0] + 0.6)
+
+
+def test_glm_prior_moves_intercept():
+    """GLM prior (GLM.java _iceptAdjust): only the intercept moves, by -log(ymu (1-prior) / (prior (1-ymu)))."""
+    import math
+    import torch
+    from llama_github_io_amd.models.glm import GLMTrainer
+    from llama_github_io_amd.models.datainfo import DataInfo
+    g = torch.Generator().manual_seed(0)
+    X = torch.randn(3, 4000, generator=g)
+    y = (torch.rand(4000, generator=g) < torch.sigmoid(X[0] - 0.5 * X[1] - 1.0)).double()
+    info = DataInfo(list("abc"), np.zeros(3, np.int32), [None] * 3, "y", ["0", "1"])
+    base = dict(family="binomial", lambda_=0.0)
+    m0 = GLMTrainer(dict(base)).fit(X, y, None, None, info)
+    m1 = GLMTrainer(dict(base, prior=0.05)).fit(X, y, None, None, info)
+    ymu = float(y.mean())
+    adj = -math.log(ymu * 0.95 / (0.05 * (1 - ymu)))
+    b0, b1 = m0.beta.reshape(-1).double(), m1.beta.reshape(-1).double()
+    assert torch.allclose(b0[:-1], b1[:-1])
+    assert float(b1[-1] - b0[-1]) == pytest.approx(adj, rel=1e-9)
+    with pytest.raises(ValueError, match="prior"):
+        GLMTrainer(dict(base, prior=1.5)).fit(X, y, None, None, info)
