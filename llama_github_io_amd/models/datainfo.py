@@ -133,8 +133,30 @@ class Expander:
     def ncats_expanded(self):
         return self.num_off
 
+    def set_cat_hash(self, n_slots: int, seed: int):
+        """Hash the one-hot categorical columns into ``n_slots`` count columns (DeepLearning
+        ``max_categorical_features``, Neurons.Input.setInput hash trick): one-hot column ``c`` adds 1 to
+        slot ``|murmur2(big-endian int c, seed) % n_slots|``; numeric columns follow the slots."""
+        nc = self.num_off
+        if n_slots >= nc:
+            return self
+        self.cat_hash = dict(n=int(n_slots), seed=int(seed), idx=[abs(_jmod(_murmur2_int(c, seed), n_slots))
+                                                                  for c in range(nc)])
+        self.names = [f"hashed_cat_{i}" for i in range(n_slots)] + self.names[nc:]
+        return self
+
     def transform(self, X: torch.Tensor, dtype=torch.float32) -> torch.Tensor:
         """[F, N] raw -> [N, P] design matrix."""
+        Z = self._transform(X, dtype)
+        h = getattr(self, "cat_hash", None)
+        if h:
+            nc = self.num_off
+            idx = torch.as_tensor(h["idx"], dtype=torch.long, device=Z.device)
+            Zc = torch.zeros(Z.shape[0], h["n"], dtype=Z.dtype, device=Z.device).index_add_(1, idx, Z[:, :nc])
+            Z = torch.cat([Zc, Z[:, nc:]], 1)
+        return Z
+
+    def _transform(self, X: torch.Tensor, dtype=torch.float32) -> torch.Tensor:
         N = X.shape[1]
         dev = X.device
         Z = torch.zeros(N, self.P, dtype=dtype, device=dev)
@@ -214,7 +236,8 @@ class Expander:
                     num_fill=None if nf is None else nf.cpu().tolist(),
                     cat_offsets=self.cat_offsets, cat_sizes=self.cat_sizes, cat_modes=self.cat_modes,
                     num_off=self.num_off, num_mean=self.num_mean.cpu().tolist(), num_sd=self.num_sd.cpu().tolist(),
-                    num_sd_raw=self.num_sd_raw.cpu().tolist(), names=self.names, P=self.P)
+                    num_sd_raw=self.num_sd_raw.cpu().tolist(), names=self.names, P=self.P,
+                    cat_hash=getattr(self, "cat_hash", None))
 
     @staticmethod
     def from_state(info, s, device=None):
@@ -226,6 +249,7 @@ class Expander:
         e.num_sd = torch.tensor(s["num_sd"], dtype=torch.float64, device=dev)
         e.num_sd_raw = torch.tensor(s["num_sd_raw"], dtype=torch.float64, device=dev)
         e.num_fill = None if s.get("num_fill") is None else torch.tensor(s["num_fill"], dtype=torch.float64, device=dev)
+        e.cat_hash = s.get("cat_hash")
         e.fitted = True
         return e
 
@@ -236,3 +260,30 @@ class Expander:
         if getattr(self, "num_fill", None) is not None:
             self.num_fill = self.num_fill.to(device)
         return self
+
+
+def _i32(v: int) -> int:
+    v &= 0xFFFFFFFF
+    return v - (1 << 32) if v >= 1 << 31 else v
+
+
+def _jmod(a: int, b: int) -> int:
+    """Java int remainder (sign of the dividend)."""
+    r = abs(a) % b
+    return -r if a < 0 else r
+
+
+def _murmur2_int(c: int, seed: int) -> int:
+    """MurmurHash2 (32 bit) of the 4 big-endian bytes of ``c`` with a 32-bit ``seed``, as a signed Java int."""
+    m = 0x5BD1E995
+    k = int.from_bytes(int(c & 0xFFFFFFFF).to_bytes(4, "big"), "little")
+    h = (_i32(seed) ^ 4) & 0xFFFFFFFF
+    k = (k * m) & 0xFFFFFFFF
+    k ^= k >> 24
+    k = (k * m) & 0xFFFFFFFF
+    h = (h * m) & 0xFFFFFFFF
+    h ^= k
+    h ^= h >> 13
+    h = (h * m) & 0xFFFFFFFF
+    h ^= h >> 15
+    return _i32(h)

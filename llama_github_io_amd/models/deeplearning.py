@@ -34,7 +34,7 @@ DL_DEFAULTS = dict(hidden=[200, 200], epochs=10.0, activation="Rectifier", adapt
                    hidden_dropout_ratios=None, l1=0.0, l2=0.0, max_w2=float("inf"),
                    initial_weight_distribution="UniformAdaptive", initial_weight_scale=1.0, loss="Automatic",
                    distribution="AUTO", tweedie_power=1.5, quantile_alpha=0.5, huber_alpha=0.9,
-                   average_activation=0.0, sparsity_beta=0.0,
+                   average_activation=0.0, sparsity_beta=0.0, max_categorical_features=2147483647,
                    mini_batch_size=1, autoencoder=False, standardize=True, use_all_factor_levels=True,
                    stopping_rounds=5, stopping_metric="AUTO", stopping_tolerance=0.0, score_interval=5.0,
                    score_training_samples=10000, seed=-1, shuffle_training_data=True, reproducible=False,
@@ -216,6 +216,11 @@ class DeepLearningTrainer:
         self._row0, self._N_glob = row0, N_glob
         ex = Expander(info, standardize=p["standardize"], use_all_factor_levels=p["use_all_factor_levels"]).fit(
             X, w, reduce=coll.all_reduce_ if sharded else None)
+        mcf = p.get("max_categorical_features")
+        mcf = 2147483647 if mcf is None else int(mcf)
+        if mcf < 1:
+            raise ValueError("max_categorical_features must be at least 1")
+        ex.set_cat_hash(mcf, seed)
         # bf16 compute: the design matrix is materialised in bf16 (half the HBM footprint and per-step
         # gather bytes; GEMM inputs need no per-step cast)
         bf16 = dev.type == "cuda" and str(p["compute_dtype"]).lower() in ("bf16", "bfloat16") and not bool(p["autoencoder"])

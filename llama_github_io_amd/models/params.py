@@ -37,7 +37,6 @@ HINTS = {
 
 # parameters not implemented by this engine: a non-default value is refused
 UNSUPPORTED = {
-    "deeplearning": {"max_categorical_features"},
     "glm": {"dispersion_learning_rate", "fix_tweedie_variance_power", "rand_link", "tweedie_epsilon",
             "checkpoint", "early_stopping"},
     "gam": {"beta_constraints", "standardize_tp_gam_cols", "prior", "early_stopping"},

@@ -55,6 +55,8 @@ def dl_columns(model):
 
 
 def write_deeplearning(model, kv, blobs):
+    if getattr(getattr(model, "expander", None), "cat_hash", None):
+        raise NotImplementedError("DeepLearning with max_categorical_features hashing has no MOJO/POJO layout")
     ex = model.expander
     cfg = model._cfg
     info = model.info

