@@ -575,6 +575,12 @@ class GLMTrainer:
         path = []
         best = (float("inf"), None, None)
         null_dev = _gsum((w * fam.deviance(y, torch.full_like(y, ymu))).sum())
+        # early_stopping (GLM.java lambda loop): relative train-deviance improvements of the last 5 submodels;
+        # once past lambda_max with >= 5 IRLS iterations done, stop when none beats 1e-4, or (validation
+        # frame) when none improved the validation deviance
+        es = p.get("early_stopping", True) is not False
+        hist_tr, hist_va = [0.0] * 5, [0.0] * 5
+        old_tr, old_va, n_iter = null_dev, None, 0
         for li, lam in enumerate(lambdas):
             l1, l2 = lam * alpha, lam * (1 - alpha)
             if p.get("cold_start") and li > 0:     # cold_start: every lambda starts from the initial coefficients
@@ -608,6 +614,7 @@ class GLMTrainer:
                 nb = solve_penalized(Gm, r, l1, l2, intercept, beta, bool(p["non_negative"]), lb=lb, ub=ub)
                 diff = float((nb - beta).abs().max())
                 beta = nb
+                n_iter += 1
                 if self.job is not None:
                     self.job.check_cancelled()
                 if diff < beps:
@@ -635,6 +642,15 @@ class GLMTrainer:
                 score = _gsum((wvv[okv] * fam.deviance(yv.double()[okv], muv[okv])).sum())
             if valid is not None and len(lambdas) > 1 and score < best[0]:
                 best = (score, beta.clone(), lam)
+            k = (len(path) - 1) % 5
+            hist_tr[k] = (old_tr - dev_tr) / old_tr if old_tr else 0.0
+            old_tr = dev_tr
+            if valid is not None and len(lambdas) > 1:
+                hist_va[k] = (old_va - score) / old_va if old_va else 1.0
+                old_va = score
+            if es and len(lambdas) > 1 and lam < lmax and n_iter >= 5:
+                if max(hist_tr) < 1e-4 or (valid is not None and max(hist_va) < 0):
+                    break
         if best[1] is not None:
             return best[1], path, best[2]
         return beta, path, lambdas[-1]

@@ -86,8 +86,15 @@ def test_glm_families():
     assert m.output["training_metrics"]["mean_per_class_error"] < 0.1
     m = GLMTrainer(dict(family="ordinal", lambda_=0)).fit(X, yk, None, None, info3)
     assert m.output["training_metrics"]["mean_per_class_error"] < 0.2
-    m = GLMTrainer(dict(family="binomial", lambda_search=True, alpha=1.0, nlambdas=20)).fit(X, y, None, None, info)
+    m = GLMTrainer(dict(family="binomial", lambda_search=True, alpha=1.0, nlambdas=20,
+                        early_stopping=False)).fit(X, y, None, None, info)
     assert len(m.output["regularization_path"]["lambdas"]) == 20
+    # early_stopping (default): the path ends once 5 submodels in a row improve train deviance < 1e-4
+    me = GLMTrainer(dict(family="binomial", lambda_search=True, alpha=1.0, nlambdas=20)).fit(X, y, None, None, info)
+    lp = me.output["regularization_path"]
+    assert 5 <= len(lp["lambdas"]) < 20
+    de = lp["explained_deviance_train"]
+    assert max(b - a for a, b in zip(de[-6:-1], de[-5:])) < 1e-4 * 1.01
 
 
 def test_kmeans_and_estimate_k():
