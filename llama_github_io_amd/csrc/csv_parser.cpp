@@ -176,7 +176,12 @@ inline int split_record(const char* buf, int64_t a, int64_t b, char sep, char qu
 
 }  // namespace
 
+#include "abi.h"
+
 extern "C" {
+
+int h2o_abi_version() { return H2O_ABI_VERSION; }
+
 
 char h2o_csv_guess_sep(const char* buf, int64_t len) {
   const char cands[] = {',', '\t', ';', '|', ' '};

@@ -25,6 +25,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include "abi.h"
+
 #define NBIN 256
 #define AMAX_SHARDS 64  // per-block |aux| maxima shards (k_amax / k_gbm_step -> k_qscale)
 #define NA_BIN 255
@@ -1323,6 +1325,8 @@ static void launch_hist(dim3 grid, size_t lds, hipStream_t s, const void* bins, 
 }
 
 extern "C" {
+
+int h2o_abi_version() { return H2O_ABI_VERSION; }
 
 int h2o_tree_sizes(int* out) {
   out[7] = AMAX_SHARDS;

@@ -173,7 +173,10 @@ def _threshold_table(uniq, tp, fp, nb):
     if n == 0:
         return []
     P, Nn = float(tp[-1]), float(fp[-1])
-    idx = torch.linspace(0, n - 1, steps=min(n, nb), device=uniq.device).round().long().unique()
+    # float64 lattice: a float32 linspace rounds n - 1 up to n past 2^24 distinct scores (one element out of
+    # bounds: the HSA 0x1016 memory fault of the 100M-row XGBoost run)
+    idx = torch.linspace(0, n - 1, steps=min(n, nb), dtype=torch.float64, device=uniq.device).round().long().unique()
+    idx = idx.clamp_(0, n - 1)
     th = uniq[idx].cpu().numpy()
     tps = tp[idx].cpu().numpy(); fps = fp[idx].cpu().numpy()
     rows = []

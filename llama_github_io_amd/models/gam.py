@@ -266,7 +266,7 @@ class GAMTrainer:
                     kid = kid if isinstance(kid, (list, tuple)) else [kid]
                     ki = torch.as_tensor([int(v) for v in kid], device=dev)
                 else:
-                    ki = torch.unique(torch.round(torch.linspace(0, Xd.shape[0] - 1, kn, device=dev)).long())
+                    ki = torch.unique(torch.round(torch.linspace(0, Xd.shape[0] - 1, kn, dtype=torch.float64, device=dev)).long())
                     order = torch.argsort(Xd[:, 0], stable=True)
                     ki = order[ki]
                 K = Xd[ki]

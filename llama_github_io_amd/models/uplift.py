@@ -53,7 +53,7 @@ def auuc(uplift, y, treat, nbins=1000, auuc_type="AUTO"):
     yt = torch.cumsum(y * t, 0)
     yc = torch.cumsum(y * (1 - t), 0)
     N = y.numel()
-    idx = torch.linspace(0, N - 1, min(nbins, N), device=y.device).long()
+    idx = torch.linspace(0, N - 1, min(nbins, N), dtype=torch.float64, device=y.device).long().clamp_(0, N - 1)
     nt, nc, yt, yc = nt[idx], nc[idx], yt[idx], yc[idx]
     qini = yt - yc * nt / nc.clamp(min=1)
     lift = yt / nt.clamp(min=1) - yc / nc.clamp(min=1)

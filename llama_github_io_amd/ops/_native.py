@@ -54,6 +54,20 @@ _HIP_SIGS = {
 }
 
 
+# Bumped whenever a C launcher's argument list changes; every native library exports h2o_abi_version()
+# (csrc/abi.h) and a library built from older sources is refused instead of being called with shifted
+# arguments.
+ABI_VERSION = 3
+
+
+def _check_abi(lib, name: str) -> None:
+    fn = getattr(lib, "h2o_abi_version", None)
+    got = fn() if fn is not None else -1
+    if got != ABI_VERSION:
+        raise RuntimeError(f"{name}: native ABI version {got} != expected {ABI_VERSION}; rebuild with "
+                           "`python -m llama_github_io_amd.build_native --force`")
+
+
 def _bind(lib, sigs):
     for name, args in sigs.items():
         fn = getattr(lib, name, None)
@@ -77,10 +91,12 @@ def hip():
     if _hip is None:
         with _lock:
             if _hip is None:
-                path = build_native.HIP_LIB
-                if not os.path.exists(path) or os.environ.get("H2O_AMD_REBUILD"):
-                    build_native.build_hip()
-                _hip = _bind(ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL), _HIP_SIGS)
+                # build_hip() is a no-op when the library is newer than every source; a stale library
+                # (launcher signatures changed since it was built) is rebuilt instead of being loaded
+                path = build_native.build_hip(force=bool(os.environ.get("H2O_AMD_REBUILD")))
+                lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+                _check_abi(lib, "libh2o_hip")
+                _hip = _bind(lib, _HIP_SIGS)
     return _hip
 
 
@@ -90,10 +106,10 @@ def rt():
     if _rt is None:
         with _lock:
             if _rt is None:
-                path = build_native.RT_LIB
-                if not os.path.exists(path):
-                    build_native.build_rt()
-                _rt = ctypes.CDLL(path)
+                path = build_native.build_rt()
+                lib = ctypes.CDLL(path)
+                _check_abi(lib, "libh2o_rt")
+                _rt = lib
     return _rt
 
 

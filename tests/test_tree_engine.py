@@ -338,3 +338,42 @@ def test_gpu_tree_modes_match_reference(case):
         assert np.array_equal(dr["bin"], dg["bin"])
         np.testing.assert_allclose(dr["wl"], dg["wl"], rtol=1e-6)
     assert torch.equal(ref.leaf_of_row, gb.leaf_of_row.cpu())
+
+
+def _big_bins(N, F, stride, seed):
+    """[N, stride] uint8 bins: F random numeric features (some NA), zero padding after them."""
+    g = torch.Generator().manual_seed(seed)
+    bins = torch.zeros(N, stride, dtype=torch.uint8)
+    bins[:, :F] = torch.randint(0, 200, (N, F), generator=g, dtype=torch.uint8)
+    bins[: N // 50, 3] = T.NA_BIN
+    y = ((bins[:, 0].float() - 100) / 60 - (bins[:, 1] > 120).float() + torch.randn(N, generator=g) > 0).float()
+    return bins, y
+
+
+@pytest.mark.gpu
+def test_gpu_tree_bins_matrix_above_2pow31_bytes():
+    """The row payload of a >2^31-byte bins matrix (42M x 52 B = 2.18 GB, the stride of the 100M x 50
+    XGBoost config) is indexed in 64 bits by every kernel: unpacked (Newton) histograms, the moving and the
+    final route and the leaf bookkeeping match RefTreeBuilder decision for decision and row for row."""
+    N, F, stride = 42_000_000, 6, 52
+    assert N * stride > (1 << 31)
+    bins, y = _big_bins(N, F, stride, 3)
+    gr = -(y - 0.5)
+    h = torch.full_like(y, 0.25)
+    aux = torch.stack([h, -gr, -gr, h], 1).contiguous()
+    p = T.SplitParams(min_w=1.0, lam=1.0, mode=T.MODE_NEWTON)
+    nb = np.full(F, 200, np.int32)
+    ic = np.zeros(F, np.int32)
+    ref = T.RefTreeBuilder(bins, F, nb, ic, None, 4, p)
+    ref.build(aux, leaf_fn=lambda ls: (ls[:, 0] / (ls[:, 1] + 1.0)).float())
+    tl_r = ref.pop_levels()[0]
+    dev = torch.device("cuda", 0)
+    gb = T.GpuTreeBuilder(bins.to(dev), F, nb, ic, None, 4, p)
+    gb.build(aux.to(dev), leaf_fn=lambda ls: (ls[:, 0] / (ls[:, 1] + 1.0)).float())
+    tl_g = gb.pop_levels()[0]
+    assert tl_g.n_leaves == tl_r.n_leaves > 8
+    for dr, dg in zip(tl_r.decs, tl_g.decs):
+        assert np.array_equal(dr["feat"], dg["feat"]) and np.array_equal(dr["bin"], dg["bin"])
+        np.testing.assert_allclose(dr["wl"], dg["wl"], rtol=1e-9)
+    np.testing.assert_allclose(tl_r.leaf_values, tl_g.leaf_values, rtol=1e-5, atol=1e-7)
+    assert torch.equal(ref.leaf_of_row, gb.leaf_of_row.cpu())
