@@ -13,10 +13,19 @@ class H2OAutoML:
                  include_algos=None, exploitation_ratio=-1, modeling_plan=None, preprocessing=None,
                  monotone_constraints=None, keep_cross_validation_predictions=False, keep_cross_validation_models=False,
                  keep_cross_validation_fold_assignment=False, sort_metric="AUTO", export_checkpoints_dir=None,
-                 verbosity="warn", **kw):
-        self._aml = _aml.AutoML(project_name, max_models, max_runtime_secs, max_runtime_secs_per_model or 0, nfolds,
-                                seed, sort_metric, include_algos, exclude_algos, stopping_metric, stopping_rounds,
-                                stopping_tolerance)
+                 verbosity="warn"):
+        self._aml = _aml.AutoML(
+            project_name=project_name, max_models=max_models, max_runtime_secs=max_runtime_secs,
+            max_runtime_secs_per_model=max_runtime_secs_per_model or 0, nfolds=nfolds, seed=seed,
+            sort_metric=sort_metric, include_algos=include_algos, exclude_algos=exclude_algos,
+            stopping_metric=stopping_metric, stopping_rounds=stopping_rounds, stopping_tolerance=stopping_tolerance,
+            balance_classes=balance_classes, class_sampling_factors=class_sampling_factors,
+            max_after_balance_size=max_after_balance_size,
+            keep_cross_validation_predictions=keep_cross_validation_predictions,
+            keep_cross_validation_models=keep_cross_validation_models,
+            keep_cross_validation_fold_assignment=keep_cross_validation_fold_assignment, verbosity=verbosity,
+            exploitation_ratio=exploitation_ratio, modeling_plan=modeling_plan, preprocessing=preprocessing,
+            monotone_constraints=monotone_constraints, export_checkpoints_dir=export_checkpoints_dir)
         self.project_name = self._aml.project_name
 
     def train(self, x=None, y=None, training_frame=None, fold_column=None, weights_column=None, validation_frame=None,

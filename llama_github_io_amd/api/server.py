@@ -799,18 +799,36 @@ def create_app(client_disconnect_timeout: float | None = None):
             return v.get("name") if isinstance(v, dict) else _unquote(v)
         inc = bm.get("include_algos")
         exc = bm.get("exclude_algos")
+        mono = None
+        for ap in bm.get("algo_parameters") or []:       # AutoMLCustomParameters: [{scope, name, value}]
+            if isinstance(ap, dict) and ap.get("name") == "monotone_constraints":
+                v = ap.get("value")
+                mono = {d["key"]: d["value"] for d in v} if isinstance(v, list) else v
         aml = AutoML(project_name=bs.get("project_name"), max_models=sc.get("max_models"),
-                     max_runtime_secs=sc.get("max_runtime_secs") or None, nfolds=bs.get("nfolds", 5),
+                     max_runtime_secs=sc.get("max_runtime_secs") or None,
+                     max_runtime_secs_per_model=sc.get("max_runtime_secs_per_model") or 0, nfolds=bs.get("nfolds", 5),
                      seed=sc.get("seed"), include_algos=inc, exclude_algos=exc,
-                     sort_metric=spec.get("sort_metric") or "AUTO")
+                     sort_metric=spec.get("sort_metric") or "AUTO",
+                     stopping_metric=sc.get("stopping_metric") or "AUTO", stopping_rounds=sc.get("stopping_rounds", 3),
+                     stopping_tolerance=sc.get("stopping_tolerance"),
+                     balance_classes=bool(bs.get("balance_classes", False)),
+                     class_sampling_factors=bs.get("class_sampling_factors"),
+                     max_after_balance_size=bs.get("max_after_balance_size", 5.0),
+                     keep_cross_validation_predictions=bool(bs.get("keep_cross_validation_predictions", False)),
+                     keep_cross_validation_models=bool(bs.get("keep_cross_validation_models", False)),
+                     keep_cross_validation_fold_assignment=bool(bs.get("keep_cross_validation_fold_assignment", False)),
+                     export_checkpoints_dir=bs.get("export_checkpoints_dir"),
+                     exploitation_ratio=bm.get("exploitation_ratio", -1), modeling_plan=bm.get("modeling_plan"),
+                     preprocessing=bm.get("preprocessing"), monotone_constraints=mono)
         fr = dkv.get(name_of(spec["training_frame"]))
         y = name_of(spec.get("response_column"))
         ig = spec.get("ignored_columns") or []
         x = [n for n in fr.names if n not in ig and n != y] if ig else None
         vf = dkv.get(name_of(spec["validation_frame"])) if spec.get("validation_frame") else None
         lb = dkv.get(name_of(spec["leaderboard_frame"])) if spec.get("leaderboard_frame") else None
+        bf = dkv.get(name_of(spec["blending_frame"])) if spec.get("blending_frame") else None
         job = Job("AutoML", dest=aml.project_name)
-        job.run_async(aml.train, x, y, fr, vf, lb, None, None, None, job)
+        job.run_async(aml.train, x, y, fr, vf, lb, bf, spec.get("fold_column"), spec.get("weights_column"), job)
         return {"__meta": v3.meta("AutoMLBuilderV99", "AutoMLBuilder", 99), "job": v3.job(job),
                 "build_control": {"project_name": aml.project_name}, "automl_id": v3.key(aml.project_name, "Key<AutoML>")}
 

@@ -105,28 +105,133 @@ def default_stopping_tolerance(nrows: int) -> float:
     return min(0.05, max(0.001, 1.0 / math.sqrt(max(nrows, 1))))
 
 
+_ALGO_NAMES = {"gbm": "gbm", "drf": "drf", "xgboost": "xgboost", "glm": "glm", "deeplearning": "deeplearning",
+               "stackedensemble": "stackedensemble", "completion": "completion"}
+_EXPLOITATION = {"lr_annealing", "lr_search"}
+
+
+def _step_alias(sid: str, alias: str) -> bool:
+    """StepDefinition.Alias membership of a step id."""
+    alias = alias.lower()
+    if alias == "all":
+        return True
+    if alias == "defaults":
+        return sid.startswith("def_") or sid == "XRT" or sid.startswith("best_of_family") or sid.startswith("all")
+    if alias == "grids":
+        return sid.startswith("grid_") or sid == "resume_best_grids"
+    if alias in ("exploitation", "optionals"):
+        return sid in _EXPLOITATION
+    raise ValueError(f"unknown modeling step alias {alias!r}")
+
+
+def custom_plan(modeling_plan) -> list:
+    """``modeling_plan`` (AutoMLBuildSpec.AutoMLBuildModels.modeling_plan, h2o-py forms): a list of
+    ``"GBM"`` (every step of the algo), ``("GBM", "defaults"|"grids"|"exploitation"|"all")``,
+    ``("GBM", ["def_1", ("grid_1", group, weight), ...])`` or ``{"name": "GBM", "alias": ...}`` /
+    ``{"name": "GBM", "steps": [{"id": "def_1", "group": 2, "weight": 10}, ...]}``. Steps keep the
+    default group / weight of the TEN_LAYERED plan unless given, and run by (group, definition order)."""
+    catalog = _plan()
+    out = []
+
+    def add(algo, sid, group=None, weight=None):
+        for a, i, g, w in catalog:
+            if a == algo and i == sid:
+                out.append((a, i, g if group in (None, -1) else int(group), w if weight in (None, -1) else int(weight)))
+                return
+        raise ValueError(f"no modeling step {sid!r} for {algo}")
+
+    for item in modeling_plan:
+        if isinstance(item, dict):
+            algo = str(item.get("name", "")).lower()
+            alias, steps = item.get("alias"), item.get("steps")
+        elif isinstance(item, (list, tuple)):
+            algo = str(item[0]).lower()
+            alias, steps = (item[1], None) if len(item) > 1 and isinstance(item[1], str) else (None, item[1] if len(item) > 1 else None)
+        else:
+            algo, alias, steps = str(item).lower(), "all", None
+        if algo not in _ALGO_NAMES:
+            raise ValueError(f"modeling_plan: unknown algo {algo!r}")
+        if steps is None:
+            for a, i, g, w in catalog:
+                if a == algo and _step_alias(i, alias or "all"):
+                    out.append((a, i, g, w))
+            continue
+        for st in steps:
+            if isinstance(st, dict):
+                add(algo, st["id"], st.get("group"), st.get("weight"))
+            elif isinstance(st, (list, tuple)):
+                add(algo, *st)
+            else:
+                add(algo, str(st))
+    order = {id(st): i for i, st in enumerate(out)}
+    return sorted(out, key=lambda st: (st[2], order[id(st)]))
+
+
+def exploitation_weights(steps, ratio: float) -> list:
+    """AutoML.distributeExplorationVsExploitationWork: exploration weights stay, the exploitation steps'
+    weights are rescaled so they make up ``ratio`` of the total (0 removes them)."""
+    if ratio is None or ratio < 0:
+        return steps
+    if ratio > 1:
+        raise ValueError("`exploitation_ratio` must be between 0 and 1.")
+    expl = [st for st in steps if st[1] in _EXPLOITATION]
+    sum_x = sum(st[3] for st in steps if st[1] not in _EXPLOITATION and st[0] != "stackedensemble")
+    sum_e = sum(st[3] for st in expl)
+    if not expl or sum_e <= 0:
+        return steps
+    new_total = int(round(sum_x / (1.0 - ratio))) if ratio < 1 else sum_x + sum_e
+    new_e = new_total - sum_x
+    return [(a, i, g, int(round(w * new_e / sum_e)) if i in _EXPLOITATION else w) for a, i, g, w in steps]
+
+
 class AutoML:
     def __init__(self, project_name=None, max_models=None, max_runtime_secs=None, max_runtime_secs_per_model=0,
                  nfolds=5, seed=None, sort_metric="AUTO", include_algos=None, exclude_algos=None,
                  stopping_metric="AUTO", stopping_rounds=3, stopping_tolerance=None, balance_classes=False,
-                 keep_cross_validation_predictions=True, keep_cross_validation_models=False, verbosity="warn", **kw):
+                 class_sampling_factors=None, max_after_balance_size=5.0, keep_cross_validation_predictions=True,
+                 keep_cross_validation_models=False, keep_cross_validation_fold_assignment=False, verbosity="warn",
+                 exploitation_ratio=-1, modeling_plan=None, preprocessing=None, monotone_constraints=None,
+                 export_checkpoints_dir=None):
         self.project_name = project_name or dkv.new_key("AutoML")
         self.max_models = max_models
         self.max_runtime_secs = max_runtime_secs if max_runtime_secs is not None else (0 if max_models else 3600)
         self.per_model = max_runtime_secs_per_model or 0
         self.nfolds = nfolds
+        if nfolds not in (0, -1) and int(nfolds) == 1:
+            raise ValueError("nfolds set to 1; use nfolds >= 2 or 0 (no cross-validation)")
         self.seed = seed if seed not in (None, -1) else int(np.random.SeedSequence().entropy % (1 << 31))
         self.sort_metric = sort_metric
         self.include = [a.lower() for a in include_algos] if include_algos else None
         self.exclude = [a.lower() for a in exclude_algos] if exclude_algos else []
         self.stopping = dict(stopping_metric=stopping_metric, stopping_rounds=stopping_rounds,
                              stopping_tolerance=stopping_tolerance)
+        # AutoMLBuildControl: class balancing and CV artefact retention go to every model that has them
+        self.balance = dict(balance_classes=bool(balance_classes), class_sampling_factors=class_sampling_factors,
+                            max_after_balance_size=max_after_balance_size)
+        self.keep_cv = dict(keep_cross_validation_models=bool(keep_cross_validation_models),
+                            keep_cross_validation_fold_assignment=bool(keep_cross_validation_fold_assignment))
+        self.keep_cv_predictions = bool(keep_cross_validation_predictions)
+        self.exploitation_ratio = float(exploitation_ratio if exploitation_ratio is not None else -1)
+        if self.exploitation_ratio > 1:
+            raise ValueError("`exploitation_ratio` must be between 0 and 1.")
+        self.modeling_plan = custom_plan(modeling_plan) if modeling_plan else None
+        pre = []
+        for st in preprocessing or []:
+            t = st.get("type") if isinstance(st, dict) else st
+            t = str(t).lower().replace("_", "")
+            if t != "targetencoding":
+                raise ValueError(f"unknown preprocessing step {st!r} (supported: 'target_encoding')")
+            pre.append("target_encoding")
+        self.preprocessing = pre
+        # AutoMLCustomParameters: monotone_constraints is the one allowed custom algo parameter
+        self.algo_params = {"monotone_constraints": monotone_constraints} if monotone_constraints else {}
+        self.export_checkpoints_dir = export_checkpoints_dir
         self.models = []
         self.event_log = []
+        self.te_model = None
 
     def _allowed(self, algo):
-        name = {"gbm": "gbm", "drf": "drf", "xgboost": "xgboost", "glm": "glm", "deeplearning": "deeplearning",
-                "stackedensemble": "stackedensemble"}[algo]
+        name = _ALGO_NAMES[algo]
         if self.include is not None and name not in self.include:
             return False
         return name not in self.exclude
@@ -144,20 +249,30 @@ class AutoML:
         and SE steps (best-of-family / all, per group and for GBM-only and XGBoost+GLM subsets) close
         each group."""
         from .parallel import collectives as coll
+        from .models import params as P_
         t0 = time.time()
         nrows = training_frame.nrows
         tol = self.stopping["stopping_tolerance"]
         tol = default_stopping_tolerance(nrows) if tol in (None, -1, "AUTO") else float(tol)
-        common = dict(nfolds=self.nfolds if not fold_column else 0, fold_assignment="Modulo",
-                      keep_cross_validation_predictions=True, keep_cross_validation_models=False,
-                      fold_column=fold_column, weights_column=weights_column)
+        nfolds = int(self.nfolds) if self.nfolds not in (None, -1) else 5
+        if blending_frame is not None and self.nfolds in (None, -1):
+            nfolds = 0          # blending mode: the SEs stack predictions on the blending frame
+        common = dict(nfolds=nfolds if not fold_column else 0, fold_assignment="Modulo",
+                      keep_cross_validation_predictions=True, fold_column=fold_column, weights_column=weights_column,
+                      **self.keep_cv)
         if self.stopping["stopping_rounds"]:
             common.update(stopping_rounds=self.stopping["stopping_rounds"], stopping_metric=self.stopping["stopping_metric"],
                           stopping_tolerance=tol)
         self._log(f"stopping tolerance {tol:.6g} (adaptive on {nrows} rows)" if self.stopping["stopping_tolerance"] in
                   (None, -1, "AUTO") else f"stopping tolerance {tol} (user)")
         cat = self._category(training_frame, y)
-        steps = [st for st in _plan() if st[0] in ("completion", "stackedensemble") or self._allowed(st[0])]
+        self.blending_frame = blending_frame
+        if self.preprocessing:
+            training_frame, validation_frame, x, common = self._target_encoding(
+                training_frame, validation_frame, x, y, fold_column, weights_column, nfolds, common)
+        plan = self.modeling_plan if self.modeling_plan is not None else _plan()
+        steps = [st for st in plan if st[0] in ("completion", "stackedensemble") or self._allowed(st[0])]
+        steps = exploitation_weights(steps, self.exploitation_ratio)
         total_w = float(sum(st[3] for st in steps)) or 1.0
         used_w = 0.0
         rng = np.random.default_rng(self.seed)
@@ -170,13 +285,22 @@ class AutoML:
         def models_left():
             return (self.max_models - n_base()) if self.max_models else 1 << 30
 
-        def can_go():
-            return coll.agree(time_left() > 0 and models_left() > 0)
+        def can_go(ignore_count=False):
+            return coll.agree(time_left() > 0 and (ignore_count or models_left() > 0))
 
-        def run(algo, name, p, share):
-            if algo != "stackedensemble" and not can_go():
+        def algo_params(algo):
+            """build-control and custom parameters, for the algos whose schema has them"""
+            sch = P_.schema(algo) or {}
+            extra = {}
+            if cat in ("Binomial", "Multinomial") and self.balance["balance_classes"]:
+                extra.update({k: v for k, v in self.balance.items() if k in sch and v is not None})
+            extra.update({k: v for k, v in self.algo_params.items() if k in sch})
+            return extra
+
+        def run(algo, name, p, share, exploit=False):
+            if algo != "stackedensemble" and not can_go(exploit and self.exploitation_ratio > 0):
                 return None
-            p = dict(p, **common)
+            p = dict(p, **common, **algo_params(algo))
             if self.per_model:
                 p["max_runtime_secs"] = self.per_model
             elif self.max_runtime_secs > 0:
@@ -184,8 +308,7 @@ class AutoML:
             mid = f"{name}_AutoML_{self.project_name}"
             try:
                 m = builder.train(algo, p, x, y, training_frame, validation_frame, job, mid)
-                self.models.append(m)
-                self._log(f"built {mid}")
+                self._register(m, mid)
                 return m
             except Exception as e:  # noqa: BLE001 - AutoML logs and moves on (EventLog)
                 self._log(f"{mid} failed: {e!r}")
@@ -196,6 +319,8 @@ class AutoML:
         for algo, sid, group, w in steps:
             share = (time_left() * w / max(total_w - used_w, 1e-9)) if self.max_runtime_secs > 0 else float("inf")
             used_w += w
+            if w <= 0:             # ModelingStep.canRun: no work allocated (e.g. exploitation_ratio=0)
+                continue
             if algo == "stackedensemble":
                 # SEs do not count against the budget: they close every group that trained base models
                 # (and the final group always runs)
@@ -203,7 +328,7 @@ class AutoML:
                         and (group <= last_group or group == 10)):
                     self._se_step(sid, x, y, training_frame, validation_frame, job)
                 continue
-            if not can_go():
+            if not can_go(sid in _EXPLOITATION and self.exploitation_ratio > 0):
                 continue
             n_before = len(self.models)
             fam = dict(gbm="GBM", xgboost="XGBoost", glm="GLM", drf="DRF", deeplearning="DeepLearning").get(algo, algo)
@@ -221,22 +346,84 @@ class AutoML:
                 best = self._best_of(["gbm"])
                 if best is not None:
                     p = {k: v for k, v in best.params.items() if k in _defaults("gbm", "def_1", self.seed, cat)}
-                    run("gbm", "GBM_lr_annealing_selection_model_1", dict(p, learn_rate_annealing=0.99), share)
+                    run("gbm", "GBM_lr_annealing_selection_model_1", dict(p, learn_rate_annealing=0.99), share, exploit=True)
             elif sid == "lr_search":
                 best = self._best_of(["xgboost"])
                 if best is not None:
                     base = {k: v for k, v in best.params.items() if k in _defaults("xgboost", "def_1", self.seed, cat)}
                     sti = int(base.get("score_tree_interval") or 5)
                     for j, lr in enumerate((0.5, 0.2, 0.1, 0.05, 0.02, 0.01, 0.005, 0.002, 0.001, 0.0005)):
-                        if not can_go():
+                        if not can_go(self.exploitation_ratio > 0):
                             break
                         run("xgboost", f"XGBoost_lr_search_selection_model_{j + 1}",
-                            dict(base, learn_rate=lr, score_tree_interval=(j + 1) * sti), share / 10)
+                            dict(base, learn_rate=lr, score_tree_interval=(j + 1) * sti), share / 10, exploit=True)
             if len(self.models) > n_before:
                 last_group = group
         self.leaderboard_frame = leaderboard_frame
+        if not self.keep_cv_predictions:
+            # the holdout predictions were kept for the SEs only (AutoML keep_cross_validation_predictions=False)
+            for m in self.models:
+                fid = m.output.pop("cross_validation_holdout_predictions_frame_id", None) if isinstance(m.output, dict) else None
+                if fid:
+                    dkv.remove(fid)
         dkv.put(self.project_name, self)
         return self
+
+    def _register(self, m, mid):
+        if self.te_model is not None and m.algo != "stackedensemble":
+            m.preprocessors = [self.te_model]       # predict / score raw frames through the TE preprocessor
+            m.output["preprocessors"] = [self.te_model.key]
+        self.models.append(m)
+        self._log(f"built {mid}")
+        if self.export_checkpoints_dir:
+            import os
+            from .persist import save_model
+            os.makedirs(self.export_checkpoints_dir, exist_ok=True)
+            save_model(m, self.export_checkpoints_dir, force=True)
+
+    def _target_encoding(self, fr, valid, x, y, fold_column, weights_column, nfolds, common):
+        """preprocessing=["target_encoding"] (ai/h2o/automl/preprocessing/TargetEncoding.java): encode the
+        categorical predictors with cardinality >= 25 whose rows-per-level exceed the blending inflection
+        point (5); with CV the encoder uses KFold leakage handling on the user fold column or a Modulo fold
+        column ``<y>_te_fold``, which the models then train on (nfolds=0). Models keep the encoder as a
+        preprocessor, so predictions on raw frames are encoded the same way."""
+        from .frame import Column
+        from .models import builder as B  # noqa: N812
+        names = list(x) if x is not None else [n for n in fr.names if n not in (y, fold_column, weights_column)]
+        te_cols = []
+        for n in names:
+            if fr.type(n) == "enum":
+                card = len(fr._col(n).domain or [])
+                if card >= 25 and fr.nrows / max(card, 1) > 5:
+                    te_cols.append(n)
+        if not te_cols:
+            self._log("target_encoding: no categorical column qualifies (cardinality >= 25)")
+            return fr, valid, x, common
+        tp = dict(blending=True, inflection_point=5, smoothing=10, noise=0.0, keep_original_categorical_columns=False,
+                  seed=self.seed)
+        train = fr
+        fcol = fold_column
+        if common.get("nfolds", 0) > 1 or fold_column:
+            tp["data_leakage_handling"] = "KFold"
+            if not fcol:
+                fcol = f"{y}_te_fold"
+                import torch
+                from .frame import engine_device
+                n = fr.nrows
+                folds = torch.arange(n, dtype=torch.float64, device=engine_device()) % nfolds   # Modulo
+                train = fr.cbind(type(fr)._from_columns([Column(fcol, "int", folds)]))
+            tp["fold_column"] = fcol
+        self.te_model = B.train("targetencoder", tp, te_cols + ([fcol] if fcol else []), y, train, None, None,
+                                f"TargetEncoding_AutoML_{self.project_name}")
+        self._log(f"target_encoding: encoded {te_cols} (experimental in the reference: no MOJO for these models)")
+        enc = self.te_model.transform(train, as_training=True)
+        x2 = [n for n in names if n not in te_cols] + [n for n in enc.names if n.endswith("_te")]
+        common = dict(common)
+        if fcol:
+            common.update(fold_column=fcol, nfolds=0)
+        v2 = self.te_model.transform(valid) if valid is not None else None
+        return enc, v2, x2, common
+
 
     @staticmethod
     def _category(fr, y):
@@ -306,7 +493,9 @@ class AutoML:
         20. A SE is only built when its base set differs from every SE built before."""
         cat = self.models[0].model_category
         metric = self._sort_key(cat)
-        base = [m for m in self.models if m.algo != "stackedensemble" and getattr(m, "cv_holdout", None) is not None]
+        blend = getattr(self, "blending_frame", None)
+        base = [m for m in self.models if m.algo != "stackedensemble" and
+                (blend is not None or getattr(m, "cv_holdout", None) is not None)]
         if sid.endswith("_gbm"):
             base = [m for m in base if m.algo == "gbm"]
         elif sid.endswith("_xglm"):
@@ -339,13 +528,15 @@ class AutoML:
         try:
             # StackedEnsembleStepsProvider.setMetalearnerParameters: the metalearner is cross-validated
             # with the AutoML nfolds, and its out-of-fold metrics are what the leaderboard ranks
-            sp = dict(base_models=[m.key for m in ms], seed=self.seed, metalearner_nfolds=self.nfolds,
-                      metalearner_fold_assignment="Modulo", keep_levelone_frame=True)
+            sp = dict(base_models=[m.key for m in ms], seed=self.seed, keep_levelone_frame=True)
+            if blend is not None:
+                sp["blending_frame"] = blend
+            else:
+                sp.update(metalearner_nfolds=self.nfolds, metalearner_fold_assignment="Modulo")
             if cat in ("Binomial", "Multinomial"):
                 sp["metalearner_transform"] = "Logit"
             se = builder.train("stackedensemble", sp, x, y, fr, valid, job, mid)
-            self.models.append(se)
-            self._log(f"built {mid}")
+            self._register(se, mid)
         except Exception as e:  # noqa: BLE001
             self._log(f"{mid} failed: {e!r}")
 

@@ -3,11 +3,14 @@
 //
 // One pass over the rows does both halves of the Lloyd step as matrix products on the matrix cores:
 //
-//  1. distance GEMM   S[row][c] = ||c||^2 - 2 x.c  (v_mfma_f32_16x16x4_f32, exact f32 fma chains)
-//     A = 16 rows x 4 dims of X, B = 4 dims x 16 centers (Cᵀ, held in registers for the whole
-//     launch). The 16x16 result leaves center c = lane&15 and rows 4*(lane>>4)+r in the lane's 4
-//     accumulator registers, so the argmin over centers is a 4-step butterfly inside each 16-lane
-//     group (ties -> smaller center index, like the reference's strict '<' scan).
+//  1. distance GEMM   S[c][row] = ||c||^2 - 2 c.x  (v_mfma_f32_16x16x4_f32, exact f32 fma chains)
+//     A = 16 centers x 4 dims of C (registers for the whole launch), B = 4 dims x 16 rows of Xᵀ
+//     (LDS). The 16x16 result leaves row = lane&15 and centers 4*(lane>>4)+r in the lane's 4
+//     accumulator registers: the argmin over centers is 4 in-lane compares plus two cross-lane steps
+//     (xor 16, xor 32), ties -> smaller center index like the reference's strict '<' scan. The same
+//     B-operand values give ||x||^2 (partial sums per lane, the same two steps).
+//     MEASURED (r3): the former orientation (D[row][center]) needed a 4-step butterfly per row and 8
+//     broadcasts per 4 rows: ~80 ds_bpermute per 16 rows, which made the kernel LDS-pipe bound.
 //  2. centroid GEMM   T[c][d] += sum_rows onehot(assign)[c][row] * w * X[row][d]
 //     A = 16 centers x 4 rows (the one-hot of the rows' argmins, built from the step-1 registers by
 //     lane shuffles), B = 4 rows x 16 dims of X (coalesced 64-byte row segments); a constant-1
@@ -53,22 +56,26 @@ __global__ __launch_bounds__(256) void k_lloyd_mfma(const float* __restrict__ X,
   const int64_t n_waves = (int64_t)gridDim.x * 4;
   const int ps = (P + 3) >> 2;
 
-  // centers as the B operand of the distance MFMA: cb[t][s] = C[t*16 + c16][4s + q]
-  float cb[KT][PS];
-  float csq[KT];
+  // centers as the A operand of the distance MFMA: ca[t][s] = C[t*16 + c16][4s + q];
+  // csq[t][r] = ||C[t*16 + 4q + r]||^2 for the D layout (FLT_MAX for padding centers)
+  float ca[KT][PS];
+  float csq[KT][4];
 #pragma unroll
   for (int t = 0; t < KT; ++t) {
     const int c = t * 16 + c16;
-    float s2 = 0.f;
 #pragma unroll
     for (int s = 0; s < PS; ++s) {
       const int d = 4 * s + q;
-      cb[t][s] = (c < K && d < P) ? C[(int64_t)c * P + d] : 0.f;
+      ca[t][s] = (c < K && d < P) ? C[(int64_t)c * P + d] : 0.f;
     }
-    if (c < K) {
-      for (int d = 0; d < P; ++d) { const float v = C[(int64_t)c * P + d]; s2 = fmaf(v, v, s2); }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int cr = t * 16 + 4 * q + r;
+      float s2 = 0.f;
+      if (cr < K)
+        for (int d = 0; d < P; ++d) { const float v = C[(int64_t)cr * P + d]; s2 = fmaf(v, v, s2); }
+      csq[t][r] = cr < K ? s2 : FLT_MAX;
     }
-    csq[t] = (c < K) ? s2 : FLT_MAX;
   }
 
   f32x4 acc[KT][PT];
@@ -77,93 +84,105 @@ __global__ __launch_bounds__(256) void k_lloyd_mfma(const float* __restrict__ X,
 #pragma unroll
     for (int u = 0; u < PT; ++u) acc[t][u] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  const bool vec4 = (P & 3) == 0;
+  // P % 4 == 0 (the host pads the design matrix): the lane's float4 groups e4 = lane + 64 i, i < PS
+  // (64 P / 4 <= 64 PS), are loaded with one dwordx4 each
+  float* wsl = lds + (size_t)4 * KM_ROWS * Pp + wv * KM_ROWS;   // per-wave row weights of the tile
+  // Software pipeline: the NEXT tile's rows (and weights) are loaded into registers while the current
+  // tile is computed from LDS. MEASURED (r2): the former load -> wait -> LDS-write loop per 64-row tile
+  // exposed one HBM round trip per float4 group (781 us per Lloyd step on 10M x 20 = ~1 TB/s).
+  float4 pf[PS];
+  float pwt = 0.f;
+  auto issue = [&](int64_t rs) {
+    const int nr = (int)((N - rs) < KM_ROWS ? (N - rs) : KM_ROWS);
+    const int nel = nr * P;
+    const float4* s4 = reinterpret_cast<const float4*>(X + rs * P);
+#pragma unroll
+    for (int i = 0; i < PS; ++i) {
+      const int e4 = lane + 64 * i;
+      pf[i] = 4 * e4 < nel ? s4[e4] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    pwt = lane < nr ? (w ? w[rs + lane] : 1.f) : 0.f;
+  };
+  // LDS destinations of the lane's groups are the same for every tile: computed once (no per-tile
+  // integer division by the runtime P); the 4 elements of a group share a row
+  int doff[PS];
+#pragma unroll
+  for (int i = 0; i < PS; ++i) {
+    const int e = 4 * (lane + 64 * i);
+    const int r = e / P, c = e - r * P;
+    doff[i] = e < KM_ROWS * P ? r * Pp + c : -1;
+  }
+  if (wave_g * KM_ROWS < N) issue(wave_g * KM_ROWS);
   for (int64_t r0 = wave_g * KM_ROWS; r0 < N; r0 += n_waves * KM_ROWS) {
     const int nrows = (int)((N - r0) < KM_ROWS ? (N - r0) : KM_ROWS);
-    const int nel = nrows * P;
-    const float* src = X + r0 * P;
-    // ---- stage 64 rows into this wave's LDS slice (row stride P+1), zero the tail rows
-    if (vec4) {
-      const float4* s4 = reinterpret_cast<const float4*>(src);
-      for (int e4 = lane; e4 < (KM_ROWS * P) / 4; e4 += 64) {
-        const int e = e4 * 4;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (e < nel) v = s4[e4];
-        const int r = e / P, c = e - r * P;       // P % 4 == 0: the 4 elements share a row
-        float* dst = xs + r * Pp + c;
-        dst[0] = v.x; dst[1] = v.y; dst[2] = v.z; dst[3] = v.w;
-      }
-    } else {
-      for (int e = lane; e < KM_ROWS * P; e += 64) {
-        const int r = e / P, c = e - r * P;
-        xs[r * Pp + c] = e < nel ? src[e] : 0.f;
+    // ---- the prefetched tile -> this wave's LDS slice (row stride P+1; tail rows are zeros)
+#pragma unroll
+    for (int i = 0; i < PS; ++i) {
+      if (doff[i] >= 0) {
+        float* dst = xs + doff[i];
+        dst[0] = pf[i].x; dst[1] = pf[i].y; dst[2] = pf[i].z; dst[3] = pf[i].w;
       }
     }
-    __builtin_amdgcn_s_waitcnt(0);   // wave-private slice: the wave's own LDS writes are visible after this
+    wsl[lane] = pwt;
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the wave's own LDS writes (vmcnt untouched)
     __builtin_amdgcn_wave_barrier();
+    {
+      const int64_t nx = r0 + n_waves * KM_ROWS;
+      if (nx < N) issue(nx);                 // next tile's loads stay in flight during the compute below
+    }
 #pragma unroll
     for (int tr = 0; tr < KM_ROWS / 16; ++tr) {
       const float* xt = xs + tr * 16 * Pp;
-      // ---- 1. distance GEMM: A[i = row c16][k = dim 4s+q]
+      // ---- 1. distance GEMM: B[k = dim 4s+q][j = row c16]; the same values give ||x||^2
       f32x4 d[KT];
 #pragma unroll
       for (int t = 0; t < KT; ++t) d[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      float xq = 0.f;
 #pragma unroll
       for (int s = 0; s < PS; ++s) {
         if (s < ps) {
-          const int dd = 4 * s + q;
-          const float a = dd < P ? xt[c16 * Pp + dd] : 0.f;
+          const float xb = xt[c16 * Pp + 4 * s + q];      // P % 4 == 0: always a real (or padding-zero) dim
+          xq = fmaf(xb, xb, xq);
 #pragma unroll
-          for (int t = 0; t < KT; ++t) d[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, cb[t][s], d[t], 0, 0, 0);
+          for (int t = 0; t < KT; ++t) d[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(ca[t][s], xb, d[t], 0, 0, 0);
         }
       }
-      float best[4];
-      int bidx[4];
+      float best = FLT_MAX;
+      int bidx = 0x7fffffff;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        best[r] = FLT_MAX;
-        bidx[r] = 0x7fffffff;
+      for (int t = 0; t < KT; ++t)
 #pragma unroll
-        for (int t = 0; t < KT; ++t) {
-          const float sc = csq[t] - 2.f * d[t][r];
-          const int ci = t * 16 + c16;
-          if (ci < K && (sc < best[r] || (sc == best[r] && ci < bidx[r]))) { best[r] = sc; bidx[r] = ci; }
+        for (int r = 0; r < 4; ++r) {
+          const float sc = csq[t][r] - 2.f * d[t][r];
+          const int ci = t * 16 + 4 * q + r;              // increasing: strict '<' keeps the smaller index
+          if (sc < best) { best = sc; bidx = ci; }
         }
-#pragma unroll
-        for (int m = 1; m < 16; m <<= 1) best[r] = bfly_min_idx(best[r], bidx[r], m);
+      best = bfly_min_idx(best, bidx, 16);
+      best = bfly_min_idx(best, bidx, 32);
+      xq += __shfl_xor(xq, 16, 64);
+      xq += __shfl_xor(xq, 32, 64);
+      const int rrow = tr * 16 + c16;                      // every lane of column c16 holds row rrow's result
+      if (q == 0 && rrow < nrows) {
+        assign[r0 + rrow] = bidx;
+        mind[r0 + rrow] = fmaxf(xq + best, 0.f);
       }
-      // ---- 2. centroid GEMM over the 16 rows in 4 steps of 4 rows (k = row 4j + q of the tile)
+      // ---- 2. centroid GEMM over the 16 rows in 4 steps of 4 rows: A[i = center][k = row 4j+q] (one-hot),
+      // B[k = row 4j+q][j = dim]; the constant-1 column at dim P accumulates the weighted counts
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int a0 = __shfl(bidx[0], j * 16, 64), a1 = __shfl(bidx[1], j * 16, 64);
-        const int a2 = __shfl(bidx[2], j * 16, 64), a3 = __shfl(bidx[3], j * 16, 64);
-        const float b0 = __shfl(best[0], j * 16, 64), b1 = __shfl(best[1], j * 16, 64);
-        const float b2 = __shfl(best[2], j * 16, 64), b3 = __shfl(best[3], j * 16, 64);
-        const int my_a = q == 0 ? a0 : (q == 1 ? a1 : (q == 2 ? a2 : a3));
-        const float my_b = q == 0 ? b0 : (q == 1 ? b1 : (q == 2 ? b2 : b3));
-        const int rt = tr * 16 + 4 * j + q;          // row within the 64-row slice
-        const int64_t rb = r0 + rt;
-        const bool rok = rt < nrows;
-        const float ww = rok ? (w ? w[rb] : 1.f) : 0.f;
+        const int rt = tr * 16 + 4 * j + q;                // row within the 64-row slice (zero-weight tail rows)
+        const int my_a = __shfl(bidx, 4 * j + q, 64);
+        const float ww = wsl[rt];
         const float* xr = xs + rt * Pp;
-        float xq = 0.f;
 #pragma unroll
         for (int u = 0; u < PT; ++u) {
           const int dd = u * 16 + c16;
-          const float xv = dd < P ? xr[dd] : 0.f;
-          xq = fmaf(xv, xv, xq);
-          const float bv = dd < P ? ww * xv : (dd == P ? ww : 0.f);
+          const float bv = dd < P ? ww * xr[dd] : (dd == P ? ww : 0.f);
 #pragma unroll
           for (int t = 0; t < KT; ++t) {
             const float av = (my_a == t * 16 + c16) ? 1.f : 0.f;
             acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[t][u], 0, 0, 0);
           }
-        }
-#pragma unroll
-        for (int m = 1; m < 16; m <<= 1) xq += __shfl_xor(xq, m, 64);
-        if (rok && c16 == 0) {
-          assign[rb] = my_a;
-          mind[rb] = fmaxf(xq + my_b, 0.f);
         }
       }
     }
@@ -182,7 +201,7 @@ __global__ __launch_bounds__(256) void k_lloyd_mfma(const float* __restrict__ X,
 template <int KT, int PS, int PT>
 int launch(const float* X, long long N, int P, const float* C, int K, const float* w, int* assign, float* mind,
            float* slabs, int grid, hipStream_t s) {
-  const size_t lds = (size_t)4 * KM_ROWS * (P + 1) * sizeof(float);
+  const size_t lds = (size_t)4 * KM_ROWS * (P + 2) * sizeof(float);   // 4 wave slices + 4 x 64 weights
   hipLaunchKernelGGL((k_lloyd_mfma<KT, PS, PT>), dim3(grid), dim3(256), lds, s, X, (int64_t)N, P, C, K, w, assign,
                      mind, slabs);
   return (int)hipGetLastError();
@@ -207,7 +226,7 @@ int h2o_kmeans_mfma_shape(int K, int P, int* out) {
 int h2o_kmeans_mfma(const float* X, long long N, int P, const float* C, int K, const float* w, int* assign,
                     float* mind, float* slabs, int grid, hipStream_t s) {
   int sh[3];
-  if (!h2o_kmeans_mfma_shape(K, P, sh) || N <= 0 || grid <= 0) return (int)hipErrorInvalidValue;
+  if (!h2o_kmeans_mfma_shape(K, P, sh) || N <= 0 || grid <= 0 || (P & 3)) return (int)hipErrorInvalidValue;
   const int KT = sh[0], PS = sh[1], PT = sh[2];
 #define L(kt, ps, pt) if (KT == kt && PS == ps && PT == pt) return launch<kt, ps, pt>(X, N, P, C, K, w, assign, mind, slabs, grid, s)
   L(1, 4, 1); L(1, 4, 2); L(1, 8, 2); L(1, 8, 3); L(1, 16, 3); L(1, 16, 4); L(1, 16, 5);

@@ -254,21 +254,43 @@ def multinomial_auc(y, probs, w):
     return float(np.mean(aucs)) if aucs else float("nan")
 
 
-@_sharded_rows("X", "assign", "w")
-def clustering_metrics(X, centers, assign, w=None) -> ModelMetrics:
-    """X [N, F] (standardised space), centers [K, F], assign [N]."""
-    X = X.double(); C = centers.double()
-    w = _w(w, X.shape[0], X.device)
-    d = ((X - C[assign]) ** 2).sum(1)
-    K = C.shape[0]
+def clustering_metrics(X, centers, assign, w=None, chunk: int = 1 << 20) -> ModelMetrics:
+    """X [N, F] (standardised space), centers [K, F], assign [N].
+
+    fp64 sums over row chunks (no [N, F] fp64 temporaries); row-sharded frames merge per-rank partial
+    sums (sizes, within-SS, column sums, then total SS about the global mean) with all-reduces instead of
+    gathering rows (``hex/ModelMetricsClustering.java`` IndependentMetricBuilder.reduce)."""
     from .ops.segment import segment_sum
-    within = segment_sum(assign, w * d, K)
-    size = segment_sum(assign, w, K)
-    mu = (w[:, None] * X).sum(0) / w.sum()
-    totss = float((w * ((X - mu) ** 2).sum(1)).sum())
+    from .parallel import collectives as coll
+    C = centers.double().to(X.device)
+    K, N = C.shape[0], X.shape[0]
+    w = _w(w, N, X.device)
+    within = torch.zeros(K, dtype=torch.float64, device=X.device)
+    size = torch.zeros(K, dtype=torch.float64, device=X.device)
+    sx = torch.zeros(X.shape[1] + 1, dtype=torch.float64, device=X.device)
+    for i in range(0, N, chunk):
+        xb, ab, wb = X[i:i + chunk].double(), assign[i:i + chunk].long(), w[i:i + chunk]
+        d = ((xb - C[ab]) ** 2).sum(1)
+        within += segment_sum(ab, wb * d, K)
+        size += segment_sum(ab, wb, K)
+        sx[:-1] += (wb[:, None] * xb).sum(0)
+        sx[-1] += wb.sum()
+    dist = coll.is_dist()
+    if dist:
+        for t in (within, size, sx):
+            coll.all_reduce_(t)
+    mu = sx[:-1] / sx[-1]
+    totss = torch.zeros(1, dtype=torch.float64, device=X.device)
+    for i in range(0, N, chunk):
+        xb, wb = X[i:i + chunk].double(), w[i:i + chunk]
+        totss += (wb * ((xb - mu) ** 2).sum(1)).sum()
+    if dist:
+        coll.all_reduce_(totss)
+    totss = float(totss)
     tw = float(within.sum())
+    n = int(coll.all_reduce_scalar(N)) if dist else N
     return ModelMetrics(model_category="Clustering", tot_withinss=tw, totss=totss, betweenss=totss - tw,
-                        withinss=within.cpu().tolist(), size=size.cpu().tolist(), nobs=int(X.shape[0]))
+                        withinss=within.cpu().tolist(), size=size.cpu().tolist(), nobs=n)
 
 
 @_sharded_rows("score", "w")

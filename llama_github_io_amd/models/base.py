@@ -186,7 +186,10 @@ class Model:
         return P
 
     def _adapt(self, frame):
-        """Replay the training frame's categorical encoding / interaction columns (models/adapt.py)."""
+        """Replay the model's preprocessors (AutoML target encoding: ``Model.Parameters._preprocessors``),
+        then the training frame's categorical encoding / interaction columns (models/adapt.py)."""
+        for pp in getattr(self, "preprocessors", None) or []:
+            frame = pp.transform(frame)
         ad = getattr(self, "adapter", None)
         return ad.apply(frame) if ad else frame
 
@@ -327,6 +330,10 @@ class Model:
         ad = getattr(self, "adapter", None)
         if ad:
             st["adapter"] = ad.to_state()
+        pps = getattr(self, "preprocessors", None)
+        if pps:
+            st["preprocessors"] = [pp.to_state() | {"__class__": type(pp).__module__ + ":" + type(pp).__name__}
+                                   for pp in pps]
         return st
 
     def _restore(self, state):
@@ -337,6 +344,9 @@ class Model:
         if state.get("calibration"):
             from ..persist import _from_state
             self.calibration_model = _from_state(dict(state["calibration"]))
+        if state.get("preprocessors"):
+            from ..persist import _from_state
+            self.preprocessors = [_from_state(dict(pp)) for pp in state["preprocessors"]]
 
     def __repr__(self):
         return f"<{type(self).__name__} key={self.key} category={self.model_category}>"

@@ -78,7 +78,9 @@ def prepare(algo: str, params: dict, x=None, y=None, training_frame=None):
     fr = training_frame
     y = _resolve_names(fr, y)
     y = y[0] if y else None
-    special = {params.get("weights_column"), params.get("offset_column"), params.get("fold_column"), y}
+    # the target encoder reads its fold column as data (KFold leakage handling), it does no CV of its own
+    special = {params.get("weights_column"), params.get("offset_column"),
+               params.get("fold_column") if algo != "targetencoder" else None, y}
     special.discard(None)
     ignored = set(_resolve_names(fr, params.get("ignored_columns")) or [])
     if x is None:
@@ -281,7 +283,7 @@ def _train(spec, algo, p, x, y, fr, validation_frame, job, model_id):
     t0 = time.time()
     nfolds = int(p.get("nfolds") or 0)
     cv_out = None
-    if nfolds > 1 or (info.fold and info.fold in fr.names):
+    if algo != "targetencoder" and (nfolds > 1 or (info.fold and info.fold in fr.names)):
         cv_out = _cross_validate(spec, p, fr, info, X, yv, w, off, seed, mid, job)
     tp = {k: v for k, v in p.items() if k not in COMMON}
     if cv_out is not None and int(p.get("stopping_rounds") or 0) > 0:

@@ -40,7 +40,7 @@ DL_DEFAULTS = dict(hidden=[200, 200], epochs=10.0, activation="Rectifier", adapt
                    score_training_samples=10000, seed=-1, shuffle_training_data=True, reproducible=False,
                    export_weights_and_biases=False, missing_values_handling="MeanImputation", max_runtime_secs=0.0,
                    compute_dtype="float32", gpu_batch_size=256, train_samples_per_iteration=-2,
-                   overwrite_with_best_model=True)
+                   overwrite_with_best_model=True, classification_stop=0.0, regression_stop=1e-6)
 
 
 class MLP(torch.nn.Module):
@@ -565,6 +565,18 @@ class DeepLearningTrainer:
         s_in = S_ep
         owb = bool(p.get("overwrite_with_best_model", True)) and not int(p.get("nfolds") or 0)
         best_loss, best_p, last_ev = float("inf"), None, {}
+        # train_samples_per_iteration (DeepLearning.computeTrainSamplesPerIteration): scoring / stopping is
+        # decided at the end of each iteration of tspi samples. 0 and -1 (no replicated data): one epoch;
+        # -2 (auto): the reference's caps of its hardware-timed estimate, min(epochs * N / 10, 100k x nodes)
+        tspi = int(p.get("train_samples_per_iteration", -2))
+        if tspi in (0, -1):
+            tspi = N_glob
+        elif tspi == -2:
+            tspi = int(max(1, min(epochs * N_glob / 10, 100000 * coll.world())))
+        elif tspi < -2:
+            raise ValueError("train_samples_per_iteration must be -2, -1, 0 or > 0")
+        model.output["actual_train_samples_per_iteration"] = tspi
+        n_iter_done = 0
         step = 0
         spe = max(1, N_glob // B)
         t_loop0 = time.time()
@@ -623,12 +635,15 @@ class DeepLearningTrainer:
             if self.job is not None and (step // 50) != ((last + 1) // 50):
                 self.job.set_progress(last / max(total, 1))
             end = last == total - 1
-            timed = time.time() - last_score > float(p["score_interval"])
+            it_end = samples // tspi > n_iter_done          # an iteration of tspi samples completed
+            first_it = it_end and n_iter_done == 0
+            if it_end:
+                n_iter_done = samples // tspi
+            timed = it_end and time.time() - last_score > float(p["score_interval"])
             if sharded:                          # every rank must take the same scoring decision
-                timed = coll.agree(timed) if step % 16 == 0 else False
-            epoch_mark = keeper.k > 0 and any(st > 0 and st % spe == 0 for st in range(step, last + 1))
+                timed = coll.agree(timed)
             step = last + 1
-            if end or timed or epoch_mark:
+            if end or timed or first_it:
                 last_score = time.time()
                 ev = self._score(model, X, y, w, samples / N_glob, valid)
                 t_scoring += time.time() - last_score
@@ -640,6 +655,9 @@ class DeepLearningTrainer:
                         best_loss, best_p = lv, fp.p.detach().clone()
                 mref = ev.get("_valid") or ev.get("_train")
                 if mref is not None and not end and keeper.add(mref):
+                    break
+                if not end and not ae and self._accuracy_reached(ev.get("_train"), cat):
+                    model.output["stopped_early"] = "achieved requested predictive accuracy on the training data"
                     break
                 if float(p["max_runtime_secs"] or 0) > 0 and coll.agree(time.time() - t0 > float(p["max_runtime_secs"])):
                     break
@@ -784,6 +802,26 @@ class DeepLearningTrainer:
             r = float(p["tweedie_power"])
             return (w * (-t * torch.exp((1 - r) * f) / (1 - r) + torch.exp((2 - r) * f) / (2 - r))).sum()
         return 0.5 * (w * (f - t) ** 2).sum()
+
+    def _accuracy_reached(self, m, cat) -> bool:
+        """DeepLearningModel.doScoring: stop once the training classification error <= classification_stop
+        (classifiers) or the training MSE <= regression_stop (regression); -1 disables either."""
+        if m is None:
+            return False
+        p = self.p
+        if cat in ("Binomial", "Multinomial"):
+            cs = float(p.get("classification_stop", 0.0))
+            if cs < 0:
+                return False
+            tab = (m.get("cm") or {}).get("table")
+            if not tab:
+                return False
+            t = np.asarray(tab, dtype=np.float64)
+            tot = t.sum()
+            err = (tot - np.trace(t)) / tot if tot > 0 else 1.0
+            return err <= cs
+        rs = float(p.get("regression_stop", 1e-6))
+        return rs >= 0 and m.get("MSE") is not None and float(m["MSE"]) <= rs
 
     def _ae_metrics(self, model, X):
         out, Z = model._forward(X)

@@ -117,12 +117,25 @@ class KMeansTrainer:
         if how == "user" and self.p.get("user_points") is not None:
             up = self.p["user_points"]
             U = up.as_tensor() if hasattr(up, "as_tensor") else torch.as_tensor(np.asarray(up, dtype=np.float32))
-            return self.ex.transform(U.T.contiguous().to(dev)) if U.shape[1] == self.info.F else U.to(dev).float()
+            U = self.ex_train.transform(U.T.contiguous().to(dev)) if U.shape[1] == self.info.F else U.to(dev).float()
+            if U.shape[1] < Z.shape[1]:
+                U = torch.nn.functional.pad(U, (0, Z.shape[1] - U.shape[1]))
+            if self.ex_train is not self.ex and U.shape[1] != self.info.F:   # user points given in design space
+                U = U - torch.nn.functional.pad(self._shift, (0, Z.shape[1] - self._shift.numel())).float()
+            return U
         first = int(rng.integers(N))
         C = self._row(Z, first)
         if how == "random":
             idx = rng.choice(N, size=min(k, N), replace=False)
+            if not coll.is_dist():
+                return Z.index_select(0, torch.as_tensor(idx, dtype=torch.long, device=dev)).clone()
             return torch.cat([self._row(Z, int(j)) for j in idx], 0)
+        if not coll.is_dist() and Z.is_cuda:
+            state = rng.bit_generator.state
+            Cd = self._init_device(Z, C, k, rng, how)
+            if Cd is not None:
+                return Cd
+            rng.bit_generator.state = state
         while C.shape[0] < k:
             _, d = kmeans_assign(Z, C)
             if how == "plusplus":
@@ -144,6 +157,27 @@ class KMeansTrainer:
             else:  # furthest
                 j = self._argmax(d)
             C = torch.cat([C, self._row(Z, j)], 0)
+        return C
+
+    def _init_device(self, Z, C, k, rng, how):
+        """Furthest / PlusPlus seeding with every choice made on the device (no host sync per center).
+        PlusPlus draws the same uniforms as the host loop; if some step had no distance mass left (the
+        host loop stops early there) the result is discarded and the host loop runs instead."""
+        dev = Z.device
+        masses = []
+        while C.shape[0] < k:
+            _, d = kmeans_assign(Z, C)
+            if how == "plusplus":
+                pr = d.double().clamp(min=0)
+                s = pr.sum()
+                masses.append(s)
+                u = float(rng.random()) * s
+                j = torch.searchsorted(torch.cumsum(pr, 0), u.view(1)).clamp_(max=Z.shape[0] - 1)
+            else:
+                j = torch.argmax(d).view(1)            # first maximum, as _argmax
+            C = torch.cat([C, Z.index_select(0, j)], 0)
+        if masses and bool((torch.stack(masses) <= 0).any()):
+            return None
         return C
 
     @staticmethod
@@ -187,34 +221,75 @@ class KMeansTrainer:
         d = ((Z.double() - C.double()[a]) ** 2).sum(1).float()
         return C, a, d, it + 1
 
+    def _step(self, Z, w, C):
+        """One Lloyd step on the device: (assign, min distance, new centers, cnt, flags [#empty, shift])."""
+        a, d, sums, cnt = kmeans_step(Z, C, w)
+        if coll.is_dist():
+            sums = coll.all_reduce_(sums)
+            cnt = coll.all_reduce_(cnt)
+        newC = torch.where(cnt[:, None] > 0, sums / cnt.clamp(min=1e-300)[:, None], C.double()).float()
+        flags = torch.stack([(cnt == 0).sum().double(), (newC - C).abs().max().double()])
+        return a, d, newC, cnt, flags
+
+    def _reseed(self, Z, newC, cnt, d):
+        """Empty clusters are re-seeded, in cluster order, at the currently worst-fit row (KMeans.java)."""
+        for e in torch.nonzero(cnt == 0).flatten().tolist():
+            j = self._argmax(d)
+            newC[e] = self._row(Z, j)[0]
+            if 0 <= j - self.row0 < d.numel():
+                d[j - self.row0] = 0
+        return newC
+
     def _lloyd(self, Z, w, C, max_it):
         csc = self.p.get("cluster_size_constraints")
         if csc:
             if coll.is_dist():
                 raise ValueError("cluster_size_constraints needs a single-process frame")
             return self._lloyd_constrained(Z, w, C, max_it, [int(v) for v in csc])
-        K = C.shape[0]
-        dev = Z.device
-        for it in range(max_it):
-            a, d, sums, cnt = kmeans_step(Z, C, w)
-            if coll.is_dist():
-                sums = coll.all_reduce_(sums)
-                cnt = coll.all_reduce_(cnt)
-            newC = torch.where(cnt[:, None] > 0, sums / cnt.clamp(min=1e-300)[:, None], C.double()).float()
-            empty = torch.nonzero(cnt == 0).flatten().tolist()
-            for e in empty:   # re-seed empty clusters at the worst-fit row
-                j = self._argmax(d)
-                newC[e] = self._row(Z, j)[0]
-                if 0 <= j - self.row0 < d.numel():
-                    d[j - self.row0] = 0
-            shift = float((newC - C).abs().max())
+        tol = 1e-6
+        if not Z.is_cuda or coll.is_dist():
+            it = 0
+            for it in range(max_it):
+                a, d, newC, cnt, flags = self._step(Z, w, C)
+                n_empty, shift = flags.tolist()          # one host sync per iteration
+                if n_empty > 0:
+                    newC = self._reseed(Z, newC, cnt, d)
+                    shift = float((newC - C).abs().max())
+                C = newC
+                if self.job is not None:
+                    self.job.check_cancelled()
+                if shift < tol:
+                    break
+            a, d = kmeans_assign(Z, C)
+            return C, a, d, it + 1
+        # single device: no blocking host sync inside the loop. Iteration i's flags travel to pinned host
+        # memory while iteration i+1 is already queued on the speculation that i re-seeded nothing and did
+        # not converge; a (rare) re-seed discards the speculative step, convergence discards it unused.
+        # Same iterates and iteration count as the synchronous loop.
+        pinned = torch.empty(2, dtype=torch.float64, pin_memory=True)
+        ev = torch.cuda.Event()
+        it = 0
+        cur = self._step(Z, w, C)
+        while True:
+            a, d, newC, cnt, flags = cur
+            pinned.copy_(flags, non_blocking=True)
+            ev.record()
+            nxt = self._step(Z, w, newC) if it + 1 < max_it else None
+            ev.synchronize()
+            n_empty, shift = float(pinned[0]), float(pinned[1])
+            if n_empty > 0:
+                newC = self._reseed(Z, newC, cnt, d)
+                shift = float((newC - C).abs().max())
+                nxt = None
+            it += 1
             C = newC
             if self.job is not None:
                 self.job.check_cancelled()
-            if shift < 1e-6:
+            if shift < tol or it >= max_it:
                 break
+            cur = nxt if nxt is not None else self._step(Z, w, C)
         a, d = kmeans_assign(Z, C)
-        return C, a, d, it + 1
+        return C, a, d, it
 
     def fit(self, X, y, w, offset, info: DataInfo, valid=None, model_key=None):
         from .shared_tree import resolve_seed
@@ -229,7 +304,22 @@ class KMeansTrainer:
         self.row0, self.N_glob = (coll.exclusive_offset(N) if coll.is_dist() else (0, N))
         self.ex = Expander(info, standardize=p["standardize"], use_all_factor_levels=True).fit(
             X, w, reduce=coll.all_reduce_ if coll.is_dist() else None)
-        Z = self.ex.transform(X)
+        # Training runs in a translated space: without standardisation the numeric columns are still centred
+        # (k-means is translation invariant) so the MFMA distance GEMM ||c||^2 - 2 x.c does not cancel on
+        # data with large column offsets; centers move back by `shift` at the end.
+        import copy
+        self.ex_train = self.ex
+        shift = None
+        if not self.ex.standardize and self.ex.nums:
+            self.ex_train = copy.copy(self.ex)
+            self.ex_train.center_only = True
+            shift = torch.zeros(self.ex.P, dtype=torch.float64, device=dev)
+            shift[self.ex.num_off:] = self.ex.num_mean.to(dev).double()
+        self._shift = shift
+        Z = self.ex_train.transform(X)
+        P0 = Z.shape[1]
+        if Z.is_cuda and P0 % 4 and P0 <= 64:      # the MFMA Lloyd kernel streams rows as float4 groups
+            Z = torch.nn.functional.pad(Z, (0, 4 - P0 % 4))
         how = str(p["init"]).lower().replace("_", "")
         max_it = int(p["max_iterations"])
         if p["estimate_k"]:
@@ -257,6 +347,16 @@ class KMeansTrainer:
         else:
             C0 = self._init_centers(Z, int(p["k"]), rng, how)
             C, a, d, iters = self._lloyd(Z, w, C0, max_it)
+        met = mm.clustering_metrics(Z, C, a, w)           # translation invariant: the training space is fine
+        if valid is not None:
+            Zv = self.ex_train.transform(valid[0])
+            if Zv.shape[1] < Z.shape[1]:
+                Zv = torch.nn.functional.pad(Zv, (0, Z.shape[1] - Zv.shape[1]))
+            av, _ = kmeans_assign(Zv, C)
+            vmet = mm.clustering_metrics(Zv, C, av)
+        C = C[:, :P0]
+        if shift is not None:
+            C = (C.double() + shift[None, :]).float()
         model = KMeansModel(model_key or make_key("kmeans"), p, info)
         model.device = dev
         model.expander = self.ex
@@ -270,12 +370,8 @@ class KMeansTrainer:
         model.output["center_names"] = self.ex.names
         model.output["k"] = C.shape[0]
         model.output["iterations"] = iters
-        met = mm.clustering_metrics(Z, C, a, w)
         model.output["training_metrics"] = met
         if valid is not None:
-            Xv = valid[0]
-            Zv = self.ex.transform(Xv)
-            av, _ = kmeans_assign(Zv, C)
-            model.output["validation_metrics"] = mm.clustering_metrics(Zv, C, av)
+            model.output["validation_metrics"] = vmet
         model.output["run_time_ms"] = int((time.time() - t0) * 1000)
         return model

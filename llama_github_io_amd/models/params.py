@@ -23,12 +23,11 @@ HINTS = {
     "replicate_training_data", "col_major", "diagnostics", "fast_mode", "score_duty_cycle",
     "target_ratio_comm_to_comp", "parallelize_cross_validation", "nparallelism", "multinode_mode", "dmatrix_type",
     "save_matrix_directory", "check_constant_response", "reproducible", "pca_impl", "response_column",
-    "auto_rebalance", "export_weights_and_biases", "verbose", "r2_stopping", "score_eval_metric_only",
+    "auto_rebalance", "export_weights_and_biases", "verbose", "score_eval_metric_only",
     "max_confusion_matrix_size", "save_transformed_framekeys", "store_knot_locations", "generate_scoring_history",
-    "score_iteration_interval", "classification_stop", "regression_stop", "train_samples_per_iteration",
-    "score_validation_sampling", "u_name", "loading_name", "build_glm_model",
+    "score_iteration_interval", "score_validation_sampling", "u_name", "loading_name", "build_glm_model",
     "compute_metrics", "num_iteration_without_new_exemplar",
-    "tree_method", "eval_metric", "export_checkpoints_dir", "gradient_epsilon", "svd_method",
+    "eval_metric", "export_checkpoints_dir", "gradient_epsilon", "svd_method",
     # DeepLearning: elastic averaging blends per-node local models into the global one between map/reduce
     # rounds; with synchronous data parallelism every rank holds the global model after each step, so it
     # is the identity here. ``sparse`` is a storage hint for sparse input.
@@ -48,6 +47,12 @@ UNSUPPORTED = {
     "word2vec": {"word_model"},
     "rulefit": {"max_categorical_levels"},
     "infogram": {"max_iterations"},
+}
+
+# parameters the reference accepts but no longer honours: a non-default value warns like the reference
+DEPRECATED = {
+    "r2_stopping": "_r2_stopping is no longer supported - please use stopping_rounds, stopping_metric and "
+                   "stopping_tolerance instead.",     # hex/tree/SharedTree.java:160
 }
 
 # values that count as "left at its default" whatever the schema says
@@ -90,6 +95,10 @@ def validate(algo: str, params: dict, extra_allowed=()) -> None:
     unknown = sorted(k for k in params if k not in allowed and not k.startswith("_"))
     if unknown:
         raise ValueError(f"{algo}: unknown parameter(s) {unknown}")
+    for k, msg in DEPRECATED.items():
+        if k in params and not _is_default(params[k], sch.get(k)) and params[k] != float("inf"):
+            import warnings
+            warnings.warn(msg, UserWarning, stacklevel=3)
     bad = sorted(k for k in UNSUPPORTED.get(algo, ()) if k in params and not _is_default(params[k], sch.get(k)))
     if bad:
         raise ValueError(f"{algo}: parameter(s) {bad} are not supported by this engine (leave them at their defaults)")

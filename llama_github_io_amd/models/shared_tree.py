@@ -133,6 +133,13 @@ class SharedTreeTrainer:
         self.p = p
 
     # ---- hooks
+    def _binning_sample(self) -> int:
+        """Rows of the quantile-edge sample (fit_binning); subclasses needing exact edges raise it."""
+        return 1 << 20
+
+    def _check_binning(self, b) -> None:
+        """Hook: refuse a binning that cannot express the requested split semantics."""
+
     def _split_params(self) -> T.SplitParams:
         sp = T.SplitParams(min_w=float(self.p["min_rows"]), min_split_improvement=float(self.p["min_split_improvement"]),
                            mode=self.mode)
@@ -188,18 +195,20 @@ class SharedTreeTrainer:
         max_bins = int(min(255, max(int(p.get("max_bins") or 255), 2)))
         if str(p.get("histogram_type", "AUTO")).lower() in ("uniformadaptive", "random", "roundrobin", "uniformrobust"):
             max_bins = int(min(255, max(p.get("nbins_top_level", 1024), p.get("nbins", 20))))
+        bsample = self._binning_sample()
         if coll.is_dist():
             # every rank must bin identically, and exactly like the single-process run: the quantile
             # sample is drawn on GLOBAL row indices (fit_binning's own rule), each rank contributes the
             # sampled rows it owns, and the edges come from the gathered sample
             n_glob = coll.exclusive_offset(N)[1]
-            Xl = sample_rows(X, 1 << 20, self.seed, self.row0, n_glob)
+            Xl = sample_rows(X, bsample, self.seed, self.row0, n_glob)
             Xs = coll.all_gather_cat(Xl.contiguous(), dim=1)
             self.binning = fit_binning(Xs, info.iscat, info.nlevels, max_bins=max_bins, seed=self.seed,
                                        max_cat_bins=int(p.get("nbins_cats") or 1024), presampled=True)
         else:
             self.binning = fit_binning(X, info.iscat, info.nlevels, max_bins=max_bins, seed=self.seed,
-                                       max_cat_bins=int(p.get("nbins_cats") or 1024))
+                                       max_cat_bins=int(p.get("nbins_cats") or 1024), sample=bsample)
+        self._check_binning(self.binning)
         bins = apply_binning(self.binning, X)
         mono = None
         if p.get("monotone_constraints"):

@@ -86,8 +86,9 @@ class StackedEnsembleTrainer:
         self.job = None
 
     def fit(self, X, y, w, offset, info: DataInfo, valid=None, model_key=None):
-        from .builder import REGISTRY
+        from .builder import REGISTRY  # noqa: F401
         from .base import model_category
+        self._train_y, self._train_w = y, w
         keys = []
         for b in self.p["base_models"]:
             if isinstance(b, str):
@@ -110,6 +111,24 @@ class StackedEnsembleTrainer:
             raise ValueError("StackedEnsemble needs base_models")
         cat = model_category(info)
         from ..parallel import collectives as coll, dframe
+        blend = self.p.get("blending_frame")
+        if blend is not None:
+            # blending mode (StackedEnsemble.java StackedEnsembleBlendingDriver): the level-one frame is the
+            # base models' predictions on the blending frame, whose response trains the metalearner; the base
+            # models need no cross-validation
+            if isinstance(blend, str):
+                blend = dkv.get(blend)
+            if blend is None or not hasattr(blend, "model_matrix"):
+                raise ValueError("blending_frame must be a frame (or a frame key)")
+            cols_ = []
+            for m in models:
+                fr = m._adapt(blend)
+                Xb, ob = fr.model_matrix(m.info, device=X.device)
+                cols_.append(_level_one([m], Xb, ob, cat))
+            L1 = torch.cat(cols_, 0).contiguous()
+            y = blend.response_tensor(info, device=X.device)
+            w = blend.weights_tensor(info, device=X.device)
+            return self._finish(models, L1, y, w, X, info, cat, valid, model_key, ytrain=(X, None, None, offset))
         holds = []
         for m in models:
             h = getattr(m, "cv_holdout", None)
@@ -125,6 +144,12 @@ class StackedEnsembleTrainer:
             else:
                 holds.append(h.reshape(-1, 1).float())
         L1 = torch.cat(holds, 1).T.contiguous().to(X.device)
+        return self._finish(models, L1, y, w, X, info, cat, valid, model_key, ytrain=(X, y, w, offset))
+
+    def _finish(self, models, L1, y, w, X, info, cat, valid, model_key, ytrain):
+        """Metalearner on the level-one frame L1 [F', N] with response y / weights w; the ensemble's
+        training metrics are scored on the training frame ``ytrain = (X, y, w, offset)``."""
+        from ..parallel import dframe
         transform = str(self.p.get("metalearner_transform") or "NONE").lower()
         if transform == "logit":
             if cat not in ("Binomial", "Multinomial"):
@@ -184,6 +209,11 @@ class StackedEnsembleTrainer:
         model.output["base_models"] = model.base_keys
         model.output["metalearner"] = meta.key
         model.output["metalearner_transform"] = transform
+        Xt, yt_, wt_, offset = ytrain
+        if yt_ is None:                      # blending: the SE's training metrics are on the training frame
+            yt_, wt_ = self._train_y, self._train_w
+        y, w = yt_, wt_
+        model.output["stacking_strategy"] = "blending" if self.p.get("blending_frame") is not None else "cross_validation"
         nst = int(self.p.get("score_training_samples") or 0)
         if 0 < nst < X.shape[1]:      # score_training_samples: training metrics on a fixed row sample
             from .shared_tree import resolve_seed

@@ -159,10 +159,12 @@ class TargetEncoderTrainer:
         prior = (Y * wt[:, None]).sum(0) / wt.sum()
         fold = None
         if str(p["data_leakage_handling"]).lower().replace("_", "") == "kfold":
-            if not p.get("fold_column") or p["fold_column"] not in info.x:
+            fc = p.get("fold_column") or info.fold       # the builder hands the fold column over in DataInfo
+            if not fc or fc not in info.x:
                 raise ValueError("k_fold leakage handling needs fold_column")
-            fold = torch.nan_to_num(X[info.x.index(p["fold_column"])]).long()
-            cats = [j for j in cats if info.x[j] != p["fold_column"]]
+            p["fold_column"] = fc
+            fold = torch.nan_to_num(X[info.x.index(fc)]).long()
+            cats = [j for j in cats if info.x[j] != fc]
         stats = {}
         for j in cats:
             L = len(info.domains[j])

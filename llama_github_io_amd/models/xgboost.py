@@ -129,8 +129,35 @@ class XGBoostTrainer(SharedTreeTrainer):
         self.K = len(info.response_domain) if d == "multinomial" else 1
         if str(self.p.get("booster")).lower() == "gblinear":
             return self._fit_linear(X, y, w, offset, info, valid, model_key)
-        self.p["max_bins"] = min(int(self.p.get("max_bins", 256)), 255)
+        tm = str(self.p.get("tree_method") or "auto").lower()
+        if tm not in ("auto", "exact", "approx", "hist"):
+            raise ValueError(f"tree_method must be one of auto, exact, approx, hist; got {tm!r}")
+        self.tree_method = tm
+        # hist / approx / auto: histogram splits on global quantile bins (approx's per-tree sketch is the
+        # same cut set up to resampling); exact: every distinct value of every numeric column is a split
+        # candidate, i.e. one bin per distinct value of the WHOLE column
+        self.p["max_bins"] = 255 if tm == "exact" else min(int(self.p.get("max_bins", 256)), 255)
         return super().fit(X, y, w, offset, info, valid, model_key)
+
+    def _binning_sample(self):
+        if getattr(self, "tree_method", "auto") == "exact":
+            return 1 << 62           # edges from every row, not a sample
+        return super()._binning_sample()
+
+    def _check_binning(self, b):
+        if getattr(self, "tree_method", "auto") != "exact":
+            return
+        # exact greedy splits are the histogram splits when no bin merges two distinct values: at most 254
+        # distinct values per numeric column (bin 255 is NA) on this engine
+        Xn = self.X
+        for f in range(b.F):
+            if b.iscat[f]:
+                continue
+            col = Xn[f][~torch.isnan(Xn[f])]
+            nd = int(torch.unique(col).numel()) if col.numel() else 0
+            if nd > 254:
+                raise ValueError(f"tree_method='exact': column {self.info.x[f]!r} has {nd} distinct values; the "
+                                 "exact split search of this engine handles at most 254 per column (use 'hist')")
 
     def _trees_per_iter(self):
         return self.K

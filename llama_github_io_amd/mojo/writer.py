@@ -133,6 +133,10 @@ def _mojo_files(model, prefix: str = "") -> dict:
 
 
 def write_mojo(model, path: str) -> str:
+    if getattr(model, "preprocessors", None):
+        # the reference refuses these too (ai/h2o/automl/preprocessing/TargetEncoding.java: "models obtained
+        # with this feature can not yet be downloaded as MOJO")
+        raise ValueError(f"model {model.key} has preprocessors (AutoML target encoding): no MOJO export")
     files = _mojo_files(model)
     os.makedirs(os.path.dirname(os.path.abspath(path)) or ".", exist_ok=True)
     with zipfile.ZipFile(path, "w", zipfile.ZIP_DEFLATED) as z:

@@ -219,10 +219,11 @@ def _mfma_shape(K, P):
 def kmeans_step(X: torch.Tensor, C: torch.Tensor, w: torch.Tensor | None = None):
     """One Lloyd step: (assign [N], min sq. distance [N], per-center weighted sums [K, P] fp64, counts [K]).
     On the GPU: ``csrc/kmeans_mfma.hip`` (distance GEMM + argmin + one-hot centroid GEMM on f32 MFMA,
-    one pass over X) for K, P <= 64; the LDS scalar kernel beyond that."""
+    one pass over X) for K, P <= 64 with P % 4 == 0 (KMeans pads its design matrix); the LDS scalar
+    kernel otherwise."""
     N, P = X.shape
     K = C.shape[0]
-    sh = _mfma_shape(K, P) if X.is_cuda and N > 0 else None
+    sh = _mfma_shape(K, P) if X.is_cuda and N > 0 and P % 4 == 0 else None
     if sh is not None and os.environ.get("H2O_KMEANS_MFMA", "1") == "1":
         KT, PS, PT = sh
         X = X.contiguous().float()

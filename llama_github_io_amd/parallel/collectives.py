@@ -236,6 +236,21 @@ def barrier():
         dist.barrier()
 
 
+def abort_world(reason: str) -> None:
+    """Abort the process group: the peers' pending and future collectives fail fast instead of waiting for
+    a rank that will never join (a one-sided error inside a sharded build). The job then fails on every rank."""
+    from ..utils import log
+    log.get().error(f"aborting the process group: {reason}")
+    try:
+        from torch.distributed.distributed_c10d import _abort_process_group
+        _abort_process_group()
+    except Exception:  # noqa: BLE001 - older torch: tearing the group down has the same effect on peers
+        try:
+            dist.destroy_process_group()
+        except Exception:  # noqa: BLE001
+            pass
+
+
 def check_same(value, what: str = "value"):
     """Raise on every rank if ``value`` (picklable) differs between ranks (SPMD divergence guard)."""
     if not world_active():

@@ -98,7 +98,27 @@ def pressure_check() -> int:
 def with_backpressure(fn, *args, **kwargs):
     """Run ``fn``; on a device out-of-memory error spill cold frames down to half of HBM, release the
     caching allocator's blocks and retry once (the reference blocks allocations until the Cleaner
-    freed memory; here the retry happens after the spill)."""
+    freed memory; here the retry happens after the spill).
+
+    Row-sharded builds run collectives inside ``fn``, so one rank cannot retry alone (its peers would wait
+    in a collective it never joins). There the spill decision is collective (every rank cleans when any
+    rank is over its high water mark), and an OOM on any rank aborts the process group: every rank fails
+    with the error instead of hanging."""
+    from ..parallel import collectives as coll
+    if coll.is_dist():
+        over = 0.0
+        if torch.cuda.is_available():
+            u = device_usage()
+            over = 1.0 if u["total"] and u["used"] / u["total"] > _state["high_water"] else 0.0
+        if coll.all_reduce_scalar(over, op=torch.distributed.ReduceOp.MAX) > 0:
+            clean()
+        try:
+            return fn(*args, **kwargs)
+        except torch.cuda.OutOfMemoryError as e:
+            _state["oom_aborts"] = _state.get("oom_aborts", 0) + 1
+            coll.abort_world(f"device out of memory on rank {coll.rank()}: {e}")
+            raise RuntimeError(f"device out of memory on rank {coll.rank()}: the sharded build was aborted on "
+                               "every rank (it cannot be retried on one rank alone)") from e
     try:
         return fn(*args, **kwargs)
     except torch.cuda.OutOfMemoryError:

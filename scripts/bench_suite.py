@@ -152,6 +152,30 @@ def bench_glm(a, dev, world, rank):
                higher_is_better=False, auc=m.auc(), n_gpus=world))
 
 
+def bench_glm_big(a, dev, world, rank):
+    """GLM binomial IRLSM on a 10M x 50 device matrix (the MFMA Gram / X'v / Z.beta kernels at scale)."""
+    from llama_github_io_amd.models.base import DataInfo
+    from llama_github_io_amd.models.glm import GLMTrainer
+    N = a.rows or 10_000_000
+    F = a.cols or 50
+    n = N // world
+    g = torch.Generator(device=dev).manual_seed(5 + rank)
+    X = torch.randn(F, n, device=dev, generator=g)
+    beta = torch.linspace(-1, 1, F, device=dev)
+    y = (torch.rand(n, device=dev, generator=g) < torch.sigmoid((beta[:, None] * X).sum(0) * 0.3)).float()
+    info = DataInfo([f"x{i}" for i in range(F)], np.zeros(F, np.int32), [None] * F, "y", ["0", "1"])
+    prm = dict(family="binomial", solver="IRLSM", lambda_=0.0, standardize=True)
+    GLMTrainer(dict(prm, max_iterations=1)).fit(X[:, :100000].contiguous(), y[:100000].contiguous(), None, None, info)
+    _sync()
+    t0 = time.perf_counter()
+    m = GLMTrainer(prm).fit(X, y, None, None, info)
+    _sync()
+    dt = time.perf_counter() - t0
+    _emit(dict(metric="GLM binomial IRLSM 10M x 50 (seconds)", value=dt, unit="s", higher_is_better=False,
+               iterations=m.output.get("iterations"), auc=m.output["training_metrics"].get("AUC"), rows=N, cols=F,
+               n_gpus=world))
+
+
 def bench_kmeans(a, dev, world, rank):
     from llama_github_io_amd.models.base import DataInfo
     from llama_github_io_amd.models.kmeans import KMeansTrainer
@@ -161,18 +185,25 @@ def bench_kmeans(a, dev, world, rank):
     g = torch.Generator(device=dev).manual_seed(3 + rank)
     X = torch.randn(F, n, device=dev, generator=g)
     info = DataInfo([f"x{i}" for i in range(F)], np.zeros(F, np.int32), [None] * F, None, None)
-    _sync()
-    t0 = time.perf_counter()
-    KMeansTrainer(dict(k=10, max_iterations=10, init="Random", seed=1, standardize=False)).fit(X, None, None, None, info)
-    _sync()
-    dt = time.perf_counter() - t0
+    KMeansTrainer(dict(k=10, max_iterations=2, init="Random", seed=1, standardize=False)).fit(X, None, None, None, info)
+    times, iters = {}, {}
+    for it in (10, 30):
+        _sync()
+        t0 = time.perf_counter()
+        m = KMeansTrainer(dict(k=10, max_iterations=it, init="Random", seed=1, standardize=False)).fit(X, None, None, None, info)
+        _sync()
+        times[it] = time.perf_counter() - t0
+        iters[it] = m.output["iterations"]
+    dt = times[10]
+    per_iter = (times[30] - times[10]) / max(iters[30] - iters[10], 1)
     _emit(dict(metric="KMeans k=10, 10 Lloyd iterations, rows/sec", value=N * 10 / dt, unit="rows/s", n_gpus=world,
-               seconds=dt, rows=N, cols=F))
+               seconds=dt, rows=N, cols=F, lloyd_ms_per_iteration_end_to_end=round(per_iter * 1e3, 3),
+               iterations=iters, fixed_seconds=round(dt - iters[10] * per_iter, 4)))
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--which", default="xgb", choices=["xgb", "dl", "glm", "kmeans", "automl"])
+    ap.add_argument("--which", default="xgb", choices=["xgb", "dl", "glm", "glm_big", "kmeans", "automl"])
     ap.add_argument("--budget", type=float, default=240.0, help="AutoML max_runtime_secs")
     ap.add_argument("--rows", type=int, default=0)
     ap.add_argument("--cols", type=int, default=0)
@@ -188,7 +219,7 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
-    dict(xgb=bench_xgb, dl=bench_dl, glm=bench_glm, kmeans=bench_kmeans, automl=bench_automl)[a.which](a, dev, world, rank)
+    dict(xgb=bench_xgb, dl=bench_dl, glm=bench_glm, glm_big=bench_glm_big, kmeans=bench_kmeans, automl=bench_automl)[a.which](a, dev, world, rank)
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()

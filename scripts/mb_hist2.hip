@@ -84,13 +84,129 @@ float run(const unsigned* b, const float* v, int N, int F, unsigned long long* o
   hipEventCreate(&a); hipEventCreate(&e);
   size_t lds = (MODE == 0 || MODE == 4 || MODE == 2 || MODE == 6) ? HPLANE * 8 : (HPLANE / 2 + 8) * 8;
   lds += lds_kb_extra * 1024;
+  hipMemset(out, 0, 8);
   hipLaunchKernelGGL((kern<MODE, BLK>), dim3(grid), dim3(BLK), lds, 0, b, v, N, F, out);
   hipError_t rc = hipDeviceSynchronize();
+  unsigned long long chk = 0;
+  hipMemcpy(&chk, out, 8, hipMemcpyDeviceToHost);
+  printf("[mode %d checksum %llx] ", MODE, chk);
   if (rc != hipSuccess) { printf("launch failed: %s\n", hipGetErrorString(rc)); exit(1); }
   float best = 1e9;
   for (int r = 0; r < 7; ++r) {
     hipEventRecord(a);
     hipLaunchKernelGGL((kern<MODE, BLK>), dim3(grid), dim3(BLK), lds, 0, b, v, N, F, out);
+    hipEventRecord(e);
+    hipEventSynchronize(e);
+    float ms; hipEventElapsedTime(&ms, a, e);
+    if (ms < best) best = ms;
+  }
+  return best;
+}
+
+
+// 2 lanes per row: each lane loads 16 B (half a row: 16 features) with one dwordx4; the wave covers 32 rows
+// per load. MODE 7: instruction i adds feature 16h + 4(i>>2) + ((i+R)&3) (uniform word, rotated byte:
+// 2-way bank conflict); MODE 8: feature 16h + ((i+R)&15) (conflict-free, per-lane word select);
+// MODE 9: loads only.
+template <int MODE, int BLK>
+__global__ __launch_bounds__(BLK) void kern2(const uint4* __restrict__ bins, const float* __restrict__ val,
+                                             int N, int F, unsigned long long* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long sm[];
+  constexpr int RPI = BLK / 2;
+  for (int i = threadIdx.x; i < HPLANE; i += BLK) sm[i] = 0ull;
+  __syncthreads();
+  const int t = threadIdx.x, h = t & 1, R = (t >> 1) & 15;
+  int off[16];
+  unsigned vm = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int f = MODE == 7 ? 16 * h + 4 * (i >> 2) + ((i + R) & 3) : 16 * h + ((i + R) & 15);
+    off[i] = fslot(f);
+    if (f < F) vm |= 1u << i;
+  }
+  const int per = (N + gridDim.x - 1) / gridDim.x;
+  const int r0 = blockIdx.x * per, r1 = min(N, r0 + per);
+  unsigned long long acc = 0;
+  for (int base = r0; base < r1; base += RPI * 4) {
+    uint4 q[4];
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const size_t row = (size_t)min(base + (t >> 1) + u * RPI, r1 - 1);
+      q[u] = bins[row * 2 + h];
+      v[u] = val[row];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (base + (t >> 1) + u * RPI >= r1) continue;
+      if (MODE == 9) { acc += q[u].x ^ q[u].y ^ q[u].z ^ q[u].w ^ __float_as_uint(v[u]); continue; }
+      const unsigned long long qa = ((unsigned long long)1 << 48) + (unsigned long long)(long long)__float2int_rz(v[u] * 1073741824.f);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        if (!((vm >> i) & 1u)) continue;
+        unsigned w;
+        int sh;
+        if (MODE == 7) {
+          w = (i >> 2) == 0 ? q[u].x : (i >> 2) == 1 ? q[u].y : (i >> 2) == 2 ? q[u].z : q[u].w;
+          sh = 8 * ((i + R) & 3);
+        } else {
+          const int wi = ((i + R) >> 2) & 3;
+          w = q[u].x;
+          w = wi == 1 ? q[u].y : w;
+          w = wi == 2 ? q[u].z : w;
+          w = wi == 3 ? q[u].w : w;
+          sh = 8 * ((i + R) & 3);
+        }
+        const unsigned bin = (w >> sh) & 0xFFu;
+        atomicAdd(sm + bin * FTILE + off[i], qa);
+      }
+    }
+  }
+  __syncthreads();
+  unsigned long long s = acc;
+  for (int i = threadIdx.x; i < HPLANE; i += BLK) s += sm[i];
+  atomicAdd(out, s);
+}
+
+// loads only, production layout (one dword per lane + the row value)
+template <int BLK>
+__global__ __launch_bounds__(BLK) void kern_ld(const unsigned* __restrict__ bins32, const float* __restrict__ val,
+                                               int N, unsigned long long* __restrict__ out) {
+  constexpr int RPI = BLK / LPR;
+  const int g = threadIdx.x / LPR, j = threadIdx.x % LPR;
+  const int per = (N + gridDim.x - 1) / gridDim.x;
+  const int r0 = blockIdx.x * per, r1 = min(N, r0 + per);
+  unsigned long long acc = 0;
+  for (int base = r0; base < r1; base += RPI * UNR) {
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const size_t row = (size_t)min(base + g + u * RPI, r1 - 1);
+      acc += bins32[row * 8 + j] ^ __float_as_uint(val[row]);
+    }
+  }
+  atomicAdd(out, acc);
+}
+
+template <int MODE, int BLK>
+float run2(const unsigned* b, const float* v, int N, int F, unsigned long long* out, int grid) {
+  hipEvent_t a, e;
+  hipEventCreate(&a); hipEventCreate(&e);
+  size_t lds = HPLANE * 8;
+  auto launch = [&]() {
+    if (MODE == 10) hipLaunchKernelGGL((kern_ld<BLK>), dim3(grid), dim3(BLK), 0, 0, b, v, N, out);
+    else hipLaunchKernelGGL((kern2<MODE, BLK>), dim3(grid), dim3(BLK), lds, 0, (const uint4*)b, v, N, F, out);
+  };
+  hipMemset(out, 0, 8);
+  launch();
+  hipError_t rc = hipDeviceSynchronize();
+  unsigned long long chk = 0;
+  hipMemcpy(&chk, out, 8, hipMemcpyDeviceToHost);
+  printf("[mode %d checksum %llx] ", MODE, chk);
+  if (rc != hipSuccess) { printf("launch failed: %s\n", hipGetErrorString(rc)); exit(1); }
+  float best = 1e9;
+  for (int r = 0; r < 7; ++r) {
+    hipEventRecord(a);
+    launch();
     hipEventRecord(e);
     hipEventSynchronize(e);
     float ms; hipEventElapsedTime(&ms, a, e);
@@ -130,5 +246,14 @@ int main() {
   // occupancy: 512-thread blocks, 2..4 per CU
   ROW(0, 512, 512, 0) ROW(0, 512, 1024, 0) ROW(1, 512, 512, 0) ROW(1, 512, 1024, 0) ROW(1, 256, 2048, 0)
   ROW(0, 1024, 256, 80)   // force one block per CU
+  const char* n2[] = {"2 lanes/row dwordx4 2-way", "2 lanes/row dwordx4 cfree", "2 lanes/row loads only", "1 dword/lane loads only"};
+#define ROW2(M, B, G)                                                                                  \
+  {                                                                                                    \
+    float ms = run2<M, B>(db, dv, N, F, dout, G);                                                      \
+    printf("%-26s blk %4d grid %4d          %7.3f ms  %6.2f Gupd/s  %5.2f TB/s\n", n2[M - 7], B, G, ms,  \
+           upd / ms / 1e6, (double)N * 36 / ms / 1e9);                                                 \
+  }
+  for (int g : {256, 512}) { ROW2(7, 1024, g) ROW2(8, 1024, g) ROW2(9, 1024, g) ROW2(10, 1024, g) }
+  ROW2(7, 512, 512) ROW2(8, 512, 512) ROW2(9, 512, 512) ROW2(10, 512, 512) ROW2(10, 256, 2048) ROW2(9, 256, 2048)
   return 0;
 }

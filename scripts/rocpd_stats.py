@@ -1,0 +1,38 @@
+#!/usr/bin/env python
+"""Kernel statistics table from a rocprofv3 rocpd database (ROCm 7.2 default output, ``*_results.db``).
+
+usage: python scripts/rocpd_stats.py gpurun_out/c1/prof_xgb/run_results.db [--top 30] [--md]
+"""
+import argparse
+import sqlite3
+
+
+def stats(db_path: str):
+    db = sqlite3.connect(db_path)
+    rows = db.execute("select name, count(*), sum(end - start), avg(end - start), min(end - start), max(end - start) "
+                      "from kernels group by name order by sum(end - start) desc").fetchall()
+    span = db.execute("select min(start), max(end) from kernels").fetchone()
+    return rows, span
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("db")
+    ap.add_argument("--top", type=int, default=30)
+    ap.add_argument("--md", action="store_true")
+    a = ap.parse_args()
+    rows, span = stats(a.db)
+    tot = sum(r[2] for r in rows)
+    print(f"kernels: {sum(r[1] for r in rows)} dispatches, {tot / 1e6:.2f} ms busy, first->last {(span[1] - span[0]) / 1e6:.2f} ms")
+    if a.md:
+        print("| kernel | calls | total ms | avg us | min us | max us | % |\n|---|---|---|---|---|---|---|")
+    for name, n, s, avg, mn, mx in rows[: a.top]:
+        nm = name if len(name) < 70 else name[:67] + "..."
+        if a.md:
+            print(f"| `{nm}` | {n} | {s / 1e6:.2f} | {avg / 1e3:.1f} | {mn / 1e3:.1f} | {mx / 1e3:.1f} | {100 * s / tot:.1f} |")
+        else:
+            print(f"{nm:70s} {n:6d} {s / 1e6:9.2f} ms {avg / 1e3:9.1f} us {100 * s / tot:5.1f} %")
+
+
+if __name__ == "__main__":
+    main()

@@ -125,3 +125,48 @@ def test_heartbeat_failure_detection():
             p.kill()
     ok_before, ok_after, dead = res["r0"]
     assert ok_before and not ok_after and dead == [1]
+
+
+def _oom_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      H2O_AMD_DEVICE="cpu")
+    sys.path.insert(0, ROOT)
+    import time as _t
+    import torch.distributed as dist
+    from llama_github_io_amd.parallel import collectives as coll
+    from llama_github_io_amd.utils import memory
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def build():
+        if rank == 1:                       # one rank runs out of device memory inside the sharded build
+            _t.sleep(0.5)
+            raise torch.cuda.OutOfMemoryError("simulated: HIP out of memory")
+        t = torch.ones(8)
+        coll.all_reduce_(t)                 # its peer is waiting in the build's next collective
+        return t
+    t0 = _t.time()
+    try:
+        memory.with_backpressure(build)
+        q.put((rank, "returned", _t.time() - t0))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, type(e).__name__, _t.time() - t0))
+
+
+def test_oom_in_sharded_build_fails_every_rank_fast():
+    """utils/memory.with_backpressure under row sharding: an OOM on one rank aborts the process group,
+    so its peer leaves the pending collective with an error instead of hanging (no one-sided retry)."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_oom_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(30)
+    assert res[0][1] != "returned" and res[1][1] == "RuntimeError", res
+    assert all(r[2] < 30 for r in res), res

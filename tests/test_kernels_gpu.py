@@ -190,8 +190,8 @@ def test_kmeans_step_kernel():
     assert torch.allclose(sums, ref, rtol=1e-4, atol=1e-2) and torch.allclose(cnt, cref, rtol=1e-4, atol=1e-2)
 
 
-@pytest.mark.parametrize("N,K,P,weighted", [(100003, 10, 20, True), (4099, 37, 50, False), (20000, 64, 64, True),
-                                             (777, 1, 1, False), (50001, 17, 33, True)])
+@pytest.mark.parametrize("N,K,P,weighted", [(100003, 10, 20, True), (4099, 37, 52, False), (20000, 64, 64, True),
+                                             (777, 1, 4, False), (50001, 17, 36, True)])
 def test_kmeans_mfma_lloyd_matches_fp32_reference(N, K, P, weighted, monkeypatch):
     """csrc/kmeans_mfma.hip (distance + centroid GEMMs on v_mfma_f32_16x16x4_f32) vs a plain PyTorch fp32/fp64
     reference of the same Lloyd step: argmin, min distance, per-center weighted sums and counts."""
@@ -339,3 +339,44 @@ def test_expander_hip_matches_cpu(standardize, dtype):
     Zg = eg.transform(X.to(dev), dtype=dtype).float().cpu()
     tol = 1e-5 if dtype == torch.float32 else 2e-2
     assert torch.allclose(Zc, Zg, rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize("init", ["Furthest", "PlusPlus", "Random"])
+def test_kmeans_offset_data_matches_cpu(init):
+    """standardize=False on columns offset by 1e4: the training space is centred, so the MFMA
+    distance GEMM does not cancel; the device run (pipelined MFMA Lloyd step, device-side seeding,
+    speculative convergence check) finds the same clustering as the CPU reference path."""
+    from llama_github_io_amd.models.kmeans import KMeansTrainer
+    g = torch.Generator().manual_seed(5)
+    N, F = 60000, 6
+    centers = torch.randn(4, F, generator=g) * 4
+    lab = torch.randint(0, 4, (N,), generator=g)
+    X = (centers[lab] + 0.3 * torch.randn(N, F, generator=g)).T.contiguous() + 1e4
+    info = _info(F)
+    info.response = None
+    prm = dict(k=4, max_iterations=20, init=init, seed=7, standardize=False)
+    mg = KMeansTrainer(prm).fit(X.to(dev), None, None, None, info)
+    mc = KMeansTrainer(prm).fit(X, None, None, None, info)
+    cg = np.array(mg.output["centers"])
+    cc = np.array(mc.output["centers"])
+    np.testing.assert_allclose(cg, cc, rtol=0, atol=1e-3)
+    assert mg.output["iterations"] == mc.output["iterations"]
+    tg, tc = mg.output["training_metrics"]["tot_withinss"], mc.output["training_metrics"]["tot_withinss"]
+    assert abs(tg - tc) <= 1e-6 * tc
+    # the recovered centers are the generating ones (clusters are well separated)
+    for c in cg:
+        assert float(((centers.numpy() + 1e4 - c) ** 2).sum(1).min()) < 0.05
+
+
+@pytest.mark.parametrize("n,idt,vdt", [(10, torch.int64, torch.float64), (3000, torch.int32, torch.float32),
+                                       (16384, torch.int64, torch.float32), (1, torch.int32, torch.float64)])
+def test_segment_sum_kernel_matches_index_add(n, idt, vdt):
+    """csrc/segment_kernels.hip (LDS-privatised fp64 segment sums) vs the fp64 index_add reference."""
+    from llama_github_io_amd.ops.segment import segment_sum
+    g = torch.Generator().manual_seed(n)
+    N = 1_234_567
+    idx = torch.randint(0, n, (N,), generator=g).to(idt)
+    v = torch.randn(N, generator=g).to(vdt)
+    got = segment_sum(idx.to(dev), v.to(dev), n).cpu()
+    ref = torch.zeros(n, dtype=torch.float64).index_add_(0, idx.long(), v.double())
+    assert got.dtype == torch.float64 and torch.allclose(got, ref, rtol=1e-12, atol=1e-9)
