@@ -63,24 +63,38 @@ def main():
     ap.add_argument("--rows", type=int, default=11_000_000)
     ap.add_argument("--depth", type=int, default=6)
     ap.add_argument("--no-job", action="store_true", help="skip the whole 100-tree job measurement")
+    ap.add_argument("--backend", default=None, help="torch.distributed backend (default: nccl = RCCL on GPUs, gloo on CPU)")
+    ap.add_argument("--device", default=None, help="cuda | cpu (default: cuda when available); cpu runs the "
+                    "reference builder, for multi-rank rehearsals of the collective protocol")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    use_gpu = torch.cuda.is_available() and args.device != "cpu"
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
+        backend = args.backend or ("nccl" if use_gpu else "gloo")
+        if use_gpu:
+            torch.cuda.set_device(local)
+            dist.init_process_group(backend, device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    dev = torch.device("cuda", local) if use_gpu else torch.device("cpu")
 
     from llama_github_io_amd.models.base import DataInfo
     from llama_github_io_amd.models.gbm import GBMTrainer
     from llama_github_io_amd.parallel import collectives as coll
 
     n_total = args.rows
-    n_local = n_total // world + (1 if rank < n_total % world else 0)
-    X, y = make_higgs_like(n_local, 1234 + 7919 * rank, dev)
+    # every rank draws the SAME global dataset and keeps its contiguous row shard: the N-GPU job trains on
+    # exactly the rows of the 1-GPU job (strong scaling on one dataset)
+    base, rem = divmod(n_total, world)
+    r0 = rank * base + min(rank, rem)
+    n_local = base + (1 if rank < rem else 0)
+    Xg, yg = make_higgs_like(n_total, 1234, dev)
+    X, y = Xg[:, r0:r0 + n_local].contiguous(), yg[r0:r0 + n_local].contiguous()
+    del Xg, yg
     F = X.shape[0]
     info = DataInfo([f"x{i}" for i in range(F)], np.zeros(F, np.int32), [None] * F, "y", ["0", "1"])
     params = dict(ntrees=args.warmup + args.steps, max_depth=args.depth, min_rows=10, learn_rate=0.1, seed=42,

@@ -1,0 +1,417 @@
+// DeepLearning training step on the matrix cores (reference: h2o-algos/src/main/java/hex/deeplearning/
+// Neurons.java fprop / bprop, DeepLearningTask.map; the mini-batch replaces the reference's per-row Hogwild).
+//
+// One optimizer step of an MLP (bias + Rectifier/Tanh hidden layers with dropout, softmax-CE or squared-error
+// output) is three launches instead of ~20 library GEMMs and elementwise kernels:
+//
+//  k_dl_rows   one workgroup per 16-row tile of the mini-batch. The tile's input rows are gathered from the
+//              resident design matrix by row index, then the WHOLE network runs on that tile with the
+//              activations in LDS: every layer is v_mfma_f32_16x16x32_bf16 over (activation tile in LDS) x
+//              (bf16 weight rows streamed from L2), with bias / activation / dropout fused in the epilogue;
+//              the output gradient (softmax - onehot) * w, and the backward pass dh = dA W, dA = dh * mask *
+//              act'(h) run the same way on transposed weight copies. The tile writes its activations and
+//              gradients TRANSPOSED ([units][rows]) for the weight-gradient GEMM and its per-column bias
+//              gradient partial sums (fixed-order reduce later, no atomics).
+//  k_dl_wgrad  dW_l = dA_lᵀ h_{l-1} for every layer in one launch: 64 x 64 output tiles x 4 row splits,
+//              operands loaded straight from the transposed buffers (contiguous along rows), fp32 partial
+//              slabs per split.
+//  k_dl_reduce sums the slabs / bias partials in a fixed order into the flat gradient buffer, scaled by
+//              1 / sum(w) of the batch (single process) or raw plus the batch weight (data parallel).
+// The fused ADADELTA kernel (dense_kernels.hip) then updates the fp32 master weights and the bf16 weight
+// shadow; k_dl_transpose refreshes the transposed shadow the backward pass reads.
+//
+// MFMA 16x16x32 bf16 operand maps (gfx950): lane l holds A[row l&15][k = 8(l>>4)+j], B[k = 8(l>>4)+j][col
+// l&15] (j = 0..7) and D[row 4(l>>4)+r][col l&15] (r = 0..3).
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __hip_bfloat16 bf16;
+
+#define DL_MAXL 6        // GEMM layers (hidden + output)
+#define DL_ROWS 16       // rows per k_dl_rows tile
+#define DL_SPLIT 4       // row splits of k_dl_wgrad
+
+struct DLArgs {
+  const bf16* Z; long long ldz; const long long* ridx; int B; int Bpad;
+  const float* w; const long long* ycls; const float* yreg;
+  const float* P; const bf16* W; const bf16* WT; const unsigned long long* step_dev;
+  bf16* hT; bf16* dT; float* bpart; float* slab; float* g; float* gsum;
+  int L, K, act, regression;
+  int n[DL_MAXL + 1];           // n[0] inputs, n[l] units of layer l, n[L] = outputs
+  int kp[DL_MAXL + 1];          // n padded to 32 (GEMM K extent when the activation is an operand)
+  int ld[DL_MAXL + 1];          // LDS row stride of activation tiles (kp + 8: spreads rows over banks)
+  long long w_off[DL_MAXL], b_off[DL_MAXL];   // layer l+1's weights / biases in the flat parameter buffer
+  long long h_off[DL_MAXL + 1], d_off[DL_MAXL + 1];
+  int bias_off[DL_MAXL + 1], bias_total;
+  float drop[DL_MAXL]; unsigned long long seed_base[DL_MAXL];
+  int lds_off[DL_MAXL + 1];     // activation tiles l = 0..L-1, then the output-gradient tile
+  int lds_g[2], lds_w;          // two gradient tiles, row weights
+  int tiles_i[DL_MAXL], tiles_j[DL_MAXL], tile_start[DL_MAXL + 1];   // k_dl_wgrad block decode
+  long long n_decay, n_total;
+};
+
+__device__ __forceinline__ uint32_t hash32(uint64_t x) {
+  x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL; x ^= x >> 33;
+  return (uint32_t)x;
+}
+// the dropout mask of dense_kernels.hip k_bias_act_fwd / k_bias_act_bwd (element index within the batch)
+__device__ __forceinline__ bool dropped(uint64_t seed, int64_t i, uint32_t thr) {
+  return hash32(seed ^ (uint64_t)i * 0x9E3779B97F4A7C15ULL) < thr;
+}
+__device__ __forceinline__ float act_f(int a, float v) {
+  return a == 1 ? (v > 0.f ? v : 0.f) : (a == 2 ? tanhf(v) : (a == 3 ? (v > 0.f ? v : expm1f(v)) : v));
+}
+__device__ __forceinline__ float dact_from_y(int a, float y) {
+  return a == 1 ? (y > 0.f ? 1.f : 0.f) : (a == 2 ? 1.f - y * y : (a == 3 ? (y > 0.f ? 1.f : y + 1.f) : 1.f));
+}
+
+// 8 bf16 of a global row [k, k+8) with a zero tail past `kvalid`; vector load when aligned
+__device__ __forceinline__ bf16x8 load8(const bf16* row, int k, int kvalid, bool vec) {
+  if (vec && k + 8 <= kvalid) return *reinterpret_cast<const bf16x8*>(row + k);
+  bf16x8 v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float f = (k + j < kvalid) ? __bfloat162float(row[k + j]) : 0.f;
+    v[j] = (__bf16)f;
+  }
+  return v;
+}
+
+// D(16 x 16 cols n0..n0+15) = A(LDS tile, 16 x K) * Bᵀ where B row n (global, contiguous along k) holds the
+// operand column n: B[k][n] = Brow(n)[k]. K is a multiple of 32; A is zero past the valid extent.
+// The B fragments come from L2 (every tile of the batch reads the same weights): KU k-steps of loads are
+// issued before their MFMAs so KU round trips overlap instead of serialising one per MFMA.
+#define KU 8
+__device__ __forceinline__ f32x4 tile_mm(const bf16* A, int lda, const bf16* Bg, long long ldb, int n0, int nvalid,
+                                         int K, int kvalid, bool vec) {
+  const int lane = threadIdx.x & 63, q = lane >> 4, c = lane & 15;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  const int n = n0 + c;
+  const bool nok = n < nvalid;
+  const bf16* brow = Bg + (long long)(nok ? n : 0) * ldb;
+  const bf16x8 z8 = {(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
+  for (int kb = 0; kb < K; kb += 32 * KU) {
+    bf16x8 b[KU];
+#pragma unroll
+    for (int u = 0; u < KU; ++u) {
+      const int k = kb + 32 * u + 8 * q;
+      b[u] = (nok && kb + 32 * u < K) ? load8(brow, k, kvalid, vec) : z8;
+    }
+#pragma unroll
+    for (int u = 0; u < KU; ++u) {
+      if (kb + 32 * u < K) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(A + c * lda + kb + 32 * u + 8 * q);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[u], acc, 0, 0, 0);
+      }
+    }
+  }
+  return acc;
+}
+
+// column sums of the 16 x 16 D tile (rows 4q + r): in-lane over r, then across the 4 lane quarters
+__device__ __forceinline__ float col_sum(f32x4 v) {
+  float s = (v[0] + v[1]) + (v[2] + v[3]);
+  s += __shfl_xor(s, 16, 64);
+  s += __shfl_xor(s, 32, 64);
+  return s;
+}
+
+__device__ __forceinline__ void store4T(bf16* dst, f32x4 v) {   // 4 consecutive rows of one unit, 8 bytes
+  union { bf16 h[4]; uint2 u; } pk;
+  pk.h[0] = __float2bfloat16(v[0]); pk.h[1] = __float2bfloat16(v[1]);
+  pk.h[2] = __float2bfloat16(v[2]); pk.h[3] = __float2bfloat16(v[3]);
+  *reinterpret_cast<uint2*>(dst) = pk.u;
+}
+
+__global__ __launch_bounds__(256) void k_dl_rows(DLArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16* S = reinterpret_cast<bf16*>(smem);
+  float* ws = reinterpret_cast<float*>(smem + a.lds_w);
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, q = lane >> 4, c = lane & 15;
+  const int r0 = blockIdx.x * DL_ROWS;
+  const int L = a.L;
+  const uint64_t step = a.step_dev ? *a.step_dev : 0ull;
+  __shared__ long long srow[DL_ROWS];
+  __shared__ float sy[DL_ROWS];
+  __shared__ long long scls[DL_ROWS];
+  if (tid < DL_ROWS) {
+    const int r = r0 + tid;
+    const long long g = r < a.B ? a.ridx[r] : -1;
+    srow[tid] = g;
+    ws[tid] = g >= 0 ? a.w[g] : 0.f;
+    if (a.regression) sy[tid] = g >= 0 ? a.yreg[g] : 0.f;
+    else scls[tid] = g >= 0 ? a.ycls[g] : -1;
+  }
+  // zero every activation / gradient tile (K padding must read as zeros)
+  {
+    const int total = a.lds_w / 4;
+    for (int i = tid; i < total; i += 256) reinterpret_cast<float*>(smem)[i] = 0.f;
+  }
+  __syncthreads();
+  // ---- gather the 16 input rows into activation tile 0
+  {
+    bf16* A0 = S + a.lds_off[0];
+    const int n0 = a.n[0], ld0 = a.ld[0];
+    const bool vec = (n0 % 8 == 0) && (a.ldz % 8 == 0);
+    const int chunks = (n0 + 7) / 8;
+    for (int i = tid; i < DL_ROWS * chunks; i += 256) {
+      const int rr = i / chunks, k = (i - rr * chunks) * 8;
+      const long long g = srow[rr];
+      if (g < 0) continue;
+      const bf16* src = a.Z + g * a.ldz;
+      bf16* dst = A0 + rr * ld0 + k;
+      if (vec) *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src + k);
+      else for (int j = 0; j < 8 && k + j < n0; ++j) dst[j] = src[k + j];
+    }
+  }
+  __syncthreads();
+  // x transposed for the first weight gradient: hT_0[k][r0 + 4 g .. + 3]
+  {
+    const bf16* A0 = S + a.lds_off[0];
+    bf16* dst = a.hT + a.h_off[0];
+    for (int i = tid; i < a.n[0] * 4; i += 256) {
+      const int k = i >> 2, g4 = (i & 3) * 4;
+      f32x4 v = {__bfloat162float(A0[(g4 + 0) * a.ld[0] + k]), __bfloat162float(A0[(g4 + 1) * a.ld[0] + k]),
+                 __bfloat162float(A0[(g4 + 2) * a.ld[0] + k]), __bfloat162float(A0[(g4 + 3) * a.ld[0] + k])};
+      store4T(dst + (long long)k * a.Bpad + r0 + g4, v);
+    }
+  }
+  // ---- forward: hidden layers
+  for (int l = 1; l < L; ++l) {
+    const bf16* Ain = S + a.lds_off[l - 1];
+    bf16* Aout = S + a.lds_off[l];
+    const int nin = a.n[l - 1], nout = a.n[l];
+    const bool vec = (nin % 8 == 0) && (a.w_off[l - 1] % 8 == 0);
+    const float drop = a.drop[l - 1], keep = 1.f - drop;
+    const uint32_t thr = (uint32_t)(drop * 4294967296.0);
+    const uint64_t seed = a.seed_base[l - 1] ^ (step * 0x9E3779B97F4A7C15ULL);
+    const int T = (nout + 15) / 16;
+    for (int t = wv; t < T; t += 4) {
+      const f32x4 acc = tile_mm(Ain, a.ld[l - 1], a.W + a.w_off[l - 1], nin, t * 16, nout, a.kp[l - 1], nin, vec);
+      const int col = t * 16 + c;
+      f32x4 o;
+      if (col < nout) {
+        const float b = a.P[a.b_off[l - 1] + col];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = act_f(a.act, acc[r] + b);
+          if (drop > 0.f) v = dropped(seed, (int64_t)(r0 + 4 * q + r) * nout + col, thr) ? 0.f : v / keep;
+          o[r] = v;
+          Aout[(4 * q + r) * a.ld[l] + col] = __float2bfloat16(v);
+        }
+        store4T(a.hT + a.h_off[l] + (long long)col * a.Bpad + r0 + 4 * q, o);
+      }
+    }
+    __syncthreads();
+  }
+  // ---- output layer + loss gradient (wave 0; K <= 16)
+  bf16* GO = S + a.lds_off[L];
+  if (wv == 0) {
+    const int nin = a.n[L - 1], K = a.K;
+    const bool vec = (nin % 8 == 0) && (a.w_off[L - 1] % 8 == 0);
+    const f32x4 acc = tile_mm(S + a.lds_off[L - 1], a.ld[L - 1], a.W + a.w_off[L - 1], nin, 0, K, a.kp[L - 1], nin, vec);
+    const bool cok = c < K;
+    const float b = cok ? a.P[a.b_off[L - 1] + c] : 0.f;
+    f32x4 g;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 4 * q + r;
+      const float o = cok ? acc[r] + b : -INFINITY;
+      const float wr = ws[row];
+      if (a.regression) {
+        g[r] = (c == 0) ? (o - sy[row]) * wr : 0.f;
+      } else {
+        float mx = o;
+        for (int m = 1; m < 16; m <<= 1) mx = fmaxf(mx, __shfl_xor(mx, m, 64));
+        const float e = cok ? __expf(o - mx) : 0.f;
+        float z = e;
+        for (int m = 1; m < 16; m <<= 1) z += __shfl_xor(z, m, 64);
+        g[r] = cok ? (e / z - (scls[row] == c ? 1.f : 0.f)) * wr : 0.f;
+      }
+      GO[row * a.ld[L] + c] = __float2bfloat16(g[r]);
+    }
+    const float cs = col_sum(g);
+    if (q == 0 && cok) a.bpart[(long long)blockIdx.x * (a.bias_total + 1) + a.bias_off[L] + c] = cs;
+    if (cok) store4T(a.dT + a.d_off[L] + (long long)c * a.Bpad + r0 + 4 * q, g);
+  }
+  __syncthreads();
+  // ---- backward through the hidden layers
+  const bf16* Gin = GO;
+  int ldg_in = a.ld[L];
+  for (int l = L - 1; l >= 1; --l) {
+    bf16* Gout = S + a.lds_g[l & 1];
+    const int nout = a.n[l], nnext = a.n[l + 1];
+    const bool vec = (nnext % 8 == 0) && (a.w_off[l] % 8 == 0);
+    const float drop = a.drop[l - 1], keep = 1.f - drop;
+    const uint32_t thr = (uint32_t)(drop * 4294967296.0);
+    const uint64_t seed = a.seed_base[l - 1] ^ (step * 0x9E3779B97F4A7C15ULL);
+    const bf16* H = S + a.lds_off[l];
+    const int T = (nout + 15) / 16;
+    for (int t = wv; t < T; t += 4) {
+      // dh = G_{l+1} W_{l+1}: B[k = unit of l+1][n = unit of l] = WT_{l+1}[n][k]
+      const f32x4 acc = tile_mm(Gin, ldg_in, a.WT + a.w_off[l], nnext, t * 16, nout, a.kp[l + 1], nnext, vec);
+      const int col = t * 16 + c;
+      f32x4 gd = {0.f, 0.f, 0.f, 0.f};
+      if (col < nout) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 4 * q + r;
+          float y = __bfloat162float(H[row * a.ld[l] + col]);
+          float gg = acc[r];
+          if (drop > 0.f) {
+            const bool d = dropped(seed, (int64_t)(r0 + row) * nout + col, thr);
+            gg = d ? 0.f : gg / keep;
+            y = d ? 0.f : y * keep;
+          }
+          gd[r] = gg * dact_from_y(a.act, y);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Gout[(4 * q + r) * a.ld[l] + col] = __float2bfloat16(gd[r]);
+      const float cs = col_sum(gd);
+      if (col < nout) {
+        if (q == 0) a.bpart[(long long)blockIdx.x * (a.bias_total + 1) + a.bias_off[l] + col] = cs;
+        store4T(a.dT + a.d_off[l] + (long long)col * a.Bpad + r0 + 4 * q, gd);
+      }
+    }
+    __syncthreads();
+    // zero the K padding of the gradient tile the next layer reads
+    for (int i = tid; i < DL_ROWS * (a.kp[l] - T * 16); i += 256) {
+      const int rr = i / (a.kp[l] - T * 16), cc = T * 16 + i % (a.kp[l] - T * 16);
+      Gout[rr * a.ld[l] + cc] = __float2bfloat16(0.f);
+    }
+    __syncthreads();
+    Gin = Gout;
+    ldg_in = a.ld[l];
+  }
+  if (tid == 0) {
+    float s = 0.f;
+    for (int i = 0; i < DL_ROWS; ++i) s += ws[i];
+    a.bpart[(long long)blockIdx.x * (a.bias_total + 1) + a.bias_total] = s;
+  }
+}
+
+// dW_l[i][j] = sum_rows dA_l[row][i] h_{l-1}[row][j]: A[i][k = row] = dT_l[i][row], B[k = row][j] = hT_{l-1}[j][row].
+// Block = one 64 x 64 tile of one layer and one row split; wave (wi, wj) owns a 32 x 32 quarter (2 x 2 MFMA tiles).
+__global__ __launch_bounds__(256) void k_dl_wgrad(DLArgs a) {
+  const int tiles = a.tile_start[a.L];
+  const int b = blockIdx.x % tiles, split = blockIdx.x / tiles;
+  int l = 0;
+  while (l + 1 < a.L && b >= a.tile_start[l + 1]) ++l;          // GEMM layer l + 1 (0-based l)
+  const int bt = b - a.tile_start[l];
+  const int ti = bt / a.tiles_j[l], tj = bt - ti * a.tiles_j[l];
+  const int ni = a.n[l + 1], nj = a.n[l];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, q = lane >> 4, c = lane & 15;
+  const int i0 = ti * 64 + (wv >> 1) * 32, j0 = tj * 64 + (wv & 1) * 32;
+  const bf16* Ab = a.dT + a.d_off[l + 1];
+  const bf16* Bb = a.hT + a.h_off[l];
+  const int rows = a.Bpad / DL_SPLIT;
+  const int k_beg = split * rows, k_end = k_beg + rows;
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int v = 0; v < 2; ++v) acc[u][v] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const bf16x8 z8 = {(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
+  for (int k0 = k_beg; k0 < k_end; k0 += 32) {
+    bf16x8 av[2], bv[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = i0 + u * 16 + c;
+      av[u] = i < ni ? *reinterpret_cast<const bf16x8*>(Ab + (long long)i * a.Bpad + k0 + 8 * q) : z8;
+      const int j = j0 + u * 16 + c;
+      bv[u] = j < nj ? *reinterpret_cast<const bf16x8*>(Bb + (long long)j * a.Bpad + k0 + 8 * q) : z8;
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int v = 0; v < 2; ++v) acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[u], bv[v], acc[u][v], 0, 0, 0);
+  }
+  float* out = a.slab + (long long)split * a.n_decay + a.w_off[l];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+      const int j = j0 + v * 16 + c;
+      if (j >= nj) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = i0 + u * 16 + 4 * q + r;
+        if (i < ni) out[(long long)i * nj + j] = acc[u][v][r];
+      }
+    }
+}
+
+// flat gradient = fixed-order sums of the weight slabs and the per-tile bias partials, times 1 / sum(w)
+// (scale_by_w) — or raw, with sum(w) stored after the gradient (data parallel: gsum = gbuf[-1]).
+__global__ __launch_bounds__(256) void k_dl_reduce(DLArgs a, int G1, int scale_by_w) {
+  __shared__ float s_sw;
+  if (threadIdx.x < 64) {
+    float s = 0.f;
+    for (int g = threadIdx.x; g < G1; g += 64) s += a.bpart[(long long)g * (a.bias_total + 1) + a.bias_total];
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if (threadIdx.x == 0) s_sw = s;
+  }
+  __syncthreads();
+  const float sw = s_sw;
+  const float inv = scale_by_w ? 1.f / fmaxf(sw, 1e-12f) : 1.f;
+  if (!scale_by_w && blockIdx.x == 0 && threadIdx.x == 0 && a.gsum) *a.gsum = sw;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < a.n_total; e += (long long)gridDim.x * blockDim.x) {
+    float v = 0.f;
+    if (e < a.n_decay) {
+#pragma unroll
+      for (int s = 0; s < DL_SPLIT; ++s) v += a.slab[(long long)s * a.n_decay + e];
+    } else {
+      int l = 0;
+      while (l + 1 < a.L && e >= a.b_off[l + 1]) ++l;
+      const int col = (int)(e - a.b_off[l]);
+      const int bo = a.bias_off[l + 1] + col;
+      for (int g = 0; g < G1; ++g) v += a.bpart[(long long)g * (a.bias_total + 1) + bo];
+    }
+    a.g[e] = v * inv;
+  }
+}
+
+// WT_l[j][i] = W_l[i][j] for every layer (the bf16 shadow the backward pass reads)
+__global__ __launch_bounds__(256) void k_dl_transpose(DLArgs a) {
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < a.n_decay; e += (long long)gridDim.x * blockDim.x) {
+    int l = 0;
+    while (l + 1 < a.L && e >= a.w_off[l + 1]) ++l;
+    const long long o = e - a.w_off[l];
+    const int nin = a.n[l], i = (int)(o / nin), j = (int)(o - (long long)i * nin);
+    const_cast<bf16*>(a.WT)[a.w_off[l] + (long long)j * a.n[l + 1] + i] = a.W[e];
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int h2o_dl_args_size() { return (int)sizeof(DLArgs); }
+
+// lds: bytes of dynamic LDS for k_dl_rows (activation + gradient tiles + row weights)
+int h2o_dl_step(const DLArgs* a, int lds, int scale_by_w, hipStream_t s) {
+  if (a->L < 1 || a->L > DL_MAXL || a->K > 16 || a->Bpad % (32 * DL_SPLIT) != 0 || lds > 160 * 1024)
+    return (int)hipErrorInvalidValue;
+  const int G1 = a->Bpad / DL_ROWS;
+  hipLaunchKernelGGL(k_dl_rows, dim3(G1), dim3(256), lds, s, *a);
+  hipLaunchKernelGGL(k_dl_wgrad, dim3(a->tile_start[a->L] * DL_SPLIT), dim3(256), 0, s, *a);
+  long long grid = (a->n_total + 255) / 256;
+  if (grid > 1024) grid = 1024;
+  hipLaunchKernelGGL(k_dl_reduce, dim3((unsigned)grid), dim3(256), 0, s, *a, G1, scale_by_w);
+  return (int)hipGetLastError();
+}
+
+int h2o_dl_transpose(const DLArgs* a, hipStream_t s) {
+  long long grid = (a->n_decay + 255) / 256;
+  if (grid > 2048) grid = 2048;
+  hipLaunchKernelGGL(k_dl_transpose, dim3((unsigned)grid), dim3(256), 0, s, *a);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -390,6 +390,8 @@ class DeepLearningTrainer:
                             q.mul_(torch.where(n2 > max_w2, torch.sqrt(max_w2 / n2), torch.ones_like(n2)))
                 if shadow is not None and (not adaptive or max_w2 < float("inf")):
                     shadow.copy_(fp.p[: fp.n_decay])
+                if fz.get("obj") is not None:
+                    fz["obj"].refresh_transposed()
 
         # Explicit training step (no autograd) for the common MLPs: GEMMs on bf16 weight copies kept by the
         # fused ADADELTA kernel, fused bias/activation/dropout epilogues, one fused softmax-CE / squared-error
@@ -451,6 +453,35 @@ class DeepLearningTrainer:
                         gbuf[:-1].copy_(fp.g)
                         gbuf[-1:].copy_(wb.sum().view(1))
 
+        # Fused MFMA step (ops/dl.py, csrc/dl_kernels.hip): gather + forward + loss gradient + backward on
+        # 16-row tiles with the activations in LDS, all weight gradients in one launch, fixed-order reduce.
+        # Built per batch capacity in alloc(); the library-GEMM explicit step above stays for other shapes.
+        from ..ops import dl as dlops
+        fz = dict(obj=None, ok=False, sridx=None)
+        if (explicit and cdt == torch.bfloat16 and os.environ.get("H2O_DL_FUSED", "1") == "1"
+                and dlops.supported(int(Z.shape[1]), [int(h_) for h_ in hidden], int(net.out.weight.shape[0]),
+                                    act_code, Z)):
+            fz["ok"] = True
+            fz["bases"] = [(seed * 1000003 + i * 7919) & ((1 << 62) - 1) for i in range(len(net.hidden))]
+
+        def fused_build(cap):
+            gout = gbuf[:-1] if sharded else fp.g
+            gsum = gbuf[-1:] if sharded else None
+            fz["obj"] = dlops.FusedMLPStep(fp, list(net.hidden) + [net.out], act_code, list(net.hid_drop),
+                                           fz["bases"], Z, wf, yt, cat == "Regression", cap, shadow, step_t, gout,
+                                           gsum)
+            fz["obj"].refresh_transposed()
+            fz["sridx"] = torch.full((cap,), -1, dtype=torch.long, device=dev)
+
+        if fz["ok"]:
+            fwd_bwd_lib = fwd_bwd
+
+            def fwd_bwd(xb, wb, tb):      # noqa: F811 - rows come from the static index buffer, not xb
+                if fz["obj"] is None:     # eager steps (no graph capture): the library-GEMM explicit step
+                    return fwd_bwd_lib(xb, wb, tb)
+                fz["obj"].args.step_dev = step_t.data_ptr()
+                fz["obj"].step(fz["sridx"])
+
         # hipGraph capture of the training step (fwd + bwd (+ update)): a fixed launch sequence on static
         # batch buffers, replayed per step. Row-sharded runs capture fwd+bwd and the update separately with
         # the one flat gradient all-reduce between them; their local batch buffer is sized to the largest
@@ -463,6 +494,8 @@ class DeepLearningTrainer:
 
         def alloc(cap):
             nonlocal sx, sw, sy
+            if fz["ok"]:
+                fused_build(cap)
             sx = torch.zeros(cap, Z.shape[1], dtype=Z.dtype, device=dev)
             sw = torch.zeros(cap, dtype=wf.dtype, device=dev)
             sy = None if ae else torch.zeros((cap,) + tdim, dtype=yt.dtype, device=dev)
@@ -522,12 +555,16 @@ class DeepLearningTrainer:
             def chunk_body():
                 for k in range(CH):
                     r = ridx[k * B:(k + 1) * B]
-                    torch.index_select(Z, 0, r, out=sx)
-                    torch.index_select(wf, 0, r, out=sw)
-                    if sy is not None:
-                        torch.index_select(yt, 0, r, out=sy)
                     net.step_dev = step_v[k:k + 1]
-                    fwd_bwd(sx, sw, sy)
+                    if fz.get("obj") is not None:         # the fused step gathers its rows itself
+                        fz["obj"].args.step_dev = step_v[k:k + 1].data_ptr()
+                        fz["obj"].step(r)
+                    else:
+                        torch.index_select(Z, 0, r, out=sx)
+                        torch.index_select(wf, 0, r, out=sw)
+                        if sy is not None:
+                            torch.index_select(yt, 0, r, out=sy)
+                        fwd_bwd(sx, sw, sy)
                     update(rate_v[k], mom_v[k], on_v[k])
                 net.step_dev = step_t
 
@@ -616,12 +653,17 @@ class DeepLearningTrainer:
                     on_t.fill_(1.0 if m > 0 else 0.0)
                 if use_graph:
                     c = rows.numel()
-                    torch.index_select(Z, 0, rows, out=sx[:c])
-                    torch.index_select(wf, 0, rows, out=sw[:c])
-                    if c < sw.numel():
-                        sw[c:].zero_()
-                    if sy is not None:
-                        torch.index_select(yt, 0, rows, out=sy[:c])
+                    if fz.get("obj") is not None:
+                        fz["sridx"][:c].copy_(rows)
+                        if c < fz["sridx"].numel():
+                            fz["sridx"][c:].fill_(-1)
+                    else:
+                        torch.index_select(Z, 0, rows, out=sx[:c])
+                        torch.index_select(wf, 0, rows, out=sw[:c])
+                        if c < sw.numel():
+                            sw[c:].zero_()
+                        if sy is not None:
+                            torch.index_select(yt, 0, rows, out=sy[:c])
                     step_t.fill_(step)
                     run_step()
                 else:
@@ -662,6 +704,7 @@ class DeepLearningTrainer:
                 if float(p["max_runtime_secs"] or 0) > 0 and coll.agree(time.time() - t0 > float(p["max_runtime_secs"])):
                     break
         model.output["training_step_explicit"] = bool(explicit)
+        model.output["training_step_fused_mfma"] = fz.get("obj") is not None
         model.output["phase_seconds"] = dict(setup=t_loop0 - t0, train_loop=time.time() - t_loop0 - t_scoring,
                                              scoring=t_scoring)
         model.output["training_step_mode"] = (

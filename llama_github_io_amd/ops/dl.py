@@ -1,0 +1,157 @@
+"""Fused MFMA training step of the DeepLearning MLP (``csrc/dl_kernels.hip``).
+
+Reference: ``hex/deeplearning/Neurons.java`` fprop / bprop (``DeepLearningTask.map``). One step is
+``k_dl_rows`` (gather + every layer forward + loss gradient + every layer backward on 16-row tiles, activations
+in LDS) -> ``k_dl_wgrad`` (all weight gradients) -> ``k_dl_reduce`` (fixed-order partial sums into the flat
+gradient buffer); the optimizer (fused ADADELTA) then refreshes the bf16 weight shadow and
+:meth:`FusedMLPStep.refresh_transposed` the transposed shadow of the backward pass.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _native as nat
+
+MAXL = 6
+ROWS = 16
+SPLIT = 4
+_vp, _ci, _cll, _cf, _cull = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong, ctypes.c_float, ctypes.c_ulonglong
+
+
+class _DLArgs(ctypes.Structure):
+    """Mirror of ``DLArgs`` in ``csrc/dl_kernels.hip``."""
+    _fields_ = ([("Z", _vp), ("ldz", _cll), ("ridx", _vp), ("B", _ci), ("Bpad", _ci),
+                 ("w", _vp), ("ycls", _vp), ("yreg", _vp),
+                 ("P", _vp), ("W", _vp), ("WT", _vp), ("step_dev", _vp),
+                 ("hT", _vp), ("dT", _vp), ("bpart", _vp), ("slab", _vp), ("g", _vp), ("gsum", _vp),
+                 ("L", _ci), ("K", _ci), ("act", _ci), ("regression", _ci),
+                 ("n", _ci * (MAXL + 1)), ("kp", _ci * (MAXL + 1)), ("ld", _ci * (MAXL + 1)),
+                 ("w_off", _cll * MAXL), ("b_off", _cll * MAXL),
+                 ("h_off", _cll * (MAXL + 1)), ("d_off", _cll * (MAXL + 1)),
+                 ("bias_off", _ci * (MAXL + 1)), ("bias_total", _ci),
+                 ("drop", _cf * MAXL), ("seed_base", _cull * MAXL),
+                 ("lds_off", _ci * (MAXL + 1)), ("lds_g", _ci * 2), ("lds_w", _ci),
+                 ("tiles_i", _ci * MAXL), ("tiles_j", _ci * MAXL), ("tile_start", _ci * (MAXL + 1)),
+                 ("n_decay", _cll), ("n_total", _cll)])
+
+
+nat.register_hip_signatures({"h2o_dl_args_size": [], "h2o_dl_step": [_vp, _ci, _ci, _vp],
+                             "h2o_dl_transpose": [_vp, _vp]})
+
+
+def _r32(n: int) -> int:
+    return (n + 31) // 32 * 32
+
+
+def supported(n_in: int, hidden, n_out: int, act_code: int, Z: torch.Tensor) -> bool:
+    """Shapes the fused step handles (else the library-GEMM explicit step runs)."""
+    L = len(hidden) + 1
+    if not Z.is_cuda or Z.dtype != torch.bfloat16 or L > MAXL or n_out > 16 or act_code not in (0, 1, 2, 3):
+        return False
+    widths = [n_in] + list(hidden)
+    lds = sum(ROWS * (_r32(n) + 8) * 2 for n in widths) + ROWS * 40 * 2 + 2 * ROWS * (_r32(max(hidden or [1])) + 8) * 2 + 64
+    return lds <= 150 * 1024 and max(widths) <= 8192
+
+
+class FusedMLPStep:
+    """Static launch arguments of the fused step for one network / mini-batch capacity.
+
+    ``lins``: the hidden Linear layers then the output layer (weights ``[out, in]`` views of the flat
+    fp32 buffer ``fp.p``); ``shadow``: bf16 copy of ``fp.p[:n_decay]`` kept by the optimizer."""
+
+    def __init__(self, fp, lins, act_code: int, drops, seed_bases, Z: torch.Tensor, w: torch.Tensor, y: torch.Tensor,
+                 regression: bool, cap: int, shadow: torch.Tensor, step_dev: torch.Tensor, out_grad: torch.Tensor,
+                 out_gsum: torch.Tensor | None):
+        self.lib = nat.hip()
+        assert self.lib.h2o_dl_args_size() == ctypes.sizeof(_DLArgs), "DLArgs layout mismatch"
+        dev = Z.device
+        L = len(lins)
+        n = [lins[0].weight.shape[1]] + [l_.weight.shape[0] for l_ in lins]
+        Bpad = (cap + ROWS * 8 - 1) // (ROWS * 8) * (ROWS * 8)      # multiple of 128 = 32 x SPLIT
+        base = fp.p.data_ptr()
+        esz = fp.p.element_size()
+        a = _DLArgs()
+        a.Z, a.ldz, a.B, a.Bpad = Z.data_ptr(), Z.stride(0), int(cap), int(Bpad)
+        a.w = w.data_ptr()
+        if regression:
+            a.yreg, a.ycls, a.regression = y.data_ptr(), 0, 1
+        else:
+            a.ycls, a.yreg, a.regression = y.data_ptr(), 0, 0
+        self.WT = torch.empty_like(shadow)
+        a.P, a.W, a.WT, a.step_dev = base, shadow.data_ptr(), self.WT.data_ptr(), step_dev.data_ptr()
+        a.L, a.K, a.act = L, n[L], int(act_code)
+        for i, v in enumerate(n):
+            a.n[i] = v
+            a.kp[i] = _r32(v)
+            a.ld[i] = _r32(v) + 8
+        bias_off, bt = [0] * (MAXL + 1), 0
+        for l in range(1, L + 1):
+            bias_off[l] = bt
+            bt += n[l]
+        for l, lin in enumerate(lins):
+            a.w_off[l] = (lin.weight.data_ptr() - base) // esz
+            a.b_off[l] = (lin.bias.data_ptr() - base) // esz
+            assert a.b_off[l] >= fp.n_decay and a.w_off[l] < fp.n_decay
+        for l in range(L + 1):
+            a.bias_off[l] = bias_off[l]
+        a.bias_total = bt
+        for i in range(L - 1):
+            a.drop[i] = float(drops[i])
+            a.seed_base[i] = int(seed_bases[i]) & ((1 << 64) - 1)
+        # transposed activations / gradients: [units][Bpad] bf16 per layer (offsets multiples of 8 elements)
+        ho, o = [], 0
+        for l in range(L):
+            ho.append(o)
+            o += n[l] * Bpad
+        do = [0]
+        for l in range(1, L + 1):
+            do.append(o)
+            o += n[l] * Bpad
+        self.T = torch.zeros(o, dtype=torch.bfloat16, device=dev)
+        for l in range(L):
+            a.h_off[l] = ho[l]
+        for l in range(1, L + 1):
+            a.d_off[l] = do[l]
+        a.hT = a.dT = self.T.data_ptr()
+        G1 = Bpad // ROWS
+        self.bpart = torch.zeros(G1 * (bt + 1), dtype=torch.float32, device=dev)
+        self.slab = torch.zeros(SPLIT * fp.n_decay, dtype=torch.float32, device=dev)
+        a.bpart, a.slab = self.bpart.data_ptr(), self.slab.data_ptr()
+        a.g = out_grad.data_ptr()
+        a.gsum = 0 if out_gsum is None else out_gsum.data_ptr()
+        # LDS: activation tiles 0..L-1, output-gradient tile, two gradient tiles, row weights (16-B aligned)
+        off = 0
+        for l in range(L):
+            a.lds_off[l] = off
+            off += ROWS * a.ld[l]
+        a.lds_off[L] = off
+        off += ROWS * a.ld[L]
+        gl = max([a.ld[l] for l in range(1, L)] or [8])
+        a.lds_g[0], a.lds_g[1] = off, off + ROWS * gl
+        off += 2 * ROWS * gl
+        a.lds_w = off * 2
+        self.lds = a.lds_w + ROWS * 4
+        ts = 0
+        for l in range(L):
+            a.tiles_i[l] = (n[l + 1] + 63) // 64
+            a.tiles_j[l] = (n[l] + 63) // 64
+            a.tile_start[l] = ts
+            ts += a.tiles_i[l] * a.tiles_j[l]
+        a.tile_start[L] = ts
+        a.n_decay, a.n_total = fp.n_decay, fp.p.numel()
+        self.args = a
+        self.scale_by_w = out_gsum is None
+        self._keep = (Z, w, y, shadow, step_dev, out_grad, out_gsum)
+
+    def step(self, ridx: torch.Tensor) -> None:
+        """One forward/backward of the rows ``ridx`` (int64; -1 = padding row) into the gradient buffer."""
+        a = self.args
+        a.ridx = ridx.data_ptr()
+        a.B = int(ridx.numel())
+        nat.check(self.lib.h2o_dl_step(ctypes.byref(a), self.lds, int(self.scale_by_w), nat.stream_ptr(ridx.device)),
+                  "dl_step")
+
+    def refresh_transposed(self) -> None:
+        nat.check(self.lib.h2o_dl_transpose(ctypes.byref(self.args), nat.stream_ptr(self.T.device)), "dl_transpose")

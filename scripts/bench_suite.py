@@ -83,6 +83,7 @@ def bench_dl(a, dev, world, rank):
                value=N * a.epochs / dt, unit="samples/s", n_gpus=world, seconds=dt, rows=N, cols=F, batch=a.batch,
                train_auc=m.output["training_metrics"]["AUC"], dtype="bf16", data="synthetic",
                step_mode=m.output.get("training_step_mode"), explicit=m.output.get("training_step_explicit"),
+               fused_mfma=m.output.get("training_step_fused_mfma"),
                phases=m.output.get("phase_seconds")))
 
 

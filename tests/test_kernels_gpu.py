@@ -380,3 +380,93 @@ def test_segment_sum_kernel_matches_index_add(n, idt, vdt):
     got = segment_sum(idx.to(dev), v.to(dev), n).cpu()
     ref = torch.zeros(n, dtype=torch.float64).index_add_(0, idx.long(), v.double())
     assert got.dtype == torch.float64 and torch.allclose(got, ref, rtol=1e-12, atol=1e-9)
+
+
+def _fused_case(n_in, hidden, K, act, drops, regression, B, seed=0):
+    """One fused MFMA step (csrc/dl_kernels.hip) and the fp32 autograd gradient of the same weighted loss
+    (weights and inputs rounded to bf16 like the kernels' operands; dropout masks from ops.dense._mask_ref)."""
+    from llama_github_io_amd.models.deeplearning import MLP
+    from llama_github_io_amd.ops import dl as dlops
+    from llama_github_io_amd.ops.dense import FlatParams, _act, _mask_ref, step_seed
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    actn = {1: "rectifier", 2: "tanh"}[act]
+    net = MLP(n_in, hidden, K, actn, False, 0.0, drops, "UniformAdaptive", 1.0, g).to(dev)
+    fp = FlatParams(net)
+    with torch.no_grad():
+        fp.p.add_(0.05 * torch.randn(fp.p.shape, generator=g).to(dev))   # non-trivial biases
+    N = 3 * B
+    Z = torch.randn(N, n_in, generator=g).to(dev).to(torch.bfloat16)
+    w = (torch.rand(N, generator=g) + 0.5).to(dev)
+    y = torch.randn(N, generator=g).to(dev) if regression else torch.randint(0, K, (N,), generator=g).to(dev)
+    ridx = torch.randperm(N, generator=g)[:B].to(dev)
+    shadow = fp.p[: fp.n_decay].to(torch.bfloat16)
+    step_t = torch.full((1,), 7, dtype=torch.int64, device=dev)
+    bases = [1234567 + 31 * i for i in range(len(hidden))]
+    fs = dlops.FusedMLPStep(fp, list(net.hidden) + [net.out], act, drops, bases, Z, w, y, regression, B, shadow,
+                            step_t, fp.g, None)
+    fs.refresh_transposed()
+    fp.g.zero_()
+    fs.step(ridx)
+    torch.cuda.synchronize()
+    got = fp.g.clone()
+    # fp32 autograd reference on the bf16-rounded operands
+    Ws = [shadow[(l_.weight.data_ptr() - fp.p.data_ptr()) // 4:][: l_.weight.numel()].float().view_as(l_.weight)
+          .clone().requires_grad_(True) for l_ in list(net.hidden) + [net.out]]
+    Bs = [l_.bias.detach().clone().requires_grad_(True) for l_ in list(net.hidden) + [net.out]]
+    h = Z[ridx].float()
+    for i in range(len(hidden)):
+        h = _act(act, h @ Ws[i].T + Bs[i])
+        if drops[i] > 0:
+            m = _mask_ref((B, hidden[i]), drops[i], step_seed(bases[i], 7), dev)
+            h = torch.where(m, h / (1 - drops[i]), torch.zeros_like(h))
+    o = h @ Ws[-1].T + Bs[-1]
+    wb = w[ridx]
+    if regression:
+        loss = (wb * 0.5 * (o[:, 0] - y[ridx]) ** 2).sum() / wb.sum()
+    else:
+        loss = (wb * torch.nn.functional.cross_entropy(o, y[ridx], reduction="none")).sum() / wb.sum()
+    loss.backward()
+    ref = torch.zeros_like(got)
+    for l_, Wg, Bg in zip(list(net.hidden) + [net.out], Ws, Bs):
+        ow = (l_.weight.data_ptr() - fp.p.data_ptr()) // 4
+        ob = (l_.bias.data_ptr() - fp.p.data_ptr()) // 4
+        ref[ow: ow + Wg.numel()] = Wg.grad.reshape(-1)
+        ref[ob: ob + Bg.numel()] = Bg.grad
+    # transposed shadow = transposed bf16 weights
+    for i, l_ in enumerate(list(net.hidden) + [net.out]):
+        ow = (l_.weight.data_ptr() - fp.p.data_ptr()) // 4
+        n_o, n_i = l_.weight.shape
+        assert torch.equal(fs.WT[ow: ow + n_o * n_i].view(n_i, n_o), shadow[ow: ow + n_o * n_i].view(n_o, n_i).T)
+    return got, ref
+
+
+@pytest.mark.parametrize("n_in,hidden,K,act,drops,regression,B", [
+    (784, [200, 200], 2, 1, [0.0, 0.0], False, 512),          # the BASELINE MLP shape
+    (37, [48, 24], 3, 2, [0.0, 0.0], False, 200),            # ragged widths: scalar loads, padding rows
+    (50, [64], 5, 1, [0.3], False, 256),                      # dropout (hash mask shared with the fwd/bwd kernels)
+    (20, [40, 16, 8], 1, 2, [0.1, 0.0, 0.2], True, 128),      # regression, 3 hidden layers
+])
+def test_dl_fused_step_matches_fp32_autograd(n_in, hidden, K, act, drops, regression, B):
+    got, ref = _fused_case(n_in, hidden, K, act, drops, regression, B)
+    rel = float((got - ref).norm() / ref.norm())
+    assert rel < 3e-2, rel
+    assert float(torch.nn.functional.cosine_similarity(got, ref, dim=0)) > 0.999
+
+
+def test_dl_trainer_uses_fused_step_and_learns(monkeypatch):
+    """The trainer's graph-chunked loop runs the fused MFMA step (no library GEMM in the loop) and reaches
+    the accuracy of the library-GEMM explicit step on the same data."""
+    from llama_github_io_amd.models.deeplearning import DeepLearningTrainer
+    g = torch.Generator(device=dev).manual_seed(1)
+    X = torch.rand(100, 60000, device=dev, generator=g)
+    y = (X[:10].sum(0) > 5).float()
+    res = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("H2O_DL_FUSED", flag)
+        m = DeepLearningTrainer(dict(hidden=[64, 64], epochs=2, compute_dtype="bf16", mini_batch_size=1024, seed=3,
+                                     stopping_rounds=0, score_interval=1e9, standardize=False)).fit(X, y, None, None,
+                                                                                                   _info(100))
+        res[flag] = m
+    assert res["1"].output["training_step_fused_mfma"] and not res["0"].output["training_step_fused_mfma"]
+    a1, a0 = res["1"].output["training_metrics"]["AUC"], res["0"].output["training_metrics"]["AUC"]
+    assert a1 > 0.9 and abs(a1 - a0) < 0.02, (a1, a0)
