@@ -5,7 +5,8 @@
 //   f[i] += leaf_value[leaf_of_row[i]]        (previous tree's contribution; optional)
 //   w_eff = w[i] * Bernoulli(sample_rate)     (row sampling, counter-based hash: no RNG state)
 //   z = negHalfGradient(y, f); num/den = gammaNum/gammaDenom
-//   aux[i] = (w_eff, w_eff*z, num, den) ; block max of |aux.x|, |aux.y| -> fixed-point scales
+//   aux[c][i] = (w_eff, w_eff*z, num, den) as four SoA planes (the histogram passes read only what they need)
+//   block maxima of the four |planes| -> fixed-point scales of the histograms and of the leaf sums
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -26,9 +27,9 @@ __device__ __forceinline__ float expc(float x) { return __expf(fminf(x, 80.f)); 
 __global__ __launch_bounds__(256) void k_gbm_step(
     long long N, long long row0, int dist, const float* __restrict__ y, const float* __restrict__ w, float* __restrict__ f,
     const float* __restrict__ vals, const int* __restrict__ leaf, float sample_rate, unsigned long long seed,
-    float p1 /*tweedie power | quantile alpha | huber delta*/, float4* __restrict__ aux,
-    unsigned* __restrict__ amax_bits /*[2*AMAX_SHARDS], |.| as uint bits, pre-zeroed*/) {
-  float ma = 0.f, mb = 0.f;
+    float p1 /*tweedie power | quantile alpha | huber delta*/, float* __restrict__ aux /*[4][N]*/,
+    unsigned* __restrict__ amax_bits /*[AMAX_SHARDS][4], |.| as uint bits, pre-zeroed*/) {
+  float ma = 0.f, mb = 0.f, mc = 0.f, md = 0.f;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += (long long)gridDim.x * blockDim.x) {
     float fi = f[i];
     if (vals) { fi += vals[leaf[i]]; f[i] = fi; }
@@ -78,26 +79,34 @@ __global__ __launch_bounds__(256) void k_gbm_step(
       }
       default: { z = yi - fi; num = wi * z; den = wi; }
     }
-    const float4 o = make_float4(wi, wi * z, num, den);
-    aux[i] = o;
-    ma = fmaxf(ma, fabsf(o.x));
-    mb = fmaxf(mb, fabsf(o.y));
+    const float wz = wi * z;
+    aux[i] = wi;
+    aux[N + i] = wz;
+    aux[2 * N + i] = num;
+    aux[3 * N + i] = den;
+    ma = fmaxf(ma, fabsf(wi));
+    mb = fmaxf(mb, fabsf(wz));
+    mc = fmaxf(mc, fabsf(num));
+    md = fmaxf(md, fabsf(den));
   }
-  // block max -> ONE atomic pair per block into one of AMAX_SHARDS shards (k_qscale folds the shards):
-  // a single hot word would serialize every wave's atomic (~12 ns each at the memory side)
+  // block max -> ONE atomic per component per block into one of AMAX_SHARDS shards (k_qscale folds the
+  // shards): a single hot word would serialize every wave's atomic (~12 ns each at the memory side)
   for (int off = 32; off > 0; off >>= 1) {
     ma = fmaxf(ma, __shfl_xor(ma, off, 64));
     mb = fmaxf(mb, __shfl_xor(mb, off, 64));
+    mc = fmaxf(mc, __shfl_xor(mc, off, 64));
+    md = fmaxf(md, __shfl_xor(md, off, 64));
   }
-  __shared__ float sm[2][4];
+  __shared__ float sm[4][4];
   const int wv = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) { sm[0][wv] = ma; sm[1][wv] = mb; }
+  if ((threadIdx.x & 63) == 0) { sm[0][wv] = ma; sm[1][wv] = mb; sm[2][wv] = mc; sm[3][wv] = md; }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int k = 1; k < (int)(blockDim.x >> 6); ++k) { ma = fmaxf(ma, sm[0][k]); mb = fmaxf(mb, sm[1][k]); }
-    unsigned* sh = amax_bits + 2 * (blockIdx.x & (AMAX_SHARDS - 1));
-    atomicMax(sh + 0, __float_as_uint(ma));   // non-negative floats order like their bit patterns
-    atomicMax(sh + 1, __float_as_uint(mb));
+  if (threadIdx.x < 4) {
+    const int c = threadIdx.x;
+    float v = sm[c][0];
+    for (int k = 1; k < (int)(blockDim.x >> 6); ++k) v = fmaxf(v, sm[c][k]);
+    // non-negative floats order like their bit patterns
+    atomicMax(amax_bits + 4 * (blockIdx.x & (AMAX_SHARDS - 1)) + c, __float_as_uint(v));
   }
 }
 
@@ -116,7 +125,7 @@ int h2o_gbm_step(long long N, long long row0, int dist, const void* y, const voi
   if (grid > 2048) grid = 2048;
   if (grid < 1) grid = 1;
   hipLaunchKernelGGL(k_gbm_step, dim3((unsigned)grid), dim3(blk), 0, s, N, row0, dist, (const float*)y, (const float*)w,
-                     (float*)f, (const float*)vals, (const int*)leaf, sample_rate, seed, p1, (float4*)aux,
+                     (float*)f, (const float*)vals, (const int*)leaf, sample_rate, seed, p1, (float*)aux,
                      (unsigned*)amax_bits);
   return (int)hipGetLastError();
 }

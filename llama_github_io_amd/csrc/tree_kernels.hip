@@ -237,10 +237,9 @@ struct RowFilter {
 // common row is then bfe + lshl_add + ds_add_u64 per feature (two atomics when not PACKED).
 template <bool FILT, bool PACKED>
 __device__ __forceinline__ void hist_rows(long long* h, float* nayy, const unsigned* __restrict__ bins32,
-                                          const float4* __restrict__ aux, int W, int wabs, int F, bool lead,
-                                          int r0, int r1, int g, int j, float& wyy, float sa, float sb, float sp,
-                                          const RowFilter& flt, int& lcnt) {
-  const float2* aux2 = (const float2*)aux;
+                                          const float* __restrict__ aw, const float* __restrict__ ay, int W, int wabs,
+                                          int F, bool lead, int r0, int r1, int g, int j, float& wyy, float sa,
+                                          float sb, float sp, const RowFilter& flt, int& lcnt) {
   const int lane = threadIdx.x & 63;
   const int rot = g & 1;
   int off[4], sh[4];
@@ -264,7 +263,8 @@ __device__ __forceinline__ void hist_rows(long long* h, float* nayy, const unsig
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
       const size_t row = (size_t)min(base + g + u * RPI, r1 - 1);
-      ab[u] = aux2[row * 2];
+      // SoA aux planes: wY always, w only when rows are weighted (aw == null: unit weights)
+      ab[u] = make_float2(aw ? aw[row] : 1.f, ay[row]);
       wd[u] = bins32[row * W + wc];
       if (FILT && flt.jw < 0) sbyte[u] = ((const uint8_t*)bins32)[row * W * 4 + flt.feat];
     }
@@ -322,7 +322,8 @@ __device__ __forceinline__ void hist_rows(long long* h, float* nayy, const unsig
 template <bool FILT, bool PACKED>
 __global__ __launch_bounds__(BLK) void k_hist_build(
     const uint8_t* __restrict__ bins, int stride /*bytes per row, multiple of 4*/,
-    const float4* __restrict__ aux, const Node* __restrict__ nodes, const int* __restrict__ tile_prefix,
+    const float* __restrict__ aw /*row weights or null (unit)*/, const float* __restrict__ ay /*w * Y*/,
+    const Node* __restrict__ nodes, const int* __restrict__ tile_prefix,
     const int* __restrict__ meta /*[0]=n_nodes [2]=n_build_tiles*/, int F, double* __restrict__ partials,
     int slot_doubles, const double* __restrict__ qs /*[sa, sb, 1/sa, 1/sb, sp, 1/sp]*/,
     const Dec* __restrict__ pdec, int* __restrict__ nl_out, int f32) {
@@ -393,8 +394,8 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
     }
     since += r1 - r0;
     float wf = 0.f;
-    hist_rows<FILT, PACKED>(h, nayy, bins32, aux, W, wabs, F, j == 0 && ftile == 0, r0, r1, g, j, wf, sa, sb, sp,
-                            flt, lcnt);
+    hist_rows<FILT, PACKED>(h, nayy, bins32, aw, ay, W, wabs, F, j == 0 && ftile == 0, r0, r1, g, j, wf, sa, sb,
+                            sp, flt, lcnt);
     wyy += (double)wf;
   }
   if (cur >= 0) flush();
@@ -956,29 +957,26 @@ __global__ void k_subtract(double* __restrict__ hist_next, const double* __restr
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_route: regroups the rows of an EVEN level e two levels down at once (TWO) and does the leaf
-// bookkeeping of every row that stops on the way. Rows are physically moved only every second level:
-// level e+1 is histogrammed by filtering the level-e ranges (k_hist_build<true>), so a depth-6 tree
-// moves its rows twice instead of five times and needs no separate counting pass.
+// k_route: regroups the rows of an EVEN level e two levels down at once. Rows are physically moved only
+// every second level: level e+1 is histogrammed by filtering the level-e ranges (k_hist_build<true>), so a
+// depth-6 tree moves its rows twice instead of five times and needs no separate counting pass.
 //   block = one TILE (2048 rows) of a level-e node; 8 waves x 256 rows, lane = row (4 rows per lane).
 //   Each row gets a slot q = 2*dirA + dirB (its grandchild); rows of a continuing grandchild move into
 //   the region of their level-(e+1) node: left grandchildren fill it from the front, right ones from the
-//   back (one atomic per (tile, slot) on curs); rows that reach a leaf write leaf_of_row (original row
-//   order, through ridx) and add their (gamma_num, gamma_den) to the leaf sums.
+//   back (one atomic per (tile, slot) on curs). Rows that reach a leaf on the way are simply not moved:
+//   leaf ids and leaf sums come from k_leaf_assign over the ORIGINAL row order after the last level, so the
+//   row payload is only the bins and the histogram inputs (wY, and w for weighted rows) — no row index.
 // Order inside a region is not preserved: histograms are fixed-point integer sums (order independent)
 // and nothing else depends on the row order within a node.
-// !TWO: route one level only (final pass of a tree whose last level is even). !MOVE: final pass, every
-// row lands on a leaf.
 #define LW 8              // waves per route block
 #define LROWS (TILE / LW) // rows per wave (256)
 #define LU (LROWS / 64)   // rows per lane (4)
 #define LMAXW 16          // max words (64 features) kept in registers per row on the fast path
 
-// NV > 0 (rows of NV x 16 B): each row is loaded ONCE into registers up front (with its aux and ridx),
-// split bytes are picked from those registers and the move stores them back — one HBM read per row
-// instead of two dependent byte loads plus the re-read of the row for the move.
+// NV > 0 (rows of NV x 16 B): each row is loaded ONCE into registers up front, split bytes are picked from
+// those registers and the move stores them back (one HBM read per row).
 __device__ __forceinline__ unsigned pick_word(uint4 v, int wi) {
-  // wi is block-uniform: a compare/select chain on values (no runtime-indexed register array -> no scratch)
+  // a compare/select chain on values (no runtime-indexed register array -> no scratch)
   unsigned r = v.x;
   r = wi == 1 ? v.y : r;
   r = wi == 2 ? v.z : r;
@@ -991,25 +989,23 @@ __device__ __forceinline__ int row_byte(uint4 v0, uint4 v1, int f) {
   return (w >> (8 * (f & 3))) & 0xFF;
 }
 __device__ __forceinline__ int row_byte4(uint4 v0, uint4 v1, uint4 v2, uint4 v3, int f) {
-  // rows of up to 64 B (NV = 3, 4): f is block-uniform, so the compare chain is uniform too
   return f < 32 ? row_byte(v0, v1, f) : row_byte(v2, v3, f - 32);
 }
 
-template <bool TWO, bool MOVE, int NV>
+template <int NV>
 __global__ __launch_bounds__(LW * 64) void k_route(
-    const uint8_t* __restrict__ sbins, const float4* __restrict__ saux, const int* __restrict__ sridx,
-    uint8_t* __restrict__ dbins, float4* __restrict__ daux, int* __restrict__ dridx, int stride,
+    const uint8_t* __restrict__ sbins, const float* __restrict__ say, const float* __restrict__ saw,
+    uint8_t* __restrict__ dbins, float* __restrict__ day, float* __restrict__ daw, int stride,
     const Node* __restrict__ nodesA, const int* __restrict__ tpA, const int* __restrict__ metaA,
     const Dec* __restrict__ decA, const int* __restrict__ clA, const int* __restrict__ crA,
     const Dec* __restrict__ decB, const int* __restrict__ clB, const int* __restrict__ crB,
-    int4* __restrict__ curs, int* __restrict__ leaf_of_row, double* __restrict__ leafsum) {
+    int4* __restrict__ curs) {
   const int n_nodes = metaA[0], n_tiles = metaA[1];
   const int t = blockIdx.x;
   if (t >= n_tiles) return;
   __shared__ Dec sA, sB[2];
-  __shared__ int sC[2], sG[4], sLeaf[4], sBase[4];
+  __shared__ int sC[2], sG[4], sBase[4];
   __shared__ int sCnt[LW][4];
-  __shared__ double sred[8][LW];
   const int node = find_node(tpA, n_nodes, t);
   const Node nd = nodesA[node];
   const int tin = t - tpA[node];
@@ -1020,45 +1016,36 @@ __global__ __launch_bounds__(LW * 64) void k_route(
   if (threadIdx.x < 2) sC[threadIdx.x] = threadIdx.x == 0 ? clA[node] : crA[node];
   __syncthreads();
   if (threadIdx.x < 4) {
-    // slot q -> grandchild (>= 0 continues) and leaf id (>= 0 when the slot ends in a leaf)
+    // slot q -> continuing grandchild (>= 0), else the row stops at a leaf
     const int q = threadIdx.x, c = sC[q >> 1];
-    int g = -1, leaf = -1;
-    if (c < 0) leaf = -1 - c;
-    else if (TWO) { g = (q & 1) ? crB[c] : clB[c]; if (g < 0) leaf = -1 - g; }
-    sG[q] = g; sLeaf[q] = leaf;
+    sG[q] = c < 0 ? -1 : ((q & 1) ? crB[c] : clB[c]);
   }
-  if (TWO) {
-    for (int k = 0; k < 2; ++k) {
-      const int c = sC[k];
-      if (c >= 0 && threadIdx.x < NI) ((int*)&sB[k])[threadIdx.x] = ((const int*)(decB + c))[threadIdx.x];
-    }
+  for (int k = 0; k < 2; ++k) {
+    const int c = sC[k];
+    if (c >= 0 && threadIdx.x < NI) ((int*)&sB[k])[threadIdx.x] = ((const int*)(decB + c))[threadIdx.x];
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int featA = sA.feat;
   const int wbase = r0 + wid * LROWS;
   const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  // 1. route every row; in-wave ranks per slot
   int q[LU], rank[LU];
   bool mv[LU];
   int cnt[4] = {0, 0, 0, 0};
-  // NV > 0: all of the tile's loads issued before any decision (rows clamped into the node: no divergence).
-  // Plain per-u scalars (not a 2-D array) so everything stays in VGPRs.
   uint4 rv0[LU], rv1[LU], rv2[LU], rv3[LU];
-  float4 ra[LU];
-  int rx[LU];
-  if (NV > 0) {
+  float ry[LU], rw[LU];
 #pragma unroll
-    for (int u = 0; u < LU; ++u) {
-      const int row = min(wbase + u * 64 + lane, r1 - 1);
+  for (int u = 0; u < LU; ++u) {
+    const int row = min(wbase + u * 64 + lane, r1 - 1);   // clamped into the node: no divergence
+    if (NV > 0) {
       const uint4* s4 = (const uint4*)(sbins + (size_t)row * stride);
       rv0[u] = s4[0];
       rv1[u] = NV > 1 ? s4[1] : make_uint4(0u, 0u, 0u, 0u);
       rv2[u] = NV > 2 ? s4[2] : make_uint4(0u, 0u, 0u, 0u);
       rv3[u] = NV > 3 ? s4[3] : make_uint4(0u, 0u, 0u, 0u);
-      ra[u] = saux[row];
-      rx[u] = sridx ? sridx[row] : row;
     }
+    ry[u] = say[row];
+    rw[u] = saw ? saw[row] : 1.f;
   }
 #pragma unroll
   for (int u = 0; u < LU; ++u) {
@@ -1068,7 +1055,7 @@ __global__ __launch_bounds__(LW * 64) void k_route(
     if (valid && featA >= 0)
       dA = dec_go_left(&sA, NV > 2 ? row_byte4(rv0[u], rv1[u], rv2[u], rv3[u], featA)
                                    : NV > 0 ? row_byte(rv0[u], rv1[u], featA) : sbins[(size_t)row * stride + featA]) ? 0 : 1;
-    if (TWO && valid && sC[dA] >= 0) {
+    if (valid && sC[dA] >= 0) {
       const Dec* b = &sB[dA];
       const int fb = b->feat;
       if (fb >= 0)
@@ -1076,7 +1063,7 @@ __global__ __launch_bounds__(LW * 64) void k_route(
                                    : NV > 0 ? row_byte(rv0[u], rv1[u], fb) : sbins[(size_t)row * stride + fb]) ? 0 : 1;
     }
     q[u] = 2 * dA + dB;
-    mv[u] = MOVE && valid && sG[q[u]] >= 0;
+    mv[u] = valid && sG[q[u]] >= 0;
     rank[u] = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -1086,62 +1073,46 @@ __global__ __launch_bounds__(LW * 64) void k_route(
       cnt[k] += __popcll(bm);
     }
   }
-  int off[4] = {0, 0, 0, 0};
-  if (MOVE) {
-    if (lane == 0) for (int k = 0; k < 4; ++k) sCnt[wid][k] = cnt[k];
-    __syncthreads();
-    if (threadIdx.x < 4) {
-      const int k = threadIdx.x;
-      int tot = 0;
-      for (int w = 0; w < LW; ++w) tot += sCnt[w][k];
-      int base = 0;
-      if (tot > 0) {
-        int4* cu = curs + sC[k >> 1];
-        base = (k & 1) ? atomicSub(&cu->y, tot) - tot : atomicAdd(&cu->x, tot);
-      }
-      sBase[k] = base;
+  if (lane == 0) for (int k = 0; k < 4; ++k) sCnt[wid][k] = cnt[k];
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    const int k = threadIdx.x;
+    int tot = 0;
+    for (int w = 0; w < LW; ++w) tot += sCnt[w][k];
+    int base = 0;
+    if (tot > 0) {
+      int4* cu = curs + sC[k >> 1];
+      base = (k & 1) ? atomicSub(&cu->y, tot) - tot : atomicAdd(&cu->x, tot);
     }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      off[k] = sBase[k];
-      for (int w = 0; w < wid; ++w) off[k] += sCnt[w][k];
-    }
+    sBase[k] = base;
   }
-  // 2. move continuing rows; leaf bookkeeping for rows that stop
-  double ls[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  int has_leaf = 0;
+  __syncthreads();
+  int off[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    off[k] = sBase[k];
+    for (int w = 0; w < wid; ++w) off[k] += sCnt[w][k];
+  }
   const int W = stride >> 2;
   const unsigned* sb32 = (const unsigned*)sbins;
   unsigned* db32 = (unsigned*)dbins;
 #pragma unroll
   for (int u = 0; u < LU; ++u) {
+    if (!mv[u]) continue;
     const int row = wbase + u * 64 + lane;
-    if (row >= r1) continue;
-    const float4 a = NV > 0 ? ra[u] : saux[row];
-    const int rr = NV > 0 ? rx[u] : (sridx ? sridx[row] : row);
-    if (mv[u]) {
-      int pos = rank[u];
+    int pos = rank[u];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) if (q[u] == k) pos += off[k];
+    for (int k = 0; k < 4; ++k) if (q[u] == k) pos += off[k];
+    unsigned* dst = db32 + (size_t)pos * W;
+    if (NV > 0) {
+      uint4* d4 = (uint4*)dst;
+      d4[0] = rv0[u];
+      if (NV > 1) d4[1] = rv1[u];
+      if (NV > 2) d4[2] = rv2[u];
+      if (NV > 3) d4[3] = rv3[u];
+    } else {
       const unsigned* src = sb32 + (size_t)row * W;
-      unsigned* dst = db32 + (size_t)pos * W;
-      if (NV > 0) {
-        uint4* d4 = (uint4*)dst;
-        d4[0] = rv0[u];
-        if (NV > 1) d4[1] = rv1[u];
-        if (NV > 2) d4[2] = rv2[u];
-        if (NV > 3) d4[3] = rv3[u];
-      } else if ((stride & 15) == 0 && stride <= 64) {      // 16-B aligned rows: vector copy
-        const uint4* s4 = (const uint4*)src;
-        uint4* d4 = (uint4*)dst;
-        const int nv = stride >> 4;
-        uint4 v[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) if (k < nv) v[k] = s4[k];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) if (k < nv) d4[k] = v[k];
-      } else if (W <= LMAXW) {
+      if (W <= LMAXW) {
         unsigned v[LMAXW];
 #pragma unroll
         for (int k = 0; k < LMAXW; ++k) if (k < W) v[k] = src[k];
@@ -1150,29 +1121,85 @@ __global__ __launch_bounds__(LW * 64) void k_route(
       } else {
         for (int k = 0; k < W; ++k) dst[k] = src[k];
       }
-      daux[pos] = a;
-      dridx[pos] = rr;
-    } else {
-      int leaf = -1;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) if (q[u] == k) { leaf = sLeaf[k]; ls[2 * k] += a.z; ls[2 * k + 1] += a.w; }
-      if (leaf >= 0) leaf_of_row[rr] = leaf;
-      has_leaf = 1;
     }
+    day[pos] = ry[u];
+    if (daw) daw[pos] = rw[u];
   }
-  // 3. leaf sums: wave -> block -> one atomic pair per (tile, leaf)
-  if (__syncthreads_or(has_leaf)) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) ls[k] = wave_sum_d(ls[k]);
-    if (lane == 0) for (int k = 0; k < 8; ++k) sred[k][wid] = ls[k];
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_leaf_assign: after the last level, every row walks the tree from the root in ORIGINAL row order
+// (master bins, coalesced) to its leaf: leaf_of_row[row] and the per-leaf Newton sums (gamma numerator /
+// denominator planes) as int64 fixed point (scales from k_qscale; sums are exact and order independent ->
+// deterministic). Small leaf sets are privatised in LDS per block, larger ones add to global int64 slots.
+// GBM.java fitBestConstants / AddTreeContributions consume these sums.
+#define LEAF_LDS_MAX 2048   // leaves privatised in LDS (2 x 8 B each = 32 KB)
+struct LevelPtrs { const Dec* dec; const int* cl; const int* cr; };
+
+template <int NV>
+__global__ __launch_bounds__(256) void k_leaf_assign(
+    const uint8_t* __restrict__ bins, int stride, long long N, const LevelPtrs* __restrict__ lv, int D,
+    const float* __restrict__ an, const float* __restrict__ ad, const double* __restrict__ qs,
+    int* __restrict__ leaf_of_row, unsigned long long* __restrict__ leafq, int leaf_cap) {
+  __shared__ unsigned long long sq[2 * LEAF_LDS_MAX];
+  const bool lds = leaf_cap <= LEAF_LDS_MAX;
+  if (lds) {
+    for (int i = threadIdx.x; i < 2 * leaf_cap; i += blockDim.x) sq[i] = 0ull;
     __syncthreads();
-    if (threadIdx.x < 4) {
-      const int k = threadIdx.x, leaf = sLeaf[k];
-      double vn = 0, vd = 0;
-      for (int w = 0; w < LW; ++w) { vn += sred[2 * k][w]; vd += sred[2 * k + 1][w]; }
-      if (leaf >= 0 && (vn != 0.0 || vd != 0.0)) { atomicAdd(leafsum + 2 * leaf, vn); atomicAdd(leafsum + 2 * leaf + 1, vd); }
+  }
+  const float sn = (float)qs[6], sd = (float)qs[7];
+  for (long long row = (long long)blockIdx.x * blockDim.x + threadIdx.x; row < N;
+       row += (long long)gridDim.x * blockDim.x) {
+    uint4 v0 = make_uint4(0u, 0u, 0u, 0u), v1 = v0, v2 = v0, v3 = v0;
+    if (NV > 0) {
+      const uint4* s4 = (const uint4*)(bins + (size_t)row * stride);
+      v0 = s4[0];
+      if (NV > 1) v1 = s4[1];
+      if (NV > 2) v2 = s4[2];
+      if (NV > 3) v3 = s4[3];
+    }
+    int i = 0, leaf = 0;
+    for (int d = 0; d < D; ++d) {
+      const Dec* dc = lv[d].dec + i;
+      const int f = dc->feat;
+      int c;
+      if (f < 0) {
+        c = lv[d].cl[i];                         // terminal node: child_l == child_r == its leaf
+      } else {
+        const int b = NV > 2 ? row_byte4(v0, v1, v2, v3, f) : NV > 0 ? row_byte(v0, v1, f)
+                                                                     : bins[(size_t)row * stride + f];
+        c = dec_go_left(dc, b) ? lv[d].cl[i] : lv[d].cr[i];
+      }
+      if (c < 0) { leaf = -1 - c; break; }
+      i = c;
+    }
+    leaf_of_row[row] = leaf;
+    const long long qn = (long long)(an[row] * sn), qd = (long long)(ad[row] * sd);
+    if (lds) {
+      if (qn) atomicAdd(sq + 2 * leaf, (unsigned long long)qn);
+      if (qd) atomicAdd(sq + 2 * leaf + 1, (unsigned long long)qd);
+    } else {
+      if (qn) atomicAdd(leafq + 2 * leaf, (unsigned long long)qn);
+      if (qd) atomicAdd(leafq + 2 * leaf + 1, (unsigned long long)qd);
     }
   }
+  if (lds) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < 2 * leaf_cap; i += blockDim.x)
+      if (sq[i]) atomicAdd(leafq + i, sq[i]);
+  }
+}
+
+// fixed-point leaf sums -> fp64 leafsum[L][2] (and, with leafval, the closed-form Newton leaf values of
+// k_leaf_values); also re-zeroes the fixed-point slots for the next tree
+__global__ void k_leafsum_finish(unsigned long long* __restrict__ leafq, const double* __restrict__ qs, int n,
+                                 double* __restrict__ leafsum) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  leafsum[2 * i] = (double)(long long)leafq[2 * i] * qs[8];
+  leafsum[2 * i + 1] = (double)(long long)leafq[2 * i + 1] * qs[9];
+  leafq[2 * i] = 0ull;
+  leafq[2 * i + 1] = 0ull;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1237,57 +1264,68 @@ __global__ void k_predict(const float* __restrict__ X, long long N, int K,
 }
 
 // ------------------------------------------------------------------------------------------------
-// Fixed-point scales of the int64 LDS histograms: max |aux.x|, |aux.y| -> qs = [2^40/max, .., max/2^40, ..]
-__global__ __launch_bounds__(256) void k_amax(const float4* __restrict__ aux, long long N, unsigned* __restrict__ amax_bits) {
-  float ma = 0.f, mb = 0.f;
+// Fixed-point scales: max |w|, |wY| (int64 LDS histograms) and max |num|, |den| (int64 leaf sums) of the SoA
+// aux planes aux[c * N + i] -> AMAX_SHARDS x 4 shard maxima (uint bits of non-negative floats)
+__global__ __launch_bounds__(256) void k_amax(const float* __restrict__ aux, long long N, unsigned* __restrict__ amax_bits) {
+  float m[4] = {0.f, 0.f, 0.f, 0.f};
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += (long long)gridDim.x * blockDim.x) {
-    const float2 v = *(const float2*)(aux + i);
-    ma = fmaxf(ma, fabsf(v.x));
-    mb = fmaxf(mb, fabsf(v.y));
+#pragma unroll
+    for (int c = 0; c < 4; ++c) m[c] = fmaxf(m[c], fabsf(aux[(size_t)c * N + i]));
   }
-  for (int off = 32; off > 0; off >>= 1) {
-    ma = fmaxf(ma, __shfl_xor(ma, off, 64));
-    mb = fmaxf(mb, __shfl_xor(mb, off, 64));
-  }
-  __shared__ float sm[2][4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+    for (int off = 32; off > 0; off >>= 1) m[c] = fmaxf(m[c], __shfl_xor(m[c], off, 64));
+  __shared__ float sm[4][4];
   const int wv = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) { sm[0][wv] = ma; sm[1][wv] = mb; }
+  if ((threadIdx.x & 63) == 0) for (int c = 0; c < 4; ++c) sm[c][wv] = m[c];
   __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int k = 1; k < (int)(blockDim.x >> 6); ++k) { ma = fmaxf(ma, sm[0][k]); mb = fmaxf(mb, sm[1][k]); }
-    unsigned* sh = amax_bits + 2 * (blockIdx.x & (AMAX_SHARDS - 1));
-    atomicMax(sh + 0, __float_as_uint(ma));
-    atomicMax(sh + 1, __float_as_uint(mb));
+  if (threadIdx.x < 4) {
+    const int c = threadIdx.x;
+    float v = sm[c][0];
+    for (int k = 1; k < (int)(blockDim.x >> 6); ++k) v = fmaxf(v, sm[c][k]);
+    atomicMax(amax_bits + 4 * (blockIdx.x & (AMAX_SHARDS - 1)) + c, __float_as_uint(v));
   }
 }
 
-// folds the AMAX_SHARDS per-shard maxima, then derives the fixed-point scales. Also the tree's
-// start-of-build reset (one launch instead of three fills): leaf counters, leaf sums, and the amax
-// shards themselves once read (the next tree's fused step re-fills them).
+// folds the AMAX_SHARDS per-shard maxima, then derives the fixed-point scales
+//   qs = [sa, sb, 1/sa, 1/sb, sp, 1/sp, sn, sd, 1/sn, 1/sd]
+// sa, sb: 2^40 / max (per-block int64 LDS histograms); sp: 2^30 / max|wY| (packed count|wY);
+// sn, sd: 2^lb / max with 2^lb * N < 2^62 (whole-tree int64 leaf sums cannot overflow).
+// Also the tree's start-of-build reset: leaf counters and the amax shards themselves once read (the next
+// tree's fused step re-fills them).
 __global__ __launch_bounds__(256) void k_qscale(unsigned* __restrict__ amax_bits, double* __restrict__ qs,
-                                                int* __restrict__ counters, double* __restrict__ leafsum,
-                                                int n_leafsum) {
-  __shared__ unsigned sm[2];
-  if (threadIdx.x < 2) {
+                                                int* __restrict__ counters, long long N) {
+  __shared__ unsigned sm[4];
+  if (threadIdx.x < 4) {
     unsigned mbits = 0u;
-    for (int k = 0; k < AMAX_SHARDS; ++k) mbits = max(mbits, amax_bits[2 * k + threadIdx.x]);
+    for (int k = 0; k < AMAX_SHARDS; ++k) mbits = max(mbits, amax_bits[4 * k + threadIdx.x]);
     sm[threadIdx.x] = mbits;
   }
   __syncthreads();
-  if (threadIdx.x < 2) {
-    const double m = (double)__uint_as_float(sm[threadIdx.x]);
-    const double sc = (m > 0.0 && m == m) ? 1099511627776.0 / m : 1.0;   // 2^40 / max
-    qs[threadIdx.x] = sc;
-    qs[2 + threadIdx.x] = 1.0 / sc;
-    if (threadIdx.x == 1) {                                                // packed wY: 2^30 / max
-      const double sp = (m > 0.0 && m == m) ? 1073741824.0 / m : 1.0;
-      qs[4] = sp;
-      qs[5] = 1.0 / sp;
+  if (threadIdx.x < 4) {
+    const int c = threadIdx.x;
+    const double m = (double)__uint_as_float(sm[c]);
+    const bool ok = m > 0.0 && m == m && m < 1e300;
+    if (c < 2) {
+      const double sc = ok ? 1099511627776.0 / m : 1.0;   // 2^40 / max
+      qs[c] = sc;
+      qs[2 + c] = 1.0 / sc;
+      if (c == 1) {                                        // packed wY: 2^30 / max
+        const double sp = ok ? 1073741824.0 / m : 1.0;
+        qs[4] = sp;
+        qs[5] = 1.0 / sp;
+      }
+    } else {
+      int lb = 61;
+      for (long long n = N; n > 0; n >>= 1) --lb;          // 2^lb * N < 2^62
+      if (lb < 8) lb = 8;
+      const double sc = ok ? ldexp(1.0, lb) / m : 1.0;
+      qs[6 + (c - 2)] = sc;
+      qs[8 + (c - 2)] = 1.0 / sc;
     }
   }
-  for (int i = threadIdx.x; i < 2 * AMAX_SHARDS; i += blockDim.x) amax_bits[i] = 0u;
+  for (int i = threadIdx.x; i < 4 * AMAX_SHARDS; i += blockDim.x) amax_bits[i] = 0u;
   if (counters && threadIdx.x < 4) counters[threadIdx.x] = 0;
-  if (leafsum) for (int i = threadIdx.x; i < n_leafsum; i += blockDim.x) leafsum[i] = 0.0;
 }
 
 // Leaf values of the GBM distributions with a closed-form Newton step (GBM.java fitBestConstants):
@@ -1311,17 +1349,19 @@ __global__ void k_leaf_values(const double* __restrict__ leafsum, int n, int log
 // ================================================================================================
 // C ABI launchers (called through ctypes with raw device pointers and the current HIP stream).
 template <bool PACKED>
-static void launch_hist(dim3 grid, size_t lds, hipStream_t s, const void* bins, int stride, const void* aux,
-                        const void* nodes, const void* tile_prefix, const void* meta, int F, void* partials,
-                        int slot_doubles, const void* qs, const void* pdec, void* nl_out, int f32) {
+static void launch_hist(dim3 grid, size_t lds, hipStream_t s, const void* bins, int stride, const void* aw,
+                        const void* ay, const void* nodes, const void* tile_prefix, const void* meta, int F,
+                        void* partials, int slot_doubles, const void* qs, const void* pdec, void* nl_out, int f32) {
   if (pdec)
     hipLaunchKernelGGL((k_hist_build<true, PACKED>), grid, dim3(BLK), lds, s, (const uint8_t*)bins, stride,
-                       (const float4*)aux, (const Node*)nodes, (const int*)tile_prefix, (const int*)meta, F,
-                       (double*)partials, slot_doubles, (const double*)qs, (const Dec*)pdec, (int*)nl_out, f32);
+                       (const float*)aw, (const float*)ay, (const Node*)nodes, (const int*)tile_prefix,
+                       (const int*)meta, F, (double*)partials, slot_doubles, (const double*)qs, (const Dec*)pdec,
+                       (int*)nl_out, f32);
   else
     hipLaunchKernelGGL((k_hist_build<false, PACKED>), grid, dim3(BLK), lds, s, (const uint8_t*)bins, stride,
-                       (const float4*)aux, (const Node*)nodes, (const int*)tile_prefix, (const int*)meta, F,
-                       (double*)partials, slot_doubles, (const double*)qs, (const Dec*)nullptr, (int*)nullptr, f32);
+                       (const float*)aw, (const float*)ay, (const Node*)nodes, (const int*)tile_prefix,
+                       (const int*)meta, F, (double*)partials, slot_doubles, (const double*)qs, (const Dec*)nullptr,
+                       (int*)nullptr, f32);
 }
 
 extern "C" {
@@ -1337,15 +1377,15 @@ int h2o_tree_sizes(int* out) {
 }
 
 // partials: >= (grid + max nodes of the level) slots of slot_doubles
-int h2o_hist_build(const void* bins, int stride, const void* aux, const void* nodes, const void* tile_prefix,
-                   const void* meta, int F, void* partials, int slot_doubles, const void* qs, int grid, int packed,
-                   const void* pdec, void* nl_out, int f32, hipStream_t s) {
+int h2o_hist_build(const void* bins, int stride, const void* aw, const void* ay, const void* nodes,
+                   const void* tile_prefix, const void* meta, int F, void* partials, int slot_doubles, const void* qs,
+                   int grid, int packed, const void* pdec, void* nl_out, int f32, hipStream_t s) {
   const int nft = (F + FTILE - 1) / FTILE;
   // packed mode needs one int64 plane (66 KB): two 16-wave blocks share a CU (32 waves, 8 per SIMD)
   const size_t lds = (packed ? HIST_LDS_BYTES - HPLANE * 8 : HIST_LDS_BYTES) + 64 * 8;
   const dim3 gr(grid, nft);
-  if (packed) launch_hist<true>(gr, lds, s, bins, stride, aux, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out, f32);
-  else launch_hist<false>(gr, lds, s, bins, stride, aux, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out, f32);
+  if (packed) launch_hist<true>(gr, lds, s, bins, stride, aw, ay, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out, f32);
+  else launch_hist<false>(gr, lds, s, bins, stride, aw, ay, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out, f32);
   return (int)hipGetLastError();
 }
 
@@ -1440,27 +1480,52 @@ static bool route_generic() {   // H2O_ROUTE_GENERIC=1: byte-load path (A/B meas
   return v == 1;
 }
 
-// two: route two levels (else one); move: regroup continuing rows into the destination buffers
-int h2o_route(const void* sbins, const void* saux, const void* sridx, void* dbins, void* daux, void* dridx,
-              int stride, const void* nodesA, const void* tpA, const void* metaA, const void* decA, const void* clA,
-              const void* crA, const void* decB, const void* clB, const void* crB, void* curs, void* leaf_of_row,
-              void* leafsum, int two, int move, int tiles_cap, hipStream_t s) {
-#define ROUTE_ARGS (const uint8_t*)sbins, (const float4*)saux, (const int*)sridx, (uint8_t*)dbins, (float4*)daux, \
-    (int*)dridx, stride, (const Node*)nodesA, (const int*)tpA, (const int*)metaA, (const Dec*)decA,          \
-    (const int*)clA, (const int*)crA, (const Dec*)decB, (const int*)clB, (const int*)crB, (int4*)curs,       \
-    (int*)leaf_of_row, (double*)leafsum
-#define ROUTE_LAUNCH(NV)                                                                                   \
-  if (two && move) hipLaunchKernelGGL((k_route<true, true, NV>), dim3(tiles_cap), dim3(LW * 64), 0, s, ROUTE_ARGS); \
-  else if (two) hipLaunchKernelGGL((k_route<true, false, NV>), dim3(tiles_cap), dim3(LW * 64), 0, s, ROUTE_ARGS); \
-  else if (!move) hipLaunchKernelGGL((k_route<false, false, NV>), dim3(tiles_cap), dim3(LW * 64), 0, s, ROUTE_ARGS); \
-  else return (int)hipErrorInvalidValue;  /* moving after a single level is never needed */
-  if (stride == 64 && !route_generic()) { ROUTE_LAUNCH(4) }
-  else if (stride == 48 && !route_generic()) { ROUTE_LAUNCH(3) }
-  else if (stride == 32 && !route_generic()) { ROUTE_LAUNCH(2) }
-  else if (stride == 16 && !route_generic()) { ROUTE_LAUNCH(1) }
-  else { ROUTE_LAUNCH(0) }
+static int nv_of(int stride) {
+  if (route_generic()) return 0;
+  return stride == 64 ? 4 : stride == 48 ? 3 : stride == 32 ? 2 : stride == 16 ? 1 : 0;
+}
+
+// regroup an even level two levels down (moving bins + wY (+ w) of continuing rows)
+int h2o_route(const void* sbins, const void* say, const void* saw, void* dbins, void* day, void* daw, int stride,
+              const void* nodesA, const void* tpA, const void* metaA, const void* decA, const void* clA,
+              const void* crA, const void* decB, const void* clB, const void* crB, void* curs, int tiles_cap,
+              hipStream_t s) {
+#define ROUTE_LAUNCH(NV)                                                                                       \
+  hipLaunchKernelGGL((k_route<NV>), dim3(tiles_cap), dim3(LW * 64), 0, s, (const uint8_t*)sbins,              \
+                     (const float*)say, (const float*)saw, (uint8_t*)dbins, (float*)day, (float*)daw, stride,  \
+                     (const Node*)nodesA, (const int*)tpA, (const int*)metaA, (const Dec*)decA, (const int*)clA, \
+                     (const int*)crA, (const Dec*)decB, (const int*)clB, (const int*)crB, (int4*)curs)
+  switch (nv_of(stride)) {
+    case 4: ROUTE_LAUNCH(4); break;
+    case 3: ROUTE_LAUNCH(3); break;
+    case 2: ROUTE_LAUNCH(2); break;
+    case 1: ROUTE_LAUNCH(1); break;
+    default: ROUTE_LAUNCH(0);
+  }
 #undef ROUTE_LAUNCH
-#undef ROUTE_ARGS
+  return (int)hipGetLastError();
+}
+
+// leaf id of every row (original order) + fixed-point leaf sums -> fp64 leafsum[leaf_cap][2]
+int h2o_leaf_assign(const void* master, int stride, long long N, const void* lvptrs, int D, const void* an,
+                    const void* ad, const void* qs, void* leaf_of_row, void* leafq, int leaf_cap, void* leafsum,
+                    hipStream_t s) {
+  long long grid = (N + 255) / 256;
+  if (grid > 2048) grid = 2048;
+  if (grid < 1) grid = 1;
+#define LA(NV) hipLaunchKernelGGL((k_leaf_assign<NV>), dim3((unsigned)grid), dim3(256), 0, s, (const uint8_t*)master, \
+                                  stride, N, (const LevelPtrs*)lvptrs, D, (const float*)an, (const float*)ad,          \
+                                  (const double*)qs, (int*)leaf_of_row, (unsigned long long*)leafq, leaf_cap)
+  switch (nv_of(stride)) {
+    case 4: LA(4); break;
+    case 3: LA(3); break;
+    case 2: LA(2); break;
+    case 1: LA(1); break;
+    default: LA(0);
+  }
+#undef LA
+  hipLaunchKernelGGL(k_leafsum_finish, dim3((leaf_cap + 255) / 256), dim3(256), 0, s, (unsigned long long*)leafq,
+                     (const double*)qs, leaf_cap, (double*)leafsum);
   return (int)hipGetLastError();
 }
 
@@ -1468,13 +1533,12 @@ int h2o_amax(const void* aux, long long N, void* amax_bits, hipStream_t s) {
   long long grid = (N + 255) / 256;
   if (grid > 2048) grid = 2048;
   if (grid < 1) grid = 1;
-  hipLaunchKernelGGL(k_amax, dim3((unsigned)grid), dim3(256), 0, s, (const float4*)aux, N, (unsigned*)amax_bits);
+  hipLaunchKernelGGL(k_amax, dim3((unsigned)grid), dim3(256), 0, s, (const float*)aux, N, (unsigned*)amax_bits);
   return (int)hipGetLastError();
 }
 
-int h2o_qscale(void* amax_bits, void* qs, void* counters, void* leafsum, int n_leafsum, hipStream_t s) {
-  hipLaunchKernelGGL(k_qscale, dim3(1), dim3(256), 0, s, (unsigned*)amax_bits, (double*)qs, (int*)counters,
-                     (double*)leafsum, n_leafsum);
+int h2o_qscale(void* amax_bits, void* qs, void* counters, long long N, hipStream_t s) {
+  hipLaunchKernelGGL(k_qscale, dim3(1), dim3(256), 0, s, (unsigned*)amax_bits, (double*)qs, (int*)counters, N);
   return (int)hipGetLastError();
 }
 
@@ -1502,19 +1566,20 @@ int h2o_predict(const void* X, long long N, int K, const void* feat, const void*
 
 
 // ================================================================================================
-// Native per-tree launch sequence. The same order of launches as GpuTreeBuilder.build's Python loop,
-// issued from C++ so a tree costs a handful of host calls instead of ~45 ctypes round trips (at
-// 1.375M rows/GPU the Python launch loop alone took ~370 us/tree and left the GPU 18 % idle).
-// Row-sharded runs stop at each collective: h2o_tree_level returns after the level's compact
-// histogram is reduced into hbuild; the caller all-reduces it and continues with h2o_tree_subtract.
+// Native per-tree launch sequence: a tree costs a handful of host calls instead of ~45 ctypes round trips
+// (at 1.375M rows/GPU the Python launch loop alone took ~370 us/tree and left the GPU 18 % idle).
+// Row-sharded runs stop at each collective: h2o_tree_level returns after the level's compact histogram is
+// reduced into hbuild; the caller all-reduces it and continues with h2o_tree_subtract.
+// Aux planes are SoA (aux[c * N + i]: 0 = w (null-able: unit weights), 1 = wY, 2 = gamma numerator,
+// 3 = gamma denominator); the routed ping-pong buffers carry bins + wY (+ w).
 #define TP_MAXL 65
 struct TreePlan {
   long long N;
-  int stride, F, D, slot, used, pf32, grid, leaf_cap, mode, random_split, pad0;
+  int stride, F, D, slot, used, pf32, grid, leaf_cap, mode, random_split, unit;
   double min_w, msi, lam, alpha, gamma;
   void *master, *partials, *hist0, *hist1, *hbuild, *cand, *scratch, *nbins_f, *iscat_f, *mono_f;
-  void *qs, *leafsum, *leaf_of_row, *counters, *rootw, *leafval;
-  void *bb[2], *ba[2], *br[2];
+  void *qs, *leafsum, *leaf_of_row, *counters, *rootw, *leafval, *leafq, *lvptrs;
+  void *bb[2], *by[2], *bw[2];
   void *nodes[TP_MAXL], *meta[TP_MAXL], *tp[TP_MAXL], *bp[TP_MAXL], *dec[TP_MAXL], *cl[TP_MAXL], *cr[TP_MAXL],
       *nl[TP_MAXL], *cur[TP_MAXL];
   int caps[TP_MAXL], tiles_cap[TP_MAXL];
@@ -1532,20 +1597,22 @@ struct TreePlan {
   void* ic[TP_MAXL];       // per level [caps][F] allowed-feature masks (ic[0] = the root's)
 };
 
-static inline void tp_level_buf(const TreePlan* P, int e, const void*& b, const void*& a, const void*& r) {
-  if (e == 0) { b = P->master; a = P->aux; r = nullptr; return; }
+static inline const float* tp_aux(const TreePlan* P, int c) { return (const float*)P->aux + (size_t)c * P->N; }
+
+// level e's row buffers: the master order (e == 0) or ping-pong buffer (e/2 - 1) % 2
+static inline void tp_level_buf(const TreePlan* P, int e, const void*& b, const void*& y, const void*& w) {
+  if (e == 0) { b = P->master; y = tp_aux(P, 1); w = P->unit ? nullptr : tp_aux(P, 0); return; }
   const int i = (e / 2 - 1) % 2;
-  b = P->bb[i]; a = P->ba[i]; r = P->br[i];
+  b = P->bb[i]; y = P->by[i]; w = P->unit ? nullptr : P->bw[i];
 }
 
-static int tp_route(const TreePlan* P, int e, int two, int move, hipStream_t s) {
-  const void *sb, *sa, *sr;
-  tp_level_buf(P, e, sb, sa, sr);
+static int tp_route(const TreePlan* P, int e, hipStream_t s) {
+  const void *sb, *sy, *sw;
+  tp_level_buf(P, e, sb, sy, sw);
   const int di = (e / 2) % 2;
-  const int b1 = two ? e + 1 : e;
-  return h2o_route(sb, sa, sr, P->bb[di], P->ba[di], P->br[di], P->stride, P->nodes[e], P->tp[e], P->meta[e],
-                   P->dec[e], P->cl[e], P->cr[e], P->dec[b1], P->cl[b1], P->cr[b1], P->cur[b1], P->leaf_of_row,
-                   P->leafsum, two, move, P->tiles_cap[e], s);
+  return h2o_route(sb, sy, sw, P->bb[di], P->by[di], P->unit ? nullptr : P->bw[di], P->stride, P->nodes[e], P->tp[e],
+                   P->meta[e], P->dec[e], P->cl[e], P->cr[e], P->dec[e + 1], P->cl[e + 1], P->cr[e + 1],
+                   P->cur[e + 1], P->tiles_cap[e], s);
 }
 
 #define TP_CHECK(x) do { int rc_ = (x); if (rc_) return rc_; } while (0)
@@ -1556,15 +1623,15 @@ int h2o_tree_plan_size() { return (int)sizeof(TreePlan); }
 int h2o_tree_root(const TreePlan* P, hipStream_t s) {
   if (P->D >= TP_MAXL - 1) return (int)hipErrorInvalidValue;
   if (P->compute_amax) TP_CHECK(h2o_amax(P->aux, P->N, P->amax_bits, s));
-  TP_CHECK(h2o_qscale(P->amax_bits, P->qs, P->counters, P->leafsum, P->leaf_cap * 2, s));
+  TP_CHECK(h2o_qscale(P->amax_bits, P->qs, P->counters, P->N, s));
   const int g0 = P->tiles_cap[0] < P->grid ? P->tiles_cap[0] : P->grid;
-  TP_CHECK(h2o_hist_build(P->master, P->stride, P->aux, P->nodes[0], P->bp[0], P->meta[0], P->F, P->partials,
-                          P->slot, P->qs, g0, P->packed, nullptr, nullptr, P->pf32, s));
+  TP_CHECK(h2o_hist_build(P->master, P->stride, P->unit ? nullptr : tp_aux(P, 0), tp_aux(P, 1), P->nodes[0], P->bp[0],
+                          P->meta[0], P->F, P->partials, P->slot, P->qs, g0, P->packed, nullptr, nullptr, P->pf32, s));
   return h2o_hist_reduce(P->partials, P->slot, P->used, P->nodes[0], P->bp[0], P->meta[0], 1, g0, P->hist0,
                          nullptr, nullptr, P->pf32, s);
 }
 
-// one level: split search + plan, then the next level's histogram (or the final routing).
+// one level: split search + plan, then the next level's histogram.
 // returns 0 = histogram done (dist: compact buffer ready for the all-reduce), 1 = last level, <0 error.
 int h2o_tree_level(const TreePlan* P, int d, int dist, hipStream_t s) {
   void* hc = (d % 2) ? P->hist1 : P->hist0;
@@ -1588,27 +1655,25 @@ int h2o_tree_level(const TreePlan* P, int d, int dist, hipStream_t s) {
                      P->caps[d + 1], s);
     if (rc) return -rc;
   }
-  if (d + 1 == P->D) {
-    rc = tp_route(P, odd ? d - 1 : d, odd ? 1 : 0, 0, s);
-    return rc ? -rc : 1;
-  }
+  if (d + 1 == P->D) return 1;             // every row's leaf: h2o_tree_leaves over the original order
   int gh;
+  const void *sb, *sy, *sw;
   if (!odd) {
+    // level d+1 (odd) is histogrammed straight from level d's ranges, filtered by level d's decisions
     gh = P->tiles_cap[d] < P->grid ? P->tiles_cap[d] : P->grid;
-    const void *sb, *sa, *sr;
-    tp_level_buf(P, d, sb, sa, sr);
-    rc = h2o_hist_build(sb, P->stride, sa, P->nodes[d + 1], P->bp[d + 1], P->meta[d + 1], P->F, P->partials, P->slot,
-                        P->qs, gh, P->packed, P->dec[d], P->nl[d], P->pf32, s);
+    tp_level_buf(P, d, sb, sy, sw);
+    rc = h2o_hist_build(sb, P->stride, sw, sy, P->nodes[d + 1], P->bp[d + 1], P->meta[d + 1], P->F, P->partials,
+                        P->slot, P->qs, gh, P->packed, P->dec[d], P->nl[d], P->pf32, s);
   } else {
-    rc = tp_route(P, d - 1, 1, 1, s);
+    // regroup level d-1's rows two levels down, then histogram level d+1 (even) contiguously
+    rc = tp_route(P, d - 1, s);
     if (rc) return -rc;
     rc = h2o_ranges(P->nodes[d + 1], P->cur[d], P->tp[d + 1], P->bp[d + 1], P->meta[d + 1], s);
     if (rc) return -rc;
     gh = P->tiles_cap[d + 1] < P->grid ? P->tiles_cap[d + 1] : P->grid;
-    const void *sb, *sa, *sr;
-    tp_level_buf(P, d + 1, sb, sa, sr);
-    rc = h2o_hist_build(sb, P->stride, sa, P->nodes[d + 1], P->bp[d + 1], P->meta[d + 1], P->F, P->partials, P->slot,
-                        P->qs, gh, P->packed, nullptr, nullptr, P->pf32, s);
+    tp_level_buf(P, d + 1, sb, sy, sw);
+    rc = h2o_hist_build(sb, P->stride, sw, sy, P->nodes[d + 1], P->bp[d + 1], P->meta[d + 1], P->F, P->partials,
+                        P->slot, P->qs, gh, P->packed, nullptr, nullptr, P->pf32, s);
   }
   if (rc) return -rc;
   if (!dist)
@@ -1627,6 +1692,12 @@ int h2o_tree_subtract(const TreePlan* P, int d, hipStream_t s) {
   return h2o_subtract(hn, hc, P->hbuild, P->nodes[d + 1], P->meta[d + 1], P->caps[d + 1], P->slot, s);
 }
 
+// after the last level: leaf_of_row (original order) + fp64 leaf sums (the caller all-reduces them when sharded)
+int h2o_tree_leaves(const TreePlan* P, hipStream_t s) {
+  return h2o_leaf_assign(P->master, P->stride, P->N, P->lvptrs, P->D, tp_aux(P, 2), tp_aux(P, 3), P->qs,
+                         P->leaf_of_row, P->leafq, P->leaf_cap, P->leafsum, s);
+}
+
 // single process: the whole tree (root .. leaves) in one host call
 int h2o_tree_all(const TreePlan* P, hipStream_t s) {
   TP_CHECK(h2o_tree_root(P, s));
@@ -1635,6 +1706,7 @@ int h2o_tree_all(const TreePlan* P, hipStream_t s) {
     if (r < 0) return -r;
     if (r == 1) break;
   }
+  TP_CHECK(h2o_tree_leaves(P, s));
   if (P->leaf_native)
     return h2o_leaf_values(P->leafsum, P->leaf_cap, P->log_link, P->scale, P->kclamp, P->mx, P->leafval, s);
   return 0;

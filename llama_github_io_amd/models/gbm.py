@@ -130,7 +130,18 @@ class GBMTrainer(SharedTreeTrainer):
         self.f = torch.tensor(init, dtype=torch.float32, device=dev).repeat(N, 1).contiguous()
         if self.offset is not None:
             self.f += self.offset[:, None]
-        self.aux = torch.empty(N, 4, dtype=torch.float32, device=dev)
+        # fused path: the step kernel writes four SoA planes [4, N] (w, wY, gamma num, gamma den); the torch
+        # path builds [N, 4] rows
+        self.aux = (torch.empty(4, N, dtype=torch.float32, device=dev) if self._fused()
+                    else torch.empty(N, 4, dtype=torch.float32, device=dev))
+
+    def _aux_soa(self):
+        return self._fused()
+
+    def _unit_weights(self):
+        # no user weights and no row sampling: every w is exactly 1, the histogram passes skip the w plane
+        return (self._fused() and getattr(self, "_wbuf", None) is None and self.p.get("weights_column") is None
+                and float(self.p["sample_rate"]) >= 1.0 and not getattr(self, "_y_has_nan", True))
 
     def _lr(self, t):
         return float(self.p["learn_rate"]) * float(self.p["learn_rate_annealing"]) ** t
@@ -150,8 +161,9 @@ class GBMTrainer(SharedTreeTrainer):
             # one HIP pass: previous tree's f update + sampling + residuals + leaf terms + scale maxima
             from ..ops import _native as nat
             if not hasattr(self, "_amax"):
-                self._amax = torch.zeros(2 * T.AMAX_SHARDS, dtype=torch.int32, device=self.dev)
+                self._amax = torch.zeros(4 * T.AMAX_SHARDS, dtype=torch.int32, device=self.dev)
                 self._wbuf = None if self.w is None or bool((self.w == 1).all()) else self.w.contiguous()
+                self._y_has_nan = bool(torch.isnan(self.y).any())
             pv, pl = self._pending if getattr(self, "_pending", None) is not None else (None, None)
             p1 = {"tweedie": self.p["tweedie_power"], "quantile": self.p["quantile_alpha"],
                   "huber": getattr(self.dist, "huber_delta", 1.0)}.get(self.dname, 0.0)
@@ -227,7 +239,8 @@ class GBMTrainer(SharedTreeTrainer):
         self._flush_pending()
         leaf = self.builder.leaf_of_row.long()
         diff = (self.y - self.f[:, k]).double()
-        w = (self.aux[:, 0] if self.w_eff is None else self.w_eff).double()
+        a0 = self.aux[0] if self.aux.shape[0] == 4 and self.aux.shape[1] == self.N else self.aux[:, 0]
+        w = (a0 if self.w_eff is None else self.w_eff).double()
         if coll.is_dist():
             # per-leaf weighted order statistics need every row of the leaf: gather (leaf, residual, weight)
             # from the shards (leaf ids are global: every rank built the same tree)

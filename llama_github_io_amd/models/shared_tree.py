@@ -133,6 +133,14 @@ class SharedTreeTrainer:
         self.p = p
 
     # ---- hooks
+    def _aux_soa(self) -> bool:
+        """The trainer's _prepare returns the row statistics as [4, N] planes (else [N, 4] rows)."""
+        return False
+
+    def _unit_weights(self) -> bool:
+        """Every row weight of the current tree is exactly 1 (no weights, no row sampling)."""
+        return False
+
     def _binning_sample(self) -> int:
         """Rows of the quantile-edge sample (fit_binning); subclasses needing exact edges raise it."""
         return 1 << 20
@@ -266,6 +274,8 @@ class SharedTreeTrainer:
                     kw["amax_bits"] = am
                 if self.dev.type == "cuda":
                     kw["packed"] = self._hist_packed()
+                    kw["soa"] = aux.dim() == 2 and aux.shape[0] == 4 and aux.shape[1] == self.N and self._aux_soa()
+                    kw["unit"] = self._unit_weights()
                     ln = self._leaf_native(t, k)
                     if ln is not None:
                         kw["leaf_native"] = ln

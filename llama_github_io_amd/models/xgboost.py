@@ -199,7 +199,9 @@ class XGBoostTrainer(SharedTreeTrainer):
         if K > 1:
             self.yk = torch.nn.functional.one_hot(torch.nan_to_num(self.y, nan=0).long(), K).float()
         self.yok = ~torch.isnan(self.y)
-        self.aux = torch.empty(N, 4, dtype=torch.float32, device=dev)
+        # [4, N] planes on the device (the histogram passes stream only the hessian / gradient planes)
+        self.aux = (torch.empty(4, N, dtype=torch.float32, device=dev) if dev.type == "cuda"
+                    else torch.empty(N, 4, dtype=torch.float32, device=dev))
         self.dart = model.output["booster"] == "dart"
         self.tree_rows = []   # dart: per tree (k, vals, leaf)
         self.tree_w = []
@@ -240,11 +242,20 @@ class XGBoostTrainer(SharedTreeTrainer):
         y = torch.nan_to_num(self.yk[:, k] if self.K > 1 else self.y, nan=0.0)
         g, h = grad_hess(self.obj, y, self.f[:, k], k, getattr(self, "probs", None), float(self.p["tweedie_power"]))
         a = self.aux
-        a[:, 0] = self.ws * h
-        a[:, 1] = -self.ws * g
-        a[:, 2] = -self.ws * g
-        a[:, 3] = self.ws * h
+        if self._aux_soa():
+            torch.mul(self.ws, h, out=a[0])
+            torch.mul(self.ws, g, out=a[1]).neg_()
+            a[2].copy_(a[1])
+            a[3].copy_(a[0])
+        else:
+            a[:, 0] = self.ws * h
+            a[:, 1] = -self.ws * g
+            a[:, 2] = -self.ws * g
+            a[:, 3] = self.ws * h
         return a
+
+    def _aux_soa(self):
+        return self.dev.type == "cuda"
 
     def _leaf_values(self, ls, t, k):
         p = self.p

@@ -393,12 +393,12 @@ class _TreePlan(ctypes.Structure):
     """Mirror of ``TreePlan`` in ``csrc/tree_kernels.hip`` (native per-tree launch sequence)."""
     _fields_ = ([("N", ctypes.c_longlong)] +
                 [(n, _ci) for n in ("stride", "F", "D", "slot", "used", "pf32", "grid", "leaf_cap", "mode",
-                                    "random_split", "pad0")] +
+                                    "random_split", "unit")] +
                 [(n, _cd) for n in ("min_w", "msi", "lam", "alpha", "gamma")] +
                 [(n, _vp) for n in ("master", "partials", "hist0", "hist1", "hbuild", "cand", "scratch", "nbins_f",
                                     "iscat_f", "mono_f", "qs", "leafsum", "leaf_of_row", "counters", "rootw",
-                                    "leafval")] +
-                [(n, _vp * 2) for n in ("bb", "ba", "br")] +
+                                    "leafval", "leafq", "lvptrs")] +
+                [(n, _vp * 2) for n in ("bb", "by", "bw")] +
                 [(n, _vp * _MAXL) for n in ("nodes", "meta", "tp", "bp", "dec", "cl", "cr", "nl", "cur")] +
                 [("caps", _ci * _MAXL), ("tiles_cap", _ci * _MAXL)] +
                 [(n, _vp) for n in ("aux", "amax_bits", "feat_ok")] +
@@ -423,7 +423,13 @@ class _Arena:
 
 
 class GpuTreeBuilder:
-    """Drives the HIP tree kernels. ``bins`` is a CUDA uint8 tensor [N, stride] (stride % 4 == 0)."""
+    """Drives the HIP tree kernels. ``bins`` is a CUDA uint8 tensor [N, stride] (stride % 4 == 0).
+
+    Row statistics arrive as four planes (``aux`` [4, N] with ``soa=True``, or the [N, 4] row-major form of
+    the CPU reference, transposed here): w, wY (histograms), gamma numerator / denominator (leaf sums).
+    The routed row payload is the bins plus wY (plus w unless ``unit``: every row weight is exactly 1); the
+    leaf of every row and the leaf sums come from one pass over the ORIGINAL row order after the last level
+    (k_leaf_assign), so rows carry no index and stop moving once they reach a leaf."""
 
     def __init__(self, bins: torch.Tensor, F: int, nbins_f, iscat_f, mono_f, max_depth: int, params: SplitParams,
                  node_cap: int = 1 << 14, grid: int = 256):
@@ -440,6 +446,8 @@ class GpuTreeBuilder:
         assert self.stride % 4 == 0
         self.F = F
         self.D = D = max(1, int(max_depth))
+        if D >= _MAXL - 1:
+            raise ValueError(f"max_depth {D} exceeds the native tree plan ({_MAXL - 2})")
         self.p = params
         self.grid = int(os.environ.get("H2O_HIST_GRID", grid))
         grid = self.grid
@@ -466,17 +474,18 @@ class GpuTreeBuilder:
         self.scratch = torch.empty(2 * capmax + 16, dtype=torch.int32, device=dev)
         self.leaf_cap = min(N + 1, 2 * sum(self.caps) + 2)
         self.leafsum = torch.zeros(self.leaf_cap, 2, dtype=torch.float64, device=dev)
+        self.leafq = torch.zeros(self.leaf_cap * 2, dtype=torch.int64, device=dev)   # fixed-point leaf sums
         self.leaf_of_row = torch.empty(N, dtype=torch.int32, device=dev)
         self.nbins_f = torch.as_tensor(np.asarray(nbins_f, dtype=np.int32), device=dev)
         self.iscat_f = torch.as_tensor(np.asarray(iscat_f, dtype=np.int32), device=dev)
         self.mono_f = None if mono_f is None else torch.as_tensor(np.asarray(mono_f, dtype=np.int32), device=dev)
         self.feat_ok_all = torch.ones(F, dtype=torch.int32, device=dev)
-        self.qs = torch.empty(8, dtype=torch.float64, device=dev)   # fixed-point scales [sa, sb, 1/sa, 1/sb, sp, 1/sp]
-        self.amax_bits = torch.zeros(2 * AMAX_SHARDS, dtype=torch.int32, device=dev)
-        # ping-pong row payload buffers
+        self.qs = torch.zeros(16, dtype=torch.float64, device=dev)  # fixed-point scales (k_qscale)
+        self.amax_bits = torch.zeros(4 * AMAX_SHARDS, dtype=torch.int32, device=dev)
+        self._soa = None                       # [4, N] staging of row-major aux input
+        # ping-pong row payload buffers: bins + wY (+ w for weighted rows, allocated on first use)
         self.bufs = [dict(bins=torch.empty(N, self.stride, dtype=torch.uint8, device=dev),
-                          aux=torch.empty(N, 4, dtype=torch.float32, device=dev),
-                          ridx=torch.empty(N, dtype=torch.int32, device=dev)) for _ in range(2)]
+                          y=torch.empty(N, dtype=torch.float32, device=dev), w=None) for _ in range(2)]
         # small per-level arrays in one arena
         ar = _Arena()
         for d in range(D + 1):
@@ -513,10 +522,11 @@ class GpuTreeBuilder:
         # raw device pointers resolved once: the per-tree launch sequence is ~45 ctypes calls and at small
         # shards (1.375M rows/GPU) the host loop, not the GPU, set the pace (82 % busy, rocprofv3 trace)
         self._pt = {name: t.data_ptr() for name, t in self.av.items()}
+        # per-level (dec, cl, cr) pointers for the leaf traversal (k_leaf_assign)
+        self.lvptrs = torch.tensor([[self._pt[f"dec{d}"], self._pt[f"cl{d}"], self._pt[f"cr{d}"]] for d in range(D)],
+                                   dtype=torch.int64).reshape(-1).to(dev)
         self.ic_map = None
         self._hp = [h.data_ptr() for h in self.hist]
-        self._bp = [dict(bins=b["bins"].data_ptr(), aux=b["aux"].data_ptr(), ridx=b["ridx"].data_ptr())
-                    for b in self.bufs]
 
     def _p(self, name):
         return self._pt[name]
@@ -542,8 +552,6 @@ class GpuTreeBuilder:
 
     def _make_plan(self):
         """Static part of the native launch plan (pointers / shapes fixed for the builder's lifetime)."""
-        if self.D >= _MAXL - 1 or os.environ.get("H2O_TREE_PYLAUNCH") == "1":
-            return None
         assert self.lib.h2o_tree_plan_size() == ctypes.sizeof(_TreePlan), "TreePlan layout mismatch"
         P = _TreePlan()
         p = self.p
@@ -556,9 +564,11 @@ class GpuTreeBuilder:
         P.nbins_f, P.iscat_f = self.nbins_f.data_ptr(), self.iscat_f.data_ptr()
         P.mono_f = 0 if self.mono_f is None else self.mono_f.data_ptr()
         P.qs, P.leafsum, P.leaf_of_row = self.qs.data_ptr(), self.leafsum.data_ptr(), self.leaf_of_row.data_ptr()
+        P.leafq, P.lvptrs = self.leafq.data_ptr(), self.lvptrs.data_ptr()
         P.counters, P.rootw, P.leafval = self._p("counters"), self._p("rootw"), self._p("leafval")
         for i in range(2):
-            P.bb[i], P.ba[i], P.br[i] = self._bp[i]["bins"], self._bp[i]["aux"], self._bp[i]["ridx"]
+            P.bb[i], P.by[i] = self.bufs[i]["bins"].data_ptr(), self.bufs[i]["y"].data_ptr()
+            P.bw[i] = 0
         for d in range(self.D + 1):
             for n in ("nodes", "meta", "tp", "bp", "dec", "cl", "cr", "nl", "cur"):
                 getattr(P, n)[d] = self._p(f"{n}{d}")
@@ -576,151 +586,47 @@ class GpuTreeBuilder:
             self._edges_dev = torch.as_tensor(np.asarray(self.p.edges, dtype=np.float32), device=self.master.device).contiguous()
         return self._edges_dev.data_ptr()
 
+    def _planes(self, aux: torch.Tensor, soa: bool) -> torch.Tensor:
+        """[4, N] float32 planes of the row statistics (row-major [N, 4] input is transposed once)."""
+        if soa:
+            assert aux.shape == (4, self.N) and aux.dtype == torch.float32 and aux.is_contiguous()
+            return aux
+        assert aux.shape == (self.N, 4) and aux.dtype == torch.float32
+        if self._soa is None:
+            self._soa = torch.empty(4, self.N, dtype=torch.float32, device=self.dev)
+        self._soa.copy_(aux.t())
+        return self._soa
+
     def build(self, aux_static: torch.Tensor, feat_ok: torch.Tensor | None = None, k_cols: int = 0, seed: int = 0,
-              leaf_fn=None, amax_bits: torch.Tensor | None = None, packed: bool = False, leaf_native=None):
-        """Launch one tree. ``leaf_fn(leafsum[L,2] f64) -> leaf values f32`` runs on device before the
-        arena snapshot, so values travel to the host with the structure (no extra sync);
-        ``leaf_native = (log_link, scale, kclamp, max_abs)`` instead computes closed-form Newton leaf values
-        in one HIP launch (k_leaf_values).
-        ``amax_bits`` (int32[2*AMAX_SHARDS], max |aux.x|, |aux.y| as float bits) may be produced by a fused
-        prepare kernel; otherwise it is computed here (k_qscale re-zeroes it after reading). ``packed``
-        (caller guarantees aux.x is a 0/1 or small integer row weight) switches the LDS histograms to one
-        packed count|wY atomic per (row, feature)."""
-        pk = int(bool(packed))
-        lib, s = self.lib, nat.stream_ptr(self.dev)
+              leaf_fn=None, amax_bits: torch.Tensor | None = None, packed: bool = False, leaf_native=None,
+              soa: bool = False, unit: bool = False):
+        """Launch one tree (one host call single-process; one per collective segment row-sharded).
+        ``leaf_fn(leafsum[L,2] f64) -> leaf values f32`` runs on device before the arena snapshot, so values
+        travel to the host with the structure (no extra sync); ``leaf_native = (log_link, scale, kclamp,
+        max_abs)`` instead computes closed-form Newton leaf values in one HIP launch (k_leaf_values).
+        ``amax_bits`` (int32[4*AMAX_SHARDS], max |plane| as float bits) may be produced by a fused prepare
+        kernel; otherwise it is computed here. ``packed`` (caller guarantees w is a 0/1 or small integer row
+        weight) switches the LDS histograms to one packed count|wY atomic per (row, feature); ``unit``
+        (every w is exactly 1) drops w from the row payload altogether."""
         if not hasattr(self, "_plan"):
             self._plan = self._make_plan()
-        if self._plan is not None:
-            return self._build_native(aux_static, feat_ok, k_cols, seed, leaf_fn, amax_bits, pk, leaf_native, s)
-        F, D, p, T = self.F, self.D, self.p, self.TILE
-        assert aux_static.shape == (self.N, 4) and aux_static.dtype == torch.float32 and aux_static.is_contiguous()
-        fo = self.feat_ok_all if feat_ok is None else feat_ok
-        slot, used, part = self.slot, self.used, self.partials.data_ptr()
-        dist = coll.is_dist()
-        # per-tree fixed-point scales for the int64 LDS histograms (|v| * 2^40 / max|v| <= 2^40); the same
-        # launch resets the leaf counters, the leaf sums and the amax shards
-        if amax_bits is None:
-            amax_bits = self.amax_bits
-            nat.check(lib.h2o_amax(aux_static.data_ptr(), self.N, amax_bits.data_ptr(), s), "amax")
-        nat.check(lib.h2o_qscale(amax_bits.data_ptr(), self.qs.data_ptr(), self._p("counters"),
-                                 self.leafsum.data_ptr(), self.leafsum.numel(), s), "qscale")
-        qs = self.qs.data_ptr()
-        hgrid = self.grid * (self.hist_bpc if pk else 1)
-        g0 = min(self.tiles_cap[0], hgrid)
-        nat.check(lib.h2o_hist_build(self.master.data_ptr(), self.stride, aux_static.data_ptr(), self._p("nodes0"),
-                                     self._p("bp0"), self._p("meta0"), F, part, slot, qs, g0, pk, 0, 0, self.pf32, s),
-                  "hist_build")
-        nat.check(lib.h2o_hist_reduce(part, slot, used, self._p("nodes0"), self._p("bp0"), self._p("meta0"), 1, g0,
-                                      self.hist[0].data_ptr(), 0, 0, self.pf32, s), "hist_reduce")
-        coll.all_reduce_(self.hist[0][:slot])
-        mono = 0 if self.mono_f is None else self.mono_f.data_ptr()
-        seed = int(seed) & _M64
-        hb = self.hbuild
-
-        master_p, aux_p = self.master.data_ptr(), aux_static.data_ptr()
-
-        def level_buf(e):
-            # rows are regrouped every second level: level e (even) lives in the master order (e == 0)
-            # or in ping-pong buffer (e/2 - 1) % 2
-            if e == 0:
-                return master_p, aux_p, 0
-            b = self._bp[(e // 2 - 1) % 2]
-            return b["bins"], b["aux"], b["ridx"]
-
-        def route(e, two, move):
-            sb, sa, sr = level_buf(e)
-            dst = self._bp[(e // 2) % 2]
-            b1 = e + 1 if two else e
-            nat.check(lib.h2o_route(sb, sa, sr, dst["bins"], dst["aux"], dst["ridx"],
-                                    self.stride, self._p(f"nodes{e}"), self._p(f"tp{e}"), self._p(f"meta{e}"),
-                                    self._p(f"dec{e}"), self._p(f"cl{e}"), self._p(f"cr{e}"), self._p(f"dec{b1}"),
-                                    self._p(f"cl{b1}"), self._p(f"cr{b1}"), self._p(f"cur{b1}"),
-                                    self.leaf_of_row.data_ptr(), self.leafsum.data_ptr(), int(two), int(move),
-                                    self.tiles_cap[e], s), "route")
-
-        hc_p = self._hp
-        cand_p, nb_p, ic_p, fo_p = self.cand.data_ptr(), self.nbins_f.data_ptr(), self.iscat_f.data_ptr(), fo.data_ptr()
-        for d in range(D):
-            hc, hn = self.hist[d % 2], self.hist[(d + 1) % 2]
-            hcp, hnp = hc_p[d % 2], hc_p[(d + 1) % 2]
-            cap = self.caps[d]
-            odd = d % 2 == 1
-            nat.check(lib.h2o_split_find(hcp, slot, self._p(f"meta{d}"), cap, F, nb_p,
-                                         ic_p, mono, p.min_w, p.min_split_improvement, p.lam,
-                                         p.alpha, p.gamma, p.mode, int(p.random_split), seed, d,
-                                         cand_p, self._p("rootw") if d == 0 else 0, self._edges_ptr(),
-                                         p.adapt_nb(d) if self._edges_ptr() else 0, s), "split_find")
-            ic_d = 0 if self.ic_map is None else self.ic_lv[d].data_ptr()
-            nat.check(lib.h2o_split_reduce(cand_p, self._p(f"meta{d}"), cap, F, fo_p, _level_k(k_cols, d),
-                                           seed, d, self._p(f"dec{d}"), ic_d, s), "split_reduce")
-            nat.check(lib.h2o_plan(self._p(f"nodes{d}"), self._p(f"meta{d}"), self._p(f"dec{d}"), self._p(f"nl{d}"),
-                                   self._p(f"nl{d - 1}") if odd else 0, self._p(f"cur{d}"), self._p(f"cl{d}"),
-                                   self._p(f"cr{d}"), self._p(f"nodes{d + 1}"), self._p(f"tp{d + 1}"),
-                                   self._p(f"meta{d + 1}"), self._p(f"bp{d + 1}"), self._p("counters"),
-                                   self.scratch.data_ptr(), d, D, p.min_w, self.caps[d + 1], self.leaf_cap, s), "plan")
-            if self.ic_map is not None and d + 1 < D:
-                nat.check(lib.h2o_ic_next(self._p(f"nodes{d + 1}"), self._p(f"meta{d + 1}"), self._p(f"dec{d}"), ic_d,
-                                          self.ic_map.data_ptr(), F, self.ic_lv[d + 1].data_ptr(), self.caps[d + 1], s),
-                          "ic_next")
-            if d + 1 == D:
-                # last level: every row lands on a leaf (routed from the last regrouped level)
-                route(d - 1 if odd else d, two=odd, move=False)
-                break
-            if not odd:
-                # level d+1 (odd) is histogrammed straight from level d's ranges, filtered by level d's
-                # decisions; the pass also counts each parent's left-goers for the next regrouping
-                gh = min(self.tiles_cap[d], hgrid)
-                sb, sa, _ = level_buf(d)
-                nat.check(lib.h2o_hist_build(sb, self.stride, sa, self._p(f"nodes{d + 1}"), self._p(f"bp{d + 1}"),
-                                             self._p(f"meta{d + 1}"), F, part, slot, qs, gh, pk,
-                                             self._p(f"dec{d}"), self._p(f"nl{d}"), self.pf32, s), "hist_build")
-            else:
-                # regroup level d-1's rows two levels down, then histogram level d+1 (even) contiguously
-                route(d - 1, two=True, move=True)
-                nat.check(lib.h2o_ranges(self._p(f"nodes{d + 1}"), self._p(f"cur{d}"), self._p(f"tp{d + 1}"),
-                                         self._p(f"bp{d + 1}"), self._p(f"meta{d + 1}"), s), "ranges")
-                gh = min(self.tiles_cap[d + 1], hgrid)
-                sb, sa, _ = level_buf(d + 1)
-                nat.check(lib.h2o_hist_build(sb, self.stride, sa, self._p(f"nodes{d + 1}"), self._p(f"bp{d + 1}"),
-                                             self._p(f"meta{d + 1}"), F, part, slot, qs, gh, pk, 0, 0, self.pf32, s),
-                          "hist_build")
-            if not dist:
-                # single process: partial sums + sibling subtraction in one pass, straight into hist_next
-                nat.check(lib.h2o_hist_reduce(part, slot, used, self._p(f"nodes{d + 1}"), self._p(f"bp{d + 1}"),
-                                              self._p(f"meta{d + 1}"), self.caps[d + 1], gh, 0, hnp,
-                                              hcp, self.pf32, s), "hist_reduce")
-            else:
-                # row-sharded: one built child per parent into the compact buffer (<= caps[d] slots), the
-                # only histogram bytes all-reduced per level, then the sibling subtraction
-                nat.check(lib.h2o_hist_reduce(part, slot, used, self._p(f"nodes{d + 1}"), self._p(f"bp{d + 1}"),
-                                              self._p(f"meta{d + 1}"), self.caps[d + 1], gh, hb.data_ptr(), 0, 0,
-                                              self.pf32, s), "hist_reduce")
-                coll.all_reduce_(hb[: self.caps[d] * slot])
-                nat.check(lib.h2o_subtract(hn.data_ptr(), hc.data_ptr(), hb.data_ptr(), self._p(f"nodes{d + 1}"),
-                                           self._p(f"meta{d + 1}"), self.caps[d + 1], slot, s), "subtract")
-        coll.all_reduce_(self.leafsum)
-        if leaf_native is not None:
-            lg, scale, kclamp, mx = leaf_native
-            nat.check(lib.h2o_leaf_values(self.leafsum.data_ptr(), self.leaf_cap, int(lg), float(scale), float(kclamp),
-                                          float(mx), self._p("leafval"), s), "leaf_values")
-        elif leaf_fn is not None:
-            vals = leaf_fn(self.leafsum)
-            self.av["leafval"].view(torch.float32)[: vals.numel()].copy_(vals.to(torch.float32))
-        return self._snapshot()
-
-    def _build_native(self, aux_static, feat_ok, k_cols, seed, leaf_fn, amax_bits, pk, leaf_native, s):
-        """build() through the native launch plan: one host call per tree (single process) or one per
-        collective segment (row-sharded)."""
-        assert aux_static.shape == (self.N, 4) and aux_static.dtype == torch.float32 and aux_static.is_contiguous()
+        planes = self._planes(aux_static, soa)
         lib, P = self.lib, self._plan
-        P.aux = aux_static.data_ptr()
+        s = nat.stream_ptr(self.dev)
+        P.aux = planes.data_ptr()
+        P.unit = int(bool(unit))
+        if not unit:
+            for i in range(2):
+                if self.bufs[i]["w"] is None:
+                    self.bufs[i]["w"] = torch.empty(self.N, dtype=torch.float32, device=self.dev)
+                P.bw[i] = self.bufs[i]["w"].data_ptr()
         P.compute_amax = int(amax_bits is None)
         P.amax_bits = (self.amax_bits if amax_bits is None else amax_bits).data_ptr()
         P.feat_ok = (self.feat_ok_all if feat_ok is None else feat_ok).data_ptr()
-        P.k_cols, P.packed, P.seed = _level_k(k_cols, 0), pk, int(seed) & _M64
+        P.k_cols, P.packed, P.seed = _level_k(k_cols, 0), int(bool(packed)), int(seed) & _M64
         for d in range(_MAXL):
             P.kc_level[d] = _level_k(k_cols, d) if isinstance(k_cols, (list, tuple)) else 0
-        P.grid = self.grid * (self.hist_bpc if pk else 1)
+        P.grid = self.grid * (self.hist_bpc if packed else 1)
         P.leaf_native = int(leaf_native is not None)
         if leaf_native is not None:
             lg, scale, kclamp, mx = leaf_native
@@ -739,6 +645,7 @@ class GpuTreeBuilder:
                     break
                 coll.all_reduce_(self.hbuild[: self.caps[d] * self.slot])
                 nat.check(lib.h2o_tree_subtract(ref, d, s), "tree_subtract")
+            nat.check(lib.h2o_tree_leaves(ref, s), "tree_leaves")
             coll.all_reduce_(self.leafsum)
             if leaf_native is not None:
                 nat.check(lib.h2o_leaf_values(self.leafsum.data_ptr(), self.leaf_cap, P.log_link, P.scale, P.kclamp,
