@@ -44,7 +44,6 @@ UNSUPPORTED = {
                        "remove_collinear_columns", "startval", "p_values_threshold", "gradient_epsilon",
                        "objective_epsilon", "early_stopping", "plug_values"},
     "glrm": {"expand_user_y"},
-    "word2vec": {"word_model"},
     "rulefit": {"max_categorical_levels"},
     "infogram": {"max_iterations"},
 }

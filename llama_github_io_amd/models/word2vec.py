@@ -1,6 +1,6 @@
 """Word2Vec (reference: ``hex/word2vec/Word2Vec.java``, ``Word2VecModel.java``, ``WordVectorTrainer.java``).
 
-Skip-gram with hierarchical softmax (H2O's only ``norm_model``): vocabulary from the training
+Skip-gram or CBOW (``word_model``) with hierarchical softmax (H2O's only ``norm_model``): vocabulary from the training
 string column (NA rows separate sentences), words below ``min_word_freq`` dropped, frequent words
 sub-sampled with ``sent_sample_rate``, a Huffman tree over counts gives each word its path
 (inner-node ids + binary codes). Training is batched on device: (center, context) pairs of a
@@ -121,6 +121,9 @@ class Word2VecModel(Model):
         self.vectors = torch.tensor(s["vectors"], dtype=torch.float32)
 
 
+MAX_EXP = 6.0   # WordVectorTrainer.MAX_EXP: dot products beyond +-6 skip the update (saturated sigmoid)
+
+
 class Word2VecTrainer:
     def __init__(self, params):
         p = dict(W2V_DEFAULTS)
@@ -152,6 +155,68 @@ class Word2VecTrainer:
         m.output["vec_size"] = V.shape[1]
         m.output["vocab_size"] = len(words)
         return m
+
+    def _cbow_epoch(self, ids, counts, total, ss, win, rng, gen, syn0, syn1, P_idx, P_code, P_mask, lr0, B, step,
+                    n_steps_est, epochs, dev):
+        """One CBOW epoch (WordVectorTrainer.map / CBOW / hierarchicalSoftmaxCBOW), batched on the device:
+        every center word's context bag (random window shrink b <= window_size, sentence-bounded) is
+        averaged into neu1, the center's Huffman path is trained against neu1 (updates skipped where
+        |neu1 . syn1| >= MAX_EXP), and the accumulated error neu1e is added to the input vectors of the
+        context words the reference updates: its hidden -> in loop runs over window slots
+        [b, window_size] only, i.e. the LEFT part of the bag."""
+        D = syn0.shape[1]
+        cen, ctx, left = [], [], []
+        for s in ids:
+            if ss > 0 and len(s):
+                f = counts[s] / total
+                keep = (np.sqrt(f / ss) + 1) * ss / f
+                s = s[rng.random(len(s)) < keep]
+            n = len(s)
+            if n < 2:
+                continue
+            b = rng.integers(0, win, n)
+            pos = np.arange(n)
+            X = np.full((n, 2 * win), -1, dtype=np.int64)
+            Lm = np.zeros((n, 2 * win), dtype=bool)
+            col = 0
+            for off in range(-win, win + 1):
+                if off == 0:
+                    continue
+                ok = (np.abs(off) <= win - b) & (pos + off >= 0) & (pos + off < n)
+                X[ok, col] = s[pos[ok] + off]
+                Lm[ok, col] = off < 0
+                col += 1
+            has = (X >= 0).any(1)
+            cen.append(s[has])
+            ctx.append(X[has])
+            left.append(Lm[has])
+        if not cen:
+            return step, n_steps_est
+        c = torch.from_numpy(np.concatenate(cen)).to(dev)
+        X = torch.from_numpy(np.concatenate(ctx)).to(dev)
+        Lm = torch.from_numpy(np.concatenate(left)).to(dev)
+        perm = torch.randperm(c.numel(), generator=gen).to(dev)
+        c, X, Lm = c[perm], X[perm], Lm[perm]
+        if n_steps_est is None:
+            n_steps_est = epochs * ((c.numel() + B - 1) // B)
+        for s0 in range(0, c.numel(), B):
+            cb, xb, lb = c[s0:s0 + B], X[s0:s0 + B], Lm[s0:s0 + B]
+            lr = max(lr0 * (1 - step / max(n_steps_est, 1)), lr0 * 1e-4)
+            step += 1
+            valid = xb >= 0
+            cnt = valid.sum(1).clamp(min=1).to(syn0.dtype)
+            h = (syn0[xb.clamp(min=0)] * valid[:, :, None]).sum(1) / cnt[:, None]      # neu1 [b, D]
+            nodes = P_idx[cb]
+            u = syn1[nodes]                                                              # [b, L, D]
+            dot = (u * h[:, None, :]).sum(-1)
+            live = (dot > -MAX_EXP) & (dot < MAX_EXP)
+            g = (1 - P_code[cb] - torch.sigmoid(dot)) * P_mask[cb] * live * lr
+            neu1e = (g[:, :, None] * u).sum(1)
+            syn1.index_add_(0, nodes.reshape(-1), (g[:, :, None] * h[:, None, :]).reshape(-1, D))
+            upd = lb & valid
+            rows = torch.nonzero(upd, as_tuple=True)
+            syn0.index_add_(0, xb[rows], neu1e[rows[0]])
+        return step, n_steps_est
 
     def fit(self, X, y, w, offset, info: DataInfo, valid=None, model_key=None):
         if self.strings is None:
@@ -203,7 +268,16 @@ class Word2VecTrainer:
         win = int(p["window_size"])
         B = int(p["batch_pairs"])
         step, n_steps_est = 0, None
+        cbow = str(p.get("word_model") or "SkipGram").lower() == "cbow"
+        if str(p.get("word_model") or "SkipGram").lower() not in ("skipgram", "cbow"):
+            raise ValueError(f"word_model must be SkipGram or CBOW, got {p.get('word_model')!r}")
         for ep in range(epochs):
+            if cbow:
+                step, n_steps_est = self._cbow_epoch(ids, counts, total, ss, win, rng, gen, syn0, syn1, P_idx, P_code,
+                                                     P_mask, lr0, B, step, n_steps_est, epochs, dev)
+                if self.job is not None:
+                    self.job.set_progress((ep + 1) / epochs)
+                continue
             centers, ctxs = [], []
             for s in ids:
                 if ss > 0 and len(s):
@@ -249,6 +323,6 @@ class Word2VecTrainer:
         model.words = words
         model.vocab = vocab
         model.vectors = syn0
-        model.output.update(vocab_size=V, vec_size=D, epochs=epochs)
+        model.output.update(vocab_size=V, vec_size=D, epochs=epochs, word_model="CBOW" if cbow else "SkipGram")
         model.output["run_time_ms"] = int((time.time() - t0) * 1000)
         return model

@@ -193,3 +193,25 @@ def test_glrm_column_losses_and_outputs(df):
     g2 = H2OGeneralizedLowRankEstimator(max_updates=3, multi_loss="Ordinal", **base)
     g2.train(x=["a", "b", "c"], training_frame=df)
     assert g2._model.output["iterations"] <= 4
+
+
+@pytest.mark.parametrize("word_model", ["CBOW", "SkipGram"])
+def test_word2vec_word_models_group_cooccurring_words(word_model):
+    """word_model=CBOW (WordVectorTrainer.CBOW / hierarchicalSoftmaxCBOW) and SkipGram: words that share
+    sentences end up nearer (cosine) than words that never co-occur."""
+    rng = np.random.default_rng(0)
+    A, Bw = ["cat", "dog", "cow", "pig"], ["one", "two", "six", "ten"]
+    words = []
+    for i in range(1500):
+        words += list(rng.choice(A if i % 2 else Bw, 6)) + [None]
+    fr = h2o.H2OFrame(pd.DataFrame({"w": words}), column_types={"w": "string"})
+    w2v = H2OWord2vecEstimator(vec_size=10, min_word_freq=1, epochs=5, seed=1, sent_sample_rate=0, window_size=3,
+                               word_model=word_model)
+    w2v.train(training_frame=fr)
+    m = w2v._model
+    assert m.output["word_model"] == word_model
+    vec = {w: m.vectors[i].double().cpu().numpy() for w, i in m.vocab.items()}
+    cos = lambda a, b: float(vec[a] @ vec[b] / np.linalg.norm(vec[a]) / np.linalg.norm(vec[b]))  # noqa: E731
+    within = np.mean([cos(a, b) for g in (A, Bw) for a in g for b in g if a < b])
+    across = np.mean([cos(a, b) for a in A for b in Bw])
+    assert within > across + 0.3, (within, across)
