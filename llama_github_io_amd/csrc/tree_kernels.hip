@@ -53,6 +53,8 @@ struct Dec {       // split decision (80 B)
   float predl, predr;
 };
 
+#define TP_MAXL_DEV 64   // deepest tree the native plan walks (TreePlan arrays hold TP_MAXL = 65 levels)
+
 struct Cand {      // best split of one (node, feature)
   double expl;     // explained "variance" of the split (larger is better)
   double gain;
@@ -455,7 +457,9 @@ __global__ __launch_bounds__(256) void k_split_find(
     const double* __restrict__ hist, int slot_doubles, const int* __restrict__ meta, int F,
     const int* __restrict__ nbins_f, const int* __restrict__ iscat_f, const int* __restrict__ mono_f,
     SplitParams p, int level, Cand* __restrict__ cand, double* __restrict__ root_w,
-    const float* __restrict__ edges /*[F][255] global bin edges (inf padded) or null*/, int adapt_nb) {
+    const float* __restrict__ edges /*[F][255] global bin edges (inf padded) or null*/, int adapt_nb, int f0) {
+  // f0: global id of this launch's first feature (feature-sliced row-sharded runs search only the rank's
+  // slice; per-feature arrays arrive offset by f0, the slot holds only the slice, cand is [node][slice])
   const int node = blockIdx.x, f = blockIdx.y, t = threadIdx.x;
   if (node >= meta[0]) return;
   __shared__ double sw[256], swy[256], skey[256];
@@ -509,7 +513,7 @@ __global__ __launch_bounds__(256) void k_split_find(
   }
   const double W = sw[255], WY = swy[255];
   const double Wall = W + wNA, WYall = WY + wyNA;
-  if (root_w && node == 0 && f == 0 && t == 0) *root_w = Wall;   // level 0: the tree's total weight
+  if (root_w && node == 0 && f + f0 == 0 && t == 0) *root_w = Wall;   // level 0: the tree's total weight
 
   auto E = [&](double ww, double yy) -> double {
     if (p.mode == 1) {
@@ -541,7 +545,7 @@ __global__ __launch_bounds__(256) void k_split_find(
     __syncthreads();
     if (s_hi > s_lo) {
       unsigned long long hsh = splitmix64(p.seed ^ ((unsigned long long)level << 48) ^
-                                          ((unsigned long long)node << 20) ^ (unsigned long long)f);
+                                          ((unsigned long long)node << 20) ^ (unsigned long long)(f + f0));
       rand_b = s_lo + 1 + (int)(hsh % (unsigned long long)(s_hi - s_lo));
     }
   }
@@ -956,6 +960,36 @@ __global__ void k_subtract(double* __restrict__ hist_next, const double* __restr
     s[i] = pa[i] - hb[i];
 }
 
+// k_hist_pack: feature-sliced reduce-scatter staging. Node slots [n][slot] (bin-major (bin, f) pairs, then
+// naYY[F], wYY) -> dst[W][n][E] where rank r's chunk holds, per node, the same layout restricted to its
+// features [r*Fs, r*Fs + Fs): (bin, f') pairs, naYY[f'], wYY (E = Fs*2*NBIN + Fs + 1). Features past F
+// are zero-filled. After reduce_scatter each rank owns the GLOBAL histograms of its slice, in the layout
+// k_split_find reads with F = Fs.
+__global__ void k_hist_pack(const double* __restrict__ src, int slot, int F, int Fs, int W, int n,
+                            double* __restrict__ dst) {
+  const long long E = (long long)Fs * 2 * NBIN + Fs + 1;
+  const long long total = (long long)W * n * E;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long e = i % E;
+    const long long rn = i / E;
+    const int node = (int)(rn % n), r = (int)(rn / n);
+    const double* sl = src + (size_t)node * slot;
+    double v;
+    if (e < (long long)Fs * 2 * NBIN) {
+      const int bin = (int)(e / (2 * Fs)), rem = (int)(e % (2 * Fs));
+      const int f = r * Fs + (rem >> 1);
+      v = f < F ? sl[(size_t)bin * 2 * F + 2 * f + (rem & 1)] : 0.0;
+    } else if (e < (long long)Fs * 2 * NBIN + Fs) {
+      const int f = r * Fs + (int)(e - (long long)Fs * 2 * NBIN);
+      v = f < F ? sl[(size_t)F * 2 * NBIN + f] : 0.0;
+    } else {
+      v = sl[(size_t)F * 2 * NBIN + F];
+    }
+    dst[i] = v;
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // k_route: regroups the rows of an EVEN level e two levels down at once. Rows are physically moved only
 // every second level: level e+1 is histogrammed by filtering the level-e ranges (k_hist_build<true>), so a
@@ -1131,22 +1165,46 @@ __global__ __launch_bounds__(LW * 64) void k_route(
 // k_leaf_assign: after the last level, every row walks the tree from the root in ORIGINAL row order
 // (master bins, coalesced) to its leaf: leaf_of_row[row] and the per-leaf Newton sums (gamma numerator /
 // denominator planes) as int64 fixed point (scales from k_qscale; sums are exact and order independent ->
-// deterministic). Small leaf sets are privatised in LDS per block, larger ones add to global int64 slots.
-// GBM.java fitBestConstants / AddTreeContributions consume these sums.
-#define LEAF_LDS_MAX 2048   // leaves privatised in LDS (2 x 8 B each = 32 KB)
-struct LevelPtrs { const Dec* dec; const int* cl; const int* cr; };
+// deterministic). GBM.java fitBestConstants / AddTreeContributions consume these sums.
+// The tree is staged in LDS as 16-B {feat, bin | na_left << 16 | is_cat << 17, child_l, child_r} records
+// (flattened by level), so a row's walk is D dependent LDS reads instead of D chains of dependent global
+// loads (MEASURED on the global walk: 419 us per tree at 11M rows, latency-bound). Categorical bitsets stay
+// in the global Dec records (read only on categorical splits). Small leaf sets are privatised in LDS.
+// Dynamic LDS: [2*leaf_cap u64 sums (if leaf_cap <= LEAF_LDS_MAX)] [n_nodes int4 (if <= LEAF_TREE_MAX)].
+#define LEAF_LDS_MAX 2048
+#define LEAF_TREE_MAX 2048
+struct LevelPtrs { const Dec* dec; const int* cl; const int* cr; long long cap; };
 
 template <int NV>
 __global__ __launch_bounds__(256) void k_leaf_assign(
     const uint8_t* __restrict__ bins, int stride, long long N, const LevelPtrs* __restrict__ lv, int D,
     const float* __restrict__ an, const float* __restrict__ ad, const double* __restrict__ qs,
-    int* __restrict__ leaf_of_row, unsigned long long* __restrict__ leafq, int leaf_cap) {
-  __shared__ unsigned long long sq[2 * LEAF_LDS_MAX];
+    int* __restrict__ leaf_of_row, unsigned long long* __restrict__ leafq, int leaf_cap, int n_nodes) {
+  extern __shared__ __align__(16) unsigned char la_smem[];
+  __shared__ int sbase[TP_MAXL_DEV + 1];
   const bool lds = leaf_cap <= LEAF_LDS_MAX;
-  if (lds) {
-    for (int i = threadIdx.x; i < 2 * leaf_cap; i += blockDim.x) sq[i] = 0ull;
-    __syncthreads();
+  const bool tl = n_nodes <= LEAF_TREE_MAX;
+  unsigned long long* sq = (unsigned long long*)la_smem;
+  int4* st = (int4*)(la_smem + (lds ? (size_t)16 * leaf_cap : 0));
+  if (threadIdx.x == 0) {
+    int b = 0;
+    for (int d = 0; d < D; ++d) { sbase[d] = b; b += (int)lv[d].cap; }
+    sbase[D] = b;
   }
+  if (lds)
+    for (int i = threadIdx.x; i < 2 * leaf_cap; i += blockDim.x) sq[i] = 0ull;
+  __syncthreads();
+  if (tl) {
+    for (int d = 0; d < D; ++d) {
+      const int c = (int)lv[d].cap, b = sbase[d];
+      for (int i = threadIdx.x; i < c; i += blockDim.x) {
+        const Dec* dc = lv[d].dec + i;
+        st[b + i] = make_int4(dc->feat, (dc->bin & 0xFFFF) | ((dc->na_left != 0) << 16) | ((dc->is_cat != 0) << 17),
+                              lv[d].cl[i], lv[d].cr[i]);
+      }
+    }
+  }
+  __syncthreads();
   const float sn = (float)qs[6], sd = (float)qs[7];
   for (long long row = (long long)blockIdx.x * blockDim.x + threadIdx.x; row < N;
        row += (long long)gridDim.x * blockDim.x) {
@@ -1158,23 +1216,39 @@ __global__ __launch_bounds__(256) void k_leaf_assign(
       if (NV > 2) v2 = s4[2];
       if (NV > 3) v3 = s4[3];
     }
+    const float a_n = an[row], a_d = ad[row];    // issued before the walk: latency overlaps it
     int i = 0, leaf = 0;
     for (int d = 0; d < D; ++d) {
-      const Dec* dc = lv[d].dec + i;
-      const int f = dc->feat;
       int c;
-      if (f < 0) {
-        c = lv[d].cl[i];                         // terminal node: child_l == child_r == its leaf
+      if (tl) {
+        const int4 e = st[sbase[d] + i];
+        if (e.x < 0) {
+          c = e.z;                               // terminal node: child_l == child_r == its leaf
+        } else {
+          const int b = NV > 2 ? row_byte4(v0, v1, v2, v3, e.x) : NV > 0 ? row_byte(v0, v1, e.x)
+                                                                         : bins[(size_t)row * stride + e.x];
+          bool gl;
+          if (b == NA_BIN) gl = (e.y >> 16) & 1;
+          else if ((e.y >> 17) & 1) gl = (lv[d].dec[i].bits[b >> 5] >> (b & 31)) & 1u;
+          else gl = b < (e.y & 0xFFFF);
+          c = gl ? e.z : e.w;
+        }
       } else {
-        const int b = NV > 2 ? row_byte4(v0, v1, v2, v3, f) : NV > 0 ? row_byte(v0, v1, f)
-                                                                     : bins[(size_t)row * stride + f];
-        c = dec_go_left(dc, b) ? lv[d].cl[i] : lv[d].cr[i];
+        const Dec* dc = lv[d].dec + i;
+        const int f = dc->feat;
+        if (f < 0) {
+          c = lv[d].cl[i];
+        } else {
+          const int b = NV > 2 ? row_byte4(v0, v1, v2, v3, f) : NV > 0 ? row_byte(v0, v1, f)
+                                                                       : bins[(size_t)row * stride + f];
+          c = dec_go_left(dc, b) ? lv[d].cl[i] : lv[d].cr[i];
+        }
       }
       if (c < 0) { leaf = -1 - c; break; }
       i = c;
     }
     leaf_of_row[row] = leaf;
-    const long long qn = (long long)(an[row] * sn), qd = (long long)(ad[row] * sd);
+    const long long qn = (long long)(a_n * sn), qd = (long long)(a_d * sd);
     if (lds) {
       if (qn) atomicAdd(sq + 2 * leaf, (unsigned long long)qn);
       if (qd) atomicAdd(sq + 2 * leaf + 1, (unsigned long long)qd);
@@ -1415,13 +1489,14 @@ int h2o_leaf_values(const void* leafsum, int n, int log_link, double scale, doub
 int h2o_split_find(const void* hist, int slot_doubles, const void* meta, int cap, int F, const void* nbins_f,
                    const void* iscat_f, const void* mono_f, double min_w, double msi, double lambda_, double alpha,
                    double gamma, int mode, int random_split, unsigned long long seed, int level, void* cand,
-                   void* root_w, const void* edges, int adapt_nb, hipStream_t s) {
+                   void* root_w, const void* edges, int adapt_nb, int f0, hipStream_t s) {
+  if (F <= 0 || cap <= 0) return 0;
   SplitParams p;
   p.min_w = min_w; p.min_split_improvement = msi; p.lambda = lambda_; p.alpha = alpha; p.gamma = gamma;
   p.mode = mode; p.random_split = random_split; p.seed = seed;
   hipLaunchKernelGGL(k_split_find, dim3(cap, F), dim3(256), 0, s, (const double*)hist, slot_doubles,
                      (const int*)meta, F, (const int*)nbins_f, (const int*)iscat_f, (const int*)mono_f, p, level,
-                     (Cand*)cand, (double*)root_w, (const float*)edges, adapt_nb);
+                     (Cand*)cand, (double*)root_w, (const float*)edges, adapt_nb, f0);
   return (int)hipGetLastError();
 }
 
@@ -1474,6 +1549,15 @@ int h2o_subtract(void* hist_next, const void* hist_cur, const void* hbuild, cons
   return (int)hipGetLastError();
 }
 
+int h2o_hist_pack(const void* src, int slot, int F, int Fs, int W, int n, void* dst, hipStream_t s) {
+  if (n <= 0) return 0;
+  const long long total = (long long)W * n * ((long long)Fs * 2 * NBIN + Fs + 1);
+  long long g = (total + 255) / 256;
+  hipLaunchKernelGGL(k_hist_pack, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, s, (const double*)src, slot,
+                     F, Fs, W, n, (double*)dst);
+  return (int)hipGetLastError();
+}
+
 static bool route_generic() {   // H2O_ROUTE_GENERIC=1: byte-load path (A/B measurements)
   static int v = -1;
   if (v < 0) { const char* e = getenv("H2O_ROUTE_GENERIC"); v = (e && e[0] == '1') ? 1 : 0; }
@@ -1509,13 +1593,16 @@ int h2o_route(const void* sbins, const void* say, const void* saw, void* dbins, 
 // leaf id of every row (original order) + fixed-point leaf sums -> fp64 leafsum[leaf_cap][2]
 int h2o_leaf_assign(const void* master, int stride, long long N, const void* lvptrs, int D, const void* an,
                     const void* ad, const void* qs, void* leaf_of_row, void* leafq, int leaf_cap, void* leafsum,
-                    hipStream_t s) {
+                    int n_nodes, hipStream_t s) {
+  if (D > TP_MAXL_DEV) return (int)hipErrorInvalidValue;
   long long grid = (N + 255) / 256;
   if (grid > 2048) grid = 2048;
   if (grid < 1) grid = 1;
-#define LA(NV) hipLaunchKernelGGL((k_leaf_assign<NV>), dim3((unsigned)grid), dim3(256), 0, s, (const uint8_t*)master, \
+  const size_t lds = (leaf_cap <= LEAF_LDS_MAX ? (size_t)16 * leaf_cap : 0) +
+                     (n_nodes <= LEAF_TREE_MAX ? (size_t)16 * n_nodes : 0);
+#define LA(NV) hipLaunchKernelGGL((k_leaf_assign<NV>), dim3((unsigned)grid), dim3(256), lds, s, (const uint8_t*)master, \
                                   stride, N, (const LevelPtrs*)lvptrs, D, (const float*)an, (const float*)ad,          \
-                                  (const double*)qs, (int*)leaf_of_row, (unsigned long long*)leafq, leaf_cap)
+                                  (const double*)qs, (int*)leaf_of_row, (unsigned long long*)leafq, leaf_cap, n_nodes)
   switch (nv_of(stride)) {
     case 4: LA(4); break;
     case 3: LA(3); break;
@@ -1595,6 +1682,11 @@ struct TreePlan {
   int pad3;
   void* ic_map;            // [F][F] interaction-constraint map (null: no constraints)
   void* ic[TP_MAXL];       // per level [caps][F] allowed-feature masks (ic[0] = the root's)
+  // feature-sliced row-sharded mode (sliced = 1): this rank searches features [fs0, fs0 + fsn) of histograms
+  // whose slots hold only the slice (sslot doubles, k_hist_pack layout); candidates go to cand_local
+  // [cap][fsn] and the caller all-gathers them into cand [cap][F]. hrecv = reduce-scattered build slots.
+  int sliced, fs0, fsn, sslot;
+  void *cand_local, *hrecv;
 };
 
 static inline const float* tp_aux(const TreePlan* P, int c) { return (const float*)P->aux + (size_t)c * P->N; }
@@ -1619,7 +1711,8 @@ static int tp_route(const TreePlan* P, int e, hipStream_t s) {
 
 int h2o_tree_plan_size() { return (int)sizeof(TreePlan); }
 
-// qscale reset + root histogram (into hist0; the caller all-reduces it when row-sharded)
+// qscale reset + root histogram (into hist0; the caller all-reduces it when row-sharded; sliced: into
+// hbuild slot 0, which the caller packs and reduce-scatters into hist0)
 int h2o_tree_root(const TreePlan* P, hipStream_t s) {
   if (P->D >= TP_MAXL - 1) return (int)hipErrorInvalidValue;
   if (P->compute_amax) TP_CHECK(h2o_amax(P->aux, P->N, P->amax_bits, s));
@@ -1627,21 +1720,33 @@ int h2o_tree_root(const TreePlan* P, hipStream_t s) {
   const int g0 = P->tiles_cap[0] < P->grid ? P->tiles_cap[0] : P->grid;
   TP_CHECK(h2o_hist_build(P->master, P->stride, P->unit ? nullptr : tp_aux(P, 0), tp_aux(P, 1), P->nodes[0], P->bp[0],
                           P->meta[0], P->F, P->partials, P->slot, P->qs, g0, P->packed, nullptr, nullptr, P->pf32, s));
-  return h2o_hist_reduce(P->partials, P->slot, P->used, P->nodes[0], P->bp[0], P->meta[0], 1, g0, P->hist0,
-                         nullptr, nullptr, P->pf32, s);
+  return h2o_hist_reduce(P->partials, P->slot, P->used, P->nodes[0], P->bp[0], P->meta[0], 1, g0,
+                         P->sliced ? P->hbuild : P->hist0, nullptr, nullptr, P->pf32, s);
 }
 
-// one level: split search + plan, then the next level's histogram.
-// returns 0 = histogram done (dist: compact buffer ready for the all-reduce), 1 = last level, <0 error.
-int h2o_tree_level(const TreePlan* P, int d, int dist, hipStream_t s) {
+// split search of level d: every feature into cand, or (sliced) this rank's feature slice into cand_local
+int h2o_tree_find(const TreePlan* P, int d, hipStream_t s) {
+  const void* hc = (d % 2) ? P->hist1 : P->hist0;
+  if (!P->sliced)
+    return h2o_split_find(hc, P->slot, P->meta[d], P->caps[d], P->F, P->nbins_f, P->iscat_f, P->mono_f, P->min_w,
+                          P->msi, P->lam, P->alpha, P->gamma, P->mode, P->random_split, P->seed, d, P->cand,
+                          d == 0 ? P->rootw : nullptr, P->edges, P->nb_level[d], 0, s);
+  const int f0 = P->fs0;
+  return h2o_split_find(hc, P->sslot, P->meta[d], P->caps[d], P->fsn, (const int*)P->nbins_f + f0,
+                        (const int*)P->iscat_f + f0, P->mono_f ? (const int*)P->mono_f + f0 : nullptr, P->min_w,
+                        P->msi, P->lam, P->alpha, P->gamma, P->mode, P->random_split, P->seed, d, P->cand_local,
+                        d == 0 ? P->rootw : nullptr, P->edges ? (const float*)P->edges + (size_t)f0 * 255 : nullptr,
+                        P->nb_level[d], f0, s);
+}
+
+// decisions (from cand) + plan, then the next level's histogram.
+// returns 0 = histogram done (dist: compact buffer ready for the collective), 1 = last level, <0 error.
+int h2o_tree_grow(const TreePlan* P, int d, int dist, hipStream_t s) {
   void* hc = (d % 2) ? P->hist1 : P->hist0;
   void* hn = (d % 2) ? P->hist0 : P->hist1;
   const int cap = P->caps[d];
   const bool odd = d % 2 == 1;
-  int rc = h2o_split_find(hc, P->slot, P->meta[d], cap, P->F, P->nbins_f, P->iscat_f, P->mono_f, P->min_w, P->msi,
-                          P->lam, P->alpha, P->gamma, P->mode, P->random_split, P->seed, d, P->cand,
-                          d == 0 ? P->rootw : nullptr, P->edges, P->nb_level[d], s);
-  if (rc) return -rc;
+  int rc;
   const int kc = P->kc_level[d] > 0 ? P->kc_level[d] : P->k_cols;
   rc = h2o_split_reduce(P->cand, P->meta[d], cap, P->F, P->feat_ok, kc, P->seed, d, P->dec[d],
                         P->ic_map ? P->ic[d] : nullptr, s);
@@ -1685,17 +1790,29 @@ int h2o_tree_level(const TreePlan* P, int d, int dist, hipStream_t s) {
   return rc ? -rc : 0;
 }
 
-// row-sharded: sibling subtraction after the compact buffer's all-reduce
+// one level: split search, decisions, plan, next histogram (single process and all-reduce mode)
+int h2o_tree_level(const TreePlan* P, int d, int dist, hipStream_t s) {
+  const int rc = h2o_tree_find(P, d, s);
+  if (rc) return -rc;
+  return h2o_tree_grow(P, d, dist, s);
+}
+
+// row-sharded: sibling subtraction after the compact buffer's all-reduce (sliced: after the reduce-scatter
+// into hrecv, on slice-layout slots)
 int h2o_tree_subtract(const TreePlan* P, int d, hipStream_t s) {
   void* hc = (d % 2) ? P->hist1 : P->hist0;
   void* hn = (d % 2) ? P->hist0 : P->hist1;
+  if (P->sliced)
+    return h2o_subtract(hn, hc, P->hrecv, P->nodes[d + 1], P->meta[d + 1], P->caps[d + 1], P->sslot, s);
   return h2o_subtract(hn, hc, P->hbuild, P->nodes[d + 1], P->meta[d + 1], P->caps[d + 1], P->slot, s);
 }
 
 // after the last level: leaf_of_row (original order) + fp64 leaf sums (the caller all-reduces them when sharded)
 int h2o_tree_leaves(const TreePlan* P, hipStream_t s) {
+  int n_nodes = 0;
+  for (int d = 0; d < P->D; ++d) n_nodes += P->caps[d];
   return h2o_leaf_assign(P->master, P->stride, P->N, P->lvptrs, P->D, tp_aux(P, 2), tp_aux(P, 3), P->qs,
-                         P->leaf_of_row, P->leafq, P->leaf_cap, P->leafsum, s);
+                         P->leaf_of_row, P->leafq, P->leaf_cap, P->leafsum, n_nodes, s);
 }
 
 // single process: the whole tree (root .. leaves) in one host call

@@ -406,7 +406,8 @@ class _TreePlan(ctypes.Structure):
                 [("seed", ctypes.c_ulonglong)] + [(n, _cd) for n in ("scale", "kclamp", "mx")] +
                 [("kc_level", _ci * _MAXL), ("pad2", _ci)] +
                 [("edges", _vp), ("nb_level", _ci * _MAXL), ("pad3", _ci)] +
-                [("ic_map", _vp), ("ic", _vp * _MAXL)])
+                [("ic_map", _vp), ("ic", _vp * _MAXL)] +
+                [(n, _ci) for n in ("sliced", "fs0", "fsn", "sslot")] + [("cand_local", _vp), ("hrecv", _vp)])
 
 
 class _Arena:
@@ -522,11 +523,56 @@ class GpuTreeBuilder:
         # raw device pointers resolved once: the per-tree launch sequence is ~45 ctypes calls and at small
         # shards (1.375M rows/GPU) the host loop, not the GPU, set the pace (82 % busy, rocprofv3 trace)
         self._pt = {name: t.data_ptr() for name, t in self.av.items()}
-        # per-level (dec, cl, cr) pointers for the leaf traversal (k_leaf_assign)
-        self.lvptrs = torch.tensor([[self._pt[f"dec{d}"], self._pt[f"cl{d}"], self._pt[f"cr{d}"]] for d in range(D)],
+        # per-level (dec, cl, cr, cap) records for the leaf traversal (k_leaf_assign)
+        self.lvptrs = torch.tensor([[self._pt[f"dec{d}"], self._pt[f"cl{d}"], self._pt[f"cr{d}"], self.caps[d]]
+                                    for d in range(D)],
                                    dtype=torch.int64).reshape(-1).to(dev)
         self.ic_map = None
         self._hp = [h.data_ptr() for h in self.hist]
+        self._init_comm(capmax)
+
+    def _init_comm(self, capmax: int):
+        """Row-sharded histogram exchange (reference: ScoreBuildHistogram2 + MRTask reduce). Default
+        ``H2O_TREE_COMM=rs``: feature-sliced — each level's built-node histograms are packed by feature slice
+        (k_hist_pack) and REDUCE-SCATTERED, so every rank holds the global histograms of F/W features only,
+        searches splits on that slice, and the per-(node, feature) candidates are ALL-GATHERED (a few KB) so
+        every rank takes the same decisions. ``ar``: all-reduce the full node histograms (every rank searches
+        every feature). Both end with one all-reduce of the leaf sums (+ the root weight)."""
+        self.W = coll.world() if coll.is_dist() else 1
+        self.sliced = self.W > 1 and os.environ.get("H2O_TREE_COMM", "rs") == "rs"
+        self.fs = self.fs0 = self.fsn = 0
+        self.sslot = self.slot
+        if not self.sliced:
+            return
+        W, F, dev = self.W, self.F, self.dev
+        self.fs = Fs = (F + W - 1) // W
+        self.fs0 = min(F, coll.rank() * Fs)
+        self.fsn = max(0, min(F, self.fs0 + Fs) - self.fs0)
+        self.sslot = Fs * 2 * NBIN + Fs + 1
+        self.hsend = torch.empty(W * capmax * self.sslot, dtype=torch.float64, device=dev)
+        self.hrecv = torch.empty(capmax * self.sslot, dtype=torch.float64, device=dev)
+        self.cand_local = torch.zeros(capmax * Fs * CAND_BYTES, dtype=torch.uint8, device=dev)
+        self.cand_all = torch.empty(W * capmax * Fs * CAND_BYTES, dtype=torch.uint8, device=dev)
+        # leaf sums + the root weight (written by the owner of feature 0) in one all-reduce
+        self.lsx = torch.zeros(self.leaf_cap * 2 + 1, dtype=torch.float64, device=dev)
+        self._rootw = self.av["rootw"].view(torch.float64)
+
+    def _rs_hist(self, src_ptr: int, n: int, out: torch.Tensor, s):
+        """Pack n build slots by feature slice and reduce-scatter them: ``out`` [n * sslot] = this rank's
+        slice of the global histograms."""
+        E = self.sslot
+        nat.check(self.lib.h2o_hist_pack(src_ptr, self.slot, self.F, self.fs, self.W, n, self.hsend.data_ptr(), s),
+                  "hist_pack")
+        coll.reduce_scatter_(out[: n * E], self.hsend[: self.W * n * E])
+
+    def _ag_cands(self, d: int):
+        """All-gather every rank's [cap][Fs] candidates into cand [cap][F] (rank r holds features r*Fs..)."""
+        cap, Fs, W, CB = self.caps[d], self.fs, self.W, CAND_BYTES
+        n = cap * Fs * CB
+        g = self.cand_all[: W * n]
+        coll.all_gather_into_(g, self.cand_local[:n])
+        full = g.view(W, cap, Fs, CB).permute(1, 0, 2, 3).reshape(cap, W * Fs, CB)[:, : self.F]
+        self.cand[: cap * self.F * CB].view(cap, self.F, CB).copy_(full)
 
     def _p(self, name):
         return self._pt[name]
@@ -577,6 +623,9 @@ class GpuTreeBuilder:
         for d in range(_MAXL):
             P.nb_level[d] = p.adapt_nb(d) if P.edges else 0
         self._set_plan_ic(P)
+        P.sliced, P.fs0, P.fsn, P.sslot = int(self.sliced), self.fs0, self.fsn, self.sslot
+        P.cand_local = self.cand_local.data_ptr() if self.sliced else 0
+        P.hrecv = self.hrecv.data_ptr() if self.sliced else 0
         return P
 
     def _edges_ptr(self):
@@ -634,6 +683,8 @@ class GpuTreeBuilder:
         ref = ctypes.byref(P)
         if not coll.is_dist():
             nat.check(lib.h2o_tree_all(ref, s), "tree_all")
+        elif self.sliced:
+            self._build_sliced(ref, P, leaf_native, s)
         else:
             nat.check(lib.h2o_tree_root(ref, s), "tree_root")
             coll.all_reduce_(self.hist[0][: self.slot])
@@ -654,6 +705,36 @@ class GpuTreeBuilder:
             vals = leaf_fn(self.leafsum)
             self.av["leafval"].view(torch.float32)[: vals.numel()].copy_(vals.to(torch.float32))
         return self._snapshot()
+
+    def _build_sliced(self, ref, P, leaf_native, s):
+        """Feature-sliced row-sharded tree: per level one reduce-scatter of the built-node histograms
+        (1/W of them land on each rank) and one all-gather of split candidates; one all-reduce at the end."""
+        lib, E = self.lib, self.sslot
+        nat.check(lib.h2o_tree_root(ref, s), "tree_root")
+        self._rs_hist(self.hbuild.data_ptr(), 1, self.hist[0], s)
+        for d in range(self.D):
+            nat.check(lib.h2o_tree_find(ref, d, s), "tree_find")
+            self._ag_cands(d)
+            r = lib.h2o_tree_grow(ref, d, 1, s)
+            if r < 0:
+                nat.check(-r, "tree_grow")
+            if r == 1:
+                break
+            self._rs_hist(self.hbuild.data_ptr(), self.caps[d], self.hrecv, s)
+            nat.check(lib.h2o_tree_subtract(ref, d, s), "tree_subtract")
+        nat.check(lib.h2o_tree_leaves(ref, s), "tree_leaves")
+        L2 = self.leaf_cap * 2
+        self.lsx[:L2].copy_(self.leafsum.view(-1))
+        if self.fs0 == 0 and self.fsn > 0:
+            self.lsx[L2:].copy_(self._rootw)
+        else:
+            self.lsx[L2:].zero_()
+        coll.all_reduce_(self.lsx)
+        self.leafsum.view(-1).copy_(self.lsx[:L2])
+        self._rootw.copy_(self.lsx[L2:])
+        if leaf_native is not None:
+            nat.check(lib.h2o_leaf_values(self.leafsum.data_ptr(), self.leaf_cap, P.log_link, P.scale, P.kclamp,
+                                          P.mx, self._p("leafval"), s), "leaf_values")
 
     def _snapshot(self):
         # the tree's structure travels to pinned host memory asynchronously: the host decodes finished

@@ -14,38 +14,70 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 
-def _worker(rank, world, port, algo, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+def _train_gpu(algo, X, y, info):
+    """Tree variants that reach the feature-sliced exchange through different kernel arguments:
+    UniformAdaptive (per-feature bin edges, offset by the slice), XRT random thresholds (global feature
+    id in the hash) and Newton-mode XGBoost."""
+    from test_distributed import _train
+    Xs = _data_full()[0].to(X.device)
+    if algo == "gbm_ua":
+        from llama_github_io_amd.models.gbm import GBMTrainer
+        m = GBMTrainer(dict(ntrees=4, max_depth=4, seed=7, histogram_type="UniformAdaptive")).fit(X, y, None, None, info)
+        return m.forest.predict_raw(Xs)[:, 0]
+    if algo == "xrt":
+        from llama_github_io_amd.models.drf import DRFTrainer
+        m = DRFTrainer(dict(ntrees=3, max_depth=4, seed=7, histogram_type="Random", sample_rate=1.0,
+                            mtries=-2)).fit(X, y, None, None, info)
+        return m.forest.predict_raw(Xs)[:, 0]
+    if algo == "xgboost":
+        from llama_github_io_amd.models.xgboost import XGBoostTrainer
+        m = XGBoostTrainer(dict(ntrees=4, max_depth=4, seed=7)).fit(X, y, None, None, info)
+        return m.forest.predict_raw(Xs)[:, 0]
+    return _train(algo, X, y, info)
+
+
+def _data_full():
+    from test_distributed import _data
+    return _data()
+
+
+def _worker(rank, world, port, algo, q, comm="rs"):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      H2O_TREE_COMM=comm)
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import torch.distributed as dist
-    from test_distributed import _data, _info, _train
+    from test_distributed import _data, _info
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         X, y = _data()
         N = X.shape[1]
         sl = slice(rank * N // world, (rank + 1) * N // world)
-        out = _train(algo, X[:, sl].contiguous().cuda(), y[sl].contiguous().cuda(), _info(X.shape[0]))
+        out = _train_gpu(algo, X[:, sl].contiguous().cuda(), y[sl].contiguous().cuda(), _info(X.shape[0]))
         if rank == 0:
             q.put(out.cpu().numpy())
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("algo", ["gbm", "glm", "kmeans"])
-def test_gpu_sharded_equals_single(algo):
+@pytest.mark.parametrize("algo,world,comm", [("gbm", 2, "rs"), ("gbm", 3, "rs"), ("gbm", 2, "ar"), ("gbm_ua", 2, "rs"),
+                                             ("xrt", 3, "rs"), ("xgboost", 2, "rs"), ("glm", 2, "rs"),
+                                             ("kmeans", 2, "rs")])
+def test_gpu_sharded_equals_single(algo, world, comm):
+    """rs = feature-sliced reduce-scatter exchange (F=5: uneven slices, 3 ranks leave one rank 1 feature);
+    ar = full-histogram all-reduce."""
     import socket
-    from test_distributed import _data, _info, _train
+    from test_distributed import _data, _info
     X, y = _data()
-    single = _train(algo, X.cuda(), y.cuda(), _info(X.shape[0])).cpu().numpy()
+    single = _train_gpu(algo, X.cuda(), y.cuda(), _info(X.shape[0])).cpu().numpy()
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, algo, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, algo, q, comm)) for r in range(world)]
     for p in procs:
         p.start()
     res = q.get(timeout=300)
