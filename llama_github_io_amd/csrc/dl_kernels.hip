@@ -12,11 +12,15 @@
 //              act'(h) run the same way on transposed weight copies. The tile writes its activations and
 //              gradients TRANSPOSED ([units][rows]) for the weight-gradient GEMM and its per-column bias
 //              gradient partial sums (fixed-order reduce later, no atomics).
-//  k_dl_wgrad  dW_l = dA_lᵀ h_{l-1} for every layer in one launch: 64 x 64 output tiles x 4 row splits,
-//              operands loaded straight from the transposed buffers (contiguous along rows), fp32 partial
-//              slabs per split.
-//  k_dl_reduce sums the slabs / bias partials in a fixed order into the flat gradient buffer, scaled by
-//              1 / sum(w) of the batch (single process) or raw plus the batch weight (data parallel).
+//  k_dl_wgrad  dW_l = dA_lᵀ h_{l-1} for every layer in one launch: one 32 x 32 output tile per workgroup,
+//              the mini-batch rows (GEMM K) interleaved over 8 waves in 32-row chunks with 4 chunks of
+//              loads in flight per wave, the 8 partial tiles summed through LDS in a fixed order and written
+//              straight into the flat gradient buffer scaled by 1 / sum(w) of the batch (single process) or
+//              raw plus the batch weight (data parallel). Trailing workgroups reduce the per-tile bias
+//              partials of k_dl_rows (one wave per bias, fixed order).
+//  MEASURED (10M x 784 [200,200], 4096-row steps, rocprofv3): the first version (16-row tiles on 4 waves,
+//  64 x 64 x 4-split weight tiles with fp32 slabs and a separate reduce) took 52 + 32 + 64 us per step:
+//  latency-bound dependent L2 round trips and a serial 256-deep bias loop, not MFMA or HBM.
 // The fused ADADELTA kernel (dense_kernels.hip) then updates the fp32 master weights and the bf16 weight
 // shadow; k_dl_transpose refreshes the transposed shadow the backward pass reads.
 //
@@ -34,13 +38,16 @@ typedef __hip_bfloat16 bf16;
 
 #define DL_MAXL 6        // GEMM layers (hidden + output)
 #define DL_ROWS 16       // rows per k_dl_rows tile
-#define DL_SPLIT 4       // row splits of k_dl_wgrad
+#define DL_THREADS 1024  // k_dl_rows workgroup: 16 waves (one 16-column output tile each per round)
+#define DL_NW (DL_THREADS / 64)
+#define WG_WAVES 8       // k_dl_wgrad waves per 32 x 32 tile (split over the mini-batch rows)
+#define WG_KU 4          // 32-row chunks of loads in flight per wave
 
 struct DLArgs {
   const bf16* Z; long long ldz; const long long* ridx; int B; int Bpad;
   const float* w; const long long* ycls; const float* yreg;
   const float* P; const bf16* W; const bf16* WT; const unsigned long long* step_dev;
-  bf16* hT; bf16* dT; float* bpart; float* slab; float* g; float* gsum;
+  bf16* hT; bf16* dT; float* bpart; float* g; float* gsum;
   int L, K, act, regression;
   int n[DL_MAXL + 1];           // n[0] inputs, n[l] units of layer l, n[L] = outputs
   int kp[DL_MAXL + 1];          // n padded to 32 (GEMM K extent when the activation is an operand)
@@ -86,7 +93,7 @@ __device__ __forceinline__ bf16x8 load8(const bf16* row, int k, int kvalid, bool
 // operand column n: B[k][n] = Brow(n)[k]. K is a multiple of 32; A is zero past the valid extent.
 // The B fragments come from L2 (every tile of the batch reads the same weights): KU k-steps of loads are
 // issued before their MFMAs so KU round trips overlap instead of serialising one per MFMA.
-#define KU 8
+#define KU 16
 __device__ __forceinline__ f32x4 tile_mm(const bf16* A, int lda, const bf16* Bg, long long ldb, int n0, int nvalid,
                                          int K, int kvalid, bool vec) {
   const int lane = threadIdx.x & 63, q = lane >> 4, c = lane & 15;
@@ -128,7 +135,7 @@ __device__ __forceinline__ void store4T(bf16* dst, f32x4 v) {   // 4 consecutive
   *reinterpret_cast<uint2*>(dst) = pk.u;
 }
 
-__global__ __launch_bounds__(256) void k_dl_rows(DLArgs a) {
+__global__ __launch_bounds__(DL_THREADS) void k_dl_rows(DLArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16* S = reinterpret_cast<bf16*>(smem);
   float* ws = reinterpret_cast<float*>(smem + a.lds_w);
@@ -150,7 +157,7 @@ __global__ __launch_bounds__(256) void k_dl_rows(DLArgs a) {
   // zero every activation / gradient tile (K padding must read as zeros)
   {
     const int total = a.lds_w / 4;
-    for (int i = tid; i < total; i += 256) reinterpret_cast<float*>(smem)[i] = 0.f;
+    for (int i = tid; i < total; i += DL_THREADS) reinterpret_cast<float*>(smem)[i] = 0.f;
   }
   __syncthreads();
   // ---- gather the 16 input rows into activation tile 0
@@ -159,7 +166,7 @@ __global__ __launch_bounds__(256) void k_dl_rows(DLArgs a) {
     const int n0 = a.n[0], ld0 = a.ld[0];
     const bool vec = (n0 % 8 == 0) && (a.ldz % 8 == 0);
     const int chunks = (n0 + 7) / 8;
-    for (int i = tid; i < DL_ROWS * chunks; i += 256) {
+    for (int i = tid; i < DL_ROWS * chunks; i += DL_THREADS) {
       const int rr = i / chunks, k = (i - rr * chunks) * 8;
       const long long g = srow[rr];
       if (g < 0) continue;
@@ -174,7 +181,7 @@ __global__ __launch_bounds__(256) void k_dl_rows(DLArgs a) {
   {
     const bf16* A0 = S + a.lds_off[0];
     bf16* dst = a.hT + a.h_off[0];
-    for (int i = tid; i < a.n[0] * 4; i += 256) {
+    for (int i = tid; i < a.n[0] * 4; i += DL_THREADS) {
       const int k = i >> 2, g4 = (i & 3) * 4;
       f32x4 v = {__bfloat162float(A0[(g4 + 0) * a.ld[0] + k]), __bfloat162float(A0[(g4 + 1) * a.ld[0] + k]),
                  __bfloat162float(A0[(g4 + 2) * a.ld[0] + k]), __bfloat162float(A0[(g4 + 3) * a.ld[0] + k])};
@@ -191,7 +198,7 @@ __global__ __launch_bounds__(256) void k_dl_rows(DLArgs a) {
     const uint32_t thr = (uint32_t)(drop * 4294967296.0);
     const uint64_t seed = a.seed_base[l - 1] ^ (step * 0x9E3779B97F4A7C15ULL);
     const int T = (nout + 15) / 16;
-    for (int t = wv; t < T; t += 4) {
+    for (int t = wv; t < T; t += DL_NW) {
       const f32x4 acc = tile_mm(Ain, a.ld[l - 1], a.W + a.w_off[l - 1], nin, t * 16, nout, a.kp[l - 1], nin, vec);
       const int col = t * 16 + c;
       f32x4 o;
@@ -252,7 +259,7 @@ __global__ __launch_bounds__(256) void k_dl_rows(DLArgs a) {
     const uint64_t seed = a.seed_base[l - 1] ^ (step * 0x9E3779B97F4A7C15ULL);
     const bf16* H = S + a.lds_off[l];
     const int T = (nout + 15) / 16;
-    for (int t = wv; t < T; t += 4) {
+    for (int t = wv; t < T; t += DL_NW) {
       // dh = G_{l+1} W_{l+1}: B[k = unit of l+1][n = unit of l] = WT_{l+1}[n][k]
       const f32x4 acc = tile_mm(Gin, ldg_in, a.WT + a.w_off[l], nnext, t * 16, nout, a.kp[l + 1], nnext, vec);
       const int col = t * 16 + c;
@@ -281,7 +288,7 @@ __global__ __launch_bounds__(256) void k_dl_rows(DLArgs a) {
     }
     __syncthreads();
     // zero the K padding of the gradient tile the next layer reads
-    for (int i = tid; i < DL_ROWS * (a.kp[l] - T * 16); i += 256) {
+    for (int i = tid; i < DL_ROWS * (a.kp[l] - T * 16); i += DL_THREADS) {
       const int rr = i / (a.kp[l] - T * 16), cc = T * 16 + i % (a.kp[l] - T * 16);
       Gout[rr * a.ld[l] + cc] = __float2bfloat16(0.f);
     }
@@ -297,84 +304,108 @@ __global__ __launch_bounds__(256) void k_dl_rows(DLArgs a) {
 }
 
 // dW_l[i][j] = sum_rows dA_l[row][i] h_{l-1}[row][j]: A[i][k = row] = dT_l[i][row], B[k = row][j] = hT_{l-1}[j][row].
-// Block = one 64 x 64 tile of one layer and one row split; wave (wi, wj) owns a 32 x 32 quarter (2 x 2 MFMA tiles).
-__global__ __launch_bounds__(256) void k_dl_wgrad(DLArgs a) {
+// Workgroup = one 32 x 32 tile of one layer (2 x 2 MFMA tiles per wave); wave w accumulates row chunks
+// w, w + 8, w + 16, ... (32 rows each); partial tiles meet in LDS and wave 0 sums them in wave order.
+// Workgroups past the weight tiles reduce bias gradients from the k_dl_rows partials (wave = bias).
+__global__ __launch_bounds__(WG_WAVES * 64) void k_dl_wgrad(DLArgs a, int G1, int scale_by_w) {
+  __shared__ float red[WG_WAVES - 1][16][64];
+  __shared__ float s_sw;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, q = lane >> 4, c = lane & 15;
+  const int bst = a.bias_total + 1;
+  if (wv == 0) {                  // sum(w) of the batch, fixed order
+    float sacc = 0.f;
+    for (int g = lane; g < G1; g += 64) sacc += a.bpart[(long long)g * bst + a.bias_total];
+    for (int o = 32; o > 0; o >>= 1) sacc += __shfl_xor(sacc, o, 64);
+    if (lane == 0) s_sw = sacc;
+  }
+  __syncthreads();
+  const float sw = s_sw;
+  const float inv = scale_by_w ? 1.f / fmaxf(sw, 1e-12f) : 1.f;
   const int tiles = a.tile_start[a.L];
-  const int b = blockIdx.x % tiles, split = blockIdx.x / tiles;
+  if ((int)blockIdx.x >= tiles) {
+    const int e = ((int)blockIdx.x - tiles) * WG_WAVES + wv;
+    if (e == 0 && lane == 0 && !scale_by_w && a.gsum) *a.gsum = sw;
+    if (e >= a.bias_total) return;
+    float sacc = 0.f;
+    for (int g = lane; g < G1; g += 64) sacc += a.bpart[(long long)g * bst + e];
+    for (int o = 32; o > 0; o >>= 1) sacc += __shfl_xor(sacc, o, 64);
+    if (lane == 0) {
+      int l = 1;
+      while (l < a.L && e >= a.bias_off[l + 1]) ++l;
+      a.g[a.b_off[l - 1] + (e - a.bias_off[l])] = sacc * inv;
+    }
+    return;
+  }
+  const int b = blockIdx.x;
   int l = 0;
   while (l + 1 < a.L && b >= a.tile_start[l + 1]) ++l;          // GEMM layer l + 1 (0-based l)
   const int bt = b - a.tile_start[l];
   const int ti = bt / a.tiles_j[l], tj = bt - ti * a.tiles_j[l];
   const int ni = a.n[l + 1], nj = a.n[l];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, q = lane >> 4, c = lane & 15;
-  const int i0 = ti * 64 + (wv >> 1) * 32, j0 = tj * 64 + (wv & 1) * 32;
+  const int i0 = ti * 32, j0 = tj * 32;
   const bf16* Ab = a.dT + a.d_off[l + 1];
   const bf16* Bb = a.hT + a.h_off[l];
-  const int rows = a.Bpad / DL_SPLIT;
-  const int k_beg = split * rows, k_end = k_beg + rows;
+  const int nch = a.Bpad / 32;
   f32x4 acc[2][2];
 #pragma unroll
   for (int u = 0; u < 2; ++u)
 #pragma unroll
     for (int v = 0; v < 2; ++v) acc[u][v] = (f32x4){0.f, 0.f, 0.f, 0.f};
   const bf16x8 z8 = {(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
-  for (int k0 = k_beg; k0 < k_end; k0 += 32) {
-    bf16x8 av[2], bv[2];
+  const bf16* arow[2];
+  const bf16* brow[2];
+  bool aok[2], bok[2];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int i = i0 + u * 16 + c;
-      av[u] = i < ni ? *reinterpret_cast<const bf16x8*>(Ab + (long long)i * a.Bpad + k0 + 8 * q) : z8;
-      const int j = j0 + u * 16 + c;
-      bv[u] = j < nj ? *reinterpret_cast<const bf16x8*>(Bb + (long long)j * a.Bpad + k0 + 8 * q) : z8;
+  for (int u = 0; u < 2; ++u) {
+    const int i = i0 + u * 16 + c, j = j0 + u * 16 + c;
+    aok[u] = i < ni; bok[u] = j < nj;
+    arow[u] = Ab + (long long)(aok[u] ? i : 0) * a.Bpad + 8 * q;
+    brow[u] = Bb + (long long)(bok[u] ? j : 0) * a.Bpad + 8 * q;
+  }
+  for (int cb = wv; cb < nch; cb += WG_WAVES * WG_KU) {
+    bf16x8 av[WG_KU][2], bv[WG_KU][2];
+#pragma unroll
+    for (int k = 0; k < WG_KU; ++k) {
+      const int ch = cb + k * WG_WAVES;
+      const bool in = ch < nch;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        av[k][u] = (in && aok[u]) ? *reinterpret_cast<const bf16x8*>(arow[u] + ch * 32) : z8;
+        bv[k][u] = (in && bok[u]) ? *reinterpret_cast<const bf16x8*>(brow[u] + ch * 32) : z8;
+      }
     }
+#pragma unroll
+    for (int k = 0; k < WG_KU; ++k)
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+          acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[k][u], bv[k][v], acc[u][v], 0, 0, 0);
+  }
+  if (wv > 0) {
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
-      for (int v = 0; v < 2; ++v) acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[u], bv[v], acc[u][v], 0, 0, 0);
+      for (int v = 0; v < 2; ++v)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[wv - 1][(u * 2 + v) * 4 + r][lane] = acc[u][v][r];
   }
-  float* out = a.slab + (long long)split * a.n_decay + a.w_off[l];
+  __syncthreads();
+  if (wv != 0) return;
+  float* out = a.g + a.w_off[l];
 #pragma unroll
   for (int u = 0; u < 2; ++u)
 #pragma unroll
     for (int v = 0; v < 2; ++v) {
       const int j = j0 + v * 16 + c;
-      if (j >= nj) continue;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
+        float t = acc[u][v][r];
+        for (int w = 0; w < WG_WAVES - 1; ++w) t += red[w][(u * 2 + v) * 4 + r][lane];
         const int i = i0 + u * 16 + 4 * q + r;
-        if (i < ni) out[(long long)i * nj + j] = acc[u][v][r];
+        if (i < ni && j < nj) out[(long long)i * nj + j] = t * inv;
       }
     }
-}
-
-// flat gradient = fixed-order sums of the weight slabs and the per-tile bias partials, times 1 / sum(w)
-// (scale_by_w) — or raw, with sum(w) stored after the gradient (data parallel: gsum = gbuf[-1]).
-__global__ __launch_bounds__(256) void k_dl_reduce(DLArgs a, int G1, int scale_by_w) {
-  __shared__ float s_sw;
-  if (threadIdx.x < 64) {
-    float s = 0.f;
-    for (int g = threadIdx.x; g < G1; g += 64) s += a.bpart[(long long)g * (a.bias_total + 1) + a.bias_total];
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-    if (threadIdx.x == 0) s_sw = s;
-  }
-  __syncthreads();
-  const float sw = s_sw;
-  const float inv = scale_by_w ? 1.f / fmaxf(sw, 1e-12f) : 1.f;
-  if (!scale_by_w && blockIdx.x == 0 && threadIdx.x == 0 && a.gsum) *a.gsum = sw;
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < a.n_total; e += (long long)gridDim.x * blockDim.x) {
-    float v = 0.f;
-    if (e < a.n_decay) {
-#pragma unroll
-      for (int s = 0; s < DL_SPLIT; ++s) v += a.slab[(long long)s * a.n_decay + e];
-    } else {
-      int l = 0;
-      while (l + 1 < a.L && e >= a.b_off[l + 1]) ++l;
-      const int col = (int)(e - a.b_off[l]);
-      const int bo = a.bias_off[l + 1] + col;
-      for (int g = 0; g < G1; ++g) v += a.bpart[(long long)g * (a.bias_total + 1) + bo];
-    }
-    a.g[e] = v * inv;
-  }
 }
 
 // WT_l[j][i] = W_l[i][j] for every layer (the bf16 shadow the backward pass reads)
@@ -396,14 +427,13 @@ int h2o_dl_args_size() { return (int)sizeof(DLArgs); }
 
 // lds: bytes of dynamic LDS for k_dl_rows (activation + gradient tiles + row weights)
 int h2o_dl_step(const DLArgs* a, int lds, int scale_by_w, hipStream_t s) {
-  if (a->L < 1 || a->L > DL_MAXL || a->K > 16 || a->Bpad % (32 * DL_SPLIT) != 0 || lds > 160 * 1024)
+  if (a->L < 1 || a->L > DL_MAXL || a->K > 16 || a->Bpad % 128 != 0 || lds > 160 * 1024)
     return (int)hipErrorInvalidValue;
   const int G1 = a->Bpad / DL_ROWS;
-  hipLaunchKernelGGL(k_dl_rows, dim3(G1), dim3(256), lds, s, *a);
-  hipLaunchKernelGGL(k_dl_wgrad, dim3(a->tile_start[a->L] * DL_SPLIT), dim3(256), 0, s, *a);
-  long long grid = (a->n_total + 255) / 256;
-  if (grid > 1024) grid = 1024;
-  hipLaunchKernelGGL(k_dl_reduce, dim3((unsigned)grid), dim3(256), 0, s, *a, G1, scale_by_w);
+  hipLaunchKernelGGL(k_dl_rows, dim3(G1), dim3(DL_THREADS), lds, s, *a);
+  const int bias_blocks = (a->bias_total + WG_WAVES - 1) / WG_WAVES;
+  hipLaunchKernelGGL(k_dl_wgrad, dim3(a->tile_start[a->L] + bias_blocks), dim3(WG_WAVES * 64), 0, s, *a, G1,
+                     scale_by_w);
   return (int)hipGetLastError();
 }
 

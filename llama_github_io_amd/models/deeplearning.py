@@ -601,7 +601,7 @@ class DeepLearningTrainer:
         sel = offs = None
         s_in = S_ep
         owb = bool(p.get("overwrite_with_best_model", True)) and not int(p.get("nfolds") or 0)
-        best_loss, best_p, last_ev = float("inf"), None, {}
+        best_loss, best_p, last_ev, best_ev = float("inf"), None, {}, None
         # train_samples_per_iteration (DeepLearning.computeTrainSamplesPerIteration): scoring / stopping is
         # decided at the end of each iteration of tspi samples. 0 and -1 (no replicated data): one epoch;
         # -2 (auto): the reference's caps of its hardware-timed estimate, min(epochs * N / 10, 100k x nodes)
@@ -694,7 +694,7 @@ class DeepLearningTrainer:
                 if owb:
                     lv = self._model_loss(ev.get("_valid") or ev.get("_train"), cat, ae)
                     if lv < best_loss:     # DeepLearningModel.doScoring: keep the lowest-loss weights
-                        best_loss, best_p = lv, fp.p.detach().clone()
+                        best_loss, best_p, best_ev = lv, fp.p.detach().clone(), ev
                 mref = ev.get("_valid") or ev.get("_train")
                 if mref is not None and not end and keeper.add(mref):
                     break
@@ -712,21 +712,32 @@ class DeepLearningTrainer:
             ("graph_chunk%d" % CH if chunk.get("g") not in (None, False) else
              ("graph_step" if gstate.get("g1") not in (None, False) else "eager (" + str(gstate.get("error") or chunk.get("error")) + ")")))
         net.step_dev = None
+        final_ev = last_ev
         if owb and best_p is not None:
             final = self._model_loss(last_ev.get("_valid") or last_ev.get("_train"), cat, ae)
             if best_loss < final:
                 with torch.no_grad():
                     fp.p.copy_(best_p)
                 model.output["best_model_loss"] = best_loss
+                final_ev = best_ev
         model.output["scoring_history"] = history
         model.output["epochs"] = prev_epochs + samples / N_glob
-        if ae:
+        # DeepLearningModel.doScoring: the model's training / validation metrics are those of its scoring
+        # event — on the score_training_samples sample (0 = every row) — not an extra pass over all rows
+        t_fm = time.time()
+        if final_ev.get("_train") is not None:
+            model.output["training_metrics"] = final_ev["_train"]
+        elif ae:
             model.output["training_metrics"] = self._ae_metrics(model, X)
         else:
             model.output["training_metrics"] = model.metrics_for(X, y, w.float())
-            if valid is not None:
+        if valid is not None and not ae:
+            if final_ev.get("_valid") is not None:
+                model.output["validation_metrics"] = final_ev["_valid"]
+            else:
                 Xv, yv, wv, ov = valid
                 model.output["validation_metrics"] = model.metrics_for(Xv, yv, wv, ov)
+        model.output["phase_seconds"]["final_metrics"] = time.time() - t_fm
         # Gedeon variable importance from the first layer weights
         W1 = net.hidden[0].weight.detach().abs() if net.hidden else net.out.weight.detach().abs()
         imp = W1.sum(0).double()

@@ -2,8 +2,9 @@
 
 Reference: ``hex/deeplearning/Neurons.java`` fprop / bprop (``DeepLearningTask.map``). One step is
 ``k_dl_rows`` (gather + every layer forward + loss gradient + every layer backward on 16-row tiles, activations
-in LDS) -> ``k_dl_wgrad`` (all weight gradients) -> ``k_dl_reduce`` (fixed-order partial sums into the flat
-gradient buffer); the optimizer (fused ADADELTA) then refreshes the bf16 weight shadow and
+in LDS) -> ``k_dl_wgrad`` (all weight gradients, split over the batch rows inside a workgroup and summed in a
+fixed order, plus the bias gradients from the row tiles' partials) straight into the flat gradient buffer;
+the optimizer (fused ADADELTA) then refreshes the bf16 weight shadow and
 :meth:`FusedMLPStep.refresh_transposed` the transposed shadow of the backward pass.
 """
 from __future__ import annotations
@@ -16,7 +17,6 @@ from . import _native as nat
 
 MAXL = 6
 ROWS = 16
-SPLIT = 4
 _vp, _ci, _cll, _cf, _cull = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong, ctypes.c_float, ctypes.c_ulonglong
 
 
@@ -25,7 +25,7 @@ class _DLArgs(ctypes.Structure):
     _fields_ = ([("Z", _vp), ("ldz", _cll), ("ridx", _vp), ("B", _ci), ("Bpad", _ci),
                  ("w", _vp), ("ycls", _vp), ("yreg", _vp),
                  ("P", _vp), ("W", _vp), ("WT", _vp), ("step_dev", _vp),
-                 ("hT", _vp), ("dT", _vp), ("bpart", _vp), ("slab", _vp), ("g", _vp), ("gsum", _vp),
+                 ("hT", _vp), ("dT", _vp), ("bpart", _vp), ("g", _vp), ("gsum", _vp),
                  ("L", _ci), ("K", _ci), ("act", _ci), ("regression", _ci),
                  ("n", _ci * (MAXL + 1)), ("kp", _ci * (MAXL + 1)), ("ld", _ci * (MAXL + 1)),
                  ("w_off", _cll * MAXL), ("b_off", _cll * MAXL),
@@ -69,7 +69,7 @@ class FusedMLPStep:
         dev = Z.device
         L = len(lins)
         n = [lins[0].weight.shape[1]] + [l_.weight.shape[0] for l_ in lins]
-        Bpad = (cap + ROWS * 8 - 1) // (ROWS * 8) * (ROWS * 8)      # multiple of 128 = 32 x SPLIT
+        Bpad = (cap + ROWS * 8 - 1) // (ROWS * 8) * (ROWS * 8)      # multiple of 128
         base = fp.p.data_ptr()
         esz = fp.p.element_size()
         a = _DLArgs()
@@ -117,8 +117,7 @@ class FusedMLPStep:
         a.hT = a.dT = self.T.data_ptr()
         G1 = Bpad // ROWS
         self.bpart = torch.zeros(G1 * (bt + 1), dtype=torch.float32, device=dev)
-        self.slab = torch.zeros(SPLIT * fp.n_decay, dtype=torch.float32, device=dev)
-        a.bpart, a.slab = self.bpart.data_ptr(), self.slab.data_ptr()
+        a.bpart = self.bpart.data_ptr()
         a.g = out_grad.data_ptr()
         a.gsum = 0 if out_gsum is None else out_gsum.data_ptr()
         # LDS: activation tiles 0..L-1, output-gradient tile, two gradient tiles, row weights (16-B aligned)
@@ -135,8 +134,8 @@ class FusedMLPStep:
         self.lds = a.lds_w + ROWS * 4
         ts = 0
         for l in range(L):
-            a.tiles_i[l] = (n[l + 1] + 63) // 64
-            a.tiles_j[l] = (n[l] + 63) // 64
+            a.tiles_i[l] = (n[l + 1] + 31) // 32
+            a.tiles_j[l] = (n[l] + 31) // 32
             a.tile_start[l] = ts
             ts += a.tiles_i[l] * a.tiles_j[l]
         a.tile_start[L] = ts
