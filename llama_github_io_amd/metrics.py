@@ -18,34 +18,47 @@ THRESHOLD_CRITERIA = ("f1", "f2", "f0point5", "accuracy", "precision", "recall",
                       "absolute_mcc", "min_per_class_accuracy", "mean_per_class_accuracy")
 
 
-def _sharded_rows(*row_args):
-    """Metrics of row-sharded predictions: all-gather the per-row arguments named in ``row_args``
-    (rank order) and compute once on the full rows — exact, and bit-identical to the single-process
-    metrics (the reference merges fixed-bin AUC2 histograms instead; the gathered predictions are a
-    few bytes per row, small next to training traffic)."""
-    import functools
-    import inspect
+def _dist() -> bool:
+    from .parallel import collectives as coll
+    return coll.is_dist()
 
-    def deco(fn):
-        sig = inspect.signature(fn)
 
-        @functools.wraps(fn)
-        def w(*args, **kwargs):
-            from .parallel import collectives as coll
-            if not coll.is_dist():
-                return fn(*args, **kwargs)
-            b = sig.bind(*args, **kwargs)
-            b.apply_defaults()
-            for name in row_args:
-                t = b.arguments.get(name)
-                if isinstance(t, torch.Tensor):
-                    dev = t.device
-                    g = coll.all_gather_cat(t.contiguous().cpu() if coll.comm_device().type == "cpu" else t.contiguous(), 0)
-                    b.arguments[name] = g.to(dev)
-            with coll.replicated():
-                return fn(*b.args, **b.kwargs)
-        return w
-    return deco
+def _allreduce(t: torch.Tensor, op=None) -> torch.Tensor:
+    """All-reduce a small statistics tensor (staged through the collective device)."""
+    from .parallel import collectives as coll
+    dev = coll.comm_device()
+    h = t.to(dev)
+    coll.all_reduce_(h, op)
+    return h.to(t.device)
+
+
+# Score lattice of the binomial metrics: 2^18 equal bins over [0, 1] (AUC2.java keeps 400 merging bins; a
+# finer FIXED lattice merges across row shards by plain summation and keeps the AUC within ~1e-6 of the
+# exact one). Every bin carries (positive weight, negative weight, max score): the threshold table, the
+# gains/lift groups and — for row-sharded frames — the ROC/PR curves come from these merged histograms.
+SCORE_BINS = 1 << 18
+
+
+def _score_hist(p, pos_w, neg_w, nb: int = SCORE_BINS):
+    """[3, nb] float64 (pos, neg, max score; -inf = empty) of scores p in [0, 1], merged over row shards."""
+    from .ops.segment import segment_sum
+    b = torch.clamp((p * nb).long(), 0, nb - 1)
+    h = torch.empty(3, nb, dtype=torch.float64, device=p.device)
+    h[0] = segment_sum(b, pos_w, nb)
+    h[1] = segment_sum(b, neg_w, nb)
+    h[2] = torch.full((nb,), float("-inf"), dtype=torch.float64, device=p.device).scatter_reduce(
+        0, b, p.double(), reduce="amax", include_self=True)
+    if _dist():
+        from torch.distributed import ReduceOp
+        h[:2] = _allreduce(h[:2].contiguous())
+        h[2] = _allreduce(h[2].contiguous(), ReduceOp.MAX)
+    return h
+
+
+def _hist_curve(h):
+    """Non-empty bins in descending score order: (pos, neg, representative score = the bin's max)."""
+    nz = torch.nonzero((h[0] + h[1]) > 0).squeeze(1).flip(0)
+    return h[0, nz], h[1, nz], h[2, nz]
 
 
 class ModelMetrics(dict):
@@ -80,31 +93,44 @@ def _w(w, n, device):
     return torch.ones(n, dtype=torch.float64, device=device) if w is None else w.double()
 
 
-@_sharded_rows("y", "pred", "w")
 def regression_metrics(y, pred, w=None, distribution=None) -> ModelMetrics:
+    """Weighted sums only (ModelMetricsRegression.MetricBuilderRegression): row shards merge by all-reduce."""
     y, pred = y.double(), pred.double()
     w = _w(w, y.numel(), y.device)
     ok = ~torch.isnan(y) & (w > 0)
     y, pred, w = y[ok], pred[ok], w[ok]
-    sw = w.sum()
     err = y - pred
-    mse = (w * err * err).sum() / sw
-    mae = (w * err.abs()).sum() / sw
-    ybar = (w * y).sum() / sw
-    var = (w * (y - ybar) ** 2).sum() / sw
-    r2 = 1 - mse / var if var > 0 else torch.tensor(float("nan"))
-    rmsle = float("nan")
-    if bool((y > -1).all()) and bool((pred > -1).all()):
-        rmsle = math.sqrt(float((w * (torch.log1p(pred) - torch.log1p(y)) ** 2).sum() / sw))
-    mrd = float(mse)
+    dev_sum = torch.zeros((), dtype=torch.float64, device=y.device)
+    dev_ok = 1.0
     if distribution is not None and distribution.name not in ("gaussian",):
         f = distribution.link_fn(torch.clamp(pred, min=1e-300)) if distribution.link == "log" else pred
         try:
-            mrd = float(distribution.deviance(w, y, f).sum() / sw)
+            dev_sum = distribution.deviance(w, y, f).sum().double()
         except Exception:  # noqa: BLE001
-            mrd = float(mse)
-    return ModelMetrics(model_category="Regression", MSE=float(mse), RMSE=math.sqrt(float(mse)), mae=float(mae),
-                        rmsle=rmsle, r2=float(r2), mean_residual_deviance=mrd, nobs=int(y.numel()))
+            dev_ok = 0.0
+    log_ok = bool((y > -1).all()) and bool((pred > -1).all())
+    lerr = (w * (torch.log1p(pred) - torch.log1p(y)) ** 2).sum() if log_ok else torch.zeros((), dtype=torch.float64,
+                                                                                              device=y.device)
+    v = torch.stack([w.sum(), (w * err * err).sum(), (w * err.abs()).sum(), (w * y).sum(), lerr, dev_sum,
+                     torch.tensor(float(y.numel()), dtype=torch.float64, device=y.device),
+                     torch.tensor(0.0 if log_ok else 1.0, dtype=torch.float64, device=y.device),
+                     torch.tensor(1.0 - dev_ok, dtype=torch.float64, device=y.device)])
+    if _dist():
+        v = _allreduce(v)
+    sw, se, sa, sy, sl, sd, n, nlog, ndev = v.tolist()
+    if sw <= 0:
+        sw = float("nan")
+    ybar = sy / sw
+    var_t = (w * (y - ybar) ** 2).sum().reshape(1)
+    var = float(_allreduce(var_t) if _dist() else var_t) / sw
+    mse, mae = se / sw, sa / sw
+    r2 = 1 - mse / var if var > 0 else float("nan")
+    rmsle = math.sqrt(sl / sw) if nlog == 0 and sw == sw else float("nan")
+    mrd = mse
+    if distribution is not None and distribution.name not in ("gaussian",) and ndev == 0:
+        mrd = sd / sw
+    return ModelMetrics(model_category="Regression", MSE=mse, RMSE=math.sqrt(mse), mae=mae,
+                        rmsle=rmsle, r2=r2, mean_residual_deviance=mrd, nobs=int(n))
 
 
 def _auc_from_sorted(pos, neg):
@@ -125,29 +151,40 @@ def _auc_from_sorted(pos, neg):
     return float(auc), float(aucpr), tp, fp
 
 
-@_sharded_rows("y", "p1", "w")
 def binomial_metrics(y, p1, w=None, domain=("0", "1"), nbins_thresholds: int = 400) -> ModelMetrics:
-    """y in {0,1}; p1 = P(class 1)."""
+    """y in {0,1}; p1 = P(class 1). Single process: exact ROC/PR AUC over the distinct scores. Row-sharded:
+    ROC/PR from the merged score-lattice histogram (no row is gathered). Threshold table and gains/lift
+    come from the lattice in both cases, so they are identical however the rows are split."""
     y, p1 = y.double(), p1.double()
     w = _w(w, y.numel(), y.device)
     ok = ~torch.isnan(y) & (w > 0)
     y, p1, w = y[ok], p1[ok], w[ok]
-    sw = w.sum()
     pc = torch.clamp(p1, 1e-15, 1 - 1e-15)
-    logloss = float(-(w * (y * torch.log(pc) + (1 - y) * torch.log(1 - pc))).sum() / sw)
-    mse = float((w * (y - p1) ** 2).sum() / sw)
-    # exact ROC over distinct scores
-    order = torch.argsort(p1, descending=True)
-    ps, ys, ws = p1[order], y[order], w[order]
-    pos, neg, uniq = _group_sorted(ps, ws * ys, ws * (1 - ys))
-    auc, aucpr, tp, fp = _auc_from_sorted(pos, neg)
-    # thresholds table (H2O keeps <= 400 bins)
-    thr_tab = _threshold_table(uniq, tp, fp, nbins_thresholds)
-    ybar = float((w * y).sum() / sw)
+    v = torch.stack([w.sum(), -(w * (y * torch.log(pc) + (1 - y) * torch.log(1 - pc))).sum(), (w * (y - p1) ** 2).sum(),
+                     (w * y).sum(), torch.tensor(float(y.numel()), dtype=torch.float64, device=y.device)])
+    if _dist():
+        v = _allreduce(v)
+    sw, sll, sse, sy, n = v.tolist()
+    if sw <= 0:
+        sw = float("nan")
+    logloss, mse = sll / sw, sse / sw
+    h = _score_hist(p1, w * y, w * (1 - y))
+    hpos, hneg, huniq = _hist_curve(h)
+    if _dist():
+        auc, aucpr, _, _ = _auc_from_sorted(hpos, hneg)
+    else:
+        order = torch.argsort(p1, descending=True)
+        ps, ys, ws = p1[order], y[order], w[order]
+        pos, neg, _ = _group_sorted(ps, ws * ys, ws * (1 - ys))
+        auc, aucpr, _, _ = _auc_from_sorted(pos, neg)
+    # thresholds table (H2O keeps <= 400 bins) over the lattice's non-empty bins
+    thr_tab = _threshold_table(huniq, torch.cumsum(hpos, 0), torch.cumsum(hneg, 0), nbins_thresholds) \
+        if hpos.numel() else []
+    ybar = sy / sw
     var = ybar * (1 - ybar)
     r2 = 1 - mse / var if var > 0 else float("nan")
     mm = ModelMetrics(model_category="Binomial", MSE=mse, RMSE=math.sqrt(mse), logloss=logloss, AUC=auc,
-                      pr_auc=aucpr, Gini=2 * auc - 1 if auc == auc else float("nan"), r2=r2, nobs=int(y.numel()),
+                      pr_auc=aucpr, Gini=2 * auc - 1 if auc == auc else float("nan"), r2=r2, nobs=int(n),
                       domain=list(domain), thresholds_and_metric_scores=thr_tab)
     if thr_tab:
         best = max(thr_tab, key=lambda r: r["f1"])
@@ -155,7 +192,7 @@ def binomial_metrics(y, p1, w=None, domain=("0", "1"), nbins_thresholds: int = 4
         mm["cm"] = dict(threshold=best["threshold"], table=[[best["tns"], best["fps"]], [best["fns"], best["tps"]]])
         mm["mean_per_class_error"] = 1 - best["mean_per_class_accuracy"]
         mm["max_criteria_and_metric_scores"] = {c: max(thr_tab, key=lambda r: r[c])[c] for c in THRESHOLD_CRITERIA}
-    mm["gains_lift_table"] = gains_lift(y, p1, w)
+    mm["gains_lift_table"] = _gains_lift_hist(hpos, hneg)
     return mm
 
 
@@ -195,6 +232,26 @@ def _threshold_table(uniq, tp, fp, nb):
     return rows
 
 
+def _gains_lift_hist(pos, neg, groups: int = 16):
+    """Gains/lift table (GainsLift.java, 16 groups) from the score-lattice curve (descending bins)."""
+    ws = pos + neg
+    if ws.numel() == 0:
+        return []
+    cw = torch.cumsum(ws, 0)
+    cpos = torch.cumsum(pos, 0)
+    tot, tot_pos = float(cw[-1]), float(cpos[-1])
+    if tot <= 0 or tot_pos <= 0:
+        return []
+    out = []
+    for g in range(1, groups + 1):
+        k = int(torch.searchsorted(cw, torch.tensor(g / groups * tot, dtype=cw.dtype, device=cw.device)).clamp(
+            max=cw.numel() - 1))
+        cum_rate = float(cpos[k] / cw[k])
+        out.append(dict(group=g, cumulative_data_fraction=float(cw[k] / tot), cumulative_capture_rate=float(cpos[k]) / tot_pos,
+                        cumulative_lift=cum_rate / (tot_pos / tot), cumulative_response_rate=cum_rate))
+    return out
+
+
 def gains_lift(y, p1, w, groups: int = 16):
     order = torch.argsort(p1, descending=True)
     ys, ws = y[order], w[order]
@@ -214,37 +271,58 @@ def gains_lift(y, p1, w, groups: int = 16):
     return out
 
 
-@_sharded_rows("y", "probs", "w")
 def multinomial_metrics(y, probs, w=None, domain=None, hit_k: int = 10) -> ModelMetrics:
-    """y: class index; probs [N, K]."""
+    """y: class index; probs [N, K]. Sums, the confusion matrix and hit counts merge by all-reduce."""
     y = y.long() if not torch.is_floating_point(y) else torch.nan_to_num(y, nan=-1).long()
     w = _w(w, y.numel(), y.device)
     ok = (y >= 0) & (w > 0)
     y, probs, w = y[ok], probs[ok].double(), w[ok]
     K = probs.shape[1]
-    sw = w.sum()
     py = torch.clamp(probs.gather(1, y[:, None]).squeeze(1), 1e-15, 1.0)
-    logloss = float(-(w * torch.log(py)).sum() / sw)
     onehot = torch.nn.functional.one_hot(y, K).double()
-    mse = float((w * ((onehot - probs) ** 2).sum(1)).sum() / sw)
     pred = probs.argmax(1)
     from .ops.segment import segment_sum
-    cm = segment_sum(y * K + pred, w, K * K).view(K, K)
-    per_class_err = 1 - torch.diag(cm) / cm.sum(1).clamp(min=1e-300)
+    cm = segment_sum(y * K + pred, w, K * K)
     rank = (probs > py[:, None]).sum(1)
-    hits = [float((w * (rank < k).double()).sum() / sw) for k in range(1, min(hit_k, K) + 1)]
+    hk = min(hit_k, K)
+    hits = torch.stack([(w * (rank < k).double()).sum() for k in range(1, hk + 1)])
+    v = torch.cat([torch.stack([w.sum(), -(w * torch.log(py)).sum(), (w * ((onehot - probs) ** 2).sum(1)).sum(),
+                                torch.tensor(float(y.numel()), dtype=torch.float64, device=y.device)]), hits, cm])
+    if _dist():
+        v = _allreduce(v)
+    sw, sll, sse, n = v[:4].tolist()
+    if sw <= 0:
+        sw = float("nan")
+    hits = (v[4:4 + hk] / sw).tolist()
+    cm = v[4 + hk:].view(K, K)
+    per_class_err = 1 - torch.diag(cm) / cm.sum(1).clamp(min=1e-300)
     auc = multinomial_auc(y, probs, w) if K <= 50 else float("nan")
-    return ModelMetrics(model_category="Multinomial", MSE=mse, RMSE=math.sqrt(mse), logloss=logloss,
+    mse = sse / sw
+    return ModelMetrics(model_category="Multinomial", MSE=mse, RMSE=math.sqrt(mse), logloss=sll / sw,
                         mean_per_class_error=float(per_class_err.mean()), cm=dict(table=cm.cpu().tolist()),
-                        hit_ratio_table=hits, nobs=int(y.numel()), domain=domain, AUC=auc)
+                        hit_ratio_table=hits, nobs=int(n), domain=domain, AUC=auc)
 
 
 def multinomial_auc(y, probs, w):
-    """Macro one-vs-rest AUC (H2O ``MultinomialAucType.MACRO_OVR``)."""
+    """Macro one-vs-rest AUC (H2O ``MultinomialAucType.MACRO_OVR``): exact per class in one process; from
+    merged per-class score-lattice histograms when the rows are sharded."""
     K = probs.shape[1]
+    dist = _dist()
+    if dist:
+        # every rank must take the same per-class skip decision: global class totals first
+        tot = _allreduce(torch.stack([torch.stack([(w * (y == k).double()).sum(), w.sum()]) for k in range(K)]))
+    nb = max(1 << 12, min(1 << 16, (1 << 19) // max(K, 1)))
     aucs = []
     for k in range(K):
         yk = (y == k).double()
+        if dist:
+            pk, wt = float(tot[k, 0]), float(tot[k, 1])
+            if pk == 0 or pk == wt:
+                continue
+            h = _score_hist(probs[:, k], w * yk, w * (1 - yk), nb)
+            pos, neg, _ = _hist_curve(h)
+            aucs.append(_auc_from_sorted(pos, neg)[0])
+            continue
         if yk.sum() == 0 or yk.sum() == yk.numel():
             continue
         order = torch.argsort(probs[:, k], descending=True)
@@ -293,19 +371,23 @@ def clustering_metrics(X, centers, assign, w=None, chunk: int = 1 << 20) -> Mode
                         withinss=within.cpu().tolist(), size=size.cpu().tolist(), nobs=n)
 
 
-@_sharded_rows("score", "w")
+def _sum_count(x: torch.Tensor):
+    v = torch.stack([x.double().sum(), torch.tensor(float(x.numel()), dtype=torch.float64, device=x.device)])
+    if _dist():
+        v = _allreduce(v)
+    return float(v[0]), int(v[1])
+
+
 def anomaly_metrics(score, w=None) -> ModelMetrics:
-    s = score.double()
-    return ModelMetrics(model_category="AnomalyDetection", mean_score=float(s.mean()), nobs=int(s.numel()))
+    s, n = _sum_count(score)
+    return ModelMetrics(model_category="AnomalyDetection", mean_score=s / max(n, 1), nobs=n)
 
 
-@_sharded_rows("err")
 def autoencoder_metrics(err) -> ModelMetrics:
-    e = err.double()
-    return ModelMetrics(model_category="AutoEncoder", MSE=float(e.mean()), RMSE=math.sqrt(float(e.mean())), nobs=int(e.numel()))
+    s, n = _sum_count(err)
+    return ModelMetrics(model_category="AutoEncoder", MSE=s / max(n, 1), RMSE=math.sqrt(s / max(n, 1)), nobs=n)
 
 
-@_sharded_rows("y", "preds", "w")
 def make_metrics(category: str, y, preds, w=None, domain=None, distribution=None) -> ModelMetrics:
     """preds: regression -> [N] mean; binomial -> [N] p1 or [N,2]; multinomial -> [N,K] probs."""
     if category == "Binomial":

@@ -21,7 +21,7 @@ import torch
 import torch.distributed as dist
 
 _tls = threading.local()
-_stats = dict(calls=0, bytes=0)
+_stats = dict(calls=0, bytes=0, row_gathers=0)
 
 
 def world_active() -> bool:
@@ -56,7 +56,7 @@ def stats(reset: bool = False) -> dict:
     """Collective call / byte counters (bench.py reports them per tree)."""
     out = dict(_stats)
     if reset:
-        _stats.update(calls=0, bytes=0)
+        _stats.update(calls=0, bytes=0, row_gathers=0)
     return out
 
 
@@ -188,6 +188,7 @@ def all_gather_cat(t: torch.Tensor, dim: int = 0, force: bool = False) -> torch.
         return t
     if _staged(t):
         return all_gather_cat(t.cpu(), dim, force).to(t.device)
+    _stats["row_gathers"] += 1
     n = torch.tensor([t.shape[dim]], device=t.device)
     sizes = [torch.zeros_like(n) for _ in range(world())]
     dist.all_gather(sizes, n)

@@ -170,3 +170,81 @@ def test_oom_in_sharded_build_fails_every_rank_fast():
         p.join(30)
     assert res[0][1] != "returned" and res[1][1] == "RuntimeError", res
     assert all(r[2] < 30 for r in res), res
+
+
+def _metrics_inputs(n=5000, seed=5):
+    g = torch.Generator().manual_seed(seed)
+    yb = (torch.rand(n, generator=g) < 0.4).double()
+    p1 = torch.sigmoid(2 * yb - 1 + torch.randn(n, generator=g))
+    w = torch.rand(n, generator=g) + 0.5
+    yr = torch.randn(n, generator=g) * 3
+    pr = yr + torch.randn(n, generator=g)
+    K = 4
+    y3 = torch.randint(0, K, (n,), generator=g)
+    logits = torch.randn(n, K, generator=g) + 1.5 * torch.nn.functional.one_hot(y3, K)
+    probs = torch.softmax(logits, 1).double()
+    score = torch.rand(n, generator=g)
+    return yb, p1, w, yr, pr, y3, probs, score
+
+
+def _all_metrics(sl):
+    from llama_github_io_amd import metrics as M
+    yb, p1, w, yr, pr, y3, probs, score = (t[sl] for t in _metrics_inputs())
+    b = M.binomial_metrics(yb, p1, w)
+    r = M.regression_metrics(yr, pr, w)
+    m = M.multinomial_metrics(y3, probs, w, domain=["a", "b", "c", "d"])
+    a = M.anomaly_metrics(score)
+    return dict(auc=b["AUC"], aucpr=b["pr_auc"], logloss=b["logloss"], mse=b["MSE"], mpce=b["mean_per_class_error"],
+                thr=[r_["threshold"] for r_ in b["thresholds_and_metric_scores"]],
+                lift=[g_["cumulative_lift"] for g_ in b["gains_lift_table"]],
+                rmse=r["RMSE"], mae=r["mae"], r2=r["r2"], rmsle=r["rmsle"], mlogloss=m["logloss"], mauc=m["AUC"],
+                mpce3=m["mean_per_class_error"], hits=m["hit_ratio_table"], cm=m["cm"]["table"],
+                ascore=a["mean_score"], n=b["nobs"])
+
+
+def _metrics_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import torch.distributed as dist
+    from llama_github_io_amd.parallel import collectives as coll
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n = _metrics_inputs()[0].numel()
+        coll.stats(reset=True)
+        out = _all_metrics(slice(rank * n // world, (rank + 1) * n // world))
+        out["row_gathers"] = coll.stats()["row_gathers"]
+        if rank == 0:
+            q.put(out)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_metrics_merge_without_row_gathers(world):
+    """Metrics of row-sharded predictions merge per-rank sufficient statistics (AUC2-style fixed score
+    lattice, weighted sums, confusion matrix) — no collective ever gathers a row tensor — and match the
+    single-process metrics (AUC within the lattice resolution)."""
+    import socket
+    single = _all_metrics(slice(None))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_metrics_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = q.get(timeout=300)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert out.pop("row_gathers") == 0
+    for k in ("auc", "aucpr", "mauc"):
+        assert abs(out[k] - single[k]) < 2e-5, (k, out[k], single[k])
+    for k in ("logloss", "mse", "mpce", "rmse", "mae", "r2", "rmsle", "mlogloss", "mpce3", "ascore"):
+        assert (out[k] != out[k] and single[k] != single[k]) or \
+            abs(out[k] - single[k]) <= 1e-12 * max(1.0, abs(single[k])), (k, out[k], single[k])
+    assert out["n"] == single["n"]
+    assert np.allclose(out["thr"], single["thr"], rtol=0, atol=0) and np.allclose(out["lift"], single["lift"], rtol=1e-12)
+    assert np.allclose(out["hits"], single["hits"], rtol=1e-12) and np.allclose(out["cm"], single["cm"], rtol=1e-12)
