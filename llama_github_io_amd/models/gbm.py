@@ -82,6 +82,25 @@ class GBMModel(SharedTreeModel):
         return out
 
 
+def _global_quantile(v: torch.Tensor, alpha) -> float:
+    """Quantile (linear interpolation at alpha * (n - 1), as torch.quantile) or, with alpha None, the lower
+    median (as torch.median) of a row-sharded column; NaN if any value is NaN. Exact, no row gather."""
+    from ..parallel.order_stats import order_statistics
+    v = v.double()
+    st = torch.tensor([float(v.numel()), float(torch.isnan(v).sum())], dtype=torch.float64)
+    if coll.is_dist():
+        st = coll.all_reduce_(st.to(coll.comm_device())).cpu()
+    n, nnan = int(st[0]), int(st[1])
+    if n == 0 or nnan:
+        return float("nan")
+    if alpha is None:
+        return order_statistics(v, [(n - 1) // 2 + 1])[0]
+    pos = alpha * (n - 1)
+    lo, hi = math.floor(pos), math.ceil(pos)
+    a, b = order_statistics(v, [lo + 1, hi + 1])
+    return a + (pos - lo) * (b - a)
+
+
 class GBMTrainer(SharedTreeTrainer):
     algo = "gbm"
     mode = T.MODE_SE
@@ -120,11 +139,11 @@ class GBMTrainer(SharedTreeTrainer):
         else:
             init = np.array([self.dist.init_f(self.y, w, self.offset, reduce=coll.all_reduce_scalar)])
             if self.dname in ORDER_STAT_DISTS:
-                yv = coll.gather_rows(self.y)          # order statistic of the GLOBAL response
+                # order statistic of the GLOBAL response (exact refinement over the shards, no row gather)
                 if self.dname == "quantile":
-                    init = np.array([float(torch.quantile(yv.double(), self.p["quantile_alpha"]))])
+                    init = np.array([_global_quantile(self.y, float(self.p["quantile_alpha"]))])
                 else:
-                    init = np.array([float(torch.median(yv.double()))])
+                    init = np.array([_global_quantile(self.y, None)])
         self.init = init
         model.init_f = init.tolist()
         self.f = torch.tensor(init, dtype=torch.float32, device=dev).repeat(N, 1).contiguous()
@@ -155,8 +174,7 @@ class GBMTrainer(SharedTreeTrainer):
         f = self.f[:, k]
         if k == 0 and self.dname == "huber":
             self._flush_pending()
-            r = coll.gather_rows((self.y - f).abs())
-            self.dist.huber_delta = float(torch.quantile(r.double()[: 1 << 24], self.p["huber_alpha"]))
+            self.dist.huber_delta = _global_quantile((self.y - f).abs(), float(self.p["huber_alpha"]))
         if self._fused():
             # one HIP pass: previous tree's f update + sampling + residuals + leaf terms + scale maxima
             from ..ops import _native as nat
@@ -241,12 +259,23 @@ class GBMTrainer(SharedTreeTrainer):
         diff = (self.y - self.f[:, k]).double()
         a0 = self.aux[0] if self.aux.shape[0] == 4 and self.aux.shape[1] == self.N else self.aux[:, 0]
         w = (a0 if self.w_eff is None else self.w_eff).double()
-        if coll.is_dist():
-            # per-leaf weighted order statistics need every row of the leaf: gather (leaf, residual, weight)
-            # from the shards (leaf ids are global: every rank built the same tree)
-            full = coll.gather_rows(torch.stack([leaf.double(), diff, w], 1))
-            leaf, diff, w = full[:, 0].long(), full[:, 1], full[:, 2]
         alpha = self.p["quantile_alpha"] if self.dname == "quantile" else 0.5
+        if coll.is_dist():
+            # per-leaf weighted order statistics over every shard's rows of the leaf (leaf ids are global:
+            # every rank built the same tree): grouped histogram refinement, no row gather
+            from ..parallel.order_stats import group_order_statistics
+            tot = segment_sum(leaf, w, L)
+            tot = coll.all_reduce_(tot.to(coll.comm_device())).to(tot.device)
+            qv = group_order_statistics(diff, leaf, L, [alpha * float(t) for t in tot.cpu()], w)
+            q = torch.tensor([0.0 if x != x else x for x in qv], dtype=torch.float64, device=diff.device)
+            if self.dname == "huber":
+                delta = self.dist.huber_delta
+                r = diff - q[leaf]
+                c = torch.sign(r) * torch.clamp(r.abs(), max=delta)
+                s = segment_sum(leaf, w * c, L)
+                s = coll.all_reduce_(s.to(coll.comm_device())).to(s.device)
+                q = q + s / tot.clamp(min=1e-300)
+            return q
         order = torch.argsort(diff)
         leaf_s = leaf[order]
         order2 = torch.argsort(leaf_s, stable=True)

@@ -1,9 +1,11 @@
 """Quantiles (reference: ``hex/quantile/Quantile.java``, ``QuantileModel.java``: probs,
 ``combine_method`` INTERPOLATE / AVERAGE / LOW / HIGH, ``weights_column``).
 
-H2O computes exact quantiles by iterative histogram refinement over the distributed column; on one
-device the column fits in HBM, so a single device sort gives the exact order statistics. With
-weights the quantile is taken on the cumulative weight (rows with weight w count w times).
+H2O computes exact quantiles by iterative histogram refinement over the distributed column. In one
+process the column fits in HBM, so a single device sort gives the exact order statistics; a row-sharded
+column runs the refinement (``parallel/order_stats.py``: <= 6 passes, one small all-reduce each) and
+gets the same values without gathering rows. With weights the quantile is taken on the cumulative
+weight (rows with weight w count w times).
 """
 from __future__ import annotations
 
@@ -23,6 +25,9 @@ def weighted_quantiles(v: torch.Tensor, probs, method: str = "interpolate", w: t
         ok &= ~torch.isnan(w) & (w > 0)
     x = v[ok]
     p = torch.as_tensor(probs, dtype=torch.float64, device=v.device)
+    from ..parallel import collectives as coll
+    if coll.is_dist():
+        return _dist_quantiles(x, p, method, None if w is None else w[ok])
     if x.numel() == 0:
         return torch.full((p.numel(),), float("nan"), dtype=torch.float64, device=v.device)
     if w is None:
@@ -55,6 +60,40 @@ def weighted_quantiles(v: torch.Tensor, probs, method: str = "interpolate", w: t
     if method == "average":
         return torch.where(lo == hi, a, (a + b) / 2)
     return a + (pos - torch.floor(pos)) * (b - a)
+
+
+def _dist_quantiles(x, p, method, ws):
+    """Row-sharded ``weighted_quantiles``: the same rank arithmetic, order statistics by refinement."""
+    from ..parallel import collectives as coll
+    from ..parallel.order_stats import order_statistics
+    tot = torch.tensor([float(x.numel()), float(ws.sum()) if ws is not None else 0.0], dtype=torch.float64)
+    tot = coll.all_reduce_(tot.to(coll.comm_device())).cpu()
+    n = tot[0].item()
+    if n == 0:
+        return torch.full((p.numel(),), float("nan"), dtype=torch.float64, device=x.device)
+    pc = p.cpu()
+    if ws is None:
+        pos = pc * (n - 1)
+        lo = torch.floor(pos).clamp(0, n - 1)
+        hi = torch.ceil(pos).clamp(0, n - 1)
+        tl, th = (lo + 1).tolist(), (hi + 1).tolist()
+    else:
+        total = tot[1].item()
+        pos = pc * (total - 1)
+        tl, th = (torch.floor(pos) + 1).tolist(), (torch.ceil(pos) + 1).tolist()
+        lo = torch.floor(pos)
+    vals = order_statistics(x, tl + th, ws)
+    a = torch.tensor(vals[: len(tl)], dtype=torch.float64)
+    b = torch.tensor(vals[len(tl):], dtype=torch.float64)
+    if method == "low":
+        out = a
+    elif method == "high":
+        out = b
+    elif method == "average":
+        out = torch.where(a == b, a, (a + b) / 2)
+    else:
+        out = a + (pos - lo) * (b - a)
+    return out.to(x.device)
 
 
 class QuantileModel(Model):

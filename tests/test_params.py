@@ -38,7 +38,6 @@ def test_unknown_parameter_raises(fr):
 
 
 @pytest.mark.parametrize("algo,param,value", [
-    ("word2vec", "word_model", "cbow"),
     ("glm", "rand_link", ["identity"]),
 ])
 def test_unsupported_parameter_raises(fr, algo, param, value):
