@@ -40,7 +40,8 @@ class AlgoSpec:
 # sums, gradients, class counts): under a multi-rank cloud they train on the local shard. Every other
 # trainer gets the gathered rows and trains replicated (identical on every rank: the same deterministic
 # program on the same data) — correct everywhere, scaled only where the collectives exist.
-DISTRIBUTED = {"gbm", "drf", "xgboost", "glm", "kmeans", "deeplearning", "naivebayes", "pca"}
+DISTRIBUTED = {"gbm", "drf", "xgboost", "glm", "kmeans", "deeplearning", "naivebayes", "pca", "quantile",
+               "isolationforest", "extendedisolationforest"}
 
 
 def register(name, trainer, supervised=True, defaults=None, **kw):
@@ -98,7 +99,7 @@ def prepare(algo: str, params: dict, x=None, y=None, training_frame=None):
                 u = torch.unique(v)
                 if sharded:                      # distinct codes over every shard
                     from ..parallel import dframe
-                    u = torch.unique(dframe.gather_tensor(u.cpu()))
+                    u = torch.unique(dframe.gather_tensor(u.cpu(), bounded=True))
                 if int(u.numel()) > 1:
                     keep.append(n)
             elif c.type == "string":

@@ -17,6 +17,7 @@ from .. import metrics as mm
 from ..parallel import collectives as coll
 from ..ops import tree as T
 from .base import DataInfo
+from ..parallel.order_stats import global_quantile
 from .distributions import ORDER_STAT_DISTS, get_distribution
 from .shared_tree import SharedTreeModel, SharedTreeTrainer
 from ..ops.segment import segment_sum
@@ -82,25 +83,6 @@ class GBMModel(SharedTreeModel):
         return out
 
 
-def _global_quantile(v: torch.Tensor, alpha) -> float:
-    """Quantile (linear interpolation at alpha * (n - 1), as torch.quantile) or, with alpha None, the lower
-    median (as torch.median) of a row-sharded column; NaN if any value is NaN. Exact, no row gather."""
-    from ..parallel.order_stats import order_statistics
-    v = v.double()
-    st = torch.tensor([float(v.numel()), float(torch.isnan(v).sum())], dtype=torch.float64)
-    if coll.is_dist():
-        st = coll.all_reduce_(st.to(coll.comm_device())).cpu()
-    n, nnan = int(st[0]), int(st[1])
-    if n == 0 or nnan:
-        return float("nan")
-    if alpha is None:
-        return order_statistics(v, [(n - 1) // 2 + 1])[0]
-    pos = alpha * (n - 1)
-    lo, hi = math.floor(pos), math.ceil(pos)
-    a, b = order_statistics(v, [lo + 1, hi + 1])
-    return a + (pos - lo) * (b - a)
-
-
 class GBMTrainer(SharedTreeTrainer):
     algo = "gbm"
     mode = T.MODE_SE
@@ -141,9 +123,9 @@ class GBMTrainer(SharedTreeTrainer):
             if self.dname in ORDER_STAT_DISTS:
                 # order statistic of the GLOBAL response (exact refinement over the shards, no row gather)
                 if self.dname == "quantile":
-                    init = np.array([_global_quantile(self.y, float(self.p["quantile_alpha"]))])
+                    init = np.array([global_quantile(self.y, float(self.p["quantile_alpha"]))])
                 else:
-                    init = np.array([_global_quantile(self.y, None)])
+                    init = np.array([global_quantile(self.y, None)])
         self.init = init
         model.init_f = init.tolist()
         self.f = torch.tensor(init, dtype=torch.float32, device=dev).repeat(N, 1).contiguous()
@@ -174,7 +156,7 @@ class GBMTrainer(SharedTreeTrainer):
         f = self.f[:, k]
         if k == 0 and self.dname == "huber":
             self._flush_pending()
-            self.dist.huber_delta = _global_quantile((self.y - f).abs(), float(self.p["huber_alpha"]))
+            self.dist.huber_delta = global_quantile((self.y - f).abs(), float(self.p["huber_alpha"]))
         if self._fused():
             # one HIP pass: previous tree's f update + sampling + residuals + leaf terms + scale maxima
             from ..ops import _native as nat

@@ -22,6 +22,7 @@ import torch
 
 from .. import metrics as mm
 from ..ops import tree as T
+from ..parallel import collectives as coll
 from .base import DataInfo, Model, make_key
 from .shared_tree import SharedTreeModel, SharedTreeTrainer
 
@@ -101,11 +102,14 @@ class IsolationForestTrainer(SharedTreeTrainer):
     def _init_model(self, model):
         model.output["model_category"] = "AnomalyDetection"
         self.aux = torch.zeros(self.N, 4, dtype=torch.float32, device=self.dev)
+        # rows of the WHOLE frame (row-sharded: every rank samples its rows at the same global rate with the
+        # global-index row RNG, and the histograms are all-reduced -> the same trees on every rank)
+        self.N_glob = int(coll.all_reduce_scalar(self.N)) if coll.is_dist() else self.N
 
     def _prepare(self, t, k):
         rate = float(self.p.get("sample_rate", -1))
         if rate <= 0:
-            rate = min(1.0, float(self.p["sample_size"]) / max(1, self.N))
+            rate = min(1.0, float(self.p["sample_size"]) / max(1, self.N_glob))
         ws = self._row_sample(rate, t)
         a = self.aux
         a[:, 0] = ws
@@ -125,13 +129,19 @@ class IsolationForestTrainer(SharedTreeTrainer):
             tree.value = np.where(tree.feat < 0, depth, 0).astype(np.float32)
         model.forest._flat.clear()
         s = model.forest.predict_raw(self.X)[:, 0]
-        model.output["min_path_length"] = int(float(s.min()))
-        model.output["max_path_length"] = int(float(s.max()))
+        mn, mx = float(s.min()), float(s.max())
+        if coll.is_dist():
+            import torch.distributed as dist
+            mn = coll.all_reduce_scalar(mn, op=dist.ReduceOp.MIN)
+            mx = coll.all_reduce_scalar(mx, op=dist.ReduceOp.MAX)
+        model.output["min_path_length"] = int(mn)
+        model.output["max_path_length"] = int(mx)
         cont = float(self.p.get("contamination", -1))
         if cont > 0:
+            from ..parallel.order_stats import global_quantile
             mn, mx = model.output["min_path_length"], model.output["max_path_length"]
             score = (mx - s.double()) / max(mx - mn, 1)
-            model.output["default_threshold"] = float(torch.quantile(score.cpu(), 1 - cont))
+            model.output["default_threshold"] = global_quantile(score, 1 - cont)
 
     def _training_metrics(self, model):
         P = model._predict_tensor(self.X)
@@ -208,15 +218,30 @@ class ExtendedIsolationForestTrainer:
         ext = int(p["extension_level"])
         if ext < 0 or ext > F - 1:
             raise ValueError(f"extension_level must be in [0, {F - 1}]")
-        S = int(min(p["sample_size"], N))
+        # row-sharded: the sample is drawn over GLOBAL row ids (same RNG on every rank); each rank contributes
+        # its sampled rows and only those S rows are exchanged (the trees are identical on every rank)
+        dist_ = coll.is_dist()
+        row0 = coll.row_offset(N) if dist_ else 0
+        Ng = int(coll.all_reduce_scalar(N)) if dist_ else N
+        S = int(min(p["sample_size"], Ng))
         limit = int(math.ceil(math.log2(max(S, 2))))
         Xh = torch.nan_to_num(X, nan=0.0).T.double()
         model = ExtendedIsolationForestModel(model_key or make_key("eif"), p, info)
         model.device = X.device
         model.output["sample_size"] = S
         for t in range(int(p["ntrees"])):
-            idx = torch.as_tensor(rng.choice(N, S, replace=False), device=X.device)
-            xs = Xh.index_select(0, idx).cpu().numpy()
+            gidx = rng.choice(Ng, S, replace=False)
+            if dist_:
+                mine = np.nonzero((gidx >= row0) & (gidx < row0 + N))[0]
+                loc = torch.as_tensor(gidx[mine] - row0, device=X.device)
+                part = torch.cat([torch.as_tensor(mine, dtype=torch.float64, device=X.device)[:, None],
+                                  Xh.index_select(0, loc)], 1)
+                dev_c = coll.comm_device()
+                allp = coll.all_gather_cat(part.to(dev_c), 0, bounded=True).cpu().numpy()
+                xs = allp[np.argsort(allp[:, 0], kind="stable"), 1:]
+            else:
+                idx = torch.as_tensor(gidx, device=X.device)
+                xs = Xh.index_select(0, idx).cpu().numpy()
             model.trees.append(_grow_eif(xs, limit, ext, rng))
         model.output["ntrees"] = len(model.trees)
         P = model._predict_tensor(X)

@@ -210,7 +210,8 @@ class SharedTreeTrainer:
             # sampled rows it owns, and the edges come from the gathered sample
             n_glob = coll.exclusive_offset(N)[1]
             Xl = sample_rows(X, bsample, self.seed, self.row0, n_glob)
-            Xs = coll.all_gather_cat(Xl.contiguous(), dim=1)
+            # (a sample of <= the binning sample size, not the frame: tree_method="exact" samples every row)
+            Xs = coll.all_gather_cat(Xl.contiguous(), dim=1, bounded=bsample < (1 << 40))
             self.binning = fit_binning(Xs, info.iscat, info.nlevels, max_bins=max_bins, seed=self.seed,
                                        max_cat_bins=int(p.get("nbins_cats") or 1024), presampled=True)
         else:

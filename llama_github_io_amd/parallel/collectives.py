@@ -181,14 +181,17 @@ def exclusive_offset(n_local: int) -> tuple:
     return int(sum(counts[:rank()])), int(sum(counts))
 
 
-def all_gather_cat(t: torch.Tensor, dim: int = 0, force: bool = False) -> torch.Tensor:
+def all_gather_cat(t: torch.Tensor, dim: int = 0, force: bool = False, bounded: bool = False) -> torch.Tensor:
     """Variable-size all-gather along ``dim`` (rank order). ``force`` gathers even inside a
-    :func:`replicated` block (frame-level gathers of sharded frames)."""
+    :func:`replicated` block (frame-level gathers of sharded frames). ``bounded``: the caller gathers a
+    fixed-size sample (e.g. 256 rows per isolation tree), not rows in proportion to the frame — it is not
+    counted in ``stats()['row_gathers']``."""
     if not (world_active() if force else is_dist()):
         return t
     if _staged(t):
-        return all_gather_cat(t.cpu(), dim, force).to(t.device)
-    _stats["row_gathers"] += 1
+        return all_gather_cat(t.cpu(), dim, force, bounded).to(t.device)
+    if not bounded:
+        _stats["row_gathers"] += 1
     n = torch.tensor([t.shape[dim]], device=t.device)
     sizes = [torch.zeros_like(n) for _ in range(world())]
     dist.all_gather(sizes, n)

@@ -140,8 +140,10 @@ def gather_frame(fr):
         return H2OFrame._from_columns([gather_column(c) for c in fr._cols.values()])
 
 
-def gather_tensor(t: torch.Tensor, dim: int = 0) -> torch.Tensor:
-    return coll.all_gather_cat(t.contiguous(), dim, force=True)
+def gather_tensor(t: torch.Tensor, dim: int = 0, bounded: bool = False) -> torch.Tensor:
+    """Concatenate every rank's ``t``; ``bounded``: t is a per-rank summary whose size does not grow with
+    the rows (distinct codes, a fixed-size sample)."""
+    return coll.all_gather_cat(t.contiguous(), dim, force=True, bounded=bounded)
 
 
 # ------------------------------------------------------------------------------------------------

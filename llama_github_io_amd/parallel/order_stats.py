@@ -108,3 +108,21 @@ def order_statistics(v: torch.Tensor, targets, w: torch.Tensor | None = None) ->
     """Values at cumulative-weight targets (1-based: target T = the first value whose cumulative weight
     reaches T; unweighted rank r is target r + 1) of the column ``v`` (NaN-free) split over the ranks."""
     return [group_order_statistics(v, None, 1, [t], w)[0] for t in targets]
+
+
+def global_quantile(v: torch.Tensor, alpha) -> float:
+    """Quantile (linear interpolation at alpha * (n - 1), as torch.quantile) or, with alpha None, the lower
+    median (as torch.median) of a row-sharded column; NaN if any value is NaN. Exact, no row gather."""
+    v = v.double()
+    st = torch.tensor([float(v.numel()), float(torch.isnan(v).sum())], dtype=torch.float64)
+    if coll.is_dist():
+        st = coll.all_reduce_(st.to(coll.comm_device())).cpu()
+    n, nnan = int(st[0]), int(st[1])
+    if n == 0 or nnan:
+        return float("nan")
+    if alpha is None:
+        return order_statistics(v, [(n - 1) // 2 + 1])[0]
+    pos = alpha * (n - 1)
+    lo, hi = math.floor(pos), math.ceil(pos)
+    a, b = order_statistics(v, [lo + 1, hi + 1])
+    return a + (pos - lo) * (b - a)

@@ -30,10 +30,11 @@ def _write_csv(path, n=1200, seed=0):
     yr = 2 * x[:, 0] + np.sin(3 * x[:, 1]) + 0.3 * rng.standard_t(3, n)
     y3 = np.array(["k0", "k1", "k2"])[np.clip((logit > -0.5).astype(int) + (logit > 1.0).astype(int), 0, 2)]
     with open(path, "w") as f:
-        f.write("x0,x1,x2,x3,cat,yb,yr,y3\n")
+        f.write("x0,x1,x2,x3,cat,yb,yr,y3,w\n")
+        wts = rng.integers(0, 4, n) * 0.5
         for i in range(n):
             xs = ",".join("" if (i % 97 == 5 and j == 2) else f"{x[i, j]:.6f}" for j in range(4))
-            f.write(f"{xs},{cat[i]},{yb[i]},{yr[i]:.6f},{y3[i]}\n")
+            f.write(f"{xs},{cat[i]},{yb[i]},{yr[i]:.6f},{y3[i]},{wts[i]}\n")
 
 
 CASES = {
@@ -56,6 +57,12 @@ CASES = {
     "deeplearning_reg": ("deeplearning", dict(hidden=[6], epochs=1, seed=2, mini_batch_size=50, activation="Tanh",
                                               adaptive_rate=False, rate=0.01, momentum_start=0.5, score_interval=1e9), "yr"),
     "coxph_gathered": ("isotonicregression", dict(), "yr"),     # a trainer without collectives (gathered rows)
+    "quantile": ("quantile", dict(probs=[0.01, 0.1, 0.5, 0.77, 0.99]), None),
+    "quantile_weighted_low": ("quantile", dict(probs=[0.25, 0.5, 0.9], combine_method="low"), None),
+    "isolationforest": ("isolationforest", dict(ntrees=6, seed=5, contamination=0.05), None),
+    "extendedisolationforest": ("extendedisolationforest", dict(ntrees=5, seed=5, extension_level=2), None),
+    "gbm_quantile_weighted": ("gbm", dict(ntrees=3, max_depth=3, seed=5, distribution="quantile", quantile_alpha=0.3,
+                                          weights_column="w"), "yr"),
 }
 
 METRIC_KEYS = ("AUC", "logloss", "MSE", "RMSE", "mae", "mean_per_class_error", "tot_withinss", "r2")
@@ -77,9 +84,19 @@ def _run_cases(csv, names, out_path):
     for name in names:
         algo, params, y = CASES[name]
         x = ["x0", "x1", "x2", "x3", "cat"] if algo != "isotonicregression" else ["x0"]
-        if algo in ("kmeans", "pca"):
+        if algo in ("kmeans", "pca", "quantile", "extendedisolationforest"):
             x = ["x0", "x1", "x2", "x3"]
-        m = builder.train(algo, dict(params), x=x, y=y, training_frame=fr)
+        pp = dict(params)
+        if name == "quantile_weighted_low":
+            pp["weights_column"] = "w"
+        import llama_github_io_amd.parallel.collectives as coll
+        g0 = coll.stats()["row_gathers"]
+        m = builder.train(algo, pp, x=x, y=y, training_frame=fr)
+        res.setdefault("row_gathers", {})[name] = coll.stats()["row_gathers"] - g0
+        if algo == "quantile":
+            q = m.output["quantiles"]
+            res[name] = dict(pred=[q[c] for c in sorted(q)], metrics={}, cv={})
+            continue
         P = m.predict(fr).as_data_frame()
         num = P.select_dtypes(include=[np.number]).to_numpy(dtype=np.float64)
         tm = m.output.get("training_metrics") or {}
@@ -126,6 +143,10 @@ def _compare(single, sharded, world):
     assert sharded["nacnt"] == single["nacnt"]
     assert np.allclose(sharded["mean_x0"], single["mean_x0"], rtol=1e-12, atol=1e-14)
     assert np.allclose(sharded["sd_x1"], single["sd_x1"], rtol=1e-12, atol=1e-14)
+    from llama_github_io_amd.models.builder import DISTRIBUTED
+    # trainers that reduce over the shards never gather rows (no all-gather proportional to the frame)
+    gathered = {n: c for n, c in sharded["row_gathers"].items() if CASES[n][0] in DISTRIBUTED and c}
+    assert not gathered, gathered
     for name in CASES:
         if name not in single:
             continue
