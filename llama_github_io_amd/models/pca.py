@@ -89,6 +89,30 @@ def _randomized(Z, k, iters, gen):
     return (s[:k] ** 2), Vt[:k].T
 
 
+def _randomized_sharded(Z, k, iters, gen):
+    """``_randomized`` over row shards: the range finder's orthonormalisation works on the all-reduced
+    q x q Gram of Y (Q = Y M with M = U S^-1/2 from its eigendecomposition), so Q never leaves its rows
+    and every product the method needs (Z^T Q, Q^T Z) is a local GEMM plus a small all-reduce."""
+    N, P = Z.shape
+    Zd = Z.double()
+    q = min(P, k + 10)
+    Om = torch.randn(P, q, dtype=torch.float64, generator=gen).to(Z.device)
+    Y = Zd @ Om
+
+    def ortho(Y):
+        G = coll.all_reduce_(Y.T @ Y)
+        s, U = torch.linalg.eigh(G)
+        keep = s > s.max().clamp(min=1e-300) * 1e-14
+        return U[:, keep] / s[keep].sqrt()[None, :]
+    for _ in range(min(iters, 5)):
+        M = ortho(Y)
+        Y = Zd @ (coll.all_reduce_(Zd.T @ Y) @ M)
+    M = ortho(Y)
+    B = M.T @ coll.all_reduce_(Y.T @ Zd)
+    _, s, Vt = torch.linalg.svd(B, full_matrices=False)
+    return (s[:k] ** 2), Vt[:k].T
+
+
 class PCAModel(Model):
     algo = "pca"
 
@@ -163,11 +187,10 @@ class PCATrainer:
             ev, V = _eig_top(G, k)
         elif method == "power":
             ev, V = _power(Zw, k, int(p["max_iterations"]), gen)
+        elif coll.is_dist():
+            ev, V = _randomized_sharded(Zw, k, int(p["max_iterations"]), gen)
         else:
-            # randomized range finder needs a QR over all rows: run it on the gathered rows
-            Zg = coll.gather_rows(Zw)
-            with coll.replicated():
-                ev, V = _randomized(Zg, k, int(p["max_iterations"]), gen)
+            ev, V = _randomized(Zw, k, int(p["max_iterations"]), gen)
         # sign convention: largest |loading| positive (stable across methods)
         sgn = torch.sign(V.gather(0, V.abs().argmax(0, keepdim=True)))
         V = V * torch.where(sgn == 0, torch.ones_like(sgn), sgn)
@@ -224,5 +247,10 @@ class SVDTrainer(PCATrainer):
         if self.p.get("keep_u", True):
             from ..frame import H2OFrame
             U = (Z.double() @ V) / d.clamp(min=1e-300)[None, :]
-            fr = H2OFrame.from_tensor(coll.gather_rows(U.float()), [f"u{i + 1}" for i in range(U.shape[1])])
+            # U keeps the training frame's row distribution (a sharded frame when the rows are sharded)
+            import contextlib
+            from ..parallel import dframe
+            ctx = dframe.shard_ctx(dframe.make_shard(U.shape[0])) if coll.is_dist() else contextlib.nullcontext()
+            with ctx:
+                fr = H2OFrame.from_tensor(U.float(), [f"u{i + 1}" for i in range(U.shape[1])])
             model.output["u_key"] = fr.frame_id

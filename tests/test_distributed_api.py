@@ -57,6 +57,9 @@ CASES = {
     "deeplearning_reg": ("deeplearning", dict(hidden=[6], epochs=1, seed=2, mini_batch_size=50, activation="Tanh",
                                               adaptive_rate=False, rate=0.01, momentum_start=0.5, score_interval=1e9), "yr"),
     "coxph_gathered": ("isotonicregression", dict(), "yr"),     # a trainer without collectives (gathered rows)
+    "svd_gram": ("svd", dict(nv=3, transform="STANDARDIZE"), None),
+    "svd_randomized": ("svd", dict(nv=2, svd_method="Randomized", transform="DEMEAN", seed=3), None),
+    "pca_randomized": ("pca", dict(k=2, transform="STANDARDIZE", pca_method="Randomized", seed=3), None),
     "quantile": ("quantile", dict(probs=[0.01, 0.1, 0.5, 0.77, 0.99]), None),
     "quantile_weighted_low": ("quantile", dict(probs=[0.25, 0.5, 0.9], combine_method="low"), None),
     "isolationforest": ("isolationforest", dict(ntrees=6, seed=5, contamination=0.05), None),
@@ -84,7 +87,7 @@ def _run_cases(csv, names, out_path):
     for name in names:
         algo, params, y = CASES[name]
         x = ["x0", "x1", "x2", "x3", "cat"] if algo != "isotonicregression" else ["x0"]
-        if algo in ("kmeans", "pca", "quantile", "extendedisolationforest"):
+        if algo in ("kmeans", "pca", "svd", "quantile", "extendedisolationforest"):
             x = ["x0", "x1", "x2", "x3"]
         pp = dict(params)
         if name == "quantile_weighted_low":
