@@ -457,9 +457,11 @@ __global__ __launch_bounds__(256) void k_split_find(
     const double* __restrict__ hist, int slot_doubles, const int* __restrict__ meta, int F,
     const int* __restrict__ nbins_f, const int* __restrict__ iscat_f, const int* __restrict__ mono_f,
     SplitParams p, int level, Cand* __restrict__ cand, double* __restrict__ root_w,
-    const float* __restrict__ edges /*[F][255] global bin edges (inf padded) or null*/, int adapt_nb, int f0) {
+    const float* __restrict__ edges /*[F][255] global bin edges (inf padded) or null*/, int adapt_nb, int f0,
+    int FL) {
   // f0: global id of this launch's first feature (feature-sliced row-sharded runs search only the rank's
-  // slice; per-feature arrays arrive offset by f0, the slot holds only the slice, cand is [node][slice])
+  // slice; per-feature arrays arrive offset by f0). FL: features of the slot LAYOUT and of the cand row
+  // stride (the slice width Fs, >= the F features searched here; F everywhere else)
   const int node = blockIdx.x, f = blockIdx.y, t = threadIdx.x;
   if (node >= meta[0]) return;
   __shared__ double sw[256], swy[256], skey[256];
@@ -468,14 +470,14 @@ __global__ __launch_bounds__(256) void k_split_find(
   __shared__ int best_i[256];
 
   const double* slot = hist + (size_t)node * slot_doubles;
-  const double* h = slot + 2 * f;          // bin-major slot: (bin, f) at bin * 2F + 2f
-  const int hs = 2 * F;
+  const double* h = slot + 2 * f;          // bin-major slot: (bin, f) at bin * 2FL + 2f
+  const int hs = 2 * FL;
   const int nb = nbins_f[f];
   const bool cat = iscat_f[f] != 0;
   const int mono = mono_f ? mono_f[f] : 0;
   const double wNA = h[NA_BIN * hs], wyNA = h[NA_BIN * hs + 1];
-  const double naYY = slot[(size_t)F * 2 * NBIN + f];
-  const double wYY = slot[(size_t)F * 2 * NBIN + F];
+  const double naYY = slot[(size_t)FL * 2 * NBIN + f];
+  const double wYY = slot[(size_t)FL * 2 * NBIN + FL];
 
   double w = 0, wy = 0;
   if (t < nb && t < NA_BIN) { w = h[t * hs]; wy = h[t * hs + 1]; }
@@ -621,7 +623,7 @@ __global__ __launch_bounds__(256) void k_split_find(
   }
   const int code = best_i[0];
   const double be = best_e[0];
-  Cand* c = cand + (size_t)node * F + f;
+  Cand* c = cand + (size_t)node * FL + f;
   // categorical bitset: left set = sorted positions < b (empty bins follow the NA direction)
   __shared__ unsigned sbits[8];
   if (t < 8) sbits[t] = 0u;
@@ -1489,14 +1491,15 @@ int h2o_leaf_values(const void* leafsum, int n, int log_link, double scale, doub
 int h2o_split_find(const void* hist, int slot_doubles, const void* meta, int cap, int F, const void* nbins_f,
                    const void* iscat_f, const void* mono_f, double min_w, double msi, double lambda_, double alpha,
                    double gamma, int mode, int random_split, unsigned long long seed, int level, void* cand,
-                   void* root_w, const void* edges, int adapt_nb, int f0, hipStream_t s) {
+                   void* root_w, const void* edges, int adapt_nb, int f0, int FL, hipStream_t s) {
   if (F <= 0 || cap <= 0) return 0;
+  if (FL < F) return (int)hipErrorInvalidValue;
   SplitParams p;
   p.min_w = min_w; p.min_split_improvement = msi; p.lambda = lambda_; p.alpha = alpha; p.gamma = gamma;
   p.mode = mode; p.random_split = random_split; p.seed = seed;
   hipLaunchKernelGGL(k_split_find, dim3(cap, F), dim3(256), 0, s, (const double*)hist, slot_doubles,
                      (const int*)meta, F, (const int*)nbins_f, (const int*)iscat_f, (const int*)mono_f, p, level,
-                     (Cand*)cand, (double*)root_w, (const float*)edges, adapt_nb, f0);
+                     (Cand*)cand, (double*)root_w, (const float*)edges, adapt_nb, f0, FL);
   return (int)hipGetLastError();
 }
 
@@ -1730,13 +1733,13 @@ int h2o_tree_find(const TreePlan* P, int d, hipStream_t s) {
   if (!P->sliced)
     return h2o_split_find(hc, P->slot, P->meta[d], P->caps[d], P->F, P->nbins_f, P->iscat_f, P->mono_f, P->min_w,
                           P->msi, P->lam, P->alpha, P->gamma, P->mode, P->random_split, P->seed, d, P->cand,
-                          d == 0 ? P->rootw : nullptr, P->edges, P->nb_level[d], 0, s);
+                          d == 0 ? P->rootw : nullptr, P->edges, P->nb_level[d], 0, P->F, s);
   const int f0 = P->fs0;
   return h2o_split_find(hc, P->sslot, P->meta[d], P->caps[d], P->fsn, (const int*)P->nbins_f + f0,
                         (const int*)P->iscat_f + f0, P->mono_f ? (const int*)P->mono_f + f0 : nullptr, P->min_w,
                         P->msi, P->lam, P->alpha, P->gamma, P->mode, P->random_split, P->seed, d, P->cand_local,
                         d == 0 ? P->rootw : nullptr, P->edges ? (const float*)P->edges + (size_t)f0 * 255 : nullptr,
-                        P->nb_level[d], f0, s);
+                        P->nb_level[d], f0, (P->sslot - 1) / (2 * NBIN + 1), s);
 }
 
 // decisions (from cand) + plan, then the next level's histogram.

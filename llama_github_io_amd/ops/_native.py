@@ -35,7 +35,7 @@ _HIP_SIGS = {
                        c_int, c_int, c_void_p, c_void_p, c_int, c_void_p],
     "h2o_split_find": [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_double, c_double,
                        c_double, c_double, c_double, c_int, c_int, c_ull, c_int, c_void_p, c_void_p, c_void_p, c_int,
-                       c_int, c_void_p],
+                       c_int, c_int, c_void_p],
     "h2o_split_reduce": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_ull, c_int, c_void_p, c_void_p, c_void_p],
     "h2o_ic_next": [c_void_p] * 6 + [c_int, c_void_p, c_int, c_void_p],
     "h2o_plan": [c_void_p] * 14 + [c_int, c_int, c_double, c_int, c_int, c_void_p],
