@@ -19,6 +19,14 @@ import torch
 
 from .base import DataInfo, Model, make_key
 from ..ops.segment import segment_sum
+from ..parallel import collectives as coll
+
+
+def _merge(t: torch.Tensor) -> torch.Tensor:
+    """Level statistics of a row-sharded frame: the sum over every rank's rows (MRTask reduce)."""
+    if not coll.is_dist():
+        return t
+    return coll.all_reduce_(t.contiguous().to(coll.comm_device())).to(t.device)
 
 TE_DEFAULTS = dict(blending=False, inflection_point=10.0, smoothing=20.0, data_leakage_handling="none", noise=0.01,
                    seed=-1, columns_to_encode=None, keep_original_categorical_columns=True, fold_column=None)
@@ -27,7 +35,7 @@ TE_DEFAULTS = dict(blending=False, inflection_point=10.0, smoothing=20.0, data_l
 class TargetEncoderModel(Model):
     algo = "targetencoder"
 
-    def _encode_col(self, codes, st, K, loo_y=None, fold=None, noise=0.0, gen=None):
+    def _encode_col(self, codes, st, K, loo_y=None, fold=None, noise=0.0, gen=None, row0=0, stream=0):
         num, den = st["num"], st["den"]           # [L, K'] and [L]
         prior = st["prior"]                        # [K']
         dev = codes.device
@@ -54,7 +62,10 @@ class TargetEncoderModel(Model):
             enc = post
         enc = torch.where((n <= 0)[:, None] | na[:, None], prior[None, :].expand_as(enc), enc)
         if noise > 0:
-            enc = enc + (torch.rand(enc.shape, generator=gen, dtype=torch.float64).to(dev) * 2 - 1) * noise
+            # counter-based per (global row, output column) uniforms: the same noise however rows are split
+            cols = [coll.row_uniform(int(gen.initial_seed()), stream * 64 + k, row0, enc.shape[0], dev)
+                    for k in range(enc.shape[1])]
+            enc = enc + (torch.stack(cols, 1) * 2 - 1) * noise
         return enc
 
     def transform(self, frame, as_training=False, noise=None, blending=None, inflection_point=None, smoothing=None):
@@ -76,12 +87,14 @@ class TargetEncoderModel(Model):
                 fold = frame._col(self.params["fold_column"]).as_float().to(dev).long()
             cols = [frame._col(n) for n in frame.names if self.params.get("keep_original_categorical_columns", True)
                     or n not in self.output["encoded_columns"]]
-            for name in self.output["encoded_columns"]:
+            sh = getattr(frame, "_shard", None)
+            row0 = sh.offset if sh is not None else 0
+            for ci, name in enumerate(self.output["encoded_columns"]):
                 if name not in frame.names:
                     continue
                 st = self.stats[name]
                 codes = _codes(frame._col(name), st["domain"], dev)
-                enc = self._encode_col(codes, st, self.K, y, fold, nz if as_training else 0.0, gen)
+                enc = self._encode_col(codes, st, self.K, y, fold, nz if as_training else 0.0, gen, row0, ci)
                 if enc.shape[1] == 1:
                     cols.append(Column(f"{name}_te", "real", enc[:, 0]))
                 else:
@@ -156,7 +169,8 @@ class TargetEncoderTrainer:
         ok = ~torch.isnan(y)
         Y = torch.where(ok[:, None], Y, torch.zeros_like(Y))
         wt = ok.double()
-        prior = (Y * wt[:, None]).sum(0) / wt.sum()
+        ps = _merge(torch.cat([(Y * wt[:, None]).sum(0), wt.sum().reshape(1)]))
+        prior = ps[:-1] / ps[-1]
         fold = None
         if str(p["data_leakage_handling"]).lower().replace("_", "") == "kfold":
             fc = p.get("fold_column") or info.fold       # the builder hands the fold column over in DataInfo
@@ -165,20 +179,24 @@ class TargetEncoderTrainer:
             p["fold_column"] = fc
             fold = torch.nan_to_num(X[info.x.index(fc)]).long()
             cats = [j for j in cats if info.x[j] != fc]
+            fmax = float(fold.max()) if fold.numel() else 0.0
+            if coll.is_dist():
+                import torch.distributed as dist
+                fmax = coll.all_reduce_scalar(fmax, op=dist.ReduceOp.MAX)
+            nf = int(fmax) + 1
         stats = {}
         for j in cats:
             L = len(info.domains[j])
             code = X[j]
             okc = ~torch.isnan(code) & ok
             c = torch.nan_to_num(code).long().clamp(0, max(L - 1, 0))
-            num = segment_sum(c[okc], Y[okc], L)
-            den = segment_sum(c[okc], torch.ones_like(c[okc], dtype=torch.float64), L)
+            num = _merge(segment_sum(c[okc], Y[okc], L))
+            den = _merge(segment_sum(c[okc], torch.ones_like(c[okc], dtype=torch.float64), L))
             st = dict(num=num, den=den, prior=prior, domain=list(info.domains[j]))
             if fold is not None:
-                nf = int(fold.max()) + 1
                 fi = fold[okc] * L + c[okc]
-                st["fold_num"] = segment_sum(fi, Y[okc], nf * L).view(nf, L, -1)
-                st["fold_den"] = segment_sum(fi, torch.ones_like(fi, dtype=torch.float64), nf * L).view(nf, L)
+                st["fold_num"] = _merge(segment_sum(fi, Y[okc], nf * L)).view(nf, L, -1)
+                st["fold_den"] = _merge(segment_sum(fi, torch.ones_like(fi, dtype=torch.float64), nf * L)).view(nf, L)
             stats[info.x[j]] = st
         model = TargetEncoderModel(model_key or make_key("te"), p, info)
         model.device = dev

@@ -60,6 +60,8 @@ CASES = {
     "svd_gram": ("svd", dict(nv=3, transform="STANDARDIZE"), None),
     "svd_randomized": ("svd", dict(nv=2, svd_method="Randomized", transform="DEMEAN", seed=3), None),
     "pca_randomized": ("pca", dict(k=2, transform="STANDARDIZE", pca_method="Randomized", seed=3), None),
+    "targetencoder": ("targetencoder", dict(blending=True, inflection_point=3, smoothing=2), "yb"),
+    "targetencoder_multi": ("targetencoder", dict(), "y3"),
     "quantile": ("quantile", dict(probs=[0.01, 0.1, 0.5, 0.77, 0.99]), None),
     "quantile_weighted_low": ("quantile", dict(probs=[0.25, 0.5, 0.9], combine_method="low"), None),
     "isolationforest": ("isolationforest", dict(ntrees=6, seed=5, contamination=0.05), None),
@@ -156,7 +158,7 @@ def _compare(single, sharded, world):
         a, b = np.asarray(single[name]["pred"]), np.asarray(sharded[name]["pred"])
         assert a.shape == b.shape, name
         tol = 1e-4 if name.startswith(("glm_multinomial", "glm_lambda", "glm_default", "deeplearning")) else 2e-5
-        assert np.allclose(a, b, atol=tol, rtol=tol), (name, np.abs(a - b).max())
+        assert np.allclose(a, b, atol=tol, rtol=tol, equal_nan=True), (name, np.nanmax(np.abs(a - b)))
         for k, v in single[name]["metrics"].items():
             assert abs(v - sharded[name]["metrics"][k]) <= tol * max(1.0, abs(v)), (name, k, v, sharded[name]["metrics"][k])
         for k, v in single[name]["cv"].items():
