@@ -58,7 +58,9 @@ class ANOVAGLMTrainer:
         from .glm import GLMTrainer
         t0 = time.time()
         p = self.p
-        ex = Expander(info, standardize=True, use_all_factor_levels=False).fit(X)
+        from ..parallel import collectives as coll
+        ex = Expander(info, standardize=True, use_all_factor_levels=False).fit(
+            X, reduce=coll.all_reduce_ if coll.is_dist() else None)
         groups = []
         for j in range(info.F):
             if info.iscat[j]:
@@ -95,7 +97,7 @@ class ANOVAGLMTrainer:
         model.full = full
         fam = full.output["family"]
         dev_full = full.output["residual_deviance"]
-        n = int((~torch.isnan(y)).sum())
+        n = int(coll.all_reduce_scalar(float((~torch.isnan(y)).sum())))
         p_full = T.shape[0] + 1
         disp = dev_full / max(n - p_full, 1)
         table = []

@@ -41,7 +41,8 @@ class AlgoSpec:
 # trainer gets the gathered rows and trains replicated (identical on every rank: the same deterministic
 # program on the same data) — correct everywhere, scaled only where the collectives exist.
 DISTRIBUTED = {"gbm", "drf", "xgboost", "glm", "kmeans", "deeplearning", "naivebayes", "pca", "quantile",
-               "isolationforest", "extendedisolationforest", "svd", "targetencoder"}
+               "isolationforest", "extendedisolationforest", "svd", "targetencoder", "gam", "anovaglm",
+               "modelselection"}
 
 
 def register(name, trainer, supervised=True, defaults=None, **kw):

@@ -29,6 +29,7 @@ import time
 import numpy as np
 import torch
 
+from ..parallel import collectives as coll
 from .base import DataInfo, Model, make_key
 
 GAM_DEFAULTS = dict(gam_columns=None, num_knots=None, scale=None, bs=None, knot_ids=None, keep_gam_cols=False,
@@ -207,8 +208,57 @@ def _as_list(v, n, default):
 
 
 def _quantile_knots(x, k):
-    qs = torch.quantile(x[: 1 << 22], torch.linspace(0, 1, int(k), dtype=torch.float64, device=x.device))
-    return torch.unique(qs)
+    """Knots at the k evenly spaced quantiles of the column (exact over every row, row-sharded too)."""
+    from .quantile import weighted_quantiles
+    qs = weighted_quantiles(x, torch.linspace(0, 1, int(k), dtype=torch.float64).tolist())
+    return torch.unique(qs.to(x.device))
+
+
+def _sum_rows(t: torch.Tensor) -> torch.Tensor:
+    """Column sums over every rank's rows."""
+    s = t.sum(0)
+    if coll.is_dist():
+        s = coll.all_reduce_(s.contiguous().to(coll.comm_device())).to(t.device)
+    return s
+
+
+def _global_rows(Xd: torch.Tensor, ids, row0: int) -> torch.Tensor:
+    """Rows at GLOBAL row indices ``ids`` of a row-sharded matrix [N, d] (the owner contributes its row;
+    one all-reduce of k x d values)."""
+    ids = torch.as_tensor(list(ids), dtype=torch.long)
+    out = torch.zeros(len(ids), Xd.shape[1], dtype=Xd.dtype, device=Xd.device)
+    mine = (ids >= row0) & (ids < row0 + Xd.shape[0])
+    if bool(mine.any()):
+        out[mine.to(Xd.device)] = Xd[(ids[mine] - row0).to(Xd.device)]
+    if coll.is_dist():
+        out = coll.all_reduce_(out.to(coll.comm_device())).to(Xd.device)
+    return out
+
+
+def _rows_at_sorted_ranks(Xd: torch.Tensor, ranks, row0: int) -> torch.Tensor:
+    """Rows whose stable sort position by column 0 (ties in global row order) is ``ranks`` — the rows
+    ``Xd[argsort(Xd[:, 0], stable=True)[ranks]]`` of the single-process code, found over row shards with
+    exact order statistics and a tie count instead of a global sort."""
+    from ..parallel.order_stats import order_statistics
+    x = Xd[:, 0].double()
+    out = []
+    for r in ranks:
+        a = order_statistics(x, [int(r) + 1])[0]
+        less = float((x < a).sum())
+        tie = torch.nonzero(x == a).squeeze(1)
+        if coll.is_dist():
+            less = coll.all_reduce_scalar(less)
+            off, _ = coll.exclusive_offset(int(tie.numel()))
+        else:
+            off = 0
+        t = int(r) - int(less)
+        row = torch.zeros(Xd.shape[1], dtype=Xd.dtype, device=Xd.device)
+        if off <= t < off + tie.numel():
+            row = Xd[tie[t - off]].clone()
+        if coll.is_dist():
+            row = coll.all_reduce_(row.to(coll.comm_device())).to(Xd.device)
+        out.append(row)
+    return torch.stack(out, 0)
 
 
 class GAMTrainer:
@@ -242,10 +292,18 @@ class GAMTrainer:
         gam_names = {c for g in groups for c in g}
         lin = [nm for nm in info.x if nm not in gam_names]
         dev = X.device
+        row0 = coll.row_offset(X.shape[1]) if coll.is_dist() else 0
+        n_glob = int(coll.all_reduce_scalar(X.shape[1])) if coll.is_dist() else X.shape[1]
         gams, names, pens, bounds = [], [], [], []
         for gi, (g, k, s, b) in enumerate(zip(groups, nk, sc, bs)):
             cols = [X[col_index[c]].double() for c in g]
-            means = [float(c[~torch.isnan(c)].mean()) for c in cols]
+            means = []
+            for c in cols:
+                okc = ~torch.isnan(c)
+                sm = torch.stack([torch.where(okc, c, torch.zeros_like(c)).sum(), okc.double().sum()])
+                if coll.is_dist():
+                    sm = coll.all_reduce_(sm.to(coll.comm_device())).cpu()
+                means.append(float(sm[0] / sm[1]))
             filled = [torch.nan_to_num(c, nan=mu) for c, mu in zip(cols, means)]
             st = dict(cols=g, bs=b, means=means, scale=s)
             if b == 0:
@@ -260,16 +318,17 @@ class GAMTrainer:
                 d = Xd.shape[1]
                 m = _tp_m(d)
                 exps = _tp_poly_exps(d, m)
-                kn = min(k, Xd.shape[0])
+                kn = min(k, n_glob)
                 if p.get("knot_ids") and gi < len(p["knot_ids"]) and p["knot_ids"][gi] is not None:
                     kid = p["knot_ids"][gi]
                     kid = kid if isinstance(kid, (list, tuple)) else [kid]
-                    ki = torch.as_tensor([int(v) for v in kid], device=dev)
+                    K = _global_rows(Xd, [int(v) for v in kid], row0)
                 else:
-                    ki = torch.unique(torch.round(torch.linspace(0, Xd.shape[0] - 1, kn, dtype=torch.float64, device=dev)).long())
-                    order = torch.argsort(Xd[:, 0], stable=True)
-                    ki = order[ki]
-                K = Xd[ki]
+                    ranks = torch.unique(torch.round(torch.linspace(0, n_glob - 1, kn, dtype=torch.float64)).long())
+                    if coll.is_dist():
+                        K = _rows_at_sorted_ranks(Xd, ranks.tolist(), row0)
+                    else:
+                        K = Xd[torch.argsort(Xd[:, 0], stable=True)[ranks.to(dev)]]
                 if K.shape[0] <= len(exps):
                     raise ValueError(f"thin-plate smoother {g} needs more than {len(exps)} knots")
                 T = _tp_poly(K, exps)                                      # [k, M]
@@ -290,7 +349,7 @@ class GAMTrainer:
                 B = (ispline_basis if b == 2 else mspline_basis)(filled[0], knots, order)
                 S = _diff_penalty(B.shape[1])
             if b != 2:                         # sum-to-zero identifiability constraint (QR reparameterisation)
-                c = B.mean(0)
+                c = _sum_rows(B) / n_glob
                 Q, _ = torch.linalg.qr(c[:, None].cpu(), mode="complete")
                 Z = Q[:, 1:]
                 st["Z"] = Z.tolist()
@@ -346,6 +405,10 @@ class GAMTrainer:
             model.output["validation_metrics"] = model.metrics_for(Xv, yv, wv, ov)
         if p["keep_gam_cols"]:
             from ..frame import H2OFrame
-            model.output["gam_transformed_center_key"] = H2OFrame.from_tensor(Xg.T, lin + names).frame_id
+            import contextlib
+            from ..parallel import dframe
+            ctx = dframe.shard_ctx(dframe.make_shard(Xg.shape[1])) if coll.is_dist() else contextlib.nullcontext()
+            with ctx:
+                model.output["gam_transformed_center_key"] = H2OFrame.from_tensor(Xg.T, lin + names).frame_id
         model.output["run_time_ms"] = int((time.time() - t0) * 1000)
         return model

@@ -66,6 +66,9 @@ class ModelSelectionTrainer:
         Xc = torch.nan_to_num(X.double())
         M = torch.cat([torch.ones(1, X.shape[1], dtype=torch.float64, device=X.device), Xc, y.double()[None]], 0)[:, ok].T
         G = gram(M.float().contiguous()) if X.is_cuda else M.T @ M
+        from ..parallel import collectives as coll
+        if coll.is_dist():                    # Gram of every rank's rows
+            G = coll.all_reduce_(G.double().contiguous().to(coll.comm_device())).to(M.device)
         yy = G[-1, -1]
         ybar = G[0, -1] / G[0, 0]
         sst = float(yy - G[0, 0] * ybar * ybar)

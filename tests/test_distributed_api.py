@@ -62,6 +62,11 @@ CASES = {
     "pca_randomized": ("pca", dict(k=2, transform="STANDARDIZE", pca_method="Randomized", seed=3), None),
     "targetencoder": ("targetencoder", dict(blending=True, inflection_point=3, smoothing=2), "yb"),
     "targetencoder_multi": ("targetencoder", dict(), "y3"),
+    "gam_cr": ("gam", dict(gam_columns=["x1"], num_knots=[6], family="binomial", seed=1), "yb"),
+    "gam_tp_is": ("gam", dict(gam_columns=[["x1", "x2"], "x3"], bs=[1, 2], num_knots=[8, 5], seed=1), "yr"),
+    "anovaglm": ("anovaglm", dict(family="gaussian", highest_interaction_term=2), "yr"),
+    "modelselection_maxr": ("modelselection", dict(mode="maxr", max_predictor_number=2), "yr"),
+    "modelselection_backward": ("modelselection", dict(mode="backward", min_predictor_number=2, family="gaussian"), "yr"),
     "quantile": ("quantile", dict(probs=[0.01, 0.1, 0.5, 0.77, 0.99]), None),
     "quantile_weighted_low": ("quantile", dict(probs=[0.25, 0.5, 0.9], combine_method="low"), None),
     "isolationforest": ("isolationforest", dict(ntrees=6, seed=5, contamination=0.05), None),
@@ -89,7 +94,7 @@ def _run_cases(csv, names, out_path):
     for name in names:
         algo, params, y = CASES[name]
         x = ["x0", "x1", "x2", "x3", "cat"] if algo != "isotonicregression" else ["x0"]
-        if algo in ("kmeans", "pca", "svd", "quantile", "extendedisolationforest"):
+        if algo in ("kmeans", "pca", "svd", "quantile", "extendedisolationforest", "anovaglm", "modelselection"):
             x = ["x0", "x1", "x2", "x3"]
         pp = dict(params)
         if name == "quantile_weighted_low":
