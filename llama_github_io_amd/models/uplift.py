@@ -19,7 +19,8 @@ import time
 import numpy as np
 import torch
 
-from ..ops.binning import apply_binning, fit_binning
+from ..ops.binning import apply_binning, fit_binning_rows
+from ..parallel import collectives as coll
 from ..ops.forest import Forest, Tree
 from ..ops.tree import NA_BIN
 from ..ops.segment import segment_sum
@@ -42,19 +43,33 @@ def _D(kind, pt, pc):
     return _metric(kind, pt, pc) + _metric(kind, 1 - pt, 1 - pc)
 
 
+def _merge(t):
+    if not coll.is_dist():
+        return t
+    return coll.all_reduce_(t.contiguous().to(coll.comm_device())).to(t.device)
+
+
 def auuc(uplift, y, treat, nbins=1000, auuc_type="AUTO"):
-    """Qini / lift / gain AUUC over uplift-sorted rows (AUUC.java); ``AUUC`` is the ``auuc_type`` curve
-    (AUTO = qini) averaged over ``nbins`` thresholds."""
+    """Qini / lift / gain AUUC (AUUC.java); ``AUUC`` is the ``auuc_type`` curve (AUTO = qini) averaged
+    over ``nbins`` thresholds. Thresholds are the uplift values at ``nbins`` evenly spaced descending
+    ranks (exact order statistics — also over row shards); each threshold's treatment / control counts
+    and responses are those of the rows scoring at or above it (ties included), merged by all-reduce."""
+    from ..parallel.order_stats import order_statistics
     nbins = 1000 if nbins is None or int(nbins) <= 0 else int(nbins)
-    order = torch.argsort(uplift, descending=True)
-    y, t = y[order].double(), treat[order].double()
-    nt = torch.cumsum(t, 0)
-    nc = torch.cumsum(1 - t, 0)
-    yt = torch.cumsum(y * t, 0)
-    yc = torch.cumsum(y * (1 - t), 0)
-    N = y.numel()
-    idx = torch.linspace(0, N - 1, min(nbins, N), dtype=torch.float64, device=y.device).long().clamp_(0, N - 1)
-    nt, nc, yt, yc = nt[idx], nc[idx], yt[idx], yc[idx]
+    u = uplift.double()
+    N = int(coll.all_reduce_scalar(float(u.numel()))) if coll.is_dist() else u.numel()
+    idx = torch.linspace(0, N - 1, min(nbins, N), dtype=torch.float64).long().clamp_(0, N - 1)
+    thr = torch.tensor(order_statistics(u, (N - idx).tolist()), dtype=torch.float64, device=u.device)   # descending
+    asc = thr.flip(0)
+    # rows contribute to every threshold <= their uplift: bucket = #thresholds <= u, then suffix sums
+    j = torch.searchsorted(asc, u, right=True)
+    y, t = y.double(), treat.double()
+    stats = torch.stack([t, 1 - t, y * t, y * (1 - t)], 1)
+    m = idx.numel()
+    c = _merge(segment_sum(j, stats, m + 1))
+    S = torch.flip(torch.cumsum(torch.flip(c, [0]), 0), [0])[1:]         # S[k-1] = rows with >= k thresholds below
+    S = S.flip(0)                                                      # descending threshold order
+    nt, nc, yt, yc = S[:, 0], S[:, 1], S[:, 2], S[:, 3]
     qini = yt - yc * nt / nc.clamp(min=1)
     lift = yt / nt.clamp(min=1) - yc / nc.clamp(min=1)
     gain = lift * (nt + nc)
@@ -109,7 +124,10 @@ class UpliftDRFTrainer:
         dev = X.device
         seed = resolve_seed(p["seed"])
         gen = torch.Generator().manual_seed(seed & 0x7FFFFFFF)
-        b = fit_binning(Xs, sub.iscat, sub.nlevels, max_bins=max(int(p["nbins"]), 2) * 4, seed=seed)
+        # row-sharded: global binning (sampled rows only), global-index in-bag draws, node statistics and
+        # histograms all-reduced -> every rank grows the single-process trees
+        b = fit_binning_rows(Xs, sub.iscat, sub.nlevels, max_bins=max(int(p["nbins"]), 2) * 4, seed=seed)
+        row0 = coll.row_offset(N) if coll.is_dist() else 0
         bins = apply_binning(b, Xs)[:, :F].long()                      # [N, F]
         yv = torch.nan_to_num(y).double()
         kind = str(p["uplift_metric"]).lower()
@@ -119,7 +137,7 @@ class UpliftDRFTrainer:
         f_t, f_c = Forest(n_classes_out=1), Forest(n_classes_out=1)
         min_rows = float(p["min_rows"])
         for t in range(int(p["ntrees"])):
-            inbag = (torch.rand(N, generator=gen) < float(p["sample_rate"])).to(dev)
+            inbag = coll.row_uniform(seed, 7000 + t, row0, N, dev) < float(p["sample_rate"])
             tree_t, tree_c = self._grow(bins, b, yv, treat, inbag, int(p["max_depth"]), min_rows, kcols, kind, gen, F)
             f_t.add(tree_t)
             f_c.add(tree_c)
@@ -147,17 +165,17 @@ class UpliftDRFTrainer:
             act = node >= 0
             rows = torch.nonzero(act).flatten()
             nd = node[rows]
-            tot = segment_sum(nd, stats[rows], A)
+            tot = _merge(segment_sum(nd, stats[rows], A))
             pt_n = tot[:, 1] / tot[:, 0].clamp(min=1)
             pc_n = tot[:, 3] / tot[:, 2].clamp(min=1)
             for i, gid in enumerate(level):
                 recs[gid]["pt"], recs[gid]["pc"] = float(pt_n[i]), float(pc_n[i])
-            if d == max_depth or rows.numel() == 0:
+            if d == max_depth or int(coll.all_reduce_scalar(float(rows.numel()))) == 0:
                 break
             idx = (nd[:, None] * F + torch.arange(F, device=dev)[None, :]) * 256 + bins[rows]
             H = torch.zeros(A * F * 256, 4, dtype=torch.float64, device=dev)
             H.index_add_(0, idx.reshape(-1), stats[rows].repeat_interleave(F, 0))
-            H = H.view(A, F, 256, 4)
+            H = _merge(H).view(A, F, 256, 4)
             L = torch.cumsum(H[:, :, :NA_BIN], 2)                   # left = bins < t+1
             R = tot[:, None, None, :] - L
             nL = L[..., 0] + L[..., 2]

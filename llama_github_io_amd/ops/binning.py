@@ -53,6 +53,20 @@ def sample_rows(X: torch.Tensor, sample: int, seed: int, row0: int = 0, n_glob: 
     return X[:, u < (sample / n_glob)]
 
 
+def fit_binning_rows(X: torch.Tensor, iscat, nlevels=None, max_bins: int = MAX_DATA_BINS, sample: int = 1 << 20,
+                     seed: int = 0, max_cat_bins: int = NA_BIN) -> "Binning":
+    """:func:`fit_binning` over the rows of EVERY rank when the rows are sharded (exactly the
+    single-process edges): each rank keeps the rows of the global-index sample it owns and only that
+    sample (<= ``sample`` rows, not the frame) is exchanged."""
+    from ..parallel import collectives as coll
+    if not coll.is_dist():
+        return fit_binning(X, iscat, nlevels, max_bins=max_bins, sample=sample, seed=seed, max_cat_bins=max_cat_bins)
+    row0, n_glob = coll.exclusive_offset(X.shape[1])
+    Xl = sample_rows(X, sample, seed, row0, n_glob)
+    Xs = coll.all_gather_cat(Xl.contiguous(), dim=1, bounded=sample < (1 << 40))
+    return fit_binning(Xs, iscat, nlevels, max_bins=max_bins, seed=seed, max_cat_bins=max_cat_bins, presampled=True)
+
+
 def fit_binning(X: torch.Tensor, iscat, nlevels=None, max_bins: int = MAX_DATA_BINS, sample: int = 1 << 20,
                 seed: int = 0, weights: torch.Tensor | None = None, max_cat_bins: int = NA_BIN,
                 presampled: bool = False) -> Binning:

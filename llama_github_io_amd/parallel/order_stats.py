@@ -106,8 +106,64 @@ def group_order_statistics(v: torch.Tensor, group: torch.Tensor | None, G: int, 
 
 def order_statistics(v: torch.Tensor, targets, w: torch.Tensor | None = None) -> list:
     """Values at cumulative-weight targets (1-based: target T = the first value whose cumulative weight
-    reaches T; unweighted rank r is target r + 1) of the column ``v`` (NaN-free) split over the ranks."""
-    return [group_order_statistics(v, None, 1, [t], w)[0] for t in targets]
+    reaches T; unweighted rank r is target r + 1) of the column ``v`` (NaN-free) split over the ranks.
+
+    Any number of targets share the passes: targets that fall into the same bucket share its refined
+    range, distinct ranges are disjoint, so every row lands in at most one active range (a searchsorted
+    over the sorted range starts) and a pass is still one bincount + one all-reduce."""
+    import torch.distributed as dist
+    dev = v.device
+    keys = order_keys(v)
+    ww = torch.ones(keys.numel(), dtype=torch.float64, device=dev) if w is None else w.double()
+    pos = ww > 0
+    keys, ww = keys[pos], ww[pos]
+    mm = torch.tensor([keys.min().item() if keys.numel() else _BIG, -(keys.max().item() if keys.numel() else -_BIG)],
+                      dtype=torch.int64, device=dev)
+    kmin, kmax = (int(x) for x in _reduce(mm, dist.ReduceOp.MIN).cpu().tolist())
+    kmax = -kmax
+    T = [float(t) for t in targets]
+    out = [math.nan] * len(T)
+    if kmin > kmax or not T:
+        return out
+    ranges = [dict(lo=kmin, hi=kmax, below=0.0, tg=list(range(len(T))))]
+    while ranges:
+        ranges.sort(key=lambda r: r["lo"])
+        total = 0
+        for r in ranges:
+            r["s"] = max(0, (r["hi"] - r["lo"]).bit_length() - _SHIFT_BITS)
+            r["off"] = r["lo"] >> r["s"]
+            r["nb"] = (r["hi"] >> r["s"]) - r["off"] + 1
+            r["base"] = total
+            total += r["nb"]
+        st = torch.tensor([r["lo"] for r in ranges], dtype=torch.int64, device=dev)
+        en = torch.tensor([r["hi"] for r in ranges], dtype=torch.int64, device=dev)
+        sh = torch.tensor([r["s"] for r in ranges], dtype=torch.int64, device=dev)
+        of = torch.tensor([r["off"] for r in ranges], dtype=torch.int64, device=dev)
+        ba = torch.tensor([r["base"] for r in ranges], dtype=torch.int64, device=dev)
+        ri = torch.searchsorted(st, keys, right=True) - 1
+        rc = ri.clamp(min=0)
+        m = (ri >= 0) & (keys <= en[rc])
+        rm = rc[m]
+        b = ba[rm] + torch.bitwise_right_shift(keys[m], sh[rm]) - of[rm]
+        h = torch.bincount(b, weights=ww[m], minlength=total)[:total].to(torch.float64)
+        hc = _reduce(h).cpu()
+        nxt = {}
+        for r in ranges:
+            c = torch.cumsum(hc[r["base"]:r["base"] + r["nb"]], 0) + r["below"]
+            js = torch.searchsorted(c, torch.tensor([T[i] for i in r["tg"]], dtype=torch.float64)).clamp(max=r["nb"] - 1)
+            for i, j in zip(r["tg"], js.tolist()):
+                s_ = r["s"]
+                blo, bhi = (r["off"] + j) << s_, ((r["off"] + j + 1) << s_) - 1
+                lo, hi = max(r["lo"], blo), min(r["hi"], bhi)
+                if s_ == 0 or lo == hi:
+                    out[i] = key_value(lo)
+                    continue
+                key = (lo, hi)
+                if key not in nxt:
+                    nxt[key] = dict(lo=lo, hi=hi, below=float(c[j - 1]) if j > 0 else r["below"], tg=[])
+                nxt[key]["tg"].append(i)
+        ranges = list(nxt.values())
+    return out
 
 
 def global_quantile(v: torch.Tensor, alpha) -> float:

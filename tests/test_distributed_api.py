@@ -30,11 +30,12 @@ def _write_csv(path, n=1200, seed=0):
     yr = 2 * x[:, 0] + np.sin(3 * x[:, 1]) + 0.3 * rng.standard_t(3, n)
     y3 = np.array(["k0", "k1", "k2"])[np.clip((logit > -0.5).astype(int) + (logit > 1.0).astype(int), 0, 2)]
     with open(path, "w") as f:
-        f.write("x0,x1,x2,x3,cat,yb,yr,y3,w\n")
+        f.write("x0,x1,x2,x3,cat,yb,yr,y3,w,trt\n")
         wts = rng.integers(0, 4, n) * 0.5
+        trt = np.where(rng.random(n) < 0.5, "treat", "ctrl")
         for i in range(n):
             xs = ",".join("" if (i % 97 == 5 and j == 2) else f"{x[i, j]:.6f}" for j in range(4))
-            f.write(f"{xs},{cat[i]},{yb[i]},{yr[i]:.6f},{y3[i]},{wts[i]}\n")
+            f.write(f"{xs},{cat[i]},{yb[i]},{yr[i]:.6f},{y3[i]},{wts[i]},{trt[i]}\n")
 
 
 CASES = {
@@ -67,6 +68,7 @@ CASES = {
     "anovaglm": ("anovaglm", dict(family="gaussian", highest_interaction_term=2), "yr"),
     "modelselection_maxr": ("modelselection", dict(mode="maxr", max_predictor_number=2), "yr"),
     "modelselection_backward": ("modelselection", dict(mode="backward", min_predictor_number=2, family="gaussian"), "yr"),
+    "upliftdrf": ("upliftdrf", dict(ntrees=3, max_depth=4, treatment_column="trt", seed=3, auuc_nbins=50), "yb"),
     "quantile": ("quantile", dict(probs=[0.01, 0.1, 0.5, 0.77, 0.99]), None),
     "quantile_weighted_low": ("quantile", dict(probs=[0.25, 0.5, 0.9], combine_method="low"), None),
     "isolationforest": ("isolationforest", dict(ntrees=6, seed=5, contamination=0.05), None),
@@ -75,7 +77,7 @@ CASES = {
                                           weights_column="w"), "yr"),
 }
 
-METRIC_KEYS = ("AUC", "logloss", "MSE", "RMSE", "mae", "mean_per_class_error", "tot_withinss", "r2")
+METRIC_KEYS = ("AUC", "logloss", "MSE", "RMSE", "mae", "mean_per_class_error", "tot_withinss", "r2", "AUUC", "qini")
 
 
 def _run_cases(csv, names, out_path):
@@ -96,6 +98,8 @@ def _run_cases(csv, names, out_path):
         x = ["x0", "x1", "x2", "x3", "cat"] if algo != "isotonicregression" else ["x0"]
         if algo in ("kmeans", "pca", "svd", "quantile", "extendedisolationforest", "anovaglm", "modelselection"):
             x = ["x0", "x1", "x2", "x3"]
+        if algo == "upliftdrf":
+            x = ["x0", "x1", "x2", "x3", "cat", "trt"]
         pp = dict(params)
         if name == "quantile_weighted_low":
             pp["weights_column"] = "w"
