@@ -30,7 +30,15 @@ from decimal import ROUND_HALF_UP, Decimal
 import numpy as np
 import torch
 
+from ..parallel import collectives as coll
 from .base import DataInfo, Model, make_key
+
+
+def _red(t: torch.Tensor, op=None) -> torch.Tensor:
+    """All-reduce over the row shards (no-op in one process): DT's MRTasks (limits, bin counts)."""
+    if not coll.is_dist():
+        return t
+    return coll.all_reduce_(t.contiguous().to(coll.comm_device()), op).to(t.device)
 
 EPSILON = 1e-6            # DT.EPSILON (limits)
 MIN_IMPROVEMENT = 1e-6    # DT.MIN_IMPROVEMENT
@@ -150,9 +158,10 @@ class DTTrainer:
         errs = []
         if int(self.p["max_depth"]) < 1:
             errs.append("Max depth has to be at least 1")
-        if torch.isnan(X).any():
+        bad = _red(torch.tensor([float(torch.isnan(X).any()), float(torch.isinf(X).any())], dtype=torch.float64))
+        if bad[0] > 0:
             errs.append("NaNs are not supported yet")
-        if torch.isinf(X).any():
+        if bad[1] > 0:
             errs.append("Infs are not supported")
         if any(int(c) for c in np.asarray(info.iscat).reshape(-1)):
             errs.append("Categorical features are not supported yet")
@@ -175,8 +184,11 @@ class DTTrainer:
         model = DTModel(model_key or make_key("dt"), p, info)
         model.device = dev
         # root: rows within the initial limits (v.min - EPSILON, v.max]
-        lo0 = Xd.min(1).values - EPSILON
-        hi0 = Xd.max(1).values
+        import torch.distributed as dist
+        big = torch.finfo(torch.float64).max
+        lo0 = _red(Xd.min(1).values if N else torch.full((F,), big, dtype=torch.float64, device=dev),
+                   dist.ReduceOp.MIN) - EPSILON
+        hi0 = _red(Xd.max(1).values if N else torch.full((F,), -big, dtype=torch.float64, device=dev), dist.ReduceOp.MAX)
         member = ((Xd > lo0[:, None]) & (Xd <= hi0[:, None])).all(0)
         node_of_row = torch.where(member, torch.zeros(N, dtype=torch.long, device=dev),
                                   torch.full((N,), -1, dtype=torch.long, device=dev))
@@ -186,7 +198,7 @@ class DTTrainer:
             if K == 0:
                 break
             ok = node_of_row >= 0
-            cnt = torch.bincount(node_of_row[ok] * 2 + yc[ok], minlength=2 * K).reshape(K, 2).cpu().numpy()
+            cnt = _red(torch.bincount(node_of_row[ok] * 2 + yc[ok], minlength=2 * K).double()).reshape(K, 2).cpu().numpy()
             stop = (depth >= D) | (cnt[:, 0] <= min_rows) | (cnt[:, 1] <= min_rows)
             best = self._best_splits(Xd, yc, node_of_row, K, ~stop, min_rows) if (~stop).any() else {}
             nxt, route = [], np.full((K, 3), -1.0)
@@ -231,7 +243,7 @@ class DTTrainer:
         act = torch.as_tensor(active, device=dev)
         ok = node_of_row >= 0
         rows = torch.nonzero(ok & act[node_of_row.clamp(min=0)]).squeeze(1)
-        if rows.numel() == 0:
+        if int(coll.all_reduce_scalar(float(rows.numel()))) == 0:
             return {}
         nd = node_of_row[rows]
         Xr = Xd[:, rows]
@@ -242,6 +254,8 @@ class DTTrainer:
             1, nd[None, :].expand(F, -1), Xr, "amin", include_self=True)
         mx = torch.full((F, K), -big, dtype=torch.float64, device=dev).scatter_reduce(
             1, nd[None, :].expand(F, -1), Xr, "amax", include_self=True)
+        import torch.distributed as dist
+        mn, mx = _red(mn, dist.ReduceOp.MIN), _red(mx, dist.ReduceOp.MAX)
         mn_h, mx_h = (mn - EPSILON).cpu().numpy(), mx.cpu().numpy()
         NB = NUM_BINS + 1
         lo = np.full((K, F, NB), np.inf)
@@ -268,7 +282,7 @@ class DTTrainer:
             inb = (b < NB) & (x > lo_t[nd, f, bc])
             key = ((nd * F + f) * NB + bc) * 2 + yr
             counts.view(-1).index_add_(0, key[inb], torch.ones(int(inb.sum()), dtype=torch.float64, device=dev))
-        c = counts                                   # [K, F, NB, 2]
+        c = _red(counts)                             # [K, F, NB, 2]
         left = c.cumsum(2)
         tot = c.sum(2, keepdim=True)
         right = tot - left

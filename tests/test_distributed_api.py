@@ -69,6 +69,7 @@ CASES = {
     "modelselection_maxr": ("modelselection", dict(mode="maxr", max_predictor_number=2), "yr"),
     "modelselection_backward": ("modelselection", dict(mode="backward", min_predictor_number=2, family="gaussian"), "yr"),
     "upliftdrf": ("upliftdrf", dict(ntrees=3, max_depth=4, treatment_column="trt", seed=3, auuc_nbins=50), "yb"),
+    "dt": ("dt", dict(max_depth=4, min_rows=20), "yb"),
     "quantile": ("quantile", dict(probs=[0.01, 0.1, 0.5, 0.77, 0.99]), None),
     "quantile_weighted_low": ("quantile", dict(probs=[0.25, 0.5, 0.9], combine_method="low"), None),
     "isolationforest": ("isolationforest", dict(ntrees=6, seed=5, contamination=0.05), None),
@@ -98,6 +99,8 @@ def _run_cases(csv, names, out_path):
         x = ["x0", "x1", "x2", "x3", "cat"] if algo != "isotonicregression" else ["x0"]
         if algo in ("kmeans", "pca", "svd", "quantile", "extendedisolationforest", "anovaglm", "modelselection"):
             x = ["x0", "x1", "x2", "x3"]
+        if algo == "dt":
+            x = ["x0", "x1", "x3"]
         if algo == "upliftdrf":
             x = ["x0", "x1", "x2", "x3", "cat", "trt"]
         pp = dict(params)
