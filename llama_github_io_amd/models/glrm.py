@@ -17,6 +17,7 @@ import time
 import numpy as np
 import torch
 
+from ..parallel import collectives as coll
 from .base import DataInfo, Model, make_key
 from .datainfo import Expander
 
@@ -147,6 +148,54 @@ def _prox(name, M, step_gamma, axis):
     raise ValueError(f"unknown GLRM regularizer {name}")
 
 
+def _red(t):
+    """Sum over every rank's rows (no-op in one process)."""
+    if not coll.is_dist():
+        return t
+    return coll.all_reduce_(t.contiguous().to(coll.comm_device())).to(t.device)
+
+
+def _top_svd_from_gram(G, k):
+    """Top-k singular values / right vectors of a tall matrix from its Gram (sign: largest |entry| > 0)."""
+    ev, V = torch.linalg.eigh(G)
+    ev, V = ev.flip(0)[:k].clamp(min=0), V.flip(1)[:, :k]
+    sgn = torch.sign(V.gather(0, V.abs().argmax(0, keepdim=True)))
+    V = V * torch.where(sgn == 0, torch.ones_like(sgn), sgn)
+    return ev.sqrt(), V.T
+
+
+def _row_normals(seed, stream, row0, n, k, dev):
+    """Standard normals [n, k] drawn per GLOBAL row (Box-Muller on counter-based uniforms): the same
+    initial representation however the rows are split."""
+    cols = []
+    for j in range(k):
+        u1 = coll.row_uniform(seed, stream + 2 * j, row0, n, dev).clamp(min=1e-300)
+        u2 = coll.row_uniform(seed, stream + 2 * j + 1, row0, n, dev)
+        cols.append(torch.sqrt(-2 * torch.log(u1)) * torch.cos(2 * math.pi * u2))
+    return torch.stack(cols, 1) if cols else torch.zeros(n, 0, dtype=torch.float64, device=dev)
+
+
+def _pick_row(d, u, A, row0):
+    """Row of A at the global inverse-CDF position u * sum(d) (k-means++ draw over row shards)."""
+    tot = float(_red(d.sum().reshape(1)))
+    cs = torch.cumsum(d, 0)
+    off = 0.0
+    if coll.is_dist():
+        sums = coll.all_gather_object(float(cs[-1]) if cs.numel() else 0.0)
+        off = sum(sums[:coll.rank()])
+    target = u * tot
+    row = torch.zeros(A.shape[1], dtype=A.dtype, device=A.device)
+    hit = torch.zeros(1, dtype=torch.float64, device=A.device)
+    owner = (cs.numel() > 0 and off < target <= off + float(cs[-1])) or (target <= 0 and row0 == 0 and cs.numel() > 0)
+    if owner:
+        j = int(torch.searchsorted(cs, torch.tensor([target - off], dtype=cs.dtype, device=cs.device)).clamp(
+            max=cs.numel() - 1))
+        row = A[j].clone()
+        hit[0] = 1.0
+    row, hit = _red(row), _red(hit)
+    return row / max(float(hit), 1.0)
+
+
 class GLRMModel(Model):
     algo = "glrm"
 
@@ -238,8 +287,9 @@ class GLRMTrainer:
         seed = resolve_seed(p["seed"])
         gen = torch.Generator().manual_seed(seed & 0x7FFFFFFF)
         t = str(p["transform"]).upper()
+        dist_ = coll.is_dist()
         ex = Expander(info, standardize=t in ("STANDARDIZE", "NORMALIZE"), use_all_factor_levels=True,
-                      center_only=(t == "DEMEAN")).fit(X)
+                      center_only=(t == "DEMEAN")).fit(X, reduce=coll.all_reduce_ if dist_ else None)
         # missing entries are excluded from the loss: keep NaNs through the expansion
         Zfull = ex.transform(X).double()
         mask = torch.ones_like(Zfull)
@@ -252,39 +302,52 @@ class GLRMTrainer:
             mask[na, lo:hi] = 0
         A = Zfull
         N, P = A.shape
+        # row-sharded (GLRM.java's MRTasks): X stays with its rows, Y and every sum over rows (objective,
+        # Y gradient, Gram of the SVD init) are all-reduced -> the single-process archetypes on every rank
+        row0 = coll.row_offset(N) if dist_ else 0
+        Ng = int(coll.all_reduce_scalar(N)) if dist_ else N
         k = int(p["k"])
         init = str(p["init"]).lower().replace("_", "")
         if init == "user" and p.get("user_y") is not None:
             uy = p["user_y"]
             Y = torch.as_tensor(uy.as_tensor().numpy() if hasattr(uy, "as_tensor") else np.asarray(uy), dtype=torch.float64).to(dev)
         elif init == "svd":
-            U, S, Vt = torch.linalg.svd(A * mask, full_matrices=False)
-            Y = (S[:k, None] * Vt[:k]).clone()
+            Am = torch.nan_to_num(A) * mask
+            S, Vt = _top_svd_from_gram(_red(Am.T @ Am), k)
+            Y = (S[:, None] * Vt).clone()
         elif init == "plusplus":
-            from .kmeans import KMeansTrainer
-            rows = [int(torch.randint(N, (1,), generator=gen))]
-            d = ((A - A[rows[0]]) ** 2 * mask).sum(1)
+            Af = torch.nan_to_num(A)
+            first = int(torch.randint(Ng, (1,), generator=gen))
+            y0 = torch.zeros(P, dtype=A.dtype, device=dev)
+            if row0 <= first < row0 + N:
+                y0 = Af[first - row0].clone()
+            ys = [_red(y0)]
+            d = ((Af - ys[0]) ** 2 * mask).sum(1)
             for _ in range(1, k):
-                pr = d / d.sum().clamp(min=1e-300)
-                j = int(torch.multinomial(pr.float().cpu(), 1, generator=gen))
-                rows.append(j)
-                d = torch.minimum(d, ((A - A[j]) ** 2 * mask).sum(1))
-            Y = A[rows].clone()
+                u = float(torch.rand(1, generator=gen, dtype=torch.float64))
+                yj = _pick_row(d, u, Af, row0)
+                ys.append(yj)
+                d = torch.minimum(d, ((Af - yj) ** 2 * mask).sum(1))
+            Y = torch.stack(ys, 0)
         else:
             Y = torch.randn(k, P, dtype=torch.float64, generator=gen).to(dev)
-        Xr = torch.randn(N, k, dtype=torch.float64, generator=gen).to(dev) * 0.1
+        Xr = _row_normals(seed, 0x61A5, row0, N, k, dev) * 0.1
         if init in ("svd", "plusplus"):
             Xr = torch.linalg.lstsq(Y.T, (A * mask).T).solution.T
         rx, ry = p["regularization_x"], p["regularization_y"]
         gx, gy = float(p["gamma_x"]), float(p["gamma_y"])
         plan = LossPlan(p, ex, info)
-        if p.get("user_x") is not None:        # init user_x: the initial representation
+        if p.get("user_x") is not None:        # init user_x: the initial representation (this rank's rows)
             ux = p["user_x"]
-            Xr = torch.as_tensor(ux.as_tensor().numpy() if hasattr(ux, "as_tensor") else np.asarray(ux),
-                                 dtype=torch.float64).to(dev).reshape(N, k)
+            ua = torch.as_tensor(ux.as_tensor().numpy() if hasattr(ux, "as_tensor") else np.asarray(ux),
+                                 dtype=torch.float64).reshape(-1, k)
+            if ua.shape[0] == Ng and Ng != N:
+                ua = ua[row0:row0 + N]
+            Xr = ua.to(dev).reshape(N, k)
 
         def objective(Xr, Y):
-            return float(plan.total(Xr @ Y, A, mask) + gx * _reg_value(rx, Xr, 1) + gy * _reg_value(ry, Y, 0))
+            local = plan.total(Xr @ Y, A, mask) + gx * _reg_value(rx, Xr, 1)
+            return float(_red(local.reshape(1))) + float(gy * _reg_value(ry, Y, 0))
 
         step = float(p["init_step_size"])
         obj = objective(Xr, Y)
@@ -302,7 +365,8 @@ class GLRMTrainer:
             Xn = _prox(rx, Xr - step * g / max(P, 1), step * gx, 1)
             Yg = Y.clone().requires_grad_(True)
             g, = torch.autograd.grad(plan.total(Xn @ Yg, A, mask), Yg)
-            Yn = _prox(ry, Y - step * g / max(N, 1), step * gy, 0)
+            g = _red(g)
+            Yn = _prox(ry, Y - step * g / max(Ng, 1), step * gy, 0)
             nobj = objective(Xn, Yn)
             if nobj < obj:
                 Xr, Y = Xn, Yn
@@ -325,15 +389,20 @@ class GLRMTrainer:
         model.plan = plan
         if p.get("recover_svd"):
             # GLRM.recoverSVD: SVD of the rank-k product X Y (singular values and right vectors)
-            _, Sv, Vt = torch.linalg.svd(Xr @ Y, full_matrices=False)
-            model.output["singular_vals"] = Sv[:k].cpu().tolist()
-            model.output["eigenvectors"] = Vt[:k].T.cpu().tolist()
+            # (X Y)^T (X Y) = Y^T (X^T X) Y with the k x k X^T X summed over the row shards
+            Sv, Vt = _top_svd_from_gram(Y.T @ _red(Xr.T @ Xr) @ Y, k)
+            model.output["singular_vals"] = Sv.cpu().tolist()
+            model.output["eigenvectors"] = Vt.T.cpu().tolist()
         model.output.update(objective=obj, iterations=it + 1, step_size=step, archetypes=Y.cpu().tolist(),
                             names_expanded=ex.names, scoring_history=hist)
+        import contextlib
         from ..frame import H2OFrame
-        rep = H2OFrame.from_tensor(Xr.float(), [f"Arch{i + 1}" for i in range(k)])
+        from ..parallel import dframe
+        ctx = dframe.shard_ctx(dframe.make_shard(N)) if dist_ else contextlib.nullcontext()
+        with ctx:                     # the representation keeps the training frame's row distribution
+            rep = H2OFrame.from_tensor(Xr.float(), [f"Arch{i + 1}" for i in range(k)])
         model.output["representation_name"] = rep.frame_id
-        model.output["training_metrics"] = dict(model_category="DimReduction", numerr=float((mask * (Xr @ Y - A) ** 2).sum()),
-                                                 nobs=N)
+        numerr = float(_red((mask * torch.nan_to_num(Xr @ Y - A) ** 2).sum().reshape(1)))
+        model.output["training_metrics"] = dict(model_category="DimReduction", numerr=numerr, nobs=Ng)
         model.output["run_time_ms"] = int((time.time() - t0) * 1000)
         return model

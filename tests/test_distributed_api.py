@@ -70,6 +70,9 @@ CASES = {
     "modelselection_backward": ("modelselection", dict(mode="backward", min_predictor_number=2, family="gaussian"), "yr"),
     "upliftdrf": ("upliftdrf", dict(ntrees=3, max_depth=4, treatment_column="trt", seed=3, auuc_nbins=50), "yb"),
     "dt": ("dt", dict(max_depth=4, min_rows=20), "yb"),
+    "glrm_svd": ("glrm", dict(k=2, init="SVD", transform="STANDARDIZE", max_iterations=30, seed=4, recover_svd=True), None),
+    "glrm_pp": ("glrm", dict(k=3, init="PlusPlus", transform="STANDARDIZE", max_iterations=20, seed=4,
+                             regularization_x="Quadratic", gamma_x=0.1), None),
     "quantile": ("quantile", dict(probs=[0.01, 0.1, 0.5, 0.77, 0.99]), None),
     "quantile_weighted_low": ("quantile", dict(probs=[0.25, 0.5, 0.9], combine_method="low"), None),
     "isolationforest": ("isolationforest", dict(ntrees=6, seed=5, contamination=0.05), None),
@@ -97,7 +100,7 @@ def _run_cases(csv, names, out_path):
     for name in names:
         algo, params, y = CASES[name]
         x = ["x0", "x1", "x2", "x3", "cat"] if algo != "isotonicregression" else ["x0"]
-        if algo in ("kmeans", "pca", "svd", "quantile", "extendedisolationforest", "anovaglm", "modelselection"):
+        if algo in ("kmeans", "pca", "svd", "quantile", "extendedisolationforest", "anovaglm", "modelselection", "glrm"):
             x = ["x0", "x1", "x2", "x3"]
         if algo == "dt":
             x = ["x0", "x1", "x3"]
