@@ -20,7 +20,19 @@ def main():
     ap.add_argument("db")
     ap.add_argument("--top", type=int, default=30)
     ap.add_argument("--md", action="store_true")
+    ap.add_argument("--timeline", default=None, help="kernel-name substring marking one step (e.g. k_gbm_step): "
+                    "print every step's wall span and GPU-busy fraction")
     a = ap.parse_args()
+    if a.timeline:
+        db = sqlite3.connect(a.db)
+        ks = db.execute("select name, start, end from kernels order by start").fetchall()
+        marks = [k[1] for k in ks if a.timeline in k[0]]
+        print(f"| step | span us | busy us | busy % |\n|---|---|---|---|")
+        for i in range(len(marks) - 1):
+            t0, t1 = marks[i], marks[i + 1]
+            busy = sum(min(e, t1) - max(s_, t0) for _, s_, e in ks if e > t0 and s_ < t1)
+            print(f"| {i} | {(t1 - t0) / 1e3:.1f} | {busy / 1e3:.1f} | {100 * busy / max(t1 - t0, 1):.0f} |")
+        return
     rows, span = stats(a.db)
     tot = sum(r[2] for r in rows)
     print(f"kernels: {sum(r[1] for r in rows)} dispatches, {tot / 1e6:.2f} ms busy, first->last {(span[1] - span[0]) / 1e6:.2f} ms")
