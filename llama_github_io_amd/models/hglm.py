@@ -23,8 +23,20 @@ import math
 import numpy as np
 import torch
 
+from ..parallel import collectives as coll
 from .base import DataInfo
 from .datainfo import Expander
+
+
+def _red(t: torch.Tensor) -> torch.Tensor:
+    """Sum over every rank's rows (the reference's MRTask reductions); no-op in one process."""
+    if not coll.is_dist():
+        return t
+    return coll.all_reduce_(t.contiguous().to(coll.comm_device())).to(t.device)
+
+
+def _rsum(t: torch.Tensor) -> float:
+    return float(_red(t.sum().reshape(1)))
 
 
 def _random_indices(info: DataInfo, random_columns):
@@ -72,7 +84,8 @@ def fit_hglm(trainer, X, y, w, off, info: DataInfo, model, p):
     offv = torch.zeros(N, dtype=torch.float64, device=dev) if off is None else off.double()
     Xf = X[fixed_idx] if fixed_idx else X[:0]
     ex = Expander(finfo, standardize=p.get("standardize", True),
-                  use_all_factor_levels=p.get("use_all_factor_levels", False)).fit(Xf, w)
+                  use_all_factor_levels=p.get("use_all_factor_levels", False)).fit(
+                      Xf, w, reduce=coll.all_reduce_ if coll.is_dist() else None)
     M1 = torch.cat([ex.transform(Xf, dtype=torch.float64), torch.ones(N, 1, dtype=torch.float64, device=dev)], 1)
     sizes = [len(info.domains[j]) for j in rand_idx]
     Z = random_design(X, rand_idx, sizes, dev)
@@ -80,13 +93,14 @@ def fit_hglm(trainer, X, y, w, off, info: DataInfo, model, p):
     P1, Q = M1.shape[1], Z.shape[1]
     col_of = torch.cat([torch.full((L,), k, dtype=torch.long) for k, L in enumerate(sizes)]).to(dev)
     r = yv - offv
-    W = float(w.sum())
-    var_y = float((w * (r - (w * r).sum() / W) ** 2).sum() / max(W - 1, 1.0))
+    W = _rsum(w)
+    rbar = _rsum(w * r) / W
+    var_y = _rsum(w * (r - rbar) ** 2) / max(W - 1, 1.0)
     sig_e = float(p.get("init_sig_e") or 0.0) or 0.6 * max(var_y, 1e-12)
     su = p.get("init_sig_u")
     sig_u = torch.full((len(sizes),), float(su) if su else 0.4 * max(var_y, 1e-12), dtype=torch.float64, device=dev)
-    Gm = M.T @ (w[:, None] * M)
-    rhs = M.T @ (w * r)
+    Gm = _red(M.T @ (w[:, None] * M))
+    rhs = _red(M.T @ (w * r))
     eps = float(p.get("objective_epsilon") or 0)
     eps = eps if eps > 0 else 1e-6
     max_it = int(p.get("max_iterations") or 0)
@@ -106,11 +120,11 @@ def fit_hglm(trainer, X, y, w, off, info: DataInfo, model, p):
         h_rand = lam * torch.diagonal(Ainv)[P1:]
         u = coef[P1:]
         dres = w * (r - eta) ** 2
-        sig_e = float(dres.sum() / (w > 0).double().mul(1 - h_data).sum().clamp(min=1e-12))
+        sig_e = _rsum(dres) / max(_rsum((w > 0).double().mul(1 - h_data)), 1e-12)
         num = torch.zeros(len(sizes), dtype=torch.float64, device=dev).index_add_(0, col_of, u * u)
         den = torch.zeros(len(sizes), dtype=torch.float64, device=dev).index_add_(0, col_of, 1 - h_rand)
         sig_u = (num / den.clamp(min=1e-12)).clamp(min=1e-12)
-        conv = float(((eta - eta_old) ** 2).sum() / (eta ** 2).sum().clamp(min=1e-300))
+        conv = _rsum((eta - eta_old) ** 2) / max(_rsum(eta ** 2), 1e-300)
         eta_old = eta
         if conv < eps:
             converged = True
@@ -121,8 +135,8 @@ def fit_hglm(trainer, X, y, w, off, info: DataInfo, model, p):
     model.beta = beta_std[None, :].clone()
     model.hglm = dict(fixed_idx=fixed_idx, rand_idx=rand_idx, sizes=sizes, u=u.clone())
     # h-likelihood: log f(y | u) + log f(u)
-    nobs = float((w > 0).sum())
-    hlik = -0.5 * (nobs * math.log(2 * math.pi * sig_e) + float(dres.sum()) / sig_e)
+    nobs = _rsum((w > 0).double())
+    hlik = -0.5 * (nobs * math.log(2 * math.pi * sig_e) + _rsum(dres) / sig_e)
     for k, Lk in enumerate(sizes):
         uk = u[col_of == k]
         hlik += -0.5 * (Lk * math.log(2 * math.pi * float(sig_u[k])) + float((uk * uk).sum()) / float(sig_u[k]))
