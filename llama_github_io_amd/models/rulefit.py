@@ -263,12 +263,23 @@ class RuleFitTrainer:
         ginfo = DataInfo(names, np.asarray(iscat, np.int32), doms, info.response, info.response_domain)
         Xg = model._glm_matrix(X)
         # support of every rule (RuleEnsemble.calculateSupport: weighted share of rows satisfying it)
-        wv = None if w is None else w.double()
+        # (row-sharded: the tree and GLM trainers reduce over the shards themselves; the supports are
+        # weighted rule counts summed over every rank's rows)
+        from ..parallel import collectives as coll
+        wv = torch.ones(Xg.shape[1], dtype=torch.float64, device=Xg.device) if w is None else w.double()
+        cnt = []
         for gi, (_, rules) in enumerate(groups):
             code = Xg[gi]
-            for r_i, r in enumerate(rules):
-                hit = (code == r_i).double()
-                r.support = float((hit * wv).sum() / wv.sum()) if wv is not None else float(hit.mean())
+            cnt += [((code == r_i).double() * wv).sum() for r_i in range(len(rules))]
+        tot = torch.stack(cnt + [wv.sum()]) if cnt else wv.sum().reshape(1)
+        if coll.is_dist():
+            tot = coll.all_reduce_(tot.to(coll.comm_device())).to(Xg.device)
+        tot = tot.cpu().tolist()
+        i = 0
+        for gi, (_, rules) in enumerate(groups):
+            for r in rules:
+                r.support = tot[i] / tot[-1]
+                i += 1
         gp = dict(alpha=1.0, seed=p["seed"])
         if p.get("lambda_") is not None:
             gp["lambda_"] = p["lambda_"]

@@ -74,6 +74,7 @@ CASES = {
     "glrm_pp": ("glrm", dict(k=3, init="PlusPlus", transform="STANDARDIZE", max_iterations=20, seed=4,
                              regularization_x="Quadratic", gamma_x=0.1), None),
     "hglm": ("glm", dict(family="gaussian", HGLM=True, random_columns=["cat"], seed=1), "yr"),
+    "rulefit": ("rulefit", dict(min_rule_length=1, max_rule_length=2, rule_generation_ntrees=3, seed=2, lambda_=1e-3), "yb"),
     "quantile": ("quantile", dict(probs=[0.01, 0.1, 0.5, 0.77, 0.99]), None),
     "quantile_weighted_low": ("quantile", dict(probs=[0.25, 0.5, 0.9], combine_method="low"), None),
     "isolationforest": ("isolationforest", dict(ntrees=6, seed=5, contamination=0.05), None),
