@@ -7,10 +7,12 @@ from __future__ import annotations
 from llama_github_io_amd.core.job import Job
 from llama_github_io_amd.models import builder
 
+from ..model_api import ModelBaseAPI
+
 _OWN = {"algo", "_parms", "_model", "model_id", "_job", "supervised_learning"}
 
 
-class H2OEstimator:
+class H2OEstimator(ModelBaseAPI):
     algo: str = ""
     supervised_learning = True
     _param_aliases: dict = {}
@@ -107,6 +109,26 @@ class H2OEstimator:
                 p[k] = v
         return train_segments(self.algo, p, x, y, training_frame, seg_cols, segments, validation_frame, parallelism,
                               segment_models_id)
+
+    def start(self, x=None, y=None, training_frame=None, offset_column=None, fold_column=None, weights_column=None,
+              validation_frame=None, **params):
+        """Non-blocking train in h2o-py; here training is synchronous and ``join()`` returns at once."""
+        for k, v in params.items():
+            setattr(self, k, v)
+        return self.train(x=x, y=y, training_frame=training_frame, offset_column=offset_column, fold_column=fold_column,
+                          weights_column=weights_column, validation_frame=validation_frame)
+
+    def weights(self, matrix_id=0):
+        m = self._m()
+        if not hasattr(m, "weights"):
+            raise ValueError(f"{self.algo} models have no weight matrices")
+        W = m.weights(matrix_id)
+        if not hasattr(W, "nrows"):            # h2o-py returns the matrix as a frame [units, inputs]
+            import torch
+            from llama_github_io_amd.frame import H2OFrame
+            W = torch.as_tensor(W, dtype=torch.float64)
+            W = H2OFrame.from_tensor(W, [f"C{i + 1}" for i in range(W.shape[1])])
+        return W
 
     def fit(self, X, y=None, **kw):  # scikit-learn style
         return self.train(x=None, y=y, training_frame=X, **kw)

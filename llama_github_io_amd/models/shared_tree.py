@@ -329,7 +329,19 @@ class SharedTreeTrainer:
         if valid is not None:
             Xv, yv, wv, ov = valid
             model.output["validation_metrics"] = model.metrics_for(Xv, yv, wv, ov)
+        if not model.output["scoring_history"]:
+            # SharedTree always scores the final model (doScoringAndSaveModel(finalScoring=true)): one history
+            # row from the final metrics, no extra pass
+            ev = dict(timestamp=time.time(), duration=time.time() - t_start, number_of_trees=built)
+            for src, pre in (("training_metrics", "training_"), ("validation_metrics", "validation_")):
+                mt = model.output.get(src)
+                for k in ("RMSE", "logloss", "AUC", "pr_auc", "mean_per_class_error", "mae", "mean_residual_deviance"):
+                    if mt is not None and hasattr(mt, "get") and mt.get(k) is not None:
+                        ev[pre + k.lower()] = mt[k]
+            model.output["scoring_history"] = [ev]
+        model.output["start_time"] = int(t_start * 1000)
         model.output["run_time_ms"] = int((time.time() - t_start) * 1000)
+        model.output["end_time"] = model.output["start_time"] + model.output["run_time_ms"]
         return model
 
     def _forest_k(self):
