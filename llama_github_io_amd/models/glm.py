@@ -236,6 +236,57 @@ def estimate_dispersion(family, y, mu, w, nobs, rank, res_dev, method="pearson",
     return _gsum((w * (y - mu) ** 2 / family.variance(mu).clamp(min=1e-30)).sum()) / dfree
 
 
+def tweedie_loglik(y, mu, w, p, phi, eps=8e-17, max_rows=200_000):
+    """Weighted Tweedie log-likelihood for 1 < p < 2 (compound Poisson-gamma; ``TweedieEstimator``): the
+    density of y > 0 by Dunn & Smyth's series W = sum_j W_j evaluated in log space over the window of
+    significant terms around j_max = y^(2-p) / (phi (2-p)) (terms below ``eps`` x the largest are dropped),
+    y = 0 in closed form. Row-sharded: rows of a fixed global-index sample, sums all-reduced."""
+    y, mu, w = y.double(), mu.double().clamp(min=1e-300), w.double()
+    if y.numel() > max_rows:
+        sel = torch.linspace(0, y.numel() - 1, max_rows, device=y.device).long()
+        scale = y.numel() / max_rows
+        y, mu, w = y[sel], mu[sel], w[sel] * scale
+    a = (2 - p) / (1 - p)
+    kappa = mu ** (2 - p) / (2 - p)
+    ll = -kappa / phi
+    pos = y > 0
+    if bool(pos.any()):
+        yp, mp = y[pos], mu[pos]
+        z = -a * torch.log(yp) + a * math.log(p - 1) - (1 - a) * math.log(phi) - math.log(2 - p)
+        jmax = (yp ** (2 - p) / (phi * (2 - p))).clamp(min=1.0)
+        sd = float(jmax.max().sqrt())
+        half = int(min(4096, math.ceil(math.sqrt(max(-2 * math.log(eps), 1.0)) * 2 * sd + 20)))
+        j0 = (jmax.round() - half).clamp(min=1.0)
+        j = j0[:, None] + torch.arange(2 * half + 1, dtype=torch.float64, device=y.device)[None, :]
+        lw = j * z[:, None] - torch.lgamma(1 + j) - torch.lgamma(-j * a)
+        logW = torch.logsumexp(lw, 1)
+        ll_pos = -torch.log(yp) + logW + (yp * mp ** (1 - p) / (1 - p) - mp ** (2 - p) / (2 - p)) / phi
+        ll = ll.clone()
+        ll[pos] = ll_pos
+    return _gsum((w * ll).sum())
+
+
+def estimate_tweedie(y, mu, w, p0, phi0, fix_phi=False, learning_rate=0.5, eps=8e-17):
+    """ML (p, phi) of the Tweedie family with mu fixed (GLM.updateTweediePandPhi / updateTweedieVariancePower:
+    Nelder-Mead over the likelihood; p kept in (1, 2), phi > 0)."""
+    from scipy.optimize import minimize
+
+    def nll(v):
+        pp = 1 + 1 / (1 + math.exp(-v[0]))                     # (1, 2)
+        ph = phi0 if fix_phi else math.exp(v[1])
+        val = tweedie_loglik(y, mu, w, pp, ph, eps)
+        return -val if math.isfinite(val) else 1e300
+
+    pc = p0 if 1 < p0 < 2 else 1.5
+    x0 = [math.log((pc - 1) / (2 - pc)), math.log(max(phi0, 1e-10))]
+    step = max(learning_rate, 1e-3)
+    simplex = [x0, [x0[0] + step, x0[1]], [x0[0], x0[1] + step]]
+    r = minimize(nll, x0, method="Nelder-Mead",
+                 options=dict(initial_simplex=simplex, xatol=1e-6, fatol=1e-9, maxiter=400))
+    pp = 1 + 1 / (1 + math.exp(-r.x[0]))
+    return pp, (phi0 if fix_phi else math.exp(r.x[1])), -float(r.fun)
+
+
 def variance_inflation_factors(ex, X, w):
     """VIF of every numeric predictor: 1 / (1 - R²_j) of regressing it on the other numeric predictors,
     = diag(R⁻¹) of their weighted correlation matrix (GLM generate_variable_inflation_factors)."""
@@ -479,6 +530,9 @@ class GLMTrainer:
         model.expander = ex
         model.output.update(family=fam, link=link, alpha=alpha)
         solver = canon(p["solver"])
+        self._ck_beta, self._ck_iter, self._n_iter, self._tweedie_phi = None, 0, None, None
+        if p.get("checkpoint"):
+            self._checkpoint(p, fam, link, solver, info, ex, model)
         if fam == "multinomial" and solver != "lbfgs":
             beta, path = self._fit_multinomial_irls(Zi, y, w, off, alpha, obj_reg, intercept, info, nobs)
             lam_best = path[-1]["lambda"] if path else 0.0
@@ -488,6 +542,9 @@ class GLMTrainer:
         else:
             family = Family(fam, link, float(p["tweedie_variance_power"]), float(p["tweedie_link_power"]), float(p["theta"]))
             beta, path, lam_best = self._fit_irls(family, Zi, y, w, off, alpha, obj_reg, intercept, valid, ex, nobs)
+            if fam == "tweedie" and p.get("fix_tweedie_variance_power") is False:
+                beta, path, lam_best, family = self._tweedie_power(family, beta, Zi, y, w, off, alpha, obj_reg, intercept,
+                                                                   valid, ex, nobs, model)
             beta = beta[None, :]
         pr = float(p.get("prior") if p.get("prior") is not None else -1.0)
         if pr != -1.0:
@@ -506,6 +563,8 @@ class GLMTrainer:
                     e["coefs"] = list(e["coefs"])
                     e["coefs"][-1] = float(e["coefs"][-1]) - math.log(ymu * (1 - pr) / (pr * (1 - ymu)))
         model.beta = beta
+        if getattr(self, "_n_iter", None) is not None:
+            model.output["iterations"] = self._n_iter
         model.output["lambda_best"] = lam_best
         model.output["lambda"] = [e["lambda"] for e in path]
         model.output["regularization_path"] = dict(lambdas=[e["lambda"] for e in path], alphas=[alpha] * len(path),
@@ -522,8 +581,69 @@ class GLMTrainer:
         model.output["run_time_ms"] = int((time.time() - t0) * 1000)
         return model
 
+    def _checkpoint(self, p, fam, link, solver, info, ex, model):
+        """Continue from a previous GLM (GLM.java: checkpoint is IRLSM only; the previous coefficients start
+        the IRLS iterations, whose count continues from the checkpoint's; scoring history carries over)."""
+        from ..core import dkv
+        ck = p["checkpoint"]
+        prev = dkv.get(ck) if isinstance(ck, str) else getattr(ck, "_model", ck)
+        if prev is None or getattr(prev, "algo", None) != "glm":
+            raise ValueError(f"checkpoint {ck!r} is not a GLM model")
+        if solver != "irlsm":
+            raise ValueError("GLM checkpoint is supported only for IRLSM.  Please specify it explicitly.  "
+                             "Do not use AUTO or default")
+        if fam in ("multinomial", "ordinal"):
+            raise ValueError("GLM checkpoint is supported for single-response families only")
+        for k, mine, theirs in (("family", fam, prev.output.get("family")), ("link", link, prev.output.get("link")),
+                                ("x", list(info.x), list(prev.info.x)), ("response", info.response, prev.info.response)):
+            if mine != theirs:
+                raise ValueError(f"checkpoint: {k} cannot change ({theirs!r} -> {mine!r})")
+        self._ck_iter = int(prev.output.get("iterations") or 0)
+        raw = self._std_to_raw(prev.expander, prev.beta[0].double())
+        self._ck_beta = self._raw_to_std(ex, raw)
+        model.output["scoring_history"] = list(prev.output.get("scoring_history") or [])
+        model.output["checkpoint"] = prev.key
+
+    def _tweedie_power(self, family, beta, Zi, y, w, off, alpha, obj_reg, intercept, valid, ex, nobs, model):
+        """fix_tweedie_variance_power = False (GLM.java Tweedie p / phi estimation): alternate the IRLSM fit of
+        beta at the current power with the ML (p, phi) of the fitted means, until p moves less than
+        dispersion_epsilon (reference defaults: start p = tweedie_variance_power, phi = init_dispersion_parameter)."""
+        p = self.p
+        if str(p.get("dispersion_parameter_method") or "ml").lower() != "ml":
+            raise ValueError("fix_tweedie_variance_power=False needs dispersion_parameter_method='ml'")
+        lr = float(p.get("dispersion_learning_rate") or 0.5)
+        if lr <= 0:
+            raise ValueError("dispersion_learning_rate must > 0")
+        teps = float(p.get("tweedie_epsilon") or 8e-17)
+        if teps <= 0:
+            raise ValueError("tweedie_epsilon must exceed 0.")
+        fix_phi = bool(p.get("fix_dispersion_parameter"))
+        pw, phi = float(p["tweedie_variance_power"]), float(p.get("init_dispersion_parameter") or 1.0)
+        deps = float(p.get("dispersion_epsilon") or 1e-4)
+        hist = []
+        path = lam = None
+        for it in range(int(p.get("max_iterations_dispersion") or 10)):
+            mu = family.linkinv(G.zbeta(Zi, beta, off))
+            npw, nphi, ll = estimate_tweedie(y, mu, w, pw, phi, fix_phi, lr, teps)
+            hist.append(dict(iteration=it, tweedie_variance_power=npw, dispersion=nphi, loglikelihood=ll))
+            moved = abs(npw - pw)
+            pw, phi = npw, nphi
+            family = Family(family.name, family.link, pw, float(p["tweedie_link_power"]), float(p["theta"]))
+            self.p = dict(p, startval=None)
+            beta, path, lam = self._fit_irls(family, Zi, y, w, off, alpha, obj_reg, intercept, valid, ex, nobs,
+                                             beta_init=beta)
+            self.p = p
+            if moved < deps:
+                break
+        model.output["tweedie_variance_power"] = pw
+        model.output["tweedie_estimation_history"] = hist
+        self._tweedie_phi = phi
+        self.p = dict(p, tweedie_variance_power=pw)
+        model.params["tweedie_variance_power"] = pw
+        return beta, path, lam, family
+
     # ---- IRLSM with Gram kernel + Cholesky / COD, optional lambda path
-    def _fit_irls(self, fam: Family, Zi, y, w, off, alpha, obj_reg, intercept, valid, ex, nobs):
+    def _fit_irls(self, fam: Family, Zi, y, w, off, alpha, obj_reg, intercept, valid, ex, nobs, beta_init=None):
         p = self.p
         dev = Zi.device
         P1 = Zi.shape[1]
@@ -531,6 +651,10 @@ class GLMTrainer:
         beta = torch.zeros(P1, dtype=torch.float64, device=dev)
         if intercept:
             beta[-1] = float(fam.linkfn(torch.tensor([min(max(ymu, 1e-6), 1 - 1e-6) if fam.name in ("binomial", "quasibinomial", "fractionalbinomial") else ymu], dtype=torch.float64))[0])
+        if beta_init is None and getattr(self, "_ck_beta", None) is not None:
+            beta_init = self._ck_beta
+        if beta_init is not None:            # warm start (checkpoint / Tweedie power re-fit)
+            beta = beta_init.clone().to(dev)
         lb, ub = self._bounds(ex, P1, dev)
         fixed = torch.zeros(P1, dtype=torch.bool, device=dev)    # coefficients pinned at 0
         if p.get("build_null_model"):
@@ -571,6 +695,12 @@ class GLMTrainer:
         max_it = int(p["max_iterations"]) if int(p["max_iterations"]) > 0 else (50 if fam.name != "gaussian" else 1)
         if fam.name == "gaussian" and fam.link == "identity":
             max_it = max(max_it, 1)
+        ck_it = getattr(self, "_ck_iter", 0)
+        if ck_it:
+            if int(p["max_iterations"]) > 0 and int(p["max_iterations"]) <= ck_it:
+                raise ValueError(f"checkpoint: max_iterations ({p['max_iterations']}) must exceed the checkpoint's "
+                                 f"iterations ({ck_it})")
+            max_it = max(max_it - ck_it, 1)
         beps = float(p["beta_epsilon"])
         path = []
         best = (float("inf"), None, None)
@@ -651,6 +781,7 @@ class GLMTrainer:
             if es and len(lambdas) > 1 and lam < lmax and n_iter >= 5:
                 if max(hist_tr) < 1e-4 or (valid is not None and max(hist_va) < 0):
                     break
+        self._n_iter = ck_it + n_iter
         if best[1] is not None:
             return best[1], path, best[2]
         return beta, path, lambdas[-1]
@@ -920,6 +1051,8 @@ class GLMTrainer:
                        residual_degrees_of_freedom=nobs - rank, aic=family.loglik_aic(y, mu, w, res_dev, nobs, rank))
             if p.get("fix_dispersion_parameter"):
                 self._disp = float(p.get("init_dispersion_parameter") or 1.0)
+            elif getattr(self, "_tweedie_phi", None) is not None:
+                self._disp = self._tweedie_phi
             else:
                 self._disp = estimate_dispersion(family, y, mu, w, nobs, rank, res_dev,
                                                  p.get("dispersion_parameter_method") or "pearson",

@@ -36,8 +36,7 @@ HINTS = {
 
 # parameters not implemented by this engine: a non-default value is refused
 UNSUPPORTED = {
-    "glm": {"dispersion_learning_rate", "fix_tweedie_variance_power", "rand_link", "tweedie_epsilon",
-            "checkpoint"},
+    "glm": {"rand_link"},
     "gam": {"beta_constraints", "standardize_tp_gam_cols", "prior", "early_stopping"},
     "anovaglm": {"early_stopping", "prior", "type", "plug_values"},
     "modelselection": {"beta_constraints", "cold_start", "influence", "max_active_predictors", "prior",

@@ -1,0 +1,78 @@
+"""GLM parameters that change the model (reference ``hex/glm/GLM.java``): ``checkpoint`` (IRLSM restart
+from a previous model, GLM.java:1310-1318 / buildModel) and ``fix_tweedie_variance_power=False`` (ML
+estimation of the Tweedie power and dispersion, GLM.java updateTweediePandPhi, GLMModel.java:725)."""
+import numpy as np
+import pandas as pd
+import pytest
+
+import h2o
+from h2o.estimators import H2OGeneralizedLinearEstimator
+
+
+@pytest.fixture(scope="module")
+def bin_frame():
+    h2o.init(verbose=False)
+    rng = np.random.default_rng(11)
+    n = 2000
+    X = rng.normal(size=(n, 3))
+    eta = 0.4 + X @ np.array([1.2, -0.8, 0.3])
+    y = np.where(rng.random(n) < 1 / (1 + np.exp(-eta)), "1", "0")
+    return h2o.H2OFrame(pd.DataFrame({"a": X[:, 0], "b": X[:, 1], "c": X[:, 2], "y": y}))
+
+
+def test_checkpoint_continues_irlsm(bin_frame):
+    x = ["a", "b", "c"]
+    full = H2OGeneralizedLinearEstimator(family="binomial", solver="IRLSM", lambda_=0.0, max_iterations=50, beta_epsilon=1e-8)
+    full.train(x=x, y="y", training_frame=bin_frame)
+    short = H2OGeneralizedLinearEstimator(family="binomial", solver="IRLSM", lambda_=0.0, max_iterations=1)
+    short.train(x=x, y="y", training_frame=bin_frame)
+    assert short._model.output["iterations"] == 1
+    c0 = short.coef()
+    assert abs(c0["a"] - full.coef()["a"]) > 1e-3            # one IRLS step is not converged
+    cont = H2OGeneralizedLinearEstimator(family="binomial", solver="IRLSM", lambda_=0.0, max_iterations=50,
+                                         beta_epsilon=1e-8, checkpoint=short.model_id)
+    cont.train(x=x, y="y", training_frame=bin_frame)
+    for k, v in full.coef().items():
+        assert abs(cont.coef()[k] - v) < 1e-6
+    assert cont._model.output["iterations"] > 1 and cont._model.output["checkpoint"] == short.model_id
+    with pytest.raises(ValueError, match="IRLSM"):
+        H2OGeneralizedLinearEstimator(family="binomial", lambda_=0.0, checkpoint=short.model_id).train(
+            x=x, y="y", training_frame=bin_frame)
+    with pytest.raises(ValueError, match="family"):
+        H2OGeneralizedLinearEstimator(family="poisson", solver="IRLSM", checkpoint=short.model_id).train(
+            x=["a", "b", "c"], y="a", training_frame=bin_frame)
+    with pytest.raises(ValueError, match="max_iterations"):
+        H2OGeneralizedLinearEstimator(family="binomial", solver="IRLSM", lambda_=0.0, max_iterations=1,
+                                      checkpoint=short.model_id).train(x=x, y="y", training_frame=bin_frame)
+
+
+def _tweedie_sample(rng, mu, phi, p):
+    lam = mu ** (2 - p) / (phi * (2 - p))
+    shape = (2 - p) / (p - 1)
+    scale = phi * (p - 1) * mu ** (p - 1)
+    n = rng.poisson(lam)
+    return np.array([rng.gamma(shape, s, k).sum() if k else 0.0 for k, s in zip(n, scale)])
+
+
+def test_tweedie_power_and_dispersion_estimated():
+    h2o.init(verbose=False)
+    rng = np.random.default_rng(5)
+    n = 6000
+    x = rng.normal(size=n)
+    mu = np.exp(0.5 + 0.6 * x)
+    y = _tweedie_sample(rng, mu, phi=1.5, p=1.4)
+    fr = h2o.H2OFrame(pd.DataFrame({"x": x, "y": y}))
+    m = H2OGeneralizedLinearEstimator(family="tweedie", link="tweedie", tweedie_variance_power=1.7, tweedie_link_power=0,
+                                      lambda_=0.0, fix_tweedie_variance_power=False, dispersion_parameter_method="ml")
+    m.train(x=["x"], y="y", training_frame=fr)
+    o = m._model.output
+    assert abs(o["tweedie_variance_power"] - 1.4) < 0.08, o["tweedie_variance_power"]
+    assert abs(o["dispersion"] - 1.5) < 0.3, o["dispersion"]
+    assert abs(m.coef()["x"] - 0.6) < 0.06
+    fixed = H2OGeneralizedLinearEstimator(family="tweedie", link="tweedie", tweedie_variance_power=1.7,
+                                          tweedie_link_power=0, lambda_=0.0)
+    fixed.train(x=["x"], y="y", training_frame=fr)
+    assert "tweedie_variance_power" not in fixed._model.output or fixed._model.output["tweedie_variance_power"] == 1.7
+    with pytest.raises(ValueError, match="ml"):
+        H2OGeneralizedLinearEstimator(family="tweedie", link="tweedie", tweedie_variance_power=1.5, tweedie_link_power=0,
+                                      fix_tweedie_variance_power=False).train(x=["x"], y="y", training_frame=fr)
