@@ -13,7 +13,9 @@
 #define AMAX_SHARDS 64  // must match tree_kernels.hip
 
 enum Dist { D_GAUSSIAN = 0, D_BERNOULLI = 1, D_QUASIBINOMIAL = 2, D_POISSON = 3, D_GAMMA = 4, D_TWEEDIE = 5,
-            D_LAPLACE = 6, D_QUANTILE = 7, D_HUBER = 8, D_MODIFIED_HUBER = 9 };
+            D_LAPLACE = 6, D_QUANTILE = 7, D_HUBER = 8, D_MODIFIED_HUBER = 9,
+            // XGBoost binary:logistic (hex/tree/xgboost ObjFunction): Newton planes w = h, wY = -g
+            D_XGB_LOGISTIC = 10 };
 
 __device__ __forceinline__ unsigned long long smix(unsigned long long x) {
   x += 0x9E3779B97F4A7C15ull;
@@ -42,7 +44,13 @@ __global__ __launch_bounds__(256) void k_gbm_step(
     }
     const float yi = y[i];
     float z, num, den;
+    float p0 = wi;                     // plane 0: the histogram weight (w; XGBoost: the hessian)
     switch (dist) {
+      case D_XGB_LOGISTIC: {
+        const float p = 1.f / (1.f + expc(-fi));
+        const float h = fmaxf(p * (1.f - p), 1e-16f);
+        z = yi - p; num = wi * z; den = wi * h; p0 = den; break;
+      }
       case D_BERNOULLI: {
         const float p = 1.f / (1.f + expc(-fi));
         z = yi - p; num = wi * z; den = wi * p * (1.f - p); break;
@@ -80,11 +88,11 @@ __global__ __launch_bounds__(256) void k_gbm_step(
       default: { z = yi - fi; num = wi * z; den = wi; }
     }
     const float wz = wi * z;
-    aux[i] = wi;
+    aux[i] = p0;
     aux[N + i] = wz;
     aux[2 * N + i] = num;
     aux[3 * N + i] = den;
-    ma = fmaxf(ma, fabsf(wi));
+    ma = fmaxf(ma, fabsf(p0));
     mb = fmaxf(mb, fabsf(wz));
     mc = fmaxf(mc, fabsf(num));
     md = fmaxf(md, fabsf(den));

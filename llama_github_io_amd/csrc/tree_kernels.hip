@@ -1407,12 +1407,15 @@ __global__ __launch_bounds__(256) void k_qscale(unsigned* __restrict__ amax_bits
 // Leaf values of the GBM distributions with a closed-form Newton step (GBM.java fitBestConstants):
 // g = num/den (0 where den == 0), log-link families take log(g); scaled by the learning rate, then
 // the multinomial / max_abs_leafnode_pred clamps and nan/inf sanitising of the PyTorch path.
+// lam / l1 (XGBoost Newton leaves, CalcWeight: -ThresholdL1(G, alpha) / (H + lambda), 0 where H = 0)
 __global__ void k_leaf_values(const double* __restrict__ leafsum, int n, int log_link, double scale, double kclamp,
-                              double mx, float* __restrict__ out) {
+                              double mx, double lam, double l1, float* __restrict__ out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const double num = leafsum[2 * i], den = leafsum[2 * i + 1];
-  double g = den == 0.0 ? 0.0 : num / den;
+  double num = leafsum[2 * i];
+  const double den = leafsum[2 * i + 1];
+  if (l1 > 0.0) num = num > l1 ? num - l1 : (num < -l1 ? num + l1 : 0.0);
+  double g = den == 0.0 ? 0.0 : num / (den + lam);
   if (log_link) g = den == 0.0 ? 0.0 : log(fmax(g, 1e-300));
   double v = scale * g;
   if (v != v) v = 0.0;                                      // nan_to_num(nan=0)
@@ -1481,10 +1484,11 @@ int h2o_hist_reduce(const void* partials, int slot_doubles, int used, const void
   return (int)hipGetLastError();
 }
 
-int h2o_leaf_values(const void* leafsum, int n, int log_link, double scale, double kclamp, double mx, void* out,
+int h2o_leaf_values(const void* leafsum, int n, int log_link, double scale, double kclamp, double mx, double lam,
+                    double l1, void* out,
                     hipStream_t s) {
   hipLaunchKernelGGL(k_leaf_values, dim3((n + 255) / 256), dim3(256), 0, s, (const double*)leafsum, n, log_link,
-                     scale, kclamp, mx, (float*)out);
+                     scale, kclamp, mx, lam, l1, (float*)out);
   return (int)hipGetLastError();
 }
 
@@ -1690,6 +1694,7 @@ struct TreePlan {
   // [cap][fsn] and the caller all-gathers them into cand [cap][F]. hrecv = reduce-scattered build slots.
   int sliced, fs0, fsn, sslot;
   void *cand_local, *hrecv;
+  double leaf_lam, leaf_l1;   // k_leaf_values regularisation (XGBoost leaves; 0 for GBM)
 };
 
 static inline const float* tp_aux(const TreePlan* P, int c) { return (const float*)P->aux + (size_t)c * P->N; }
@@ -1828,7 +1833,8 @@ int h2o_tree_all(const TreePlan* P, hipStream_t s) {
   }
   TP_CHECK(h2o_tree_leaves(P, s));
   if (P->leaf_native)
-    return h2o_leaf_values(P->leafsum, P->leaf_cap, P->log_link, P->scale, P->kclamp, P->mx, P->leafval, s);
+    return h2o_leaf_values(P->leafsum, P->leaf_cap, P->log_link, P->scale, P->kclamp, P->mx, P->leaf_lam, P->leaf_l1,
+                           P->leafval, s);
   return 0;
 }
 #undef TP_CHECK

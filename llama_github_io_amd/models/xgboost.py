@@ -231,7 +231,54 @@ class XGBoostTrainer(SharedTreeTrainer):
                 kk, vals, leaf = self.tree_rows[it * self.K + k]
                 self.f[:, kk] -= self.tree_w[it] * vals[leaf.long()]
 
+    # ---- fused HIP row step (gbm_kernels.hip k_gbm_step, D_XGB_LOGISTIC / D_GAUSSIAN): the previous tree's
+    # margin update, the gradient / hessian planes and the fixed-point scale maxima in ONE pass over the rows
+    # (the torch path is ~10 elementwise kernels over N rows per tree); leaves by k_leaf_values
+    _FUSED_OBJ = {"bernoulli": 10, "gaussian": 0}
+
+    def _fused(self):
+        if getattr(self, "_fused_ok", None) is None:
+            self._fused_ok = bool(
+                self.dev.type == "cuda" and self.K == 1 and self.obj in self._FUSED_OBJ and not self.dart
+                and str(self.p.get("booster", "gbtree")).lower() != "gblinear"
+                and float(self.p.get("sample_rate", 1.0)) >= 1.0 and bool(self.yok.all())
+                and bool((self.w == 1).all()))
+        return self._fused_ok
+
+    def _amax_for_build(self):
+        if not self._fused():
+            return None
+        if not hasattr(self, "_amax"):
+            self._amax = torch.zeros(4 * T.AMAX_SHARDS, dtype=torch.int32, device=self.dev)
+        return self._amax
+
+    def _leaf_native(self, t, k):
+        if not self._fused():
+            return None
+        p = self.p
+        self._vals = self.builder.leaf_values_view()
+        lr = float(p["learn_rate"])
+        mds = float(p.get("max_delta_step") or 0)
+        return (0, lr, 0.0, lr * mds if mds > 0 else float("inf"), float(p["reg_lambda"]), float(p["reg_alpha"]))
+
+    def _flush_pending(self):
+        pend = getattr(self, "_pending", None)
+        if pend is not None:
+            from ..ops import _native as nat
+            vals, leaf = pend
+            nat.call("h2o_add_leaf", self.N, self.f.data_ptr(), 1, vals.data_ptr(), leaf.data_ptr(), nat.stream_ptr(self.dev))
+            self._pending = None
+
     def _prepare(self, t, k):
+        if self._fused():
+            from ..ops import _native as nat
+            self._amax_for_build()
+            pv, pl = self._pending if getattr(self, "_pending", None) is not None else (None, None)
+            nat.call("h2o_gbm_step", self.N, self.row0, self._FUSED_OBJ[self.obj], self.y.data_ptr(), 0,
+                     self.f.data_ptr(), 0 if pv is None else pv.data_ptr(), 0 if pl is None else pl.data_ptr(),
+                     1.0, 0, 0.0, self.aux.data_ptr(), self._amax.data_ptr(), nat.stream_ptr(self.dev))
+            self._pending = None
+            return self.aux
         if k == 0:
             if self.dart:
                 self._dart_drop(t)
@@ -273,6 +320,9 @@ class XGBoostTrainer(SharedTreeTrainer):
 
     def _update(self, t, k):
         leaf = self.builder.leaf_of_row
+        if self._fused():
+            self._pending = (self._vals, leaf)   # applied by the next fused step (or _flush_pending)
+            return
         if self.dart:
             # gbm::Dart::NormalizeTrees (leaf values already carry eta; lr = eta / trees per iteration):
             #   tree:   new trees weigh 1 / (k + lr), dropped trees are scaled by k / (k + lr)
@@ -300,6 +350,7 @@ class XGBoostTrainer(SharedTreeTrainer):
             self.f[:, k] += self._vals[leaf.long()]
 
     def _finish(self, model, built):
+        self._flush_pending()
         if self.dart:
             # fold the dart weights into the stored leaf values
             for i, tree in enumerate(model.forest.trees):
@@ -309,6 +360,7 @@ class XGBoostTrainer(SharedTreeTrainer):
             model.forest._flat.clear()
 
     def _training_metrics(self, model):
+        self._flush_pending()
         f, y, w = self.f, self.y, self.w
         if self.obj == "multinomial":
             return mm.multinomial_metrics(y, torch.softmax(f, 1), w, self.info.response_domain)

@@ -407,7 +407,8 @@ class _TreePlan(ctypes.Structure):
                 [("kc_level", _ci * _MAXL), ("pad2", _ci)] +
                 [("edges", _vp), ("nb_level", _ci * _MAXL), ("pad3", _ci)] +
                 [("ic_map", _vp), ("ic", _vp * _MAXL)] +
-                [(n, _ci) for n in ("sliced", "fs0", "fsn", "sslot")] + [("cand_local", _vp), ("hrecv", _vp)])
+                [(n, _ci) for n in ("sliced", "fs0", "fsn", "sslot")] + [("cand_local", _vp), ("hrecv", _vp)] +
+                [("leaf_lam", _cd), ("leaf_l1", _cd)])
 
 
 class _Arena:
@@ -678,8 +679,10 @@ class GpuTreeBuilder:
         P.grid = self.grid * (self.hist_bpc if packed else 1)
         P.leaf_native = int(leaf_native is not None)
         if leaf_native is not None:
-            lg, scale, kclamp, mx = leaf_native
+            lg, scale, kclamp, mx = leaf_native[:4]
+            lam, l1 = (tuple(leaf_native[4:6]) + (0.0, 0.0))[:2]
             P.log_link, P.scale, P.kclamp, P.mx = int(lg), float(scale), float(kclamp), float(mx)
+            P.leaf_lam, P.leaf_l1 = float(lam), float(l1)
         ref = ctypes.byref(P)
         if not coll.is_dist():
             nat.check(lib.h2o_tree_all(ref, s), "tree_all")
@@ -700,7 +703,7 @@ class GpuTreeBuilder:
             coll.all_reduce_(self.leafsum)
             if leaf_native is not None:
                 nat.check(lib.h2o_leaf_values(self.leafsum.data_ptr(), self.leaf_cap, P.log_link, P.scale, P.kclamp,
-                                              P.mx, self._p("leafval"), s), "leaf_values")
+                                              P.mx, P.leaf_lam, P.leaf_l1, self._p("leafval"), s), "leaf_values")
         if leaf_native is None and leaf_fn is not None:
             vals = leaf_fn(self.leafsum)
             self.av["leafval"].view(torch.float32)[: vals.numel()].copy_(vals.to(torch.float32))
@@ -734,7 +737,7 @@ class GpuTreeBuilder:
         self._rootw.copy_(self.lsx[L2:])
         if leaf_native is not None:
             nat.check(lib.h2o_leaf_values(self.leafsum.data_ptr(), self.leaf_cap, P.log_link, P.scale, P.kclamp,
-                                          P.mx, self._p("leafval"), s), "leaf_values")
+                                          P.mx, P.leaf_lam, P.leaf_l1, self._p("leafval"), s), "leaf_values")
 
     def _snapshot(self):
         # the tree's structure travels to pinned host memory asynchronously: the host decodes finished

@@ -470,3 +470,33 @@ def test_dl_trainer_uses_fused_step_and_learns(monkeypatch):
     assert res["1"].output["training_step_fused_mfma"] and not res["0"].output["training_step_fused_mfma"]
     a1, a0 = res["1"].output["training_metrics"]["AUC"], res["0"].output["training_metrics"]["AUC"]
     assert a1 > 0.9 and abs(a1 - a0) < 0.02, (a1, a0)
+
+
+@pytest.mark.parametrize("obj,extra", [("bernoulli", dict(reg_lambda=2.0, reg_alpha=0.5, max_delta_step=0.3)),
+                                       ("gaussian", dict(reg_lambda=1.0))])
+def test_xgboost_fused_step_matches_torch_path(obj, extra):
+    """The fused XGBoost row step (k_gbm_step D_XGB_LOGISTIC / D_GAUSSIAN + k_leaf_values with lambda / alpha /
+    max_delta_step) grows the same trees as the torch gradient path."""
+    from llama_github_io_amd.models.base import DataInfo
+    from llama_github_io_amd.models.xgboost import XGBoostTrainer
+    g = torch.Generator().manual_seed(3)
+    N, F = 20000, 6
+    X = torch.randn(F, N, generator=g)
+    if obj == "bernoulli":
+        y = (torch.rand(N, generator=g) < torch.sigmoid(X[0] - X[1] + 0.5 * X[2] * X[3])).float()
+        info = DataInfo([f"x{i}" for i in range(F)], np.zeros(F, np.int32), [None] * F, "y", ["0", "1"])
+    else:
+        y = X[0] * 2 + torch.sin(X[1]) + 0.1 * torch.randn(N, generator=g)
+        info = DataInfo([f"x{i}" for i in range(F)], np.zeros(F, np.int32), [None] * F, "y", None)
+    params = dict(ntrees=8, max_depth=4, learn_rate=0.3, seed=1, **extra)
+
+    class TorchPath(XGBoostTrainer):
+        def _fused(self):
+            return False
+    fused_tr = XGBoostTrainer(dict(params))
+    mf = fused_tr.fit(X.cuda(), y.cuda(), None, None, info)
+    assert fused_tr._fused()
+    mt = TorchPath(dict(params)).fit(X.cuda(), y.cuda(), None, None, info)
+    pf = mf._predict_tensor(X.cuda()).double().cpu()
+    pt = mt._predict_tensor(X.cuda()).double().cpu()
+    assert torch.allclose(pf, pt, rtol=2e-4, atol=2e-5), (pf - pt).abs().max()
