@@ -269,6 +269,7 @@ class GAMTrainer:
             params["lambda_"] = params.pop("lambda")
         p.update({k: v for k, v in params.items() if v is not None})
         self.p = p
+        self._explicit = {k for k, v in params.items() if v is not None}
         self.job = None
 
     def fit(self, X, y, w, offset, info: DataInfo, valid=None, model_key=None):
@@ -375,6 +376,8 @@ class GAMTrainer:
                          info.response, info.response_domain)
         gp = {k: v for k, v in p.items() if k not in ("gam_columns", "num_knots", "scale", "bs", "knot_ids", "keep_gam_cols",
                                                       "spline_orders", "splines_non_negative", "scale_tp_penalty_mat")}
+        if gp.get("lambda_search") and "lambda_" not in self._explicit:
+            gp.pop("lambda_", None)           # the lambda path replaces the default fixed lambda
         tr = GLMTrainer(gp)
         # the GLM expands categoricals first, then numerics (linear numerics, then every smoother column):
         # the smoothers' penalty block is the tail of the coefficient vector (before the intercept)

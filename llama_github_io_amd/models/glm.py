@@ -847,6 +847,8 @@ class GLMTrainer:
                 lb[j] = float(row["lower_bounds"]) * sc
             if "upper_bounds" in df.columns and not pd.isna(row["upper_bounds"]):
                 ub[j] = float(row["upper_bounds"]) * sc
+        if extra is not None:                              # GAM I-spline non-negativity on top of the user's
+            lb = torch.maximum(lb, extra.to(dev))
         return lb, ub
 
     def _collinear(self, Zi, w, intercept):

@@ -123,6 +123,13 @@ class ModelSelectionTrainer:
                 hist.append((score(cur), list(cur)))
                 if len(cur) == kmin:
                     break
+                thr = float(p.get("p_values_threshold") or 0.0)
+                if thr > 0:
+                    # ModelSelection.buildBackwardModels: stop once every predictor's p-value (intercept
+                    # excluded) is at or below the threshold
+                    pv = m.output.get("p_values") or {}
+                    if all(v <= thr for k, v in pv.items() if not k.startswith("Intercept")):
+                        break
                 z = m.output["z_values"]
                 j_drop = min(cur, key=lambda j: abs(z.get(info.x[j], 0.0)))
                 cur = [j for j in cur if j != j_drop]

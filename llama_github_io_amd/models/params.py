@@ -37,10 +37,10 @@ HINTS = {
 # parameters not implemented by this engine: a non-default value is refused
 UNSUPPORTED = {
     "glm": {"rand_link"},
-    "gam": {"beta_constraints", "standardize_tp_gam_cols", "prior", "early_stopping"},
+    "gam": {"standardize_tp_gam_cols"},
     "anovaglm": {"early_stopping", "prior", "type", "plug_values"},
     "modelselection": {"beta_constraints", "cold_start", "influence", "max_active_predictors", "prior",
-                       "remove_collinear_columns", "startval", "p_values_threshold", "gradient_epsilon",
+                       "remove_collinear_columns", "startval", "gradient_epsilon",
                        "objective_epsilon", "early_stopping", "plug_values"},
     "glrm": {"expand_user_y"},
     "rulefit": {"max_categorical_levels"},

@@ -2,6 +2,7 @@
 cubic regression (bs=0), thin plate (bs=1, several columns), monotone I-splines (bs=2), M-splines
 (bs=3), and categorical linear predictors."""
 import numpy as np
+import pandas as pd
 import pytest
 import torch
 
@@ -99,3 +100,35 @@ def test_gam_passes_glm_options_through():
     m2.train(x=["a", "b", "c", "c2"], y="y", training_frame=fr)
     m3 = H2OGeneralizedAdditiveEstimator(cold_start=True, objective_epsilon=1e-6, **base)
     m3.train(x=["a", "b", "c"], y="y", training_frame=fr)
+
+
+def test_gam_beta_constraints_prior_and_early_stopping():
+    """GAM passes beta_constraints, prior and early_stopping to its GLM (GAM.java builds the GLM with the
+    same parameters): a bounded linear coefficient is clipped, the prior moves the intercept, and early
+    stopping shortens the lambda path."""
+    import h2o
+    from h2o.estimators import H2OGeneralizedAdditiveEstimator
+    h2o.init(verbose=False)
+    rng = np.random.default_rng(4)
+    n = 3000
+    a, b = rng.normal(size=n), rng.uniform(-2, 2, n)
+    yb = np.where(rng.random(n) < 1 / (1 + np.exp(-(1.5 * a + np.sin(2 * b)))), "1", "0")
+    fr = h2o.H2OFrame(pd.DataFrame({"a": a, "b": b, "y": yb}))
+    base = dict(family="binomial", gam_columns=["b"], num_knots=[6], lambda_=0.0)
+    free = H2OGeneralizedAdditiveEstimator(**base)
+    free.train(x=["a", "b"], y="y", training_frame=fr)
+    assert free._model.output["coefficients"]["a"] > 1.0
+    bc = h2o.H2OFrame(pd.DataFrame({"names": ["a"], "lower_bounds": [-10.0], "upper_bounds": [0.5]}))
+    bounded = H2OGeneralizedAdditiveEstimator(beta_constraints=bc, **base)
+    bounded.train(x=["a", "b"], y="y", training_frame=fr)
+    assert abs(bounded._model.output["coefficients"]["a"] - 0.5) < 1e-6
+    pr = H2OGeneralizedAdditiveEstimator(prior=0.2, **base)
+    pr.train(x=["a", "b"], y="y", training_frame=fr)
+    assert pr._model.output["coefficients"]["Intercept"] < free._model.output["coefficients"]["Intercept"] - 0.3
+    ls = dict(family="binomial", gam_columns=["b"], num_knots=[6], lambda_search=True, nlambdas=40)
+    es = H2OGeneralizedAdditiveEstimator(early_stopping=True, **ls)
+    es.train(x=["a", "b"], y="y", training_frame=fr)
+    noes = H2OGeneralizedAdditiveEstimator(early_stopping=False, **ls)
+    noes.train(x=["a", "b"], y="y", training_frame=fr)
+    assert len(noes._model.glm.output["lambda"]) == 40
+    assert len(es._model.glm.output["lambda"]) <= 40

@@ -76,3 +76,23 @@ def test_tweedie_power_and_dispersion_estimated():
     with pytest.raises(ValueError, match="ml"):
         H2OGeneralizedLinearEstimator(family="tweedie", link="tweedie", tweedie_variance_power=1.5, tweedie_link_power=0,
                                       fix_tweedie_variance_power=False).train(x=["x"], y="y", training_frame=fr)
+
+
+def test_modelselection_backward_p_values_threshold():
+    """ModelSelection backward mode stops removing predictors once every p-value is <= p_values_threshold
+    (ModelSelection.buildBackwardModels)."""
+    from h2o.estimators import H2OModelSelectionEstimator
+    h2o.init(verbose=False)
+    rng = np.random.default_rng(2)
+    n = 1500
+    X = rng.normal(size=(n, 5))
+    y = 3 * X[:, 0] - 2 * X[:, 1] + 0.05 * X[:, 2] + rng.normal(size=n)
+    fr = h2o.H2OFrame(pd.DataFrame({f"x{i}": X[:, i] for i in range(5)} | {"y": y}))
+    full = H2OModelSelectionEstimator(mode="backward", min_predictor_number=1, family="gaussian")
+    full.train(x=[f"x{i}" for i in range(5)], y="y", training_frame=fr)
+    stop = H2OModelSelectionEstimator(mode="backward", min_predictor_number=1, family="gaussian", p_values_threshold=0.01)
+    stop.train(x=[f"x{i}" for i in range(5)], y="y", training_frame=fr)
+    sizes_full = [len(r["predictor_names"]) for r in full._model.output["result"]]
+    sizes_stop = [len(r["predictor_names"]) for r in stop._model.output["result"]]
+    assert min(sizes_full) == 1 and min(sizes_stop) == 2        # x0, x1 are both highly significant
+    assert sorted(stop._model.output["result"][0]["predictor_names"]) == ["x0", "x1"]
