@@ -140,6 +140,16 @@ class GenericModel(Model):
             m.meta_transform = ki.get("metalearner_transform", "NONE")
             if m.info.response_domain is None and m.meta.info.response_domain is not None:
                 m.info.response_domain = list(m.meta.info.response_domain)   # out-of-range domain entry
+        elif algo == "gam":
+            m.gam = A.load_gam(ki, mj["files"])
+            ncen = int(ki["num_expanded_gam_columns_center"])
+            normal = xs[: nfeat - ncen]
+            src = [c for cs in m.gam["cols"] for c in cs if c not in normal]
+            src = list(dict.fromkeys(src))
+            m.gam["n_normal"] = len(normal)
+            m.gam["src_index"] = [(normal + src).index(cs[0]) for cs in m.gam["cols"]]
+            m.info = DataInfo(normal + src, np.concatenate([iscat[: len(normal)], np.zeros(len(src), np.int32)]),
+                              doms[: len(normal)] + [None] * len(src), resp, rdom)
         elif algo == "rulefit":
             m.rulefit = A.load_rulefit(ki)
             m.glm_sub = GenericModel.from_mojo(path, m.rulefit["linear_key"],
@@ -337,6 +347,18 @@ class GenericModel(Model):
                 return torch.softmax(eta, 1).float()
             from .glm import Family
             mu = Family(fam, link, 0.0, float(ki.get("tweedie_link_power", 1.0))).linkinv(eta[:, 0])
+            if fam in ("binomial", "quasibinomial", "fractionalbinomial"):
+                return torch.stack([1 - mu, mu], 1).float()
+            return mu.float()
+        if algo == "gam":
+            from ..mojo import algos as A
+            g = self.gam
+            eta = A.score_gam(g, X[: g["n_normal"]], [X[i] for i in g["src_index"]])
+            if offset is not None:
+                eta = eta + offset.double()
+            from .glm import Family
+            fam = "binomial" if g["family"] == "bernoulli" else g["family"]
+            mu = Family(fam, g["link"], 0.0, g["tlp"]).linkinv(eta)
             if fam in ("binomial", "quasibinomial", "fractionalbinomial"):
                 return torch.stack([1 - mu, mu], 1).float()
             return mu.float()

@@ -856,3 +856,202 @@ def score_rulefit(st, glm, X, parent_info):
     for i, n in enumerate(st["linear_names"][:len(gx)]):
         rows[gx.index(n)] = test[i]
     return glm._predict_tensor(torch.stack(rows, 0))
+
+
+# ================================================================================================ GAM
+# GAMMojoWriter layout (h2o-algos/src/main/java/hex/gam/GAMMojoWriter.java:writeModelData) read by
+# h2o-genmodel GamMojoReader / GamMojoModelBase: the GLM part (cats, cat_offsets, numsCenter, NA fills,
+# family / link, beta_center over [categorical one-hot, linear numerics, centred gam columns, intercept] on
+# the raw scale) and per smoother, in the reader's SORTED order (cubic regression, I-spline, M-spline):
+# knots [gam][1][k], the cubic F rows B^-1 D (``_binvD`` [k-2][k]), the centring transposes
+# (``zTranspose`` [k-1][k]; I-splines are not centred), the un-centred beta and the column names.
+# Thin-plate smoothers (bs = 1) are refused: their MOJO carries H2O's own polynomial / distance basis.
+_BS_ORDER = {0: 0, 2: 1, 3: 2}
+
+
+def _gam_blocks(model):
+    """Smoother blocks of a GAM in reader order: (user index, state, centred names, uncentred names)."""
+    if any(g["bs"] == 1 for g in model.gams):
+        raise ValueError("GAM MOJO: thin-plate smoothers (bs=1) are not exportable in the reference layout")
+    names = list(model.glm.info.x)
+    lin = list(model.lin_x)
+    off = len(lin)
+    blocks = []
+    for gi, g in enumerate(model.gams):
+        nb = int(g["nb"])
+        cn = names[off:off + nb]
+        off += nb
+        tag = "_".join(g["cols"])
+        unc = nb + (1 if g.get("Z") is not None else 0)
+        suffix = {0: "cr", 2: "is", 3: "ms"}[g["bs"]]
+        blocks.append((gi, g, cn, [f"{tag}_{suffix}_nc_{i}" for i in range(unc)]))
+    blocks.sort(key=lambda b: (_BS_ORDER[b[1]["bs"]], b[0]))
+    return blocks
+
+
+def _blob_3d(arrs) -> bytes:
+    return b"".join(np.asarray(a, dtype=">f8").tobytes() for a in arrs)
+
+
+def write_gam(model, kv, blobs):
+    glm = model.glm
+    ex = glm.expander
+    fam = glm.output["family"]
+    if fam in ("multinomial", "ordinal"):
+        raise ValueError("GAM MOJO: multinomial / ordinal GAMs are not exported")
+    blocks = _gam_blocks(model)
+    n_lin_num = sum(1 for j in ex.nums if glm.info.x[j] in model.lin_x)
+    kv["use_all_factor_levels"] = "true" if ex.use_all else "false"
+    kv["cats"] = len(ex.cats)
+    kv["cat_offsets"] = _arr(list(ex.cat_offsets) + [ex.num_off])
+    kv["numsCenter"] = n_lin_num
+    kv["num"] = n_lin_num + len(blocks)
+    kv["mean_imputation"] = "true"
+    kv["numNAFillsCenter"] = _arr([float(v) for v in ex.num_mean.cpu().tolist()[:n_lin_num]])
+    kv["catNAFills"] = _arr([int(v) for v in ex.cat_modes])
+    kv["family"] = "bernoulli" if fam == "binomial" else fam
+    kv["link"] = glm.output["link"]
+    if fam == "tweedie":
+        kv["tweedie_link_power"] = float(glm.params.get("tweedie_link_power", 1.0))
+    gam_cols = [g["cols"] for g in model.gams]
+    kv["num_knots"] = _arr([len(g["knots"]) for g in model.gams])
+    kv["num_knots_sorted"] = _arr([len(b[1]["knots"]) for b in blocks])
+    blobs["gam_columns"] = "".join(c + "\n" for cs in gam_cols for c in cs)
+    blobs["gam_columns_sorted"] = "".join(c + "\n" for b in blocks for c in b[1]["cols"])
+    kv["gam_column_dim"] = _arr([len(cs) for cs in gam_cols])
+    kv["gam_column_dim_sorted"] = _arr([len(b[1]["cols"]) for b in blocks])
+    # raw-scale coefficients: [cat one-hot | linear numerics | gam blocks (user order) | intercept]
+    braw, ic = ex.destandardize(glm.beta[0, :-1], float(glm.beta[0, -1]))
+    braw = braw.double().cpu().numpy()
+    head = braw[: ex.num_off + n_lin_num]
+    gam_beta, pos = {}, ex.num_off + n_lin_num
+    for gi, g in enumerate(model.gams):
+        gam_beta[gi] = braw[pos:pos + int(g["nb"])]
+        pos += int(g["nb"])
+    center, nocenter, cnames, ncnames = list(head), list(head), [], []
+    for gi, g, cn, ncn in blocks:
+        bc = gam_beta[gi]
+        center += bc.tolist()
+        Z = np.asarray(g["Z"]) if g.get("Z") is not None else None
+        nocenter += (Z @ bc).tolist() if Z is not None else bc.tolist()
+        cnames.append(cn)
+        ncnames.append(ncn)
+    center.append(ic)
+    nocenter.append(ic)
+    kv["num_expanded_gam_columns"] = sum(len(n) for n in ncnames)
+    kv["num_expanded_gam_columns_center"] = sum(len(n) for n in cnames)
+    normal = [glm.info.x[j] for j in list(ex.cats) + [j for j in ex.nums if glm.info.x[j] in model.lin_x]]
+    nc_all = normal + [n for ns in ncnames for n in ns]
+    blobs["_names_no_centering"] = "".join(n + "\n" for n in nc_all)
+    kv["total feature size"] = len(nc_all)
+    kv["gamColName_dim"] = _arr([len(n) for n in ncnames])
+    blobs["gamColNamesCenter"] = "".join(n + "\n" for ns in cnames for n in ns)
+    blobs["gamColNames"] = "".join(n + "\n" for ns in ncnames for n in ns)
+    kv["beta"] = _arr([float(v) for v in nocenter])
+    kv["beta length per class"] = len(nocenter)
+    kv["beta_center"] = _arr([float(v) for v in center])
+    kv["beta center length per class"] = len(center)
+    kv["bs"] = _arr([int(g["bs"]) for g in model.gams])
+    kv["bs_sorted"] = _arr([int(b[1]["bs"]) for b in blocks])
+    blobs["knots"] = _blob_3d([[b[1]["knots"]] for b in blocks])
+    blobs["zTranspose"] = _blob_3d([np.asarray(b[1]["Z"]).T if b[1].get("Z") is not None else np.zeros((0, 0))
+                                    for b in blocks])
+    kv["_d"] = _arr([1] * len(blocks))
+    kv["num_CS_col"] = sum(1 for b in blocks if b[1]["bs"] == 0)
+    kv["num_IS_col"] = sum(1 for b in blocks if b[1]["bs"] == 2)
+    kv["num_MS_col"] = sum(1 for b in blocks if b[1]["bs"] == 3)
+    if kv["num_IS_col"] or kv["num_MS_col"]:
+        kv["spline_orders_sorted"] = _arr([int(b[1].get("order", 0)) for b in blocks])
+        kv["spline_orders"] = _arr([int(g.get("order", 0)) for g in model.gams])
+    kv["num_TP_col"] = 0
+    if kv["num_CS_col"]:
+        blobs["_binvD"] = _blob_3d([np.asarray(b[1]["F"])[1:-1] for b in blocks if b[1]["bs"] == 0])
+    # this framework imputes a missing smoother input with its training mean before the basis expansion
+    kv["gam_na_fill_sorted"] = _arr([float(b[1]["means"][0]) for b in blocks])
+    gi = glm.info
+    order = list(ex.cats) + [j for j in ex.nums if gi.x[j] in model.lin_x]     # DataInfo order: cats first
+    return [gi.x[j] for j in order] + [n for ns in cnames for n in ns], [gi.domains[j] for j in order]
+
+
+def load_gam(ki, files):
+    """GamMojoReader: the fields the scorer needs (reader order)."""
+    def f(k, default="[]"):
+        from .reader import _floats
+        return _floats(ki.get(k, default))
+
+    def lines(name):
+        b = files[name]
+        return [s for s in (b.decode() if isinstance(b, bytes) else b).split("\n") if s]
+
+    def d3(name, dims):
+        raw = np.frombuffer(files[name], dtype=">f8") if name in files else np.zeros(0)
+        out, pos = [], 0
+        for a, b in dims:
+            out.append(raw[pos:pos + a * b].reshape(a, b).astype(np.float64))
+            pos += a * b
+        return out
+    bs = [int(v) for v in f("bs_sorted")]
+    nk = [int(v) for v in f("num_knots_sorted")]
+    orders = [int(v) for v in f("spline_orders_sorted")] if "spline_orders_sorted" in ki else [0] * len(bs)
+    dims = [int(v) for v in f("gam_column_dim_sorted")]
+    cols_flat = lines("gam_columns_sorted")
+    cols, pos = [], 0
+    for d in dims:
+        cols.append(cols_flat[pos:pos + d])
+        pos += d
+    basis = [k if b == 0 else k + o - 2 for b, k, o in zip(bs, nk, orders)]
+    zdims = [(0, 0) if b == 2 else (n - 1, n) for b, n in zip(bs, basis)]
+    st = dict(bs=bs, num_knots=nk, orders=orders, cols=cols,
+              knots=[k[0] for k in d3("knots", [(1, n) for n in nk])],
+              zT=d3("zTranspose", zdims),
+              binvD=d3("_binvD", [(n - 2, n) for b, n in zip(bs, nk) if b == 0]),
+              beta_center=np.asarray(f("beta_center")), cats=int(ki["cats"]),
+              cat_offsets=[int(v) for v in f("cat_offsets")], nums=int(ki["numsCenter"]),
+              use_all=ki.get("use_all_factor_levels") == "true", num_fill=f("numNAFillsCenter"),
+              cat_fill=[int(v) for v in f("catNAFills")], family=ki["family"], link=ki["link"],
+              tlp=float(ki.get("tweedie_link_power", 0.0)), gam_fill=f("gam_na_fill_sorted"))
+    return st
+
+
+def score_gam(st, X_lin, gam_x):
+    """GamMojoModel.gamScore0: eta = beta_center . [cat one-hot, numerics, centred smoother bases] +
+    intercept, then the inverse link (X_lin [F_lin, N] in cats-then-nums order; gam_x: per smoother [N])."""
+    from ..models.gam import cr_basis, ispline_basis, mspline_basis
+    dev = X_lin.device
+    N = X_lin.shape[1]
+    beta = torch.as_tensor(st["beta_center"], dtype=torch.float64, device=dev)
+    eta = torch.full((N,), float(beta[-1]), dtype=torch.float64, device=dev)
+    co = st["cat_offsets"]
+    for i in range(st["cats"]):
+        v = X_lin[i].double()
+        v = torch.where(torch.isnan(v), torch.full_like(v, float(st["cat_fill"][i])), v)
+        iv = v.long() if st["use_all"] else v.long() - 1
+        idx = iv + co[i]
+        ok = (iv >= 0) & (idx < co[i + 1])
+        eta = eta + torch.where(ok, beta[idx.clamp(0, beta.numel() - 1)], torch.zeros_like(eta))
+    noff = co[st["cats"]]
+    for j in range(st["nums"]):
+        v = X_lin[st["cats"] + j].double()
+        v = torch.where(torch.isnan(v), torch.full_like(v, float(st["num_fill"][j])), v)
+        eta = eta + beta[noff + j] * v
+    pos = noff + st["nums"]
+    cs = 0
+    for g, (b, x) in enumerate(zip(st["bs"], gam_x)):
+        x = torch.nan_to_num(x.double(), nan=float(st["gam_fill"][g]) if st["gam_fill"] else 0.0)
+        kn = torch.as_tensor(st["knots"][g], dtype=torch.float64, device=dev)
+        if b == 0:
+            F = torch.cat([torch.zeros(1, kn.numel(), dtype=torch.float64),
+                           torch.as_tensor(st["binvD"][cs]), torch.zeros(1, kn.numel(), dtype=torch.float64)])
+            cs += 1
+            B = cr_basis(x, kn.cpu(), F)
+        elif b == 2:
+            B = ispline_basis(x, kn, st["orders"][g])
+        else:
+            B = mspline_basis(x, kn, st["orders"][g])
+        zT = st["zT"][g]
+        if zT.size:
+            B = B @ torch.as_tensor(zT.T, dtype=torch.float64, device=dev)
+        nb = B.shape[1]
+        eta = eta + B @ beta[pos:pos + nb]
+        pos += nb
+    return eta

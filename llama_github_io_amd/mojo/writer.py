@@ -108,6 +108,14 @@ def _mojo_files(model, prefix: str = "") -> dict:
         XG.write(model, kv, blobs)
     elif algo == "rulefit":
         A.write_rulefit(model, kv, blobs)
+    elif algo == "gam":
+        gcols, gdoms = A.write_gam(model, kv, blobs)
+        cols = gcols + ([info.response] if info.response else [])
+        doms = gdoms + [None] * (len(gcols) - len(gdoms)) + ([info.response_domain] if info.response else [])
+        kv["n_features"] = len(cols) - (1 if info.response else 0)
+        kv["n_columns"] = len(cols)
+        kv["n_domains"] = sum(1 for d in doms if d is not None)
+        kv["mojo_version"] = "1.00"
     else:
         _generic_state(model, kv, blobs)
     buf = io.StringIO()
