@@ -280,3 +280,72 @@ def test_naivebayes_pojo_constants_reproduce_model(df):
             ll += np.where(na[:, None], 0, -0.5 * z * z - np.log(sd)[None, :] - 0.5 * np.log(2 * np.pi))
     e = np.exp(ll - ll.max(1, keepdims=True))
     assert np.allclose(e / e.sum(1, keepdims=True), mod.score_tensor(X).double().numpy(), atol=1e-5)
+
+
+def _const(src, name, kind="double"):
+    m = re.search(rf"public static final {kind}\[\](?:\[\])? {name} = new {kind}\[\](?:\[\])? \{{(.*?)\}};", src, re.S)
+    body = m.group(1)
+    if "{" in body:
+        return np.array([[float(v) for v in row.split(",") if v.strip()] for row in re.findall(r"\{(.*?)\}", body)])
+    return np.array([float(v) for v in body.split(",") if v.strip()])
+
+
+def _design_replay(src, D, P):
+    """Python replay of the emitted z[] construction (_design_java)."""
+    cats, offs = _const(src, "CATS", "int").astype(int), _const(src, "CAT_OFFS", "int").astype(int)
+    levels, modes = _const(src, "CAT_LEVELS", "int").astype(int), _const(src, "CAT_MODES", "int").astype(int)
+    nums = _const(src, "NUMS", "int").astype(int)
+    fill, sub, mul = _const(src, "NUM_FILL"), _const(src, "NUM_SUB"), _const(src, "NUM_MUL")
+    start = int(re.search(r"int col = c - (\d+);", src).group(1))
+    noff = int(re.search(r"z\[(\d+) \+ i\] = \(v - NUM_SUB", src).group(1))
+    n = len(D[0])
+    Z = np.zeros((n, P))
+    for i, j in enumerate(cats):
+        v = D[j]
+        c = np.where(np.isnan(v), modes[i], np.nan_to_num(v)).astype(int)
+        ok = (c >= 0) & (c < levels[i]) & (c - start >= 0)
+        Z[np.nonzero(ok)[0], offs[i] + (c - start)[ok]] = 1
+    for i, j in enumerate(nums):
+        v = np.where(np.isnan(D[j]), fill[i], D[j])
+        Z[:, noff + i] = (v - sub[i]) * mul[i]
+    return Z
+
+
+@pytest.mark.parametrize("algo", ["pca", "svd"])
+def test_pca_svd_pojo_reproduces_model(df, algo):
+    from h2o.estimators import H2OPrincipalComponentAnalysisEstimator, H2OSingularValueDecompositionEstimator
+    if algo == "pca":
+        m = H2OPrincipalComponentAnalysisEstimator(k=2, transform="STANDARDIZE", use_all_factor_levels=True)
+    else:
+        m = H2OSingularValueDecompositionEstimator(nv=2, transform="DEMEAN")
+    m.train(x=["a", "b", "c"], training_frame=df)
+    src = P.pojo_source(m._model)
+    assert "public final double[] score0(double[] data, double[] preds)" in src
+    V = _const(src, "EIGVECS")
+    Z = _design_replay(src, _cols(df, m._model), V.shape[0])
+    got = Z @ V
+    ref = m.predict(df).as_data_frame().to_numpy(dtype=float)
+    assert np.allclose(got, ref, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("y,booster", [("y", "gbtree"), ("r", "gbtree"), ("r", "gblinear")])
+def test_xgboost_pojo_reproduces_model(df, y, booster):
+    from h2o.estimators import H2OXGBoostEstimator
+    m = H2OXGBoostEstimator(ntrees=5, max_depth=3, seed=1, booster=booster)
+    m.train(x=["a", "b", "c"], y=y, training_frame=df)
+    src = P.pojo_source(m._model)
+    D = _cols(df, m._model)
+    if booster == "gblinear":
+        W, bias = _const(src, "W"), _const(src, "BIAS")
+        f = _design_replay(src, D, W.shape[1]) @ W[0] + bias[0]
+    else:
+        sub = _tree_functions(src)
+        init = float(re.search(r"double\[\] f = new double\[\] \{(.*?)\};", src).group(1))
+        f = np.full(len(D[0]), init)
+        for call in re.findall(r"f\[0\] \+= \(float\) (\w+)\.score0\(data\);", src):
+            f = f + np.float32(sub[call](D))
+    pred = m.predict(df).as_data_frame()
+    if y == "y":
+        assert np.allclose(1 / (1 + np.exp(-f)), pred["1"].to_numpy(), atol=1e-5)
+    else:
+        assert np.allclose(f, pred["predict"].to_numpy(), rtol=1e-5, atol=1e-4)
