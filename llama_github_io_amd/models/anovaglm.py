@@ -55,6 +55,8 @@ class ANOVAGLMTrainer:
 
     def fit(self, X, y, w, offset, info: DataInfo, valid=None, model_key=None):
         from scipy import stats
+        if int(self.p.get("type") or 0) not in (0, 3):
+            raise ValueError("ANOVAGLM: only type 3 sums of squares are supported (type=3 or the default 0)")
         from .glm import GLMTrainer
         t0 = time.time()
         p = self.p
@@ -86,7 +88,12 @@ class ANOVAGLMTrainer:
             spans.append((term, k, k + len(idx)))
             names += [f"{term}_{i}" for i in range(len(idx))]
             k += len(idx)
-        gp = {kk: v for kk, v in p.items() if kk in ("family", "link", "lambda_", "alpha", "seed")}
+        # GLM fields ANOVAGLM passes to its GLMs (ANOVAGLMUtils.buildGLMParameters; "type" and
+        # "save_transformed_framekeys" are the ANOVA-only ones)
+        gp = {kk: v for kk, v in p.items() if kk in ("family", "link", "lambda_", "alpha", "seed", "early_stopping", "prior",
+                                                     "plug_values", "missing_values_handling", "tweedie_variance_power",
+                                                     "tweedie_link_power", "theta", "solver", "max_iterations",
+                                                     "non_negative", "compute_p_values") and v is not None}
         gp["standardize"] = False
 
         def fitg(rows):

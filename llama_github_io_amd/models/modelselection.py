@@ -46,12 +46,30 @@ class ModelSelectionModel(Model):
         return self.best_models[i].output["coefficients"]
 
 
+# GLM parameters ModelSelection hands to every GLM it builds (ModelSelectionUtils.generateGLMParameters copies
+# the shared GLM fields of the ModelSelection parameters onto each GLM)
+_GLM_PASS = ("beta_constraints", "cold_start", "max_active_predictors", "prior", "remove_collinear_columns",
+             "startval", "objective_epsilon", "gradient_epsilon", "early_stopping", "plug_values",
+             "missing_values_handling", "standardize", "intercept", "non_negative", "max_iterations", "influence",
+             "tweedie_variance_power", "tweedie_link_power", "theta", "link", "solver")
+
+
 class ModelSelectionTrainer:
     def __init__(self, params):
         p = dict(MS_DEFAULTS)
         p.update({k: v for k, v in params.items() if v is not None})
         self.p = p
         self.job = None
+
+    def _glm(self, **kw):
+        from .glm import GLMTrainer
+        gp = {k: self.p[k] for k in _GLM_PASS if self.p.get(k) is not None}
+        gp.update(family=self.p["family"], lambda_=0.0)
+        if gp.get("influence") and not kw.get("final"):
+            gp.pop("influence")                       # diagnostics only for the reported best models
+        kw.pop("final", None)
+        gp.update(kw)
+        return GLMTrainer(gp)
 
     def fit(self, X, y, w, offset, info: DataInfo, valid=None, model_key=None):
         from .glm import GLMTrainer
@@ -86,7 +104,7 @@ class ModelSelectionTrainer:
                 return r2(cols)
             sub = DataInfo([info.x[j] for j in cols], np.asarray(info.iscat)[cols], [info.domains[j] for j in cols],
                            info.response, info.response_domain)
-            m = GLMTrainer(dict(family=p["family"], lambda_=0.0)).fit(X[cols].contiguous(), y, w, offset, sub)
+            m = self._glm().fit(X[cols].contiguous(), y, w, offset, sub)
             return -m.output["residual_deviance"]
 
         best = []
@@ -118,8 +136,7 @@ class ModelSelectionTrainer:
             while len(cur) >= kmin:
                 sub = DataInfo([info.x[j] for j in cur], np.asarray(info.iscat)[cur], [info.domains[j] for j in cur],
                                info.response, info.response_domain)
-                m = GLMTrainer(dict(family=p["family"], lambda_=0.0, compute_p_values=True, standardize=False)).fit(
-                    X[cur].contiguous(), y, w, offset, sub)
+                m = self._glm(compute_p_values=True, standardize=False).fit(X[cur].contiguous(), y, w, offset, sub)
                 hist.append((score(cur), list(cur)))
                 if len(cur) == kmin:
                     break
@@ -143,7 +160,7 @@ class ModelSelectionTrainer:
         for s, cols in best:
             sub = DataInfo([info.x[j] for j in cols], np.asarray(info.iscat)[cols], [info.domains[j] for j in cols],
                            info.response, info.response_domain)
-            m = GLMTrainer(dict(family=p["family"], lambda_=0.0)).fit(X[cols].contiguous(), y, w, offset, sub)
+            m = self._glm(final=True).fit(X[cols].contiguous(), y, w, offset, sub)
             model.best_cols.append(cols)
             model.best_models.append(m)
             rows.append(dict(model_name=f"best {len(cols)} predictor(s) model", predictor_names=[info.x[j] for j in cols],

@@ -38,10 +38,7 @@ HINTS = {
 UNSUPPORTED = {
     "glm": {"rand_link"},
     "gam": {"standardize_tp_gam_cols"},
-    "anovaglm": {"early_stopping", "prior", "type", "plug_values"},
-    "modelselection": {"beta_constraints", "cold_start", "influence", "max_active_predictors", "prior",
-                       "remove_collinear_columns", "startval", "gradient_epsilon",
-                       "objective_epsilon", "early_stopping", "plug_values"},
+
     "glrm": {"expand_user_y"},
     "rulefit": {"max_categorical_levels"},
     "infogram": {"max_iterations"},

@@ -96,3 +96,30 @@ def test_modelselection_backward_p_values_threshold():
     sizes_stop = [len(r["predictor_names"]) for r in stop._model.output["result"]]
     assert min(sizes_full) == 1 and min(sizes_stop) == 2        # x0, x1 are both highly significant
     assert sorted(stop._model.output["result"][0]["predictor_names"]) == ["x0", "x1"]
+
+
+def test_modelselection_and_anova_pass_glm_parameters():
+    """ModelSelection / ANOVAGLM build their GLMs with the shared GLM parameters (beta_constraints, prior,
+    remove_collinear_columns, ...); ANOVAGLM supports type 3 sums of squares only."""
+    from h2o.estimators import H2OANOVAGLMEstimator, H2OModelSelectionEstimator
+    h2o.init(verbose=False)
+    rng = np.random.default_rng(8)
+    n = 1200
+    X = rng.normal(size=(n, 3))
+    y = 2 * X[:, 0] - X[:, 1] + rng.normal(size=n)
+    fr = h2o.H2OFrame(pd.DataFrame({"x0": X[:, 0], "x1": X[:, 1], "x2": X[:, 2], "y": y}))
+    bc = h2o.H2OFrame(pd.DataFrame({"names": ["x0"], "lower_bounds": [-5.0], "upper_bounds": [1.0]}))
+    ms = H2OModelSelectionEstimator(mode="maxr", max_predictor_number=2, beta_constraints=bc)
+    ms.train(x=["x0", "x1", "x2"], y="y", training_frame=fr)
+    assert abs(ms._model.coef(2)["x0"] - 1.0) < 1e-6
+    yb = np.where(rng.random(n) < 1 / (1 + np.exp(-X[:, 0])), "1", "0")
+    frb = h2o.H2OFrame(pd.DataFrame({"x0": X[:, 0], "x1": X[:, 1], "y": yb}))
+    a0 = H2OANOVAGLMEstimator(family="binomial", highest_interaction_term=1)
+    a0.train(x=["x0", "x1"], y="y", training_frame=frb)
+    a1 = H2OANOVAGLMEstimator(family="binomial", highest_interaction_term=1, prior=0.1)
+    a1.train(x=["x0", "x1"], y="y", training_frame=frb)
+    i0 = a0._model.full.output["coefficients"]["Intercept"]
+    i1 = a1._model.full.output["coefficients"]["Intercept"]
+    assert i1 < i0 - 1.0
+    with pytest.raises(ValueError, match="type 3"):
+        H2OANOVAGLMEstimator(family="binomial", type=1).train(x=["x0", "x1"], y="y", training_frame=frb)
