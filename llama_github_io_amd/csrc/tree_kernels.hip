@@ -339,26 +339,12 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
   // of build tiles: blocks split only the rows that are histogrammed (no idle blocks on skipped siblings)
   const int n_nodes = meta[0], n_tiles = meta[2];
   if (n_nodes <= 0 || n_tiles <= 0) return;
-  // XCD-aware block order (1-D grid of G x nft blocks): the nft feature-tile blocks of one row range get
-  // block ids 8 apart, so the round-robin dispatch puts them on the SAME XCD at about the same time and the
-  // second one streams the rows out of that XCD's L2 instead of HBM (F > FTILE, e.g. 50 features: the
-  // y-major grid read every row twice from HBM).
-  const int nft = (F + FTILE - 1) / FTILE;
-  const int G = gridDim.x / nft;
-  int bx, ftile;
-  {
-    const int bid = blockIdx.x, full = (G / 8) * 8;
-    if (bid < full * nft) {
-      const int g = bid / (8 * nft), r = bid - g * 8 * nft;
-      ftile = r >> 3; bx = g * 8 + (r & 7);
-    } else {
-      const int rem = G - full, r = bid - full * nft;
-      ftile = r / rem; bx = full + r % rem;
-    }
-  }
-  const int per = (n_tiles + G - 1) / G;
-  const int t0 = bx * per, t1 = min(n_tiles, t0 + per);
+  const int per = (n_tiles + gridDim.x - 1) / gridDim.x;
+  const int t0 = blockIdx.x * per, t1 = min(n_tiles, t0 + per);
   if (t0 >= t1) return;
+  // (MEASURED: an XCD-aware 1-D order putting the feature-tile blocks of one row range on the same XCD
+  // made XGBoost 100M x 50 histograms 9-20 % SLOWER — 4.56 -> 4.97 ms filtered, 2.32 -> 2.80 ms plain)
+  const int ftile = blockIdx.y;
   const int W = stride >> 2;
   const int g = threadIdx.x / LPR, j = threadIdx.x % LPR;
   const int wabs = ftile * LPR + j;        // absolute word index of this lane
@@ -375,7 +361,7 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
     double v[4] = {wyy, (double)lcnt, 0, 0};
     block_sum4(v, red);
     __syncthreads();
-    const size_t so = (size_t)(bx + cur) * slot_doubles;
+    const size_t so = (size_t)(blockIdx.x + cur) * slot_doubles;
     flush_partial(h, nayy, v[0], ftile, F, f32 ? (double*)((float*)partials + so) : partials + so, qs, packed, acc,
                   f32 != 0);
     if (FILT && threadIdx.x == 0 && v[1] != 0.0) atomicAdd(nl_out + cur_parent, (int)v[1]);
@@ -1478,7 +1464,7 @@ int h2o_hist_build(const void* bins, int stride, const void* aw, const void* ay,
   const int nft = (F + FTILE - 1) / FTILE;
   // packed mode needs one int64 plane (66 KB): two 16-wave blocks share a CU (32 waves, 8 per SIMD)
   const size_t lds = (packed ? HIST_LDS_BYTES - HPLANE * 8 : HIST_LDS_BYTES) + 64 * 8;
-  const dim3 gr(grid * nft);                 // 1-D: k_hist_build derives (row block, feature tile), XCD-aware
+  const dim3 gr(grid, nft);
   if (packed) launch_hist<true>(gr, lds, s, bins, stride, aw, ay, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out, f32);
   else launch_hist<false>(gr, lds, s, bins, stride, aw, ay, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out, f32);
   return (int)hipGetLastError();
