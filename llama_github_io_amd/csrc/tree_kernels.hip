@@ -215,8 +215,17 @@ __device__ __forceinline__ float row_yy(float a, float b) {
 // Parent-decision filter of an odd-level histogram (k_hist_build<true>): only rows of the parent's
 // range that go to `dir` are accumulated; `count` lanes tally the parent's left-goers. The numeric
 // test runs on registers; only categorical splits read the bitset (LDS copy of the decision).
+// Bins layouts. Row-major: row r's F feature bytes at r * stride. PLANAR (F > 32): 32-feature planes,
+// feature f of row r at ((f >> 5) * N + r) * 32 + (f & 31) — the histogram block of feature tile t reads
+// only plane t (32 B per row) instead of pulling every 64-B row line once per feature tile.
+__device__ __forceinline__ size_t bin_off(long long row, int f, int stride, long long N, int planar) {
+  return planar ? ((size_t)(f >> 5) * (size_t)N + (size_t)row) * 32 + (f & 31) : (size_t)row * stride + f;
+}
+
 struct RowFilter {
   const Dec* pd;   // parent decision (LDS copy)
+  const uint8_t* fptr;   // byte of the split feature in row 0 (layout-aware); row r at fptr[r * fstride]
+  int fstride;
   int feat;        // its split feature
   int jw;          // lane (within the 8-lane row group) whose word holds `feat`, or -1: load the byte
   int dir;         // 0: accumulate left-goers, 1: right-goers
@@ -268,7 +277,7 @@ __device__ __forceinline__ void hist_rows(long long* h, float* nayy, const unsig
       // SoA aux planes: wY always, w only when rows are weighted (aw == null: unit weights)
       ab[u] = make_float2(aw ? aw[row] : 1.f, ay[row]);
       wd[u] = bins32[row * W + wc];
-      if (FILT && flt.jw < 0) sbyte[u] = ((const uint8_t*)bins32)[row * W * 4 + flt.feat];
+      if (FILT && flt.jw < 0) sbyte[u] = flt.fptr[row * (size_t)flt.fstride];
     }
     if (FILT && flt.jw >= 0) {
       // the split feature's byte is in lane jw's word of the same row group: one cross-lane read
@@ -328,7 +337,7 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
     const Node* __restrict__ nodes, const int* __restrict__ tile_prefix,
     const int* __restrict__ meta /*[0]=n_nodes [2]=n_build_tiles*/, int F, double* __restrict__ partials,
     int slot_doubles, const double* __restrict__ qs /*[sa, sb, 1/sa, 1/sb, sp, 1/sp]*/,
-    const Dec* __restrict__ pdec, int* __restrict__ nl_out, int f32) {
+    const Dec* __restrict__ pdec, int* __restrict__ nl_out, int f32, long long N, int planar) {
   constexpr bool packed = PACKED;
   extern __shared__ __attribute__((aligned(16))) long long smem64[];
   long long* h = smem64;                                 // 2 planes (PACKED: 1 -> two blocks per CU fit)
@@ -345,14 +354,16 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
   // (MEASURED: an XCD-aware 1-D order putting the feature-tile blocks of one row range on the same XCD
   // made XGBoost 100M x 50 histograms 9-20 % SLOWER — 4.56 -> 4.97 ms filtered, 2.32 -> 2.80 ms plain)
   const int ftile = blockIdx.y;
-  const int W = stride >> 2;
+  // planar: this block reads only its 32-feature plane (8 words per row, features counted from the plane)
+  const int W = planar ? LPR : stride >> 2;
   const int g = threadIdx.x / LPR, j = threadIdx.x % LPR;
-  const int wabs = ftile * LPR + j;        // absolute word index of this lane
-  const unsigned* bins32 = (const unsigned*)bins;
+  const int wabs = planar ? j : ftile * LPR + j;        // word index of this lane within a row of bins32
+  const int Fl = planar ? F - ftile * FTILE : F;
+  const unsigned* bins32 = (const unsigned*)(planar ? bins + (size_t)ftile * (size_t)N * 32 : bins);
   const float sa = (float)qs[0], sb = (float)qs[1], sp = (float)qs[4];
 
   __shared__ Dec spd;
-  RowFilter flt{&spd, 0, -1, 0, 0, 0, 0, false};
+  RowFilter flt{&spd, bins, stride, 0, -1, 0, 0, 0, 0, false};
   int lcnt = 0;
   int cur = -1, since = 0, cur_parent = -1;
   bool acc = false;
@@ -389,6 +400,8 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
       __syncthreads();
       if (FILT) {
         flt.feat = spd.feat;
+        flt.fptr = bins + bin_off(0, spd.feat, stride, N, planar);
+        flt.fstride = planar ? 32 : stride;
         const int jw = (spd.feat >> 2) - ftile * LPR;
         flt.jw = (jw >= 0 && jw < LPR) ? jw : -1;
         flt.dir = nd.dir;
@@ -398,7 +411,7 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
     }
     since += r1 - r0;
     float wf = 0.f;
-    hist_rows<FILT, PACKED>(h, nayy, bins32, aw, ay, W, wabs, F, j == 0 && ftile == 0, r0, r1, g, j, wf, sa, sb,
+    hist_rows<FILT, PACKED>(h, nayy, bins32, aw, ay, W, wabs, Fl, j == 0 && ftile == 0, r0, r1, g, j, wf, sa, sb,
                             sp, flt, lcnt);
     wyy += (double)wf;
   }
@@ -1037,7 +1050,7 @@ __global__ __launch_bounds__(LW * 64) void k_route(
     const Node* __restrict__ nodesA, const int* __restrict__ tpA, const int* __restrict__ metaA,
     const Dec* __restrict__ decA, const int* __restrict__ clA, const int* __restrict__ crA,
     const Dec* __restrict__ decB, const int* __restrict__ clB, const int* __restrict__ crB,
-    int4* __restrict__ curs) {
+    int4* __restrict__ curs, long long N, int planar) {
   const int n_nodes = metaA[0], n_tiles = metaA[1];
   const int t = blockIdx.x;
   if (t >= n_tiles) return;
@@ -1076,11 +1089,13 @@ __global__ __launch_bounds__(LW * 64) void k_route(
   for (int u = 0; u < LU; ++u) {
     const int row = min(wbase + u * 64 + lane, r1 - 1);   // clamped into the node: no divergence
     if (NV > 0) {
-      const uint4* s4 = (const uint4*)(sbins + (size_t)row * stride);
+      // planar (NV == 4): words 0-7 from plane 0, 8-15 from plane 1 — the same registers as a 64-B row
+      const uint4* s4 = (const uint4*)(sbins + (planar ? (size_t)row * 32 : (size_t)row * stride));
+      const uint4* s4b = planar ? (const uint4*)(sbins + ((size_t)N + row) * 32) : s4 + 2;
       rv0[u] = s4[0];
       rv1[u] = NV > 1 ? s4[1] : make_uint4(0u, 0u, 0u, 0u);
-      rv2[u] = NV > 2 ? s4[2] : make_uint4(0u, 0u, 0u, 0u);
-      rv3[u] = NV > 3 ? s4[3] : make_uint4(0u, 0u, 0u, 0u);
+      rv2[u] = NV > 2 ? s4b[0] : make_uint4(0u, 0u, 0u, 0u);
+      rv3[u] = NV > 3 ? s4b[1] : make_uint4(0u, 0u, 0u, 0u);
     }
     ry[u] = say[row];
     rw[u] = saw ? saw[row] : 1.f;
@@ -1092,13 +1107,13 @@ __global__ __launch_bounds__(LW * 64) void k_route(
     int dA = 0, dB = 0;
     if (valid && featA >= 0)
       dA = dec_go_left(&sA, NV > 2 ? row_byte4(rv0[u], rv1[u], rv2[u], rv3[u], featA)
-                                   : NV > 0 ? row_byte(rv0[u], rv1[u], featA) : sbins[(size_t)row * stride + featA]) ? 0 : 1;
+                                   : NV > 0 ? row_byte(rv0[u], rv1[u], featA) : sbins[bin_off(row, featA, stride, N, planar)]) ? 0 : 1;
     if (valid && sC[dA] >= 0) {
       const Dec* b = &sB[dA];
       const int fb = b->feat;
       if (fb >= 0)
         dB = dec_go_left(b, NV > 2 ? row_byte4(rv0[u], rv1[u], rv2[u], rv3[u], fb)
-                                   : NV > 0 ? row_byte(rv0[u], rv1[u], fb) : sbins[(size_t)row * stride + fb]) ? 0 : 1;
+                                   : NV > 0 ? row_byte(rv0[u], rv1[u], fb) : sbins[bin_off(row, fb, stride, N, planar)]) ? 0 : 1;
     }
     q[u] = 2 * dA + dB;
     mv[u] = valid && sG[q[u]] >= 0;
@@ -1141,13 +1156,21 @@ __global__ __launch_bounds__(LW * 64) void k_route(
     int pos = rank[u];
 #pragma unroll
     for (int k = 0; k < 4; ++k) if (q[u] == k) pos += off[k];
-    unsigned* dst = db32 + (size_t)pos * W;
+    unsigned* dst = db32 + (size_t)pos * (planar ? 8 : W);
     if (NV > 0) {
       uint4* d4 = (uint4*)dst;
+      uint4* d4b = planar ? (uint4*)(db32 + ((size_t)N + pos) * 8) : d4 + 2;
       d4[0] = rv0[u];
       if (NV > 1) d4[1] = rv1[u];
-      if (NV > 2) d4[2] = rv2[u];
-      if (NV > 3) d4[3] = rv3[u];
+      if (NV > 2) d4b[0] = rv2[u];
+      if (NV > 3) d4b[1] = rv3[u];
+    } else if (planar) {
+      for (int pl = 0; pl < (W >> 3); ++pl) {
+        const unsigned* src = sb32 + ((size_t)pl * N + row) * 8;
+        unsigned* d = db32 + ((size_t)pl * N + pos) * 8;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) d[k] = src[k];
+      }
     } else {
       const unsigned* src = sb32 + (size_t)row * W;
       if (W <= LMAXW) {
@@ -1183,7 +1206,7 @@ template <int NV>
 __global__ __launch_bounds__(256) void k_leaf_assign(
     const uint8_t* __restrict__ bins, int stride, long long N, const LevelPtrs* __restrict__ lv, int D,
     const float* __restrict__ an, const float* __restrict__ ad, const double* __restrict__ qs,
-    int* __restrict__ leaf_of_row, unsigned long long* __restrict__ leafq, int leaf_cap, int n_nodes) {
+    int* __restrict__ leaf_of_row, unsigned long long* __restrict__ leafq, int leaf_cap, int n_nodes, int planar) {
   extern __shared__ __align__(16) unsigned char la_smem[];
   __shared__ int sbase[TP_MAXL_DEV + 1];
   const bool lds = leaf_cap <= LEAF_LDS_MAX;
@@ -1214,11 +1237,12 @@ __global__ __launch_bounds__(256) void k_leaf_assign(
        row += (long long)gridDim.x * blockDim.x) {
     uint4 v0 = make_uint4(0u, 0u, 0u, 0u), v1 = v0, v2 = v0, v3 = v0;
     if (NV > 0) {
-      const uint4* s4 = (const uint4*)(bins + (size_t)row * stride);
+      const uint4* s4 = (const uint4*)(bins + (planar ? (size_t)row * 32 : (size_t)row * stride));
+      const uint4* s4b = planar ? (const uint4*)(bins + ((size_t)N + row) * 32) : s4 + 2;
       v0 = s4[0];
       if (NV > 1) v1 = s4[1];
-      if (NV > 2) v2 = s4[2];
-      if (NV > 3) v3 = s4[3];
+      if (NV > 2) v2 = s4b[0];
+      if (NV > 3) v3 = s4b[1];
     }
     const float a_n = an[row], a_d = ad[row];    // issued before the walk: latency overlaps it
     int i = 0, leaf = 0;
@@ -1230,7 +1254,7 @@ __global__ __launch_bounds__(256) void k_leaf_assign(
           c = e.z;                               // terminal node: child_l == child_r == its leaf
         } else {
           const int b = NV > 2 ? row_byte4(v0, v1, v2, v3, e.x) : NV > 0 ? row_byte(v0, v1, e.x)
-                                                                         : bins[(size_t)row * stride + e.x];
+                                                                         : bins[bin_off(row, e.x, stride, N, planar)];
           bool gl;
           if (b == NA_BIN) gl = (e.y >> 16) & 1;
           else if ((e.y >> 17) & 1) gl = (lv[d].dec[i].bits[b >> 5] >> (b & 31)) & 1u;
@@ -1244,7 +1268,7 @@ __global__ __launch_bounds__(256) void k_leaf_assign(
           c = lv[d].cl[i];
         } else {
           const int b = NV > 2 ? row_byte4(v0, v1, v2, v3, f) : NV > 0 ? row_byte(v0, v1, f)
-                                                                       : bins[(size_t)row * stride + f];
+                                                                       : bins[bin_off(row, f, stride, N, planar)];
           c = dec_go_left(dc, b) ? lv[d].cl[i] : lv[d].cr[i];
         }
       }
@@ -1286,12 +1310,12 @@ __global__ void k_leafsum_finish(unsigned long long* __restrict__ leafq, const d
 // categorical (iscat): bin = code (< nb) else NA. NaN -> NA_BIN.
 __global__ void k_bin_assign(const float* __restrict__ X, long long N, int F, int stride,
                              const float* __restrict__ edges, int max_edges, const int* __restrict__ nedges,
-                             const int* __restrict__ iscat, uint8_t* __restrict__ bins) {
+                             const int* __restrict__ iscat, uint8_t* __restrict__ bins, int planar) {
   const long long row = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (row >= N) return;
-  uint8_t* out = bins + row * stride;
   for (int f = 0; f < stride; ++f) {
-    if (f >= F) { out[f] = 0; continue; }
+    uint8_t* outf = bins + bin_off(row, f, stride, N, planar);
+    if (f >= F) { *outf = 0; continue; }
     const float x = X[(long long)f * N + row];
     int b;
     if (x != x) b = NA_BIN;
@@ -1304,7 +1328,7 @@ __global__ void k_bin_assign(const float* __restrict__ X, long long N, int F, in
       while (lo < hi) { const int mid = (lo + hi) >> 1; if (e[mid] <= x) lo = mid + 1; else hi = mid; }
       b = lo;
     }
-    out[f] = (uint8_t)b;
+    *outf = (uint8_t)b;
   }
 }
 
@@ -1432,17 +1456,18 @@ __global__ void k_leaf_values(const double* __restrict__ leafsum, int n, int log
 template <bool PACKED>
 static void launch_hist(dim3 grid, size_t lds, hipStream_t s, const void* bins, int stride, const void* aw,
                         const void* ay, const void* nodes, const void* tile_prefix, const void* meta, int F,
-                        void* partials, int slot_doubles, const void* qs, const void* pdec, void* nl_out, int f32) {
+                        void* partials, int slot_doubles, const void* qs, const void* pdec, void* nl_out, int f32,
+                        long long N, int planar) {
   if (pdec)
     hipLaunchKernelGGL((k_hist_build<true, PACKED>), grid, dim3(BLK), lds, s, (const uint8_t*)bins, stride,
                        (const float*)aw, (const float*)ay, (const Node*)nodes, (const int*)tile_prefix,
                        (const int*)meta, F, (double*)partials, slot_doubles, (const double*)qs, (const Dec*)pdec,
-                       (int*)nl_out, f32);
+                       (int*)nl_out, f32, N, planar);
   else
     hipLaunchKernelGGL((k_hist_build<false, PACKED>), grid, dim3(BLK), lds, s, (const uint8_t*)bins, stride,
                        (const float*)aw, (const float*)ay, (const Node*)nodes, (const int*)tile_prefix,
                        (const int*)meta, F, (double*)partials, slot_doubles, (const double*)qs, (const Dec*)nullptr,
-                       (int*)nullptr, f32);
+                       (int*)nullptr, f32, N, planar);
 }
 
 extern "C" {
@@ -1460,13 +1485,14 @@ int h2o_tree_sizes(int* out) {
 // partials: >= (grid + max nodes of the level) slots of slot_doubles
 int h2o_hist_build(const void* bins, int stride, const void* aw, const void* ay, const void* nodes,
                    const void* tile_prefix, const void* meta, int F, void* partials, int slot_doubles, const void* qs,
-                   int grid, int packed, const void* pdec, void* nl_out, int f32, hipStream_t s) {
+                   int grid, int packed, const void* pdec, void* nl_out, int f32, long long N, int planar,
+                   hipStream_t s) {
   const int nft = (F + FTILE - 1) / FTILE;
   // packed mode needs one int64 plane (66 KB): two 16-wave blocks share a CU (32 waves, 8 per SIMD)
   const size_t lds = (packed ? HIST_LDS_BYTES - HPLANE * 8 : HIST_LDS_BYTES) + 64 * 8;
   const dim3 gr(grid, nft);
-  if (packed) launch_hist<true>(gr, lds, s, bins, stride, aw, ay, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out, f32);
-  else launch_hist<false>(gr, lds, s, bins, stride, aw, ay, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out, f32);
+  if (packed) launch_hist<true>(gr, lds, s, bins, stride, aw, ay, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out, f32, N, planar);
+  else launch_hist<false>(gr, lds, s, bins, stride, aw, ay, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out, f32, N, planar);
   return (int)hipGetLastError();
 }
 
@@ -1582,12 +1608,13 @@ static int nv_of(int stride) {
 int h2o_route(const void* sbins, const void* say, const void* saw, void* dbins, void* day, void* daw, int stride,
               const void* nodesA, const void* tpA, const void* metaA, const void* decA, const void* clA,
               const void* crA, const void* decB, const void* clB, const void* crB, void* curs, int tiles_cap,
-              hipStream_t s) {
+              long long N, int planar, hipStream_t s) {
+  if (planar && (stride % 32 != 0 || stride < 64)) return (int)hipErrorInvalidValue;
 #define ROUTE_LAUNCH(NV)                                                                                       \
   hipLaunchKernelGGL((k_route<NV>), dim3(tiles_cap), dim3(LW * 64), 0, s, (const uint8_t*)sbins,              \
                      (const float*)say, (const float*)saw, (uint8_t*)dbins, (float*)day, (float*)daw, stride,  \
                      (const Node*)nodesA, (const int*)tpA, (const int*)metaA, (const Dec*)decA, (const int*)clA, \
-                     (const int*)crA, (const Dec*)decB, (const int*)clB, (const int*)crB, (int4*)curs)
+                     (const int*)crA, (const Dec*)decB, (const int*)clB, (const int*)crB, (int4*)curs, N, planar)
   switch (nv_of(stride)) {
     case 4: ROUTE_LAUNCH(4); break;
     case 3: ROUTE_LAUNCH(3); break;
@@ -1602,7 +1629,7 @@ int h2o_route(const void* sbins, const void* say, const void* saw, void* dbins, 
 // leaf id of every row (original order) + fixed-point leaf sums -> fp64 leafsum[leaf_cap][2]
 int h2o_leaf_assign(const void* master, int stride, long long N, const void* lvptrs, int D, const void* an,
                     const void* ad, const void* qs, void* leaf_of_row, void* leafq, int leaf_cap, void* leafsum,
-                    int n_nodes, hipStream_t s) {
+                    int n_nodes, int planar, hipStream_t s) {
   if (D > TP_MAXL_DEV) return (int)hipErrorInvalidValue;
   long long grid = (N + 255) / 256;
   if (grid > 2048) grid = 2048;
@@ -1611,7 +1638,7 @@ int h2o_leaf_assign(const void* master, int stride, long long N, const void* lvp
                      (n_nodes <= LEAF_TREE_MAX ? (size_t)16 * n_nodes : 0);
 #define LA(NV) hipLaunchKernelGGL((k_leaf_assign<NV>), dim3((unsigned)grid), dim3(256), lds, s, (const uint8_t*)master, \
                                   stride, N, (const LevelPtrs*)lvptrs, D, (const float*)an, (const float*)ad,          \
-                                  (const double*)qs, (int*)leaf_of_row, (unsigned long long*)leafq, leaf_cap, n_nodes)
+                                  (const double*)qs, (int*)leaf_of_row, (unsigned long long*)leafq, leaf_cap, n_nodes, planar)
   switch (nv_of(stride)) {
     case 4: LA(4); break;
     case 3: LA(3); break;
@@ -1639,11 +1666,12 @@ int h2o_qscale(void* amax_bits, void* qs, void* counters, long long N, hipStream
 }
 
 int h2o_bin_assign(const void* X, long long N, int F, int stride, const void* edges, int max_edges,
-                   const void* nedges, const void* iscat, void* bins, hipStream_t s) {
+                   const void* nedges, const void* iscat, void* bins, int planar, hipStream_t s) {
+  if (planar && (stride % 32 != 0 || stride < 64)) return (int)hipErrorInvalidValue;
   const int blk = 256;
   const long long grid = (N + blk - 1) / blk;
   hipLaunchKernelGGL(k_bin_assign, dim3((unsigned)grid), dim3(blk), 0, s, (const float*)X, N, F, stride,
-                     (const float*)edges, max_edges, (const int*)nedges, (const int*)iscat, (uint8_t*)bins);
+                     (const float*)edges, max_edges, (const int*)nedges, (const int*)iscat, (uint8_t*)bins, planar);
   return (int)hipGetLastError();
 }
 
@@ -1697,6 +1725,7 @@ struct TreePlan {
   int sliced, fs0, fsn, sslot;
   void *cand_local, *hrecv;
   double leaf_lam, leaf_l1;   // k_leaf_values regularisation (XGBoost leaves; 0 for GBM)
+  int planar, pad_planar;     // bins layout of master and the ping-pong buffers (see bin_off)
 };
 
 static inline const float* tp_aux(const TreePlan* P, int c) { return (const float*)P->aux + (size_t)c * P->N; }
@@ -1714,7 +1743,7 @@ static int tp_route(const TreePlan* P, int e, hipStream_t s) {
   const int di = (e / 2) % 2;
   return h2o_route(sb, sy, sw, P->bb[di], P->by[di], P->unit ? nullptr : P->bw[di], P->stride, P->nodes[e], P->tp[e],
                    P->meta[e], P->dec[e], P->cl[e], P->cr[e], P->dec[e + 1], P->cl[e + 1], P->cr[e + 1],
-                   P->cur[e + 1], P->tiles_cap[e], s);
+                   P->cur[e + 1], P->tiles_cap[e], P->N, P->planar, s);
 }
 
 #define TP_CHECK(x) do { int rc_ = (x); if (rc_) return rc_; } while (0)
@@ -1729,7 +1758,8 @@ int h2o_tree_root(const TreePlan* P, hipStream_t s) {
   TP_CHECK(h2o_qscale(P->amax_bits, P->qs, P->counters, P->N, s));
   const int g0 = P->tiles_cap[0] < P->grid ? P->tiles_cap[0] : P->grid;
   TP_CHECK(h2o_hist_build(P->master, P->stride, P->unit ? nullptr : tp_aux(P, 0), tp_aux(P, 1), P->nodes[0], P->bp[0],
-                          P->meta[0], P->F, P->partials, P->slot, P->qs, g0, P->packed, nullptr, nullptr, P->pf32, s));
+                          P->meta[0], P->F, P->partials, P->slot, P->qs, g0, P->packed, nullptr, nullptr, P->pf32, P->N,
+                          P->planar, s));
   return h2o_hist_reduce(P->partials, P->slot, P->used, P->nodes[0], P->bp[0], P->meta[0], 1, g0,
                          P->sliced ? P->hbuild : P->hist0, nullptr, nullptr, P->pf32, s);
 }
@@ -1778,7 +1808,7 @@ int h2o_tree_grow(const TreePlan* P, int d, int dist, hipStream_t s) {
     gh = P->tiles_cap[d] < P->grid ? P->tiles_cap[d] : P->grid;
     tp_level_buf(P, d, sb, sy, sw);
     rc = h2o_hist_build(sb, P->stride, sw, sy, P->nodes[d + 1], P->bp[d + 1], P->meta[d + 1], P->F, P->partials,
-                        P->slot, P->qs, gh, P->packed, P->dec[d], P->nl[d], P->pf32, s);
+                        P->slot, P->qs, gh, P->packed, P->dec[d], P->nl[d], P->pf32, P->N, P->planar, s);
   } else {
     // regroup level d-1's rows two levels down, then histogram level d+1 (even) contiguously
     rc = tp_route(P, d - 1, s);
@@ -1788,7 +1818,7 @@ int h2o_tree_grow(const TreePlan* P, int d, int dist, hipStream_t s) {
     gh = P->tiles_cap[d + 1] < P->grid ? P->tiles_cap[d + 1] : P->grid;
     tp_level_buf(P, d + 1, sb, sy, sw);
     rc = h2o_hist_build(sb, P->stride, sw, sy, P->nodes[d + 1], P->bp[d + 1], P->meta[d + 1], P->F, P->partials,
-                        P->slot, P->qs, gh, P->packed, nullptr, nullptr, P->pf32, s);
+                        P->slot, P->qs, gh, P->packed, nullptr, nullptr, P->pf32, P->N, P->planar, s);
   }
   if (rc) return -rc;
   if (!dist)
@@ -1822,7 +1852,7 @@ int h2o_tree_leaves(const TreePlan* P, hipStream_t s) {
   int n_nodes = 0;
   for (int d = 0; d < P->D; ++d) n_nodes += P->caps[d];
   return h2o_leaf_assign(P->master, P->stride, P->N, P->lvptrs, P->D, tp_aux(P, 2), tp_aux(P, 3), P->qs,
-                         P->leaf_of_row, P->leafq, P->leaf_cap, P->leafsum, n_nodes, s);
+                         P->leaf_of_row, P->leafq, P->leaf_cap, P->leafsum, n_nodes, P->planar, s);
 }
 
 // single process: the whole tree (root .. leaves) in one host call

@@ -218,7 +218,7 @@ class SharedTreeTrainer:
             self.binning = fit_binning(X, info.iscat, info.nlevels, max_bins=max_bins, seed=self.seed,
                                        max_cat_bins=int(p.get("nbins_cats") or 1024), sample=bsample)
         self._check_binning(self.binning)
-        bins = apply_binning(self.binning, X)
+        bins = apply_binning(self.binning, X, planar=X.is_cuda)
         mono = None
         if p.get("monotone_constraints"):
             mono = np.zeros(F, dtype=np.int32)

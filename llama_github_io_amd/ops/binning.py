@@ -132,7 +132,9 @@ def fit_binning(X: torch.Tensor, iscat, nlevels=None, max_bins: int = MAX_DATA_B
         nbins[f] = e.size + 1
     # rows of more than 12 features are padded to 16 B multiples so the partition kernel moves them
     # with 16-byte vector loads/stores (2 per 28-feature row instead of 7 dword pairs)
-    stride = (F + 3) // 4 * 4 if F <= 12 else (F + 15) // 16 * 16
+    # > 32 features: whole 32-byte planes (the device engine stores such bins PLANAR, one plane per
+    # histogram feature tile — apply_binning(planar=True))
+    stride = (F + 3) // 4 * 4 if F <= 12 else ((F + 15) // 16 * 16 if F <= 32 else (F + 31) // 32 * 32)
     return Binning(F, stride, edges, nbins, iscat, nlevels, l2b)
 
 
@@ -149,8 +151,9 @@ def _edge_table(b: Binning, device):
     return torch.from_numpy(tab).to(device), torch.from_numpy(ned).to(device), maxe
 
 
-def apply_binning(b: Binning, X: torch.Tensor) -> torch.Tensor:
-    """X float32 [F, N] -> uint8 bins [N, stride] (row-major) on X's device."""
+def apply_binning(b: Binning, X: torch.Tensor, planar: bool = False) -> torch.Tensor:
+    """X float32 [F, N] -> uint8 bins [N, stride] (row-major) on X's device; with ``planar`` (device, stride a
+    multiple of 32 and >= 64) the [stride / 32, N, 32] plane layout of the tree engine."""
     F, N = X.shape
     assert F == b.F
     Xc = X
@@ -167,9 +170,11 @@ def apply_binning(b: Binning, X: torch.Tensor) -> torch.Tensor:
     if X.is_cuda:
         tab, ned, maxe = _edge_table(b, X.device)
         iscat = torch.from_numpy(b.iscat.astype(np.int32)).to(X.device)
-        out = torch.empty(N, b.stride, dtype=torch.uint8, device=X.device)
+        planar = bool(planar) and b.stride >= 64 and b.stride % 32 == 0
+        out = (torch.empty(b.stride // 32, N, 32, dtype=torch.uint8, device=X.device) if planar
+               else torch.empty(N, b.stride, dtype=torch.uint8, device=X.device))
         nat.call("h2o_bin_assign", Xc.data_ptr(), N, F, b.stride, tab.data_ptr(), maxe, ned.data_ptr(),
-                 iscat.data_ptr(), out.data_ptr(), nat.stream_ptr(X.device))
+                 iscat.data_ptr(), out.data_ptr(), int(planar), nat.stream_ptr(X.device))
         return out
     out = torch.zeros(N, b.stride, dtype=torch.uint8)
     for f in range(F):

@@ -408,7 +408,7 @@ class _TreePlan(ctypes.Structure):
                 [("edges", _vp), ("nb_level", _ci * _MAXL), ("pad3", _ci)] +
                 [("ic_map", _vp), ("ic", _vp * _MAXL)] +
                 [(n, _ci) for n in ("sliced", "fs0", "fsn", "sslot")] + [("cand_local", _vp), ("hrecv", _vp)] +
-                [("leaf_lam", _cd), ("leaf_l1", _cd)])
+                [("leaf_lam", _cd), ("leaf_l1", _cd)] + [("planar", _ci), ("pad_planar", _ci)])
 
 
 class _Arena:
@@ -435,7 +435,15 @@ class GpuTreeBuilder:
 
     def __init__(self, bins: torch.Tensor, F: int, nbins_f, iscat_f, mono_f, max_depth: int, params: SplitParams,
                  node_cap: int = 1 << 14, grid: int = 256):
-        assert bins.is_cuda and bins.dtype == torch.uint8 and bins.dim() == 2
+        assert bins.is_cuda and bins.dtype == torch.uint8 and bins.dim() in (2, 3)
+        # > 32 features: PLANAR bins [stride / 32, N, 32] (apply_binning(planar=True)); a row-major [N, stride]
+        # input with whole 32-byte planes is converted once (H2O_BINS_ROWMAJOR=1 keeps row-major: A/B runs)
+        if bins.dim() == 2 and bins.shape[1] >= 64 and bins.shape[1] % 32 == 0 and \
+                os.environ.get("H2O_BINS_ROWMAJOR") != "1":
+            bins = bins.view(bins.shape[0], bins.shape[1] // 32, 32).permute(1, 0, 2).contiguous()
+        self.planar = bins.dim() == 3
+        if self.planar:
+            assert bins.shape[2] == 32 and bins.shape[0] >= 2
         self.lib = nat.hip()
         sz = np.zeros(8, dtype=np.int32)
         self.lib.h2o_tree_sizes(sz.ctypes.data)
@@ -444,7 +452,10 @@ class GpuTreeBuilder:
         self.TILE = int(sz[3])
         dev = bins.device
         self.dev = dev
-        self.N, self.stride = bins.shape
+        if self.planar:
+            self.N, self.stride = bins.shape[1], bins.shape[0] * 32
+        else:
+            self.N, self.stride = bins.shape
         assert self.stride % 4 == 0
         self.F = F
         self.D = D = max(1, int(max_depth))
@@ -456,7 +467,7 @@ class GpuTreeBuilder:
         # fp32 per-block partial histograms (half the flush + reduce bytes; the reduce sums in fp64)
         # MEASURED (scripts/gpu_small_shard_sweep.sh): 0.511 -> 0.492 ms/tree at 1.375M rows and 0.718 -> 0.707
         # at 2.75M (the per-rank shards of an 8/4-GPU HIGGS run); no gain at 11M. Small test shards keep fp64.
-        self.pf32 = int(os.environ.get("H2O_PARTIAL_F32", "1" if 1_000_000 <= bins.shape[0] <= 4_000_000 else "0"))
+        self.pf32 = int(os.environ.get("H2O_PARTIAL_F32", "1" if 1_000_000 <= self.N <= 4_000_000 else "0"))
         self.master = bins
         N, T = self.N, self.TILE
         self.caps = [min(1 << d, node_cap) for d in range(D)] + [1]
@@ -486,7 +497,7 @@ class GpuTreeBuilder:
         self.amax_bits = torch.zeros(4 * AMAX_SHARDS, dtype=torch.int32, device=dev)
         self._soa = None                       # [4, N] staging of row-major aux input
         # ping-pong row payload buffers: bins + wY (+ w for weighted rows, allocated on first use)
-        self.bufs = [dict(bins=torch.empty(N, self.stride, dtype=torch.uint8, device=dev),
+        self.bufs = [dict(bins=torch.empty(N * self.stride, dtype=torch.uint8, device=dev),
                           y=torch.empty(N, dtype=torch.float32, device=dev), w=None) for _ in range(2)]
         # small per-level arrays in one arena
         ar = _Arena()
@@ -625,6 +636,7 @@ class GpuTreeBuilder:
             P.nb_level[d] = p.adapt_nb(d) if P.edges else 0
         self._set_plan_ic(P)
         P.sliced, P.fs0, P.fsn, P.sslot = int(self.sliced), self.fs0, self.fsn, self.sslot
+        P.planar = int(self.planar)
         P.cand_local = self.cand_local.data_ptr() if self.sliced else 0
         P.hrecv = self.hrecv.data_ptr() if self.sliced else 0
         return P

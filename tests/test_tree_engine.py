@@ -105,6 +105,14 @@ def test_gpu_bin_assign_matches_cpu():
     cpu = apply_binning(b, X)
     gpu = apply_binning(b, X.cuda()).cpu()
     assert torch.equal(cpu, gpu)
+    # planar layout (F > 32): plane p holds features 32p .. 32p + 31 of every row
+    X2, y2, info2 = _data(N=20000, F=70, cat=True, seed=3)
+    b2 = fit_binning(X2, info2.iscat, info2.nlevels, max_bins=255)
+    assert b2.stride == 96
+    rows = apply_binning(b2, X2)
+    pl = apply_binning(b2, X2.cuda(), planar=True).cpu()
+    assert pl.shape == (3, 20000, 32)
+    assert torch.equal(pl.permute(1, 0, 2).reshape(20000, 96), rows)
 
 
 @pytest.mark.gpu
