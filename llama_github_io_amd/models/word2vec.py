@@ -241,6 +241,15 @@ class Word2VecTrainer:
         if cur:
             sents.append(cur)
         cnt = Counter(w for s in sents for w in s)
+        from ..parallel import collectives as coll
+        dist = coll.is_dist()
+        if dist:
+            # row-sharded text (WordVectorTrainer's MRTask over chunks): the vocabulary is the merged word
+            # count of every rank (a summary bounded by the vocabulary, not the rows)
+            merged = Counter()
+            for c in coll.all_gather_object(dict(cnt)):
+                merged.update(c)
+            cnt = merged
         words = sorted([w for w, c in cnt.items() if c >= int(p["min_word_freq"])], key=lambda w: (-cnt[w], w))
         vocab = {w: i for i, w in enumerate(words)}
         V, D = len(words), int(p["vec_size"])
@@ -271,10 +280,17 @@ class Word2VecTrainer:
         cbow = str(p.get("word_model") or "SkipGram").lower() == "cbow"
         if str(p.get("word_model") or "SkipGram").lower() not in ("skipgram", "cbow"):
             raise ValueError(f"word_model must be SkipGram or CBOW, got {p.get('word_model')!r}")
+        def sync():
+            # WordVectorTrainer.reduce / postGlobal: each rank trained its own sentences this epoch; the
+            # model is the average of the ranks' weights
+            if dist:
+                for t in (syn0, syn1):
+                    t.copy_(coll.all_reduce_(t.contiguous().to(coll.comm_device())).to(t.device) / coll.world())
         for ep in range(epochs):
             if cbow:
                 step, n_steps_est = self._cbow_epoch(ids, counts, total, ss, win, rng, gen, syn0, syn1, P_idx, P_code,
                                                      P_mask, lr0, B, step, n_steps_est, epochs, dev)
+                sync()
                 if self.job is not None:
                     self.job.set_progress((ep + 1) / epochs)
                 continue
@@ -296,6 +312,7 @@ class Word2VecTrainer:
                     centers.append(s[pos[ok]])
                     ctxs.append(s[pos[ok] + off])
             if not centers:
+                sync()
                 continue
             c = torch.from_numpy(np.concatenate(centers)).to(dev)
             x = torch.from_numpy(np.concatenate(ctxs)).to(dev)
@@ -316,6 +333,7 @@ class Word2VecTrainer:
                 du = g[:, :, None] * h[:, None, :]
                 syn1.index_add_(0, nodes.reshape(-1), du.reshape(-1, D))
                 syn0.index_add_(0, xb, dh)
+            sync()
             if self.job is not None:
                 self.job.set_progress((ep + 1) / epochs)
         model = Word2VecModel(model_key or make_key("word2vec"), p, info)

@@ -248,3 +248,56 @@ def test_sharded_metrics_merge_without_row_gathers(world):
     assert out["n"] == single["n"]
     assert np.allclose(out["thr"], single["thr"], rtol=0, atol=0) and np.allclose(out["lift"], single["lift"], rtol=1e-12)
     assert np.allclose(out["hits"], single["hits"], rtol=1e-12) and np.allclose(out["cm"], single["cm"], rtol=1e-12)
+
+
+def _w2v_tokens():
+    rng = np.random.default_rng(0)
+    A, B = ["cat", "dog", "cow", "pig"], ["one", "two", "six", "ten"]
+    words = []
+    for i in range(1600):
+        words += list(rng.choice(A if i % 2 else B, 6)) + [None]
+    return words, A, B
+
+
+def _w2v_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import torch.distributed as dist
+    from llama_github_io_amd.models.base import DataInfo
+    from llama_github_io_amd.models.word2vec import Word2VecTrainer
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        words, A, B = _w2v_tokens()
+        n = len(words)
+        local = words[rank * n // world:(rank + 1) * n // world]
+        tr = Word2VecTrainer(dict(vec_size=10, min_word_freq=1, epochs=5, seed=1, sent_sample_rate=0, window_size=3))
+        m = tr.fit_strings(np.array(local, dtype=object), DataInfo(["w"], np.zeros(1, np.int32), [None], None, None))
+        vec = {w: m.vectors[i].double().numpy() for w, i in m.vocab.items()}
+        cos = lambda a, b: float(vec[a] @ vec[b] / np.linalg.norm(vec[a]) / np.linalg.norm(vec[b]))  # noqa: E731
+        within = np.mean([cos(a, b) for g in (A, B) for a in g for b in g if a < b])
+        across = np.mean([cos(a, b) for a in A for b in B])
+        q.put((rank, sorted(m.vocab), within, across, float(m.vectors.sum())))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_word2vec_sharded_text_trains_one_model():
+    """Word2Vec over row-sharded text (WordVectorTrainer MRTask): merged vocabulary, per-epoch model
+    averaging; every rank ends with the same vectors, and co-occurring words are nearer."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_w2v_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = sorted([q.get(timeout=300) for _ in range(2)])
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    (_, v0, w0, a0, s0), (_, v1, w1, a1, s1) = out
+    assert v0 == v1 and abs(s0 - s1) < 1e-6
+    assert w0 > a0 + 0.3, (w0, a0)
