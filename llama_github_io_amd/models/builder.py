@@ -42,7 +42,7 @@ class AlgoSpec:
 # program on the same data) — correct everywhere, scaled only where the collectives exist.
 DISTRIBUTED = {"gbm", "drf", "xgboost", "glm", "kmeans", "deeplearning", "naivebayes", "pca", "quantile",
                "isolationforest", "extendedisolationforest", "svd", "targetencoder", "gam", "anovaglm",
-               "modelselection", "upliftdrf", "dt", "glrm", "rulefit", "word2vec"}
+               "modelselection", "upliftdrf", "dt", "glrm", "rulefit", "word2vec", "isotonicregression"}
 
 
 def register(name, trainer, supervised=True, defaults=None, **kw):

@@ -1,8 +1,15 @@
 """Isotonic regression (reference: ``hex/isotonic/IsotonicRegression.java``, ``PoolAdjacentViolators``).
 
-Weighted pool-adjacent-violators on the rows sorted by the single predictor (device sort, host
-PAVA over unique x — linear time), thresholds kept as (x, y) knots; scoring interpolates linearly
-between knots on device; ``out_of_bounds`` = NA (default) or clip.
+Weighted pool-adjacent-violators on the rows sorted by the single predictor, thresholds kept as (x, y)
+knots; scoring interpolates linearly between knots on device; ``out_of_bounds`` = NA (default) or clip.
+
+Row-sharded training follows the reference's two-stage driver
+(``hex/isotonic/PoolAdjacentViolatorsDriver.java`` runPAV: sort, PAV per chunk, PAV again over the chunk
+results) without moving rows to one place: each rank folds its rows to (x, sum w, sum w*y) per distinct x,
+exact order-statistic splitters cut the x axis into one contiguous range per rank, one all-to-all sends each
+distinct x to its range's owner, every rank pools its range (valid: a range is a contiguous run of the
+sorted axis), and a final PAV over the ranks' pooled blocks — the model-sized summary the reference also
+collects into one chunk — gives the same fit on every rank.
 """
 from __future__ import annotations
 
@@ -11,6 +18,8 @@ import time
 import numpy as np
 import torch
 
+from ..parallel import collectives as coll
+from ..parallel.order_stats import order_statistics
 from .base import DataInfo, Model, make_key
 
 
@@ -25,6 +34,40 @@ def pava(y, w):
             ww = w1 + w2
             vals.append((v1 * w1 + v2 * w2) / ww if ww > 0 else v1); wts.append(ww); counts.append(c1 + c2)
     return np.repeat(vals, counts)
+
+
+def pava_blocks(y, w, xlo, xhi):
+    """Weighted PAV over ordered blocks (value, weight, first x, last x): the pooled blocks, as arrays."""
+    v, ww, lo, hi = [], [], [], []
+    for yi, wi, a, b in zip(y, w, xlo, xhi):
+        v.append(yi); ww.append(wi); lo.append(a); hi.append(b)
+        while len(v) > 1 and v[-2] > v[-1]:
+            v2, w2, h2 = v.pop(), ww.pop(), hi.pop()
+            lo.pop()
+            s = ww[-1] + w2
+            v[-1] = (v[-1] * ww[-1] + v2 * w2) / s if s > 0 else v[-1]
+            ww[-1], hi[-1] = s, h2
+    return np.array(v), np.array(ww), np.array(lo), np.array(hi)
+
+
+def _fold(x, w, wy):
+    """Rows -> (sorted distinct x, sum w, sum w*y)."""
+    ux, inv = torch.unique(x, return_inverse=True)
+    return (ux, torch.zeros_like(ux).index_add_(0, inv, w), torch.zeros_like(ux).index_add_(0, inv, wy))
+
+
+def _owned_range(ux, sw, swy):
+    """Send each distinct x to the rank owning its range of the global x axis (splitters = exact order
+    statistics of the distinct-x entries, so ranges hold about equally many); returns this rank's entries."""
+    W = coll.world()
+    n = torch.tensor([float(ux.numel())], dtype=torch.float64)
+    M = int(coll.all_reduce_(n.to(coll.comm_device())).item())
+    targets = [k * M // W + 1 for k in range(1, W)]
+    spl = order_statistics(ux, targets) if M else []
+    spl = torch.tensor([s for s in spl], dtype=torch.float64, device=ux.device)
+    dest = torch.searchsorted(spl, ux.contiguous(), right=True) if len(spl) else torch.zeros_like(ux, dtype=torch.long)
+    got = coll.exchange_rows(torch.stack([ux, sw, swy], 1), dest)
+    return _fold(got[:, 0], got[:, 1], got[:, 2])
 
 
 class IsotonicModel(Model):
@@ -71,20 +114,36 @@ class IsotonicTrainer:
         w = torch.ones(N, dtype=torch.float64, device=x.device) if w is None else w.double()
         ok = ~torch.isnan(x) & ~torch.isnan(y) & (w > 0)
         x, yy, w = x[ok], y.double()[ok], w[ok]
-        ux, inv = torch.unique(x, return_inverse=True)
-        sw = torch.zeros_like(ux).index_add_(0, inv, w)
-        swy = torch.zeros_like(ux).index_add_(0, inv, w * yy)
-        yb = (swy / sw).cpu().numpy()
-        fit = pava(yb, sw.cpu().numpy())
+        ux, sw, swy = _fold(x, w, w * yy)
+        if coll.is_dist():
+            ux, sw, swy = _owned_range(ux, sw, swy)
         uxn = ux.cpu().numpy()
-        # keep only knots where the fitted step function changes (+ ends)
-        keep = np.ones(len(fit), dtype=bool)
-        if len(fit) > 2:
-            keep[1:-1] = ~((fit[1:-1] == fit[:-2]) & (fit[1:-1] == fit[2:]))
+        blk = np.stack(pava_blocks((swy / sw).cpu().numpy(), sw.cpu().numpy(), uxn, uxn), 1) \
+            if len(uxn) else np.zeros((0, 4))
+        if coll.is_dist():
+            # ranks own consecutive x ranges, so rank order is x order; the blocks are the compressed PAV
+            # summary (model-sized), the final pass pools across the range boundaries
+            blk = coll.all_gather_cat(torch.from_numpy(np.ascontiguousarray(blk)).to(coll.comm_device()),
+                                      bounded=True).cpu().numpy()
+            blk = np.stack(pava_blocks(blk[:, 0], blk[:, 1], blk[:, 2], blk[:, 3]), 1)
+        if not len(blk):
+            raise ValueError("isotonic regression needs at least one row with a non-NA x, y and weight > 0")
+        # knots where the fitted step function changes: the first and last x of each run of equal values
+        v, lo, hi = blk[:, 0], blk[:, 2], blk[:, 3]
+        start = np.r_[True, v[1:] != v[:-1]]
+        end = np.r_[v[1:] != v[:-1], True]
+        kx, ky = [], []
+        for i in range(len(v)):
+            if start[i]:
+                kx.append(lo[i]); ky.append(v[i])
+            if end[i]:
+                j = i
+                if hi[j] != kx[-1]:
+                    kx.append(hi[j]); ky.append(v[j])
         model = IsotonicModel(model_key or make_key("isotonic"), self.p, info)
         model.device = X.device
-        model.thresholds_x = uxn[keep].tolist()
-        model.thresholds_y = fit[keep].tolist()
+        model.thresholds_x = [float(a) for a in kx]
+        model.thresholds_y = [float(a) for a in ky]
         model.output["thresholds_x"] = model.thresholds_x
         model.output["thresholds_y"] = model.thresholds_y
         model.output["training_metrics"] = model.metrics_for(X, y, None)

@@ -213,6 +213,27 @@ def gather_rows(t):
     return all_gather_cat(t.contiguous(), 0)
 
 
+def exchange_rows(t: torch.Tensor, dest: torch.Tensor) -> torch.Tensor:
+    """Variable-size all-to-all of the rows of ``t`` ([n, ...]): row i goes to rank ``dest[i]``; returns the
+    rows this rank received, grouped by source rank (source order kept within a group). Each row moves
+    once — the partition step of a distributed sort, not a gather."""
+    if not is_dist():
+        return t
+    if _staged(t):
+        return exchange_rows(t.cpu(), dest.cpu()).to(t.device)
+    W = world()
+    order = torch.argsort(dest, stable=True)
+    ts = t[order].contiguous()
+    send = torch.bincount(dest.long(), minlength=W).to(torch.int64)
+    recv = torch.empty_like(send)
+    dist.all_to_all_single(recv, send)
+    sc, rc = send.tolist(), recv.tolist()
+    out = torch.empty((sum(rc),) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    _count(ts)
+    dist.all_to_all_single(out, ts, rc, sc)
+    return out
+
+
 def broadcast_(t: torch.Tensor, src: int = 0) -> torch.Tensor:
     if is_dist():
         _count(t)

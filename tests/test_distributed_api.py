@@ -2,8 +2,8 @@
 
 Every rank runs the same script (SPMD, as under torchrun): ``h2o.init()`` joins the process group,
 ``h2o.import_file`` parses its own byte range of the CSV (ParseDataset: domains unified over the
-ranks), and each trainer either all-reduces over the shards (GBM/DRF/XGB/GLM/KMeans/DL/NB/PCA) or
-trains replicated on gathered rows. The sharded run must produce the model and training metrics of
+ranks), and each trainer reduces over the shards (all-reduce / reduce-scatter / exact order statistics /
+an all-to-all range partition), never gathering rows in proportion to the frame. The sharded run must produce the model and training metrics of
 the single-process run (reference: ``water/MRTask.java`` reduce semantics — the cluster size never
 changes the answer).
 """
@@ -57,7 +57,8 @@ CASES = {
     "deeplearning": ("deeplearning", dict(hidden=[8, 8], epochs=2, seed=1, mini_batch_size=64, score_interval=1e9), "yb"),
     "deeplearning_reg": ("deeplearning", dict(hidden=[6], epochs=1, seed=2, mini_batch_size=50, activation="Tanh",
                                               adaptive_rate=False, rate=0.01, momentum_start=0.5, score_interval=1e9), "yr"),
-    "coxph_gathered": ("isotonicregression", dict(), "yr"),     # a trainer without collectives (gathered rows)
+    "isotonic": ("isotonicregression", dict(), "yr"),
+    "isotonic_weighted": ("isotonicregression", dict(weights_column="w", out_of_bounds="clip"), "yr"),
     "svd_gram": ("svd", dict(nv=3, transform="STANDARDIZE"), None),
     "svd_randomized": ("svd", dict(nv=2, svd_method="Randomized", transform="DEMEAN", seed=3), None),
     "pca_randomized": ("pca", dict(k=2, transform="STANDARDIZE", pca_method="Randomized", seed=3), None),
