@@ -42,7 +42,8 @@ class AlgoSpec:
 # program on the same data) — correct everywhere, scaled only where the collectives exist.
 DISTRIBUTED = {"gbm", "drf", "xgboost", "glm", "kmeans", "deeplearning", "naivebayes", "pca", "quantile",
                "isolationforest", "extendedisolationforest", "svd", "targetencoder", "gam", "anovaglm",
-               "modelselection", "upliftdrf", "dt", "glrm", "rulefit", "word2vec", "isotonicregression"}
+               "modelselection", "upliftdrf", "dt", "glrm", "rulefit", "word2vec", "isotonicregression",
+               "coxph"}
 
 
 def register(name, trainer, supervised=True, defaults=None, **kw):

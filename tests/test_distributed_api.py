@@ -57,6 +57,9 @@ CASES = {
     "deeplearning": ("deeplearning", dict(hidden=[8, 8], epochs=2, seed=1, mini_batch_size=64, score_interval=1e9), "yb"),
     "deeplearning_reg": ("deeplearning", dict(hidden=[6], epochs=1, seed=2, mini_batch_size=50, activation="Tanh",
                                               adaptive_rate=False, rate=0.01, momentum_start=0.5, score_interval=1e9), "yr"),
+    "coxph": ("coxph", dict(stop_column="x3"), "yb"),
+    "coxph_strata_breslow": ("coxph", dict(stop_column="x3", stratify_by=["cat"], ties="breslow", weights_column="w"),
+                             "yb"),
     "isotonic": ("isotonicregression", dict(), "yr"),
     "isotonic_weighted": ("isotonicregression", dict(weights_column="w", out_of_bounds="clip"), "yr"),
     "svd_gram": ("svd", dict(nv=3, transform="STANDARDIZE"), None),
@@ -84,7 +87,8 @@ CASES = {
                                           weights_column="w"), "yr"),
 }
 
-METRIC_KEYS = ("AUC", "logloss", "MSE", "RMSE", "mae", "mean_per_class_error", "tot_withinss", "r2", "AUUC", "qini")
+METRIC_KEYS = ("AUC", "logloss", "MSE", "RMSE", "mae", "mean_per_class_error", "tot_withinss", "r2", "AUUC", "qini",
+               "concordance", "loglik")
 
 
 def _run_cases(csv, names, out_path):
