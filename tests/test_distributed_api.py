@@ -60,6 +60,7 @@ CASES = {
     "coxph": ("coxph", dict(stop_column="x3"), "yb"),
     "coxph_strata_breslow": ("coxph", dict(stop_column="x3", stratify_by=["cat"], ties="breslow", weights_column="w"),
                              "yb"),
+    "aggregator": ("aggregator", dict(target_num_exemplars=60, rel_tol_num_exemplars=0.3, save_mapping_frame=True), None),
     "isotonic": ("isotonicregression", dict(), "yr"),
     "isotonic_weighted": ("isotonicregression", dict(weights_column="w", out_of_bounds="clip"), "yr"),
     "svd_gram": ("svd", dict(nv=3, transform="STANDARDIZE"), None),
@@ -107,7 +108,7 @@ def _run_cases(csv, names, out_path):
     for name in names:
         algo, params, y = CASES[name]
         x = ["x0", "x1", "x2", "x3", "cat"] if algo != "isotonicregression" else ["x0"]
-        if algo in ("kmeans", "pca", "svd", "quantile", "extendedisolationforest", "anovaglm", "modelselection", "glrm"):
+        if algo in ("aggregator", "kmeans", "pca", "svd", "quantile", "extendedisolationforest", "anovaglm", "modelselection", "glrm"):
             x = ["x0", "x1", "x2", "x3"]
         if algo == "dt":
             x = ["x0", "x1", "x3"]
@@ -124,6 +125,13 @@ def _run_cases(csv, names, out_path):
             q = m.output["quantiles"]
             res[name] = dict(pred=[q[c] for c in sorted(q)], metrics={}, cv={})
             continue
+        if algo == "aggregator":
+            agg = m.aggregated_frame().as_data_frame()
+            mp = h2o.get_frame(m.output["mapping_frame"]).as_data_frame()
+            res.setdefault("shapes", {})[name] = [list(agg.shape), list(mp.shape)]
+            res[name] = dict(pred=agg.select_dtypes(include=[np.number]).to_numpy(np.float64).ravel().tolist()
+                             + mp.to_numpy(np.float64).ravel().tolist(), metrics={}, cv={})
+            continue
         P = m.predict(fr).as_data_frame()
         num = P.select_dtypes(include=[np.number]).to_numpy(dtype=np.float64)
         tm = m.output.get("training_metrics") or {}
@@ -138,7 +146,8 @@ def _run_cases(csv, names, out_path):
 
 def _worker(rank, world, port, csv, names, out_path):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank), H2O_AMD_DEVICE="cpu", OMP_NUM_THREADS="1")
+                      LOCAL_RANK=str(rank), H2O_AMD_DEVICE="cpu", OMP_NUM_THREADS="1",
+                      H2O_AGG_CHUNK="250")   # aggregator chunks straddle the shard boundaries
     _run_cases(csv, names, out_path)
     import torch.distributed as dist
     if dist.is_initialized():
