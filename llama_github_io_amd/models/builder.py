@@ -43,7 +43,7 @@ class AlgoSpec:
 DISTRIBUTED = {"gbm", "drf", "xgboost", "glm", "kmeans", "deeplearning", "naivebayes", "pca", "quantile",
                "isolationforest", "extendedisolationforest", "svd", "targetencoder", "gam", "anovaglm",
                "modelselection", "upliftdrf", "dt", "glrm", "rulefit", "word2vec", "isotonicregression",
-               "coxph", "aggregator"}
+               "coxph", "aggregator", "psvm"}
 
 
 def register(name, trainer, supervised=True, defaults=None, **kw):

@@ -61,6 +61,7 @@ CASES = {
     "coxph_strata_breslow": ("coxph", dict(stop_column="x3", stratify_by=["cat"], ties="breslow", weights_column="w"),
                              "yb"),
     "aggregator": ("aggregator", dict(target_num_exemplars=60, rel_tol_num_exemplars=0.3, save_mapping_frame=True), None),
+    "psvm": ("psvm", dict(gamma=0.3, hyper_param=0.5), "yb"),
     "isotonic": ("isotonicregression", dict(), "yr"),
     "isotonic_weighted": ("isotonicregression", dict(weights_column="w", out_of_bounds="clip"), "yr"),
     "svd_gram": ("svd", dict(nv=3, transform="STANDARDIZE"), None),
@@ -108,7 +109,7 @@ def _run_cases(csv, names, out_path):
     for name in names:
         algo, params, y = CASES[name]
         x = ["x0", "x1", "x2", "x3", "cat"] if algo != "isotonicregression" else ["x0"]
-        if algo in ("aggregator", "kmeans", "pca", "svd", "quantile", "extendedisolationforest", "anovaglm", "modelselection", "glrm"):
+        if algo in ("psvm", "aggregator", "kmeans", "pca", "svd", "quantile", "extendedisolationforest", "anovaglm", "modelselection", "glrm"):
             x = ["x0", "x1", "x2", "x3"]
         if algo == "dt":
             x = ["x0", "x1", "x3"]
