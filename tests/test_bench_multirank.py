@@ -41,4 +41,5 @@ def test_bench_multirank_gloo_matches_single(world):
     many = _run(world)
     assert many["n_gpus"] == world and many["steps"] == 3 and many["config"]["global_batch"] == 6000
     assert many["config"]["collectives_per_tree"] > 0 and many["config"]["comm_bytes_per_tree"] > 0
-    assert abs(many["config"]["train_auc_after_all_trees"] - one["config"]["train_auc_after_all_trees"]) < 1e-6
+    # one process: exact AUC; sharded: AUC from the all-reduced 2^18-cell score lattice (mergeable metrics)
+    assert abs(many["config"]["train_auc_after_all_trees"] - one["config"]["train_auc_after_all_trees"]) < 5e-5
