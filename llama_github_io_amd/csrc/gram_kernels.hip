@@ -1,16 +1,20 @@
 // Weighted Gram matrix G = Zᵀ·diag(w)·Z on f32-input MFMA (GLM IRLSM GramTask, PCA GramSVD,
-// covariance for Aggregator/KMeans init).
+// covariance for Aggregator/KMeans init), optionally with one extra column u appended to Z (the
+// augmented Gram [Z u]ᵀ W [Z u] carries the IRLS right-hand side Zᵀ W u in its last column, so one pass
+// over Z replaces the Gram + Xᵀv pair of GLMIterationTask).
 //
 // Reference: h2o-algos/src/main/java/hex/gram/Gram.java (GramTask.map: per-row rank-1 updates in
 // fp64, reduced over chunks) and hex/glm/GLMTask.java (GLMIterationTask). MI355X design:
-//  * 256-thread workgroup (4 waves, 2x2) owns one 64x64 output tile (ti <= tj: only the upper
-//    triangle of tiles is computed, the host mirrors it) and one contiguous slice of rows.
-//  * Rows stream through LDS in 64-row stages (double-buffered via a register prefetch of the
-//    next stage): As[r][i] = w[r]·Z[r][i0+i], Bs[r][j] = Z[r][j0+j].
-//  * Each wave issues v_mfma_f32_32x32x2_f32 (exact f32 products, k-ordered fma chain) over the
-//    stage: lane l feeds A[i = l&31][k = l>>5] and B[k = l>>5][j = l&31], i.e. two rows per MFMA.
-//  * Every row slice writes its own fp32 slab; the slabs are summed in fp64 on the host stream
-//    (deterministic, no float atomics; keeps fp32 accumulation runs short: rows/slice ≈ N/S).
+//  * one wave per (64x64 tile pair ti <= tj, row slice): no LDS, no barriers. v_mfma_f32_32x32x2_f32
+//    takes A[i = l&31][k = l>>5] and B[k = l>>5][j = l&31], i.e. lane l loads column (l&31) of row
+//    2kk + (l>>5): one coalesced 128-byte read per half wave per 32 columns, straight into the MFMA
+//    operand registers. A diagonal tile is 3 MFMAs per row pair (the lower-left 32x32 block is the
+//    transpose of the upper-right one), an off-diagonal tile 4.
+//  * UNRG row pairs are loaded before their MFMAs (UNRG x 2-4 loads in flight per lane); many waves
+//    per SIMD (no LDS limit on occupancy) hide the HBM latency that the LDS-staged version (4 waves
+//    per 64 KiB of LDS, 2 blocks per CU) exposed: 10M x 51 took ~3 ms, 6x its MFMA bound.
+//  * every wave writes its own fp32 slab; the slabs are summed in fp64 on the stream (deterministic,
+//    no float atomics; fp32 runs stay short: rows per slice ~ N / S).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -19,90 +23,66 @@ namespace {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int TILE = 64;
-constexpr int BK = 64;       // rows per LDS stage
-constexpr int THREADS = 256;
+constexpr int UNRG = 8;      // row pairs in flight per lane
 
-__global__ __launch_bounds__(THREADS) void k_gram(const float* __restrict__ Z, int64_t ldz, const float* __restrict__ w,
-                                                  int64_t N, int P, int nT, int64_t rows_per_split,
-                                                  float* __restrict__ slabs, int Ppad) {
-  // tile pair from blockIdx.x over the upper triangle
+__device__ __forceinline__ float zload(const float* __restrict__ Z, int64_t ldz, const float* __restrict__ u,
+                                       int64_t r, bool ok, int c, int P) {
+  if (!ok) return 0.f;
+  if (c < P) return Z[r * ldz + c];
+  return (u != nullptr && c == P) ? u[r] : 0.f;
+}
+
+__global__ __launch_bounds__(64) void k_gram(const float* __restrict__ Z, int64_t ldz, const float* __restrict__ w,
+                                             const float* __restrict__ u, int64_t N, int P, int nT,
+                                             int64_t rows_per_split, float* __restrict__ slabs, int Ppad) {
   int pair = blockIdx.x;
   int ti = 0;
   while (pair >= nT - ti) { pair -= nT - ti; ++ti; }
   const int tj = ti + pair;
   const int i0 = ti * TILE, j0 = tj * TILE;
-  const int split = blockIdx.y;
-  const int64_t r_begin = (int64_t)split * rows_per_split;
-  int64_t r_end = r_begin + rows_per_split;
-  if (r_end > N) r_end = N;
-
-  __shared__ float As[2][BK][TILE];
-  __shared__ float Bs[2][BK][TILE];
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int wy = wave >> 1, wx = wave & 1;
-  const int col = tid & 63;        // load column within the tile
-  const int rsub = tid >> 6;       // 0..3: row phase for loads
-  const bool diag = (ti == tj);
-
-  f32x16 acc;
-  for (int k = 0; k < 16; ++k) acc[k] = 0.f;
-
-  float ra[BK / 4], rb[BK / 4];
-  auto load_stage = [&](int64_t r0) {
+  const bool diag = ti == tj;
+  const int64_t r_begin = (int64_t)blockIdx.y * rows_per_split;
+  const int64_t r_end = min(N, r_begin + rows_per_split);
+  const int lane = threadIdx.x;
+  const int c = lane & 31, kh = lane >> 5;
+  f32x16 a00, a01, a10, a11;
 #pragma unroll
-    for (int m = 0; m < BK / 4; ++m) {
-      const int64_t r = r0 + rsub + 4 * m;
-      float a = 0.f, b = 0.f;
-      if (r < r_end) {
-        const float ww = w ? w[r] : 1.f;
-        const float* zr = Z + r * ldz;
-        const float zi = (i0 + col < P) ? zr[i0 + col] : 0.f;
-        a = ww * zi;
-        b = diag ? zi : ((j0 + col < P) ? zr[j0 + col] : 0.f);
+  for (int k = 0; k < 16; ++k) { a00[k] = 0.f; a01[k] = 0.f; a10[k] = 0.f; a11[k] = 0.f; }
+  for (int64_t base = r_begin; base < r_end; base += 2 * UNRG) {
+    float x0[UNRG], x1[UNRG], y0[UNRG], y1[UNRG], ww[UNRG];
+#pragma unroll
+    for (int q = 0; q < UNRG; ++q) {
+      const int64_t r = base + 2 * q + kh;
+      const bool ok = r < r_end;
+      const int64_t rc = ok ? r : r_begin;
+      ww[q] = ok ? (w ? w[rc] : 1.f) : 0.f;
+      x0[q] = zload(Z, ldz, u, rc, ok, i0 + c, P);
+      x1[q] = zload(Z, ldz, u, rc, ok, i0 + 32 + c, P);
+      if (!diag) {
+        y0[q] = zload(Z, ldz, u, rc, ok, j0 + c, P);
+        y1[q] = zload(Z, ldz, u, rc, ok, j0 + 32 + c, P);
       }
-      ra[m] = a; rb[m] = b;
     }
-  };
-  auto store_stage = [&](int buf) {
 #pragma unroll
-    for (int m = 0; m < BK / 4; ++m) {
-      As[buf][rsub + 4 * m][col] = ra[m];
-      Bs[buf][rsub + 4 * m][col] = rb[m];
+    for (int q = 0; q < UNRG; ++q) {
+      const float b0 = diag ? x0[q] : y0[q], b1 = diag ? x1[q] : y1[q];
+      const float wa0 = ww[q] * x0[q], wa1 = ww[q] * x1[q];
+      a00 = __builtin_amdgcn_mfma_f32_32x32x2f32(wa0, b0, a00, 0, 0, 0);
+      a01 = __builtin_amdgcn_mfma_f32_32x32x2f32(wa0, b1, a01, 0, 0, 0);
+      a11 = __builtin_amdgcn_mfma_f32_32x32x2f32(wa1, b1, a11, 0, 0, 0);
+      if (!diag) a10 = __builtin_amdgcn_mfma_f32_32x32x2f32(wa1, b0, a10, 0, 0, 0);
     }
-  };
-
-  int buf = 0;
-  if (r_begin < r_end) {
-    load_stage(r_begin);
-    store_stage(0);
   }
-  __syncthreads();
-  for (int64_t r0 = r_begin; r0 < r_end; r0 += BK) {
-    const bool more = r0 + BK < r_end;
-    if (more) load_stage(r0 + BK);  // global loads in flight while the MFMAs run
-    const int ai = 32 * wy + (lane & 31);
-    const int bj = 32 * wx + (lane & 31);
-    const int kh = lane >> 5;
-#pragma unroll 8
-    for (int kk = 0; kk < BK / 2; ++kk) {
-      const float a = As[buf][2 * kk + kh][ai];
-      const float b = Bs[buf][2 * kk + kh][bj];
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
-    }
-    if (more) store_stage(buf ^ 1);
-    __syncthreads();
-    buf ^= 1;
-  }
-  // epilogue: C/D map col = lane&31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5)
-  float* out = slabs + (size_t)split * Ppad * Ppad;
-  const int oc = j0 + 32 * wx + (lane & 31);
+  // epilogue: D[row = (k&3) + 8*(k>>2) + 4*(lane>>5)][col = lane&31] per 32x32 quadrant
+  float* out = slabs + (size_t)blockIdx.y * Ppad * Ppad;
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
-    const int orow = i0 + 32 * wy + (k & 3) + 8 * (k >> 2) + 4 * (lane >> 5);
-    out[(size_t)orow * Ppad + oc] = acc[k];
+    const int rr = (k & 3) + 8 * (k >> 2) + 4 * kh;
+    out[(size_t)(i0 + rr) * Ppad + j0 + c] = a00[k];
+    out[(size_t)(i0 + rr) * Ppad + j0 + 32 + c] = a01[k];
+    out[(size_t)(i0 + 32 + rr) * Ppad + j0 + 32 + c] = a11[k];
+    if (diag) out[(size_t)(i0 + 32 + c) * Ppad + j0 + rr] = a01[k];     // lower-left = upper-rightᵀ
+    else out[(size_t)(i0 + 32 + rr) * Ppad + j0 + c] = a10[k];
   }
 }
 
@@ -138,60 +118,74 @@ __global__ __launch_bounds__(256) void k_xtv(const float* __restrict__ Z, int64_
 }  // namespace
 
 // eta = Z @ B (+ off): Z [N, P] fp32 row-major, B [P, R] fp64 (R <= 8), eta [N, R] fp64 — the GLM linear
-// predictor without an fp64 copy of Z (GLMIterationTask's per-row x·beta). 256 rows per block; 32-column
-// tiles staged through LDS with coalesced loads (row stride padded to 33 floats: conflict-free column reads),
-// one row per thread, fp64 accumulation.
-#define ZB_ROWS 256
-#define ZB_COLS 32
-__global__ __launch_bounds__(ZB_ROWS) void k_zbeta(const float* __restrict__ Z, int64_t ldz, const double* __restrict__ B,
-                                                   int R, int64_t N, int P, const double* __restrict__ off,
-                                                   double* __restrict__ eta) {
-  __shared__ float tile[ZB_ROWS * (ZB_COLS + 1)];
-  __shared__ double bt[ZB_COLS * 8];
-  const int t = threadIdx.x;
-  const int64_t r0 = (int64_t)blockIdx.x * ZB_ROWS;
-  double acc[8];
+// predictor without an fp64 copy of Z (GLMIterationTask's per-row x·beta). A half wave owns a row: lane
+// l reads columns (l&31) + 32m of row 2q + (l>>5) (coalesced 128-byte reads, ZB_UNR row pairs in flight),
+// multiplies by its register copy of B, and a 32-lane butterfly of fp64 shuffles sums each row. The
+// previous LDS-tiled version (one row per thread) read 2 GB of a 10M x 50 Z at 1.45 TB/s.
+#define ZB_UNR 8
+template <int RT>   // RT = R (1: IRLS eta), 8: any R <= 8
+__global__ __launch_bounds__(256) void k_zbeta(const float* __restrict__ Z, int64_t ldz, const double* __restrict__ B,
+                                               int R, int64_t N, int P, const double* __restrict__ off,
+                                               double* __restrict__ eta) {
+  const int lane = threadIdx.x & 63, c = lane & 31, kh = lane >> 5;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int M = (P + 31) / 32;
+  const int RR = RT == 1 ? 1 : R;
+  for (int64_t base = wave * 2 * ZB_UNR; base < N; base += nwaves * 2 * ZB_UNR) {
+    double acc[ZB_UNR][RT];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) acc[k] = 0.0;
-  for (int c0 = 0; c0 < P; c0 += ZB_COLS) {
-    const int nc = min(ZB_COLS, P - c0);
-    for (int i = t; i < ZB_ROWS * ZB_COLS; i += ZB_ROWS) {
-      const int rr = i / ZB_COLS, cc = i - rr * ZB_COLS;
-      const int64_t row = r0 + rr;
-      tile[rr * (ZB_COLS + 1) + cc] = (row < N && cc < nc) ? Z[row * ldz + c0 + cc] : 0.f;
-    }
-    for (int i = t; i < ZB_COLS * R; i += ZB_ROWS) {
-      const int cc = i / R, k = i - cc * R;
-      bt[cc * 8 + k] = cc < nc ? B[(int64_t)(c0 + cc) * R + k] : 0.0;
-    }
-    __syncthreads();
-    for (int cc = 0; cc < nc; ++cc) {
-      const double z = (double)tile[t * (ZB_COLS + 1) + cc];
+    for (int q = 0; q < ZB_UNR; ++q)
 #pragma unroll
-      for (int k = 0; k < 8; ++k)
-        if (k < R) acc[k] += z * bt[cc * 8 + k];
-    }
-    __syncthreads();
-  }
-  const int64_t row = r0 + t;
-  if (row < N) {
-    const double o = off ? off[row] : 0.0;
+      for (int k = 0; k < RT; ++k) acc[q][k] = 0.0;
+    // two 32-column chunks per step: 2 * ZB_UNR independent loads in flight per lane
+    for (int m = 0; m < M; m += 2) {
+      float z0[ZB_UNR], z1[ZB_UNR];
+      const int c0 = 32 * m + c, c1 = c0 + 32;
+      const bool ok0 = c0 < P, ok1 = c1 < P;
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
-      if (k < R) eta[row * R + k] = acc[k] + o;
+      for (int q = 0; q < ZB_UNR; ++q) {
+        const int64_t r = base + 2 * q + kh;
+        const bool rok = r < N;
+        const float* zr = Z + (rok ? r : 0) * ldz;
+        z0[q] = (ok0 && rok) ? zr[c0] : 0.f;
+        z1[q] = (ok1 && rok) ? zr[c1] : 0.f;
+      }
+#pragma unroll
+      for (int k = 0; k < RT; ++k) {
+        if (k >= RR) break;
+        const double b0 = ok0 ? B[(int64_t)c0 * RR + k] : 0.0;
+        const double b1 = ok1 ? B[(int64_t)c1 * RR + k] : 0.0;
+#pragma unroll
+        for (int q = 0; q < ZB_UNR; ++q) acc[q][k] += (double)z0[q] * b0 + (double)z1[q] * b1;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < ZB_UNR; ++q) {
+      const int64_t r = base + 2 * q + kh;
+#pragma unroll
+      for (int k = 0; k < RT; ++k) {
+        if (k >= RR) break;
+        double v = acc[q][k];
+#pragma unroll
+        for (int sh = 16; sh >= 1; sh >>= 1) v += __shfl_xor(v, sh, 64);
+        if (c == 0 && r < N) eta[r * RR + k] = v + (off ? off[r] : 0.0);
+      }
+    }
   }
 }
 
 extern "C" {
 
 // slabs: fp32 [S, Ppad, Ppad], Ppad = ceil(P/64)*64 (caller zero-fills nothing: every upper tile is written)
-int h2o_gram(const float* Z, long long ldz, const float* w, long long N, int P, int S, float* slabs, int Ppad,
-             hipStream_t stream) {
-  if (P <= 0 || N < 0 || S <= 0 || Ppad % TILE != 0 || Ppad < P) return (int)hipErrorInvalidValue;
+// u (nullable): the extra column P of the augmented matrix (Ppad > P required then)
+int h2o_gram(const float* Z, long long ldz, const float* w, const float* u, long long N, int P, int S, float* slabs,
+             int Ppad, hipStream_t stream) {
+  if (P <= 0 || N < 0 || S <= 0 || Ppad % TILE != 0 || Ppad < P + (u ? 1 : 0)) return (int)hipErrorInvalidValue;
   const int nT = Ppad / TILE;
-  const long long rps = ((N + S - 1) / S + BK - 1) / BK * BK;
+  const long long rps = ((N + S - 1) / S + 1) / 2 * 2;
   dim3 grid(nT * (nT + 1) / 2, S);
-  hipLaunchKernelGGL(k_gram, grid, dim3(THREADS), 0, stream, Z, (int64_t)ldz, w, (int64_t)N, P, nT, (int64_t)rps,
+  hipLaunchKernelGGL(k_gram, grid, dim3(64), 0, stream, Z, (int64_t)ldz, w, u, (int64_t)N, P, nT, (int64_t)rps,
                      slabs, Ppad);
   return (int)hipGetLastError();
 }
@@ -208,9 +202,14 @@ int h2o_xtv(const float* Z, long long ldz, const float* v, int R, long long N, i
 int h2o_zbeta(const float* Z, long long ldz, const double* B, int R, long long N, int P, const double* off,
               double* eta, hipStream_t stream) {
   if (R < 1 || R > 8 || N <= 0) return N <= 0 ? 0 : (int)hipErrorInvalidValue;
-  const long long grid = (N + ZB_ROWS - 1) / ZB_ROWS;
-  hipLaunchKernelGGL(k_zbeta, dim3((unsigned)grid), dim3(ZB_ROWS), 0, stream, Z, (int64_t)ldz, B, R, (int64_t)N, P, off,
-                     eta);
+  long long grid = (N + 4 * 2 * ZB_UNR - 1) / (4 * 2 * ZB_UNR);     // 4 waves per block, 2*ZB_UNR rows per wave
+  if (grid > 8192) grid = 8192;
+  if (R == 1)
+    hipLaunchKernelGGL(k_zbeta<1>, dim3((unsigned)grid), dim3(256), 0, stream, Z, (int64_t)ldz, B, R, (int64_t)N, P,
+                       off, eta);
+  else
+    hipLaunchKernelGGL(k_zbeta<8>, dim3((unsigned)grid), dim3(256), 0, stream, Z, (int64_t)ldz, B, R, (int64_t)N, P,
+                       off, eta);
   return (int)hipGetLastError();
 }
 

@@ -136,6 +136,7 @@ __device__ void block_sum4(double v[4], double* scratch /* >= 4*(BLK/64) */) {
 // nayy (fp32 NA-bin wYY, rare) follows the planes.
 #define HPLANE (NBIN * FTILE + 16)
 #define HIST_LDS_BYTES (2 * HPLANE * 8 + FTILE * 4)
+#define HIST_LDS_TAIL (64 * 8 + TILE * 4 + 2 * (TILE / BLK) * (BLK / 64) * 4)   // red + FILT row list + counts
 __device__ __forceinline__ int fslot(int fl) { return (fl & 16) | ((fl + ((fl >> 4) << 1)) & 15); }
 
 __device__ __forceinline__ void lds_zero64(long long* h, int n) {
@@ -238,10 +239,54 @@ struct RowFilter {
   }
 };
 
-#define UNR 8   // hist: rows per lane group loaded before any atomic (8 independent loads per lane)
 
 // Histogram rows [r0, r1) of one node into LDS: lane group g (8 lanes, one 4-feature row word each)
 // takes rows g, g + RPI, ...; UNR rows per lane group are loaded before any atomic.
+// MEASURED: this loop is VALU-issue bound, not memory bound (prefetching / 4..16 rows in flight all ran
+// within 1.5 %), so everything per-lane is hoisted: the 4 feature slots and byte shifts of the lane's word
+// (rotated by row parity, see the layout note), feature validity, and an all-bytes NA test per word; the
+// common row is then bfe + lshl_add + ds_add_u64 per feature (two atomics when not PACKED).
+// FILT (odd levels): the rows of a parent tile that the parent's decision sends to the built child, as an
+// ascending row list in LDS (one lane per row tests the split byte; wave ballots + a (pass, wave) prefix
+// place them). The histogram loop then runs over full lane groups of selected rows: filtering inside it
+// left about half of each wave's lanes idle through the atomics (the loop is issue-bound), so a filtered
+// pass cost two plain passes. ftile-0 blocks also count the parent's left-goers (nl_out).
+__device__ __forceinline__ int filt_compact(const RowFilter& flt, int r0, int r1, int* lst, int* wcnt, int& lcnt) {
+  constexpr int NP = TILE / BLK;     // rows per thread (NW waves per block)
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  bool sel[NP];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int row = r0 + p * BLK + threadIdx.x;
+    bool sl = false;
+    if (row < r1) {
+      const bool gl = flt.left(flt.fptr[(size_t)row * (size_t)flt.fstride]);
+      if (flt.count) lcnt += gl ? 1 : 0;
+      sl = (gl ? 0 : 1) == flt.dir;
+    }
+    sel[p] = sl;
+    const unsigned long long m = __ballot(sl);
+    if (lane == 0) wcnt[p * NW + wv] = __popcll(m);
+  }
+  __syncthreads();
+  int S = 0;
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const unsigned long long m = __ballot(sel[p]);
+    int base = 0;
+    for (int k = 0; k < p * NW + wv; ++k) base += wcnt[k];
+    if (sel[p]) lst[base + __popcll(m & ((1ull << lane) - 1ull))] = r0 + p * BLK + threadIdx.x;
+  }
+  for (int k = 0; k < NP * NW; ++k) S += wcnt[k];
+  __syncthreads();
+  return S;
+}
+
+#define UNR 8   // hist: rows per lane group loaded before any atomic (8 independent loads per lane)
+
+// Histogram rows [r0, r1) of one node into LDS (FILT: entries [r0, r1) of the LDS row list): lane group g
+// (8 lanes, one 4-feature row word each) takes rows g, g + RPI, ...; UNR rows per lane group are loaded
+// before any atomic.
 // MEASURED: this loop is VALU-issue bound, not memory bound (prefetching / 4..16 rows in flight all ran
 // within 1.5 %), so everything per-lane is hoisted: the 4 feature slots and byte shifts of the lane's word
 // (rotated by row parity, see the layout note), feature validity, and an all-bytes NA test per word; the
@@ -250,8 +295,7 @@ template <bool FILT, bool PACKED>
 __device__ __forceinline__ void hist_rows(long long* h, float* nayy, const unsigned* __restrict__ bins32,
                                           const float* __restrict__ aw, const float* __restrict__ ay, int W, int wabs,
                                           int F, bool lead, int r0, int r1, int g, int j, float& wyy, float sa,
-                                          float sb, float sp, const RowFilter& flt, int& lcnt) {
-  const int lane = threadIdx.x & 63;
+                                          float sb, float sp, const int* lst) {
   const int rot = g & 1;
   int off[4], sh[4];
   unsigned vmask = 0u;
@@ -268,32 +312,20 @@ __device__ __forceinline__ void hist_rows(long long* h, float* nayy, const unsig
   for (int base = r0; base < r1; base += RPI * UNR) {
     unsigned wd[UNR];
     float2 ab[UNR];
-    int sbyte[UNR];
     // unconditional loads (rows clamped into the node, words into the row): no exec-mask branches here;
     // rows past r1 are skipped below, invalid words have vmask == 0
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
-      const size_t row = (size_t)min(base + g + u * RPI, r1 - 1);
+      const int idx = min(base + g + u * RPI, r1 - 1);
+      const size_t row = FILT ? (size_t)lst[idx] : (size_t)idx;
       // SoA aux planes: wY always, w only when rows are weighted (aw == null: unit weights)
       ab[u] = make_float2(aw ? aw[row] : 1.f, ay[row]);
       wd[u] = bins32[row * W + wc];
-      if (FILT && flt.jw < 0) sbyte[u] = flt.fptr[row * (size_t)flt.fstride];
-    }
-    if (FILT && flt.jw >= 0) {
-      // the split feature's byte is in lane jw's word of the same row group: one cross-lane read
-#pragma unroll
-      for (int u = 0; u < UNR; ++u)
-        sbyte[u] = (__shfl(wd[u], (lane & ~(LPR - 1)) + flt.jw, 64) >> (8 * (flt.feat & 3))) & 0xFF;
     }
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
-      const int row = base + g + u * RPI;
-      if (row >= r1) continue;
-      if (FILT) {
-        const bool gl = flt.left(sbyte[u]);
-        if (flt.count) lcnt += gl ? 1 : 0;
-        if ((gl ? 0 : 1) != flt.dir) continue;
-      }
+      const int idx = base + g + u * RPI;
+      if (idx >= r1) continue;
       if (lead) wyy += row_yy(ab[u].x, ab[u].y);
       if (vmask == 0u) continue;
       const long long qa = PACKED ? qpack(ab[u].x, ab[u].y, sp) : q64(ab[u].x, sa);
@@ -343,6 +375,8 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
   long long* h = smem64;                                 // 2 planes (PACKED: 1 -> two blocks per CU fit)
   float* nayy = (float*)(smem64 + (PACKED ? 1 : 2) * HPLANE);   // FTILE
   double* red = (double*)(nayy + FTILE);                 // 64 doubles scratch
+  int* lst = (int*)(red + 64);                           // FILT: the tile's selected rows (TILE)
+  int* wcnt = lst + TILE;                                // FILT: per (pass, wave) selected counts
 
   // tile_prefix here is the BUILD-tile prefix (only nodes with build=1 own tiles) and meta[2] the number
   // of build tiles: blocks split only the rows that are histogrammed (no idle blocks on skipped siblings)
@@ -406,13 +440,19 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
         flt.jw = (jw >= 0 && jw < LPR) ? jw : -1;
         flt.dir = nd.dir;
         flt.bin = spd.bin; flt.na_left = spd.na_left; flt.is_cat = spd.is_cat;
-        flt.count = ftile == 0 && j == 0;
+        flt.count = ftile == 0;
       }
     }
     since += r1 - r0;
     float wf = 0.f;
-    hist_rows<FILT, PACKED>(h, nayy, bins32, aw, ay, W, wabs, Fl, j == 0 && ftile == 0, r0, r1, g, j, wf, sa, sb,
-                            sp, flt, lcnt);
+    if (FILT) {
+      const int S = filt_compact(flt, r0, r1, lst, wcnt, lcnt);
+      hist_rows<FILT, PACKED>(h, nayy, bins32, aw, ay, W, wabs, Fl, j == 0 && ftile == 0, 0, S, g, j, wf, sa, sb,
+                              sp, lst);
+    } else {
+      hist_rows<FILT, PACKED>(h, nayy, bins32, aw, ay, W, wabs, Fl, j == 0 && ftile == 0, r0, r1, g, j, wf, sa, sb,
+                              sp, nullptr);
+    }
     wyy += (double)wf;
   }
   if (cur >= 0) flush();
@@ -694,18 +734,24 @@ __global__ __launch_bounds__(256) void k_split_find(
 }
 
 // k_split_reduce: best feature per node (with per-tree feature mask and per-node column sampling).
+// fgroup (nullable): engine column -> original feature. A numeric feature binned wider than one byte holds
+// several adjacent engine columns (interleaved edge subsets, see ops/binning.py); column sampling draws
+// ORIGINAL features (key and rank of a column = its feature's), so such a feature is in or out as a whole.
 __global__ __launch_bounds__(64) void k_split_reduce(
     const Cand* __restrict__ cand, const int* __restrict__ meta, int F,
     const int* __restrict__ feat_ok /*[F] per-tree mask, 1 = usable*/, int k_cols,
     unsigned long long seed, int level, Dec* __restrict__ dec,
-    const unsigned char* __restrict__ node_ok /*[nodes][F] interaction-constraint mask or null*/) {
+    const unsigned char* __restrict__ node_ok /*[nodes][F] interaction-constraint mask or null*/,
+    const int* __restrict__ fgroup) {
   const int node = blockIdx.x, lane = threadIdx.x;
   if (node >= meta[0]) return;
   const unsigned char* nok = node_ok ? node_ok + (size_t)node * F : nullptr;
   auto usable = [&](int f) { return feat_ok[f] != 0 && (!nok || nok[f] != 0); };
+  auto gid = [&](int f) { return fgroup ? fgroup[f] : f; };
+  auto leader = [&](int f) { return !fgroup || f == 0 || fgroup[f] != fgroup[f - 1]; };
   const unsigned long long base = splitmix64(seed ^ ((unsigned long long)(level + 1) << 40) ^ (unsigned long long)node);
   int n_ok = 0;
-  for (int f = lane; f < F; f += 64) n_ok += usable(f) ? 1 : 0;
+  for (int f = lane; f < F; f += 64) n_ok += (usable(f) && leader(f)) ? 1 : 0;
   n_ok = wave_sum_i(n_ok);
   const bool sample = k_cols > 0 && k_cols < n_ok;
   double be = -1.0e300;
@@ -713,12 +759,13 @@ __global__ __launch_bounds__(64) void k_split_reduce(
   for (int f = lane; f < F; f += 64) {
     if (!usable(f)) continue;
     if (sample) {
-      const unsigned long long kf = splitmix64(base + (unsigned long long)f);
+      const int gf = gid(f);
+      const unsigned long long kf = splitmix64(base + (unsigned long long)gf);
       int rank = 0;
       for (int g2 = 0; g2 < F; ++g2) {
-        if (!usable(g2)) continue;
-        const unsigned long long kg = splitmix64(base + (unsigned long long)g2);
-        rank += (kg < kf || (kg == kf && g2 < f)) ? 1 : 0;
+        if (!usable(g2) || !leader(g2)) continue;
+        const unsigned long long kg = splitmix64(base + (unsigned long long)gid(g2));
+        rank += (kg < kf || (kg == kf && gid(g2) < gf)) ? 1 : 0;
       }
       if (rank >= k_cols) continue;
     }
@@ -1305,30 +1352,63 @@ __global__ void k_leafsum_finish(unsigned long long* __restrict__ leafq, const d
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_bin_assign: X (column-major fp32 [F][N]) -> row-major uint8 bins [N][stride].
+// k_bin_assign: X (column-major fp32 [F][N]) -> uint8 bins, row-major [N][stride] or planar [stride/32][N][32].
 // Numeric: bin = #edges <= x (edges sorted, per feature `nedges` of them at edges + f*max_edges);
-// categorical (iscat): bin = code (< nb) else NA. NaN -> NA_BIN.
-__global__ void k_bin_assign(const float* __restrict__ X, long long N, int F, int stride,
-                             const float* __restrict__ edges, int max_edges, const int* __restrict__ nedges,
-                             const int* __restrict__ iscat, uint8_t* __restrict__ bins, int planar) {
-  const long long row = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (row >= N) return;
-  for (int f = 0; f < stride; ++f) {
-    uint8_t* outf = bins + bin_off(row, f, stride, N, planar);
-    if (f >= F) { *outf = 0; continue; }
-    const float x = X[(long long)f * N + row];
-    int b;
-    if (x != x) b = NA_BIN;
-    else if (iscat[f]) {
-      const int code = (int)x;
-      b = (code >= 0 && code <= nedges[f]) ? code : NA_BIN;
-    } else {
-      const float* e = edges + (size_t)f * max_edges;
-      int lo = 0, hi = nedges[f];
-      while (lo < hi) { const int mid = (lo + hi) >> 1; if (e[mid] <= x) lo = mid + 1; else hi = mid; }
-      b = lo;
+// categorical (iscat): bin = code (<= nedges) else NA. NaN -> NA_BIN.
+// blockIdx.y = a group of 32 features whose edge tables are staged in LDS (binary searches stay on chip);
+// a thread bins one row's 32 features into 8 packed dwords and writes them with 16-byte / dword stores
+// (one byte store per feature was the bottleneck: 5e9 bins of a 100M x 50 frame took 99 ms).
+__global__ __launch_bounds__(256) void k_bin_assign(const float* __restrict__ X, long long N, int F, int stride,
+                                                    const float* __restrict__ edges, int max_edges,
+                                                    const int* __restrict__ nedges, const int* __restrict__ iscat,
+                                                    uint8_t* __restrict__ bins, int planar,
+                                                    const int* __restrict__ xmap /*engine col -> X row, null = id*/) {
+  extern __shared__ float se[];                       // [32][max_edges]
+  __shared__ int sn[32], sc[32];
+  const int f0 = blockIdx.y * 32;
+  const int nf = min(32, stride - f0);                // multiple of 4 (stride is)
+  const int nr = max(0, min(32, F - f0));             // real features in the group
+  for (int i = threadIdx.x; i < nr * max_edges; i += blockDim.x)
+    se[i] = edges[(size_t)f0 * max_edges + i];
+  if (threadIdx.x < 32) {
+    sn[threadIdx.x] = threadIdx.x < nr ? nedges[f0 + threadIdx.x] : 0;
+    sc[threadIdx.x] = threadIdx.x < nr ? iscat[f0 + threadIdx.x] : 0;
+  }
+  __syncthreads();
+  for (long long row = (long long)blockIdx.x * blockDim.x + threadIdx.x; row < N;
+       row += (long long)gridDim.x * blockDim.x) {
+    uint32_t wd[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) wd[k] = 0u;
+#pragma unroll
+    for (int fl = 0; fl < 32; ++fl) {
+      if (fl < nr) {
+        const int xr = xmap ? xmap[f0 + fl] : f0 + fl;
+        const float x = X[(long long)xr * N + row];
+        int b;
+        if (x != x) b = NA_BIN;
+        else if (sc[fl]) {
+          const int code = (int)x;
+          b = (code >= 0 && code <= sn[fl]) ? code : NA_BIN;
+        } else {
+          const float* e = se + fl * max_edges;
+          int lo = 0, hi = sn[fl];
+          while (lo < hi) { const int mid = (lo + hi) >> 1; if (e[mid] <= x) lo = mid + 1; else hi = mid; }
+          b = lo;
+        }
+        wd[fl >> 2] |= (uint32_t)(b & 0xFF) << (8 * (fl & 3));
+      }
     }
-    *outf = (uint8_t)b;
+    if (planar) {
+      uint4* dst = reinterpret_cast<uint4*>(bins + ((long long)blockIdx.y * N + row) * 32);
+      dst[0] = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+      dst[1] = make_uint4(wd[4], wd[5], wd[6], wd[7]);
+    } else {
+      uint32_t* dst = reinterpret_cast<uint32_t*>(bins + row * stride + f0);
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (4 * k < nf) dst[k] = wd[k];
+    }
   }
 }
 
@@ -1477,7 +1557,7 @@ int h2o_abi_version() { return H2O_ABI_VERSION; }
 int h2o_tree_sizes(int* out) {
   out[7] = AMAX_SHARDS;
   out[0] = sizeof(Node); out[1] = sizeof(Dec); out[2] = sizeof(Cand); out[3] = TILE; out[4] = FTILE;
-  out[5] = HIST_LDS_BYTES + 64 * 8;  // k_hist_build LDS bytes
+  out[5] = HIST_LDS_BYTES + HIST_LDS_TAIL;  // k_hist_build LDS bytes
   out[6] = BLK;
   return 0;
 }
@@ -1489,7 +1569,7 @@ int h2o_hist_build(const void* bins, int stride, const void* aw, const void* ay,
                    hipStream_t s) {
   const int nft = (F + FTILE - 1) / FTILE;
   // packed mode needs one int64 plane (66 KB): two 16-wave blocks share a CU (32 waves, 8 per SIMD)
-  const size_t lds = (packed ? HIST_LDS_BYTES - HPLANE * 8 : HIST_LDS_BYTES) + 64 * 8;
+  const size_t lds = (packed ? HIST_LDS_BYTES - HPLANE * 8 : HIST_LDS_BYTES) + HIST_LDS_TAIL;
   const dim3 gr(grid, nft);
   if (packed) launch_hist<true>(gr, lds, s, bins, stride, aw, ay, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out, f32, N, planar);
   else launch_hist<false>(gr, lds, s, bins, stride, aw, ay, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out, f32, N, planar);
@@ -1536,9 +1616,11 @@ int h2o_split_find(const void* hist, int slot_doubles, const void* meta, int cap
 }
 
 int h2o_split_reduce(const void* cand, const void* meta, int cap, int F, const void* feat_ok, int k_cols,
-                     unsigned long long seed, int level, void* dec, const void* node_ok, hipStream_t s) {
+                     unsigned long long seed, int level, void* dec, const void* node_ok, const void* fgroup,
+                     hipStream_t s) {
   hipLaunchKernelGGL(k_split_reduce, dim3(cap), dim3(64), 0, s, (const Cand*)cand, (const int*)meta, F,
-                     (const int*)feat_ok, k_cols, seed, level, (Dec*)dec, (const unsigned char*)node_ok);
+                     (const int*)feat_ok, k_cols, seed, level, (Dec*)dec, (const unsigned char*)node_ok,
+                     (const int*)fgroup);
   return (int)hipGetLastError();
 }
 
@@ -1666,12 +1748,20 @@ int h2o_qscale(void* amax_bits, void* qs, void* counters, long long N, hipStream
 }
 
 int h2o_bin_assign(const void* X, long long N, int F, int stride, const void* edges, int max_edges,
-                   const void* nedges, const void* iscat, void* bins, int planar, hipStream_t s) {
+                   const void* nedges, const void* iscat, void* bins, int planar, const void* xmap,
+                   hipStream_t s) {
   if (planar && (stride % 32 != 0 || stride < 64)) return (int)hipErrorInvalidValue;
+  if (stride % 4 != 0 || max_edges < 1 || (size_t)32 * max_edges * sizeof(float) > 96 * 1024)
+    return (int)hipErrorInvalidValue;
   const int blk = 256;
-  const long long grid = (N + blk - 1) / blk;
-  hipLaunchKernelGGL(k_bin_assign, dim3((unsigned)grid), dim3(blk), 0, s, (const float*)X, N, F, stride,
-                     (const float*)edges, max_edges, (const int*)nedges, (const int*)iscat, (uint8_t*)bins, planar);
+  const int groups = (stride + 31) / 32;
+  long long grid = (N + blk - 1) / blk;
+  if (grid > 4096) grid = 4096;
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL(k_bin_assign, dim3((unsigned)grid, (unsigned)groups), dim3(blk),
+                     (size_t)32 * max_edges * sizeof(float), s, (const float*)X, N, F, stride,
+                     (const float*)edges, max_edges, (const int*)nedges, (const int*)iscat, (uint8_t*)bins, planar,
+                     (const int*)xmap);
   return (int)hipGetLastError();
 }
 
@@ -1726,6 +1816,7 @@ struct TreePlan {
   void *cand_local, *hrecv;
   double leaf_lam, leaf_l1;   // k_leaf_values regularisation (XGBoost leaves; 0 for GBM)
   int planar, pad_planar;     // bins layout of master and the ping-pong buffers (see bin_off)
+  void* fgroup;               // [F] engine column -> original feature (null: identity), k_split_reduce
 };
 
 static inline const float* tp_aux(const TreePlan* P, int c) { return (const float*)P->aux + (size_t)c * P->N; }
@@ -1789,7 +1880,7 @@ int h2o_tree_grow(const TreePlan* P, int d, int dist, hipStream_t s) {
   int rc;
   const int kc = P->kc_level[d] > 0 ? P->kc_level[d] : P->k_cols;
   rc = h2o_split_reduce(P->cand, P->meta[d], cap, P->F, P->feat_ok, kc, P->seed, d, P->dec[d],
-                        P->ic_map ? P->ic[d] : nullptr, s);
+                        P->ic_map ? P->ic[d] : nullptr, P->fgroup, s);
   if (rc) return -rc;
   rc = h2o_plan(P->nodes[d], P->meta[d], P->dec[d], P->nl[d], odd ? P->nl[d - 1] : nullptr, P->cur[d], P->cl[d],
                 P->cr[d], P->nodes[d + 1], P->tp[d + 1], P->meta[d + 1], P->bp[d + 1], P->counters, P->scratch, d,

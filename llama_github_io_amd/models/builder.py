@@ -37,13 +37,13 @@ class AlgoSpec:
 
 
 # Trainers that reduce their sufficient statistics over row-sharded tensors (histograms, Gram, centroid
-# sums, gradients, class counts): under a multi-rank cloud they train on the local shard. Every other
-# trainer gets the gathered rows and trains replicated (identical on every rank: the same deterministic
-# program on the same data) — correct everywhere, scaled only where the collectives exist.
+# sums, gradients, class counts, exact order statistics, all-to-all range partitions): under a multi-rank
+# cloud they train on the local shard. That is every trainer that reads rows; the rest (grep, generic)
+# get the gathered rows and run replicated (identical on every rank).
 DISTRIBUTED = {"gbm", "drf", "xgboost", "glm", "kmeans", "deeplearning", "naivebayes", "pca", "quantile",
                "isolationforest", "extendedisolationforest", "svd", "targetencoder", "gam", "anovaglm",
                "modelselection", "upliftdrf", "dt", "glrm", "rulefit", "word2vec", "isotonicregression",
-               "coxph", "aggregator", "psvm"}
+               "coxph", "aggregator", "psvm", "infogram", "stackedensemble"}
 
 
 def register(name, trainer, supervised=True, defaults=None, **kw):

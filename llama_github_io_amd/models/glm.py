@@ -722,8 +722,7 @@ class GLMTrainer:
                 var = fam.variance(mu)
                 wi = w / (var * gp * gp).clamp(min=1e-30)
                 zi = eta - off + (y - mu) * gp
-                Gm = G.gram(Zi, wi.float())
-                r = G.xtv(Zi, (wi * zi).float())
+                Gm, r = G.gram(Zi, wi.float(), zi.float())      # one pass: Zᵀ W Z and Zᵀ W z
                 if coll.is_dist():
                     Gm = coll.all_reduce_(Gm)
                     r = coll.all_reduce_(r)
@@ -922,8 +921,8 @@ class GLMTrainer:
                     wi = (w * pc * (1 - pc)).clamp(min=1e-10 * float(w.max()) if w.numel() else 0.0)
                     eta_c = G.zbeta(Zi, B[c])
                     zi = eta_c + (Y[:, c] - pc) / (pc * (1 - pc)).clamp(min=1e-10)
-                    Gm = _gvec(G.gram(Zi, wi.float())) * obj_reg
-                    r = _gvec(G.xtv(Zi, (wi * zi).float())) * obj_reg
+                    Gm, r = G.gram(Zi, wi.float(), zi.float())
+                    Gm, r = _gvec(Gm) * obj_reg, _gvec(r) * obj_reg
                     if not intercept:
                         Gm[-1, :] = 0
                         Gm[:, -1] = 0

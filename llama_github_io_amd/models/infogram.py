@@ -7,7 +7,8 @@ mean log₂ p̂(y|all \\ j) (EstimateCMI: per-row log probability of the observe
 [0, 1] by its maximum. Safe infogram (``protected_columns`` given): relevance from the model on
 non-protected features; CMI_j = log-likelihood gain of (protected ∪ {j}) over protected only.
 Admissible = relevance ≥ ``relevance_threshold`` and cmi ≥ ``cmi_threshold``. The per-feature
-models are GBMs on the device tree engine (``algorithm`` may pick GLM/DRF/DeepLearning).
+models are GBMs on the device tree engine (``algorithm`` may pick GLM/DRF/DeepLearning). On a row-sharded
+frame the per-feature models train sharded and the log-likelihood means are merged sums.
 """
 from __future__ import annotations
 
@@ -17,7 +18,14 @@ import time
 import numpy as np
 import torch
 
+from ..parallel import collectives as coll
 from .base import DataInfo, Model, make_key
+
+
+def _red(t: torch.Tensor) -> torch.Tensor:
+    if not coll.is_dist():
+        return t
+    return coll.all_reduce_(t.contiguous().to(coll.comm_device())).to(t.device)
 
 INFO_DEFAULTS = dict(algorithm="AUTO", algorithm_params=None, protected_columns=None, cmi_threshold=0.1,
                      relevance_threshold=0.1, total_information_threshold=-1.0, net_information_threshold=-1.0,
@@ -68,14 +76,18 @@ class InfogramTrainer:
         return m
 
     def _loglik(self, m, X, y, cols):
+        """Mean log2 likelihood of the observed responses (EstimateCMI); sums merged over the row shards."""
         P = m.score_tensor(X[cols].contiguous())
         if P.dim() == 1:                        # regression: Gaussian log-likelihood proxy
             r = (y - P).double()
-            s2 = float((r * r).mean()) + 1e-12
-            return float((-0.5 * r * r / s2 - 0.5 * math.log(2 * math.pi * s2)).mean()) / math.log(2)
+            st = _red(torch.stack([(r * r).sum(), torch.tensor(float(r.numel()), dtype=torch.float64,
+                                                               device=r.device)]))
+            s2 = float(st[0] / st[1]) + 1e-12
+            return (-0.5 * float(st[0]) / s2 / float(st[1]) - 0.5 * math.log(2 * math.pi * s2)) / math.log(2)
         py = P.double().gather(1, torch.nan_to_num(y).long()[:, None])[:, 0]
         ok = py > 0
-        return float(torch.log(py[ok]).mean()) / math.log(2)
+        st = _red(torch.stack([torch.log(py[ok]).sum(), ok.double().sum()]))
+        return float(st[0] / st[1]) / math.log(2)
 
     def fit(self, X, y, w, offset, info: DataInfo, valid=None, model_key=None):
         t0 = time.time()
@@ -85,8 +97,10 @@ class InfogramTrainer:
             raise ValueError("data_fraction must be in (0, 1]")
         if frac < 1.0:      # Infogram data_fraction: the CMI / relevance models see a random row sample
             from .shared_tree import resolve_seed
-            g = torch.Generator().manual_seed(resolve_seed(p.get("seed", -1)) & 0x7FFFFFFF)
-            keep = (torch.rand(X.shape[1], generator=g) < frac).to(X.device)
+            # a per-global-row draw: the same sample however the rows are sharded
+            start = coll.row_offset(X.shape[1])
+            keep = coll.row_uniform(resolve_seed(p.get("seed", -1)) & 0x7FFFFFFF, 23, start, X.shape[1],
+                                    X.device) < frac
             X, y = X[:, keep], y[keep]
             w = None if w is None else w[keep]
         prot = [c for c in (p["protected_columns"] or []) if c in info.x]

@@ -18,7 +18,7 @@ import torch
 
 from .. import metrics as mm
 from ..ops import tree as T
-from ..ops.binning import Binning, apply_binning, fit_binning, sample_rows
+from ..ops.binning import WIDE_MAX_BINS, Binning, apply_binning, fit_binning, sample_rows
 from ..ops.forest import Forest, Tree, levels_to_tree
 from ..parallel import collectives as coll
 from .base import DataInfo, Model, ScoreKeeper, make_key, model_category, variable_importance
@@ -201,8 +201,11 @@ class SharedTreeTrainer:
         self.X = X
         # ---- binning (QuantilesGlobal on the whole training set, shared by every tree)
         max_bins = int(min(255, max(int(p.get("max_bins") or 255), 2)))
-        if str(p.get("histogram_type", "AUTO")).lower() in ("uniformadaptive", "random", "roundrobin", "uniformrobust"):
-            max_bins = int(min(255, max(p.get("nbins_top_level", 1024), p.get("nbins", 20))))
+        ht_ = str(p.get("histogram_type", "AUTO")).lower().replace("_", "")
+        if ht_ in ("auto", "uniformadaptive", "random", "roundrobin", "uniformrobust") and "nbins_top_level" in p:
+            # DHistogram's root resolution: nbins_top_level (default 1024) bins; above 255 the numeric
+            # features are binned wide (several engine columns each, ops/binning.py)
+            max_bins = int(min(WIDE_MAX_BINS, max(int(p.get("nbins_top_level") or 1024), int(p.get("nbins") or 20))))
         bsample = self._binning_sample()
         if coll.is_dist():
             # every rank must bin identically, and exactly like the single-process run: the quantile
@@ -227,10 +230,16 @@ class SharedTreeTrainer:
                     mono[info.x.index(k)] = int(v)
         max_depth = int(p["max_depth"]) if int(p["max_depth"]) > 0 else 32
         node_cap = int(p.get("node_cap", 1 << 14))
-        self.builder = T.make_builder(bins, F, self.binning.nbins, self.binning.iscat, mono, max_depth,
+        bn = self.binning
+        self.builder = T.make_builder(bins, bn.F, bn.nbins, bn.iscat, bn.expand(mono), max_depth,
                                       self._split_params(), node_cap=node_cap)
+        if bn.vmap is not None:
+            self.builder.set_feature_groups(bn.vmap)
         if p.get("interaction_constraints"):
-            self.builder.set_interaction_constraints(*interaction_map(p["interaction_constraints"], info.x))
+            icm, root = interaction_map(p["interaction_constraints"], info.x)
+            if bn.vmap is not None:
+                icm, root = icm[np.ix_(bn.vmap, bn.vmap)], root[bn.vmap]
+            self.builder.set_interaction_constraints(icm, root)
         self.builder = self._wrap_builder(self.builder)
         model = self.model_cls(model_key or make_key(self.algo), p, info)
         model.binning = self.binning
@@ -264,7 +273,7 @@ class SharedTreeTrainer:
         ht = dict(prepare=0.0, build=0.0, update=0.0, drain=0.0, loop=0.0, build_max=0.0)
         for t in range(start, ntrees):
             tl0 = time.perf_counter()
-            feat_ok = self._tree_feature_mask(rng, F)
+            feat_ok = self.binning.expand(self._tree_feature_mask(rng, F))
             for k in range(K):
                 h0 = time.perf_counter()
                 aux = self._prepare(t, k)
@@ -366,10 +375,11 @@ class SharedTreeTrainer:
         del handles[:len(levels)]
         for (h, k), tl in zip(done, levels):
             forest.add_levels(tl, self.binning, k)     # flattened lazily (Forest.trees)
+            vm = self.binning.vmap
             for d in tl.decs:
                 fe = d["feat"]
                 m = fe >= 0
-                np.add.at(gains, fe[m], np.maximum(d["gain"][m], 0.0))
+                np.add.at(gains, fe[m] if vm is None else vm[fe[m]], np.maximum(d["gain"][m], 0.0))
 
     def _summary(self, forest: Forest, built):
         depths = [t.depth() for t in forest.trees] or [0]

@@ -128,7 +128,8 @@ class StackedEnsembleTrainer:
             L1 = torch.cat(cols_, 0).contiguous()
             y = blend.response_tensor(info, device=X.device)
             w = blend.weights_tensor(info, device=X.device)
-            return self._finish(models, L1, y, w, X, info, cat, valid, model_key, ytrain=(X, None, None, offset))
+            return self._finish(models, L1, y, w, X, info, cat, valid, model_key, ytrain=(X, None, None, offset),
+                                l1_sharded=getattr(blend, "_shard", None) is not None)
         holds = []
         for m in models:
             h = getattr(m, "cv_holdout", None)
@@ -144,12 +145,15 @@ class StackedEnsembleTrainer:
             else:
                 holds.append(h.reshape(-1, 1).float())
         L1 = torch.cat(holds, 1).T.contiguous().to(X.device)
-        return self._finish(models, L1, y, w, X, info, cat, valid, model_key, ytrain=(X, y, w, offset))
+        return self._finish(models, L1, y, w, X, info, cat, valid, model_key, ytrain=(X, y, w, offset),
+                            l1_sharded=coll.is_dist())
 
-    def _finish(self, models, L1, y, w, X, info, cat, valid, model_key, ytrain):
+    def _finish(self, models, L1, y, w, X, info, cat, valid, model_key, ytrain, l1_sharded=False):
         """Metalearner on the level-one frame L1 [F', N] with response y / weights w; the ensemble's
-        training metrics are scored on the training frame ``ytrain = (X, y, w, offset)``."""
-        from ..parallel import dframe
+        training metrics are scored on the training frame ``ytrain = (X, y, w, offset)``. On a row-sharded
+        cloud the level-one frame holds this rank's rows (the base models' holdouts are sharded the same
+        way) and the metalearner trains sharded."""
+        from ..parallel import collectives as coll, dframe
         transform = str(self.p.get("metalearner_transform") or "NONE").lower()
         if transform == "logit":
             if cat not in ("Binomial", "Multinomial"):
@@ -177,7 +181,7 @@ class StackedEnsembleTrainer:
         # buildMetalearner): with metalearner_nfolds it is cross-validated there, so the ensemble's
         # cross-validation metrics are out-of-fold twice over (base holdouts -> metalearner holdouts)
         from ..frame import Column, H2OFrame
-        with dframe.shard_ctx(None):
+        with dframe.shard_ctx(dframe.make_shard(L1.shape[1]) if l1_sharded else None):
             cols = [Column(n, "real", L1[i].double()) for i, n in enumerate(names)]
             if info.response_domain is not None:
                 yc = torch.nan_to_num(y.float(), nan=-1).to(torch.int32)
@@ -215,10 +219,11 @@ class StackedEnsembleTrainer:
         y, w = yt_, wt_
         model.output["stacking_strategy"] = "blending" if self.p.get("blending_frame") is not None else "cross_validation"
         nst = int(self.p.get("score_training_samples") or 0)
-        if 0 < nst < X.shape[1]:      # score_training_samples: training metrics on a fixed row sample
+        start, n_glob = coll.exclusive_offset(X.shape[1]) if coll.is_dist() else (0, X.shape[1])
+        if 0 < nst < n_glob:      # score_training_samples: training metrics on a row sample of about nst rows
             from .shared_tree import resolve_seed
-            g = torch.Generator().manual_seed(resolve_seed(self.p.get("seed", -1)) & 0x7FFFFFFF)
-            si = torch.randperm(X.shape[1], generator=g)[:nst].to(X.device)
+            u = coll.row_uniform(resolve_seed(self.p.get("seed", -1)) & 0x7FFFFFFF, 29, start, X.shape[1], X.device)
+            si = torch.nonzero(u < nst / n_glob).flatten()
             model.output["training_metrics"] = model.metrics_for(X[:, si], y[si], None if w is None else w[si],
                                                                  None if offset is None else offset[si])
         else:

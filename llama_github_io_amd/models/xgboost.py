@@ -150,9 +150,10 @@ class XGBoostTrainer(SharedTreeTrainer):
         # exact greedy splits are the histogram splits when no bin merges two distinct values: at most 254
         # distinct values per numeric column (bin 255 is NA) on this engine
         Xn = self.X
-        for f in range(b.F):
-            if b.iscat[f]:
+        for j in range(b.F):
+            if b.iscat[j]:
                 continue
+            f = b.orig(j)
             col = Xn[f][~torch.isnan(Xn[f])]
             nd = int(torch.unique(col).numel()) if col.numel() else 0
             if nd > 254:

@@ -5,6 +5,14 @@ Reference: ``hex/tree/GlobalQuantilesCalc.java`` (global quantile split points) 
 edges are exact sample values: ``bin(x) = #{edges <= x}``, so a split "bins < b go left" is the
 threshold rule ``x < edges[b-1]`` on raw values. Categorical columns use their level codes as bins
 (levels beyond 254 are folded by frequency into one shared bin). NaN -> NA bin 255.
+
+Wide numeric bins (``max_bins`` up to 1016, e.g. UniformAdaptive's ``nbins_top_level = 1024``,
+``SharedTreeModel.java:57``): a feature with more than 254 edges e is binned as n = ceil(|e| / 254) adjacent
+ENGINE columns, column k holding the byte bin of the edge subset e[k::n]. With fine bin t = #{e <= x} = 4h + l
+(n = 4), column k's bin is #{e[k::4] <= x} = h + [l > k], and its split "bin < h'" is exactly the fine split
+"t <= 4(h' - 1) + k": the n columns together offer every threshold of the fine edges, their histograms are
+exact, and the uint8 engine (histograms, routing, leaf walk) runs unchanged. ``vmap`` maps engine columns to
+the original features (split decoding, column sampling, constraints, importances).
 """
 from __future__ import annotations
 
@@ -16,6 +24,9 @@ import torch
 from . import _native as nat
 from .tree import MAX_DATA_BINS, NA_BIN
 
+SUB_EDGES = MAX_DATA_BINS - 1            # edges one engine column holds (254)
+WIDE_MAX_BINS = 4 * SUB_EDGES            # data bins of a wide numeric feature (1016 = 4 engine columns)
+
 
 @dataclass
 class Binning:
@@ -26,18 +37,37 @@ class Binning:
     iscat: np.ndarray               # int32 [F]
     nlevels: np.ndarray             # int32 [F] categorical cardinality (0 numeric)
     level_to_bin: list = field(default_factory=list)  # per feature: int array (None = identity)
+    vmap: np.ndarray | None = None  # int32 [F] engine column -> original feature (None: identity)
+
+    # every per-feature field above is per ENGINE column (F of them); see the module note on wide bins
+    @property
+    def F_orig(self) -> int:
+        return self.F if self.vmap is None else int(self.vmap.max()) + 1 if len(self.vmap) else 0
+
+    def orig(self, f: int) -> int:
+        return f if self.vmap is None else int(self.vmap[f])
+
+    def expand(self, a):
+        """Per-original-feature array -> per engine column (None passes through)."""
+        if a is None or self.vmap is None:
+            return a
+        if torch.is_tensor(a):
+            return a[torch.as_tensor(self.vmap, device=a.device, dtype=torch.long)].contiguous()
+        return np.asarray(a)[self.vmap]
 
     def to_state(self):
         return dict(F=self.F, stride=self.stride, edges=[None if e is None else e.tolist() for e in self.edges],
                     nbins=self.nbins.tolist(), iscat=self.iscat.tolist(), nlevels=self.nlevels.tolist(),
-                    level_to_bin=[None if m is None else m.tolist() for m in self.level_to_bin])
+                    level_to_bin=[None if m is None else m.tolist() for m in self.level_to_bin],
+                    vmap=None if self.vmap is None else self.vmap.tolist())
 
     @staticmethod
     def from_state(s):
         return Binning(s["F"], s["stride"], [None if e is None else np.asarray(e, dtype=np.float32) for e in s["edges"]],
                        np.asarray(s["nbins"], dtype=np.int32), np.asarray(s["iscat"], dtype=np.int32),
                        np.asarray(s["nlevels"], dtype=np.int32),
-                       [None if m is None else np.asarray(m, dtype=np.int64) for m in s["level_to_bin"]])
+                       [None if m is None else np.asarray(m, dtype=np.int64) for m in s["level_to_bin"]],
+                       None if s.get("vmap") is None else np.asarray(s["vmap"], dtype=np.int32))
 
 
 def sample_rows(X: torch.Tensor, sample: int, seed: int, row0: int = 0, n_glob: int | None = None) -> torch.Tensor:
@@ -76,10 +106,11 @@ def fit_binning(X: torch.Tensor, iscat, nlevels=None, max_bins: int = MAX_DATA_B
     then per-feature distinct / quantile gathers; only the <=255 edges per feature reach the host.
     ``max_cat_bins`` (nbins_cats, capped at 255): categoricals with more levels keep their most
     frequent ``max_cat_bins - 1`` levels as bins and fold the rest into one shared bin.
-    ``presampled``: X already is the (gathered) sample."""
+    ``presampled``: X already is the (gathered) sample. ``max_bins`` above 255 (at most 1016) bins numeric
+    features with more distinct values into several engine columns (module note)."""
     cat_cap = int(min(max(2, max_cat_bins), NA_BIN))
     F, N = X.shape
-    max_bins = int(min(max(2, max_bins), MAX_DATA_BINS))
+    max_bins = int(min(max(2, max_bins), WIDE_MAX_BINS))
     iscat = np.asarray(iscat, dtype=np.int32)
     nlevels = np.zeros(F, dtype=np.int32) if nlevels is None else np.asarray(nlevels, dtype=np.int32)
     Xs = X if presampled else sample_rows(X, sample, seed)
@@ -130,12 +161,28 @@ def fit_binning(X: torch.Tensor, iscat, nlevels=None, max_bins: int = MAX_DATA_B
         e = e.float().cpu().numpy()
         edges.append(e)
         nbins[f] = e.size + 1
+    vmap = None
+    if any(e is not None and e.size > SUB_EDGES for e in edges):
+        # wide features -> n adjacent engine columns with the interleaved edge subsets e[k::n]
+        cols = []
+        for f in range(F):
+            e = edges[f]
+            n = 1 if e is None or e.size <= SUB_EDGES else -(-e.size // SUB_EDGES)
+            for k in range(n):
+                ek = e if n == 1 else np.ascontiguousarray(e[k::n])
+                cols.append((f, ek, (ek.size + 1) if e is not None else nbins[f]))
+        vmap = np.asarray([c[0] for c in cols], dtype=np.int32)
+        edges = [c[1] for c in cols]
+        nbins = np.asarray([c[2] for c in cols], dtype=np.int32)
+        iscat, nlevels = iscat[vmap], nlevels[vmap]
+        l2b = [l2b[f] for f in vmap]
+        F = len(cols)
     # rows of more than 12 features are padded to 16 B multiples so the partition kernel moves them
     # with 16-byte vector loads/stores (2 per 28-feature row instead of 7 dword pairs)
     # > 32 features: whole 32-byte planes (the device engine stores such bins PLANAR, one plane per
     # histogram feature tile — apply_binning(planar=True))
     stride = (F + 3) // 4 * 4 if F <= 12 else ((F + 15) // 16 * 16 if F <= 32 else (F + 31) // 32 * 32)
-    return Binning(F, stride, edges, nbins, iscat, nlevels, l2b)
+    return Binning(F, stride, edges, nbins, iscat, nlevels, l2b, vmap)
 
 
 def _edge_table(b: Binning, device):
@@ -152,16 +199,17 @@ def _edge_table(b: Binning, device):
 
 
 def apply_binning(b: Binning, X: torch.Tensor, planar: bool = False) -> torch.Tensor:
-    """X float32 [F, N] -> uint8 bins [N, stride] (row-major) on X's device; with ``planar`` (device, stride a
-    multiple of 32 and >= 64) the [stride / 32, N, 32] plane layout of the tree engine."""
+    """X float32 [F, N] (original features) -> uint8 bins [N, stride] (row-major, one byte per ENGINE column) on
+    X's device; with ``planar`` (device, stride a multiple of 32 and >= 64) the [stride / 32, N, 32] plane
+    layout of the tree engine."""
     F, N = X.shape
-    assert F == b.F
+    assert F == b.F_orig
     Xc = X
     if any(m is not None for m in b.level_to_bin):
         Xc = X.clone()
         for f, m in enumerate(b.level_to_bin):
             if m is not None:
-                col = Xc[f]
+                col = Xc[b.orig(f)]
                 ok = ~torch.isnan(col)
                 mt = torch.as_tensor(m, device=X.device, dtype=torch.float32)
                 codes = col[ok].long().clamp(0, m.size - 1)
@@ -173,12 +221,14 @@ def apply_binning(b: Binning, X: torch.Tensor, planar: bool = False) -> torch.Te
         planar = bool(planar) and b.stride >= 64 and b.stride % 32 == 0
         out = (torch.empty(b.stride // 32, N, 32, dtype=torch.uint8, device=X.device) if planar
                else torch.empty(N, b.stride, dtype=torch.uint8, device=X.device))
-        nat.call("h2o_bin_assign", Xc.data_ptr(), N, F, b.stride, tab.data_ptr(), maxe, ned.data_ptr(),
-                 iscat.data_ptr(), out.data_ptr(), int(planar), nat.stream_ptr(X.device))
+        xmap = None if b.vmap is None else torch.as_tensor(b.vmap, dtype=torch.int32, device=X.device)
+        nat.call("h2o_bin_assign", Xc.data_ptr(), N, b.F, b.stride, tab.data_ptr(), maxe, ned.data_ptr(),
+                 iscat.data_ptr(), out.data_ptr(), int(planar), 0 if xmap is None else xmap.data_ptr(),
+                 nat.stream_ptr(X.device))
         return out
     out = torch.zeros(N, b.stride, dtype=torch.uint8)
-    for f in range(F):
-        col = Xc[f]
+    for f in range(b.F):
+        col = Xc[b.orig(f)]
         nan = torch.isnan(col)
         if b.iscat[f]:
             code = torch.nan_to_num(col, nan=-1).long()

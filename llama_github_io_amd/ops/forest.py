@@ -91,7 +91,8 @@ def levels_to_tree(tl: TreeLevels, binning, leaf_values=None) -> Tree:
             if f < 0:
                 value[g] = vals[-1 - cl] if cl < 0 and -1 - cl < nv else 0.0
                 continue
-            feat[g], bins[g], nal[g], iscat[g], gain[g] = f, bz[i], nz[i], cz[i], gz[i]
+            # engine column -> original feature (wide numeric features span several engine columns)
+            feat[g], bins[g], nal[g], iscat[g], gain[g] = binning.orig(f), bz[i], nz[i], cz[i], gz[i]
             if cz[i]:
                 nl = int(binning.nlevels[f])
                 bits_b = decs["bits"][i]

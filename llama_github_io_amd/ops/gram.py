@@ -10,7 +10,8 @@ import torch
 from . import _native as nat
 
 nat.register_hip_signatures({
-    "h2o_gram": [nat.c_void_p, nat.c_ll, nat.c_void_p, nat.c_ll, nat.c_int, nat.c_int, nat.c_void_p, nat.c_int, nat.c_void_p],
+    "h2o_gram": [nat.c_void_p, nat.c_ll, nat.c_void_p, nat.c_void_p, nat.c_ll, nat.c_int, nat.c_int, nat.c_void_p,
+                 nat.c_int, nat.c_void_p],
     "h2o_xtv": [nat.c_void_p, nat.c_ll, nat.c_void_p, nat.c_int, nat.c_ll, nat.c_int, nat.c_int, nat.c_void_p, nat.c_void_p],
     "h2o_zbeta": [nat.c_void_p, nat.c_ll, nat.c_void_p, nat.c_int, nat.c_ll, nat.c_int, nat.c_void_p, nat.c_void_p,
                   nat.c_void_p],
@@ -43,32 +44,37 @@ def zbeta(Z: torch.Tensor, B: torch.Tensor, off=None) -> torch.Tensor:
 
 
 def _splits(N: int, pairs: int) -> int:
-    target = max(1, 2048 // max(1, pairs))        # >= ~8 waves of workgroups per XCD on 256 CUs
-    return int(max(1, min(target, (N + 4095) // 4096)))
+    target = max(1, 4096 // max(1, pairs))        # one wave per (tile pair, slice): ~16 waves per CU
+    return int(max(1, min(target, (N + 1023) // 1024)))
 
 
-def gram(Z: torch.Tensor, w: torch.Tensor | None = None) -> torch.Tensor:
-    """Zᵀ diag(w) Z in float64. Z: [N, P] float32 row-major."""
+def gram(Z: torch.Tensor, w: torch.Tensor | None = None, u: torch.Tensor | None = None):
+    """Zᵀ diag(w) Z in float64. Z: [N, P] float32 row-major. With ``u`` ([N]) also Zᵀ diag(w) u from the
+    same pass over Z (the augmented Gram's last column): returns (G, r)."""
     N, P = Z.shape
     if not Z.is_cuda:
         Zd = Z.double()
-        return (Zd * (w.double()[:, None] if w is not None else 1.0)).T @ Zd
+        Zw = Zd * (w.double()[:, None] if w is not None else 1.0)
+        G = Zw.T @ Zd
+        return G if u is None else (G, Zw.T @ u.double())
     Z = Z.contiguous().float()
     wf = None if w is None else w.contiguous().float()
-    Ppad = (P + 63) // 64 * 64
+    uf = None if u is None else u.contiguous().float()
+    Pa = P + (1 if u is not None else 0)
+    Ppad = (Pa + 63) // 64 * 64
     nT = Ppad // 64
     pairs = nT * (nT + 1) // 2
     S = _splits(N, pairs)
     slabs = torch.zeros(S, Ppad, Ppad, dtype=torch.float32, device=Z.device)
     if N > 0:
-        nat.call("h2o_gram", Z.data_ptr(), P, 0 if wf is None else wf.data_ptr(), N, P, S, slabs.data_ptr(), Ppad,
-                 nat.stream_ptr(Z.device))
-    G = slabs.sum(0, dtype=torch.float64)[:P, :P]
+        nat.call("h2o_gram", Z.data_ptr(), P, 0 if wf is None else wf.data_ptr(), 0 if uf is None else uf.data_ptr(),
+                 N, P, S, slabs.data_ptr(), Ppad, nat.stream_ptr(Z.device))
+    G = slabs.sum(0, dtype=torch.float64)[:Pa, :Pa]
     # only tiles with ti <= tj were computed: mirror the strictly-lower tile blocks
     up = torch.triu(torch.ones(nT, nT, dtype=torch.bool, device=Z.device))
-    mask = up.repeat_interleave(64, 0).repeat_interleave(64, 1)[:P, :P]
+    mask = up.repeat_interleave(64, 0).repeat_interleave(64, 1)[:Pa, :Pa]
     G = torch.where(mask, G, G.T)
-    return G
+    return G if u is None else (G[:P, :P].contiguous(), G[:P, P].contiguous())
 
 
 def xtv(Z: torch.Tensor, v: torch.Tensor) -> torch.Tensor:

@@ -224,19 +224,24 @@ def split_find_ref(h, nayy, wyy, nbins_f, iscat_f, mono_f, p: SplitParams, level
     return out
 
 
-def split_reduce_ref(cands, feat_ok, k_cols, seed, level, node, node_ok=None):
+def split_reduce_ref(cands, feat_ok, k_cols, seed, level, node, node_ok=None, fgroup=None):
+    """k_split_reduce: best usable column; with ``fgroup`` (engine column -> original feature) the column
+    sample draws original features, whose adjacent engine columns share one key and rank."""
     F = len(cands)
+    gid = list(range(F)) if fgroup is None else [int(g) for g in fgroup]
+    lead = [f == 0 or gid[f] != gid[f - 1] for f in range(F)]
     base = splitmix64((seed ^ ((level + 1) << 40) ^ node) & _M64)
     ok = [bool(feat_ok[f]) and (node_ok is None or bool(node_ok[f])) for f in range(F)]
-    n_ok = sum(ok)
+    n_ok = sum(1 for f in range(F) if ok[f] and lead[f])
     sample = 0 < k_cols < n_ok
     allowed = ok[:]
     if sample:
-        keys = [splitmix64((base + f) & _M64) for f in range(F)]
+        keys = [splitmix64((base + gid[f]) & _M64) for f in range(F)]
         for f in range(F):
             if not ok[f]:
                 continue
-            rank = sum(1 for g in range(F) if ok[g] and (keys[g] < keys[f] or (keys[g] == keys[f] and g < f)))
+            rank = sum(1 for g in range(F) if ok[g] and lead[g] and
+                       (keys[g] < keys[f] or (keys[g] == keys[f] and gid[g] < gid[f])))
             allowed[f] = rank < k_cols
     be, bf = -1.0e300, -1
     for f in range(F):
@@ -294,6 +299,11 @@ class RefTreeBuilder:
         self.ic_map = np.asarray(ic_map, dtype=np.uint8)
         self.ic_root = np.asarray(root_ok, dtype=np.uint8)
 
+    def set_feature_groups(self, fgroup):
+        """Engine column -> original feature (wide numeric features span adjacent columns): column sampling
+        draws original features."""
+        self.fgroup = None if fgroup is None else np.asarray(fgroup, dtype=np.int64)
+
     def _hist(self, rows, aux):
         F = self.F
         h = np.zeros((F, 256, 2))
@@ -332,7 +342,8 @@ class RefTreeBuilder:
                     nayy = flat[h.size: h.size + F]
                     wyy = float(flat[-1])
                 cands = split_find_ref(h, nayy, wyy, self.nbins_f, self.iscat_f, self.mono_f, p, d, i, seed)
-                dl[i] = split_reduce_ref(cands, feat_ok, _level_k(k_cols, d), seed, d, i, level_ok[i])
+                dl[i] = split_reduce_ref(cands, feat_ok, _level_k(k_cols, d), seed, d, i, level_ok[i],
+                                         getattr(self, "fgroup", None))
             cl = np.zeros(n, dtype=np.int64); cr = np.zeros(n, dtype=np.int64)
             nxt, nxt_ok = [], []
             act = 0
@@ -408,7 +419,8 @@ class _TreePlan(ctypes.Structure):
                 [("edges", _vp), ("nb_level", _ci * _MAXL), ("pad3", _ci)] +
                 [("ic_map", _vp), ("ic", _vp * _MAXL)] +
                 [(n, _ci) for n in ("sliced", "fs0", "fsn", "sslot")] + [("cand_local", _vp), ("hrecv", _vp)] +
-                [("leaf_lam", _cd), ("leaf_l1", _cd)] + [("planar", _ci), ("pad_planar", _ci)])
+                [("leaf_lam", _cd), ("leaf_l1", _cd)] + [("planar", _ci), ("pad_planar", _ci)] +
+                [("fgroup", _vp)])
 
 
 class _Arena:
@@ -600,6 +612,13 @@ class GpuTreeBuilder:
         if getattr(self, "_plan", None) is not None:
             self._set_plan_ic(self._plan)
 
+    def set_feature_groups(self, fgroup):
+        """Engine column -> original feature (k_split_reduce column sampling by original feature)."""
+        self.fgroup = None if fgroup is None else torch.as_tensor(np.asarray(fgroup, dtype=np.int32),
+                                                                  device=self.dev).contiguous()
+        if getattr(self, "_plan", None) is not None:
+            self._plan.fgroup = 0 if self.fgroup is None else self.fgroup.data_ptr()
+
     def _set_plan_ic(self, P):
         if self.ic_map is None:
             P.ic_map = 0
@@ -635,6 +654,8 @@ class GpuTreeBuilder:
         for d in range(_MAXL):
             P.nb_level[d] = p.adapt_nb(d) if P.edges else 0
         self._set_plan_ic(P)
+        fg = getattr(self, "fgroup", None)
+        P.fgroup = 0 if fg is None else fg.data_ptr()
         P.sliced, P.fs0, P.fsn, P.sslot = int(self.sliced), self.fs0, self.fsn, self.sslot
         P.planar = int(self.planar)
         P.cand_local = self.cand_local.data_ptr() if self.sliced else 0

@@ -62,6 +62,8 @@ CASES = {
                              "yb"),
     "aggregator": ("aggregator", dict(target_num_exemplars=60, rel_tol_num_exemplars=0.3, save_mapping_frame=True), None),
     "psvm": ("psvm", dict(gamma=0.3, hyper_param=0.5), "yb"),
+    "infogram": ("infogram", dict(top_n_features=4, seed=3, algorithm_params=dict(ntrees=4, max_depth=3)), "yb"),
+    "stackedensemble": ("stackedensemble", dict(), "yb"),
     "isotonic": ("isotonicregression", dict(), "yr"),
     "isotonic_weighted": ("isotonicregression", dict(weights_column="w", out_of_bounds="clip"), "yr"),
     "svd_gram": ("svd", dict(nv=3, transform="STANDARDIZE"), None),
@@ -118,6 +120,11 @@ def _run_cases(csv, names, out_path):
         pp = dict(params)
         if name == "quantile_weighted_low":
             pp["weights_column"] = "w"
+        if algo == "stackedensemble":
+            base = [builder.train(a, dict(nfolds=3, fold_assignment="Modulo", keep_cross_validation_predictions=True,
+                                          seed=1, **kw), x=x, y=y, training_frame=fr, model_id=f"se_{a}")
+                    for a, kw in (("gbm", dict(ntrees=3, max_depth=3)), ("glm", dict(family="binomial")))]
+            pp["base_models"] = [b.key for b in base]
         import llama_github_io_amd.parallel.collectives as coll
         g0 = coll.stats()["row_gathers"]
         m = builder.train(algo, pp, x=x, y=y, training_frame=fr)
@@ -125,6 +132,9 @@ def _run_cases(csv, names, out_path):
         if algo == "quantile":
             q = m.output["quantiles"]
             res[name] = dict(pred=[q[c] for c in sorted(q)], metrics={}, cv={})
+            continue
+        if algo == "infogram":
+            res[name] = dict(pred=m.output["relevance"] + m.output["cmi_raw"], metrics={}, cv={})
             continue
         if algo == "aggregator":
             agg = m.aggregated_frame().as_data_frame()

@@ -26,6 +26,13 @@ def test_gram_matches_fp64(N, P):
     v = torch.randn(N, 3, device=dev, generator=g)
     assert torch.allclose(xtv(Z, v), Z.double().T @ v.double(), rtol=1e-4, atol=1e-3)
     assert torch.allclose(gram(Z), Z.double().T @ Z.double(), rtol=1e-4, atol=1e-2)
+    # augmented pass (GLM IRLS): Zᵀ W Z and Zᵀ W u from one read of Z
+    u = torch.randn(N, device=dev, generator=g)
+    G2, r = gram(Z, w, u)
+    assert torch.all((G2 - ref).abs() <= 1e-5 * scale + 1e-6)
+    rref = (Z.double() * w.double()[:, None]).T @ u.double()
+    rsc = (Z.double().abs() * w.double()[:, None]).T @ u.double().abs()
+    assert torch.all((r - rref).abs() <= 1e-5 * rsc + 1e-6)
 
 
 def test_kmeans_assign_matches_reference():

@@ -385,3 +385,87 @@ def test_gpu_tree_bins_matrix_above_2pow31_bytes():
         np.testing.assert_allclose(dr["wl"], dg["wl"], rtol=1e-9)
     np.testing.assert_allclose(tl_r.leaf_values, tl_g.leaf_values, rtol=1e-5, atol=1e-7)
     assert torch.equal(ref.leaf_of_row, gb.leaf_of_row.cpu())
+
+
+def test_wide_binning_columns_are_interleaved_edge_subsets():
+    """nbins_top_level = 1024 (SharedTreeModel.java:57): a numeric feature with more than 254 edges is binned
+    as adjacent engine columns over the edge subsets e[k::n]; every fine threshold is one column's split."""
+    g = torch.Generator().manual_seed(1)
+    X = torch.rand(3, 20000, generator=g)
+    X[1] = torch.randint(0, 40, (20000,), generator=g).float()        # few distinct values: one column
+    X[2, :100] = float("nan")
+    b = fit_binning(X, np.zeros(3, np.int32), None, max_bins=1016)
+    assert b.F_orig == 3 and list(b.vmap) == [0, 0, 0, 0, 1, 2, 2, 2, 2]
+    fine0 = fit_binning(X[:1], np.zeros(1, np.int32), None, max_bins=1016)
+    bins = apply_binning(b, X).long()
+    for j in range(b.F):
+        f = b.orig(j)
+        e = torch.from_numpy(b.edges[j])
+        ref = torch.bucketize(torch.nan_to_num(X[f], nan=0.0), e, right=True)
+        ref = torch.where(torch.isnan(X[f]), torch.full_like(ref, T.NA_BIN), ref)
+        assert torch.equal(bins[:, j], ref)
+    # feature 0: the 4 columns' thresholds are exactly the fine thresholds
+    ef = np.concatenate([b.edges[j] for j in range(4)])
+    assert np.array_equal(np.sort(ef), np.sort(np.concatenate([fine0.edges[j] for j in range(fine0.F)])))
+    fine = torch.bucketize(X[0], torch.from_numpy(np.sort(ef)), right=True)
+    for t in (1, 2, 3, 4, 5, 500, 1013):
+        k, h = (t - 1) % 4, (t - 1) // 4 + 1      # fine split t <=> column k split at bin h
+        assert torch.equal(bins[:, k] < h, fine < t)
+
+
+def test_wide_bins_split_resolution_and_grouped_sampling():
+    g = torch.Generator().manual_seed(2)
+    N = 40000
+    X = torch.rand(2, N, generator=g)
+    y = (X[0] > 0.50037).float()
+    info = DataInfo(["a", "b"], np.zeros(2, np.int32), [None, None], "y", None)
+    thr = {}
+    for top in (1024, 255):
+        m = GBMTrainer(dict(ntrees=1, max_depth=1, learn_rate=1.0, histogram_type="UniformAdaptive", min_rows=1,
+                            nbins_top_level=top, distribution="gaussian", seed=1)).fit(X, y, None, None, info)
+        t = m.forest.trees[0]
+        assert int(t.feat[0]) == 0
+        thr[top] = abs(float(t.thr[0]) - 0.50037)
+    assert thr[1024] < 1.5e-3 and thr[1024] <= thr[255]
+    # column sampling draws original features: a wide feature's columns are in or out together
+    fgroup = np.array([0, 0, 0, 0, 1, 2])
+    for seed in range(40):
+        allowed = []
+        for f in range(6):
+            c = [dict(valid=(i == f), expl=1.0, bin=1, na_left=0, is_cat=0, bits=np.zeros(8, np.uint32), gain=1.0,
+                      wl=1.0, wr=1.0, predl=0.0, predr=0.0) for i in range(6)]
+            allowed.append(T.split_reduce_ref(c, np.ones(6), 1, seed, 0, 0, None, fgroup)["feat"] == f)
+        assert sum(allowed) in (1, 4) and (sum(allowed) == 1) == (not allowed[0])
+        assert len(set(allowed[:4])) == 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["plain", "kcols_adaptive"])
+def test_gpu_wide_bins_match_reference(case):
+    """1016-bin numeric features (4 engine columns each) on the GPU engine vs RefTreeBuilder: identical
+    decisions, left weights and leaf assignment, including grouped column sampling (k_split_reduce fgroup)."""
+    X, y, info = _data(N=30000, cat=True, seed=11)
+    b = fit_binning(X, info.iscat, info.nlevels, max_bins=1016)
+    assert b.vmap is not None and b.F > X.shape[0]
+    bins = apply_binning(b, X)
+    g = y - y.mean()
+    aux = torch.stack([torch.ones_like(y), g, g, torch.ones_like(y)], 1).contiguous()
+    k_cols = 0
+    p = T.SplitParams(min_w=10)
+    if case == "kcols_adaptive":
+        k_cols = 3
+        p = T.SplitParams(min_w=10, adapt_nbins=20, adapt_top=1024, edges=_edge_tab(b))
+    ref = T.RefTreeBuilder(bins, b.F, b.nbins, b.iscat, None, 5, p)
+    ref.set_feature_groups(b.vmap)
+    ref.build(aux, None, k_cols, seed=5, leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1]).float())
+    tl_r = ref.pop_levels()[0]
+    dev = torch.device("cuda", 0)
+    gb = T.GpuTreeBuilder(apply_binning(b, X.to(dev), planar=b.stride >= 64), b.F, b.nbins, b.iscat, None, 5, p)
+    gb.set_feature_groups(b.vmap)
+    gb.build(aux.to(dev), None, k_cols, seed=5, leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1]).float())
+    tl_g = gb.pop_levels()[0]
+    assert tl_g.n_leaves == tl_r.n_leaves
+    for dr, dg in zip(tl_r.decs, tl_g.decs):
+        assert np.array_equal(dr["feat"], dg["feat"]) and np.array_equal(dr["bin"], dg["bin"])
+        np.testing.assert_allclose(dr["wl"], dg["wl"], rtol=1e-6)
+    assert torch.equal(ref.leaf_of_row, gb.leaf_of_row.cpu())
