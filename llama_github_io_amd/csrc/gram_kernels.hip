@@ -118,60 +118,77 @@ __global__ __launch_bounds__(256) void k_xtv(const float* __restrict__ Z, int64_
 }  // namespace
 
 // eta = Z @ B (+ off): Z [N, P] fp32 row-major, B [P, R] fp64 (R <= 8), eta [N, R] fp64 — the GLM linear
-// predictor without an fp64 copy of Z (GLMIterationTask's per-row x·beta). A half wave owns a row: lane
-// l reads columns (l&31) + 32m of row 2q + (l>>5) (coalesced 128-byte reads, ZB_UNR row pairs in flight),
-// multiplies by its register copy of B, and a 32-lane butterfly of fp64 shuffles sums each row. The
-// previous LDS-tiled version (one row per thread) read 2 GB of a 10M x 50 Z at 1.45 TB/s.
-#define ZB_UNR 8
-template <int RT>   // RT = R (1: IRLS eta), 8: any R <= 8
-__global__ __launch_bounds__(256) void k_zbeta(const float* __restrict__ Z, int64_t ldz, const double* __restrict__ B,
-                                               int R, int64_t N, int P, const double* __restrict__ off,
-                                               double* __restrict__ eta) {
-  const int lane = threadIdx.x & 63, c = lane & 31, kh = lane >> 5;
-  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  const int M = (P + 31) / 32;
-  const int RR = RT == 1 ? 1 : R;
-  for (int64_t base = wave * 2 * ZB_UNR; base < N; base += nwaves * 2 * ZB_UNR) {
-    double acc[ZB_UNR][RT];
-#pragma unroll
-    for (int q = 0; q < ZB_UNR; ++q)
-#pragma unroll
-      for (int k = 0; k < RT; ++k) acc[q][k] = 0.0;
-    // two 32-column chunks per step: 2 * ZB_UNR independent loads in flight per lane
-    for (int m = 0; m < M; m += 2) {
-      float z0[ZB_UNR], z1[ZB_UNR];
-      const int c0 = 32 * m + c, c1 = c0 + 32;
-      const bool ok0 = c0 < P, ok1 = c1 < P;
-#pragma unroll
-      for (int q = 0; q < ZB_UNR; ++q) {
-        const int64_t r = base + 2 * q + kh;
-        const bool rok = r < N;
-        const float* zr = Z + (rok ? r : 0) * ldz;
-        z0[q] = (ok0 && rok) ? zr[c0] : 0.f;
-        z1[q] = (ok1 && rok) ? zr[c1] : 0.f;
-      }
-#pragma unroll
-      for (int k = 0; k < RT; ++k) {
-        if (k >= RR) break;
-        const double b0 = ok0 ? B[(int64_t)c0 * RR + k] : 0.0;
-        const double b1 = ok1 ? B[(int64_t)c1 * RR + k] : 0.0;
-#pragma unroll
-        for (int q = 0; q < ZB_UNR; ++q) acc[q][k] += (double)z0[q] * b0 + (double)z1[q] * b1;
-      }
+// predictor without an fp64 copy of Z (GLMIterationTask's per-row x·beta). A block owns TR consecutive rows,
+// i.e. one contiguous TR*P-float span of Z: it is pulled into LDS with 16-byte loads (every lane of every
+// load instruction reading consecutive bytes, all issued before the first use), then each thread
+// accumulates one row's dot products in fp64 from LDS (row stride P words: odd P is bank-conflict free)
+// and writes eta once. MEASURED: column-tiled / half-wave-per-row variants read the 204-byte rows of a
+// 10M x 51 Z at 1.1-1.45 TB/s (several partial cache lines per load instruction).
+#define ZB_THREADS 256
+#define ZB_LDS_FLOATS 12288    // 48 KiB of Z per block
+__global__ __launch_bounds__(ZB_THREADS) void k_zbeta(const float* __restrict__ Z, int64_t ldz,
+                                                      const double* __restrict__ B, int R, int64_t N, int P, int TR,
+                                                      const double* __restrict__ off, double* __restrict__ eta) {
+  __shared__ __attribute__((aligned(16))) float tile[ZB_LDS_FLOATS];
+  __shared__ double bt[1024];                            // B when P * R <= 1024, else read from global
+  const int t = threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.x * TR;
+  if (r0 >= N) return;
+  const int nr = (int)min((int64_t)TR, N - r0);
+  const bool bl = P * R <= 1024;
+  if (bl)
+    for (int i = t; i < P * R; i += ZB_THREADS) bt[i] = B[i];
+  const int64_t n = (int64_t)nr * P;
+  const float* src = Z + r0 * ldz;
+  if (ldz == P && ((reinterpret_cast<uintptr_t>(src) & 15) == 0)) {
+    const int n4 = (int)(n >> 2);
+    const float4* s4 = reinterpret_cast<const float4*>(src);
+    float4* d4 = reinterpret_cast<float4*>(tile);
+    for (int i = t; i < n4; i += ZB_THREADS) d4[i] = s4[i];
+    for (int i = 4 * n4 + t; i < n; i += ZB_THREADS) tile[i] = src[i];
+  } else {
+    for (int i = t; i < n; i += ZB_THREADS) {
+      const int rr = i / P, cc = i - rr * P;
+      tile[i] = src[(int64_t)rr * ldz + cc];
     }
+  }
+  __syncthreads();
+  if (t >= nr) return;
+  const float* zr = tile + t * P;
+  double acc[8];
 #pragma unroll
-    for (int q = 0; q < ZB_UNR; ++q) {
-      const int64_t r = base + 2 * q + kh;
+  for (int k = 0; k < 8; ++k) acc[k] = 0.0;
+  if (R == 1) {
+    for (int c = 0; c < P; ++c) acc[0] += (double)zr[c] * (bl ? bt[c] : B[c]);
+  } else {
+    for (int c = 0; c < P; ++c) {
+      const double z = (double)zr[c];
 #pragma unroll
-      for (int k = 0; k < RT; ++k) {
-        if (k >= RR) break;
-        double v = acc[q][k];
-#pragma unroll
-        for (int sh = 16; sh >= 1; sh >>= 1) v += __shfl_xor(v, sh, 64);
-        if (c == 0 && r < N) eta[r * RR + k] = v + (off ? off[r] : 0.0);
-      }
+      for (int k = 0; k < 8; ++k)
+        if (k < R) acc[k] += z * (bl ? bt[c * R + k] : B[(int64_t)c * R + k]);
     }
+  }
+  const int64_t row = r0 + t;
+  const double o = off ? off[row] : 0.0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+    if (k < R) eta[row * R + k] = acc[k] + o;
+}
+
+// very wide designs (P > 12288, e.g. one-hot of huge factors): one wave per row, lanes stride the columns,
+// fp64 wave reduction
+__global__ __launch_bounds__(256) void k_zbeta_wide(const float* __restrict__ Z, int64_t ldz,
+                                                   const double* __restrict__ B, int R, int64_t N, int P,
+                                                   const double* __restrict__ off, double* __restrict__ eta) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (row >= N) return;
+  const float* zr = Z + row * ldz;
+  for (int k = 0; k < R; ++k) {
+    double a = 0.0;
+    for (int c = lane; c < P; c += 64) a += (double)zr[c] * B[(int64_t)c * R + k];
+    for (int sh = 32; sh >= 1; sh >>= 1) a += __shfl_xor(a, sh, 64);
+    if (lane == 0) eta[row * R + k] = a + (off ? off[row] : 0.0);
   }
 }
 
@@ -202,14 +219,20 @@ int h2o_xtv(const float* Z, long long ldz, const float* v, int R, long long N, i
 int h2o_zbeta(const float* Z, long long ldz, const double* B, int R, long long N, int P, const double* off,
               double* eta, hipStream_t stream) {
   if (R < 1 || R > 8 || N <= 0) return N <= 0 ? 0 : (int)hipErrorInvalidValue;
-  long long grid = (N + 4 * 2 * ZB_UNR - 1) / (4 * 2 * ZB_UNR);     // 4 waves per block, 2*ZB_UNR rows per wave
-  if (grid > 8192) grid = 8192;
-  if (R == 1)
-    hipLaunchKernelGGL(k_zbeta<1>, dim3((unsigned)grid), dim3(256), 0, stream, Z, (int64_t)ldz, B, R, (int64_t)N, P,
-                       off, eta);
-  else
-    hipLaunchKernelGGL(k_zbeta<8>, dim3((unsigned)grid), dim3(256), 0, stream, Z, (int64_t)ldz, B, R, (int64_t)N, P,
-                       off, eta);
+  if (P <= 0 || ldz < P) return (int)hipErrorInvalidValue;
+  // rows per block: the LDS span (<= 48 KiB), at most one per thread, a multiple of 4 (16-byte spans)
+  int TR = ZB_LDS_FLOATS / P;
+  if (TR > ZB_THREADS) TR = ZB_THREADS;
+  TR &= ~3;
+  if (TR < 1) TR = 1;
+  if ((long long)TR * P > ZB_LDS_FLOATS) {
+    hipLaunchKernelGGL(k_zbeta_wide, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, stream, Z, (int64_t)ldz, B, R,
+                       (int64_t)N, P, off, eta);
+    return (int)hipGetLastError();
+  }
+  const long long grid = (N + TR - 1) / TR;
+  hipLaunchKernelGGL(k_zbeta, dim3((unsigned)grid), dim3(ZB_THREADS), 0, stream, Z, (int64_t)ldz, B, R, (int64_t)N, P,
+                     TR, off, eta);
   return (int)hipGetLastError();
 }
 

@@ -141,20 +141,51 @@ def split_find_ref(h, nayy, wyy, nbins_f, iscat_f, mono_f, p: SplitParams, level
                 hi = e[a_hi if a_hi <= nb - 2 else nb - 2]
                 if hi > lo:
                     sc = anb / (hi - lo)
-                    cnt = lambda x: int(min(max(math.floor((x - lo) * sc), 0), anb - 1))  # noqa: E731
-                    allowed = {t for t in range(1, nb) if cnt(e[t - 1]) > (cnt(e[t - 2]) if t >= 2 else 0)}
+                    c = np.clip(np.floor((e[:nb - 1] - lo) * sc), 0, anb - 1)     # cnt(e[t - 1]), t = 1 .. nb-1
+                    allowed = c > np.concatenate([[0.0], c[:-1]])
         best_e, best_code = -1.0e300, -1
         cands = []
         if wNA >= p.min_w and W > 0 and not random_mode:
             cands.append((float(_E(p.mode, p, W, WY) + _E(p.mode, p, wNA, wyNA)), 0))
-        for t in range(1, nb):
-            if random_mode and t != rand_b:
-                continue
-            if allowed is not None and t not in allowed:
-                continue
-            wb = sw[t] - sw[t - 1]
-            if wb == 0.0 and not random_mode:
-                continue
+        if random_mode:
+            ts = [rand_b] if 1 <= rand_b < nb else []
+        else:
+            ts = None
+        if ts is None and nb > 1:
+            # every threshold t = 1 .. nb-1 at once (same float64 operations as the per-t rule below)
+            t = np.arange(1, nb)
+            m = (sw[t] - sw[t - 1]) != 0.0
+            if allowed is not None:
+                m &= allowed
+            wlo, wylo = sw[t - 1], swy[t - 1]
+            whi, wyhi = W - wlo, WY - wylo
+
+            def lv(a, b):
+                if p.mode == MODE_NEWTON:
+                    return b / (a + p.lam)
+                with np.errstate(divide="ignore", invalid="ignore"):
+                    return np.where(a > 0, b / np.where(a > 0, a, 1.0), 0.0)
+
+            def mono_ok(a1, b1, a2, b2):
+                return np.ones_like(a1, dtype=bool) if mono == 0 else mono * lv(a1, b1) <= mono * lv(a2, b2)
+            if wNA == 0.0:
+                ok = m & (wlo >= p.min_w) & (whi >= p.min_w) & mono_ok(wlo, wylo, whi, wyhi)
+                ev = _E(p.mode, p, wlo, wylo) + _E(p.mode, p, whi, wyhi)
+                code = t * 2 + (wlo > whi)
+            else:
+                ok1 = m & (wlo + wNA >= p.min_w) & (whi >= p.min_w) & mono_ok(wlo + wNA, wylo + wyNA, whi, wyhi)
+                e1 = _E(p.mode, p, wlo + wNA, wylo + wyNA) + _E(p.mode, p, whi, wyhi)
+                ok2 = m & (wlo >= p.min_w) & (whi + wNA >= p.min_w) & mono_ok(wlo, wylo, whi + wNA, wyhi + wyNA)
+                e2 = _E(p.mode, p, wlo, wylo) + _E(p.mode, p, whi + wNA, wyhi + wyNA)
+                right = ok2 & (~ok1 | (e2 > e1))
+                ok = ok1 | ok2
+                ev = np.where(right, e2, e1)
+                code = t * 2 + np.where(right, 0, 1)
+            if ok.any():
+                ev, code = ev[ok], code[ok]
+                be = float(ev.max())
+                cands.append((be, int(code[ev == be].min())))
+        for t in (ts or []):
             wlo, wylo = sw[t - 1], swy[t - 1]
             whi, wyhi = W - wlo, WY - wylo
             my_e, my_c = -1.0e300, -1
@@ -311,11 +342,15 @@ class RefTreeBuilder:
         a32 = aux[rows, 0]; b32 = aux[rows, 1]
         yy = np.where(a32 > 0, (b32 * b32 / np.where(a32 > 0, a32, 1)).astype(np.float32), 0).astype(np.float64)
         nayy = np.zeros(F)
-        for f in range(F):
-            bf = self.bins[rows, f].astype(np.int64)
-            h[f, :, 0] = np.bincount(bf, weights=a, minlength=256)
-            h[f, :, 1] = np.bincount(bf, weights=b, minlength=256)
-            nayy[f] = yy[bf == NA_BIN].sum()
+        for f0 in range(0, F, 16):          # 16 features per bincount (same per-bin summation order)
+            f1 = min(F, f0 + 16)
+            bf = self.bins[rows, f0:f1].astype(np.int64)
+            key = (bf + 256 * np.arange(f1 - f0)[None, :]).T.reshape(-1)
+            n = 256 * (f1 - f0)
+            h[f0:f1, :, 0] = np.bincount(key, weights=np.tile(a, f1 - f0), minlength=n).reshape(f1 - f0, 256)
+            h[f0:f1, :, 1] = np.bincount(key, weights=np.tile(b, f1 - f0), minlength=n).reshape(f1 - f0, 256)
+            for j in range(f1 - f0):
+                nayy[f0 + j] = yy[bf[:, j] == NA_BIN].sum()
         return h, nayy, yy.sum()
 
     def build(self, aux_static: torch.Tensor, feat_ok=None, k_cols: int = 0, seed: int = 0, leaf_fn=None):

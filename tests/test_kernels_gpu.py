@@ -286,7 +286,7 @@ def test_fused_gbm_step_matches_eager_path(dist, monkeypatch):
     _ = (a, b)
 
 
-@pytest.mark.parametrize("N,P,R", [(1000, 7, 1), (70001, 51, 1), (5000, 130, 3), (33, 200, 8)])
+@pytest.mark.parametrize("N,P,R", [(1000, 7, 1), (70001, 51, 1), (5000, 130, 3), (33, 200, 8), (37, 13001, 2)])
 def test_zbeta_matches_fp64(N, P, R):
     # GLM linear predictor: fp32 design read once, fp64 accumulation (k_zbeta) vs the fp64 matmul
     from llama_github_io_amd.ops.gram import zbeta

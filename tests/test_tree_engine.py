@@ -448,7 +448,9 @@ def test_gpu_wide_bins_match_reference(case):
     b = fit_binning(X, info.iscat, info.nlevels, max_bins=1016)
     assert b.vmap is not None and b.F > X.shape[0]
     bins = apply_binning(b, X)
-    g = y - y.mean()
+    # +-0.5 gradients quantize exactly onto the fixed-point histogram grid: adjacent fine thresholds give
+    # near-equal gains, and only an exact grid keeps the GPU's and the fp64 reference's order of them equal
+    g = y - 0.5
     aux = torch.stack([torch.ones_like(y), g, g, torch.ones_like(y)], 1).contiguous()
     k_cols = 0
     p = T.SplitParams(min_w=10)
