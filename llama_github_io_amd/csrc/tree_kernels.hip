@@ -34,6 +34,7 @@
 #define BLK 1024                // one 16-wave block per CU (the int64 LDS histogram is 128 KiB)
 #define NW (BLK / 64)
 #define TILE 2048               // rows per work tile
+#define LEAFQ_STRIPES 16        // fixed-point leaf-sum copies (leafq: LEAFQ_STRIPES * 2 * leaf_cap slots)
 #define LPR 8                   // lanes per row
 #define RPI (BLK / LPR)         // rows per iteration (128)
 
@@ -1328,14 +1329,18 @@ __global__ __launch_bounds__(256) void k_leaf_assign(
       if (qn) atomicAdd(sq + 2 * leaf, (unsigned long long)qn);
       if (qd) atomicAdd(sq + 2 * leaf + 1, (unsigned long long)qd);
     } else {
-      if (qn) atomicAdd(leafq + 2 * leaf, (unsigned long long)qn);
-      if (qd) atomicAdd(leafq + 2 * leaf + 1, (unsigned long long)qd);
+      unsigned long long* lq = leafq + (size_t)(blockIdx.x % LEAFQ_STRIPES) * 2 * leaf_cap;
+      if (qn) atomicAdd(lq + 2 * leaf, (unsigned long long)qn);
+      if (qd) atomicAdd(lq + 2 * leaf + 1, (unsigned long long)qd);
     }
   }
   if (lds) {
     __syncthreads();
+    // one of LEAFQ_STRIPES copies per block (k_leafsum_finish adds them): 2048 blocks flushing into one
+    // set of leaf slots serialised on those few L2 addresses (57 us of a 1.375M-row tree)
+    unsigned long long* lq = leafq + (size_t)(blockIdx.x % LEAFQ_STRIPES) * 2 * leaf_cap;
     for (int i = threadIdx.x; i < 2 * leaf_cap; i += blockDim.x)
-      if (sq[i]) atomicAdd(leafq + i, sq[i]);
+      if (sq[i]) atomicAdd(lq + i, sq[i]);
   }
 }
 
@@ -1345,10 +1350,16 @@ __global__ void k_leafsum_finish(unsigned long long* __restrict__ leafq, const d
                                  double* __restrict__ leafsum) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  leafsum[2 * i] = (double)(long long)leafq[2 * i] * qs[8];
-  leafsum[2 * i + 1] = (double)(long long)leafq[2 * i + 1] * qs[9];
-  leafq[2 * i] = 0ull;
-  leafq[2 * i + 1] = 0ull;
+  long long a = 0, b = 0;
+  for (int k = 0; k < LEAFQ_STRIPES; ++k) {                 // n == leaf_cap: stripe k at k * 2 * n
+    unsigned long long* q = leafq + (size_t)k * 2 * n;
+    a += (long long)q[2 * i];
+    b += (long long)q[2 * i + 1];
+    q[2 * i] = 0ull;
+    q[2 * i + 1] = 0ull;
+  }
+  leafsum[2 * i] = (double)a * qs[8];
+  leafsum[2 * i + 1] = (double)b * qs[9];
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1556,6 +1567,7 @@ int h2o_abi_version() { return H2O_ABI_VERSION; }
 
 int h2o_tree_sizes(int* out) {
   out[7] = AMAX_SHARDS;
+  out[8] = LEAFQ_STRIPES;
   out[0] = sizeof(Node); out[1] = sizeof(Dec); out[2] = sizeof(Cand); out[3] = TILE; out[4] = FTILE;
   out[5] = HIST_LDS_BYTES + HIST_LDS_TAIL;  // k_hist_build LDS bytes
   out[6] = BLK;

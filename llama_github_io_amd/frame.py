@@ -37,28 +37,33 @@ def engine_device():
 
 # ================================================================================================
 class Column:
-    __slots__ = ("name", "type", "_data", "domain", "strings", "_spilled")
+    __slots__ = ("name", "type", "_data", "domain", "strings", "_spilled", "_codec")
 
     def __init__(self, name, type_, data=None, domain=None, strings=None):
         self.name = name
         self.type = type_
         self._data = data
         self._spilled = None
+        self._codec = None
         self.domain = domain
         self.strings = strings
 
-    # device residency: a column spilled by the memory manager comes back on first access
+    # device residency: a column spilled by the memory manager comes back on first access; a compressed
+    # column (see compress()) is decoded for good on the first ``data`` access (callers may write it)
     @property
     def data(self):
         if self._spilled is not None:
             from .utils import memory
             memory.restore_column(self)
+        if self._codec is not None:
+            self._data, self._codec = _decode(self._data, self._codec), None
         return self._data
 
     @data.setter
     def data(self, v):
         self._data = v
         self._spilled = None
+        self._codec = None
 
     def raw_data(self):
         return self._data
@@ -70,8 +75,43 @@ class Column:
     def spilled_device(self):
         return self._spilled
 
+    # ---- chunk compression (water/fvec C1/C2/C4 and the scaled C1S/C2S/C4S chunks)
+    def compress(self) -> int:
+        """Store a numeric column as 8/16/32-bit integer codes when every value is an integer or a decimal
+        with at most 4 places whose scaled range fits (NA = the type's minimum); values decode bit-exactly
+        as (code + base) / 10^k. Returns the bytes saved (0: left as is)."""
+        if self.type not in ("real", "int") or self._codec is not None or self._spilled is not None:
+            return 0
+        d = self._data
+        if d is None or not torch.is_floating_point(d) or d.dim() != 1:
+            return 0
+        enc = _encode(d)
+        if enc is None:
+            return 0
+        codes, codec = enc
+        saved = d.numel() * d.element_size() - codes.numel() * codes.element_size()
+        if saved <= 0:
+            return 0
+        self._data, self._codec = codes, codec
+        return saved
+
+    @property
+    def compressed(self) -> bool:
+        return self._codec is not None
+
+    def values(self) -> torch.Tensor:
+        """Read-only numeric values without decoding the column for good (model matrices, statistics)."""
+        if self._codec is None:
+            return self.data
+        if self._spilled is not None:
+            from .utils import memory
+            memory.restore_column(self)
+        return _decode(self._data, self._codec)
+
     @property
     def n(self):
+        if self._codec is not None:
+            return int(self._data.numel())
         if self.type == "string":
             return len(self.strings)
         if self.type == "uuid":
@@ -102,7 +142,7 @@ class Column:
             return torch.from_numpy(vals).to(engine_device())
         if self.type == "uuid":
             return torch.full((self.n,), float("nan"), dtype=torch.float64, device=self.data.device)
-        return self.data
+        return self.values()
 
     def take(self, idx: torch.Tensor):
         if self.type == "string":
@@ -119,6 +159,53 @@ class Column:
             dom = np.array(self.domain + [None], dtype=object)
             return dom[np.where(codes < 0, len(self.domain), codes)]
         return self.data.cpu().numpy()
+
+
+_CODEC_MIN_ROWS = 1024
+
+
+def _encode(x: torch.Tensor):
+    """(int codes, (base, k, dtype)) with x == (codes + base) / 10^k bit for bit (NaN <-> the minimum code),
+    or None. Tries k = 0..4 decimal places, the narrowest of int8 / int16 / int32."""
+    if x.numel() < _CODEC_MIN_ROWS or bool(torch.isinf(x).any()):
+        return None
+    fin = ~torch.isnan(x)
+    v = x[fin].double()
+    if v.numel() == 0:
+        return None
+    for k in range(5):
+        p = float(10 ** k)
+        sv = torch.round(v * p)
+        if float(sv.abs().max()) >= 2.0 ** 52:
+            return None
+        if not torch.equal((sv / p).to(x.dtype), x[fin]):
+            continue
+        lo, hi = float(sv.min()), float(sv.max())
+        for dt, bits in ((torch.int8, 8), (torch.int16, 16), (torch.int32, 32)):
+            half = 2 ** (bits - 1)
+            if hi - lo <= 2 * half - 2:
+                base = lo + half - 1
+                codes = torch.full(x.shape, -half, dtype=dt, device=x.device)
+                codes[fin] = (sv - base).to(dt)
+                return codes, (base, k, x.dtype)
+        return None
+    return None
+
+
+def _decode(codes: torch.Tensor, codec) -> torch.Tensor:
+    base, k, dt = codec
+    na = codes == torch.iinfo(codes.dtype).min
+    v = (codes.double() + base) / float(10 ** k)
+    return torch.where(na, torch.full_like(v, float("nan")), v).to(dt)
+
+
+def compress_frame(fr) -> int:
+    """Compress every numeric column of a frame (parse-time default, as the reference's chunk encodings);
+    H2O_COMPRESS=0 turns it off. Returns the bytes saved."""
+    import os
+    if os.environ.get("H2O_COMPRESS", "1") == "0":
+        return 0
+    return sum(c.compress() for c in fr._cols.values())
 
 
 _UUID_NA = -(1 << 63)

@@ -545,6 +545,8 @@ def import_file(path=None, destination_frame=None, parse=True, header=0, sep=Non
         frames = [fr if fr._shard is not None else dframe.shard_frame(fr) for fr in frames]
     out = frames[0] if len(frames) == 1 else _rbind_sharded(frames)
     _detect_uuid(out, col_types)
+    from ..frame import compress_frame
+    compress_frame(out)             # integer / short-decimal numeric columns as 8/16/32-bit codes
     dest = destination_frame or _dest_name(files[0])
     from ..core import dkv
     dkv.remove(out.frame_id) if out.frame_id != dest and dkv.contains(out.frame_id) else None

@@ -492,7 +492,7 @@ class GpuTreeBuilder:
         if self.planar:
             assert bins.shape[2] == 32 and bins.shape[0] >= 2
         self.lib = nat.hip()
-        sz = np.zeros(8, dtype=np.int32)
+        sz = np.zeros(16, dtype=np.int32)
         self.lib.h2o_tree_sizes(sz.ctypes.data)
         assert sz[0] == NODE_DT.itemsize and sz[1] == DEC_DT.itemsize and sz[2] == CAND_BYTES, sz
         assert sz[7] == AMAX_SHARDS, sz
@@ -534,7 +534,8 @@ class GpuTreeBuilder:
         self.scratch = torch.empty(2 * capmax + 16, dtype=torch.int32, device=dev)
         self.leaf_cap = min(N + 1, 2 * sum(self.caps) + 2)
         self.leafsum = torch.zeros(self.leaf_cap, 2, dtype=torch.float64, device=dev)
-        self.leafq = torch.zeros(self.leaf_cap * 2, dtype=torch.int64, device=dev)   # fixed-point leaf sums
+        # fixed-point leaf sums, LEAFQ_STRIPES copies (blocks spread their flush atomics over them)
+        self.leafq = torch.zeros(int(sz[8]) * self.leaf_cap * 2, dtype=torch.int64, device=dev)
         self.leaf_of_row = torch.empty(N, dtype=torch.int32, device=dev)
         self.nbins_f = torch.as_tensor(np.asarray(nbins_f, dtype=np.int32), device=dev)
         self.iscat_f = torch.as_tensor(np.asarray(iscat_f, dtype=np.int32), device=dev)
