@@ -108,7 +108,7 @@ def prepare(algo: str, params: dict, x=None, y=None, training_frame=None):
                 keep.append(n)
             else:
                 from ..parallel import dframe
-                m = dframe.moments(c.data, sharded)
+                m = dframe.moments(c.values(), sharded)     # compressed columns stay encoded
                 if m["n"] > 0 and (m["max"] != m["min"] or m["nas"] > 0):
                     keep.append(n)
         xs = keep

@@ -57,3 +57,44 @@ def test_uuid_columns(tmp_path):
     sub = fr[fr["x"] >= 18, :].as_data_frame()["id"].tolist()
     assert sub == us[18:] + [None]
     assert fr["id"].isna().as_data_frame().values.ravel().tolist()[-2:] == [0, 1]
+
+
+def test_numeric_columns_compress_bit_exactly(tmp_path, monkeypatch):
+    """Chunk compression (C1/C2/C4 and the scaled C1S/C2S/C4S encodings of water/fvec): integer and
+    short-decimal numeric columns are stored as 8/16/32-bit codes at import and decode bit for bit; writes
+    through ``data`` decode the column for good; models see the same values."""
+    import numpy as np
+    import pandas as pd
+    import torch
+    import h2o
+    from h2o.estimators import H2OGradientBoostingEstimator
+    h2o.init(verbose=False)
+    rng = np.random.default_rng(3)
+    n = 4000
+    df = pd.DataFrame({"small": rng.integers(0, 100, n), "mid": rng.integers(-20000, 20000, n),
+                       "dec": np.round(rng.normal(size=n) * 50, 2), "real": rng.normal(size=n)})
+    df.loc[::11, "dec"] = np.nan
+    df["y"] = (df["small"] + df["real"] * 10 > 50).astype(int)
+    p = tmp_path / "c.csv"
+    df.to_csv(p, index=False)
+    fr = h2o.import_file(str(p))
+    cols = fr._cols
+    assert cols["small"].compressed and cols["small"].raw_data().dtype == torch.int8
+    assert cols["mid"].compressed and cols["mid"].raw_data().dtype == torch.int16
+    assert cols["dec"].compressed and not cols["real"].compressed
+    for name in ("small", "mid", "dec", "real"):
+        v = cols[name].values().cpu().numpy()
+        ref = df[name].to_numpy(dtype=np.float64)
+        assert np.array_equal(np.isnan(v), np.isnan(ref)) and np.array_equal(v[~np.isnan(v)], ref[~np.isnan(ref)])
+    m1 = H2OGradientBoostingEstimator(ntrees=3, max_depth=3, seed=1)
+    m1.train(x=["small", "mid", "dec", "real"], y="y", training_frame=fr)
+    assert cols["small"].compressed                      # model matrices decode transiently
+    monkeypatch.setenv("H2O_COMPRESS", "0")
+    fr2 = h2o.import_file(str(p))
+    assert not fr2._cols["small"].compressed
+    m2 = H2OGradientBoostingEstimator(ntrees=3, max_depth=3, seed=1)
+    m2.train(x=["small", "mid", "dec", "real"], y="y", training_frame=fr2)
+    assert np.allclose(m1.predict(fr).as_data_frame().to_numpy(float), m2.predict(fr2).as_data_frame().to_numpy(float))
+    c = cols["mid"]
+    c.data[0] = 12345.5                                  # a write decodes the column for good
+    assert not c.compressed and float(c.values()[0]) == 12345.5
