@@ -711,6 +711,13 @@ class GLMTrainer:
         es = p.get("early_stopping", True) is not False
         hist_tr, hist_va = [0.0] * 5, [0.0] * 5
         old_tr, old_va, n_iter = null_dev, None, 0
+        if valid is not None and len(lambdas) > 1:
+            # GLM.java seeds the validation improvements with the null model's validation deviance
+            yv0, wv0 = valid[1], valid[2]
+            okv0 = ~torch.isnan(yv0)
+            wv0 = torch.ones_like(yv0, dtype=torch.float64) if wv0 is None else wv0.double()
+            old_va = _gsum((wv0[okv0] * fam.deviance(yv0.double()[okv0],
+                                                      torch.full_like(yv0.double()[okv0], ymu))).sum())
         for li, lam in enumerate(lambdas):
             l1, l2 = lam * alpha, lam * (1 - alpha)
             if p.get("cold_start") and li > 0:     # cold_start: every lambda starts from the initial coefficients

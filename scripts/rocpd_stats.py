@@ -22,7 +22,22 @@ def main():
     ap.add_argument("--md", action="store_true")
     ap.add_argument("--timeline", default=None, help="kernel-name substring marking one step (e.g. k_gbm_step): "
                     "print every step's wall span and GPU-busy fraction")
+    ap.add_argument("--sequence", default=None, help="kernel-name substring marking one step: print the dispatch "
+                    "sequence (name, duration, gap before it) of the step after its 10th occurrence")
     a = ap.parse_args()
+    if a.sequence:
+        db = sqlite3.connect(a.db)
+        ks = db.execute("select name, start, end from kernels order by start").fetchall()
+        idx = [i for i, k in enumerate(ks) if a.sequence in k[0]]
+        if len(idx) < 12:
+            print("not enough steps")
+            return
+        i0, i1 = idx[10], idx[11]
+        print(f"step span {(ks[i1][1] - ks[i0][1]) / 1e3:.1f} us, {i1 - i0} dispatches\n| # | kernel | us | gap us |\n|---|---|---|---|")
+        for j in range(i0, i1):
+            nm = ks[j][0] if len(ks[j][0]) < 60 else ks[j][0][:57] + "..."
+            print(f"| {j - i0} | `{nm}` | {(ks[j][2] - ks[j][1]) / 1e3:.1f} | {(ks[j][1] - ks[j - 1][2]) / 1e3:.1f} |")
+        return
     if a.timeline:
         db = sqlite3.connect(a.db)
         ks = db.execute("select name, start, end from kernels order by start").fetchall()
