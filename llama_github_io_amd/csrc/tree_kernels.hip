@@ -734,18 +734,14 @@ __global__ __launch_bounds__(256) void k_split_find(
   }
 }
 
-// k_split_reduce: best feature per node (with per-tree feature mask and per-node column sampling).
+// Best feature of one node (one wave; lane = threadIdx.x & 63): k_split_reduce, and k_plan's prologue on
+// levels of at most PLAN_REDUCE_MAX nodes (the single plan block's 16 waves take the nodes; no extra launch).
 // fgroup (nullable): engine column -> original feature. A numeric feature binned wider than one byte holds
 // several adjacent engine columns (interleaved edge subsets, see ops/binning.py); column sampling draws
 // ORIGINAL features (key and rank of a column = its feature's), so such a feature is in or out as a whole.
-__global__ __launch_bounds__(64) void k_split_reduce(
-    const Cand* __restrict__ cand, const int* __restrict__ meta, int F,
-    const int* __restrict__ feat_ok /*[F] per-tree mask, 1 = usable*/, int k_cols,
-    unsigned long long seed, int level, Dec* __restrict__ dec,
-    const unsigned char* __restrict__ node_ok /*[nodes][F] interaction-constraint mask or null*/,
-    const int* __restrict__ fgroup) {
-  const int node = blockIdx.x, lane = threadIdx.x;
-  if (node >= meta[0]) return;
+__device__ void reduce_node(const Cand* __restrict__ cand, int node, int F, const int* __restrict__ feat_ok, int k_cols,
+                            unsigned long long seed, int level, Dec* __restrict__ dec,
+                            const unsigned char* __restrict__ node_ok, const int* __restrict__ fgroup, int lane) {
   const unsigned char* nok = node_ok ? node_ok + (size_t)node * F : nullptr;
   auto usable = [&](int f) { return feat_ok[f] != 0 && (!nok || nok[f] != 0); };
   auto gid = [&](int f) { return fgroup ? fgroup[f] : f; };
@@ -795,6 +791,28 @@ __global__ __launch_bounds__(64) void k_split_reduce(
     dec[node] = d;
   }
 }
+
+__global__ __launch_bounds__(64) void k_split_reduce(
+    const Cand* __restrict__ cand, const int* __restrict__ meta, int F,
+    const int* __restrict__ feat_ok /*[F] per-tree mask, 1 = usable*/, int k_cols,
+    unsigned long long seed, int level, Dec* __restrict__ dec,
+    const unsigned char* __restrict__ node_ok /*[nodes][F] interaction-constraint mask or null*/,
+    const int* __restrict__ fgroup) {
+  const int node = blockIdx.x;
+  if (node >= meta[0]) return;
+  reduce_node(cand, node, F, feat_ok, k_cols, seed, level, dec, node_ok, fgroup, threadIdx.x);
+}
+
+struct PlanReduce {          // k_plan's fused k_split_reduce (cand == null: decisions already made)
+  const Cand* cand;
+  int F;
+  const int* feat_ok;
+  int k_cols;
+  unsigned long long seed;
+  const unsigned char* node_ok;
+  const int* fgroup;
+};
+#define PLAN_REDUCE_MAX 256
 
 // ------------------------------------------------------------------------------------------------
 // Block-wide exclusive scan helper for k_plan (1024 threads, int values). Returns exclusive prefix
@@ -861,16 +879,21 @@ __device__ void level_tile_prefix(const Node* __restrict__ next, int nn, int* __
 //   (curs[c] = {front, back, region start, region end}, from the parent's left count prev_nl) and
 //   k_ranges turns the final cursors into ranges + tile prefix.
 __global__ __launch_bounds__(1024) void k_plan(
-    const Node* __restrict__ nodes, const int* __restrict__ meta, const Dec* __restrict__ dec,
+    const Node* __restrict__ nodes, const int* __restrict__ meta, Dec* __restrict__ dec,
     int* __restrict__ node_nl, const int* __restrict__ prev_nl, int4* __restrict__ curs,
     int* __restrict__ child_l, int* __restrict__ child_r,
     Node* __restrict__ next, int* __restrict__ next_tile_prefix, int* __restrict__ next_meta,
     int* __restrict__ next_build_prefix,
     int* __restrict__ counters, int* __restrict__ scratch /* >= cap_cur ints */,
-    int depth, int max_depth, double min_w, int cap_next, int leaf_cap) {
+    int depth, int max_depth, double min_w, int cap_next, int leaf_cap, PlanReduce pr) {
   __shared__ int sh[17];
   const int n = meta[0];
   const int T = blockDim.x, tid = threadIdx.x;
+  if (pr.cand) {
+    for (int node = tid >> 6; node < n; node += T >> 6)
+      reduce_node(pr.cand, node, pr.F, pr.feat_ok, pr.k_cols, pr.seed, depth, dec, pr.node_ok, pr.fgroup, tid & 63);
+    __syncthreads();                     // the block's own decisions (global) before the plan reads them
+  }
   const bool odd = depth & 1;
   int total;
   const int perN = (n + T - 1) / T;
@@ -1346,8 +1369,26 @@ __global__ __launch_bounds__(256) void k_leaf_assign(
 
 // fixed-point leaf sums -> fp64 leafsum[L][2] (and, with leafval, the closed-form Newton leaf values of
 // k_leaf_values); also re-zeroes the fixed-point slots for the next tree
+struct LeafVals {       // closed-form leaf values folded into k_leafsum_finish (out == null: none)
+  int log_link;
+  double scale, kclamp, mx, lam, l1;
+  float* out;
+};
+
+__device__ __forceinline__ float leaf_value(double num, double den, const LeafVals& v) {
+  if (v.l1 > 0.0) num = num > v.l1 ? num - v.l1 : (num < -v.l1 ? num + v.l1 : 0.0);
+  double g = den == 0.0 ? 0.0 : num / (den + v.lam);
+  if (v.log_link) g = den == 0.0 ? 0.0 : log(fmax(g, 1e-300));
+  double x = v.scale * g;
+  if (x != x) x = 0.0;                                      // nan_to_num(nan=0)
+  if (v.kclamp > 0.0) x = fmin(fmax(x, -v.kclamp), v.kclamp);  // multinomial +-1e4
+  if (isinf(x)) x = x > 0 ? 1e4 : -1e4;                      // nan_to_num(posinf/neginf=+-1e4)
+  x = fmin(fmax(x, -v.mx), v.mx);                           // max_abs_leafnode_pred (inf: no-op)
+  return (float)x;
+}
+
 __global__ void k_leafsum_finish(unsigned long long* __restrict__ leafq, const double* __restrict__ qs, int n,
-                                 double* __restrict__ leafsum) {
+                                 double* __restrict__ leafsum, LeafVals lv) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   long long a = 0, b = 0;
@@ -1360,6 +1401,7 @@ __global__ void k_leafsum_finish(unsigned long long* __restrict__ leafq, const d
   }
   leafsum[2 * i] = (double)a * qs[8];
   leafsum[2 * i + 1] = (double)b * qs[9];
+  if (lv.out) lv.out[i] = leaf_value(leafsum[2 * i], leafsum[2 * i + 1], lv);   // single process: no second launch
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1529,17 +1571,8 @@ __global__ void k_leaf_values(const double* __restrict__ leafsum, int n, int log
                               double mx, double lam, double l1, float* __restrict__ out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  double num = leafsum[2 * i];
-  const double den = leafsum[2 * i + 1];
-  if (l1 > 0.0) num = num > l1 ? num - l1 : (num < -l1 ? num + l1 : 0.0);
-  double g = den == 0.0 ? 0.0 : num / (den + lam);
-  if (log_link) g = den == 0.0 ? 0.0 : log(fmax(g, 1e-300));
-  double v = scale * g;
-  if (v != v) v = 0.0;                                      // nan_to_num(nan=0)
-  if (kclamp > 0.0) v = fmin(fmax(v, -kclamp), kclamp);      // multinomial +-1e4
-  if (isinf(v)) v = v > 0 ? 1e4 : -1e4;                      // nan_to_num(posinf/neginf=+-1e4)
-  v = fmin(fmax(v, -mx), mx);                               // max_abs_leafnode_pred (inf: no-op)
-  out[i] = (float)v;
+  const LeafVals v{log_link, scale, kclamp, mx, lam, l1, out};
+  out[i] = leaf_value(leafsum[2 * i], leafsum[2 * i + 1], v);
 }
 
 // ================================================================================================
@@ -1645,15 +1678,24 @@ int h2o_ic_next(const void* next, const void* next_meta, const void* dec, const 
   return (int)hipGetLastError();
 }
 
+static int plan_launch(const void* nodes, const void* meta, void* dec, void* node_nl, const void* prev_nl, void* curs,
+                       void* child_l, void* child_r, void* next, void* next_tile_prefix, void* next_meta,
+                       void* next_build_prefix, void* counters, void* scratch, int depth, int max_depth, double min_w,
+                       int cap_next, int leaf_cap, PlanReduce pr, hipStream_t s) {
+  hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, s, (const Node*)nodes, (const int*)meta, (Dec*)dec,
+                     (int*)node_nl, (const int*)prev_nl, (int4*)curs, (int*)child_l, (int*)child_r, (Node*)next,
+                     (int*)next_tile_prefix, (int*)next_meta, (int*)next_build_prefix, (int*)counters, (int*)scratch,
+                     depth, max_depth, min_w, cap_next, leaf_cap, pr);
+  return (int)hipGetLastError();
+}
+
 int h2o_plan(const void* nodes, const void* meta, const void* dec, void* node_nl, const void* prev_nl, void* curs,
              void* child_l, void* child_r, void* next, void* next_tile_prefix, void* next_meta, void* next_build_prefix,
              void* counters, void* scratch, int depth, int max_depth, double min_w, int cap_next, int leaf_cap,
              hipStream_t s) {
-  hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, s, (const Node*)nodes, (const int*)meta, (const Dec*)dec,
-                     (int*)node_nl, (const int*)prev_nl, (int4*)curs, (int*)child_l, (int*)child_r, (Node*)next,
-                     (int*)next_tile_prefix, (int*)next_meta, (int*)next_build_prefix, (int*)counters, (int*)scratch,
-                     depth, max_depth, min_w, cap_next, leaf_cap);
-  return (int)hipGetLastError();
+  PlanReduce pr{nullptr, 0, nullptr, 0, 0ull, nullptr, nullptr};
+  return plan_launch(nodes, meta, (void*)dec, node_nl, prev_nl, curs, child_l, child_r, next, next_tile_prefix,
+                     next_meta, next_build_prefix, counters, scratch, depth, max_depth, min_w, cap_next, leaf_cap, pr, s);
 }
 
 int h2o_ranges(void* next, const void* curs, void* tp, void* bp, void* meta, hipStream_t s) {
@@ -1721,9 +1763,9 @@ int h2o_route(const void* sbins, const void* say, const void* saw, void* dbins, 
 }
 
 // leaf id of every row (original order) + fixed-point leaf sums -> fp64 leafsum[leaf_cap][2]
-int h2o_leaf_assign(const void* master, int stride, long long N, const void* lvptrs, int D, const void* an,
-                    const void* ad, const void* qs, void* leaf_of_row, void* leafq, int leaf_cap, void* leafsum,
-                    int n_nodes, int planar, hipStream_t s) {
+static int leaf_assign_launch(const void* master, int stride, long long N, const void* lvptrs, int D, const void* an,
+                              const void* ad, const void* qs, void* leaf_of_row, void* leafq, int leaf_cap,
+                              void* leafsum, int n_nodes, int planar, LeafVals lv, hipStream_t s) {
   if (D > TP_MAXL_DEV) return (int)hipErrorInvalidValue;
   long long grid = (N + 255) / 256;
   if (grid > 2048) grid = 2048;
@@ -1742,8 +1784,16 @@ int h2o_leaf_assign(const void* master, int stride, long long N, const void* lvp
   }
 #undef LA
   hipLaunchKernelGGL(k_leafsum_finish, dim3((leaf_cap + 255) / 256), dim3(256), 0, s, (unsigned long long*)leafq,
-                     (const double*)qs, leaf_cap, (double*)leafsum);
+                     (const double*)qs, leaf_cap, (double*)leafsum, lv);
   return (int)hipGetLastError();
+}
+
+int h2o_leaf_assign(const void* master, int stride, long long N, const void* lvptrs, int D, const void* an,
+                    const void* ad, const void* qs, void* leaf_of_row, void* leafq, int leaf_cap, void* leafsum,
+                    int n_nodes, int planar, hipStream_t s) {
+  const LeafVals lv{0, 0.0, 0.0, 0.0, 0.0, 0.0, nullptr};
+  return leaf_assign_launch(master, stride, N, lvptrs, D, an, ad, qs, leaf_of_row, leafq, leaf_cap, leafsum, n_nodes,
+                            planar, lv, s);
 }
 
 int h2o_amax(const void* aux, long long N, void* amax_bits, hipStream_t s) {
@@ -1891,12 +1941,19 @@ int h2o_tree_grow(const TreePlan* P, int d, int dist, hipStream_t s) {
   const bool odd = d % 2 == 1;
   int rc;
   const int kc = P->kc_level[d] > 0 ? P->kc_level[d] : P->k_cols;
-  rc = h2o_split_reduce(P->cand, P->meta[d], cap, P->F, P->feat_ok, kc, P->seed, d, P->dec[d],
-                        P->ic_map ? P->ic[d] : nullptr, P->fgroup, s);
-  if (rc) return -rc;
-  rc = h2o_plan(P->nodes[d], P->meta[d], P->dec[d], P->nl[d], odd ? P->nl[d - 1] : nullptr, P->cur[d], P->cl[d],
-                P->cr[d], P->nodes[d + 1], P->tp[d + 1], P->meta[d + 1], P->bp[d + 1], P->counters, P->scratch, d,
-                P->D, P->min_w, P->caps[d + 1], P->leaf_cap, s);
+  // small levels: the plan block picks the decisions itself (one launch instead of two)
+  PlanReduce pr{nullptr, P->F, (const int*)P->feat_ok, kc, P->seed,
+                P->ic_map ? (const unsigned char*)P->ic[d] : nullptr, (const int*)P->fgroup};
+  if (cap <= PLAN_REDUCE_MAX) {
+    pr.cand = (const Cand*)P->cand;
+  } else {
+    rc = h2o_split_reduce(P->cand, P->meta[d], cap, P->F, P->feat_ok, kc, P->seed, d, P->dec[d],
+                          P->ic_map ? P->ic[d] : nullptr, P->fgroup, s);
+    if (rc) return -rc;
+  }
+  rc = plan_launch(P->nodes[d], P->meta[d], P->dec[d], P->nl[d], odd ? P->nl[d - 1] : nullptr, P->cur[d], P->cl[d],
+                   P->cr[d], P->nodes[d + 1], P->tp[d + 1], P->meta[d + 1], P->bp[d + 1], P->counters, P->scratch, d,
+                   P->D, P->min_w, P->caps[d + 1], P->leaf_cap, pr, s);
   if (rc) return -rc;
   if (P->ic_map && d + 1 < P->D) {
     rc = h2o_ic_next(P->nodes[d + 1], P->meta[d + 1], P->dec[d], P->ic[d], P->ic_map, P->F, P->ic[d + 1],
@@ -1951,14 +2008,18 @@ int h2o_tree_subtract(const TreePlan* P, int d, hipStream_t s) {
 }
 
 // after the last level: leaf_of_row (original order) + fp64 leaf sums (the caller all-reduces them when sharded)
-int h2o_tree_leaves(const TreePlan* P, hipStream_t s) {
+static int tree_leaves(const TreePlan* P, bool values, hipStream_t s) {
   int n_nodes = 0;
   for (int d = 0; d < P->D; ++d) n_nodes += P->caps[d];
-  return h2o_leaf_assign(P->master, P->stride, P->N, P->lvptrs, P->D, tp_aux(P, 2), tp_aux(P, 3), P->qs,
-                         P->leaf_of_row, P->leafq, P->leaf_cap, P->leafsum, n_nodes, P->planar, s);
+  const LeafVals lv{P->log_link, P->scale, P->kclamp, P->mx, P->leaf_lam, P->leaf_l1,
+                    values ? (float*)P->leafval : nullptr};
+  return leaf_assign_launch(P->master, P->stride, P->N, P->lvptrs, P->D, tp_aux(P, 2), tp_aux(P, 3), P->qs,
+                            P->leaf_of_row, P->leafq, P->leaf_cap, P->leafsum, n_nodes, P->planar, lv, s);
 }
 
-// single process: the whole tree (root .. leaves) in one host call
+int h2o_tree_leaves(const TreePlan* P, hipStream_t s) { return tree_leaves(P, false, s); }
+
+// single process: the whole tree (root .. leaves, and leaf_native values in the leaf-sum pass) in one host call
 int h2o_tree_all(const TreePlan* P, hipStream_t s) {
   TP_CHECK(h2o_tree_root(P, s));
   for (int d = 0; d < P->D; ++d) {
@@ -1966,11 +2027,7 @@ int h2o_tree_all(const TreePlan* P, hipStream_t s) {
     if (r < 0) return -r;
     if (r == 1) break;
   }
-  TP_CHECK(h2o_tree_leaves(P, s));
-  if (P->leaf_native)
-    return h2o_leaf_values(P->leafsum, P->leaf_cap, P->log_link, P->scale, P->kclamp, P->mx, P->leaf_lam, P->leaf_l1,
-                           P->leafval, s);
-  return 0;
+  return tree_leaves(P, P->leaf_native != 0, s);
 }
 #undef TP_CHECK
 

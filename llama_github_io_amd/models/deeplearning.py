@@ -403,6 +403,14 @@ class DeepLearningTrainer:
                     and ((cat in ("Binomial", "Multinomial") and dist in ("bernoulli", "multinomial")
                           and lname in ("automatic", "crossentropy", "cross_entropy"))
                          or (cat == "Regression" and dist == "gaussian" and lname in ("automatic", "quadratic"))))
+        from ..ops import dl as dlops
+        if explicit and p.get("reproducible"):
+            # reproducible=True (bit-identical seeded runs): the library-GEMM explicit step accumulates bias
+            # gradients with float atomics; only the fused step (fixed-order reductions) or autograd qualify
+            bf16 = dtype is not None and dev.type == "cuda"
+            if not (bf16 and os.environ.get("H2O_DL_FUSED", "1") == "1" and dlops.supported(
+                    int(Z.shape[1]), [int(h_) for h_ in hidden], int(net.out.weight.shape[0]), ACT[net.act], Z)):
+                explicit = False
         shadow = None
         if explicit:
             lins = list(net.hidden) + [net.out]
@@ -456,7 +464,6 @@ class DeepLearningTrainer:
         # Fused MFMA step (ops/dl.py, csrc/dl_kernels.hip): gather + forward + loss gradient + backward on
         # 16-row tiles with the activations in LDS, all weight gradients in one launch, fixed-order reduce.
         # Built per batch capacity in alloc(); the library-GEMM explicit step above stays for other shapes.
-        from ..ops import dl as dlops
         fz = dict(obj=None, ok=False, sridx=None)
         if (explicit and cdt == torch.bfloat16 and os.environ.get("H2O_DL_FUSED", "1") == "1"
                 and dlops.supported(int(Z.shape[1]), [int(h_) for h_ in hidden], int(net.out.weight.shape[0]),

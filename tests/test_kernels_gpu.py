@@ -507,3 +507,22 @@ def test_xgboost_fused_step_matches_torch_path(obj, extra):
     pf = mf._predict_tensor(X.cuda()).double().cpu()
     pt = mt._predict_tensor(X.cuda()).double().cpu()
     assert torch.allclose(pf, pt, rtol=2e-4, atol=2e-5), (pf - pt).abs().max()
+
+
+@pytest.mark.parametrize("hidden", [[16, 16], [7]])
+def test_deeplearning_reproducible_is_bit_identical(hidden):
+    """reproducible=True: two seeded runs give bit-identical models (the fused step's fixed-order
+    reductions, or autograd where the library-GEMM step would accumulate bias gradients atomically)."""
+    from llama_github_io_amd.models.base import DataInfo
+    from llama_github_io_amd.models.deeplearning import DeepLearningTrainer
+    g = torch.Generator(device=dev).manual_seed(4)
+    N, F = 20000, 12
+    X = torch.randn(F, N, device=dev, generator=g)
+    y = (X[0] - X[1] + 0.3 * torch.randn(N, device=dev, generator=g) > 0).float()
+    info = DataInfo([f"x{i}" for i in range(F)], np.zeros(F, np.int32), [None] * F, "y", ["0", "1"])
+    preds = []
+    for _ in range(2):
+        m = DeepLearningTrainer(dict(hidden=hidden, epochs=2, seed=7, reproducible=True, mini_batch_size=64,
+                                     score_interval=1e9)).fit(X, y, None, None, info)
+        preds.append(m.score_tensor(X).cpu())
+    assert torch.equal(preds[0], preds[1])
