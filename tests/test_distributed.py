@@ -301,3 +301,61 @@ def test_word2vec_sharded_text_trains_one_model():
     (_, v0, w0, a0, s0), (_, v1, w1, a1, s1) = out
     assert v0 == v1 and abs(s0 - s1) < 1e-6
     assert w0 > a0 + 0.3, (w0, a0)
+
+
+def _x2_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import torch
+    import torch.distributed as dist
+    from llama_github_io_amd.parallel import collectives as coll
+    from llama_github_io_amd.parallel.order_stats import order_statistics
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = torch.Generator().manual_seed(rank)
+        n = 50 + 37 * rank                             # uneven shards
+        v = torch.randn(n, generator=g, dtype=torch.float64)
+        ids = torch.arange(n, dtype=torch.float64) + 1000 * rank
+        # range partition by exact splitters (the isotonic / concordance pattern)
+        tot = int(coll.all_reduce_(torch.tensor([float(n)], dtype=torch.float64)).item())
+        spl = torch.tensor(order_statistics(v, [k * tot // world + 1 for k in range(1, world)]), dtype=torch.float64)
+        dest = torch.searchsorted(spl, v.contiguous(), right=True)
+        got = coll.exchange_rows(torch.stack([v, ids], 1), dest)
+        parts = coll.all_gather_object(got.tolist())
+        if rank == 0:
+            q.put(dict(parts=parts, spl=spl.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_exchange_rows_range_partition(world):
+    """collectives.exchange_rows (variable all-to-all): each row moves once, to the rank owning its key range;
+    rows arrive grouped by source rank in their original order; nothing is lost or duplicated."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_x2_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = q.get(timeout=300)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    parts, spl = out["parts"], out["spl"]
+    allrows = [r for part in parts for r in part]
+    assert len(allrows) == sum(50 + 37 * r for r in range(world))
+    assert len({r[1] for r in allrows}) == len(allrows)
+    for k, part in enumerate(parts):                   # rank k holds exactly the keys of range k
+        lo = -np.inf if k == 0 else spl[k - 1]
+        hi = np.inf if k == world - 1 else spl[k]
+        assert all(lo <= r[0] < hi for r in part)
+        src = [int(r[1]) // 1000 for r in part]
+        assert src == sorted(src)                       # grouped by source rank
+        for sr in set(src):
+            ids = [r[1] for r in part if int(r[1]) // 1000 == sr]
+            assert ids == sorted(ids)                   # source order kept
