@@ -13,6 +13,14 @@ ENGINE columns, column k holding the byte bin of the edge subset e[k::n]. With f
 "t <= 4(h' - 1) + k": the n columns together offer every threshold of the fine edges, their histograms are
 exact, and the uint8 engine (histograms, routing, leaf walk) runs unchanged. ``vmap`` maps engine columns to
 the original features (split decoding, column sampling, constraints, importances).
+
+Wide categoricals (``nbins_cats`` up to 1016 levels kept apart, H2O default 1024, ``SharedTreeModel.java:72``):
+a categorical with L > 254 bins spans n = ceil(L / 254) adjacent engine columns; column k holds the levels of
+bins [254k, 254k + L_k) as bins 0..L_k-1 and every other level in one "elsewhere" bin L_k (NA stays bin 255).
+No level is folded. Each column's subset split (bins sorted by mean response, DTree.java) treats the other
+blocks' levels as one unit, so the split family is the union of the per-block families — a subset of H2O's
+single sort over all L levels; the histograms and routing stay exact byte-bin operations. Decoding maps
+the column's bitset back through ``level_to_bin`` to a bitset over all L original levels.
 """
 from __future__ import annotations
 
@@ -104,11 +112,12 @@ def fit_binning(X: torch.Tensor, iscat, nlevels=None, max_bins: int = MAX_DATA_B
     Numeric edges are QuantilesGlobal cut points of a ~``sample``-row sample (all distinct values
     when there are at most ``max_bins``), computed on X's device: one batched sort of the sample,
     then per-feature distinct / quantile gathers; only the <=255 edges per feature reach the host.
-    ``max_cat_bins`` (nbins_cats, capped at 255): categoricals with more levels keep their most
-    frequent ``max_cat_bins - 1`` levels as bins and fold the rest into one shared bin.
+    ``max_cat_bins`` (nbins_cats, at most 1016): categoricals with more levels keep their most
+    frequent ``max_cat_bins - 1`` levels as bins and fold the rest into one shared bin; categoricals with
+    more than 254 bins are WIDE categoricals (module note).
     ``presampled``: X already is the (gathered) sample. ``max_bins`` above 255 (at most 1016) bins numeric
     features with more distinct values into several engine columns (module note)."""
-    cat_cap = int(min(max(2, max_cat_bins), NA_BIN))
+    cat_cap = int(min(max(2, max_cat_bins), WIDE_MAX_BINS))
     F, N = X.shape
     max_bins = int(min(max(2, max_bins), WIDE_MAX_BINS))
     iscat = np.asarray(iscat, dtype=np.int32)
@@ -162,20 +171,31 @@ def fit_binning(X: torch.Tensor, iscat, nlevels=None, max_bins: int = MAX_DATA_B
         edges.append(e)
         nbins[f] = e.size + 1
     vmap = None
-    if any(e is not None and e.size > SUB_EDGES for e in edges):
-        # wide features -> n adjacent engine columns with the interleaved edge subsets e[k::n]
+    wide_cat = [bool(iscat[f]) and nbins[f] > SUB_EDGES for f in range(F)]
+    if any(e is not None and e.size > SUB_EDGES for e in edges) or any(wide_cat):
+        # wide numeric features -> n adjacent engine columns with the interleaved edge subsets e[k::n];
+        # wide categoricals -> n adjacent engine columns of (at most) 254 consecutive bins each
         cols = []
         for f in range(F):
             e = edges[f]
+            if wide_cat[f]:
+                nb = int(nbins[f])
+                lb = np.arange(nlevels[f], dtype=np.int64) if l2b[f] is None else l2b[f]
+                n = -(-nb // SUB_EDGES)
+                for k in range(n):
+                    b0, nk = k * SUB_EDGES, min(SUB_EDGES, nb - k * SUB_EDGES)
+                    inb = (lb >= b0) & (lb < b0 + nk)
+                    cols.append((f, None, nk + 1, np.where(inb, lb - b0, nk)))
+                continue
             n = 1 if e is None or e.size <= SUB_EDGES else -(-e.size // SUB_EDGES)
             for k in range(n):
                 ek = e if n == 1 else np.ascontiguousarray(e[k::n])
-                cols.append((f, ek, (ek.size + 1) if e is not None else nbins[f]))
+                cols.append((f, ek, (ek.size + 1) if e is not None else nbins[f], l2b[f]))
         vmap = np.asarray([c[0] for c in cols], dtype=np.int32)
         edges = [c[1] for c in cols]
         nbins = np.asarray([c[2] for c in cols], dtype=np.int32)
         iscat, nlevels = iscat[vmap], nlevels[vmap]
-        l2b = [l2b[f] for f in vmap]
+        l2b = [c[3] for c in cols]
         F = len(cols)
     # rows of more than 12 features are padded to 16 B multiples so the partition kernel moves them
     # with 16-byte vector loads/stores (2 per 28-feature row instead of 7 dword pairs)
@@ -204,31 +224,36 @@ def apply_binning(b: Binning, X: torch.Tensor, planar: bool = False) -> torch.Te
     layout of the tree engine."""
     F, N = X.shape
     assert F == b.F_orig
-    Xc = X
-    if any(m is not None for m in b.level_to_bin):
-        Xc = X.clone()
-        for f, m in enumerate(b.level_to_bin):
-            if m is not None:
-                col = Xc[b.orig(f)]
-                ok = ~torch.isnan(col)
-                mt = torch.as_tensor(m, device=X.device, dtype=torch.float32)
-                codes = col[ok].long().clamp(0, m.size - 1)
-                col[ok] = mt[codes]
-    Xc = Xc.contiguous().float()
+    # source row of every engine column: its original feature, or (remapped categoricals: folded or
+    # wide-categorical blocks) an extra row holding the column's own level -> bin codes
+    src = [b.orig(f) for f in range(b.F)]
+    maps = [(f, m) for f, m in enumerate(b.level_to_bin or []) if m is not None]
+    if maps:
+        Xc = torch.empty(F + len(maps), N, dtype=torch.float32, device=X.device)
+        Xc[:F] = X
+        for i, (f, m) in enumerate(maps):
+            col = X[b.orig(f)]
+            mt = torch.as_tensor(m, device=X.device, dtype=torch.float32)
+            codes = torch.nan_to_num(col, nan=0.0).long().clamp(0, m.size - 1)
+            Xc[F + i] = torch.where(torch.isnan(col), col, mt[codes])
+            src[f] = F + i
+    else:
+        Xc = X.contiguous().float()
     if X.is_cuda:
         tab, ned, maxe = _edge_table(b, X.device)
         iscat = torch.from_numpy(b.iscat.astype(np.int32)).to(X.device)
         planar = bool(planar) and b.stride >= 64 and b.stride % 32 == 0
         out = (torch.empty(b.stride // 32, N, 32, dtype=torch.uint8, device=X.device) if planar
                else torch.empty(N, b.stride, dtype=torch.uint8, device=X.device))
-        xmap = None if b.vmap is None else torch.as_tensor(b.vmap, dtype=torch.int32, device=X.device)
+        xmap = (None if b.vmap is None and not maps
+                else torch.as_tensor(np.asarray(src, dtype=np.int32), dtype=torch.int32, device=X.device))
         nat.call("h2o_bin_assign", Xc.data_ptr(), N, b.F, b.stride, tab.data_ptr(), maxe, ned.data_ptr(),
                  iscat.data_ptr(), out.data_ptr(), int(planar), 0 if xmap is None else xmap.data_ptr(),
                  nat.stream_ptr(X.device))
         return out
     out = torch.zeros(N, b.stride, dtype=torch.uint8)
     for f in range(b.F):
-        col = Xc[b.orig(f)]
+        col = Xc[src[f]]
         nan = torch.isnan(col)
         if b.iscat[f]:
             code = torch.nan_to_num(col, nan=-1).long()

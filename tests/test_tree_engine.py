@@ -471,3 +471,90 @@ def test_gpu_wide_bins_match_reference(case):
         assert np.array_equal(dr["feat"], dg["feat"]) and np.array_equal(dr["bin"], dg["bin"])
         np.testing.assert_allclose(dr["wl"], dg["wl"], rtol=1e-6)
     assert torch.equal(ref.leaf_of_row, gb.leaf_of_row.cpu())
+
+
+def _wide_cat_data(N=30000, L=1000, seed=3, device="cpu"):
+    """A 1000-level categorical whose level set {l % 7 == 2} raises the response, next to numerics."""
+    g = torch.Generator().manual_seed(seed)
+    X = torch.randn(4, N, generator=g)
+    lv = torch.randint(0, L, (N,), generator=g)
+    X[2] = lv.float()
+    X[2, :150] = float("nan")
+    logit = X[0] - 0.5 * X[1] + 1.4 * ((lv % 7) == 2).float() - 0.6 * (lv >= 800).float() - 0.3
+    y = (torch.rand(N, generator=g) < torch.sigmoid(logit)).float()
+    iscat = np.array([0, 0, 1, 0], np.int32)
+    info = DataInfo(["a", "b", "c", "d"], iscat, [None, None, [f"L{i}" for i in range(L)], None], "y", ["0", "1"])
+    return X.to(device), y.to(device), info
+
+
+def test_wide_categorical_binning_keeps_every_level():
+    """nbins_cats = 1024 (SharedTreeModel.java:72): a 1000-level categorical is not folded; it spans 4 engine
+    columns of 254 consecutive levels, each with one 'elsewhere' bin for the other blocks' levels."""
+    X, y, info = _wide_cat_data()
+    b = fit_binning(X, info.iscat, info.nlevels, max_cat_bins=1024)
+    assert list(b.vmap) == [0, 1, 2, 2, 2, 2, 3]
+    assert [int(b.nbins[j]) for j in range(2, 6)] == [255, 255, 255, 239]
+    bins = apply_binning(b, X).long()
+    lv = torch.nan_to_num(X[2], nan=-1).long()
+    for k, j in enumerate(range(2, 6)):
+        nk = int(b.nbins[j]) - 1
+        inb = (lv >= 254 * k) & (lv < 254 * k + nk)
+        exp = torch.where(inb, lv - 254 * k, torch.full_like(lv, nk))
+        exp = torch.where(lv < 0, torch.full_like(lv, T.NA_BIN), exp)
+        assert torch.equal(bins[:, j], exp)
+    # every level keeps its own bin: exactly one column holds a row's level, the others say 'elsewhere'
+    own = sum(((bins[:, j] < int(b.nbins[j]) - 1)).long() for j in range(2, 6))
+    assert torch.equal(own, (lv >= 0).long())
+    # more levels than nbins_cats: the most frequent nbins_cats - 1 levels keep their bins (fold the rest)
+    bf = fit_binning(X, info.iscat, info.nlevels, max_cat_bins=300)
+    assert sum(int(bf.nbins[j]) - 1 for j in range(bf.F) if bf.orig(j) == 2) == 300
+
+
+def test_wide_categorical_gbm_decodes_to_level_sets():
+    """A GBM split on a wide categorical column decodes to a bitset over all 1000 original levels; scoring
+    raw rows through the decoded trees reproduces the training-time leaf values."""
+    X, y, info = _wide_cat_data()
+    m = GBMTrainer(dict(ntrees=3, max_depth=4, seed=1, nbins_cats=1024, min_rows=5)).fit(X, y, None, None, info)
+    trees = m.forest.trees
+    cat_nodes = [(t, i) for t in trees for i in range(len(t.feat)) if t.feat[i] == 2 and t.is_cat[i]]
+    assert cat_nodes, "the level-set signal should be split on"
+    for t, i in cat_nodes:
+        assert int(t.cat_nbits[i]) == 1000
+    auc = m.output["training_metrics"]["AUC"]
+    P = m.score_tensor(X)
+    assert P.shape == (X.shape[1], 2) and auc > 0.7
+    # level 2 (block 0) and level 2 + 7 * 40 = 282 (block 1) share the signal: the first wide-categorical
+    # split sends them the same way
+    t, i = cat_nodes[0]
+    bits = np.asarray(t.cat_bits[i])
+    side = lambda l: (bits[l >> 5] >> (l & 31)) & 1
+    same = [side(l) == side(2) for l in (9, 16, 23) if l < 254]
+    assert all(same)
+
+
+@pytest.mark.gpu
+def test_gpu_wide_categorical_matches_reference():
+    """1000-level categorical (4 engine columns) on the GPU engine vs RefTreeBuilder: identical decisions
+    (categorical bitsets included), left weights and leaf assignment."""
+    X, y, info = _wide_cat_data()
+    b = fit_binning(X, info.iscat, info.nlevels, max_cat_bins=1024)
+    bins = apply_binning(b, X)
+    g = y - 0.5
+    aux = torch.stack([torch.ones_like(y), g, g, torch.ones_like(y)], 1).contiguous()
+    p = T.SplitParams(min_w=10)
+    ref = T.RefTreeBuilder(bins, b.F, b.nbins, b.iscat, None, 5, p)
+    ref.set_feature_groups(b.vmap)
+    ref.build(aux, None, 0, seed=5, leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1]).float())
+    tl_r = ref.pop_levels()[0]
+    dev = torch.device("cuda", 0)
+    gb = T.GpuTreeBuilder(apply_binning(b, X.to(dev)), b.F, b.nbins, b.iscat, None, 5, p)
+    gb.set_feature_groups(b.vmap)
+    gb.build(aux.to(dev), None, 0, seed=5, leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1]).float())
+    tl_g = gb.pop_levels()[0]
+    assert tl_g.n_leaves == tl_r.n_leaves
+    assert any(int(f) in (2, 3, 4, 5) for d in tl_r.decs for f in d["feat"])
+    for dr, dg in zip(tl_r.decs, tl_g.decs):
+        assert np.array_equal(dr["feat"], dg["feat"]) and np.array_equal(dr["bin"], dg["bin"])
+        assert np.array_equal(dr["bits"], dg["bits"])
+        np.testing.assert_allclose(dr["wl"], dg["wl"], rtol=1e-6)
+    assert torch.equal(ref.leaf_of_row, gb.leaf_of_row.cpu())
