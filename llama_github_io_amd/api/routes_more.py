@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import glob
 import math
+import json
 import os
 import tempfile
 import time
@@ -609,7 +610,8 @@ def register(app, _params, _unquote, _model_json):
         name = name or dkv.new_key("nps")
         os.makedirs(nps_path(cat), exist_ok=True)
         with open(nps_path(cat, name), "w") as f:
-            f.write(str(p.get("value", "")))
+            v = p.get("value", "")      # JSON-looking values arrive parsed: store them as JSON text again
+            f.write(v if isinstance(v, str) else json.dumps(v))
         return {"__meta": v3.meta("NodePersistentStorageV3", "NodePersistentStorage"), "category": cat, "name": name}
 
     @app.delete("/3/NodePersistentStorage/{cat}/{name}")

@@ -869,6 +869,22 @@ def create_app(client_disconnect_timeout: float | None = None):
         return {"__meta": v3.meta("LeaderboardV99", "Leaderboard", 99), "project_name": pid,
                 "models": [v3.model_key(r["model_id"]) for r in rows], "table": table}
 
+    # ---- Flow web UI (h2o-web): the notebook page and its command layer (api/flow/)
+    flow_dir = os.path.join(os.path.dirname(os.path.abspath(__file__)), "flow")
+
+    @app.get("/")
+    def root():
+        from fastapi.responses import RedirectResponse
+        return RedirectResponse("/flow/index.html")
+
+    @app.get("/flow/{name}")
+    def flow_file(name: str):
+        path = os.path.join(flow_dir, os.path.basename(name))
+        if not os.path.isfile(path):
+            raise KeyError(f"no Flow file {name}")
+        media = "text/html" if name.endswith(".html") else "application/javascript"
+        return FileResponse(path, media_type=media)
+
     return app
 
 
