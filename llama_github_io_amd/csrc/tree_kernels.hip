@@ -252,8 +252,19 @@ struct RowFilter {
 // place them). The histogram loop then runs over full lane groups of selected rows: filtering inside it
 // left about half of each wave's lanes idle through the atomics (the loop is issue-bound), so a filtered
 // pass cost two plain passes. ftile-0 blocks also count the parent's left-goers (nl_out).
-__device__ __forceinline__ int filt_compact(const RowFilter& flt, int r0, int r1, int* lst, int* wcnt, int& lcnt) {
-  constexpr int NP = TILE / BLK;     // rows per thread (NW waves per block)
+#define FNP (TILE / BLK)   // FILT: rows per thread of a tile
+// split-feature bytes of this thread's rows of tile [r0, r1) (rows past r1 load row r1 - 1, unused)
+__device__ __forceinline__ void filt_load(const RowFilter& flt, int r0, int r1, unsigned (&byt)[FNP]) {
+#pragma unroll
+  for (int p = 0; p < FNP; ++p) {
+    const int row = min(r0 + p * BLK + (int)threadIdx.x, r1 - 1);
+    byt[p] = flt.fptr[(size_t)row * (size_t)flt.fstride];
+  }
+}
+
+__device__ __forceinline__ int filt_compact(const RowFilter& flt, int r0, int r1, int* lst, int* wcnt, int& lcnt,
+                                            const unsigned (&byt)[FNP]) {
+  constexpr int NP = FNP;            // rows per thread (NW waves per block)
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   bool sel[NP];
 #pragma unroll
@@ -261,7 +272,7 @@ __device__ __forceinline__ int filt_compact(const RowFilter& flt, int r0, int r1
     const int row = r0 + p * BLK + threadIdx.x;
     bool sl = false;
     if (row < r1) {
-      const bool gl = flt.left(flt.fptr[(size_t)row * (size_t)flt.fstride]);
+      const bool gl = flt.left((int)byt[p]);
       if (flt.count) lcnt += gl ? 1 : 0;
       sl = (gl ? 0 : 1) == flt.dir;
     }
@@ -401,6 +412,8 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
   RowFilter flt{&spd, bins, stride, 0, -1, 0, 0, 0, 0, false};
   int lcnt = 0;
   int cur = -1, since = 0, cur_parent = -1;
+  unsigned pre[FNP];                 // FILT: prefetched split bytes of tile pre_t
+  int pre_t = -1;
   bool acc = false;
   double wyy = 0.0;
   auto flush = [&]() {
@@ -447,7 +460,18 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
     since += r1 - r0;
     float wf = 0.f;
     if (FILT) {
-      const int S = filt_compact(flt, r0, r1, lst, wcnt, lcnt);
+      // the split bytes of this tile were prefetched during the previous tile's atomics when both tiles
+      // belong to the same node (the common case); a node change loads them here
+      if (pre_t != t) filt_load(flt, r0, r1, pre);
+      const int S = filt_compact(flt, r0, r1, lst, wcnt, lcnt, pre);
+      // prefetch the next tile's split bytes (same node: same filter) so their latency hides behind the atomics
+      const int rn0 = r0 + TILE, nend = nd.start + nd.len;
+      if (t + 1 < t1 && rn0 < nend) {
+        filt_load(flt, rn0, min(rn0 + TILE, nend), pre);
+        pre_t = t + 1;
+      } else {
+        pre_t = -1;
+      }
       hist_rows<FILT, PACKED>(h, nayy, bins32, aw, ay, W, wabs, Fl, j == 0 && ftile == 0, 0, S, g, j, wf, sa, sb,
                               sp, lst);
     } else {
