@@ -137,7 +137,8 @@ __device__ void block_sum4(double v[4], double* scratch /* >= 4*(BLK/64) */) {
 // nayy (fp32 NA-bin wYY, rare) follows the planes.
 #define HPLANE (NBIN * FTILE + 16)
 #define HIST_LDS_BYTES (2 * HPLANE * 8 + FTILE * 4)
-#define HIST_LDS_TAIL (64 * 8 + TILE * 4 + 2 * (TILE / BLK) * (BLK / 64) * 4)   // red + FILT row list + counts
+#define WQCAP 192   // FILT: per-wave queue of selected rows (< 64 carried over + one tile's 128 rows)
+#define HIST_LDS_TAIL (64 * 8 + (BLK / 64) * WQCAP * 4)   // red + FILT per-wave row queues
 __device__ __forceinline__ int fslot(int fl) { return (fl & 16) | ((fl + ((fl >> 4) << 1)) & 15); }
 
 __device__ __forceinline__ void lds_zero64(long long* h, int n) {
@@ -252,46 +253,49 @@ struct RowFilter {
 // place them). The histogram loop then runs over full lane groups of selected rows: filtering inside it
 // left about half of each wave's lanes idle through the atomics (the loop is issue-bound), so a filtered
 // pass cost two plain passes. ftile-0 blocks also count the parent's left-goers (nl_out).
-#define FNP (TILE / BLK)   // FILT: rows per thread of a tile
-// split-feature bytes of this thread's rows of tile [r0, r1) (rows past r1 load row r1 - 1, unused)
+// orders LDS accesses of different lanes of one wave (compiler and hardware), without a block barrier
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+#define FNP (TILE / BLK)   // FILT: rows per lane of a tile
+#define WROWS (TILE / NW)   // FILT: rows of a tile per wave (a contiguous 128-row slice)
+// split-feature bytes of this lane's rows of its wave's slice of tile [r0, r1) (rows past r1 load row r1 - 1,
+// unused)
 __device__ __forceinline__ void filt_load(const RowFilter& flt, int r0, int r1, unsigned (&byt)[FNP]) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
   for (int p = 0; p < FNP; ++p) {
-    const int row = min(r0 + p * BLK + (int)threadIdx.x, r1 - 1);
+    const int row = min(r0 + wv * WROWS + p * 64 + lane, r1 - 1);
     byt[p] = flt.fptr[(size_t)row * (size_t)flt.fstride];
   }
 }
 
-__device__ __forceinline__ int filt_compact(const RowFilter& flt, int r0, int r1, int* lst, int* wcnt, int& lcnt,
-                                            const unsigned (&byt)[FNP]) {
-  constexpr int NP = FNP;            // rows per thread (NW waves per block)
+// WAVE-LOCAL compaction (no block barrier): the wave appends the rows of its tile slice that the parent's
+// decision sends to the built child to its own LDS queue wq (ascending), after the qn rows still queued.
+// MEASURED before (block-wide list, two __syncthreads per tile): every wave waited on the slowest wave's
+// split-byte loads and then on the gathers, with nothing to overlap them — the filtered pass over half the
+// rows cost as much as a plain pass over all of them.
+__device__ __forceinline__ int filt_append(const RowFilter& flt, int r0, int r1, int* wq, int qn, int& lcnt,
+                                           const unsigned (&byt)[FNP]) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  bool sel[NP];
+  const unsigned long long below = (1ull << lane) - 1ull;
 #pragma unroll
-  for (int p = 0; p < NP; ++p) {
-    const int row = r0 + p * BLK + threadIdx.x;
+  for (int p = 0; p < FNP; ++p) {
+    const int row = r0 + wv * WROWS + p * 64 + lane;
     bool sl = false;
     if (row < r1) {
       const bool gl = flt.left((int)byt[p]);
       if (flt.count) lcnt += gl ? 1 : 0;
       sl = (gl ? 0 : 1) == flt.dir;
     }
-    sel[p] = sl;
     const unsigned long long m = __ballot(sl);
-    if (lane == 0) wcnt[p * NW + wv] = __popcll(m);
+    if (sl) wq[qn + __popcll(m & below)] = row;
+    qn += __popcll(m);
   }
-  __syncthreads();
-  int S = 0;
-#pragma unroll
-  for (int p = 0; p < NP; ++p) {
-    const unsigned long long m = __ballot(sel[p]);
-    int base = 0;
-    for (int k = 0; k < p * NW + wv; ++k) base += wcnt[k];
-    if (sel[p]) lst[base + __popcll(m & ((1ull << lane) - 1ull))] = r0 + p * BLK + threadIdx.x;
-  }
-  for (int k = 0; k < NP * NW; ++k) S += wcnt[k];
-  __syncthreads();
-  return S;
+  return qn;
 }
 
 #define UNR 8   // hist: rows per lane group loaded before any atomic (8 independent loads per lane)
@@ -303,7 +307,7 @@ __device__ __forceinline__ int filt_compact(const RowFilter& flt, int r0, int r1
 // within 1.5 %), so everything per-lane is hoisted: the 4 feature slots and byte shifts of the lane's word
 // (rotated by row parity, see the layout note), feature validity, and an all-bytes NA test per word; the
 // common row is then bfe + lshl_add + ds_add_u64 per feature (two atomics when not PACKED).
-template <bool FILT, bool PACKED>
+template <bool FILT, bool PACKED, int GR = RPI>
 __device__ __forceinline__ void hist_rows(long long* h, float* nayy, const unsigned* __restrict__ bins32,
                                           const float* __restrict__ aw, const float* __restrict__ ay, int W, int wabs,
                                           int F, bool lead, int r0, int r1, int g, int j, float& wyy, float sa,
@@ -321,14 +325,14 @@ __device__ __forceinline__ void hist_rows(long long* h, float* nayy, const unsig
   const bool full = vmask == 0xFFFFFFFFu;
   const int wc = min(wabs, W - 1);
   unsigned long long* H = (unsigned long long*)h;
-  for (int base = r0; base < r1; base += RPI * UNR) {
+  for (int base = r0; base < r1; base += GR * UNR) {
     unsigned wd[UNR];
     float2 ab[UNR];
     // unconditional loads (rows clamped into the node, words into the row): no exec-mask branches here;
     // rows past r1 are skipped below, invalid words have vmask == 0
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
-      const int idx = min(base + g + u * RPI, r1 - 1);
+      const int idx = min(base + g + u * GR, r1 - 1);
       const size_t row = FILT ? (size_t)lst[idx] : (size_t)idx;
       // SoA aux planes: wY always, w only when rows are weighted (aw == null: unit weights)
       ab[u] = make_float2(aw ? aw[row] : 1.f, ay[row]);
@@ -336,7 +340,7 @@ __device__ __forceinline__ void hist_rows(long long* h, float* nayy, const unsig
     }
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
-      const int idx = base + g + u * RPI;
+      const int idx = base + g + u * GR;
       if (idx >= r1) continue;
       if (lead) wyy += row_yy(ab[u].x, ab[u].y);
       if (vmask == 0u) continue;
@@ -387,8 +391,8 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
   long long* h = smem64;                                 // 2 planes (PACKED: 1 -> two blocks per CU fit)
   float* nayy = (float*)(smem64 + (PACKED ? 1 : 2) * HPLANE);   // FTILE
   double* red = (double*)(nayy + FTILE);                 // 64 doubles scratch
-  int* lst = (int*)(red + 64);                           // FILT: the tile's selected rows (TILE)
-  int* wcnt = lst + TILE;                                // FILT: per (pass, wave) selected counts
+  const int lane = threadIdx.x & 63;
+  int* wq = (int*)(red + 64) + (threadIdx.x >> 6) * WQCAP;   // FILT: this wave's queue of selected rows
 
   // tile_prefix here is the BUILD-tile prefix (only nodes with build=1 own tiles) and meta[2] the number
   // of build tiles: blocks split only the rows that are histogrammed (no idle blocks on skipped siblings)
@@ -414,9 +418,23 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
   int cur = -1, since = 0, cur_parent = -1;
   unsigned pre[FNP];                 // FILT: prefetched split bytes of tile pre_t
   int pre_t = -1;
+  int qn = 0;                        // FILT: rows in this wave's queue (wave-uniform)
   bool acc = false;
   double wyy = 0.0;
+  // FILT: histogram the wave's queued rows of the current node (before its LDS histogram is flushed)
+  auto drain = [&]() {
+    if (FILT && qn > 0) {
+      float wf2 = 0.f;
+      wave_sync_lds();
+      hist_rows<FILT, PACKED, 8>(h, nayy, bins32, aw, ay, W, wabs, Fl, j == 0 && ftile == 0, 0, qn, lane >> 3, j, wf2,
+                                 sa, sb, sp, wq);
+      wyy += (double)wf2;
+      qn = 0;
+      wave_sync_lds();
+    }
+  };
   auto flush = [&]() {
+    drain();
     double v[4] = {wyy, (double)lcnt, 0, 0};
     block_sum4(v, red);
     __syncthreads();
@@ -463,7 +481,7 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
       // the split bytes of this tile were prefetched during the previous tile's atomics when both tiles
       // belong to the same node (the common case); a node change loads them here
       if (pre_t != t) filt_load(flt, r0, r1, pre);
-      const int S = filt_compact(flt, r0, r1, lst, wcnt, lcnt, pre);
+      qn = filt_append(flt, r0, r1, wq, qn, lcnt, pre);
       // prefetch the next tile's split bytes (same node: same filter) so their latency hides behind the atomics
       const int rn0 = r0 + TILE, nend = nd.start + nd.len;
       if (t + 1 < t1 && rn0 < nend) {
@@ -472,8 +490,19 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
       } else {
         pre_t = -1;
       }
-      hist_rows<FILT, PACKED>(h, nayy, bins32, aw, ay, W, wabs, Fl, j == 0 && ftile == 0, 0, S, g, j, wf, sa, sb,
-                              sp, lst);
+      // full 64-row batches of the wave's queue (8 lane groups x UNR rows); the rest waits for the next tile
+      // of this node (or the drain before the flush)
+      while (qn >= 64) {
+        wave_sync_lds();
+        hist_rows<FILT, PACKED, 8>(h, nayy, bins32, aw, ay, W, wabs, Fl, j == 0 && ftile == 0, 0, 64, lane >> 3, j, wf,
+                                   sa, sb, sp, wq);
+        const int rest = qn - 64;                        // <= 127: move to the queue front (no lane overlap)
+        wave_sync_lds();
+        const int v0 = lane < rest ? wq[64 + lane] : 0, v1 = lane + 64 < rest ? wq[128 + lane] : 0;
+        if (lane < rest) wq[lane] = v0;
+        if (lane + 64 < rest) wq[64 + lane] = v1;
+        qn = rest;
+      }
     } else {
       hist_rows<FILT, PACKED>(h, nayy, bins32, aw, ay, W, wabs, Fl, j == 0 && ftile == 0, r0, r1, g, j, wf, sa, sb,
                               sp, nullptr);

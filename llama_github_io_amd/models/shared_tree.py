@@ -185,6 +185,10 @@ class SharedTreeTrainer:
     def _trees_per_iter(self) -> int:
         return 1
 
+    # H2O's SharedTree binning: nbins_top_level root resolution for the adaptive histogram types
+    # (XGBoost bins by its own max_bins instead)
+    _adaptive_top_level = True
+
     # ---- main
     def fit(self, X, y, w, offset, info: DataInfo, valid=None, model_key=None) -> SharedTreeModel:
         t_start = time.time()
@@ -202,7 +206,8 @@ class SharedTreeTrainer:
         # ---- binning (QuantilesGlobal on the whole training set, shared by every tree)
         max_bins = int(min(255, max(int(p.get("max_bins") or 255), 2)))
         ht_ = str(p.get("histogram_type", "AUTO")).lower().replace("_", "")
-        if ht_ in ("auto", "uniformadaptive", "random", "roundrobin", "uniformrobust") and "nbins_top_level" in p:
+        if (self._adaptive_top_level and ht_ in ("auto", "uniformadaptive", "random", "roundrobin", "uniformrobust")
+                and "nbins_top_level" in p):
             # DHistogram's root resolution: nbins_top_level (default 1024) bins; above 255 the numeric
             # features are binned wide (several engine columns each, ops/binning.py)
             max_bins = int(min(WIDE_MAX_BINS, max(int(p.get("nbins_top_level") or 1024), int(p.get("nbins") or 20))))

@@ -116,6 +116,9 @@ class XGBoostTrainer(SharedTreeTrainer):
         p = _alias(p)
         super().__init__(p)
 
+    # xgboost's hist bins come from max_bins alone (H2O's nbins_top_level is not an XGBoost parameter)
+    _adaptive_top_level = False
+
     def _split_params(self):
         p = self.p
         return T.SplitParams(min_w=float(p["min_rows"]), min_split_improvement=0.0, lam=float(p["reg_lambda"]),
