@@ -63,6 +63,9 @@ def main():
     ap.add_argument("--rows", type=int, default=11_000_000)
     ap.add_argument("--depth", type=int, default=6)
     ap.add_argument("--no-job", action="store_true", help="skip the whole 100-tree job measurement")
+    ap.add_argument("--histogram-type", default="QuantilesGlobal",
+                    help="H2O histogram_type (the headline config is QuantilesGlobal; AUTO = UniformAdaptive with "
+                    "nbins_top_level=1024, H2O's default)")
     ap.add_argument("--backend", default=None, help="torch.distributed backend (default: nccl = RCCL on GPUs, gloo on CPU)")
     ap.add_argument("--device", default=None, help="cuda | cpu (default: cuda when available); cpu runs the "
                     "reference builder, for multi-rank rehearsals of the collective protocol")
@@ -98,7 +101,7 @@ def main():
     F = X.shape[0]
     info = DataInfo([f"x{i}" for i in range(F)], np.zeros(F, np.int32), [None] * F, "y", ["0", "1"])
     params = dict(ntrees=args.warmup + args.steps, max_depth=args.depth, min_rows=10, learn_rate=0.1, seed=42,
-                  distribution="bernoulli", histogram_type="QuantilesGlobal")
+                  distribution="bernoulli", histogram_type=args.histogram_type)
 
     # the trainer exposes a per-tree hook so the bench can time exactly K steps after W warmup steps
     times = {}
@@ -158,7 +161,8 @@ def main():
             "value": round(rows_per_sec, 1), "unit": "rows/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "fp32", "data": "synthetic HIGGS-shaped 11M x 28",
-            "config": {"model": "GBM bernoulli ntrees=100 max_depth=6 min_rows=10 lr=0.1 QuantilesGlobal(255 bins)",
+            "config": {"model": "GBM bernoulli ntrees=100 max_depth=6 min_rows=10 lr=0.1 " + (
+                           "QuantilesGlobal(255 bins)" if args.histogram_type == "QuantilesGlobal" else args.histogram_type),
                        "global_batch": n_total, "seq_len": None, "parallelism": f"dp{world} (row-sharded, hist all-reduce)",
                        "rows": n_total, "features": F, "train_auc_after_all_trees": tm.get("AUC") if tm else None,
                        "collectives_per_tree": round(comm["calls"] / args.steps, 2),
