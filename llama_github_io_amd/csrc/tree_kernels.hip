@@ -1375,29 +1375,18 @@ __global__ __launch_bounds__(256) void k_leaf_assign(
   }
   __syncthreads();
   const float sn = (float)qs[6], sd = (float)qs[7];
-  // software-pipelined: the next row's bins and statistics are loaded before this row's walk (one row per
-  // thread in flight left the walk latency-bound: 11M rows in 110 us, ~4.2 TB/s)
-  const long long rstep = (long long)gridDim.x * blockDim.x;
-  auto load_row = [&](long long r, uint4& w0, uint4& w1, uint4& w2, uint4& w3, float& xn, float& xd) {
+  for (long long row = (long long)blockIdx.x * blockDim.x + threadIdx.x; row < N;
+       row += (long long)gridDim.x * blockDim.x) {
+    uint4 v0 = make_uint4(0u, 0u, 0u, 0u), v1 = v0, v2 = v0, v3 = v0;
     if (NV > 0) {
-      const uint4* s4 = (const uint4*)(bins + (planar ? (size_t)r * 32 : (size_t)r * stride));
-      const uint4* s4b = planar ? (const uint4*)(bins + ((size_t)N + r) * 32) : s4 + 2;
-      w0 = s4[0];
-      if (NV > 1) w1 = s4[1];
-      if (NV > 2) w2 = s4b[0];
-      if (NV > 3) w3 = s4b[1];
+      const uint4* s4 = (const uint4*)(bins + (planar ? (size_t)row * 32 : (size_t)row * stride));
+      const uint4* s4b = planar ? (const uint4*)(bins + ((size_t)N + row) * 32) : s4 + 2;
+      v0 = s4[0];
+      if (NV > 1) v1 = s4[1];
+      if (NV > 2) v2 = s4b[0];
+      if (NV > 3) v3 = s4b[1];
     }
-    xn = an[r];
-    xd = ad[r];
-  };
-  long long row = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  uint4 v0 = make_uint4(0u, 0u, 0u, 0u), v1 = v0, v2 = v0, v3 = v0;
-  float a_n = 0.f, a_d = 0.f;
-  if (row < N) load_row(row, v0, v1, v2, v3, a_n, a_d);
-  for (; row < N; row += rstep) {
-    uint4 n0 = make_uint4(0u, 0u, 0u, 0u), n1 = n0, n2 = n0, n3 = n0;
-    float nn = 0.f, nd = 0.f;
-    if (row + rstep < N) load_row(row + rstep, n0, n1, n2, n3, nn, nd);
+    const float a_n = an[row], a_d = ad[row];    // issued before the walk: latency overlaps it
     int i = 0, leaf = 0;
     for (int d = 0; d < D; ++d) {
       int c;
@@ -1438,7 +1427,6 @@ __global__ __launch_bounds__(256) void k_leaf_assign(
       if (qn) atomicAdd(lq + 2 * leaf, (unsigned long long)qn);
       if (qd) atomicAdd(lq + 2 * leaf + 1, (unsigned long long)qd);
     }
-    v0 = n0; v1 = n1; v2 = n2; v3 = n3; a_n = nn; a_d = nd;
   }
   if (lds) {
     __syncthreads();
