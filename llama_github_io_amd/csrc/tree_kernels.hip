@@ -307,24 +307,31 @@ __device__ __forceinline__ int filt_append(const RowFilter& flt, int r0, int r1,
 // within 1.5 %), so everything per-lane is hoisted: the 4 feature slots and byte shifts of the lane's word
 // (rotated by row parity, see the layout note), feature validity, and an all-bytes NA test per word; the
 // common row is then bfe + lshl_add + ds_add_u64 per feature (two atomics when not PACKED).
-template <bool FILT, bool PACKED, int GR = RPI>
+template <bool FILT, bool PACKED, bool UNIT, int GR = RPI>
 __device__ __forceinline__ void hist_rows(long long* h, float* nayy, const unsigned* __restrict__ bins32,
                                           const float* __restrict__ aw, const float* __restrict__ ay, int W, int wabs,
                                           int F, bool lead, int r0, int r1, int g, int j, float& wyy, float sa,
                                           float sb, float sp, const int* lst) {
   const int rot = g & 1;
-  int off[4], sh[4];
+  unsigned offb[4], sh[4];           // byte offset of the lane's feature slot in a bin row; its byte's shift
   unsigned vmask = 0u;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int kk = (k + rot) & 3;
-    off[k] = fslot(j * 4 + kk);
-    sh[k] = 8 * kk;
+    offb[k] = (unsigned)fslot(j * 4 + kk) * 8u;
+    sh[k] = 8u * kk;
     if (wabs < W && wabs * 4 + kk < F) vmask |= 0xFFu << (8 * kk);
   }
   const bool full = vmask == 0xFFFFFFFFu;
   const int wc = min(wabs, W - 1);
-  unsigned long long* H = (unsigned long long*)h;
+  char* Hb = (char*)h;
+  // entry (bin, slot) at byte (bin * FTILE + slot) * 8 = (bin << 8) + offb: one v_bfe_u32 + one v_lshl_add_u32
+  // per atomic (MEASURED: the shift / and / shift / add form the compiler made of the index expression was 4 VALU
+  // per atomic, and this loop is VALU-issue bound: ~12 VALU per LDS instruction in rocprofv3 PMC)
+  static_assert(FTILE * 8 == 256, "bin row of the LDS histogram is 256 bytes");
+  auto ent = [&](unsigned w, int k) -> unsigned long long* {
+    return (unsigned long long*)(Hb + ((__builtin_amdgcn_ubfe(w, sh[k], 8) << 8) + offb[k]));
+  };
   for (int base = r0; base < r1; base += GR * UNR) {
     unsigned wd[UNR];
     float2 ab[UNR];
@@ -335,16 +342,18 @@ __device__ __forceinline__ void hist_rows(long long* h, float* nayy, const unsig
       const int idx = min(base + g + u * GR, r1 - 1);
       const size_t row = FILT ? (size_t)lst[idx] : (size_t)idx;
       // SoA aux planes: wY always, w only when rows are weighted (aw == null: unit weights)
-      ab[u] = make_float2(aw ? aw[row] : 1.f, ay[row]);
+      ab[u] = make_float2(UNIT ? 1.f : (aw ? aw[row] : 1.f), ay[row]);
       wd[u] = bins32[row * W + wc];
     }
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
       const int idx = base + g + u * GR;
       if (idx >= r1) continue;
-      if (lead) wyy += row_yy(ab[u].x, ab[u].y);
+      // UNIT (packed, every row weight exactly 1): constant count part, yy = wY^2 (no reciprocal)
+      if (lead) wyy += UNIT ? ab[u].y * ab[u].y : row_yy(ab[u].x, ab[u].y);
       if (vmask == 0u) continue;
-      const long long qa = PACKED ? qpack(ab[u].x, ab[u].y, sp) : q64(ab[u].x, sa);
+      const long long qa = UNIT ? (1ll << PACK_SHIFT) + (long long)__float2int_rz(ab[u].y * sp)
+                                : PACKED ? qpack(ab[u].x, ab[u].y, sp) : q64(ab[u].x, sa);
       const long long qb = PACKED ? 0ll : q64(ab[u].y, sb);
       const unsigned w = wd[u];
       const unsigned x = ~w | ~vmask;                     // a zero byte of x = an NA bin of a valid feature
@@ -352,17 +361,17 @@ __device__ __forceinline__ void hist_rows(long long* h, float* nayy, const unsig
       if (full && !has_na) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          unsigned long long* p = H + (((w >> sh[k]) & 0xFFu) * FTILE + off[k]);
+          unsigned long long* p = ent(w, k);
           atomicAdd(p, (unsigned long long)qa);
           if (!PACKED) atomicAdd(p + HPLANE, (unsigned long long)qb);
         }
       } else {
-        const float yy = row_yy(ab[u].x, ab[u].y);
+        const float yy = UNIT ? ab[u].y * ab[u].y : row_yy(ab[u].x, ab[u].y);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           if (!((vmask >> sh[k]) & 1u)) continue;
-          const unsigned bin = (w >> sh[k]) & 0xFFu;
-          unsigned long long* p = H + (bin * FTILE + off[k]);
+          const unsigned bin = __builtin_amdgcn_ubfe(w, sh[k], 8);
+          unsigned long long* p = ent(w, k);
           atomicAdd(p, (unsigned long long)qa);
           if (!PACKED) atomicAdd(p + HPLANE, (unsigned long long)qb);
           if (bin == NA_BIN) atomicAdd(nayy + j * 4 + (sh[k] >> 3), yy);
@@ -378,7 +387,7 @@ __device__ __forceinline__ void hist_rows(long long* h, float* nayy, const unsig
 // (deterministic, no global atomics). grid = (G, n_ftiles); each block takes a contiguous tile range.
 // FILT (odd levels): a node's tiles cover its PARENT's rows; only rows the parent's decision sends to
 // this child are accumulated, and ftile-0 blocks add the parent's left-going row count to nl_out.
-template <bool FILT, bool PACKED>
+template <bool FILT, bool PACKED, bool UNIT = false>
 __global__ __launch_bounds__(BLK) void k_hist_build(
     const uint8_t* __restrict__ bins, int stride /*bytes per row, multiple of 4*/,
     const float* __restrict__ aw /*row weights or null (unit)*/, const float* __restrict__ ay /*w * Y*/,
@@ -426,7 +435,7 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
     if (FILT && qn > 0) {
       float wf2 = 0.f;
       wave_sync_lds();
-      hist_rows<FILT, PACKED, 8>(h, nayy, bins32, aw, ay, W, wabs, Fl, j == 0 && ftile == 0, 0, qn, lane >> 3, j, wf2,
+      hist_rows<FILT, PACKED, UNIT, 8>(h, nayy, bins32, aw, ay, W, wabs, Fl, j == 0 && ftile == 0, 0, qn, lane >> 3, j, wf2,
                                  sa, sb, sp, wq);
       wyy += (double)wf2;
       qn = 0;
@@ -494,7 +503,7 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
       // of this node (or the drain before the flush)
       while (qn >= 64) {
         wave_sync_lds();
-        hist_rows<FILT, PACKED, 8>(h, nayy, bins32, aw, ay, W, wabs, Fl, j == 0 && ftile == 0, 0, 64, lane >> 3, j, wf,
+        hist_rows<FILT, PACKED, UNIT, 8>(h, nayy, bins32, aw, ay, W, wabs, Fl, j == 0 && ftile == 0, 0, 64, lane >> 3, j, wf,
                                    sa, sb, sp, wq);
         const int rest = qn - 64;                        // <= 127: move to the queue front (no lane overlap)
         wave_sync_lds();
@@ -504,7 +513,7 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
         qn = rest;
       }
     } else {
-      hist_rows<FILT, PACKED>(h, nayy, bins32, aw, ay, W, wabs, Fl, j == 0 && ftile == 0, r0, r1, g, j, wf, sa, sb,
+      hist_rows<FILT, PACKED, UNIT>(h, nayy, bins32, aw, ay, W, wabs, Fl, j == 0 && ftile == 0, r0, r1, g, j, wf, sa, sb,
                               sp, nullptr);
     }
     wyy += (double)wf;
@@ -1648,18 +1657,18 @@ __global__ void k_leaf_values(const double* __restrict__ leafsum, int n, int log
 
 // ================================================================================================
 // C ABI launchers (called through ctypes with raw device pointers and the current HIP stream).
-template <bool PACKED>
+template <bool PACKED, bool UNIT = false>
 static void launch_hist(dim3 grid, size_t lds, hipStream_t s, const void* bins, int stride, const void* aw,
                         const void* ay, const void* nodes, const void* tile_prefix, const void* meta, int F,
                         void* partials, int slot_doubles, const void* qs, const void* pdec, void* nl_out, int f32,
                         long long N, int planar) {
   if (pdec)
-    hipLaunchKernelGGL((k_hist_build<true, PACKED>), grid, dim3(BLK), lds, s, (const uint8_t*)bins, stride,
+    hipLaunchKernelGGL((k_hist_build<true, PACKED, UNIT>), grid, dim3(BLK), lds, s, (const uint8_t*)bins, stride,
                        (const float*)aw, (const float*)ay, (const Node*)nodes, (const int*)tile_prefix,
                        (const int*)meta, F, (double*)partials, slot_doubles, (const double*)qs, (const Dec*)pdec,
                        (int*)nl_out, f32, N, planar);
   else
-    hipLaunchKernelGGL((k_hist_build<false, PACKED>), grid, dim3(BLK), lds, s, (const uint8_t*)bins, stride,
+    hipLaunchKernelGGL((k_hist_build<false, PACKED, UNIT>), grid, dim3(BLK), lds, s, (const uint8_t*)bins, stride,
                        (const float*)aw, (const float*)ay, (const Node*)nodes, (const int*)tile_prefix,
                        (const int*)meta, F, (double*)partials, slot_doubles, (const double*)qs, (const Dec*)nullptr,
                        (int*)nullptr, f32, N, planar);
@@ -1687,7 +1696,9 @@ int h2o_hist_build(const void* bins, int stride, const void* aw, const void* ay,
   // packed mode needs one int64 plane (66 KB): two 16-wave blocks share a CU (32 waves, 8 per SIMD)
   const size_t lds = (packed ? HIST_LDS_BYTES - HPLANE * 8 : HIST_LDS_BYTES) + HIST_LDS_TAIL;
   const dim3 gr(grid, nft);
-  if (packed) launch_hist<true>(gr, lds, s, bins, stride, aw, ay, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out, f32, N, planar);
+  if (packed && aw == nullptr)   // unit row weights (the trainer dropped the w plane)
+    launch_hist<true, true>(gr, lds, s, bins, stride, aw, ay, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out, f32, N, planar);
+  else if (packed) launch_hist<true>(gr, lds, s, bins, stride, aw, ay, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out, f32, N, planar);
   else launch_hist<false>(gr, lds, s, bins, stride, aw, ay, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out, f32, N, planar);
   return (int)hipGetLastError();
 }
