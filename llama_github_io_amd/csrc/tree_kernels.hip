@@ -311,7 +311,7 @@ template <bool FILT, bool PACKED, bool UNIT, int GR = RPI>
 __device__ __forceinline__ void hist_rows(long long* h, float* nayy, const unsigned* __restrict__ bins32,
                                           const float* __restrict__ aw, const float* __restrict__ ay, int W, int wabs,
                                           int F, bool lead, int r0, int r1, int g, int j, float& wyy, float sa,
-                                          float sb, float sp, const int* lst) {
+                                          float sb, float sp, const int* lst, bool no_na) {
   const int rot = g & 1;
   unsigned offb[4], sh[4];           // byte offset of the lane's feature slot in a bin row; its byte's shift
   unsigned vmask = 0u;
@@ -357,7 +357,7 @@ __device__ __forceinline__ void hist_rows(long long* h, float* nayy, const unsig
       const long long qb = PACKED ? 0ll : q64(ab[u].y, sb);
       const unsigned w = wd[u];
       const unsigned x = ~w | ~vmask;                     // a zero byte of x = an NA bin of a valid feature
-      const bool has_na = ((x - 0x01010101u) & ~x & 0x80808080u) != 0u;
+      const bool has_na = !no_na && ((x - 0x01010101u) & ~x & 0x80808080u) != 0u;
       if (full && !has_na) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -413,6 +413,8 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
   // (MEASURED: an XCD-aware 1-D order putting the feature-tile blocks of one row range on the same XCD
   // made XGBoost 100M x 50 histograms 9-20 % SLOWER — 4.56 -> 4.97 ms filtered, 2.32 -> 2.80 ms plain)
   const int ftile = blockIdx.y;
+  const bool no_na = (planar >> 1) & 1;   // launch flag bit 1: no NA bin in the bins (skip the per-word test)
+  planar &= 1;
   // planar: this block reads only its 32-feature plane (8 words per row, features counted from the plane)
   const int W = planar ? LPR : stride >> 2;
   const int g = threadIdx.x / LPR, j = threadIdx.x % LPR;
@@ -436,7 +438,7 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
       float wf2 = 0.f;
       wave_sync_lds();
       hist_rows<FILT, PACKED, UNIT, 8>(h, nayy, bins32, aw, ay, W, wabs, Fl, j == 0 && ftile == 0, 0, qn, lane >> 3, j, wf2,
-                                 sa, sb, sp, wq);
+                                 sa, sb, sp, wq, no_na);
       wyy += (double)wf2;
       qn = 0;
       wave_sync_lds();
@@ -504,7 +506,7 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
       while (qn >= 64) {
         wave_sync_lds();
         hist_rows<FILT, PACKED, UNIT, 8>(h, nayy, bins32, aw, ay, W, wabs, Fl, j == 0 && ftile == 0, 0, 64, lane >> 3, j, wf,
-                                   sa, sb, sp, wq);
+                                   sa, sb, sp, wq, no_na);
         const int rest = qn - 64;                        // <= 127: move to the queue front (no lane overlap)
         wave_sync_lds();
         const int v0 = lane < rest ? wq[64 + lane] : 0, v1 = lane + 64 < rest ? wq[128 + lane] : 0;
@@ -514,7 +516,7 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
       }
     } else {
       hist_rows<FILT, PACKED, UNIT>(h, nayy, bins32, aw, ay, W, wabs, Fl, j == 0 && ftile == 0, r0, r1, g, j, wf, sa, sb,
-                              sp, nullptr);
+                              sp, nullptr, no_na);
     }
     wyy += (double)wf;
   }
@@ -1959,7 +1961,8 @@ struct TreePlan {
   int sliced, fs0, fsn, sslot;
   void *cand_local, *hrecv;
   double leaf_lam, leaf_l1;   // k_leaf_values regularisation (XGBoost leaves; 0 for GBM)
-  int planar, pad_planar;     // bins layout of master and the ping-pong buffers (see bin_off)
+  int planar, no_na;          // bins layout of master and the ping-pong buffers (see bin_off); no_na: no NA bin
+                              // anywhere in the bins (the histogram loop skips its per-word NA test)
   void* fgroup;               // [F] engine column -> original feature (null: identity), k_split_reduce
 };
 
@@ -1994,7 +1997,7 @@ int h2o_tree_root(const TreePlan* P, hipStream_t s) {
   const int g0 = P->tiles_cap[0] < P->grid ? P->tiles_cap[0] : P->grid;
   TP_CHECK(h2o_hist_build(P->master, P->stride, P->unit ? nullptr : tp_aux(P, 0), tp_aux(P, 1), P->nodes[0], P->bp[0],
                           P->meta[0], P->F, P->partials, P->slot, P->qs, g0, P->packed, nullptr, nullptr, P->pf32, P->N,
-                          P->planar, s));
+                          P->planar | (P->no_na << 1), s));
   return h2o_hist_reduce(P->partials, P->slot, P->used, P->nodes[0], P->bp[0], P->meta[0], 1, g0,
                          P->sliced ? P->hbuild : P->hist0, nullptr, nullptr, P->pf32, s);
 }
@@ -2050,7 +2053,7 @@ int h2o_tree_grow(const TreePlan* P, int d, int dist, hipStream_t s) {
     gh = P->tiles_cap[d] < P->grid ? P->tiles_cap[d] : P->grid;
     tp_level_buf(P, d, sb, sy, sw);
     rc = h2o_hist_build(sb, P->stride, sw, sy, P->nodes[d + 1], P->bp[d + 1], P->meta[d + 1], P->F, P->partials,
-                        P->slot, P->qs, gh, P->packed, P->dec[d], P->nl[d], P->pf32, P->N, P->planar, s);
+                        P->slot, P->qs, gh, P->packed, P->dec[d], P->nl[d], P->pf32, P->N, P->planar | (P->no_na << 1), s);
   } else {
     // regroup level d-1's rows two levels down, then histogram level d+1 (even) contiguously
     rc = tp_route(P, d - 1, s);
@@ -2060,7 +2063,7 @@ int h2o_tree_grow(const TreePlan* P, int d, int dist, hipStream_t s) {
     gh = P->tiles_cap[d + 1] < P->grid ? P->tiles_cap[d + 1] : P->grid;
     tp_level_buf(P, d + 1, sb, sy, sw);
     rc = h2o_hist_build(sb, P->stride, sw, sy, P->nodes[d + 1], P->bp[d + 1], P->meta[d + 1], P->F, P->partials,
-                        P->slot, P->qs, gh, P->packed, nullptr, nullptr, P->pf32, P->N, P->planar, s);
+                        P->slot, P->qs, gh, P->packed, nullptr, nullptr, P->pf32, P->N, P->planar | (P->no_na << 1), s);
   }
   if (rc) return -rc;
   if (!dist)

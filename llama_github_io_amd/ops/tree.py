@@ -454,7 +454,7 @@ class _TreePlan(ctypes.Structure):
                 [("edges", _vp), ("nb_level", _ci * _MAXL), ("pad3", _ci)] +
                 [("ic_map", _vp), ("ic", _vp * _MAXL)] +
                 [(n, _ci) for n in ("sliced", "fs0", "fsn", "sslot")] + [("cand_local", _vp), ("hrecv", _vp)] +
-                [("leaf_lam", _cd), ("leaf_l1", _cd)] + [("planar", _ci), ("pad_planar", _ci)] +
+                [("leaf_lam", _cd), ("leaf_l1", _cd)] + [("planar", _ci), ("no_na", _ci)] +
                 [("fgroup", _vp)])
 
 
@@ -694,9 +694,30 @@ class GpuTreeBuilder:
         P.fgroup = 0 if fg is None else fg.data_ptr()
         P.sliced, P.fs0, P.fsn, P.sslot = int(self.sliced), self.fs0, self.fsn, self.sslot
         P.planar = int(self.planar)
+        P.no_na = int(self._no_na())
         P.cand_local = self.cand_local.data_ptr() if self.sliced else 0
         P.hrecv = self.hrecv.data_ptr() if self.sliced else 0
         return P
+
+    def _no_na(self) -> bool:
+        """True when no feature byte of the bins is the NA bin: the histogram loop then skips its per-word NA
+        test (rows are only permuted between levels, so the property holds for every level's buffer)."""
+        b, F = self.master, self.F
+        if b.numel() == 0:
+            return True
+        hit = torch.zeros((), dtype=torch.bool, device=b.device)
+        step = 1 << 24
+        if self.planar:
+            for pl in range(b.shape[0]):
+                nf = min(32, F - 32 * pl)
+                if nf <= 0:
+                    break
+                for r0 in range(0, b.shape[1], step):
+                    hit |= (b[pl, r0:r0 + step, :nf] == NA_BIN).any()
+        else:
+            for r0 in range(0, b.shape[0], step):
+                hit |= (b[r0:r0 + step, :F] == NA_BIN).any()
+        return not bool(hit)
 
     def _edges_ptr(self):
         if self.p.edges is None or not self.p.adapt_nbins:

@@ -574,3 +574,33 @@ def test_xgboost_bins_by_max_bins_not_nbins_top_level():
     tg = GBMTrainer(dict(ntrees=1, max_depth=2, seed=1))
     tg.fit(X, y, None, None, info)
     assert tg.binning.F > 3            # GBM's UniformAdaptive default: nbins_top_level = 1024 -> wide bins
+
+
+@pytest.mark.gpu
+def test_gpu_no_na_bins_match_reference():
+    """Bins without any NA byte take the histogram loop's no-NA fast path (TreePlan.no_na): decisions, left
+    weights and leaf assignment still equal the reference builder's."""
+    g = torch.Generator().manual_seed(12)
+    N, F = 40000, 6
+    X = torch.randn(F, N, generator=g)
+    y = (torch.rand(N, generator=g) < torch.sigmoid(1.5 * X[0] - X[1] + 0.5 * X[2] * X[3])).float()
+    b = fit_binning(X, np.zeros(F, np.int32), None)
+    bins = apply_binning(b, X)
+    assert not bool((bins[:, :F] == T.NA_BIN).any())
+    gr = y - 0.5
+    aux = torch.stack([torch.ones_like(y), gr, gr, torch.ones_like(y)], 1).contiguous()
+    p = T.SplitParams(min_w=10)
+    ref = T.RefTreeBuilder(bins, b.F, b.nbins, b.iscat, None, 6, p)
+    ref.build(aux, None, 0, seed=3, leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1]).float())
+    tl_r = ref.pop_levels()[0]
+    dev = torch.device("cuda", 0)
+    gb = T.GpuTreeBuilder(apply_binning(b, X.to(dev)), b.F, b.nbins, b.iscat, None, 6, p)
+    assert gb._no_na()
+    gb.build(aux.to(dev), None, 0, seed=3, leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1]).float(), packed=True,
+             unit=True, soa=False)
+    tl_g = gb.pop_levels()[0]
+    assert tl_g.n_leaves == tl_r.n_leaves > 16
+    for dr, dg in zip(tl_r.decs, tl_g.decs):
+        assert np.array_equal(dr["feat"], dg["feat"]) and np.array_equal(dr["bin"], dg["bin"])
+        np.testing.assert_allclose(dr["wl"], dg["wl"], rtol=1e-9)
+    assert torch.equal(ref.leaf_of_row, gb.leaf_of_row.cpu())
