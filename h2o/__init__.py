@@ -333,8 +333,40 @@ def download_pojo(model, path="", get_jar=True, jar_name=""):
     return _dp(getattr(model, "_model", model), path, get_jar, jar_name)
 
 
-def flow():
-    raise NotImplementedError("the Flow web UI is not shipped; use the REST API (python -m llama_github_io_amd.api.server)")
+_flow_server = {}
+
+
+def flow(open_browser=True, port=None):
+    """Open the Flow notebook UI (h2o.py ``flow``): ``/flow/index.html`` of the connected REST server, or — in
+    process — of a REST server started on 127.0.0.1 in a background thread over this process's frames and
+    models. Returns the URL."""
+    from . import _conn
+    if _conn.is_remote():
+        url = _conn.current().url + "/flow/index.html"
+    else:
+        if "url" not in _flow_server:
+            import socket
+            import threading
+            import time as _time
+            import uvicorn
+            from llama_github_io_amd.api.server import create_app
+            if port is None:
+                s = socket.socket()
+                s.bind(("127.0.0.1", 0))
+                port = s.getsockname()[1]
+                s.close()
+            srv = uvicorn.Server(uvicorn.Config(create_app(), host="127.0.0.1", port=int(port), log_level="warning"))
+            threading.Thread(target=srv.run, daemon=True, name="h2o-flow").start()
+            for _ in range(200):
+                if srv.started:
+                    break
+                _time.sleep(0.05)
+            _flow_server.update(url=f"http://127.0.0.1:{port}", server=srv)
+        url = _flow_server["url"] + "/flow/index.html"
+    if open_browser:
+        import webbrowser
+        webbrowser.open(url, new=1)
+    return url
 
 
 def explain(models, frame, columns=None, top_n_features=5, **kw):

@@ -154,3 +154,21 @@ def test_flow_notebook_end_to_end(tmp_path):
     assert res["runAutoML"]["kind"] == "leaderboard" and "Leaderboard" in res["runAutoML"]["html"]
     assert res["loadFlow"]["kind"] == "notebook" and "importAndParse" in res["loadFlow"]["html"]
     assert "DONE" in res["getJobs"]["html"]
+
+
+def test_h2o_flow_serves_in_process_frames():
+    """h2o.flow() in process starts a local REST server over this process's DKV and returns the Flow URL."""
+    import urllib.request
+    import h2o
+    import pandas as pd
+    h2o.init()
+    fr = h2o.H2OFrame(pd.DataFrame({"a": [1.0, 2.0, 3.0], "b": ["x", "y", "x"]}), destination_frame="flow_inproc")
+    url = h2o.flow(open_browser=False)
+    assert url.endswith("/flow/index.html")
+    page = urllib.request.urlopen(url, timeout=30).read().decode()
+    assert "H2O Flow" in page
+    base = url.rsplit("/flow/", 1)[0]
+    frames = json.loads(urllib.request.urlopen(base + "/3/Frames", timeout=30).read().decode())
+    assert any((f["frame_id"]["name"] if isinstance(f["frame_id"], dict) else f["frame_id"]) == "flow_inproc"
+               for f in frames["frames"])
+    assert fr.nrow == 3
