@@ -527,7 +527,9 @@ class GpuTreeBuilder:
         self.hbuild = torch.empty(max(self.caps[:D]) * self.slot, dtype=torch.float64, device=dev)
         # per-block partial histograms of one level (k_hist_build -> k_hist_reduce): G + nodes slots
         # (packed histograms fit two blocks per CU; H2O_HIST_BPC=2 launches hist_bpc * grid blocks)
-        self.hist_bpc = int(os.environ.get("H2O_HIST_BPC", "1"))   # measured: 2 is 3-14 % slower
+        # measured: 2 is 3-14 % slower; again with the barrier-free filtered pass (round 3): 11M 1.34 -> 1.40,
+        # 1.375M 0.423 -> 0.474 ms/tree (the doubled partial slots cost more than the extra waves gain)
+        self.hist_bpc = int(os.environ.get("H2O_HIST_BPC", "1"))
         self.partials = torch.empty((self.hist_bpc * grid + capmax) * self.slot, dtype=torch.float64, device=dev)
         self.tiles_cap = [(N + T - 1) // T + c for c in self.caps]
         self.cand = torch.empty(capmax * F * CAND_BYTES, dtype=torch.uint8, device=dev)
