@@ -40,6 +40,16 @@ __device__ __forceinline__ float bfly_min_idx(float v, int& idx, int mask) {
 // once and both GEMMs take their operands from LDS (row stride P+1 keeps the strided A-operand
 // reads of the distance GEMM on distinct banks).
 #define KM_ROWS 64
+// LDS row stride of a wave's slice: the smallest stride >= P + 1 that is 17 mod 32, so the distance GEMM's
+// B-operand reads (lanes c16 x q, address c16 * Pp + q) and the centroid GEMM's row reads (q * Pp + c16) of
+// each 32-lane half fall on (nearly) distinct banks — P + 1 = 21 left 25 % of the LDS-active cycles in bank
+// conflicts (PMC, profiles/r3_session2_kmeans_c31.md). Kept only while three 4-wave blocks still fit a CU's
+// LDS (the VGPR-bound occupancy).
+__host__ __device__ inline int km_stride(int P) {
+  int pp = P + 1;
+  const int adj = pp + ((17 - pp % 32) + 32) % 32;
+  return adj <= 52 ? adj : pp;
+}
 template <int KT, int PS, int PT>
 __global__ __launch_bounds__(256) void k_lloyd_mfma(const float* __restrict__ X, int64_t N, int P,
                                                     const float* __restrict__ C, int K,
@@ -50,7 +60,7 @@ __global__ __launch_bounds__(256) void k_lloyd_mfma(const float* __restrict__ X,
   const int wv = threadIdx.x >> 6;
   const int q = lane >> 4;          // 0..3
   const int c16 = lane & 15;        // 0..15
-  const int Pp = P + 1;
+  const int Pp = km_stride(P);
   float* xs = lds + (size_t)wv * KM_ROWS * Pp;
   const int64_t wave_g = (int64_t)blockIdx.x * 4 + wv;
   const int64_t n_waves = (int64_t)gridDim.x * 4;
@@ -201,7 +211,7 @@ __global__ __launch_bounds__(256) void k_lloyd_mfma(const float* __restrict__ X,
 template <int KT, int PS, int PT>
 int launch(const float* X, long long N, int P, const float* C, int K, const float* w, int* assign, float* mind,
            float* slabs, int grid, hipStream_t s) {
-  const size_t lds = (size_t)4 * KM_ROWS * (P + 2) * sizeof(float);   // 4 wave slices + 4 x 64 weights
+  const size_t lds = ((size_t)4 * KM_ROWS * km_stride(P) + 4 * KM_ROWS) * sizeof(float);   // 4 slices + 4 x 64 weights
   hipLaunchKernelGGL((k_lloyd_mfma<KT, PS, PT>), dim3(grid), dim3(256), lds, s, X, (int64_t)N, P, C, K, w, assign,
                      mind, slabs);
   return (int)hipGetLastError();
@@ -216,10 +226,31 @@ extern "C" {
 int h2o_kmeans_mfma_shape(int K, int P, int* out) {
   if (K < 1 || P < 1 || K > 64 || P > 64) return 0;
   const int KT = K <= 16 ? 1 : (K <= 32 ? 2 : 4);
-  const int PS = P <= 16 ? 4 : (P <= 32 ? 8 : 16);
+  const int PS = P <= 16 ? 4 : (P <= 24 ? 6 : (P <= 32 ? 8 : 16));   // prefetch float4 groups per lane >= P / 4
   const int PT = (P + 1 + 15) / 16;
   out[0] = KT; out[1] = PS; out[2] = PT;
   return 1;
+}
+
+// Grid that fills the GPU exactly once: CUs x resident blocks per CU of this shape's kernel. Every block
+// grid-strides over the rows with an equal share, so a grid above one resident round (the former fixed 1024
+// blocks at 3 resident blocks per CU = 768) ran a second, one-third-full round of equal length.
+int h2o_kmeans_mfma_grid(int K, int P) {
+  int sh[3];
+  if (!h2o_kmeans_mfma_shape(K, P, sh)) return 0;
+  int dev = 0, cus = 0, per = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 0;
+  const size_t lds = ((size_t)4 * KM_ROWS * km_stride(P) + 4 * KM_ROWS) * sizeof(float);
+  const int KT = sh[0], PS = sh[1], PT = sh[2];
+  hipError_t e = hipErrorInvalidValue;
+#define O(kt, ps, pt) if (KT == kt && PS == ps && PT == pt) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_lloyd_mfma<kt, ps, pt>, 256, lds)
+  O(1, 4, 1); O(1, 4, 2); O(1, 6, 2); O(1, 8, 2); O(1, 8, 3); O(1, 16, 3); O(1, 16, 4); O(1, 16, 5);
+  O(2, 4, 1); O(2, 4, 2); O(2, 6, 2); O(2, 8, 2); O(2, 8, 3); O(2, 16, 3); O(2, 16, 4); O(2, 16, 5);
+  O(4, 4, 1); O(4, 4, 2); O(4, 6, 2); O(4, 8, 2); O(4, 8, 3); O(4, 16, 3); O(4, 16, 4); O(4, 16, 5);
+#undef O
+  if (e != hipSuccess || per < 1) per = 1;
+  return cus * per;
 }
 
 // slabs: [grid*4][KT*16][PT*16] fp32 (caller allocates with the shape from h2o_kmeans_mfma_shape)
@@ -229,9 +260,9 @@ int h2o_kmeans_mfma(const float* X, long long N, int P, const float* C, int K, c
   if (!h2o_kmeans_mfma_shape(K, P, sh) || N <= 0 || grid <= 0 || (P & 3)) return (int)hipErrorInvalidValue;
   const int KT = sh[0], PS = sh[1], PT = sh[2];
 #define L(kt, ps, pt) if (KT == kt && PS == ps && PT == pt) return launch<kt, ps, pt>(X, N, P, C, K, w, assign, mind, slabs, grid, s)
-  L(1, 4, 1); L(1, 4, 2); L(1, 8, 2); L(1, 8, 3); L(1, 16, 3); L(1, 16, 4); L(1, 16, 5);
-  L(2, 4, 1); L(2, 4, 2); L(2, 8, 2); L(2, 8, 3); L(2, 16, 3); L(2, 16, 4); L(2, 16, 5);
-  L(4, 4, 1); L(4, 4, 2); L(4, 8, 2); L(4, 8, 3); L(4, 16, 3); L(4, 16, 4); L(4, 16, 5);
+  L(1, 4, 1); L(1, 4, 2); L(1, 6, 2); L(1, 8, 2); L(1, 8, 3); L(1, 16, 3); L(1, 16, 4); L(1, 16, 5);
+  L(2, 4, 1); L(2, 4, 2); L(2, 6, 2); L(2, 8, 2); L(2, 8, 3); L(2, 16, 3); L(2, 16, 4); L(2, 16, 5);
+  L(4, 4, 1); L(4, 4, 2); L(4, 6, 2); L(4, 8, 2); L(4, 8, 3); L(4, 16, 3); L(4, 16, 4); L(4, 16, 5);
 #undef L
   return (int)hipErrorInvalidValue;
 }

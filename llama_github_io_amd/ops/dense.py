@@ -231,7 +231,8 @@ def kmeans_step(X: torch.Tensor, C: torch.Tensor, w: torch.Tensor | None = None)
         wf = None if w is None else w.contiguous().float()
         a = torch.empty(N, dtype=torch.int32, device=X.device)
         d = torch.empty(N, dtype=torch.float32, device=X.device)
-        grid = int(max(1, min(1024, (N + 63) // 64)))
+        full = int(nat.hip().h2o_kmeans_mfma_grid(int(K), int(P))) or 1024   # one resident round of blocks
+        grid = int(max(1, min(full, (N + 63) // 64)))
         slab = torch.empty(grid * 4, KT * 16, PT * 16, dtype=torch.float32, device=X.device)
         nat.call("h2o_kmeans_mfma", X.data_ptr(), N, P, C.data_ptr(), K, 0 if wf is None else wf.data_ptr(),
                  a.data_ptr(), d.data_ptr(), slab.data_ptr(), grid, nat.stream_ptr(X.device))
