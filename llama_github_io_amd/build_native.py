@@ -55,7 +55,7 @@ def build_hip(force: bool = False, verbose: bool = False) -> str:
             subprocess.run(cmd, check=True)
         objs.append(o)
     tmp = HIP_LIB + ".tmp"
-    subprocess.run([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs, check=True)
+    subprocess.run([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs + ["-ldl"], check=True)
     os.replace(tmp, HIP_LIB)
     return HIP_LIB
 

@@ -13,8 +13,8 @@
 //     per-node histogram lives privately in LDS (fixed-point int64, see below).
 //   * only the smaller child of each split is histogrammed (k_hist_build over its contiguous rows),
 //     into a COMPACT buffer indexed by the parent (one built child per parent); the sibling comes
-//     from parent - child (k_subtract), in fp64. Row-sharded runs all-reduce only that compact
-//     buffer: half the bytes of reducing every child slot of the level.
+//     from parent - child (fused into k_hist_reduce, or into k_split_find on row-sharded levels), in fp64.
+//     Row-sharded runs exchange only that compact buffer: half the bytes of every child slot of the level.
 //   * split search, child planning, leaf numbering and tile planning all stay on device: a whole
 //     tree is a fixed launch sequence with no host synchronisation.
 //   * rows reaching a leaf write their leaf id in ORIGINAL row order (scatter through ridx) and stop
@@ -529,10 +529,10 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
 // its partials sit at b + n. With hist_next != nullptr (single process) the sibling subtraction is fused:
 // hist_next[n] = sum and hist_next[sib] = hist_cur[parent] - sum (no compact-buffer round trip).
 #define RW 8   // waves per k_hist_reduce block: wave w sums partials b0 + w, b0 + w + RW, ... of 64 columns
-template <typename P>
+template <typename P, typename TO>
 __global__ __launch_bounds__(RW * 64) void k_hist_reduce(
     const P* __restrict__ partials, int slot_doubles, int used, const Node* __restrict__ nodes,
-    const int* __restrict__ bp, const int* __restrict__ meta, int G, double* __restrict__ out,
+    const int* __restrict__ bp, const int* __restrict__ meta, int G, TO* __restrict__ out, int ostride,
     double* __restrict__ hist_next, const double* __restrict__ hist_cur) {
   const int node = blockIdx.y;
   if (node >= meta[0]) return;
@@ -563,7 +563,7 @@ __global__ __launch_bounds__(RW * 64) void k_hist_reduce(
   double acc = red[0][lane];
 #pragma unroll
   for (int k = 1; k < RW; ++k) acc += red[k][lane];
-  if (out) out[(size_t)oslot * slot_doubles + i] = acc;
+  if (out) out[(size_t)oslot * ostride + i] = (TO)acc;   // the compact build slot (row-sharded: wire dtype)
   if (hist_next) {
     hist_next[(size_t)node * slot_doubles + i] = acc;
     if (nd.sib >= 0)
@@ -572,13 +572,24 @@ __global__ __launch_bounds__(RW * 64) void k_hist_reduce(
 }
 
 // ------------------------------------------------------------------------------------------------
+// Row-sharded levels: the node histograms are DERIVED inside k_split_find from the exchanged build slots
+// (fused sibling subtraction, no separate k_subtract launch): node = build ? recv[parent] : prev[parent] -
+// recv[parent]; each (node, feature) block also writes its feature's part of the node slot (the next level
+// subtracts from it). recv: [parent][E] in the wire dtype.
+struct Derive {
+  const void* recv;
+  int f32, E;
+  const double* prev;      // the previous level's node histograms (slot stride = slot_doubles)
+  const Node* nodes;       // this level's node list (parent, build)
+};
+
 // k_split_find: best split point per (node, feature). grid = (C, F), block 256 (thread = bin).
 __global__ __launch_bounds__(256) void k_split_find(
-    const double* __restrict__ hist, int slot_doubles, const int* __restrict__ meta, int F,
+    double* __restrict__ hist, int slot_doubles, const int* __restrict__ meta, int F,
     const int* __restrict__ nbins_f, const int* __restrict__ iscat_f, const int* __restrict__ mono_f,
     SplitParams p, int level, Cand* __restrict__ cand, double* __restrict__ root_w,
     const float* __restrict__ edges /*[F][255] global bin edges (inf padded) or null*/, int adapt_nb, int f0,
-    int FL) {
+    int FL, Derive dv) {
   // f0: global id of this launch's first feature (feature-sliced row-sharded runs search only the rank's
   // slice; per-feature arrays arrive offset by f0). FL: features of the slot LAYOUT and of the cand row
   // stride (the slice width Fs, >= the F features searched here; F everywhere else)
@@ -589,18 +600,32 @@ __global__ __launch_bounds__(256) void k_split_find(
   __shared__ double best_e[256];
   __shared__ int best_i[256];
 
-  const double* slot = hist + (size_t)node * slot_doubles;
-  const double* h = slot + 2 * f;          // bin-major slot: (bin, f) at bin * 2FL + 2f
+  double* slot = hist + (size_t)node * slot_doubles;
   const int hs = 2 * FL;
   const int nb = nbins_f[f];
   const bool cat = iscat_f[f] != 0;
   const int mono = mono_f ? mono_f[f] : 0;
-  const double wNA = h[NA_BIN * hs], wyNA = h[NA_BIN * hs + 1];
-  const double naYY = slot[(size_t)FL * 2 * NBIN + f];
-  const double wYY = slot[(size_t)FL * 2 * NBIN + FL];
-
-  double w = 0, wy = 0;
-  if (t < nb && t < NA_BIN) { w = h[t * hs]; wy = h[t * hs + 1]; }
+  const size_t iNA = (size_t)NA_BIN * hs + 2 * f, iT = (size_t)t * hs + 2 * f;
+  const size_t iNY = (size_t)FL * 2 * NBIN + f, iWY = (size_t)FL * 2 * NBIN + FL;
+  double wNA, wyNA, naYY, wYY, w = 0, wy = 0;
+  if (dv.recv) {
+    const Node nd = dv.nodes[node];
+    const int ps = nd.parent < 0 ? 0 : nd.parent;
+    const size_t rb = (size_t)ps * dv.E;
+    const double* pv = dv.prev + (size_t)ps * slot_doubles;
+    auto ld = [&](size_t i) -> double {
+      const double r = dv.f32 ? (double)((const float*)dv.recv)[rb + i] : ((const double*)dv.recv)[rb + i];
+      return nd.build ? r : pv[i] - r;
+    };
+    wNA = ld(iNA); wyNA = ld(iNA + 1); naYY = ld(iNY); wYY = ld(iWY);
+    const double a = ld(iT), b = ld(iT + 1);
+    slot[iT] = a; slot[iT + 1] = b;                      // this feature's bins (NA included: t = NA_BIN)
+    if (t == 0) { slot[iNY] = naYY; if (f == 0) slot[iWY] = wYY; }
+    if (t < nb && t < NA_BIN) { w = a; wy = b; }
+  } else {
+    wNA = slot[iNA]; wyNA = slot[iNA + 1]; naYY = slot[iNY]; wYY = slot[iWY];
+    if (t < nb && t < NA_BIN) { w = slot[iT]; wy = slot[iT + 1]; }
+  }
   sidx[t] = t;
   if (cat) {
     // sort bins by mean response (empty bins first, out-of-range bins last) — DTree.java:1006
@@ -821,9 +846,18 @@ __global__ __launch_bounds__(256) void k_split_find(
 // fgroup (nullable): engine column -> original feature. A numeric feature binned wider than one byte holds
 // several adjacent engine columns (interleaved edge subsets, see ops/binning.py); column sampling draws
 // ORIGINAL features (key and rank of a column = its feature's), so such a feature is in or out as a whole.
+// cfs > 0: cand is the RANK-MAJOR all-gather of a feature-sliced run, [W][ccap][cfs] (rank r searched
+// features r*cfs ..), read in place instead of being permuted into [cap][F] first.
+__device__ __forceinline__ const Cand& cand_at(const Cand* __restrict__ cand, int node, int f, int F, int cfs,
+                                               int ccap) {
+  if (cfs > 0) return cand[((size_t)(f / cfs) * ccap + node) * cfs + f % cfs];
+  return cand[(size_t)node * F + f];
+}
+
 __device__ void reduce_node(const Cand* __restrict__ cand, int node, int F, const int* __restrict__ feat_ok, int k_cols,
                             unsigned long long seed, int level, Dec* __restrict__ dec,
-                            const unsigned char* __restrict__ node_ok, const int* __restrict__ fgroup, int lane) {
+                            const unsigned char* __restrict__ node_ok, const int* __restrict__ fgroup, int lane,
+                            int cfs = 0, int ccap = 0) {
   const unsigned char* nok = node_ok ? node_ok + (size_t)node * F : nullptr;
   auto usable = [&](int f) { return feat_ok[f] != 0 && (!nok || nok[f] != 0); };
   auto gid = [&](int f) { return fgroup ? fgroup[f] : f; };
@@ -848,7 +882,7 @@ __device__ void reduce_node(const Cand* __restrict__ cand, int node, int F, cons
       }
       if (rank >= k_cols) continue;
     }
-    const Cand& c = cand[(size_t)node * F + f];
+    const Cand& c = cand_at(cand, node, f, F, cfs, ccap);
     if (c.valid && (bf < 0 || c.expl > be)) { be = c.expl; bf = f; }
   }
   // wave argmax, ties -> smaller feature index
@@ -861,7 +895,7 @@ __device__ void reduce_node(const Cand* __restrict__ cand, int node, int F, cons
     Dec d;
     d.feat = bf;
     if (bf >= 0) {
-      const Cand& c = cand[(size_t)node * F + bf];
+      const Cand& c = cand_at(cand, node, bf, F, cfs, ccap);
       d.bin = c.bin; d.na_left = c.na_left; d.is_cat = c.is_cat;
       for (int k = 0; k < 8; ++k) d.bits[k] = c.bits[k];
       d.gain = c.gain; d.wl = c.wl; d.wr = c.wr; d.predl = c.predl; d.predr = c.predr;
@@ -879,10 +913,10 @@ __global__ __launch_bounds__(64) void k_split_reduce(
     const int* __restrict__ feat_ok /*[F] per-tree mask, 1 = usable*/, int k_cols,
     unsigned long long seed, int level, Dec* __restrict__ dec,
     const unsigned char* __restrict__ node_ok /*[nodes][F] interaction-constraint mask or null*/,
-    const int* __restrict__ fgroup) {
+    const int* __restrict__ fgroup, int cfs, int ccap) {
   const int node = blockIdx.x;
   if (node >= meta[0]) return;
-  reduce_node(cand, node, F, feat_ok, k_cols, seed, level, dec, node_ok, fgroup, threadIdx.x);
+  reduce_node(cand, node, F, feat_ok, k_cols, seed, level, dec, node_ok, fgroup, threadIdx.x, cfs, ccap);
 }
 
 struct PlanReduce {          // k_plan's fused k_split_reduce (cand == null: decisions already made)
@@ -893,6 +927,7 @@ struct PlanReduce {          // k_plan's fused k_split_reduce (cand == null: dec
   unsigned long long seed;
   const unsigned char* node_ok;
   const int* fgroup;
+  int cfs, ccap;             // rank-major sliced candidates (see cand_at); 0 = [cap][F]
 };
 #define PLAN_REDUCE_MAX 256
 
@@ -973,7 +1008,8 @@ __global__ __launch_bounds__(1024) void k_plan(
   const int T = blockDim.x, tid = threadIdx.x;
   if (pr.cand) {
     for (int node = tid >> 6; node < n; node += T >> 6)
-      reduce_node(pr.cand, node, pr.F, pr.feat_ok, pr.k_cols, pr.seed, depth, dec, pr.node_ok, pr.fgroup, tid & 63);
+      reduce_node(pr.cand, node, pr.F, pr.feat_ok, pr.k_cols, pr.seed, depth, dec, pr.node_ok, pr.fgroup, tid & 63,
+                  pr.cfs, pr.ccap);
     __syncthreads();                     // the block's own decisions (global) before the plan reads them
   }
   const bool odd = depth & 1;
@@ -1111,32 +1147,14 @@ __global__ void k_zero_hist(double* __restrict__ hbuild, const Node* __restrict_
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < slot_doubles; i += gridDim.x * blockDim.x) s[i] = 0.0;
 }
 
-// k_subtract: next-level node histograms from the compact build buffer: the built child copies its
-// slot, the sibling is parent - built child (fp64). Both read hbuild[parent].
-__global__ void k_subtract(double* __restrict__ hist_next, const double* __restrict__ hist_cur,
-                           const double* __restrict__ hbuild, const Node* __restrict__ next,
-                           const int* __restrict__ meta, int slot_doubles) {
-  const int node = blockIdx.y;
-  if (node >= meta[0]) return;
-  const Node nd = next[node];
-  double* s = hist_next + (size_t)node * slot_doubles;
-  const double* hb = hbuild + (size_t)nd.parent * slot_doubles;
-  if (nd.build) {
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < slot_doubles; i += gridDim.x * blockDim.x) s[i] = hb[i];
-    return;
-  }
-  const double* pa = hist_cur + (size_t)nd.parent * slot_doubles;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < slot_doubles; i += gridDim.x * blockDim.x)
-    s[i] = pa[i] - hb[i];
-}
-
 // k_hist_pack: feature-sliced reduce-scatter staging. Node slots [n][slot] (bin-major (bin, f) pairs, then
 // naYY[F], wYY) -> dst[W][n][E] where rank r's chunk holds, per node, the same layout restricted to its
 // features [r*Fs, r*Fs + Fs): (bin, f') pairs, naYY[f'], wYY (E = Fs*2*NBIN + Fs + 1). Features past F
 // are zero-filled. After reduce_scatter each rank owns the GLOBAL histograms of its slice, in the layout
 // k_split_find reads with F = Fs.
+template <typename TO>
 __global__ void k_hist_pack(const double* __restrict__ src, int slot, int F, int Fs, int W, int n,
-                            double* __restrict__ dst) {
+                            TO* __restrict__ dst) {
   const long long E = (long long)Fs * 2 * NBIN + Fs + 1;
   const long long total = (long long)W * n * E;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
@@ -1156,7 +1174,7 @@ __global__ void k_hist_pack(const double* __restrict__ src, int slot, int F, int
     } else {
       v = sl[(size_t)F * 2 * NBIN + F];
     }
-    dst[i] = v;
+    dst[i] = (TO)v;
   }
 }
 
@@ -1676,6 +1694,16 @@ static void launch_hist(dim3 grid, size_t lds, hipStream_t s, const void* bins, 
                        (int*)nullptr, f32, N, planar);
 }
 
+template <typename P, typename TO>
+static void reduce_launch(const void* partials, int slot_doubles, int used, const void* nodes, const void* bp,
+                          const void* meta, int cap, int grid, void* out, int ostride, void* hist_next,
+                          const void* hist_cur, hipStream_t s) {
+  const int gx = (used + 63) / 64;
+  hipLaunchKernelGGL((k_hist_reduce<P, TO>), dim3(gx, cap), dim3(RW * 64), 0, s, (const P*)partials, slot_doubles,
+                     used, (const Node*)nodes, (const int*)bp, (const int*)meta, grid, (TO*)out, ostride,
+                     (double*)hist_next, (const double*)hist_cur);
+}
+
 extern "C" {
 
 int h2o_abi_version() { return H2O_ABI_VERSION; }
@@ -1705,19 +1733,21 @@ int h2o_hist_build(const void* bins, int stride, const void* aw, const void* ay,
   return (int)hipGetLastError();
 }
 
-// grid: the G the matching h2o_hist_build ran with; out / hist_next may be null (see k_hist_reduce)
+
+// grid: the G the matching h2o_hist_build ran with; out / hist_next may be null (see k_hist_reduce).
+// out: compact build slots of ostride values (0: slot_doubles), fp32 when out_f32 (the exchange's wire dtype)
 int h2o_hist_reduce(const void* partials, int slot_doubles, int used, const void* nodes, const void* bp,
                     const void* meta, int cap, int grid, void* out, void* hist_next, const void* hist_cur,
-                    int f32, hipStream_t s) {
-  const int gx = (used + 63) / 64;
-  if (f32)
-    hipLaunchKernelGGL(k_hist_reduce<float>, dim3(gx, cap), dim3(RW * 64), 0, s, (const float*)partials, slot_doubles,
-                       used, (const Node*)nodes, (const int*)bp, (const int*)meta, grid, (double*)out,
-                       (double*)hist_next, (const double*)hist_cur);
+                    int f32, int out_f32, int ostride, hipStream_t s) {
+  if (ostride <= 0) ostride = slot_doubles;
+  if (f32 && out_f32)
+    reduce_launch<float, float>(partials, slot_doubles, used, nodes, bp, meta, cap, grid, out, ostride, hist_next, hist_cur, s);
+  else if (f32)
+    reduce_launch<float, double>(partials, slot_doubles, used, nodes, bp, meta, cap, grid, out, ostride, hist_next, hist_cur, s);
+  else if (out_f32)
+    reduce_launch<double, float>(partials, slot_doubles, used, nodes, bp, meta, cap, grid, out, ostride, hist_next, hist_cur, s);
   else
-    hipLaunchKernelGGL(k_hist_reduce<double>, dim3(gx, cap), dim3(RW * 64), 0, s, (const double*)partials,
-                       slot_doubles, used, (const Node*)nodes, (const int*)bp, (const int*)meta, grid, (double*)out,
-                       (double*)hist_next, (const double*)hist_cur);
+    reduce_launch<double, double>(partials, slot_doubles, used, nodes, bp, meta, cap, grid, out, ostride, hist_next, hist_cur, s);
   return (int)hipGetLastError();
 }
 
@@ -1729,27 +1759,34 @@ int h2o_leaf_values(const void* leafsum, int n, int log_link, double scale, doub
   return (int)hipGetLastError();
 }
 
+static int split_find_launch(void* hist, int slot_doubles, const void* meta, int cap, int F, const void* nbins_f,
+                             const void* iscat_f, const void* mono_f, const SplitParams& p, int level, void* cand,
+                             void* root_w, const void* edges, int adapt_nb, int f0, int FL, Derive dv, hipStream_t s) {
+  if (F <= 0 || cap <= 0) return 0;
+  if (FL < F) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_split_find, dim3(cap, F), dim3(256), 0, s, (double*)hist, slot_doubles,
+                     (const int*)meta, F, (const int*)nbins_f, (const int*)iscat_f, (const int*)mono_f, p, level,
+                     (Cand*)cand, (double*)root_w, (const float*)edges, adapt_nb, f0, FL, dv);
+  return (int)hipGetLastError();
+}
+
 int h2o_split_find(const void* hist, int slot_doubles, const void* meta, int cap, int F, const void* nbins_f,
                    const void* iscat_f, const void* mono_f, double min_w, double msi, double lambda_, double alpha,
                    double gamma, int mode, int random_split, unsigned long long seed, int level, void* cand,
                    void* root_w, const void* edges, int adapt_nb, int f0, int FL, hipStream_t s) {
-  if (F <= 0 || cap <= 0) return 0;
-  if (FL < F) return (int)hipErrorInvalidValue;
   SplitParams p;
   p.min_w = min_w; p.min_split_improvement = msi; p.lambda = lambda_; p.alpha = alpha; p.gamma = gamma;
   p.mode = mode; p.random_split = random_split; p.seed = seed;
-  hipLaunchKernelGGL(k_split_find, dim3(cap, F), dim3(256), 0, s, (const double*)hist, slot_doubles,
-                     (const int*)meta, F, (const int*)nbins_f, (const int*)iscat_f, (const int*)mono_f, p, level,
-                     (Cand*)cand, (double*)root_w, (const float*)edges, adapt_nb, f0, FL);
-  return (int)hipGetLastError();
+  return split_find_launch((void*)hist, slot_doubles, meta, cap, F, nbins_f, iscat_f, mono_f, p, level, cand, root_w,
+                           edges, adapt_nb, f0, FL, Derive{nullptr, 0, 0, nullptr, nullptr}, s);
 }
 
 int h2o_split_reduce(const void* cand, const void* meta, int cap, int F, const void* feat_ok, int k_cols,
                      unsigned long long seed, int level, void* dec, const void* node_ok, const void* fgroup,
-                     hipStream_t s) {
+                     int cfs, hipStream_t s) {
   hipLaunchKernelGGL(k_split_reduce, dim3(cap), dim3(64), 0, s, (const Cand*)cand, (const int*)meta, F,
                      (const int*)feat_ok, k_cols, seed, level, (Dec*)dec, (const unsigned char*)node_ok,
-                     (const int*)fgroup);
+                     (const int*)fgroup, cfs, cap);
   return (int)hipGetLastError();
 }
 
@@ -1777,7 +1814,7 @@ int h2o_plan(const void* nodes, const void* meta, const void* dec, void* node_nl
              void* child_l, void* child_r, void* next, void* next_tile_prefix, void* next_meta, void* next_build_prefix,
              void* counters, void* scratch, int depth, int max_depth, double min_w, int cap_next, int leaf_cap,
              hipStream_t s) {
-  PlanReduce pr{nullptr, 0, nullptr, 0, 0ull, nullptr, nullptr};
+  PlanReduce pr{nullptr, 0, nullptr, 0, 0ull, nullptr, nullptr, 0, 0};
   return plan_launch(nodes, meta, (void*)dec, node_nl, prev_nl, curs, child_l, child_r, next, next_tile_prefix,
                      next_meta, next_build_prefix, counters, scratch, depth, max_depth, min_w, cap_next, leaf_cap, pr, s);
 }
@@ -1795,21 +1832,17 @@ int h2o_zero_hist(void* hist, const void* next, const void* meta, int cap, int s
   return (int)hipGetLastError();
 }
 
-int h2o_subtract(void* hist_next, const void* hist_cur, const void* hbuild, const void* next, const void* meta,
-                 int cap, int slot_doubles, hipStream_t s) {
-  const int gx = (slot_doubles + 1023) / 1024;
-  hipLaunchKernelGGL(k_subtract, dim3(gx < 64 ? gx : 64, cap), dim3(256), 0, s, (double*)hist_next,
-                     (const double*)hist_cur, (const double*)hbuild, (const Node*)next, (const int*)meta,
-                     slot_doubles);
-  return (int)hipGetLastError();
-}
 
-int h2o_hist_pack(const void* src, int slot, int F, int Fs, int W, int n, void* dst, hipStream_t s) {
+// out_f32: write the packed slices as fp32 (the wire format of the sliced exchange)
+int h2o_hist_pack(const void* src, int slot, int F, int Fs, int W, int n, void* dst, int out_f32, hipStream_t s) {
   if (n <= 0) return 0;
   const long long total = (long long)W * n * ((long long)Fs * 2 * NBIN + Fs + 1);
   long long g = (total + 255) / 256;
-  hipLaunchKernelGGL(k_hist_pack, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, s, (const double*)src, slot,
-                     F, Fs, W, n, (double*)dst);
+  const dim3 gr((unsigned)(g < 4096 ? g : 4096));
+  if (out_f32)
+    hipLaunchKernelGGL(k_hist_pack<float>, gr, dim3(256), 0, s, (const double*)src, slot, F, Fs, W, n, (float*)dst);
+  else
+    hipLaunchKernelGGL(k_hist_pack<double>, gr, dim3(256), 0, s, (const double*)src, slot, F, Fs, W, n, (double*)dst);
   return (int)hipGetLastError();
 }
 
@@ -1928,8 +1961,7 @@ int h2o_predict(const void* X, long long N, int K, const void* feat, const void*
 // ================================================================================================
 // Native per-tree launch sequence: a tree costs a handful of host calls instead of ~45 ctypes round trips
 // (at 1.375M rows/GPU the Python launch loop alone took ~370 us/tree and left the GPU 18 % idle).
-// Row-sharded runs stop at each collective: h2o_tree_level returns after the level's compact histogram is
-// reduced into hbuild; the caller all-reduces it and continues with h2o_tree_subtract.
+// Row-sharded runs use h2o_tree_dist: the same launches with the level collectives enqueued in between.
 // Aux planes are SoA (aux[c * N + i]: 0 = w (null-able: unit weights), 1 = wY, 2 = gamma numerator,
 // 3 = gamma denominator); the routed ping-pong buffers carry bins + wY (+ w).
 #define TP_MAXL 65
@@ -1964,7 +1996,22 @@ struct TreePlan {
   int planar, no_na;          // bins layout of master and the ping-pong buffers (see bin_off); no_na: no NA bin
                               // anywhere in the bins (the histogram loop skips its per-word NA test)
   void* fgroup;               // [F] engine column -> original feature (null: identity), k_split_reduce
+  // collective transport of a row-sharded tree (h2o_tree_dist): coll_fn(coll_ctx, op, send, recv, count, dtype,
+  // stream), see h2o_coll_fn. RCCL (h2o_rccl_coll + an ncclComm_t) on a GPU node; a host callback under gloo.
+  void* coll_fn;
+  void* coll_ctx;
+  int W, cf32;                // ranks; cf32: exchanged histograms travel as fp32 (half the bytes)
+  int cand_fs;                // features per rank of the rank-major candidate all-gather (sliced)
+  int dist;                   // row-sharded (h2o_tree_dist): build slots go out in the exchange's layout
+  void *hsend, *cand_all, *lsx;  // [W][n][E] packed send slots, [W][cap][Fs] candidates, leaf sums + root weight
 };
+
+// op codes / dtypes of the collective transport
+enum { H2O_COLL_ALLREDUCE = 0, H2O_COLL_REDUCE_SCATTER = 1, H2O_COLL_ALLGATHER = 2 };
+enum { H2O_DT_F32 = 0, H2O_DT_F64 = 1, H2O_DT_U8 = 2 };
+// count: ALLREDUCE elements, REDUCE_SCATTER elements received per rank, ALLGATHER elements sent per rank
+typedef int (*h2o_coll_fn)(void* ctx, int op, const void* send, void* recv, long long count, int dtype,
+                           hipStream_t s);
 
 static inline const float* tp_aux(const TreePlan* P, int c) { return (const float*)P->aux + (size_t)c * P->N; }
 
@@ -1998,23 +2045,34 @@ int h2o_tree_root(const TreePlan* P, hipStream_t s) {
   TP_CHECK(h2o_hist_build(P->master, P->stride, P->unit ? nullptr : tp_aux(P, 0), tp_aux(P, 1), P->nodes[0], P->bp[0],
                           P->meta[0], P->F, P->partials, P->slot, P->qs, g0, P->packed, nullptr, nullptr, P->pf32, P->N,
                           P->planar | (P->no_na << 1), s));
+  // row-sharded all-reduce: straight into the wire buffer; sliced: hbuild (packed by slice next)
+  if (P->dist && !P->sliced)
+    return h2o_hist_reduce(P->partials, P->slot, P->used, P->nodes[0], P->bp[0], P->meta[0], 1, g0, P->hrecv, nullptr,
+                           nullptr, P->pf32, P->cf32, P->sslot, s);
   return h2o_hist_reduce(P->partials, P->slot, P->used, P->nodes[0], P->bp[0], P->meta[0], 1, g0,
-                         P->sliced ? P->hbuild : P->hist0, nullptr, nullptr, P->pf32, s);
+                         P->sliced ? P->hbuild : P->hist0, nullptr, nullptr, P->pf32, 0, 0, s);
 }
 
-// split search of level d: every feature into cand, or (sliced) this rank's feature slice into cand_local
+// split search of level d: every feature into cand, or (sliced) this rank's feature slice into cand_local.
+// Row-sharded: the level's node histograms are derived from the exchanged build slots on the way (Derive).
 int h2o_tree_find(const TreePlan* P, int d, hipStream_t s) {
-  const void* hc = (d % 2) ? P->hist1 : P->hist0;
+  void* hc = (d % 2) ? P->hist1 : P->hist0;
+  const void* hp = (d % 2) ? P->hist0 : P->hist1;      // level d-1 (unused at the root: build = 1)
+  SplitParams p;
+  p.min_w = P->min_w; p.min_split_improvement = P->msi; p.lambda = P->lam; p.alpha = P->alpha; p.gamma = P->gamma;
+  p.mode = P->mode; p.random_split = P->random_split; p.seed = P->seed;
+  const int hs = P->sliced ? P->sslot : P->slot;
+  const Derive dv = P->dist ? Derive{P->hrecv, P->cf32, P->sslot, (const double*)hp, (const Node*)P->nodes[d]}
+                            : Derive{nullptr, 0, 0, nullptr, nullptr};
   if (!P->sliced)
-    return h2o_split_find(hc, P->slot, P->meta[d], P->caps[d], P->F, P->nbins_f, P->iscat_f, P->mono_f, P->min_w,
-                          P->msi, P->lam, P->alpha, P->gamma, P->mode, P->random_split, P->seed, d, P->cand,
-                          d == 0 ? P->rootw : nullptr, P->edges, P->nb_level[d], 0, P->F, s);
+    return split_find_launch(hc, hs, P->meta[d], P->caps[d], P->F, P->nbins_f, P->iscat_f, P->mono_f, p, d, P->cand,
+                             d == 0 ? P->rootw : nullptr, P->edges, P->nb_level[d], 0, P->F, dv, s);
   const int f0 = P->fs0;
-  return h2o_split_find(hc, P->sslot, P->meta[d], P->caps[d], P->fsn, (const int*)P->nbins_f + f0,
-                        (const int*)P->iscat_f + f0, P->mono_f ? (const int*)P->mono_f + f0 : nullptr, P->min_w,
-                        P->msi, P->lam, P->alpha, P->gamma, P->mode, P->random_split, P->seed, d, P->cand_local,
-                        d == 0 ? P->rootw : nullptr, P->edges ? (const float*)P->edges + (size_t)f0 * 255 : nullptr,
-                        P->nb_level[d], f0, (P->sslot - 1) / (2 * NBIN + 1), s);
+  return split_find_launch(hc, hs, P->meta[d], P->caps[d], P->fsn, (const int*)P->nbins_f + f0,
+                           (const int*)P->iscat_f + f0, P->mono_f ? (const int*)P->mono_f + f0 : nullptr, p, d,
+                           P->cand_local, d == 0 ? P->rootw : nullptr,
+                           P->edges ? (const float*)P->edges + (size_t)f0 * 255 : nullptr, P->nb_level[d], f0,
+                           (P->sslot - 1) / (2 * NBIN + 1), dv, s);
 }
 
 // decisions (from cand) + plan, then the next level's histogram.
@@ -2027,13 +2085,16 @@ int h2o_tree_grow(const TreePlan* P, int d, int dist, hipStream_t s) {
   int rc;
   const int kc = P->kc_level[d] > 0 ? P->kc_level[d] : P->k_cols;
   // small levels: the plan block picks the decisions itself (one launch instead of two)
+  // sliced: the rank-major all-gather of every rank's candidates, read in place (cand_at)
+  const void* cand = P->sliced ? P->cand_all : P->cand;
+  const int cfs = P->sliced ? P->cand_fs : 0;
   PlanReduce pr{nullptr, P->F, (const int*)P->feat_ok, kc, P->seed,
-                P->ic_map ? (const unsigned char*)P->ic[d] : nullptr, (const int*)P->fgroup};
+                P->ic_map ? (const unsigned char*)P->ic[d] : nullptr, (const int*)P->fgroup, cfs, cap};
   if (cap <= PLAN_REDUCE_MAX) {
-    pr.cand = (const Cand*)P->cand;
+    pr.cand = (const Cand*)cand;
   } else {
-    rc = h2o_split_reduce(P->cand, P->meta[d], cap, P->F, P->feat_ok, kc, P->seed, d, P->dec[d],
-                          P->ic_map ? P->ic[d] : nullptr, P->fgroup, s);
+    rc = h2o_split_reduce(cand, P->meta[d], cap, P->F, P->feat_ok, kc, P->seed, d, P->dec[d],
+                          P->ic_map ? P->ic[d] : nullptr, P->fgroup, cfs, s);
     if (rc) return -rc;
   }
   rc = plan_launch(P->nodes[d], P->meta[d], P->dec[d], P->nl[d], odd ? P->nl[d - 1] : nullptr, P->cur[d], P->cl[d],
@@ -2068,10 +2129,13 @@ int h2o_tree_grow(const TreePlan* P, int d, int dist, hipStream_t s) {
   if (rc) return -rc;
   if (!dist)
     rc = h2o_hist_reduce(P->partials, P->slot, P->used, P->nodes[d + 1], P->bp[d + 1], P->meta[d + 1], P->caps[d + 1],
-                         gh, nullptr, hn, hc, P->pf32, s);
-  else
+                         gh, nullptr, hn, hc, P->pf32, 0, 0, s);
+  else if (P->sliced)
     rc = h2o_hist_reduce(P->partials, P->slot, P->used, P->nodes[d + 1], P->bp[d + 1], P->meta[d + 1], P->caps[d + 1],
-                         gh, P->hbuild, nullptr, nullptr, P->pf32, s);
+                         gh, P->hbuild, nullptr, nullptr, P->pf32, 0, 0, s);
+  else   // all-reduce exchange: the build slots go straight into the wire buffer
+    rc = h2o_hist_reduce(P->partials, P->slot, P->used, P->nodes[d + 1], P->bp[d + 1], P->meta[d + 1], P->caps[d + 1],
+                         gh, P->hrecv, nullptr, nullptr, P->pf32, P->cf32, P->sslot, s);
   return rc ? -rc : 0;
 }
 
@@ -2082,15 +2146,6 @@ int h2o_tree_level(const TreePlan* P, int d, int dist, hipStream_t s) {
   return h2o_tree_grow(P, d, dist, s);
 }
 
-// row-sharded: sibling subtraction after the compact buffer's all-reduce (sliced: after the reduce-scatter
-// into hrecv, on slice-layout slots)
-int h2o_tree_subtract(const TreePlan* P, int d, hipStream_t s) {
-  void* hc = (d % 2) ? P->hist1 : P->hist0;
-  void* hn = (d % 2) ? P->hist0 : P->hist1;
-  if (P->sliced)
-    return h2o_subtract(hn, hc, P->hrecv, P->nodes[d + 1], P->meta[d + 1], P->caps[d + 1], P->sslot, s);
-  return h2o_subtract(hn, hc, P->hbuild, P->nodes[d + 1], P->meta[d + 1], P->caps[d + 1], P->slot, s);
-}
 
 // after the last level: leaf_of_row (original order) + fp64 leaf sums (the caller all-reduces them when sharded)
 static int tree_leaves(const TreePlan* P, bool values, hipStream_t s) {
@@ -2103,6 +2158,72 @@ static int tree_leaves(const TreePlan* P, bool values, hipStream_t s) {
 }
 
 int h2o_tree_leaves(const TreePlan* P, hipStream_t s) { return tree_leaves(P, false, s); }
+
+static inline int coll(const TreePlan* P, int op, const void* snd, void* rcv, long long count, int dt, hipStream_t s) {
+  return ((h2o_coll_fn)P->coll_fn)(P->coll_ctx, op, snd, rcv, count, dt, s);
+}
+
+// The histogram exchange of n build slots (src: slots of `slot` doubles, slot = parent) into hrecv, in the wire
+// dtype (cf32: fp32, half the bytes; else fp64):
+//  * sliced: pack by feature slice into hsend [W][n][sslot] and REDUCE-SCATTER -> hrecv [n][sslot] holds the
+//    GLOBAL histograms of this rank's features;
+//  * all-reduce: k_hist_reduce wrote the build slots straight into hrecv ([n][E = used]); ALL-REDUCE in place.
+// The next k_split_find derives the node histograms from hrecv (fused sibling subtraction).
+static int exchange(const TreePlan* P, int n, hipStream_t s) {
+  const int dt = P->cf32 ? H2O_DT_F32 : H2O_DT_F64;
+  if (P->sliced) {
+    TP_CHECK(h2o_hist_pack(P->hbuild, P->slot, P->F, P->cand_fs, P->W, n, P->hsend, P->cf32, s));
+    return coll(P, H2O_COLL_REDUCE_SCATTER, P->hsend, P->hrecv, (long long)n * P->sslot, dt, s);
+  }
+  // k_hist_reduce already wrote the build slots into hrecv ([n][E = used], wire dtype)
+  return coll(P, H2O_COLL_ALLREDUCE, P->hrecv, P->hrecv, (long long)n * P->sslot, dt, s);
+}
+
+// Row-sharded tree (reference: hex/tree/ScoreBuildHistogram2.java + water/MRTask.java reduce), the whole tree
+// in ONE host call: every kernel and every collective is enqueued on stream s in order, the host never waits.
+//  * all-reduce (default): per level the built-node histograms are all-reduced; every rank searches every
+//    feature of the same global histograms, so every rank takes the same decisions. One collective per level.
+//  * sliced: per level the built-node histograms are reduce-scattered by feature slice (rank r gets the GLOBAL
+//    histograms of features [r*Fs, r*Fs+Fs)), each rank searches its slice, and the per-(node, feature)
+//    candidates are all-gathered (a few KB, read in place rank-major): 1/W of the split search per rank, but two
+//    collectives per level.
+// Both end with one all-reduce of the leaf sums (sliced: + the root weight, which only the owner of feature 0
+// computes).
+int h2o_tree_dist(const TreePlan* P, hipStream_t s) {
+  if (!P->coll_fn || P->W < 1) return (int)hipErrorInvalidValue;
+  if (!P->dist) return (int)hipErrorInvalidValue;
+  TP_CHECK(h2o_tree_root(P, s));               // -> hbuild slot 0 (sliced) / hrecv slot 0
+  const long long L2 = 2LL * P->leaf_cap;
+  TP_CHECK(exchange(P, 1, s));
+  for (int d = 0; d < P->D; ++d) {
+    TP_CHECK(h2o_tree_find(P, d, s));
+    if (P->sliced)
+      TP_CHECK(coll(P, H2O_COLL_ALLGATHER, P->cand_local, P->cand_all,
+                    (long long)P->caps[d] * P->cand_fs * (long long)sizeof(Cand), H2O_DT_U8, s));
+    const int r = h2o_tree_grow(P, d, 1, s);
+    if (r < 0) return -r;
+    if (r == 1) break;
+    TP_CHECK(exchange(P, P->caps[d], s));
+  }
+  TP_CHECK(h2o_tree_leaves(P, s));
+  if (P->sliced) {
+    double* lsx = (double*)P->lsx;
+    TP_CHECK((int)hipMemcpyAsync(lsx, P->leafsum, (size_t)L2 * 8, hipMemcpyDeviceToDevice, s));
+    if (P->fs0 == 0 && P->fsn > 0)
+      TP_CHECK((int)hipMemcpyAsync(lsx + L2, P->rootw, 8, hipMemcpyDeviceToDevice, s));
+    else
+      TP_CHECK((int)hipMemsetAsync(lsx + L2, 0, 8, s));
+    TP_CHECK(coll(P, H2O_COLL_ALLREDUCE, lsx, lsx, L2 + 1, H2O_DT_F64, s));
+    TP_CHECK((int)hipMemcpyAsync(P->leafsum, lsx, (size_t)L2 * 8, hipMemcpyDeviceToDevice, s));
+    TP_CHECK((int)hipMemcpyAsync(P->rootw, lsx + L2, 8, hipMemcpyDeviceToDevice, s));
+  } else {
+    TP_CHECK(coll(P, H2O_COLL_ALLREDUCE, P->leafsum, P->leafsum, L2, H2O_DT_F64, s));
+  }
+  if (P->leaf_native)
+    TP_CHECK(h2o_leaf_values(P->leafsum, P->leaf_cap, P->log_link, P->scale, P->kclamp, P->mx, P->leaf_lam,
+                             P->leaf_l1, P->leafval, s));
+  return 0;
+}
 
 // single process: the whole tree (root .. leaves, and leaf_native values in the leaf-sum pass) in one host call
 int h2o_tree_all(const TreePlan* P, hipStream_t s) {

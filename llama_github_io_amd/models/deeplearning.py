@@ -4,10 +4,19 @@ momentum updates, max_w2), ``DeepLearningTask.java`` (Hogwild! map)).
 
 MI355X design: synchronous mini-batch SGD instead of Hogwild (lock-free races do not map to a GPU).
 Hidden layers are hipBLASLt GEMMs (bf16 or fp32 via ``compute_dtype``) followed by the fused HIP
-bias+activation+dropout epilogue (``ops.dense.BiasAct``, forward and backward). Multi-GPU is data
-parallel with ONE flat bucket all-reduce of all gradients per step over RCCL (the ADADELTA state is
-replicated, so every rank applies the identical update = H2O's model averaging with a 1-step
-period). Supports Rectifier/Tanh/ExpRectifier/Maxout (+WithDropout), input/hidden dropout, L1/L2,
+bias+activation+dropout epilogue (``ops.dense.BiasAct``, forward and backward), or the hand-written fused MFMA
+step (``csrc/dl_kernels.hip``).
+
+Multi-GPU (row-sharded) follows H2O's map/reduce semantics (``DeepLearningTask.java:169-224``,
+``DeepLearningModelInfo.add/div``): every rank trains its OWN copy of the model on its own rows for one
+iteration of ``train_samples_per_iteration`` global samples (tspi / W local samples, the single-GPU
+hipGraph-chunked step path), then ONE flat all-reduce averages the weights, biases and optimizer state
+(ADADELTA E[g^2] / E[dx^2], momenta). With ``elastic_averaging`` the ranks keep their local models and a
+consensus model is the time average pa * node-average + (1 - pa) * previous consensus
+(``DeepLearningModelInfo.timeAverage``), with the elastic pull ``elastic_averaging_regularization * (w - w_EA)``
+in every local gradient (``Neurons.java:263,414``); the consensus is the model scored and returned.
+``H2O_DL_DP=sync`` instead all-reduces the gradient of every global mini-batch (1-step averaging).
+Supports Rectifier/Tanh/ExpRectifier/Maxout (+WithDropout), input/hidden dropout, L1/L2,
 max_w2, ADADELTA (rho, epsilon) or momentum SGD with rate annealing/decay and Nesterov,
 autoencoder + ``anomaly`` (per-row reconstruction MSE) + ``deepfeatures``, regression
 distributions (gaussian/poisson/gamma/tweedie/laplace/quantile/huber), early stopping.
@@ -40,7 +49,8 @@ DL_DEFAULTS = dict(hidden=[200, 200], epochs=10.0, activation="Rectifier", adapt
                    score_training_samples=10000, seed=-1, shuffle_training_data=True, reproducible=False,
                    export_weights_and_biases=False, missing_values_handling="MeanImputation", max_runtime_secs=0.0,
                    compute_dtype="float32", gpu_batch_size=256, train_samples_per_iteration=-2,
-                   overwrite_with_best_model=True, classification_stop=0.0, regression_stop=1e-6)
+                   overwrite_with_best_model=True, classification_stop=0.0, regression_stop=1e-6,
+                   elastic_averaging=False, elastic_averaging_moving_rate=0.9, elastic_averaging_regularization=1e-3)
 
 
 class MLP(torch.nn.Module):
@@ -212,6 +222,14 @@ class DeepLearningTrainer:
             # DataInfo skipMissing: rows with a missing predictor do not train
             w = torch.where(torch.isnan(X).any(0), torch.zeros_like(w), w)
         sharded = coll.is_dist()
+        # data parallelism: per-iteration model averaging (H2O semantics, default) or per-step gradient sync
+        dp_avg = sharded and os.environ.get("H2O_DL_DP", "average") != "sync"
+        gsync = sharded and not dp_avg
+        Wn = coll.world() if sharded else 1
+        dp_local = dp_avg and os.environ.get("H2O_DL_DP") == "local"
+        elastic = dp_avg and not dp_local and bool(p.get("elastic_averaging"))
+        # dropout masks: each rank of a model-averaging run trains on different rows with its own stream
+        dseed = (seed ^ (coll.rank() * 0x9E3779B97F4A7C15)) & ((1 << 63) - 1) if dp_avg else seed
         row0, N_glob = coll.exclusive_offset(N) if sharded else (0, N)
         self._row0, self._N_glob = row0, N_glob
         ex = Expander(info, standardize=p["standardize"], use_all_factor_levels=p["use_all_factor_levels"]).fit(
@@ -296,6 +314,9 @@ class DeepLearningTrainer:
             # handful of large batches would barely move (the reference does one update per row)
             B = max(1, min(int(p["gpu_batch_size"]), N_glob // 1024))
         B = max(1, min(B, N_glob))
+        if dp_avg:   # local mini-batches: never larger than the smallest shard
+            bt = torch.tensor([float(min(B, N))], dtype=torch.float64, device=coll.comm_device())
+            B = max(1, int(coll.all_reduce_min_(bt).item()))
         from ..ops.dense import FlatParams
         fp = FlatParams(net)                 # params/grads as views of two flat buffers
         params = fp.params
@@ -318,10 +339,11 @@ class DeepLearningTrainer:
         keeper = ScoreKeeper(p["stopping_rounds"], p["stopping_metric"], p["stopping_tolerance"],
                              "Regression" if ae else cat)
         epochs = float(p["epochs"]) - prev_epochs
-        total = int(math.ceil(epochs * N_glob / B))
+        Bg = B * Wn if dp_avg else B          # global samples per (local) step
+        total = int(math.ceil(epochs * N_glob / Bg))
         # the epoch permutation is drawn on the device (a host randperm of 10M rows costs ~0.3 s per epoch);
-        # every rank draws the same one from the same seed
-        g = torch.Generator(device=dev).manual_seed(seed & 0x7FFFFFFF)
+        # every rank draws the same one from the same seed (model averaging: each rank its own local one)
+        g = torch.Generator(device=dev).manual_seed((seed + (1000003 * coll.rank() if dp_avg else 0)) & 0x7FFFFFFF)
         history = []
         samples = 0
         last_score = time.time()
@@ -332,7 +354,17 @@ class DeepLearningTrainer:
         rate_t = torch.zeros((), dtype=torch.float32, device=dev)
         mom_t = torch.zeros((), dtype=torch.float32, device=dev)
         on_t = torch.zeros((), dtype=torch.float32, device=dev)
-        gbuf = torch.empty(fp.g.numel() + 1, dtype=fp.g.dtype, device=fp.g.device) if sharded else None
+        gbuf = torch.empty(fp.g.numel() + 1, dtype=fp.g.dtype, device=fp.g.device) if gsync else None
+        # elastic averaging: consensus parameters w_EA and the device switch of the elastic pull (off until
+        # the first consensus exists, as the reference's null _wEA in the first iteration)
+        ea_lam = float(p.get("elastic_averaging_regularization") or 0.0)
+        ea_pa = float(p.get("elastic_averaging_moving_rate") or 0.9)
+        if elastic and not (0.0 < ea_pa <= 1.0):
+            raise ValueError("elastic_averaging_moving_rate must be in (0, 1]")
+        # (allocated up front: captured step graphs read it in place)
+        ea = torch.zeros(fp.p.numel() * (3 if bool(p["adaptive_rate"]) else 2) if elastic else 0,
+                         dtype=torch.float32, device=dev)
+        ea_on = torch.zeros((), dtype=torch.float32, device=dev)
         tdim = tuple(yt.shape[1:]) if yt is not None else ()
 
         # sparse autoencoder (Neurons.compute_sparsity / update_bias): a rolling mean activation per neuron
@@ -349,7 +381,7 @@ class DeepLearningTrainer:
             fp.zero_grad()
             net.track = {} if sparse else None
             with torch.autocast(device_type=dev.type, dtype=dtype, enabled=dtype is not None):
-                o = net(xb, seed)
+                o = net(xb, dseed)
             ls = self._loss(o.float(), xb if ae else tb, wb, cat, dist, ae)
             if sparse:
                 dec = 0.999 ** xb.shape[0]
@@ -357,7 +389,7 @@ class DeepLearningTrainer:
                     a.mul_(dec).add_(net.track[l] * (1.0 - dec))
                     ls = ls + wb.sum() * beta_sp * ((a - tgt_a) * net.hidden[l].bias.float()).sum()
                 net.track = None
-            if sharded:
+            if gsync:
                 ls.backward()
                 gbuf[:-1].copy_(fp.g)
                 gbuf[-1:].copy_(wb.sum().view(1))
@@ -368,8 +400,10 @@ class DeepLearningTrainer:
             """Optimizer step on the flat buffers (ADADELTA: one fused HIP launch; momentum SGD with rate
             annealing / Nesterov from the device scalars rate_t, mom_t, on_t), then max_w2 row clipping."""
             with torch.no_grad():
-                if sharded:       # data parallel: the all-reduced [sum-gradient, batch weight] -> mean gradient
+                if gsync:         # data parallel: the all-reduced [sum-gradient, batch weight] -> mean gradient
                     fp.g.copy_(gbuf[:-1] / gbuf[-1].clamp(min=1e-12))
+                if elastic and ea_lam > 0:   # elastic pull towards the consensus (Neurons.java:263,414)
+                    fp.g.add_((fp.p - ea[: fp.p.numel()]) * (ea_on * ea_lam))
                 if adaptive:      # ADADELTA (Neurons.java: rho, epsilon); also refreshes the bf16 weights
                     fp.adadelta(rho, eps, l1, l2, shadow)
                 else:
@@ -433,13 +467,13 @@ class DeepLearningTrainer:
             def fwd_bwd(xb, wb, tb):      # noqa: F811 - the explicit step replaces the autograd one
                 with torch.no_grad():
                     fp.g[fp.n_decay:].zero_()
-                    if not sharded:
+                    if not gsync:
                         torch.reciprocal(wb.sum().clamp(min=1e-12).view(1), out=inv_t)
                     hs = [xb if xb.dtype == cdt else xb.to(cdt)]
                     seeds = []
                     for i, lin in enumerate(net.hidden):
                         drop = net.hid_drop[i]
-                        base = (seed * 1000003 + i * 7919) & ((1 << 62) - 1)
+                        base = (dseed * 1000003 + i * 7919) & ((1 << 62) - 1)
                         sd = (base, net.step_dev) if net.step_dev is not None else (step_seed(base, net.step), None)
                         seeds.append(sd)
                         a_ = torch.mm(hs[-1], Wc[i].t())
@@ -457,7 +491,7 @@ class DeepLearningTrainer:
                         gW[i].copy_(torch.mm(dA.t(), hs[i]))
                         if i > 0:
                             dh = torch.mm(dA, Wc[i])
-                    if sharded:
+                    if gsync:
                         gbuf[:-1].copy_(fp.g)
                         gbuf[-1:].copy_(wb.sum().view(1))
 
@@ -469,11 +503,11 @@ class DeepLearningTrainer:
                 and dlops.supported(int(Z.shape[1]), [int(h_) for h_ in hidden], int(net.out.weight.shape[0]),
                                     act_code, Z)):
             fz["ok"] = True
-            fz["bases"] = [(seed * 1000003 + i * 7919) & ((1 << 62) - 1) for i in range(len(net.hidden))]
+            fz["bases"] = [(dseed * 1000003 + i * 7919) & ((1 << 62) - 1) for i in range(len(net.hidden))]
 
         def fused_build(cap):
-            gout = gbuf[:-1] if sharded else fp.g
-            gsum = gbuf[-1:] if sharded else None
+            gout = gbuf[:-1] if gsync else fp.g
+            gsum = gbuf[-1:] if gsync else None
             fz["obj"] = dlops.FusedMLPStep(fp, list(net.hidden) + [net.out], act_code, list(net.hid_drop),
                                            fz["bases"], Z, wf, yt, cat == "Regression", cap, shadow, step_t, gout,
                                            gsum)
@@ -513,11 +547,11 @@ class DeepLearningTrainer:
                 side.wait_stream(torch.cuda.current_stream(dev))
                 with torch.cuda.stream(side):
                     fwd_bwd(sx, sw, sy)
-                    if not sharded:
+                    if not gsync:
                         update()
                 torch.cuda.current_stream(dev).wait_stream(side)
                 gstate["warm"] += 1
-                if sharded:
+                if gsync:
                     coll.all_reduce_(gbuf)
                     update()
                 return
@@ -526,10 +560,10 @@ class DeepLearningTrainer:
                     g1 = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(g1):
                         fwd_bwd(sx, sw, sy)
-                        if not sharded:
+                        if not gsync:
                             update()
                     g2 = None
-                    if sharded:
+                    if gsync:
                         g2 = torch.cuda.CUDAGraph()
                         with torch.cuda.graph(g2):
                             update()
@@ -538,19 +572,19 @@ class DeepLearningTrainer:
                     gstate.update(g1=False, error=f"{type(e).__name__}: {e}")
             if gstate["g1"] is False:
                 fwd_bwd(sx, sw, sy)
-                if sharded:
+                if gsync:
                     coll.all_reduce_(gbuf)
                 update()
                 return
             gstate["g1"].replay()
-            if sharded:
+            if gsync:
                 coll.all_reduce_(gbuf)
                 gstate["g2"].replay()
 
-        # Single process: CH consecutive steps (gather of the batch rows from the resident design matrix
-        # included) are captured in ONE graph and replayed per chunk — the host issues one index copy, one
-        # arange and one replay per CH steps instead of launching ~40 kernels per step.
-        CH = max(1, int(os.environ.get("H2O_DL_CHUNK", "16"))) if (use_graph and not sharded) else 1
+        # Single process (and each rank of a model-averaging run): CH consecutive steps (gather of the batch
+        # rows from the resident design matrix included) are captured in ONE graph and replayed per chunk — the
+        # host issues one index copy, one arange and one replay per CH steps instead of ~40 kernels per step.
+        CH = max(1, int(os.environ.get("H2O_DL_CHUNK", "16"))) if (use_graph and not gsync) else 1
         chunk = dict(g=None)
         if CH > 1:
             ridx = torch.zeros(CH * B, dtype=torch.long, device=dev)
@@ -603,7 +637,8 @@ class DeepLearningTrainer:
         # global row order per epoch: mini-batches are consecutive B-slices of a permutation of the GLOBAL
         # rows; under row sharding each rank takes the members of the batch it owns (one host sync per
         # epoch for the per-step counts), so the summed gradient is the single-process one
-        S_ep = N_glob // B
+        N_perm = N if dp_avg else N_glob       # model averaging: each rank walks its own rows
+        S_ep = N_perm // B
         perm = None
         sel = offs = None
         s_in = S_ep
@@ -619,17 +654,69 @@ class DeepLearningTrainer:
             tspi = int(max(1, min(epochs * N_glob / 10, 100000 * coll.world())))
         elif tspi < -2:
             raise ValueError("train_samples_per_iteration must be -2, -1, 0 or > 0")
+        spi = 0
+        if dp_avg:
+            # steps per iteration (the averaging period), a multiple of the graph chunk when it is longer: the
+            # collective falls between two chunk replays
+            spi = max(1, int(round(tspi / Bg)))
+            if spi >= CH > 1:
+                spi = max(CH, int(round(spi / CH)) * CH)
+            tspi = spi * Bg
         model.output["actual_train_samples_per_iteration"] = tspi
+        n_avg = 0
+
+        def dp_average():
+            """End of an iteration (DeepLearningTask.reduce + postGlobal): ONE all-reduce of [weights+biases,
+            optimizer state] / W; elastic: the consensus time average (DeepLearningModelInfo.timeAverage)."""
+            nonlocal n_avg
+            if dp_local:          # H2O_DL_DP=local (tests): the per-rank local models, never averaged
+                n_avg += 1
+                return
+            st = [fp.p] + ([fp.eg2, fp.edx2] if adaptive else [mom])
+            buf = torch.cat(st)
+            coll.all_reduce_(buf)
+            buf.div_(Wn)
+            n_avg += 1
+            if elastic:
+                if n_avg == 1:
+                    ea.copy_(buf)
+                else:
+                    ea.mul_(1.0 - ea_pa).add_(buf, alpha=ea_pa)
+                ea_on.fill_(1.0)
+                return
+            o = 0
+            with torch.no_grad():
+                for t_ in st:
+                    t_.copy_(buf[o:o + t_.numel()])
+                    o += t_.numel()
+                if shadow is not None:
+                    shadow.copy_(fp.p[: fp.n_decay])
+                if fz.get("obj") is not None:
+                    fz["obj"].refresh_transposed()
+
+        def consensus_swap():
+            """elastic: put the consensus weights in place for scoring; returns the local ones."""
+            if not elastic or n_avg == 0:
+                return None
+            loc = fp.p.detach().clone()
+            with torch.no_grad():
+                fp.p.copy_(ea[: fp.p.numel()])
+            return loc
+
+        def local_restore(loc):
+            if loc is not None:
+                with torch.no_grad():
+                    fp.p.copy_(loc)
         n_iter_done = 0
         step = 0
-        spe = max(1, N_glob // B)
+        spe = max(1, N_perm // B)
         t_loop0 = time.time()
         t_scoring = 0.0
         while step < total:
             if s_in >= S_ep:
-                perm = torch.randperm(N_glob, generator=g, device=dev)
+                perm = torch.randperm(N_perm, generator=g, device=dev)
                 s_in = 0
-                if sharded:
+                if gsync:
                     mine = (perm >= row0) & (perm < row0 + N)
                     mine[S_ep * B:] = False
                     sel = torch.nonzero(mine).squeeze(1)
@@ -643,12 +730,12 @@ class DeepLearningTrainer:
             net.train()
             n = 1
             if (CH > 1 and gstate["warm"] >= 2 and chunk["g"] is not False and s_in + CH <= S_ep
-                    and step + CH <= total):
+                    and step + CH <= total and (not dp_avg or step % spi + CH <= spi)):
                 net.step = step
                 if run_chunk(perm[s_in * B:(s_in + CH) * B], step, samples):
                     n = CH
             if n == 1:
-                if sharded:
+                if gsync:
                     rows = perm[sel[offs[s_in]:offs[s_in + 1]]] - row0
                 else:
                     rows = perm[s_in * B:(s_in + 1) * B]
@@ -675,11 +762,11 @@ class DeepLearningTrainer:
                     run_step()
                 else:
                     fwd_bwd(Z.index_select(0, rows), wf.index_select(0, rows), None if ae else yt.index_select(0, rows))
-                    if sharded:
+                    if gsync:
                         coll.all_reduce_(gbuf)
                     update()
             s_in += n
-            samples += n * B
+            samples += n * Bg
             last = step + n - 1
             if self.job is not None and (step // 50) != ((last + 1) // 50):
                 self.job.set_progress(last / max(total, 1))
@@ -692,8 +779,11 @@ class DeepLearningTrainer:
             if sharded:                          # every rank must take the same scoring decision
                 timed = coll.agree(timed)
             step = last + 1
+            if dp_avg and (it_end or end):
+                dp_average()
             if end or timed or first_it:
                 last_score = time.time()
+                loc = consensus_swap()
                 ev = self._score(model, X, y, w, samples / N_glob, valid)
                 t_scoring += time.time() - last_score
                 history.append({k: v for k, v in ev.items() if not k.startswith("_")})
@@ -702,6 +792,7 @@ class DeepLearningTrainer:
                     lv = self._model_loss(ev.get("_valid") or ev.get("_train"), cat, ae)
                     if lv < best_loss:     # DeepLearningModel.doScoring: keep the lowest-loss weights
                         best_loss, best_p, best_ev = lv, fp.p.detach().clone(), ev
+                local_restore(loc)
                 mref = ev.get("_valid") or ev.get("_train")
                 if mref is not None and not end and keeper.add(mref):
                     break
@@ -719,6 +810,12 @@ class DeepLearningTrainer:
             ("graph_chunk%d" % CH if chunk.get("g") not in (None, False) else
              ("graph_step" if gstate.get("g1") not in (None, False) else "eager (" + str(gstate.get("error") or chunk.get("error")) + ")")))
         net.step_dev = None
+        if elastic and n_avg:               # the consensus is the model (DeepLearningTask.postGlobal)
+            with torch.no_grad():
+                fp.p.copy_(ea[: fp.p.numel()])
+        model.output["data_parallel"] = ("model_averaging" + ("_elastic" if elastic else "")) if dp_avg else (
+            "gradient_sync" if gsync else None)
+        model.output["averaging_rounds"] = n_avg
         final_ev = last_ev
         if owb and best_p is not None:
             final = self._model_loss(last_ev.get("_valid") or last_ev.get("_train"), cat, ae)

@@ -117,10 +117,13 @@ class KMeansTrainer:
         if how == "user" and self.p.get("user_points") is not None:
             up = self.p["user_points"]
             U = up.as_tensor() if hasattr(up, "as_tensor") else torch.as_tensor(np.asarray(up, dtype=np.float32))
-            U = self.ex_train.transform(U.T.contiguous().to(dev)) if U.shape[1] == self.info.F else U.to(dev).float()
+            # decide the space of the points BEFORE transforming / padding them: original-feature points are
+            # centred by ex_train.transform already; only design-space points still need the shift
+            orig = U.shape[1] == self.info.F
+            U = self.ex_train.transform(U.T.contiguous().to(dev)) if orig else U.to(dev).float()
             if U.shape[1] < Z.shape[1]:
                 U = torch.nn.functional.pad(U, (0, Z.shape[1] - U.shape[1]))
-            if self.ex_train is not self.ex and U.shape[1] != self.info.F:   # user points given in design space
+            if self.ex_train is not self.ex and not orig:   # user points given in design space
                 U = U - torch.nn.functional.pad(self._shift, (0, Z.shape[1] - self._shift.numel())).float()
             return U
         first = int(rng.integers(N))

@@ -28,10 +28,8 @@ HINTS = {
     "score_iteration_interval", "score_validation_sampling", "u_name", "loading_name", "build_glm_model",
     "compute_metrics", "num_iteration_without_new_exemplar",
     "eval_metric", "export_checkpoints_dir", "gradient_epsilon", "svd_method",
-    # DeepLearning: elastic averaging blends per-node local models into the global one between map/reduce
-    # rounds; with synchronous data parallelism every rank holds the global model after each step, so it
-    # is the identity here. ``sparse`` is a storage hint for sparse input.
-    "elastic_averaging", "elastic_averaging_moving_rate", "elastic_averaging_regularization", "sparse",
+    # DeepLearning ``sparse`` is a storage hint for sparse input.
+    "sparse",
 }
 
 # parameters not implemented by this engine: a non-default value is refused

@@ -27,8 +27,15 @@ _HIP_SIGS = {
     "h2o_tree_level": [c_void_p, c_int, c_int, c_void_p],
     "h2o_tree_find": [c_void_p, c_int, c_void_p],
     "h2o_tree_grow": [c_void_p, c_int, c_int, c_void_p],
-    "h2o_hist_pack": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
-    "h2o_tree_subtract": [c_void_p, c_int, c_void_p],
+    "h2o_hist_pack": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p],
+    "h2o_tree_dist": [c_void_p, c_void_p],
+    "h2o_rccl_load": [ctypes.c_char_p],
+    "h2o_rccl_version": [],
+    "h2o_rccl_unique_id": [c_void_p],
+    "h2o_rccl_id_bytes": [],
+    "h2o_rccl_init": [c_void_p, c_int, c_void_p, c_int],
+    "h2o_rccl_destroy": [c_void_p, c_int],
+    "h2o_rccl_coll": [c_void_p, c_int, c_void_p, c_void_p, c_ll, c_int, c_void_p],
     "h2o_tree_all": [c_void_p, c_void_p],
     "h2o_tree_leaves": [c_void_p, c_void_p],
     "h2o_hist_build": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p,
@@ -37,12 +44,11 @@ _HIP_SIGS = {
                        c_double, c_double, c_double, c_int, c_int, c_ull, c_int, c_void_p, c_void_p, c_void_p, c_int,
                        c_int, c_int, c_void_p],
     "h2o_split_reduce": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_ull, c_int, c_void_p, c_void_p, c_void_p,
-                         c_void_p],
+                         c_int, c_void_p],
     "h2o_ic_next": [c_void_p] * 6 + [c_int, c_void_p, c_int, c_void_p],
     "h2o_plan": [c_void_p] * 14 + [c_int, c_int, c_double, c_int, c_int, c_void_p],
     "h2o_ranges": [c_void_p] * 6,
     "h2o_zero_hist": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
-    "h2o_subtract": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
     "h2o_route": [c_void_p] * 6 + [c_int] + [c_void_p] * 10 + [c_int, c_ll, c_int, c_void_p],
     "h2o_leaf_assign": [c_void_p, c_int, c_ll, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                         c_void_p, c_int, c_int, c_void_p],
@@ -54,7 +60,7 @@ _HIP_SIGS = {
     "h2o_kmeans_mfma": [c_void_p, c_ll, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p],
     "h2o_qscale": [c_void_p, c_void_p, c_void_p, c_ll, c_void_p],
     "h2o_hist_reduce": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
-                        c_void_p, c_int, c_void_p],
+                        c_void_p, c_int, c_int, c_int, c_void_p],
     "h2o_leaf_values": [c_void_p, c_int, c_int, c_double, c_double, c_double, c_double, c_double, c_void_p, c_void_p],
     "h2o_gbm_step": [c_ll, c_ll, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_float, c_ull,
                      ctypes.c_float, c_void_p, c_void_p, c_void_p],
@@ -66,7 +72,7 @@ _HIP_SIGS = {
 # Bumped whenever a C launcher's argument list changes; every native library exports h2o_abi_version()
 # (csrc/abi.h) and a library built from older sources is refused instead of being called with shifted
 # arguments.
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 
 def _check_abi(lib, name: str) -> None:

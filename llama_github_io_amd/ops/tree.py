@@ -455,7 +455,8 @@ class _TreePlan(ctypes.Structure):
                 [("ic_map", _vp), ("ic", _vp * _MAXL)] +
                 [(n, _ci) for n in ("sliced", "fs0", "fsn", "sslot")] + [("cand_local", _vp), ("hrecv", _vp)] +
                 [("leaf_lam", _cd), ("leaf_l1", _cd)] + [("planar", _ci), ("no_na", _ci)] +
-                [("fgroup", _vp)])
+                [("fgroup", _vp)] + [("coll_fn", _vp), ("coll_ctx", _vp)] +
+                [(n, _ci) for n in ("W", "cf32", "cand_fs", "dist")] + [(n, _vp) for n in ("hsend", "cand_all", "lsx")])
 
 
 class _Arena:
@@ -594,47 +595,72 @@ class GpuTreeBuilder:
         self._init_comm(capmax)
 
     def _init_comm(self, capmax: int):
-        """Row-sharded histogram exchange (reference: ScoreBuildHistogram2 + MRTask reduce). Default
-        ``H2O_TREE_COMM=rs``: feature-sliced — each level's built-node histograms are packed by feature slice
-        (k_hist_pack) and REDUCE-SCATTERED, so every rank holds the global histograms of F/W features only,
-        searches splits on that slice, and the per-(node, feature) candidates are ALL-GATHERED (a few KB) so
-        every rank takes the same decisions. ``ar``: all-reduce the full node histograms (every rank searches
-        every feature). Both end with one all-reduce of the leaf sums (+ the root weight)."""
+        """Row-sharded histogram exchange (reference: ScoreBuildHistogram2 + MRTask reduce), run by the native
+        driver ``h2o_tree_dist``: one host call per tree enqueues every kernel and collective on the stream.
+
+        ``H2O_TREE_COMM=ar`` (default): each level's built-node histograms are ALL-REDUCED, every rank searches
+        every feature of the same global histograms — one collective per level (the exchange is latency-bound:
+        a depth-6 HIGGS tree moves 32 histogram slots, 3.7 MB in fp64, in 6 level collectives).
+        ``rs``: feature-sliced — the histograms are packed by feature slice (k_hist_pack) and REDUCE-SCATTERED, so
+        every rank holds the global histograms of F/W features only and searches that slice; the per-(node,
+        feature) candidates are ALL-GATHERED (a few KB, read in place rank-major) — two collectives per level,
+        1/W of the split search each. Both end with one all-reduce of the leaf sums (+ the root weight).
+        Wire dtype ``H2O_TREE_COMM_DTYPE``: ``f64`` (default; decisions equal the single-process ones, exact
+        ties included) or ``f32`` (half the bytes; a tie between two equal-gain splits may break differently).
+
+        Transport: RCCL from C++ when the process group runs ``nccl`` (:class:`parallel.rccl.NativeComm`), else
+        the same driver with host-staged callbacks (:class:`parallel.rccl.HostTransport`, gloo).
+        ``H2O_TREE_COMM_FORCE=ar|rs`` runs the row-sharded driver at world size 1 (a 1-rank RCCL communicator):
+        the 1-GPU rehearsal of the multi-GPU path."""
+        force = os.environ.get("H2O_TREE_COMM_FORCE", "")
+        self.dist_mode = coll.is_dist() or force in ("rs", "ar")
         self.W = coll.world() if coll.is_dist() else 1
-        self.sliced = self.W > 1 and os.environ.get("H2O_TREE_COMM", "rs") == "rs"
+        mode = force if force in ("rs", "ar") else os.environ.get("H2O_TREE_COMM", "ar")
+        self.sliced = self.dist_mode and mode == "rs"
+        self.cf32 = int(self.dist_mode and os.environ.get("H2O_TREE_COMM_DTYPE", "f64") == "f32")
         self.fs = self.fs0 = self.fsn = 0
         self.sslot = self.slot
-        if not self.sliced:
+        self.transport = None
+        if not self.dist_mode:
             return
         W, F, dev = self.W, self.F, self.dev
-        self.fs = Fs = (F + W - 1) // W
-        self.fs0 = min(F, coll.rank() * Fs)
-        self.fsn = max(0, min(F, self.fs0 + Fs) - self.fs0)
-        self.sslot = Fs * 2 * NBIN + Fs + 1
-        self.hsend = torch.empty(W * capmax * self.sslot, dtype=torch.float64, device=dev)
-        self.hrecv = torch.empty(capmax * self.sslot, dtype=torch.float64, device=dev)
-        self.cand_local = torch.zeros(capmax * Fs * CAND_BYTES, dtype=torch.uint8, device=dev)
-        self.cand_all = torch.empty(W * capmax * Fs * CAND_BYTES, dtype=torch.uint8, device=dev)
-        # leaf sums + the root weight (written by the owner of feature 0) in one all-reduce
-        self.lsx = torch.zeros(self.leaf_cap * 2 + 1, dtype=torch.float64, device=dev)
-        self._rootw = self.av["rootw"].view(torch.float64)
+        wire = torch.float32 if self.cf32 else torch.float64
+        self.hsend = self.cand_local = self.cand_all = self.lsx = None
+        if self.sliced:
+            self.fs = Fs = (F + W - 1) // W
+            self.fs0 = min(F, coll.rank() * Fs)
+            self.fsn = max(0, min(F, self.fs0 + Fs) - self.fs0)
+            self.sslot = Fs * 2 * NBIN + Fs + 1
+            self.hsend = torch.empty(W * capmax * self.sslot, dtype=wire, device=dev)
+            self.cand_local = torch.zeros(capmax * Fs * CAND_BYTES, dtype=torch.uint8, device=dev)
+            self.cand_all = torch.zeros(W * capmax * Fs * CAND_BYTES, dtype=torch.uint8, device=dev)
+            # leaf sums + the root weight (written by the owner of feature 0) in one all-reduce
+            self.lsx = torch.zeros(self.leaf_cap * 2 + 1, dtype=torch.float64, device=dev)
+        else:
+            self.sslot = self.used            # exchanged slots hold the used values of a slot
+        self.hrecv = torch.empty(capmax * self.sslot, dtype=wire, device=dev)
+        from ..parallel import rccl
+        comm = rccl.native_comm(force=bool(force))
+        if comm is not None:
+            self.transport = comm
+        else:
+            bufs = [self.hist[0], self.hbuild, self.leafsum, self.hsend, self.hrecv, self.cand_local,
+                    self.cand_all, self.lsx]
+            self.transport = rccl.HostTransport(bufs)
 
-    def _rs_hist(self, src_ptr: int, n: int, out: torch.Tensor, s):
-        """Pack n build slots by feature slice and reduce-scatter them: ``out`` [n * sslot] = this rank's
-        slice of the global histograms."""
-        E = self.sslot
-        nat.check(self.lib.h2o_hist_pack(src_ptr, self.slot, self.F, self.fs, self.W, n, self.hsend.data_ptr(), s),
-                  "hist_pack")
-        coll.reduce_scatter_(out[: n * E], self.hsend[: self.W * n * E])
-
-    def _ag_cands(self, d: int):
-        """All-gather every rank's [cap][Fs] candidates into cand [cap][F] (rank r holds features r*Fs..)."""
-        cap, Fs, W, CB = self.caps[d], self.fs, self.W, CAND_BYTES
-        n = cap * Fs * CB
-        g = self.cand_all[: W * n]
-        coll.all_gather_into_(g, self.cand_local[:n])
-        full = g.view(W, cap, Fs, CB).permute(1, 0, 2, 3).reshape(cap, W * Fs, CB)[:, : self.F]
-        self.cand[: cap * self.F * CB].view(cap, self.F, CB).copy_(full)
+    def comm_per_tree(self) -> tuple:
+        """(collectives, bytes handed to them) of one row-sharded tree of full depth (the driver's sequence is
+        fixed: levels past the last split run on empty node lists)."""
+        D, W = self.D, self.W
+        if not self.dist_mode:
+            return 0, 0
+        es = 4 if self.cf32 else 8
+        slots = [1] + self.caps[:D - 1]
+        if self.sliced:
+            rs = sum(W * n * self.sslot * es for n in slots)
+            ag = sum(self.caps[d] * self.fs * CAND_BYTES for d in range(D))
+            return len(slots) + D + 1, rs + ag + (self.leaf_cap * 2 + 1) * 8
+        return len(slots) + 1, sum(n * self.sslot * es for n in slots) + self.leaf_cap * 2 * 8
 
     def _p(self, name):
         return self._pt[name]
@@ -698,7 +724,12 @@ class GpuTreeBuilder:
         P.planar = int(self.planar)
         P.no_na = int(self._no_na())
         P.cand_local = self.cand_local.data_ptr() if self.sliced else 0
-        P.hrecv = self.hrecv.data_ptr() if self.sliced else 0
+        P.hrecv = self.hrecv.data_ptr() if self.dist_mode else 0
+        P.W, P.cf32, P.cand_fs, P.dist = self.W, self.cf32, self.fs, int(self.dist_mode)
+        if self.sliced:
+            P.hsend, P.cand_all, P.lsx = self.hsend.data_ptr(), self.cand_all.data_ptr(), self.lsx.data_ptr()
+        if self.transport is not None:
+            P.coll_fn, P.coll_ctx = self.transport.fn, self.transport.ctx
         return P
 
     def _no_na(self) -> bool:
@@ -776,60 +807,21 @@ class GpuTreeBuilder:
             P.log_link, P.scale, P.kclamp, P.mx = int(lg), float(scale), float(kclamp), float(mx)
             P.leaf_lam, P.leaf_l1 = float(lam), float(l1)
         ref = ctypes.byref(P)
-        if not coll.is_dist():
+        if not self.dist_mode:
             nat.check(lib.h2o_tree_all(ref, s), "tree_all")
-        elif self.sliced:
-            self._build_sliced(ref, P, leaf_native, s)
         else:
-            nat.check(lib.h2o_tree_root(ref, s), "tree_root")
-            coll.all_reduce_(self.hist[0][: self.slot])
-            for d in range(self.D):
-                r = lib.h2o_tree_level(ref, d, 1, s)
-                if r < 0:
-                    nat.check(-r, "tree_level")
-                if r == 1:
-                    break
-                coll.all_reduce_(self.hbuild[: self.caps[d] * self.slot])
-                nat.check(lib.h2o_tree_subtract(ref, d, s), "tree_subtract")
-            nat.check(lib.h2o_tree_leaves(ref, s), "tree_leaves")
-            coll.all_reduce_(self.leafsum)
-            if leaf_native is not None:
-                nat.check(lib.h2o_leaf_values(self.leafsum.data_ptr(), self.leaf_cap, P.log_link, P.scale, P.kclamp,
-                                              P.mx, P.leaf_lam, P.leaf_l1, self._p("leafval"), s), "leaf_values")
+            rc = lib.h2o_tree_dist(ref, s)
+            err = getattr(self.transport, "error", None)
+            if err is not None:
+                self.transport.error = None
+                raise RuntimeError(f"tree collective failed: {err}") from err
+            nat.check(rc, "tree_dist")
+            if isinstance(self.transport, _native_comm_cls()):   # (host transport counts its own calls)
+                coll.add_stats(*self.comm_per_tree())
         if leaf_native is None and leaf_fn is not None:
             vals = leaf_fn(self.leafsum)
             self.av["leafval"].view(torch.float32)[: vals.numel()].copy_(vals.to(torch.float32))
         return self._snapshot()
-
-    def _build_sliced(self, ref, P, leaf_native, s):
-        """Feature-sliced row-sharded tree: per level one reduce-scatter of the built-node histograms
-        (1/W of them land on each rank) and one all-gather of split candidates; one all-reduce at the end."""
-        lib, E = self.lib, self.sslot
-        nat.check(lib.h2o_tree_root(ref, s), "tree_root")
-        self._rs_hist(self.hbuild.data_ptr(), 1, self.hist[0], s)
-        for d in range(self.D):
-            nat.check(lib.h2o_tree_find(ref, d, s), "tree_find")
-            self._ag_cands(d)
-            r = lib.h2o_tree_grow(ref, d, 1, s)
-            if r < 0:
-                nat.check(-r, "tree_grow")
-            if r == 1:
-                break
-            self._rs_hist(self.hbuild.data_ptr(), self.caps[d], self.hrecv, s)
-            nat.check(lib.h2o_tree_subtract(ref, d, s), "tree_subtract")
-        nat.check(lib.h2o_tree_leaves(ref, s), "tree_leaves")
-        L2 = self.leaf_cap * 2
-        self.lsx[:L2].copy_(self.leafsum.view(-1))
-        if self.fs0 == 0 and self.fsn > 0:
-            self.lsx[L2:].copy_(self._rootw)
-        else:
-            self.lsx[L2:].zero_()
-        coll.all_reduce_(self.lsx)
-        self.leafsum.view(-1).copy_(self.lsx[:L2])
-        self._rootw.copy_(self.lsx[L2:])
-        if leaf_native is not None:
-            nat.check(lib.h2o_leaf_values(self.leafsum.data_ptr(), self.leaf_cap, P.log_link, P.scale, P.kclamp,
-                                          P.mx, P.leaf_lam, P.leaf_l1, self._p("leafval"), s), "leaf_values")
 
     def _snapshot(self):
         # the tree's structure travels to pinned host memory asynchronously: the host decodes finished
@@ -884,6 +876,11 @@ class GpuTreeBuilder:
         n_leaves = int(arr("counters", np.int32)[0])
         vals = arr("leafval", np.float32)[:n_leaves].copy()
         return TreeLevels(decs, cls, crs, n_leaves, vals, root_weight)
+
+
+def _native_comm_cls():
+    from ..parallel.rccl import NativeComm
+    return NativeComm
 
 
 # ================================================================================================

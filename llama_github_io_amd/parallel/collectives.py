@@ -60,6 +60,12 @@ def stats(reset: bool = False) -> dict:
     return out
 
 
+def add_stats(calls: int, nbytes: int) -> None:
+    """Account collectives issued from native code (the tree driver's RCCL calls)."""
+    _stats["calls"] += int(calls)
+    _stats["bytes"] += int(nbytes)
+
+
 def _count(t: torch.Tensor):
     _stats["calls"] += 1
     _stats["bytes"] += t.numel() * t.element_size()

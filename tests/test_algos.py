@@ -114,6 +114,23 @@ def test_kmeans_and_estimate_k():
     assert m.output["k"] == 3
 
 
+def test_kmeans_user_points_original_space_offset_with_categorical():
+    """user points given in ORIGINAL feature space are centred by the transform once; with a
+    categorical column the design is wider than F and the points must not be shifted a second time."""
+    from llama_github_io_amd.models.kmeans import KMeansTrainer
+    g = torch.Generator().manual_seed(4)
+    N = 1500
+    cs = torch.tensor([[100.0, 110, 0], [120, 100, 1], [90, 90, 2]])
+    lab = torch.arange(N) % 3
+    X = cs[lab].T.clone()
+    X[:2] += 0.5 * torch.randn(2, N, generator=g)
+    info = DataInfo(["a", "b", "c"], np.array([0, 0, 1], np.int32), [None, None, ["x", "y", "z"]], None, None)
+    m = KMeansTrainer(dict(k=3, init="User", user_points=cs.numpy(), max_iterations=1, standardize=False,
+                           seed=1)).fit(X, None, None, None, info)
+    C = np.asarray(m.output["centers"], dtype=np.float64)
+    np.testing.assert_allclose(C[:, -2:], cs[:, :2].numpy(), atol=0.2)   # centers: one-hot levels, then numerics
+
+
 def test_deeplearning_regression_and_autoencoder():
     from llama_github_io_amd.models.deeplearning import DeepLearningTrainer
     Xr, yr, infor = _reg()

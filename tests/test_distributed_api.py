@@ -158,7 +158,9 @@ def _run_cases(csv, names, out_path):
 def _worker(rank, world, port, csv, names, out_path):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank), H2O_AMD_DEVICE="cpu", OMP_NUM_THREADS="1",
-                      H2O_AGG_CHUNK="250")   # aggregator chunks straddle the shard boundaries
+                      H2O_AGG_CHUNK="250",   # aggregator chunks straddle the shard boundaries
+                      H2O_DL_DP="sync")      # DeepLearning: per-step gradient sync (== single process);
+    # the default model-averaging mode is pinned by tests/test_dl_model_averaging.py
     _run_cases(csv, names, out_path)
     import torch.distributed as dist
     if dist.is_initialized():

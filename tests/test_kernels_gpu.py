@@ -375,6 +375,25 @@ def test_kmeans_offset_data_matches_cpu(init):
         assert float(((centers.numpy() + 1e4 - c) ** 2).sum(1).min()) < 0.05
 
 
+def test_kmeans_user_points_offset_padded_matches_cpu():
+    """standardize=False, F=6 (padded to 8 columns on the GPU), data offset by 1e4, init=User with
+    points in original space: the device run starts from the user's points, as the CPU run does."""
+    from llama_github_io_amd.models.kmeans import KMeansTrainer
+    g = torch.Generator().manual_seed(8)
+    N, F = 40000, 6
+    centers = torch.randn(4, F, generator=g) * 4
+    lab = torch.randint(0, 4, (N,), generator=g)
+    X = (centers[lab] + 0.3 * torch.randn(N, F, generator=g)).T.contiguous() + 1e4
+    info = _info(F)
+    info.response = None
+    prm = dict(k=4, max_iterations=1, init="User", user_points=(centers + 1e4).numpy(), seed=7, standardize=False)
+    mg = KMeansTrainer(prm).fit(X.to(dev), None, None, None, info)
+    mc = KMeansTrainer(prm).fit(X, None, None, None, info)
+    cg = np.array(mg.output["centers"])
+    np.testing.assert_allclose(cg, np.array(mc.output["centers"]), rtol=0, atol=1e-3)
+    np.testing.assert_allclose(cg, (centers + 1e4).numpy(), atol=0.05)
+
+
 @pytest.mark.parametrize("n,idt,vdt", [(10, torch.int64, torch.float64), (3000, torch.int32, torch.float32),
                                        (16384, torch.int64, torch.float32), (1, torch.int32, torch.float64)])
 def test_segment_sum_kernel_matches_index_add(n, idt, vdt):

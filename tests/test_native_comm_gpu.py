@@ -1,0 +1,129 @@
+"""The row-sharded tree driver (``h2o_tree_dist``) on RCCL, rehearsed on one GPU.
+
+RCCL refuses two ranks on one device, so a 1-GPU box runs the multi-GPU code path with a 1-RANK RCCL
+communicator (``H2O_TREE_COMM_FORCE``): every kernel of the histogram exchange (k_hist_pack into the fp64 or fp32
+wire format, all-reduce or feature-sliced reduce-scatter + rank-major candidate all-gather read in place, sibling
+subtraction from the received slots, leaf-sum all-reduce) runs through ``ncclAllReduce`` / ``ncclReduceScatter`` /
+``ncclAllGather`` on the compute stream. Multi-rank protocol correctness is pinned by the same native driver
+under gloo at world 2/3 (``tests/test_distributed_gpu.py``). Oracle: :class:`RefTreeBuilder` (fp64 NumPy)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+from llama_github_io_amd.ops import tree as T
+from llama_github_io_amd.ops.binning import apply_binning, fit_binning
+
+pytestmark = pytest.mark.gpu
+
+from test_tree_engine import _data  # noqa: E402
+
+
+@pytest.fixture
+def force_env(monkeypatch):
+    def set_(mode, dtype="f32"):
+        monkeypatch.setenv("H2O_TREE_COMM_FORCE", mode)
+        monkeypatch.setenv("H2O_TREE_COMM_DTYPE", dtype)
+    return set_
+
+
+def test_rccl_one_rank_collectives(force_env):
+    from llama_github_io_amd.parallel import rccl
+    c = rccl.native_comm(force=True)
+    assert c is not None and c.world == 1
+    x = torch.arange(1000, dtype=torch.float64, device="cuda")
+    y = torch.empty_like(x)
+    c.collective(rccl.OP_ALLREDUCE, x, y, 1000, rccl.DT_F64)
+    c.collective(rccl.OP_REDUCE_SCATTER, x.float(), y.float(), 1000, rccl.DT_F32)
+    z = torch.empty(1000, dtype=torch.float32, device="cuda")
+    c.collective(rccl.OP_ALLGATHER, x.float().contiguous(), z, 1000, rccl.DT_F32)
+    torch.cuda.synchronize()
+    assert torch.equal(y, x) and torch.equal(z, x.float())
+
+
+def _ref_and_gpu(depth, mode, dtype, force_env, seed=5, cat=True, N=20000):
+    X, y, info = _data(N=N, cat=cat, seed=seed)
+    b = fit_binning(X, info.iscat, info.nlevels, max_bins=64)
+    bins = apply_binning(b, X)
+    aux = torch.stack([torch.ones_like(y), y - y.mean(), y - y.mean(), torch.ones_like(y)], 1).contiguous()
+    p = T.SplitParams(min_w=10)
+    ref = T.RefTreeBuilder(bins, X.shape[0], b.nbins, b.iscat, None, depth, p)
+    ref.build(aux, leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1]).float())
+    tl_r = ref.pop_levels()[0]
+    force_env(mode, dtype)
+    dev = torch.device("cuda", 0)
+    gb = T.GpuTreeBuilder(bins.to(dev), X.shape[0], b.nbins, b.iscat, None, depth, p)
+    return ref, tl_r, gb, aux.to(dev)
+
+
+@pytest.mark.parametrize("depth,mode,dtype", [(6, "ar", "f64"), (5, "rs", "f64"), (7, "rs", "f64"), (6, "ar", "f32"),
+                                              (6, "rs", "f32")])
+def test_row_sharded_tree_on_rccl_matches_reference(depth, mode, dtype, force_env):
+    """f64 wire: the decisions of the fp64 reference exactly. f32 wire (half the bytes): the same tree up to ties
+    between equal-gain splits of one node (same rows either way), which fp32 rounding may break differently."""
+    from llama_github_io_amd.parallel import rccl
+    ref, tl_r, gb, aux = _ref_and_gpu(depth, mode, dtype, force_env)
+    assert gb.dist_mode and isinstance(gb.transport, rccl.NativeComm)
+    assert gb.sliced == (mode == "rs") and gb.cf32 == int(dtype == "f32")
+    for _ in range(2):   # the second tree reuses every buffer (and the communicator)
+        gb.build(aux, leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1]).float())
+        tl_g = gb.pop_levels()[0]
+        assert tl_g.root_weight == pytest.approx(tl_r.root_weight)
+        if dtype == "f32":
+            # the first level where a tie broke differently: equal gains there; the subtree below may differ
+            for dr, dg in zip(tl_r.decs, tl_g.decs):
+                if len(dr) != len(dg) or not np.array_equal(dr["feat"], dg["feat"]):
+                    n = min(len(dr), len(dg))
+                    np.testing.assert_allclose(dr["gain"][:n], dg["gain"][:n], rtol=1e-5)
+                    break
+            assert (ref.leaf_of_row == gb.leaf_of_row.cpu()).float().mean() > 0.95
+            continue
+        assert tl_g.n_leaves == tl_r.n_leaves
+        for dr, dg in zip(tl_r.decs, tl_g.decs):
+            assert np.array_equal(dr["feat"], dg["feat"])
+            assert np.array_equal(dr["bin"], dg["bin"])
+            np.testing.assert_allclose(dr["wl"], dg["wl"], rtol=1e-5)
+        np.testing.assert_allclose(tl_r.leaf_values, tl_g.leaf_values, rtol=1e-4, atol=1e-6)
+        assert torch.equal(ref.leaf_of_row, gb.leaf_of_row.cpu())
+
+
+def test_gbm_on_rccl_equals_single_process(force_env, monkeypatch):
+    """A whole GBM (gradients, leaf values on device, prediction update) through the 1-rank RCCL driver."""
+    from llama_github_io_amd.models.gbm import GBMTrainer
+    X, y, info = _data(N=30000, cat=True, seed=9)
+    dev = torch.device("cuda", 0)
+    X, y = X.to(dev), y.to(dev)
+    params = dict(ntrees=6, max_depth=5, seed=3)
+    single = GBMTrainer(params).fit(X, y, None, None, info).forest.predict_raw(X)
+    force_env("ar", "f64")
+    tr = GBMTrainer(params)
+    m = tr.fit(X, y, None, None, info)
+    sharded = m.forest.predict_raw(X)
+    assert torch.allclose(single, sharded, atol=1e-4, rtol=1e-4)
+
+
+def test_tree_on_one_rank_nccl_process_group(force_env):
+    """The communicator is created over a real (1-rank) ``nccl`` process group: the unique-id broadcast path."""
+    import torch.distributed as dist
+    from llama_github_io_amd.parallel import rccl
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        rccl.reset()
+        ref, tl_r, gb, aux = _ref_and_gpu(6, "rs", "f64", force_env, seed=11)
+        assert isinstance(gb.transport, rccl.NativeComm)
+        gb.build(aux, leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1]).float())
+        tl_g = gb.pop_levels()[0]
+        for dr, dg in zip(tl_r.decs, tl_g.decs):
+            assert np.array_equal(dr["feat"], dg["feat"]) and np.array_equal(dr["bin"], dg["bin"])
+        assert torch.equal(ref.leaf_of_row, gb.leaf_of_row.cpu())
+    finally:
+        rccl.reset()
+        dist.destroy_process_group()
