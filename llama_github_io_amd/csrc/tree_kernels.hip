@@ -300,18 +300,41 @@ __device__ __forceinline__ int filt_append(const RowFilter& flt, int r0, int r1,
 
 #define UNR 8   // hist: rows per lane group loaded before any atomic (8 independent loads per lane)
 
+// Row loads of the histogram loop. BUF: 32-bit buffer offsets into the bins (rows of 2^lgw bytes) and the aux planes
+// (each < 4 GiB; the host checks): one shift per row and per-unroll SGPR offsets instead of a 64-bit multiply-add
+// per load (the loop is VALU-issue bound, see hist_rows).
+struct HistSrc {
+  const unsigned* bins32;
+  const float* aw;
+  const float* ay;
+  __amdgpu_buffer_rsrc_t rb, ra, rw;
+  int lgw;
+};
+
+__device__ __forceinline__ HistSrc make_src(const unsigned* bins32, const float* aw, const float* ay, long long N, int W,
+                                            int lgw) {
+  // (descriptors are built unconditionally: a few SALU; only BUF kernels use them)
+  return HistSrc{bins32, aw, ay,
+                 __builtin_amdgcn_make_buffer_rsrc((void*)bins32, 0, (int)(unsigned)((unsigned long long)N * W * 4),
+                                                   0x00020000),
+                 __builtin_amdgcn_make_buffer_rsrc((void*)ay, 0, (int)(unsigned)(N * 4), 0x00020000),
+                 __builtin_amdgcn_make_buffer_rsrc((void*)(aw ? aw : ay), 0, (int)(unsigned)(N * 4), 0x00020000),
+                 lgw};
+}
+
 // Histogram rows [r0, r1) of one node into LDS (FILT: entries [r0, r1) of the LDS row list): lane group g
-// (8 lanes, one 4-feature row word each) takes rows g, g + RPI, ...; UNR rows per lane group are loaded
+// (8 lanes, one 4-feature row word each) takes rows g, g + GR, ...; UNR rows per lane group are loaded
 // before any atomic.
 // MEASURED: this loop is VALU-issue bound, not memory bound (prefetching / 4..16 rows in flight all ran
 // within 1.5 %), so everything per-lane is hoisted: the 4 feature slots and byte shifts of the lane's word
-// (rotated by row parity, see the layout note), feature validity, and an all-bytes NA test per word; the
-// common row is then bfe + lshl_add + ds_add_u64 per feature (two atomics when not PACKED).
-template <bool FILT, bool PACKED, bool UNIT, int GR = RPI>
-__device__ __forceinline__ void hist_rows(long long* h, float* nayy, const unsigned* __restrict__ bins32,
-                                          const float* __restrict__ aw, const float* __restrict__ ay, int W, int wabs,
+// (rotated by row parity, see the layout note), feature validity; NONA (no NA bin anywhere, a launch-time
+// property of the bins) drops the per-word NA test at compile time; a batch wholly inside the node skips the
+// per-row bounds tests; BUF addresses with 32-bit offsets. The common row is then bfe + lshl_add + ds_add_u64
+// per feature (two atomics when not PACKED).
+template <bool FILT, bool PACKED, bool UNIT, bool NONA, bool BUF, int GR = RPI>
+__device__ __forceinline__ void hist_rows(long long* h, float* nayy, const HistSrc& src, int W, int wabs,
                                           int F, bool lead, int r0, int r1, int g, int j, float& wyy, float sa,
-                                          float sb, float sp, const int* lst, bool no_na) {
+                                          float sb, float sp, const int* lst) {
   const int rot = g & 1;
   unsigned offb[4], sh[4];           // byte offset of the lane's feature slot in a bin row; its byte's shift
   unsigned vmask = 0u;
@@ -322,8 +345,8 @@ __device__ __forceinline__ void hist_rows(long long* h, float* nayy, const unsig
     sh[k] = 8u * kk;
     if (wabs < W && wabs * 4 + kk < F) vmask |= 0xFFu << (8 * kk);
   }
-  const bool full = vmask == 0xFFFFFFFFu;
   const int wc = min(wabs, W - 1);
+  const bool weighted = !UNIT && src.aw != nullptr;
   char* Hb = (char*)h;
   // entry (bin, slot) at byte (bin * FTILE + slot) * 8 = (bin << 8) + offb: one v_bfe_u32 + one v_lshl_add_u32
   // per atomic (MEASURED: the shift / and / shift / add form the compiler made of the index expression was 4 VALU
@@ -335,48 +358,75 @@ __device__ __forceinline__ void hist_rows(long long* h, float* nayy, const unsig
   for (int base = r0; base < r1; base += GR * UNR) {
     unsigned wd[UNR];
     float2 ab[UNR];
-    // unconditional loads (rows clamped into the node, words into the row): no exec-mask branches here;
-    // rows past r1 are skipped below, invalid words have vmask == 0
+    const bool whole = base + GR * UNR <= r1;          // block-uniform: no row of the batch is past r1
+    if (BUF && !FILT && whole) {
+      // consecutive rows: one voffset per batch, the unroll steps are SGPR offsets
+      const unsigned row0 = (unsigned)(base + g);
+      const unsigned vb = (row0 << src.lgw) + (unsigned)wc * 4u, va = row0 * 4u;
 #pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      const int idx = min(base + g + u * GR, r1 - 1);
-      const size_t row = FILT ? (size_t)lst[idx] : (size_t)idx;
-      // SoA aux planes: wY always, w only when rows are weighted (aw == null: unit weights)
-      ab[u] = make_float2(UNIT ? 1.f : (aw ? aw[row] : 1.f), ay[row]);
-      wd[u] = bins32[row * W + wc];
+      for (int u = 0; u < UNR; ++u) {
+        wd[u] = __builtin_amdgcn_raw_buffer_load_b32(src.rb, vb, (unsigned)(u * GR) << src.lgw, 0);
+        const float y = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(src.ra, va, u * GR * 4, 0));
+        const float w = weighted ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(src.rw, va, u * GR * 4, 0))
+                                 : 1.f;
+        ab[u] = make_float2(w, y);
+      }
+    } else {
+      // unconditional loads (rows clamped into the node, words into the row): no exec-mask branches here;
+      // rows past r1 are skipped below, invalid words have vmask == 0
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const int idx = whole ? base + g + u * GR : min(base + g + u * GR, r1 - 1);
+        const int row = FILT ? lst[idx] : idx;
+        if (BUF) {
+          const unsigned ro = (unsigned)row;
+          wd[u] = __builtin_amdgcn_raw_buffer_load_b32(src.rb, (ro << src.lgw) + (unsigned)wc * 4u, 0, 0);
+          const float y = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(src.ra, ro * 4u, 0, 0));
+          const float w = weighted ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(src.rw, ro * 4u, 0, 0)) : 1.f;
+          ab[u] = make_float2(w, y);
+        } else {
+          // SoA aux planes: wY always, w only when rows are weighted (aw == null: unit weights)
+          ab[u] = make_float2(weighted ? src.aw[row] : 1.f, src.ay[row]);
+          wd[u] = src.bins32[(size_t)row * W + wc];
+        }
+      }
     }
-#pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      const int idx = base + g + u * GR;
-      if (idx >= r1) continue;
+    // One row word: BRANCH-FREE atomics. Every lane adds all 4 of its word's features, valid or not: a feature past
+    // F (a partial last word, or a lane whose word is past the row) has the slot of a feature >= the tile's count,
+    // an LDS column the flush never reads, so its atomics are harmless — no divergent full / partial paths (the
+    // former per-row exec-mask juggling cost ~10 SALU per row). Only the rare NA-bin yy tally branches.
+    auto row = [&](int u) {
       // UNIT (packed, every row weight exactly 1): constant count part, yy = wY^2 (no reciprocal)
       if (lead) wyy += UNIT ? ab[u].y * ab[u].y : row_yy(ab[u].x, ab[u].y);
-      if (vmask == 0u) continue;
-      const long long qa = UNIT ? (1ll << PACK_SHIFT) + (long long)__float2int_rz(ab[u].y * sp)
+      // (int) conversion truncates toward zero (v_cvt_i32_f32): the __float2int_rz form added a v_trunc_f32
+      const long long qa = UNIT ? (1ll << PACK_SHIFT) + (long long)(int)(ab[u].y * sp)
                                 : PACKED ? qpack(ab[u].x, ab[u].y, sp) : q64(ab[u].x, sa);
       const long long qb = PACKED ? 0ll : q64(ab[u].y, sb);
       const unsigned w = wd[u];
-      const unsigned x = ~w | ~vmask;                     // a zero byte of x = an NA bin of a valid feature
-      const bool has_na = !no_na && ((x - 0x01010101u) & ~x & 0x80808080u) != 0u;
-      if (full && !has_na) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          unsigned long long* p = ent(w, k);
-          atomicAdd(p, (unsigned long long)qa);
-          if (!PACKED) atomicAdd(p + HPLANE, (unsigned long long)qb);
-        }
-      } else {
-        const float yy = UNIT ? ab[u].y * ab[u].y : row_yy(ab[u].x, ab[u].y);
+      for (int k = 0; k < 4; ++k) {
+        unsigned long long* p = ent(w, k);
+        atomicAdd(p, (unsigned long long)qa);
+        if (!PACKED) atomicAdd(p + HPLANE, (unsigned long long)qb);
+      }
+      if (!NONA) {
+        const unsigned x = ~w | ~vmask;                   // a zero byte of x = an NA bin of a valid feature
+        if (((x - 0x01010101u) & ~x & 0x80808080u) != 0u) {
+          const float yy = UNIT ? ab[u].y * ab[u].y : row_yy(ab[u].x, ab[u].y);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          if (!((vmask >> sh[k]) & 1u)) continue;
-          const unsigned bin = __builtin_amdgcn_ubfe(w, sh[k], 8);
-          unsigned long long* p = ent(w, k);
-          atomicAdd(p, (unsigned long long)qa);
-          if (!PACKED) atomicAdd(p + HPLANE, (unsigned long long)qb);
-          if (bin == NA_BIN) atomicAdd(nayy + j * 4 + (sh[k] >> 3), yy);
+          for (int k = 0; k < 4; ++k)
+            if (((vmask >> sh[k]) & 1u) && __builtin_amdgcn_ubfe(w, sh[k], 8) == NA_BIN)
+              atomicAdd(nayy + j * 4 + (sh[k] >> 3), yy);
         }
       }
+    };
+    if (whole) {
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) row(u);
+    } else {
+#pragma unroll
+      for (int u = 0; u < UNR; ++u)
+        if (base + g + u * GR < r1) row(u);
     }
   }
 }
@@ -387,14 +437,14 @@ __device__ __forceinline__ void hist_rows(long long* h, float* nayy, const unsig
 // (deterministic, no global atomics). grid = (G, n_ftiles); each block takes a contiguous tile range.
 // FILT (odd levels): a node's tiles cover its PARENT's rows; only rows the parent's decision sends to
 // this child are accumulated, and ftile-0 blocks add the parent's left-going row count to nl_out.
-template <bool FILT, bool PACKED, bool UNIT = false>
+template <bool FILT, bool PACKED, bool UNIT, bool NONA, bool BUF>
 __global__ __launch_bounds__(BLK) void k_hist_build(
     const uint8_t* __restrict__ bins, int stride /*bytes per row, multiple of 4*/,
     const float* __restrict__ aw /*row weights or null (unit)*/, const float* __restrict__ ay /*w * Y*/,
     const Node* __restrict__ nodes, const int* __restrict__ tile_prefix,
     const int* __restrict__ meta /*[0]=n_nodes [2]=n_build_tiles*/, int F, double* __restrict__ partials,
     int slot_doubles, const double* __restrict__ qs /*[sa, sb, 1/sa, 1/sb, sp, 1/sp]*/,
-    const Dec* __restrict__ pdec, int* __restrict__ nl_out, int f32, long long N, int planar) {
+    const Dec* __restrict__ pdec, int* __restrict__ nl_out, int f32, long long N, int planar, int lgw) {
   constexpr bool packed = PACKED;
   extern __shared__ __attribute__((aligned(16))) long long smem64[];
   long long* h = smem64;                                 // 2 planes (PACKED: 1 -> two blocks per CU fit)
@@ -413,7 +463,6 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
   // (MEASURED: an XCD-aware 1-D order putting the feature-tile blocks of one row range on the same XCD
   // made XGBoost 100M x 50 histograms 9-20 % SLOWER — 4.56 -> 4.97 ms filtered, 2.32 -> 2.80 ms plain)
   const int ftile = blockIdx.y;
-  const bool no_na = (planar >> 1) & 1;   // launch flag bit 1: no NA bin in the bins (skip the per-word test)
   planar &= 1;
   // planar: this block reads only its 32-feature plane (8 words per row, features counted from the plane)
   const int W = planar ? LPR : stride >> 2;
@@ -422,6 +471,7 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
   const int Fl = planar ? F - ftile * FTILE : F;
   const unsigned* bins32 = (const unsigned*)(planar ? bins + (size_t)ftile * (size_t)N * 32 : bins);
   const float sa = (float)qs[0], sb = (float)qs[1], sp = (float)qs[4];
+  const HistSrc src = make_src(bins32, aw, ay, N, W, lgw);
 
   __shared__ Dec spd;
   RowFilter flt{&spd, bins, stride, 0, -1, 0, 0, 0, 0, false};
@@ -437,8 +487,8 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
     if (FILT && qn > 0) {
       float wf2 = 0.f;
       wave_sync_lds();
-      hist_rows<FILT, PACKED, UNIT, 8>(h, nayy, bins32, aw, ay, W, wabs, Fl, j == 0 && ftile == 0, 0, qn, lane >> 3, j, wf2,
-                                 sa, sb, sp, wq, no_na);
+      hist_rows<FILT, PACKED, UNIT, NONA, BUF, 8>(h, nayy, src, W, wabs, Fl, j == 0 && ftile == 0, 0, qn, lane >> 3, j,
+                                                  wf2, sa, sb, sp, wq);
       wyy += (double)wf2;
       qn = 0;
       wave_sync_lds();
@@ -505,8 +555,8 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
       // of this node (or the drain before the flush)
       while (qn >= 64) {
         wave_sync_lds();
-        hist_rows<FILT, PACKED, UNIT, 8>(h, nayy, bins32, aw, ay, W, wabs, Fl, j == 0 && ftile == 0, 0, 64, lane >> 3, j, wf,
-                                   sa, sb, sp, wq, no_na);
+        hist_rows<FILT, PACKED, UNIT, NONA, BUF, 8>(h, nayy, src, W, wabs, Fl, j == 0 && ftile == 0, 0, 64, lane >> 3, j,
+                                                    wf, sa, sb, sp, wq);
         const int rest = qn - 64;                        // <= 127: move to the queue front (no lane overlap)
         wave_sync_lds();
         const int v0 = lane < rest ? wq[64 + lane] : 0, v1 = lane + 64 < rest ? wq[128 + lane] : 0;
@@ -515,8 +565,8 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
         qn = rest;
       }
     } else {
-      hist_rows<FILT, PACKED, UNIT>(h, nayy, bins32, aw, ay, W, wabs, Fl, j == 0 && ftile == 0, r0, r1, g, j, wf, sa, sb,
-                              sp, nullptr, no_na);
+      hist_rows<FILT, PACKED, UNIT, NONA, BUF>(h, nayy, src, W, wabs, Fl, j == 0 && ftile == 0, r0, r1, g, j, wf, sa, sb,
+                                               sp, nullptr);
     }
     wyy += (double)wf;
   }
@@ -1677,21 +1727,44 @@ __global__ void k_leaf_values(const double* __restrict__ leafsum, int n, int log
 
 // ================================================================================================
 // C ABI launchers (called through ctypes with raw device pointers and the current HIP stream).
-template <bool PACKED, bool UNIT = false>
+template <bool FILT, bool PACKED, bool UNIT, bool NONA, bool BUF>
+static void launch_hist4(dim3 grid, size_t lds, hipStream_t s, const void* bins, int stride, const void* aw,
+                         const void* ay, const void* nodes, const void* tile_prefix, const void* meta, int F,
+                         void* partials, int slot_doubles, const void* qs, const void* pdec, void* nl_out, int f32,
+                         long long N, int planar, int lgw) {
+  hipLaunchKernelGGL((k_hist_build<FILT, PACKED, UNIT, NONA, BUF>), grid, dim3(BLK), lds, s, (const uint8_t*)bins,
+                     stride, (const float*)aw, (const float*)ay, (const Node*)nodes, (const int*)tile_prefix,
+                     (const int*)meta, F, (double*)partials, slot_doubles, (const double*)qs, (const Dec*)pdec,
+                     (int*)nl_out, f32, N, planar, lgw);
+}
+
+template <bool PACKED, bool UNIT>
 static void launch_hist(dim3 grid, size_t lds, hipStream_t s, const void* bins, int stride, const void* aw,
                         const void* ay, const void* nodes, const void* tile_prefix, const void* meta, int F,
                         void* partials, int slot_doubles, const void* qs, const void* pdec, void* nl_out, int f32,
                         long long N, int planar) {
-  if (pdec)
-    hipLaunchKernelGGL((k_hist_build<true, PACKED, UNIT>), grid, dim3(BLK), lds, s, (const uint8_t*)bins, stride,
-                       (const float*)aw, (const float*)ay, (const Node*)nodes, (const int*)tile_prefix,
-                       (const int*)meta, F, (double*)partials, slot_doubles, (const double*)qs, (const Dec*)pdec,
-                       (int*)nl_out, f32, N, planar);
-  else
-    hipLaunchKernelGGL((k_hist_build<false, PACKED, UNIT>), grid, dim3(BLK), lds, s, (const uint8_t*)bins, stride,
-                       (const float*)aw, (const float*)ay, (const Node*)nodes, (const int*)tile_prefix,
-                       (const int*)meta, F, (double*)partials, slot_doubles, (const double*)qs, (const Dec*)nullptr,
-                       (int*)nullptr, f32, N, planar);
+  // flags: bit 0 planar bins, bit 1 no NA bin anywhere (NONA kernels)
+  const bool nona = (planar >> 1) & 1;
+  planar &= 1;
+  // BUF: the bins buffer this kernel reads (row-major, or one 32-byte plane) and the aux planes fit 32-bit offsets
+  // and the row bytes are a power of two
+  const int rowb = planar ? 32 : stride;
+  const unsigned long long bytes = (unsigned long long)N * (unsigned long long)rowb;
+  int lgw = -1;
+  for (int k = 0; k < 12; ++k) if (rowb == (1 << k)) lgw = k;
+  const bool buf = lgw >= 0 && bytes < (1ull << 31) && (unsigned long long)N * 4ull < (1ull << 31);
+#define H2O_HIST_CASE(F_, N_, B_) \
+  launch_hist4<F_, PACKED, UNIT, N_, B_>(grid, lds, s, bins, stride, aw, ay, nodes, tile_prefix, meta, F, partials, \
+                                          slot_doubles, qs, pdec, nl_out, f32, N, planar, lgw)
+  const bool filt = pdec != nullptr;
+  if (filt) {
+    if (nona) { if (buf) H2O_HIST_CASE(true, true, true); else H2O_HIST_CASE(true, true, false); }
+    else { if (buf) H2O_HIST_CASE(true, false, true); else H2O_HIST_CASE(true, false, false); }
+  } else {
+    if (nona) { if (buf) H2O_HIST_CASE(false, true, true); else H2O_HIST_CASE(false, true, false); }
+    else { if (buf) H2O_HIST_CASE(false, false, true); else H2O_HIST_CASE(false, false, false); }
+  }
+#undef H2O_HIST_CASE
 }
 
 template <typename P, typename TO>
@@ -1728,8 +1801,8 @@ int h2o_hist_build(const void* bins, int stride, const void* aw, const void* ay,
   const dim3 gr(grid, nft);
   if (packed && aw == nullptr)   // unit row weights (the trainer dropped the w plane)
     launch_hist<true, true>(gr, lds, s, bins, stride, aw, ay, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out, f32, N, planar);
-  else if (packed) launch_hist<true>(gr, lds, s, bins, stride, aw, ay, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out, f32, N, planar);
-  else launch_hist<false>(gr, lds, s, bins, stride, aw, ay, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out, f32, N, planar);
+  else if (packed) launch_hist<true, false>(gr, lds, s, bins, stride, aw, ay, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out, f32, N, planar);
+  else launch_hist<false, false>(gr, lds, s, bins, stride, aw, ay, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out, f32, N, planar);
   return (int)hipGetLastError();
 }
 

@@ -419,7 +419,8 @@ class H2OFrame:
         raise TypeError(f"cannot build an H2OFrame from {type(obj)}")
 
     @staticmethod
-    def from_predictions(P: torch.Tensor, category: str, domain, threshold=None, names=None) -> "H2OFrame":
+    def from_predictions(P: torch.Tensor, category: str, domain, threshold=None, names=None,
+                         labels=None) -> "H2OFrame":
         dev = P.device
         if names is not None:
             P2 = P if P.dim() == 2 else P.reshape(-1, 1)
@@ -432,7 +433,7 @@ class H2OFrame:
             cols += [Column(str(d), "real", P[:, i].double()) for i, d in enumerate(domain)]
             return H2OFrame._from_columns(cols)
         if category == "Multinomial":
-            lab = P.argmax(1).to(torch.int32)
+            lab = (P.argmax(1) if labels is None else labels).to(torch.int32)
             cols = [Column("predict", "enum", lab, list(domain))]
             cols += [Column(str(d), "real", P[:, i].double()) for i, d in enumerate(domain)]
             return H2OFrame._from_columns(cols)

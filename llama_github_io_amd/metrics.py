@@ -271,8 +271,9 @@ def gains_lift(y, p1, w, groups: int = 16):
     return out
 
 
-def multinomial_metrics(y, probs, w=None, domain=None, hit_k: int = 10) -> ModelMetrics:
-    """y: class index; probs [N, K]. Sums, the confusion matrix and hit counts merge by all-reduce."""
+def multinomial_metrics(y, probs, w=None, domain=None, hit_k: int = 10, labels=None) -> ModelMetrics:
+    """y: class index; probs [N, K]. Sums, the confusion matrix and hit counts merge by all-reduce.
+    ``labels`` [N]: the model's predicted classes when they are not argmax(probs) (ordinal GLM)."""
     y = y.long() if not torch.is_floating_point(y) else torch.nan_to_num(y, nan=-1).long()
     w = _w(w, y.numel(), y.device)
     ok = (y >= 0) & (w > 0)
@@ -280,7 +281,7 @@ def multinomial_metrics(y, probs, w=None, domain=None, hit_k: int = 10) -> Model
     K = probs.shape[1]
     py = torch.clamp(probs.gather(1, y[:, None]).squeeze(1), 1e-15, 1.0)
     onehot = torch.nn.functional.one_hot(y, K).double()
-    pred = probs.argmax(1)
+    pred = probs.argmax(1) if labels is None else labels.to(probs.device)[ok].long()
     from .ops.segment import segment_sum
     cm = segment_sum(y * K + pred, w, K * K)
     rank = (probs > py[:, None]).sum(1)
@@ -388,11 +389,12 @@ def autoencoder_metrics(err) -> ModelMetrics:
     return ModelMetrics(model_category="AutoEncoder", MSE=s / max(n, 1), RMSE=math.sqrt(s / max(n, 1)), nobs=n)
 
 
-def make_metrics(category: str, y, preds, w=None, domain=None, distribution=None) -> ModelMetrics:
-    """preds: regression -> [N] mean; binomial -> [N] p1 or [N,2]; multinomial -> [N,K] probs."""
+def make_metrics(category: str, y, preds, w=None, domain=None, distribution=None, labels=None) -> ModelMetrics:
+    """preds: regression -> [N] mean; binomial -> [N] p1 or [N,2]; multinomial -> [N,K] probs (``labels``: the
+    predicted classes when they are not the argmax)."""
     if category == "Binomial":
         p1 = preds[:, -1] if preds.dim() == 2 else preds
         return binomial_metrics(y, p1, w, domain or ("0", "1"))
     if category == "Multinomial":
-        return multinomial_metrics(y, preds, w, domain)
+        return multinomial_metrics(y, preds, w, domain, labels=labels)
     return regression_metrics(y, preds.reshape(-1), w, distribution)

@@ -200,7 +200,8 @@ class Model:
             X, offset = frame.model_matrix(self.info, device=self.device)
             P = self.score_tensor(X, offset)
             out = H2OFrame.from_predictions(P, self.model_category, self.info.response_domain,
-                                            threshold=self.default_threshold(), names=self.prediction_names())
+                                            threshold=self.default_threshold(), names=self.prediction_names(),
+                                            labels=self.predict_labels(P))
             cm = getattr(self, "calibration_model", None)
             if cm is not None and P.dim() == 2 and P.shape[1] == 2:
                 out = out.cbind(self._calibrated(P))
@@ -229,6 +230,10 @@ class Model:
         """Column names of a multi-column non-classification prediction frame (None = defaults)."""
         return None
 
+    def predict_labels(self, P):
+        """Predicted classes when the model's rule is not argmax of the class probabilities (None = argmax)."""
+        return None
+
     def default_threshold(self):
         tm = self.output.get("training_metrics") or {}
         vm = self.output.get("validation_metrics") or {}
@@ -239,7 +244,8 @@ class Model:
         cat = self.model_category
         if cat in ("Binomial", "Multinomial", "Regression"):
             return mm.make_metrics(cat, y.to(P.device), P, None if w is None else w.to(P.device),
-                                   self.info.response_domain, getattr(self, "distribution", None))
+                                   self.info.response_domain, getattr(self, "distribution", None),
+                                   labels=self.predict_labels(P))
         return None
 
     def model_performance(self, test_data=None, train=False, valid=False, xval=False):

@@ -442,7 +442,8 @@ def _cross_validate(spec, p, fr, info, X, yv, w, off, seed, mid, job):
     out["_cv_lengths"] = [float(m.output.get("ntrees") or m.output.get("epochs") or 0) for m in models
                           if (m.output.get("ntrees") or m.output.get("epochs"))]
     if yv is not None and holdout is not None:
-        cvm = mm.make_metrics(cat, yv, holdout, w, info.response_domain)
+        cvm = mm.make_metrics(cat, yv, holdout, w, info.response_domain,
+                              labels=models[0].predict_labels(holdout) if models else None)
         out["cross_validation_metrics"] = cvm
         summ = {}
         for key in ("AUC", "pr_auc", "logloss", "MSE", "RMSE", "mae", "r2", "mean_per_class_error", "mean_residual_deviance"):

@@ -24,6 +24,7 @@ import time
 
 import numpy as np
 import torch
+import torch.distributed
 
 from .. import metrics as mm
 from ..parallel import collectives as coll
@@ -32,6 +33,8 @@ from .base import DataInfo, Model, make_key
 from .datainfo import Expander
 from .params import canon
 from ..ops.segment import segment_sum
+
+_MIN, _MAX = torch.distributed.ReduceOp.MIN, torch.distributed.ReduceOp.MAX
 
 GLM_DEFAULTS = dict(family="AUTO", link="family_default", solver="AUTO", alpha=None, lambda_=None, lambda_search=False,
                     nlambdas=-1, lambda_min_ratio=-1.0, standardize=True, intercept=True, max_iterations=-1,
@@ -350,6 +353,16 @@ class GLMModel(Model):
             return torch.stack([1 - mu, mu], 1).float()
         return mu.float()
 
+    def predict_labels(self, P):
+        """Ordinal (GLMModel.score0): the first class whose cumulative probability exceeds 1/2 (eta_c > 0), else the
+        last class — the median of the predicted distribution, not its mode."""
+        if self.output.get("family") != "ordinal" or P.dim() != 2:
+            return None
+        cum = P.double().cumsum(1)[:, :-1] > 0.5
+        K = P.shape[1]
+        first = torch.where(cum.any(1), cum.int().argmax(1), torch.full_like(cum[:, 0], K - 1, dtype=torch.long))
+        return first
+
     # ---- h2o-py accessors
     def coef(self):
         return self.output.get("coefficients")
@@ -488,6 +501,41 @@ class GLMTrainer:
             link = DEFAULT_LINK[fam]
         return fam, link
 
+    def _validate(self, fam, link, y, info):
+        """The reference's family / solver checks (``hex/glm/GLM.java:876-953``), on global response ranges."""
+        solver = canon(self.p["solver"])
+        if solver in ("gradientdescentlh", "gradientdescentsqerr") and fam != "ordinal":
+            raise ValueError("Solvers GRADIENT_DESCENT_LH and GRADIENT_DESCENT_SQERR are only supported for ordinal "
+                             "regression.  Do not choose them unless you specify your family to be ordinal")
+        ncls = len(info.response_domain) if info.response_domain is not None else 1
+        yy = y[~torch.isnan(y)] if y is not None else None
+        lo = float(coll.all_reduce_scalar(float(yy.min()) if yy is not None and yy.numel() else float("inf"),
+                                          op=_MIN)) if yy is not None else 0.0
+        hi = float(coll.all_reduce_scalar(float(yy.max()) if yy is not None and yy.numel() else float("-inf"),
+                                          op=_MAX)) if yy is not None else 0.0
+        if fam == "binomial" and ncls != 2 and not (ncls == 1 and lo >= 0 and hi <= 1 and
+                                                     bool(((yy == 0) | (yy == 1)).all())):
+            raise ValueError("Binomial requires the response to be a 2-class categorical or a binary column (0/1)")
+        if fam in ("multinomial", "ordinal") and ncls <= 2:
+            raise ValueError(f"{fam.capitalize()} requires a categorical response with at least 3 levels (for 2 class "
+                             "problem use family=binomial.")
+        if fam == "ordinal" and link in ("oprobit", "ologlog"):
+            raise ValueError("Ordinal regression only supports ologit as link.")
+        if fam in ("poisson", "negativebinomial"):
+            if ncls != 1:
+                raise ValueError("Poisson and Negative Binomial require the response to be numeric.")
+            if lo < 0:
+                raise ValueError("Poisson and Negative Binomial require response >= 0")
+            if fam == "negativebinomial" and float(self.p["theta"]) <= 0:
+                raise ValueError("Illegal Negative Binomial theta value.  Valid theta values be > 0 and <= 1.")
+        if fam == "gamma" and lo <= 0:
+            raise ValueError("Response value for gamma distribution must be greater than 0.")
+        if fam in ("tweedie", "quasibinomial") and ncls != 1:
+            raise ValueError(f"{fam.capitalize()} requires the response to be numeric.")
+        if fam == "fractionalbinomial" and (lo < 0 or hi > 1):
+            raise ValueError(f"Response '{info.response}' must be between 0 and 1 for fractional_binomial family. "
+                             f"Min: {lo:f}, Max: {hi:f}")
+
     def fit(self, X, y, w, offset, info: DataInfo, valid=None, model_key=None):
         t0 = time.time()
         p = self.p
@@ -504,6 +552,7 @@ class GLMTrainer:
             model.output["run_time_ms"] = int((time.time() - t0) * 1000)
             return model
         fam, link = self._family(info)
+        self._validate(fam, link, y, info)
         N = X.shape[1]
         w = torch.ones(N, dtype=torch.float64, device=dev) if w is None else w.double()
         y = y.double()
@@ -969,10 +1018,20 @@ class GLMTrainer:
             B = torch.zeros(1, P1, dtype=torch.float64, device=dev, requires_grad=True)
             th_raw = torch.zeros(K - 1, dtype=torch.float64, device=dev, requires_grad=True)
             yl = y.long()
+            sqerr = canon(p["solver"]) == "gradientdescentsqerr"
+            cls = torch.arange(K - 1, device=dev)
 
             def nll(B):
                 th = torch.cumsum(torch.cat([th_raw[:1], torch.nn.functional.softplus(th_raw[1:])]), 0)
                 eta = (Zd[:, :-1] @ B[0, :-1]) + off
+                if sqerr:
+                    # GRADIENT_DESCENT_SQERR (GLMTask.computeGradientMultipliersSQERR): threshold c's linear
+                    # predictor e_c = th_c - eta must be negative for c < y and positive for c >= y; each
+                    # violation costs 0.5 e_c^2
+                    e = th[None, :] - eta[:, None]
+                    below = cls[None, :] < yl[:, None]
+                    viol = torch.where(below, e > 0, e <= 0)
+                    return (w * (0.5 * torch.where(viol, e * e, torch.zeros_like(e))).sum(1)).sum() * obj_reg
                 cdf = torch.sigmoid(th[None, :] - eta[:, None])
                 cdf = torch.cat([torch.zeros_like(cdf[:, :1]), cdf, torch.ones_like(cdf[:, :1])], 1)
                 pr = (cdf.gather(1, (yl + 1)[:, None]) - cdf.gather(1, yl[:, None]))[:, 0].clamp(min=1e-15)
@@ -1088,7 +1147,9 @@ class GLMTrainer:
             rank = int((beta.abs() > 0).sum())
             out.update(residual_deviance=res_dev, null_deviance=null_dev, aic=res_dev + 2 * rank,
                        null_degrees_of_freedom=nobs - 1, residual_degrees_of_freedom=nobs - rank)
-        tm = mm.make_metrics(cat, yv[ok], P[ok], w[ok].float(), model.info.response_domain)
+        lab = model.predict_labels(P)
+        tm = mm.make_metrics(cat, yv[ok], P[ok], w[ok].float(), model.info.response_domain,
+                             labels=None if lab is None else lab[ok])
         if tm is not None:
             tm.update(null_deviance=out.get("null_deviance"), residual_deviance=out.get("residual_deviance"),
                       AIC=out.get("aic"))

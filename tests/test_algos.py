@@ -97,6 +97,30 @@ def test_glm_families():
     assert max(b - a for a, b in zip(de[-6:-1], de[-5:])) < 1e-4 * 1.01
 
 
+def test_glm_ordinal_sqerr_solver_and_solver_family_validation():
+    """GLM.java:880-883 (GRADIENT_DESCENT_* only with ordinal) and GLMTask.computeGradientMultipliersSQERR (the
+    squared-error ordinal objective is a different model from the likelihood one, and still classifies)."""
+    from llama_github_io_amd.models.glm import GLMTrainer
+    X, y, info = _cls()
+    yk = torch.bucketize(X[0] - X[1], torch.tensor([-0.5, 0.5])).float()
+    info3 = DataInfo(info.x, info.iscat, info.domains, "y", ["a", "b", "c"])
+    lh = GLMTrainer(dict(family="ordinal", lambda_=0, solver="GRADIENT_DESCENT_LH")).fit(X, yk, None, None, info3)
+    sq = GLMTrainer(dict(family="ordinal", lambda_=0, solver="GRADIENT_DESCENT_SQERR")).fit(X, yk, None, None, info3)
+    assert sq.output["training_metrics"]["mean_per_class_error"] < 0.2
+    a = np.array(list(lh.output["coefficients"].values()))
+    b = np.array(list(sq.output["coefficients"].values()))
+    assert np.abs(a - b).max() > 1e-2
+    with pytest.raises(ValueError, match="only supported for ordinal"):
+        GLMTrainer(dict(family="binomial", solver="GRADIENT_DESCENT_LH")).fit(X, y, None, None, info)
+    with pytest.raises(ValueError, match="at least 3 levels"):
+        GLMTrainer(dict(family="ordinal")).fit(X, y, None, None, info)
+    Xr, yr, infor = _reg()
+    with pytest.raises(ValueError, match="greater than 0"):
+        GLMTrainer(dict(family="gamma")).fit(Xr, yr, None, None, infor)
+    with pytest.raises(ValueError, match="response >= 0"):
+        GLMTrainer(dict(family="poisson")).fit(Xr, yr, None, None, infor)
+
+
 def test_kmeans_and_estimate_k():
     from llama_github_io_amd.models.kmeans import KMeansTrainer
     g = torch.Generator().manual_seed(0)
