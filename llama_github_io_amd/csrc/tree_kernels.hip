@@ -178,22 +178,31 @@ template <typename P>
 __device__ __forceinline__ void put_partial(P* q, double d, bool acc) {
   *q = acc ? (P)((double)*q + d) : (P)d;
 }
+// srep/snb (LDS, per tile feature): replica count and bin count of a low-cardinality feature whose updates were
+// spread over `srep` copies of its bins (see hist_rows); bin b < nb is the sum of the copies b + c * nb.
 __device__ void flush_partial(const long long* h, const float* nayy, double node_wyy, int ftile, int F,
                               double* __restrict__ part, const double* __restrict__ qs, bool packed, bool acc,
-                              bool f32) {
+                              bool f32, const int* srep, const int* snb) {
   const int f0 = ftile * FTILE;
   const int nf = min(FTILE, F - f0);
   const double inv_a = qs[2], inv_b = qs[3], inv_p = qs[5];
   for (int i = threadIdx.x; i < nf * 2 * NBIN; i += blockDim.x) {
     const int bin = i / (2 * nf), rem = i - bin * 2 * nf, fl = rem >> 1, r = rem & 1;
-    const int e = bin * FTILE + fslot(fl);
+    const int reps = srep[fl], nb = snb[fl];
+    long long q = 0;                       // the entry's fixed-point value (plane r), replicas summed
+    if (reps == 1 || bin < nb) {
+      for (int c = 0; c < reps; ++c) {
+        const int e = (bin + c * nb) * FTILE + fslot(fl);
+        q += packed ? h[e] : h[r * HPLANE + e];
+      }
+    }
     double d;
     if (packed) {
       long long c, v;
-      unpack(h[e], c, v);
+      unpack(q, c, v);
       d = r ? (double)v * inv_p : (double)c;
     } else {
-      d = (double)h[r * HPLANE + e] * (r ? inv_b : inv_a);
+      d = (double)q * (r ? inv_b : inv_a);
     }
     const size_t e2 = (size_t)bin * 2 * F + 2 * (f0 + fl) + r;
     if (f32) put_partial((float*)part + e2, d, acc);
@@ -298,7 +307,10 @@ __device__ __forceinline__ int filt_append(const RowFilter& flt, int r0, int r1,
   return qn;
 }
 
-#define UNR 8   // hist: rows per lane group loaded before any atomic (8 independent loads per lane)
+#ifndef H2O_UNR
+#define H2O_UNR 8
+#endif
+// hist: rows per lane group loaded before any atomic (UNR independent loads per lane; the FILT queue batches use 8)
 
 // Row loads of the histogram loop. BUF: 32-bit buffer offsets into the bins (rows of 2^lgw bytes) and the aux planes
 // (each < 4 GiB; the host checks): one shift per row and per-unroll SGPR offsets instead of a 64-bit multiply-add
@@ -331,20 +343,26 @@ __device__ __forceinline__ HistSrc make_src(const unsigned* bins32, const float*
 // property of the bins) drops the per-word NA test at compile time; a batch wholly inside the node skips the
 // per-row bounds tests; BUF addresses with 32-bit offsets. The common row is then bfe + lshl_add + ds_add_u64
 // per feature (two atomics when not PACKED).
-template <bool FILT, bool PACKED, bool UNIT, bool NONA, bool BUF, int GR = RPI>
+template <bool FILT, bool PACKED, bool UNIT, bool NONA, bool BUF, int GR = RPI, int UNR = H2O_UNR>
 __device__ __forceinline__ void hist_rows(long long* h, float* nayy, const HistSrc& src, int W, int wabs,
                                           int F, bool lead, int r0, int r1, int g, int j, float& wyy, float sa,
-                                          float sb, float sp, const int* lst) {
+                                          float sb, float sp, const int* lst, const int* srep, const int* snb) {
   const int rot = g & 1;
   unsigned offb[4], sh[4];           // byte offset of the lane's feature slot in a bin row; its byte's shift
   unsigned vmask = 0u;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int kk = (k + rot) & 3;
-    offb[k] = (unsigned)fslot(j * 4 + kk) * 8u;
+    const int fl = j * 4 + kk;
+    // low-cardinality features (srep > 1, NONA only): same-parity rows of a lane group collide on the few bins of
+    // such a feature (SQ_LDS_ADDR_CONFLICT ~ SQ_LDS_IDX_ACTIVE on HIGGS-like data with 3-valued b-tags); their
+    // updates go to copy (g >> 1) mod srep of the feature's bins, summed by the flush
+    const int c = (g >> 1) & (srep[fl] - 1);
+    offb[k] = (unsigned)fslot(fl) * 8u + ((unsigned)(c * snb[fl]) << 8);
     sh[k] = 8u * kk;
     if (wabs < W && wabs * 4 + kk < F) vmask |= 0xFFu << (8 * kk);
   }
+  const bool live = vmask != 0u;     // a lane whose word is past the row adds nothing (no dummy atomics)
   const int wc = min(wabs, W - 1);
   const bool weighted = !UNIT && src.aw != nullptr;
   char* Hb = (char*)h;
@@ -391,10 +409,10 @@ __device__ __forceinline__ void hist_rows(long long* h, float* nayy, const HistS
         }
       }
     }
-    // One row word: BRANCH-FREE atomics. Every lane adds all 4 of its word's features, valid or not: a feature past
-    // F (a partial last word, or a lane whose word is past the row) has the slot of a feature >= the tile's count,
-    // an LDS column the flush never reads, so its atomics are harmless — no divergent full / partial paths (the
-    // former per-row exec-mask juggling cost ~10 SALU per row). Only the rare NA-bin yy tally branches.
+    // One row word: every live lane adds all 4 of its word's features, valid or not: a feature past F (a partial last
+    // word) has the slot of a feature >= the tile's count, an LDS column the flush never reads, so its atomics are
+    // harmless — no divergent full / partial paths (the former per-row exec-mask juggling cost ~10 SALU per row).
+    // Only the rare NA-bin yy tally branches.
     auto row = [&](int u) {
       // UNIT (packed, every row weight exactly 1): constant count part, yy = wY^2 (no reciprocal)
       if (lead) wyy += UNIT ? ab[u].y * ab[u].y : row_yy(ab[u].x, ab[u].y);
@@ -403,11 +421,13 @@ __device__ __forceinline__ void hist_rows(long long* h, float* nayy, const HistS
                                 : PACKED ? qpack(ab[u].x, ab[u].y, sp) : q64(ab[u].x, sa);
       const long long qb = PACKED ? 0ll : q64(ab[u].y, sb);
       const unsigned w = wd[u];
+      if (live) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        unsigned long long* p = ent(w, k);
-        atomicAdd(p, (unsigned long long)qa);
-        if (!PACKED) atomicAdd(p + HPLANE, (unsigned long long)qb);
+        for (int k = 0; k < 4; ++k) {
+          unsigned long long* p = ent(w, k);
+          atomicAdd(p, (unsigned long long)qa);
+          if (!PACKED) atomicAdd(p + HPLANE, (unsigned long long)qb);
+        }
       }
       if (!NONA) {
         const unsigned x = ~w | ~vmask;                   // a zero byte of x = an NA bin of a valid feature
@@ -444,7 +464,8 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
     const Node* __restrict__ nodes, const int* __restrict__ tile_prefix,
     const int* __restrict__ meta /*[0]=n_nodes [2]=n_build_tiles*/, int F, double* __restrict__ partials,
     int slot_doubles, const double* __restrict__ qs /*[sa, sb, 1/sa, 1/sb, sp, 1/sp]*/,
-    const Dec* __restrict__ pdec, int* __restrict__ nl_out, int f32, long long N, int planar, int lgw) {
+    const Dec* __restrict__ pdec, int* __restrict__ nl_out, int f32, long long N, int planar, int lgw,
+    const int* __restrict__ nbins_f /*[F] (NONA: low-cardinality spreading) or null*/) {
   constexpr bool packed = PACKED;
   extern __shared__ __attribute__((aligned(16))) long long smem64[];
   long long* h = smem64;                                 // 2 planes (PACKED: 1 -> two blocks per CU fit)
@@ -472,6 +493,15 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
   const unsigned* bins32 = (const unsigned*)(planar ? bins + (size_t)ftile * (size_t)N * 32 : bins);
   const float sa = (float)qs[0], sb = (float)qs[1], sp = (float)qs[4];
   const HistSrc src = make_src(bins32, aw, ay, N, W, lgw);
+  // per tile feature: bin count and copies of its bins (NONA: no NA bin, so copies of bins < nb never reach 255)
+  __shared__ int srep[FTILE], snb[FTILE];
+  if (threadIdx.x < FTILE) {
+    const int fg = ftile * FTILE + threadIdx.x;
+    const int nb = (NONA && nbins_f && fg < F) ? nbins_f[fg] : 0;
+    srep[threadIdx.x] = (nb > 0 && nb * 4 <= NA_BIN) ? 4 : (nb > 0 && nb * 2 <= NA_BIN) ? 2 : 1;
+    snb[threadIdx.x] = nb;
+  }
+  __syncthreads();
 
   __shared__ Dec spd;
   RowFilter flt{&spd, bins, stride, 0, -1, 0, 0, 0, 0, false};
@@ -487,8 +517,8 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
     if (FILT && qn > 0) {
       float wf2 = 0.f;
       wave_sync_lds();
-      hist_rows<FILT, PACKED, UNIT, NONA, BUF, 8>(h, nayy, src, W, wabs, Fl, j == 0 && ftile == 0, 0, qn, lane >> 3, j,
-                                                  wf2, sa, sb, sp, wq);
+      hist_rows<FILT, PACKED, UNIT, NONA, BUF, 8, 8>(h, nayy, src, W, wabs, Fl, j == 0 && ftile == 0, 0, qn, lane >> 3, j,
+                                                     wf2, sa, sb, sp, wq, srep, snb);
       wyy += (double)wf2;
       qn = 0;
       wave_sync_lds();
@@ -501,7 +531,7 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
     __syncthreads();
     const size_t so = (size_t)(blockIdx.x + cur) * slot_doubles;
     flush_partial(h, nayy, v[0], ftile, F, f32 ? (double*)((float*)partials + so) : partials + so, qs, packed, acc,
-                  f32 != 0);
+                  f32 != 0, srep, snb);
     if (FILT && threadIdx.x == 0 && v[1] != 0.0) atomicAdd(nl_out + cur_parent, (int)v[1]);
     __syncthreads();
   };
@@ -555,8 +585,8 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
       // of this node (or the drain before the flush)
       while (qn >= 64) {
         wave_sync_lds();
-        hist_rows<FILT, PACKED, UNIT, NONA, BUF, 8>(h, nayy, src, W, wabs, Fl, j == 0 && ftile == 0, 0, 64, lane >> 3, j,
-                                                    wf, sa, sb, sp, wq);
+        hist_rows<FILT, PACKED, UNIT, NONA, BUF, 8, 8>(h, nayy, src, W, wabs, Fl, j == 0 && ftile == 0, 0, 64, lane >> 3, j,
+                                                       wf, sa, sb, sp, wq, srep, snb);
         const int rest = qn - 64;                        // <= 127: move to the queue front (no lane overlap)
         wave_sync_lds();
         const int v0 = lane < rest ? wq[64 + lane] : 0, v1 = lane + 64 < rest ? wq[128 + lane] : 0;
@@ -566,7 +596,7 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
       }
     } else {
       hist_rows<FILT, PACKED, UNIT, NONA, BUF>(h, nayy, src, W, wabs, Fl, j == 0 && ftile == 0, r0, r1, g, j, wf, sa, sb,
-                                               sp, nullptr);
+                                               sp, nullptr, srep, snb);
     }
     wyy += (double)wf;
   }
@@ -1731,18 +1761,18 @@ template <bool FILT, bool PACKED, bool UNIT, bool NONA, bool BUF>
 static void launch_hist4(dim3 grid, size_t lds, hipStream_t s, const void* bins, int stride, const void* aw,
                          const void* ay, const void* nodes, const void* tile_prefix, const void* meta, int F,
                          void* partials, int slot_doubles, const void* qs, const void* pdec, void* nl_out, int f32,
-                         long long N, int planar, int lgw) {
+                         long long N, int planar, int lgw, const void* nbins_f) {
   hipLaunchKernelGGL((k_hist_build<FILT, PACKED, UNIT, NONA, BUF>), grid, dim3(BLK), lds, s, (const uint8_t*)bins,
                      stride, (const float*)aw, (const float*)ay, (const Node*)nodes, (const int*)tile_prefix,
                      (const int*)meta, F, (double*)partials, slot_doubles, (const double*)qs, (const Dec*)pdec,
-                     (int*)nl_out, f32, N, planar, lgw);
+                     (int*)nl_out, f32, N, planar, lgw, (const int*)nbins_f);
 }
 
 template <bool PACKED, bool UNIT>
 static void launch_hist(dim3 grid, size_t lds, hipStream_t s, const void* bins, int stride, const void* aw,
                         const void* ay, const void* nodes, const void* tile_prefix, const void* meta, int F,
                         void* partials, int slot_doubles, const void* qs, const void* pdec, void* nl_out, int f32,
-                        long long N, int planar) {
+                        long long N, int planar, const void* nbins_f) {
   // flags: bit 0 planar bins, bit 1 no NA bin anywhere (NONA kernels)
   const bool nona = (planar >> 1) & 1;
   planar &= 1;
@@ -1755,7 +1785,7 @@ static void launch_hist(dim3 grid, size_t lds, hipStream_t s, const void* bins, 
   const bool buf = lgw >= 0 && bytes < (1ull << 31) && (unsigned long long)N * 4ull < (1ull << 31);
 #define H2O_HIST_CASE(F_, N_, B_) \
   launch_hist4<F_, PACKED, UNIT, N_, B_>(grid, lds, s, bins, stride, aw, ay, nodes, tile_prefix, meta, F, partials, \
-                                          slot_doubles, qs, pdec, nl_out, f32, N, planar, lgw)
+                                          slot_doubles, qs, pdec, nl_out, f32, N, planar, lgw, nbins_f)
   const bool filt = pdec != nullptr;
   if (filt) {
     if (nona) { if (buf) H2O_HIST_CASE(true, true, true); else H2O_HIST_CASE(true, true, false); }
@@ -1790,19 +1820,20 @@ int h2o_tree_sizes(int* out) {
   return 0;
 }
 
-// partials: >= (grid + max nodes of the level) slots of slot_doubles
+// partials: >= (grid + max nodes of the level) slots of slot_doubles. nbins_f (nullable): per-feature bin counts,
+// which let NONA launches spread the updates of low-cardinality features over copies of their bins.
 int h2o_hist_build(const void* bins, int stride, const void* aw, const void* ay, const void* nodes,
                    const void* tile_prefix, const void* meta, int F, void* partials, int slot_doubles, const void* qs,
                    int grid, int packed, const void* pdec, void* nl_out, int f32, long long N, int planar,
-                   hipStream_t s) {
+                   const void* nbins_f, hipStream_t s) {
   const int nft = (F + FTILE - 1) / FTILE;
   // packed mode needs one int64 plane (66 KB): two 16-wave blocks share a CU (32 waves, 8 per SIMD)
   const size_t lds = (packed ? HIST_LDS_BYTES - HPLANE * 8 : HIST_LDS_BYTES) + HIST_LDS_TAIL;
   const dim3 gr(grid, nft);
   if (packed && aw == nullptr)   // unit row weights (the trainer dropped the w plane)
-    launch_hist<true, true>(gr, lds, s, bins, stride, aw, ay, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out, f32, N, planar);
-  else if (packed) launch_hist<true, false>(gr, lds, s, bins, stride, aw, ay, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out, f32, N, planar);
-  else launch_hist<false, false>(gr, lds, s, bins, stride, aw, ay, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out, f32, N, planar);
+    launch_hist<true, true>(gr, lds, s, bins, stride, aw, ay, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out, f32, N, planar, nbins_f);
+  else if (packed) launch_hist<true, false>(gr, lds, s, bins, stride, aw, ay, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out, f32, N, planar, nbins_f);
+  else launch_hist<false, false>(gr, lds, s, bins, stride, aw, ay, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out, f32, N, planar, nbins_f);
   return (int)hipGetLastError();
 }
 
@@ -2117,7 +2148,7 @@ int h2o_tree_root(const TreePlan* P, hipStream_t s) {
   const int g0 = P->tiles_cap[0] < P->grid ? P->tiles_cap[0] : P->grid;
   TP_CHECK(h2o_hist_build(P->master, P->stride, P->unit ? nullptr : tp_aux(P, 0), tp_aux(P, 1), P->nodes[0], P->bp[0],
                           P->meta[0], P->F, P->partials, P->slot, P->qs, g0, P->packed, nullptr, nullptr, P->pf32, P->N,
-                          P->planar | (P->no_na << 1), s));
+                          P->planar | (P->no_na << 1), P->nbins_f, s));
   // row-sharded all-reduce: straight into the wire buffer; sliced: hbuild (packed by slice next)
   if (P->dist && !P->sliced)
     return h2o_hist_reduce(P->partials, P->slot, P->used, P->nodes[0], P->bp[0], P->meta[0], 1, g0, P->hrecv, nullptr,
@@ -2187,7 +2218,8 @@ int h2o_tree_grow(const TreePlan* P, int d, int dist, hipStream_t s) {
     gh = P->tiles_cap[d] < P->grid ? P->tiles_cap[d] : P->grid;
     tp_level_buf(P, d, sb, sy, sw);
     rc = h2o_hist_build(sb, P->stride, sw, sy, P->nodes[d + 1], P->bp[d + 1], P->meta[d + 1], P->F, P->partials,
-                        P->slot, P->qs, gh, P->packed, P->dec[d], P->nl[d], P->pf32, P->N, P->planar | (P->no_na << 1), s);
+                        P->slot, P->qs, gh, P->packed, P->dec[d], P->nl[d], P->pf32, P->N, P->planar | (P->no_na << 1),
+                        P->nbins_f, s);
   } else {
     // regroup level d-1's rows two levels down, then histogram level d+1 (even) contiguously
     rc = tp_route(P, d - 1, s);
@@ -2197,7 +2229,8 @@ int h2o_tree_grow(const TreePlan* P, int d, int dist, hipStream_t s) {
     gh = P->tiles_cap[d + 1] < P->grid ? P->tiles_cap[d + 1] : P->grid;
     tp_level_buf(P, d + 1, sb, sy, sw);
     rc = h2o_hist_build(sb, P->stride, sw, sy, P->nodes[d + 1], P->bp[d + 1], P->meta[d + 1], P->F, P->partials,
-                        P->slot, P->qs, gh, P->packed, nullptr, nullptr, P->pf32, P->N, P->planar | (P->no_na << 1), s);
+                        P->slot, P->qs, gh, P->packed, nullptr, nullptr, P->pf32, P->N, P->planar | (P->no_na << 1),
+                        P->nbins_f, s);
   }
   if (rc) return -rc;
   if (!dist)

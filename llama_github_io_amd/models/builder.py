@@ -395,12 +395,15 @@ def _custom_metric(model, ref, X, y, w, off, which):
     else:
         rows = P[:, None]
     from ..parallel import collectives as coll
-    rows, y, w, off = (coll.gather_rows(t) for t in (rows, y, w, off))
-    name, val = udf.custom_metric_value(ref, rows.cpu().numpy(), y.double().cpu().numpy(),
-                                        None if w is None else w.double().cpu().numpy(),
-                                        None if off is None else off.double().cpu().numpy(), model)
+    # map/reduce per shard; only the small metric states travel (gathered in rank order and reduced with the
+    # user's reduce, as MRTask reduces CMetricFunc states across nodes) — no row gather
+    st = udf.custom_metric_state(ref, rows.cpu().numpy(), y.double().cpu().numpy(),
+                                 None if w is None else w.double().cpu().numpy(),
+                                 None if off is None else off.double().cpu().numpy(), model)
+    states = coll.all_gather_object(None if st is None else [float(v) for v in st]) if coll.is_dist() else [st]
+    name, _ = udf.resolve(ref)
     mets["custom_metric_name"] = name
-    mets["custom_metric_value"] = val
+    mets["custom_metric_value"] = udf.custom_metric_finish(ref, states)
 
 
 def _cross_validate(spec, p, fr, info, X, yv, w, off, seed, mid, job):

@@ -34,7 +34,7 @@ from .base import DataInfo, Model, make_key
 
 GAM_DEFAULTS = dict(gam_columns=None, num_knots=None, scale=None, bs=None, knot_ids=None, keep_gam_cols=False,
                     spline_orders=None, splines_non_negative=None, standardize=False, family="AUTO", lambda_=0.0,
-                    alpha=0.0, seed=-1, scale_tp_penalty_mat=False)
+                    alpha=0.0, seed=-1, scale_tp_penalty_mat=False, standardize_tp_gam_cols=False)
 
 
 # ------------------------------------------------------------------------------------------------ B-splines
@@ -156,12 +156,24 @@ def _tp_poly(Xd, exps):
 
 
 def tp_basis(Xd, st):
-    """[radial part (reparameterised) | polynomial part] for rows Xd [n, d]."""
+    """[radial part (reparameterised) | polynomial part] for rows Xd [n, d].
+
+    ``standardize_tp_gam_cols`` (``st["inv_std"]``): distances between data and knots are measured on coordinates
+    scaled by 1/sd of each column, and the polynomial part is taken of x - mean/sd, as the reference's
+    GamUtilsThinPlateRegression.calculateDistance / calculatePolynomialBasis do with standardizeGAM."""
     K = torch.as_tensor(st["knots"], dtype=torch.float64, device=Xd.device)
-    r = torch.cdist(Xd, K)
+    inv = st.get("inv_std")
+    if inv is not None:
+        iv = torch.as_tensor(inv, dtype=torch.float64, device=Xd.device)
+        mu = torch.as_tensor(st["means"], dtype=torch.float64, device=Xd.device)
+        r = torch.cdist(Xd * iv, K * iv)
+        Xp = Xd - mu * iv
+    else:
+        r = torch.cdist(Xd, K)
+        Xp = Xd
     E = _tp_eta(r, st["m"], Xd.shape[1])
     Zr = torch.as_tensor(st["Zr"], dtype=torch.float64, device=Xd.device)
-    P = _tp_poly(Xd, st["exps"])
+    P = _tp_poly(Xp, st["exps"])
     return torch.cat([E @ Zr, P], 1)
 
 
@@ -332,10 +344,24 @@ class GAMTrainer:
                         K = Xd[torch.argsort(Xd[:, 0], stable=True)[ranks.to(dev)]]
                 if K.shape[0] <= len(exps):
                     raise ValueError(f"thin-plate smoother {g} needs more than {len(exps)} knots")
+                inv = None
+                if p.get("standardize_tp_gam_cols"):
+                    # 1 / sample sd of each column (GAM.java: _predictVec.vec(c).sigma(), NAs skipped)
+                    inv = []
+                    for c, mu in zip(cols, means):
+                        okc = ~torch.isnan(c)
+                        v = torch.stack([torch.where(okc, (c - mu) ** 2, torch.zeros_like(c)).sum(), okc.double().sum()])
+                        if coll.is_dist():
+                            v = coll.all_reduce_(v.to(coll.comm_device())).cpu()
+                        sd = math.sqrt(float(v[0]) / max(float(v[1]) - 1.0, 1.0))
+                        inv.append(1.0 / sd if sd > 0 else 1.0)
+                    st["inv_std"] = inv
+                ivk = torch.as_tensor(inv, dtype=torch.float64, device=K.device) if inv is not None else None
+                Kd = K * ivk if ivk is not None else K                    # the distance coordinates of the knots
                 T = _tp_poly(K, exps)                                      # [k, M]
                 Q, _ = torch.linalg.qr(T, mode="complete")
                 Zr = Q[:, len(exps):]                                      # radial coefs orthogonal to T at the knots
-                Ek = _tp_eta(torch.cdist(K, K), m, d)
+                Ek = _tp_eta(torch.cdist(Kd, Kd), m, d)
                 S_r = Zr.T @ Ek @ Zr
                 st.update(knots=K.cpu().tolist(), m=m, exps=exps, Zr=Zr.cpu().tolist())
                 B = tp_basis(Xd, st)

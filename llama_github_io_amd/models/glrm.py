@@ -279,6 +279,32 @@ class GLRMTrainer:
         self.p = p
         self.job = None
 
+    @staticmethod
+    def _user_y(U, ex, info, k, P, expand):
+        """Initial archetypes from user_y (GLRM.java:187,400-425). ``expand_user_y`` (default): user_y holds the
+        ORIGINAL columns (categoricals as level indices) and is expanded — one-hot categoricals first, then the
+        numerics, as DataInfo permutes them; otherwise user_y already holds the P expanded columns."""
+        if U.shape[0] != k:
+            raise ValueError(f"The user-specified Y must have k = {k} rows")
+        if not expand:
+            if U.shape[1] != P:
+                raise ValueError(f"The user-specified Y must have the same number of columns ({P}) as the "
+                                 "training observations")
+            return U.clone()
+        if U.shape[1] != info.F:
+            raise ValueError(f"The user-specified Y must have the same number of columns ({info.F}) as the "
+                             "training observations")
+        Y = torch.zeros(k, P, dtype=torch.float64, device=U.device)
+        for i, j in enumerate(ex.cats):
+            lv = torch.nan_to_num(U[:, j], nan=-1).long() - (0 if ex.use_all else 1)
+            lo, n = ex.cat_offsets[i], ex.cat_sizes[i]
+            for r in range(k):
+                if 0 <= int(lv[r]) < n:
+                    Y[r, lo + int(lv[r])] = 1.0
+        for t, j in enumerate(ex.nums):
+            Y[:, ex.num_off + t] = U[:, j]
+        return Y
+
     def fit(self, X, y, w, offset, info: DataInfo, valid=None, model_key=None):
         from .shared_tree import resolve_seed
         t0 = time.time()
@@ -310,7 +336,9 @@ class GLRMTrainer:
         init = str(p["init"]).lower().replace("_", "")
         if init == "user" and p.get("user_y") is not None:
             uy = p["user_y"]
-            Y = torch.as_tensor(uy.as_tensor().numpy() if hasattr(uy, "as_tensor") else np.asarray(uy), dtype=torch.float64).to(dev)
+            U = torch.as_tensor(uy.as_tensor().numpy() if hasattr(uy, "as_tensor") else np.asarray(uy),
+                                dtype=torch.float64).to(dev)
+            Y = self._user_y(U, ex, info, k, P, bool(p.get("expand_user_y", True)))
         elif init == "svd":
             Am = torch.nan_to_num(A) * mask
             S, Vt = _top_svd_from_gram(_red(Am.T @ Am), k)

@@ -35,12 +35,9 @@ HINTS = {
 # parameters not implemented by this engine: a non-default value is refused
 UNSUPPORTED = {
     "glm": {"rand_link"},
-    "gam": {"standardize_tp_gam_cols"},
-
-    "glrm": {"expand_user_y"},
-    "rulefit": {"max_categorical_levels"},
-    "infogram": {"max_iterations"},
 }
+# (Infogram ``max_iterations`` is a schema field with no InfogramParameters counterpart in the reference
+# (hex/schemas/InfogramV3.java:82): accepted and, as there, without effect.)
 
 # parameters the reference accepts but no longer honours: a non-default value warns like the reference
 DEPRECATED = {

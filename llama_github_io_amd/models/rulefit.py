@@ -25,7 +25,7 @@ from .base import DataInfo, Model, make_key
 
 RF_DEFAULTS = dict(algorithm="AUTO", min_rule_length=3, max_rule_length=3, max_num_rules=-1,
                    model_type="rules_and_linear", rule_generation_ntrees=50, remove_duplicates=True, lambda_=None,
-                   distribution="AUTO", seed=-1)
+                   distribution="AUTO", seed=-1, max_categorical_levels=10)
 
 
 class Condition:
@@ -217,6 +217,43 @@ class RuleFitTrainer:
         self.p = p
         self.job = None
 
+    @staticmethod
+    def _enum_limited(X, info, maxl):
+        """The rule trees see categoricals through EnumLimited (RuleFit.java:113-114): the ``maxl`` most frequent
+        levels (global counts) keep their own code, the rest share one ``other`` level. Returns the tree design,
+        its DataInfo and per feature the original level indices behind each limited code (None: unchanged)."""
+        from ..parallel import collectives as coll
+        Xt, doms, lmap = X, list(info.domains), [None] * info.F
+        for j in range(info.F):
+            dom = info.domains[j]
+            if not info.iscat[j] or dom is None or len(dom) <= maxl:
+                continue
+            c = X[j]
+            ok = ~torch.isnan(c)
+            cnt = torch.bincount(c[ok].long(), minlength=len(dom)).double()
+            if coll.is_dist():
+                cnt = coll.all_reduce_(cnt.to(coll.comm_device())).to(c.device)
+            keep = sorted(np.argsort(-cnt.cpu().numpy(), kind="stable")[:maxl].tolist())
+            m = torch.full((len(dom),), float(len(keep)), dtype=X.dtype, device=X.device)
+            for i, k in enumerate(keep):
+                m[k] = float(i)
+            if Xt is X:
+                Xt = X.clone()
+            Xt[j] = torch.where(ok, m[c.clamp(min=0).long()], c)
+            doms[j] = [dom[k] for k in keep] + ["other"]
+            lmap[j] = [[k] for k in keep] + [[k for k in range(len(dom)) if k not in set(keep)]]
+        tinfo = DataInfo(info.x, info.iscat, doms, info.response, info.response_domain)
+        return Xt, tinfo, lmap
+
+    @staticmethod
+    def _unlimit(rules, lmap):
+        """Categorical conditions on limited codes -> the original levels they stand for (names stay those of the
+        limited domain, 'other' included, as the reference's rule text shows them)."""
+        for r in rules:
+            for c in r.conds:
+                if c.ctype == "cat" and lmap[c.feat] is not None:
+                    c.levels = sorted(k for lv in c.levels for k in lmap[c.feat][lv])
+
     def fit(self, X, y, w, offset, info: DataInfo, valid=None, model_key=None):
         from .drf import DRFTrainer
         from .gbm import GBMTrainer
@@ -231,20 +268,23 @@ class RuleFitTrainer:
         dom = info.response_domain
         multi = dom is not None and len(dom) > 2
         groups = []
+        Xt, tinfo, lmap = self._enum_limited(X, info, int(p.get("max_categorical_levels") or 10))
         if mtype != "linear":
             for mid, d in enumerate(depths):
                 kw = dict(ntrees=ntrees, max_depth=d, seed=p["seed"])
                 if str(p.get("distribution", "AUTO")).upper() != "AUTO":
                     kw["distribution"] = p["distribution"]
                 tr = GBMTrainer(kw) if algo == "GBM" else DRFTrainer(kw)
-                m = tr.fit(X, y, w, offset, info)
+                m = tr.fit(Xt, y, w, offset, tinfo)
                 fr = m.forest
                 K = max(1, fr.K)
                 for t, (tree, c) in enumerate(zip(fr.trees, fr.tree_class)):
                     tj = t // K
                     suffix = f"_{dom[c]}" if multi else ""
                     name = f"M{mid}T{tj}C{c}" if multi else f"M{mid}T{tj}"
-                    groups.append((name, leaf_rules(tree, mid, tj, info.x, info.domains, suffix)))
+                    rules = leaf_rules(tree, mid, tj, info.x, tinfo.domains, suffix)
+                    self._unlimit(rules, lmap)
+                    groups.append((name, rules))
                 # columns ordered (model, tree, class) as in createGLMTrainFrame
             groups.sort(key=lambda g: _group_key(g[0]))
         model = RuleFitModel(model_key or make_key("rulefit"), p, info)

@@ -39,7 +39,7 @@ _HIP_SIGS = {
     "h2o_tree_all": [c_void_p, c_void_p],
     "h2o_tree_leaves": [c_void_p, c_void_p],
     "h2o_hist_build": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p,
-                       c_int, c_int, c_void_p, c_void_p, c_int, c_ll, c_int, c_void_p],
+                       c_int, c_int, c_void_p, c_void_p, c_int, c_ll, c_int, c_void_p, c_void_p],
     "h2o_split_find": [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_double, c_double,
                        c_double, c_double, c_double, c_int, c_int, c_ull, c_int, c_void_p, c_void_p, c_void_p, c_int,
                        c_int, c_int, c_void_p],
@@ -108,7 +108,9 @@ def hip():
             if _hip is None:
                 # build_hip() is a no-op when the library is newer than every source; a stale library
                 # (launcher signatures changed since it was built) is rebuilt instead of being loaded
-                path = build_native.build_hip(force=bool(os.environ.get("H2O_AMD_REBUILD")))
+                # H2O_HIP_LIB: an alternative build of the same sources (A/B runs of compile-time kernel variants)
+                path = os.environ.get("H2O_HIP_LIB") or build_native.build_hip(
+                    force=bool(os.environ.get("H2O_AMD_REBUILD")))
                 lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
                 _check_abi(lib, "libh2o_hip")
                 _hip = _bind(lib, _HIP_SIGS)

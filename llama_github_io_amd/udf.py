@@ -70,7 +70,26 @@ def custom_metric_value(ref: str, preds: np.ndarray, actual: np.ndarray, w=None,
     ``preds`` [N, P] in the reference's prediction layout ([label, p0, p1, ...] or [value]),
     ``actual`` [N] (class index for classification)."""
     name, obj = resolve(ref)
+    return name, custom_metric_finish(ref, [custom_metric_state(ref, preds, actual, w, offset, model)])
+
+
+def custom_metric_finish(ref: str, states: list) -> float:
+    """The reduce of per-shard map/reduce states (in shard order; empty shards give None) and the metric —
+    MRTask's reduce across nodes (water/udf/CMetricFunc: the state is all that travels)."""
+    _, obj = resolve(ref)
+    state = None
+    for s in states:
+        if s is not None:
+            state = s if state is None else obj.reduce(state, s)
+    return float(obj.metric(state))
+
+
+def custom_metric_state(ref: str, preds: np.ndarray, actual: np.ndarray, w=None, offset=None, model=None):
+    """map + reduce over the rows of one shard: the shard's metric state (None for no rows)."""
+    name, obj = resolve(ref)
     n = preds.shape[0]
+    if n == 0:
+        return None
     w = np.ones(n) if w is None else np.asarray(w, dtype=np.float64)
     o = np.zeros(n) if offset is None else np.asarray(offset, dtype=np.float64)
     try:                                    # vectorised: columns in, per-row state columns out, summed
@@ -95,7 +114,7 @@ def custom_metric_value(ref: str, preds: np.ndarray, actual: np.ndarray, w=None,
         for i in range(n):
             s = obj.map(list(preds[i]), [float(actual[i])], float(w[i]), float(o[i]), model)
             state = s if state is None else obj.reduce(state, s)
-    return name, float(obj.metric(state))
+    return state
 
 
 class CustomDistributionFns:

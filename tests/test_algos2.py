@@ -195,6 +195,55 @@ def test_glrm_column_losses_and_outputs(df):
     assert g2._model.output["iterations"] <= 4
 
 
+def test_rulefit_max_categorical_levels_enum_limited():
+    """RuleFit.java:113-114: the rule trees see categoricals through EnumLimited(max_categorical_levels); rules on
+    the grouped 'other' level still evaluate on the original levels."""
+    from llama_github_io_amd.models.base import DataInfo
+    from llama_github_io_amd.models.rulefit import RuleFitTrainer
+    import torch
+    g = torch.Generator().manual_seed(2)
+    N = 3000
+    lv = torch.randint(0, 12, (N,), generator=g).float()
+    x1 = torch.randn(N, generator=g)
+    y = ((lv >= 6).float() * 1.5 + 0.5 * x1 + 0.3 * torch.randn(N, generator=g))
+    X = torch.stack([lv, x1])
+    info = DataInfo(["c", "x1"], np.array([1, 0], np.int32), [[f"L{i}" for i in range(12)], None], "y", None)
+    m = RuleFitTrainer(dict(max_categorical_levels=3, rule_generation_ntrees=5, min_rule_length=1,
+                            max_rule_length=2, seed=1, model_type="rules")).fit(X, y, None, None, info)
+    cat_conds = [c for _, rules in m.rule_groups for r in rules for c in r.conds if c.ctype == "cat"]
+    assert cat_conds and any("other" in c.level_names for c in cat_conds)
+    for c in cat_conds:       # every condition is on original level indices, 'other' expanded to its 9 levels
+        assert set(c.levels) <= set(range(12))
+        if "other" in c.level_names:
+            assert len(c.levels) >= 9
+    m10 = RuleFitTrainer(dict(max_categorical_levels=20, rule_generation_ntrees=5, min_rule_length=1, max_rule_length=2, seed=1,
+                              model_type="rules")).fit(X, y, None, None, info)
+    assert not any("other" in c.level_names for _, rules in m10.rule_groups for r in rules for c in r.conds
+                   if c.ctype == "cat")
+
+
+def test_glrm_expand_user_y(df):
+    """GLRM.java:187,400-425: with expand_user_y (default) user_y holds the original columns, categoricals as
+    levels, and is one-hot expanded; expand_user_y=False takes already expanded archetypes. Both give the same
+    start, so the same model."""
+    from llama_github_io_amd.models.base import DataInfo
+    from llama_github_io_amd.models.glrm import GLRMTrainer
+    import torch
+    g = torch.Generator().manual_seed(3)
+    N = 400
+    X = torch.stack([torch.randn(N, generator=g), torch.randint(0, 3, (N,), generator=g).float(),
+                     torch.randn(N, generator=g)])
+    info = DataInfo(["a", "c", "b"], np.array([0, 1, 0], np.int32), [None, ["x", "y", "z"], None], None, None)
+    orig = np.array([[0.5, 2, -1.0], [-0.3, 0, 0.7]])                 # a, c (level index), b
+    expanded = np.array([[0, 0, 1, 0.5, -1.0], [1, 0, 0, -0.3, 0.7]])  # c.x c.y c.z | a b
+    base = dict(k=2, init="User", max_iterations=5, transform="NONE", seed=1)
+    m1 = GLRMTrainer(dict(base, user_y=orig)).fit(X, None, None, None, info)
+    m2 = GLRMTrainer(dict(base, user_y=expanded, expand_user_y=False)).fit(X, None, None, None, info)
+    np.testing.assert_allclose(np.array(m1.archetypes()), np.array(m2.archetypes()), rtol=1e-9, atol=1e-9)
+    with pytest.raises(ValueError, match="same number of columns"):
+        GLRMTrainer(dict(base, user_y=orig, expand_user_y=False)).fit(X, None, None, None, info)
+
+
 @pytest.mark.parametrize("word_model", ["CBOW", "SkipGram"])
 def test_word2vec_word_models_group_cooccurring_words(word_model):
     """word_model=CBOW (WordVectorTrainer.CBOW / hierarchicalSoftmaxCBOW) and SkipGram: words that share

@@ -89,10 +89,25 @@ CASES = {
     "extendedisolationforest": ("extendedisolationforest", dict(ntrees=5, seed=5, extension_level=2), None),
     "gbm_quantile_weighted": ("gbm", dict(ntrees=3, max_depth=3, seed=5, distribution="quantile", quantile_alpha=0.3,
                                           weights_column="w"), "yr"),
+    # custom metric (CMetricFunc map/reduce): per-shard states reduced across ranks, no row gather
+    "gbm_custom_metric": ("gbm", dict(ntrees=3, max_depth=3, seed=5), "yr"),
 }
 
+
+class WeightedMAE:
+    """A CMetricFunc (h2o-py custom metric protocol): state = [sum w|err|, sum w]."""
+
+    def map(self, pred, act, w, o, model):
+        return [w * abs(pred[0] - act[0]), w]
+
+    def reduce(self, l, r):
+        return [l[0] + r[0], l[1] + r[1]]
+
+    def metric(self, l):
+        return l[0] / l[1]
+
 METRIC_KEYS = ("AUC", "logloss", "MSE", "RMSE", "mae", "mean_per_class_error", "tot_withinss", "r2", "AUUC", "qini",
-               "concordance", "loglik")
+               "concordance", "loglik", "custom_metric_value")
 
 
 def _run_cases(csv, names, out_path):
@@ -120,6 +135,8 @@ def _run_cases(csv, names, out_path):
         pp = dict(params)
         if name == "quantile_weighted_low":
             pp["weights_column"] = "w"
+        if name == "gbm_custom_metric":
+            pp["custom_metric_func"] = h2o.upload_custom_metric(WeightedMAE, func_name="dist_wmae")
         if algo == "stackedensemble":
             base = [builder.train(a, dict(nfolds=3, fold_assignment="Modulo", keep_cross_validation_predictions=True,
                                           seed=1, **kw), x=x, y=y, training_frame=fr, model_id=f"se_{a}")

@@ -54,6 +54,25 @@ def test_thin_plate_two_columns(data):
     assert np.corrcoef(pred, truth)[0, 1] > 0.97
 
 
+def test_thin_plate_standardize_tp_gam_cols(data):
+    """GAMModel._standardize_tp_gam_cols (GamUtilsThinPlateRegression: distances on sd-scaled coordinates): with one
+    column on a 1000x larger scale the isotropic distance ignores the small column unless the columns are
+    standardized, which recovers the fit."""
+    import h2o
+    from h2o.estimators import H2OGeneralizedAdditiveEstimator
+    fr, a, b, shift = data
+    fr2 = h2o.H2OFrame({"a": (a * 1000.0).tolist(), "b": b.tolist(), "y": (np.sin(a) + 0.5 * b ** 2).tolist()})
+    preds = {}
+    for flag in (False, True):
+        m = H2OGeneralizedAdditiveEstimator(gam_columns=[["a", "b"]], num_knots=[40], bs=[1], family="gaussian",
+                                            standardize_tp_gam_cols=flag)
+        m.train(x=[], y="y", training_frame=fr2)
+        preds[flag] = m.predict(fr2).as_data_frame()["predict"].values
+    truth = np.sin(a) + 0.5 * b ** 2
+    assert np.abs(preds[True] - preds[False]).max() > 1e-3
+    assert np.corrcoef(preds[True], truth)[0, 1] > 0.97
+
+
 def test_monotone_ispline(data):
     from h2o.estimators import H2OGeneralizedAdditiveEstimator
     import h2o
