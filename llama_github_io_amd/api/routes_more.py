@@ -181,89 +181,7 @@ def register(app, _params, _unquote, _model_json):
     @app.get("/3/Tree")
     def tree(model: str, tree_number: int, tree_class: str | None = None, plain_language_rules: str = "AUTO"):
         """hex/tree/TreeHandler.java: one tree as breadth-first node arrays."""
-        m = get_model(model)
-        forest = getattr(m, "forest", None)
-        if forest is None:
-            raise ValueError(f"model {model} has no trees")
-        dom = m.info.response_domain
-        K = max(int(getattr(forest, "n_classes_out", 1) or 1), 1)
-        cls = 0
-        tc = _unquote(tree_class)
-        if tc not in (None, "", "null") and dom is not None and K > 1:
-            if tc not in dom:
-                raise ValueError(f"tree_class {tc!r} is not a response level")
-            cls = dom.index(tc)
-        idx = [i for i, c in enumerate(forest.tree_class) if c == cls]
-        if tree_number < 0 or tree_number >= len(idx):
-            raise ValueError(f"tree_number must be in [0, {len(idx)})")
-        t = forest.trees[idx[tree_number]]
-        order, pos = [0], {0: 0}
-        i = 0
-        while i < len(order):
-            n = order[i]
-            if t.feat[n] >= 0:
-                for c in (int(t.left[n]), int(t.right[n])):
-                    pos[c] = len(order)
-                    order.append(c)
-            i += 1
-        names = m.info.x
-        L, R, desc, thr, feats, levels, nas, preds = [], [], [], [], [], [None] * len(order), [], []
-        for q, n in enumerate(order):
-            if t.feat[n] < 0:
-                L.append(-1)
-                R.append(-1)
-                thr.append("NaN")
-                feats.append(None)
-                nas.append(None)
-                preds.append(float(t.value[n]))
-                desc.append(f"Leaf node {n}: prediction {float(t.value[n]):.6g}")
-                continue
-            f = int(t.feat[n])
-            ln, rn = int(t.left[n]), int(t.right[n])
-            L.append(pos[ln] + 1000000)          # node ids (opaque to the client): BFS position + offset
-            R.append(pos[rn] + 1000000)
-            feats.append(names[f])
-            nas.append("LEFT" if bool(t.na_left[n]) else "RIGHT")
-            preds.append(float("nan"))
-            if t.is_cat[n] and t.cat_bits[n] is not None:
-                bits = np.asarray(t.cat_bits[n], dtype=np.uint32)
-                nb = int(t.cat_nbits[n]) if t.cat_nbits[n] else len(m.info.domains[f] or [])
-                left_lv = [lv for lv in range(nb) if (bits[lv >> 5] >> (lv & 31)) & 1]
-                right_lv = [lv for lv in range(nb) if not (bits[lv >> 5] >> (lv & 31)) & 1]
-                levels[pos[ln]] = left_lv
-                levels[pos[rn]] = right_lv
-                thr.append("NaN")
-                desc.append(f"Node {n}: {names[f]} in left levels; NA {'left' if t.na_left[n] else 'right'}")
-            else:
-                thr.append(float(t.thr[n]))
-                desc.append(f"Node {n}: {names[f]} < {float(t.thr[n]):.6g}; NA {'left' if t.na_left[n] else 'right'}")
-        rules = None
-        if str(plain_language_rules).upper() == "TRUE" or (str(plain_language_rules).upper() == "AUTO" and len(order) < 64):
-            rules = _rules(order, L, R, feats, thr, nas, preds)
-        return {"__meta": v3.meta("TreeV3", "Tree"), "model": v3.model_key(m.key), "tree_number": tree_number,
-                "tree_class": tc if tc not in ("null",) else None, "left_children": L, "right_children": R,
-                "root_node_id": 1000000, "thresholds": thr, "features": feats, "levels": levels, "nas": nas,
-                "descriptions": desc, "predictions": [v3.num(v) for v in preds],
-                "tree_decision_path": rules, "decision_paths": None if rules is None else [rules] * len(order),
-                "plain_language_rules": plain_language_rules}
-
-    def _rules(order, L, R, feats, thr, nas, preds):
-        lines = []
-
-        def walk(i, conds):
-            if L[i] == -1:
-                lines.append(("If " + " and ".join(conds) if conds else "Always") + f" then {preds[i]:.6g}")
-                return
-            ln, rn = L[i] - 1000000, R[i] - 1000000
-            t = thr[i]
-            if t == "NaN":
-                walk(ln, conds + [f"{feats[i]} in left levels"])
-                walk(rn, conds + [f"{feats[i]} in right levels"])
-            else:
-                walk(ln, conds + [f"{feats[i]} < {t:.6g}" + (" or NA" if nas[i] == "LEFT" else "")])
-                walk(rn, conds + [f"{feats[i]} >= {t:.6g}" + (" or NA" if nas[i] == "RIGHT" else "")])
-        walk(0, [])
-        return "\n".join(lines)
+        return tree_json(get_model(model), tree_number, _unquote(tree_class), plain_language_rules)
 
     # ------------------------------------------------------------------------- frame transforms
     @app.post("/3/Interaction")
@@ -823,13 +741,43 @@ def register(app, _params, _unquote, _model_json):
     for meth, path, why in (("POST", "/3/DecryptionSetup", "encrypted input files are not supported"),
                             ("POST", "/3/ImportHiveTable", "Hive is not available (single-node MI355X engine)"),
                             ("POST", "/3/SaveToHiveTable", "Hive is not available (single-node MI355X engine)"),
-                            ("POST", "/99/Assembly", "munging pipelines (Assembly) are not supported; use Rapids"),
-                            ("GET", "/99/Assembly.java/{aid}/{fname}", "munging pipelines (Assembly) are not supported")):
+                            # the MOJO 2 pipeline export needs the external mojo2-runtime jar on the Java
+                            # classpath in the reference too (h2o-py assembly.py:download_mojo)
+                            ("GET", "/99/Assembly.fetch_mojo_pipeline/{aid}/{fname}",
+                             "MOJO 2 munging pipelines need the mojo2-runtime library, which this engine does not "
+                             "ship; export the assembly as a POJO (/99/Assembly.java)")):
         def make(why=why):
             def h():
                 raise NotImplementedError(why)
             return h
         app.add_api_route(path, make(), methods=[meth])
+
+    # ---- munging pipelines (water/api/AssemblyHandler.java, AssemblyV99)
+    @app.post("/99/Assembly")
+    async def assembly_fit(request: Request):
+        from .. import assembly
+        from ..core import dkv as _dkv
+        p = await _params(request)
+        steps = p.get("steps")
+        if isinstance(steps, str):
+            steps = [steps]
+        fid = _unquote(p.get("frame"))
+        fr = _dkv.get(fid)
+        if fr is None:
+            raise KeyError(f"frame {fid} not found")
+        asm, out = assembly.fit_rest([_unquote(x) for x in steps or []], fr)
+        return {"__meta": v3.meta("AssemblyV99", "Assembly"), "steps": steps, "frame": v3.frame_key(fid),
+                "assembly": {"__meta": v3.meta("AssemblyKeyV3", "Key<Assembly>"), "name": asm.key,
+                             "type": "Key<Assembly>", "URL": None},
+                "result": v3.frame_key(out.frame_id)}
+
+    @app.get("/99/Assembly.java/{aid}/{fname}")
+    def assembly_java(aid: str, fname: str):
+        from ..core import dkv as _dkv
+        asm = _dkv.get(aid)
+        if asm is None or not hasattr(asm, "to_java"):
+            raise KeyError(f"assembly {aid} not found")
+        return PlainTextResponse(asm.to_java(fname))
 
     @app.post("/99/ImportSQLTable")
     async def import_sql(request: Request):
@@ -841,3 +789,90 @@ def register(app, _params, _unquote, _model_json):
         dest = fr.frame_id
         job = done_job(dest, "ImportSQLTable")
         return {"__meta": v3.meta("JobV3", "Job"), "job": v3.job(job), **v3.job(job)}
+
+
+def tree_json(m, tree_number: int, tc=None, plain_language_rules: str = "AUTO") -> dict:
+    """TreeV3 of one tree of a tree model (hex/tree/TreeHandler.java), breadth-first node arrays; shared by GET
+    /3/Tree and the in-process ``h2o.tree.H2OTree``."""
+    forest = getattr(m, "forest", None)
+    if forest is None:
+        raise ValueError(f"model {m.key} has no trees")
+    dom = m.info.response_domain
+    K = max(int(getattr(forest, "n_classes_out", 1) or 1), 1)
+    cls = 0
+    if tc not in (None, "", "null") and dom is not None and K > 1:
+        if tc not in dom:
+            raise ValueError(f"tree_class {tc!r} is not a response level")
+        cls = dom.index(tc)
+    idx = [i for i, c in enumerate(forest.tree_class) if c == cls]
+    if tree_number < 0 or tree_number >= len(idx):
+        raise ValueError(f"tree_number must be in [0, {len(idx)})")
+    t = forest.trees[idx[tree_number]]
+    order, pos = [0], {0: 0}
+    i = 0
+    while i < len(order):
+        n = order[i]
+        if t.feat[n] >= 0:
+            for c in (int(t.left[n]), int(t.right[n])):
+                pos[c] = len(order)
+                order.append(c)
+        i += 1
+    names = m.info.x
+    L, R, desc, thr, feats, levels, nas, preds = [], [], [], [], [], [None] * len(order), [], []
+    for q, n in enumerate(order):
+        if t.feat[n] < 0:
+            L.append(-1)
+            R.append(-1)
+            thr.append("NaN")
+            feats.append(None)
+            nas.append(None)
+            preds.append(float(t.value[n]))
+            desc.append(f"Leaf node {n}: prediction {float(t.value[n]):.6g}")
+            continue
+        f = int(t.feat[n])
+        ln, rn = int(t.left[n]), int(t.right[n])
+        L.append(pos[ln] + 1000000)          # node ids (opaque to the client): BFS position + offset
+        R.append(pos[rn] + 1000000)
+        feats.append(names[f])
+        nas.append("LEFT" if bool(t.na_left[n]) else "RIGHT")
+        preds.append(float("nan"))
+        if t.is_cat[n] and t.cat_bits[n] is not None:
+            bits = np.asarray(t.cat_bits[n], dtype=np.uint32)
+            nb = int(t.cat_nbits[n]) if t.cat_nbits[n] else len(m.info.domains[f] or [])
+            left_lv = [lv for lv in range(nb) if (bits[lv >> 5] >> (lv & 31)) & 1]
+            right_lv = [lv for lv in range(nb) if not (bits[lv >> 5] >> (lv & 31)) & 1]
+            levels[pos[ln]] = left_lv
+            levels[pos[rn]] = right_lv
+            thr.append("NaN")
+            desc.append(f"Node {n}: {names[f]} in left levels; NA {'left' if t.na_left[n] else 'right'}")
+        else:
+            thr.append(float(t.thr[n]))
+            desc.append(f"Node {n}: {names[f]} < {float(t.thr[n]):.6g}; NA {'left' if t.na_left[n] else 'right'}")
+    rules = None
+    if str(plain_language_rules).upper() == "TRUE" or (str(plain_language_rules).upper() == "AUTO" and len(order) < 64):
+        rules = tree_rules(L, R, feats, thr, nas, preds)
+    return {"__meta": v3.meta("TreeV3", "Tree"), "model": v3.model_key(m.key), "tree_number": tree_number,
+            "tree_class": tc if tc not in ("null",) else None, "left_children": L, "right_children": R,
+            "root_node_id": 1000000, "thresholds": thr, "features": feats, "levels": levels, "nas": nas,
+            "descriptions": desc, "predictions": [v3.num(v) for v in preds],
+            "tree_decision_path": rules, "decision_paths": None if rules is None else [rules] * len(order),
+            "plain_language_rules": plain_language_rules}
+
+
+def tree_rules(L, R, feats, thr, nas, preds):
+    lines = []
+
+    def walk(i, conds):
+        if L[i] == -1:
+            lines.append(("If " + " and ".join(conds) if conds else "Always") + f" then {preds[i]:.6g}")
+            return
+        ln, rn = L[i] - 1000000, R[i] - 1000000
+        t = thr[i]
+        if t == "NaN":
+            walk(ln, conds + [f"{feats[i]} in left levels"])
+            walk(rn, conds + [f"{feats[i]} in right levels"])
+        else:
+            walk(ln, conds + [f"{feats[i]} < {t:.6g}" + (" or NA" if nas[i] == "LEFT" else "")])
+            walk(rn, conds + [f"{feats[i]} >= {t:.6g}" + (" or NA" if nas[i] == "RIGHT" else "")])
+    walk(0, [])
+    return "\n".join(lines)

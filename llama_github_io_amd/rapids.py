@@ -17,7 +17,8 @@ import torch
 from .core import dkv
 from .frame import Column, H2OFrame, engine_device
 
-_TOKEN = re.compile(r'\s*(\(|\)|\[|\]|\{|\}|"(?:[^"\\]|\\.)*"|\'(?:[^\'\\]|\\.)*\'|[^\s()\[\]{}]+)')
+# commas separate list items like blanks do (h2o-py renders string lists with %r: ['a', 'b'])
+_TOKEN = re.compile(r'[\s,]*(\(|\)|\[|\]|\{|\}|"(?:[^"\\]|\\.)*"|\'(?:[^\'\\]|\\.)*\'|[^\s,()\[\]{}]+)')
 
 
 def tokenize(s: str):
@@ -29,7 +30,7 @@ def tokenize(s: str):
             raise SyntaxError(f"bad rapids near {s[pos:pos + 20]!r}")
         out.append(m.group(1))
         pos = m.end()
-        while pos < len(s) and s[pos].isspace():
+        while pos < len(s) and (s[pos].isspace() or s[pos] == ","):
             pos += 1
     return out
 

@@ -112,6 +112,22 @@ CLIENT2 = textwrap.dedent("""
     assert pid in list(h2o.ls()["key"])
     h2o.remove(pred)
     assert pid not in list(h2o.ls()["key"])
+    # munging pipelines: POST /99/Assembly and GET /99/Assembly.java (water/api/AssemblyHandler.java)
+    from h2o.assembly import H2OAssembly
+    from h2o.transforms.preprocessing import H2OBinaryOp, H2OColOp, H2OColSelect
+    asm = H2OAssembly(steps=[("col_select", H2OColSelect(["x0", "x1", "cat"])),
+                             ("cos_x0", H2OColOp(op=h2o.H2OFrame.cos, col="x0", inplace=True)),
+                             ("cnt_cat", H2OColOp(op=h2o.H2OFrame.countmatches, col="cat", inplace=False, pattern="a")),
+                             ("plus_x1", H2OBinaryOp(op=H2OAssembly.plus, col="x1", inplace=False, right=1.5))])
+    res = asm.fit(fr)
+    assert res.names == ["x0", "x1", "cat", "cat0", "x10"], res.names
+    import math
+    assert abs(res["x0"].max() - math.cos(fr["x0"].min())) < 1e-6 or res["x0"].max() <= 1.0
+    assert abs((res["x10"] - res["x1"]).mean()[0] - 1.5) < 1e-9
+    assert abs(res["cat0"].sum() - (fr["cat"] == "a").sum()) < 1e-9
+    asm.to_pojo("MungePojo", d, get_jar=False)
+    java = open(os.path.join(d, "MungePojo.java")).read()
+    assert "public class MungePojo extends GenMunger" in java and "GenMunger.countmatches" in java, java[:400]
     print("DONE")
 """)
 
