@@ -72,7 +72,12 @@ struct SplitParams {
   int mode;                // 0 = squared error (GBM/DRF, H2O semantics), 1 = Newton (XGBoost), 2 = random (IsoForest)
   int random_split;        // extremely randomized / isolation: pick a random threshold
   unsigned long long seed;
+  int hist_type;           // numeric candidate lattice (with adapt_nb > 1): HT_* below
+  int pad;
 };
+
+// histogram types (SharedTreeParameters.HistogramType) as candidate lattices over the global bins
+enum { HT_QUANTILES = 0, HT_UNIFORM = 1, HT_RANDOM = 2, HT_ROBUST = 3, HT_ROUND_ROBIN = 4 };
 
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ unsigned long long splitmix64(unsigned long long x) {
@@ -663,6 +668,12 @@ struct Derive {
   const Node* nodes;       // this level's node list (parent, build)
 };
 
+// a + x * y rounded twice (never contracted into an fma): split points the host reference reproduces bit-exactly
+__device__ __forceinline__ double add_mul_rn(double a, double x, double y) {
+#pragma clang fp contract(off)
+  return a + x * y;
+}
+
 // k_split_find: best split point per (node, feature). grid = (C, F), block 256 (thread = bin).
 __global__ __launch_bounds__(256) void k_split_find(
     double* __restrict__ hist, int slot_doubles, const int* __restrict__ meta, int F,
@@ -784,21 +795,36 @@ __global__ __launch_bounds__(256) void k_split_find(
       rand_b = s_lo + 1 + (int)(hsh % (unsigned long long)(s_hi - s_lo));
     }
   }
-  // UniformAdaptive (DHistogram, the H2O default): a node's numeric split candidates are the
-  // adapt_nb - 1 uniform cut points of its occupied value range; on the global-bin lattice a
-  // threshold t ("bins < t go left" = x < edge[t-1]) is kept iff some cut point falls in
-  // (edge[t-2], edge[t-1]]. adapt_nb = max(nbins, nbins_top_level >> level); 0 = QuantilesGlobal.
+  // Numeric candidate lattice of the histogram type (DHistogram / DTree), over the node's occupied value range
+  // [lo, hi] on the global-bin lattice: a threshold t ("bins < t go left" = x < edge[t-1]) is kept iff one of
+  // the type's split points falls in (edge[t-2], edge[t-1]]. adapt_nb = max(nbins, nbins_top_level >> level).
+  //  UniformAdaptive: adapt_nb - 1 uniform cut points (the H2O default).
+  //  Random: adapt_nb - 1 uniformly random cut points (DHistogram.makeRandomSplitPoints).
+  //  UniformRobust: UniformAdaptive, unless <= 20% of the uniform cells hold data; then GuidedSplitPoints:
+  //    the non-empty cells are kept and refined uniformly, the freed budget adapt_nb - K - 2 handed out in
+  //    ceil(budget * share) portions by descending cell share (DTree.java:398-409). The share is the cell's
+  //    weight: the 2-statistic histogram has no per-bin sum of squares for the reference's per-bin SE.
+  //  RoundRobin: one of {AUTO, UniformAdaptive, Random, QuantilesGlobal} per (node, feature), drawn from
+  //    the tree seed (DHistogram.java:226-229).
+  int lt = (adapt_nb > 1 && edges != nullptr && !cat && !random_mode) ? p.hist_type : HT_QUANTILES;
+  if (lt == HT_ROUND_ROBIN) {
+    const unsigned r = (unsigned)(splitmix64(p.seed ^ 0xDECAFull ^ ((unsigned long long)level << 48) ^
+                                             ((unsigned long long)node << 20) ^ (unsigned long long)(f + f0)) & 3ull);
+    lt = r == 3 ? HT_QUANTILES : (r == 2 ? HT_RANDOM : HT_UNIFORM);
+  }
   bool lattice_ok = true;
-  if (adapt_nb > 1 && edges != nullptr && !cat && !random_mode) {
-    __shared__ int a_lo, a_hi;
-    if (t == 0) { a_lo = 0; a_hi = -1; }
+  if (lt != HT_QUANTILES) {
+    __shared__ int a_lo, a_hi, s_guided;
+    __shared__ unsigned char smark[256];
+    if (t == 0) { a_lo = 0; a_hi = -1; s_guided = 0; }
+    smark[t] = 0;
     __syncthreads();
     const double cw = sw[t], pw = t > 0 ? sw[t - 1] : 0.0;
     if (t < nb && cw > 0 && pw == 0) a_lo = t;
     if (t < nb && W > 0 && cw == W && pw < W) a_hi = t;
     __syncthreads();
     const float* e = edges + (size_t)f * 255;
-    if (a_hi > a_lo && a_hi - a_lo + 1 > adapt_nb) {
+    if (a_hi > a_lo && (lt == HT_RANDOM || a_hi - a_lo + 1 > adapt_nb)) {
       const double lo = (double)e[a_lo > 0 ? a_lo - 1 : 0];
       const double hi = (double)e[a_hi <= nb - 2 ? a_hi : nb - 2];
       if (hi > lo) {
@@ -807,7 +833,78 @@ __global__ __launch_bounds__(256) void k_split_find(
           double c = floor((x - lo) * sc);
           return (int)(c < 0 ? 0 : (c > adapt_nb - 1 ? adapt_nb - 1 : c));
         };
-        lattice_ok = t >= 1 && t < nb && cnt((double)e[t - 1]) > (t >= 2 ? cnt((double)e[t - 2]) : 0);
+        // a split point x marks threshold t = 1 + (first i with edge[i] >= x), t <= nb - 1
+        auto mark = [&](double x) {
+          int a = 0, b = nb - 1;
+          while (a < b) { const int m = (a + b) >> 1; if ((double)e[m] >= x) b = m; else a = m + 1; }
+          if (a < nb - 1) smark[a + 1] = 1;
+        };
+        if (lt == HT_ROBUST) {
+          // cells (adapt_nb < 256 here) of the uniform lattice: bin t's lower edge lies in cell(t); the
+          // bins of one cell are contiguous, so a cell's weight is a difference of the prefix sums
+          __shared__ int cstart[256];
+          __shared__ double cwt[256];
+          __shared__ int s_k;
+          if (t == 0) s_k = 0;
+          cwt[t] = 0.0;
+          __syncthreads();
+          const int ci = (t >= a_lo && t <= a_hi) ? (t == a_lo ? 0 : cnt((double)e[t - 1])) : -1;
+          const int cprev = (t > a_lo && t <= a_hi) ? (t - 1 == a_lo ? 0 : cnt((double)e[t - 2])) : -1;
+          if (ci >= 0 && ci != cprev) cstart[ci] = t;
+          __syncthreads();
+          const int cnext = (t >= a_lo && t < a_hi) ? cnt((double)e[t]) : -1;
+          if (ci >= 0 && ci != cnext) {
+            const double wc = sw[t] - (cstart[ci] > 0 ? sw[cstart[ci] - 1] : 0.0);
+            cwt[ci] = wc;
+            if (wc > 0) atomicAdd(&s_k, 1);
+          }
+          __syncthreads();
+          const int K = s_k;
+          const int budget = adapt_nb - K - 2;
+          if ((double)K <= 0.2 * (double)adapt_nb && budget > 0 && K > 0) {
+            // rank of this cell in descending weight (ties: lower cell first), then the budget prefix
+            const double mw = t < adapt_nb ? cwt[t] : 0.0;
+            __shared__ int qv[256];
+            __shared__ int rk[256];
+            int q = 0, r = 0;
+            if (mw > 0) {
+              q = (int)ceil((double)budget * mw / W);
+              for (int c = 0; c < adapt_nb; ++c) {
+                const double oc = cwt[c];
+                r += (oc > mw || (oc == mw && c < t)) ? 1 : 0;
+              }
+            }
+            qv[t] = q; rk[t] = mw > 0 ? r : 1 << 20;
+            __syncthreads();
+            if (mw > 0) {
+              int before = 0;
+              for (int c = 0; c < adapt_nb; ++c) before += (rk[c] < r) ? qv[c] : 0;
+              const int left = budget - before;
+              const int nnew = left <= 0 ? 0 : (q < left ? q : left);
+              const double step = (hi - lo) / (double)adapt_nb;
+              const double c0 = add_mul_rn(lo, step, (double)t);
+              const double sub = step / (double)(1 + nnew);
+              for (int j = 0; j <= nnew; ++j) mark(add_mul_rn(c0, sub, (double)j));
+            }
+            if (t == 0) { mark(lo); mark(hi); s_guided = 1; }
+          }
+          __syncthreads();
+          if (!s_guided) lt = HT_UNIFORM;
+        }
+        if (lt == HT_UNIFORM) {
+          lattice_ok = t >= 1 && t < nb && cnt((double)e[t - 1]) > (t >= 2 ? cnt((double)e[t - 2]) : 0);
+        } else {
+          if (lt == HT_RANDOM) {
+            for (int k = 1 + t; k < adapt_nb; k += 256) {
+              const unsigned long long h = splitmix64(p.seed ^ 0xC0FFEEull ^ ((unsigned long long)level << 48) ^
+                                                      ((unsigned long long)node << 20) ^
+                                                      ((unsigned long long)(f + f0) << 10) ^ (unsigned long long)k);
+              mark(add_mul_rn(lo, hi - lo, (double)(h >> 11) * 0x1p-53));
+            }
+          }
+          __syncthreads();
+          lattice_ok = t >= 1 && t < nb && smark[t] != 0;
+        }
       }
     }
   }
@@ -1877,10 +1974,10 @@ static int split_find_launch(void* hist, int slot_doubles, const void* meta, int
 int h2o_split_find(const void* hist, int slot_doubles, const void* meta, int cap, int F, const void* nbins_f,
                    const void* iscat_f, const void* mono_f, double min_w, double msi, double lambda_, double alpha,
                    double gamma, int mode, int random_split, unsigned long long seed, int level, void* cand,
-                   void* root_w, const void* edges, int adapt_nb, int f0, int FL, hipStream_t s) {
+                   void* root_w, const void* edges, int adapt_nb, int hist_type, int f0, int FL, hipStream_t s) {
   SplitParams p;
   p.min_w = min_w; p.min_split_improvement = msi; p.lambda = lambda_; p.alpha = alpha; p.gamma = gamma;
-  p.mode = mode; p.random_split = random_split; p.seed = seed;
+  p.mode = mode; p.random_split = random_split; p.seed = seed; p.hist_type = hist_type; p.pad = 0;
   return split_find_launch((void*)hist, slot_doubles, meta, cap, F, nbins_f, iscat_f, mono_f, p, level, cand, root_w,
                            edges, adapt_nb, f0, FL, Derive{nullptr, 0, 0, nullptr, nullptr}, s);
 }
@@ -2081,7 +2178,7 @@ struct TreePlan {
   int caps[TP_MAXL], tiles_cap[TP_MAXL];
   // per tree
   void *aux, *amax_bits, *feat_ok;
-  int compute_amax, k_cols, packed, leaf_native, log_link, pad1;
+  int compute_amax, k_cols, packed, leaf_native, log_link, hist_type;
   unsigned long long seed;
   double scale, kclamp, mx;
   int kc_level[TP_MAXL];   // per-level column sample size (col_sample_rate_change_per_level); 0 = k_cols
@@ -2164,7 +2261,7 @@ int h2o_tree_find(const TreePlan* P, int d, hipStream_t s) {
   const void* hp = (d % 2) ? P->hist0 : P->hist1;      // level d-1 (unused at the root: build = 1)
   SplitParams p;
   p.min_w = P->min_w; p.min_split_improvement = P->msi; p.lambda = P->lam; p.alpha = P->alpha; p.gamma = P->gamma;
-  p.mode = P->mode; p.random_split = P->random_split; p.seed = P->seed;
+  p.mode = P->mode; p.random_split = P->random_split; p.seed = P->seed; p.hist_type = P->hist_type; p.pad = 0;
   const int hs = P->sliced ? P->sslot : P->slot;
   const Derive dv = P->dist ? Derive{P->hrecv, P->cf32, P->sslot, (const double*)hp, (const Node*)P->nodes[d]}
                             : Derive{nullptr, 0, 0, nullptr, nullptr};

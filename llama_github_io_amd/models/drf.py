@@ -1,5 +1,6 @@
 """Distributed Random Forest and Extremely Randomized Trees (reference: ``hex/tree/drf/DRF.java``,
-``DRFModel.java``; ``histogram_type='Random'`` = XRT).
+``DRFModel.java``; ``histogram_type='Random'`` = XRT: random split points per histogram,
+``DHistogram.makeRandomSplitPoints``).
 
 Per iteration one tree per class (one tree for binomial/regression, ``binomial_double_trees`` builds
 two), each grown on the device engine with squared-error splits of the class indicator over a
@@ -57,11 +58,6 @@ class DRFTrainer(SharedTreeTrainer):
         p = dict(DRF_DEFAULTS)
         p.update({k: v for k, v in params.items() if v is not None or k not in p})
         super().__init__(p)
-
-    def _split_params(self):
-        sp = super()._split_params()
-        sp.random_split = str(self.p.get("histogram_type", "AUTO")).lower() == "random"
-        return sp
 
     def fit(self, X, y, w, offset, info, valid=None, model_key=None):
         self.nclass = len(info.response_domain) if info.response_domain else 1

@@ -503,10 +503,12 @@ class GLMTrainer:
 
     def _validate(self, fam, link, y, info):
         """The reference's family / solver checks (``hex/glm/GLM.java:876-953``), on global response ranges."""
+        def err(field, msg):     # ModelBuilder.error(): "ERRR on field: _family: ..."
+            raise ValueError(f"ERRR on field: _{field}: {msg}")
         solver = canon(self.p["solver"])
         if solver in ("gradientdescentlh", "gradientdescentsqerr") and fam != "ordinal":
-            raise ValueError("Solvers GRADIENT_DESCENT_LH and GRADIENT_DESCENT_SQERR are only supported for ordinal "
-                             "regression.  Do not choose them unless you specify your family to be ordinal")
+            err("solver", "Solvers GRADIENT_DESCENT_LH and GRADIENT_DESCENT_SQERR are only supported for ordinal "
+                           "regression.  Do not choose them unless you specify your family to be ordinal")
         ncls = len(info.response_domain) if info.response_domain is not None else 1
         yy = y[~torch.isnan(y)] if y is not None else None
         lo = float(coll.all_reduce_scalar(float(yy.min()) if yy is not None and yy.numel() else float("inf"),
@@ -515,26 +517,26 @@ class GLMTrainer:
                                           op=_MAX)) if yy is not None else 0.0
         if fam == "binomial" and ncls != 2 and not (ncls == 1 and lo >= 0 and hi <= 1 and
                                                      bool(((yy == 0) | (yy == 1)).all())):
-            raise ValueError("Binomial requires the response to be a 2-class categorical or a binary column (0/1)")
+            err("family", "Binomial requires the response to be a 2-class categorical or a binary column (0/1)")
         if fam in ("multinomial", "ordinal") and ncls <= 2:
-            raise ValueError(f"{fam.capitalize()} requires a categorical response with at least 3 levels (for 2 class "
-                             "problem use family=binomial.")
+            err("family", f"{fam.capitalize()} requires a categorical response with at least 3 levels (for 2 class "
+                           "problem use family=binomial.")
         if fam == "ordinal" and link in ("oprobit", "ologlog"):
-            raise ValueError("Ordinal regression only supports ologit as link.")
+            err("family", "Ordinal regression only supports ologit as link.")
         if fam in ("poisson", "negativebinomial"):
             if ncls != 1:
-                raise ValueError("Poisson and Negative Binomial require the response to be numeric.")
+                err("family", "Poisson and Negative Binomial require the response to be numeric.")
             if lo < 0:
-                raise ValueError("Poisson and Negative Binomial require response >= 0")
+                err("family", "Poisson and Negative Binomial require response >= 0")
             if fam == "negativebinomial" and float(self.p["theta"]) <= 0:
-                raise ValueError("Illegal Negative Binomial theta value.  Valid theta values be > 0 and <= 1.")
+                err("theta", "Illegal Negative Binomial theta value.  Valid theta values be > 0 and <= 1.")
         if fam == "gamma" and lo <= 0:
-            raise ValueError("Response value for gamma distribution must be greater than 0.")
+            err("family", "Response value for gamma distribution must be greater than 0.")
         if fam in ("tweedie", "quasibinomial") and ncls != 1:
-            raise ValueError(f"{fam.capitalize()} requires the response to be numeric.")
+            err("family", f"{fam.capitalize()} requires the response to be numeric.")
         if fam == "fractionalbinomial" and (lo < 0 or hi > 1):
-            raise ValueError(f"Response '{info.response}' must be between 0 and 1 for fractional_binomial family. "
-                             f"Min: {lo:f}, Max: {hi:f}")
+            err("response_column", f"Response '{info.response}' must be between 0 and 1 for fractional_binomial family. "
+                                     f"Min: {lo:f}, Max: {hi:f}")
 
     def fit(self, X, y, w, offset, info: DataInfo, valid=None, model_key=None):
         t0 = time.time()

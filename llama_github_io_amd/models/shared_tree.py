@@ -152,11 +152,17 @@ class SharedTreeTrainer:
         sp = T.SplitParams(min_w=float(self.p["min_rows"]), min_split_improvement=float(self.p["min_split_improvement"]),
                            mode=self.mode)
         ht = str(self.p.get("histogram_type", "AUTO")).lower().replace("_", "")
-        if ht in ("auto", "uniformadaptive") and getattr(self, "binning", None) is not None:
-            # DHistogram UniformAdaptive: nbins_top_level bins at the root, halved per level down to nbins
+        if ht not in T.HIST_TYPES:
+            raise ValueError(f"histogram_type {self.p.get('histogram_type')!r} is not one of "
+                             "AUTO, UniformAdaptive, Random, QuantilesGlobal, RoundRobin, UniformRobust")
+        if T.HIST_TYPES[ht] != T.HT_QUANTILES and getattr(self, "binning", None) is not None:
+            # DHistogram: nbins_top_level bins at the root, halved per level down to nbins, laid out as the
+            # type's split points (uniform / random / SE-guided / per-histogram round robin) over the
+            # global bin edges — see _lattice in ops/tree.py
             sp.adapt_nbins = int(self.p.get("nbins") or 20)
             sp.adapt_top = int(self.p.get("nbins_top_level") or 1024)
             sp.edges = self._edge_table()
+            sp.hist_type = T.HIST_TYPES[ht]
         return sp
 
     def _edge_table(self):

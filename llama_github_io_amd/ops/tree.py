@@ -38,6 +38,10 @@ DEC_DT = np.dtype([("feat", "<i4"), ("bin", "<i4"), ("na_left", "<i4"), ("is_cat
                    ("gain", "<f8"), ("wl", "<f8"), ("wr", "<f8"), ("predl", "<f4"), ("predr", "<f4")])
 CAND_BYTES = 88
 MODE_SE, MODE_NEWTON, MODE_RANDOM = 0, 1, 2
+# histogram types as candidate lattices over the global bins (k_split_find HT_*)
+HT_QUANTILES, HT_UNIFORM, HT_RANDOM, HT_ROBUST, HT_ROUND_ROBIN = 0, 1, 2, 3, 4
+HIST_TYPES = {"auto": HT_UNIFORM, "uniformadaptive": HT_UNIFORM, "random": HT_RANDOM, "uniformrobust": HT_ROBUST,
+              "roundrobin": HT_ROUND_ROBIN, "quantilesglobal": HT_QUANTILES}
 _M64 = (1 << 64) - 1
 
 
@@ -62,6 +66,8 @@ class SplitParams:
     adapt_nbins: int = 0
     adapt_top: int = 0
     edges: object = None
+    # lattice of the split points (HT_*): UniformAdaptive, Random, UniformRobust or RoundRobin
+    hist_type: int = 1
 
     def adapt_nb(self, level: int) -> int:
         if not self.adapt_nbins or self.edges is None:
@@ -102,6 +108,74 @@ def _leafv(mode, p, w, y):
     return y / w if w > 0 else 0.0
 
 
+def _lattice(p: SplitParams, level, node, f, nb, w, sw, W, seed, off):
+    """Allowed thresholds t = 1 .. nb-1 of the histogram type's split points (None = every threshold);
+    mirrors the lattice block of k_split_find (UniformAdaptive / Random / UniformRobust / RoundRobin)."""
+    anb = p.adapt_nb(level)
+    lt = p.hist_type if (anb > 1 and not off) else HT_QUANTILES
+    if lt == HT_ROUND_ROBIN:
+        r = splitmix64((seed ^ 0xDECAF ^ (level << 48) ^ (node << 20) ^ f) & _M64) & 3
+        lt = HT_QUANTILES if r == 3 else (HT_RANDOM if r == 2 else HT_UNIFORM)
+    if lt == HT_QUANTILES:
+        return None
+    occ = np.nonzero(w[:nb] > 0)[0]
+    if not (occ.size and occ[-1] > occ[0]):
+        return None
+    a_lo, a_hi = int(occ[0]), int(occ[-1])
+    if lt != HT_RANDOM and not a_hi - a_lo + 1 > anb:
+        return None
+    e = np.asarray(p.edges[f], dtype=np.float32).astype(np.float64)
+    lo = float(e[a_lo - 1 if a_lo > 0 else 0])
+    hi = float(e[a_hi if a_hi <= nb - 2 else nb - 2])
+    if not hi > lo:
+        return None
+    sc = anb / (hi - lo)
+
+    def cnt(x):
+        return int(min(max(np.floor((x - lo) * sc), 0), anb - 1))
+
+    mark = np.zeros(max(nb, 1), dtype=bool)        # mark[t]: threshold t is kept
+    ee = e[:nb - 1]
+
+    def put(x):
+        i = int(np.searchsorted(ee, x, side="left"))   # first i with edge[i] >= x
+        if i < nb - 1:
+            mark[i + 1] = True
+    if lt == HT_ROBUST:
+        cell = np.array([0 if t == a_lo else cnt(e[t - 1]) for t in range(a_lo, a_hi + 1)])
+        cw = np.zeros(anb)
+        for c in np.unique(cell):
+            ts = np.nonzero(cell == c)[0] + a_lo
+            cw[c] = sw[ts[-1]] - (sw[ts[0] - 1] if ts[0] > 0 else 0.0)
+        K = int((cw > 0).sum())
+        budget = anb - K - 2
+        if K <= 0.2 * anb and budget > 0 and K > 0:
+            nz = [c for c in range(anb) if cw[c] > 0]
+            order = sorted(nz, key=lambda c: (-cw[c], c))
+            left = budget
+            step = (hi - lo) / anb
+            for c in order:
+                q = int(np.ceil(budget * cw[c] / W))
+                nnew = max(0, min(q, left))
+                left -= min(q, left) if left > 0 else 0
+                c0 = lo + step * float(c)
+                sub = step / float(1 + nnew)
+                for j in range(nnew + 1):
+                    put(c0 + sub * float(j))
+            put(lo)
+            put(hi)
+        else:
+            lt = HT_UNIFORM
+    if lt == HT_UNIFORM:
+        c = np.clip(np.floor((e[:nb - 1] - lo) * sc), 0, anb - 1)     # cnt(e[t - 1]), t = 1 .. nb-1
+        return c > np.concatenate([[0.0], c[:-1]])
+    if lt == HT_RANDOM:
+        for k in range(1, anb):
+            h = splitmix64((seed ^ 0xC0FFEE ^ (level << 48) ^ (node << 20) ^ (f << 10) ^ k) & _M64)
+            put(lo + (hi - lo) * (float(h >> 11) * 2.0 ** -53))
+    return mark[1:nb]
+
+
 def split_find_ref(h, nayy, wyy, nbins_f, iscat_f, mono_f, p: SplitParams, level: int, node: int, seed: int):
     """h: float64 [F, 256, 2]. Returns list of per-feature candidate dicts."""
     F = h.shape[0]
@@ -130,19 +204,7 @@ def split_find_ref(h, nayy, wyy, nbins_f, iscat_f, mono_f, p: SplitParams, level
                 lo, hi = int(occ[0]), int(occ[-1])
                 hsh = splitmix64((seed ^ (level << 48) ^ (node << 20) ^ f) & _M64)
                 rand_b = lo + 1 + int(hsh % (hi - lo))
-        allowed = None
-        anb = p.adapt_nb(level)
-        if anb > 1 and not cat and not random_mode:
-            occ = np.nonzero(w[:nb] > 0)[0]
-            if occ.size and occ[-1] > occ[0] and occ[-1] - occ[0] + 1 > anb:
-                a_lo, a_hi = int(occ[0]), int(occ[-1])
-                e = np.asarray(p.edges[f], dtype=np.float32).astype(np.float64)
-                lo = e[a_lo - 1 if a_lo > 0 else 0]
-                hi = e[a_hi if a_hi <= nb - 2 else nb - 2]
-                if hi > lo:
-                    sc = anb / (hi - lo)
-                    c = np.clip(np.floor((e[:nb - 1] - lo) * sc), 0, anb - 1)     # cnt(e[t - 1]), t = 1 .. nb-1
-                    allowed = c > np.concatenate([[0.0], c[:-1]])
+        allowed = _lattice(p, level, node, f, nb, w, sw, W, seed, cat or random_mode)
         best_e, best_code = -1.0e300, -1
         cands = []
         if wNA >= p.min_w and W > 0 and not random_mode:
@@ -448,7 +510,7 @@ class _TreePlan(ctypes.Structure):
                 [(n, _vp * _MAXL) for n in ("nodes", "meta", "tp", "bp", "dec", "cl", "cr", "nl", "cur")] +
                 [("caps", _ci * _MAXL), ("tiles_cap", _ci * _MAXL)] +
                 [(n, _vp) for n in ("aux", "amax_bits", "feat_ok")] +
-                [(n, _ci) for n in ("compute_amax", "k_cols", "packed", "leaf_native", "log_link", "pad1")] +
+                [(n, _ci) for n in ("compute_amax", "k_cols", "packed", "leaf_native", "log_link", "hist_type")] +
                 [("seed", ctypes.c_ulonglong)] + [(n, _cd) for n in ("scale", "kclamp", "mx")] +
                 [("kc_level", _ci * _MAXL), ("pad2", _ci)] +
                 [("edges", _vp), ("nb_level", _ci * _MAXL), ("pad3", _ci)] +
@@ -717,6 +779,7 @@ class GpuTreeBuilder:
         P.edges = self._edges_ptr()
         for d in range(_MAXL):
             P.nb_level[d] = p.adapt_nb(d) if P.edges else 0
+        P.hist_type = int(p.hist_type)
         self._set_plan_ic(P)
         fg = getattr(self, "fgroup", None)
         P.fgroup = 0 if fg is None else fg.data_ptr()

@@ -292,20 +292,81 @@ def test_uniform_adaptive_lattice_restricts_candidates():
     assert int(q.pop_levels()[0].decs[0]["feat"][0]) == f
 
 
+def _skewed_hist(nb=200, anb=20):
+    """One numeric feature with two far outliers: the bulk lies in [0, 10], the range reaches 200, so on a
+    uniform lattice of the node's range all the bulk sits in the first cell."""
+    e = np.concatenate([np.linspace(0, 10, nb - 3), [190.0, 200.0]]).astype(np.float32)
+    tab = np.full((1, 255), np.inf, dtype=np.float32)
+    tab[0, :nb - 1] = e
+    w = np.zeros(256)
+    w[:nb] = 1.0 + (np.arange(nb) % 7)
+    return tab, w, np.cumsum(w)
+
+
+def test_histogram_type_lattices():
+    """UniformRobust switches to guided split points (GuidedSplitPoints) on a sparse uniform lattice and
+    keeps more thresholds where the data is; Random draws its cut points from the seed; RoundRobin mixes
+    UniformAdaptive / Random / QuantilesGlobal over (node, feature)."""
+    nb, anb = 200, 20
+    tab, w, sw = _skewed_hist(nb, anb)
+    W = float(sw[255])
+
+    flat = np.full((1, 255), np.inf, dtype=np.float32)
+    flat[0, :nb - 1] = np.linspace(0, 10, nb - 1)
+
+    def lat(ht, node=0, seed=5, edges=tab):
+        p = T.SplitParams(adapt_nbins=anb, adapt_top=anb, edges=edges, hist_type=ht)
+        return T._lattice(p, 3, node, 0, nb, w, sw, W, seed, False)
+
+    uni, rob = lat(T.HT_UNIFORM), lat(T.HT_ROBUST)
+    assert uni.shape == rob.shape == (nb - 1,)
+    # the uniform cells of width 10 leave the bulk one cell; the guided points refine it
+    assert uni[:120].sum() <= 2 and rob[:120].sum() >= 5
+    assert rob.sum() <= anb + 1
+    r1, r2 = lat(T.HT_RANDOM, seed=1, edges=flat), lat(T.HT_RANDOM, seed=2, edges=flat)
+    assert 10 <= r1.sum() <= anb - 1 and not np.array_equal(r1, r2)
+    uflat = lat(T.HT_UNIFORM, edges=flat)
+    kinds = set()
+    for node in range(40):
+        a = lat(T.HT_ROUND_ROBIN, node=node, edges=flat)
+        kinds.add("q" if a is None else ("u" if np.array_equal(a, uflat) else "r"))
+    assert kinds == {"q", "u", "r"}
+    assert lat(T.HT_QUANTILES) is None
+
+
+@pytest.mark.parametrize("ht", ["UniformRobust", "RoundRobin", "Random", "QuantilesGlobal"])
+def test_gbm_histogram_types_train(ht):
+    X, y, info = _data(N=4000, seed=6)
+    X = X.clone()
+    X[2] = torch.exp(3 * X[2])                       # a skewed feature for UniformRobust's guided points
+    m = GBMTrainer(dict(ntrees=5, max_depth=4, seed=3, histogram_type=ht)).fit(X, y, None, None, info)
+    assert m.output["training_metrics"]["AUC"] > 0.7
+    with pytest.raises(ValueError):
+        GBMTrainer(dict(ntrees=1, histogram_type="Bogus")).fit(X, y, None, None, info)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", ["adaptive", "newton", "random", "mono", "kcols", "featok", "multiclass",
-                                  "interaction"])
+                                  "interaction", "hist_random", "hist_robust", "hist_roundrobin"])
 def test_gpu_tree_modes_match_reference(case):
     """Every split mode of k_split_find / k_split_reduce pinned against RefTreeBuilder (identical
     feature / bin / left weight per decision and identical leaf assignment)."""
     X, y, info = _data(N=20000, cat=True, seed=9)
-    b = fit_binning(X, info.iscat, info.nlevels, max_bins=128)
+    if case.startswith("hist_"):
+        X = X.clone()
+        X[2] = torch.exp(4 * X[2])                   # heavy tail: sparse uniform lattices (UniformRobust)
+        y = y + (X[2] > 2).float()
+    b = fit_binning(X, info.iscat, info.nlevels, max_bins=255 if case.startswith("hist_") else 128)
     bins = apply_binning(b, X)
     g = y - y.mean()
     aux = torch.stack([torch.ones_like(y), g, g, torch.ones_like(y)], 1).contiguous()
     mono, feat_ok, k_cols, depth = None, None, 0, 5
     if case == "adaptive":
         p = T.SplitParams(min_w=10, adapt_nbins=20, adapt_top=128, edges=_edge_tab(b))
+    elif case.startswith("hist_"):
+        ht = {"hist_random": T.HT_RANDOM, "hist_robust": T.HT_ROBUST, "hist_roundrobin": T.HT_ROUND_ROBIN}[case]
+        p = T.SplitParams(min_w=10, adapt_nbins=20, adapt_top=256, edges=_edge_tab(b), hist_type=ht)
+        depth = 6
     elif case == "newton":
         h = torch.full_like(y, 0.25)
         aux = torch.stack([h, -g, -g, h], 1).contiguous()
@@ -344,6 +405,31 @@ def test_gpu_tree_modes_match_reference(case):
     for dr, dg in zip(tl_r.decs, tl_g.decs):
         assert np.array_equal(dr["feat"], dg["feat"])
         assert np.array_equal(dr["bin"], dg["bin"])
+        np.testing.assert_allclose(dr["wl"], dg["wl"], rtol=1e-6)
+    assert torch.equal(ref.leaf_of_row, gb.leaf_of_row.cpu())
+
+
+@pytest.mark.gpu
+def test_gpu_partial_f32_path_matches_reference():
+    """The fp32 block partials (pf32, switched on for 1M-4M-row builders: the per-rank shard of the 4- and
+    8-GPU headline runs) give the same decisions and leaves as the fp64 reference at 1.6M rows."""
+    X, y, info = _data(N=1_600_000, F=8, cat=True, seed=21)
+    b = fit_binning(X, info.iscat, info.nlevels, max_bins=255)
+    bins = apply_binning(b, X)
+    g = y - y.mean()
+    aux = torch.stack([torch.ones_like(y), g, g, torch.ones_like(y)], 1).contiguous()
+    p = T.SplitParams(min_w=10)
+    ref = T.RefTreeBuilder(bins, X.shape[0], b.nbins, b.iscat, None, 6, p)
+    ref.build(aux, leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1]).float())
+    tl_r = ref.pop_levels()[0]
+    dev = torch.device("cuda", 0)
+    gb = T.GpuTreeBuilder(bins.to(dev), X.shape[0], b.nbins, b.iscat, None, 6, p)
+    assert gb.pf32 == 1
+    gb.build(aux.to(dev), leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1]).float())
+    tl_g = gb.pop_levels()[0]
+    assert tl_g.n_leaves == tl_r.n_leaves
+    for dr, dg in zip(tl_r.decs, tl_g.decs):
+        assert np.array_equal(dr["feat"], dg["feat"]) and np.array_equal(dr["bin"], dg["bin"])
         np.testing.assert_allclose(dr["wl"], dg["wl"], rtol=1e-6)
     assert torch.equal(ref.leaf_of_row, gb.leaf_of_row.cpu())
 
