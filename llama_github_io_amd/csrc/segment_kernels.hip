@@ -5,7 +5,8 @@
 // matrix). torch.bincount(weights=fp64) lowers to global fp64 atomics on n addresses: with n = 10
 // every atomic serialises at the memory side (MEASURED r3: 13.8 ms per 1M rows, 91 % of a KMeans job).
 // Here every block privatises the n segment sums in LDS (ds_add_f64), writes its partial row, and a
-// second launch sums the partials of each segment in block order (fixed order across blocks).
+// second launch sums the partials of each segment in block order. Only that cross-block order is fixed: the
+// LDS atomics inside a block land in scheduling order, so the fp64 sums are not bit-reproducible run to run.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 

@@ -171,8 +171,8 @@ def _encode(x: torch.Tensor):
         return None
     fin = ~torch.isnan(x)
     v = x[fin].double()
-    if v.numel() == 0:
-        return None
+    if v.numel() == 0 or bool(((v == 0) & torch.signbit(v)).any()):
+        return None                  # empty, or a -0.0 that integer codes would decode as +0.0
     for k in range(5):
         p = float(10 ** k)
         sv = torch.round(v * p)

@@ -98,3 +98,14 @@ def test_numeric_columns_compress_bit_exactly(tmp_path, monkeypatch):
     c = cols["mid"]
     c.data[0] = 12345.5                                  # a write decodes the column for good
     assert not c.compressed and float(c.values()[0]) == 12345.5
+
+
+def test_column_codec_keeps_negative_zero():
+    """A column holding -0.0 is not integer-compressed (codes would decode it as +0.0)."""
+    import torch
+    from llama_github_io_amd.frame import _encode
+    x = torch.zeros(4096)
+    x[7] = 1.5
+    assert _encode(x) is not None
+    x[5] = -0.0
+    assert _encode(x) is None

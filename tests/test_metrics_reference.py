@@ -170,3 +170,22 @@ def test_naive_bayes_matches_sklearn():
     sk = GaussianNB(var_smoothing=0).fit(X, y).predict_proba(X)[:, 1]
     # H2O uses the unbiased (n-1) variance; sklearn the biased one: agreement to a few 1e-3
     np.testing.assert_allclose(ours, sk, atol=5e-3)
+
+
+def test_lattice_threshold_table_tracks_exact_scores(binom):
+    """The threshold table / max-F1 threshold come from the 2^18-bin score lattice in every process layout
+    (identical single vs sharded). Thresholds are bin maxima, so the criteria sit within one lattice bin of
+    the exact distinct-score optimum (parity with AUC2's 400 merging bins is unpinned: no reference fixture)."""
+    y, p, _ = binom
+    m = mm.binomial_metrics(torch.tensor(y), torch.tensor(p), None, ["0", "1"])
+    order = np.argsort(-p, kind="stable")
+    ps, ys = p[order], y[order]
+    tp, fp = np.cumsum(ys), np.cumsum(1 - ys)
+    last = np.r_[ps[1:] != ps[:-1], True]                   # one point per distinct score
+    f1 = 2 * tp[last] / (tp[last] + fp[last] + ys.sum())
+    best = float(f1.max())
+    row = max(m["thresholds_and_metric_scores"], key=lambda r: r["f1"])
+    assert row["f1"] == pytest.approx(best, abs=2e-3)
+    assert abs(m["max_f1_threshold"] - float(ps[last][f1.argmax()])) < 0.02
+    # every reported threshold is an observed score
+    assert all(np.any(np.isclose(p, r["threshold"], rtol=0, atol=1e-12)) for r in m["thresholds_and_metric_scores"])
