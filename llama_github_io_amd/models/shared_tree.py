@@ -141,6 +141,18 @@ class SharedTreeTrainer:
         """Every row weight of the current tree is exactly 1 (no weights, no row sampling)."""
         return False
 
+    def _max_bins(self) -> int:
+        """Data bins per numeric feature of the global binning (above 255: wide engine columns)."""
+        p = self.p
+        max_bins = int(min(255, max(int(p.get("max_bins") or 255), 2)))
+        ht_ = str(p.get("histogram_type", "AUTO")).lower().replace("_", "")
+        if (self._adaptive_top_level and ht_ in ("auto", "uniformadaptive", "random", "roundrobin", "uniformrobust")
+                and "nbins_top_level" in p):
+            # DHistogram's root resolution: nbins_top_level (default 1024) bins; above 255 the numeric
+            # features are binned wide (several engine columns each, ops/binning.py)
+            max_bins = int(min(WIDE_MAX_BINS, max(int(p.get("nbins_top_level") or 1024), int(p.get("nbins") or 20))))
+        return max_bins
+
     def _binning_sample(self) -> int:
         """Rows of the quantile-edge sample (fit_binning); subclasses needing exact edges raise it."""
         return 1 << 20
@@ -210,13 +222,7 @@ class SharedTreeTrainer:
         self.y = y.float().to(dev)
         self.X = X
         # ---- binning (QuantilesGlobal on the whole training set, shared by every tree)
-        max_bins = int(min(255, max(int(p.get("max_bins") or 255), 2)))
-        ht_ = str(p.get("histogram_type", "AUTO")).lower().replace("_", "")
-        if (self._adaptive_top_level and ht_ in ("auto", "uniformadaptive", "random", "roundrobin", "uniformrobust")
-                and "nbins_top_level" in p):
-            # DHistogram's root resolution: nbins_top_level (default 1024) bins; above 255 the numeric
-            # features are binned wide (several engine columns each, ops/binning.py)
-            max_bins = int(min(WIDE_MAX_BINS, max(int(p.get("nbins_top_level") or 1024), int(p.get("nbins") or 20))))
+        max_bins = self._max_bins()
         bsample = self._binning_sample()
         if coll.is_dist():
             # every rank must bin identically, and exactly like the single-process run: the quantile

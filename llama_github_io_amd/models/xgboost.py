@@ -18,6 +18,7 @@ import torch
 
 from .. import metrics as mm
 from ..ops import tree as T
+from ..ops.binning import WIDE_MAX_BINS
 from .base import Model
 from .datainfo import Expander
 from .shared_tree import SharedTreeModel, SharedTreeTrainer
@@ -139,8 +140,15 @@ class XGBoostTrainer(SharedTreeTrainer):
         # hist / approx / auto: histogram splits on global quantile bins (approx's per-tree sketch is the
         # same cut set up to resampling); exact: every distinct value of every numeric column is a split
         # candidate, i.e. one bin per distinct value of the WHOLE column
-        self.p["max_bins"] = 255 if tm == "exact" else min(int(self.p.get("max_bins", 256)), 255)
+        if tm != "exact":
+            self.p["max_bins"] = min(int(self.p.get("max_bins", 256)), 255)
         return super().fit(X, y, w, offset, info, valid, model_key)
+
+    def _max_bins(self):
+        # exact: one bin per distinct value, up to the wide-column capacity (4 engine columns, 1016 edges)
+        if getattr(self, "tree_method", "auto") == "exact":
+            return WIDE_MAX_BINS
+        return super()._max_bins()
 
     def _binning_sample(self):
         if getattr(self, "tree_method", "auto") == "exact":
@@ -150,18 +158,19 @@ class XGBoostTrainer(SharedTreeTrainer):
     def _check_binning(self, b):
         if getattr(self, "tree_method", "auto") != "exact":
             return
-        # exact greedy splits are the histogram splits when no bin merges two distinct values: at most 254
-        # distinct values per numeric column (bin 255 is NA) on this engine
+        # exact greedy splits are the histogram splits when no bin merges two distinct values: at most 1016
+        # distinct values per numeric column (254 per engine column, wide columns beyond, ops/binning.py)
         Xn = self.X
         for j in range(b.F):
-            if b.iscat[j]:
+            if b.iscat[j] or (j > 0 and b.orig(j) == b.orig(j - 1)):
                 continue
             f = b.orig(j)
             col = Xn[f][~torch.isnan(Xn[f])]
             nd = int(torch.unique(col).numel()) if col.numel() else 0
-            if nd > 254:
+            if nd > WIDE_MAX_BINS:
                 raise ValueError(f"tree_method='exact': column {self.info.x[f]!r} has {nd} distinct values; the "
-                                 "exact split search of this engine handles at most 254 per column (use 'hist')")
+                                 f"exact split search of this engine handles at most {WIDE_MAX_BINS} per column "
+                                 "(use 'hist')")
 
     def _trees_per_iter(self):
         return self.K

@@ -204,3 +204,36 @@ def test_deeplearning_explicit_step_matches_autograd(kind, extra, monkeypatch):
         assert m.output["training_step_explicit"] == (flag == "1")
         res.append(torch.cat([q.detach().reshape(-1) for q in m.net.parameters()]))
     assert torch.allclose(res[0], res[1], atol=1e-5, rtol=1e-4)
+
+
+def test_xgboost_exact_splits_beyond_254_distinct_values():
+    """tree_method='exact' with 700 distinct values (wide engine columns): the root split is the exact greedy
+    split — the same left set as a brute-force search over every distinct threshold."""
+    from llama_github_io_amd.models.xgboost import XGBoostTrainer
+    g = torch.Generator().manual_seed(3)
+    N = 5000
+    x = torch.randint(0, 700, (N,), generator=g).float() / 7.0
+    y = torch.sin(x / 15.0) + 0.3 * torch.randn(N, generator=g)
+    X = x[None].clone()
+    info = DataInfo(["x"], np.zeros(1, np.int32), [None], "y", None)
+    m = XGBoostTrainer(dict(ntrees=1, max_depth=1, learn_rate=1.0, reg_lambda=0.0, min_rows=1, seed=1,
+                            tree_method="exact")).fit(X, y, None, None, info)
+    pred = m._predict_tensor(X).reshape(-1)
+    left = pred == pred[torch.argmin(x)]
+    # brute force: squared error, Newton gain G^2/H with H = count (lambda = 0)
+    xs, order = torch.sort(x.double())
+    r = (y.double() - y.double().mean())[order]
+    cg = torch.cumsum(r, 0)
+    G, n = float(cg[-1]), N
+    best, thr = -1.0, None
+    vals = torch.unique(xs)
+    for v in vals[1:]:
+        k = int(torch.searchsorted(xs, v))          # rows < v
+        gl = float(cg[k - 1])
+        gain = gl * gl / k + (G - gl) ** 2 / (n - k)
+        if gain > best:
+            best, thr = gain, float(v)
+    assert torch.equal(left, x < thr)
+    with pytest.raises(ValueError, match="distinct values"):
+        XGBoostTrainer(dict(ntrees=1, tree_method="exact")).fit(torch.randn(1, 3000), y[:3000].clone(), None, None,
+                                                                info)
