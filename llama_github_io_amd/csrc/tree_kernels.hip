@@ -187,7 +187,7 @@ __device__ __forceinline__ void put_partial(P* q, double d, bool acc) {
 // spread over `srep` copies of its bins (see hist_rows); bin b < nb is the sum of the copies b + c * nb.
 __device__ void flush_partial(const long long* h, const float* nayy, double node_wyy, int ftile, int F,
                               double* __restrict__ part, const double* __restrict__ qs, bool packed, bool acc,
-                              bool f32, const int* srep, const int* snb) {
+                              bool f32, const int* srep, const int* snb, const int* sfine) {
   const int f0 = ftile * FTILE;
   const int nf = min(FTILE, F - f0);
   const double inv_a = qs[2], inv_b = qs[3], inv_p = qs[5];
@@ -195,7 +195,17 @@ __device__ void flush_partial(const long long* h, const float* nayy, double node
     const int bin = i / (2 * nf), rem = i - bin * 2 * nf, fl = rem >> 1, r = rem & 1;
     const int reps = srep[fl], nb = snb[fl];
     long long q = 0;                       // the entry's fixed-point value (plane r), replicas summed
-    if (reps == 1 || bin < nb) {
+    if (sfine[fl]) {
+      // column k of a fine group: bin b holds fine bins t = 4h + l with h + [l > k] == b, i.e. entries
+      // (b, l <= k) and (b - 1, l > k) of the fine histogram (NA: t = 1020 = entry (255, 0))
+      const int m = fl & ~3, k = fl & 3;
+      const int pl = packed ? 0 : r * HPLANE;
+#pragma unroll
+      for (int l = 0; l < 4; ++l) {
+        const int bb = l <= k ? bin : bin - 1;
+        if (bb >= 0) q += h[pl + bb * FTILE + fslot(m + l)];
+      }
+    } else if (reps == 1 || bin < nb) {
       for (int c = 0; c < reps; ++c) {
         const int e = (bin + c * nb) * FTILE + fslot(fl);
         q += packed ? h[e] : h[r * HPLANE + e];
@@ -351,7 +361,8 @@ __device__ __forceinline__ HistSrc make_src(const unsigned* bins32, const float*
 template <bool FILT, bool PACKED, bool UNIT, bool NONA, bool BUF, int GR = RPI, int UNR = H2O_UNR>
 __device__ __forceinline__ void hist_rows(long long* h, float* nayy, const HistSrc& src, int W, int wabs,
                                           int F, bool lead, int r0, int r1, int g, int j, float& wyy, float sa,
-                                          float sb, float sp, const int* lst, const int* srep, const int* snb) {
+                                          float sb, float sp, const int* lst, const int* srep, const int* snb,
+                                          const int* sfine) {
   const int rot = g & 1;
   unsigned offb[4], sh[4];           // byte offset of the lane's feature slot in a bin row; its byte's shift
   unsigned vmask = 0u;
@@ -368,6 +379,13 @@ __device__ __forceinline__ void hist_rows(long long* h, float* nayy, const HistS
     if (wabs < W && wabs * 4 + kk < F) vmask |= 0xFFu << (8 * kk);
   }
   const bool live = vmask != 0u;     // a lane whose word is past the row adds nothing (no dummy atomics)
+  // FINE word: the 4 bytes are the 4 interleaved engine columns of ONE wide numeric feature (ops/binning.py), so
+  // their byte sum is the fine bin t = #{edges <= x} (NA: 4 x 255 = 1020) and one atomic into fine entry
+  // (bin t >> 2, column t & 3) replaces four; the flush rebuilds the four column histograms from the fine one
+  const bool fine = live && sfine[j * 4] != 0;
+  unsigned fsl[4];
+#pragma unroll
+  for (int l = 0; l < 4; ++l) fsl[l] = (unsigned)fslot(j * 4 + l) * 8u;
   const int wc = min(wabs, W - 1);
   const bool weighted = !UNIT && src.aw != nullptr;
   char* Hb = (char*)h;
@@ -426,7 +444,14 @@ __device__ __forceinline__ void hist_rows(long long* h, float* nayy, const HistS
                                 : PACKED ? qpack(ab[u].x, ab[u].y, sp) : q64(ab[u].x, sa);
       const long long qb = PACKED ? 0ll : q64(ab[u].y, sb);
       const unsigned w = wd[u];
-      if (live) {
+      if (fine) {
+        const unsigned t = __builtin_amdgcn_sad_u8(w, 0u, 0u);          // sum of the 4 bytes
+        const unsigned l = t & 3u;
+        const unsigned so = (l & 2u) ? ((l & 1u) ? fsl[3] : fsl[2]) : ((l & 1u) ? fsl[1] : fsl[0]);
+        unsigned long long* p = (unsigned long long*)(Hb + (((t >> 2) << 8) + so));
+        atomicAdd(p, (unsigned long long)qa);
+        if (!PACKED) atomicAdd(p + HPLANE, (unsigned long long)qb);
+      } else if (live) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           unsigned long long* p = ent(w, k);
@@ -470,7 +495,8 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
     const int* __restrict__ meta /*[0]=n_nodes [2]=n_build_tiles*/, int F, double* __restrict__ partials,
     int slot_doubles, const double* __restrict__ qs /*[sa, sb, 1/sa, 1/sb, sp, 1/sp]*/,
     const Dec* __restrict__ pdec, int* __restrict__ nl_out, int f32, long long N, int planar, int lgw,
-    const int* __restrict__ nbins_f /*[F] (NONA: low-cardinality spreading) or null*/) {
+    const int* __restrict__ nbins_f /*[F] (NONA: low-cardinality spreading) or null*/,
+    const int* __restrict__ fine_f /*[F] 1 = column of an aligned 4-column wide numeric group, or null*/) {
   constexpr bool packed = PACKED;
   extern __shared__ __attribute__((aligned(16))) long long smem64[];
   long long* h = smem64;                                 // 2 planes (PACKED: 1 -> two blocks per CU fit)
@@ -499,12 +525,14 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
   const float sa = (float)qs[0], sb = (float)qs[1], sp = (float)qs[4];
   const HistSrc src = make_src(bins32, aw, ay, N, W, lgw);
   // per tile feature: bin count and copies of its bins (NONA: no NA bin, so copies of bins < nb never reach 255)
-  __shared__ int srep[FTILE], snb[FTILE];
+  __shared__ int srep[FTILE], snb[FTILE], sfine[FTILE];
   if (threadIdx.x < FTILE) {
     const int fg = ftile * FTILE + threadIdx.x;
-    const int nb = (NONA && nbins_f && fg < F) ? nbins_f[fg] : 0;
+    const int fi = (fine_f && fg < F) ? fine_f[fg] : 0;
+    const int nb = (NONA && nbins_f && fg < F && !fi) ? nbins_f[fg] : 0;
     srep[threadIdx.x] = (nb > 0 && nb * 4 <= NA_BIN) ? 4 : (nb > 0 && nb * 2 <= NA_BIN) ? 2 : 1;
     snb[threadIdx.x] = nb;
+    sfine[threadIdx.x] = fi;
   }
   __syncthreads();
 
@@ -523,7 +551,7 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
       float wf2 = 0.f;
       wave_sync_lds();
       hist_rows<FILT, PACKED, UNIT, NONA, BUF, 8, 8>(h, nayy, src, W, wabs, Fl, j == 0 && ftile == 0, 0, qn, lane >> 3, j,
-                                                     wf2, sa, sb, sp, wq, srep, snb);
+                                                     wf2, sa, sb, sp, wq, srep, snb, sfine);
       wyy += (double)wf2;
       qn = 0;
       wave_sync_lds();
@@ -536,7 +564,7 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
     __syncthreads();
     const size_t so = (size_t)(blockIdx.x + cur) * slot_doubles;
     flush_partial(h, nayy, v[0], ftile, F, f32 ? (double*)((float*)partials + so) : partials + so, qs, packed, acc,
-                  f32 != 0, srep, snb);
+                  f32 != 0, srep, snb, sfine);
     if (FILT && threadIdx.x == 0 && v[1] != 0.0) atomicAdd(nl_out + cur_parent, (int)v[1]);
     __syncthreads();
   };
@@ -591,7 +619,7 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
       while (qn >= 64) {
         wave_sync_lds();
         hist_rows<FILT, PACKED, UNIT, NONA, BUF, 8, 8>(h, nayy, src, W, wabs, Fl, j == 0 && ftile == 0, 0, 64, lane >> 3, j,
-                                                       wf, sa, sb, sp, wq, srep, snb);
+                                                       wf, sa, sb, sp, wq, srep, snb, sfine);
         const int rest = qn - 64;                        // <= 127: move to the queue front (no lane overlap)
         wave_sync_lds();
         const int v0 = lane < rest ? wq[64 + lane] : 0, v1 = lane + 64 < rest ? wq[128 + lane] : 0;
@@ -601,7 +629,7 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
       }
     } else {
       hist_rows<FILT, PACKED, UNIT, NONA, BUF>(h, nayy, src, W, wabs, Fl, j == 0 && ftile == 0, r0, r1, g, j, wf, sa, sb,
-                                               sp, nullptr, srep, snb);
+                                               sp, nullptr, srep, snb, sfine);
     }
     wyy += (double)wf;
   }
@@ -1858,18 +1886,18 @@ template <bool FILT, bool PACKED, bool UNIT, bool NONA, bool BUF>
 static void launch_hist4(dim3 grid, size_t lds, hipStream_t s, const void* bins, int stride, const void* aw,
                          const void* ay, const void* nodes, const void* tile_prefix, const void* meta, int F,
                          void* partials, int slot_doubles, const void* qs, const void* pdec, void* nl_out, int f32,
-                         long long N, int planar, int lgw, const void* nbins_f) {
+                         long long N, int planar, int lgw, const void* nbins_f, const void* fine_f) {
   hipLaunchKernelGGL((k_hist_build<FILT, PACKED, UNIT, NONA, BUF>), grid, dim3(BLK), lds, s, (const uint8_t*)bins,
                      stride, (const float*)aw, (const float*)ay, (const Node*)nodes, (const int*)tile_prefix,
                      (const int*)meta, F, (double*)partials, slot_doubles, (const double*)qs, (const Dec*)pdec,
-                     (int*)nl_out, f32, N, planar, lgw, (const int*)nbins_f);
+                     (int*)nl_out, f32, N, planar, lgw, (const int*)nbins_f, (const int*)fine_f);
 }
 
 template <bool PACKED, bool UNIT>
 static void launch_hist(dim3 grid, size_t lds, hipStream_t s, const void* bins, int stride, const void* aw,
                         const void* ay, const void* nodes, const void* tile_prefix, const void* meta, int F,
                         void* partials, int slot_doubles, const void* qs, const void* pdec, void* nl_out, int f32,
-                        long long N, int planar, const void* nbins_f) {
+                        long long N, int planar, const void* nbins_f, const void* fine_f) {
   // flags: bit 0 planar bins, bit 1 no NA bin anywhere (NONA kernels)
   const bool nona = (planar >> 1) & 1;
   planar &= 1;
@@ -1882,7 +1910,7 @@ static void launch_hist(dim3 grid, size_t lds, hipStream_t s, const void* bins, 
   const bool buf = lgw >= 0 && bytes < (1ull << 31) && (unsigned long long)N * 4ull < (1ull << 31);
 #define H2O_HIST_CASE(F_, N_, B_) \
   launch_hist4<F_, PACKED, UNIT, N_, B_>(grid, lds, s, bins, stride, aw, ay, nodes, tile_prefix, meta, F, partials, \
-                                          slot_doubles, qs, pdec, nl_out, f32, N, planar, lgw, nbins_f)
+                                          slot_doubles, qs, pdec, nl_out, f32, N, planar, lgw, nbins_f, fine_f)
   const bool filt = pdec != nullptr;
   if (filt) {
     if (nona) { if (buf) H2O_HIST_CASE(true, true, true); else H2O_HIST_CASE(true, true, false); }
@@ -1918,19 +1946,20 @@ int h2o_tree_sizes(int* out) {
 }
 
 // partials: >= (grid + max nodes of the level) slots of slot_doubles. nbins_f (nullable): per-feature bin counts,
-// which let NONA launches spread the updates of low-cardinality features over copies of their bins.
+// which let NONA launches spread the updates of low-cardinality features over copies of their bins. fine_f
+// (nullable): 1 for the columns of word-aligned 4-column wide numeric groups (one fine atomic per row and group).
 int h2o_hist_build(const void* bins, int stride, const void* aw, const void* ay, const void* nodes,
                    const void* tile_prefix, const void* meta, int F, void* partials, int slot_doubles, const void* qs,
                    int grid, int packed, const void* pdec, void* nl_out, int f32, long long N, int planar,
-                   const void* nbins_f, hipStream_t s) {
+                   const void* nbins_f, const void* fine_f, hipStream_t s) {
   const int nft = (F + FTILE - 1) / FTILE;
   // packed mode needs one int64 plane (66 KB): two 16-wave blocks share a CU (32 waves, 8 per SIMD)
   const size_t lds = (packed ? HIST_LDS_BYTES - HPLANE * 8 : HIST_LDS_BYTES) + HIST_LDS_TAIL;
   const dim3 gr(grid, nft);
   if (packed && aw == nullptr)   // unit row weights (the trainer dropped the w plane)
-    launch_hist<true, true>(gr, lds, s, bins, stride, aw, ay, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out, f32, N, planar, nbins_f);
-  else if (packed) launch_hist<true, false>(gr, lds, s, bins, stride, aw, ay, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out, f32, N, planar, nbins_f);
-  else launch_hist<false, false>(gr, lds, s, bins, stride, aw, ay, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out, f32, N, planar, nbins_f);
+    launch_hist<true, true>(gr, lds, s, bins, stride, aw, ay, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out, f32, N, planar, nbins_f, fine_f);
+  else if (packed) launch_hist<true, false>(gr, lds, s, bins, stride, aw, ay, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out, f32, N, planar, nbins_f, fine_f);
+  else launch_hist<false, false>(gr, lds, s, bins, stride, aw, ay, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out, f32, N, planar, nbins_f, fine_f);
   return (int)hipGetLastError();
 }
 
@@ -2205,6 +2234,7 @@ struct TreePlan {
   int cand_fs;                // features per rank of the rank-major candidate all-gather (sliced)
   int dist;                   // row-sharded (h2o_tree_dist): build slots go out in the exchange's layout
   void *hsend, *cand_all, *lsx;  // [W][n][E] packed send slots, [W][cap][Fs] candidates, leaf sums + root weight
+  void* fine_f;               // [F] int32: columns of word-aligned 4-column wide numeric groups (or null)
 };
 
 // op codes / dtypes of the collective transport
@@ -2245,7 +2275,7 @@ int h2o_tree_root(const TreePlan* P, hipStream_t s) {
   const int g0 = P->tiles_cap[0] < P->grid ? P->tiles_cap[0] : P->grid;
   TP_CHECK(h2o_hist_build(P->master, P->stride, P->unit ? nullptr : tp_aux(P, 0), tp_aux(P, 1), P->nodes[0], P->bp[0],
                           P->meta[0], P->F, P->partials, P->slot, P->qs, g0, P->packed, nullptr, nullptr, P->pf32, P->N,
-                          P->planar | (P->no_na << 1), P->nbins_f, s));
+                          P->planar | (P->no_na << 1), P->nbins_f, P->fine_f, s));
   // row-sharded all-reduce: straight into the wire buffer; sliced: hbuild (packed by slice next)
   if (P->dist && !P->sliced)
     return h2o_hist_reduce(P->partials, P->slot, P->used, P->nodes[0], P->bp[0], P->meta[0], 1, g0, P->hrecv, nullptr,
@@ -2316,7 +2346,7 @@ int h2o_tree_grow(const TreePlan* P, int d, int dist, hipStream_t s) {
     tp_level_buf(P, d, sb, sy, sw);
     rc = h2o_hist_build(sb, P->stride, sw, sy, P->nodes[d + 1], P->bp[d + 1], P->meta[d + 1], P->F, P->partials,
                         P->slot, P->qs, gh, P->packed, P->dec[d], P->nl[d], P->pf32, P->N, P->planar | (P->no_na << 1),
-                        P->nbins_f, s);
+                        P->nbins_f, P->fine_f, s);
   } else {
     // regroup level d-1's rows two levels down, then histogram level d+1 (even) contiguously
     rc = tp_route(P, d - 1, s);
@@ -2327,7 +2357,7 @@ int h2o_tree_grow(const TreePlan* P, int d, int dist, hipStream_t s) {
     tp_level_buf(P, d + 1, sb, sy, sw);
     rc = h2o_hist_build(sb, P->stride, sw, sy, P->nodes[d + 1], P->bp[d + 1], P->meta[d + 1], P->F, P->partials,
                         P->slot, P->qs, gh, P->packed, nullptr, nullptr, P->pf32, P->N, P->planar | (P->no_na << 1),
-                        P->nbins_f, s);
+                        P->nbins_f, P->fine_f, s);
   }
   if (rc) return -rc;
   if (!dist)

@@ -39,7 +39,7 @@ _HIP_SIGS = {
     "h2o_tree_all": [c_void_p, c_void_p],
     "h2o_tree_leaves": [c_void_p, c_void_p],
     "h2o_hist_build": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p,
-                       c_int, c_int, c_void_p, c_void_p, c_int, c_ll, c_int, c_void_p, c_void_p],
+                       c_int, c_int, c_void_p, c_void_p, c_int, c_ll, c_int, c_void_p, c_void_p, c_void_p],
     "h2o_split_find": [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_double, c_double,
                        c_double, c_double, c_double, c_int, c_int, c_ull, c_int, c_void_p, c_void_p, c_void_p, c_int,
                        c_int, c_int, c_int, c_void_p],
@@ -72,7 +72,7 @@ _HIP_SIGS = {
 # Bumped whenever a C launcher's argument list changes; every native library exports h2o_abi_version()
 # (csrc/abi.h) and a library built from older sources is refused instead of being called with shifted
 # arguments.
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 
 def _check_abi(lib, name: str) -> None:

@@ -175,7 +175,9 @@ def fit_binning(X: torch.Tensor, iscat, nlevels=None, max_bins: int = MAX_DATA_B
     if any(e is not None and e.size > SUB_EDGES for e in edges) or any(wide_cat):
         # wide numeric features -> n adjacent engine columns with the interleaved edge subsets e[k::n];
         # wide categoricals -> n adjacent engine columns of (at most) 254 consecutive bins each
-        cols = []
+        # the features of exactly 4 interleaved columns go FIRST, so each one fills one aligned 4-byte row word:
+        # the histogram kernel then adds one fine-bin atomic per row and feature (sum of the 4 bytes) instead of 4
+        quad, rest = [], []
         for f in range(F):
             e = edges[f]
             if wide_cat[f]:
@@ -185,12 +187,13 @@ def fit_binning(X: torch.Tensor, iscat, nlevels=None, max_bins: int = MAX_DATA_B
                 for k in range(n):
                     b0, nk = k * SUB_EDGES, min(SUB_EDGES, nb - k * SUB_EDGES)
                     inb = (lb >= b0) & (lb < b0 + nk)
-                    cols.append((f, None, nk + 1, np.where(inb, lb - b0, nk)))
+                    rest.append((f, None, nk + 1, np.where(inb, lb - b0, nk)))
                 continue
             n = 1 if e is None or e.size <= SUB_EDGES else -(-e.size // SUB_EDGES)
             for k in range(n):
                 ek = e if n == 1 else np.ascontiguousarray(e[k::n])
-                cols.append((f, ek, (ek.size + 1) if e is not None else nbins[f], l2b[f]))
+                (quad if n == 4 else rest).append((f, ek, (ek.size + 1) if e is not None else nbins[f], l2b[f]))
+        cols = quad + rest
         vmap = np.asarray([c[0] for c in cols], dtype=np.int32)
         edges = [c[1] for c in cols]
         nbins = np.asarray([c[2] for c in cols], dtype=np.int32)

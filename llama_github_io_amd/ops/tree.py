@@ -45,6 +45,21 @@ HIST_TYPES = {"auto": HT_UNIFORM, "uniformadaptive": HT_UNIFORM, "random": HT_RA
 _M64 = (1 << 64) - 1
 
 
+def fine_columns(fgroup, iscat, F):
+    """int32 [F]: 1 for the columns of the word-aligned (4m .. 4m+3) groups of exactly 4 engine columns of one
+    numeric feature (wide numeric bins, ops/binning.py) — the histogram kernel adds one fine-bin atomic per row and
+    group there — or None when there is no such group."""
+    if fgroup is None:
+        return None
+    g = np.asarray(fgroup, dtype=np.int64)
+    out = np.zeros(F, dtype=np.int32)
+    for m in range(0, F - 3, 4):
+        if (g[m] == g[m + 3] and (m == 0 or g[m - 1] != g[m]) and (m + 4 >= F or g[m + 4] != g[m])
+                and not any(int(iscat[m + l]) for l in range(4))):
+            out[m:m + 4] = 1
+    return out if out.any() else None
+
+
 def splitmix64(x: int) -> int:
     x = (x + 0x9E3779B97F4A7C15) & _M64
     x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & _M64
@@ -518,7 +533,8 @@ class _TreePlan(ctypes.Structure):
                 [(n, _ci) for n in ("sliced", "fs0", "fsn", "sslot")] + [("cand_local", _vp), ("hrecv", _vp)] +
                 [("leaf_lam", _cd), ("leaf_l1", _cd)] + [("planar", _ci), ("no_na", _ci)] +
                 [("fgroup", _vp)] + [("coll_fn", _vp), ("coll_ctx", _vp)] +
-                [(n, _ci) for n in ("W", "cf32", "cand_fs", "dist")] + [(n, _vp) for n in ("hsend", "cand_all", "lsx")])
+                [(n, _ci) for n in ("W", "cf32", "cand_fs", "dist")] + [(n, _vp) for n in ("hsend", "cand_all", "lsx")] +
+                [("fine_f", _vp)])
 
 
 class _Arena:
@@ -604,6 +620,8 @@ class GpuTreeBuilder:
         self.leaf_of_row = torch.empty(N, dtype=torch.int32, device=dev)
         self.nbins_f = torch.as_tensor(np.asarray(nbins_f, dtype=np.int32), device=dev)
         self.iscat_f = torch.as_tensor(np.asarray(iscat_f, dtype=np.int32), device=dev)
+        self.iscat_np = np.asarray(iscat_f, dtype=np.int32)
+        self.fine_f = None
         self.mono_f = None if mono_f is None else torch.as_tensor(np.asarray(mono_f, dtype=np.int32), device=dev)
         self.feat_ok_all = torch.ones(F, dtype=torch.int32, device=dev)
         self.qs = torch.zeros(16, dtype=torch.float64, device=dev)  # fixed-point scales (k_qscale)
@@ -742,8 +760,13 @@ class GpuTreeBuilder:
         """Engine column -> original feature (k_split_reduce column sampling by original feature)."""
         self.fgroup = None if fgroup is None else torch.as_tensor(np.asarray(fgroup, dtype=np.int32),
                                                                   device=self.dev).contiguous()
+        self.fine_f = fine_columns(fgroup, self.iscat_np, self.F)
+        if self.fine_f is not None:
+            self.fine_f = torch.as_tensor(self.fine_f, device=self.dev).contiguous()
         if getattr(self, "_plan", None) is not None:
             self._plan.fgroup = 0 if self.fgroup is None else self.fgroup.data_ptr()
+            self._plan.fine_f = (0 if self.fine_f is None or os.environ.get("H2O_HIST_FINE") == "0"
+                                 else self.fine_f.data_ptr())
 
     def _set_plan_ic(self, P):
         if self.ic_map is None:
@@ -783,6 +806,7 @@ class GpuTreeBuilder:
         self._set_plan_ic(P)
         fg = getattr(self, "fgroup", None)
         P.fgroup = 0 if fg is None else fg.data_ptr()
+        P.fine_f = 0 if self.fine_f is None or os.environ.get("H2O_HIST_FINE") == "0" else self.fine_f.data_ptr()
         P.sliced, P.fs0, P.fsn, P.sslot = int(self.sliced), self.fs0, self.fsn, self.sslot
         P.planar = int(self.planar)
         P.no_na = int(self._no_na())

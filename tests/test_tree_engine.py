@@ -481,7 +481,14 @@ def test_wide_binning_columns_are_interleaved_edge_subsets():
     X[1] = torch.randint(0, 40, (20000,), generator=g).float()        # few distinct values: one column
     X[2, :100] = float("nan")
     b = fit_binning(X, np.zeros(3, np.int32), None, max_bins=1016)
-    assert b.F_orig == 3 and list(b.vmap) == [0, 0, 0, 0, 1, 2, 2, 2, 2]
+    # 4-column features first (each fills one aligned row word), then the rest
+    assert b.F_orig == 3 and list(b.vmap) == [0, 0, 0, 0, 2, 2, 2, 2, 1]
+    assert list(T.fine_columns(b.vmap, b.iscat, b.F)) == [1] * 8 + [0]
+    # the fine bin is the byte sum of the 4 columns (NA: 4 x 255)
+    fsum = apply_binning(b, X).long()[:, 4:8].sum(1)
+    e2 = np.sort(np.concatenate([b.edges[j] for j in range(4, 8)]))
+    ref2 = torch.bucketize(torch.nan_to_num(X[2], nan=0.0), torch.from_numpy(e2), right=True)
+    assert torch.equal(fsum, torch.where(torch.isnan(X[2]), torch.full_like(ref2, 4 * T.NA_BIN), ref2))
     fine0 = fit_binning(X[:1], np.zeros(1, np.int32), None, max_bins=1016)
     bins = apply_binning(b, X).long()
     for j in range(b.F):
@@ -526,7 +533,7 @@ def test_wide_bins_split_resolution_and_grouped_sampling():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["plain", "kcols_adaptive"])
+@pytest.mark.parametrize("case", ["plain", "kcols_adaptive", "newton"])
 def test_gpu_wide_bins_match_reference(case):
     """1016-bin numeric features (4 engine columns each) on the GPU engine vs RefTreeBuilder: identical
     decisions, left weights and leaf assignment, including grouped column sampling (k_split_reduce fgroup)."""
@@ -543,6 +550,11 @@ def test_gpu_wide_bins_match_reference(case):
     if case == "kcols_adaptive":
         k_cols = 3
         p = T.SplitParams(min_w=10, adapt_nbins=20, adapt_top=1024, edges=_edge_tab(b))
+    elif case == "newton":           # unpacked two-plane histograms through the fine-bin atomics
+        h = torch.full_like(y, 0.25)
+        aux = torch.stack([h, -g, -g, h], 1).contiguous()
+        p = T.SplitParams(min_w=1.0, lam=1.0, mode=T.MODE_NEWTON)
+    assert T.fine_columns(b.vmap, b.iscat, b.F).sum() == 20     # 5 numeric features of 4 aligned columns
     ref = T.RefTreeBuilder(bins, b.F, b.nbins, b.iscat, None, 5, p)
     ref.set_feature_groups(b.vmap)
     ref.build(aux, None, k_cols, seed=5, leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1]).float())
