@@ -26,6 +26,10 @@
 //
 // MFMA 16x16x32 bf16 operand maps (gfx950): lane l holds A[row l&15][k = 8(l>>4)+j], B[k = 8(l>>4)+j][col
 // l&15] (j = 0..7) and D[row 4(l>>4)+r][col l&15] (r = 0..3).
+// fp32 (compute_dtype="float32", the H2O default): the same kernels on v_mfma_f32_16x16x4_f32 with fp32
+// activations in LDS, the fp32 master weights read in place and fp32 transposed buffers. A lane loads 4
+// consecutive k (one float4) of its A row and B column and issues 4 MFMAs, MFMA j taking element j: every
+// MFMA pairs A[i][4q + j] with B[4q + j][n] for lane quarter q, so the 4 cover 16 k.
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
 #include <stdint.h>
@@ -44,10 +48,10 @@ typedef __hip_bfloat16 bf16;
 #define WG_KU 4          // 32-row chunks of loads in flight per wave
 
 struct DLArgs {
-  const bf16* Z; long long ldz; const long long* ridx; int B; int Bpad;
+  const void* Z; long long ldz; const long long* ridx; int B; int Bpad;
   const float* w; const long long* ycls; const float* yreg;
-  const float* P; const bf16* W; const bf16* WT; const unsigned long long* step_dev;
-  bf16* hT; bf16* dT; float* bpart; float* g; float* gsum;
+  const float* P; const void* W; void* WT; const unsigned long long* step_dev;
+  void* hT; void* dT; float* bpart; float* g; float* gsum;
   int L, K, act, regression;
   int n[DL_MAXL + 1];           // n[0] inputs, n[l] units of layer l, n[L] = outputs
   int kp[DL_MAXL + 1];          // n padded to 32 (GEMM K extent when the activation is an operand)
@@ -60,6 +64,7 @@ struct DLArgs {
   int lds_g[2], lds_w;          // two gradient tiles, row weights
   int tiles_i[DL_MAXL], tiles_j[DL_MAXL], tile_start[DL_MAXL + 1];   // k_dl_wgrad block decode
   long long n_decay, n_total;
+  int f32, pad_;                // 1: fp32 operands (Z, W, WT, hT, dT, LDS tiles), 0: bf16
 };
 
 __device__ __forceinline__ uint32_t hash32(uint64_t x) {
@@ -120,6 +125,53 @@ __device__ __forceinline__ f32x4 tile_mm(const bf16* A, int lda, const bf16* Bg,
   return acc;
 }
 
+// fp32 operands: 4 consecutive k of one row (zero tail past kvalid)
+__device__ __forceinline__ float4 load4(const float* row, int k, int kvalid, bool vec) {
+  if (vec && k + 4 <= kvalid) return *reinterpret_cast<const float4*>(row + k);
+  float4 v;
+  v.x = k < kvalid ? row[k] : 0.f;
+  v.y = k + 1 < kvalid ? row[k + 1] : 0.f;
+  v.z = k + 2 < kvalid ? row[k + 2] : 0.f;
+  v.w = k + 3 < kvalid ? row[k + 3] : 0.f;
+  return v;
+}
+
+#define KU4 8
+__device__ __forceinline__ f32x4 tile_mm(const float* A, int lda, const float* Bg, long long ldb, int n0, int nvalid,
+                                         int K, int kvalid, bool vec) {
+  const int lane = threadIdx.x & 63, q = lane >> 4, c = lane & 15;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  const int n = n0 + c;
+  const bool nok = n < nvalid;
+  const float* brow = Bg + (long long)(nok ? n : 0) * ldb;
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int kb = 0; kb < K; kb += 16 * KU4) {
+    float4 b[KU4];
+#pragma unroll
+    for (int u = 0; u < KU4; ++u) {
+      const int k = kb + 16 * u + 4 * q;
+      b[u] = (nok && kb + 16 * u < K) ? load4(brow, k, kvalid, vec) : z4;
+    }
+#pragma unroll
+    for (int u = 0; u < KU4; ++u) {
+      if (kb + 16 * u < K) {
+        const float4 a = *reinterpret_cast<const float4*>(A + c * lda + kb + 16 * u + 4 * q);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b[u].x, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b[u].y, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b[u].z, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b[u].w, acc, 0, 0, 0);
+      }
+    }
+  }
+  return acc;
+}
+
+__device__ __forceinline__ float to_f(bf16 v) { return __bfloat162float(v); }
+__device__ __forceinline__ float to_f(float v) { return v; }
+template <typename T> __device__ __forceinline__ T from_f(float v);
+template <> __device__ __forceinline__ bf16 from_f<bf16>(float v) { return __float2bfloat16(v); }
+template <> __device__ __forceinline__ float from_f<float>(float v) { return v; }
+
 // column sums of the 16 x 16 D tile (rows 4q + r): in-lane over r, then across the 4 lane quarters
 __device__ __forceinline__ float col_sum(f32x4 v) {
   float s = (v[0] + v[1]) + (v[2] + v[3]);
@@ -134,10 +186,20 @@ __device__ __forceinline__ void store4T(bf16* dst, f32x4 v) {   // 4 consecutive
   pk.h[2] = __float2bfloat16(v[2]); pk.h[3] = __float2bfloat16(v[3]);
   *reinterpret_cast<uint2*>(dst) = pk.u;
 }
+__device__ __forceinline__ void store4T(float* dst, f32x4 v) {  // fp32: 16 bytes
+  *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+}
 
+template <typename T>
 __global__ __launch_bounds__(DL_THREADS) void k_dl_rows(DLArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  bf16* S = reinterpret_cast<bf16*>(smem);
+  T* S = reinterpret_cast<T*>(smem);
+  const T* Zg = reinterpret_cast<const T*>(a.Z);
+  const T* Wg = reinterpret_cast<const T*>(a.W);
+  const T* WTg = reinterpret_cast<const T*>(a.WT);
+  T* hTg = reinterpret_cast<T*>(a.hT);
+  T* dTg = reinterpret_cast<T*>(a.dT);
+  constexpr int VE = 16 / sizeof(T);     // elements per 16-byte vector
   float* ws = reinterpret_cast<float*>(smem + a.lds_w);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, q = lane >> 4, c = lane & 15;
   const int r0 = blockIdx.x * DL_ROWS;
@@ -162,44 +224,44 @@ __global__ __launch_bounds__(DL_THREADS) void k_dl_rows(DLArgs a) {
   __syncthreads();
   // ---- gather the 16 input rows into activation tile 0
   {
-    bf16* A0 = S + a.lds_off[0];
+    T* A0 = S + a.lds_off[0];
     const int n0 = a.n[0], ld0 = a.ld[0];
-    const bool vec = (n0 % 8 == 0) && (a.ldz % 8 == 0);
-    const int chunks = (n0 + 7) / 8;
+    const bool vec = (n0 % VE == 0) && (a.ldz % VE == 0);
+    const int chunks = (n0 + VE - 1) / VE;
     for (int i = tid; i < DL_ROWS * chunks; i += DL_THREADS) {
-      const int rr = i / chunks, k = (i - rr * chunks) * 8;
+      const int rr = i / chunks, k = (i - rr * chunks) * VE;
       const long long g = srow[rr];
       if (g < 0) continue;
-      const bf16* src = a.Z + g * a.ldz;
-      bf16* dst = A0 + rr * ld0 + k;
+      const T* src = Zg + g * a.ldz;
+      T* dst = A0 + rr * ld0 + k;
       if (vec) *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src + k);
-      else for (int j = 0; j < 8 && k + j < n0; ++j) dst[j] = src[k + j];
+      else for (int j = 0; j < VE && k + j < n0; ++j) dst[j] = src[k + j];
     }
   }
   __syncthreads();
   // x transposed for the first weight gradient: hT_0[k][r0 + 4 g .. + 3]
   {
-    const bf16* A0 = S + a.lds_off[0];
-    bf16* dst = a.hT + a.h_off[0];
+    const T* A0 = S + a.lds_off[0];
+    T* dst = hTg + a.h_off[0];
     for (int i = tid; i < a.n[0] * 4; i += DL_THREADS) {
       const int k = i >> 2, g4 = (i & 3) * 4;
-      f32x4 v = {__bfloat162float(A0[(g4 + 0) * a.ld[0] + k]), __bfloat162float(A0[(g4 + 1) * a.ld[0] + k]),
-                 __bfloat162float(A0[(g4 + 2) * a.ld[0] + k]), __bfloat162float(A0[(g4 + 3) * a.ld[0] + k])};
+      f32x4 v = {to_f(A0[(g4 + 0) * a.ld[0] + k]), to_f(A0[(g4 + 1) * a.ld[0] + k]),
+                 to_f(A0[(g4 + 2) * a.ld[0] + k]), to_f(A0[(g4 + 3) * a.ld[0] + k])};
       store4T(dst + (long long)k * a.Bpad + r0 + g4, v);
     }
   }
   // ---- forward: hidden layers
   for (int l = 1; l < L; ++l) {
-    const bf16* Ain = S + a.lds_off[l - 1];
-    bf16* Aout = S + a.lds_off[l];
+    const T* Ain = S + a.lds_off[l - 1];
+    T* Aout = S + a.lds_off[l];
     const int nin = a.n[l - 1], nout = a.n[l];
-    const bool vec = (nin % 8 == 0) && (a.w_off[l - 1] % 8 == 0);
+    const bool vec = (nin % VE == 0) && (a.w_off[l - 1] % VE == 0);
     const float drop = a.drop[l - 1], keep = 1.f - drop;
     const uint32_t thr = (uint32_t)(drop * 4294967296.0);
     const uint64_t seed = a.seed_base[l - 1] ^ (step * 0x9E3779B97F4A7C15ULL);
-    const int T = (nout + 15) / 16;
-    for (int t = wv; t < T; t += DL_NW) {
-      const f32x4 acc = tile_mm(Ain, a.ld[l - 1], a.W + a.w_off[l - 1], nin, t * 16, nout, a.kp[l - 1], nin, vec);
+    const int NT = (nout + 15) / 16;
+    for (int t = wv; t < NT; t += DL_NW) {
+      const f32x4 acc = tile_mm(Ain, a.ld[l - 1], Wg + a.w_off[l - 1], nin, t * 16, nout, a.kp[l - 1], nin, vec);
       const int col = t * 16 + c;
       f32x4 o;
       if (col < nout) {
@@ -209,19 +271,19 @@ __global__ __launch_bounds__(DL_THREADS) void k_dl_rows(DLArgs a) {
           float v = act_f(a.act, acc[r] + b);
           if (drop > 0.f) v = dropped(seed, (int64_t)(r0 + 4 * q + r) * nout + col, thr) ? 0.f : v / keep;
           o[r] = v;
-          Aout[(4 * q + r) * a.ld[l] + col] = __float2bfloat16(v);
+          Aout[(4 * q + r) * a.ld[l] + col] = from_f<T>(v);
         }
-        store4T(a.hT + a.h_off[l] + (long long)col * a.Bpad + r0 + 4 * q, o);
+        store4T(hTg + a.h_off[l] + (long long)col * a.Bpad + r0 + 4 * q, o);
       }
     }
     __syncthreads();
   }
   // ---- output layer + loss gradient (wave 0; K <= 16)
-  bf16* GO = S + a.lds_off[L];
+  T* GO = S + a.lds_off[L];
   if (wv == 0) {
     const int nin = a.n[L - 1], K = a.K;
-    const bool vec = (nin % 8 == 0) && (a.w_off[L - 1] % 8 == 0);
-    const f32x4 acc = tile_mm(S + a.lds_off[L - 1], a.ld[L - 1], a.W + a.w_off[L - 1], nin, 0, K, a.kp[L - 1], nin, vec);
+    const bool vec = (nin % VE == 0) && (a.w_off[L - 1] % VE == 0);
+    const f32x4 acc = tile_mm(S + a.lds_off[L - 1], a.ld[L - 1], Wg + a.w_off[L - 1], nin, 0, K, a.kp[L - 1], nin, vec);
     const bool cok = c < K;
     const float b = cok ? a.P[a.b_off[L - 1] + c] : 0.f;
     f32x4 g;
@@ -240,35 +302,35 @@ __global__ __launch_bounds__(DL_THREADS) void k_dl_rows(DLArgs a) {
         for (int m = 1; m < 16; m <<= 1) z += __shfl_xor(z, m, 64);
         g[r] = cok ? (e / z - (scls[row] == c ? 1.f : 0.f)) * wr : 0.f;
       }
-      GO[row * a.ld[L] + c] = __float2bfloat16(g[r]);
+      GO[row * a.ld[L] + c] = from_f<T>(g[r]);
     }
     const float cs = col_sum(g);
     if (q == 0 && cok) a.bpart[(long long)blockIdx.x * (a.bias_total + 1) + a.bias_off[L] + c] = cs;
-    if (cok) store4T(a.dT + a.d_off[L] + (long long)c * a.Bpad + r0 + 4 * q, g);
+    if (cok) store4T(dTg + a.d_off[L] + (long long)c * a.Bpad + r0 + 4 * q, g);
   }
   __syncthreads();
   // ---- backward through the hidden layers
-  const bf16* Gin = GO;
+  const T* Gin = GO;
   int ldg_in = a.ld[L];
   for (int l = L - 1; l >= 1; --l) {
-    bf16* Gout = S + a.lds_g[l & 1];
+    T* Gout = S + a.lds_g[l & 1];
     const int nout = a.n[l], nnext = a.n[l + 1];
-    const bool vec = (nnext % 8 == 0) && (a.w_off[l] % 8 == 0);
+    const bool vec = (nnext % VE == 0) && (a.w_off[l] % VE == 0);
     const float drop = a.drop[l - 1], keep = 1.f - drop;
     const uint32_t thr = (uint32_t)(drop * 4294967296.0);
     const uint64_t seed = a.seed_base[l - 1] ^ (step * 0x9E3779B97F4A7C15ULL);
-    const bf16* H = S + a.lds_off[l];
-    const int T = (nout + 15) / 16;
-    for (int t = wv; t < T; t += DL_NW) {
+    const T* H = S + a.lds_off[l];
+    const int NT = (nout + 15) / 16;
+    for (int t = wv; t < NT; t += DL_NW) {
       // dh = G_{l+1} W_{l+1}: B[k = unit of l+1][n = unit of l] = WT_{l+1}[n][k]
-      const f32x4 acc = tile_mm(Gin, ldg_in, a.WT + a.w_off[l], nnext, t * 16, nout, a.kp[l + 1], nnext, vec);
+      const f32x4 acc = tile_mm(Gin, ldg_in, WTg + a.w_off[l], nnext, t * 16, nout, a.kp[l + 1], nnext, vec);
       const int col = t * 16 + c;
       f32x4 gd = {0.f, 0.f, 0.f, 0.f};
       if (col < nout) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int row = 4 * q + r;
-          float y = __bfloat162float(H[row * a.ld[l] + col]);
+          float y = to_f(H[row * a.ld[l] + col]);
           float gg = acc[r];
           if (drop > 0.f) {
             const bool d = dropped(seed, (int64_t)(r0 + row) * nout + col, thr);
@@ -279,18 +341,18 @@ __global__ __launch_bounds__(DL_THREADS) void k_dl_rows(DLArgs a) {
         }
       }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) Gout[(4 * q + r) * a.ld[l] + col] = __float2bfloat16(gd[r]);
+      for (int r = 0; r < 4; ++r) Gout[(4 * q + r) * a.ld[l] + col] = from_f<T>(gd[r]);
       const float cs = col_sum(gd);
       if (col < nout) {
         if (q == 0) a.bpart[(long long)blockIdx.x * (a.bias_total + 1) + a.bias_off[l] + col] = cs;
-        store4T(a.dT + a.d_off[l] + (long long)col * a.Bpad + r0 + 4 * q, gd);
+        store4T(dTg + a.d_off[l] + (long long)col * a.Bpad + r0 + 4 * q, gd);
       }
     }
     __syncthreads();
     // zero the K padding of the gradient tile the next layer reads
-    for (int i = tid; i < DL_ROWS * (a.kp[l] - T * 16); i += DL_THREADS) {
-      const int rr = i / (a.kp[l] - T * 16), cc = T * 16 + i % (a.kp[l] - T * 16);
-      Gout[rr * a.ld[l] + cc] = __float2bfloat16(0.f);
+    for (int i = tid; i < DL_ROWS * (a.kp[l] - NT * 16); i += DL_THREADS) {
+      const int rr = i / (a.kp[l] - NT * 16), cc = NT * 16 + i % (a.kp[l] - NT * 16);
+      Gout[rr * a.ld[l] + cc] = from_f<T>(0.f);
     }
     __syncthreads();
     Gin = Gout;
@@ -307,6 +369,66 @@ __global__ __launch_bounds__(DL_THREADS) void k_dl_rows(DLArgs a) {
 // Workgroup = one 32 x 32 tile of one layer (2 x 2 MFMA tiles per wave); wave w accumulates row chunks
 // w, w + 8, w + 16, ... (32 rows each); partial tiles meet in LDS and wave 0 sums them in wave order.
 // Workgroups past the weight tiles reduce bias gradients from the k_dl_rows partials (wave = bias).
+// MFMA accumulation of one wave's row chunks of a 32 x 32 weight-gradient tile (A rows arow[u] = dT of units i,
+// B rows brow[v] = hT of units j, both along the batch rows = GEMM K).
+// bf16: 32-row chunks (8 rows per lane, one 16x16x32 MFMA); fp32: 16-row chunks (4 rows per lane, 4 MFMAs).
+__device__ __forceinline__ void wgrad_acc(const bf16* const (&arow)[2], const bf16* const (&brow)[2], const bool (&aok)[2],
+                                          const bool (&bok)[2], int nrows, int wv, f32x4 (&acc)[2][2]) {
+  const int nch = nrows / 32;
+  const bf16x8 z8 = {(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
+  for (int cb = wv; cb < nch; cb += WG_WAVES * WG_KU) {
+    bf16x8 av[WG_KU][2], bv[WG_KU][2];
+#pragma unroll
+    for (int k = 0; k < WG_KU; ++k) {
+      const int ch = cb + k * WG_WAVES;
+      const bool in = ch < nch;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        av[k][u] = (in && aok[u]) ? *reinterpret_cast<const bf16x8*>(arow[u] + ch * 32) : z8;
+        bv[k][u] = (in && bok[u]) ? *reinterpret_cast<const bf16x8*>(brow[u] + ch * 32) : z8;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < WG_KU; ++k)
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+          acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[k][u], bv[k][v], acc[u][v], 0, 0, 0);
+  }
+}
+__device__ __forceinline__ void wgrad_acc(const float* const (&arow)[2], const float* const (&brow)[2],
+                                          const bool (&aok)[2], const bool (&bok)[2], int nrows, int wv,
+                                          f32x4 (&acc)[2][2]) {
+  const int nch = nrows / 16;
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int cb = wv; cb < nch; cb += WG_WAVES * WG_KU) {
+    float4 av[WG_KU][2], bv[WG_KU][2];
+#pragma unroll
+    for (int k = 0; k < WG_KU; ++k) {
+      const int ch = cb + k * WG_WAVES;
+      const bool in = ch < nch;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        av[k][u] = (in && aok[u]) ? *reinterpret_cast<const float4*>(arow[u] + ch * 16) : z4;
+        bv[k][u] = (in && bok[u]) ? *reinterpret_cast<const float4*>(brow[u] + ch * 16) : z4;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < WG_KU; ++k)
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int v = 0; v < 2; ++v) {
+          acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[k][u].x, bv[k][v].x, acc[u][v], 0, 0, 0);
+          acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[k][u].y, bv[k][v].y, acc[u][v], 0, 0, 0);
+          acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[k][u].z, bv[k][v].z, acc[u][v], 0, 0, 0);
+          acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[k][u].w, bv[k][v].w, acc[u][v], 0, 0, 0);
+        }
+  }
+}
+
+template <typename T>
 __global__ __launch_bounds__(WG_WAVES * 64) void k_dl_wgrad(DLArgs a, int G1, int scale_by_w) {
   __shared__ float red[WG_WAVES - 1][16][64];
   __shared__ float s_sw;
@@ -343,45 +465,25 @@ __global__ __launch_bounds__(WG_WAVES * 64) void k_dl_wgrad(DLArgs a, int G1, in
   const int ti = bt / a.tiles_j[l], tj = bt - ti * a.tiles_j[l];
   const int ni = a.n[l + 1], nj = a.n[l];
   const int i0 = ti * 32, j0 = tj * 32;
-  const bf16* Ab = a.dT + a.d_off[l + 1];
-  const bf16* Bb = a.hT + a.h_off[l];
-  const int nch = a.Bpad / 32;
+  const T* Ab = reinterpret_cast<const T*>(a.dT) + a.d_off[l + 1];
+  const T* Bb = reinterpret_cast<const T*>(a.hT) + a.h_off[l];
   f32x4 acc[2][2];
 #pragma unroll
   for (int u = 0; u < 2; ++u)
 #pragma unroll
     for (int v = 0; v < 2; ++v) acc[u][v] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  const bf16x8 z8 = {(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
-  const bf16* arow[2];
-  const bf16* brow[2];
+  constexpr int LPQ = 16 / sizeof(T);     // batch rows per lane quarter and chunk step
+  const T* arow[2];
+  const T* brow[2];
   bool aok[2], bok[2];
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int i = i0 + u * 16 + c, j = j0 + u * 16 + c;
     aok[u] = i < ni; bok[u] = j < nj;
-    arow[u] = Ab + (long long)(aok[u] ? i : 0) * a.Bpad + 8 * q;
-    brow[u] = Bb + (long long)(bok[u] ? j : 0) * a.Bpad + 8 * q;
+    arow[u] = Ab + (long long)(aok[u] ? i : 0) * a.Bpad + LPQ * q;
+    brow[u] = Bb + (long long)(bok[u] ? j : 0) * a.Bpad + LPQ * q;
   }
-  for (int cb = wv; cb < nch; cb += WG_WAVES * WG_KU) {
-    bf16x8 av[WG_KU][2], bv[WG_KU][2];
-#pragma unroll
-    for (int k = 0; k < WG_KU; ++k) {
-      const int ch = cb + k * WG_WAVES;
-      const bool in = ch < nch;
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        av[k][u] = (in && aok[u]) ? *reinterpret_cast<const bf16x8*>(arow[u] + ch * 32) : z8;
-        bv[k][u] = (in && bok[u]) ? *reinterpret_cast<const bf16x8*>(brow[u] + ch * 32) : z8;
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < WG_KU; ++k)
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int v = 0; v < 2; ++v)
-          acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[k][u], bv[k][v], acc[u][v], 0, 0, 0);
-  }
+  wgrad_acc(arow, brow, aok, bok, a.Bpad, wv, acc);
   if (wv > 0) {
 #pragma unroll
     for (int u = 0; u < 2; ++u)
@@ -409,13 +511,16 @@ __global__ __launch_bounds__(WG_WAVES * 64) void k_dl_wgrad(DLArgs a, int G1, in
 }
 
 // WT_l[j][i] = W_l[i][j] for every layer (the bf16 shadow the backward pass reads)
+template <typename T>
 __global__ __launch_bounds__(256) void k_dl_transpose(DLArgs a) {
+  const T* W = reinterpret_cast<const T*>(a.W);
+  T* WT = reinterpret_cast<T*>(a.WT);
   for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < a.n_decay; e += (long long)gridDim.x * blockDim.x) {
     int l = 0;
     while (l + 1 < a.L && e >= a.w_off[l + 1]) ++l;
     const long long o = e - a.w_off[l];
     const int nin = a.n[l], i = (int)(o / nin), j = (int)(o - (long long)i * nin);
-    const_cast<bf16*>(a.WT)[a.w_off[l] + (long long)j * a.n[l + 1] + i] = a.W[e];
+    WT[a.w_off[l] + (long long)j * a.n[l + 1] + i] = W[e];
   }
 }
 
@@ -430,17 +535,23 @@ int h2o_dl_step(const DLArgs* a, int lds, int scale_by_w, hipStream_t s) {
   if (a->L < 1 || a->L > DL_MAXL || a->K > 16 || a->Bpad % 128 != 0 || lds > 160 * 1024)
     return (int)hipErrorInvalidValue;
   const int G1 = a->Bpad / DL_ROWS;
-  hipLaunchKernelGGL(k_dl_rows, dim3(G1), dim3(DL_THREADS), lds, s, *a);
   const int bias_blocks = (a->bias_total + WG_WAVES - 1) / WG_WAVES;
-  hipLaunchKernelGGL(k_dl_wgrad, dim3(a->tile_start[a->L] + bias_blocks), dim3(WG_WAVES * 64), 0, s, *a, G1,
-                     scale_by_w);
+  const dim3 gw(a->tile_start[a->L] + bias_blocks);
+  if (a->f32) {
+    hipLaunchKernelGGL(k_dl_rows<float>, dim3(G1), dim3(DL_THREADS), lds, s, *a);
+    hipLaunchKernelGGL(k_dl_wgrad<float>, gw, dim3(WG_WAVES * 64), 0, s, *a, G1, scale_by_w);
+  } else {
+    hipLaunchKernelGGL(k_dl_rows<bf16>, dim3(G1), dim3(DL_THREADS), lds, s, *a);
+    hipLaunchKernelGGL(k_dl_wgrad<bf16>, gw, dim3(WG_WAVES * 64), 0, s, *a, G1, scale_by_w);
+  }
   return (int)hipGetLastError();
 }
 
 int h2o_dl_transpose(const DLArgs* a, hipStream_t s) {
   long long grid = (a->n_decay + 255) / 256;
   if (grid > 2048) grid = 2048;
-  hipLaunchKernelGGL(k_dl_transpose, dim3((unsigned)grid), dim3(256), 0, s, *a);
+  if (a->f32) hipLaunchKernelGGL(k_dl_transpose<float>, dim3((unsigned)grid), dim3(256), 0, s, *a);
+  else hipLaunchKernelGGL(k_dl_transpose<bf16>, dim3((unsigned)grid), dim3(256), 0, s, *a);
   return (int)hipGetLastError();
 }
 

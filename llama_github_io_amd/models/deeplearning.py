@@ -441,8 +441,7 @@ class DeepLearningTrainer:
         if explicit and p.get("reproducible"):
             # reproducible=True (bit-identical seeded runs): the library-GEMM explicit step accumulates bias
             # gradients with float atomics; only the fused step (fixed-order reductions) or autograd qualify
-            bf16 = dtype is not None and dev.type == "cuda"
-            if not (bf16 and os.environ.get("H2O_DL_FUSED", "1") == "1" and dlops.supported(
+            if not (dev.type == "cuda" and os.environ.get("H2O_DL_FUSED", "1") == "1" and dlops.supported(
                     int(Z.shape[1]), [int(h_) for h_ in hidden], int(net.out.weight.shape[0]), ACT[net.act], Z)):
                 explicit = False
         shadow = None
@@ -496,10 +495,12 @@ class DeepLearningTrainer:
                         gbuf[-1:].copy_(wb.sum().view(1))
 
         # Fused MFMA step (ops/dl.py, csrc/dl_kernels.hip): gather + forward + loss gradient + backward on
-        # 16-row tiles with the activations in LDS, all weight gradients in one launch, fixed-order reduce.
+        # 16-row tiles with the activations in LDS, all weight gradients in one launch, fixed-order reduce;
+        # bf16 (v_mfma_f32_16x16x32_bf16) or the default fp32 compute (v_mfma_f32_16x16x4_f32).
         # Built per batch capacity in alloc(); the library-GEMM explicit step above stays for other shapes.
         fz = dict(obj=None, ok=False, sridx=None)
-        if (explicit and cdt == torch.bfloat16 and os.environ.get("H2O_DL_FUSED", "1") == "1"
+        if (explicit and os.environ.get("H2O_DL_FUSED", "1") == "1"
+                and (cdt == torch.bfloat16 or os.environ.get("H2O_DL_FUSED_F32", "1") == "1")
                 and dlops.supported(int(Z.shape[1]), [int(h_) for h_ in hidden], int(net.out.weight.shape[0]),
                                     act_code, Z)):
             fz["ok"] = True

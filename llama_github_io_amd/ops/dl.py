@@ -4,8 +4,8 @@ Reference: ``hex/deeplearning/Neurons.java`` fprop / bprop (``DeepLearningTask.m
 ``k_dl_rows`` (gather + every layer forward + loss gradient + every layer backward on 16-row tiles, activations
 in LDS) -> ``k_dl_wgrad`` (all weight gradients, split over the batch rows inside a workgroup and summed in a
 fixed order, plus the bias gradients from the row tiles' partials) straight into the flat gradient buffer;
-the optimizer (fused ADADELTA) then refreshes the bf16 weight shadow and
-:meth:`FusedMLPStep.refresh_transposed` the transposed shadow of the backward pass.
+the optimizer (fused ADADELTA) then refreshes the bf16 weight shadow (bf16 operands; fp32 operands read the
+master weights in place) and :meth:`FusedMLPStep.refresh_transposed` the transposed copy of the backward pass.
 """
 from __future__ import annotations
 
@@ -34,7 +34,7 @@ class _DLArgs(ctypes.Structure):
                  ("drop", _cf * MAXL), ("seed_base", _cull * MAXL),
                  ("lds_off", _ci * (MAXL + 1)), ("lds_g", _ci * 2), ("lds_w", _ci),
                  ("tiles_i", _ci * MAXL), ("tiles_j", _ci * MAXL), ("tile_start", _ci * (MAXL + 1)),
-                 ("n_decay", _cll), ("n_total", _cll)])
+                 ("n_decay", _cll), ("n_total", _cll), ("f32", _ci), ("pad_", _ci)])
 
 
 nat.register_hip_signatures({"h2o_dl_args_size": [], "h2o_dl_step": [_vp, _ci, _ci, _vp],
@@ -45,13 +45,22 @@ def _r32(n: int) -> int:
     return (n + 31) // 32 * 32
 
 
+def _pad(esz: int) -> int:
+    """LDS row padding (elements) of the activation tiles: 16 bytes (spreads rows over the banks)."""
+    return 16 // esz
+
+
 def supported(n_in: int, hidden, n_out: int, act_code: int, Z: torch.Tensor) -> bool:
-    """Shapes the fused step handles (else the library-GEMM explicit step runs)."""
+    """Shapes the fused step handles (else the library-GEMM explicit step runs): bf16 or fp32 operands."""
     L = len(hidden) + 1
-    if not Z.is_cuda or Z.dtype != torch.bfloat16 or L > MAXL or n_out > 16 or act_code not in (0, 1, 2, 3):
+    if not Z.is_cuda or Z.dtype not in (torch.bfloat16, torch.float32) or L > MAXL or n_out > 16 or \
+            act_code not in (0, 1, 2, 3):
         return False
+    esz = Z.element_size()
+    pd = _pad(esz)
     widths = [n_in] + list(hidden)
-    lds = sum(ROWS * (_r32(n) + 8) * 2 for n in widths) + ROWS * 40 * 2 + 2 * ROWS * (_r32(max(hidden or [1])) + 8) * 2 + 64
+    lds = (sum(ROWS * (_r32(n) + pd) * esz for n in widths) + ROWS * (32 + pd) * esz
+           + 2 * ROWS * (_r32(max(hidden or [1])) + pd) * esz + 64)
     return lds <= 150 * 1024 and max(widths) <= 8192
 
 
@@ -59,7 +68,8 @@ class FusedMLPStep:
     """Static launch arguments of the fused step for one network / mini-batch capacity.
 
     ``lins``: the hidden Linear layers then the output layer (weights ``[out, in]`` views of the flat
-    fp32 buffer ``fp.p``); ``shadow``: bf16 copy of ``fp.p[:n_decay]`` kept by the optimizer."""
+    fp32 buffer ``fp.p``); ``shadow``: bf16 copy of ``fp.p[:n_decay]`` kept by the optimizer, or None: fp32
+    operands (``Z`` fp32, the master weights read in place, fp32 transposed copies and LDS tiles)."""
 
     def __init__(self, fp, lins, act_code: int, drops, seed_bases, Z: torch.Tensor, w: torch.Tensor, y: torch.Tensor,
                  regression: bool, cap: int, shadow: torch.Tensor, step_dev: torch.Tensor, out_grad: torch.Tensor,
@@ -79,13 +89,19 @@ class FusedMLPStep:
             a.yreg, a.ycls, a.regression = y.data_ptr(), 0, 1
         else:
             a.ycls, a.yreg, a.regression = y.data_ptr(), 0, 0
-        self.WT = torch.empty_like(shadow)
-        a.P, a.W, a.WT, a.step_dev = base, shadow.data_ptr(), self.WT.data_ptr(), step_dev.data_ptr()
+        f32 = shadow is None
+        assert Z.dtype == (torch.float32 if f32 else torch.bfloat16)
+        cdt = torch.float32 if f32 else torch.bfloat16
+        cesz = 4 if f32 else 2
+        wsrc = fp.p[: fp.n_decay] if f32 else shadow
+        self.WT = torch.empty_like(wsrc)
+        a.P, a.W, a.WT, a.step_dev = base, wsrc.data_ptr(), self.WT.data_ptr(), step_dev.data_ptr()
+        a.f32 = int(f32)
         a.L, a.K, a.act = L, n[L], int(act_code)
         for i, v in enumerate(n):
             a.n[i] = v
             a.kp[i] = _r32(v)
-            a.ld[i] = _r32(v) + 8
+            a.ld[i] = _r32(v) + _pad(cesz)
         bias_off, bt = [0] * (MAXL + 1), 0
         for l in range(1, L + 1):
             bias_off[l] = bt
@@ -100,7 +116,7 @@ class FusedMLPStep:
         for i in range(L - 1):
             a.drop[i] = float(drops[i])
             a.seed_base[i] = int(seed_bases[i]) & ((1 << 64) - 1)
-        # transposed activations / gradients: [units][Bpad] bf16 per layer (offsets multiples of 8 elements)
+        # transposed activations / gradients: [units][Bpad] per layer (offsets multiples of 8 elements)
         ho, o = [], 0
         for l in range(L):
             ho.append(o)
@@ -109,7 +125,7 @@ class FusedMLPStep:
         for l in range(1, L + 1):
             do.append(o)
             o += n[l] * Bpad
-        self.T = torch.zeros(o, dtype=torch.bfloat16, device=dev)
+        self.T = torch.zeros(o, dtype=cdt, device=dev)
         for l in range(L):
             a.h_off[l] = ho[l]
         for l in range(1, L + 1):
@@ -130,7 +146,7 @@ class FusedMLPStep:
         gl = max([a.ld[l] for l in range(1, L)] or [8])
         a.lds_g[0], a.lds_g[1] = off, off + ROWS * gl
         off += 2 * ROWS * gl
-        a.lds_w = off * 2
+        a.lds_w = off * cesz
         self.lds = a.lds_w + ROWS * 4
         ts = 0
         for l in range(L):
@@ -142,7 +158,7 @@ class FusedMLPStep:
         a.n_decay, a.n_total = fp.n_decay, fp.p.numel()
         self.args = a
         self.scale_by_w = out_gsum is None
-        self._keep = (Z, w, y, shadow, step_dev, out_grad, out_gsum)
+        self._keep = (Z, w, y, wsrc, step_dev, out_grad, out_gsum)
 
     def step(self, ridx: torch.Tensor) -> None:
         """One forward/backward of the rows ``ridx`` (int64; -1 = padding row) into the gradient buffer."""

@@ -70,18 +70,19 @@ def bench_dl(a, dev, world, rank):
     y = (X[:20].sum(0) > 10).float()
     info = DataInfo([f"p{i}" for i in range(F)], np.zeros(F, np.int32), [None] * F, "y", ["0", "1"])
     # untimed warmup fit on a slice: library init / kernel autotuning / graph capture code paths
-    DeepLearningTrainer(dict(hidden=[200, 200], epochs=1, compute_dtype="bf16", mini_batch_size=a.batch, seed=1,
+    cd = a.dtype
+    DeepLearningTrainer(dict(hidden=[200, 200], epochs=1, compute_dtype=cd, mini_batch_size=a.batch, seed=1,
                              stopping_rounds=0, score_interval=1e9, standardize=False)).fit(
         X[:, :8 * a.batch].contiguous(), y[:8 * a.batch].contiguous(), None, None, info)
     _sync()
     t0 = time.perf_counter()
-    m = DeepLearningTrainer(dict(hidden=[200, 200], epochs=a.epochs, compute_dtype="bf16", mini_batch_size=a.batch,
+    m = DeepLearningTrainer(dict(hidden=[200, 200], epochs=a.epochs, compute_dtype=cd, mini_batch_size=a.batch,
                                  seed=1, stopping_rounds=0, score_interval=1e9, standardize=False)).fit(X, y, None, None, info)
     _sync()
     dt = time.perf_counter() - t0
-    _emit(dict(metric="DeepLearning MLP [200,200] train samples/sec (10M x 784, bf16, data-parallel)",
+    _emit(dict(metric=f"DeepLearning MLP [200,200] train samples/sec (10M x 784, {cd}, data-parallel)",
                value=N * a.epochs / dt, unit="samples/s", n_gpus=world, seconds=dt, rows=N, cols=F, batch=a.batch,
-               train_auc=m.output["training_metrics"]["AUC"], dtype="bf16", data="synthetic",
+               train_auc=m.output["training_metrics"]["AUC"], dtype=cd, data="synthetic",
                step_mode=m.output.get("training_step_mode"), explicit=m.output.get("training_step_explicit"),
                fused_mfma=m.output.get("training_step_fused_mfma"),
                phases=m.output.get("phase_seconds")))
@@ -211,6 +212,7 @@ def main():
     ap.add_argument("--trees", type=int, default=0)
     ap.add_argument("--epochs", type=float, default=1.0)
     ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--dtype", default="bf16", help="DeepLearning compute_dtype (bf16 | float32)")
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -408,9 +408,10 @@ def test_segment_sum_kernel_matches_index_add(n, idt, vdt):
     assert got.dtype == torch.float64 and torch.allclose(got, ref, rtol=1e-12, atol=1e-9)
 
 
-def _fused_case(n_in, hidden, K, act, drops, regression, B, seed=0):
+def _fused_case(n_in, hidden, K, act, drops, regression, B, seed=0, f32=False):
     """One fused MFMA step (csrc/dl_kernels.hip) and the fp32 autograd gradient of the same weighted loss
-    (weights and inputs rounded to bf16 like the kernels' operands; dropout masks from ops.dense._mask_ref)."""
+    (bf16 path: weights and inputs rounded to bf16 like the kernels' operands; f32: the fp32 master weights and
+    inputs, v_mfma_f32_16x16x4_f32; dropout masks from ops.dense._mask_ref)."""
     from llama_github_io_amd.models.deeplearning import MLP
     from llama_github_io_amd.ops import dl as dlops
     from llama_github_io_amd.ops.dense import FlatParams, _act, _mask_ref, step_seed
@@ -421,11 +422,12 @@ def _fused_case(n_in, hidden, K, act, drops, regression, B, seed=0):
     with torch.no_grad():
         fp.p.add_(0.05 * torch.randn(fp.p.shape, generator=g).to(dev))   # non-trivial biases
     N = 3 * B
-    Z = torch.randn(N, n_in, generator=g).to(dev).to(torch.bfloat16)
+    Z = torch.randn(N, n_in, generator=g).to(dev).to(torch.float32 if f32 else torch.bfloat16)
     w = (torch.rand(N, generator=g) + 0.5).to(dev)
     y = torch.randn(N, generator=g).to(dev) if regression else torch.randint(0, K, (N,), generator=g).to(dev)
     ridx = torch.randperm(N, generator=g)[:B].to(dev)
-    shadow = fp.p[: fp.n_decay].to(torch.bfloat16)
+    shadow = None if f32 else fp.p[: fp.n_decay].to(torch.bfloat16)
+    wsrc = fp.p[: fp.n_decay] if f32 else shadow
     step_t = torch.full((1,), 7, dtype=torch.int64, device=dev)
     bases = [1234567 + 31 * i for i in range(len(hidden))]
     fs = dlops.FusedMLPStep(fp, list(net.hidden) + [net.out], act, drops, bases, Z, w, y, regression, B, shadow,
@@ -436,7 +438,7 @@ def _fused_case(n_in, hidden, K, act, drops, regression, B, seed=0):
     torch.cuda.synchronize()
     got = fp.g.clone()
     # fp32 autograd reference on the bf16-rounded operands
-    Ws = [shadow[(l_.weight.data_ptr() - fp.p.data_ptr()) // 4:][: l_.weight.numel()].float().view_as(l_.weight)
+    Ws = [wsrc[(l_.weight.data_ptr() - fp.p.data_ptr()) // 4:][: l_.weight.numel()].float().view_as(l_.weight)
           .clone().requires_grad_(True) for l_ in list(net.hidden) + [net.out]]
     Bs = [l_.bias.detach().clone().requires_grad_(True) for l_ in list(net.hidden) + [net.out]]
     h = Z[ridx].float()
@@ -462,7 +464,7 @@ def _fused_case(n_in, hidden, K, act, drops, regression, B, seed=0):
     for i, l_ in enumerate(list(net.hidden) + [net.out]):
         ow = (l_.weight.data_ptr() - fp.p.data_ptr()) // 4
         n_o, n_i = l_.weight.shape
-        assert torch.equal(fs.WT[ow: ow + n_o * n_i].view(n_i, n_o), shadow[ow: ow + n_o * n_i].view(n_o, n_i).T)
+        assert torch.equal(fs.WT[ow: ow + n_o * n_i].view(n_i, n_o), wsrc[ow: ow + n_o * n_i].view(n_o, n_i).T)
     return got, ref
 
 
@@ -479,6 +481,20 @@ def test_dl_fused_step_matches_fp32_autograd(n_in, hidden, K, act, drops, regres
     assert float(torch.nn.functional.cosine_similarity(got, ref, dim=0)) > 0.999
 
 
+@pytest.mark.parametrize("n_in,hidden,K,act,drops,regression,B", [
+    (784, [200, 200], 2, 1, [0.0, 0.0], False, 512),          # the BASELINE MLP shape, default fp32 compute
+    (37, [48, 24], 3, 2, [0.0, 0.0], False, 200),            # ragged widths: scalar loads, padding rows
+    (50, [64], 5, 1, [0.3], False, 256),
+    (20, [40, 16, 8], 1, 2, [0.1, 0.0, 0.2], True, 128),
+])
+def test_dl_fused_fp32_step_matches_fp32_autograd(n_in, hidden, K, act, drops, regression, B):
+    """fp32 operands (compute_dtype='float32', the H2O default) on v_mfma_f32_16x16x4_f32: exact fp32 products,
+    so only the summation order separates the kernels from autograd."""
+    got, ref = _fused_case(n_in, hidden, K, act, drops, regression, B, f32=True)
+    rel = float((got - ref).norm() / ref.norm())
+    assert rel < 1e-4, rel
+
+
 def test_dl_trainer_uses_fused_step_and_learns(monkeypatch):
     """The trainer's graph-chunked loop runs the fused MFMA step (no library GEMM in the loop) and reaches
     the accuracy of the library-GEMM explicit step on the same data."""
@@ -486,16 +502,17 @@ def test_dl_trainer_uses_fused_step_and_learns(monkeypatch):
     g = torch.Generator(device=dev).manual_seed(1)
     X = torch.rand(100, 60000, device=dev, generator=g)
     y = (X[:10].sum(0) > 5).float()
-    res = {}
-    for flag in ("1", "0"):
-        monkeypatch.setenv("H2O_DL_FUSED", flag)
-        m = DeepLearningTrainer(dict(hidden=[64, 64], epochs=2, compute_dtype="bf16", mini_batch_size=1024, seed=3,
-                                     stopping_rounds=0, score_interval=1e9, standardize=False)).fit(X, y, None, None,
-                                                                                                   _info(100))
-        res[flag] = m
-    assert res["1"].output["training_step_fused_mfma"] and not res["0"].output["training_step_fused_mfma"]
-    a1, a0 = res["1"].output["training_metrics"]["AUC"], res["0"].output["training_metrics"]["AUC"]
-    assert a1 > 0.9 and abs(a1 - a0) < 0.02, (a1, a0)
+    for cd in ("bf16", "float32"):
+        res = {}
+        for flag in ("1", "0"):
+            monkeypatch.setenv("H2O_DL_FUSED", flag)
+            m = DeepLearningTrainer(dict(hidden=[64, 64], epochs=2, compute_dtype=cd, mini_batch_size=1024, seed=3,
+                                         stopping_rounds=0, score_interval=1e9, standardize=False)).fit(
+                X, y, None, None, _info(100))
+            res[flag] = m
+        assert res["1"].output["training_step_fused_mfma"] and not res["0"].output["training_step_fused_mfma"]
+        a1, a0 = res["1"].output["training_metrics"]["AUC"], res["0"].output["training_metrics"]["AUC"]
+        assert a1 > 0.9 and abs(a1 - a0) < 0.02, (cd, a1, a0)
 
 
 @pytest.mark.parametrize("obj,extra", [("bernoulli", dict(reg_lambda=2.0, reg_alpha=0.5, max_delta_step=0.3)),
