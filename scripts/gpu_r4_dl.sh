@@ -11,4 +11,6 @@ timeout -k 10 300 python scripts/bench_suite.py --which dl --rows 2000000 --dtyp
 timeout -k 10 300 python scripts/bench_suite.py --which dl --rows 2000000 --dtype float32 > $O/bench_f32.json 2> $O/bench_f32.err || exit $?
 timeout -k 10 300 python scripts/bench_suite.py --which dl --rows 1250000 --dtype bf16 > $O/bench_bf16_shard.json 2> $O/bench_bf16_shard.err || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_f32 -o run -- python scripts/bench_suite.py --which dl --rows 1000000 --dtype float32 > $O/prof_f32.log 2>&1 || exit $?
+python3 scripts/rocpd_stats.py $O/prof_f32/run_results.db --top 30 --md > $O/kernel_stats_f32.md || exit 1
+rm -rf $O/prof_f32
 cat $O/bench_bf16.json $O/bench_f32.json $O/bench_bf16_shard.json
