@@ -65,6 +65,8 @@ struct DLArgs {
   int tiles_i[DL_MAXL], tiles_j[DL_MAXL], tile_start[DL_MAXL + 1];   // k_dl_wgrad block decode
   long long n_decay, n_total;
   int f32, pad_;                // 1: fp32 operands (Z, W, WT, hT, dT, LDS tiles), 0: bf16
+  float in_drop; int lds_lg;    // input dropout ratio; K > 16: byte offset of the fp32 [16][K] logit tile
+  unsigned long long in_seed;   // input dropout seed base
 };
 
 __device__ __forceinline__ uint32_t hash32(uint64_t x) {
@@ -239,6 +241,20 @@ __global__ __launch_bounds__(DL_THREADS) void k_dl_rows(DLArgs a) {
     }
   }
   __syncthreads();
+  // input dropout (input_dropout_ratio): hash mask over (batch row, input), survivors scaled by 1 / keep
+  if (a.in_drop > 0.f) {
+    T* A0 = S + a.lds_off[0];
+    const int n0 = a.n[0], ld0 = a.ld[0];
+    const float keep = 1.f - a.in_drop;
+    const uint32_t thr = (uint32_t)(a.in_drop * 4294967296.0);
+    const uint64_t seed = a.in_seed ^ (step * 0x9E3779B97F4A7C15ULL);
+    for (int i = tid; i < DL_ROWS * n0; i += DL_THREADS) {
+      const int rr = i / n0, k = i - rr * n0;
+      T* e = A0 + rr * ld0 + k;
+      *e = dropped(seed, (int64_t)(r0 + rr) * n0 + k, thr) ? from_f<T>(0.f) : from_f<T>(to_f(*e) / keep);
+    }
+    __syncthreads();
+  }
   // x transposed for the first weight gradient: hT_0[k][r0 + 4 g .. + 3]
   {
     const T* A0 = S + a.lds_off[0];
@@ -278,9 +294,52 @@ __global__ __launch_bounds__(DL_THREADS) void k_dl_rows(DLArgs a) {
     }
     __syncthreads();
   }
-  // ---- output layer + loss gradient (wave 0; K <= 16)
+  // ---- output layer + loss gradient (wave 0 when K <= 16; K > 16: logit tiles over the waves, then one wave
+  // per row for the softmax, then one thread per class for the bias partials and the transposed gradient)
   T* GO = S + a.lds_off[L];
-  if (wv == 0) {
+  if (a.K > 16) {
+    float* LG = reinterpret_cast<float*>(smem + a.lds_lg);
+    const int nin = a.n[L - 1], K = a.K;
+    const bool vec = (nin % VE == 0) && (a.w_off[L - 1] % VE == 0);
+    for (int t = wv; t < (K + 15) / 16; t += DL_NW) {
+      const f32x4 acc = tile_mm(S + a.lds_off[L - 1], a.ld[L - 1], Wg + a.w_off[L - 1], nin, t * 16, K, a.kp[L - 1],
+                                nin, vec);
+      const int col = t * 16 + c;
+      if (col < K) {
+        const float b = a.P[a.b_off[L - 1] + col];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) LG[(4 * q + r) * K + col] = acc[r] + b;
+      }
+    }
+    __syncthreads();
+    if (wv < DL_ROWS) {
+      const int row = wv;
+      float* lg = LG + row * K;
+      float mx = -INFINITY;
+      for (int k = lane; k < K; k += 64) mx = fmaxf(mx, lg[k]);
+      for (int m = 32; m > 0; m >>= 1) mx = fmaxf(mx, __shfl_xor(mx, m, 64));
+      float z = 0.f;
+      for (int k = lane; k < K; k += 64) z += __expf(lg[k] - mx);
+      for (int m = 32; m > 0; m >>= 1) z += __shfl_xor(z, m, 64);
+      const float wr = ws[row];
+      const long long cls = scls[row];
+      for (int k = lane; k < K; k += 64) {
+        const float gk = (__expf(lg[k] - mx) / z - (cls == k ? 1.f : 0.f)) * wr;
+        lg[k] = gk;
+        GO[row * a.ld[L] + k] = from_f<T>(gk);
+      }
+    }
+    __syncthreads();
+    for (int k = tid; k < K; k += DL_THREADS) {
+      float cs = 0.f;
+      for (int g4 = 0; g4 < DL_ROWS; g4 += 4) {
+        const f32x4 v = {LG[(g4 + 0) * K + k], LG[(g4 + 1) * K + k], LG[(g4 + 2) * K + k], LG[(g4 + 3) * K + k]};
+        cs += (v[0] + v[1]) + (v[2] + v[3]);
+        store4T(dTg + a.d_off[L] + (long long)k * a.Bpad + r0 + g4, v);
+      }
+      a.bpart[(long long)blockIdx.x * (a.bias_total + 1) + a.bias_off[L] + k] = cs;
+    }
+  } else if (wv == 0) {
     const int nin = a.n[L - 1], K = a.K;
     const bool vec = (nin % VE == 0) && (a.w_off[L - 1] % VE == 0);
     const f32x4 acc = tile_mm(S + a.lds_off[L - 1], a.ld[L - 1], Wg + a.w_off[L - 1], nin, 0, K, a.kp[L - 1], nin, vec);
@@ -532,7 +591,8 @@ int h2o_dl_args_size() { return (int)sizeof(DLArgs); }
 
 // lds: bytes of dynamic LDS for k_dl_rows (activation + gradient tiles + row weights)
 int h2o_dl_step(const DLArgs* a, int lds, int scale_by_w, hipStream_t s) {
-  if (a->L < 1 || a->L > DL_MAXL || a->K > 16 || a->Bpad % 128 != 0 || lds > 160 * 1024)
+  if (a->L < 1 || a->L > DL_MAXL || (a->K > 16 && (a->regression || a->lds_lg <= 0)) || a->Bpad % 128 != 0 ||
+      lds > 160 * 1024)
     return (int)hipErrorInvalidValue;
   const int G1 = a->Bpad / DL_ROWS;
   const int bias_blocks = (a->bias_total + WG_WAVES - 1) / WG_WAVES;

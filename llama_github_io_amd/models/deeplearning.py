@@ -432,12 +432,18 @@ class DeepLearningTrainer:
         # output-gradient pass; weight gradients land in the flat buffer, bias gradients are accumulated by
         # the epilogue kernels straight into it (~20 launches per step instead of ~45).
         lname = str(p["loss"]).lower()
+        from ..ops import dl as dlops
+        in_drop = float(p["input_dropout_ratio"])
+        # input dropout runs in the fused step only (the library-GEMM explicit step has no input mask)
+        fused_shape = (dev.type == "cuda" and os.environ.get("H2O_DL_FUSED", "1") == "1" and net.act in ACT
+                       and (Z.dtype == torch.bfloat16 or os.environ.get("H2O_DL_FUSED_F32", "1") == "1")
+                       and dlops.supported(int(Z.shape[1]), [int(h_) for h_ in hidden], int(net.out.weight.shape[0]),
+                                           ACT[net.act], Z))
         explicit = (os.environ.get("H2O_DL_EXPLICIT", "1") == "1" and not ae and not maxout
-                    and float(p["input_dropout_ratio"]) == 0 and net.act in ACT
+                    and (in_drop == 0 or fused_shape) and net.act in ACT
                     and ((cat in ("Binomial", "Multinomial") and dist in ("bernoulli", "multinomial")
                           and lname in ("automatic", "crossentropy", "cross_entropy"))
                          or (cat == "Regression" and dist == "gaussian" and lname in ("automatic", "quadratic"))))
-        from ..ops import dl as dlops
         if explicit and p.get("reproducible"):
             # reproducible=True (bit-identical seeded runs): the library-GEMM explicit step accumulates bias
             # gradients with float atomics; only the fused step (fixed-order reductions) or autograd qualify
@@ -511,7 +517,7 @@ class DeepLearningTrainer:
             gsum = gbuf[-1:] if gsync else None
             fz["obj"] = dlops.FusedMLPStep(fp, list(net.hidden) + [net.out], act_code, list(net.hid_drop),
                                            fz["bases"], Z, wf, yt, cat == "Regression", cap, shadow, step_t, gout,
-                                           gsum)
+                                           gsum, in_drop, (dseed * 1000003 + 104729) & ((1 << 62) - 1))
             fz["obj"].refresh_transposed()
             fz["sridx"] = torch.full((cap,), -1, dtype=torch.long, device=dev)
 

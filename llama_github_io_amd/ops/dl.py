@@ -17,6 +17,7 @@ from . import _native as nat
 
 MAXL = 6
 ROWS = 16
+MAXK = 256          # output classes of the fused step (K > 16: fp32 [16][K] logit tile in LDS)
 _vp, _ci, _cll, _cf, _cull = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong, ctypes.c_float, ctypes.c_ulonglong
 
 
@@ -34,7 +35,8 @@ class _DLArgs(ctypes.Structure):
                  ("drop", _cf * MAXL), ("seed_base", _cull * MAXL),
                  ("lds_off", _ci * (MAXL + 1)), ("lds_g", _ci * 2), ("lds_w", _ci),
                  ("tiles_i", _ci * MAXL), ("tiles_j", _ci * MAXL), ("tile_start", _ci * (MAXL + 1)),
-                 ("n_decay", _cll), ("n_total", _cll), ("f32", _ci), ("pad_", _ci)])
+                 ("n_decay", _cll), ("n_total", _cll), ("f32", _ci), ("pad_", _ci),
+                 ("in_drop", _cf), ("lds_lg", _ci), ("in_seed", _cull)])
 
 
 nat.register_hip_signatures({"h2o_dl_args_size": [], "h2o_dl_step": [_vp, _ci, _ci, _vp],
@@ -53,14 +55,14 @@ def _pad(esz: int) -> int:
 def supported(n_in: int, hidden, n_out: int, act_code: int, Z: torch.Tensor) -> bool:
     """Shapes the fused step handles (else the library-GEMM explicit step runs): bf16 or fp32 operands."""
     L = len(hidden) + 1
-    if not Z.is_cuda or Z.dtype not in (torch.bfloat16, torch.float32) or L > MAXL or n_out > 16 or \
+    if not Z.is_cuda or Z.dtype not in (torch.bfloat16, torch.float32) or L > MAXL or n_out > MAXK or \
             act_code not in (0, 1, 2, 3):
         return False
     esz = Z.element_size()
     pd = _pad(esz)
     widths = [n_in] + list(hidden)
-    lds = (sum(ROWS * (_r32(n) + pd) * esz for n in widths) + ROWS * (32 + pd) * esz
-           + 2 * ROWS * (_r32(max(hidden or [1])) + pd) * esz + 64)
+    lds = (sum(ROWS * (_r32(n) + pd) * esz for n in widths) + ROWS * (_r32(n_out) + pd) * esz
+           + 2 * ROWS * (_r32(max(hidden or [1])) + pd) * esz + 64 + (ROWS * n_out * 4 if n_out > 16 else 0))
     return lds <= 150 * 1024 and max(widths) <= 8192
 
 
@@ -73,7 +75,7 @@ class FusedMLPStep:
 
     def __init__(self, fp, lins, act_code: int, drops, seed_bases, Z: torch.Tensor, w: torch.Tensor, y: torch.Tensor,
                  regression: bool, cap: int, shadow: torch.Tensor, step_dev: torch.Tensor, out_grad: torch.Tensor,
-                 out_gsum: torch.Tensor | None):
+                 out_gsum: torch.Tensor | None, in_drop: float = 0.0, in_seed: int = 0):
         self.lib = nat.hip()
         assert self.lib.h2o_dl_args_size() == ctypes.sizeof(_DLArgs), "DLArgs layout mismatch"
         dev = Z.device
@@ -148,6 +150,12 @@ class FusedMLPStep:
         off += 2 * ROWS * gl
         a.lds_w = off * cesz
         self.lds = a.lds_w + ROWS * 4
+        if n[L] > 16:                  # fp32 [16][K] logits of the wide softmax (16-byte aligned)
+            assert not regression and n[L] <= MAXK
+            a.lds_lg = (self.lds + 15) // 16 * 16
+            self.lds = a.lds_lg + ROWS * n[L] * 4
+        a.in_drop = float(in_drop)
+        a.in_seed = int(in_seed) & ((1 << 64) - 1)
         ts = 0
         for l in range(L):
             a.tiles_i[l] = (n[l + 1] + 31) // 32

@@ -408,7 +408,7 @@ def test_segment_sum_kernel_matches_index_add(n, idt, vdt):
     assert got.dtype == torch.float64 and torch.allclose(got, ref, rtol=1e-12, atol=1e-9)
 
 
-def _fused_case(n_in, hidden, K, act, drops, regression, B, seed=0, f32=False):
+def _fused_case(n_in, hidden, K, act, drops, regression, B, seed=0, f32=False, in_drop=0.0):
     """One fused MFMA step (csrc/dl_kernels.hip) and the fp32 autograd gradient of the same weighted loss
     (bf16 path: weights and inputs rounded to bf16 like the kernels' operands; f32: the fp32 master weights and
     inputs, v_mfma_f32_16x16x4_f32; dropout masks from ops.dense._mask_ref)."""
@@ -430,8 +430,9 @@ def _fused_case(n_in, hidden, K, act, drops, regression, B, seed=0, f32=False):
     wsrc = fp.p[: fp.n_decay] if f32 else shadow
     step_t = torch.full((1,), 7, dtype=torch.int64, device=dev)
     bases = [1234567 + 31 * i for i in range(len(hidden))]
+    in_seed = 99991
     fs = dlops.FusedMLPStep(fp, list(net.hidden) + [net.out], act, drops, bases, Z, w, y, regression, B, shadow,
-                            step_t, fp.g, None)
+                            step_t, fp.g, None, in_drop, in_seed)
     fs.refresh_transposed()
     fp.g.zero_()
     fs.step(ridx)
@@ -442,6 +443,11 @@ def _fused_case(n_in, hidden, K, act, drops, regression, B, seed=0, f32=False):
           .clone().requires_grad_(True) for l_ in list(net.hidden) + [net.out]]
     Bs = [l_.bias.detach().clone().requires_grad_(True) for l_ in list(net.hidden) + [net.out]]
     h = Z[ridx].float()
+    if in_drop > 0:                  # input dropout: the kernels' hash mask over (batch row, input)
+        m = _mask_ref((B, n_in), in_drop, step_seed(in_seed, 7), dev)
+        h = torch.where(m, h / (1 - in_drop), torch.zeros_like(h))
+        if not f32:                  # the bf16 kernels round the scaled inputs to bf16
+            h = h.to(torch.bfloat16).float()
     for i in range(len(hidden)):
         h = _act(act, h @ Ws[i].T + Bs[i])
         if drops[i] > 0:
@@ -493,6 +499,18 @@ def test_dl_fused_fp32_step_matches_fp32_autograd(n_in, hidden, K, act, drops, r
     got, ref = _fused_case(n_in, hidden, K, act, drops, regression, B, f32=True)
     rel = float((got - ref).norm() / ref.norm())
     assert rel < 1e-4, rel
+
+
+@pytest.mark.parametrize("f32", [False, True])
+@pytest.mark.parametrize("n_in,hidden,K,in_drop", [
+    (60, [64, 32], 40, 0.0),         # K > 16: logit tile over the waves, one wave per row for the softmax
+    (90, [48], 200, 0.2),            # 200 classes with input dropout
+    (784, [200, 200], 2, 0.1),       # input dropout on the BASELINE shape
+])
+def test_dl_fused_step_wide_softmax_and_input_dropout(n_in, hidden, K, in_drop, f32):
+    got, ref = _fused_case(n_in, hidden, K, 1, [0.0] * len(hidden), False, 256, f32=f32, in_drop=in_drop)
+    rel = float((got - ref).norm() / ref.norm())
+    assert rel < (1e-4 if f32 else 3e-2), rel
 
 
 def test_dl_trainer_uses_fused_step_and_learns(monkeypatch):
@@ -562,3 +580,24 @@ def test_deeplearning_reproducible_is_bit_identical(hidden):
                                      score_interval=1e9)).fit(X, y, None, None, info)
         preds.append(m.score_tensor(X).cpu())
     assert torch.equal(preds[0], preds[1])
+
+
+def test_dl_trainer_fused_multinomial_input_dropout(monkeypatch):
+    """30 classes with input dropout train through the fused step (wide softmax, input mask) and match the
+    autograd path's accuracy (H2O_DL_FUSED=0)."""
+    from llama_github_io_amd.models.base import DataInfo
+    from llama_github_io_amd.models.deeplearning import DeepLearningTrainer
+    g = torch.Generator(device=dev).manual_seed(2)
+    F, N, K = 40, 40000, 30
+    X = torch.rand(F, N, device=dev, generator=g)
+    y = torch.clamp((X[:3].sum(0) / 3 * K).long(), 0, K - 1).float()
+    info = DataInfo([f"x{i}" for i in range(F)], np.zeros(F, np.int32), [None] * F, "y", [str(i) for i in range(K)])
+    acc = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("H2O_DL_FUSED", flag)
+        m = DeepLearningTrainer(dict(hidden=[64], epochs=4, input_dropout_ratio=0.1, mini_batch_size=512, seed=5,
+                                     stopping_rounds=0, score_interval=1e9, standardize=False)).fit(X, y, None, None,
+                                                                                                    info)
+        assert bool(m.output["training_step_fused_mfma"]) == (flag == "1")
+        acc[flag] = 1 - m.output["training_metrics"]["mean_per_class_error"]
+    assert acc["1"] > 0.3 and abs(acc["1"] - acc["0"]) < 0.1, acc
