@@ -116,9 +116,25 @@ def show_progress():
 # ---- frames
 def import_file(path=None, destination_frame=None, parse=True, header=0, sep=None, col_names=None, col_types=None,
                 na_strings=None, pattern=None, skipped_columns=None, custom_non_data_line_markers=None,
-                partition_by=None, quotechar=None, escapechar=None):
+                partition_by=None, quotechar=None, escapechar=None, decrypt_tool=None):
     return _parse.import_file(path, destination_frame, parse, header, sep, col_names, col_types, na_strings, pattern,
-                              skipped_columns, custom_non_data_line_markers, partition_by, quotechar, escapechar)
+                              skipped_columns, custom_non_data_line_markers, partition_by, quotechar, escapechar,
+                              decrypt_tool=decrypt_tool)
+
+
+def decryption_setup(keystore, keystore_type="JCEKS", key_alias=None, password=None, decrypt_tool="",
+                     decrypt_impl="water.parser.GenericDecryptionTool", cipher_spec=None):
+    """R ``h2o.decryptionSetup`` / ``POST /3/DecryptionSetup``: install a Decryption Tool reading the secret key
+    ``key_alias`` of a (JCEKS) keystore file; pass the returned key to ``import_file(decrypt_tool=...)``."""
+    from llama_github_io_amd.io import decrypt as _dec
+    for n, v in (("key_alias", key_alias), ("password", password), ("cipher_spec", cipher_spec)):
+        if not isinstance(v, str) or not v:
+            raise ValueError(f"`{n}` must be a non-empty character string")
+    ks = getattr(keystore, "frame_id", keystore)
+    setup = _dec.DecryptionSetup(keystore_id=ks, keystore_type=keystore_type, key_alias=key_alias,
+                                 password=password, cipher_spec=cipher_spec, decrypt_tool_id=decrypt_tool or None,
+                                 decrypt_impl=decrypt_impl)
+    return _dec.make_tool(setup).key_id
 
 
 def upload_file(path, destination_frame=None, header=0, sep=None, col_names=None, col_types=None, na_strings=None,

@@ -738,8 +738,26 @@ def register(app, _params, _unquote, _model_json):
         return PlainTextResponse("thread dump written to the server log")
 
     # endpoints of the Java cluster that have no meaning for this engine answer with an H2OError naming why
-    for meth, path, why in (("POST", "/3/DecryptionSetup", "encrypted input files are not supported"),
-                            ("POST", "/3/ImportHiveTable", "Hive is not available (single-node MI355X engine)"),
+    @app.post("/3/DecryptionSetup")
+    async def decryption_setup(request: Request):
+        """DecryptionSetupHandler.setupDecryption: build the tool from the keystore (a raw file key), install it."""
+        from ..io import decrypt as dec
+        p = await _params(request)
+        ks = p.get("keystore_id")
+        ks = ks.get("name") if isinstance(ks, dict) else ks
+        setup = dec.DecryptionSetup(keystore_id=_unquote(ks), keystore_type=p.get("keystore_type") or "JCEKS",
+                                    key_alias=p.get("key_alias") or "", password=p.get("password") or "",
+                                    cipher_spec=p.get("cipher_spec") or "",
+                                    decrypt_tool_id=_unquote(p.get("decrypt_tool_id")) or None,
+                                    decrypt_impl=p.get("decrypt_impl") or "water.parser.GenericDecryptionTool")
+        tool = dec.make_tool(setup)
+        return {"__meta": v3.meta("DecryptionSetupV3", "DecryptionSetup"),
+                "decrypt_tool_id": {"__meta": v3.meta("DecryptionToolKeyV3", "Key<DecryptionTool>"),
+                                    "name": tool.key_id, "type": "Key<DecryptionTool>", "URL": None},
+                "decrypt_impl": setup.decrypt_impl, "keystore_id": v3.frame_key(str(setup.keystore_id)),
+                "keystore_type": setup.keystore_type, "key_alias": setup.key_alias, "cipher_spec": setup.cipher_spec}
+
+    for meth, path, why in (("POST", "/3/ImportHiveTable", "Hive is not available (single-node MI355X engine)"),
                             ("POST", "/3/SaveToHiveTable", "Hive is not available (single-node MI355X engine)"),
                             # the MOJO 2 pipeline export needs the external mojo2-runtime jar on the Java
                             # classpath in the reference too (h2o-py assembly.py:download_mojo)

@@ -348,7 +348,9 @@ def create_app(client_disconnect_timeout: float | None = None):
         src = [_unquote(x) for x in (src if isinstance(src, list) else [src])]
         sep = p.get("separator")
         sep = chr(sep) if isinstance(sep, int) else sep
-        st = P.parse_setup(src[0], header=int(p.get("check_header", 0) or 0), separator=sep)
+        dt = p.get("decrypt_tool")
+        dt = _unquote(dt.get("name") if isinstance(dt, dict) else dt) or None
+        st = P.parse_setup(src[0], header=int(p.get("check_header", 0) or 0), separator=sep, decrypt_tool=dt)
         st = _clean(st)
         tmap = {"real": "Numeric", "int": "Numeric", "enum": "Enum", "string": "String", "time": "Time"}
         ctypes_ = [tmap.get(t, t) for t in (st.get("column_types") or [])]
@@ -380,9 +382,11 @@ def create_app(client_disconnect_timeout: float | None = None):
             tmap = {"numeric": "real", "enum": "enum", "string": "string", "time": "time", "uuid": "string",
                     "categorical": "enum", "factor": "enum", "real": "real", "int": "int"}
             ct = [tmap.get(str(t).lower(), None) for t in ct]
+        dt = p.get("decrypt_tool")
+        dt = _unquote(dt.get("name") if isinstance(dt, dict) else dt) or None
         job = Job("Parse", dest=dest)
         job.run_async(P.import_file, src, dest, True, int(p.get("check_header", 0) or 0), sep,
-                      p.get("column_names"), ct, p.get("na_strings"))
+                      p.get("column_names"), ct, p.get("na_strings"), decrypt_tool=dt)
         return {"__meta": v3.meta("ParseV3", "Iced"), "job": v3.job(job), "destination_frame": v3.frame_key(dest),
                 "rows": 0}
 

@@ -68,7 +68,7 @@ def build_rt(force: bool = False, verbose: bool = False) -> str:
         return RT_LIB
     os.makedirs(LIB, exist_ok=True)
     tmp = RT_LIB + ".tmp"
-    cmd = ["g++", "-O3", "-march=x86-64-v2", "-shared", "-fPIC", "-std=c++17", "-pthread", "-I", CSRC, "-o", tmp] + srcs
+    cmd = ["g++", "-O3", "-march=x86-64-v2", "-shared", "-fPIC", "-std=c++17", "-pthread", "-I", CSRC, "-o", tmp] + srcs + ["-lcrypto"]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)

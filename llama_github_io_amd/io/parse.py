@@ -30,7 +30,19 @@ _TYPE_ALIASES = {"numeric": "real", "real": "real", "float": "real", "double": "
 
 
 # ------------------------------------------------------------------------------------------------
-def _read_bytes(path: str) -> bytes:
+def _read_bytes(path: str, decrypt_tool=None) -> bytes:
+    if decrypt_tool is not None:
+        # DecryptionTool.decryptInputStream: decrypt the raw file, then unpack a gzip / zip container by its magic
+        from .decrypt import get_tool
+        with open(path, "rb") as f:
+            data = get_tool(decrypt_tool).decrypt(f.read())
+        if data[:2] == b"\x1f\x8b":
+            return gzip.decompress(data)
+        if data[:4] == b"PK\x03\x04":
+            with zipfile.ZipFile(io.BytesIO(data)) as z:
+                names = [n for n in z.namelist() if not n.endswith("/")]
+                return b"".join(z.read(n) for n in names)
+        return data
     if path.endswith(".gz"):
         with gzip.open(path, "rb") as f:
             return f.read()
@@ -60,6 +72,17 @@ def _expand(path) -> list:
     return [path]
 
 
+def _plain_name(path: str, decrypt_tool) -> str:
+    """The file name parse-type guessing sees: an encrypted file's extension (.aes / .enc) says nothing."""
+    if decrypt_tool is None:
+        return path
+    low = path.lower()
+    for ext in (".aes", ".enc", ".encrypted"):
+        if low.endswith(ext):
+            return path[: -len(ext)]
+    return path
+
+
 def guess_parse_type(path: str, head: bytes) -> str:
     low = path.lower()
     for ext, t in ((".parquet", "PARQUET"), (".svm", "SVMLight"), (".svmlight", "SVMLight"), (".arff", "ARFF"),
@@ -79,11 +102,11 @@ def guess_parse_type(path: str, head: bytes) -> str:
 
 
 def parse_setup(path, destination_frame=None, header=0, separator=None, column_names=None, column_types=None,
-                na_strings=None) -> dict:
+                na_strings=None, decrypt_tool=None) -> dict:
     """``/3/ParseSetup``: guess parse type, separator, header, column names and types."""
     files = _expand(path)
-    head = _read_bytes(files[0])[: 1 << 20]
-    ptype = guess_parse_type(files[0], head)
+    head = _read_bytes(files[0], decrypt_tool)[: 1 << 20]
+    ptype = guess_parse_type(_plain_name(files[0], decrypt_tool), head)
     out = dict(source_frames=[{"name": f} for f in files], parse_type=ptype, destination_frame=destination_frame or
                _dest_name(files[0]), check_header=header, separator=None, column_names=None, column_types=None,
                number_columns=0, na_strings=na_strings)
@@ -483,8 +506,9 @@ def parse_parquet(path: str, device=None) -> H2OFrame:
 
 def import_file(path=None, destination_frame=None, parse=True, header=0, sep=None, col_names=None, col_types=None,
                 na_strings=None, pattern=None, skipped_columns=None, custom_non_data_line_markers=None,
-                partition_by=None, quotechar=None, escapechar=None) -> H2OFrame:
-    """``h2o.import_file``: file, directory, glob or list; multiple files are row-bound (ParseDataset)."""
+                partition_by=None, quotechar=None, escapechar=None, decrypt_tool=None) -> H2OFrame:
+    """``h2o.import_file``: file, directory, glob or list; multiple files are row-bound (ParseDataset).
+    ``decrypt_tool``: key (or object) of a Decryption Tool (io/decrypt.py) applied to every file first."""
     files = _expand(path)
     if pattern:
         import re
@@ -495,7 +519,8 @@ def import_file(path=None, destination_frame=None, parse=True, header=0, sep=Non
     frames = []
     from ..parallel import dframe
     for i, f in enumerate(files):
-        dist_parse = dframe.active() and not dframe.in_method()
+        # an encrypted file is decrypted whole (ECB / padding), not split into per-rank byte ranges
+        dist_parse = dframe.active() and not dframe.in_method() and decrypt_tool is None
         if dist_parse:
             with open(f, "rb") as fh:
                 head = fh.read(4096)
@@ -505,14 +530,14 @@ def import_file(path=None, destination_frame=None, parse=True, header=0, sep=Non
             if ptype != "CSV":
                 dist_parse = False
         if not dist_parse or ptype != "CSV":
-            buf = _read_bytes(f)
-            ptype = guess_parse_type(f, buf[:4096])
+            buf = _read_bytes(f, decrypt_tool)
+            ptype = guess_parse_type(_plain_name(f, decrypt_tool), buf[:4096])
         if ptype == "SVMLight":
             fr = parse_svmlight(buf)
         elif ptype == "ARFF":
             fr = parse_arff(buf)
         elif ptype == "PARQUET":
-            fr = parse_parquet(f)
+            fr = parse_parquet(io.BytesIO(buf) if decrypt_tool is not None else f)
         elif ptype in ("XLS", "XLSX", "AVRO"):
             from . import formats
             grid = {"XLS": formats.read_xls, "XLSX": formats.read_xlsx, "AVRO": formats.read_avro}[ptype](buf)
