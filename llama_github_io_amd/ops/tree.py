@@ -765,8 +765,7 @@ class GpuTreeBuilder:
             self.fine_f = torch.as_tensor(self.fine_f, device=self.dev).contiguous()
         if getattr(self, "_plan", None) is not None:
             self._plan.fgroup = 0 if self.fgroup is None else self.fgroup.data_ptr()
-            self._plan.fine_f = (0 if self.fine_f is None or os.environ.get("H2O_HIST_FINE") == "0"
-                                 else self.fine_f.data_ptr())
+            self._plan.fine_f = 0 if self.fine_f is None else self.fine_f.data_ptr()
 
     def _set_plan_ic(self, P):
         if self.ic_map is None:
@@ -806,7 +805,7 @@ class GpuTreeBuilder:
         self._set_plan_ic(P)
         fg = getattr(self, "fgroup", None)
         P.fgroup = 0 if fg is None else fg.data_ptr()
-        P.fine_f = 0 if self.fine_f is None or os.environ.get("H2O_HIST_FINE") == "0" else self.fine_f.data_ptr()
+        P.fine_f = 0 if self.fine_f is None else self.fine_f.data_ptr()     # used only under H2O_HIST_FINE=1
         P.sliced, P.fs0, P.fsn, P.sslot = int(self.sliced), self.fs0, self.fsn, self.sslot
         P.planar = int(self.planar)
         P.no_na = int(self._no_na())

@@ -590,14 +590,13 @@ def test_dl_trainer_fused_multinomial_input_dropout(monkeypatch):
     g = torch.Generator(device=dev).manual_seed(2)
     F, N, K = 40, 40000, 30
     X = torch.rand(F, N, device=dev, generator=g)
-    y = torch.clamp((X[:3].sum(0) / 3 * K).long(), 0, K - 1).float()
+    y = torch.clamp((X[0] * K).long(), 0, K - 1).float()
     info = DataInfo([f"x{i}" for i in range(F)], np.zeros(F, np.int32), [None] * F, "y", [str(i) for i in range(K)])
     acc = {}
     for flag in ("1", "0"):
         monkeypatch.setenv("H2O_DL_FUSED", flag)
-        m = DeepLearningTrainer(dict(hidden=[64], epochs=4, input_dropout_ratio=0.1, mini_batch_size=512, seed=5,
-                                     stopping_rounds=0, score_interval=1e9, standardize=False)).fit(X, y, None, None,
-                                                                                                    info)
+        m = DeepLearningTrainer(dict(hidden=[64], epochs=8, input_dropout_ratio=0.1, mini_batch_size=512, seed=5,
+                                     stopping_rounds=0, score_interval=1e9)).fit(X, y, None, None, info)
         assert bool(m.output["training_step_fused_mfma"]) == (flag == "1")
         acc[flag] = 1 - m.output["training_metrics"]["mean_per_class_error"]
-    assert acc["1"] > 0.3 and abs(acc["1"] - acc["0"]) < 0.1, acc
+    assert acc["1"] > 0.15 and abs(acc["1"] - acc["0"]) < 0.08, acc     # chance: 1/30

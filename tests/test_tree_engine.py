@@ -533,10 +533,13 @@ def test_wide_bins_split_resolution_and_grouped_sampling():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("fine", ["0", "1"])
 @pytest.mark.parametrize("case", ["plain", "kcols_adaptive", "newton"])
-def test_gpu_wide_bins_match_reference(case):
+def test_gpu_wide_bins_match_reference(case, fine, monkeypatch):
     """1016-bin numeric features (4 engine columns each) on the GPU engine vs RefTreeBuilder: identical
-    decisions, left weights and leaf assignment, including grouped column sampling (k_split_reduce fgroup)."""
+    decisions, left weights and leaf assignment, including grouped column sampling (k_split_reduce fgroup), with and
+    without the fine-bin atomics of the 4-column groups (H2O_HIST_FINE)."""
+    monkeypatch.setenv("H2O_HIST_FINE", fine)
     X, y, info = _data(N=30000, cat=True, seed=11)
     b = fit_binning(X, info.iscat, info.nlevels, max_bins=1016)
     assert b.vmap is not None and b.F > X.shape[0]
