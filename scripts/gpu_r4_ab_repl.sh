@@ -1,13 +1,21 @@
 #!/bin/bash
-# Same-box A/B of the histogram's low-cardinality bin replicas (H2O_HIST_REPL=0 turns them off), alternated twice.
+# Same-box A/B of histogram settings: low-cardinality bin replicas (H2O_HIST_REPL=0 turns them off) and the
+# histogram grid (H2O_HIST_GRID: blocks per launch; 256 = one 16-wave block per CU, 512 = two).
 set -o pipefail
 O=gpurun_out/r4_ab_repl
 mkdir -p $O
 export TMPDIR=/tmp
+run() {  # name rows steps env...
+  local n=$1 r=$2 st=$3; shift 3
+  env "$@" timeout -k 10 200 python bench.py --rows $r --steps $st --warmup 5 --no-job > $O/$n.json 2> $O/$n.err || return $?
+  python3 -c "import json; d=json.load(open('$O/$n.json')); print('$n', d['ms_per_step'])"
+}
 for i in 1 2; do
-  timeout -k 10 200 python bench.py --steps 20 --warmup 5 --no-job > $O/on_$i.json 2> $O/on_$i.err || exit $?
-  H2O_HIST_REPL=0 timeout -k 10 200 python bench.py --steps 20 --warmup 5 --no-job > $O/off_$i.json 2> $O/off_$i.err || exit $?
+  run on_$i 11000000 20 H2O_HIST_REPL=1 || exit $?
+  run off_$i 11000000 20 H2O_HIST_REPL=0 || exit $?
+  run g512_$i 11000000 20 H2O_HIST_GRID=512 || exit $?
 done
-timeout -k 10 200 python bench.py --rows 1375000 --steps 50 --warmup 5 --no-job > $O/on_1375k.json 2> $O/on_1375k.err || exit $?
-H2O_HIST_REPL=0 timeout -k 10 200 python bench.py --rows 1375000 --steps 50 --warmup 5 --no-job > $O/off_1375k.json 2> $O/off_1375k.err || exit $?
-for f in $O/*.json; do python3 -c "import json,sys; d=json.load(open('$f')); print('$f', d['ms_per_step'])"; done
+run g384 11000000 20 H2O_HIST_GRID=384 || exit $?
+run on_1375k 1375000 50 H2O_HIST_REPL=1 || exit $?
+run off_1375k 1375000 50 H2O_HIST_REPL=0 || exit $?
+run g512_1375k 1375000 50 H2O_HIST_GRID=512 || exit $?
