@@ -101,10 +101,19 @@ __global__ __launch_bounds__(256) void k_bias_act_bwd(const T* __restrict__ gy, 
 // ADADELTA (Neurons.java: rho, epsilon) fused over the FLAT parameter buffer of the whole network:
 // one launch updates every weight and bias (the per-tensor torch version is ~36 launches per step).
 // L1/L2 apply to weights only: elements [0, n_decay) are the weight matrices, the rest biases.
+// Transposed weight copy the fused DL step's backward pass reads (ops/dl.py): layer l's [n_out][n_in] block at
+// w_off[l] is also written as [n_in][n_out] (bf16 or fp32), so no separate transpose launch follows the update.
+struct WTMap {
+  void* wt;
+  int f32, L;
+  long long w_off[7];
+  int n_in[6], n_out[6];
+};
+
 __global__ __launch_bounds__(256) void k_adadelta(float* __restrict__ p, const float* __restrict__ g,
                                                   float* __restrict__ eg2, float* __restrict__ edx2, int64_t n,
                                                   int64_t n_decay, float rho, float eps, float l1, float l2,
-                                                  __hip_bfloat16* __restrict__ shadow) {
+                                                  __hip_bfloat16* __restrict__ shadow, WTMap tm) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const float pi = p[i];
     float gi = g[i];
@@ -115,6 +124,16 @@ __global__ __launch_bounds__(256) void k_adadelta(float* __restrict__ p, const f
     edx2[i] = rho * edx2[i] + (1.f - rho) * d * d;
     p[i] = pi + d;
     if (shadow && i < n_decay) shadow[i] = __float2bfloat16(pi + d);   // bf16 weights for the next GEMMs
+    if (tm.wt && i < n_decay) {
+      int l = 0;
+      while (l + 1 < tm.L && i >= tm.w_off[l + 1]) ++l;
+      const int64_t o = i - tm.w_off[l];
+      const int nin = tm.n_in[l];
+      const int64_t r = o / nin, c = o - r * nin;
+      const int64_t t = tm.w_off[l] + c * tm.n_out[l] + r;
+      if (tm.f32) ((float*)tm.wt)[t] = pi + d;
+      else ((__hip_bfloat16*)tm.wt)[t] = __float2bfloat16(pi + d);
+    }
   }
 }
 
@@ -235,13 +254,21 @@ int h2o_num_transform(const float* X, long long N, const int* rows, int nf, cons
   return (int)hipGetLastError();
 }
 
+// wt (nullable): transposed copy to write along (tm_off/tm_in/tm_out: L layers' offsets and shapes)
 int h2o_adadelta(float* p, const float* g, float* eg2, float* edx2, long long n, long long n_decay, float rho, float eps,
-                 float l1, float l2, void* shadow, hipStream_t stream) {
+                 float l1, float l2, void* shadow, void* wt, int wt_f32, int L, const long long* tm_off,
+                 const int* tm_in, const int* tm_out, hipStream_t stream) {
   long long grid = (n + 255) / 256;
   if (grid > 4096) grid = 4096;
   if (grid < 1) grid = 1;
+  WTMap tm{};
+  if (wt) {
+    if (L < 1 || L > 6) return (int)hipErrorInvalidValue;
+    tm.wt = wt; tm.f32 = wt_f32; tm.L = L;
+    for (int l = 0; l < L; ++l) { tm.w_off[l] = tm_off[l]; tm.n_in[l] = tm_in[l]; tm.n_out[l] = tm_out[l]; }
+  }
   hipLaunchKernelGGL(k_adadelta, dim3((unsigned)grid), dim3(256), 0, stream, p, g, eg2, edx2, (int64_t)n,
-                     (int64_t)n_decay, rho, eps, l1, l2, (__hip_bfloat16*)shadow);
+                     (int64_t)n_decay, rho, eps, l1, l2, (__hip_bfloat16*)shadow, tm);
   return (int)hipGetLastError();
 }
 

@@ -404,8 +404,10 @@ class DeepLearningTrainer:
                     fp.g.copy_(gbuf[:-1] / gbuf[-1].clamp(min=1e-12))
                 if elastic and ea_lam > 0:   # elastic pull towards the consensus (Neurons.java:263,414)
                     fp.g.add_((fp.p - ea[: fp.p.numel()]) * (ea_on * ea_lam))
-                if adaptive:      # ADADELTA (Neurons.java: rho, epsilon); also refreshes the bf16 weights
-                    fp.adadelta(rho, eps, l1, l2, shadow)
+                fobj = fz.get("obj")
+                if adaptive:      # ADADELTA (Neurons.java: rho, epsilon); also refreshes the bf16 weights and
+                    # (fused step) the transposed copy its backward pass reads
+                    fp.adadelta(rho, eps, l1, l2, shadow, None if fobj is None else fobj.wt_map)
                 else:
                     gg = fp.g.clone()
                     nd = fp.n_decay
@@ -424,8 +426,8 @@ class DeepLearningTrainer:
                             q.mul_(torch.where(n2 > max_w2, torch.sqrt(max_w2 / n2), torch.ones_like(n2)))
                 if shadow is not None and (not adaptive or max_w2 < float("inf")):
                     shadow.copy_(fp.p[: fp.n_decay])
-                if fz.get("obj") is not None:
-                    fz["obj"].refresh_transposed()
+                if fobj is not None and (not adaptive or max_w2 < float("inf")):
+                    fobj.refresh_transposed()
 
         # Explicit training step (no autograd) for the common MLPs: GEMMs on bf16 weight copies kept by the
         # fused ADADELTA kernel, fused bias/activation/dropout epilogues, one fused softmax-CE / squared-error

@@ -166,6 +166,11 @@ class FusedMLPStep:
         a.n_decay, a.n_total = fp.n_decay, fp.p.numel()
         self.args = a
         self.scale_by_w = out_gsum is None
+        # the optimizer writes WT in its own launch (FlatParams.adadelta(wt=...)): host arrays of layer shapes
+        import numpy as _np
+        self.wt_map = (self.WT, _np.ascontiguousarray([a.w_off[l] for l in range(L)] + [fp.n_decay], dtype=_np.int64),
+                       _np.ascontiguousarray(n[:L], dtype=_np.int32),
+                       _np.ascontiguousarray(n[1:L + 1], dtype=_np.int32))
         self._keep = (Z, w, y, wsrc, step_dev, out_grad, out_gsum)
 
     def step(self, ridx: torch.Tensor) -> None:
