@@ -326,9 +326,6 @@ __device__ __forceinline__ int filt_append(const RowFilter& flt, int r0, int r1,
 #ifndef H2O_UNR
 #define H2O_UNR 8
 #endif
-#ifndef H2O_PIPE
-#define H2O_PIPE 1      // plain passes: software-pipelined batches over merged same-node tiles (0: A/B baseline)
-#endif
 // hist: rows per lane group loaded before any atomic (UNR independent loads per lane; the FILT queue batches use 8)
 
 // Row loads of the histogram loop. BUF: 32-bit buffer offsets into the bins (rows of 2^lgw bytes) and the aux planes
@@ -353,6 +350,11 @@ __device__ __forceinline__ HistSrc make_src(const unsigned* bins32, const float*
                  lgw};
 }
 
+// MEASURED (r4, 11M x 28 HIGGS shape, same-box A/B): the plain pass issues 11M x 28 = 308M ds_add_u64 in ~131 us,
+// one wave-level atomic per ~16 cycles per CU: it runs at the LDS atomic rate. Software-pipelining the row batches
+// across merged same-node tiles changed nothing (1.376-1.394 vs 1.380-1.388 ms/tree), a 64-VGPR build with two
+// blocks per CU was 13 % slower (spills), 512 / 384 blocks per launch 5-8 % slower (more partials), and spreading
+// low-cardinality features over bin replicas removed the SQ_LDS_ADDR_CONFLICT cycles (1.8e8 -> 5e6) at equal time.
 // Histogram rows [r0, r1) of one node into LDS (FILT: entries [r0, r1) of the LDS row list): lane group g
 // (8 lanes, one 4-feature row word each) takes rows g, g + GR, ...; UNR rows per lane group are loaded
 // before any atomic.
@@ -400,83 +402,6 @@ __device__ __forceinline__ void hist_rows(long long* h, float* nayy, const HistS
   auto ent = [&](unsigned w, int k) -> unsigned long long* {
     return (unsigned long long*)(Hb + ((__builtin_amdgcn_ubfe(w, sh[k], 8) << 8) + offb[k]));
   };
-  // One row word: every live lane adds all 4 of its word's features, valid or not: a feature past F (a partial last
-  // word) has the slot of a feature >= the tile's count, an LDS column the flush never reads, so its atomics are
-  // harmless — no divergent full / partial paths (the former per-row exec-mask juggling cost ~10 SALU per row).
-  // Only the rare NA-bin yy tally branches.
-  auto row_v = [&](const unsigned w, const float2 abv) {
-    // UNIT (packed, every row weight exactly 1): constant count part, yy = wY^2 (no reciprocal)
-    if (lead) wyy += UNIT ? abv.y * abv.y : row_yy(abv.x, abv.y);
-    // (int) conversion truncates toward zero (v_cvt_i32_f32): the __float2int_rz form added a v_trunc_f32
-    const long long qa = UNIT ? (1ll << PACK_SHIFT) + (long long)(int)(abv.y * sp)
-                              : PACKED ? qpack(abv.x, abv.y, sp) : q64(abv.x, sa);
-    const long long qb = PACKED ? 0ll : q64(abv.y, sb);
-    if (fine) {
-      const unsigned t = __builtin_amdgcn_sad_u8(w, 0u, 0u);          // sum of the 4 bytes
-      const unsigned l = t & 3u;
-      const unsigned so = (l & 2u) ? ((l & 1u) ? fsl[3] : fsl[2]) : ((l & 1u) ? fsl[1] : fsl[0]);
-      unsigned long long* p = (unsigned long long*)(Hb + (((t >> 2) << 8) + so));
-      atomicAdd(p, (unsigned long long)qa);
-      if (!PACKED) atomicAdd(p + HPLANE, (unsigned long long)qb);
-    } else if (live) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        unsigned long long* p = ent(w, k);
-        atomicAdd(p, (unsigned long long)qa);
-        if (!PACKED) atomicAdd(p + HPLANE, (unsigned long long)qb);
-      }
-    }
-    if (!NONA) {
-      const unsigned x = ~w | ~vmask;                   // a zero byte of x = an NA bin of a valid feature
-      if (((x - 0x01010101u) & ~x & 0x80808080u) != 0u) {
-        const float yy = UNIT ? abv.y * abv.y : row_yy(abv.x, abv.y);
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          if (((vmask >> sh[k]) & 1u) && __builtin_amdgcn_ubfe(w, sh[k], 8) == NA_BIN)
-            atomicAdd(nayy + j * 4 + (sh[k] >> 3), yy);
-      }
-    }
-  };
-#if H2O_PIPE
-  // Contiguous rows (plain passes): software pipeline over whole batches, two register sets in turn — the next
-  // batch's loads are in flight while this batch's atomics issue (the loop above hid no memory latency: each
-  // batch waited for its own loads first).
-  if (BUF && !FILT && r0 + GR * UNR <= r1) {
-    unsigned wA[UNR], wB[UNR];
-    float2 aA[UNR], aB[UNR];
-    auto load = [&](int b, unsigned (&wd)[UNR], float2 (&ab)[UNR]) {
-      const unsigned row0 = (unsigned)(b + g);
-      const unsigned vb = (row0 << src.lgw) + (unsigned)wc * 4u, va = row0 * 4u;
-#pragma unroll
-      for (int u = 0; u < UNR; ++u) {
-        wd[u] = __builtin_amdgcn_raw_buffer_load_b32(src.rb, vb, (unsigned)(u * GR) << src.lgw, 0);
-        const float y = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(src.ra, va, u * GR * 4, 0));
-        const float w = weighted ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(src.rw, va, u * GR * 4, 0))
-                                 : 1.f;
-        ab[u] = make_float2(w, y);
-      }
-    };
-    int base = r0;
-    load(base, wA, aA);
-    for (;;) {
-      const int n1 = base + GR * UNR;
-      const bool m1 = n1 + GR * UNR <= r1;           // block-uniform
-      if (m1) load(n1, wB, aB);
-#pragma unroll
-      for (int u = 0; u < UNR; ++u) row_v(wA[u], aA[u]);
-      base = n1;
-      if (!m1) break;
-      const int n2 = base + GR * UNR;
-      const bool m2 = n2 + GR * UNR <= r1;
-      if (m2) load(n2, wA, aA);
-#pragma unroll
-      for (int u = 0; u < UNR; ++u) row_v(wB[u], aB[u]);
-      base = n2;
-      if (!m2) break;
-    }
-    r0 = base;                                       // a partial last batch goes through the loop below
-  }
-#endif
   for (int base = r0; base < r1; base += GR * UNR) {
     unsigned wd[UNR];
     float2 ab[UNR];
@@ -513,7 +438,44 @@ __device__ __forceinline__ void hist_rows(long long* h, float* nayy, const HistS
         }
       }
     }
-    auto row = [&](int u) { row_v(wd[u], ab[u]); };
+    // One row word: every live lane adds all 4 of its word's features, valid or not: a feature past F (a partial last
+    // word) has the slot of a feature >= the tile's count, an LDS column the flush never reads, so its atomics are
+    // harmless — no divergent full / partial paths (the former per-row exec-mask juggling cost ~10 SALU per row).
+    // Only the rare NA-bin yy tally branches.
+    auto row = [&](int u) {
+      // UNIT (packed, every row weight exactly 1): constant count part, yy = wY^2 (no reciprocal)
+      if (lead) wyy += UNIT ? ab[u].y * ab[u].y : row_yy(ab[u].x, ab[u].y);
+      // (int) conversion truncates toward zero (v_cvt_i32_f32): the __float2int_rz form added a v_trunc_f32
+      const long long qa = UNIT ? (1ll << PACK_SHIFT) + (long long)(int)(ab[u].y * sp)
+                                : PACKED ? qpack(ab[u].x, ab[u].y, sp) : q64(ab[u].x, sa);
+      const long long qb = PACKED ? 0ll : q64(ab[u].y, sb);
+      const unsigned w = wd[u];
+      if (fine) {
+        const unsigned t = __builtin_amdgcn_sad_u8(w, 0u, 0u);          // sum of the 4 bytes
+        const unsigned l = t & 3u;
+        const unsigned so = (l & 2u) ? ((l & 1u) ? fsl[3] : fsl[2]) : ((l & 1u) ? fsl[1] : fsl[0]);
+        unsigned long long* p = (unsigned long long*)(Hb + (((t >> 2) << 8) + so));
+        atomicAdd(p, (unsigned long long)qa);
+        if (!PACKED) atomicAdd(p + HPLANE, (unsigned long long)qb);
+      } else if (live) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          unsigned long long* p = ent(w, k);
+          atomicAdd(p, (unsigned long long)qa);
+          if (!PACKED) atomicAdd(p + HPLANE, (unsigned long long)qb);
+        }
+      }
+      if (!NONA) {
+        const unsigned x = ~w | ~vmask;                   // a zero byte of x = an NA bin of a valid feature
+        if (((x - 0x01010101u) & ~x & 0x80808080u) != 0u) {
+          const float yy = UNIT ? ab[u].y * ab[u].y : row_yy(ab[u].x, ab[u].y);
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (((vmask >> sh[k]) & 1u) && __builtin_amdgcn_ubfe(w, sh[k], 8) == NA_BIN)
+              atomicAdd(nayy + j * 4 + (sh[k] >> 3), yy);
+        }
+      }
+    };
     if (whole) {
 #pragma unroll
       for (int u = 0; u < UNR; ++u) row(u);
@@ -531,11 +493,8 @@ __device__ __forceinline__ void hist_rows(long long* h, float* nayy, const HistS
 // (deterministic, no global atomics). grid = (G, n_ftiles); each block takes a contiguous tile range.
 // FILT (odd levels): a node's tiles cover its PARENT's rows; only rows the parent's decision sends to
 // this child are accumulated, and ftile-0 blocks add the parent's left-going row count to nl_out.
-#ifndef H2O_HIST_MINW
-#define H2O_HIST_MINW 1   // min waves per SIMD the register budget is sized for (8: <= 64 VGPRs, two blocks per CU)
-#endif
 template <bool FILT, bool PACKED, bool UNIT, bool NONA, bool BUF>
-__global__ __launch_bounds__(BLK, H2O_HIST_MINW) void k_hist_build(
+__global__ __launch_bounds__(BLK) void k_hist_build(
     const uint8_t* __restrict__ bins, int stride /*bytes per row, multiple of 4*/,
     const float* __restrict__ aw /*row weights or null (unit)*/, const float* __restrict__ ay /*w * Y*/,
     const Node* __restrict__ nodes, const int* __restrict__ tile_prefix,
@@ -675,21 +634,8 @@ __global__ __launch_bounds__(BLK, H2O_HIST_MINW) void k_hist_build(
         qn = rest;
       }
     } else {
-      int r1m = r1;
-#if H2O_PIPE
-      // the following tiles of the same node inside this flush window become one row range: the software
-      // pipeline of hist_rows then runs across tile boundaries
-      const int nend = nd.start + nd.len;
-      while (t + 1 < t1 && r1m < nend) {
-        const int nr = min(r1m + TILE, nend);
-        if (packed && since + (nr - r1m) > PACK_MAX) break;
-        since += nr - r1m;
-        r1m = nr;
-        ++t;
-      }
-#endif
-      hist_rows<FILT, PACKED, UNIT, NONA, BUF>(h, nayy, src, W, wabs, Fl, j == 0 && ftile == 0, r0, r1m, g, j, wf, sa,
-                                               sb, sp, nullptr, srep, snb, sfine);
+      hist_rows<FILT, PACKED, UNIT, NONA, BUF>(h, nayy, src, W, wabs, Fl, j == 0 && ftile == 0, r0, r1, g, j, wf, sa, sb,
+                                               sp, nullptr, srep, snb, sfine);
     }
     wyy += (double)wf;
   }

@@ -999,13 +999,19 @@ class DeepLearningTrainer:
         N = X.shape[1]
         Ng, r0 = getattr(self, "_N_glob", N), getattr(self, "_row0", 0)
         n = int(p["score_training_samples"]) or Ng
-        if n >= Ng:
+        key = (N, Ng, r0, n)
+        cached = getattr(self, "_score_idx", None)
+        if cached is not None and cached[0] == key:
+            idx = cached[1]          # the same seeded sample at every scoring event
+        elif n >= Ng:
             idx = torch.arange(N, device=X.device)
-        else:       # a sample of GLOBAL rows (same rows however the frame is sharded)
-            # drawn on the device (a host randperm of 10M rows costs ~0.2 s per scoring event)
-            gi = torch.randperm(Ng, device=X.device, generator=torch.Generator(device=X.device).manual_seed(
-                int(p.get("seed") or 0) & 0x7FFFFFFF))[:n]
-            idx = gi[(gi >= r0) & (gi < r0 + N)] - r0
+        else:
+            # MRUtils.sampleFrame: every GLOBAL row kept with probability n / N (counter-based per-row uniforms:
+            # the same rows however the frame is sharded; no device randperm / sort of the whole frame)
+            from ..parallel import collectives as _c
+            u = _c.row_uniform(int(p.get("seed") or 0), 0x5C0BE, r0, N, X.device)
+            idx = torch.nonzero(u < n / Ng).squeeze(1)
+        self._score_idx = (key, idx)
         Xs = X[:, idx]
         ev = dict(epochs=epochs, timestamp=time.time())
         if p["autoencoder"]:
