@@ -12,12 +12,11 @@
 //              act'(h) run the same way on transposed weight copies. The tile writes its activations and
 //              gradients TRANSPOSED ([units][rows]) for the weight-gradient GEMM and its per-column bias
 //              gradient partial sums (fixed-order reduce later, no atomics).
-//  k_dl_wgrad  dW_l = dA_lᵀ h_{l-1} for every layer in one launch: one 32 x 32 output tile per workgroup,
-//              the mini-batch rows (GEMM K) interleaved over 8 waves in 32-row chunks with 4 chunks of
-//              loads in flight per wave, the 8 partial tiles summed through LDS in a fixed order and written
-//              straight into the flat gradient buffer scaled by 1 / sum(w) of the batch (single process) or
-//              raw plus the batch weight (data parallel). Trailing workgroups reduce the per-tile bias
-//              partials of k_dl_rows (one wave per bias, fixed order).
+//  k_dl_wgrad  dW_l = dA_lᵀ h_{l-1} for every layer in one launch: 64 x 64 output tiles, the mini-batch rows
+//              (GEMM K) split over workgroups and, inside one, over 4 waves; partials summed in a fixed order
+//              and written straight into the flat gradient buffer scaled by 1 / sum(w) of the batch (single
+//              process) or raw plus the batch weight (data parallel). Trailing workgroups reduce the per-tile
+//              bias partials of k_dl_rows (one wave per bias, fixed order).
 //  MEASURED (10M x 784 [200,200], 4096-row steps, rocprofv3): the first version (16-row tiles on 4 waves,
 //  64 x 64 x 4-split weight tiles with fp32 slabs and a separate reduce) took 52 + 32 + 64 us per step:
 //  latency-bound dependent L2 round trips and a serial 256-deep bias loop, not MFMA or HBM.
@@ -44,8 +43,6 @@ typedef __hip_bfloat16 bf16;
 #define DL_ROWS 16       // rows per k_dl_rows tile
 #define DL_THREADS 1024  // k_dl_rows workgroup: 16 waves (one 16-column output tile each per round)
 #define DL_NW (DL_THREADS / 64)
-#define WG_WAVES 8       // k_dl_wgrad waves per 32 x 32 tile (split over the mini-batch rows)
-#define WG_KU 4          // 32-row chunks of loads in flight per wave
 
 struct DLArgs {
   const void* Z; long long ldz; const long long* ridx; int B; int Bpad;
@@ -67,6 +64,9 @@ struct DLArgs {
   int f32, pad_;                // 1: fp32 operands (Z, W, WT, hT, dT, LDS tiles), 0: bf16
   float in_drop; int lds_lg;    // input dropout ratio; K > 16: byte offset of the fp32 [16][K] logit tile
   unsigned long long in_seed;   // input dropout seed base
+  int wsplit, pad2_;            // k_dl_wgrad: batch-row (GEMM K) splits per 64 x 64 tile
+  float* wpart;                 // [tiles][wsplit][64 * 64] fp32 partial tiles
+  unsigned* wcnt;               // [tiles] arrival counters (zero between steps: the last arrival resets)
 };
 
 __device__ __forceinline__ uint32_t hash32(uint64_t x) {
@@ -428,69 +428,63 @@ __global__ __launch_bounds__(DL_THREADS) void k_dl_rows(DLArgs a) {
 // Workgroup = one 32 x 32 tile of one layer (2 x 2 MFMA tiles per wave); wave w accumulates row chunks
 // w, w + 8, w + 16, ... (32 rows each); partial tiles meet in LDS and wave 0 sums them in wave order.
 // Workgroups past the weight tiles reduce bias gradients from the k_dl_rows partials (wave = bias).
-// MFMA accumulation of one wave's row chunks of a 32 x 32 weight-gradient tile (A rows arow[u] = dT of units i,
-// B rows brow[v] = hT of units j, both along the batch rows = GEMM K).
-// bf16: 32-row chunks (8 rows per lane, one 16x16x32 MFMA); fp32: 16-row chunks (4 rows per lane, 4 MFMAs).
-__device__ __forceinline__ void wgrad_acc(const bf16* const (&arow)[2], const bf16* const (&brow)[2], const bool (&aok)[2],
-                                          const bool (&bok)[2], int nrows, int wv, f32x4 (&acc)[2][2]) {
-  const int nch = nrows / 32;
+// dW_l[i][j] = sum_rows dA_l[row][i] h_{l-1}[row][j]: A[i][k = row] = dT_l[i][row], B[k = row][j] = hT_{l-1}[j][row]
+// (both operands contiguous along the batch rows = GEMM K). One 64 x 64 output tile per (tile, split) workgroup of
+// 4 waves: the batch rows are cut into `wsplit` ranges (enough workgroups to fill the chip) and each wave takes
+// every 4th chunk of its workgroup's range with all 16 MFMA tiles of the 64 x 64 block in registers (per chunk 4 A
+// and 4 B fragments feed 16 MFMAs). The 4 waves meet in LDS in wave order, the split partials in a global buffer;
+// the workgroup arriving last for a tile sums them in split order (deterministic) into the gradient.
+// MEASURED (r4): 32 x 32 tiles re-read every operand row 7-25 times from L2 (225 MB per fp32 step, 92 us).
+// bf16: 32-row chunks, 8 rows per lane quarter (v_mfma_f32_16x16x32_bf16); fp32: 16-row chunks, 4 rows per lane
+// quarter and 4 v_mfma_f32_16x16x4_f32 each.
+#define WG4 4
+// operand fragments of one chunk: 4 A rows-blocks and 4 B column-blocks per lane
+struct FragB { bf16x8 a[4], b[4]; };
+struct FragF { float4 a[4], b[4]; };
+__device__ __forceinline__ void wg_load(FragB& f, const bf16* const (&ar)[4], const bf16* const (&br)[4],
+                                        const bool (&aok)[4], const bool (&bok)[4], int ch) {
   const bf16x8 z8 = {(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
-  for (int cb = wv; cb < nch; cb += WG_WAVES * WG_KU) {
-    bf16x8 av[WG_KU][2], bv[WG_KU][2];
 #pragma unroll
-    for (int k = 0; k < WG_KU; ++k) {
-      const int ch = cb + k * WG_WAVES;
-      const bool in = ch < nch;
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        av[k][u] = (in && aok[u]) ? *reinterpret_cast<const bf16x8*>(arow[u] + ch * 32) : z8;
-        bv[k][u] = (in && bok[u]) ? *reinterpret_cast<const bf16x8*>(brow[u] + ch * 32) : z8;
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < WG_KU; ++k)
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int v = 0; v < 2; ++v)
-          acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[k][u], bv[k][v], acc[u][v], 0, 0, 0);
+  for (int u = 0; u < 4; ++u) {
+    f.a[u] = aok[u] ? *reinterpret_cast<const bf16x8*>(ar[u] + ch * 32) : z8;
+    f.b[u] = bok[u] ? *reinterpret_cast<const bf16x8*>(br[u] + ch * 32) : z8;
   }
 }
-__device__ __forceinline__ void wgrad_acc(const float* const (&arow)[2], const float* const (&brow)[2],
-                                          const bool (&aok)[2], const bool (&bok)[2], int nrows, int wv,
-                                          f32x4 (&acc)[2][2]) {
-  const int nch = nrows / 16;
+__device__ __forceinline__ void wg_load(FragF& f, const float* const (&ar)[4], const float* const (&br)[4],
+                                        const bool (&aok)[4], const bool (&bok)[4], int ch) {
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int cb = wv; cb < nch; cb += WG_WAVES * WG_KU) {
-    float4 av[WG_KU][2], bv[WG_KU][2];
 #pragma unroll
-    for (int k = 0; k < WG_KU; ++k) {
-      const int ch = cb + k * WG_WAVES;
-      const bool in = ch < nch;
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        av[k][u] = (in && aok[u]) ? *reinterpret_cast<const float4*>(arow[u] + ch * 16) : z4;
-        bv[k][u] = (in && bok[u]) ? *reinterpret_cast<const float4*>(brow[u] + ch * 16) : z4;
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < WG_KU; ++k)
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int v = 0; v < 2; ++v) {
-          acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[k][u].x, bv[k][v].x, acc[u][v], 0, 0, 0);
-          acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[k][u].y, bv[k][v].y, acc[u][v], 0, 0, 0);
-          acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[k][u].z, bv[k][v].z, acc[u][v], 0, 0, 0);
-          acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[k][u].w, bv[k][v].w, acc[u][v], 0, 0, 0);
-        }
+  for (int u = 0; u < 4; ++u) {
+    f.a[u] = aok[u] ? *reinterpret_cast<const float4*>(ar[u] + ch * 16) : z4;
+    f.b[u] = bok[u] ? *reinterpret_cast<const float4*>(br[u] + ch * 16) : z4;
   }
 }
+__device__ __forceinline__ void wg_mma(const FragB& f, f32x4 (&acc)[4][4]) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[u], f.b[v], acc[u][v], 0, 0, 0);
+}
+__device__ __forceinline__ void wg_mma(const FragF& f, f32x4 (&acc)[4][4]) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x4f32(f.a[u].x, f.b[v].x, acc[u][v], 0, 0, 0);
+      acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x4f32(f.a[u].y, f.b[v].y, acc[u][v], 0, 0, 0);
+      acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x4f32(f.a[u].z, f.b[v].z, acc[u][v], 0, 0, 0);
+      acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x4f32(f.a[u].w, f.b[v].w, acc[u][v], 0, 0, 0);
+    }
+}
+template <typename T> struct FragOf;
+template <> struct FragOf<bf16> { typedef FragB type; };
+template <> struct FragOf<float> { typedef FragF type; };
 
 template <typename T>
-__global__ __launch_bounds__(WG_WAVES * 64) void k_dl_wgrad(DLArgs a, int G1, int scale_by_w) {
-  __shared__ float red[WG_WAVES - 1][16][64];
+__global__ __launch_bounds__(WG4 * 64) void k_dl_wgrad(DLArgs a, int G1, int scale_by_w) {
+  __shared__ float red[WG4 - 1][16 * 4][64];
   __shared__ float s_sw;
+  __shared__ int s_last;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, q = lane >> 4, c = lane & 15;
   const int bst = a.bias_total + 1;
   if (wv == 0) {                  // sum(w) of the batch, fixed order
@@ -502,9 +496,10 @@ __global__ __launch_bounds__(WG_WAVES * 64) void k_dl_wgrad(DLArgs a, int G1, in
   __syncthreads();
   const float sw = s_sw;
   const float inv = scale_by_w ? 1.f / fmaxf(sw, 1e-12f) : 1.f;
+  const int S = a.wsplit;
   const int tiles = a.tile_start[a.L];
-  if ((int)blockIdx.x >= tiles) {
-    const int e = ((int)blockIdx.x - tiles) * WG_WAVES + wv;
+  if ((int)blockIdx.x >= tiles * S) {
+    const int e = ((int)blockIdx.x - tiles * S) * WG4 + wv;
     if (e == 0 && lane == 0 && !scale_by_w && a.gsum) *a.gsum = sw;
     if (e >= a.bias_total) return;
     float sacc = 0.f;
@@ -517,56 +512,90 @@ __global__ __launch_bounds__(WG_WAVES * 64) void k_dl_wgrad(DLArgs a, int G1, in
     }
     return;
   }
-  const int b = blockIdx.x;
+  const int b = (int)blockIdx.x / S, sp = (int)blockIdx.x - b * S;
   int l = 0;
   while (l + 1 < a.L && b >= a.tile_start[l + 1]) ++l;          // GEMM layer l + 1 (0-based l)
   const int bt = b - a.tile_start[l];
   const int ti = bt / a.tiles_j[l], tj = bt - ti * a.tiles_j[l];
   const int ni = a.n[l + 1], nj = a.n[l];
-  const int i0 = ti * 32, j0 = tj * 32;
+  const int i0 = ti * 64, j0 = tj * 64;
   const T* Ab = reinterpret_cast<const T*>(a.dT) + a.d_off[l + 1];
   const T* Bb = reinterpret_cast<const T*>(a.hT) + a.h_off[l];
-  f32x4 acc[2][2];
+  constexpr int CH = sizeof(T) == 2 ? 32 : 16;      // batch rows per chunk
+  constexpr int LPQ = CH / 4;                       // rows per lane quarter
+  f32x4 acc[4][4];
 #pragma unroll
-  for (int u = 0; u < 2; ++u)
+  for (int u = 0; u < 4; ++u)
 #pragma unroll
-    for (int v = 0; v < 2; ++v) acc[u][v] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  constexpr int LPQ = 16 / sizeof(T);     // batch rows per lane quarter and chunk step
-  const T* arow[2];
-  const T* brow[2];
-  bool aok[2], bok[2];
+    for (int v = 0; v < 4; ++v) acc[u][v] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const T* ar[4];
+  const T* br[4];
+  bool aok[4], bok[4];
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
+  for (int u = 0; u < 4; ++u) {
     const int i = i0 + u * 16 + c, j = j0 + u * 16 + c;
     aok[u] = i < ni; bok[u] = j < nj;
-    arow[u] = Ab + (long long)(aok[u] ? i : 0) * a.Bpad + LPQ * q;
-    brow[u] = Bb + (long long)(bok[u] ? j : 0) * a.Bpad + LPQ * q;
+    ar[u] = Ab + (long long)(aok[u] ? i : 0) * a.Bpad + LPQ * q;
+    br[u] = Bb + (long long)(bok[u] ? j : 0) * a.Bpad + LPQ * q;
   }
-  wgrad_acc(arow, brow, aok, bok, a.Bpad, wv, acc);
+  const int nch = a.Bpad / CH;
+  const int c0 = (int)((long long)nch * sp / S), c1 = (int)((long long)nch * (sp + 1) / S);
+  // two-stage pipeline: the next chunk's fragments load while this chunk's MFMAs issue
+  typename FragOf<T>::type f0, f1;
+  int ch = c0 + wv;
+  if (ch < c1) wg_load(f0, ar, br, aok, bok, ch);
+  while (ch < c1) {
+    const int n1 = ch + WG4;
+    if (n1 < c1) wg_load(f1, ar, br, aok, bok, n1);
+    wg_mma(f0, acc);
+    if (n1 >= c1) break;
+    const int n2 = n1 + WG4;
+    if (n2 < c1) wg_load(f0, ar, br, aok, bok, n2);
+    wg_mma(f1, acc);
+    ch = n2;
+  }
+  // the 4 waves' tiles meet in LDS (wave order)
   if (wv > 0) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+    for (int u = 0; u < 4; ++u)
 #pragma unroll
-      for (int v = 0; v < 2; ++v)
+      for (int v = 0; v < 4; ++v)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) red[wv - 1][(u * 2 + v) * 4 + r][lane] = acc[u][v][r];
+        for (int r = 0; r < 4; ++r) red[wv - 1][(u * 4 + v) * 4 + r][lane] = acc[u][v][r];
   }
   __syncthreads();
-  if (wv != 0) return;
+  const long long tile_off = (long long)b * S * 4096;
+  float* mine = a.wpart + tile_off + (long long)sp * 4096;
+  if (wv == 0) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int v = 0; v < 4; ++v)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float t = acc[u][v][r];
+          for (int w = 0; w < WG4 - 1; ++w) t += red[w][(u * 4 + v) * 4 + r][lane];
+          // partial tile element (row 16u + 4q + r, col 16v + c)
+          mine[(u * 16 + 4 * q + r) * 64 + v * 16 + c] = t;
+        }
+    __threadfence();
+    if (lane == 0) s_last = (int)(atomicAdd(a.wcnt + b, 1u) == (unsigned)(S - 1));
+  }
+  __syncthreads();
+  if (!s_last) return;
+  // last arrival for this tile: sum the split partials in split order, write the gradient, reset the counter
+  __threadfence();
+  const float* parts = a.wpart + tile_off;
   float* out = a.g + a.w_off[l];
-#pragma unroll
-  for (int u = 0; u < 2; ++u)
-#pragma unroll
-    for (int v = 0; v < 2; ++v) {
-      const int j = j0 + v * 16 + c;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float t = acc[u][v][r];
-        for (int w = 0; w < WG_WAVES - 1; ++w) t += red[w][(u * 2 + v) * 4 + r][lane];
-        const int i = i0 + u * 16 + 4 * q + r;
-        if (i < ni && j < nj) out[(long long)i * nj + j] = t * inv;
-      }
-    }
+  for (int e = threadIdx.x; e < 4096; e += WG4 * 64) {
+    const int rr = e >> 6, cc = e & 63;
+    const int i = i0 + rr, j = j0 + cc;
+    if (i >= ni || j >= nj) continue;
+    float t = 0.f;
+    for (int s2 = 0; s2 < S; ++s2) t += parts[(long long)s2 * 4096 + e];
+    out[(long long)i * nj + j] = t * inv;
+  }
+  if (threadIdx.x == 0) a.wcnt[b] = 0u;
 }
 
 // WT_l[j][i] = W_l[i][j] for every layer (the bf16 shadow the backward pass reads)
@@ -595,14 +624,15 @@ int h2o_dl_step(const DLArgs* a, int lds, int scale_by_w, hipStream_t s) {
       lds > 160 * 1024)
     return (int)hipErrorInvalidValue;
   const int G1 = a->Bpad / DL_ROWS;
-  const int bias_blocks = (a->bias_total + WG_WAVES - 1) / WG_WAVES;
-  const dim3 gw(a->tile_start[a->L] + bias_blocks);
+  if (a->wsplit < 1 || !a->wpart || !a->wcnt) return (int)hipErrorInvalidValue;
+  const int bias_blocks = (a->bias_total + WG4 - 1) / WG4;
+  const dim3 gw(a->tile_start[a->L] * a->wsplit + bias_blocks);
   if (a->f32) {
     hipLaunchKernelGGL(k_dl_rows<float>, dim3(G1), dim3(DL_THREADS), lds, s, *a);
-    hipLaunchKernelGGL(k_dl_wgrad<float>, gw, dim3(WG_WAVES * 64), 0, s, *a, G1, scale_by_w);
+    hipLaunchKernelGGL(k_dl_wgrad<float>, gw, dim3(WG4 * 64), 0, s, *a, G1, scale_by_w);
   } else {
     hipLaunchKernelGGL(k_dl_rows<bf16>, dim3(G1), dim3(DL_THREADS), lds, s, *a);
-    hipLaunchKernelGGL(k_dl_wgrad<bf16>, gw, dim3(WG_WAVES * 64), 0, s, *a, G1, scale_by_w);
+    hipLaunchKernelGGL(k_dl_wgrad<bf16>, gw, dim3(WG4 * 64), 0, s, *a, G1, scale_by_w);
   }
   return (int)hipGetLastError();
 }

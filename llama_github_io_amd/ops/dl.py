@@ -36,7 +36,8 @@ class _DLArgs(ctypes.Structure):
                  ("lds_off", _ci * (MAXL + 1)), ("lds_g", _ci * 2), ("lds_w", _ci),
                  ("tiles_i", _ci * MAXL), ("tiles_j", _ci * MAXL), ("tile_start", _ci * (MAXL + 1)),
                  ("n_decay", _cll), ("n_total", _cll), ("f32", _ci), ("pad_", _ci),
-                 ("in_drop", _cf), ("lds_lg", _ci), ("in_seed", _cull)])
+                 ("in_drop", _cf), ("lds_lg", _ci), ("in_seed", _cull),
+                 ("wsplit", _ci), ("pad2_", _ci), ("wpart", _vp), ("wcnt", _vp)])
 
 
 nat.register_hip_signatures({"h2o_dl_args_size": [], "h2o_dl_step": [_vp, _ci, _ci, _vp],
@@ -158,11 +159,18 @@ class FusedMLPStep:
         a.in_seed = int(in_seed) & ((1 << 64) - 1)
         ts = 0
         for l in range(L):
-            a.tiles_i[l] = (n[l + 1] + 31) // 32
-            a.tiles_j[l] = (n[l] + 31) // 32
+            a.tiles_i[l] = (n[l + 1] + 63) // 64
+            a.tiles_j[l] = (n[l] + 63) // 64
             a.tile_start[l] = ts
             ts += a.tiles_i[l] * a.tiles_j[l]
         a.tile_start[L] = ts
+        # weight-gradient GEMM: 64 x 64 tiles x `wsplit` batch-row ranges (~768 workgroups of 4 waves), fp32
+        # partial tiles and per-tile arrival counters (the last workgroup of a tile sums and resets)
+        nch = Bpad // (16 if f32 else 32)
+        a.wsplit = max(1, min(nch // 4, -(-768 // ts)))
+        self.wpart = torch.empty(ts * a.wsplit * 4096, dtype=torch.float32, device=dev)
+        self.wcnt = torch.zeros(ts, dtype=torch.int32, device=dev)
+        a.wpart, a.wcnt = self.wpart.data_ptr(), self.wcnt.data_ptr()
         a.n_decay, a.n_total = fp.n_decay, fp.p.numel()
         self.args = a
         self.scale_by_w = out_gsum is None
