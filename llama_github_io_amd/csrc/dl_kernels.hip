@@ -587,13 +587,22 @@ __global__ __launch_bounds__(WG4 * 64) void k_dl_wgrad(DLArgs a, int G1, int sca
   __threadfence();
   const float* parts = a.wpart + tile_off;
   float* out = a.g + a.w_off[l];
-  for (int e = threadIdx.x; e < 4096; e += WG4 * 64) {
-    const int rr = e >> 6, cc = e & 63;
-    const int i = i0 + rr, j = j0 + cc;
-    if (i >= ni || j >= nj) continue;
-    float t = 0.f;
-    for (int s2 = 0; s2 < S; ++s2) t += parts[(long long)s2 * 4096 + e];
-    out[(long long)i * nj + j] = t * inv;
+  // 16 elements per thread, split-outer: each round issues 16 independent loads (a split-inner loop per element
+  // serialised ~S x 16 load latencies in this one workgroup)
+  constexpr int EPT = 4096 / (WG4 * 64);
+  float t[EPT];
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) t[k] = 0.f;
+  for (int s2 = 0; s2 < S; ++s2) {
+    const float* ps = parts + (long long)s2 * 4096 + threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) t[k] += ps[k * WG4 * 64];
+  }
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) {
+    const int e = threadIdx.x + k * WG4 * 64;
+    const int i = i0 + (e >> 6), j = j0 + (e & 63);
+    if (i < ni && j < nj) out[(long long)i * nj + j] = t[k] * inv;
   }
   if (threadIdx.x == 0) a.wcnt[b] = 0u;
 }
