@@ -111,7 +111,12 @@ def native_comm(force: bool = False) -> NativeComm | None:
         c = _comms.get(key)
         if c is not None:
             return c
-        lib = load_rccl()
+        try:
+            lib = load_rccl()
+        except (OSError, RuntimeError) as e:   # no RCCL library (symmetric on every rank): torch's collectives
+            import warnings
+            warnings.warn(f"native RCCL communicator unavailable ({e}); tree exchange through torch.distributed")
+            return None
         uid = _new_uid(lib) if rank == 0 else b""
         if world > 1:
             n = lib.h2o_rccl_id_bytes()
