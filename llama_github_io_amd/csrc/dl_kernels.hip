@@ -64,7 +64,10 @@ struct DLArgs {
   int f32, pad_;                // 1: fp32 operands (Z, W, WT, hT, dT, LDS tiles), 0: bf16
   float in_drop; int lds_lg;    // input dropout ratio; K > 16: byte offset of the fp32 [16][K] logit tile
   unsigned long long in_seed;   // input dropout seed base
-  int wsplit, pad2_;            // k_dl_wgrad: batch-row (GEMM K) splits per 64 x 64 tile
+  int wsplit, maxout;           // k_dl_wgrad: batch-row (GEMM K) splits per 64 x 64 tile; 1: Maxout hidden layers
+  int ng[DL_MAXL + 1];          // GEMM output width of layer l (2 n[l] for Maxout hidden layers: two channels)
+  int kpg[DL_MAXL + 1], ldg[DL_MAXL + 1];   // ng padded to 32, LDS row stride of gradient tiles of width ng
+  int lds_mx[DL_MAXL];          // Maxout: byte offset of layer l's [16][n[l]] winning-channel bytes
   float* wpart;                 // [tiles][wsplit][64 * 64] fp32 partial tiles
   unsigned* wcnt;               // [tiles] arrival counters (zero between steps: the last arrival resets)
 };
@@ -276,15 +279,29 @@ __global__ __launch_bounds__(DL_THREADS) void k_dl_rows(DLArgs a) {
     const uint32_t thr = (uint32_t)(drop * 4294967296.0);
     const uint64_t seed = a.seed_base[l - 1] ^ (step * 0x9E3779B97F4A7C15ULL);
     const int NT = (nout + 15) / 16;
+    unsigned char* win = a.maxout ? smem + a.lds_mx[l] : nullptr;
     for (int t = wv; t < NT; t += DL_NW) {
       const f32x4 acc = tile_mm(Ain, a.ld[l - 1], Wg + a.w_off[l - 1], nin, t * 16, nout, a.kp[l - 1], nin, vec);
+      // Maxout (Neurons.Maxout, 2 channels): channel 1 = weight / bias rows [nout, 2 nout)
+      f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};
+      if (a.maxout)
+        acc1 = tile_mm(Ain, a.ld[l - 1], Wg + a.w_off[l - 1] + (long long)nout * nin, nin, t * 16, nout, a.kp[l - 1], nin,
+                       vec);
       const int col = t * 16 + c;
       f32x4 o;
       if (col < nout) {
         const float b = a.P[a.b_off[l - 1] + col];
+        const float b1 = a.maxout ? a.P[a.b_off[l - 1] + nout + col] : 0.f;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float v = act_f(a.act, acc[r] + b);
+          float v;
+          if (a.maxout) {
+            const float z0 = acc[r] + b, z1 = acc1[r] + b1;
+            v = z1 > z0 ? z1 : z0;
+            win[(4 * q + r) * nout + col] = z1 > z0 ? 1 : 0;
+          } else {
+            v = act_f(a.act, acc[r] + b);
+          }
           if (drop > 0.f) v = dropped(seed, (int64_t)(r0 + 4 * q + r) * nout + col, thr) ? 0.f : v / keep;
           o[r] = v;
           Aout[(4 * q + r) * a.ld[l] + col] = from_f<T>(v);
@@ -373,7 +390,9 @@ __global__ __launch_bounds__(DL_THREADS) void k_dl_rows(DLArgs a) {
   int ldg_in = a.ld[L];
   for (int l = L - 1; l >= 1; --l) {
     T* Gout = S + a.lds_g[l & 1];
-    const int nout = a.n[l], nnext = a.n[l + 1];
+    const int nout = a.n[l], nnext = a.ng[l + 1];     // layer l+1's GEMM width (its WT rows)
+    const int ldo = a.ldg[l];
+    const unsigned char* win = a.maxout ? smem + a.lds_mx[l] : nullptr;
     const bool vec = (nnext % VE == 0) && (a.w_off[l] % VE == 0);
     const float drop = a.drop[l - 1], keep = 1.f - drop;
     const uint32_t thr = (uint32_t)(drop * 4294967296.0);
@@ -382,7 +401,7 @@ __global__ __launch_bounds__(DL_THREADS) void k_dl_rows(DLArgs a) {
     const int NT = (nout + 15) / 16;
     for (int t = wv; t < NT; t += DL_NW) {
       // dh = G_{l+1} W_{l+1}: B[k = unit of l+1][n = unit of l] = WT_{l+1}[n][k]
-      const f32x4 acc = tile_mm(Gin, ldg_in, WTg + a.w_off[l], nnext, t * 16, nout, a.kp[l + 1], nnext, vec);
+      const f32x4 acc = tile_mm(Gin, ldg_in, WTg + a.w_off[l], nnext, t * 16, nout, a.kpg[l + 1], nnext, vec);
       const int col = t * 16 + c;
       f32x4 gd = {0.f, 0.f, 0.f, 0.f};
       if (col < nout) {
@@ -396,26 +415,55 @@ __global__ __launch_bounds__(DL_THREADS) void k_dl_rows(DLArgs a) {
             gg = d ? 0.f : gg / keep;
             y = d ? 0.f : y * keep;
           }
-          gd[r] = gg * dact_from_y(a.act, y);
+          gd[r] = a.maxout ? gg : gg * dact_from_y(a.act, y);
         }
       }
+      if (!a.maxout) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) Gout[(4 * q + r) * a.ld[l] + col] = from_f<T>(gd[r]);
-      const float cs = col_sum(gd);
-      if (col < nout) {
-        if (q == 0) a.bpart[(long long)blockIdx.x * (a.bias_total + 1) + a.bias_off[l] + col] = cs;
-        store4T(dTg + a.d_off[l] + (long long)col * a.Bpad + r0 + 4 * q, gd);
+        for (int r = 0; r < 4; ++r) Gout[(4 * q + r) * ldo + col] = from_f<T>(gd[r]);
+        const float cs = col_sum(gd);
+        if (col < nout) {
+          if (q == 0) a.bpart[(long long)blockIdx.x * (a.bias_total + 1) + a.bias_off[l] + col] = cs;
+          store4T(dTg + a.d_off[l] + (long long)col * a.Bpad + r0 + 4 * q, gd);
+        }
+      } else {
+        // the gradient flows to the winning channel only: GEMM columns col (channel 0) and nout + col (channel 1)
+        f32x4 g0, g1;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool w1 = col < nout && win[(4 * q + r) * nout + col] != 0;
+          g0[r] = w1 ? 0.f : gd[r];
+          g1[r] = w1 ? gd[r] : 0.f;
+        }
+        const float cs0 = col_sum(g0), cs1 = col_sum(g1);
+        if (col < nout) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            Gout[(4 * q + r) * ldo + col] = from_f<T>(g0[r]);
+            Gout[(4 * q + r) * ldo + nout + col] = from_f<T>(g1[r]);
+          }
+          if (q == 0) {
+            a.bpart[(long long)blockIdx.x * (a.bias_total + 1) + a.bias_off[l] + col] = cs0;
+            a.bpart[(long long)blockIdx.x * (a.bias_total + 1) + a.bias_off[l] + nout + col] = cs1;
+          }
+          store4T(dTg + a.d_off[l] + (long long)col * a.Bpad + r0 + 4 * q, g0);
+          store4T(dTg + a.d_off[l] + (long long)(nout + col) * a.Bpad + r0 + 4 * q, g1);
+        }
       }
     }
     __syncthreads();
-    // zero the K padding of the gradient tile the next layer reads
-    for (int i = tid; i < DL_ROWS * (a.kp[l] - NT * 16); i += DL_THREADS) {
-      const int rr = i / (a.kp[l] - NT * 16), cc = NT * 16 + i % (a.kp[l] - NT * 16);
-      Gout[rr * a.ld[l] + cc] = from_f<T>(0.f);
+    // zero the K padding of the gradient tile the next layer reads (columns past the written ones)
+    {
+      const int w0 = a.maxout ? 2 * nout : NT * 16;
+      const int wz = a.kpg[l] - w0;
+      for (int i = tid; i < DL_ROWS * wz; i += DL_THREADS) {
+        const int rr = i / wz, cc = w0 + i % wz;
+        Gout[rr * ldo + cc] = from_f<T>(0.f);
+      }
     }
     __syncthreads();
     Gin = Gout;
-    ldg_in = a.ld[l];
+    ldg_in = ldo;
   }
   if (tid == 0) {
     float s = 0.f;
@@ -517,7 +565,7 @@ __global__ __launch_bounds__(WG4 * 64) void k_dl_wgrad(DLArgs a, int G1, int sca
   while (l + 1 < a.L && b >= a.tile_start[l + 1]) ++l;          // GEMM layer l + 1 (0-based l)
   const int bt = b - a.tile_start[l];
   const int ti = bt / a.tiles_j[l], tj = bt - ti * a.tiles_j[l];
-  const int ni = a.n[l + 1], nj = a.n[l];
+  const int ni = a.ng[l + 1], nj = a.n[l];
   const int i0 = ti * 64, j0 = tj * 64;
   const T* Ab = reinterpret_cast<const T*>(a.dT) + a.d_off[l + 1];
   const T* Bb = reinterpret_cast<const T*>(a.hT) + a.h_off[l];
@@ -617,7 +665,7 @@ __global__ __launch_bounds__(256) void k_dl_transpose(DLArgs a) {
     while (l + 1 < a.L && e >= a.w_off[l + 1]) ++l;
     const long long o = e - a.w_off[l];
     const int nin = a.n[l], i = (int)(o / nin), j = (int)(o - (long long)i * nin);
-    WT[a.w_off[l] + (long long)j * a.n[l + 1] + i] = W[e];
+    WT[a.w_off[l] + (long long)j * a.ng[l + 1] + i] = W[e];
   }
 }
 

@@ -440,8 +440,9 @@ class DeepLearningTrainer:
         fused_shape = (dev.type == "cuda" and os.environ.get("H2O_DL_FUSED", "1") == "1" and net.act in ACT
                        and (Z.dtype == torch.bfloat16 or os.environ.get("H2O_DL_FUSED_F32", "1") == "1")
                        and dlops.supported(int(Z.shape[1]), [int(h_) for h_ in hidden], int(net.out.weight.shape[0]),
-                                           ACT[net.act], Z))
-        explicit = (os.environ.get("H2O_DL_EXPLICIT", "1") == "1" and not ae and not maxout
+                                           ACT[net.act], Z, maxout))
+        # Maxout and input dropout run in the fused step only (the library-GEMM explicit step has neither)
+        explicit = (os.environ.get("H2O_DL_EXPLICIT", "1") == "1" and not ae and (not maxout or fused_shape)
                     and (in_drop == 0 or fused_shape) and net.act in ACT
                     and ((cat in ("Binomial", "Multinomial") and dist in ("bernoulli", "multinomial")
                           and lname in ("automatic", "crossentropy", "cross_entropy"))
@@ -450,7 +451,8 @@ class DeepLearningTrainer:
             # reproducible=True (bit-identical seeded runs): the library-GEMM explicit step accumulates bias
             # gradients with float atomics; only the fused step (fixed-order reductions) or autograd qualify
             if not (dev.type == "cuda" and os.environ.get("H2O_DL_FUSED", "1") == "1" and dlops.supported(
-                    int(Z.shape[1]), [int(h_) for h_ in hidden], int(net.out.weight.shape[0]), ACT[net.act], Z)):
+                    int(Z.shape[1]), [int(h_) for h_ in hidden], int(net.out.weight.shape[0]), ACT[net.act], Z,
+                    maxout)):
                 explicit = False
         shadow = None
         if explicit:
@@ -510,7 +512,7 @@ class DeepLearningTrainer:
         if (explicit and os.environ.get("H2O_DL_FUSED", "1") == "1"
                 and (cdt == torch.bfloat16 or os.environ.get("H2O_DL_FUSED_F32", "1") == "1")
                 and dlops.supported(int(Z.shape[1]), [int(h_) for h_ in hidden], int(net.out.weight.shape[0]),
-                                    act_code, Z)):
+                                    act_code, Z, maxout)):
             fz["ok"] = True
             fz["bases"] = [(dseed * 1000003 + i * 7919) & ((1 << 62) - 1) for i in range(len(net.hidden))]
 
@@ -519,7 +521,7 @@ class DeepLearningTrainer:
             gsum = gbuf[-1:] if gsync else None
             fz["obj"] = dlops.FusedMLPStep(fp, list(net.hidden) + [net.out], act_code, list(net.hid_drop),
                                            fz["bases"], Z, wf, yt, cat == "Regression", cap, shadow, step_t, gout,
-                                           gsum, in_drop, (dseed * 1000003 + 104729) & ((1 << 62) - 1))
+                                           gsum, in_drop, (dseed * 1000003 + 104729) & ((1 << 62) - 1), maxout)
             fz["obj"].refresh_transposed()
             fz["sridx"] = torch.full((cap,), -1, dtype=torch.long, device=dev)
 

@@ -37,7 +37,8 @@ class _DLArgs(ctypes.Structure):
                  ("tiles_i", _ci * MAXL), ("tiles_j", _ci * MAXL), ("tile_start", _ci * (MAXL + 1)),
                  ("n_decay", _cll), ("n_total", _cll), ("f32", _ci), ("pad_", _ci),
                  ("in_drop", _cf), ("lds_lg", _ci), ("in_seed", _cull),
-                 ("wsplit", _ci), ("pad2_", _ci), ("wpart", _vp), ("wcnt", _vp)])
+                 ("wsplit", _ci), ("maxout", _ci), ("ng", _ci * (MAXL + 1)), ("kpg", _ci * (MAXL + 1)),
+                 ("ldg", _ci * (MAXL + 1)), ("lds_mx", _ci * MAXL), ("wpart", _vp), ("wcnt", _vp)])
 
 
 nat.register_hip_signatures({"h2o_dl_args_size": [], "h2o_dl_step": [_vp, _ci, _ci, _vp],
@@ -53,7 +54,7 @@ def _pad(esz: int) -> int:
     return 16 // esz
 
 
-def supported(n_in: int, hidden, n_out: int, act_code: int, Z: torch.Tensor) -> bool:
+def supported(n_in: int, hidden, n_out: int, act_code: int, Z: torch.Tensor, maxout: bool = False) -> bool:
     """Shapes the fused step handles (else the library-GEMM explicit step runs): bf16 or fp32 operands."""
     L = len(hidden) + 1
     if not Z.is_cuda or Z.dtype not in (torch.bfloat16, torch.float32) or L > MAXL or n_out > MAXK or \
@@ -62,8 +63,10 @@ def supported(n_in: int, hidden, n_out: int, act_code: int, Z: torch.Tensor) -> 
     esz = Z.element_size()
     pd = _pad(esz)
     widths = [n_in] + list(hidden)
+    gw = max([(2 if maxout else 1) * h for h in hidden] or [1])
     lds = (sum(ROWS * (_r32(n) + pd) * esz for n in widths) + ROWS * (_r32(n_out) + pd) * esz
-           + 2 * ROWS * (_r32(max(hidden or [1])) + pd) * esz + 64 + (ROWS * n_out * 4 if n_out > 16 else 0))
+           + 2 * ROWS * (_r32(gw) + pd) * esz + 64 + (ROWS * n_out * 4 if n_out > 16 else 0)
+           + (ROWS * sum(hidden) + 16 * L if maxout else 0))
     return lds <= 150 * 1024 and max(widths) <= 8192
 
 
@@ -76,12 +79,14 @@ class FusedMLPStep:
 
     def __init__(self, fp, lins, act_code: int, drops, seed_bases, Z: torch.Tensor, w: torch.Tensor, y: torch.Tensor,
                  regression: bool, cap: int, shadow: torch.Tensor, step_dev: torch.Tensor, out_grad: torch.Tensor,
-                 out_gsum: torch.Tensor | None, in_drop: float = 0.0, in_seed: int = 0):
+                 out_gsum: torch.Tensor | None, in_drop: float = 0.0, in_seed: int = 0, maxout: bool = False):
         self.lib = nat.hip()
         assert self.lib.h2o_dl_args_size() == ctypes.sizeof(_DLArgs), "DLArgs layout mismatch"
         dev = Z.device
         L = len(lins)
-        n = [lins[0].weight.shape[1]] + [l_.weight.shape[0] for l_ in lins]
+        # n: activation widths; ng: GEMM output widths (Maxout hidden layers hold 2 channels of n[l] rows each)
+        ng = [lins[0].weight.shape[1]] + [l_.weight.shape[0] for l_ in lins]
+        n = [ng[0]] + [(g // 2 if (maxout and l < L - 1) else g) for l, g in enumerate(ng[1:])]
         Bpad = (cap + ROWS * 8 - 1) // (ROWS * 8) * (ROWS * 8)      # multiple of 128
         base = fp.p.data_ptr()
         esz = fp.p.element_size()
@@ -105,10 +110,14 @@ class FusedMLPStep:
             a.n[i] = v
             a.kp[i] = _r32(v)
             a.ld[i] = _r32(v) + _pad(cesz)
+            a.ng[i] = ng[i]
+            a.kpg[i] = _r32(ng[i])
+            a.ldg[i] = _r32(ng[i]) + _pad(cesz)
+        a.maxout = int(bool(maxout))
         bias_off, bt = [0] * (MAXL + 1), 0
         for l in range(1, L + 1):
             bias_off[l] = bt
-            bt += n[l]
+            bt += ng[l]
         for l, lin in enumerate(lins):
             a.w_off[l] = (lin.weight.data_ptr() - base) // esz
             a.b_off[l] = (lin.bias.data_ptr() - base) // esz
@@ -127,7 +136,7 @@ class FusedMLPStep:
         do = [0]
         for l in range(1, L + 1):
             do.append(o)
-            o += n[l] * Bpad
+            o += ng[l] * Bpad
         self.T = torch.zeros(o, dtype=cdt, device=dev)
         for l in range(L):
             a.h_off[l] = ho[l]
@@ -146,11 +155,15 @@ class FusedMLPStep:
             off += ROWS * a.ld[l]
         a.lds_off[L] = off
         off += ROWS * a.ld[L]
-        gl = max([a.ld[l] for l in range(1, L)] or [8])
+        gl = max([a.ldg[l] for l in range(1, L)] or [8])
         a.lds_g[0], a.lds_g[1] = off, off + ROWS * gl
         off += 2 * ROWS * gl
         a.lds_w = off * cesz
         self.lds = a.lds_w + ROWS * 4
+        if maxout:                     # winning-channel bytes of every hidden layer
+            for l in range(1, L):
+                a.lds_mx[l] = self.lds
+                self.lds += (ROWS * n[l] + 15) // 16 * 16
         if n[L] > 16:                  # fp32 [16][K] logits of the wide softmax (16-byte aligned)
             assert not regression and n[L] <= MAXK
             a.lds_lg = (self.lds + 15) // 16 * 16
@@ -159,7 +172,7 @@ class FusedMLPStep:
         a.in_seed = int(in_seed) & ((1 << 64) - 1)
         ts = 0
         for l in range(L):
-            a.tiles_i[l] = (n[l + 1] + 63) // 64
+            a.tiles_i[l] = (ng[l + 1] + 63) // 64
             a.tiles_j[l] = (n[l] + 63) // 64
             a.tile_start[l] = ts
             ts += a.tiles_i[l] * a.tiles_j[l]
@@ -178,7 +191,7 @@ class FusedMLPStep:
         import numpy as _np
         self.wt_map = (self.WT, _np.ascontiguousarray([a.w_off[l] for l in range(L)] + [fp.n_decay], dtype=_np.int64),
                        _np.ascontiguousarray(n[:L], dtype=_np.int32),
-                       _np.ascontiguousarray(n[1:L + 1], dtype=_np.int32))
+                       _np.ascontiguousarray(ng[1:L + 1], dtype=_np.int32))
         self._keep = (Z, w, y, wsrc, step_dev, out_grad, out_gsum)
 
     def step(self, ridx: torch.Tensor) -> None:

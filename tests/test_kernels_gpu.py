@@ -408,7 +408,7 @@ def test_segment_sum_kernel_matches_index_add(n, idt, vdt):
     assert got.dtype == torch.float64 and torch.allclose(got, ref, rtol=1e-12, atol=1e-9)
 
 
-def _fused_case(n_in, hidden, K, act, drops, regression, B, seed=0, f32=False, in_drop=0.0):
+def _fused_case(n_in, hidden, K, act, drops, regression, B, seed=0, f32=False, in_drop=0.0, maxout=False):
     """One fused MFMA step (csrc/dl_kernels.hip) and the fp32 autograd gradient of the same weighted loss
     (bf16 path: weights and inputs rounded to bf16 like the kernels' operands; f32: the fp32 master weights and
     inputs, v_mfma_f32_16x16x4_f32; dropout masks from ops.dense._mask_ref)."""
@@ -417,7 +417,7 @@ def _fused_case(n_in, hidden, K, act, drops, regression, B, seed=0, f32=False, i
     from llama_github_io_amd.ops.dense import FlatParams, _act, _mask_ref, step_seed
     g = torch.Generator(device="cpu").manual_seed(seed)
     actn = {1: "rectifier", 2: "tanh"}[act]
-    net = MLP(n_in, hidden, K, actn, False, 0.0, drops, "UniformAdaptive", 1.0, g).to(dev)
+    net = MLP(n_in, hidden, K, actn, maxout, 0.0, drops, "UniformAdaptive", 1.0, g).to(dev)
     fp = FlatParams(net)
     with torch.no_grad():
         fp.p.add_(0.05 * torch.randn(fp.p.shape, generator=g).to(dev))   # non-trivial biases
@@ -432,7 +432,7 @@ def _fused_case(n_in, hidden, K, act, drops, regression, B, seed=0, f32=False, i
     bases = [1234567 + 31 * i for i in range(len(hidden))]
     in_seed = 99991
     fs = dlops.FusedMLPStep(fp, list(net.hidden) + [net.out], act, drops, bases, Z, w, y, regression, B, shadow,
-                            step_t, fp.g, None, in_drop, in_seed)
+                            step_t, fp.g, None, in_drop, in_seed, maxout)
     fs.refresh_transposed()
     fp.g.zero_()
     fs.step(ridx)
@@ -449,7 +449,11 @@ def _fused_case(n_in, hidden, K, act, drops, regression, B, seed=0, f32=False, i
         if not f32:                  # the bf16 kernels round the scaled inputs to bf16
             h = h.to(torch.bfloat16).float()
     for i in range(len(hidden)):
-        h = _act(act, h @ Ws[i].T + Bs[i])
+        if maxout:                   # two channels: weight / bias rows [0, u) and [u, 2u)
+            z = h @ Ws[i].T + Bs[i]
+            h = torch.maximum(z[:, :hidden[i]], z[:, hidden[i]:])
+        else:
+            h = _act(act, h @ Ws[i].T + Bs[i])
         if drops[i] > 0:
             m = _mask_ref((B, hidden[i]), drops[i], step_seed(bases[i], 7), dev)
             h = torch.where(m, h / (1 - drops[i]), torch.zeros_like(h))
@@ -471,6 +475,7 @@ def _fused_case(n_in, hidden, K, act, drops, regression, B, seed=0, f32=False, i
         ow = (l_.weight.data_ptr() - fp.p.data_ptr()) // 4
         n_o, n_i = l_.weight.shape
         assert torch.equal(fs.WT[ow: ow + n_o * n_i].view(n_i, n_o), wsrc[ow: ow + n_o * n_i].view(n_o, n_i).T)
+    assert int(fs.wcnt.abs().sum()) == 0             # every split-K tile counter was reset by its last arrival
     return got, ref
 
 
@@ -600,3 +605,33 @@ def test_dl_trainer_fused_multinomial_input_dropout(monkeypatch):
         assert bool(m.output["training_step_fused_mfma"]) == (flag == "1")
         acc[flag] = 1 - m.output["training_metrics"]["mean_per_class_error"]
     assert acc["1"] > 0.15 and abs(acc["1"] - acc["0"]) < 0.08, acc     # chance: 1/30
+
+
+@pytest.mark.parametrize("f32", [False, True])
+@pytest.mark.parametrize("n_in,hidden,K,drops", [
+    (784, [200, 200], 2, [0.0, 0.0]),   # Maxout on the BASELINE shape
+    (37, [48, 24], 3, [0.2, 0.0]),      # ragged widths (channel blocks not multiples of 16), hidden dropout
+    (20, [40, 16, 8], 30, [0.0, 0.1, 0.0]),
+])
+def test_dl_fused_step_maxout_matches_fp32_autograd(n_in, hidden, K, drops, f32):
+    """Maxout hidden layers (Neurons.Maxout, 2 channels): the winning channel takes the gradient."""
+    got, ref = _fused_case(n_in, hidden, K, 1, drops, False, 256, f32=f32, maxout=True)
+    rel = float((got - ref).norm() / ref.norm())
+    assert rel < (1e-4 if f32 else 3e-2), rel
+
+
+def test_dl_trainer_maxout_runs_fused(monkeypatch):
+    """activation='Maxout' trains through the fused step and matches the autograd path's AUC."""
+    from llama_github_io_amd.models.deeplearning import DeepLearningTrainer
+    g = torch.Generator(device=dev).manual_seed(4)
+    X = torch.rand(50, 30000, device=dev, generator=g)
+    y = (X[:8].sum(0) > 4).float()
+    res = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("H2O_DL_FUSED", flag)
+        m = DeepLearningTrainer(dict(hidden=[32, 32], activation="Maxout", epochs=3, mini_batch_size=512, seed=2,
+                                     stopping_rounds=0, score_interval=1e9)).fit(X, y, None, None, _info(50))
+        res[flag] = m
+    assert res["1"].output["training_step_fused_mfma"] and not res["0"].output["training_step_fused_mfma"]
+    a1, a0 = res["1"].output["training_metrics"]["AUC"], res["0"].output["training_metrics"]["AUC"]
+    assert a1 > 0.85 and abs(a1 - a0) < 0.05, (a1, a0)
