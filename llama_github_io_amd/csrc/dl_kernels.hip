@@ -68,8 +68,8 @@ struct DLArgs {
   int ng[DL_MAXL + 1];          // GEMM output width of layer l (2 n[l] for Maxout hidden layers: two channels)
   int kpg[DL_MAXL + 1], ldg[DL_MAXL + 1];   // ng padded to 32, LDS row stride of gradient tiles of width ng
   int lds_mx[DL_MAXL];          // Maxout: byte offset of layer l's [16][n[l]] winning-channel bytes
-  float* wpart;                 // [tiles][wsplit][64 * 64] fp32 partial tiles
-  unsigned* wcnt;               // [tiles] arrival counters (zero between steps: the last arrival resets)
+  float* wpart;                 // [tiles][wsplit][64 * 64] fp32 partial tiles, then the batch's 1 / sum(w)
+  unsigned* wcnt;               // (unused)
 };
 
 __device__ __forceinline__ uint32_t hash32(uint64_t x) {
@@ -480,8 +480,8 @@ __global__ __launch_bounds__(DL_THREADS) void k_dl_rows(DLArgs a) {
 // (both operands contiguous along the batch rows = GEMM K). One 64 x 64 output tile per (tile, split) workgroup of
 // 4 waves: the batch rows are cut into `wsplit` ranges (enough workgroups to fill the chip) and each wave takes
 // every 4th chunk of its workgroup's range with all 16 MFMA tiles of the 64 x 64 block in registers (per chunk 4 A
-// and 4 B fragments feed 16 MFMAs). The 4 waves meet in LDS in wave order, the split partials in a global buffer;
-// the workgroup arriving last for a tile sums them in split order (deterministic) into the gradient.
+// and 4 B fragments feed 16 MFMAs). The 4 waves meet in LDS in wave order, the split partials in a global buffer,
+// and k_dl_wsum sums them in split order (deterministic) into the gradient.
 // MEASURED (r4): 32 x 32 tiles re-read every operand row 7-25 times from L2 (225 MB per fp32 step, 92 us).
 // bf16: 32-row chunks, 8 rows per lane quarter (v_mfma_f32_16x16x32_bf16); fp32: 16-row chunks, 4 rows per lane
 // quarter and 4 v_mfma_f32_16x16x4_f32 each.
@@ -532,23 +532,26 @@ template <typename T>
 __global__ __launch_bounds__(WG4 * 64) void k_dl_wgrad(DLArgs a, int G1, int scale_by_w) {
   __shared__ float red[WG4 - 1][16 * 4][64];
   __shared__ float s_sw;
-  __shared__ int s_last;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, q = lane >> 4, c = lane & 15;
   const int bst = a.bias_total + 1;
-  if (wv == 0) {                  // sum(w) of the batch, fixed order
-    float sacc = 0.f;
-    for (int g = lane; g < G1; g += 64) sacc += a.bpart[(long long)g * bst + a.bias_total];
-    for (int o = 32; o > 0; o >>= 1) sacc += __shfl_xor(sacc, o, 64);
-    if (lane == 0) s_sw = sacc;
-  }
-  __syncthreads();
-  const float sw = s_sw;
-  const float inv = scale_by_w ? 1.f / fmaxf(sw, 1e-12f) : 1.f;
   const int S = a.wsplit;
   const int tiles = a.tile_start[a.L];
   if ((int)blockIdx.x >= tiles * S) {
+    // trailing workgroups: sum(w) of the batch (fixed order) and the bias gradients
+    if (wv == 0) {
+      float sacc = 0.f;
+      for (int g = lane; g < G1; g += 64) sacc += a.bpart[(long long)g * bst + a.bias_total];
+      for (int o = 32; o > 0; o >>= 1) sacc += __shfl_xor(sacc, o, 64);
+      if (lane == 0) s_sw = sacc;
+    }
+    __syncthreads();
+    const float sw = s_sw;
+    const float inv = scale_by_w ? 1.f / fmaxf(sw, 1e-12f) : 1.f;
     const int e = ((int)blockIdx.x - tiles * S) * WG4 + wv;
-    if (e == 0 && lane == 0 && !scale_by_w && a.gsum) *a.gsum = sw;
+    if (e == 0 && lane == 0) {
+      a.wpart[(long long)tiles * S * 4096] = inv;          // for k_dl_wsum
+      if (!scale_by_w && a.gsum) *a.gsum = sw;
+    }
     if (e >= a.bias_total) return;
     float sacc = 0.f;
     for (int g = lane; g < G1; g += 64) sacc += a.bpart[(long long)g * bst + e];
@@ -626,34 +629,30 @@ __global__ __launch_bounds__(WG4 * 64) void k_dl_wgrad(DLArgs a, int G1, int sca
           // partial tile element (row 16u + 4q + r, col 16v + c)
           mine[(u * 16 + 4 * q + r) * 64 + v * 16 + c] = t;
         }
-    __threadfence();
-    if (lane == 0) s_last = (int)(atomicAdd(a.wcnt + b, 1u) == (unsigned)(S - 1));
   }
-  __syncthreads();
-  if (!s_last) return;
-  // last arrival for this tile: sum the split partials in split order, write the gradient, reset the counter
-  __threadfence();
-  const float* parts = a.wpart + tile_off;
-  float* out = a.g + a.w_off[l];
-  // 16 elements per thread, split-outer: each round issues 16 independent loads (a split-inner loop per element
-  // serialised ~S x 16 load latencies in this one workgroup)
-  constexpr int EPT = 4096 / (WG4 * 64);
-  float t[EPT];
-#pragma unroll
-  for (int k = 0; k < EPT; ++k) t[k] = 0.f;
-  for (int s2 = 0; s2 < S; ++s2) {
-    const float* ps = parts + (long long)s2 * 4096 + threadIdx.x;
-#pragma unroll
-    for (int k = 0; k < EPT; ++k) t[k] += ps[k * WG4 * 64];
-  }
-#pragma unroll
-  for (int k = 0; k < EPT; ++k) {
-    const int e = threadIdx.x + k * WG4 * 64;
-    const int i = i0 + (e >> 6), j = j0 + (e & 63);
-    if (i < ni && j < nj) out[(long long)i * nj + j] = t[k] * inv;
-  }
-  if (threadIdx.x == 0) a.wcnt[b] = 0u;
 }
+
+// dW = (sum over the split partials in split order) * inv, one thread per tile element (the next launch on the
+// stream sees every partial: no cross-workgroup fences — an agent-scope release per workgroup wrote back L2)
+__global__ __launch_bounds__(256) void k_dl_wsum(DLArgs a) {
+  const int S = a.wsplit;
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  const int b = (int)(e >> 12), el = (int)(e & 4095);
+  if (b >= a.tile_start[a.L]) return;
+  const float inv = a.wpart[(long long)a.tile_start[a.L] * S * 4096];   // 1 / sum(w) or 1 (k_dl_wgrad)
+  int l = 0;
+  while (l + 1 < a.L && b >= a.tile_start[l + 1]) ++l;
+  const int bt = b - a.tile_start[l];
+  const int ti = bt / a.tiles_j[l], tj = bt - ti * a.tiles_j[l];
+  const int i = ti * 64 + (el >> 6), j = tj * 64 + (el & 63);
+  const int ni = a.ng[l + 1], nj = a.n[l];
+  if (i >= ni || j >= nj) return;
+  const float* ps = a.wpart + (long long)b * S * 4096 + el;
+  float t = 0.f;
+  for (int s2 = 0; s2 < S; ++s2) t += ps[(long long)s2 * 4096];
+  a.g[a.w_off[l] + (long long)i * nj + j] = t * inv;
+}
+
 
 // WT_l[j][i] = W_l[i][j] for every layer (the bf16 shadow the backward pass reads)
 template <typename T>
@@ -681,15 +680,18 @@ int h2o_dl_step(const DLArgs* a, int lds, int scale_by_w, hipStream_t s) {
       lds > 160 * 1024)
     return (int)hipErrorInvalidValue;
   const int G1 = a->Bpad / DL_ROWS;
-  if (a->wsplit < 1 || !a->wpart || !a->wcnt) return (int)hipErrorInvalidValue;
+  if (a->wsplit < 1 || !a->wpart) return (int)hipErrorInvalidValue;
+  const unsigned gsum_blocks = (unsigned)(((long long)a->tile_start[a->L] * 4096 + 255) / 256);
   const int bias_blocks = (a->bias_total + WG4 - 1) / WG4;
   const dim3 gw(a->tile_start[a->L] * a->wsplit + bias_blocks);
   if (a->f32) {
     hipLaunchKernelGGL(k_dl_rows<float>, dim3(G1), dim3(DL_THREADS), lds, s, *a);
     hipLaunchKernelGGL(k_dl_wgrad<float>, gw, dim3(WG4 * 64), 0, s, *a, G1, scale_by_w);
+    hipLaunchKernelGGL(k_dl_wsum, dim3(gsum_blocks), dim3(256), 0, s, *a);
   } else {
     hipLaunchKernelGGL(k_dl_rows<bf16>, dim3(G1), dim3(DL_THREADS), lds, s, *a);
     hipLaunchKernelGGL(k_dl_wgrad<bf16>, gw, dim3(WG4 * 64), 0, s, *a, G1, scale_by_w);
+    hipLaunchKernelGGL(k_dl_wsum, dim3(gsum_blocks), dim3(256), 0, s, *a);
   }
   return (int)hipGetLastError();
 }

@@ -177,11 +177,11 @@ class FusedMLPStep:
             a.tile_start[l] = ts
             ts += a.tiles_i[l] * a.tiles_j[l]
         a.tile_start[L] = ts
-        # weight-gradient GEMM: 64 x 64 tiles x `wsplit` batch-row ranges (~768 workgroups of 4 waves), fp32
-        # partial tiles and per-tile arrival counters (the last workgroup of a tile sums and resets)
+        # weight-gradient GEMM: 64 x 64 tiles x `wsplit` batch-row ranges (~768 workgroups of 4 waves) into fp32
+        # partial tiles, summed in split order by k_dl_wsum
         nch = Bpad // (16 if f32 else 32)
         a.wsplit = max(1, min(nch // 4, -(-768 // ts)))
-        self.wpart = torch.empty(ts * a.wsplit * 4096, dtype=torch.float32, device=dev)
+        self.wpart = torch.empty(ts * a.wsplit * 4096 + 1, dtype=torch.float32, device=dev)
         self.wcnt = torch.zeros(ts, dtype=torch.int32, device=dev)
         a.wpart, a.wcnt = self.wpart.data_ptr(), self.wcnt.data_ptr()
         a.n_decay, a.n_total = fp.n_decay, fp.p.numel()
