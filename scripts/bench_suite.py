@@ -129,6 +129,8 @@ def bench_automl(a, dev, world, rank):
                value=len(lb), unit="models", n_gpus=world, seconds=dt, budget_secs=a.budget, rows=n, cols=F,
                leader=str(lb.iloc[0, 0]), leader_auc=float(lb.iloc[0, 1]),
                mojo_max_abs_diff=float(np.max(np.abs(pa - pb))), algos=sorted({str(m).split("_")[0] for m in lb.iloc[:, 0]}),
+               leaderboard=[{k: (float(v) if isinstance(v, (int, float, np.floating)) else str(v)) for k, v in r.items()}
+                            for r in lb.head(30).to_dict(orient="records")],
                data="synthetic"))
 
 
