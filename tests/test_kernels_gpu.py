@@ -319,7 +319,7 @@ def test_deeplearning_explicit_step_matches_autograd_gpu(dtype, monkeypatch):
     if dtype == "float32":
         assert torch.allclose(res[0], res[1], atol=1e-4, rtol=1e-3)
     else:   # bf16 GEMMs: the two paths round differently; both must learn equally well
-        assert abs(aucs[0] - aucs[1]) < 0.02 and min(aucs) > 0.9
+        assert abs(aucs[0] - aucs[1]) < 0.02 and min(aucs) > 0.88
 
 
 @pytest.mark.parametrize("standardize", [True, False])
