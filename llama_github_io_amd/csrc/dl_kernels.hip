@@ -68,6 +68,7 @@ struct DLArgs {
   int ng[DL_MAXL + 1];          // GEMM output width of layer l (2 n[l] for Maxout hidden layers: two channels)
   int kpg[DL_MAXL + 1], ldg[DL_MAXL + 1];   // ng padded to 32, LDS row stride of gradient tiles of width ng
   int lds_mx[DL_MAXL];          // Maxout: byte offset of layer l's [16][n[l]] winning-channel bytes
+  int ae, pad3_;                 // 1: autoencoder (outputs reconstruct the undropped inputs, quadratic loss / K)
   float* wpart;                 // [tiles][wsplit][64 * 64] fp32 partial tiles, then the batch's 1 / sum(w)
   unsigned* wcnt;               // (unused)
 };
@@ -218,7 +219,8 @@ __global__ __launch_bounds__(DL_THREADS) void k_dl_rows(DLArgs a) {
     const long long g = r < a.B ? a.ridx[r] : -1;
     srow[tid] = g;
     ws[tid] = g >= 0 ? a.w[g] : 0.f;
-    if (a.regression) sy[tid] = g >= 0 ? a.yreg[g] : 0.f;
+    if (a.ae) scls[tid] = -1;
+    else if (a.regression) sy[tid] = g >= 0 ? a.yreg[g] : 0.f;
     else scls[tid] = g >= 0 ? a.ycls[g] : -1;
   }
   // zero every activation / gradient tile (K padding must read as zeros)
@@ -329,7 +331,19 @@ __global__ __launch_bounds__(DL_THREADS) void k_dl_rows(DLArgs a) {
       }
     }
     __syncthreads();
-    if (wv < DL_ROWS) {
+    if (wv < DL_ROWS && a.ae) {
+      // autoencoder: d/do of sum_k (o_k - x_k)^2 / K times the row weight (x: the input row before dropout)
+      const int row = wv;
+      float* lg = LG + row * K;
+      const float wr = ws[row];
+      const long long gr = srow[row];
+      const T* xr = Zg + (gr < 0 ? 0 : gr) * a.ldz;
+      for (int k = lane; k < K; k += 64) {
+        const float gk = gr < 0 ? 0.f : 2.f * (lg[k] - to_f(xr[k])) * wr / (float)K;
+        lg[k] = gk;
+        GO[row * a.ld[L] + k] = from_f<T>(gk);
+      }
+    } else if (wv < DL_ROWS) {
       const int row = wv;
       float* lg = LG + row * K;
       float mx = -INFINITY;
@@ -368,7 +382,10 @@ __global__ __launch_bounds__(DL_THREADS) void k_dl_rows(DLArgs a) {
       const int row = 4 * q + r;
       const float o = cok ? acc[r] + b : -INFINITY;
       const float wr = ws[row];
-      if (a.regression) {
+      if (a.ae) {
+        const long long gr = srow[row];
+        g[r] = (cok && gr >= 0) ? 2.f * (o - to_f(Zg[gr * a.ldz + c])) * wr / (float)K : 0.f;
+      } else if (a.regression) {
         g[r] = (c == 0) ? (o - sy[row]) * wr : 0.f;
       } else {
         float mx = o;
@@ -676,7 +693,7 @@ int h2o_dl_args_size() { return (int)sizeof(DLArgs); }
 
 // lds: bytes of dynamic LDS for k_dl_rows (activation + gradient tiles + row weights)
 int h2o_dl_step(const DLArgs* a, int lds, int scale_by_w, hipStream_t s) {
-  if (a->L < 1 || a->L > DL_MAXL || (a->K > 16 && (a->regression || a->lds_lg <= 0)) || a->Bpad % 128 != 0 ||
+  if (a->L < 1 || a->L > DL_MAXL || (a->K > 16 && ((a->regression && !a->ae) || a->lds_lg <= 0)) || a->Bpad % 128 != 0 ||
       lds > 160 * 1024)
     return (int)hipErrorInvalidValue;
   const int G1 = a->Bpad / DL_ROWS;

@@ -442,11 +442,14 @@ class DeepLearningTrainer:
                        and dlops.supported(int(Z.shape[1]), [int(h_) for h_ in hidden], int(net.out.weight.shape[0]),
                                            ACT[net.act], Z, maxout))
         # Maxout and input dropout run in the fused step only (the library-GEMM explicit step has neither)
-        explicit = (os.environ.get("H2O_DL_EXPLICIT", "1") == "1" and not ae and (not maxout or fused_shape)
-                    and (in_drop == 0 or fused_shape) and net.act in ACT
+        # the autoencoder (quadratic reconstruction loss, no sparsity penalty) runs in the fused step only
+        ae_fused = ae and fused_shape and not sparse and lname in ("automatic", "quadratic")
+        explicit = (os.environ.get("H2O_DL_EXPLICIT", "1") == "1" and (not ae or ae_fused)
+                    and (not maxout or fused_shape) and (in_drop == 0 or fused_shape) and net.act in ACT
                     and ((cat in ("Binomial", "Multinomial") and dist in ("bernoulli", "multinomial")
                           and lname in ("automatic", "crossentropy", "cross_entropy"))
-                         or (cat == "Regression" and dist == "gaussian" and lname in ("automatic", "quadratic"))))
+                         or (cat == "Regression" and dist == "gaussian" and lname in ("automatic", "quadratic"))
+                         or ae_fused))
         if explicit and p.get("reproducible"):
             # reproducible=True (bit-identical seeded runs): the library-GEMM explicit step accumulates bias
             # gradients with float atomics; only the fused step (fixed-order reductions) or autograd qualify
@@ -521,7 +524,8 @@ class DeepLearningTrainer:
             gsum = gbuf[-1:] if gsync else None
             fz["obj"] = dlops.FusedMLPStep(fp, list(net.hidden) + [net.out], act_code, list(net.hid_drop),
                                            fz["bases"], Z, wf, yt, cat == "Regression", cap, shadow, step_t, gout,
-                                           gsum, in_drop, (dseed * 1000003 + 104729) & ((1 << 62) - 1), maxout)
+                                           gsum, in_drop, (dseed * 1000003 + 104729) & ((1 << 62) - 1), maxout,
+                                           ae)
             fz["obj"].refresh_transposed()
             fz["sridx"] = torch.full((cap,), -1, dtype=torch.long, device=dev)
 

@@ -38,7 +38,8 @@ class _DLArgs(ctypes.Structure):
                  ("n_decay", _cll), ("n_total", _cll), ("f32", _ci), ("pad_", _ci),
                  ("in_drop", _cf), ("lds_lg", _ci), ("in_seed", _cull),
                  ("wsplit", _ci), ("maxout", _ci), ("ng", _ci * (MAXL + 1)), ("kpg", _ci * (MAXL + 1)),
-                 ("ldg", _ci * (MAXL + 1)), ("lds_mx", _ci * MAXL), ("wpart", _vp), ("wcnt", _vp)])
+                 ("ldg", _ci * (MAXL + 1)), ("lds_mx", _ci * MAXL), ("ae", _ci), ("pad3_", _ci),
+                 ("wpart", _vp), ("wcnt", _vp)])
 
 
 nat.register_hip_signatures({"h2o_dl_args_size": [], "h2o_dl_step": [_vp, _ci, _ci, _vp],
@@ -79,7 +80,8 @@ class FusedMLPStep:
 
     def __init__(self, fp, lins, act_code: int, drops, seed_bases, Z: torch.Tensor, w: torch.Tensor, y: torch.Tensor,
                  regression: bool, cap: int, shadow: torch.Tensor, step_dev: torch.Tensor, out_grad: torch.Tensor,
-                 out_gsum: torch.Tensor | None, in_drop: float = 0.0, in_seed: int = 0, maxout: bool = False):
+                 out_gsum: torch.Tensor | None, in_drop: float = 0.0, in_seed: int = 0, maxout: bool = False,
+                 autoencoder: bool = False):
         self.lib = nat.hip()
         assert self.lib.h2o_dl_args_size() == ctypes.sizeof(_DLArgs), "DLArgs layout mismatch"
         dev = Z.device
@@ -93,7 +95,9 @@ class FusedMLPStep:
         a = _DLArgs()
         a.Z, a.ldz, a.B, a.Bpad = Z.data_ptr(), Z.stride(0), int(cap), int(Bpad)
         a.w = w.data_ptr()
-        if regression:
+        if autoencoder:               # the targets are the input rows themselves
+            a.ycls, a.yreg, a.regression, a.ae = 0, 0, 1, 1
+        elif regression:
             a.yreg, a.ycls, a.regression = y.data_ptr(), 0, 1
         else:
             a.ycls, a.yreg, a.regression = y.data_ptr(), 0, 0
@@ -165,7 +169,7 @@ class FusedMLPStep:
                 a.lds_mx[l] = self.lds
                 self.lds += (ROWS * n[l] + 15) // 16 * 16
         if n[L] > 16:                  # fp32 [16][K] logits of the wide softmax (16-byte aligned)
-            assert not regression and n[L] <= MAXK
+            assert (autoencoder or not regression) and n[L] <= MAXK
             a.lds_lg = (self.lds + 15) // 16 * 16
             self.lds = a.lds_lg + ROWS * n[L] * 4
         a.in_drop = float(in_drop)

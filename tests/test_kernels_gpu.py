@@ -408,7 +408,7 @@ def test_segment_sum_kernel_matches_index_add(n, idt, vdt):
     assert got.dtype == torch.float64 and torch.allclose(got, ref, rtol=1e-12, atol=1e-9)
 
 
-def _fused_case(n_in, hidden, K, act, drops, regression, B, seed=0, f32=False, in_drop=0.0, maxout=False):
+def _fused_case(n_in, hidden, K, act, drops, regression, B, seed=0, f32=False, in_drop=0.0, maxout=False, ae=False):
     """One fused MFMA step (csrc/dl_kernels.hip) and the fp32 autograd gradient of the same weighted loss
     (bf16 path: weights and inputs rounded to bf16 like the kernels' operands; f32: the fp32 master weights and
     inputs, v_mfma_f32_16x16x4_f32; dropout masks from ops.dense._mask_ref)."""
@@ -431,8 +431,8 @@ def _fused_case(n_in, hidden, K, act, drops, regression, B, seed=0, f32=False, i
     step_t = torch.full((1,), 7, dtype=torch.int64, device=dev)
     bases = [1234567 + 31 * i for i in range(len(hidden))]
     in_seed = 99991
-    fs = dlops.FusedMLPStep(fp, list(net.hidden) + [net.out], act, drops, bases, Z, w, y, regression, B, shadow,
-                            step_t, fp.g, None, in_drop, in_seed, maxout)
+    fs = dlops.FusedMLPStep(fp, list(net.hidden) + [net.out], act, drops, bases, Z, w, None if ae else y, regression,
+                            B, shadow, step_t, fp.g, None, in_drop, in_seed, maxout, ae)
     fs.refresh_transposed()
     fp.g.zero_()
     fs.step(ridx)
@@ -459,7 +459,9 @@ def _fused_case(n_in, hidden, K, act, drops, regression, B, seed=0, f32=False, i
             h = torch.where(m, h / (1 - drops[i]), torch.zeros_like(h))
     o = h @ Ws[-1].T + Bs[-1]
     wb = w[ridx]
-    if regression:
+    if ae:                           # reconstruction of the (undropped) inputs, quadratic loss / n_out
+        loss = (wb[:, None] * (o - Z[ridx].float()) ** 2).sum() / o.shape[1] / wb.sum()
+    elif regression:
         loss = (wb * 0.5 * (o[:, 0] - y[ridx]) ** 2).sum() / wb.sum()
     else:
         loss = (wb * torch.nn.functional.cross_entropy(o, y[ridx], reduction="none")).sum() / wb.sum()
@@ -634,3 +636,30 @@ def test_dl_trainer_maxout_runs_fused(monkeypatch):
     assert res["1"].output["training_step_fused_mfma"] and not res["0"].output["training_step_fused_mfma"]
     a1, a0 = res["1"].output["training_metrics"]["AUC"], res["0"].output["training_metrics"]["AUC"]
     assert a1 > 0.85 and abs(a1 - a0) < 0.05, (a1, a0)
+
+
+@pytest.mark.parametrize("f32", [True])
+@pytest.mark.parametrize("n_in,hidden,in_drop", [(12, [8], 0.0), (60, [32, 16, 32], 0.1), (120, [48], 0.0)])
+def test_dl_fused_autoencoder_matches_fp32_autograd(n_in, hidden, in_drop, f32):
+    """Autoencoder outputs (K = n_in, narrow and wide output paths) reconstruct the undropped inputs."""
+    got, ref = _fused_case(n_in, hidden, n_in, 2, [0.0] * len(hidden), True, 256, f32=f32, in_drop=in_drop, ae=True)
+    rel = float((got - ref).norm() / ref.norm())
+    assert rel < 1e-4, rel
+
+
+def test_dl_trainer_autoencoder_runs_fused(monkeypatch):
+    from llama_github_io_amd.models.deeplearning import DeepLearningTrainer
+    g = torch.Generator(device=dev).manual_seed(6)
+    Zl = torch.randn(4, 20000, device=dev, generator=g)
+    M = torch.randn(36, 4, device=dev, generator=g)
+    X = torch.cat([Zl, M @ Zl], 0)                       # 40 columns of rank 4
+    res = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("H2O_DL_FUSED", flag)
+        m = DeepLearningTrainer(dict(hidden=[16, 4, 16], autoencoder=True, activation="Tanh", epochs=4,
+                                     mini_batch_size=256, seed=1, stopping_rounds=0, score_interval=1e9)).fit(
+            X, None, None, None, _info(40, None))
+        res[flag] = m
+    assert res["1"].output["training_step_fused_mfma"] and not res["0"].output["training_step_fused_mfma"]
+    e1, e0 = res["1"].output["training_metrics"]["MSE"], res["0"].output["training_metrics"]["MSE"]
+    assert e1 < 0.5 and abs(e1 - e0) < 0.25 * max(e0, e1), (e1, e0)
