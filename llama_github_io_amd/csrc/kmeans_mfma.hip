@@ -45,10 +45,20 @@ __device__ __forceinline__ float bfly_min_idx(float v, int& idx, int mask) {
 // each 32-lane half fall on (nearly) distinct banks — P + 1 = 21 left 25 % of the LDS-active cycles in bank
 // conflicts (PMC, profiles/r3_session2_kmeans_c31.md). Kept only while three 4-wave blocks still fit a CU's
 // LDS (the VGPR-bound occupancy).
+#ifndef KM_VEC
+#define KM_VEC 0
+#endif
+// KM_VEC: stride P or P + 4 with P / 4 odd — rows 16-byte aligned (one ds_write_b128 per staged float4 group
+// instead of four ds_write_b32) and the distance GEMM's reads (c16 * Pp + 4 s + q: c16 * Pp / 4 distinct mod 16)
+// still on 64 distinct banks
 __host__ __device__ inline int km_stride(int P) {
+#if KM_VEC
+  return ((P / 4) & 1) ? P : P + 4;
+#else
   int pp = P + 1;
   const int adj = pp + ((17 - pp % 32) + 32) % 32;
   return adj <= 52 ? adj : pp;
+#endif
 }
 template <int KT, int PS, int PT>
 __global__ __launch_bounds__(256) void k_lloyd_mfma(const float* __restrict__ X, int64_t N, int P,
@@ -130,7 +140,11 @@ __global__ __launch_bounds__(256) void k_lloyd_mfma(const float* __restrict__ X,
     for (int i = 0; i < PS; ++i) {
       if (doff[i] >= 0) {
         float* dst = xs + doff[i];
+#if KM_VEC
+        *reinterpret_cast<float4*>(dst) = pf[i];
+#else
         dst[0] = pf[i].x; dst[1] = pf[i].y; dst[2] = pf[i].z; dst[3] = pf[i].w;
+#endif
       }
     }
     wsl[lane] = pwt;
