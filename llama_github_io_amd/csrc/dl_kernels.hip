@@ -70,7 +70,6 @@ struct DLArgs {
   int lds_mx[DL_MAXL];          // Maxout: byte offset of layer l's [16][n[l]] winning-channel bytes
   int ae, pad3_;                 // 1: autoencoder (outputs reconstruct the undropped inputs, quadratic loss / K)
   float* wpart;                 // [tiles][wsplit][64 * 64] fp32 partial tiles, then the batch's 1 / sum(w)
-  unsigned* wcnt;               // (unused)
 };
 
 __device__ __forceinline__ uint32_t hash32(uint64_t x) {

@@ -39,7 +39,7 @@ class _DLArgs(ctypes.Structure):
                  ("in_drop", _cf), ("lds_lg", _ci), ("in_seed", _cull),
                  ("wsplit", _ci), ("maxout", _ci), ("ng", _ci * (MAXL + 1)), ("kpg", _ci * (MAXL + 1)),
                  ("ldg", _ci * (MAXL + 1)), ("lds_mx", _ci * MAXL), ("ae", _ci), ("pad3_", _ci),
-                 ("wpart", _vp), ("wcnt", _vp)])
+                 ("wpart", _vp)])
 
 
 nat.register_hip_signatures({"h2o_dl_args_size": [], "h2o_dl_step": [_vp, _ci, _ci, _vp],
@@ -186,8 +186,7 @@ class FusedMLPStep:
         nch = Bpad // (16 if f32 else 32)
         a.wsplit = max(1, min(nch // 4, -(-768 // ts)))
         self.wpart = torch.empty(ts * a.wsplit * 4096 + 1, dtype=torch.float32, device=dev)
-        self.wcnt = torch.zeros(ts, dtype=torch.int32, device=dev)
-        a.wpart, a.wcnt = self.wpart.data_ptr(), self.wcnt.data_ptr()
+        a.wpart = self.wpart.data_ptr()
         a.n_decay, a.n_total = fp.n_decay, fp.p.numel()
         self.args = a
         self.scale_by_w = out_gsum is None
