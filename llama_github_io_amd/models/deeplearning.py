@@ -528,14 +528,6 @@ class DeepLearningTrainer:
                                            ae)
             fz["obj"].refresh_transposed()
             fz["sridx"] = torch.full((cap,), -1, dtype=torch.long, device=dev)
-            if fz.get("hogwild"):
-                # a second step object on the same parameters (shared transposed weights), own gradient buffer
-                fz["g2"] = torch.zeros_like(fp.g)
-                fz["obj2"] = dlops.FusedMLPStep(fp, list(net.hidden) + [net.out], act_code, list(net.hid_drop),
-                                                fz["bases"], Z, wf, yt, cat == "Regression", cap, shadow, step_t,
-                                                fz["g2"], None, in_drop,
-                                                (dseed * 1000003 + 104729) & ((1 << 62) - 1), maxout, ae,
-                                                wt=fz["obj"].WT)
 
         if fz["ok"]:
             fwd_bwd_lib = fwd_bwd
@@ -608,13 +600,6 @@ class DeepLearningTrainer:
         # rows from the resident design matrix included) are captured in ONE graph and replayed per chunk — the
         # host issues one index copy, one arange and one replay per CH steps instead of ~40 kernels per step.
         CH = max(1, int(os.environ.get("H2O_DL_CHUNK", "16"))) if (use_graph and not gsync) else 1
-        # Hogwild (the reference's default asynchronous updates, reproducible=False): two mini-batches in flight on
-        # two streams over the same parameters, each step's ADADELTA update landing whenever it completes — the
-        # latency-bound fused steps of one batch overlap the other's. Fused ADADELTA steps only.
-        fz["hogwild"] = (fz["ok"] and CH > 1 and CH % 2 == 0 and adaptive and not elastic and not gsync
-                         and max_w2 == float("inf") and not p.get("reproducible")
-                         and os.environ.get("H2O_DL_HOGWILD", "0") == "1")
-        hw_stream = torch.cuda.Stream(dev) if fz["hogwild"] else None
         chunk = dict(g=None)
         if CH > 1:
             ridx = torch.zeros(CH * B, dtype=torch.long, device=dev)
@@ -624,19 +609,6 @@ class DeepLearningTrainer:
             on_v = torch.zeros(CH, dtype=torch.float32, device=dev)
 
             def chunk_body():
-                if fz.get("hogwild") and fz.get("obj2") is not None:
-                    main = torch.cuda.current_stream(dev)
-                    hw_stream.wait_stream(main)
-                    for k in range(0, CH, 2):
-                        for j, (obj, gb, st) in enumerate(((fz["obj"], fp.g, main), (fz["obj2"], fz["g2"], hw_stream))):
-                            with torch.cuda.stream(st):
-                                obj.args.step_dev = step_v[k + j:k + j + 1].data_ptr()
-                                obj.step(ridx[(k + j) * B:(k + j + 1) * B])
-                                with torch.no_grad():
-                                    fp.adadelta(rho, eps, l1, l2, shadow, obj.wt_map, g=gb)
-                    main.wait_stream(hw_stream)
-                    net.step_dev = step_t
-                    return
                 for k in range(CH):
                     r = ridx[k * B:(k + 1) * B]
                     net.step_dev = step_v[k:k + 1]

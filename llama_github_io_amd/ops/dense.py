@@ -59,12 +59,10 @@ class FlatParams:
     def zero_grad(self):
         self.g.zero_()
 
-    def adadelta(self, rho, eps, l1=0.0, l2=0.0, shadow=None, wt=None, g=None):
+    def adadelta(self, rho, eps, l1=0.0, l2=0.0, shadow=None, wt=None):
         """``shadow`` (bf16 [n_decay], optional): also written with the updated weights (the bf16 copies the
         explicit MLP step multiplies with). ``wt``: (tensor, layer offsets, n_in, n_out) — the transposed
-        weight copy of the fused DL step, written in the same launch (ops/dl.py FusedMLPStep.wt_map). ``g``: the
-        gradient buffer to apply (default ``self.g``)."""
-        g = self.g if g is None else g
+        weight copy of the fused DL step, written in the same launch (ops/dl.py FusedMLPStep.wt_map)."""
         if self.p.is_cuda:
             if wt is None:
                 wtp, f32, L, o, i, u = 0, 0, 0, 0, 0, 0
@@ -72,11 +70,11 @@ class FlatParams:
                 t, o_, i_, u_ = wt
                 wtp, f32, L = t.data_ptr(), int(t.dtype == torch.float32), len(i_)
                 o, i, u = o_.ctypes.data, i_.ctypes.data, u_.ctypes.data     # host arrays, copied at launch
-            call("h2o_adadelta", self.p.data_ptr(), g.data_ptr(), self.eg2.data_ptr(), self.edx2.data_ptr(),
+            call("h2o_adadelta", self.p.data_ptr(), self.g.data_ptr(), self.eg2.data_ptr(), self.edx2.data_ptr(),
                  self.p.numel(), self.n_decay, float(rho), float(eps), float(l1), float(l2),
                  0 if shadow is None else shadow.data_ptr(), wtp, f32, L, o, i, u, stream_ptr(self.p.device))
             return
-        g = g.clone()
+        g = self.g.clone()
         w = slice(0, self.n_decay)
         g[w] += l2 * self.p[w] + l1 * torch.sign(self.p[w])
         self.eg2.mul_(rho).addcmul_(g, g, value=1 - rho)

@@ -81,7 +81,7 @@ class FusedMLPStep:
     def __init__(self, fp, lins, act_code: int, drops, seed_bases, Z: torch.Tensor, w: torch.Tensor, y: torch.Tensor,
                  regression: bool, cap: int, shadow: torch.Tensor, step_dev: torch.Tensor, out_grad: torch.Tensor,
                  out_gsum: torch.Tensor | None, in_drop: float = 0.0, in_seed: int = 0, maxout: bool = False,
-                 autoencoder: bool = False, wt: torch.Tensor | None = None):
+                 autoencoder: bool = False):
         self.lib = nat.hip()
         assert self.lib.h2o_dl_args_size() == ctypes.sizeof(_DLArgs), "DLArgs layout mismatch"
         dev = Z.device
@@ -106,8 +106,7 @@ class FusedMLPStep:
         cdt = torch.float32 if f32 else torch.bfloat16
         cesz = 4 if f32 else 2
         wsrc = fp.p[: fp.n_decay] if f32 else shadow
-        # wt: share another step object's transposed weights (concurrent steps on the same parameters)
-        self.WT = torch.empty_like(wsrc) if wt is None else wt
+        self.WT = torch.empty_like(wsrc)
         a.P, a.W, a.WT, a.step_dev = base, wsrc.data_ptr(), self.WT.data_ptr(), step_dev.data_ptr()
         a.f32 = int(f32)
         a.L, a.K, a.act = L, n[L], int(act_code)
