@@ -108,6 +108,13 @@ struct WTMap {
   int f32, L;
   long long w_off[7];
   int n_in[6], n_out[6];
+  // the weight gradients straight from the fused step's split partials (dl_kernels.hip k_dl_wgrad): element
+  // (r, c) of layer l sums partial[tile(l, r / 64, c / 64)][s][(r % 64) * 64 + c % 64] over the S splits, times
+  // the batch's 1 / sum(w) at wpart[inv_off] (the separate split-sum launch and the g round trip are skipped)
+  const float* wpart;
+  int S, pad_;
+  long long inv_off;
+  int tile_start[7], tiles_j[6];
 };
 
 __global__ __launch_bounds__(256) void k_adadelta(float* __restrict__ p, const float* __restrict__ g,
@@ -116,7 +123,25 @@ __global__ __launch_bounds__(256) void k_adadelta(float* __restrict__ p, const f
                                                   __hip_bfloat16* __restrict__ shadow, WTMap tm) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const float pi = p[i];
-    float gi = g[i];
+    // layer, row and column of a weight (the split-partial read and the transposed write)
+    int l = 0;
+    int64_t r = 0, c = 0;
+    if ((tm.wt || tm.wpart) && i < n_decay) {
+      while (l + 1 < tm.L && i >= tm.w_off[l + 1]) ++l;
+      const int64_t o = i - tm.w_off[l];
+      r = o / tm.n_in[l];
+      c = o - r * tm.n_in[l];
+    }
+    float gi;
+    if (tm.wpart && i < n_decay) {
+      const int64_t b = tm.tile_start[l] + (r >> 6) * tm.tiles_j[l] + (c >> 6);
+      const float* ps = tm.wpart + b * tm.S * 4096 + ((r & 63) << 6) + (c & 63);
+      float t = 0.f;
+      for (int s2 = 0; s2 < tm.S; ++s2) t += ps[(int64_t)s2 * 4096];
+      gi = t * tm.wpart[tm.inv_off];
+    } else {
+      gi = g[i];
+    }
     if (i < n_decay) gi += l2 * pi + (pi > 0.f ? l1 : (pi < 0.f ? -l1 : 0.f));
     const float e = rho * eg2[i] + (1.f - rho) * gi * gi;
     const float d = -sqrtf(edx2[i] + eps) / sqrtf(e + eps) * gi;
@@ -125,11 +150,6 @@ __global__ __launch_bounds__(256) void k_adadelta(float* __restrict__ p, const f
     p[i] = pi + d;
     if (shadow && i < n_decay) shadow[i] = __float2bfloat16(pi + d);   // bf16 weights for the next GEMMs
     if (tm.wt && i < n_decay) {
-      int l = 0;
-      while (l + 1 < tm.L && i >= tm.w_off[l + 1]) ++l;
-      const int64_t o = i - tm.w_off[l];
-      const int nin = tm.n_in[l];
-      const int64_t r = o / nin, c = o - r * nin;
       const int64_t t = tm.w_off[l] + c * tm.n_out[l] + r;
       if (tm.f32) ((float*)tm.wt)[t] = pi + d;
       else ((__hip_bfloat16*)tm.wt)[t] = __float2bfloat16(pi + d);
@@ -257,7 +277,8 @@ int h2o_num_transform(const float* X, long long N, const int* rows, int nf, cons
 // wt (nullable): transposed copy to write along (tm_off/tm_in/tm_out: L layers' offsets and shapes)
 int h2o_adadelta(float* p, const float* g, float* eg2, float* edx2, long long n, long long n_decay, float rho, float eps,
                  float l1, float l2, void* shadow, void* wt, int wt_f32, int L, const long long* tm_off,
-                 const int* tm_in, const int* tm_out, hipStream_t stream) {
+                 const int* tm_in, const int* tm_out, const float* wpart, int S, long long inv_off,
+                 const int* tile_start, const int* tiles_j, hipStream_t stream) {
   long long grid = (n + 255) / 256;
   if (grid > 4096) grid = 4096;
   if (grid < 1) grid = 1;
@@ -266,6 +287,11 @@ int h2o_adadelta(float* p, const float* g, float* eg2, float* edx2, long long n,
     if (L < 1 || L > 6) return (int)hipErrorInvalidValue;
     tm.wt = wt; tm.f32 = wt_f32; tm.L = L;
     for (int l = 0; l < L; ++l) { tm.w_off[l] = tm_off[l]; tm.n_in[l] = tm_in[l]; tm.n_out[l] = tm_out[l]; }
+    if (wpart) {
+      tm.wpart = wpart; tm.S = S; tm.inv_off = inv_off;
+      for (int l = 0; l <= L; ++l) tm.tile_start[l] = tile_start[l];
+      for (int l = 0; l < L; ++l) tm.tiles_j[l] = tiles_j[l];
+    }
   }
   hipLaunchKernelGGL(k_adadelta, dim3((unsigned)grid), dim3(256), 0, stream, p, g, eg2, edx2, (int64_t)n,
                      (int64_t)n_decay, rho, eps, l1, l2, (__hip_bfloat16*)shadow, tm);

@@ -68,7 +68,8 @@ struct DLArgs {
   int ng[DL_MAXL + 1];          // GEMM output width of layer l (2 n[l] for Maxout hidden layers: two channels)
   int kpg[DL_MAXL + 1], ldg[DL_MAXL + 1];   // ng padded to 32, LDS row stride of gradient tiles of width ng
   int lds_mx[DL_MAXL];          // Maxout: byte offset of layer l's [16][n[l]] winning-channel bytes
-  int ae, pad3_;                 // 1: autoencoder (outputs reconstruct the undropped inputs, quadratic loss / K)
+  int ae, no_wsum;               // 1: autoencoder (outputs reconstruct the undropped inputs, quadratic loss / K);
+                                // no_wsum: the optimizer reads the split partials itself (no k_dl_wsum launch)
   float* wpart;                 // [tiles][wsplit][64 * 64] fp32 partial tiles, then the batch's 1 / sum(w)
 };
 
@@ -703,11 +704,11 @@ int h2o_dl_step(const DLArgs* a, int lds, int scale_by_w, hipStream_t s) {
   if (a->f32) {
     hipLaunchKernelGGL(k_dl_rows<float>, dim3(G1), dim3(DL_THREADS), lds, s, *a);
     hipLaunchKernelGGL(k_dl_wgrad<float>, gw, dim3(WG4 * 64), 0, s, *a, G1, scale_by_w);
-    hipLaunchKernelGGL(k_dl_wsum, dim3(gsum_blocks), dim3(256), 0, s, *a);
+    if (!a->no_wsum) hipLaunchKernelGGL(k_dl_wsum, dim3(gsum_blocks), dim3(256), 0, s, *a);
   } else {
     hipLaunchKernelGGL(k_dl_rows<bf16>, dim3(G1), dim3(DL_THREADS), lds, s, *a);
     hipLaunchKernelGGL(k_dl_wgrad<bf16>, gw, dim3(WG4 * 64), 0, s, *a, G1, scale_by_w);
-    hipLaunchKernelGGL(k_dl_wsum, dim3(gsum_blocks), dim3(256), 0, s, *a);
+    if (!a->no_wsum) hipLaunchKernelGGL(k_dl_wsum, dim3(gsum_blocks), dim3(256), 0, s, *a);
   }
   return (int)hipGetLastError();
 }

@@ -407,7 +407,7 @@ class DeepLearningTrainer:
                 fobj = fz.get("obj")
                 if adaptive:      # ADADELTA (Neurons.java: rho, epsilon); also refreshes the bf16 weights and
                     # (fused step) the transposed copy its backward pass reads
-                    fp.adadelta(rho, eps, l1, l2, shadow, None if fobj is None else fobj.wt_map)
+                    fp.adadelta(rho, eps, l1, l2, shadow, None if fobj is None else fz["wt"])
                 else:
                     gg = fp.g.clone()
                     nd = fp.n_decay
@@ -528,6 +528,13 @@ class DeepLearningTrainer:
                                            ae)
             fz["obj"].refresh_transposed()
             fz["sridx"] = torch.full((cap,), -1, dtype=torch.long, device=dev)
+            # nothing but ADADELTA reads the weight gradient (no all-reduce, no elastic pull): the update sums
+            # the fused step's split partials itself (one launch fewer per step)
+            if (adaptive and not gsync and not (elastic and ea_lam > 0)
+                    and os.environ.get("H2O_DL_FUSE_WSUM", "1") == "1"):
+                fz["wt"] = fz["obj"].optimizer_reads_partials()
+            else:
+                fz["wt"] = fz["obj"].wt_map
 
         if fz["ok"]:
             fwd_bwd_lib = fwd_bwd

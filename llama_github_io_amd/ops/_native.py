@@ -72,7 +72,7 @@ _HIP_SIGS = {
 # Bumped whenever a C launcher's argument list changes; every native library exports h2o_abi_version()
 # (csrc/abi.h) and a library built from older sources is refused instead of being called with shifted
 # arguments.
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 
 def _check_abi(lib, name: str) -> None:

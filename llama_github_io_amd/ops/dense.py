@@ -25,7 +25,8 @@ nat.register_hip_signatures({
                         nat.c_void_p, nat.c_void_p, nat.c_void_p],
     "h2o_adadelta": [nat.c_void_p, nat.c_void_p, nat.c_void_p, nat.c_void_p, nat.c_ll, nat.c_ll, nat.ctypes.c_float,
                      nat.ctypes.c_float, nat.ctypes.c_float, nat.ctypes.c_float, nat.c_void_p, nat.c_void_p, nat.c_int,
-                     nat.c_int, nat.c_void_p, nat.c_void_p, nat.c_void_p, nat.c_void_p],
+                     nat.c_int, nat.c_void_p, nat.c_void_p, nat.c_void_p, nat.c_void_p, nat.c_int, nat.c_ll,
+                     nat.c_void_p, nat.c_void_p, nat.c_void_p],
     "h2o_out_grad": [nat.c_void_p, nat.c_void_p, nat.c_void_p, nat.c_void_p, nat.c_void_p, nat.c_ll, nat.c_int,
                      nat.c_void_p, nat.c_void_p, nat.c_int, nat.c_void_p],
 })
@@ -64,15 +65,20 @@ class FlatParams:
         explicit MLP step multiplies with). ``wt``: (tensor, layer offsets, n_in, n_out) — the transposed
         weight copy of the fused DL step, written in the same launch (ops/dl.py FusedMLPStep.wt_map)."""
         if self.p.is_cuda:
+            wpp, S, inv_off, ts, tj = 0, 0, 0, 0, 0
             if wt is None:
                 wtp, f32, L, o, i, u = 0, 0, 0, 0, 0, 0
             else:
-                t, o_, i_, u_ = wt
+                t, o_, i_, u_ = wt[:4]
                 wtp, f32, L = t.data_ptr(), int(t.dtype == torch.float32), len(i_)
                 o, i, u = o_.ctypes.data, i_.ctypes.data, u_.ctypes.data     # host arrays, copied at launch
+                if len(wt) > 4:       # weight gradients from the fused step's split partials
+                    wpp, S, inv_off = wt[4].data_ptr(), int(wt[5]), int(wt[6])
+                    ts, tj = wt[7].ctypes.data, wt[8].ctypes.data
             call("h2o_adadelta", self.p.data_ptr(), self.g.data_ptr(), self.eg2.data_ptr(), self.edx2.data_ptr(),
                  self.p.numel(), self.n_decay, float(rho), float(eps), float(l1), float(l2),
-                 0 if shadow is None else shadow.data_ptr(), wtp, f32, L, o, i, u, stream_ptr(self.p.device))
+                 0 if shadow is None else shadow.data_ptr(), wtp, f32, L, o, i, u, wpp, S, inv_off, ts, tj,
+                 stream_ptr(self.p.device))
             return
         g = self.g.clone()
         w = slice(0, self.n_decay)

@@ -38,7 +38,7 @@ class _DLArgs(ctypes.Structure):
                  ("n_decay", _cll), ("n_total", _cll), ("f32", _ci), ("pad_", _ci),
                  ("in_drop", _cf), ("lds_lg", _ci), ("in_seed", _cull),
                  ("wsplit", _ci), ("maxout", _ci), ("ng", _ci * (MAXL + 1)), ("kpg", _ci * (MAXL + 1)),
-                 ("ldg", _ci * (MAXL + 1)), ("lds_mx", _ci * MAXL), ("ae", _ci), ("pad3_", _ci),
+                 ("ldg", _ci * (MAXL + 1)), ("lds_mx", _ci * MAXL), ("ae", _ci), ("no_wsum", _ci),
                  ("wpart", _vp)])
 
 
@@ -195,7 +195,17 @@ class FusedMLPStep:
         self.wt_map = (self.WT, _np.ascontiguousarray([a.w_off[l] for l in range(L)] + [fp.n_decay], dtype=_np.int64),
                        _np.ascontiguousarray(n[:L], dtype=_np.int32),
                        _np.ascontiguousarray(ng[1:L + 1], dtype=_np.int32))
+        self._tile_start = _np.ascontiguousarray([a.tile_start[l] for l in range(L + 1)], dtype=_np.int32)
+        self._tiles_j = _np.ascontiguousarray([a.tiles_j[l] for l in range(L)], dtype=_np.int32)
         self._keep = (Z, w, y, wsrc, step_dev, out_grad, out_gsum)
+
+    def optimizer_reads_partials(self) -> tuple:
+        """Skip the split-sum launch: the fused ADADELTA update sums the weight-gradient partials itself (the
+        weight part of the gradient buffer is then never written). Returns the optimizer's ``wt`` argument."""
+        self.args.no_wsum = 1
+        a = self.args
+        return self.wt_map + (self.wpart, int(a.wsplit), int(a.tile_start[a.L]) * int(a.wsplit) * 4096,
+                              self._tile_start, self._tiles_j)
 
     def step(self, ridx: torch.Tensor) -> None:
         """One forward/backward of the rows ``ridx`` (int64; -1 = padding row) into the gradient buffer."""
