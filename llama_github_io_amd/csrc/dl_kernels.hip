@@ -73,6 +73,15 @@ struct DLArgs {
   float* wpart;                 // [tiles][wsplit][64 * 64] fp32 partial tiles, then the batch's 1 / sum(w)
 };
 
+#ifdef DL_TIMING
+// per-workgroup phase clocks of the last k_dl_rows launch (diagnostic build only: scripts/build_alt.sh dlt
+// -DDL_TIMING, read back with h2o_dl_timing)
+__device__ unsigned long long g_dl_t[4096 * 16];
+#define DLT(i) do { if (threadIdx.x == 0 && blockIdx.x < 4096) g_dl_t[blockIdx.x * 16 + (i)] = wall_clock64(); } while (0)
+#else
+#define DLT(i) do { } while (0)
+#endif
+
 __device__ __forceinline__ uint32_t hash32(uint64_t x) {
   x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL; x ^= x >> 33;
   return (uint32_t)x;
@@ -211,6 +220,7 @@ __global__ __launch_bounds__(DL_THREADS) void k_dl_rows(DLArgs a) {
   const int r0 = blockIdx.x * DL_ROWS;
   const int L = a.L;
   const uint64_t step = a.step_dev ? *a.step_dev : 0ull;
+  DLT(0);
   __shared__ long long srow[DL_ROWS];
   __shared__ float sy[DL_ROWS];
   __shared__ long long scls[DL_ROWS];
@@ -229,6 +239,7 @@ __global__ __launch_bounds__(DL_THREADS) void k_dl_rows(DLArgs a) {
     for (int i = tid; i < total; i += DL_THREADS) reinterpret_cast<float*>(smem)[i] = 0.f;
   }
   __syncthreads();
+  DLT(1);
   // ---- gather the 16 input rows into activation tile 0
   {
     T* A0 = S + a.lds_off[0];
@@ -246,6 +257,7 @@ __global__ __launch_bounds__(DL_THREADS) void k_dl_rows(DLArgs a) {
     }
   }
   __syncthreads();
+  DLT(2);
   // input dropout (input_dropout_ratio): hash mask over (batch row, input), survivors scaled by 1 / keep
   if (a.in_drop > 0.f) {
     T* A0 = S + a.lds_off[0];
@@ -312,6 +324,7 @@ __global__ __launch_bounds__(DL_THREADS) void k_dl_rows(DLArgs a) {
       }
     }
     __syncthreads();
+    DLT(2 + l);
   }
   // ---- output layer + loss gradient (wave 0 when K <= 16; K > 16: logit tiles over the waves, then one wave
   // per row for the softmax, then one thread per class for the bias partials and the transposed gradient)
@@ -402,6 +415,7 @@ __global__ __launch_bounds__(DL_THREADS) void k_dl_rows(DLArgs a) {
     if (cok) store4T(dTg + a.d_off[L] + (long long)c * a.Bpad + r0 + 4 * q, g);
   }
   __syncthreads();
+  DLT(8);
   // ---- backward through the hidden layers
   const T* Gin = GO;
   int ldg_in = a.ld[L];
@@ -479,6 +493,7 @@ __global__ __launch_bounds__(DL_THREADS) void k_dl_rows(DLArgs a) {
       }
     }
     __syncthreads();
+    DLT(8 + l);
     Gin = Gout;
     ldg_in = ldo;
   }
@@ -487,6 +502,7 @@ __global__ __launch_bounds__(DL_THREADS) void k_dl_rows(DLArgs a) {
     for (int i = 0; i < DL_ROWS; ++i) s += ws[i];
     a.bpart[(long long)blockIdx.x * (a.bias_total + 1) + a.bias_total] = s;
   }
+  DLT(15);
 }
 
 // dW_l[i][j] = sum_rows dA_l[row][i] h_{l-1}[row][j]: A[i][k = row] = dT_l[i][row], B[k = row][j] = hT_{l-1}[j][row].
@@ -722,3 +738,10 @@ int h2o_dl_transpose(const DLArgs* a, hipStream_t s) {
 }
 
 }  // extern "C"
+
+#ifdef DL_TIMING
+extern "C" int h2o_dl_timing(unsigned long long* out, int n) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dl_t), sizeof(unsigned long long) * (size_t)n, 0,
+                                  hipMemcpyDeviceToHost);
+}
+#endif

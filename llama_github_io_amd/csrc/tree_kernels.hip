@@ -74,7 +74,7 @@ struct SplitParams {
   int random_split;        // extremely randomized / isolation: pick a random threshold
   unsigned long long seed;
   int hist_type;           // numeric candidate lattice (with adapt_nb > 1): HT_* below
-  int pad;
+  int fcut;                // > 0: only columns < fcut are searched (narrow levels of wide numeric bins, TreePlan)
 };
 
 // histogram types (SharedTreeParameters.HistogramType) as candidate lattices over the global bins
@@ -720,6 +720,10 @@ __global__ __launch_bounds__(256) void k_split_find(
   // stride (the slice width Fs, >= the F features searched here; F everywhere else)
   const int node = blockIdx.x, f = blockIdx.y, t = threadIdx.x;
   if (node >= meta[0]) return;
+  if (p.fcut > 0 && f + f0 >= p.fcut) {     // a column this level does not search (its histogram is not built)
+    if (t == 0) cand[(size_t)node * FL + f].valid = 0;
+    return;
+  }
   __shared__ double sw[256], swy[256], skey[256];
   __shared__ int sidx[256];
   __shared__ double best_e[256];
@@ -1054,9 +1058,10 @@ __global__ __launch_bounds__(256) void k_split_find(
 
 // Best feature of one node (one wave; lane = threadIdx.x & 63): k_split_reduce, and k_plan's prologue on
 // levels of at most PLAN_REDUCE_MAX nodes (the single plan block's 16 waves take the nodes; no extra launch).
-// fgroup (nullable): engine column -> original feature. A numeric feature binned wider than one byte holds
-// several adjacent engine columns (interleaved edge subsets, see ops/binning.py); column sampling draws
-// ORIGINAL features (key and rank of a column = its feature's), so such a feature is in or out as a whole.
+// fgroup (nullable): engine column -> original feature in bits 0-29; bit 30 set = not the feature's first
+// column. A numeric feature binned wider than one byte holds several engine columns (interleaved edge subsets,
+// see ops/binning.py); column sampling draws ORIGINAL features (key and rank of a column = its feature's), so
+// such a feature is in or out as a whole.
 // cfs > 0: cand is the RANK-MAJOR all-gather of a feature-sliced run, [W][ccap][cfs] (rank r searched
 // features r*cfs ..), read in place instead of being permuted into [cap][F] first.
 __device__ __forceinline__ const Cand& cand_at(const Cand* __restrict__ cand, int node, int f, int F, int cfs,
@@ -1071,8 +1076,8 @@ __device__ void reduce_node(const Cand* __restrict__ cand, int node, int F, cons
                             int cfs = 0, int ccap = 0) {
   const unsigned char* nok = node_ok ? node_ok + (size_t)node * F : nullptr;
   auto usable = [&](int f) { return feat_ok[f] != 0 && (!nok || nok[f] != 0); };
-  auto gid = [&](int f) { return fgroup ? fgroup[f] : f; };
-  auto leader = [&](int f) { return !fgroup || f == 0 || fgroup[f] != fgroup[f - 1]; };
+  auto gid = [&](int f) { return fgroup ? (fgroup[f] & 0x3FFFFFFF) : f; };
+  auto leader = [&](int f) { return !fgroup || (fgroup[f] & 0x40000000) == 0; };
   const unsigned long long base = splitmix64(seed ^ ((unsigned long long)(level + 1) << 40) ^ (unsigned long long)node);
   int n_ok = 0;
   for (int f = lane; f < F; f += 64) n_ok += (usable(f) && leader(f)) ? 1 : 0;
@@ -1487,15 +1492,18 @@ __global__ __launch_bounds__(LW * 64) void k_route(
     const int row = wbase + u * 64 + lane;
     const bool valid = row < r1;
     int dA = 0, dB = 0;
+    // (a split column past the registers — narrow copies, lp > 0 — is read from the source)
     if (valid && featA >= 0)
-      dA = dec_go_left(&sA, NV > 2 ? row_byte4(rv0[u], rv1[u], rv2[u], rv3[u], featA)
-                                   : NV > 0 ? row_byte(rv0[u], rv1[u], featA) : sbins[bin_off(row, featA, stride, N, planar)]) ? 0 : 1;
+      dA = dec_go_left(&sA, (NV > 0 && featA >= NV * 16) ? sbins[bin_off(row, featA, stride, N, planar)]
+                            : NV > 2 ? row_byte4(rv0[u], rv1[u], rv2[u], rv3[u], featA)
+                            : NV > 0 ? row_byte(rv0[u], rv1[u], featA) : sbins[bin_off(row, featA, stride, N, planar)]) ? 0 : 1;
     if (valid && sC[dA] >= 0) {
       const Dec* b = &sB[dA];
       const int fb = b->feat;
       if (fb >= 0)
-        dB = dec_go_left(b, NV > 2 ? row_byte4(rv0[u], rv1[u], rv2[u], rv3[u], fb)
-                                   : NV > 0 ? row_byte(rv0[u], rv1[u], fb) : sbins[bin_off(row, fb, stride, N, planar)]) ? 0 : 1;
+        dB = dec_go_left(b, (NV > 0 && fb >= NV * 16) ? sbins[bin_off(row, fb, stride, N, planar)]
+                            : NV > 2 ? row_byte4(rv0[u], rv1[u], rv2[u], rv3[u], fb)
+                            : NV > 0 ? row_byte(rv0[u], rv1[u], fb) : sbins[bin_off(row, fb, stride, N, planar)]) ? 0 : 1;
     }
     q[u] = 2 * dA + dB;
     mv[u] = valid && sG[q[u]] >= 0;
@@ -1954,11 +1962,13 @@ int h2o_tree_sizes(int* out) {
 // partials: >= (grid + max nodes of the level) slots of slot_doubles. nbins_f (nullable): per-feature bin counts,
 // which let NONA launches spread the updates of low-cardinality features over copies of their bins. fine_f
 // (nullable): 1 for the columns of word-aligned 4-column wide numeric groups (one fine atomic per row and group).
+// nft_lim > 0: only the first nft_lim feature tiles (planes) are built (narrow levels; the slot layout stays F)
 int h2o_hist_build(const void* bins, int stride, const void* aw, const void* ay, const void* nodes,
                    const void* tile_prefix, const void* meta, int F, void* partials, int slot_doubles, const void* qs,
                    int grid, int packed, const void* pdec, void* nl_out, int f32, long long N, int planar,
-                   const void* nbins_f, const void* fine_f, hipStream_t s) {
-  const int nft = (F + FTILE - 1) / FTILE;
+                   const void* nbins_f, const void* fine_f, int nft_lim, hipStream_t s) {
+  int nft = (F + FTILE - 1) / FTILE;
+  if (nft_lim > 0 && nft_lim < nft) nft = nft_lim;
   // A/B switches: H2O_HIST_REPL=0 drops the low-cardinality bin replicas, H2O_HIST_FINE=1 enables the
   // fine-bin atomics of 4-column wide groups (MEASURED slower: AUTO 11M plain pass 482 vs 325 us, r4)
   const char* e_repl = getenv("H2O_HIST_REPL");
@@ -2020,7 +2030,7 @@ int h2o_split_find(const void* hist, int slot_doubles, const void* meta, int cap
                    void* root_w, const void* edges, int adapt_nb, int hist_type, int f0, int FL, hipStream_t s) {
   SplitParams p;
   p.min_w = min_w; p.min_split_improvement = msi; p.lambda = lambda_; p.alpha = alpha; p.gamma = gamma;
-  p.mode = mode; p.random_split = random_split; p.seed = seed; p.hist_type = hist_type; p.pad = 0;
+  p.mode = mode; p.random_split = random_split; p.seed = seed; p.hist_type = hist_type; p.fcut = 0;
   return split_find_launch((void*)hist, slot_doubles, meta, cap, F, nbins_f, iscat_f, mono_f, p, level, cand, root_w,
                            edges, adapt_nb, f0, FL, Derive{nullptr, 0, 0, nullptr, nullptr}, s);
 }
@@ -2102,17 +2112,20 @@ static int nv_of(int stride) {
 }
 
 // regroup an even level two levels down (moving bins + wY (+ w) of continuing rows)
+// lp > 0 (planar): only the first lp (1 or 2) planes of each row move — the narrow levels below read no other
+// column; split bytes of columns past them (the decisions of the levels above) are read from the source
 int h2o_route(const void* sbins, const void* say, const void* saw, void* dbins, void* day, void* daw, int stride,
               const void* nodesA, const void* tpA, const void* metaA, const void* decA, const void* clA,
               const void* crA, const void* decB, const void* clB, const void* crB, void* curs, int tiles_cap,
-              long long N, int planar, hipStream_t s) {
+              long long N, int planar, int lp, hipStream_t s) {
   if (planar && (stride % 32 != 0 || stride < 64)) return (int)hipErrorInvalidValue;
+  if (lp < 0 || lp > 2 || (lp > 0 && !planar)) return (int)hipErrorInvalidValue;
 #define ROUTE_LAUNCH(NV)                                                                                       \
   hipLaunchKernelGGL((k_route<NV>), dim3(tiles_cap), dim3(LW * 64), 0, s, (const uint8_t*)sbins,              \
                      (const float*)say, (const float*)saw, (uint8_t*)dbins, (float*)day, (float*)daw, stride,  \
                      (const Node*)nodesA, (const int*)tpA, (const int*)metaA, (const Dec*)decA, (const int*)clA, \
                      (const int*)crA, (const Dec*)decB, (const int*)clB, (const int*)crB, (int4*)curs, N, planar)
-  switch (nv_of(stride)) {
+  switch (lp == 1 ? 2 : lp == 2 ? 4 : nv_of(stride)) {
     case 4: ROUTE_LAUNCH(4); break;
     case 3: ROUTE_LAUNCH(3); break;
     case 2: ROUTE_LAUNCH(2); break;
@@ -2249,6 +2262,11 @@ struct TreePlan {
   int dist;                   // row-sharded (h2o_tree_dist): build slots go out in the exchange's layout
   void *hsend, *cand_all, *lsx;  // [W][n][E] packed send slots, [W][cap][Fs] candidates, leaf sums + root weight
   void* fine_f;               // [F] int32: columns of word-aligned 4-column wide numeric groups (or null)
+  // narrow levels of wide numeric bins (ops/binning.py layout: columns [0, lo_F) hold every feature's first
+  // column, the other interleaved edge subsets follow): from level lo_from on (adaptive bin count <= 256) only
+  // columns < lo_F are histogrammed and searched, and the routes that feed those levels move only the planes
+  // holding them. lo_F = 0: off.
+  int lo_F, lo_from;
 };
 
 // op codes / dtypes of the collective transport
@@ -2267,13 +2285,18 @@ static inline void tp_level_buf(const TreePlan* P, int e, const void*& b, const 
   b = P->bb[i]; y = P->by[i]; w = P->unit ? nullptr : P->bw[i];
 }
 
+static inline bool tp_narrow(const TreePlan* P, int d) { return P->lo_F > 0 && d >= P->lo_from; }
+static inline int tp_lo_planes(const TreePlan* P) { return (P->lo_F + FTILE - 1) / FTILE; }
+
 static int tp_route(const TreePlan* P, int e, hipStream_t s) {
   const void *sb, *sy, *sw;
   tp_level_buf(P, e, sb, sy, sw);
   const int di = (e / 2) % 2;
+  // rows of level e + 2 (and below) are read by narrow levels only: move just the low planes
+  const int lp = (tp_narrow(P, e + 2) && P->planar && tp_lo_planes(P) <= 2) ? tp_lo_planes(P) : 0;
   return h2o_route(sb, sy, sw, P->bb[di], P->by[di], P->unit ? nullptr : P->bw[di], P->stride, P->nodes[e], P->tp[e],
                    P->meta[e], P->dec[e], P->cl[e], P->cr[e], P->dec[e + 1], P->cl[e + 1], P->cr[e + 1],
-                   P->cur[e + 1], P->tiles_cap[e], P->N, P->planar, s);
+                   P->cur[e + 1], P->tiles_cap[e], P->N, P->planar, lp, s);
 }
 
 #define TP_CHECK(x) do { int rc_ = (x); if (rc_) return rc_; } while (0)
@@ -2289,7 +2312,7 @@ int h2o_tree_root(const TreePlan* P, hipStream_t s) {
   const int g0 = P->tiles_cap[0] < P->grid ? P->tiles_cap[0] : P->grid;
   TP_CHECK(h2o_hist_build(P->master, P->stride, P->unit ? nullptr : tp_aux(P, 0), tp_aux(P, 1), P->nodes[0], P->bp[0],
                           P->meta[0], P->F, P->partials, P->slot, P->qs, g0, P->packed, nullptr, nullptr, P->pf32, P->N,
-                          P->planar | (P->no_na << 1), P->nbins_f, P->fine_f, s));
+                          P->planar | (P->no_na << 1), P->nbins_f, P->fine_f, tp_narrow(P, 0) ? tp_lo_planes(P) : 0, s));
   // row-sharded all-reduce: straight into the wire buffer; sliced: hbuild (packed by slice next)
   if (P->dist && !P->sliced)
     return h2o_hist_reduce(P->partials, P->slot, P->used, P->nodes[0], P->bp[0], P->meta[0], 1, g0, P->hrecv, nullptr,
@@ -2305,7 +2328,8 @@ int h2o_tree_find(const TreePlan* P, int d, hipStream_t s) {
   const void* hp = (d % 2) ? P->hist0 : P->hist1;      // level d-1 (unused at the root: build = 1)
   SplitParams p;
   p.min_w = P->min_w; p.min_split_improvement = P->msi; p.lambda = P->lam; p.alpha = P->alpha; p.gamma = P->gamma;
-  p.mode = P->mode; p.random_split = P->random_split; p.seed = P->seed; p.hist_type = P->hist_type; p.pad = 0;
+  p.mode = P->mode; p.random_split = P->random_split; p.seed = P->seed; p.hist_type = P->hist_type;
+  p.fcut = tp_narrow(P, d) ? P->lo_F : 0;
   const int hs = P->sliced ? P->sslot : P->slot;
   const Derive dv = P->dist ? Derive{P->hrecv, P->cf32, P->sslot, (const double*)hp, (const Node*)P->nodes[d]}
                             : Derive{nullptr, 0, 0, nullptr, nullptr};
@@ -2360,7 +2384,7 @@ int h2o_tree_grow(const TreePlan* P, int d, int dist, hipStream_t s) {
     tp_level_buf(P, d, sb, sy, sw);
     rc = h2o_hist_build(sb, P->stride, sw, sy, P->nodes[d + 1], P->bp[d + 1], P->meta[d + 1], P->F, P->partials,
                         P->slot, P->qs, gh, P->packed, P->dec[d], P->nl[d], P->pf32, P->N, P->planar | (P->no_na << 1),
-                        P->nbins_f, P->fine_f, s);
+                        P->nbins_f, P->fine_f, tp_narrow(P, d + 1) ? tp_lo_planes(P) : 0, s);
   } else {
     // regroup level d-1's rows two levels down, then histogram level d+1 (even) contiguously
     rc = tp_route(P, d - 1, s);
@@ -2371,7 +2395,7 @@ int h2o_tree_grow(const TreePlan* P, int d, int dist, hipStream_t s) {
     tp_level_buf(P, d + 1, sb, sy, sw);
     rc = h2o_hist_build(sb, P->stride, sw, sy, P->nodes[d + 1], P->bp[d + 1], P->meta[d + 1], P->F, P->partials,
                         P->slot, P->qs, gh, P->packed, nullptr, nullptr, P->pf32, P->N, P->planar | (P->no_na << 1),
-                        P->nbins_f, P->fine_f, s);
+                        P->nbins_f, P->fine_f, tp_narrow(P, d + 1) ? tp_lo_planes(P) : 0, s);
   }
   if (rc) return -rc;
   if (!dist)

@@ -24,6 +24,7 @@ the column's bitset back through ``level_to_bin`` to a bitset over all L origina
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -46,6 +47,7 @@ class Binning:
     nlevels: np.ndarray             # int32 [F] categorical cardinality (0 numeric)
     level_to_bin: list = field(default_factory=list)  # per feature: int array (None = identity)
     vmap: np.ndarray | None = None  # int32 [F] engine column -> original feature (None: identity)
+    n_low: int = 0                  # engine columns [0, n_low) = every feature's first column (narrow view), 0: none
 
     # every per-feature field above is per ENGINE column (F of them); see the module note on wide bins
     @property
@@ -67,7 +69,7 @@ class Binning:
         return dict(F=self.F, stride=self.stride, edges=[None if e is None else e.tolist() for e in self.edges],
                     nbins=self.nbins.tolist(), iscat=self.iscat.tolist(), nlevels=self.nlevels.tolist(),
                     level_to_bin=[None if m is None else m.tolist() for m in self.level_to_bin],
-                    vmap=None if self.vmap is None else self.vmap.tolist())
+                    vmap=None if self.vmap is None else self.vmap.tolist(), n_low=int(self.n_low))
 
     @staticmethod
     def from_state(s):
@@ -75,7 +77,8 @@ class Binning:
                        np.asarray(s["nbins"], dtype=np.int32), np.asarray(s["iscat"], dtype=np.int32),
                        np.asarray(s["nlevels"], dtype=np.int32),
                        [None if m is None else np.asarray(m, dtype=np.int64) for m in s["level_to_bin"]],
-                       None if s.get("vmap") is None else np.asarray(s["vmap"], dtype=np.int32))
+                       None if s.get("vmap") is None else np.asarray(s["vmap"], dtype=np.int32),
+                       int(s.get("n_low", 0)))
 
 
 def sample_rows(X: torch.Tensor, sample: int, seed: int, row0: int = 0, n_glob: int | None = None) -> torch.Tensor:
@@ -171,13 +174,19 @@ def fit_binning(X: torch.Tensor, iscat, nlevels=None, max_bins: int = MAX_DATA_B
         edges.append(e)
         nbins[f] = e.size + 1
     vmap = None
+    n_low = 0
     wide_cat = [bool(iscat[f]) and nbins[f] > SUB_EDGES for f in range(F)]
     if any(e is not None and e.size > SUB_EDGES for e in edges) or any(wide_cat):
         # wide numeric features -> n adjacent engine columns with the interleaved edge subsets e[k::n];
         # wide categoricals -> n adjacent engine columns of (at most) 254 consecutive bins each
-        # the features of exactly 4 interleaved columns go FIRST, so each one fills one aligned 4-byte row word:
-        # the histogram kernel then adds one fine-bin atomic per row and feature (sum of the 4 bytes) instead of 4
-        quad, rest = [], []
+        # Layout: every feature's FIRST column (edge subset e[0::n], ~254 quantile edges; all blocks of a wide
+        # categorical) leads, the other subsets follow: from the level on where the adaptive bin count drops to
+        # 256 the tree searches only the leading n_low columns (ops/tree.narrow_from), whose planes alone are
+        # histogrammed and moved. H2O_HIST_FINE=1 keeps the former layout instead: the features of exactly 4
+        # interleaved columns first, each filling one aligned 4-byte row word (one fine-bin atomic per row and
+        # feature in the histogram kernel).
+        fine_layout = os.environ.get("H2O_HIST_FINE") == "1"
+        quad, rest, low, high = [], [], [], []
         for f in range(F):
             e = edges[f]
             if wide_cat[f]:
@@ -187,13 +196,21 @@ def fit_binning(X: torch.Tensor, iscat, nlevels=None, max_bins: int = MAX_DATA_B
                 for k in range(n):
                     b0, nk = k * SUB_EDGES, min(SUB_EDGES, nb - k * SUB_EDGES)
                     inb = (lb >= b0) & (lb < b0 + nk)
-                    rest.append((f, None, nk + 1, np.where(inb, lb - b0, nk)))
+                    c = (f, None, nk + 1, np.where(inb, lb - b0, nk))
+                    rest.append(c)
+                    low.append(c)
                 continue
             n = 1 if e is None or e.size <= SUB_EDGES else -(-e.size // SUB_EDGES)
             for k in range(n):
                 ek = e if n == 1 else np.ascontiguousarray(e[k::n])
-                (quad if n == 4 else rest).append((f, ek, (ek.size + 1) if e is not None else nbins[f], l2b[f]))
-        cols = quad + rest
+                c = (f, ek, (ek.size + 1) if e is not None else nbins[f], l2b[f])
+                (quad if n == 4 else rest).append(c)
+                (low if k == 0 else high).append(c)
+        if fine_layout:
+            cols = quad + rest
+        else:
+            cols = low + high
+            n_low = len(low) if high else 0
         vmap = np.asarray([c[0] for c in cols], dtype=np.int32)
         edges = [c[1] for c in cols]
         nbins = np.asarray([c[2] for c in cols], dtype=np.int32)
@@ -205,7 +222,7 @@ def fit_binning(X: torch.Tensor, iscat, nlevels=None, max_bins: int = MAX_DATA_B
     # > 32 features: whole 32-byte planes (the device engine stores such bins PLANAR, one plane per
     # histogram feature tile — apply_binning(planar=True))
     stride = (F + 3) // 4 * 4 if F <= 12 else ((F + 15) // 16 * 16 if F <= 32 else (F + 31) // 32 * 32)
-    return Binning(F, stride, edges, nbins, iscat, nlevels, l2b, vmap)
+    return Binning(F, stride, edges, nbins, iscat, nlevels, l2b, vmap, n_low)
 
 
 def _edge_table(b: Binning, device):

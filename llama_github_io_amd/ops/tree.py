@@ -60,6 +60,35 @@ def fine_columns(fgroup, iscat, F):
     return out if out.any() else None
 
 
+def narrow_from(p: "SplitParams", n_low: int, F: int) -> int:
+    """First level of the NARROW view of wide numeric bins (or -1): with an adaptive histogram type, levels whose
+    bin count max(nbins, nbins_top_level >> d) is at most 256 search only engine columns [0, n_low) — every
+    feature's first interleaved edge subset (ops/binning.py layout), i.e. their cut points snap to a ~254-edge
+    quantile sub-lattice instead of all ~1016 edges — so their histograms, searches and row moves cost what a
+    255-bin QuantilesGlobal run does (H2O_TREE_NARROW=0: every level searches every column)."""
+    if n_low <= 0 or n_low >= F or os.environ.get("H2O_TREE_NARROW", "1") == "0":
+        return -1
+    if not p.adapt_nbins or p.edges is None:
+        return -1
+    for d in range(64):
+        if 0 < p.adapt_nb(d) <= 256:
+            return d
+    return -1
+
+
+def encode_groups(fgroup) -> np.ndarray | None:
+    """int32 [F] for the device: the original feature in bits 0-29, bit 30 on every column but the feature's
+    first (k_split_reduce's column-sampling leaders)."""
+    if fgroup is None:
+        return None
+    g = np.asarray(fgroup, dtype=np.int64)
+    seen, out = set(), np.empty(g.size, dtype=np.int32)
+    for f, v in enumerate(g.tolist()):
+        out[f] = v | (0 if v not in seen else 1 << 30)
+        seen.add(v)
+    return out
+
+
 def splitmix64(x: int) -> int:
     x = (x + 0x9E3779B97F4A7C15) & _M64
     x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & _M64
@@ -334,10 +363,11 @@ def split_find_ref(h, nayy, wyy, nbins_f, iscat_f, mono_f, p: SplitParams, level
 
 def split_reduce_ref(cands, feat_ok, k_cols, seed, level, node, node_ok=None, fgroup=None):
     """k_split_reduce: best usable column; with ``fgroup`` (engine column -> original feature) the column
-    sample draws original features, whose adjacent engine columns share one key and rank."""
+    sample draws original features, whose engine columns share one key and rank (the feature's first column
+    counts it)."""
     F = len(cands)
     gid = list(range(F)) if fgroup is None else [int(g) for g in fgroup]
-    lead = [f == 0 or gid[f] != gid[f - 1] for f in range(F)]
+    lead = [gid[f] not in gid[:f] for f in range(F)] if fgroup is not None else [True] * F
     base = splitmix64((seed ^ ((level + 1) << 40) ^ node) & _M64)
     ok = [bool(feat_ok[f]) and (node_ok is None or bool(node_ok[f])) for f in range(F)]
     n_ok = sum(1 for f in range(F) if ok[f] and lead[f])
@@ -401,16 +431,18 @@ class RefTreeBuilder:
         self.node_cap = node_cap
         self.N = self.bins.shape[0]
         self.ic_map = None
+        self.n_low = 0
 
     def set_interaction_constraints(self, ic_map, root_ok):
         """``ic_map`` [F, F] (row f: features allowed to interact with f), ``root_ok`` [F]."""
         self.ic_map = np.asarray(ic_map, dtype=np.uint8)
         self.ic_root = np.asarray(root_ok, dtype=np.uint8)
 
-    def set_feature_groups(self, fgroup):
-        """Engine column -> original feature (wide numeric features span adjacent columns): column sampling
-        draws original features."""
+    def set_feature_groups(self, fgroup, n_low: int = 0):
+        """Engine column -> original feature (wide numeric features span several columns): column sampling
+        draws original features. ``n_low``: leading columns of the narrow view (:func:`narrow_from`)."""
         self.fgroup = None if fgroup is None else np.asarray(fgroup, dtype=np.int64)
+        self.n_low = int(n_low)
 
     def _hist(self, rows, aux):
         F = self.F
@@ -435,6 +467,7 @@ class RefTreeBuilder:
         F, D, p = self.F, self.D, self.p
         feat_ok = np.ones(F, dtype=np.int32) if feat_ok is None else np.asarray(feat_ok)
         leaf_of_row = np.full(self.N, -1, dtype=np.int64)
+        lo_from = narrow_from(p, self.n_low, F)
         leafsum = []
         level_rows = [np.arange(self.N)]
         level_ok = [None if self.ic_map is None else self.ic_root]
@@ -454,6 +487,9 @@ class RefTreeBuilder:
                     nayy = flat[h.size: h.size + F]
                     wyy = float(flat[-1])
                 cands = split_find_ref(h, nayy, wyy, self.nbins_f, self.iscat_f, self.mono_f, p, d, i, seed)
+                if 0 <= lo_from <= d:           # narrow level: the columns past n_low are not searched
+                    for f in range(self.n_low, F):
+                        cands[f]["valid"] = False
                 dl[i] = split_reduce_ref(cands, feat_ok, _level_k(k_cols, d), seed, d, i, level_ok[i],
                                          getattr(self, "fgroup", None))
             cl = np.zeros(n, dtype=np.int64); cr = np.zeros(n, dtype=np.int64)
@@ -534,7 +570,7 @@ class _TreePlan(ctypes.Structure):
                 [("leaf_lam", _cd), ("leaf_l1", _cd)] + [("planar", _ci), ("no_na", _ci)] +
                 [("fgroup", _vp)] + [("coll_fn", _vp), ("coll_ctx", _vp)] +
                 [(n, _ci) for n in ("W", "cf32", "cand_fs", "dist")] + [(n, _vp) for n in ("hsend", "cand_all", "lsx")] +
-                [("fine_f", _vp)])
+                [("fine_f", _vp)] + [("lo_F", _ci), ("lo_from", _ci)])
 
 
 class _Arena:
@@ -609,7 +645,8 @@ class GpuTreeBuilder:
         # measured: 2 is 3-14 % slower; again with the barrier-free filtered pass (round 3): 11M 1.34 -> 1.40,
         # 1.375M 0.423 -> 0.474 ms/tree (the doubled partial slots cost more than the extra waves gain)
         self.hist_bpc = int(os.environ.get("H2O_HIST_BPC", "1"))
-        self.partials = torch.empty((self.hist_bpc * grid + capmax) * self.slot, dtype=torch.float64, device=dev)
+        # (zeroed: narrow levels leave the partial entries of columns they do not build untouched)
+        self.partials = torch.zeros((self.hist_bpc * grid + capmax) * self.slot, dtype=torch.float64, device=dev)
         self.tiles_cap = [(N + T - 1) // T + c for c in self.caps]
         self.cand = torch.empty(capmax * F * CAND_BYTES, dtype=torch.uint8, device=dev)
         self.scratch = torch.empty(2 * capmax + 16, dtype=torch.int32, device=dev)
@@ -622,6 +659,7 @@ class GpuTreeBuilder:
         self.iscat_f = torch.as_tensor(np.asarray(iscat_f, dtype=np.int32), device=dev)
         self.iscat_np = np.asarray(iscat_f, dtype=np.int32)
         self.fine_f = None
+        self.n_low = 0
         self.mono_f = None if mono_f is None else torch.as_tensor(np.asarray(mono_f, dtype=np.int32), device=dev)
         self.feat_ok_all = torch.ones(F, dtype=torch.int32, device=dev)
         self.qs = torch.zeros(16, dtype=torch.float64, device=dev)  # fixed-point scales (k_qscale)
@@ -756,16 +794,23 @@ class GpuTreeBuilder:
         if getattr(self, "_plan", None) is not None:
             self._set_plan_ic(self._plan)
 
-    def set_feature_groups(self, fgroup):
-        """Engine column -> original feature (k_split_reduce column sampling by original feature)."""
-        self.fgroup = None if fgroup is None else torch.as_tensor(np.asarray(fgroup, dtype=np.int32),
-                                                                  device=self.dev).contiguous()
+    def set_feature_groups(self, fgroup, n_low: int = 0):
+        """Engine column -> original feature (k_split_reduce column sampling by original feature); ``n_low``:
+        leading columns of the narrow view (:func:`narrow_from`)."""
+        enc = encode_groups(fgroup)
+        self.fgroup = None if enc is None else torch.as_tensor(enc, device=self.dev).contiguous()
         self.fine_f = fine_columns(fgroup, self.iscat_np, self.F)
         if self.fine_f is not None:
             self.fine_f = torch.as_tensor(self.fine_f, device=self.dev).contiguous()
+        self.n_low = int(n_low)
         if getattr(self, "_plan", None) is not None:
             self._plan.fgroup = 0 if self.fgroup is None else self.fgroup.data_ptr()
             self._plan.fine_f = 0 if self.fine_f is None else self.fine_f.data_ptr()
+            self._set_plan_narrow(self._plan)
+
+    def _set_plan_narrow(self, P):
+        lo_from = narrow_from(self.p, self.n_low, self.F)
+        P.lo_F, P.lo_from = (self.n_low, lo_from) if lo_from >= 0 else (0, 0)
 
     def _set_plan_ic(self, P):
         if self.ic_map is None:
@@ -806,6 +851,7 @@ class GpuTreeBuilder:
         fg = getattr(self, "fgroup", None)
         P.fgroup = 0 if fg is None else fg.data_ptr()
         P.fine_f = 0 if self.fine_f is None else self.fine_f.data_ptr()     # used only under H2O_HIST_FINE=1
+        self._set_plan_narrow(P)
         P.sliced, P.fs0, P.fsn, P.sslot = int(self.sliced), self.fs0, self.fsn, self.sslot
         P.planar = int(self.planar)
         P.no_na = int(self._no_na())

@@ -473,20 +473,29 @@ def test_gpu_tree_bins_matrix_above_2pow31_bytes():
     assert torch.equal(ref.leaf_of_row, gb.leaf_of_row.cpu())
 
 
-def test_wide_binning_columns_are_interleaved_edge_subsets():
+@pytest.mark.parametrize("fine", ["0", "1"])
+def test_wide_binning_columns_are_interleaved_edge_subsets(fine, monkeypatch):
     """nbins_top_level = 1024 (SharedTreeModel.java:57): a numeric feature with more than 254 edges is binned
-    as adjacent engine columns over the edge subsets e[k::n]; every fine threshold is one column's split."""
+    as engine columns over the edge subsets e[k::n]; every fine threshold is one column's split."""
+    monkeypatch.setenv("H2O_HIST_FINE", fine)
     g = torch.Generator().manual_seed(1)
     X = torch.rand(3, 20000, generator=g)
     X[1] = torch.randint(0, 40, (20000,), generator=g).float()        # few distinct values: one column
     X[2, :100] = float("nan")
     b = fit_binning(X, np.zeros(3, np.int32), None, max_bins=1016)
-    # 4-column features first (each fills one aligned row word), then the rest
-    assert b.F_orig == 3 and list(b.vmap) == [0, 0, 0, 0, 2, 2, 2, 2, 1]
-    assert list(T.fine_columns(b.vmap, b.iscat, b.F)) == [1] * 8 + [0]
+    if fine == "1":
+        # 4-column features first (each fills one aligned row word), then the rest
+        assert b.F_orig == 3 and list(b.vmap) == [0, 0, 0, 0, 2, 2, 2, 2, 1] and b.n_low == 0
+        assert list(T.fine_columns(b.vmap, b.iscat, b.F)) == [1] * 8 + [0]
+    else:
+        # every feature's first column leads (the narrow view of levels with <= 256 adaptive bins)
+        assert b.F_orig == 3 and list(b.vmap) == [0, 1, 2, 0, 0, 0, 2, 2, 2] and b.n_low == 3
+        assert T.fine_columns(b.vmap, b.iscat, b.F) is None
+    c0 = [int(j) for j in np.nonzero(b.vmap == 0)[0]]
+    c2 = [int(j) for j in np.nonzero(b.vmap == 2)[0]]
     # the fine bin is the byte sum of the 4 columns (NA: 4 x 255)
-    fsum = apply_binning(b, X).long()[:, 4:8].sum(1)
-    e2 = np.sort(np.concatenate([b.edges[j] for j in range(4, 8)]))
+    fsum = apply_binning(b, X).long()[:, c2].sum(1)
+    e2 = np.sort(np.concatenate([b.edges[j] for j in c2]))
     ref2 = torch.bucketize(torch.nan_to_num(X[2], nan=0.0), torch.from_numpy(e2), right=True)
     assert torch.equal(fsum, torch.where(torch.isnan(X[2]), torch.full_like(ref2, 4 * T.NA_BIN), ref2))
     fine0 = fit_binning(X[:1], np.zeros(1, np.int32), None, max_bins=1016)
@@ -498,12 +507,12 @@ def test_wide_binning_columns_are_interleaved_edge_subsets():
         ref = torch.where(torch.isnan(X[f]), torch.full_like(ref, T.NA_BIN), ref)
         assert torch.equal(bins[:, j], ref)
     # feature 0: the 4 columns' thresholds are exactly the fine thresholds
-    ef = np.concatenate([b.edges[j] for j in range(4)])
+    ef = np.concatenate([b.edges[j] for j in c0])
     assert np.array_equal(np.sort(ef), np.sort(np.concatenate([fine0.edges[j] for j in range(fine0.F)])))
-    fine = torch.bucketize(X[0], torch.from_numpy(np.sort(ef)), right=True)
+    fb = torch.bucketize(X[0], torch.from_numpy(np.sort(ef)), right=True)
     for t in (1, 2, 3, 4, 5, 500, 1013):
         k, h = (t - 1) % 4, (t - 1) // 4 + 1      # fine split t <=> column k split at bin h
-        assert torch.equal(bins[:, k] < h, fine < t)
+        assert torch.equal(bins[:, c0[k]] < h, fb < t)
 
 
 def test_wide_bins_split_resolution_and_grouped_sampling():
@@ -530,17 +539,47 @@ def test_wide_bins_split_resolution_and_grouped_sampling():
             allowed.append(T.split_reduce_ref(c, np.ones(6), 1, seed, 0, 0, None, fgroup)["feat"] == f)
         assert sum(allowed) in (1, 4) and (sum(allowed) == 1) == (not allowed[0])
         assert len(set(allowed[:4])) == 1
+    # the narrow layout: the feature's first column leads, its other columns follow the other features
+    fgroup = np.array([0, 1, 2, 0, 0, 0])
+    assert list(T.encode_groups(fgroup)) == [0, 1, 2, 1 << 30, 1 << 30, 1 << 30]
+    for seed in range(40):
+        allowed = []
+        for f in range(6):
+            c = [dict(valid=(i == f), expl=1.0, bin=1, na_left=0, is_cat=0, bits=np.zeros(8, np.uint32), gain=1.0,
+                      wl=1.0, wr=1.0, predl=0.0, predr=0.0) for i in range(6)]
+            allowed.append(T.split_reduce_ref(c, np.ones(6), 1, seed, 0, 0, None, fgroup)["feat"] == f)
+        assert len({allowed[0], allowed[3], allowed[4], allowed[5]}) == 1 and sum(allowed) in (1, 4)
+
+
+def test_narrow_levels_search_only_first_columns():
+    """AUTO (UniformAdaptive, nbins_top_level 1024): from the level whose adaptive bin count is <= 256 the
+    reference builder searches only every feature's first column (ops/tree.narrow_from)."""
+    X, y, info = _data(N=20000, F=4, seed=3)
+    b = fit_binning(X, info.iscat, info.nlevels, max_bins=1016)
+    assert b.n_low == 4 and b.F == 16
+    p = T.SplitParams(min_w=5, adapt_nbins=20, adapt_top=1024, edges=_edge_tab(b))
+    assert T.narrow_from(p, b.n_low, b.F) == 2
+    assert T.narrow_from(T.SplitParams(min_w=5), b.n_low, b.F) == -1          # QuantilesGlobal: every level
+    g = y - 0.5
+    aux = torch.stack([torch.ones_like(y), g, g, torch.ones_like(y)], 1).contiguous()
+    ref = T.RefTreeBuilder(apply_binning(b, X), b.F, b.nbins, b.iscat, None, 6, p)
+    ref.set_feature_groups(b.vmap, b.n_low)
+    ref.build(aux, None, 0, seed=1)
+    tl = ref.pop_levels()[0]
+    assert all(int(f) < b.n_low for d in tl.decs[2:] for f in d["feat"] if f >= 0)
+    assert any(int(f) >= b.n_low for d in tl.decs[:2] for f in d["feat"])
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("fine", ["0", "1"])
-@pytest.mark.parametrize("case", ["plain", "kcols_adaptive", "newton"])
+@pytest.mark.parametrize("case", ["plain", "kcols_adaptive", "newton", "narrow_planar"])
 def test_gpu_wide_bins_match_reference(case, fine, monkeypatch):
     """1016-bin numeric features (4 engine columns each) on the GPU engine vs RefTreeBuilder: identical
     decisions, left weights and leaf assignment, including grouped column sampling (k_split_reduce fgroup), with and
-    without the fine-bin atomics of the 4-column groups (H2O_HIST_FINE)."""
+    without the fine-bin atomics of the 4-column groups (H2O_HIST_FINE, its aligned layout), and the narrow levels
+    of the default layout (adaptive cases: first columns only from level 2; planar: the routes move one plane)."""
     monkeypatch.setenv("H2O_HIST_FINE", fine)
-    X, y, info = _data(N=30000, cat=True, seed=11)
+    X, y, info = _data(N=30000, F=10 if case == "narrow_planar" else 6, cat=True, seed=11)
     b = fit_binning(X, info.iscat, info.nlevels, max_bins=1016)
     assert b.vmap is not None and b.F > X.shape[0]
     bins = apply_binning(b, X)
@@ -553,18 +592,25 @@ def test_gpu_wide_bins_match_reference(case, fine, monkeypatch):
     if case == "kcols_adaptive":
         k_cols = 3
         p = T.SplitParams(min_w=10, adapt_nbins=20, adapt_top=1024, edges=_edge_tab(b))
+    elif case == "narrow_planar":
+        assert b.stride >= 64
+        p = T.SplitParams(min_w=10, adapt_nbins=20, adapt_top=1024, edges=_edge_tab(b))
     elif case == "newton":           # unpacked two-plane histograms through the fine-bin atomics
         h = torch.full_like(y, 0.25)
         aux = torch.stack([h, -g, -g, h], 1).contiguous()
         p = T.SplitParams(min_w=1.0, lam=1.0, mode=T.MODE_NEWTON)
-    assert T.fine_columns(b.vmap, b.iscat, b.F).sum() == 20     # 5 numeric features of 4 aligned columns
+    if fine == "1":
+        nnum = X.shape[0] - 1
+        assert T.fine_columns(b.vmap, b.iscat, b.F).sum() == 4 * nnum   # numeric features of 4 aligned columns
+    else:
+        assert b.n_low == X.shape[0]
     ref = T.RefTreeBuilder(bins, b.F, b.nbins, b.iscat, None, 5, p)
-    ref.set_feature_groups(b.vmap)
+    ref.set_feature_groups(b.vmap, b.n_low)
     ref.build(aux, None, k_cols, seed=5, leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1]).float())
     tl_r = ref.pop_levels()[0]
     dev = torch.device("cuda", 0)
     gb = T.GpuTreeBuilder(apply_binning(b, X.to(dev), planar=b.stride >= 64), b.F, b.nbins, b.iscat, None, 5, p)
-    gb.set_feature_groups(b.vmap)
+    gb.set_feature_groups(b.vmap, b.n_low)
     gb.build(aux.to(dev), None, k_cols, seed=5, leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1]).float())
     tl_g = gb.pop_levels()[0]
     assert tl_g.n_leaves == tl_r.n_leaves
