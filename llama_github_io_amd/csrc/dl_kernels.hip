@@ -71,7 +71,42 @@ struct DLArgs {
   int ae, no_wsum;               // 1: autoencoder (outputs reconstruct the undropped inputs, quadratic loss / K);
                                 // no_wsum: the optimizer reads the split partials itself (no k_dl_wsum launch)
   float* wpart;                 // [tiles][wsplit][64 * 64] fp32 partial tiles, then the batch's 1 / sum(w)
+  // weight matrices staged in LDS for the launch (the layers after the first are small): byte offset of the
+  // copy of W / WT of GEMM layer li, -1 = read from global; stg_n16[li] = 16-byte units of one such matrix
+  int stg_w[DL_MAXL], stg_wt[DL_MAXL], stg_n16[DL_MAXL];
 };
+
+// Copies the staged weight matrices into LDS: up to 8 16-byte units per thread, every load issued before any
+// store (one memory round trip, overlapping the row-metadata loads that follow)
+#define DL_STAGE_U 8
+__device__ __forceinline__ void stage_weights(const DLArgs& a, unsigned char* smem) {
+  const uint4* Wg = reinterpret_cast<const uint4*>(a.W);
+  const uint4* WTg = reinterpret_cast<const uint4*>(a.WT);
+  const int esz = a.f32 ? 4 : 2;
+  uint4 v[DL_STAGE_U];
+  int dst[DL_STAGE_U];
+#pragma unroll
+  for (int u = 0; u < DL_STAGE_U; ++u) {
+    int idx = (int)threadIdx.x + u * DL_THREADS;
+    dst[u] = -1;
+    for (int sg = 0; sg < 2 * a.L; ++sg) {
+      const int li = sg >> 1;
+      const int off = (sg & 1) ? a.stg_wt[li] : a.stg_w[li];
+      if (off < 0) continue;
+      const int c16 = a.stg_n16[li];
+      if (idx < c16) {
+        const long long s16 = a.w_off[li] * esz / 16 + idx;
+        v[u] = (sg & 1) ? WTg[s16] : Wg[s16];
+        dst[u] = off + idx * 16;
+        break;
+      }
+      idx -= c16;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < DL_STAGE_U; ++u)
+    if (dst[u] >= 0) *reinterpret_cast<uint4*>(smem + dst[u]) = v[u];
+}
 
 #ifdef DL_TIMING
 // per-workgroup phase clocks of the last k_dl_rows launch (diagnostic build only: scripts/build_alt.sh dlt
@@ -221,6 +256,7 @@ __global__ __launch_bounds__(DL_THREADS) void k_dl_rows(DLArgs a) {
   const int L = a.L;
   const uint64_t step = a.step_dev ? *a.step_dev : 0ull;
   DLT(0);
+  stage_weights(a, smem);          // (beyond the zeroed tiles; ready after the first barrier)
   __shared__ long long srow[DL_ROWS];
   __shared__ float sy[DL_ROWS];
   __shared__ long long scls[DL_ROWS];
@@ -288,19 +324,20 @@ __global__ __launch_bounds__(DL_THREADS) void k_dl_rows(DLArgs a) {
     const T* Ain = S + a.lds_off[l - 1];
     T* Aout = S + a.lds_off[l];
     const int nin = a.n[l - 1], nout = a.n[l];
-    const bool vec = (nin % VE == 0) && (a.w_off[l - 1] % VE == 0);
+    const bool stg = a.stg_w[l - 1] >= 0;
+    const T* Wl = stg ? reinterpret_cast<const T*>(smem + a.stg_w[l - 1]) : Wg + a.w_off[l - 1];
+    const bool vec = (nin % VE == 0) && (stg || a.w_off[l - 1] % VE == 0);
     const float drop = a.drop[l - 1], keep = 1.f - drop;
     const uint32_t thr = (uint32_t)(drop * 4294967296.0);
     const uint64_t seed = a.seed_base[l - 1] ^ (step * 0x9E3779B97F4A7C15ULL);
     const int NT = (nout + 15) / 16;
     unsigned char* win = a.maxout ? smem + a.lds_mx[l] : nullptr;
     for (int t = wv; t < NT; t += DL_NW) {
-      const f32x4 acc = tile_mm(Ain, a.ld[l - 1], Wg + a.w_off[l - 1], nin, t * 16, nout, a.kp[l - 1], nin, vec);
+      const f32x4 acc = tile_mm(Ain, a.ld[l - 1], Wl, nin, t * 16, nout, a.kp[l - 1], nin, vec);
       // Maxout (Neurons.Maxout, 2 channels): channel 1 = weight / bias rows [nout, 2 nout)
       f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};
       if (a.maxout)
-        acc1 = tile_mm(Ain, a.ld[l - 1], Wg + a.w_off[l - 1] + (long long)nout * nin, nin, t * 16, nout, a.kp[l - 1], nin,
-                       vec);
+        acc1 = tile_mm(Ain, a.ld[l - 1], Wl + (long long)nout * nin, nin, t * 16, nout, a.kp[l - 1], nin, vec);
       const int col = t * 16 + c;
       f32x4 o;
       if (col < nout) {
@@ -332,10 +369,11 @@ __global__ __launch_bounds__(DL_THREADS) void k_dl_rows(DLArgs a) {
   if (a.K > 16) {
     float* LG = reinterpret_cast<float*>(smem + a.lds_lg);
     const int nin = a.n[L - 1], K = a.K;
-    const bool vec = (nin % VE == 0) && (a.w_off[L - 1] % VE == 0);
+    const bool stg = a.stg_w[L - 1] >= 0;
+    const T* Wo = stg ? reinterpret_cast<const T*>(smem + a.stg_w[L - 1]) : Wg + a.w_off[L - 1];
+    const bool vec = (nin % VE == 0) && (stg || a.w_off[L - 1] % VE == 0);
     for (int t = wv; t < (K + 15) / 16; t += DL_NW) {
-      const f32x4 acc = tile_mm(S + a.lds_off[L - 1], a.ld[L - 1], Wg + a.w_off[L - 1], nin, t * 16, K, a.kp[L - 1],
-                                nin, vec);
+      const f32x4 acc = tile_mm(S + a.lds_off[L - 1], a.ld[L - 1], Wo, nin, t * 16, K, a.kp[L - 1], nin, vec);
       const int col = t * 16 + c;
       if (col < K) {
         const float b = a.P[a.b_off[L - 1] + col];
@@ -385,8 +423,10 @@ __global__ __launch_bounds__(DL_THREADS) void k_dl_rows(DLArgs a) {
     }
   } else if (wv == 0) {
     const int nin = a.n[L - 1], K = a.K;
-    const bool vec = (nin % VE == 0) && (a.w_off[L - 1] % VE == 0);
-    const f32x4 acc = tile_mm(S + a.lds_off[L - 1], a.ld[L - 1], Wg + a.w_off[L - 1], nin, 0, K, a.kp[L - 1], nin, vec);
+    const bool stg = a.stg_w[L - 1] >= 0;
+    const T* Wo = stg ? reinterpret_cast<const T*>(smem + a.stg_w[L - 1]) : Wg + a.w_off[L - 1];
+    const bool vec = (nin % VE == 0) && (stg || a.w_off[L - 1] % VE == 0);
+    const f32x4 acc = tile_mm(S + a.lds_off[L - 1], a.ld[L - 1], Wo, nin, 0, K, a.kp[L - 1], nin, vec);
     const bool cok = c < K;
     const float b = cok ? a.P[a.b_off[L - 1] + c] : 0.f;
     f32x4 g;
@@ -424,7 +464,9 @@ __global__ __launch_bounds__(DL_THREADS) void k_dl_rows(DLArgs a) {
     const int nout = a.n[l], nnext = a.ng[l + 1];     // layer l+1's GEMM width (its WT rows)
     const int ldo = a.ldg[l];
     const unsigned char* win = a.maxout ? smem + a.lds_mx[l] : nullptr;
-    const bool vec = (nnext % VE == 0) && (a.w_off[l] % VE == 0);
+    const bool stg = a.stg_wt[l] >= 0;
+    const T* WTl = stg ? reinterpret_cast<const T*>(smem + a.stg_wt[l]) : WTg + a.w_off[l];
+    const bool vec = (nnext % VE == 0) && (stg || a.w_off[l] % VE == 0);
     const float drop = a.drop[l - 1], keep = 1.f - drop;
     const uint32_t thr = (uint32_t)(drop * 4294967296.0);
     const uint64_t seed = a.seed_base[l - 1] ^ (step * 0x9E3779B97F4A7C15ULL);
@@ -432,7 +474,7 @@ __global__ __launch_bounds__(DL_THREADS) void k_dl_rows(DLArgs a) {
     const int NT = (nout + 15) / 16;
     for (int t = wv; t < NT; t += DL_NW) {
       // dh = G_{l+1} W_{l+1}: B[k = unit of l+1][n = unit of l] = WT_{l+1}[n][k]
-      const f32x4 acc = tile_mm(Gin, ldg_in, WTg + a.w_off[l], nnext, t * 16, nout, a.kpg[l + 1], nnext, vec);
+      const f32x4 acc = tile_mm(Gin, ldg_in, WTl, nnext, t * 16, nout, a.kpg[l + 1], nnext, vec);
       const int col = t * 16 + c;
       f32x4 gd = {0.f, 0.f, 0.f, 0.f};
       if (col < nout) {

@@ -652,7 +652,7 @@ template <typename P, typename TO>
 __global__ __launch_bounds__(RW * 64) void k_hist_reduce(
     const P* __restrict__ partials, int slot_doubles, int used, const Node* __restrict__ nodes,
     const int* __restrict__ bp, const int* __restrict__ meta, int G, TO* __restrict__ out, int ostride,
-    double* __restrict__ hist_next, const double* __restrict__ hist_cur) {
+    double* __restrict__ hist_next, const double* __restrict__ hist_cur, int lo_F) {
   const int node = blockIdx.y;
   if (node >= meta[0]) return;
   const Node nd = nodes[node];
@@ -664,7 +664,14 @@ __global__ __launch_bounds__(RW * 64) void k_hist_reduce(
   const int b0 = t0 / per, b1 = t1 > t0 ? (t1 - 1) / per : b0 - 1;
   const int oslot = nd.parent >= 0 ? nd.parent : 0;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int i = blockIdx.x * 64 + lane;
+  int i = blockIdx.x * 64 + lane;
+  if (lo_F > 0) {
+    // narrow level: only the entries of columns < lo_F ([bin][lo_F][2] of the [bin][F][2] layout) and the tail
+    const int F = (used - 1) / (2 * NBIN + 1), lo2 = 2 * lo_F;
+    const int vb = NBIN * lo2;
+    if (i >= vb + F + 1) i = used;   // past the virtual range: idle lane
+    else i = i < vb ? (i / lo2) * 2 * F + i % lo2 : NBIN * 2 * F + (i - vb);
+  }
   const int ic = min(i, used - 1);
   // 4 independent loads in flight per lane; fixed summation order -> deterministic result
   double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
@@ -1939,11 +1946,14 @@ static void launch_hist(dim3 grid, size_t lds, hipStream_t s, const void* bins, 
 template <typename P, typename TO>
 static void reduce_launch(const void* partials, int slot_doubles, int used, const void* nodes, const void* bp,
                           const void* meta, int cap, int grid, void* out, int ostride, void* hist_next,
-                          const void* hist_cur, hipStream_t s) {
-  const int gx = (used + 63) / 64;
+                          const void* hist_cur, int lo_F, hipStream_t s) {
+  const int F = (used - 1) / (2 * NBIN + 1);
+  if (lo_F >= F) lo_F = 0;
+  const int n = lo_F > 0 ? NBIN * 2 * lo_F + F + 1 : used;
+  const int gx = (n + 63) / 64;
   hipLaunchKernelGGL((k_hist_reduce<P, TO>), dim3(gx, cap), dim3(RW * 64), 0, s, (const P*)partials, slot_doubles,
                      used, (const Node*)nodes, (const int*)bp, (const int*)meta, grid, (TO*)out, ostride,
-                     (double*)hist_next, (const double*)hist_cur);
+                     (double*)hist_next, (const double*)hist_cur, lo_F);
 }
 
 extern "C" {
@@ -1990,18 +2000,19 @@ int h2o_hist_build(const void* bins, int stride, const void* aw, const void* ay,
 
 // grid: the G the matching h2o_hist_build ran with; out / hist_next may be null (see k_hist_reduce).
 // out: compact build slots of ostride values (0: slot_doubles), fp32 when out_f32 (the exchange's wire dtype)
+// lo_F > 0 (narrow level): only the entries of columns < lo_F (and the NA / node tails) are summed
 int h2o_hist_reduce(const void* partials, int slot_doubles, int used, const void* nodes, const void* bp,
                     const void* meta, int cap, int grid, void* out, void* hist_next, const void* hist_cur,
-                    int f32, int out_f32, int ostride, hipStream_t s) {
+                    int f32, int out_f32, int ostride, int lo_F, hipStream_t s) {
   if (ostride <= 0) ostride = slot_doubles;
   if (f32 && out_f32)
-    reduce_launch<float, float>(partials, slot_doubles, used, nodes, bp, meta, cap, grid, out, ostride, hist_next, hist_cur, s);
+    reduce_launch<float, float>(partials, slot_doubles, used, nodes, bp, meta, cap, grid, out, ostride, hist_next, hist_cur, lo_F, s);
   else if (f32)
-    reduce_launch<float, double>(partials, slot_doubles, used, nodes, bp, meta, cap, grid, out, ostride, hist_next, hist_cur, s);
+    reduce_launch<float, double>(partials, slot_doubles, used, nodes, bp, meta, cap, grid, out, ostride, hist_next, hist_cur, lo_F, s);
   else if (out_f32)
-    reduce_launch<double, float>(partials, slot_doubles, used, nodes, bp, meta, cap, grid, out, ostride, hist_next, hist_cur, s);
+    reduce_launch<double, float>(partials, slot_doubles, used, nodes, bp, meta, cap, grid, out, ostride, hist_next, hist_cur, lo_F, s);
   else
-    reduce_launch<double, double>(partials, slot_doubles, used, nodes, bp, meta, cap, grid, out, ostride, hist_next, hist_cur, s);
+    reduce_launch<double, double>(partials, slot_doubles, used, nodes, bp, meta, cap, grid, out, ostride, hist_next, hist_cur, lo_F, s);
   return (int)hipGetLastError();
 }
 
@@ -2316,9 +2327,10 @@ int h2o_tree_root(const TreePlan* P, hipStream_t s) {
   // row-sharded all-reduce: straight into the wire buffer; sliced: hbuild (packed by slice next)
   if (P->dist && !P->sliced)
     return h2o_hist_reduce(P->partials, P->slot, P->used, P->nodes[0], P->bp[0], P->meta[0], 1, g0, P->hrecv, nullptr,
-                           nullptr, P->pf32, P->cf32, P->sslot, s);
+                           nullptr, P->pf32, P->cf32, P->sslot, tp_narrow(P, 0) ? P->lo_F : 0, s);
   return h2o_hist_reduce(P->partials, P->slot, P->used, P->nodes[0], P->bp[0], P->meta[0], 1, g0,
-                         P->sliced ? P->hbuild : P->hist0, nullptr, nullptr, P->pf32, 0, 0, s);
+                         P->sliced ? P->hbuild : P->hist0, nullptr, nullptr, P->pf32, 0, 0,
+                         tp_narrow(P, 0) ? P->lo_F : 0, s);
 }
 
 // split search of level d: every feature into cand, or (sliced) this rank's feature slice into cand_local.
@@ -2398,15 +2410,16 @@ int h2o_tree_grow(const TreePlan* P, int d, int dist, hipStream_t s) {
                         P->nbins_f, P->fine_f, tp_narrow(P, d + 1) ? tp_lo_planes(P) : 0, s);
   }
   if (rc) return -rc;
+  const int lo = tp_narrow(P, d + 1) ? P->lo_F : 0;
   if (!dist)
     rc = h2o_hist_reduce(P->partials, P->slot, P->used, P->nodes[d + 1], P->bp[d + 1], P->meta[d + 1], P->caps[d + 1],
-                         gh, nullptr, hn, hc, P->pf32, 0, 0, s);
+                         gh, nullptr, hn, hc, P->pf32, 0, 0, lo, s);
   else if (P->sliced)
     rc = h2o_hist_reduce(P->partials, P->slot, P->used, P->nodes[d + 1], P->bp[d + 1], P->meta[d + 1], P->caps[d + 1],
-                         gh, P->hbuild, nullptr, nullptr, P->pf32, 0, 0, s);
+                         gh, P->hbuild, nullptr, nullptr, P->pf32, 0, 0, lo, s);
   else   // all-reduce exchange: the build slots go straight into the wire buffer
     rc = h2o_hist_reduce(P->partials, P->slot, P->used, P->nodes[d + 1], P->bp[d + 1], P->meta[d + 1], P->caps[d + 1],
-                         gh, P->hrecv, nullptr, nullptr, P->pf32, P->cf32, P->sslot, s);
+                         gh, P->hrecv, nullptr, nullptr, P->pf32, P->cf32, P->sslot, lo, s);
   return rc ? -rc : 0;
 }
 
