@@ -206,6 +206,8 @@ class FusedMLPStep:
         # partial tiles, summed in split order by k_dl_wsum
         nch = Bpad // (16 if f32 else 32)
         a.wsplit = max(1, min(nch // 4, -(-768 // ts)))
+        if os.environ.get("H2O_DL_WSPLIT"):            # A/B: fewer splits = fewer partial bytes, less parallelism
+            a.wsplit = max(1, min(nch // 4, int(os.environ["H2O_DL_WSPLIT"])))
         self.wpart = torch.empty(ts * a.wsplit * 4096 + 1, dtype=torch.float32, device=dev)
         a.wpart = self.wpart.data_ptr()
         a.n_decay, a.n_total = fp.n_decay, fp.p.numel()

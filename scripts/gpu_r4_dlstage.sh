@@ -13,6 +13,10 @@ for st in 1 0; do
     echo "stage=$st $dt: $(tail -1 $O/bench_${dt}_$st.log | cut -c1-260)"
   done
 done
+for ws in 4 6 16; do
+  H2O_DL_WSPLIT=$ws timeout -k 10 200 python scripts/bench_suite.py --which dl --rows 2000000 --dtype bf16 > $O/bench_ws$ws.log 2>&1 || exit 1
+  echo "wsplit=$ws bf16: $(tail -1 $O/bench_ws$ws.log | cut -c1-200)"
+done
 for dt in bf16 float32; do
   H2O_HIP_LIB=$PWD/llama_github_io_amd/lib_alt/dlt.so timeout -k 10 240 python scripts/dl_phase_timing.py $dt > $O/phase_$dt.log 2>&1 || { tail -20 $O/phase_$dt.log; exit 1; }
   grep -v amdgpu.ids $O/phase_$dt.log
