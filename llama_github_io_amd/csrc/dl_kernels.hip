@@ -269,25 +269,35 @@ __global__ __launch_bounds__(DL_THREADS) void k_dl_rows(DLArgs a) {
     else if (a.regression) sy[tid] = g >= 0 ? a.yreg[g] : 0.f;
     else scls[tid] = g >= 0 ? a.ycls[g] : -1;
   }
-  // zero every activation / gradient tile (K padding must read as zeros)
+  // zero every activation / gradient tile (K padding must read as zeros) except the input rows' data columns,
+  // which the gather below writes in full — so the gather needs no barrier after the zeroing
+  T* A0 = S + a.lds_off[0];
+  const int n0 = a.n[0], ld0 = a.ld[0];
   {
     const int total = a.lds_w / 4;
-    for (int i = tid; i < total; i += DL_THREADS) reinterpret_cast<float*>(smem)[i] = 0.f;
+    const int a0s = a.lds_off[0] * (int)sizeof(T) / 4, a0e = (a.lds_off[0] + DL_ROWS * ld0) * (int)sizeof(T) / 4;
+    for (int i = tid; i < total; i += DL_THREADS)
+      if (i < a0s || i >= a0e) reinterpret_cast<float*>(smem)[i] = 0.f;
+    const int pw = ld0 - n0;
+    for (int i = tid; i < DL_ROWS * pw; i += DL_THREADS) A0[(i / pw) * ld0 + n0 + i % pw] = from_f<T>(0.f);
   }
-  __syncthreads();
   DLT(1);
-  // ---- gather the 16 input rows into activation tile 0
+  // ---- gather the 16 input rows into activation tile 0: each thread reads its row's index itself (one
+  // dependent round trip, index -> row, instead of index -> barrier -> row); padding rows are zero
   {
-    T* A0 = S + a.lds_off[0];
-    const int n0 = a.n[0], ld0 = a.ld[0];
     const bool vec = (n0 % VE == 0) && (a.ldz % VE == 0);
     const int chunks = (n0 + VE - 1) / VE;
     for (int i = tid; i < DL_ROWS * chunks; i += DL_THREADS) {
       const int rr = i / chunks, k = (i - rr * chunks) * VE;
-      const long long g = srow[rr];
-      if (g < 0) continue;
-      const T* src = Zg + g * a.ldz;
+      const int r = r0 + rr;
+      const long long g = r < a.B ? a.ridx[r] : -1;
       T* dst = A0 + rr * ld0 + k;
+      if (g < 0) {
+        if (vec) *reinterpret_cast<uint4*>(dst) = make_uint4(0u, 0u, 0u, 0u);
+        else for (int j = 0; j < VE && k + j < n0; ++j) dst[j] = from_f<T>(0.f);
+        continue;
+      }
+      const T* src = Zg + g * a.ldz;
       if (vec) *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src + k);
       else for (int j = 0; j < VE && k + j < n0; ++j) dst[j] = src[k + j];
     }
