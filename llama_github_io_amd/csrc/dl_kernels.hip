@@ -85,23 +85,26 @@ __device__ __forceinline__ void stage_weights(const DLArgs& a, unsigned char* sm
   const int esz = a.f32 ? 4 : 2;
   uint4 v[DL_STAGE_U];
   int dst[DL_STAGE_U];
+  // fixed trip counts, no early exit: the unit arrays stay in registers (a data-dependent break sent them to scratch)
 #pragma unroll
   for (int u = 0; u < DL_STAGE_U; ++u) {
     int idx = (int)threadIdx.x + u * DL_THREADS;
-    dst[u] = -1;
-    for (int sg = 0; sg < 2 * a.L; ++sg) {
+    const uint4* src = Wg;
+    int d = -1;
+#pragma unroll
+    for (int sg = 0; sg < 2 * DL_MAXL; ++sg) {
       const int li = sg >> 1;
       const int off = (sg & 1) ? a.stg_wt[li] : a.stg_w[li];
-      if (off < 0) continue;
-      const int c16 = a.stg_n16[li];
-      if (idx < c16) {
-        const long long s16 = a.w_off[li] * esz / 16 + idx;
-        v[u] = (sg & 1) ? WTg[s16] : Wg[s16];
-        dst[u] = off + idx * 16;
-        break;
+      const int c16 = (li < a.L && off >= 0) ? a.stg_n16[li] : 0;
+      const bool hit = d < 0 && idx < c16;
+      if (hit) {
+        src = ((sg & 1) ? WTg : Wg) + a.w_off[li] * esz / 16 + idx;
+        d = off + idx * 16;
       }
-      idx -= c16;
+      if (d < 0) idx -= c16;
     }
+    v[u] = d >= 0 ? *src : make_uint4(0u, 0u, 0u, 0u);
+    dst[u] = d;
   }
 #pragma unroll
   for (int u = 0; u < DL_STAGE_U; ++u)
@@ -212,6 +215,48 @@ __device__ __forceinline__ f32x4 tile_mm(const float* A, int lda, const float* B
         acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b[u].w, acc, 0, 0, 0);
       }
     }
+  }
+  return acc;
+}
+
+// D = A(LDS tile, 16 x K) * B with B[k][n] = W[k * ldw + n] (W in LDS, rows along n): the backward pass reading a
+// staged forward weight matrix in place of its transposed copy (8 / 4 scalar LDS reads per MFMA operand)
+__device__ __forceinline__ f32x4 tile_mm_tl(const bf16* A, int lda, const bf16* W, int ldw, int n0, int nvalid, int K,
+                                            int kvalid) {
+  const int lane = threadIdx.x & 63, q = lane >> 4, c = lane & 15;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  const int n = n0 + c;
+  const bool nok = n < nvalid;
+  for (int kb = 0; kb < K; kb += 32) {
+    bf16x8 b;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = kb + 8 * q + j;
+      b[j] = (nok && k < kvalid) ? (__bf16)__bfloat162float(W[k * ldw + n]) : (__bf16)0.f;
+    }
+    const bf16x8 av = *reinterpret_cast<const bf16x8*>(A + c * lda + kb + 8 * q);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, b, acc, 0, 0, 0);
+  }
+  return acc;
+}
+__device__ __forceinline__ f32x4 tile_mm_tl(const float* A, int lda, const float* W, int ldw, int n0, int nvalid, int K,
+                                            int kvalid) {
+  const int lane = threadIdx.x & 63, q = lane >> 4, c = lane & 15;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  const int n = n0 + c;
+  const bool nok = n < nvalid;
+  for (int kb = 0; kb < K; kb += 16) {
+    const float4 av = *reinterpret_cast<const float4*>(A + c * lda + kb + 4 * q);
+    float bv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = kb + 4 * q + j;
+      bv[j] = (nok && k < kvalid) ? W[k * ldw + n] : 0.f;
+    }
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv[1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv[2], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv[3], acc, 0, 0, 0);
   }
   return acc;
 }
@@ -477,6 +522,8 @@ __global__ __launch_bounds__(DL_THREADS) void k_dl_rows(DLArgs a) {
     const bool stg = a.stg_wt[l] >= 0;
     const T* WTl = stg ? reinterpret_cast<const T*>(smem + a.stg_wt[l]) : WTg + a.w_off[l];
     const bool vec = (nnext % VE == 0) && (stg || a.w_off[l] % VE == 0);
+    // no staged transpose but the forward matrix W_{l+1} [nnext][nout] is staged: read it transposed on chip
+    const T* Wtl = (!stg && a.stg_w[l] >= 0) ? reinterpret_cast<const T*>(smem + a.stg_w[l]) : nullptr;
     const float drop = a.drop[l - 1], keep = 1.f - drop;
     const uint32_t thr = (uint32_t)(drop * 4294967296.0);
     const uint64_t seed = a.seed_base[l - 1] ^ (step * 0x9E3779B97F4A7C15ULL);
@@ -484,7 +531,8 @@ __global__ __launch_bounds__(DL_THREADS) void k_dl_rows(DLArgs a) {
     const int NT = (nout + 15) / 16;
     for (int t = wv; t < NT; t += DL_NW) {
       // dh = G_{l+1} W_{l+1}: B[k = unit of l+1][n = unit of l] = WT_{l+1}[n][k]
-      const f32x4 acc = tile_mm(Gin, ldg_in, WTl, nnext, t * 16, nout, a.kpg[l + 1], nnext, vec);
+      const f32x4 acc = Wtl ? tile_mm_tl(Gin, ldg_in, Wtl, nout, t * 16, nout, a.kpg[l + 1], nnext)
+                            : tile_mm(Gin, ldg_in, WTl, nnext, t * 16, nout, a.kpg[l + 1], nnext, vec);
       const int col = t * 16 + c;
       f32x4 gd = {0.f, 0.f, 0.f, 0.f};
       if (col < nout) {

@@ -176,7 +176,8 @@ class FusedMLPStep:
         # weight matrices of the layers after the first staged in LDS per launch (k_dl_rows stage_weights): the
         # forward of layer 2+, the output layer and the backward through WT read them on chip instead of as one
         # dependent L2/HBM round trip per layer. Greedy in order of use within the LDS left (and 8 16-byte units
-        # per thread); H2O_DL_STAGE=0 keeps every weight read global.
+        # per thread); a transpose is staged only when its forward matrix is not (the backward then reads W
+        # transposed in LDS). H2O_DL_STAGE=0 keeps every weight read global.
         for li in range(MAXL):
             a.stg_w[li] = a.stg_wt[li] = -1
             a.stg_n16[li] = 0
@@ -188,6 +189,8 @@ class FusedMLPStep:
                 nb = ng[li + 1] * n[li] * cesz
                 if nb % 16 or a.w_off[li] % ve or staged + nb > room:
                     continue
+                if kind == "wt" and a.stg_w[li] >= 0 and os.environ.get("H2O_DL_STAGE_WT") != "1":
+                    continue            # the backward reads the staged forward matrix transposed (tile_mm_tl)
                 off = (self.lds + 15) // 16 * 16
                 getattr(a, "stg_" + kind)[li] = off
                 a.stg_n16[li] = nb // 16
