@@ -1650,8 +1650,9 @@ __global__ __launch_bounds__(256) void k_leaf_assign(
         if (e.x < 0) {
           c = e.z;                               // terminal node: child_l == child_r == its leaf
         } else {
-          const int b = NV > 2 ? row_byte4(v0, v1, v2, v3, e.x) : NV > 0 ? row_byte(v0, v1, e.x)
-                                                                         : bins[bin_off(row, e.x, stride, N, planar)];
+          const int b = (NV > 0 && e.x >= NV * 16) ? bins[bin_off(row, e.x, stride, N, planar)]
+                        : NV > 2 ? row_byte4(v0, v1, v2, v3, e.x) : NV > 0 ? row_byte(v0, v1, e.x)
+                                 : bins[bin_off(row, e.x, stride, N, planar)];
           bool gl;
           if (b == NA_BIN) gl = (e.y >> 16) & 1;
           else if ((e.y >> 17) & 1) gl = (lv[d].dec[i].bits[b >> 5] >> (b & 31)) & 1u;
@@ -1664,8 +1665,9 @@ __global__ __launch_bounds__(256) void k_leaf_assign(
         if (f < 0) {
           c = lv[d].cl[i];
         } else {
-          const int b = NV > 2 ? row_byte4(v0, v1, v2, v3, f) : NV > 0 ? row_byte(v0, v1, f)
-                                                                       : bins[bin_off(row, f, stride, N, planar)];
+          const int b = (NV > 0 && f >= NV * 16) ? bins[bin_off(row, f, stride, N, planar)]
+                        : NV > 2 ? row_byte4(v0, v1, v2, v3, f) : NV > 0 ? row_byte(v0, v1, f)
+                                 : bins[bin_off(row, f, stride, N, planar)];
           c = dec_go_left(dc, b) ? lv[d].cl[i] : lv[d].cr[i];
         }
       }
@@ -2160,7 +2162,9 @@ static int leaf_assign_launch(const void* master, int stride, long long N, const
 #define LA(NV) hipLaunchKernelGGL((k_leaf_assign<NV>), dim3((unsigned)grid), dim3(256), lds, s, (const uint8_t*)master, \
                                   stride, N, (const LevelPtrs*)lvptrs, D, (const float*)an, (const float*)ad,          \
                                   (const double*)qs, (int*)leaf_of_row, (unsigned long long*)leafq, leaf_cap, n_nodes, planar)
-  switch (nv_of(stride)) {
+  // planar rows of more than two planes: the first two planes in registers (every feature of the narrow levels),
+  // split bytes of later planes loaded per level
+  switch ((planar && stride > 64 && !route_generic()) ? 4 : nv_of(stride)) {
     case 4: LA(4); break;
     case 3: LA(3); break;
     case 2: LA(2); break;
@@ -2274,10 +2278,11 @@ struct TreePlan {
   void *hsend, *cand_all, *lsx;  // [W][n][E] packed send slots, [W][cap][Fs] candidates, leaf sums + root weight
   void* fine_f;               // [F] int32: columns of word-aligned 4-column wide numeric groups (or null)
   // narrow levels of wide numeric bins (ops/binning.py layout: columns [0, lo_F) hold every feature's first
-  // column, the other interleaved edge subsets follow): from level lo_from on (adaptive bin count <= 256) only
-  // columns < lo_F are histogrammed and searched, and the routes that feed those levels move only the planes
-  // holding them. lo_F = 0: off.
-  int lo_F, lo_from;
+  // column, [lo_F, mid_F) the subsets that halve the edge spacing, the rest follow): from level lo_from on
+  // (adaptive bin count <= 256) only columns < lo_F, from mid_from on (<= 512) only columns < mid_F are
+  // histogrammed, reduced and searched, and the routes that feed such levels move only the planes holding them.
+  // lo_F / mid_F = 0: off.
+  int lo_F, lo_from, mid_F, mid_from;
 };
 
 // op codes / dtypes of the collective transport
@@ -2296,15 +2301,21 @@ static inline void tp_level_buf(const TreePlan* P, int e, const void*& b, const 
   b = P->bb[i]; y = P->by[i]; w = P->unit ? nullptr : P->bw[i];
 }
 
-static inline bool tp_narrow(const TreePlan* P, int d) { return P->lo_F > 0 && d >= P->lo_from; }
-static inline int tp_lo_planes(const TreePlan* P) { return (P->lo_F + FTILE - 1) / FTILE; }
+// columns level d searches (0 = all) and the planes (feature tiles) holding them
+static inline int tp_fcut(const TreePlan* P, int d) {
+  if (P->lo_F > 0 && d >= P->lo_from) return P->lo_F;
+  if (P->mid_F > 0 && d >= P->mid_from) return P->mid_F;
+  return 0;
+}
+static inline int tp_planes(int fc) { return fc > 0 ? (fc + FTILE - 1) / FTILE : 0; }
 
 static int tp_route(const TreePlan* P, int e, hipStream_t s) {
   const void *sb, *sy, *sw;
   tp_level_buf(P, e, sb, sy, sw);
   const int di = (e / 2) % 2;
   // rows of level e + 2 (and below) are read by narrow levels only: move just the low planes
-  const int lp = (tp_narrow(P, e + 2) && P->planar && tp_lo_planes(P) <= 2) ? tp_lo_planes(P) : 0;
+  const int np = tp_planes(tp_fcut(P, e + 2));
+  const int lp = (P->planar && np <= 2) ? np : 0;
   return h2o_route(sb, sy, sw, P->bb[di], P->by[di], P->unit ? nullptr : P->bw[di], P->stride, P->nodes[e], P->tp[e],
                    P->meta[e], P->dec[e], P->cl[e], P->cr[e], P->dec[e + 1], P->cl[e + 1], P->cr[e + 1],
                    P->cur[e + 1], P->tiles_cap[e], P->N, P->planar, lp, s);
@@ -2323,14 +2334,14 @@ int h2o_tree_root(const TreePlan* P, hipStream_t s) {
   const int g0 = P->tiles_cap[0] < P->grid ? P->tiles_cap[0] : P->grid;
   TP_CHECK(h2o_hist_build(P->master, P->stride, P->unit ? nullptr : tp_aux(P, 0), tp_aux(P, 1), P->nodes[0], P->bp[0],
                           P->meta[0], P->F, P->partials, P->slot, P->qs, g0, P->packed, nullptr, nullptr, P->pf32, P->N,
-                          P->planar | (P->no_na << 1), P->nbins_f, P->fine_f, tp_narrow(P, 0) ? tp_lo_planes(P) : 0, s));
+                          P->planar | (P->no_na << 1), P->nbins_f, P->fine_f, tp_planes(tp_fcut(P, 0)), s));
   // row-sharded all-reduce: straight into the wire buffer; sliced: hbuild (packed by slice next)
   if (P->dist && !P->sliced)
     return h2o_hist_reduce(P->partials, P->slot, P->used, P->nodes[0], P->bp[0], P->meta[0], 1, g0, P->hrecv, nullptr,
-                           nullptr, P->pf32, P->cf32, P->sslot, tp_narrow(P, 0) ? P->lo_F : 0, s);
+                           nullptr, P->pf32, P->cf32, P->sslot, tp_fcut(P, 0), s);
   return h2o_hist_reduce(P->partials, P->slot, P->used, P->nodes[0], P->bp[0], P->meta[0], 1, g0,
                          P->sliced ? P->hbuild : P->hist0, nullptr, nullptr, P->pf32, 0, 0,
-                         tp_narrow(P, 0) ? P->lo_F : 0, s);
+                         tp_fcut(P, 0), s);
 }
 
 // split search of level d: every feature into cand, or (sliced) this rank's feature slice into cand_local.
@@ -2341,7 +2352,7 @@ int h2o_tree_find(const TreePlan* P, int d, hipStream_t s) {
   SplitParams p;
   p.min_w = P->min_w; p.min_split_improvement = P->msi; p.lambda = P->lam; p.alpha = P->alpha; p.gamma = P->gamma;
   p.mode = P->mode; p.random_split = P->random_split; p.seed = P->seed; p.hist_type = P->hist_type;
-  p.fcut = tp_narrow(P, d) ? P->lo_F : 0;
+  p.fcut = tp_fcut(P, d);
   const int hs = P->sliced ? P->sslot : P->slot;
   const Derive dv = P->dist ? Derive{P->hrecv, P->cf32, P->sslot, (const double*)hp, (const Node*)P->nodes[d]}
                             : Derive{nullptr, 0, 0, nullptr, nullptr};
@@ -2396,7 +2407,7 @@ int h2o_tree_grow(const TreePlan* P, int d, int dist, hipStream_t s) {
     tp_level_buf(P, d, sb, sy, sw);
     rc = h2o_hist_build(sb, P->stride, sw, sy, P->nodes[d + 1], P->bp[d + 1], P->meta[d + 1], P->F, P->partials,
                         P->slot, P->qs, gh, P->packed, P->dec[d], P->nl[d], P->pf32, P->N, P->planar | (P->no_na << 1),
-                        P->nbins_f, P->fine_f, tp_narrow(P, d + 1) ? tp_lo_planes(P) : 0, s);
+                        P->nbins_f, P->fine_f, tp_planes(tp_fcut(P, d + 1)), s);
   } else {
     // regroup level d-1's rows two levels down, then histogram level d+1 (even) contiguously
     rc = tp_route(P, d - 1, s);
@@ -2407,10 +2418,10 @@ int h2o_tree_grow(const TreePlan* P, int d, int dist, hipStream_t s) {
     tp_level_buf(P, d + 1, sb, sy, sw);
     rc = h2o_hist_build(sb, P->stride, sw, sy, P->nodes[d + 1], P->bp[d + 1], P->meta[d + 1], P->F, P->partials,
                         P->slot, P->qs, gh, P->packed, nullptr, nullptr, P->pf32, P->N, P->planar | (P->no_na << 1),
-                        P->nbins_f, P->fine_f, tp_narrow(P, d + 1) ? tp_lo_planes(P) : 0, s);
+                        P->nbins_f, P->fine_f, tp_planes(tp_fcut(P, d + 1)), s);
   }
   if (rc) return -rc;
-  const int lo = tp_narrow(P, d + 1) ? P->lo_F : 0;
+  const int lo = tp_fcut(P, d + 1);
   if (!dist)
     rc = h2o_hist_reduce(P->partials, P->slot, P->used, P->nodes[d + 1], P->bp[d + 1], P->meta[d + 1], P->caps[d + 1],
                          gh, nullptr, hn, hc, P->pf32, 0, 0, lo, s);

@@ -251,7 +251,7 @@ class SharedTreeTrainer:
         self.builder = T.make_builder(bins, bn.F, bn.nbins, bn.iscat, bn.expand(mono), max_depth,
                                       self._split_params(), node_cap=node_cap)
         if bn.vmap is not None:
-            self.builder.set_feature_groups(bn.vmap, getattr(bn, "n_low", 0))
+            self.builder.set_feature_groups(bn.vmap, getattr(bn, "n_low", 0), getattr(bn, "n_mid", 0))
         if p.get("interaction_constraints"):
             icm, root = interaction_map(p["interaction_constraints"], info.x)
             if bn.vmap is not None:

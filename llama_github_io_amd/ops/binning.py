@@ -48,6 +48,7 @@ class Binning:
     level_to_bin: list = field(default_factory=list)  # per feature: int array (None = identity)
     vmap: np.ndarray | None = None  # int32 [F] engine column -> original feature (None: identity)
     n_low: int = 0                  # engine columns [0, n_low) = every feature's first column (narrow view), 0: none
+    n_mid: int = 0                  # [0, n_mid): + the subsets halving the edge spacing (512-bin levels), 0: none
 
     # every per-feature field above is per ENGINE column (F of them); see the module note on wide bins
     @property
@@ -69,7 +70,8 @@ class Binning:
         return dict(F=self.F, stride=self.stride, edges=[None if e is None else e.tolist() for e in self.edges],
                     nbins=self.nbins.tolist(), iscat=self.iscat.tolist(), nlevels=self.nlevels.tolist(),
                     level_to_bin=[None if m is None else m.tolist() for m in self.level_to_bin],
-                    vmap=None if self.vmap is None else self.vmap.tolist(), n_low=int(self.n_low))
+                    vmap=None if self.vmap is None else self.vmap.tolist(), n_low=int(self.n_low),
+                    n_mid=int(self.n_mid))
 
     @staticmethod
     def from_state(s):
@@ -78,7 +80,7 @@ class Binning:
                        np.asarray(s["nlevels"], dtype=np.int32),
                        [None if m is None else np.asarray(m, dtype=np.int64) for m in s["level_to_bin"]],
                        None if s.get("vmap") is None else np.asarray(s["vmap"], dtype=np.int32),
-                       int(s.get("n_low", 0)))
+                       int(s.get("n_low", 0)), int(s.get("n_mid", 0)))
 
 
 def sample_rows(X: torch.Tensor, sample: int, seed: int, row0: int = 0, n_glob: int | None = None) -> torch.Tensor:
@@ -174,19 +176,20 @@ def fit_binning(X: torch.Tensor, iscat, nlevels=None, max_bins: int = MAX_DATA_B
         edges.append(e)
         nbins[f] = e.size + 1
     vmap = None
-    n_low = 0
+    n_low = n_mid = 0
     wide_cat = [bool(iscat[f]) and nbins[f] > SUB_EDGES for f in range(F)]
     if any(e is not None and e.size > SUB_EDGES for e in edges) or any(wide_cat):
         # wide numeric features -> n adjacent engine columns with the interleaved edge subsets e[k::n];
         # wide categoricals -> n adjacent engine columns of (at most) 254 consecutive bins each
-        # Layout: every feature's FIRST column (edge subset e[0::n], ~254 quantile edges; all blocks of a wide
-        # categorical) leads, the other subsets follow: from the level on where the adaptive bin count drops to
-        # 256 the tree searches only the leading n_low columns (ops/tree.narrow_from), whose planes alone are
-        # histogrammed and moved. H2O_HIST_FINE=1 keeps the former layout instead: the features of exactly 4
-        # interleaved columns first, each filling one aligned 4-byte row word (one fine-bin atomic per row and
-        # feature in the histogram kernel).
+        # Layout in three tiers: every feature's FIRST column (edge subset e[0::n], ~254 quantile edges; all blocks
+        # of a wide categorical), then the other subsets except the odd ones of 4-column features (with k = 2
+        # these halve the edge spacing: e[0::4] + e[2::4] = e[0::2]), then those odd subsets. From the level on
+        # where the adaptive bin count drops to 512 the tree searches only the first two tiers (n_mid columns),
+        # from 256 only the first (n_low; ops/tree.narrow_cut): only their planes are histogrammed and moved.
+        # H2O_HIST_FINE=1 keeps the former layout instead: the features of exactly 4 interleaved columns first,
+        # each filling one aligned 4-byte row word (one fine-bin atomic per row and feature in the histogram kernel).
         fine_layout = os.environ.get("H2O_HIST_FINE") == "1"
-        quad, rest, low, high = [], [], [], []
+        quad, rest, low, mid, high = [], [], [], [], []
         for f in range(F):
             e = edges[f]
             if wide_cat[f]:
@@ -205,12 +208,13 @@ def fit_binning(X: torch.Tensor, iscat, nlevels=None, max_bins: int = MAX_DATA_B
                 ek = e if n == 1 else np.ascontiguousarray(e[k::n])
                 c = (f, ek, (ek.size + 1) if e is not None else nbins[f], l2b[f])
                 (quad if n == 4 else rest).append(c)
-                (low if k == 0 else high).append(c)
+                (low if k == 0 else high if (n == 4 and k % 2) else mid).append(c)
         if fine_layout:
             cols = quad + rest
         else:
-            cols = low + high
-            n_low = len(low) if high else 0
+            cols = low + mid + high
+            n_low = len(low) if (mid or high) else 0
+            n_mid = len(low) + len(mid) if high else 0
         vmap = np.asarray([c[0] for c in cols], dtype=np.int32)
         edges = [c[1] for c in cols]
         nbins = np.asarray([c[2] for c in cols], dtype=np.int32)
@@ -222,7 +226,7 @@ def fit_binning(X: torch.Tensor, iscat, nlevels=None, max_bins: int = MAX_DATA_B
     # > 32 features: whole 32-byte planes (the device engine stores such bins PLANAR, one plane per
     # histogram feature tile — apply_binning(planar=True))
     stride = (F + 3) // 4 * 4 if F <= 12 else ((F + 15) // 16 * 16 if F <= 32 else (F + 31) // 32 * 32)
-    return Binning(F, stride, edges, nbins, iscat, nlevels, l2b, vmap, n_low)
+    return Binning(F, stride, edges, nbins, iscat, nlevels, l2b, vmap, n_low, n_mid)
 
 
 def _edge_table(b: Binning, device):

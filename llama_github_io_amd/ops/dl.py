@@ -177,11 +177,13 @@ class FusedMLPStep:
         # forward of layer 2+, the output layer and the backward through WT read them on chip instead of as one
         # dependent L2/HBM round trip per layer. Greedy in order of use within the LDS left (and 8 16-byte units
         # per thread); a transpose is staged only when its forward matrix is not (the backward then reads W
-        # transposed in LDS). H2O_DL_STAGE=0 keeps every weight read global.
+        # transposed in LDS). Off by default (H2O_DL_STAGE=1): MEASURED r4 (bf16 [200,200], phase clocks) the
+        # staging loads cost ~5 us at kernel start (the weights the previous launch wrote come from MALL/HBM to
+        # every CU) while the later phases gained < 0.4 us each: latency there is not the weight reads.
         for li in range(MAXL):
             a.stg_w[li] = a.stg_wt[li] = -1
             a.stg_n16[li] = 0
-        if os.environ.get("H2O_DL_STAGE", "1") == "1":
+        if os.environ.get("H2O_DL_STAGE", "0") == "1":
             ve = 16 // cesz
             room = min(150 * 1024 - self.lds, 8 * 1024 * 16)
             staged = 0

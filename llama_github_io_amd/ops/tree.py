@@ -54,26 +54,40 @@ def fine_columns(fgroup, iscat, F):
     g = np.asarray(fgroup, dtype=np.int64)
     out = np.zeros(F, dtype=np.int32)
     for m in range(0, F - 3, 4):
-        if (g[m] == g[m + 3] and (m == 0 or g[m - 1] != g[m]) and (m + 4 >= F or g[m + 4] != g[m])
+        if (g[m] == g[m + 1] == g[m + 2] == g[m + 3] and (m == 0 or g[m - 1] != g[m]) and (m + 4 >= F or g[m + 4] != g[m])
                 and not any(int(iscat[m + l]) for l in range(4))):
             out[m:m + 4] = 1
     return out if out.any() else None
 
 
-def narrow_from(p: "SplitParams", n_low: int, F: int) -> int:
-    """First level of the NARROW view of wide numeric bins (or -1): with an adaptive histogram type, levels whose
-    bin count max(nbins, nbins_top_level >> d) is at most 256 search only engine columns [0, n_low) — every
-    feature's first interleaved edge subset (ops/binning.py layout), i.e. their cut points snap to a ~254-edge
-    quantile sub-lattice instead of all ~1016 edges — so their histograms, searches and row moves cost what a
-    255-bin QuantilesGlobal run does (H2O_TREE_NARROW=0: every level searches every column)."""
-    if n_low <= 0 or n_low >= F or os.environ.get("H2O_TREE_NARROW", "1") == "0":
-        return -1
-    if not p.adapt_nbins or p.edges is None:
-        return -1
+def narrow_cut(p: "SplitParams", n_low: int, n_mid: int, F: int):
+    """Columns each level searches under the NARROW views of wide numeric bins: ``(mid_from, lo_from)``, the first
+    levels (or -1) from which only engine columns [0, n_mid) resp. [0, n_low) are searched (ops/binning.py three-tier
+    layout). With an adaptive histogram type a level whose bin count max(nbins, nbins_top_level >> d) is at most
+    512 needs no finer edge spacing than every other fine edge (the first two tiers), at most 256 than every fourth
+    (the first tier, ~254 quantile edges); their histograms, searches and row moves then cost what a 2x / 1x
+    255-bin QuantilesGlobal run does. H2O_TREE_NARROW=0: every level searches every column."""
+    off = (-1, -1)
+    if os.environ.get("H2O_TREE_NARROW", "1") == "0" or not p.adapt_nbins or p.edges is None:
+        return off
+    lo = mid = -1
     for d in range(64):
-        if 0 < p.adapt_nb(d) <= 256:
-            return d
-    return -1
+        nb = p.adapt_nb(d)
+        if mid < 0 and 0 < n_mid < F and 0 < nb <= 512:
+            mid = d
+        if lo < 0 and 0 < n_low < F and 0 < nb <= 256:
+            lo = d
+    return mid, lo
+
+
+def level_fcut(cut, n_low: int, n_mid: int, d: int) -> int:
+    """Columns level ``d`` searches (0 = all) for ``cut = narrow_cut(...)``."""
+    mid, lo = cut
+    if lo >= 0 and d >= lo:
+        return n_low
+    if mid >= 0 and d >= mid:
+        return n_mid
+    return 0
 
 
 def encode_groups(fgroup) -> np.ndarray | None:
@@ -431,18 +445,18 @@ class RefTreeBuilder:
         self.node_cap = node_cap
         self.N = self.bins.shape[0]
         self.ic_map = None
-        self.n_low = 0
+        self.n_low = self.n_mid = 0
 
     def set_interaction_constraints(self, ic_map, root_ok):
         """``ic_map`` [F, F] (row f: features allowed to interact with f), ``root_ok`` [F]."""
         self.ic_map = np.asarray(ic_map, dtype=np.uint8)
         self.ic_root = np.asarray(root_ok, dtype=np.uint8)
 
-    def set_feature_groups(self, fgroup, n_low: int = 0):
+    def set_feature_groups(self, fgroup, n_low: int = 0, n_mid: int = 0):
         """Engine column -> original feature (wide numeric features span several columns): column sampling
-        draws original features. ``n_low``: leading columns of the narrow view (:func:`narrow_from`)."""
+        draws original features. ``n_low`` / ``n_mid``: leading columns of the narrow views (:func:`narrow_cut`)."""
         self.fgroup = None if fgroup is None else np.asarray(fgroup, dtype=np.int64)
-        self.n_low = int(n_low)
+        self.n_low, self.n_mid = int(n_low), int(n_mid)
 
     def _hist(self, rows, aux):
         F = self.F
@@ -467,7 +481,7 @@ class RefTreeBuilder:
         F, D, p = self.F, self.D, self.p
         feat_ok = np.ones(F, dtype=np.int32) if feat_ok is None else np.asarray(feat_ok)
         leaf_of_row = np.full(self.N, -1, dtype=np.int64)
-        lo_from = narrow_from(p, self.n_low, F)
+        cut = narrow_cut(p, self.n_low, self.n_mid, F)
         leafsum = []
         level_rows = [np.arange(self.N)]
         level_ok = [None if self.ic_map is None else self.ic_root]
@@ -487,8 +501,9 @@ class RefTreeBuilder:
                     nayy = flat[h.size: h.size + F]
                     wyy = float(flat[-1])
                 cands = split_find_ref(h, nayy, wyy, self.nbins_f, self.iscat_f, self.mono_f, p, d, i, seed)
-                if 0 <= lo_from <= d:           # narrow level: the columns past n_low are not searched
-                    for f in range(self.n_low, F):
+                fc = level_fcut(cut, self.n_low, self.n_mid, d)
+                if fc:                          # narrow level: the columns past fc are not searched
+                    for f in range(fc, F):
                         cands[f]["valid"] = False
                 dl[i] = split_reduce_ref(cands, feat_ok, _level_k(k_cols, d), seed, d, i, level_ok[i],
                                          getattr(self, "fgroup", None))
@@ -570,7 +585,7 @@ class _TreePlan(ctypes.Structure):
                 [("leaf_lam", _cd), ("leaf_l1", _cd)] + [("planar", _ci), ("no_na", _ci)] +
                 [("fgroup", _vp)] + [("coll_fn", _vp), ("coll_ctx", _vp)] +
                 [(n, _ci) for n in ("W", "cf32", "cand_fs", "dist")] + [(n, _vp) for n in ("hsend", "cand_all", "lsx")] +
-                [("fine_f", _vp)] + [("lo_F", _ci), ("lo_from", _ci)])
+                [("fine_f", _vp)] + [(n, _ci) for n in ("lo_F", "lo_from", "mid_F", "mid_from")])
 
 
 class _Arena:
@@ -659,7 +674,7 @@ class GpuTreeBuilder:
         self.iscat_f = torch.as_tensor(np.asarray(iscat_f, dtype=np.int32), device=dev)
         self.iscat_np = np.asarray(iscat_f, dtype=np.int32)
         self.fine_f = None
-        self.n_low = 0
+        self.n_low = self.n_mid = 0
         self.mono_f = None if mono_f is None else torch.as_tensor(np.asarray(mono_f, dtype=np.int32), device=dev)
         self.feat_ok_all = torch.ones(F, dtype=torch.int32, device=dev)
         self.qs = torch.zeros(16, dtype=torch.float64, device=dev)  # fixed-point scales (k_qscale)
@@ -794,23 +809,24 @@ class GpuTreeBuilder:
         if getattr(self, "_plan", None) is not None:
             self._set_plan_ic(self._plan)
 
-    def set_feature_groups(self, fgroup, n_low: int = 0):
-        """Engine column -> original feature (k_split_reduce column sampling by original feature); ``n_low``:
-        leading columns of the narrow view (:func:`narrow_from`)."""
+    def set_feature_groups(self, fgroup, n_low: int = 0, n_mid: int = 0):
+        """Engine column -> original feature (k_split_reduce column sampling by original feature); ``n_low`` /
+        ``n_mid``: leading columns of the narrow views (:func:`narrow_cut`)."""
         enc = encode_groups(fgroup)
         self.fgroup = None if enc is None else torch.as_tensor(enc, device=self.dev).contiguous()
         self.fine_f = fine_columns(fgroup, self.iscat_np, self.F)
         if self.fine_f is not None:
             self.fine_f = torch.as_tensor(self.fine_f, device=self.dev).contiguous()
-        self.n_low = int(n_low)
+        self.n_low, self.n_mid = int(n_low), int(n_mid)
         if getattr(self, "_plan", None) is not None:
             self._plan.fgroup = 0 if self.fgroup is None else self.fgroup.data_ptr()
             self._plan.fine_f = 0 if self.fine_f is None else self.fine_f.data_ptr()
             self._set_plan_narrow(self._plan)
 
     def _set_plan_narrow(self, P):
-        lo_from = narrow_from(self.p, self.n_low, self.F)
-        P.lo_F, P.lo_from = (self.n_low, lo_from) if lo_from >= 0 else (0, 0)
+        mid, lo = narrow_cut(self.p, self.n_low, self.n_mid, self.F)
+        P.lo_F, P.lo_from = (self.n_low, lo) if lo >= 0 else (0, 0)
+        P.mid_F, P.mid_from = (self.n_mid, mid) if mid >= 0 else (0, 0)
 
     def _set_plan_ic(self, P):
         if self.ic_map is None:

@@ -488,10 +488,12 @@ def test_wide_binning_columns_are_interleaved_edge_subsets(fine, monkeypatch):
         assert b.F_orig == 3 and list(b.vmap) == [0, 0, 0, 0, 2, 2, 2, 2, 1] and b.n_low == 0
         assert list(T.fine_columns(b.vmap, b.iscat, b.F)) == [1] * 8 + [0]
     else:
-        # every feature's first column leads (the narrow view of levels with <= 256 adaptive bins)
-        assert b.F_orig == 3 and list(b.vmap) == [0, 1, 2, 0, 0, 0, 2, 2, 2] and b.n_low == 3
+        # every feature's first column leads (narrow view of levels with <= 256 adaptive bins), then the k = 2
+        # subsets (with the first: every other fine edge, the 512-bin levels), then the odd subsets
+        assert b.F_orig == 3 and list(b.vmap) == [0, 1, 2, 0, 2, 0, 0, 2, 2] and (b.n_low, b.n_mid) == (3, 5)
         assert T.fine_columns(b.vmap, b.iscat, b.F) is None
-    c0 = [int(j) for j in np.nonzero(b.vmap == 0)[0]]
+    # feature 0's columns in subset order k (column k holds e[k::4]: its first edge is fine edge k)
+    c0 = sorted((int(j) for j in np.nonzero(b.vmap == 0)[0]), key=lambda j: float(b.edges[j][0]))
     c2 = [int(j) for j in np.nonzero(b.vmap == 2)[0]]
     # the fine bin is the byte sum of the 4 columns (NA: 4 x 255)
     fsum = apply_binning(b, X).long()[:, c2].sum(1)
@@ -552,21 +554,24 @@ def test_wide_bins_split_resolution_and_grouped_sampling():
 
 
 def test_narrow_levels_search_only_first_columns():
-    """AUTO (UniformAdaptive, nbins_top_level 1024): from the level whose adaptive bin count is <= 256 the
-    reference builder searches only every feature's first column (ops/tree.narrow_from)."""
+    """AUTO (UniformAdaptive, nbins_top_level 1024): the level whose adaptive bin count is 512 searches every
+    other fine edge (first two column tiers), from 256 on only every feature's first column (ops/tree.narrow_cut)."""
     X, y, info = _data(N=20000, F=4, seed=3)
     b = fit_binning(X, info.iscat, info.nlevels, max_bins=1016)
-    assert b.n_low == 4 and b.F == 16
+    assert (b.n_low, b.n_mid, b.F) == (4, 8, 16)
     p = T.SplitParams(min_w=5, adapt_nbins=20, adapt_top=1024, edges=_edge_tab(b))
-    assert T.narrow_from(p, b.n_low, b.F) == 2
-    assert T.narrow_from(T.SplitParams(min_w=5), b.n_low, b.F) == -1          # QuantilesGlobal: every level
+    cut = T.narrow_cut(p, b.n_low, b.n_mid, b.F)
+    assert cut == (1, 2)
+    assert [T.level_fcut(cut, b.n_low, b.n_mid, d) for d in range(4)] == [0, 8, 4, 4]
+    assert T.narrow_cut(T.SplitParams(min_w=5), b.n_low, b.n_mid, b.F) == (-1, -1)    # QuantilesGlobal
     g = y - 0.5
     aux = torch.stack([torch.ones_like(y), g, g, torch.ones_like(y)], 1).contiguous()
     ref = T.RefTreeBuilder(apply_binning(b, X), b.F, b.nbins, b.iscat, None, 6, p)
-    ref.set_feature_groups(b.vmap, b.n_low)
+    ref.set_feature_groups(b.vmap, b.n_low, b.n_mid)
     ref.build(aux, None, 0, seed=1)
     tl = ref.pop_levels()[0]
     assert all(int(f) < b.n_low for d in tl.decs[2:] for f in d["feat"] if f >= 0)
+    assert all(int(f) < b.n_mid for f in tl.decs[1]["feat"] if f >= 0)
     assert any(int(f) >= b.n_low for d in tl.decs[:2] for f in d["feat"])
 
 
@@ -605,12 +610,12 @@ def test_gpu_wide_bins_match_reference(case, fine, monkeypatch):
     else:
         assert b.n_low == X.shape[0]
     ref = T.RefTreeBuilder(bins, b.F, b.nbins, b.iscat, None, 5, p)
-    ref.set_feature_groups(b.vmap, b.n_low)
+    ref.set_feature_groups(b.vmap, b.n_low, b.n_mid)
     ref.build(aux, None, k_cols, seed=5, leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1]).float())
     tl_r = ref.pop_levels()[0]
     dev = torch.device("cuda", 0)
     gb = T.GpuTreeBuilder(apply_binning(b, X.to(dev), planar=b.stride >= 64), b.F, b.nbins, b.iscat, None, 5, p)
-    gb.set_feature_groups(b.vmap, b.n_low)
+    gb.set_feature_groups(b.vmap, b.n_low, b.n_mid)
     gb.build(aux.to(dev), None, k_cols, seed=5, leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1]).float())
     tl_g = gb.pop_levels()[0]
     assert tl_g.n_leaves == tl_r.n_leaves
