@@ -17,6 +17,9 @@
 //              and written straight into the flat gradient buffer scaled by 1 / sum(w) of the batch (single
 //              process) or raw plus the batch weight (data parallel). Trailing workgroups reduce the per-tile
 //              bias partials of k_dl_rows (one wave per bias, fixed order).
+//  MEASURED (r4, DL_TIMING phase clocks): staging the weights of layers 2+ in LDS per launch cost ~5 us of
+//  loads at kernel start and gained < 0.4 us per later phase (their time is not the weight reads): dropped.
+//  Prefetching layer 1's first round of weight fragments into registers before the gathers spilled (128 VGPRs).
 //  MEASURED (10M x 784 [200,200], 4096-row steps, rocprofv3): the first version (16-row tiles on 4 waves,
 //  64 x 64 x 4-split weight tiles with fp32 slabs and a separate reduce) took 52 + 32 + 64 us per step:
 //  latency-bound dependent L2 round trips and a serial 256-deep bias loop, not MFMA or HBM.
@@ -71,45 +74,7 @@ struct DLArgs {
   int ae, no_wsum;               // 1: autoencoder (outputs reconstruct the undropped inputs, quadratic loss / K);
                                 // no_wsum: the optimizer reads the split partials itself (no k_dl_wsum launch)
   float* wpart;                 // [tiles][wsplit][64 * 64] fp32 partial tiles, then the batch's 1 / sum(w)
-  // weight matrices staged in LDS for the launch (the layers after the first are small): byte offset of the
-  // copy of W / WT of GEMM layer li, -1 = read from global; stg_n16[li] = 16-byte units of one such matrix
-  int stg_w[DL_MAXL], stg_wt[DL_MAXL], stg_n16[DL_MAXL];
 };
-
-// Copies the staged weight matrices into LDS: up to 8 16-byte units per thread, every load issued before any
-// store (one memory round trip, overlapping the row-metadata loads that follow)
-#define DL_STAGE_U 8
-__device__ __forceinline__ void stage_weights(const DLArgs& a, unsigned char* smem) {
-  const uint4* Wg = reinterpret_cast<const uint4*>(a.W);
-  const uint4* WTg = reinterpret_cast<const uint4*>(a.WT);
-  const int esz = a.f32 ? 4 : 2;
-  uint4 v[DL_STAGE_U];
-  int dst[DL_STAGE_U];
-  // fixed trip counts, no early exit: the unit arrays stay in registers (a data-dependent break sent them to scratch)
-#pragma unroll
-  for (int u = 0; u < DL_STAGE_U; ++u) {
-    int idx = (int)threadIdx.x + u * DL_THREADS;
-    const uint4* src = Wg;
-    int d = -1;
-#pragma unroll
-    for (int sg = 0; sg < 2 * DL_MAXL; ++sg) {
-      const int li = sg >> 1;
-      const int off = (sg & 1) ? a.stg_wt[li] : a.stg_w[li];
-      const int c16 = (li < a.L && off >= 0) ? a.stg_n16[li] : 0;
-      const bool hit = d < 0 && idx < c16;
-      if (hit) {
-        src = ((sg & 1) ? WTg : Wg) + a.w_off[li] * esz / 16 + idx;
-        d = off + idx * 16;
-      }
-      if (d < 0) idx -= c16;
-    }
-    v[u] = d >= 0 ? *src : make_uint4(0u, 0u, 0u, 0u);
-    dst[u] = d;
-  }
-#pragma unroll
-  for (int u = 0; u < DL_STAGE_U; ++u)
-    if (dst[u] >= 0) *reinterpret_cast<uint4*>(smem + dst[u]) = v[u];
-}
 
 #ifdef DL_TIMING
 // per-workgroup phase clocks of the last k_dl_rows launch (diagnostic build only: scripts/build_alt.sh dlt
@@ -219,48 +184,6 @@ __device__ __forceinline__ f32x4 tile_mm(const float* A, int lda, const float* B
   return acc;
 }
 
-// D = A(LDS tile, 16 x K) * B with B[k][n] = W[k * ldw + n] (W in LDS, rows along n): the backward pass reading a
-// staged forward weight matrix in place of its transposed copy (8 / 4 scalar LDS reads per MFMA operand)
-__device__ __forceinline__ f32x4 tile_mm_tl(const bf16* A, int lda, const bf16* W, int ldw, int n0, int nvalid, int K,
-                                            int kvalid) {
-  const int lane = threadIdx.x & 63, q = lane >> 4, c = lane & 15;
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  const int n = n0 + c;
-  const bool nok = n < nvalid;
-  for (int kb = 0; kb < K; kb += 32) {
-    bf16x8 b;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int k = kb + 8 * q + j;
-      b[j] = (nok && k < kvalid) ? (__bf16)__bfloat162float(W[k * ldw + n]) : (__bf16)0.f;
-    }
-    const bf16x8 av = *reinterpret_cast<const bf16x8*>(A + c * lda + kb + 8 * q);
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, b, acc, 0, 0, 0);
-  }
-  return acc;
-}
-__device__ __forceinline__ f32x4 tile_mm_tl(const float* A, int lda, const float* W, int ldw, int n0, int nvalid, int K,
-                                            int kvalid) {
-  const int lane = threadIdx.x & 63, q = lane >> 4, c = lane & 15;
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  const int n = n0 + c;
-  const bool nok = n < nvalid;
-  for (int kb = 0; kb < K; kb += 16) {
-    const float4 av = *reinterpret_cast<const float4*>(A + c * lda + kb + 4 * q);
-    float bv[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int k = kb + 4 * q + j;
-      bv[j] = (nok && k < kvalid) ? W[k * ldw + n] : 0.f;
-    }
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv[0], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv[1], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv[2], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv[3], acc, 0, 0, 0);
-  }
-  return acc;
-}
-
 __device__ __forceinline__ float to_f(bf16 v) { return __bfloat162float(v); }
 __device__ __forceinline__ float to_f(float v) { return v; }
 template <typename T> __device__ __forceinline__ T from_f(float v);
@@ -301,7 +224,6 @@ __global__ __launch_bounds__(DL_THREADS) void k_dl_rows(DLArgs a) {
   const int L = a.L;
   const uint64_t step = a.step_dev ? *a.step_dev : 0ull;
   DLT(0);
-  stage_weights(a, smem);          // (beyond the zeroed tiles; ready after the first barrier)
   __shared__ long long srow[DL_ROWS];
   __shared__ float sy[DL_ROWS];
   __shared__ long long scls[DL_ROWS];
@@ -379,9 +301,8 @@ __global__ __launch_bounds__(DL_THREADS) void k_dl_rows(DLArgs a) {
     const T* Ain = S + a.lds_off[l - 1];
     T* Aout = S + a.lds_off[l];
     const int nin = a.n[l - 1], nout = a.n[l];
-    const bool stg = a.stg_w[l - 1] >= 0;
-    const T* Wl = stg ? reinterpret_cast<const T*>(smem + a.stg_w[l - 1]) : Wg + a.w_off[l - 1];
-    const bool vec = (nin % VE == 0) && (stg || a.w_off[l - 1] % VE == 0);
+    const T* Wl = Wg + a.w_off[l - 1];
+    const bool vec = (nin % VE == 0) && (a.w_off[l - 1] % VE == 0);
     const float drop = a.drop[l - 1], keep = 1.f - drop;
     const uint32_t thr = (uint32_t)(drop * 4294967296.0);
     const uint64_t seed = a.seed_base[l - 1] ^ (step * 0x9E3779B97F4A7C15ULL);
@@ -424,9 +345,8 @@ __global__ __launch_bounds__(DL_THREADS) void k_dl_rows(DLArgs a) {
   if (a.K > 16) {
     float* LG = reinterpret_cast<float*>(smem + a.lds_lg);
     const int nin = a.n[L - 1], K = a.K;
-    const bool stg = a.stg_w[L - 1] >= 0;
-    const T* Wo = stg ? reinterpret_cast<const T*>(smem + a.stg_w[L - 1]) : Wg + a.w_off[L - 1];
-    const bool vec = (nin % VE == 0) && (stg || a.w_off[L - 1] % VE == 0);
+    const T* Wo = Wg + a.w_off[L - 1];
+    const bool vec = (nin % VE == 0) && (a.w_off[L - 1] % VE == 0);
     for (int t = wv; t < (K + 15) / 16; t += DL_NW) {
       const f32x4 acc = tile_mm(S + a.lds_off[L - 1], a.ld[L - 1], Wo, nin, t * 16, K, a.kp[L - 1], nin, vec);
       const int col = t * 16 + c;
@@ -478,9 +398,8 @@ __global__ __launch_bounds__(DL_THREADS) void k_dl_rows(DLArgs a) {
     }
   } else if (wv == 0) {
     const int nin = a.n[L - 1], K = a.K;
-    const bool stg = a.stg_w[L - 1] >= 0;
-    const T* Wo = stg ? reinterpret_cast<const T*>(smem + a.stg_w[L - 1]) : Wg + a.w_off[L - 1];
-    const bool vec = (nin % VE == 0) && (stg || a.w_off[L - 1] % VE == 0);
+    const T* Wo = Wg + a.w_off[L - 1];
+    const bool vec = (nin % VE == 0) && (a.w_off[L - 1] % VE == 0);
     const f32x4 acc = tile_mm(S + a.lds_off[L - 1], a.ld[L - 1], Wo, nin, 0, K, a.kp[L - 1], nin, vec);
     const bool cok = c < K;
     const float b = cok ? a.P[a.b_off[L - 1] + c] : 0.f;
@@ -519,11 +438,8 @@ __global__ __launch_bounds__(DL_THREADS) void k_dl_rows(DLArgs a) {
     const int nout = a.n[l], nnext = a.ng[l + 1];     // layer l+1's GEMM width (its WT rows)
     const int ldo = a.ldg[l];
     const unsigned char* win = a.maxout ? smem + a.lds_mx[l] : nullptr;
-    const bool stg = a.stg_wt[l] >= 0;
-    const T* WTl = stg ? reinterpret_cast<const T*>(smem + a.stg_wt[l]) : WTg + a.w_off[l];
-    const bool vec = (nnext % VE == 0) && (stg || a.w_off[l] % VE == 0);
-    // no staged transpose but the forward matrix W_{l+1} [nnext][nout] is staged: read it transposed on chip
-    const T* Wtl = (!stg && a.stg_w[l] >= 0) ? reinterpret_cast<const T*>(smem + a.stg_w[l]) : nullptr;
+    const T* WTl = WTg + a.w_off[l];
+    const bool vec = (nnext % VE == 0) && (a.w_off[l] % VE == 0);
     const float drop = a.drop[l - 1], keep = 1.f - drop;
     const uint32_t thr = (uint32_t)(drop * 4294967296.0);
     const uint64_t seed = a.seed_base[l - 1] ^ (step * 0x9E3779B97F4A7C15ULL);
@@ -531,8 +447,7 @@ __global__ __launch_bounds__(DL_THREADS) void k_dl_rows(DLArgs a) {
     const int NT = (nout + 15) / 16;
     for (int t = wv; t < NT; t += DL_NW) {
       // dh = G_{l+1} W_{l+1}: B[k = unit of l+1][n = unit of l] = WT_{l+1}[n][k]
-      const f32x4 acc = Wtl ? tile_mm_tl(Gin, ldg_in, Wtl, nout, t * 16, nout, a.kpg[l + 1], nnext)
-                            : tile_mm(Gin, ldg_in, WTl, nnext, t * 16, nout, a.kpg[l + 1], nnext, vec);
+      const f32x4 acc = tile_mm(Gin, ldg_in, WTl, nnext, t * 16, nout, a.kpg[l + 1], nnext, vec);
       const int col = t * 16 + c;
       f32x4 gd = {0.f, 0.f, 0.f, 0.f};
       if (col < nout) {

@@ -40,7 +40,7 @@ class _DLArgs(ctypes.Structure):
                  ("in_drop", _cf), ("lds_lg", _ci), ("in_seed", _cull),
                  ("wsplit", _ci), ("maxout", _ci), ("ng", _ci * (MAXL + 1)), ("kpg", _ci * (MAXL + 1)),
                  ("ldg", _ci * (MAXL + 1)), ("lds_mx", _ci * MAXL), ("ae", _ci), ("no_wsum", _ci),
-                 ("wpart", _vp), ("stg_w", _ci * MAXL), ("stg_wt", _ci * MAXL), ("stg_n16", _ci * MAXL)])
+                 ("wpart", _vp)])
 
 
 nat.register_hip_signatures({"h2o_dl_args_size": [], "h2o_dl_step": [_vp, _ci, _ci, _vp],
@@ -173,31 +173,6 @@ class FusedMLPStep:
             assert (autoencoder or not regression) and n[L] <= MAXK
             a.lds_lg = (self.lds + 15) // 16 * 16
             self.lds = a.lds_lg + ROWS * n[L] * 4
-        # weight matrices of the layers after the first staged in LDS per launch (k_dl_rows stage_weights): the
-        # forward of layer 2+, the output layer and the backward through WT read them on chip instead of as one
-        # dependent L2/HBM round trip per layer. Greedy in order of use within the LDS left (and 8 16-byte units
-        # per thread); a transpose is staged only when its forward matrix is not (the backward then reads W
-        # transposed in LDS). Off by default (H2O_DL_STAGE=1): MEASURED r4 (bf16 [200,200], phase clocks) the
-        # staging loads cost ~5 us at kernel start (the weights the previous launch wrote come from MALL/HBM to
-        # every CU) while the later phases gained < 0.4 us each: latency there is not the weight reads.
-        for li in range(MAXL):
-            a.stg_w[li] = a.stg_wt[li] = -1
-            a.stg_n16[li] = 0
-        if os.environ.get("H2O_DL_STAGE", "0") == "1":
-            ve = 16 // cesz
-            room = min(150 * 1024 - self.lds, 8 * 1024 * 16)
-            staged = 0
-            for kind, li in [("w", li) for li in range(1, L)] + [("wt", li) for li in range(L - 1, 0, -1)]:
-                nb = ng[li + 1] * n[li] * cesz
-                if nb % 16 or a.w_off[li] % ve or staged + nb > room:
-                    continue
-                if kind == "wt" and a.stg_w[li] >= 0 and os.environ.get("H2O_DL_STAGE_WT") != "1":
-                    continue            # the backward reads the staged forward matrix transposed (tile_mm_tl)
-                off = (self.lds + 15) // 16 * 16
-                getattr(a, "stg_" + kind)[li] = off
-                a.stg_n16[li] = nb // 16
-                self.lds = off + nb
-                staged += nb
         a.in_drop = float(in_drop)
         a.in_seed = int(in_seed) & ((1 << 64) - 1)
         ts = 0
