@@ -1444,12 +1444,12 @@ __global__ __launch_bounds__(LW * 64) void k_route(
     const Node* __restrict__ nodesA, const int* __restrict__ tpA, const int* __restrict__ metaA,
     const Dec* __restrict__ decA, const int* __restrict__ clA, const int* __restrict__ crA,
     const Dec* __restrict__ decB, const int* __restrict__ clB, const int* __restrict__ crB,
-    int4* __restrict__ curs, long long N, int planar) {
+    int4* __restrict__ curs, long long N, int planar, uint8_t* __restrict__ lvl2) {
   const int n_nodes = metaA[0], n_tiles = metaA[1];
   const int t = blockIdx.x;
   if (t >= n_tiles) return;
   __shared__ Dec sA, sB[2];
-  __shared__ int sC[2], sG[4], sBase[4];
+  __shared__ int sC[2], sG[4], sBase[4], sL[4];
   __shared__ int sCnt[LW][4];
   const int node = find_node(tpA, n_nodes, t);
   const Node nd = nodesA[node];
@@ -1464,6 +1464,9 @@ __global__ __launch_bounds__(LW * 64) void k_route(
     // slot q -> continuing grandchild (>= 0), else the row stops at a leaf
     const int q = threadIdx.x, c = sC[q >> 1];
     sG[q] = c < 0 ? -1 : ((q & 1) ? crB[c] : clB[c]);
+    // lvl2 code of slot q: the grandchild's node index, or 128 + the leaf the row stops at
+    const int g = c < 0 ? c : sG[q];
+    sL[q] = g >= 0 ? g : 128 + (-1 - g);
   }
   for (int k = 0; k < 2; ++k) {
     const int c = sC[k];
@@ -1514,6 +1517,7 @@ __global__ __launch_bounds__(LW * 64) void k_route(
     }
     q[u] = 2 * dA + dB;
     mv[u] = valid && sG[q[u]] >= 0;
+    if (lvl2 && valid) lvl2[row] = (uint8_t)sL[q[u]];   // (e = 0: rows in original order)
     rank[u] = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -1603,7 +1607,8 @@ template <int NV>
 __global__ __launch_bounds__(256) void k_leaf_assign(
     const uint8_t* __restrict__ bins, int stride, long long N, const LevelPtrs* __restrict__ lv, int D,
     const float* __restrict__ an, const float* __restrict__ ad, const double* __restrict__ qs,
-    int* __restrict__ leaf_of_row, unsigned long long* __restrict__ leafq, int leaf_cap, int n_nodes, int planar) {
+    int* __restrict__ leaf_of_row, unsigned long long* __restrict__ leafq, int leaf_cap, int n_nodes, int planar,
+    const uint8_t* __restrict__ lvl2 /*null, or every row's level-2 node / 128 + leaf (k_route of the root)*/) {
   extern __shared__ __align__(16) unsigned char la_smem[];
   __shared__ int sbase[TP_MAXL_DEV + 1];
   const bool lds = leaf_cap <= LEAF_LDS_MAX;
@@ -1642,8 +1647,13 @@ __global__ __launch_bounds__(256) void k_leaf_assign(
       if (NV > 3) v3 = s4b[1];
     }
     const float a_n = an[row], a_d = ad[row];    // issued before the walk: latency overlaps it
-    int i = 0, leaf = 0;
-    for (int d = 0; d < D; ++d) {
+    int i = 0, leaf = 0, d0 = 0;
+    if (lvl2) {                                  // the root route's level-2 position: walk from level 2
+      const int code = lvl2[row];
+      d0 = (code & 128) ? D : 2;
+      if (code & 128) leaf = code & 127; else i = code;
+    }
+    for (int d = d0; d < D; ++d) {
       int c;
       if (tl) {
         const int4 e = st[sbase[d] + i];
@@ -2127,17 +2137,20 @@ static int nv_of(int stride) {
 // regroup an even level two levels down (moving bins + wY (+ w) of continuing rows)
 // lp > 0 (planar): only the first lp (1 or 2) planes of each row move — the narrow levels below read no other
 // column; split bytes of columns past them (the decisions of the levels above) are read from the source
+// lvl2 (nullable; the root route only): per ORIGINAL row its level-2 node, or 128 + its leaf (k_leaf_assign
+// starts there)
 int h2o_route(const void* sbins, const void* say, const void* saw, void* dbins, void* day, void* daw, int stride,
               const void* nodesA, const void* tpA, const void* metaA, const void* decA, const void* clA,
               const void* crA, const void* decB, const void* clB, const void* crB, void* curs, int tiles_cap,
-              long long N, int planar, int lp, hipStream_t s) {
+              long long N, int planar, int lp, void* lvl2, hipStream_t s) {
   if (planar && (stride % 32 != 0 || stride < 64)) return (int)hipErrorInvalidValue;
   if (lp < 0 || lp > 2 || (lp > 0 && !planar)) return (int)hipErrorInvalidValue;
 #define ROUTE_LAUNCH(NV)                                                                                       \
   hipLaunchKernelGGL((k_route<NV>), dim3(tiles_cap), dim3(LW * 64), 0, s, (const uint8_t*)sbins,              \
                      (const float*)say, (const float*)saw, (uint8_t*)dbins, (float*)day, (float*)daw, stride,  \
                      (const Node*)nodesA, (const int*)tpA, (const int*)metaA, (const Dec*)decA, (const int*)clA, \
-                     (const int*)crA, (const Dec*)decB, (const int*)clB, (const int*)crB, (int4*)curs, N, planar)
+                     (const int*)crA, (const Dec*)decB, (const int*)clB, (const int*)crB, (int4*)curs, N, planar, \
+                     (uint8_t*)lvl2)
   switch (lp == 1 ? 2 : lp == 2 ? 4 : nv_of(stride)) {
     case 4: ROUTE_LAUNCH(4); break;
     case 3: ROUTE_LAUNCH(3); break;
@@ -2152,7 +2165,8 @@ int h2o_route(const void* sbins, const void* say, const void* saw, void* dbins, 
 // leaf id of every row (original order) + fixed-point leaf sums -> fp64 leafsum[leaf_cap][2]
 static int leaf_assign_launch(const void* master, int stride, long long N, const void* lvptrs, int D, const void* an,
                               const void* ad, const void* qs, void* leaf_of_row, void* leafq, int leaf_cap,
-                              void* leafsum, int n_nodes, int planar, LeafVals lv, hipStream_t s) {
+                              void* leafsum, int n_nodes, int planar, LeafVals lv, hipStream_t s,
+                              const void* lvl2 = nullptr) {
   if (D > TP_MAXL_DEV) return (int)hipErrorInvalidValue;
   long long grid = (N + 255) / 256;
   if (grid > 2048) grid = 2048;
@@ -2161,10 +2175,11 @@ static int leaf_assign_launch(const void* master, int stride, long long N, const
                      (n_nodes <= LEAF_TREE_MAX ? (size_t)16 * n_nodes : 0);
 #define LA(NV) hipLaunchKernelGGL((k_leaf_assign<NV>), dim3((unsigned)grid), dim3(256), lds, s, (const uint8_t*)master, \
                                   stride, N, (const LevelPtrs*)lvptrs, D, (const float*)an, (const float*)ad,          \
-                                  (const double*)qs, (int*)leaf_of_row, (unsigned long long*)leafq, leaf_cap, n_nodes, planar)
-  // planar rows of more than two planes: the first two planes in registers (every feature of the narrow levels),
-  // split bytes of later planes loaded per level
-  switch ((planar && stride > 64 && !route_generic()) ? 4 : nv_of(stride)) {
+                                  (const double*)qs, (int*)leaf_of_row, (unsigned long long*)leafq, leaf_cap, n_nodes, planar, \
+                                  (const uint8_t*)lvl2)
+  // planar rows of more than two planes: with the root route's level-2 positions (narrow levels below) only the
+  // first plane in registers, else the first two; split bytes of later planes are loaded per level
+  switch ((planar && stride > 64 && !route_generic()) ? (lvl2 ? 2 : 4) : nv_of(stride)) {
     case 4: LA(4); break;
     case 3: LA(3); break;
     case 2: LA(2); break;
@@ -2283,6 +2298,7 @@ struct TreePlan {
   // histogrammed, reduced and searched, and the routes that feed such levels move only the planes holding them.
   // lo_F / mid_F = 0: off.
   int lo_F, lo_from, mid_F, mid_from;
+  void* lvl2;                 // [N] uint8: the root route's level-2 node / 128 + leaf per row (narrow runs; or null)
 };
 
 // op codes / dtypes of the collective transport
@@ -2308,6 +2324,11 @@ static inline int tp_fcut(const TreePlan* P, int d) {
   return 0;
 }
 static inline int tp_planes(int fc) { return fc > 0 ? (fc + FTILE - 1) / FTILE : 0; }
+// the root route records every row's level-2 position when the levels below are narrow and planar (the leaf walk
+// then skips the two levels whose split bytes live in other planes)
+static inline void* tp_lvl2(const TreePlan* P) {
+  return (P->lvl2 && P->planar && P->D > 2 && tp_fcut(P, 2) > 0 && tp_fcut(P, 2) <= FTILE) ? P->lvl2 : nullptr;
+}
 
 static int tp_route(const TreePlan* P, int e, hipStream_t s) {
   const void *sb, *sy, *sw;
@@ -2318,7 +2339,7 @@ static int tp_route(const TreePlan* P, int e, hipStream_t s) {
   const int lp = (P->planar && np <= 2) ? np : 0;
   return h2o_route(sb, sy, sw, P->bb[di], P->by[di], P->unit ? nullptr : P->bw[di], P->stride, P->nodes[e], P->tp[e],
                    P->meta[e], P->dec[e], P->cl[e], P->cr[e], P->dec[e + 1], P->cl[e + 1], P->cr[e + 1],
-                   P->cur[e + 1], P->tiles_cap[e], P->N, P->planar, lp, s);
+                   P->cur[e + 1], P->tiles_cap[e], P->N, P->planar, lp, e == 0 ? tp_lvl2(P) : nullptr, s);
 }
 
 #define TP_CHECK(x) do { int rc_ = (x); if (rc_) return rc_; } while (0)
@@ -2449,7 +2470,7 @@ static int tree_leaves(const TreePlan* P, bool values, hipStream_t s) {
   const LeafVals lv{P->log_link, P->scale, P->kclamp, P->mx, P->leaf_lam, P->leaf_l1,
                     values ? (float*)P->leafval : nullptr};
   return leaf_assign_launch(P->master, P->stride, P->N, P->lvptrs, P->D, tp_aux(P, 2), tp_aux(P, 3), P->qs,
-                            P->leaf_of_row, P->leafq, P->leaf_cap, P->leafsum, n_nodes, P->planar, lv, s);
+                            P->leaf_of_row, P->leafq, P->leaf_cap, P->leafsum, n_nodes, P->planar, lv, s, tp_lvl2(P));
 }
 
 int h2o_tree_leaves(const TreePlan* P, hipStream_t s) { return tree_leaves(P, false, s); }
