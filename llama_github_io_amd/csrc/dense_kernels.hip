@@ -219,33 +219,72 @@ __global__ __launch_bounds__(256) void k_num_stats(const float* __restrict__ X, 
 }
 
 // Z[r, col0 + j] = (isnan(x) ? fill_j : x - sub_j) * mul_j for the numeric rows listed in `rows`, through a
-// 64-row x 32-feature LDS tile: reads coalesced along N, writes coalesced along P.
+// 128-row x 32-feature LDS tile: 16-byte reads along N (4 rows per lane), 16-byte writes along P (8 bf16 / 4 fp32
+// features of one row per lane). MEASURED before (64 x 32 tile, one float read and one 2-byte write per element):
+// 5.9 ms for 2M x 784 (1.6 TB/s), most of a 10M-row DeepLearning setup.
+template <typename T> struct NT_VEC;
+template <> struct NT_VEC<__hip_bfloat16> { static constexpr int n = 8; };
+template <> struct NT_VEC<float> { static constexpr int n = 4; };
+__device__ __forceinline__ uint4 pack_row(const float* v, __hip_bfloat16*) {
+  union { __hip_bfloat16 h[8]; uint4 u; } pk;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) pk.h[j] = __float2bfloat16(v[j]);
+  return pk.u;
+}
+__device__ __forceinline__ uint4 pack_row(const float* v, float*) {
+  return make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3]));
+}
 template <typename T>
 __global__ __launch_bounds__(256) void k_num_transform(const float* __restrict__ X, int64_t N, const int* __restrict__ rows,
                                                        int nf, const float* __restrict__ fill, const float* __restrict__ sub,
                                                        const float* __restrict__ mul, T* __restrict__ Z, int ldz, int col0) {
-  __shared__ float tile[32][65];
-  const int64_t r0 = (int64_t)blockIdx.x * 64;
+  __shared__ float tile[32][129];
+  const int64_t r0 = (int64_t)blockIdx.x * 128;
   const int f0 = blockIdx.y * 32;
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;   // 64 x 4
-  for (int k = ty; k < 32; k += 4) {
+  const int t = threadIdx.x;
+  const bool vin = (N % 4) == 0;
+  // read: thread t takes rows r0 + 4 (t % 32) .. + 3 of features t / 32 + 8 i
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int k = t / 32 + 8 * i, c = t % 32;
     const int f = f0 + k;
-    const int64_t r = r0 + tx;
-    float v = 0.f;
-    if (f < nf && r < N) {
-      v = X[(int64_t)rows[f] * N + r];
-      v = (v != v) ? fill[f] : v;
-      v = (v - sub[f]) * mul[f];
+    const int64_t r = r0 + 4 * c;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    if (f < nf) {
+      const float* x = X + (int64_t)rows[f] * N;
+      if (vin && r + 3 < N) {
+        const float4 q = *reinterpret_cast<const float4*>(x + r);
+        v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = r + j < N ? x[r + j] : 0.f;
+      }
+      const float fl = fill[f], sb = sub[f], ml = mul[f];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = ((v[j] != v[j]) ? fl : v[j]) - sb, v[j] *= ml;
     }
-    tile[k][tx] = v;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) tile[k][4 * c + j] = v[j];
   }
   __syncthreads();
-  // write: each warp-row of 32 lanes covers the 32 features of one row
-  const int lx = threadIdx.x & 31, ly = threadIdx.x >> 5;   // 32 x 8
-  for (int rr = ly; rr < 64; rr += 8) {
+  // write: VN consecutive features of one row per 16-byte store
+  constexpr int VN = NT_VEC<T>::n, CPR = 32 / VN;          // chunks per row
+  const bool vout = (ldz % VN) == 0 && ((col0 + f0) % VN) == 0;
+  for (int idx = t; idx < 128 * CPR; idx += 256) {
+    const int rr = idx / CPR, q = idx % CPR;
     const int64_t r = r0 + rr;
-    const int f = f0 + lx;
-    if (r < N && f < nf) st(Z, r * ldz + col0 + f, tile[lx][rr]);
+    if (r >= N) continue;
+    const int fq = f0 + q * VN;
+    float v[VN];
+#pragma unroll
+    for (int j = 0; j < VN; ++j) v[j] = tile[q * VN + j][rr];
+    T* dst = Z + r * ldz + col0 + fq;
+    if (vout && fq + VN <= nf) {
+      *reinterpret_cast<uint4*>(dst) = pack_row(v, (T*)nullptr);
+    } else {
+#pragma unroll
+      for (int j = 0; j < VN; ++j) if (fq + j < nf) st(dst, j, v[j]);
+    }
   }
 }
 
@@ -264,7 +303,7 @@ int h2o_num_stats(const float* X, long long N, const int* rows, int nf, const fl
 int h2o_num_transform(const float* X, long long N, const int* rows, int nf, const float* fill, const float* sub,
                       const float* mul, void* Z, int ldz, int col0, int bf16, hipStream_t s) {
   if (N <= 0 || nf <= 0) return 0;
-  dim3 grid((unsigned)((N + 63) / 64), (unsigned)((nf + 31) / 32));
+  dim3 grid((unsigned)((N + 127) / 128), (unsigned)((nf + 31) / 32));
   if (bf16)
     hipLaunchKernelGGL(k_num_transform<__hip_bfloat16>, grid, dim3(256), 0, s, X, (int64_t)N, rows, nf, fill, sub, mul,
                        (__hip_bfloat16*)Z, ldz, col0);

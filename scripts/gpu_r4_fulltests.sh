@@ -11,3 +11,8 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.
 tail -2 $O/smoke.log
 timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err || exit $?
 cat $O/bench.json
+# the other BASELINE configurations (one line each)
+timeout -k 10 400 python scripts/bench_suite.py --which dl > $O/dl10m.log 2>&1 || { tail -5 $O/dl10m.log; exit 1; }
+tail -1 $O/dl10m.log | cut -c1-400
+timeout -k 10 400 python scripts/bench_suite.py --which xgb > $O/xgb.log 2>&1 || { tail -5 $O/xgb.log; exit 1; }
+tail -1 $O/xgb.log | cut -c1-400

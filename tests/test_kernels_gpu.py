@@ -324,19 +324,24 @@ def test_deeplearning_explicit_step_matches_autograd_gpu(dtype, monkeypatch):
 
 @pytest.mark.parametrize("standardize", [True, False])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_expander_hip_matches_cpu(standardize, dtype):
-    # k_num_stats / k_num_transform (NaN fill, centring, scaling, transpose) vs the PyTorch path
+@pytest.mark.parametrize("N,cat", [(10001, True), (10000, False)])
+def test_expander_hip_matches_cpu(standardize, dtype, N, cat):
+    # k_num_stats / k_num_transform (NaN fill, centring, scaling, transpose) vs the PyTorch path; N % 4 == 0
+    # without categoricals takes the 16-byte read / write paths
     from llama_github_io_amd.models.base import DataInfo
     from llama_github_io_amd.models.datainfo import Expander
     g = torch.Generator().manual_seed(4)
-    F, N = 70, 10001
+    F = 70
     X = torch.randn(F, N, generator=g) * 3 + 1
     X[2, ::7] = float("nan")
-    X[5] = torch.randint(0, 4, (N,), generator=g).float()
-    X[5, ::11] = float("nan")
     iscat = np.zeros(F, np.int32)
-    iscat[5] = 1
-    info = DataInfo([f"x{i}" for i in range(F)], iscat, [None] * 5 + [["a", "b", "c", "d"]] + [None] * (F - 6), "y", None)
+    doms = [None] * F
+    if cat:
+        X[5] = torch.randint(0, 4, (N,), generator=g).float()
+        X[5, ::11] = float("nan")
+        iscat[5] = 1
+        doms[5] = ["a", "b", "c", "d"]
+    info = DataInfo([f"x{i}" for i in range(F)], iscat, doms, "y", None)
     w = torch.rand(N, generator=g).double()
     ec = Expander(info, standardize=standardize).fit(X, w)
     eg = Expander(info, standardize=standardize).fit(X.to(dev), w.to(dev))
