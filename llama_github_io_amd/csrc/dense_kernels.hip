@@ -197,12 +197,21 @@ __global__ __launch_bounds__(256) void k_num_stats(const float* __restrict__ X, 
   const int j = blockIdx.y;
   const float* x = X + (int64_t)rows[j] * N;
   double a = 0.0, b = 0.0, c = 0.0;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += (int64_t)gridDim.x * blockDim.x) {
-    const float v = x[i];
+  auto add = [&](float v, int64_t i) {
     if (v == v) {
       const double ww = w ? (double)w[i] : 1.0;
       a += ww; b += ww * v; c += ww * (double)v * v;
     }
+  };
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if ((N & 3) == 0) {     // 16-byte loads: 4 consecutive rows per lane
+    for (int64_t i = 4 * i0; i < N; i += 4 * stride) {
+      const float4 q = *reinterpret_cast<const float4*>(x + i);
+      add(q.x, i); add(q.y, i + 1); add(q.z, i + 2); add(q.w, i + 3);
+    }
+  } else {
+    for (int64_t i = i0; i < N; i += stride) add(x[i], i);
   }
   __shared__ double red[3][8];
   for (int o = 32; o > 0; o >>= 1) {
