@@ -205,8 +205,19 @@ __global__ __launch_bounds__(256) void k_num_stats(const float* __restrict__ X, 
   };
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if ((N & 3) == 0) {     // 16-byte loads: 4 consecutive rows per lane
-    for (int64_t i = 4 * i0; i < N; i += 4 * stride) {
+  if ((N & 3) == 0) {     // 16-byte loads, 4 in flight per lane: 4 consecutive rows each
+    int64_t i = 4 * i0;
+    for (; i + 12 * stride < N; i += 16 * stride) {
+      float4 q[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) q[u] = *reinterpret_cast<const float4*>(x + i + 4 * u * stride);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t b = i + 4 * u * stride;
+        add(q[u].x, b); add(q[u].y, b + 1); add(q[u].z, b + 2); add(q[u].w, b + 3);
+      }
+    }
+    for (; i < N; i += 4 * stride) {
       const float4 q = *reinterpret_cast<const float4*>(x + i);
       add(q.x, i); add(q.y, i + 1); add(q.z, i + 2); add(q.w, i + 3);
     }
@@ -248,10 +259,10 @@ __global__ __launch_bounds__(256) void k_num_transform(const float* __restrict__
                                                        int nf, const float* __restrict__ fill, const float* __restrict__ sub,
                                                        const float* __restrict__ mul, T* __restrict__ Z, int ldz, int col0) {
   __shared__ float tile[32][129];
-  const int64_t r0 = (int64_t)blockIdx.x * 128;
   const int f0 = blockIdx.y * 32;
   const int t = threadIdx.x;
   const bool vin = (N % 4) == 0;
+  for (int64_t r0 = (int64_t)blockIdx.x * 128; r0 < N; r0 += (int64_t)gridDim.x * 128) {
   // read: thread t takes rows r0 + 4 (t % 32) .. + 3 of features t / 32 + 8 i
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -295,6 +306,8 @@ __global__ __launch_bounds__(256) void k_num_transform(const float* __restrict__
       for (int j = 0; j < VN; ++j) if (fq + j < nf) st(dst, j, v[j]);
     }
   }
+  __syncthreads();          // the tile is refilled for the next row range
+  }
 }
 
 }  // namespace
@@ -312,7 +325,11 @@ int h2o_num_stats(const float* X, long long N, const int* rows, int nf, const fl
 int h2o_num_transform(const float* X, long long N, const int* rows, int nf, const float* fill, const float* sub,
                       const float* mul, void* Z, int ldz, int col0, int bf16, hipStream_t s) {
   if (N <= 0 || nf <= 0) return 0;
-  dim3 grid((unsigned)((N + 127) / 128), (unsigned)((nf + 31) / 32));
+  // row tiles strided over a bounded grid (each block several 128-row tiles of its 32 features)
+  long long gx = (N + 127) / 128;
+  const long long cap = (8192 + (nf + 31) / 32 - 1) / ((nf + 31) / 32) * 4;
+  if (gx > cap) gx = cap;
+  dim3 grid((unsigned)gx, (unsigned)((nf + 31) / 32));
   if (bf16)
     hipLaunchKernelGGL(k_num_transform<__hip_bfloat16>, grid, dim3(256), 0, s, X, (int64_t)N, rows, nf, fill, sub, mul,
                        (__hip_bfloat16*)Z, ldz, col0);
