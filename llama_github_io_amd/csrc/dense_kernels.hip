@@ -238,10 +238,12 @@ __global__ __launch_bounds__(256) void k_num_stats(const float* __restrict__ X, 
   }
 }
 
-// Z[r, col0 + j] = (isnan(x) ? fill_j : x - sub_j) * mul_j for the numeric rows listed in `rows`, through a
-// 128-row x 32-feature LDS tile: 16-byte reads along N (4 rows per lane), 16-byte writes along P (8 bf16 / 4 fp32
-// features of one row per lane). MEASURED before (64 x 32 tile, one float read and one 2-byte write per element):
-// 5.9 ms for 2M x 784 (1.6 TB/s), most of a 10M-row DeepLearning setup.
+// Z[r, col0 + j] = (isnan(x) ? fill_j : x - sub_j) * mul_j for the numeric rows listed in `rows`. A block owns
+// 32 rows and walks the features in chunks of 256 through a [256][33] LDS tile: every read is one feature's 32
+// rows (128 contiguous bytes, 16-byte loads), every write a row's 256-feature run (512 B / 1 KB contiguous,
+// 16-byte stores) — whole cache lines both ways.
+// MEASURED before: one element per lane (5.9 ms for 2M x 784, 1.6 TB/s); 128-row x 32-feature tiles with 16-byte
+// accesses, whose 64-byte row pieces left every written line partial (15.7 ms for 10M x 784, 3 TB/s).
 template <typename T> struct NT_VEC;
 template <> struct NT_VEC<__hip_bfloat16> { static constexpr int n = 8; };
 template <> struct NT_VEC<float> { static constexpr int n = 4; };
@@ -254,59 +256,62 @@ __device__ __forceinline__ uint4 pack_row(const float* v, __hip_bfloat16*) {
 __device__ __forceinline__ uint4 pack_row(const float* v, float*) {
   return make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3]));
 }
+#define NT_ROWS 32
+#define NT_FC 256
 template <typename T>
 __global__ __launch_bounds__(256) void k_num_transform(const float* __restrict__ X, int64_t N, const int* __restrict__ rows,
                                                        int nf, const float* __restrict__ fill, const float* __restrict__ sub,
                                                        const float* __restrict__ mul, T* __restrict__ Z, int ldz, int col0) {
-  __shared__ float tile[32][129];
-  const int f0 = blockIdx.y * 32;
+  __shared__ float tile[NT_FC][NT_ROWS + 1];
   const int t = threadIdx.x;
   const bool vin = (N % 4) == 0;
-  for (int64_t r0 = (int64_t)blockIdx.x * 128; r0 < N; r0 += (int64_t)gridDim.x * 128) {
-  // read: thread t takes rows r0 + 4 (t % 32) .. + 3 of features t / 32 + 8 i
+  constexpr int VN = NT_VEC<T>::n, CPR = NT_FC / VN;          // 16-byte chunks per row and feature chunk
+  for (int64_t r0 = (int64_t)blockIdx.x * NT_ROWS; r0 < N; r0 += (int64_t)gridDim.x * NT_ROWS) {
+    for (int fc = 0; fc < nf; fc += NT_FC) {
+      // read: thread t takes rows r0 + 4 (t % 8) .. + 3 of features fc + t / 8 + 32 i
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int k = t / 32 + 8 * i, c = t % 32;
-    const int f = f0 + k;
-    const int64_t r = r0 + 4 * c;
-    float v[4] = {0.f, 0.f, 0.f, 0.f};
-    if (f < nf) {
-      const float* x = X + (int64_t)rows[f] * N;
-      if (vin && r + 3 < N) {
-        const float4 q = *reinterpret_cast<const float4*>(x + r);
-        v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
-      } else {
+      for (int i = 0; i < NT_FC / 32; ++i) {
+        const int k = t / 8 + 32 * i, c = t % 8;
+        const int f = fc + k;
+        const int64_t r = r0 + 4 * c;
+        float v[4] = {0.f, 0.f, 0.f, 0.f};
+        if (f < nf) {
+          const float* x = X + (int64_t)rows[f] * N;
+          if (vin && r + 3 < N) {
+            const float4 q = *reinterpret_cast<const float4*>(x + r);
+            v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+          } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = r + j < N ? x[r + j] : 0.f;
+            for (int j = 0; j < 4; ++j) v[j] = r + j < N ? x[r + j] : 0.f;
+          }
+          const float fl = fill[f], sb = sub[f], ml = mul[f];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = ((v[j] != v[j]) ? fl : v[j]) - sb, v[j] *= ml;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) tile[k][4 * c + j] = v[j];
       }
-      const float fl = fill[f], sb = sub[f], ml = mul[f];
+      __syncthreads();
+      // write: VN consecutive features of one row per 16-byte store
+      const bool vout = (ldz % VN) == 0 && ((col0 + fc) % VN) == 0;
+      for (int idx = t; idx < NT_ROWS * CPR; idx += 256) {
+        const int rr = idx / CPR, q = idx % CPR;
+        const int64_t r = r0 + rr;
+        const int fq = fc + q * VN;
+        if (r >= N || fq >= nf) continue;
+        float v[VN];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = ((v[j] != v[j]) ? fl : v[j]) - sb, v[j] *= ml;
+        for (int j = 0; j < VN; ++j) v[j] = tile[q * VN + j][rr];
+        T* dst = Z + r * ldz + col0 + fq;
+        if (vout && fq + VN <= nf) {
+          *reinterpret_cast<uint4*>(dst) = pack_row(v, (T*)nullptr);
+        } else {
+#pragma unroll
+          for (int j = 0; j < VN; ++j) if (fq + j < nf) st(dst, j, v[j]);
+        }
+      }
+      __syncthreads();        // the tile is refilled for the next feature chunk / row range
     }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) tile[k][4 * c + j] = v[j];
-  }
-  __syncthreads();
-  // write: VN consecutive features of one row per 16-byte store
-  constexpr int VN = NT_VEC<T>::n, CPR = 32 / VN;          // chunks per row
-  const bool vout = (ldz % VN) == 0 && ((col0 + f0) % VN) == 0;
-  for (int idx = t; idx < 128 * CPR; idx += 256) {
-    const int rr = idx / CPR, q = idx % CPR;
-    const int64_t r = r0 + rr;
-    if (r >= N) continue;
-    const int fq = f0 + q * VN;
-    float v[VN];
-#pragma unroll
-    for (int j = 0; j < VN; ++j) v[j] = tile[q * VN + j][rr];
-    T* dst = Z + r * ldz + col0 + fq;
-    if (vout && fq + VN <= nf) {
-      *reinterpret_cast<uint4*>(dst) = pack_row(v, (T*)nullptr);
-    } else {
-#pragma unroll
-      for (int j = 0; j < VN; ++j) if (fq + j < nf) st(dst, j, v[j]);
-    }
-  }
-  __syncthreads();          // the tile is refilled for the next row range
   }
 }
 
@@ -325,11 +330,10 @@ int h2o_num_stats(const float* X, long long N, const int* rows, int nf, const fl
 int h2o_num_transform(const float* X, long long N, const int* rows, int nf, const float* fill, const float* sub,
                       const float* mul, void* Z, int ldz, int col0, int bf16, hipStream_t s) {
   if (N <= 0 || nf <= 0) return 0;
-  // row tiles strided over a bounded grid (each block several 128-row tiles of its 32 features)
-  long long gx = (N + 127) / 128;
-  const long long cap = (8192 + (nf + 31) / 32 - 1) / ((nf + 31) / 32) * 4;
-  if (gx > cap) gx = cap;
-  dim3 grid((unsigned)gx, (unsigned)((nf + 31) / 32));
+  // 32-row blocks strided over a bounded grid
+  long long gx = (N + NT_ROWS - 1) / NT_ROWS;
+  if (gx > 16384) gx = 16384;
+  dim3 grid((unsigned)gx);
   if (bf16)
     hipLaunchKernelGGL(k_num_transform<__hip_bfloat16>, grid, dim3(256), 0, s, X, (int64_t)N, rows, nf, fill, sub, mul,
                        (__hip_bfloat16*)Z, ldz, col0);
