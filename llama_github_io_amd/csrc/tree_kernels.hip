@@ -1940,7 +1940,10 @@ static void launch_hist(dim3 grid, size_t lds, hipStream_t s, const void* bins, 
   const unsigned long long bytes = (unsigned long long)N * (unsigned long long)rowb;
   int lgw = -1;
   for (int k = 0; k < 12; ++k) if (rowb == (1 << k)) lgw = k;
-  const bool buf = lgw >= 0 && bytes < (1ull << 31) && (unsigned long long)N * 4ull < (1ull << 31);
+  // (buffer offsets and NUM_RECORDS are unsigned 32-bit: up to 4 GiB per buffer, e.g. a 100M-row 32-byte plane)
+  const char* e_buf = getenv("H2O_HIST_BUF");     // A/B and test switch: 0 = 64-bit addressing
+  const bool buf = lgw >= 0 && bytes < (1ull << 32) && (unsigned long long)N * 4ull < (1ull << 32) &&
+                   !(e_buf && strcmp(e_buf, "0") == 0);
 #define H2O_HIST_CASE(F_, N_, B_) \
   launch_hist4<F_, PACKED, UNIT, N_, B_>(grid, lds, s, bins, stride, aw, ay, nodes, tile_prefix, meta, F, partials, \
                                           slot_doubles, qs, pdec, nl_out, f32, N, planar, lgw, nbins_f, fine_f)

@@ -445,6 +445,41 @@ def _big_bins(N, F, stride, seed):
 
 
 @pytest.mark.gpu
+def test_gpu_planar_plane_above_2pow31_bytes_buffer_addressing(monkeypatch):
+    """Planes of more than 2^31 bytes (70M rows x 32 B, like the 100M x 50 XGBoost config) take the 32-bit
+    unsigned buffer-offset histogram path: the same tree as the 64-bit addressing path, decision for decision
+    and row for row."""
+    N, F = 70_000_000, 6
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(5)
+    bins = torch.zeros(N, 64, dtype=torch.uint8, device=dev)
+    bins[:, :F] = torch.randint(0, 200, (N, F), generator=g, device=dev, dtype=torch.uint8)
+    y = ((bins[:, 0].float() - 100) / 60 - (bins[:, 1] > 120).float() +
+         torch.randn(N, generator=g, device=dev) > 0).float()
+    gr = -(y - 0.5)
+    h = torch.full_like(y, 0.25)
+    aux = torch.stack([h, -gr, -gr, h], 0).contiguous()
+    p = T.SplitParams(min_w=1.0, lam=1.0, mode=T.MODE_NEWTON)
+    nb = np.full(F, 200, np.int32)
+    ic = np.zeros(F, np.int32)
+    out = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("H2O_HIST_BUF", flag)
+        gb = T.GpuTreeBuilder(bins, F, nb, ic, None, 4, p)
+        assert gb.planar and gb.N * 32 > (1 << 31)
+        gb.build(aux, soa=True, leaf_fn=lambda ls: (ls[:, 0] / (ls[:, 1] + 1.0)).float())
+        out.append((gb.pop_levels()[0], gb.leaf_of_row.clone()))
+        del gb
+        torch.cuda.empty_cache()
+    (ta, la), (tb, lb) = out
+    assert ta.n_leaves == tb.n_leaves > 8
+    for da, db in zip(ta.decs, tb.decs):
+        assert np.array_equal(da["feat"], db["feat"]) and np.array_equal(da["bin"], db["bin"])
+        np.testing.assert_array_equal(da["wl"], db["wl"])
+    assert torch.equal(la, lb)
+
+
+@pytest.mark.gpu
 def test_gpu_tree_bins_matrix_above_2pow31_bytes():
     """The row payload of a >2^31-byte bins matrix (42M x 52 B = 2.18 GB, the stride of the 100M x 50
     XGBoost config) is indexed in 64 bits by every kernel: unpacked (Newton) histograms, the moving and the
