@@ -23,7 +23,10 @@ namespace {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int TILE = 64;
-constexpr int UNRG = 8;      // row pairs in flight per lane
+#ifndef GRAM_UNRG
+#define GRAM_UNRG 8
+#endif
+constexpr int UNRG = GRAM_UNRG;      // row pairs in flight per lane
 
 __device__ __forceinline__ float zload(const float* __restrict__ Z, int64_t ldz, const float* __restrict__ u,
                                        int64_t r, bool ok, int c, int P) {

@@ -5,6 +5,8 @@ in fp64); CPU tensors use the fp64 PyTorch reference (the test oracle).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _native as nat
@@ -44,7 +46,8 @@ def zbeta(Z: torch.Tensor, B: torch.Tensor, off=None) -> torch.Tensor:
 
 
 def _splits(N: int, pairs: int) -> int:
-    target = max(1, 4096 // max(1, pairs))        # one wave per (tile pair, slice): ~16 waves per CU
+    waves = int(os.environ.get("H2O_GRAM_WAVES", "4096"))     # A/B: waves per launch
+    target = max(1, waves // max(1, pairs))       # one wave per (tile pair, slice): ~16 waves per CU
     return int(max(1, min(target, (N + 1023) // 1024)))
 
 
