@@ -4,7 +4,9 @@ set -o pipefail
 O=gpurun_out/r4_gram
 mkdir -p $O
 export TMPDIR=/tmp
-for cfg in "4096 main" "8192 main" "16384 main" "4096 unrg16"; do
+CFGS=${GRAM_CFGS:-"4096,main 8192,main 16384,main 4096,unrg16"}
+for cfg in $CFGS; do
+  cfg=${cfg/,/ }
   set -- $cfg
   lib=""; [ "$2" != main ] && lib="H2O_HIP_LIB=$PWD/llama_github_io_amd/lib_alt/$2.so"
   env H2O_GRAM_WAVES=$1 $lib timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/p_$1_$2 -o run -- python scripts/bench_suite.py --which glm_big > $O/run_$1_$2.log 2>&1 || { tail -5 $O/run_$1_$2.log; exit 1; }
