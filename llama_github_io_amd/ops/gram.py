@@ -46,8 +46,10 @@ def zbeta(Z: torch.Tensor, B: torch.Tensor, off=None) -> torch.Tensor:
 
 
 def _splits(N: int, pairs: int) -> int:
-    waves = int(os.environ.get("H2O_GRAM_WAVES", "4096"))     # A/B: waves per launch
-    target = max(1, waves // max(1, pairs))       # one wave per (tile pair, slice): ~16 waves per CU
+    # one wave per (tile pair, slice): ~32 waves per CU. MEASURED r4 (10M x 51 augmented Gram, k_gram):
+    # 4096 waves 1163 us, 8192 923, 16384 1004; 16 row pairs in flight per lane (GRAM_UNRG) 907-942 (kept 8)
+    waves = int(os.environ.get("H2O_GRAM_WAVES", "8192"))
+    target = max(1, waves // max(1, pairs))
     return int(max(1, min(target, (N + 1023) // 1024)))
 
 
