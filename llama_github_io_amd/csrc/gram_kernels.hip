@@ -102,7 +102,17 @@ __global__ __launch_bounds__(256) void k_xtv(const float* __restrict__ Z, int64_
   __shared__ float red[4][64][8];
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (p < P) {
-    for (int64_t r = r_begin + rq; r < r_end; r += 4) {
+    int64_t r = r_begin + rq;
+    // 4 rows per step, their loads issued before the accumulation (one load in flight per lane before)
+    for (; r + 12 < r_end; r += 16) {
+      float z[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) z[u] = Z[(r + 4 * u) * ldz + p];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        for (int q = 0; q < R && q < 8; ++q) acc[q] += z[u] * v[(r + 4 * u) * R + q];
+    }
+    for (; r < r_end; r += 4) {
       const float z = Z[r * ldz + p];
       for (int q = 0; q < R && q < 8; ++q) acc[q] += z * v[r * R + q];
     }
@@ -147,7 +157,20 @@ __global__ __launch_bounds__(ZB_THREADS) void k_zbeta(const float* __restrict__ 
     const int n4 = (int)(n >> 2);
     const float4* s4 = reinterpret_cast<const float4*>(src);
     float4* d4 = reinterpret_cast<float4*>(tile);
-    for (int i = t; i < n4; i += ZB_THREADS) d4[i] = s4[i];
+    // every 16-byte load of the span is issued before the first LDS store (12 in flight per lane; a
+    // load -> store loop waited on each one)
+    constexpr int ZU = ZB_LDS_FLOATS / 4 / ZB_THREADS;
+    float4 v[ZU];
+#pragma unroll
+    for (int u = 0; u < ZU; ++u) {
+      const int i = t + u * ZB_THREADS;
+      v[u] = i < n4 ? s4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < ZU; ++u) {
+      const int i = t + u * ZB_THREADS;
+      if (i < n4) d4[i] = v[u];
+    }
     for (int i = 4 * n4 + t; i < n; i += ZB_THREADS) tile[i] = src[i];
   } else {
     for (int i = t; i < n; i += ZB_THREADS) {
