@@ -502,7 +502,8 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
     int slot_doubles, const double* __restrict__ qs /*[sa, sb, 1/sa, 1/sb, sp, 1/sp]*/,
     const Dec* __restrict__ pdec, int* __restrict__ nl_out, int f32, long long N, int planar, int lgw,
     const int* __restrict__ nbins_f /*[F] (NONA: low-cardinality spreading) or null*/,
-    const int* __restrict__ fine_f /*[F] 1 = column of an aligned 4-column wide numeric group, or null*/) {
+    const int* __restrict__ fine_f /*[F] 1 = column of an aligned 4-column wide numeric group, or null*/,
+    const uint8_t* __restrict__ fdir /*FILT: per row 0 = left / 1 = right of the parent split, or null*/) {
   constexpr bool packed = PACKED;
   extern __shared__ __attribute__((aligned(16))) long long smem64[];
   long long* h = smem64;                                 // 2 planes (PACKED: 1 -> two blocks per CU fit)
@@ -598,10 +599,12 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
         flt.feat = spd.feat;
         flt.fptr = bins + bin_off(0, spd.feat, stride, N, planar);
         flt.fstride = planar ? 32 : stride;
+        if (fdir) { flt.fptr = fdir; flt.fstride = 1; }
         const int jw = (spd.feat >> 2) - ftile * LPR;
         flt.jw = (jw >= 0 && jw < LPR) ? jw : -1;
         flt.dir = nd.dir;
         flt.bin = spd.bin; flt.na_left = spd.na_left; flt.is_cat = spd.is_cat;
+        if (fdir) { flt.bin = 1; flt.na_left = 0; flt.is_cat = 0; }    // direction bytes: 0 goes left
         flt.count = ftile == 0;
       }
     }
@@ -1444,7 +1447,8 @@ __global__ __launch_bounds__(LW * 64) void k_route(
     const Node* __restrict__ nodesA, const int* __restrict__ tpA, const int* __restrict__ metaA,
     const Dec* __restrict__ decA, const int* __restrict__ clA, const int* __restrict__ crA,
     const Dec* __restrict__ decB, const int* __restrict__ clB, const int* __restrict__ crB,
-    int4* __restrict__ curs, long long N, int planar, uint8_t* __restrict__ lvl2) {
+    int4* __restrict__ curs, long long N, int planar, uint8_t* __restrict__ lvl2,
+    const uint8_t* __restrict__ fdir /*root route: per row the root split's direction (k_row_dir), or null*/) {
   const int n_nodes = metaA[0], n_tiles = metaA[1];
   const int t = blockIdx.x;
   if (t >= n_tiles) return;
@@ -1503,7 +1507,9 @@ __global__ __launch_bounds__(LW * 64) void k_route(
     const bool valid = row < r1;
     int dA = 0, dB = 0;
     // (a split column past the registers — narrow copies, lp > 0 — is read from the source)
-    if (valid && featA >= 0)
+    if (fdir) {
+      dA = valid && featA >= 0 ? fdir[row] : 0;
+    } else if (valid && featA >= 0)
       dA = dec_go_left(&sA, (NV > 0 && featA >= NV * 16) ? sbins[bin_off(row, featA, stride, N, planar)]
                             : NV > 2 ? row_byte4(rv0[u], rv1[u], rv2[u], rv3[u], featA)
                             : NV > 0 ? row_byte(rv0[u], rv1[u], featA) : sbins[bin_off(row, featA, stride, N, planar)]) ? 0 : 1;
@@ -1587,6 +1593,20 @@ __global__ __launch_bounds__(LW * 64) void k_route(
     day[pos] = ry[u];
     if (daw) daw[pos] = rw[u];
   }
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_row_dir: every row's side of the root split (0 left, 1 right), one byte per row in the original order. Narrow
+// runs read the root split's column from a plane nothing else of level 1 reads: the two level-1 histogram blocks
+// and the root route then read these bytes (1 B per row) instead of that plane (32 B per row each).
+__global__ __launch_bounds__(256) void k_row_dir(const uint8_t* __restrict__ bins, int stride, long long N, int planar,
+                                                 const Dec* __restrict__ dec, uint8_t* __restrict__ out) {
+  __shared__ Dec sd;
+  if (threadIdx.x < (int)(sizeof(Dec) / 4)) ((int*)&sd)[threadIdx.x] = ((const int*)dec)[threadIdx.x];
+  __syncthreads();
+  const int f = sd.feat;
+  for (long long row = (long long)blockIdx.x * blockDim.x + threadIdx.x; row < N; row += (long long)gridDim.x * blockDim.x)
+    out[row] = (f >= 0 && !dec_go_left(&sd, bins[bin_off(row, f, stride, N, planar)])) ? 1 : 0;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1919,18 +1939,18 @@ template <bool FILT, bool PACKED, bool UNIT, bool NONA, bool BUF>
 static void launch_hist4(dim3 grid, size_t lds, hipStream_t s, const void* bins, int stride, const void* aw,
                          const void* ay, const void* nodes, const void* tile_prefix, const void* meta, int F,
                          void* partials, int slot_doubles, const void* qs, const void* pdec, void* nl_out, int f32,
-                         long long N, int planar, int lgw, const void* nbins_f, const void* fine_f) {
+                         long long N, int planar, int lgw, const void* nbins_f, const void* fine_f, const void* fdir) {
   hipLaunchKernelGGL((k_hist_build<FILT, PACKED, UNIT, NONA, BUF>), grid, dim3(BLK), lds, s, (const uint8_t*)bins,
                      stride, (const float*)aw, (const float*)ay, (const Node*)nodes, (const int*)tile_prefix,
                      (const int*)meta, F, (double*)partials, slot_doubles, (const double*)qs, (const Dec*)pdec,
-                     (int*)nl_out, f32, N, planar, lgw, (const int*)nbins_f, (const int*)fine_f);
+                     (int*)nl_out, f32, N, planar, lgw, (const int*)nbins_f, (const int*)fine_f, (const uint8_t*)fdir);
 }
 
 template <bool PACKED, bool UNIT>
 static void launch_hist(dim3 grid, size_t lds, hipStream_t s, const void* bins, int stride, const void* aw,
                         const void* ay, const void* nodes, const void* tile_prefix, const void* meta, int F,
                         void* partials, int slot_doubles, const void* qs, const void* pdec, void* nl_out, int f32,
-                        long long N, int planar, const void* nbins_f, const void* fine_f) {
+                        long long N, int planar, const void* nbins_f, const void* fine_f, const void* fdir) {
   // flags: bit 0 planar bins, bit 1 no NA bin anywhere (NONA kernels)
   const bool nona = (planar >> 1) & 1;
   planar &= 1;
@@ -1946,7 +1966,7 @@ static void launch_hist(dim3 grid, size_t lds, hipStream_t s, const void* bins, 
                    !(e_buf && strcmp(e_buf, "0") == 0);
 #define H2O_HIST_CASE(F_, N_, B_) \
   launch_hist4<F_, PACKED, UNIT, N_, B_>(grid, lds, s, bins, stride, aw, ay, nodes, tile_prefix, meta, F, partials, \
-                                          slot_doubles, qs, pdec, nl_out, f32, N, planar, lgw, nbins_f, fine_f)
+                                          slot_doubles, qs, pdec, nl_out, f32, N, planar, lgw, nbins_f, fine_f, fdir)
   const bool filt = pdec != nullptr;
   if (filt) {
     if (nona) { if (buf) H2O_HIST_CASE(true, true, true); else H2O_HIST_CASE(true, true, false); }
@@ -1991,7 +2011,7 @@ int h2o_tree_sizes(int* out) {
 int h2o_hist_build(const void* bins, int stride, const void* aw, const void* ay, const void* nodes,
                    const void* tile_prefix, const void* meta, int F, void* partials, int slot_doubles, const void* qs,
                    int grid, int packed, const void* pdec, void* nl_out, int f32, long long N, int planar,
-                   const void* nbins_f, const void* fine_f, int nft_lim, hipStream_t s) {
+                   const void* nbins_f, const void* fine_f, int nft_lim, const void* fdir, hipStream_t s) {
   int nft = (F + FTILE - 1) / FTILE;
   if (nft_lim > 0 && nft_lim < nft) nft = nft_lim;
   // A/B switches: H2O_HIST_REPL=0 drops the low-cardinality bin replicas, H2O_HIST_FINE=1 enables the
@@ -2006,9 +2026,9 @@ int h2o_hist_build(const void* bins, int stride, const void* aw, const void* ay,
   const size_t lds = (packed ? HIST_LDS_BYTES - HPLANE * 8 : HIST_LDS_BYTES) + HIST_LDS_TAIL;
   const dim3 gr(grid, nft);
   if (packed && aw == nullptr)   // unit row weights (the trainer dropped the w plane)
-    launch_hist<true, true>(gr, lds, s, bins, stride, aw, ay, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out, f32, N, planar, nbins_f, fine_f);
-  else if (packed) launch_hist<true, false>(gr, lds, s, bins, stride, aw, ay, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out, f32, N, planar, nbins_f, fine_f);
-  else launch_hist<false, false>(gr, lds, s, bins, stride, aw, ay, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out, f32, N, planar, nbins_f, fine_f);
+    launch_hist<true, true>(gr, lds, s, bins, stride, aw, ay, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out, f32, N, planar, nbins_f, fine_f, fdir);
+  else if (packed) launch_hist<true, false>(gr, lds, s, bins, stride, aw, ay, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out, f32, N, planar, nbins_f, fine_f, fdir);
+  else launch_hist<false, false>(gr, lds, s, bins, stride, aw, ay, nodes, tile_prefix, meta, F, partials, slot_doubles, qs, pdec, nl_out, f32, N, planar, nbins_f, fine_f, fdir);
   return (int)hipGetLastError();
 }
 
@@ -2145,7 +2165,7 @@ static int nv_of(int stride) {
 int h2o_route(const void* sbins, const void* say, const void* saw, void* dbins, void* day, void* daw, int stride,
               const void* nodesA, const void* tpA, const void* metaA, const void* decA, const void* clA,
               const void* crA, const void* decB, const void* clB, const void* crB, void* curs, int tiles_cap,
-              long long N, int planar, int lp, void* lvl2, hipStream_t s) {
+              long long N, int planar, int lp, void* lvl2, const void* fdir, hipStream_t s) {
   if (planar && (stride % 32 != 0 || stride < 64)) return (int)hipErrorInvalidValue;
   if (lp < 0 || lp > 2 || (lp > 0 && !planar)) return (int)hipErrorInvalidValue;
 #define ROUTE_LAUNCH(NV)                                                                                       \
@@ -2153,7 +2173,7 @@ int h2o_route(const void* sbins, const void* say, const void* saw, void* dbins, 
                      (const float*)say, (const float*)saw, (uint8_t*)dbins, (float*)day, (float*)daw, stride,  \
                      (const Node*)nodesA, (const int*)tpA, (const int*)metaA, (const Dec*)decA, (const int*)clA, \
                      (const int*)crA, (const Dec*)decB, (const int*)clB, (const int*)crB, (int4*)curs, N, planar, \
-                     (uint8_t*)lvl2)
+                     (uint8_t*)lvl2, (const uint8_t*)fdir)
   switch (lp == 1 ? 2 : lp == 2 ? 4 : nv_of(stride)) {
     case 4: ROUTE_LAUNCH(4); break;
     case 3: ROUTE_LAUNCH(3); break;
@@ -2302,6 +2322,7 @@ struct TreePlan {
   // lo_F / mid_F = 0: off.
   int lo_F, lo_from, mid_F, mid_from;
   void* lvl2;                 // [N] uint8: the root route's level-2 node / 128 + leaf per row (narrow runs; or null)
+  void* fdir;                 // [N] uint8: the root split's side per row (k_row_dir; narrow planar runs, or null)
 };
 
 // op codes / dtypes of the collective transport
@@ -2342,7 +2363,8 @@ static int tp_route(const TreePlan* P, int e, hipStream_t s) {
   const int lp = (P->planar && np <= 2) ? np : 0;
   return h2o_route(sb, sy, sw, P->bb[di], P->by[di], P->unit ? nullptr : P->bw[di], P->stride, P->nodes[e], P->tp[e],
                    P->meta[e], P->dec[e], P->cl[e], P->cr[e], P->dec[e + 1], P->cl[e + 1], P->cr[e + 1],
-                   P->cur[e + 1], P->tiles_cap[e], P->N, P->planar, lp, e == 0 ? tp_lvl2(P) : nullptr, s);
+                   P->cur[e + 1], P->tiles_cap[e], P->N, P->planar, lp, e == 0 ? tp_lvl2(P) : nullptr,
+                   (e == 0 && tp_lvl2(P) && P->fdir) ? P->fdir : nullptr, s);
 }
 
 #define TP_CHECK(x) do { int rc_ = (x); if (rc_) return rc_; } while (0)
@@ -2358,7 +2380,7 @@ int h2o_tree_root(const TreePlan* P, hipStream_t s) {
   const int g0 = P->tiles_cap[0] < P->grid ? P->tiles_cap[0] : P->grid;
   TP_CHECK(h2o_hist_build(P->master, P->stride, P->unit ? nullptr : tp_aux(P, 0), tp_aux(P, 1), P->nodes[0], P->bp[0],
                           P->meta[0], P->F, P->partials, P->slot, P->qs, g0, P->packed, nullptr, nullptr, P->pf32, P->N,
-                          P->planar | (P->no_na << 1), P->nbins_f, P->fine_f, tp_planes(tp_fcut(P, 0)), s));
+                          P->planar | (P->no_na << 1), P->nbins_f, P->fine_f, tp_planes(tp_fcut(P, 0)), nullptr, s));
   // row-sharded all-reduce: straight into the wire buffer; sliced: hbuild (packed by slice next)
   if (P->dist && !P->sliced)
     return h2o_hist_reduce(P->partials, P->slot, P->used, P->nodes[0], P->bp[0], P->meta[0], 1, g0, P->hrecv, nullptr,
@@ -2429,9 +2451,22 @@ int h2o_tree_grow(const TreePlan* P, int d, int dist, hipStream_t s) {
     // level d+1 (odd) is histogrammed straight from level d's ranges, filtered by level d's decisions
     gh = P->tiles_cap[d] < P->grid ? P->tiles_cap[d] : P->grid;
     tp_level_buf(P, d, sb, sy, sw);
+    // level 1 of a narrow planar run: the root split's side of every row as bytes (read by the level-1
+    // histogram blocks and the root route instead of the split column's plane)
+    const void* fdir = nullptr;
+    if (d == 0 && tp_lvl2(P) && P->fdir) {
+      long long g = (P->N + 255) / 256;
+      if (g > 4096) g = 4096;
+      if (g < 1) g = 1;
+      hipLaunchKernelGGL(k_row_dir, dim3((unsigned)g), dim3(256), 0, s, (const uint8_t*)P->master, P->stride, P->N,
+                         P->planar, (const Dec*)P->dec[0], (uint8_t*)P->fdir);
+      rc = (int)hipGetLastError();
+      if (rc) return -rc;
+      fdir = P->fdir;
+    }
     rc = h2o_hist_build(sb, P->stride, sw, sy, P->nodes[d + 1], P->bp[d + 1], P->meta[d + 1], P->F, P->partials,
                         P->slot, P->qs, gh, P->packed, P->dec[d], P->nl[d], P->pf32, P->N, P->planar | (P->no_na << 1),
-                        P->nbins_f, P->fine_f, tp_planes(tp_fcut(P, d + 1)), s);
+                        P->nbins_f, P->fine_f, tp_planes(tp_fcut(P, d + 1)), fdir, s);
   } else {
     // regroup level d-1's rows two levels down, then histogram level d+1 (even) contiguously
     rc = tp_route(P, d - 1, s);
@@ -2442,7 +2477,7 @@ int h2o_tree_grow(const TreePlan* P, int d, int dist, hipStream_t s) {
     tp_level_buf(P, d + 1, sb, sy, sw);
     rc = h2o_hist_build(sb, P->stride, sw, sy, P->nodes[d + 1], P->bp[d + 1], P->meta[d + 1], P->F, P->partials,
                         P->slot, P->qs, gh, P->packed, nullptr, nullptr, P->pf32, P->N, P->planar | (P->no_na << 1),
-                        P->nbins_f, P->fine_f, tp_planes(tp_fcut(P, d + 1)), s);
+                        P->nbins_f, P->fine_f, tp_planes(tp_fcut(P, d + 1)), nullptr, s);
   }
   if (rc) return -rc;
   const int lo = tp_fcut(P, d + 1);

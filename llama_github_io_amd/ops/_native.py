@@ -39,7 +39,8 @@ _HIP_SIGS = {
     "h2o_tree_all": [c_void_p, c_void_p],
     "h2o_tree_leaves": [c_void_p, c_void_p],
     "h2o_hist_build": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p,
-                       c_int, c_int, c_void_p, c_void_p, c_int, c_ll, c_int, c_void_p, c_void_p, c_int, c_void_p],
+                       c_int, c_int, c_void_p, c_void_p, c_int, c_ll, c_int, c_void_p, c_void_p, c_int, c_void_p,
+                       c_void_p],
     "h2o_split_find": [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_double, c_double,
                        c_double, c_double, c_double, c_int, c_int, c_ull, c_int, c_void_p, c_void_p, c_void_p, c_int,
                        c_int, c_int, c_int, c_void_p],
@@ -49,7 +50,7 @@ _HIP_SIGS = {
     "h2o_plan": [c_void_p] * 14 + [c_int, c_int, c_double, c_int, c_int, c_void_p],
     "h2o_ranges": [c_void_p] * 6,
     "h2o_zero_hist": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
-    "h2o_route": [c_void_p] * 6 + [c_int] + [c_void_p] * 10 + [c_int, c_ll, c_int, c_int, c_void_p, c_void_p],
+    "h2o_route": [c_void_p] * 6 + [c_int] + [c_void_p] * 10 + [c_int, c_ll, c_int, c_int, c_void_p, c_void_p, c_void_p],
     "h2o_leaf_assign": [c_void_p, c_int, c_ll, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                         c_void_p, c_int, c_int, c_void_p],
     "h2o_bin_assign": [c_void_p, c_ll, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
@@ -72,7 +73,7 @@ _HIP_SIGS = {
 # Bumped whenever a C launcher's argument list changes; every native library exports h2o_abi_version()
 # (csrc/abi.h) and a library built from older sources is refused instead of being called with shifted
 # arguments.
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 
 def _check_abi(lib, name: str) -> None:

@@ -585,7 +585,7 @@ class _TreePlan(ctypes.Structure):
                 [("leaf_lam", _cd), ("leaf_l1", _cd)] + [("planar", _ci), ("no_na", _ci)] +
                 [("fgroup", _vp)] + [("coll_fn", _vp), ("coll_ctx", _vp)] +
                 [(n, _ci) for n in ("W", "cf32", "cand_fs", "dist")] + [(n, _vp) for n in ("hsend", "cand_all", "lsx")] +
-                [("fine_f", _vp)] + [(n, _ci) for n in ("lo_F", "lo_from", "mid_F", "mid_from")] + [("lvl2", _vp)])
+                [("fine_f", _vp)] + [(n, _ci) for n in ("lo_F", "lo_from", "mid_F", "mid_from")] + [("lvl2", _vp), ("fdir", _vp)])
 
 
 class _Arena:
@@ -828,9 +828,13 @@ class GpuTreeBuilder:
         P.lo_F, P.lo_from = (self.n_low, lo) if lo >= 0 else (0, 0)
         P.mid_F, P.mid_from = (self.n_mid, mid) if mid >= 0 else (0, 0)
         # every row's level-2 position from the root route (the leaf walk starts there; narrow planar runs only)
+        # and the root split's side of every row (level 1 reads these bytes instead of the split column's plane)
         if lo >= 0 and self.planar and getattr(self, "_lvl2", None) is None:
             self._lvl2 = torch.empty(self.N, dtype=torch.uint8, device=self.dev)
-        P.lvl2 = self._lvl2.data_ptr() if (lo >= 0 and self.planar) else 0
+            self._fdir = torch.empty(self.N, dtype=torch.uint8, device=self.dev)
+        on = lo >= 0 and self.planar
+        P.lvl2 = self._lvl2.data_ptr() if on else 0
+        P.fdir = self._fdir.data_ptr() if on else 0
 
     def _set_plan_ic(self, P):
         if self.ic_map is None:
