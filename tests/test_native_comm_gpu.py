@@ -89,6 +89,37 @@ def test_row_sharded_tree_on_rccl_matches_reference(depth, mode, dtype, force_en
         assert torch.equal(ref.leaf_of_row, gb.leaf_of_row.cpu())
 
 
+@pytest.mark.parametrize("mode", ["ar", "rs"])
+def test_narrow_planar_tree_on_rccl_matches_reference(mode, force_env):
+    """H2O's default histogram on wide bins (1016 edges per feature, planar rows): the narrow levels (column
+    limits, low-entry reduce, one-plane routes, root-direction bytes, level-2 leaf-walk start) through the
+    row-sharded driver on a 1-rank RCCL communicator, decision for decision against RefTreeBuilder."""
+    from test_tree_engine import _edge_tab
+    X, y, info = _data(N=30000, F=10, cat=True, seed=11)
+    b = fit_binning(X, info.iscat, info.nlevels, max_bins=1016)
+    assert b.stride >= 64 and b.n_low == X.shape[0]
+    bins = apply_binning(b, X)
+    g = y - 0.5
+    aux = torch.stack([torch.ones_like(y), g, g, torch.ones_like(y)], 1).contiguous()
+    p = T.SplitParams(min_w=10, adapt_nbins=20, adapt_top=1024, edges=_edge_tab(b))
+    ref = T.RefTreeBuilder(bins, b.F, b.nbins, b.iscat, None, 5, p)
+    ref.set_feature_groups(b.vmap, b.n_low, b.n_mid)
+    ref.build(aux, leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1]).float())
+    tl_r = ref.pop_levels()[0]
+    force_env(mode, "f64")
+    dev = torch.device("cuda", 0)
+    gb = T.GpuTreeBuilder(apply_binning(b, X.to(dev), planar=True), b.F, b.nbins, b.iscat, None, 5, p)
+    gb.set_feature_groups(b.vmap, b.n_low, b.n_mid)
+    assert gb.dist_mode and gb.planar
+    gb.build(aux.to(dev), leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1]).float())
+    tl_g = gb.pop_levels()[0]
+    assert tl_g.n_leaves == tl_r.n_leaves
+    for dr, dg in zip(tl_r.decs, tl_g.decs):
+        assert np.array_equal(dr["feat"], dg["feat"]) and np.array_equal(dr["bin"], dg["bin"])
+        np.testing.assert_allclose(dr["wl"], dg["wl"], rtol=1e-6)
+    assert torch.equal(ref.leaf_of_row, gb.leaf_of_row.cpu())
+
+
 def test_gbm_on_rccl_equals_single_process(force_env, monkeypatch):
     """A whole GBM (gradients, leaf values on device, prediction update) through the 1-rank RCCL driver."""
     from llama_github_io_amd.models.gbm import GBMTrainer
