@@ -676,17 +676,16 @@ __global__ __launch_bounds__(RW * 64) void k_hist_reduce(
     else i = i < vb ? (i / lo2) * 2 * F + i % lo2 : NBIN * 2 * F + (i - vb);
   }
   const int ic = min(i, used - 1);
-  // 4 independent loads in flight per lane; fixed summation order -> deterministic result
-  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  // 8 independent loads in flight per lane (the root's 256 partials: 4 dependent rounds per wave instead of 8);
+  // fixed summation order -> deterministic result
+  double a[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
   int b = b0 + w;
-  for (; b + 3 * RW <= b1; b += 4 * RW) {
-    a0 += (double)partials[(size_t)(b + node) * slot_doubles + ic];
-    a1 += (double)partials[(size_t)(b + RW + node) * slot_doubles + ic];
-    a2 += (double)partials[(size_t)(b + 2 * RW + node) * slot_doubles + ic];
-    a3 += (double)partials[(size_t)(b + 3 * RW + node) * slot_doubles + ic];
+  for (; b + 7 * RW <= b1; b += 8 * RW) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a[k] += (double)partials[(size_t)(b + k * RW + node) * slot_doubles + ic];
   }
-  for (; b <= b1; b += RW) a0 += (double)partials[(size_t)(b + node) * slot_doubles + ic];
-  red[w][lane] = (a0 + a1) + (a2 + a3);
+  for (; b <= b1; b += RW) a[0] += (double)partials[(size_t)(b + node) * slot_doubles + ic];
+  red[w][lane] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
   __syncthreads();
   if (w != 0 || i >= used) return;
   double acc = red[0][lane];
