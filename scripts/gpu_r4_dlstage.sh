@@ -1,6 +1,7 @@
 #!/bin/bash
 # DL: weights of the small layers staged in LDS — GPU tests, A/B bench (H2O_DL_STAGE=0/1), phase clocks.
 set -o pipefail
+[ -f llama_github_io_amd/lib_alt/dlt.so ] || bash scripts/build_alt.sh dlt -DDL_TIMING > /dev/null || exit 1
 O=gpurun_out/r4_dlstage
 mkdir -p $O
 export TMPDIR=/tmp

@@ -1,6 +1,7 @@
 #!/bin/bash
 # k_dl_rows phase clocks (diagnostic DL_TIMING build) for bf16 and fp32
 set -o pipefail
+[ -f llama_github_io_amd/lib_alt/dlt.so ] || bash scripts/build_alt.sh dlt -DDL_TIMING > /dev/null || exit 1
 O=gpurun_out/r4_dlt
 mkdir -p $O
 for dt in bf16 float32; do

@@ -1,6 +1,7 @@
 #!/bin/bash
 # GLM Gram A/B: waves per launch (4096 / 8192 / 16384) and 16 row pairs in flight (alt build).
 set -o pipefail
+[ -f llama_github_io_amd/lib_alt/unrg16.so ] || bash scripts/build_alt.sh unrg16 -DGRAM_UNRG=16 > /dev/null || exit 1
 O=gpurun_out/r4_gram
 mkdir -p $O
 export TMPDIR=/tmp

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Three-tier narrow levels: tree-engine GPU tests, AUTO / QG bench, AUTO profile + tree sequence; DL phase clocks.
 set -o pipefail
+[ -f llama_github_io_amd/lib_alt/dlt.so ] || bash scripts/build_alt.sh dlt -DDL_TIMING > /dev/null || exit 1
 O=gpurun_out/r4_narrow2
 mkdir -p $O
 export TMPDIR=/tmp
