@@ -138,7 +138,9 @@ __global__ __launch_bounds__(256) void k_xtv(const float* __restrict__ Z, int64_
 // and writes eta once. MEASURED: column-tiled / half-wave-per-row variants read the 204-byte rows of a
 // 10M x 51 Z at 1.1-1.45 TB/s (several partial cache lines per load instruction).
 #define ZB_THREADS 256
+#ifndef ZB_LDS_FLOATS
 #define ZB_LDS_FLOATS 12288    // 48 KiB of Z per block
+#endif
 __global__ __launch_bounds__(ZB_THREADS) void k_zbeta(const float* __restrict__ Z, int64_t ldz,
                                                       const double* __restrict__ B, int R, int64_t N, int P, int TR,
                                                       const double* __restrict__ off, double* __restrict__ eta) {
