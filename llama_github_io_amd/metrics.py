@@ -214,8 +214,7 @@ def _threshold_table(uniq, tp, fp, nb):
     # bounds: the HSA 0x1016 memory fault of the 100M-row XGBoost run)
     idx = torch.linspace(0, n - 1, steps=min(n, nb), dtype=torch.float64, device=uniq.device).round().long().unique()
     idx = idx.clamp_(0, n - 1)
-    th = uniq[idx].cpu().numpy()
-    tps = tp[idx].cpu().numpy(); fps = fp[idx].cpu().numpy()
+    th, tps, fps = torch.stack([uniq[idx].double(), tp[idx].double(), fp[idx].double()]).cpu().numpy()   # one copy
     rows = []
     for t, a, b in zip(th, tps, fps):
         fn, tn = P - a, Nn - b
