@@ -49,6 +49,10 @@ def bench_xgb(a, dev, world, rank):
     y = (torch.rand(n, device=dev, generator=g) < torch.sigmoid(logit)).float()
     info = DataInfo([f"x{i}" for i in range(F)], np.zeros(F, np.int32), [None] * F, "y", ["0", "1"])
     T = a.trees or 500
+    # untimed warmup fit on a slice: library / kernel code objects page in on a fresh box (a cold first fit
+    # measured 230 ms/tree instead of ~22)
+    XGBoostTrainer(dict(ntrees=2, max_depth=6, learn_rate=0.3, seed=1, max_bins=256)).fit(
+        X[:, :1_000_000].contiguous(), y[:1_000_000].contiguous(), None, None, info)
     _sync()
     t0 = time.perf_counter()
     m = XGBoostTrainer(dict(ntrees=T, max_depth=6, learn_rate=0.3, seed=1, max_bins=256)).fit(X, y, None, None, info)
