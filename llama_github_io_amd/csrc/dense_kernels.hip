@@ -238,6 +238,54 @@ __global__ __launch_bounds__(256) void k_num_stats(const float* __restrict__ X, 
   }
 }
 
+// The same moments over the FLATTENED [nf][N] span (N % 4 == 0): block b reads the 64 KiB at b * NS_SPAN of the
+// listed rows laid end to end (at most two features per block), so the resident blocks stream one contiguous
+// window of X instead of 64 slices of every feature at once. MEASURED before: 9.9 ms for 10M x 784 (3.1 TB/s).
+#define NS_SPAN 16384
+__global__ __launch_bounds__(256) void k_num_stats_flat(const float* __restrict__ X, int64_t N,
+                                                        const int* __restrict__ rows, int nf,
+                                                        const float* __restrict__ w, double* __restrict__ out) {
+  const int64_t total = (int64_t)nf * N;
+  const int64_t e0 = (int64_t)blockIdx.x * NS_SPAN;
+  if (e0 >= total) return;
+  const int64_t e1 = e0 + NS_SPAN < total ? e0 + NS_SPAN : total;
+  __shared__ double red[3][4];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int64_t s = e0; s < e1;) {                // one or two features
+    const int j = (int)(s / N);
+    const int64_t fend = ((int64_t)j + 1) * N < e1 ? ((int64_t)j + 1) * N : e1;
+    const float* x = X + (int64_t)rows[j] * N;
+    const int64_t i0 = s - (int64_t)j * N, i1 = fend - (int64_t)j * N;
+    double a = 0.0, b = 0.0, c = 0.0;
+#pragma unroll 4
+    for (int64_t i = i0 + 4 * (int64_t)threadIdx.x; i < i1; i += 4 * 256) {
+      const float4 q = *reinterpret_cast<const float4*>(x + i);
+      const float4 wq = w ? *reinterpret_cast<const float4*>(w + i) : make_float4(1.f, 1.f, 1.f, 1.f);
+      const float v[4] = {q.x, q.y, q.z, q.w}, wv4[4] = {wq.x, wq.y, wq.z, wq.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (v[k] == v[k]) {
+          const double ww = (double)wv4[k];
+          a += ww; b += ww * v[k]; c += ww * (double)v[k] * v[k];
+        }
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      a += __shfl_down(a, o, 64); b += __shfl_down(b, o, 64); c += __shfl_down(c, o, 64);
+    }
+    if (lane == 0) { red[0][wv] = a; red[1][wv] = b; red[2][wv] = c; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const double s0 = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+      const double s1 = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+      const double s2 = (red[2][0] + red[2][1]) + (red[2][2] + red[2][3]);
+      atomicAdd(out + 3 * j, s0); atomicAdd(out + 3 * j + 1, s1); atomicAdd(out + 3 * j + 2, s2);
+    }
+    __syncthreads();
+    s = fend;
+  }
+}
+
 // Z[r, col0 + j] = (isnan(x) ? fill_j : x - sub_j) * mul_j for the numeric rows listed in `rows`. A block owns
 // 32 rows and walks the features in chunks of 256 through a [256][33] LDS tile: every read is one feature's 32
 // rows (128 contiguous bytes, 16-byte loads), every write a row's 256-feature run (512 B / 1 KB contiguous,
@@ -321,6 +369,11 @@ extern "C" {
 
 int h2o_num_stats(const float* X, long long N, const int* rows, int nf, const float* w, double* out, hipStream_t s) {
   if (N <= 0 || nf <= 0) return 0;
+  if ((N & 3) == 0) {
+    const long long nb = ((long long)nf * N + NS_SPAN - 1) / NS_SPAN;
+    hipLaunchKernelGGL(k_num_stats_flat, dim3((unsigned)nb), dim3(256), 0, s, X, (int64_t)N, rows, nf, w, out);
+    return (int)hipGetLastError();
+  }
   long long g = (N + 255) / 256;
   if (g > 64) g = 64;
   hipLaunchKernelGGL(k_num_stats, dim3((unsigned)g, (unsigned)nf), dim3(256), 0, s, X, (int64_t)N, rows, w, out);

@@ -85,7 +85,9 @@ class Expander:
             rows = torch.as_tensor(self.nums, dtype=torch.int32, device=dev)
             st = torch.zeros(k, 3, dtype=torch.float64, device=dev)
             wf = w.float().contiguous()
-            nat.call("h2o_num_stats", X.data_ptr(), N, rows.data_ptr(), k, wf.data_ptr(), st.data_ptr(),
+            # unit row weights are not re-read once per feature (784 x the weight column on a 784-wide frame)
+            unit = N > 0 and bool((wf == 1).all())
+            nat.call("h2o_num_stats", X.data_ptr(), N, rows.data_ptr(), k, 0 if unit else wf.data_ptr(), st.data_ptr(),
                      nat.stream_ptr(dev))
             sw, s1, s2 = st[:, 0].clone(), st[:, 1].clone(), st[:, 2].clone()
             CH = 0
