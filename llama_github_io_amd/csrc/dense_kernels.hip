@@ -304,8 +304,12 @@ __device__ __forceinline__ uint4 pack_row(const float* v, __hip_bfloat16*) {
 __device__ __forceinline__ uint4 pack_row(const float* v, float*) {
   return make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3]));
 }
+#ifndef NT_ROWS
 #define NT_ROWS 32
+#endif
+#ifndef NT_FC
 #define NT_FC 256
+#endif
 template <typename T>
 __global__ __launch_bounds__(256) void k_num_transform(const float* __restrict__ X, int64_t N, const int* __restrict__ rows,
                                                        int nf, const float* __restrict__ fill, const float* __restrict__ sub,
@@ -316,10 +320,11 @@ __global__ __launch_bounds__(256) void k_num_transform(const float* __restrict__
   constexpr int VN = NT_VEC<T>::n, CPR = NT_FC / VN;          // 16-byte chunks per row and feature chunk
   for (int64_t r0 = (int64_t)blockIdx.x * NT_ROWS; r0 < N; r0 += (int64_t)gridDim.x * NT_ROWS) {
     for (int fc = 0; fc < nf; fc += NT_FC) {
-      // read: thread t takes rows r0 + 4 (t % 8) .. + 3 of features fc + t / 8 + 32 i
+      // read: thread t takes rows r0 + 4 (t % CPF) .. + 3 of features fc + t / CPF + FPP i
+      constexpr int CPF = NT_ROWS / 4, FPP = 256 / CPF;
 #pragma unroll
-      for (int i = 0; i < NT_FC / 32; ++i) {
-        const int k = t / 8 + 32 * i, c = t % 8;
+      for (int i = 0; i < NT_FC / FPP; ++i) {
+        const int k = t / CPF + FPP * i, c = t % CPF;
         const int f = fc + k;
         const int64_t r = r0 + 4 * c;
         float v[4] = {0.f, 0.f, 0.f, 0.f};
