@@ -863,6 +863,8 @@ def create_app(client_disconnect_timeout: float | None = None):
 
     from .routes_more import register as _register_more
     _register_more(app, _params, _unquote, _model_json)
+    from .routes_v4 import register as _register_v4
+    _register_v4(app, _params)
 
     @app.get("/99/Leaderboards/{pid}")
     def leaderboard_get(pid: str):

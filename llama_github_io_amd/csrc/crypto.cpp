@@ -59,8 +59,10 @@ int h2o_pbe_md5_3des_decrypt(const unsigned char* salt8, int iters, const unsign
                              const unsigned char* in, long long inlen, unsigned char* out, long long* outlen) {
   unsigned char salt[8];
   memcpy(salt, salt8, 8);
-  if (memcmp(salt, salt + 4, 4) == 0) {          // identical halves: reverse the first one
-    for (int i = 0; i < 2; ++i) { const unsigned char t = salt[i]; salt[i] = salt[3 - i]; salt[3 - i] = t; }
+  if (memcmp(salt, salt + 4, 4) == 0) {
+    // identical halves: the JDK's PBES1Core means to reverse the first half but stores the swapped byte at index
+    // 3 - 1 on both turns, so [a, b, c, d] becomes [d, a, b, d]; keystores sealed by the JDK need the same bytes
+    for (int i = 0; i < 2; ++i) { const unsigned char t = salt[i]; salt[i] = salt[3 - i]; salt[3 - 1] = t; }
   }
   unsigned char derived[32];
   EVP_MD_CTX* md = EVP_MD_CTX_new();

@@ -60,6 +60,10 @@ def _expand(path) -> list:
         for p in path:
             out += _expand(p)
         return out
+    from . import persist_url
+    urls = persist_url.resolve(path)        # http(s):// -> fetched whole into the persist cache (PersistEagerHTTP)
+    if urls is not None:
+        return urls
     path = os.path.expanduser(str(path))
     if path.startswith("file://"):
         path = path[7:]

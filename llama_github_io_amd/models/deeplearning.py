@@ -637,7 +637,7 @@ class DeepLearningTrainer:
                 if not adaptive:
                     rs, ms = [], []
                     for k in range(CH):
-                        smp = samples0 + (k + 1) * B
+                        smp = samples0 + (k + 1) * Bg     # the global sample count, as the single-step path
                         rs.append(float(p["rate"]) / (1 + float(p["rate_annealing"]) * smp))
                         ms.append(self._momentum(smp))
                     rate_v.copy_(torch.tensor(rs, dtype=torch.float32))
@@ -763,8 +763,8 @@ class DeepLearningTrainer:
                     rows = perm[s_in * B:(s_in + 1) * B]
                 net.step = step
                 if not adaptive:
-                    m = self._momentum(samples + B)
-                    rate_t.fill_(float(p["rate"]) / (1 + float(p["rate_annealing"]) * (samples + B)))
+                    m = self._momentum(samples + Bg)
+                    rate_t.fill_(float(p["rate"]) / (1 + float(p["rate_annealing"]) * (samples + Bg)))
                     mom_t.fill_(m)
                     on_t.fill_(1.0 if m > 0 else 0.0)
                 if use_graph:
@@ -798,7 +798,12 @@ class DeepLearningTrainer:
             if it_end:
                 n_iter_done = samples // tspi
             timed = it_end and time.time() - last_score > float(p["score_interval"])
-            if sharded:                          # every rank must take the same scoring decision
+            # every rank must take the same scoring decision. The collective runs only at iteration ends: ranks
+            # may take different step paths (a graph chunk of CH steps vs single steps, from rank-local shard
+            # sizes / epoch boundaries / capture success), so the number of loop turns differs per rank, but a
+            # chunk never straddles an iteration end (spi is a multiple of CH), so every rank sees it_end at the
+            # same global step and issues the same sequence of collectives (agree, then dp_average)
+            if sharded and it_end:
                 timed = coll.agree(timed)
             step = last + 1
             if dp_avg and (it_end or end):

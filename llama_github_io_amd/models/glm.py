@@ -515,8 +515,12 @@ class GLMTrainer:
                                           op=_MIN)) if yy is not None else 0.0
         hi = float(coll.all_reduce_scalar(float(yy.max()) if yy is not None and yy.numel() else float("-inf"),
                                           op=_MAX)) if yy is not None else 0.0
-        if fam == "binomial" and ncls != 2 and not (ncls == 1 and lo >= 0 and hi <= 1 and
-                                                     bool(((yy == 0) | (yy == 1)).all())):
+        # Vec.isBinary is a property of the whole column: the local 0/1 test is reduced (MIN over the ranks) so
+        # that every rank raises, or none does, before the GLM collectives start
+        binary = 1.0
+        if fam == "binomial" and ncls == 1 and yy is not None:
+            binary = float(coll.all_reduce_scalar(1.0 if bool(((yy == 0) | (yy == 1)).all()) else 0.0, op=_MIN))
+        if fam == "binomial" and ncls != 2 and not (ncls == 1 and lo >= 0 and hi <= 1 and binary > 0.5):
             err("family", "Binomial requires the response to be a 2-class categorical or a binary column (0/1)")
         if fam in ("multinomial", "ordinal") and ncls <= 2:
             err("family", f"{fam.capitalize()} requires a categorical response with at least 3 levels (for 2 class "

@@ -72,6 +72,18 @@ def fit_hglm(trainer, X, y, w, off, info: DataInfo, model, p):
     rand_idx = _random_indices(info, p.get("random_columns") or [])
     if not rand_idx:
         raise ValueError("HGLM needs random_columns")
+    # GLMModel.GLMParameters.validate (hex/glm/GLMModel.java:534-548): one link per random column, identity only
+    rlink = p.get("rand_link")
+    if rlink not in (None, [], ()):
+        rlink = [rlink] if isinstance(rlink, str) else list(rlink)
+        if len(rlink) != len(rand_idx):
+            raise ValueError("HGLM _rand_link: must have the same length as random_columns.")
+        for lk in rlink:
+            if str(lk).lower().replace("_", "") not in ("identity", "familydefault"):
+                raise ValueError("HGLM only supports identity link functions for now.")
+    link = str(p.get("link") or "family_default").lower().replace("_", "")
+    if link not in ("identity", "familydefault"):
+        raise ValueError("HGLM only supports identity link functions for now.")
     fixed_idx = [j for j in range(info.F) if j not in rand_idx]
     finfo = DataInfo([info.x[j] for j in fixed_idx], np.asarray(info.iscat)[fixed_idx],
                      [info.domains[j] for j in fixed_idx], info.response, info.response_domain)

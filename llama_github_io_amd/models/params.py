@@ -33,9 +33,9 @@ HINTS = {
 }
 
 # parameters not implemented by this engine: a non-default value is refused
-UNSUPPORTED = {
-    "glm": {"rand_link"},
-}
+UNSUPPORTED: dict = {}
+# (GLM ``rand_link`` is validated where the reference validates it: HGLM accepts identity / family_default per random
+# column, hex/glm/GLMModel.java:534-548, see models/hglm.py)
 # (Infogram ``max_iterations`` is a schema field with no InfogramParameters counterpart in the reference
 # (hex/schemas/InfogramV3.java:82): accepted and, as there, without effect.)
 

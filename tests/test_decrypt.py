@@ -79,3 +79,43 @@ def test_rest_decryption_setup_and_parse():
     bad = c.post("/3/DecryptionSetup", json=dict(keystore_id=KS, key_alias="secretKeyAlias", password="x",
                                                  cipher_spec=SPEC))
     assert bad.status_code >= 400
+
+
+def _jdk_pbe_md5_3des_seal(salt: bytes, iters: int, password: str, plain: bytes) -> bytes:
+    """PBEWithMD5AndTripleDES encryption as com.sun.crypto.provider.PBES1Core does it, modelled in Python:
+    MD5 chains over each salt half, DESede/CBC with the derived IV, PKCS5 padding. Salts with identical halves go
+    through the JDK's swap loop that stores at index 3 - 1 ([a, b, c, d] -> [d, a, b, d])."""
+    import hashlib
+    from llama_github_io_amd.io.decrypt import cipher_encrypt
+    s = bytearray(salt)
+    if s[:4] == s[4:]:
+        for i in range(2):
+            t = s[i]
+            s[i] = s[3 - i]
+            s[3 - 1] = t
+    pw = bytes(ord(ch) & 0x7F for ch in password)
+    derived = b""
+    for h in range(2):
+        buf = bytes(s[4 * h:4 * h + 4])
+        for _ in range(iters):
+            buf = hashlib.md5(buf + pw).digest()
+        derived += buf
+    key, iv = derived[:24], derived[24:32]
+    n = 8 - len(plain) % 8
+    data = plain + bytes([n]) * n
+    out, prev = b"", iv
+    for i in range(0, len(data), 8):
+        blk = bytes(a ^ b for a, b in zip(data[i:i + 8], prev))
+        prev = cipher_encrypt("DESede/ECB/NoPadding", key, blk)
+        out += prev
+    return out
+
+
+@pytest.mark.parametrize("salt", [bytes([1, 2, 3, 4, 9, 8, 7, 6]), bytes([0x11, 0x22, 0x33, 0x44] * 2)])
+def test_pbe_unseal_matches_jdk_salt_handling(salt):
+    """JCEKS key sealing: random salts and the equal-halves case, where the JDK's PBES1Core turns the first half
+    [a, b, c, d] into [d, a, b, d] (not a reversal); keys it sealed must unseal bit-exactly."""
+    from llama_github_io_amd.io.decrypt import _pbe_unseal
+    plain = b"secret key material \x00\x01\x02 of 37 bytes!!"
+    sealed = _jdk_pbe_md5_3des_seal(salt, 20, "Password123", plain)
+    assert _pbe_unseal(salt, 20, "Password123", sealed) == plain

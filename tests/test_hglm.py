@@ -56,3 +56,21 @@ def test_hglm_requires_gaussian(data):
     with pytest.raises(Exception):
         H2OGeneralizedLinearEstimator(family="poisson", HGLM=True, random_columns=["grp"]).train(
             x=["x", "grp"], y="y", training_frame=fr)
+
+
+def test_hglm_rand_link_identity_accepted_others_refused(data):
+    """GLMModel.java:534-548: rand_link may name identity / family_default per random column (the same model as the
+    default); any other link, or a list of the wrong length, is refused with the reference's message."""
+    fr, _ = data
+    kw = dict(family="gaussian", HGLM=True, random_columns=["grp"], rand_family=["gaussian"], standardize=False)
+    a = H2OGeneralizedLinearEstimator(**kw)
+    a.train(x=["x", "grp"], y="y", training_frame=fr)
+    b = H2OGeneralizedLinearEstimator(rand_link=["identity"], **kw)
+    b.train(x=["x", "grp"], y="y", training_frame=fr)
+    assert b._model.output["coefficients"]["x"] == pytest.approx(a._model.output["coefficients"]["x"], rel=1e-12)
+    np.testing.assert_allclose(b._model.output["ubeta"], a._model.output["ubeta"], rtol=1e-12)
+    with pytest.raises(Exception, match="identity link"):
+        H2OGeneralizedLinearEstimator(rand_link=["log"], **kw).train(x=["x", "grp"], y="y", training_frame=fr)
+    with pytest.raises(Exception, match="same length"):
+        H2OGeneralizedLinearEstimator(rand_link=["identity", "identity"], **kw).train(x=["x", "grp"], y="y",
+                                                                                         training_frame=fr)

@@ -37,12 +37,11 @@ def test_unknown_parameter_raises(fr):
         builder.train("glm", dict(lamda=0.1), x=X, y="y", training_frame=fr)
 
 
-@pytest.mark.parametrize("algo,param,value", [
-    ("glm", "rand_link", ["identity"]),
-])
-def test_unsupported_parameter_raises(fr, algo, param, value):
-    with pytest.raises(ValueError, match="not supported"):
-        builder.train(algo, {param: value, "seed": 1}, x=X, y="y", training_frame=fr)
+def test_no_parameter_is_refused_any_more():
+    """Every h2o-py parameter is implemented: the UNSUPPORTED table is empty (GLM ``rand_link`` is validated by
+    HGLM as the reference does, tests/test_hglm.py)."""
+    from llama_github_io_amd.models.params import UNSUPPORTED
+    assert not any(UNSUPPORTED.values())
 
 
 def test_execution_hints_accepted(fr):
