@@ -48,7 +48,8 @@ def init(name: str | None = None, distributed: bool | None = None, backend: str 
         _state["name"] = name or os.environ.get("H2O_CLOUD_NAME", f"h2o_amd_{os.getpid()}")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if distributed is None:
-        distributed = world > 1
+        # (H2O_FORCE_SHARDED=1: a 1-rank group still forms, so the sharded paths run through its collectives)
+        distributed = world > 1 or (os.environ.get("H2O_FORCE_SHARDED") == "1" and "MASTER_ADDR" in os.environ)
     if distributed and not dist.is_initialized():
         if torch.cuda.is_available() and os.environ.get("H2O_AMD_DEVICE", "cuda") != "cpu":
             local = int(os.environ.get("LOCAL_RANK", "0"))

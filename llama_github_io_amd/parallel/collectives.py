@@ -24,9 +24,18 @@ _tls = threading.local()
 _stats = dict(calls=0, bytes=0, row_gathers=0)
 
 
+def forced_sharded() -> bool:
+    """``H2O_FORCE_SHARDED=1``: a process group of ONE rank counts as a cloud, so every trainer takes its
+    row-sharded path and its collectives run through the group's backend (ProcessGroupNCCL = RCCL on the
+    1-GPU box: device tensors, MIN/MAX on int64, object gathers, stream order) instead of being skipped."""
+    import os
+    return os.environ.get("H2O_FORCE_SHARDED") == "1"
+
+
 def world_active() -> bool:
-    """A process group of more than one rank exists (independent of the replicated context)."""
-    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    """A process group of more than one rank exists (independent of the replicated context), or one rank with
+    :func:`forced_sharded`."""
+    return dist.is_available() and dist.is_initialized() and (dist.get_world_size() > 1 or forced_sharded())
 
 
 def is_dist() -> bool:

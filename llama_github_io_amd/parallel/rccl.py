@@ -104,7 +104,8 @@ def native_comm(force: bool = False) -> NativeComm | None:
         return None
     world = dist.get_world_size() if have_pg else 1
     rank = dist.get_rank() if have_pg else 0
-    if world == 1 and not force:
+    from . import collectives as _coll
+    if world == 1 and not (force or _coll.forced_sharded()):
         return None
     key = (world, rank, torch.cuda.current_device(), id(dist.group.WORLD) if have_pg else 0)
     with _lock:

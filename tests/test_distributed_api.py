@@ -143,9 +143,10 @@ def _run_cases(csv, names, out_path):
                     for a, kw in (("gbm", dict(ntrees=3, max_depth=3)), ("glm", dict(family="binomial")))]
             pp["base_models"] = [b.key for b in base]
         import llama_github_io_amd.parallel.collectives as coll
-        g0 = coll.stats()["row_gathers"]
+        g0, c0 = coll.stats()["row_gathers"], coll.stats()["calls"]
         m = builder.train(algo, pp, x=x, y=y, training_frame=fr)
         res.setdefault("row_gathers", {})[name] = coll.stats()["row_gathers"] - g0
+        res.setdefault("calls", {})[name] = coll.stats()["calls"] - c0
         if algo == "quantile":
             q = m.output["quantiles"]
             res[name] = dict(pred=[q[c] for c in sorted(q)], metrics={}, cv={})
