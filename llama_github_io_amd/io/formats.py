@@ -387,8 +387,14 @@ def read_avro(buf: bytes):
         block = b.read(size)
         if codec == "deflate":
             block = zlib.decompress(block, -15)
+        elif codec == "snappy":
+            # Avro's snappy codec: a raw snappy block followed by the big-endian CRC-32 of the uncompressed bytes
+            raw = snappy_decompress(block[:-4])
+            if zlib.crc32(raw) & 0xFFFFFFFF != int.from_bytes(block[-4:], "big"):
+                raise ValueError("Avro snappy block CRC mismatch")
+            block = raw
         elif codec != "null":
-            raise NotImplementedError(f"Avro codec {codec} is not supported (null, deflate)")
+            raise NotImplementedError(f"Avro codec {codec} is not supported (null, deflate, snappy)")
         bb = io.BytesIO(block)
         nm = {}
         for _ in range(count):
@@ -396,6 +402,58 @@ def read_avro(buf: bytes):
         if b.read(16) != sync:
             raise ValueError("Avro sync marker mismatch")
     return [names] + rows
+
+
+def snappy_decompress(buf: bytes) -> bytes:
+    """Raw snappy format (the framing-free block format): a varint of the uncompressed length, then literal and
+    back-reference (copy) elements. Decoded in pure Python: Avro blocks are small."""
+    n, shift, i = 0, 0, 0
+    while True:
+        c = buf[i]
+        i += 1
+        n |= (c & 0x7F) << shift
+        if c < 0x80:
+            break
+        shift += 7
+    out = bytearray()
+    L = len(buf)
+    while i < L:
+        tag = buf[i]
+        i += 1
+        t = tag & 3
+        if t == 0:                                   # literal
+            ln = tag >> 2
+            if ln >= 60:
+                nb = ln - 59
+                ln = int.from_bytes(buf[i:i + nb], "little")
+                i += nb
+            ln += 1
+            out += buf[i:i + ln]
+            i += ln
+            continue
+        if t == 1:                                   # copy, 1-byte offset
+            ln = 4 + ((tag >> 2) & 7)
+            off = ((tag >> 5) << 8) | buf[i]
+            i += 1
+        elif t == 2:                                 # copy, 2-byte offset
+            ln = 1 + (tag >> 2)
+            off = int.from_bytes(buf[i:i + 2], "little")
+            i += 2
+        else:                                        # copy, 4-byte offset
+            ln = 1 + (tag >> 2)
+            off = int.from_bytes(buf[i:i + 4], "little")
+            i += 4
+        if off <= 0 or off > len(out):
+            raise ValueError("corrupt snappy data (bad copy offset)")
+        st = len(out) - off
+        if off >= ln:
+            out += out[st:st + ln]
+        else:                                        # overlapping copy: byte by byte
+            for k in range(ln):
+                out.append(out[st + k])
+    if len(out) != n:
+        raise ValueError(f"corrupt snappy data (length {len(out)} != {n})")
+    return bytes(out)
 
 
 # ================================================================================================ frame

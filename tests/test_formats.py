@@ -124,7 +124,13 @@ def _avro_bytes(codec="deflate"):
         recs += struct.pack("<d", x) + _zzenc(len(s)) + s.encode()
         recs += _zzenc(0) if f is None else _zzenc(1) + _zzenc(f)
         recs += _zzenc(c)
-    block = zlib.compress(recs)[2:-4] if codec == "deflate" else recs
+    if codec == "deflate":
+        block = zlib.compress(recs)[2:-4]
+    elif codec == "snappy":      # raw snappy (pyarrow's codec as the independent encoder) + big-endian CRC-32
+        import pyarrow as pa
+        block = pa.compress(recs, codec="snappy", asbytes=True) + (zlib.crc32(recs) & 0xFFFFFFFF).to_bytes(4, "big")
+    else:
+        block = recs
     sync = bytes(range(16))
     meta = {"avro.schema": json.dumps(schema).encode(), "avro.codec": codec.encode()}
     out = b"Obj\x01" + _zzenc(len(meta))
@@ -151,7 +157,7 @@ def test_spreadsheets(tmp_path, kind):
     _check(h2o.import_file(str(p)))
 
 
-@pytest.mark.parametrize("codec", ["null", "deflate"])
+@pytest.mark.parametrize("codec", ["null", "deflate", "snappy"])
 def test_avro(tmp_path, codec):
     h2o.init(verbose=False)
     p = tmp_path / "t.avro"
@@ -170,3 +176,14 @@ def test_orc_roundtrip(tmp_path):
     po.write_table(pa.Table.from_pandas(pd.DataFrame({"x": [1.5, 2.0], "name": ["a", "b"]})), str(p))
     df = h2o.import_file(str(p)).as_data_frame()
     assert list(df["x"]) == [1.5, 2.0]
+
+
+def test_snappy_decoder_matches_pyarrow():
+    """The pure-Python raw snappy decoder (Avro snappy blocks) against pyarrow's encoder: literals of every length
+    class, overlapping and far back-references."""
+    import pyarrow as pa
+    from llama_github_io_amd.io.formats import snappy_decompress
+    rng = np.random.default_rng(0)
+    for data in (b"", b"a", b"abcabcabcabcabcabcabc" * 50, bytes(rng.integers(0, 256, 70000, dtype=np.uint8)),
+                 (b"x" * 1000 + bytes(rng.integers(0, 4, 5000, dtype=np.uint8))) * 20):
+        assert snappy_decompress(pa.compress(data, codec="snappy", asbytes=True)) == data
