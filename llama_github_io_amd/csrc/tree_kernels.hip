@@ -155,18 +155,20 @@ __device__ __forceinline__ long long q64(float v, float scale) {
   return (long long)(v * scale);   // |v*scale| <= 2^40: exact conversion of the fp32 product
 }
 
-// PACKED mode (row weights are small integers, e.g. 1 or a 0/1 sample mask): ONE ds_add_u64 per
-// (row, feature) instead of two — count in bits [48, 64), wY in the low 48 bits as signed fixed point
-// scaled to |q| <= 2^30 per row (one v_cvt_i32_f32 per row). A flush window holds < 2^15 rows (PACK_MAX), so the signed low
-// part never exceeds 2^46 and the count never carries out: decode with one arithmetic shift.
+// PACKED mode (row weights are 0 / 1: unit weights or a sample mask): ONE ds_add_u64 per (row, feature) instead of
+// two — count in bits [48, 64) as an UNSIGNED 16-bit field, wY in the low 48 bits as signed fixed point scaled to
+// |q| <= 2^30 per row (one v_cvt_i32_f32 per row). A flush window holds < 2^16 rows (PACK_MAX), so the signed low part
+// stays inside +-2^46 and the count never carries out: decode with one logical shift of the biased value.
+// (r5: the window was 15 tiles with a signed count field, so a root block of 11M / 256 = 43K rows flushed twice, the
+// second flush reading its partial slot back; 31 tiles keep one flush per block at that size)
 #define PACK_SHIFT 48
-#define PACK_MAX 30720   // rows per LDS flush window in packed mode (15 tiles)
+#define PACK_MAX 63488   // rows per LDS flush window in packed mode (31 tiles)
 __device__ __forceinline__ long long qpack(float w, float b, float scale_p) {
   return ((long long)__float2int_rz(w) << PACK_SHIFT) + (long long)__float2int_rz(b * scale_p);
 }
 __device__ __forceinline__ void unpack(long long v, long long& cnt, long long& val) {
-  cnt = (v + (1ll << (PACK_SHIFT - 1))) >> PACK_SHIFT;
-  val = v - (cnt << PACK_SHIFT);
+  cnt = (long long)(((unsigned long long)v + (1ull << (PACK_SHIFT - 1))) >> PACK_SHIFT);
+  val = (long long)((unsigned long long)v - ((unsigned long long)cnt << PACK_SHIFT));
 }
 
 // Flush of one block's LDS histogram into ITS OWN partial slot (plain stores, no global atomics):
@@ -192,8 +194,12 @@ __device__ void flush_partial(const long long* h, const float* nayy, double node
   const int f0 = ftile * FTILE;
   const int nf = min(FTILE, F - f0);
   const double inv_a = qs[2], inv_b = qs[3], inv_p = qs[5];
-  for (int i = threadIdx.x; i < nf * 2 * NBIN; i += blockDim.x) {
-    const int bin = i / (2 * nf), rem = i - bin * 2 * nf, fl = rem >> 1, r = rem & 1;
+  // (bin, rem) of entry i advanced incrementally: no integer division per entry
+  const int row2 = 2 * nf, dbin = (int)blockDim.x / row2, drem = (int)blockDim.x - dbin * row2;
+  int bin = (int)threadIdx.x / row2, rem = (int)threadIdx.x - bin * row2;
+  for (int i = threadIdx.x; i < nf * 2 * NBIN; i += blockDim.x, bin += dbin, rem += drem) {
+    if (rem >= row2) { rem -= row2; ++bin; }
+    const int fl = rem >> 1, r = rem & 1;
     const int reps = srep[fl], nb = snb[fl];
     long long q = 0;                       // the entry's fixed-point value (plane r), replicas summed
     if (sfine[fl]) {
@@ -364,7 +370,7 @@ __device__ __forceinline__ HistSrc make_src(const unsigned* bins32, const float*
 // property of the bins) drops the per-word NA test at compile time; a batch wholly inside the node skips the
 // per-row bounds tests; BUF addresses with 32-bit offsets. The common row is then bfe + lshl_add + ds_add_u64
 // per feature (two atomics when not PACKED).
-template <bool FILT, bool PACKED, bool UNIT, bool NONA, bool BUF, int GR = RPI, int UNR = H2O_UNR>
+template <bool FILT, bool PACKED, bool UNIT, bool NONA, bool BUF, bool FINE, int GR = RPI, int UNR = H2O_UNR>
 __device__ __forceinline__ void hist_rows(long long* h, float* nayy, const HistSrc& src, int W, int wabs,
                                           int F, bool lead, int r0, int r1, int g, int j, float& wyy, float sa,
                                           float sb, float sp, const int* lst, const int* srep, const int* snb,
@@ -388,7 +394,7 @@ __device__ __forceinline__ void hist_rows(long long* h, float* nayy, const HistS
   // FINE word: the 4 bytes are the 4 interleaved engine columns of ONE wide numeric feature (ops/binning.py), so
   // their byte sum is the fine bin t = #{edges <= x} (NA: 4 x 255 = 1020) and one atomic into fine entry
   // (bin t >> 2, column t & 3) replaces four; the flush rebuilds the four column histograms from the fine one
-  const bool fine = live && sfine[j * 4] != 0;
+  const bool fine = FINE && live && sfine[j * 4] != 0;
   unsigned fsl[4];
 #pragma unroll
   for (int l = 0; l < 4; ++l) fsl[l] = (unsigned)fslot(j * 4 + l) * 8u;
@@ -450,7 +456,7 @@ __device__ __forceinline__ void hist_rows(long long* h, float* nayy, const HistS
                                 : PACKED ? qpack(ab[u].x, ab[u].y, sp) : q64(ab[u].x, sa);
       const long long qb = PACKED ? 0ll : q64(ab[u].y, sb);
       const unsigned w = wd[u];
-      if (fine) {
+      if (FINE && fine) {
         const unsigned t = __builtin_amdgcn_sad_u8(w, 0u, 0u);          // sum of the 4 bytes
         const unsigned l = t & 3u;
         const unsigned so = (l & 2u) ? ((l & 1u) ? fsl[3] : fsl[2]) : ((l & 1u) ? fsl[1] : fsl[0]);
@@ -487,13 +493,238 @@ __device__ __forceinline__ void hist_rows(long long* h, float* nayy, const HistS
   }
 }
 
+// Plain (non-FILT) histogram of node rows [r0, r1) — one contiguous run of a node inside the block's tile range (a
+// whole window, not a tile): the per-lane setup runs once per run, and the loads of batch k + 1 are issued before the
+// atomics of batch k (double-buffered registers), so the wave's next rows are in flight while it feeds the LDS.
+// MEASURED (r5, scripts/mb_hist4.hip, 11M x 28): the pure LDS atomic rate is 8 cycles per ds_add_u64 wave-instruction
+// per CU (63 us for 308M updates) and the loads alone stream at ~6 TB/s (68 us); the per-tile loop with a per-row
+// fine / live branch reached only 135 us.
+template <bool PACKED, bool UNIT, bool NONA, bool BUF, bool FINE>
+__device__ __forceinline__ void hist_span(long long* h, float* nayy, const HistSrc& src, int W, int wabs, int F,
+                                          bool lead, int r0, int r1, int g, int j, float& wyy, float sa, float sb,
+                                          float sp, const int* srep, const int* snb, const int* sfine,
+                                          bool no_atoms = false) {
+  constexpr int GR = RPI, UNR = H2O_UNR;
+  const int rot = g & 1;
+  unsigned offb[4], sh[4];
+  unsigned vmask = 0u;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int kk = (k + rot) & 3;
+    const int fl = j * 4 + kk;
+    const int c = (g >> 1) & (srep[fl] - 1);
+    offb[k] = (unsigned)fslot(fl) * 8u + ((unsigned)(c * snb[fl]) << 8);
+    sh[k] = 8u * kk;
+    if (wabs < W && wabs * 4 + kk < F) vmask |= 0xFFu << (8 * kk);
+  }
+  const bool live = vmask != 0u && !no_atoms;
+  const bool fine = FINE && live && sfine[j * 4] != 0;
+  unsigned fsl[4];
+#pragma unroll
+  for (int l = 0; l < 4; ++l) fsl[l] = (unsigned)fslot(j * 4 + l) * 8u;
+  const int wc = min(wabs, W - 1);
+  const bool weighted = !UNIT && src.aw != nullptr;
+  char* Hb = (char*)h;
+  auto load = [&](int base, unsigned (&wd)[UNR], float2 (&ab)[UNR]) {
+    if (BUF && base + GR * UNR <= r1) {
+      const unsigned row0 = (unsigned)(base + g);
+      const unsigned vb = (row0 << src.lgw) + (unsigned)wc * 4u, va = row0 * 4u;
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        wd[u] = __builtin_amdgcn_raw_buffer_load_b32(src.rb, vb, (unsigned)(u * GR) << src.lgw, 0);
+        const float y = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(src.ra, va, u * GR * 4, 0));
+        const float w = weighted ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(src.rw, va, u * GR * 4, 0))
+                                 : 1.f;
+        ab[u] = make_float2(w, y);
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const int row = min(base + g + u * GR, r1 - 1);
+        if (BUF) {
+          const unsigned ro = (unsigned)row;
+          wd[u] = __builtin_amdgcn_raw_buffer_load_b32(src.rb, (ro << src.lgw) + (unsigned)wc * 4u, 0, 0);
+          const float y = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(src.ra, ro * 4u, 0, 0));
+          const float w = weighted ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(src.rw, ro * 4u, 0, 0)) : 1.f;
+          ab[u] = make_float2(w, y);
+        } else {
+          ab[u] = make_float2(weighted ? src.aw[row] : 1.f, src.ay[row]);
+          wd[u] = src.bins32[(size_t)row * W + wc];
+        }
+      }
+    }
+  };
+  unsigned wdn[UNR];
+  float2 abn[UNR];
+  if (r0 < r1) load(r0, wdn, abn);
+  for (int base = r0; base < r1; base += GR * UNR) {
+    unsigned wd[UNR];
+    float2 ab[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) { wd[u] = wdn[u]; ab[u] = abn[u]; }
+    if (base + GR * UNR < r1) load(base + GR * UNR, wdn, abn);
+    auto atoms = [&](int u) {
+      const long long qa = UNIT ? (1ll << PACK_SHIFT) + (long long)(int)(ab[u].y * sp)
+                                : PACKED ? qpack(ab[u].x, ab[u].y, sp) : q64(ab[u].x, sa);
+      const long long qb = PACKED ? 0ll : q64(ab[u].y, sb);
+      const unsigned w = wd[u];
+      if (FINE && fine) {
+        const unsigned t = __builtin_amdgcn_sad_u8(w, 0u, 0u);
+        const unsigned l = t & 3u;
+        const unsigned so = (l & 2u) ? ((l & 1u) ? fsl[3] : fsl[2]) : ((l & 1u) ? fsl[1] : fsl[0]);
+        unsigned long long* p = (unsigned long long*)(Hb + (((t >> 2) << 8) + so));
+        atomicAdd(p, (unsigned long long)qa);
+        if (!PACKED) atomicAdd(p + HPLANE, (unsigned long long)qb);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          unsigned long long* p = (unsigned long long*)(Hb + ((__builtin_amdgcn_ubfe(w, sh[k], 8) << 8) + offb[k]));
+          atomicAdd(p, (unsigned long long)qa);
+          if (!PACKED) atomicAdd(p + HPLANE, (unsigned long long)qb);
+        }
+      }
+    };
+    auto row = [&](int u) {
+      if (lead) wyy += UNIT ? ab[u].y * ab[u].y : row_yy(ab[u].x, ab[u].y);
+      if (FINE && live) atoms(u);
+      if (!NONA) {
+        const unsigned w = wd[u];
+        const unsigned x = ~w | ~vmask;
+        if (((x - 0x01010101u) & ~x & 0x80808080u) != 0u) {
+          const float yy = UNIT ? ab[u].y * ab[u].y : row_yy(ab[u].x, ab[u].y);
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (((vmask >> sh[k]) & 1u) && __builtin_amdgcn_ubfe(w, sh[k], 8) == NA_BIN)
+              atomicAdd(nayy + j * 4 + (sh[k] >> 3), yy);
+        }
+      }
+    };
+    // !FINE: the lane's live test (a lane whose word holds no feature of the tile issues no atomics) is ONE exec-mask
+    // branch around the batch's atomics, not one per row
+    if (base + GR * UNR <= r1) {
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) row(u);
+      if (!FINE && live) {
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) atoms(u);
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < UNR; ++u)
+        if (base + g + u * GR < r1) row(u);
+      if (!FINE && live) {
+#pragma unroll
+        for (int u = 0; u < UNR; ++u)
+          if (base + g + u * GR < r1) atoms(u);
+      }
+    }
+  }
+}
+
+// FILT (odd levels), software-pipelined: a wave gathers the rows of its NEXT 64-row queue batch (one row per 8-lane
+// group and step, UNR = 8 steps) and only then issues the atomics of the batch gathered before, so the gathers' latency
+// hides behind that batch's atomics. MEASURED (r5 PMC, 11M HIGGS): the unpipelined filtered pass spent 55 % of its
+// wave cycles waiting on memory (SQ_WAIT_ANY), each batch's gathers exposed in full.
+struct FiltLane {   // per-lane setup of a FILT kernel (constant per block: feature tile and lane group fixed)
+  unsigned offb[4];  // byte offset of the slot of byte k of the ROTATED word (see filt_atoms)
+  unsigned vmask;    // valid features of the lane's word, in the original byte order
+  int wc, rot;
+  bool live, fine, weighted, lead;
+};
+
+template <bool PACKED, bool UNIT, bool FINE>
+__device__ __forceinline__ FiltLane filt_lane(const HistSrc& src, int W, int wabs, int F, int g8, int j, bool lead,
+                                              const int* srep, const int* snb, const int* sfine) {
+  FiltLane L;
+  L.rot = g8 & 1;
+  L.vmask = 0u;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int kk = (k + L.rot) & 3;
+    const int fl = j * 4 + kk;
+    const int c = (g8 >> 1) & (srep[fl] - 1);
+    L.offb[k] = (unsigned)fslot(fl) * 8u + ((unsigned)(c * snb[fl]) << 8);
+    if (wabs < W && wabs * 4 + kk < F) L.vmask |= 0xFFu << (8 * kk);
+  }
+  L.live = L.vmask != 0u;
+  L.fine = FINE && L.live && sfine[j * 4] != 0;
+  L.wc = min(wabs, W - 1);
+  L.weighted = !UNIT && src.aw != nullptr;
+  L.lead = lead;
+  return L;
+}
+
+// gather the queued rows wq[0, n) (entry g8 + 8u per step; entries past n load row wq[n - 1], unused)
+template <bool UNIT, bool BUF>
+__device__ __forceinline__ void filt_gather(const FiltLane& L, const HistSrc& src, int W, const int* wq, int n, int g8,
+                                            unsigned (&wd)[8], float (&yv)[8], float (&wv)[8]) {
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int row = wq[min(g8 + 8 * u, n - 1)];
+    if (BUF) {
+      const unsigned ro = (unsigned)row;
+      wd[u] = __builtin_amdgcn_raw_buffer_load_b32(src.rb, (ro << src.lgw) + (unsigned)L.wc * 4u, 0, 0);
+      yv[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(src.ra, ro * 4u, 0, 0));
+      if (!UNIT) wv[u] = L.weighted ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(src.rw, ro * 4u, 0, 0)) : 1.f;
+    } else {
+      yv[u] = src.ay[row];
+      if (!UNIT) wv[u] = L.weighted ? src.aw[row] : 1.f;
+      wd[u] = src.bins32[(size_t)row * W + L.wc];
+    }
+  }
+}
+
+// the atomics (and NA / yy tallies) of a gathered batch of n rows. The word is rotated by the lane group's parity
+// (byte k of the rotated word = feature 4j + ((k + rot) & 3), one v_alignbyte per row) so the byte extracts use
+// constant shifts; same-parity rows of a 16-lane group then add distinct features (bank-conflict-free layout).
+template <bool PACKED, bool UNIT, bool NONA, bool FINE>
+__device__ __forceinline__ void filt_atoms(const FiltLane& L, long long* h, float* nayy, int n, int g8, int j,
+                                           const unsigned (&wd)[8], const float (&yv)[8], const float (&wv)[8],
+                                           float& wyy, float sa, float sb, float sp) {
+  char* Hb = (char*)h;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    if (g8 + 8 * u >= n) continue;
+    const float x = UNIT ? 1.f : wv[u];
+    if (L.lead) wyy += UNIT ? yv[u] * yv[u] : row_yy(x, yv[u]);
+    const long long qa = UNIT ? (1ll << PACK_SHIFT) + (long long)(int)(yv[u] * sp)
+                              : PACKED ? qpack(x, yv[u], sp) : q64(x, sa);
+    const long long qb = PACKED ? 0ll : q64(yv[u], sb);
+    const unsigned w = wd[u];
+    if (FINE && L.fine) {
+      const unsigned t = __builtin_amdgcn_sad_u8(w, 0u, 0u);
+      const unsigned l = t & 3u;
+      unsigned long long* p = (unsigned long long*)(Hb + (((t >> 2) << 8) + (unsigned)fslot(j * 4 + (int)l) * 8u));
+      atomicAdd(p, (unsigned long long)qa);
+      if (!PACKED) atomicAdd(p + HPLANE, (unsigned long long)qb);
+    } else if (L.live) {
+      const unsigned wr = __builtin_amdgcn_alignbyte(w, w, L.rot);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        unsigned long long* p = (unsigned long long*)(Hb + ((__builtin_amdgcn_ubfe(wr, 8 * k, 8) << 8) + L.offb[k]));
+        atomicAdd(p, (unsigned long long)qa);
+        if (!PACKED) atomicAdd(p + HPLANE, (unsigned long long)qb);
+      }
+    }
+    if (!NONA) {
+      const unsigned xx = ~w | ~L.vmask;
+      if (((xx - 0x01010101u) & ~xx & 0x80808080u) != 0u) {
+        const float yy = UNIT ? yv[u] * yv[u] : row_yy(x, yv[u]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (((L.vmask >> (8 * k)) & 1u) && __builtin_amdgcn_ubfe(w, 8 * k, 8) == NA_BIN) atomicAdd(nayy + j * 4 + k, yy);
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // k_hist_build: histograms of all nodes with build==1 of a level, as per-block PARTIAL slots
 // (partials + (blockIdx.x + node) * slot_doubles); k_hist_reduce sums them per node in a fixed order
 // (deterministic, no global atomics). grid = (G, n_ftiles); each block takes a contiguous tile range.
 // FILT (odd levels): a node's tiles cover its PARENT's rows; only rows the parent's decision sends to
 // this child are accumulated, and ftile-0 blocks add the parent's left-going row count to nl_out.
-template <bool FILT, bool PACKED, bool UNIT, bool NONA, bool BUF>
+template <bool FILT, bool PACKED, bool UNIT, bool NONA, bool BUF, bool FINE>
 __global__ __launch_bounds__(BLK) void k_hist_build(
     const uint8_t* __restrict__ bins, int stride /*bytes per row, multiple of 4*/,
     const float* __restrict__ aw /*row weights or null (unit)*/, const float* __restrict__ ay /*w * Y*/,
@@ -503,7 +734,8 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
     const Dec* __restrict__ pdec, int* __restrict__ nl_out, int f32, long long N, int planar, int lgw,
     const int* __restrict__ nbins_f /*[F] (NONA: low-cardinality spreading) or null*/,
     const int* __restrict__ fine_f /*[F] 1 = column of an aligned 4-column wide numeric group, or null*/,
-    const uint8_t* __restrict__ fdir /*FILT: per row 0 = left / 1 = right of the parent split, or null*/) {
+    const uint8_t* __restrict__ fdir /*FILT: per row 0 = left / 1 = right of the parent split, or null*/,
+    int dbg /*A/B diagnostics (H2O_HIST_DBG): bit 0 skips the partial flush, bit 1 the plain pass's atomics*/) {
   constexpr bool packed = PACKED;
   extern __shared__ __attribute__((aligned(16))) long long smem64[];
   long long* h = smem64;                                 // 2 planes (PACKED: 1 -> two blocks per CU fit)
@@ -547,25 +779,39 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
   RowFilter flt{&spd, bins, stride, 0, -1, 0, 0, 0, 0, false};
   int lcnt = 0;
   int cur = -1, since = 0, cur_parent = -1;
-  unsigned pre[FNP];                 // FILT: prefetched split bytes of tile pre_t
-  int pre_t = -1;
+  unsigned pre[FNP], pre2[FNP];      // FILT: prefetched split bytes of tiles pre_t and pre2_t
+  int pre_t = -1, pre2_t = -1;
   int qn = 0;                        // FILT: rows in this wave's queue (wave-uniform)
   bool acc = false;
   double wyy = 0.0;
   // FILT: histogram the wave's queued rows of the current node (before its LDS histogram is flushed)
+  // FILT pipeline state: the batch gathered last (its atomics not yet issued)
+  const FiltLane FL = filt_lane<PACKED, UNIT, FINE>(src, W, wabs, Fl, lane >> 3, j, j == 0 && ftile == 0, srep, snb,
+                                                    sfine);
+  unsigned wdP[8];
+  float yP[8], wP[8];
+  int np = 0;                        // rows of the pending batch (0: none)
   auto drain = [&]() {
-    if (FILT && qn > 0) {
-      float wf2 = 0.f;
+    if (!FILT) return;
+    float wf2 = 0.f;
+    if (qn > 0) {
+      unsigned wdN[8];
+      float yN[8], wN[8];
       wave_sync_lds();
-      hist_rows<FILT, PACKED, UNIT, NONA, BUF, 8, 8>(h, nayy, src, W, wabs, Fl, j == 0 && ftile == 0, 0, qn, lane >> 3, j,
-                                                     wf2, sa, sb, sp, wq, srep, snb, sfine);
-      wyy += (double)wf2;
+      filt_gather<UNIT, BUF>(FL, src, W, wq, qn, lane >> 3, wdN, yN, wN);
+      if (np > 0) filt_atoms<PACKED, UNIT, NONA, FINE>(FL, h, nayy, np, lane >> 3, j, wdP, yP, wP, wf2, sa, sb, sp);
+      filt_atoms<PACKED, UNIT, NONA, FINE>(FL, h, nayy, qn, lane >> 3, j, wdN, yN, wN, wf2, sa, sb, sp);
       qn = 0;
       wave_sync_lds();
+    } else if (np > 0) {
+      filt_atoms<PACKED, UNIT, NONA, FINE>(FL, h, nayy, np, lane >> 3, j, wdP, yP, wP, wf2, sa, sb, sp);
     }
+    np = 0;
+    wyy += (double)wf2;
   };
   auto flush = [&]() {
     drain();
+    if (dbg & 1) return;
     double v[4] = {wyy, (double)lcnt, 0, 0};
     block_sum4(v, red);
     __syncthreads();
@@ -575,7 +821,43 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
     if (FILT && threadIdx.x == 0 && v[1] != 0.0) atomicAdd(nl_out + cur_parent, (int)v[1]);
     __syncthreads();
   };
-  for (int t = t0; t < t1; ++t) {
+  if (!FILT) {
+    // plain levels: the block's tiles are runs of whole node ranges — one hist_span per (node, packed window), no
+    // per-tile node lookup or per-tile lane setup
+    int t = t0;
+    while (t < t1) {
+      const int node = find_node(tile_prefix, n_nodes, t);
+      const Node nd = nodes[node];
+      const int tn0 = tile_prefix[node];
+      const int te = max(t + 1, min(t1, tile_prefix[node + 1]));
+      int rs = nd.start + (t - tn0) * TILE;
+      const int re = min(nd.start + nd.len, nd.start + (te - tn0) * TILE);
+      t = te;
+      if (!nd.build) continue;
+      while (rs < re) {
+        if (node != cur || (packed && since >= PACK_MAX)) {
+          if (cur >= 0) flush();
+          acc = node == cur;
+          lds_zero64(h, packed ? HPLANE : 2 * HPLANE);
+          for (int i = threadIdx.x; i < FTILE; i += blockDim.x) nayy[i] = 0.f;
+          wyy = 0.0;
+          lcnt = 0;
+          since = 0;
+          cur = node;
+          cur_parent = nd.parent;
+          __syncthreads();
+        }
+        const int we = packed ? min(re, rs + (PACK_MAX - since)) : re;
+        float wf = 0.f;
+        hist_span<PACKED, UNIT, NONA, BUF, FINE>(h, nayy, src, W, wabs, Fl, j == 0 && ftile == 0, rs, we, g, j, wf, sa,
+                                                 sb, sp, srep, snb, sfine, (dbg & 2) != 0);
+        wyy += (double)wf;
+        since += we - rs;
+        rs = we;
+      }
+    }
+  }
+  for (int t = FILT ? t0 : t1; t < t1; ++t) {
     const int node = find_node(tile_prefix, n_nodes, t);
     const Node nd = nodes[node];
     if (!nd.build) continue;
@@ -613,32 +895,49 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
     if (FILT) {
       // the split bytes of this tile were prefetched during the previous tile's atomics when both tiles
       // belong to the same node (the common case); a node change loads them here
+      // split bytes are prefetched TWO tiles ahead (same node: same filter): the direction loads are this pass's HBM
+      // stream (every line of the parent's rows), so a wave keeps two tiles of them in flight behind its atomics
       if (pre_t != t) filt_load(flt, r0, r1, pre);
-      qn = filt_append(flt, r0, r1, wq, qn, lcnt, pre);
-      // prefetch the next tile's split bytes (same node: same filter) so their latency hides behind the atomics
-      const int rn0 = r0 + TILE, nend = nd.start + nd.len;
-      if (t + 1 < t1 && rn0 < nend) {
-        filt_load(flt, rn0, min(rn0 + TILE, nend), pre);
+      unsigned curb[FNP];
+#pragma unroll
+      for (int k = 0; k < FNP; ++k) curb[k] = pre[k];
+      const int nend = nd.start + nd.len;
+      const int rn1 = r0 + TILE, rn2 = r0 + 2 * TILE;
+      if (pre2_t == t + 1) {
+#pragma unroll
+        for (int k = 0; k < FNP; ++k) pre[k] = pre2[k];
+        pre_t = t + 1;
+      } else if (t + 1 < t1 && rn1 < nend) {
+        filt_load(flt, rn1, min(rn1 + TILE, nend), pre);
         pre_t = t + 1;
       } else {
         pre_t = -1;
       }
+      if (t + 2 < t1 && rn2 < nend) {
+        filt_load(flt, rn2, min(rn2 + TILE, nend), pre2);
+        pre2_t = t + 2;
+      } else {
+        pre2_t = -1;
+      }
+      qn = filt_append(flt, r0, r1, wq, qn, lcnt, curb);
       // full 64-row batches of the wave's queue (8 lane groups x UNR rows); the rest waits for the next tile
       // of this node (or the drain before the flush)
       while (qn >= 64) {
+        unsigned wdN[8];
+        float yN[8], wN[8];
         wave_sync_lds();
-        hist_rows<FILT, PACKED, UNIT, NONA, BUF, 8, 8>(h, nayy, src, W, wabs, Fl, j == 0 && ftile == 0, 0, 64, lane >> 3, j,
-                                                       wf, sa, sb, sp, wq, srep, snb, sfine);
+        filt_gather<UNIT, BUF>(FL, src, W, wq, 64, lane >> 3, wdN, yN, wN);   // the next batch's loads go out first
         const int rest = qn - 64;                        // <= 127: move to the queue front (no lane overlap)
         wave_sync_lds();
         const int v0 = lane < rest ? wq[64 + lane] : 0, v1 = lane + 64 < rest ? wq[128 + lane] : 0;
         if (lane < rest) wq[lane] = v0;
         if (lane + 64 < rest) wq[64 + lane] = v1;
         qn = rest;
+        if (np > 0) filt_atoms<PACKED, UNIT, NONA, FINE>(FL, h, nayy, np, lane >> 3, j, wdP, yP, wP, wf, sa, sb, sp);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) { wdP[u] = wdN[u]; yP[u] = yN[u]; wP[u] = wN[u]; }
+        np = 64;
       }
-    } else {
-      hist_rows<FILT, PACKED, UNIT, NONA, BUF>(h, nayy, src, W, wabs, Fl, j == 0 && ftile == 0, r0, r1, g, j, wf, sa, sb,
-                                               sp, nullptr, srep, snb, sfine);
     }
     wyy += (double)wf;
   }
@@ -1934,15 +2233,26 @@ __global__ void k_leaf_values(const double* __restrict__ leafsum, int n, int log
 
 // ================================================================================================
 // C ABI launchers (called through ctypes with raw device pointers and the current HIP stream).
+static int hist_dbg() {   // H2O_HIST_DBG: diagnostics of the histogram pass (A/B timing only; never in a real run)
+  const char* e = getenv("H2O_HIST_DBG");
+  return e ? atoi(e) : 0;
+}
+
 template <bool FILT, bool PACKED, bool UNIT, bool NONA, bool BUF>
 static void launch_hist4(dim3 grid, size_t lds, hipStream_t s, const void* bins, int stride, const void* aw,
                          const void* ay, const void* nodes, const void* tile_prefix, const void* meta, int F,
                          void* partials, int slot_doubles, const void* qs, const void* pdec, void* nl_out, int f32,
                          long long N, int planar, int lgw, const void* nbins_f, const void* fine_f, const void* fdir) {
-  hipLaunchKernelGGL((k_hist_build<FILT, PACKED, UNIT, NONA, BUF>), grid, dim3(BLK), lds, s, (const uint8_t*)bins,
-                     stride, (const float*)aw, (const float*)ay, (const Node*)nodes, (const int*)tile_prefix,
-                     (const int*)meta, F, (double*)partials, slot_doubles, (const double*)qs, (const Dec*)pdec,
-                     (int*)nl_out, f32, N, planar, lgw, (const int*)nbins_f, (const int*)fine_f, (const uint8_t*)fdir);
+#define H2O_HB(FINE_)                                                                                              \
+  hipLaunchKernelGGL((k_hist_build<FILT, PACKED, UNIT, NONA, BUF, FINE_>), grid, dim3(BLK), lds, s,               \
+                     (const uint8_t*)bins, stride, (const float*)aw, (const float*)ay, (const Node*)nodes,         \
+                     (const int*)tile_prefix, (const int*)meta, F, (double*)partials, slot_doubles, (const double*)qs, \
+                     (const Dec*)pdec, (int*)nl_out, f32, N, planar, lgw, (const int*)nbins_f, (const int*)fine_f,  \
+                     (const uint8_t*)fdir, hist_dbg())
+  // FINE (fine-bin atomics of aligned 4-column wide groups, off by default): a separate instantiation, so the common
+  // kernels carry no per-row fine / live branch
+  if (fine_f) H2O_HB(true); else H2O_HB(false);
+#undef H2O_HB
 }
 
 template <bool PACKED, bool UNIT>
