@@ -138,12 +138,54 @@ __global__ __launch_bounds__(256) void k_xtv(const float* __restrict__ Z, int64_
 // and writes eta once. MEASURED: column-tiled / half-wave-per-row variants read the 204-byte rows of a
 // 10M x 51 Z at 1.1-1.45 TB/s (several partial cache lines per load instruction).
 #define ZB_THREADS 256
+// IRLS epilogue of the z.beta pass (R == 1; GLMIterationTask's per-row working weight and response): with wi set,
+// the row's mu = linkinv(eta), g'(mu) and V(mu) give wi = w / max(V g'^2, 1e-30) and zi = eta - off + (y - mu) g'
+// as fp32 (the Gram pass's inputs) instead of eta — the ~12 fp64 elementwise launches of the torch chain become
+// this epilogue. fam: 0 gaussian, 1 binomial / quasibinomial / fractionalbinomial, 2 poisson, 3 gamma;
+// link: 0 identity, 1 logit, 2 log, 3 inverse (the clamps of glm.Family).
+struct IrlsOut {
+  int fam, link;
+  const double* y;
+  const double* w;
+  float* wi;
+  float* zi;
+};
+__device__ __forceinline__ void irls_row(const IrlsOut& io, int64_t row, double e, double o) {
+  double mu, gp;
+  switch (io.link) {
+    case 1: {
+      mu = 1.0 / (1.0 + exp(-e));
+      const double m = fmin(fmax(mu, 1e-10), 1.0 - 1e-10);
+      gp = 1.0 / (m * (1.0 - m));
+      break;
+    }
+    case 2: mu = exp(fmin(e, 700.0)); gp = 1.0 / fmax(mu, 1e-10); break;
+    case 3: {
+      const double s = e + 1e-300;
+      const double ee = fabs(e) < 1e-10 ? 1e-10 * (double)((s > 0.0) - (s < 0.0)) : e;
+      mu = 1.0 / ee;
+      gp = -1.0 / fmax(mu * mu, 1e-20);
+      break;
+    }
+    default: mu = e; gp = 1.0;
+  }
+  double var;
+  switch (io.fam) {
+    case 1: { const double m = fmin(fmax(mu, 1e-10), 1.0 - 1e-10); var = m * (1.0 - m); break; }
+    case 2: var = fmax(mu, 1e-10); break;
+    case 3: var = fmax(mu * mu, 1e-20); break;
+    default: var = 1.0;
+  }
+  io.wi[row] = (float)(io.w[row] / fmax(var * gp * gp, 1e-30));
+  io.zi[row] = (float)(e - o + (io.y[row] - mu) * gp);
+}
 #ifndef ZB_LDS_FLOATS
 #define ZB_LDS_FLOATS 12288    // 48 KiB of Z per block
 #endif
 __global__ __launch_bounds__(ZB_THREADS) void k_zbeta(const float* __restrict__ Z, int64_t ldz,
                                                       const double* __restrict__ B, int R, int64_t N, int P, int TR,
-                                                      const double* __restrict__ off, double* __restrict__ eta) {
+                                                      const double* __restrict__ off, double* __restrict__ eta,
+                                                      IrlsOut io) {
   __shared__ __attribute__((aligned(16))) float tile[ZB_LDS_FLOATS];
   __shared__ double bt[1024];                            // B when P * R <= 1024, else read from global
   const int t = threadIdx.x;
@@ -198,6 +240,10 @@ __global__ __launch_bounds__(ZB_THREADS) void k_zbeta(const float* __restrict__ 
   }
   const int64_t row = r0 + t;
   const double o = off ? off[row] : 0.0;
+  if (io.wi) {
+    irls_row(io, row, acc[0] + o, o);
+    return;
+  }
 #pragma unroll
   for (int k = 0; k < 8; ++k)
     if (k < R) eta[row * R + k] = acc[k] + o;
@@ -260,7 +306,23 @@ int h2o_zbeta(const float* Z, long long ldz, const double* B, int R, long long N
   }
   const long long grid = (N + TR - 1) / TR;
   hipLaunchKernelGGL(k_zbeta, dim3((unsigned)grid), dim3(ZB_THREADS), 0, stream, Z, (int64_t)ldz, B, R, (int64_t)N, P,
-                     TR, off, eta);
+                     TR, off, eta, IrlsOut{0, 0, nullptr, nullptr, nullptr, nullptr});
+  return (int)hipGetLastError();
+}
+
+// The IRLS pass (see IrlsOut): wi / zi fp32 [N] from Z [N, P] fp32, beta fp64 [P], off / y / w fp64 [N]. Designs
+// whose rows do not fit the LDS span (P > ZB_LDS_FLOATS / 4) are refused (the caller keeps the torch chain).
+int h2o_irls_wz(const float* Z, long long ldz, const double* B, long long N, int P, const double* off,
+                const double* y, const double* w, int fam, int link, float* wi, float* zi, hipStream_t stream) {
+  if (N <= 0) return 0;
+  if (P <= 0 || ldz < P || fam < 0 || fam > 3 || link < 0 || link > 3) return (int)hipErrorInvalidValue;
+  int TR = ZB_LDS_FLOATS / P;
+  if (TR > ZB_THREADS) TR = ZB_THREADS;
+  TR &= ~3;
+  if (TR < 4) return (int)hipErrorInvalidValue;
+  const long long grid = (N + TR - 1) / TR;
+  hipLaunchKernelGGL(k_zbeta, dim3((unsigned)grid), dim3(ZB_THREADS), 0, stream, Z, (int64_t)ldz, B, 1, (int64_t)N, P,
+                     TR, off, (double*)nullptr, IrlsOut{fam, link, y, w, wi, zi});
   return (int)hipGetLastError();
 }
 

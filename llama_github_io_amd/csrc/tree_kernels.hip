@@ -163,12 +163,18 @@ __device__ __forceinline__ long long q64(float v, float scale) {
 // second flush reading its partial slot back; 31 tiles keep one flush per block at that size)
 #define PACK_SHIFT 48
 #define PACK_MAX 63488   // rows per LDS flush window in packed mode (31 tiles)
-__device__ __forceinline__ long long qpack(float w, float b, float scale_p) {
+// FPACK (XGBoost: the row weight is a float hessian): the same one-atomic word with 32 / 32 fields, hessian
+// * sw unsigned in the high half, wY * sp signed in the low half, both rounded to nearest; k_qscale sizes
+// sw = 0.99 * 2^32 / (PACK_MAX * max h) and sp = 0.99 * 2^31 / (PACK_MAX * max |wY|), so a window never
+// carries (~2^-15 of the largest row value per row: fp32-class histogram sums at half the LDS atomics).
+// sw / shf come from qs[10] / qs[12] (count mode: 1, 48); the branch is uniform over the kernel.
+__device__ __forceinline__ long long qpack(float w, float b, float scale_p, float sw, float shf) {
+  if (shf < 40.f) return ((long long)__float2uint_rn(w * sw) << 32) + (long long)__float2int_rn(b * scale_p);
   return ((long long)__float2int_rz(w) << PACK_SHIFT) + (long long)__float2int_rz(b * scale_p);
 }
-__device__ __forceinline__ void unpack(long long v, long long& cnt, long long& val) {
-  cnt = (long long)(((unsigned long long)v + (1ull << (PACK_SHIFT - 1))) >> PACK_SHIFT);
-  val = (long long)((unsigned long long)v - ((unsigned long long)cnt << PACK_SHIFT));
+__device__ __forceinline__ void unpack(long long v, long long& cnt, long long& val, int shift = PACK_SHIFT) {
+  cnt = (long long)(((unsigned long long)v + (1ull << (shift - 1))) >> shift);
+  val = (long long)((unsigned long long)v - ((unsigned long long)cnt << shift));
 }
 
 // Flush of one block's LDS histogram into ITS OWN partial slot (plain stores, no global atomics):
@@ -194,6 +200,46 @@ __device__ void flush_partial(const long long* h, const float* nayy, double node
   const int f0 = ftile * FTILE;
   const int nf = min(FTILE, F - f0);
   const double inv_a = qs[2], inv_b = qs[3], inv_p = qs[5];
+  if (packed) {
+    const int pshift = (int)qs[12];
+    const double inv_w = qs[11];
+    // one packed u64 holds both planes of (bin, feature): a lane reads it once (replicas summed), unpacks once and
+    // stores the (w, wY) pair with one 16-byte (8-byte f32) store
+    const int dbin = (int)blockDim.x / nf, drem = (int)blockDim.x - dbin * nf;
+    int bin = (int)threadIdx.x / nf, fl = (int)threadIdx.x - bin * nf;
+    for (int i = threadIdx.x; i < nf * NBIN; i += blockDim.x, bin += dbin, fl += drem) {
+      if (fl >= nf) { fl -= nf; ++bin; }
+      const int reps = srep[fl], nb = snb[fl];
+      long long q = 0;
+      if (sfine[fl]) {
+        const int m = fl & ~3, k = fl & 3;
+#pragma unroll
+        for (int l = 0; l < 4; ++l) {
+          const int bb = l <= k ? bin : bin - 1;
+          if (bb >= 0) q += h[bb * FTILE + fslot(m + l)];
+        }
+      } else if (reps == 1) {
+        q = h[bin * FTILE + fslot(fl)];
+      } else if (bin < nb) {
+        for (int c = 0; c < reps; ++c) q += h[(bin + c * nb) * FTILE + fslot(fl)];
+      }
+      long long c, v;
+      unpack(q, c, v, pshift);
+      const double dc = (double)c * inv_w, dv = (double)v * inv_p;
+      const size_t e2 = (size_t)bin * 2 * F + 2 * (f0 + fl);
+      if (f32) {
+        float2* p2 = (float2*)((float*)part + e2);
+        float2 o = make_float2((float)dc, (float)dv);
+        if (acc) { const float2 a = *p2; o = make_float2((float)((double)a.x + dc), (float)((double)a.y + dv)); }
+        *p2 = o;
+      } else {
+        double2* p2 = (double2*)(part + e2);
+        double2 o = make_double2(dc, dv);
+        if (acc) { const double2 a = *p2; o.x += a.x; o.y += a.y; }
+        *p2 = o;
+      }
+    }
+  } else {
   // (bin, rem) of entry i advanced incrementally: no integer division per entry
   const int row2 = 2 * nf, dbin = (int)blockDim.x / row2, drem = (int)blockDim.x - dbin * row2;
   int bin = (int)threadIdx.x / row2, rem = (int)threadIdx.x - bin * row2;
@@ -206,29 +252,20 @@ __device__ void flush_partial(const long long* h, const float* nayy, double node
       // column k of a fine group: bin b holds fine bins t = 4h + l with h + [l > k] == b, i.e. entries
       // (b, l <= k) and (b - 1, l > k) of the fine histogram (NA: t = 1020 = entry (255, 0))
       const int m = fl & ~3, k = fl & 3;
-      const int pl = packed ? 0 : r * HPLANE;
+      const int pl = r * HPLANE;
 #pragma unroll
       for (int l = 0; l < 4; ++l) {
         const int bb = l <= k ? bin : bin - 1;
         if (bb >= 0) q += h[pl + bb * FTILE + fslot(m + l)];
       }
     } else if (reps == 1 || bin < nb) {
-      for (int c = 0; c < reps; ++c) {
-        const int e = (bin + c * nb) * FTILE + fslot(fl);
-        q += packed ? h[e] : h[r * HPLANE + e];
-      }
+      for (int c = 0; c < reps; ++c) q += h[r * HPLANE + (bin + c * nb) * FTILE + fslot(fl)];
     }
-    double d;
-    if (packed) {
-      long long c, v;
-      unpack(q, c, v);
-      d = r ? (double)v * inv_p : (double)c;
-    } else {
-      d = (double)q * (r ? inv_b : inv_a);
-    }
+    const double d = (double)q * (r ? inv_b : inv_a);
     const size_t e2 = (size_t)bin * 2 * F + 2 * (f0 + fl) + r;
     if (f32) put_partial((float*)part + e2, d, acc);
     else put_partial(part + e2, d, acc);
+  }
   }
   for (int i = threadIdx.x; i < nf; i += blockDim.x) {
     const size_t e2 = (size_t)F * 2 * NBIN + f0 + i;
@@ -453,7 +490,7 @@ __device__ __forceinline__ void hist_rows(long long* h, float* nayy, const HistS
       if (lead) wyy += UNIT ? ab[u].y * ab[u].y : row_yy(ab[u].x, ab[u].y);
       // (int) conversion truncates toward zero (v_cvt_i32_f32): the __float2int_rz form added a v_trunc_f32
       const long long qa = UNIT ? (1ll << PACK_SHIFT) + (long long)(int)(ab[u].y * sp)
-                                : PACKED ? qpack(ab[u].x, ab[u].y, sp) : q64(ab[u].x, sa);
+                                : PACKED ? qpack(ab[u].x, ab[u].y, sp, sa, sb) : q64(ab[u].x, sa);
       const long long qb = PACKED ? 0ll : q64(ab[u].y, sb);
       const unsigned w = wd[u];
       if (FINE && fine) {
@@ -565,7 +602,7 @@ __device__ __forceinline__ void hist_span(long long* h, float* nayy, const HistS
     if (base + GR * UNR < r1) load(base + GR * UNR, wdn, abn);
     auto atoms = [&](int u) {
       const long long qa = UNIT ? (1ll << PACK_SHIFT) + (long long)(int)(ab[u].y * sp)
-                                : PACKED ? qpack(ab[u].x, ab[u].y, sp) : q64(ab[u].x, sa);
+                                : PACKED ? qpack(ab[u].x, ab[u].y, sp, sa, sb) : q64(ab[u].x, sa);
       const long long qb = PACKED ? 0ll : q64(ab[u].y, sb);
       const unsigned w = wd[u];
       if (FINE && fine) {
@@ -688,7 +725,7 @@ __device__ __forceinline__ void filt_atoms(const FiltLane& L, long long* h, floa
     const float x = UNIT ? 1.f : wv[u];
     if (L.lead) wyy += UNIT ? yv[u] * yv[u] : row_yy(x, yv[u]);
     const long long qa = UNIT ? (1ll << PACK_SHIFT) + (long long)(int)(yv[u] * sp)
-                              : PACKED ? qpack(x, yv[u], sp) : q64(x, sa);
+                              : PACKED ? qpack(x, yv[u], sp, sa, sb) : q64(x, sa);
     const long long qb = PACKED ? 0ll : q64(yv[u], sb);
     const unsigned w = wd[u];
     if (FINE && L.fine) {
@@ -761,7 +798,8 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
   const int wabs = planar ? j : ftile * LPR + j;        // word index of this lane within a row of bins32
   const int Fl = planar ? F - ftile * FTILE : F;
   const unsigned* bins32 = (const unsigned*)(planar ? bins + (size_t)ftile * (size_t)N * 32 : bins);
-  const float sa = (float)qs[0], sb = (float)qs[1], sp = (float)qs[4];
+  // packed modes have no second plane: sa / sb carry the weight scale and field shift of the packed word
+  const float sa = (float)qs[PACKED ? 10 : 0], sb = (float)qs[PACKED ? 12 : 1], sp = (float)qs[4];
   const HistSrc src = make_src(bins32, aw, ay, N, W, lgw);
   // per tile feature: bin count and copies of its bins (NONA: no NA bin, so copies of bins < nb never reach 255)
   __shared__ int srep[FTILE], snb[FTILE], sfine[FTILE];
@@ -2185,7 +2223,7 @@ __global__ __launch_bounds__(256) void k_amax(const float* __restrict__ aux, lon
 // Also the tree's start-of-build reset: leaf counters and the amax shards themselves once read (the next
 // tree's fused step re-fills them).
 __global__ __launch_bounds__(256) void k_qscale(unsigned* __restrict__ amax_bits, double* __restrict__ qs,
-                                                int* __restrict__ counters, long long N) {
+                                                int* __restrict__ counters, long long N, int fpack) {
   __shared__ unsigned sm[4];
   if (threadIdx.x < 4) {
     unsigned mbits = 0u;
@@ -2201,10 +2239,15 @@ __global__ __launch_bounds__(256) void k_qscale(unsigned* __restrict__ amax_bits
       const double sc = ok ? 1099511627776.0 / m : 1.0;   // 2^40 / max
       qs[c] = sc;
       qs[2 + c] = 1.0 / sc;
-      if (c == 1) {                                        // packed wY: 2^30 / max
-        const double sp = ok ? 1073741824.0 / m : 1.0;
+      if (c == 1) {                                        // packed wY: 2^30 / max (FPACK: 32-bit field)
+        const double sp = !ok ? 1.0 : fpack ? 0.99 * 2147483648.0 / ((double)PACK_MAX * m) : 1073741824.0 / m;
         qs[4] = sp;
         qs[5] = 1.0 / sp;
+      } else {                                             // packed weight field: scale, 1 / scale, shift
+        const double sw = (fpack && ok) ? 0.99 * 4294967296.0 / ((double)PACK_MAX * m) : 1.0;
+        qs[10] = sw;
+        qs[11] = 1.0 / sw;
+        qs[12] = fpack ? 32.0 : (double)PACK_SHIFT;
       }
     } else {
       int lb = 61;
@@ -2540,8 +2583,8 @@ int h2o_amax(const void* aux, long long N, void* amax_bits, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-int h2o_qscale(void* amax_bits, void* qs, void* counters, long long N, hipStream_t s) {
-  hipLaunchKernelGGL(k_qscale, dim3(1), dim3(256), 0, s, (unsigned*)amax_bits, (double*)qs, (int*)counters, N);
+int h2o_qscale(void* amax_bits, void* qs, void* counters, long long N, int fpack, hipStream_t s) {
+  hipLaunchKernelGGL(k_qscale, dim3(1), dim3(256), 0, s, (unsigned*)amax_bits, (double*)qs, (int*)counters, N, fpack);
   return (int)hipGetLastError();
 }
 
@@ -2632,6 +2675,7 @@ struct TreePlan {
   int lo_F, lo_from, mid_F, mid_from;
   void* lvl2;                 // [N] uint8: the root route's level-2 node / 128 + leaf per row (narrow runs; or null)
   void* fdir;                 // [N] uint8: the root split's side per row (k_row_dir; narrow planar runs, or null)
+  int num_plane, pad4;        // aux plane of the leaf-sum numerator (2; 1 when the step kernel elides num == wY)
 };
 
 // op codes / dtypes of the collective transport
@@ -2685,7 +2729,7 @@ int h2o_tree_plan_size() { return (int)sizeof(TreePlan); }
 int h2o_tree_root(const TreePlan* P, hipStream_t s) {
   if (P->D >= TP_MAXL - 1) return (int)hipErrorInvalidValue;
   if (P->compute_amax) TP_CHECK(h2o_amax(P->aux, P->N, P->amax_bits, s));
-  TP_CHECK(h2o_qscale(P->amax_bits, P->qs, P->counters, P->N, s));
+  TP_CHECK(h2o_qscale(P->amax_bits, P->qs, P->counters, P->N, P->packed == 2, s));
   const int g0 = P->tiles_cap[0] < P->grid ? P->tiles_cap[0] : P->grid;
   TP_CHECK(h2o_hist_build(P->master, P->stride, P->unit ? nullptr : tp_aux(P, 0), tp_aux(P, 1), P->nodes[0], P->bp[0],
                           P->meta[0], P->F, P->partials, P->slot, P->qs, g0, P->packed, nullptr, nullptr, P->pf32, P->N,
@@ -2816,7 +2860,7 @@ static int tree_leaves(const TreePlan* P, bool values, hipStream_t s) {
   for (int d = 0; d < P->D; ++d) n_nodes += P->caps[d];
   const LeafVals lv{P->log_link, P->scale, P->kclamp, P->mx, P->leaf_lam, P->leaf_l1,
                     values ? (float*)P->leafval : nullptr};
-  return leaf_assign_launch(P->master, P->stride, P->N, P->lvptrs, P->D, tp_aux(P, 2), tp_aux(P, 3), P->qs,
+  return leaf_assign_launch(P->master, P->stride, P->N, P->lvptrs, P->D, tp_aux(P, P->num_plane), tp_aux(P, 3), P->qs,
                             P->leaf_of_row, P->leafq, P->leaf_cap, P->leafsum, n_nodes, P->planar, lv, s, tp_lvl2(P));
 }
 

@@ -147,10 +147,19 @@ class Expander:
         self.names = [f"hashed_cat_{i}" for i in range(n_slots)] + self.names[nc:]
         return self
 
-    def transform(self, X: torch.Tensor, dtype=torch.float32) -> torch.Tensor:
-        """[F, N] raw -> [N, P] design matrix."""
-        Z = self._transform(X, dtype)
+    def transform(self, X: torch.Tensor, dtype=torch.float32, extra=None) -> torch.Tensor:
+        """[F, N] raw -> [N, P] design matrix; ``extra`` (a constant, e.g. GLM's intercept column 1 / 0) appends
+        column P = extra, written in place ([N, P + 1], no concatenation copy of the design)."""
         h = getattr(self, "cat_hash", None)
+        if extra is not None and not h:
+            return self._transform(X, dtype, extra)
+        Z = self._transform(X, dtype)
+        if extra is not None:
+            Z = self._hash_cats(Z, h)
+            return torch.cat([Z, torch.full((Z.shape[0], 1), float(extra), dtype=Z.dtype, device=Z.device)], 1)
+        return self._hash_cats(Z, h)
+
+    def _hash_cats(self, Z, h):
         if h:
             nc = self.num_off
             idx = torch.as_tensor(h["idx"], dtype=torch.long, device=Z.device)
@@ -158,10 +167,16 @@ class Expander:
             Z = torch.cat([Zc, Z[:, nc:]], 1)
         return Z
 
-    def _transform(self, X: torch.Tensor, dtype=torch.float32) -> torch.Tensor:
+    def _transform(self, X: torch.Tensor, dtype=torch.float32, extra=None) -> torch.Tensor:
         N = X.shape[1]
         dev = X.device
-        Z = torch.zeros(N, self.P, dtype=dtype, device=dev)
+        ncol = self.P + (0 if extra is None else 1)
+        dense = (not self.cats and self.nums and self.num_off == 0 and len(self.nums) == self.P and _hip_ok(X)
+                 and dtype in (torch.float32, torch.bfloat16))
+        # every column written below (all-numeric HIP transform): no zero fill of the [N, P] design
+        Z = (torch.empty if dense else torch.zeros)(N, ncol, dtype=dtype, device=dev)
+        if extra is not None:
+            Z[:, self.P] = float(extra)
         start = 0 if self.use_all else 1
         for i, j in enumerate(self.cats):
             codes = X[j]
@@ -190,7 +205,7 @@ class Expander:
             sub = mu if (self.standardize or self.center_only) else torch.zeros_like(mu)
             mul = (1.0 / self.num_sd.to(dev).float()) if self.standardize else torch.ones_like(mu)
             nat.call("h2o_num_transform", X.data_ptr(), N, rows.data_ptr(), k, fill.data_ptr(), sub.contiguous().data_ptr(),
-                     mul.contiguous().data_ptr(), Z.data_ptr(), self.P, self.num_off, int(dtype == torch.bfloat16),
+                     mul.contiguous().data_ptr(), Z.data_ptr(), ncol, self.num_off, int(dtype == torch.bfloat16),
                      nat.stream_ptr(dev))
             return Z
         for a in range(0, len(self.nums), CH):

@@ -25,6 +25,9 @@ from ..ops.segment import segment_sum
 _FUSED_DIST = {"gaussian": 0, "bernoulli": 1, "quasibinomial": 2, "poisson": 3, "gamma": 4, "tweedie": 5,
                "laplace": 6, "quantile": 7, "huber": 8, "modified_huber": 9}
 
+# fused distributions whose gamma numerator is w * z (GBM.java gammaNum of DistributionFactory): plane 2 == plane 1
+_NUM_IS_WZ = frozenset({"gaussian", "bernoulli", "quasibinomial", "laplace", "quantile", "huber"})
+
 GBM_DEFAULTS = dict(ntrees=50, max_depth=5, min_rows=10.0, learn_rate=0.1, learn_rate_annealing=1.0,
                     sample_rate=1.0, col_sample_rate=1.0, col_sample_rate_change_per_level=1.0,
                     col_sample_rate_per_tree=1.0, distribution="AUTO", tweedie_power=1.5, quantile_alpha=0.5,
@@ -144,6 +147,15 @@ class GBMTrainer(SharedTreeTrainer):
         return (self._fused() and getattr(self, "_wbuf", None) is None and self.p.get("weights_column") is None
                 and float(self.p["sample_rate"]) >= 1.0 and not getattr(self, "_y_has_nan", True))
 
+    def _step_skip(self):
+        # planes the fused step need not store: 0 (w) when every weight is 1 and nothing reads w (the order-statistic
+        # leaves read it), 2 (gamma numerator) where it equals w * z (the leaf sums then read plane 1)
+        sk = 1 if self._unit_weights() and self.dname not in ORDER_STAT_DISTS else 0
+        return sk | (4 if self.dname in _NUM_IS_WZ else 0)
+
+    def _num_plane(self):
+        return 1 if self._fused() and self.dname in _NUM_IS_WZ else 2
+
     def _lr(self, t):
         return float(self.p["learn_rate"]) * float(self.p["learn_rate_annealing"]) ** t
 
@@ -171,7 +183,7 @@ class GBMTrainer(SharedTreeTrainer):
                      0 if self._wbuf is None else self._wbuf.data_ptr(), self.f.data_ptr(),
                      0 if pv is None else pv.data_ptr(), 0 if pl is None else pl.data_ptr(),
                      float(self.p["sample_rate"]), (self.seed * 0x9E3779B1 + t * 7919) & ((1 << 64) - 1),
-                     float(p1), self.aux.data_ptr(), self._amax.data_ptr(), nat.stream_ptr(self.dev))
+                     float(p1), self.aux.data_ptr(), self._amax.data_ptr(), self._step_skip(), nat.stream_ptr(self.dev))
             self._pending = None
             self.w_eff = None
             return self.aux

@@ -571,9 +571,8 @@ class GLMTrainer:
         ex = Expander(info, standardize=p["standardize"], use_all_factor_levels=p["use_all_factor_levels"] or
                       fam == "multinomial", missing=p["missing_values_handling"],
                       plug_values=p.get("plug_values")).fit(X, w, reduce=coll.all_reduce_ if coll.is_dist() else None)
-        Z = ex.transform(X)  # [N, P] f32
         intercept = bool(p["intercept"])
-        Zi = torch.cat([Z, torch.ones(N, 1, dtype=Z.dtype, device=dev) if intercept else torch.zeros(N, 1, dtype=Z.dtype, device=dev)], 1)
+        Zi = ex.transform(X, extra=1.0 if intercept else 0.0)  # [N, P + 1] f32: the design + intercept column
         alpha = p["alpha"]
         alpha = float((alpha if isinstance(alpha, (int, float)) else alpha[0]) if alpha is not None else
                       (0.0 if canon(p["solver"]) == "lbfgs" else 0.5))
@@ -778,13 +777,14 @@ class GLMTrainer:
             if p.get("cold_start") and li > 0:     # cold_start: every lambda starts from the initial coefficients
                 beta = beta_start.clone()
             for it in range(max(max_it, 1)):
-                eta = G.zbeta(Zi, beta, off)
-                mu = fam.linkinv(eta)
-                gp = fam.dlink(mu)
-                var = fam.variance(mu)
-                wi = w / (var * gp * gp).clamp(min=1e-30)
-                zi = eta - off + (y - mu) * gp
-                Gm, r = G.gram(Zi, wi.float(), zi.float())      # one pass: Zᵀ W Z and Zᵀ W z
+                wz = G.irls_wz(Zi, beta, off, y, w, fam.name, fam.link)   # fused: one pass, fp32 wi / zi
+                if wz is None:
+                    eta = G.zbeta(Zi, beta, off)
+                    mu = fam.linkinv(eta)
+                    gp = fam.dlink(mu)
+                    var = fam.variance(mu)
+                    wz = ((w / (var * gp * gp).clamp(min=1e-30)).float(), (eta - off + (y - mu) * gp).float())
+                Gm, r = G.gram(Zi, wz[0], wz[1])      # one pass: Zᵀ W Z and Zᵀ W z
                 if coll.is_dist():
                     Gm = coll.all_reduce_(Gm)
                     r = coll.all_reduce_(r)

@@ -137,6 +137,9 @@ class SharedTreeTrainer:
         """The trainer's _prepare returns the row statistics as [4, N] planes (else [N, 4] rows)."""
         return False
 
+    def _num_plane(self) -> int:
+        return 2
+
     def _unit_weights(self) -> bool:
         """Every row weight of the current tree is exactly 1 (no weights, no row sampling)."""
         return False
@@ -303,6 +306,8 @@ class SharedTreeTrainer:
                     kw["packed"] = self._hist_packed()
                     kw["soa"] = aux.dim() == 2 and aux.shape[0] == 4 and aux.shape[1] == self.N and self._aux_soa()
                     kw["unit"] = self._unit_weights()
+                    if kw["soa"]:
+                        kw["num_plane"] = self._num_plane()
                     ln = self._leaf_native(t, k)
                     if ln is not None:
                         kw["leaf_native"] = ln

@@ -12,6 +12,7 @@ descent on the expanded design matrix.
 from __future__ import annotations
 
 import math
+import os
 
 import numpy as np
 import torch
@@ -249,6 +250,19 @@ class XGBoostTrainer(SharedTreeTrainer):
     # (the torch path is ~10 elementwise kernels over N rows per tree); leaves by k_leaf_values
     _FUSED_OBJ = {"bernoulli": 10, "gaussian": 0}
 
+    def _hist_packed(self):
+        # one LDS atomic per (row, feature): squared error rows weigh exactly 1 (count|wY word); logistic hessians
+        # go in the 32/32 fixed-point FPACK word (2 = tree.build packed mode; H2O_XGB_FPACK=0: two 64-bit atomics)
+        if not self._fused():
+            return False
+        if self.obj == "gaussian":
+            return True
+        return 2 if os.environ.get("H2O_XGB_FPACK", "1") != "0" else False
+
+    def _num_plane(self):
+        # both fused objectives store num == w * z only in plane 1 (h2o_gbm_step skip bit 2)
+        return 1 if self._fused() else 2
+
     def _fused(self):
         if getattr(self, "_fused_ok", None) is None:
             self._fused_ok = bool(
@@ -289,7 +303,7 @@ class XGBoostTrainer(SharedTreeTrainer):
             pv, pl = self._pending if getattr(self, "_pending", None) is not None else (None, None)
             nat.call("h2o_gbm_step", self.N, self.row0, self._FUSED_OBJ[self.obj], self.y.data_ptr(), 0,
                      self.f.data_ptr(), 0 if pv is None else pv.data_ptr(), 0 if pl is None else pl.data_ptr(),
-                     1.0, 0, 0.0, self.aux.data_ptr(), self._amax.data_ptr(), nat.stream_ptr(self.dev))
+                     1.0, 0, 0.0, self.aux.data_ptr(), self._amax.data_ptr(), 4, nat.stream_ptr(self.dev))
             self._pending = None
             return self.aux
         if k == 0:

@@ -59,12 +59,12 @@ _HIP_SIGS = {
     "h2o_kmeans_mfma_shape": [c_int, c_int, c_void_p],
     "h2o_kmeans_mfma_grid": [c_int, c_int],
     "h2o_kmeans_mfma": [c_void_p, c_ll, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p],
-    "h2o_qscale": [c_void_p, c_void_p, c_void_p, c_ll, c_void_p],
+    "h2o_qscale": [c_void_p, c_void_p, c_void_p, c_ll, c_int, c_void_p],
     "h2o_hist_reduce": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
                         c_void_p, c_int, c_int, c_int, c_int, c_void_p],
     "h2o_leaf_values": [c_void_p, c_int, c_int, c_double, c_double, c_double, c_double, c_double, c_void_p, c_void_p],
     "h2o_gbm_step": [c_ll, c_ll, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_float, c_ull,
-                     ctypes.c_float, c_void_p, c_void_p, c_void_p],
+                     ctypes.c_float, c_void_p, c_void_p, c_int, c_void_p],
     "h2o_add_leaf": [c_ll, c_void_p, c_int, c_void_p, c_void_p, c_void_p],
     "h2o_predict": [c_void_p, c_ll, c_int] + [c_void_p] * 11 + [c_int, c_void_p, c_void_p, c_void_p],
 }

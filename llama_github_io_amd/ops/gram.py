@@ -17,7 +17,36 @@ nat.register_hip_signatures({
     "h2o_xtv": [nat.c_void_p, nat.c_ll, nat.c_void_p, nat.c_int, nat.c_ll, nat.c_int, nat.c_int, nat.c_void_p, nat.c_void_p],
     "h2o_zbeta": [nat.c_void_p, nat.c_ll, nat.c_void_p, nat.c_int, nat.c_ll, nat.c_int, nat.c_void_p, nat.c_void_p,
                   nat.c_void_p],
+    "h2o_irls_wz": [nat.c_void_p, nat.c_ll, nat.c_void_p, nat.c_ll, nat.c_int, nat.c_void_p, nat.c_void_p, nat.c_void_p,
+                    nat.c_int, nat.c_int, nat.c_void_p, nat.c_void_p, nat.c_void_p],
 })
+
+# glm.Family -> the k_zbeta IRLS epilogue's codes (csrc/gram_kernels.hip IrlsOut)
+_IRLS_FAM = {"gaussian": 0, "binomial": 1, "quasibinomial": 1, "fractionalbinomial": 1, "poisson": 2, "gamma": 3}
+_IRLS_LINK = {"identity": 0, "logit": 1, "log": 2, "inverse": 3}
+
+
+def irls_wz(Z: torch.Tensor, beta: torch.Tensor, off, y: torch.Tensor, w: torch.Tensor, family: str, link: str):
+    """IRLS working weights and response of one iteration, fp32 [N] each, in the z.beta pass (one HIP launch:
+    eta = Z beta + off, mu, g'(mu), V(mu) per row) — or None where the family / link / device is not covered and
+    the caller keeps the torch chain. Same formulas and clamps as ``glm.Family``."""
+    if (not Z.is_cuda or family not in _IRLS_FAM or link not in _IRLS_LINK or beta.dim() != 1
+            or Z.shape[1] > 3072 or os.environ.get("H2O_GLM_FUSED_IRLS", "1") == "0"):
+        return None
+    N, P = Z.shape
+    Z = Z.contiguous()
+    od = None
+    if off is not None:
+        od = (off if torch.is_tensor(off) else torch.full((N,), float(off), device=Z.device)).double()
+        od = (od.expand(N) if od.numel() == 1 else od).contiguous()
+    yd, wd = y.contiguous().double(), w.contiguous().double()
+    wi = torch.empty(N, dtype=torch.float32, device=Z.device)
+    zi = torch.empty(N, dtype=torch.float32, device=Z.device)
+    if N > 0:
+        nat.call("h2o_irls_wz", Z.data_ptr(), P, beta.contiguous().double().data_ptr(), N, P,
+                 0 if od is None else od.data_ptr(), yd.data_ptr(), wd.data_ptr(), _IRLS_FAM[family], _IRLS_LINK[link],
+                 wi.data_ptr(), zi.data_ptr(), nat.stream_ptr(Z.device))
+    return wi, zi
 
 
 def zbeta(Z: torch.Tensor, B: torch.Tensor, off=None) -> torch.Tensor:

@@ -585,7 +585,8 @@ class _TreePlan(ctypes.Structure):
                 [("leaf_lam", _cd), ("leaf_l1", _cd)] + [("planar", _ci), ("no_na", _ci)] +
                 [("fgroup", _vp)] + [("coll_fn", _vp), ("coll_ctx", _vp)] +
                 [(n, _ci) for n in ("W", "cf32", "cand_fs", "dist")] + [(n, _vp) for n in ("hsend", "cand_all", "lsx")] +
-                [("fine_f", _vp)] + [(n, _ci) for n in ("lo_F", "lo_from", "mid_F", "mid_from")] + [("lvl2", _vp), ("fdir", _vp)])
+                [("fine_f", _vp)] + [(n, _ci) for n in ("lo_F", "lo_from", "mid_F", "mid_from")] + [("lvl2", _vp), ("fdir", _vp)] +
+                [("num_plane", _ci), ("pad4", _ci)])
 
 
 class _Arena:
@@ -927,15 +928,16 @@ class GpuTreeBuilder:
         return self._soa
 
     def build(self, aux_static: torch.Tensor, feat_ok: torch.Tensor | None = None, k_cols: int = 0, seed: int = 0,
-              leaf_fn=None, amax_bits: torch.Tensor | None = None, packed: bool = False, leaf_native=None,
-              soa: bool = False, unit: bool = False):
+              leaf_fn=None, amax_bits: torch.Tensor | None = None, packed: bool | int = False, leaf_native=None,
+              soa: bool = False, unit: bool = False, num_plane: int = 2):
         """Launch one tree (one host call single-process; one per collective segment row-sharded).
         ``leaf_fn(leafsum[L,2] f64) -> leaf values f32`` runs on device before the arena snapshot, so values
         travel to the host with the structure (no extra sync); ``leaf_native = (log_link, scale, kclamp,
         max_abs)`` instead computes closed-form Newton leaf values in one HIP launch (k_leaf_values).
         ``amax_bits`` (int32[4*AMAX_SHARDS], max |plane| as float bits) may be produced by a fused prepare
         kernel; otherwise it is computed here. ``packed`` (caller guarantees w is a 0/1 or small integer row
-        weight) switches the LDS histograms to one packed count|wY atomic per (row, feature); ``unit``
+        weight) switches the LDS histograms to one packed count|wY atomic per (row, feature), ``packed=2`` (float
+        weights, XGBoost hessians) to the 32/32 fixed-point hessian|wY word (FPACK, k_qscale scales); ``unit``
         (every w is exactly 1) drops w from the row payload altogether."""
         if not hasattr(self, "_plan"):
             self._plan = self._make_plan()
@@ -944,6 +946,7 @@ class GpuTreeBuilder:
         s = nat.stream_ptr(self.dev)
         P.aux = planes.data_ptr()
         P.unit = int(bool(unit))
+        P.num_plane = int(num_plane) if soa else 2
         if not unit:
             for i in range(2):
                 if self.bufs[i]["w"] is None:
@@ -952,7 +955,7 @@ class GpuTreeBuilder:
         P.compute_amax = int(amax_bits is None)
         P.amax_bits = (self.amax_bits if amax_bits is None else amax_bits).data_ptr()
         P.feat_ok = (self.feat_ok_all if feat_ok is None else feat_ok).data_ptr()
-        P.k_cols, P.packed, P.seed = _level_k(k_cols, 0), int(bool(packed)), int(seed) & _M64
+        P.k_cols, P.packed, P.seed = _level_k(k_cols, 0), (2 if packed == 2 else int(bool(packed))), int(seed) & _M64
         for d in range(_MAXL):
             P.kc_level[d] = _level_k(k_cols, d) if isinstance(k_cols, (list, tuple)) else 0
         P.grid = self.grid * (self.hist_bpc if packed else 1)

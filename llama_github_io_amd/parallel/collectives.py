@@ -83,15 +83,21 @@ def _count(t: torch.Tensor):
 
 
 def _staged(t: torch.Tensor) -> bool:
-    """gloo cannot run every collective on device tensors: stage those through host memory."""
-    return t.is_cuda and dist.get_backend() != "nccl"
+    """The tensor is not on the backend's device: gloo cannot run every collective on device tensors and RCCL
+    ('nccl') runs none on host tensors — stage it through the backend's device (host for gloo, the rank's GPU
+    for RCCL)."""
+    return t.is_cuda != (dist.get_backend() == "nccl")
+
+
+def _stage(t: torch.Tensor) -> torch.Tensor:
+    return t.detach().to(comm_device())
 
 
 def all_reduce_(t: torch.Tensor, op=None) -> torch.Tensor:
     if is_dist():
         _count(t)
         if _staged(t):
-            h = t.detach().cpu()
+            h = _stage(t)
             dist.all_reduce(h, op=op or dist.ReduceOp.SUM)
             t.copy_(h)
         else:
@@ -118,7 +124,7 @@ def reduce_scatter_(out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
         return out
     _count(inp)
     if _staged(inp):
-        h = inp.detach().cpu()
+        h = _stage(inp)
         dist.all_reduce(h)
         n = out.numel()
         out.copy_(h.view(-1)[rank() * n:(rank() + 1) * n].view_as(out))
@@ -134,9 +140,10 @@ def all_gather_into_(out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
         return out
     _count(inp)
     if _staged(inp):
-        parts = [torch.empty_like(inp, device="cpu") for _ in range(world())]
-        dist.all_gather(parts, inp.detach().cpu())
-        out.copy_(torch.cat([p.reshape(-1) for p in parts]).view_as(out))
+        h = _stage(inp)
+        parts = [torch.empty_like(h) for _ in range(world())]
+        dist.all_gather(parts, h)
+        out.copy_(torch.cat([p.reshape(-1) for p in parts]).view_as(out).to(out.device))
     else:
         dist.all_gather_into_tensor(out, inp.contiguous())
     return out
@@ -204,7 +211,7 @@ def all_gather_cat(t: torch.Tensor, dim: int = 0, force: bool = False, bounded: 
     if not (world_active() if force else is_dist()):
         return t
     if _staged(t):
-        return all_gather_cat(t.cpu(), dim, force, bounded).to(t.device)
+        return all_gather_cat(_stage(t), dim, force, bounded).to(t.device)
     if not bounded:
         _stats["row_gathers"] += 1
     n = torch.tensor([t.shape[dim]], device=t.device)
@@ -235,7 +242,7 @@ def exchange_rows(t: torch.Tensor, dest: torch.Tensor) -> torch.Tensor:
     if not is_dist():
         return t
     if _staged(t):
-        return exchange_rows(t.cpu(), dest.cpu()).to(t.device)
+        return exchange_rows(_stage(t), dest.to(comm_device())).to(t.device)
     W = world()
     order = torch.argsort(dest, stable=True)
     ts = t[order].contiguous()
@@ -253,7 +260,7 @@ def broadcast_(t: torch.Tensor, src: int = 0) -> torch.Tensor:
     if is_dist():
         _count(t)
         if _staged(t):
-            h = t.detach().cpu()
+            h = _stage(t)
             dist.broadcast(h, src)
             t.copy_(h)
         else:

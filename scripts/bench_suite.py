@@ -31,10 +31,26 @@ def _sync():
         torch.cuda.synchronize()
 
 
-def _emit(d):
+def _emit(d, iterations=None):
+    """One JSON line (rank 0) with the collective counters of the timed fit (calls / bytes through the process
+    group's backend: RCCL under torchrun or H2O_FORCE_SHARDED=1) and, given iterations, calls per iteration."""
     from llama_github_io_amd.parallel import collectives as coll
+    st = coll.stats()
+    d = dict(d, collectives=dict(calls=st["calls"], bytes=st["bytes"], backend=_backend()))
+    if iterations:
+        d["collectives_per_iteration"] = round(st["calls"] / float(iterations), 2)
     if coll.rank() == 0:
         print(json.dumps(d), flush=True)
+
+
+def _backend():
+    import torch.distributed as dist
+    return dist.get_backend() if dist.is_available() and dist.is_initialized() else None
+
+
+def _reset_stats():
+    from llama_github_io_amd.parallel import collectives as coll
+    coll.stats(reset=True)
 
 
 def bench_xgb(a, dev, world, rank):
@@ -54,13 +70,14 @@ def bench_xgb(a, dev, world, rank):
     XGBoostTrainer(dict(ntrees=2, max_depth=6, learn_rate=0.3, seed=1, max_bins=256)).fit(
         X[:, :1_000_000].contiguous(), y[:1_000_000].contiguous(), None, None, info)
     _sync()
+    _reset_stats()
     t0 = time.perf_counter()
     m = XGBoostTrainer(dict(ntrees=T, max_depth=6, learn_rate=0.3, seed=1, max_bins=256)).fit(X, y, None, None, info)
     _sync()
     dt = time.perf_counter() - t0
     _emit(dict(metric="XGBoost hist train rows/sec (500 trees, depth 6, 100M x 50)", value=N * T / dt / T, unit="rows/s",
                n_gpus=world, seconds=dt, ms_per_tree=dt * 1000 / T, trees=T, rows=N, cols=F,
-               train_auc=m.output["training_metrics"]["AUC"], dtype="fp32", data="synthetic"))
+               train_auc=m.output["training_metrics"]["AUC"], dtype="fp32", data="synthetic"), iterations=T)
 
 
 def bench_dl(a, dev, world, rank):
@@ -79,6 +96,7 @@ def bench_dl(a, dev, world, rank):
                              stopping_rounds=0, score_interval=1e9, standardize=False)).fit(
         X[:, :8 * a.batch].contiguous(), y[:8 * a.batch].contiguous(), None, None, info)
     _sync()
+    _reset_stats()
     t0 = time.perf_counter()
     m = DeepLearningTrainer(dict(hidden=[200, 200], epochs=a.epochs, compute_dtype=cd, mini_batch_size=a.batch,
                                  seed=1, stopping_rounds=0, score_interval=1e9, standardize=False)).fit(X, y, None, None, info)
@@ -86,10 +104,11 @@ def bench_dl(a, dev, world, rank):
     dt = time.perf_counter() - t0
     _emit(dict(metric=f"DeepLearning MLP [200,200] train samples/sec (10M x 784, {cd}, data-parallel)",
                value=N * a.epochs / dt, unit="samples/s", n_gpus=world, seconds=dt, rows=N, cols=F, batch=a.batch,
-               train_auc=m.output["training_metrics"]["AUC"], dtype=cd, data="synthetic",
+               train_auc=m.output["training_metrics"]["AUC"], train_logloss=m.output["training_metrics"].get("logloss"),
+               dtype=cd, data="synthetic",
                step_mode=m.output.get("training_step_mode"), explicit=m.output.get("training_step_explicit"),
                fused_mfma=m.output.get("training_step_fused_mfma"),
-               phases=m.output.get("phase_seconds")))
+               phases=m.output.get("phase_seconds")), iterations=m.output.get("averaging_rounds") or len(m.output.get("scoring_history") or []) or None)
 
 
 def bench_automl(a, dev, world, rank):
@@ -175,13 +194,14 @@ def bench_glm_big(a, dev, world, rank):
     prm = dict(family="binomial", solver="IRLSM", lambda_=0.0, standardize=True)
     GLMTrainer(dict(prm, max_iterations=1)).fit(X[:, :100000].contiguous(), y[:100000].contiguous(), None, None, info)
     _sync()
+    _reset_stats()
     t0 = time.perf_counter()
     m = GLMTrainer(prm).fit(X, y, None, None, info)
     _sync()
     dt = time.perf_counter() - t0
     _emit(dict(metric="GLM binomial IRLSM 10M x 50 (seconds)", value=dt, unit="s", higher_is_better=False,
                iterations=m.output.get("iterations"), auc=m.output["training_metrics"].get("AUC"), rows=N, cols=F,
-               n_gpus=world))
+               n_gpus=world), iterations=m.output.get("iterations"))
 
 
 def bench_kmeans(a, dev, world, rank):
@@ -195,18 +215,24 @@ def bench_kmeans(a, dev, world, rank):
     info = DataInfo([f"x{i}" for i in range(F)], np.zeros(F, np.int32), [None] * F, None, None)
     KMeansTrainer(dict(k=10, max_iterations=2, init="Random", seed=1, standardize=False)).fit(X, None, None, None, info)
     times, iters = {}, {}
+    calls = {}
     for it in (10, 30):
         _sync()
+        _reset_stats()
         t0 = time.perf_counter()
         m = KMeansTrainer(dict(k=10, max_iterations=it, init="Random", seed=1, standardize=False)).fit(X, None, None, None, info)
         _sync()
         times[it] = time.perf_counter() - t0
         iters[it] = m.output["iterations"]
+        from llama_github_io_amd.parallel import collectives as coll
+        calls[it] = coll.stats()["calls"]
     dt = times[10]
     per_iter = (times[30] - times[10]) / max(iters[30] - iters[10], 1)
     _emit(dict(metric="KMeans k=10, 10 Lloyd iterations, rows/sec", value=N * 10 / dt, unit="rows/s", n_gpus=world,
                seconds=dt, rows=N, cols=F, lloyd_ms_per_iteration_end_to_end=round(per_iter * 1e3, 3),
-               iterations=iters, fixed_seconds=round(dt - iters[10] * per_iter, 4)))
+               iterations=iters, fixed_seconds=round(dt - iters[10] * per_iter, 4),
+               collectives_per_lloyd_iteration=round((calls[30] - calls[10]) / max(iters[30] - iters[10], 1), 2)),
+          iterations=iters[30])
 
 
 def main():
@@ -223,13 +249,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    forced = os.environ.get("H2O_FORCE_SHARDED") == "1"
+    if world > 1 or forced:
+        # H2O_FORCE_SHARDED=1 on one GPU: a 1-rank RCCL group; every trainer takes its sharded path and its
+        # collectives run through ProcessGroupNCCL
         import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
     dict(xgb=bench_xgb, dl=bench_dl, glm=bench_glm, glm_big=bench_glm_big, kmeans=bench_kmeans, automl=bench_automl)[a.which](a, dev, world, rank)
-    if world > 1:
+    if world > 1 or forced:
         import torch.distributed as dist
         dist.destroy_process_group()
 

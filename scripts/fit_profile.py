@@ -1,0 +1,66 @@
+"""Where a trainer's fit spends its wall time (GPU box): cProfile of one warm fit of the bench configurations —
+GLM binomial IRLSM 10M x 50, DeepLearning MLP [200, 200] bf16 10M x 784 (batch 4096, 1 epoch).
+usage: python scripts/fit_profile.py --which glm|dl [--rows N] [--cols F] [--top 45]"""
+import argparse
+import cProfile
+import io
+import os
+import pstats
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--which", default="glm", choices=["glm", "dl"])
+    ap.add_argument("--rows", type=int, default=10_000_000)
+    ap.add_argument("--cols", type=int, default=0)
+    ap.add_argument("--top", type=int, default=45)
+    a = ap.parse_args()
+    from llama_github_io_amd.models.base import DataInfo
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(5)
+    N = a.rows
+    if a.which == "glm":
+        from llama_github_io_amd.models.glm import GLMTrainer as Tr
+        F = a.cols or 50
+        X = torch.randn(F, N, device=dev, generator=g)
+        beta = torch.linspace(-1, 1, F, device=dev)
+        y = (torch.rand(N, device=dev, generator=g) < torch.sigmoid((beta[:, None] * X).sum(0) * 0.3)).float()
+        prm = dict(family="binomial", solver="IRLSM", lambda_=0.0, standardize=True)
+        warm = dict(prm, max_iterations=1)
+    else:
+        from llama_github_io_amd.models.deeplearning import DeepLearningTrainer as Tr
+        F = a.cols or 784
+        X = torch.rand(F, N, device=dev, generator=g)
+        y = (X[:20].sum(0) > 10).float()
+        prm = dict(hidden=[200, 200], epochs=1, compute_dtype="bf16", mini_batch_size=4096, seed=1, stopping_rounds=0,
+                   score_interval=1e9, standardize=False)
+        warm = dict(prm)
+    info = DataInfo([f"x{i}" for i in range(F)], np.zeros(F, np.int32), [None] * F, "y", ["0", "1"])
+    Tr(warm).fit(X[:, :100000].contiguous(), y[:100000].contiguous(), None, None, info)
+    for _ in range(2):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        m = Tr(dict(prm)).fit(X, y, None, None, info)
+        torch.cuda.synchronize()
+        print(f"fit {1000 * (time.perf_counter() - t0):.2f} ms phases {m.output.get('phase_seconds')}", flush=True)
+    pr = cProfile.Profile()
+    torch.cuda.synchronize()
+    pr.enable()
+    Tr(dict(prm)).fit(X, y, None, None, info)
+    torch.cuda.synchronize()
+    pr.disable()
+    for key in ("cumulative", "tottime"):
+        s = io.StringIO()
+        pstats.Stats(pr, stream=s).sort_stats(key).print_stats(a.top)
+        print(s.getvalue(), flush=True)
+
+
+if __name__ == "__main__":
+    main()

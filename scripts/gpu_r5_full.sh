@@ -4,7 +4,7 @@ set -o pipefail
 O=gpurun_out/r5/${TAG:-full}
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 1500 python3 -u -m pytest -x -q --timeout 600 --timeout-method thread tests -m gpu > $O/tests.log 2>&1 || { tail -60 $O/tests.log; exit 1; }
+timeout -k 10 840 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread tests -m gpu > $O/tests.log 2>&1 || { tail -60 $O/tests.log; exit 1; }
 tail -3 $O/tests.log
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { cat $O/smoke.log; exit 1; }
 tail -1 $O/smoke.log
