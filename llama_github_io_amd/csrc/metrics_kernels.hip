@@ -1,0 +1,36 @@
+// Binomial metrics score lattice (reference: hex/AUC2.java AUCBuilder — per-threshold-bin positive / negative
+// weights and the bin's score; here a fixed 2^18-bin lattice over [0, 1], metrics._score_hist): ONE pass over the
+// rows does the three per-bin reductions the torch path ran as two weighted bincounts and a scatter_reduce
+// (three passes, 10M-row binomial metrics ~10 ms). Bins are spread over 2^18 addresses, so fp64 global atomics
+// rarely collide; the max score uses the order of non-negative doubles' bit patterns (u64 atomicMax).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+__global__ __launch_bounds__(256) void k_score_hist(const double* __restrict__ p, const double* __restrict__ y,
+                                                    const double* __restrict__ w, long long n, int nb,
+                                                    double* __restrict__ pos, double* __restrict__ neg,
+                                                    unsigned long long* __restrict__ mx) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const double pi = p[i], yi = y[i], wi = w ? w[i] : 1.0;
+    long long b = (long long)(pi * (double)nb);
+    b = b < 0 ? 0 : (b > nb - 1 ? nb - 1 : b);
+    const double wp = wi * yi, wn = wi * (1.0 - yi);
+    if (wp != 0.0) atomicAdd(pos + b, wp);
+    if (wn != 0.0) atomicAdd(neg + b, wn);
+    atomicMax(mx + b, (unsigned long long)__double_as_longlong(fmax(pi, 0.0)));
+  }
+}
+
+extern "C" {
+// pos / neg / mx: [nb] zero-filled by the caller (mx as the bits of +0.0)
+int h2o_score_hist(const void* p, const void* y, const void* w, long long n, int nb, void* pos, void* neg, void* mx,
+                   hipStream_t s) {
+  if (n <= 0) return 0;
+  if (nb <= 0) return (int)hipErrorInvalidValue;
+  long long grid = (n + 255) / 256;
+  if (grid > 4096) grid = 4096;
+  hipLaunchKernelGGL(k_score_hist, dim3((unsigned)grid), dim3(256), 0, s, (const double*)p, (const double*)y,
+                     (const double*)w, n, nb, (double*)pos, (double*)neg, (unsigned long long*)mx);
+  return (int)hipGetLastError();
+}
+}

@@ -10,6 +10,7 @@ python object with H2O's metric names (``auc``, ``aucpr``, ``logloss``, ``mse``,
 from __future__ import annotations
 
 import math
+import os
 
 import numpy as np
 import torch
@@ -39,15 +40,29 @@ def _allreduce(t: torch.Tensor, op=None) -> torch.Tensor:
 SCORE_BINS = 1 << 18
 
 
-def _score_hist(p, pos_w, neg_w, nb: int = SCORE_BINS):
-    """[3, nb] float64 (pos, neg, max score; -inf = empty) of scores p in [0, 1], merged over row shards."""
-    from .ops.segment import segment_sum
-    b = torch.clamp((p * nb).long(), 0, nb - 1)
-    h = torch.empty(3, nb, dtype=torch.float64, device=p.device)
-    h[0] = segment_sum(b, pos_w, nb)
-    h[1] = segment_sum(b, neg_w, nb)
-    h[2] = torch.full((nb,), float("-inf"), dtype=torch.float64, device=p.device).scatter_reduce(
-        0, b, p.double(), reduce="amax", include_self=True)
+def _score_hist(p, pos_w, neg_w, nb: int = SCORE_BINS, y=None, w=None):
+    """[3, nb] float64 (pos, neg, max score; -inf = empty) of scores p in [0, 1], merged over row shards. With
+    y / w given on a GPU: one HIP pass (csrc/metrics_kernels.hip) instead of three torch reductions."""
+    if y is not None and p.is_cuda and os.environ.get("H2O_METRICS_HIP", "1") != "0":
+        from .ops import _native as nat
+        h = torch.zeros(3, nb, dtype=torch.float64, device=p.device)
+        pd, yd = p.double().contiguous(), y.double().contiguous()
+        wd = None if w is None else w.double().contiguous()
+        nat.call("h2o_score_hist", pd.data_ptr(), yd.data_ptr(), 0 if wd is None else wd.data_ptr(), pd.numel(), nb,
+                 h[0].data_ptr(), h[1].data_ptr(), h[2].data_ptr(), nat.stream_ptr(p.device))
+        mx = h[2].view(torch.int64).view(torch.float64)
+        h[2] = torch.where((h[0] + h[1]) > 0, mx, torch.full_like(mx, float("-inf")))
+    else:
+        from .ops.segment import segment_sum
+        if pos_w is None:
+            wd = torch.ones_like(p, dtype=torch.float64) if w is None else w.double()
+            pos_w, neg_w = wd * y, wd * (1 - y)
+        b = torch.clamp((p * nb).long(), 0, nb - 1)
+        h = torch.empty(3, nb, dtype=torch.float64, device=p.device)
+        h[0] = segment_sum(b, pos_w, nb)
+        h[1] = segment_sum(b, neg_w, nb)
+        h[2] = torch.full((nb,), float("-inf"), dtype=torch.float64, device=p.device).scatter_reduce(
+            0, b, p.double(), reduce="amax", include_self=True)
     if _dist():
         from torch.distributed import ReduceOp
         h[:2] = _allreduce(h[:2].contiguous())
@@ -168,7 +183,7 @@ def binomial_metrics(y, p1, w=None, domain=("0", "1"), nbins_thresholds: int = 4
     if sw <= 0:
         sw = float("nan")
     logloss, mse = sll / sw, sse / sw
-    h = _score_hist(p1, w * y, w * (1 - y))
+    h = _score_hist(p1, None, None, y=y, w=w)
     hpos, hneg, huniq = _hist_curve(h)
     if _dist():
         auc, aucpr, _, _ = _auc_from_sorted(hpos, hneg)

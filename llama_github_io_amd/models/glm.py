@@ -723,21 +723,24 @@ class GLMTrainer:
             self.collinear = [ex.names[j] for j in torch.nonzero(fixed[:-1]).flatten().tolist()]
         beta = torch.where(fixed, torch.zeros_like(beta), beta)
         beta_start = beta.clone()
-        # gradient at the null model -> lambda max
-        eta = G.zbeta(Zi, beta, off)
-        mu = fam.linkinv(eta)
-        gvec = fam.dlink(mu)
-        var = fam.variance(mu)
-        grad = -(_gvec(G.xtv(Zi, (w * (y - mu) / (var * gvec)).float())) * obj_reg)
-        if intercept:
-            grad[-1] = 0
-        lmax = float(grad.abs().max()) / max(alpha, 1e-2)
+        lam_in = p["lambda_"]
+        # gradient at the null model -> lambda max: only when a lambda is derived from it (search / default lambda)
+        # or a lambda path's early stopping compares against it — a single given lambda skips its two passes
+        lmax = float("inf")
+        if lam_in is None or (isinstance(lam_in, (list, tuple)) and len(lam_in) > 1):
+            eta = G.zbeta(Zi, beta, off)
+            mu = fam.linkinv(eta)
+            gvec = fam.dlink(mu)
+            var = fam.variance(mu)
+            grad = -(_gvec(G.xtv(Zi, (w * (y - mu) / (var * gvec)).float())) * obj_reg)
+            if intercept:
+                grad[-1] = 0
+            lmax = float(grad.abs().max()) / max(alpha, 1e-2)
         lmr = float(p["lambda_min_ratio"])
         if lmr <= 0:
             lmr = 1e-4 if (nobs >> 4) > (P1 - 1) else 1e-2
             if alpha == 0:
                 lmr *= 1e-2
-        lam_in = p["lambda_"]
         if lam_in is not None:
             lambdas = [float(v) for v in (lam_in if isinstance(lam_in, (list, tuple)) else [lam_in])]
         elif p["lambda_search"]:

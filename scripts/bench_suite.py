@@ -93,19 +93,19 @@ def bench_dl(a, dev, world, rank):
     # untimed warmup fit on a slice: library init / kernel autotuning / graph capture code paths
     cd = a.dtype
     DeepLearningTrainer(dict(hidden=[200, 200], epochs=1, compute_dtype=cd, mini_batch_size=a.batch, seed=1,
-                             stopping_rounds=0, score_interval=1e9, standardize=False)).fit(
+                             stopping_rounds=0, score_interval=1e9, standardize=a.standardize)).fit(
         X[:, :8 * a.batch].contiguous(), y[:8 * a.batch].contiguous(), None, None, info)
     _sync()
     _reset_stats()
     t0 = time.perf_counter()
     m = DeepLearningTrainer(dict(hidden=[200, 200], epochs=a.epochs, compute_dtype=cd, mini_batch_size=a.batch,
-                                 seed=1, stopping_rounds=0, score_interval=1e9, standardize=False)).fit(X, y, None, None, info)
+                                 seed=1, stopping_rounds=0, score_interval=1e9, standardize=a.standardize)).fit(X, y, None, None, info)
     _sync()
     dt = time.perf_counter() - t0
     _emit(dict(metric=f"DeepLearning MLP [200,200] train samples/sec (10M x 784, {cd}, data-parallel)",
                value=N * a.epochs / dt, unit="samples/s", n_gpus=world, seconds=dt, rows=N, cols=F, batch=a.batch,
                train_auc=m.output["training_metrics"]["AUC"], train_logloss=m.output["training_metrics"].get("logloss"),
-               dtype=cd, data="synthetic",
+               standardize=a.standardize, dtype=cd, data="synthetic",
                step_mode=m.output.get("training_step_mode"), explicit=m.output.get("training_step_explicit"),
                fused_mfma=m.output.get("training_step_fused_mfma"),
                phases=m.output.get("phase_seconds")), iterations=m.output.get("averaging_rounds") or len(m.output.get("scoring_history") or []) or None)
@@ -245,6 +245,9 @@ def main():
     ap.add_argument("--epochs", type=float, default=1.0)
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--dtype", default="bf16", help="DeepLearning compute_dtype (bf16 | float32)")
+    ap.add_argument("--no-standardize", dest="standardize", action="store_false",
+                    help="DeepLearning: skip input standardization (H2O's default standardize=True; unstandardized "
+                    "[0, 1] inputs leave the 1-epoch ADADELTA model miscalibrated, profiles/r5_dl_calibration.md)")
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -40,7 +40,7 @@ def main():
         X = torch.rand(F, N, device=dev, generator=g)
         y = (X[:20].sum(0) > 10).float()
         prm = dict(hidden=[200, 200], epochs=1, compute_dtype="bf16", mini_batch_size=4096, seed=1, stopping_rounds=0,
-                   score_interval=1e9, standardize=False)
+                   score_interval=1e9, standardize=True)
         warm = dict(prm)
     info = DataInfo([f"x{i}" for i in range(F)], np.zeros(F, np.int32), [None] * F, "y", ["0", "1"])
     Tr(warm).fit(X[:, :100000].contiguous(), y[:100000].contiguous(), None, None, info)
