@@ -188,7 +188,7 @@ __global__ __launch_bounds__(256) void k_lloyd_mfma(const float* __restrict__ X,
       xq += __shfl_xor(xq, 32, 64);
       const int rrow = tr * 16 + c16;                      // every lane of column c16 holds row rrow's result
       if (q == 0 && rrow < nrows) {
-        assign[r0 + rrow] = bidx;
+        if (assign) assign[r0 + rrow] = bidx;        // (null: the Lloyd loop does not read assignments)
         mind[r0 + rrow] = fmaxf(xq + best, 0.f);
       }
       // ---- 2. centroid GEMM over the 16 rows in 4 steps of 4 rows: A[i = center][k = row 4j+q] (one-hot),
@@ -213,8 +213,33 @@ __global__ __launch_bounds__(256) void k_lloyd_mfma(const float* __restrict__ X,
     }
     __builtin_amdgcn_wave_barrier();   // the slice is rewritten by the next iteration's loads
   }
-  // ---- per-wave slab: [KT*16 centers][PT*16 dims], D layout row = 4q + r (center), col = c16 (dim)
-  float* out = slabs + wave_g * (int64_t)(KT * 16) * (PT * 16);
+  // ---- per-BLOCK slab: [KT*16 centers][PT*16 dims], D layout row = 4q + r (center), col = c16 (dim). The four
+  // waves' accumulators are summed through LDS (the staging slices are free now), so the host-side fp64 reduction
+  // reads one slab per block instead of four (MEASURED r5: the torch slab sum was ~40 us of a 454 us iteration)
+  constexpr int SL = KT * 16 * PT * 16;
+  float* red = lds;                                   // one slab (SL <= the staging slices, see km_stride)
+  for (int src = 1; src < 4; ++src) {
+    __syncthreads();
+    if (wv == src) {
+#pragma unroll
+      for (int t = 0; t < KT; ++t)
+#pragma unroll
+        for (int u = 0; u < PT; ++u)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) red[(t * 16 + 4 * q + r) * (PT * 16) + u * 16 + c16] = acc[t][u][r];
+    }
+    __syncthreads();
+    if (wv == 0) {
+#pragma unroll
+      for (int t = 0; t < KT; ++t)
+#pragma unroll
+        for (int u = 0; u < PT; ++u)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[t][u][r] += red[(t * 16 + 4 * q + r) * (PT * 16) + u * 16 + c16];
+    }
+  }
+  if (wv != 0) return;
+  float* out = slabs + (int64_t)blockIdx.x * SL;
 #pragma unroll
   for (int t = 0; t < KT; ++t)
 #pragma unroll
@@ -232,9 +257,50 @@ int launch(const float* X, long long N, int P, const float* C, int K, const floa
   return (int)hipGetLastError();
 }
 
+// The rest of a Lloyd iteration in one launch (KMeans.java: new centers = sums / counts, empty clusters keep their
+// center for the re-seed, convergence = the largest center move): tot = the fp64 sum of the per-block slabs
+// ([.][ldt], count in column P). Replaces ~6 small torch launches per iteration.
+__global__ __launch_bounds__(256) void k_kmeans_update(const double* __restrict__ tot, int ldt, int K, int P,
+                                                       const float* __restrict__ C, float* __restrict__ newC,
+                                                       double* __restrict__ cnt_out, double* __restrict__ flags) {
+  __shared__ float smax[4];
+  __shared__ int sempty[4];
+  float mx = 0.f;
+  int empty = 0;
+  for (int i = threadIdx.x; i < K * P; i += 256) {
+    const int c = i / P, d = i - c * P;
+    const double cnt = tot[(int64_t)c * ldt + P];
+    const float v = cnt > 0.0 ? (float)(tot[(int64_t)c * ldt + d] / fmax(cnt, 1e-300)) : C[i];
+    newC[i] = v;
+    mx = fmaxf(mx, fabsf(v - C[i]));
+  }
+  for (int c = threadIdx.x; c < K; c += 256) {
+    const double cnt = tot[(int64_t)c * ldt + P];
+    cnt_out[c] = cnt;
+    empty += cnt == 0.0 ? 1 : 0;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    empty += __shfl_xor(empty, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) { smax[threadIdx.x >> 6] = mx; sempty[threadIdx.x >> 6] = empty; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    flags[0] = (double)(sempty[0] + sempty[1] + sempty[2] + sempty[3]);
+    flags[1] = (double)fmaxf(fmaxf(smax[0], smax[1]), fmaxf(smax[2], smax[3]));
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+int h2o_kmeans_update(const double* tot, int ldt, int K, int P, const float* C, float* newC, double* cnt,
+                      double* flags, hipStream_t s) {
+  if (K < 1 || P < 1 || ldt < P + 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_kmeans_update, dim3(1), dim3(256), 0, s, tot, ldt, K, P, C, newC, cnt, flags);
+  return (int)hipGetLastError();
+}
 
 // Shape class the MFMA Lloyd kernel supports (0 = not supported: caller falls back).
 // Returns KT*100 + PS*10... encoded as (KT, PS, PT) via out[3].
@@ -268,7 +334,7 @@ int h2o_kmeans_mfma_grid(int K, int P) {
   return cus * per;
 }
 
-// slabs: [grid*4][KT*16][PT*16] fp32 (caller allocates with the shape from h2o_kmeans_mfma_shape)
+// slabs: [grid][KT*16][PT*16] fp32 (one per block; caller allocates with the shape from h2o_kmeans_mfma_shape)
 int h2o_kmeans_mfma(const float* X, long long N, int P, const float* C, int K, const float* w, int* assign,
                     float* mind, float* slabs, int grid, hipStream_t s) {
   int sh[3];

@@ -988,7 +988,10 @@ __global__ __launch_bounds__(BLK) void k_hist_build(
 // its partials sit at b + n. With hist_next != nullptr (single process) the sibling subtraction is fused:
 // hist_next[n] = sum and hist_next[sib] = hist_cur[parent] - sum (no compact-buffer round trip).
 #define RW 8   // waves per k_hist_reduce block: wave w sums partials b0 + w, b0 + w + RW, ... of 64 columns
-template <typename P, typename TO>
+// COLS (levels of many small nodes, fan-in <= ~32 partials): each wave owns 64 columns of its own and sums ALL the
+// node's partials of them — no LDS combine, 8x fewer blocks. MEASURED r5: the partial-split form launched
+// 225 x 32 blocks at level 5 of the headline tree, 2-3 loads per lane each (14 us for ~36 MB).
+template <typename P, typename TO, bool COLS>
 __global__ __launch_bounds__(RW * 64) void k_hist_reduce(
     const P* __restrict__ partials, int slot_doubles, int used, const Node* __restrict__ nodes,
     const int* __restrict__ bp, const int* __restrict__ meta, int G, TO* __restrict__ out, int ostride,
@@ -1004,7 +1007,7 @@ __global__ __launch_bounds__(RW * 64) void k_hist_reduce(
   const int b0 = t0 / per, b1 = t1 > t0 ? (t1 - 1) / per : b0 - 1;
   const int oslot = nd.parent >= 0 ? nd.parent : 0;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  int i = blockIdx.x * 64 + lane;
+  int i = (COLS ? blockIdx.x * RW + w : blockIdx.x) * 64 + lane;
   if (lo_F > 0) {
     // narrow level: only the entries of columns < lo_F ([bin][lo_F][2] of the [bin][F][2] layout) and the tail
     const int F = (used - 1) / (2 * NBIN + 1), lo2 = 2 * lo_F;
@@ -1016,18 +1019,23 @@ __global__ __launch_bounds__(RW * 64) void k_hist_reduce(
   // 8 independent loads in flight per lane (the root's 256 partials: 4 dependent rounds per wave instead of 8);
   // fixed summation order -> deterministic result
   double a[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-  int b = b0 + w;
-  for (; b + 7 * RW <= b1; b += 8 * RW) {
+  constexpr int ST = COLS ? 1 : RW;     // partial stride of this wave
+  int b = b0 + (COLS ? 0 : w);
+  for (; b + 7 * ST <= b1; b += 8 * ST) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) a[k] += (double)partials[(size_t)(b + k * RW + node) * slot_doubles + ic];
+    for (int k = 0; k < 8; ++k) a[k] += (double)partials[(size_t)(b + k * ST + node) * slot_doubles + ic];
   }
-  for (; b <= b1; b += RW) a[0] += (double)partials[(size_t)(b + node) * slot_doubles + ic];
-  red[w][lane] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
-  __syncthreads();
-  if (w != 0 || i >= used) return;
-  double acc = red[0][lane];
+  for (; b <= b1; b += ST) a[0] += (double)partials[(size_t)(b + node) * slot_doubles + ic];
+  double acc = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+  if (!COLS) {
+    red[w][lane] = acc;
+    __syncthreads();
+    if (w != 0) return;
+    acc = red[0][lane];
 #pragma unroll
-  for (int k = 1; k < RW; ++k) acc += red[k][lane];
+    for (int k = 1; k < RW; ++k) acc += red[k][lane];
+  }
+  if (i >= used) return;
   if (out) out[(size_t)oslot * ostride + i] = (TO)acc;   // the compact build slot (row-sharded: wire dtype)
   if (hist_next) {
     hist_next[(size_t)node * slot_doubles + i] = acc;
@@ -2337,8 +2345,16 @@ static void reduce_launch(const void* partials, int slot_doubles, int used, cons
   const int F = (used - 1) / (2 * NBIN + 1);
   if (lo_F >= F) lo_F = 0;
   const int n = lo_F > 0 ? NBIN * 2 * lo_F + F + 1 : used;
+  // many node slots at this level (>= 16: a built node's rows span <= ~1/8 of the grid): column-wave form
+  if (cap >= 16 && !getenv("H2O_REDUCE_SPLIT")) {
+    const int gx = (n + 64 * RW - 1) / (64 * RW);
+    hipLaunchKernelGGL((k_hist_reduce<P, TO, true>), dim3(gx, cap), dim3(RW * 64), 0, s, (const P*)partials,
+                       slot_doubles, used, (const Node*)nodes, (const int*)bp, (const int*)meta, grid, (TO*)out,
+                       ostride, (double*)hist_next, (const double*)hist_cur, lo_F);
+    return;
+  }
   const int gx = (n + 63) / 64;
-  hipLaunchKernelGGL((k_hist_reduce<P, TO>), dim3(gx, cap), dim3(RW * 64), 0, s, (const P*)partials, slot_doubles,
+  hipLaunchKernelGGL((k_hist_reduce<P, TO, false>), dim3(gx, cap), dim3(RW * 64), 0, s, (const P*)partials, slot_doubles,
                      used, (const Node*)nodes, (const int*)bp, (const int*)meta, grid, (TO*)out, ostride,
                      (double*)hist_next, (const double*)hist_cur, lo_F);
 }

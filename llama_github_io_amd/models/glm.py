@@ -336,8 +336,10 @@ class GLMModel(Model):
         return eta
 
     def _predict_tensor(self, X, offset=None):
+        return self._from_eta(self._eta(X, offset))
+
+    def _from_eta(self, eta):
         fam = self.output["family"]
-        eta = self._eta(X, offset)
         if fam == "multinomial":
             return torch.softmax(eta, 1).float()
         if fam == "ordinal":
@@ -1109,7 +1111,12 @@ class GLMTrainer:
         out["standardized_coefficients"] = coefs_std
         out["coefficients_table"] = [dict(names=n, coefficients=coefs[n], standardized_coefficients=coefs_std.get(n))
                                      for n in coefs]
-        P = model._predict_tensor(X, offset)
+        if fam not in ("multinomial", "ordinal") and K == 1 and getattr(model, "hglm", None) is None:
+            # training predictions from the training design (it already holds the intercept column): no second
+            # expander transform of X
+            P = model._from_eta(G.zbeta(Zi, beta[0].to(Zi.device), off)[:, None])
+        else:
+            P = model._predict_tensor(X, offset)
         cat = model.model_category
         yv = y.float()
         ok = w > 0

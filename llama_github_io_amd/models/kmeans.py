@@ -16,7 +16,7 @@ import numpy as np
 import torch
 
 from .. import metrics as mm
-from ..ops.dense import kmeans_assign, kmeans_step
+from ..ops.dense import kmeans_assign, kmeans_lloyd_step, kmeans_step
 from ..parallel import collectives as coll
 from .base import DataInfo, Model, make_key
 from .datainfo import Expander
@@ -226,7 +226,12 @@ class KMeansTrainer:
 
     def _step(self, Z, w, C):
         """One Lloyd step on the device: (assign, min distance, new centers, cnt, flags [#empty, shift])."""
-        a, d, sums, cnt = kmeans_step(Z, C, w)
+        if not coll.is_dist():
+            r = kmeans_lloyd_step(Z, C, w)      # MFMA step + fused center update (2 launches + the slab sum)
+            if r is not None:
+                d, newC, cnt, flags = r
+                return None, d, newC, cnt, flags
+        a, d, sums, cnt = kmeans_step(Z, C, w, need_assign=False)
         if coll.is_dist():
             sums = coll.all_reduce_(sums)
             cnt = coll.all_reduce_(cnt)

@@ -59,6 +59,7 @@ _HIP_SIGS = {
     "h2o_kmeans_mfma_shape": [c_int, c_int, c_void_p],
     "h2o_kmeans_mfma_grid": [c_int, c_int],
     "h2o_kmeans_mfma": [c_void_p, c_ll, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p],
+    "h2o_kmeans_update": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "h2o_qscale": [c_void_p, c_void_p, c_void_p, c_ll, c_int, c_void_p],
     "h2o_score_hist": [c_void_p, c_void_p, c_void_p, c_ll, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "h2o_hist_reduce": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,

@@ -230,8 +230,13 @@ def _mfma_shape(K, P):
     return (out[0], out[1], out[2]) if ok else None
 
 
-def kmeans_step(X: torch.Tensor, C: torch.Tensor, w: torch.Tensor | None = None):
+_KM_GRID: dict = {}     # (K, P) -> blocks of one resident round of the MFMA Lloyd kernel (occupancy query, cached)
+
+
+def kmeans_step(X: torch.Tensor, C: torch.Tensor, w: torch.Tensor | None = None, need_assign: bool = True):
     """One Lloyd step: (assign [N], min sq. distance [N], per-center weighted sums [K, P] fp64, counts [K]).
+    ``need_assign=False`` (the Lloyd loop, which reads only distances, sums and counts): the MFMA kernel does not
+    store assignments and None is returned in their place.
     On the GPU: ``csrc/kmeans_mfma.hip`` (distance GEMM + argmin + one-hot centroid GEMM on f32 MFMA,
     one pass over X) for K, P <= 64 with P % 4 == 0 (KMeans pads its design matrix); the LDS scalar
     kernel otherwise."""
@@ -243,15 +248,18 @@ def kmeans_step(X: torch.Tensor, C: torch.Tensor, w: torch.Tensor | None = None)
         X = X.contiguous().float()
         C = C.contiguous().float()
         wf = None if w is None else w.contiguous().float()
-        a = torch.empty(N, dtype=torch.int32, device=X.device)
+        a = torch.empty(N, dtype=torch.int32, device=X.device) if need_assign else None
         d = torch.empty(N, dtype=torch.float32, device=X.device)
-        full = int(nat.hip().h2o_kmeans_mfma_grid(int(K), int(P))) or 1024   # one resident round of blocks
+        key = (int(K), int(P))
+        full = _KM_GRID.get(key)
+        if full is None:
+            full = _KM_GRID[key] = int(nat.hip().h2o_kmeans_mfma_grid(*key)) or 1024   # one resident round
         grid = int(max(1, min(full, (N + 63) // 64)))
-        slab = torch.empty(grid * 4, KT * 16, PT * 16, dtype=torch.float32, device=X.device)
+        slab = torch.empty(grid, KT * 16, PT * 16, dtype=torch.float32, device=X.device)   # one per block
         nat.call("h2o_kmeans_mfma", X.data_ptr(), N, P, C.data_ptr(), K, 0 if wf is None else wf.data_ptr(),
-                 a.data_ptr(), d.data_ptr(), slab.data_ptr(), grid, nat.stream_ptr(X.device))
+                 0 if a is None else a.data_ptr(), d.data_ptr(), slab.data_ptr(), grid, nat.stream_ptr(X.device))
         tot = slab.sum(0, dtype=torch.float64)
-        return a.long(), d, tot[:K, :P].contiguous(), tot[:K, P].contiguous()
+        return (a.long() if a is not None else None), d, tot[:K, :P].contiguous(), tot[:K, P].contiguous()
     if X.is_cuda and (K * P + 256 * (P + 1) + 512) * 4 <= 160 * 1024 and N > 0 and K * (P + 1) <= 8192:
         X = X.contiguous().float()
         C = C.contiguous().float()
@@ -275,6 +283,38 @@ def kmeans_step(X: torch.Tensor, C: torch.Tensor, w: torch.Tensor | None = None)
     ends = torch.cumsum(nrows, 0)
     sums = cs[ends] - cs[ends - nrows]
     return a, d, sums, cnt
+
+
+def kmeans_lloyd_step(X: torch.Tensor, C: torch.Tensor, w: torch.Tensor | None = None):
+    """One single-process Lloyd iteration on the MFMA kernel plus the fused center update (k_kmeans_update):
+    (min sq. distance [N], new centers [K, P] f32, counts [K] f64, flags [#empty, max shift] f64) — or None where the
+    MFMA shape does not apply (the caller runs kmeans_step + its torch update)."""
+    N, P = X.shape
+    K = C.shape[0]
+    sh = _mfma_shape(K, P) if X.is_cuda and N > 0 and P % 4 == 0 else None
+    if sh is None or os.environ.get("H2O_KMEANS_MFMA", "1") != "1":
+        return None
+    KT, PS, PT = sh
+    X = X.contiguous().float()
+    Cf = C.contiguous().float()
+    wf = None if w is None else w.contiguous().float()
+    d = torch.empty(N, dtype=torch.float32, device=X.device)
+    key = (int(K), int(P))
+    full = _KM_GRID.get(key)
+    if full is None:
+        full = _KM_GRID[key] = int(nat.hip().h2o_kmeans_mfma_grid(*key)) or 1024
+    grid = int(max(1, min(full, (N + 63) // 64)))
+    slab = torch.empty(grid, KT * 16, PT * 16, dtype=torch.float32, device=X.device)
+    s = nat.stream_ptr(X.device)
+    nat.call("h2o_kmeans_mfma", X.data_ptr(), N, P, Cf.data_ptr(), K, 0 if wf is None else wf.data_ptr(), 0,
+             d.data_ptr(), slab.data_ptr(), grid, s)
+    tot = slab.sum(0, dtype=torch.float64)
+    newC = torch.empty(K, P, dtype=torch.float32, device=X.device)
+    cnt = torch.empty(K, dtype=torch.float64, device=X.device)
+    flags = torch.empty(2, dtype=torch.float64, device=X.device)
+    nat.call("h2o_kmeans_update", tot.data_ptr(), PT * 16, K, P, Cf.data_ptr(), newC.data_ptr(), cnt.data_ptr(),
+             flags.data_ptr(), s)
+    return d, newC, cnt, flags
 
 
 def kmeans_assign(X: torch.Tensor, C: torch.Tensor):

@@ -189,3 +189,19 @@ def test_lattice_threshold_table_tracks_exact_scores(binom):
     assert abs(m["max_f1_threshold"] - float(ps[last][f1.argmax()])) < 0.02
     # every reported threshold is an observed score
     assert all(np.any(np.isclose(p, r["threshold"], rtol=0, atol=1e-12)) for r in m["thresholds_and_metric_scores"])
+
+
+def test_lattice_auc_for_large_frames_is_close_to_exact(monkeypatch):
+    """Frames of >= LATTICE_AUC_ROWS rows take AUC from the 2^18-bin score lattice (no full sort)."""
+    import numpy as np
+    import sklearn.metrics as skm
+    import torch
+    from llama_github_io_amd import metrics as M
+    rng = np.random.default_rng(3)
+    n = 200_000
+    p = rng.random(n)
+    y = (rng.random(n) < p).astype(np.float64)
+    monkeypatch.setattr(M, "LATTICE_AUC_ROWS", 1000)
+    m = M.binomial_metrics(torch.tensor(y), torch.tensor(p))
+    assert abs(m["AUC"] - skm.roc_auc_score(y, p)) < 1e-5
+    assert abs(m["pr_auc"] - skm.average_precision_score(y, p)) < 2e-3
