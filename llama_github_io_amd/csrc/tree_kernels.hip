@@ -1785,17 +1785,15 @@ __device__ __forceinline__ int row_byte4(uint4 v0, uint4 v1, uint4 v2, uint4 v3,
 }
 
 template <int NV>
-__global__ __launch_bounds__(LW * 64) void k_route(
+__device__ __forceinline__ void route_tile(
     const uint8_t* __restrict__ sbins, const float* __restrict__ say, const float* __restrict__ saw,
     uint8_t* __restrict__ dbins, float* __restrict__ day, float* __restrict__ daw, int stride,
     const Node* __restrict__ nodesA, const int* __restrict__ tpA, const int* __restrict__ metaA,
     const Dec* __restrict__ decA, const int* __restrict__ clA, const int* __restrict__ crA,
     const Dec* __restrict__ decB, const int* __restrict__ clB, const int* __restrict__ crB,
     int4* __restrict__ curs, long long N, int planar, uint8_t* __restrict__ lvl2,
-    const uint8_t* __restrict__ fdir /*root route: per row the root split's direction (k_row_dir), or null*/) {
-  const int n_nodes = metaA[0], n_tiles = metaA[1];
-  const int t = blockIdx.x;
-  if (t >= n_tiles) return;
+    const uint8_t* __restrict__ fdir, int t) {
+  const int n_nodes = metaA[0];
   __shared__ Dec sA, sB[2];
   __shared__ int sC[2], sG[4], sBase[4], sL[4];
   __shared__ int sCnt[LW][4];
@@ -1937,6 +1935,59 @@ __global__ __launch_bounds__(LW * 64) void k_route(
     day[pos] = ry[u];
     if (daw) daw[pos] = rw[u];
   }
+}
+
+// k_ranges work folded into the route's LAST block (ro.done != null): every block counts itself out on ro.done
+// after its cursor atomics have returned (it used their results), so the block that draws the final ticket sees the
+// final cursors. The cursors are read back with agent-scope atomic loads (they were only ever updated by atomics at
+// the coherence point; no fence / L2 write-back is needed), the node list and prefixes are written with plain
+// stores that the next kernel reads. Saves one launch per route (MEASURED r5: k_ranges 4.6 us, 2 per tree).
+struct RangesOut {
+  Node* next;
+  int* tp;
+  int* bp;
+  int* meta;
+  int* done;     // zero before the launch; the last block resets it
+};
+template <int NV>
+__global__ __launch_bounds__(LW * 64) void k_route(
+    const uint8_t* __restrict__ sbins, const float* __restrict__ say, const float* __restrict__ saw,
+    uint8_t* __restrict__ dbins, float* __restrict__ day, float* __restrict__ daw, int stride,
+    const Node* __restrict__ nodesA, const int* __restrict__ tpA, const int* __restrict__ metaA,
+    const Dec* __restrict__ decA, const int* __restrict__ clA, const int* __restrict__ crA,
+    const Dec* __restrict__ decB, const int* __restrict__ clB, const int* __restrict__ crB,
+    int4* __restrict__ curs, long long N, int planar, uint8_t* __restrict__ lvl2,
+    const uint8_t* __restrict__ fdir /*root route: per row the root split's direction (k_row_dir), or null*/,
+    RangesOut ro) {
+  const int t = blockIdx.x;
+  if (t < metaA[1])
+    route_tile<NV>(sbins, say, saw, dbins, day, daw, stride, nodesA, tpA, metaA, decA, clA, crA, decB, clB, crB, curs,
+                   N, planar, lvl2, fdir, t);
+  if (!ro.done) return;
+  __shared__ int s_last;
+  __shared__ int sh[17];
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = atomicAdd(ro.done, 1) == (int)gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  const int nn = ro.meta[0];
+  for (int i = threadIdx.x; i < nn; i += blockDim.x) {
+    Node nd = ro.next[i];
+    int* cp = (int*)(curs + nd.parent);
+    if (nd.dir == 0) {
+      const int z = __hip_atomic_load(cp + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      nd.start = z;
+      nd.len = __hip_atomic_load(cp + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - z;
+    } else {
+      const int y = __hip_atomic_load(cp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      nd.start = y;
+      nd.len = __hip_atomic_load(cp + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - y;
+    }
+    ro.next[i] = nd;
+  }
+  __syncthreads();
+  level_tile_prefix(ro.next, nn, ro.tp, ro.bp, ro.meta, sh);
+  if (threadIdx.x == 0) atomicExch(ro.done, 0);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2530,10 +2581,11 @@ static int nv_of(int stride) {
 // column; split bytes of columns past them (the decisions of the levels above) are read from the source
 // lvl2 (nullable; the root route only): per ORIGINAL row its level-2 node, or 128 + its leaf (k_leaf_assign
 // starts there)
-int h2o_route(const void* sbins, const void* say, const void* saw, void* dbins, void* day, void* daw, int stride,
-              const void* nodesA, const void* tpA, const void* metaA, const void* decA, const void* clA,
-              const void* crA, const void* decB, const void* clB, const void* crB, void* curs, int tiles_cap,
-              long long N, int planar, int lp, void* lvl2, const void* fdir, hipStream_t s) {
+static int route_launch(const void* sbins, const void* say, const void* saw, void* dbins, void* day, void* daw,
+                        int stride, const void* nodesA, const void* tpA, const void* metaA, const void* decA,
+                        const void* clA, const void* crA, const void* decB, const void* clB, const void* crB,
+                        void* curs, int tiles_cap, long long N, int planar, int lp, void* lvl2, const void* fdir,
+                        RangesOut ro, hipStream_t s) {
   if (planar && (stride % 32 != 0 || stride < 64)) return (int)hipErrorInvalidValue;
   if (lp < 0 || lp > 2 || (lp > 0 && !planar)) return (int)hipErrorInvalidValue;
 #define ROUTE_LAUNCH(NV)                                                                                       \
@@ -2541,7 +2593,7 @@ int h2o_route(const void* sbins, const void* say, const void* saw, void* dbins, 
                      (const float*)say, (const float*)saw, (uint8_t*)dbins, (float*)day, (float*)daw, stride,  \
                      (const Node*)nodesA, (const int*)tpA, (const int*)metaA, (const Dec*)decA, (const int*)clA, \
                      (const int*)crA, (const Dec*)decB, (const int*)clB, (const int*)crB, (int4*)curs, N, planar, \
-                     (uint8_t*)lvl2, (const uint8_t*)fdir)
+                     (uint8_t*)lvl2, (const uint8_t*)fdir, ro)
   switch (lp == 1 ? 2 : lp == 2 ? 4 : nv_of(stride)) {
     case 4: ROUTE_LAUNCH(4); break;
     case 3: ROUTE_LAUNCH(3); break;
@@ -2551,6 +2603,15 @@ int h2o_route(const void* sbins, const void* say, const void* saw, void* dbins, 
   }
 #undef ROUTE_LAUNCH
   return (int)hipGetLastError();
+}
+
+int h2o_route(const void* sbins, const void* say, const void* saw, void* dbins, void* day, void* daw, int stride,
+              const void* nodesA, const void* tpA, const void* metaA, const void* decA, const void* clA,
+              const void* crA, const void* decB, const void* clB, const void* crB, void* curs, int tiles_cap,
+              long long N, int planar, int lp, void* lvl2, const void* fdir, hipStream_t s) {
+  return route_launch(sbins, say, saw, dbins, day, daw, stride, nodesA, tpA, metaA, decA, clA, crA, decB, clB, crB,
+                      curs, tiles_cap, N, planar, lp, lvl2, fdir, RangesOut{nullptr, nullptr, nullptr, nullptr, nullptr},
+                      s);
 }
 
 // leaf id of every row (original order) + fixed-point leaf sums -> fp64 leafsum[leaf_cap][2]
@@ -2723,17 +2784,27 @@ static inline void* tp_lvl2(const TreePlan* P) {
   return (P->lvl2 && P->planar && P->D > 2 && tp_fcut(P, 2) > 0 && tp_fcut(P, 2) <= FTILE) ? P->lvl2 : nullptr;
 }
 
-static int tp_route(const TreePlan* P, int e, hipStream_t s) {
+// fused: the route's last block also turns the final cursors into level e+2's ranges and tile prefixes (k_ranges)
+static bool route_fused_ranges() {
+  static int v = -1;
+  if (v < 0) { const char* e = getenv("H2O_ROUTE_RANGES"); v = (e && e[0] == '0') ? 0 : 1; }
+  return v == 1;
+}
+
+static int tp_route(const TreePlan* P, int e, hipStream_t s, bool ranges) {
   const void *sb, *sy, *sw;
   tp_level_buf(P, e, sb, sy, sw);
   const int di = (e / 2) % 2;
   // rows of level e + 2 (and below) are read by narrow levels only: move just the low planes
   const int np = tp_planes(tp_fcut(P, e + 2));
   const int lp = (P->planar && np <= 2) ? np : 0;
-  return h2o_route(sb, sy, sw, P->bb[di], P->by[di], P->unit ? nullptr : P->bw[di], P->stride, P->nodes[e], P->tp[e],
-                   P->meta[e], P->dec[e], P->cl[e], P->cr[e], P->dec[e + 1], P->cl[e + 1], P->cr[e + 1],
-                   P->cur[e + 1], P->tiles_cap[e], P->N, P->planar, lp, e == 0 ? tp_lvl2(P) : nullptr,
-                   (e == 0 && tp_lvl2(P) && P->fdir) ? P->fdir : nullptr, s);
+  const RangesOut ro = ranges ? RangesOut{(Node*)P->nodes[e + 2], (int*)P->tp[e + 2], (int*)P->bp[e + 2],
+                                          (int*)P->meta[e + 2], (int*)P->counters + 1}
+                              : RangesOut{nullptr, nullptr, nullptr, nullptr, nullptr};
+  return route_launch(sb, sy, sw, P->bb[di], P->by[di], P->unit ? nullptr : P->bw[di], P->stride, P->nodes[e], P->tp[e],
+                      P->meta[e], P->dec[e], P->cl[e], P->cr[e], P->dec[e + 1], P->cl[e + 1], P->cr[e + 1],
+                      P->cur[e + 1], P->tiles_cap[e], P->N, P->planar, lp, e == 0 ? tp_lvl2(P) : nullptr,
+                      (e == 0 && tp_lvl2(P) && P->fdir) ? P->fdir : nullptr, ro, s);
 }
 
 #define TP_CHECK(x) do { int rc_ = (x); if (rc_) return rc_; } while (0)
@@ -2838,10 +2909,13 @@ int h2o_tree_grow(const TreePlan* P, int d, int dist, hipStream_t s) {
                         P->nbins_f, P->fine_f, tp_planes(tp_fcut(P, d + 1)), fdir, s);
   } else {
     // regroup level d-1's rows two levels down, then histogram level d+1 (even) contiguously
-    rc = tp_route(P, d - 1, s);
+    const bool fused = route_fused_ranges() && P->tiles_cap[d - 1] > 0;
+    rc = tp_route(P, d - 1, s, fused);
     if (rc) return -rc;
-    rc = h2o_ranges(P->nodes[d + 1], P->cur[d], P->tp[d + 1], P->bp[d + 1], P->meta[d + 1], s);
-    if (rc) return -rc;
+    if (!fused) {
+      rc = h2o_ranges(P->nodes[d + 1], P->cur[d], P->tp[d + 1], P->bp[d + 1], P->meta[d + 1], s);
+      if (rc) return -rc;
+    }
     gh = P->tiles_cap[d + 1] < P->grid ? P->tiles_cap[d + 1] : P->grid;
     tp_level_buf(P, d + 1, sb, sy, sw);
     rc = h2o_hist_build(sb, P->stride, sw, sy, P->nodes[d + 1], P->bp[d + 1], P->meta[d + 1], P->F, P->partials,

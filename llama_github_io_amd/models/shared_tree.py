@@ -404,8 +404,9 @@ class SharedTreeTrainer:
                 np.add.at(gains, fe[m] if vm is None else vm[fe[m]], np.maximum(d["gain"][m], 0.0))
 
     def _summary(self, forest: Forest, built):
-        depths = [t.depth() for t in forest.trees] or [0]
-        leaves = [t.n_leaves() for t in forest.trees] or [0]
+        dl = forest.depth_leaves()
+        depths = [d for d, _ in dl] or [0]
+        leaves = [n for _, n in dl] or [0]
         return dict(number_of_trees=built, number_of_internal_trees=len(forest), min_depth=int(min(depths)),
                     max_depth=int(max(depths)), mean_depth=float(np.mean(depths)), min_leaves=int(min(leaves)),
                     max_leaves=int(max(leaves)), mean_leaves=float(np.mean(leaves)))

@@ -134,14 +134,42 @@ def fit_binning(X: torch.Tensor, iscat, nlevels=None, max_bins: int = MAX_DATA_B
         Xn = Xs[num_cols].float()
         Xn = torch.where(torch.isnan(Xn), torch.full_like(Xn, float("inf")), Xn)
         srt, _ = torch.sort(Xn, dim=1)
-        nfin = torch.isfinite(srt).sum(1).cpu().numpy()
         M = srt.shape[1]
-        # distinct-value counts of every feature in one pass (sorted rows: count value changes)
+        # distinct-value counts of every feature in one pass (sorted rows: count value changes); finite counts,
+        # distinct counts and the first value of every feature reach the host in ONE copy
+        fin = torch.isfinite(srt)
         if M > 1:
-            chg = (srt[:, 1:] != srt[:, :-1]) & torch.isfinite(srt[:, 1:])
-            ndist = (chg.sum(1) + torch.isfinite(srt[:, 0]).long()).cpu().numpy()
+            chg = (srt[:, 1:] != srt[:, :-1]) & fin[:, 1:]
+            stats = torch.stack([fin.sum(1).double(), (chg.sum(1) + fin[:, 0].long()).double(), srt[:, 0].double()], 1)
         else:
-            ndist = nfin.copy()
+            chg = None
+            stats = torch.stack([fin.sum(1).double(), fin.sum(1).double(), srt[:, 0].double()], 1)
+        stats = stats.cpu().numpy()
+        nfin, ndist, first = stats[:, 0].astype(np.int64), stats[:, 1].astype(np.int64), stats[:, 2]
+        # every numeric feature's edges in two batched gathers (one host copy each) instead of a gather + copy per
+        # feature (MEASURED r5: the per-feature loop was ~60 host syncs, ~10 ms of a 100-tree GBM job)
+        pre_edges = {}
+        kq = [k for k in range(len(num_cols)) if nfin[k] > 0 and ndist[k] > max_bins]
+        if kq:
+            q = (np.arange(1, max_bins, dtype=np.int64)[None, :] * nfin[kq][:, None]) // max_bins
+            vals = srt[torch.as_tensor(kq, device=srt.device)].gather(
+                1, torch.as_tensor(q, device=srt.device)).float().cpu().numpy()
+            for r, k in enumerate(kq):
+                e = np.unique(vals[r])
+                pre_edges[k] = np.ascontiguousarray(e[e > np.float32(first[k])], dtype=np.float32)
+        kd = [k for k in range(len(num_cols)) if 0 < nfin[k] and ndist[k] <= max_bins and np.isfinite(first[k])]
+        if kd and chg is not None:
+            sub = chg[torch.as_tensor(kd, device=srt.device)]
+            rc = torch.nonzero(sub)                                  # (row of kd, position - 1), row-major order
+            vals = srt[torch.as_tensor(kd, device=srt.device)][rc[:, 0], rc[:, 1] + 1].float()
+            both = torch.cat([rc[:, 0].float()[:, None], vals[:, None]], 1).cpu().numpy() if rc.numel() else \
+                np.zeros((0, 2), dtype=np.float32)
+            rows = both[:, 0].astype(np.int64)
+            for r, k in enumerate(kd):
+                pre_edges[k] = np.ascontiguousarray(both[rows == r, 1], dtype=np.float32)
+        elif kd:
+            for k in kd:
+                pre_edges[k] = np.zeros(0, dtype=np.float32)
     for f in range(F):
         if iscat[f]:
             nl = int(nlevels[f]) if nlevels[f] > 0 else int(torch.nan_to_num(X[f], nan=-1).max().item()) + 1
@@ -165,14 +193,17 @@ def fit_binning(X: torch.Tensor, iscat, nlevels=None, max_bins: int = MAX_DATA_B
         if n == 0:
             edges.append(np.zeros(0, dtype=np.float32)); nbins[f] = 1
             continue
-        row = srt[k, :n]
-        if int(ndist[k]) <= max_bins:
-            e = torch.unique_consecutive(row)[1:]
+        if k in pre_edges:
+            e = pre_edges[k]
         else:
-            q = (torch.arange(1, max_bins, device=row.device, dtype=torch.int64) * n) // max_bins
-            e = torch.unique_consecutive(row[q])
-            e = e[e > row[0]]  # first bin must be non-empty
-        e = e.float().cpu().numpy()
+            row = srt[k, :n]
+            if int(ndist[k]) <= max_bins:
+                e = torch.unique_consecutive(row)[1:]
+            else:
+                q = (torch.arange(1, max_bins, device=row.device, dtype=torch.int64) * n) // max_bins
+                e = torch.unique_consecutive(row[q])
+                e = e[e > row[0]]  # first bin must be non-empty
+            e = e.float().cpu().numpy()
         edges.append(e)
         nbins[f] = e.size + 1
     vmap = None

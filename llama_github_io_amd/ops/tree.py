@@ -644,8 +644,9 @@ class GpuTreeBuilder:
         grid = self.grid
         # fp32 per-block partial histograms (half the flush + reduce bytes; the reduce sums in fp64)
         # MEASURED (scripts/gpu_small_shard_sweep.sh): 0.511 -> 0.492 ms/tree at 1.375M rows and 0.718 -> 0.707
-        # at 2.75M (the per-rank shards of an 8/4-GPU HIGGS run); no gain at 11M. Small test shards keep fp64.
-        self.pf32 = int(os.environ.get("H2O_PARTIAL_F32", "1" if 1_000_000 <= self.N <= 4_000_000 else "0"))
+        # at 2.75M (the per-rank shards of an 8/4-GPU HIGGS run); r5, after the vectorized flush, also at 11M:
+        # 1.262-1.268 -> 1.244-1.253 ms/tree, same trees (scripts/gpu_r5_c13.sh). Small test shards keep fp64.
+        self.pf32 = int(os.environ.get("H2O_PARTIAL_F32", "1" if self.N >= 1_000_000 else "0"))
         self.master = bins
         N, T = self.N, self.TILE
         self.caps = [min(1 << d, node_cap) for d in range(D)] + [1]

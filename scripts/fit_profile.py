@@ -17,7 +17,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--which", default="glm", choices=["glm", "dl"])
+    ap.add_argument("--which", default="glm", choices=["glm", "dl", "gbm"])
     ap.add_argument("--rows", type=int, default=10_000_000)
     ap.add_argument("--cols", type=int, default=0)
     ap.add_argument("--top", type=int, default=45)
@@ -34,6 +34,16 @@ def main():
         y = (torch.rand(N, device=dev, generator=g) < torch.sigmoid((beta[:, None] * X).sum(0) * 0.3)).float()
         prm = dict(family="binomial", solver="IRLSM", lambda_=0.0, standardize=True)
         warm = dict(prm, max_iterations=1)
+    elif a.which == "gbm":
+        # the bench's 100-tree job (binning, 100 trees, training metrics) on the HIGGS shape
+        import bench
+        from llama_github_io_amd.models.gbm import GBMTrainer as Tr
+        N = a.rows if a.rows != 10_000_000 else 11_000_000
+        X, y = bench.make_higgs_like(N, 1234, dev)
+        F = X.shape[0]
+        prm = dict(ntrees=100, max_depth=6, min_rows=10, learn_rate=0.1, seed=42, distribution="bernoulli",
+                   histogram_type="QuantilesGlobal")
+        warm = dict(prm, ntrees=5)
     else:
         from llama_github_io_amd.models.deeplearning import DeepLearningTrainer as Tr
         F = a.cols or 784
@@ -43,7 +53,10 @@ def main():
                    score_interval=1e9, standardize=True)
         warm = dict(prm)
     info = DataInfo([f"x{i}" for i in range(F)], np.zeros(F, np.int32), [None] * F, "y", ["0", "1"])
-    Tr(warm).fit(X[:, :100000].contiguous(), y[:100000].contiguous(), None, None, info)
+    if a.which == "gbm":
+        Tr(warm).fit(X, y, None, None, info)
+    else:
+        Tr(warm).fit(X[:, :100000].contiguous(), y[:100000].contiguous(), None, None, info)
     for _ in range(2):
         torch.cuda.synchronize()
         t0 = time.perf_counter()

@@ -791,3 +791,21 @@ def test_gpu_no_na_bins_match_reference():
         assert np.array_equal(dr["feat"], dg["feat"]) and np.array_equal(dr["bin"], dg["bin"])
         np.testing.assert_allclose(dr["wl"], dg["wl"], rtol=1e-9)
     assert torch.equal(ref.leaf_of_row, gb.leaf_of_row.cpu())
+
+
+def test_forest_depth_leaves_from_level_records_match_decoded_trees():
+    """Forest.depth_leaves() reads pending trees from their level records (no flattening): same (depth, leaves)
+    as the decoded node tables."""
+    from llama_github_io_amd.ops.forest import Forest
+    X, y, info = _data(N=20_000, F=6, cat=True, seed=5)
+    b = fit_binning(X, info.iscat, info.nlevels, max_bins=64)
+    bins = apply_binning(b, X)
+    g = y - y.mean()
+    aux = torch.stack([torch.ones_like(y), g, g, torch.ones_like(y)], 1).contiguous()
+    fr = Forest()
+    for depth, mw in ((6, 10), (3, 10), (5, 4000)):
+        ref = T.RefTreeBuilder(bins, X.shape[0], b.nbins, b.iscat, None, depth, T.SplitParams(min_w=mw))
+        ref.build(aux, leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1]).float())
+        fr.add_levels(ref.pop_levels()[0], b)
+    a = fr.depth_leaves()
+    assert a == [(t.depth(), t.n_leaves()) for t in fr.trees]
