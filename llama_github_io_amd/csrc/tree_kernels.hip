@@ -1063,7 +1063,7 @@ __device__ __forceinline__ double add_mul_rn(double a, double x, double y) {
 }
 
 // k_split_find: best split point per (node, feature). grid = (C, F), block 256 (thread = bin).
-__global__ __launch_bounds__(256) void k_split_find(
+__device__ __forceinline__ void split_find_body(
     double* __restrict__ hist, int slot_doubles, const int* __restrict__ meta, int F,
     const int* __restrict__ nbins_f, const int* __restrict__ iscat_f, const int* __restrict__ mono_f,
     SplitParams p, int level, Cand* __restrict__ cand, double* __restrict__ root_w,
@@ -1565,7 +1565,7 @@ __device__ void level_tile_prefix(const Node* __restrict__ next, int nn, int* __
 //   odd node's region of the next buffer from both ends; this kernel sets up those cursors
 //   (curs[c] = {front, back, region start, region end}, from the parent's left count prev_nl) and
 //   k_ranges turns the final cursors into ranges + tile prefix.
-__global__ __launch_bounds__(1024) void k_plan(
+__device__ void plan_body(
     const Node* __restrict__ nodes, const int* __restrict__ meta, Dec* __restrict__ dec,
     int* __restrict__ node_nl, const int* __restrict__ prev_nl, int4* __restrict__ curs,
     int* __restrict__ child_l, int* __restrict__ child_r,
@@ -1674,6 +1674,73 @@ __global__ __launch_bounds__(1024) void k_plan(
   } else if (tid == 0) {
     next_meta[0] = nn; next_meta[1] = 0; next_meta[2] = 0;
   }
+}
+
+__global__ __launch_bounds__(1024) void k_plan(
+    const Node* __restrict__ nodes, const int* __restrict__ meta, Dec* __restrict__ dec,
+    int* __restrict__ node_nl, const int* __restrict__ prev_nl, int4* __restrict__ curs,
+    int* __restrict__ child_l, int* __restrict__ child_r,
+    Node* __restrict__ next, int* __restrict__ next_tile_prefix, int* __restrict__ next_meta,
+    int* __restrict__ next_build_prefix, int* __restrict__ counters, int* __restrict__ scratch,
+    int depth, int max_depth, double min_w, int cap_next, int leaf_cap, PlanReduce pr) {
+  plan_body(nodes, meta, dec, node_nl, prev_nl, curs, child_l, child_r, next, next_tile_prefix, next_meta,
+            next_build_prefix, counters, scratch, depth, max_depth, min_w, cap_next, leaf_cap, pr);
+}
+
+__global__ __launch_bounds__(256) void k_split_find(
+    double* __restrict__ hist, int slot_doubles, const int* __restrict__ meta, int F,
+    const int* __restrict__ nbins_f, const int* __restrict__ iscat_f, const int* __restrict__ mono_f,
+    SplitParams p, int level, Cand* __restrict__ cand, double* __restrict__ root_w,
+    const float* __restrict__ edges, int adapt_nb, int f0, int FL, Derive dv) {
+  split_find_body(hist, slot_doubles, meta, F, nbins_f, iscat_f, mono_f, p, level, cand, root_w, edges, adapt_nb, f0,
+                  FL, dv);
+}
+
+// k_split_find with the level's k_plan folded into its LAST block (single process, <= PLAN_REDUCE_MAX nodes): every
+// (node, feature) block publishes its candidate with an agent-scope RELEASE ticket on `done`; the block drawing the
+// final ticket acquires (L2 invalidate) and runs the plan — reduce_node over the candidates, child numbering, the
+// next level's node list and tile prefixes — with its 256 threads. One launch per level instead of two.
+struct PlanArgs {
+  const Node* nodes;
+  const int* meta;
+  Dec* dec;
+  int* node_nl;
+  const int* prev_nl;
+  int4* curs;
+  int* child_l;
+  int* child_r;
+  Node* next;
+  int* next_tp;
+  int* next_meta;
+  int* next_bp;
+  int* counters;
+  int* scratch;
+  int depth, max_depth, cap_next, leaf_cap;
+  double min_w;
+  PlanReduce pr;
+  int* done;       // zero before the launch; the last block resets it
+};
+
+__global__ __launch_bounds__(256) void k_split_find_plan(
+    double* __restrict__ hist, int slot_doubles, const int* __restrict__ meta, int F,
+    const int* __restrict__ nbins_f, const int* __restrict__ iscat_f, const int* __restrict__ mono_f,
+    SplitParams p, int level, Cand* __restrict__ cand, double* __restrict__ root_w,
+    const float* __restrict__ edges, int adapt_nb, int f0, int FL, Derive dv, PlanArgs pa) {
+  split_find_body(hist, slot_doubles, meta, F, nbins_f, iscat_f, mono_f, p, level, cand, root_w, edges, adapt_nb, f0,
+                  FL, dv);
+  __shared__ int s_last;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int total = (int)(gridDim.x * gridDim.y);
+    s_last = __hip_atomic_fetch_add(pa.done, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) == total - 1;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  plan_body(pa.nodes, pa.meta, pa.dec, pa.node_nl, pa.prev_nl, pa.curs, pa.child_l, pa.child_r, pa.next, pa.next_tp,
+            pa.next_meta, pa.next_bp, pa.counters, pa.scratch, pa.depth, pa.max_depth, pa.min_w, pa.cap_next,
+            pa.leaf_cap, pa.pr);
+  if (threadIdx.x == 0) __hip_atomic_store(pa.done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Interaction constraints (GlobalInteractionConstraints / BranchInteractionConstraints): a child may split
@@ -2019,7 +2086,7 @@ __global__ __launch_bounds__(256) void k_row_dir(const uint8_t* __restrict__ bin
 struct LevelPtrs { const Dec* dec; const int* cl; const int* cr; long long cap; };
 
 template <int NV>
-__global__ __launch_bounds__(256) void k_leaf_assign(
+__device__ __forceinline__ void leaf_assign_body(
     const uint8_t* __restrict__ bins, int stride, long long N, const LevelPtrs* __restrict__ lv, int D,
     const float* __restrict__ an, const float* __restrict__ ad, const double* __restrict__ qs,
     int* __restrict__ leaf_of_row, unsigned long long* __restrict__ leafq, int leaf_cap, int n_nodes, int planar,
@@ -2140,10 +2207,8 @@ __device__ __forceinline__ float leaf_value(double num, double den, const LeafVa
   return (float)x;
 }
 
-__global__ void k_leafsum_finish(unsigned long long* __restrict__ leafq, const double* __restrict__ qs, int n,
-                                 double* __restrict__ leafsum, LeafVals lv) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+__device__ __forceinline__ void leafsum_one(unsigned long long* __restrict__ leafq, const double* __restrict__ qs,
+                                            int n, double* __restrict__ leafsum, const LeafVals& lv, int i) {
   long long a = 0, b = 0;
   for (int k = 0; k < LEAFQ_STRIPES; ++k) {                 // n == leaf_cap: stripe k at k * 2 * n
     unsigned long long* q = leafq + (size_t)k * 2 * n;
@@ -2155,6 +2220,34 @@ __global__ void k_leafsum_finish(unsigned long long* __restrict__ leafq, const d
   leafsum[2 * i] = (double)a * qs[8];
   leafsum[2 * i + 1] = (double)b * qs[9];
   if (lv.out) lv.out[i] = leaf_value(leafsum[2 * i], leafsum[2 * i + 1], lv);   // single process: no second launch
+}
+
+__global__ void k_leafsum_finish(unsigned long long* __restrict__ leafq, const double* __restrict__ qs, int n,
+                                 double* __restrict__ leafsum, LeafVals lv) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) leafsum_one(leafq, qs, n, leafsum, lv, i);
+}
+
+// k_leaf_assign with k_leafsum_finish folded into its LAST block: every block's leaf-sum atomics are ordered before
+// its agent-scope RELEASE ticket on `done`; the block drawing the final ticket acquires and finishes all leaf_cap
+// leaves (fp64 sums, re-zeroed fixed-point slots, closed-form values). One launch per tree instead of two.
+template <int NV>
+__global__ __launch_bounds__(256) void k_leaf_assign(
+    const uint8_t* __restrict__ bins, int stride, long long N, const LevelPtrs* __restrict__ lv, int D,
+    const float* __restrict__ an, const float* __restrict__ ad, const double* __restrict__ qs,
+    int* __restrict__ leaf_of_row, unsigned long long* __restrict__ leafq, int leaf_cap, int n_nodes, int planar,
+    const uint8_t* __restrict__ lvl2, double* __restrict__ leafsum, LeafVals vals, int* __restrict__ done) {
+  leaf_assign_body<NV>(bins, stride, N, lv, D, an, ad, qs, leaf_of_row, leafq, leaf_cap, n_nodes, planar, lvl2);
+  if (!done) return;
+  __shared__ int s_last;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    s_last = __hip_atomic_fetch_add(done, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  for (int i = threadIdx.x; i < leaf_cap; i += blockDim.x) leafsum_one(leafq, qs, leaf_cap, leafsum, vals, i);
+  if (threadIdx.x == 0) __hip_atomic_store(done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2618,7 +2711,7 @@ int h2o_route(const void* sbins, const void* say, const void* saw, void* dbins, 
 static int leaf_assign_launch(const void* master, int stride, long long N, const void* lvptrs, int D, const void* an,
                               const void* ad, const void* qs, void* leaf_of_row, void* leafq, int leaf_cap,
                               void* leafsum, int n_nodes, int planar, LeafVals lv, hipStream_t s,
-                              const void* lvl2 = nullptr) {
+                              const void* lvl2 = nullptr, int* done = nullptr) {
   if (D > TP_MAXL_DEV) return (int)hipErrorInvalidValue;
   long long grid = (N + 255) / 256;
   if (grid > 2048) grid = 2048;
@@ -2628,7 +2721,7 @@ static int leaf_assign_launch(const void* master, int stride, long long N, const
 #define LA(NV) hipLaunchKernelGGL((k_leaf_assign<NV>), dim3((unsigned)grid), dim3(256), lds, s, (const uint8_t*)master, \
                                   stride, N, (const LevelPtrs*)lvptrs, D, (const float*)an, (const float*)ad,          \
                                   (const double*)qs, (int*)leaf_of_row, (unsigned long long*)leafq, leaf_cap, n_nodes, planar, \
-                                  (const uint8_t*)lvl2)
+                                  (const uint8_t*)lvl2, (double*)leafsum, lv, done)
   // planar rows of more than two planes: with the root route's level-2 positions (narrow levels below) only the
   // first plane in registers, else the first two; split bytes of later planes are loaded per level
   switch ((planar && stride > 64 && !route_generic()) ? (lvl2 ? 2 : 4) : nv_of(stride)) {
@@ -2639,8 +2732,9 @@ static int leaf_assign_launch(const void* master, int stride, long long N, const
     default: LA(0);
   }
 #undef LA
-  hipLaunchKernelGGL(k_leafsum_finish, dim3((leaf_cap + 255) / 256), dim3(256), 0, s, (unsigned long long*)leafq,
-                     (const double*)qs, leaf_cap, (double*)leafsum, lv);
+  if (!done)
+    hipLaunchKernelGGL(k_leafsum_finish, dim3((leaf_cap + 255) / 256), dim3(256), 0, s, (unsigned long long*)leafq,
+                       (const double*)qs, leaf_cap, (double*)leafsum, lv);
   return (int)hipGetLastError();
 }
 
@@ -2855,7 +2949,45 @@ int h2o_tree_find(const TreePlan* P, int d, hipStream_t s) {
 
 // decisions (from cand) + plan, then the next level's histogram.
 // returns 0 = histogram done (dist: compact buffer ready for the collective), 1 = last level, <0 error.
-int h2o_tree_grow(const TreePlan* P, int d, int dist, hipStream_t s) {
+static int tree_grow(const TreePlan* P, int d, int dist, hipStream_t s, bool plan_done);
+int h2o_tree_grow(const TreePlan* P, int d, int dist, hipStream_t s) { return tree_grow(P, d, dist, s, false); }
+
+// single-process levels of <= PLAN_REDUCE_MAX nodes: split search + plan in one launch (k_split_find_plan). OFF by
+// default (H2O_PLAN_FUSED=1 turns it on). MEASURED r5 (scripts/gpu_r5_c15.sh, 11M HIGGS): the per-block agent-scope
+// release (buffer_wbl2) of the ticket made k_split_find_plan 16-43 us per level against 13-19 for the two launches,
+// and the tree 1.262 -> 1.372 ms (24 dispatches instead of 31): on MI355X an L2 write-back per block costs far more
+// than a kernel boundary.
+static bool plan_fused() {
+  static int v = -1;
+  if (v < 0) { const char* e = getenv("H2O_PLAN_FUSED"); v = (e && e[0] == '1') ? 1 : 0; }
+  return v == 1;
+}
+
+static int tree_find_plan(const TreePlan* P, int d, hipStream_t s) {
+  void* hc = (d % 2) ? P->hist1 : P->hist0;
+  SplitParams p;
+  p.min_w = P->min_w; p.min_split_improvement = P->msi; p.lambda = P->lam; p.alpha = P->alpha; p.gamma = P->gamma;
+  p.mode = P->mode; p.random_split = P->random_split; p.seed = P->seed; p.hist_type = P->hist_type;
+  p.fcut = tp_fcut(P, d);
+  const int cap = P->caps[d];
+  const int kc = P->kc_level[d] > 0 ? P->kc_level[d] : P->k_cols;
+  const PlanReduce pr{(const Cand*)P->cand, P->F, (const int*)P->feat_ok, kc, P->seed,
+                      P->ic_map ? (const unsigned char*)P->ic[d] : nullptr, (const int*)P->fgroup, 0, cap};
+  const bool odd = d % 2 == 1;
+  const PlanArgs pa{(const Node*)P->nodes[d], (const int*)P->meta[d], (Dec*)P->dec[d], (int*)P->nl[d],
+                    odd ? (const int*)P->nl[d - 1] : nullptr, (int4*)P->cur[d], (int*)P->cl[d], (int*)P->cr[d],
+                    (Node*)P->nodes[d + 1], (int*)P->tp[d + 1], (int*)P->meta[d + 1], (int*)P->bp[d + 1],
+                    (int*)P->counters, (int*)P->scratch, d, P->D, P->caps[d + 1], P->leaf_cap, P->min_w, pr,
+                    (int*)P->counters + 2};
+  if (P->F <= 0 || cap <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_split_find_plan, dim3(cap, P->F), dim3(256), 0, s, (double*)hc, P->slot, (const int*)P->meta[d],
+                     P->F, (const int*)P->nbins_f, (const int*)P->iscat_f, (const int*)P->mono_f, p, d,
+                     (Cand*)P->cand, d == 0 ? (double*)P->rootw : nullptr, (const float*)P->edges, P->nb_level[d], 0,
+                     P->F, Derive{nullptr, 0, 0, nullptr, nullptr}, pa);
+  return (int)hipGetLastError();
+}
+
+static int tree_grow(const TreePlan* P, int d, int dist, hipStream_t s, bool plan_done) {
   void* hc = (d % 2) ? P->hist1 : P->hist0;
   void* hn = (d % 2) ? P->hist0 : P->hist1;
   const int cap = P->caps[d];
@@ -2868,17 +3000,19 @@ int h2o_tree_grow(const TreePlan* P, int d, int dist, hipStream_t s) {
   const int cfs = P->sliced ? P->cand_fs : 0;
   PlanReduce pr{nullptr, P->F, (const int*)P->feat_ok, kc, P->seed,
                 P->ic_map ? (const unsigned char*)P->ic[d] : nullptr, (const int*)P->fgroup, cfs, cap};
-  if (cap <= PLAN_REDUCE_MAX) {
-    pr.cand = (const Cand*)cand;
-  } else {
-    rc = h2o_split_reduce(cand, P->meta[d], cap, P->F, P->feat_ok, kc, P->seed, d, P->dec[d],
-                          P->ic_map ? P->ic[d] : nullptr, P->fgroup, cfs, s);
+  if (!plan_done) {
+    if (cap <= PLAN_REDUCE_MAX) {
+      pr.cand = (const Cand*)cand;
+    } else {
+      rc = h2o_split_reduce(cand, P->meta[d], cap, P->F, P->feat_ok, kc, P->seed, d, P->dec[d],
+                            P->ic_map ? P->ic[d] : nullptr, P->fgroup, cfs, s);
+      if (rc) return -rc;
+    }
+    rc = plan_launch(P->nodes[d], P->meta[d], P->dec[d], P->nl[d], odd ? P->nl[d - 1] : nullptr, P->cur[d], P->cl[d],
+                     P->cr[d], P->nodes[d + 1], P->tp[d + 1], P->meta[d + 1], P->bp[d + 1], P->counters, P->scratch,
+                     d, P->D, P->min_w, P->caps[d + 1], P->leaf_cap, pr, s);
     if (rc) return -rc;
   }
-  rc = plan_launch(P->nodes[d], P->meta[d], P->dec[d], P->nl[d], odd ? P->nl[d - 1] : nullptr, P->cur[d], P->cl[d],
-                   P->cr[d], P->nodes[d + 1], P->tp[d + 1], P->meta[d + 1], P->bp[d + 1], P->counters, P->scratch, d,
-                   P->D, P->min_w, P->caps[d + 1], P->leaf_cap, pr, s);
-  if (rc) return -rc;
   if (P->ic_map && d + 1 < P->D) {
     rc = h2o_ic_next(P->nodes[d + 1], P->meta[d + 1], P->dec[d], P->ic[d], P->ic_map, P->F, P->ic[d + 1],
                      P->caps[d + 1], s);
@@ -2938,9 +3072,10 @@ int h2o_tree_grow(const TreePlan* P, int d, int dist, hipStream_t s) {
 
 // one level: split search, decisions, plan, next histogram (single process and all-reduce mode)
 int h2o_tree_level(const TreePlan* P, int d, int dist, hipStream_t s) {
-  const int rc = h2o_tree_find(P, d, s);
+  const bool fuse = !dist && !P->dist && !P->sliced && P->caps[d] <= PLAN_REDUCE_MAX && plan_fused();
+  const int rc = fuse ? tree_find_plan(P, d, s) : h2o_tree_find(P, d, s);
   if (rc) return -rc;
-  return h2o_tree_grow(P, d, dist, s);
+  return tree_grow(P, d, dist, s, fuse);
 }
 
 
@@ -2950,8 +3085,13 @@ static int tree_leaves(const TreePlan* P, bool values, hipStream_t s) {
   for (int d = 0; d < P->D; ++d) n_nodes += P->caps[d];
   const LeafVals lv{P->log_link, P->scale, P->kclamp, P->mx, P->leaf_lam, P->leaf_l1,
                     values ? (float*)P->leafval : nullptr};
+  // (H2O_LEAF_FUSED=1: k_leafsum_finish in the leaf-assign launch's last block. OFF by default — MEASURED r5: the
+  // 2048 per-block release fences made k_leaf_assign 221 us against 115 + 4 for the two launches)
+  static int fused = -1;
+  if (fused < 0) { const char* e = getenv("H2O_LEAF_FUSED"); fused = (e && e[0] == '1') ? 1 : 0; }
   return leaf_assign_launch(P->master, P->stride, P->N, P->lvptrs, P->D, tp_aux(P, P->num_plane), tp_aux(P, 3), P->qs,
-                            P->leaf_of_row, P->leafq, P->leaf_cap, P->leafsum, n_nodes, P->planar, lv, s, tp_lvl2(P));
+                            P->leaf_of_row, P->leafq, P->leaf_cap, P->leafsum, n_nodes, P->planar, lv, s, tp_lvl2(P),
+                            fused ? (int*)P->counters + 3 : nullptr);
 }
 
 int h2o_tree_leaves(const TreePlan* P, hipStream_t s) { return tree_leaves(P, false, s); }
