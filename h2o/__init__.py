@@ -399,8 +399,27 @@ def cluster_status():
     return _rt.cluster_status()
 
 
-def set_s3_credentials(*a, **k):
-    raise NotImplementedError("no network persistence backends in this build")
+def set_s3_credentials(secret_key_id, secret_access_key, session_token=None):
+    """Credentials of every later ``s3://`` import (h2o.persist.set_s3_credentials; io/persist_store.py signs the
+    S3 REST requests with them, AWS Signature V4)."""
+    from .exceptions import H2OValueError
+    if secret_key_id is None:
+        raise H2OValueError("Secret key ID must be specified")
+    if secret_access_key is None:
+        raise H2OValueError("Secret access key must be specified")
+    if not secret_key_id:
+        raise H2OValueError("Secret key ID must not be empty")
+    if not secret_access_key:
+        raise H2OValueError("Secret access key must not be empty")
+    from llama_github_io_amd.io import persist_store
+    persist_store.set_s3_credentials(secret_key_id, secret_access_key, session_token)
+    print("Credentials successfully set.")
+
+
+def remove_s3_credentials():
+    from llama_github_io_amd.io import persist_store
+    persist_store.remove_s3_credentials()
+    print("Credentials successfully removed.")
 
 
 from . import grid, automl  # noqa: E402,F401

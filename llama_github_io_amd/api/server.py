@@ -307,6 +307,32 @@ def create_app(client_disconnect_timeout: float | None = None):
         dkv.remove(key)
         return {"__meta": v3.meta("RemoveV3", "Iced"), "key": v3.key(key)}
 
+    # ---- object-store credentials (PersistS3Handler: POST sets, DELETE removes; the schema is echoed back)
+    @app.post("/3/PersistS3")
+    async def persist_s3_set(request: Request):
+        from ..io import persist_store
+        p = await _params(request)
+        kid, sec, tok = p.get("secret_key_id"), p.get("secret_access_key"), p.get("session_token")
+        if kid is None:
+            raise ValueError("The field 'S3_SECRET_KEY_ID' may not be null.")
+        if sec is None:
+            raise ValueError("The field 'S3_SECRET_ACCESS_KEY' may not be null.")
+        kid, sec = str(kid).strip(), str(sec).strip()
+        tok = None if tok in (None, "None") else str(tok).strip()
+        if tok is not None and not tok:
+            raise ValueError("The field 'S3_SESSION_TOKEN' may not be empty")
+        persist_store.set_s3_credentials(kid, sec, tok)
+        return {"__meta": v3.meta("PersistS3CredentialsV3", "Iced"), "secret_key_id": kid, "secret_access_key": sec,
+                "session_token": tok}
+
+    @app.delete("/3/PersistS3")
+    async def persist_s3_remove(request: Request):
+        from ..io import persist_store
+        p = await _params(request)
+        persist_store.remove_s3_credentials()
+        return {"__meta": v3.meta("PersistS3CredentialsV3", "Iced"), "secret_key_id": p.get("secret_key_id"),
+                "secret_access_key": p.get("secret_access_key"), "session_token": p.get("session_token")}
+
     # ---- ingest
     @app.post("/3/ImportFiles")
     @app.get("/3/ImportFiles")

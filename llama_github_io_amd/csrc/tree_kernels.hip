@@ -2231,14 +2231,15 @@ __global__ void k_leafsum_finish(unsigned long long* __restrict__ leafq, const d
 // k_leaf_assign with k_leafsum_finish folded into its LAST block: every block's leaf-sum atomics are ordered before
 // its agent-scope RELEASE ticket on `done`; the block drawing the final ticket acquires and finishes all leaf_cap
 // leaves (fp64 sums, re-zeroed fixed-point slots, closed-form values). One launch per tree instead of two.
-template <int NV>
+// (FUSE is a template switch: the tail costs the unfused kernel 14 VGPRs — 34 -> 48 — and MEASURED r5 115 -> 140 us)
+template <int NV, bool FUSE>
 __global__ __launch_bounds__(256) void k_leaf_assign(
     const uint8_t* __restrict__ bins, int stride, long long N, const LevelPtrs* __restrict__ lv, int D,
     const float* __restrict__ an, const float* __restrict__ ad, const double* __restrict__ qs,
     int* __restrict__ leaf_of_row, unsigned long long* __restrict__ leafq, int leaf_cap, int n_nodes, int planar,
     const uint8_t* __restrict__ lvl2, double* __restrict__ leafsum, LeafVals vals, int* __restrict__ done) {
   leaf_assign_body<NV>(bins, stride, N, lv, D, an, ad, qs, leaf_of_row, leafq, leaf_cap, n_nodes, planar, lvl2);
-  if (!done) return;
+  if (!FUSE || !done) return;
   __shared__ int s_last;
   __syncthreads();
   if (threadIdx.x == 0)
@@ -2718,7 +2719,8 @@ static int leaf_assign_launch(const void* master, int stride, long long N, const
   if (grid < 1) grid = 1;
   const size_t lds = (leaf_cap <= LEAF_LDS_MAX ? (size_t)16 * leaf_cap : 0) +
                      (n_nodes <= LEAF_TREE_MAX ? (size_t)16 * n_nodes : 0);
-#define LA(NV) hipLaunchKernelGGL((k_leaf_assign<NV>), dim3((unsigned)grid), dim3(256), lds, s, (const uint8_t*)master, \
+#define LA(NV) do { if (done) { LA2(NV, true); } else { LA2(NV, false); } } while (0)
+#define LA2(NV, FU) hipLaunchKernelGGL((k_leaf_assign<NV, FU>), dim3((unsigned)grid), dim3(256), lds, s, (const uint8_t*)master, \
                                   stride, N, (const LevelPtrs*)lvptrs, D, (const float*)an, (const float*)ad,          \
                                   (const double*)qs, (int*)leaf_of_row, (unsigned long long*)leafq, leaf_cap, n_nodes, planar, \
                                   (const uint8_t*)lvl2, (double*)leafsum, lv, done)
@@ -2732,6 +2734,7 @@ static int leaf_assign_launch(const void* master, int stride, long long N, const
     default: LA(0);
   }
 #undef LA
+#undef LA2
   if (!done)
     hipLaunchKernelGGL(k_leafsum_finish, dim3((leaf_cap + 255) / 256), dim3(256), 0, s, (unsigned long long*)leafq,
                        (const double*)qs, leaf_cap, (double*)leafsum, lv);
@@ -2751,6 +2754,38 @@ int h2o_amax(const void* aux, long long N, void* amax_bits, hipStream_t s) {
   if (grid > 2048) grid = 2048;
   if (grid < 1) grid = 1;
   hipLaunchKernelGGL(k_amax, dim3((unsigned)grid), dim3(256), 0, s, (const float*)aux, N, (unsigned*)amax_bits);
+  return (int)hipGetLastError();
+}
+
+// Tree snapshot to pinned host memory from a kernel (the arena's 16-byte words stored straight into the mapped
+// host buffer) instead of a runtime device-to-host copy. (r5 A/B: the runtime copy started ~12 us after the last
+// tree kernel in every tree.)
+__global__ __launch_bounds__(256) void k_snap_copy(const uint4* __restrict__ src, uint4* __restrict__ dst, long long n16,
+                                                   const unsigned char* __restrict__ srcb, unsigned char* __restrict__ dstb,
+                                                   long long nbytes) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (long long)gridDim.x * blockDim.x)
+    dst[i] = src[i];
+  const long long t = n16 * 16 + (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < nbytes) dstb[t] = srcb[t];
+}
+
+// device address of a pinned host buffer (hipHostGetDevicePointer); nonzero return: not mapped for the device
+int h2o_host_dev_ptr(void* host, unsigned long long* out) {
+  void* d = nullptr;
+  const hipError_t e = hipHostGetDevicePointer(&d, host, 0);
+  *out = (unsigned long long)(uintptr_t)d;
+  return (int)e;
+}
+
+int h2o_snap_copy(const void* src, void* dst, long long nbytes, hipStream_t s) {
+  if (nbytes <= 0) return 0;
+  if ((((uintptr_t)src) | ((uintptr_t)dst)) & 15) return (int)hipErrorInvalidValue;
+  const long long n16 = nbytes / 16;
+  long long grid = (n16 + 255) / 256;
+  if (grid < 1) grid = 1;
+  if (grid > 64) grid = 64;
+  hipLaunchKernelGGL(k_snap_copy, dim3((unsigned)grid), dim3(256), 0, s, (const uint4*)src, (uint4*)dst, n16,
+                     (const unsigned char*)src, (unsigned char*)dst, nbytes);
   return (int)hipGetLastError();
 }
 

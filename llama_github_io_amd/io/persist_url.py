@@ -6,8 +6,9 @@
 type guess (``.csv``, ``.gz``, ``.zip``, ``.parquet``, ...) and the destination frame name work as for a local file.
 A URL that was already fetched in this process is not fetched again unless ``refresh`` is asked for.
 
-Object stores (``s3://``, ``s3a://``, ``s3n://``, ``gs://``, ``hdfs://``) need their vendor SDKs, which are not part
-of this build: they fail with an error naming the scheme instead of being mistaken for a local path.
+Object stores (``s3://``, ``s3a://``, ``s3n://``, ``gs://``, ``hdfs://``) are read through their REST protocols
+(``persist_store``: S3 with Signature V4, the Cloud Storage JSON API, WebHDFS) into the same cache; ``maprfs://``
+fails with an error naming the scheme.
 """
 from __future__ import annotations
 
@@ -52,15 +53,21 @@ def _file_name(url: str) -> str:
 def fetch(url: str, refresh: bool = False, timeout: float = 600.0) -> str:
     """Download ``url`` (GET, redirects followed) into the cache; returns the local file path.
     PersistEagerHTTP: a non-2xx answer is an error, the body is taken whole."""
+    req = urllib.request.Request(url, headers={"User-Agent": "h2o-mi355x/persist-http"})
+    return download(url, lambda t: urllib.request.urlopen(req, timeout=t), _file_name(url), refresh, timeout)
+
+
+def download(key: str, opener, name: str, refresh: bool = False, timeout: float = 600.0) -> str:
+    """Body of ``opener(timeout)`` (a urllib response) into the cache under ``key`` (file name ``name``)."""
+    url = key
     with _lock:
         if not refresh and url in _cache and os.path.exists(_cache[url]):
             return _cache[url]
         sub = os.path.join(_cache_dir(), hashlib.sha1(url.encode()).hexdigest()[:16])
         os.makedirs(sub, exist_ok=True)
-        dst = os.path.join(sub, _file_name(url))
-        req = urllib.request.Request(url, headers={"User-Agent": "h2o-mi355x/persist-http"})
+        dst = os.path.join(sub, name or "object")
         try:
-            with urllib.request.urlopen(req, timeout=timeout) as r, open(dst + ".part", "wb") as f:
+            with opener(timeout) as r, open(dst + ".part", "wb") as f:
                 code = getattr(r, "status", 200)
                 if code // 100 != 2:
                     raise OSError(f"HTTP {code} for {url}")
@@ -75,10 +82,13 @@ def fetch(url: str, refresh: bool = False, timeout: float = 600.0) -> str:
 
 
 def resolve(path) -> list | None:
-    """Local files for a URL source, or None when ``path`` is not a URL. Object-store schemes raise."""
+    """Local files for a URL source, or None when ``path`` is not a URL."""
     s = scheme(path)
     if s in HTTP_SCHEMES:
         return [fetch(str(path))]
+    if s in ("s3", "s3a", "s3n", "gs", "hdfs"):
+        from . import persist_store
+        return persist_store.resolve(str(path), lambda key, opener, name: download(key, opener, name))
     if s in STORE_SCHEMES:
         raise ValueError(f"persist backend for '{s}://' is not available in this build (the reference reads it "
                          f"through its {s.upper()} SDK; copy the file to a local or http(s) location instead)")

@@ -560,6 +560,7 @@ class RefTreeBuilder:
 
 # ================================================================================================
 _MAXL = 65
+_SNAP_KERNEL = os.environ.get("H2O_SNAP_KERNEL", "1") != "0"
 _vp, _ci, _cd = ctypes.c_void_p, ctypes.c_int, ctypes.c_double
 
 
@@ -993,11 +994,26 @@ class GpuTreeBuilder:
         # in the launches (820 us/tree host, 1.09 vs 0.575 ms/tree at 1.375M rows): kept on the compute stream
         host = self._pinned_pool.pop() if self._pinned_pool else torch.empty(self.arena.numel(), dtype=torch.uint8,
                                                                                pin_memory=True)
-        host.copy_(self.arena, non_blocking=True)
+        dptr = self._snap_dev_ptr(host) if self.dev.type == "cuda" and _SNAP_KERNEL else 0
+        if dptr:
+            # the snapshot kernel stores into the mapped pinned buffer (no runtime device-to-host copy)
+            nat.call("h2o_snap_copy", self.arena.data_ptr(), dptr, self.arena.numel(), nat.stream_ptr(self.dev))
+        else:
+            host.copy_(self.arena, non_blocking=True)
         ev = self._event_pool.pop() if self._event_pool else torch.cuda.Event()
         ev.record()
         self.history.append((host, ev))
         return len(self.history) - 1
+
+    def _snap_dev_ptr(self, host: torch.Tensor) -> int:
+        """Device address of a pinned snapshot buffer (0: not device-mapped -> runtime copy), cached per buffer."""
+        cache = self.__dict__.setdefault("_dev_ptrs", {})
+        hp = host.data_ptr()
+        if hp not in cache:
+            out = ctypes.c_ulonglong(0)
+            rc = nat.hip().h2o_host_dev_ptr(ctypes.c_void_p(hp), ctypes.byref(out))
+            cache[hp] = int(out.value) if rc == 0 and host.is_pinned() and out.value % 16 == 0 else 0
+        return cache[hp]
 
     def leaf_values_view(self) -> torch.Tensor:
         """Device float32 leaf values of the last built tree (valid until the next build writes them)."""

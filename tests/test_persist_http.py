@@ -1,6 +1,6 @@
 """``import_file("http://...")`` (water/persist/PersistManager.java:301,423, PersistEagerHTTP.java) against a local
 stdlib HTTP server: CSV and gzip bodies, the REST ImportFiles -> ParseSetup -> Parse flow, a 404, and the refusal of
-object-store schemes whose SDKs are not in this build."""
+a store scheme with no backend here (maprfs)."""
 import functools
 import gzip
 import http.server
@@ -47,9 +47,8 @@ def test_http_errors_and_object_stores(server):
     base, _ = server
     with pytest.raises(FileNotFoundError, match="Unable to import file from URL"):
         h2o.import_file(base + "/missing.csv")
-    for url in ("s3://bucket/x.csv", "gs://bucket/x.csv", "hdfs://nn/x.csv"):
-        with pytest.raises(ValueError, match="persist backend"):
-            h2o.import_file(url)
+    with pytest.raises(ValueError, match="persist backend"):
+        h2o.import_file("maprfs://cluster/x.csv")     # (s3 / gs / hdfs: tests/test_persist_store.py)
 
 
 def test_rest_import_parse_over_http(server):
