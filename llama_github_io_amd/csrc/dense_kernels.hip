@@ -305,6 +305,8 @@ __device__ __forceinline__ uint4 pack_row(const float* v, float*) {
   return make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3]));
 }
 // MEASURED r4 (10M x 784 bf16): 32 rows x 256 features 13.19 ms, 128 rows x 64 features 12.46 ms
+// MEASURED r5: issuing the next (rows, feature chunk) item's loads before the current tile's stores (register
+// pipeline) 14.0 ms — slower; not kept (scripts/experiments/num_transform_pipeline.diff).
 #ifndef NT_ROWS
 #define NT_ROWS 128
 #endif

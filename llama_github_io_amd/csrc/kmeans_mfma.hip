@@ -19,6 +19,13 @@
 // Each wave walks 16-row tiles (grid-stride) and keeps its sums in AGPR/VGPR accumulators; at the
 // end it writes one [KT*16][PT*16] fp32 slab (no atomics). The host sums the slabs in fp64.
 // Rows are read once (X: 4*P bytes/row) -> the launch streams at HBM rate.
+// MEASURED r5 (10M x 20, k = 10): two 64-row tiles in flight per wave (register double buffer, 3 waves / SIMD)
+// 322.7 us vs 318.0 us with one — the kernel is not bound by outstanding HBM reads; not kept
+// (scripts/experiments/kmeans_double_buffer.diff, profiles/r5_kmeans_db_kernel_stats.md).
+// MEASURED r5: the 64-row tile in phases over its four 16-row sub-tiles (distance MFMAs of different sub-tiles
+// interleaved, one store branch per tile) with the row weight moved into the one-hot A operand and the counts'
+// constant column kept in LDS (the B operand is read with no per-element VALU): 318.0 -> 286.6 us per Lloyd
+// kernel, 0.352 -> 0.321 ms per iteration end to end (profiles/r5_kmeans_phased_kernel_stats.md).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <float.h>
@@ -133,6 +140,7 @@ __global__ __launch_bounds__(256) void k_lloyd_mfma(const float* __restrict__ X,
     const int r = e / P, c = e - r * P;
     doff[i] = e < KM_ROWS * P ? r * Pp + c : -1;
   }
+  xs[lane * Pp + P] = 1.f;   // column P of each of the 64 rows (never staged over): the centroid GEMM's counts
   if (wave_g * KM_ROWS < N) issue(wave_g * KM_ROWS);
   for (int64_t r0 = wave_g * KM_ROWS; r0 < N; r0 += n_waves * KM_ROWS) {
     const int nrows = (int)((N - r0) < KM_ROWS ? (N - r0) : KM_ROWS);
@@ -155,61 +163,90 @@ __global__ __launch_bounds__(256) void k_lloyd_mfma(const float* __restrict__ X,
       const int64_t nx = r0 + n_waves * KM_ROWS;
       if (nx < N) issue(nx);                 // next tile's loads stay in flight during the compute below
     }
+    // The 64-row tile in phases, each over the 4 16-row sub-tiles, so independent MFMA chains / shuffles of
+    // different sub-tiles interleave (the former per-sub-tile order serialised distance -> argmin -> shuffle ->
+    // centroid chains; the stores' divergent branch split the schedule once per sub-tile).
+    // G sub-tiles per phase group (registers: G x KT distance tiles live at once)
+    constexpr int G = KT == 1 ? 4 : (KT == 2 ? 2 : 1);
 #pragma unroll
-    for (int tr = 0; tr < KM_ROWS / 16; ++tr) {
-      const float* xt = xs + tr * 16 * Pp;
-      // ---- 1. distance GEMM: B[k = dim 4s+q][j = row c16]; the same values give ||x||^2
-      f32x4 d[KT];
+    for (int g0 = 0; g0 < KM_ROWS / 16; g0 += G) {
+    // ---- 1. distance GEMM: B[k = dim 4s+q][j = row c16]; the same values give ||x||^2
+    f32x4 d[G][KT];
+    float xq[G];
 #pragma unroll
-      for (int t = 0; t < KT; ++t) d[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
-      float xq = 0.f;
+    for (int tr = 0; tr < G; ++tr) {
+      xq[tr] = 0.f;
 #pragma unroll
-      for (int s = 0; s < PS; ++s) {
-        if (s < ps) {
-          const float xb = xt[c16 * Pp + 4 * s + q];      // P % 4 == 0: always a real (or padding-zero) dim
-          xq = fmaf(xb, xb, xq);
+      for (int t = 0; t < KT; ++t) d[tr][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
 #pragma unroll
-          for (int t = 0; t < KT; ++t) d[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(ca[t][s], xb, d[t], 0, 0, 0);
+    for (int s = 0; s < PS; ++s) {
+      if (s < ps) {
+#pragma unroll
+        for (int tr = 0; tr < G; ++tr) {
+          const float xb = xs[((g0 + tr) * 16 + c16) * Pp + 4 * s + q];   // P % 4 == 0: a real (or padding-zero) dim
+          xq[tr] = fmaf(xb, xb, xq[tr]);
+#pragma unroll
+          for (int t = 0; t < KT; ++t) d[tr][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(ca[t][s], xb, d[tr][t], 0, 0, 0);
         }
       }
-      float best = FLT_MAX;
-      int bidx = 0x7fffffff;
+    }
+    // ---- argmin over the centers (ties -> smaller index), then ||x||^2 across the lane quarters
+    int bidx[G];
+    float best[G];
+#pragma unroll
+    for (int tr = 0; tr < G; ++tr) {
+      best[tr] = FLT_MAX;
+      bidx[tr] = 0x7fffffff;
 #pragma unroll
       for (int t = 0; t < KT; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float sc = csq[t][r] - 2.f * d[t][r];
+          const float sc = csq[t][r] - 2.f * d[tr][t][r];
           const int ci = t * 16 + 4 * q + r;              // increasing: strict '<' keeps the smaller index
-          if (sc < best) { best = sc; bidx = ci; }
+          if (sc < best[tr]) { best[tr] = sc; bidx[tr] = ci; }
         }
-      best = bfly_min_idx(best, bidx, 16);
-      best = bfly_min_idx(best, bidx, 32);
-      xq += __shfl_xor(xq, 16, 64);
-      xq += __shfl_xor(xq, 32, 64);
-      const int rrow = tr * 16 + c16;                      // every lane of column c16 holds row rrow's result
-      if (q == 0 && rrow < nrows) {
-        if (assign) assign[r0 + rrow] = bidx;        // (null: the Lloyd loop does not read assignments)
-        mind[r0 + rrow] = fmaxf(xq + best, 0.f);
+    }
+#pragma unroll
+    for (int tr = 0; tr < G; ++tr) best[tr] = bfly_min_idx(best[tr], bidx[tr], 16);
+#pragma unroll
+    for (int tr = 0; tr < G; ++tr) best[tr] = bfly_min_idx(best[tr], bidx[tr], 32);
+#pragma unroll
+    for (int tr = 0; tr < G; ++tr) xq[tr] += __shfl_xor(xq[tr], 16, 64);
+#pragma unroll
+    for (int tr = 0; tr < G; ++tr) xq[tr] += __shfl_xor(xq[tr], 32, 64);
+    if (q == 0) {                                      // every lane of column c16 holds row tr*16 + c16's result
+#pragma unroll
+      for (int tr = 0; tr < G; ++tr) {
+        const int rrow = (g0 + tr) * 16 + c16;
+        if (rrow < nrows) {
+          if (assign) assign[r0 + rrow] = bidx[tr];  // (null: the Lloyd loop does not read assignments)
+          mind[r0 + rrow] = fmaxf(xq[tr] + best[tr], 0.f);
+        }
       }
-      // ---- 2. centroid GEMM over the 16 rows in 4 steps of 4 rows: A[i = center][k = row 4j+q] (one-hot),
-      // B[k = row 4j+q][j = dim]; the constant-1 column at dim P accumulates the weighted counts
+    }
+    // ---- 2. centroid GEMM in steps of 4 rows: A[i = center][k = row 4j+q] = onehot * row weight, B[k = row][j =
+    // dim] read straight from the slice, whose column P holds 1.0 (the weighted counts) — no per-element VALU
+#pragma unroll
+    for (int tr = 0; tr < G; ++tr) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int rt = tr * 16 + 4 * j + q;                // row within the 64-row slice (zero-weight tail rows)
-        const int my_a = __shfl(bidx, 4 * j + q, 64);
+        const int rt = (g0 + tr) * 16 + 4 * j + q;                // row within the 64-row slice (zero-weight tail rows)
+        const int my_a = __shfl(bidx[tr], 4 * j + q, 64);
         const float ww = wsl[rt];
         const float* xr = xs + rt * Pp;
 #pragma unroll
         for (int u = 0; u < PT; ++u) {
           const int dd = u * 16 + c16;
-          const float bv = dd < P ? ww * xr[dd] : (dd == P ? ww : 0.f);
+          const float bv = dd <= P ? xr[dd] : 0.f;
 #pragma unroll
           for (int t = 0; t < KT; ++t) {
-            const float av = (my_a == t * 16 + c16) ? 1.f : 0.f;
+            const float av = (my_a == t * 16 + c16) ? ww : 0.f;
             acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[t][u], 0, 0, 0);
           }
         }
       }
+    }
     }
     __builtin_amdgcn_wave_barrier();   // the slice is rewritten by the next iteration's loads
   }

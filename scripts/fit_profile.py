@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--rows", type=int, default=10_000_000)
     ap.add_argument("--cols", type=int, default=0)
     ap.add_argument("--top", type=int, default=45)
+    ap.add_argument("--no-cprofile", action="store_true", help="timed fits only (for a kernel trace of the last fit)")
     a = ap.parse_args()
     from llama_github_io_amd.models.base import DataInfo
     dev = torch.device("cuda", 0)
@@ -63,6 +64,8 @@ def main():
         m = Tr(dict(prm)).fit(X, y, None, None, info)
         torch.cuda.synchronize()
         print(f"fit {1000 * (time.perf_counter() - t0):.2f} ms phases {m.output.get('phase_seconds')}", flush=True)
+    if a.no_cprofile:
+        return
     pr = cProfile.Profile()
     torch.cuda.synchronize()
     pr.enable()

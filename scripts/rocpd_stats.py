@@ -24,7 +24,33 @@ def main():
                     "print every step's wall span and GPU-busy fraction")
     ap.add_argument("--sequence", default=None, help="kernel-name substring marking one step: print the dispatch "
                     "sequence (name, duration, gap before it) of the step after its 10th occurrence")
+    ap.add_argument("--gaps", default=None, help="kernel-name substring marking the start of the window (its LAST "
+                    "occurrence; e.g. k_num_stats for a DL fit): list the idle gaps > --min-gap us up to the trace end")
+    ap.add_argument("--min-gap", type=float, default=50.0)
     a = ap.parse_args()
+    if a.gaps:
+        db = sqlite3.connect(a.db)
+        ks = db.execute("select name, start, end from kernels order by start").fetchall()
+        idx = [i for i, k in enumerate(ks) if a.gaps in k[0]]
+        if not idx:
+            print("marker not found")
+            return
+        i0 = idx[-1]
+        t0, t1 = ks[i0][1], max(k[2] for k in ks[i0:])
+        busy, last_end, gaps, prev = 0, t0, [], ""
+        for nm, st, en in ks[i0:]:
+            if st > last_end and (st - last_end) / 1e3 >= a.min_gap:
+                gaps.append(((st - last_end) / 1e3, prev, nm))
+            busy += max(0, en - max(st, last_end))
+            last_end = max(last_end, en)
+            prev = nm
+        print(f"window {(t1 - t0) / 1e3:.1f} us, busy {busy / 1e3:.1f} us, idle {(t1 - t0 - busy) / 1e3:.1f} us; "
+              f"gaps >= {a.min_gap:g} us: {len(gaps)}, {sum(g[0] for g in gaps):.1f} us")
+        print("| gap us | after | before |\n|---|---|---|")
+        short = lambda n: n if len(n) < 50 else n[:47] + "..."
+        for g, p_, n in gaps:
+            print(f"| {g:.1f} | `{short(p_)}` | `{short(n)}` |")
+        return
     if a.sequence:
         db = sqlite3.connect(a.db)
         ks = db.execute("select name, start, end from kernels order by start").fetchall()
