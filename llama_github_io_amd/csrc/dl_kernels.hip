@@ -20,6 +20,8 @@
 //  MEASURED (r4, DL_TIMING phase clocks): staging the weights of layers 2+ in LDS per launch cost ~5 us of
 //  loads at kernel start and gained < 0.4 us per later phase (their time is not the weight reads): dropped.
 //  Prefetching layer 1's first round of weight fragments into registers before the gathers spilled (128 VGPRs).
+//  MEASURED (r5): writing the layer-1 input transpose (hT0) from the 3 waves without a layer-1 tile while the other
+//  13 run the layer-1 MFMAs: 31.1 -> 31.6 us per step (not on the critical path; scripts/experiments/dl_hT0_overlap.diff).
 //  MEASURED (10M x 784 [200,200], 4096-row steps, rocprofv3): the first version (16-row tiles on 4 waves,
 //  64 x 64 x 4-split weight tiles with fp32 slabs and a separate reduce) took 52 + 32 + 64 us per step:
 //  latency-bound dependent L2 round trips and a serial 256-deep bias loop, not MFMA or HBM.
