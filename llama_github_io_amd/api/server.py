@@ -158,9 +158,10 @@ def _multipart_first_file(body: bytes, boundary: str):
     return body, "upload"
 
 
-def create_app(client_disconnect_timeout: float | None = None):
+def create_app(client_disconnect_timeout: float | None = None, login=None):
     """``client_disconnect_timeout`` (seconds; env ``H2O_CLIENT_DISCONNECT_TIMEOUT``) starts the
-    ClientDisconnectCheckThread equivalent (``api/clients.py``)."""
+    ClientDisconnectCheckThread equivalent (``api/clients.py``). ``login`` (``api/security.LoginConfig``): the
+    ``-hash_login -login_conf [-form_auth -session_timeout]`` authentication of every route."""
     if FastAPI is None:
         raise RuntimeError("fastapi is not installed")
     runtime.init()
@@ -917,17 +918,33 @@ def create_app(client_disconnect_timeout: float | None = None):
         media = "text/html" if name.endswith(".html") else "application/javascript"
         return FileResponse(path, media_type=media)
 
+    if login is not None:
+        from . import security
+        security.install(app, login.validate())
     return app
 
 
-def main():
+def main(argv=None):
     import argparse
     import uvicorn
+    from .security import LoginConfig
     ap = argparse.ArgumentParser()
-    ap.add_argument("--port", type=int, default=54321)
-    ap.add_argument("--ip", default="127.0.0.1")
-    a = ap.parse_args()
-    uvicorn.run(create_app(), host=a.ip, port=a.port, log_level="warning")
+    ap.add_argument("--port", "-port", type=int, default=54321)
+    ap.add_argument("--ip", "-ip", default="127.0.0.1")
+    # H2O.java login options (single dash accepted as in `java -jar h2o.jar -hash_login -login_conf realm.properties`)
+    for flag in ("hash_login", "ldap_login", "kerberos_login", "spnego_login", "pam_login", "form_auth"):
+        ap.add_argument(f"--{flag}", f"-{flag}", action="store_true")
+    ap.add_argument("--login_conf", "-login_conf", default=None)
+    ap.add_argument("--session_timeout", "-session_timeout", type=int, default=0)
+    a = ap.parse_args(argv)
+    login = LoginConfig(hash_login=a.hash_login, ldap_login=a.ldap_login, kerberos_login=a.kerberos_login,
+                        spnego_login=a.spnego_login, pam_login=a.pam_login, login_conf=a.login_conf,
+                        form_auth=a.form_auth, session_timeout=a.session_timeout)
+    try:
+        login.validate()
+    except ValueError as e:
+        ap.error(str(e))
+    uvicorn.run(create_app(login=login), host=a.ip, port=a.port, log_level="warning")
 
 
 if __name__ == "__main__":
