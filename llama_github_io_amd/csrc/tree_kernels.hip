@@ -2427,6 +2427,183 @@ __global__ void k_leaf_values(const double* __restrict__ leafsum, int n, int log
   out[i] = leaf_value(leafsum[2 * i], leafsum[2 * i + 1], v);
 }
 
+// ------------------------------------------------------------------------------------------------
+// k_hist_root16: the ROOT histogram of the wide-bin (AUTO = UniformAdaptive, nbins_top_level 1024) layout from a
+// 16-bit fine-bin plane instead of the engine's byte columns. A wide numeric feature's n engine columns hold the
+// interleaved edge subsets e[k::n] (ops/binning.py), so the sum of its n column bytes is its fine bin
+// t = #{edges <= x} (NA: 1023) and column k's bin is (t - k + n - 1) / n: the root needs ONE fine histogram per
+// feature, read from 2 bytes per row and feature, instead of n byte histograms from n bytes (the tiered byte layout
+// spreads a feature's columns over up to 4 32-byte planes: 4 x 352 MB and 4 atomics per row and feature at 11M x 28).
+// Packed modes only (one int64 plane): entry (t, slot) at (t * 16 + slot) * 8 bytes, 1024 x 16 x 8 = 128 KiB, one
+// 16-wave block per CU. Block (x, y) = the tile range of the standard root pass's block x (same partial slot, so
+// k_hist_reduce is unchanged) and fine plane y (16 features = 8 words per row). A word carries 2 features; rows of
+// odd parity add its high half first, so the 16 lanes of a ds_add_u64 group (2 rows x 8 words) hit 16 distinct
+// slots = 16 distinct bank pairs (bank = 32 (t & 1) + 2 slot). The flush rebuilds every engine column of the plane's
+// features from the fine histogram (n entries per (column, bin)) into the standard [bin][F][2] partial slot.
+#define R16_NB 1024
+#define R16_NA 1023
+#define R16_FS 16                     // fine features per plane / block
+#define R16_LDS (R16_NB * R16_FS * 8 + R16_FS * 4 + 64 * 8)
+template <bool UNIT>
+__global__ __launch_bounds__(BLK) void k_hist_root16(
+    const unsigned* __restrict__ fine32 /*[planes][N][8] words (2 x uint16)*/, const float* __restrict__ aw,
+    const float* __restrict__ ay, long long N, const int* __restrict__ meta, const int* __restrict__ fcol /*[slots][4]*/,
+    const int* __restrict__ fnc /*[slots]: engine columns of the slot's feature (0: empty)*/, int F,
+    double* __restrict__ partials, int slot_doubles, const double* __restrict__ qs, int f32) {
+  extern __shared__ __attribute__((aligned(16))) long long smem64[];
+  long long* h = smem64;
+  float* nayy = (float*)(smem64 + R16_NB * R16_FS);
+  double* red = (double*)(nayy + R16_FS);
+  const int n_tiles = meta[2];
+  if (n_tiles <= 0) return;
+  const int per = (n_tiles + gridDim.x - 1) / gridDim.x;
+  const int t0 = blockIdx.x * per, t1 = min(n_tiles, t0 + per);
+  if (t0 >= t1) return;
+  const long long rb = (long long)t0 * TILE, re = min(N, (long long)t1 * TILE);
+  const int ft = blockIdx.y;
+  const unsigned* w32 = fine32 + (size_t)ft * (size_t)N * 8;
+  const int g = threadIdx.x / LPR, j = threadIdx.x % LPR;
+  const bool lead = j == 0 && ft == 0;
+  const float sa = (float)qs[10], sb = (float)qs[12], sp = (float)qs[4];
+  const int pshift = (int)qs[12];
+  const double inv_w = qs[11], inv_p = qs[5];
+  constexpr int UNR = 8;
+  char* Hb = (char*)h;
+  const unsigned slo = (unsigned)(2 * j) * 8u, shi = (unsigned)(2 * j + 1) * 8u;
+  double wyy_blk = 0.0;
+  bool acc = false;
+  for (long long ws = rb; ws < re; ws += PACK_MAX) {
+    const long long we = min(re, ws + PACK_MAX);
+    for (int i = threadIdx.x; i < R16_NB * R16_FS; i += BLK) h[i] = 0ll;
+    if (threadIdx.x < R16_FS) nayy[threadIdx.x] = 0.f;
+    __syncthreads();
+    float wyy = 0.f;
+    for (long long base = ws; base < we; base += (long long)RPI * UNR) {
+      unsigned wd[UNR];
+      float yv[UNR], wv[UNR];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const long long row = min(base + g + (long long)u * RPI, we - 1);
+        wd[u] = w32[(size_t)row * 8 + j];
+        yv[u] = ay[row];
+        wv[u] = UNIT ? 1.f : (aw ? aw[row] : 1.f);
+      }
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const long long row = base + g + (long long)u * RPI;
+        if (row >= we) continue;
+        const long long qa = UNIT ? (1ll << PACK_SHIFT) + (long long)(int)(yv[u] * sp) : qpack(wv[u], yv[u], sp, sa, sb);
+        const unsigned w = wd[u];
+        const unsigned tl = w & 0xFFFFu, th = w >> 16;
+        // row parity: even rows add the low feature first, odd rows the high one (distinct slots per lane group)
+        const bool odd = (row & 1) != 0;
+        const unsigned t_a = odd ? th : tl, t_b = odd ? tl : th;
+        const unsigned s_a = odd ? shi : slo, s_b = odd ? slo : shi;
+        atomicAdd((unsigned long long*)(Hb + ((t_a << 7) + s_a)), (unsigned long long)qa);
+        atomicAdd((unsigned long long*)(Hb + ((t_b << 7) + s_b)), (unsigned long long)qa);
+        const float yy = UNIT ? yv[u] * yv[u] : row_yy(wv[u], yv[u]);
+        if (lead) wyy += yy;
+        if (tl == R16_NA) atomicAdd(nayy + 2 * j, yy);
+        if (th == R16_NA) atomicAdd(nayy + 2 * j + 1, yy);
+      }
+    }
+    double v[4] = {(double)wyy, 0.0, 0.0, 0.0};
+    block_sum4(v, red);
+    __syncthreads();
+    wyy_blk = v[0];
+    // flush: every engine column of the plane's features, [bin][F][2] (count * inv_w, wY * inv_p)
+    double* part = partials + (size_t)blockIdx.x * slot_doubles;
+    // (a wave covers the 64 (feature, subset) columns of one bin: its stores stay inside one [F][2] bin row)
+    for (int i = threadIdx.x; i < R16_FS * 4 * NBIN; i += BLK) {
+      const int bin = i >> 6, sl = (i >> 2) & 15, k = i & 3;
+      const int slot = ft * R16_FS + sl;
+      const int n = fnc[slot];
+      if (k >= n) continue;
+      const int col = fcol[slot * 4 + k];
+      long long q = 0;
+      if (bin == NA_BIN) {
+        q = h[R16_NA * R16_FS + sl];
+      } else {
+        // t with (t - k + n - 1) / n == bin: t = n * bin + k - m, m = 0 .. n-1, t >= 0
+        for (int m = 0; m < n; ++m) {
+          const int t = n * bin + k - m;
+          if (t >= 0 && t < R16_NA) q += h[t * R16_FS + sl];
+        }
+      }
+      long long c, val;
+      unpack(q, c, val, pshift);
+      const double dc = (double)c * inv_w, dv = (double)val * inv_p;
+      const size_t e2 = (size_t)bin * 2 * F + 2 * col;
+      if (f32) {
+        float2* p2 = (float2*)((float*)part + e2);
+        float2 o = make_float2((float)dc, (float)dv);
+        if (acc) { const float2 a = *p2; o = make_float2((float)((double)a.x + dc), (float)((double)a.y + dv)); }
+        *p2 = o;
+      } else {
+        double2* p2 = (double2*)(part + e2);
+        double2 o = make_double2(dc, dv);
+        if (acc) { const double2 a = *p2; o.x += a.x; o.y += a.y; }
+        *p2 = o;
+      }
+    }
+    for (int i = threadIdx.x; i < R16_FS * 4; i += BLK) {
+      const int sl = i >> 2, k = i & 3, slot = ft * R16_FS + sl;
+      if (k >= fnc[slot]) continue;
+      const size_t e2 = (size_t)F * 2 * NBIN + fcol[slot * 4 + k];
+      if (f32) put_partial((float*)part + e2, (double)nayy[sl], acc);
+      else put_partial(part + e2, (double)nayy[sl], acc);
+    }
+    if (threadIdx.x == 0 && ft == 0) {
+      const size_t e2 = (size_t)F * 2 * NBIN + F;
+      if (f32) put_partial((float*)part + e2, wyy_blk, acc);
+      else put_partial(part + e2, wyy_blk, acc);
+    }
+    acc = true;
+    __syncthreads();
+  }
+}
+
+// Fine planes of k_hist_root16 from the engine's planar byte bins (once per training): row r's slot s = the sum of
+// the bytes of its feature's engine columns, 1023 when the feature is NA (all of its columns hold NA_BIN). One
+// thread per row reads the row's 32-byte piece of every plane (coalesced) and accumulates into its LDS column.
+__global__ __launch_bounds__(256) void k_fine16_build(const uint8_t* __restrict__ master, int planes, long long N,
+                                                      const int* __restrict__ cslot /*[planes * 32] slot or -1*/,
+                                                      int nslot, unsigned short* __restrict__ fine) {
+  __shared__ unsigned short acc[64][256];
+  const int tid = threadIdx.x;
+  const long long row = (long long)blockIdx.x * 256 + tid;
+  for (int k = 0; k < nslot; ++k) acc[k][tid] = 0;
+  if (row >= N) return;
+  for (int pl = 0; pl < planes; ++pl) {
+    const uint4* src = (const uint4*)(master + ((size_t)pl * (size_t)N + (size_t)row) * 32);
+    const uint4 v0 = src[0], v1 = src[1];
+    const unsigned wd[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+    for (int c = 0; c < 32; ++c) {
+      const int sl = cslot[pl * 32 + c];
+      if (sl < 0) continue;
+      const unsigned b = (wd[c >> 2] >> (8 * (c & 3))) & 0xFFu;
+      if (b == NA_BIN) acc[sl][tid] = 0x8000;
+      else acc[sl][tid] = (unsigned short)(acc[sl][tid] + b);
+    }
+  }
+  const int p16 = (nslot + 15) / 16;
+  for (int q = 0; q < p16; ++q) {
+    unsigned w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      unsigned lo = 0, hi = 0;
+      const int s0 = q * 16 + 2 * i, s1 = s0 + 1;
+      if (s0 < nslot) { lo = acc[s0][tid]; lo = (lo & 0x8000u) ? 1023u : lo; }
+      if (s1 < nslot) { hi = acc[s1][tid]; hi = (hi & 0x8000u) ? 1023u : hi; }
+      w[i] = lo | (hi << 16);
+    }
+    uint4* dst = (uint4*)(fine + ((size_t)q * (size_t)N + (size_t)row) * 16);
+    dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    dst[1] = make_uint4(w[4], w[5], w[6], w[7]);
+  }
+}
+
 // ================================================================================================
 // C ABI launchers (called through ctypes with raw device pointers and the current HIP stream).
 static int hist_dbg() {   // H2O_HIST_DBG: diagnostics of the histogram pass (A/B timing only; never in a real run)
@@ -2545,6 +2722,32 @@ int h2o_hist_build(const void* bins, int stride, const void* aw, const void* ay,
   return (int)hipGetLastError();
 }
 
+
+// fine: [ceil(nslot / 16)][N][16] uint16 (see k_fine16_build); nslot <= 64
+int h2o_fine16_build(const void* master, int planes, long long N, const void* cslot, int nslot, void* fine,
+                     hipStream_t s) {
+  if (nslot < 1 || nslot > 64 || planes < 1 || N <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_fine16_build, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, (const uint8_t*)master, planes,
+                     N, (const int*)cslot, nslot, (unsigned short*)fine);
+  return (int)hipGetLastError();
+}
+
+// Root histogram from the 16-bit fine planes (k_hist_root16): packed modes only (packed 1 / 2); planes = slots / 16.
+int h2o_hist_root16(const void* fine, int planes, const void* aw, const void* ay, long long N, const void* meta,
+                    const void* fcol, const void* fnc, int F, void* partials, int slot_doubles, const void* qs, int grid,
+                    int f32, hipStream_t s) {
+  if (planes < 1 || grid < 1 || N <= 0) return (int)hipErrorInvalidValue;
+  const dim3 gr(grid, planes);
+  if (aw == nullptr)
+    hipLaunchKernelGGL((k_hist_root16<true>), gr, dim3(BLK), R16_LDS, s, (const unsigned*)fine, (const float*)aw,
+                       (const float*)ay, N, (const int*)meta, (const int*)fcol, (const int*)fnc, F, (double*)partials,
+                       slot_doubles, (const double*)qs, f32);
+  else
+    hipLaunchKernelGGL((k_hist_root16<false>), gr, dim3(BLK), R16_LDS, s, (const unsigned*)fine, (const float*)aw,
+                       (const float*)ay, N, (const int*)meta, (const int*)fcol, (const int*)fnc, F, (double*)partials,
+                       slot_doubles, (const double*)qs, f32);
+  return (int)hipGetLastError();
+}
 
 // grid: the G the matching h2o_hist_build ran with; out / hist_next may be null (see k_hist_reduce).
 // out: compact build slots of ostride values (0: slot_doubles), fp32 when out_f32 (the exchange's wire dtype)
@@ -2882,6 +3085,11 @@ struct TreePlan {
   void* lvl2;                 // [N] uint8: the root route's level-2 node / 128 + leaf per row (narrow runs; or null)
   void* fdir;                 // [N] uint8: the root split's side per row (k_row_dir; narrow planar runs, or null)
   int num_plane, pad4;        // aux plane of the leaf-sum numerator (2; 1 when the step kernel elides num == wY)
+  // root pass of the wide-bin layout from 16-bit fine planes (k_hist_root16; packed modes; null: the byte columns)
+  void* fine16;               // [f16_planes][N][16] uint16 fine bins per original feature
+  void* f16col;               // [f16_planes * 16][4] int32: engine column of subset k (or -1)
+  void* f16n;                 // [f16_planes * 16] int32: the feature's engine columns (0: empty slot)
+  int f16_planes, pad5;
 };
 
 // op codes / dtypes of the collective transport
@@ -2947,6 +3155,10 @@ int h2o_tree_root(const TreePlan* P, hipStream_t s) {
   if (P->compute_amax) TP_CHECK(h2o_amax(P->aux, P->N, P->amax_bits, s));
   TP_CHECK(h2o_qscale(P->amax_bits, P->qs, P->counters, P->N, P->packed == 2, s));
   const int g0 = P->tiles_cap[0] < P->grid ? P->tiles_cap[0] : P->grid;
+  if (P->fine16 && P->packed && !P->sliced && tp_fcut(P, 0) == 0)
+    TP_CHECK(h2o_hist_root16(P->fine16, P->f16_planes, P->unit ? nullptr : tp_aux(P, 0), tp_aux(P, 1), P->N, P->meta[0],
+                             P->f16col, P->f16n, P->F, P->partials, P->slot, P->qs, g0, P->pf32, s));
+  else
   TP_CHECK(h2o_hist_build(P->master, P->stride, P->unit ? nullptr : tp_aux(P, 0), tp_aux(P, 1), P->nodes[0], P->bp[0],
                           P->meta[0], P->F, P->partials, P->slot, P->qs, g0, P->packed, nullptr, nullptr, P->pf32, P->N,
                           P->planar | (P->no_na << 1), P->nbins_f, P->fine_f, tp_planes(tp_fcut(P, 0)), nullptr, s));

@@ -63,6 +63,7 @@ _HIP_SIGS = {
     "h2o_qscale": [c_void_p, c_void_p, c_void_p, c_ll, c_int, c_void_p],
     "h2o_score_hist": [c_void_p, c_void_p, c_void_p, c_ll, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "h2o_snap_copy": [c_void_p, c_void_p, c_ll, c_void_p],
+    "h2o_fine16_build": [c_void_p, c_int, c_ll, c_void_p, c_int, c_void_p, c_void_p],
     "h2o_host_dev_ptr": [c_void_p, c_void_p],
     "h2o_hist_reduce": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
                         c_void_p, c_int, c_int, c_int, c_int, c_void_p],

@@ -587,7 +587,8 @@ class _TreePlan(ctypes.Structure):
                 [("fgroup", _vp)] + [("coll_fn", _vp), ("coll_ctx", _vp)] +
                 [(n, _ci) for n in ("W", "cf32", "cand_fs", "dist")] + [(n, _vp) for n in ("hsend", "cand_all", "lsx")] +
                 [("fine_f", _vp)] + [(n, _ci) for n in ("lo_F", "lo_from", "mid_F", "mid_from")] + [("lvl2", _vp), ("fdir", _vp)] +
-                [("num_plane", _ci), ("pad4", _ci)])
+                [("num_plane", _ci), ("pad4", _ci)] +
+                [(n, _vp) for n in ("fine16", "f16col", "f16n")] + [("f16_planes", _ci), ("pad5", _ci)])
 
 
 class _Arena:
@@ -820,6 +821,8 @@ class GpuTreeBuilder:
         ``n_mid``: leading columns of the narrow views (:func:`narrow_cut`)."""
         enc = encode_groups(fgroup)
         self.fgroup = None if enc is None else torch.as_tensor(enc, device=self.dev).contiguous()
+        self._fgroup_np = None if fgroup is None else np.asarray(fgroup, dtype=np.int64)
+        self._fine16 = None
         self.fine_f = fine_columns(fgroup, self.iscat_np, self.F)
         if self.fine_f is not None:
             self.fine_f = torch.as_tensor(self.fine_f, device=self.dev).contiguous()
@@ -828,6 +831,7 @@ class GpuTreeBuilder:
             self._plan.fgroup = 0 if self.fgroup is None else self.fgroup.data_ptr()
             self._plan.fine_f = 0 if self.fine_f is None else self.fine_f.data_ptr()
             self._set_plan_narrow(self._plan)
+            self._set_plan_fine16(self._plan)
 
     def _set_plan_narrow(self, P):
         mid, lo = narrow_cut(self.p, self.n_low, self.n_mid, self.F)
@@ -841,6 +845,63 @@ class GpuTreeBuilder:
         on = lo >= 0 and self.planar
         P.lvl2 = self._lvl2.data_ptr() if on else 0
         P.fdir = self._fdir.data_ptr() if on else 0
+
+    def _fine16_map(self):
+        """Slot maps of the root pass from 16-bit fine planes (k_hist_root16), or None when it does not apply: the
+        wide-bin layout (several engine columns per numeric feature holding the interleaved edge subsets e[k::n]),
+        planar bins, at most 4 columns per feature and 64 features, no wide categorical. Returns (cslot [planes*32],
+        fcol [slots][4], fn [slots], nslot); slots are the original features in first-column order, a feature's
+        columns ordered by subset k (= by first edge)."""
+        if os.environ.get("H2O_HIST_ROOT16", "1") == "0" or not self.planar or self.dev.type != "cuda":
+            return None
+        fg = getattr(self, "_fgroup_np", None)
+        if fg is None or not (self.n_low or self.n_mid) or self.p.edges is None:
+            return None
+        F = self.F
+        edges = np.asarray(self.p.edges, dtype=np.float32)
+        order, cols = [], {}
+        for c in range(F):
+            g = int(fg[c])
+            if g not in cols:
+                cols[g] = []
+                order.append(g)
+            cols[g].append(c)
+        nslot = len(order)
+        if nslot > 64:
+            return None
+        ns = (nslot + 15) // 16 * 16
+        cslot = np.full(self.master.shape[0] * 32, -1, dtype=np.int32)
+        fcol = np.full((ns, 4), -1, dtype=np.int32)
+        fn = np.zeros(ns, dtype=np.int32)
+        for s_, g in enumerate(order):
+            cs = cols[g]
+            if len(cs) > 4 or (len(cs) > 1 and any(int(self.iscat_np[c]) for c in cs)):
+                return None
+            cs = sorted(cs, key=lambda c: float(edges[c, 0]))      # subset k holds edge k first
+            fcol[s_, :len(cs)] = cs
+            fn[s_] = len(cs)
+            cslot[cs] = s_
+        return cslot, fcol, fn, nslot
+
+    def _set_plan_fine16(self, P):
+        P.fine16 = P.f16col = P.f16n = 0
+        P.f16_planes = 0
+        m = self._fine16_map()
+        if m is None:
+            return
+        cslot, fcol, fn, nslot = m
+        dev = self.dev
+        if getattr(self, "_fine16", None) is None:
+            planes16 = (nslot + 15) // 16
+            self._f16_cslot = torch.as_tensor(cslot, device=dev)
+            self._f16col = torch.as_tensor(fcol.reshape(-1), device=dev)
+            self._f16n = torch.as_tensor(fn, device=dev)
+            self._fine16 = torch.empty(planes16 * self.N * 16, dtype=torch.int16, device=dev)
+            nat.call("h2o_fine16_build", self.master.data_ptr(), int(self.master.shape[0]), self.N,
+                     self._f16_cslot.data_ptr(), nslot, self._fine16.data_ptr(), nat.stream_ptr(dev))
+            self._f16_planes = planes16
+        P.fine16, P.f16col, P.f16n = self._fine16.data_ptr(), self._f16col.data_ptr(), self._f16n.data_ptr()
+        P.f16_planes = self._f16_planes
 
     def _set_plan_ic(self, P):
         if self.ic_map is None:
@@ -882,6 +943,7 @@ class GpuTreeBuilder:
         P.fgroup = 0 if fg is None else fg.data_ptr()
         P.fine_f = 0 if self.fine_f is None else self.fine_f.data_ptr()     # used only under H2O_HIST_FINE=1
         self._set_plan_narrow(P)
+        self._set_plan_fine16(P)
         P.sliced, P.fs0, P.fsn, P.sslot = int(self.sliced), self.fs0, self.fsn, self.sslot
         P.planar = int(self.planar)
         P.no_na = int(self._no_na())

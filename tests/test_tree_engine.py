@@ -660,6 +660,43 @@ def test_gpu_wide_bins_match_reference(case, fine, monkeypatch):
     assert torch.equal(ref.leaf_of_row, gb.leaf_of_row.cpu())
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("unit", [True, False])
+def test_gpu_root16_matches_reference(unit, monkeypatch):
+    """The wide-bin root pass from 16-bit fine planes (k_hist_root16: one fine histogram per feature, the engine
+    columns rebuilt in the flush) in the packed modes the GBM trainer runs (unit weights / a 0-1 row mask), NA rows
+    included: identical decisions, left weights and leaf assignment vs RefTreeBuilder, and the byte-column root pass
+    (H2O_HIST_ROOT16=0) gives the same tree."""
+    X, y, info = _data(N=30000, F=10, cat=True, seed=11)
+    b = fit_binning(X, info.iscat, info.nlevels, max_bins=1016)
+    assert b.vmap is not None and b.stride >= 64 and b.n_low == X.shape[0]
+    bins = apply_binning(b, X)
+    g = y - 0.5
+    w = torch.ones_like(y) if unit else (torch.rand(y.shape, generator=torch.Generator().manual_seed(2)) < 0.8).float()
+    aux = torch.stack([w, w * g, w * g, w], 1).contiguous()
+    p = T.SplitParams(min_w=10, adapt_nbins=20, adapt_top=1024, edges=_edge_tab(b))
+    ref = T.RefTreeBuilder(bins, b.F, b.nbins, b.iscat, None, 5, p)
+    ref.set_feature_groups(b.vmap, b.n_low, b.n_mid)
+    ref.build(aux, None, 0, seed=5, leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1].clamp(min=1e-12)).float())
+    tl_r = ref.pop_levels()[0]
+    dev = torch.device("cuda", 0)
+    out = {}
+    for r16 in ("1", "0"):
+        monkeypatch.setenv("H2O_HIST_ROOT16", r16)
+        gb = T.GpuTreeBuilder(apply_binning(b, X.to(dev), planar=True), b.F, b.nbins, b.iscat, None, 5, p)
+        gb.set_feature_groups(b.vmap, b.n_low, b.n_mid)
+        gb.build(aux.to(dev), None, 0, seed=5, leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1].clamp(min=1e-12)).float(),
+                 packed=True, unit=unit)
+        assert bool(gb._plan.fine16) == (r16 == "1")
+        out[r16] = (gb.pop_levels()[0], gb.leaf_of_row.cpu())
+    for r16, (tl_g, leaf) in out.items():
+        assert tl_g.n_leaves == tl_r.n_leaves, r16
+        for dr, dg in zip(tl_r.decs, tl_g.decs):
+            assert np.array_equal(dr["feat"], dg["feat"]) and np.array_equal(dr["bin"], dg["bin"]), r16
+            np.testing.assert_allclose(dr["wl"], dg["wl"], rtol=1e-6)
+        assert torch.equal(ref.leaf_of_row, leaf), r16
+
+
 def _wide_cat_data(N=30000, L=1000, seed=3, device="cpu"):
     """A 1000-level categorical whose level set {l % 7 == 2} raises the response, next to numerics."""
     g = torch.Generator().manual_seed(seed)
