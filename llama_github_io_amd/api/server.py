@@ -936,6 +936,11 @@ def main(argv=None):
         ap.add_argument(f"--{flag}", f"-{flag}", action="store_true")
     ap.add_argument("--login_conf", "-login_conf", default=None)
     ap.add_argument("--session_timeout", "-session_timeout", type=int, default=0)
+    # HTTPS from a Java KeyStore (H2O.java -jks / -jks_pass / -jks_alias / -hostname_as_jks_alias; api/tls.py)
+    ap.add_argument("--jks", "-jks", default=None)
+    ap.add_argument("--jks_pass", "-jks_pass", default=None)
+    ap.add_argument("--jks_alias", "-jks_alias", default=None)
+    ap.add_argument("--hostname_as_jks_alias", "-hostname_as_jks_alias", action="store_true")
     a = ap.parse_args(argv)
     login = LoginConfig(hash_login=a.hash_login, ldap_login=a.ldap_login, kerberos_login=a.kerberos_login,
                         spnego_login=a.spnego_login, pam_login=a.pam_login, login_conf=a.login_conf,
@@ -944,7 +949,15 @@ def main(argv=None):
         login.validate()
     except ValueError as e:
         ap.error(str(e))
-    uvicorn.run(create_app(login=login), host=a.ip, port=a.port, log_level="warning")
+    ssl_kw = {}
+    if a.jks:
+        from .tls import pem_files
+        try:
+            cf, kf = pem_files(a.jks, a.jks_pass, a.jks_alias, a.hostname_as_jks_alias)
+        except (OSError, ValueError) as e:
+            ap.error(f"-jks {a.jks}: {e}")
+        ssl_kw = dict(ssl_certfile=cf, ssl_keyfile=kf)
+    uvicorn.run(create_app(login=login), host=a.ip, port=a.port, log_level="warning", **ssl_kw)
 
 
 if __name__ == "__main__":
