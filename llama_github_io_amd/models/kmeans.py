@@ -227,7 +227,12 @@ class KMeansTrainer:
     def _step(self, Z, w, C):
         """One Lloyd step on the device: (assign, min distance, new centers, cnt, flags [#empty, shift])."""
         if not coll.is_dist():
-            r = kmeans_lloyd_step(Z, C, w)      # MFMA step + fused center update (2 launches + the slab sum)
+            # the kernel's row weights: none for unit weights (no 40 MB weight read and no fp64 -> fp32 cast per
+            # iteration), else the fp32 copy made once per Lloyd loop
+            wk = getattr(self, "_wk", w)
+            if wk is not None and wk.numel() != Z.shape[0]:
+                wk = w
+            r = kmeans_lloyd_step(Z, C, wk)      # MFMA step + fused center update (2 launches + the slab sum)
             if r is not None:
                 d, newC, cnt, flags = r
                 return None, d, newC, cnt, flags
@@ -249,6 +254,7 @@ class KMeansTrainer:
         return newC
 
     def _lloyd(self, Z, w, C, max_it):
+        self._wk = None if getattr(self, "_unit_w", False) else w.float().contiguous()
         csc = self.p.get("cluster_size_constraints")
         if csc:
             if coll.is_dist():
@@ -308,6 +314,7 @@ class KMeansTrainer:
         N = X.shape[1]
         seed = resolve_seed(p["seed"])
         rng = np.random.default_rng(seed & 0xFFFFFFFF)
+        self._unit_w = w is None
         w = torch.ones(N, dtype=torch.float64, device=dev) if w is None else w.double()
         self.row0, self.N_glob = (coll.exclusive_offset(N) if coll.is_dist() else (0, N))
         self.ex = Expander(info, standardize=p["standardize"], use_all_factor_levels=True).fit(
