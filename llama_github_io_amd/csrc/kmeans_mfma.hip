@@ -55,13 +55,14 @@ __device__ __forceinline__ float bfly_min_idx(float v, int& idx, int mask) {
 #ifndef KM_VEC
 #define KM_VEC 0
 #endif
-// KM_VEC: stride P or P + 4 with P / 4 odd — rows 16-byte aligned (one ds_write_b128 per staged float4 group
+// KM_VEC: stride P + 8 or P + 4 with stride / 4 odd — rows 16-byte aligned (one ds_write_b128 per staged float4 group
 // instead of four ds_write_b32) and the distance GEMM's reads (c16 * Pp + 4 s + q: c16 * Pp / 4 distinct mod 16)
 // still on 64 distinct banks. MEASURED (r4, 10M x 20, k = 10, same box): 0.3965 / 0.3984 vs 0.3977 / 0.4001 ms per
-// Lloyd step — the staging stores are not the limit; kept off.
+// Lloyd step — the staging stores are not the limit; kept off. Again after the r5 phased tile: 284.3 vs 285.6 us.
 __host__ __device__ inline int km_stride(int P) {
 #if KM_VEC
-  return ((P / 4) & 1) ? P : P + 4;
+  // > P: column P of every row holds the centroid GEMM's constant 1 (the counts), see the staging loop
+  return ((P / 4) & 1) ? P + 8 : P + 4;
 #else
   int pp = P + 1;
   const int adj = pp + ((17 - pp % 32) + 32) % 32;
