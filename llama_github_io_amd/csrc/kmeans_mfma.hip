@@ -29,6 +29,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <float.h>
+#include <stdlib.h>
 
 namespace {
 
@@ -59,27 +60,28 @@ __device__ __forceinline__ float bfly_min_idx(float v, int& idx, int mask) {
 // instead of four ds_write_b32) and the distance GEMM's reads (c16 * Pp + 4 s + q: c16 * Pp / 4 distinct mod 16)
 // still on 64 distinct banks. MEASURED (r4, 10M x 20, k = 10, same box): 0.3965 / 0.3984 vs 0.3977 / 0.4001 ms per
 // Lloyd step — the staging stores are not the limit; kept off. Again after the r5 phased tile: 284.3 vs 285.6 us.
-__host__ __device__ inline int km_stride(int P) {
+// occ4: the 4-waves-per-SIMD variant (k_lloyd_mfma4) keeps the unpadded stride P + 1 unless the bank-spreading one
+// still fits four 4-wave blocks in a CU's LDS (stride <= 38).
+__host__ __device__ inline int km_stride(int P, bool occ4 = false) {
 #if KM_VEC
   // > P: column P of every row holds the centroid GEMM's constant 1 (the counts), see the staging loop
   return ((P / 4) & 1) ? P + 8 : P + 4;
 #else
   int pp = P + 1;
   const int adj = pp + ((17 - pp % 32) + 32) % 32;
-  return adj <= 52 ? adj : pp;
+  return adj <= (occ4 ? 38 : 52) ? adj : pp;
 #endif
 }
-template <int KT, int PS, int PT>
-__global__ __launch_bounds__(256) void k_lloyd_mfma(const float* __restrict__ X, int64_t N, int P,
-                                                    const float* __restrict__ C, int K,
-                                                    const float* __restrict__ w, int* __restrict__ assign,
-                                                    float* __restrict__ mind, float* __restrict__ slabs) {
+template <int KT, int PS, int PT, int G, bool OCC4>
+__device__ __forceinline__ void lloyd_body(const float* __restrict__ X, int64_t N, int P, const float* __restrict__ C,
+                                           int K, const float* __restrict__ w, int* __restrict__ assign,
+                                           float* __restrict__ mind, float* __restrict__ slabs) {
   extern __shared__ float lds[];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   const int q = lane >> 4;          // 0..3
   const int c16 = lane & 15;        // 0..15
-  const int Pp = km_stride(P);
+  const int Pp = km_stride(P, OCC4);
   float* xs = lds + (size_t)wv * KM_ROWS * Pp;
   const int64_t wave_g = (int64_t)blockIdx.x * 4 + wv;
   const int64_t n_waves = (int64_t)gridDim.x * 4;
@@ -168,7 +170,6 @@ __global__ __launch_bounds__(256) void k_lloyd_mfma(const float* __restrict__ X,
     // different sub-tiles interleave (the former per-sub-tile order serialised distance -> argmin -> shuffle ->
     // centroid chains; the stores' divergent branch split the schedule once per sub-tile).
     // G sub-tiles per phase group (registers: G x KT distance tiles live at once)
-    constexpr int G = KT == 1 ? 4 : (KT == 2 ? 2 : 1);
 #pragma unroll
     for (int g0 = 0; g0 < KM_ROWS / 16; g0 += G) {
     // ---- 1. distance GEMM: B[k = dim 4s+q][j = row c16]; the same values give ||x||^2
@@ -286,10 +287,53 @@ __global__ __launch_bounds__(256) void k_lloyd_mfma(const float* __restrict__ X,
       for (int r = 0; r < 4; ++r) out[(int64_t)(t * 16 + 4 * q + r) * (PT * 16) + u * 16 + c16] = acc[t][u][r];
 }
 
+#define KM_ARGS const float* __restrict__ X, int64_t N, int P, const float* __restrict__ C, int K, \
+                const float* __restrict__ w, int* __restrict__ assign, float* __restrict__ mind, float* __restrict__ slabs
+template <int KT, int PS, int PT>
+__global__ __launch_bounds__(256) void k_lloyd_mfma(KM_ARGS) {
+  lloyd_body<KT, PS, PT, (KT == 1 ? 4 : (KT == 2 ? 2 : 1)), false>(X, N, P, C, K, w, assign, mind, slabs);
+}
+// 4 waves / SIMD: phase groups of 2 sub-tiles (G = 4 needs more than 128 VGPRs) and the unpadded LDS stride.
+// MEASURED r5 (10M x 20, k = 10; scripts/gpu_r5_c27.sh): 287.7 us (3 waves, G = 4, stride 49) -> 258.8 us.
+template <int KT, int PS, int PT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_lloyd_mfma4(KM_ARGS) {
+  lloyd_body<KT, PS, PT, (KT == 1 ? 2 : 1), true>(X, N, P, C, K, w, assign, mind, slabs);
+}
+#undef KM_ARGS
+// shapes whose 4-wave variant compiles without spills (-Rpass-analysis=kernel-resource-usage)
+__host__ __device__ constexpr bool km_occ4(int KT, int PS, int PT) {
+  return KT == 1 && PS <= 6 && PT <= 2;
+}
+static bool km_occ4_enabled() {
+  static int v = -1;
+  if (v < 0) { const char* e = getenv("H2O_KM_OCC4"); v = (e && e[0] == '0') ? 0 : 1; }
+  return v == 1;
+}
+template <int KT, int PS, int PT>
+static bool km_use4() { return km_occ4(KT, PS, PT) && km_occ4_enabled(); }
+
+template <int KT, int PS, int PT>
+hipError_t km_occ(int* per, int P) {
+  const bool o4 = km_use4<KT, PS, PT>();
+  const size_t lds = ((size_t)4 * KM_ROWS * km_stride(P, o4) + 4 * KM_ROWS) * sizeof(float);
+  if constexpr (km_occ4(KT, PS, PT)) {
+    if (o4) return hipOccupancyMaxActiveBlocksPerMultiprocessor(per, k_lloyd_mfma4<KT, PS, PT>, 256, lds);
+  }
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(per, k_lloyd_mfma<KT, PS, PT>, 256, lds);
+}
+
 template <int KT, int PS, int PT>
 int launch(const float* X, long long N, int P, const float* C, int K, const float* w, int* assign, float* mind,
            float* slabs, int grid, hipStream_t s) {
-  const size_t lds = ((size_t)4 * KM_ROWS * km_stride(P) + 4 * KM_ROWS) * sizeof(float);   // 4 slices + 4 x 64 weights
+  const bool o4 = km_use4<KT, PS, PT>();
+  const size_t lds = ((size_t)4 * KM_ROWS * km_stride(P, o4) + 4 * KM_ROWS) * sizeof(float);   // 4 slices + 4 x 64 weights
+  if constexpr (km_occ4(KT, PS, PT)) {
+    if (o4) {
+      hipLaunchKernelGGL((k_lloyd_mfma4<KT, PS, PT>), dim3(grid), dim3(256), lds, s, X, (int64_t)N, P, C, K, w, assign,
+                         mind, slabs);
+      return (int)hipGetLastError();
+    }
+  }
   hipLaunchKernelGGL((k_lloyd_mfma<KT, PS, PT>), dim3(grid), dim3(256), lds, s, X, (int64_t)N, P, C, K, w, assign,
                      mind, slabs);
   return (int)hipGetLastError();
@@ -360,10 +404,9 @@ int h2o_kmeans_mfma_grid(int K, int P) {
   int dev = 0, cus = 0, per = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return 0;
-  const size_t lds = ((size_t)4 * KM_ROWS * km_stride(P) + 4 * KM_ROWS) * sizeof(float);
   const int KT = sh[0], PS = sh[1], PT = sh[2];
   hipError_t e = hipErrorInvalidValue;
-#define O(kt, ps, pt) if (KT == kt && PS == ps && PT == pt) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_lloyd_mfma<kt, ps, pt>, 256, lds)
+#define O(kt, ps, pt) if (KT == kt && PS == ps && PT == pt) e = km_occ<kt, ps, pt>(&per, P)
   O(1, 4, 1); O(1, 4, 2); O(1, 6, 2); O(1, 8, 2); O(1, 8, 3); O(1, 16, 3); O(1, 16, 4); O(1, 16, 5);
   O(2, 4, 1); O(2, 4, 2); O(2, 6, 2); O(2, 8, 2); O(2, 8, 3); O(2, 16, 3); O(2, 16, 4); O(2, 16, 5);
   O(4, 4, 1); O(4, 4, 2); O(4, 6, 2); O(4, 8, 2); O(4, 8, 3); O(4, 16, 3); O(4, 16, 4); O(4, 16, 5);
