@@ -295,9 +295,15 @@ __global__ __launch_bounds__(256) void k_lloyd_mfma(KM_ARGS) {
 }
 // 4 waves / SIMD: phase groups of 2 sub-tiles (G = 4 needs more than 128 VGPRs) and the unpadded LDS stride.
 // MEASURED r5 (10M x 20, k = 10; scripts/gpu_r5_c27.sh): 287.7 us (3 waves, G = 4, stride 49) -> 258.8 us.
+#ifndef KM_W4
+#define KM_W4 4         // A/B: waves per SIMD of the high-occupancy variant (5 with G = 1 spills: 253 -> 329 us)
+#endif
+#ifndef KM_G4
+#define KM_G4 2         // A/B: its phase-group size (K <= 16)
+#endif
 template <int KT, int PS, int PT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_lloyd_mfma4(KM_ARGS) {
-  lloyd_body<KT, PS, PT, (KT == 1 ? 2 : 1), true>(X, N, P, C, K, w, assign, mind, slabs);
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KM_W4, KM_W4))) void k_lloyd_mfma4(KM_ARGS) {
+  lloyd_body<KT, PS, PT, (KT == 1 ? KM_G4 : 1), true>(X, N, P, C, K, w, assign, mind, slabs);
 }
 #undef KM_ARGS
 // shapes whose 4-wave variant compiles without spills (-Rpass-analysis=kernel-resource-usage)
@@ -389,7 +395,8 @@ int h2o_kmeans_update(const double* tot, int ldt, int K, int P, const float* C, 
 int h2o_kmeans_mfma_shape(int K, int P, int* out) {
   if (K < 1 || P < 1 || K > 64 || P > 64) return 0;
   const int KT = K <= 16 ? 1 : (K <= 32 ? 2 : 4);
-  const int PS = P <= 16 ? 4 : (P <= 24 ? 6 : (P <= 32 ? 8 : 16));   // prefetch float4 groups per lane >= P / 4
+  // float4 groups per lane >= P / 4 (MEASURED r5: a PS = 5 shape for P = 20 saved 2 VGPRs, 263 vs 253-259 us: not kept)
+  const int PS = P <= 16 ? 4 : (P <= 24 ? 6 : (P <= 32 ? 8 : 16));
   const int PT = (P + 1 + 15) / 16;
   out[0] = KT; out[1] = PS; out[2] = PT;
   return 1;
