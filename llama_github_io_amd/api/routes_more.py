@@ -391,6 +391,29 @@ def register(app, _params, _unquote, _model_json):
         return {"__meta": v3.meta("Word2VecTransformV3", "Word2VecTransform"), "model": v3.model_key(m.key),
                 "words_frame": v3.frame_key(words_frame), "vectors_frame": v3.frame_key(dest)}
 
+    @app.get("/3/TargetEncoderTransform")
+    def te_transform(request: Request):
+        """TargetEncoderHandler.transform (h2o-extensions/target-encoder .../TargetEncoderHandler.java:14-37):
+        blending / inflection_point / smoothing / noise not given (or inflection_point, smoothing < 0, noise < -1)
+        keep the model's values; returns the transformed frame's key."""
+        q = {k: _unquote(v) for k, v in request.query_params.items()}
+        m = get_model(q["model"])
+        fr = get_frame(q["frame"])
+        tb = lambda v: str(v).lower() in ("true", "1")     # noqa: E731
+        kw = dict(as_training=tb(q.get("as_training", "false")))
+        if "blending" in q:
+            kw["blending"] = tb(q["blending"])
+        for k in ("inflection_point", "smoothing"):
+            if k in q and float(q[k]) >= 0:
+                kw[k] = float(q[k])
+        if "noise" in q and float(q["noise"]) >= -1:
+            kw["noise"] = float(q["noise"])
+        out = m.transform(fr, **kw)
+        dest = dkv.new_key("te_transform")
+        out.frame_id = dest
+        dkv.put(dest, out)
+        return v3.frame_key(dest)
+
     # ------------------------------------------------------------------------- persistence
     @app.get("/3/Models.fetch.bin/{mid}")
     def fetch_bin(mid: str):

@@ -264,3 +264,22 @@ def test_word2vec_word_models_group_cooccurring_words(word_model):
     within = np.mean([cos(a, b) for g in (A, Bw) for a in g for b in g if a < b])
     across = np.mean([cos(a, b) for a in A for b in Bw])
     assert within > across + 0.3, (within, across)
+
+
+def test_target_encoder_transform_rest(df):
+    """GET /3/TargetEncoderTransform (TargetEncoderHandler.transform): model defaults unless overridden; the
+    returned key names the transformed frame, equal to the in-process transform."""
+    te = H2OTargetEncoderEstimator(blending=True, inflection_point=5, smoothing=10, noise=0)
+    te.train(x=["c"], y="y", training_frame=df)
+    r = h2o.api("GET /3/TargetEncoderTransform", data=dict(model=te.model_id, frame=df.frame_id, as_training=False))
+    out = h2o.get_frame(r["name"])
+    ref = te.transform(df)
+    assert out.names == ref.names and np.allclose(out["c_te"].as_data_frame()["c_te"].to_numpy(),
+                                                    ref["c_te"].as_data_frame()["c_te"].to_numpy())
+    # blending=false overrides the model's blending: the plain posterior per level
+    r2 = h2o.api("GET /3/TargetEncoderTransform", data=dict(model=te.model_id, frame=df.frame_id, blending=False,
+                                                             noise=-2))
+    v = h2o.get_frame(r2["name"]).as_data_frame()
+    d = df.as_data_frame()
+    post = d.assign(y1=(d.y.astype(str) == "1").astype(float)).groupby("c").y1.mean()
+    assert np.allclose(v["c_te"].to_numpy(), d.c.map(post).to_numpy())
