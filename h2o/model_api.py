@@ -251,6 +251,19 @@ class ModelBaseAPI:
             raise ValueError(f"{self.algo} models have no network")
         return m
 
+    def deepfeatures(self, test_data, layer):
+        """Hidden layer ``layer`` (0-based index, or the layer name) of a DeepLearning model on ``test_data``
+        (model_base.py deepfeatures: /4/Predictions deep_features_hidden_layer)."""
+        if test_data is None:
+            raise ValueError("Must specify test data")
+        m = self._dl()
+        if not str(layer).isdigit():
+            names = [f"hidden_{i}" for i in range(len(list(m.net.hidden)))]
+            if layer not in names:
+                raise ValueError(f"unknown hidden layer {layer!r} (one of {names})")
+            layer = names.index(layer)
+        return m.deepfeatures(test_data, int(layer))
+
     def biases(self, vector_id=0):
         from llama_github_io_amd.frame import H2OFrame
         m = self._dl()

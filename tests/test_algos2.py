@@ -283,3 +283,14 @@ def test_target_encoder_transform_rest(df):
     d = df.as_data_frame()
     post = d.assign(y1=(d.y.astype(str) == "1").astype(float)).groupby("c").y1.mean()
     assert np.allclose(v["c_te"].to_numpy(), d.c.map(post).to_numpy())
+
+
+def test_deepfeatures_api(df):
+    """ModelBase.deepfeatures (model_base.py:382): hidden layer activations of a DeepLearning model."""
+    from h2o.estimators import H2ODeepLearningEstimator
+    m = H2ODeepLearningEstimator(hidden=[5, 3], epochs=2, seed=1)
+    m.train(x=["a", "b"], y="y", training_frame=df)
+    f = m.deepfeatures(df, 1)
+    assert f.names == ["DF.L2.C1", "DF.L2.C2", "DF.L2.C3"] and f.nrows == df.nrows
+    with pytest.raises(ValueError):
+        m.deepfeatures(None, 0)
