@@ -61,6 +61,63 @@ class H2OAutoML:
     def predict(self, test_data):
         return self.leader.predict(test_data)
 
+    # ---- h2o-py/h2o/automl/_base.py / _estimator.py surface
+    @property
+    def key(self):
+        return self.project_name
+
+    def detach(self):
+        """Release the client-side job handle (the AutoML run and its models stay in the store)."""
+        self._job = None
+
+    @property
+    def training_info(self):
+        """event_log name / value pairs of the run: start / stop epochs and duration."""
+        a = self._aml
+        t0, t1 = getattr(a, "start_epoch", None), getattr(a, "stop_epoch", None)
+        if t0 is None:
+            return {}
+        out = {"start_epoch": str(int(t0)), "creation_epoch": str(int(t0))}
+        if t1 is not None:
+            out.update(stop_epoch=str(int(t1)), duration_secs=str(int(round(t1 - t0))))
+        return out
+
+    @property
+    def modeling_steps(self):
+        """The executed plan, re-injectable as ``modeling_plan`` of a new run: [{name, steps: [{id, group, weight}]}]."""
+        out, idx = [], {}
+        for fam, sid, group, w in getattr(self._aml, "executed_steps", []):
+            if fam not in idx:
+                idx[fam] = len(out)
+                out.append(dict(name=fam, steps=[]))
+            out[idx[fam]]["steps"].append(dict(id=sid, group=int(group), weight=int(w)))
+        return out
+
+    def get_leaderboard(self, extra_columns=None):
+        return get_leaderboard(self, extra_columns)
+
+    def download_mojo(self, path=".", get_genmodel_jar=False, genmodel_name=""):
+        return self.leader.download_mojo(path, get_genmodel_jar, genmodel_name)
+
+    def download_pojo(self, path="", get_genmodel_jar=False, genmodel_name=""):
+        from . import download_pojo
+        return download_pojo(self.leader, path, get_jar=get_genmodel_jar, jar_name=genmodel_name)
+
+    def pareto_front(self, test_frame=None, x_metric=None, y_metric=None, optimum="top left", title=None,
+                     color_col="algo"):
+        """Leaderboard models not dominated in (x_metric, y_metric); by default predict_time_per_row_ms vs the
+        sort metric (h2o.explanation pareto_front over get_leaderboard('ALL'))."""
+        from .explanation import pareto_front as _pf
+        lb = get_leaderboard(self, "ALL").as_data_frame()
+        if test_frame is not None:
+            from llama_github_io_amd.automl import leaderboard_frame
+            rows, _ = leaderboard_frame([dkv.get(k) for k in lb["model_id"]], test_frame)
+            lb = lb.drop(columns=[c for c in lb.columns if c not in ("model_id", "algo", "training_time_ms",
+                                                                        "predict_time_per_row_ms")])
+            import pandas as pd
+            lb = lb.merge(pd.DataFrame(rows), on="model_id")
+        return _pf(lb, x_metric=x_metric, y_metric=y_metric, optimum=optimum, title=title, color_col=color_col)
+
     def get_best_model(self, algorithm=None, criterion=None):
         rows, _ = self._aml.leaderboard_rows()
         for r in rows:
@@ -71,4 +128,37 @@ class H2OAutoML:
 
 
 def get_leaderboard(aml, extra_columns=None):
-    return aml.leaderboard
+    """autoh2o.get_leaderboard: the leaderboard plus the optional columns 'training_time_ms',
+    'predict_time_per_row_ms' and 'algo' ('ALL': every one)."""
+    import time as _time
+    import pandas as pd
+    from llama_github_io_amd.frame import H2OFrame
+    rows, cols = aml._aml.leaderboard_rows()
+    df = pd.DataFrame(rows, columns=cols)
+    if extra_columns is None:
+        return H2OFrame(df)
+    ex = [extra_columns] if isinstance(extra_columns, str) else list(extra_columns)
+    if any(str(e).upper() == "ALL" for e in ex):
+        ex = ["training_time_ms", "predict_time_per_row_ms", "algo"]
+    for c in ex:
+        if c not in ("training_time_ms", "predict_time_per_row_ms", "algo"):
+            raise ValueError(f"unknown leaderboard extension {c!r}")
+    ms = [dkv.get(k) for k in df["model_id"]]
+    if "training_time_ms" in ex:
+        df["training_time_ms"] = [int(m.output.get("run_time_ms") or 0) for m in ms]
+    if "predict_time_per_row_ms" in ex:
+        fr = getattr(aml._aml, "leaderboard_frame", None) or getattr(aml._aml, "training_frame_ref", None)
+        vals = []
+        for m in ms:
+            if fr is None:
+                vals.append(float("nan"))
+                continue
+            t0 = _time.perf_counter()
+            m.predict(fr)
+            vals.append(1000.0 * (_time.perf_counter() - t0) / max(1, fr.nrows))
+        df["predict_time_per_row_ms"] = vals
+    if "algo" in ex:
+        df["algo"] = [m.algo.replace("gbm", "GBM").replace("xgboost", "XGBoost").replace("glm", "GLM")
+                      .replace("drf", "DRF").replace("deeplearning", "DeepLearning")
+                      .replace("stackedensemble", "StackedEnsemble") for m in ms]
+    return H2OFrame(df)

@@ -316,6 +316,9 @@ class AutoML:
 
         counters = {}
         last_group = 0
+        self.executed_steps = []      # (algo family, step id, group, weight) of the steps that built models
+        self.training_frame_ref = training_frame      # predict_time_per_row_ms without a leaderboard frame
+        self.start_epoch = t0
         for algo, sid, group, w in steps:
             share = (time_left() * w / max(total_w - used_w, 1e-9)) if self.max_runtime_secs > 0 else float("inf")
             used_w += w
@@ -326,7 +329,10 @@ class AutoML:
                 # (and the final group always runs)
                 if (self._allowed("stackedensemble") and len(self.models) >= 2 and self.models[0].info.response
                         and (group <= last_group or group == 10)):
+                    n_se = len(self.models)
                     self._se_step(sid, x, y, training_frame, validation_frame, job)
+                    if len(self.models) > n_se:
+                        self.executed_steps.append(("StackedEnsemble", sid, group, w))
                 continue
             if not can_go(sid in _EXPLOITATION and self.exploitation_ratio > 0):
                 continue
@@ -359,6 +365,8 @@ class AutoML:
                             dict(base, learn_rate=lr, score_tree_interval=(j + 1) * sti), share / 10, exploit=True)
             if len(self.models) > n_before:
                 last_group = group
+                self.executed_steps.append((fam if algo != "completion" else "completion", sid, group, w))
+        self.stop_epoch = time.time()
         self.leaderboard_frame = leaderboard_frame
         if not self.keep_cv_predictions:
             # the holdout predictions were kept for the SEs only (AutoML keep_cross_validation_predictions=False)
