@@ -99,11 +99,231 @@ class ModelMetrics(dict):
     def mean_per_class_error(self): return self.get("mean_per_class_error")
     def gini(self): return self.get("Gini")
 
+    # ---- h2o-py model metrics surface (h2o-py/h2o/model/metrics/*.py): thresholds, confusion matrices, ROC,
+    # gains / lift, deviance / likelihood, clustering and survival / uplift scalars
+    _ALIASES = dict(fallout="fpr", missrate="fnr", recall="tpr", sensitivity="tpr", specificity="tnr")
+    MAXIMIZING = ("absolute_mcc", "accuracy", "precision", "f0point5", "f1", "f2", "mean_per_class_accuracy",
+                  "min_per_class_accuracy", "tns", "fns", "fps", "tps", "tnr", "fnr", "fpr", "tpr",
+                  "fallout", "missrate", "recall", "sensitivity", "specificity")
+
+    def _thr_rows(self):
+        rows = self.get("thresholds_and_metric_scores") or []
+        out = []
+        for r in rows:
+            r = dict(r)
+            P, N = r["tps"] + r["fns"], r["tns"] + r["fps"]
+            r.setdefault("tpr", r["tps"] / P if P > 0 else 0.0)
+            r.setdefault("fnr", r["fns"] / P if P > 0 else 0.0)
+            r.setdefault("tnr", r["tns"] / N if N > 0 else 0.0)
+            r.setdefault("fpr", r["fps"] / N if N > 0 else 0.0)
+            out.append(r)
+        return out
+
+    def find_threshold_by_max_metric(self, metric):
+        m = self._ALIASES.get(metric, metric)
+        rows = self._thr_rows()
+        if not rows:
+            raise ValueError("no threshold table (binomial metrics only)")
+        return max(rows, key=lambda r: r[m])["threshold"]
+
+    def find_idx_by_threshold(self, threshold):
+        rows = self._thr_rows()
+        th = [r["threshold"] for r in rows]
+        if threshold in th:
+            return th.index(threshold)
+        return min(range(len(th)), key=lambda i: abs(th[i] - threshold))
+
+    def metric(self, metric, thresholds=None):
+        """[[threshold, value], ...] with ``.value`` (scalar for None / one threshold), as h2o-py's metric()."""
+        if metric not in self.MAXIMIZING:
+            raise ValueError("The only allowable metrics are " + ", ".join(self.MAXIMIZING))
+        m = self._ALIASES.get(metric, metric)
+        rows = self._thr_rows()
+        scalar = thresholds is None or isinstance(thresholds, (int, float))
+        if thresholds is None:
+            ts = [self.find_threshold_by_max_metric(m)]
+        elif thresholds == "all":
+            ts = [r["threshold"] for r in rows]
+        elif isinstance(thresholds, (int, float)):
+            ts = [thresholds]
+        else:
+            ts = list(thresholds)
+        out = _MetricList([t, rows[self.find_idx_by_threshold(t)][m]] for t in ts)
+        out.value = out[0][1] if scalar else [r[1] for r in out]
+        return out
+
+    def F1(self, thresholds=None): return self.metric("f1", thresholds)
+    def F2(self, thresholds=None): return self.metric("f2", thresholds)
+    def F0point5(self, thresholds=None): return self.metric("f0point5", thresholds)
+    def accuracy(self, thresholds=None): return self.metric("accuracy", thresholds)
+    def precision(self, thresholds=None): return self.metric("precision", thresholds)
+    def recall(self, thresholds=None): return self.metric("tpr", thresholds)
+    def sensitivity(self, thresholds=None): return self.metric("tpr", thresholds)
+    def tpr(self, thresholds=None): return self.metric("tpr", thresholds)
+    def tnr(self, thresholds=None): return self.metric("tnr", thresholds)
+    def specificity(self, thresholds=None): return self.metric("tnr", thresholds)
+    def fpr(self, thresholds=None): return self.metric("fpr", thresholds)
+    def fallout(self, thresholds=None): return self.metric("fpr", thresholds)
+    def fnr(self, thresholds=None): return self.metric("fnr", thresholds)
+    def missrate(self, thresholds=None): return self.metric("fnr", thresholds)
+    def mcc(self, thresholds=None): return self.metric("absolute_mcc", thresholds)
+
+    def error(self, thresholds=None):
+        acc = self.metric("accuracy", thresholds)
+        out = _MetricList([t, 1 - v] for t, v in acc)
+        out.value = [1 - v for v in acc.value] if isinstance(acc.value, list) else 1 - acc.value
+        return out
+
+    def max_per_class_error(self, thresholds=None):
+        acc = self.metric("min_per_class_accuracy", thresholds)
+        out = _MetricList([t, 1 - v] for t, v in acc)
+        out.value = [1 - v for v in acc.value] if isinstance(acc.value, list) else 1 - acc.value
+        return out
+
+    @property
+    def thresholds(self):
+        return [r["threshold"] for r in self._thr_rows()]
+
+    @property
+    def fprs(self):
+        return [r["fpr"] for r in self._thr_rows()]
+
+    @property
+    def tprs(self):
+        return [r["tpr"] for r in self._thr_rows()]
+
+    def roc(self):
+        """(false positive rates, true positive rates) over the threshold table."""
+        return self.fprs, self.tprs
+
+    def confusion_matrix(self, metrics=None, thresholds=None):
+        """Binomial: ConfusionMatrix at the threshold maximizing ``metrics`` (default f1) or at ``thresholds``;
+        multinomial / ordinal: the model's confusion matrix."""
+        if not self.get("thresholds_and_metric_scores"):
+            cm = self.get("cm")
+            if cm is None:
+                return None
+            dom = list(self.get("domain") or range(len(cm["table"])))
+            return ConfusionMatrix(cm["table"], dom, "Confusion Matrix: Row labels: Actual class; Column labels: "
+                                                      "Predicted class")
+        if metrics is None and thresholds is None:
+            metrics = ["f1"]
+        ml = metrics if isinstance(metrics, list) else ([] if metrics is None else [metrics])
+        tl = thresholds if isinstance(thresholds, list) else ([] if thresholds is None else [thresholds])
+        if not all(m.lower() in self.MAXIMIZING for m in ml):
+            raise ValueError("The only allowable metrics are " + ", ".join(self.MAXIMIZING))
+        rows = self._thr_rows()
+        items = [(t, None) for t in tl] + [(self.find_threshold_by_max_metric(m.lower()), m) for m in ml]
+        out = []
+        for t, m in items:
+            r = rows[self.find_idx_by_threshold(t)]
+            hdr = (f"Confusion Matrix (Act/Pred) for max {m} @ threshold = {r['threshold']}" if m else
+                   f"Confusion Matrix (Act/Pred) @ threshold = {r['threshold']}")
+            out.append(ConfusionMatrix([[r["tns"], r["fps"]], [r["fns"], r["tps"]]],
+                                       list(self.get("domain") or ["0", "1"]), hdr))
+        return out[0] if len(out) == 1 else out
+
+    def gains_lift(self):
+        import pandas as pd
+        gl = self.get("gains_lift_table")
+        return pd.DataFrame(gl) if gl else None
+
+    def plot(self, type="roc", server=False, save_plot_path=None, plot=True):
+        """ROC ('roc'), precision-recall ('pr') or gains/lift ('gainslift') curve; a matplotlib figure."""
+        import matplotlib
+        matplotlib.use("Agg", force=False)
+        import matplotlib.pyplot as plt
+        fig, ax = plt.subplots()
+        if type == "roc":
+            ax.plot(self.fprs, self.tprs)
+            ax.set_xlabel("False Positive Rate")
+            ax.set_ylabel("True Positive Rate")
+            ax.set_title(f"ROC Curve (AUC = {self.get('AUC')})")
+        elif type == "pr":
+            rows = self._thr_rows()
+            ax.plot([r["tpr"] for r in rows], [r["precision"] for r in rows])
+            ax.set_xlabel("Recall")
+            ax.set_ylabel("Precision")
+        else:
+            gl = self.gains_lift()
+            ax.plot(gl["cumulative_data_fraction"], gl["cumulative_lift"])
+            ax.set_xlabel("Cumulative data fraction")
+            ax.set_ylabel("Cumulative lift")
+        if save_plot_path:
+            fig.savefig(save_plot_path)
+        return fig
+
+    def n(self): return self.get("nobs")
+    def residual_deviance(self): return self.get("residual_deviance")
+    def residual_degrees_of_freedom(self): return self.get("residual_degrees_of_freedom")
+    def null_deviance(self): return self.get("null_deviance")
+    def null_degrees_of_freedom(self): return self.get("null_degrees_of_freedom")
+    def aic(self): return self.get("AIC", self.get("aic"))
+    def loglikelihood(self): return self.get("loglikelihood")
+    def hglm_metric(self, metric_string): return self.get(metric_string)
+    def custom_metric_name(self): return self.get("custom_metric_name")
+    def custom_metric_value(self): return self.get("custom_metric_value")
+    def tot_withinss(self): return self.get("tot_withinss")
+    def totss(self): return self.get("totss")
+    def betweenss(self): return self.get("betweenss")
+    def num_err(self): return self.get("numerr", self.get("num_err"))
+    def cat_err(self): return self.get("caterr", self.get("cat_err"))
+    def concordance(self): return self.get("concordance")
+    def concordant(self): return self.get("concordant")
+    def tied_y(self): return self.get("tied_y")
+    def mean_score(self): return self.get("mean_score")
+    def mean_normalized_score(self): return self.get("mean_normalized_score")
+    def auuc(self, metric=None): return self.get("AUUC")
+    def auuc_normalized(self, metric=None): return self.get("auuc_normalized")
+    def qini(self): return self.get("qini")
+    def aecu(self, metric="qini"): return (self.get("aecu_table") or {}).get(metric, self.get("aecu"))
+    def auuc_table(self): return self.get("auuc_table")
+    def aecu_table(self): return self.get("aecu_table")
+    def uplift(self, metric="AUTO"): return (self.get("auuc_table") or {}).get("uplift")
+    def uplift_normalized(self, metric="AUTO"): return (self.get("auuc_table") or {}).get("uplift_normalized")
+    def uplift_random(self, metric="AUTO"): return (self.get("auuc_table") or {}).get("uplift_random")
+    def multinomial_auc_table(self): return self.get("multinomial_auc_table")
+    def multinomial_aucpr_table(self): return self.get("multinomial_aucpr_table")
+
+    def show(self, verbosity=None, fmt=None):
+        print(repr(self))
+
     def __repr__(self):
         keys = [k for k in ("model_category", "MSE", "RMSE", "mae", "r2", "logloss", "AUC", "pr_auc",
                             "mean_per_class_error", "mean_residual_deviance", "tot_withinss", "betweenss")
                 if k in self]
         return "ModelMetrics(" + ", ".join(f"{k}={self[k]}" for k in keys) + ")"
+
+
+class _MetricList(list):
+    """[[threshold, value], ...] with a ``value`` attribute (h2o-py metrics' List)."""
+    value = None
+
+
+class ConfusionMatrix:
+    """h2o-py ConfusionMatrix: ``table`` (pandas, with the per-row Error and Rate columns) and ``to_list()``."""
+
+    def __init__(self, cm, domains, table_header=""):
+        import pandas as pd
+        self._cm = [[float(v) for v in r] for r in cm]
+        self.domains = [str(d) for d in domains]
+        self.table_header = table_header
+        rows = []
+        for i, r in enumerate(self._cm):
+            tot = sum(r)
+            err = tot - r[i]
+            rows.append(r + [err / tot if tot else 0.0, f"({int(err)}.0/{int(tot)}.0)"])
+        tot_err = sum(sum(r) - r[i] for i, r in enumerate(self._cm))
+        tot = sum(sum(r) for r in self._cm)
+        rows.append([sum(r[j] for r in self._cm) for j in range(len(self._cm))] +
+                    [tot_err / tot if tot else 0.0, f"({int(tot_err)}.0/{int(tot)}.0)"])
+        self.table = pd.DataFrame(rows, index=self.domains + ["Total"], columns=self.domains + ["Error", "Rate"])
+
+    def to_list(self):
+        return [[int(v) for v in r] for r in self._cm]
+
+    def __repr__(self):
+        return f"{self.table_header}\n{self.table}"
 
 
 def _w(w, n, device):

@@ -355,6 +355,39 @@ class GLMModel(Model):
             return torch.stack([1 - mu, mu], 1).float()
         return mu.float()
 
+    def metrics_for(self, X, y, w=None, offset=None):
+        """ModelMetrics*GLM of a scored frame: the family metrics plus residual / null deviance (null model = the
+        training mean response through the link, with the frame's offset), their degrees of freedom and AIC
+        (hex/glm/GLMMetricBuilder)."""
+        m = super().metrics_for(X, y, w, offset)
+        fam = self.output.get("family")
+        if m is None or fam in ("multinomial", "ordinal") or getattr(self, "hglm", None) is not None:
+            return m
+        dev = self.device
+        f = Family(fam, self.output["link"], self.params.get("tweedie_variance_power", 0.0),
+                   self.params.get("tweedie_link_power", 1.0), self.params.get("theta", 1e-10))
+        eta = self._eta(X, offset)[:, 0]
+        mu = f.linkinv(eta)
+        yy = y.to(dev).double()
+        ww = torch.ones_like(yy) if w is None else w.to(dev).double()
+        ok = ~torch.isnan(yy) & (ww > 0)
+        yy, ww, mu = yy[ok], ww[ok], mu[ok]
+        res_dev = float((ww * f.deviance(yy, mu)).sum())
+        ymu = self.output.get("training_ymu")
+        if ymu is None:
+            ymu = float((ww * yy).sum() / ww.sum().clamp(min=1e-300))
+        null_eta = f.linkfn(torch.full_like(yy, float(ymu)))
+        if offset is not None:
+            null_eta = null_eta + offset.to(dev).double()[ok]
+        null_dev = float((ww * f.deviance(yy, f.linkinv(null_eta))).sum())
+        nobs = int(ok.sum())
+        rank = int((self.beta.abs() > 0).sum())
+        m.update(residual_deviance=res_dev, null_deviance=null_dev,
+                 null_degrees_of_freedom=nobs - (1 if self.params.get("intercept", True) else 0),
+                 residual_degrees_of_freedom=nobs - rank,
+                 AIC=f.loglik_aic(yy, mu, ww, res_dev, nobs, rank))
+        return m
+
     def predict_labels(self, P):
         """Ordinal (GLMModel.score0): the first class whose cumulative probability exceeds 1/2 (eta_c > 0), else the
         last class — the median of the predicted distribution, not its mode."""
@@ -1125,6 +1158,7 @@ class GLMTrainer:
             mu = (P[:, 1] if P.dim() == 2 else P).double()
             res_dev = _gsum((w * family.deviance(y, mu)).sum())
             ymu = _gsum((w * y).sum()) / _gsum(w.sum())
+            out["training_ymu"] = float(ymu)
             null_mu = torch.full_like(y, ymu)
             if offset is not None:
                 null_mu = family.linkinv(family.linkfn(null_mu) + off)

@@ -50,6 +50,16 @@ class KMeansModel(Model):
         a = self._predict_tensor(X)
         return H2OFrame._from_columns([Column("predict", "int", a.double())])
 
+    def metrics_for(self, X, y, w=None, offset=None):
+        """Clustering metrics of a scored frame (ModelMetricsClustering: within / between / total SS, sizes) in the
+        model's standardized space (the sums of squares are translation invariant)."""
+        Z = self.expander.transform(X.to(self.device))
+        C = self.centers_std.to(Z.device)
+        if Z.shape[1] < C.shape[1]:
+            Z = torch.nn.functional.pad(Z, (0, C.shape[1] - Z.shape[1]))
+        a, _ = kmeans_assign(Z, C)
+        return mm.clustering_metrics(Z, C, a, None if w is None else w.to(Z.device).double())
+
     def centers(self):
         return self.output["centers"]
 
