@@ -316,6 +316,122 @@ class Model:
         m = self.output.get(src) or {}
         return m.get(name)
 
+    # ---- h2o-py model-level metric delegation (model/models/binomial.py, multinomial.py: _delegate_to_metrics):
+    # the training metrics unless train / valid / xval pick others; several picked -> {"train": .., "valid": ..}
+    def _delegate(self, method, *args, train=False, valid=False, xval=False, **kw):
+        from .. import metrics as _mm
+        if not (train or valid or xval):
+            train = True
+        sel = [(k, src) for k, src, on in (("train", "training_metrics", train), ("valid", "validation_metrics", valid),
+                                          ("xval", "cross_validation_metrics", xval)) if on]
+        res = {}
+        for k, src in sel:
+            m = self.output.get(src)
+            if m is not None and not isinstance(m, _mm.ModelMetrics):
+                m = _mm.ModelMetrics(m)
+            res[k] = getattr(m, method)(*args, **kw) if m is not None else None
+        return next(iter(res.values())) if len(res) == 1 else res
+
+    def F1(self, thresholds=None, train=False, valid=False, xval=False):
+        return self._delegate("F1", thresholds, train=train, valid=valid, xval=xval)
+
+    def F2(self, thresholds=None, train=False, valid=False, xval=False):
+        return self._delegate("F2", thresholds, train=train, valid=valid, xval=xval)
+
+    def F0point5(self, thresholds=None, train=False, valid=False, xval=False):
+        return self._delegate("F0point5", thresholds, train=train, valid=valid, xval=xval)
+
+    def accuracy(self, thresholds=None, train=False, valid=False, xval=False):
+        return self._delegate("accuracy", thresholds, train=train, valid=valid, xval=xval)
+
+    def error(self, thresholds=None, train=False, valid=False, xval=False):
+        return self._delegate("error", thresholds, train=train, valid=valid, xval=xval)
+
+    def precision(self, thresholds=None, train=False, valid=False, xval=False):
+        return self._delegate("precision", thresholds, train=train, valid=valid, xval=xval)
+
+    def recall(self, thresholds=None, train=False, valid=False, xval=False):
+        return self._delegate("recall", thresholds, train=train, valid=valid, xval=xval)
+
+    def sensitivity(self, thresholds=None, train=False, valid=False, xval=False):
+        return self._delegate("sensitivity", thresholds, train=train, valid=valid, xval=xval)
+
+    def specificity(self, thresholds=None, train=False, valid=False, xval=False):
+        return self._delegate("specificity", thresholds, train=train, valid=valid, xval=xval)
+
+    def tpr(self, thresholds=None, train=False, valid=False, xval=False):
+        return self._delegate("tpr", thresholds, train=train, valid=valid, xval=xval)
+
+    def tnr(self, thresholds=None, train=False, valid=False, xval=False):
+        return self._delegate("tnr", thresholds, train=train, valid=valid, xval=xval)
+
+    def fpr(self, thresholds=None, train=False, valid=False, xval=False):
+        return self._delegate("fpr", thresholds, train=train, valid=valid, xval=xval)
+
+    def fnr(self, thresholds=None, train=False, valid=False, xval=False):
+        return self._delegate("fnr", thresholds, train=train, valid=valid, xval=xval)
+
+    def fallout(self, thresholds=None, train=False, valid=False, xval=False):
+        return self._delegate("fallout", thresholds, train=train, valid=valid, xval=xval)
+
+    def missrate(self, thresholds=None, train=False, valid=False, xval=False):
+        return self._delegate("missrate", thresholds, train=train, valid=valid, xval=xval)
+
+    def mcc(self, thresholds=None, train=False, valid=False, xval=False):
+        return self._delegate("mcc", thresholds, train=train, valid=valid, xval=xval)
+
+    def max_per_class_error(self, thresholds=None, train=False, valid=False, xval=False):
+        return self._delegate("max_per_class_error", thresholds, train=train, valid=valid, xval=xval)
+
+    def mean_per_class_error(self, train=False, valid=False, xval=False):
+        return self._m("mean_per_class_error", train, valid, xval)
+
+    def metric(self, metric, thresholds=None, train=False, valid=False, xval=False):
+        return self._delegate("metric", metric, thresholds, train=train, valid=valid, xval=xval)
+
+    def find_threshold_by_max_metric(self, metric, train=False, valid=False, xval=False):
+        return self._delegate("find_threshold_by_max_metric", metric, train=train, valid=valid, xval=xval)
+
+    def find_idx_by_threshold(self, threshold, train=False, valid=False, xval=False):
+        return self._delegate("find_idx_by_threshold", threshold, train=train, valid=valid, xval=xval)
+
+    def confusion_matrix(self, metrics=None, thresholds=None, train=False, valid=False, xval=False):
+        if metrics is not None and hasattr(metrics, "model_matrix"):      # h2o-py: confusion_matrix(frame)
+            return self.model_performance(metrics).confusion_matrix()
+        return self._delegate("confusion_matrix", metrics, thresholds, train=train, valid=valid, xval=xval)
+
+    def roc(self, train=False, valid=False, xval=False):
+        return self._delegate("roc", train=train, valid=valid, xval=xval)
+
+    def gains_lift(self, train=False, valid=False, xval=False):
+        return self._delegate("gains_lift", train=train, valid=valid, xval=xval)
+
+    def gains_lift_plot(self, type="both", server=False, save_plot_path=None, plot=True):
+        return self._delegate("plot", "gainslift", server, save_plot_path, plot)
+
+    def plot(self, timestep="AUTO", metric="AUTO", server=False, save_plot_path=None, **kw):
+        """Binomial: the ROC curve of the training metrics (h2o-py plots the scoring history for other models)."""
+        return self._delegate("plot", "roc", server, save_plot_path)
+
+    def kolmogorov_smirnov(self, train=False, valid=False, xval=False):
+        """max |TPR - FPR| over the threshold table (the gains/lift table's K-S statistic)."""
+        def ks(roc):
+            if roc is None:
+                return None
+            f, t = roc
+            return max((abs(y - x) for x, y in zip(f, t)), default=None)
+        r = self.roc(train=train, valid=valid, xval=xval)
+        return {k: ks(v) for k, v in r.items()} if isinstance(r, dict) else ks(r)
+
+    def hit_ratio_table(self, train=False, valid=False, xval=False):
+        return self._m("hit_ratio_table", train, valid, xval) or self._m("hit_ratios", train, valid, xval)
+
+    def multinomial_auc_table(self, train=False, valid=False, xval=False):
+        return self._m("multinomial_auc_table", train, valid, xval)
+
+    def multinomial_aucpr_table(self, train=False, valid=False, xval=False):
+        return self._m("multinomial_aucpr_table", train, valid, xval)
+
     def auc(self, train=False, valid=False, xval=False): return self._m("AUC", train, valid, xval)
     def aucpr(self, train=False, valid=False, xval=False): return self._m("pr_auc", train, valid, xval)
     def logloss(self, train=False, valid=False, xval=False): return self._m("logloss", train, valid, xval)

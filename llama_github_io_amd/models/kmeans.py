@@ -60,6 +60,17 @@ class KMeansModel(Model):
         a, _ = kmeans_assign(Z, C)
         return mm.clustering_metrics(Z, C, a, None if w is None else w.to(Z.device).double())
 
+    def num_iterations(self):
+        return int(self.output.get("iterations") or 0)
+
+    def centroid_stats(self, train=False, valid=False):
+        """Per-centroid table (centroid, size, within_cluster_sum_of_squares) as in ModelMetricsClustering."""
+        import pandas as pd
+        m = self.output.get("validation_metrics" if valid else "training_metrics") or {}
+        size, within = m.get("size") or [], m.get("withinss") or []
+        return pd.DataFrame(dict(centroid=list(range(1, len(size) + 1)), size=size,
+                                 within_cluster_sum_of_squares=within))
+
     def centers(self):
         return self.output["centers"]
 

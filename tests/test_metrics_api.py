@@ -73,3 +73,29 @@ def test_glm_frame_deviance_matches_training(fr):
     assert abs(pg.null_deviance() - out["null_deviance"]) < 1e-6 * out["null_deviance"]
     assert pg.residual_degrees_of_freedom() == out["residual_degrees_of_freedom"]
     assert abs(pg.aic() - out["aic"]) < 1e-6 * abs(out["aic"])
+
+
+def test_model_level_metric_delegation(fr):
+    """H2OBinomialModel accessors (model/models/binomial.py): training metrics by default, a dict for several."""
+    tr, va = fr.split_frame([0.7], seed=2)
+    m = H2OGradientBoostingEstimator(ntrees=5, seed=1)
+    m.train(x=["a", "b"], y="y", training_frame=tr, validation_frame=va)
+    assert m.F1().value == m.model_performance(train=True).F1().value
+    both = m.F1(train=True, valid=True)
+    assert set(both) == {"train", "valid"}
+    assert m.find_threshold_by_max_metric("f1", valid=True) == m.model_performance(valid=True).find_threshold_by_max_metric("f1")
+    cm = m.confusion_matrix(valid=True)
+    assert sum(map(sum, cm.to_list())) == va.nrows
+    assert sum(map(sum, m.confusion_matrix(va).to_list())) == va.nrows
+    f, t = m.roc()
+    ks = m.kolmogorov_smirnov()
+    assert 0 < ks <= 1 and abs(ks - max(abs(b - a) for a, b in zip(f, t))) < 1e-12
+    assert 0 <= m.mean_per_class_error() <= 1 and len(m.gains_lift()) == 16
+
+
+def test_kmeans_model_accessors(fr):
+    k = H2OKMeansEstimator(k=3, seed=1)
+    k.train(x=["a", "b"], training_frame=fr)
+    cs = k.centroid_stats()
+    assert list(cs.columns) == ["centroid", "size", "within_cluster_sum_of_squares"] and cs["size"].sum() == fr.nrows
+    assert k.num_iterations() >= 1 and abs(sum(k.withinss()) - k.tot_withinss()) < 1e-6 * k.tot_withinss()
