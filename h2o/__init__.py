@@ -437,3 +437,9 @@ import_frame = import_file
 from .explanation import (model_correlation, model_correlation_heatmap, pareto_front, pd_multi_plot,  # noqa: E402,F401
                           register_explain_methods, varimp, varimp_heatmap)
 register_explain_methods()
+
+
+def make_leaderboard(object, leaderboard_frame=None, sort_metric="AUTO", extra_columns=(), scoring_data="AUTO"):
+    """Leaderboard over models / grids / AutoML runs (h2o-py scoring.make_leaderboard)."""
+    from .scoring import make_leaderboard as _ml
+    return _ml(object, leaderboard_frame, sort_metric, extra_columns, scoring_data)

@@ -111,11 +111,10 @@ class H2OAutoML:
         lb = get_leaderboard(self, "ALL").as_data_frame()
         if test_frame is not None:
             from llama_github_io_amd.automl import leaderboard_frame
-            rows, _ = leaderboard_frame([dkv.get(k) for k in lb["model_id"]], test_frame)
+            scored = leaderboard_frame([dkv.get(k) for k in lb["model_id"]], test_frame).as_data_frame()
             lb = lb.drop(columns=[c for c in lb.columns if c not in ("model_id", "algo", "training_time_ms",
                                                                         "predict_time_per_row_ms")])
-            import pandas as pd
-            lb = lb.merge(pd.DataFrame(rows), on="model_id")
+            lb = lb.merge(scored, on="model_id")
         return _pf(lb, x_metric=x_metric, y_metric=y_metric, optimum=optimum, title=title, color_col=color_col)
 
     def get_best_model(self, algorithm=None, criterion=None):
