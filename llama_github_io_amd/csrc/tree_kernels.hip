@@ -3275,7 +3275,9 @@ static int tree_grow(const TreePlan* P, int d, int dist, hipStream_t s, bool pla
     // level 1 of a narrow planar run: the root split's side of every row as bytes (read by the level-1
     // histogram blocks and the root route instead of the split column's plane)
     const void* fdir = nullptr;
-    if (d == 0 && tp_lvl2(P) && P->fdir) {
+    // (also every planar run whose level 1 builds >= 2 planes, e.g. XGBoost 100M x 50: each plane's histogram blocks
+    // would otherwise read the root split column's plane once per plane)
+    if (d == 0 && P->fdir && (tp_lvl2(P) || (P->planar && tp_planes(tp_fcut(P, 1) > 0 ? tp_fcut(P, 1) : P->F) >= 2))) {
       long long g = (P->N + 255) / 256;
       if (g > 4096) g = 4096;
       if (g < 1) g = 1;

@@ -839,12 +839,16 @@ class GpuTreeBuilder:
         P.mid_F, P.mid_from = (self.n_mid, mid) if mid >= 0 else (0, 0)
         # every row's level-2 position from the root route (the leaf walk starts there; narrow planar runs only)
         # and the root split's side of every row (level 1 reads these bytes instead of the split column's plane)
-        if lo >= 0 and self.planar and getattr(self, "_lvl2", None) is None:
-            self._lvl2 = torch.empty(self.N, dtype=torch.uint8, device=self.dev)
-            self._fdir = torch.empty(self.N, dtype=torch.uint8, device=self.dev)
+        # planar runs of >= 2 planes (e.g. XGBoost 100M x 50) also get the root split's side as bytes for level 1
+        wide = self.planar and self.F > 32 and os.environ.get("H2O_ROW_DIR_PLANAR", "1") != "0"
+        if (lo >= 0 and self.planar) or wide:
+            if getattr(self, "_fdir", None) is None:
+                self._fdir = torch.empty(self.N, dtype=torch.uint8, device=self.dev)
+            if lo >= 0 and getattr(self, "_lvl2", None) is None:
+                self._lvl2 = torch.empty(self.N, dtype=torch.uint8, device=self.dev)
         on = lo >= 0 and self.planar
         P.lvl2 = self._lvl2.data_ptr() if on else 0
-        P.fdir = self._fdir.data_ptr() if on else 0
+        P.fdir = self._fdir.data_ptr() if (on or wide) else 0
 
     def _fine16_map(self):
         """Slot maps of the root pass from 16-bit fine planes (k_hist_root16), or None when it does not apply: the

@@ -226,6 +226,36 @@ def test_gpu_tree_matches_reference_row_widths(F):
     assert torch.equal(ref.leaf_of_row, gb.leaf_of_row.cpu())
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("F", [40, 70])
+@pytest.mark.parametrize("row_dir", ["1", "0"])
+def test_gpu_planar_tree_matches_reference(F, row_dir, monkeypatch):
+    """Planar bins (F > 32, one 32-byte plane per feature tile) as the XGBoost / wide GBM runs use them, with and
+    without the root split's direction bytes for level 1 (H2O_ROW_DIR_PLANAR): decisions and leaves of the fp64
+    reference."""
+    monkeypatch.setenv("H2O_ROW_DIR_PLANAR", row_dir)
+    X, y, info = _data(N=30000, F=F, cat=True, seed=F + 1)
+    g = torch.Generator().manual_seed(F)
+    X[F - 1] = X[0] * 0.5 + torch.randn(X.shape[1], generator=g)
+    b = fit_binning(X, info.iscat, info.nlevels, max_bins=64)
+    bins = apply_binning(b, X)
+    aux = torch.stack([torch.ones_like(y), y - 0.5, y - 0.5, torch.ones_like(y)], 1).contiguous()
+    p = T.SplitParams(min_w=10)
+    ref = T.RefTreeBuilder(bins, F, b.nbins, b.iscat, None, 6, p)
+    ref.build(aux, leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1]).float())
+    tl_r = ref.pop_levels()[0]
+    dev = torch.device("cuda", 0)
+    gb = T.GpuTreeBuilder(apply_binning(b, X.to(dev), planar=True), F, b.nbins, b.iscat, None, 6, p)
+    assert gb.planar
+    gb.build(aux.to(dev), leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1]).float(), packed=True, unit=True)
+    assert bool(gb._plan.fdir) == (row_dir == "1")
+    tl_g = gb.pop_levels()[0]
+    assert tl_g.n_leaves == tl_r.n_leaves
+    for dr, dg in zip(tl_r.decs, tl_g.decs):
+        assert np.array_equal(dr["feat"], dg["feat"]) and np.array_equal(dr["bin"], dg["bin"])
+    assert torch.equal(ref.leaf_of_row, gb.leaf_of_row.cpu())
+
+
 def _edge_tab(b):
     tab = np.full((b.F, 255), np.inf, dtype=np.float32)
     for f, e in enumerate(b.edges):
