@@ -839,8 +839,10 @@ class GpuTreeBuilder:
         P.mid_F, P.mid_from = (self.n_mid, mid) if mid >= 0 else (0, 0)
         # every row's level-2 position from the root route (the leaf walk starts there; narrow planar runs only)
         # and the root split's side of every row (level 1 reads these bytes instead of the split column's plane)
-        # planar runs of >= 2 planes (e.g. XGBoost 100M x 50) also get the root split's side as bytes for level 1
-        wide = self.planar and self.F > 32 and os.environ.get("H2O_ROW_DIR_PLANAR", "1") != "0"
+        # H2O_ROW_DIR_PLANAR=1: planar runs of >= 2 planes (e.g. XGBoost 100M x 50) also get the root split's side as
+        # bytes for level 1. MEASURED r5 (scripts/gpu_r5_c30.sh): 17.48-17.75 vs 17.53 ms/tree — the second plane's
+        # read of the split column hits the caches; off by default
+        wide = self.planar and self.F > 32 and os.environ.get("H2O_ROW_DIR_PLANAR", "0") == "1"
         if (lo >= 0 and self.planar) or wide:
             if getattr(self, "_fdir", None) is None:
                 self._fdir = torch.empty(self.N, dtype=torch.uint8, device=self.dev)

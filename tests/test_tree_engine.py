@@ -248,7 +248,7 @@ def test_gpu_planar_tree_matches_reference(F, row_dir, monkeypatch):
     gb = T.GpuTreeBuilder(apply_binning(b, X.to(dev), planar=True), F, b.nbins, b.iscat, None, 6, p)
     assert gb.planar
     gb.build(aux.to(dev), leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1]).float(), packed=True, unit=True)
-    assert bool(gb._plan.fdir) == (row_dir == "1")
+    assert bool(gb._plan.fdir) == (row_dir == "1")      # (off by default; the A/B switch keeps its path tested)
     tl_g = gb.pop_levels()[0]
     assert tl_g.n_leaves == tl_r.n_leaves
     for dr, dg in zip(tl_r.decs, tl_g.decs):
