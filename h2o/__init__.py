@@ -300,6 +300,75 @@ def import_mojo(mojo_path, model_id=None):
 upload_mojo = import_mojo
 
 
+def mojo_predict_csv(input_csv_path, mojo_zip_path, output_csv_path=None, genmodel_jar_path=None, classpath=None,
+                     java_options=None, verbose=False, setInvNumNA=False, predict_contributions=False,
+                     predict_calibrated=False, extra_cmd_args=None):
+    """Score a CSV file with a MOJO zip and write ``output_csv_path`` (default ``prediction.csv`` next to the zip);
+    returns the prediction rows as dicts (reference: ``h2o-py/h2o/utils/shared_utils.py:478``, which runs
+    ``hex.genmodel.tools.PredictCsv`` in a JVM). Here the MOJO is scored by the native MOJO reader, so
+    ``genmodel_jar_path`` / ``classpath`` / ``java_options`` / ``extra_cmd_args`` are accepted and unused.
+    ``setInvNumNA``: unparsable numbers become NA (PredictCsv ``--setConvertInvalidNum``) instead of an error."""
+    import csv
+    import os
+    import pandas as pd
+    from llama_github_io_amd.models.generic import GenericModel
+    if not os.path.isfile(input_csv_path):
+        raise RuntimeError("Input csv cannot be found at %s" % input_csv_path)
+    mojo_zip_path = os.path.abspath(mojo_zip_path)
+    if not os.path.isfile(mojo_zip_path):
+        raise RuntimeError("MOJO zip cannot be found at %s" % mojo_zip_path)
+    if output_csv_path is None:
+        output_csv_path = os.path.join(os.path.dirname(mojo_zip_path), "prediction.csv")
+    m = GenericModel.from_mojo(mojo_zip_path)
+    df = pd.read_csv(input_csv_path)
+    if "Unnamed: 0" in df.columns and "Unnamed: 0" not in m.info.x:     # pandas index written by to_csv
+        df = df.drop(columns=["Unnamed: 0"])
+    for j, name in enumerate(m.info.x):
+        if name not in df.columns:
+            continue
+        if m.info.iscat[j]:
+            df[name] = df[name].astype("string")
+        elif df[name].dtype == object:
+            num = pd.to_numeric(df[name], errors="coerce")
+            bad = num.isna() & df[name].notna()
+            if bad.any() and not setInvNumNA:
+                raise ValueError(f"invalid numeric value {df[name][bad].iloc[0]!r} in column {name!r} "
+                                 "(setInvNumNA=True turns it into NA)")
+            df[name] = num
+    types = {n: "enum" for j, n in enumerate(m.info.x) if m.info.iscat[j] and n in df.columns}
+    fr = H2OFrame(df, column_types=types or None)
+    if verbose:
+        print("input_csv:\t%s\nmojo_zip:\t%s\noutput_csv:\t%s" % (input_csv_path, mojo_zip_path, output_csv_path))
+    pred = m.predict_contributions(fr) if predict_contributions else m.predict(fr)
+    out = pred.as_data_frame()
+    if not predict_calibrated:
+        out = out[[c for c in out.columns if not str(c).startswith("cal_")]]
+    out.to_csv(output_csv_path, index=False)
+    with open(output_csv_path) as fh:
+        return list(csv.DictReader(fh))
+
+
+def mojo_predict_pandas(dataframe, mojo_zip_path, genmodel_jar_path=None, classpath=None, java_options=None,
+                        verbose=False, setInvNumNA=False, predict_contributions=False, predict_calibrated=False):
+    """Score a pandas DataFrame with a MOJO zip (reference: ``h2o-py/h2o/utils/shared_utils.py:442``); returns the
+    predictions as a DataFrame."""
+    import os
+    import shutil
+    import tempfile
+    import pandas as pd
+    if not isinstance(dataframe, pd.DataFrame):
+        raise TypeError("dataframe must be a pandas.DataFrame")
+    d = tempfile.mkdtemp()
+    try:
+        inp, outp = os.path.join(d, "input.csv"), os.path.join(d, "prediction.csv")
+        dataframe.to_csv(inp)
+        mojo_predict_csv(inp, mojo_zip_path, outp, genmodel_jar_path, classpath, java_options, verbose, setInvNumNA,
+                         predict_contributions, predict_calibrated)
+        return pd.read_csv(outp)
+    finally:
+        shutil.rmtree(d)
+
+
 def print_mojo(mojo_path, format="json", tree_index=None):
     from llama_github_io_amd.mojo import reader
     return reader.print_mojo(mojo_path, format, tree_index)
@@ -424,7 +493,7 @@ def remove_s3_credentials():
 
 from . import grid, automl  # noqa: E402,F401
 from .grid import H2OGridSearch  # noqa: E402,F401
-from .automl import H2OAutoML, get_leaderboard  # noqa: E402,F401
+from .automl import H2OAutoML, get_automl, get_leaderboard  # noqa: E402,F401
 
 from ._more import (api, cluster_info, connection, demo, download_all_logs, download_csv,  # noqa: E402,F401
                     enable_expr_optimizations, estimate_cluster_mem, frame, get_timezone, import_hive_table,

@@ -126,6 +126,18 @@ class H2OAutoML:
         return None
 
 
+def get_automl(project_name):
+    """The AutoML run of ``project_name`` (reference: ``h2o-py/h2o/automl/autoh2o.py:13``): an object with the
+    run's ``project_name``, ``leader``, ``leaderboard``, ``event_log`` and ``training_info``."""
+    a = dkv.get(project_name)
+    if not isinstance(a, _aml.AutoML):
+        raise ValueError(f"no AutoML instance with project_name {project_name!r}")
+    out = H2OAutoML.__new__(H2OAutoML)
+    out._aml = a
+    out.project_name = a.project_name
+    return out
+
+
 def get_leaderboard(aml, extra_columns=None):
     """autoh2o.get_leaderboard: the leaderboard plus the optional columns 'training_time_ms',
     'predict_time_per_row_ms' and 'algo' ('ALL': every one)."""
