@@ -334,6 +334,23 @@ def _level_key(s):
 class H2OFrame:
     """Distributed-in-HBM frame with the h2o-py ``H2OFrame`` API surface."""
 
+    @property
+    def frame_id(self):
+        """The frame's key in the DKV (reference ``h2o-py/h2o/frame.py:392``)."""
+        return self.__dict__.get("_frame_id")
+
+    @frame_id.setter
+    def frame_id(self, newid):
+        # assigning a new id renames the frame's DKV entry (the reference's setter issues a Rapids ``rename``)
+        old = self.__dict__.get("_frame_id")
+        self.__dict__["_frame_id"] = newid
+        if old is not None and newid != old and dkv.contains(old) and dkv.get(old) is self:
+            try:
+                dkv.remove(old)
+            except RuntimeError:     # write-locked by a running job: the old key stays until the job ends
+                pass
+            dkv.put(newid, self)
+
     def __init__(self, python_obj=None, destination_frame=None, header=0, separator=",", column_names=None,
                  column_types=None, na_strings=None, skipped_columns=None):
         self._cols: "OrderedDict[str, Column]" = OrderedDict()

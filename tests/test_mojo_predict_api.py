@@ -66,3 +66,12 @@ def test_get_automl(data):
     assert got.leaderboard.as_data_frame().shape == aml.leaderboard.as_data_frame().shape
     with pytest.raises(ValueError):
         h2o.get_automl("no_such_project")
+
+
+def test_frame_id_setter_renames_dkv_entry():
+    fr = h2o.H2OFrame(pd.DataFrame({"a": [1.0, 2.0, 3.0]}))
+    old = fr.frame_id
+    fr.frame_id = "renamed_frame_x"
+    assert fr.frame_id == "renamed_frame_x"
+    assert h2o.get_frame("renamed_frame_x") is not None
+    assert old not in [str(k) for k in h2o.ls()["key"]]
