@@ -219,6 +219,9 @@ def install(app, cfg: LoginConfig) -> None:
     async def login_gate(request, call_next):
         if request.method == "TRACE":
             return Response(status_code=405)
+        from . import cloud
+        if cloud.is_internal(request.headers):     # a cloud rank re-running a request rank 0 already authenticated
+            return await call_next(request)
         path = request.url.path
         headers = request.headers
         page = "text/html" in (headers.get("accept") or "")

@@ -657,8 +657,13 @@ def create_app(client_disconnect_timeout: float | None = None, login=None):
     def mojo(mid: str):
         import tempfile
         from ..mojo.writer import write_mojo
-        path = os.path.join(tempfile.gettempdir(), f"{mid}.zip")
-        write_mojo(_get_model(mid), path)
+        from . import cloud
+        m = _get_model(mid)
+        path = cloud.shared_path(f"{mid}.zip") if cloud.in_task() else os.path.join(tempfile.gettempdir(), f"{mid}.zip")
+        cloud.rank0_write(lambda: write_mojo(m, path))
+        if cloud.in_task() and cloud.rank() != 0:
+            from fastapi.responses import Response
+            return Response(b"")
         return FileResponse(path, filename=f"{mid}.zip", headers={"Content-Disposition": f'attachment; filename="{mid}.zip"'})
 
     @app.get("/99/Models.bin/{mid}")
@@ -812,9 +817,19 @@ def create_app(client_disconnect_timeout: float | None = None, login=None):
         if "multipart/form-data" in ct and "boundary=" in ct:
             data, fname = _multipart_first_file(body, ct.split("boundary=", 1)[1].strip().strip('"'))
         ext = os.path.splitext(fname)[1] or ".csv"
-        fd, path = tempfile.mkstemp(prefix="h2o_upload_", suffix=ext)
-        with os.fdopen(fd, "wb") as f:
-            f.write(data)
+        from . import cloud
+        if cloud.in_task():          # REST cloud: one copy, written by rank 0, at a path every rank derives
+            path = cloud.shared_path(f"upload{ext}")
+
+            def write():
+                with open(path + ".part", "wb") as f:
+                    f.write(data)
+                os.replace(path + ".part", path)
+            cloud.rank0_write(write)
+        else:
+            fd, path = tempfile.mkstemp(prefix="h2o_upload_", suffix=ext)
+            with os.fdopen(fd, "wb") as f:
+                f.write(data)
         return {"__meta": v3.meta("PostFileV3", "Iced"), "destination_frame": path, "total_bytes": len(data)}
 
     @app.post("/99/AutoMLBuilder")
@@ -918,6 +933,9 @@ def create_app(client_disconnect_timeout: float | None = None, login=None):
         media = "text/html" if name.endswith(".html") else "application/javascript"
         return FileResponse(path, media_type=media)
 
+    # multi-rank cloud: rank 0 routes every cloud request through the executor (inside the login gate)
+    from . import cloud
+    cloud.install(app)
     if login is not None:
         from . import security
         security.install(app, login.validate())
@@ -957,7 +975,24 @@ def main(argv=None):
         except (OSError, ValueError) as e:
             ap.error(f"-jks {a.jks}: {e}")
         ssl_kw = dict(ssl_certfile=cf, ssl_keyfile=kf)
-    uvicorn.run(create_app(login=login), host=a.ip, port=a.port, log_level="warning", **ssl_kw)
+    app = create_app(login=login)
+    from . import cloud
+    from ..parallel import collectives as coll
+    if coll.world_active():
+        # the SPMD cloud: every rank builds the same app; rank 0 serves HTTP, the others execute its requests
+        ex = cloud.CloudExecutor(app)
+        if ex.rank != 0:
+            ex.loop()
+            runtime.shutdown()
+            return
+        ex.start()
+        try:
+            uvicorn.run(app, host=a.ip, port=a.port, log_level="warning", **ssl_kw)
+        finally:
+            ex.stop()
+            runtime.shutdown()
+        return
+    uvicorn.run(app, host=a.ip, port=a.port, log_level="warning", **ssl_kw)
 
 
 if __name__ == "__main__":

@@ -76,7 +76,7 @@ def cloud(st: dict) -> dict:
     for i, n in enumerate(st.get("nodes") or []):
         nodes.append({"__meta": meta("NodeV3", "Iced"), "h2o": n.get("h2o", "127.0.0.1"), "ip_port": n.get("h2o", ""),
                       "healthy": bool(n.get("healthy", True)), "last_ping": int(time.time() * 1000),
-                      "pid": 0, "num_cpus": n.get("num_cpus") or 0, "cpus_allowed": n.get("num_cpus") or 0,
+                      "pid": int(n.get("pid", 0) or 0), "num_cpus": n.get("num_cpus") or 0, "cpus_allowed": n.get("num_cpus") or 0,
                       "nthreads": n.get("num_cpus") or 0, "sys_load": 0.0, "my_cpu_pct": -1, "sys_cpu_pct": -1,
                       "mem_value_size": 0, "pojo_mem": 0, "free_mem": n.get("free_mem", 0) or 0,
                       "max_mem": n.get("mem_total", 0) or 0, "swap_mem": 0, "num_keys": 0, "free_disk": 0,

@@ -24,6 +24,11 @@ from .core.job import Job
 from .grid import _metric_of
 from .models import builder
 
+
+def _coll():
+    from .parallel import collectives as coll
+    return coll
+
 _DEFAULT_SORT = {"Binomial": "auc", "Multinomial": "mean_per_class_error", "Regression": "mean_residual_deviance"}
 _DESC = {"auc", "aucpr", "r2"}
 
@@ -199,7 +204,7 @@ class AutoML:
         self.nfolds = nfolds
         if nfolds not in (0, -1) and int(nfolds) == 1:
             raise ValueError("nfolds set to 1; use nfolds >= 2 or 0 (no cross-validation)")
-        self.seed = seed if seed not in (None, -1) else int(np.random.SeedSequence().entropy % (1 << 31))
+        self.seed = seed if seed not in (None, -1) else _coll().shared_entropy(1 << 31)
         self.sort_metric = sort_metric
         self.include = [a.lower() for a in include_algos] if include_algos else None
         self.exclude = [a.lower() for a in exclude_algos] if exclude_algos else []

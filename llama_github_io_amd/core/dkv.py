@@ -21,7 +21,9 @@ _counter = itertools.count(1)
 
 
 def new_key(prefix: str = "key") -> str:
-    return f"{prefix}_{int(time.time() * 1000) % 100_000_000:08d}_{next(_counter)}"
+    from ..api import cloud            # inside a REST cloud task every rank must mint the same key
+    k = cloud.task_key(prefix) if cloud.active() else None
+    return k or f"{prefix}_{int(time.time() * 1000) % 100_000_000:08d}_{next(_counter)}"
 
 
 def put(key: str, value) -> None:

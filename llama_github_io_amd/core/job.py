@@ -69,7 +69,10 @@ class Job:
         return self._cancel.is_set()
 
     def check_cancelled(self) -> None:
-        if self._cancel.is_set():
+        from ..api import cloud
+        # REST cloud: a cancel reaches rank 0 only; every rank stops at the same check (rank 0's flag, broadcast)
+        flag = cloud.agree_flag(self._cancel.is_set()) if cloud.active() else self._cancel.is_set()
+        if flag:
             raise JobCancelled(self.key)
         from ..parallel import cluster
         cluster.check()
@@ -108,6 +111,9 @@ class Job:
         return self.result
 
     def run_async(self, fn, *args, **kwargs) -> "Job":
+        from ..api import cloud
+        if cloud.defer_job(self, fn, args, kwargs):     # REST cloud: the executor runs it on every rank, in order
+            return self
         self._thread = threading.Thread(target=self._execute, args=(fn, args, kwargs), daemon=True,
                                         name=f"h2o-job-{self.key}")
         self._thread.start()

@@ -82,18 +82,36 @@ def is_running() -> bool:
     return _state["started"] is not None
 
 
+def node_info() -> dict:
+    """This rank's entry of the cloud's node list (CloudV3 ``nodes``)."""
+    import torch.distributed as dist
+    d = device()
+    rk = dist.get_rank() if dist.is_initialized() else 0
+    if d.type == "cuda":
+        props = torch.cuda.get_device_properties(d)
+        free, total = torch.cuda.mem_get_info(d)
+        return dict(h2o=f"{socket.gethostname()}/rank{rk}", gpu=props.name, gcn_arch=getattr(props, "gcnArchName", ""),
+                    num_cus=props.multi_processor_count, mem_total=total, free_mem=free, healthy=True, rank=rk,
+                    device=str(d), pid=os.getpid())
+    return dict(h2o=f"{socket.gethostname()}/rank{rk}", gpu=None, num_cpus=os.cpu_count(), healthy=True, rank=rk,
+                device=str(d), pid=os.getpid())
+
+
 def cluster_status() -> dict:
     import torch.distributed as dist
     world = dist.get_world_size() if dist.is_initialized() else 1
     d = device()
-    nodes = []
-    if d.type == "cuda":
-        props = torch.cuda.get_device_properties(d)
-        free, total = torch.cuda.mem_get_info(d)
-        nodes.append(dict(h2o=socket.gethostname(), gpu=props.name, gcn_arch=getattr(props, "gcnArchName", ""),
-                          num_cus=props.multi_processor_count, mem_total=total, free_mem=free, healthy=True))
+    from ..api import cloud
+    ex = cloud.executor()
+    if ex is not None:          # the REST cloud: every rank's entry (gathered at cloud start), rank 0's live
+        nodes = [dict(n) for n in ex.nodes]
+        nodes[0] = node_info()
+        from ..parallel import cluster as _cl
+        dead = set(_cl.status()["dead"])
+        for n in nodes:
+            n["healthy"] = n.get("rank") not in dead
     else:
-        nodes.append(dict(h2o=socket.gethostname(), gpu=None, num_cpus=os.cpu_count(), healthy=True))
+        nodes = [node_info()]
     from ..parallel import cluster
     from ..utils import memory
     hb = cluster.status()

@@ -500,5 +500,9 @@ _key_counter = [0]
 
 
 def make_key(algo: str) -> str:
+    from ..api import cloud            # REST cloud task: the same model key on every rank
+    k = cloud.task_key(f"{algo.upper()}_model") if cloud.active() else None
+    if k:
+        return k
     _key_counter[0] += 1
     return f"{algo.upper()}_model_{int(time.time() * 1000) % 10_000_000}_{_key_counter[0]}"

@@ -164,7 +164,8 @@ def _fold_ids(fr, info, params, n, seed):
 def _seed_of(params):
     s = params.get("seed")
     if s is None or int(s) == -1:
-        return int(np.random.SeedSequence().entropy % (1 << 62))
+        from ..parallel import collectives as coll
+        return coll.shared_entropy(1 << 62)
     return int(s)
 
 

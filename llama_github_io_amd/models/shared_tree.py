@@ -34,9 +34,13 @@ SHARED_TREE_DEFAULTS = dict(
 )
 
 
+_CANCEL_EVERY = 4     # trees between cancellation checks of a REST job
+
+
 def resolve_seed(seed) -> int:
     if seed is None or int(seed) == -1:
-        return int(np.random.SeedSequence().entropy % (1 << 62))
+        from ..parallel import collectives as coll
+        return coll.shared_entropy(1 << 62)
     return int(seed)
 
 
@@ -344,6 +348,11 @@ class SharedTreeTrainer:
                 self._save_in_training(model, built, ck_dir)
             if max_rt > 0 and coll.agree(time.time() - t_start > max_rt):
                 break
+            job = getattr(self, "job", None)
+            if job is not None:                  # SharedTree.doScoringAndSaveModel: progress + stop_requested per tree
+                job.worked = job.work * built / max(ntrees, 1)
+                if (built - start) % _CANCEL_EVERY == 0:
+                    job.check_cancelled()        # (REST cloud: a collective; every rank checks at the same trees)
         self._drain(handles, forest, gains)
         if hprof and built > start + 2:
             n = (built - start - 2) * K

@@ -192,6 +192,13 @@ def broadcast_object(obj, src: int = 0):
     return box[0]
 
 
+def shared_entropy(modulus: int) -> int:
+    """A fresh random integer in [0, modulus) that every rank agrees on (rank 0's draw): unseeded models of a
+    sharded run (seed = -1) must still sample rows / columns alike on every rank."""
+    v = int(np.random.SeedSequence().entropy % int(modulus))
+    return int(broadcast_object(v)) if world_active() else v
+
+
 def exclusive_offset(n_local: int) -> tuple:
     """(global index of this rank's first row, global row count) for a rank-ordered row split."""
     if not world_active():

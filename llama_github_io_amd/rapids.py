@@ -291,7 +291,9 @@ class Session:
             value = _as_frame(value)
         elif value.frame_id != name and dkv.get(value.frame_id) is value:
             # the source keeps its own key (AstAssign builds a new Frame over the same vecs)
-            value = H2OFrame._from_columns([value._col(n) for n in value.names])
+            from .parallel import dframe
+            with dframe.shard_ctx(value._shard):      # a row-sharded source stays sharded under its new name
+                value = H2OFrame._from_columns([value._col(n) for n in value.names])
         dkv.put(name, value)
         value.frame_id = name
         return value

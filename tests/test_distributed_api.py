@@ -243,3 +243,79 @@ def test_sharded_api_equals_single(csv_and_single, world):
     csv, single, d = csv_and_single
     sharded = _launch(world, csv, list(CASES), str(d / f"w{world}.json"))
     _compare(single, sharded, world)
+
+
+def _run_selection(csv, out_path):
+    """Grid search and AutoML as SPMD programs (their budgets, model counts and orders agree over the ranks:
+    ``coll.agree`` / ``broadcast_object``; every model trains row-sharded)."""
+    sys.path.insert(0, ROOT)
+    import h2o
+    from h2o.automl import H2OAutoML
+    from h2o.estimators import H2OGradientBoostingEstimator
+    from h2o.grid import H2OGridSearch
+    h2o.init(verbose=False)
+    fr = h2o.import_file(csv)
+    x = ["x0", "x1", "x2", "x3", "cat"]
+    res = {"cloud_size": h2o.cluster().cloud_size}
+    gs = H2OGridSearch(H2OGradientBoostingEstimator(ntrees=3, seed=1),
+                       hyper_params={"max_depth": [2, 3], "learn_rate": [0.1, 0.3]})
+    gs.train(x=x, y="yb", training_frame=fr)
+    g = gs.get_grid(sort_by="auc", decreasing=True)
+    res["grid_n"] = len(g.model_ids)
+    res["grid_auc"] = sorted(float(m.auc()) for m in g.models)
+    gr = H2OGridSearch(H2OGradientBoostingEstimator(ntrees=2, seed=2), hyper_params={"max_depth": [1, 2, 3, 4]},
+                       search_criteria={"strategy": "RandomDiscrete", "max_models": 2, "seed": 5})
+    gr.train(x=x, y="yb", training_frame=fr)
+    res["random_grid"] = sorted(int(m.actual_params["max_depth"]) for m in gr.models)
+    # (AutoML's tree steps train up to 10^4 early-stopped trees: far too slow for the CPU reference builder; the SPMD
+    # control flow — budgets, step plan, CV, leaderboard, the stacked ensemble — is what this pins)
+    aml = H2OAutoML(max_models=3, seed=3, nfolds=2, include_algos=["GLM", "StackedEnsemble"])
+    aml.train(x=x, y="yb", training_frame=fr)
+    lb = aml.leaderboard.as_data_frame()
+    res["aml_n"] = int(len(lb))
+    res["aml_algos"] = sorted(str(m).split("_")[0] for m in lb["model_id"])
+    res["aml_auc"] = sorted(float(v) for v in lb["auc"])
+    import llama_github_io_amd.parallel.collectives as coll
+    if coll.rank() == 0:
+        with open(out_path, "w") as f:
+            json.dump(res, f)
+
+
+def _sel_worker(rank, world, port, csv, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), H2O_AMD_DEVICE="cpu", OMP_NUM_THREADS="1")
+    _run_selection(csv, out_path)
+    import torch.distributed as dist
+    if dist.is_initialized():
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def _launch_sel(world, csv, out_path):
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_sel_worker, args=(r, world, port, csv, out_path)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(900)
+        assert p.exitcode == 0, f"rank exited with {p.exitcode}"
+    with open(out_path) as f:
+        return json.load(f)
+
+
+def test_sharded_grid_and_automl_equal_single(tmp_path):
+    csv = str(tmp_path / "data.csv")
+    _write_csv(csv)
+    one = _launch_sel(1, csv, str(tmp_path / "sel1.json"))
+    two = _launch_sel(2, csv, str(tmp_path / "sel2.json"))
+    assert one["cloud_size"] == 1 and two["cloud_size"] == 2
+    assert two["grid_n"] == one["grid_n"] == 4
+    assert np.allclose(two["grid_auc"], one["grid_auc"], atol=1e-4)
+    assert two["random_grid"] == one["random_grid"] and len(one["random_grid"]) == 2
+    assert two["aml_n"] == one["aml_n"] >= 1 and two["aml_algos"] == one["aml_algos"]
+    # CV AUCs of sharded runs merge fixed-lattice score histograms (equal to ~1e-4)
+    assert np.allclose(two["aml_auc"], one["aml_auc"], atol=1e-4), (one["aml_auc"], two["aml_auc"])
