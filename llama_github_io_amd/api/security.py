@@ -124,6 +124,7 @@ class LoginConfig:
     login_conf: str | None = None
     form_auth: bool = False
     session_timeout: int = 0          # minutes of inactivity (form_auth); 0 = no timeout
+    secure_cookies: bool = False      # the server speaks HTTPS (-jks): session cookies carry the Secure flag
 
     def validate(self) -> "LoginConfig":
         import os
@@ -160,16 +161,30 @@ _FORM = """<!DOCTYPE html><html><head><title>H2O Login</title></head><body>
 
 
 class _Sessions:
-    def __init__(self, timeout_s: float):
+    """Logged-in sessions only (the pre-login target travels in a short-lived cookie, never here). Bounded: expired
+    entries are swept on every new session and at most ``cap`` live ones are kept (the least recently seen go)."""
+
+    def __init__(self, timeout_s: float, cap: int = 4096):
         self.timeout_s = timeout_s
+        self.cap = int(cap)
         self._lock = threading.Lock()
         self._s: dict[str, dict] = {}
 
     def new(self, **kw) -> str:
         sid = secrets.token_urlsafe(24)
+        now = time.time()
         with self._lock:
-            self._s[sid] = dict(kw, seen=time.time())
+            if self.timeout_s:
+                for k in [k for k, v in self._s.items() if now - v["seen"] > self.timeout_s]:
+                    del self._s[k]
+            while len(self._s) >= self.cap:
+                del self._s[min(self._s, key=lambda k: self._s[k]["seen"])]
+            self._s[sid] = dict(kw, seen=now)
         return sid
+
+    def __len__(self) -> int:
+        with self._lock:
+            return len(self._s)
 
     def get(self, sid: str | None) -> dict | None:
         if not sid:
@@ -184,6 +199,21 @@ class _Sessions:
                 return None
             s["seen"] = now
             return s
+
+
+TARGET_COOKIE = "H2O_LOGIN_TARGET"
+
+
+def _safe_target(t: str | None) -> str:
+    """A post-login redirect target that stays on this server: a single-slash absolute path, or '/'."""
+    from urllib.parse import unquote
+    if not t:
+        return "/"
+    raw = unquote(t)
+    if not raw.startswith("/") or raw.startswith("//") or "\\" in raw or ":" in raw.split("?", 1)[0] or \
+            any(ord(ch) < 32 for ch in raw):
+        return "/"
+    return t
 
 
 def _is_browser(headers) -> bool:
@@ -209,7 +239,9 @@ def install(app, cfg: LoginConfig) -> None:
     from starlette.responses import HTMLResponse, JSONResponse, RedirectResponse, Response
     svc = HashLoginService(cfg.login_conf)
     sessions = _Sessions(60.0 * cfg.session_timeout)
+    install.sessions = sessions                  # (tests: the live session table)
     cookie = "JSESSIONID"
+    secure = bool(cfg.secure_cookies)
 
     def unauthorized(msg="Access denied. Please login."):
         return JSONResponse(status_code=401, content={"http_status": 401, "msg": msg},
@@ -234,12 +266,11 @@ def install(app, cfg: LoginConfig) -> None:
             form = parse_qs((await request.body()).decode("utf-8", "replace"))
             user = (form.get("j_username") or [""])[0]
             pw = (form.get("j_password") or [""])[0]
-            pending = sessions.get(request.cookies.get(cookie))
             if not svc.login(user, pw):
                 return RedirectResponse("/loginError", status_code=303)
-            target = (pending or {}).get("target") or "/"
-            r = RedirectResponse(target, status_code=303)
-            r.set_cookie(cookie, sessions.new(user=user), httponly=True, path="/")
+            r = RedirectResponse(_safe_target(request.cookies.get(TARGET_COOKIE)), status_code=303)
+            r.set_cookie(cookie, sessions.new(user=user), httponly=True, path="/", secure=secure)
+            r.delete_cookie(TARGET_COOKIE, path="/")
             return r
         s = sessions.get(request.cookies.get(cookie))
         if s is not None and s.get("user"):
@@ -248,9 +279,10 @@ def install(app, cfg: LoginConfig) -> None:
         if cred is not None and svc.login(*cred):
             return await call_next(request)
         if cfg.form_auth and _is_browser(headers):
-            # FormAuthenticator: remember the requested URI in a pending session, send the browser to the form
-            target = path + (("?" + request.url.query) if request.url.query else "")
+            # FormAuthenticator: remember the requested URI (a short-lived cookie: no server state per anonymous
+            # request), send the browser to the form
+            target = _safe_target(quote(path + (("?" + request.url.query) if request.url.query else ""), safe="/?=&"))
             r = RedirectResponse("/login", status_code=302)
-            r.set_cookie(cookie, sessions.new(target=quote(target, safe="/?=&")), httponly=True, path="/")
+            r.set_cookie(TARGET_COOKIE, target, max_age=600, httponly=True, path="/", secure=secure)
             return r
         return unauthorized()

@@ -975,6 +975,7 @@ def main(argv=None):
         except (OSError, ValueError) as e:
             ap.error(f"-jks {a.jks}: {e}")
         ssl_kw = dict(ssl_certfile=cf, ssl_keyfile=kf)
+        login.secure_cookies = True
     app = create_app(login=login)
     from . import cloud
     from ..parallel import collectives as coll
@@ -987,12 +988,31 @@ def main(argv=None):
             return
         ex.start()
         try:
-            uvicorn.run(app, host=a.ip, port=a.port, log_level="warning", **ssl_kw)
+            _serve(app, a.ip, a.port, ssl_kw)
         finally:
             ex.stop()
             runtime.shutdown()
         return
-    uvicorn.run(app, host=a.ip, port=a.port, log_level="warning", **ssl_kw)
+    _serve(app, a.ip, a.port, ssl_kw)
+
+
+def uvicorn_config(app, host, port, ssl_kw):
+    """uvicorn config with the TLS context built up front: the unsealed private key's PEM file (``-jks``) is deleted
+    as soon as the SSL context holds it, so it never outlives startup on disk."""
+    import shutil
+    import uvicorn
+    cfg = uvicorn.Config(app, host=host, port=port, log_level="warning", **ssl_kw)
+    if ssl_kw:
+        try:
+            cfg.load()
+        finally:
+            shutil.rmtree(os.path.dirname(ssl_kw["ssl_keyfile"]), ignore_errors=True)
+    return cfg
+
+
+def _serve(app, host, port, ssl_kw):
+    import uvicorn
+    uvicorn.Server(uvicorn_config(app, host, port, ssl_kw)).run()
 
 
 if __name__ == "__main__":

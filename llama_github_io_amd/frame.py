@@ -342,14 +342,15 @@ class H2OFrame:
     @frame_id.setter
     def frame_id(self, newid):
         # assigning a new id renames the frame's DKV entry (the reference's setter issues a Rapids ``rename``)
+        # A frame a running job write-locks cannot be renamed (the reference's Rapids rename fails on a locked key):
+        # the rename raises and the frame keeps its one key.
         old = self.__dict__.get("_frame_id")
-        self.__dict__["_frame_id"] = newid
         if old is not None and newid != old and dkv.contains(old) and dkv.get(old) is self:
-            try:
-                dkv.remove(old)
-            except RuntimeError:     # write-locked by a running job: the old key stays until the job ends
-                pass
+            dkv.remove(old)          # RuntimeError while write-locked: nothing changed
+            self.__dict__["_frame_id"] = newid
             dkv.put(newid, self)
+            return
+        self.__dict__["_frame_id"] = newid
 
     def __init__(self, python_obj=None, destination_frame=None, header=0, separator=",", column_names=None,
                  column_types=None, na_strings=None, skipped_columns=None):

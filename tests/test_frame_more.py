@@ -79,3 +79,17 @@ def test_concat_rep_getrow_structure(fr, capsys):
     assert fr[0, :].getrow()[1] == 1.0
     fr.structure()
     assert "obs. of 3 variables" in capsys.readouterr().out
+
+
+def test_frame_id_rename_refused_while_write_locked():
+    """Renaming a frame a job holds write-locked fails and leaves exactly one live key (reference Rapids rename)."""
+    import pytest
+    from llama_github_io_amd.core import dkv
+    from llama_github_io_amd.frame import H2OFrame
+    fr = H2OFrame({"a": [1.0, 2.0]}, destination_frame="locked_src")
+    with dkv.write_lock("locked_src"):
+        with pytest.raises(RuntimeError):
+            fr.frame_id = "locked_dst"
+        assert fr.frame_id == "locked_src" and dkv.get("locked_src") is fr and not dkv.contains("locked_dst")
+    fr.frame_id = "locked_dst"
+    assert dkv.get("locked_dst") is fr and not dkv.contains("locked_src")

@@ -60,7 +60,7 @@ def _leaf_paths(tl):
     return leaves, nodes
 
 
-def _assert_same_tree_up_to_ties(tl_r, tl_g, lr, lg, rtol=1e-5):
+def _assert_same_tree_up_to_ties(tl_r, tl_g, lr, lg, rtol=1e-5, vectorized=False):
     """Tie-aware exact comparison of a tree grown from fp32-wire histograms with the fp64 reference tree:
     * wherever the two trees take different decisions, the two decisions have equal gain (a tie between equal-gain
       splits, which fp32 rounding of the exchanged sums may break differently), and
@@ -80,6 +80,17 @@ def _assert_same_tree_up_to_ties(tl_r, tl_g, lr, lg, rtol=1e-5):
         assert abs(float(dr["gain"]) - float(dg["gain"])) <= rtol * g, (path, dr["feat"], dg["feat"], dr["gain"],
                                                                          dg["gain"])
         tied.append(path)
+    if vectorized:          # per-leaf codes instead of per-row path strings (100M-row trees)
+        paths = sorted(set(leaves_r.values()) | set(leaves_g.values()))
+        code = {q: i for i, q in enumerate(paths)}
+        cr = np.array([code[leaves_r[k]] for k in range(len(leaves_r))], dtype=np.int64)
+        cg = np.array([code[leaves_g[k]] for k in range(len(leaves_g))], dtype=np.int64)
+        fr = np.array([not any(leaves_r[k].startswith(t) for t in tied) for k in range(len(leaves_r))])
+        lr, lg = np.asarray(lr, dtype=np.int64), np.asarray(lg, dtype=np.int64)
+        free = fr[lr]
+        assert free.mean() > 0.5, "ties under the root"
+        assert (cr[lr][free] == cg[lg][free]).all(), int((cr[lr][free] != cg[lg][free]).sum())
+        return
     pr = np.array([leaves_r[int(k)] for k in lr], dtype=object)
     pg = np.array([leaves_g[int(k)] for k in lg], dtype=object)
     free = np.array([not any(p.startswith(t) for t in tied) for p in pr])
@@ -196,3 +207,32 @@ def test_tree_on_one_rank_nccl_process_group(force_env):
     finally:
         rccl.reset()
         dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_gpu_partial_f32_default_at_100m_rows(monkeypatch):
+    """fp32 per-block partial histograms are the default for every N >= 1M (H2O_PARTIAL_F32): at 100M rows (the
+    XGBoost BASELINE shape's row count) the tree equals the fp64-partials tree up to equal-gain ties, and rows are
+    routed identically below every non-tied node."""
+    N, F = 100_000_000, 8
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(11)
+    bins = torch.randint(0, 250, (N, 32), generator=g, device=dev, dtype=torch.uint8)
+    bins[:, F:] = 0
+    y = ((bins[:, 0].float() - 125) / 70 - (bins[:, 1] > 130).float() + 0.5 * torch.sin(bins[:, 2].float() / 20) +
+         torch.randn(N, generator=g, device=dev) > 0).float()
+    aux = torch.stack([torch.ones_like(y), y - 0.5, y - 0.5, torch.full_like(y, 0.25)], 0).contiguous()
+    p = T.SplitParams(min_w=10)
+    nb = np.full(F, 250, np.int32)
+    ic = np.zeros(F, np.int32)
+    out = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("H2O_PARTIAL_F32", flag)
+        gb = T.GpuTreeBuilder(bins, F, nb, ic, None, 6, p)
+        assert gb.pf32 == int(flag)
+        gb.build(aux, soa=True, packed=True, unit=True, leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1]).float())
+        out.append((gb.pop_levels()[0], gb.leaf_of_row.cpu().numpy().copy()))
+        del gb
+        torch.cuda.empty_cache()
+    (tl64, l64), (tl32, l32) = out
+    _assert_same_tree_up_to_ties(tl64, tl32, l64, l32, vectorized=True)

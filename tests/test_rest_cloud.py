@@ -17,7 +17,7 @@ import pytest
 REF = "/root/reference/h2o-py"
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
-pytestmark = pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "h2o")), reason="reference h2o-py not present")
+needs_ref = pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "h2o")), reason="reference h2o-py not present")
 
 CLIENT = textwrap.dedent("""
     import json, os, sys, tempfile
@@ -78,19 +78,28 @@ def _data(tmp_path, n=600):
     return csv
 
 
-def _serve_and_run(tmp_path, csv, world):
+def _serve_and_run(tmp_path, csv, world, env_over=None, torchrun=False):
     port = _free_port()
     env = dict(os.environ, PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", H2O_AMD_DEVICE="cpu",
                OMP_NUM_THREADS="2")
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
-    if world == 1:
+    if env_over:
+        env.update(env_over)
+        if env_over.get("H2O_AMD_DEVICE") == "cuda":
+            for k in ("CUDA_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES"):
+                if os.environ.get(k) is None:
+                    env.pop(k, None)
+                else:
+                    env[k] = os.environ[k]
+    if world == 1 and not torchrun:
         cmd = [sys.executable, "-m", "llama_github_io_amd.api.server", "--port", str(port)]
     else:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
                "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
                "-m", "llama_github_io_amd.api.server", "--port", str(port)]
-    log = open(tmp_path / f"server{world}.log", "w")
+    tag = f"{world}{'t' if torchrun else ''}{env.get('H2O_AMD_DEVICE')}"
+    log = open(tmp_path / f"server{tag}.log", "w")
     srv = subprocess.Popen(cmd, cwd=ROOT, env=env, stdout=log, stderr=subprocess.STDOUT, start_new_session=True)
     try:
         t0 = time.time()
@@ -99,16 +108,16 @@ def _serve_and_run(tmp_path, csv, world):
                 socket.create_connection(("127.0.0.1", port), timeout=1).close()
                 break
             except OSError:
-                assert srv.poll() is None, open(tmp_path / f"server{world}.log").read()[-3000:]
+                assert srv.poll() is None, open(tmp_path / f"server{tag}.log").read()[-3000:]
                 time.sleep(0.5)
-        script = tmp_path / f"client{world}.py"
+        script = tmp_path / f"client{tag}.py"
         script.write_text(CLIENT % dict(ref=REF, port=port, csv=str(csv)))
         cenv = {k: v for k, v in os.environ.items() if k != "PYTHONPATH"}
         r = subprocess.run([sys.executable, str(script)], cwd=str(tmp_path), env=cenv, capture_output=True, text=True,
                            timeout=900)
         out = r.stdout + r.stderr
         lines = [ln for ln in r.stdout.splitlines() if ln.startswith("RESULT ")]
-        assert r.returncode == 0 and lines, out[-4000:] + open(tmp_path / f"server{world}.log").read()[-4000:]
+        assert r.returncode == 0 and lines, out[-4000:] + open(tmp_path / f"server{tag}.log").read()[-4000:]
         return json.loads(lines[0][7:])
     finally:
         os.killpg(srv.pid, 15)
@@ -120,6 +129,7 @@ def _serve_and_run(tmp_path, csv, world):
         log.close()
 
 
+@needs_ref
 def test_rest_cloud_two_ranks_matches_single_process(tmp_path):
     csv = _data(tmp_path)
     one = _serve_and_run(tmp_path, csv, 1)
@@ -170,6 +180,7 @@ CANCEL_CLIENT = textwrap.dedent("""
 """)
 
 
+@needs_ref
 def test_rest_cloud_cancel_and_polling(tmp_path):
     """``GET /3/Jobs`` answers while a cloud job runs (rank 0 alone); ``cancel`` stops the job on EVERY rank at the
     same progress check, and the cloud keeps serving in lock step afterwards."""
@@ -184,3 +195,65 @@ def test_rest_cloud_cancel_and_polling(tmp_path):
     assert out["seen"] is not None and 0 < out["seen"] < 1
     assert out["cancel_status"] == 200 and out["status"] == "CANCELLED"
     assert out["auc"] > 0.7 and out["nodes"] == 2
+
+
+RAW_CLIENT = textwrap.dedent('''
+    import io, json, sys, time, zipfile
+    import requests
+    base = "http://127.0.0.1:%(port)d"
+
+    def call(method, route, **data):
+        enc = {k: (json.dumps(v) if isinstance(v, (list, dict)) else v) for k, v in data.items()}
+        r = requests.request(method, base + route, params=enc if method == "GET" else None,
+                             data=None if method == "GET" else enc, timeout=600)
+        assert r.status_code == 200, (route, r.status_code, r.text[:500])
+        return r
+
+    def wait(job):
+        key = job["key"]["name"]
+        while True:
+            j = call("GET", "/3/Jobs/" + key).json()["jobs"][0]
+            if j["status"] in ("DONE", "FAILED", "CANCELLED"):
+                assert j["status"] == "DONE", j
+                return j
+            time.sleep(0.1)
+
+    out = {"cloud_size": call("GET", "/3/Cloud").json()["cloud_size"]}
+    src = call("POST", "/3/ImportFiles", path=%(csv)r).json()["destination_frames"]
+    ps = call("POST", "/3/ParseSetup", source_frames=src).json()
+    wait(call("POST", "/3/Parse", source_frames=src, destination_frame="d.hex", column_names=ps["column_names"],
+              column_types=ps["column_types"], separator=ps["separator"], check_header=ps["check_header"]).json()["job"])
+    for algo, params in (("gbm", dict(ntrees=5, max_depth=3, seed=1)), ("glm", dict(family="binomial", lambda_=1e-3))):
+        j = call("POST", "/3/ModelBuilders/" + algo, training_frame="d.hex", response_column="yb", model_id=algo + "_m",
+                 **params).json()["job"]
+        wait(j)
+        m = call("GET", "/3/Models/" + algo + "_m").json()["models"][0]
+        out[algo + "_auc"] = m["output"]["training_metrics"]["AUC"]
+    call("POST", "/3/Predictions/models/gbm_m/frames/d.hex", predictions_frame="p.hex")
+    csv_txt = call("GET", "/3/DownloadDataset", frame_id="p.hex").text.splitlines()
+    out["pred_yes"] = [float(l.split(",")[2]) for l in csv_txt[1:]]
+    z = zipfile.ZipFile(io.BytesIO(call("GET", "/3/Models/gbm_m/mojo").content))
+    out["mojo_files"] = sorted(z.namelist())[:5]
+    print("RESULT " + json.dumps(out))
+''')
+
+
+@pytest.mark.gpu
+def test_rest_cloud_gpu_rank_matches_single_process(tmp_path):
+    """The cloud executor on a GPU: a 1-rank ``nccl`` cloud (``H2O_FORCE_SHARDED=1``: every trainer takes its
+    row-sharded path, collectives through RCCL from the executor thread) serves the same models and predictions as
+    the plain single-process GPU server (raw REST client: no reference tree on the GPU box)."""
+    global CLIENT
+    csv = _data(tmp_path)
+    saved = CLIENT
+    CLIENT = RAW_CLIENT
+    try:
+        gpu_env = dict(H2O_AMD_DEVICE="cuda")
+        one = _serve_and_run(tmp_path, csv, 1, env_over=gpu_env)
+        cl = _serve_and_run(tmp_path, csv, 1, env_over=dict(gpu_env, H2O_FORCE_SHARDED="1"), torchrun=True)
+    finally:
+        CLIENT = saved
+    assert one["cloud_size"] == cl["cloud_size"] == 1
+    assert abs(one["gbm_auc"] - cl["gbm_auc"]) < 1e-4 and abs(one["glm_auc"] - cl["glm_auc"]) < 1e-4
+    assert np.allclose(one["pred_yes"], cl["pred_yes"], atol=1e-5) and len(cl["pred_yes"]) == 600
+    assert one["mojo_files"] == cl["mojo_files"]

@@ -110,3 +110,51 @@ def test_login_option_rules(tmp_path):
     with pytest.raises(SystemExit):
         main(["-form_auth"])
     assert not L().validate().enabled
+
+
+def test_form_auth_anonymous_requests_leave_no_server_state(tmp_path):
+    """Cookie-less browser requests keep their post-login target in a short-lived cookie: the session table stays
+    empty however many arrive, and only a successful login adds (one) entry."""
+    app = create_app(login=security.LoginConfig(hash_login=True, login_conf=_realm(tmp_path), form_auth=True))
+    ua = {"User-Agent": "Mozilla/flood"}
+    for i in range(300):
+        r = TestClient(app).get(f"/3/Frames/f{i}", headers=ua, follow_redirects=False)
+        assert r.status_code == 302
+    assert len(security.install.sessions) == 0
+    c = TestClient(app)
+    c.get("/3/Cloud", headers=ua, follow_redirects=False)
+    ok = c.post("/j_security_check", data={"j_username": "jenkins_user", "j_password": "jenkins_pwd42"}, headers=ua,
+                follow_redirects=False)
+    assert ok.status_code == 303 and ok.headers["location"] == "/3/Cloud"
+    assert len(security.install.sessions) == 1
+
+
+def test_form_auth_never_redirects_off_host(tmp_path):
+    app = create_app(login=security.LoginConfig(hash_login=True, login_conf=_realm(tmp_path), form_auth=True))
+    ua = {"User-Agent": "Mozilla/x"}
+    for bad in ("//evil.example/x", "/\\evil.example", "https://evil.example/", "/%2F%2Fevil.example"):
+        c = TestClient(app)
+        c.cookies.set(security.TARGET_COOKIE, bad)
+        ok = c.post("/j_security_check", data={"j_username": "jenkins_user", "j_password": "jenkins_pwd42"},
+                    headers=ua, follow_redirects=False)
+        assert ok.status_code == 303 and ok.headers["location"] == "/", (bad, ok.headers["location"])
+    c = TestClient(app)
+    c.get("//evil.example/x", headers=ua, follow_redirects=False)
+    ok = c.post("/j_security_check", data={"j_username": "jenkins_user", "j_password": "jenkins_pwd42"}, headers=ua,
+                follow_redirects=False)
+    loc = ok.headers["location"]
+    assert loc.startswith("/") and not loc.startswith("//"), loc
+    # a bounded table even when sessions never expire (session_timeout 0)
+    s = security._Sessions(0.0, cap=8)
+    for _ in range(50):
+        s.new(user="u")
+    assert len(s) == 8
+
+
+def test_secure_cookie_flag_over_https(tmp_path):
+    app = create_app(login=security.LoginConfig(hash_login=True, login_conf=_realm(tmp_path), form_auth=True,
+                                                secure_cookies=True))
+    c = TestClient(app, base_url="https://testserver")
+    ok = c.post("/j_security_check", data={"j_username": "jenkins_user", "j_password": "jenkins_pwd42"},
+                headers={"User-Agent": "Mozilla/x"}, follow_redirects=False)
+    assert "secure" in ok.headers["set-cookie"].lower()

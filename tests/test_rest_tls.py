@@ -64,3 +64,14 @@ def test_https_server_with_login(tmp_path):
     finally:
         server.should_exit = True
         th.join(10)
+
+
+def test_jks_private_key_pem_deleted_after_startup(tmp_path):
+    """The PEM files unsealed from the keystore live only until uvicorn has built its SSL context."""
+    pytest.importorskip("uvicorn")
+    from llama_github_io_amd.api.server import create_app, uvicorn_config
+    cf, kf = tls.pem_files(KS, "password")
+    assert os.path.exists(kf)
+    cfg = uvicorn_config(create_app(), "127.0.0.1", 0, dict(ssl_certfile=cf, ssl_keyfile=kf))
+    assert cfg.loaded and cfg.ssl is not None
+    assert not os.path.exists(kf) and not os.path.exists(cf) and not os.path.exists(os.path.dirname(kf))
