@@ -75,6 +75,19 @@ struct SplitParams {
   unsigned long long seed;
   int hist_type;           // numeric candidate lattice (with adapt_nb > 1): HT_* below
   int fcut;                // > 0: only columns < fcut are searched (narrow levels of wide numeric bins, TreePlan)
+  // The reference's node range (DTree.java:337-375) for the adaptive lattices (range_on != 0): the root bins over
+  // its columns' [min, max] (vrange: exact extremes of every column over ALL rows; the open-ended first / last bins
+  // map to them); a node at depth >= 1 over the range its PARENT's histogram observed (hprev: the previous level's
+  // node histograms, same slot layout), narrowed at the parent's numeric split (pdec) for every column of the split
+  // feature (fgroup: engine column -> feature in bits 0-29; null = identity). Global column ids throughout (f + f0);
+  // edges_all: [F][255] edges of every column (the split column's threshold value).
+  const float* vrange;
+  const double* hprev;
+  const Dec* pdec;
+  const Node* rnodes;
+  const int* fgroup;
+  const float* edges_all;
+  int range_on, pad_r;
 };
 
 // histogram types (SharedTreeParameters.HistogramType) as candidate lattices over the global bins
@@ -1214,11 +1227,48 @@ __device__ __forceinline__ void split_find_body(
     const double cw = sw[t], pw = t > 0 ? sw[t - 1] : 0.0;
     if (t < nb && cw > 0 && pw == 0) a_lo = t;
     if (t < nb && W > 0 && cw == W && pw < W) a_hi = t;
+    __shared__ int r_lo, r_hi;
+    const bool ranged = p.range_on != 0;
+    if (ranged) {
+      // the observed range the node bins over: its own at the root, its parent's below (the parent's slot of the
+      // previous level's histograms, this column's data bins)
+      if (t == 0) { r_lo = 1 << 30; r_hi = -1; }
+      __syncthreads();
+      const Node* rn = p.rnodes ? p.rnodes + node : nullptr;
+      const bool up = level > 0 && rn != nullptr && rn->parent >= 0 && p.hprev != nullptr;
+      if (up) {
+        const double pwt = (t < nb && t < NA_BIN) ? p.hprev[(size_t)rn->parent * slot_doubles + (size_t)t * hs + 2 * f]
+                                                  : 0.0;
+        if (pwt > 0) { atomicMin(&r_lo, t); atomicMax(&r_hi, t); }
+      } else if (t < nb && t < NA_BIN && w > 0) {
+        atomicMin(&r_lo, t); atomicMax(&r_hi, t);
+      }
+    }
     __syncthreads();
     const float* e = edges + (size_t)f * 255;
-    if (a_hi > a_lo && (lt == HT_RANDOM || a_hi - a_lo + 1 > adapt_nb)) {
-      const double lo = (double)e[a_lo > 0 ? a_lo - 1 : 0];
-      const double hi = (double)e[a_hi <= nb - 2 ? a_hi : nb - 2];
+    if (a_hi > a_lo && (ranged || lt == HT_RANDOM || a_hi - a_lo + 1 > adapt_nb)) {
+      double lo = (double)e[a_lo > 0 ? a_lo - 1 : 0];
+      double hi = (double)e[a_hi <= nb - 2 ? a_hi : nb - 2];
+      if (ranged) {
+        const int gf = f + f0;
+        if (r_hi < 0) {
+          lo = hi = 0.0;                              // the parent saw no value of this column: no lattice cut
+        } else {
+          lo = r_lo > 0 ? (double)e[r_lo - 1] : (double)p.vrange[2 * gf];
+          hi = r_hi < nb - 1 ? (double)e[r_hi] : (double)p.vrange[2 * gf + 1];
+          const Node* rn = p.rnodes ? p.rnodes + node : nullptr;
+          if (level > 0 && rn != nullptr && rn->parent >= 0 && p.pdec != nullptr) {
+            const Dec& pd = p.pdec[rn->parent];
+            const bool same = p.fgroup ? ((p.fgroup[gf] & 0x3FFFFFFF) == (p.fgroup[pd.feat] & 0x3FFFFFFF))
+                                       : (pd.feat == gf);
+            if (pd.feat >= 0 && !pd.is_cat && pd.bin != NA_BIN && pd.bin > 0 && same) {
+              const double v = (double)p.edges_all[(size_t)pd.feat * 255 + pd.bin - 1];
+              if (rn->dir == 0) hi = hi < v ? hi : v;
+              else lo = lo > v ? lo : v;
+            }
+          }
+        }
+      }
       if (hi > lo) {
         const double sc = (double)adapt_nb / (hi - lo);
         auto cnt = [&](double x) -> int {
@@ -2793,6 +2843,8 @@ int h2o_split_find(const void* hist, int slot_doubles, const void* meta, int cap
   SplitParams p;
   p.min_w = min_w; p.min_split_improvement = msi; p.lambda = lambda_; p.alpha = alpha; p.gamma = gamma;
   p.mode = mode; p.random_split = random_split; p.seed = seed; p.hist_type = hist_type; p.fcut = 0;
+  p.vrange = nullptr; p.hprev = nullptr; p.pdec = nullptr; p.rnodes = nullptr; p.fgroup = nullptr; p.edges_all = nullptr;
+  p.range_on = 0; p.pad_r = 0;
   return split_find_launch((void*)hist, slot_doubles, meta, cap, F, nbins_f, iscat_f, mono_f, p, level, cand, root_w,
                            edges, adapt_nb, f0, FL, Derive{nullptr, 0, 0, nullptr, nullptr}, s);
 }
@@ -3090,7 +3142,22 @@ struct TreePlan {
   void* f16col;               // [f16_planes * 16][4] int32: engine column of subset k (or -1)
   void* f16n;                 // [f16_planes * 16] int32: the feature's engine columns (0: empty slot)
   int f16_planes, pad5;
+  // the reference's node ranges of the adaptive lattices (SplitParams.range_on / vrange): [F][2] exact column extremes
+  void* vrange;
+  int range_on, pad6;
 };
+
+// node-range fields of a level's split search (see SplitParams)
+static inline void tp_node_range(const TreePlan* P, int d, const void* hprev, SplitParams& p) {
+  p.range_on = (P->range_on && P->vrange && P->edges && P->nb_level[d] > 1) ? 1 : 0;
+  p.vrange = (const float*)P->vrange;
+  p.hprev = d > 0 ? (const double*)hprev : nullptr;
+  p.pdec = d > 0 ? (const Dec*)P->dec[d - 1] : nullptr;
+  p.rnodes = (const Node*)P->nodes[d];
+  p.fgroup = (const int*)P->fgroup;
+  p.edges_all = (const float*)P->edges;
+  p.pad_r = 0;
+}
 
 // op codes / dtypes of the collective transport
 enum { H2O_COLL_ALLREDUCE = 0, H2O_COLL_REDUCE_SCATTER = 1, H2O_COLL_ALLGATHER = 2 };
@@ -3180,6 +3247,7 @@ int h2o_tree_find(const TreePlan* P, int d, hipStream_t s) {
   p.min_w = P->min_w; p.min_split_improvement = P->msi; p.lambda = P->lam; p.alpha = P->alpha; p.gamma = P->gamma;
   p.mode = P->mode; p.random_split = P->random_split; p.seed = P->seed; p.hist_type = P->hist_type;
   p.fcut = tp_fcut(P, d);
+  tp_node_range(P, d, hp, p);
   const int hs = P->sliced ? P->sslot : P->slot;
   const Derive dv = P->dist ? Derive{P->hrecv, P->cf32, P->sslot, (const double*)hp, (const Node*)P->nodes[d]}
                             : Derive{nullptr, 0, 0, nullptr, nullptr};
@@ -3216,6 +3284,7 @@ static int tree_find_plan(const TreePlan* P, int d, hipStream_t s) {
   p.min_w = P->min_w; p.min_split_improvement = P->msi; p.lambda = P->lam; p.alpha = P->alpha; p.gamma = P->gamma;
   p.mode = P->mode; p.random_split = P->random_split; p.seed = P->seed; p.hist_type = P->hist_type;
   p.fcut = tp_fcut(P, d);
+  tp_node_range(P, d, (d % 2) ? P->hist0 : P->hist1, p);
   const int cap = P->caps[d];
   const int kc = P->kc_level[d] > 0 ? P->kc_level[d] : P->k_cols;
   const PlanReduce pr{(const Cand*)P->cand, P->F, (const int*)P->feat_ok, kc, P->seed,

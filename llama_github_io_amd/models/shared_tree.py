@@ -182,7 +182,25 @@ class SharedTreeTrainer:
             sp.adapt_top = int(self.p.get("nbins_top_level") or 1024)
             sp.edges = self._edge_table()
             sp.hist_type = T.HIST_TYPES[ht]
+            sp.vrange = getattr(self, "_vrange", None)
+            sp.parent_range = os.environ.get("H2O_HIST_PARENT_RANGE", "1") != "0"
         return sp
+
+    def _value_range_table(self, X):
+        """[F_engine, 2] float32: every column's exact (min, max) over ALL rows (all ranks), the range of the
+        reference's root histogram (DHistogram.initialHist: the column's rollup min / max)."""
+        Xf = X.float()
+        nan = torch.isnan(Xf)
+        mn = torch.where(nan, torch.full_like(Xf, float("inf")), Xf).amin(1) if Xf.shape[1] else \
+            torch.full((Xf.shape[0],), float("inf"), device=Xf.device)
+        mx = torch.where(nan, torch.full_like(Xf, float("-inf")), Xf).amax(1) if Xf.shape[1] else \
+            torch.full((Xf.shape[0],), float("-inf"), device=Xf.device)
+        if coll.is_dist():
+            coll.all_reduce_min_(mn)
+            coll.all_reduce_max_(mx)
+        vr = torch.stack([mn, mx], 1).cpu().numpy().astype(np.float32)
+        vm = self.binning.vmap
+        return vr if vm is None else vr[np.asarray(vm)]
 
     def _edge_table(self):
         tab = np.full((self.binning.F, 255), np.inf, dtype=np.float32)
@@ -245,6 +263,8 @@ class SharedTreeTrainer:
             self.binning = fit_binning(X, info.iscat, info.nlevels, max_bins=max_bins, seed=self.seed,
                                        max_cat_bins=int(p.get("nbins_cats") or 1024), sample=bsample)
         self._check_binning(self.binning)
+        ht = str(p.get("histogram_type", "AUTO")).lower().replace("_", "")
+        self._vrange = self._value_range_table(X) if T.HIST_TYPES.get(ht, 0) != T.HT_QUANTILES else None
         bins = apply_binning(self.binning, X, planar=X.is_cuda)
         mono = None
         if p.get("monotone_constraints"):

@@ -126,6 +126,12 @@ class SplitParams:
     edges: object = None
     # lattice of the split points (HT_*): UniformAdaptive, Random, UniformRobust or RoundRobin
     hist_type: int = 1
+    # [F, 2] float32 exact (min, max) of every engine column over ALL rows (the root histogram's range,
+    # DHistogram.initialHist); with it the open-ended first / last bins map to the true extremes. None: edges only.
+    vrange: object = None
+    # the reference's node range (DTree.java:337-375): a node at depth >= 1 bins over the range its PARENT's
+    # histogram observed, narrowed at the parent's split for the split feature; False: the node's own occupied range
+    parent_range: bool = True
 
     def adapt_nb(self, level: int) -> int:
         if not self.adapt_nbins or self.edges is None:
@@ -166,9 +172,25 @@ def _leafv(mode, p, w, y):
     return y / w if w > 0 else 0.0
 
 
-def _lattice(p: SplitParams, level, node, f, nb, w, sw, W, seed, off):
+def _bin_lo(p: SplitParams, f, b):
+    """Lower value bound of data bin b of engine column f (bin 0: the column's true minimum when known)."""
+    if b > 0:
+        return float(np.float32(p.edges[f][b - 1]))
+    return float(np.float32(p.vrange[f][0])) if p.vrange is not None else float(np.float32(p.edges[f][0]))
+
+
+def _bin_hi(p: SplitParams, f, b, nb):
+    """Upper (exclusive) value bound of data bin b (the last data bin: the column's true maximum when known)."""
+    if b < nb - 1:
+        return float(np.float32(p.edges[f][b]))
+    return float(np.float32(p.vrange[f][1])) if p.vrange is not None else float(np.float32(p.edges[f][nb - 2]))
+
+
+def _lattice(p: SplitParams, level, node, f, nb, w, sw, W, seed, off, vr=None):
     """Allowed thresholds t = 1 .. nb-1 of the histogram type's split points (None = every threshold);
-    mirrors the lattice block of k_split_find (UniformAdaptive / Random / UniformRobust / RoundRobin)."""
+    mirrors the lattice block of k_split_find (UniformAdaptive / Random / UniformRobust / RoundRobin).
+    ``vr`` = (lo, hi): the node's value range (the parent's observed range narrowed at its split, see
+    :meth:`RefTreeBuilder.build`); None: the node's own occupied range."""
     anb = p.adapt_nb(level)
     lt = p.hist_type if (anb > 1 and not off) else HT_QUANTILES
     if lt == HT_ROUND_ROBIN:
@@ -180,11 +202,14 @@ def _lattice(p: SplitParams, level, node, f, nb, w, sw, W, seed, off):
     if not (occ.size and occ[-1] > occ[0]):
         return None
     a_lo, a_hi = int(occ[0]), int(occ[-1])
-    if lt != HT_RANDOM and not a_hi - a_lo + 1 > anb:
-        return None
     e = np.asarray(p.edges[f], dtype=np.float32).astype(np.float64)
-    lo = float(e[a_lo - 1 if a_lo > 0 else 0])
-    hi = float(e[a_hi if a_hi <= nb - 2 else nb - 2])
+    if vr is not None:
+        lo, hi = float(vr[0]), float(vr[1])
+    else:
+        if lt != HT_RANDOM and not a_hi - a_lo + 1 > anb:
+            return None
+        lo = float(e[a_lo - 1 if a_lo > 0 else 0])
+        hi = float(e[a_hi if a_hi <= nb - 2 else nb - 2])
     if not hi > lo:
         return None
     sc = anb / (hi - lo)
@@ -234,8 +259,10 @@ def _lattice(p: SplitParams, level, node, f, nb, w, sw, W, seed, off):
     return mark[1:nb]
 
 
-def split_find_ref(h, nayy, wyy, nbins_f, iscat_f, mono_f, p: SplitParams, level: int, node: int, seed: int):
-    """h: float64 [F, 256, 2]. Returns list of per-feature candidate dicts."""
+def split_find_ref(h, nayy, wyy, nbins_f, iscat_f, mono_f, p: SplitParams, level: int, node: int, seed: int,
+                   vranges=None):
+    """h: float64 [F, 256, 2]. Returns list of per-feature candidate dicts. ``vranges``: [F, 2] value ranges of
+    the node (reference node ranges, :meth:`RefTreeBuilder.build`) or None."""
     F = h.shape[0]
     out = []
     for f in range(F):
@@ -262,7 +289,8 @@ def split_find_ref(h, nayy, wyy, nbins_f, iscat_f, mono_f, p: SplitParams, level
                 lo, hi = int(occ[0]), int(occ[-1])
                 hsh = splitmix64((seed ^ (level << 48) ^ (node << 20) ^ f) & _M64)
                 rand_b = lo + 1 + int(hsh % (hi - lo))
-        allowed = _lattice(p, level, node, f, nb, w, sw, W, seed, cat or random_mode)
+        allowed = _lattice(p, level, node, f, nb, w, sw, W, seed, cat or random_mode,
+                           None if vranges is None else vranges[f])
         best_e, best_code = -1.0e300, -1
         cands = []
         if wNA >= p.min_w and W > 0 and not random_mode:
@@ -476,8 +504,50 @@ class RefTreeBuilder:
                 nayy[f0 + j] = yy[bf[:, j] == NA_BIN].sum()
         return h, nayy, yy.sum()
 
+    def _ranges_on(self) -> bool:
+        p = self.p
+        return (bool(p.parent_range) and bool(p.adapt_nbins) and p.edges is not None and p.vrange is not None
+                and p.hist_type != HT_QUANTILES)
+
+    def _occupied(self, h):
+        """[F, 2] int: first / last occupied data bin of every column of a node histogram (-1: none)."""
+        F = self.F
+        occ = np.full((F, 2), -1, dtype=np.int64)
+        for f in range(F):
+            nb = min(int(self.nbins_f[f]), NA_BIN)
+            nz = np.nonzero(h[f, :nb, 0] > 0)[0]
+            if nz.size:
+                occ[f] = (nz[0], nz[-1])
+        return occ
+
+    def _value_ranges(self, occ, split=None, side=0):
+        """[F, 2] value ranges of a node: the parent's observed ranges ``occ`` (bins -> values; the open-ended
+        first / last bins -> the column's true extremes), and for the parent's numeric split ``split`` = (column,
+        bin) the narrowing of every column of the same feature at the split value (DTree.java:360-375: the left
+        side's exclusive max / the right side's min)."""
+        p, F = self.p, self.F
+        vr = np.full((F, 2), np.nan)
+        for f in range(F):
+            if occ[f, 0] < 0 or self.iscat_f[f]:
+                continue
+            nb = int(self.nbins_f[f])
+            vr[f] = (_bin_lo(p, f, int(occ[f, 0])), _bin_hi(p, f, int(occ[f, 1]), nb))
+        if split is not None:
+            sf, b = split
+            v = float(np.float32(p.edges[sf][b - 1]))
+            grp = getattr(self, "fgroup", None)
+            for f in range(F):
+                same = f == sf if grp is None else grp[f] == grp[sf]
+                if same and not np.isnan(vr[f, 0]):
+                    if side == 0:
+                        vr[f, 1] = min(vr[f, 1], v)
+                    else:
+                        vr[f, 0] = max(vr[f, 0], v)
+        return vr
+
     def build(self, aux_static: torch.Tensor, feat_ok=None, k_cols: int = 0, seed: int = 0, leaf_fn=None):
         aux = aux_static.detach().cpu().numpy().astype(np.float32)
+        ranges = self._ranges_on()
         F, D, p = self.F, self.D, self.p
         feat_ok = np.ones(F, dtype=np.int32) if feat_ok is None else np.asarray(feat_ok)
         leaf_of_row = np.full(self.N, -1, dtype=np.int64)
@@ -485,12 +555,14 @@ class RefTreeBuilder:
         leafsum = []
         level_rows = [np.arange(self.N)]
         level_ok = [None if self.ic_map is None else self.ic_root]
+        level_vr = [None]                 # per node: [F, 2] value ranges (None at the root: its own, set below)
         decs, cls, crs = [], [], []
         n_leaves = 0
         for d in range(D):
             cap_next = min(1 << (d + 1), self.node_cap) if d + 1 < D else 1
             n = len(level_rows)
             dl = np.zeros(n, dtype=DEC_DT)
+            level_occ = []
             for i, rows in enumerate(level_rows):
                 h, nayy, wyy = self._hist(rows, aux)
                 if coll.is_dist():  # row-sharded: every rank sees the global node histogram
@@ -500,7 +572,11 @@ class RefTreeBuilder:
                     h = flat[: h.size].reshape(h.shape)
                     nayy = flat[h.size: h.size + F]
                     wyy = float(flat[-1])
-                cands = split_find_ref(h, nayy, wyy, self.nbins_f, self.iscat_f, self.mono_f, p, d, i, seed)
+                vr = None
+                if ranges:
+                    level_occ.append(self._occupied(h))
+                    vr = level_vr[i] if level_vr[i] is not None else self._value_ranges(level_occ[i])
+                cands = split_find_ref(h, nayy, wyy, self.nbins_f, self.iscat_f, self.mono_f, p, d, i, seed, vr)
                 fc = level_fcut(cut, self.n_low, self.n_mid, d)
                 if fc:                          # narrow level: the columns past fc are not searched
                     for f in range(fc, F):
@@ -508,7 +584,7 @@ class RefTreeBuilder:
                 dl[i] = split_reduce_ref(cands, feat_ok, _level_k(k_cols, d), seed, d, i, level_ok[i],
                                          getattr(self, "fgroup", None))
             cl = np.zeros(n, dtype=np.int64); cr = np.zeros(n, dtype=np.int64)
-            nxt, nxt_ok = [], []
+            nxt, nxt_ok, nxt_vr = [], [], []
             act = 0
             for i, rows in enumerate(level_rows):
                 dd = dl[i]
@@ -527,6 +603,10 @@ class RefTreeBuilder:
                     if active:
                         arr[i] = len(nxt); nxt.append(crow)
                         nxt_ok.append(None if self.ic_map is None else level_ok[i] & self.ic_map[dd["feat"]])
+                        if ranges:
+                            num = not dd["is_cat"] and int(dd["bin"]) != NA_BIN
+                            nxt_vr.append(self._value_ranges(level_occ[i], (int(dd["feat"]), int(dd["bin"]))
+                                                             if num else None, side))
                     else:
                         lid = n_leaves; n_leaves += 1
                         arr[i] = -1 - lid
@@ -535,6 +615,7 @@ class RefTreeBuilder:
             decs.append(dl); cls.append(cl); crs.append(cr)
             level_rows = nxt
             level_ok = nxt_ok
+            level_vr = nxt_vr if ranges else [None] * len(nxt)
             if not nxt:
                 break
         res = TreeLevels(decs, cls, crs, n_leaves)
@@ -588,7 +669,8 @@ class _TreePlan(ctypes.Structure):
                 [(n, _ci) for n in ("W", "cf32", "cand_fs", "dist")] + [(n, _vp) for n in ("hsend", "cand_all", "lsx")] +
                 [("fine_f", _vp)] + [(n, _ci) for n in ("lo_F", "lo_from", "mid_F", "mid_from")] + [("lvl2", _vp), ("fdir", _vp)] +
                 [("num_plane", _ci), ("pad4", _ci)] +
-                [(n, _vp) for n in ("fine16", "f16col", "f16n")] + [("f16_planes", _ci), ("pad5", _ci)])
+                [(n, _vp) for n in ("fine16", "f16col", "f16n")] + [("f16_planes", _ci), ("pad5", _ci)] +
+                [("vrange", _vp), ("range_on", _ci), ("pad6", _ci)])
 
 
 class _Arena:
@@ -944,6 +1026,13 @@ class GpuTreeBuilder:
         for d in range(_MAXL):
             P.nb_level[d] = p.adapt_nb(d) if P.edges else 0
         P.hist_type = int(p.hist_type)
+        # the reference's node ranges (SplitParams.parent_range): exact column extremes on the device
+        if P.edges and p.vrange is not None and p.parent_range and p.hist_type != HT_QUANTILES:
+            self._vrange_dev = torch.as_tensor(np.asarray(p.vrange, dtype=np.float32).reshape(-1),
+                                               device=self.dev).contiguous()
+            P.vrange, P.range_on = self._vrange_dev.data_ptr(), 1
+        else:
+            P.vrange, P.range_on = 0, 0
         self._set_plan_ic(P)
         fg = getattr(self, "fgroup", None)
         P.fgroup = 0 if fg is None else fg.data_ptr()

@@ -52,6 +52,9 @@ def metrics(ps, X, y):
     return round(ll, 5), round(float(roc_auc_score(y.numpy(), p.numpy())), 4)
 
 
+SUB = 0
+
+
 def train(mode, X, y, H, B, epochs, rho=0.99, eps=1e-8, seed=1):
     ps = init(X.shape[1], H, seed)
     Eg = [torch.zeros_like(p) for p in ps]
@@ -83,6 +86,29 @@ def train(mode, X, y, H, B, epochs, rho=0.99, eps=1e-8, seed=1):
                             rate = torch.sqrt((d + eps) / (e + eps))
                             d.mul_(rho).add_((1 - rho) * rate * rate * gg * gg)
                             p.sub_(rate * gg)
+                elif mode in ("batch_sub", "batch_sub_mean"):
+                    # per-row-equivalent sub-steps: B ADADELTA steps per batch, each moving along the batch-mean
+                    # gradient; the accumulators see the per-row mean square (batch_sub: (delta^2)^T (x^2), one extra
+                    # GEMM on device) or the squared mean (batch_sub_mean: no extra pass)
+                    from torch.func import grad, vmap
+
+                    def lossf(pp, xi, yi):
+                        return torch.nn.functional.cross_entropy(fwd(pp, xi[None]), yi[None])
+                    if mode == "batch_sub":
+                        per = vmap(grad(lossf), in_dims=(None, 0, 0))([p.detach() for p in ps], X[idx], y[idx])
+                        gms = [gi.mean(0) for gi in per]
+                        qs = [(gi * gi).mean(0) for gi in per]
+                    else:
+                        loss = torch.nn.functional.cross_entropy(fwd(ps, X[idx]), y[idx])
+                        gms = list(torch.autograd.grad(loss, ps))
+                        qs = [gm * gm for gm in gms]
+                    with torch.no_grad():
+                        for p, gm, q, e, d in zip(ps, gms, qs, Eg, Ed):
+                            for _ in range(SUB if SUB else B):
+                                e.mul_(rho).add_((1 - rho) * q)
+                                rate = torch.sqrt((d + eps) / (e + eps))
+                                d.mul_(rho).add_((1 - rho) * rate * rate * q)
+                                p.sub_(rate * gm)
                 else:   # batch_seq: exact per-row sums S1, S2 (per-sample gradients via vmap)
                     from torch.func import functional_call, grad, vmap
 
@@ -108,9 +134,13 @@ def main():
     ap.add_argument("--hidden", type=int, default=32)
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--epochs", type=int, default=3)
+    ap.add_argument("--modes", default="batch_mean,batch_seq,rowwise")
+    ap.add_argument("--sub", type=int, default=0, help="sub-steps per batch for batch_sub* (0 = batch size)")
     a = ap.parse_args()
     X, y = data(a.rows, a.feat)
-    for mode in ("batch_mean", "batch_seq", "rowwise"):
+    global SUB
+    SUB = a.sub
+    for mode in a.modes.split(","):
         print(json.dumps({"mode": mode, "batch": 1 if mode == "rowwise" else a.batch,
                           "epochs_logloss_auc": train(mode, X, y, a.hidden, a.batch, a.epochs)}), flush=True)
 

@@ -126,7 +126,8 @@ def main():
     ap.add_argument("--holdout", type=int, default=50_000)
     ap.add_argument("--trees", type=int, default=30)
     ap.add_argument("--depth", type=int, default=5)
-    ap.add_argument("--out", default="profiles/r5_default_histogram_report")
+    ap.add_argument("--out", default="profiles/r6_default_histogram_report")
+    ap.add_argument("--shapes", default="higgs28,lognormal10,counts6,regress8")
     a = ap.parse_args()
     import h2o
     from llama_github_io_amd.ops import dhist_oracle as O
@@ -134,6 +135,8 @@ def main():
     res = {}
     n = a.rows + a.holdout
     for name, (X, y, dist) in shapes(n).items():
+        if name not in a.shapes.split(","):
+            continue
         Xtr, ytr, Xho, yho = X[:a.rows], y[:a.rows], X[a.rows:], y[a.rows:]
         sd = Xtr.std(0) + 1e-300
         r = res[name] = {"rows": a.rows, "features": X.shape[1], "distribution": dist}

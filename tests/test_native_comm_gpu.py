@@ -143,14 +143,16 @@ def test_narrow_planar_tree_on_rccl_matches_reference(mode, force_env):
     """H2O's default histogram on wide bins (1016 edges per feature, planar rows): the narrow levels (column
     limits, low-entry reduce, one-plane routes, root-direction bytes, level-2 leaf-walk start) through the
     row-sharded driver on a 1-rank RCCL communicator, decision for decision against RefTreeBuilder."""
-    from test_tree_engine import _edge_tab
+    from test_tree_engine import _edge_tab, _vr
     X, y, info = _data(N=30000, F=10, cat=True, seed=11)
+    X = X.clone()
+    X[1] = torch.exp(3 * X[1])              # heavy tail: the reference's node ranges (parent-observed, narrowed)
     b = fit_binning(X, info.iscat, info.nlevels, max_bins=1016)
     assert b.stride >= 64 and b.n_low == X.shape[0]
     bins = apply_binning(b, X)
     g = y - 0.5
     aux = torch.stack([torch.ones_like(y), g, g, torch.ones_like(y)], 1).contiguous()
-    p = T.SplitParams(min_w=10, adapt_nbins=20, adapt_top=1024, edges=_edge_tab(b))
+    p = T.SplitParams(min_w=10, adapt_nbins=20, adapt_top=1024, edges=_edge_tab(b), vrange=_vr(b, X))
     ref = T.RefTreeBuilder(bins, b.F, b.nbins, b.iscat, None, 5, p)
     ref.set_feature_groups(b.vmap, b.n_low, b.n_mid)
     ref.build(aux, leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1]).float())

@@ -377,25 +377,32 @@ def test_gbm_histogram_types_train(ht):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", ["adaptive", "newton", "random", "mono", "kcols", "featok", "multiclass",
-                                  "interaction", "hist_random", "hist_robust", "hist_roundrobin"])
+                                  "interaction", "hist_random", "hist_robust", "hist_roundrobin", "adaptive_range",
+                                  "hist_robust_range", "hist_random_range"])
 def test_gpu_tree_modes_match_reference(case):
     """Every split mode of k_split_find / k_split_reduce pinned against RefTreeBuilder (identical
     feature / bin / left weight per decision and identical leaf assignment)."""
     X, y, info = _data(N=20000, cat=True, seed=9)
-    if case.startswith("hist_"):
+    if case.startswith("hist_") or case == "adaptive_range":
         X = X.clone()
         X[2] = torch.exp(4 * X[2])                   # heavy tail: sparse uniform lattices (UniformRobust)
         y = y + (X[2] > 2).float()
     b = fit_binning(X, info.iscat, info.nlevels, max_bins=255 if case.startswith("hist_") else 128)
+    # the reference's node ranges (DTree.java:337-375): exact column extremes, parent-observed ranges below the root
+    Xn = torch.nan_to_num(X, nan=float("inf"))
+    vr = np.stack([Xn.amin(1).numpy(), torch.nan_to_num(X, nan=-float("inf")).amax(1).numpy()], 1).astype(np.float32)
     bins = apply_binning(b, X)
     g = y - y.mean()
     aux = torch.stack([torch.ones_like(y), g, g, torch.ones_like(y)], 1).contiguous()
     mono, feat_ok, k_cols, depth = None, None, 0, 5
-    if case == "adaptive":
-        p = T.SplitParams(min_w=10, adapt_nbins=20, adapt_top=128, edges=_edge_tab(b))
+    if case in ("adaptive", "adaptive_range"):
+        p = T.SplitParams(min_w=10, adapt_nbins=20, adapt_top=128, edges=_edge_tab(b),
+                          vrange=vr if case == "adaptive_range" else None)
     elif case.startswith("hist_"):
-        ht = {"hist_random": T.HT_RANDOM, "hist_robust": T.HT_ROBUST, "hist_roundrobin": T.HT_ROUND_ROBIN}[case]
-        p = T.SplitParams(min_w=10, adapt_nbins=20, adapt_top=256, edges=_edge_tab(b), hist_type=ht)
+        ht = {"hist_random": T.HT_RANDOM, "hist_robust": T.HT_ROBUST,
+              "hist_roundrobin": T.HT_ROUND_ROBIN}[case.replace("_range", "")]
+        p = T.SplitParams(min_w=10, adapt_nbins=20, adapt_top=256, edges=_edge_tab(b), hist_type=ht,
+                          vrange=vr if case.endswith("_range") else None)
         depth = 6
     elif case == "newton":
         h = torch.full_like(y, 0.25)
@@ -618,6 +625,14 @@ def test_wide_bins_split_resolution_and_grouped_sampling():
         assert len({allowed[0], allowed[3], allowed[4], allowed[5]}) == 1 and sum(allowed) in (1, 4)
 
 
+def _vr(b, X):
+    """[F_engine, 2] exact column extremes (SplitParams.vrange: the reference's root range, DHistogram.initialHist)."""
+    lo = torch.nan_to_num(X, nan=float("inf")).amin(1).numpy()
+    hi = torch.nan_to_num(X, nan=-float("inf")).amax(1).numpy()
+    vr = np.stack([lo, hi], 1).astype(np.float32)
+    return vr if b.vmap is None else vr[np.asarray(b.vmap)]
+
+
 def test_narrow_levels_search_only_first_columns():
     """AUTO (UniformAdaptive, nbins_top_level 1024): the level whose adaptive bin count is 512 searches every
     other fine edge (first two column tiers), from 256 on only every feature's first column (ops/tree.narrow_cut)."""
@@ -642,14 +657,18 @@ def test_narrow_levels_search_only_first_columns():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("fine", ["0", "1"])
-@pytest.mark.parametrize("case", ["plain", "kcols_adaptive", "newton", "narrow_planar"])
+@pytest.mark.parametrize("case", ["plain", "kcols_adaptive", "newton", "narrow_planar", "kcols_adaptive_range",
+                                  "narrow_planar_range"])
 def test_gpu_wide_bins_match_reference(case, fine, monkeypatch):
     """1016-bin numeric features (4 engine columns each) on the GPU engine vs RefTreeBuilder: identical
     decisions, left weights and leaf assignment, including grouped column sampling (k_split_reduce fgroup), with and
     without the fine-bin atomics of the 4-column groups (H2O_HIST_FINE, its aligned layout), and the narrow levels
     of the default layout (adaptive cases: first columns only from level 2; planar: the routes move one plane)."""
     monkeypatch.setenv("H2O_HIST_FINE", fine)
-    X, y, info = _data(N=30000, F=10 if case == "narrow_planar" else 6, cat=True, seed=11)
+    X, y, info = _data(N=30000, F=10 if case.startswith("narrow_planar") else 6, cat=True, seed=11)
+    if case.endswith("_range"):
+        X = X.clone()
+        X[1] = torch.exp(3 * X[1])          # a heavy tail: the parent-observed ranges and extremes matter
     b = fit_binning(X, info.iscat, info.nlevels, max_bins=1016)
     assert b.vmap is not None and b.F > X.shape[0]
     bins = apply_binning(b, X)
@@ -659,12 +678,13 @@ def test_gpu_wide_bins_match_reference(case, fine, monkeypatch):
     aux = torch.stack([torch.ones_like(y), g, g, torch.ones_like(y)], 1).contiguous()
     k_cols = 0
     p = T.SplitParams(min_w=10)
-    if case == "kcols_adaptive":
+    vr = _vr(b, X) if case.endswith("_range") else None
+    if case.startswith("kcols_adaptive"):
         k_cols = 3
-        p = T.SplitParams(min_w=10, adapt_nbins=20, adapt_top=1024, edges=_edge_tab(b))
-    elif case == "narrow_planar":
+        p = T.SplitParams(min_w=10, adapt_nbins=20, adapt_top=1024, edges=_edge_tab(b), vrange=vr)
+    elif case.startswith("narrow_planar"):
         assert b.stride >= 64
-        p = T.SplitParams(min_w=10, adapt_nbins=20, adapt_top=1024, edges=_edge_tab(b))
+        p = T.SplitParams(min_w=10, adapt_nbins=20, adapt_top=1024, edges=_edge_tab(b), vrange=vr)
     elif case == "newton":           # unpacked two-plane histograms through the fine-bin atomics
         h = torch.full_like(y, 0.25)
         aux = torch.stack([h, -g, -g, h], 1).contiguous()
@@ -704,7 +724,7 @@ def test_gpu_root16_matches_reference(unit, monkeypatch):
     g = y - 0.5
     w = torch.ones_like(y) if unit else (torch.rand(y.shape, generator=torch.Generator().manual_seed(2)) < 0.8).float()
     aux = torch.stack([w, w * g, w * g, w], 1).contiguous()
-    p = T.SplitParams(min_w=10, adapt_nbins=20, adapt_top=1024, edges=_edge_tab(b))
+    p = T.SplitParams(min_w=10, adapt_nbins=20, adapt_top=1024, edges=_edge_tab(b), vrange=_vr(b, X))
     ref = T.RefTreeBuilder(bins, b.F, b.nbins, b.iscat, None, 5, p)
     ref.set_feature_groups(b.vmap, b.n_low, b.n_mid)
     ref.build(aux, None, 0, seed=5, leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1].clamp(min=1e-12)).float())
