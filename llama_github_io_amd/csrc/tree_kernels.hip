@@ -44,12 +44,15 @@ struct Node {      // one active node of a level (rows [start, start+len) of the
       dir /*odd levels: 0 left / 1 right child*/, pad1, pad2;
 };
 
-struct Dec {       // split decision (80 B)
+#define NBW 32     // 32-bit words of a decision bitset: 1024 bins (the levels of a wide-categorical group)
+#define GROUP_CAT 2
+struct Dec {       // split decision (176 B)
   int feat;        // -1: no split (terminal)
-  int bin;         // numeric: data bins < bin go left
+  int bin;         // numeric: data bins < bin go left; group split: the group's packed 'elsewhere' bytes
   int na_left;     // NA rows go left?
-  int is_cat;      // categorical: bitset `bits` over bins -> 1 = left
-  unsigned bits[8];
+  int is_cat;      // categorical: bitset `bits` over bins -> 1 = left; GROUP_CAT: a wide-categorical group
+                   // (columns feat..feat+3, one aligned row word; bits over the global bins 254k + b)
+  unsigned bits[NBW];
   double gain;     // improvement (for variable importance)
   double wl, wr;   // weighted row counts left/right
   float predl, predr;
@@ -63,7 +66,7 @@ struct Cand {      // best split of one (node, feature)
   double wl, wr;
   float predl, predr;
   int bin, na_left, valid, is_cat;
-  unsigned bits[8];
+  unsigned bits[NBW];
 };
 
 struct SplitParams {
@@ -88,6 +91,9 @@ struct SplitParams {
   const int* fgroup;
   const float* edges_all;
   int range_on, pad_r;
+  // wide-categorical groups (Binning.gcat, null: none): a group's first column = its real columns (1..4), its
+  // other columns -1; the first column's block searches one histogram over all of the group's levels
+  const int* gcat;
 };
 
 // histogram types (SharedTreeParameters.HistogramType) as candidate lattices over the global bins
@@ -106,6 +112,27 @@ __device__ __forceinline__ bool dec_go_left(const Dec* d, int b) {
   if (b == NA_BIN) return d->na_left != 0;
   if (d->is_cat) return (d->bits[b >> 5] >> (b & 31)) & 1u;
   return b < d->bin;
+}
+
+// the global bin (254k + byte) of a row of a wide-categorical group from its aligned group word: the one real
+// column whose byte is not its 'elsewhere' bin (byte k of `pack`; 0 = padding) holds the level; -1 = NA
+__device__ __forceinline__ int group_level(unsigned word, unsigned pack) {
+  if ((word & 0xFFu) == NA_BIN) return -1;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const unsigned ek = (pack >> (8 * k)) & 0xFFu, b = (word >> (8 * k)) & 0xFFu;
+    if (ek != 0u && b != ek) return 254 * k + (int)b;
+  }
+  return -1;
+}
+
+// a decision on its row key: the split column's byte, or (GROUP_CAT) the group's aligned row word
+__device__ __forceinline__ bool dec_go_left_key(const Dec* d, unsigned v) {
+  if (d->is_cat == GROUP_CAT) {
+    const int l = group_level(v, (unsigned)d->bin);
+    return l < 0 ? d->na_left != 0 : ((d->bits[l >> 5] >> (l & 31)) & 1u) != 0u;
+  }
+  return dec_go_left(d, (int)v);
 }
 
 // node index of tile t: largest i with tile_prefix[i] <= t
@@ -315,7 +342,12 @@ struct RowFilter {
   int dir;         // 0: accumulate left-goers, 1: right-goers
   int bin, na_left, is_cat;
   bool count;
-  __device__ __forceinline__ bool left(int b) const {
+  __device__ __forceinline__ bool left(unsigned v) const {
+    if (is_cat == GROUP_CAT) {              // v: the group's aligned row word
+      const int l = group_level(v, (unsigned)bin);
+      return l < 0 ? na_left != 0 : ((pd->bits[l >> 5] >> (l & 31)) & 1u) != 0u;
+    }
+    const int b = (int)v;
     if (b == NA_BIN) return na_left != 0;
     if (is_cat) return (pd->bits[b >> 5] >> (b & 31)) & 1u;
     return b < bin;
@@ -347,6 +379,14 @@ __device__ __forceinline__ void wave_sync_lds() {
 // unused)
 __device__ __forceinline__ void filt_load(const RowFilter& flt, int r0, int r1, unsigned (&byt)[FNP]) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (flt.is_cat == GROUP_CAT) {          // a wide-categorical group split: the group's aligned row word
+#pragma unroll
+    for (int p = 0; p < FNP; ++p) {
+      const int row = min(r0 + wv * WROWS + p * 64 + lane, r1 - 1);
+      byt[p] = *reinterpret_cast<const unsigned*>(flt.fptr + (size_t)row * (size_t)flt.fstride);
+    }
+    return;
+  }
 #pragma unroll
   for (int p = 0; p < FNP; ++p) {
     const int row = min(r0 + wv * WROWS + p * 64 + lane, r1 - 1);
@@ -368,7 +408,7 @@ __device__ __forceinline__ int filt_append(const RowFilter& flt, int r0, int r1,
     const int row = r0 + wv * WROWS + p * 64 + lane;
     bool sl = false;
     if (row < r1) {
-      const bool gl = flt.left((int)byt[p]);
+      const bool gl = flt.left(byt[p]);
       if (flt.count) lcnt += gl ? 1 : 0;
       sl = (gl ? 0 : 1) == flt.dir;
     }
@@ -1075,7 +1115,242 @@ __device__ __forceinline__ double add_mul_rn(double a, double x, double y) {
   return a + x * y;
 }
 
+// ------------------------------------------------------------------------------------------------
+// Wide-categorical group split (H2O's single sort over ALL levels, DTree.java:1004-1013): the group's first column
+// block merges the group's real columns into one histogram over the global bins g = 254k + b (k = column, b < its
+// 'elsewhere' bin), sorts all of them by mean response (empty bins first, ties by bin), scans every threshold of
+// the sorted order and writes one candidate whose bitset covers every level (NBW words). Same rules, order and
+// tie breaks as the single-column categorical search above (RefTreeBuilder: ops/tree.py split_find_ref, gcat).
+struct HistRead {        // a node histogram entry: the slot, or (row-sharded) derived from the exchanged build slots
+  const double* slot;
+  const void* recv;
+  const double* pv;
+  size_t rb;
+  int f32, build, derive;
+  __device__ __forceinline__ double operator()(size_t i) const {
+    if (!derive) return slot[i];
+    const double r = f32 ? (double)((const float*)recv)[rb + i] : ((const double*)recv)[rb + i];
+    return build ? r : pv[i] - r;
+  }
+};
+#define GBINS 1024
+__device__ void split_find_group(const HistRead& hv, int node, int f, int gg, int hs, int FL,
+                                 const int* __restrict__ nbins_f, const int* __restrict__ mono_f, const SplitParams& p,
+                                 int level, int f0, Cand* __restrict__ cand) {
+  __shared__ double gk[GBINS], gw[GBINS], gy[GBINS];
+  __shared__ int gi[GBINS];
+  __shared__ double gwt[8];
+  __shared__ double gbe[4];
+  __shared__ int gbc[4];
+  __shared__ unsigned gbits[NBW];
+  __shared__ int s_lo, s_hi;
+  const int t = threadIdx.x;                 // 256 threads, 4 bins each
+  int L = 0;
+  for (int k = 0; k < gg; ++k) L = 254 * k + (nbins_f[f + k] - 1);
+  for (int i = t; i < GBINS; i += 256) {
+    const int k = i / 254, b = i - 254 * k;
+    double w = 0.0, y = 0.0;
+    bool in = false;
+    if (k < gg && b < nbins_f[f + k] - 1) {
+      in = true;
+      w = hv((size_t)b * hs + 2 * (f + k));
+      y = hv((size_t)b * hs + 2 * (f + k) + 1);
+    }
+    gw[i] = w; gy[i] = y;
+    gk[i] = in ? (w > 0 ? y / w : -1.0e308) : 1.0e308;
+    gi[i] = i;
+  }
+  if (t < NBW) gbits[t] = 0u;
+  __syncthreads();
+  // bitonic sort of (key, bin) ascending over the 1024 entries
+  for (int k = 2; k <= GBINS; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = t; i < GBINS; i += 256) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const bool up = (i & k) == 0;
+          const double a = gk[i], b = gk[ixj];
+          const int ia = gi[i], ib = gi[ixj];
+          const bool gt = (a > b) || (a == b && ia > ib);
+          if (gt == up) { gk[i] = b; gk[ixj] = a; gi[i] = ib; gi[ixj] = ia; }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // inclusive prefix sums of (w, wy) in sorted order: thread t owns positions 4t .. 4t+3
+  double a[4], b[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { a[j] = gw[gi[4 * t + j]]; b[j] = gy[gi[4 * t + j]]; }
+#pragma unroll
+  for (int j = 1; j < 4; ++j) { a[j] += a[j - 1]; b[j] += b[j - 1]; }
+  {
+    const int lane = t & 63, wv = t >> 6;
+    double sa = a[3], sb = b[3];
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const double a2 = __shfl_up(sa, o, 64), b2 = __shfl_up(sb, o, 64);
+      if (lane >= o) { sa += a2; sb += b2; }
+    }
+    if (lane == 63) { gwt[wv] = sa; gwt[4 + wv] = sb; }
+    __syncthreads();
+    double oa = sa - a[3], ob = sb - b[3];          // exclusive prefix within the wave
+    for (int k = 0; k < wv; ++k) { oa += gwt[k]; ob += gwt[4 + k]; }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { a[j] += oa; b[j] += ob; }
+  }
+  __syncthreads();                                  // every gw / gy read done: reuse them as the sorted sums
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { gw[4 * t + j] = a[j]; gy[4 * t + j] = b[j]; }
+  __syncthreads();
+  const double* sw = gw;
+  const double* swy = gy;
+  const double W = sw[GBINS - 1], WY = swy[GBINS - 1];
+  const size_t iNA = (size_t)NA_BIN * hs + 2 * f;
+  const double wNA = hv(iNA), wyNA = hv(iNA + 1);
+  const double naYY = hv((size_t)FL * 2 * NBIN + f), wYY = hv((size_t)FL * 2 * NBIN + FL);
+  const double Wall = W + wNA, WYall = WY + wyNA;
+  auto E = [&](double ww, double yy) -> double {
+    if (p.mode == 1) {
+      double g = yy;
+      if (p.alpha > 0) g = (g > p.alpha) ? g - p.alpha : (g < -p.alpha ? g + p.alpha : 0.0);
+      return g * g / (ww + p.lambda);
+    }
+    return ww > 0 ? yy * yy / ww : 0.0;
+  };
+  auto leafv = [&](double ww, double yy) -> double {
+    return p.mode == 1 ? yy / (ww + p.lambda) : (ww > 0 ? yy / ww : 0.0);
+  };
+  const double min_w = p.min_w;
+  const int mono = mono_f ? mono_f[f] : 0;
+  const bool random_mode = p.random_split != 0;
+  int rand_b = -1;
+  if (random_mode) {
+    if (t == 0) { s_lo = 0; s_hi = -1; }
+    __syncthreads();
+    for (int j = 0; j < 4; ++j) {
+      const int q = 4 * t + j;
+      const double cw = sw[q], pw = q > 0 ? sw[q - 1] : 0.0;
+      if (q < L && cw > 0 && pw == 0) s_lo = q;
+      if (q < L && W > 0 && cw == W && pw < W) s_hi = q;
+    }
+    __syncthreads();
+    if (s_hi > s_lo) {
+      const unsigned long long hsh = splitmix64(p.seed ^ ((unsigned long long)level << 48) ^
+                                                ((unsigned long long)node << 20) ^ (unsigned long long)(f + f0));
+      rand_b = s_lo + 1 + (int)(hsh % (unsigned long long)(s_hi - s_lo));
+    }
+  }
+  double my_e = -1.0e300;
+  int my_code = -1;
+  for (int j = 0; j < 4; ++j) {
+    const int q = 4 * t + j;                        // threshold: sorted positions < q go left
+    if (q < 1 || q >= L || (random_mode && q != rand_b)) continue;
+    const double wb = sw[q] - sw[q - 1];
+    if (!(wb != 0.0 || random_mode)) continue;
+    const double wlo = sw[q - 1], wylo = swy[q - 1];
+    const double whi = W - wlo, wyhi = WY - wylo;
+    double ce = -1.0e300;
+    int cc = -1;
+    if (wNA == 0.0) {
+      if (wlo >= min_w && whi >= min_w) {
+        const double e = E(wlo, wylo) + E(whi, wyhi);
+        const bool ok = mono == 0 || (mono * leafv(wlo, wylo) <= mono * leafv(whi, wyhi));
+        if (ok) { ce = e; cc = q * 2 + (wlo > whi ? 1 : 0); }
+      }
+    } else {
+      if (wlo + wNA >= min_w && whi >= min_w) {
+        const double e = E(wlo + wNA, wylo + wyNA) + E(whi, wyhi);
+        const bool ok = mono == 0 || (mono * leafv(wlo + wNA, wylo + wyNA) <= mono * leafv(whi, wyhi));
+        if (ok && e > ce) { ce = e; cc = q * 2 + 1; }
+      }
+      if (wlo >= min_w && whi + wNA >= min_w) {
+        const double e = E(wlo, wylo) + E(whi + wNA, wyhi + wyNA);
+        const bool ok = mono == 0 || (mono * leafv(wlo, wylo) <= mono * leafv(whi + wNA, wyhi + wyNA));
+        if (ok && e > ce) { ce = e; cc = q * 2 + 0; }
+      }
+    }
+    if (cc >= 0 && (my_code < 0 || ce > my_e || (ce == my_e && cc < my_code))) { my_e = ce; my_code = cc; }
+  }
+  if (t == 0 && wNA >= min_w && W > 0 && !random_mode) {     // NA vs REST: the incumbent, wins ties
+    const double e = E(W, WY) + E(wNA, wyNA);
+    if (my_code < 0 || e > my_e || e == my_e) { my_e = e; my_code = 0; }
+  }
+  {
+    const int lane = t & 63, wv = t >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double e2 = __shfl_xor(my_e, o, 64);
+      const int c2 = __shfl_xor(my_code, o, 64);
+      if (c2 >= 0 && (my_code < 0 || e2 > my_e || (e2 == my_e && c2 < my_code))) { my_e = e2; my_code = c2; }
+    }
+    if (lane == 0) { gbe[wv] = my_e; gbc[wv] = my_code; }
+    __syncthreads();
+    if (t == 0) {
+      for (int k = 1; k < 4; ++k) {
+        const double e2 = gbe[k];
+        const int c2 = gbc[k];
+        if (c2 >= 0 && (gbc[0] < 0 || e2 > gbe[0] || (e2 == gbe[0] && c2 < gbc[0]))) { gbe[0] = e2; gbc[0] = c2; }
+      }
+    }
+    __syncthreads();
+  }
+  const int code = gbc[0];
+  const double be = gbe[0];
+  int bsp = 0, nal = 0;
+  if (code > 0) { bsp = code >> 1; nal = code & 1; }
+  if (code > 0) {
+    for (int j = 0; j < 4; ++j) {
+      const int q = 4 * t + j;
+      if (q >= L) continue;
+      const int cidx = gi[q];
+      const bool empty = (sw[q] - (q > 0 ? sw[q - 1] : 0.0)) == 0.0;
+      const bool left = empty ? (nal != 0) : (q < bsp);
+      if (left) atomicOr(&gbits[cidx >> 5], 1u << (cidx & 31));
+    }
+  }
+  __syncthreads();
+  if (t == 0) {
+    int valid = 0;
+    double wl = 0, wr = 0, yl = 0, yr = 0;
+    if (code == 0) { wl = W; yl = WY; wr = wNA; yr = wyNA; }
+    else if (code > 0) {
+      wl = sw[bsp - 1]; yl = swy[bsp - 1]; wr = W - wl; yr = WY - yl;
+      if (nal) { wl += wNA; yl += wyNA; } else { wr += wNA; yr += wyNA; }
+    }
+    const double Epar = E(Wall, WYall);
+    double gain = be - Epar;
+    if (code >= 0 && Wall >= 2.0 * min_w) {
+      if (p.mode == 0) {
+        const double var = wYY * Wall - WYall * WYall;
+        const double seBefore = (wNA >= min_w) ? (wYY - Epar) : ((wYY - naYY) - E(W, WY));
+        const double seAfter = wYY - be;
+        const float pl = (float)(yl / wl), pr = (float)(yr / wr);
+        valid = ((float)var != 0.f) && (seAfter < seBefore * (1.0 - p.min_split_improvement)) &&
+                (pl != pr) && wl >= min_w && wr >= min_w;
+        if (random_mode) valid = wl > 0 && wr > 0;
+      } else if (p.mode == 1) {
+        valid = (0.5 * gain - p.gamma) > 1e-6 && wl >= min_w && wr >= min_w;
+        gain = 0.5 * gain - p.gamma;
+      } else {
+        valid = wl > 0 && wr > 0;
+      }
+    }
+    unsigned pack = 0u;
+    for (int k = 0; k < gg; ++k) pack |= (unsigned)(nbins_f[f + k] - 1) << (8 * k);
+    Cand* c = cand + (size_t)node * FL + f;
+    c->expl = be; c->gain = gain; c->wl = wl; c->wr = wr;
+    c->predl = (float)leafv(wl, yl); c->predr = (float)leafv(wr, yr);
+    c->bin = (int)pack;
+    c->na_left = (code == 0) ? 0 : nal;
+    c->valid = valid;
+    c->is_cat = GROUP_CAT;
+  }
+  if (t < NBW) cand[(size_t)node * FL + f].bits[t] = code == 0 ? 0xFFFFFFFFu : gbits[t];
+}
+
 // k_split_find: best split point per (node, feature). grid = (C, F), block 256 (thread = bin).
+template <bool GRP>
 __device__ __forceinline__ void split_find_body(
     double* __restrict__ hist, int slot_doubles, const int* __restrict__ meta, int F,
     const int* __restrict__ nbins_f, const int* __restrict__ iscat_f, const int* __restrict__ mono_f,
@@ -1121,6 +1396,28 @@ __device__ __forceinline__ void split_find_body(
   } else {
     wNA = slot[iNA]; wyNA = slot[iNA + 1]; naYY = slot[iNY]; wYY = slot[iWY];
     if (t < nb && t < NA_BIN) { w = slot[iT]; wy = slot[iT + 1]; }
+  }
+  if (GRP && p.gcat) {
+    const int gg = p.gcat[f + f0];
+    if (gg < 0) {                       // a group member or padding column: the group's first column searches it
+      if (t == 0) {
+        Cand* c = cand + (size_t)node * FL + f;
+        c->valid = 0; c->expl = -1.0e300; c->is_cat = 0;
+      }
+      return;
+    }
+    if (gg > 0) {
+      HistRead hr{slot, dv.recv, nullptr, 0, dv.f32, 1, dv.recv != nullptr ? 1 : 0};
+      if (dv.recv) {
+        const Node nd = dv.nodes[node];
+        const int ps = nd.parent < 0 ? 0 : nd.parent;
+        hr.rb = (size_t)ps * dv.E;
+        hr.pv = dv.prev + (size_t)ps * slot_doubles;
+        hr.build = nd.build;
+      }
+      split_find_group(hr, node, f, gg, hs, FL, nbins_f, mono_f, p, level, f0, cand);
+      return;
+    }
   }
   sidx[t] = t;
   if (cat) {
@@ -1453,11 +1750,9 @@ __device__ __forceinline__ void split_find_body(
     c->na_left = (code == 0) ? 0 : nal;
     c->valid = valid;
     c->is_cat = cat ? 1 : 0;
-    for (int k = 0; k < 8; ++k) c->bits[k] = cat ? sbits[k] : 0u;
-    if (cat && code == 0) {  // NA vs REST on a categorical: every level left
-      for (int k = 0; k < 8; ++k) c->bits[k] = 0xFFFFFFFFu;
-    }
   }
+  // the bitset: one word per thread (NA vs REST on a categorical: every level left)
+  if (t < NBW) c->bits[t] = (cat && code == 0) ? 0xFFFFFFFFu : ((cat && t < 8) ? sbits[t] : 0u);
 }
 
 // Best feature of one node (one wave; lane = threadIdx.x & 63): k_split_reduce, and k_plan's prologue on
@@ -1511,21 +1806,20 @@ __device__ void reduce_node(const Cand* __restrict__ cand, int node, int F, cons
     const int f2 = __shfl_xor(bf, o, 64);
     if (f2 >= 0 && (bf < 0 || e2 > be || (e2 == be && f2 < bf))) { be = e2; bf = f2; }
   }
+  Dec* dn = dec + node;
   if (lane == 0) {
-    Dec d;
-    d.feat = bf;
+    dn->feat = bf;
     if (bf >= 0) {
       const Cand& c = cand_at(cand, node, bf, F, cfs, ccap);
-      d.bin = c.bin; d.na_left = c.na_left; d.is_cat = c.is_cat;
-      for (int k = 0; k < 8; ++k) d.bits[k] = c.bits[k];
-      d.gain = c.gain; d.wl = c.wl; d.wr = c.wr; d.predl = c.predl; d.predr = c.predr;
+      dn->bin = c.bin; dn->na_left = c.na_left; dn->is_cat = c.is_cat;
+      dn->gain = c.gain; dn->wl = c.wl; dn->wr = c.wr; dn->predl = c.predl; dn->predr = c.predr;
     } else {
-      d.bin = 0; d.na_left = 0; d.is_cat = 0;
-      for (int k = 0; k < 8; ++k) d.bits[k] = 0u;
-      d.gain = 0; d.wl = 0; d.wr = 0; d.predl = 0; d.predr = 0;
+      dn->bin = 0; dn->na_left = 0; dn->is_cat = 0;
+      dn->gain = 0; dn->wl = 0; dn->wr = 0; dn->predl = 0; dn->predr = 0;
     }
-    dec[node] = d;
   }
+  // the bitset: one word per lane (bf is wave-uniform after the argmax)
+  if (lane < NBW) dn->bits[lane] = bf >= 0 ? cand_at(cand, node, bf, F, cfs, ccap).bits[lane] : 0u;
 }
 
 __global__ __launch_bounds__(64) void k_split_reduce(
@@ -1737,13 +2031,14 @@ __global__ __launch_bounds__(1024) void k_plan(
             next_build_prefix, counters, scratch, depth, max_depth, min_w, cap_next, leaf_cap, pr);
 }
 
+template <bool GRP>
 __global__ __launch_bounds__(256) void k_split_find(
     double* __restrict__ hist, int slot_doubles, const int* __restrict__ meta, int F,
     const int* __restrict__ nbins_f, const int* __restrict__ iscat_f, const int* __restrict__ mono_f,
     SplitParams p, int level, Cand* __restrict__ cand, double* __restrict__ root_w,
     const float* __restrict__ edges, int adapt_nb, int f0, int FL, Derive dv) {
-  split_find_body(hist, slot_doubles, meta, F, nbins_f, iscat_f, mono_f, p, level, cand, root_w, edges, adapt_nb, f0,
-                  FL, dv);
+  split_find_body<GRP>(hist, slot_doubles, meta, F, nbins_f, iscat_f, mono_f, p, level, cand, root_w, edges, adapt_nb,
+                       f0, FL, dv);
 }
 
 // k_split_find with the level's k_plan folded into its LAST block (single process, <= PLAN_REDUCE_MAX nodes): every
@@ -1776,8 +2071,8 @@ __global__ __launch_bounds__(256) void k_split_find_plan(
     const int* __restrict__ nbins_f, const int* __restrict__ iscat_f, const int* __restrict__ mono_f,
     SplitParams p, int level, Cand* __restrict__ cand, double* __restrict__ root_w,
     const float* __restrict__ edges, int adapt_nb, int f0, int FL, Derive dv, PlanArgs pa) {
-  split_find_body(hist, slot_doubles, meta, F, nbins_f, iscat_f, mono_f, p, level, cand, root_w, edges, adapt_nb, f0,
-                  FL, dv);
+  split_find_body<false>(hist, slot_doubles, meta, F, nbins_f, iscat_f, mono_f, p, level, cand, root_w, edges,
+                         adapt_nb, f0, FL, dv);
   __shared__ int s_last;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -1900,6 +2195,27 @@ __device__ __forceinline__ int row_byte(uint4 v0, uint4 v1, int f) {
 __device__ __forceinline__ int row_byte4(uint4 v0, uint4 v1, uint4 v2, uint4 v3, int f) {
   return f < 32 ? row_byte(v0, v1, f) : row_byte(v2, v3, f - 32);
 }
+// the aligned row word holding column f (f % 4 == 0: a wide-categorical group)
+__device__ __forceinline__ unsigned row_word(uint4 v0, uint4 v1, int f) {
+  const int wi = f >> 2;
+  return wi < 4 ? pick_word(v0, wi) : pick_word(v1, wi - 4);
+}
+__device__ __forceinline__ unsigned row_word4(uint4 v0, uint4 v1, uint4 v2, uint4 v3, int f) {
+  return f < 32 ? row_word(v0, v1, f) : row_word(v2, v3, f - 32);
+}
+// a decision's row key from registers (NV > 0) or memory: the split byte, or a group split's row word
+template <int NV>
+__device__ __forceinline__ unsigned split_key(bool grp, int f, uint4 v0, uint4 v1, uint4 v2, uint4 v3,
+                                              const uint8_t* __restrict__ bins, long long row, int stride, long long N,
+                                              int planar) {
+  if (grp) {
+    if (NV > 0 && f < NV * 16) return NV > 2 ? row_word4(v0, v1, v2, v3, f) : row_word(v0, v1, f);
+    return *reinterpret_cast<const unsigned*>(bins + bin_off(row, f, stride, N, planar));
+  }
+  return (NV > 0 && f >= NV * 16) ? bins[bin_off(row, f, stride, N, planar)]
+         : NV > 2 ? (unsigned)row_byte4(v0, v1, v2, v3, f) : NV > 0 ? (unsigned)row_byte(v0, v1, f)
+                  : bins[bin_off(row, f, stride, N, planar)];
+}
 
 template <int NV>
 __device__ __forceinline__ void route_tile(
@@ -1938,6 +2254,10 @@ __device__ __forceinline__ void route_tile(
   __syncthreads();
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int featA = sA.feat;
+  // per-tile constants of the two decision levels (wide-categorical group splits read a row word)
+  const bool grpA = sA.is_cat == GROUP_CAT;
+  const int fB0 = sC[0] >= 0 ? sB[0].feat : -1, fB1 = sC[1] >= 0 ? sB[1].feat : -1;
+  const bool grpB0 = sC[0] >= 0 && sB[0].is_cat == GROUP_CAT, grpB1 = sC[1] >= 0 && sB[1].is_cat == GROUP_CAT;
   const int wbase = r0 + wid * LROWS;
   const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   int q[LU], rank[LU];
@@ -1969,16 +2289,14 @@ __device__ __forceinline__ void route_tile(
     if (fdir) {
       dA = valid && featA >= 0 ? fdir[row] : 0;
     } else if (valid && featA >= 0)
-      dA = dec_go_left(&sA, (NV > 0 && featA >= NV * 16) ? sbins[bin_off(row, featA, stride, N, planar)]
-                            : NV > 2 ? row_byte4(rv0[u], rv1[u], rv2[u], rv3[u], featA)
-                            : NV > 0 ? row_byte(rv0[u], rv1[u], featA) : sbins[bin_off(row, featA, stride, N, planar)]) ? 0 : 1;
+      dA = dec_go_left_key(&sA, split_key<NV>(grpA, featA, rv0[u], rv1[u], rv2[u], rv3[u], sbins, row, stride, N,
+                                              planar)) ? 0 : 1;
     if (valid && sC[dA] >= 0) {
       const Dec* b = &sB[dA];
-      const int fb = b->feat;
+      const int fb = dA ? fB1 : fB0;
       if (fb >= 0)
-        dB = dec_go_left(b, (NV > 0 && fb >= NV * 16) ? sbins[bin_off(row, fb, stride, N, planar)]
-                            : NV > 2 ? row_byte4(rv0[u], rv1[u], rv2[u], rv3[u], fb)
-                            : NV > 0 ? row_byte(rv0[u], rv1[u], fb) : sbins[bin_off(row, fb, stride, N, planar)]) ? 0 : 1;
+        dB = dec_go_left_key(b, split_key<NV>(dA ? grpB1 : grpB0, fb, rv0[u], rv1[u], rv2[u], rv3[u], sbins, row,
+                                              stride, N, planar)) ? 0 : 1;
     }
     q[u] = 2 * dA + dB;
     mv[u] = valid && sG[q[u]] >= 0;
@@ -2118,7 +2436,9 @@ __global__ __launch_bounds__(256) void k_row_dir(const uint8_t* __restrict__ bin
   __syncthreads();
   const int f = sd.feat;
   for (long long row = (long long)blockIdx.x * blockDim.x + threadIdx.x; row < N; row += (long long)gridDim.x * blockDim.x)
-    out[row] = (f >= 0 && !dec_go_left(&sd, bins[bin_off(row, f, stride, N, planar)])) ? 1 : 0;
+    out[row] = (f >= 0 && !dec_go_left_key(&sd, sd.is_cat == GROUP_CAT
+                                                   ? *reinterpret_cast<const unsigned*>(bins + bin_off(row, f, stride, N, planar))
+                                                   : (unsigned)bins[bin_off(row, f, stride, N, planar)])) ? 1 : 0;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2160,7 +2480,8 @@ __device__ __forceinline__ void leaf_assign_body(
       const int c = (int)lv[d].cap, b = sbase[d];
       for (int i = threadIdx.x; i < c; i += blockDim.x) {
         const Dec* dc = lv[d].dec + i;
-        st[b + i] = make_int4(dc->feat, (dc->bin & 0xFFFF) | ((dc->na_left != 0) << 16) | ((dc->is_cat != 0) << 17),
+        st[b + i] = make_int4(dc->feat, (dc->bin & 0xFFFF) | ((dc->na_left != 0) << 16) | ((dc->is_cat != 0) << 17) |
+                                            ((dc->is_cat == GROUP_CAT) << 18),
                               lv[d].cl[i], lv[d].cr[i]);
       }
     }
@@ -2191,6 +2512,9 @@ __device__ __forceinline__ void leaf_assign_body(
         const int4 e = st[sbase[d] + i];
         if (e.x < 0) {
           c = e.z;                               // terminal node: child_l == child_r == its leaf
+        } else if ((e.y >> 18) & 1) {            // wide-categorical group: the row word, the record in global
+          const Dec* dc = lv[d].dec + i;
+          c = dec_go_left_key(dc, split_key<NV>(true, e.x, v0, v1, v2, v3, bins, row, stride, N, planar)) ? e.z : e.w;
         } else {
           const int b = (NV > 0 && e.x >= NV * 16) ? bins[bin_off(row, e.x, stride, N, planar)]
                         : NV > 2 ? row_byte4(v0, v1, v2, v3, e.x) : NV > 0 ? row_byte(v0, v1, e.x)
@@ -2207,10 +2531,8 @@ __device__ __forceinline__ void leaf_assign_body(
         if (f < 0) {
           c = lv[d].cl[i];
         } else {
-          const int b = (NV > 0 && f >= NV * 16) ? bins[bin_off(row, f, stride, N, planar)]
-                        : NV > 2 ? row_byte4(v0, v1, v2, v3, f) : NV > 0 ? row_byte(v0, v1, f)
-                                 : bins[bin_off(row, f, stride, N, planar)];
-          c = dec_go_left(dc, b) ? lv[d].cl[i] : lv[d].cr[i];
+          c = dec_go_left_key(dc, split_key<NV>(dc->is_cat == GROUP_CAT, f, v0, v1, v2, v3, bins, row, stride, N,
+                                                planar)) ? lv[d].cl[i] : lv[d].cr[i];
         }
       }
       if (c < 0) { leaf = -1 - c; break; }
@@ -2830,9 +3152,14 @@ static int split_find_launch(void* hist, int slot_doubles, const void* meta, int
                              void* root_w, const void* edges, int adapt_nb, int f0, int FL, Derive dv, hipStream_t s) {
   if (F <= 0 || cap <= 0) return 0;
   if (FL < F) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_split_find, dim3(cap, F), dim3(256), 0, s, (double*)hist, slot_doubles,
-                     (const int*)meta, F, (const int*)nbins_f, (const int*)iscat_f, (const int*)mono_f, p, level,
-                     (Cand*)cand, (double*)root_w, (const float*)edges, adapt_nb, f0, FL, dv);
+  if (p.gcat)
+    hipLaunchKernelGGL(k_split_find<true>, dim3(cap, F), dim3(256), 0, s, (double*)hist, slot_doubles,
+                       (const int*)meta, F, (const int*)nbins_f, (const int*)iscat_f, (const int*)mono_f, p, level,
+                       (Cand*)cand, (double*)root_w, (const float*)edges, adapt_nb, f0, FL, dv);
+  else
+    hipLaunchKernelGGL(k_split_find<false>, dim3(cap, F), dim3(256), 0, s, (double*)hist, slot_doubles,
+                       (const int*)meta, F, (const int*)nbins_f, (const int*)iscat_f, (const int*)mono_f, p, level,
+                       (Cand*)cand, (double*)root_w, (const float*)edges, adapt_nb, f0, FL, dv);
   return (int)hipGetLastError();
 }
 
@@ -2844,7 +3171,7 @@ int h2o_split_find(const void* hist, int slot_doubles, const void* meta, int cap
   p.min_w = min_w; p.min_split_improvement = msi; p.lambda = lambda_; p.alpha = alpha; p.gamma = gamma;
   p.mode = mode; p.random_split = random_split; p.seed = seed; p.hist_type = hist_type; p.fcut = 0;
   p.vrange = nullptr; p.hprev = nullptr; p.pdec = nullptr; p.rnodes = nullptr; p.fgroup = nullptr; p.edges_all = nullptr;
-  p.range_on = 0; p.pad_r = 0;
+  p.range_on = 0; p.pad_r = 0; p.gcat = nullptr;
   return split_find_launch((void*)hist, slot_doubles, meta, cap, F, nbins_f, iscat_f, mono_f, p, level, cand, root_w,
                            edges, adapt_nb, f0, FL, Derive{nullptr, 0, 0, nullptr, nullptr}, s);
 }
@@ -3145,6 +3472,7 @@ struct TreePlan {
   // the reference's node ranges of the adaptive lattices (SplitParams.range_on / vrange): [F][2] exact column extremes
   void* vrange;
   int range_on, pad6;
+  void* gcat;                 // [F] wide-categorical groups (SplitParams.gcat), or null
 };
 
 // node-range fields of a level's split search (see SplitParams)
@@ -3157,6 +3485,7 @@ static inline void tp_node_range(const TreePlan* P, int d, const void* hprev, Sp
   p.fgroup = (const int*)P->fgroup;
   p.edges_all = (const float*)P->edges;
   p.pad_r = 0;
+  p.gcat = (const int*)P->gcat;
 }
 
 // op codes / dtypes of the collective transport
@@ -3390,7 +3719,7 @@ static int tree_grow(const TreePlan* P, int d, int dist, hipStream_t s, bool pla
 
 // one level: split search, decisions, plan, next histogram (single process and all-reduce mode)
 int h2o_tree_level(const TreePlan* P, int d, int dist, hipStream_t s) {
-  const bool fuse = !dist && !P->dist && !P->sliced && P->caps[d] <= PLAN_REDUCE_MAX && plan_fused();
+  const bool fuse = !dist && !P->dist && !P->sliced && P->caps[d] <= PLAN_REDUCE_MAX && plan_fused() && !P->gcat;
   const int rc = fuse ? tree_find_plan(P, d, s) : h2o_tree_find(P, d, s);
   if (rc) return -rc;
   return tree_grow(P, d, dist, s, fuse);

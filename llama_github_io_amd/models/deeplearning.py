@@ -309,10 +309,13 @@ class DeepLearningTrainer:
                 yt = torch.nan_to_num(y, nan=0).long()
         B = int(p["mini_batch_size"])
         if B <= 1:
-            # Hogwild single-row SGD -> GPU mini-batches of up to gpu_batch_size rows, but never fewer than
-            # ~1024 updates per epoch: ADADELTA starts from zero step sizes, so a small frame trained in a
-            # handful of large batches would barely move (the reference does one update per row)
-            B = max(1, min(int(p["gpu_batch_size"]), N_glob // 1024))
+            # H2O's default mini_batch_size = 1 is one ADADELTA step per ROW (Neurons.java:229-296). ADADELTA warms
+            # its step sizes up per STEP, so the GPU's B-row steps (one step on the batch-mean gradient) are sized
+            # to keep >= ~16K steps per epoch: B = N // 16384 in [1, gpu_batch_size]. MEASURED (fp64 oracle,
+            # scripts/dl_default_semantics.py, profiles/r6_dl_default_semantics.md): one-epoch logloss within
+            # 0-3 % of the per-row reference at 10k / 100k / 1M rows; the former rule (N // 1024 up to 256: 9 /
+            # 97 / 256-row steps) was 12 / 25 / 18 % worse. Set mini_batch_size for throughput instead.
+            B = max(1, min(int(p["gpu_batch_size"]), N_glob // 16384))
         B = max(1, min(B, N_glob))
         if dp_avg:   # local mini-batches: never larger than the smallest shard
             bt = torch.tensor([float(min(B, N))], dtype=torch.float64, device=coll.comm_device())
@@ -829,6 +832,7 @@ class DeepLearningTrainer:
                 if float(p["max_runtime_secs"] or 0) > 0 and coll.agree(time.time() - t0 > float(p["max_runtime_secs"])):
                     break
         model.output["training_step_explicit"] = bool(explicit)
+        model.output["mini_batch_rows"] = int(B)           # rows per optimizer step (see the default rule above)
         model.output["training_step_fused_mfma"] = fz.get("obj") is not None
         model.output["phase_seconds"] = dict(setup=t_loop0 - t0, train_loop=time.time() - t_loop0 - t_scoring,
                                              scoring=t_scoring)

@@ -279,6 +279,8 @@ class SharedTreeTrainer:
                                       self._split_params(), node_cap=node_cap)
         if bn.vmap is not None:
             self.builder.set_feature_groups(bn.vmap, getattr(bn, "n_low", 0), getattr(bn, "n_mid", 0))
+            if bn.cat_groups:
+                self.builder.set_cat_groups(bn.gcat())
         if p.get("interaction_constraints"):
             icm, root = interaction_map(p["interaction_constraints"], info.x)
             if bn.vmap is not None:

@@ -15,12 +15,14 @@ exact, and the uint8 engine (histograms, routing, leaf walk) runs unchanged. ``v
 the original features (split decoding, column sampling, constraints, importances).
 
 Wide categoricals (``nbins_cats`` up to 1016 levels kept apart, H2O default 1024, ``SharedTreeModel.java:72``):
-a categorical with L > 254 bins spans n = ceil(L / 254) adjacent engine columns; column k holds the levels of
-bins [254k, 254k + L_k) as bins 0..L_k-1 and every other level in one "elsewhere" bin L_k (NA stays bin 255).
-No level is folded. Each column's subset split (bins sorted by mean response, DTree.java) treats the other
-blocks' levels as one unit, so the split family is the union of the per-block families — a subset of H2O's
-single sort over all L levels; the histograms and routing stay exact byte-bin operations. Decoding maps
-the column's bitset back through ``level_to_bin`` to a bitset over all L original levels.
+a categorical with L > 254 bins spans n = ceil(L / 254) engine columns; column k holds the levels of bins
+[254k, 254k + L_k) as bins 0..L_k-1 and every other level in one "elsewhere" bin L_k (NA stays bin 255). No
+level is folded. The n columns form a GROUP at a 4-aligned engine position, padded to 4 with constant columns
+(``cat_groups``, ``pad``), so a row's group bytes are one aligned 32-bit word of its bins: the split search
+merges the group's histograms into one histogram over all L levels and sorts ALL of them by mean response
+(H2O's single sort, DTree.java:1004-1013), and the group decision (a bitset over the L bins) routes a row from
+that word (the one column whose byte is not 'elsewhere' names the row's level). The byte histograms stay
+exact. Decoding maps the bitset back through ``level_to_bin`` to a bitset over the original levels.
 """
 from __future__ import annotations
 
@@ -49,6 +51,8 @@ class Binning:
     vmap: np.ndarray | None = None  # int32 [F] engine column -> original feature (None: identity)
     n_low: int = 0                  # engine columns [0, n_low) = every feature's first column (narrow view), 0: none
     n_mid: int = 0                  # [0, n_mid): + the subsets halving the edge spacing (512-bin levels), 0: none
+    cat_groups: list = field(default_factory=list)   # wide categoricals: (first engine column, real columns)
+    pad: np.ndarray | None = None   # bool [F]: constant padding column of a wide-categorical group (bin 0)
 
     # every per-feature field above is per ENGINE column (F of them); see the module note on wide bins
     @property
@@ -71,7 +75,8 @@ class Binning:
                     nbins=self.nbins.tolist(), iscat=self.iscat.tolist(), nlevels=self.nlevels.tolist(),
                     level_to_bin=[None if m is None else m.tolist() for m in self.level_to_bin],
                     vmap=None if self.vmap is None else self.vmap.tolist(), n_low=int(self.n_low),
-                    n_mid=int(self.n_mid))
+                    n_mid=int(self.n_mid), cat_groups=[list(map(int, g)) for g in self.cat_groups],
+                    pad=None if self.pad is None else self.pad.astype(int).tolist())
 
     @staticmethod
     def from_state(s):
@@ -80,7 +85,20 @@ class Binning:
                        np.asarray(s["nlevels"], dtype=np.int32),
                        [None if m is None else np.asarray(m, dtype=np.int64) for m in s["level_to_bin"]],
                        None if s.get("vmap") is None else np.asarray(s["vmap"], dtype=np.int32),
-                       int(s.get("n_low", 0)), int(s.get("n_mid", 0)))
+                       int(s.get("n_low", 0)), int(s.get("n_mid", 0)),
+                       [tuple(g) for g in s.get("cat_groups", [])],
+                       None if s.get("pad") is None else np.asarray(s["pad"], dtype=bool))
+
+    def gcat(self) -> np.ndarray | None:
+        """int32 [F] for the engine: a wide-categorical group's first column = its number of real columns (1..4),
+        its other columns (real and padding) = -1, every other column 0; None without groups."""
+        if not self.cat_groups:
+            return None
+        g = np.zeros(self.F, dtype=np.int32)
+        for c0, n in self.cat_groups:
+            g[c0] = n
+            g[c0 + 1:c0 + 4] = -1
+        return g
 
 
 def sample_rows(X: torch.Tensor, sample: int, seed: int, row0: int = 0, n_glob: int | None = None) -> torch.Tensor:
@@ -220,19 +238,23 @@ def fit_binning(X: torch.Tensor, iscat, nlevels=None, max_bins: int = MAX_DATA_B
         # H2O_HIST_FINE=1 keeps the former layout instead: the features of exactly 4 interleaved columns first,
         # each filling one aligned 4-byte row word (one fine-bin atomic per row and feature in the histogram kernel).
         fine_layout = os.environ.get("H2O_HIST_FINE") == "1"
-        quad, rest, low, mid, high = [], [], [], [], []
+        quad, rest, low, mid, high, groups = [], [], [], [], [], []
         for f in range(F):
             e = edges[f]
             if wide_cat[f]:
+                # a group of n real columns padded to 4 (the group's bytes are one aligned row word)
                 nb = int(nbins[f])
                 lb = np.arange(nlevels[f], dtype=np.int64) if l2b[f] is None else l2b[f]
                 n = -(-nb // SUB_EDGES)
-                for k in range(n):
-                    b0, nk = k * SUB_EDGES, min(SUB_EDGES, nb - k * SUB_EDGES)
-                    inb = (lb >= b0) & (lb < b0 + nk)
-                    c = (f, None, nk + 1, np.where(inb, lb - b0, nk))
-                    rest.append(c)
-                    low.append(c)
+                g = []
+                for k in range(4):
+                    if k < n:
+                        b0, nk = k * SUB_EDGES, min(SUB_EDGES, nb - k * SUB_EDGES)
+                        inb = (lb >= b0) & (lb < b0 + nk)
+                        g.append((f, None, nk + 1, np.where(inb, lb - b0, nk), False))
+                    else:
+                        g.append((f, None, 1, np.zeros(max(int(nlevels[f]), 1), dtype=np.int64), True))
+                groups.append((g, n))
                 continue
             n = 1 if e is None or e.size <= SUB_EDGES else -(-e.size // SUB_EDGES)
             for k in range(n):
@@ -240,12 +262,18 @@ def fit_binning(X: torch.Tensor, iscat, nlevels=None, max_bins: int = MAX_DATA_B
                 c = (f, ek, (ek.size + 1) if e is not None else nbins[f], l2b[f])
                 (quad if n == 4 else rest).append(c)
                 (low if k == 0 else high if (n == 4 and k % 2) else mid).append(c)
+        gcols = [c for g, _ in groups for c in g]
+        cat_groups = []
+        for i, (_, n) in enumerate(groups):
+            cat_groups.append((4 * i, n))
         if fine_layout:
-            cols = quad + rest
+            cols = gcols + quad + rest
         else:
-            cols = low + mid + high
-            n_low = len(low) if (mid or high) else 0
-            n_mid = len(low) + len(mid) if high else 0
+            cols = gcols + low + mid + high
+            n_low = len(gcols) + len(low) if (mid or high) else 0
+            n_mid = len(gcols) + len(low) + len(mid) if high else 0
+        pad = np.asarray([len(c) > 4 and c[4] for c in cols], dtype=bool)
+        cols = [c[:4] for c in cols]
         vmap = np.asarray([c[0] for c in cols], dtype=np.int32)
         edges = [c[1] for c in cols]
         nbins = np.asarray([c[2] for c in cols], dtype=np.int32)
@@ -257,7 +285,10 @@ def fit_binning(X: torch.Tensor, iscat, nlevels=None, max_bins: int = MAX_DATA_B
     # > 32 features: whole 32-byte planes (the device engine stores such bins PLANAR, one plane per
     # histogram feature tile — apply_binning(planar=True))
     stride = (F + 3) // 4 * 4 if F <= 12 else ((F + 15) // 16 * 16 if F <= 32 else (F + 31) // 32 * 32)
-    return Binning(F, stride, edges, nbins, iscat, nlevels, l2b, vmap, n_low, n_mid)
+    if vmap is None:
+        cat_groups, pad = [], None
+    return Binning(F, stride, edges, nbins, iscat, nlevels, l2b, vmap, n_low, n_mid, cat_groups,
+                   pad if pad is not None and pad.any() else None)
 
 
 def _edge_table(b: Binning, device):
@@ -287,11 +318,14 @@ def apply_binning(b: Binning, X: torch.Tensor, planar: bool = False) -> torch.Te
         Xc = torch.empty(F + len(maps), N, dtype=torch.float32, device=X.device)
         Xc[:F] = X
         for i, (f, m) in enumerate(maps):
+            src[f] = F + i
+            if b.pad is not None and b.pad[f]:       # group padding: bin 0 on every row (NA included)
+                Xc[F + i] = 0.0
+                continue
             col = X[b.orig(f)]
             mt = torch.as_tensor(m, device=X.device, dtype=torch.float32)
             codes = torch.nan_to_num(col, nan=0.0).long().clamp(0, m.size - 1)
             Xc[F + i] = torch.where(torch.isnan(col), col, mt[codes])
-            src[f] = F + i
     else:
         Xc = X.contiguous().float()
     if X.is_cuda:

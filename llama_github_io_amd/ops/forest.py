@@ -96,10 +96,26 @@ def levels_to_tree(tl: TreeLevels, binning, leaf_values=None) -> Tree:
             if cz[i]:
                 nl = int(binning.nlevels[f])
                 bits_b = decs["bits"][i]
-                m = binning.level_to_bin[f] if binning.level_to_bin else None
                 lv = np.arange(nl)
-                bl = lv if m is None else m[lv]
-                inleft = ((bits_b[bl >> 5] >> (bl & 31).astype(np.uint32)) & 1).astype(bool)
+                if cz[i] == 2:
+                    # wide-categorical group split: the bitset is over the group's global bins 254k + b (level_to_bin
+                    # of real column k names the levels it holds; the others' bytes say 'elsewhere' = nbins - 1)
+                    bl = np.full(nl, -1, dtype=np.int64)
+                    for k in range(4):
+                        if f + k >= binning.F or binning.orig(f + k) != binning.orig(f) or \
+                                (binning.pad is not None and binning.pad[f + k]):
+                            break
+                        mk = np.asarray(binning.level_to_bin[f + k], dtype=np.int64)
+                        hold = mk[lv] < int(binning.nbins[f + k]) - 1
+                        bl[hold] = 254 * k + mk[lv][hold]
+                    inleft = np.zeros(nl, dtype=bool)
+                    ok = bl >= 0
+                    inleft[ok] = ((bits_b[bl[ok] >> 5] >> (bl[ok] & 31).astype(np.uint32)) & 1).astype(bool)
+                    iscat[g] = 1
+                else:
+                    m = binning.level_to_bin[f] if binning.level_to_bin else None
+                    bl = lv if m is None else m[lv]
+                    inleft = ((bits_b[bl >> 5] >> (bl & 31).astype(np.uint32)) & 1).astype(bool)
                 words = np.zeros((nl + 31) // 32, dtype=np.uint32)
                 lvl = np.nonzero(inleft)[0]
                 np.bitwise_or.at(words, lvl >> 5, (np.uint32(1) << (lvl & 31).astype(np.uint32)))

@@ -34,9 +34,11 @@ AMAX_SHARDS = 64   # per-block |aux| maxima shards (csrc: AMAX_SHARDS)
 
 NODE_DT = np.dtype([("start", "<i4"), ("len", "<i4"), ("build", "<i4"), ("parent", "<i4"), ("sib", "<i4"),
                     ("dir", "<i4"), ("p1", "<i4"), ("p2", "<i4")])
-DEC_DT = np.dtype([("feat", "<i4"), ("bin", "<i4"), ("na_left", "<i4"), ("is_cat", "<i4"), ("bits", "<u4", (8,)),
+NBW = 32            # 32-bit words of a decision bitset: 1024 bins (a wide-categorical group's levels)
+DEC_DT = np.dtype([("feat", "<i4"), ("bin", "<i4"), ("na_left", "<i4"), ("is_cat", "<i4"), ("bits", "<u4", (NBW,)),
                    ("gain", "<f8"), ("wl", "<f8"), ("wr", "<f8"), ("predl", "<f4"), ("predr", "<f4")])
-CAND_BYTES = 88
+CAND_BYTES = 184
+GROUP_CAT = 2       # Dec.is_cat of a wide-categorical group split: bin = the group's packed 'elsewhere' bytes
 MODE_SE, MODE_NEWTON, MODE_RANDOM = 0, 1, 2
 # histogram types as candidate lattices over the global bins (k_split_find HT_*)
 HT_QUANTILES, HT_UNIFORM, HT_RANDOM, HT_ROBUST, HT_ROUND_ROBIN = 0, 1, 2, 3, 4
@@ -259,27 +261,52 @@ def _lattice(p: SplitParams, level, node, f, nb, w, sw, W, seed, off, vr=None):
     return mark[1:nb]
 
 
+def group_pack(nbins_f, f, n) -> int:
+    """Dec.bin of a group split: byte k = the 'elsewhere' bin of the group's k-th real column (0: padding)."""
+    v = sum(int(nbins_f[f + k] - 1) << (8 * k) for k in range(n))
+    return v - (1 << 32) if v >= 1 << 31 else v          # as the int32 the record holds
+
+
+def _invalid_cand():
+    return dict(expl=-1.0e300, gain=0.0, wl=0.0, wr=0.0, bin=0, na_left=0, valid=False, is_cat=0,
+                bits=np.zeros(NBW, dtype=np.uint32), predl=0.0, predr=0.0)
+
+
 def split_find_ref(h, nayy, wyy, nbins_f, iscat_f, mono_f, p: SplitParams, level: int, node: int, seed: int,
-                   vranges=None):
+                   vranges=None, gcat=None):
     """h: float64 [F, 256, 2]. Returns list of per-feature candidate dicts. ``vranges``: [F, 2] value ranges of
-    the node (reference node ranges, :meth:`RefTreeBuilder.build`) or None."""
+    the node (reference node ranges, :meth:`RefTreeBuilder.build`) or None. ``gcat`` (Binning.gcat): a
+    wide-categorical group's first column searches ONE histogram over all the group's levels (global bin 254k + b
+    of real column k), its other columns offer nothing."""
     F = h.shape[0]
     out = []
     for f in range(F):
+        grp = 0 if gcat is None else int(gcat[f])
+        if grp < 0:
+            out.append(_invalid_cand())
+            continue
         nb = int(nbins_f[f])
         cat = bool(iscat_f[f])
         mono = int(mono_f[f]) if mono_f is not None else 0
-        w = np.zeros(256); wy = np.zeros(256)
-        lim = min(nb, NA_BIN)
-        w[:lim] = h[f, :lim, 0]; wy[:lim] = h[f, :lim, 1]
+        M = 256 if grp == 0 else 1024
+        w = np.zeros(M); wy = np.zeros(M)
+        if grp == 0:
+            lim = min(nb, NA_BIN)
+            w[:lim] = h[f, :lim, 0]; wy[:lim] = h[f, :lim, 1]
+        else:                          # the group's levels, 'elsewhere' bins dropped
+            for k in range(grp):
+                nk = int(nbins_f[f + k]) - 1
+                w[254 * k:254 * k + nk] = h[f + k, :nk, 0]; wy[254 * k:254 * k + nk] = h[f + k, :nk, 1]
+                nb = 254 * k + nk
+            cat = True
         wNA, wyNA = h[f, NA_BIN, 0], h[f, NA_BIN, 1]
-        idx = np.arange(256)
+        idx = np.arange(M)
         if cat:
             key = np.where(idx < nb, np.where(w > 0, wy / np.where(w > 0, w, 1), -1.0e308), 1.0e308)
             idx = np.lexsort((idx, key))  # sort by key then index
             w = w[idx]; wy = wy[idx]
         sw = np.cumsum(w); swy = np.cumsum(wy)
-        W, WY = sw[255], swy[255]
+        W, WY = sw[M - 1], swy[M - 1]
         Wall, WYall = W + wNA, WY + wyNA
         random_mode = p.random_split
         rand_b = -1
@@ -359,7 +386,7 @@ def split_find_ref(h, nayy, wyy, nbins_f, iscat_f, mono_f, p: SplitParams, level
             if best_code < 0 or e > best_e or (e == best_e and c < best_code):
                 best_e, best_code = e, c
         b, nal = (best_code >> 1, best_code & 1) if best_code > 0 else (0, 0)
-        bits = np.zeros(8, dtype=np.uint32)
+        bits = np.zeros(NBW, dtype=np.uint32)
         if cat and best_code > 0:
             for t in range(nb):
                 cidx = idx[t]
@@ -397,9 +424,12 @@ def split_find_ref(h, nayy, wyy, nbins_f, iscat_f, mono_f, p: SplitParams, level
                 valid = wl > 0 and wr > 0
         if cat and best_code == 0:
             bits[:] = 0xFFFFFFFF
-        out.append(dict(expl=best_e, gain=gain, wl=wl, wr=wr, bin=NA_BIN if best_code == 0 else b,
-                        na_left=0 if best_code == 0 else nal, valid=bool(valid), is_cat=int(cat), bits=bits,
-                        predl=_leafv(p.mode, p, wl, yl), predr=_leafv(p.mode, p, wr, yr)))
+        cbin = NA_BIN if best_code == 0 else b
+        if grp > 0:
+            cbin = group_pack(nbins_f, f, grp)
+        out.append(dict(expl=best_e, gain=gain, wl=wl, wr=wr, bin=cbin,
+                        na_left=0 if best_code == 0 else nal, valid=bool(valid), is_cat=GROUP_CAT if grp else int(cat),
+                        bits=bits, predl=_leafv(p.mode, p, wl, yl), predr=_leafv(p.mode, p, wr, yr)))
     return out
 
 
@@ -445,9 +475,30 @@ def _level_k(k_cols, d: int) -> int:
     return int(k_cols)
 
 
+def group_level_np(pack: int, b4: np.ndarray) -> np.ndarray:
+    """Global bin (254k + byte) of every row of a wide-categorical group from its 4 group bytes [n, 4]; -1 = NA."""
+    b4 = np.asarray(b4, dtype=np.int64)
+    lvl = np.full(b4.shape[0], -1, dtype=np.int64)
+    na = b4[:, 0] == NA_BIN
+    for k in range(4):
+        ek = ((int(pack) & 0xFFFFFFFF) >> (8 * k)) & 255
+        if ek == 0:
+            continue
+        hit = (lvl < 0) & ~na & (b4[:, k] != ek)
+        lvl[hit] = 254 * k + b4[hit, k]
+    return lvl
+
+
 def dec_go_left_np(d, b: np.ndarray) -> np.ndarray:
+    """``b``: the split column's bins [n] — or, for a group split (is_cat == GROUP_CAT), the group's 4 bytes [n, 4]."""
     if d["feat"] < 0:
-        return np.ones_like(b, dtype=bool)
+        return np.ones(b.shape[0], dtype=bool)
+    if int(d["is_cat"]) == GROUP_CAT:
+        lvl = group_level_np(int(d["bin"]), b)
+        bits = d["bits"]
+        lc = np.maximum(lvl, 0)
+        gl = ((bits[lc >> 5] >> (lc & 31).astype(np.uint32)) & 1).astype(bool)
+        return np.where(lvl < 0, bool(d["na_left"]), gl)
     na = b == NA_BIN
     if d["is_cat"]:
         bits = d["bits"]
@@ -474,6 +525,7 @@ class RefTreeBuilder:
         self.N = self.bins.shape[0]
         self.ic_map = None
         self.n_low = self.n_mid = 0
+        self.gcat = None
 
     def set_interaction_constraints(self, ic_map, root_ok):
         """``ic_map`` [F, F] (row f: features allowed to interact with f), ``root_ok`` [F]."""
@@ -485,6 +537,16 @@ class RefTreeBuilder:
         draws original features. ``n_low`` / ``n_mid``: leading columns of the narrow views (:func:`narrow_cut`)."""
         self.fgroup = None if fgroup is None else np.asarray(fgroup, dtype=np.int64)
         self.n_low, self.n_mid = int(n_low), int(n_mid)
+
+    def set_cat_groups(self, gcat):
+        """Wide-categorical groups (Binning.gcat): one search over all of a group's levels (H2O's single sort)."""
+        self.gcat = None if gcat is None else np.asarray(gcat, dtype=np.int32)
+
+    def _split_bytes(self, d, rows):
+        f = int(d["feat"])
+        if int(d["is_cat"]) == GROUP_CAT:
+            return self.bins[rows, f:f + 4].astype(np.int64)
+        return self.bins[rows, f].astype(np.int64)
 
     def _hist(self, rows, aux):
         F = self.F
@@ -576,7 +638,8 @@ class RefTreeBuilder:
                 if ranges:
                     level_occ.append(self._occupied(h))
                     vr = level_vr[i] if level_vr[i] is not None else self._value_ranges(level_occ[i])
-                cands = split_find_ref(h, nayy, wyy, self.nbins_f, self.iscat_f, self.mono_f, p, d, i, seed, vr)
+                cands = split_find_ref(h, nayy, wyy, self.nbins_f, self.iscat_f, self.mono_f, p, d, i, seed, vr,
+                                       self.gcat)
                 fc = level_fcut(cut, self.n_low, self.n_mid, d)
                 if fc:                          # narrow level: the columns past fc are not searched
                     for f in range(fc, F):
@@ -594,7 +657,7 @@ class RefTreeBuilder:
                     leaf_of_row[rows] = lid
                     leafsum.append((aux[rows, 2].astype(np.float64).sum(), aux[rows, 3].astype(np.float64).sum()))
                     continue
-                gl = dec_go_left_np(dd, self.bins[rows, dd["feat"]].astype(np.int64))
+                gl = dec_go_left_np(dd, self._split_bytes(dd, rows))
                 lrows, rrows = rows[gl], rows[~gl]
                 for side, crow, wside, arr in ((0, lrows, dd["wl"], cl), (1, rrows, dd["wr"], cr)):
                     active = d + 1 < D and wside >= 2.0 * p.min_w and act < cap_next
@@ -670,7 +733,7 @@ class _TreePlan(ctypes.Structure):
                 [("fine_f", _vp)] + [(n, _ci) for n in ("lo_F", "lo_from", "mid_F", "mid_from")] + [("lvl2", _vp), ("fdir", _vp)] +
                 [("num_plane", _ci), ("pad4", _ci)] +
                 [(n, _vp) for n in ("fine16", "f16col", "f16n")] + [("f16_planes", _ci), ("pad5", _ci)] +
-                [("vrange", _vp), ("range_on", _ci), ("pad6", _ci)])
+                [("vrange", _vp), ("range_on", _ci), ("pad6", _ci)] + [("gcat", _vp)])
 
 
 class _Arena:
@@ -915,6 +978,16 @@ class GpuTreeBuilder:
             self._set_plan_narrow(self._plan)
             self._set_plan_fine16(self._plan)
 
+    def set_cat_groups(self, gcat):
+        """Wide-categorical groups (Binning.gcat, see RefTreeBuilder.set_cat_groups): k_split_find's group path."""
+        if gcat is not None and self.sliced:
+            raise ValueError("wide-categorical groups need the all-reduce histogram exchange (H2O_TREE_COMM=ar): a "
+                             "feature slice could cut a group")
+        self.gcat_np = None if gcat is None else np.asarray(gcat, dtype=np.int32)
+        self.gcat = None if gcat is None else torch.as_tensor(self.gcat_np, device=self.dev).contiguous()
+        if getattr(self, "_plan", None) is not None:
+            self._plan.gcat = 0 if self.gcat is None else self.gcat.data_ptr()
+
     def _set_plan_narrow(self, P):
         mid, lo = narrow_cut(self.p, self.n_low, self.n_mid, self.F)
         P.lo_F, P.lo_from = (self.n_low, lo) if lo >= 0 else (0, 0)
@@ -1036,6 +1109,8 @@ class GpuTreeBuilder:
         self._set_plan_ic(P)
         fg = getattr(self, "fgroup", None)
         P.fgroup = 0 if fg is None else fg.data_ptr()
+        gc = getattr(self, "gcat", None)
+        P.gcat = 0 if gc is None else gc.data_ptr()
         P.fine_f = 0 if self.fine_f is None else self.fine_f.data_ptr()     # used only under H2O_HIST_FINE=1
         self._set_plan_narrow(P)
         self._set_plan_fine16(P)

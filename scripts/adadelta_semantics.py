@@ -77,7 +77,19 @@ def train(mode, X, y, H, B, epochs, rho=0.99, eps=1e-8, seed=1):
         else:
             for s in range(0, n - B + 1, B):
                 idx = perm[s:s + B]
-                if mode == "batch_mean":
+                if mode.startswith("batch_scaled"):
+                    # linear-scaling rule on ADADELTA: one step on the batch-mean gradient, displacement times
+                    # B ("batch_scaled") or sqrt(B) ("batch_scaled_sqrt")
+                    mult = B if mode == "batch_scaled" else math.sqrt(B)
+                    loss = torch.nn.functional.cross_entropy(fwd(ps, X[idx]), y[idx])
+                    gr = torch.autograd.grad(loss, ps)
+                    with torch.no_grad():
+                        for p, gg, e, d in zip(ps, gr, Eg, Ed):
+                            e.mul_(rho).add_((1 - rho) * gg * gg)
+                            rate = torch.sqrt((d + eps) / (e + eps))
+                            d.mul_(rho).add_((1 - rho) * rate * rate * gg * gg)
+                            p.sub_(mult * rate * gg)
+                elif mode == "batch_mean":
                     loss = torch.nn.functional.cross_entropy(fwd(ps, X[idx]), y[idx])
                     gr = torch.autograd.grad(loss, ps)
                     with torch.no_grad():

@@ -238,3 +238,36 @@ def test_gpu_partial_f32_default_at_100m_rows(monkeypatch):
         torch.cuda.empty_cache()
     (tl64, l64), (tl32, l32) = out
     _assert_same_tree_up_to_ties(tl64, tl32, l64, l32, vectorized=True)
+
+
+def test_wide_categorical_group_on_rccl_matches_reference(force_env):
+    """A 1000-level categorical group split through the row-sharded driver on a 1-rank RCCL communicator: the leader
+    column's block derives the group's histograms from the exchanged build slots (Derive) and decides exactly as
+    RefTreeBuilder's single sort over all levels."""
+    from test_tree_engine import _wide_cat_data
+    X, y, info = _wide_cat_data()
+    b = fit_binning(X, info.iscat, info.nlevels, max_cat_bins=1024)
+    bins = apply_binning(b, X)
+    g = y - 0.5
+    aux = torch.stack([torch.ones_like(y), g, g, torch.ones_like(y)], 1).contiguous()
+    p = T.SplitParams(min_w=10)
+    ref = T.RefTreeBuilder(bins, b.F, b.nbins, b.iscat, None, 5, p)
+    ref.set_feature_groups(b.vmap)
+    ref.set_cat_groups(b.gcat())
+    ref.build(aux, leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1]).float())
+    tl_r = ref.pop_levels()[0]
+    force_env("ar", "f64")
+    dev = torch.device("cuda", 0)
+    gb = T.GpuTreeBuilder(apply_binning(b, X.to(dev)), b.F, b.nbins, b.iscat, None, 5, p)
+    gb.set_feature_groups(b.vmap)
+    gb.set_cat_groups(b.gcat())
+    assert gb.dist_mode
+    gb.build(aux.to(dev), leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1]).float())
+    tl_g = gb.pop_levels()[0]
+    assert tl_g.n_leaves == tl_r.n_leaves
+    assert sum(int(c) == T.GROUP_CAT for d in tl_r.decs for c in d["is_cat"]) >= 2
+    for dr, dg in zip(tl_r.decs, tl_g.decs):
+        assert np.array_equal(dr["feat"], dg["feat"]) and np.array_equal(dr["bin"], dg["bin"])
+        assert np.array_equal(dr["bits"], dg["bits"])
+        np.testing.assert_allclose(dr["wl"], dg["wl"], rtol=1e-6)
+    assert torch.equal(ref.leaf_of_row, gb.leaf_of_row.cpu())

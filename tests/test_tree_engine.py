@@ -608,7 +608,7 @@ def test_wide_bins_split_resolution_and_grouped_sampling():
     for seed in range(40):
         allowed = []
         for f in range(6):
-            c = [dict(valid=(i == f), expl=1.0, bin=1, na_left=0, is_cat=0, bits=np.zeros(8, np.uint32), gain=1.0,
+            c = [dict(valid=(i == f), expl=1.0, bin=1, na_left=0, is_cat=0, bits=np.zeros(T.NBW, np.uint32), gain=1.0,
                       wl=1.0, wr=1.0, predl=0.0, predr=0.0) for i in range(6)]
             allowed.append(T.split_reduce_ref(c, np.ones(6), 1, seed, 0, 0, None, fgroup)["feat"] == f)
         assert sum(allowed) in (1, 4) and (sum(allowed) == 1) == (not allowed[0])
@@ -619,7 +619,7 @@ def test_wide_bins_split_resolution_and_grouped_sampling():
     for seed in range(40):
         allowed = []
         for f in range(6):
-            c = [dict(valid=(i == f), expl=1.0, bin=1, na_left=0, is_cat=0, bits=np.zeros(8, np.uint32), gain=1.0,
+            c = [dict(valid=(i == f), expl=1.0, bin=1, na_left=0, is_cat=0, bits=np.zeros(T.NBW, np.uint32), gain=1.0,
                       wl=1.0, wr=1.0, predl=0.0, predr=0.0) for i in range(6)]
             allowed.append(T.split_reduce_ref(c, np.ones(6), 1, seed, 0, 0, None, fgroup)["feat"] == f)
         assert len({allowed[0], allowed[3], allowed[4], allowed[5]}) == 1 and sum(allowed) in (1, 4)
@@ -763,21 +763,23 @@ def _wide_cat_data(N=30000, L=1000, seed=3, device="cpu"):
 
 def test_wide_categorical_binning_keeps_every_level():
     """nbins_cats = 1024 (SharedTreeModel.java:72): a 1000-level categorical is not folded; it spans 4 engine
-    columns of 254 consecutive levels, each with one 'elsewhere' bin for the other blocks' levels."""
+    columns of 254 consecutive levels, each with one 'elsewhere' bin for the other blocks' levels, grouped at a
+    4-aligned engine position (one row word)."""
     X, y, info = _wide_cat_data()
     b = fit_binning(X, info.iscat, info.nlevels, max_cat_bins=1024)
-    assert list(b.vmap) == [0, 1, 2, 2, 2, 2, 3]
-    assert [int(b.nbins[j]) for j in range(2, 6)] == [255, 255, 255, 239]
+    assert list(b.vmap) == [2, 2, 2, 2, 0, 1, 3] and b.cat_groups == [(0, 4)] and b.pad is None
+    assert [int(b.nbins[j]) for j in range(0, 4)] == [255, 255, 255, 239]
+    assert list(b.gcat()) == [4, -1, -1, -1, 0, 0, 0]
     bins = apply_binning(b, X).long()
     lv = torch.nan_to_num(X[2], nan=-1).long()
-    for k, j in enumerate(range(2, 6)):
+    for k, j in enumerate(range(0, 4)):
         nk = int(b.nbins[j]) - 1
         inb = (lv >= 254 * k) & (lv < 254 * k + nk)
         exp = torch.where(inb, lv - 254 * k, torch.full_like(lv, nk))
         exp = torch.where(lv < 0, torch.full_like(lv, T.NA_BIN), exp)
         assert torch.equal(bins[:, j], exp)
     # every level keeps its own bin: exactly one column holds a row's level, the others say 'elsewhere'
-    own = sum(((bins[:, j] < int(b.nbins[j]) - 1)).long() for j in range(2, 6))
+    own = sum(((bins[:, j] < int(b.nbins[j]) - 1)).long() for j in range(0, 4))
     assert torch.equal(own, (lv >= 0).long())
     # more levels than nbins_cats: the most frequent nbins_cats - 1 levels keep their bins (fold the rest)
     bf = fit_binning(X, info.iscat, info.nlevels, max_cat_bins=300)
@@ -797,36 +799,104 @@ def test_wide_categorical_gbm_decodes_to_level_sets():
     auc = m.output["training_metrics"]["AUC"]
     P = m.score_tensor(X)
     assert P.shape == (X.shape[1], 2) and auc > 0.7
-    # level 2 (block 0) and level 2 + 7 * 40 = 282 (block 1) share the signal: the first wide-categorical
-    # split sends them the same way
+    # the levels sharing the signal (l % 7 == 2) go one way, across ALL blocks (one sort over the 1000 levels)
     t, i = cat_nodes[0]
     bits = np.asarray(t.cat_bits[i])
     side = lambda l: (bits[l >> 5] >> (l & 31)) & 1
-    same = [side(l) == side(2) for l in (9, 16, 23) if l < 254]
-    assert all(same)
+    assert all(side(l) == side(2) for l in (9, 16, 23, 282, 513, 772, 996))
+
+
+def _h2o_cat_split(codes, g, L, min_rows):
+    """H2O's categorical split at one node (DTree.java:1004-1013): sort ALL levels by mean response (empty levels
+    first), one scan over the sorted order, best squared-error reduction. Returns the left level set."""
+    w = np.bincount(codes, minlength=L).astype(np.float64)
+    wy = np.bincount(codes, weights=g, minlength=L)
+    key = np.where(w > 0, wy / np.where(w > 0, w, 1), -1e308)
+    order = np.lexsort((np.arange(L), key))
+    sw, swy = np.cumsum(w[order]), np.cumsum(wy[order])
+    W, WY = sw[-1], swy[-1]
+    best, bt = -np.inf, -1
+    for t in range(1, L):
+        wl, yl = sw[t - 1], swy[t - 1]
+        wr, yr = W - wl, WY - yl
+        if w[order[t]] == 0 or wl < min_rows or wr < min_rows:
+            continue
+        e = yl * yl / wl + yr * yr / wr
+        if e > best:
+            best, bt = e, t
+    return {int(l) for l in order[:bt] if w[l] > 0}
+
+
+@pytest.mark.parametrize("L", [300, 1000])
+def test_wide_categorical_split_is_h2o_single_sort(L):
+    """The root split of a 300- / 1000-level categorical (2 real columns + 2 padding / 4 real columns) is H2O's
+    single sort over all levels: the same left level set as the direct implementation of the reference rule, and
+    the decision routes every row to that side."""
+    g_ = torch.Generator().manual_seed(7)
+    N = 40000
+    lv = torch.randint(0, L, (N,), generator=g_)
+    X = torch.stack([torch.randn(N, generator=g_) * 0.01, lv.float()])
+    eff = torch.sin(lv.float() * 0.37) + (lv % 11 == 3).float()
+    y = (torch.rand(N, generator=g_) < torch.sigmoid(2 * eff)).float()
+    iscat = np.array([0, 1], np.int32)
+    info = DataInfo(["a", "c"], iscat, [None, [f"L{i}" for i in range(L)]], "y", ["0", "1"])
+    b = fit_binning(X, info.iscat, info.nlevels, max_cat_bins=1024)
+    n = -(-L // 254)
+    assert b.cat_groups == [(0, n)] and (b.pad is None) == (n == 4)
+    bins = apply_binning(b, X)
+    gr = (y - y.mean()).double()
+    aux = torch.stack([torch.ones_like(y), gr.float(), gr.float(), torch.ones_like(y)], 1).contiguous()
+    ref = T.RefTreeBuilder(bins, b.F, b.nbins, b.iscat, None, 1, T.SplitParams(min_w=10))
+    ref.set_feature_groups(b.vmap)
+    ref.set_cat_groups(b.gcat())
+    ref.build(aux, None, 0, seed=1)
+    d = ref.pop_levels()[0].decs[0][0]
+    assert int(d["feat"]) == 0 and int(d["is_cat"]) == T.GROUP_CAT
+    want = _h2o_cat_split(lv.numpy(), aux[:, 1].double().numpy(), L, 10)
+    # global bin = level here (no folding): bit l of the decision
+    got = {l for l in range(L) if (int(d["bits"][l >> 5]) >> (l & 31)) & 1 and (lv == l).any()}
+    assert got == want
+    left = ref.leaf_of_row.numpy() == 0
+    assert np.array_equal(left, np.isin(lv.numpy(), sorted(want)))
 
 
 @pytest.mark.gpu
-def test_gpu_wide_categorical_matches_reference():
-    """1000-level categorical (4 engine columns) on the GPU engine vs RefTreeBuilder: identical decisions
-    (categorical bitsets included), left weights and leaf assignment."""
-    X, y, info = _wide_cat_data()
+@pytest.mark.parametrize("case", ["L1000", "L300_padded", "L1000_newton", "L1000_planar"])
+def test_gpu_wide_categorical_matches_reference(case):
+    """1000-level categorical (a 4-column group) and 300-level one (2 real + 2 padding columns) on the GPU engine vs
+    RefTreeBuilder: the group split is one sort over ALL levels (H2O's rule) — identical decisions (1024-bit group
+    bitsets included), left weights and leaf assignment; also Newton splits and the planar (> 32 column) layout."""
+    L = 300 if case.startswith("L300") else 1000
+    X, y, info = _wide_cat_data(L=L)
+    if case.endswith("planar"):                     # 40 more numeric columns: planar bins, the group in plane 0
+        g_ = torch.Generator().manual_seed(4)
+        X = torch.cat([X, torch.randn(40, X.shape[1], generator=g_)])
+        info = DataInfo(info.x + [f"z{i}" for i in range(40)], np.concatenate([info.iscat, np.zeros(40, np.int32)]),
+                        info.domains + [None] * 40, "y", ["0", "1"])
     b = fit_binning(X, info.iscat, info.nlevels, max_cat_bins=1024)
+    assert b.cat_groups == [(0, -(-L // 254))]
     bins = apply_binning(b, X)
     g = y - 0.5
     aux = torch.stack([torch.ones_like(y), g, g, torch.ones_like(y)], 1).contiguous()
     p = T.SplitParams(min_w=10)
+    if case.endswith("newton"):
+        h = torch.full_like(y, 0.25)
+        aux = torch.stack([h, -g, -g, h], 1).contiguous()
+        p = T.SplitParams(min_w=1.0, lam=1.0, mode=T.MODE_NEWTON)
     ref = T.RefTreeBuilder(bins, b.F, b.nbins, b.iscat, None, 5, p)
     ref.set_feature_groups(b.vmap)
+    ref.set_cat_groups(b.gcat())
     ref.build(aux, None, 0, seed=5, leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1]).float())
     tl_r = ref.pop_levels()[0]
     dev = torch.device("cuda", 0)
-    gb = T.GpuTreeBuilder(apply_binning(b, X.to(dev)), b.F, b.nbins, b.iscat, None, 5, p)
+    gb = T.GpuTreeBuilder(apply_binning(b, X.to(dev), planar=b.stride >= 64), b.F, b.nbins, b.iscat, None, 5, p)
+    assert gb.planar == case.endswith("planar")
     gb.set_feature_groups(b.vmap)
+    gb.set_cat_groups(b.gcat())
     gb.build(aux.to(dev), None, 0, seed=5, leaf_fn=lambda ls: (ls[:, 0] / ls[:, 1]).float())
     tl_g = gb.pop_levels()[0]
     assert tl_g.n_leaves == tl_r.n_leaves
-    assert any(int(f) in (2, 3, 4, 5) for d in tl_r.decs for f in d["feat"])
+    assert sum(int(c) == T.GROUP_CAT for d in tl_r.decs for c in d["is_cat"]) >= 2
     for dr, dg in zip(tl_r.decs, tl_g.decs):
         assert np.array_equal(dr["feat"], dg["feat"]) and np.array_equal(dr["bin"], dg["bin"])
         assert np.array_equal(dr["bits"], dg["bits"])
@@ -896,3 +966,29 @@ def test_forest_depth_leaves_from_level_records_match_decoded_trees():
         fr.add_levels(ref.pop_levels()[0], b)
     a = fr.depth_leaves()
     assert a == [(t.depth(), t.n_leaves()) for t in fr.trees]
+
+
+def test_wide_categorical_group_split_mojo_roundtrip(tmp_path):
+    """A GBM whose splits are 1000-level group splits (one sort over all levels): the level bitsets survive the MOJO
+    (writer -> reader -> scoring equals the model's own predictions, every level of the split set scored alike)."""
+    import h2o
+    import pandas as pd
+    from h2o.estimators import H2OGenericEstimator, H2OGradientBoostingEstimator
+    X, y, info = _wide_cat_data(N=8000)
+    lv = X[2].numpy()
+    df = pd.DataFrame({"a": X[0].numpy(), "b": X[1].numpy(),
+                       "c": [None if np.isnan(v) else f"L{int(v)}" for v in lv], "d": X[3].numpy(),
+                       "y": np.where(y.numpy() > 0.5, "1", "0")})
+    h2o.init(verbose=False)
+    fr = h2o.H2OFrame(df, column_types={"c": "enum", "y": "enum"})
+    m = H2OGradientBoostingEstimator(ntrees=4, max_depth=3, seed=1, min_rows=5, nbins_cats=1024)
+    m.train(x=["a", "b", "c", "d"], y="y", training_frame=fr)
+    trees = m._model.forest.trees if hasattr(m, "_model") else None
+    path = m.download_mojo(str(tmp_path))
+    g = H2OGenericEstimator(path=path)
+    g.train()
+    a = m.predict(fr).as_data_frame()
+    b = g.predict(fr).as_data_frame()
+    assert np.allclose(a["1"].values, b["1"].values, atol=1e-6)
+    if trees is not None:
+        assert any(int(t.cat_nbits[i]) >= 900 for t in trees for i in range(len(t.feat)) if t.is_cat[i])
