@@ -127,8 +127,9 @@ __device__ __forceinline__ int group_level(unsigned word, unsigned pack) {
 }
 
 // a decision on its row key: the split column's byte, or (GROUP_CAT) the group's aligned row word
+template <bool GRP = true>
 __device__ __forceinline__ bool dec_go_left_key(const Dec* d, unsigned v) {
-  if (d->is_cat == GROUP_CAT) {
+  if (GRP && d->is_cat == GROUP_CAT) {
     const int l = group_level(v, (unsigned)d->bin);
     return l < 0 ? d->na_left != 0 : ((d->bits[l >> 5] >> (l & 31)) & 1u) != 0u;
   }
@@ -2204,11 +2205,12 @@ __device__ __forceinline__ unsigned row_word4(uint4 v0, uint4 v1, uint4 v2, uint
   return f < 32 ? row_word(v0, v1, f) : row_word(v2, v3, f - 32);
 }
 // a decision's row key from registers (NV > 0) or memory: the split byte, or a group split's row word
-template <int NV>
+// (GRP: the tree can hold group splits; without groups the route / leaf walk compile to the byte path only)
+template <int NV, bool GRP>
 __device__ __forceinline__ unsigned split_key(bool grp, int f, uint4 v0, uint4 v1, uint4 v2, uint4 v3,
                                               const uint8_t* __restrict__ bins, long long row, int stride, long long N,
                                               int planar) {
-  if (grp) {
+  if (GRP && grp) {
     if (NV > 0 && f < NV * 16) return NV > 2 ? row_word4(v0, v1, v2, v3, f) : row_word(v0, v1, f);
     return *reinterpret_cast<const unsigned*>(bins + bin_off(row, f, stride, N, planar));
   }
@@ -2217,7 +2219,7 @@ __device__ __forceinline__ unsigned split_key(bool grp, int f, uint4 v0, uint4 v
                   : bins[bin_off(row, f, stride, N, planar)];
 }
 
-template <int NV>
+template <int NV, bool GRP>
 __device__ __forceinline__ void route_tile(
     const uint8_t* __restrict__ sbins, const float* __restrict__ say, const float* __restrict__ saw,
     uint8_t* __restrict__ dbins, float* __restrict__ day, float* __restrict__ daw, int stride,
@@ -2289,14 +2291,14 @@ __device__ __forceinline__ void route_tile(
     if (fdir) {
       dA = valid && featA >= 0 ? fdir[row] : 0;
     } else if (valid && featA >= 0)
-      dA = dec_go_left_key(&sA, split_key<NV>(grpA, featA, rv0[u], rv1[u], rv2[u], rv3[u], sbins, row, stride, N,
-                                              planar)) ? 0 : 1;
+      dA = dec_go_left_key<GRP>(&sA, split_key<NV, GRP>(grpA, featA, rv0[u], rv1[u], rv2[u], rv3[u], sbins, row, stride,
+                                                        N, planar)) ? 0 : 1;
     if (valid && sC[dA] >= 0) {
       const Dec* b = &sB[dA];
       const int fb = dA ? fB1 : fB0;
       if (fb >= 0)
-        dB = dec_go_left_key(b, split_key<NV>(dA ? grpB1 : grpB0, fb, rv0[u], rv1[u], rv2[u], rv3[u], sbins, row,
-                                              stride, N, planar)) ? 0 : 1;
+        dB = dec_go_left_key<GRP>(b, split_key<NV, GRP>(dA ? grpB1 : grpB0, fb, rv0[u], rv1[u], rv2[u], rv3[u], sbins,
+                                                        row, stride, N, planar)) ? 0 : 1;
     }
     q[u] = 2 * dA + dB;
     mv[u] = valid && sG[q[u]] >= 0;
@@ -2384,7 +2386,7 @@ struct RangesOut {
   int* meta;
   int* done;     // zero before the launch; the last block resets it
 };
-template <int NV>
+template <int NV, bool GRP>
 __global__ __launch_bounds__(LW * 64) void k_route(
     const uint8_t* __restrict__ sbins, const float* __restrict__ say, const float* __restrict__ saw,
     uint8_t* __restrict__ dbins, float* __restrict__ day, float* __restrict__ daw, int stride,
@@ -2396,8 +2398,8 @@ __global__ __launch_bounds__(LW * 64) void k_route(
     RangesOut ro) {
   const int t = blockIdx.x;
   if (t < metaA[1])
-    route_tile<NV>(sbins, say, saw, dbins, day, daw, stride, nodesA, tpA, metaA, decA, clA, crA, decB, clB, crB, curs,
-                   N, planar, lvl2, fdir, t);
+    route_tile<NV, GRP>(sbins, say, saw, dbins, day, daw, stride, nodesA, tpA, metaA, decA, clA, crA, decB, clB, crB,
+                        curs, N, planar, lvl2, fdir, t);
   if (!ro.done) return;
   __shared__ int s_last;
   __shared__ int sh[17];
@@ -2455,7 +2457,7 @@ __global__ __launch_bounds__(256) void k_row_dir(const uint8_t* __restrict__ bin
 #define LEAF_TREE_MAX 2048
 struct LevelPtrs { const Dec* dec; const int* cl; const int* cr; long long cap; };
 
-template <int NV>
+template <int NV, bool GRP>
 __device__ __forceinline__ void leaf_assign_body(
     const uint8_t* __restrict__ bins, int stride, long long N, const LevelPtrs* __restrict__ lv, int D,
     const float* __restrict__ an, const float* __restrict__ ad, const double* __restrict__ qs,
@@ -2512,9 +2514,10 @@ __device__ __forceinline__ void leaf_assign_body(
         const int4 e = st[sbase[d] + i];
         if (e.x < 0) {
           c = e.z;                               // terminal node: child_l == child_r == its leaf
-        } else if ((e.y >> 18) & 1) {            // wide-categorical group: the row word, the record in global
+        } else if (GRP && ((e.y >> 18) & 1)) {   // wide-categorical group: the row word, the record in global
           const Dec* dc = lv[d].dec + i;
-          c = dec_go_left_key(dc, split_key<NV>(true, e.x, v0, v1, v2, v3, bins, row, stride, N, planar)) ? e.z : e.w;
+          c = dec_go_left_key<GRP>(dc, split_key<NV, GRP>(true, e.x, v0, v1, v2, v3, bins, row, stride, N, planar))
+                  ? e.z : e.w;
         } else {
           const int b = (NV > 0 && e.x >= NV * 16) ? bins[bin_off(row, e.x, stride, N, planar)]
                         : NV > 2 ? row_byte4(v0, v1, v2, v3, e.x) : NV > 0 ? row_byte(v0, v1, e.x)
@@ -2531,8 +2534,8 @@ __device__ __forceinline__ void leaf_assign_body(
         if (f < 0) {
           c = lv[d].cl[i];
         } else {
-          c = dec_go_left_key(dc, split_key<NV>(dc->is_cat == GROUP_CAT, f, v0, v1, v2, v3, bins, row, stride, N,
-                                                planar)) ? lv[d].cl[i] : lv[d].cr[i];
+          c = dec_go_left_key<GRP>(dc, split_key<NV, GRP>(dc->is_cat == GROUP_CAT, f, v0, v1, v2, v3, bins, row, stride,
+                                                          N, planar)) ? lv[d].cl[i] : lv[d].cr[i];
         }
       }
       if (c < 0) { leaf = -1 - c; break; }
@@ -2604,13 +2607,13 @@ __global__ void k_leafsum_finish(unsigned long long* __restrict__ leafq, const d
 // its agent-scope RELEASE ticket on `done`; the block drawing the final ticket acquires and finishes all leaf_cap
 // leaves (fp64 sums, re-zeroed fixed-point slots, closed-form values). One launch per tree instead of two.
 // (FUSE is a template switch: the tail costs the unfused kernel 14 VGPRs — 34 -> 48 — and MEASURED r5 115 -> 140 us)
-template <int NV, bool FUSE>
+template <int NV, bool FUSE, bool GRP>
 __global__ __launch_bounds__(256) void k_leaf_assign(
     const uint8_t* __restrict__ bins, int stride, long long N, const LevelPtrs* __restrict__ lv, int D,
     const float* __restrict__ an, const float* __restrict__ ad, const double* __restrict__ qs,
     int* __restrict__ leaf_of_row, unsigned long long* __restrict__ leafq, int leaf_cap, int n_nodes, int planar,
     const uint8_t* __restrict__ lvl2, double* __restrict__ leafsum, LeafVals vals, int* __restrict__ done) {
-  leaf_assign_body<NV>(bins, stride, N, lv, D, an, ad, qs, leaf_of_row, leafq, leaf_cap, n_nodes, planar, lvl2);
+  leaf_assign_body<NV, GRP>(bins, stride, N, lv, D, an, ad, qs, leaf_of_row, leafq, leaf_cap, n_nodes, planar, lvl2);
   if (!FUSE || !done) return;
   __shared__ int s_last;
   __syncthreads();
@@ -3261,11 +3264,12 @@ static int route_launch(const void* sbins, const void* say, const void* saw, voi
                         int stride, const void* nodesA, const void* tpA, const void* metaA, const void* decA,
                         const void* clA, const void* crA, const void* decB, const void* clB, const void* crB,
                         void* curs, int tiles_cap, long long N, int planar, int lp, void* lvl2, const void* fdir,
-                        RangesOut ro, hipStream_t s) {
+                        RangesOut ro, hipStream_t s, int grp = 0) {
   if (planar && (stride % 32 != 0 || stride < 64)) return (int)hipErrorInvalidValue;
   if (lp < 0 || lp > 2 || (lp > 0 && !planar)) return (int)hipErrorInvalidValue;
-#define ROUTE_LAUNCH(NV)                                                                                       \
-  hipLaunchKernelGGL((k_route<NV>), dim3(tiles_cap), dim3(LW * 64), 0, s, (const uint8_t*)sbins,              \
+#define ROUTE_LAUNCH(NV) do { if (grp) ROUTE_LAUNCH2(NV, true); else ROUTE_LAUNCH2(NV, false); } while (0)
+#define ROUTE_LAUNCH2(NV, G)                                                                                   \
+  hipLaunchKernelGGL((k_route<NV, G>), dim3(tiles_cap), dim3(LW * 64), 0, s, (const uint8_t*)sbins,           \
                      (const float*)say, (const float*)saw, (uint8_t*)dbins, (float*)day, (float*)daw, stride,  \
                      (const Node*)nodesA, (const int*)tpA, (const int*)metaA, (const Dec*)decA, (const int*)clA, \
                      (const int*)crA, (const Dec*)decB, (const int*)clB, (const int*)crB, (int4*)curs, N, planar, \
@@ -3278,6 +3282,7 @@ static int route_launch(const void* sbins, const void* say, const void* saw, voi
     default: ROUTE_LAUNCH(0);
   }
 #undef ROUTE_LAUNCH
+#undef ROUTE_LAUNCH2
   return (int)hipGetLastError();
 }
 
@@ -3294,15 +3299,16 @@ int h2o_route(const void* sbins, const void* say, const void* saw, void* dbins, 
 static int leaf_assign_launch(const void* master, int stride, long long N, const void* lvptrs, int D, const void* an,
                               const void* ad, const void* qs, void* leaf_of_row, void* leafq, int leaf_cap,
                               void* leafsum, int n_nodes, int planar, LeafVals lv, hipStream_t s,
-                              const void* lvl2 = nullptr, int* done = nullptr) {
+                              const void* lvl2 = nullptr, int* done = nullptr, int grp = 0) {
   if (D > TP_MAXL_DEV) return (int)hipErrorInvalidValue;
   long long grid = (N + 255) / 256;
   if (grid > 2048) grid = 2048;
   if (grid < 1) grid = 1;
   const size_t lds = (leaf_cap <= LEAF_LDS_MAX ? (size_t)16 * leaf_cap : 0) +
                      (n_nodes <= LEAF_TREE_MAX ? (size_t)16 * n_nodes : 0);
-#define LA(NV) do { if (done) { LA2(NV, true); } else { LA2(NV, false); } } while (0)
-#define LA2(NV, FU) hipLaunchKernelGGL((k_leaf_assign<NV, FU>), dim3((unsigned)grid), dim3(256), lds, s, (const uint8_t*)master, \
+#define LA(NV) do { if (done) { LA1(NV, true); } else { LA1(NV, false); } } while (0)
+#define LA1(NV, FU) do { if (grp) { LA2(NV, FU, true); } else { LA2(NV, FU, false); } } while (0)
+#define LA2(NV, FU, G) hipLaunchKernelGGL((k_leaf_assign<NV, FU, G>), dim3((unsigned)grid), dim3(256), lds, s, (const uint8_t*)master, \
                                   stride, N, (const LevelPtrs*)lvptrs, D, (const float*)an, (const float*)ad,          \
                                   (const double*)qs, (int*)leaf_of_row, (unsigned long long*)leafq, leaf_cap, n_nodes, planar, \
                                   (const uint8_t*)lvl2, (double*)leafsum, lv, done)
@@ -3316,6 +3322,7 @@ static int leaf_assign_launch(const void* master, int stride, long long N, const
     default: LA(0);
   }
 #undef LA
+#undef LA1
 #undef LA2
   if (!done)
     hipLaunchKernelGGL(k_leafsum_finish, dim3((leaf_cap + 255) / 256), dim3(256), 0, s, (unsigned long long*)leafq,
@@ -3537,7 +3544,7 @@ static int tp_route(const TreePlan* P, int e, hipStream_t s, bool ranges) {
   return route_launch(sb, sy, sw, P->bb[di], P->by[di], P->unit ? nullptr : P->bw[di], P->stride, P->nodes[e], P->tp[e],
                       P->meta[e], P->dec[e], P->cl[e], P->cr[e], P->dec[e + 1], P->cl[e + 1], P->cr[e + 1],
                       P->cur[e + 1], P->tiles_cap[e], P->N, P->planar, lp, e == 0 ? tp_lvl2(P) : nullptr,
-                      (e == 0 && tp_lvl2(P) && P->fdir) ? P->fdir : nullptr, ro, s);
+                      (e == 0 && tp_lvl2(P) && P->fdir) ? P->fdir : nullptr, ro, s, P->gcat != nullptr);
 }
 
 #define TP_CHECK(x) do { int rc_ = (x); if (rc_) return rc_; } while (0)
@@ -3738,7 +3745,7 @@ static int tree_leaves(const TreePlan* P, bool values, hipStream_t s) {
   if (fused < 0) { const char* e = getenv("H2O_LEAF_FUSED"); fused = (e && e[0] == '1') ? 1 : 0; }
   return leaf_assign_launch(P->master, P->stride, P->N, P->lvptrs, P->D, tp_aux(P, P->num_plane), tp_aux(P, 3), P->qs,
                             P->leaf_of_row, P->leafq, P->leaf_cap, P->leafsum, n_nodes, P->planar, lv, s, tp_lvl2(P),
-                            fused ? (int*)P->counters + 3 : nullptr);
+                            fused ? (int*)P->counters + 3 : nullptr, P->gcat != nullptr);
 }
 
 int h2o_tree_leaves(const TreePlan* P, hipStream_t s) { return tree_leaves(P, false, s); }
