@@ -1909,6 +1909,10 @@ __device__ void level_tile_prefix(const Node* __restrict__ next, int nn, int* __
 // Odd depth (next level even): the children's ranges are only known after k_route, which fills each
 //   odd node's region of the next buffer from both ends; this kernel sets up those cursors
 //   (curs[c] = {front, back, region start, region end}, from the parent's left count prev_nl) and
+// the fields of a decision the plan reads (the 176-B record carries a 1024-bit set it never needs)
+struct DecLite { int feat; double wl, wr; };
+__device__ __forceinline__ DecLite dec_lite(const Dec* d) { return DecLite{d->feat, d->wl, d->wr}; }
+
 //   k_ranges turns the final cursors into ranges + tile prefix.
 __device__ void plan_body(
     const Node* __restrict__ nodes, const int* __restrict__ meta, Dec* __restrict__ dec,
@@ -1946,7 +1950,7 @@ __device__ void plan_body(
   // 1. children: active / leaf classification, compaction with capacity
   int act_cnt = 0;
   for (int i = na; i < nb2; ++i) {
-    const Dec d = dec[i];
+    const DecLite d = dec_lite(dec + i);
     int a = 0;
     if (d.feat >= 0 && depth + 1 < max_depth) {
       // child activity is decided from GLOBAL (all-reduced) weights so every rank plans alike
@@ -1961,7 +1965,7 @@ __device__ void plan_body(
   {
     int ao = act_off;
     for (int i = na; i < nb2; ++i) {
-      const Dec d = dec[i];
+      const DecLite d = dec_lite(dec + i);
       int flags = 0, lv = 0;
       if (d.feat < 0) { lv = 1; }
       else {
@@ -1982,7 +1986,7 @@ __device__ void plan_body(
   int ao = act_off;
   int lo = leaf_base0 + leaf_off;
   for (int i = na; i < nb2; ++i) {
-    const Dec d = dec[i];
+    const DecLite d = dec_lite(dec + i);
     const Node nd = nodes[i];
     const int flags = scratch[i];
     if (d.feat < 0) {
