@@ -14,8 +14,9 @@ Reference behaviour (re-expressed for the FastAPI server, no Jetty):
     Please login." otherwise (``water/webserver/H2OHttpViewImpl.java:112-152``); TRACE is refused with 405 (gateHandler).
 The realm file is Jetty's PropertyUserStore format, ``user: credential[, role ...]`` (``#`` comments), with a
 credential in plain text or Jetty's ``OBF:`` / ``MD5:`` / ``CRYPT:`` forms (``h2o-assemblies/main/tests/python/
-realm.properties`` is a plain one). LDAP / Kerberos / PAM / SPNEGO need JAAS login modules and their servers, which
-this image does not have: they are refused at startup with that reason.
+realm.properties`` is a plain one). ``-ldap_login -login_conf <JAAS file>`` authenticates against an LDAP server with
+Jetty LdapLoginModule's semantics (:mod:`.ldap`). Kerberos / PAM / SPNEGO need JAAS modules, a KDC or the host's PAM
+stack, which this image does not have: they are refused at startup with that reason.
 """
 from __future__ import annotations
 
@@ -142,14 +143,50 @@ class LoginConfig:
                              "with of a LoginService.")
         if self.session_timeout and not self.form_auth:
             raise ValueError("Session timeout can only be enabled for Form based authentication (use -form_auth)")
-        if self.ldap_login or self.kerberos_login or self.spnego_login or self.pam_login:
-            raise ValueError("LDAP / Kerberos / SPNEGO / PAM logins need JAAS login modules and their servers, which "
-                             "this build does not include; use -hash_login")
+        if self.kerberos_login or self.spnego_login or self.pam_login:
+            raise ValueError("Kerberos / SPNEGO / PAM logins need JAAS login modules and their servers, which "
+                             "this build does not include; use -hash_login or -ldap_login")
+        if self.ldap_login:
+            from .ldap import LdapLoginService
+            LdapLoginService(self.login_conf)        # a malformed JAAS config fails at startup, not at first login
         return self
 
     @property
     def enabled(self) -> bool:
-        return self.hash_login
+        return self.hash_login or self.ldap_login
+
+    def service(self):
+        if self.ldap_login:
+            from .ldap import LdapLoginService
+            return _CachedLogin(LdapLoginService(self.login_conf))
+        return HashLoginService(self.login_conf)
+
+
+class _CachedLogin:
+    """Remembers successful logins of a remote login service for ``ttl_s`` (Basic auth re-sends the credentials on
+    every request; without this each REST call would be an LDAP round trip). Only a salted digest of the credentials
+    is kept."""
+
+    def __init__(self, svc, ttl_s: float = 60.0, cap: int = 1024):
+        self.svc, self.ttl_s, self.cap = svc, ttl_s, cap
+        self._salt = secrets.token_bytes(16)
+        self._ok: dict[bytes, float] = {}
+        self._lock = threading.Lock()
+
+    def login(self, user: str, password: str) -> bool:
+        k = hashlib.sha256(self._salt + user.encode("utf-8") + b"\0" + password.encode("utf-8")).digest()
+        now = time.time()
+        with self._lock:
+            t = self._ok.get(k)
+            if t is not None and now - t < self.ttl_s:
+                return True
+        if not self.svc.login(user, password):
+            return False
+        with self._lock:
+            if len(self._ok) >= self.cap:
+                self._ok.clear()
+            self._ok[k] = now
+        return True
 
 
 _FORM = """<!DOCTYPE html><html><head><title>H2O Login</title></head><body>
@@ -236,8 +273,9 @@ def install(app, cfg: LoginConfig) -> None:
     """Constrain every route of ``app`` to authenticated users (no-op when no login method is configured)."""
     if not cfg.enabled:
         return
+    from starlette.concurrency import run_in_threadpool
     from starlette.responses import HTMLResponse, JSONResponse, RedirectResponse, Response
-    svc = HashLoginService(cfg.login_conf)
+    svc = cfg.service()
     sessions = _Sessions(60.0 * cfg.session_timeout)
     install.sessions = sessions                  # (tests: the live session table)
     cookie = "JSESSIONID"
@@ -266,7 +304,7 @@ def install(app, cfg: LoginConfig) -> None:
             form = parse_qs((await request.body()).decode("utf-8", "replace"))
             user = (form.get("j_username") or [""])[0]
             pw = (form.get("j_password") or [""])[0]
-            if not svc.login(user, pw):
+            if not await run_in_threadpool(svc.login, user, pw):
                 return RedirectResponse("/loginError", status_code=303)
             r = RedirectResponse(_safe_target(request.cookies.get(TARGET_COOKIE)), status_code=303)
             r.set_cookie(cookie, sessions.new(user=user), httponly=True, path="/", secure=secure)
@@ -276,7 +314,7 @@ def install(app, cfg: LoginConfig) -> None:
         if s is not None and s.get("user"):
             return await call_next(request)
         cred = _basic_user(headers)
-        if cred is not None and svc.login(*cred):
+        if cred is not None and await run_in_threadpool(svc.login, *cred):
             return await call_next(request)
         if cfg.form_auth and _is_browser(headers):
             # FormAuthenticator: remember the requested URI (a short-lived cookie: no server state per anonymous

@@ -106,6 +106,8 @@ def test_login_option_rules(tmp_path):
     with pytest.raises(ValueError, match="File does not exist"):
         L(hash_login=True, login_conf=str(tmp_path / "missing")).validate()
     with pytest.raises(ValueError, match="JAAS"):
+        L(kerberos_login=True, login_conf=realm).validate()
+    with pytest.raises(ValueError, match="JAAS"):            # a realm file is not a JAAS LDAP config
         L(ldap_login=True, login_conf=realm).validate()
     with pytest.raises(SystemExit):
         main(["-form_auth"])
