@@ -317,6 +317,11 @@ class SharedTreeTrainer:
         built = start
         hprof = os.environ.get("H2O_HOST_PROF") == "1"    # host seconds per phase (launch-bound diagnosis)
         ht = dict(prepare=0.0, build=0.0, update=0.0, drain=0.0, loop=0.0, build_max=0.0)
+        # H2O_TREE_GC=0: no cyclic garbage collection inside the tree loop (A/B of host stalls between trees)
+        import gc
+        gc_was = gc.isenabled()
+        if os.environ.get("H2O_TREE_GC", "1") == "0":
+            gc.disable()
         for t in range(start, ntrees):
             tl0 = time.perf_counter()
             feat_ok = self.binning.expand(self._tree_feature_mask(rng, F))
@@ -376,6 +381,8 @@ class SharedTreeTrainer:
                 if (built - start) % _CANCEL_EVERY == 0:
                     job.check_cancelled()        # (REST cloud: a collective; every rank checks at the same trees)
         self._drain(handles, forest, gains)
+        if gc_was:
+            gc.enable()
         if hprof and built > start + 2:
             n = (built - start - 2) * K
             print("[host-prof] us/tree " + " ".join(f"{k}={v / (1 if k.endswith('_max') else n) * 1e6:.1f}"

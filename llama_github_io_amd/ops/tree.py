@@ -1204,7 +1204,10 @@ class GpuTreeBuilder:
             P.leaf_lam, P.leaf_l1 = float(lam), float(l1)
         ref = ctypes.byref(P)
         if not self.dist_mode:
-            nat.check(lib.h2o_tree_all(ref, s), "tree_all")
+            if self._graph_replay(P, k_cols):
+                pass
+            else:
+                nat.check(lib.h2o_tree_all(ref, s), "tree_all")
         else:
             rc = lib.h2o_tree_dist(ref, s)
             err = getattr(self.transport, "error", None)
@@ -1218,6 +1221,49 @@ class GpuTreeBuilder:
             vals = leaf_fn(self.leafsum)
             self.av["leafval"].view(torch.float32)[: vals.numel()].copy_(vals.to(torch.float32))
         return self._snapshot()
+
+    # ---- hipGraph replay of the per-tree launch sequence (single process)
+    def _seed_used(self, P, k_cols) -> bool:
+        """Does any kernel of the tree read the seed? (column sampling, random splits, Random / RoundRobin lattices)"""
+        ht = int(self.p.hist_type)
+        return (bool(P.k_cols) or any(int(v) for v in P.kc_level) or bool(P.random_split)
+                or (bool(P.edges) and ht in (HT_RANDOM, HT_ROUND_ROBIN)))
+
+    def _graph_replay(self, P, k_cols) -> bool:
+        """The whole tree as ONE hipGraph launch: the native sequence (h2o_tree_all, ~30 kernels) is captured once
+        into a torch.cuda.CUDAGraph and replayed for every tree whose launch plan is byte-identical (kernel arguments
+        are baked in at capture: the plan struct is the signature; the seed only when a kernel reads it). A plan that
+        changes every tree (e.g. learn_rate_annealing in the leaf values) stops the capture after 3 misses.
+        ``H2O_TREE_GRAPH=0``: direct launches."""
+        if self.dev.type != "cuda" or os.environ.get("H2O_TREE_GRAPH", "1") == "0" or self.__dict__.get("_graph_off"):
+            return False
+        seed = P.seed
+        if not self._seed_used(P, k_cols):
+            P.seed = 0
+        sig = bytes(P)
+        P.seed = seed
+        g = self.__dict__.get("_graph")
+        if g is None or self.__dict__.get("_graph_sig") != sig:
+            misses = self.__dict__.get("_graph_misses", 0) + (g is not None)
+            self._graph_misses = misses
+            if misses >= 3:
+                self._graph_off = True
+                self._graph = None
+                return False
+            g = torch.cuda.CUDAGraph()
+            try:
+                with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                    rc = self.lib.h2o_tree_all(ctypes.byref(P), nat.stream_ptr(self.dev))
+            except Exception:          # noqa: BLE001 - capture refused by the runtime: launch directly from now on
+                self._graph_off = True
+                self._graph = None
+                return False
+            nat.check(rc, "tree_all (capture)")
+            self._graph, self._graph_sig = g, sig
+        else:
+            self._graph_misses = 0
+        self._graph.replay()
+        return True
 
     def _snapshot(self):
         # the tree's structure travels to pinned host memory asynchronously: the host decodes finished
