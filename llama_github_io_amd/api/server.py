@@ -885,9 +885,17 @@ def create_app(client_disconnect_timeout: float | None = None, login=None):
                                f"models sorted by {cols[1] if len(cols) > 1 else ''}",
                                row_headers=[str(i) for i in range(len(rows))])
 
+    def _automl(pid):
+        """An AutoML by project name, or by H2O's AutoML key ``<project>@@<response>`` (AutoML.java key naming,
+        what Flow's getLeaderboard cells name)."""
+        aml = dkv.get(pid)
+        if aml is None and "@@" in pid:
+            aml = dkv.get(pid.split("@@", 1)[0])
+        return aml
+
     @app.get("/99/AutoML/{pid}")
     def automl_get(pid: str):
-        aml = dkv.get(pid)
+        aml = _automl(pid)
         if aml is None:
             raise KeyError(f"AutoML {pid} not found")
         rows, table = _leaderboard_table(aml)
@@ -910,7 +918,7 @@ def create_app(client_disconnect_timeout: float | None = None, login=None):
 
     @app.get("/99/Leaderboards/{pid}")
     def leaderboard_get(pid: str):
-        aml = dkv.get(pid)
+        aml = _automl(pid)
         if aml is None:
             raise KeyError(f"AutoML {pid} not found")
         rows, table = _leaderboard_table(aml)

@@ -1108,6 +1108,8 @@ class H2OFrame:
 
     def impute(self, column=-1, method="mean", combine_method="interpolate", by=None, group_by_frame=None, values=None):
         targets = self.names if column in (-1, None) else self._resolve(column)
+        if by not in (None, [], ()):
+            return self._impute_by(targets, method, by)
         res = []
         if self._shard is not None:
             # global statistics (collectives), applied to each shard in place
@@ -1141,6 +1143,60 @@ class H2OFrame:
                 c.data = torch.nan_to_num(c.data, nan=fill)
                 res.append(fill)
         return res
+
+    def _impute_by(self, targets, method, by):
+        """Group-wise imputation (AstImpute.java:205-257): each NA of a target column takes the aggregate of its
+        group of the ``by`` columns — mean / median of a numeric column, mode of a categorical one, NAs removed
+        ("rm"); a group whose aggregate is NA keeps its NAs. NA keys form a group of their own (AstGroup). Row
+        sharded frames gather the key and target columns, aggregate once, and write their own rows back.
+        Returns {target: {group key tuple: fill}}."""
+        bys = self._resolve(by if isinstance(by, (list, tuple)) else [by])
+        sharded = self._shard is not None
+        if sharded:
+            from .parallel import collectives as coll
+            row0 = coll.row_offset(self.nrows)
+
+        def full(t):
+            return dframe.gather_tensor(t) if sharded else t
+        keys = torch.stack([full(self._cols[b].as_float()).double() for b in bys], 1)
+        keys = torch.nan_to_num(keys, nan=float("inf"))          # NA keys: one group
+        uk, inv = torch.unique(keys, dim=0, return_inverse=True)
+        G = uk.shape[0]
+        out = {}
+        for n in targets:
+            if n in bys:
+                raise ValueError(f"column {n} is both imputed and a group-by column")
+            c = self._cols[n]
+            if c.type not in _NUMERIC and c.type != "enum":
+                continue
+            v = full(c.data.double() if c.type != "enum" else torch.where(c.data < 0, torch.nan, c.data.double()))
+            ok = ~torch.isnan(v)
+            if c.type == "enum" or method == "mode":
+                fill = torch.full((G,), float("nan"), dtype=torch.float64, device=v.device)
+                for gi in range(G):
+                    vv = v[ok & (inv == gi)]
+                    if vv.numel():
+                        fill[gi] = float(torch.mode(vv).values)
+            elif method == "median":
+                fill = torch.full((G,), float("nan"), dtype=torch.float64, device=v.device)
+                for gi in range(G):
+                    vv = v[ok & (inv == gi)]
+                    if vv.numel():
+                        fill[gi] = float(torch.quantile(vv, 0.5))
+            else:
+                s = torch.zeros(G, dtype=torch.float64, device=v.device).index_add_(0, inv[ok], v[ok])
+                k = torch.zeros(G, dtype=torch.float64, device=v.device).index_add_(0, inv[ok], torch.ones_like(v[ok]))
+                fill = s / k
+            filled = torch.where(ok, v, fill[inv])
+            if sharded:
+                filled = filled[row0:row0 + self.nrows]
+            if c.type == "enum":
+                c.data = torch.where(torch.isnan(filled), -1, filled).to(c.data.dtype)
+            else:
+                c.data = filled.to(c.data.dtype)
+            ukc = uk.cpu().tolist()
+            out[n] = {tuple(None if math.isinf(x) else x for x in ukc[gi]): float(fill[gi]) for gi in range(G)}
+        return out
 
     def scale(self, center=True, scale=True):
         cols = []

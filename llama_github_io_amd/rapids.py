@@ -328,9 +328,13 @@ class Session:
         return g.get_frame()
 
     def _impute(self, fr, col, method, combine, by, *rest):
+        """(h2o.impute data col method combine_method groupby groupByFrame values) — AstImpute.java:86."""
         fr = _frame(fr)
-        fr.impute(int(col), method)
-        return [0.0]
+        by = [int(b) for b in (by if isinstance(by, list) else ([] if by in (None, "_") else [by]))]
+        col = int(col)
+        r = fr.impute(-1 if col < 0 else col, str(method).lower(), str(combine).lower(),
+                      by=[fr.names[b] for b in by] or None)
+        return [0.0] if by else [float(x) for x in r] or [0.0]
 
     # ---- evaluation
     def eval_node(self, node):

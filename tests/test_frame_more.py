@@ -93,3 +93,39 @@ def test_frame_id_rename_refused_while_write_locked():
         assert fr.frame_id == "locked_src" and dkv.get("locked_src") is fr and not dkv.contains("locked_dst")
     fr.frame_id = "locked_dst"
     assert dkv.get("locked_dst") is fr and not dkv.contains("locked_src")
+
+
+def test_impute_by_group_matches_pandas():
+    """h2o.impute with groupByCols (AstImpute.java:205-257): NAs take their group's mean / median / mode; a group
+    with no observed value keeps its NAs; NA keys are a group of their own."""
+    import numpy as np
+    import pandas as pd
+    from llama_github_io_amd.frame import H2OFrame
+    from llama_github_io_amd.rapids import rapids
+    rng = np.random.default_rng(3)
+    n = 300
+    df = pd.DataFrame({"g": rng.choice(["a", "b", "c", None], n), "h": rng.integers(0, 3, n).astype(float),
+                       "x": rng.normal(size=n), "e": rng.choice(["u", "v", "w"], n)})
+    df.loc[rng.random(n) < 0.2, "x"] = np.nan
+    df.loc[df.g == "c", "x"] = np.nan                                  # a group with nothing to impute from
+    df.loc[rng.random(n) < 0.2, "e"] = None
+    for method in ("mean", "median"):
+        fr = H2OFrame(df.copy())
+        fr.impute("x", method, by=["g", "h"])
+        got = fr.as_data_frame()["x"].to_numpy()
+        key = df.g.fillna("NA") + "|" + df.h.astype(str)
+        agg = df.x.groupby(key).transform(method)
+        want = df.x.fillna(agg).to_numpy()
+        np.testing.assert_allclose(got, want, rtol=1e-12, equal_nan=True)
+        assert np.isnan(got[(df.g == "c").to_numpy()]).all()
+    fr = H2OFrame(df.copy())
+    fr.impute("e", "mode", by=["h"])
+    got = fr.as_data_frame()["e"]
+    for hv in (0.0, 1.0, 2.0):
+        m = (df.h == hv).to_numpy()
+        mode = df.e[m].value_counts().sort_index().idxmax()             # ties: the smallest level, as torch.mode
+        assert (got[m & df.e.isna().to_numpy()] == mode).all()
+    # through Rapids (Flow's imputeColumn cell): column 2 by columns [0 1]
+    fr = H2OFrame(df.copy(), destination_frame="imp_by")
+    rapids('(h2o.impute imp_by 2 "mean" "interpolate" [0 1] _ _)')
+    assert np.isnan(fr.as_data_frame()["x"].to_numpy()).sum() == int((df.g == "c").sum())
