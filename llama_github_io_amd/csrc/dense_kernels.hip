@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 namespace {
 
@@ -154,6 +155,80 @@ __global__ __launch_bounds__(256) void k_adadelta(float* __restrict__ p, const f
       if (tm.f32) ((float*)tm.wt)[t] = pi + d;
       else ((__hip_bfloat16*)tm.wt)[t] = __float2bfloat16(pi + d);
     }
+  }
+}
+
+// The same update with the transposed copy: one workgroup per 8-row strip of a 64 x 64 weight tile (the
+// k_dl_wgrad tiling; 8 strips per tile so a [784, 200, 200, 2] network spreads over ~580 workgroups),
+// trailing workgroups take the biases. The flat per-element kernel above writes the transpose with a stride of
+// n_out elements (one cache line per weight); here the updated strip goes through LDS and both copies are written
+// along their contiguous axis (the transposed one in 16-element runs).
+// MEASURED (r6, 10M x 784 [200,200] bf16, 4096-row steps): one workgroup per whole tile (74 workgroups, 16
+// elements x S split partials per thread) took 54.7 us per step against 8.6 for the flat kernel; end to end
+// (scripts/gpu_r6_wave.sh, two runs each) 8-row strips 58.4 / 57.8M samples/s, 16-row 56.7 / 55.8, flat 57.5 / 57.4.
+
+__device__ __forceinline__ float adadelta_one(float pi, float gi, float* eg2, float* edx2, int64_t i, bool decay,
+                                              float rho, float eps, float l1, float l2) {
+  if (decay) gi += l2 * pi + (pi > 0.f ? l1 : (pi < 0.f ? -l1 : 0.f));
+  const float e = rho * eg2[i] + (1.f - rho) * gi * gi;
+  const float d = -sqrtf(edx2[i] + eps) / sqrtf(e + eps) * gi;
+  eg2[i] = e;
+  edx2[i] = rho * edx2[i] + (1.f - rho) * d * d;
+  return pi + d;
+}
+
+template <int AD_STRIP>
+__global__ __launch_bounds__(256) void k_adadelta_tiles(float* __restrict__ p, const float* __restrict__ g,
+                                                        float* __restrict__ eg2, float* __restrict__ edx2, int64_t n,
+                                                        int64_t n_decay, float rho, float eps, float l1, float l2,
+                                                        __hip_bfloat16* __restrict__ shadow, WTMap tm) {
+  __shared__ float tile[AD_STRIP][65];
+  constexpr int NS = 64 / AD_STRIP;
+  const int nst = tm.tile_start[tm.L] * NS;
+  if ((int)blockIdx.x >= nst) {                     // biases: plain elementwise
+    const int64_t i = n_decay + (int64_t)(blockIdx.x - nst) * 256 + threadIdx.x;
+    if (i < n) p[i] = adadelta_one(p[i], g[i], eg2, edx2, i, false, rho, eps, l1, l2);
+    return;
+  }
+  const int b = blockIdx.x / NS, strip = blockIdx.x % NS;
+  int l = 0;
+  while (l + 1 < tm.L && b >= tm.tile_start[l + 1]) ++l;
+  const int t = b - tm.tile_start[l];
+  const int r0 = (t / tm.tiles_j[l]) * 64 + strip * AD_STRIP, c0 = (t % tm.tiles_j[l]) * 64;
+  const int nin = tm.n_in[l], nout = tm.n_out[l];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = c0 + tx;
+  const float* ps = tm.wpart ? tm.wpart + (int64_t)b * tm.S * 4096 + strip * AD_STRIP * 64 : nullptr;
+  float gs[AD_STRIP / 4];
+#pragma unroll
+  for (int k = 0; k < AD_STRIP / 4; ++k) gs[k] = 0.f;
+  if (ps) {                                         // all split partials of the thread's rows in flight together
+    for (int s2 = 0; s2 < tm.S; ++s2)
+#pragma unroll
+      for (int k = 0; k < AD_STRIP / 4; ++k) gs[k] += ps[(int64_t)s2 * 4096 + (ty + 4 * k) * 64 + tx];
+  }
+  const float inv = tm.wpart ? tm.wpart[tm.inv_off] : 0.f;
+#pragma unroll
+  for (int k = 0; k < AD_STRIP / 4; ++k) {
+    const int rr = ty + 4 * k, r = r0 + rr;
+    if (r >= nout || c >= nin) continue;
+    const int64_t i = tm.w_off[l] + (int64_t)r * nin + c;
+    const float gi = ps ? gs[k] * inv : g[i];
+    const float v = adadelta_one(p[i], gi, eg2, edx2, i, true, rho, eps, l1, l2);
+    p[i] = v;
+    if (shadow) shadow[i] = __float2bfloat16(v);
+    tile[rr][tx] = v;
+  }
+  __syncthreads();
+  // transposed: WT[c][r]; thread -> (column cc of the strip's 64, row run of 16): lanes 0-15 one column
+  const int rr = threadIdx.x & (AD_STRIP - 1);
+  const int r = r0 + rr;
+  for (int cc = threadIdx.x / AD_STRIP; cc < 64; cc += 256 / AD_STRIP) {
+    const int c2 = c0 + cc;
+    if (r >= nout || c2 >= nin) continue;
+    const int64_t o = tm.w_off[l] + (int64_t)c2 * nout + r;
+    if (tm.f32) ((float*)tm.wt)[o] = tile[rr][cc];
+    else ((__hip_bfloat16*)tm.wt)[o] = __float2bfloat16(tile[rr][cc]);
   }
 }
 
@@ -421,6 +496,36 @@ int h2o_adadelta(float* p, const float* g, float* eg2, float* edx2, long long n,
       tm.wpart = wpart; tm.S = S; tm.inv_off = inv_off;
       for (int l = 0; l <= L; ++l) tm.tile_start[l] = tile_start[l];
       for (int l = 0; l < L; ++l) tm.tiles_j[l] = tiles_j[l];
+    }
+    // tiled update (H2O_ADADELTA_FLAT=1 keeps the per-element kernel): the 64 x 64 tile map of the weights, which
+    // must be the one the split partials were written with, and weights laid out back to back from offset 0
+    static int flat = -1;
+    if (flat < 0) { const char* e = getenv("H2O_ADADELTA_FLAT"); flat = (e && e[0] == '1') ? 1 : 0; }
+    bool ok = !flat;
+    long long ts = 0, off = 0;
+    int tsv[7], tjv[6];
+    for (int l = 0; l < L && ok; ++l) {
+      tjv[l] = (tm.n_in[l] + 63) / 64;
+      tsv[l] = (int)ts;
+      ts += (long long)((tm.n_out[l] + 63) / 64) * tjv[l];
+      ok = tm.w_off[l] == off;
+      off += (long long)tm.n_in[l] * tm.n_out[l];
+      if (wpart) ok = ok && tsv[l] == tm.tile_start[l] && tjv[l] == tm.tiles_j[l];
+    }
+    tsv[L] = (int)ts;
+    ok = ok && off == n_decay && ts < (1LL << 30) && (!wpart || tm.tile_start[L] == tsv[L]);
+    if (ok) {
+      for (int l = 0; l <= L; ++l) tm.tile_start[l] = tsv[l];
+      for (int l = 0; l < L; ++l) tm.tiles_j[l] = tjv[l];
+      // H2O_ADADELTA_STRIP=8 (default) | 16 | 64 rows per workgroup
+      static int strip = 0;
+      if (!strip) { const char* e = getenv("H2O_ADADELTA_STRIP"); strip = e ? atoi(e) : 8;
+                    if (strip != 16 && strip != 64) strip = 8; }
+      const long long grid2 = ts * (64 / strip) + (n - n_decay + 255) / 256;
+      auto kern = strip == 8 ? k_adadelta_tiles<8> : strip == 64 ? k_adadelta_tiles<64> : k_adadelta_tiles<16>;
+      hipLaunchKernelGGL(kern, dim3((unsigned)grid2), dim3(256), 0, stream, p, g, eg2, edx2, (int64_t)n,
+                         (int64_t)n_decay, rho, eps, l1, l2, (__hip_bfloat16*)shadow, tm);
+      return (int)hipGetLastError();
     }
   }
   hipLaunchKernelGGL(k_adadelta, dim3((unsigned)grid), dim3(256), 0, stream, p, g, eg2, edx2, (int64_t)n,

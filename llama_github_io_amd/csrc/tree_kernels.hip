@@ -1843,6 +1843,7 @@ struct PlanReduce {          // k_plan's fused k_split_reduce (cand == null: dec
   const unsigned char* node_ok;
   const int* fgroup;
   int cfs, ccap;             // rank-major sliced candidates (see cand_at); 0 = [cap][F]
+  int no_wave;               // 1: levels of <= 64 nodes take the block plan too (H2O_PLAN_WAVE=0)
 };
 #define PLAN_REDUCE_MAX 256
 
@@ -1914,6 +1915,97 @@ struct DecLite { int feat; double wl, wr; };
 __device__ __forceinline__ DecLite dec_lite(const Dec* d) { return DecLite{d->feat, d->wl, d->wr}; }
 
 //   k_ranges turns the final cursors into ranges + tile prefix.
+
+__device__ __forceinline__ int wave_excl_scan(int v, int* total) {
+  const int lane = threadIdx.x & 63;
+  int x = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  *total = __shfl(x, 63, 64);
+  return x - v;
+}
+
+// The plan of a level of <= 64 nodes on ONE wave, lane = node, every prefix a wave scan in registers: the same
+// numbering, children and tile prefixes as the block version below (whose four block scans each cost three
+// barriers and a serial pass over the waves). The next level's tile prefix is computed from the children each
+// lane creates (its children are consecutive in the next list), so the next list is never read back.
+__device__ void plan_wave(
+    const Node* __restrict__ nodes, int n, Dec* __restrict__ dec, int* __restrict__ node_nl,
+    const int* __restrict__ prev_nl, int4* __restrict__ curs, int* __restrict__ child_l, int* __restrict__ child_r,
+    Node* __restrict__ next, int* __restrict__ next_tile_prefix, int* __restrict__ next_meta,
+    int* __restrict__ next_build_prefix, int* __restrict__ counters, int depth, int max_depth, double min_w,
+    int cap_next, int leaf_cap) {
+  const int i = threadIdx.x;                       // lane = node
+  const bool odd = depth & 1;
+  const bool live = i < n;
+  Node nd{0, 0, 0, -1, -1, 0, 0, 0};
+  DecLite d{-1, 0.0, 0.0};
+  if (live) {
+    nd = nodes[i];
+    d = dec_lite(dec + i);
+    if (!odd) {
+      node_nl[i] = 0;
+    } else {
+      const int nl = nd.parent >= 0 ? prev_nl[nd.parent] : 0;
+      const int cs = nd.start + (nd.dir ? nl : 0);
+      const int ce = nd.dir ? nd.start + nd.len : nd.start + nl;
+      curs[i] = make_int4(cs, ce, cs, ce);
+    }
+  }
+  const bool split = live && d.feat >= 0;
+  const bool la = split && depth + 1 < max_depth && d.wl >= 2.0 * min_w;
+  const bool ra = split && depth + 1 < max_depth && d.wr >= 2.0 * min_w;
+  int act_total;
+  const int act_off = wave_excl_scan((la ? 1 : 0) + (ra ? 1 : 0), &act_total);
+  int ao = act_off;
+  int li = -1, ri = -1;
+  if (la) { if (ao < cap_next) li = ao; ++ao; }
+  if (ra) { if (ao < cap_next) ri = ao; ++ao; }
+  const int lv = !live ? 0 : (!split ? 1 : 2 - (li >= 0) - (ri >= 0));
+  const int leaf_base0 = counters[0];
+  int n_leaves_new;
+  int lo = leaf_base0 + wave_excl_scan(lv, &n_leaves_new);
+  if (live) {
+    if (!split) {
+      const int lid = min(lo, leaf_cap - 1);
+      child_l[i] = -1 - lid; child_r[i] = -1 - lid;
+    } else {
+      child_l[i] = li >= 0 ? li : -1 - min(lo++, leaf_cap - 1);
+      child_r[i] = ri >= 0 ? ri : -1 - min(lo++, leaf_cap - 1);
+      if (li >= 0 && ri >= 0) {
+        const bool build_left = d.wl <= d.wr;
+        next[li] = Node{nd.start, nd.len, build_left ? 1 : 0, i, ri, 0, 0, 0};
+        next[ri] = Node{nd.start, nd.len, build_left ? 0 : 1, i, li, 1, 0, 0};
+      } else if (li >= 0) {
+        next[li] = Node{nd.start, nd.len, 1, i, -1, 0, 0, 0};
+      } else if (ri >= 0) {
+        next[ri] = Node{nd.start, nd.len, 1, i, -1, 1, 0, 0};
+      }
+    }
+  }
+  const int nn = min(act_total, cap_next);
+  if (i == 0) counters[0] = min(leaf_base0 + n_leaves_new, leaf_cap);
+  if (odd) {
+    if (i == 0) { next_meta[0] = nn; next_meta[1] = 0; next_meta[2] = 0; }
+    return;
+  }
+  // even depth: the next (odd) level's nodes keep the parent's range — tiles of its children, in child order
+  const int kt = (nd.len + TILE - 1) / TILE;
+  const bool lb = li >= 0 && (ri < 0 || d.wl <= d.wr);
+  const bool rb = ri >= 0 && !(li >= 0 && d.wl <= d.wr);
+  int tot, totb;
+  int off = wave_excl_scan((li >= 0 ? kt : 0) + (ri >= 0 ? kt : 0), &tot);
+  int offb = wave_excl_scan((lb ? kt : 0) + (rb ? kt : 0), &totb);
+  if (li >= 0) { next_tile_prefix[li] = off; next_build_prefix[li] = offb; off += kt; offb += lb ? kt : 0; }
+  if (ri >= 0) { next_tile_prefix[ri] = off; next_build_prefix[ri] = offb; }
+  if (i == 0) {
+    next_tile_prefix[nn] = tot; next_build_prefix[nn] = totb;
+    next_meta[0] = nn; next_meta[1] = tot; next_meta[2] = totb;
+  }
+}
+
 __device__ void plan_body(
     const Node* __restrict__ nodes, const int* __restrict__ meta, Dec* __restrict__ dec,
     int* __restrict__ node_nl, const int* __restrict__ prev_nl, int4* __restrict__ curs,
@@ -1930,6 +2022,12 @@ __device__ void plan_body(
       reduce_node(pr.cand, node, pr.F, pr.feat_ok, pr.k_cols, pr.seed, depth, dec, pr.node_ok, pr.fgroup, tid & 63,
                   pr.cfs, pr.ccap);
     __syncthreads();                     // the block's own decisions (global) before the plan reads them
+  }
+  if (n <= 64 && !pr.no_wave) {       // small level: wave 0 alone (the other waves are done)
+    if (tid < 64)
+      plan_wave(nodes, n, dec, node_nl, prev_nl, curs, child_l, child_r, next, next_tile_prefix, next_meta,
+                next_build_prefix, counters, depth, max_depth, min_w, cap_next, leaf_cap);
+    return;
   }
   const bool odd = depth & 1;
   int total;
@@ -3201,10 +3299,17 @@ int h2o_ic_next(const void* next, const void* next_meta, const void* dec, const 
   return (int)hipGetLastError();
 }
 
+static int plan_wave_off() {
+  static int v = -1;
+  if (v < 0) { const char* e = getenv("H2O_PLAN_WAVE"); v = (e && e[0] == '0') ? 1 : 0; }
+  return v;
+}
+
 static int plan_launch(const void* nodes, const void* meta, void* dec, void* node_nl, const void* prev_nl, void* curs,
                        void* child_l, void* child_r, void* next, void* next_tile_prefix, void* next_meta,
                        void* next_build_prefix, void* counters, void* scratch, int depth, int max_depth, double min_w,
                        int cap_next, int leaf_cap, PlanReduce pr, hipStream_t s) {
+  pr.no_wave = plan_wave_off();
   hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, s, (const Node*)nodes, (const int*)meta, (Dec*)dec,
                      (int*)node_nl, (const int*)prev_nl, (int4*)curs, (int*)child_l, (int*)child_r, (Node*)next,
                      (int*)next_tile_prefix, (int*)next_meta, (int*)next_build_prefix, (int*)counters, (int*)scratch,

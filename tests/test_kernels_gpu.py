@@ -170,6 +170,40 @@ def test_fused_adadelta_matches_reference():
     assert torch.allclose(fc.eg2, fg.eg2.cpu(), atol=1e-9, rtol=1e-4)
 
 
+@pytest.mark.parametrize("wt_dtype", [torch.bfloat16, torch.float32])
+def test_tiled_adadelta_with_transposed_copy(wt_dtype):
+    """k_adadelta_tiles (64 x 64 weight tiles through LDS): master weights, bf16 shadow and the transposed copy of
+    every layer (edge tiles included) against the fp32 reference update."""
+    import numpy as np
+    from llama_github_io_amd.ops.dense import FlatParams
+    torch.manual_seed(1)
+    dims = [100, 70, 130, 3]
+    lins = [torch.nn.Linear(a, b) for a, b in zip(dims[:-1], dims[1:])]
+    fc, fg = FlatParams(torch.nn.Sequential(*lins)), FlatParams(torch.nn.Sequential(*[
+        torch.nn.Linear(a, b) for a, b in zip(dims[:-1], dims[1:])]).to(dev))
+    fg.p.copy_(fc.p.to(dev))
+    offs, o = [], 0
+    for a, b in zip(dims[:-1], dims[1:]):
+        offs.append(o)
+        o += a * b
+    assert o == fc.n_decay
+    wt = torch.zeros(fc.n_decay, dtype=wt_dtype, device=dev)
+    shadow = torch.zeros(fc.n_decay, dtype=torch.bfloat16, device=dev)
+    wmap = (wt, np.array(offs + [o], np.int64), np.array(dims[:-1], np.int32), np.array(dims[1:], np.int32))
+    for it in range(3):
+        gr = torch.randn(fc.g.numel(), generator=torch.Generator().manual_seed(it))
+        fc.g.copy_(gr)
+        fg.g.copy_(gr.to(dev))
+        fc.adadelta(0.99, 1e-8, l1=1e-4, l2=1e-3)
+        fg.adadelta(0.99, 1e-8, l1=1e-4, l2=1e-3, shadow=shadow, wt=wmap)
+    assert torch.allclose(fc.p, fg.p.cpu(), atol=1e-6, rtol=1e-5)
+    assert torch.allclose(fc.edx2, fg.edx2.cpu(), atol=1e-9, rtol=1e-4)
+    assert torch.equal(shadow.cpu(), fg.p[:o].cpu().bfloat16())
+    for l, (a, b) in enumerate(zip(dims[:-1], dims[1:])):
+        W = fg.p[offs[l]:offs[l] + a * b].view(b, a)
+        assert torch.equal(wt[offs[l]:offs[l] + a * b].view(a, b).cpu(), W.t().to(wt_dtype).cpu()), l
+
+
 @pytest.mark.parametrize("n,C", [(7, 0), (5000, 0), (9, 13), (3000, 4)])
 def test_segment_sum_paths(n, C):
     from llama_github_io_amd.ops.segment import segment_sum
