@@ -22,7 +22,7 @@ and the two login paths of Jetty's LdapLoginModule:
 The LDAPv3 client is a small BER codec over a socket (RFC 4511 BindRequest / SearchRequest, simple authentication);
 no LDAP library is in the image. ``useLdaps="true"`` wraps the socket in TLS with certificate and host-name
 verification against the system trust store, or against the CA bundle named by the extra option ``caFile``.
-Kerberos / SPNEGO / PAM stay refused.
+Kerberos / SPNEGO stay refused (PAM: :mod:`.pam`).
 """
 from __future__ import annotations
 
@@ -187,7 +187,8 @@ def parse_jaas(text: str) -> dict:
         head = re.match(r"\s*([\w.$]+)\s+(required|requisite|sufficient|optional)\b", body)
         if not head:
             continue
-        opts = dict(re.findall(r'(\w+)\s*=\s*"([^"]*)"', body[head.end():]))
+        opts = {k: (q if q or not u else u) for k, q, u in
+                re.findall(r'(\w+)\s*=\s*(?:"([^"]*)"|([^\s;"]+))', body[head.end():])}
         out[m.group(1)] = dict(opts, module=head.group(1), flag=head.group(2))
     return out
 

@@ -15,8 +15,9 @@ Reference behaviour (re-expressed for the FastAPI server, no Jetty):
 The realm file is Jetty's PropertyUserStore format, ``user: credential[, role ...]`` (``#`` comments), with a
 credential in plain text or Jetty's ``OBF:`` / ``MD5:`` / ``CRYPT:`` forms (``h2o-assemblies/main/tests/python/
 realm.properties`` is a plain one). ``-ldap_login -login_conf <JAAS file>`` authenticates against an LDAP server with
-Jetty LdapLoginModule's semantics (:mod:`.ldap`). Kerberos / PAM / SPNEGO need JAAS modules, a KDC or the host's PAM
-stack, which this image does not have: they are refused at startup with that reason.
+Jetty LdapLoginModule's semantics (:mod:`.ldap`); ``-pam_login`` through the host's libpam as h2o-jaas-pam's
+PamLoginModule (:mod:`.pam`). Kerberos / SPNEGO need a KDC and JAAS Krb5 modules, which this image does not have:
+they are refused at startup with that reason.
 """
 from __future__ import annotations
 
@@ -143,22 +144,24 @@ class LoginConfig:
                              "with of a LoginService.")
         if self.session_timeout and not self.form_auth:
             raise ValueError("Session timeout can only be enabled for Form based authentication (use -form_auth)")
-        if self.kerberos_login or self.spnego_login or self.pam_login:
-            raise ValueError("Kerberos / SPNEGO / PAM logins need JAAS login modules and their servers, which "
-                             "this build does not include; use -hash_login or -ldap_login")
-        if self.ldap_login:
-            from .ldap import LdapLoginService
-            LdapLoginService(self.login_conf)        # a malformed JAAS config fails at startup, not at first login
+        if self.kerberos_login or self.spnego_login:
+            raise ValueError("Kerberos / SPNEGO logins need a KDC and JAAS Krb5 modules, which this build does not "
+                             "include; use -hash_login, -ldap_login or -pam_login")
+        if self.ldap_login or self.pam_login:
+            self.service()                          # a malformed JAAS config fails at startup, not at first login
         return self
 
     @property
     def enabled(self) -> bool:
-        return self.hash_login or self.ldap_login
+        return self.hash_login or self.ldap_login or self.pam_login
 
     def service(self):
         if self.ldap_login:
             from .ldap import LdapLoginService
             return _CachedLogin(LdapLoginService(self.login_conf))
+        if self.pam_login:
+            from .pam import PamLoginService
+            return _CachedLogin(PamLoginService(self.login_conf))
         return HashLoginService(self.login_conf)
 
 

@@ -105,7 +105,7 @@ def test_login_option_rules(tmp_path):
         L(hash_login=True, login_conf=realm, session_timeout=3).validate()
     with pytest.raises(ValueError, match="File does not exist"):
         L(hash_login=True, login_conf=str(tmp_path / "missing")).validate()
-    with pytest.raises(ValueError, match="JAAS"):
+    with pytest.raises(ValueError, match="JAAS|KDC"):
         L(kerberos_login=True, login_conf=realm).validate()
     with pytest.raises(ValueError, match="JAAS"):            # a realm file is not a JAAS LDAP config
         L(ldap_login=True, login_conf=realm).validate()
