@@ -873,6 +873,7 @@ class DeepLearningTrainer:
                 Xv, yv, wv, ov = valid
                 model.output["validation_metrics"] = model.metrics_for(Xv, yv, wv, ov)
         model.output["phase_seconds"]["final_metrics"] = time.time() - t_fm
+        self._score_rows = None
         # Gedeon variable importance from the first layer weights
         W1 = net.hidden[0].weight.detach().abs() if net.hidden else net.out.weight.detach().abs()
         imp = W1.sum(0).double()
@@ -1033,16 +1034,21 @@ class DeepLearningTrainer:
             from ..parallel import collectives as _c
             u = _c.row_uniform(int(p.get("seed") or 0), 0x5C0BE, r0, N, X.device)
             idx = torch.nonzero(u < n / Ng).squeeze(1)
+        # the sampled rows are gathered once per fit (X, y and w do not change while it trains)
+        samp = getattr(self, "_score_rows", None)
+        if samp is None or samp[0] != key or samp[1] != (X.data_ptr(), tuple(X.shape)):
+            samp = (key, (X.data_ptr(), tuple(X.shape)), X[:, idx], None if y is None else y[idx], w[idx].float())
+            self._score_rows = samp
         self._score_idx = (key, idx)
-        Xs = X[:, idx]
+        Xs, ys, ws = samp[2], samp[3], samp[4]
         ev = dict(epochs=epochs, timestamp=time.time())
         if p["autoencoder"]:
             m = self._ae_metrics(model, Xs)
         else:
-            m = model.metrics_for(Xs, y[idx], w[idx].float())
+            m = model.metrics_for(Xs, ys, ws)
             if self._dist == "huber" and hasattr(self, "_hdelta"):
                 from .quantile import weighted_quantiles
-                r = (y[idx].double() - model._predict_tensor(Xs).reshape(-1).double()).abs()
+                r = (ys.double() - model._predict_tensor(Xs).reshape(-1).double()).abs()
                 dq = float(weighted_quantiles(r, [float(p["huber_alpha"])], w=w[idx])[0])
                 if math.isfinite(dq):
                     self._hdelta.fill_(dq)
