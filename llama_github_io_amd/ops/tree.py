@@ -868,6 +868,8 @@ class GpuTreeBuilder:
         npre = int(os.environ.get("H2O_TREE_SNAP_POOL", "8")) if dev.type == "cuda" else 0
         self._pinned_pool = [torch.empty(self.arena.numel(), dtype=torch.uint8, pin_memory=True) for _ in range(npre)]
         self._event_pool = [torch.cuda.Event() for _ in range(npre)]
+        self._decoded = []      # trees decoded early by a bounded-lookahead wait (_snapshot), handed out first
+        self._snap_wait = npre > 0 and os.environ.get("H2O_TREE_SNAP_WAIT", "1") == "1"
         # raw device pointers resolved once: the per-tree launch sequence is ~45 ctypes calls and at small
         # shards (1.375M rows/GPU) the host loop, not the GPU, set the pace (82 % busy, rocprofv3 trace)
         self._pt = {name: t.data_ptr() for name, t in self.av.items()}
@@ -1270,6 +1272,12 @@ class GpuTreeBuilder:
         # trees (pop_levels(ready_only=True)) while the GPU builds the next ones. MEASURED: moving the
         # device-to-host copy to a side stream (device staging ring + stream events) made the host block
         # in the launches (820 us/tree host, 1.09 vs 0.575 ms/tree at 1.375M rows): kept on the compute stream
+        if not self._pinned_pool and self.history and self._snap_wait:
+            # bounded lookahead: the host is a whole pool of trees ahead of the GPU. Wait for the OLDEST tree
+            # (the GPU still has the rest of the pool queued, so it does not idle) and decode it now, instead of
+            # a pinned allocation (hipHostMalloc serialises with the device: a GPU gap per tree once the host runs
+            # ahead — profiles/r6_final_tree_timeline_1375000.md). H2O_TREE_SNAP_WAIT=0: allocate as before.
+            self._decoded.extend(self._pop(1))
         host = self._pinned_pool.pop() if self._pinned_pool else torch.empty(self.arena.numel(), dtype=torch.uint8,
                                                                                pin_memory=True)
         dptr = self._snap_dev_ptr(host) if self.dev.type == "cuda" and _SNAP_KERNEL else 0
@@ -1300,8 +1308,12 @@ class GpuTreeBuilder:
     def pop_levels(self, ready_only: bool = False) -> list:
         """Decode built trees in build order: all of them, or (``ready_only``) the prefix whose snapshot
         copies have completed — never blocks in that mode."""
+        out, self._decoded = self._decoded, []
+        return out + self._pop(None, ready_only)
+
+    def _pop(self, limit, ready_only: bool = False) -> list:
         out = []
-        while self.history:
+        while self.history and (limit is None or len(out) < limit):
             host, ev = self.history[0]
             if ready_only and not ev.query():
                 break
