@@ -277,12 +277,14 @@ void* h2o_csv_parse(const char* buf, int64_t len, char sep, int header /*-1 gues
   nt = std::max(1, std::min(nt, 64));
   if (nrows < 20000) nt = 1;
   std::vector<std::thread> th;
+  // per-thread column tallies, summed after the join (the threads must not add into the shared Col counters)
+  std::vector<std::vector<int64_t>> ttext((size_t)nt, std::vector<int64_t>(nc, 0)), tnum((size_t)nt, std::vector<int64_t>(nc, 0));
   for (int t = 0; t < nt; ++t) {
     th.emplace_back([&, t]() {
       std::vector<int64_t> lco; std::vector<int32_t> lcl; std::vector<uint8_t> lcq;
       const int64_t lo = nrows * t / nt, hi = nrows * (t + 1) / nt;
-      int64_t ntext[256] = {0}, nnum[256] = {0};
-      std::vector<int64_t> vtext(nc, 0), vnum(nc, 0);
+      std::vector<int64_t>& vtext = ttext[(size_t)t];
+      std::vector<int64_t>& vnum = tnum[(size_t)t];
       for (int64_t r_ = lo; r_ < hi; ++r_) {
         int64_t ra, rb;
         rec_span(recs[r_ + row0], ra, rb);
@@ -300,11 +302,11 @@ void* h2o_csv_parse(const char* buf, int64_t len, char sep, int header /*-1 gues
           else { col->kind[r_] = 2; ++vtext[c]; }
         }
       }
-      (void)ntext; (void)nnum;
-      for (int c = 0; c < nc; ++c) { r->cols[c]->n_text += vtext[c]; r->cols[c]->n_num += vnum[c]; }
     });
   }
   for (auto& x : th) x.join();
+  for (int t = 0; t < nt; ++t)
+    for (int c = 0; c < nc; ++c) { r->cols[c]->n_text += ttext[(size_t)t][c]; r->cols[c]->n_num += tnum[(size_t)t][c]; }
   return r;
 }
 

@@ -40,8 +40,12 @@ def _beat(rank, world, store, stop):
                 if r == rank:
                     continue
                 try:
-                    v = json.loads(store.get(f"h2o_hb/{r}"))
-                    _state["last"][r] = v["t"]
+                    # check() first: a get() of a key the peer has not written yet BLOCKS in the store client for
+                    # its whole timeout, and a daemon thread parked in that C++ call at interpreter exit can abort
+                    # the process ("terminate called without an active exception")
+                    if store.check([f"h2o_hb/{r}"]):
+                        v = json.loads(store.get(f"h2o_hb/{r}"))
+                        _state["last"][r] = v["t"]
                 except Exception:  # noqa: BLE001 - peer has not written yet
                     v = None
                 t = _state["last"].get(r)
@@ -64,11 +68,13 @@ def start(interval: float = 1.0, timeout: float = 30.0) -> bool:
     if store is None or dist.get_world_size() < 2:
         return False
     _state.update(interval=float(interval), timeout=float(timeout), healthy=True, dead=[])
-    stop = threading.Event()
-    th = threading.Thread(target=_beat, args=(dist.get_rank(), dist.get_world_size(), store, stop), daemon=True,
+    ev = threading.Event()
+    th = threading.Thread(target=_beat, args=(dist.get_rank(), dist.get_world_size(), store, ev), daemon=True,
                           name="h2o-heartbeat")
-    _state["thread"], _state["stop"] = th, stop
+    _state["thread"], _state["stop"] = th, ev
     th.start()
+    import atexit
+    atexit.register(stop)            # join the thread before the store / process group are torn down
     return True
 
 
