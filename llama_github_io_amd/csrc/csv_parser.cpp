@@ -330,6 +330,7 @@ int h2o_csv_get(void* h, int c, double* num, uint8_t* kind, int64_t* off, int32_
   Result* r = (Result*)h;
   Col* col = r->cols[c];
   const size_t n = (size_t)r->nrows;
+  if (n == 0) return 0;                 // (empty vectors: data() may be null, and memcpy from null is undefined)
   if (num) std::memcpy(num, col->num.data(), n * sizeof(double));
   if (kind) std::memcpy(kind, col->kind.data(), n);
   if (off) std::memcpy(off, col->off.data(), n * sizeof(int64_t));
