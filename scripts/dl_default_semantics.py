@@ -65,20 +65,24 @@ def logloss(ps, X, y):
     return float(-np.log(np.clip(p, 1e-15, 1)).mean())
 
 
-def train_one_epoch(X, y, B, H, rho=0.99, eps=1e-8, seed=1):
+def train_one_epoch(X, y, B, H, rho=0.99, eps=1e-8, seed=1, stale=1):
+    """stale = S > 1: S consecutive B-row mini-batches take their gradients at the SAME weights, then the S ADADELTA
+    updates apply in order (Hogwild-style staleness of up to S - 1 updates: what S concurrent row streams do)."""
     ps = init(X.shape[1], H, seed)
     Eg = [np.zeros_like(p) for p in ps]
     Ed = [np.zeros_like(p) for p in ps]
     perm = np.random.default_rng(seed + 7).permutation(X.shape[0])
-    for s in range(0, X.shape[0] - B + 1, B):
-        idx = perm[s:s + B]
-        for p, g, e, d in zip(ps, grads(ps, X[idx], y[idx]), Eg, Ed):
-            e *= rho
-            e += (1 - rho) * g * g
-            rate = np.sqrt((d + eps) / (e + eps))
-            d *= rho
-            d += (1 - rho) * rate * rate * g * g
-            p -= rate * g
+    starts = list(range(0, X.shape[0] - B + 1, B))
+    for k in range(0, len(starts), stale):
+        gs = [grads(ps, X[perm[s:s + B]], y[perm[s:s + B]]) for s in starts[k:k + stale]]
+        for gl in gs:
+            for p, g, e, d in zip(ps, gl, Eg, Ed):
+                e *= rho
+                e += (1 - rho) * g * g
+                rate = np.sqrt((d + eps) / (e + eps))
+                d *= rho
+                d += (1 - rho) * rate * rate * g * g
+                p -= rate * g
     return ps
 
 
@@ -88,14 +92,15 @@ def main():
     ap.add_argument("--batches", default="1,2,4,8,16,64,256")
     ap.add_argument("--feat", type=int, default=100)
     ap.add_argument("--hidden", type=int, default=32)
+    ap.add_argument("--stale", default="1", help="comma list of S: gradients of S mini-batches at the same weights")
     a = ap.parse_args()
     Xh, yh = data(20000, a.feat, 99)
     for n in [int(v) for v in a.rows.split(",")]:
         X, y = data(n, a.feat, 0)
-        for B in [int(v) for v in a.batches.split(",")]:
+        for B, S in [(int(v), int(s_)) for v in a.batches.split(",") for s_ in a.stale.split(",")]:
             t0 = time.time()
-            ps = train_one_epoch(X, y, B, a.hidden)
-            print(json.dumps(dict(rows=n, batch=B, steps=n // B, train_logloss=round(logloss(ps, X, y), 5),
+            ps = train_one_epoch(X, y, B, a.hidden, stale=S)
+            print(json.dumps(dict(rows=n, batch=B, stale=S, steps=n // B, train_logloss=round(logloss(ps, X, y), 5),
                                   holdout_logloss=round(logloss(ps, Xh, yh), 5), seconds=round(time.time() - t0, 1))),
                   flush=True)
 
