@@ -38,6 +38,7 @@ NBW = 32            # 32-bit words of a decision bitset: 1024 bins (a wide-categ
 DEC_DT = np.dtype([("feat", "<i4"), ("bin", "<i4"), ("na_left", "<i4"), ("is_cat", "<i4"), ("bits", "<u4", (NBW,)),
                    ("gain", "<f8"), ("wl", "<f8"), ("wr", "<f8"), ("predl", "<f4"), ("predr", "<f4")])
 CAND_BYTES = 184
+_GRAPH_CACHE = 16          # captured per-tree graphs kept (one per launch-plan signature)
 GROUP_CAT = 2       # Dec.is_cat of a wide-categorical group split: bin = the group's packed 'elsewhere' bytes
 MODE_SE, MODE_NEWTON, MODE_RANDOM = 0, 1, 2
 # histogram types as candidate lattices over the global bins (k_split_find HT_*)
@@ -1234,8 +1235,9 @@ class GpuTreeBuilder:
     def _graph_replay(self, P, k_cols) -> bool:
         """The whole tree as ONE hipGraph launch: the native sequence (h2o_tree_all, ~30 kernels) is captured once
         into a torch.cuda.CUDAGraph and replayed for every tree whose launch plan is byte-identical (kernel arguments
-        are baked in at capture: the plan struct is the signature; the seed only when a kernel reads it). A plan that
-        changes every tree (e.g. learn_rate_annealing in the leaf values) stops the capture after 3 misses.
+        are baked in at capture: the plan struct is the signature; the seed only when a kernel reads it). Up to 16 plans
+        keep their graphs (the K classes of a multinomial model share one); a plan that changes every tree (e.g. learn_rate_annealing in the
+        leaf values) stops the capture after 16 new signatures without a replay.
         ``H2O_TREE_GRAPH=0``: direct launches."""
         if self.dev.type != "cuda" or os.environ.get("H2O_TREE_GRAPH", "1") == "0" or self.__dict__.get("_graph_off"):
             return False
@@ -1244,13 +1246,16 @@ class GpuTreeBuilder:
             P.seed = 0
         sig = bytes(P)
         P.seed = seed
-        g = self.__dict__.get("_graph")
-        if g is None or self.__dict__.get("_graph_sig") != sig:
-            misses = self.__dict__.get("_graph_misses", 0) + (g is not None)
+        # one graph per plan signature (plans that alternate between trees keep theirs): up to _GRAPH_CACHE of them;
+        # a run of new signatures with no replay in between (the plan changes every tree) turns capture off
+        cache = self.__dict__.setdefault("_graphs", {})
+        g = cache.get(sig)
+        if g is None:
+            misses = self.__dict__.get("_graph_misses", 0) + 1
             self._graph_misses = misses
-            if misses >= 3:
+            if misses > _GRAPH_CACHE:
                 self._graph_off = True
-                self._graph = None
+                cache.clear()
                 return False
             g = torch.cuda.CUDAGraph()
             try:
@@ -1258,13 +1263,15 @@ class GpuTreeBuilder:
                     rc = self.lib.h2o_tree_all(ctypes.byref(P), nat.stream_ptr(self.dev))
             except Exception:          # noqa: BLE001 - capture refused by the runtime: launch directly from now on
                 self._graph_off = True
-                self._graph = None
+                cache.clear()
                 return False
             nat.check(rc, "tree_all (capture)")
-            self._graph, self._graph_sig = g, sig
+            if len(cache) >= _GRAPH_CACHE:
+                cache.pop(next(iter(cache)))
+            cache[sig] = g
         else:
             self._graph_misses = 0
-        self._graph.replay()
+        g.replay()
         return True
 
     def _snapshot(self):

@@ -702,3 +702,22 @@ def test_dl_trainer_autoencoder_runs_fused(monkeypatch):
     assert res["1"].output["training_step_fused_mfma"] and not res["0"].output["training_step_fused_mfma"]
     e1, e0 = res["1"].output["training_metrics"]["MSE"], res["0"].output["training_metrics"]["MSE"]
     assert e1 < 0.5 and abs(e1 - e0) < 0.25 * max(e0, e1), (e1, e0)
+
+
+def test_tree_graph_replay_per_class_plans(monkeypatch):
+    """Per-tree graph replay on a 3-class multinomial GBM (the classes share one launch plan, so one captured graph
+    serves every tree): the trees equal the direct-launch ones exactly."""
+    from llama_github_io_amd.models.gbm import GBMTrainer
+    g = torch.Generator(device=dev).manual_seed(9)
+    N, F = 30000, 5
+    X = torch.randn(F, N, device=dev, generator=g)
+    y = (X[0] > 0.3).float() + (X[1] + X[2] > 0.5).float()
+    params = dict(ntrees=6, max_depth=4, seed=4, distribution="multinomial")
+    monkeypatch.setenv("H2O_TREE_GRAPH", "1")
+    tr = GBMTrainer(dict(params))
+    a = tr.fit(X, y, None, None, _info(F, ("0", "1", "2")))
+    gb = getattr(tr.builder, "inner", tr.builder)
+    assert 1 <= len(gb._graphs) <= 3 and not gb.__dict__.get("_graph_off")
+    monkeypatch.setenv("H2O_TREE_GRAPH", "0")
+    b = GBMTrainer(dict(params)).fit(X, y, None, None, _info(F, ("0", "1", "2")))
+    assert torch.equal(a.score_tensor(X).cpu(), b.score_tensor(X).cpu())
