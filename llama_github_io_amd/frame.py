@@ -1154,7 +1154,8 @@ class H2OFrame:
         sharded = self._shard is not None
         if sharded:
             from .parallel import collectives as coll
-            row0 = coll.row_offset(self.nrows)
+            n_local = int(next(iter(self._cols.values())).data.shape[0])     # this rank's rows (nrows is global)
+            row0 = coll.row_offset(n_local)
 
         def full(t):
             return dframe.gather_tensor(t) if sharded else t
@@ -1189,7 +1190,7 @@ class H2OFrame:
                 fill = s / k
             filled = torch.where(ok, v, fill[inv])
             if sharded:
-                filled = filled[row0:row0 + self.nrows]
+                filled = filled[row0:row0 + n_local]
             if c.type == "enum":
                 c.data = torch.where(torch.isnan(filled), -1, filled).to(c.data.dtype)
             else:

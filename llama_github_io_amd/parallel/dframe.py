@@ -301,7 +301,7 @@ PLAIN = {
     "nrows", "nrow", "ncols", "ncol", "shape", "dim", "types", "dtypes", "type", "columns_by_type", "__len__", "_col",
     "_resolve", "set_names", "set_name", "rename", "__getitem__", "_rows", "__setitem__", "__delitem__", "drop", "pop",
     "__repr__", "show", "isfactor", "isnumeric", "isstring", "levels", "nlevels", "_num", "_reduce", "mean", "sum",
-    "max", "min", "sd", "std", "var", "nacnt", "any", "all", "summary", "describe", "asfactor", "impute", "scale",
+    "max", "min", "sd", "std", "var", "nacnt", "any", "all", "summary", "describe", "asfactor", "impute", "_impute_by", "scale",
     "split_frame", "runif", "kfold_column", "modulo_kfold_column", "head", "tail", "refresh", "key", "__iter__",
     "__contains__", "__hash__", "__eq__", "__ne__", "__lt__", "__le__", "__gt__", "__ge__", "__and__", "__or__",
     "__add__", "__radd__", "__sub__", "__rsub__", "__mul__", "__rmul__", "__truediv__", "__rtruediv__",

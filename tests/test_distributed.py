@@ -359,3 +359,60 @@ def test_exchange_rows_range_partition(world):
         for sr in set(src):
             ids = [r[1] for r in part if int(r[1]) // 1000 == sr]
             assert ids == sorted(ids)                   # source order kept
+
+
+def _impute_worker(rank, world, port, csv, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), H2O_AMD_DEVICE="cpu", OMP_NUM_THREADS="1")
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import h2o
+    import torch.distributed as dist
+    h2o.init()
+    try:
+        fr = h2o.import_file(csv)
+        assert fr._shard is not None
+        fr.impute("x", "mean", by=["g", "h"])
+        fr.impute("e", "mode", by=["h"])
+        df = fr.as_data_frame()
+        if rank == 0:
+            q.put(dict(x=df["x"].tolist(), e=df["e"].astype(str).tolist()))
+    finally:
+        if dist.is_initialized():
+            dist.barrier()
+            dist.destroy_process_group()
+
+
+def test_sharded_group_impute_equals_single(tmp_path):
+    """h2o.impute with groupByCols on a row-sharded frame (gloo world 2): the key / target columns are gathered,
+    aggregated once, and each rank fills its own rows — equal to the single-process result."""
+    import socket
+    import pandas as pd
+    rng = np.random.default_rng(11)
+    n = 2000
+    df = pd.DataFrame({"g": rng.choice(["a", "b", "c"], n), "h": rng.integers(0, 3, n),
+                       "x": rng.normal(size=n).round(4), "e": rng.choice(["u", "v", "w"], n)})
+    df.loc[rng.random(n) < 0.2, "x"] = np.nan
+    df.loc[rng.random(n) < 0.2, "e"] = None
+    csv = tmp_path / "imp.csv"
+    df.to_csv(csv, index=False)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_impute_worker, args=(r, 2, port, str(csv), q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = q.get(timeout=300)
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    from llama_github_io_amd.frame import H2OFrame
+    single = H2OFrame(pd.read_csv(csv), destination_frame="imp_single")
+    single["g"] = single["g"].asfactor() if single.type("g") != "enum" else single["g"]
+    single.impute("x", "mean", by=["g", "h"])
+    single.impute("e", "mode", by=["h"])
+    sd = single.as_data_frame()
+    np.testing.assert_allclose(np.asarray(out["x"], dtype=float), sd["x"].to_numpy(dtype=float), rtol=1e-12)
+    assert out["e"] == sd["e"].astype(str).tolist()
