@@ -150,9 +150,10 @@ struct IrlsOut {
   float* wi;
   float* zi;
 };
-__device__ __forceinline__ void irls_row(const IrlsOut& io, int64_t row, double e, double o) {
+__device__ __forceinline__ void irls_eval(int fam, int link, double e, double o, double y, double w, float& wi,
+                                          float& zi) {
   double mu, gp;
-  switch (io.link) {
+  switch (link) {
     case 1: {
       mu = 1.0 / (1.0 + exp(-e));
       const double m = fmin(fmax(mu, 1e-10), 1.0 - 1e-10);
@@ -170,14 +171,88 @@ __device__ __forceinline__ void irls_row(const IrlsOut& io, int64_t row, double 
     default: mu = e; gp = 1.0;
   }
   double var;
-  switch (io.fam) {
+  switch (fam) {
     case 1: { const double m = fmin(fmax(mu, 1e-10), 1.0 - 1e-10); var = m * (1.0 - m); break; }
     case 2: var = fmax(mu, 1e-10); break;
     case 3: var = fmax(mu * mu, 1e-20); break;
     default: var = 1.0;
   }
-  io.wi[row] = (float)(io.w[row] / fmax(var * gp * gp, 1e-30));
-  io.zi[row] = (float)(e - o + (io.y[row] - mu) * gp);
+  wi = (float)(w / fmax(var * gp * gp, 1e-30));
+  zi = (float)(e - o + (y - mu) * gp);
+}
+__device__ __forceinline__ void irls_row(const IrlsOut& io, int64_t row, double e, double o) {
+  irls_eval(io.fam, io.link, e, o, io.y[row], io.w[row], io.wi[row], io.zi[row]);
+}
+
+// The IRLS pass fused into the Gram pass, for designs whose augmented rows fit one 64-column tile
+// (P + 1 <= 64: a wave already holds whole rows of Z for k_gram's diagonal tile). Per batch of 16 rows each
+// lane has the fp64 partial x.beta of its 2 columns for 8 row slots; a butterfly reduce-scatter over the
+// 32 lanes of a row half (xor 16 / 8 / 4 keep half the slots each, xor 2 / 1 finish) leaves lane l with
+// the full eta of slot (l >> 2) & 7 — 9 fp64 shuffles instead of 40, and one exp per lane instead of 8.
+// That lane evaluates irls_eval for its row; wi and zi go back to the slot's 32 lanes by 16 fp32
+// shuffles, zi lands in column P (the u column), and the MFMAs of k_gram's diagonal tile follow. The
+// separate k_zbeta IRLS pass (a second full read of Z plus wi / zi round trips) disappears.
+__global__ __launch_bounds__(64) void k_gram_irls(const float* __restrict__ Z, int64_t ldz,
+                                                  const double* __restrict__ beta, const double* __restrict__ off,
+                                                  IrlsOut io, int64_t N, int P, int64_t rows_per_split,
+                                                  float* __restrict__ slabs) {
+  const int64_t r_begin = (int64_t)blockIdx.y * rows_per_split;
+  const int64_t r_end = min(N, r_begin + rows_per_split);
+  const int lane = threadIdx.x;
+  const int c = lane & 31, kh = lane >> 5;
+  const int s_me = (lane >> 2) & 7;
+  const int b4 = (lane >> 4) & 1, b3 = (lane >> 3) & 1, b2 = (lane >> 2) & 1;
+  const double be0 = c < P ? beta[c] : 0.0, be1 = 32 + c < P ? beta[32 + c] : 0.0;
+  f32x16 a00, a01, a11;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) { a00[k] = 0.f; a01[k] = 0.f; a11[k] = 0.f; }
+  for (int64_t base = r_begin; base < r_end; base += 16) {
+    float x0[8], x1[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int64_t r = base + 2 * q + kh;
+      const bool ok = r < r_end;
+      x0[q] = ok && c < P ? Z[r * ldz + c] : 0.f;
+      x1[q] = ok && 32 + c < P ? Z[r * ldz + 32 + c] : 0.f;
+    }
+    const int64_t rm = base + 2 * s_me + kh;
+    const bool okm = rm < r_end;
+    const int64_t rmc = okm ? rm : r_begin;
+    const double ym = io.y[rmc], wm = io.w[rmc], om = off ? off[rmc] : 0.0;
+    double p[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) p[q] = (double)x0[q] * be0 + (double)x1[q] * be1;
+    double p4[4], p2[2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) p4[i] = (b4 ? p[4 + i] : p[i]) + __shfl_xor(b4 ? p[i] : p[4 + i], 16, 64);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) p2[i] = (b3 ? p4[2 + i] : p4[i]) + __shfl_xor(b3 ? p4[i] : p4[2 + i], 8, 64);
+    double e = (b2 ? p2[1] : p2[0]) + __shfl_xor(b2 ? p2[0] : p2[1], 4, 64);
+    e += __shfl_xor(e, 2, 64);
+    e += __shfl_xor(e, 1, 64);
+    float wim = 0.f, zim = 0.f;
+    if (okm) irls_eval(io.fam, io.link, e + om, om, ym, wm, wim, zim);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int src = (kh << 5) | (q << 2);
+      const float wq = __shfl(wim, src, 64), zq = __shfl(zim, src, 64);
+      if (c == P) x0[q] = zq;
+      if (32 + c == P) x1[q] = zq;
+      const float wa0 = wq * x0[q], wa1 = wq * x1[q];
+      a00 = __builtin_amdgcn_mfma_f32_32x32x2f32(wa0, x0[q], a00, 0, 0, 0);
+      a01 = __builtin_amdgcn_mfma_f32_32x32x2f32(wa0, x1[q], a01, 0, 0, 0);
+      a11 = __builtin_amdgcn_mfma_f32_32x32x2f32(wa1, x1[q], a11, 0, 0, 0);
+    }
+  }
+  float* out = slabs + (size_t)blockIdx.y * TILE * TILE;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int rr = (k & 3) + 8 * (k >> 2) + 4 * kh;
+    out[(size_t)rr * TILE + c] = a00[k];
+    out[(size_t)rr * TILE + 32 + c] = a01[k];
+    out[(size_t)(32 + rr) * TILE + 32 + c] = a11[k];
+    out[(size_t)(32 + c) * TILE + rr] = a01[k];
+  }
 }
 #ifndef ZB_LDS_FLOATS
 #define ZB_LDS_FLOATS 12288    // 48 KiB of Z per block
@@ -323,6 +398,19 @@ int h2o_irls_wz(const float* Z, long long ldz, const double* B, long long N, int
   const long long grid = (N + TR - 1) / TR;
   hipLaunchKernelGGL(k_zbeta, dim3((unsigned)grid), dim3(ZB_THREADS), 0, stream, Z, (int64_t)ldz, B, 1, (int64_t)N, P,
                      TR, off, (double*)nullptr, IrlsOut{fam, link, y, w, wi, zi});
+  return (int)hipGetLastError();
+}
+
+// Fused IRLS + augmented Gram (k_gram_irls): slabs fp32 [S, 64, 64] of [Z zi]ᵀ diag(wi) [Z zi] with wi / zi
+// evaluated in the pass (beta fp64 [P], off / y / w fp64 [N]); P + 1 <= 64 only.
+int h2o_gram_irls(const float* Z, long long ldz, const double* B, long long N, int P, const double* off,
+                  const double* y, const double* w, int fam, int link, int S, float* slabs, hipStream_t stream) {
+  if (N <= 0) return 0;
+  if (P <= 0 || P + 1 > TILE || ldz < P || S <= 0 || fam < 0 || fam > 3 || link < 0 || link > 3)
+    return (int)hipErrorInvalidValue;
+  const long long rps = ((N + S - 1) / S + 1) / 2 * 2;
+  hipLaunchKernelGGL(k_gram_irls, dim3(1, S), dim3(64), 0, stream, Z, (int64_t)ldz, B, off,
+                     IrlsOut{fam, link, y, w, nullptr, nullptr}, (int64_t)N, P, (int64_t)rps, slabs);
   return (int)hipGetLastError();
 }
 

@@ -815,14 +815,18 @@ class GLMTrainer:
             if p.get("cold_start") and li > 0:     # cold_start: every lambda starts from the initial coefficients
                 beta = beta_start.clone()
             for it in range(max(max_it, 1)):
-                wz = G.irls_wz(Zi, beta, off, y, w, fam.name, fam.link)   # fused: one pass, fp32 wi / zi
-                if wz is None:
-                    eta = G.zbeta(Zi, beta, off)
-                    mu = fam.linkinv(eta)
-                    gp = fam.dlink(mu)
-                    var = fam.variance(mu)
-                    wz = ((w / (var * gp * gp).clamp(min=1e-30)).float(), (eta - off + (y - mu) * gp).float())
-                Gm, r = G.gram(Zi, wz[0], wz[1])      # one pass: Zᵀ W Z and Zᵀ W z
+                # one pass over Z: eta / wi / zi evaluated inside the augmented Gram pass (P + 1 <= 64)
+                gr = G.gram_irls(Zi, beta, off, y, w, fam.name, fam.link)
+                if gr is None:
+                    wz = G.irls_wz(Zi, beta, off, y, w, fam.name, fam.link)   # fused: one pass, fp32 wi / zi
+                    if wz is None:
+                        eta = G.zbeta(Zi, beta, off)
+                        mu = fam.linkinv(eta)
+                        gp = fam.dlink(mu)
+                        var = fam.variance(mu)
+                        wz = ((w / (var * gp * gp).clamp(min=1e-30)).float(), (eta - off + (y - mu) * gp).float())
+                    gr = G.gram(Zi, wz[0], wz[1])      # one pass: Zᵀ W Z and Zᵀ W z
+                Gm, r = gr
                 if coll.is_dist():
                     Gm = coll.all_reduce_(Gm)
                     r = coll.all_reduce_(r)

@@ -19,6 +19,8 @@ nat.register_hip_signatures({
                   nat.c_void_p],
     "h2o_irls_wz": [nat.c_void_p, nat.c_ll, nat.c_void_p, nat.c_ll, nat.c_int, nat.c_void_p, nat.c_void_p, nat.c_void_p,
                     nat.c_int, nat.c_int, nat.c_void_p, nat.c_void_p, nat.c_void_p],
+    "h2o_gram_irls": [nat.c_void_p, nat.c_ll, nat.c_void_p, nat.c_ll, nat.c_int, nat.c_void_p, nat.c_void_p,
+                      nat.c_void_p, nat.c_int, nat.c_int, nat.c_int, nat.c_void_p, nat.c_void_p],
 })
 
 # glm.Family -> the k_zbeta IRLS epilogue's codes (csrc/gram_kernels.hip IrlsOut)
@@ -47,6 +49,31 @@ def irls_wz(Z: torch.Tensor, beta: torch.Tensor, off, y: torch.Tensor, w: torch.
                  0 if od is None else od.data_ptr(), yd.data_ptr(), wd.data_ptr(), _IRLS_FAM[family], _IRLS_LINK[link],
                  wi.data_ptr(), zi.data_ptr(), nat.stream_ptr(Z.device))
     return wi, zi
+
+
+def gram_irls(Z: torch.Tensor, beta: torch.Tensor, off, y: torch.Tensor, w: torch.Tensor, family: str, link: str):
+    """One IRLS iteration's (Zᵀ W Z, Zᵀ W z) in ONE pass over Z (``k_gram_irls``: eta, mu, g'(mu), V(mu) per row
+    inside the Gram pass) — or None where not covered (CPU, family / link outside the epilogue, P + 1 > 64,
+    ``H2O_GLM_GRAM_IRLS=0``); the caller then runs ``irls_wz`` + ``gram``. Same formulas as ``irls_wz``."""
+    if (not Z.is_cuda or family not in _IRLS_FAM or link not in _IRLS_LINK or beta.dim() != 1
+            or Z.shape[1] + 1 > 64 or os.environ.get("H2O_GLM_GRAM_IRLS", "0") == "0"
+            or os.environ.get("H2O_GLM_FUSED_IRLS", "1") == "0"):
+        return None
+    N, P = Z.shape
+    Z = Z.contiguous().float()
+    od = None
+    if off is not None:
+        od = (off if torch.is_tensor(off) else torch.full((N,), float(off), device=Z.device)).double()
+        od = (od.expand(N) if od.numel() == 1 else od).contiguous()
+    yd, wd = y.contiguous().double(), w.contiguous().double()
+    S = _splits(N, 1)
+    slabs = torch.zeros(S, 64, 64, dtype=torch.float32, device=Z.device)
+    if N > 0:
+        nat.call("h2o_gram_irls", Z.data_ptr(), P, beta.contiguous().double().data_ptr(), N, P,
+                 0 if od is None else od.data_ptr(), yd.data_ptr(), wd.data_ptr(), _IRLS_FAM[family],
+                 _IRLS_LINK[link], S, slabs.data_ptr(), nat.stream_ptr(Z.device))
+    G = slabs.sum(0, dtype=torch.float64)
+    return G[:P, :P].contiguous(), G[:P, P].contiguous()
 
 
 def zbeta(Z: torch.Tensor, B: torch.Tensor, off=None) -> torch.Tensor:
