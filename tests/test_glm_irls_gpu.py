@@ -62,8 +62,9 @@ def test_glm_fit_fused_equals_torch_chain(monkeypatch):
 
 @pytest.mark.parametrize("fam,link", CASES)
 @pytest.mark.parametrize("P", [13, 37, 63])
-def test_gram_irls_matches_two_pass(fam, link, P):
+def test_gram_irls_matches_two_pass(fam, link, P, monkeypatch):
     """k_gram_irls (eta / wi / zi inside the augmented Gram pass) against irls_wz + gram and the fp64 chain."""
+    monkeypatch.setenv("H2O_GLM_GRAM_IRLS", "1")
     from llama_github_io_amd.models.glm import Family
     from llama_github_io_amd.ops import gram as G
     dev = torch.device("cuda", 0)
@@ -101,8 +102,9 @@ def test_gram_irls_matches_two_pass(fam, link, P):
     torch.testing.assert_close(out[1], Zd.T @ (wd * zd), rtol=1e-4, atol=1e-4 * scale)
 
 
-def test_gram_irls_tiny_and_refusals():
+def test_gram_irls_tiny_and_refusals(monkeypatch):
     """N smaller than one 16-row batch, no offset; P + 1 > 64 and CPU fall back (None)."""
+    monkeypatch.setenv("H2O_GLM_GRAM_IRLS", "1")
     from llama_github_io_amd.ops import gram as G
     dev = torch.device("cuda", 0)
     Z = torch.randn(5, 7, device=dev)
