@@ -56,7 +56,7 @@ def gram_irls(Z: torch.Tensor, beta: torch.Tensor, off, y: torch.Tensor, w: torc
     inside the Gram pass) — or None where not covered (CPU, family / link outside the epilogue, P + 1 > 64,
     ``H2O_GLM_GRAM_IRLS=0``); the caller then runs ``irls_wz`` + ``gram``. Same formulas as ``irls_wz``."""
     if (not Z.is_cuda or family not in _IRLS_FAM or link not in _IRLS_LINK or beta.dim() != 1
-            or Z.shape[1] + 1 > 64 or os.environ.get("H2O_GLM_GRAM_IRLS", "0") == "0"
+            or Z.shape[1] + 1 > 64 or os.environ.get("H2O_GLM_GRAM_IRLS", "1") == "0"
             or os.environ.get("H2O_GLM_FUSED_IRLS", "1") == "0"):
         return None
     N, P = Z.shape
