@@ -391,10 +391,12 @@ __device__ __forceinline__ uint4 pack_row(const float* v, float*) {
 template <typename T>
 __global__ __launch_bounds__(256) void k_num_transform(const float* __restrict__ X, int64_t N, const int* __restrict__ rows,
                                                        int nf, const float* __restrict__ fill, const float* __restrict__ sub,
-                                                       const float* __restrict__ mul, T* __restrict__ Z, int ldz, int col0) {
+                                                       const float* __restrict__ mul, T* __restrict__ Z, int ldz, int col0,
+                                                       float extra, int has_extra) {
   __shared__ float tile[NT_FC][NT_ROWS + 1];
   const int t = threadIdx.x;
   const bool vin = (N % 4) == 0;
+  const bool lin = col0 == 0 && nf <= NT_FC && ldz == nf + has_extra;
   constexpr int VN = NT_VEC<T>::n, CPR = NT_FC / VN;          // 16-byte chunks per row and feature chunk
   for (int64_t r0 = (int64_t)blockIdx.x * NT_ROWS; r0 < N; r0 += (int64_t)gridDim.x * NT_ROWS) {
     for (int fc = 0; fc < nf; fc += NT_FC) {
@@ -423,6 +425,21 @@ __global__ __launch_bounds__(256) void k_num_transform(const float* __restrict__
         for (int j = 0; j < 4; ++j) tile[k][4 * c + j] = v[j];
       }
       __syncthreads();
+      if (lin) {
+        // whole rows (col0 == 0, ldz == nf + has_extra, one feature chunk): the block's output is ONE contiguous
+        // span of NT_ROWS * ldz elements, written by consecutive lanes (the extra constant column included) —
+        // MEASURED r6 (GLM 10M x 50, ldz 51): the 16-byte-row-chunk stores below cannot vectorise at an odd
+        // ldz and ran 1.5 ms plus a 0.67 ms strided torch fill of the intercept column
+        const int64_t nrow = min((int64_t)NT_ROWS, N - r0);
+        const int span = (int)nrow * ldz;
+        T* dst = Z + r0 * ldz;
+        for (int o = t; o < span; o += 256) {
+          const int rr = o / ldz, col = o - rr * ldz;
+          st(dst, o, col < nf ? tile[col][rr] : extra);
+        }
+        __syncthreads();
+        continue;
+      }
       // write: VN consecutive features of one row per 16-byte store
       const bool vout = (ldz % VN) == 0 && ((col0 + fc) % VN) == 0;
       for (int idx = t; idx < NT_ROWS * CPR; idx += 256) {
@@ -463,8 +480,12 @@ int h2o_num_stats(const float* X, long long N, const int* rows, int nf, const fl
   return (int)hipGetLastError();
 }
 
+// has_extra: also fill column nf of the whole-row layout (col0 == 0, ldz == nf + 1, nf <= NT_FC) with `extra`
+// (the GLM intercept column); refused for any other layout (the caller fills it itself then)
 int h2o_num_transform(const float* X, long long N, const int* rows, int nf, const float* fill, const float* sub,
-                      const float* mul, void* Z, int ldz, int col0, int bf16, hipStream_t s) {
+                      const float* mul, void* Z, int ldz, int col0, int bf16, float extra, int has_extra,
+                      hipStream_t s) {
+  if (has_extra && (col0 != 0 || nf > NT_FC || ldz != nf + 1)) return (int)hipErrorInvalidValue;
   if (N <= 0 || nf <= 0) return 0;
   // 32-row blocks strided over a bounded grid
   long long gx = (N + NT_ROWS - 1) / NT_ROWS;
@@ -472,10 +493,10 @@ int h2o_num_transform(const float* X, long long N, const int* rows, int nf, cons
   dim3 grid((unsigned)gx);
   if (bf16)
     hipLaunchKernelGGL(k_num_transform<__hip_bfloat16>, grid, dim3(256), 0, s, X, (int64_t)N, rows, nf, fill, sub, mul,
-                       (__hip_bfloat16*)Z, ldz, col0);
+                       (__hip_bfloat16*)Z, ldz, col0, extra, has_extra);
   else
     hipLaunchKernelGGL(k_num_transform<float>, grid, dim3(256), 0, s, X, (int64_t)N, rows, nf, fill, sub, mul, (float*)Z,
-                       ldz, col0);
+                       ldz, col0, extra, has_extra);
   return (int)hipGetLastError();
 }
 

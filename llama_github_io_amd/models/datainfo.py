@@ -27,7 +27,8 @@ def _hip_ok(X) -> bool:
     nat.register_hip_signatures({
         "h2o_num_stats": [nat.c_void_p, nat.c_ll, nat.c_void_p, nat.c_int, nat.c_void_p, nat.c_void_p, nat.c_void_p],
         "h2o_num_transform": [nat.c_void_p, nat.c_ll, nat.c_void_p, nat.c_int, nat.c_void_p, nat.c_void_p, nat.c_void_p,
-                              nat.c_void_p, nat.c_int, nat.c_int, nat.c_int, nat.c_void_p],
+                              nat.c_void_p, nat.c_int, nat.c_int, nat.c_int, nat.ctypes.c_float, nat.c_int,
+                              nat.c_void_p],
     })
     return True
 
@@ -175,7 +176,10 @@ class Expander:
                  and dtype in (torch.float32, torch.bfloat16))
         # every column written below (all-numeric HIP transform): no zero fill of the [N, P] design
         Z = (torch.empty if dense else torch.zeros)(N, ncol, dtype=dtype, device=dev)
-        if extra is not None:
+        # whole rows of <= 64 numeric columns: k_num_transform writes the constant extra column too (one contiguous
+        # store span per block instead of a strided fill)
+        kx = dense and extra is not None and self.P <= 64
+        if extra is not None and not kx:
             Z[:, self.P] = float(extra)
         start = 0 if self.use_all else 1
         for i, j in enumerate(self.cats):
@@ -206,7 +210,7 @@ class Expander:
             mul = (1.0 / self.num_sd.to(dev).float()) if self.standardize else torch.ones_like(mu)
             nat.call("h2o_num_transform", X.data_ptr(), N, rows.data_ptr(), k, fill.data_ptr(), sub.contiguous().data_ptr(),
                      mul.contiguous().data_ptr(), Z.data_ptr(), ncol, self.num_off, int(dtype == torch.bfloat16),
-                     nat.stream_ptr(dev))
+                     float(extra) if kx else 0.0, int(kx), nat.stream_ptr(dev))
             return Z
         for a in range(0, len(self.nums), CH):
             Xn = X[self.nums[a:a + CH]].to(dtype=torch.float64)

@@ -387,6 +387,28 @@ def test_expander_hip_matches_cpu(standardize, dtype, N, cat):
     assert torch.allclose(Zc, Zg, rtol=tol, atol=tol)
 
 
+@pytest.mark.parametrize("F", [7, 50, 63, 64, 65])
+@pytest.mark.parametrize("N", [10000, 10003, 129])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_expander_extra_column_matches_cpu(F, N, dtype):
+    # the whole-row layout with the constant extra (intercept) column: k_num_transform's contiguous-span store
+    # (F + 1 <= 65 columns) and the strided-fill fallback (F > 64) against the PyTorch path
+    from llama_github_io_amd.models.base import DataInfo
+    from llama_github_io_amd.models.datainfo import Expander
+    g = torch.Generator().manual_seed(F + N)
+    X = torch.randn(F, N, generator=g) * 2 - 1
+    X[0, ::5] = float("nan")
+    info = DataInfo([f"x{i}" for i in range(F)], np.zeros(F, np.int32), [None] * F, "y", None)
+    ec = Expander(info, standardize=True).fit(X, None)
+    eg = Expander(info, standardize=True).fit(X.to(dev), None)
+    Zc = ec.transform(X, dtype=torch.float32, extra=1.0)
+    Zg = eg.transform(X.to(dev), dtype=dtype, extra=1.0).float().cpu()
+    assert Zg.shape == (N, F + 1)
+    assert bool((Zg[:, F] == 1.0).all())
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    assert torch.allclose(Zc, Zg, rtol=tol, atol=tol)
+
+
 @pytest.mark.parametrize("init", ["Furthest", "PlusPlus", "Random"])
 def test_kmeans_offset_data_matches_cpu(init):
     """standardize=False on columns offset by 1e4: the training space is centred, so the MFMA
