@@ -27,7 +27,33 @@ def main():
     ap.add_argument("--gaps", default=None, help="kernel-name substring marking the start of the window (its LAST "
                     "occurrence; e.g. k_num_stats for a DL fit): list the idle gaps > --min-gap us up to the trace end")
     ap.add_argument("--min-gap", type=float, default=50.0)
+    ap.add_argument("--window", default=None, help="kernel-name substring marking the start of the window (its LAST "
+                    "occurrence): per-kernel table of that window, then every dispatch in order with its gap")
     a = ap.parse_args()
+    if a.window:
+        db = sqlite3.connect(a.db)
+        ks = db.execute("select name, start, end from kernels order by start").fetchall()
+        idx = [i for i, k in enumerate(ks) if a.window in k[0]]
+        if not idx:
+            print("marker not found")
+            return
+        w = ks[idx[-1]:]
+        t0, t1 = w[0][1], max(k[2] for k in w)
+        agg = {}
+        for nm, st, en in w:
+            c, tt = agg.get(nm, (0, 0))
+            agg[nm] = (c + 1, tt + en - st)
+        busy = sum(v[1] for v in agg.values())
+        short = lambda n: n if len(n) < 70 else n[:67] + "..."
+        print(f"window {(t1 - t0) / 1e3:.1f} us, {len(w)} dispatches, busy {busy / 1e3:.1f} us\n"
+              "| kernel | calls | total us | % |\n|---|---|---|---|")
+        for nm, (c, tt) in sorted(agg.items(), key=lambda kv: -kv[1][1])[: a.top]:
+            print(f"| `{short(nm)}` | {c} | {tt / 1e3:.1f} | {100 * tt / max(busy, 1):.1f} |")
+        print("\n| # | kernel | us | gap us |\n|---|---|---|---|")
+        for j, (nm, st, en) in enumerate(w):
+            gap = (st - w[j - 1][2]) / 1e3 if j else 0.0
+            print(f"| {j} | `{short(nm)}` | {(en - st) / 1e3:.1f} | {gap:.1f} |")
+        return
     if a.gaps:
         db = sqlite3.connect(a.db)
         ks = db.execute("select name, start, end from kernels order by start").fetchall()
