@@ -17,7 +17,10 @@ __global__ __launch_bounds__(256) void k_score_hist(const double* __restrict__ p
     const double wp = wi * yi, wn = wi * (1.0 - yi);
     if (wp != 0.0) atomicAdd(pos + b, wp);
     if (wn != 0.0) atomicAdd(neg + b, wn);
-    atomicMax(mx + b, (unsigned long long)__double_as_longlong(fmax(pi, 0.0)));
+    // the bin's max changes ~ln(rows per bin) times: a relaxed load first skips most of the atomics (a stale
+    // value only costs an unneeded atomicMax, which is monotone)
+    const unsigned long long bits = (unsigned long long)__double_as_longlong(fmax(pi, 0.0));
+    if (bits > __hip_atomic_load(mx + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(mx + b, bits);
   }
 }
 

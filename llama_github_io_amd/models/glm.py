@@ -852,7 +852,10 @@ class GLMTrainer:
                     self.job.check_cancelled()
                 if diff < beps:
                     break
-            mu = fam.linkinv(G.zbeta(Zi, beta, off))
+            eta_tr = G.zbeta(Zi, beta, off)
+            # kept for _outputs: the training predictions of the returned beta are this same Z.beta pass
+            self._last_eta = (beta, Zi, off, eta_tr)
+            mu = fam.linkinv(eta_tr)
             dev_tr = _gsum((w * fam.deviance(y, mu)).sum())
             entry = dict(lambda_=lam, dev_explained=1 - dev_tr / null_dev if null_dev > 0 else 0.0,
                          coefs=beta.cpu().tolist())
@@ -1151,7 +1154,13 @@ class GLMTrainer:
         if fam not in ("multinomial", "ordinal") and K == 1 and getattr(model, "hglm", None) is None:
             # training predictions from the training design (it already holds the intercept column): no second
             # expander transform of X
-            P = model._from_eta(G.zbeta(Zi, beta[0].to(Zi.device), off)[:, None])
+            le, self._last_eta = getattr(self, "_last_eta", None), None
+            if (le is not None and le[1] is Zi and le[2] is off and le[0].shape == beta[0].shape
+                    and torch.equal(le[0].to(beta.device, torch.float64), beta[0].double())):
+                eta = le[3]                    # the fit's last deviance pass already holds Z.beta + off
+            else:
+                eta = G.zbeta(Zi, beta[0].to(Zi.device), off)
+            P = model._from_eta(eta[:, None])
         else:
             P = model._predict_tensor(X, offset)
         cat = model.model_category
