@@ -16,8 +16,10 @@ The realm file is Jetty's PropertyUserStore format, ``user: credential[, role ..
 credential in plain text or Jetty's ``OBF:`` / ``MD5:`` / ``CRYPT:`` forms (``h2o-assemblies/main/tests/python/
 realm.properties`` is a plain one). ``-ldap_login -login_conf <JAAS file>`` authenticates against an LDAP server with
 Jetty LdapLoginModule's semantics (:mod:`.ldap`); ``-pam_login`` through the host's libpam as h2o-jaas-pam's
-PamLoginModule (:mod:`.pam`). Kerberos / SPNEGO need a KDC and JAAS Krb5 modules, which this image does not have:
-they are refused at startup with that reason.
+PamLoginModule (:mod:`.pam`). ``-kerberos_login`` checks Basic credentials with a Kerberos AS exchange (JAAS
+Krb5LoginModule) and ``-spnego_login`` accepts ``Authorization: Negotiate`` tokens with GSSAPI (Jetty's
+SpnegoAuthenticator; ``-spnego_properties`` names the ``targetName``) — both through the host's MIT Kerberos
+libraries (:mod:`.krb5`).
 """
 from __future__ import annotations
 
@@ -127,6 +129,7 @@ class LoginConfig:
     form_auth: bool = False
     session_timeout: int = 0          # minutes of inactivity (form_auth); 0 = no timeout
     secure_cookies: bool = False      # the server speaks HTTPS (-jks): session cookies carry the Secure flag
+    spnego_properties: str | None = None   # -spnego_properties: Java properties with the acceptor's targetName
 
     def validate(self) -> "LoginConfig":
         import os
@@ -144,18 +147,26 @@ class LoginConfig:
                              "with of a LoginService.")
         if self.session_timeout and not self.form_auth:
             raise ValueError("Session timeout can only be enabled for Form based authentication (use -form_auth)")
-        if self.kerberos_login or self.spnego_login:
-            raise ValueError("Kerberos / SPNEGO logins need a KDC and JAAS Krb5 modules, which this build does not "
-                             "include; use -hash_login, -ldap_login or -pam_login")
-        if self.ldap_login or self.pam_login:
-            self.service()                          # a malformed JAAS config fails at startup, not at first login
+        if self.spnego_properties is not None and not os.path.exists(self.spnego_properties):
+            raise ValueError(f"File does not exist: {self.spnego_properties}")
+        if self.ldap_login or self.pam_login or self.kerberos_login or self.spnego_login:
+            try:
+                self.service()                      # a malformed JAAS config fails at startup, not at first login
+            except RuntimeError as e:               # the host lacks the login's native library
+                raise ValueError(str(e)) from None
         return self
 
     @property
     def enabled(self) -> bool:
-        return self.hash_login or self.ldap_login or self.pam_login
+        return self.hash_login or self.ldap_login or self.pam_login or self.kerberos_login or self.spnego_login
 
     def service(self):
+        if self.spnego_login:
+            from .krb5 import SpnegoService
+            return SpnegoService(self.login_conf, self.spnego_properties)
+        if self.kerberos_login:
+            from .krb5 import Krb5LoginService
+            return _CachedLogin(Krb5LoginService(self.login_conf))
         if self.ldap_login:
             from .ldap import LdapLoginService
             return _CachedLogin(LdapLoginService(self.login_conf))
@@ -316,6 +327,21 @@ def install(app, cfg: LoginConfig) -> None:
         s = sessions.get(request.cookies.get(cookie))
         if s is not None and s.get("user"):
             return await call_next(request)
+        if cfg.spnego_login:
+            # SpnegoAuthenticator: a Negotiate token is accepted with GSSAPI, else 401 + "WWW-Authenticate: Negotiate"
+            from .krb5 import negotiate_token
+            tok = negotiate_token(headers)
+            reply = None
+            if tok:
+                user, reply = await run_in_threadpool(svc.accept, tok)
+                if user:
+                    r = await call_next(request)
+                    if reply:
+                        r.headers["WWW-Authenticate"] = "Negotiate " + base64.b64encode(reply).decode("ascii")
+                    return r
+            return JSONResponse(status_code=401, content={"http_status": 401, "msg": "Access denied. Please login."},
+                                headers={"WWW-Authenticate": "Negotiate" + (
+                                    " " + base64.b64encode(reply).decode("ascii") if reply else "")})
         cred = _basic_user(headers)
         if cred is not None and await run_in_threadpool(svc.login, *cred):
             return await call_next(request)

@@ -961,6 +961,7 @@ def main(argv=None):
     for flag in ("hash_login", "ldap_login", "kerberos_login", "spnego_login", "pam_login", "form_auth"):
         ap.add_argument(f"--{flag}", f"-{flag}", action="store_true")
     ap.add_argument("--login_conf", "-login_conf", default=None)
+    ap.add_argument("--spnego_properties", "-spnego_properties", default=None)
     ap.add_argument("--session_timeout", "-session_timeout", type=int, default=0)
     # HTTPS from a Java KeyStore (H2O.java -jks / -jks_pass / -jks_alias / -hostname_as_jks_alias; api/tls.py)
     ap.add_argument("--jks", "-jks", default=None)
@@ -970,7 +971,8 @@ def main(argv=None):
     a = ap.parse_args(argv)
     login = LoginConfig(hash_login=a.hash_login, ldap_login=a.ldap_login, kerberos_login=a.kerberos_login,
                         spnego_login=a.spnego_login, pam_login=a.pam_login, login_conf=a.login_conf,
-                        form_auth=a.form_auth, session_timeout=a.session_timeout)
+                        form_auth=a.form_auth, session_timeout=a.session_timeout,
+                        spnego_properties=a.spnego_properties)
     try:
         login.validate()
     except ValueError as e:
