@@ -853,10 +853,10 @@ class GLMTrainer:
                 if diff < beps:
                     break
             eta_tr = G.zbeta(Zi, beta, off)
-            # kept for _outputs: the training predictions of the returned beta are this same Z.beta pass
-            self._last_eta = (beta, Zi, off, eta_tr)
             mu = fam.linkinv(eta_tr)
             dev_tr = _gsum((w * fam.deviance(y, mu)).sum())
+            # kept for _outputs: the training predictions / residual deviance of the returned beta are this pass's
+            self._last_eta = (beta, Zi, off, eta_tr, w, y, (fam.name, fam.link), dev_tr)
             entry = dict(lambda_=lam, dev_explained=1 - dev_tr / null_dev if null_dev > 0 else 0.0,
                          coefs=beta.cpu().tolist())
             entry["lambda"] = lam
@@ -1140,6 +1140,7 @@ class GLMTrainer:
         if fam == "ordinal":
             out["ordinal_thresholds"] = self._ordinal_th
         K = beta.shape[0]
+        same_dev = None
         coefs, coefs_std = {}, {}
         for k in range(K):
             braw, ic = ex.destandardize(beta[k, :-1], float(beta[k, -1]))
@@ -1158,6 +1159,7 @@ class GLMTrainer:
             if (le is not None and le[1] is Zi and le[2] is off and le[0].shape == beta[0].shape
                     and torch.equal(le[0].to(beta.device, torch.float64), beta[0].double())):
                 eta = le[3]                    # the fit's last deviance pass already holds Z.beta + off
+                same_dev = le                  # ... and the residual deviance of that beta (checked below)
             else:
                 eta = G.zbeta(Zi, beta[0].to(Zi.device), off)
             P = model._from_eta(eta[:, None])
@@ -1169,7 +1171,11 @@ class GLMTrainer:
         if fam not in ("multinomial", "ordinal"):
             family = Family(fam, link, float(p["tweedie_variance_power"]), float(p["tweedie_link_power"]), float(p["theta"]))
             mu = (P[:, 1] if P.dim() == 2 else P).double()
-            res_dev = _gsum((w * family.deviance(y, mu)).sum())
+            if (same_dev is not None and same_dev[4] is w and same_dev[5] is y and fam != "tweedie"
+                    and same_dev[6] == (family.name, family.link)):
+                res_dev = same_dev[7]
+            else:
+                res_dev = _gsum((w * family.deviance(y, mu)).sum())
             ymu = _gsum((w * y).sum()) / _gsum(w.sum())
             out["training_ymu"] = float(ymu)
             null_mu = torch.full_like(y, ymu)
