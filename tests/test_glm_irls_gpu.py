@@ -118,3 +118,39 @@ def test_gram_irls_tiny_and_refusals(monkeypatch):
     assert G.gram_irls(torch.randn(10, 64, device=dev), torch.zeros(64, device=dev, dtype=torch.float64), None,
                        y.new_zeros(10), y.new_ones(10), "gaussian", "identity") is None
     assert G.gram_irls(Z.cpu(), beta.cpu(), None, y.cpu(), w.cpu(), "gaussian", "identity") is None
+
+
+def test_glm_fit_takes_fused_gram_irls_path(monkeypatch):
+    """A GPU IRLSM fit with P + 1 <= 64 runs k_gram_irls: the two-pass kernels are never called, and the fit equals
+    the two-pass one (H2O_GLM_GRAM_IRLS=0)."""
+    import numpy as np
+    from llama_github_io_amd.models.base import DataInfo
+    from llama_github_io_amd.models.glm import GLMTrainer
+    from llama_github_io_amd.ops import gram as G
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(9)
+    F, N = 20, 300_000
+    X = torch.randn(F, N, device=dev, generator=g)
+    y = torch.poisson(torch.exp(0.2 * X[0] - 0.1 * X[1] + 0.5), generator=g)
+    info = DataInfo([f"x{i}" for i in range(F)], np.zeros(F, np.int32), [None] * F, "y", None)
+    prm = dict(family="poisson", lambda_=0.0, standardize=True)
+    calls = {"fused": 0}
+    real = G.gram_irls
+
+    def spy(*a, **k):
+        out = real(*a, **k)
+        calls["fused"] += out is not None
+        return out
+
+    def boom(*a, **k):
+        raise AssertionError("two-pass IRLS kernel called on the fused path")
+
+    monkeypatch.setattr(G, "gram_irls", spy)
+    monkeypatch.setattr(G, "irls_wz", boom)
+    mf = GLMTrainer(dict(prm)).fit(X, y, None, None, info)
+    assert calls["fused"] >= 2
+    monkeypatch.undo()
+    monkeypatch.setenv("H2O_GLM_GRAM_IRLS", "0")
+    mt = GLMTrainer(dict(prm)).fit(X, y, None, None, info)
+    assert np.allclose(mf.beta.cpu().numpy(), mt.beta.cpu().numpy(), atol=1e-6)
+    assert abs(mf.output["residual_deviance"] - mt.output["residual_deviance"]) <= 1e-6 * mt.output["residual_deviance"]
